@@ -1,0 +1,214 @@
+"""Headline benchmark: Mrows/s of filter -> group_by -> agg(sum) over a
+1e9-row OHLCV-shaped frame (symbol: i64, open/high/low/close: f64), inputs
+resident in HBM, on N GPUs (one process per GPU).
+
+    python bench.py [--gpus N --steps K --warmup W --rows R --groups G]
+
+One step = one full query `filter(close > 250).group_by(symbol).agg(
+open.sum(), high.sum(), low.sum(), close.sum())` through the C-ABI.  With
+N > 1 each rank holds its own R-row shard (weak scaling), aggregates it
+locally into exact partial states, and the partial states are hash-
+partitioned by key and exchanged with one RCCL all-to-all, then merged
+(DESIGN.md §Multi-GPU).  Rank 0 prints one JSON line.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Mrows/sec filter+groupby-agg on 1e9-row f64/i64; achieved HBM GB/s vs peak"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
+THRESHOLD = 250.0
+BYTES_PER_ROW = 8 + 4 * 8      # key + open/high/low/close read once (close is also the predicate)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--rows", type=float, default=1e9, help="rows per GPU")
+    ap.add_argument("--groups", type=int, default=100, help="distinct symbols (h2oai id4: K=100)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline time budget")
+    ap.add_argument("--cpu-rows", type=float, default=3e7, help="cpu_baseline sample rows")
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def make_data(torch, n: int, groups: int, seed: int):
+    """OHLCV-shaped synthetic columns generated on the device, chunked."""
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    base = torch.rand(groups, device=dev, generator=g, dtype=torch.float64) * 480.0 + 10.0
+    sym = torch.empty(n, dtype=torch.int64, device=dev)
+    cols = {k: torch.empty(n, dtype=torch.float64, device=dev) for k in ("open", "high", "low", "close")}
+    chunk = 1 << 26
+    for s in range(0, n, chunk):
+        e = min(n, s + chunk)
+        m = e - s
+        k = torch.randint(0, groups, (m,), device=dev, generator=g, dtype=torch.int64)
+        sym[s:e] = k * 7919 + 1_000_000  # sparse symbol ids
+        p = base[k]
+        o = p * torch.exp(0.02 * torch.randn(m, device=dev, generator=g, dtype=torch.float64))
+        c = p * torch.exp(0.02 * torch.randn(m, device=dev, generator=g, dtype=torch.float64))
+        spread = torch.rand(m, device=dev, generator=g, dtype=torch.float64) * 0.01
+        cols["open"][s:e] = o
+        cols["close"][s:e] = c
+        cols["high"][s:e] = torch.maximum(o, c) * (1.0 + spread)
+        cols["low"][s:e] = torch.minimum(o, c) * (1.0 - spread)
+    torch.cuda.synchronize()
+    return sym, cols
+
+
+def cpu_baseline(rows: int, groups: int, seconds: float) -> dict:
+    """The oracle's OpenMP restatement of the reference's streaming hash
+    aggregation, timed on the host cores (rank 0, N=1 only)."""
+    from oracle import oracle as O
+
+    threads = min(16, len(os.sched_getaffinity(0)))
+    rng = np.random.default_rng(1)
+    base = rng.uniform(10, 490, groups)
+    k = rng.integers(0, groups, rows)
+    key = (k * 7919 + 1_000_000).astype(np.int64)
+    p = base[k]
+    o = p * np.exp(0.02 * rng.standard_normal(rows))
+    c = p * np.exp(0.02 * rng.standard_normal(rows))
+    sp = rng.random(rows) * 0.01
+    h = np.maximum(o, c) * (1 + sp)
+    lo = np.minimum(o, c) * (1 - sp)
+    O.baseline_filter_groupby_sum(key[:1000], c[:1000], THRESHOLD, [o[:1000], h[:1000], lo[:1000], c[:1000]],
+                                  threads)
+    times = []
+    t_end = time.perf_counter() + seconds
+    while time.perf_counter() < t_end or not times:
+        t0 = time.perf_counter()
+        O.baseline_filter_groupby_sum(key, c, THRESHOLD, [o, h, lo, c], threads)
+        times.append(time.perf_counter() - t0)
+    t = float(np.median(times))
+    return {"value": rows / t / 1e6, "unit": "Mrows/s", "cores": threads, "kind": "port",
+            "sample": f"{rows:.0e} rows x {len(times)} runs of the same query (median), OpenMP "
+                      f"{threads} threads, oracle/polars_oracle.c:or_baseline_filter_groupby_sum"}
+
+
+def load_traffic(n_rows: int):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, if any
+    (profiles/traffic.json written by tools/pmc_traffic.py)."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        t = json.load(open(path))
+        if int(t.get("rows", -1)) == n_rows:
+            return float(t["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+    return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    import polaroid_amd as pl
+    from polaroid_amd import distributed as pdist
+
+    pl._native.check(pl._native.lib().plgpu_set_device(torch.cuda.current_device()))
+    n = int(args.rows)
+    sym, cols = make_data(torch, n, args.groups, seed=1234 + rank)
+    df = pl.DataFrame([pl.Series.from_torch("symbol", sym)] +
+                      [pl.Series.from_torch(k, v) for k, v in cols.items()])
+    aggs = [pl.col(k).sum() for k in ("open", "high", "low", "close")]
+    query = df.lazy().filter(pl.col("close") > THRESHOLD).group_by("symbol").agg(*aggs)
+
+    def step(info):
+        if world == 1:
+            return query.collect(info=info)
+        return pdist.group_by_agg(df, "symbol", aggs, pl.col("close") > THRESHOLD, info=info)
+
+    for _ in range(args.warmup):
+        step({})
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    kernel_ms = []
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        info = {}
+        out = step(info)
+        kernel_ms.append(info.get("main_kernel_ms", float("nan")))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    ms_per_step = dt / args.steps * 1e3
+    total_rows = n * world
+    value = total_rows * args.steps / dt / 1e6
+    kms = float(np.mean(kernel_ms))
+    achieved = BYTES_PER_ROW * n / (kms * 1e-3) / 1e9
+    traffic = load_traffic(n)
+    result = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "Mrows/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic OHLCV-shaped columns generated on device (torch RNG), inputs resident in HBM",
+        "config": {
+            "workload": "filter(close > 250).group_by(symbol).agg(open/high/low/close.sum()) "
+                        f"{n:.0e} rows per GPU, {args.groups} groups (metric size; configs[1] = 1e8 rows)",
+            "rows_per_gpu": n, "groups": args.groups, "global_batch": total_rows,
+            "columns": "symbol:i64 open,high,low,close:f64",
+            "selectivity": None if out is None else round(float(info.get("rows_selected", 0)) / n, 4),
+            "parallelism": f"hash-partitioned x{world}" if world > 1 else "single GPU",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "kernel": "gb_kernel<1,8> (fused filter + LDS hash aggregation)",
+            "kernel_ms": round(kms, 4),
+            "bytes_per_row": BYTES_PER_ROW,
+        },
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        result["cpu_baseline"] = cpu_baseline(int(args.cpu_rows), args.groups, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

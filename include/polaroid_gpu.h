@@ -1,0 +1,212 @@
+/*
+ * polaroid_gpu.h — C-ABI of the MI355X columnar executor backend.
+ *
+ * This is the drop-in boundary a Polars host (Rust, via `extern "C"` +
+ * bindgen, or Python via ctypes) binds to run the filter / arithmetic /
+ * comparison / hash-group-by-aggregation hot path on gfx950.  Only plain C
+ * types cross it: device pointers, lengths, Arrow bit-packed validity
+ * bitmaps (LSB-first, Arrow offset semantics), status codes.  No torch or
+ * HIP types appear in any signature; `stream` is an opaque hipStream_t
+ * (NULL = the library's default stream).
+ *
+ * Each entry point names the reference interface it replaces
+ * (paths relative to /root/reference/crates).
+ *
+ * Column ownership follows the Arrow C data interface: a column produced by
+ * the library carries a non-NULL `release` callback that the consumer must
+ * call exactly once; borrowed input columns have `release == NULL`.
+ */
+#ifndef POLAROID_GPU_H
+#define POLAROID_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PLGPU_ABI_VERSION 1
+
+/* ---------------------------------------------------------------- status */
+/* Error classes mirror polars_error::PolarsError variants
+ * (polars-error/src/lib.rs) so the host can map them 1:1. */
+enum plgpu_status {
+    PLGPU_OK = 0,
+    PLGPU_ERR_INVALID = -1,        /* InvalidOperation                      */
+    PLGPU_ERR_SCHEMA = -2,         /* SchemaMismatch / ComputeError (dtype)  */
+    PLGPU_ERR_SHAPE = -3,          /* ShapeMismatch (column lengths differ)  */
+    PLGPU_ERR_OOM = -4,            /* device allocation failed               */
+    PLGPU_ERR_HIP = -5,            /* HIP runtime error                      */
+    PLGPU_ERR_NO_DEVICE = -6,      /* no gfx950 device visible               */
+    PLGPU_ERR_CAPACITY = -7        /* internal table overflow (retry failed) */
+};
+
+/* ---------------------------------------------------------------- dtypes */
+/* Physical types of the path; Arrow format string in the comment. */
+enum plgpu_dtype {
+    PLGPU_BOOL = 1, /* "b"  bit-packed values, LSB first               */
+    PLGPU_I32 = 2,  /* "i"                                             */
+    PLGPU_I64 = 3,  /* "l"                                             */
+    PLGPU_F64 = 4,  /* "g"                                             */
+    PLGPU_U32 = 5   /* "I"  polars IdxSize (count / len outputs)       */
+};
+
+/* One Arrow array in device memory (Arrow C Device Data Interface,
+ * ARROW_DEVICE_ROCM = 10, flattened to the two buffers the path uses). */
+typedef struct plgpu_column {
+    int32_t dtype;            /* enum plgpu_dtype                                  */
+    int32_t device_id;        /* HIP device ordinal                                */
+    int64_t length;           /* logical length                                    */
+    int64_t offset;           /* Arrow offset (elements; bits for PLGPU_BOOL)      */
+    int64_t null_count;       /* -1 = unknown                                      */
+    const void* values;       /* device ptr, Arrow buffers[1]                      */
+    const uint8_t* validity;  /* device ptr, Arrow buffers[0]; NULL = all valid    */
+    void (*release)(struct plgpu_column*); /* NULL for borrowed columns             */
+    void* private_data;
+} plgpu_column;
+
+/* ------------------------------------------------------- expression ISA */
+/* A physical expression (polars-expr/src/expressions/{binary,column,
+ * literal}.rs) is lowered to a postfix program evaluated per row on the
+ * GPU.  Semantics per op follow the reference kernels cited below. */
+enum plgpu_opcode {
+    PLGPU_OP_COL = 1,       /* push column[arg]                                 */
+    PLGPU_OP_LIT_F64 = 2,   /* push f64 literal imm.f64                         */
+    PLGPU_OP_LIT_I64 = 3,   /* push i64 literal imm.i64                         */
+    PLGPU_OP_LIT_BOOL = 4,  /* push bool literal imm.i64 != 0                   */
+    PLGPU_OP_LIT_NULL = 5,  /* push typed null (arg = plgpu_dtype)              */
+    /* arithmetic: polars-compute/src/arithmetic/{signed,float}.rs;
+     * int (+,-,*) wrap; int op float -> float; `/` is true division (f64). */
+    PLGPU_OP_ADD = 10,
+    PLGPU_OP_SUB = 11,
+    PLGPU_OP_MUL = 12,
+    PLGPU_OP_TRUEDIV = 13,
+    PLGPU_OP_NEG = 14,
+    PLGPU_OP_ABS = 15,
+    PLGPU_OP_CAST_F64 = 16,
+    /* comparisons: TotalOrd semantics, polars-utils/src/total_ord.rs:317-368
+     * (NaN == NaN, NaN greatest); null in -> null out. */
+    PLGPU_OP_EQ = 20,
+    PLGPU_OP_NE = 21,
+    PLGPU_OP_LT = 22,
+    PLGPU_OP_LE = 23,
+    PLGPU_OP_GT = 24,
+    PLGPU_OP_GE = 25,
+    PLGPU_OP_EQ_MISSING = 26, /* null == null, never null out */
+    PLGPU_OP_NE_MISSING = 27,
+    /* boolean: Kleene logic, polars-compute/src/bitwise + ops::and/or */
+    PLGPU_OP_AND = 30,
+    PLGPU_OP_OR = 31,
+    PLGPU_OP_NOT = 32,
+    PLGPU_OP_IS_NULL = 33,
+    PLGPU_OP_IS_NOT_NULL = 34,
+    PLGPU_OP_IS_NAN = 35,
+    PLGPU_OP_IS_FINITE = 36
+};
+
+typedef struct plgpu_instr {
+    int32_t op;   /* enum plgpu_opcode */
+    int32_t arg;  /* column index / dtype */
+    union {
+        double f64;
+        int64_t i64;
+    } imm;
+} plgpu_instr;
+
+#define PLGPU_MAX_STACK 8
+#define PLGPU_MAX_PROGRAM 64
+#define PLGPU_MAX_COLS 8
+
+/* -------------------------------------------------------- aggregations */
+/* polars-core/src/frame/group_by/aggregations/mod.rs (agg_sum :581,
+ * agg_mean :659, agg_min/agg_max) and the streaming reductions the lazy
+ * engine actually runs for a partitionable group-by
+ * (polars-mem-engine/src/planner/lp.rs:648 -> polars-expr/src/reduce/
+ * {sum,mean,min_max,count,len}.rs). */
+enum plgpu_agg_kind {
+    PLGPU_AGG_SUM = 1,   /* f64: correctly-rounded exact sum; i64: wrapping  */
+    PLGPU_AGG_MEAN = 2,  /* f64 out, null if no non-null values              */
+    PLGPU_AGG_MIN = 3,   /* NaN ignored unless all NaN (min_ignore_nan)      */
+    PLGPU_AGG_MAX = 4,
+    PLGPU_AGG_COUNT = 5, /* non-null count, u32 (IdxSize)                    */
+    PLGPU_AGG_LEN = 6    /* group length incl. nulls, u32                    */
+};
+
+typedef struct plgpu_agg {
+    int32_t kind; /* enum plgpu_agg_kind */
+    int32_t col;  /* input column index */
+} plgpu_agg;
+
+/* Diagnostics of one group-by call (for tests / bench / rocprof cross-check). */
+typedef struct plgpu_groupby_info {
+    int64_t rows_in;
+    int64_t rows_selected;       /* rows passing the fused predicate            */
+    int64_t groups;
+    int64_t global_path_rows;    /* rows that missed the LDS table             */
+    int32_t reruns;              /* fixed-point window / table-size retries    */
+    int32_t lds_slots;           /* per-workgroup LDS hash-table capacity      */
+    int32_t grid;                /* workgroups in the main launch              */
+    int32_t sum_inexact;         /* bit i: f64 sum acc i rounded below window  */
+    int64_t table_capacity;      /* global hash-table slots                    */
+    double main_kernel_ms;       /* device time of the aggregation kernel      */
+} plgpu_groupby_info;
+
+/* ---------------------------------------------------------------- basics */
+int plgpu_abi_version(void);
+const char* plgpu_last_error(void);           /* thread-local message        */
+int plgpu_device_count(int* out);
+int plgpu_set_device(int device);
+int plgpu_synchronize(void* stream);
+
+/* Stream-ordered device allocator (native caching pool). */
+int plgpu_alloc(void** out_ptr, size_t bytes, void* stream);
+int plgpu_free(void* ptr, void* stream);
+int plgpu_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream);
+int plgpu_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream);
+int plgpu_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream);
+
+/* Release a library-produced column (no-op for borrowed ones). */
+void plgpu_column_release(plgpu_column* col);
+
+/* ------------------------------------------------------------ hot path */
+
+/* Evaluate a physical expression over `ncols` input columns of equal length
+ * into a new column (BOOL / I64 / F64).  Replaces PhysicalExpr::evaluate for
+ * column/literal/binary expressions (polars-expr/src/expressions/binary.rs)
+ * and the broadcast comparison kernels TotalOrdKernel::tot_*_kernel_broadcast
+ * (polars-compute/src/comparisons/{scalar,simd}.rs). */
+int plgpu_eval(const plgpu_column* cols, int32_t ncols, const plgpu_instr* program,
+               int32_t n_instr, plgpu_column* out, void* stream);
+
+/* Filter `ncols` columns by a BOOL mask (null = false) into new columns.
+ * Replaces polars-compute/src/filter/mod.rs:18 `filter` (and
+ * DataFrame::filter, polars-core/src/frame/mod.rs:2012, which FilterExec
+ * calls in polars-mem-engine/src/executors/filter.rs:51). */
+int plgpu_filter(const plgpu_column* cols, int32_t ncols, const plgpu_column* mask,
+                 plgpu_column* out_cols, int64_t* out_len, void* stream);
+
+/* Fused FilterExec + predicate: evaluate `program` (must yield BOOL) and
+ * compact the columns in one pipeline (no materialised mask column). */
+int plgpu_filter_expr(const plgpu_column* cols, int32_t ncols, const plgpu_instr* program,
+                      int32_t n_instr, plgpu_column* out_cols, int64_t* out_len,
+                      void* stream);
+
+/* Hash group-by on one integer key column with aggregations, optionally
+ * fused with a filter predicate (`program` may be NULL / n_instr 0).
+ * Replaces GroupByExec / GroupByStreamingExec
+ * (polars-mem-engine/src/executors/group_by.rs:117,
+ * group_by_streaming.rs) for keys = [col(k)], aggs over plain columns.
+ * Output: `out_key` (I64, null group allowed) and `out_aggs[naggs]`.
+ * maintain_order != 0 orders groups by first occurrence (the reference's
+ * `maintain_order=True`); otherwise group order is unspecified, as in the
+ * reference. */
+int plgpu_group_by_agg(const plgpu_column* key, const plgpu_column* cols, int32_t ncols,
+                       const plgpu_instr* program, int32_t n_instr, const plgpu_agg* aggs,
+                       int32_t naggs, int32_t maintain_order, plgpu_column* out_key,
+                       plgpu_column* out_aggs, plgpu_groupby_info* info, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* POLAROID_GPU_H */

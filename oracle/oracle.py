@@ -1,0 +1,201 @@
+"""TEST INFRASTRUCTURE ONLY — numpy/ctypes front end of oracle/polars_oracle.c.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use
+this module, as the checker.  See polars_oracle.c for the reference
+file:line each function restates.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "_build", "liboracle.so")
+
+BOOL, I32, I64, F64, U32 = 1, 2, 3, 4, 5
+SUM_KAHAN, SUM_NAIVE, SUM_EXACT = 0, 1, 2
+AGG = dict(sum=1, mean=2, min=3, max=4, count=5, len=6)
+
+
+class _Col(C.Structure):  # layout of plgpu_column (include/polaroid_gpu.h)
+    _fields_ = [
+        ("dtype", C.c_int32), ("device_id", C.c_int32), ("length", C.c_int64), ("offset", C.c_int64),
+        ("null_count", C.c_int64), ("values", C.c_void_p), ("validity", C.c_void_p),
+        ("release", C.c_void_p), ("private_data", C.c_void_p),
+    ]
+
+
+class _Imm(C.Union):
+    _fields_ = [("f64", C.c_double), ("i64", C.c_int64)]
+
+
+class _Instr(C.Structure):
+    _fields_ = [("op", C.c_int32), ("arg", C.c_int32), ("imm", _Imm)]
+
+
+class _Agg(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("col", C.c_int32)]
+
+
+_lib = None
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = C.CDLL(LIB)
+        L.or_eval.restype = C.c_int
+        L.or_filter.restype = C.c_int64
+        L.or_group_by_agg.restype = C.c_int64
+        L.or_fsum.restype = C.c_double
+        L.or_fsum.argtypes = [C.c_void_p, C.c_int64]
+        L.or_baseline_filter_groupby_sum.restype = C.c_int64
+        L.or_baseline_filter_groupby_sum.argtypes = [
+            C.c_void_p, C.c_void_p, C.c_double, C.c_void_p, C.c_int32, C.c_int64, C.c_int32,
+            C.POINTER(C.c_double)]
+        _lib = L
+    return _lib
+
+
+def _np_dtype(code: int):
+    return {I32: np.int32, I64: np.int64, F64: np.float64, U32: np.uint32}[code]
+
+
+def _code_of(a: np.ndarray) -> int:
+    if a.dtype == np.bool_:
+        return BOOL
+    return {np.dtype(np.int32): I32, np.dtype(np.int64): I64, np.dtype(np.float64): F64,
+            np.dtype(np.uint32): U32}[a.dtype]
+
+
+class HostCol:
+    """(values, validity) numpy pair exposed as a plgpu_column over host memory."""
+
+    def __init__(self, values: np.ndarray, valid: np.ndarray | None = None):
+        self.code = _code_of(values)
+        n = values.shape[0]
+        if self.code == BOOL:
+            self.buf = np.packbits(values.astype(np.uint8), bitorder="little")
+            if self.buf.size == 0:
+                self.buf = np.zeros(1, np.uint8)
+        else:
+            self.buf = np.ascontiguousarray(values)
+        self.vbuf = None if valid is None else np.packbits(valid.astype(np.uint8), bitorder="little")
+        self.c = _Col()
+        self.c.dtype = self.code
+        self.c.length = n
+        self.c.offset = 0
+        self.c.values = self.buf.ctypes.data if self.buf.size else None
+        self.c.validity = self.vbuf.ctypes.data if self.vbuf is not None and self.vbuf.size else None
+        if valid is not None and self.c.validity is None:
+            self.vbuf = np.zeros(1, np.uint8)
+            self.c.validity = self.vbuf.ctypes.data
+
+
+def _cols(cols: list[HostCol]):
+    arr = (_Col * max(1, len(cols)))()
+    for i, c in enumerate(cols):
+        arr[i] = c.c
+    return arr
+
+
+def _prog(program):
+    if not program:
+        return None, 0
+    arr = (_Instr * len(program))()
+    for i, (op, arg, imm) in enumerate(program):
+        arr[i].op, arr[i].arg = op, arg
+        if op == 2:
+            arr[i].imm.f64 = float(imm)
+        else:
+            arr[i].imm.i64 = int(imm)
+    return arr, len(program)
+
+
+def eval_program(cols: list[HostCol], program, nrows: int):
+    """Returns (dtype_code, values ndarray, validity bool ndarray)."""
+    words = (nrows + 63) // 64 + 1
+    vals = np.zeros(max(nrows, 1) * 8 + 8, dtype=np.uint8)
+    valid = np.zeros(words * 8, dtype=np.uint8)
+    p, n = _prog(program)
+    dt = lib().or_eval(_cols(cols), len(cols), p, n, C.c_int64(nrows), vals.ctypes.data_as(C.c_void_p),
+                       valid.ctypes.data_as(C.c_void_p))
+    if dt < 0:
+        raise ValueError("oracle: ill-typed program")
+    validity = np.unpackbits(valid, bitorder="little")[:nrows].astype(bool)
+    if dt == BOOL:
+        v = np.unpackbits(vals, bitorder="little")[:nrows].astype(bool)
+    elif dt == I64:
+        v = vals[: nrows * 8].view(np.int64).copy()
+    else:
+        v = vals[: nrows * 8].view(np.float64).copy()
+    return dt, v, validity
+
+
+def filter_column(cols: list[HostCol], program, nrows: int, which: int):
+    c = cols[which]
+    eb = 4 if c.code in (I32, U32) else 8
+    out = np.zeros(max(nrows, 1) * eb, dtype=np.uint8)
+    outv = np.zeros((nrows + 7) // 8 + 8, dtype=np.uint8)
+    p, n = _prog(program)
+    m = lib().or_filter(_cols(cols), len(cols), p, n, C.c_int64(nrows), which,
+                        out.ctypes.data_as(C.c_void_p), outv.ctypes.data_as(C.c_void_p))
+    vals = out[: m * eb].view(_np_dtype(c.code)).copy()
+    valid = np.unpackbits(outv, bitorder="little")[:m].astype(bool)
+    return vals, valid
+
+
+def group_by_agg(key: HostCol, cols: list[HostCol], program, aggs: list[tuple[str, int]], nrows: int,
+                 sum_mode: int = SUM_EXACT):
+    """Groups in first-occurrence order.  Returns (keys, key_valid, [(values, valid)])."""
+    maxg = max(nrows, 1)
+    keys = np.zeros(maxg, np.int64)
+    kvalid = np.zeros(maxg, np.uint8)
+    outs, outv = [], []
+    for kind, ci in aggs:
+        code = cols[ci].code
+        if kind in ("count", "len"):
+            dt = np.uint32
+        elif kind == "mean" or code == F64:
+            dt = np.float64
+        else:
+            dt = np.int64
+        outs.append(np.zeros(maxg, dt))
+        outv.append(np.zeros(maxg, np.uint8))
+    agg_arr = (_Agg * max(1, len(aggs)))()
+    for i, (kind, ci) in enumerate(aggs):
+        agg_arr[i].kind, agg_arr[i].col = AGG[kind], ci
+    vp = (C.c_void_p * max(1, len(aggs)))(*[o.ctypes.data for o in outs])
+    vv = (C.c_void_p * max(1, len(aggs)))(*[o.ctypes.data for o in outv])
+    p, n = _prog(program)
+    g = lib().or_group_by_agg(C.byref(key.c), _cols(cols), len(cols), p, n, agg_arr, len(aggs),
+                              C.c_int64(nrows), sum_mode, C.c_int64(maxg), keys.ctypes.data_as(C.c_void_p),
+                              kvalid.ctypes.data_as(C.c_void_p), vp, vv)
+    if g < 0:
+        raise ValueError("oracle: group_by failed")
+    return keys[:g].copy(), kvalid[:g].astype(bool), [(o[:g].copy(), v[:g].astype(bool))
+                                                       for o, v in zip(outs, outv)]
+
+
+def fsum(x: np.ndarray) -> float:
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    return lib().or_fsum(x.ctypes.data, x.shape[0])
+
+
+def baseline_filter_groupby_sum(key: np.ndarray, pred: np.ndarray, k: float, sums: list[np.ndarray],
+                                threads: int) -> tuple[int, float]:
+    ptrs = (C.c_void_p * len(sums))(*[s.ctypes.data for s in sums])
+    chk = C.c_double(0.0)
+    g = lib().or_baseline_filter_groupby_sum(key.ctypes.data, pred.ctypes.data, k, ptrs, len(sums),
+                                             key.shape[0], threads, C.byref(chk))
+    return int(g), chk.value

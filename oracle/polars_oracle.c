@@ -1,0 +1,692 @@
+/*
+ * polars_oracle.c — TEST INFRASTRUCTURE ONLY.
+ *
+ * A plain-C, single-threaded (plus one OpenMP baseline entry) restatement of
+ * the reference's CPU algorithms for the filter -> group_by -> agg path.  It
+ * is the checker the parity tests compare the HIP path against, and the
+ * `cpu_baseline` leg of bench.py.  Nothing in the product path (polaroid_amd/)
+ * links, imports or calls it.
+ *
+ * Reference (Rust, /root/reference/crates — unbuildable here: no rustc) is
+ * followed function by function; each function cites file:line.
+ * Pinned by: the JSON fixtures in tests/golden (truth tables and expected outputs from the
+ * reference's own tests, see tests/golden/make_golden.py) and by CPython's
+ * math.fsum for the exact-sum leg (tests/test_oracle.py).
+ *
+ * Host buffers use the same plgpu_column struct as the C-ABI (host pointers).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/polaroid_gpu.h"
+
+#define OR_EXPORT __attribute__((visibility("default")))
+
+/* ------------------------------------------------------------ helpers */
+static inline int bit_get(const uint8_t* bm, int64_t i) { return (bm[i >> 3] >> (i & 7)) & 1; }
+static inline void bit_set(uint8_t* bm, int64_t i, int v) {
+    if (v) bm[i >> 3] |= (uint8_t)(1u << (i & 7));
+    else bm[i >> 3] &= (uint8_t)~(1u << (i & 7));
+}
+static inline int col_valid(const plgpu_column* c, int64_t r) {
+    return c->validity == NULL ? 1 : bit_get(c->validity, c->offset + r);
+}
+
+/* A typed scalar as seen by the expression interpreter. */
+typedef struct {
+    int dt; /* PLGPU_BOOL / PLGPU_I64 / PLGPU_F64 */
+    int valid;
+    int64_t i;
+    double f;
+} val_t;
+
+static val_t col_get(const plgpu_column* c, int64_t r) {
+    val_t v;
+    v.valid = col_valid(c, r);
+    v.i = 0;
+    v.f = 0.0;
+    int64_t p = c->offset + r;
+    switch (c->dtype) {
+    case PLGPU_BOOL: v.dt = PLGPU_BOOL; v.i = bit_get((const uint8_t*)c->values, p); break;
+    case PLGPU_I32: v.dt = PLGPU_I64; v.i = ((const int32_t*)c->values)[p]; break;
+    case PLGPU_U32: v.dt = PLGPU_I64; v.i = ((const uint32_t*)c->values)[p]; break;
+    case PLGPU_I64: v.dt = PLGPU_I64; v.i = ((const int64_t*)c->values)[p]; break;
+    default: v.dt = PLGPU_F64; v.f = ((const double*)c->values)[p]; break;
+    }
+    return v;
+}
+
+/* TotalOrd for f64: polars-utils/src/total_ord.rs:317-368.
+ * tot_ge(a,b) = a.is_nan() | (a >= b); tot_lt = !tot_ge; tot_gt(a,b) = tot_lt(b,a);
+ * tot_le(a,b) = tot_ge(b,a); tot_eq: NaN == NaN. */
+static int f_tot_ge(double a, double b) { return isnan(a) || a >= b; }
+static int f_tot_eq(double a, double b) { return isnan(a) ? isnan(b) : a == b; }
+static int f_cmp(int op, double a, double b) {
+    switch (op) {
+    case PLGPU_OP_EQ: return f_tot_eq(a, b);
+    case PLGPU_OP_NE: return !f_tot_eq(a, b);
+    case PLGPU_OP_LT: return !f_tot_ge(a, b);
+    case PLGPU_OP_LE: return f_tot_ge(b, a);
+    case PLGPU_OP_GT: return !f_tot_ge(b, a);
+    case PLGPU_OP_GE: return f_tot_ge(a, b);
+    }
+    return 0;
+}
+static int i_cmp(int op, int64_t a, int64_t b) {
+    switch (op) {
+    case PLGPU_OP_EQ: return a == b;
+    case PLGPU_OP_NE: return a != b;
+    case PLGPU_OP_LT: return a < b;
+    case PLGPU_OP_LE: return a <= b;
+    case PLGPU_OP_GT: return a > b;
+    case PLGPU_OP_GE: return a >= b;
+    }
+    return 0;
+}
+
+/* One postfix program, one row.  Returns 0 on success, -1 on type error. */
+static int eval_row(const plgpu_column* cols, const plgpu_instr* prog, int n, int64_t r, val_t* out) {
+    val_t st[PLGPU_MAX_STACK];
+    int sp = 0;
+    for (int k = 0; k < n; ++k) {
+        const plgpu_instr* in = &prog[k];
+        val_t a, b, z;
+        memset(&z, 0, sizeof z);
+        switch (in->op) {
+        case PLGPU_OP_COL: st[sp++] = col_get(&cols[in->arg], r); break;
+        case PLGPU_OP_LIT_F64: z.dt = PLGPU_F64; z.valid = 1; z.f = in->imm.f64; st[sp++] = z; break;
+        case PLGPU_OP_LIT_I64: z.dt = PLGPU_I64; z.valid = 1; z.i = in->imm.i64; st[sp++] = z; break;
+        case PLGPU_OP_LIT_BOOL: z.dt = PLGPU_BOOL; z.valid = 1; z.i = in->imm.i64 != 0; st[sp++] = z; break;
+        case PLGPU_OP_LIT_NULL:
+            z.dt = in->arg == PLGPU_F64 ? PLGPU_F64 : (in->arg == PLGPU_BOOL ? PLGPU_BOOL : PLGPU_I64);
+            z.valid = 0;
+            st[sp++] = z;
+            break;
+        case PLGPU_OP_ADD: case PLGPU_OP_SUB: case PLGPU_OP_MUL: case PLGPU_OP_TRUEDIV: {
+            b = st[--sp]; a = st[--sp];
+            if (a.dt == PLGPU_BOOL || b.dt == PLGPU_BOOL) return -1;
+            z.valid = a.valid && b.valid;
+            /* supertype: i64 (op) i64 -> i64 except true division -> f64
+             * (polars-plan/src/plans/aexpr/schema.rs get_arithmetic_field);
+             * integer ops wrap (polars-compute/src/arithmetic/signed.rs). */
+            if (a.dt == PLGPU_I64 && b.dt == PLGPU_I64 && in->op != PLGPU_OP_TRUEDIV) {
+                uint64_t x = (uint64_t)a.i, y = (uint64_t)b.i;
+                z.dt = PLGPU_I64;
+                z.i = (int64_t)(in->op == PLGPU_OP_ADD ? x + y : in->op == PLGPU_OP_SUB ? x - y : x * y);
+            } else {
+                double x = a.dt == PLGPU_F64 ? a.f : (double)a.i;
+                double y = b.dt == PLGPU_F64 ? b.f : (double)b.i;
+                z.dt = PLGPU_F64;
+                z.f = in->op == PLGPU_OP_ADD ? x + y : in->op == PLGPU_OP_SUB ? x - y
+                    : in->op == PLGPU_OP_MUL ? x * y : x / y;
+            }
+            st[sp++] = z;
+            break;
+        }
+        case PLGPU_OP_NEG: case PLGPU_OP_ABS:
+            a = st[--sp];
+            if (a.dt == PLGPU_BOOL) return -1;
+            if (a.dt == PLGPU_I64) {
+                uint64_t x = (uint64_t)a.i;
+                a.i = in->op == PLGPU_OP_NEG ? (int64_t)(0 - x) : (a.i < 0 ? (int64_t)(0 - x) : a.i);
+            } else {
+                a.f = in->op == PLGPU_OP_NEG ? -a.f : fabs(a.f);
+            }
+            st[sp++] = a;
+            break;
+        case PLGPU_OP_CAST_F64:
+            a = st[--sp];
+            if (a.dt != PLGPU_F64) { a.f = (double)a.i; a.dt = PLGPU_F64; }
+            st[sp++] = a;
+            break;
+        case PLGPU_OP_EQ: case PLGPU_OP_NE: case PLGPU_OP_LT: case PLGPU_OP_LE:
+        case PLGPU_OP_GT: case PLGPU_OP_GE: case PLGPU_OP_EQ_MISSING: case PLGPU_OP_NE_MISSING: {
+            b = st[--sp]; a = st[--sp];
+            int missing = in->op == PLGPU_OP_EQ_MISSING || in->op == PLGPU_OP_NE_MISSING;
+            int op = in->op == PLGPU_OP_EQ_MISSING ? PLGPU_OP_EQ
+                   : in->op == PLGPU_OP_NE_MISSING ? PLGPU_OP_NE : in->op;
+            z.dt = PLGPU_BOOL;
+            if (!(a.valid && b.valid)) {
+                if (missing) {
+                    /* null == null; null != value (polars eq_missing) */
+                    int eq = !a.valid && !b.valid;
+                    z.valid = 1;
+                    z.i = op == PLGPU_OP_EQ ? eq : !eq;
+                } else {
+                    z.valid = 0;
+                }
+            } else {
+                z.valid = 1;
+                if (a.dt == PLGPU_F64 || b.dt == PLGPU_F64) {
+                    double x = a.dt == PLGPU_F64 ? a.f : (double)a.i;
+                    double y = b.dt == PLGPU_F64 ? b.f : (double)b.i;
+                    z.i = f_cmp(op, x, y);
+                } else {
+                    z.i = i_cmp(op, a.i, b.i);
+                }
+            }
+            st[sp++] = z;
+            break;
+        }
+        case PLGPU_OP_AND: case PLGPU_OP_OR: {
+            /* Kleene logic (polars-arrow/src/compute/boolean_kleene.rs). */
+            b = st[--sp]; a = st[--sp];
+            if (a.dt != PLGPU_BOOL || b.dt != PLGPU_BOOL) return -1;
+            z.dt = PLGPU_BOOL;
+            if (in->op == PLGPU_OP_AND) {
+                if ((a.valid && !a.i) || (b.valid && !b.i)) { z.valid = 1; z.i = 0; }
+                else if (a.valid && b.valid) { z.valid = 1; z.i = 1; }
+                else z.valid = 0;
+            } else {
+                if ((a.valid && a.i) || (b.valid && b.i)) { z.valid = 1; z.i = 1; }
+                else if (a.valid && b.valid) { z.valid = 1; z.i = 0; }
+                else z.valid = 0;
+            }
+            st[sp++] = z;
+            break;
+        }
+        case PLGPU_OP_NOT:
+            a = st[--sp];
+            if (a.dt != PLGPU_BOOL) return -1;
+            a.i = !a.i;
+            st[sp++] = a;
+            break;
+        case PLGPU_OP_IS_NULL: case PLGPU_OP_IS_NOT_NULL:
+            a = st[--sp];
+            z.dt = PLGPU_BOOL; z.valid = 1;
+            z.i = in->op == PLGPU_OP_IS_NULL ? !a.valid : a.valid;
+            st[sp++] = z;
+            break;
+        case PLGPU_OP_IS_NAN: case PLGPU_OP_IS_FINITE:
+            a = st[--sp];
+            if (a.dt == PLGPU_BOOL) return -1;
+            z.dt = PLGPU_BOOL; z.valid = a.valid;
+            if (a.dt == PLGPU_F64) z.i = in->op == PLGPU_OP_IS_NAN ? isnan(a.f) : isfinite(a.f);
+            else z.i = in->op == PLGPU_OP_IS_NAN ? 0 : 1;
+            st[sp++] = z;
+            break;
+        default:
+            return -1;
+        }
+    }
+    if (sp != 1) return -1;
+    *out = st[0];
+    return 0;
+}
+
+/* Evaluate a program for all rows.  out_values: BOOL -> bit-packed bytes,
+ * I64 -> int64, F64 -> double; out_validity bit-packed (always written).
+ * Returns the output dtype or -1. */
+OR_EXPORT int or_eval(const plgpu_column* cols, int32_t ncols, const plgpu_instr* prog, int32_t n,
+                      int64_t nrows, void* out_values, uint8_t* out_validity) {
+    (void)ncols;
+    int dt = -1;
+    for (int64_t r = 0; r < nrows; ++r) {
+        val_t v;
+        if (eval_row(cols, prog, n, r, &v) != 0) return -1;
+        dt = v.dt;
+        bit_set(out_validity, r, v.valid);
+        if (v.dt == PLGPU_BOOL) bit_set((uint8_t*)out_values, r, v.valid ? (int)v.i : 0);
+        else if (v.dt == PLGPU_I64) ((int64_t*)out_values)[r] = v.valid ? v.i : 0;
+        else ((double*)out_values)[r] = v.valid ? v.f : 0.0;
+    }
+    return dt;
+}
+
+/* Filter mask from a program: null -> false (polars-compute/src/filter/mod.rs:21-27). */
+static int eval_mask(const plgpu_column* cols, const plgpu_instr* prog, int n, int64_t r) {
+    if (n <= 0) return 1;
+    val_t v;
+    if (eval_row(cols, prog, n, r, &v) != 0) return 0;
+    return v.dt == PLGPU_BOOL && v.valid && v.i;
+}
+
+/* Filter one fixed-width column by a program-derived mask; stable order
+ * (polars-compute/src/filter/primitive.rs filter_values_and_validity).
+ * elem_bytes: 4 or 8; BOOL columns are not supported by this helper.
+ * Returns the number of selected rows. */
+OR_EXPORT int64_t or_filter(const plgpu_column* cols, int32_t ncols, const plgpu_instr* prog, int32_t n,
+                            int64_t nrows, int32_t which, void* out_values, uint8_t* out_validity) {
+    (void)ncols;
+    const plgpu_column* c = &cols[which];
+    int eb = (c->dtype == PLGPU_I32 || c->dtype == PLGPU_U32) ? 4 : 8;
+    int64_t o = 0;
+    for (int64_t r = 0; r < nrows; ++r) {
+        if (!eval_mask(cols, prog, n, r)) continue;
+        memcpy((char*)out_values + o * eb, (const char*)c->values + (c->offset + r) * eb, eb);
+        if (out_validity) bit_set(out_validity, o, col_valid(c, r));
+        ++o;
+    }
+    return o;
+}
+
+/* ---------------------------------------------------------- exact sum */
+/* Shewchuk's exact-partials summation with a correctly rounded result (the
+ * algorithm CPython's math.fsum publishes).  Used as the "exact" leg. */
+typedef struct {
+    double* p;
+    int n, cap;
+    double special; /* accumulates inf / nan IEEE-wise */
+    int has_special;
+} fsum_t;
+
+static void fsum_init(fsum_t* s) { s->p = NULL; s->n = s->cap = 0; s->special = 0.0; s->has_special = 0; }
+static void fsum_add(fsum_t* s, double x) {
+    if (!isfinite(x)) { s->special += x; s->has_special = 1; return; }
+    int i = 0;
+    for (int j = 0; j < s->n; ++j) {
+        double y = s->p[j];
+        if (fabs(x) < fabs(y)) { double t = x; x = y; y = t; }
+        double hi = x + y;
+        double lo = y - (hi - x);
+        if (lo != 0.0) s->p[i++] = lo;
+        x = hi;
+    }
+    if (i + 1 > s->cap) { s->cap = s->cap ? s->cap * 2 : 8; s->p = (double*)realloc(s->p, sizeof(double) * s->cap); }
+    s->p[i++] = x;
+    s->n = i;
+}
+static double fsum_result(fsum_t* s) {
+    if (s->has_special) return s->special;
+    int n = s->n;
+    double hi = 0.0, lo = 0.0;
+    if (n > 0) {
+        hi = s->p[--n];
+        while (n > 0) {
+            double x = hi, y = s->p[--n];
+            hi = x + y;
+            double yr = hi - x;
+            lo = y - yr;
+            if (lo != 0.0) break;
+        }
+        /* round-half-even correction across the remaining partials */
+        if (n > 0 && ((lo < 0.0 && s->p[n - 1] < 0.0) || (lo > 0.0 && s->p[n - 1] > 0.0))) {
+            double y = lo * 2.0;
+            double x = hi + y;
+            double yr = x - hi;
+            if (y == yr) hi = x;
+        }
+    }
+    return hi;
+}
+static void fsum_free(fsum_t* s) { free(s->p); }
+
+/* ------------------------------------------------------------ group_by */
+/* Row-order hash grouping (polars-core/src/frame/group_by/hashing.rs
+ * group_by_threaded_slice / into_groups.rs): groups in order of first
+ * occurrence, each group's rows ascending (GroupsIdx {first, all}).
+ * Null keys form their own group. */
+typedef struct {
+    int64_t* keys;
+    int64_t* gid;   /* slot -> group id */
+    uint8_t* used;
+    int64_t cap;
+} imap_t;
+
+static uint64_t mix64(uint64_t x) {
+    x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33;
+    return x;
+}
+static void imap_init(imap_t* m, int64_t expect) {
+    int64_t cap = 16;
+    while (cap < 2 * expect + 16) cap <<= 1;
+    m->cap = cap;
+    m->keys = (int64_t*)malloc(sizeof(int64_t) * cap);
+    m->gid = (int64_t*)malloc(sizeof(int64_t) * cap);
+    m->used = (uint8_t*)calloc(cap, 1);
+}
+static void imap_free(imap_t* m) { free(m->keys); free(m->gid); free(m->used); }
+/* returns group id, inserting new_gid if absent */
+static int64_t imap_get_or_insert(imap_t* m, int64_t key, int64_t new_gid, int* inserted) {
+    uint64_t h = mix64((uint64_t)key) & (uint64_t)(m->cap - 1);
+    for (;;) {
+        if (!m->used[h]) { m->used[h] = 1; m->keys[h] = key; m->gid[h] = new_gid; *inserted = 1; return new_gid; }
+        if (m->keys[h] == key) { *inserted = 0; return m->gid[h]; }
+        h = (h + 1) & (uint64_t)(m->cap - 1);
+    }
+}
+
+typedef struct {
+    int64_t ngroups;
+    int64_t* first;    /* first row of each group                        */
+    int64_t* key;      /* key value                                      */
+    uint8_t* key_null; /* 1 if the null group                            */
+    int64_t* start;    /* CSR offsets into rows[]                        */
+    int64_t* rows;     /* member rows in ascending order                 */
+} groups_t;
+
+static void build_groups(const plgpu_column* key, const plgpu_column* cols, const plgpu_instr* prog, int n,
+                         int64_t nrows, groups_t* g) {
+    imap_t m;
+    imap_init(&m, nrows < 1024 ? nrows : 1024);
+    int64_t cap = 64, ng = 0, null_gid = -1;
+    int64_t* gid_of_row = (int64_t*)malloc(sizeof(int64_t) * (nrows ? nrows : 1));
+    g->first = (int64_t*)malloc(sizeof(int64_t) * cap);
+    g->key = (int64_t*)malloc(sizeof(int64_t) * cap);
+    g->key_null = (uint8_t*)malloc(cap);
+    int64_t* cnt = (int64_t*)calloc(cap, sizeof(int64_t));
+    for (int64_t r = 0; r < nrows; ++r) {
+        gid_of_row[r] = -1;
+        if (!eval_mask(cols, prog, n, r)) continue;
+        val_t k = col_get(key, r);
+        int64_t gi;
+        int ins = 0;
+        if (!k.valid) {
+            if (null_gid < 0) { null_gid = ng; ins = 1; }
+            gi = null_gid;
+        } else {
+            if (m.cap < 2 * (ng + 1)) {
+                /* grow */
+                imap_t m2;
+                imap_init(&m2, 2 * m.cap);
+                for (int64_t s = 0; s < m.cap; ++s)
+                    if (m.used[s]) { int d; imap_get_or_insert(&m2, m.keys[s], m.gid[s], &d); }
+                imap_free(&m);
+                m = m2;
+            }
+            gi = imap_get_or_insert(&m, k.i, ng, &ins);
+        }
+        if (ins) {
+            if (ng == cap) {
+                cap *= 2;
+                g->first = (int64_t*)realloc(g->first, sizeof(int64_t) * cap);
+                g->key = (int64_t*)realloc(g->key, sizeof(int64_t) * cap);
+                g->key_null = (uint8_t*)realloc(g->key_null, cap);
+                cnt = (int64_t*)realloc(cnt, sizeof(int64_t) * cap);
+            }
+            g->first[ng] = r;
+            g->key[ng] = k.valid ? k.i : 0;
+            g->key_null[ng] = !k.valid;
+            cnt[ng] = 0;
+            ++ng;
+        }
+        cnt[gi]++;
+        gid_of_row[r] = gi;
+    }
+    g->ngroups = ng;
+    g->start = (int64_t*)malloc(sizeof(int64_t) * (ng + 1));
+    g->start[0] = 0;
+    for (int64_t i = 0; i < ng; ++i) g->start[i + 1] = g->start[i] + cnt[i];
+    g->rows = (int64_t*)malloc(sizeof(int64_t) * (g->start[ng] ? g->start[ng] : 1));
+    for (int64_t i = 0; i < ng; ++i) cnt[i] = g->start[i];
+    for (int64_t r = 0; r < nrows; ++r)
+        if (gid_of_row[r] >= 0) g->rows[cnt[gid_of_row[r]]++] = r;
+    free(cnt);
+    free(gid_of_row);
+    imap_free(&m);
+}
+static void free_groups(groups_t* g) {
+    free(g->first); free(g->key); free(g->key_null); free(g->start); free(g->rows);
+}
+
+/* sum_mode for f64 SUM / MEAN:
+ *   0 = KahanSum in row order   (polars-core .../aggregations/mod.rs:581-610,
+ *                                polars-utils/src/kahan_sum.rs)
+ *   1 = naive `+=` in row order  (polars-expr/src/reduce/sum.rs:103-110, one thread)
+ *   2 = exact, correctly rounded (what the GPU path computes)             */
+static double f64_sum_group(const plgpu_column* c, const int64_t* rows, int64_t len, int mode, int64_t* nvalid) {
+    int64_t nv = 0;
+    if (mode == 0 && len == 1) {
+        /* agg_sum: `idx.len() == 1 => arr.get(first).unwrap_or(0)` (:590);
+         * the streaming fold (modes 1, 2) starts from +0.0 instead. */
+        val_t v = col_get(c, rows[0]);
+        *nvalid = v.valid;
+        return v.valid ? v.f : 0.0;
+    }
+    if (mode == 0) {
+        double sum = 0.0, err = 0.0;
+        for (int64_t i = 0; i < len; ++i) {
+            val_t v = col_get(c, rows[i]);
+            if (!v.valid) continue;
+            ++nv;
+            double x = v.f;
+            if (isfinite(x)) {
+                double y = x - err;
+                double t = sum + y;
+                err = (t - sum) - y;
+                sum = t;
+            } else {
+                sum += x;
+            }
+        }
+        *nvalid = nv;
+        return sum;
+    } else if (mode == 1) {
+        double sum = 0.0;
+        for (int64_t i = 0; i < len; ++i) {
+            val_t v = col_get(c, rows[i]);
+            if (!v.valid) continue;
+            ++nv;
+            sum += v.f;
+        }
+        *nvalid = nv;
+        return sum;
+    } else {
+        fsum_t s;
+        fsum_init(&s);
+        for (int64_t i = 0; i < len; ++i) {
+            val_t v = col_get(c, rows[i]);
+            if (!v.valid) continue;
+            ++nv;
+            fsum_add(&s, v.f);
+        }
+        double r = fsum_result(&s);
+        fsum_free(&s);
+        *nvalid = nv;
+        return r + 0.0; /* exact zero -> +0.0, as the fold from +0.0 gives */
+    }
+}
+
+/* Group-by with aggregations, groups in first-occurrence order
+ * (maintain_order=True).  For each agg a: out_vals[a] is int64_t[] for I64
+ * results, uint32_t[] for COUNT/LEN, double[] otherwise; out_valid[a] is a
+ * byte-per-group validity array.  Returns the number of groups, or -1. */
+OR_EXPORT int64_t or_group_by_agg(const plgpu_column* key, const plgpu_column* cols, int32_t ncols,
+                                  const plgpu_instr* prog, int32_t n, const plgpu_agg* aggs, int32_t naggs,
+                                  int64_t nrows, int32_t sum_mode, int64_t max_groups, int64_t* out_keys,
+                                  uint8_t* out_key_valid, void** out_vals, uint8_t** out_valid) {
+    (void)ncols;
+    groups_t g;
+    build_groups(key, cols, prog, n, nrows, &g);
+    if (g.ngroups > max_groups) { free_groups(&g); return -1; }
+    for (int64_t gi = 0; gi < g.ngroups; ++gi) {
+        out_keys[gi] = g.key[gi];
+        out_key_valid[gi] = !g.key_null[gi];
+        const int64_t* rows = g.rows + g.start[gi];
+        int64_t len = g.start[gi + 1] - g.start[gi];
+        for (int a = 0; a < naggs; ++a) {
+            const plgpu_column* c = &cols[aggs[a].col];
+            int isf = c->dtype == PLGPU_F64;
+            uint8_t valid = 1;
+            switch (aggs[a].kind) {
+            case PLGPU_AGG_LEN: ((uint32_t*)out_vals[a])[gi] = (uint32_t)len; break;
+            case PLGPU_AGG_COUNT: {
+                uint32_t nv = 0;
+                for (int64_t i = 0; i < len; ++i) nv += col_valid(c, rows[i]);
+                ((uint32_t*)out_vals[a])[gi] = nv;
+                break;
+            }
+            case PLGPU_AGG_SUM:
+                if (isf) {
+                    int64_t nv;
+                    ((double*)out_vals[a])[gi] = f64_sum_group(c, rows, len, sum_mode, &nv);
+                } else {
+                    /* integer sum wraps (Rust release arithmetic) */
+                    uint64_t s = 0;
+                    for (int64_t i = 0; i < len; ++i) {
+                        val_t v = col_get(c, rows[i]);
+                        if (v.valid) s += (uint64_t)v.i;
+                    }
+                    ((int64_t*)out_vals[a])[gi] = (int64_t)s;
+                }
+                break;
+            case PLGPU_AGG_MEAN: {
+                /* agg_mean (mod.rs:659-700): sum / non-null count, null if 0 */
+                int64_t nv = 0;
+                double s;
+                if (isf) {
+                    s = f64_sum_group(c, rows, len, sum_mode, &nv);
+                } else {
+                    fsum_t fs;
+                    fsum_init(&fs);
+                    double ks = 0.0, ke = 0.0;
+                    for (int64_t i = 0; i < len; ++i) {
+                        val_t v = col_get(c, rows[i]);
+                        if (!v.valid) continue;
+                        ++nv;
+                        double x = (double)v.i;
+                        if (sum_mode == 2) fsum_add(&fs, x);
+                        else { double y = x - ke; double t = ks + y; ke = (t - ks) - y; ks = t; }
+                    }
+                    s = sum_mode == 2 ? fsum_result(&fs) : ks;
+                    fsum_free(&fs);
+                }
+                if (nv == 0) { valid = 0; ((double*)out_vals[a])[gi] = 0.0; }
+                else ((double*)out_vals[a])[gi] = s / (double)nv;
+                break;
+            }
+            case PLGPU_AGG_MIN: case PLGPU_AGG_MAX: {
+                /* min_ignore_nan / max_ignore_nan (polars-utils/src/min_max.rs:91-98,
+                 * polars-expr/src/reduce/min_max.rs:100-130): NaN only if every
+                 * valid value is NaN; null if no valid value. */
+                int is_min = aggs[a].kind == PLGPU_AGG_MIN;
+                int any = 0, any_num = 0;
+                double bf = 0.0;
+                int64_t bi = 0;
+                for (int64_t i = 0; i < len; ++i) {
+                    val_t v = col_get(c, rows[i]);
+                    if (!v.valid) continue;
+                    any = 1;
+                    if (isf) {
+                        if (isnan(v.f)) continue;
+                        if (!any_num) bf = v.f;
+                        else if (is_min ? (v.f < bf || (v.f == bf && signbit(v.f))) : (v.f > bf || (v.f == bf && !signbit(v.f)))) bf = v.f;
+                        any_num = 1;
+                    } else {
+                        if (!any_num || (is_min ? v.i < bi : v.i > bi)) bi = v.i;
+                        any_num = 1;
+                    }
+                }
+                if (!any) valid = 0;
+                if (isf) ((double*)out_vals[a])[gi] = any_num ? bf : (any ? NAN : 0.0);
+                else ((int64_t*)out_vals[a])[gi] = bi;
+                break;
+            }
+            default:
+                free_groups(&g);
+                return -1;
+            }
+            out_valid[a][gi] = valid;
+        }
+    }
+    int64_t ng = g.ngroups;
+    free_groups(&g);
+    return ng;
+}
+
+/* Exact, correctly rounded sum of a plain f64 array (pinned to math.fsum
+ * in tests/test_oracle.py). */
+OR_EXPORT double or_fsum(const double* x, int64_t n) {
+    fsum_t s;
+    fsum_init(&s);
+    for (int64_t i = 0; i < n; ++i) fsum_add(&s, x[i]);
+    double r = fsum_result(&s);
+    fsum_free(&s);
+    return r;
+}
+
+/* ------------------------------------------------------ CPU baseline */
+/* The bench's cpu_baseline leg: `filter(col(p) > k).group_by(key).agg(
+ * [col(c).sum() for c in sums])` over no-null columns, restating the
+ * streaming engine's partitioned hash aggregation (polars-stream group_by
+ * + polars-expr/src/reduce/sum.rs): each thread folds a contiguous morsel
+ * into a private hash table with naive `+=`, then tables are combined
+ * (combine_subset).  Returns the number of groups; out_sum_of_sums is a
+ * checksum (sum over groups and columns) so the work is not elided. */
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+OR_EXPORT int64_t or_baseline_filter_groupby_sum(const int64_t* key, const double* pred, double k,
+                                                 const double* const* sums, int32_t nsums, int64_t nrows,
+                                                 int32_t threads, double* out_sum_of_sums) {
+    int T = threads > 0 ? threads : 1;
+    typedef struct { imap_t m; double* acc; int64_t ng, cap; int64_t* keys; } part_t;
+    part_t* parts = (part_t*)calloc(T, sizeof(part_t));
+#pragma omp parallel num_threads(T)
+    {
+#ifdef _OPENMP
+        int t = omp_get_thread_num();
+#else
+        int t = 0;
+#endif
+        part_t* p = &parts[t];
+        imap_init(&p->m, 4096);
+        p->cap = 4096;
+        p->acc = (double*)calloc((size_t)p->cap * nsums, sizeof(double));
+        p->keys = (int64_t*)malloc(sizeof(int64_t) * p->cap);
+        int64_t lo = nrows * t / T, hi = nrows * (t + 1) / T;
+        for (int64_t r = lo; r < hi; ++r) {
+            double x = pred[r];
+            if (!(isnan(x) || x > k)) continue; /* tot_gt(x, k) with k not NaN */
+            if (p->m.cap < 2 * (p->ng + 1)) {
+                imap_t m2;
+                imap_init(&m2, 2 * p->m.cap);
+                for (int64_t s = 0; s < p->m.cap; ++s)
+                    if (p->m.used[s]) { int d; imap_get_or_insert(&m2, p->m.keys[s], p->m.gid[s], &d); }
+                imap_free(&p->m);
+                p->m = m2;
+            }
+            int ins;
+            int64_t gi = imap_get_or_insert(&p->m, key[r], p->ng, &ins);
+            if (ins) {
+                if (p->ng == p->cap) {
+                    p->cap *= 2;
+                    p->acc = (double*)realloc(p->acc, sizeof(double) * p->cap * nsums);
+                    p->keys = (int64_t*)realloc(p->keys, sizeof(int64_t) * p->cap);
+                }
+                memset(p->acc + p->ng * nsums, 0, sizeof(double) * nsums);
+                p->keys[p->ng] = key[r];
+                p->ng++;
+            }
+            double* a = p->acc + gi * nsums;
+            for (int c = 0; c < nsums; ++c) a[c] += sums[c][r];
+        }
+    }
+    /* combine partials into thread 0's table */
+    part_t* d = &parts[0];
+    for (int t = 1; t < T; ++t) {
+        part_t* p = &parts[t];
+        for (int64_t i = 0; i < p->ng; ++i) {
+            if (d->m.cap < 2 * (d->ng + 1)) {
+                imap_t m2;
+                imap_init(&m2, 2 * d->m.cap);
+                for (int64_t s = 0; s < d->m.cap; ++s)
+                    if (d->m.used[s]) { int dd; imap_get_or_insert(&m2, d->m.keys[s], d->m.gid[s], &dd); }
+                imap_free(&d->m);
+                d->m = m2;
+            }
+            int ins;
+            int64_t gi = imap_get_or_insert(&d->m, p->keys[i], d->ng, &ins);
+            if (ins) {
+                if (d->ng == d->cap) {
+                    d->cap *= 2;
+                    d->acc = (double*)realloc(d->acc, sizeof(double) * d->cap * nsums);
+                    d->keys = (int64_t*)realloc(d->keys, sizeof(int64_t) * d->cap);
+                }
+                memset(d->acc + d->ng * nsums, 0, sizeof(double) * nsums);
+                d->keys[d->ng] = p->keys[i];
+                d->ng++;
+            }
+            for (int c = 0; c < nsums; ++c) d->acc[gi * nsums + c] += p->acc[i * nsums + c];
+        }
+    }
+    double chk = 0.0;
+    for (int64_t i = 0; i < d->ng * nsums; ++i) chk += d->acc[i];
+    *out_sum_of_sums = chk;
+    int64_t ng = d->ng;
+    for (int t = 0; t < T; ++t) { imap_free(&parts[t].m); free(parts[t].acc); free(parts[t].keys); }
+    free(parts);
+    return ng;
+}

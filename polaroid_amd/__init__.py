@@ -1,0 +1,50 @@
+"""polaroid_amd — MI355X-native executor backend for the Polars filter /
+arithmetic / comparison / hash-group-by-aggregation hot path.
+
+    import polaroid_amd as pl
+    out = (pl.DataFrame({...}).lazy()
+             .filter(pl.col("close") > 100.0)
+             .group_by("symbol")
+             .agg(pl.col("volume").sum(), pl.col("close").mean())
+             .collect())
+
+All compute runs in libpolaroid_gpu.so (hand-written HIP kernels for
+gfx950) behind the C-ABI of include/polaroid_gpu.h.
+"""
+
+from . import _native
+from ._native import (
+    ComputeError,
+    DeviceError,
+    InvalidOperationError,
+    OutOfMemoryError,
+    PolaroidError,
+    ShapeError,
+    device_count,
+)
+from .expr import Expr, col, count, len, lit, max, mean, min, sum
+from .frame import (
+    Boolean,
+    DataFrame,
+    DataType,
+    Float64,
+    GroupBy,
+    Int32,
+    Int64,
+    LazyFrame,
+    LazyGroupBy,
+    Series,
+    UInt32,
+    from_dict,
+)
+
+__all__ = [
+    "Boolean", "ComputeError", "DataFrame", "DataType", "DeviceError", "Expr", "Float64", "GroupBy",
+    "Int32", "Int64", "InvalidOperationError", "LazyFrame", "LazyGroupBy", "OutOfMemoryError",
+    "PolaroidError", "Series", "ShapeError", "UInt32", "col", "count", "device_count", "from_dict",
+    "len", "lit", "max", "mean", "min", "sum",
+]
+
+
+def native_library_path() -> str:
+    return _native.LIB_PATH

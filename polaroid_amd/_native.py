@@ -1,0 +1,189 @@
+"""ctypes binding of the C-ABI in include/polaroid_gpu.h.
+
+The product path always goes through libpolaroid_gpu.so; there is no CPU
+fallback.  If the library is missing the import fails loudly.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpolaroid_gpu.so")
+
+# dtypes (enum plgpu_dtype)
+BOOL, I32, I64, F64, U32 = 1, 2, 3, 4, 5
+DTYPE_BYTES = {I32: 4, I64: 8, F64: 8, U32: 4}
+
+# status codes
+OK = 0
+ERR_INVALID, ERR_SCHEMA, ERR_SHAPE, ERR_OOM, ERR_HIP, ERR_NO_DEVICE, ERR_CAPACITY = (
+    -1, -2, -3, -4, -5, -6, -7)
+
+# opcodes (enum plgpu_opcode)
+OP = dict(
+    COL=1, LIT_F64=2, LIT_I64=3, LIT_BOOL=4, LIT_NULL=5,
+    ADD=10, SUB=11, MUL=12, TRUEDIV=13, NEG=14, ABS=15, CAST_F64=16,
+    EQ=20, NE=21, LT=22, LE=23, GT=24, GE=25, EQ_MISSING=26, NE_MISSING=27,
+    AND=30, OR=31, NOT=32, IS_NULL=33, IS_NOT_NULL=34, IS_NAN=35, IS_FINITE=36,
+)
+AGG = dict(sum=1, mean=2, min=3, max=4, count=5, len=6)
+MAX_COLS = 8
+
+
+class Column(C.Structure):
+    pass
+
+
+RELEASE_FN = C.CFUNCTYPE(None, C.POINTER(Column))
+Column._fields_ = [
+    ("dtype", C.c_int32),
+    ("device_id", C.c_int32),
+    ("length", C.c_int64),
+    ("offset", C.c_int64),
+    ("null_count", C.c_int64),
+    ("values", C.c_void_p),
+    ("validity", C.c_void_p),
+    ("release", C.c_void_p),
+    ("private_data", C.c_void_p),
+]
+
+
+class _Imm(C.Union):
+    _fields_ = [("f64", C.c_double), ("i64", C.c_int64)]
+
+
+class Instr(C.Structure):
+    _fields_ = [("op", C.c_int32), ("arg", C.c_int32), ("imm", _Imm)]
+
+
+class Agg(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("col", C.c_int32)]
+
+
+class GroupByInfo(C.Structure):
+    _fields_ = [
+        ("rows_in", C.c_int64),
+        ("rows_selected", C.c_int64),
+        ("groups", C.c_int64),
+        ("global_path_rows", C.c_int64),
+        ("reruns", C.c_int32),
+        ("lds_slots", C.c_int32),
+        ("grid", C.c_int32),
+        ("sum_inexact", C.c_int32),
+        ("table_capacity", C.c_int64),
+        ("main_kernel_ms", C.c_double),
+    ]
+
+    def as_dict(self) -> dict:
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+# Every symbol declared in include/polaroid_gpu.h, with its signature.
+_P = C.c_void_p
+_COLP = C.POINTER(Column)
+SIGNATURES = {
+    "plgpu_abi_version": (C.c_int, []),
+    "plgpu_last_error": (C.c_char_p, []),
+    "plgpu_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "plgpu_set_device": (C.c_int, [C.c_int]),
+    "plgpu_synchronize": (C.c_int, [_P]),
+    "plgpu_alloc": (C.c_int, [C.POINTER(C.c_void_p), C.c_size_t, _P]),
+    "plgpu_free": (C.c_int, [_P, _P]),
+    "plgpu_memcpy_h2d": (C.c_int, [_P, _P, C.c_size_t, _P]),
+    "plgpu_memcpy_d2h": (C.c_int, [_P, _P, C.c_size_t, _P]),
+    "plgpu_memcpy_d2d": (C.c_int, [_P, _P, C.c_size_t, _P]),
+    "plgpu_column_release": (None, [_COLP]),
+    "plgpu_eval": (C.c_int, [_COLP, C.c_int32, C.POINTER(Instr), C.c_int32, _COLP, _P]),
+    "plgpu_filter": (C.c_int, [_COLP, C.c_int32, _COLP, _COLP, C.POINTER(C.c_int64), _P]),
+    "plgpu_filter_expr": (C.c_int, [_COLP, C.c_int32, C.POINTER(Instr), C.c_int32, _COLP,
+                                    C.POINTER(C.c_int64), _P]),
+    "plgpu_group_by_agg": (C.c_int, [_COLP, _COLP, C.c_int32, C.POINTER(Instr), C.c_int32,
+                                     C.POINTER(Agg), C.c_int32, C.c_int32, _COLP, _COLP,
+                                     C.POINTER(GroupByInfo), _P]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libpolaroid_gpu.so (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"polaroid_amd native library missing: {LIB_PATH}. Build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (make -C polaroid_amd/csrc)."
+            )
+        handle = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = handle
+    return _lib
+
+
+class PolaroidError(Exception):
+    """Base error of the GPU executor."""
+
+
+class ComputeError(PolaroidError):
+    pass
+
+
+class InvalidOperationError(PolaroidError):
+    pass
+
+
+class ShapeError(PolaroidError):
+    pass
+
+
+class OutOfMemoryError(PolaroidError):
+    pass
+
+
+class DeviceError(PolaroidError):
+    pass
+
+
+_ERRMAP = {
+    ERR_INVALID: InvalidOperationError,
+    ERR_SCHEMA: ComputeError,
+    ERR_SHAPE: ShapeError,
+    ERR_OOM: OutOfMemoryError,
+    ERR_HIP: DeviceError,
+    ERR_NO_DEVICE: DeviceError,
+    ERR_CAPACITY: ComputeError,
+}
+
+
+def check(rc: int) -> None:
+    if rc != OK:
+        msg = lib().plgpu_last_error().decode(errors="replace")
+        raise _ERRMAP.get(rc, PolaroidError)(msg)
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    rc = lib().plgpu_device_count(C.byref(n))
+    return n.value if rc == OK else 0
+
+
+class DeviceBuffer:
+    """Raw device allocation from the library's stream-ordered pool."""
+
+    __slots__ = ("ptr", "nbytes")
+
+    def __init__(self, nbytes: int):
+        p = C.c_void_p()
+        check(lib().plgpu_alloc(C.byref(p), C.c_size_t(max(int(nbytes), 1)), None))
+        self.ptr = p.value
+        self.nbytes = int(nbytes)
+
+    def __del__(self):
+        if getattr(self, "ptr", None) and _lib is not None:
+            _lib.plgpu_free(C.c_void_p(self.ptr), None)
+            self.ptr = None

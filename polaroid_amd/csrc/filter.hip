@@ -1,0 +1,381 @@
+// filter.hip — expression evaluation and filter compaction on gfx950.
+//
+// plgpu_eval:        PhysicalExpr::evaluate for column / literal / binary
+//                    expressions; Boolean results are bit-packed with one
+//                    wave64 ballot per 64 rows (Arrow LSB-first layout).
+// plgpu_filter*:     polars-compute/src/filter/mod.rs:18 (null mask = false),
+//                    three launches: mask+tile counts -> tile scan -> stable
+//                    scatter.  Each wave owns whole 64-row mask words, so the
+//                    in-word rank is one popcount of (word & lanemask_lt).
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <vector>
+
+#include "plgpu_internal.hpp"
+
+namespace plgpu {
+
+constexpr int kEvalThreads = 256;
+constexpr int kTileRows = 4096;                 // rows per filter tile
+constexpr int kTileWords = kTileRows / 64;      // 64 mask words per tile
+constexpr int kFilterThreads = 256;             // 4 waves; 16 words per wave per tile
+
+struct ColArgs {
+    DevCol c[PLGPU_MAX_COLS];
+};
+
+static int grid_for(int64_t items, int threads, int max_blocks = 256 * 16) {
+    int64_t b = (items + threads - 1) / threads;
+    if (b < 1) b = 1;
+    if (b > max_blocks) b = max_blocks;
+    return (int)b;
+}
+
+// ---------------------------------------------------------------- eval
+template <int SIMPLE>
+__global__ __launch_bounds__(kEvalThreads) void eval_kernel(ColArgs cols, DevProgram prog, int64_t n,
+                                                            uint64_t* __restrict__ out_values,
+                                                            uint64_t* __restrict__ out_validity) {
+    const int lane = threadIdx.x & 63;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < n; base += stride) {
+        const int64_t r = base + threadIdx.x;
+        uint64_t v = 0;
+        bool ok = false;
+        if (r < n) {
+            if (SIMPLE) {
+                const DevCol& c = cols.c[prog.simple_col];
+                ok = dev_valid(c, r);
+                v = simple_pred(prog.simple_isf, prog.simple_op, dev_load(c, r), prog.simple_imm) ? 1 : 0;
+            } else {
+                RowVal rv = eval_row(prog.code, prog.n, cols.c, r);
+                v = rv.v;
+                ok = rv.valid;
+            }
+        }
+        const uint64_t vbits = __ballot(ok);
+        const int64_t word = r >> 6;
+        if (prog.out_dtype == PLGPU_BOOL) {
+            const uint64_t bbits = __ballot(ok && (v & 1));
+            if (lane == 0 && base + (threadIdx.x & ~63) < n) {
+                out_values[word] = bbits;
+                out_validity[word] = vbits;
+            }
+        } else {
+            if (r < n) out_values[r] = ok ? v : 0ull;
+            if (lane == 0 && base + (threadIdx.x & ~63) < n) out_validity[word] = vbits;
+        }
+    }
+}
+
+// ------------------------------------------------------------- filter
+// Mask source: either a BOOL column (values & validity, null = false) or a
+// lowered program.  Writes one u64 per 64 rows and one count per tile.
+template <int SRC>  // 0 = bool column, 1 = simple predicate, 2 = program
+__global__ __launch_bounds__(kFilterThreads) void filter_mask_kernel(ColArgs cols, DevProgram prog, DevCol mask,
+                                                                     int64_t n, int64_t ntiles,
+                                                                     uint64_t* __restrict__ mask_words,
+                                                                     uint32_t* __restrict__ tile_counts) {
+    __shared__ uint32_t wave_cnt[kFilterThreads / 64];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        uint32_t cnt = 0;
+        for (int it = 0; it < kTileRows / kFilterThreads; ++it) {
+            const int64_t r = t * kTileRows + it * kFilterThreads + threadIdx.x;
+            bool sel = false;
+            if (r < n) {
+                if (SRC == 0) {
+                    sel = dev_valid(mask, r) && (dev_load(mask, r) & 1);
+                } else if (SRC == 1) {
+                    const DevCol& c = cols.c[prog.simple_col];
+                    sel = dev_valid(c, r) && simple_pred(prog.simple_isf, prog.simple_op, dev_load(c, r), prog.simple_imm);
+                } else {
+                    RowVal rv = eval_row(prog.code, prog.n, cols.c, r);
+                    sel = rv.valid && (rv.v & 1);
+                }
+            }
+            const uint64_t w = __ballot(sel);
+            if (lane == 0) mask_words[t * kTileWords + it * (kFilterThreads / 64) + wave] = w;
+            cnt += (uint32_t)__popcll(w);
+        }
+        if (lane == 0) wave_cnt[wave] = cnt;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t s = 0;
+            for (int w = 0; w < kFilterThreads / 64; ++w) s += wave_cnt[w];
+            tile_counts[t] = s;
+        }
+        __syncthreads();
+    }
+}
+
+// Exclusive scan of tile counts (single workgroup; ntiles <= a few 1e5).
+__global__ __launch_bounds__(1024) void scan_tiles_kernel(const uint32_t* __restrict__ counts, int64_t ntiles,
+                                                         uint64_t* __restrict__ offsets,
+                                                         uint64_t* __restrict__ total) {
+    __shared__ uint64_t part[1024];
+    const int tid = threadIdx.x;
+    const int64_t per = (ntiles + 1023) / 1024;
+    const int64_t lo = tid * per;
+    const int64_t hi = lo + per < ntiles ? lo + per : ntiles;
+    uint64_t s = 0;
+    for (int64_t i = lo; i < hi; ++i) s += counts[i];
+    part[tid] = s;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+        uint64_t x = tid >= off ? part[tid - off] : 0;
+        __syncthreads();
+        part[tid] += x;
+        __syncthreads();
+    }
+    uint64_t run = part[tid] - s;  // exclusive
+    for (int64_t i = lo; i < hi; ++i) {
+        offsets[i] = run;
+        run += counts[i];
+    }
+    if (tid == 1023) *total = part[1023];
+}
+
+__device__ __forceinline__ uint64_t wave_or64(uint64_t x) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) x |= __shfl_xor(x, off, 64);
+    return x;
+}
+
+// Stable scatter of one column by the mask words.
+template <int EB>  // element bytes (4 or 8); 0 = bit-packed bool
+__global__ __launch_bounds__(kFilterThreads) void filter_scatter_kernel(DevCol col, int64_t n, int64_t ntiles,
+                                                                        const uint64_t* __restrict__ mask_words,
+                                                                        const uint64_t* __restrict__ tile_off,
+                                                                        void* __restrict__ out_values,
+                                                                        uint64_t* __restrict__ out_validity) {
+    __shared__ uint64_t words[kTileWords];
+    __shared__ uint32_t prefix[kTileWords];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const uint64_t lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        if (threadIdx.x < kTileWords) {
+            uint64_t w = mask_words[t * kTileWords + threadIdx.x];
+            words[threadIdx.x] = w;
+            prefix[threadIdx.x] = (uint32_t)__popcll(w);
+        }
+        __syncthreads();
+        if (threadIdx.x < 64) {  // inclusive scan of 64 counts in one wave
+            uint32_t x = prefix[threadIdx.x];
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                uint32_t y = __shfl_up(x, off, 64);
+                if (lane >= off) x += y;
+            }
+            prefix[threadIdx.x] = x - (uint32_t)__popcll(words[threadIdx.x]);
+        }
+        __syncthreads();
+        const uint64_t base_off = tile_off[t];
+        for (int it = 0; it < kTileRows / kFilterThreads; ++it) {
+            const int wi = it * (kFilterThreads / 64) + wave;
+            const uint64_t w = words[wi];
+            if (w == 0) continue;  // wave-uniform
+            const int64_t r = t * kTileRows + it * kFilterThreads + threadIdx.x;
+            const bool sel = (w >> lane) & 1;
+            const uint32_t rank = (uint32_t)__popcll(w & lt_mask);
+            const uint64_t pos = base_off + prefix[wi] + rank;
+            if (sel) {
+                const int64_t p = col.offset + r;
+                if (EB == 8) ((uint64_t*)out_values)[pos] = ((const uint64_t*)col.values)[p];
+                else if (EB == 4) ((uint32_t*)out_values)[pos] = ((const uint32_t*)col.values)[p];
+            }
+            if (EB == 0 || col.validity != nullptr) {
+                // Pack bits of the selected rows at their output ranks, then
+                // OR the (<=64-bit) run into the output bitmap.
+                const uint64_t wpos = base_off + prefix[wi];
+                uint64_t vb = 0, bb = 0;
+                if (sel) {
+                    if (col.validity != nullptr && dev_valid(col, r)) vb = 1ull << rank;
+                    if (col.validity == nullptr) vb = 1ull << rank;
+                    if (EB == 0 && (dev_load(col, r) & 1)) bb = 1ull << rank;
+                }
+                vb = wave_or64(vb);
+                if (EB == 0) bb = wave_or64(bb);
+                if (lane == 0) {
+                    const uint64_t word = wpos >> 6;
+                    const int sh = (int)(wpos & 63);
+                    const int cntw = __popcll(w);
+                    (void)cntw;
+                    atomicOr((unsigned long long*)&out_validity[word], (unsigned long long)(vb << sh));
+                    if (sh != 0 && (vb >> (64 - sh)) != 0)
+                        atomicOr((unsigned long long*)&out_validity[word + 1], (unsigned long long)(vb >> (64 - sh)));
+                    if (EB == 0) {
+                        uint64_t* ov = (uint64_t*)out_values;
+                        atomicOr((unsigned long long*)&ov[word], (unsigned long long)(bb << sh));
+                        if (sh != 0 && (bb >> (64 - sh)) != 0)
+                            atomicOr((unsigned long long*)&ov[word + 1], (unsigned long long)(bb >> (64 - sh)));
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+static ColArgs pack_cols(const plgpu_column* cols, int32_t ncols) {
+    ColArgs a;
+    std::memset(&a, 0, sizeof a);
+    for (int i = 0; i < ncols && i < PLGPU_MAX_COLS; ++i) {
+        a.c[i].values = cols[i].values;
+        a.c[i].validity = cols[i].validity;
+        a.c[i].offset = cols[i].offset;
+        a.c[i].dtype = cols[i].dtype;
+    }
+    return a;
+}
+
+static int check_cols(const plgpu_column* cols, int32_t ncols, int64_t* n) {
+    if (ncols < 0 || ncols > PLGPU_MAX_COLS) return fail(PLGPU_ERR_INVALID, "too many columns (max 8)");
+    if (ncols == 0) { *n = 0; return PLGPU_OK; }
+    *n = cols[0].length;
+    for (int i = 0; i < ncols; ++i) {
+        if (cols[i].length != *n)
+            return fail(PLGPU_ERR_SHAPE, "all columns must have the same length");
+        if (cols[i].values == nullptr && cols[i].length > 0)
+            return fail(PLGPU_ERR_INVALID, "column has no values buffer");
+    }
+    return PLGPU_OK;
+}
+
+// Shared body of plgpu_filter / plgpu_filter_expr.
+static int run_filter(const plgpu_column* cols, int32_t ncols, int src, const DevProgram* prog,
+                      const plgpu_column* mask, plgpu_column* out_cols, int64_t* out_len, hipStream_t s) {
+    int64_t n = 0;
+    int rc = check_cols(cols, ncols, &n);
+    if (rc) return rc;
+    if (src == 0) {
+        if (mask->dtype != PLGPU_BOOL) {
+            return fail(PLGPU_ERR_SCHEMA, "filter predicate must be of type `Boolean`");
+        }
+        if (ncols > 0 && mask->length != n) return fail(PLGPU_ERR_SHAPE, "filter's length differs from that of the mask");
+        if (ncols == 0) n = mask->length;
+    }
+    for (int i = 0; i < ncols; ++i) std::memset(&out_cols[i], 0, sizeof(plgpu_column));
+    const int64_t ntiles = (n + kTileRows - 1) / kTileRows;
+    ColArgs ca = pack_cols(cols, ncols);
+    DevCol md;
+    std::memset(&md, 0, sizeof md);
+    if (src == 0) {
+        md.values = mask->values;
+        md.validity = mask->validity;
+        md.offset = mask->offset;
+        md.dtype = PLGPU_BOOL;
+    }
+    DevProgram dp;
+    if (prog) dp = *prog;
+    else std::memset(&dp, 0, sizeof dp);
+
+    uint64_t* mask_words = nullptr;
+    uint32_t* counts = nullptr;
+    uint64_t* offs = nullptr;  // ntiles offsets + 1 total
+    uint64_t total = 0;
+    if (ntiles > 0) {
+        if ((rc = dev_alloc((void**)&mask_words, ntiles * kTileWords * 8, s))) return rc;
+        if ((rc = dev_alloc((void**)&counts, ntiles * 4, s))) { dev_free(mask_words, s); return rc; }
+        if ((rc = dev_alloc((void**)&offs, (ntiles + 1) * 8, s))) {
+            dev_free(mask_words, s);
+            dev_free(counts, s);
+            return rc;
+        }
+        const int g = grid_for(ntiles, 1, 256 * 8);
+        if (src == 0)
+            filter_mask_kernel<0><<<g, kFilterThreads, 0, s>>>(ca, dp, md, n, ntiles, mask_words, counts);
+        else if (dp.simple)
+            filter_mask_kernel<1><<<g, kFilterThreads, 0, s>>>(ca, dp, md, n, ntiles, mask_words, counts);
+        else
+            filter_mask_kernel<2><<<g, kFilterThreads, 0, s>>>(ca, dp, md, n, ntiles, mask_words, counts);
+        scan_tiles_kernel<<<1, 1024, 0, s>>>(counts, ntiles, offs, offs + ntiles);
+        PLGPU_HIP(hipGetLastError());
+        PLGPU_HIP(hipMemcpyAsync(&total, offs + ntiles, 8, hipMemcpyDeviceToHost, s));
+        PLGPU_HIP(hipStreamSynchronize(s));
+    }
+    for (int i = 0; i < ncols; ++i) {
+        const bool need_valid = cols[i].validity != nullptr;
+        rc = make_owned_column(&out_cols[i], cols[i].dtype, (int64_t)total,
+                               need_valid || cols[i].dtype == PLGPU_BOOL, s);
+        if (rc) break;
+        if (total == 0) continue;
+        if (out_cols[i].validity)
+            PLGPU_HIP(hipMemsetAsync((void*)out_cols[i].validity, 0, ((total + 63) / 64) * 8, s));
+        if (cols[i].dtype == PLGPU_BOOL) {
+            PLGPU_HIP(hipMemsetAsync((void*)out_cols[i].values, 0, ((total + 63) / 64) * 8, s));
+        }
+        DevCol dc = ca.c[i];
+        const int g = grid_for(ntiles, 1, 256 * 8);
+        uint64_t* ovalid = (uint64_t*)out_cols[i].validity;
+        if (cols[i].dtype == PLGPU_BOOL)
+            filter_scatter_kernel<0><<<g, kFilterThreads, 0, s>>>(dc, n, ntiles, mask_words, offs,
+                                                                  (void*)out_cols[i].values, ovalid);
+        else if (dtype_bytes(cols[i].dtype) == 8)
+            filter_scatter_kernel<8><<<g, kFilterThreads, 0, s>>>(dc, n, ntiles, mask_words, offs,
+                                                                  (void*)out_cols[i].values, ovalid);
+        else
+            filter_scatter_kernel<4><<<g, kFilterThreads, 0, s>>>(dc, n, ntiles, mask_words, offs,
+                                                                  (void*)out_cols[i].values, ovalid);
+        PLGPU_HIP(hipGetLastError());
+        if (!need_valid && cols[i].dtype == PLGPU_BOOL) out_cols[i].null_count = 0;
+    }
+    dev_free(mask_words, s);
+    dev_free(counts, s);
+    dev_free(offs, s);
+    if (rc) {
+        for (int i = 0; i < ncols; ++i) plgpu_column_release(&out_cols[i]);
+        return rc;
+    }
+    *out_len = (int64_t)total;
+    return PLGPU_OK;
+}
+
+}  // namespace plgpu
+
+using namespace plgpu;
+
+PLGPU_API int plgpu_eval(const plgpu_column* cols, int32_t ncols, const plgpu_instr* program, int32_t n_instr,
+                         plgpu_column* out, void* stream) {
+    hipStream_t s = as_stream(stream);
+    int64_t n = 0;
+    int rc = check_cols(cols, ncols, &n);
+    if (rc) return rc;
+    DevProgram dp;
+    if ((rc = lower_program(cols, ncols, program, n_instr, &dp))) return rc;
+    if (ncols == 0) return fail(PLGPU_ERR_INVALID, "eval needs at least one column to define the length");
+    if ((rc = make_owned_column(out, dp.out_dtype, n, true, s))) return rc;
+    if (n == 0) return PLGPU_OK;
+    ColArgs ca = pack_cols(cols, ncols);
+    const int g = grid_for(n, kEvalThreads);
+    if (dp.simple)
+        eval_kernel<1><<<g, kEvalThreads, 0, s>>>(ca, dp, n, (uint64_t*)out->values, (uint64_t*)out->validity);
+    else
+        eval_kernel<0><<<g, kEvalThreads, 0, s>>>(ca, dp, n, (uint64_t*)out->values, (uint64_t*)out->validity);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        plgpu_column_release(out);
+        return hip_fail(e, "eval_kernel launch");
+    }
+    return PLGPU_OK;
+}
+
+PLGPU_API int plgpu_filter(const plgpu_column* cols, int32_t ncols, const plgpu_column* mask,
+                           plgpu_column* out_cols, int64_t* out_len, void* stream) {
+    if (mask == nullptr) return fail(PLGPU_ERR_INVALID, "mask is NULL");
+    return run_filter(cols, ncols, 0, nullptr, mask, out_cols, out_len, as_stream(stream));
+}
+
+PLGPU_API int plgpu_filter_expr(const plgpu_column* cols, int32_t ncols, const plgpu_instr* program,
+                                int32_t n_instr, plgpu_column* out_cols, int64_t* out_len, void* stream) {
+    DevProgram dp;
+    int rc = lower_program(cols, ncols, program, n_instr, &dp);
+    if (rc) return rc;
+    if (dp.out_dtype != PLGPU_BOOL) {
+        return fail(PLGPU_ERR_SCHEMA, "filter predicate must be of type `Boolean`");
+    }
+    return run_filter(cols, ncols, dp.simple ? 1 : 2, &dp, nullptr, out_cols, out_len, as_stream(stream));
+}

@@ -1,0 +1,290 @@
+// plgpu_internal.hpp — shared internals of the gfx950 executor backend.
+//
+// Device side: Arrow column access, polars TotalOrd comparisons, the typed
+// row interpreter for lowered expression programs, orderable encodings and
+// the exact fixed-point representation used by f64 sums.
+// Host side: error plumbing, the stream-ordered allocator, program lowering.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "../../include/polaroid_gpu.h"
+
+#define PLGPU_API extern "C" __attribute__((visibility("default")))
+
+namespace plgpu {
+
+// ------------------------------------------------------------------ host
+void set_error(const std::string& msg);
+int fail(int code, const std::string& msg);
+int hip_fail(hipError_t e, const char* what);
+
+#define PLGPU_HIP(expr)                                   \
+    do {                                                  \
+        hipError_t _e = (expr);                           \
+        if (_e != hipSuccess) return plgpu::hip_fail(_e, #expr); \
+    } while (0)
+
+hipStream_t as_stream(void* s);
+int dev_alloc(void** p, size_t bytes, hipStream_t s);
+void dev_free(void* p, hipStream_t s);
+
+// A library-owned device column buffer set (released via plgpu_column.release).
+struct OwnedBuffers {
+    void* values = nullptr;
+    void* validity = nullptr;
+    hipStream_t stream = nullptr;
+};
+// Fill `out` as an owning column over freshly allocated buffers.
+int make_owned_column(plgpu_column* out, int32_t dtype, int64_t length, bool with_validity,
+                      hipStream_t s);
+
+inline int dtype_bytes(int32_t dt) {
+    switch (dt) {
+    case PLGPU_I32:
+    case PLGPU_U32: return 4;
+    case PLGPU_I64:
+    case PLGPU_F64: return 8;
+    default: return 0;  // BOOL is bit-packed
+    }
+}
+
+// --------------------------------------------------------- device columns
+struct DevCol {
+    const void* values;
+    const uint8_t* validity;
+    int64_t offset;
+    int32_t dtype;
+    int32_t _pad;
+};
+
+// Lowered (typed) program: the host resolves every operand type, inserts
+// casts, and emits one micro-op per step so the device interpreter does no
+// type dispatch of its own.
+enum DevOp : int32_t {
+    D_COL_F64 = 1, D_COL_I64, D_COL_I32, D_COL_U32, D_COL_BOOL,
+    D_LIT, D_NULL,
+    D_ADD_I, D_SUB_I, D_MUL_I, D_NEG_I, D_ABS_I,
+    D_ADD_F, D_SUB_F, D_MUL_F, D_DIV_F, D_NEG_F, D_ABS_F,
+    D_I2F_0, D_I2F_1,  // cast top / second-from-top i64 -> f64
+    D_EQ_F, D_NE_F, D_LT_F, D_LE_F, D_GT_F, D_GE_F,
+    D_EQ_I, D_NE_I, D_LT_I, D_LE_I, D_GT_I, D_GE_I,
+    D_EQM_F, D_NEM_F, D_EQM_I, D_NEM_I, D_EQM_B, D_NEM_B,
+    D_EQ_B, D_NE_B,
+    D_AND, D_OR, D_NOT, D_ISNULL, D_ISNOTNULL, D_ISNAN_F, D_ISFINITE_F, D_FALSE_VALID
+};
+
+struct DevInstr {
+    int32_t op;
+    int32_t arg;
+    uint64_t imm;
+};
+
+struct DevProgram {
+    DevInstr code[PLGPU_MAX_PROGRAM];
+    int32_t n;
+    int32_t out_dtype;  // PLGPU_BOOL / PLGPU_I64 / PLGPU_F64
+    // Fast path: program is exactly `col(c) <cmp> literal` (c numeric).
+    int32_t simple;     // 0 = no, 1 = yes
+    int32_t simple_col;
+    int32_t simple_op;  // D_*_F or D_*_I compare op
+    int32_t simple_isf; // compare in f64
+    uint64_t simple_imm;
+};
+
+// Type-check and lower a user program over `cols`.  Returns PLGPU_OK or an
+// error code (message set).
+int lower_program(const plgpu_column* cols, int32_t ncols, const plgpu_instr* prog, int32_t n,
+                  DevProgram* out);
+
+// ------------------------------------------------------------ device code
+constexpr uint64_t kEmptyKey = 0x8000000000000000ull;  // INT64_MIN sentinel
+
+__device__ __forceinline__ double as_f64(uint64_t b) { return __longlong_as_double((long long)b); }
+__device__ __forceinline__ uint64_t f64_bits(double d) { return (uint64_t)__double_as_longlong(d); }
+
+__device__ __forceinline__ bool dev_valid(const DevCol& c, int64_t r) {
+    if (c.validity == nullptr) return true;
+    int64_t p = c.offset + r;
+    return (c.validity[p >> 3] >> (p & 7)) & 1;
+}
+
+// Raw 64-bit payload of column c at row r (ints sign/zero-extended, bool as 0/1).
+__device__ __forceinline__ uint64_t dev_load(const DevCol& c, int64_t r) {
+    int64_t p = c.offset + r;
+    switch (c.dtype) {
+    case PLGPU_F64:
+    case PLGPU_I64: return ((const uint64_t*)c.values)[p];
+    case PLGPU_I32: return (uint64_t)(int64_t)((const int32_t*)c.values)[p];
+    case PLGPU_U32: return (uint64_t)((const uint32_t*)c.values)[p];
+    default: return (((const uint8_t*)c.values)[p >> 3] >> (p & 7)) & 1;
+    }
+}
+
+// polars-utils/src/total_ord.rs:317-368 for f64: NaN == NaN, NaN greatest.
+__device__ __forceinline__ bool tot_ge_f(double a, double b) { return __builtin_isnan(a) | (a >= b); }
+__device__ __forceinline__ bool tot_eq_f(double a, double b) {
+    return __builtin_isnan(a) ? __builtin_isnan(b) : (a == b);
+}
+// op encoded as 0..5 = eq, ne, lt, le, gt, ge
+__device__ __forceinline__ bool cmp_f(int op, double a, double b) {
+    switch (op) {
+    case 0: return tot_eq_f(a, b);
+    case 1: return !tot_eq_f(a, b);
+    case 2: return !tot_ge_f(a, b);
+    case 3: return tot_ge_f(b, a);
+    case 4: return !tot_ge_f(b, a);
+    default: return tot_ge_f(a, b);
+    }
+}
+__device__ __forceinline__ bool cmp_i(int op, int64_t a, int64_t b) {
+    switch (op) {
+    case 0: return a == b;
+    case 1: return a != b;
+    case 2: return a < b;
+    case 3: return a <= b;
+    case 4: return a > b;
+    default: return a >= b;
+    }
+}
+
+// Evaluate a lowered program for one row.  The stack lives in eight named
+// registers shifted by static moves (no runtime-indexed arrays -> no
+// scratch); the validity of stack entry j is bit j of `vm`.
+struct RowVal {
+    uint64_t v;
+    bool valid;
+};
+
+__device__ __forceinline__ RowVal eval_row(const DevInstr* __restrict__ code, int n, const DevCol* cols,
+                                           int64_t r) {
+    uint64_t s0 = 0, s1 = 0, s2 = 0, s3 = 0, s4 = 0, s5 = 0, s6 = 0, s7 = 0;
+    uint32_t vm = 0;
+#define PUSH(x, ok)                                                        \
+    do {                                                                   \
+        s7 = s6; s6 = s5; s5 = s4; s4 = s3; s3 = s2; s2 = s1; s1 = s0;     \
+        s0 = (x);                                                          \
+        vm = (vm << 1) | ((ok) ? 1u : 0u);                                 \
+    } while (0)
+#define POP1()                                                             \
+    do {                                                                   \
+        s0 = s1; s1 = s2; s2 = s3; s3 = s4; s4 = s5; s5 = s6; s6 = s7;     \
+        vm >>= 1;                                                          \
+    } while (0)
+    for (int k = 0; k < n; ++k) {
+        const int op = code[k].op;
+        const int arg = code[k].arg;
+        const uint64_t imm = code[k].imm;
+        switch (op) {
+        case D_COL_F64:
+        case D_COL_I64:
+        case D_COL_I32:
+        case D_COL_U32:
+        case D_COL_BOOL: {
+            const DevCol& c = cols[arg];
+            bool ok = dev_valid(c, r);
+            uint64_t x = dev_load(c, r);
+            PUSH(x, ok);
+            break;
+        }
+        case D_LIT: PUSH(imm, true); break;
+        case D_NULL: PUSH(0ull, false); break;
+        case D_NEG_I: s0 = 0ull - s0; break;
+        case D_ABS_I: s0 = ((int64_t)s0 < 0) ? 0ull - s0 : s0; break;
+        case D_NEG_F: s0 ^= 0x8000000000000000ull; break;
+        case D_ABS_F: s0 &= 0x7fffffffffffffffull; break;
+        case D_I2F_0: s0 = f64_bits((double)(int64_t)s0); break;
+        case D_I2F_1: s1 = f64_bits((double)(int64_t)s1); break;
+        case D_NOT: s0 = s0 ^ 1ull; break;
+        case D_ISNULL: s0 = (vm & 1u) ? 0ull : 1ull; vm |= 1u; break;
+        case D_ISNOTNULL: s0 = (vm & 1u) ? 1ull : 0ull; vm |= 1u; break;
+        case D_ISNAN_F: s0 = __builtin_isnan(as_f64(s0)) ? 1ull : 0ull; break;
+        case D_ISFINITE_F: s0 = __builtin_isfinite(as_f64(s0)) ? 1ull : 0ull; break;
+        case D_FALSE_VALID: s0 = 0ull; vm |= 1u; break;
+        default: {
+            // binary: a = s1, b = s0
+            const uint64_t a = s1, b = s0;
+            const bool va = (vm >> 1) & 1u, vb = vm & 1u;
+            uint64_t res = 0;
+            bool ok = va & vb;
+            switch (op) {
+            case D_ADD_I: res = a + b; break;
+            case D_SUB_I: res = a - b; break;
+            case D_MUL_I: res = a * b; break;
+            case D_ADD_F: res = f64_bits(as_f64(a) + as_f64(b)); break;
+            case D_SUB_F: res = f64_bits(as_f64(a) - as_f64(b)); break;
+            case D_MUL_F: res = f64_bits(as_f64(a) * as_f64(b)); break;
+            case D_DIV_F: res = f64_bits(as_f64(a) / as_f64(b)); break;
+            case D_EQ_F: case D_NE_F: case D_LT_F: case D_LE_F: case D_GT_F: case D_GE_F:
+                res = cmp_f(op - D_EQ_F, as_f64(a), as_f64(b)) ? 1ull : 0ull;
+                break;
+            case D_EQ_I: case D_NE_I: case D_LT_I: case D_LE_I: case D_GT_I: case D_GE_I:
+                res = cmp_i(op - D_EQ_I, (int64_t)a, (int64_t)b) ? 1ull : 0ull;
+                break;
+            case D_EQ_B: res = (a == b) ? 1ull : 0ull; break;
+            case D_NE_B: res = (a != b) ? 1ull : 0ull; break;
+            case D_EQM_F: case D_NEM_F: case D_EQM_I: case D_NEM_I: case D_EQM_B: case D_NEM_B: {
+                bool eq;
+                if (va & vb) {
+                    eq = (op == D_EQM_F || op == D_NEM_F) ? tot_eq_f(as_f64(a), as_f64(b)) : (a == b);
+                } else {
+                    eq = !va && !vb;
+                }
+                bool ne_op = (op == D_NEM_F || op == D_NEM_I || op == D_NEM_B);
+                res = (ne_op ? !eq : eq) ? 1ull : 0ull;
+                ok = true;
+                break;
+            }
+            case D_AND: {
+                // Kleene: false dominates nulls.
+                bool fa = va && !(a & 1), fb = vb && !(b & 1);
+                if (fa || fb) { res = 0; ok = true; }
+                else { res = 1; ok = va & vb; }
+                break;
+            }
+            case D_OR: {
+                bool ta = va && (a & 1), tb = vb && (b & 1);
+                if (ta || tb) { res = 1; ok = true; }
+                else { res = 0; ok = va & vb; }
+                break;
+            }
+            default: break;
+            }
+            POP1();
+            s0 = res;
+            vm = (vm & ~1u) | (ok ? 1u : 0u);
+            break;
+        }
+        }
+    }
+#undef PUSH
+#undef POP1
+    (void)s7;
+    return RowVal{s0, (vm & 1u) != 0};
+}
+
+// Fast-path predicate `col <cmp> imm`, null -> false.
+__device__ __forceinline__ bool simple_pred(bool isf, int op, uint64_t x, uint64_t imm) {
+    return isf ? cmp_f(op, as_f64(x), as_f64(imm)) : cmp_i(op, (int64_t)x, (int64_t)imm);
+}
+
+// Fibonacci hashing of a 64-bit key into `bits` bits.
+__device__ __forceinline__ uint32_t hash_slot(uint64_t key, int bits) {
+    return bits == 0 ? 0u : (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - bits));
+}
+
+// Orderable unsigned encodings: unsigned compare == total order.
+__device__ __forceinline__ uint64_t ord_f64(uint64_t b) {
+    return (b & 0x8000000000000000ull) ? ~b : (b | 0x8000000000000000ull);
+}
+__device__ __forceinline__ uint64_t unord_f64(uint64_t u) {
+    return (u & 0x8000000000000000ull) ? (u & 0x7fffffffffffffffull) : ~u;
+}
+__device__ __forceinline__ uint64_t ord_i64(uint64_t b) { return b ^ 0x8000000000000000ull; }
+
+inline int wave_size() { return 64; }
+
+}  // namespace plgpu

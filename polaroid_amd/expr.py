@@ -1,0 +1,267 @@
+"""Expression DSL mirroring py-polars' `pl.col` / `pl.lit` / Expr API for the
+filter -> arithmetic/comparison -> group_by-agg path.
+
+An Expr is lowered to the postfix program of include/polaroid_gpu.h
+(`plgpu_instr`), which the native library type-checks and runs per row on
+the GPU (reference: polars-expr/src/expressions/{column,literal,binary}.rs).
+"""
+
+from __future__ import annotations
+
+import builtins
+from typing import Any, Sequence
+
+from . import _native as N
+
+_AGG_KINDS = ("sum", "mean", "min", "max", "count", "len")
+
+
+class Expr:
+    """A node of the expression tree."""
+
+    __slots__ = ("kind", "args", "op", "value", "_name")
+
+    def __init__(self, kind: str, args: Sequence["Expr"] = (), op: str | None = None,
+                 value: Any = None, name: str | None = None):
+        self.kind = kind          # col | lit | bin | un | agg | alias | len
+        self.args = tuple(args)
+        self.op = op
+        self.value = value
+        self._name = name
+
+    # ---------------------------------------------------------- naming
+    def output_name(self) -> str:
+        if self.kind == "alias":
+            return self.value
+        if self.kind == "col":
+            return self.value
+        if self.kind == "len":
+            return "len"
+        if self.kind == "lit":
+            return "literal"
+        return self.args[0].output_name()
+
+    def meta_root_names(self) -> list[str]:
+        if self.kind == "col":
+            return [self.value]
+        out: list[str] = []
+        for a in self.args:
+            for n in a.meta_root_names():
+                if n not in out:
+                    out.append(n)
+        return out
+
+    def __repr__(self) -> str:
+        if self.kind == "col":
+            return f'col("{self.value}")'
+        if self.kind == "lit":
+            return f"lit({self.value!r})"
+        if self.kind == "bin":
+            return f"[({self.args[0]!r}) {self.op} ({self.args[1]!r})]"
+        if self.kind == "alias":
+            return f'{self.args[0]!r}.alias("{self.value}")'
+        if self.kind == "len":
+            return "len()"
+        return f"{self.args[0]!r}.{self.op}()"
+
+    def __bool__(self):
+        raise TypeError("the truth value of an Expr is ambiguous")
+
+    # -------------------------------------------------------- operators
+    def _bin(self, op: str, other: Any, swap: bool = False) -> "Expr":
+        o = _to_expr(other)
+        return Expr("bin", (o, self) if swap else (self, o), op=op)
+
+    def __add__(self, o): return self._bin("+", o)
+    def __radd__(self, o): return self._bin("+", o, True)
+    def __sub__(self, o): return self._bin("-", o)
+    def __rsub__(self, o): return self._bin("-", o, True)
+    def __mul__(self, o): return self._bin("*", o)
+    def __rmul__(self, o): return self._bin("*", o, True)
+    def __truediv__(self, o): return self._bin("/", o)
+    def __rtruediv__(self, o): return self._bin("/", o, True)
+    def __gt__(self, o): return self._bin(">", o)
+    def __ge__(self, o): return self._bin(">=", o)
+    def __lt__(self, o): return self._bin("<", o)
+    def __le__(self, o): return self._bin("<=", o)
+    def __eq__(self, o): return self._bin("==", o)  # type: ignore[override]
+    def __ne__(self, o): return self._bin("!=", o)  # type: ignore[override]
+    def __and__(self, o): return self._bin("&", o)
+    def __rand__(self, o): return self._bin("&", o, True)
+    def __or__(self, o): return self._bin("|", o)
+    def __ror__(self, o): return self._bin("|", o, True)
+    def __neg__(self): return Expr("un", (self,), op="neg")
+    def __abs__(self): return Expr("un", (self,), op="abs")
+    def __invert__(self): return Expr("un", (self,), op="not")
+    __hash__ = object.__hash__
+
+    def gt(self, o): return self._bin(">", o)
+    def ge(self, o): return self._bin(">=", o)
+    def lt(self, o): return self._bin("<", o)
+    def le(self, o): return self._bin("<=", o)
+    def eq(self, o): return self._bin("==", o)
+    def ne(self, o): return self._bin("!=", o)
+    def eq_missing(self, o): return self._bin("eq_missing", o)
+    def ne_missing(self, o): return self._bin("ne_missing", o)
+    def add(self, o): return self._bin("+", o)
+    def sub(self, o): return self._bin("-", o)
+    def mul(self, o): return self._bin("*", o)
+    def truediv(self, o): return self._bin("/", o)
+    def and_(self, o): return self._bin("&", o)
+    def or_(self, o): return self._bin("|", o)
+    def not_(self): return Expr("un", (self,), op="not")
+    def abs(self): return Expr("un", (self,), op="abs")
+    def is_null(self): return Expr("un", (self,), op="is_null")
+    def is_not_null(self): return Expr("un", (self,), op="is_not_null")
+    def is_nan(self): return Expr("un", (self,), op="is_nan")
+    def is_finite(self): return Expr("un", (self,), op="is_finite")
+
+    def cast(self, dtype) -> "Expr":
+        from .frame import Float64
+        if dtype is Float64 or dtype == "f64":
+            return Expr("un", (self,), op="cast_f64")
+        raise N.InvalidOperationError(f"cast to {dtype} is not supported on the GPU executor")
+
+    def alias(self, name: str) -> "Expr":
+        return Expr("alias", (self,), value=name)
+
+    # ----------------------------------------------------- aggregations
+    def sum(self): return Expr("agg", (self,), op="sum")
+    def mean(self): return Expr("agg", (self,), op="mean")
+    def min(self): return Expr("agg", (self,), op="min")
+    def max(self): return Expr("agg", (self,), op="max")
+    def count(self): return Expr("agg", (self,), op="count")
+    def len(self): return Expr("agg", (self,), op="len")
+
+
+def _to_expr(v: Any) -> Expr:
+    return v if isinstance(v, Expr) else lit(v)
+
+
+def col(name: str) -> Expr:
+    return Expr("col", value=name)
+
+
+def lit(value: Any) -> Expr:
+    if isinstance(value, Expr):
+        return value
+    return Expr("lit", value=value)
+
+
+def len() -> Expr:  # noqa: A001 - mirrors pl.len()
+    return Expr("len")
+
+
+def sum(name: str) -> Expr:  # noqa: A001
+    return col(name).sum()
+
+
+def mean(name: str) -> Expr:
+    return col(name).mean()
+
+
+def min(name: str) -> Expr:  # noqa: A001
+    return col(name).min()
+
+
+def max(name: str) -> Expr:  # noqa: A001
+    return col(name).max()
+
+
+def count(name: str) -> Expr:
+    return col(name).count()
+
+
+_BIN_OPS = {
+    "+": "ADD", "-": "SUB", "*": "MUL", "/": "TRUEDIV",
+    ">": "GT", ">=": "GE", "<": "LT", "<=": "LE", "==": "EQ", "!=": "NE",
+    "eq_missing": "EQ_MISSING", "ne_missing": "NE_MISSING", "&": "AND", "|": "OR",
+}
+_UN_OPS = {
+    "neg": "NEG", "abs": "ABS", "not": "NOT", "is_null": "IS_NULL",
+    "is_not_null": "IS_NOT_NULL", "is_nan": "IS_NAN", "is_finite": "IS_FINITE",
+    "cast_f64": "CAST_F64",
+}
+
+
+def lower(expr: Expr, col_index: dict[str, int], schema: dict[str, int]) -> list[tuple[int, int, Any]]:
+    """Lower an (aggregation-free) Expr to a postfix program.
+
+    Returns a list of (opcode, arg, imm) triples; `imm` is a float for
+    LIT_F64 and an int otherwise.
+    """
+    out: list[tuple[int, int, Any]] = []
+
+    def dtype_of(e: Expr) -> int | None:
+        if e.kind == "col":
+            return schema.get(e.value)
+        if e.kind == "lit":
+            v = e.value
+            if isinstance(v, bool):
+                return N.BOOL
+            if isinstance(v, int):
+                return N.I64
+            if isinstance(v, float):
+                return N.F64
+            return None
+        if e.kind == "alias":
+            return dtype_of(e.args[0])
+        if e.kind == "bin":
+            if e.op in ("+", "-", "*"):
+                a, b = dtype_of(e.args[0]), dtype_of(e.args[1])
+                return N.F64 if N.F64 in (a, b) else (a or b)
+            return N.F64 if e.op == "/" else N.BOOL
+        return None
+
+    def emit(e: Expr, hint: int | None = None) -> None:
+        k = e.kind
+        if k == "alias":
+            emit(e.args[0], hint)
+        elif k == "col":
+            if e.value not in col_index:
+                raise N.ComputeError(f'unable to find column "{e.value}"')
+            out.append((N.OP["COL"], col_index[e.value], 0))
+        elif k == "lit":
+            v = e.value
+            if v is None:
+                dt = hint if hint in (N.F64, N.I64, N.BOOL) else N.I64
+                out.append((N.OP["LIT_NULL"], dt, 0))
+            elif isinstance(v, bool):
+                out.append((N.OP["LIT_BOOL"], 0, int(v)))
+            elif isinstance(v, int):
+                if not -(2 ** 63) <= v < 2 ** 63:
+                    raise N.InvalidOperationError(f"integer literal {v} does not fit Int64")
+                out.append((N.OP["LIT_I64"], 0, v))
+            elif isinstance(v, float):
+                out.append((N.OP["LIT_F64"], 0, float(v)))
+            else:
+                raise N.InvalidOperationError(f"literal of type {type(v).__name__} is not supported")
+        elif k == "bin":
+            a, b = e.args
+            emit(a, dtype_of(b))
+            emit(b, dtype_of(a))
+            out.append((N.OP[_BIN_OPS[e.op]], 0, 0))
+        elif k == "un":
+            emit(e.args[0])
+            out.append((N.OP[_UN_OPS[e.op]], 0, 0))
+        elif k in ("agg", "len"):
+            raise N.InvalidOperationError(f"aggregation {e!r} is not allowed in this context")
+        else:
+            raise N.InvalidOperationError(f"unsupported expression {e!r}")
+
+    emit(expr)
+    if not out:
+        raise N.InvalidOperationError("empty expression")
+    return out
+
+
+def to_instr_array(prog: list[tuple[int, int, Any]]):
+    arr = (N.Instr * builtins.len(prog))()
+    for i, (op, arg, imm) in enumerate(prog):
+        arr[i].op = op
+        arr[i].arg = arg
+        if op == N.OP["LIT_F64"]:
+            arr[i].imm.f64 = float(imm)
+        else:
+            arr[i].imm.i64 = int(imm)
+    return arr

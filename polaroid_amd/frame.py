@@ -1,0 +1,613 @@
+"""Series / DataFrame / LazyFrame mirroring py-polars' API over device columns.
+
+Columns live in HBM as Arrow arrays (values buffer + LSB-first validity
+bitmap).  `LazyFrame.collect()` plans the query the way polars-mem-engine
+builds executors (polars-mem-engine/src/planner/lp.rs) and runs every node
+through the C-ABI of libpolaroid_gpu.so; a Filter directly below a GroupBy
+is pushed into the aggregation kernel (one pass over the data).
+"""
+
+from __future__ import annotations
+
+import builtins
+import ctypes as C
+from typing import Any, Iterable, Sequence
+
+import numpy as np
+
+from . import _native as N
+from .expr import Expr, col, lower, to_instr_array
+
+
+# ------------------------------------------------------------------ dtypes
+class DataType:
+    code = 0
+    name = "?"
+    np_dtype: Any = None
+
+    def __repr__(self):
+        return self.name
+
+
+class _Int64(DataType):
+    code, name, np_dtype = N.I64, "Int64", np.int64
+
+
+class _Int32(DataType):
+    code, name, np_dtype = N.I32, "Int32", np.int32
+
+
+class _UInt32(DataType):
+    code, name, np_dtype = N.U32, "UInt32", np.uint32
+
+
+class _Float64(DataType):
+    code, name, np_dtype = N.F64, "Float64", np.float64
+
+
+class _Boolean(DataType):
+    code, name, np_dtype = N.BOOL, "Boolean", np.bool_
+
+
+Int64, Int32, UInt32, Float64, Boolean = _Int64(), _Int32(), _UInt32(), _Float64(), _Boolean()
+_BY_CODE = {d.code: d for d in (Int64, Int32, UInt32, Float64, Boolean)}
+
+
+def _dtype_from_numpy(a: np.ndarray) -> DataType:
+    k = a.dtype
+    if k == np.bool_:
+        return Boolean
+    if k == np.int64:
+        return Int64
+    if k == np.int32:
+        return Int32
+    if k == np.uint32:
+        return UInt32
+    if k == np.float64:
+        return Float64
+    if np.issubdtype(k, np.integer):
+        return Int64
+    if np.issubdtype(k, np.floating):
+        return Float64
+    raise N.InvalidOperationError(f"unsupported numpy dtype {k}")
+
+
+def _pack_bits(mask: np.ndarray) -> np.ndarray:
+    """bool array -> Arrow LSB-first bitmap padded to 8-byte words."""
+    n = mask.shape[0]
+    words = (n + 63) // 64
+    packed = np.packbits(mask.astype(np.uint8), bitorder="little")
+    out = np.zeros(words * 8, dtype=np.uint8)
+    out[: packed.shape[0]] = packed
+    return out
+
+
+def _unpack_bits(buf: np.ndarray, offset: int, n: int) -> np.ndarray:
+    bits = np.unpackbits(buf, bitorder="little")
+    return bits[offset: offset + n].astype(bool)
+
+
+class _Owned:
+    """Keeps a library-produced column alive; releases it once."""
+
+    __slots__ = ("col",)
+
+    def __init__(self, col: N.Column):
+        self.col = col
+
+    def __del__(self):
+        if self.col is not None and self.col.release and N._lib is not None:
+            N._lib.plgpu_column_release(C.byref(self.col))
+            self.col = None
+
+
+# ------------------------------------------------------------------ Series
+class Series:
+    """A named Arrow array in device memory."""
+
+    __slots__ = ("name", "_col", "_keep")
+
+    def __init__(self, name: str = "", values: Any = None, dtype: DataType | None = None):
+        self.name = name
+        self._keep: list = []
+        if values is None:
+            values = []
+        if isinstance(values, Series):
+            self._col, self._keep = values._col, values._keep
+            return
+        validity = None
+        if isinstance(values, np.ndarray):
+            arr = values
+        else:
+            vals = list(values)
+            validity = np.array([v is not None for v in vals], dtype=bool)
+            if dtype is None:
+                nonnull = [v for v in vals if v is not None]
+                if any(isinstance(v, float) for v in nonnull):
+                    dtype = Float64
+                elif nonnull and builtins.all(isinstance(v, bool) for v in nonnull):
+                    dtype = Boolean
+                else:
+                    dtype = Int64
+            fill = False if dtype is Boolean else 0
+            arr = np.array([fill if v is None else v for v in vals], dtype=dtype.np_dtype)
+            if validity.all():
+                validity = None
+        if dtype is not None and arr.dtype != dtype.np_dtype:
+            arr = arr.astype(dtype.np_dtype)
+        dt = dtype or _dtype_from_numpy(arr)
+        self._upload(np.ascontiguousarray(arr), dt, validity)
+
+    # construction helpers -------------------------------------------------
+    def _upload(self, arr: np.ndarray, dt: DataType, validity: np.ndarray | None) -> None:
+        n = int(arr.shape[0])
+        col_ = N.Column()
+        col_.dtype = dt.code
+        col_.length = n
+        col_.offset = 0
+        col_.null_count = 0 if validity is None else int((~validity).sum())
+        if dt is Boolean:
+            payload = _pack_bits(arr.astype(bool))
+        else:
+            payload = arr
+        vbuf = N.DeviceBuffer(payload.nbytes)
+        if payload.nbytes:
+            N.check(N.lib().plgpu_memcpy_h2d(C.c_void_p(vbuf.ptr), payload.ctypes.data_as(C.c_void_p),
+                                             payload.nbytes, None))
+        col_.values = vbuf.ptr
+        self._keep = [vbuf]
+        if validity is not None:
+            bits = _pack_bits(validity)
+            mbuf = N.DeviceBuffer(bits.nbytes)
+            N.check(N.lib().plgpu_memcpy_h2d(C.c_void_p(mbuf.ptr), bits.ctypes.data_as(C.c_void_p),
+                                             bits.nbytes, None))
+            col_.validity = mbuf.ptr
+            self._keep.append(mbuf)
+        self._col = col_
+
+    @classmethod
+    def from_numpy(cls, name: str, values: np.ndarray, valid: np.ndarray | None = None,
+                   dtype: DataType | None = None) -> "Series":
+        """Upload a numpy array (plus optional boolean validity) to the device."""
+        s = cls.__new__(cls)
+        s.name = name
+        arr = np.ascontiguousarray(values)
+        dt = dtype or _dtype_from_numpy(arr)
+        if arr.dtype != dt.np_dtype:
+            arr = arr.astype(dt.np_dtype)
+        s._upload(arr, dt, None if valid is None else np.asarray(valid, dtype=bool))
+        return s
+
+    def slice(self, offset: int, length: int | None = None) -> "Series":
+        """Zero-copy slice (Arrow offset semantics), like Series.slice."""
+        n = self.len()
+        offset = max(0, min(int(offset), n))
+        length = n - offset if length is None else max(0, min(int(length), n - offset))
+        s = Series.__new__(Series)
+        s.name = self.name
+        c = N.Column.from_buffer_copy(self._col)
+        c.offset = self._col.offset + offset
+        c.length = length
+        c.release = None
+        c.private_data = None
+        c.null_count = -1 if self._col.validity else 0
+        s._col = c
+        s._keep = [self]
+        return s
+
+    @classmethod
+    def _from_native(cls, name: str, col_: N.Column) -> "Series":
+        s = cls.__new__(cls)
+        s.name = name
+        s._col = col_
+        s._keep = [_Owned(col_)] if col_.release else []
+        return s
+
+    @classmethod
+    def from_device(cls, name: str, dtype: DataType, values_ptr: int, length: int,
+                    validity_ptr: int | None = None, offset: int = 0, keepalive: Any = None,
+                    null_count: int = -1) -> "Series":
+        """Borrow existing device buffers (e.g. torch tensors) without copying."""
+        s = cls.__new__(cls)
+        s.name = name
+        c = N.Column()
+        c.dtype = dtype.code
+        c.length = int(length)
+        c.offset = int(offset)
+        c.null_count = 0 if validity_ptr is None else int(null_count)
+        c.values = int(values_ptr)
+        c.validity = int(validity_ptr) if validity_ptr else None
+        s._col = c
+        s._keep = [keepalive] if keepalive is not None else []
+        return s
+
+    @classmethod
+    def from_torch(cls, name: str, tensor, validity=None) -> "Series":
+        import torch
+
+        m = {torch.int64: Int64, torch.int32: Int32, torch.float64: Float64}
+        if tensor.dtype not in m or not tensor.is_cuda or not tensor.is_contiguous():
+            raise N.InvalidOperationError("from_torch needs a contiguous int64/int32/float64 GPU tensor")
+        vptr = validity.data_ptr() if validity is not None else None
+        return cls.from_device(name, m[tensor.dtype], tensor.data_ptr(), tensor.numel(), vptr,
+                               keepalive=(tensor, validity))
+
+    # properties -----------------------------------------------------------
+    @property
+    def dtype(self) -> DataType:
+        return _BY_CODE[self._col.dtype]
+
+    def len(self) -> int:
+        return int(self._col.length)
+
+    def __len__(self) -> int:
+        return self.len()
+
+    def alias(self, name: str) -> "Series":
+        s = Series.__new__(Series)
+        s.name, s._col, s._keep = name, self._col, self._keep
+        return s
+
+    # host materialisation (tests / display only) --------------------------
+    def _download(self, ptr, nbytes) -> np.ndarray:
+        out = np.empty(nbytes, dtype=np.uint8)
+        if nbytes:
+            N.check(N.lib().plgpu_memcpy_d2h(out.ctypes.data_as(C.c_void_p), C.c_void_p(ptr), nbytes, None))
+        return out
+
+    def validity_numpy(self) -> np.ndarray:
+        n, off = self.len(), int(self._col.offset)
+        if not self._col.validity:
+            return np.ones(n, dtype=bool)
+        nb = (off + n + 7) // 8
+        return _unpack_bits(self._download(self._col.validity, nb), off, n)
+
+    def to_numpy(self) -> np.ndarray:
+        """Values as numpy (null slots hold whatever the buffer holds)."""
+        n, off = self.len(), int(self._col.offset)
+        dt = self.dtype
+        if dt is Boolean:
+            nb = (off + n + 7) // 8
+            return _unpack_bits(self._download(self._col.values, nb), off, n)
+        eb = np.dtype(dt.np_dtype).itemsize
+        raw = self._download(self._col.values + off * eb if self._col.values else 0, n * eb)
+        return raw.view(dt.np_dtype).copy()
+
+    def to_list(self) -> list:
+        vals = self.to_numpy().tolist()
+        valid = self.validity_numpy()
+        return [v if ok else None for v, ok in zip(vals, valid)]
+
+    def null_count(self) -> int:
+        return int((~self.validity_numpy()).sum())
+
+    def __repr__(self) -> str:
+        return f"shape: ({self.len()},)\nSeries: '{self.name}' [{self.dtype}]\n{self.to_list()[:20]}"
+
+    # eager conveniences mirroring Series.filter ------------------------------
+    def filter(self, mask: "Series") -> "Series":
+        out = (N.Column * 1)()
+        n = C.c_int64(0)
+        cols = (N.Column * 1)(self._col)
+        m = mask._col
+        N.check(N.lib().plgpu_filter(cols, 1, C.byref(m), out, C.byref(n), None))
+        return Series._from_native(self.name, out[0])
+
+
+# --------------------------------------------------------------- DataFrame
+class DataFrame:
+    def __init__(self, data: Any = None, schema: Any = None):
+        self._cols: dict[str, Series] = {}
+        if data is None:
+            data = {}
+        if isinstance(data, dict):
+            for name, v in data.items():
+                dt = None
+                if isinstance(schema, dict) and name in schema:
+                    dt = schema[name]
+                s = v.alias(name) if isinstance(v, Series) else Series(name, v, dt)
+                self._cols[name] = s
+        elif isinstance(data, (list, tuple)) and builtins.all(isinstance(s, Series) for s in data):
+            for s in data:
+                self._cols[s.name] = s
+        else:
+            raise N.InvalidOperationError("DataFrame expects a dict of columns or a list of Series")
+        h = {s.len() for s in self._cols.values()}
+        if builtins.len(h) > 1:
+            raise N.ShapeError("could not create a new DataFrame: lengths don't match")
+
+    @property
+    def columns(self) -> list[str]:
+        return list(self._cols)
+
+    @property
+    def height(self) -> int:
+        return next(iter(self._cols.values())).len() if self._cols else 0
+
+    @property
+    def width(self) -> int:
+        return builtins.len(self._cols)
+
+    @property
+    def schema(self) -> dict[str, DataType]:
+        return {k: s.dtype for k, s in self._cols.items()}
+
+    @property
+    def shape(self) -> tuple[int, int]:
+        return (self.height, self.width)
+
+    def __getitem__(self, name: str) -> Series:
+        return self._cols[name]
+
+    def get_column(self, name: str) -> Series:
+        return self._cols[name]
+
+    def is_empty(self) -> bool:
+        return self.height == 0
+
+    def to_dict(self, as_series: bool = True) -> dict:
+        if as_series:
+            return dict(self._cols)
+        return {k: s.to_list() for k, s in self._cols.items()}
+
+    def rows(self) -> list[tuple]:
+        cols = [s.to_list() for s in self._cols.values()]
+        return list(zip(*cols)) if cols else []
+
+    def lazy(self) -> "LazyFrame":
+        return LazyFrame(("scan", self))
+
+    def filter(self, *predicates: Expr, **constraints: Any) -> "DataFrame":
+        return self.lazy().filter(*predicates, **constraints).collect()
+
+    def group_by(self, *by: Any, maintain_order: bool = False) -> "GroupBy":
+        return GroupBy(self.lazy(), by, maintain_order)
+
+    def select(self, *exprs: Any) -> "DataFrame":
+        return self.lazy().select(*exprs).collect()
+
+    def with_columns(self, *exprs: Any) -> "DataFrame":
+        return self.lazy().with_columns(*exprs).collect()
+
+    def __repr__(self) -> str:
+        return f"DataFrame(shape={self.shape}, schema={self.schema})"
+
+
+# --------------------------------------------------------------- LazyFrame
+def _parse_exprs(items: Sequence[Any]) -> list[Expr]:
+    out: list[Expr] = []
+    for it in items:
+        if isinstance(it, (list, tuple)):
+            out.extend(_parse_exprs(it))
+        elif isinstance(it, str):
+            out.append(col(it))
+        elif isinstance(it, Expr):
+            out.append(it)
+        else:
+            raise N.InvalidOperationError(f"cannot interpret {it!r} as an expression")
+    return out
+
+
+def _combine_predicates(preds: Sequence[Expr], constraints: dict) -> Expr:
+    ps = list(_parse_exprs(preds)) + [col(k) == v for k, v in constraints.items()]
+    if not ps:
+        raise N.InvalidOperationError("filter needs at least one predicate")
+    p = ps[0]
+    for q in ps[1:]:
+        p = p & q
+    return p
+
+
+class LazyFrame:
+    """A logical plan: ('scan', df) | ('filter', input, pred) | ('group_by', input,
+    keys, aggs, maintain_order) | ('select' / 'with_columns', input, exprs)."""
+
+    def __init__(self, node: tuple):
+        self._node = node
+
+    def filter(self, *predicates: Expr, **constraints: Any) -> "LazyFrame":
+        return LazyFrame(("filter", self._node, _combine_predicates(predicates, constraints)))
+
+    def group_by(self, *by: Any, maintain_order: bool = False) -> "LazyGroupBy":
+        return LazyGroupBy(self, by, maintain_order)
+
+    def select(self, *exprs: Any) -> "LazyFrame":
+        return LazyFrame(("select", self._node, _parse_exprs(exprs)))
+
+    def with_columns(self, *exprs: Any) -> "LazyFrame":
+        return LazyFrame(("with_columns", self._node, _parse_exprs(exprs)))
+
+    def collect(self, engine: str = "gpu", info: dict | None = None) -> DataFrame:
+        """Execute on the GPU.  `engine` is accepted for API parity with
+        polars' `collect(engine=...)`; every node runs on the HIP executor."""
+        return _execute(self._node, info)
+
+    def explain(self) -> str:
+        return _explain(self._node)
+
+
+class LazyGroupBy:
+    def __init__(self, lf: LazyFrame, by: Sequence[Any], maintain_order: bool):
+        keys = _parse_exprs(by)
+        if builtins.len(keys) != 1 or keys[0].kind != "col":
+            raise N.InvalidOperationError("the GPU executor groups by exactly one key column")
+        self._lf, self._key, self._maintain = lf, keys[0].value, maintain_order
+
+    def agg(self, *aggs: Any, **named: Any) -> LazyFrame:
+        exprs = _parse_exprs(aggs) + [e.alias(k) for k, e in named.items()]
+        return LazyFrame(("group_by", self._lf._node, self._key, exprs, self._maintain))
+
+    def len(self, name: str = "len") -> LazyFrame:
+        from .expr import len as len_expr
+        return self.agg(len_expr().alias(name))
+
+
+class GroupBy:
+    """Eager DataFrame.group_by: runs the lazy plan (as py-polars does)."""
+
+    def __init__(self, lf: LazyFrame, by: Sequence[Any], maintain_order: bool):
+        self._g = LazyGroupBy(lf, by, maintain_order)
+
+    def agg(self, *aggs: Any, **named: Any) -> DataFrame:
+        return self._g.agg(*aggs, **named).collect()
+
+    def len(self, name: str = "len") -> DataFrame:
+        return self._g.len(name).collect()
+
+
+# ----------------------------------------------------------------- planner
+def _explain(node: tuple, depth: int = 0) -> str:
+    pad = "  " * depth
+    kind = node[0]
+    if kind == "scan":
+        return f"{pad}DF {node[1].columns}"
+    if kind == "filter":
+        return f"{pad}FILTER {node[2]!r}\n" + _explain(node[1], depth + 1)
+    if kind == "group_by":
+        return f"{pad}AGGREGATE {node[3]!r} BY {node[2]}\n" + _explain(node[1], depth + 1)
+    return f"{pad}{kind.upper()} {node[2]!r}\n" + _explain(node[1], depth + 1)
+
+
+def _program(expr: Expr, df: DataFrame) -> tuple[list[Series], Any, int]:
+    names = expr.meta_root_names()
+    if builtins.len(names) > N.MAX_COLS:
+        raise N.InvalidOperationError("expression references more than 8 columns")
+    for nm in names:
+        if nm not in df._cols:
+            raise N.ComputeError(f'unable to find column "{nm}"; valid columns: {df.columns}')
+    idx = {nm: i for i, nm in enumerate(names)}
+    schema = {nm: df._cols[nm].dtype.code for nm in names}
+    prog = lower(expr, idx, schema)
+    return [df._cols[nm] for nm in names], to_instr_array(prog), builtins.len(prog)
+
+
+def _col_array(series: Sequence[Series]):
+    arr = (N.Column * max(1, builtins.len(series)))()
+    for i, s in enumerate(series):
+        arr[i] = s._col
+    return arr
+
+
+def _eval(expr: Expr, df: DataFrame) -> Series:
+    if expr.kind in ("col",) or (expr.kind == "alias" and expr.args[0].kind == "col"):
+        return df._cols[expr.meta_root_names()[0]].alias(expr.output_name())
+    used, prog, n = _program(expr, df)
+    if not used:
+        raise N.InvalidOperationError("literal-only expressions are not supported on the GPU executor")
+    out = N.Column()
+    N.check(N.lib().plgpu_eval(_col_array(used), builtins.len(used), prog, n, C.byref(out), None))
+    return Series._from_native(expr.output_name(), out)
+
+
+def _filter(df: DataFrame, pred: Expr) -> DataFrame:
+    used, prog, n = _program(pred, df)
+    names = df.columns
+    if not used:
+        # literal predicate: broadcast over the frame via a column of it
+        raise N.InvalidOperationError("literal-only predicates are not supported on the GPU executor")
+    # The fused path evaluates the predicate inside the compaction kernels; the
+    # predicate's columns must be in the same call, so compact in chunks of up
+    # to 8 columns that always carry the predicate columns first.
+    pred_names = [s.name for s in used]
+    others = [nm for nm in names if nm not in pred_names]
+    room = N.MAX_COLS - builtins.len(pred_names)
+    chunks = [others[i: i + room] for i in range(0, builtins.len(others), room)] or [[]]
+    result: dict[str, Series] = {}
+    for chunk in chunks:
+        series = used + [df._cols[nm] for nm in chunk]
+        out = (N.Column * builtins.len(series))()
+        cnt = C.c_int64(0)
+        N.check(N.lib().plgpu_filter_expr(_col_array(series), builtins.len(series), prog, n, out,
+                                          C.byref(cnt), None))
+        for i, s in enumerate(series):
+            result.setdefault(s.name, Series._from_native(s.name, out[i]))
+    return DataFrame([result[nm] for nm in names])
+
+
+_AGG_CODE = N.AGG
+
+
+def _group_by(df: DataFrame, key: str, aggs: list[Expr], maintain_order: bool,
+              pred: Expr | None, info: dict | None) -> DataFrame:
+    if key not in df._cols:
+        raise N.ComputeError(f'unable to find column "{key}"')
+    specs: list[tuple[str, str]] = []  # (kind, column)
+    out_names: list[str] = []
+    for e in aggs:
+        name = e.output_name()
+        base = e.args[0] if e.kind == "alias" else e
+        if base.kind == "len":
+            specs.append(("len", key))
+        elif base.kind == "agg" and base.args[0].kind == "col":
+            specs.append((base.op, base.args[0].value))
+        else:
+            raise N.InvalidOperationError(
+                f"aggregation {e!r} is not supported on the GPU executor (need col(..).sum/mean/min/max/count/len)")
+        out_names.append(name)
+    # columns passed to the kernel: predicate columns + aggregated columns
+    names: list[str] = []
+    prog, n_instr = None, 0
+    if pred is not None:
+        names = pred.meta_root_names()
+    for _, c_ in specs:
+        if c_ not in names:
+            names.append(c_)
+    if builtins.len(names) > N.MAX_COLS:
+        raise N.InvalidOperationError("group-by references more than 8 columns")
+    for nm in names:
+        if nm not in df._cols:
+            raise N.ComputeError(f'unable to find column "{nm}"')
+    idx = {nm: i for i, nm in enumerate(names)}
+    if pred is not None:
+        schema = {nm: df._cols[nm].dtype.code for nm in names}
+        p = lower(pred, idx, schema)
+        prog, n_instr = to_instr_array(p), builtins.len(p)
+    agg_arr = (N.Agg * max(1, builtins.len(specs)))()
+    for i, (k, c_) in enumerate(specs):
+        agg_arr[i].kind = _AGG_CODE[k]
+        agg_arr[i].col = idx[c_]
+    cols = _col_array([df._cols[nm] for nm in names])
+    out_key = N.Column()
+    out_aggs = (N.Column * max(1, builtins.len(specs)))()
+    gi = N.GroupByInfo()
+    keycol = df._cols[key]._col
+    N.check(N.lib().plgpu_group_by_agg(C.byref(keycol), cols, builtins.len(names), prog, n_instr, agg_arr,
+                                       builtins.len(specs), int(bool(maintain_order)), C.byref(out_key),
+                                       out_aggs, C.byref(gi), None))
+    if info is not None:
+        info.update(gi.as_dict())
+    series = [Series._from_native(key, out_key)]
+    for i, nm in enumerate(out_names):
+        series.append(Series._from_native(nm, out_aggs[i]))
+    return DataFrame(series)
+
+
+def _execute(node: tuple, info: dict | None = None) -> DataFrame:
+    kind = node[0]
+    if kind == "scan":
+        return node[1]
+    if kind == "filter":
+        df = _execute(node[1], info)
+        return _filter(df, node[2])
+    if kind == "group_by":
+        child = node[1]
+        pred = None
+        if child[0] == "filter":  # predicate pushed into the aggregation kernel
+            pred = child[2]
+            child = child[1]
+        df = _execute(child, info)
+        return _group_by(df, node[2], node[3], node[4], pred, info)
+    if kind in ("select", "with_columns"):
+        df = _execute(node[1], info)
+        new = [_eval(e, df) for e in node[2]]
+        if kind == "select":
+            return DataFrame(new)
+        cols = dict(df._cols)
+        for s in new:
+            cols[s.name] = s
+        return DataFrame(list(cols.values()))
+    raise N.InvalidOperationError(f"unknown plan node {kind}")
+
+
+def from_dict(data: dict, schema: Any = None) -> DataFrame:
+    return DataFrame(data, schema)

@@ -1,0 +1,203 @@
+"""Generate the golden fixtures in tests/golden/ from the reference's own tests.
+
+The reference (polars, Rust + py-polars) cannot be built or imported in this
+image (no rustc; `import polars` fails), so each fixture transcribes the
+inputs and expected outputs a reference test asserts, citing the test by
+file:line (paths relative to /root/reference/py-polars/tests/unit).  Floats
+are stored as float.hex() strings so NaN / -0.0 / inf survive JSON exactly;
+None is null.
+
+    python tests/golden/make_golden.py      # rewrites the *.json files
+"""
+
+from __future__ import annotations
+
+import json
+import math
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def fx(v):
+    """Encode a value: floats as hex strings, everything else as-is."""
+    if isinstance(v, float):
+        return v.hex()
+    if isinstance(v, list):
+        return [fx(x) for x in v]
+    return v
+
+
+# ---------------------------------------------------------------------------
+# 1. Total-order comparison truth table.
+#    operations/test_comparison.py:206-245 states the rule the reference is
+#    checked against: "normal < nan, nan == nan, nulls propagate" for the
+#    plain operators and "null < normal < nan, nan == nan, null == null" for
+#    eq_missing / ne_missing; :340-350 lists INTERESTING_FLOAT_VALUES and
+#    :353-370 runs every (lhs, rhs) pair as `pl.col("l") <op> rhs`.
+INTERESTING = [0.0, -0.0, -1.0, 1.0, -float("nan"), float("nan"), -float("inf"), float("inf"), None]
+
+
+def _ordering(lhs, rhs, missing):
+    if lhs is None or rhs is None:
+        if not missing:
+            return None
+        if lhs is None and rhs is None:
+            return "="
+        return "<" if lhs is None else ">"
+    ln, rn = math.isnan(lhs), math.isnan(rhs)
+    if ln and rn:
+        return "="
+    if ln or lhs > rhs:
+        return ">"
+    if rn or lhs < rhs:
+        return "<"
+    return "="
+
+
+def compare_table():
+    rows = []
+    for lhs in INTERESTING:
+        for rhs in INTERESTING:
+            ref = _ordering(lhs, rhs, False)
+            miss = _ordering(lhs, rhs, True)
+            exp = {
+                "eq": None if ref is None else ref == "=",
+                "ne": None if ref is None else ref != "=",
+                "lt": None if ref is None else ref == "<",
+                "le": None if ref is None else ref in "<=",
+                "gt": None if ref is None else ref == ">",
+                "ge": None if ref is None else ref in ">=",
+                "eq_missing": miss == "=",
+                "ne_missing": miss != "=",
+            }
+            rows.append({"lhs": fx(lhs), "rhs": fx(rhs), "expected": exp})
+    return {"source": "py-polars/tests/unit/operations/test_comparison.py:206-245,340-370",
+            "cases": rows}
+
+
+# ---------------------------------------------------------------------------
+# 2. Group-by cases with the expected outputs the reference asserts.
+#    Keys that the reference test writes as strings are mapped to Int64
+#    codes in first-occurrence order (the path under test groups integer
+#    keys); the code -> label map is kept in "key_labels".
+def group_by_cases():
+    cases = []
+    cases.append({
+        "name": "test_group_by_sum",
+        "source": "operations/test_group_by.py:30-51",
+        "key": [0, 1, 0, 1, 1, 2], "key_labels": ["a", "b", "c"],
+        "cols": {"b": {"dtype": "i64", "values": [1, 2, 3, 4, 5, 6]}},
+        "aggs": [["sum", "b"]], "maintain_order": True,
+        "expected": {"key": [0, 1, 2], "b": [4, 11, 6]},
+    })
+    cases.append({
+        "name": "test_group_by_count",
+        "source": "operations/test_group_by.py:53-67",
+        "key": [0, 0, 1, 1, 1], "key_labels": ["a", "b"],
+        "cols": {"a": {"dtype": "i64", "values": [1, 2, 3, 4, 5]}},
+        "aggs": [["count", "a"]], "maintain_order": True,
+        "expected": {"key": [0, 1], "a": [2, 3]},
+    })
+    cases.append({
+        "name": "test_group_by_mean_by_dtype[Float64]",
+        "source": "operations/test_group_by.py:80,141-160",
+        "key": [0, 0, 0, 1], "key_labels": ["a", "b"],
+        "cols": {"Float64": {"dtype": "f64", "values": fx([1.0, 2.0, 3.0, 4.0])}},
+        "aggs": [["mean", "Float64"]], "maintain_order": True,
+        "expected": {"key": [0, 1], "Float64": fx([2.0, 4.0])},
+    })
+    cases.append({
+        "name": "test_group_by_mean_by_dtype[Int64-like]",
+        "source": "operations/test_group_by.py:73-79,141-160",
+        "key": [0, 0, 0, 1], "key_labels": ["a", "b"],
+        "cols": {"Int64": {"dtype": "i64", "values": [1, 2, 3, 4]}},
+        "aggs": [["mean", "Int64"]], "maintain_order": True,
+        "expected": {"key": [0, 1], "Int64": fx([2.0, 4.0])},
+    })
+    a = [1] * 10 + [2] * 10 + [3] * 10
+    b = [1] * 10 + [None] * 20
+    cases.append({
+        "name": "test_partitioned_group_by_nulls_mean_21838",
+        "source": "operations/test_group_by.py:1109-1117",
+        "key": a,
+        "cols": {"b": {"dtype": "i64", "values": b}},
+        "aggs": [["mean", "b"]], "maintain_order": False, "sort_by_key": True,
+        "expected": {"key": [1, 2, 3], "b": fx([1.0, None, None])},
+    })
+    nan, inf = float("nan"), float("inf")
+    groups = ["both nan", "both nan", "nan and 5", "nan and 5", "nan and null", "nan and null",
+              "both none", "both none", "both inf", "both inf", "inf and null", "inf and null"]
+    labels = list(dict.fromkeys(groups))
+    vals = [nan, nan, nan, 5.0, nan, None, None, None, inf, inf, inf, None]
+    cases.append({
+        "name": "test_nan_inf_aggregation",
+        "source": "operations/aggregation/test_aggregations.py:523-560",
+        "key": [labels.index(g) for g in groups], "key_labels": labels,
+        "cols": {"value": {"dtype": "f64", "values": fx(vals)}},
+        "aggs": [["min", "value", "min"], ["max", "value", "max"], ["mean", "value", "mean"]],
+        "maintain_order": True,
+        "expected": {
+            "key": list(range(6)),
+            "min": fx([nan, 5.0, nan, None, inf, inf]),
+            "max": fx([nan, 5.0, nan, None, inf, inf]),
+            "mean": fx([nan, nan, nan, None, inf, inf]),
+        },
+    })
+    return {"cases": cases}
+
+
+# ---------------------------------------------------------------------------
+# 3. Filter cases.
+def filter_cases():
+    cases = []
+    cases.append({
+        "name": "test_simplify_expression_lit_true_4376",
+        "source": "operations/test_filter.py:17-25",
+        # pl.DataFrame([[1, 4, 7], [2, 5, 8], [3, 6, 9]]) builds columns from the inner lists
+        "cols": {"column_0": [1, 4, 7], "column_1": [2, 5, 8], "column_2": [3, 6, 9]},
+        "predicate": "lit(True) | (col('column_0') == 1)",
+        "expected_rows": [[1, 2, 3], [4, 5, 6], [7, 8, 9]],
+    })
+    cases.append({
+        "name": "test_binary_simplification_5971",
+        "source": "operations/test_filter.py:157-164",
+        "cols": {"a": [1, 2, 3, 4]},
+        "predicate": "(col('a') > 2) | lit(False)",
+        "expected_mask": [False, False, True, True],
+    })
+    cases.append({
+        "name": "test_filter_19771",
+        "source": "operations/test_filter.py:314-316",
+        "cols": {"a": [None, None]},
+        "predicate": "lit(True)",
+        "expected_rows": [[None], [None]],
+    })
+    cases.append({
+        "name": "test_filter_on_empty[Int32]",
+        "source": "operations/test_filter.py:93-110",
+        "cols": {"a": []},
+        "predicate": "col('a').is_null()",
+        "expected_rows": [],
+    })
+    cases.append({
+        "name": "test_filter_horizontal_selector_15428",
+        "source": "operations/test_filter.py:262-266",
+        "cols": {"a": [1, 2, 3]},
+        "predicate": "col('a') <= 2",
+        "expected_rows": [[1], [2]],
+    })
+    return {"cases": cases}
+
+
+def main():
+    for name, obj in (("compare_total_order.json", compare_table()),
+                      ("group_by_cases.json", group_by_cases()),
+                      ("filter_cases.json", filter_cases())):
+        with open(os.path.join(HERE, name), "w") as f:
+            json.dump(obj, f, indent=1, sort_keys=False)
+            f.write("\n")
+
+
+if __name__ == "__main__":
+    main()

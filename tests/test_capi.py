@@ -1,0 +1,132 @@
+"""CPU: the C-ABI library loads, exports every symbol include/polaroid_gpu.h
+declares, its struct layouts match the ctypes mirror, and host-side
+validation (program type-checking, argument checks) errors without a GPU."""
+
+import ctypes as C
+import os
+import re
+import subprocess
+import tempfile
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "polaroid_gpu.h")
+
+
+@pytest.fixture(scope="module")
+def N():
+    from polaroid_amd import _native
+
+    if not os.path.exists(_native.LIB_PATH):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "polaroid_amd", "csrc")], check=True)
+    _native.lib()
+    return _native
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(plgpu_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_every_declared_symbol_is_exported_and_bound(N):
+    decl = declared_functions()
+    assert len(decl) >= 15
+    lib = C.CDLL(N.LIB_PATH)
+    for name in decl:
+        assert hasattr(lib, name), f"{name} declared in include/polaroid_gpu.h but not exported"
+        assert name in N.SIGNATURES, f"{name} not bound in polaroid_amd/_native.py"
+    assert sorted(N.SIGNATURES) == decl
+
+
+def test_struct_layouts_match_header(N):
+    probe = r"""
+    #include <stdio.h>
+    #include <stddef.h>
+    #include "polaroid_gpu.h"
+    int main(void) {
+      printf("%zu %zu %zu %zu %zu\n", sizeof(plgpu_column), offsetof(plgpu_column, values),
+             offsetof(plgpu_column, release), sizeof(plgpu_instr), offsetof(plgpu_instr, imm));
+      printf("%zu %zu %zu\n", sizeof(plgpu_agg), sizeof(plgpu_groupby_info),
+             offsetof(plgpu_groupby_info, main_kernel_ms));
+      return 0;
+    }
+    """
+    with tempfile.TemporaryDirectory() as d:
+        src, exe = os.path.join(d, "p.c"), os.path.join(d, "p")
+        open(src, "w").write(probe)
+        subprocess.run(["gcc", "-I", os.path.dirname(HEADER), src, "-o", exe], check=True)
+        out = subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split()
+    got = [int(x) for x in out]
+    exp = [C.sizeof(N.Column), N.Column.values.offset, N.Column.release.offset, C.sizeof(N.Instr),
+           N.Instr.imm.offset, C.sizeof(N.Agg), C.sizeof(N.GroupByInfo), N.GroupByInfo.main_kernel_ms.offset]
+    assert got == exp
+
+
+def test_abi_version(N):
+    assert N.lib().plgpu_abi_version() == 1
+
+
+def _instrs(N, prog):
+    arr = (N.Instr * len(prog))()
+    for i, (op, arg, imm) in enumerate(prog):
+        arr[i].op, arr[i].arg = op, arg
+        if op == N.OP["LIT_F64"]:
+            arr[i].imm.f64 = imm
+        else:
+            arr[i].imm.i64 = imm
+    return arr
+
+
+def _host_col(N, dtype, n):
+    c = N.Column()
+    c.dtype, c.length = dtype, n
+    c.values = 0x1000  # never dereferenced: validation fails before any device work
+    return c
+
+
+@pytest.mark.parametrize(
+    "prog, code",
+    [
+        ([("AND", 0, 0)], "ERR_INVALID"),                                   # stack underflow
+        ([("COL", 0, 0), ("LIT_BOOL", 0, 1), ("ADD", 0, 0)], "ERR_INVALID"),  # bool arithmetic
+        ([("COL", 0, 0), ("NOT", 0, 0)], "ERR_SCHEMA"),                     # not on f64
+        ([("COL", 0, 0), ("COL", 1, 0), ("AND", 0, 0)], "ERR_SCHEMA"),      # and on numerics
+        ([("COL", 5, 0)], "ERR_INVALID"),                                   # bad column index
+        ([("COL", 1, 0), ("IS_NAN", 0, 0)], "ERR_INVALID"),                 # is_nan on int
+        ([("COL", 0, 0), ("COL", 0, 0)], "ERR_INVALID"),                    # two results
+    ],
+)
+def test_program_type_errors_without_gpu(N, prog, code):
+    cols = (N.Column * 2)(_host_col(N, N.F64, 4), _host_col(N, N.I64, 4))
+    p = _instrs(N, [(N.OP[o], a, i) for o, a, i in prog])
+    out = N.Column()
+    rc = N.lib().plgpu_eval(cols, 2, p, len(prog), C.byref(out), None)
+    assert rc == getattr(N, code), N.lib().plgpu_last_error()
+    assert N.lib().plgpu_last_error()
+
+
+def test_filter_predicate_must_be_boolean_without_gpu(N):
+    cols = (N.Column * 1)(_host_col(N, N.F64, 4))
+    p = _instrs(N, [(N.OP["COL"], 0, 0), (N.OP["LIT_F64"], 0, 1.0), (N.OP["ADD"], 0, 0)])
+    out = (N.Column * 1)()
+    n = C.c_int64()
+    rc = N.lib().plgpu_filter_expr(cols, 1, p, 3, out, C.byref(n), None)
+    assert rc == N.ERR_SCHEMA
+    assert "must be of type `Boolean`" in N.lib().plgpu_last_error().decode()
+
+
+def test_group_by_argument_checks_without_gpu(N):
+    key = _host_col(N, N.F64, 4)
+    cols = (N.Column * 1)(_host_col(N, N.F64, 4))
+    aggs = (N.Agg * 1)()
+    aggs[0].kind, aggs[0].col = N.AGG["sum"], 0
+    ok, outs = N.Column(), (N.Column * 1)()
+    rc = N.lib().plgpu_group_by_agg(C.byref(key), cols, 1, None, 0, aggs, 1, 0, C.byref(ok), outs, None, None)
+    assert rc == N.ERR_SCHEMA  # key must be Int64/Int32
+    key = _host_col(N, N.I64, 4)
+    cols = (N.Column * 1)(_host_col(N, N.F64, 5))
+    rc = N.lib().plgpu_group_by_agg(C.byref(key), cols, 1, None, 0, aggs, 1, 0, C.byref(ok), outs, None, None)
+    assert rc == N.ERR_SHAPE

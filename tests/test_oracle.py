@@ -1,0 +1,155 @@
+"""CPU: pin the oracle (oracle/polars_oracle.c) before trusting it.
+
+* against the golden fixtures transcribed from the reference's own tests;
+* the exact-sum leg against CPython's math.fsum;
+* the Kahan leg (the reference's GroupByExec fold) within 1 ULP of exact on
+  same-sign data, the naive leg (the streaming reducer) within Higham's
+  bound gamma_{n-1} * sum|x|.
+"""
+
+import math
+
+import numpy as np
+import pytest
+
+from conftest import load_golden, unhex
+from oracle import oracle as O
+
+OPS = dict(eq=20, ne=21, lt=22, le=23, gt=24, ge=25, eq_missing=26, ne_missing=27)
+
+
+def _fcol(vals):
+    valid = np.array([v is not None for v in vals], dtype=bool)
+    arr = np.array([0.0 if v is None else v for v in vals], dtype=np.float64)
+    return O.HostCol(arr, None if valid.all() else valid)
+
+
+def test_compare_truth_table_scalar_and_column():
+    g = load_golden("compare_total_order.json")
+    assert len(g["cases"]) == 81
+    for case in g["cases"]:
+        lhs, rhs = unhex(case["lhs"]), unhex(case["rhs"])
+        lcol = _fcol([lhs, 0.0])
+        rcol = _fcol([rhs, 0.0])
+        for opname, exp in case["expected"].items():
+            # column vs column
+            dt, v, valid = O.eval_program([lcol, rcol], [(1, 0, 0), (1, 1, 0), (OPS[opname], 0, 0)], 2)
+            got = bool(v[0]) if valid[0] else None
+            assert got == exp, (lhs, rhs, opname)
+            # column vs scalar literal (pl.col("l") <op> rhs)
+            lit = (5, 4, 0) if rhs is None else (2, 0, rhs)
+            dt, v, valid = O.eval_program([lcol], [(1, 0, 0), lit, (OPS[opname], 0, 0)], 2)
+            got = bool(v[0]) if valid[0] else None
+            assert got == exp, (lhs, rhs, opname, "scalar")
+
+
+def _case_cols(case):
+    cols, names = [], []
+    for name, spec in case["cols"].items():
+        vals = unhex(spec["values"]) if spec["dtype"] == "f64" else spec["values"]
+        valid = np.array([v is not None for v in vals], dtype=bool)
+        dt = np.float64 if spec["dtype"] == "f64" else np.int64
+        fill = 0.0 if dt is np.float64 else 0
+        arr = np.array([fill if v is None else v for v in vals], dtype=dt)
+        cols.append(O.HostCol(arr, None if valid.all() else valid))
+        names.append(name)
+    return cols, names
+
+
+def _same(a, b):
+    if a is None or b is None:
+        return a is None and b is None
+    if isinstance(a, float) or isinstance(b, float):
+        if math.isnan(a) or math.isnan(b):
+            return math.isnan(a) and math.isnan(b)
+    return a == b
+
+
+@pytest.mark.parametrize("mode", [O.SUM_KAHAN, O.SUM_NAIVE, O.SUM_EXACT])
+def test_group_by_golden(mode):
+    for case in load_golden("group_by_cases.json")["cases"]:
+        cols, names = _case_cols(case)
+        key = O.HostCol(np.array(case["key"], dtype=np.int64))
+        aggs = [(a[0], names.index(a[1])) for a in case["aggs"]]
+        keys, kvalid, outs = O.group_by_agg(key, cols, None, aggs, len(case["key"]), mode)
+        order = np.argsort(keys, kind="stable") if case.get("sort_by_key") else np.arange(len(keys))
+        assert keys[order].tolist() == case["expected"]["key"], case["name"]
+        for a, (vals, valid) in zip(case["aggs"], outs):
+            outname = a[2] if len(a) > 2 else a[1]
+            exp = unhex(case["expected"][outname])
+            got = [v if ok else None for v, ok in zip(vals[order].tolist(), valid[order].tolist())]
+            assert all(_same(x, y) for x, y in zip(got, exp)), (case["name"], outname, got, exp)
+
+
+def test_filter_golden():
+    for case in load_golden("filter_cases.json")["cases"]:
+        names = list(case["cols"])
+        cols = []
+        for nm in names:
+            vals = case["cols"][nm]
+            valid = np.array([v is not None for v in vals], dtype=bool)
+            arr = np.array([0 if v is None else v for v in vals], dtype=np.int64)
+            cols.append(O.HostCol(arr, None if valid.all() else valid))
+        n = len(case["cols"][names[0]])
+        # predicates of the fixtures, as postfix programs
+        progs = {
+            "lit(True) | (col('column_0') == 1)": [(4, 0, 1), (1, 0, 0), (3, 0, 1), (20, 0, 0), (31, 0, 0)],
+            "(col('a') > 2) | lit(False)": [(1, 0, 0), (3, 0, 2), (24, 0, 0), (4, 0, 0), (31, 0, 0)],
+            "lit(True)": [(1, 0, 0), (34, 0, 0), (1, 0, 0), (33, 0, 0), (31, 0, 0)],  # x.is_not_null() | x.is_null()
+            "col('a').is_null()": [(1, 0, 0), (33, 0, 0)],
+            "col('a') <= 2": [(1, 0, 0), (3, 0, 2), (23, 0, 0)],
+        }
+        prog = progs[case["predicate"]]
+        if "expected_mask" in case:
+            dt, v, valid = O.eval_program(cols, prog, n)
+            assert [bool(x) for x in v] == case["expected_mask"]
+            continue
+        outs = [O.filter_column(cols, prog, n, i) for i in range(len(cols))]
+        rows = [list(r) for r in zip(*[[x if ok else None for x, ok in zip(v.tolist(), va.tolist())]
+                                       for v, va in outs])] if outs else []
+        assert rows == case["expected_rows"], case["name"]
+
+
+@pytest.mark.parametrize("seed", range(5))
+def test_fsum_matches_math_fsum(seed):
+    rng = np.random.default_rng(seed)
+    x = rng.standard_normal(5000) * 10.0 ** rng.integers(-30, 30, 5000)
+    x[::97] = -x[::89][: len(x[::97])]
+    assert O.fsum(x) == math.fsum(x)
+
+
+def _ulp_diff(a: float, b: float) -> int:
+    ia = np.array(a).view(np.int64).item()
+    ib = np.array(b).view(np.int64).item()
+    return abs(ia - ib)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_sum_modes_bounds(seed):
+    rng = np.random.default_rng(100 + seed)
+    n = 20000
+    key = rng.integers(0, 50, n).astype(np.int64)
+    v = rng.uniform(1.0, 1000.0, n)
+    kc, vc = O.HostCol(key), O.HostCol(v)
+    res = {m: O.group_by_agg(kc, [vc], None, [("sum", 0)], n, m) for m in (0, 1, 2)}
+    k0 = res[2][0]
+    for m in (0, 1):
+        assert (res[m][0] == k0).all()
+    for gi, kv in enumerate(k0):
+        exact = res[2][2][0][0][gi]
+        assert exact == math.fsum(v[key == kv])
+        assert _ulp_diff(res[0][2][0][0][gi], exact) <= 1           # Kahan
+        cnt = int((key == kv).sum())
+        bound = (cnt - 1) * 2.0 ** -53 / (1 - (cnt - 1) * 2.0 ** -53) * np.abs(v[key == kv]).sum()
+        assert abs(res[1][2][0][0][gi] - exact) <= bound           # naive (Higham)
+
+
+def test_baseline_matches_group_by():
+    rng = np.random.default_rng(7)
+    n = 50000
+    key = rng.integers(0, 100, n).astype(np.int64)
+    a, b = rng.uniform(0, 100, n), rng.uniform(0, 100, n)
+    g, chk = O.baseline_filter_groupby_sum(key, a, 50.0, [a, b], threads=4)
+    sel = a > 50.0
+    assert g == len(np.unique(key[sel]))
+    assert abs(chk - (a[sel].sum() + b[sel].sum())) < 1e-6 * chk
