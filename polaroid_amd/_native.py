@@ -107,6 +107,19 @@ SIGNATURES = {
 _lib = None
 
 
+def _share_hip_runtime_with_torch() -> None:
+    """PyTorch-ROCm wheels bundle their own libamdhip64.so.7.  If this
+    library were loaded first, the process would end up with two HIP
+    runtimes (ours from /opt/rocm and torch's), which breaks whichever
+    initialises second.  Importing torch first makes the dynamic loader
+    resolve our DT_NEEDED libamdhip64.so.7 to torch's copy (same SONAME), so
+    device pointers, streams and RCCL buffers are shared by one runtime."""
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+
+
 def lib():
     """Load libpolaroid_gpu.so (raises if it was not built)."""
     global _lib
@@ -116,6 +129,7 @@ def lib():
                 f"polaroid_amd native library missing: {LIB_PATH}. Build it with "
                 "`python -c 'import __graft_entry__ as g; g.build()'` (make -C polaroid_amd/csrc)."
             )
+        _share_hip_runtime_with_torch()
         handle = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(handle, name)

@@ -21,6 +21,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <vector>
@@ -554,6 +556,7 @@ struct FinParams {
     int64_t* out_keys;
     uint32_t* out_key_valid;
     uint64_t* out_first;  // optional
+    int64_t cap;          // allocated output rows (guards against a miscount)
 };
 
 __global__ void gb_finalize_kernel(GbParams p, FinParams fp) {
@@ -563,6 +566,7 @@ __global__ void gb_finalize_kernel(GbParams p, FinParams fp) {
         const uint64_t len = *gfield(p, p.f_len, s);
         if (len == 0) continue;
         const int64_t g = (int64_t)atomicAdd((unsigned long long*)&p.status[ST_GROUPS_OUT], 1ull);
+        if (g >= fp.cap) continue;
         const bool null_key = s == p.gcap;
         fp.out_keys[g] = null_key ? 0 : (int64_t)(s == p.gcap + 1 ? kEmptyKey : *gfield(p, 0, s));
         if (!null_key) atomicOr(&fp.out_key_valid[g >> 5], 1u << (g & 31));
@@ -850,7 +854,35 @@ PLGPU_API int plgpu_group_by_agg(const plgpu_column* key, const plgpu_column* co
         if ((rc = dev_alloc((void**)&gtab, gwords * 8, s))) break;
         p.gtab = gtab;
         const int ig = (int)std::min<int64_t>((int64_t)(gwords + 255) / 256, 256 * 16);
-        gb_init_table_kernel<<<ig, 256, 0, s>>>(gtab, p.gcap + 2, p.nfields, p.min_init_mask);
+        if (getenv("PLGPU_MEMSET_INIT")) {
+            for (int f = 0; f < p.nfields; ++f) {
+                const int byte = f == 0 ? 0 : (((p.min_init_mask >> f) & 1ull) ? 0xFF : 0);
+                PLGPU_HIP(hipMemsetAsync(gtab + (size_t)f * (p.gcap + 2), byte, (size_t)(p.gcap + 2) * 8, s));
+            }
+            gb_init_table_kernel<<<ig, 256, 0, s>>>(gtab, p.gcap + 2, 1, 0);
+        } else {
+            gb_init_table_kernel<<<ig, 256, 0, s>>>(gtab, p.gcap + 2, p.nfields, p.min_init_mask);
+        }
+        if (getenv("PLGPU_DEBUG")) {
+            std::vector<uint64_t> chk(gwords);
+            PLGPU_HIP(hipMemcpyAsync(chk.data(), gtab, gwords * 8, hipMemcpyDeviceToHost, s));
+            PLGPU_HIP(hipStreamSynchronize(s));
+            size_t bad = 0;
+            for (size_t i = 0; i < gwords; ++i) {
+                const int f = (int)(i / (size_t)(p.gcap + 2));
+                const uint64_t want = f == 0 ? kEmptyKey : (((p.min_init_mask >> f) & 1ull) ? ~0ull : 0ull);
+                bad += chk[i] != want;
+            }
+            size_t firstbad = gwords;
+            for (size_t i = 0; i < gwords && firstbad == gwords; ++i) {
+                const int f = (int)(i / (size_t)(p.gcap + 2));
+                const uint64_t want = f == 0 ? kEmptyKey : (((p.min_init_mask >> f) & 1ull) ? ~0ull : 0ull);
+                if (chk[i] != want) firstbad = i;
+            }
+            fprintf(stderr, "[plgpu] init check: %zu bad words of %zu (gtab=%p) first bad %zu field %zu val %llx mask %llx\n",
+                    bad, gwords, (void*)gtab, firstbad, firstbad / (size_t)(p.gcap + 2),
+                    firstbad < gwords ? (unsigned long long)chk[firstbad] : 0ull, (unsigned long long)p.min_init_mask);
+        }
         PLGPU_HIP(hipMemsetAsync(status, 0, ST_WORDS * 8, s));
         if (bottoms_from_host) {
             PLGPU_HIP(hipMemcpyAsync(bottoms, host_bottoms, sizeof host_bottoms, hipMemcpyHostToDevice, s));
@@ -864,6 +896,18 @@ PLGPU_API int plgpu_group_by_agg(const plgpu_column* key, const plgpu_column* co
         PLGPU_HIP(hipMemcpyAsync(st, status, sizeof st, hipMemcpyDeviceToHost, s));
         PLGPU_HIP(hipMemcpyAsync(host_bottoms, bottoms, sizeof host_bottoms, hipMemcpyDeviceToHost, s));
         PLGPU_HIP(hipStreamSynchronize(s));
+        if (getenv("PLGPU_DEBUG")) {
+            fprintf(stderr,
+                    "[plgpu] gb attempt %d: n=%lld grid=%d lcap=%d gcap=%lld nfields=%d lds=%zu newkeys=%llu "
+                    "special=%llu global_rows=%llu full=%llu selected=%llu\n",
+                    attempt, (long long)n, pl.grid, p.lcap, (long long)p.gcap, p.nfields, pl.lds_bytes,
+                    (unsigned long long)st[ST_NEWKEYS], (unsigned long long)st[ST_SPECIAL],
+                    (unsigned long long)st[ST_GLOBAL_ROWS], (unsigned long long)st[ST_TABLE_FULL],
+                    (unsigned long long)st[ST_SELECTED]);
+            for (int a = 0; a < p.nacc; ++a)
+                fprintf(stderr, "[plgpu]   acc %d flags=%d bottom=%d maxex=%llu fx=%llu\n", a, p.acc[a].flags,
+                        host_bottoms[a], (unsigned long long)st[ST_MAXEX + a], (unsigned long long)st[ST_FXFLAGS + a]);
+        }
         bool again = false;
         if (st[ST_TABLE_FULL] > 0) {
             gbits = log2_ceil(std::max<int64_t>((int64_t)st[ST_NEWKEYS] * 4, p.gcap * 8));
@@ -942,10 +986,27 @@ PLGPU_API int plgpu_group_by_agg(const plgpu_column* key, const plgpu_column* co
         fp.out_key_valid = (uint32_t*)out_key->validity;
         (void)hipMemsetAsync((void*)out_key->validity, 0, ((groups + 63) / 64) * 8, s);
         fp.out_first = first;
+        fp.cap = groups;
         const int fg = (int)std::min<int64_t>((p.gcap + 2 + 255) / 256, 256 * 16);
         gb_finalize_kernel<<<fg, 256, 0, s>>>(p, fp);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) rc = hip_fail(e, "gb_finalize_kernel");
+        uint64_t produced = 0;
+        if (rc == PLGPU_OK) {
+            e = hipMemcpyAsync(&produced, status + ST_GROUPS_OUT, 8, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e != hipSuccess) rc = hip_fail(e, "finalize count");
+        }
+        if (rc == PLGPU_OK && (int64_t)produced != groups) {
+            char buf[256];
+            snprintf(buf, sizeof buf,
+                     "internal: group count mismatch (inserted %llu + specials %llu, finalized %llu, "
+                     "global rows %llu, table_full %llu)",
+                     (unsigned long long)st[ST_NEWKEYS], (unsigned long long)st[ST_SPECIAL],
+                     (unsigned long long)produced, (unsigned long long)st[ST_GLOBAL_ROWS],
+                     (unsigned long long)st[ST_TABLE_FULL]);
+            rc = fail(PLGPU_ERR_CAPACITY, buf);
+        }
     }
     if (rc == PLGPU_OK && maintain_order && groups > 1) {
         // order groups by first occurrence (host argsort of `groups` row ids)

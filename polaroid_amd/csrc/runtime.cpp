@@ -3,8 +3,12 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "plgpu_internal.hpp"
@@ -28,46 +32,85 @@ int hip_fail(hipError_t e, const char* what) {
 
 hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
-// Stream-ordered caching pool: hipMallocAsync on the device's default memory
-// pool with the release threshold raised so freed blocks stay cached across
-// synchronisations (the bench loop re-allocates the same sizes every step).
-static bool g_pool_ready[64];
-
-static void ensure_pool() {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64 || g_pool_ready[dev]) return;
-    hipMemPool_t pool;
-    if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
-        uint64_t thr = ~0ull;
-        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
-    }
-    (void)hipGetLastError();
-    g_pool_ready[dev] = true;
+// Caching device allocator.  Blocks come from hipMalloc and are recycled
+// through size-keyed free lists instead of being returned with hipFree
+// (which synchronises the device).  Every entry point enqueues its work on
+// one stream and frees only after the kernels that use a block were
+// enqueued, so stream order makes reuse safe.  (hipMallocAsync's default
+// pool was measured to lose writes into a recycled block on this ROCm
+// build, see DESIGN.md "Allocator"; it is not used.)
+namespace {
+struct Pool {
+    std::mutex mu;
+    std::multimap<size_t, void*> free_blocks;        // size -> ptr
+    std::unordered_map<void*, size_t> sizes;         // every block we own
+    size_t cached = 0;
+};
+Pool& pool_for(int dev) {
+    static Pool pools[64];
+    return pools[(dev >= 0 && dev < 64) ? dev : 0];
 }
+size_t round_bytes(size_t b) {
+    if (b <= (size_t(1) << 20)) return (b + 255) & ~size_t(255);
+    return (b + (size_t(2) << 20) - 1) & ~((size_t(2) << 20) - 1);  // 2 MiB granules
+}
+void release_cached(Pool& P) {
+    for (auto& kv : P.free_blocks) {
+        (void)hipFree(kv.second);
+        P.sizes.erase(kv.second);
+    }
+    P.free_blocks.clear();
+    P.cached = 0;
+}
+}  // namespace
 
 int dev_alloc(void** p, size_t bytes, hipStream_t s) {
+    (void)s;
     *p = nullptr;
-    if (bytes == 0) bytes = 256;
-    ensure_pool();
-    hipError_t e = hipMallocAsync(p, bytes, s);
+    const size_t want = round_bytes(bytes == 0 ? 256 : bytes);
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    Pool& P = pool_for(dev);
+    std::lock_guard<std::mutex> lk(P.mu);
+    auto it = P.free_blocks.lower_bound(want);
+    if (it != P.free_blocks.end() && it->first <= want + want / 4) {
+        *p = it->second;
+        P.cached -= it->first;
+        P.free_blocks.erase(it);
+        return PLGPU_OK;
+    }
+    hipError_t e = hipMalloc(p, want);
     if (e != hipSuccess) {
         (void)hipGetLastError();
-        e = hipMalloc(p, bytes);
+        (void)hipDeviceSynchronize();
+        release_cached(P);
+        e = hipMalloc(p, want);
         if (e != hipSuccess) {
+            (void)hipGetLastError();
+            *p = nullptr;
             char buf[128];
             snprintf(buf, sizeof buf, "device allocation of %zu bytes failed", bytes);
             return fail(PLGPU_ERR_OOM, buf);
         }
     }
+    P.sizes[*p] = want;
     return PLGPU_OK;
 }
 
 void dev_free(void* p, hipStream_t s) {
+    (void)s;
     if (p == nullptr) return;
-    if (hipFreeAsync(p, s) != hipSuccess) {
-        (void)hipGetLastError();
-        (void)hipFree(p);
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    Pool& P = pool_for(dev);
+    std::lock_guard<std::mutex> lk(P.mu);
+    auto it = P.sizes.find(p);
+    if (it == P.sizes.end()) {
+        (void)hipFree(p);  // not ours: release directly
+        return;
     }
+    P.free_blocks.emplace(it->second, p);
+    P.cached += it->second;
 }
 
 static void release_owned(plgpu_column* c) {

@@ -500,11 +500,13 @@ def _eval(expr: Expr, df: DataFrame) -> Series:
 
 
 def _filter(df: DataFrame, pred: Expr) -> DataFrame:
-    used, prog, n = _program(pred, df)
     names = df.columns
-    if not used:
-        # literal predicate: broadcast over the frame via a column of it
-        raise N.InvalidOperationError("literal-only predicates are not supported on the GPU executor")
+    if not pred.meta_root_names():
+        # Constant predicate (plan-time simplification, as polars'
+        # simplify_expression does): keep every row or none.
+        keep = _const_bool(pred)
+        return DataFrame([s if keep else s.slice(0, 0) for s in df._cols.values()])
+    used, prog, n = _program(pred, df)
     # The fused path evaluates the predicate inside the compaction kernels; the
     # predicate's columns must be in the same call, so compact in chunks of up
     # to 8 columns that always carry the predicate columns first.
@@ -525,6 +527,27 @@ def _filter(df: DataFrame, pred: Expr) -> DataFrame:
 
 
 _AGG_CODE = N.AGG
+
+
+def _const_bool(e: Expr):
+    """Kleene evaluation of a column-free boolean predicate (null -> drop)."""
+    def ev(x: Expr):
+        if x.kind == "alias":
+            return ev(x.args[0])
+        if x.kind == "lit":
+            if x.value is None or isinstance(x.value, bool):
+                return x.value
+            raise N.ComputeError("filter predicate must be of type `Boolean`")
+        if x.kind == "un" and x.op == "not":
+            v = ev(x.args[0])
+            return None if v is None else not v
+        if x.kind == "bin" and x.op in ("&", "|"):
+            a, b = ev(x.args[0]), ev(x.args[1])
+            if x.op == "&":
+                return False if (a is False or b is False) else (None if (a is None or b is None) else True)
+            return True if (a is True or b is True) else (None if (a is None or b is None) else False)
+        raise N.InvalidOperationError(f"unsupported constant predicate {x!r}")
+    return ev(e) is True
 
 
 def _group_by(df: DataFrame, key: str, aggs: list[Expr], maintain_order: bool,
