@@ -7,17 +7,22 @@
 // polars-core/src/frame/group_by/aggregations/mod.rs:581 (agg_sum).
 //
 // Design:
-//  * one persistent launch streams the key + referenced columns once,
-//    coalesced, evaluating the predicate in registers (no mask column);
+//  * a planning launch samples the key column (distinct-key estimate, sizes
+//    the LDS and global tables) and the summed f64 columns (max exponent ->
+//    fixed-point window);
+//  * one persistent launch streams the key + referenced columns once with
+//    16-byte loads, four rows per thread issued before any is consumed,
+//    evaluating the predicate in registers (no mask column);
 //  * each workgroup owns an LDS open-addressing table (key -> slot) whose
 //    accumulators are updated with LDS atomics; rows whose key does not fit
-//    the LDS table go straight to the global table (device-scope atomics);
+//    go straight to the global table (device-scope atomics); when the key
+//    sample says the groups cannot fit LDS at all, the LDS stage is skipped;
 //  * at the end each workgroup folds its LDS table into the global table;
-//  * f64 sums are exact: every value is converted to a 120-bit fixed-point
-//    integer (3 carry-free 40-bit limbs in LDS, one 192-bit two's-complement
-//    integer per group in HBM) and rounded once at the end, so the result is
-//    the correctly rounded sum, independent of the order of arrival — the
-//    deterministic answer that Kahan / naive row-order folds approximate.
+//  * f64 sums are exact: every value becomes a 120-bit fixed-point integer
+//    (3 carry-free 40-bit limbs in LDS, one 192-bit two's-complement integer
+//    per group in HBM), rounded once at the end: the correctly rounded sum,
+//    independent of arrival order — the deterministic answer the reference's
+//    Kahan / naive row-order folds approximate.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -34,11 +39,13 @@ namespace plgpu {
 constexpr int kGbThreads = 512;
 constexpr int kMaxAcc = 6;
 constexpr int kMaxFields = 48;
-constexpr int kLdsProbe = 32;
+constexpr int kLdsProbe = 16;
 constexpr int kGlobalProbe = 4096;
 constexpr int kSumWindowBits = 120;   // fixed-point window of one value
 constexpr int kHeadroomBinades = 8;   // above the sampled max exponent
 constexpr int64_t kMaxRowsPerWg = int64_t(1) << 22;  // keeps 40-bit limbs exact in int64
+constexpr int kPlanSamples = 65536;
+constexpr int kPlanSetSlots = 4096;   // LDS hash set of the distinct-key sample (32 KiB)
 
 // Acc flags
 enum : int32_t { A_FSUM = 1, A_FSUMCAST = 2, A_ISUM = 4, A_CNT = 8, A_MIN = 16, A_MAX = 32, A_FLAGS = 64 };
@@ -52,15 +59,18 @@ enum : int {
     ST_SELECTED = 3,
     ST_SPECIAL = 4,      // bit0 null group present, bit1 INT64_MIN group present
     ST_GROUPS_OUT = 5,   // finalize counter
+    ST_DISTINCT = 6,     // plan: distinct keys in the sample (saturates at kPlanSetSlots/2)
+    ST_SAMPLED = 7,      // plan: keys sampled
     ST_MAXEX = 8,        // + acc
     ST_FXFLAGS = 16,     // + acc: bit0 overflow, bit1 inexact
     ST_WORDS = 24
 };
 
 struct AccSpec {
-    int32_t col;
+    DevCol c;         // the aggregated column
     int32_t flags;
-    int32_t f_sum;    // FSUM/FSUMCAST: 3 limb fields; ISUM: 1 field
+    int32_t isf;      // column is f64 (compared / summed as f64)
+    int32_t f_sum;    // FSUM/FSUMCAST: 3 limb fields
     int32_t f_isum;
     int32_t f_cnt;
     int32_t f_min;
@@ -70,18 +80,25 @@ struct AccSpec {
 
 struct GbParams {
     DevCol key;
-    DevCol cols[PLGPU_MAX_COLS];
+    DevCol cols[PLGPU_MAX_COLS];  // all input columns (program predicates)
+    DevCol pred_col;              // simple predicate column
     int64_t n;
+    int64_t row_begin;            // generic kernel: first row it owns
+    int64_t n_full;               // fast kernel: rows [0, n_full), a multiple of its tile
+    int32_t ablate;               // timing experiments only (PLGPU_ABLATE); 0 in production
+    int32_t _pad2;
     int32_t nacc;
     int32_t nfields;
     AccSpec acc[kMaxAcc];
+    uint64_t desc[kMaxAcc];  // packed per-acc descriptors (see dfield)
+    int32_t bottom[kMaxAcc]; // fixed-point bottoms of the main launch (by value)
+    int32_t pred_acc;       // acc whose column is the simple predicate's, or -1
     int32_t f_len;
     int32_t f_first;        // -1 unless maintain_order
-    uint64_t min_init_mask; // fields initialised to ~0
     int32_t lbits;
+    uint64_t min_init_mask; // fields initialised to ~0
     int32_t lcap;
     int32_t gbits;
-    int32_t _pad;
     int64_t gcap;
     uint64_t* gtab;         // nfields regions of (gcap + 2) words; field 0 = keys
     const int32_t* bottoms; // [kMaxAcc]
@@ -148,15 +165,13 @@ __device__ __forceinline__ bool fx_limbs(uint64_t b, int bottom, uint64_t& l0, u
     }
     ex_out = ex;
     const int sh = (int)ex - 1075 - bottom;
-    uint64_t lo, hi;
+    unsigned __int128 F;
     if (sh >= 0) {
-        if (sh + 53 > kSumWindowBits) {
+        if (sh > kSumWindowBits - 53) {
             fl |= 1u;
             return false;
         }
-        if (sh == 0) { lo = m; hi = 0; }
-        else if (sh < 64) { lo = m << sh; hi = m >> (64 - sh); }
-        else { lo = 0; hi = m << (sh - 64); }
+        F = (unsigned __int128)m << sh;
     } else {
         const int k = -sh;
         if (k > 53) {
@@ -169,13 +184,12 @@ __device__ __forceinline__ bool fx_limbs(uint64_t b, int bottom, uint64_t& l0, u
         if (rem) fl |= 2u;
         if (rem > half || (rem == half && (q & 1))) ++q;
         if (q == 0) return false;
-        lo = q;
-        hi = 0;
+        F = q;
     }
     constexpr uint64_t M40 = (1ull << 40) - 1;
-    l0 = lo & M40;
-    l1 = ((lo >> 40) | (hi << 24)) & M40;
-    l2 = hi >> 16;
+    l0 = (uint64_t)F & M40;
+    l1 = (uint64_t)(F >> 40) & M40;
+    l2 = (uint64_t)(F >> 80);
     if (b >> 63) {
         l0 = 0ull - l0;
         l1 = 0ull - l1;
@@ -221,241 +235,525 @@ __device__ __forceinline__ uint64_t* gfield(const GbParams& p, int f, int64_t s)
     return p.gtab + (int64_t)f * (p.gcap + 2) + s;
 }
 
-// Per-thread running diagnostics, reduced once per workgroup.
+__device__ __forceinline__ uint64_t widen32(uint32_t v, int32_t dtype) {
+    return dtype == PLGPU_U32 ? (uint64_t)v : (uint64_t)(int64_t)(int32_t)v;
+}
+
+// Two consecutive rows (r0, r0+1) of a column; one 16-byte (8-byte for
+// 32-bit types) load when both are in range and the pair is aligned.
+__device__ __forceinline__ void load_pair(const DevCol& c, int64_t r0, int64_t n, uint64_t& a, uint64_t& b) {
+    const int64_t p = c.offset + r0;
+    const bool wide = c.dtype == PLGPU_F64 || c.dtype == PLGPU_I64;
+    if (r0 + 1 < n && (p & 1) == 0) {
+        if (wide) {
+            const ulonglong2 v = *reinterpret_cast<const ulonglong2*>((const uint64_t*)c.values + p);
+            a = v.x;
+            b = v.y;
+        } else {
+            const uint2 v = *reinterpret_cast<const uint2*>((const uint32_t*)c.values + p);
+            a = widen32(v.x, c.dtype);
+            b = widen32(v.y, c.dtype);
+        }
+    } else {
+        a = r0 < n ? dev_load(c, r0) : 0ull;
+        b = r0 + 1 < n ? dev_load(c, r0 + 1) : 0ull;
+    }
+}
+
+// Per-thread running diagnostics, reduced once per wave.
 struct ThreadDiag {
-    uint32_t maxex[kMaxAcc];
-    uint32_t fxfl[kMaxAcc];
+    uint32_t fxbits;   // 2 bits per acc: overflow (1), inexact (2)
     uint32_t nsel;
     uint32_t nglobal;
+    uint32_t special;
 };
 
-// Apply one selected row to an LDS slot (LDS=true) or a global slot.
-template <bool LDS>
+// Packed per-acc descriptor word (uniform): field indices and flags, so the
+// per-row code walks the accs in a rolled loop with one copy of the logic
+// and only two scalar registers per acc live.
+//   [0,8) flags  [8,16) f_sum  [16,24) f_isum  [24,32) f_cnt
+//   [32,40) f_min  [40,48) f_max  [48,56) f_flags  [56] isf
+// Absent fields are 0xFF.
+__device__ __forceinline__ int dfield(uint64_t d, int sh) { return (int)((d >> sh) & 0xFF); }
+constexpr int kNoField = 0xFF;
+
+// Apply one selected row's aggregated values to slot s of the LDS table
+// (LDS=true) or of the global table.  `v` / `dd` / `bot` are consumed
+// (rotated) in place.
+template <bool LDS, int NA>
 __device__ __forceinline__ void apply_row(const GbParams& p, uint64_t* lds, int L, int64_t s, int64_t row,
-                                          const uint64_t* vals, uint32_t validmask, ThreadDiag& d) {
+                                          uint64_t (&v)[NA], uint32_t vm, uint64_t (&dd)[NA], int (&bot)[NA],
+                                          int nacc, ThreadDiag& diag) {
     auto F = [&](int f) -> unsigned long long* {
         if (LDS) return (unsigned long long*)&lds[f * L + s];
         return (unsigned long long*)gfield(p, f, s);
     };
     atomicAdd(F(p.f_len), 1ull);
     if (p.f_first >= 0) atomicMin(F(p.f_first), (unsigned long long)row);
-#pragma unroll
-    for (int a = 0; a < kMaxAcc; ++a) {
-        if (a >= p.nacc) break;
-        if (!((validmask >> a) & 1u)) continue;
-        const AccSpec& ac = p.acc[a];
-        const uint64_t x = vals[a];
-        if (ac.f_cnt >= 0) atomicAdd(F(ac.f_cnt), 1ull);
-        if (ac.flags & (A_FSUM | A_FSUMCAST | A_MIN | A_MAX)) {
-            const bool isf = (ac.flags & A_FSUMCAST) == 0 && p.cols[ac.col].dtype == PLGPU_F64;
+#pragma unroll 1
+    for (int k = 0; k < nacc; ++k) {
+        const uint64_t d = dd[0];
+        const uint32_t flags = (uint32_t)d & 0xFF;
+        const uint64_t x = v[0];
+        if (vm & 1u) {
+            const int f_cnt = dfield(d, 24);
+            if (f_cnt != kNoField) atomicAdd(F(f_cnt), 1ull);
+            const bool isf = (d >> 56) & 1;
             bool is_nan = false;
+            bool fsum_ok = false;
+            uint64_t sb = x;  // bits summed as f64
             if (isf) {
                 const uint64_t ab = x & 0x7fffffffffffffffull;
                 if (ab >= 0x7ff0000000000000ull) {
-                    uint32_t fl = ab > 0x7ff0000000000000ull ? FL_NAN : ((x >> 63) ? FL_NINF : FL_PINF);
+                    const uint32_t fl = ab > 0x7ff0000000000000ull ? FL_NAN : ((x >> 63) ? FL_NINF : FL_PINF);
                     is_nan = fl == FL_NAN;
-                    atomicOr(F(ac.f_flags), (unsigned long long)fl);
-                } else if (ac.flags & A_FSUM) {
-                    uint64_t l0, l1, l2;
-                    uint32_t ex;
-                    if (fx_limbs(x, p.bottoms[a], l0, l1, l2, d.fxfl[a], ex)) {
-                        d.maxex[a] = d.maxex[a] > ex ? d.maxex[a] : ex;
-                        if (LDS) {
-                            if (l0) atomicAdd(F(ac.f_sum), (unsigned long long)l0);
-                            if (l1) atomicAdd(F(ac.f_sum + 1), (unsigned long long)l1);
-                            if (l2) atomicAdd(F(ac.f_sum + 2), (unsigned long long)l2);
-                        } else {
-                            uint64_t w0, w1, w2;
-                            limbs_to_192((int64_t)l0, (int64_t)l1, (int64_t)l2, w0, w1, w2);
-                            g_add192((uint64_t*)F(ac.f_sum), (uint64_t*)F(ac.f_sum + 1), (uint64_t*)F(ac.f_sum + 2),
-                                     w0, w1, w2);
-                        }
-                    }
+                    atomicOr(F(dfield(d, 48)), (unsigned long long)fl);
+                } else {
+                    fsum_ok = (flags & A_FSUM) != 0;
                 }
+            } else if (flags & A_FSUMCAST) {
+                sb = f64_bits((double)(int64_t)x);
+                fsum_ok = true;
             }
-            if (ac.flags & A_FSUMCAST) {
+            if (fsum_ok) {
                 uint64_t l0, l1, l2;
-                uint32_t ex;
-                const uint64_t xb = f64_bits((double)(int64_t)x);
-                if (fx_limbs(xb, p.bottoms[a], l0, l1, l2, d.fxfl[a], ex)) {
-                    d.maxex[a] = d.maxex[a] > ex ? d.maxex[a] : ex;
+                uint32_t ex = 0, fl = 0;
+                const bool ok = fx_limbs(sb, bot[0], l0, l1, l2, fl, ex);
+                diag.fxbits |= fl << (2 * k);
+                if (ok) {
+                    const int f = dfield(d, 8);
                     if (LDS) {
-                        if (l0) atomicAdd(F(ac.f_sum), (unsigned long long)l0);
-                        if (l1) atomicAdd(F(ac.f_sum + 1), (unsigned long long)l1);
-                        if (l2) atomicAdd(F(ac.f_sum + 2), (unsigned long long)l2);
+                        atomicAdd(F(f), (unsigned long long)l0);
+                        atomicAdd(F(f + 1), (unsigned long long)l1);
+                        atomicAdd(F(f + 2), (unsigned long long)l2);
                     } else {
                         uint64_t w0, w1, w2;
                         limbs_to_192((int64_t)l0, (int64_t)l1, (int64_t)l2, w0, w1, w2);
-                        g_add192((uint64_t*)F(ac.f_sum), (uint64_t*)F(ac.f_sum + 1), (uint64_t*)F(ac.f_sum + 2), w0,
-                                 w1, w2);
+                        g_add192((uint64_t*)F(f), (uint64_t*)F(f + 1), (uint64_t*)F(f + 2), w0, w1, w2);
                     }
                 }
             }
-            if ((ac.flags & (A_MIN | A_MAX)) && !is_nan) {
+            if ((flags & (A_MIN | A_MAX)) && !is_nan) {
                 const uint64_t o = isf ? ord_f64(x) : ord_i64(x);
-                if (ac.flags & A_MIN) atomicMin(F(ac.f_min), (unsigned long long)o);
-                if (ac.flags & A_MAX) atomicMax(F(ac.f_max), (unsigned long long)o);
+                if (flags & A_MIN) atomicMin(F(dfield(d, 32)), (unsigned long long)o);
+                if (flags & A_MAX) atomicMax(F(dfield(d, 40)), (unsigned long long)o);
             }
+            if (flags & A_ISUM) atomicAdd(F(dfield(d, 16)), (unsigned long long)x);
         }
-        if (ac.flags & A_ISUM) atomicAdd(F(ac.f_isum), (unsigned long long)x);
+        // rotate the per-acc registers (static moves, no indexed access)
+#pragma unroll
+        for (int i = 0; i + 1 < NA; ++i) {
+            v[i] = v[i + 1];
+            dd[i] = dd[i + 1];
+            bot[i] = bot[i + 1];
+        }
+        vm >>= 1;
     }
 }
 
-template <int PRED, int KEYW>  // PRED: 0 none, 1 simple, 2 program; KEYW: 4 / 8 bytes
-__global__ __launch_bounds__(kGbThreads) void gb_kernel(GbParams p, DevProgram prog) {
-    extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
-    const int L = p.lcap + 2;
-    for (int i = threadIdx.x; i < p.nfields * L; i += blockDim.x) {
-        const int f = i / L;
-        lds[i] = f == 0 ? kEmptyKey : (((p.min_init_mask >> f) & 1ull) ? ~0ull : 0ull);
+// Row on the global table.  kvalid=false -> null group slot.
+template <int NA>
+__device__ __forceinline__ void global_row(const GbParams& p, uint64_t key, bool kvalid, int64_t row,
+                                           uint64_t (&v)[NA], uint32_t vm, uint64_t (&dd)[NA], int (&bot)[NA],
+                                           int nacc, ThreadDiag& diag) {
+    int64_t gs;
+    if (!kvalid) gs = p.gcap;
+    else if (key == kEmptyKey) gs = p.gcap + 1;
+    else gs = g_find(p, key);
+    if (gs < 0) {
+        atomicAdd((unsigned long long*)&p.status[ST_TABLE_FULL], 1ull);
+        return;
     }
-    ThreadDiag d;
-#pragma unroll
-    for (int a = 0; a < kMaxAcc; ++a) { d.maxex[a] = 0; d.fxfl[a] = 0; }
-    d.nsel = 0;
-    d.nglobal = 0;
-    __syncthreads();
+    if (gs >= p.gcap) diag.special |= gs == p.gcap ? 1u : 2u;
+    apply_row<false, NA>(p, nullptr, 0, gs, row, v, vm, dd, bot, nacc, diag);
+}
 
-    const int64_t n = p.n;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += stride) {
-        // ---- predicate
-        bool sel = true;
-        if (PRED == 1) {
-            const DevCol& c = p.cols[prog.simple_col];
-            sel = dev_valid(c, r) && simple_pred(prog.simple_isf, prog.simple_op, dev_load(c, r), prog.simple_imm);
-        } else if (PRED == 2) {
-            RowVal rv = eval_row(prog.code, prog.n, p.cols, r);
-            sel = rv.valid && (rv.v & 1);
-        }
-        if (!sel) continue;
-        // ---- loads (key + aggregated columns)
-        const int64_t kp = p.key.offset + r;
-        const uint64_t key = KEYW == 8 ? ((const uint64_t*)p.key.values)[kp]
-                                       : (uint64_t)(int64_t)((const int32_t*)p.key.values)[kp];
-        const bool kvalid = dev_valid(p.key, r);
-        uint64_t vals[kMaxAcc];
-        uint32_t vmask = 0;
-#pragma unroll
-        for (int a = 0; a < kMaxAcc; ++a) {
-            vals[a] = 0;
-            if (a < p.nacc) {
-                const DevCol& c = p.cols[p.acc[a].col];
-                vals[a] = dev_load(c, r);
-                vmask |= dev_valid(c, r) ? (1u << a) : 0u;
-            }
-        }
-        ++d.nsel;
-        int s;
-        if (!kvalid) s = p.lcap;
-        else if (key == kEmptyKey) s = p.lcap + 1;
-        else s = lds_find(lds, p.lbits, p.lcap, key);
-        if (s >= 0) {
-            apply_row<true>(p, lds, L, s, r, vals, vmask, d);
-        } else {
-            ++d.nglobal;
-            const int64_t gs = g_find(p, key);
-            if (gs < 0) {
-                atomicAdd((unsigned long long*)&p.status[ST_TABLE_FULL], 1ull);
+// End of a main launch: fold the workgroup's LDS table into the global
+// table, then publish the per-thread diagnostics (one atomic per wave).
+template <bool USE_LDS>
+__device__ __forceinline__ void flush_and_report(const GbParams& p, uint64_t* lds, int L, ThreadDiag& d) {
+    if (USE_LDS) {
+        __syncthreads();
+        for (int s = threadIdx.x; s < L; s += blockDim.x) {
+            const uint64_t len = lds[p.f_len * L + s];
+            if (len == 0) continue;
+            int64_t gs;
+            if (s == p.lcap) {
+                gs = p.gcap;
+                d.special |= 1u;
+            } else if (s == p.lcap + 1) {
+                gs = p.gcap + 1;
+                d.special |= 2u;
             } else {
-                apply_row<false>(p, lds, L, gs, r, vals, vmask, d);
+                gs = g_find(p, lds[s]);
+                if (gs < 0) {
+                    atomicAdd((unsigned long long*)&p.status[ST_TABLE_FULL], 1ull);
+                    continue;
+                }
+            }
+            atomicAdd((unsigned long long*)gfield(p, p.f_len, gs), (unsigned long long)len);
+            if (p.f_first >= 0)
+                atomicMin((unsigned long long*)gfield(p, p.f_first, gs), (unsigned long long)lds[p.f_first * L + s]);
+            for (int a = 0; a < p.nacc; ++a) {
+                const AccSpec& ac = p.acc[a];
+                if (ac.f_cnt >= 0) {
+                    const uint64_t v = lds[ac.f_cnt * L + s];
+                    if (v) atomicAdd((unsigned long long*)gfield(p, ac.f_cnt, gs), (unsigned long long)v);
+                }
+                if (ac.flags & (A_FSUM | A_FSUMCAST)) {
+                    uint64_t w0, w1, w2;
+                    limbs_to_192((int64_t)lds[ac.f_sum * L + s], (int64_t)lds[(ac.f_sum + 1) * L + s],
+                                 (int64_t)lds[(ac.f_sum + 2) * L + s], w0, w1, w2);
+                    g_add192(gfield(p, ac.f_sum, gs), gfield(p, ac.f_sum + 1, gs), gfield(p, ac.f_sum + 2, gs), w0,
+                             w1, w2);
+                }
+                if (ac.flags & A_ISUM) {
+                    const uint64_t v = lds[ac.f_isum * L + s];
+                    if (v) atomicAdd((unsigned long long*)gfield(p, ac.f_isum, gs), (unsigned long long)v);
+                }
+                if (ac.flags & A_MIN) {
+                    const uint64_t v = lds[ac.f_min * L + s];
+                    if (v != ~0ull) atomicMin((unsigned long long*)gfield(p, ac.f_min, gs), (unsigned long long)v);
+                }
+                if (ac.flags & A_MAX) {
+                    const uint64_t v = lds[ac.f_max * L + s];
+                    if (v) atomicMax((unsigned long long*)gfield(p, ac.f_max, gs), (unsigned long long)v);
+                }
+                if (ac.f_flags >= 0) {
+                    const uint64_t v = lds[ac.f_flags * L + s];
+                    if (v) atomicOr((unsigned long long*)gfield(p, ac.f_flags, gs), (unsigned long long)v);
+                }
             }
         }
     }
-    __syncthreads();
-
-    // ---- fold the LDS table into the global table
-    for (int s = threadIdx.x; s < L; s += blockDim.x) {
-        const uint64_t len = lds[p.f_len * L + s];
-        if (len == 0) continue;
-        int64_t gs;
-        if (s == p.lcap) {
-            gs = p.gcap;
-            atomicOr((unsigned long long*)&p.status[ST_SPECIAL], 1ull);
-        } else if (s == p.lcap + 1) {
-            gs = p.gcap + 1;
-            atomicOr((unsigned long long*)&p.status[ST_SPECIAL], 2ull);
-        } else {
-            gs = g_find(p, lds[s]);
-            if (gs < 0) {
-                atomicAdd((unsigned long long*)&p.status[ST_TABLE_FULL], 1ull);
-                continue;
-            }
-        }
-        atomicAdd((unsigned long long*)gfield(p, p.f_len, gs), (unsigned long long)len);
-        if (p.f_first >= 0)
-            atomicMin((unsigned long long*)gfield(p, p.f_first, gs), (unsigned long long)lds[p.f_first * L + s]);
-        for (int a = 0; a < p.nacc; ++a) {
-            const AccSpec& ac = p.acc[a];
-            if (ac.f_cnt >= 0) {
-                const uint64_t v = lds[ac.f_cnt * L + s];
-                if (v) atomicAdd((unsigned long long*)gfield(p, ac.f_cnt, gs), (unsigned long long)v);
-            }
-            if (ac.flags & (A_FSUM | A_FSUMCAST)) {
-                uint64_t w0, w1, w2;
-                limbs_to_192((int64_t)lds[ac.f_sum * L + s], (int64_t)lds[(ac.f_sum + 1) * L + s],
-                             (int64_t)lds[(ac.f_sum + 2) * L + s], w0, w1, w2);
-                g_add192(gfield(p, ac.f_sum, gs), gfield(p, ac.f_sum + 1, gs), gfield(p, ac.f_sum + 2, gs), w0, w1,
-                         w2);
-            }
-            if (ac.flags & A_ISUM) {
-                const uint64_t v = lds[ac.f_isum * L + s];
-                if (v) atomicAdd((unsigned long long*)gfield(p, ac.f_isum, gs), (unsigned long long)v);
-            }
-            if (ac.flags & A_MIN) {
-                const uint64_t v = lds[ac.f_min * L + s];
-                if (v != ~0ull) atomicMin((unsigned long long*)gfield(p, ac.f_min, gs), (unsigned long long)v);
-            }
-            if (ac.flags & A_MAX) {
-                const uint64_t v = lds[ac.f_max * L + s];
-                if (v) atomicMax((unsigned long long*)gfield(p, ac.f_max, gs), (unsigned long long)v);
-            }
-            if (ac.f_flags >= 0) {
-                const uint64_t v = lds[ac.f_flags * L + s];
-                if (v) atomicOr((unsigned long long*)gfield(p, ac.f_flags, gs), (unsigned long long)v);
-            }
-        }
-    }
-
-    // ---- diagnostics: one atomic per wave
     uint64_t nsel = d.nsel, nglob = d.nglobal;
+    uint32_t special = d.special, fx = d.fxbits;
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
         nsel += __shfl_xor(nsel, off, 64);
         nglob += __shfl_xor(nglob, off, 64);
+        special |= __shfl_xor(special, off, 64);
+        fx |= __shfl_xor(fx, off, 64);
     }
-    const int lane = threadIdx.x & 63;
-    if (lane == 0) {
+    if ((threadIdx.x & 63) == 0) {
         if (nsel) atomicAdd((unsigned long long*)&p.status[ST_SELECTED], (unsigned long long)nsel);
         if (nglob) atomicAdd((unsigned long long*)&p.status[ST_GLOBAL_ROWS], (unsigned long long)nglob);
-    }
-#pragma unroll
-    for (int a = 0; a < kMaxAcc; ++a) {
-        uint32_t mx = d.maxex[a], fl = d.fxfl[a];
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
-            const uint32_t o = __shfl_xor(mx, off, 64);
-            mx = mx > o ? mx : o;
-            fl |= __shfl_xor(fl, off, 64);
-        }
-        if (lane == 0 && a < p.nacc) {
-            if (mx) atomicMax((unsigned long long*)&p.status[ST_MAXEX + a], (unsigned long long)mx);
-            if (fl) atomicOr((unsigned long long*)&p.status[ST_FXFLAGS + a], (unsigned long long)fl);
-        }
+        if (special) atomicOr((unsigned long long*)&p.status[ST_SPECIAL], (unsigned long long)special);
+        if (fx) atomicOr((unsigned long long*)&p.status[ST_FXFLAGS], (unsigned long long)fx);
     }
 }
 
-// Sampled max exponent -> fixed-point bottom, one workgroup per acc.
-__global__ __launch_bounds__(256) void gb_sample_kernel(GbParams p, int32_t* bottoms, int64_t samples) {
+template <int NA>
+__device__ __forceinline__ void load_descs(const GbParams& p, uint64_t (&dd)[NA], int (&bot)[NA]) {
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+        // kernel-argument values: no memory access inside the row loop (a
+        // load there would wait for the prefetched tile / LDS atomics)
+        dd[a] = a < p.nacc ? p.desc[a] : 0ull;
+        bot[a] = a < p.nacc ? p.bottom[a] : 0;
+    }
+}
+
+__device__ __forceinline__ void init_lds(const GbParams& p, uint64_t* lds, int L) {
+    for (int f = 0; f < p.nfields; ++f) {
+        const uint64_t v = f == 0 ? kEmptyKey : (((p.min_init_mask >> f) & 1ull) ? ~0ull : 0ull);
+        for (int i = threadIdx.x; i < L; i += blockDim.x) lds[f * L + i] = v;
+    }
+}
+
+// slot codes of a row within a tile
+constexpr int kNotSelected = -2;
+constexpr int kGlobalKey = -1;
+constexpr int kGlobalNull = -3;
+
+// Generic kernel: any dtype / validity / offset / predicate, rows
+// [row_begin, n) in tiles of four rows per thread.
+template <int PRED, bool USE_LDS>  // PRED: 0 none, 1 simple, 2 program
+__global__ __launch_bounds__(kGbThreads) void gb_kernel(GbParams p, DevProgram prog) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+    const int L = p.lcap + 2;
+    if (USE_LDS) init_lds(p, lds, L);
+    ThreadDiag d = {0u, 0u, 0u, 0u};
+    const int nacc = p.nacc;
+    uint64_t dd0[kMaxAcc];
+    int bot0[kMaxAcc];
+    load_descs(p, dd0, bot0);
+    if (USE_LDS) __syncthreads();
+
+    const int64_t n = p.n;
+    const int T = blockDim.x;
+    const int64_t tile = (int64_t)T * 4;
+    for (int64_t base = p.row_begin + (int64_t)blockIdx.x * tile; base < n; base += (int64_t)gridDim.x * tile) {
+        const int64_t r0 = base + 2 * threadIdx.x;
+        const int64_t r2 = r0 + 2 * T;
+        uint64_t key[4], pv[4];
+        uint64_t v[kMaxAcc][4];
+        load_pair(p.key, r0, n, key[0], key[1]);
+        load_pair(p.key, r2, n, key[2], key[3]);
+#pragma unroll
+        for (int a = 0; a < kMaxAcc; ++a) {
+            if (a < nacc) {
+                load_pair(p.acc[a].c, r0, n, v[a][0], v[a][1]);
+                load_pair(p.acc[a].c, r2, n, v[a][2], v[a][3]);
+            } else {
+                v[a][0] = v[a][1] = v[a][2] = v[a][3] = 0;
+            }
+        }
+        if (PRED == 1 && p.pred_acc < 0) {
+            load_pair(p.pred_col, r0, n, pv[0], pv[1]);
+            load_pair(p.pred_col, r2, n, pv[2], pv[3]);
+        }
+        int slot[4];
+        uint32_t vm[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int64_t r = (j < 2 ? r0 : r2) + (j & 1);
+            bool sel = r < n;
+            if (sel && PRED == 1) {
+                uint64_t x = pv[j];
+#pragma unroll
+                for (int a = 0; a < kMaxAcc; ++a)
+                    if (a == p.pred_acc) x = v[a][j];
+                sel = dev_valid(p.pred_col, r) && simple_pred(prog.simple_isf, prog.simple_op, x, prog.simple_imm);
+            } else if (sel && PRED == 2) {
+                const RowVal rv = eval_row(prog.code, prog.n, p.cols, r);
+                sel = rv.valid && (rv.v & 1);
+            }
+            vm[j] = 0;
+            slot[j] = kNotSelected;
+            if (sel) {
+#pragma unroll
+                for (int a = 0; a < kMaxAcc; ++a)
+                    if (a < nacc && dev_valid(p.acc[a].c, r)) vm[j] |= 1u << a;
+                if (!dev_valid(p.key, r)) slot[j] = USE_LDS ? p.lcap : kGlobalNull;
+                else if (USE_LDS && key[j] == kEmptyKey) slot[j] = p.lcap + 1;
+                else slot[j] = kGlobalKey;
+            }
+        }
+#pragma unroll 1
+        for (int j = 0; j < 4; ++j) {
+            const int64_t r = (j < 2 ? r0 : r2) + (j & 1);
+            int s = slot[0];
+            if (s != kNotSelected) {
+                ++d.nsel;
+                uint64_t rv[kMaxAcc], dd[kMaxAcc];
+                int bot[kMaxAcc];
+#pragma unroll
+                for (int a = 0; a < kMaxAcc; ++a) {
+                    rv[a] = v[a][0];
+                    dd[a] = dd0[a];
+                    bot[a] = bot0[a];
+                }
+                if (USE_LDS && s == kGlobalKey) s = lds_find(lds, p.lbits, p.lcap, key[0]);
+                if (s >= 0) {
+                    apply_row<true, kMaxAcc>(p, lds, L, s, r, rv, vm[0], dd, bot, nacc, d);
+                } else {
+                    ++d.nglobal;
+                    global_row<kMaxAcc>(p, key[0], s != kGlobalNull, r, rv, vm[0], dd, bot, nacc, d);
+                }
+            }
+            slot[0] = slot[1]; slot[1] = slot[2]; slot[2] = slot[3];
+            vm[0] = vm[1]; vm[1] = vm[2]; vm[2] = vm[3];
+            key[0] = key[1]; key[1] = key[2]; key[2] = key[3];
+#pragma unroll
+            for (int a = 0; a < kMaxAcc; ++a) {
+                v[a][0] = v[a][1];
+                v[a][1] = v[a][2];
+                v[a][2] = v[a][3];
+            }
+        }
+    }
+    flush_and_report<USE_LDS>(p, lds, L, d);
+}
+
+// ------------------------------------------------------------- fast path
+// Common case: no validity bitmaps, 8-byte key and aggregated columns at
+// even offsets of 16-byte aligned buffers, no predicate or `col <cmp> lit`,
+// LDS table in use.  Rows [0, n_full) in tiles of 4 rows per thread; the
+// tail and every other case go through gb_kernel.  Loads of the next tile
+// are issued before the current tile's LDS atomics, so HBM reads overlap
+// the aggregation.
+template <int NACC>
+struct FastTile {
+    uint64_t key[4];
+    uint64_t v[NACC > 0 ? NACC : 1][4];
+    uint64_t pv[4];
+};
+
+template <int NACC, int PRED>
+__device__ __forceinline__ void fast_load(const GbParams& p, int64_t t, FastTile<NACC>& x) {
+    const int T = blockDim.x;
+    const int64_t r0 = t * (int64_t)T * 4 + 2 * threadIdx.x;
+    const int64_t r2 = r0 + 2 * T;
+    const uint64_t* kp = (const uint64_t*)p.key.values + p.key.offset;
+    ulonglong2 a = *reinterpret_cast<const ulonglong2*>(kp + r0);
+    ulonglong2 b = *reinterpret_cast<const ulonglong2*>(kp + r2);
+    x.key[0] = a.x; x.key[1] = a.y; x.key[2] = b.x; x.key[3] = b.y;
+#pragma unroll
+    for (int c = 0; c < NACC; ++c) {
+        const uint64_t* vp = (const uint64_t*)p.acc[c].c.values + p.acc[c].c.offset;
+        a = *reinterpret_cast<const ulonglong2*>(vp + r0);
+        b = *reinterpret_cast<const ulonglong2*>(vp + r2);
+        x.v[c][0] = a.x; x.v[c][1] = a.y; x.v[c][2] = b.x; x.v[c][3] = b.y;
+    }
+    if (PRED == 1 && p.pred_acc < 0) {
+        const uint64_t* pp = (const uint64_t*)p.pred_col.values + p.pred_col.offset;
+        a = *reinterpret_cast<const ulonglong2*>(pp + r0);
+        b = *reinterpret_cast<const ulonglong2*>(pp + r2);
+        x.pv[0] = a.x; x.pv[1] = a.y; x.pv[2] = b.x; x.pv[3] = b.y;
+    }
+}
+
+template <int NACC, int PRED>
+__global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProgram prog) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+    constexpr int NA = NACC > 0 ? NACC : 1;
+    const int L = p.lcap + 2;
+    init_lds(p, lds, L);
+    ThreadDiag d = {0u, 0u, 0u, 0u};
+    uint64_t dd0[NA];
+    int bot0[NA];
+    load_descs(p, dd0, bot0);
+    __syncthreads();
+
+    const int T = blockDim.x;
+    const int64_t ntiles = p.n_full / ((int64_t)T * 4);
+    constexpr uint32_t VM = (1u << NACC) - 1u;
+    int64_t t = blockIdx.x;
+    FastTile<NACC> cur;
+    if (t < ntiles) fast_load<NACC, PRED>(p, t, cur);
+    for (; t < ntiles; t += gridDim.x) {
+        const int64_t r0 = t * (int64_t)T * 4 + 2 * threadIdx.x;
+        const int64_t r2 = r0 + 2 * T;
+        // ---- predicate + batched LDS probes of the four rows
+        int slot[4];
+        uint64_t probe[4];
+        uint32_t h[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            bool sel = true;
+            if (PRED == 1) {
+                uint64_t x = cur.pv[j];
+#pragma unroll
+                for (int a = 0; a < NACC; ++a)
+                    if (a == p.pred_acc) x = cur.v[a][j];
+                sel = simple_pred(prog.simple_isf, prog.simple_op, x, prog.simple_imm);
+            }
+            slot[j] = sel ? (cur.key[j] == kEmptyKey ? p.lcap + 1 : kGlobalKey) : kNotSelected;
+            h[j] = hash_slot(cur.key[j], p.lbits);
+            probe[j] = lds_load(&lds[h[j]]);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (slot[j] == kGlobalKey && probe[j] == cur.key[j]) slot[j] = (int)h[j];
+        // ---- next tile's loads go out before this tile's atomics
+        FastTile<NACC> nxt;
+        const int64_t tn = t + gridDim.x;
+        if (tn < ntiles) fast_load<NACC, PRED>(p, tn, nxt);
+        // ---- apply rows one at a time (rolled; arrays shift statically)
+#pragma unroll 1
+        for (int j = 0; j < 4; ++j) {
+            const int64_t r = (j < 2 ? r0 : r2) + (j & 1);
+            int s = slot[0];
+            if (s != kNotSelected) {
+                ++d.nsel;
+                uint64_t rv[NA], dd[NA];
+                int bot[NA];
+#pragma unroll
+                for (int a = 0; a < NA; ++a) {
+                    rv[a] = cur.v[a][0];
+                    dd[a] = dd0[a];
+                    bot[a] = bot0[a];
+                }
+                if (s == kGlobalKey) s = lds_find(lds, p.lbits, p.lcap, cur.key[0]);
+                if (s >= 0) {
+                    apply_row<true, NA>(p, lds, L, s, r, rv, VM, dd, bot, NACC, d);
+                } else {
+                    ++d.nglobal;
+                    global_row<NA>(p, cur.key[0], true, r, rv, VM, dd, bot, NACC, d);
+                }
+            }
+            slot[0] = slot[1]; slot[1] = slot[2]; slot[2] = slot[3];
+            cur.key[0] = cur.key[1]; cur.key[1] = cur.key[2]; cur.key[2] = cur.key[3];
+#pragma unroll
+            for (int a = 0; a < NACC; ++a) {
+                cur.v[a][0] = cur.v[a][1];
+                cur.v[a][1] = cur.v[a][2];
+                cur.v[a][2] = cur.v[a][3];
+            }
+        }
+        cur = nxt;
+    }
+    flush_and_report<true>(p, lds, L, d);
+}
+
+// Exact max exponent of a summed column (rerun path only: refits the
+// fixed-point window after an overflow / inexact flag).
+__global__ __launch_bounds__(256) void gb_maxexp_kernel(GbParams p, int a) {
+    const AccSpec& ac = p.acc[a];
+    uint32_t mx = 0;
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < p.n; r += (int64_t)gridDim.x * blockDim.x) {
+        if (!dev_valid(ac.c, r)) continue;
+        uint64_t x = dev_load(ac.c, r);
+        if (ac.flags & A_FSUMCAST) x = f64_bits((double)(int64_t)x);
+        const uint32_t ex = (uint32_t)(x >> 52) & 0x7FF;
+        if (ex != 0x7FF && ex > mx) mx = ex;
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const uint32_t o = __shfl_xor(mx, off, 64);
+        mx = mx > o ? mx : o;
+    }
+    if ((threadIdx.x & 63) == 0 && mx) atomicMax((unsigned long long*)&p.status[ST_MAXEX + a], (unsigned long long)mx);
+}
+
+// Planning launch: blocks [0, nacc) sample the summed columns' max exponent
+// (-> fixed-point bottom); block nacc counts distinct keys in a strided
+// sample with an LDS hash set (-> table sizes).
+__global__ __launch_bounds__(256) void gb_plan_kernel(GbParams p, int32_t* bottoms, int64_t samples) {
     __shared__ uint32_t red[256];
+    __shared__ uint64_t set[kPlanSetSlots];
+    __shared__ uint32_t distinct;
     const int a = blockIdx.x;
+    const int64_t n = p.n;
+    const int64_t step = n > samples ? n / samples : 1;
+    if (a == p.nacc) {
+        for (int i = threadIdx.x; i < kPlanSetSlots; i += blockDim.x) set[i] = kEmptyKey;
+        if (threadIdx.x == 0) distinct = 0;
+        __syncthreads();
+        const int bits = __builtin_ctz(kPlanSetSlots);
+        for (int64_t i = threadIdx.x; i < samples && i * step < n; i += blockDim.x) {
+            const int64_t r = i * step;
+            if (!dev_valid(p.key, r)) continue;
+            const uint64_t k = dev_load(p.key, r);
+            if (k == kEmptyKey) continue;
+            uint32_t h = hash_slot(k, bits);
+            for (int q = 0; q < 64; ++q) {
+                const uint32_t s = (h + q) & (kPlanSetSlots - 1);
+                uint64_t o = lds_load(&set[s]);
+                if (o == k) break;
+                if (o == kEmptyKey) {
+                    o = atomicCAS((unsigned long long*)&set[s], (unsigned long long)kEmptyKey, (unsigned long long)k);
+                    if (o == kEmptyKey) {
+                        atomicAdd(&distinct, 1u);
+                        break;
+                    }
+                    if (o == k) break;
+                }
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            p.status[ST_DISTINCT] = distinct;
+            p.status[ST_SAMPLED] = (uint64_t)((n + step - 1) / step < samples ? (n + step - 1) / step : samples);
+        }
+        return;
+    }
     const AccSpec& ac = p.acc[a];
     uint32_t mx = 0;
     if (ac.flags & (A_FSUM | A_FSUMCAST)) {
-        const DevCol& c = p.cols[ac.col];
-        const int64_t n = p.n;
-        const int64_t step = n > samples ? n / samples : 1;
-        for (int64_t i = threadIdx.x; i * step < n && i < samples; i += blockDim.x) {
+        const DevCol& c = ac.c;
+        for (int64_t i = threadIdx.x; i < samples && i * step < n; i += blockDim.x) {
             const int64_t r = i * step;
             if (!dev_valid(c, r)) continue;
             uint64_t x = dev_load(c, r);
@@ -473,16 +771,18 @@ __global__ __launch_bounds__(256) void gb_sample_kernel(GbParams p, int32_t* bot
     if (threadIdx.x == 0) {
         int e = red[0] == 0 ? 2046 : (int)red[0] + kHeadroomBinades;
         if (e > 2046) e = 2046;
-        // fits iff ex <= bottom + 1075 + (window - 53)
+        // a value fits iff ex <= bottom + 1075 + (window - 53)
         bottoms[a] = e - 1075 - (kSumWindowBits - 53);
     }
 }
 
 __global__ void gb_init_table_kernel(uint64_t* gtab, int64_t words_per_field, int nfields, uint64_t min_init_mask) {
-    const int64_t total = words_per_field * nfields;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-        const int f = (int)(i / words_per_field);
-        gtab[i] = f == 0 ? kEmptyKey : (((min_init_mask >> f) & 1ull) ? ~0ull : 0ull);
+    for (int f = 0; f < nfields; ++f) {
+        const uint64_t v = f == 0 ? kEmptyKey : (((min_init_mask >> f) & 1ull) ? ~0ull : 0ull);
+        uint64_t* q = gtab + (int64_t)f * words_per_field;
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words_per_field;
+             i += (int64_t)gridDim.x * blockDim.x)
+            q[i] = v;
     }
 }
 
@@ -659,28 +959,31 @@ static int num_cus() {
     return g_num_cus;
 }
 
+static DevCol to_dev(const plgpu_column& c) {
+    DevCol d;
+    std::memset(&d, 0, sizeof d);
+    d.values = c.values;
+    d.validity = c.validity;
+    d.offset = c.offset;
+    d.dtype = c.dtype;
+    return d;
+}
+
 struct Plan {
     GbParams p;
     std::vector<OutSpec> outs;
     int acc_of_agg[64];
     size_t lds_bytes;
     int grid;
+    bool use_lds;
 };
 
 static int plan_groupby(const plgpu_column* key, const plgpu_column* cols, int32_t ncols, const plgpu_agg* aggs,
-                        int32_t naggs, bool maintain_order, Plan* pl) {
+                        int32_t naggs, bool maintain_order, const DevProgram& dp, Plan* pl) {
     GbParams& p = pl->p;
     std::memset(&p, 0, sizeof p);
-    p.key.values = key->values;
-    p.key.validity = key->validity;
-    p.key.offset = key->offset;
-    p.key.dtype = key->dtype;
-    for (int i = 0; i < ncols; ++i) {
-        p.cols[i].values = cols[i].values;
-        p.cols[i].validity = cols[i].validity;
-        p.cols[i].offset = cols[i].offset;
-        p.cols[i].dtype = cols[i].dtype;
-    }
+    p.key = to_dev(*key);
+    for (int i = 0; i < ncols; ++i) p.cols[i] = to_dev(cols[i]);
     p.n = key->length;
     int nf = 1;  // field 0: keys
     p.f_len = nf++;
@@ -689,7 +992,6 @@ static int plan_groupby(const plgpu_column* key, const plgpu_column* cols, int32
     int acc_of_col[PLGPU_MAX_COLS];
     for (int i = 0; i < PLGPU_MAX_COLS; ++i) acc_of_col[i] = -1;
     p.nacc = 0;
-    // pass 1: flags per column
     for (int i = 0; i < naggs; ++i) {
         const int c = aggs[i].col;
         if (c < 0 || c >= ncols) return fail(PLGPU_ERR_INVALID, "aggregation column index out of range");
@@ -701,15 +1003,19 @@ static int plan_groupby(const plgpu_column* key, const plgpu_column* cols, int32
             acc_of_col[c] = p.nacc;
             AccSpec& ac = p.acc[p.nacc++];
             std::memset(&ac, 0xff, sizeof ac);
-            ac.col = c;
+            ac.c = to_dev(cols[c]);
             ac.flags = 0;
+            ac.isf = dt == PLGPU_F64;
         }
         AccSpec& ac = p.acc[acc_of_col[c]];
         const bool isf = dt == PLGPU_F64;
         const bool nullable = cols[c].validity != nullptr;
         switch (aggs[i].kind) {
         case PLGPU_AGG_SUM: ac.flags |= isf ? (A_FSUM | A_FLAGS) : A_ISUM; break;
-        case PLGPU_AGG_MEAN: ac.flags |= isf ? (A_FSUM | A_FLAGS) : A_FSUMCAST; if (nullable) ac.flags |= A_CNT; break;
+        case PLGPU_AGG_MEAN:
+            ac.flags |= isf ? (A_FSUM | A_FLAGS) : A_FSUMCAST;
+            if (nullable) ac.flags |= A_CNT;
+            break;
         case PLGPU_AGG_MIN: ac.flags |= A_MIN | (isf ? A_FLAGS : 0) | A_CNT; break;
         case PLGPU_AGG_MAX: ac.flags |= A_MAX | (isf ? A_FLAGS : 0) | A_CNT; break;
         case PLGPU_AGG_COUNT: if (nullable) ac.flags |= A_CNT; break;
@@ -718,20 +1024,38 @@ static int plan_groupby(const plgpu_column* key, const plgpu_column* cols, int32
         }
         pl->acc_of_agg[i] = acc_of_col[c];
     }
-    // MIN/MAX validity needs a non-null count only when the column is nullable
     for (int a = 0; a < p.nacc; ++a) {
         AccSpec& ac = p.acc[a];
-        if ((ac.flags & A_CNT) && cols[ac.col].validity == nullptr) ac.flags &= ~A_CNT;
-        if (ac.flags & (A_FSUM | A_FSUMCAST)) { ac.f_sum = nf; nf += 3; }
+        if ((ac.flags & A_CNT) && ac.c.validity == nullptr) ac.flags &= ~A_CNT;
+        if (ac.flags & (A_FSUM | A_FSUMCAST)) {
+            ac.f_sum = nf;
+            nf += 3;
+        }
         if (ac.flags & A_ISUM) ac.f_isum = nf++;
         if (ac.flags & A_CNT) ac.f_cnt = nf++;
-        if (ac.flags & A_MIN) { ac.f_min = nf++; p.min_init_mask |= 1ull << ac.f_min; }
+        if (ac.flags & A_MIN) {
+            ac.f_min = nf++;
+            p.min_init_mask |= 1ull << ac.f_min;
+        }
         if (ac.flags & A_MAX) ac.f_max = nf++;
         if (ac.flags & A_FLAGS) ac.f_flags = nf++;
     }
     if (nf > kMaxFields) return fail(PLGPU_ERR_INVALID, "too many accumulator fields");
+    if (nf > 255) return fail(PLGPU_ERR_INVALID, "too many accumulator fields");
     p.nfields = nf;
-    // outputs
+    for (int a = 0; a < p.nacc; ++a) {
+        const AccSpec& ac = p.acc[a];
+        auto fb = [](int f) -> uint64_t { return f < 0 ? (uint64_t)kNoField : (uint64_t)f; };
+        p.desc[a] = (uint64_t)(ac.flags & 0xFF) | (fb(ac.f_sum) << 8) | (fb(ac.f_isum) << 16) | (fb(ac.f_cnt) << 24) |
+                    (fb(ac.f_min) << 32) | (fb(ac.f_max) << 40) | (fb(ac.f_flags) << 48) |
+                    ((uint64_t)(ac.isf ? 1 : 0) << 56);
+    }
+    // simple predicate: reuse an aggregated column's registers when possible
+    p.pred_acc = -1;
+    if (dp.simple) {
+        p.pred_col = to_dev(cols[dp.simple_col]);
+        if (acc_of_col[dp.simple_col] >= 0) p.pred_acc = acc_of_col[dp.simple_col];
+    }
     pl->outs.clear();
     for (int i = 0; i < naggs; ++i) {
         OutSpec o;
@@ -744,54 +1068,102 @@ static int plan_groupby(const plgpu_column* key, const plgpu_column* cols, int32
         case PLGPU_AGG_LEN:
         case PLGPU_AGG_COUNT: o.out_dtype = PLGPU_U32; break;
         case PLGPU_AGG_MEAN: o.out_dtype = PLGPU_F64; break;
-        default: o.out_dtype = dt == PLGPU_F64 ? PLGPU_F64 : (dt == PLGPU_I64 ? PLGPU_I64 : dt); break;
+        default: o.out_dtype = dt; break;
         }
         pl->outs.push_back(o);
     }
-    // LDS sizing: as many slots as fit 80 KiB (two 512-thread workgroups per CU)
-    const size_t budget = 80 * 1024;
-    int lbits = 12;
-    while (lbits > 6 && (size_t)nf * ((1u << lbits) + 2) * 8 > budget) --lbits;
-    p.lbits = lbits;
-    p.lcap = 1 << lbits;
-    pl->lds_bytes = (size_t)nf * (p.lcap + 2) * 8;
-    const int per_cu = pl->lds_bytes <= 80 * 1024 ? 2 : 1;
-    int64_t grid = (int64_t)num_cus() * per_cu;
-    const int64_t need = (p.n + kMaxRowsPerWg - 1) / kMaxRowsPerWg;
-    if (grid < need) grid = need;
-    const int64_t useful = (p.n + kGbThreads - 1) / kGbThreads;
-    if (grid > useful) grid = useful < 1 ? 1 : useful;
-    pl->grid = (int)grid;
     return PLGPU_OK;
-}
-
-template <int PRED, int KEYW>
-static hipError_t launch_main(const Plan& pl, const DevProgram& dp, hipStream_t s) {
-    static bool attr_set = false;
-    if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)gb_kernel<PRED, KEYW>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
-        attr_set = true;
-    }
-    gb_kernel<PRED, KEYW><<<pl.grid, kGbThreads, pl.lds_bytes, s>>>(pl.p, dp);
-    return hipGetLastError();
-}
-
-static hipError_t launch_main_dispatch(const Plan& pl, const DevProgram& dp, int pred, int keyw, hipStream_t s) {
-    if (keyw == 8) {
-        if (pred == 0) return launch_main<0, 8>(pl, dp, s);
-        if (pred == 1) return launch_main<1, 8>(pl, dp, s);
-        return launch_main<2, 8>(pl, dp, s);
-    }
-    if (pred == 0) return launch_main<0, 4>(pl, dp, s);
-    if (pred == 1) return launch_main<1, 4>(pl, dp, s);
-    return launch_main<2, 4>(pl, dp, s);
 }
 
 static int log2_ceil(int64_t x) {
     int b = 0;
     while ((int64_t(1) << b) < x) ++b;
     return b;
+}
+
+// Size the LDS table / grid from the distinct-key sample of the plan kernel.
+static void size_tables(Plan* pl, uint64_t distinct, uint64_t sampled, int* gbits_out) {
+    GbParams& p = pl->p;
+    const int64_t n = p.n;
+    const int nf = p.nfields;
+    // Max LDS slots at one workgroup per CU (160 KiB), power of two.
+    int lmax_bits = 12;
+    while (lmax_bits > 6 && (size_t)nf * ((1u << lmax_bits) + 2) * 8 > 160 * 1024) --lmax_bits;
+    const bool saturated = distinct >= (uint64_t)kPlanSetSlots / 2;
+    int want_bits = log2_ceil(std::max<int64_t>(64, (int64_t)distinct * 2));
+    pl->use_lds = !saturated && want_bits <= lmax_bits;
+    if (!pl->use_lds) want_bits = 6;  // keep a tiny (unused) table
+    p.lbits = want_bits;
+    p.lcap = 1 << want_bits;
+    pl->lds_bytes = pl->use_lds ? (size_t)nf * (p.lcap + 2) * 8 : 0;
+    // Global table: the sample saw most keys if distinct << sampled.
+    int64_t est;
+    if (saturated || sampled == 0) est = n;
+    else if ((int64_t)distinct * 4 < (int64_t)sampled) est = (int64_t)distinct * 2 + 64;
+    else est = std::min<int64_t>(n, (int64_t)((double)distinct * (double)n / (double)sampled) + 64);
+    *gbits_out = log2_ceil(std::max<int64_t>(1024, est * 2));
+    // Grid: fill the chip (LDS permitting), rows per workgroup bounded for
+    // the limb headroom.
+    int per_cu = 4;
+    if (pl->lds_bytes > 0) per_cu = (int)std::max<size_t>(1, std::min<size_t>(4, (160 * 1024) / pl->lds_bytes));
+    int64_t grid = (int64_t)num_cus() * per_cu;
+    const int64_t need = (n + kMaxRowsPerWg - 1) / kMaxRowsPerWg;
+    if (grid < need) grid = need;
+    const int64_t useful = (n + 4 * kGbThreads - 1) / (4 * kGbThreads);
+    if (grid > useful) grid = useful < 1 ? 1 : useful;
+    pl->grid = (int)grid;
+}
+
+template <int PRED, bool LDS>
+static hipError_t launch_main(const Plan& pl, const DevProgram& dp, hipStream_t s) {
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)gb_kernel<PRED, LDS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        attr_set = true;
+    }
+    gb_kernel<PRED, LDS><<<pl.grid, kGbThreads, pl.lds_bytes, s>>>(pl.p, dp);
+    return hipGetLastError();
+}
+
+template <int NACC, int PRED>
+static hipError_t launch_fast(const Plan& pl, const DevProgram& dp, hipStream_t s) {
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)gb_fast_kernel<NACC, PRED>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr_set = true;
+    }
+    gb_fast_kernel<NACC, PRED><<<pl.grid, kGbThreads, pl.lds_bytes, s>>>(pl.p, dp);
+    return hipGetLastError();
+}
+
+template <int NACC>
+static hipError_t launch_fast_nacc(const Plan& pl, const DevProgram& dp, int pred, hipStream_t s) {
+    return pred == 0 ? launch_fast<NACC, 0>(pl, dp, s) : launch_fast<NACC, 1>(pl, dp, s);
+}
+
+static hipError_t launch_fast_dispatch(const Plan& pl, const DevProgram& dp, int pred, hipStream_t s) {
+    switch (pl.p.nacc) {
+    case 0: return launch_fast_nacc<0>(pl, dp, pred, s);
+    case 1: return launch_fast_nacc<1>(pl, dp, pred, s);
+    case 2: return launch_fast_nacc<2>(pl, dp, pred, s);
+    case 3: return launch_fast_nacc<3>(pl, dp, pred, s);
+    case 4: return launch_fast_nacc<4>(pl, dp, pred, s);
+    case 5: return launch_fast_nacc<5>(pl, dp, pred, s);
+    default: return launch_fast_nacc<6>(pl, dp, pred, s);
+    }
+}
+
+static hipError_t launch_main_dispatch(const Plan& pl, const DevProgram& dp, int pred, hipStream_t s) {
+    if (pl.use_lds) {
+        if (pred == 0) return launch_main<0, true>(pl, dp, s);
+        if (pred == 1) return launch_main<1, true>(pl, dp, s);
+        return launch_main<2, true>(pl, dp, s);
+    }
+    if (pred == 0) return launch_main<0, false>(pl, dp, s);
+    if (pred == 1) return launch_main<1, false>(pl, dp, s);
+    return launch_main<2, false>(pl, dp, s);
 }
 
 }  // namespace plgpu
@@ -826,9 +1198,10 @@ PLGPU_API int plgpu_group_by_agg(const plgpu_column* key, const plgpu_column* co
         pred = dp.simple ? 1 : 2;
     }
     Plan pl;
-    if ((rc = plan_groupby(key, cols, ncols, aggs, naggs, maintain_order != 0, &pl))) return rc;
+    if ((rc = plan_groupby(key, cols, ncols, aggs, naggs, maintain_order != 0, dp, &pl))) return rc;
     GbParams& p = pl.p;
     const int64_t n = p.n;
+    const bool debug = getenv("PLGPU_DEBUG") != nullptr;
 
     // device scratch: status + bottoms
     uint64_t* status = nullptr;
@@ -836,13 +1209,37 @@ PLGPU_API int plgpu_group_by_agg(const plgpu_column* key, const plgpu_column* co
     int32_t* bottoms = (int32_t*)(status + ST_WORDS);
     p.status = status;
     p.bottoms = bottoms;
-
-    int64_t cap_hint = n < (int64_t(1) << 20) ? n : (int64_t(1) << 20);
-    int gbits = log2_ceil(cap_hint * 2 < 1024 ? 1024 : cap_hint * 2);
-    uint64_t* gtab = nullptr;
-    int32_t host_bottoms[kMaxAcc] = {0};
-    bool bottoms_from_host = false;
     uint64_t st[ST_WORDS];
+    int32_t host_bottoms[kMaxAcc] = {0};
+
+    // ---- plan launch: sampled exponents + distinct keys
+    PLGPU_HIP(hipMemsetAsync(status, 0, ST_WORDS * 8, s));
+    gb_plan_kernel<<<p.nacc + 1, 256, 0, s>>>(p, bottoms, kPlanSamples);
+    PLGPU_HIP(hipGetLastError());
+    PLGPU_HIP(hipMemcpyAsync(st, status, sizeof st, hipMemcpyDeviceToHost, s));
+    PLGPU_HIP(hipMemcpyAsync(host_bottoms, bottoms, sizeof host_bottoms, hipMemcpyDeviceToHost, s));
+    PLGPU_HIP(hipStreamSynchronize(s));
+    int gbits = 10;
+    size_tables(&pl, st[ST_DISTINCT], st[ST_SAMPLED], &gbits);
+    {
+        // fast path eligibility: no nulls, 8-byte
+        // columns at even offsets of 16-byte aligned buffers, simple or no
+        // predicate, LDS table in use
+        auto ok = [](const DevCol& c) {
+            return (c.dtype == PLGPU_I64 || c.dtype == PLGPU_F64) && c.validity == nullptr && (c.offset & 1) == 0 &&
+                   ((uintptr_t)c.values & 15) == 0;
+        };
+        bool fast = pl.use_lds && pred != 2 && ok(p.key);
+        for (int a = 0; a < p.nacc; ++a) fast = fast && ok(p.acc[a].c);
+        if (pred == 1 && p.pred_acc < 0) fast = fast && ok(p.pred_col);
+        if (getenv("PLGPU_NO_FAST")) fast = false;
+        p.ablate = getenv("PLGPU_ABLATE") ? atoi(getenv("PLGPU_ABLATE")) : 0;
+        const int64_t tile = 4 * (int64_t)kGbThreads;
+        p.n_full = fast ? (n / tile) * tile : 0;
+        p.row_begin = p.n_full;
+    }
+
+    uint64_t* gtab = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     PLGPU_HIP(hipEventCreate(&ev0));
     PLGPU_HIP(hipEventCreate(&ev1));
@@ -850,87 +1247,73 @@ PLGPU_API int plgpu_group_by_agg(const plgpu_column* key, const plgpu_column* co
     for (;; ++attempt) {
         p.gbits = gbits;
         p.gcap = int64_t(1) << gbits;
-        const size_t gwords = (size_t)p.nfields * (p.gcap + 2);
-        if ((rc = dev_alloc((void**)&gtab, gwords * 8, s))) break;
+        const size_t wpf = (size_t)(p.gcap + 2);
+        if ((rc = dev_alloc((void**)&gtab, wpf * p.nfields * 8, s))) break;
         p.gtab = gtab;
-        const int ig = (int)std::min<int64_t>((int64_t)(gwords + 255) / 256, 256 * 16);
-        if (getenv("PLGPU_MEMSET_INIT")) {
-            for (int f = 0; f < p.nfields; ++f) {
-                const int byte = f == 0 ? 0 : (((p.min_init_mask >> f) & 1ull) ? 0xFF : 0);
-                PLGPU_HIP(hipMemsetAsync(gtab + (size_t)f * (p.gcap + 2), byte, (size_t)(p.gcap + 2) * 8, s));
-            }
-            gb_init_table_kernel<<<ig, 256, 0, s>>>(gtab, p.gcap + 2, 1, 0);
-        } else {
-            gb_init_table_kernel<<<ig, 256, 0, s>>>(gtab, p.gcap + 2, p.nfields, p.min_init_mask);
-        }
-        if (getenv("PLGPU_DEBUG")) {
-            std::vector<uint64_t> chk(gwords);
-            PLGPU_HIP(hipMemcpyAsync(chk.data(), gtab, gwords * 8, hipMemcpyDeviceToHost, s));
-            PLGPU_HIP(hipStreamSynchronize(s));
-            size_t bad = 0;
-            for (size_t i = 0; i < gwords; ++i) {
-                const int f = (int)(i / (size_t)(p.gcap + 2));
-                const uint64_t want = f == 0 ? kEmptyKey : (((p.min_init_mask >> f) & 1ull) ? ~0ull : 0ull);
-                bad += chk[i] != want;
-            }
-            size_t firstbad = gwords;
-            for (size_t i = 0; i < gwords && firstbad == gwords; ++i) {
-                const int f = (int)(i / (size_t)(p.gcap + 2));
-                const uint64_t want = f == 0 ? kEmptyKey : (((p.min_init_mask >> f) & 1ull) ? ~0ull : 0ull);
-                if (chk[i] != want) firstbad = i;
-            }
-            fprintf(stderr, "[plgpu] init check: %zu bad words of %zu (gtab=%p) first bad %zu field %zu val %llx mask %llx\n",
-                    bad, gwords, (void*)gtab, firstbad, firstbad / (size_t)(p.gcap + 2),
-                    firstbad < gwords ? (unsigned long long)chk[firstbad] : 0ull, (unsigned long long)p.min_init_mask);
-        }
-        PLGPU_HIP(hipMemsetAsync(status, 0, ST_WORDS * 8, s));
-        if (bottoms_from_host) {
-            PLGPU_HIP(hipMemcpyAsync(bottoms, host_bottoms, sizeof host_bottoms, hipMemcpyHostToDevice, s));
-        } else if (p.nacc > 0) {
-            gb_sample_kernel<<<p.nacc, 256, 0, s>>>(p, bottoms, 65536);
-        }
+        const int ig = (int)std::min<int64_t>((int64_t)(wpf + 255) / 256, 256 * 8);
+        gb_init_table_kernel<<<ig, 256, 0, s>>>(gtab, (int64_t)wpf, p.nfields, p.min_init_mask);
+        // keep the plan words, clear the run words
+        PLGPU_HIP(hipMemsetAsync(status, 0, 6 * 8, s));
+        PLGPU_HIP(hipMemsetAsync(status + ST_MAXEX, 0, (ST_WORDS - ST_MAXEX) * 8, s));
+        PLGPU_HIP(hipMemcpyAsync(bottoms, host_bottoms, sizeof host_bottoms, hipMemcpyHostToDevice, s));
+        for (int a = 0; a < kMaxAcc; ++a) p.bottom[a] = host_bottoms[a];
         PLGPU_HIP(hipGetLastError());
         PLGPU_HIP(hipEventRecord(ev0, s));
-        if (n > 0) PLGPU_HIP(launch_main_dispatch(pl, dp, pred, key->dtype == PLGPU_I64 ? 8 : 4, s));
+        if (n > 0) {
+            if (p.n_full > 0) PLGPU_HIP(launch_fast_dispatch(pl, dp, pred, s));
+            if (p.row_begin < n) {
+                Plan tail = pl;
+                const int64_t rows = n - p.row_begin;
+                const int64_t g = (rows + 4 * kGbThreads - 1) / (4 * kGbThreads);
+                tail.grid = (int)std::min<int64_t>(pl.grid, g < 1 ? 1 : g);
+                PLGPU_HIP(launch_main_dispatch(tail, dp, pred, s));
+            }
+        }
         PLGPU_HIP(hipEventRecord(ev1, s));
         PLGPU_HIP(hipMemcpyAsync(st, status, sizeof st, hipMemcpyDeviceToHost, s));
         PLGPU_HIP(hipMemcpyAsync(host_bottoms, bottoms, sizeof host_bottoms, hipMemcpyDeviceToHost, s));
         PLGPU_HIP(hipStreamSynchronize(s));
-        if (getenv("PLGPU_DEBUG")) {
+        if (debug) {
             fprintf(stderr,
-                    "[plgpu] gb attempt %d: n=%lld grid=%d lcap=%d gcap=%lld nfields=%d lds=%zu newkeys=%llu "
-                    "special=%llu global_rows=%llu full=%llu selected=%llu\n",
-                    attempt, (long long)n, pl.grid, p.lcap, (long long)p.gcap, p.nfields, pl.lds_bytes,
+                    "[plgpu] gb attempt %d: n=%lld grid=%d lds=%d lcap=%d gcap=%lld nfields=%d lds_bytes=%zu "
+                    "distinct=%llu/%llu newkeys=%llu special=%llu global_rows=%llu full=%llu selected=%llu\n",
+                    attempt, (long long)n, pl.grid, (int)pl.use_lds, p.lcap, (long long)p.gcap, p.nfields,
+                    pl.lds_bytes, (unsigned long long)st[ST_DISTINCT], (unsigned long long)st[ST_SAMPLED],
                     (unsigned long long)st[ST_NEWKEYS], (unsigned long long)st[ST_SPECIAL],
                     (unsigned long long)st[ST_GLOBAL_ROWS], (unsigned long long)st[ST_TABLE_FULL],
                     (unsigned long long)st[ST_SELECTED]);
-            for (int a = 0; a < p.nacc; ++a)
-                fprintf(stderr, "[plgpu]   acc %d flags=%d bottom=%d maxex=%llu fx=%llu\n", a, p.acc[a].flags,
-                        host_bottoms[a], (unsigned long long)st[ST_MAXEX + a], (unsigned long long)st[ST_FXFLAGS + a]);
         }
         bool again = false;
         if (st[ST_TABLE_FULL] > 0) {
-            gbits = log2_ceil(std::max<int64_t>((int64_t)st[ST_NEWKEYS] * 4, p.gcap * 8));
+            gbits = std::max(gbits + 3, log2_ceil((int64_t)st[ST_NEWKEYS] * 4));
             again = true;
         }
-        for (int a = 0; a < p.nacc; ++a) {
-            if (!(p.acc[a].flags & (A_FSUM | A_FSUMCAST))) continue;
-            const int tmax = (int)st[ST_MAXEX + a];
-            const int allowed = host_bottoms[a] + 1075 + (kSumWindowBits - 53);
-            const uint64_t fl = st[ST_FXFLAGS + a];
-            if ((fl & 1u) || ((fl & 2u) && tmax > 0 && tmax < allowed)) {
-                // refit the window to the true max exponent
-                const int e = (fl & 1u) ? std::max(tmax, allowed + 1) : tmax;
-                host_bottoms[a] = e - 1075 - (kSumWindowBits - 53);
-                again = true;
+        uint32_t fxflag_accs = 0;
+        for (int a = 0; a < p.nacc; ++a)
+            if ((p.acc[a].flags & (A_FSUM | A_FSUMCAST)) && ((st[ST_FXFLAGS] >> (2 * a)) & 3u)) fxflag_accs |= 1u << a;
+        if (fxflag_accs) {
+            // exact max exponent of each flagged column, then refit its window
+            for (int a = 0; a < p.nacc; ++a)
+                if ((fxflag_accs >> a) & 1u) gb_maxexp_kernel<<<std::max(1, num_cus() * 4), 256, 0, s>>>(p, a);
+            PLGPU_HIP(hipGetLastError());
+            PLGPU_HIP(hipMemcpyAsync(st, status, sizeof st, hipMemcpyDeviceToHost, s));
+            PLGPU_HIP(hipStreamSynchronize(s));
+            for (int a = 0; a < p.nacc; ++a) {
+                if (!((fxflag_accs >> a) & 1u)) continue;
+                const uint64_t fl = (st[ST_FXFLAGS] >> (2 * a)) & 3u;
+                const int tmax = (int)st[ST_MAXEX + a];
+                const int allowed = host_bottoms[a] + 1075 + (kSumWindowBits - 53);
+                if ((fl & 1u) || ((fl & 2u) && tmax > 0 && tmax < allowed)) {
+                    // overflowed values were dropped, so the whole pass reruns
+                    host_bottoms[a] = std::max(tmax, 1) - 1075 - (kSumWindowBits - 53);
+                    again = true;
+                }
             }
         }
         if (!again || attempt >= 3) {
             if (again) rc = fail(PLGPU_ERR_CAPACITY, "group-by did not converge after retries");
             break;
         }
-        // overflowed values were dropped: the whole pass must rerun
-        bottoms_from_host = true;
         dev_free(gtab, s);
         gtab = nullptr;
     }
@@ -943,30 +1326,24 @@ PLGPU_API int plgpu_group_by_agg(const plgpu_column* key, const plgpu_column* co
         dev_free(status, s);
         return rc;
     }
-    // overflow that persisted means the window could not hold a value: the
-    // max exponent pass above already refit it, so only inexact remains.
-    int64_t groups = (int64_t)st[ST_NEWKEYS] + ((st[ST_SPECIAL] & 1) ? 1 : 0) + ((st[ST_SPECIAL] & 2) ? 1 : 0);
+    const int64_t groups =
+        (int64_t)st[ST_NEWKEYS] + ((st[ST_SPECIAL] & 1) ? 1 : 0) + ((st[ST_SPECIAL] & 2) ? 1 : 0);
     info->rows_in = n;
     info->rows_selected = (int64_t)st[ST_SELECTED];
     info->groups = groups;
     info->global_path_rows = (int64_t)st[ST_GLOBAL_ROWS];
     info->reruns = attempt;
-    info->lds_slots = p.lcap;
+    info->lds_slots = pl.use_lds ? p.lcap : 0;
     info->grid = pl.grid;
     info->table_capacity = p.gcap;
     info->main_kernel_ms = ms;
     for (int a = 0; a < p.nacc; ++a)
-        if (st[ST_FXFLAGS + a] & 2u) info->sum_inexact |= 1 << a;
+        if ((st[ST_FXFLAGS] >> (2 * a)) & 2u) info->sum_inexact |= 1 << a;
 
     // ---- outputs
     FinParams fp;
     std::memset(&fp, 0, sizeof fp);
-    rc = make_owned_column(out_key, key->dtype == PLGPU_I32 ? PLGPU_I32 : PLGPU_I64, groups, true, s);
-    if (rc == PLGPU_OK && key->dtype == PLGPU_I32) {
-        // keys are materialised as i64 first, then narrowed below
-        plgpu_column_release(out_key);
-        rc = make_owned_column(out_key, PLGPU_I64, groups, true, s);
-    }
+    rc = make_owned_column(out_key, PLGPU_I64, groups, true, s);
     for (int i = 0; i < naggs && rc == PLGPU_OK; ++i) {
         const OutSpec& o = pl.outs[i];
         const bool nullable = o.kind == PLGPU_AGG_MEAN || o.kind == PLGPU_AGG_MIN || o.kind == PLGPU_AGG_MAX;
@@ -1052,20 +1429,20 @@ PLGPU_API int plgpu_group_by_agg(const plgpu_column* key, const plgpu_column* co
             }
         }
     }
-    if (rc == PLGPU_OK && key->dtype == PLGPU_I32 && groups > 0) {
+    if (rc == PLGPU_OK && key->dtype == PLGPU_I32) {
         // narrow the key back to Int32 (the reference keeps the key dtype)
         plgpu_column nk;
         rc = make_owned_column(&nk, PLGPU_I32, groups, true, s);
-        if (rc == PLGPU_OK) {
+        if (rc == PLGPU_OK && groups > 0) {
             const int gg = (int)std::min<int64_t>((groups + 255) / 256, 4096);
             narrow_i64_kernel<<<gg, 256, 0, s>>>((const int64_t*)out_key->values, (int32_t*)nk.values, groups);
             (void)hipMemcpyAsync((void*)nk.validity, out_key->validity, ((groups + 63) / 64) * 8,
                                  hipMemcpyDeviceToDevice, s);
+        }
+        if (rc == PLGPU_OK) {
             plgpu_column_release(out_key);
             *out_key = nk;
         }
-    } else if (rc == PLGPU_OK && key->dtype == PLGPU_I32) {
-        out_key->dtype = PLGPU_I32;
     }
     if (rc == PLGPU_OK) {
         out_key->null_count = (st[ST_SPECIAL] & 1) ? 1 : 0;
