@@ -196,7 +196,7 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
-            "kernel": "gb_kernel<1,8> (fused filter + LDS hash aggregation)",
+            "kernel": "gb_fast_kernel<4,1,true,2> (fused filter + LDS hash aggregation, exact f64 sums)",
             "kernel_ms": round(kms, 4),
             "bytes_per_row": BYTES_PER_ROW,
         },

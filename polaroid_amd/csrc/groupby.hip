@@ -573,38 +573,50 @@ __global__ __launch_bounds__(kGbThreads) void gb_kernel(GbParams p, DevProgram p
 // tail and every other case go through gb_kernel.  Loads of the next tile
 // are issued before the current tile's LDS atomics, so HBM reads overlap
 // the aggregation.
-template <int NACC>
+template <int NACC, int ROWS>
 struct FastTile {
-    uint64_t key[4];
-    uint64_t v[NACC > 0 ? NACC : 1][4];
-    uint64_t pv[4];
+    uint64_t key[ROWS];
+    uint64_t v[NACC > 0 ? NACC : 1][ROWS];
+    uint64_t pv[ROWS];
 };
 
-template <int NACC, int PRED>
-__device__ __forceinline__ void fast_load(const GbParams& p, int64_t t, FastTile<NACC>& x) {
+// Row j of tile t for this thread: pairs of consecutive rows, pair q at
+// t*T*ROWS + q*2*T + 2*tid.
+__device__ __forceinline__ int64_t fast_row(int64_t t, int T, int rows, int j) {
+    return t * (int64_t)T * rows + (int64_t)(j >> 1) * 2 * T + 2 * threadIdx.x + (j & 1);
+}
+
+template <int NACC, int PRED, int ROWS>
+__device__ __forceinline__ void fast_load(const GbParams& p, int64_t t, FastTile<NACC, ROWS>& x) {
     const int T = blockDim.x;
-    const int64_t r0 = t * (int64_t)T * 4 + 2 * threadIdx.x;
-    const int64_t r2 = r0 + 2 * T;
     const uint64_t* kp = (const uint64_t*)p.key.values + p.key.offset;
-    ulonglong2 a = *reinterpret_cast<const ulonglong2*>(kp + r0);
-    ulonglong2 b = *reinterpret_cast<const ulonglong2*>(kp + r2);
-    x.key[0] = a.x; x.key[1] = a.y; x.key[2] = b.x; x.key[3] = b.y;
 #pragma unroll
-    for (int c = 0; c < NACC; ++c) {
-        const uint64_t* vp = (const uint64_t*)p.acc[c].c.values + p.acc[c].c.offset;
-        a = *reinterpret_cast<const ulonglong2*>(vp + r0);
-        b = *reinterpret_cast<const ulonglong2*>(vp + r2);
-        x.v[c][0] = a.x; x.v[c][1] = a.y; x.v[c][2] = b.x; x.v[c][3] = b.y;
-    }
-    if (PRED == 1 && p.pred_acc < 0) {
-        const uint64_t* pp = (const uint64_t*)p.pred_col.values + p.pred_col.offset;
-        a = *reinterpret_cast<const ulonglong2*>(pp + r0);
-        b = *reinterpret_cast<const ulonglong2*>(pp + r2);
-        x.pv[0] = a.x; x.pv[1] = a.y; x.pv[2] = b.x; x.pv[3] = b.y;
+    for (int q = 0; q < ROWS / 2; ++q) {
+        const int64_t r = fast_row(t, T, ROWS, 2 * q);
+        const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(kp + r);
+        x.key[2 * q] = a.x;
+        x.key[2 * q + 1] = a.y;
+#pragma unroll
+        for (int c = 0; c < NACC; ++c) {
+            const uint64_t* vp = (const uint64_t*)p.acc[c].c.values + p.acc[c].c.offset;
+            const ulonglong2 b = *reinterpret_cast<const ulonglong2*>(vp + r);
+            x.v[c][2 * q] = b.x;
+            x.v[c][2 * q + 1] = b.y;
+        }
+        if (PRED == 1 && p.pred_acc < 0) {
+            const uint64_t* pp = (const uint64_t*)p.pred_col.values + p.pred_col.offset;
+            const ulonglong2 b = *reinterpret_cast<const ulonglong2*>(pp + r);
+            x.pv[2 * q] = b.x;
+            x.pv[2 * q + 1] = b.y;
+        }
     }
 }
 
-template <int NACC, int PRED>
+// SUMONLY: every acc is an f64 sum / mean (flags A_FSUM|A_FLAGS, no count /
+// min / max), no maintain_order: the field layout is compile-time
+// (key 0, len 1, acc a: limbs 2+4a..4+4a, flags 5+4a) and the per-acc code
+// is unrolled with no descriptor decode.
+template <int NACC, int PRED, bool SUMONLY, int ROWS>
 __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProgram prog) {
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
     constexpr int NA = NACC > 0 ? NACC : 1;
@@ -617,20 +629,18 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
     __syncthreads();
 
     const int T = blockDim.x;
-    const int64_t ntiles = p.n_full / ((int64_t)T * 4);
+    const int64_t ntiles = p.n_full / ((int64_t)T * ROWS);
     constexpr uint32_t VM = (1u << NACC) - 1u;
     int64_t t = blockIdx.x;
-    FastTile<NACC> cur;
-    if (t < ntiles) fast_load<NACC, PRED>(p, t, cur);
+    FastTile<NACC, ROWS> cur;
+    if (t < ntiles) fast_load<NACC, PRED, ROWS>(p, t, cur);
     for (; t < ntiles; t += gridDim.x) {
-        const int64_t r0 = t * (int64_t)T * 4 + 2 * threadIdx.x;
-        const int64_t r2 = r0 + 2 * T;
-        // ---- predicate + batched LDS probes of the four rows
-        int slot[4];
-        uint64_t probe[4];
-        uint32_t h[4];
+        // ---- predicate + batched LDS probes of the tile's rows
+        int slot[ROWS];
+        uint64_t probe[ROWS];
+        uint32_t h[ROWS];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < ROWS; ++j) {
             bool sel = true;
             if (PRED == 1) {
                 uint64_t x = cur.pv[j];
@@ -644,16 +654,16 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
             probe[j] = lds_load(&lds[h[j]]);
         }
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < ROWS; ++j)
             if (slot[j] == kGlobalKey && probe[j] == cur.key[j]) slot[j] = (int)h[j];
         // ---- next tile's loads go out before this tile's atomics
-        FastTile<NACC> nxt;
+        FastTile<NACC, ROWS> nxt;
         const int64_t tn = t + gridDim.x;
-        if (tn < ntiles) fast_load<NACC, PRED>(p, tn, nxt);
+        if (tn < ntiles) fast_load<NACC, PRED, ROWS>(p, tn, nxt);
         // ---- apply rows one at a time (rolled; arrays shift statically)
 #pragma unroll 1
-        for (int j = 0; j < 4; ++j) {
-            const int64_t r = (j < 2 ? r0 : r2) + (j & 1);
+        for (int j = 0; j < ROWS; ++j) {
+            const int64_t r = fast_row(t, T, ROWS, j);
             int s = slot[0];
             if (s != kNotSelected) {
                 ++d.nsel;
@@ -666,20 +676,42 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
                     bot[a] = bot0[a];
                 }
                 if (s == kGlobalKey) s = lds_find(lds, p.lbits, p.lcap, cur.key[0]);
-                if (s >= 0) {
+                if (SUMONLY && s >= 0) {
+                    unsigned long long* q = (unsigned long long*)&lds[s];
+                    atomicAdd(q + L, 1ull);
+#pragma unroll
+                    for (int a = 0; a < NACC; ++a) {
+                        const uint64_t x = rv[a];
+                        const uint64_t ab = x & 0x7fffffffffffffffull;
+                        if (ab >= 0x7ff0000000000000ull) {
+                            atomicOr(q + (5 + 4 * a) * L,
+                                     (unsigned long long)(ab > 0x7ff0000000000000ull ? FL_NAN
+                                                          : ((x >> 63) ? FL_NINF : FL_PINF)));
+                        } else {
+                            uint64_t l0, l1, l2;
+                            uint32_t ex = 0, fl = 0;
+                            const bool ok = fx_limbs(x, bot[a], l0, l1, l2, fl, ex);
+                            d.fxbits |= fl << (2 * a);
+                            if (ok) {
+                                atomicAdd(q + (2 + 4 * a) * L, (unsigned long long)l0);
+                                atomicAdd(q + (3 + 4 * a) * L, (unsigned long long)l1);
+                                atomicAdd(q + (4 + 4 * a) * L, (unsigned long long)l2);
+                            }
+                        }
+                    }
+                } else if (s >= 0) {
                     apply_row<true, NA>(p, lds, L, s, r, rv, VM, dd, bot, NACC, d);
                 } else {
                     ++d.nglobal;
                     global_row<NA>(p, cur.key[0], true, r, rv, VM, dd, bot, NACC, d);
                 }
             }
-            slot[0] = slot[1]; slot[1] = slot[2]; slot[2] = slot[3];
-            cur.key[0] = cur.key[1]; cur.key[1] = cur.key[2]; cur.key[2] = cur.key[3];
 #pragma unroll
-            for (int a = 0; a < NACC; ++a) {
-                cur.v[a][0] = cur.v[a][1];
-                cur.v[a][1] = cur.v[a][2];
-                cur.v[a][2] = cur.v[a][3];
+            for (int i = 0; i + 1 < ROWS; ++i) {
+                slot[i] = slot[i + 1];
+                cur.key[i] = cur.key[i + 1];
+#pragma unroll
+                for (int a = 0; a < NACC; ++a) cur.v[a][i] = cur.v[a][i + 1];
             }
         }
         cur = nxt;
@@ -976,6 +1008,10 @@ struct Plan {
     size_t lds_bytes;
     int grid;
     bool use_lds;
+    bool sum_only;
+    int fast_rows;     // rows per thread per tile in the fast kernel (2 / 4)
+    int fast_threads;  // workgroup size of the fast kernel
+    int fast_grid;
 };
 
 static int plan_groupby(const plgpu_column* key, const plgpu_column* cols, int32_t ncols, const plgpu_agg* aggs,
@@ -1126,21 +1162,29 @@ static hipError_t launch_main(const Plan& pl, const DevProgram& dp, hipStream_t 
     return hipGetLastError();
 }
 
-template <int NACC, int PRED>
-static hipError_t launch_fast(const Plan& pl, const DevProgram& dp, hipStream_t s) {
+template <int NACC, int PRED, bool SUMONLY, int ROWS>
+static hipError_t launch_fast_rows(const Plan& pl, const DevProgram& dp, hipStream_t s) {
     static bool attr_set = false;
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)gb_fast_kernel<NACC, PRED>,
+        (void)hipFuncSetAttribute((const void*)gb_fast_kernel<NACC, PRED, SUMONLY, ROWS>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_set = true;
     }
-    gb_fast_kernel<NACC, PRED><<<pl.grid, kGbThreads, pl.lds_bytes, s>>>(pl.p, dp);
+    gb_fast_kernel<NACC, PRED, SUMONLY, ROWS><<<pl.fast_grid, pl.fast_threads, pl.lds_bytes, s>>>(pl.p, dp);
     return hipGetLastError();
+}
+
+template <int NACC, int PRED, bool SUMONLY>
+static hipError_t launch_fast(const Plan& pl, const DevProgram& dp, hipStream_t s) {
+    return pl.fast_rows == 2 ? launch_fast_rows<NACC, PRED, SUMONLY, 2>(pl, dp, s)
+                             : launch_fast_rows<NACC, PRED, SUMONLY, 4>(pl, dp, s);
 }
 
 template <int NACC>
 static hipError_t launch_fast_nacc(const Plan& pl, const DevProgram& dp, int pred, hipStream_t s) {
-    return pred == 0 ? launch_fast<NACC, 0>(pl, dp, s) : launch_fast<NACC, 1>(pl, dp, s);
+    if (pl.sum_only)
+        return pred == 0 ? launch_fast<NACC, 0, true>(pl, dp, s) : launch_fast<NACC, 1, true>(pl, dp, s);
+    return pred == 0 ? launch_fast<NACC, 0, false>(pl, dp, s) : launch_fast<NACC, 1, false>(pl, dp, s);
 }
 
 static hipError_t launch_fast_dispatch(const Plan& pl, const DevProgram& dp, int pred, hipStream_t s) {
@@ -1234,8 +1278,30 @@ PLGPU_API int plgpu_group_by_agg(const plgpu_column* key, const plgpu_column* co
         if (pred == 1 && p.pred_acc < 0) fast = fast && ok(p.pred_col);
         if (getenv("PLGPU_NO_FAST")) fast = false;
         p.ablate = getenv("PLGPU_ABLATE") ? atoi(getenv("PLGPU_ABLATE")) : 0;
-        const int64_t tile = 4 * (int64_t)kGbThreads;
+        pl.fast_rows = getenv("PLGPU_FAST_ROWS") ? atoi(getenv("PLGPU_FAST_ROWS")) : 2;
+        if (pl.fast_rows != 2 && pl.fast_rows != 4) pl.fast_rows = 2;
+        pl.fast_threads = getenv("PLGPU_FAST_THREADS") ? atoi(getenv("PLGPU_FAST_THREADS")) : 512;
+        if (pl.fast_threads != 256 && pl.fast_threads != 512) pl.fast_threads = 256;
+        const int64_t tile = (int64_t)pl.fast_rows * pl.fast_threads;
         p.n_full = fast ? (n / tile) * tile : 0;
+        {
+            // as many workgroups as the LDS budget allows per CU (up to 8)
+            int per_cu = (int)std::max<size_t>(1, std::min<size_t>(8, pl.lds_bytes ? (160 * 1024) / pl.lds_bytes : 8));
+            int64_t g = (int64_t)num_cus() * per_cu;
+            const int64_t need = (p.n_full + kMaxRowsPerWg - 1) / kMaxRowsPerWg;
+            if (g < need) g = need;
+            const int64_t useful = p.n_full / tile;
+            if (g > useful) g = useful < 1 ? 1 : useful;
+            pl.fast_grid = (int)g;
+        }
+        // sum-only signature with the compile-time field layout
+        bool so = p.f_first < 0 && p.f_len == 1 && p.nacc > 0;
+        for (int a = 0; a < p.nacc; ++a) {
+            const AccSpec& ac = p.acc[a];
+            so = so && ac.isf && ac.flags == (A_FSUM | A_FLAGS) && ac.f_sum == 2 + 4 * a && ac.f_flags == 5 + 4 * a &&
+                 ac.f_cnt < 0;
+        }
+        pl.sum_only = so && !getenv("PLGPU_NO_SUMONLY");
         p.row_begin = p.n_full;
     }
 

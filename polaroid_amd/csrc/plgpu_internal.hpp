@@ -266,9 +266,25 @@ __device__ __forceinline__ RowVal eval_row(const DevInstr* __restrict__ code, in
     return RowVal{s0, (vm & 1u) != 0};
 }
 
-// Fast-path predicate `col <cmp> imm`, null -> false.
+// Fast-path predicate `col <cmp> imm` (null handled by the caller),
+// branch-free: classify the pair as lt / eq / gt under the total order
+// (trichotomy holds with NaN greatest, NaN == NaN) and test the class
+// against the op's accept mask.  op 0..5 = eq, ne, lt, le, gt, ge with
+// masks (lt=1, eq=2, gt=4) 2, 5, 1, 3, 4, 6 packed one nibble per op.
 __device__ __forceinline__ bool simple_pred(bool isf, int op, uint64_t x, uint64_t imm) {
-    return isf ? cmp_f(op, as_f64(x), as_f64(imm)) : cmp_i(op, (int64_t)x, (int64_t)imm);
+    const uint32_t accept = (0x643152u >> (4 * op)) & 0xFu;
+    uint32_t cls;
+    if (isf) {
+        const double a = as_f64(x), b = as_f64(imm);
+        const bool an = __builtin_isnan(a), bn = __builtin_isnan(b);
+        const bool eq = (an & bn) | (a == b);
+        const bool lt = !an & (bn | (a < b));
+        cls = eq ? 2u : (lt ? 1u : 4u);
+    } else {
+        const int64_t a = (int64_t)x, b = (int64_t)imm;
+        cls = a == b ? 2u : (a < b ? 1u : 4u);
+    }
+    return (cls & accept) != 0u;
 }
 
 // Fibonacci hashing of a 64-bit key into `bits` bits.

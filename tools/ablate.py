@@ -21,11 +21,14 @@ res = {m: [] for m in modes}
 for rnd in range(6):
     for m in modes:
         os.environ["PLGPU_ABLATE"] = m
+        for k in ("PLGPU_NO_FAST", "PLGPU_NO_SUMONLY"):
+            os.environ.pop(k, None)
         if m.startswith("nofast"):
             os.environ["PLGPU_NO_FAST"] = "1"
             os.environ["PLGPU_ABLATE"] = "0"
-        else:
-            os.environ.pop("PLGPU_NO_FAST", None)
+        if m.startswith("nosumonly"):
+            os.environ["PLGPU_NO_SUMONLY"] = "1"
+            os.environ["PLGPU_ABLATE"] = "0"
         info = {}
         q.collect(info=info)
         if rnd > 0:
