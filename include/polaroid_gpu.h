@@ -149,7 +149,9 @@ typedef struct plgpu_groupby_info {
     int32_t grid;                /* workgroups in the main launch              */
     int32_t sum_inexact;         /* bit i: f64 sum acc i rounded below window  */
     int64_t table_capacity;      /* global hash-table slots                    */
-    double main_kernel_ms;       /* device time of the aggregation kernel      */
+    double main_kernel_ms;       /* device time of the aggregation kernel(s)   */
+    int32_t path;                /* 0 generic, 1 fast, 2 fast sum-only kernel  */
+    int32_t _reserved;
 } plgpu_groupby_info;
 
 /* ---------------------------------------------------------------- basics */

@@ -74,6 +74,8 @@ class GroupByInfo(C.Structure):
         ("sum_inexact", C.c_int32),
         ("table_capacity", C.c_int64),
         ("main_kernel_ms", C.c_double),
+        ("path", C.c_int32),
+        ("_reserved", C.c_int32),
     ]
 
     def as_dict(self) -> dict:

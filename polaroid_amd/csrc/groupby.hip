@@ -1403,6 +1403,7 @@ PLGPU_API int plgpu_group_by_agg(const plgpu_column* key, const plgpu_column* co
     info->grid = pl.grid;
     info->table_capacity = p.gcap;
     info->main_kernel_ms = ms;
+    info->path = p.n_full > 0 ? (pl.sum_only ? 2 : 1) : 0;
     for (int a = 0; a < p.nacc; ++a)
         if ((st[ST_FXFLAGS] >> (2 * a)) & 2u) info->sum_inexact |= 1 << a;
 

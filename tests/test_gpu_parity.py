@@ -285,6 +285,44 @@ def test_group_by_with_predicate_vs_oracle(gpu, pname):
                     kahan_cols=("a",) if pname == "simple_f64" else ())
 
 
+def _nonull_frame(rng, n, specials=False):
+    a = rng.standard_normal(n) * 100
+    if specials:
+        a[rng.random(n) < 0.001] = np.nan
+        a[rng.random(n) < 0.001] = np.inf
+        a[rng.random(n) < 0.001] = -np.inf
+        a[rng.random(n) < 0.01] = -0.0
+    b = rng.integers(-10**12, 10**12, n).astype(np.int64)
+    d = rng.uniform(1.0, 1000.0, n)
+    return {"a": (a, None), "b": (b, None), "d": (d, None)}
+
+
+FAST_AGGS = {
+    "sumonly": [("sum", "a"), ("sum", "d"), ("mean", "a")],
+    "mixed": [("sum", "a"), ("max", "d"), ("sum", "b"), ("count", "a"), ("len", "a"), ("min", "b")],
+}
+
+
+@pytest.mark.parametrize("n", [1, 1023, 1024, 1025, 4097, 300001])
+@pytest.mark.parametrize("aggset", list(FAST_AGGS))
+@pytest.mark.parametrize("pname", [None, "simple_f64", "simple_i64"])
+def test_group_by_fast_path_vs_oracle(gpu, n, aggset, pname):
+    """Null-free 8-byte columns take gb_fast_kernel (sum-only variant for
+    `sumonly`); the tail rows beyond the last full tile take gb_kernel."""
+    rng = np.random.default_rng(n + len(aggset))
+    cols = _nonull_frame(rng, n, specials=(n % 2 == 1))
+    key = rng.integers(0, 37, n).astype(np.int64) * 1_000_003 - 5
+    key[rng.random(n) < 0.01] = np.iinfo(np.int64).min
+    info = {}
+    if pname is None:
+        _check_group_by(cols, key, None, FAST_AGGS[aggset], None, None, [], False, info)
+    else:
+        mk, names, prog = PREDICATES[pname]
+        _check_group_by(cols, key, None, FAST_AGGS[aggset], mk(), prog, names, False, info)
+    if n >= 1024:
+        assert info["path"] == (2 if aggset == "sumonly" else 1), info
+
+
 def test_group_by_special_keys_and_i32_key(gpu):
     rng = np.random.default_rng(5)
     n = 20000
