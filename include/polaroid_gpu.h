@@ -208,6 +208,64 @@ int plgpu_group_by_agg(const plgpu_column* key, const plgpu_column* cols, int32_
                        int32_t naggs, int32_t maintain_order, plgpu_column* out_key,
                        plgpu_column* out_aggs, plgpu_groupby_info* info, void* stream);
 
+
+/* ---- hash-partitioned group-by (one process per GPU) ----------------------
+ * Mirrors the partitioned sink of the streaming group-by
+ * (polars-stream/src/nodes/group_by.rs:216 `combine_locals`): each local
+ * builder pre-aggregates, splits its pre-aggregates by a hash partitioner
+ * (group_by.rs:85 `add_pre_agg`, :509 HashPartitioner) and each partition
+ * folds the pre-aggregates routed to it (group_by.rs:378 `combine_subset`).
+ * Here a "local" is one GPU's shard, partitions are ranks, and the
+ * pre-aggregates are exact partial states (records) moved by one RCCL
+ * all-to-all.  A record is `record_words` u64 words:
+ * [kind (0 key, 1 null key, 2 INT64_MIN key), key, state fields...].
+ * All ranks must aggregate with the SAME f64 fixed-point windows
+ * (`bottoms`, PLGPU_GB_MAX_ACC int32): each rank starts from its sampled
+ * windows, ranks agree on the element-wise MAX of the hints, and a rank
+ * re-runs its partial stage while its used windows differ from the agreed
+ * ones (polaroid_amd/distributed.py). */
+typedef struct plgpu_gb_partial plgpu_gb_partial;
+
+#define PLGPU_GB_MAX_ACC 6
+
+/* Words per exported record for this aggregation schema (lengths ignored). */
+int plgpu_gb_record_words(const plgpu_column* cols, int32_t ncols, const plgpu_agg* aggs,
+                          int32_t naggs, int32_t* out_words);
+
+/* Sampled fixed-point windows of this shard (out_bottoms[PLGPU_GB_MAX_ACC]). */
+int plgpu_gb_plan_bottoms(const plgpu_column* key, const plgpu_column* cols, int32_t ncols,
+                          const plgpu_agg* aggs, int32_t naggs, int32_t* out_bottoms,
+                          void* stream);
+
+/* Filter + pre-aggregate this shard.  `bottoms` (6 int32) are the agreed
+ * windows, or NULL to use this shard's sampled ones; the windows actually
+ * used come back in out_bottoms_used[6].  Returns a handle holding the
+ * partial table, the number of groups (*out_records), and whether a window
+ * must move for an exact sum (*out_refit, new windows in out_bottoms_hint[6];
+ * without a refit the hint equals the used windows). */
+int plgpu_gb_partial_begin(const plgpu_column* key, const plgpu_column* cols, int32_t ncols,
+                           const plgpu_instr* program, int32_t n_instr, const plgpu_agg* aggs,
+                           int32_t naggs, const int32_t* bottoms, int32_t world,
+                           plgpu_gb_partial** out, int64_t* out_records, int32_t* out_bottoms_used,
+                           int32_t* out_refit, int32_t* out_bottoms_hint,
+                           plgpu_groupby_info* info, void* stream);
+
+/* Write the partial groups as records into device buffer `dst_records`
+ * (out_records * record_words u64), grouped by destination rank in rank
+ * order; out_counts[world] receives the records per destination. */
+int plgpu_gb_partial_export(plgpu_gb_partial* h, void* dst_records, int64_t* out_counts,
+                            void* stream);
+
+void plgpu_gb_partial_free(plgpu_gb_partial* h);
+
+/* Fold `n_records` received records (device memory) into this rank's
+ * partition and finalize it like plgpu_group_by_agg (`cols` supplies the
+ * dtypes only; `key_dtype` is the original key dtype). */
+int plgpu_gb_merge(const void* records, int64_t n_records, const plgpu_column* cols,
+                   int32_t ncols, const plgpu_agg* aggs, int32_t naggs, const int32_t* bottoms,
+                   int32_t key_dtype, plgpu_column* out_key, plgpu_column* out_aggs,
+                   plgpu_groupby_info* info, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -104,7 +104,23 @@ SIGNATURES = {
     "plgpu_group_by_agg": (C.c_int, [_COLP, _COLP, C.c_int32, C.POINTER(Instr), C.c_int32,
                                      C.POINTER(Agg), C.c_int32, C.c_int32, _COLP, _COLP,
                                      C.POINTER(GroupByInfo), _P]),
+    "plgpu_gb_record_words": (C.c_int, [_COLP, C.c_int32, C.POINTER(Agg), C.c_int32,
+                                        C.POINTER(C.c_int32)]),
+    "plgpu_gb_plan_bottoms": (C.c_int, [_COLP, _COLP, C.c_int32, C.POINTER(Agg), C.c_int32,
+                                        C.POINTER(C.c_int32), _P]),
+    "plgpu_gb_partial_begin": (C.c_int, [_COLP, _COLP, C.c_int32, C.POINTER(Instr), C.c_int32,
+                                         C.POINTER(Agg), C.c_int32, C.POINTER(C.c_int32), C.c_int32,
+                                         C.POINTER(C.c_void_p), C.POINTER(C.c_int64),
+                                         C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                                         C.POINTER(GroupByInfo), _P]),
+    "plgpu_gb_partial_export": (C.c_int, [_P, _P, C.POINTER(C.c_int64), _P]),
+    "plgpu_gb_partial_free": (None, [_P]),
+    "plgpu_gb_merge": (C.c_int, [_P, C.c_int64, _COLP, C.c_int32, C.POINTER(Agg), C.c_int32,
+                                 C.POINTER(C.c_int32), C.c_int32, _COLP, _COLP,
+                                 C.POINTER(GroupByInfo), _P]),
 }
+
+GB_MAX_ACC = 6
 
 _lib = None
 

@@ -49,6 +49,8 @@ constexpr int kPlanSetSlots = 4096;   // LDS hash set of the distinct-key sample
 
 // Acc flags
 enum : int32_t { A_FSUM = 1, A_FSUMCAST = 2, A_ISUM = 4, A_CNT = 8, A_MIN = 16, A_MAX = 32, A_FLAGS = 64 };
+// Per-field merge ops of partial states
+enum : uint8_t { FOP_NONE = 0, FOP_ADD = 1, FOP_MIN = 2, FOP_MAX = 3, FOP_OR = 4, FOP_ADD192 = 5, FOP_SKIP = 6 };
 // Special-value flags (f64)
 enum : uint32_t { FL_NAN = 1, FL_PINF = 2, FL_NINF = 4 };
 // Status words
@@ -92,6 +94,7 @@ struct GbParams {
     AccSpec acc[kMaxAcc];
     uint64_t desc[kMaxAcc];  // packed per-acc descriptors (see dfield)
     int32_t bottom[kMaxAcc]; // fixed-point bottoms of the main launch (by value)
+    uint8_t fop[kMaxFields]; // per-field merge op (partial-state merge)
     int32_t pred_acc;       // acc whose column is the simple predicate's, or -1
     int32_t f_len;
     int32_t f_first;        // -1 unless maintain_order
@@ -977,6 +980,86 @@ __global__ void gather_bits_kernel(const uint32_t* __restrict__ src, const int64
     }
 }
 
+// --------------------------------------------- partial states (multi-GPU)
+// Record of one group: [kind (0 key, 1 null, 2 INT64_MIN), key, fields
+// 1..nfields-1 in table representation]; record_words = nfields + 1.
+__device__ __forceinline__ int dest_rank(uint64_t kind, uint64_t key, int world) {
+    if (kind != 0 || world <= 1) return 0;
+    const uint64_t h = (key ^ (key >> 31)) * 0xC2B2AE3D27D4EB4Full;
+    return (int)((h >> 33) % (uint64_t)world);
+}
+
+__device__ __forceinline__ bool slot_record(const GbParams& p, int64_t s, uint64_t& kind, uint64_t& key) {
+    if (*gfield(p, p.f_len, s) == 0) return false;
+    kind = s == p.gcap ? 1 : (s == p.gcap + 1 ? 2 : 0);
+    key = kind == 0 ? *gfield(p, 0, s) : (kind == 2 ? kEmptyKey : 0);
+    return true;
+}
+
+__global__ void gb_export_count_kernel(GbParams p, int world, uint64_t* counts) {
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < p.gcap + 2;
+         s += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t kind, key;
+        if (!slot_record(p, s, kind, key)) continue;
+        atomicAdd((unsigned long long*)&counts[dest_rank(kind, key, world)], 1ull);
+    }
+}
+
+__global__ void gb_export_kernel(GbParams p, int world, uint64_t* cursor, uint64_t* out) {
+    const int rw = p.nfields + 1;
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < p.gcap + 2;
+         s += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t kind, key;
+        if (!slot_record(p, s, kind, key)) continue;
+        const uint64_t idx = atomicAdd((unsigned long long*)&cursor[dest_rank(kind, key, world)], 1ull);
+        uint64_t* r = out + idx * rw;
+        r[0] = kind;
+        r[1] = key;
+        for (int f = 1; f < p.nfields; ++f) r[1 + f] = *gfield(p, f, s);
+    }
+}
+
+// Fold records (from any rank) into the global table.
+__global__ void gb_merge_kernel(GbParams p, const uint64_t* __restrict__ rec, int64_t nrec) {
+    const int rw = p.nfields + 1;
+    uint32_t special = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nrec; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t* r = rec + i * rw;
+        const uint64_t kind = r[0];
+        int64_t gs;
+        if (kind == 1) {
+            gs = p.gcap;
+            special |= 1u;
+        } else if (kind == 2) {
+            gs = p.gcap + 1;
+            special |= 2u;
+        } else {
+            gs = g_find(p, r[1]);
+        }
+        if (gs < 0) {
+            atomicAdd((unsigned long long*)&p.status[ST_TABLE_FULL], 1ull);
+            continue;
+        }
+        for (int f = 1; f < p.nfields; ++f) {
+            const uint64_t v = r[1 + f];
+            unsigned long long* q = (unsigned long long*)gfield(p, f, gs);
+            switch (p.fop[f]) {
+            case FOP_ADD: if (v) atomicAdd(q, (unsigned long long)v); break;
+            case FOP_MIN: if (v != ~0ull) atomicMin(q, (unsigned long long)v); break;
+            case FOP_MAX: if (v) atomicMax(q, (unsigned long long)v); break;
+            case FOP_OR: if (v) atomicOr(q, (unsigned long long)v); break;
+            case FOP_ADD192:
+                g_add192(gfield(p, f, gs), gfield(p, f + 1, gs), gfield(p, f + 2, gs), v, r[2 + f], r[3 + f]);
+                break;
+            default: break;
+            }
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) special |= __shfl_xor(special, off, 64);
+    if ((threadIdx.x & 63) == 0 && special) atomicOr((unsigned long long*)&p.status[ST_SPECIAL], (unsigned long long)special);
+}
+
 // ------------------------------------------------------------- host
 static int g_num_cus = 0;
 static int num_cus() {
@@ -1015,7 +1098,8 @@ struct Plan {
 };
 
 static int plan_groupby(const plgpu_column* key, const plgpu_column* cols, int32_t ncols, const plgpu_agg* aggs,
-                        int32_t naggs, bool maintain_order, const DevProgram& dp, Plan* pl) {
+                        int32_t naggs, bool maintain_order, const DevProgram& dp, Plan* pl,
+                        bool force_counts = false) {
     GbParams& p = pl->p;
     std::memset(&p, 0, sizeof p);
     p.key = to_dev(*key);
@@ -1045,7 +1129,9 @@ static int plan_groupby(const plgpu_column* key, const plgpu_column* cols, int32
         }
         AccSpec& ac = p.acc[acc_of_col[c]];
         const bool isf = dt == PLGPU_F64;
-        const bool nullable = cols[c].validity != nullptr;
+        // partial / merge mode keeps the record layout schema-only (the same on
+        // every rank whatever its validity bitmaps): counts always present
+        const bool nullable = cols[c].validity != nullptr || force_counts;
         switch (aggs[i].kind) {
         case PLGPU_AGG_SUM: ac.flags |= isf ? (A_FSUM | A_FLAGS) : A_ISUM; break;
         case PLGPU_AGG_MEAN:
@@ -1062,7 +1148,7 @@ static int plan_groupby(const plgpu_column* key, const plgpu_column* cols, int32
     }
     for (int a = 0; a < p.nacc; ++a) {
         AccSpec& ac = p.acc[a];
-        if ((ac.flags & A_CNT) && ac.c.validity == nullptr) ac.flags &= ~A_CNT;
+        if ((ac.flags & A_CNT) && ac.c.validity == nullptr && !force_counts) ac.flags &= ~A_CNT;
         if (ac.flags & (A_FSUM | A_FSUMCAST)) {
             ac.f_sum = nf;
             nf += 3;
@@ -1079,6 +1165,22 @@ static int plan_groupby(const plgpu_column* key, const plgpu_column* cols, int32
     if (nf > kMaxFields) return fail(PLGPU_ERR_INVALID, "too many accumulator fields");
     if (nf > 255) return fail(PLGPU_ERR_INVALID, "too many accumulator fields");
     p.nfields = nf;
+    std::memset(p.fop, 0, sizeof p.fop);
+    p.fop[p.f_len] = FOP_ADD;
+    if (p.f_first >= 0) p.fop[p.f_first] = FOP_MIN;
+    for (int a = 0; a < p.nacc; ++a) {
+        const AccSpec& ac = p.acc[a];
+        if (ac.f_sum >= 0) {
+            p.fop[ac.f_sum] = FOP_ADD192;
+            p.fop[ac.f_sum + 1] = FOP_SKIP;
+            p.fop[ac.f_sum + 2] = FOP_SKIP;
+        }
+        if (ac.f_isum >= 0) p.fop[ac.f_isum] = FOP_ADD;
+        if (ac.f_cnt >= 0) p.fop[ac.f_cnt] = FOP_ADD;
+        if (ac.f_min >= 0) p.fop[ac.f_min] = FOP_MIN;
+        if (ac.f_max >= 0) p.fop[ac.f_max] = FOP_MAX;
+        if (ac.f_flags >= 0) p.fop[ac.f_flags] = FOP_OR;
+    }
     for (int a = 0; a < p.nacc; ++a) {
         const AccSpec& ac = p.acc[a];
         auto fb = [](int f) -> uint64_t { return f < 0 ? (uint64_t)kNoField : (uint64_t)f; };
@@ -1210,214 +1312,279 @@ static hipError_t launch_main_dispatch(const Plan& pl, const DevProgram& dp, int
     return launch_main<2, false>(pl, dp, s);
 }
 
-}  // namespace plgpu
+// One group-by execution: plan, sampled windows, table, main launches,
+// finalize.  Shared by plgpu_group_by_agg (single GPU) and the partial /
+// merge entry points of the hash-partitioned multi-GPU group-by.
+struct GbRun {
+    Plan pl;
+    DevProgram dp;
+    int pred = 0;
+    hipStream_t s = nullptr;
+    uint64_t* status = nullptr;  // ST_WORDS words + kMaxAcc int32 bottoms
+    int32_t* bottoms = nullptr;
+    uint64_t* gtab = nullptr;
+    uint64_t st[ST_WORDS];
+    int32_t hb[kMaxAcc];         // host copy of the fixed-point bottoms
+    int gbits = 10;
+    int attempts = 0;
+    float ms = 0.f;
+    int32_t key_dtype = PLGPU_I64;
+    bool maintain = false;
+    int world = 1;
 
-using namespace plgpu;
+    GbRun() {
+        std::memset(st, 0, sizeof st);
+        std::memset(hb, 0, sizeof hb);
+    }
+    ~GbRun() {
+        dev_free(gtab, s);
+        dev_free(status, s);
+    }
+};
 
-PLGPU_API int plgpu_group_by_agg(const plgpu_column* key, const plgpu_column* cols, int32_t ncols,
-                                 const plgpu_instr* program, int32_t n_instr, const plgpu_agg* aggs, int32_t naggs,
-                                 int32_t maintain_order, plgpu_column* out_key, plgpu_column* out_aggs,
-                                 plgpu_groupby_info* info, void* stream) {
-    hipStream_t s = as_stream(stream);
-    if (key == nullptr || out_key == nullptr) return fail(PLGPU_ERR_INVALID, "key / out_key is NULL");
+static int gb_prepare(GbRun& R, const plgpu_column* key, const plgpu_column* cols, int32_t ncols,
+                      const plgpu_instr* program, int32_t n_instr, const plgpu_agg* aggs, int32_t naggs,
+                      bool maintain_order, bool force_counts, void* stream) {
+    R.s = as_stream(stream);
+    if (key == nullptr) return fail(PLGPU_ERR_INVALID, "key is NULL");
     if (ncols < 0 || ncols > PLGPU_MAX_COLS) return fail(PLGPU_ERR_INVALID, "too many columns (max 8)");
     if (naggs < 0 || naggs > PLGPU_MAX_COLS * 2) return fail(PLGPU_ERR_INVALID, "too many aggregations (max 16)");
     if (key->dtype != PLGPU_I64 && key->dtype != PLGPU_I32)
         return fail(PLGPU_ERR_SCHEMA, "group-by key must be Int64 or Int32");
     for (int i = 0; i < ncols; ++i)
         if (cols[i].length != key->length) return fail(PLGPU_ERR_SHAPE, "columns must match the key length");
-    std::memset(out_key, 0, sizeof *out_key);
-    for (int i = 0; i < naggs; ++i) std::memset(&out_aggs[i], 0, sizeof(plgpu_column));
-    plgpu_groupby_info local_info;
-    if (info == nullptr) info = &local_info;
-    std::memset(info, 0, sizeof *info);
-
-    DevProgram dp;
-    std::memset(&dp, 0, sizeof dp);
-    int pred = 0;
+    R.key_dtype = key->dtype;
+    R.maintain = maintain_order;
+    std::memset(&R.dp, 0, sizeof R.dp);
     int rc;
     if (program != nullptr && n_instr > 0) {
-        if ((rc = lower_program(cols, ncols, program, n_instr, &dp))) return rc;
-        if (dp.out_dtype != PLGPU_BOOL) return fail(PLGPU_ERR_SCHEMA, "filter predicate must be of type `Boolean`");
-        pred = dp.simple ? 1 : 2;
+        if ((rc = lower_program(cols, ncols, program, n_instr, &R.dp))) return rc;
+        if (R.dp.out_dtype != PLGPU_BOOL) return fail(PLGPU_ERR_SCHEMA, "filter predicate must be of type `Boolean`");
+        R.pred = R.dp.simple ? 1 : 2;
     }
-    Plan pl;
-    if ((rc = plan_groupby(key, cols, ncols, aggs, naggs, maintain_order != 0, dp, &pl))) return rc;
+    if ((rc = plan_groupby(key, cols, ncols, aggs, naggs, maintain_order, R.dp, &R.pl, force_counts))) return rc;
+    if ((rc = dev_alloc((void**)&R.status, ST_WORDS * 8 + kMaxAcc * 4, R.s))) return rc;
+    R.bottoms = (int32_t*)(R.status + ST_WORDS);
+    R.pl.p.status = R.status;
+    R.pl.p.bottoms = R.bottoms;
+    PLGPU_HIP(hipMemsetAsync(R.status, 0, ST_WORDS * 8 + kMaxAcc * 4, R.s));
+    return PLGPU_OK;
+}
+
+// Planning launch -> distinct-key estimate, fixed-point bottoms, table
+// sizes, kernel choice.  `fixed` (nullable) overrides the sampled bottoms.
+static int gb_plan(GbRun& R, const int32_t* fixed) {
+    Plan& pl = R.pl;
+    GbParams& p = pl.p;
+    const int64_t n = p.n;
+    gb_plan_kernel<<<p.nacc + 1, 256, 0, R.s>>>(p, R.bottoms, kPlanSamples);
+    PLGPU_HIP(hipGetLastError());
+    PLGPU_HIP(hipMemcpyAsync(R.st, R.status, sizeof R.st, hipMemcpyDeviceToHost, R.s));
+    PLGPU_HIP(hipMemcpyAsync(R.hb, R.bottoms, sizeof R.hb, hipMemcpyDeviceToHost, R.s));
+    PLGPU_HIP(hipStreamSynchronize(R.s));
+    if (fixed)
+        for (int a = 0; a < kMaxAcc; ++a) R.hb[a] = fixed[a];
+    size_tables(&pl, R.st[ST_DISTINCT], R.st[ST_SAMPLED], &R.gbits);
+    // fast path eligibility: no nulls, 8-byte columns
+    // at even offsets of 16-byte aligned buffers, simple or no predicate,
+    // LDS table in use
+    auto ok = [](const DevCol& c) {
+        return (c.dtype == PLGPU_I64 || c.dtype == PLGPU_F64) && c.validity == nullptr && (c.offset & 1) == 0 &&
+               ((uintptr_t)c.values & 15) == 0;
+    };
+    bool fast = pl.use_lds && R.pred != 2 && ok(p.key);
+    for (int a = 0; a < p.nacc; ++a) fast = fast && ok(p.acc[a].c);
+    if (R.pred == 1 && p.pred_acc < 0) fast = fast && ok(p.pred_col);
+    if (getenv("PLGPU_NO_FAST")) fast = false;
+    p.ablate = getenv("PLGPU_ABLATE") ? atoi(getenv("PLGPU_ABLATE")) : 0;
+    pl.fast_rows = getenv("PLGPU_FAST_ROWS") ? atoi(getenv("PLGPU_FAST_ROWS")) : 2;
+    if (pl.fast_rows != 2 && pl.fast_rows != 4) pl.fast_rows = 2;
+    pl.fast_threads = getenv("PLGPU_FAST_THREADS") ? atoi(getenv("PLGPU_FAST_THREADS")) : 512;
+    if (pl.fast_threads != 256 && pl.fast_threads != 512) pl.fast_threads = 512;
+    const int64_t tile = (int64_t)pl.fast_rows * pl.fast_threads;
+    p.n_full = fast ? (n / tile) * tile : 0;
+    {
+        // as many workgroups as the LDS budget allows per CU (up to 8)
+        const int per_cu =
+            (int)std::max<size_t>(1, std::min<size_t>(8, pl.lds_bytes ? (160 * 1024) / pl.lds_bytes : 8));
+        int64_t g = (int64_t)num_cus() * per_cu;
+        const int64_t need = (p.n_full + kMaxRowsPerWg - 1) / kMaxRowsPerWg;
+        if (g < need) g = need;
+        const int64_t useful = p.n_full / tile;
+        if (g > useful) g = useful < 1 ? 1 : useful;
+        pl.fast_grid = (int)g;
+    }
+    // sum-only signature with the compile-time field layout
+    bool so = p.f_first < 0 && p.f_len == 1 && p.nacc > 0;
+    for (int a = 0; a < p.nacc; ++a) {
+        const AccSpec& ac = p.acc[a];
+        so = so && ac.isf && ac.flags == (A_FSUM | A_FLAGS) && ac.f_sum == 2 + 4 * a && ac.f_flags == 5 + 4 * a &&
+             ac.f_cnt < 0;
+    }
+    pl.sum_only = so && !getenv("PLGPU_NO_SUMONLY");
+    p.row_begin = p.n_full;
+    return PLGPU_OK;
+}
+
+static int gb_alloc_table(GbRun& R) {
+    GbParams& p = R.pl.p;
+    dev_free(R.gtab, R.s);
+    R.gtab = nullptr;
+    p.gbits = R.gbits;
+    p.gcap = int64_t(1) << R.gbits;
+    const size_t wpf = (size_t)(p.gcap + 2);
+    int rc = dev_alloc((void**)&R.gtab, wpf * p.nfields * 8, R.s);
+    if (rc) return rc;
+    p.gtab = R.gtab;
+    const int ig = (int)std::min<int64_t>((int64_t)(wpf + 255) / 256, 256 * 8);
+    gb_init_table_kernel<<<ig, 256, 0, R.s>>>(R.gtab, (int64_t)wpf, p.nfields, p.min_init_mask);
+    // keep the plan words (distinct / sampled), clear the run words
+    PLGPU_HIP(hipMemsetAsync(R.status, 0, 6 * 8, R.s));
+    PLGPU_HIP(hipMemsetAsync(R.status + ST_MAXEX, 0, (ST_WORDS - ST_MAXEX) * 8, R.s));
+    PLGPU_HIP(hipGetLastError());
+    return PLGPU_OK;
+}
+
+// Exact max exponents of the flagged accs -> refit bottoms in `hint`.
+// Returns true when some window changes.
+static int gb_refit(GbRun& R, uint32_t flagged, int32_t* hint, bool* changed) {
+    GbParams& p = R.pl.p;
+    *changed = false;
+    for (int a = 0; a < kMaxAcc; ++a) hint[a] = R.hb[a];
+    if (!flagged) return PLGPU_OK;
+    for (int a = 0; a < p.nacc; ++a)
+        if ((flagged >> a) & 1u) gb_maxexp_kernel<<<std::max(1, num_cus() * 4), 256, 0, R.s>>>(p, a);
+    PLGPU_HIP(hipGetLastError());
+    PLGPU_HIP(hipMemcpyAsync(R.st, R.status, sizeof R.st, hipMemcpyDeviceToHost, R.s));
+    PLGPU_HIP(hipStreamSynchronize(R.s));
+    for (int a = 0; a < p.nacc; ++a) {
+        if (!((flagged >> a) & 1u)) continue;
+        const uint64_t fl = (R.st[ST_FXFLAGS] >> (2 * a)) & 3u;
+        const int tmax = (int)R.st[ST_MAXEX + a];
+        const int allowed = R.hb[a] + 1075 + (kSumWindowBits - 53);
+        if ((fl & 1u) || ((fl & 2u) && tmax > 0 && tmax < allowed)) {
+            // overflowed values were dropped, so the whole pass reruns
+            hint[a] = std::max(tmax, 1) - 1075 - (kSumWindowBits - 53);
+            *changed = *changed || hint[a] != R.hb[a];
+        }
+    }
+    return PLGPU_OK;
+}
+
+// Main launches with table-size reruns; window refits too when auto_refit.
+// Without auto_refit a needed refit is reported in *refit / hint.
+static int gb_main(GbRun& R, bool auto_refit, bool* refit, int32_t* hint) {
+    Plan& pl = R.pl;
     GbParams& p = pl.p;
     const int64_t n = p.n;
     const bool debug = getenv("PLGPU_DEBUG") != nullptr;
-
-    // device scratch: status + bottoms
-    uint64_t* status = nullptr;
-    if ((rc = dev_alloc((void**)&status, ST_WORDS * 8 + kMaxAcc * 4, s))) return rc;
-    int32_t* bottoms = (int32_t*)(status + ST_WORDS);
-    p.status = status;
-    p.bottoms = bottoms;
-    uint64_t st[ST_WORDS];
-    int32_t host_bottoms[kMaxAcc] = {0};
-
-    // ---- plan launch: sampled exponents + distinct keys
-    PLGPU_HIP(hipMemsetAsync(status, 0, ST_WORDS * 8, s));
-    gb_plan_kernel<<<p.nacc + 1, 256, 0, s>>>(p, bottoms, kPlanSamples);
-    PLGPU_HIP(hipGetLastError());
-    PLGPU_HIP(hipMemcpyAsync(st, status, sizeof st, hipMemcpyDeviceToHost, s));
-    PLGPU_HIP(hipMemcpyAsync(host_bottoms, bottoms, sizeof host_bottoms, hipMemcpyDeviceToHost, s));
-    PLGPU_HIP(hipStreamSynchronize(s));
-    int gbits = 10;
-    size_tables(&pl, st[ST_DISTINCT], st[ST_SAMPLED], &gbits);
-    {
-        // fast path eligibility: no nulls, 8-byte
-        // columns at even offsets of 16-byte aligned buffers, simple or no
-        // predicate, LDS table in use
-        auto ok = [](const DevCol& c) {
-            return (c.dtype == PLGPU_I64 || c.dtype == PLGPU_F64) && c.validity == nullptr && (c.offset & 1) == 0 &&
-                   ((uintptr_t)c.values & 15) == 0;
-        };
-        bool fast = pl.use_lds && pred != 2 && ok(p.key);
-        for (int a = 0; a < p.nacc; ++a) fast = fast && ok(p.acc[a].c);
-        if (pred == 1 && p.pred_acc < 0) fast = fast && ok(p.pred_col);
-        if (getenv("PLGPU_NO_FAST")) fast = false;
-        p.ablate = getenv("PLGPU_ABLATE") ? atoi(getenv("PLGPU_ABLATE")) : 0;
-        pl.fast_rows = getenv("PLGPU_FAST_ROWS") ? atoi(getenv("PLGPU_FAST_ROWS")) : 2;
-        if (pl.fast_rows != 2 && pl.fast_rows != 4) pl.fast_rows = 2;
-        pl.fast_threads = getenv("PLGPU_FAST_THREADS") ? atoi(getenv("PLGPU_FAST_THREADS")) : 512;
-        if (pl.fast_threads != 256 && pl.fast_threads != 512) pl.fast_threads = 256;
-        const int64_t tile = (int64_t)pl.fast_rows * pl.fast_threads;
-        p.n_full = fast ? (n / tile) * tile : 0;
-        {
-            // as many workgroups as the LDS budget allows per CU (up to 8)
-            int per_cu = (int)std::max<size_t>(1, std::min<size_t>(8, pl.lds_bytes ? (160 * 1024) / pl.lds_bytes : 8));
-            int64_t g = (int64_t)num_cus() * per_cu;
-            const int64_t need = (p.n_full + kMaxRowsPerWg - 1) / kMaxRowsPerWg;
-            if (g < need) g = need;
-            const int64_t useful = p.n_full / tile;
-            if (g > useful) g = useful < 1 ? 1 : useful;
-            pl.fast_grid = (int)g;
-        }
-        // sum-only signature with the compile-time field layout
-        bool so = p.f_first < 0 && p.f_len == 1 && p.nacc > 0;
-        for (int a = 0; a < p.nacc; ++a) {
-            const AccSpec& ac = p.acc[a];
-            so = so && ac.isf && ac.flags == (A_FSUM | A_FLAGS) && ac.f_sum == 2 + 4 * a && ac.f_flags == 5 + 4 * a &&
-                 ac.f_cnt < 0;
-        }
-        pl.sum_only = so && !getenv("PLGPU_NO_SUMONLY");
-        p.row_begin = p.n_full;
-    }
-
-    uint64_t* gtab = nullptr;
+    if (refit) *refit = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     PLGPU_HIP(hipEventCreate(&ev0));
     PLGPU_HIP(hipEventCreate(&ev1));
-    int attempt = 0;
-    for (;; ++attempt) {
-        p.gbits = gbits;
-        p.gcap = int64_t(1) << gbits;
-        const size_t wpf = (size_t)(p.gcap + 2);
-        if ((rc = dev_alloc((void**)&gtab, wpf * p.nfields * 8, s))) break;
-        p.gtab = gtab;
-        const int ig = (int)std::min<int64_t>((int64_t)(wpf + 255) / 256, 256 * 8);
-        gb_init_table_kernel<<<ig, 256, 0, s>>>(gtab, (int64_t)wpf, p.nfields, p.min_init_mask);
-        // keep the plan words, clear the run words
-        PLGPU_HIP(hipMemsetAsync(status, 0, 6 * 8, s));
-        PLGPU_HIP(hipMemsetAsync(status + ST_MAXEX, 0, (ST_WORDS - ST_MAXEX) * 8, s));
-        PLGPU_HIP(hipMemcpyAsync(bottoms, host_bottoms, sizeof host_bottoms, hipMemcpyHostToDevice, s));
-        for (int a = 0; a < kMaxAcc; ++a) p.bottom[a] = host_bottoms[a];
-        PLGPU_HIP(hipGetLastError());
-        PLGPU_HIP(hipEventRecord(ev0, s));
+    int rc = PLGPU_OK;
+    for (R.attempts = 0;; ++R.attempts) {
+        if ((rc = gb_alloc_table(R))) break;
+        PLGPU_HIP(hipMemcpyAsync(R.bottoms, R.hb, sizeof R.hb, hipMemcpyHostToDevice, R.s));
+        for (int a = 0; a < kMaxAcc; ++a) p.bottom[a] = R.hb[a];
+        PLGPU_HIP(hipEventRecord(ev0, R.s));
         if (n > 0) {
-            if (p.n_full > 0) PLGPU_HIP(launch_fast_dispatch(pl, dp, pred, s));
+            if (p.n_full > 0) PLGPU_HIP(launch_fast_dispatch(pl, R.dp, R.pred, R.s));
             if (p.row_begin < n) {
                 Plan tail = pl;
                 const int64_t rows = n - p.row_begin;
                 const int64_t g = (rows + 4 * kGbThreads - 1) / (4 * kGbThreads);
                 tail.grid = (int)std::min<int64_t>(pl.grid, g < 1 ? 1 : g);
-                PLGPU_HIP(launch_main_dispatch(tail, dp, pred, s));
+                PLGPU_HIP(launch_main_dispatch(tail, R.dp, R.pred, R.s));
             }
         }
-        PLGPU_HIP(hipEventRecord(ev1, s));
-        PLGPU_HIP(hipMemcpyAsync(st, status, sizeof st, hipMemcpyDeviceToHost, s));
-        PLGPU_HIP(hipMemcpyAsync(host_bottoms, bottoms, sizeof host_bottoms, hipMemcpyDeviceToHost, s));
-        PLGPU_HIP(hipStreamSynchronize(s));
+        PLGPU_HIP(hipEventRecord(ev1, R.s));
+        PLGPU_HIP(hipMemcpyAsync(R.st, R.status, sizeof R.st, hipMemcpyDeviceToHost, R.s));
+        PLGPU_HIP(hipStreamSynchronize(R.s));
         if (debug) {
             fprintf(stderr,
-                    "[plgpu] gb attempt %d: n=%lld grid=%d lds=%d lcap=%d gcap=%lld nfields=%d lds_bytes=%zu "
-                    "distinct=%llu/%llu newkeys=%llu special=%llu global_rows=%llu full=%llu selected=%llu\n",
-                    attempt, (long long)n, pl.grid, (int)pl.use_lds, p.lcap, (long long)p.gcap, p.nfields,
-                    pl.lds_bytes, (unsigned long long)st[ST_DISTINCT], (unsigned long long)st[ST_SAMPLED],
-                    (unsigned long long)st[ST_NEWKEYS], (unsigned long long)st[ST_SPECIAL],
-                    (unsigned long long)st[ST_GLOBAL_ROWS], (unsigned long long)st[ST_TABLE_FULL],
-                    (unsigned long long)st[ST_SELECTED]);
+                    "[plgpu] gb attempt %d: n=%lld grid=%d/%d lds=%d lcap=%d gcap=%lld nfields=%d lds_bytes=%zu "
+                    "fast=%lld sumonly=%d distinct=%llu/%llu newkeys=%llu special=%llu global_rows=%llu full=%llu "
+                    "selected=%llu fx=%llx\n",
+                    R.attempts, (long long)n, pl.grid, pl.fast_grid, (int)pl.use_lds, p.lcap, (long long)p.gcap,
+                    p.nfields, pl.lds_bytes, (long long)p.n_full, (int)pl.sum_only,
+                    (unsigned long long)R.st[ST_DISTINCT], (unsigned long long)R.st[ST_SAMPLED],
+                    (unsigned long long)R.st[ST_NEWKEYS], (unsigned long long)R.st[ST_SPECIAL],
+                    (unsigned long long)R.st[ST_GLOBAL_ROWS], (unsigned long long)R.st[ST_TABLE_FULL],
+                    (unsigned long long)R.st[ST_SELECTED], (unsigned long long)R.st[ST_FXFLAGS]);
         }
         bool again = false;
-        if (st[ST_TABLE_FULL] > 0) {
-            gbits = std::max(gbits + 3, log2_ceil((int64_t)st[ST_NEWKEYS] * 4));
+        if (R.st[ST_TABLE_FULL] > 0) {
+            R.gbits = std::max(R.gbits + 3, log2_ceil((int64_t)R.st[ST_NEWKEYS] * 4));
             again = true;
         }
-        uint32_t fxflag_accs = 0;
+        uint32_t flagged = 0;
         for (int a = 0; a < p.nacc; ++a)
-            if ((p.acc[a].flags & (A_FSUM | A_FSUMCAST)) && ((st[ST_FXFLAGS] >> (2 * a)) & 3u)) fxflag_accs |= 1u << a;
-        if (fxflag_accs) {
-            // exact max exponent of each flagged column, then refit its window
-            for (int a = 0; a < p.nacc; ++a)
-                if ((fxflag_accs >> a) & 1u) gb_maxexp_kernel<<<std::max(1, num_cus() * 4), 256, 0, s>>>(p, a);
-            PLGPU_HIP(hipGetLastError());
-            PLGPU_HIP(hipMemcpyAsync(st, status, sizeof st, hipMemcpyDeviceToHost, s));
-            PLGPU_HIP(hipStreamSynchronize(s));
-            for (int a = 0; a < p.nacc; ++a) {
-                if (!((fxflag_accs >> a) & 1u)) continue;
-                const uint64_t fl = (st[ST_FXFLAGS] >> (2 * a)) & 3u;
-                const int tmax = (int)st[ST_MAXEX + a];
-                const int allowed = host_bottoms[a] + 1075 + (kSumWindowBits - 53);
-                if ((fl & 1u) || ((fl & 2u) && tmax > 0 && tmax < allowed)) {
-                    // overflowed values were dropped, so the whole pass reruns
-                    host_bottoms[a] = std::max(tmax, 1) - 1075 - (kSumWindowBits - 53);
+            if ((p.acc[a].flags & (A_FSUM | A_FSUMCAST)) && ((R.st[ST_FXFLAGS] >> (2 * a)) & 3u)) flagged |= 1u << a;
+        if (flagged) {
+            int32_t h[kMaxAcc];
+            bool changed = false;
+            if ((rc = gb_refit(R, flagged, h, &changed))) break;
+            if (changed) {
+                if (auto_refit) {
+                    for (int a = 0; a < kMaxAcc; ++a) R.hb[a] = h[a];
                     again = true;
+                } else {
+                    if (refit) *refit = true;
+                    if (hint)
+                        for (int a = 0; a < kMaxAcc; ++a) hint[a] = h[a];
                 }
             }
         }
-        if (!again || attempt >= 3) {
-            if (again) rc = fail(PLGPU_ERR_CAPACITY, "group-by did not converge after retries");
+        if (!again) break;
+        if (R.attempts >= 3) {
+            rc = fail(PLGPU_ERR_CAPACITY, "group-by did not converge after retries");
             break;
         }
-        dev_free(gtab, s);
-        gtab = nullptr;
     }
-    float ms = 0.f;
-    if (rc == PLGPU_OK) (void)hipEventElapsedTime(&ms, ev0, ev1);
+    if (rc == PLGPU_OK) (void)hipEventElapsedTime(&R.ms, ev0, ev1);
     (void)hipEventDestroy(ev0);
     (void)hipEventDestroy(ev1);
-    if (rc) {
-        dev_free(gtab, s);
-        dev_free(status, s);
-        return rc;
-    }
-    const int64_t groups =
-        (int64_t)st[ST_NEWKEYS] + ((st[ST_SPECIAL] & 1) ? 1 : 0) + ((st[ST_SPECIAL] & 2) ? 1 : 0);
-    info->rows_in = n;
-    info->rows_selected = (int64_t)st[ST_SELECTED];
-    info->groups = groups;
-    info->global_path_rows = (int64_t)st[ST_GLOBAL_ROWS];
-    info->reruns = attempt;
-    info->lds_slots = pl.use_lds ? p.lcap : 0;
-    info->grid = pl.grid;
-    info->table_capacity = p.gcap;
-    info->main_kernel_ms = ms;
-    info->path = p.n_full > 0 ? (pl.sum_only ? 2 : 1) : 0;
-    for (int a = 0; a < p.nacc; ++a)
-        if ((st[ST_FXFLAGS] >> (2 * a)) & 2u) info->sum_inexact |= 1 << a;
+    return rc;
+}
 
-    // ---- outputs
+static int64_t gb_groups(const GbRun& R) {
+    return (int64_t)R.st[ST_NEWKEYS] + ((R.st[ST_SPECIAL] & 1) ? 1 : 0) + ((R.st[ST_SPECIAL] & 2) ? 1 : 0);
+}
+
+static void gb_fill_info(const GbRun& R, plgpu_groupby_info* info) {
+    const GbParams& p = R.pl.p;
+    std::memset(info, 0, sizeof *info);
+    info->rows_in = p.n;
+    info->rows_selected = (int64_t)R.st[ST_SELECTED];
+    info->groups = gb_groups(R);
+    info->global_path_rows = (int64_t)R.st[ST_GLOBAL_ROWS];
+    info->reruns = R.attempts;
+    info->lds_slots = R.pl.use_lds ? p.lcap : 0;
+    info->grid = p.n_full > 0 ? R.pl.fast_grid : R.pl.grid;
+    info->table_capacity = p.gcap;
+    info->main_kernel_ms = R.ms;
+    info->path = p.n_full > 0 ? (R.pl.sum_only ? 2 : 1) : 0;
+    for (int a = 0; a < p.nacc; ++a)
+        if ((R.st[ST_FXFLAGS] >> (2 * a)) & 2u) info->sum_inexact |= 1 << a;
+}
+
+// Global table -> output columns (+ first-occurrence order, key narrowing).
+static int gb_finalize(GbRun& R, int32_t naggs, plgpu_column* out_key, plgpu_column* out_aggs) {
+    Plan& pl = R.pl;
+    GbParams& p = pl.p;
+    hipStream_t s = R.s;
+    const int64_t groups = gb_groups(R);
     FinParams fp;
     std::memset(&fp, 0, sizeof fp);
-    rc = make_owned_column(out_key, PLGPU_I64, groups, true, s);
+    int rc = make_owned_column(out_key, PLGPU_I64, groups, true, s);
     for (int i = 0; i < naggs && rc == PLGPU_OK; ++i) {
         const OutSpec& o = pl.outs[i];
         const bool nullable = o.kind == PLGPU_AGG_MEAN || o.kind == PLGPU_AGG_MIN || o.kind == PLGPU_AGG_MAX;
         rc = make_owned_column(&out_aggs[i], o.out_dtype, groups, nullable, s);
     }
     uint64_t* first = nullptr;
-    if (rc == PLGPU_OK && maintain_order && groups > 0) rc = dev_alloc((void**)&first, groups * 8, s);
+    if (rc == PLGPU_OK && R.maintain && groups > 0) rc = dev_alloc((void**)&first, groups * 8, s);
     if (rc == PLGPU_OK && groups > 0) {
         fp.nout = naggs;
         for (int i = 0; i < naggs; ++i) {
@@ -1437,7 +1604,7 @@ PLGPU_API int plgpu_group_by_agg(const plgpu_column* key, const plgpu_column* co
         if (e != hipSuccess) rc = hip_fail(e, "gb_finalize_kernel");
         uint64_t produced = 0;
         if (rc == PLGPU_OK) {
-            e = hipMemcpyAsync(&produced, status + ST_GROUPS_OUT, 8, hipMemcpyDeviceToHost, s);
+            e = hipMemcpyAsync(&produced, R.status + ST_GROUPS_OUT, 8, hipMemcpyDeviceToHost, s);
             if (e == hipSuccess) e = hipStreamSynchronize(s);
             if (e != hipSuccess) rc = hip_fail(e, "finalize count");
         }
@@ -1446,13 +1613,13 @@ PLGPU_API int plgpu_group_by_agg(const plgpu_column* key, const plgpu_column* co
             snprintf(buf, sizeof buf,
                      "internal: group count mismatch (inserted %llu + specials %llu, finalized %llu, "
                      "global rows %llu, table_full %llu)",
-                     (unsigned long long)st[ST_NEWKEYS], (unsigned long long)st[ST_SPECIAL],
-                     (unsigned long long)produced, (unsigned long long)st[ST_GLOBAL_ROWS],
-                     (unsigned long long)st[ST_TABLE_FULL]);
+                     (unsigned long long)R.st[ST_NEWKEYS], (unsigned long long)R.st[ST_SPECIAL],
+                     (unsigned long long)produced, (unsigned long long)R.st[ST_GLOBAL_ROWS],
+                     (unsigned long long)R.st[ST_TABLE_FULL]);
             rc = fail(PLGPU_ERR_CAPACITY, buf);
         }
     }
-    if (rc == PLGPU_OK && maintain_order && groups > 1) {
+    if (rc == PLGPU_OK && R.maintain && groups > 1) {
         // order groups by first occurrence (host argsort of `groups` row ids)
         std::vector<uint64_t> hf(groups);
         std::vector<int64_t> perm(groups);
@@ -1496,7 +1663,7 @@ PLGPU_API int plgpu_group_by_agg(const plgpu_column* key, const plgpu_column* co
             }
         }
     }
-    if (rc == PLGPU_OK && key->dtype == PLGPU_I32) {
+    if (rc == PLGPU_OK && R.key_dtype == PLGPU_I32) {
         // narrow the key back to Int32 (the reference keeps the key dtype)
         plgpu_column nk;
         rc = make_owned_column(&nk, PLGPU_I32, groups, true, s);
@@ -1512,15 +1679,180 @@ PLGPU_API int plgpu_group_by_agg(const plgpu_column* key, const plgpu_column* co
         }
     }
     if (rc == PLGPU_OK) {
-        out_key->null_count = (st[ST_SPECIAL] & 1) ? 1 : 0;
-        PLGPU_HIP(hipStreamSynchronize(s));
+        out_key->null_count = (R.st[ST_SPECIAL] & 1) ? 1 : 0;
+        hipError_t e = hipStreamSynchronize(s);
+        if (e != hipSuccess) rc = hip_fail(e, "finalize sync");
     }
     dev_free(first, s);
-    dev_free(gtab, s);
-    dev_free(status, s);
     if (rc) {
         plgpu_column_release(out_key);
         for (int i = 0; i < naggs; ++i) plgpu_column_release(&out_aggs[i]);
     }
     return rc;
+}
+
+}  // namespace plgpu
+
+using namespace plgpu;
+
+PLGPU_API int plgpu_group_by_agg(const plgpu_column* key, const plgpu_column* cols, int32_t ncols,
+                                 const plgpu_instr* program, int32_t n_instr, const plgpu_agg* aggs, int32_t naggs,
+                                 int32_t maintain_order, plgpu_column* out_key, plgpu_column* out_aggs,
+                                 plgpu_groupby_info* info, void* stream) {
+    if (out_key == nullptr) return fail(PLGPU_ERR_INVALID, "out_key is NULL");
+    std::memset(out_key, 0, sizeof *out_key);
+    for (int i = 0; i < naggs && out_aggs; ++i) std::memset(&out_aggs[i], 0, sizeof(plgpu_column));
+    GbRun R;
+    int rc = gb_prepare(R, key, cols, ncols, program, n_instr, aggs, naggs, maintain_order != 0, false, stream);
+    if (!rc) rc = gb_plan(R, nullptr);
+    if (!rc) rc = gb_main(R, true, nullptr, nullptr);
+    if (rc) return rc;
+    if (info) gb_fill_info(R, info);
+    return gb_finalize(R, naggs, out_key, out_aggs);
+}
+
+// ------------------------------------------------------- multi-GPU partials
+struct plgpu_gb_partial {
+    GbRun run;
+};
+
+PLGPU_API int plgpu_gb_record_words(const plgpu_column* cols, int32_t ncols, const plgpu_agg* aggs, int32_t naggs,
+                                    int32_t* out_words) {
+    if (out_words == nullptr || (cols == nullptr && ncols > 0)) return fail(PLGPU_ERR_INVALID, "NULL argument");
+    if (ncols < 0 || ncols > PLGPU_MAX_COLS) return fail(PLGPU_ERR_INVALID, "too many columns (max 8)");
+    std::vector<plgpu_column> c2(cols, cols + ncols);
+    for (auto& c : c2) c.length = 0;
+    plgpu_column k;
+    std::memset(&k, 0, sizeof k);
+    k.dtype = PLGPU_I64;
+    Plan pl;
+    DevProgram dp;
+    std::memset(&dp, 0, sizeof dp);
+    const int rc = plan_groupby(&k, c2.data(), ncols, aggs, naggs, false, dp, &pl, true);
+    if (rc) return rc;
+    *out_words = pl.p.nfields + 1;
+    return PLGPU_OK;
+}
+
+PLGPU_API int plgpu_gb_plan_bottoms(const plgpu_column* key, const plgpu_column* cols, int32_t ncols,
+                                    const plgpu_agg* aggs, int32_t naggs, int32_t* out_bottoms, void* stream) {
+    if (out_bottoms == nullptr) return fail(PLGPU_ERR_INVALID, "out_bottoms is NULL");
+    GbRun R;
+    int rc = gb_prepare(R, key, cols, ncols, nullptr, 0, aggs, naggs, false, true, stream);
+    if (!rc) rc = gb_plan(R, nullptr);
+    if (rc) return rc;
+    for (int a = 0; a < kMaxAcc; ++a) out_bottoms[a] = R.hb[a];
+    return PLGPU_OK;
+}
+
+PLGPU_API int plgpu_gb_partial_begin(const plgpu_column* key, const plgpu_column* cols, int32_t ncols,
+                                     const plgpu_instr* program, int32_t n_instr, const plgpu_agg* aggs,
+                                     int32_t naggs, const int32_t* bottoms, int32_t world, plgpu_gb_partial** out,
+                                     int64_t* out_records, int32_t* out_bottoms_used, int32_t* out_refit,
+                                     int32_t* out_bottoms_hint, plgpu_groupby_info* info, void* stream) {
+    if (out == nullptr || out_records == nullptr || out_bottoms_used == nullptr || out_refit == nullptr ||
+        out_bottoms_hint == nullptr)
+        return fail(PLGPU_ERR_INVALID, "NULL argument");
+    if (world < 1) return fail(PLGPU_ERR_INVALID, "world must be >= 1");
+    *out = nullptr;
+    plgpu_gb_partial* h = new plgpu_gb_partial();
+    GbRun& R = h->run;
+    R.world = world;
+    bool refit = false;
+    int rc = gb_prepare(R, key, cols, ncols, program, n_instr, aggs, naggs, false, true, stream);
+    if (!rc) rc = gb_plan(R, bottoms);
+    if (!rc) rc = gb_main(R, false, &refit, out_bottoms_hint);
+    if (rc) {
+        delete h;
+        return rc;
+    }
+    for (int a = 0; a < kMaxAcc; ++a) {
+        out_bottoms_used[a] = R.hb[a];
+        if (!refit) out_bottoms_hint[a] = R.hb[a];
+    }
+    *out_refit = refit ? 1 : 0;
+    *out_records = gb_groups(R);
+    if (info) gb_fill_info(R, info);
+    *out = h;
+    return PLGPU_OK;
+}
+
+PLGPU_API int plgpu_gb_partial_export(plgpu_gb_partial* h, void* dst_records, int64_t* out_counts, void* stream) {
+    if (h == nullptr || out_counts == nullptr) return fail(PLGPU_ERR_INVALID, "NULL argument");
+    GbRun& R = h->run;
+    hipStream_t s = stream ? as_stream(stream) : R.s;
+    const GbParams& p = R.pl.p;
+    const int W = R.world;
+    uint64_t* counts = nullptr;  // [W] counts, [W] cursors
+    int rc = dev_alloc((void**)&counts, (size_t)W * 16, s);
+    if (rc) return rc;
+    PLGPU_HIP(hipMemsetAsync(counts, 0, (size_t)W * 16, s));
+    const int fg = (int)std::min<int64_t>((p.gcap + 2 + 255) / 256, 256 * 16);
+    gb_export_count_kernel<<<fg, 256, 0, s>>>(p, W, counts);
+    std::vector<uint64_t> hc(W), cur(W);
+    PLGPU_HIP(hipMemcpyAsync(hc.data(), counts, (size_t)W * 8, hipMemcpyDeviceToHost, s));
+    PLGPU_HIP(hipStreamSynchronize(s));
+    uint64_t run = 0;
+    for (int w = 0; w < W; ++w) {
+        cur[w] = run;
+        run += hc[w];
+        out_counts[w] = (int64_t)hc[w];
+    }
+    if (run > 0) {
+        if (dst_records == nullptr) {
+            dev_free(counts, s);
+            return fail(PLGPU_ERR_INVALID, "dst_records is NULL");
+        }
+        PLGPU_HIP(hipMemcpyAsync(counts + W, cur.data(), (size_t)W * 8, hipMemcpyHostToDevice, s));
+        gb_export_kernel<<<fg, 256, 0, s>>>(p, W, counts + W, (uint64_t*)dst_records);
+        PLGPU_HIP(hipGetLastError());
+    }
+    PLGPU_HIP(hipStreamSynchronize(s));
+    dev_free(counts, s);
+    return PLGPU_OK;
+}
+
+PLGPU_API void plgpu_gb_partial_free(plgpu_gb_partial* h) { delete h; }
+
+PLGPU_API int plgpu_gb_merge(const void* records, int64_t n_records, const plgpu_column* cols, int32_t ncols,
+                             const plgpu_agg* aggs, int32_t naggs, const int32_t* bottoms, int32_t key_dtype,
+                             plgpu_column* out_key, plgpu_column* out_aggs, plgpu_groupby_info* info, void* stream) {
+    if (out_key == nullptr || bottoms == nullptr || (cols == nullptr && ncols > 0))
+        return fail(PLGPU_ERR_INVALID, "NULL argument");
+    if (ncols < 0 || ncols > PLGPU_MAX_COLS) return fail(PLGPU_ERR_INVALID, "too many columns (max 8)");
+    if (n_records < 0 || (n_records > 0 && records == nullptr)) return fail(PLGPU_ERR_INVALID, "bad records");
+    std::memset(out_key, 0, sizeof *out_key);
+    for (int i = 0; i < naggs && out_aggs; ++i) std::memset(&out_aggs[i], 0, sizeof(plgpu_column));
+    // the schema alone fixes the record layout: a length-0 key of the right
+    // dtype and the columns' dtypes (their buffers are not read)
+    std::vector<plgpu_column> c2(cols, cols + ncols);
+    for (auto& c : c2) c.length = 0;
+    plgpu_column k;
+    std::memset(&k, 0, sizeof k);
+    k.dtype = key_dtype == PLGPU_I32 ? PLGPU_I32 : PLGPU_I64;
+    GbRun R;
+    int rc = gb_prepare(R, &k, c2.data(), ncols, nullptr, 0, aggs, naggs, false, true, stream);
+    if (rc) return rc;
+    for (int a = 0; a < kMaxAcc; ++a) {
+        R.hb[a] = bottoms[a];
+        R.pl.p.bottom[a] = bottoms[a];
+    }
+    R.gbits = log2_ceil(std::max<int64_t>(1024, n_records * 2));
+    GbParams& p = R.pl.p;
+    for (R.attempts = 0;; ++R.attempts) {
+        if ((rc = gb_alloc_table(R))) return rc;
+        PLGPU_HIP(hipMemcpyAsync(R.bottoms, R.hb, sizeof R.hb, hipMemcpyHostToDevice, R.s));
+        if (n_records > 0) {
+            const int g = (int)std::min<int64_t>((n_records + 255) / 256, 256 * 16);
+            gb_merge_kernel<<<g, 256, 0, R.s>>>(p, (const uint64_t*)records, n_records);
+            PLGPU_HIP(hipGetLastError());
+        }
+        PLGPU_HIP(hipMemcpyAsync(R.st, R.status, sizeof R.st, hipMemcpyDeviceToHost, R.s));
+        PLGPU_HIP(hipStreamSynchronize(R.s));
+        if (R.st[ST_TABLE_FULL] == 0) break;
+        if (R.attempts >= 3) return fail(PLGPU_ERR_CAPACITY, "merge did not converge");
+        R.gbits += 3;
+    }
+    if (info) gb_fill_info(R, info);
+    return gb_finalize(R, naggs, out_key, out_aggs);
 }

@@ -550,8 +550,15 @@ def _const_bool(e: Expr):
     return ev(e) is True
 
 
-def _group_by(df: DataFrame, key: str, aggs: list[Expr], maintain_order: bool,
-              pred: Expr | None, info: dict | None) -> DataFrame:
+class _GbCall:
+    """Lowered arguments of one group-by call through the C-ABI (shared by
+    the single-GPU path and polaroid_amd.distributed)."""
+
+    __slots__ = ("key", "keycol", "names", "cols", "ncols", "prog", "n_instr", "aggs", "naggs",
+                 "out_names", "_keep")
+
+
+def _gb_lower(df: DataFrame, key: str, aggs: list[Expr], pred: Expr | None) -> _GbCall:
     if key not in df._cols:
         raise N.ComputeError(f'unable to find column "{key}"')
     specs: list[tuple[str, str]] = []  # (kind, column)
@@ -569,7 +576,8 @@ def _group_by(df: DataFrame, key: str, aggs: list[Expr], maintain_order: bool,
         out_names.append(name)
     # columns passed to the kernel: predicate columns + aggregated columns
     names: list[str] = []
-    prog, n_instr = None, 0
+    g = _GbCall()
+    g.prog, g.n_instr = None, 0
     if pred is not None:
         names = pred.meta_root_names()
     for _, c_ in specs:
@@ -584,25 +592,42 @@ def _group_by(df: DataFrame, key: str, aggs: list[Expr], maintain_order: bool,
     if pred is not None:
         schema = {nm: df._cols[nm].dtype.code for nm in names}
         p = lower(pred, idx, schema)
-        prog, n_instr = to_instr_array(p), builtins.len(p)
+        g.prog, g.n_instr = to_instr_array(p), builtins.len(p)
     agg_arr = (N.Agg * max(1, builtins.len(specs)))()
     for i, (k, c_) in enumerate(specs):
         agg_arr[i].kind = _AGG_CODE[k]
         agg_arr[i].col = idx[c_]
-    cols = _col_array([df._cols[nm] for nm in names])
+    g.key = key
+    g.keycol = df._cols[key]._col
+    g.names = names
+    g.cols = _col_array([df._cols[nm] for nm in names])
+    g.ncols = builtins.len(names)
+    g.aggs = agg_arr
+    g.naggs = builtins.len(specs)
+    g.out_names = out_names
+    g._keep = [df._cols[nm] for nm in names] + [df._cols[key]]
+    return g
+
+
+def _gb_frame(g: _GbCall, out_key: N.Column, out_aggs) -> DataFrame:
+    series = [Series._from_native(g.key, out_key)]
+    for i, nm in enumerate(g.out_names):
+        series.append(Series._from_native(nm, out_aggs[i]))
+    return DataFrame(series)
+
+
+def _group_by(df: DataFrame, key: str, aggs: list[Expr], maintain_order: bool,
+              pred: Expr | None, info: dict | None) -> DataFrame:
+    g = _gb_lower(df, key, aggs, pred)
     out_key = N.Column()
-    out_aggs = (N.Column * max(1, builtins.len(specs)))()
+    out_aggs = (N.Column * max(1, g.naggs))()
     gi = N.GroupByInfo()
-    keycol = df._cols[key]._col
-    N.check(N.lib().plgpu_group_by_agg(C.byref(keycol), cols, builtins.len(names), prog, n_instr, agg_arr,
-                                       builtins.len(specs), int(bool(maintain_order)), C.byref(out_key),
+    N.check(N.lib().plgpu_group_by_agg(C.byref(g.keycol), g.cols, g.ncols, g.prog, g.n_instr, g.aggs,
+                                       g.naggs, int(bool(maintain_order)), C.byref(out_key),
                                        out_aggs, C.byref(gi), None))
     if info is not None:
         info.update(gi.as_dict())
-    series = [Series._from_native(key, out_key)]
-    for i, nm in enumerate(out_names):
-        series.append(Series._from_native(nm, out_aggs[i]))
-    return DataFrame(series)
+    return _gb_frame(g, out_key, out_aggs)
 
 
 def _execute(node: tuple, info: dict | None = None) -> DataFrame:

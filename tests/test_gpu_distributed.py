@@ -1,0 +1,198 @@
+"""GPU parity of the hash-partitioned group-by (partial -> export -> merge)
+through the C-ABI, against the oracle's exact leg on the concatenated data.
+
+A W-way partitioned run is simulated in one process on one GPU: W shards are
+pre-aggregated by plgpu_gb_partial_begin (after the same window agreement
+distributed.agree_windows performs), exported with plgpu_gb_partial_export,
+the records for each destination are concatenated the way all_to_all_single
+lays them out, and each destination merges with plgpu_gb_merge.  The union
+of the W partitions must equal the single-pass result bit for bit (exact
+f64 sums are associative, so sharding cannot change them).  The real
+torch.distributed path is exercised at world_size 1 over RCCL.
+"""
+
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import polaroid_amd as pl
+from polaroid_amd import distributed as D
+from polaroid_amd.frame import _gb_lower
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _bits(a):
+    return np.asarray(a, dtype=np.float64).view(np.uint64)
+
+
+def _frame(rng, n, scale=100.0, nulls=True):
+    a = rng.standard_normal(n) * scale
+    a[rng.random(n) < 0.01] = np.nan
+    a[rng.random(n) < 0.005] = np.inf
+    a[rng.random(n) < 0.01] = -0.0
+    b = rng.integers(-10**12, 10**12, n).astype(np.int64)
+    d = rng.uniform(-5, 5, n)
+    va = (rng.random(n) > 0.05) if nulls else None
+    vd = (rng.random(n) > 0.05) if nulls else None
+    return {"a": (a, va), "b": (b, None), "d": (d, vd)}
+
+
+AGGS = [("sum", "a"), ("mean", "a"), ("min", "a"), ("max", "d"), ("count", "a"), ("len", "a"),
+        ("sum", "b"), ("sum", "d")]
+
+
+def _simulate(shards, world, aggs, pred):
+    """Run the partitioned protocol over `shards` (list of GPU DataFrames)."""
+    import torch
+
+    exprs = [getattr(pl.col(c), k)().alias(f"{k}_{c}") for k, c in aggs]
+    parts = [D.GpuPartial(_gb_lower(df, "k", exprs, pred), world) for df in shards]
+    state = [p.begin(None) for p in parts]          # (used, refit, hint)
+    for _ in range(D.MAX_WINDOW_ROUNDS):
+        agreed = [max(s[2][i] for s in state) for i in range(6)]
+        need = [s[0] != agreed for s in state]
+        if not any(need):
+            break
+        for i, p in enumerate(parts):
+            if need[i]:
+                state[i] = p.begin(agreed)
+    else:
+        raise AssertionError("windows did not converge")
+    rw = parts[0].record_words
+    exported = [p.export() for p in parts]
+    frames = []
+    for dest in range(world):
+        segs = []
+        n = 0
+        for send, counts in exported:
+            off = sum(counts[:dest]) * rw
+            segs.append(send[off: off + counts[dest] * rw])
+            n += counts[dest]
+        recv = torch.cat(segs) if segs else torch.empty(0, dtype=torch.int64, device="cuda")
+        out, _ = parts[dest].merge(recv.contiguous(), n, agreed)
+        frames.append(out)
+    return frames, agreed
+
+
+def _check(frames, cols, key, kvalid, aggs, pred_prog, names):
+    n = key.shape[0]
+    hc = [O.HostCol(cols[c][0], cols[c][1]) for c in names]
+    okeys, okvalid, oouts = O.group_by_agg(O.HostCol(key, kvalid), hc, pred_prog,
+                                           [(k, names.index(c)) for k, c in aggs], n, O.SUM_EXACT)
+    gk = np.concatenate([f["k"].to_numpy().astype(np.int64) for f in frames])
+    gkv = np.concatenate([f["k"].validity_numpy() for f in frames])
+    # each group on exactly one rank
+    assert gk.shape[0] == okeys.shape[0]
+    assert len(set(gk[gkv].tolist())) == int(gkv.sum())
+    assert int((~gkv).sum()) <= 1
+    go, oo = np.lexsort((gk, ~gkv)), np.lexsort((okeys, ~okvalid))
+    assert np.array_equal(gkv[go], okvalid[oo])
+    assert np.array_equal(gk[go][gkv[go]], okeys[oo][okvalid[oo]])
+    for (kind, c), (ov, ovalid) in zip(aggs, oouts):
+        gv = np.concatenate([f[f"{kind}_{c}"].to_numpy() for f in frames])[go]
+        gvalid = np.concatenate([f[f"{kind}_{c}"].validity_numpy() for f in frames])[go]
+        ov, ovalid = ov[oo], ovalid[oo]
+        assert np.array_equal(gvalid, ovalid), (kind, c)
+        if ov.dtype == np.float64:
+            g, o = gv[ovalid], ov[ovalid]
+            assert np.array_equal(np.isnan(g), np.isnan(o)), (kind, c)
+            m = ~np.isnan(o)
+            assert np.array_equal(_bits(g)[m], _bits(o)[m]), (kind, c, g[m][:4], o[m][:4])
+        else:
+            assert np.array_equal(gv[ovalid].astype(np.int64), ov[ovalid].astype(np.int64)), (kind, c)
+
+
+def _run_case(world, nshards, n, card, pred=None, pred_prog=None, pred_names=(), scales=None, nulls=True,
+              specials=True):
+    rng = np.random.default_rng(world * 1000 + n + card)
+    parts = []
+    for s in range(nshards):
+        sc = scales[s] if scales else 100.0
+        parts.append(_frame(rng, n, sc, nulls))
+    cols = {c: (np.concatenate([p[c][0] for p in parts]),
+                None if parts[0][c][1] is None else np.concatenate([p[c][1] for p in parts]))
+            for c in parts[0]}
+    N = n * nshards
+    key = rng.integers(0, card, N).astype(np.int64) * 1_000_003 - 77
+    kvalid = None
+    if specials:
+        key[rng.random(N) < 0.01] = np.iinfo(np.int64).min
+        kvalid = rng.random(N) > 0.01
+    names = list(dict.fromkeys(list(pred_names) + [c for _, c in AGGS]))
+    shards = []
+    for s in range(nshards):
+        sl = slice(s * n, (s + 1) * n)
+        data = {"k": pl.Series.from_numpy("k", key[sl], None if kvalid is None else kvalid[sl])}
+        for c in names:
+            v, m = cols[c]
+            data[c] = pl.Series.from_numpy(c, v[sl], None if m is None else m[sl])
+        shards.append(pl.DataFrame(data))
+    frames, agreed = _simulate(shards, world, AGGS, pred)
+    _check(frames, cols, key, kvalid, AGGS, pred_prog, names)
+    return frames, agreed
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+@pytest.mark.parametrize("card", [1, 100, 20000])
+def test_partitioned_vs_oracle(gpu, world, card):
+    _run_case(world, world, 30000, card)
+
+
+def test_partitioned_with_predicate(gpu):
+    prog = [(1, 0, 0), (2, 0, 0.5), (24, 0, 0)]   # d > 0.5
+    _run_case(4, 4, 50000, 500, pred=pl.col("d") > 0.5, pred_prog=prog, pred_names=["d"])
+
+
+def test_partitioned_window_agreement(gpu):
+    """Shards of very different magnitude sample different windows; the
+    agreed (MAX) window must reproduce the exact sum of all shards."""
+    frames, agreed = _run_case(2, 2, 40000, 50, scales=[1e-3, 1e12], nulls=False, specials=False)
+
+
+def test_partitioned_fast_path_shards(gpu):
+    """Null-free 8-byte shards take the fast kernel in the partial stage."""
+    _run_case(2, 2, 262144, 100, nulls=False, specials=False)
+
+
+def test_partitioned_empty_shard(gpu):
+    _run_case(2, 3, 0, 10)
+
+
+def test_group_by_agg_world1_rccl(gpu):
+    """The torch.distributed path itself (nccl = RCCL), one rank."""
+    import torch
+    import torch.distributed as dist
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        rng = np.random.default_rng(3)
+        n = 100_000
+        cols = _frame(rng, n)
+        key = rng.integers(0, 300, n).astype(np.int64)
+        df = pl.DataFrame({"k": pl.Series.from_numpy("k", key), "a": pl.Series.from_numpy("a", *cols["a"]),
+                           "d": pl.Series.from_numpy("d", *cols["d"])})
+        info = {}
+        out = D.group_by_agg(df, "k", [pl.col("a").sum().alias("sum_a"), pl.col("d").mean().alias("mean_d")],
+                             pl.col("d") > 0.0, info=info)
+        ref = df.lazy().filter(pl.col("d") > 0.0).group_by("k").agg(
+            pl.col("a").sum().alias("sum_a"), pl.col("d").mean().alias("mean_d")).collect()
+        go, ro = np.argsort(out["k"].to_numpy()), np.argsort(ref["k"].to_numpy())
+        assert np.array_equal(out["k"].to_numpy()[go], ref["k"].to_numpy()[ro])
+        for c in ("sum_a", "mean_d"):
+            g, r = out[c].to_numpy()[go], ref[c].to_numpy()[ro]
+            assert np.array_equal(out[c].validity_numpy()[go], ref[c].validity_numpy()[ro])
+            assert np.array_equal(np.isnan(g), np.isnan(r))
+            m = ~np.isnan(r)
+            assert np.array_equal(_bits(g)[m], _bits(r)[m])
+        assert info["groups"] == ref.height
+    finally:
+        dist.destroy_process_group()
