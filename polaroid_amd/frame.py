@@ -273,6 +273,35 @@ class Series:
         raw = self._download(self._col.values + off * eb if self._col.values else 0, n * eb)
         return raw.view(dt.np_dtype).copy()
 
+    # Arrow interchange (polars DataFrames cross the plugin boundary as Arrow)
+    @classmethod
+    def from_arrow(cls, name: str, arr) -> "Series":
+        """Upload a pyarrow Array / ChunkedArray (int64/int32/uint32/float64/bool)."""
+        import pyarrow as pa
+
+        if isinstance(arr, pa.ChunkedArray):
+            arr = arr.combine_chunks() if arr.num_chunks != 1 else arr.chunk(0)
+        m = {pa.int64(): Int64, pa.int32(): Int32, pa.uint32(): UInt32, pa.float64(): Float64,
+             pa.bool_(): Boolean}
+        dt = m.get(arr.type)
+        if dt is None:
+            raise N.InvalidOperationError(f"column {name!r}: arrow type {arr.type} is not supported on the GPU")
+        valid = None
+        if arr.null_count:
+            valid = arr.is_valid().to_numpy(zero_copy_only=False)
+            arr = arr.fill_null(False if dt is Boolean else 0)
+        vals = arr.to_numpy(zero_copy_only=False)
+        return cls.from_numpy(name, vals, valid, dt)
+
+    def to_arrow(self):
+        import pyarrow as pa
+
+        t = {"Int64": pa.int64(), "Int32": pa.int32(), "UInt32": pa.uint32(), "Float64": pa.float64(),
+             "Boolean": pa.bool_()}[self.dtype.name]
+        vals = self.to_numpy()
+        valid = self.validity_numpy()
+        return pa.array(vals, type=t, mask=None if valid.all() else ~valid)
+
     def to_list(self) -> list:
         vals = self.to_numpy().tolist()
         valid = self.validity_numpy()
@@ -353,6 +382,15 @@ class DataFrame:
     def rows(self) -> list[tuple]:
         cols = [s.to_list() for s in self._cols.values()]
         return list(zip(*cols)) if cols else []
+
+    @classmethod
+    def from_arrow(cls, table) -> "DataFrame":
+        return cls([Series.from_arrow(nm, table.column(nm)) for nm in table.column_names])
+
+    def to_arrow(self):
+        import pyarrow as pa
+
+        return pa.table({nm: s.to_arrow() for nm, s in self._cols.items()})
 
     def lazy(self) -> "LazyFrame":
         return LazyFrame(("scan", self))

@@ -1,0 +1,242 @@
+"""Polars GPU-engine plugin: `lf.collect(engine="gpu")` executed on MI355X.
+
+The reference dispatches `collect(engine="gpu")` through a post-optimisation
+callback (py-polars/src/polars/lazyframe/frame.py:208 `_gpu_engine_callback`,
+which hands `cudf_polars.execute_with_cudf` to Rust; the callback receives a
+`NodeTraverser` over the optimised IR, crates/polars-python/src/lazyframe/
+general.rs:47 `post_opt_callback`).  The callback may replace the root
+subtree with a Python UDF via `NodeTraverser.set_udf`
+(crates/polars-python/src/lazyframe/visit.rs:158), which polars turns into a
+`PythonScan` node that the in-memory engine calls as
+`fn(with_columns, predicate, n_rows, should_time)`
+(crates/polars-mem-engine/src/executors/scan/python_scan.rs:91).
+
+`execute_with_polaroid` has the same signature and contract as
+`execute_with_cudf`: it translates the IR (node classes of
+crates/polars-python/src/lazyframe/visitor/nodes.rs, expression classes of
+.../visitor/expr_nodes.rs) for the hot path — DataFrameScan, Filter,
+Select/HStack of arithmetic + comparisons, GroupBy on one integer key with
+sum/mean/min/max/count/len — into a polaroid_amd plan and installs a UDF that
+runs it through libpolaroid_gpu.so.  A query outside that path is left to
+polars' own engine unless `raise_on_fail` is set (the reference GPU engine's
+behaviour).  Once accepted, nothing falls back: a missing HIP library or a
+device error raises.
+"""
+
+from __future__ import annotations
+
+from typing import Any, Callable
+
+from . import _native as N
+from .expr import Expr, col, lit
+from .frame import DataFrame, LazyFrame
+
+__all__ = ["execute_with_polaroid", "Unsupported", "translate"]
+
+
+class Unsupported(Exception):
+    """The IR is outside the GPU hot path."""
+
+
+def _name(obj) -> str:
+    return type(obj).__name__
+
+
+def _enum_name(v) -> str:
+    s = str(v)
+    return s.rsplit(".", 1)[-1]
+
+
+_BINOPS: dict[str, Callable[[Expr, Expr], Expr]] = {
+    "Eq": lambda a, b: a == b, "NotEq": lambda a, b: a != b, "Lt": lambda a, b: a < b,
+    "LtEq": lambda a, b: a <= b, "Gt": lambda a, b: a > b, "GtEq": lambda a, b: a >= b,
+    "EqValidity": lambda a, b: a.eq_missing(b), "NotEqValidity": lambda a, b: a.ne_missing(b),
+    "Plus": lambda a, b: a + b, "Minus": lambda a, b: a - b, "Multiply": lambda a, b: a * b,
+    "TrueDivide": lambda a, b: a / b, "And": lambda a, b: a & b, "Or": lambda a, b: a | b,
+    "LogicalAnd": lambda a, b: a & b, "LogicalOr": lambda a, b: a | b,
+}
+
+_BOOLFUNCS: dict[str, Callable[[Expr], Expr]] = {
+    "IsNull": lambda a: a.is_null(), "IsNotNull": lambda a: a.is_not_null(), "IsNan": lambda a: a.is_nan(),
+    "IsFinite": lambda a: a.is_finite(), "Not": lambda a: ~a,
+}
+
+
+class _Translator:
+    def __init__(self, nt):
+        self.nt = nt
+
+    # ---------------------------------------------------------- expressions
+    def expr(self, node: int) -> Expr:
+        e = self.nt.view_expression(node)
+        k = _name(e)
+        if k == "Column":
+            return col(str(e.name))
+        if k == "Literal":
+            v = e.value
+            if v is None or isinstance(v, (bool, int, float)):
+                return lit(v)
+            raise Unsupported(f"literal {v!r}")
+        if k == "BinaryExpr":
+            op = _enum_name(e.op)
+            if op not in _BINOPS:
+                raise Unsupported(f"operator {op}")
+            return _BINOPS[op](self.expr(e.left), self.expr(e.right))
+        if k == "Cast":
+            dt = str(e.dtype)
+            if dt.startswith("Float64"):
+                return self.expr(e.expr).cast("f64")
+            raise Unsupported(f"cast to {dt}")
+        if k == "Function":
+            fd = e.function_data
+            fname = _enum_name(fd[0]) if isinstance(fd, tuple) and fd else _enum_name(fd)
+            if fname == "Abs":
+                return abs(self.expr(e.input[0]))
+            if fname == "Negate":
+                return -self.expr(e.input[0])
+            if fname in _BOOLFUNCS and len(e.input) == 1:
+                return _BOOLFUNCS[fname](self.expr(e.input[0]))
+            raise Unsupported(f"function {fname}")
+        raise Unsupported(f"expression {k}")
+
+    def agg(self, node: int, key: str) -> Expr:
+        e = self.nt.view_expression(node)
+        k = _name(e)
+        if k == "Len":
+            return col(key).len()
+        if k != "Agg":
+            raise Unsupported(f"aggregation expression {k}")
+        name = str(e.name)
+        if len(e.arguments) != 1:
+            raise Unsupported("multi-argument aggregation")
+        arg = self.nt.view_expression(e.arguments[0])
+        if _name(arg) != "Column":
+            raise Unsupported("aggregation over a computed expression")
+        c = col(str(arg.name))
+        if name in ("sum", "mean"):
+            return getattr(c, name)()
+        if name in ("min", "max"):
+            if e.options:  # propagate_nans=True (nan_min / nan_max)
+                raise Unsupported(f"{name} with NaN propagation")
+            return getattr(c, name)()
+        if name == "count":
+            return c.len() if e.options else c.count()
+        raise Unsupported(f"aggregation {name}")
+
+    # ---------------------------------------------------------------- plans
+    def plan(self) -> tuple:
+        """Translate the subtree at the traverser's current node."""
+        node = self.nt.view_current_node()
+        k = _name(node)
+        if k == "DataFrameScan":
+            if getattr(node, "selection", None) is not None:
+                raise Unsupported("scan predicate")
+            proj = node.projection
+            return ("polars_scan", node.df, None if proj is None else list(proj))
+        if k in ("Filter", "Select", "HStack", "GroupBy", "SimpleProjection"):
+            child = self.child(node.input)
+            if k == "Filter":
+                return ("filter", child, self.expr(node.predicate.node))
+            if k == "SimpleProjection":
+                names = list(self.nt.get_schema().keys())
+                return ("select", child, [col(n) for n in names])
+            if k in ("Select", "HStack"):
+                exprs = node.expr if k == "Select" else node.exprs
+                out = []
+                for ei in exprs:
+                    x = self.expr(ei.node)
+                    out.append(x if x.output_name() == ei.output_name else x.alias(ei.output_name))
+                return ("select" if k == "Select" else "with_columns", child, out)
+            # GroupBy
+            opts = node.options
+            if getattr(opts, "dynamic", None) is not None or getattr(opts, "rolling", None) is not None:
+                raise Unsupported("dynamic / rolling group-by")
+            if getattr(opts, "slice", None) is not None:
+                raise Unsupported("group-by slice")
+            if len(node.keys) != 1:
+                raise Unsupported("multi-key group-by")
+            kx = self.nt.view_expression(node.keys[0].node)
+            if _name(kx) != "Column" or str(kx.name) != node.keys[0].output_name:
+                raise Unsupported("group-by key must be a plain column")
+            key = str(kx.name)
+            aggs = []
+            for ai in node.aggs:
+                a = self.agg(ai.node, key)
+                aggs.append(a.alias(ai.output_name))
+            return ("group_by", child, key, aggs, bool(node.maintain_order))
+        raise Unsupported(f"plan node {k}")
+
+    def child(self, input_node: int) -> tuple:
+        here = self.nt.get_node()
+        self.nt.set_node(input_node)
+        try:
+            return self.plan()
+        finally:
+            self.nt.set_node(here)
+
+
+def translate(nt) -> tuple:
+    """IR at `nt`'s current node -> polaroid_amd plan tuple (raises Unsupported)."""
+    return _Translator(nt).plan()
+
+
+def _bind_scans(node: tuple) -> tuple:
+    """Upload the polars DataFrames of the scans (Arrow -> HBM)."""
+    if node[0] == "polars_scan":
+        table = node[1].to_arrow()
+        if node[2] is not None:
+            table = table.select(node[2])
+        return ("scan", DataFrame.from_arrow(table))
+    return (node[0], _bind_scans(node[1])) + tuple(node[2:])
+
+
+def _to_polars(table):
+    import polars  # the caller is polars itself, so it is importable there
+
+    return polars.from_arrow(table)
+
+
+def run_plan(plan: tuple, n_rows: int | None = None, to_frame=None):
+    """Execute a translated plan on the GPU; returns a polars DataFrame (or
+    whatever `to_frame` makes of the result's Arrow table)."""
+    N.lib()  # fail loudly when the HIP library is missing
+    lf = LazyFrame(_bind_scans(plan))
+    out = lf.collect()
+    table = out.to_arrow()
+    if n_rows is not None:
+        table = table.slice(0, n_rows)
+    return (to_frame or _to_polars)(table)
+
+
+def _config_flag(config: Any, name: str, default: bool = False) -> bool:
+    """Read a flag from a polars GPUEngine (attribute) or a plain dict."""
+    if config is None:
+        return default
+    if isinstance(config, dict):
+        return bool(config.get(name, default))
+    return bool(getattr(config, name, default))
+
+
+def execute_with_polaroid(nt, duration_since_start: int | None = None, *, config: Any = None,
+                          to_frame=None) -> None:
+    """Post-optimisation callback with `cudf_polars.execute_with_cudf`'s
+    signature.  Installs a GPU UDF at the root when the query is on the hot
+    path; otherwise leaves the plan untouched (or raises with
+    `raise_on_fail`)."""
+    try:
+        plan = translate(nt)
+    except Unsupported as exc:
+        if _config_flag(config, "raise_on_fail"):
+            raise N.InvalidOperationError(f"query is not supported by the MI355X engine: {exc}") from exc
+        return
+    N.lib()  # a GPU plan was accepted: the HIP library must be present
+
+    def _udf(with_columns, predicate, n_rows, should_time=False):
+        df = run_plan(plan, n_rows, to_frame)
+        if with_columns is not None:
+            df = df.select(with_columns)
+        if should_time:
+            return df, []
+        return df
+
+    nt.set_udf(_udf)
