@@ -151,7 +151,7 @@ typedef struct plgpu_groupby_info {
     int64_t table_capacity;      /* global hash-table slots                    */
     double main_kernel_ms;       /* device time of the aggregation kernel(s)   */
     int32_t path;                /* 0 generic, 1 fast, 2 fast sum-only kernel  */
-    int32_t _reserved;
+    int32_t sum_limbs;           /* 40-bit LDS limbs per f64 sum (2 or 3)      */
 } plgpu_groupby_info;
 
 /* ---------------------------------------------------------------- basics */

@@ -75,7 +75,7 @@ class GroupByInfo(C.Structure):
         ("table_capacity", C.c_int64),
         ("main_kernel_ms", C.c_double),
         ("path", C.c_int32),
-        ("_reserved", C.c_int32),
+        ("sum_limbs", C.c_int32),
     ]
 
     def as_dict(self) -> dict:

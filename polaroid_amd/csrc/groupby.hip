@@ -30,6 +30,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <numeric>
+#include <tuple>
 #include <vector>
 
 #include "plgpu_internal.hpp"
@@ -42,6 +43,8 @@ constexpr int kMaxFields = 48;
 constexpr int kLdsProbe = 16;
 constexpr int kGlobalProbe = 4096;
 constexpr int kSumWindowBits = 120;   // fixed-point window of one value
+constexpr int kLimb2Margin = 4;
+constexpr int kGridRounds = 8;        // fast kernel grid = rounds x resident workgroups       // binades below the smallest sampled exponent kept by 2 limbs
 constexpr int kHeadroomBinades = 8;   // above the sampled max exponent
 constexpr int64_t kMaxRowsPerWg = int64_t(1) << 22;  // keeps 40-bit limbs exact in int64
 constexpr int kPlanSamples = 65536;
@@ -65,6 +68,7 @@ enum : int {
     ST_SAMPLED = 7,      // plan: keys sampled
     ST_MAXEX = 8,        // + acc
     ST_FXFLAGS = 16,     // + acc: bit0 overflow, bit1 inexact
+    ST_MINEX = 17,       // + acc: plan: smallest sampled exponent of a nonzero value
     ST_WORDS = 24
 };
 
@@ -156,6 +160,7 @@ __device__ __forceinline__ int64_t g_find(const GbParams& p, uint64_t key) {
 // f64 bits -> three carry-free 40-bit limbs of the fixed-point value
 // x / 2^bottom (rounded half-even below the window).  Returns false for
 // zero / rounded-away values; sets FX overflow (1) / inexact (2) in fl.
+template <int WBITS = kSumWindowBits>
 __device__ __forceinline__ bool fx_limbs(uint64_t b, int bottom, uint64_t& l0, uint64_t& l1, uint64_t& l2,
                                          uint32_t& fl, uint32_t& ex_out) {
     uint32_t ex = (uint32_t)(b >> 52) & 0x7FF;
@@ -170,7 +175,7 @@ __device__ __forceinline__ bool fx_limbs(uint64_t b, int bottom, uint64_t& l0, u
     const int sh = (int)ex - 1075 - bottom;
     unsigned __int128 F;
     if (sh >= 0) {
-        if (sh > kSumWindowBits - 53) {
+        if (sh > WBITS - 53) {
             fl |= 1u;
             return false;
         }
@@ -191,14 +196,54 @@ __device__ __forceinline__ bool fx_limbs(uint64_t b, int bottom, uint64_t& l0, u
     }
     constexpr uint64_t M40 = (1ull << 40) - 1;
     l0 = (uint64_t)F & M40;
-    l1 = (uint64_t)(F >> 40) & M40;
-    l2 = (uint64_t)(F >> 80);
+    if (WBITS > 80) {
+        l1 = (uint64_t)(F >> 40) & M40;
+        l2 = (uint64_t)(F >> 80);
+    } else {
+        l1 = (uint64_t)(F >> 40);
+        l2 = 0;
+    }
     if (b >> 63) {
         l0 = 0ull - l0;
         l1 = 0ull - l1;
         l2 = 0ull - l2;
     }
     return true;
+}
+
+// Branch-free conversion for the common case: a finite value whose bits all
+// fall inside the window (no rounding, no overflow), or zero.  LIMBS 3: the
+// 120-bit window at `bottom`; LIMBS 2: its top 80 bits (bottom + 40), limbs
+// returned in l0, l1 (l2 = 0).  Returns false (limbs 0) when the value needs
+// fx_limbs (inf / NaN, bits below the window, overflow).
+template <int LIMBS>
+__device__ __forceinline__ bool fx_limbs_fast(uint64_t x, int bottom, uint64_t& l0, uint64_t& l1, uint64_t& l2) {
+    // The signed value t = +-m * 2^sh (sh >= 0, t < 2^W) is split as
+    // t = l0 + l1 * 2^40 (+ l2 * 2^80) with l0 (and l1 in the 3-limb case)
+    // taken as the low 40 bits (>= 0) and the top limb as the arithmetic
+    // shift (signed): carry-free, exact, and no per-limb negation.
+    // Subnormals take the slow path (ex == 0 is only accepted for zero);
+    // inf / NaN exceed the window for every reachable bottom.
+    constexpr uint64_t M40 = (1ull << 40) - 1;
+    constexpr int W = LIMBS == 3 ? kSumWindowBits : kSumWindowBits - 40;
+    const uint32_t hi = (uint32_t)(x >> 32);
+    const uint32_t ex = (hi >> 20) & 0x7FF;
+    const int sh = (int)ex - 1075 - (LIMBS == 3 ? bottom : bottom + 40);
+    const bool inrange = (uint32_t)sh <= (uint32_t)(W - 53) && ex != 0;
+    const bool zero = (x & 0x7fffffffffffffffull) == 0;
+    const uint64_t m = inrange ? ((x & 0x000FFFFFFFFFFFFFull) | (1ull << 52)) : 0ull;
+    const int64_t sm = (int64_t)x < 0 ? -(int64_t)m : (int64_t)m;
+    const uint32_t s = inrange ? (uint32_t)sh : 0u;
+    if (LIMBS == 3) {
+        l0 = s < 40 ? ((uint64_t)sm << s) & M40 : 0ull;
+        l1 = (s <= 40 ? (uint64_t)(sm >> (40 - s)) : ((uint64_t)sm << (s - 40))) & M40;
+        l2 = (uint64_t)(sm >> (s > 16 ? 80 - s : 63));
+    } else {
+        l0 = ((uint64_t)sm << s) & M40;
+        l1 = (uint64_t)(sm >> (40 - s));  // s <= 27
+        l2 = 0;
+    }
+    return inrange || zero;
 }
 
 // Signed limb sums -> 192-bit two's complement words.
@@ -619,12 +664,37 @@ __device__ __forceinline__ void fast_load(const GbParams& p, int64_t t, FastTile
 // min / max), no maintain_order: the field layout is compile-time
 // (key 0, len 1, acc a: limbs 2+4a..4+4a, flags 5+4a) and the per-acc code
 // is unrolled with no descriptor decode.
-template <int NACC, int PRED, bool SUMONLY, int ROWS>
-__global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProgram prog) {
+// LIMBS (SUMONLY only): 3 = the full 120-bit window; 2 = its top 80 bits
+// (bottom + 40), chosen by the plan when the sampled exponents span few
+// binades.  A value with bits below the 2-limb window sets the inexact flag
+// and the host reruns with 3 limbs, so results never depend on the choice.
+// The two limbs land in fields (3+4a, 4+4a): the 3-limb representation with
+// a zero low limb, so the flush and finalize are unchanged.
+// ABL (timing ablations, never dispatched in production): 1 no atomics,
+// 2 len atomic only, 3 limb conversion without limb atomics.
+// WPE: minimum waves per SIMD the register allocation must allow (1 = no
+// constraint); 6 caps VGPRs at 80, i.e. three 512-thread workgroups per CU.
+template <int NACC, int PRED, bool SUMONLY, int ROWS, int LIMBS = 3, int ABL = 0, int WPE = 1>
+__global__ __launch_bounds__(kGbThreads) __attribute__((amdgpu_waves_per_eu(WPE))) void gb_fast_kernel(
+    GbParams p, DevProgram prog) {
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
     constexpr int NA = NACC > 0 ? NACC : 1;
+    // SLIM (sum-only, 2 limbs): LDS fields key 0, len 1, acc a: limbs
+    // 2+3a, 3+3a, flags 4+3a (the unused low limb of the 3-limb layout is
+    // not stored, so more workgroups fit per CU)
+    constexpr bool SLIM = SUMONLY && LIMBS == 2;
+    auto so_mid = [](int a) { return SLIM ? 2 + 3 * a : 3 + 4 * a; };
+    auto so_top = [](int a) { return SLIM ? 3 + 3 * a : 4 + 4 * a; };
+    auto so_flags = [](int a) { return SLIM ? 4 + 3 * a : 5 + 4 * a; };
     const int L = p.lcap + 2;
-    init_lds(p, lds, L);
+    if (SLIM) {
+        for (int f = 0; f < 2 + 3 * NACC; ++f) {
+            const uint64_t v = f == 0 ? kEmptyKey : 0ull;
+            for (int i = threadIdx.x; i < L; i += blockDim.x) lds[f * L + i] = v;
+        }
+    } else {
+        init_lds(p, lds, L);
+    }
     ThreadDiag d = {0u, 0u, 0u, 0u};
     uint64_t dd0[NA];
     int bot0[NA];
@@ -681,24 +751,52 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
                 if (s == kGlobalKey) s = lds_find(lds, p.lbits, p.lcap, cur.key[0]);
                 if (SUMONLY && s >= 0) {
                     unsigned long long* q = (unsigned long long*)&lds[s];
-                    atomicAdd(q + L, 1ull);
+                    if (ABL == 1) {
+#pragma unroll
+                        for (int a = 0; a < NACC; ++a) d.special ^= (uint32_t)rv[a] & 0x80000000u;
+                    } else {
+                        atomicAdd(q + L, 1ull);
+                    }
+                    uint32_t slow = 0;
 #pragma unroll
                     for (int a = 0; a < NACC; ++a) {
-                        const uint64_t x = rv[a];
-                        const uint64_t ab = x & 0x7fffffffffffffffull;
-                        if (ab >= 0x7ff0000000000000ull) {
-                            atomicOr(q + (5 + 4 * a) * L,
-                                     (unsigned long long)(ab > 0x7ff0000000000000ull ? FL_NAN
-                                                          : ((x >> 63) ? FL_NINF : FL_PINF)));
+                        if (ABL == 1 || ABL == 2) break;
+                        uint64_t l0, l1, l2;
+                        const bool ok = fx_limbs_fast<LIMBS>(rv[a], bot[a], l0, l1, l2);
+                        slow |= (ok ? 0u : 1u) << a;
+                        if (ABL == 3) {
+                            d.special ^= (uint32_t)(l0 ^ l1 ^ l2) & 0x80000000u;
                         } else {
-                            uint64_t l0, l1, l2;
-                            uint32_t ex = 0, fl = 0;
-                            const bool ok = fx_limbs(x, bot[a], l0, l1, l2, fl, ex);
-                            d.fxbits |= fl << (2 * a);
-                            if (ok) {
-                                atomicAdd(q + (2 + 4 * a) * L, (unsigned long long)l0);
-                                atomicAdd(q + (3 + 4 * a) * L, (unsigned long long)l1);
-                                atomicAdd(q + (4 + 4 * a) * L, (unsigned long long)l2);
+                            // zero limbs (slow lanes, zero values) add nothing
+                            if (LIMBS == 3) atomicAdd(q + (2 + 4 * a) * L, (unsigned long long)l0);
+                            atomicAdd(q + so_mid(a) * L, (unsigned long long)(LIMBS == 3 ? l1 : l0));
+                            atomicAdd(q + so_top(a) * L, (unsigned long long)(LIMBS == 3 ? l2 : l1));
+                        }
+                    }
+                    if (slow) {
+                        // inf / NaN flags, rounding below the window, overflow
+#pragma unroll
+                        for (int a = 0; a < NACC; ++a) {
+                            if (!((slow >> a) & 1u)) continue;
+                            const uint64_t x = rv[a];
+                            const uint64_t ab = x & 0x7fffffffffffffffull;
+                            if (ab >= 0x7ff0000000000000ull) {
+                                atomicOr(q + so_flags(a) * L,
+                                         (unsigned long long)(ab > 0x7ff0000000000000ull ? FL_NAN
+                                                              : ((x >> 63) ? FL_NINF : FL_PINF)));
+                            } else {
+                                uint64_t l0, l1, l2;
+                                uint32_t ex = 0, fl = 0;
+                                const bool ok = LIMBS == 3
+                                                    ? fx_limbs<kSumWindowBits>(x, bot[a], l0, l1, l2, fl, ex)
+                                                    : fx_limbs<kSumWindowBits - 40>(x, bot[a] + 40, l0, l1, l2, fl,
+                                                                                    ex);
+                                d.fxbits |= fl << (2 * a);
+                                if (ok) {
+                                    if (LIMBS == 3) atomicAdd(q + (2 + 4 * a) * L, (unsigned long long)l0);
+                                    atomicAdd(q + so_mid(a) * L, (unsigned long long)(LIMBS == 3 ? l1 : l0));
+                                    atomicAdd(q + so_top(a) * L, (unsigned long long)(LIMBS == 3 ? l2 : l1));
+                                }
                             }
                         }
                     }
@@ -719,7 +817,40 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
         }
         cur = nxt;
     }
-    flush_and_report<true>(p, lds, L, d);
+    if (SLIM) {
+        __syncthreads();
+        for (int sl = threadIdx.x; sl < L; sl += blockDim.x) {
+            const uint64_t len = lds[L + sl];
+            if (len == 0) continue;
+            int64_t gs;
+            if (sl == p.lcap) {
+                gs = p.gcap;
+                d.special |= 1u;
+            } else if (sl == p.lcap + 1) {
+                gs = p.gcap + 1;
+                d.special |= 2u;
+            } else {
+                gs = g_find(p, lds[sl]);
+                if (gs < 0) {
+                    atomicAdd((unsigned long long*)&p.status[ST_TABLE_FULL], 1ull);
+                    continue;
+                }
+            }
+            atomicAdd((unsigned long long*)gfield(p, p.f_len, gs), (unsigned long long)len);
+#pragma unroll
+            for (int a = 0; a < NACC; ++a) {
+                const int f = p.acc[a].f_sum;
+                uint64_t w0, w1, w2;
+                limbs_to_192(0, (int64_t)lds[so_mid(a) * L + sl], (int64_t)lds[so_top(a) * L + sl], w0, w1, w2);
+                g_add192(gfield(p, f, gs), gfield(p, f + 1, gs), gfield(p, f + 2, gs), w0, w1, w2);
+                const uint64_t fl = lds[so_flags(a) * L + sl];
+                if (fl) atomicOr((unsigned long long*)gfield(p, p.acc[a].f_flags, gs), (unsigned long long)fl);
+            }
+        }
+        flush_and_report<false>(p, lds, L, d);
+    } else {
+        flush_and_report<true>(p, lds, L, d);
+    }
 }
 
 // Exact max exponent of a summed column (rerun path only: refits the
@@ -747,6 +878,7 @@ __global__ __launch_bounds__(256) void gb_maxexp_kernel(GbParams p, int a) {
 // sample with an LDS hash set (-> table sizes).
 __global__ __launch_bounds__(256) void gb_plan_kernel(GbParams p, int32_t* bottoms, int64_t samples) {
     __shared__ uint32_t red[256];
+    __shared__ uint32_t red2[256];
     __shared__ uint64_t set[kPlanSetSlots];
     __shared__ uint32_t distinct;
     const int a = blockIdx.x;
@@ -785,7 +917,7 @@ __global__ __launch_bounds__(256) void gb_plan_kernel(GbParams p, int32_t* botto
         return;
     }
     const AccSpec& ac = p.acc[a];
-    uint32_t mx = 0;
+    uint32_t mx = 0, mn = 0x7FF;
     if (ac.flags & (A_FSUM | A_FSUMCAST)) {
         const DevCol& c = ac.c;
         for (int64_t i = threadIdx.x; i < samples && i * step < n; i += blockDim.x) {
@@ -795,15 +927,22 @@ __global__ __launch_bounds__(256) void gb_plan_kernel(GbParams p, int32_t* botto
             if (ac.flags & A_FSUMCAST) x = f64_bits((double)(int64_t)x);
             const uint32_t ex = (uint32_t)(x >> 52) & 0x7FF;
             if (ex != 0x7FF && ex > mx) mx = ex;
+            // smallest exponent of a nonzero finite value (subnormals: 0)
+            if ((x & 0x7fffffffffffffffull) != 0 && ex != 0x7FF && ex < mn) mn = ex;
         }
     }
     red[threadIdx.x] = mx;
+    red2[threadIdx.x] = mn;
     __syncthreads();
     for (int off = 128; off >= 1; off >>= 1) {
-        if (threadIdx.x < off) red[threadIdx.x] = max(red[threadIdx.x], red[threadIdx.x + off]);
+        if (threadIdx.x < off) {
+            red[threadIdx.x] = max(red[threadIdx.x], red[threadIdx.x + off]);
+            red2[threadIdx.x] = min(red2[threadIdx.x], red2[threadIdx.x + off]);
+        }
         __syncthreads();
     }
     if (threadIdx.x == 0) {
+        p.status[ST_MINEX + a] = red2[0];
         int e = red[0] == 0 ? 2046 : (int)red[0] + kHeadroomBinades;
         if (e > 2046) e = 2046;
         // a value fits iff ex <= bottom + 1075 + (window - 53)
@@ -1092,9 +1231,12 @@ struct Plan {
     int grid;
     bool use_lds;
     bool sum_only;
+    int limbs;         // SUMONLY: 40-bit LDS limbs per f64 sum (3, or 2 for narrow exponent spans)
+    int ablate;        // timing ablation variant (PLGPU_ABLATE; never set in production)
     int fast_rows;     // rows per thread per tile in the fast kernel (2 / 4)
     int fast_threads;  // workgroup size of the fast kernel
     int fast_grid;
+    mutable int launched_grid;  // grid of the last fast launch (info)
 };
 
 static int plan_groupby(const plgpu_column* key, const plgpu_column* cols, int32_t ncols, const plgpu_agg* aggs,
@@ -1264,28 +1406,68 @@ static hipError_t launch_main(const Plan& pl, const DevProgram& dp, hipStream_t 
     return hipGetLastError();
 }
 
-template <int NACC, int PRED, bool SUMONLY, int ROWS>
+// Workgroups of `kern` resident per CU at this LDS size (cached).
+static int resident_per_cu(const void* kern, int threads, size_t lds) {
+    static std::vector<std::tuple<const void*, int, size_t, int>> cache;
+    for (auto& c : cache)
+        if (std::get<0>(c) == kern && std::get<1>(c) == threads && std::get<2>(c) == lds) return std::get<3>(c);
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, threads, lds) != hipSuccess || nb < 1) nb = 1;
+    cache.emplace_back(kern, threads, lds, nb);
+    return nb;
+}
+
+template <int NACC, int PRED, bool SUMONLY, int ROWS, int LIMBS = 3, int ABL = 0, int WPE = 1>
 static hipError_t launch_fast_rows(const Plan& pl, const DevProgram& dp, hipStream_t s) {
+    const void* kern = (const void*)gb_fast_kernel<NACC, PRED, SUMONLY, ROWS, LIMBS, ABL, WPE>;
     static bool attr_set = false;
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)gb_fast_kernel<NACC, PRED, SUMONLY, ROWS>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_set = true;
     }
-    gb_fast_kernel<NACC, PRED, SUMONLY, ROWS><<<pl.fast_grid, pl.fast_threads, pl.lds_bytes, s>>>(pl.p, dp);
+    const size_t lds = (SUMONLY && LIMBS == 2) ? (size_t)(2 + 3 * NACC) * (pl.p.lcap + 2) * 8 : pl.lds_bytes;
+    // kGridRounds rounds of the workgroups resident per CU: later rounds'
+    // table init / flush overlap earlier rounds' streaming (PLGPU_OCC_GRID=k
+    // overrides the round count for tuning)
+    const char* e = getenv("PLGPU_OCC_GRID");
+    const int rounds = e ? std::max(1, atoi(e)) : kGridRounds;
+    const int64_t need = (pl.p.n_full + kMaxRowsPerWg - 1) / kMaxRowsPerWg;
+    int64_t g = (int64_t)num_cus() * resident_per_cu(kern, pl.fast_threads, lds) * rounds;
+    if (g < need) g = need;
+    const int64_t useful = pl.p.n_full / ((int64_t)pl.fast_threads * ROWS);
+    if (g > useful) g = std::max<int64_t>(1, useful);
+    const int grid = (int)g;
+    pl.launched_grid = grid;
+    gb_fast_kernel<NACC, PRED, SUMONLY, ROWS, LIMBS, ABL, WPE><<<grid, pl.fast_threads, lds, s>>>(pl.p, dp);
     return hipGetLastError();
 }
 
 template <int NACC, int PRED, bool SUMONLY>
 static hipError_t launch_fast(const Plan& pl, const DevProgram& dp, hipStream_t s) {
-    return pl.fast_rows == 2 ? launch_fast_rows<NACC, PRED, SUMONLY, 2>(pl, dp, s)
-                             : launch_fast_rows<NACC, PRED, SUMONLY, 4>(pl, dp, s);
+    if (SUMONLY && pl.limbs == 2) return launch_fast_rows<NACC, PRED, SUMONLY, 2, 2>(pl, dp, s);
+    return launch_fast_rows<NACC, PRED, SUMONLY, 2>(pl, dp, s);
+}
+
+// Ablations of the headline configuration only (tools/ablate.py).
+static hipError_t launch_ablation(const Plan& pl, const DevProgram& dp, hipStream_t s) {
+    switch (pl.ablate) {
+    case 1: return launch_fast_rows<4, 1, true, 2, 3, 1>(pl, dp, s);
+    case 2: return launch_fast_rows<4, 1, true, 2, 3, 2>(pl, dp, s);
+    case 3: return launch_fast_rows<4, 1, true, 2, 3, 3>(pl, dp, s);
+    case 4: return launch_fast_rows<4, 1, true, 2, 2, 3>(pl, dp, s);
+    case 5: return launch_fast_rows<4, 1, true, 2, 3, 0, 6>(pl, dp, s);
+    case 6: return launch_fast_rows<4, 1, true, 2, 2, 0, 6>(pl, dp, s);
+    case 7: return launch_fast_rows<4, 1, true, 2, 2, 0>(pl, dp, s);
+    default: return launch_fast_rows<4, 1, true, 2, 3, 0>(pl, dp, s);
+    }
 }
 
 template <int NACC>
 static hipError_t launch_fast_nacc(const Plan& pl, const DevProgram& dp, int pred, hipStream_t s) {
-    if (pl.sum_only)
+    if (pl.sum_only) {
+        if (NACC == 4 && pred == 1 && pl.ablate > 0) return launch_ablation(pl, dp, s);
         return pred == 0 ? launch_fast<NACC, 0, true>(pl, dp, s) : launch_fast<NACC, 1, true>(pl, dp, s);
+    }
     return pred == 0 ? launch_fast<NACC, 0, false>(pl, dp, s) : launch_fast<NACC, 1, false>(pl, dp, s);
 }
 
@@ -1396,9 +1578,8 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
     for (int a = 0; a < p.nacc; ++a) fast = fast && ok(p.acc[a].c);
     if (R.pred == 1 && p.pred_acc < 0) fast = fast && ok(p.pred_col);
     if (getenv("PLGPU_NO_FAST")) fast = false;
-    p.ablate = getenv("PLGPU_ABLATE") ? atoi(getenv("PLGPU_ABLATE")) : 0;
-    pl.fast_rows = getenv("PLGPU_FAST_ROWS") ? atoi(getenv("PLGPU_FAST_ROWS")) : 2;
-    if (pl.fast_rows != 2 && pl.fast_rows != 4) pl.fast_rows = 2;
+    pl.ablate = getenv("PLGPU_ABLATE") ? atoi(getenv("PLGPU_ABLATE")) : 0;
+    pl.fast_rows = 2;
     pl.fast_threads = getenv("PLGPU_FAST_THREADS") ? atoi(getenv("PLGPU_FAST_THREADS")) : 512;
     if (pl.fast_threads != 256 && pl.fast_threads != 512) pl.fast_threads = 512;
     const int64_t tile = (int64_t)pl.fast_rows * pl.fast_threads;
@@ -1422,6 +1603,17 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
              ac.f_cnt < 0;
     }
     pl.sum_only = so && !getenv("PLGPU_NO_SUMONLY");
+    // two LDS limbs when every sampled nonzero value of every summed column
+    // sits at least kLimb2Margin binades above the 2-limb window's bottom
+    pl.limbs = 3;
+    if (pl.sum_only && !getenv("PLGPU_NO_LIMB2")) {
+        bool two = true;
+        for (int a = 0; a < p.nacc; ++a) {
+            const int mn = (int)R.st[ST_MINEX + a];
+            if (mn != 0x7FF && mn < R.hb[a] + 40 + 1075 + kLimb2Margin) two = false;
+        }
+        if (two) pl.limbs = 2;
+    }
     p.row_begin = p.n_full;
     return PLGPU_OK;
 }
@@ -1521,6 +1713,16 @@ static int gb_main(GbRun& R, bool auto_refit, bool* refit, int32_t* hint) {
         uint32_t flagged = 0;
         for (int a = 0; a < p.nacc; ++a)
             if ((p.acc[a].flags & (A_FSUM | A_FSUMCAST)) && ((R.st[ST_FXFLAGS] >> (2 * a)) & 3u)) flagged |= 1u << a;
+        if (flagged && pl.limbs == 2 && p.n_full > 0 && pl.sum_only) {
+            // a value fell below the 2-limb window (or out of the top): redo
+            // the pass with the full 3-limb window before any refit
+            pl.limbs = 3;
+            again = true;
+            uint32_t over = 0;
+            for (int a = 0; a < p.nacc; ++a)
+                if ((R.st[ST_FXFLAGS] >> (2 * a)) & 1u) over |= 1u << a;
+            flagged = over;
+        }
         if (flagged) {
             int32_t h[kMaxAcc];
             bool changed = false;
@@ -1561,10 +1763,11 @@ static void gb_fill_info(const GbRun& R, plgpu_groupby_info* info) {
     info->global_path_rows = (int64_t)R.st[ST_GLOBAL_ROWS];
     info->reruns = R.attempts;
     info->lds_slots = R.pl.use_lds ? p.lcap : 0;
-    info->grid = p.n_full > 0 ? R.pl.fast_grid : R.pl.grid;
+    info->grid = p.n_full > 0 ? R.pl.launched_grid : R.pl.grid;
     info->table_capacity = p.gcap;
     info->main_kernel_ms = R.ms;
     info->path = p.n_full > 0 ? (R.pl.sum_only ? 2 : 1) : 0;
+    info->sum_limbs = p.n_full > 0 && R.pl.sum_only ? R.pl.limbs : 3;
     for (int a = 0; a < p.nacc; ++a)
         if ((R.st[ST_FXFLAGS] >> (2 * a)) & 2u) info->sum_inexact |= 1 << a;
 }
