@@ -200,7 +200,8 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
-            "kernel": "gb_fast_kernel<4,1,true,2> (fused filter + LDS hash aggregation, exact f64 sums)",
+            "kernel": f"gb_fast_kernel<NACC=4,PRED=1,SUMONLY,ROWS=2,LIMBS={info.get('sum_limbs', 3)}> "
+                      f"(fused filter + LDS hash aggregation, exact f64 sums), grid {info.get('grid')}",
             "kernel_ms": round(kms, 4),
             "bytes_per_row": BYTES_PER_ROW,
         },

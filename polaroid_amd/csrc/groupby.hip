@@ -68,7 +68,7 @@ enum : int {
     ST_SAMPLED = 7,      // plan: keys sampled
     ST_MAXEX = 8,        // + acc
     ST_FXFLAGS = 16,     // + acc: bit0 overflow, bit1 inexact
-    ST_MINEX = 17,       // + acc: plan: smallest sampled exponent of a nonzero value
+    ST_MINEX = 17,       // + acc: 0x7FF - smallest exponent of a nonzero finite value (plan / maxexp)
     ST_WORDS = 24
 };
 
@@ -857,20 +857,136 @@ __global__ __launch_bounds__(kGbThreads) __attribute__((amdgpu_waves_per_eu(WPE)
 // fixed-point window after an overflow / inexact flag).
 __global__ __launch_bounds__(256) void gb_maxexp_kernel(GbParams p, int a) {
     const AccSpec& ac = p.acc[a];
-    uint32_t mx = 0;
+    uint32_t mx = 0, inv_mn = 0;  // inv_mn = 0x7FF - (smallest exponent of a nonzero finite value)
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < p.n; r += (int64_t)gridDim.x * blockDim.x) {
         if (!dev_valid(ac.c, r)) continue;
         uint64_t x = dev_load(ac.c, r);
         if (ac.flags & A_FSUMCAST) x = f64_bits((double)(int64_t)x);
         const uint32_t ex = (uint32_t)(x >> 52) & 0x7FF;
         if (ex != 0x7FF && ex > mx) mx = ex;
+        if (ex != 0x7FF && (x & 0x7fffffffffffffffull) != 0 && 0x7FF - ex > inv_mn) inv_mn = 0x7FF - ex;
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
         const uint32_t o = __shfl_xor(mx, off, 64);
         mx = mx > o ? mx : o;
+        const uint32_t q = __shfl_xor(inv_mn, off, 64);
+        inv_mn = inv_mn > q ? inv_mn : q;
     }
     if ((threadIdx.x & 63) == 0 && mx) atomicMax((unsigned long long*)&p.status[ST_MAXEX + a], (unsigned long long)mx);
+    if ((threadIdx.x & 63) == 0 && inv_mn)
+        atomicMax((unsigned long long*)&p.status[ST_MINEX + a], (unsigned long long)inv_mn);
+}
+
+// ------------------------------------------------------------ wide sums
+// Exact fallback for an f64 sum whose values span more binades than one
+// fixed-point window holds (e.g. 1e300 in one group, 1e3 in another): a
+// second pass adds every selected value, as its 53-bit mantissa, into a
+// per-group big integer of 24-bit digits held in int64 words (carry-free
+// for 2^39 additions per word) from the column's exact smallest exponent
+// upwards.  gb_wide_round_kernel then normalises the digits and rounds once
+// (half-even), so the sum is still the correctly rounded exact sum.
+constexpr int kWideDigit = 24;
+
+template <int PRED>
+__global__ __launch_bounds__(256) void gb_wide_kernel(GbParams p, DevProgram prog, int a, int exmin, int nwords,
+                                                      int64_t* __restrict__ wide) {
+    const AccSpec& ac = p.acc[a];
+    constexpr uint64_t M24 = (1ull << kWideDigit) - 1;
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < p.n; r += (int64_t)gridDim.x * blockDim.x) {
+        if (!dev_valid(ac.c, r)) continue;
+        if (PRED == 1) {
+            if (!dev_valid(p.pred_col, r)) continue;
+            if (!simple_pred(prog.simple_isf, prog.simple_op, dev_load(p.pred_col, r), prog.simple_imm)) continue;
+        } else if (PRED == 2) {
+            const RowVal rv = eval_row(prog.code, prog.n, p.cols, r);
+            if (!(rv.valid && (rv.v & 1))) continue;
+        }
+        uint64_t x = dev_load(ac.c, r);
+        if (ac.flags & A_FSUMCAST) x = f64_bits((double)(int64_t)x);
+        uint32_t ex = (uint32_t)(x >> 52) & 0x7FF;
+        uint64_t m = x & 0x000FFFFFFFFFFFFFull;
+        if (ex == 0x7FF || (ex == 0 && m == 0)) continue;  // inf / NaN flags come from the main pass
+        if (ex == 0) ex = 1;
+        else m |= 1ull << 52;
+        int64_t gs;
+        if (!dev_valid(p.key, r)) {
+            gs = p.gcap;
+        } else {
+            const uint64_t k = dev_load(p.key, r);
+            gs = k == kEmptyKey ? p.gcap + 1 : g_find(p, k);
+        }
+        if (gs < 0) continue;
+        const int pos = (int)ex - exmin;
+        const unsigned __int128 v = (unsigned __int128)m << (pos % kWideDigit);
+        int64_t* q = wide + gs * nwords + pos / kWideDigit;
+        const bool neg = (int64_t)x < 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int64_t dg = (int64_t)((uint64_t)(v >> (kWideDigit * k)) & M24);
+            if (dg) atomicAdd((unsigned long long*)&q[k], (unsigned long long)(neg ? -dg : dg));
+        }
+    }
+}
+
+__global__ void gb_wide_round_kernel(GbParams p, int exmin, int nwords, int64_t* __restrict__ wide,
+                                     double* __restrict__ out) {
+    constexpr int64_t M24 = (1ll << kWideDigit) - 1;
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < p.gcap + 2;
+         s += (int64_t)gridDim.x * blockDim.x) {
+        if (*gfield(p, p.f_len, s) == 0) continue;
+        int64_t* d = wide + s * nwords;
+        // normalise to digits in [0, 2^24) and a signed carry out of the top
+        int64_t c = 0;
+        for (int k = 0; k < nwords; ++k) {
+            const int64_t t = d[k] + c;
+            c = t >> kWideDigit;
+            d[k] = t & M24;
+        }
+        const bool neg = c < 0;
+        if (neg) {  // magnitude of a negative number: negate and renormalise
+            c = 0;
+            for (int k = 0; k < nwords; ++k) {
+                const int64_t t = -d[k] + c;
+                c = t >> kWideDigit;
+                d[k] = t & M24;
+            }
+        }
+        int top = nwords - 1;
+        while (top >= 0 && d[top] == 0) --top;
+        if (top < 0) {
+            out[s] = 0.0;
+            continue;
+        }
+        // the top (up to) 96 bits of the magnitude, plus a sticky bit
+        unsigned __int128 acc = 0;
+        int k = top;
+        for (int taken = 0; k >= 0 && taken < 4; --k, ++taken) acc = (acc << kWideDigit) | (uint64_t)d[k];
+        bool sticky = false;
+        for (int j = k; j >= 0; --j) sticky |= d[j] != 0;
+        const int low = k + 1;  // lowest digit inside acc
+        const uint64_t hi64 = (uint64_t)(acc >> 64);
+        const int lz = hi64 ? __clzll(hi64) : 64 + __clzll((uint64_t)acc);
+        acc <<= lz;  // leading one at bit 127
+        // value = acc * 2^(kWideDigit*low + E0 - lz), E0 = exmin - 1075
+        const int e2 = 127 + kWideDigit * low + (exmin - 1075) - lz;  // exponent of the leading bit
+        int kept = 53;
+        if (e2 < -1022) kept = 53 - (-1022 - e2);
+        double r;
+        if (kept <= 0) {
+            // below half the smallest subnormal unless exactly representable rounding up
+            const bool above_half = kept == 0 && (((uint64_t)(acc >> 64) << 1) != 0 || (uint64_t)acc != 0 || sticky);
+            r = (kept == 0 && above_half) ? __builtin_ldexp(1.0, -1074) : 0.0;
+        } else {
+            uint64_t mant = (uint64_t)(acc >> (128 - kept));
+            const unsigned __int128 rest = acc << kept;  // bits below the kept ones, leading first
+            const bool half = (uint64_t)(rest >> 127) & 1;
+            const bool below = (rest << 1) != 0 || sticky;
+            if (half && (below || (mant & 1))) ++mant;
+            r = __builtin_ldexp((double)mant, e2 - kept + 1);
+        }
+        out[s] = neg ? -r : r;
+    }
 }
 
 // Planning launch: blocks [0, nacc) sample the summed columns' max exponent
@@ -942,7 +1058,7 @@ __global__ __launch_bounds__(256) void gb_plan_kernel(GbParams p, int32_t* botto
         __syncthreads();
     }
     if (threadIdx.x == 0) {
-        p.status[ST_MINEX + a] = red2[0];
+        p.status[ST_MINEX + a] = 0x7FF - red2[0];
         int e = red[0] == 0 ? 2046 : (int)red[0] + kHeadroomBinades;
         if (e > 2046) e = 2046;
         // a value fits iff ex <= bottom + 1075 + (window - 53)
@@ -1031,6 +1147,7 @@ struct FinParams {
     uint32_t* out_key_valid;
     uint64_t* out_first;  // optional
     int64_t cap;          // allocated output rows (guards against a miscount)
+    const double* wide[kMaxAcc];  // per acc: rounded wide sums per slot, or null
 };
 
 __global__ void gb_finalize_kernel(GbParams p, FinParams fp) {
@@ -1066,6 +1183,7 @@ __global__ void gb_finalize_kernel(GbParams p, FinParams fp) {
                 if (flags & FL_NAN || ((flags & FL_PINF) && (flags & FL_NINF))) sum = __builtin_nan("");
                 else if (flags & FL_PINF) sum = __builtin_inf();
                 else if (flags & FL_NINF) sum = -__builtin_inf();
+                else if (fp.wide[os.acc]) sum = fp.wide[os.acc][s];
                 else sum = fx_to_double(*gfield(p, ac.f_sum, s), *gfield(p, ac.f_sum + 1, s),
                                         *gfield(p, ac.f_sum + 2, s), p.bottoms[os.acc]);
                 if (os.kind == PLGPU_AGG_MEAN) {
@@ -1513,12 +1631,21 @@ struct GbRun {
     int32_t key_dtype = PLGPU_I64;
     bool maintain = false;
     int world = 1;
+    uint32_t wide = 0;                       // accs summed by the wide fallback
+    int wide_exmin[kMaxAcc] = {0};
+    int wide_exmax[kMaxAcc] = {0};
+    int64_t* wide_digits[kMaxAcc] = {nullptr};
+    double* wide_sum[kMaxAcc] = {nullptr};
 
     GbRun() {
         std::memset(st, 0, sizeof st);
         std::memset(hb, 0, sizeof hb);
     }
     ~GbRun() {
+        for (int a = 0; a < kMaxAcc; ++a) {
+            dev_free(wide_digits[a], s);
+            dev_free(wide_sum[a], s);
+        }
         dev_free(gtab, s);
         dev_free(status, s);
     }
@@ -1609,7 +1736,7 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
     if (pl.sum_only && !getenv("PLGPU_NO_LIMB2")) {
         bool two = true;
         for (int a = 0; a < p.nacc; ++a) {
-            const int mn = (int)R.st[ST_MINEX + a];
+            const int mn = 0x7FF - (int)R.st[ST_MINEX + a];
             if (mn != 0x7FF && mn < R.hb[a] + 40 + 1075 + kLimb2Margin) two = false;
         }
         if (two) pl.limbs = 2;
@@ -1639,9 +1766,10 @@ static int gb_alloc_table(GbRun& R) {
 
 // Exact max exponents of the flagged accs -> refit bottoms in `hint`.
 // Returns true when some window changes.
-static int gb_refit(GbRun& R, uint32_t flagged, int32_t* hint, bool* changed) {
+static int gb_refit(GbRun& R, uint32_t flagged, int32_t* hint, bool* changed, uint32_t* wide) {
     GbParams& p = R.pl.p;
     *changed = false;
+    *wide = 0;
     for (int a = 0; a < kMaxAcc; ++a) hint[a] = R.hb[a];
     if (!flagged) return PLGPU_OK;
     for (int a = 0; a < p.nacc; ++a)
@@ -1651,14 +1779,41 @@ static int gb_refit(GbRun& R, uint32_t flagged, int32_t* hint, bool* changed) {
     PLGPU_HIP(hipStreamSynchronize(R.s));
     for (int a = 0; a < p.nacc; ++a) {
         if (!((flagged >> a) & 1u)) continue;
-        const uint64_t fl = (R.st[ST_FXFLAGS] >> (2 * a)) & 3u;
-        const int tmax = (int)R.st[ST_MAXEX + a];
-        const int allowed = R.hb[a] + 1075 + (kSumWindowBits - 53);
-        if ((fl & 1u) || ((fl & 2u) && tmax > 0 && tmax < allowed)) {
-            // overflowed values were dropped, so the whole pass reruns
-            hint[a] = std::max(tmax, 1) - 1075 - (kSumWindowBits - 53);
+        const int tmax = std::max((int)R.st[ST_MAXEX + a], 1);
+        const int tmin = std::max(0x7FF - (int)R.st[ST_MINEX + a], 1);
+        if (tmax - tmin <= kSumWindowBits - 53) {
+            // one window holds every value exactly: put its top at the max
+            hint[a] = tmax - 1075 - (kSumWindowBits - 53);
             *changed = *changed || hint[a] != R.hb[a];
+        } else {
+            // wider than a window: exact big-integer pass for this column
+            *wide |= 1u << a;
+            R.wide_exmin[a] = std::min(tmin, tmax);
+            R.wide_exmax[a] = tmax;
         }
+    }
+    return PLGPU_OK;
+}
+
+// Exact wide sums for the accs in R.wide (see gb_wide_kernel).
+static int gb_wide(GbRun& R) {
+    GbParams& p = R.pl.p;
+    for (int a = 0; a < p.nacc; ++a) {
+        if (!((R.wide >> a) & 1u)) continue;
+        const int exmin = R.wide_exmin[a];
+        const int nwords = (R.wide_exmax[a] - exmin) / kWideDigit + 6;
+        const size_t slots = (size_t)(p.gcap + 2);
+        int rc = dev_alloc((void**)&R.wide_digits[a], slots * nwords * 8, R.s);
+        if (!rc) rc = dev_alloc((void**)&R.wide_sum[a], slots * 8, R.s);
+        if (rc) return rc;
+        PLGPU_HIP(hipMemsetAsync(R.wide_digits[a], 0, slots * nwords * 8, R.s));
+        const int g = std::max(1, num_cus() * 8);
+        if (R.pred == 0) gb_wide_kernel<0><<<g, 256, 0, R.s>>>(p, R.dp, a, exmin, nwords, R.wide_digits[a]);
+        else if (R.pred == 1) gb_wide_kernel<1><<<g, 256, 0, R.s>>>(p, R.dp, a, exmin, nwords, R.wide_digits[a]);
+        else gb_wide_kernel<2><<<g, 256, 0, R.s>>>(p, R.dp, a, exmin, nwords, R.wide_digits[a]);
+        const int fg = (int)std::min<int64_t>((p.gcap + 2 + 255) / 256, 256 * 16);
+        gb_wide_round_kernel<<<fg, 256, 0, R.s>>>(p, exmin, nwords, R.wide_digits[a], R.wide_sum[a]);
+        PLGPU_HIP(hipGetLastError());
     }
     return PLGPU_OK;
 }
@@ -1713,6 +1868,7 @@ static int gb_main(GbRun& R, bool auto_refit, bool* refit, int32_t* hint) {
         uint32_t flagged = 0;
         for (int a = 0; a < p.nacc; ++a)
             if ((p.acc[a].flags & (A_FSUM | A_FSUMCAST)) && ((R.st[ST_FXFLAGS] >> (2 * a)) & 3u)) flagged |= 1u << a;
+        flagged &= ~R.wide;
         if (flagged && pl.limbs == 2 && p.n_full > 0 && pl.sum_only) {
             // a value fell below the 2-limb window (or out of the top): redo
             // the pass with the full 3-limb window before any refit
@@ -1726,10 +1882,19 @@ static int gb_main(GbRun& R, bool auto_refit, bool* refit, int32_t* hint) {
         if (flagged) {
             int32_t h[kMaxAcc];
             bool changed = false;
-            if ((rc = gb_refit(R, flagged, h, &changed))) break;
+            uint32_t wide = 0;
+            if ((rc = gb_refit(R, flagged, h, &changed, &wide))) break;
+            if (wide && !auto_refit) {
+                rc = fail(PLGPU_ERR_CAPACITY,
+                          "f64 sum: the values of one column span more binades than the partitioned "
+                          "group-by's fixed-point window; use the single-GPU group-by for this column");
+                break;
+            }
+            R.wide |= wide;
             if (changed) {
                 if (auto_refit) {
-                    for (int a = 0; a < kMaxAcc; ++a) R.hb[a] = h[a];
+                    for (int a = 0; a < kMaxAcc; ++a)
+                        if (!((R.wide >> a) & 1u)) R.hb[a] = h[a];
                     again = true;
                 } else {
                     if (refit) *refit = true;
@@ -1747,6 +1912,7 @@ static int gb_main(GbRun& R, bool auto_refit, bool* refit, int32_t* hint) {
     if (rc == PLGPU_OK) (void)hipEventElapsedTime(&R.ms, ev0, ev1);
     (void)hipEventDestroy(ev0);
     (void)hipEventDestroy(ev1);
+    if (rc == PLGPU_OK && R.wide) rc = gb_wide(R);
     return rc;
 }
 
@@ -1769,7 +1935,7 @@ static void gb_fill_info(const GbRun& R, plgpu_groupby_info* info) {
     info->path = p.n_full > 0 ? (R.pl.sum_only ? 2 : 1) : 0;
     info->sum_limbs = p.n_full > 0 && R.pl.sum_only ? R.pl.limbs : 3;
     for (int a = 0; a < p.nacc; ++a)
-        if ((R.st[ST_FXFLAGS] >> (2 * a)) & 2u) info->sum_inexact |= 1 << a;
+        if (((R.st[ST_FXFLAGS] >> (2 * a)) & 2u) && !((R.wide >> a) & 1u)) info->sum_inexact |= 1 << a;
 }
 
 // Global table -> output columns (+ first-occurrence order, key narrowing).
@@ -1801,6 +1967,7 @@ static int gb_finalize(GbRun& R, int32_t naggs, plgpu_column* out_key, plgpu_col
         (void)hipMemsetAsync((void*)out_key->validity, 0, ((groups + 63) / 64) * 8, s);
         fp.out_first = first;
         fp.cap = groups;
+        for (int a = 0; a < kMaxAcc; ++a) fp.wide[a] = R.wide_sum[a];
         const int fg = (int)std::min<int64_t>((p.gcap + 2 + 255) / 256, 256 * 16);
         gb_finalize_kernel<<<fg, 256, 0, s>>>(p, fp);
         hipError_t e = hipGetLastError();

@@ -417,3 +417,82 @@ def test_group_by_large_properties(gpu):
     k3, s3, _ = run(key, px, 2.0)
     assert np.array_equal(_bits(s3), _bits(s1 * 2.0))
     assert int(l1.sum()) == int((px > 500.0).sum().item())
+
+
+# ------------------------------------------------- sum window variants
+def _sum_only_frame(n, seed):
+    rng = np.random.default_rng(seed)
+    d = rng.uniform(1.0, 1000.0, n)
+    e = rng.uniform(-50.0, 50.0, n)
+    e[e == 0] = 1.0
+    key = rng.integers(0, 50, n).astype(np.int64) * 3 + 1
+    return rng, key, d, e
+
+
+@pytest.mark.parametrize("inject", [None, "tiny", "subnormal", "huge", "negzero"])
+def test_sum_window_two_limbs_and_reruns(gpu, inject):
+    """Narrow exponent spans take the 2-limb LDS window; values the sampled
+    plan did not see (tiny / subnormal / huge, placed off the sample
+    stride) force the 3-limb rerun or a window refit.  The result is the
+    exact sum either way."""
+    n = 300_001
+    rng, key, d, e = _sum_only_frame(n, 17)
+    step = n // 65536
+    off = np.arange(1, n, step)[:-1] + 1   # never a multiple of the stride
+    pos = rng.choice(off[off % step != 0], 40, replace=False)
+    if inject == "tiny":
+        d[pos] = 1e-30
+    elif inject == "subnormal":
+        d[pos] = 5e-324
+    elif inject == "huge":
+        d[pos] = 1e300
+    elif inject == "negzero":
+        d[pos] = -0.0
+    info = {}
+    cols = {"d": (d, None), "e": (e, None)}
+    _check_group_by(cols, key, None, [("sum", "d"), ("sum", "e"), ("mean", "d")], None, None, [], False, info)
+    assert info["path"] == 2
+    if inject in (None, "negzero"):
+        assert info["sum_limbs"] == 2 and info["reruns"] == 0, info
+    else:
+        assert info["reruns"] >= 1, info
+
+
+@pytest.mark.parametrize("nulls", [False, True])
+def test_sum_wide_exponent_span_is_exact(gpu, nulls):
+    """Values spanning far more binades than one fixed-point window (1e300,
+    1, 1e-300, subnormals, cancellation) take the exact wide fallback; sums
+    are still math.fsum of each group, bit for bit."""
+    rng = np.random.default_rng(99)
+    n = 200_000
+    key = rng.integers(0, 40, n).astype(np.int64)
+    d = rng.uniform(-1.0, 1.0, n)
+    big = rng.random(n) < 0.01
+    d[big] = rng.choice([1e300, -1e300, 3e299], big.sum())
+    small = rng.random(n) < 0.01
+    d[small] = rng.choice([1e-300, -2.5e-300, 5e-324, 1e-310], small.sum())
+    # an exact cancellation: +1e300, -1e300 and 1.0 in group 41 only
+    key[:3] = 41
+    d[:3] = [1e300, 1.0, -1e300]
+    valid = (rng.random(n) > 0.05) if nulls else None
+    if valid is not None:
+        valid[:3] = True
+    info = {}
+    cols = {"d": (d, valid), "e": (rng.uniform(1, 2, n), None)}
+    out = _check_group_by(cols, key, None, [("sum", "d"), ("mean", "d"), ("sum", "e")], None, None, [], False, info)
+    got = dict(zip(out["k"].to_list(), out["sum_d"].to_list()))
+    assert got[41] == 1.0
+    assert info["sum_inexact"] == 0
+
+
+def test_sum_wide_with_program_predicate(gpu):
+    rng = np.random.default_rng(5)
+    n = 100_000
+    cols = _rand_frame(rng, n)
+    a = cols["a"][0].copy()
+    a[rng.random(n) < 0.01] = 1e280
+    a[rng.random(n) < 0.01] = 1e-280
+    cols["a"] = (a, cols["a"][1])
+    key = rng.integers(0, 30, n).astype(np.int64)
+    mk, names, prog = PREDICATES["program"]
+    _check_group_by(cols, key, None, [("sum", "a"), ("mean", "a"), ("len", "a")], mk(), prog, names, False)
