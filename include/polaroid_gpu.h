@@ -266,6 +266,39 @@ int plgpu_gb_merge(const void* records, int64_t n_records, const plgpu_column* c
                    int32_t key_dtype, plgpu_column* out_key, plgpu_column* out_aggs,
                    plgpu_groupby_info* info, void* stream);
 
+/* ---- hash join ------------------------------------------------------------
+ * maintain_order (polars-ops/src/frame/join/args.rs:100 MaintainOrderJoin)
+ * and validate (args.rs JoinValidation). */
+enum plgpu_join_order {
+    PLGPU_JOIN_ORDER_NONE = 0,        /* unspecified (build on the shorter side) */
+    PLGPU_JOIN_ORDER_LEFT = 1,        /* left row order (then right row order)   */
+    PLGPU_JOIN_ORDER_RIGHT = 2,       /* right row order (then left row order)   */
+    PLGPU_JOIN_ORDER_LEFT_RIGHT = 3,
+    PLGPU_JOIN_ORDER_RIGHT_LEFT = 4
+};
+enum plgpu_join_validate {
+    PLGPU_JOIN_VALIDATE_M_M = 0,
+    PLGPU_JOIN_VALIDATE_1_M = 1,      /* left keys unique  */
+    PLGPU_JOIN_VALIDATE_M_1 = 2,      /* right keys unique */
+    PLGPU_JOIN_VALIDATE_1_1 = 3
+};
+
+/* Inner equi-join on one integer key (I64 / I32 / U32; the two sides may
+ * differ, values compare as integers).  Produces the matching row pairs as
+ * two UInt32 index columns (the reference's IdxSize pairs).  Null keys match
+ * only when nulls_equal != 0.  Replaces
+ * polars-ops/src/frame/join/hash_join/single_keys_inner.rs:45
+ * hash_join_tuples_inner (via _inner_join / JoinDispatch). */
+int plgpu_join_inner(const plgpu_column* left_key, const plgpu_column* right_key,
+                     int32_t nulls_equal, int32_t maintain_order, int32_t validate,
+                     plgpu_column* out_left_idx, plgpu_column* out_right_idx, void* stream);
+
+/* out_cols[i] = cols[i][idx] (UInt32 indices, no nulls), validity carried.
+ * Replaces the join materialisation take
+ * (polars-core/src/chunked_array/ops/gather.rs, DataFrame::take_unchecked). */
+int plgpu_gather(const plgpu_column* cols, int32_t ncols, const plgpu_column* idx,
+                 plgpu_column* out_cols, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -57,6 +57,8 @@ def lib():
         L.or_eval.restype = C.c_int
         L.or_filter.restype = C.c_int64
         L.or_group_by_agg.restype = C.c_int64
+        L.or_join_inner.restype = C.c_int64
+        L.or_join_inner.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int64, C.c_void_p, C.c_void_p]
         L.or_fsum.restype = C.c_double
         L.or_fsum.argtypes = [C.c_void_p, C.c_int64]
         L.or_baseline_filter_groupby_sum.restype = C.c_int64
@@ -185,6 +187,19 @@ def group_by_agg(key: HostCol, cols: list[HostCol], program, aggs: list[tuple[st
         raise ValueError("oracle: group_by failed")
     return keys[:g].copy(), kvalid[:g].astype(bool), [(o[:g].copy(), v[:g].astype(bool))
                                                        for o, v in zip(outs, outv)]
+
+
+def join_inner(left: HostCol, right: HostCol, nulls_equal: bool = False):
+    """Inner-join row pairs in (left, right) order: (left_idx, right_idx)."""
+    cap = 1 << 16
+    while True:
+        ol = np.zeros(cap, np.int64)
+        orr = np.zeros(cap, np.int64)
+        n = lib().or_join_inner(C.byref(left.c), C.byref(right.c), int(nulls_equal), cap,
+                                ol.ctypes.data, orr.ctypes.data)
+        if n >= 0:
+            return ol[:n].copy(), orr[:n].copy()
+        cap *= 4
 
 
 def fsum(x: np.ndarray) -> float:

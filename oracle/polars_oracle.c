@@ -690,3 +690,80 @@ OR_EXPORT int64_t or_baseline_filter_groupby_sum(const int64_t* key, const doubl
     free(parts);
     return ng;
 }
+
+/* ------------------------------------------------------------ hash join
+ * polars-ops/src/frame/join/hash_join/single_keys_inner.rs:45
+ * hash_join_tuples_inner: a hash table key -> IdxVec of build rows (rows in
+ * insertion = row order; null keys inserted only when nulls_equal,
+ * single_keys.rs build_tables), then every probe row in order looks its key
+ * up (probe_inner, :11) and emits (probe_idx, build_idx) for each build row.
+ * Restated with the right side as the build side and the left side probed
+ * in order, i.e. the pairs in (left, right) order ("left_right"); the
+ * reference's other orders are permutations of the same pairs.
+ * The "hash table" is a (key, row) array sorted by key then row. */
+typedef struct {
+    int64_t key;
+    int64_t row;
+    int is_null;
+} jn_item;
+
+static int jn_cmp(const void* a, const void* b) {
+    const jn_item* x = (const jn_item*)a;
+    const jn_item* y = (const jn_item*)b;
+    if (x->is_null != y->is_null) return x->is_null < y->is_null ? -1 : 1;
+    if (!x->is_null && x->key != y->key) return x->key < y->key ? -1 : 1;
+    return x->row < y->row ? -1 : (x->row > y->row ? 1 : 0);
+}
+
+static int64_t col_int(const plgpu_column* c, int64_t r) {
+    const int64_t p = c->offset + r;
+    switch (c->dtype) {
+    case PLGPU_I32: return ((const int32_t*)c->values)[p];
+    case PLGPU_U32: return ((const uint32_t*)c->values)[p];
+    default: return ((const int64_t*)c->values)[p];
+    }
+}
+
+/* Returns the number of pairs (or -1 if more than cap). */
+OR_EXPORT int64_t or_join_inner(const plgpu_column* lk, const plgpu_column* rk, int32_t nulls_equal, int64_t cap,
+                                int64_t* out_l, int64_t* out_r) {
+    const int64_t nr = rk->length, nl = lk->length;
+    jn_item* t = (jn_item*)malloc(sizeof(jn_item) * (size_t)(nr > 0 ? nr : 1));
+    int64_t m = 0;
+    for (int64_t r = 0; r < nr; ++r) {
+        const int v = col_valid(rk, r);
+        if (!v && !nulls_equal) continue;
+        t[m].is_null = !v;
+        t[m].key = v ? col_int(rk, r) : 0;
+        t[m].row = r;
+        ++m;
+    }
+    qsort(t, (size_t)m, sizeof(jn_item), jn_cmp);
+    int64_t n = 0;
+    for (int64_t l = 0; l < nl; ++l) {
+        const int v = col_valid(lk, l);
+        if (!v && !nulls_equal) continue;
+        jn_item q;
+        q.is_null = !v;
+        q.key = v ? col_int(lk, l) : 0;
+        q.row = -1;
+        /* first item >= (key, -1) */
+        int64_t lo = 0, hi = m;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) / 2;
+            if (jn_cmp(&t[mid], &q) < 0) lo = mid + 1;
+            else hi = mid;
+        }
+        for (int64_t i = lo; i < m && t[i].is_null == q.is_null && (q.is_null || t[i].key == q.key); ++i) {
+            if (n >= cap) {
+                free(t);
+                return -1;
+            }
+            out_l[n] = l;
+            out_r[n] = t[i].row;
+            ++n;
+        }
+    }
+    free(t);
+    return n;
+}

@@ -1,0 +1,697 @@
+// Hash inner join on one integer key, and multi-column gather (the join's
+// materialisation step).
+//
+// Reference (paths under /root/reference/crates):
+//   polars-ops/src/frame/join/hash_join/single_keys_inner.rs:45
+//     hash_join_tuples_inner: build hash tables on the shorter relation,
+//     probe with the other, emit (left_idx, right_idx) IdxSize pairs;
+//   polars-ops/src/frame/join/args.rs:25 JoinArgs (nulls_equal,
+//     maintain_order, validate);
+//   polars-core/src/chunked_array/ops/gather.rs (take by index) for the
+//     materialisation.
+//
+// MI355X design:
+//   build  - open-addressing table of 16-byte entries {key, ref, cnt} in HBM
+//            (2^k slots, load <= 0.6, sized to stay resident in the 256 MiB
+//            Infinity Cache for 1e7 build rows); one 16-byte load per probe
+//            step returns key, count and (unique keys) the build row itself;
+//            duplicate keys keep a CSR row list (ref = offset);
+//   probe  - count pass (per 4096-row tile) -> scan -> write pass with
+//            block-level scans, so pairs come out in probe-row order; rows
+//            of one key follow build-row order (segments sorted when needed);
+//   gather - one kernel per output column, validity bits re-packed with a
+//            wave-wide OR.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "plgpu_internal.hpp"
+
+namespace plgpu {
+
+constexpr int kJnThreads = 256;
+constexpr int kJnTileRows = 4096;          // probe tile (16 rows per thread)
+constexpr int kJnProbeLimit = 1 << 16;      // linear-probe bound before "table full"
+constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
+
+struct JnEntry {
+    uint64_t key;
+    uint32_t ref;  // cnt == 1: the build row; cnt > 1: CSR offset into rows
+    uint32_t cnt;
+};
+
+struct JnTable {
+    JnEntry* ent;      // cap + 2 entries: [cap] null key, [cap+1] INT64_MIN key
+    uint32_t* rows;    // CSR row lists of duplicate keys
+    int bits;
+    int64_t cap;
+};
+
+__device__ __forceinline__ int64_t jn_find(const JnTable& t, uint64_t key) {
+    const uint64_t mask = (uint64_t)t.cap - 1;
+    uint64_t s = hash_slot(key, t.bits);
+    for (int i = 0; i < kJnProbeLimit; ++i, s = (s + 1) & mask) {
+        const uint64_t k = __hip_atomic_load(&t.ent[s].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (k == key) return (int64_t)s;
+        if (k == kEmptyKey) return -1;
+    }
+    return -1;
+}
+
+// ----------------------------------------------------------------- scan
+// Exclusive scan of n u64 values: out[i] = sum(in[0..i)), out[n] = total.
+constexpr int kScanThreads = 256;
+constexpr int kScanPer = 16;  // values per thread per block chunk
+constexpr int64_t kScanChunk = (int64_t)kScanThreads * kScanPer;
+
+__device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t* wsum, uint64_t& total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint64_t x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint64_t y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+    }
+    if (lane == 63) wsum[wid] = x;
+    __syncthreads();
+    uint64_t base = 0;
+    total = 0;
+    const int nw = blockDim.x >> 6;
+    for (int w = 0; w < nw; ++w) {
+        if (w < wid) base += wsum[w];
+        total += wsum[w];
+    }
+    __syncthreads();
+    return base + x - v;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kScanThreads) void scan_reduce_kernel(const T* __restrict__ in, int64_t n,
+                                                                   uint64_t* __restrict__ part) {
+    __shared__ uint64_t wsum[kScanThreads / 64];
+    const int64_t base = (int64_t)blockIdx.x * kScanChunk;
+    uint64_t s = 0;
+    for (int k = 0; k < kScanPer; ++k) {
+        const int64_t i = base + (int64_t)k * kScanThreads + threadIdx.x;
+        if (i < n) s += (uint64_t)in[i];
+    }
+    uint64_t total;
+    (void)block_excl_scan(s, wsum, total);
+    if (threadIdx.x == 0) part[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(1024) void scan_parts_kernel(uint64_t* __restrict__ part, int64_t nparts,
+                                                          uint64_t* __restrict__ total_out) {
+    __shared__ uint64_t wsum[16];
+    const int64_t per = (nparts + 1023) / 1024;
+    const int64_t lo = threadIdx.x * per;
+    const int64_t hi = lo + per < nparts ? lo + per : nparts;
+    uint64_t s = 0;
+    for (int64_t i = lo; i < hi; ++i) s += part[i];
+    uint64_t total;
+    uint64_t run = block_excl_scan(s, wsum, total);
+    for (int64_t i = lo; i < hi; ++i) {
+        const uint64_t v = part[i];
+        part[i] = run;
+        run += v;
+    }
+    if (threadIdx.x == 0) *total_out = total;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kScanThreads) void scan_apply_kernel(const T* __restrict__ in, int64_t n,
+                                                                  const uint64_t* __restrict__ part,
+                                                                  uint64_t* __restrict__ out) {
+    __shared__ uint64_t wsum[kScanThreads / 64];
+    // thread owns kScanPer consecutive values so the chunk scans in order
+    const int64_t base = (int64_t)blockIdx.x * kScanChunk + (int64_t)threadIdx.x * kScanPer;
+    uint64_t v[kScanPer];
+    uint64_t s = 0;
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+        const int64_t i = base + k;
+        v[k] = i < n ? (uint64_t)in[i] : 0;
+        s += v[k];
+    }
+    uint64_t total;
+    uint64_t run = block_excl_scan(s, wsum, total) + part[blockIdx.x];
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+        const int64_t i = base + k;
+        if (i < n) out[i] = run;
+        run += v[k];
+    }
+}
+
+// out: n + 1 u64 (out[n] = total).  part: scratch of ceil(n / chunk) + 1.
+template <typename T>
+static hipError_t scan_exclusive(const T* in, int64_t n, uint64_t* out, uint64_t* part, hipStream_t s) {
+    const int64_t nb = std::max<int64_t>(1, (n + kScanChunk - 1) / kScanChunk);
+    scan_reduce_kernel<T><<<(unsigned)nb, kScanThreads, 0, s>>>(in, n, part);
+    scan_parts_kernel<<<1, 1024, 0, s>>>(part, nb, out + n);
+    scan_apply_kernel<T><<<(unsigned)nb, kScanThreads, 0, s>>>(in, n, part, out);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- build
+__global__ void jn_init_kernel(JnEntry* ent, int64_t n, uint32_t* cnt) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        ent[i].key = kEmptyKey;
+        ent[i].ref = 0;
+        ent[i].cnt = 0;
+        cnt[i] = 0;
+    }
+}
+
+// Insert the build keys; bslot[i] = entry of row i (kNoSlot: null key that
+// never matches).  status[0] counts rows that found no free slot.
+__global__ void jn_build_kernel(DevCol bk, int64_t nb, JnTable t, bool nulls_equal, uint32_t* __restrict__ cnt,
+                                uint32_t* __restrict__ bslot, unsigned long long* status) {
+    const uint64_t mask = (uint64_t)t.cap - 1;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nb; i += (int64_t)gridDim.x * blockDim.x) {
+        int64_t slot;
+        if (!dev_valid(bk, i)) {
+            slot = nulls_equal ? t.cap : -1;
+        } else {
+            const uint64_t key = dev_load(bk, i);
+            if (key == kEmptyKey) {
+                slot = t.cap + 1;
+            } else {
+                slot = -2;
+                uint64_t s = hash_slot(key, t.bits);
+                for (int p = 0; p < kJnProbeLimit; ++p, s = (s + 1) & mask) {
+                    uint64_t k = __hip_atomic_load(&t.ent[s].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (k == kEmptyKey) {
+                        k = atomicCAS((unsigned long long*)&t.ent[s].key, (unsigned long long)kEmptyKey,
+                                      (unsigned long long)key);
+                        if (k == kEmptyKey) k = key;
+                    }
+                    if (k == key) {
+                        slot = (int64_t)s;
+                        break;
+                    }
+                }
+                if (slot == -2) {
+                    atomicAdd(&status[0], 1ull);
+                    slot = -1;
+                }
+            }
+        }
+        if (slot >= 0) {
+            atomicAdd(&cnt[slot], 1u);
+            bslot[i] = (uint32_t)slot;
+        } else {
+            bslot[i] = kNoSlot;
+        }
+    }
+}
+
+// Entries get their CSR offset / count; status[1] = max count.
+__global__ void jn_entries_kernel(JnTable t, const uint32_t* __restrict__ cnt, const uint64_t* __restrict__ off,
+                                  unsigned long long* status) {
+    uint32_t mx = 0;
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < t.cap + 2;
+         s += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t c = cnt[s];
+        t.ent[s].cnt = c;
+        t.ent[s].ref = (uint32_t)off[s];
+        mx = c > mx ? c : mx;
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const uint32_t y = __shfl_xor(mx, o, 64);
+        mx = y > mx ? y : mx;
+    }
+    if ((threadIdx.x & 63) == 0 && mx) atomicMax(&status[1], (unsigned long long)mx);
+}
+
+// Row lists: rows[off[slot] + k] = build row; unique keys store the row in
+// the entry itself.
+__global__ void jn_scatter_kernel(int64_t nb, JnTable t, const uint32_t* __restrict__ bslot,
+                                  uint32_t* __restrict__ cursor) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nb; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t s = bslot[i];
+        if (s == kNoSlot) continue;
+        const JnEntry e = t.ent[s];
+        const uint32_t k = atomicAdd(&cursor[s], 1u);
+        t.rows[e.ref + k] = (uint32_t)i;
+    }
+}
+
+__global__ void jn_unique_ref_kernel(JnTable t) {
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < t.cap + 2;
+         s += (int64_t)gridDim.x * blockDim.x) {
+        if (t.ent[s].cnt == 1) t.ent[s].ref = t.rows[t.ent[s].ref];
+    }
+}
+
+// Sort the row list of every duplicate key (build-row order, as the
+// reference's IdxVec is filled in row order).  Short lists: one thread,
+// insertion sort; long lists: one workgroup, odd-even transposition.
+constexpr uint32_t kShortList = 64;
+__global__ void jn_sort_short_kernel(JnTable t, uint32_t* __restrict__ long_slots,
+                                     unsigned long long* __restrict__ nlong) {
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < t.cap + 2;
+         s += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t c = t.ent[s].cnt;
+        if (c <= 1) continue;
+        if (c > kShortList) {
+            const unsigned long long k = atomicAdd(nlong, 1ull);
+            long_slots[k] = (uint32_t)s;
+            continue;
+        }
+        uint32_t* r = t.rows + t.ent[s].ref;
+        for (uint32_t i = 1; i < c; ++i) {
+            const uint32_t x = r[i];
+            uint32_t j = i;
+            while (j > 0 && r[j - 1] > x) {
+                r[j] = r[j - 1];
+                --j;
+            }
+            r[j] = x;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void jn_sort_long_kernel(JnTable t, const uint32_t* __restrict__ long_slots) {
+    const uint32_t s = long_slots[blockIdx.x];
+    const uint32_t c = t.ent[s].cnt;
+    uint32_t* r = t.rows + t.ent[s].ref;
+    for (uint32_t phase = 0; phase < c; ++phase) {
+        for (uint32_t i = 2 * threadIdx.x + (phase & 1); i + 1 < c; i += 2 * blockDim.x) {
+            const uint32_t a = r[i], b = r[i + 1];
+            if (a > b) {
+                r[i] = b;
+                r[i + 1] = a;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------- probe
+__device__ __forceinline__ uint32_t jn_row_matches(const DevCol& pk, int64_t r, const JnTable& t, bool nulls_equal,
+                                                   int64_t& slot) {
+    slot = -1;
+    if (!dev_valid(pk, r)) {
+        if (!nulls_equal) return 0;
+        slot = t.cap;
+    } else {
+        const uint64_t key = dev_load(pk, r);
+        slot = key == kEmptyKey ? t.cap + 1 : jn_find(t, key);
+        if (slot < 0) return 0;
+    }
+    return t.ent[slot].cnt;
+}
+
+__global__ __launch_bounds__(kJnThreads) void jn_probe_count_kernel(DevCol pk, int64_t np, JnTable t,
+                                                                    bool nulls_equal,
+                                                                    uint64_t* __restrict__ tile_counts,
+                                                                    int64_t ntiles) {
+    __shared__ uint64_t wsum[kJnThreads / 64];
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        uint64_t c = 0;
+        for (int k = 0; k < kJnTileRows / kJnThreads; ++k) {
+            const int64_t r = tile * kJnTileRows + (int64_t)k * kJnThreads + threadIdx.x;
+            if (r >= np) break;
+            int64_t slot;
+            c += jn_row_matches(pk, r, t, nulls_equal, slot);
+        }
+        uint64_t total;
+        (void)block_excl_scan(c, wsum, total);
+        if (threadIdx.x == 0) tile_counts[tile] = total;
+    }
+}
+
+// Pairs in probe-row order: within a tile, row r = base + k*T + tid is
+// ranked k*T + tid; one block scan per k.
+__global__ __launch_bounds__(kJnThreads) void jn_probe_write_kernel(DevCol pk, int64_t np, JnTable t,
+                                                                    bool nulls_equal,
+                                                                    const uint64_t* __restrict__ tile_off,
+                                                                    int64_t ntiles, uint32_t* __restrict__ out_p,
+                                                                    uint32_t* __restrict__ out_b) {
+    __shared__ uint64_t wsum[kJnThreads / 64];
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        uint64_t run = tile_off[tile];
+        for (int k = 0; k < kJnTileRows / kJnThreads; ++k) {
+            const int64_t r = tile * kJnTileRows + (int64_t)k * kJnThreads + threadIdx.x;
+            int64_t slot = -1;
+            const uint32_t c = r < np ? jn_row_matches(pk, r, t, nulls_equal, slot) : 0u;
+            uint64_t total;
+            const uint64_t pos = run + block_excl_scan(c, wsum, total);
+            if (c) {
+                const JnEntry e = t.ent[slot];
+                if (c == 1) {
+                    out_p[pos] = (uint32_t)r;
+                    out_b[pos] = e.ref;
+                } else {
+                    for (uint32_t j = 0; j < c; ++j) {
+                        out_p[pos + j] = (uint32_t)r;
+                        out_b[pos + j] = t.rows[e.ref + j];
+                    }
+                }
+            }
+            run += total;
+        }
+    }
+}
+
+// --------------------------------------------------------------- gather
+template <int EB>  // element bytes 4 / 8
+__global__ void gather_col_kernel(DevCol c, const uint32_t* __restrict__ idx, int64_t n, void* __restrict__ out,
+                                  uint64_t* __restrict__ out_valid) {
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < n; base += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t o = base + threadIdx.x;
+        bool valid = false;
+        if (o < n) {
+            const int64_t r = idx[o];
+            const int64_t p = c.offset + r;
+            if (EB == 8) ((uint64_t*)out)[o] = ((const uint64_t*)c.values)[p];
+            else ((uint32_t*)out)[o] = ((const uint32_t*)c.values)[p];
+            valid = dev_valid(c, r);
+        }
+        if (out_valid) {
+            // blockDim is a multiple of 64 and base of 64: one word per wave
+            const uint64_t w = __ballot(valid);
+            if ((threadIdx.x & 63) == 0 && base + threadIdx.x < n) out_valid[(base + threadIdx.x) >> 6] = w;
+        }
+    }
+}
+
+__global__ void gather_bool_kernel(DevCol c, const uint32_t* __restrict__ idx, int64_t n,
+                                   uint64_t* __restrict__ out, uint64_t* __restrict__ out_valid) {
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < n; base += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t o = base + threadIdx.x;
+        bool v = false, valid = false;
+        if (o < n) {
+            const int64_t r = idx[o];
+            v = dev_load(c, r) & 1;
+            valid = dev_valid(c, r);
+        }
+        const uint64_t wv = __ballot(v), wm = __ballot(valid);
+        if ((threadIdx.x & 63) == 0 && o < n) {
+            out[o >> 6] = wv;
+            if (out_valid) out_valid[o >> 6] = wm;
+        }
+    }
+}
+
+static int gather_into(const plgpu_column& src, const uint32_t* idx, int64_t n, plgpu_column* out, hipStream_t s) {
+    const bool nullable = src.validity != nullptr;
+    int rc = make_owned_column(out, src.dtype, n, nullable, s);
+    if (rc) return rc;
+    if (n == 0) return PLGPU_OK;
+    DevCol c;
+    std::memset(&c, 0, sizeof c);
+    c.dtype = src.dtype;
+    c.offset = src.offset;
+    c.values = src.values;
+    c.validity = src.validity;
+    const int g = (int)std::min<int64_t>((n + 255) / 256, 256 * 64);
+    uint64_t* ov = (uint64_t*)out->validity;
+    if (src.dtype == PLGPU_BOOL)
+        gather_bool_kernel<<<g, 256, 0, s>>>(c, idx, n, (uint64_t*)out->values, ov);
+    else if (dtype_bytes(src.dtype) == 8)
+        gather_col_kernel<8><<<g, 256, 0, s>>>(c, idx, n, (void*)out->values, ov);
+    else
+        gather_col_kernel<4><<<g, 256, 0, s>>>(c, idx, n, (void*)out->values, ov);
+    PLGPU_HIP(hipGetLastError());
+    out->null_count = nullable ? -1 : 0;
+    return PLGPU_OK;
+}
+
+static int log2_ceil64(int64_t x) {
+    int b = 0;
+    while ((int64_t(1) << b) < x) ++b;
+    return b;
+}
+
+}  // namespace plgpu
+
+using namespace plgpu;
+
+// Built hash table of one join side (kept for the probe).
+struct JnBuilt {
+    JnTable t;
+    uint64_t max_count = 0;
+    int64_t rows = 0;
+    JnBuilt() { std::memset(&t, 0, sizeof t); }
+};
+
+static void jn_free(JnBuilt& b, hipStream_t s) {
+    dev_free(b.t.ent, s);
+    dev_free(b.t.rows, s);
+    b.t.ent = nullptr;
+    b.t.rows = nullptr;
+}
+
+// Build the table over `key` (rows [0, n)); sorted row lists if `ordered`.
+static int jn_build(const plgpu_column* key, bool nulls_equal, bool ordered, JnBuilt* out, hipStream_t s) {
+    const int64_t nb = key->length;
+    DevCol bk;
+    std::memset(&bk, 0, sizeof bk);
+    bk.dtype = key->dtype;
+    bk.offset = key->offset;
+    bk.values = key->values;
+    bk.validity = key->validity;
+    int bits = std::max(10, log2_ceil64((nb * 5 + 2) / 3));  // load <= 0.6
+    uint32_t* cnt = nullptr;
+    uint32_t* bslot = nullptr;
+    uint64_t* off = nullptr;
+    uint64_t* part = nullptr;
+    unsigned long long* status = nullptr;
+    int rc = PLGPU_OK;
+    JnBuilt b;
+    for (int attempt = 0;; ++attempt) {
+        b.t.bits = bits;
+        b.t.cap = int64_t(1) << bits;
+        const int64_t ne = b.t.cap + 2;
+        if ((rc = dev_alloc((void**)&b.t.ent, ne * sizeof(JnEntry), s))) break;
+        if ((rc = dev_alloc((void**)&cnt, ne * 4, s))) break;
+        if ((rc = dev_alloc((void**)&bslot, std::max<int64_t>(nb, 1) * 4, s))) break;
+        if ((rc = dev_alloc((void**)&status, 16, s))) break;
+        PLGPU_HIP(hipMemsetAsync(status, 0, 16, s));
+        const int gi = (int)std::min<int64_t>((ne + 255) / 256, 256 * 32);
+        jn_init_kernel<<<gi, 256, 0, s>>>(b.t.ent, ne, cnt);
+        if (nb > 0) {
+            const int gb = (int)std::min<int64_t>((nb + 255) / 256, 256 * 32);
+            jn_build_kernel<<<gb, 256, 0, s>>>(bk, nb, b.t, nulls_equal, cnt, bslot, status);
+        }
+        PLGPU_HIP(hipGetLastError());
+        unsigned long long st[2];
+        PLGPU_HIP(hipMemcpyAsync(st, status, 16, hipMemcpyDeviceToHost, s));
+        PLGPU_HIP(hipStreamSynchronize(s));
+        if (st[0] == 0) break;
+        if (attempt >= 3) {
+            rc = fail(PLGPU_ERR_CAPACITY, "join build table did not converge");
+            break;
+        }
+        dev_free(b.t.ent, s);
+        dev_free(cnt, s);
+        dev_free(bslot, s);
+        dev_free(status, s);
+        b.t.ent = nullptr;
+        cnt = bslot = nullptr;
+        status = nullptr;
+        bits += 2;
+    }
+    const int64_t ne = b.t.cap + 2;
+    const int64_t nparts = (ne + kScanChunk - 1) / kScanChunk + 1;
+    if (!rc) rc = dev_alloc((void**)&off, (ne + 1) * 8, s);
+    if (!rc) rc = dev_alloc((void**)&part, nparts * 8, s);
+    if (!rc) rc = dev_alloc((void**)&b.t.rows, std::max<int64_t>(nb, 1) * 4, s);
+    if (!rc) {
+        hipError_t e = scan_exclusive<uint32_t>(cnt, ne, off, part, s);
+        if (e != hipSuccess) rc = hip_fail(e, "join build scan");
+    }
+    if (!rc) {
+        const int ge = (int)std::min<int64_t>((ne + 255) / 256, 256 * 32);
+        jn_entries_kernel<<<ge, 256, 0, s>>>(b.t, cnt, off, status);
+        hipError_t e = hipMemsetAsync(cnt, 0, ne * 4, s);  // reused as scatter cursors
+        if (e == hipSuccess && nb > 0) {
+            const int gb = (int)std::min<int64_t>((nb + 255) / 256, 256 * 32);
+            jn_scatter_kernel<<<gb, 256, 0, s>>>(nb, b.t, bslot, cnt);
+            e = hipGetLastError();
+        }
+        unsigned long long st[2] = {0, 0};
+        if (e == hipSuccess) e = hipMemcpyAsync(st, status, 16, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) rc = hip_fail(e, "join build");
+        b.max_count = st[1];
+    }
+    if (!rc && ordered && b.max_count > 1) {
+        // deterministic build-row order inside each duplicate key
+        uint32_t* long_slots = nullptr;
+        unsigned long long* nlong = status;  // reuse word 0
+        rc = dev_alloc((void**)&long_slots, ne * 4, s);
+        if (!rc) {
+            (void)hipMemsetAsync(nlong, 0, 8, s);
+            const int ge = (int)std::min<int64_t>((ne + 255) / 256, 256 * 32);
+            jn_sort_short_kernel<<<ge, 256, 0, s>>>(b.t, long_slots, nlong);
+            unsigned long long nl = 0;
+            hipError_t e = hipMemcpyAsync(&nl, nlong, 8, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e == hipSuccess && nl > 0) {
+                jn_sort_long_kernel<<<(unsigned)nl, 256, 0, s>>>(b.t, long_slots);
+                e = hipGetLastError();
+            }
+            if (e != hipSuccess) rc = hip_fail(e, "join list sort");
+        }
+        dev_free(long_slots, s);
+    }
+    if (!rc) {
+        const int ge = (int)std::min<int64_t>((ne + 255) / 256, 256 * 32);
+        jn_unique_ref_kernel<<<ge, 256, 0, s>>>(b.t);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) rc = hip_fail(e, "join build refs");
+    }
+    dev_free(cnt, s);
+    dev_free(bslot, s);
+    dev_free(off, s);
+    dev_free(part, s);
+    dev_free(status, s);
+    if (rc) {
+        jn_free(b, s);
+        return rc;
+    }
+    b.rows = nb;
+    *out = b;
+    return PLGPU_OK;
+}
+
+// Probe with `key`; pairs (probe row, build row) in probe-row order.
+static int jn_probe(const plgpu_column* key, const JnBuilt& b, bool nulls_equal, plgpu_column* out_p,
+                    plgpu_column* out_b, hipStream_t s) {
+    const int64_t np = key->length;
+    DevCol pk;
+    std::memset(&pk, 0, sizeof pk);
+    pk.dtype = key->dtype;
+    pk.offset = key->offset;
+    pk.values = key->values;
+    pk.validity = key->validity;
+    const int64_t ntiles = std::max<int64_t>(1, (np + kJnTileRows - 1) / kJnTileRows);
+    uint64_t* tcount = nullptr;
+    uint64_t* toff = nullptr;
+    uint64_t* part = nullptr;
+    int rc = dev_alloc((void**)&tcount, ntiles * 8, s);
+    if (!rc) rc = dev_alloc((void**)&toff, (ntiles + 1) * 8, s);
+    if (!rc) rc = dev_alloc((void**)&part, ((ntiles + kScanChunk - 1) / kScanChunk + 1) * 8, s);
+    uint64_t total = 0;
+    const int g = (int)std::min<int64_t>(ntiles, 256 * 16);
+    if (!rc) {
+        jn_probe_count_kernel<<<g, kJnThreads, 0, s>>>(pk, np, b.t, nulls_equal, tcount, ntiles);
+        hipError_t e = hipGetLastError();
+        if (e == hipSuccess) e = scan_exclusive<uint64_t>(tcount, ntiles, toff, part, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(&total, toff + ntiles, 8, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) rc = hip_fail(e, "join probe count");
+    }
+    if (!rc && total >= 0xFFFFFFFFull) rc = fail(PLGPU_ERR_CAPACITY, "join output exceeds the u32 index space");
+    if (!rc) rc = make_owned_column(out_p, PLGPU_U32, (int64_t)total, false, s);
+    if (!rc) rc = make_owned_column(out_b, PLGPU_U32, (int64_t)total, false, s);
+    if (!rc && total > 0) {
+        jn_probe_write_kernel<<<g, kJnThreads, 0, s>>>(pk, np, b.t, nulls_equal, toff, ntiles,
+                                                       (uint32_t*)out_p->values, (uint32_t*)out_b->values);
+        hipError_t e = hipGetLastError();
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) rc = hip_fail(e, "join probe write");
+    }
+    dev_free(tcount, s);
+    dev_free(toff, s);
+    dev_free(part, s);
+    if (rc) {
+        plgpu_column_release(out_p);
+        plgpu_column_release(out_b);
+    }
+    return rc;
+}
+
+static int check_key(const plgpu_column* k) {
+    if (k == nullptr) return fail(PLGPU_ERR_INVALID, "join key is NULL");
+    if (k->dtype != PLGPU_I64 && k->dtype != PLGPU_I32 && k->dtype != PLGPU_U32)
+        return fail(PLGPU_ERR_SCHEMA, "join key must be an integer column (Int64 / Int32 / UInt32)");
+    if (k->length >= 0xFFFFFFFFll) return fail(PLGPU_ERR_CAPACITY, "join side exceeds the u32 index space");
+    return PLGPU_OK;
+}
+
+PLGPU_API int plgpu_join_inner(const plgpu_column* left_key, const plgpu_column* right_key, int32_t nulls_equal,
+                               int32_t maintain_order, int32_t validate, plgpu_column* out_left_idx,
+                               plgpu_column* out_right_idx, void* stream) {
+    hipStream_t s = as_stream(stream);
+    int rc;
+    if ((rc = check_key(left_key)) || (rc = check_key(right_key))) return rc;
+    if (out_left_idx == nullptr || out_right_idx == nullptr) return fail(PLGPU_ERR_INVALID, "NULL output");
+    if (maintain_order < PLGPU_JOIN_ORDER_NONE || maintain_order > PLGPU_JOIN_ORDER_RIGHT_LEFT)
+        return fail(PLGPU_ERR_INVALID, "invalid maintain_order");
+    std::memset(out_left_idx, 0, sizeof *out_left_idx);
+    std::memset(out_right_idx, 0, sizeof *out_right_idx);
+    const bool neq = nulls_equal != 0;
+    // the probe order decides the output order: probe the side whose order
+    // must be kept; otherwise build on the shorter side as the reference does
+    bool build_right;
+    if (maintain_order == PLGPU_JOIN_ORDER_LEFT || maintain_order == PLGPU_JOIN_ORDER_LEFT_RIGHT)
+        build_right = true;
+    else if (maintain_order == PLGPU_JOIN_ORDER_RIGHT || maintain_order == PLGPU_JOIN_ORDER_RIGHT_LEFT)
+        build_right = false;
+    else
+        build_right = right_key->length <= left_key->length;
+    const bool ordered = maintain_order != PLGPU_JOIN_ORDER_NONE;
+    JnBuilt b;
+    rc = jn_build(build_right ? right_key : left_key, neq, ordered, &b, s);
+    if (rc) return rc;
+    // validation (args.rs JoinValidation): "1:m" left unique, "m:1" right
+    // unique, "1:1" both; duplicates of the build side are known from the
+    // table, the probe side needs its own table
+    const bool need_left = validate == PLGPU_JOIN_VALIDATE_1_M || validate == PLGPU_JOIN_VALIDATE_1_1;
+    const bool need_right = validate == PLGPU_JOIN_VALIDATE_M_1 || validate == PLGPU_JOIN_VALIDATE_1_1;
+    auto unique_side = [&](bool right_side, bool* unique) -> int {
+        if (right_side == build_right) {
+            *unique = b.max_count <= 1;
+            return PLGPU_OK;
+        }
+        JnBuilt o;
+        int r2 = jn_build(right_side ? right_key : left_key, neq, false, &o, s);
+        if (r2) return r2;
+        *unique = o.max_count <= 1;
+        jn_free(o, s);
+        return PLGPU_OK;
+    };
+    bool ok = true;
+    if (!rc && need_left) rc = unique_side(false, &ok);
+    if (!rc && !ok) rc = fail(PLGPU_ERR_SCHEMA, "join keys did not fulfill 1:m validation");
+    if (!rc && need_right) rc = unique_side(true, &ok);
+    if (!rc && !ok)
+        rc = fail(PLGPU_ERR_SCHEMA, validate == PLGPU_JOIN_VALIDATE_1_1 ? "join keys did not fulfill 1:1 validation"
+                                                                        : "join keys did not fulfill m:1 validation");
+    if (!rc) {
+        if (build_right) rc = jn_probe(left_key, b, neq, out_left_idx, out_right_idx, s);
+        else rc = jn_probe(right_key, b, neq, out_right_idx, out_left_idx, s);
+    }
+    jn_free(b, s);
+    (void)hipStreamSynchronize(s);
+    return rc;
+}
+
+PLGPU_API int plgpu_gather(const plgpu_column* cols, int32_t ncols, const plgpu_column* idx, plgpu_column* out_cols,
+                           void* stream) {
+    hipStream_t s = as_stream(stream);
+    if (idx == nullptr || (ncols > 0 && (cols == nullptr || out_cols == nullptr)))
+        return fail(PLGPU_ERR_INVALID, "NULL argument");
+    if (idx->dtype != PLGPU_U32) return fail(PLGPU_ERR_SCHEMA, "gather indices must be UInt32");
+    if (idx->validity != nullptr) return fail(PLGPU_ERR_INVALID, "gather indices must not contain nulls");
+    for (int i = 0; i < ncols; ++i) std::memset(&out_cols[i], 0, sizeof(plgpu_column));
+    const uint32_t* ix = (const uint32_t*)idx->values + idx->offset;
+    int rc = PLGPU_OK;
+    for (int i = 0; i < ncols && rc == PLGPU_OK; ++i) rc = gather_into(cols[i], ix, idx->length, &out_cols[i], s);
+    if (rc == PLGPU_OK) {
+        hipError_t e = hipStreamSynchronize(s);
+        if (e != hipSuccess) rc = hip_fail(e, "gather");
+    }
+    if (rc)
+        for (int i = 0; i < ncols; ++i) plgpu_column_release(&out_cols[i]);
+    return rc;
+}

@@ -398,6 +398,14 @@ class DataFrame:
     def filter(self, *predicates: Expr, **constraints: Any) -> "DataFrame":
         return self.lazy().filter(*predicates, **constraints).collect()
 
+    def join(self, other: "DataFrame", on: str | None = None, how: str = "inner", *,
+             left_on: str | None = None, right_on: str | None = None, suffix: str = "_right",
+             validate: str = "m:m", nulls_equal: bool = False, maintain_order: str | None = None) -> "DataFrame":
+        """Eager join (py-polars DataFrame.join): runs the lazy plan."""
+        return self.lazy().join(other.lazy(), on, how, left_on=left_on, right_on=right_on, suffix=suffix,
+                                validate=validate, nulls_equal=nulls_equal,
+                                maintain_order=maintain_order).collect()
+
     def group_by(self, *by: Any, maintain_order: bool = False) -> "GroupBy":
         return GroupBy(self.lazy(), by, maintain_order)
 
@@ -448,6 +456,29 @@ class LazyFrame:
 
     def group_by(self, *by: Any, maintain_order: bool = False) -> "LazyGroupBy":
         return LazyGroupBy(self, by, maintain_order)
+
+    def join(self, other: "LazyFrame", on: str | None = None, how: str = "inner", *,
+             left_on: str | None = None, right_on: str | None = None, suffix: str = "_right",
+             validate: str = "m:m", nulls_equal: bool = False, maintain_order: str | None = None) -> "LazyFrame":
+        """Equi-join on one integer key column (py-polars LazyFrame.join;
+        polars-ops/src/frame/join/args.rs:25 JoinArgs)."""
+        if on is not None:
+            if left_on is not None or right_on is not None:
+                raise ValueError("cannot use 'on' together with 'left_on' / 'right_on'")
+            left_on = right_on = on
+        if left_on is None or right_on is None:
+            raise ValueError("must specify `on` OR `left_on` and `right_on`")
+        for k in (left_on, right_on):
+            if not isinstance(k, str):
+                raise N.InvalidOperationError("the GPU executor joins on exactly one key column")
+        if how != "inner":
+            raise N.InvalidOperationError(f"join how={how!r} is not supported on the GPU executor (inner only)")
+        if validate not in N.JOIN_VALIDATE:
+            raise ValueError(f"invalid `validate` argument {validate!r}")
+        if maintain_order not in N.JOIN_ORDER:
+            raise ValueError(f"invalid `maintain_order` argument {maintain_order!r}")
+        return LazyFrame(("join", self._node, other._node, left_on, right_on, suffix, validate, bool(nulls_equal),
+                          maintain_order))
 
     def select(self, *exprs: Any) -> "LazyFrame":
         return LazyFrame(("select", self._node, _parse_exprs(exprs)))
@@ -503,6 +534,9 @@ def _explain(node: tuple, depth: int = 0) -> str:
         return f"{pad}FILTER {node[2]!r}\n" + _explain(node[1], depth + 1)
     if kind == "group_by":
         return f"{pad}AGGREGATE {node[3]!r} BY {node[2]}\n" + _explain(node[1], depth + 1)
+    if kind == "join":
+        return (f"{pad}INNER JOIN ON {node[3]} = {node[4]}\n" + _explain(node[1], depth + 1) + "\n"
+                + _explain(node[2], depth + 1))
     return f"{pad}{kind.upper()} {node[2]!r}\n" + _explain(node[1], depth + 1)
 
 
@@ -668,10 +702,47 @@ def _group_by(df: DataFrame, key: str, aggs: list[Expr], maintain_order: bool,
     return _gb_frame(g, out_key, out_aggs)
 
 
+def _join(left: DataFrame, right: DataFrame, left_on: str, right_on: str, suffix: str, validate: str,
+          nulls_equal: bool, maintain_order: str | None) -> DataFrame:
+    for df, k in ((left, left_on), (right, right_on)):
+        if k not in df._cols:
+            raise N.ComputeError(f'unable to find column "{k}"; valid columns: {df.columns}')
+    lk, rk = left._cols[left_on], right._cols[right_on]
+    if lk.dtype not in (Int64, Int32, UInt32):
+        raise N.InvalidOperationError(f"join key dtype {lk.dtype} is not supported on the GPU executor (integers)")
+    if lk.dtype is not rk.dtype:
+        raise N.InvalidOperationError(
+            f"join keys must have the same dtype on the GPU executor (got {lk.dtype} and {rk.dtype})")
+    li, ri = N.Column(), N.Column()
+    N.check(N.lib().plgpu_join_inner(C.byref(lk._col), C.byref(rk._col), int(nulls_equal),
+                                     N.JOIN_ORDER[maintain_order], N.JOIN_VALIDATE[validate], C.byref(li),
+                                     C.byref(ri), None))
+    lidx, ridx = Series._from_native("__left_idx", li), Series._from_native("__right_idx", ri)
+
+    def take(df: DataFrame, names: list[str], idx: Series) -> list[Series]:
+        if not names:
+            return []
+        out = (N.Column * builtins.len(names))()
+        N.check(N.lib().plgpu_gather(_col_array([df._cols[n] for n in names]), builtins.len(names),
+                                     C.byref(idx._col), out, None))
+        return [Series._from_native(n, out[i]) for i, n in enumerate(names)]
+
+    lnames = left.columns
+    rnames = [n for n in right.columns if n != right_on]
+    out = take(left, lnames, lidx)
+    for s in take(right, rnames, ridx):
+        if s.name in lnames:
+            s.name = s.name + suffix
+        out.append(s)
+    return DataFrame(out)
+
+
 def _execute(node: tuple, info: dict | None = None) -> DataFrame:
     kind = node[0]
     if kind == "scan":
         return node[1]
+    if kind == "join":
+        return _join(_execute(node[1], info), _execute(node[2], info), *node[3:])
     if kind == "filter":
         df = _execute(node[1], info)
         return _filter(df, node[2])

@@ -190,10 +190,97 @@ def filter_cases():
     return {"cases": cases}
 
 
+# ---------------------------------------------------------------------------
+# 4. Inner joins on one integer key (operations/test_join.py).  Each case:
+#    left / right columns, the join arguments, and what the test asserts:
+#    `expected` rows (as a multiset unless `ordered`), `expected_height`, or
+#    `raises` for a validation error.
+def join_cases():
+    cases = []
+    cases.append({
+        "name": "test_join_negative_integers",
+        "source": "operations/test_join.py:129-151",
+        "left": {"a": [-1, -6, -3, 0]},
+        "right": {"a": [-6, -1, -4, -2, 0], "b": [-6, -1, -4, -2, 0]},
+        "on": "a", "args": {},
+        "expected": {"a": [-6, -1, 0], "b": [-6, -1, 0]}, "ordered": False,
+    })
+    for order, exp in (("left", [2, 1, 1, 1, 1]), ("right", [1, 1, 1, 1, 2])):
+        cases.append({
+            "name": f"test_join_preserve_order_inner[{order}]",
+            "source": "operations/test_join.py:1284-1305",
+            "left": {"a": [None, 2, 1, 1, 5]},
+            "right": {"a": [1, 1, None, 2], "b": [6, 7, 8, 9]},
+            "on": "a", "args": {"maintain_order": order},
+            "expected_column": {"a": exp},
+        })
+    for order in ("none", "left_right", "right_left"):
+        cases.append({
+            "name": f"test_join_null_equal[{order}] with_null",
+            "source": "operations/test_join.py:1916-1931",
+            "left": {"x": [1, None, None], "y": [1, 2, 3]},
+            "right": {"x": [1, None], "z": [1, 2]},
+            "on": "x", "args": {"nulls_equal": True, "maintain_order": order},
+            "expected": {"x": [1, None, None], "y": [1, 2, 3], "z": [1, 2, 2]},
+            "ordered": order != "none",
+        })
+    cases.append({
+        "name": "test_join_null_equal without_null",
+        "source": "operations/test_join.py:1932-1935",
+        "left": {"x": [1, None, None], "y": [1, 2, 3]},
+        "right": {"x": [1, 3], "z": [1, 3]},
+        "on": "x", "args": {"nulls_equal": True},
+        "expected": {"x": [1], "y": [1], "z": [1]}, "ordered": True,
+    })
+    # joining on four identical columns == joining on one of them
+    col = [None if a % 6 == 0 else a for a in range(138)]
+    for neq, h in ((True, 644), (False, 115)):
+        cases.append({
+            "name": f"test_join_4_columns_with_validity[nulls_equal={neq}]",
+            "source": "operations/test_join.py:978-997 (b = c = d = a, so one key is equivalent)",
+            "left": {"a": col}, "right": {"a": col},
+            "on": "a", "args": {"nulls_equal": neq},
+            "expected_height": h,
+        })
+    cases.append({
+        "name": "test_join eager a=foo",
+        "source": "operations/test_join.py:268-279 (integer key columns only)",
+        "left": {"a": [1, 2, 1, 1]}, "right": {"foo": [1, 1, 1]},
+        "left_on": "a", "right_on": "foo", "args": {},
+        "expected_height": 9,
+    })
+    # validation: (unique, duplicate) frames of the test, on "id"
+    frames = {
+        "short_unique": [1, 2, 3, 4], "short_duplicate": [1, 2, 3, 1],
+        "long_unique": [1, 2, 3, 4, 5], "long_duplicate": [1, 2, 3, 1, 5],
+    }
+    for u, d in (("long_unique", "long_duplicate"), ("long_unique", "short_duplicate"),
+                 ("short_unique", "long_duplicate")):
+        for left, right, validate, raises in (
+                (u, d, "1:m", False), (d, u, "1:m", True), (u, d, "1:1", True), (d, u, "1:1", True),
+                (u, d, "m:1", True), (d, u, "m:1", False), (d, u, "m:m", False), (u, d, "m:m", False)):
+            cases.append({
+                "name": f"test_join_validation[{left} x {right}, {validate}]",
+                "source": "operations/test_join.py:713-796",
+                "left": {"id": frames[left]}, "right": {"id": frames[right]},
+                "on": "id", "args": {"validate": validate},
+                "raises": raises,
+            })
+    cases.append({
+        "name": "test_join_empties[inner]",
+        "source": "operations/test_join.py:1079-1084",
+        "left": {"col2": []}, "right": {"col2": []},
+        "on": "col2", "args": {},
+        "expected_height": 0,
+    })
+    return {"cases": cases}
+
+
 def main():
     for name, obj in (("compare_total_order.json", compare_table()),
                       ("group_by_cases.json", group_by_cases()),
-                      ("filter_cases.json", filter_cases())):
+                      ("filter_cases.json", filter_cases()),
+                      ("join_cases.json", join_cases())):
         with open(os.path.join(HERE, name), "w") as f:
             json.dump(obj, f, indent=1, sort_keys=False)
             f.write("\n")

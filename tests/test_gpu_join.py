@@ -1,0 +1,177 @@
+"""GPU parity of the hash inner join and the gather (materialisation)
+through the C-ABI, against the oracle's restatement of
+hash_join_tuples_inner (oracle/polars_oracle.c:or_join_inner) and the
+golden cases of operations/test_join.py.
+
+Bar: bit-exact.  Pair sequences are compared exactly for the ordered modes
+(left / left_right: (left, right) order; right / right_left: (right, left)
+order) and as multisets for maintain_order="none" (unspecified, as in the
+reference).
+"""
+
+import numpy as np
+import pytest
+
+import polaroid_amd as pl
+from conftest import load_golden
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _series(name, vals):
+    dt = pl.Int64
+    return pl.Series(name, vals, dt)
+
+
+def _frame(d):
+    return pl.DataFrame([_series(k, v) for k, v in d.items()])
+
+
+def test_join_golden(gpu):
+    for case in load_golden("join_cases.json")["cases"]:
+        left, right = _frame(case["left"]), _frame(case["right"])
+        kw = dict(case["args"])
+        if "on" in case:
+            kw["on"] = case["on"]
+        else:
+            kw["left_on"], kw["right_on"] = case["left_on"], case["right_on"]
+        if "raises" in case:
+            if case["raises"]:
+                with pytest.raises(pl.ComputeError, match="validation"):
+                    left.join(right, **kw)
+            else:
+                left.join(right, **kw)
+            continue
+        out = left.join(right, **kw)
+        if "expected_height" in case:
+            assert out.height == case["expected_height"], case["name"]
+            continue
+        if "expected_column" in case:
+            (c, exp), = case["expected_column"].items()
+            assert out[c].to_list() == exp, case["name"]
+            continue
+        exp = case["expected"]
+        cols = list(exp)
+        got = list(zip(*[out[c].to_list() for c in cols]))
+        want = list(zip(*[exp[c] for c in cols]))
+        if not case["ordered"]:
+            key = lambda t: tuple((x is None, x if x is not None else 0) for x in t)  # noqa: E731
+            got, want = sorted(got, key=key), sorted(want, key=key)
+        assert got == want, case["name"]
+
+
+def _rand_keys(rng, n, card, null_frac, specials):
+    k = rng.integers(-card // 2, card - card // 2, n).astype(np.int64) * 1_000_003
+    if specials and n:
+        k[rng.random(n) < 0.01] = np.iinfo(np.int64).min
+        k[rng.random(n) < 0.01] = np.iinfo(np.int64).max
+    valid = rng.random(n) >= null_frac
+    return k, valid
+
+
+@pytest.mark.parametrize("nl,nr,card", [(0, 10, 5), (10, 0, 5), (1, 1, 1), (1000, 100, 50), (100, 1000, 50),
+                                        (20000, 5000, 3000), (300001, 40000, 100000), (5000, 4000, 7)])
+@pytest.mark.parametrize("nulls_equal", [False, True])
+@pytest.mark.parametrize("order", ["none", "left", "right", "left_right", "right_left"])
+def test_join_pairs_vs_oracle(gpu, nl, nr, card, nulls_equal, order):
+    rng = np.random.default_rng(nl * 7 + nr + card)
+    lk, lv = _rand_keys(rng, nl, card, 0.05, True)
+    rk, rv = _rand_keys(rng, nr, card, 0.05, True)
+    ol, orr = O.join_inner(O.HostCol(lk, lv), O.HostCol(rk, rv), nulls_equal)
+    left = pl.DataFrame({"k": pl.Series.from_numpy("k", lk, lv), "li": pl.Series.from_numpy("li", np.arange(nl))})
+    right = pl.DataFrame({"k": pl.Series.from_numpy("k", rk, rv), "ri": pl.Series.from_numpy("ri", np.arange(nr))})
+    out = left.join(right, on="k", nulls_equal=nulls_equal, maintain_order=order)
+    gl, gr = out["li"].to_numpy(), out["ri"].to_numpy()
+    gk, kv = out["k"].to_numpy(), out["k"].validity_numpy()
+    assert gl.shape == ol.shape
+    if order in ("right", "right_left"):
+        perm = np.lexsort((ol, orr))
+        ol, orr = ol[perm], orr[perm]
+    if order == "none":
+        a = np.lexsort((gr, gl))
+        gl, gr, gk, kv = gl[a], gr[a], gk[a], kv[a]
+    assert np.array_equal(gl, ol) and np.array_equal(gr, orr)
+    # the output key is the left key of each pair (coalesced), nulls included
+    assert np.array_equal(kv, lv[gl])
+    assert np.array_equal(gk[kv], lk[gl][kv])
+
+
+def test_join_columns_suffix_validity_and_dtypes(gpu):
+    rng = np.random.default_rng(3)
+    n = 5000
+    lk = rng.integers(0, 500, n).astype(np.int32)
+    rk = np.arange(600, dtype=np.int32)[rng.permutation(600)]
+    a = rng.standard_normal(n)
+    va = rng.random(n) > 0.2
+    flag = rng.random(n) > 0.5
+    vflag = rng.random(n) > 0.1
+    b = rng.standard_normal(600)
+    left = pl.DataFrame({"k": pl.Series.from_numpy("k", lk), "v": pl.Series.from_numpy("v", a, va),
+                         "f": pl.Series.from_numpy("f", flag, vflag)})
+    right = pl.DataFrame({"k": pl.Series.from_numpy("k", rk), "v": pl.Series.from_numpy("v", b),
+                          "u": pl.Series.from_numpy("u", rk.astype(np.uint32))})
+    out = left.join(right, on="k", maintain_order="left", validate="m:1")
+    assert out.columns == ["k", "v", "f", "v_right", "u"]
+    assert out["k"].dtype == pl.Int32 and out["u"].dtype == pl.UInt32 and out["f"].dtype == pl.Boolean
+    ol, orr = O.join_inner(O.HostCol(lk.astype(np.int64)), O.HostCol(rk.astype(np.int64)))
+    assert out.height == ol.shape[0]
+    assert np.array_equal(out["v"].validity_numpy(), va[ol])
+    assert np.array_equal(out["v"].to_numpy()[va[ol]], a[ol][va[ol]])
+    assert np.array_equal(out["f"].validity_numpy(), vflag[ol])
+    assert np.array_equal(out["f"].to_numpy()[vflag[ol]], flag[ol][vflag[ol]])
+    assert np.array_equal(out["v_right"].to_numpy(), b[orr])
+    assert np.array_equal(out["u"].to_numpy(), rk[orr].astype(np.uint32))
+    with pytest.raises(pl.ComputeError, match="validation"):
+        left.join(right, on="k", validate="1:1")
+
+
+def test_join_many_duplicates(gpu):
+    """A hot key with a long row list (> the short-list sort) keeps
+    build-row order in the ordered modes."""
+    rng = np.random.default_rng(11)
+    lk = np.concatenate([np.full(3, 7), rng.integers(0, 50, 2000)]).astype(np.int64)
+    rk = np.concatenate([np.full(5000, 7), rng.integers(0, 50, 3000)]).astype(np.int64)
+    rng.shuffle(rk)
+    left = pl.DataFrame({"k": pl.Series.from_numpy("k", lk), "li": pl.Series.from_numpy("li", np.arange(lk.size))})
+    right = pl.DataFrame({"k": pl.Series.from_numpy("k", rk), "ri": pl.Series.from_numpy("ri", np.arange(rk.size))})
+    ol, orr = O.join_inner(O.HostCol(lk), O.HostCol(rk))
+    out = left.join(right, on="k", maintain_order="left_right")
+    assert np.array_equal(out["li"].to_numpy(), ol) and np.array_equal(out["ri"].to_numpy(), orr)
+
+
+def test_join_errors(gpu):
+    left = _frame({"k": [1, 2]})
+    right = _frame({"k": [1]})
+    with pytest.raises(pl.InvalidOperationError):
+        left.join(right, on="k", how="left")
+    with pytest.raises(ValueError):
+        left.join(right)
+    f = pl.DataFrame({"k": pl.Series("k", [1.0], pl.Float64)})
+    with pytest.raises(pl.InvalidOperationError):
+        f.join(f, on="k")
+
+
+@pytest.mark.slow
+def test_join_large_properties(gpu):
+    """1e8 probe rows x 1e6 unique build keys: every probe key matching a
+    build key appears exactly once; the pair count and a checksum of the
+    gathered columns agree with what the construction implies."""
+    import torch
+
+    n, m = 100_000_000, 1_000_000
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5)
+    pk = torch.randint(0, 2 * m, (n,), device="cuda", generator=g, dtype=torch.int64)
+    bk = torch.randperm(2 * m, device="cuda", generator=g)[:m].to(torch.int64)
+    payload = bk * 3 + 1
+    left = pl.DataFrame([pl.Series.from_torch("k", pk)])
+    right = pl.DataFrame([pl.Series.from_torch("k", bk), pl.Series.from_torch("p", payload)])
+    out = left.join(right, on="k")
+    member = torch.zeros(2 * m, dtype=torch.bool, device="cuda")
+    member[bk] = True
+    expect = int(member[pk].sum().item())
+    assert out.height == expect
+    k = torch.from_numpy(out["k"].to_numpy())
+    p = torch.from_numpy(out["p"].to_numpy())
+    assert torch.equal(p, k * 3 + 1)

@@ -153,3 +153,55 @@ def test_baseline_matches_group_by():
     sel = a > 50.0
     assert g == len(np.unique(key[sel]))
     assert abs(chk - (a[sel].sum() + b[sel].sum())) < 1e-6 * chk
+
+
+# ------------------------------------------------------------------ joins
+def _golden_join_pairs(case):
+    lname = case.get("left_on", case.get("on"))
+    rname = case.get("right_on", case.get("on"))
+    lv = case["left"][lname]
+    rv = case["right"][rname]
+    lk = O.HostCol(np.array([0 if v is None else v for v in lv], np.int64), np.array([v is not None for v in lv]))
+    rk = O.HostCol(np.array([0 if v is None else v for v in rv], np.int64), np.array([v is not None for v in rv]))
+    return O.join_inner(lk, rk, case["args"].get("nulls_equal", False))
+
+
+def test_oracle_join_golden():
+    """The oracle's inner join reproduces every join assertion transcribed
+    from operations/test_join.py (tests/golden/join_cases.json)."""
+    for case in load_golden("join_cases.json")["cases"]:
+        li, ri = _golden_join_pairs(case)
+        if "raises" in case:
+            lname = case.get("left_on", case.get("on"))
+            lvals, rvals = case["left"][lname], case["right"][case.get("right_on", lname)]
+            v = case["args"]["validate"]
+            left_unique = len(set(lvals)) == len(lvals)
+            right_unique = len(set(rvals)) == len(rvals)
+            ok = {"m:m": True, "1:m": left_unique, "m:1": right_unique, "1:1": left_unique and right_unique}[v]
+            assert ok != case["raises"], case["name"]
+            continue
+        if "expected_height" in case:
+            assert len(li) == case["expected_height"], case["name"]
+            continue
+        lname = case.get("on")
+        order = case["args"].get("maintain_order")
+        if order in ("right", "right_left"):
+            perm = np.lexsort((li, ri))
+            li, ri = li[perm], ri[perm]
+        rows = []
+        for a, b in zip(li, ri):
+            row = {k: v[a] for k, v in case["left"].items()}
+            row.update({k: v[b] for k, v in case["right"].items() if k != lname})
+            rows.append(row)
+        if "expected_column" in case:
+            (cname, exp), = case["expected_column"].items()
+            assert [r[cname] for r in rows] == exp, case["name"]
+            continue
+        exp = case["expected"]
+        cols = list(exp)
+        got = [tuple(r[c] for c in cols) for r in rows]
+        want = list(zip(*[exp[c] for c in cols]))
+        if not case["ordered"]:
+            key = lambda t: tuple((x is None, x if x is not None else 0) for x in t)  # noqa: E731
+            got, want = sorted(got, key=key), sorted(want, key=key)
+        assert got == want, case["name"]
