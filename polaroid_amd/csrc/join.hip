@@ -38,24 +38,31 @@ constexpr int kJnTileRows = 4096;          // probe tile (16 rows per thread)
 constexpr int kJnProbeLimit = 1 << 16;      // linear-probe bound before "table full"
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
 
-struct JnEntry {
-    uint64_t key;
-    uint32_t ref;  // cnt == 1: the build row; cnt > 1: CSR offset into rows
-    uint32_t cnt;
-};
+// Table: keys[cap] (8 B, EMPTY = INT64_MIN) and ref[cap + 2] (4 B):
+//   ref < 2^31          the single build row of a unique key;
+//   ref == kRefList     duplicate key: rows[off[s] .. off[s + 1]);
+//   ref == kRefNone     no build row (special slots only).
+// Slots cap / cap + 1 are the null key / INT64_MIN key.  For 1e7 build rows
+// keys + ref are 201 MB, inside the 256 MiB Infinity Cache.
+constexpr uint32_t kRefList = 0x80000000u;
+constexpr uint32_t kRefNone = 0xFFFFFFFFu;
 
 struct JnTable {
-    JnEntry* ent;      // cap + 2 entries: [cap] null key, [cap+1] INT64_MIN key
-    uint32_t* rows;    // CSR row lists of duplicate keys
+    uint64_t* keys;
+    uint32_t* ref;
+    uint32_t* off;     // cap + 3 CSR offsets (duplicate keys only)
+    uint32_t* rows;    // CSR row lists
     int bits;
     int64_t cap;
 };
 
+// Slot of `key`, or -1.  Keys are read with plain loads: the table is
+// immutable during the probe.
 __device__ __forceinline__ int64_t jn_find(const JnTable& t, uint64_t key) {
     const uint64_t mask = (uint64_t)t.cap - 1;
     uint64_t s = hash_slot(key, t.bits);
     for (int i = 0; i < kJnProbeLimit; ++i, s = (s + 1) & mask) {
-        const uint64_t k = __hip_atomic_load(&t.ent[s].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t k = t.keys[s];
         if (k == key) return (int64_t)s;
         if (k == kEmptyKey) return -1;
     }
@@ -158,16 +165,15 @@ static hipError_t scan_exclusive(const T* in, int64_t n, uint64_t* out, uint64_t
 }
 
 // ---------------------------------------------------------------- build
-__global__ void jn_init_kernel(JnEntry* ent, int64_t n, uint32_t* cnt) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        ent[i].key = kEmptyKey;
-        ent[i].ref = 0;
-        ent[i].cnt = 0;
+__global__ void jn_init_kernel(JnTable t, uint32_t* cnt) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < t.cap + 2;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        if (i < t.cap) t.keys[i] = kEmptyKey;
         cnt[i] = 0;
     }
 }
 
-// Insert the build keys; bslot[i] = entry of row i (kNoSlot: null key that
+// Insert the build keys; bslot[i] = slot of row i (kNoSlot: a null key that
 // never matches).  status[0] counts rows that found no free slot.
 __global__ void jn_build_kernel(DevCol bk, int64_t nb, JnTable t, bool nulls_equal, uint32_t* __restrict__ cnt,
                                 uint32_t* __restrict__ bslot, unsigned long long* status) {
@@ -184,9 +190,9 @@ __global__ void jn_build_kernel(DevCol bk, int64_t nb, JnTable t, bool nulls_equ
                 slot = -2;
                 uint64_t s = hash_slot(key, t.bits);
                 for (int p = 0; p < kJnProbeLimit; ++p, s = (s + 1) & mask) {
-                    uint64_t k = __hip_atomic_load(&t.ent[s].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    uint64_t k = __hip_atomic_load(&t.keys[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     if (k == kEmptyKey) {
-                        k = atomicCAS((unsigned long long*)&t.ent[s].key, (unsigned long long)kEmptyKey,
+                        k = atomicCAS((unsigned long long*)&t.keys[s], (unsigned long long)kEmptyKey,
                                       (unsigned long long)key);
                         if (k == kEmptyKey) k = key;
                     }
@@ -210,16 +216,19 @@ __global__ void jn_build_kernel(DevCol bk, int64_t nb, JnTable t, bool nulls_equ
     }
 }
 
-// Entries get their CSR offset / count; status[1] = max count.
-__global__ void jn_entries_kernel(JnTable t, const uint32_t* __restrict__ cnt, const uint64_t* __restrict__ off,
+// CSR offsets (u32) and max count (status[1]); ref gets kRefNone / kRefList
+// (unique keys are filled in after the scatter).
+__global__ void jn_offsets_kernel(JnTable t, const uint32_t* __restrict__ cnt, const uint64_t* __restrict__ off64,
                                   unsigned long long* status) {
     uint32_t mx = 0;
-    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < t.cap + 2;
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < t.cap + 3;
          s += (int64_t)gridDim.x * blockDim.x) {
-        const uint32_t c = cnt[s];
-        t.ent[s].cnt = c;
-        t.ent[s].ref = (uint32_t)off[s];
-        mx = c > mx ? c : mx;
+        t.off[s] = (uint32_t)off64[s];
+        if (s < t.cap + 2) {
+            const uint32_t c = cnt[s];
+            t.ref[s] = c == 0 ? kRefNone : kRefList;
+            mx = c > mx ? c : mx;
+        }
     }
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
@@ -229,23 +238,20 @@ __global__ void jn_entries_kernel(JnTable t, const uint32_t* __restrict__ cnt, c
     if ((threadIdx.x & 63) == 0 && mx) atomicMax(&status[1], (unsigned long long)mx);
 }
 
-// Row lists: rows[off[slot] + k] = build row; unique keys store the row in
-// the entry itself.
 __global__ void jn_scatter_kernel(int64_t nb, JnTable t, const uint32_t* __restrict__ bslot,
                                   uint32_t* __restrict__ cursor) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nb; i += (int64_t)gridDim.x * blockDim.x) {
         const uint32_t s = bslot[i];
         if (s == kNoSlot) continue;
-        const JnEntry e = t.ent[s];
         const uint32_t k = atomicAdd(&cursor[s], 1u);
-        t.rows[e.ref + k] = (uint32_t)i;
+        t.rows[t.off[s] + k] = (uint32_t)i;
     }
 }
 
 __global__ void jn_unique_ref_kernel(JnTable t) {
     for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < t.cap + 2;
          s += (int64_t)gridDim.x * blockDim.x) {
-        if (t.ent[s].cnt == 1) t.ent[s].ref = t.rows[t.ent[s].ref];
+        if (t.off[s + 1] - t.off[s] == 1) t.ref[s] = t.rows[t.off[s]];
     }
 }
 
@@ -257,14 +263,14 @@ __global__ void jn_sort_short_kernel(JnTable t, uint32_t* __restrict__ long_slot
                                      unsigned long long* __restrict__ nlong) {
     for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < t.cap + 2;
          s += (int64_t)gridDim.x * blockDim.x) {
-        const uint32_t c = t.ent[s].cnt;
+        const uint32_t c = t.off[s + 1] - t.off[s];
         if (c <= 1) continue;
         if (c > kShortList) {
             const unsigned long long k = atomicAdd(nlong, 1ull);
             long_slots[k] = (uint32_t)s;
             continue;
         }
-        uint32_t* r = t.rows + t.ent[s].ref;
+        uint32_t* r = t.rows + t.off[s];
         for (uint32_t i = 1; i < c; ++i) {
             const uint32_t x = r[i];
             uint32_t j = i;
@@ -279,8 +285,8 @@ __global__ void jn_sort_short_kernel(JnTable t, uint32_t* __restrict__ long_slot
 
 __global__ __launch_bounds__(256) void jn_sort_long_kernel(JnTable t, const uint32_t* __restrict__ long_slots) {
     const uint32_t s = long_slots[blockIdx.x];
-    const uint32_t c = t.ent[s].cnt;
-    uint32_t* r = t.rows + t.ent[s].ref;
+    const uint32_t c = t.off[s + 1] - t.off[s];
+    uint32_t* r = t.rows + t.off[s];
     for (uint32_t phase = 0; phase < c; ++phase) {
         for (uint32_t i = 2 * threadIdx.x + (phase & 1); i + 1 < c; i += 2 * blockDim.x) {
             const uint32_t a = r[i], b = r[i + 1];
@@ -294,32 +300,84 @@ __global__ __launch_bounds__(256) void jn_sort_long_kernel(JnTable t, const uint
 }
 
 // ---------------------------------------------------------------- probe
-__device__ __forceinline__ uint32_t jn_row_matches(const DevCol& pk, int64_t r, const JnTable& t, bool nulls_equal,
-                                                   int64_t& slot) {
-    slot = -1;
-    if (!dev_valid(pk, r)) {
-        if (!nulls_equal) return 0;
-        slot = t.cap;
-    } else {
-        const uint64_t key = dev_load(pk, r);
-        slot = key == kEmptyKey ? t.cap + 1 : jn_find(t, key);
-        if (slot < 0) return 0;
-    }
-    return t.ent[slot].cnt;
-}
-
-__global__ __launch_bounds__(kJnThreads) void jn_probe_count_kernel(DevCol pk, int64_t np, JnTable t,
-                                                                    bool nulls_equal,
+// Pass A: one lookup per probe row -> match word m[r] (the build row, or
+// kRefList | slot for a duplicate key, or kRefNone) and per-tile output
+// counts.  The probe keys are streamed with non-temporal loads so they do
+// not evict the table from the Infinity Cache.
+template <bool NULLABLE>
+__global__ __launch_bounds__(kJnThreads) void jn_probe_match_kernel(DevCol pk, int64_t np, JnTable t,
+                                                                    bool nulls_equal, uint32_t* __restrict__ m,
                                                                     uint64_t* __restrict__ tile_counts,
                                                                     int64_t ntiles) {
     __shared__ uint64_t wsum[kJnThreads / 64];
+    const uint64_t* kp = (const uint64_t*)pk.values + pk.offset;
+    const bool wide = pk.dtype == PLGPU_I64;
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        uint64_t c = 0;
-        for (int k = 0; k < kJnTileRows / kJnThreads; ++k) {
+        constexpr int R = kJnTileRows / kJnThreads;
+        uint64_t key[R];
+        bool valid[R];
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
             const int64_t r = tile * kJnTileRows + (int64_t)k * kJnThreads + threadIdx.x;
-            if (r >= np) break;
-            int64_t slot;
-            c += jn_row_matches(pk, r, t, nulls_equal, slot);
+            valid[k] = r < np;
+            key[k] = 0;
+            if (valid[k]) {
+                key[k] = wide ? __builtin_nontemporal_load(kp + r) : dev_load(pk, r);
+                if (NULLABLE) valid[k] = dev_valid(pk, r) ? true : false;
+            }
+        }
+        // batched first probes: every row's home slot is loaded before any
+        // comparison, so the table reads of the 16 rows overlap
+        int64_t slot[R];
+        uint64_t home[R];
+        const uint64_t mask = (uint64_t)t.cap - 1;
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            slot[k] = (int64_t)hash_slot(key[k], t.bits);
+            home[k] = t.keys[slot[k]];
+        }
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const int64_t r = tile * kJnTileRows + (int64_t)k * kJnThreads + threadIdx.x;
+            if (r >= np || (NULLABLE && !valid[k])) {
+                slot[k] = (r < np && NULLABLE && !valid[k] && nulls_equal) ? t.cap : -1;
+            } else if (key[k] == kEmptyKey) {
+                slot[k] = t.cap + 1;
+            } else if (home[k] == key[k]) {
+                // hit at the home slot
+            } else if (home[k] == kEmptyKey) {
+                slot[k] = -1;
+            } else {
+                // continue the linear probe from the next slot
+                uint64_t sl = ((uint64_t)slot[k] + 1) & mask;
+                slot[k] = -1;
+                for (int i = 1; i < kJnProbeLimit; ++i, sl = (sl + 1) & mask) {
+                    const uint64_t kk = t.keys[sl];
+                    if (kk == key[k]) {
+                        slot[k] = (int64_t)sl;
+                        break;
+                    }
+                    if (kk == kEmptyKey) break;
+                }
+            }
+        }
+        uint32_t ref[R];
+#pragma unroll
+        for (int k = 0; k < R; ++k) ref[k] = slot[k] >= 0 ? t.ref[slot[k]] : kRefNone;
+        uint64_t c = 0;
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const int64_t r = tile * kJnTileRows + (int64_t)k * kJnThreads + threadIdx.x;
+            if (r >= np) continue;
+            uint32_t w = kRefNone;
+            if (ref[k] == kRefList) {
+                w = kRefList | (uint32_t)slot[k];
+                c += t.off[slot[k] + 1] - t.off[slot[k]];
+            } else if (ref[k] != kRefNone) {
+                w = ref[k];
+                c += 1;
+            }
+            __builtin_nontemporal_store(w, m + r);
         }
         uint64_t total;
         (void)block_excl_scan(c, wsum, total);
@@ -327,32 +385,45 @@ __global__ __launch_bounds__(kJnThreads) void jn_probe_count_kernel(DevCol pk, i
     }
 }
 
-// Pairs in probe-row order: within a tile, row r = base + k*T + tid is
+// Pass B: pairs in probe-row order.  Row r = base + k*T + tid of a tile is
 // ranked k*T + tid; one block scan per k.
-__global__ __launch_bounds__(kJnThreads) void jn_probe_write_kernel(DevCol pk, int64_t np, JnTable t,
-                                                                    bool nulls_equal,
-                                                                    const uint64_t* __restrict__ tile_off,
-                                                                    int64_t ntiles, uint32_t* __restrict__ out_p,
-                                                                    uint32_t* __restrict__ out_b) {
+__global__ __launch_bounds__(kJnThreads) void jn_probe_emit_kernel(int64_t np, JnTable t,
+                                                                   const uint32_t* __restrict__ m,
+                                                                   const uint64_t* __restrict__ tile_off,
+                                                                   int64_t ntiles, uint32_t* __restrict__ out_p,
+                                                                   uint32_t* __restrict__ out_b) {
     __shared__ uint64_t wsum[kJnThreads / 64];
+    constexpr int R = kJnTileRows / kJnThreads;
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        uint64_t run = tile_off[tile];
-        for (int k = 0; k < kJnTileRows / kJnThreads; ++k) {
+        uint32_t w[R];
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
             const int64_t r = tile * kJnTileRows + (int64_t)k * kJnThreads + threadIdx.x;
-            int64_t slot = -1;
-            const uint32_t c = r < np ? jn_row_matches(pk, r, t, nulls_equal, slot) : 0u;
+            w[k] = r < np ? __builtin_nontemporal_load(m + r) : kRefNone;
+        }
+        uint64_t run = tile_off[tile];
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const int64_t r = tile * kJnTileRows + (int64_t)k * kJnThreads + threadIdx.x;
+            uint32_t c = 0, lo = 0;
+            if (w[k] != kRefNone) {
+                if (w[k] & kRefList) {
+                    const uint32_t slot = w[k] & ~kRefList;
+                    lo = t.off[slot];
+                    c = t.off[slot + 1] - lo;
+                } else {
+                    c = 1;
+                }
+            }
             uint64_t total;
             const uint64_t pos = run + block_excl_scan(c, wsum, total);
-            if (c) {
-                const JnEntry e = t.ent[slot];
-                if (c == 1) {
-                    out_p[pos] = (uint32_t)r;
-                    out_b[pos] = e.ref;
-                } else {
-                    for (uint32_t j = 0; j < c; ++j) {
-                        out_p[pos + j] = (uint32_t)r;
-                        out_b[pos + j] = t.rows[e.ref + j];
-                    }
+            if (c == 1 && !(w[k] & kRefList)) {
+                out_p[pos] = (uint32_t)r;
+                out_b[pos] = w[k];
+            } else {
+                for (uint32_t j = 0; j < c; ++j) {
+                    out_p[pos + j] = (uint32_t)r;
+                    out_b[pos + j] = t.rows[lo + j];
                 }
             }
             run += total;
@@ -360,24 +431,52 @@ __global__ __launch_bounds__(kJnThreads) void jn_probe_write_kernel(DevCol pk, i
     }
 }
 
+static int num_cus_jn() {
+    static int n = 0;
+    if (n == 0) {
+        int dev = 0;
+        hipDeviceProp_t prop;
+        n = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+                ? prop.multiProcessorCount
+                : 256;
+    }
+    return n;
+}
+
 // --------------------------------------------------------------- gather
 template <int EB>  // element bytes 4 / 8
-__global__ void gather_col_kernel(DevCol c, const uint32_t* __restrict__ idx, int64_t n, void* __restrict__ out,
-                                  uint64_t* __restrict__ out_valid) {
-    for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < n; base += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t o = base + threadIdx.x;
-        bool valid = false;
-        if (o < n) {
-            const int64_t r = idx[o];
-            const int64_t p = c.offset + r;
-            if (EB == 8) ((uint64_t*)out)[o] = ((const uint64_t*)c.values)[p];
-            else ((uint32_t*)out)[o] = ((const uint32_t*)c.values)[p];
-            valid = dev_valid(c, r);
+__global__ __launch_bounds__(256) void gather_col_kernel(DevCol c, const uint32_t* __restrict__ idx, int64_t n,
+                                                         void* __restrict__ out, uint64_t* __restrict__ out_valid) {
+    // 4 outputs per thread (strided by the block), loads issued together
+    constexpr int K = 4;
+    const int64_t step = (int64_t)gridDim.x * blockDim.x * K;
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x * K; base < n; base += step) {
+        uint32_t r[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int64_t o = base + (int64_t)k * blockDim.x + threadIdx.x;
+            r[k] = o < n ? __builtin_nontemporal_load(idx + o) : 0u;
         }
-        if (out_valid) {
-            // blockDim is a multiple of 64 and base of 64: one word per wave
-            const uint64_t w = __ballot(valid);
-            if ((threadIdx.x & 63) == 0 && base + threadIdx.x < n) out_valid[(base + threadIdx.x) >> 6] = w;
+        uint64_t v[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int64_t o = base + (int64_t)k * blockDim.x + threadIdx.x;
+            const int64_t p = c.offset + r[k];
+            v[k] = 0;
+            if (o < n) v[k] = EB == 8 ? ((const uint64_t*)c.values)[p] : ((const uint32_t*)c.values)[p];
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int64_t o = base + (int64_t)k * blockDim.x + threadIdx.x;
+            if (o < n) {
+                if (EB == 8) __builtin_nontemporal_store(v[k], (uint64_t*)out + o);
+                else __builtin_nontemporal_store((uint32_t)v[k], (uint32_t*)out + o);
+            }
+            if (out_valid) {
+                // one validity word per wave and k (o of lane 0 is a multiple of 64)
+                const uint64_t w = __ballot(o < n && dev_valid(c, r[k]));
+                if ((threadIdx.x & 63) == 0 && o < n) out_valid[o >> 6] = w;
+            }
         }
     }
 }
@@ -411,7 +510,7 @@ static int gather_into(const plgpu_column& src, const uint32_t* idx, int64_t n, 
     c.offset = src.offset;
     c.values = src.values;
     c.validity = src.validity;
-    const int g = (int)std::min<int64_t>((n + 255) / 256, 256 * 64);
+    const int g = (int)std::min<int64_t>((n + 1023) / 1024, (int64_t)num_cus_jn() * 16);
     uint64_t* ov = (uint64_t*)out->validity;
     if (src.dtype == PLGPU_BOOL)
         gather_bool_kernel<<<g, 256, 0, s>>>(c, idx, n, (uint64_t*)out->values, ov);
@@ -443,40 +542,45 @@ struct JnBuilt {
 };
 
 static void jn_free(JnBuilt& b, hipStream_t s) {
-    dev_free(b.t.ent, s);
+    dev_free(b.t.keys, s);
+    dev_free(b.t.ref, s);
+    dev_free(b.t.off, s);
     dev_free(b.t.rows, s);
-    b.t.ent = nullptr;
-    b.t.rows = nullptr;
+    std::memset(&b.t, 0, sizeof b.t);
+}
+
+static DevCol as_dev(const plgpu_column* c) {
+    DevCol d;
+    std::memset(&d, 0, sizeof d);
+    d.dtype = c->dtype;
+    d.offset = c->offset;
+    d.values = c->values;
+    d.validity = c->validity;
+    return d;
 }
 
 // Build the table over `key` (rows [0, n)); sorted row lists if `ordered`.
 static int jn_build(const plgpu_column* key, bool nulls_equal, bool ordered, JnBuilt* out, hipStream_t s) {
     const int64_t nb = key->length;
-    DevCol bk;
-    std::memset(&bk, 0, sizeof bk);
-    bk.dtype = key->dtype;
-    bk.offset = key->offset;
-    bk.values = key->values;
-    bk.validity = key->validity;
+    const DevCol bk = as_dev(key);
     int bits = std::max(10, log2_ceil64((nb * 5 + 2) / 3));  // load <= 0.6
     uint32_t* cnt = nullptr;
     uint32_t* bslot = nullptr;
-    uint64_t* off = nullptr;
+    uint64_t* off64 = nullptr;
     uint64_t* part = nullptr;
     unsigned long long* status = nullptr;
-    int rc = PLGPU_OK;
+    int rc = dev_alloc((void**)&status, 16, s);
+    if (!rc) rc = dev_alloc((void**)&bslot, std::max<int64_t>(nb, 1) * 4, s);
     JnBuilt b;
-    for (int attempt = 0;; ++attempt) {
+    for (int attempt = 0; !rc; ++attempt) {
         b.t.bits = bits;
         b.t.cap = int64_t(1) << bits;
         const int64_t ne = b.t.cap + 2;
-        if ((rc = dev_alloc((void**)&b.t.ent, ne * sizeof(JnEntry), s))) break;
+        if ((rc = dev_alloc((void**)&b.t.keys, b.t.cap * 8, s))) break;
         if ((rc = dev_alloc((void**)&cnt, ne * 4, s))) break;
-        if ((rc = dev_alloc((void**)&bslot, std::max<int64_t>(nb, 1) * 4, s))) break;
-        if ((rc = dev_alloc((void**)&status, 16, s))) break;
         PLGPU_HIP(hipMemsetAsync(status, 0, 16, s));
         const int gi = (int)std::min<int64_t>((ne + 255) / 256, 256 * 32);
-        jn_init_kernel<<<gi, 256, 0, s>>>(b.t.ent, ne, cnt);
+        jn_init_kernel<<<gi, 256, 0, s>>>(b.t, cnt);
         if (nb > 0) {
             const int gb = (int)std::min<int64_t>((nb + 255) / 256, 256 * 32);
             jn_build_kernel<<<gb, 256, 0, s>>>(bk, nb, b.t, nulls_equal, cnt, bslot, status);
@@ -490,28 +594,26 @@ static int jn_build(const plgpu_column* key, bool nulls_equal, bool ordered, JnB
             rc = fail(PLGPU_ERR_CAPACITY, "join build table did not converge");
             break;
         }
-        dev_free(b.t.ent, s);
+        dev_free(b.t.keys, s);
         dev_free(cnt, s);
-        dev_free(bslot, s);
-        dev_free(status, s);
-        b.t.ent = nullptr;
-        cnt = bslot = nullptr;
-        status = nullptr;
+        b.t.keys = nullptr;
+        cnt = nullptr;
         bits += 2;
     }
     const int64_t ne = b.t.cap + 2;
-    const int64_t nparts = (ne + kScanChunk - 1) / kScanChunk + 1;
-    if (!rc) rc = dev_alloc((void**)&off, (ne + 1) * 8, s);
-    if (!rc) rc = dev_alloc((void**)&part, nparts * 8, s);
+    if (!rc) rc = dev_alloc((void**)&b.t.ref, ne * 4, s);
+    if (!rc) rc = dev_alloc((void**)&b.t.off, (ne + 1) * 4, s);
+    if (!rc) rc = dev_alloc((void**)&off64, (ne + 1) * 8, s);
+    if (!rc) rc = dev_alloc((void**)&part, ((ne + kScanChunk - 1) / kScanChunk + 1) * 8, s);
     if (!rc) rc = dev_alloc((void**)&b.t.rows, std::max<int64_t>(nb, 1) * 4, s);
     if (!rc) {
-        hipError_t e = scan_exclusive<uint32_t>(cnt, ne, off, part, s);
-        if (e != hipSuccess) rc = hip_fail(e, "join build scan");
-    }
-    if (!rc) {
-        const int ge = (int)std::min<int64_t>((ne + 255) / 256, 256 * 32);
-        jn_entries_kernel<<<ge, 256, 0, s>>>(b.t, cnt, off, status);
-        hipError_t e = hipMemsetAsync(cnt, 0, ne * 4, s);  // reused as scatter cursors
+        hipError_t e = scan_exclusive<uint32_t>(cnt, ne, off64, part, s);
+        const int ge = (int)std::min<int64_t>((ne + 256) / 256, 256 * 32);
+        if (e == hipSuccess) {
+            jn_offsets_kernel<<<ge, 256, 0, s>>>(b.t, cnt, off64, status);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) e = hipMemsetAsync(cnt, 0, ne * 4, s);  // reused as scatter cursors
         if (e == hipSuccess && nb > 0) {
             const int gb = (int)std::min<int64_t>((nb + 255) / 256, 256 * 32);
             jn_scatter_kernel<<<gb, 256, 0, s>>>(nb, b.t, bslot, cnt);
@@ -551,7 +653,7 @@ static int jn_build(const plgpu_column* key, bool nulls_equal, bool ordered, JnB
     }
     dev_free(cnt, s);
     dev_free(bslot, s);
-    dev_free(off, s);
+    dev_free(off64, s);
     dev_free(part, s);
     dev_free(status, s);
     if (rc) {
@@ -567,42 +669,41 @@ static int jn_build(const plgpu_column* key, bool nulls_equal, bool ordered, JnB
 static int jn_probe(const plgpu_column* key, const JnBuilt& b, bool nulls_equal, plgpu_column* out_p,
                     plgpu_column* out_b, hipStream_t s) {
     const int64_t np = key->length;
-    DevCol pk;
-    std::memset(&pk, 0, sizeof pk);
-    pk.dtype = key->dtype;
-    pk.offset = key->offset;
-    pk.values = key->values;
-    pk.validity = key->validity;
+    const DevCol pk = as_dev(key);
     const int64_t ntiles = std::max<int64_t>(1, (np + kJnTileRows - 1) / kJnTileRows);
     uint64_t* tcount = nullptr;
     uint64_t* toff = nullptr;
     uint64_t* part = nullptr;
+    uint32_t* m = nullptr;
     int rc = dev_alloc((void**)&tcount, ntiles * 8, s);
     if (!rc) rc = dev_alloc((void**)&toff, (ntiles + 1) * 8, s);
     if (!rc) rc = dev_alloc((void**)&part, ((ntiles + kScanChunk - 1) / kScanChunk + 1) * 8, s);
+    if (!rc) rc = dev_alloc((void**)&m, std::max<int64_t>(np, 1) * 4, s);
     uint64_t total = 0;
-    const int g = (int)std::min<int64_t>(ntiles, 256 * 16);
+    const int g = (int)std::min<int64_t>(ntiles, (int64_t)num_cus_jn() * 8);
     if (!rc) {
-        jn_probe_count_kernel<<<g, kJnThreads, 0, s>>>(pk, np, b.t, nulls_equal, tcount, ntiles);
+        if (pk.validity) jn_probe_match_kernel<true><<<g, kJnThreads, 0, s>>>(pk, np, b.t, nulls_equal, m, tcount, ntiles);
+        else jn_probe_match_kernel<false><<<g, kJnThreads, 0, s>>>(pk, np, b.t, nulls_equal, m, tcount, ntiles);
         hipError_t e = hipGetLastError();
         if (e == hipSuccess) e = scan_exclusive<uint64_t>(tcount, ntiles, toff, part, s);
         if (e == hipSuccess) e = hipMemcpyAsync(&total, toff + ntiles, 8, hipMemcpyDeviceToHost, s);
         if (e == hipSuccess) e = hipStreamSynchronize(s);
-        if (e != hipSuccess) rc = hip_fail(e, "join probe count");
+        if (e != hipSuccess) rc = hip_fail(e, "join probe match");
     }
     if (!rc && total >= 0xFFFFFFFFull) rc = fail(PLGPU_ERR_CAPACITY, "join output exceeds the u32 index space");
     if (!rc) rc = make_owned_column(out_p, PLGPU_U32, (int64_t)total, false, s);
     if (!rc) rc = make_owned_column(out_b, PLGPU_U32, (int64_t)total, false, s);
     if (!rc && total > 0) {
-        jn_probe_write_kernel<<<g, kJnThreads, 0, s>>>(pk, np, b.t, nulls_equal, toff, ntiles,
-                                                       (uint32_t*)out_p->values, (uint32_t*)out_b->values);
+        jn_probe_emit_kernel<<<g, kJnThreads, 0, s>>>(np, b.t, m, toff, ntiles, (uint32_t*)out_p->values,
+                                                      (uint32_t*)out_b->values);
         hipError_t e = hipGetLastError();
         if (e == hipSuccess) e = hipStreamSynchronize(s);
-        if (e != hipSuccess) rc = hip_fail(e, "join probe write");
+        if (e != hipSuccess) rc = hip_fail(e, "join probe emit");
     }
     dev_free(tcount, s);
     dev_free(toff, s);
     dev_free(part, s);
+    dev_free(m, s);
     if (rc) {
         plgpu_column_release(out_p);
         plgpu_column_release(out_b);

@@ -1,0 +1,68 @@
+"""Join workload of BASELINE.json configs[3]: 1e9-row probe x 1e7-row build
+hash inner join on an i64 key, one GPU, inputs resident in HBM.
+
+    python tools/bench_join.py [--probe 1e9 --build 1e7 --steps 5 --warmup 1]
+
+A step = `probe.join(build, on="k")` materialised: the build table, the
+ordered probe and the gather of k, the probe payload and the build payload.
+Build keys are a random 1e7-subset of [0, 2e7); probe keys are uniform on
+[0, 2e7), so half of the probe rows match exactly one build row.
+Prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--probe", type=float, default=1e9)
+    ap.add_argument("--build", type=float, default=1e7)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    args = ap.parse_args()
+    import torch
+
+    import polaroid_amd as pl
+
+    n, m = int(args.probe), int(args.build)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(7)
+    pk = torch.empty(n, dtype=torch.int64, device="cuda")
+    pv = torch.empty(n, dtype=torch.float64, device="cuda")
+    chunk = 1 << 27
+    for s in range(0, n, chunk):
+        e = min(n, s + chunk)
+        pk[s:e] = torch.randint(0, 2 * m, (e - s,), device="cuda", generator=g)
+        pv[s:e] = torch.rand(e - s, device="cuda", generator=g, dtype=torch.float64)
+    bk = torch.randperm(2 * m, device="cuda", generator=g)[:m].to(torch.int64)
+    bv = torch.rand(m, device="cuda", generator=g, dtype=torch.float64)
+    probe = pl.DataFrame([pl.Series.from_torch("k", pk), pl.Series.from_torch("pv", pv)])
+    build = pl.DataFrame([pl.Series.from_torch("k", bk), pl.Series.from_torch("bv", bv)])
+    out = None
+    for _ in range(args.warmup):
+        out = probe.join(build, on="k")
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = probe.join(build, on="k")
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / args.steps
+    rows_out = out.height
+    print(json.dumps({
+        "metric": "Mrows/sec hash inner-join probe (1e9 probe x 1e7 build, i64 key), materialised",
+        "value": round(n / dt / 1e6, 1), "unit": "Mrows/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True,
+        "dtype": "int64", "data": "synthetic keys/payloads generated on device",
+        "config": {"workload": "probe.join(build, on='k') inner, output k, pv, bv", "probe_rows": n,
+                   "build_rows": m, "output_rows": rows_out},
+    }), flush=True)
+
+
+if __name__ == "__main__":
+    main()
