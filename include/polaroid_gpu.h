@@ -299,6 +299,29 @@ int plgpu_join_inner(const plgpu_column* left_key, const plgpu_column* right_key
 int plgpu_gather(const plgpu_column* cols, int32_t ncols, const plgpu_column* idx,
                  plgpu_column* out_cols, void* stream);
 
+/* ---- sort ------------------------------------------------------------------
+ * Stable arg-sort of one column (I64 / I32 / U32 / F64) into a UInt32
+ * permutation: TotalOrd order (NaN greatest, -0.0 == 0.0), descending
+ * reverses the order of distinct values while equal values keep their row
+ * order, nulls first unless nulls_last.  Replaces
+ * polars-core/src/chunked_array/ops/sort/arg_sort.rs arg_sort with
+ * SortOptions { maintain_order: true } (options.rs:32); DataFrame.sort is
+ * this permutation followed by plgpu_gather. */
+int plgpu_arg_sort(const plgpu_column* key, int32_t descending, int32_t nulls_last,
+                   plgpu_column* out_idx, void* stream);
+
+/* ---- rolling windows ---------------------------------------------------------
+ * Fixed-size window sum / mean (window_size rows, min_periods non-null rows
+ * for a valid output, optionally centred), like Series.rolling_sum /
+ * rolling_mean.  Float64 (and integer mean) results are the correctly
+ * rounded window sums (divided by the non-null count); integer sums wrap.
+ * Replaces polars-compute/src/rolling/no_nulls/{sum,mean}.rs rolling_sum /
+ * rolling_mean and nulls/{sum,mean}.rs (rolling/sum.rs:7 SumWindow). */
+enum plgpu_rolling_kind { PLGPU_ROLLING_SUM = 1, PLGPU_ROLLING_MEAN = 2 };
+
+int plgpu_rolling(const plgpu_column* values, int32_t kind, int64_t window_size,
+                  int64_t min_periods, int32_t center, plgpu_column* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

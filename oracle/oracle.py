@@ -59,6 +59,11 @@ def lib():
         L.or_group_by_agg.restype = C.c_int64
         L.or_join_inner.restype = C.c_int64
         L.or_join_inner.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int64, C.c_void_p, C.c_void_p]
+        L.or_arg_sort.restype = None
+        L.or_arg_sort.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p]
+        L.or_rolling.restype = None
+        L.or_rolling.argtypes = [C.c_void_p, C.c_int32, C.c_int64, C.c_int64, C.c_int32, C.c_int32, C.c_void_p,
+                                 C.c_void_p, C.c_void_p]
         L.or_fsum.restype = C.c_double
         L.or_fsum.argtypes = [C.c_void_p, C.c_int64]
         L.or_baseline_filter_groupby_sum.restype = C.c_int64
@@ -200,6 +205,32 @@ def join_inner(left: HostCol, right: HostCol, nulls_equal: bool = False):
         if n >= 0:
             return ol[:n].copy(), orr[:n].copy()
         cap *= 4
+
+
+def arg_sort(col: HostCol, descending: bool = False, nulls_last: bool = False) -> np.ndarray:
+    out = np.zeros(max(col.c.length, 1), np.int64)
+    lib().or_arg_sort(C.byref(col.c), int(descending), int(nulls_last), out.ctypes.data)
+    return out[: col.c.length].copy()
+
+
+ROLLING_REFERENCE, ROLLING_EXACT = 0, 1
+
+
+def rolling(col: HostCol, kind: str, window_size: int, min_periods: int | None = None, center: bool = False,
+            mode: int = ROLLING_REFERENCE):
+    """rolling_sum / rolling_mean -> (values, valid).  mode 0 restates the
+    reference's Kahan sliding window; mode 1 is the exact window sum."""
+    n = col.c.length
+    mp = window_size if min_periods is None else min_periods
+    k = {"sum": 1, "mean": 2}[kind]
+    of = np.zeros(max(n, 1), np.float64)
+    oi = np.zeros(max(n, 1), np.int64)
+    ov = np.zeros(max(n, 1), np.uint8)
+    lib().or_rolling(C.byref(col.c), k, window_size, mp, int(center), mode, of.ctypes.data, oi.ctypes.data,
+                     ov.ctypes.data)
+    isint = k == 1 and col.code != F64
+    vals = (oi if isint else of)[:n].copy()
+    return vals, ov[:n].astype(bool)
 
 
 def fsum(x: np.ndarray) -> float:

@@ -767,3 +767,217 @@ OR_EXPORT int64_t or_join_inner(const plgpu_column* lk, const plgpu_column* rk, 
     free(t);
     return n;
 }
+
+/* ------------------------------------------------------------------ sort
+ * polars-core/src/chunked_array/ops/sort/arg_sort.rs:7 sort_impl: a stable
+ * sort of (idx, value) pairs by TotalOrd (total_ord.rs: NaN == NaN and
+ * greatest, -0.0 == 0.0); descending reverses the comparator (equal values
+ * keep their order); nulls are placed first, or last with nulls_last, in row
+ * order.  Restated as a comparison sort with the row index as tie-break. */
+typedef struct {
+    const plgpu_column* c;
+    int descending;
+} srt_ctx;
+static srt_ctx g_srt;
+
+static int srt_cmp_val(int64_t a, int64_t b) {
+    const plgpu_column* c = g_srt.c;
+    if (c->dtype == PLGPU_F64) {
+        const double x = ((const double*)c->values)[c->offset + a];
+        const double y = ((const double*)c->values)[c->offset + b];
+        const int xn = isnan(x), yn = isnan(y);
+        if (xn || yn) return xn == yn ? 0 : (xn ? 1 : -1);
+        return x < y ? -1 : (x > y ? 1 : 0); /* -0.0 == 0.0 */
+    }
+    const int64_t x = col_int(c, a), y = col_int(c, b);
+    return x < y ? -1 : (x > y ? 1 : 0);
+}
+
+static int srt_cmp(const void* pa, const void* pb) {
+    const int64_t a = *(const int64_t*)pa, b = *(const int64_t*)pb;
+    int r = srt_cmp_val(a, b);
+    if (g_srt.descending) r = -r;
+    if (r) return r;
+    return a < b ? -1 : (a > b ? 1 : 0);
+}
+
+OR_EXPORT void or_arg_sort(const plgpu_column* c, int32_t descending, int32_t nulls_last, int64_t* out) {
+    const int64_t n = c->length;
+    int64_t* v = (int64_t*)malloc(sizeof(int64_t) * (size_t)(n > 0 ? n : 1));
+    int64_t nv = 0, nn = 0;
+    for (int64_t r = 0; r < n; ++r)
+        if (col_valid(c, r)) v[nv++] = r;
+    g_srt.c = c;
+    g_srt.descending = descending;
+    qsort(v, (size_t)nv, sizeof(int64_t), srt_cmp);
+    nn = n - nv;
+    int64_t* dv = nulls_last ? out : out + nn;
+    int64_t* dn = nulls_last ? out + nv : out;
+    memcpy(dv, v, sizeof(int64_t) * (size_t)nv);
+    int64_t k = 0;
+    for (int64_t r = 0; r < n; ++r)
+        if (!col_valid(c, r)) dn[k++] = r;
+    free(v);
+}
+
+/* --------------------------------------------------------------- rolling
+ * polars-compute/src/rolling/sum.rs:7 SumWindow: Kahan add of values
+ * entering the window (err_add) and Kahan subtract of values leaving it
+ * (err_sub), non-finite values counted apart (finalize: only +inf -> +inf,
+ * only -inf -> -inf, else NaN); update() resets when the new window does not
+ * overlap the last one.  mean.rs:6 MeanWindow: sum / (len - null_count).
+ * Drivers: no_nulls/mod.rs:43 (windows shorter than min_periods are skipped
+ * without updating) and nulls/mod.rs:38 (every window updated, valid iff
+ * non-null count >= min_periods); bounds mod.rs:68 det_offsets / :71
+ * det_offsets_center.  mode 0 restates that arithmetic exactly; mode 1 is
+ * the exact window sum (math.fsum of the finite values) used to pin the GPU
+ * bit for bit. */
+typedef struct {
+    double sum, err_add, err_sub;
+    int64_t isum;
+    int64_t nonfinite, pinf, ninf, null_count, last_start, last_end;
+} sw_t;
+
+static void sw_reset(sw_t* w) {
+    w->sum = w->err_add = w->err_sub = 0.0;
+    w->isum = 0;
+    w->nonfinite = w->pinf = w->ninf = w->null_count = 0;
+}
+
+static double rl_val(const plgpu_column* c, int64_t r) {
+    if (c->dtype == PLGPU_F64) return ((const double*)c->values)[c->offset + r];
+    return (double)col_int(c, r);
+}
+
+static void sw_add(sw_t* w, const plgpu_column* c, int64_t r, int isint) {
+    if (isint) {
+        w->isum = (int64_t)((uint64_t)w->isum + (uint64_t)col_int(c, r));
+        return;
+    }
+    const double v = rl_val(c, r);
+    if (isfinite(v)) {
+        const double y = v - w->err_add;
+        const double ns = w->sum + y;
+        w->err_add = (ns - w->sum) - y;
+        w->sum = ns;
+    } else {
+        w->nonfinite += 1;
+        w->pinf += v > 0.0;
+        w->ninf += v < 0.0;
+    }
+}
+
+static void sw_sub(sw_t* w, const plgpu_column* c, int64_t r, int isint) {
+    if (isint) {
+        w->isum = (int64_t)((uint64_t)w->isum - (uint64_t)col_int(c, r));
+        return;
+    }
+    const double v = rl_val(c, r);
+    if (isfinite(v)) {
+        const double val = 0.0 - v;
+        const double y = val - w->err_sub;
+        const double ns = w->sum + y;
+        w->err_sub = (ns - w->sum) - y;
+        w->sum = ns;
+    } else {
+        w->nonfinite -= 1;
+        w->pinf -= v > 0.0;
+        w->ninf -= v < 0.0;
+    }
+}
+
+static double sw_update(sw_t* w, const plgpu_column* c, int64_t s, int64_t e, int isint) {
+    if (s >= w->last_end) {
+        sw_reset(w);
+        w->last_start = s;
+        w->last_end = s;
+    }
+    for (int64_t r = w->last_start; r < s; ++r) {
+        if (col_valid(c, r)) sw_sub(w, c, r, isint);
+        else w->null_count -= 1;
+    }
+    for (int64_t r = w->last_end; r < e; ++r) {
+        if (col_valid(c, r)) sw_add(w, c, r, isint);
+        else w->null_count += 1;
+    }
+    w->last_start = s;
+    w->last_end = e;
+    if (w->nonfinite == 0) return w->sum;
+    if (w->nonfinite == w->pinf) return INFINITY;
+    if (w->nonfinite == w->ninf) return -INFINITY;
+    return NAN;
+}
+
+static void rl_offsets(int64_t i, int64_t ws, int64_t n, int center, int64_t* s, int64_t* e) {
+    if (center) {
+        const int64_t right = (ws + 1) / 2;
+        const int64_t left = ws - right;
+        *s = i > left ? i - left : 0;
+        *e = i + right < n ? i + right : n;
+    } else {
+        *s = i + 1 > ws ? i + 1 - ws : 0;
+        *e = i + 1;
+    }
+}
+
+/* kind 1 sum / 2 mean; out_f64 or out_i64 (integer sums); out_valid bytes. */
+OR_EXPORT void or_rolling(const plgpu_column* c, int32_t kind, int64_t ws, int64_t min_periods, int32_t center,
+                          int32_t mode, double* out_f64, int64_t* out_i64, uint8_t* out_valid) {
+    const int64_t n = c->length;
+    const int isint = kind == 1 && c->dtype != PLGPU_F64;
+    int has_nulls = 0;
+    for (int64_t r = 0; r < n && !has_nulls; ++r) has_nulls = !col_valid(c, r);
+    sw_t w;
+    memset(&w, 0, sizeof w);
+    for (int64_t i = 0; i < n; ++i) {
+        int64_t s, e;
+        rl_offsets(i, ws, n, center, &s, &e);
+        double v = 0.0;
+        int valid;
+        int64_t nn = 0;
+        if (mode == 0) {
+            if (!has_nulls && e - s < min_periods) {
+                out_valid[i] = 0;
+                if (isint) out_i64[i] = 0;
+                else out_f64[i] = 0.0;
+                continue;
+            }
+            v = sw_update(&w, c, s, e, isint);
+            nn = (e - s) - w.null_count;
+            valid = nn >= min_periods;
+        } else {
+            /* exact: fsum of the finite non-null values, specials by count */
+            double* buf = (double*)malloc(sizeof(double) * (size_t)(e - s > 0 ? e - s : 1));
+            int64_t m = 0, pinf = 0, ninf = 0, nan = 0;
+            uint64_t isum = 0;
+            for (int64_t r = s; r < e; ++r) {
+                if (!col_valid(c, r)) continue;
+                ++nn;
+                if (isint) {
+                    isum += (uint64_t)col_int(c, r);
+                    continue;
+                }
+                const double x = rl_val(c, r);
+                if (isnan(x)) ++nan;
+                else if (isinf(x)) (x > 0 ? ++pinf : ++ninf);
+                else buf[m++] = x;
+            }
+            v = or_fsum(buf, m);
+            free(buf);
+            if (nan || (pinf && ninf)) v = NAN;
+            else if (pinf) v = INFINITY;
+            else if (ninf) v = -INFINITY;
+            w.isum = (int64_t)isum;
+            valid = nn >= min_periods && e > s;
+        }
+        if (kind == 2) {
+            if (nn == 0) valid = 0;
+            else v = v / (double)nn;
+        }
+        out_valid[i] = (uint8_t)valid;
+        /* SumWindow<i32, i32> wraps in 32 bits */
+        if (isint && c->dtype == PLGPU_I32) w.isum = (int64_t)(int32_t)(uint32_t)(uint64_t)w.isum;
+        if (isint) out_i64[i] = valid ? w.isum : 0;
+        else out_f64[i] = valid ? v : 0.0;
+    }
+}

@@ -120,11 +120,14 @@ SIGNATURES = {
                                  C.POINTER(GroupByInfo), _P]),
     "plgpu_join_inner": (C.c_int, [_COLP, _COLP, C.c_int32, C.c_int32, C.c_int32, _COLP, _COLP, _P]),
     "plgpu_gather": (C.c_int, [_COLP, C.c_int32, _COLP, _COLP, _P]),
+    "plgpu_arg_sort": (C.c_int, [_COLP, C.c_int32, C.c_int32, _COLP, _P]),
+    "plgpu_rolling": (C.c_int, [_COLP, C.c_int32, C.c_int64, C.c_int64, C.c_int32, _COLP, _P]),
 }
 
 GB_MAX_ACC = 6
 JOIN_ORDER = {None: 0, "none": 0, "left": 1, "right": 2, "left_right": 3, "right_left": 4}
 JOIN_VALIDATE = {"m:m": 0, "1:m": 1, "m:1": 2, "1:1": 3}
+ROLLING = {"sum": 1, "mean": 2}
 
 _lib = None
 

@@ -42,7 +42,6 @@ constexpr int kMaxAcc = 6;
 constexpr int kMaxFields = 48;
 constexpr int kLdsProbe = 16;
 constexpr int kGlobalProbe = 4096;
-constexpr int kSumWindowBits = 120;   // fixed-point window of one value
 constexpr int kLimb2Margin = 4;
 constexpr int kGridRounds = 8;        // fast kernel grid = rounds x resident workgroups       // binades below the smallest sampled exponent kept by 2 limbs
 constexpr int kHeadroomBinades = 8;   // above the sampled max exponent
@@ -157,60 +156,6 @@ __device__ __forceinline__ int64_t g_find(const GbParams& p, uint64_t key) {
     return -1;
 }
 
-// f64 bits -> three carry-free 40-bit limbs of the fixed-point value
-// x / 2^bottom (rounded half-even below the window).  Returns false for
-// zero / rounded-away values; sets FX overflow (1) / inexact (2) in fl.
-template <int WBITS = kSumWindowBits>
-__device__ __forceinline__ bool fx_limbs(uint64_t b, int bottom, uint64_t& l0, uint64_t& l1, uint64_t& l2,
-                                         uint32_t& fl, uint32_t& ex_out) {
-    uint32_t ex = (uint32_t)(b >> 52) & 0x7FF;
-    uint64_t m = b & 0x000FFFFFFFFFFFFFull;
-    if (ex == 0) {
-        if (m == 0) return false;
-        ex = 1;
-    } else {
-        m |= 0x0010000000000000ull;
-    }
-    ex_out = ex;
-    const int sh = (int)ex - 1075 - bottom;
-    unsigned __int128 F;
-    if (sh >= 0) {
-        if (sh > WBITS - 53) {
-            fl |= 1u;
-            return false;
-        }
-        F = (unsigned __int128)m << sh;
-    } else {
-        const int k = -sh;
-        if (k > 53) {
-            fl |= 2u;
-            return false;
-        }
-        uint64_t q = m >> k;
-        const uint64_t rem = m & ((1ull << k) - 1);
-        const uint64_t half = 1ull << (k - 1);
-        if (rem) fl |= 2u;
-        if (rem > half || (rem == half && (q & 1))) ++q;
-        if (q == 0) return false;
-        F = q;
-    }
-    constexpr uint64_t M40 = (1ull << 40) - 1;
-    l0 = (uint64_t)F & M40;
-    if (WBITS > 80) {
-        l1 = (uint64_t)(F >> 40) & M40;
-        l2 = (uint64_t)(F >> 80);
-    } else {
-        l1 = (uint64_t)(F >> 40);
-        l2 = 0;
-    }
-    if (b >> 63) {
-        l0 = 0ull - l0;
-        l1 = 0ull - l1;
-        l2 = 0ull - l2;
-    }
-    return true;
-}
-
 // Branch-free conversion for the common case: a finite value whose bits all
 // fall inside the window (no rounding, no overflow), or zero.  LIMBS 3: the
 // 120-bit window at `bottom`; LIMBS 2: its top 80 bits (bottom + 40), limbs
@@ -244,21 +189,6 @@ __device__ __forceinline__ bool fx_limbs_fast(uint64_t x, int bottom, uint64_t& 
         l2 = 0;
     }
     return inrange || zero;
-}
-
-// Signed limb sums -> 192-bit two's complement words.
-__device__ __forceinline__ void limbs_to_192(int64_t L0, int64_t L1, int64_t L2, uint64_t& w0, uint64_t& w1,
-                                             uint64_t& w2) {
-    const __int128 A = (__int128)L0 + ((__int128)L1 << 40);
-    const uint64_t a0 = (uint64_t)A;
-    const uint64_t a1 = (uint64_t)(A >> 64);
-    const uint64_t a2 = A < 0 ? ~0ull : 0ull;
-    const uint64_t b1 = (uint64_t)L2 << 16;
-    const uint64_t b2 = (uint64_t)(L2 >> 48);
-    w0 = a0;
-    w1 = a1 + b1;
-    const uint64_t c = w1 < a1 ? 1ull : 0ull;
-    w2 = a2 + b2 + c;
 }
 
 // Exact 192-bit atomic accumulate (mod 2^192) with explicit carries.
@@ -1077,59 +1007,6 @@ __global__ void gb_init_table_kernel(uint64_t* gtab, int64_t words_per_field, in
 }
 
 // 192-bit two's complement * 2^bottom -> correctly rounded double.
-__device__ double fx_to_double(uint64_t w0, uint64_t w1, uint64_t w2, int bottom) {
-    const bool neg = (int64_t)w2 < 0;
-    if (neg) {
-        w0 = ~w0; w1 = ~w1; w2 = ~w2;
-        w0 += 1;
-        const uint64_t c0 = w0 == 0;
-        w1 += c0;
-        const uint64_t c1 = c0 && w1 == 0;
-        w2 += c1;
-    }
-    if ((w0 | w1 | w2) == 0) return 0.0;
-    int p;
-    if (w2) p = 128 + 63 - __clzll(w2);
-    else if (w1) p = 64 + 63 - __clzll(w1);
-    else p = 63 - __clzll(w0);
-    uint64_t mant;
-    int e = bottom;
-    if (p <= 52) {
-        mant = w0;
-    } else {
-        const int sh = p - 52;
-        // mant = (W >> sh) & (2^53 - 1 | 2^52)
-        auto shr = [&](int k) -> uint64_t {  // low 64 bits of W >> k
-            if (k >= 128) return w2 >> (k - 128);
-            if (k >= 64) {
-                const int j = k - 64;
-                return j == 0 ? w1 : (w1 >> j) | (w2 << (64 - j));
-            }
-            return k == 0 ? w0 : (w0 >> k) | (w1 << (64 - k));
-        };
-        mant = shr(sh) & ((1ull << 53) - 1);
-        const uint64_t halfbit = (shr(sh - 1) & 1ull);
-        // sticky: any bit below sh - 1
-        bool sticky = false;
-        const int sb = sh - 1;  // bits [0, sb) must be checked
-        if (sb > 0) {
-            if (sb >= 128) sticky = w0 || w1 || (sb > 128 && (w2 & ((sb - 128 >= 64) ? ~0ull : ((1ull << (sb - 128)) - 1))));
-            else if (sb >= 64) sticky = w0 || (w1 & ((sb - 64 == 0) ? 0ull : ((1ull << (sb - 64)) - 1)));
-            else sticky = (w0 & ((1ull << sb) - 1)) != 0;
-        }
-        if (halfbit && (sticky || (mant & 1))) {
-            ++mant;
-            if (mant == (1ull << 53)) {
-                mant >>= 1;
-                ++e;
-            }
-        }
-        e += sh;
-    }
-    const double r = ldexp((double)mant, e);
-    return neg ? -r : r;
-}
-
 struct OutSpec {
     int32_t kind;
     int32_t acc;

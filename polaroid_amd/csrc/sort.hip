@@ -1,0 +1,354 @@
+// Stable LSD radix arg-sort of one column (the sort_by / arg_sort hot path).
+//
+// Reference (paths under /root/reference/crates):
+//   polars-core/src/chunked_array/ops/sort/arg_sort.rs:7 sort_impl /
+//     arg_sort: stable sort of (idx, value) pairs by TotalOrd
+//     (polars-utils/src/total_ord.rs: NaN == NaN and greatest, -0.0 == 0.0),
+//     descending by a reversed comparator (equal values keep their order),
+//     nulls gathered first or last (SortOptions, options.rs:32);
+//   DataFrame::sort -> arg_sort then take (gather.rs).
+//
+// MI355X design:
+//   prep     - nulls are split off in order; keys become order-preserving
+//              u64 codes (descending = complement), carried with u32 row ids;
+//   histo    - one read of the codes gives all 8 byte histograms, so bytes
+//              that are constant over the column cost no pass;
+//   per pass - upsweep (per-tile digit counts) -> device scan (digit-major)
+//              -> downsweep: a tile of 4096 codes is ranked stably in LDS
+//              (wave64 ballot peer masks per digit) and written out in
+//              digit runs, so global writes are coalesced.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+
+#include "plgpu_internal.hpp"
+#include "scan.hpp"
+
+namespace plgpu {
+
+constexpr int kSrtThreads = 256;
+constexpr int kSrtPer = 16;
+constexpr int kSrtTile = kSrtThreads * kSrtPer;  // 4096 codes per tile
+
+__device__ __forceinline__ uint64_t sort_code(const DevCol& c, int64_t r, bool descending) {
+    uint64_t b = dev_load(c, r);
+    uint64_t k;
+    if (c.dtype == PLGPU_F64) {
+        if ((b & 0x7fffffffffffffffull) == 0) b = 0;                      // -0.0 == 0.0
+        else if ((b & 0x7fffffffffffffffull) > 0x7ff0000000000000ull) b = 0x7ff8000000000000ull;  // one NaN
+        k = ord_f64(b);
+    } else if (c.dtype == PLGPU_U32) {
+        k = b;
+    } else if (c.dtype == PLGPU_I32) {
+        k = (uint64_t)((uint32_t)b ^ 0x80000000u);  // upper bytes constant: their passes are skipped
+    } else {
+        k = b ^ 0x8000000000000000ull;  // I64 / I32 (sign-extended)
+    }
+    return descending ? ~k : k;
+}
+
+// Per 1024-row block: valid-row counts (for the null split).
+__global__ __launch_bounds__(256) void srt_count_valid_kernel(DevCol c, int64_t n, uint32_t* __restrict__ cnt) {
+    __shared__ uint32_t s;
+    const int64_t base = (int64_t)blockIdx.x * 1024;
+    if (threadIdx.x == 0) s = 0;
+    __syncthreads();
+    uint32_t v = 0;
+    for (int k = 0; k < 4; ++k) {
+        const int64_t r = base + k * 256 + threadIdx.x;
+        v += (r < n && dev_valid(c, r)) ? 1u : 0u;
+    }
+    atomicAdd(&s, v);
+    __syncthreads();
+    if (threadIdx.x == 0) cnt[blockIdx.x] = s;
+}
+
+// Codes + row ids of the valid rows (in row order) and the null row ids (in
+// row order) -- block b's valid rows start at voff[b], its nulls at
+// b*1024 - voff[b].
+__global__ __launch_bounds__(256) void srt_prep_kernel(DevCol c, int64_t n, bool descending,
+                                                       const uint64_t* __restrict__ voff, uint64_t* __restrict__ keys,
+                                                       uint32_t* __restrict__ idx, uint32_t* __restrict__ nulls) {
+    __shared__ uint32_t wv[4], wn[4];
+    const int64_t base = (int64_t)blockIdx.x * 1024;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint64_t vpos = voff[blockIdx.x];
+    uint64_t npos = (uint64_t)base - vpos;
+    for (int k = 0; k < 4; ++k) {
+        const int64_t r = base + k * 256 + threadIdx.x;
+        const bool in = r < n;
+        const bool valid = in && dev_valid(c, r);
+        const uint64_t bv = __ballot(valid), bn = __ballot(in && !valid);
+        const uint64_t lt = (1ull << lane) - 1;
+        if (lane == 0) {
+            wv[wid] = (uint32_t)__popcll(bv);
+            wn[wid] = (uint32_t)__popcll(bn);
+        }
+        __syncthreads();
+        uint64_t pv = vpos, pn = npos;
+        uint32_t tv = 0, tn = 0;
+        for (int w = 0; w < 4; ++w) {
+            if (w < wid) {
+                pv += wv[w];
+                pn += wn[w];
+            }
+            tv += wv[w];
+            tn += wn[w];
+        }
+        if (valid) {
+            const uint64_t p = pv + __popcll(bv & lt);
+            keys[p] = sort_code(c, r, descending);
+            idx[p] = (uint32_t)r;
+        } else if (in) {
+            nulls[pn + __popcll(bn & lt)] = (uint32_t)r;
+        }
+        vpos += tv;
+        npos += tn;
+        __syncthreads();
+    }
+}
+
+__global__ void srt_codes_kernel(DevCol c, int64_t n, bool descending, uint64_t* __restrict__ keys,
+                                 uint32_t* __restrict__ idx) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+        keys[r] = sort_code(c, r, descending);
+        idx[r] = (uint32_t)r;
+    }
+}
+
+// All eight byte histograms in one read: hist[byte * 256 + digit].
+__global__ __launch_bounds__(256) void srt_histo_kernel(const uint64_t* __restrict__ keys, int64_t n,
+                                                        unsigned long long* __restrict__ hist) {
+    __shared__ uint32_t h[8 * 256];
+    for (int i = threadIdx.x; i < 8 * 256; i += 256) h[i] = 0;
+    __syncthreads();
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = keys[i];
+#pragma unroll
+        for (int b = 0; b < 8; ++b) atomicAdd(&h[b * 256 + ((k >> (8 * b)) & 0xFF)], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 8 * 256; i += 256)
+        if (h[i]) atomicAdd(&hist[i], (unsigned long long)h[i]);
+}
+
+// Upsweep: digit counts of every tile, digit-major (cnt[d * ntiles + t]).
+__global__ __launch_bounds__(kSrtThreads) void srt_upsweep_kernel(const uint64_t* __restrict__ keys, int64_t n,
+                                                                  int shift, int64_t ntiles,
+                                                                  uint32_t* __restrict__ cnt) {
+    __shared__ uint32_t h[256];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const int64_t base = (int64_t)blockIdx.x * kSrtTile;
+#pragma unroll
+    for (int k = 0; k < kSrtPer; ++k) {
+        const int64_t i = base + k * kSrtThreads + threadIdx.x;
+        if (i < n) atomicAdd(&h[(keys[i] >> shift) & 0xFF], 1u);
+    }
+    __syncthreads();
+    cnt[(int64_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
+}
+
+// Downsweep: stable scatter of one tile by the digit at `shift`.
+__global__ __launch_bounds__(kSrtThreads) void srt_downsweep_kernel(const uint64_t* __restrict__ keys_in,
+                                                                    const uint32_t* __restrict__ idx_in, int64_t n,
+                                                                    int shift, int64_t ntiles,
+                                                                    const uint64_t* __restrict__ off,
+                                                                    uint64_t* __restrict__ keys_out,
+                                                                    uint32_t* __restrict__ idx_out) {
+    __shared__ uint64_t skey[kSrtTile];
+    __shared__ uint32_t sidx[kSrtTile];
+    __shared__ uint32_t dstart[256];
+    __shared__ uint32_t run[256];
+    __shared__ uint32_t wcnt[kSrtThreads / 64][256];
+    __shared__ uint64_t wsum[kSrtThreads / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int64_t base = (int64_t)blockIdx.x * kSrtTile;
+    const int m = n - base < kSrtTile ? (int)(n - base) : kSrtTile;
+    // tile digit counts -> local starts
+    run[tid] = 0;
+    for (int w = 0; w < kSrtThreads / 64; ++w) wcnt[w][tid] = 0;
+    __syncthreads();
+    uint64_t k[kSrtPer];
+#pragma unroll
+    for (int j = 0; j < kSrtPer; ++j) {
+        const int i = j * kSrtThreads + tid;
+        k[j] = i < m ? keys_in[base + i] : 0;
+        if (i < m) atomicAdd(&run[(k[j] >> shift) & 0xFF], 1u);
+    }
+    __syncthreads();
+    uint64_t total;
+    const uint32_t mycnt = run[tid];
+    dstart[tid] = (uint32_t)block_excl_scan(mycnt, wsum, total);
+    run[tid] = 0;
+    __syncthreads();
+    const uint64_t lt = (1ull << lane) - 1;
+#pragma unroll
+    for (int j = 0; j < kSrtPer; ++j) {
+        const int i = j * kSrtThreads + tid;
+        const bool valid = i < m;
+        const uint32_t d = (uint32_t)(k[j] >> shift) & 0xFF;
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const uint64_t bb = __ballot((d >> b) & 1);
+            peers &= ((d >> b) & 1) ? bb : ~bb;
+        }
+        const uint32_t rank = (uint32_t)__popcll(peers & lt);
+        if (valid && rank == 0) wcnt[wid][d] = (uint32_t)__popcll(peers);
+        __syncthreads();
+        if (valid) {
+            uint32_t pos = dstart[d] + run[d] + rank;
+            for (int w = 0; w < wid; ++w) pos += wcnt[w][d];
+            skey[pos] = k[j];
+            sidx[pos] = idx_in[base + i];
+        }
+        __syncthreads();
+        uint32_t add = 0;
+        for (int w = 0; w < kSrtThreads / 64; ++w) {
+            add += wcnt[w][tid];
+            wcnt[w][tid] = 0;
+        }
+        run[tid] += add;
+        __syncthreads();
+    }
+    // coalesced write-out: consecutive threads, consecutive slots of a digit run
+    for (int p = tid; p < m; p += kSrtThreads) {
+        const uint64_t kk = skey[p];
+        const uint32_t d = (uint32_t)(kk >> shift) & 0xFF;
+        const uint64_t o = off[(int64_t)d * ntiles + blockIdx.x] + (uint64_t)(p - dstart[d]);
+        keys_out[o] = kk;
+        idx_out[o] = sidx[p];
+    }
+}
+
+__global__ void srt_place_nulls_kernel(const uint32_t* __restrict__ nulls, int64_t nn, uint32_t* __restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nn; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = nulls[i];
+}
+
+}  // namespace plgpu
+
+using namespace plgpu;
+
+PLGPU_API int plgpu_arg_sort(const plgpu_column* key, int32_t descending, int32_t nulls_last, plgpu_column* out_idx,
+                             void* stream) {
+    hipStream_t s = as_stream(stream);
+    if (key == nullptr || out_idx == nullptr) return fail(PLGPU_ERR_INVALID, "NULL argument");
+    std::memset(out_idx, 0, sizeof *out_idx);
+    if (key->dtype != PLGPU_I64 && key->dtype != PLGPU_I32 && key->dtype != PLGPU_U32 && key->dtype != PLGPU_F64)
+        return fail(PLGPU_ERR_SCHEMA, "sort key must be Int64 / Int32 / UInt32 / Float64");
+    const int64_t n = key->length;
+    if (n >= 0xFFFFFFFFll) return fail(PLGPU_ERR_CAPACITY, "sort input exceeds the u32 index space");
+    DevCol c;
+    std::memset(&c, 0, sizeof c);
+    c.dtype = key->dtype;
+    c.offset = key->offset;
+    c.values = key->values;
+    c.validity = key->validity;
+    int rc = make_owned_column(out_idx, PLGPU_U32, n, false, s);
+    if (rc || n == 0) return rc;
+    uint64_t* keys[2] = {nullptr, nullptr};
+    uint32_t* idx[2] = {nullptr, nullptr};
+    uint32_t* nulls = nullptr;
+    uint32_t* cnt = nullptr;
+    uint64_t* off = nullptr;
+    uint64_t* part = nullptr;
+    unsigned long long* hist = nullptr;
+    const int64_t nblk = (n + 1023) / 1024;
+    for (int i = 0; i < 2 && !rc; ++i) {
+        rc = dev_alloc((void**)&keys[i], n * 8, s);
+        if (!rc) rc = dev_alloc((void**)&idx[i], n * 4, s);
+    }
+    if (!rc) rc = dev_alloc((void**)&hist, 8 * 256 * 8, s);
+    int64_t nv = n;  // valid rows
+    const int cus = 256;
+    if (!rc && c.validity) {
+        uint64_t* voff = nullptr;
+        uint32_t* vcnt = nullptr;
+        rc = dev_alloc((void**)&vcnt, nblk * 4, s);
+        if (!rc) rc = dev_alloc((void**)&voff, (nblk + 1) * 8, s);
+        if (!rc) rc = dev_alloc((void**)&part, ((nblk + kScanChunk - 1) / kScanChunk + 1) * 8, s);
+        if (!rc) rc = dev_alloc((void**)&nulls, n * 4, s);
+        if (!rc) {
+            srt_count_valid_kernel<<<(unsigned)nblk, 256, 0, s>>>(c, n, vcnt);
+            hipError_t e = scan_exclusive<uint32_t>(vcnt, nblk, voff, part, s);
+            uint64_t tv = 0;
+            if (e == hipSuccess) {
+                srt_prep_kernel<<<(unsigned)nblk, 256, 0, s>>>(c, n, descending != 0, voff, keys[0], idx[0], nulls);
+                e = hipGetLastError();
+            }
+            if (e == hipSuccess) e = hipMemcpyAsync(&tv, voff + nblk, 8, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e != hipSuccess) rc = hip_fail(e, "sort prep");
+            nv = (int64_t)tv;
+        }
+        dev_free(vcnt, s);
+        dev_free(voff, s);
+        dev_free(part, s);
+        part = nullptr;
+    } else if (!rc) {
+        srt_codes_kernel<<<(unsigned)std::min<int64_t>((n + 255) / 256, cus * 16), 256, 0, s>>>(
+            c, n, descending != 0, keys[0], idx[0]);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) rc = hip_fail(e, "sort codes");
+    }
+    unsigned long long h[8 * 256];
+    if (!rc && nv > 0) {
+        hipError_t e = hipMemsetAsync(hist, 0, 8 * 256 * 8, s);
+        if (e == hipSuccess) {
+            srt_histo_kernel<<<(unsigned)std::min<int64_t>((nv + 255) / 256, cus * 8), 256, 0, s>>>(keys[0], nv, hist);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) e = hipMemcpyAsync(h, hist, sizeof h, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) rc = hip_fail(e, "sort histogram");
+    }
+    int cur = 0;
+    const int64_t ntiles = (nv + kSrtTile - 1) / kSrtTile;
+    if (!rc && nv > 0) {
+        rc = dev_alloc((void**)&cnt, ntiles * 256 * 4, s);
+        if (!rc) rc = dev_alloc((void**)&off, (ntiles * 256 + 1) * 8, s);
+        if (!rc) rc = dev_alloc((void**)&part, ((ntiles * 256 + kScanChunk - 1) / kScanChunk + 1) * 8, s);
+    }
+    for (int byte = 0; byte < 8 && !rc && nv > 0; ++byte) {
+        bool constant = false;
+        for (int d = 0; d < 256; ++d) constant = constant || h[byte * 256 + d] == (unsigned long long)nv;
+        if (constant) continue;  // every code has the same byte: the pass is the identity
+        const int shift = 8 * byte;
+        srt_upsweep_kernel<<<(unsigned)ntiles, kSrtThreads, 0, s>>>(keys[cur], nv, shift, ntiles, cnt);
+        hipError_t e = scan_exclusive<uint32_t>(cnt, ntiles * 256, off, part, s);
+        if (e == hipSuccess) {
+            srt_downsweep_kernel<<<(unsigned)ntiles, kSrtThreads, 0, s>>>(keys[cur], idx[cur], nv, shift, ntiles, off,
+                                                                         keys[cur ^ 1], idx[cur ^ 1]);
+            e = hipGetLastError();
+        }
+        if (e != hipSuccess) rc = hip_fail(e, "sort pass");
+        cur ^= 1;
+    }
+    if (!rc) {
+        uint32_t* out = (uint32_t*)out_idx->values;
+        const int64_t nn = n - nv;
+        // nulls first (default) or last, each group in row order
+        uint32_t* vdst = nulls_last ? out : out + nn;
+        uint32_t* ndst = nulls_last ? out + nv : out;
+        hipError_t e = hipSuccess;
+        if (nv > 0) e = hipMemcpyAsync(vdst, idx[cur], nv * 4, hipMemcpyDeviceToDevice, s);
+        if (e == hipSuccess && nn > 0) e = hipMemcpyAsync(ndst, nulls, nn * 4, hipMemcpyDeviceToDevice, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) rc = hip_fail(e, "sort output");
+    }
+    for (int i = 0; i < 2; ++i) {
+        dev_free(keys[i], s);
+        dev_free(idx[i], s);
+    }
+    dev_free(nulls, s);
+    dev_free(cnt, s);
+    dev_free(off, s);
+    dev_free(part, s);
+    dev_free(hist, s);
+    if (rc) plgpu_column_release(out_idx);
+    return rc;
+}

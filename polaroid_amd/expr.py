@@ -62,6 +62,8 @@ class Expr:
             return f'{self.args[0]!r}.alias("{self.value}")'
         if self.kind == "len":
             return "len()"
+        if self.kind == "rolling":
+            return f"{self.args[0]!r}.rolling_{self.op}{self.value}"
         return f"{self.args[0]!r}.{self.op}()"
 
     def __bool__(self):
@@ -132,6 +134,34 @@ class Expr:
     def max(self): return Expr("agg", (self,), op="max")
     def count(self): return Expr("agg", (self,), op="count")
     def len(self): return Expr("agg", (self,), op="len")
+
+    # ------------------------------------------------- window / ordering
+    def rolling_sum(self, window_size: int, weights=None, *, min_samples: int | None = None,
+                    center: bool = False) -> "Expr":
+        """Fixed-window sum (Expr.rolling_sum)."""
+        return _rolling(self, "sum", window_size, weights, min_samples, center)
+
+    def rolling_mean(self, window_size: int, weights=None, *, min_samples: int | None = None,
+                     center: bool = False) -> "Expr":
+        """Fixed-window mean (Expr.rolling_mean)."""
+        return _rolling(self, "mean", window_size, weights, min_samples, center)
+
+    def sort(self, *, descending: bool = False, nulls_last: bool = False) -> "Expr":
+        return Expr("sort", (self,), op="sort", value=(bool(descending), bool(nulls_last)))
+
+    def arg_sort(self, *, descending: bool = False, nulls_last: bool = False) -> "Expr":
+        return Expr("sort", (self,), op="arg_sort", value=(bool(descending), bool(nulls_last)))
+
+
+def _rolling(e: Expr, kind: str, window_size: int, weights, min_samples, center) -> Expr:
+    if weights is not None:
+        raise N.InvalidOperationError("weighted rolling windows are not supported on the GPU executor")
+    if not isinstance(window_size, int) or window_size < 1:
+        raise N.InvalidOperationError("`window_size` must be a positive integer")
+    ms = window_size if min_samples is None else int(min_samples)
+    if ms > window_size:
+        raise N.InvalidOperationError("`min_samples` should be <= `window_size`")
+    return Expr("rolling", (e,), op=kind, value=(window_size, ms, bool(center)))
 
 
 def _to_expr(v: Any) -> Expr:

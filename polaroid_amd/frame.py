@@ -313,6 +313,39 @@ class Series:
     def __repr__(self) -> str:
         return f"shape: ({self.len()},)\nSeries: '{self.name}' [{self.dtype}]\n{self.to_list()[:20]}"
 
+    # sort / rolling (Series.arg_sort, Series.sort, Series.rolling_*) ---------
+    def arg_sort(self, *, descending: bool = False, nulls_last: bool = False) -> "Series":
+        out = N.Column()
+        N.check(N.lib().plgpu_arg_sort(C.byref(self._col), int(descending), int(nulls_last), C.byref(out), None))
+        return Series._from_native(self.name, out)
+
+    def gather(self, idx: "Series") -> "Series":
+        out = (N.Column * 1)()
+        N.check(N.lib().plgpu_gather((N.Column * 1)(self._col), 1, C.byref(idx._col), out, None))
+        return Series._from_native(self.name, out[0])
+
+    def sort(self, *, descending: bool = False, nulls_last: bool = False) -> "Series":
+        return self.gather(self.arg_sort(descending=descending, nulls_last=nulls_last))
+
+    def _rolling(self, kind: int, window_size: int, min_samples: int | None, center: bool) -> "Series":
+        out = N.Column()
+        ms = window_size if min_samples is None else min_samples
+        N.check(N.lib().plgpu_rolling(C.byref(self._col), kind, int(window_size), int(ms), int(center),
+                                      C.byref(out), None))
+        return Series._from_native(self.name, out)
+
+    def rolling_sum(self, window_size: int, weights=None, *, min_samples: int | None = None,
+                    center: bool = False) -> "Series":
+        if weights is not None:
+            raise N.InvalidOperationError("weighted rolling windows are not supported on the GPU executor")
+        return self._rolling(N.ROLLING["sum"], window_size, min_samples, center)
+
+    def rolling_mean(self, window_size: int, weights=None, *, min_samples: int | None = None,
+                     center: bool = False) -> "Series":
+        if weights is not None:
+            raise N.InvalidOperationError("weighted rolling windows are not supported on the GPU executor")
+        return self._rolling(N.ROLLING["mean"], window_size, min_samples, center)
+
     # eager conveniences mirroring Series.filter ------------------------------
     def filter(self, mask: "Series") -> "Series":
         out = (N.Column * 1)()
@@ -398,6 +431,12 @@ class DataFrame:
     def filter(self, *predicates: Expr, **constraints: Any) -> "DataFrame":
         return self.lazy().filter(*predicates, **constraints).collect()
 
+    def sort(self, by: str, *, descending: bool = False, nulls_last: bool = False,
+             maintain_order: bool = False) -> "DataFrame":
+        """DataFrame.sort on one column (always stable, so maintain_order holds)."""
+        return self.lazy().sort(by, descending=descending, nulls_last=nulls_last,
+                                maintain_order=maintain_order).collect()
+
     def join(self, other: "DataFrame", on: str | None = None, how: str = "inner", *,
              left_on: str | None = None, right_on: str | None = None, suffix: str = "_right",
              validate: str = "m:m", nulls_equal: bool = False, maintain_order: str | None = None) -> "DataFrame":
@@ -456,6 +495,12 @@ class LazyFrame:
 
     def group_by(self, *by: Any, maintain_order: bool = False) -> "LazyGroupBy":
         return LazyGroupBy(self, by, maintain_order)
+
+    def sort(self, by: str, *, descending: bool = False, nulls_last: bool = False,
+             maintain_order: bool = False) -> "LazyFrame":
+        if not isinstance(by, str):
+            raise N.InvalidOperationError("the GPU executor sorts by exactly one column")
+        return LazyFrame(("sort", self._node, by, bool(descending), bool(nulls_last)))
 
     def join(self, other: "LazyFrame", on: str | None = None, how: str = "inner", *,
              left_on: str | None = None, right_on: str | None = None, suffix: str = "_right",
@@ -563,6 +608,17 @@ def _col_array(series: Sequence[Series]):
 def _eval(expr: Expr, df: DataFrame) -> Series:
     if expr.kind in ("col",) or (expr.kind == "alias" and expr.args[0].kind == "col"):
         return df._cols[expr.meta_root_names()[0]].alias(expr.output_name())
+    base = expr.args[0] if expr.kind == "alias" else expr
+    if base.kind in ("rolling", "sort"):
+        inner = _eval(base.args[0], df)
+        if base.kind == "rolling":
+            w, ms, center = base.value
+            res = inner._rolling(N.ROLLING[base.op], w, ms, center)
+        elif base.op == "arg_sort":
+            res = inner.arg_sort(descending=base.value[0], nulls_last=base.value[1])
+        else:
+            res = inner.sort(descending=base.value[0], nulls_last=base.value[1])
+        return res.alias(expr.output_name())
     used, prog, n = _program(expr, df)
     if not used:
         raise N.InvalidOperationError("literal-only expressions are not supported on the GPU executor")
@@ -737,12 +793,25 @@ def _join(left: DataFrame, right: DataFrame, left_on: str, right_on: str, suffix
     return DataFrame(out)
 
 
+def _sort(df: DataFrame, by: str, descending: bool, nulls_last: bool) -> DataFrame:
+    if by not in df._cols:
+        raise N.ComputeError(f'unable to find column "{by}"; valid columns: {df.columns}')
+    idx = df._cols[by].arg_sort(descending=descending, nulls_last=nulls_last)
+    names = df.columns
+    out = (N.Column * builtins.len(names))()
+    N.check(N.lib().plgpu_gather(_col_array([df._cols[n] for n in names]), builtins.len(names),
+                                 C.byref(idx._col), out, None))
+    return DataFrame([Series._from_native(n, out[i]) for i, n in enumerate(names)])
+
+
 def _execute(node: tuple, info: dict | None = None) -> DataFrame:
     kind = node[0]
     if kind == "scan":
         return node[1]
     if kind == "join":
         return _join(_execute(node[1], info), _execute(node[2], info), *node[3:])
+    if kind == "sort":
+        return _sort(_execute(node[1], info), node[2], node[3], node[4])
     if kind == "filter":
         df = _execute(node[1], info)
         return _filter(df, node[2])

@@ -276,11 +276,86 @@ def join_cases():
     return {"cases": cases}
 
 
+# ---------------------------------------------------------------------------
+# 5. Sorting (operations/test_sort.py).  `values` of one column; expected
+#    arg-sort or sorted values for (descending, nulls_last).
+def sort_cases():
+    cases = []
+    a = [1.0, 2.0, 3.0, None, None]
+    cases.append({"name": "test_arg_sort_nulls[nulls_last=True]", "source": "operations/test_sort.py:213-221",
+                  "values": a, "args": {"nulls_last": True}, "expected_arg_sort": [0, 1, 2, 3, 4]})
+    cases.append({"name": "test_arg_sort_nulls[nulls_last=False]", "source": "operations/test_sort.py:213-221",
+                  "values": a, "args": {"nulls_last": False}, "expected_arg_sort": [3, 4, 0, 1, 2]})
+    cases.append({"name": "test_arg_sort_nulls sorted values", "source": "operations/test_sort.py:223-227",
+                  "values": a, "args": {"nulls_last": False}, "expected_sorted": [None, None, 1.0, 2.0, 3.0]})
+    cases.append({"name": "test_sort_nans_3740", "source": "operations/test_sort.py:299-315",
+                  "values": [0.0, None, float("nan"), float("-inf"), float("inf")], "args": {},
+                  "expected_arg_sort": [1, 3, 0, 4, 2]})   # keys [2, 4, 1, 5, 3] - 1
+    cases.append({"name": "test_arg_sort_rank_nans", "source": "operations/test_sort.py:517-531",
+                  "values": [1.0, float("nan")], "args": {}, "expected_arg_sort": [0, 1]})
+    cases.append({"name": "test_sort_series_nulls_last", "source": "operations/test_sort.py:951-963",
+                  "values": [1, None, 3], "args": {"nulls_last": True}, "expected_sorted": [1, 3, None]})
+    x = [1, 3, None, 2, None]
+    for descending in (True, False):
+        for nulls_last in (True, False):
+            sentinel = 100 if descending ^ nulls_last else -100
+            ref = sorted(x, key=lambda k: sentinel if k is None else k, reverse=descending)
+            cases.append({"name": f"test_sort_descending_nulls_last[{descending}-{nulls_last}]",
+                          "source": "operations/test_sort.py:979-1001",
+                          "values": x, "args": {"descending": descending, "nulls_last": nulls_last},
+                          "expected_sorted": ref})
+    cases.append({"name": "test_sort_descending", "source": "operations/test_sort.py:801-806",
+                  "values": [1, 2, 3], "args": {"descending": True}, "expected_sorted": [3, 2, 1]})
+    return {"cases": cases}
+
+
+# ---------------------------------------------------------------------------
+# 6. Fixed-window rolling sum / mean (operations/rolling/test_rolling.py,
+#    lazyframe/test_lazyframe.py, polars-compute rolling/no_nulls/sum.rs
+#    unit test).  `expected` with None for null outputs.
+def rolling_cases():
+    nan = float("nan")
+    cases = []
+    cases.append({"name": "test_rolling_infinity", "source": "operations/rolling/test_rolling.py:288-292",
+                  "values": [float("-inf"), 5.0, 5.0], "kind": "mean", "window": 2, "min": None, "center": False,
+                  "expected": [None, float("-inf"), 5.0]})
+    cases.append({"name": "test_rolling_ints mean", "source": "operations/rolling/test_rolling.py:873-891",
+                  "values": [1, 2, 3, 2, 1], "kind": "mean", "window": 2, "min": None, "center": False,
+                  "expected": [None, 1.5, 2.5, 2.5, 1.5]})
+    cases.append({"name": "test_rolling_ints sum", "source": "operations/rolling/test_rolling.py:881-889",
+                  "values": [1, 2, 3, 2, 1], "kind": "sum", "window": 2, "min": None, "center": False,
+                  "expected": [None, 3, 5, 5, 3]})
+    for kind, ms, exp in (("mean", 1, [1.0, 1.5, 2.0, 3.0, 4.0]), ("mean", None, [None, None, 2.0, 3.0, 4.0]),
+                          ("sum", 1, [1, 3, 6, 9, 12]), ("sum", None, [None, None, 6, 9, 12])):
+        cases.append({"name": f"test_rolling fruits_cars A rolling_{kind}(3, min_samples={ms})",
+                      "source": "lazyframe/test_lazyframe.py:734-763",
+                      "values": [1, 2, 3, 4, 5], "kind": kind, "window": 3, "min": ms, "center": False,
+                      "expected": exp})
+    v = [1.0, 2.0, 3.0, 4.0]
+    for w, ms, center, exp in ((2, 2, False, [None, 3.0, 5.0, 7.0]), (2, 1, False, [1.0, 3.0, 5.0, 7.0]),
+                               (4, 1, False, [1.0, 3.0, 6.0, 10.0]), (4, 1, True, [3.0, 6.0, 10.0, 9.0]),
+                               (4, 4, True, [None, None, 10.0, None])):
+        cases.append({"name": f"test_rolling_sum(w={w}, min={ms}, center={center})",
+                      "source": "crates/polars-compute/src/rolling/no_nulls/sum.rs:69-96",
+                      "values": v, "kind": "sum", "window": w, "min": ms, "center": center, "expected": exp})
+    cases.append({"name": "test_rolling_sum nan", "source": "crates/polars-compute/src/rolling/no_nulls/sum.rs:98-117",
+                  "values": [1.0, 2.0, 3.0, nan, 5.0, 6.0, 7.0], "kind": "sum", "window": 3, "min": 3,
+                  "center": False, "expected": [None, None, 6.0, nan, nan, nan, 18.0]})
+    stab = [0.0, 290.57, 107.0, 172.0, 124.25, 304.0, 379.5, 347.35, 1516.41, 386.12, 226.5, 294.62, 125.5,
+            0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0]
+    cases.append({"name": "test_rolling_sum_stability_11146 (last value)",
+                  "source": "operations/rolling/test_rolling.py:1476-1510",
+                  "values": stab, "kind": "mean", "window": 8, "min": 1, "center": False, "expected_last": 0.0})
+    return {"cases": cases}
+
+
 def main():
     for name, obj in (("compare_total_order.json", compare_table()),
                       ("group_by_cases.json", group_by_cases()),
                       ("filter_cases.json", filter_cases()),
-                      ("join_cases.json", join_cases())):
+                      ("join_cases.json", join_cases()),
+                      ("sort_cases.json", sort_cases()),
+                      ("rolling_cases.json", rolling_cases())):
         with open(os.path.join(HERE, name), "w") as f:
             json.dump(obj, f, indent=1, sort_keys=False)
             f.write("\n")
