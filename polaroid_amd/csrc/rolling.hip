@@ -295,6 +295,173 @@ __global__ __launch_bounds__(kRlThreads) void rl_tile_kernel(RlParams p) {
     }
 }
 
+// Small windows (w <= kSlideMaxW): a workgroup stages 4096 outputs' inputs
+// in LDS (coalesced), then each thread slides an exact fixed-point window
+// over 16 consecutive outputs: per output, the limbs of the value entering
+// are added and those of the value leaving subtracted (integer arithmetic,
+// so no drift), and the sum is rounded once.  Outputs go back through LDS
+// so the global stores are coalesced.
+constexpr int kSlideMaxW = 64;
+constexpr int kSlideRun = 8;
+constexpr int kSlideOut = kRlThreads * kSlideRun;  // 2048
+
+struct RlAcc {
+    int64_t l0, l1, l2, isum;
+    int32_t nn, pinf, ninf, nan;
+};
+
+// Limbs of a finite value known to lie in the tile's window (zero allowed):
+// t = +-m * 2^sh split as l0 + l1 * 2^40 + l2 * 2^80 (low limbs >= 0, top
+// limb signed), branch-free.
+__device__ __forceinline__ void rl_limbs(uint64_t b, int bottom, int64_t& l0, int64_t& l1, int64_t& l2) {
+    constexpr uint64_t M40 = (1ull << 40) - 1;
+    const uint32_t ex = (uint32_t)(b >> 52) & 0x7FF;
+    const uint64_t m = (b & 0x000FFFFFFFFFFFFFull) | ((uint64_t)(ex != 0) << 52);
+    const int sh0 = (int)(ex ? ex : 1) - 1075 - bottom;
+    const uint32_t sh = sh0 < 0 ? 0u : (uint32_t)sh0;  // only zero can fall below (m == 0)
+    const int64_t sm = (int64_t)b < 0 ? -(int64_t)m : (int64_t)m;
+    l0 = sh < 40 ? (int64_t)(((uint64_t)sm << sh) & M40) : 0;
+    l1 = (int64_t)((sh <= 40 ? (uint64_t)(sm >> (40 - sh)) : ((uint64_t)sm << (sh - 40))) & M40);
+    l2 = sm >> (sh > 16 ? 80 - sh : 63);
+}
+
+// Correctly rounded double of (l0 + l1*2^40 + l2*2^80) * 2^bottom for limb
+// sums of at most a few thousand values (|total| < 2^126): the magnitude is
+// normalised, its top 64 bits carry a sticky bit for the rest (round to
+// odd), and one u64 -> f64 conversion rounds.  Results that would be
+// subnormal take fx_to_double.
+__device__ __forceinline__ double rl_to_double(int64_t l0, int64_t l1, int64_t l2, int bottom) {
+    const __int128 t = (__int128)l0 + ((__int128)l1 << 40) + ((__int128)l2 << 80);
+    if (t == 0) return 0.0;
+    const bool neg = t < 0;
+    unsigned __int128 u = neg ? (unsigned __int128)(-t) : (unsigned __int128)t;
+    const uint64_t hi = (uint64_t)(u >> 64);
+    const int lz = hi ? __clzll(hi) : 64 + __clzll((uint64_t)u);
+    u <<= lz;
+    const uint64_t top = (uint64_t)(u >> 64) | (((uint64_t)u) != 0 ? 1ull : 0ull);
+    const int e = 64 - lz + bottom;  // value ~= top * 2^e, leading bit at 2^(63 + e)
+    if (63 + e < -1021) {
+        uint64_t w0, w1, w2;
+        limbs_to_192(l0, l1, l2, w0, w1, w2);
+        return fx_to_double(w0, w1, w2, bottom);
+    }
+    const double r = __builtin_ldexp((double)top, e);
+    return neg ? -r : r;
+}
+
+template <bool NULLABLE>
+__device__ __forceinline__ void rl_acc(const RlParams& p, const uint64_t* vals, const uint8_t* vld, int j, int bottom,
+                                       int sign, RlAcc& a) {
+    if (NULLABLE && !vld[j]) return;
+    a.nn += sign;
+    const uint64_t b = vals[j];
+    if (p.out_int) {
+        a.isum = (int64_t)((uint64_t)a.isum + (uint64_t)(sign > 0 ? b : 0ull - b));
+        return;
+    }
+    const uint64_t ab = b & 0x7fffffffffffffffull;
+    if (ab >= 0x7ff0000000000000ull) {
+        if (ab > 0x7ff0000000000000ull) a.nan += sign;
+        else if (b >> 63) a.ninf += sign;
+        else a.pinf += sign;
+        return;
+    }
+    int64_t x0, x1, x2;
+    rl_limbs(b, bottom, x0, x1, x2);
+    if (sign > 0) {
+        a.l0 += x0;
+        a.l1 += x1;
+        a.l2 += x2;
+    } else {
+        a.l0 -= x0;
+        a.l1 -= x1;
+        a.l2 -= x2;
+    }
+}
+
+template <bool NULLABLE>
+__global__ __launch_bounds__(kRlThreads) void rl_slide_kernel(RlParams p) {
+    __shared__ uint64_t vals[kSlideOut + kSlideMaxW];
+    __shared__ uint8_t vld[NULLABLE ? kSlideOut + kSlideMaxW : 1];
+    __shared__ uint64_t outv[kSlideOut];
+    __shared__ uint64_t outm[kSlideOut / 64];
+    __shared__ uint32_t red[2];
+    const int tid = threadIdx.x;
+    const int64_t o0 = (int64_t)blockIdx.x * kSlideOut;
+    const int64_t o1 = o0 + kSlideOut < p.n ? o0 + kSlideOut : p.n;
+    int64_t lo, hi, tmp;
+    rl_bounds(p, o0, lo, tmp);
+    rl_bounds(p, o1 - 1, tmp, hi);
+    const int m = (int)(hi - lo);
+    if (tid < 2) red[tid] = 0;
+    if (tid < kSlideOut / 64) outm[tid] = 0;
+    __syncthreads();
+    uint32_t mx = 0, inv_mn = 0;
+    for (int j = tid; j < m; j += kRlThreads) {
+        const int64_t r = lo + j;
+        const bool v = !NULLABLE || dev_valid(p.c, r);
+        const uint64_t b = p.out_int ? dev_load(p.c, r) : rl_bits(p, r);
+        vals[j] = b;
+        if (NULLABLE) vld[j] = v;
+        if (!p.out_int && v) {
+            const uint32_t ex = (uint32_t)(b >> 52) & 0x7FF;
+            if (ex != 0x7FF && (b << 1) != 0) {
+                const uint32_t e1 = ex ? ex : 1;
+                mx = e1 > mx ? e1 : mx;
+                inv_mn = 0x7FF - e1 > inv_mn ? 0x7FF - e1 : inv_mn;
+            }
+        }
+    }
+    atomicMax(&red[0], mx);
+    atomicMax(&red[1], inv_mn);
+    __syncthreads();
+    const int tmax = (int)red[0], tmin = 0x7FF - (int)red[1];
+    const bool exact_path = !p.out_int && tmax > 0 && tmax - tmin > kSumWindowBits - 53;
+    const int bottom = (tmax > 0 ? tmax : 1) - 1075 - (kSumWindowBits - 53);
+    const int64_t i0 = o0 + (int64_t)tid * kSlideRun;
+    RlAcc a = {0, 0, 0, 0, 0, 0, 0, 0};
+    int64_t ps = 0, pe = 0;
+    for (int k = 0; k < kSlideRun; ++k) {
+        const int64_t i = i0 + k;
+        if (i >= o1) break;
+        int64_t s, e;
+        rl_bounds(p, i, s, e);
+        double sum = 0.0;
+        RlCounts cnt;
+        if (exact_path) {
+            cnt = {0, 0, 0, 0};
+            for (int64_t r = s; r < e; ++r) rl_count(p, r, cnt);
+            sum = rl_exact_sum(p, s, e);
+        } else {
+            if (k == 0) {
+                for (int64_t r = s; r < e; ++r) rl_acc<NULLABLE>(p, vals, vld, (int)(r - lo), bottom, 1, a);
+            } else {
+                for (int64_t r = ps; r < s; ++r) rl_acc<NULLABLE>(p, vals, vld, (int)(r - lo), bottom, -1, a);
+                for (int64_t r = pe; r < e; ++r) rl_acc<NULLABLE>(p, vals, vld, (int)(r - lo), bottom, 1, a);
+            }
+            cnt = {a.nn, a.pinf, a.ninf, a.nan};
+            if (!p.out_int) sum = rl_to_double(a.l0, a.l1, a.l2, bottom);
+        }
+        ps = s;
+        pe = e;
+        bool valid;
+        RlParams q = p;  // write into the LDS staging buffer (index i - o0)
+        q.out = outv;
+        q.out_int = p.out_int ? PLGPU_I64 : 0;
+        rl_write(q, i - o0, sum, a.isum, cnt, e - s, valid);
+        if (valid) atomicOr((unsigned long long*)&outm[(i - o0) >> 6], 1ull << ((i - o0) & 63));
+    }
+    __syncthreads();
+    // coalesced write-out of values and validity words
+    for (int j = tid; j < (int)(o1 - o0); j += kRlThreads) {
+        const int64_t i = o0 + j;
+        if (!p.out_int) ((double*)p.out)[i] = __longlong_as_double((long long)outv[j]);
+        else if (p.out_int == PLGPU_I64) ((int64_t*)p.out)[i] = (int64_t)outv[j];
+        else ((int32_t*)p.out)[i] = (int32_t)(int64_t)outv[j];
+    }
+    for (int j = tid; j < (int)((o1 - o0 + 63) / 64); j += kRlThreads) p.out_valid[(o0 >> 6) + j] = outm[j];
+}
+
 // Windows too wide for the LDS stage: per-output direct summation.
 __global__ void rl_direct_kernel(RlParams p) {
     for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < p.n; base += (int64_t)gridDim.x * blockDim.x) {
@@ -352,7 +519,11 @@ PLGPU_API int plgpu_rolling(const plgpu_column* values, int32_t kind, int64_t wi
     p.out = (void*)out->values;
     p.out_valid = (uint64_t*)out->validity;
     const int64_t tiles = (p.n + kRlOut - 1) / kRlOut;
-    if (window_size - 1 + kRlOut <= 2048)
+    if (window_size <= kSlideMaxW) {
+        const int64_t g = (p.n + kSlideOut - 1) / kSlideOut;
+        if (p.c.validity) rl_slide_kernel<true><<<(unsigned)g, kRlThreads, 0, s>>>(p);
+        else rl_slide_kernel<false><<<(unsigned)g, kRlThreads, 0, s>>>(p);
+    } else if (window_size - 1 + kRlOut <= 2048)
         rl_tile_kernel<2048><<<(unsigned)tiles, kRlThreads, 0, s>>>(p);
     else if (window_size - 1 + kRlOut <= 4096)
         rl_tile_kernel<4096><<<(unsigned)tiles, kRlThreads, 0, s>>>(p);
