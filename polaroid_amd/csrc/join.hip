@@ -405,6 +405,72 @@ __global__ void gather_bool_kernel(DevCol c, const uint32_t* __restrict__ idx, i
     }
 }
 
+// Many 8-byte columns gathered by one random index: the columns are first
+// packed row-major (sequential read, sequential write), so each random row
+// fetch brings every column's value in one or two cache lines instead of
+// one line per column.
+constexpr int kAosMax = 8;
+
+struct AosCols {
+    const uint64_t* src[kAosMax];
+    uint64_t* dst[kAosMax];
+};
+
+template <int NC>
+__global__ __launch_bounds__(256) void aos_pack_kernel(AosCols c, int64_t rows, uint64_t* __restrict__ aos) {
+    constexpr int NP = (NC + 1) & ~1;  // row stride in u64 (16-byte aligned rows)
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t v[NP];
+#pragma unroll
+        for (int k = 0; k < NC; ++k) v[k] = __builtin_nontemporal_load(c.src[k] + r);
+        if (NP != NC) v[NP - 1] = 0;
+        ulonglong2* q = reinterpret_cast<ulonglong2*>(aos + r * NP);
+#pragma unroll
+        for (int k = 0; k < NP / 2; ++k) q[k] = make_ulonglong2(v[2 * k], v[2 * k + 1]);
+    }
+}
+
+template <int NC>
+__global__ __launch_bounds__(256) void aos_gather_kernel(const uint64_t* __restrict__ aos,
+                                                         const uint32_t* __restrict__ idx, int64_t n, AosCols c) {
+    constexpr int NP = (NC + 1) & ~1;
+    for (int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; o < n; o += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = __builtin_nontemporal_load(idx + o);
+        const ulonglong2* q = reinterpret_cast<const ulonglong2*>(aos + r * NP);
+        uint64_t v[NP];
+#pragma unroll
+        for (int k = 0; k < NP / 2; ++k) {
+            const ulonglong2 x = q[k];
+            v[2 * k] = x.x;
+            v[2 * k + 1] = x.y;
+        }
+#pragma unroll
+        for (int k = 0; k < NC; ++k) __builtin_nontemporal_store(v[k], c.dst[k] + o);
+    }
+}
+
+template <int NC>
+static hipError_t aos_run(const AosCols& c, int64_t rows, const uint32_t* idx, int64_t n, uint64_t* aos,
+                          hipStream_t s) {
+    const int g = std::max(1, num_cus_jn() * 16);
+    aos_pack_kernel<NC><<<g, 256, 0, s>>>(c, rows, aos);
+    aos_gather_kernel<NC><<<g, 256, 0, s>>>(aos, idx, n, c);
+    return hipGetLastError();
+}
+
+static hipError_t aos_dispatch(int nc, const AosCols& c, int64_t rows, const uint32_t* idx, int64_t n,
+                               uint64_t* aos, hipStream_t s) {
+    switch (nc) {
+    case 2: return aos_run<2>(c, rows, idx, n, aos, s);
+    case 3: return aos_run<3>(c, rows, idx, n, aos, s);
+    case 4: return aos_run<4>(c, rows, idx, n, aos, s);
+    case 5: return aos_run<5>(c, rows, idx, n, aos, s);
+    case 6: return aos_run<6>(c, rows, idx, n, aos, s);
+    case 7: return aos_run<7>(c, rows, idx, n, aos, s);
+    default: return aos_run<8>(c, rows, idx, n, aos, s);
+    }
+}
+
 static int gather_into(const plgpu_column& src, const uint32_t* idx, int64_t n, plgpu_column* out, hipStream_t s) {
     const bool nullable = src.validity != nullptr;
     int rc = make_owned_column(out, src.dtype, n, nullable, s);
@@ -692,8 +758,45 @@ PLGPU_API int plgpu_gather(const plgpu_column* cols, int32_t ncols, const plgpu_
     if (idx->validity != nullptr) return fail(PLGPU_ERR_INVALID, "gather indices must not contain nulls");
     for (int i = 0; i < ncols; ++i) std::memset(&out_cols[i], 0, sizeof(plgpu_column));
     const uint32_t* ix = (const uint32_t*)idx->values + idx->offset;
+    const int64_t n = idx->length;
     int rc = PLGPU_OK;
-    for (int i = 0; i < ncols && rc == PLGPU_OK; ++i) rc = gather_into(cols[i], ix, idx->length, &out_cols[i], s);
+    // null-free 8-byte columns of one length: row-major packed gather, in
+    // groups of up to kAosMax; everything else column by column
+    std::vector<int> packed;
+    if (n >= (1 << 20) && !getenv("PLGPU_NO_AOS_GATHER")) {
+        for (int i = 0; i < ncols; ++i)
+            if (cols[i].validity == nullptr && dtype_bytes(cols[i].dtype) == 8 && cols[i].dtype != PLGPU_BOOL &&
+                cols[i].length == cols[0].length)
+                packed.push_back(i);
+        // the packing pass costs a sequential read + write of every column, so
+        // it only pays when several columns share the random index
+        if (packed.size() < 4) packed.clear();
+    }
+    std::vector<bool> done(ncols, false);
+    for (size_t g0 = 0; g0 < packed.size() && rc == PLGPU_OK; g0 += kAosMax) {
+        const int nc = (int)std::min<size_t>(kAosMax, packed.size() - g0);
+        if (nc < 4) break;  // leftover columns go the per-column way
+        const int64_t rows = cols[packed[g0]].length;
+        AosCols c;
+        std::memset(&c, 0, sizeof c);
+        for (int k = 0; k < nc; ++k) {
+            const plgpu_column& src = cols[packed[g0 + k]];
+            rc = make_owned_column(&out_cols[packed[g0 + k]], src.dtype, n, false, s);
+            if (rc) break;
+            c.src[k] = (const uint64_t*)src.values + src.offset;
+            c.dst[k] = (uint64_t*)out_cols[packed[g0 + k]].values;
+            done[packed[g0 + k]] = true;
+        }
+        uint64_t* aos = nullptr;
+        if (!rc) rc = dev_alloc((void**)&aos, (size_t)rows * ((nc + 1) & ~1) * 8, s);
+        if (!rc) {
+            hipError_t e = aos_dispatch(nc, c, rows, ix, n, aos, s);
+            if (e != hipSuccess) rc = hip_fail(e, "packed gather");
+        }
+        dev_free(aos, s);
+    }
+    for (int i = 0; i < ncols && rc == PLGPU_OK; ++i)
+        if (!done[i]) rc = gather_into(cols[i], ix, n, &out_cols[i], s);
     if (rc == PLGPU_OK) {
         hipError_t e = hipStreamSynchronize(s);
         if (e != hipSuccess) rc = hip_fail(e, "gather");

@@ -11,8 +11,8 @@
 // MI355X design:
 //   prep     - nulls are split off in order; keys become order-preserving
 //              u64 codes (descending = complement), carried with u32 row ids;
-//   histo    - one read of the codes gives all 8 byte histograms, so bytes
-//              that are constant over the column cost no pass;
+//   bits     - one read of the codes gives their OR and AND, so bytes that
+//              are constant over the column cost no pass;
 //   per pass - upsweep (per-tile digit counts) -> device scan (digit-major)
 //              -> downsweep: a tile of 4096 codes is ranked stably in LDS
 //              (wave64 ballot peer masks per digit) and written out in
@@ -118,20 +118,25 @@ __global__ void srt_codes_kernel(DevCol c, int64_t n, bool descending, uint64_t*
     }
 }
 
-// All eight byte histograms in one read: hist[byte * 256 + digit].
-__global__ __launch_bounds__(256) void srt_histo_kernel(const uint64_t* __restrict__ keys, int64_t n,
-                                                        unsigned long long* __restrict__ hist) {
-    __shared__ uint32_t h[8 * 256];
-    for (int i = threadIdx.x; i < 8 * 256; i += 256) h[i] = 0;
-    __syncthreads();
+// OR and AND of all codes in one read: a byte whose bits agree over the
+// column ((OR ^ AND) byte == 0) is constant, and its pass is skipped.
+__global__ __launch_bounds__(256) void srt_bits_kernel(const uint64_t* __restrict__ keys, int64_t n,
+                                                       unsigned long long* __restrict__ bits) {
+    uint64_t o = 0, a = ~0ull;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const uint64_t k = keys[i];
-#pragma unroll
-        for (int b = 0; b < 8; ++b) atomicAdd(&h[b * 256 + ((k >> (8 * b)) & 0xFF)], 1u);
+        o |= k;
+        a &= k;
     }
-    __syncthreads();
-    for (int i = threadIdx.x; i < 8 * 256; i += 256)
-        if (h[i]) atomicAdd(&hist[i], (unsigned long long)h[i]);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        o |= __shfl_xor(o, off, 64);
+        a &= __shfl_xor(a, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicOr(&bits[0], (unsigned long long)o);
+        atomicAnd(&bits[1], (unsigned long long)a);
+    }
 }
 
 // Upsweep: digit counts of every tile, digit-major (cnt[d * ntiles + t]).
@@ -151,45 +156,43 @@ __global__ __launch_bounds__(kSrtThreads) void srt_upsweep_kernel(const uint64_t
     cnt[(int64_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
 }
 
-// Downsweep: stable scatter of one tile by the digit at `shift`.
+// Downsweep: stable scatter of one tile by the digit at `shift`.  Wave w
+// ranks its own contiguous 1024 codes row by row (64 codes per row, peer
+// masks from 8 ballots, per-wave digit counters in LDS -- no barriers), then
+// one block-wide combine turns (wave, digit) counts into local positions;
+// the tile is staged in LDS in digit order and written out in runs.
 __global__ __launch_bounds__(kSrtThreads) void srt_downsweep_kernel(const uint64_t* __restrict__ keys_in,
                                                                     const uint32_t* __restrict__ idx_in, int64_t n,
                                                                     int shift, int64_t ntiles,
                                                                     const uint64_t* __restrict__ off,
                                                                     uint64_t* __restrict__ keys_out,
                                                                     uint32_t* __restrict__ idx_out) {
+    constexpr int NW = kSrtThreads / 64;
+    constexpr int ROWS = kSrtTile / kSrtThreads;  // rows of 64 per wave (16)
     __shared__ uint64_t skey[kSrtTile];
     __shared__ uint32_t sidx[kSrtTile];
     __shared__ uint32_t dstart[256];
-    __shared__ uint32_t run[256];
-    __shared__ uint32_t wcnt[kSrtThreads / 64][256];
-    __shared__ uint64_t wsum[kSrtThreads / 64];
+    __shared__ uint32_t cnt[NW][256];
+    __shared__ uint64_t wsum[NW];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int64_t base = (int64_t)blockIdx.x * kSrtTile;
     const int m = n - base < kSrtTile ? (int)(n - base) : kSrtTile;
-    // tile digit counts -> local starts
-    run[tid] = 0;
-    for (int w = 0; w < kSrtThreads / 64; ++w) wcnt[w][tid] = 0;
-    __syncthreads();
-    uint64_t k[kSrtPer];
+    for (int w = 0; w < NW; ++w) cnt[w][tid] = 0;
+    uint64_t k[ROWS];
+    uint32_t rk[ROWS];
+    const int c0 = wid * (kSrtTile / NW);  // this wave's chunk
 #pragma unroll
-    for (int j = 0; j < kSrtPer; ++j) {
-        const int i = j * kSrtThreads + tid;
-        k[j] = i < m ? keys_in[base + i] : 0;
-        if (i < m) atomicAdd(&run[(k[j] >> shift) & 0xFF], 1u);
+    for (int r = 0; r < ROWS; ++r) {
+        const int i = c0 + r * 64 + lane;
+        k[r] = i < m ? keys_in[base + i] : 0;
     }
-    __syncthreads();
-    uint64_t total;
-    const uint32_t mycnt = run[tid];
-    dstart[tid] = (uint32_t)block_excl_scan(mycnt, wsum, total);
-    run[tid] = 0;
     __syncthreads();
     const uint64_t lt = (1ull << lane) - 1;
 #pragma unroll
-    for (int j = 0; j < kSrtPer; ++j) {
-        const int i = j * kSrtThreads + tid;
+    for (int r = 0; r < ROWS; ++r) {
+        const int i = c0 + r * 64 + lane;
         const bool valid = i < m;
-        const uint32_t d = (uint32_t)(k[j] >> shift) & 0xFF;
+        const uint32_t d = (uint32_t)(k[r] >> shift) & 0xFF;
         uint64_t peers = __ballot(valid);
 #pragma unroll
         for (int b = 0; b < 8; ++b) {
@@ -197,23 +200,36 @@ __global__ __launch_bounds__(kSrtThreads) void srt_downsweep_kernel(const uint64
             peers &= ((d >> b) & 1) ? bb : ~bb;
         }
         const uint32_t rank = (uint32_t)__popcll(peers & lt);
-        if (valid && rank == 0) wcnt[wid][d] = (uint32_t)__popcll(peers);
-        __syncthreads();
-        if (valid) {
-            uint32_t pos = dstart[d] + run[d] + rank;
-            for (int w = 0; w < wid; ++w) pos += wcnt[w][d];
-            skey[pos] = k[j];
+        const uint32_t old = cnt[wid][d];
+        rk[r] = old + rank;
+        // the group's leader bumps the counter (program order within the wave
+        // keeps every peer's read before this write)
+        if (valid && rank == 0) cnt[wid][d] = old + (uint32_t)__popcll(peers);
+    }
+    __syncthreads();
+    {
+        // thread = digit: wave prefixes and the tile's digit starts
+        uint32_t c[NW], t = 0;
+        for (int w = 0; w < NW; ++w) {
+            c[w] = cnt[w][tid];
+            cnt[w][tid] = t;
+            t += c[w];
+        }
+        uint64_t total;
+        dstart[tid] = (uint32_t)block_excl_scan(t, wsum, total);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) {
+        const int i = c0 + r * 64 + lane;
+        if (i < m) {
+            const uint32_t d = (uint32_t)(k[r] >> shift) & 0xFF;
+            const uint32_t pos = dstart[d] + cnt[wid][d] + rk[r];
+            skey[pos] = k[r];
             sidx[pos] = idx_in[base + i];
         }
-        __syncthreads();
-        uint32_t add = 0;
-        for (int w = 0; w < kSrtThreads / 64; ++w) {
-            add += wcnt[w][tid];
-            wcnt[w][tid] = 0;
-        }
-        run[tid] += add;
-        __syncthreads();
     }
+    __syncthreads();
     // coalesced write-out: consecutive threads, consecutive slots of a digit run
     for (int p = tid; p < m; p += kSrtThreads) {
         const uint64_t kk = skey[p];
@@ -295,16 +311,16 @@ PLGPU_API int plgpu_arg_sort(const plgpu_column* key, int32_t descending, int32_
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) rc = hip_fail(e, "sort codes");
     }
-    unsigned long long h[8 * 256];
+    unsigned long long h[2] = {0ull, ~0ull};
     if (!rc && nv > 0) {
-        hipError_t e = hipMemsetAsync(hist, 0, 8 * 256 * 8, s);
+        hipError_t e = hipMemcpyAsync(hist, h, 16, hipMemcpyHostToDevice, s);
         if (e == hipSuccess) {
-            srt_histo_kernel<<<(unsigned)std::min<int64_t>((nv + 255) / 256, cus * 8), 256, 0, s>>>(keys[0], nv, hist);
+            srt_bits_kernel<<<(unsigned)std::min<int64_t>((nv + 255) / 256, cus * 8), 256, 0, s>>>(keys[0], nv, hist);
             e = hipGetLastError();
         }
-        if (e == hipSuccess) e = hipMemcpyAsync(h, hist, sizeof h, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(h, hist, 16, hipMemcpyDeviceToHost, s);
         if (e == hipSuccess) e = hipStreamSynchronize(s);
-        if (e != hipSuccess) rc = hip_fail(e, "sort histogram");
+        if (e != hipSuccess) rc = hip_fail(e, "sort key bits");
     }
     int cur = 0;
     const int64_t ntiles = (nv + kSrtTile - 1) / kSrtTile;
@@ -314,9 +330,7 @@ PLGPU_API int plgpu_arg_sort(const plgpu_column* key, int32_t descending, int32_
         if (!rc) rc = dev_alloc((void**)&part, ((ntiles * 256 + kScanChunk - 1) / kScanChunk + 1) * 8, s);
     }
     for (int byte = 0; byte < 8 && !rc && nv > 0; ++byte) {
-        bool constant = false;
-        for (int d = 0; d < 256; ++d) constant = constant || h[byte * 256 + d] == (unsigned long long)nv;
-        if (constant) continue;  // every code has the same byte: the pass is the identity
+        if ((((h[0] ^ h[1]) >> (8 * byte)) & 0xFF) == 0) continue;  // constant byte: the pass is the identity
         const int shift = 8 * byte;
         srt_upsweep_kernel<<<(unsigned)ntiles, kSrtThreads, 0, s>>>(keys[cur], nv, shift, ntiles, cnt);
         hipError_t e = scan_exclusive<uint32_t>(cnt, ntiles * 256, off, part, s);
