@@ -16,7 +16,8 @@ subtree with a Python UDF via `NodeTraverser.set_udf`
 crates/polars-python/src/lazyframe/visitor/nodes.rs, expression classes of
 .../visitor/expr_nodes.rs) for the hot path — DataFrameScan, Filter,
 Select/HStack of arithmetic + comparisons, GroupBy on one integer key with
-sum/mean/min/max/count/len — into a polaroid_amd plan and installs a UDF that
+sum/mean/min/max/count/len, inner Join on one integer key, Sort by one
+column — into a polaroid_amd plan and installs a UDF that
 runs it through libpolaroid_gpu.so.  A query outside that path is left to
 polars' own engine unless `raise_on_fail` is set (the reference GPU engine's
 behaviour).  Once accepted, nothing falls back: a missing HIP library or a
@@ -67,8 +68,14 @@ class _Translator:
         self.nt = nt
 
     # ---------------------------------------------------------- expressions
+    def view(self, node: int):
+        try:
+            return self.nt.view_expression(node)
+        except NotImplementedError as exc:  # e.g. rolling expressions (expr_nodes.rs:1192)
+            raise Unsupported(str(exc)) from exc
+
     def expr(self, node: int) -> Expr:
-        e = self.nt.view_expression(node)
+        e = self.view(node)
         k = _name(e)
         if k == "Column":
             return col(str(e.name))
@@ -100,7 +107,7 @@ class _Translator:
         raise Unsupported(f"expression {k}")
 
     def agg(self, node: int, key: str) -> Expr:
-        e = self.nt.view_expression(node)
+        e = self.view(node)
         k = _name(e)
         if k == "Len":
             return col(key).len()
@@ -133,6 +140,35 @@ class _Translator:
                 raise Unsupported("scan predicate")
             proj = node.projection
             return ("polars_scan", node.df, None if proj is None else list(proj))
+        if k == "Join":
+            # options: (how, nulls_equal, slice, suffix, coalesce, maintain_order), nodes.rs:536
+            how, nulls_equal, slc, suffix, _coalesce, order = node.options
+            if str(how) != "inner":
+                raise Unsupported(f"{how} join")
+            if slc is not None:
+                raise Unsupported("join slice")
+            if len(node.left_on) != 1 or len(node.right_on) != 1:
+                raise Unsupported("multi-key join")
+            lk = self.nt.view_expression(node.left_on[0].node)
+            rk = self.nt.view_expression(node.right_on[0].node)
+            if _name(lk) != "Column" or _name(rk) != "Column":
+                raise Unsupported("join keys must be plain columns")
+            left = self.child(node.input_left)
+            right = self.child(node.input_right)
+            order = str(order).lower()
+            return ("join", left, right, str(lk.name), str(rk.name), str(suffix), "m:m", bool(nulls_equal),
+                    order if order in ("none", "left", "right", "left_right", "right_left") else "none")
+        if k == "Sort":
+            if node.slice is not None:
+                raise Unsupported("sort slice")
+            if len(node.by_column) != 1:
+                raise Unsupported("multi-column sort")
+            by = self.nt.view_expression(node.by_column[0].node)
+            if _name(by) != "Column":
+                raise Unsupported("sort by an expression")
+            _maintain, nulls_last, descending = node.sort_options
+            child = self.child(node.input)
+            return ("sort", child, str(by.name), bool(descending[0]), bool(nulls_last[0]))
         if k in ("Filter", "Select", "HStack", "GroupBy", "SimpleProjection"):
             child = self.child(node.input)
             if k == "Filter":
@@ -187,6 +223,8 @@ def _bind_scans(node: tuple) -> tuple:
         if node[2] is not None:
             table = table.select(node[2])
         return ("scan", DataFrame.from_arrow(table))
+    if node[0] == "join":
+        return (node[0], _bind_scans(node[1]), _bind_scans(node[2])) + tuple(node[3:])
     return (node[0], _bind_scans(node[1])) + tuple(node[2:])
 
 

@@ -169,3 +169,43 @@ def test_udf_runs_on_gpu_and_matches(gpu):
         assert out.column("w")[i].as_py() == float(w[m].sum()) / int(m.sum())
         assert out.column("len")[i].as_py() == int(m.sum())
         assert out.column("cnt")[i].as_py() == int((m & vvalid).sum())
+
+
+def test_translate_join_and_sort():
+    table = _table()[0]
+    nt = FakeNT(table)
+    left = nt.p("DataFrameScan", ["k", "v", "w"], df=FakePolarsDF(table), projection=None, selection=None)
+    right = nt.p("DataFrameScan", ["k", "v", "w"], df=FakePolarsDF(table), projection=None, selection=None)
+    j = nt.p("Join", ["k", "v", "w", "v_right", "w_right"], input_left=left, input_right=right,
+             left_on=[PyExprIR(nt.col("k"), "k")], right_on=[PyExprIR(nt.col("k"), "k")],
+             options=("inner", False, None, "_right", True, "left"))
+    nt.p("Sort", ["k", "v", "w", "v_right", "w_right"], input=j, by_column=[PyExprIR(nt.col("w"), "w")],
+         sort_options=(False, [True], [True]), slice=None)
+    plan = PE.translate(nt)
+    assert plan[0] == "sort" and plan[2] == "w" and plan[3] is True and plan[4] is True
+    jn = plan[1]
+    assert jn[0] == "join" and jn[3] == "k" and jn[4] == "k" and jn[5] == "_right" and jn[8] == "left"
+    assert jn[1][0] == "polars_scan" and jn[2][0] == "polars_scan"
+    # outer joins, rolling expressions (NotImplemented in the visitor) stay on polars
+    nt.lp[j].options = ("full", False, None, "_right", True, "none")
+    with pytest.raises(PE.Unsupported):
+        PE.translate(nt)
+
+
+@pytest.mark.gpu
+def test_udf_join_sort_on_gpu(gpu):
+    table, k, v, w, vvalid = _table(20_000, 5)
+    right = pa.table({"k": pa.array(np.arange(13, dtype=np.int64)), "z": pa.array(np.arange(13) * 1.5)})
+    nt = FakeNT(table)
+    left = nt.p("DataFrameScan", ["k", "v", "w"], df=FakePolarsDF(table), projection=None, selection=None)
+    rs = nt.p("DataFrameScan", ["k", "z"], df=FakePolarsDF(right), projection=None, selection=None)
+    j = nt.p("Join", ["k", "v", "w", "z"], input_left=left, input_right=rs,
+             left_on=[PyExprIR(nt.col("k"), "k")], right_on=[PyExprIR(nt.col("k"), "k")],
+             options=("inner", False, None, "_right", True, "left"))
+    nt.p("Sort", ["k", "v", "w", "z"], input=j, by_column=[PyExprIR(nt.col("w"), "w")],
+         sort_options=(True, [False], [False]), slice=None)
+    PE.execute_with_polaroid(nt, None, to_frame=lambda t: t)
+    out = nt.udf(None, None, None, False)
+    order = np.argsort(w, kind="stable")
+    assert out.column("w").to_pylist() == w[order].tolist()
+    assert out.column("z").to_pylist() == (k[order] * 1.5).tolist()
