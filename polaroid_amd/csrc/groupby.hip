@@ -636,8 +636,9 @@ __global__ __launch_bounds__(kGbThreads) __attribute__((amdgpu_waves_per_eu(WPE)
     constexpr uint32_t VM = (1u << NACC) - 1u;
     int64_t t = blockIdx.x;
     FastTile<NACC, ROWS> cur;
-    if (t < ntiles) fast_load<NACC, PRED, ROWS>(p, t, cur);
+    if (ABL != 5 && t < ntiles) fast_load<NACC, PRED, ROWS>(p, t, cur);
     for (; t < ntiles; t += gridDim.x) {
+        if (ABL == 5) fast_load<NACC, PRED, ROWS>(p, t, cur);  // ablation: no prefetch
         // ---- predicate + batched LDS probes of the tile's rows
         int slot[ROWS];
         uint64_t probe[ROWS];
@@ -662,7 +663,7 @@ __global__ __launch_bounds__(kGbThreads) __attribute__((amdgpu_waves_per_eu(WPE)
         // ---- next tile's loads go out before this tile's atomics
         FastTile<NACC, ROWS> nxt;
         const int64_t tn = t + gridDim.x;
-        if (tn < ntiles) fast_load<NACC, PRED, ROWS>(p, tn, nxt);
+        if (ABL != 5 && tn < ntiles) fast_load<NACC, PRED, ROWS>(p, tn, nxt);
         // ---- apply rows one at a time (rolled; arrays shift statically)
 #pragma unroll 1
         for (int j = 0; j < ROWS; ++j) {
@@ -745,7 +746,7 @@ __global__ __launch_bounds__(kGbThreads) __attribute__((amdgpu_waves_per_eu(WPE)
                 for (int a = 0; a < NACC; ++a) cur.v[a][i] = cur.v[a][i + 1];
             }
         }
-        cur = nxt;
+        if (ABL != 5) cur = nxt;
     }
     if (SLIM) {
         __syncthreads();
@@ -1453,6 +1454,8 @@ static hipError_t launch_ablation(const Plan& pl, const DevProgram& dp, hipStrea
     case 5: return launch_fast_rows<4, 1, true, 2, 3, 0, 6>(pl, dp, s);
     case 6: return launch_fast_rows<4, 1, true, 2, 2, 0, 6>(pl, dp, s);
     case 7: return launch_fast_rows<4, 1, true, 2, 2, 0>(pl, dp, s);
+    case 8: return launch_fast_rows<4, 1, true, 2, 2, 5>(pl, dp, s);
+    case 9: return launch_fast_rows<4, 1, true, 4, 2, 5>(pl, dp, s);
     default: return launch_fast_rows<4, 1, true, 2, 3, 0>(pl, dp, s);
     }
 }

@@ -430,22 +430,21 @@ __global__ __launch_bounds__(256) void aos_pack_kernel(AosCols c, int64_t rows, 
     }
 }
 
+// NP/2 lanes cooperate on one row: each loads 16 bytes (two columns) of
+// it, so one load instruction of a wave fetches whole contiguous rows.
 template <int NC>
 __global__ __launch_bounds__(256) void aos_gather_kernel(const uint64_t* __restrict__ aos,
                                                          const uint32_t* __restrict__ idx, int64_t n, AosCols c) {
     constexpr int NP = (NC + 1) & ~1;
-    for (int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; o < n; o += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t r = __builtin_nontemporal_load(idx + o);
-        const ulonglong2* q = reinterpret_cast<const ulonglong2*>(aos + r * NP);
-        uint64_t v[NP];
-#pragma unroll
-        for (int k = 0; k < NP / 2; ++k) {
-            const ulonglong2 x = q[k];
-            v[2 * k] = x.x;
-            v[2 * k + 1] = x.y;
-        }
-#pragma unroll
-        for (int k = 0; k < NC; ++k) __builtin_nontemporal_store(v[k], c.dst[k] + o);
+    constexpr int L = NP / 2;  // lanes per row
+    const int64_t nl = n * L;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nl; t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t o = t / L;
+        const int q = (int)(t - o * L);
+        const int64_t r = idx[o];
+        const ulonglong2 x = reinterpret_cast<const ulonglong2*>(aos + r * NP)[q];
+        __builtin_nontemporal_store(x.x, c.dst[2 * q] + o);
+        if (2 * q + 1 < NC) __builtin_nontemporal_store(x.y, c.dst[2 * q + 1] + o);
     }
 }
 

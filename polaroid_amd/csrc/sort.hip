@@ -172,6 +172,7 @@ __global__ __launch_bounds__(kSrtThreads) void srt_downsweep_kernel(const uint64
     __shared__ uint64_t skey[kSrtTile];
     __shared__ uint32_t sidx[kSrtTile];
     __shared__ uint32_t dstart[256];
+    __shared__ uint64_t gbase[256];  // global position of local slot 0 of each digit run
     __shared__ uint32_t cnt[NW][256];
     __shared__ uint64_t wsum[NW];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -216,7 +217,9 @@ __global__ __launch_bounds__(kSrtThreads) void srt_downsweep_kernel(const uint64
             t += c[w];
         }
         uint64_t total;
-        dstart[tid] = (uint32_t)block_excl_scan(t, wsum, total);
+        const uint32_t ds = (uint32_t)block_excl_scan(t, wsum, total);
+        dstart[tid] = ds;
+        gbase[tid] = off[(int64_t)tid * ntiles + blockIdx.x] - ds;
     }
     __syncthreads();
 #pragma unroll
@@ -233,8 +236,7 @@ __global__ __launch_bounds__(kSrtThreads) void srt_downsweep_kernel(const uint64
     // coalesced write-out: consecutive threads, consecutive slots of a digit run
     for (int p = tid; p < m; p += kSrtThreads) {
         const uint64_t kk = skey[p];
-        const uint32_t d = (uint32_t)(kk >> shift) & 0xFF;
-        const uint64_t o = off[(int64_t)d * ntiles + blockIdx.x] + (uint64_t)(p - dstart[d]);
+        const uint64_t o = gbase[(kk >> shift) & 0xFF] + (uint64_t)p;
         keys_out[o] = kk;
         idx_out[o] = sidx[p];
     }

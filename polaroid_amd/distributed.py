@@ -105,7 +105,7 @@ class GpuPartial:
             self.handle = C.c_void_p()
 
     def __del__(self):
-        if N._lib is not None:
+        if N is not None and N._lib is not None:  # not during interpreter shutdown
             self.free()
 
     def begin(self, bottoms):
