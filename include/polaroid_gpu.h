@@ -208,6 +208,23 @@ int plgpu_group_by_agg(const plgpu_column* key, const plgpu_column* cols, int32_
                        int32_t naggs, int32_t maintain_order, plgpu_column* out_key,
                        plgpu_column* out_aggs, plgpu_groupby_info* info, void* stream);
 
+/* Group-by on 1..8 key columns (I64 / I32 / U32 / F64 / BOOL, nullable).
+ * Replaces the multi-key branch of DataFrame::group_by_with_series
+ * (polars-core/src/frame/group_by/mod.rs:91): the reference row-encodes the
+ * keys (chunked_array/ops/row_encode.rs:11) and groups the encoded rows, so
+ * groups are distinct key tuples, a null equal only to a null and f64 keys
+ * compared by TotalOrd.  Here the tuples are hashed to 64 bits, grouped by
+ * the single-key kernels, and every row is verified against its group's first
+ * row (a hash collision re-runs with another seed; PLGPU_ERR_CAPACITY after 4
+ * seeds).  `out_keys[nkeys]` take the key columns' dtypes and hold each
+ * group's first-row tuple; `maintain_order`, aggregations and the fused
+ * predicate are as for plgpu_group_by_agg. */
+int plgpu_group_by_agg_multi(const plgpu_column* keys, int32_t nkeys, const plgpu_column* cols,
+                             int32_t ncols, const plgpu_instr* program, int32_t n_instr,
+                             const plgpu_agg* aggs, int32_t naggs, int32_t maintain_order,
+                             plgpu_column* out_keys, plgpu_column* out_aggs,
+                             plgpu_groupby_info* info, void* stream);
+
 
 /* ---- hash-partitioned group-by (one process per GPU) ----------------------
  * Mirrors the partitioned sink of the streaming group-by

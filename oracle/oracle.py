@@ -194,6 +194,55 @@ def group_by_agg(key: HostCol, cols: list[HostCol], program, aggs: list[tuple[st
                                                        for o, v in zip(outs, outv)]
 
 
+def _row_words(values: np.ndarray, valid: np.ndarray | None) -> np.ndarray:
+    """One key column as 2 uint64 words per row (validity, canonical value):
+    the unordered row encoding of polars-core/src/chunked_array/ops/
+    row_encode.rs:11 up to a bijection (a null encodes as (0, 0); f64 by
+    TotalOrd: -0.0 == 0.0, every NaN equal)."""
+    n = values.shape[0]
+    v = np.ones(n, bool) if valid is None else valid.astype(bool)
+    if values.dtype == np.float64:
+        w = values.view(np.uint64).copy()
+        w[values == 0] = 0
+        w[np.isnan(values)] = 0x7FF8000000000000
+    elif values.dtype == np.bool_:
+        w = values.astype(np.uint64)
+    else:
+        w = values.astype(np.int64).view(np.uint64)
+    w = np.where(v, w, np.uint64(0))
+    return np.stack([v.astype(np.uint64), w], axis=1)
+
+
+def group_by_agg_multi(keys: list[tuple[np.ndarray, np.ndarray | None]], cols: list[HostCol], program,
+                       aggs: list[tuple[str, int]], nrows: int, sum_mode: int = SUM_EXACT):
+    """Group-by on several key columns, restating DataFrame::group_by_with_series
+    (polars-core/src/frame/group_by/mod.rs:91): rows are encoded
+    (row_encode.rs:11) and grouped by the encoded tuple.  The tuples get dense
+    ids here and or_group_by_agg aggregates by id.  Groups in first-occurrence
+    order of the selected rows; each group's key tuple is its first selected
+    row's.  Returns ([(key values, key valid)], [(agg values, agg valid)])."""
+    enc = np.concatenate([_row_words(v, m) for v, m in keys], axis=1) if nrows else np.zeros((0, 2), np.uint64)
+    if nrows:
+        _, inv = np.unique(enc, axis=0, return_inverse=True)
+        ids = inv.reshape(-1).astype(np.int64)
+    else:
+        ids = np.zeros(0, np.int64)
+    gids, _, outs = group_by_agg(HostCol(ids), cols, program, aggs, nrows, sum_mode)
+    if program:
+        _, sel, selv = eval_program(cols, program, nrows)
+        sel = sel & selv
+    else:
+        sel = np.ones(nrows, bool)
+    first = np.full(ids.max() + 1 if nrows else 1, np.iinfo(np.int64).max, np.int64)
+    rows = np.nonzero(sel)[0]
+    np.minimum.at(first, ids[rows], rows)  # first selected row per tuple id
+    rep = first[gids]
+    out_keys = []
+    for v, m in keys:
+        out_keys.append((v[rep], np.ones(rep.size, bool) if m is None else m[rep].astype(bool)))
+    return out_keys, outs
+
+
 def join_inner(left: HostCol, right: HostCol, nulls_equal: bool = False):
     """Inner-join row pairs in (left, right) order: (left_idx, right_idx)."""
     cap = 1 << 16

@@ -16,6 +16,7 @@ from . import _native
 from ._native import (
     ComputeError,
     DeviceError,
+    DuplicateError,
     InvalidOperationError,
     OutOfMemoryError,
     PolaroidError,
@@ -39,7 +40,7 @@ from .frame import (
 )
 
 __all__ = [
-    "Boolean", "ComputeError", "DataFrame", "DataType", "DeviceError", "Expr", "Float64", "GroupBy",
+    "Boolean", "ComputeError", "DataFrame", "DataType", "DeviceError", "DuplicateError", "Expr", "Float64", "GroupBy",
     "Int32", "Int64", "InvalidOperationError", "LazyFrame", "LazyGroupBy", "OutOfMemoryError",
     "PolaroidError", "Series", "ShapeError", "UInt32", "col", "count", "device_count", "from_dict",
     "len", "lit", "max", "mean", "min", "sum",

@@ -30,6 +30,7 @@ OP = dict(
 )
 AGG = dict(sum=1, mean=2, min=3, max=4, count=5, len=6)
 MAX_COLS = 8
+MAX_KEYS = 8
 
 
 class Column(C.Structure):
@@ -104,6 +105,9 @@ SIGNATURES = {
     "plgpu_group_by_agg": (C.c_int, [_COLP, _COLP, C.c_int32, C.POINTER(Instr), C.c_int32,
                                      C.POINTER(Agg), C.c_int32, C.c_int32, _COLP, _COLP,
                                      C.POINTER(GroupByInfo), _P]),
+    "plgpu_group_by_agg_multi": (C.c_int, [_COLP, C.c_int32, _COLP, C.c_int32, C.POINTER(Instr), C.c_int32,
+                                           C.POINTER(Agg), C.c_int32, C.c_int32, _COLP, _COLP,
+                                           C.POINTER(GroupByInfo), _P]),
     "plgpu_gb_record_words": (C.c_int, [_COLP, C.c_int32, C.POINTER(Agg), C.c_int32,
                                         C.POINTER(C.c_int32)]),
     "plgpu_gb_plan_bottoms": (C.c_int, [_COLP, _COLP, C.c_int32, C.POINTER(Agg), C.c_int32,
@@ -177,6 +181,10 @@ class InvalidOperationError(PolaroidError):
 
 
 class ShapeError(PolaroidError):
+    pass
+
+
+class DuplicateError(PolaroidError):
     pass
 
 

@@ -1510,6 +1510,7 @@ struct GbRun {
     float ms = 0.f;
     int32_t key_dtype = PLGPU_I64;
     bool maintain = false;
+    bool want_first = false;                 // keep each group's first selected row (multi-key)
     int world = 1;
     uint32_t wide = 0;                       // accs summed by the wide fallback
     int wide_exmin[kMaxAcc] = {0};
@@ -1551,7 +1552,9 @@ static int gb_prepare(GbRun& R, const plgpu_column* key, const plgpu_column* col
         if (R.dp.out_dtype != PLGPU_BOOL) return fail(PLGPU_ERR_SCHEMA, "filter predicate must be of type `Boolean`");
         R.pred = R.dp.simple ? 1 : 2;
     }
-    if ((rc = plan_groupby(key, cols, ncols, aggs, naggs, maintain_order, R.dp, &R.pl, force_counts))) return rc;
+    if ((rc = plan_groupby(key, cols, ncols, aggs, naggs, maintain_order || R.want_first, R.dp, &R.pl,
+                           force_counts)))
+        return rc;
     if ((rc = dev_alloc((void**)&R.status, ST_WORDS * 8 + kMaxAcc * 4, R.s))) return rc;
     R.bottoms = (int32_t*)(R.status + ST_WORDS);
     R.pl.p.status = R.status;
@@ -1819,7 +1822,10 @@ static void gb_fill_info(const GbRun& R, plgpu_groupby_info* info) {
 }
 
 // Global table -> output columns (+ first-occurrence order, key narrowing).
-static int gb_finalize(GbRun& R, int32_t naggs, plgpu_column* out_key, plgpu_column* out_aggs) {
+// `keep_first` (R.want_first): receives each output group's first selected
+// row, in output order (device buffer, caller frees).
+static int gb_finalize(GbRun& R, int32_t naggs, plgpu_column* out_key, plgpu_column* out_aggs,
+                       uint64_t** keep_first = nullptr) {
     Plan& pl = R.pl;
     GbParams& p = pl.p;
     hipStream_t s = R.s;
@@ -1833,7 +1839,7 @@ static int gb_finalize(GbRun& R, int32_t naggs, plgpu_column* out_key, plgpu_col
         rc = make_owned_column(&out_aggs[i], o.out_dtype, groups, nullable, s);
     }
     uint64_t* first = nullptr;
-    if (rc == PLGPU_OK && R.maintain && groups > 0) rc = dev_alloc((void**)&first, groups * 8, s);
+    if (rc == PLGPU_OK && (R.maintain || keep_first) && groups > 0) rc = dev_alloc((void**)&first, groups * 8, s);
     if (rc == PLGPU_OK && groups > 0) {
         fp.nout = naggs;
         for (int i = 0; i < naggs; ++i) {
@@ -1906,6 +1912,11 @@ static int gb_finalize(GbRun& R, int32_t naggs, plgpu_column* out_key, plgpu_col
                 rc = permute(out_key);
                 for (int i = 0; i < naggs && rc == PLGPU_OK; ++i) rc = permute(&out_aggs[i]);
                 dev_free(dperm, s);
+                if (rc == PLGPU_OK && keep_first) {
+                    // first rows in output order = the sorted first rows
+                    std::sort(hf.begin(), hf.end());
+                    (void)hipMemcpyAsync(first, hf.data(), groups * 8, hipMemcpyHostToDevice, s);
+                }
                 if (rc == PLGPU_OK) {
                     e = hipStreamSynchronize(s);  // keep `perm` alive until the copy ran
                     if (e != hipSuccess) rc = hip_fail(e, "permute");
@@ -1933,12 +1944,118 @@ static int gb_finalize(GbRun& R, int32_t naggs, plgpu_column* out_key, plgpu_col
         hipError_t e = hipStreamSynchronize(s);
         if (e != hipSuccess) rc = hip_fail(e, "finalize sync");
     }
+    if (rc == PLGPU_OK && keep_first) {
+        *keep_first = first;
+        first = nullptr;
+    }
     dev_free(first, s);
     if (rc) {
         plgpu_column_release(out_key);
         for (int i = 0; i < naggs; ++i) plgpu_column_release(&out_aggs[i]);
     }
     return rc;
+}
+
+// ------------------------------------------------------ multi-key group-by
+// The reference groups several key columns by row-encoding them
+// (polars-core/src/frame/group_by/mod.rs:91 encode_rows_vertical_par_unordered
+// -> chunked_array/ops/row_encode.rs:11) and grouping the encoded rows:
+// tuple equality, a null distinct from every value.  Here each row's tuple is
+// hashed to 64 bits in one pass, the single-key kernels group the hashes
+// (keeping each group's first row), and a verify pass checks every row's
+// tuple against its group's first row; a collision re-runs with a new seed.
+constexpr int kMaxKeys = 8;
+
+struct MkKeys {
+    DevCol c[kMaxKeys];
+    int32_t n;
+    int32_t _pad;
+};
+
+__device__ __forceinline__ uint64_t mk_fmix(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0xFF51AFD7ED558CCDull;
+    x ^= x >> 33;
+    x *= 0xC4CEB9FE1A85EC53ull;
+    x ^= x >> 33;
+    return x;
+}
+
+// Canonical key word: f64 keys compare by TotalOrd (-0 == 0, NaN == NaN).
+__device__ __forceinline__ uint64_t mk_word(const DevCol& c, int64_t r) {
+    uint64_t x = dev_load(c, r);
+    if (c.dtype == PLGPU_F64) {
+        if ((x & 0x7FFFFFFFFFFFFFFFull) == 0) x = 0;
+        else if ((x & 0x7FFFFFFFFFFFFFFFull) > 0x7FF0000000000000ull) x = 0x7FF8000000000000ull;
+    }
+    return x;
+}
+
+__global__ void mk_hash_kernel(MkKeys k, int64_t n, uint64_t seed, uint64_t mask, uint64_t* __restrict__ out) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t h = seed;
+        for (int i = 0; i < k.n; ++i) {
+            const DevCol& c = k.c[i];
+            const uint64_t w = dev_valid(c, r) ? mk_fmix(mk_word(c, r) ^ seed) : 0x6A09E667F3BCC909ull + (uint64_t)i;
+            h = mk_fmix(h * 0x9E3779B97F4A7C15ull + w + (uint64_t)i);
+        }
+        out[r] = h & mask;
+    }
+}
+
+// Read-only probe of the global table: slot of `key`, or -1.
+__device__ __forceinline__ int64_t g_lookup(const GbParams& p, uint64_t key) {
+    if (key == kEmptyKey) return p.gcap + 1;
+    const uint64_t mask = (uint64_t)p.gcap - 1;
+    const uint64_t h = p.gbits == 0 ? 0 : ((key * 0x9E3779B97F4A7C15ull) >> (64 - p.gbits));
+    const int lim = p.gcap < kGlobalProbe ? (int)p.gcap : kGlobalProbe;
+    for (int i = 0; i < lim; ++i) {
+        const uint64_t s = (h + (uint64_t)i) & mask;
+        const uint64_t k = p.gtab[s];
+        if (k == key) return (int64_t)s;
+        if (k == kEmptyKey) return -1;
+    }
+    return -1;
+}
+
+// Every row whose hash names a group must hold that group's tuple.  (Rows the
+// predicate dropped are checked too: a differing tuple there is a genuine
+// 64-bit collision as well, and only costs a re-run.)
+__global__ void mk_verify_kernel(GbParams p, MkKeys k, const uint64_t* __restrict__ hashes, int64_t n,
+                                 uint32_t* __restrict__ collision) {
+    bool bad = false;
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t s = g_lookup(p, hashes[r]);
+        if (s < 0 || *gfield(p, p.f_len, s) == 0) continue;
+        const int64_t rep = (int64_t)*gfield(p, p.f_first, s);
+        if (rep == r) continue;
+        for (int i = 0; i < k.n; ++i) {
+            const DevCol& c = k.c[i];
+            const bool va = dev_valid(c, r), vb = dev_valid(c, rep);
+            bad |= va != vb || (va && mk_word(c, r) != mk_word(c, rep));
+        }
+    }
+    if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(collision, 1u);
+}
+
+// out[g] = key column c at row rows[g] (validity bit-packed, zeroed first).
+__global__ void mk_gather_key_kernel(DevCol c, const uint64_t* __restrict__ rows, int64_t g_n, void* out,
+                                     uint32_t* out_valid) {
+    for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < g_n; g += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = (int64_t)rows[g];
+        const bool v = dev_valid(c, r);
+        const uint64_t x = dev_load(c, r);
+        switch (c.dtype) {
+        case PLGPU_F64:
+        case PLGPU_I64: ((uint64_t*)out)[g] = x; break;
+        case PLGPU_I32:
+        case PLGPU_U32: ((uint32_t*)out)[g] = (uint32_t)x; break;
+        default:
+            if (x & 1) atomicOr(&((uint32_t*)out)[g >> 5], 1u << (g & 31));
+            break;
+        }
+        if (out_valid && v) atomicOr(&out_valid[g >> 5], 1u << (g & 31));
+    }
 }
 
 }  // namespace plgpu
@@ -2105,4 +2222,100 @@ PLGPU_API int plgpu_gb_merge(const void* records, int64_t n_records, const plgpu
     }
     if (info) gb_fill_info(R, info);
     return gb_finalize(R, naggs, out_key, out_aggs);
+}
+
+// ------------------------------------------------------ multi-key group-by
+PLGPU_API int plgpu_group_by_agg_multi(const plgpu_column* keys, int32_t nkeys, const plgpu_column* cols,
+                                       int32_t ncols, const plgpu_instr* program, int32_t n_instr,
+                                       const plgpu_agg* aggs, int32_t naggs, int32_t maintain_order,
+                                       plgpu_column* out_keys, plgpu_column* out_aggs, plgpu_groupby_info* info,
+                                       void* stream) {
+    if (keys == nullptr || out_keys == nullptr) return fail(PLGPU_ERR_INVALID, "keys / out_keys is NULL");
+    if (nkeys < 1 || nkeys > kMaxKeys) return fail(PLGPU_ERR_INVALID, "number of key columns must be 1..8");
+    for (int i = 0; i < nkeys; ++i) std::memset(&out_keys[i], 0, sizeof(plgpu_column));
+    for (int i = 0; i < naggs && out_aggs; ++i) std::memset(&out_aggs[i], 0, sizeof(plgpu_column));
+    const int64_t n = keys[0].length;
+    MkKeys mk;
+    std::memset(&mk, 0, sizeof mk);
+    mk.n = nkeys;
+    for (int i = 0; i < nkeys; ++i) {
+        const int32_t dt = keys[i].dtype;
+        if (dt != PLGPU_I64 && dt != PLGPU_I32 && dt != PLGPU_U32 && dt != PLGPU_F64 && dt != PLGPU_BOOL)
+            return fail(PLGPU_ERR_SCHEMA, "group-by keys must be Int64, Int32, UInt32, Float64 or Boolean");
+        if (keys[i].length != n) return fail(PLGPU_ERR_SHAPE, "key columns must have equal lengths");
+        mk.c[i] = to_dev(keys[i]);
+    }
+    hipStream_t s = as_stream(stream);
+    uint64_t* hashes = nullptr;
+    uint32_t* collision = nullptr;
+    int rc = dev_alloc((void**)&hashes, (size_t)std::max<int64_t>(n, 1) * 8, s);
+    if (!rc) rc = dev_alloc((void**)&collision, 4, s);
+    plgpu_column hk;
+    std::memset(&hk, 0, sizeof hk);
+    hk.dtype = PLGPU_I64;
+    hk.length = n;
+    hk.values = hashes;
+    const int hg = (int)std::min<int64_t>((n + 255) / 256, (int64_t)num_cus() * 16);
+    bool done = false;
+    for (int attempt = 0; attempt < 4 && !rc && !done; ++attempt) {
+        const uint64_t seed = 0x243F6A8885A308D3ull * (uint64_t)(2 * attempt + 1);
+        // PLGPU_MK_COLLIDE (tests only): a 3-bit first hash forces the
+        // collision -> re-seed path
+        const uint64_t mask = attempt == 0 && getenv("PLGPU_MK_COLLIDE") ? 7ull : ~0ull;
+        if (n > 0) mk_hash_kernel<<<std::max(hg, 1), 256, 0, s>>>(mk, n, seed, mask, hashes);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) { rc = hip_fail(e, "mk_hash_kernel"); break; }
+        GbRun R;
+        R.want_first = true;
+        rc = gb_prepare(R, &hk, cols, ncols, program, n_instr, aggs, naggs, maintain_order != 0, false, stream);
+        if (!rc) rc = gb_plan(R, nullptr);
+        if (!rc) rc = gb_main(R, true, nullptr, nullptr);
+        if (rc) break;
+        plgpu_column hout;
+        uint64_t* first = nullptr;
+        if ((rc = gb_finalize(R, naggs, &hout, out_aggs, &first))) break;
+        const int64_t groups = hout.length;
+        plgpu_column_release(&hout);
+        uint32_t coll = 0;
+        if (n > 0 && groups > 0) {
+            (void)hipMemsetAsync(collision, 0, 4, s);
+            mk_verify_kernel<<<std::max(hg, 1), 256, 0, s>>>(R.pl.p, mk, hashes, n, collision);
+            e = hipGetLastError();
+            if (e == hipSuccess) e = hipMemcpyAsync(&coll, collision, 4, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e != hipSuccess) rc = hip_fail(e, "mk_verify_kernel");
+        }
+        if (!rc && !coll) {
+            const int gg = (int)std::min<int64_t>((groups + 255) / 256, 4096);
+            for (int i = 0; i < nkeys && !rc; ++i) {
+                const bool nullable = keys[i].validity != nullptr;
+                rc = make_owned_column(&out_keys[i], keys[i].dtype, groups, nullable, s);
+                if (rc || groups == 0) continue;
+                if (keys[i].dtype == PLGPU_BOOL) (void)hipMemsetAsync((void*)out_keys[i].values, 0, ((groups + 63) / 64) * 8, s);
+                if (nullable) (void)hipMemsetAsync((void*)out_keys[i].validity, 0, ((groups + 63) / 64) * 8, s);
+                mk_gather_key_kernel<<<gg, 256, 0, s>>>(mk.c[i], first, groups, (void*)out_keys[i].values,
+                                                        (uint32_t*)out_keys[i].validity);
+                e = hipGetLastError();
+                if (e != hipSuccess) rc = hip_fail(e, "mk_gather_key_kernel");
+            }
+            if (!rc) {
+                e = hipStreamSynchronize(s);
+                if (e != hipSuccess) rc = hip_fail(e, "multi-key gather");
+            }
+            if (!rc && info) {
+                gb_fill_info(R, info);
+                info->reruns += attempt;
+            }
+            done = !rc;
+        }
+        dev_free(first, s);
+        if (!done)
+            for (int i = 0; i < naggs; ++i) plgpu_column_release(&out_aggs[i]);
+    }
+    dev_free(collision, s);
+    dev_free(hashes, s);
+    if (!rc && !done) rc = fail(PLGPU_ERR_CAPACITY, "multi-key group-by: unresolved 64-bit hash collisions");
+    if (rc)
+        for (int i = 0; i < nkeys; ++i) plgpu_column_release(&out_keys[i]);
+    return rc;
 }

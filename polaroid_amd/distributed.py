@@ -178,6 +178,8 @@ def group_by_agg(df, key: str, aggs: Sequence[Expr], predicate: Expr | None = No
         raise N.InvalidOperationError("the GPU group-by needs the nccl (RCCL) backend")
     aggs = [a if isinstance(a, Expr) else col(a) for a in aggs]
     g = _gb_lower(df, key, list(aggs), predicate)
+    if g.keycol.dtype not in (N.I64, N.I32) or len(g.keys) != 1:
+        raise N.InvalidOperationError("the multi-GPU group-by takes one Int64 / Int32 key column")
     part = GpuPartial(g, world)
     out, mi = run_partitioned(part, world, group, device)
     torch.cuda.synchronize()

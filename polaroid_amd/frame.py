@@ -543,9 +543,14 @@ class LazyFrame:
 class LazyGroupBy:
     def __init__(self, lf: LazyFrame, by: Sequence[Any], maintain_order: bool):
         keys = _parse_exprs(by)
-        if builtins.len(keys) != 1 or keys[0].kind != "col":
-            raise N.InvalidOperationError("the GPU executor groups by exactly one key column")
-        self._lf, self._key, self._maintain = lf, keys[0].value, maintain_order
+        if not keys or any(k.kind != "col" for k in keys) or builtins.len(keys) > N.MAX_KEYS:
+            raise N.InvalidOperationError("the GPU executor groups by 1..8 plain key columns")
+        names = [k.value for k in keys]
+        if builtins.len(set(names)) != builtins.len(names):
+            raise N.DuplicateError("group-by keys must be distinct columns")
+        # one key: its name; several: a tuple of names (plan node field 2)
+        self._lf, self._maintain = lf, maintain_order
+        self._key = names[0] if builtins.len(names) == 1 else tuple(names)
 
     def agg(self, *aggs: Any, **named: Any) -> LazyFrame:
         exprs = _parse_exprs(aggs) + [e.alias(k) for k, e in named.items()]
@@ -682,20 +687,32 @@ class _GbCall:
     """Lowered arguments of one group-by call through the C-ABI (shared by
     the single-GPU path and polaroid_amd.distributed)."""
 
-    __slots__ = ("key", "keycol", "names", "cols", "ncols", "prog", "n_instr", "aggs", "naggs",
+    __slots__ = ("key", "keys", "keycol", "keycols", "names", "cols", "ncols", "prog", "n_instr", "aggs", "naggs",
                  "out_names", "_keep")
 
 
-def _gb_lower(df: DataFrame, key: str, aggs: list[Expr], pred: Expr | None) -> _GbCall:
-    if key not in df._cols:
-        raise N.ComputeError(f'unable to find column "{key}"')
+def _gb_keys(key: str | tuple) -> list[str]:
+    return [key] if isinstance(key, str) else list(key)
+
+
+def _gb_lower(df: DataFrame, key: str | tuple, aggs: list[Expr], pred: Expr | None) -> _GbCall:
+    keys = _gb_keys(key)
+    for k in keys:
+        if k not in df._cols:
+            raise N.ComputeError(f'unable to find column "{k}"')
+    key = keys[0]
+    # len() needs some aggregatable column for its accumulator slot (it only
+    # reads the group's row count): the first non-Boolean key, else any column
+    len_col = next((k for k in keys if df._cols[k].dtype is not Boolean), None)
+    if len_col is None:
+        len_col = next((c for c in df.columns if df._cols[c].dtype is not Boolean), key)
     specs: list[tuple[str, str]] = []  # (kind, column)
     out_names: list[str] = []
     for e in aggs:
         name = e.output_name()
         base = e.args[0] if e.kind == "alias" else e
         if base.kind == "len":
-            specs.append(("len", key))
+            specs.append(("len", len_col))
         elif base.kind == "agg" and base.args[0].kind == "col":
             specs.append((base.op, base.args[0].value))
         else:
@@ -726,33 +743,46 @@ def _gb_lower(df: DataFrame, key: str, aggs: list[Expr], pred: Expr | None) -> _
         agg_arr[i].kind = _AGG_CODE[k]
         agg_arr[i].col = idx[c_]
     g.key = key
+    g.keys = keys
     g.keycol = df._cols[key]._col
+    g.keycols = _col_array([df._cols[k] for k in keys])
     g.names = names
     g.cols = _col_array([df._cols[nm] for nm in names])
     g.ncols = builtins.len(names)
     g.aggs = agg_arr
     g.naggs = builtins.len(specs)
     g.out_names = out_names
-    g._keep = [df._cols[nm] for nm in names] + [df._cols[key]]
+    g._keep = [df._cols[nm] for nm in names] + [df._cols[k] for k in keys]
     return g
 
 
-def _gb_frame(g: _GbCall, out_key: N.Column, out_aggs) -> DataFrame:
-    series = [Series._from_native(g.key, out_key)]
+def _gb_frame(g: _GbCall, out_key, out_aggs) -> DataFrame:
+    """`out_key`: one Column, or an array of len(g.keys) Columns."""
+    if isinstance(out_key, N.Column):
+        series = [Series._from_native(g.key, out_key)]
+    else:
+        series = [Series._from_native(k, out_key[i]) for i, k in enumerate(g.keys)]
     for i, nm in enumerate(g.out_names):
         series.append(Series._from_native(nm, out_aggs[i]))
     return DataFrame(series)
 
 
-def _group_by(df: DataFrame, key: str, aggs: list[Expr], maintain_order: bool,
+def _group_by(df: DataFrame, key: str | tuple, aggs: list[Expr], maintain_order: bool,
               pred: Expr | None, info: dict | None) -> DataFrame:
     g = _gb_lower(df, key, aggs, pred)
-    out_key = N.Column()
     out_aggs = (N.Column * max(1, g.naggs))()
     gi = N.GroupByInfo()
-    N.check(N.lib().plgpu_group_by_agg(C.byref(g.keycol), g.cols, g.ncols, g.prog, g.n_instr, g.aggs,
-                                       g.naggs, int(bool(maintain_order)), C.byref(out_key),
-                                       out_aggs, C.byref(gi), None))
+    if builtins.len(g.keys) == 1 and g.keycol.dtype in (N.I64, N.I32):
+        out_key = N.Column()
+        N.check(N.lib().plgpu_group_by_agg(C.byref(g.keycol), g.cols, g.ncols, g.prog, g.n_instr, g.aggs,
+                                           g.naggs, int(bool(maintain_order)), C.byref(out_key),
+                                           out_aggs, C.byref(gi), None))
+    else:
+        # several keys (or a UInt32 / Float64 / Boolean key): hashed tuples
+        out_key = (N.Column * builtins.len(g.keys))()
+        N.check(N.lib().plgpu_group_by_agg_multi(g.keycols, builtins.len(g.keys), g.cols, g.ncols, g.prog,
+                                                 g.n_instr, g.aggs, g.naggs, int(bool(maintain_order)),
+                                                 out_key, out_aggs, C.byref(gi), None))
     if info is not None:
         info.update(gi.as_dict())
     return _gb_frame(g, out_key, out_aggs)

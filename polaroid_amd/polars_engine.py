@@ -189,15 +189,18 @@ class _Translator:
                 raise Unsupported("dynamic / rolling group-by")
             if getattr(opts, "slice", None) is not None:
                 raise Unsupported("group-by slice")
-            if len(node.keys) != 1:
-                raise Unsupported("multi-key group-by")
-            kx = self.nt.view_expression(node.keys[0].node)
-            if _name(kx) != "Column" or str(kx.name) != node.keys[0].output_name:
-                raise Unsupported("group-by key must be a plain column")
-            key = str(kx.name)
+            if not 1 <= len(node.keys) <= 8:
+                raise Unsupported("group-by on more than 8 keys")
+            names = []
+            for ki in node.keys:
+                kx = self.nt.view_expression(ki.node)
+                if _name(kx) != "Column" or str(kx.name) != ki.output_name:
+                    raise Unsupported("group-by key must be a plain column")
+                names.append(str(kx.name))
+            key = names[0] if len(names) == 1 else tuple(names)
             aggs = []
             for ai in node.aggs:
-                a = self.agg(ai.node, key)
+                a = self.agg(ai.node, names[0])
                 aggs.append(a.alias(ai.output_name))
             return ("group_by", child, key, aggs, bool(node.maintain_order))
         raise Unsupported(f"plan node {k}")

@@ -148,6 +148,51 @@ def group_by_cases():
 
 
 # ---------------------------------------------------------------------------
+# 2b. Multi-key group-by cases.  String / date keys of the reference tests are
+#     label-encoded into integers (tuple equality is unchanged by a
+#     bijection); a list aggregation (`agg(pl.col("c"))`) is checked through
+#     its per-group lengths (`len`).
+def group_by_multi_cases():
+    cases = []
+    cases.append({
+        "name": "test_nan_in_group_by_agg",
+        "source": "datatypes/test_float.py:8-18",
+        "keys": {"bar": {"dtype": "i64", "values": [0, 0, 0, 0]},
+                 "key": {"dtype": "i64", "values": [0, 0, 0, 0], "labels": ["a"]}},
+        "cols": {"value": {"dtype": "f64", "values": fx([18.58, 18.78, float("nan"), 18.63])}},
+        "aggs": [["max", "value", "max"], ["min", "value", "min"]], "maintain_order": False,
+        "expected": {"bar": [0], "key": [0], "max": fx([18.78]), "min": fx([18.58])},
+    })
+    cases.append({
+        "name": "test_group_by_partitioned_ending_cast",
+        "source": "operations/test_group_by.py:968-973",
+        "keys": {"a": {"dtype": "i64", "values": [1] * 5}, "b": {"dtype": "i64", "values": [1] * 5}},
+        "cols": {"a": {"dtype": "i64", "values": [1] * 5}},
+        "aggs": [["len", "a", "num"]], "maintain_order": False,
+        "expected": {"a": [1], "b": [1], "num": [5]},
+    })
+    cases.append({
+        "name": "test_group_by_with_null",
+        "source": "operations/test_group_by.py:1080-1089",
+        "keys": {"a": {"dtype": "i64", "values": [None, None, None, None]},
+                 "b": {"dtype": "i64", "values": [1, 1, 2, 2]}},
+        "cols": {"c": {"dtype": "i64", "values": [0, 1, 2, 3], "labels": ["x", "y", "z", "u"]}},
+        "aggs": [["len", "c", "c_len"]], "maintain_order": True,
+        "expected": {"a": [None, None], "b": [1, 2], "c_len": [2, 2]},
+    })
+    cases.append({
+        "name": "test_streaming_literal_group_by_mean",
+        "source": "streaming/test_streaming.py:100-118",
+        "keys": {"x": {"dtype": "i64", "values": [0, 0], "labels": ["constant"]},
+                 "y": {"dtype": "i64", "values": [0, 1], "labels": ["a", "b"]}},
+        "cols": {"z": {"dtype": "i64", "values": [1, 2]}},
+        "aggs": [["mean", "z", "z"]], "maintain_order": False, "sort_by": "y",
+        "expected": {"x": [0, 0], "y": [0, 1], "z": fx([1.0, 2.0])},
+    })
+    return {"cases": cases}
+
+
+# ---------------------------------------------------------------------------
 # 3. Filter cases.
 def filter_cases():
     cases = []
@@ -352,6 +397,7 @@ def rolling_cases():
 def main():
     for name, obj in (("compare_total_order.json", compare_table()),
                       ("group_by_cases.json", group_by_cases()),
+                      ("group_by_multi_cases.json", group_by_multi_cases()),
                       ("filter_cases.json", filter_cases()),
                       ("join_cases.json", join_cases()),
                       ("sort_cases.json", sort_cases()),

@@ -61,6 +61,14 @@ def test_plan_pushes_filter_into_group_by():
     assert "FILTER" in text
 
 
-def test_group_by_needs_one_key():
+def test_group_by_key_validation():
+    lf = pl.LazyFrame(("scan", pl.DataFrame({})))
+    g = lf.group_by("a", "b")  # several keys: a tuple in the plan node
+    assert g._key == ("a", "b")
+    assert lf.group_by("a")._key == "a"
     with pytest.raises(pl.InvalidOperationError):
-        pl.LazyFrame(("scan", pl.DataFrame({}))).group_by("a", "b")
+        lf.group_by(pl.col("a") + 1)
+    with pytest.raises(pl.InvalidOperationError):
+        lf.group_by(*[f"k{i}" for i in range(9)])
+    with pytest.raises(pl.DuplicateError):
+        lf.group_by("a", "a")

@@ -281,3 +281,60 @@ def test_oracle_rolling_reference_vs_exact_ulp():
             else:
                 scale = mag if kind == "sum" else mag / np.minimum(i + 1, w)
                 assert (np.abs(r - e) / scale).max() <= 1e-12, (w, kind)
+
+
+def _spec_arr(spec):
+    """Fixture column -> (numpy values, validity or None)."""
+    vals = unhex(spec["values"]) if spec["dtype"] == "f64" else spec["values"]
+    valid = np.array([v is not None for v in vals], dtype=bool)
+    dt = np.float64 if spec["dtype"] == "f64" else np.int64
+    arr = np.array([(0.0 if dt is np.float64 else 0) if v is None else v for v in vals], dtype=dt)
+    return arr, (None if valid.all() else valid)
+
+
+def test_group_by_multi_golden():
+    """Multi-key fixtures (tests/golden/group_by_multi_cases.json) through the
+    row-encoding restatement (oracle.group_by_agg_multi)."""
+    for case in load_golden("group_by_multi_cases.json")["cases"]:
+        keys = [_spec_arr(s) for s in case["keys"].values()]
+        cols, names = _case_cols(case)
+        aggs = [(a[0], names.index(a[1])) for a in case["aggs"]]
+        okeys, outs = O.group_by_agg_multi(keys, cols, None, aggs, len(keys[0][0]))
+        knames = list(case["keys"])
+        order = np.arange(len(okeys[0][0]))
+        if "sort_by" in case:
+            order = np.argsort(okeys[knames.index(case["sort_by"])][0], kind="stable")
+        for kn, (v, m) in zip(knames, okeys):
+            got = [x if ok else None for x, ok in zip(v[order].tolist(), m[order].tolist())]
+            assert got == case["expected"][kn], (case["name"], kn, got)
+        for a, (v, m) in zip(case["aggs"], outs):
+            exp = unhex(case["expected"][a[2]])
+            got = [x if ok else None for x, ok in zip(v[order].tolist(), m[order].tolist())]
+            assert all(_same(x, y) for x, y in zip(got, exp)), (case["name"], a, got, exp)
+
+
+def test_group_by_multi_matches_tuple_dict():
+    """The multi-key restatement against a plain dict of tuples (nulls, -0.0
+    / NaN keys, predicate-free)."""
+    rng = np.random.default_rng(3)
+    n = 3000
+    a = rng.integers(0, 4, n).astype(np.int64)
+    av = rng.random(n) > 0.2
+    b = rng.choice(np.array([0.0, -0.0, np.nan, 1.5]), n)
+    c = rng.random(n) < 0.5
+    x = rng.standard_normal(n)
+    okeys, outs = O.group_by_agg_multi([(a, av), (b, None), (c, None)], [O.HostCol(x)], None,
+                                       [("sum", 0), ("len", 0)], n)
+    exp = {}
+    for i in range(n):
+        t = (int(a[i]) if av[i] else None, "nan" if np.isnan(b[i]) else float(b[i]) + 0.0, bool(c[i]))
+        exp.setdefault(t, []).append(x[i])
+    got = {}
+    for g in range(len(okeys[0][0])):
+        bv = okeys[1][0][g]
+        t = (int(okeys[0][0][g]) if okeys[0][1][g] else None, "nan" if np.isnan(bv) else float(bv) + 0.0,
+             bool(okeys[2][0][g]))
+        got[t] = (outs[0][0][g], int(outs[1][0][g]))
+    assert set(got) == set(exp)
+    for t, xs in exp.items():
+        assert got[t] == (math.fsum(xs), len(xs))

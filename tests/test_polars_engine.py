@@ -138,7 +138,7 @@ def test_unsupported_leaves_plan_to_polars():
     assert nt.udf is None
     with pytest.raises(pl.InvalidOperationError):
         PE.execute_with_polaroid(nt, None, config={"raise_on_fail": True})
-    # NaN-propagating min (nan_min) and multi-key group-by are outside the path too
+    # NaN-propagating min (nan_min) is outside the path too
     nt2 = _filter_groupby_ir(table)
     nt2.lp[nt2.root].aggs[0] = PyExprIR(nt2.e("Agg", name="min", arguments=[nt2.col("v")], options=True), "v")
     with pytest.raises(PE.Unsupported):
@@ -209,3 +209,33 @@ def test_udf_join_sort_on_gpu(gpu):
     order = np.argsort(w, kind="stable")
     assert out.column("w").to_pylist() == w[order].tolist()
     assert out.column("z").to_pylist() == (k[order] * 1.5).tolist()
+
+
+def test_translate_multi_key_group_by():
+    table = _table()[0]
+    nt = _filter_groupby_ir(table)
+    nt.lp[nt.root].keys.append(PyExprIR(nt.col("w"), "w"))
+    plan = PE.translate(nt)
+    assert plan[0] == "group_by" and plan[2] == ("k", "w")
+    # a computed key stays on polars
+    nt.lp[nt.root].keys[1] = PyExprIR(nt.bin(nt.col("w"), "Plus", nt.lit(1)), "w")
+    with pytest.raises(PE.Unsupported):
+        PE.translate(nt)
+
+
+@pytest.mark.gpu
+def test_udf_multi_key_group_by_on_gpu(gpu):
+    table, k, v, w, vvalid = _table(50_000, 8)
+    nt = _filter_groupby_ir(table)
+    nt.lp[nt.root].keys.append(PyExprIR(nt.col("w"), "w"))
+    nt.schemas[nt.root] = ["k", "w", "v", "w_mean", "len", "cnt"]
+    nt.lp[nt.root].aggs[1] = PyExprIR(nt.e("Agg", name="mean", arguments=[nt.col("w")], options=None), "w_mean")
+    PE.execute_with_polaroid(nt, None, to_frame=lambda t: t)
+    out = nt.udf(None, None, None, False)
+    sel = ((v > 0.5) & vvalid) | (w == 3)
+    first = list(dict.fromkeys(zip(k[sel].tolist(), w[sel].tolist())))
+    assert list(zip(out.column("k").to_pylist(), out.column("w").to_pylist())) == first
+    for i, (kk, ww) in enumerate(first):
+        m = sel & (k == kk) & (w == ww)
+        assert out.column("v")[i].as_py() == math.fsum(v[m & vvalid])
+        assert out.column("len")[i].as_py() == int(m.sum())
