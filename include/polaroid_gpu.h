@@ -310,6 +310,19 @@ int plgpu_join_inner(const plgpu_column* left_key, const plgpu_column* right_key
                      int32_t nulls_equal, int32_t maintain_order, int32_t validate,
                      plgpu_column* out_left_idx, plgpu_column* out_right_idx, void* stream);
 
+/* Inner join on 1..8 key columns per side (pairwise equal dtypes: I64 / I32 /
+ * U32 / F64 / BOOL).  Replaces the multi-key branch of the reference's join
+ * (polars-ops/src/frame/join/mod.rs:625 prepare_keys_multiple: both sides'
+ * keys row-encoded, then hash-joined as binary keys; a tuple holding a null
+ * joins only when nulls_equal).  Here tuples are hashed to 64 bits
+ * (tuplehash.hpp), joined with the single-key kernels, and every output pair
+ * is verified tuple by tuple (a collision re-runs with another seed).
+ * Arguments, output and order modes as plgpu_join_inner. */
+int plgpu_join_inner_multi(const plgpu_column* left_keys, const plgpu_column* right_keys,
+                           int32_t nkeys, int32_t nulls_equal, int32_t maintain_order,
+                           int32_t validate, plgpu_column* out_left_idx,
+                           plgpu_column* out_right_idx, void* stream);
+
 /* out_cols[i] = cols[i][idx] (UInt32 indices, no nulls), validity carried.
  * Replaces the join materialisation take
  * (polars-core/src/chunked_array/ops/gather.rs, DataFrame::take_unchecked). */

@@ -256,6 +256,37 @@ def join_inner(left: HostCol, right: HostCol, nulls_equal: bool = False):
         cap *= 4
 
 
+def join_inner_multi(left_keys: list[tuple[np.ndarray, np.ndarray | None]],
+                     right_keys: list[tuple[np.ndarray, np.ndarray | None]], nulls_equal: bool = False):
+    """Inner join on several key columns, restating the reference's multi-key
+    join (polars-ops/src/frame/join/mod.rs:625 prepare_keys_multiple): both
+    sides' key tuples are row-encoded (row_encode.rs:11) and joined as one
+    key; without nulls_equal a tuple holding a null is a null key
+    (encode_rows_vertical_par_unordered_broadcast_nulls).  Here equal tuples
+    get one dense id and or_join_inner joins the ids.  Pairs in (left, right)
+    order."""
+    nl, nr = left_keys[0][0].shape[0], right_keys[0][0].shape[0]
+    enc_l = np.concatenate([_row_words(v, m) for v, m in left_keys], axis=1)
+    enc_r = np.concatenate([_row_words(v, m) for v, m in right_keys], axis=1)
+    enc = np.concatenate([enc_l, enc_r], axis=0)
+    if nl + nr:
+        _, inv = np.unique(enc, axis=0, return_inverse=True)
+        ids = inv.reshape(-1).astype(np.int64)
+    else:
+        ids = np.zeros(0, np.int64)
+
+    def valid(keys, n):
+        v = np.ones(n, bool)
+        if not nulls_equal:
+            for _, m in keys:
+                if m is not None:
+                    v &= m.astype(bool)
+        return None if v.all() else v
+
+    return join_inner(HostCol(ids[:nl].copy(), valid(left_keys, nl)), HostCol(ids[nl:].copy(), valid(right_keys, nr)),
+                      nulls_equal)
+
+
 def arg_sort(col: HostCol, descending: bool = False, nulls_last: bool = False) -> np.ndarray:
     out = np.zeros(max(col.c.length, 1), np.int64)
     lib().or_arg_sort(C.byref(col.c), int(descending), int(nulls_last), out.ctypes.data)

@@ -34,6 +34,7 @@
 #include <vector>
 
 #include "plgpu_internal.hpp"
+#include "tuplehash.hpp"
 
 namespace plgpu {
 
@@ -1964,42 +1965,9 @@ static int gb_finalize(GbRun& R, int32_t naggs, plgpu_column* out_key, plgpu_col
 // hashed to 64 bits in one pass, the single-key kernels group the hashes
 // (keeping each group's first row), and a verify pass checks every row's
 // tuple against its group's first row; a collision re-runs with a new seed.
-constexpr int kMaxKeys = 8;
-
-struct MkKeys {
-    DevCol c[kMaxKeys];
-    int32_t n;
-    int32_t _pad;
-};
-
-__device__ __forceinline__ uint64_t mk_fmix(uint64_t x) {
-    x ^= x >> 33;
-    x *= 0xFF51AFD7ED558CCDull;
-    x ^= x >> 33;
-    x *= 0xC4CEB9FE1A85EC53ull;
-    x ^= x >> 33;
-    return x;
-}
-
-// Canonical key word: f64 keys compare by TotalOrd (-0 == 0, NaN == NaN).
-__device__ __forceinline__ uint64_t mk_word(const DevCol& c, int64_t r) {
-    uint64_t x = dev_load(c, r);
-    if (c.dtype == PLGPU_F64) {
-        if ((x & 0x7FFFFFFFFFFFFFFFull) == 0) x = 0;
-        else if ((x & 0x7FFFFFFFFFFFFFFFull) > 0x7FF0000000000000ull) x = 0x7FF8000000000000ull;
-    }
-    return x;
-}
-
 __global__ void mk_hash_kernel(MkKeys k, int64_t n, uint64_t seed, uint64_t mask, uint64_t* __restrict__ out) {
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
-        uint64_t h = seed;
-        for (int i = 0; i < k.n; ++i) {
-            const DevCol& c = k.c[i];
-            const uint64_t w = dev_valid(c, r) ? mk_fmix(mk_word(c, r) ^ seed) : 0x6A09E667F3BCC909ull + (uint64_t)i;
-            h = mk_fmix(h * 0x9E3779B97F4A7C15ull + w + (uint64_t)i);
-        }
-        out[r] = h & mask;
+        out[r] = mk_row_hash(k, r, seed) & mask;
     }
 }
 
@@ -2028,12 +1996,7 @@ __global__ void mk_verify_kernel(GbParams p, MkKeys k, const uint64_t* __restric
         const int64_t s = g_lookup(p, hashes[r]);
         if (s < 0 || *gfield(p, p.f_len, s) == 0) continue;
         const int64_t rep = (int64_t)*gfield(p, p.f_first, s);
-        if (rep == r) continue;
-        for (int i = 0; i < k.n; ++i) {
-            const DevCol& c = k.c[i];
-            const bool va = dev_valid(c, r), vb = dev_valid(c, rep);
-            bad |= va != vb || (va && mk_word(c, r) != mk_word(c, rep));
-        }
+        if (rep != r) bad |= !mk_equal(k, r, k, rep);
     }
     if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(collision, 1u);
 }

@@ -31,6 +31,7 @@
 
 #include "plgpu_internal.hpp"
 #include "scan.hpp"
+#include "tuplehash.hpp"
 
 namespace plgpu {
 
@@ -690,18 +691,14 @@ static int check_key(const plgpu_column* k) {
     return PLGPU_OK;
 }
 
-PLGPU_API int plgpu_join_inner(const plgpu_column* left_key, const plgpu_column* right_key, int32_t nulls_equal,
-                               int32_t maintain_order, int32_t validate, plgpu_column* out_left_idx,
-                               plgpu_column* out_right_idx, void* stream) {
-    hipStream_t s = as_stream(stream);
+// Inner join of two checked key columns (validation failures return
+// PLGPU_ERR_SCHEMA; nothing else does).
+static int join_inner_impl(const plgpu_column* left_key, const plgpu_column* right_key, bool neq,
+                           int32_t maintain_order, int32_t validate, plgpu_column* out_left_idx,
+                           plgpu_column* out_right_idx, hipStream_t s) {
     int rc;
-    if ((rc = check_key(left_key)) || (rc = check_key(right_key))) return rc;
-    if (out_left_idx == nullptr || out_right_idx == nullptr) return fail(PLGPU_ERR_INVALID, "NULL output");
-    if (maintain_order < PLGPU_JOIN_ORDER_NONE || maintain_order > PLGPU_JOIN_ORDER_RIGHT_LEFT)
-        return fail(PLGPU_ERR_INVALID, "invalid maintain_order");
     std::memset(out_left_idx, 0, sizeof *out_left_idx);
     std::memset(out_right_idx, 0, sizeof *out_right_idx);
-    const bool neq = nulls_equal != 0;
     // the probe order decides the output order: probe the side whose order
     // must be kept; otherwise build on the shorter side as the reference does
     bool build_right;
@@ -744,6 +741,149 @@ PLGPU_API int plgpu_join_inner(const plgpu_column* left_key, const plgpu_column*
         else rc = jn_probe(right_key, b, neq, out_right_idx, out_left_idx, s);
     }
     jn_free(b, s);
+    (void)hipStreamSynchronize(s);
+    return rc;
+}
+
+// ------------------------------------------------------- multi-key join
+// Key tuples -> 64-bit hashes (tuplehash.hpp); a tuple holding a null is a
+// null key unless nulls_equal.  Validity is written one wave ballot per 64
+// rows (grid-stride bases are multiples of 64).
+__global__ __launch_bounds__(256) void jn_tuple_hash_kernel(MkKeys k, int64_t n, uint64_t seed, uint64_t mask, bool neq,
+                                                            uint64_t* __restrict__ hash,
+                                                            uint64_t* __restrict__ valid_words) {
+    for (int64_t r0 = (int64_t)blockIdx.x * blockDim.x; r0 < n; r0 += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = r0 + threadIdx.x;
+        const bool in = r < n;
+        const bool v = in && (neq || !mk_any_null(k, r));
+        if (in) hash[r] = mk_row_hash(k, r, seed) & mask;
+        const uint64_t b = __ballot(v);
+        const int64_t w0 = r - (threadIdx.x & 63);
+        if ((threadIdx.x & 63) == 0 && w0 < n) valid_words[w0 >> 6] = b;
+    }
+}
+
+// Every output pair must join equal tuples (a hash collision otherwise).
+__global__ __launch_bounds__(256) void jn_verify_kernel(MkKeys a, MkKeys b, const uint32_t* __restrict__ ia,
+                                                        const uint32_t* __restrict__ ib, int64_t n,
+                                                        uint32_t* __restrict__ bad) {
+    bool x = false;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        x |= !mk_equal(a, ia[i], b, ib[i]);
+    if (__any(x) && (threadIdx.x & 63) == 0) atomicOr(bad, 1u);
+}
+
+PLGPU_API int plgpu_join_inner(const plgpu_column* left_key, const plgpu_column* right_key, int32_t nulls_equal,
+                               int32_t maintain_order, int32_t validate, plgpu_column* out_left_idx,
+                               plgpu_column* out_right_idx, void* stream) {
+    int rc;
+    if ((rc = check_key(left_key)) || (rc = check_key(right_key))) return rc;
+    if (out_left_idx == nullptr || out_right_idx == nullptr) return fail(PLGPU_ERR_INVALID, "NULL output");
+    if (maintain_order < PLGPU_JOIN_ORDER_NONE || maintain_order > PLGPU_JOIN_ORDER_RIGHT_LEFT)
+        return fail(PLGPU_ERR_INVALID, "invalid maintain_order");
+    return join_inner_impl(left_key, right_key, nulls_equal != 0, maintain_order, validate, out_left_idx,
+                           out_right_idx, as_stream(stream));
+}
+
+PLGPU_API int plgpu_join_inner_multi(const plgpu_column* left_keys, const plgpu_column* right_keys, int32_t nkeys,
+                                     int32_t nulls_equal, int32_t maintain_order, int32_t validate,
+                                     plgpu_column* out_left_idx, plgpu_column* out_right_idx, void* stream) {
+    hipStream_t s = as_stream(stream);
+    if (left_keys == nullptr || right_keys == nullptr || out_left_idx == nullptr || out_right_idx == nullptr)
+        return fail(PLGPU_ERR_INVALID, "NULL argument");
+    if (nkeys < 1 || nkeys > kMaxKeys) return fail(PLGPU_ERR_INVALID, "number of join keys must be 1..8");
+    if (maintain_order < PLGPU_JOIN_ORDER_NONE || maintain_order > PLGPU_JOIN_ORDER_RIGHT_LEFT)
+        return fail(PLGPU_ERR_INVALID, "invalid maintain_order");
+    std::memset(out_left_idx, 0, sizeof *out_left_idx);
+    std::memset(out_right_idx, 0, sizeof *out_right_idx);
+    MkKeys ka, kb;
+    std::memset(&ka, 0, sizeof ka);
+    std::memset(&kb, 0, sizeof kb);
+    ka.n = kb.n = nkeys;
+    const int64_t nl = left_keys[0].length, nr = right_keys[0].length;
+    for (int i = 0; i < nkeys; ++i) {
+        const int32_t dt = left_keys[i].dtype;
+        if (dt != PLGPU_I64 && dt != PLGPU_I32 && dt != PLGPU_U32 && dt != PLGPU_F64 && dt != PLGPU_BOOL)
+            return fail(PLGPU_ERR_SCHEMA, "join keys must be Int64, Int32, UInt32, Float64 or Boolean");
+        if (right_keys[i].dtype != dt) return fail(PLGPU_ERR_SCHEMA, "datatypes of join keys don't match");
+        if (left_keys[i].length != nl || right_keys[i].length != nr)
+            return fail(PLGPU_ERR_SHAPE, "join key columns of one side must have equal lengths");
+        ka.c[i] = as_dev(&left_keys[i]);
+        kb.c[i] = as_dev(&right_keys[i]);
+    }
+    if (nl >= 0xFFFFFFFFll || nr >= 0xFFFFFFFFll) return fail(PLGPU_ERR_CAPACITY, "join side exceeds the u32 index space");
+    const bool neq = nulls_equal != 0;
+    uint64_t *hl = nullptr, *hr = nullptr, *vl = nullptr, *vr = nullptr;
+    uint32_t* bad = nullptr;
+    int rc = dev_alloc((void**)&hl, std::max<int64_t>(nl, 1) * 8, s);
+    if (!rc) rc = dev_alloc((void**)&hr, std::max<int64_t>(nr, 1) * 8, s);
+    if (!rc) rc = dev_alloc((void**)&vl, ((nl + 63) / 64 + 1) * 8, s);
+    if (!rc) rc = dev_alloc((void**)&vr, ((nr + 63) / 64 + 1) * 8, s);
+    if (!rc) rc = dev_alloc((void**)&bad, 4, s);
+    plgpu_column cl, cr;
+    std::memset(&cl, 0, sizeof cl);
+    std::memset(&cr, 0, sizeof cr);
+    cl.dtype = cr.dtype = PLGPU_I64;
+    cl.length = nl;
+    cr.length = nr;
+    cl.values = hl;
+    cr.values = hr;
+    // null tuples are dropped through the key validity (nulls_equal: every
+    // tuple is a value, nulls included, and no validity is needed)
+    cl.validity = neq ? nullptr : (const uint8_t*)vl;
+    cr.validity = neq ? nullptr : (const uint8_t*)vr;
+    cl.null_count = cr.null_count = neq ? 0 : -1;
+    const int cus = num_cus_jn();
+    bool done = false;
+    int validation_fails = 0;
+    for (int attempt = 0; attempt < 4 && !rc && !done; ++attempt) {
+        const uint64_t seed = 0x243F6A8885A308D3ull * (uint64_t)(2 * attempt + 1);
+        // PLGPU_MK_COLLIDE (tests only): a 3-bit first hash forces collisions
+        const uint64_t mask = attempt == 0 && getenv("PLGPU_MK_COLLIDE") ? 7ull : ~0ull;
+        if (nl > 0)
+            jn_tuple_hash_kernel<<<(unsigned)std::min<int64_t>((nl + 255) / 256, cus * 16), 256, 0, s>>>(ka, nl, seed,
+                                                                                                       mask, neq, hl, vl);
+        if (nr > 0)
+            jn_tuple_hash_kernel<<<(unsigned)std::min<int64_t>((nr + 255) / 256, cus * 16), 256, 0, s>>>(kb, nr, seed,
+                                                                                                       mask, neq, hr, vr);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) {
+            rc = hip_fail(e, "join tuple hash");
+            break;
+        }
+        rc = join_inner_impl(&cl, &cr, neq, maintain_order, validate, out_left_idx, out_right_idx, s);
+        if (rc == PLGPU_ERR_SCHEMA && ++validation_fails < 2) {
+            // a duplicate hash may be a collision of distinct tuples: a second
+            // seed tells a real duplicate (fails again) from a collision
+            rc = PLGPU_OK;
+            continue;
+        }
+        if (rc) break;
+        const int64_t np = out_left_idx->length;
+        uint32_t hbad = 0;
+        if (np > 0) {
+            e = hipMemsetAsync(bad, 0, 4, s);
+            if (e == hipSuccess) {
+                jn_verify_kernel<<<(unsigned)std::min<int64_t>((np + 255) / 256, cus * 16), 256, 0, s>>>(
+                    ka, kb, (const uint32_t*)out_left_idx->values, (const uint32_t*)out_right_idx->values, np, bad);
+                e = hipGetLastError();
+            }
+            if (e == hipSuccess) e = hipMemcpyAsync(&hbad, bad, 4, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e != hipSuccess) rc = hip_fail(e, "join tuple verify");
+        }
+        if (!rc && !hbad) done = true;
+        else {
+            plgpu_column_release(out_left_idx);
+            plgpu_column_release(out_right_idx);
+        }
+    }
+    dev_free(hl, s);
+    dev_free(hr, s);
+    dev_free(vl, s);
+    dev_free(vr, s);
+    dev_free(bad, s);
+    if (!rc && !done) rc = fail(PLGPU_ERR_CAPACITY, "multi-key join: unresolved 64-bit hash collisions");
     (void)hipStreamSynchronize(s);
     return rc;
 }

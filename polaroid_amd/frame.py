@@ -513,9 +513,12 @@ class LazyFrame:
             left_on = right_on = on
         if left_on is None or right_on is None:
             raise ValueError("must specify `on` OR `left_on` and `right_on`")
-        for k in (left_on, right_on):
-            if not isinstance(k, str):
-                raise N.InvalidOperationError("the GPU executor joins on exactly one key column")
+        left_on, right_on = _join_keys(left_on), _join_keys(right_on)
+        nl = 1 if isinstance(left_on, str) else builtins.len(left_on)
+        nr = 1 if isinstance(right_on, str) else builtins.len(right_on)
+        if nl != nr:
+            raise N.InvalidOperationError("the number of columns given as join key (left: %d, right: %d) "
+                                          "should be equal" % (nl, nr))
         if how != "inner":
             raise N.InvalidOperationError(f"join how={how!r} is not supported on the GPU executor (inner only)")
         if validate not in N.JOIN_VALIDATE:
@@ -538,6 +541,17 @@ class LazyFrame:
 
     def explain(self) -> str:
         return _explain(self._node)
+
+
+def _join_keys(on: Any) -> str | tuple:
+    """Join key spec -> one name, or a tuple of 2..8 plain column names."""
+    keys = _parse_exprs([on])
+    if not keys or any(k.kind != "col" for k in keys):
+        raise N.InvalidOperationError("the GPU executor joins on plain key columns")
+    if builtins.len(keys) > N.MAX_KEYS:
+        raise N.InvalidOperationError("the GPU executor joins on at most 8 key columns")
+    names = [k.value for k in keys]
+    return names[0] if builtins.len(names) == 1 else tuple(names)
 
 
 class LazyGroupBy:
@@ -788,21 +802,27 @@ def _group_by(df: DataFrame, key: str | tuple, aggs: list[Expr], maintain_order:
     return _gb_frame(g, out_key, out_aggs)
 
 
-def _join(left: DataFrame, right: DataFrame, left_on: str, right_on: str, suffix: str, validate: str,
-          nulls_equal: bool, maintain_order: str | None) -> DataFrame:
-    for df, k in ((left, left_on), (right, right_on)):
-        if k not in df._cols:
-            raise N.ComputeError(f'unable to find column "{k}"; valid columns: {df.columns}')
-    lk, rk = left._cols[left_on], right._cols[right_on]
-    if lk.dtype not in (Int64, Int32, UInt32):
-        raise N.InvalidOperationError(f"join key dtype {lk.dtype} is not supported on the GPU executor (integers)")
-    if lk.dtype is not rk.dtype:
-        raise N.InvalidOperationError(
-            f"join keys must have the same dtype on the GPU executor (got {lk.dtype} and {rk.dtype})")
+def _join(left: DataFrame, right: DataFrame, left_on: str | tuple, right_on: str | tuple, suffix: str,
+          validate: str, nulls_equal: bool, maintain_order: str | None) -> DataFrame:
+    lkeys, rkeys = _gb_keys(left_on), _gb_keys(right_on)
+    for df, ks in ((left, lkeys), (right, rkeys)):
+        for k in ks:
+            if k not in df._cols:
+                raise N.ComputeError(f'unable to find column "{k}"; valid columns: {df.columns}')
+    lks, rks = [left._cols[k] for k in lkeys], [right._cols[k] for k in rkeys]
+    for lk, rk in zip(lks, rks):
+        if lk.dtype is not rk.dtype:
+            raise N.InvalidOperationError(
+                f"join keys must have the same dtype on the GPU executor (got {lk.dtype} and {rk.dtype})")
     li, ri = N.Column(), N.Column()
-    N.check(N.lib().plgpu_join_inner(C.byref(lk._col), C.byref(rk._col), int(nulls_equal),
-                                     N.JOIN_ORDER[maintain_order], N.JOIN_VALIDATE[validate], C.byref(li),
-                                     C.byref(ri), None))
+    order, val = N.JOIN_ORDER[maintain_order], N.JOIN_VALIDATE[validate]
+    if builtins.len(lks) == 1 and lks[0].dtype in (Int64, Int32, UInt32):
+        N.check(N.lib().plgpu_join_inner(C.byref(lks[0]._col), C.byref(rks[0]._col), int(nulls_equal), order, val,
+                                         C.byref(li), C.byref(ri), None))
+    else:
+        # several keys (or a Float64 / Boolean key): hashed tuples, pairs verified
+        N.check(N.lib().plgpu_join_inner_multi(_col_array(lks), _col_array(rks), builtins.len(lks),
+                                               int(nulls_equal), order, val, C.byref(li), C.byref(ri), None))
     lidx, ridx = Series._from_native("__left_idx", li), Series._from_native("__right_idx", ri)
 
     def take(df: DataFrame, names: list[str], idx: Series) -> list[Series]:
@@ -814,7 +834,7 @@ def _join(left: DataFrame, right: DataFrame, left_on: str, right_on: str, suffix
         return [Series._from_native(n, out[i]) for i, n in enumerate(names)]
 
     lnames = left.columns
-    rnames = [n for n in right.columns if n != right_on]
+    rnames = [n for n in right.columns if n not in rkeys]
     out = take(left, lnames, lidx)
     for s in take(right, rnames, ridx):
         if s.name in lnames:

@@ -147,16 +147,19 @@ class _Translator:
                 raise Unsupported(f"{how} join")
             if slc is not None:
                 raise Unsupported("join slice")
-            if len(node.left_on) != 1 or len(node.right_on) != 1:
-                raise Unsupported("multi-key join")
-            lk = self.nt.view_expression(node.left_on[0].node)
-            rk = self.nt.view_expression(node.right_on[0].node)
-            if _name(lk) != "Column" or _name(rk) != "Column":
-                raise Unsupported("join keys must be plain columns")
+            if not 1 <= len(node.left_on) <= 8 or len(node.left_on) != len(node.right_on):
+                raise Unsupported("join key count")
+            names = []
+            for side in (node.left_on, node.right_on):
+                ks = [self.nt.view_expression(e.node) for e in side]
+                if any(_name(x) != "Column" for x in ks):
+                    raise Unsupported("join keys must be plain columns")
+                ks = [str(x.name) for x in ks]
+                names.append(ks[0] if len(ks) == 1 else tuple(ks))
             left = self.child(node.input_left)
             right = self.child(node.input_right)
             order = str(order).lower()
-            return ("join", left, right, str(lk.name), str(rk.name), str(suffix), "m:m", bool(nulls_equal),
+            return ("join", left, right, names[0], names[1], str(suffix), "m:m", bool(nulls_equal),
                     order if order in ("none", "left", "right", "left_right", "right_left") else "none")
         if k == "Sort":
             if node.slice is not None:

@@ -322,6 +322,41 @@ def join_cases():
 
 
 # ---------------------------------------------------------------------------
+# 4b. Multi-key inner joins (string columns label-encoded into integers).
+def join_multi_cases():
+    cases = []
+    col = [None if a % 6 == 0 else a for a in range(138)]
+    for neq, h in ((True, 644), (False, 115)):
+        cases.append({
+            "name": f"test_join_4_columns_with_validity[nulls_equal={neq}]",
+            "source": "operations/test_join.py:975-995",
+            "left": {"a": col, "b": col, "c": col, "d": col},
+            "right": {"a": col, "b": col, "c": col, "d": col},
+            "on": ["a", "b", "c", "d"], "args": {"nulls_equal": neq},
+            "expected_height": h, "expected_width": 4,
+        })
+    cases.append({
+        "name": "test_join_concat_projection_pd_case_7071 (join part)",
+        "source": "operations/test_join.py:660-670",
+        "left": {"id": [1, 2], "value": [100, 200]},
+        "right": {"id": [1, 3], "value": [100, 300]},
+        "on": ["id", "value"], "args": {},
+        "expected": {"id": [1], "value": [100]},
+    })
+    cases.append({
+        "name": "test_join_filter_pushdown_inner_join",
+        "source": "operations/test_join.py:2179-2200",
+        "left": {"a": [1, 2, 3, 4, 5], "b": [1, 2, 3, 4, None], "c": [0, 1, 2, 3, 4]},
+        "right": {"a": [1, 2, 3, 4, 5], "b": [1, 2, 3, None, 5], "c": [0, 1, 2, 3, 4]},
+        "labels": {"c": ["a", "b", "c", "d", "e"], "c_right": ["A", "B", "C", "D", "E"]},
+        "on": ["a", "b"], "args": {"maintain_order": "left_right"},
+        "post_filter": ["b", "<=", 2],
+        "expected": {"a": [1, 2], "b": [1, 2], "c": [0, 1], "c_right": [0, 1]},
+    })
+    return {"cases": cases}
+
+
+# ---------------------------------------------------------------------------
 # 5. Sorting (operations/test_sort.py).  `values` of one column; expected
 #    arg-sort or sorted values for (descending, nulls_last).
 def sort_cases():
@@ -400,6 +435,7 @@ def main():
                       ("group_by_multi_cases.json", group_by_multi_cases()),
                       ("filter_cases.json", filter_cases()),
                       ("join_cases.json", join_cases()),
+                      ("join_multi_cases.json", join_multi_cases()),
                       ("sort_cases.json", sort_cases()),
                       ("rolling_cases.json", rolling_cases())):
         with open(os.path.join(HERE, name), "w") as f:

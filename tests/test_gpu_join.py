@@ -147,9 +147,16 @@ def test_join_errors(gpu):
         left.join(right, on="k", how="left")
     with pytest.raises(ValueError):
         left.join(right)
-    f = pl.DataFrame({"k": pl.Series("k", [1.0], pl.Float64)})
+    # Float64 keys join by TotalOrd equality (-0.0 == 0.0, NaN == NaN), through
+    # the tuple-hash path
+    f = pl.DataFrame({"k": pl.Series("k", [1.0, -0.0, float("nan")], pl.Float64),
+                      "i": pl.Series("i", [0, 1, 2], pl.Int64)})
+    g = pl.DataFrame({"k": pl.Series("k", [0.0, float("nan"), 2.0], pl.Float64),
+                      "j": pl.Series("j", [0, 1, 2], pl.Int64)})
+    out = f.join(g, on="k", maintain_order="left")
+    assert out["i"].to_list() == [1, 2] and out["j"].to_list() == [0, 1]
     with pytest.raises(pl.InvalidOperationError):
-        f.join(f, on="k")
+        f.join(left, on="k")  # Float64 vs Int64 keys
 
 
 @pytest.mark.slow

@@ -338,3 +338,58 @@ def test_group_by_multi_matches_tuple_dict():
     assert set(got) == set(exp)
     for t, xs in exp.items():
         assert got[t] == (math.fsum(xs), len(xs))
+
+
+def _keys_of(frame, names):
+    out = []
+    for nm in names:
+        vals = frame[nm]
+        valid = np.array([v is not None for v in vals], dtype=bool)
+        arr = np.array([0 if v is None else v for v in vals], dtype=np.int64)
+        out.append((arr, None if valid.all() else valid))
+    return out
+
+
+def _join_multi_rows(case, li, ri):
+    """Output rows (dicts) of a multi-key fixture join: left columns, then the
+    right non-key columns (suffix `_right` on a name clash)."""
+    rows = []
+    for a, b in zip(li, ri):
+        row = {k: v[a] for k, v in case["left"].items()}
+        for k, v in case["right"].items():
+            if k not in case["on"]:
+                row[k + "_right" if k in row else k] = v[b]
+        rows.append(row)
+    return rows
+
+
+def test_join_multi_golden():
+    """Multi-key join fixtures (tests/golden/join_multi_cases.json) through
+    the row-encoding restatement (oracle.join_inner_multi)."""
+    for case in load_golden("join_multi_cases.json")["cases"]:
+        neq = case["args"].get("nulls_equal", False)
+        li, ri = O.join_inner_multi(_keys_of(case["left"], case["on"]), _keys_of(case["right"], case["on"]), neq)
+        if "expected_height" in case:
+            assert len(li) == case["expected_height"], case["name"]
+            continue
+        rows = _join_multi_rows(case, li, ri)
+        if "post_filter" in case:
+            c, op, v = case["post_filter"]
+            assert op == "<="
+            rows = [r for r in rows if r[c] is not None and r[c] <= v]
+        exp = case["expected"]
+        assert [tuple(r[c] for c in exp) for r in rows] == list(zip(*exp.values())), case["name"]
+
+
+def test_join_multi_matches_nested_loop():
+    rng = np.random.default_rng(8)
+    nl, nr = 400, 300
+    la, ra = rng.integers(0, 5, nl), rng.integers(0, 5, nr)
+    lb, rb = rng.integers(0, 4, nl), rng.integers(0, 4, nr)
+    lbv, rbv = rng.random(nl) > 0.2, rng.random(nr) > 0.2
+    for neq in (False, True):
+        li, ri = O.join_inner_multi([(la, None), (lb, lbv)], [(ra, None), (rb, rbv)], neq)
+        exp = sorted((i, j) for i in range(nl) for j in range(nr)
+                     if la[i] == ra[j] and ((lbv[i] and rbv[j] and lb[i] == rb[j]) or
+                                            (neq and not lbv[i] and not rbv[j])))
+        assert sorted(zip(li.tolist(), ri.tolist())) == exp

@@ -239,3 +239,16 @@ def test_udf_multi_key_group_by_on_gpu(gpu):
         m = sel & (k == kk) & (w == ww)
         assert out.column("v")[i].as_py() == math.fsum(v[m & vvalid])
         assert out.column("len")[i].as_py() == int(m.sum())
+
+
+def test_translate_multi_key_join():
+    table = _table()[0]
+    nt = FakeNT(table)
+    left = nt.p("DataFrameScan", ["k", "v", "w"], df=FakePolarsDF(table), projection=None, selection=None)
+    right = nt.p("DataFrameScan", ["k", "v", "w"], df=FakePolarsDF(table), projection=None, selection=None)
+    nt.p("Join", ["k", "v", "w", "v_right"], input_left=left, input_right=right,
+         left_on=[PyExprIR(nt.col("k"), "k"), PyExprIR(nt.col("w"), "w")],
+         right_on=[PyExprIR(nt.col("k"), "k"), PyExprIR(nt.col("w"), "w")],
+         options=("inner", True, None, "_right", True, "none"))
+    plan = PE.translate(nt)
+    assert plan[0] == "join" and plan[3] == ("k", "w") and plan[4] == ("k", "w") and plan[7] is True
