@@ -340,6 +340,17 @@ int plgpu_gather(const plgpu_column* cols, int32_t ncols, const plgpu_column* id
 int plgpu_arg_sort(const plgpu_column* key, int32_t descending, int32_t nulls_last,
                    plgpu_column* out_idx, void* stream);
 
+/* Stable arg-sort by 1..8 columns (I64 / I32 / U32 / F64 / BOOL), each with
+ * its own `descending[j]` and `nulls_last[j]`.  Replaces
+ * polars-core/src/chunked_array/ops/sort/arg_sort_multiple.rs:24
+ * arg_sort_multiple_impl (lexicographic compare, column by column, nulls
+ * placed per column independently of `descending`; maintain_order = a stable
+ * result, which this always is).  LSD over the columns: each column is one
+ * stable radix sort of its codes through the running permutation, plus one
+ * pass placing its nulls. */
+int plgpu_arg_sort_multi(const plgpu_column* keys, int32_t nkeys, const int32_t* descending,
+                         const int32_t* nulls_last, plgpu_column* out_idx, void* stream);
+
 /* ---- rolling windows ---------------------------------------------------------
  * Fixed-size window sum / mean (window_size rows, min_periods non-null rows
  * for a valid output, optionally centred), like Series.rolling_sum /

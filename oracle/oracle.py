@@ -296,6 +296,30 @@ def arg_sort(col: HostCol, descending: bool = False, nulls_last: bool = False) -
 ROLLING_REFERENCE, ROLLING_EXACT = 0, 1
 
 
+def arg_sort_multi(cols: list[tuple[np.ndarray, np.ndarray | None]], descending: list[bool],
+                   nulls_last: list[bool]) -> np.ndarray:
+    """Stable multi-column arg-sort restating arg_sort_multiple_impl
+    (polars-core/src/chunked_array/ops/sort/arg_sort_multiple.rs:24):
+    lexicographic over the columns; per column TotalOrd on the values
+    (NaN greatest, -0.0 == 0.0), reversed when descending, and nulls first or
+    last by that column's nulls_last alone; ties keep row order
+    (maintain_order)."""
+    n = cols[0][0].shape[0]
+    lex = []
+    for (v, m), desc, nl in reversed(list(zip(cols, descending, nulls_last))):
+        valid = np.ones(n, bool) if m is None else m.astype(bool)
+        w = v.astype(np.float64) + 0.0 if v.dtype == np.float64 else v.astype(np.int64)
+        w = np.where(valid, w, w[valid][0] if valid.any() else 0)
+        _, rank = np.unique(w, return_inverse=True)   # NaNs equal and last
+        rank = rank.reshape(-1).astype(np.int64)
+        if desc:
+            rank = rank.max(initial=0) - rank
+        rank = np.where(valid, rank, 0)
+        flag = np.where(valid, 0, 1) if nl else np.where(valid, 1, 0)
+        lex += [rank, flag]
+    return np.lexsort(lex) if n else np.zeros(0, np.int64)
+
+
 def rolling(col: HostCol, kind: str, window_size: int, min_periods: int | None = None, center: bool = False,
             mode: int = ROLLING_REFERENCE):
     """rolling_sum / rolling_mean -> (values, valid).  mode 0 restates the

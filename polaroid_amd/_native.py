@@ -126,6 +126,7 @@ SIGNATURES = {
                                          _P]),
     "plgpu_join_inner": (C.c_int, [_COLP, _COLP, C.c_int32, C.c_int32, C.c_int32, _COLP, _COLP, _P]),
     "plgpu_gather": (C.c_int, [_COLP, C.c_int32, _COLP, _COLP, _P]),
+    "plgpu_arg_sort_multi": (C.c_int, [_COLP, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32), _COLP, _P]),
     "plgpu_arg_sort": (C.c_int, [_COLP, C.c_int32, C.c_int32, _COLP, _P]),
     "plgpu_rolling": (C.c_int, [_COLP, C.c_int32, C.c_int64, C.c_int64, C.c_int32, _COLP, _P]),
 }

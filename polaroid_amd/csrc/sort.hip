@@ -242,6 +242,28 @@ __global__ __launch_bounds__(kSrtThreads) void srt_downsweep_kernel(const uint64
     }
 }
 
+// Multi-column sort: the codes of column c at the rows of the current
+// permutation (null rows get code 0; their place comes from the null pass).
+__global__ void srt_perm_codes_kernel(DevCol c, int64_t n, bool descending, const uint32_t* __restrict__ perm,
+                                      uint64_t* __restrict__ keys) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = perm[i];
+        keys[i] = dev_valid(c, r) ? sort_code(c, r, descending) : 0ull;
+    }
+}
+
+// Null placement of column c as a one-byte code: 0 sorts first.
+__global__ void srt_null_codes_kernel(DevCol c, int64_t n, bool nulls_last, const uint32_t* __restrict__ perm,
+                                      uint64_t* __restrict__ keys) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        keys[i] = (dev_valid(c, perm[i]) == nulls_last) ? 0ull : 1ull;
+}
+
+__global__ void srt_iota_kernel(int64_t n, uint32_t* __restrict__ idx) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        idx[i] = (uint32_t)i;
+}
+
 __global__ void srt_place_nulls_kernel(const uint32_t* __restrict__ nulls, int64_t nn, uint32_t* __restrict__ out) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nn; i += (int64_t)gridDim.x * blockDim.x)
         out[i] = nulls[i];
@@ -250,6 +272,63 @@ __global__ void srt_place_nulls_kernel(const uint32_t* __restrict__ nulls, int64
 }  // namespace plgpu
 
 using namespace plgpu;
+
+// Scratch of the radix passes over n codes.
+struct SrtScratch {
+    uint32_t* cnt = nullptr;
+    uint64_t* off = nullptr;
+    uint64_t* part = nullptr;
+    unsigned long long* hist = nullptr;
+    int alloc(int64_t n, hipStream_t s) {
+        const int64_t ntiles = (n + kSrtTile - 1) / kSrtTile;
+        int rc = dev_alloc((void**)&hist, 16, s);
+        if (!rc && n > 0) rc = dev_alloc((void**)&cnt, ntiles * 256 * 4, s);
+        if (!rc && n > 0) rc = dev_alloc((void**)&off, (ntiles * 256 + 1) * 8, s);
+        if (!rc && n > 0) rc = dev_alloc((void**)&part, ((ntiles * 256 + kScanChunk - 1) / kScanChunk + 1) * 8, s);
+        return rc;
+    }
+    void release(hipStream_t s) {
+        dev_free(cnt, s);
+        dev_free(off, s);
+        dev_free(part, s);
+        dev_free(hist, s);
+        cnt = nullptr;
+        off = nullptr;
+        part = nullptr;
+        hist = nullptr;
+    }
+};
+
+// Stable LSD passes over the bytes of keys[cur] that vary (one OR/AND read
+// finds them), carrying idx[cur]; `cur` names the buffers holding the result.
+static int radix_passes(uint64_t* keys[2], uint32_t* idx[2], int64_t nv, int& cur, SrtScratch& sc, hipStream_t s) {
+    if (nv <= 0) return PLGPU_OK;
+    const int cus = 256;
+    unsigned long long h[2] = {0ull, ~0ull};
+    hipError_t e = hipMemcpyAsync(sc.hist, h, 16, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) {
+        srt_bits_kernel<<<(unsigned)std::min<int64_t>((nv + 255) / 256, cus * 8), 256, 0, s>>>(keys[cur], nv, sc.hist);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(h, sc.hist, 16, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return hip_fail(e, "sort key bits");
+    const int64_t ntiles = (nv + kSrtTile - 1) / kSrtTile;
+    for (int byte = 0; byte < 8; ++byte) {
+        if ((((h[0] ^ h[1]) >> (8 * byte)) & 0xFF) == 0) continue;  // constant byte: the pass is the identity
+        const int shift = 8 * byte;
+        srt_upsweep_kernel<<<(unsigned)ntiles, kSrtThreads, 0, s>>>(keys[cur], nv, shift, ntiles, sc.cnt);
+        e = scan_exclusive<uint32_t>(sc.cnt, ntiles * 256, sc.off, sc.part, s);
+        if (e == hipSuccess) {
+            srt_downsweep_kernel<<<(unsigned)ntiles, kSrtThreads, 0, s>>>(keys[cur], idx[cur], nv, shift, ntiles,
+                                                                         sc.off, keys[cur ^ 1], idx[cur ^ 1]);
+            e = hipGetLastError();
+        }
+        if (e != hipSuccess) return hip_fail(e, "sort pass");
+        cur ^= 1;
+    }
+    return PLGPU_OK;
+}
 
 PLGPU_API int plgpu_arg_sort(const plgpu_column* key, int32_t descending, int32_t nulls_last, plgpu_column* out_idx,
                              void* stream) {
@@ -271,16 +350,12 @@ PLGPU_API int plgpu_arg_sort(const plgpu_column* key, int32_t descending, int32_
     uint64_t* keys[2] = {nullptr, nullptr};
     uint32_t* idx[2] = {nullptr, nullptr};
     uint32_t* nulls = nullptr;
-    uint32_t* cnt = nullptr;
-    uint64_t* off = nullptr;
     uint64_t* part = nullptr;
-    unsigned long long* hist = nullptr;
     const int64_t nblk = (n + 1023) / 1024;
     for (int i = 0; i < 2 && !rc; ++i) {
         rc = dev_alloc((void**)&keys[i], n * 8, s);
         if (!rc) rc = dev_alloc((void**)&idx[i], n * 4, s);
     }
-    if (!rc) rc = dev_alloc((void**)&hist, 8 * 256 * 8, s);
     int64_t nv = n;  // valid rows
     const int cus = 256;
     if (!rc && c.validity) {
@@ -313,37 +388,11 @@ PLGPU_API int plgpu_arg_sort(const plgpu_column* key, int32_t descending, int32_
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) rc = hip_fail(e, "sort codes");
     }
-    unsigned long long h[2] = {0ull, ~0ull};
-    if (!rc && nv > 0) {
-        hipError_t e = hipMemcpyAsync(hist, h, 16, hipMemcpyHostToDevice, s);
-        if (e == hipSuccess) {
-            srt_bits_kernel<<<(unsigned)std::min<int64_t>((nv + 255) / 256, cus * 8), 256, 0, s>>>(keys[0], nv, hist);
-            e = hipGetLastError();
-        }
-        if (e == hipSuccess) e = hipMemcpyAsync(h, hist, 16, hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
-        if (e != hipSuccess) rc = hip_fail(e, "sort key bits");
-    }
     int cur = 0;
-    const int64_t ntiles = (nv + kSrtTile - 1) / kSrtTile;
-    if (!rc && nv > 0) {
-        rc = dev_alloc((void**)&cnt, ntiles * 256 * 4, s);
-        if (!rc) rc = dev_alloc((void**)&off, (ntiles * 256 + 1) * 8, s);
-        if (!rc) rc = dev_alloc((void**)&part, ((ntiles * 256 + kScanChunk - 1) / kScanChunk + 1) * 8, s);
-    }
-    for (int byte = 0; byte < 8 && !rc && nv > 0; ++byte) {
-        if ((((h[0] ^ h[1]) >> (8 * byte)) & 0xFF) == 0) continue;  // constant byte: the pass is the identity
-        const int shift = 8 * byte;
-        srt_upsweep_kernel<<<(unsigned)ntiles, kSrtThreads, 0, s>>>(keys[cur], nv, shift, ntiles, cnt);
-        hipError_t e = scan_exclusive<uint32_t>(cnt, ntiles * 256, off, part, s);
-        if (e == hipSuccess) {
-            srt_downsweep_kernel<<<(unsigned)ntiles, kSrtThreads, 0, s>>>(keys[cur], idx[cur], nv, shift, ntiles, off,
-                                                                         keys[cur ^ 1], idx[cur ^ 1]);
-            e = hipGetLastError();
-        }
-        if (e != hipSuccess) rc = hip_fail(e, "sort pass");
-        cur ^= 1;
-    }
+    SrtScratch sc;
+    if (!rc) rc = sc.alloc(nv, s);
+    if (!rc) rc = radix_passes(keys, idx, nv, cur, sc, s);
+    sc.release(s);
     if (!rc) {
         uint32_t* out = (uint32_t*)out_idx->values;
         const int64_t nn = n - nv;
@@ -361,10 +410,76 @@ PLGPU_API int plgpu_arg_sort(const plgpu_column* key, int32_t descending, int32_
         dev_free(idx[i], s);
     }
     dev_free(nulls, s);
-    dev_free(cnt, s);
-    dev_free(off, s);
-    dev_free(part, s);
-    dev_free(hist, s);
+    if (rc) plgpu_column_release(out_idx);
+    return rc;
+}
+
+// Multi-column arg_sort: LSD over the columns (last column first), each
+// column one stable radix sort of its codes gathered through the current
+// permutation, then -- if it has nulls -- one stable pass placing them.
+PLGPU_API int plgpu_arg_sort_multi(const plgpu_column* keys_in, int32_t nkeys, const int32_t* descending,
+                                   const int32_t* nulls_last, plgpu_column* out_idx, void* stream) {
+    hipStream_t s = as_stream(stream);
+    if (keys_in == nullptr || out_idx == nullptr || descending == nullptr || nulls_last == nullptr)
+        return fail(PLGPU_ERR_INVALID, "NULL argument");
+    std::memset(out_idx, 0, sizeof *out_idx);
+    if (nkeys < 1 || nkeys > 8) return fail(PLGPU_ERR_INVALID, "number of sort columns must be 1..8");
+    const int64_t n = keys_in[0].length;
+    for (int j = 0; j < nkeys; ++j) {
+        const int32_t dt = keys_in[j].dtype;
+        if (dt != PLGPU_I64 && dt != PLGPU_I32 && dt != PLGPU_U32 && dt != PLGPU_F64 && dt != PLGPU_BOOL)
+            return fail(PLGPU_ERR_SCHEMA, "sort keys must be Int64 / Int32 / UInt32 / Float64 / Boolean");
+        if (keys_in[j].length != n) return fail(PLGPU_ERR_SHAPE, "sort columns must have equal lengths");
+    }
+    if (n >= 0xFFFFFFFFll) return fail(PLGPU_ERR_CAPACITY, "sort input exceeds the u32 index space");
+    int rc = make_owned_column(out_idx, PLGPU_U32, n, false, s);
+    if (rc || n == 0) return rc;
+    uint64_t* keys[2] = {nullptr, nullptr};
+    uint32_t* idx[2] = {nullptr, nullptr};
+    for (int i = 0; i < 2 && !rc; ++i) {
+        rc = dev_alloc((void**)&keys[i], n * 8, s);
+        if (!rc) rc = dev_alloc((void**)&idx[i], n * 4, s);
+    }
+    SrtScratch sc;
+    if (!rc) rc = sc.alloc(n, s);
+    int cur = 0;
+    const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 256 * 16);
+    if (!rc) {
+        srt_iota_kernel<<<g, 256, 0, s>>>(n, idx[0]);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) rc = hip_fail(e, "sort iota");
+    }
+    for (int j = nkeys - 1; j >= 0 && !rc; --j) {
+        DevCol c;
+        std::memset(&c, 0, sizeof c);
+        c.dtype = keys_in[j].dtype;
+        c.offset = keys_in[j].offset;
+        c.values = keys_in[j].values;
+        c.validity = keys_in[j].validity;
+        srt_perm_codes_kernel<<<g, 256, 0, s>>>(c, n, descending[j] != 0, idx[cur], keys[cur]);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) {
+            rc = hip_fail(e, "sort codes");
+            break;
+        }
+        rc = radix_passes(keys, idx, n, cur, sc, s);
+        if (!rc && c.validity && keys_in[j].null_count != 0) {
+            srt_null_codes_kernel<<<g, 256, 0, s>>>(c, n, nulls_last[j] != 0, idx[cur], keys[cur]);
+            e = hipGetLastError();
+            if (e != hipSuccess) rc = hip_fail(e, "sort null codes");
+            if (!rc) rc = radix_passes(keys, idx, n, cur, sc, s);
+        }
+    }
+    if (!rc) {
+        hipError_t e = hipMemcpyAsync((void*)out_idx->values, idx[cur], n * 4, hipMemcpyDeviceToDevice, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) rc = hip_fail(e, "sort output");
+    }
+    sc.release(s);
+    for (int i = 0; i < 2; ++i) {
+        dev_free(keys[i], s);
+        dev_free(idx[i], s);
+    }
     if (rc) plgpu_column_release(out_idx);
     return rc;
 }

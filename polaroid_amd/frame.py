@@ -431,10 +431,11 @@ class DataFrame:
     def filter(self, *predicates: Expr, **constraints: Any) -> "DataFrame":
         return self.lazy().filter(*predicates, **constraints).collect()
 
-    def sort(self, by: str, *, descending: bool = False, nulls_last: bool = False,
+    def sort(self, by: Any, *more_by: Any, descending: bool | Sequence[bool] = False,
+             nulls_last: bool | Sequence[bool] = False, multithreaded: bool = True,
              maintain_order: bool = False) -> "DataFrame":
-        """DataFrame.sort on one column (always stable, so maintain_order holds)."""
-        return self.lazy().sort(by, descending=descending, nulls_last=nulls_last,
+        """DataFrame.sort by 1..8 columns (always stable, so maintain_order holds)."""
+        return self.lazy().sort(by, *more_by, descending=descending, nulls_last=nulls_last,
                                 maintain_order=maintain_order).collect()
 
     def join(self, other: "DataFrame", on: str | None = None, how: str = "inner", *,
@@ -496,11 +497,27 @@ class LazyFrame:
     def group_by(self, *by: Any, maintain_order: bool = False) -> "LazyGroupBy":
         return LazyGroupBy(self, by, maintain_order)
 
-    def sort(self, by: str, *, descending: bool = False, nulls_last: bool = False,
+    def sort(self, by: Any, *more_by: Any, descending: bool | Sequence[bool] = False,
+             nulls_last: bool | Sequence[bool] = False, multithreaded: bool = True,
              maintain_order: bool = False) -> "LazyFrame":
-        if not isinstance(by, str):
-            raise N.InvalidOperationError("the GPU executor sorts by exactly one column")
-        return LazyFrame(("sort", self._node, by, bool(descending), bool(nulls_last)))
+        """Sort by 1..8 plain columns (py-polars LazyFrame.sort); per-column
+        `descending` / `nulls_last` as bools or sequences of bools."""
+        keys = _parse_exprs([by, *more_by])
+        if not keys or any(k.kind != "col" for k in keys) or builtins.len(keys) > N.MAX_KEYS:
+            raise N.InvalidOperationError("the GPU executor sorts by 1..8 plain columns")
+        names = [k.value for k in keys]
+
+        def per_col(v, what):
+            vals = [bool(v)] * builtins.len(names) if isinstance(v, bool) else [bool(x) for x in v]
+            if builtins.len(vals) != builtins.len(names):
+                raise ValueError(f"the length of `{what}` ({builtins.len(vals)}) does not match the length of "
+                                 f"`by` ({builtins.len(names)})")
+            return vals
+
+        desc, nl = per_col(descending, "descending"), per_col(nulls_last, "nulls_last")
+        if builtins.len(names) == 1:
+            return LazyFrame(("sort", self._node, names[0], desc[0], nl[0]))
+        return LazyFrame(("sort", self._node, tuple(names), tuple(desc), tuple(nl)))
 
     def join(self, other: "LazyFrame", on: str | None = None, how: str = "inner", *,
              left_on: str | None = None, right_on: str | None = None, suffix: str = "_right",
@@ -843,10 +860,22 @@ def _join(left: DataFrame, right: DataFrame, left_on: str | tuple, right_on: str
     return DataFrame(out)
 
 
-def _sort(df: DataFrame, by: str, descending: bool, nulls_last: bool) -> DataFrame:
-    if by not in df._cols:
-        raise N.ComputeError(f'unable to find column "{by}"; valid columns: {df.columns}')
-    idx = df._cols[by].arg_sort(descending=descending, nulls_last=nulls_last)
+def _sort(df: DataFrame, by: str | tuple, descending: bool | tuple, nulls_last: bool | tuple) -> DataFrame:
+    names = _gb_keys(by)
+    for nm in names:
+        if nm not in df._cols:
+            raise N.ComputeError(f'unable to find column "{nm}"; valid columns: {df.columns}')
+    if builtins.len(names) == 1 and df._cols[names[0]].dtype is not Boolean:
+        idx = df._cols[names[0]].arg_sort(descending=bool(descending), nulls_last=bool(nulls_last))
+    else:
+        k = builtins.len(names)
+        desc = descending if isinstance(descending, tuple) else (descending,)
+        nl = nulls_last if isinstance(nulls_last, tuple) else (nulls_last,)
+        out_idx = N.Column()
+        N.check(N.lib().plgpu_arg_sort_multi(_col_array([df._cols[nm] for nm in names]), k,
+                                             (C.c_int32 * k)(*map(int, desc)), (C.c_int32 * k)(*map(int, nl)),
+                                             C.byref(out_idx), None))
+        idx = Series._from_native("__idx", out_idx)
     names = df.columns
     out = (N.Column * builtins.len(names))()
     N.check(N.lib().plgpu_gather(_col_array([df._cols[n] for n in names]), builtins.len(names),

@@ -164,14 +164,20 @@ class _Translator:
         if k == "Sort":
             if node.slice is not None:
                 raise Unsupported("sort slice")
-            if len(node.by_column) != 1:
-                raise Unsupported("multi-column sort")
-            by = self.nt.view_expression(node.by_column[0].node)
-            if _name(by) != "Column":
+            if not 1 <= len(node.by_column) <= 8:
+                raise Unsupported("sort by more than 8 columns")
+            bys = [self.nt.view_expression(e.node) for e in node.by_column]
+            if any(_name(b) != "Column" for b in bys):
                 raise Unsupported("sort by an expression")
             _maintain, nulls_last, descending = node.sort_options
+            k = len(bys)
+            # the visitor gives one flag per column, or a single broadcast flag
+            desc = [bool(descending[i if len(descending) == k else 0]) for i in range(k)]
+            nl = [bool(nulls_last[i if len(nulls_last) == k else 0]) for i in range(k)]
             child = self.child(node.input)
-            return ("sort", child, str(by.name), bool(descending[0]), bool(nulls_last[0]))
+            if k == 1:
+                return ("sort", child, str(bys[0].name), desc[0], nl[0])
+            return ("sort", child, tuple(str(b.name) for b in bys), tuple(desc), tuple(nl))
         if k in ("Filter", "Select", "HStack", "GroupBy", "SimpleProjection"):
             child = self.child(node.input)
             if k == "Filter":

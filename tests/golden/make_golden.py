@@ -389,6 +389,46 @@ def sort_cases():
     return {"cases": cases}
 
 
+# 5b. Multi-column sort (frames of operations/test_sort.py; `expected` holds
+#     the sorted columns; string/datetime columns label-encoded in order).
+def sort_multi_cases():
+    cases = []
+    x, y = [None, 1, None, 3], [3, 2, None, 1]
+    for nl, desc, ex, ey in (([False, True], False, [None, None, 1, 3], [3, None, 2, 1]),
+                             ([True, False], False, [1, 3, None, None], [2, 1, None, 3]),
+                             ([True, False], True, [3, 1, None, None], [1, 2, None, 3]),
+                             ([False, True], True, [None, None, 3, 1], [3, None, 1, 2]),
+                             ([False, True], [True, False], [None, None, 3, 1], [3, None, 1, 2])):
+        cases.append({"name": f"test_expr_sort_by_multi_nulls_last[{nl}-{desc}]",
+                      "source": "operations/test_sort.py:158-188",
+                      "frame": {"x": x, "y": y}, "by": ["x", "y"],
+                      "args": {"nulls_last": nl, "descending": desc},
+                      "expected": {"x": ex, "y": ey}})
+    cases.append({"name": "test_sort_by[b, c]", "source": "operations/test_sort.py:76-100",
+                  "frame": {"a": [1, 2, 3, 4, 5], "b": [1, 1, 1, 2, 2], "c": [2, 3, 1, 2, 1]},
+                  "by": ["b", "c"], "args": {"maintain_order": True},
+                  "expected": {"a": [3, 1, 2, 5, 4]}})
+    cases.append({"name": "test_sort_dates_multiples", "source": "operations/test_sort.py:48-72",
+                  "frame": {"date": [0, 0, 1, 1, 2], "values": [5, 4, 3, 2, 1]},
+                  "labels": {"date": ["2021-01-01 00:00:00", "2021-01-02 00:00:00", "2021-01-03 00:00:00"]},
+                  "by": ["date", "values"], "args": {}, "expected": {"values": [4, 5, 2, 3, 1]}})
+    cases.append({"name": "test_sort_descending (2 columns)", "source": "operations/test_sort.py:801-809",
+                  "frame": {"a": [1, 2, 3], "b": [4, 5, 6]}, "by": ["a", "b"], "args": {"descending": [True, True]},
+                  "expected": {"a": [3, 2, 1], "b": [6, 5, 4]}})
+    fx_, fy = [1, 3, None, 2, None], [1, 3, 0, 2, 0]
+    for descending in (True, False):
+        for nulls_last in (True, False):
+            sentinel = 100 if descending ^ nulls_last else -100
+            rx = sorted(fx_, key=lambda k: sentinel if k is None else k, reverse=descending)
+            ry = sorted(fy, key=lambda k: sentinel if k == 0 else k, reverse=descending)
+            cases.append({"name": f"test_sort_descending_nulls_last[x,y-{descending}-{nulls_last}]",
+                          "source": "operations/test_sort.py:979-1001",
+                          "frame": {"x": fx_, "y": fy}, "by": ["x", "y"],
+                          "args": {"descending": descending, "nulls_last": nulls_last},
+                          "expected": {"x": rx, "y": ry}})
+    return {"cases": cases}
+
+
 # ---------------------------------------------------------------------------
 # 6. Fixed-window rolling sum / mean (operations/rolling/test_rolling.py,
 #    lazyframe/test_lazyframe.py, polars-compute rolling/no_nulls/sum.rs
@@ -437,6 +477,7 @@ def main():
                       ("join_cases.json", join_cases()),
                       ("join_multi_cases.json", join_multi_cases()),
                       ("sort_cases.json", sort_cases()),
+                      ("sort_multi_cases.json", sort_multi_cases()),
                       ("rolling_cases.json", rolling_cases())):
         with open(os.path.join(HERE, name), "w") as f:
             json.dump(obj, f, indent=1, sort_keys=False)

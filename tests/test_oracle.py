@@ -393,3 +393,41 @@ def test_join_multi_matches_nested_loop():
                      if la[i] == ra[j] and ((lbv[i] and rbv[j] and lb[i] == rb[j]) or
                                             (neq and not lbv[i] and not rbv[j])))
         assert sorted(zip(li.tolist(), ri.tolist())) == exp
+
+
+def _frame_cols(frame, names):
+    return [(np.array([0 if v is None else v for v in frame[nm]], dtype=np.int64),
+             np.array([v is not None for v in frame[nm]], dtype=bool)) for nm in names]
+
+
+def test_sort_multi_golden():
+    """Multi-column sort fixtures (tests/golden/sort_multi_cases.json)."""
+    for case in load_golden("sort_multi_cases.json")["cases"]:
+        k = len(case["by"])
+        desc = case["args"].get("descending", False)
+        nl = case["args"].get("nulls_last", False)
+        desc = desc if isinstance(desc, list) else [desc] * k
+        nl = nl if isinstance(nl, list) else [nl] * k
+        perm = O.arg_sort_multi(_frame_cols(case["frame"], case["by"]), desc, nl)
+        for c, exp in case["expected"].items():
+            assert [case["frame"][c][i] for i in perm] == exp, (case["name"], c)
+
+
+def test_sort_multi_matches_python_sorted():
+    rng = np.random.default_rng(4)
+    n = 2000
+    a = rng.choice(np.array([0.0, -0.0, 1.0, np.nan, -np.inf]), n)
+    b = rng.integers(0, 5, n)
+    bv = rng.random(n) > 0.3
+    for da, db, nla, nlb in [(False, False, False, False), (True, False, True, False), (False, True, False, True),
+                             (True, True, True, True)]:
+        perm = O.arg_sort_multi([(a, None), (b, bv)], [da, db], [nla, nlb])
+
+        def key(i):
+            x = a[i]
+            ka = (2 if np.isnan(x) else 1, 0.0 if np.isnan(x) else x + 0.0)
+            ka = (-ka[0], -ka[1]) if da else ka
+            kb = (0, 0) if not bv[i] else (1, -int(b[i]) if db else int(b[i]))
+            kb = (kb[0] if not nlb else 1 - kb[0], kb[1])
+            return (ka, kb, i)
+        assert perm.tolist() == sorted(range(n), key=key)

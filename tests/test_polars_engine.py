@@ -252,3 +252,17 @@ def test_translate_multi_key_join():
          options=("inner", True, None, "_right", True, "none"))
     plan = PE.translate(nt)
     assert plan[0] == "join" and plan[3] == ("k", "w") and plan[4] == ("k", "w") and plan[7] is True
+
+
+def test_translate_multi_column_sort():
+    table = _table()[0]
+    nt = FakeNT(table)
+    scan = nt.p("DataFrameScan", ["k", "v", "w"], df=FakePolarsDF(table), projection=None, selection=None)
+    nt.p("Sort", ["k", "v", "w"], input=scan, by_column=[PyExprIR(nt.col("k"), "k"), PyExprIR(nt.col("w"), "w")],
+         sort_options=(True, [False, True], [True, False]), slice=None)
+    plan = PE.translate(nt)
+    assert plan[0] == "sort" and plan[2] == ("k", "w") and plan[3] == (True, False) and plan[4] == (False, True)
+    # a broadcast single flag applies to every column
+    nt.lp[nt.root].sort_options = (False, [True], [False])
+    plan = PE.translate(nt)
+    assert plan[3] == (False, False) and plan[4] == (True, True)
