@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -34,6 +35,7 @@
 #include <vector>
 
 #include "plgpu_internal.hpp"
+#include "scan.hpp"
 #include "tuplehash.hpp"
 
 namespace plgpu {
@@ -110,6 +112,13 @@ struct GbParams {
     uint64_t* gtab;         // nfields regions of (gcap + 2) words; field 0 = keys
     const int32_t* bottoms; // [kMaxAcc]
     uint64_t* status;       // [ST_WORDS]
+    // partitioned launches (gb_kernel<.., PART>): partition q = b / part_blocks
+    // owns rows [part_range[q], part_range[q + 1]) of the partition buffers;
+    // part_rows maps them back to input rows (first-row field)
+    const uint64_t* part_range;
+    const uint32_t* part_rows;
+    int32_t part_blocks;
+    int32_t _pad3;
 };
 
 // ------------------------------------------------------------ helpers
@@ -447,7 +456,7 @@ constexpr int kGlobalNull = -3;
 
 // Generic kernel: any dtype / validity / offset / predicate, rows
 // [row_begin, n) in tiles of four rows per thread.
-template <int PRED, bool USE_LDS>  // PRED: 0 none, 1 simple, 2 program
+template <int PRED, bool USE_LDS, bool PART = false>  // PRED: 0 none, 1 simple, 2 program
 __global__ __launch_bounds__(kGbThreads) void gb_kernel(GbParams p, DevProgram prog) {
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
     const int L = p.lcap + 2;
@@ -459,10 +468,22 @@ __global__ __launch_bounds__(kGbThreads) void gb_kernel(GbParams p, DevProgram p
     load_descs(p, dd0, bot0);
     if (USE_LDS) __syncthreads();
 
-    const int64_t n = p.n;
+    int64_t n = p.n;
     const int T = blockDim.x;
     const int64_t tile = (int64_t)T * 4;
-    for (int64_t base = p.row_begin + (int64_t)blockIdx.x * tile; base < n; base += (int64_t)gridDim.x * tile) {
+    int64_t first = p.row_begin + (int64_t)blockIdx.x * tile, stride = (int64_t)gridDim.x * tile;
+    int64_t lo = 0;
+    if (PART) {
+        // this block's share of its partition (PRED is 0: rows are selected);
+        // tiles start at an even row for the 16-byte pair loads, rows below
+        // the partition's first are masked
+        const int q = blockIdx.x / p.part_blocks, sub = blockIdx.x % p.part_blocks;
+        lo = (int64_t)p.part_range[q];
+        first = (lo & ~int64_t(1)) + (int64_t)sub * tile;
+        n = (int64_t)p.part_range[q + 1];
+        stride = (int64_t)p.part_blocks * tile;
+    }
+    for (int64_t base = first; base < n; base += stride) {
         const int64_t r0 = base + 2 * threadIdx.x;
         const int64_t r2 = r0 + 2 * T;
         uint64_t key[4], pv[4];
@@ -487,7 +508,7 @@ __global__ __launch_bounds__(kGbThreads) void gb_kernel(GbParams p, DevProgram p
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int64_t r = (j < 2 ? r0 : r2) + (j & 1);
-            bool sel = r < n;
+            bool sel = r < n && (!PART || r >= lo);
             if (sel && PRED == 1) {
                 uint64_t x = pv[j];
 #pragma unroll
@@ -515,6 +536,7 @@ __global__ __launch_bounds__(kGbThreads) void gb_kernel(GbParams p, DevProgram p
             int s = slot[0];
             if (s != kNotSelected) {
                 ++d.nsel;
+                const int64_t row = PART ? (int64_t)(p.part_rows ? p.part_rows[r] : 0) : r;
                 uint64_t rv[kMaxAcc], dd[kMaxAcc];
                 int bot[kMaxAcc];
 #pragma unroll
@@ -525,10 +547,10 @@ __global__ __launch_bounds__(kGbThreads) void gb_kernel(GbParams p, DevProgram p
                 }
                 if (USE_LDS && s == kGlobalKey) s = lds_find(lds, p.lbits, p.lcap, key[0]);
                 if (s >= 0) {
-                    apply_row<true, kMaxAcc>(p, lds, L, s, r, rv, vm[0], dd, bot, nacc, d);
+                    apply_row<true, kMaxAcc>(p, lds, L, s, row, rv, vm[0], dd, bot, nacc, d);
                 } else {
                     ++d.nglobal;
-                    global_row<kMaxAcc>(p, key[0], s != kGlobalNull, r, rv, vm[0], dd, bot, nacc, d);
+                    global_row<kMaxAcc>(p, key[0], s != kGlobalNull, row, rv, vm[0], dd, bot, nacc, d);
                 }
             }
             slot[0] = slot[1]; slot[1] = slot[2]; slot[2] = slot[3];
@@ -543,6 +565,148 @@ __global__ __launch_bounds__(kGbThreads) void gb_kernel(GbParams p, DevProgram p
         }
     }
     flush_and_report<USE_LDS>(p, lds, L, d);
+}
+
+// ------------------------------------------------------ partitioned path
+// Keys with more groups than one LDS table holds: the selected rows are
+// first scattered into 2^pbits hash partitions (key, aggregated values and,
+// for the first-row field, the input row id, all widened to 8 bytes), so
+// every partition's groups fit the LDS table of the workgroups that then
+// aggregate it (gb_kernel<0, true, true>).  The partition hash is
+// independent of the table hashes (hash_slot / g_find use the top bits of a
+// multiplicative hash).  Order inside a partition is irrelevant: every
+// aggregate is order-independent (exact sums, min / max, counts, min row).
+constexpr int kPartMaxBits = 10;
+constexpr int kPartThreads = 256;
+
+__device__ __forceinline__ uint32_t part_of(uint64_t key, int pbits) {
+    return pbits == 0 ? 0u : (uint32_t)(mk_fmix(key ^ 0x2545F4914F6CDD1Dull) >> (64 - pbits));
+}
+
+template <int PRED>
+__device__ __forceinline__ bool part_sel(const GbParams& p, const DevProgram& prog, int64_t r) {
+    if (PRED == 0) return true;
+    if (PRED == 1)
+        return dev_valid(p.pred_col, r) &&
+               simple_pred(prog.simple_isf, prog.simple_op, dev_load(p.pred_col, r), prog.simple_imm);
+    const RowVal rv = eval_row(prog.code, prog.n, p.cols, r);
+    return rv.valid && (rv.v & 1);
+}
+
+// Each partition workgroup of pass 1 / 2 owns one contiguous chunk of rows
+// (a multiple of the tile), so the scan of the partition-major count matrix
+// cnt[q * G + b] gives every (partition, chunk) run its place and pass 2
+// needs no global atomics.
+constexpr int kPartPer = 8;
+constexpr int64_t kPartTile = (int64_t)kPartThreads * kPartPer;  // 2048 rows
+
+__device__ __forceinline__ void part_chunk(int64_t n, int64_t& lo, int64_t& hi) {
+    const int64_t tiles = (n + kPartTile - 1) / kPartTile;
+    const int64_t per = (tiles + gridDim.x - 1) / gridDim.x;
+    lo = std::min<int64_t>(n, (int64_t)blockIdx.x * per * kPartTile);
+    hi = std::min<int64_t>(n, lo + per * kPartTile);
+}
+
+// Pass 1: selected rows per (partition, chunk).
+template <int PRED>
+__global__ __launch_bounds__(kPartThreads) void gb_part_count_kernel(GbParams p, DevProgram prog, int pbits,
+                                                                     uint32_t* __restrict__ cnt) {
+    __shared__ uint32_t h[1 << kPartMaxBits];
+    const int P = 1 << pbits;
+    for (int i = threadIdx.x; i < P; i += blockDim.x) h[i] = 0;
+    __syncthreads();
+    int64_t lo, hi;
+    part_chunk(p.n, lo, hi);
+    for (int64_t r = lo + threadIdx.x; r < hi; r += blockDim.x)
+        if (part_sel<PRED>(p, prog, r)) atomicAdd(&h[part_of(dev_load(p.key, r), pbits)], 1u);
+    __syncthreads();
+    for (int i = threadIdx.x; i < P; i += blockDim.x) cnt[(int64_t)i * gridDim.x + blockIdx.x] = h[i];
+}
+
+// Partition boundaries: range[q] = off[q * G] (q = 0..P).
+__global__ void gb_part_bounds_kernel(const uint64_t* __restrict__ off, int P, int G, uint64_t* __restrict__ range) {
+    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q <= P; q += gridDim.x * blockDim.x)
+        range[q] = off[(int64_t)q * G];
+}
+
+struct PartOut {
+    uint64_t* key;
+    uint64_t* acc[kMaxAcc];
+    uint32_t* rows;  // null unless the first-row field is in use
+};
+
+// Pass 2: per tile of 2048 rows, the selected rows are ranked by partition in
+// LDS (histogram -> block scan -> partition-ordered slots), then written out
+// slot by slot, so each partition's rows of the tile leave as one run per
+// column; the second read of the tile's values hits L2.
+template <int PRED>
+__global__ __launch_bounds__(kPartThreads) void gb_part_scatter_kernel(GbParams p, DevProgram prog, int pbits,
+                                                                       const uint64_t* __restrict__ off, PartOut o) {
+    __shared__ uint32_t h[1 << kPartMaxBits];
+    __shared__ uint32_t lstart[1 << kPartMaxBits];
+    __shared__ uint64_t gcur[1 << kPartMaxBits];
+    __shared__ uint16_t srow[kPartTile];
+    __shared__ uint16_t spart[kPartTile];
+    __shared__ uint64_t wsum[kPartThreads / 64];
+    __shared__ uint32_t tile_sel;
+    const int P = 1 << pbits;
+    constexpr int QPT = (1 << kPartMaxBits) / kPartThreads;  // partitions per thread in the scan
+    for (int i = threadIdx.x; i < P; i += blockDim.x) gcur[i] = off[(int64_t)i * gridDim.x + blockIdx.x];
+    int64_t lo, hi;
+    part_chunk(p.n, lo, hi);
+    for (int64_t base = lo; base < hi; base += kPartTile) {
+        for (int i = threadIdx.x; i < P; i += blockDim.x) h[i] = 0;
+        __syncthreads();
+        uint32_t pr[kPartPer];
+#pragma unroll
+        for (int k = 0; k < kPartPer; ++k) {
+            const int64_t r = base + k * kPartThreads + threadIdx.x;
+            pr[k] = ~0u;
+            if (r < hi && part_sel<PRED>(p, prog, r)) {
+                const uint32_t q = part_of(dev_load(p.key, r), pbits);
+                pr[k] = (q << 16) | atomicAdd(&h[q], 1u);
+            }
+        }
+        __syncthreads();
+        // exclusive scan of the tile histogram over the partitions
+        uint32_t c[QPT], sum = 0;
+#pragma unroll
+        for (int j = 0; j < QPT; ++j) {
+            const int q = threadIdx.x * QPT + j;
+            c[j] = q < P ? h[q] : 0u;
+            sum += c[j];
+        }
+        uint64_t total;
+        uint32_t run = (uint32_t)block_excl_scan(sum, wsum, total);
+#pragma unroll
+        for (int j = 0; j < QPT; ++j) {
+            const int q = threadIdx.x * QPT + j;
+            if (q < P) lstart[q] = run;
+            run += c[j];
+        }
+        if (threadIdx.x == 0) tile_sel = (uint32_t)total;
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kPartPer; ++k) {
+            if (pr[k] == ~0u) continue;
+            const uint32_t q = pr[k] >> 16;
+            const uint32_t slot = lstart[q] + (pr[k] & 0xFFFFu);
+            srow[slot] = (uint16_t)(k * kPartThreads + threadIdx.x);
+            spart[slot] = (uint16_t)q;
+        }
+        __syncthreads();
+        const uint32_t m = tile_sel;
+        for (uint32_t t = threadIdx.x; t < m; t += blockDim.x) {
+            const uint32_t q = spart[t];
+            const int64_t r = base + srow[t];
+            const uint64_t pos = gcur[q] + (t - lstart[q]);
+            o.key[pos] = dev_load(p.key, r);
+            for (int a = 0; a < p.nacc; ++a) o.acc[a][pos] = dev_load(p.acc[a].c, r);
+            if (o.rows) o.rows[pos] = (uint32_t)r;
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < P; i += blockDim.x) gcur[i] += h[i];
+    }
 }
 
 // ------------------------------------------------------------- fast path
@@ -1359,7 +1523,8 @@ static int log2_ceil(int64_t x) {
 }
 
 // Size the LDS table / grid from the distinct-key sample of the plan kernel.
-static void size_tables(Plan* pl, uint64_t distinct, uint64_t sampled, int* gbits_out) {
+static void size_tables(Plan* pl, uint64_t distinct, uint64_t sampled, int* gbits_out, int64_t hll_est = -1,
+                        int64_t* est_out = nullptr) {
     GbParams& p = pl->p;
     const int64_t n = p.n;
     const int nf = p.nfields;
@@ -1375,10 +1540,12 @@ static void size_tables(Plan* pl, uint64_t distinct, uint64_t sampled, int* gbit
     pl->lds_bytes = pl->use_lds ? (size_t)nf * (p.lcap + 2) * 8 : 0;
     // Global table: the sample saw most keys if distinct << sampled.
     int64_t est;
-    if (saturated || sampled == 0) est = n;
+    if ((saturated || sampled == 0) && hll_est >= 0) est = std::min<int64_t>(n, hll_est + hll_est / 4 + 1024);
+    else if (saturated || sampled == 0) est = n;
     else if ((int64_t)distinct * 4 < (int64_t)sampled) est = (int64_t)distinct * 2 + 64;
     else est = std::min<int64_t>(n, (int64_t)((double)distinct * (double)n / (double)sampled) + 64);
     *gbits_out = log2_ceil(std::max<int64_t>(1024, est * 2));
+    if (est_out) *est_out = est;
     // Grid: fill the chip (LDS permitting), rows per workgroup bounded for
     // the limb headroom.
     int per_cu = 4;
@@ -1518,10 +1685,22 @@ struct GbRun {
     int wide_exmax[kMaxAcc] = {0};
     int64_t* wide_digits[kMaxAcc] = {nullptr};
     double* wide_sum[kMaxAcc] = {nullptr};
+    int64_t est_groups = -1;                 // plan's group estimate (sampled / HLL)
+    // partitioned path (gb_partition): buffers, ranges, launch shape
+    bool part = false;
+    int pbits = 0;
+    int part_lbits = 0;
+    int part_blocks = 1;
+    uint64_t* pbuf = nullptr;
+    uint64_t* prange = nullptr;              // scan of the count matrix + partition bounds
+    const uint64_t* part_range = nullptr;    // P + 1 partition boundaries (inside prange)
+    int64_t part_rows_total = 0;
+    PartOut pout;
 
     GbRun() {
         std::memset(st, 0, sizeof st);
         std::memset(hb, 0, sizeof hb);
+        std::memset(&pout, 0, sizeof pout);
     }
     ~GbRun() {
         for (int a = 0; a < kMaxAcc; ++a) {
@@ -1530,6 +1709,8 @@ struct GbRun {
         }
         dev_free(gtab, s);
         dev_free(status, s);
+        dev_free(pbuf, s);
+        dev_free(prange, s);
     }
 };
 
@@ -1564,6 +1745,41 @@ static int gb_prepare(GbRun& R, const plgpu_column* key, const plgpu_column* col
     return PLGPU_OK;
 }
 
+// HyperLogLog distinct-key count over the whole key column (2^12 registers,
+// ~1.6 % standard error), run only when the plan's sample saturates: it
+// sizes the global table for high-cardinality keys instead of assuming every
+// row is a new group.
+constexpr int kHllBits = 12;
+
+__global__ __launch_bounds__(256) void gb_hll_kernel(DevCol key, int64_t n, uint32_t* __restrict__ regs) {
+    __shared__ uint32_t r[1 << kHllBits];
+    for (int i = threadIdx.x; i < (1 << kHllBits); i += blockDim.x) r[i] = 0;
+    __syncthreads();
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        if (!dev_valid(key, i)) continue;
+        const uint64_t h = mk_fmix(dev_load(key, i) ^ 0x5851F42D4C957F2Dull);
+        const uint32_t j = (uint32_t)(h >> (64 - kHllBits));
+        const uint32_t rho = (uint32_t)__clzll((h << kHllBits) | (1ull << (kHllBits - 1))) + 1;
+        if (rho > r[j]) atomicMax(&r[j], rho);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < (1 << kHllBits); i += blockDim.x)
+        if (r[i]) atomicMax(&regs[i], r[i]);
+}
+
+static double hll_estimate(const uint32_t* regs) {
+    const double m = (double)(1 << kHllBits);
+    double sum = 0;
+    int zeros = 0;
+    for (int i = 0; i < (1 << kHllBits); ++i) {
+        sum += std::ldexp(1.0, -(int)regs[i]);
+        zeros += regs[i] == 0;
+    }
+    double e = (0.7213 / (1.0 + 1.079 / m)) * m * m / sum;
+    if (e <= 2.5 * m && zeros > 0) e = m * std::log(m / zeros);  // linear counting
+    return e;
+}
+
 // Planning launch -> distinct-key estimate, fixed-point bottoms, table
 // sizes, kernel choice.  `fixed` (nullable) overrides the sampled bottoms.
 static int gb_plan(GbRun& R, const int32_t* fixed) {
@@ -1577,7 +1793,25 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
     PLGPU_HIP(hipStreamSynchronize(R.s));
     if (fixed)
         for (int a = 0; a < kMaxAcc; ++a) R.hb[a] = fixed[a];
-    size_tables(&pl, R.st[ST_DISTINCT], R.st[ST_SAMPLED], &R.gbits);
+    int64_t hll = -1;
+    if (R.st[ST_DISTINCT] >= (uint64_t)kPlanSetSlots / 2 && n > 4 * (int64_t)kPlanSamples &&
+        !getenv("PLGPU_NO_HLL")) {
+        uint32_t* regs = nullptr;
+        std::vector<uint32_t> h(1 << kHllBits);
+        int rc = dev_alloc((void**)&regs, h.size() * 4, R.s);
+        if (rc) return rc;
+        hipError_t e = hipMemsetAsync(regs, 0, h.size() * 4, R.s);
+        if (e == hipSuccess) {
+            gb_hll_kernel<<<num_cus() * 4, 256, 0, R.s>>>(p.key, n, regs);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) e = hipMemcpyAsync(h.data(), regs, h.size() * 4, hipMemcpyDeviceToHost, R.s);
+        if (e == hipSuccess) e = hipStreamSynchronize(R.s);
+        dev_free(regs, R.s);
+        if (e != hipSuccess) return hip_fail(e, "gb_hll_kernel");
+        hll = (int64_t)hll_estimate(h.data());
+    }
+    size_tables(&pl, R.st[ST_DISTINCT], R.st[ST_SAMPLED], &R.gbits, hll, &R.est_groups);
     // fast path eligibility: no nulls, 8-byte columns
     // at even offsets of 16-byte aligned buffers, simple or no predicate,
     // LDS table in use
@@ -1626,7 +1860,128 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
         if (two) pl.limbs = 2;
     }
     p.row_begin = p.n_full;
+    // partitioned path: too many groups for one LDS table, but few enough
+    // that 2^kPartMaxBits partitions of LDS tables hold them; key and
+    // aggregated columns null-free (they are copied as raw words)
+    R.part = false;
+    if (!pl.use_lds && n >= (int64_t(1) << 20) && R.est_groups > 0 && p.key.validity == nullptr &&
+        !(p.f_first >= 0 && n >= 0xFFFFFFFFll) && !getenv("PLGPU_NO_PART")) {
+        bool ok2 = true;
+        for (int a = 0; a < p.nacc; ++a) ok2 = ok2 && p.acc[a].c.validity == nullptr;
+        // LDS table of the partition workgroups: two per CU, or one when
+        // 2^kPartMaxBits partitions of the smaller table are not enough
+        const int64_t want = R.est_groups + (R.est_groups >> 3);
+        for (size_t budget : {(size_t)80 * 1024, (size_t)160 * 1024}) {
+            int lb = 13;
+            while (lb > 6 && (size_t)p.nfields * ((1u << lb) + 2) * 8 > budget) --lb;
+            const int64_t per = (int64_t(1) << lb) / 2;  // groups per partition at load 1/2
+            int pb = 0;
+            while (pb < kPartMaxBits && want > (per << pb)) ++pb;
+            if (ok2 && want <= (per << pb)) {
+                R.part = true;
+                R.pbits = pb;
+                R.part_lbits = lb;
+                break;
+            }
+        }
+    }
+    if (R.part) p.n_full = 0, p.row_begin = 0;
     return PLGPU_OK;
+}
+
+// Scatter the selected rows into the hash partitions (once per run; the
+// attempts of gb_main reuse them).
+static int gb_partition(GbRun& R) {
+    GbParams& p = R.pl.p;
+    hipStream_t s = R.s;
+    const int P = 1 << R.pbits;
+    const int G = num_cus() * 8;
+    const int64_t ncnt = (int64_t)P * G;
+    uint32_t* cnt = nullptr;
+    uint64_t* part = nullptr;
+    int rc = dev_alloc((void**)&cnt, ncnt * 4, s);
+    if (!rc) rc = dev_alloc((void**)&R.prange, (ncnt + 1 + P + 1) * 8, s);
+    if (!rc) rc = dev_alloc((void**)&part, ((ncnt + kScanChunk - 1) / kScanChunk + 1) * 8, s);
+    uint64_t* off = R.prange;
+    uint64_t* range = R.prange + ncnt + 1;
+    std::vector<uint64_t> hr(P + 1);
+    if (!rc) {
+        switch (R.pred) {
+        case 0: gb_part_count_kernel<0><<<G, kPartThreads, 0, s>>>(p, R.dp, R.pbits, cnt); break;
+        case 1: gb_part_count_kernel<1><<<G, kPartThreads, 0, s>>>(p, R.dp, R.pbits, cnt); break;
+        default: gb_part_count_kernel<2><<<G, kPartThreads, 0, s>>>(p, R.dp, R.pbits, cnt); break;
+        }
+        hipError_t e = hipGetLastError();
+        if (e == hipSuccess) e = scan_exclusive<uint32_t>(cnt, ncnt, off, part, s);
+        if (e == hipSuccess) {
+            gb_part_bounds_kernel<<<(P + 256) / 256, 256, 0, s>>>(off, P, G, range);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) e = hipMemcpyAsync(hr.data(), range, (P + 1) * 8, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) rc = hip_fail(e, "gb_part_count_kernel");
+    }
+    dev_free(cnt, s);
+    dev_free(part, s);
+    if (rc) return rc;
+    uint64_t maxpart = 0;
+    for (int q = 0; q < P; ++q) maxpart = std::max<uint64_t>(maxpart, hr[q + 1] - hr[q]);
+    const int64_t rows = (int64_t)std::max<uint64_t>(hr[P], 2) + 2;
+    R.part_rows_total = (int64_t)hr[P];
+    const bool want_rows = p.f_first >= 0;
+    const size_t words = (size_t)rows * (1 + p.nacc) + (want_rows ? ((size_t)rows + 1) / 2 : 0);
+    if ((rc = dev_alloc((void**)&R.pbuf, words * 8, s))) return rc;
+    R.pout.key = R.pbuf;
+    for (int a = 0; a < p.nacc; ++a) R.pout.acc[a] = R.pbuf + (size_t)rows * (1 + a);
+    R.pout.rows = want_rows ? (uint32_t*)(R.pbuf + (size_t)rows * (1 + p.nacc)) : nullptr;
+    switch (R.pred) {
+    case 0: gb_part_scatter_kernel<0><<<G, kPartThreads, 0, s>>>(p, R.dp, R.pbits, off, R.pout); break;
+    case 1: gb_part_scatter_kernel<1><<<G, kPartThreads, 0, s>>>(p, R.dp, R.pbits, off, R.pout); break;
+    default: gb_part_scatter_kernel<2><<<G, kPartThreads, 0, s>>>(p, R.dp, R.pbits, off, R.pout); break;
+    }
+    PLGPU_HIP(hipGetLastError());
+    R.part_range = range;
+    // workgroups per partition: fill the chip, bound rows per workgroup
+    int nb = (int)std::max<int64_t>(1, (2 * (int64_t)num_cus() + P - 1) / P);
+    while ((int64_t)maxpart > (int64_t)nb * (kMaxRowsPerWg / 2)) nb *= 2;
+    R.part_blocks = nb;
+    return PLGPU_OK;
+}
+
+// The main pass over the partition buffers.
+static hipError_t launch_partitioned(const GbRun& R) {
+    Plan pp = R.pl;
+    GbParams& q = pp.p;
+    const GbParams& p = R.pl.p;
+    std::memset(&q.key, 0, sizeof q.key);
+    q.key.values = R.pout.key;
+    q.key.dtype = PLGPU_I64;
+    for (int a = 0; a < p.nacc; ++a) {
+        DevCol c;
+        std::memset(&c, 0, sizeof c);
+        c.values = R.pout.acc[a];
+        c.dtype = p.acc[a].isf ? PLGPU_F64 : PLGPU_I64;
+        q.acc[a].c = c;
+    }
+    q.n = R.part_rows_total;
+    q.row_begin = 0;
+    q.n_full = 0;
+    q.part_range = R.part_range;
+    q.part_rows = R.pout.rows;
+    q.part_blocks = R.part_blocks;
+    q.lbits = R.part_lbits;
+    q.lcap = 1 << R.part_lbits;
+    const size_t lds = (size_t)p.nfields * (q.lcap + 2) * 8;
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)gb_kernel<0, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        attr_set = true;
+    }
+    DevProgram none;
+    std::memset(&none, 0, sizeof none);
+    gb_kernel<0, true, true><<<(1 << R.pbits) * R.part_blocks, kGbThreads, lds, R.s>>>(q, none);
+    return hipGetLastError();
 }
 
 static int gb_alloc_table(GbRun& R) {
@@ -1714,12 +2069,15 @@ static int gb_main(GbRun& R, bool auto_refit, bool* refit, int32_t* hint) {
     PLGPU_HIP(hipEventCreate(&ev0));
     PLGPU_HIP(hipEventCreate(&ev1));
     int rc = PLGPU_OK;
-    for (R.attempts = 0;; ++R.attempts) {
+    if (R.part && n > 0 && R.pbuf == nullptr) rc = gb_partition(R);
+    for (R.attempts = 0; rc == PLGPU_OK; ++R.attempts) {
         if ((rc = gb_alloc_table(R))) break;
         PLGPU_HIP(hipMemcpyAsync(R.bottoms, R.hb, sizeof R.hb, hipMemcpyHostToDevice, R.s));
         for (int a = 0; a < kMaxAcc; ++a) p.bottom[a] = R.hb[a];
         PLGPU_HIP(hipEventRecord(ev0, R.s));
-        if (n > 0) {
+        if (n > 0 && R.part) {
+            PLGPU_HIP(launch_partitioned(R));
+        } else if (n > 0) {
             if (p.n_full > 0) PLGPU_HIP(launch_fast_dispatch(pl, R.dp, R.pred, R.s));
             if (p.row_begin < n) {
                 Plan tail = pl;
@@ -1816,7 +2174,7 @@ static void gb_fill_info(const GbRun& R, plgpu_groupby_info* info) {
     info->grid = p.n_full > 0 ? R.pl.launched_grid : R.pl.grid;
     info->table_capacity = p.gcap;
     info->main_kernel_ms = R.ms;
-    info->path = p.n_full > 0 ? (R.pl.sum_only ? 2 : 1) : 0;
+    info->path = R.part ? 3 : (p.n_full > 0 ? (R.pl.sum_only ? 2 : 1) : 0);
     info->sum_limbs = p.n_full > 0 && R.pl.sum_only ? R.pl.limbs : 3;
     for (int a = 0; a < p.nacc; ++a)
         if (((R.st[ST_FXFLAGS] >> (2 * a)) & 2u) && !((R.wide >> a) & 1u)) info->sum_inexact |= 1 << a;
@@ -1986,17 +2344,43 @@ __device__ __forceinline__ int64_t g_lookup(const GbParams& p, uint64_t key) {
     return -1;
 }
 
+// Every group's representative tuple (its first row), slot-aligned with the
+// table: vw[i * (gcap + 2) + s] = canonical word of key i (0 for a null),
+// vm[s] = validity bits.  The verify pass then reads these L2-resident
+// arrays instead of the representative rows themselves.
+__global__ __launch_bounds__(256) void mk_rep_kernel(GbParams p, MkKeys k, uint64_t* __restrict__ vw,
+                                                     uint32_t* __restrict__ vm) {
+    const int64_t total = p.gcap + 2;
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < total; s += (int64_t)gridDim.x * blockDim.x) {
+        if (*gfield(p, p.f_len, s) == 0) continue;
+        const int64_t rep = (int64_t)*gfield(p, p.f_first, s);
+        uint32_t m = 0;
+        for (int i = 0; i < k.n; ++i) {
+            const bool v = dev_valid(k.c[i], rep);
+            m |= (v ? 1u : 0u) << i;
+            vw[(int64_t)i * total + s] = v ? mk_word(k.c[i], rep) : 0ull;
+        }
+        vm[s] = m;
+    }
+}
+
 // Every row whose hash names a group must hold that group's tuple.  (Rows the
 // predicate dropped are checked too: a differing tuple there is a genuine
 // 64-bit collision as well, and only costs a re-run.)
-__global__ void mk_verify_kernel(GbParams p, MkKeys k, const uint64_t* __restrict__ hashes, int64_t n,
-                                 uint32_t* __restrict__ collision) {
+__global__ __launch_bounds__(256) void mk_verify_kernel(GbParams p, MkKeys k, const uint64_t* __restrict__ hashes,
+                                                        int64_t n, const uint64_t* __restrict__ vw,
+                                                        const uint32_t* __restrict__ vm,
+                                                        uint32_t* __restrict__ collision) {
+    const int64_t total = p.gcap + 2;
     bool bad = false;
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
         const int64_t s = g_lookup(p, hashes[r]);
         if (s < 0 || *gfield(p, p.f_len, s) == 0) continue;
-        const int64_t rep = (int64_t)*gfield(p, p.f_first, s);
-        if (rep != r) bad |= !mk_equal(k, r, k, rep);
+        const uint32_t m = vm[s];
+        for (int i = 0; i < k.n; ++i) {
+            const bool v = dev_valid(k.c[i], r);
+            bad |= v != (bool)((m >> i) & 1u) || (v && mk_word(k.c[i], r) != vw[(int64_t)i * total + s]);
+        }
     }
     if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(collision, 1u);
 }
@@ -2188,6 +2572,64 @@ PLGPU_API int plgpu_gb_merge(const void* records, int64_t n_records, const plgpu
 }
 
 // ------------------------------------------------------ multi-key group-by
+// Packed path: group by the exact Int64 code, then decode the output codes
+// into the key columns.
+static int gb_multi_packed(const MkKeys& mk, const MkPack& pk, int64_t n, const plgpu_column* keys, int32_t nkeys,
+                           const plgpu_column* cols, int32_t ncols, const plgpu_instr* program, int32_t n_instr,
+                           const plgpu_agg* aggs, int32_t naggs, int32_t maintain_order, plgpu_column* out_keys,
+                           plgpu_column* out_aggs, plgpu_groupby_info* info, void* stream) {
+    hipStream_t s = as_stream(stream);
+    uint64_t* codes = nullptr;
+    int rc = dev_alloc((void**)&codes, (size_t)std::max<int64_t>(n, 1) * 8, s);
+    if (rc) return rc;
+    if (n > 0) {
+        const int g = (int)std::min<int64_t>((n + 255) / 256, (int64_t)num_cus() * 16);
+        mk_pack_kernel<<<g, 256, 0, s>>>(mk, pk, n, codes, nullptr);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) rc = hip_fail(e, "mk_pack_kernel");
+    }
+    plgpu_column ck;
+    std::memset(&ck, 0, sizeof ck);
+    ck.dtype = PLGPU_I64;
+    ck.length = n;
+    ck.values = codes;
+    plgpu_column hout;
+    std::memset(&hout, 0, sizeof hout);
+    {
+        GbRun R;
+        if (!rc) rc = gb_prepare(R, &ck, cols, ncols, program, n_instr, aggs, naggs, maintain_order != 0, false, stream);
+        if (!rc) rc = gb_plan(R, nullptr);
+        if (!rc) rc = gb_main(R, true, nullptr, nullptr);
+        if (!rc && info) gb_fill_info(R, info);
+        if (!rc) rc = gb_finalize(R, naggs, &hout, out_aggs);
+    }
+    dev_free(codes, s);
+    if (rc) return rc;
+    const int64_t groups = hout.length;
+    const int gg = (int)std::max<int64_t>(1, std::min<int64_t>((groups + 255) / 256, 4096));
+    for (int i = 0; i < nkeys && !rc; ++i) {
+        const bool nullable = pk.nullable[i] != 0;
+        rc = make_owned_column(&out_keys[i], keys[i].dtype, groups, nullable, s);
+        if (rc || groups == 0) continue;
+        if (keys[i].dtype == PLGPU_BOOL) (void)hipMemsetAsync((void*)out_keys[i].values, 0, ((groups + 63) / 64) * 8, s);
+        if (nullable) (void)hipMemsetAsync((void*)out_keys[i].validity, 0, ((groups + 63) / 64) * 8, s);
+        mk_unpack_kernel<<<gg, 256, 0, s>>>((const int64_t*)hout.values, nullptr, groups, pk, i, keys[i].dtype,
+                                            (void*)out_keys[i].values, (uint32_t*)out_keys[i].validity);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) rc = hip_fail(e, "mk_unpack_kernel");
+    }
+    if (!rc) {
+        hipError_t e = hipStreamSynchronize(s);
+        if (e != hipSuccess) rc = hip_fail(e, "multi-key decode");
+    }
+    plgpu_column_release(&hout);
+    if (rc) {
+        for (int i = 0; i < nkeys; ++i) plgpu_column_release(&out_keys[i]);
+        for (int i = 0; i < naggs; ++i) plgpu_column_release(&out_aggs[i]);
+    }
+    return rc;
+}
+
 PLGPU_API int plgpu_group_by_agg_multi(const plgpu_column* keys, int32_t nkeys, const plgpu_column* cols,
                                        int32_t ncols, const plgpu_instr* program, int32_t n_instr,
                                        const plgpu_agg* aggs, int32_t naggs, int32_t maintain_order,
@@ -2209,6 +2651,16 @@ PLGPU_API int plgpu_group_by_agg_multi(const plgpu_column* keys, int32_t nkeys, 
         mk.c[i] = to_dev(keys[i]);
     }
     hipStream_t s = as_stream(stream);
+    const int hg = (int)std::min<int64_t>((n + 255) / 256, (int64_t)num_cus() * 16);
+    {
+        // integer keys whose ranges fit 63 bits together: one exact packed
+        // Int64 key, grouped by the single-key paths (no hash, no verify)
+        MkPack pk;
+        int rc = mk_plan_pack(mk, n, nullptr, 0, std::max(hg, 1), &pk, s);
+        if (rc) return rc;
+        if (pk.ok) return gb_multi_packed(mk, pk, n, keys, nkeys, cols, ncols, program, n_instr, aggs, naggs,
+                                          maintain_order, out_keys, out_aggs, info, stream);
+    }
     uint64_t* hashes = nullptr;
     uint32_t* collision = nullptr;
     int rc = dev_alloc((void**)&hashes, (size_t)std::max<int64_t>(n, 1) * 8, s);
@@ -2218,7 +2670,6 @@ PLGPU_API int plgpu_group_by_agg_multi(const plgpu_column* keys, int32_t nkeys, 
     hk.dtype = PLGPU_I64;
     hk.length = n;
     hk.values = hashes;
-    const int hg = (int)std::min<int64_t>((n + 255) / 256, (int64_t)num_cus() * 16);
     bool done = false;
     for (int attempt = 0; attempt < 4 && !rc && !done; ++attempt) {
         const uint64_t seed = 0x243F6A8885A308D3ull * (uint64_t)(2 * attempt + 1);
@@ -2241,8 +2692,15 @@ PLGPU_API int plgpu_group_by_agg_multi(const plgpu_column* keys, int32_t nkeys, 
         plgpu_column_release(&hout);
         uint32_t coll = 0;
         if (n > 0 && groups > 0) {
+            const int64_t total = R.pl.p.gcap + 2;
+            uint64_t* vw = nullptr;
+            if ((rc = dev_alloc((void**)&vw, (size_t)total * (nkeys * 8 + 4), s))) break;
+            uint32_t* vmask = (uint32_t*)(vw + (size_t)total * nkeys);
             (void)hipMemsetAsync(collision, 0, 4, s);
-            mk_verify_kernel<<<std::max(hg, 1), 256, 0, s>>>(R.pl.p, mk, hashes, n, collision);
+            mk_rep_kernel<<<(unsigned)std::min<int64_t>((total + 255) / 256, 4096), 256, 0, s>>>(R.pl.p, mk, vw,
+                                                                                               vmask);
+            mk_verify_kernel<<<std::max(hg, 1), 256, 0, s>>>(R.pl.p, mk, hashes, n, vw, vmask, collision);
+            dev_free(vw, s);
             e = hipGetLastError();
             if (e == hipSuccess) e = hipMemcpyAsync(&coll, collision, 4, hipMemcpyDeviceToHost, s);
             if (e == hipSuccess) e = hipStreamSynchronize(s);

@@ -813,6 +813,50 @@ PLGPU_API int plgpu_join_inner_multi(const plgpu_column* left_keys, const plgpu_
     }
     if (nl >= 0xFFFFFFFFll || nr >= 0xFFFFFFFFll) return fail(PLGPU_ERR_CAPACITY, "join side exceeds the u32 index space");
     const bool neq = nulls_equal != 0;
+    const int cus = num_cus_jn();
+    {
+        // integer keys whose common ranges fit 63 bits: both sides packed into
+        // one exact Int64 key (a tuple with a null is a null key unless
+        // nulls_equal), joined once, no verification
+        MkPack pk;
+        int rc = mk_plan_pack(ka, nl, &kb, nr, cus * 16, &pk, s);
+        if (rc) return rc;
+        if (pk.ok) {
+            uint64_t *cl = nullptr, *cr = nullptr;
+            rc = dev_alloc((void**)&cl, (std::max<int64_t>(nl, 1) + (nl + 63) / 64 + 1) * 8, s);
+            if (!rc) rc = dev_alloc((void**)&cr, (std::max<int64_t>(nr, 1) + (nr + 63) / 64 + 1) * 8, s);
+            uint64_t* vl = cl ? cl + std::max<int64_t>(nl, 1) : nullptr;
+            uint64_t* vr = cr ? cr + std::max<int64_t>(nr, 1) : nullptr;
+            if (!rc && nl > 0)
+                mk_pack_kernel<<<(unsigned)std::min<int64_t>((nl + 255) / 256, cus * 16), 256, 0, s>>>(
+                    ka, pk, nl, cl, neq ? nullptr : vl);
+            if (!rc && nr > 0)
+                mk_pack_kernel<<<(unsigned)std::min<int64_t>((nr + 255) / 256, cus * 16), 256, 0, s>>>(
+                    kb, pk, nr, cr, neq ? nullptr : vr);
+            if (!rc) {
+                hipError_t e = hipGetLastError();
+                if (e != hipSuccess) rc = hip_fail(e, "mk_pack_kernel");
+            }
+            if (!rc) {
+                plgpu_column a, b;
+                std::memset(&a, 0, sizeof a);
+                std::memset(&b, 0, sizeof b);
+                a.dtype = b.dtype = PLGPU_I64;
+                a.length = nl;
+                b.length = nr;
+                a.values = cl;
+                b.values = cr;
+                a.validity = neq ? nullptr : (const uint8_t*)vl;
+                b.validity = neq ? nullptr : (const uint8_t*)vr;
+                a.null_count = b.null_count = neq ? 0 : -1;
+                rc = join_inner_impl(&a, &b, neq, maintain_order, validate, out_left_idx, out_right_idx, s);
+            }
+            dev_free(cl, s);
+            dev_free(cr, s);
+            (void)hipStreamSynchronize(s);
+            return rc;
+        }
+    }
     uint64_t *hl = nullptr, *hr = nullptr, *vl = nullptr, *vr = nullptr;
     uint32_t* bad = nullptr;
     int rc = dev_alloc((void**)&hl, std::max<int64_t>(nl, 1) * 8, s);
@@ -833,7 +877,6 @@ PLGPU_API int plgpu_join_inner_multi(const plgpu_column* left_keys, const plgpu_
     cl.validity = neq ? nullptr : (const uint8_t*)vl;
     cr.validity = neq ? nullptr : (const uint8_t*)vr;
     cl.null_count = cr.null_count = neq ? 0 : -1;
-    const int cus = num_cus_jn();
     bool done = false;
     int validation_fails = 0;
     for (int attempt = 0; attempt < 4 && !rc && !done; ++attempt) {

@@ -7,6 +7,9 @@
 // verifies tuples afterwards.
 #pragma once
 
+#include <cstdlib>
+#include <cstring>
+
 #include "plgpu_internal.hpp"
 
 namespace plgpu {
@@ -64,4 +67,169 @@ __device__ __forceinline__ bool mk_equal(const MkKeys& a, int64_t ra, const MkKe
     return eq;
 }
 
+}  // namespace plgpu
+
+// ---------------------------------------------------------------------------
+// Exact packing: when every key is an integer (or Boolean) column whose value
+// range, plus a null code, fits next to the others in 63 bits, a tuple is
+// encoded injectively as one Int64 -- the multi-key operators then run as
+// single-key ones with no hashing, no verification and no collision path.
+// Field i = null ? 0 : v - min_i + (nullable_i ? 1 : 0), at bit shift_i.
+namespace plgpu {
+namespace {  // internal linkage: included by several translation units
+
+struct MkPack {
+    int32_t n;
+    int32_t ok;
+    int64_t minv[kMaxKeys];
+    int32_t shift[kMaxKeys];
+    int32_t bits[kMaxKeys];
+    int32_t nullable[kMaxKeys];
+};
+
+// Per key column: [ord(min), ord(max), any null] at stats[3 * i ...]; ord(x)
+// = x ^ 2^63 so unsigned atomics order signed values.
+__global__ __launch_bounds__(256) void mk_range_kernel(MkKeys k, int64_t n, unsigned long long* __restrict__ stats) {
+    for (int i = 0; i < k.n; ++i) {
+        const DevCol& c = k.c[i];
+        uint64_t mn = ~0ull, mx = 0, nul = 0;
+        for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+            if (!dev_valid(c, r)) {
+                nul = 1;
+                continue;
+            }
+            const uint64_t o = dev_load(c, r) ^ 0x8000000000000000ull;
+            mn = o < mn ? o : mn;
+            mx = o > mx ? o : mx;
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const uint64_t a = __shfl_xor(mn, off, 64), b = __shfl_xor(mx, off, 64);
+            mn = a < mn ? a : mn;
+            mx = b > mx ? b : mx;
+            nul |= __shfl_xor(nul, off, 64);
+        }
+        if ((threadIdx.x & 63) == 0) {
+            if (mn != ~0ull) atomicMin(&stats[3 * i], (unsigned long long)mn);
+            if (mx != 0) atomicMax(&stats[3 * i + 1], (unsigned long long)mx);
+            if (nul) atomicOr(&stats[3 * i + 2], 1ull);
+        }
+    }
+}
+
+// Packed Int64 code per row; `valid_words` (optional): one bit per row, 0
+// when the tuple holds a null and nulls are not values (join without
+// nulls_equal).
+__global__ __launch_bounds__(256) void mk_pack_kernel(MkKeys k, MkPack pk, int64_t n, uint64_t* __restrict__ out,
+                                                      uint64_t* __restrict__ valid_words) {
+    for (int64_t r0 = (int64_t)blockIdx.x * blockDim.x; r0 < n; r0 += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = r0 + threadIdx.x;
+        const bool in = r < n;
+        bool anynull = false;
+        uint64_t code = 0;
+        if (in) {
+            for (int i = 0; i < k.n; ++i) {
+                const DevCol& c = k.c[i];
+                uint64_t f;
+                if (dev_valid(c, r)) f = (uint64_t)((int64_t)dev_load(c, r) - pk.minv[i]) + (pk.nullable[i] ? 1u : 0u);
+                else {
+                    f = 0;
+                    anynull = true;
+                }
+                code |= f << pk.shift[i];
+            }
+            out[r] = code;
+        }
+        if (valid_words) {
+            const uint64_t b = __ballot(in && !anynull);
+            if ((threadIdx.x & 63) == 0 && r - (threadIdx.x & 63) < n) valid_words[(r - (threadIdx.x & 63)) >> 6] = b;
+        }
+    }
+}
+
+// Packed codes -> key column i (dtype of the input key; validity zeroed
+// beforehand; Boolean values bit-packed, zeroed beforehand).
+__global__ __launch_bounds__(256) void mk_unpack_kernel(const int64_t* __restrict__ codes, const uint32_t* code_valid,
+                                                        int64_t g_n, MkPack pk, int i, int32_t dtype, void* out,
+                                                        uint32_t* out_valid) {
+    for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < g_n; g += (int64_t)gridDim.x * blockDim.x) {
+        const bool cv = code_valid == nullptr || ((code_valid[g >> 5] >> (g & 31)) & 1u);
+        const uint64_t mask = pk.bits[i] >= 64 ? ~0ull : ((1ull << pk.bits[i]) - 1);
+        const uint64_t f = ((uint64_t)codes[g] >> pk.shift[i]) & mask;
+        const bool valid = cv && !(pk.nullable[i] && f == 0);
+        const int64_t v = valid ? pk.minv[i] + (int64_t)(f - (pk.nullable[i] ? 1u : 0u)) : 0;
+        switch (dtype) {
+        case PLGPU_I64: ((int64_t*)out)[g] = v; break;
+        case PLGPU_I32: ((int32_t*)out)[g] = (int32_t)v; break;
+        case PLGPU_U32: ((uint32_t*)out)[g] = (uint32_t)v; break;
+        default:
+            if (v & 1) atomicOr(&((uint32_t*)out)[g >> 5], 1u << (g & 31));
+            break;
+        }
+        if (out_valid && valid) atomicOr(&out_valid[g >> 5], 1u << (g & 31));
+    }
+}
+
+// Range pass over `ka` (and `kb`, the other join side, when non-null) and the
+// packing plan; pk->ok = 0 when a key is Float64 or the fields need > 63 bits.
+inline int mk_plan_pack(const MkKeys& ka, int64_t na, const MkKeys* kb, int64_t nb, int grid, MkPack* pk,
+                        hipStream_t s) {
+    std::memset(pk, 0, sizeof *pk);
+    pk->n = ka.n;
+    for (int i = 0; i < ka.n; ++i)
+        if (ka.c[i].dtype == PLGPU_F64) return PLGPU_OK;
+    if (getenv("PLGPU_NO_PACK")) return PLGPU_OK;
+    unsigned long long* st = nullptr;
+    const size_t bytes = 2 * 3 * kMaxKeys * 8;
+    int rc = dev_alloc((void**)&st, bytes, s);
+    if (rc) return rc;
+    unsigned long long h[2 * 3 * kMaxKeys];
+    for (int j = 0; j < 2 * kMaxKeys; ++j) {
+        h[3 * j] = ~0ull;
+        h[3 * j + 1] = 0;
+        h[3 * j + 2] = 0;
+    }
+    hipError_t e = hipMemcpyAsync(st, h, bytes, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && na > 0) {
+        mk_range_kernel<<<grid, 256, 0, s>>>(ka, na, st);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess && kb && nb > 0) {
+        mk_range_kernel<<<grid, 256, 0, s>>>(*kb, nb, st + 3 * kMaxKeys);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(h, st, bytes, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    dev_free(st, s);
+    if (e != hipSuccess) return hip_fail(e, "key range pass");
+    int shift = 0;
+    for (int i = 0; i < ka.n; ++i) {
+        uint64_t mn = h[3 * i], mx = h[3 * i + 1];
+        bool nul = h[3 * i + 2] != 0;
+        if (kb) {
+            const uint64_t mn2 = h[3 * (kMaxKeys + i)], mx2 = h[3 * (kMaxKeys + i) + 1];
+            mn = mn2 < mn ? mn2 : mn;
+            mx = mx2 > mx ? mx2 : mx;
+            nul = nul || h[3 * (kMaxKeys + i) + 2] != 0;
+        }
+        if (mn > mx) {  // no valid value anywhere: one code (null or 0)
+            mn = mx = 0x8000000000000000ull;
+        }
+        const uint64_t span = mx - mn;  // of ord values == of the signed values
+        const uint64_t codes = span + (nul ? 2u : 1u);
+        if (span >= (1ull << 62)) return PLGPU_OK;
+        int b = 0;
+        while (b < 63 && (1ull << b) < codes) ++b;
+        pk->minv[i] = (int64_t)(mn ^ 0x8000000000000000ull);
+        pk->shift[i] = shift;
+        pk->bits[i] = b;
+        pk->nullable[i] = nul ? 1 : 0;
+        shift += b;
+        if (shift > 63) return PLGPU_OK;
+    }
+    pk->ok = 1;
+    return PLGPU_OK;
+}
+
+}  // namespace
 }  // namespace plgpu

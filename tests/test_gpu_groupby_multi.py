@@ -91,7 +91,12 @@ AGGS = [("sum", "a"), ("mean", "d"), ("min", "b"), ("max", "a"), ("count", "d"),
 
 @pytest.mark.parametrize("card", [1, 5, 300, 20000])
 @pytest.mark.parametrize("maintain_order", [False, True])
-def test_two_int_keys_vs_oracle(gpu, card, maintain_order):
+@pytest.mark.parametrize("pack", [True, False])
+def test_two_int_keys_vs_oracle(gpu, card, maintain_order, pack, monkeypatch):
+    """Integer keys go through the exact packed Int64 key; PLGPU_NO_PACK
+    forces the hash + verify path on the same data."""
+    if not pack:
+        monkeypatch.setenv("PLGPU_NO_PACK", "1")
     rng = np.random.default_rng(card + 7)
     n = 150_000
     cols = _rand_frame(rng, n)
@@ -131,8 +136,11 @@ def test_key_count_and_single_non_int_key(gpu, nkeys):
     _check(keys, cols, [("sum", "d"), ("len", "a")], nkeys != 3)
 
 
-def test_many_groups_and_special_hashes(gpu):
+@pytest.mark.parametrize("pack", [True, False])
+def test_many_groups_and_special_hashes(gpu, pack, monkeypatch):
     """~1e6 distinct tuples over 2e6 rows (global-table path)."""
+    if not pack:
+        monkeypatch.setenv("PLGPU_NO_PACK", "1")
     rng = np.random.default_rng(99)
     n = 2_000_000
     cols = {"a": (rng.standard_normal(n), None), "b": (rng.integers(-9, 9, n).astype(np.int64), None)}
@@ -148,6 +156,7 @@ def test_collision_triggers_reseed(gpu, monkeypatch):
     """A forced 3-bit first hash merges distinct tuples; the verify pass
     must catch it and the re-seeded run must be exact."""
     monkeypatch.setenv("PLGPU_MK_COLLIDE", "1")
+    monkeypatch.setenv("PLGPU_NO_PACK", "1")  # integer keys would be packed exactly
     rng = np.random.default_rng(4)
     n = 30_000
     cols = _rand_frame(rng, n)
@@ -199,3 +208,21 @@ def test_group_by_multi_golden(gpu):
                 else:
                     assert g == e, (case["name"], nm, got, exp)
         assert len(got) == len(exp)
+
+
+def test_packed_key_ranges_extremes(gpu):
+    """Packing at the edges: full-range Int32 / UInt32 keys, negative Int64
+    ranges, an all-null key, Boolean keys; and a pair whose ranges need more
+    than 63 bits (hash path)."""
+    rng = np.random.default_rng(17)
+    n = 60_000
+    cols = _rand_frame(rng, n)
+    i32 = rng.choice(np.array([-2**31, 2**31 - 1, 0, -1], dtype=np.int32), n)
+    u32 = rng.choice(np.array([0, 2**32 - 1, 7], dtype=np.uint32), n)
+    neg = rng.integers(-10**15, -10**15 + 50, n).astype(np.int64)
+    alln = (np.zeros(n, np.int64), np.zeros(n, bool))
+    b = rng.random(n) < 0.5
+    _check({"i32": (i32, rng.random(n) > 0.1), "u32": (u32, None), "neg": (neg, None), "z": alln,
+            "bk": (b, rng.random(n) > 0.3)}, cols, [("sum", "a"), ("len", "b")], True)
+    wide = rng.choice(np.array([np.iinfo(np.int64).min, np.iinfo(np.int64).max, 0]), n)
+    _check({"w1": (wide, None), "w2": (wide[::-1].copy(), None)}, cols, [("sum", "d"), ("len", "a")], False)

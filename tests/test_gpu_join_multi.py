@@ -60,7 +60,12 @@ def _df(keys, names, idxname):
 @pytest.mark.parametrize("nkeys", [2, 4])
 @pytest.mark.parametrize("nulls_equal", [False, True])
 @pytest.mark.parametrize("order", ["none", "left", "right", "left_right", "right_left"])
-def test_join_multi_pairs_vs_oracle(gpu, nl, nr, card, nkeys, nulls_equal, order):
+@pytest.mark.parametrize("pack", [True, False])
+def test_join_multi_pairs_vs_oracle(gpu, nl, nr, card, nkeys, nulls_equal, order, pack, monkeypatch):
+    """Key sets without Float64 pack into one exact Int64 key; PLGPU_NO_PACK
+    forces the hash + pair-verify path."""
+    if not pack:
+        monkeypatch.setenv("PLGPU_NO_PACK", "1")
     rng = np.random.default_rng(nl + 3 * nr + card + nkeys)
     lk, rk = _keys(rng, nl, card)[:nkeys], _keys(rng, nr, card)[:nkeys]
     names = ["a", "b", "f", "t"][:nkeys]
@@ -98,6 +103,7 @@ def test_join_multi_left_right_on_and_collisions(gpu, monkeypatch):
     """Different key names per side; a forced 3-bit first hash must be
     caught by the pair verification and re-run."""
     monkeypatch.setenv("PLGPU_MK_COLLIDE", "1")
+    monkeypatch.setenv("PLGPU_NO_PACK", "1")
     rng = np.random.default_rng(2)
     lk, rk = _keys(rng, 5000, 30), _keys(rng, 700, 30)
     ol, orr = O.join_inner_multi(lk[:3], rk[:3], False)

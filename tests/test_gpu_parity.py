@@ -323,6 +323,31 @@ def test_group_by_fast_path_vs_oracle(gpu, n, aggset, pname):
         assert info["path"] == (2 if aggset == "sumonly" else 1), info
 
 
+@pytest.mark.parametrize("card", [5000, 60000, 300000])
+@pytest.mark.parametrize("pname", [None, "simple_f64", "program"])
+@pytest.mark.parametrize("maintain_order", [False, True])
+def test_group_by_partitioned_vs_oracle(gpu, card, pname, maintain_order):
+    """More groups than one LDS table: the selected rows are scattered into
+    hash partitions whose groups fit LDS tables (info path 3)."""
+    rng = np.random.default_rng(card + (pname is None))
+    n = 1_500_001
+    a = rng.standard_normal(n) * 100
+    a[rng.random(n) < 0.001] = np.nan
+    a[rng.random(n) < 0.001] = -0.0
+    cols = {"a": (a, None), "b": (rng.integers(-10**12, 10**12, n).astype(np.int64), None),
+            "c": (rng.integers(-50, 50, n).astype(np.int32), None), "d": (rng.uniform(-5, 5, n), None)}
+    key = rng.integers(0, card, n).astype(np.int64) * 7919 - 3
+    key[rng.random(n) < 0.001] = np.iinfo(np.int64).min
+    aggs = [("sum", "a"), ("mean", "d"), ("min", "b"), ("max", "c"), ("sum", "c"), ("len", "a")]
+    info = {}
+    if pname is None:
+        _check_group_by(cols, key, None, aggs, None, None, [], maintain_order, info)
+    else:
+        mk, names, prog = PREDICATES[pname]
+        _check_group_by(cols, key, None, aggs, mk(), prog, names, maintain_order, info)
+    assert info["path"] == 3, info
+
+
 def test_group_by_special_keys_and_i32_key(gpu):
     rng = np.random.default_rng(5)
     n = 20000
