@@ -329,6 +329,34 @@ int plgpu_join_inner_multi(const plgpu_column* left_keys, const plgpu_column* ri
 int plgpu_gather(const plgpu_column* cols, int32_t ncols, const plgpu_column* idx,
                  plgpu_column* out_cols, void* stream);
 
+/* ---- row shuffles (multi-GPU join / group-by) -------------------------------
+ * Stable hash partitioning of rows by 1..8 key columns into nparts (1..1024)
+ * partitions: out_perm (UInt32, library-owned) lists the rows partition by
+ * partition, in row order within each; out_counts[p] = rows of partition p.
+ * A key tuple holding a null is dropped when nulls_equal == 0 (it cannot
+ * join) and routed to partition 0 otherwise.  The partition of a row depends
+ * only on its key values, so every rank routes equal keys alike.  Replaces
+ * polars-utils/src/hashing.rs:101 HashPartitioner::hash_to_partition as
+ * used by polars-stream/src/nodes/joins/equi_join.rs:445 / :740
+ * (partition_and_sink / partition_and_probe). */
+int plgpu_hash_partition(const plgpu_column* keys, int32_t nkeys, int32_t nparts,
+                         int32_t nulls_equal, plgpu_column* out_perm, int64_t* out_counts,
+                         void* stream);
+
+/* Pack rows into caller-owned flat buffers (e.g. RCCL send tensors):
+ * dst_values[i][o] = cols[i][idx[o]] (idx NULL: o), 8 / 4 bytes per value,
+ * one byte (0/1) per Boolean value; dst_valid[i] (when dst_valid and
+ * dst_valid[i] are non-NULL) gets one validity byte per row.  The
+ * send-side half of the reference's per-partition DataFrame::take. */
+int plgpu_gather_rows(const plgpu_column* cols, int32_t ncols, const plgpu_column* idx,
+                      void* const* dst_values, uint8_t* const* dst_valid, void* stream);
+
+/* Bytes (0 / non-zero) -> Arrow LSB-first bitmap of ceil(n / 64) 8-byte
+ * words; *out_zero_count (optional) = number of zero bytes (the null count
+ * of a validity mask).  The receive-side inverse of plgpu_gather_rows. */
+int plgpu_pack_bits(const uint8_t* bytes, int64_t n, uint8_t* out_bits, int64_t* out_zero_count,
+                    void* stream);
+
 /* ---- sort ------------------------------------------------------------------
  * Stable arg-sort of one column (I64 / I32 / U32 / F64) into a UInt32
  * permutation: TotalOrd order (NaN greatest, -0.0 == 0.0), descending

@@ -126,6 +126,9 @@ SIGNATURES = {
                                          _P]),
     "plgpu_join_inner": (C.c_int, [_COLP, _COLP, C.c_int32, C.c_int32, C.c_int32, _COLP, _COLP, _P]),
     "plgpu_gather": (C.c_int, [_COLP, C.c_int32, _COLP, _COLP, _P]),
+    "plgpu_hash_partition": (C.c_int, [_COLP, C.c_int32, C.c_int32, C.c_int32, _COLP, C.POINTER(C.c_int64), _P]),
+    "plgpu_gather_rows": (C.c_int, [_COLP, C.c_int32, _COLP, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), _P]),
+    "plgpu_pack_bits": (C.c_int, [_P, C.c_int64, _P, C.POINTER(C.c_int64), _P]),
     "plgpu_arg_sort_multi": (C.c_int, [_COLP, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32), _COLP, _P]),
     "plgpu_arg_sort": (C.c_int, [_COLP, C.c_int32, C.c_int32, _COLP, _P]),
     "plgpu_rolling": (C.c_int, [_COLP, C.c_int32, C.c_int64, C.c_int64, C.c_int32, _COLP, _P]),

@@ -189,3 +189,271 @@ def group_by_agg(df, key: str, aggs: Sequence[Expr], predicate: Expr | None = No
         d["groups"] = mi.groups
         info.update(d)
     return out
+
+
+# ====================================================================== join
+# Multi-GPU inner equi-join.  The reference's streaming equi-join
+# (polars-stream/src/nodes/joins/equi_join.rs) splits both sides with one
+# HashPartitioner (:445 partition_and_sink for the build side, :740
+# partition_and_probe for the probe side) so that partition p of the build
+# side only meets partition p of the probe side.  Across GPUs:
+#
+#   shuffle   - every rank hash-partitions both of its shards by key into
+#               `world` partitions (plgpu_hash_partition), packs the rows
+#               partition-major into flat buffers (plgpu_gather_rows) and
+#               exchanges them with one all-to-all per buffer (RCCL over
+#               xGMI); each rank then joins the partition it owns with the
+#               single-GPU join.  Volume = both sides' rows, once.
+#   broadcast - when the smaller side is small (a dimension table such as
+#               BASELINE configs[3]'s 1e7-row build), it is all-gathered to
+#               every rank and each rank joins its local shard of the larger
+#               side against it: the large side never moves, so the per-rank
+#               work is the local probe (weak scaling).
+#
+# Either way each rank returns its share of the inner join; the union over
+# ranks equals the single-process join as a multiset of rows (the order is
+# unspecified, as with the reference's maintain_order="none").
+
+JOIN_BROADCAST_ROWS = 1 << 26  # the smaller side is broadcast up to 64M rows (all ranks)
+
+_TORCH_WIRE = {N.I64: "int64", N.F64: "int64", N.I32: "int32", N.U32: "int32", N.BOOL: "uint8"}
+
+
+class WireColumn:
+    """One column on the wire: values (8 / 4 bytes per row, Booleans one
+    byte) and an optional validity byte mask, as flat torch tensors."""
+
+    __slots__ = ("name", "dtype", "values", "valid")
+
+    def __init__(self, name: str, dtype: int, values, valid):
+        self.name, self.dtype, self.values, self.valid = name, dtype, values, valid
+
+
+def _wire_spec(cols: Sequence[WireColumn], group) -> list[tuple[str, int, bool]]:
+    """(name, dtype, nullable) agreed by all ranks: the schemas must match and
+    a column is sent with a validity mask if any rank holds nulls in it."""
+    import torch.distributed as dist
+
+    mine = [(c.name, int(c.dtype), c.valid is not None) for c in cols]
+    world = dist.get_world_size(group)
+    allspecs: list = [None] * world
+    dist.all_gather_object(allspecs, mine, group=group)
+    base = [(n, d) for n, d, _ in allspecs[0]]
+    for s in allspecs[1:]:
+        if [(n, d) for n, d, _ in s] != base:
+            raise N.ComputeError("multi-GPU join: the ranks' shards have different schemas")
+    return [(n, d, any(s[i][2] for s in allspecs)) for i, (n, d) in enumerate(base)]
+
+
+def _fill_valid(c: WireColumn, nullable: bool):
+    import torch
+
+    if nullable and c.valid is None:
+        c.valid = torch.ones(c.values.shape[0], dtype=torch.uint8, device=c.values.device)
+    elif not nullable:
+        c.valid = None
+
+
+def exchange_columns(cols: Sequence[WireColumn], counts: Sequence[int], group=None):
+    """All-to-all of rows grouped by destination rank (`counts[r]` rows for
+    rank r, in rank order).  Returns (received columns, rows received)."""
+    import torch
+    import torch.distributed as dist
+
+    spec = _wire_spec(cols, group)
+    device = cols[0].values.device if cols else torch.device("cpu")
+    sc = torch.tensor(list(counts), dtype=torch.int64, device=device)
+    rc = torch.empty_like(sc)
+    dist.all_to_all_single(rc, sc, group=group)
+    rcounts = [int(v) for v in rc.tolist()]
+    n = sum(rcounts)
+    out = []
+    for c, (name, dt, nullable) in zip(cols, spec):
+        _fill_valid(c, nullable)
+        bufs = []
+        for t in (c.values, c.valid):
+            if t is None:
+                bufs.append(None)
+                continue
+            r = torch.empty(n, dtype=t.dtype, device=t.device)
+            dist.all_to_all_single(r, t, output_split_sizes=rcounts, input_split_sizes=list(counts), group=group)
+            bufs.append(r)
+        out.append(WireColumn(name, dt, bufs[0], bufs[1]))
+    return out, n
+
+
+def allgather_columns(cols: Sequence[WireColumn], rows: int, group=None):
+    """Every rank receives every rank's rows (rank order).  Returns
+    (columns, total rows)."""
+    import torch
+    import torch.distributed as dist
+
+    spec = _wire_spec(cols, group)
+    world = dist.get_world_size(group)
+    device = cols[0].values.device if cols else torch.device("cpu")
+    cnt = torch.tensor([rows], dtype=torch.int64, device=device)
+    allc = [torch.empty_like(cnt) for _ in range(world)]
+    dist.all_gather(allc, cnt, group=group)
+    counts = [int(t.item()) for t in allc]
+    cap = max(counts) if counts else 0
+    total = sum(counts)
+    out = []
+    for c, (name, dt, nullable) in zip(cols, spec):
+        _fill_valid(c, nullable)
+        bufs = []
+        for t in (c.values, c.valid):
+            if t is None:
+                bufs.append(None)
+                continue
+            padded = torch.zeros(cap, dtype=t.dtype, device=t.device)
+            padded[:rows] = t[:rows]
+            parts = [torch.empty(cap, dtype=t.dtype, device=t.device) for _ in range(world)]
+            dist.all_gather(parts, padded, group=group)
+            bufs.append(torch.cat([p[:k] for p, k in zip(parts, counts)]) if total else
+                        torch.empty(0, dtype=t.dtype, device=t.device))
+        out.append(WireColumn(name, dt, bufs[0], bufs[1]))
+    return out, total
+
+
+class GpuJoinOps:
+    """The device half of the multi-GPU join, all through the C-ABI."""
+
+    @staticmethod
+    def rows(df) -> int:
+        return df.height
+
+    @staticmethod
+    def partition(df, keys: Sequence[str], world: int, nulls_equal: bool):
+        from .frame import _col_array
+
+        perm = N.Column()
+        counts = (C.c_int64 * world)()
+        ks = [df[k] for k in keys]
+        N.check(N.lib().plgpu_hash_partition(_col_array(ks), len(ks), world, int(nulls_equal), C.byref(perm),
+                                             counts, None))
+        from .frame import Series
+
+        return Series._from_native("__perm", perm), [int(c) for c in counts]
+
+    @staticmethod
+    def to_wire(df, perm=None) -> list[WireColumn]:
+        import torch
+
+        from .frame import _col_array
+
+        n = df.height if perm is None else perm.len()
+        dev = torch.device("cuda", torch.cuda.current_device())
+        names = df.columns
+        out = []
+        for nm in names:
+            s = df[nm]
+            dt = s.dtype.code
+            vals = torch.empty(n, dtype=getattr(torch, _TORCH_WIRE[dt]), device=dev)
+            valid = torch.empty(n, dtype=torch.uint8, device=dev) if s._col.validity else None
+            out.append(WireColumn(nm, dt, vals, valid))
+        if names and n:
+            dv = (C.c_void_p * len(names))(*[c.values.data_ptr() for c in out])
+            vv = (C.c_void_p * len(names))(*[c.valid.data_ptr() if c.valid is not None else None for c in out])
+            N.check(N.lib().plgpu_gather_rows(_col_array([df[nm] for nm in names]), len(names),
+                                              C.byref(perm._col) if perm is not None else None, dv, vv, None))
+        return out
+
+    @staticmethod
+    def from_wire(cols: Sequence[WireColumn], n: int):
+        from .frame import DataFrame, Series, _BY_CODE
+
+        series = []
+        for c in cols:
+            dt = _BY_CODE[c.dtype]
+            keep: list = [c.values, c.valid]
+            vptr = c.values.data_ptr()
+            if c.dtype == N.BOOL:
+                bits = N.DeviceBuffer(((n + 63) // 64) * 8)
+                N.check(N.lib().plgpu_pack_bits(C.c_void_p(vptr), n, C.c_void_p(bits.ptr), None, None))
+                vptr = bits.ptr
+                keep.append(bits)
+            mptr, nulls = None, 0
+            if c.valid is not None:
+                vb = N.DeviceBuffer(((n + 63) // 64) * 8)
+                z = C.c_int64(0)
+                N.check(N.lib().plgpu_pack_bits(C.c_void_p(c.valid.data_ptr()), n, C.c_void_p(vb.ptr), C.byref(z),
+                                                None))
+                mptr, nulls = vb.ptr, int(z.value)
+                keep.append(vb)
+            series.append(Series.from_device(c.name, dt, vptr, n, mptr, keepalive=keep, null_count=nulls))
+        return DataFrame(series)
+
+    @staticmethod
+    def local_join(left, right, left_on, right_on, suffix: str, nulls_equal: bool):
+        from .frame import _join
+
+        return _join(left, right, left_on, right_on, suffix, "m:m", nulls_equal, "none")
+
+
+def run_join(ops, left, right, left_keys: Sequence[str], right_keys: Sequence[str], suffix: str,
+             nulls_equal: bool, strategy: str, group, device, info: dict | None = None):
+    """The multi-GPU join protocol over any `ops` implementation (the GPU one
+    above, or a host model in tests/test_distributed.py)."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    sizes = torch.tensor([ops.rows(left), ops.rows(right)], dtype=torch.int64, device=device)
+    dist.all_reduce(sizes, group=group)
+    nl, nr = (int(v) for v in sizes.tolist())
+    if strategy == "auto":
+        strategy = "broadcast" if min(nl, nr) <= JOIN_BROADCAST_ROWS else "shuffle"
+    if strategy not in ("broadcast", "shuffle"):
+        raise ValueError(f"invalid join strategy {strategy!r}")
+    lk = left_keys[0] if len(left_keys) == 1 else tuple(left_keys)
+    rk = right_keys[0] if len(right_keys) == 1 else tuple(right_keys)
+    if strategy == "broadcast":
+        if nr <= nl:
+            cols, n = allgather_columns(ops.to_wire(right), ops.rows(right), group)
+            right = ops.from_wire(cols, n)
+        else:
+            cols, n = allgather_columns(ops.to_wire(left), ops.rows(left), group)
+            left = ops.from_wire(cols, n)
+        moved = n
+    else:
+        moved = 0
+        sides = []
+        for df, keys in ((left, left_keys), (right, right_keys)):
+            perm, counts = ops.partition(df, keys, world, nulls_equal)
+            cols, n = exchange_columns(ops.to_wire(df, perm), counts, group)
+            sides.append(ops.from_wire(cols, n))
+            moved += n
+        left, right = sides
+    out = ops.local_join(left, right, lk, rk, suffix, nulls_equal)
+    if info is not None:
+        info.update({"strategy": strategy, "left_rows": nl, "right_rows": nr, "rows_received": moved})
+    return out
+
+
+def join(left, right, on: str | Sequence[str] | None = None, *, left_on=None, right_on=None,
+         suffix: str = "_right", nulls_equal: bool = False, strategy: str = "auto", group=None,
+         info: dict | None = None):
+    """`left.join(right, on=..., how="inner")` over the shards held by all
+    ranks of `group` (one GPU per rank, RCCL).  Returns this rank's share of
+    the result; the union over ranks is the join of the concatenated shards.
+    strategy: "auto" (broadcast the smaller side up to JOIN_BROADCAST_ROWS
+    rows, else shuffle), "broadcast" or "shuffle"."""
+    import torch
+    import torch.distributed as dist
+
+    if not dist.is_initialized():
+        raise N.InvalidOperationError("torch.distributed is not initialised")
+    device = _device_for(group)
+    if device.type != "cuda":
+        raise N.InvalidOperationError("the GPU join needs the nccl (RCCL) backend")
+    if on is not None:
+        left_on = right_on = on
+    if left_on is None or right_on is None:
+        raise ValueError("must specify `on` OR `left_on` and `right_on`")
+    lks = [left_on] if isinstance(left_on, str) else list(left_on)
+    rks = [right_on] if isinstance(right_on, str) else list(right_on)
+    if len(lks) != len(rks):
+        raise N.InvalidOperationError("the number of join key columns must be equal on both sides")
+    out = run_join(GpuJoinOps, left, right, lks, rks, suffix, nulls_equal, strategy, group, device, info)
+    torch.cuda.synchronize()
+    return out
