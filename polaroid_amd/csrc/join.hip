@@ -294,11 +294,13 @@ __global__ __launch_bounds__(kJnThreads) void jn_probe_match_kernel(DevCol pk, i
 
 // Pass B: pairs in probe-row order.  Row r = base + k*T + tid of a tile is
 // ranked k*T + tid; one block scan per k.
+// `rowmap` (partitioned probe): position r holds probe row rowmap[r].
 __global__ __launch_bounds__(kJnThreads) void jn_probe_emit_kernel(int64_t np, JnTable t,
                                                                    const uint32_t* __restrict__ m,
                                                                    const uint64_t* __restrict__ tile_off,
                                                                    int64_t ntiles, uint32_t* __restrict__ out_p,
-                                                                   uint32_t* __restrict__ out_b) {
+                                                                   uint32_t* __restrict__ out_b,
+                                                                   const uint32_t* __restrict__ rowmap) {
     __shared__ uint64_t wsum[kJnThreads / 64];
     constexpr int R = kJnTileRows / kJnThreads;
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
@@ -324,18 +326,286 @@ __global__ __launch_bounds__(kJnThreads) void jn_probe_emit_kernel(int64_t np, J
             }
             uint64_t total;
             const uint64_t pos = run + block_excl_scan(c, wsum, total);
+            const uint32_t pr = c ? (rowmap ? rowmap[r] : (uint32_t)r) : 0u;
             if (c == 1 && !(w[k] & kRefList)) {
-                out_p[pos] = (uint32_t)r;
+                out_p[pos] = pr;
                 out_b[pos] = w[k];
             } else {
                 for (uint32_t j = 0; j < c; ++j) {
-                    out_p[pos + j] = (uint32_t)r;
+                    out_p[pos + j] = pr;
                     out_b[pos + j] = t.rows[lo + j];
                 }
             }
             run += total;
         }
     }
+}
+
+
+// ------------------------------------------ partitioned probe (large builds)
+// For builds whose table cannot stay in L2 (>= 2^18 distinct keys) the
+// random table reads of the plain probe are served by the Infinity Cache at
+// ~1.5 line requests per probe row, which bounds it at ~30 ms per 1e9 rows.
+// The partitioned probe (maintain_order="none") turns them into streaming:
+//   build - the distinct keys of the global table are split into P = 2^pb
+//           partition tables of 2^cbits slots ({key, ref word}, load <= 0.6,
+//           ~0.5-1.5 MB each, sized to sit in one XCD's 4 MiB L2);
+//   count / scatter - the probe rows are radix-partitioned by the same hash
+//           into (key, row) pairs: per-chunk LDS histograms, a device scan,
+//           and 4096-row tiles ranked in LDS so every partition's rows of a
+//           tile leave as one coalesced run; null (nulls_equal) and
+//           INT64_MIN keys go to one extra "special" bucket;
+//   match - partitions are numbered so that the P/8 partitions of an XCD
+//           group are contiguous, and blocks b, b+8, ... (one XCD under the
+//           observed round-robin placement; speed only, never correctness)
+//           sweep one group, so each XCD's L2 holds the one or two tables
+//           its blocks are probing;
+//   emit  - the plain emit kernel through the row map.
+// Output pairs come in partition order, which maintain_order="none"
+// leaves unspecified (the reference's order there is its thread chunking).
+constexpr int kPjThreads = 256;
+constexpr int kPjPer = 16;
+constexpr int kPjTile = kPjThreads * kPjPer;  // 4096 rows
+constexpr int kPjMaxBits = 10;
+constexpr int kPjMaxBuckets = (1 << kPjMaxBits) + 1;  // + the special bucket
+constexpr int kPjQpt = (kPjMaxBuckets + kPjThreads - 1) / kPjThreads;
+constexpr uint64_t kPjSalt = 0x9FB21C651E98DF25ull;
+
+__device__ __forceinline__ uint64_t pj_hash(uint64_t key) { return mk_fmix(key ^ kPjSalt); }
+
+// Top pb bits of the hash, rotated so the P/8 partitions of XCD group
+// (raw & 7) are contiguous: q = (raw & 7) * P/8 + raw / 8.
+__device__ __forceinline__ uint32_t pj_part(uint64_t h, int pb) {
+    const uint32_t raw = (uint32_t)(h >> (64 - pb));
+    return ((raw & 7u) << (pb - 3)) | (raw >> 3);
+}
+
+struct PjTab {
+    uint64_t* keys;  // P * 2^cbits, EMPTY = INT64_MIN
+    uint32_t* refs;  // ref word: build row, or kRefList | global slot
+    int pb;
+    int cbits;
+};
+
+// Distinct regular keys per partition at pb = kPjMaxBits.
+__global__ __launch_bounds__(256) void pj_bcount_kernel(JnTable t, uint32_t* __restrict__ pcount) {
+    __shared__ uint32_t h[1 << kPjMaxBits];
+    for (int i = threadIdx.x; i < (1 << kPjMaxBits); i += blockDim.x) h[i] = 0;
+    __syncthreads();
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < t.cap; s += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = t.keys[s];
+        if (k != kEmptyKey) atomicAdd(&h[pj_part(pj_hash(k), kPjMaxBits)], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < (1 << kPjMaxBits); i += blockDim.x)
+        if (h[i]) atomicAdd(&pcount[i], h[i]);
+}
+
+__global__ void pj_init_kernel(PjTab pt, int64_t slots) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < slots; i += (int64_t)gridDim.x * blockDim.x)
+        pt.keys[i] = kEmptyKey;
+}
+
+__global__ __launch_bounds__(256) void pj_binsert_kernel(JnTable t, PjTab pt) {
+    const uint64_t mask = (1ull << pt.cbits) - 1;
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < t.cap; s += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = t.keys[s];
+        if (k == kEmptyKey) continue;
+        const uint64_t h = pj_hash(k);
+        const uint64_t base = (uint64_t)pj_part(h, pt.pb) << pt.cbits;
+        const uint32_t ref = t.ref[s];
+        const uint32_t w = ref == kRefList ? (kRefList | (uint32_t)s) : ref;
+        uint64_t sl = h & mask;
+        for (uint64_t i = 0; i <= mask; ++i, sl = (sl + 1) & mask) {
+            const unsigned long long prev =
+                atomicCAS((unsigned long long*)&pt.keys[base + sl], (unsigned long long)kEmptyKey, (unsigned long long)k);
+            if (prev == (unsigned long long)kEmptyKey) {
+                pt.refs[base + sl] = w;
+                break;
+            }
+        }
+    }
+}
+
+// Bucket of probe row r (P = special, ~0u = dropped null); key word out.
+__device__ __forceinline__ uint32_t pj_bucket(const DevCol& pk, int64_t r, int pb, bool neq, uint64_t& key) {
+    key = 0;
+    if (!dev_valid(pk, r)) return neq ? (1u << pb) : ~0u;
+    key = dev_load(pk, r);
+    if (key == kEmptyKey) return 1u << pb;
+    return pj_part(pj_hash(key), pb);
+}
+
+__device__ __forceinline__ void pj_chunk(int64_t n, int64_t& lo, int64_t& hi) {
+    const int64_t tiles = (n + kPjTile - 1) / kPjTile;
+    const int64_t per = (tiles + gridDim.x - 1) / gridDim.x;
+    lo = std::min<int64_t>(n, (int64_t)blockIdx.x * per * kPjTile);
+    hi = std::min<int64_t>(n, lo + per * kPjTile);
+}
+
+// cnt[q * G + b]: rows of block b's chunk in bucket q.
+__global__ __launch_bounds__(kPjThreads) void pj_count_kernel(DevCol pk, int64_t np, int pb, bool neq,
+                                                              uint32_t* __restrict__ cnt) {
+    __shared__ uint32_t h[kPjMaxBuckets];
+    const int B = (1 << pb) + 1;
+    for (int i = threadIdx.x; i < B; i += blockDim.x) h[i] = 0;
+    __syncthreads();
+    int64_t lo, hi;
+    pj_chunk(np, lo, hi);
+    for (int64_t r = lo + threadIdx.x; r < hi; r += blockDim.x) {
+        uint64_t key;
+        const uint32_t q = pj_bucket(pk, r, pb, neq, key);
+        if (q != ~0u) atomicAdd(&h[q], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < B; i += blockDim.x) cnt[(int64_t)i * gridDim.x + blockIdx.x] = h[i];
+}
+
+__global__ __launch_bounds__(kPjThreads) void pj_scatter_kernel(DevCol pk, int64_t np, int pb, bool neq,
+                                                                const uint64_t* __restrict__ off,
+                                                                uint64_t* __restrict__ okey,
+                                                                uint32_t* __restrict__ orow) {
+    __shared__ uint32_t h[kPjMaxBuckets];
+    __shared__ uint32_t lstart[kPjMaxBuckets];
+    __shared__ uint64_t gcur[kPjMaxBuckets];
+    __shared__ uint64_t skey[kPjTile];
+    __shared__ uint16_t srow[kPjTile];
+    __shared__ uint16_t sbk[kPjTile];
+    __shared__ uint64_t wsum[kPjThreads / 64];
+    __shared__ uint32_t tile_n;
+    const int B = (1 << pb) + 1;
+    for (int i = threadIdx.x; i < B; i += blockDim.x) gcur[i] = off[(int64_t)i * gridDim.x + blockIdx.x];
+    int64_t lo, hi;
+    pj_chunk(np, lo, hi);
+    for (int64_t base = lo; base < hi; base += kPjTile) {
+        for (int i = threadIdx.x; i < B; i += blockDim.x) h[i] = 0;
+        __syncthreads();
+        uint32_t pr[kPjPer];
+        uint64_t key[kPjPer];
+#pragma unroll
+        for (int k = 0; k < kPjPer; ++k) {
+            const int64_t r = base + k * kPjThreads + threadIdx.x;
+            pr[k] = ~0u;
+            key[k] = 0;
+            if (r < hi) {
+                const uint32_t q = pj_bucket(pk, r, pb, neq, key[k]);
+                if (q != ~0u) pr[k] = (q << 12) | atomicAdd(&h[q], 1u);
+            }
+        }
+        __syncthreads();
+        uint32_t c[kPjQpt], sum = 0;
+#pragma unroll
+        for (int j = 0; j < kPjQpt; ++j) {
+            const int q = threadIdx.x * kPjQpt + j;
+            c[j] = q < B ? h[q] : 0u;
+            sum += c[j];
+        }
+        uint64_t total;
+        uint32_t run = (uint32_t)block_excl_scan(sum, wsum, total);
+#pragma unroll
+        for (int j = 0; j < kPjQpt; ++j) {
+            const int q = threadIdx.x * kPjQpt + j;
+            if (q < B) lstart[q] = run;
+            run += c[j];
+        }
+        if (threadIdx.x == 0) tile_n = (uint32_t)total;
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kPjPer; ++k) {
+            if (pr[k] == ~0u) continue;
+            const uint32_t q = pr[k] >> 12;
+            const uint32_t slot = lstart[q] + (pr[k] & 0xFFFu);
+            skey[slot] = key[k];
+            srow[slot] = (uint16_t)(k * kPjThreads + threadIdx.x);
+            sbk[slot] = (uint16_t)q;
+        }
+        __syncthreads();
+        const uint32_t m = tile_n;
+        for (uint32_t t = threadIdx.x; t < m; t += blockDim.x) {
+            const uint32_t q = sbk[t];
+            const uint64_t pos = gcur[q] + (t - lstart[q]);
+            okey[pos] = skey[t];
+            orow[pos] = (uint32_t)(base + srow[t]);
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < B; i += blockDim.x) gcur[i] += h[i];
+    }
+}
+
+// Match pass over the partitioned rows: m[r] = ref word, per-tile output
+// counts.  Tiles [grp[x], grp[x + 1]) belong to XCD group x.
+__global__ __launch_bounds__(kJnThreads) void pj_match_kernel(const uint64_t* __restrict__ pkey,
+                                                              const uint32_t* __restrict__ prow, int64_t n,
+                                                              int64_t special_lo, PjTab pt, JnTable t, DevCol pk,
+                                                              bool neq, const int64_t* __restrict__ grp,
+                                                              uint32_t* __restrict__ m,
+                                                              uint64_t* __restrict__ tile_counts) {
+    __shared__ uint64_t wsum[kJnThreads / 64];
+    constexpr int R = kJnTileRows / kJnThreads;
+    const int x = blockIdx.x & 7;
+    const int64_t W = gridDim.x >> 3;
+    const int64_t t_hi = grp[x + 1];
+    const uint64_t mask = (1ull << pt.cbits) - 1;
+    for (int64_t tile = grp[x] + (blockIdx.x >> 3); tile < t_hi; tile += W) {
+        uint64_t key[R];
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const int64_t r = tile * kJnTileRows + (int64_t)k * kJnThreads + threadIdx.x;
+            key[k] = r < n ? __builtin_nontemporal_load(pkey + r) : 0;
+        }
+        uint64_t slot[R], home[R];
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const uint64_t h = pj_hash(key[k]);
+            slot[k] = ((uint64_t)pj_part(h, pt.pb) << pt.cbits) | (h & mask);
+            home[k] = pt.keys[slot[k]];
+        }
+        uint32_t w[R];
+        uint64_t c = 0;
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const int64_t r = tile * kJnTileRows + (int64_t)k * kJnThreads + threadIdx.x;
+            w[k] = kRefNone;
+            if (r >= n) continue;
+            if (r >= special_lo) {
+                // null (nulls_equal) or INT64_MIN key: the global special slots
+                const int64_t gs = dev_valid(pk, prow[r]) ? t.cap + 1 : t.cap;
+                const uint32_t ref = t.ref[gs];
+                w[k] = ref == kRefList ? (kRefList | (uint32_t)gs) : ref;
+            } else {
+                uint64_t sl = slot[k];
+                uint64_t kk = home[k];
+                const uint64_t tb = sl & ~mask;
+                for (uint64_t i = 0; i <= mask; ++i) {
+                    if (kk == key[k]) {
+                        w[k] = pt.refs[sl];
+                        break;
+                    }
+                    if (kk == kEmptyKey) break;
+                    sl = tb | ((sl + 1) & mask);
+                    kk = pt.keys[sl];
+                }
+            }
+            if (w[k] != kRefNone) {
+                if (w[k] & kRefList) {
+                    const uint32_t gs = w[k] & ~kRefList;
+                    c += t.off[gs + 1] - t.off[gs];
+                } else {
+                    c += 1;
+                }
+            }
+            __builtin_nontemporal_store(w[k], m + r);
+        }
+        uint64_t total;
+        (void)block_excl_scan(c, wsum, total);
+        if (threadIdx.x == 0) tile_counts[tile] = total;
+    }
+}
+
+
+__global__ void pj_bounds_kernel(const uint64_t* __restrict__ off, int B, int G, int64_t* __restrict__ range) {
+    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q <= B; q += gridDim.x * blockDim.x)
+        range[q] = (int64_t)off[(int64_t)q * G];
 }
 
 static int num_cus_jn() {
@@ -667,7 +937,7 @@ static int jn_probe(const plgpu_column* key, const JnBuilt& b, bool nulls_equal,
     if (!rc) rc = make_owned_column(out_b, PLGPU_U32, (int64_t)total, false, s);
     if (!rc && total > 0) {
         jn_probe_emit_kernel<<<g, kJnThreads, 0, s>>>(np, b.t, m, toff, ntiles, (uint32_t*)out_p->values,
-                                                      (uint32_t*)out_b->values);
+                                                      (uint32_t*)out_b->values, nullptr);
         hipError_t e = hipGetLastError();
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (e != hipSuccess) rc = hip_fail(e, "join probe emit");
@@ -681,6 +951,144 @@ static int jn_probe(const plgpu_column* key, const JnBuilt& b, bool nulls_equal,
         plgpu_column_release(out_b);
     }
     return rc;
+}
+
+
+// Partitioned probe (see pj_* kernels).  *used = false (nothing done) when
+// the build has too few distinct keys for it to pay.
+static int jn_probe_partitioned(const plgpu_column* key, const JnBuilt& b, bool nulls_equal, plgpu_column* out_p,
+                                plgpu_column* out_b, bool* used, hipStream_t s) {
+    *used = false;
+    const int64_t np = key->length;
+    const DevCol pk = as_dev(key);
+    const int cus = num_cus_jn();
+    // opt-in (PLGPU_JOIN_PARTITIONED=1): measured slower end to end on the
+    // 1e9 x 1e7 workload, because the pairs leave in partition order and the
+    // materialising gathers of the probe columns become random (DESIGN.md
+    // §Join, "partitioned probe")
+    const char* force = getenv("PLGPU_JOIN_PARTITIONED");
+    const bool forced = force && force[0] == '1';
+    if (!forced) return PLGPU_OK;
+    // distinct keys per fine partition
+    constexpr int PF = 1 << kPjMaxBits;
+    uint32_t* pcount = nullptr;
+    int rc = dev_alloc((void**)&pcount, PF * 4, s);
+    if (rc) return rc;
+    std::vector<uint32_t> fine(PF);
+    hipError_t e = hipMemsetAsync(pcount, 0, PF * 4, s);
+    if (e == hipSuccess) {
+        pj_bcount_kernel<<<(unsigned)std::min<int64_t>((b.t.cap + 255) / 256, cus * 8), 256, 0, s>>>(b.t, pcount);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(fine.data(), pcount, PF * 4, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    dev_free(pcount, s);
+    if (e != hipSuccess) return hip_fail(e, "partitioned join: build count");
+    int64_t distinct = 0;
+    for (uint32_t c : fine) distinct += c;
+    int pb = 3;
+    while (pb < kPjMaxBits && distinct > (int64_t(40000) << pb)) ++pb;
+    std::vector<int64_t> coarse((size_t)1 << pb, 0);
+    for (int q = 0; q < PF; ++q) {
+        const int raw = ((q & ((PF >> 3) - 1)) << 3) | (q >> (kPjMaxBits - 3));  // un-rotate pj_part
+        coarse[raw >> (kPjMaxBits - pb)] += fine[q];
+    }
+    int64_t mx = 1;
+    for (int64_t c : coarse) mx = std::max(mx, c);
+    int cb = 6;
+    while ((double)(int64_t(1) << cb) * 0.6 < (double)mx) ++cb;
+    const int P = 1 << pb, B = P + 1;
+    PjTab pt;
+    pt.pb = pb;
+    pt.cbits = cb;
+    pt.keys = nullptr;
+    pt.refs = nullptr;
+    const int64_t slots = (int64_t)P << cb;
+    const int64_t G = std::max<int64_t>(1, std::min<int64_t>((np + kPjTile - 1) / kPjTile, (int64_t)cus * 4));
+    const int64_t ncnt = (int64_t)B * G;
+    uint32_t* cnt = nullptr;
+    uint64_t *off = nullptr, *part = nullptr, *pkey = nullptr, *tcount = nullptr, *toff = nullptr, *tpart = nullptr;
+    uint32_t *prow = nullptr, *m = nullptr;
+    int64_t* range = nullptr;
+    rc = dev_alloc((void**)&pt.keys, slots * 8, s);
+    if (!rc) rc = dev_alloc((void**)&pt.refs, slots * 4, s);
+    if (!rc) rc = dev_alloc((void**)&cnt, ncnt * 4, s);
+    if (!rc) rc = dev_alloc((void**)&off, (ncnt + 1) * 8, s);
+    if (!rc) rc = dev_alloc((void**)&part, ((ncnt + kScanChunk - 1) / kScanChunk + 1) * 8, s);
+    if (!rc) rc = dev_alloc((void**)&range, (B + 1 + 9) * 8, s);
+    std::vector<int64_t> hr(B + 1);
+    if (!rc) {
+        pj_init_kernel<<<(unsigned)std::min<int64_t>((slots + 255) / 256, cus * 16), 256, 0, s>>>(pt, slots);
+        pj_binsert_kernel<<<(unsigned)std::min<int64_t>((b.t.cap + 255) / 256, cus * 16), 256, 0, s>>>(b.t, pt);
+        pj_count_kernel<<<(unsigned)G, kPjThreads, 0, s>>>(pk, np, pb, nulls_equal, cnt);
+        e = hipGetLastError();
+        if (e == hipSuccess) e = scan_exclusive<uint32_t>(cnt, ncnt, off, part, s);
+        if (e == hipSuccess) {
+            pj_bounds_kernel<<<(B + 256) / 256, 256, 0, s>>>(off, B, (int)G, range);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) e = hipMemcpyAsync(hr.data(), range, (B + 1) * 8, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) rc = hip_fail(e, "partitioned join: probe count");
+    }
+    const int64_t n = hr[B];  // rows kept (null keys dropped unless nulls_equal)
+    const int64_t ntiles = std::max<int64_t>(1, (n + kJnTileRows - 1) / kJnTileRows);
+    if (!rc) rc = dev_alloc((void**)&pkey, std::max<int64_t>(n, 1) * 8, s);
+    if (!rc) rc = dev_alloc((void**)&prow, std::max<int64_t>(n, 1) * 4, s);
+    if (!rc) rc = dev_alloc((void**)&m, std::max<int64_t>(n, 1) * 4, s);
+    if (!rc) rc = dev_alloc((void**)&tcount, ntiles * 8, s);
+    if (!rc) rc = dev_alloc((void**)&toff, (ntiles + 1) * 8, s);
+    if (!rc) rc = dev_alloc((void**)&tpart, ((ntiles + kScanChunk - 1) / kScanChunk + 1) * 8, s);
+    uint64_t total = 0;
+    if (!rc) {
+        // XCD group x: partitions [x P/8, (x+1) P/8) -> tiles [grp[x], grp[x+1])
+        int64_t grp[9];
+        grp[0] = 0;
+        for (int x = 1; x < 8; ++x) grp[x] = std::max(grp[x - 1], hr[(int64_t)x * (P >> 3)] / kJnTileRows);
+        grp[8] = ntiles;
+        int64_t* dgrp = range + B + 1;
+        e = hipMemcpyAsync(dgrp, grp, sizeof grp, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess) {
+            pj_scatter_kernel<<<(unsigned)G, kPjThreads, 0, s>>>(pk, np, pb, nulls_equal, off, pkey, prow);
+            pj_match_kernel<<<(unsigned)(cus * 8), kJnThreads, 0, s>>>(pkey, prow, n, hr[P], pt, b.t, pk, nulls_equal,
+                                                                     dgrp, m, tcount);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) e = scan_exclusive<uint64_t>(tcount, ntiles, toff, tpart, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(&total, toff + ntiles, 8, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) rc = hip_fail(e, "partitioned join: probe");
+    }
+    if (!rc && total >= 0xFFFFFFFFull) rc = fail(PLGPU_ERR_CAPACITY, "join output exceeds the u32 index space");
+    if (!rc) rc = make_owned_column(out_p, PLGPU_U32, (int64_t)total, false, s);
+    if (!rc) rc = make_owned_column(out_b, PLGPU_U32, (int64_t)total, false, s);
+    if (!rc && total > 0) {
+        const int g = (int)std::min<int64_t>(ntiles, (int64_t)cus * 8);
+        jn_probe_emit_kernel<<<g, kJnThreads, 0, s>>>(n, b.t, m, toff, ntiles, (uint32_t*)out_p->values,
+                                                      (uint32_t*)out_b->values, prow);
+        e = hipGetLastError();
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) rc = hip_fail(e, "partitioned join: emit");
+    }
+    dev_free(pt.keys, s);
+    dev_free(pt.refs, s);
+    dev_free(cnt, s);
+    dev_free(off, s);
+    dev_free(part, s);
+    dev_free(range, s);
+    dev_free(pkey, s);
+    dev_free(prow, s);
+    dev_free(m, s);
+    dev_free(tcount, s);
+    dev_free(toff, s);
+    dev_free(tpart, s);
+    if (rc) {
+        plgpu_column_release(out_p);
+        plgpu_column_release(out_b);
+        return rc;
+    }
+    *used = true;
+    return PLGPU_OK;
 }
 
 static int check_key(const plgpu_column* k) {
@@ -737,8 +1145,12 @@ static int join_inner_impl(const plgpu_column* left_key, const plgpu_column* rig
         rc = fail(PLGPU_ERR_SCHEMA, validate == PLGPU_JOIN_VALIDATE_1_1 ? "join keys did not fulfill 1:1 validation"
                                                                         : "join keys did not fulfill m:1 validation");
     if (!rc) {
-        if (build_right) rc = jn_probe(left_key, b, neq, out_left_idx, out_right_idx, s);
-        else rc = jn_probe(right_key, b, neq, out_right_idx, out_left_idx, s);
+        const plgpu_column* pkey = build_right ? left_key : right_key;
+        plgpu_column* op = build_right ? out_left_idx : out_right_idx;
+        plgpu_column* ob = build_right ? out_right_idx : out_left_idx;
+        bool used = false;
+        if (!ordered) rc = jn_probe_partitioned(pkey, b, neq, op, ob, &used, s);
+        if (!rc && !used) rc = jn_probe(pkey, b, neq, op, ob, s);
     }
     jn_free(b, s);
     (void)hipStreamSynchronize(s);

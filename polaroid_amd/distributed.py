@@ -52,6 +52,61 @@ def _allreduce_max(vals: Sequence[int], group, device) -> list[int]:
     return [int(v) for v in t.tolist()]
 
 
+def _settle(device) -> None:
+    """Host-wait for the received buffers.  RCCL writes them on its own
+    (non-blocking) stream and a synchronous collective only orders torch's
+    current stream after it; the library's kernels run on the HIP null
+    stream, so without this wait they could read a buffer still being
+    received."""
+    import torch
+
+    if device.type == "cuda":
+        torch.cuda.current_stream(device).synchronize()
+
+
+# Largest per-peer message of one all-to-all.  On this image's RCCL
+# (2.26.6) an all_to_all_single moving 4 GB to one peer corrupted data
+# (tools/check_shuffle_scale.py: key checksum mismatch at 5e8 int64 rows,
+# fine at 4e7), so bigger exchanges go in rounds of point-to-point
+# transfers of at most this many bytes per peer.
+A2A_MAX_BYTES = 1 << 30
+
+
+def alltoallv(out, inp, out_splits: Sequence[int], in_splits: Sequence[int], group=None) -> None:
+    """all_to_all_single(out, inp, out_splits, in_splits), in rounds of at
+    most A2A_MAX_BYTES per peer (views of the flat tensors, no copies)."""
+    import torch.distributed as dist
+
+    esz = inp.element_size()
+    if max(list(out_splits) + list(in_splits) + [0]) * esz <= A2A_MAX_BYTES:
+        dist.all_to_all_single(out, inp, output_split_sizes=list(out_splits), input_split_sizes=list(in_splits),
+                               group=group)
+        return
+    world = dist.get_world_size(group)
+    me = dist.get_rank(group)
+    chunk = max(1, A2A_MAX_BYTES // esz)
+    soff = [sum(in_splits[:p]) for p in range(world)]
+    roff = [sum(out_splits[:p]) for p in range(world)]
+    rounds = (max(list(out_splits) + list(in_splits)) + chunk - 1) // chunk
+    for r in range(rounds):
+        ops = []
+        for p in range(world):
+            s0, s1 = min(in_splits[p], r * chunk), min(in_splits[p], (r + 1) * chunk)
+            r0, r1 = min(out_splits[p], r * chunk), min(out_splits[p], (r + 1) * chunk)
+            if p == me:
+                if s1 > s0:
+                    out[roff[p] + r0: roff[p] + r1].copy_(inp[soff[p] + s0: soff[p] + s1])
+                continue
+            peer = p if group is None else dist.get_global_rank(group, p)
+            if s1 > s0:
+                ops.append(dist.P2POp(dist.isend, inp[soff[p] + s0: soff[p] + s1], peer, group))
+            if r1 > r0:
+                ops.append(dist.P2POp(dist.irecv, out[roff[p] + r0: roff[p] + r1], peer, group))
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+
+
 def exchange_records(send, counts: Sequence[int], record_words: int, group=None):
     """All-to-all of records grouped by destination rank.  `send` is a flat
     int64 tensor of sum(counts) * record_words words; returns (recv, n)."""
@@ -64,8 +119,8 @@ def exchange_records(send, counts: Sequence[int], record_words: int, group=None)
     dist.all_to_all_single(rc, sc, group=group)
     rcounts = [int(v) for v in rc.tolist()]
     recv = torch.empty(sum(rcounts) * record_words, dtype=torch.int64, device=device)
-    dist.all_to_all_single(recv, send, output_split_sizes=[c * record_words for c in rcounts],
-                           input_split_sizes=[c * record_words for c in counts], group=group)
+    alltoallv(recv, send, [c * record_words for c in rcounts], [c * record_words for c in counts], group)
+    _settle(device)
     return recv, sum(rcounts)
 
 
@@ -276,9 +331,10 @@ def exchange_columns(cols: Sequence[WireColumn], counts: Sequence[int], group=No
                 bufs.append(None)
                 continue
             r = torch.empty(n, dtype=t.dtype, device=t.device)
-            dist.all_to_all_single(r, t, output_split_sizes=rcounts, input_split_sizes=list(counts), group=group)
+            alltoallv(r, t, rcounts, list(counts), group)
             bufs.append(r)
         out.append(WireColumn(name, dt, bufs[0], bufs[1]))
+    _settle(device)
     return out, n
 
 
@@ -312,6 +368,7 @@ def allgather_columns(cols: Sequence[WireColumn], rows: int, group=None):
             bufs.append(torch.cat([p[:k] for p, k in zip(parts, counts)]) if total else
                         torch.empty(0, dtype=t.dtype, device=t.device))
         out.append(WireColumn(name, dt, bufs[0], bufs[1]))
+    _settle(device)
     return out, total
 
 

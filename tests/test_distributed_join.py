@@ -225,3 +225,44 @@ def test_join_protocol_gloo(world, strategy, keys, nulls_equal, sizes):
             for row in res[r][0]:
                 kt = tuple(row[i] for i in range(len(keys)))
                 assert seen.setdefault(kt, r) == r
+
+
+def _a2a_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rng = np.random.default_rng(rank)
+        splits = [int(x) for x in rng.integers(0, 40, world)]
+        splits[(rank + 1) % world] = 0  # an empty segment
+        inp = torch.arange(sum(splits), dtype=torch.int64) + 1000 * rank
+        sc = torch.tensor(splits, dtype=torch.int64)
+        rc = torch.empty_like(sc)
+        dist.all_to_all_single(rc, sc)
+        rsplits = [int(v) for v in rc.tolist()]
+        direct = torch.empty(sum(rsplits), dtype=torch.int64)
+        dist.all_to_all_single(direct, inp, output_split_sizes=rsplits, input_split_sizes=splits)
+        D.A2A_MAX_BYTES = 64  # 8 int64 per peer and round: many rounds
+        chunked = torch.full((sum(rsplits),), -1, dtype=torch.int64)
+        D.alltoallv(chunked, inp, rsplits, splits)
+        q.put((rank, torch.equal(direct, chunked), sum(rsplits)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_alltoallv_rounds_gloo(world):
+    """The round-wise point-to-point all-to-all (used above A2A_MAX_BYTES per
+    peer) delivers exactly what all_to_all_single does."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_a2a_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok for _, ok, _ in res)
+    assert sum(n for _, _, n in res) > 0

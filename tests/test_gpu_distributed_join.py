@@ -258,5 +258,23 @@ def test_join_world1_rccl(gpu):
             assert out.columns == ref.columns
             assert np.array_equal(out["flag"].to_numpy()[a], ref["flag"].to_numpy()[b])
             assert np.array_equal(out["flag"].validity_numpy()[a], ref["flag"].validity_numpy()[b])
+        # large enough that reading a receive buffer before RCCL finished
+        # writing it would show (the buffers are host-waited on)
+        import torch
+
+        g = torch.Generator(device="cuda")
+        g.manual_seed(1)
+        pk = torch.randint(0, 4_000_000, (40_000_000,), device="cuda", generator=g)
+        bk = torch.randperm(4_000_000, device="cuda", generator=g)[:2_000_000].contiguous()
+        big_l = pl.DataFrame([pl.Series.from_torch("k", pk)])
+        big_r = pl.DataFrame([pl.Series.from_torch("k", bk), pl.Series.from_torch("p", bk * 3 + 1)])
+        member = torch.zeros(4_000_000, dtype=torch.bool, device="cuda")
+        member[bk] = True
+        expect = int(member[pk].sum().item())
+        for strategy in ("shuffle", "broadcast"):
+            out = D.join(big_l, big_r, on="k", strategy=strategy)
+            assert out.height == expect, strategy
+            k = torch.from_numpy(out["k"].to_numpy())
+            assert torch.equal(torch.from_numpy(out["p"].to_numpy()), k * 3 + 1), strategy
     finally:
         dist.destroy_process_group()

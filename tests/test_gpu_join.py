@@ -182,3 +182,57 @@ def test_join_large_properties(gpu):
     k = torch.from_numpy(out["k"].to_numpy())
     p = torch.from_numpy(out["p"].to_numpy())
     assert torch.equal(p, k * 3 + 1)
+
+
+@pytest.mark.parametrize("nl,nr,card,dups", [(0, 10, 5, False), (10, 0, 5, False), (1, 1, 1, False),
+                                             (20000, 5000, 3000, True), (300001, 40000, 100000, False),
+                                             (2_000_003, 700_000, 1_500_000, False),
+                                             (1_000_000, 450_000, 200_000, True)])
+@pytest.mark.parametrize("nulls_equal", [False, True])
+def test_join_partitioned_vs_oracle(gpu, nl, nr, card, dups, nulls_equal, monkeypatch):
+    """The partitioned probe (per-XCD L2 partition tables; maintain_order
+    "none"), forced on at every size: pairs as a multiset, bit-exact, with
+    null / INT64_MIN / INT64_MAX keys, duplicate build keys (CSR row lists)
+    and P from 8 to 32 partitions."""
+    monkeypatch.setenv("PLGPU_JOIN_PARTITIONED", "1")
+    rng = np.random.default_rng(nl + nr + card)
+    nf = 0.05 if nl < 500_000 else 1e-4  # nulls_equal joins every null pair: keep that product small
+    lk, lv = _rand_keys(rng, nl, card, nf, True)
+    rk, rv = _rand_keys(rng, nr, card, nf, True)
+    if dups and nr:
+        rk[rng.random(nr) < 0.2] = rk[0]
+    ol, orr = O.join_inner(O.HostCol(lk, lv), O.HostCol(rk, rv), nulls_equal)
+    left = pl.DataFrame({"k": pl.Series.from_numpy("k", lk, lv), "li": pl.Series.from_numpy("li", np.arange(nl))})
+    right = pl.DataFrame({"k": pl.Series.from_numpy("k", rk, rv), "ri": pl.Series.from_numpy("ri", np.arange(nr))})
+    out = left.join(right, on="k", nulls_equal=nulls_equal)
+    gl, gr = out["li"].to_numpy(), out["ri"].to_numpy()
+    gk, kv = out["k"].to_numpy(), out["k"].validity_numpy()
+    assert gl.shape == ol.shape
+    a = np.lexsort((gr, gl))
+    gl, gr, gk, kv = gl[a], gr[a], gk[a], kv[a]
+    b = np.lexsort((orr, ol))
+    assert np.array_equal(gl, ol[b]) and np.array_equal(gr, orr[b])
+    assert np.array_equal(kv, lv[gl])
+    assert np.array_equal(gk[kv], lk[gl][kv])
+    # the same join without the partitioned probe gives the same multiset
+    monkeypatch.setenv("PLGPU_JOIN_PARTITIONED", "0")
+    ref = left.join(right, on="k", nulls_equal=nulls_equal)
+    c = np.lexsort((ref["ri"].to_numpy(), ref["li"].to_numpy()))
+    assert np.array_equal(ref["li"].to_numpy()[c], gl) and np.array_equal(ref["ri"].to_numpy()[c], gr)
+
+
+def test_join_partitioned_int32_and_validation(gpu, monkeypatch):
+    monkeypatch.setenv("PLGPU_JOIN_PARTITIONED", "1")
+    rng = np.random.default_rng(4)
+    pool = rng.integers(-2**31, 2**31 - 1, 20_000).astype(np.int32)
+    lk = pool[rng.integers(0, pool.size, 100_000)]  # left keys repeat: 1:1 must fail
+    rk = np.unique(lk[rng.random(100_000) < 0.3])
+    rng.shuffle(rk)
+    left = pl.DataFrame({"k": pl.Series.from_numpy("k", lk), "li": pl.Series.from_numpy("li", np.arange(lk.size))})
+    right = pl.DataFrame({"k": pl.Series.from_numpy("k", rk), "ri": pl.Series.from_numpy("ri", np.arange(rk.size))})
+    out = left.join(right, on="k", validate="m:1")
+    ol, orr = O.join_inner(O.HostCol(lk), O.HostCol(rk))
+    a, b = np.lexsort((out["ri"].to_numpy(), out["li"].to_numpy())), np.lexsort((orr, ol))
+    assert np.array_equal(out["li"].to_numpy()[a], ol[b]) and np.array_equal(out["ri"].to_numpy()[a], orr[b])
+    with pytest.raises(pl.ComputeError, match="validation"):
+        left.join(right, on="k", validate="1:1")

@@ -8,6 +8,13 @@ ordered probe and the gather of k, the probe payload and the build payload.
 Build keys are a random 1e7-subset of [0, 2e7); probe keys are uniform on
 [0, 2e7), so half of the probe rows match exactly one build row.
 Prints one JSON line.
+
+With --dist (under `python -m torch.distributed.run --nproc-per-node N`):
+every rank holds --probe rows of the probe side and --build / N rows of the
+build side, and the step is polaroid_amd.distributed.join (RCCL; "auto"
+broadcasts the 1e7-row build side, so the probe never moves: weak scaling);
+the time is the max over ranks between barriers and `value` counts the
+probe rows of all ranks.
 """
 import argparse
 import json
@@ -25,12 +32,16 @@ def main():
     ap.add_argument("--build", type=float, default=1e7)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--dist", action="store_true")
+    ap.add_argument("--strategy", default="auto")
     args = ap.parse_args()
     import torch
 
     import polaroid_amd as pl
 
     n, m = int(args.probe), int(args.build)
+    if args.dist:
+        return dist_main(args, n, m)
     g = torch.Generator(device="cuda")
     g.manual_seed(7)
     pk = torch.empty(n, dtype=torch.int64, device="cuda")
@@ -62,6 +73,62 @@ def main():
         "config": {"workload": "probe.join(build, on='k') inner, output k, pv, bv", "probe_rows": n,
                    "build_rows": m, "output_rows": rows_out},
     }), flush=True)
+
+
+def dist_main(args, n, m):
+    import torch
+    import torch.distributed as dist
+
+    import polaroid_amd as pl
+    from polaroid_amd import distributed as D
+
+    rank, world = int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1))
+    torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", 0)))
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    dist.init_process_group("nccl", rank=rank, world_size=world)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(7)  # the same build-key permutation on every rank
+    bk_all = torch.randperm(2 * m, device="cuda", generator=g)[:m].to(torch.int64)
+    lo, hi = rank * m // world, (rank + 1) * m // world
+    bk = bk_all[lo:hi].clone()
+    del bk_all
+    g.manual_seed(100 + rank)
+    pk = torch.empty(n, dtype=torch.int64, device="cuda")
+    pv = torch.empty(n, dtype=torch.float64, device="cuda")
+    chunk = 1 << 27
+    for s in range(0, n, chunk):
+        e = min(n, s + chunk)
+        pk[s:e] = torch.randint(0, 2 * m, (e - s,), device="cuda", generator=g)
+        pv[s:e] = torch.rand(e - s, device="cuda", generator=g, dtype=torch.float64)
+    bv = torch.rand(hi - lo, device="cuda", generator=g, dtype=torch.float64)
+    probe = pl.DataFrame([pl.Series.from_torch("k", pk), pl.Series.from_torch("pv", pv)])
+    build = pl.DataFrame([pl.Series.from_torch("k", bk), pl.Series.from_torch("bv", bv)])
+    info = {}
+    out = None
+    for _ in range(args.warmup):
+        out = D.join(probe, build, on="k", strategy=args.strategy, info=info)
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = D.join(probe, build, on="k", strategy=args.strategy, info=info)
+    torch.cuda.synchronize()
+    dt = torch.tensor([(time.perf_counter() - t0) / args.steps], dtype=torch.float64, device="cuda")
+    dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    rows = torch.tensor([out.height], dtype=torch.int64, device="cuda")
+    dist.all_reduce(rows)
+    if rank == 0:
+        t = float(dt.item())
+        print(json.dumps({
+            "metric": "Mrows/sec hash inner-join probe (1e9 probe x 1e7 build, i64 key), materialised",
+            "value": round(world * n / t / 1e6, 1), "unit": "Mrows/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(t * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "dtype": "int64", "data": "synthetic keys/payloads generated on device",
+            "config": {"workload": "distributed.join(probe, build, on='k') inner, output k, pv, bv",
+                       "probe_rows_per_gpu": n, "build_rows_total": m, "strategy": info.get("strategy"),
+                       "output_rows": int(rows.item())},
+        }), flush=True)
+    dist.destroy_process_group()
 
 
 if __name__ == "__main__":
