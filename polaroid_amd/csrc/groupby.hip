@@ -599,6 +599,7 @@ __device__ __forceinline__ bool part_sel(const GbParams& p, const DevProgram& pr
 // needs no global atomics.
 constexpr int kPartPer = 8;
 constexpr int64_t kPartTile = (int64_t)kPartThreads * kPartPer;  // 2048 rows
+constexpr int kPartRegAcc = 3;
 
 __device__ __forceinline__ void part_chunk(int64_t n, int64_t& lo, int64_t& hi) {
     const int64_t tiles = (n + kPartTile - 1) / kPartTile;
@@ -636,16 +637,20 @@ struct PartOut {
 };
 
 // Pass 2: per tile of 2048 rows, the selected rows are ranked by partition in
-// LDS (histogram -> block scan -> partition-ordered slots), then written out
-// slot by slot, so each partition's rows of the tile leave as one run per
-// column; the second read of the tile's values hits L2.
+// LDS (histogram -> block scan -> partition-ordered slots).  Then, column by
+// column (key, each aggregated column, the row ids), the tile's values are
+// read coalesced, placed in LDS at their slots and written out slot by slot,
+// so each partition's rows of the tile leave as one coalesced run per
+// column.  (Writing straight from global memory in slot order made every
+// 128-B line of a column be requested once per row it holds: 27 ms per 1e9
+// rows, request-bound.)
 template <int PRED>
 __global__ __launch_bounds__(kPartThreads) void gb_part_scatter_kernel(GbParams p, DevProgram prog, int pbits,
                                                                        const uint64_t* __restrict__ off, PartOut o) {
     __shared__ uint32_t h[1 << kPartMaxBits];
     __shared__ uint32_t lstart[1 << kPartMaxBits];
     __shared__ uint64_t gcur[1 << kPartMaxBits];
-    __shared__ uint16_t srow[kPartTile];
+    __shared__ uint64_t sval[kPartTile];
     __shared__ uint16_t spart[kPartTile];
     __shared__ uint64_t wsum[kPartThreads / 64];
     __shared__ uint32_t tile_sel;
@@ -654,16 +659,34 @@ __global__ __launch_bounds__(kPartThreads) void gb_part_scatter_kernel(GbParams 
     for (int i = threadIdx.x; i < P; i += blockDim.x) gcur[i] = off[(int64_t)i * gridDim.x + blockIdx.x];
     int64_t lo, hi;
     part_chunk(p.n, lo, hi);
+    const int ncols = 1 + p.nacc + (o.rows ? 1 : 0);
     for (int64_t base = lo; base < hi; base += kPartTile) {
         for (int i = threadIdx.x; i < P; i += blockDim.x) h[i] = 0;
         __syncthreads();
         uint32_t pr[kPartPer];
+        uint64_t key[kPartPer];
+        // the first kPartRegAcc aggregated columns are loaded with the key,
+        // so a tile waits for memory once
+        uint64_t av[kPartRegAcc][kPartPer];
+#pragma unroll
+        for (int a = 0; a < kPartRegAcc; ++a) {
+#pragma unroll
+            for (int k = 0; k < kPartPer; ++k) {
+                const int64_t r = base + k * kPartThreads + threadIdx.x;
+                av[a][k] = (a < p.nacc && r < hi) ? dev_load(p.acc[a].c, r) : 0;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kPartPer; ++k) {
+            const int64_t r = base + k * kPartThreads + threadIdx.x;
+            key[k] = r < hi ? dev_load(p.key, r) : 0;
+        }
 #pragma unroll
         for (int k = 0; k < kPartPer; ++k) {
             const int64_t r = base + k * kPartThreads + threadIdx.x;
             pr[k] = ~0u;
             if (r < hi && part_sel<PRED>(p, prog, r)) {
-                const uint32_t q = part_of(dev_load(p.key, r), pbits);
+                const uint32_t q = part_of(key[k], pbits);
                 pr[k] = (q << 16) | atomicAdd(&h[q], 1u);
             }
         }
@@ -686,25 +709,40 @@ __global__ __launch_bounds__(kPartThreads) void gb_part_scatter_kernel(GbParams 
         }
         if (threadIdx.x == 0) tile_sel = (uint32_t)total;
         __syncthreads();
+        // slot of each selected row (in registers), partition of each slot
 #pragma unroll
         for (int k = 0; k < kPartPer; ++k) {
             if (pr[k] == ~0u) continue;
             const uint32_t q = pr[k] >> 16;
             const uint32_t slot = lstart[q] + (pr[k] & 0xFFFFu);
-            srow[slot] = (uint16_t)(k * kPartThreads + threadIdx.x);
+            pr[k] = slot;
             spart[slot] = (uint16_t)q;
         }
-        __syncthreads();
         const uint32_t m = tile_sel;
-        for (uint32_t t = threadIdx.x; t < m; t += blockDim.x) {
-            const uint32_t q = spart[t];
-            const int64_t r = base + srow[t];
-            const uint64_t pos = gcur[q] + (t - lstart[q]);
-            o.key[pos] = dev_load(p.key, r);
-            for (int a = 0; a < p.nacc; ++a) o.acc[a][pos] = dev_load(p.acc[a].c, r);
-            if (o.rows) o.rows[pos] = (uint32_t)r;
+        for (int col = 0; col < ncols; ++col) {
+            // col 0: key; 1..nacc: aggregated columns; last: row ids
+#pragma unroll
+            for (int k = 0; k < kPartPer; ++k) {
+                if (pr[k] == ~0u) continue;
+                const int64_t r = base + k * kPartThreads + threadIdx.x;
+                uint64_t v = (uint64_t)r;
+                if (col == 0) v = key[k];
+#pragma unroll
+                for (int a = 0; a < kPartRegAcc; ++a)
+                    if (col == a + 1) v = av[a][k];
+                if (col > kPartRegAcc && col <= p.nacc) v = dev_load(p.acc[col - 1].c, r);
+                sval[pr[k]] = v;
+            }
+            __syncthreads();
+            uint64_t* dst = col == 0 ? o.key : (col <= p.nacc ? o.acc[col - 1] : nullptr);
+            for (uint32_t t = threadIdx.x; t < m; t += blockDim.x) {
+                const uint32_t q = spart[t];
+                const uint64_t pos = gcur[q] + (t - lstart[q]);
+                if (dst) dst[pos] = sval[t];
+                else o.rows[pos] = (uint32_t)sval[t];
+            }
+            __syncthreads();
         }
-        __syncthreads();
         for (int i = threadIdx.x; i < P; i += blockDim.x) gcur[i] += h[i];
     }
 }
@@ -1895,7 +1933,7 @@ static int gb_partition(GbRun& R) {
     GbParams& p = R.pl.p;
     hipStream_t s = R.s;
     const int P = 1 << R.pbits;
-    const int G = num_cus() * 8;
+    const int G = getenv("PLGPU_PART_G") ? std::max(1, atoi(getenv("PLGPU_PART_G"))) : num_cus() * 8;
     const int64_t ncnt = (int64_t)P * G;
     uint32_t* cnt = nullptr;
     uint64_t* part = nullptr;
