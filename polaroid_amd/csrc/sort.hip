@@ -114,7 +114,7 @@ __global__ void srt_codes_kernel(DevCol c, int64_t n, bool descending, uint64_t*
                                  uint32_t* __restrict__ idx) {
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
         keys[r] = sort_code(c, r, descending);
-        idx[r] = (uint32_t)r;
+        if (idx) idx[r] = (uint32_t)r;
     }
 }
 
@@ -139,6 +139,16 @@ __global__ __launch_bounds__(256) void srt_bits_kernel(const uint64_t* __restric
     }
 }
 
+// Representations of the (code, row id) stream between passes:
+//   SEP    - codes u64 + row ids u32 in two buffers (12 B per row);
+//   PACKED - one u64 word (remaining code bits << 32 | row id) once the
+//            code bits still to be sorted fit 32 bits (LSD: the bytes below
+//            the current pass are never looked at again), 8 B per row;
+//   IDX    - the last pass writes the row ids only (4 B per row).
+// For 40-bit timestamps the traffic per pass drops from 24 to 16 B per row
+// after the first pass, and the last pass writes 4 B instead of 12.
+enum SrtOut { SRT_SEP = 0, SRT_PACK = 1, SRT_IDX = 2 };
+
 // Upsweep: digit counts of every tile, digit-major (cnt[d * ntiles + t]).
 __global__ __launch_bounds__(kSrtThreads) void srt_upsweep_kernel(const uint64_t* __restrict__ keys, int64_t n,
                                                                   int shift, int64_t ntiles,
@@ -150,27 +160,32 @@ __global__ __launch_bounds__(kSrtThreads) void srt_upsweep_kernel(const uint64_t
 #pragma unroll
     for (int k = 0; k < kSrtPer; ++k) {
         const int64_t i = base + k * kSrtThreads + threadIdx.x;
-        if (i < n) atomicAdd(&h[(keys[i] >> shift) & 0xFF], 1u);
+        if (i < n) atomicAdd(&h[(__builtin_nontemporal_load(keys + i) >> shift) & 0xFF], 1u);
     }
     __syncthreads();
     cnt[(int64_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
 }
 
-// Downsweep: stable scatter of one tile by the digit at `shift`.  Wave w
-// ranks its own contiguous 1024 codes row by row (64 codes per row, peer
-// masks from 8 ballots, per-wave digit counters in LDS -- no barriers), then
-// one block-wide combine turns (wave, digit) counts into local positions;
-// the tile is staged in LDS in digit order and written out in runs.
+// Downsweep: stable scatter of one tile by the digit at `shift` (of the
+// input representation).  Wave w ranks its own contiguous 1024 codes row by
+// row (64 codes per row, peer masks from 8 ballots, per-wave digit counters
+// in LDS -- no barriers), then one block-wide combine turns (wave, digit)
+// counts into local positions; the tile is staged in LDS in digit order and
+// written out in runs.  IN_P: input is PACKED.  OUT: SrtOut; a SEP -> PACK
+// transition keeps (code >> cons) & kmask as the remaining code.
+template <bool IN_P, int OUT>
 __global__ __launch_bounds__(kSrtThreads) void srt_downsweep_kernel(const uint64_t* __restrict__ keys_in,
                                                                     const uint32_t* __restrict__ idx_in, int64_t n,
                                                                     int shift, int64_t ntiles,
                                                                     const uint64_t* __restrict__ off,
                                                                     uint64_t* __restrict__ keys_out,
-                                                                    uint32_t* __restrict__ idx_out) {
+                                                                    uint32_t* __restrict__ idx_out, int cons,
+                                                                    uint64_t kmask) {
     constexpr int NW = kSrtThreads / 64;
     constexpr int ROWS = kSrtTile / kSrtThreads;  // rows of 64 per wave (16)
-    __shared__ uint64_t skey[kSrtTile];
-    __shared__ uint32_t sidx[kSrtTile];
+    __shared__ uint64_t skey[OUT == SRT_IDX ? 1 : kSrtTile];
+    __shared__ uint32_t sidx[OUT == SRT_PACK ? 1 : kSrtTile];
+    __shared__ uint8_t sdig[kSrtTile];
     __shared__ uint32_t dstart[256];
     __shared__ uint64_t gbase[256];  // global position of local slot 0 of each digit run
     __shared__ uint32_t cnt[NW][256];
@@ -185,7 +200,7 @@ __global__ __launch_bounds__(kSrtThreads) void srt_downsweep_kernel(const uint64
 #pragma unroll
     for (int r = 0; r < ROWS; ++r) {
         const int i = c0 + r * 64 + lane;
-        k[r] = i < m ? keys_in[base + i] : 0;
+        k[r] = i < m ? __builtin_nontemporal_load(keys_in + base + i) : 0;
     }
     __syncthreads();
     const uint64_t lt = (1ull << lane) - 1;
@@ -228,17 +243,26 @@ __global__ __launch_bounds__(kSrtThreads) void srt_downsweep_kernel(const uint64
         if (i < m) {
             const uint32_t d = (uint32_t)(k[r] >> shift) & 0xFF;
             const uint32_t pos = dstart[d] + cnt[wid][d] + rk[r];
-            skey[pos] = k[r];
-            sidx[pos] = idx_in[base + i];
+            sdig[pos] = (uint8_t)d;
+            if (IN_P) {
+                if (OUT == SRT_IDX) sidx[pos] = (uint32_t)k[r];
+                else skey[pos] = k[r];
+            } else {
+                const uint32_t id = idx_in ? __builtin_nontemporal_load(idx_in + base + i) : (uint32_t)(base + i);
+                if (OUT == SRT_PACK) skey[pos] = (((k[r] >> cons) & kmask) << 32) | id;
+                else {
+                    if (OUT == SRT_SEP) skey[pos] = k[r];
+                    sidx[pos] = id;
+                }
+            }
         }
     }
     __syncthreads();
     // coalesced write-out: consecutive threads, consecutive slots of a digit run
     for (int p = tid; p < m; p += kSrtThreads) {
-        const uint64_t kk = skey[p];
-        const uint64_t o = gbase[(kk >> shift) & 0xFF] + (uint64_t)p;
-        keys_out[o] = kk;
-        idx_out[o] = sidx[p];
+        const uint64_t o = gbase[sdig[p]] + (uint64_t)p;
+        if (OUT != SRT_IDX) keys_out[o] = skey[p];
+        if (OUT != SRT_PACK) idx_out[o] = sidx[p];
     }
 }
 
@@ -300,8 +324,18 @@ struct SrtScratch {
 };
 
 // Stable LSD passes over the bytes of keys[cur] that vary (one OR/AND read
-// finds them), carrying idx[cur]; `cur` names the buffers holding the result.
-static int radix_passes(uint64_t* keys[2], uint32_t* idx[2], int64_t nv, int& cur, SrtScratch& sc, hipStream_t s) {
+// finds them), carrying idx[cur] (nullptr in idx[cur]: row ids are the
+// positions); the result (row ids) ends in idx[cur].  Codes and ids switch
+// to the PACKED representation as soon as the remaining code bits fit 32.
+template <bool IN_P, int OUT>
+static void srt_down(const uint64_t* ki, const uint32_t* ii, int64_t nv, int shift, int64_t ntiles,
+                     const uint64_t* off, uint64_t* ko, uint32_t* io, int cons, uint64_t kmask, hipStream_t s) {
+    srt_downsweep_kernel<IN_P, OUT><<<(unsigned)ntiles, kSrtThreads, 0, s>>>(ki, ii, nv, shift, ntiles, off, ko, io,
+                                                                          cons, kmask);
+}
+
+static int radix_passes(uint64_t* keys[2], uint32_t* idx[2], int64_t nv, int& cur, SrtScratch& sc, hipStream_t s,
+                        bool ids_implicit = false) {
     if (nv <= 0) return PLGPU_OK;
     const int cus = 256;
     unsigned long long h[2] = {0ull, ~0ull};
@@ -314,16 +348,47 @@ static int radix_passes(uint64_t* keys[2], uint32_t* idx[2], int64_t nv, int& cu
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) return hip_fail(e, "sort key bits");
     const int64_t ntiles = (nv + kSrtTile - 1) / kSrtTile;
-    for (int byte = 0; byte < 8; ++byte) {
-        if ((((h[0] ^ h[1]) >> (8 * byte)) & 0xFF) == 0) continue;  // constant byte: the pass is the identity
-        const int shift = 8 * byte;
+    int bytes[8], nb = 0;
+    for (int byte = 0; byte < 8; ++byte)
+        if ((((h[0] ^ h[1]) >> (8 * byte)) & 0xFF) != 0) bytes[nb++] = byte;  // constant bytes: identity passes
+    if (nb == 0) {
+        if (ids_implicit) {
+            srt_iota_kernel<<<(unsigned)std::min<int64_t>((nv + 255) / 256, cus * 16), 256, 0, s>>>(nv, idx[cur]);
+            e = hipGetLastError();
+            if (e != hipSuccess) return hip_fail(e, "sort iota");
+        }
+        return PLGPU_OK;
+    }
+    const int hi_bits = 8 * (bytes[nb - 1] + 1);
+    const bool nopack = getenv("PLGPU_SORT_NO_PACK") != nullptr;
+    bool packed = false;
+    int cons = 0;  // code bits dropped by the packing
+    for (int j = 0; j < nb; ++j) {
+        const int S = 8 * bytes[j];
+        const int shift = packed ? 32 + S - cons : S;
+        const uint32_t* ii = (ids_implicit && j == 0) ? nullptr : idx[cur];
         srt_upsweep_kernel<<<(unsigned)ntiles, kSrtThreads, 0, s>>>(keys[cur], nv, shift, ntiles, sc.cnt);
         e = scan_exclusive<uint32_t>(sc.cnt, ntiles * 256, sc.off, sc.part, s);
-        if (e == hipSuccess) {
-            srt_downsweep_kernel<<<(unsigned)ntiles, kSrtThreads, 0, s>>>(keys[cur], idx[cur], nv, shift, ntiles,
-                                                                         sc.off, keys[cur ^ 1], idx[cur ^ 1]);
-            e = hipGetLastError();
+        if (e != hipSuccess) return hip_fail(e, "sort scan");
+        const bool last = j == nb - 1;
+        const int ncons = S + 8;
+        const bool to_pack = !packed && !last && !nopack && hi_bits - ncons <= 32;
+        const uint64_t kmask = hi_bits - ncons >= 64 ? ~0ull : ((1ull << (hi_bits - ncons)) - 1);
+        uint64_t* ko = keys[cur ^ 1];
+        uint32_t* io = idx[cur ^ 1];
+        if (packed) {
+            if (last) srt_down<true, SRT_IDX>(keys[cur], ii, nv, shift, ntiles, sc.off, ko, io, 0, 0, s);
+            else srt_down<true, SRT_PACK>(keys[cur], ii, nv, shift, ntiles, sc.off, ko, io, 0, 0, s);
+        } else if (last) {
+            srt_down<false, SRT_IDX>(keys[cur], ii, nv, shift, ntiles, sc.off, ko, io, 0, 0, s);
+        } else if (to_pack) {
+            srt_down<false, SRT_PACK>(keys[cur], ii, nv, shift, ntiles, sc.off, ko, io, ncons, kmask, s);
+            packed = true;
+            cons = ncons;
+        } else {
+            srt_down<false, SRT_SEP>(keys[cur], ii, nv, shift, ntiles, sc.off, ko, io, 0, 0, s);
         }
+        e = hipGetLastError();
         if (e != hipSuccess) return hip_fail(e, "sort pass");
         cur ^= 1;
     }
@@ -383,15 +448,16 @@ PLGPU_API int plgpu_arg_sort(const plgpu_column* key, int32_t descending, int32_
         dev_free(part, s);
         part = nullptr;
     } else if (!rc) {
+        // row ids stay implicit (= positions) until the first pass writes them
         srt_codes_kernel<<<(unsigned)std::min<int64_t>((n + 255) / 256, cus * 16), 256, 0, s>>>(
-            c, n, descending != 0, keys[0], idx[0]);
+            c, n, descending != 0, keys[0], nullptr);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) rc = hip_fail(e, "sort codes");
     }
     int cur = 0;
     SrtScratch sc;
     if (!rc) rc = sc.alloc(nv, s);
-    if (!rc) rc = radix_passes(keys, idx, nv, cur, sc, s);
+    if (!rc) rc = radix_passes(keys, idx, nv, cur, sc, s, c.validity == nullptr);
     sc.release(s);
     if (!rc) {
         uint32_t* out = (uint32_t*)out_idx->values;
