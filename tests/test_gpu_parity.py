@@ -448,8 +448,8 @@ def test_group_by_large_properties(gpu):
 def _sum_only_frame(n, seed):
     rng = np.random.default_rng(seed)
     d = rng.uniform(1.0, 1000.0, n)
-    e = rng.uniform(-50.0, 50.0, n)
-    e[e == 0] = 1.0
+    # |e| >= 0.5: the exponent span is narrow whichever rows the plan samples
+    e = rng.uniform(0.5, 50.0, n) * rng.choice([-1.0, 1.0], n)
     key = rng.integers(0, 50, n).astype(np.int64) * 3 + 1
     return rng, key, d, e
 
@@ -462,9 +462,12 @@ def test_sum_window_two_limbs_and_reruns(gpu, inject):
     exact sum either way."""
     n = 300_001
     rng, key, d, e = _sum_only_frame(n, 17)
-    step = n // 65536
-    off = np.arange(1, n, step)[:-1] + 1   # never a multiple of the stride
-    pos = rng.choice(off[off % step != 0], 40, replace=False)
+    # the plan samples 4096 clusters of 16 consecutive rows, cluster c at
+    # row c * (n // 4096) (groupby.hip plan_row): inject outside them
+    cstep = n // 4096
+    rows = np.arange(n)
+    unsampled = rows[(rows >= 4096 * cstep) | (rows % cstep >= 16)]
+    pos = rng.choice(unsampled, 40, replace=False)
     if inject == "tiny":
         d[pos] = 1e-30
     elif inject == "subnormal":
