@@ -300,6 +300,49 @@ enum plgpu_join_validate {
     PLGPU_JOIN_VALIDATE_1_1 = 3
 };
 
+/* Join type (polars-ops/src/frame/join/args.rs JoinType; cross / as-of /
+ * IE joins are not on the GPU path). */
+enum plgpu_join_how {
+    PLGPU_JOIN_INNER = 0,
+    PLGPU_JOIN_LEFT = 1,
+    PLGPU_JOIN_RIGHT = 2,
+    PLGPU_JOIN_FULL = 3,
+    PLGPU_JOIN_SEMI = 4,
+    PLGPU_JOIN_ANTI = 5
+};
+
+/* Equi-join of any type on one integer key (I64 / I32 / U32).  Produces the
+ * row pairs as two UInt32 index columns; a row without a partner has a null
+ * partner index (left / right / full joins: the reference's
+ * NullableIdxSize / ChunkJoinOptIds), and such an index column carries an
+ * Arrow validity bitmap.  Semi / anti joins produce the kept left rows in
+ * `out_left_idx` (in left-row order) and an empty `out_right_idx`.  Pair
+ * order is the reference's for every maintain_order mode (left joins are
+ * always in left order; full joins with maintain_order "none" leave the
+ * order unspecified, as the reference's hash-table drain does).  Replaces
+ *   inner  single_keys_inner.rs:45 hash_join_tuples_inner,
+ *   left   single_keys_left.rs:106 hash_join_tuples_left (+ the ordering of
+ *          dispatch_left_right.rs:143 maintain_order_idx),
+ *   right  dispatch_left_right.rs:19 right_join_from_series,
+ *   full   single_keys_outer.rs:181 hash_join_tuples_outer (+ the ordering of
+ *          hash_join/mod.rs:164 _full_join_from_series),
+ *   semi / anti  single_keys_semi_anti.rs:111 / :95
+ * (paths under polars-ops/src/frame/join/). */
+int plgpu_join(const plgpu_column* left_key, const plgpu_column* right_key, int32_t how, int32_t nulls_equal,
+               int32_t maintain_order, int32_t validate, plgpu_column* out_left_idx, plgpu_column* out_right_idx,
+               void* stream);
+
+/* plgpu_join on 1..8 key columns per side (pairwise equal dtypes: I64 / I32
+ * / U32 / F64 / BOOL; join/mod.rs:625 prepare_keys_multiple). */
+int plgpu_join_multi(const plgpu_column* left_keys, const plgpu_column* right_keys, int32_t nkeys, int32_t how,
+                     int32_t nulls_equal, int32_t maintain_order, int32_t validate, plgpu_column* out_left_idx,
+                     plgpu_column* out_right_idx, void* stream);
+
+/* out[i] = a[i] if valid, else b[i] (same dtype and length); the coalesced
+ * key columns of a full join with coalesce=True
+ * (polars-ops/src/frame/join/general.rs:52 _coalesce_full_join). */
+int plgpu_coalesce(const plgpu_column* a, const plgpu_column* b, plgpu_column* out, void* stream);
+
 /* Inner equi-join on one integer key (I64 / I32 / U32; the two sides may
  * differ, values compare as integers).  Produces the matching row pairs as
  * two UInt32 index columns (the reference's IdxSize pairs).  Null keys match
@@ -323,9 +366,10 @@ int plgpu_join_inner_multi(const plgpu_column* left_keys, const plgpu_column* ri
                            int32_t validate, plgpu_column* out_left_idx,
                            plgpu_column* out_right_idx, void* stream);
 
-/* out_cols[i] = cols[i][idx] (UInt32 indices, no nulls), validity carried.
- * Replaces the join materialisation take
- * (polars-core/src/chunked_array/ops/gather.rs, DataFrame::take_unchecked). */
+/* out_cols[i] = cols[i][idx] (UInt32 indices), validity carried; a null
+ * index gathers a null.  Replaces the join materialisation take
+ * (polars-core/src/chunked_array/ops/gather.rs, DataFrame::take_unchecked;
+ * IdxCa::with_nullable_idx for the outer joins' nullable indices). */
 int plgpu_gather(const plgpu_column* cols, int32_t ncols, const plgpu_column* idx,
                  plgpu_column* out_cols, void* stream);
 

@@ -59,6 +59,8 @@ def lib():
         L.or_group_by_agg.restype = C.c_int64
         L.or_join_inner.restype = C.c_int64
         L.or_join_inner.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int64, C.c_void_p, C.c_void_p]
+        L.or_join.restype = C.c_int64
+        L.or_join.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int64, C.c_void_p, C.c_void_p]
         L.or_arg_sort.restype = None
         L.or_arg_sort.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p]
         L.or_rolling.restype = None
@@ -254,6 +256,98 @@ def join_inner(left: HostCol, right: HostCol, nulls_equal: bool = False):
         if n >= 0:
             return ol[:n].copy(), orr[:n].copy()
         cap *= 4
+
+
+_HOW = {"left": 1, "full": 3, "semi": 4, "anti": 5}
+_FLIP = {None: "none", "none": "none", "left": "right", "right": "left", "left_right": "right_left",
+         "right_left": "left_right"}
+_IDX_NULL = np.int64(2**32 - 1)  # IdxSize::MAX, the reference's null index
+
+
+def _raw_join(left: HostCol, right: HostCol, how: str, nulls_equal: bool):
+    if how == "inner":
+        return join_inner(left, right, nulls_equal)
+    cap = 1 << 16
+    while True:
+        ol = np.zeros(cap, np.int64)
+        orr = np.zeros(cap, np.int64)
+        n = lib().or_join(C.byref(left.c), C.byref(right.c), _HOW[how], int(nulls_equal), cap,
+                          ol.ctypes.data, orr.ctypes.data)
+        if n >= 0:
+            return ol[:n].copy(), orr[:n].copy()
+        cap *= 4
+
+
+def _sort_pairs(ol: np.ndarray, orr: np.ndarray, by: list[str]):
+    """Stable sort of the pairs by the listed index columns, a null (-1)
+    index last (SortMultipleOptions maintain_order + nulls_last)."""
+    if not by or ol.size == 0:
+        return ol, orr
+    cols = {"a": np.where(ol < 0, _IDX_NULL, ol), "b": np.where(orr < 0, _IDX_NULL, orr)}
+    perm = np.lexsort(tuple(cols[c] for c in reversed(by)))  # lexsort is stable
+    return ol[perm], orr[perm]
+
+
+def join(left: HostCol, right: HostCol, how: str = "inner", nulls_equal: bool = False,
+         maintain_order: str | None = "none"):
+    """Row pairs of a join of any type in the reference's order for
+    `maintain_order`: (left_idx, right_idx) with -1 as the null index;
+    semi / anti: (left rows, None).
+      inner   pairs in (left, right) order; "right" / "right_left" sort them
+              by the right index (hash_join/mod.rs _inner_join orders);
+      left    left order (the reference's left join is always ordered);
+              "right" / "right_left" stably sort by the raw right index,
+              whose null is IdxSize::MAX (dispatch_left_right.rs:143
+              maintain_order_idx);
+      right   the left join with the sides swapped and the order flipped
+              (dispatch_left_right.rs:19);
+      full    stable sort by the listed columns, nulls last
+              (hash_join/mod.rs:164); "none" leaves the order unspecified.
+    """
+    order = maintain_order or "none"
+    if how == "right":
+        r, l = join(right, left, "left", nulls_equal, _FLIP[order])
+        return l, r
+    ol, orr = _raw_join(left, right, how, nulls_equal)
+    if how in ("semi", "anti"):
+        return ol, None
+    if how in ("inner", "left"):
+        if order in ("right", "right_left"):
+            return _sort_pairs(ol, orr, ["b", "a"] if how == "inner" else ["b"])
+        return ol, orr
+    by = {"none": [], "left": ["a"], "left_right": ["a", "b"], "right": ["b"], "right_left": ["b", "a"]}[order]
+    return _sort_pairs(ol, orr, by)
+
+
+def join_multi(left_keys: list[tuple[np.ndarray, np.ndarray | None]],
+               right_keys: list[tuple[np.ndarray, np.ndarray | None]], how: str = "inner",
+               nulls_equal: bool = False, maintain_order: str | None = "none"):
+    """`join` on several key columns: tuples encoded to dense ids as in
+    join_inner_multi, then joined as one key."""
+    lc, rc = _multi_ids(left_keys, right_keys, nulls_equal)
+    return join(lc, rc, how, nulls_equal, maintain_order)
+
+
+def _multi_ids(left_keys, right_keys, nulls_equal: bool):
+    nl, nr = left_keys[0][0].shape[0], right_keys[0][0].shape[0]
+    enc_l = np.concatenate([_row_words(v, m) for v, m in left_keys], axis=1)
+    enc_r = np.concatenate([_row_words(v, m) for v, m in right_keys], axis=1)
+    enc = np.concatenate([enc_l, enc_r], axis=0)
+    if nl + nr:
+        _, inv = np.unique(enc, axis=0, return_inverse=True)
+        ids = inv.reshape(-1).astype(np.int64)
+    else:
+        ids = np.zeros(0, np.int64)
+
+    def valid(keys, n):
+        v = np.ones(n, bool)
+        if not nulls_equal:
+            for _, m in keys:
+                if m is not None:
+                    v &= m.astype(bool)
+        return None if v.all() else v
+
+    return HostCol(ids[:nl].copy(), valid(left_keys, nl)), HostCol(ids[nl:].copy(), valid(right_keys, nr))
 
 
 def join_inner_multi(left_keys: list[tuple[np.ndarray, np.ndarray | None]],

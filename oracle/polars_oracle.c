@@ -768,6 +768,87 @@ OR_EXPORT int64_t or_join_inner(const plgpu_column* lk, const plgpu_column* rk, 
     return n;
 }
 
+/* ------------------------------------------------------- other join types
+ * The same build (right side, key -> rows in row order) probed by every left
+ * row in order; how:
+ *   1 left   single_keys_left.rs:106 hash_join_tuples_left: each left row's
+ *            matches in right-row order, or (l, null) when it has none;
+ *   3 full   single_keys_outer.rs:101 probe_outer: the left join's pairs,
+ *            then every right row that no left row matched as (null, r)
+ *            (null right keys among them unless nulls_equal) -- the
+ *            reference drains these in hash-table order, restated here in
+ *            right-row order;
+ *   4 semi / 5 anti  single_keys_semi_anti.rs:111 / :95: the left rows with
+ *            / without a match, in left-row order (out_r unused).
+ * (paths under polars-ops/src/frame/join/hash_join/).  -1 is a null index.
+ * The right join and the maintain_order permutations are restated in
+ * oracle.py on top of these sequences.  Returns the number of rows, or -1
+ * if more than cap. */
+OR_EXPORT int64_t or_join(const plgpu_column* lk, const plgpu_column* rk, int32_t how, int32_t nulls_equal,
+                          int64_t cap, int64_t* out_l, int64_t* out_r) {
+    const int64_t nr = rk->length, nl = lk->length;
+    jn_item* t = (jn_item*)malloc(sizeof(jn_item) * (size_t)(nr > 0 ? nr : 1));
+    char* hit = (char*)calloc((size_t)(nr > 0 ? nr : 1), 1);
+    int64_t m = 0, n = 0;
+    for (int64_t r = 0; r < nr; ++r) {
+        const int v = col_valid(rk, r);
+        if (!v && !nulls_equal) continue;
+        t[m].is_null = !v;
+        t[m].key = v ? col_int(rk, r) : 0;
+        t[m].row = r;
+        ++m;
+    }
+    qsort(t, (size_t)m, sizeof(jn_item), jn_cmp);
+#define OR_PUSH(a, b)                    \
+    do {                                 \
+        if (n >= cap) goto overflow;     \
+        out_l[n] = (a);                  \
+        if (out_r) out_r[n] = (b);       \
+        ++n;                             \
+    } while (0)
+    for (int64_t l = 0; l < nl; ++l) {
+        const int v = col_valid(lk, l);
+        int64_t lo = m, hi = m;
+        if (v || nulls_equal) {
+            jn_item q;
+            q.is_null = !v;
+            q.key = v ? col_int(lk, l) : 0;
+            q.row = -1;
+            int64_t a = 0, b = m;
+            while (a < b) {
+                const int64_t mid = (a + b) / 2;
+                if (jn_cmp(&t[mid], &q) < 0) a = mid + 1;
+                else b = mid;
+            }
+            lo = hi = a;
+            while (hi < m && t[hi].is_null == q.is_null && (q.is_null || t[hi].key == q.key)) ++hi;
+        }
+        if (how == 4 || how == 5) {
+            if ((hi > lo) == (how == 4)) OR_PUSH(l, -1);
+            continue;
+        }
+        if (hi == lo) {
+            OR_PUSH(l, -1);
+            continue;
+        }
+        for (int64_t i = lo; i < hi; ++i) {
+            OR_PUSH(l, t[i].row);
+            hit[t[i].row] = 1;
+        }
+    }
+    if (how == 3)
+        for (int64_t r = 0; r < nr; ++r)
+            if (!hit[r]) OR_PUSH(-1, r);
+#undef OR_PUSH
+    free(t);
+    free(hit);
+    return n;
+overflow:
+    free(t);
+    free(hit);
+    return -1;
+}
+
 /* ------------------------------------------------------------------ sort
  * polars-core/src/chunked_array/ops/sort/arg_sort.rs:7 sort_impl: a stable
  * sort of (idx, value) pairs by TotalOrd (total_ord.rs: NaN == NaN and

@@ -125,6 +125,10 @@ SIGNATURES = {
     "plgpu_join_inner_multi": (C.c_int, [_COLP, _COLP, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _COLP, _COLP,
                                          _P]),
     "plgpu_join_inner": (C.c_int, [_COLP, _COLP, C.c_int32, C.c_int32, C.c_int32, _COLP, _COLP, _P]),
+    "plgpu_join": (C.c_int, [_COLP, _COLP, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _COLP, _COLP, _P]),
+    "plgpu_join_multi": (C.c_int, [_COLP, _COLP, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _COLP,
+                                   _COLP, _P]),
+    "plgpu_coalesce": (C.c_int, [_COLP, _COLP, _COLP, _P]),
     "plgpu_gather": (C.c_int, [_COLP, C.c_int32, _COLP, _COLP, _P]),
     "plgpu_hash_partition": (C.c_int, [_COLP, C.c_int32, C.c_int32, C.c_int32, _COLP, C.POINTER(C.c_int64), _P]),
     "plgpu_gather_rows": (C.c_int, [_COLP, C.c_int32, _COLP, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), _P]),
@@ -137,6 +141,7 @@ SIGNATURES = {
 GB_MAX_ACC = 6
 JOIN_ORDER = {None: 0, "none": 0, "left": 1, "right": 2, "left_right": 3, "right_left": 4}
 JOIN_VALIDATE = {"m:m": 0, "1:m": 1, "m:1": 2, "1:1": 3}
+JOIN_HOW = {"inner": 0, "left": 1, "right": 2, "full": 3, "semi": 4, "anti": 5}
 ROLLING = {"sum": 1, "mean": 2}
 
 _lib = None

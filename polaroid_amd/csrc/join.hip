@@ -207,15 +207,28 @@ __global__ __launch_bounds__(256) void jn_sort_long_kernel(JnTable t, const uint
 }
 
 // ---------------------------------------------------------------- probe
+// Probe modes (one per join type; DESIGN.md §Join types):
+//   JM_INNER  matching pairs only (hash_join_tuples_inner);
+//   JM_OUTER  matching pairs, and (row, null) for a row without a match
+//             (hash_join_tuples_left, probe_outer's no-match arm);
+//   JM_SEMI   the rows with a match, once each (hash_join_tuples_left_semi);
+//   JM_ANTI   the rows without a match (hash_join_tuples_left_anti);
+//   JM_DRAIN  the build side's own rows whose slot was never marked by a
+//             probe (probe_outer's drain of untracked build rows).
+// MARK: a matched probe row sets flags[slot] (full joins and right-ordered
+// left joins drain the unmarked build rows afterwards).
+constexpr int JM_INNER = 0, JM_OUTER = 1, JM_SEMI = 2, JM_ANTI = 3, JM_DRAIN = 4;
+constexpr uint32_t kNullIdx = 0xFFFFFFFFu;  // null index in an output pair
+
 // Pass A: one lookup per probe row -> match word m[r] (the build row, or
 // kRefList | slot for a duplicate key, or kRefNone) and per-tile output
 // counts.  The probe keys are streamed with non-temporal loads so they do
 // not evict the table from the Infinity Cache.
-template <bool NULLABLE>
+template <bool NULLABLE, int MODE, bool MARK>
 __global__ __launch_bounds__(kJnThreads) void jn_probe_match_kernel(DevCol pk, int64_t np, JnTable t,
                                                                     bool nulls_equal, uint32_t* __restrict__ m,
                                                                     uint64_t* __restrict__ tile_counts,
-                                                                    int64_t ntiles) {
+                                                                    int64_t ntiles, uint8_t* __restrict__ flags) {
     __shared__ uint64_t wsum[kJnThreads / 64];
     const uint64_t* kp = (const uint64_t*)pk.values + pk.offset;
     const bool wide = pk.dtype == PLGPU_I64;
@@ -270,19 +283,31 @@ __global__ __launch_bounds__(kJnThreads) void jn_probe_match_kernel(DevCol pk, i
         }
         uint32_t ref[R];
 #pragma unroll
-        for (int k = 0; k < R; ++k) ref[k] = slot[k] >= 0 ? t.ref[slot[k]] : kRefNone;
+        for (int k = 0; k < R; ++k) {
+            if (MODE == JM_DRAIN) ref[k] = (slot[k] >= 0 && flags[slot[k]]) ? 0u : kRefNone;
+            else ref[k] = slot[k] >= 0 ? t.ref[slot[k]] : kRefNone;
+        }
         uint64_t c = 0;
 #pragma unroll
         for (int k = 0; k < R; ++k) {
             const int64_t r = tile * kJnTileRows + (int64_t)k * kJnThreads + threadIdx.x;
             if (r >= np) continue;
+            const bool hit = ref[k] != kRefNone;
             uint32_t w = kRefNone;
-            if (ref[k] == kRefList) {
-                w = kRefList | (uint32_t)slot[k];
-                c += t.off[slot[k] + 1] - t.off[slot[k]];
-            } else if (ref[k] != kRefNone) {
-                w = ref[k];
-                c += 1;
+            if (MODE == JM_SEMI || MODE == JM_ANTI || MODE == JM_DRAIN) {
+                w = hit ? 0u : kRefNone;
+                c += (MODE == JM_SEMI) == hit ? 1 : 0;
+            } else {
+                if (ref[k] == kRefList) {
+                    w = kRefList | (uint32_t)slot[k];
+                    c += t.off[slot[k] + 1] - t.off[slot[k]];
+                } else if (hit) {
+                    w = ref[k];
+                    c += 1;
+                } else if (MODE == JM_OUTER) {
+                    c += 1;
+                }
+                if (MARK && hit) flags[slot[k]] = 1;
             }
             __builtin_nontemporal_store(w, m + r);
         }
@@ -294,7 +319,11 @@ __global__ __launch_bounds__(kJnThreads) void jn_probe_match_kernel(DevCol pk, i
 
 // Pass B: pairs in probe-row order.  Row r = base + k*T + tid of a tile is
 // ranked k*T + tid; one block scan per k.
-// `rowmap` (partitioned probe): position r holds probe row rowmap[r].
+// `rowmap` (partitioned probe, semi/anti selection): position r holds probe
+// row rowmap[r].
+// JM_OUTER writes kNullIdx as the build row of an unmatched probe row;
+// JM_SEMI / JM_ANTI / JM_DRAIN write probe rows only (out_b unused).
+template <int MODE>
 __global__ __launch_bounds__(kJnThreads) void jn_probe_emit_kernel(int64_t np, JnTable t,
                                                                    const uint32_t* __restrict__ m,
                                                                    const uint64_t* __restrict__ tile_off,
@@ -315,7 +344,11 @@ __global__ __launch_bounds__(kJnThreads) void jn_probe_emit_kernel(int64_t np, J
         for (int k = 0; k < R; ++k) {
             const int64_t r = tile * kJnTileRows + (int64_t)k * kJnThreads + threadIdx.x;
             uint32_t c = 0, lo = 0;
-            if (w[k] != kRefNone) {
+            if (MODE == JM_SEMI) {
+                c = w[k] != kRefNone ? 1u : 0u;
+            } else if (MODE == JM_ANTI || MODE == JM_DRAIN) {
+                c = (r < np && w[k] == kRefNone) ? 1u : 0u;
+            } else if (w[k] != kRefNone) {
                 if (w[k] & kRefList) {
                     const uint32_t slot = w[k] & ~kRefList;
                     lo = t.off[slot];
@@ -323,11 +356,18 @@ __global__ __launch_bounds__(kJnThreads) void jn_probe_emit_kernel(int64_t np, J
                 } else {
                     c = 1;
                 }
+            } else if (MODE == JM_OUTER && r < np) {
+                c = 1;
             }
             uint64_t total;
             const uint64_t pos = run + block_excl_scan(c, wsum, total);
             const uint32_t pr = c ? (rowmap ? rowmap[r] : (uint32_t)r) : 0u;
-            if (c == 1 && !(w[k] & kRefList)) {
+            if (MODE == JM_SEMI || MODE == JM_ANTI || MODE == JM_DRAIN) {
+                if (c) out_p[pos] = pr;
+            } else if (MODE == JM_OUTER && c == 1 && w[k] == kRefNone) {
+                out_p[pos] = pr;
+                out_b[pos] = kNullIdx;
+            } else if (c == 1 && !(w[k] & kRefList)) {
                 out_p[pos] = pr;
                 out_b[pos] = w[k];
             } else {
@@ -621,26 +661,35 @@ static int num_cus_jn() {
 }
 
 // --------------------------------------------------------------- gather
+// `iv` (optional): validity of the index column (Arrow bits from `ioff`); a
+// null index gathers a null (IdxCa::with_nullable_idx + take in the
+// reference's left / full join materialisation).
+__device__ __forceinline__ bool idx_null(const uint8_t* iv, int64_t ioff, int64_t o) {
+    return iv != nullptr && !((iv[(ioff + o) >> 3] >> ((ioff + o) & 7)) & 1);
+}
+
 template <int EB>  // element bytes 4 / 8
 __global__ __launch_bounds__(256) void gather_col_kernel(DevCol c, const uint32_t* __restrict__ idx, int64_t n,
-                                                         void* __restrict__ out, uint64_t* __restrict__ out_valid) {
+                                                         void* __restrict__ out, uint64_t* __restrict__ out_valid,
+                                                         const uint8_t* __restrict__ iv, int64_t ioff) {
     // 4 outputs per thread (strided by the block), loads issued together
     constexpr int K = 4;
     const int64_t step = (int64_t)gridDim.x * blockDim.x * K;
     for (int64_t base = (int64_t)blockIdx.x * blockDim.x * K; base < n; base += step) {
         uint32_t r[K];
+        bool in[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const int64_t o = base + (int64_t)k * blockDim.x + threadIdx.x;
             r[k] = o < n ? __builtin_nontemporal_load(idx + o) : 0u;
+            in[k] = o < n && !idx_null(iv, ioff, o);
         }
         uint64_t v[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            const int64_t o = base + (int64_t)k * blockDim.x + threadIdx.x;
             const int64_t p = c.offset + r[k];
             v[k] = 0;
-            if (o < n) v[k] = EB == 8 ? ((const uint64_t*)c.values)[p] : ((const uint32_t*)c.values)[p];
+            if (in[k]) v[k] = EB == 8 ? ((const uint64_t*)c.values)[p] : ((const uint32_t*)c.values)[p];
         }
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -651,7 +700,7 @@ __global__ __launch_bounds__(256) void gather_col_kernel(DevCol c, const uint32_
             }
             if (out_valid) {
                 // one validity word per wave and k (o of lane 0 is a multiple of 64)
-                const uint64_t w = __ballot(o < n && dev_valid(c, r[k]));
+                const uint64_t w = __ballot(in[k] && dev_valid(c, r[k]));
                 if ((threadIdx.x & 63) == 0 && o < n) out_valid[o >> 6] = w;
             }
         }
@@ -659,11 +708,12 @@ __global__ __launch_bounds__(256) void gather_col_kernel(DevCol c, const uint32_
 }
 
 __global__ void gather_bool_kernel(DevCol c, const uint32_t* __restrict__ idx, int64_t n,
-                                   uint64_t* __restrict__ out, uint64_t* __restrict__ out_valid) {
+                                   uint64_t* __restrict__ out, uint64_t* __restrict__ out_valid,
+                                   const uint8_t* __restrict__ iv, int64_t ioff) {
     for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < n; base += (int64_t)gridDim.x * blockDim.x) {
         const int64_t o = base + threadIdx.x;
         bool v = false, valid = false;
-        if (o < n) {
+        if (o < n && !idx_null(iv, ioff, o)) {
             const int64_t r = idx[o];
             v = dev_load(c, r) & 1;
             valid = dev_valid(c, r);
@@ -741,8 +791,9 @@ static hipError_t aos_dispatch(int nc, const AosCols& c, int64_t rows, const uin
     }
 }
 
-static int gather_into(const plgpu_column& src, const uint32_t* idx, int64_t n, plgpu_column* out, hipStream_t s) {
-    const bool nullable = src.validity != nullptr;
+static int gather_into(const plgpu_column& src, const uint32_t* idx, int64_t n, plgpu_column* out, hipStream_t s,
+                       const uint8_t* iv = nullptr, int64_t ioff = 0) {
+    const bool nullable = src.validity != nullptr || iv != nullptr;
     int rc = make_owned_column(out, src.dtype, n, nullable, s);
     if (rc) return rc;
     if (n == 0) return PLGPU_OK;
@@ -755,11 +806,11 @@ static int gather_into(const plgpu_column& src, const uint32_t* idx, int64_t n, 
     const int g = (int)std::min<int64_t>((n + 1023) / 1024, (int64_t)num_cus_jn() * 16);
     uint64_t* ov = (uint64_t*)out->validity;
     if (src.dtype == PLGPU_BOOL)
-        gather_bool_kernel<<<g, 256, 0, s>>>(c, idx, n, (uint64_t*)out->values, ov);
+        gather_bool_kernel<<<g, 256, 0, s>>>(c, idx, n, (uint64_t*)out->values, ov, iv, ioff);
     else if (dtype_bytes(src.dtype) == 8)
-        gather_col_kernel<8><<<g, 256, 0, s>>>(c, idx, n, (void*)out->values, ov);
+        gather_col_kernel<8><<<g, 256, 0, s>>>(c, idx, n, (void*)out->values, ov, iv, ioff);
     else
-        gather_col_kernel<4><<<g, 256, 0, s>>>(c, idx, n, (void*)out->values, ov);
+        gather_col_kernel<4><<<g, 256, 0, s>>>(c, idx, n, (void*)out->values, ov, iv, ioff);
     PLGPU_HIP(hipGetLastError());
     out->null_count = nullable ? -1 : 0;
     return PLGPU_OK;
@@ -907,50 +958,147 @@ static int jn_build(const plgpu_column* key, bool nulls_equal, bool ordered, JnB
     return PLGPU_OK;
 }
 
-// Probe with `key`; pairs (probe row, build row) in probe-row order.
-static int jn_probe(const plgpu_column* key, const JnBuilt& b, bool nulls_equal, plgpu_column* out_p,
-                    plgpu_column* out_b, hipStream_t s) {
-    const int64_t np = key->length;
-    const DevCol pk = as_dev(key);
-    const int64_t ntiles = std::max<int64_t>(1, (np + kJnTileRows - 1) / kJnTileRows);
+// One probe pass: per-row match words, per-tile output counts and their
+// exclusive scan; `total` output rows.
+struct JnPass {
+    uint32_t* m = nullptr;
     uint64_t* tcount = nullptr;
     uint64_t* toff = nullptr;
     uint64_t* part = nullptr;
-    uint32_t* m = nullptr;
-    int rc = dev_alloc((void**)&tcount, ntiles * 8, s);
-    if (!rc) rc = dev_alloc((void**)&toff, (ntiles + 1) * 8, s);
-    if (!rc) rc = dev_alloc((void**)&part, ((ntiles + kScanChunk - 1) / kScanChunk + 1) * 8, s);
-    if (!rc) rc = dev_alloc((void**)&m, std::max<int64_t>(np, 1) * 4, s);
+    int64_t np = 0;
+    int64_t ntiles = 0;
     uint64_t total = 0;
-    const int g = (int)std::min<int64_t>(ntiles, (int64_t)num_cus_jn() * 8);
-    if (!rc) {
-        if (pk.validity) jn_probe_match_kernel<true><<<g, kJnThreads, 0, s>>>(pk, np, b.t, nulls_equal, m, tcount, ntiles);
-        else jn_probe_match_kernel<false><<<g, kJnThreads, 0, s>>>(pk, np, b.t, nulls_equal, m, tcount, ntiles);
-        hipError_t e = hipGetLastError();
-        if (e == hipSuccess) e = scan_exclusive<uint64_t>(tcount, ntiles, toff, part, s);
-        if (e == hipSuccess) e = hipMemcpyAsync(&total, toff + ntiles, 8, hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
-        if (e != hipSuccess) rc = hip_fail(e, "join probe match");
-    }
-    if (!rc && total >= 0xFFFFFFFFull) rc = fail(PLGPU_ERR_CAPACITY, "join output exceeds the u32 index space");
-    if (!rc) rc = make_owned_column(out_p, PLGPU_U32, (int64_t)total, false, s);
-    if (!rc) rc = make_owned_column(out_b, PLGPU_U32, (int64_t)total, false, s);
-    if (!rc && total > 0) {
-        jn_probe_emit_kernel<<<g, kJnThreads, 0, s>>>(np, b.t, m, toff, ntiles, (uint32_t*)out_p->values,
-                                                      (uint32_t*)out_b->values, nullptr);
-        hipError_t e = hipGetLastError();
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
-        if (e != hipSuccess) rc = hip_fail(e, "join probe emit");
-    }
-    dev_free(tcount, s);
-    dev_free(toff, s);
-    dev_free(part, s);
-    dev_free(m, s);
-    if (rc) {
-        plgpu_column_release(out_p);
-        plgpu_column_release(out_b);
-    }
+};
+
+static void jn_pass_free(JnPass& p, hipStream_t s) {
+    dev_free(p.m, s);
+    dev_free(p.tcount, s);
+    dev_free(p.toff, s);
+    dev_free(p.part, s);
+    p = JnPass();
+}
+
+static int jn_pass_alloc(int64_t np, JnPass* p, hipStream_t s) {
+    p->np = np;
+    p->ntiles = std::max<int64_t>(1, (np + kJnTileRows - 1) / kJnTileRows);
+    int rc = dev_alloc((void**)&p->tcount, p->ntiles * 8, s);
+    if (!rc) rc = dev_alloc((void**)&p->toff, (p->ntiles + 1) * 8, s);
+    if (!rc) rc = dev_alloc((void**)&p->part, ((p->ntiles + kScanChunk - 1) / kScanChunk + 1) * 8, s);
+    if (!rc) rc = dev_alloc((void**)&p->m, std::max<int64_t>(np, 1) * 4, s);
     return rc;
+}
+
+static int jn_pass_grid(const JnPass& p) { return (int)std::min<int64_t>(p.ntiles, (int64_t)num_cus_jn() * 8); }
+
+// Scan of the tile counts -> p->total (host).
+static int jn_pass_scan(JnPass* p, hipStream_t s, const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = scan_exclusive<uint64_t>(p->tcount, p->ntiles, p->toff, p->part, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(&p->total, p->toff + p->ntiles, 8, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    return e == hipSuccess ? PLGPU_OK : hip_fail(e, what);
+}
+
+template <int MODE, bool MARK>
+static void jn_launch_match(const DevCol& pk, const JnPass& p, const JnBuilt& b, bool neq, uint8_t* flags,
+                            hipStream_t s) {
+    const int g = jn_pass_grid(p);
+    if (pk.validity)
+        jn_probe_match_kernel<true, MODE, MARK><<<g, kJnThreads, 0, s>>>(pk, p.np, b.t, neq, p.m, p.tcount, p.ntiles,
+                                                                         flags);
+    else
+        jn_probe_match_kernel<false, MODE, MARK><<<g, kJnThreads, 0, s>>>(pk, p.np, b.t, neq, p.m, p.tcount, p.ntiles,
+                                                                          flags);
+}
+
+// Match pass of `key` against the table in `mode` (MARK: set flags[slot] of
+// every matched slot; JM_DRAIN reads them).
+static int jn_match(const plgpu_column* key, const JnBuilt& b, bool neq, int mode, bool mark, uint8_t* flags,
+                    JnPass* p, hipStream_t s) {
+    int rc = jn_pass_alloc(key->length, p, s);
+    if (rc) return rc;
+    const DevCol pk = as_dev(key);
+    switch (mode) {
+    case JM_INNER:
+        if (mark) jn_launch_match<JM_INNER, true>(pk, *p, b, neq, flags, s);
+        else jn_launch_match<JM_INNER, false>(pk, *p, b, neq, flags, s);
+        break;
+    case JM_OUTER:
+        if (mark) jn_launch_match<JM_OUTER, true>(pk, *p, b, neq, flags, s);
+        else jn_launch_match<JM_OUTER, false>(pk, *p, b, neq, flags, s);
+        break;
+    case JM_SEMI: jn_launch_match<JM_SEMI, false>(pk, *p, b, neq, flags, s); break;
+    case JM_ANTI: jn_launch_match<JM_ANTI, false>(pk, *p, b, neq, flags, s); break;
+    default: jn_launch_match<JM_DRAIN, false>(pk, *p, b, neq, flags, s); break;
+    }
+    return jn_pass_scan(p, s, "join probe match");
+}
+
+// Emit pass: rows / pairs of `p` in probe-row order into out_p / out_b.
+static int jn_emit(const JnPass& p, const JnBuilt& b, int mode, uint32_t* out_p, uint32_t* out_b,
+                   const uint32_t* rowmap, hipStream_t s) {
+    if (p.total == 0) return PLGPU_OK;
+    const int g = jn_pass_grid(p);
+    switch (mode) {
+    case JM_INNER:
+        jn_probe_emit_kernel<JM_INNER><<<g, kJnThreads, 0, s>>>(p.np, b.t, p.m, p.toff, p.ntiles, out_p, out_b, rowmap);
+        break;
+    case JM_OUTER:
+        jn_probe_emit_kernel<JM_OUTER><<<g, kJnThreads, 0, s>>>(p.np, b.t, p.m, p.toff, p.ntiles, out_p, out_b, rowmap);
+        break;
+    case JM_SEMI:
+        jn_probe_emit_kernel<JM_SEMI><<<g, kJnThreads, 0, s>>>(p.np, b.t, p.m, p.toff, p.ntiles, out_p, out_b, rowmap);
+        break;
+    default:
+        jn_probe_emit_kernel<JM_ANTI><<<g, kJnThreads, 0, s>>>(p.np, b.t, p.m, p.toff, p.ntiles, out_p, out_b, rowmap);
+        break;
+    }
+    PLGPU_HIP(hipGetLastError());
+    return PLGPU_OK;
+}
+
+// Validity bits of an index column: kNullIdx entries are null.
+__global__ __launch_bounds__(256) void jn_idx_validity_kernel(const uint32_t* __restrict__ v, int64_t n,
+                                                              uint64_t* __restrict__ words) {
+    for (int64_t r0 = (int64_t)blockIdx.x * blockDim.x; r0 < n; r0 += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = r0 + threadIdx.x;
+        const uint64_t w = __ballot(r < n && v[r] != kNullIdx);
+        if ((threadIdx.x & 63) == 0 && r < n) words[r >> 6] = w;
+    }
+}
+
+static int jn_idx_validity(plgpu_column* c, hipStream_t s) {
+    if (c->validity == nullptr || c->length == 0) return PLGPU_OK;
+    const int g = (int)std::min<int64_t>((c->length + 255) / 256, (int64_t)num_cus_jn() * 16);
+    jn_idx_validity_kernel<<<g, 256, 0, s>>>((const uint32_t*)c->values, c->length, (uint64_t*)c->validity);
+    PLGPU_HIP(hipGetLastError());
+    return PLGPU_OK;
+}
+
+// Semi / anti rows out of verified left-join pairs (a ascending, b =
+// kNullIdx for a row without a match): semi keeps the first pair of every
+// matched left row, anti the unmatched rows.  A kept pair gets the JM_ANTI
+// emit mark (kRefNone); the emit writes a[i] through its row map.
+__global__ __launch_bounds__(kJnThreads) void jn_select_kernel(const uint32_t* __restrict__ a,
+                                                               const uint32_t* __restrict__ b, int64_t n, bool semi,
+                                                               uint32_t* __restrict__ m,
+                                                               uint64_t* __restrict__ tile_counts, int64_t ntiles) {
+    __shared__ uint64_t wsum[kJnThreads / 64];
+    constexpr int R = kJnTileRows / kJnThreads;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        uint64_t c = 0;
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const int64_t r = tile * kJnTileRows + (int64_t)k * kJnThreads + threadIdx.x;
+            if (r >= n) continue;
+            const bool keep = semi ? (b[r] != kNullIdx && (r == 0 || a[r - 1] != a[r])) : b[r] == kNullIdx;
+            m[r] = keep ? kRefNone : 0u;
+            c += keep ? 1 : 0;
+        }
+        uint64_t total;
+        (void)block_excl_scan(c, wsum, total);
+        if (threadIdx.x == 0) tile_counts[tile] = total;
+    }
 }
 
 
@@ -1064,8 +1212,8 @@ static int jn_probe_partitioned(const plgpu_column* key, const JnBuilt& b, bool 
     if (!rc) rc = make_owned_column(out_b, PLGPU_U32, (int64_t)total, false, s);
     if (!rc && total > 0) {
         const int g = (int)std::min<int64_t>(ntiles, (int64_t)cus * 8);
-        jn_probe_emit_kernel<<<g, kJnThreads, 0, s>>>(n, b.t, m, toff, ntiles, (uint32_t*)out_p->values,
-                                                      (uint32_t*)out_b->values, prow);
+        jn_probe_emit_kernel<JM_INNER><<<g, kJnThreads, 0, s>>>(n, b.t, m, toff, ntiles, (uint32_t*)out_p->values,
+                                                                (uint32_t*)out_b->values, prow);
         e = hipGetLastError();
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (e != hipSuccess) rc = hip_fail(e, "partitioned join: emit");
@@ -1099,24 +1247,67 @@ static int check_key(const plgpu_column* k) {
     return PLGPU_OK;
 }
 
-// Inner join of two checked key columns (validation failures return
-// PLGPU_ERR_SCHEMA; nothing else does).
-static int join_inner_impl(const plgpu_column* left_key, const plgpu_column* right_key, bool neq,
-                           int32_t maintain_order, int32_t validate, plgpu_column* out_left_idx,
-                           plgpu_column* out_right_idx, hipStream_t s) {
+// Join of two checked key columns (validation failures return
+// PLGPU_ERR_SCHEMA; nothing else does).  How each join type maps onto a
+// build side, probe mode and drain (DESIGN.md §Join types):
+//   inner  probe the side whose order is kept (else build the shorter side);
+//   left   build right, probe left with JM_OUTER -- left order, matches in
+//          right-row order, as hash_join_tuples_left; with a right-first
+//          order, build left, probe right (JM_INNER, marking) and drain the
+//          unmatched left rows, which is what the reference's stable sort by
+//          the right index (dispatch_left_right.rs:143) yields;
+//   right  the left join with the sides swapped and the order flipped
+//          (dispatch_left_right.rs:19);
+//   full   probe with JM_OUTER + marks, then drain the unmarked build rows
+//          (probe_outer); the build side follows maintain_order so that the
+//          pairs come out already in the reference's sorted order
+//          (hash_join/mod.rs:164), else the shorter side as
+//          det_hash_prone_order;
+//   semi / anti  build right, probe left (hash_join_tuples_left_semi/_anti).
+static int join_impl(const plgpu_column* left_key, const plgpu_column* right_key, int32_t how, bool neq,
+                     int32_t maintain_order, int32_t validate, plgpu_column* out_left_idx,
+                     plgpu_column* out_right_idx, hipStream_t s) {
     int rc;
     std::memset(out_left_idx, 0, sizeof *out_left_idx);
     std::memset(out_right_idx, 0, sizeof *out_right_idx);
-    // the probe order decides the output order: probe the side whose order
-    // must be kept; otherwise build on the shorter side as the reference does
-    bool build_right;
-    if (maintain_order == PLGPU_JOIN_ORDER_LEFT || maintain_order == PLGPU_JOIN_ORDER_LEFT_RIGHT)
+    if (how == PLGPU_JOIN_RIGHT) {
+        static const int32_t flip[5] = {PLGPU_JOIN_ORDER_NONE, PLGPU_JOIN_ORDER_RIGHT, PLGPU_JOIN_ORDER_LEFT,
+                                        PLGPU_JOIN_ORDER_RIGHT_LEFT, PLGPU_JOIN_ORDER_LEFT_RIGHT};
+        return join_impl(right_key, left_key, PLGPU_JOIN_LEFT, neq, flip[maintain_order], validate, out_right_idx,
+                         out_left_idx, s);
+    }
+    const bool order_left = maintain_order == PLGPU_JOIN_ORDER_LEFT || maintain_order == PLGPU_JOIN_ORDER_LEFT_RIGHT;
+    const bool order_right =
+        maintain_order == PLGPU_JOIN_ORDER_RIGHT || maintain_order == PLGPU_JOIN_ORDER_RIGHT_LEFT;
+    bool build_right, ordered = maintain_order != PLGPU_JOIN_ORDER_NONE, drain = false;
+    int mode;
+    switch (how) {
+    case PLGPU_JOIN_LEFT:
+        build_right = !order_right;
+        mode = order_right ? JM_INNER : JM_OUTER;
+        drain = order_right;
+        ordered = true;  // the reference's left join is ordered in every mode
+        break;
+    case PLGPU_JOIN_FULL:
+        build_right = order_left || (!order_right && right_key->length <= left_key->length);
+        mode = JM_OUTER;
+        drain = true;
+        break;
+    case PLGPU_JOIN_SEMI:
+    case PLGPU_JOIN_ANTI:
         build_right = true;
-    else if (maintain_order == PLGPU_JOIN_ORDER_RIGHT || maintain_order == PLGPU_JOIN_ORDER_RIGHT_LEFT)
-        build_right = false;
-    else
-        build_right = right_key->length <= left_key->length;
-    const bool ordered = maintain_order != PLGPU_JOIN_ORDER_NONE;
+        mode = how == PLGPU_JOIN_SEMI ? JM_SEMI : JM_ANTI;
+        ordered = false;
+        validate = PLGPU_JOIN_VALIDATE_M_M;  // semi / anti joins do not validate
+        break;
+    default:
+        // the probe order decides the output order: probe the side whose
+        // order must be kept; otherwise build on the shorter side as the
+        // reference does
+        build_right = order_left || (!order_right && right_key->length <= left_key->length);
+        mode = JM_INNER;
+        break;
+    }
     JnBuilt b;
     rc = jn_build(build_right ? right_key : left_key, neq, ordered, &b, s);
     if (rc) return rc;
@@ -1144,16 +1335,81 @@ static int join_inner_impl(const plgpu_column* left_key, const plgpu_column* rig
     if (!rc && !ok)
         rc = fail(PLGPU_ERR_SCHEMA, validate == PLGPU_JOIN_VALIDATE_1_1 ? "join keys did not fulfill 1:1 validation"
                                                                         : "join keys did not fulfill m:1 validation");
-    if (!rc) {
-        const plgpu_column* pkey = build_right ? left_key : right_key;
-        plgpu_column* op = build_right ? out_left_idx : out_right_idx;
-        plgpu_column* ob = build_right ? out_right_idx : out_left_idx;
-        bool used = false;
-        if (!ordered) rc = jn_probe_partitioned(pkey, b, neq, op, ob, &used, s);
-        if (!rc && !used) rc = jn_probe(pkey, b, neq, op, ob, s);
+    if (rc) {
+        jn_free(b, s);
+        return rc;
     }
+    const plgpu_column* pkey = build_right ? left_key : right_key;
+    const plgpu_column* bkey = build_right ? right_key : left_key;
+    plgpu_column* op = build_right ? out_left_idx : out_right_idx;
+    plgpu_column* ob = build_right ? out_right_idx : out_left_idx;
+    bool used = false;
+    if (mode == JM_INNER && !ordered && !drain) rc = jn_probe_partitioned(pkey, b, neq, op, ob, &used, s);
+    if (rc || used) {
+        jn_free(b, s);
+        (void)hipStreamSynchronize(s);
+        return rc;
+    }
+    uint8_t* flags = nullptr;
+    JnPass pp, dp;
+    if (drain) {
+        rc = dev_alloc((void**)&flags, b.t.cap + 2, s);
+        if (!rc && hipMemsetAsync(flags, 0, b.t.cap + 2, s) != hipSuccess) rc = fail(PLGPU_ERR_HIP, "join flags");
+    }
+    if (!rc) rc = jn_match(pkey, b, neq, mode, drain, flags, &pp, s);
+    if (!rc && drain) rc = jn_match(bkey, b, neq, JM_DRAIN, false, flags, &dp, s);
+    const uint64_t total = pp.total + dp.total;
+    const bool rows_only = mode == JM_SEMI || mode == JM_ANTI;
+    if (!rc && total >= 0xFFFFFFFFull) rc = fail(PLGPU_ERR_CAPACITY, "join output exceeds the u32 index space");
+    // null partners: the probe side's in drained rows, the build side's for
+    // unmatched probe rows (JM_OUTER)
+    if (!rc) rc = make_owned_column(op, PLGPU_U32, (int64_t)total, drain, s);
+    if (!rc) rc = make_owned_column(ob, PLGPU_U32, rows_only ? 0 : (int64_t)total, mode == JM_OUTER, s);
+    if (!rc) rc = jn_emit(pp, b, mode, (uint32_t*)op->values, (uint32_t*)ob->values, nullptr, s);
+    if (!rc && drain && dp.total > 0) {
+        // drained build rows, each with a null probe-side partner
+        rc = jn_emit(dp, b, JM_DRAIN, (uint32_t*)ob->values + pp.total, nullptr, nullptr, s);
+        if (!rc && hipMemsetAsync((uint32_t*)op->values + pp.total, 0xFF, dp.total * 4, s) != hipSuccess)
+            rc = fail(PLGPU_ERR_HIP, "join drain fill");
+    }
+    if (!rc) rc = jn_idx_validity(op, s);
+    if (!rc) rc = jn_idx_validity(ob, s);
+    if (!rc) {
+        hipError_t e = hipStreamSynchronize(s);
+        if (e != hipSuccess) rc = hip_fail(e, "join emit");
+    }
+    jn_pass_free(pp, s);
+    jn_pass_free(dp, s);
+    dev_free(flags, s);
     jn_free(b, s);
+    if (rc) {
+        plgpu_column_release(out_left_idx);
+        plgpu_column_release(out_right_idx);
+    }
     (void)hipStreamSynchronize(s);
+    return rc;
+}
+
+// Semi / anti rows from verified left-join pairs (multi-key hashed path).
+static int jn_select_rows(const plgpu_column& li, const plgpu_column& ri, bool semi, plgpu_column* out,
+                          hipStream_t s) {
+    std::memset(out, 0, sizeof *out);
+    JnPass p;
+    int rc = jn_pass_alloc(li.length, &p, s);
+    if (!rc) {
+        jn_select_kernel<<<jn_pass_grid(p), kJnThreads, 0, s>>>((const uint32_t*)li.values, (const uint32_t*)ri.values,
+                                                                p.np, semi, p.m, p.tcount, p.ntiles);
+        rc = jn_pass_scan(&p, s, "join semi/anti select");
+    }
+    JnBuilt none;
+    if (!rc) rc = make_owned_column(out, PLGPU_U32, (int64_t)p.total, false, s);
+    if (!rc) rc = jn_emit(p, none, JM_ANTI, (uint32_t*)out->values, nullptr, (const uint32_t*)li.values, s);
+    if (!rc) {
+        hipError_t e = hipStreamSynchronize(s);
+        if (e != hipSuccess) rc = hip_fail(e, "join semi/anti select");
+    }
+    jn_pass_free(p, s);
+    if (rc) plgpu_column_release(out);
     return rc;
 }
 
@@ -1181,31 +1437,55 @@ __global__ __launch_bounds__(256) void jn_verify_kernel(MkKeys a, MkKeys b, cons
                                                         uint32_t* __restrict__ bad) {
     bool x = false;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        x |= !mk_equal(a, ia[i], b, ib[i]);
+        if (ia[i] != kNullIdx && ib[i] != kNullIdx) x |= !mk_equal(a, ia[i], b, ib[i]);
     if (__any(x) && (threadIdx.x & 63) == 0) atomicOr(bad, 1u);
+}
+
+static int check_args(int32_t how, int32_t maintain_order, int32_t validate) {
+    if (how < PLGPU_JOIN_INNER || how > PLGPU_JOIN_ANTI) return fail(PLGPU_ERR_INVALID, "invalid join type");
+    if (maintain_order < PLGPU_JOIN_ORDER_NONE || maintain_order > PLGPU_JOIN_ORDER_RIGHT_LEFT)
+        return fail(PLGPU_ERR_INVALID, "invalid maintain_order");
+    if (validate < PLGPU_JOIN_VALIDATE_M_M || validate > PLGPU_JOIN_VALIDATE_1_1)
+        return fail(PLGPU_ERR_INVALID, "invalid validate");
+    return PLGPU_OK;
+}
+
+PLGPU_API int plgpu_join(const plgpu_column* left_key, const plgpu_column* right_key, int32_t how, int32_t nulls_equal,
+                         int32_t maintain_order, int32_t validate, plgpu_column* out_left_idx,
+                         plgpu_column* out_right_idx, void* stream) {
+    int rc;
+    if ((rc = check_key(left_key)) || (rc = check_key(right_key))) return rc;
+    if (out_left_idx == nullptr || out_right_idx == nullptr) return fail(PLGPU_ERR_INVALID, "NULL output");
+    if ((rc = check_args(how, maintain_order, validate))) return rc;
+    return join_impl(left_key, right_key, how, nulls_equal != 0, maintain_order, validate, out_left_idx,
+                     out_right_idx, as_stream(stream));
 }
 
 PLGPU_API int plgpu_join_inner(const plgpu_column* left_key, const plgpu_column* right_key, int32_t nulls_equal,
                                int32_t maintain_order, int32_t validate, plgpu_column* out_left_idx,
                                plgpu_column* out_right_idx, void* stream) {
-    int rc;
-    if ((rc = check_key(left_key)) || (rc = check_key(right_key))) return rc;
-    if (out_left_idx == nullptr || out_right_idx == nullptr) return fail(PLGPU_ERR_INVALID, "NULL output");
-    if (maintain_order < PLGPU_JOIN_ORDER_NONE || maintain_order > PLGPU_JOIN_ORDER_RIGHT_LEFT)
-        return fail(PLGPU_ERR_INVALID, "invalid maintain_order");
-    return join_inner_impl(left_key, right_key, nulls_equal != 0, maintain_order, validate, out_left_idx,
-                           out_right_idx, as_stream(stream));
+    return plgpu_join(left_key, right_key, PLGPU_JOIN_INNER, nulls_equal, maintain_order, validate, out_left_idx,
+                      out_right_idx, stream);
 }
 
 PLGPU_API int plgpu_join_inner_multi(const plgpu_column* left_keys, const plgpu_column* right_keys, int32_t nkeys,
                                      int32_t nulls_equal, int32_t maintain_order, int32_t validate,
                                      plgpu_column* out_left_idx, plgpu_column* out_right_idx, void* stream) {
+    return plgpu_join_multi(left_keys, right_keys, nkeys, PLGPU_JOIN_INNER, nulls_equal, maintain_order, validate,
+                            out_left_idx, out_right_idx, stream);
+}
+
+PLGPU_API int plgpu_join_multi(const plgpu_column* left_keys, const plgpu_column* right_keys, int32_t nkeys,
+                               int32_t how, int32_t nulls_equal, int32_t maintain_order, int32_t validate,
+                               plgpu_column* out_left_idx, plgpu_column* out_right_idx, void* stream) {
     hipStream_t s = as_stream(stream);
     if (left_keys == nullptr || right_keys == nullptr || out_left_idx == nullptr || out_right_idx == nullptr)
         return fail(PLGPU_ERR_INVALID, "NULL argument");
     if (nkeys < 1 || nkeys > kMaxKeys) return fail(PLGPU_ERR_INVALID, "number of join keys must be 1..8");
-    if (maintain_order < PLGPU_JOIN_ORDER_NONE || maintain_order > PLGPU_JOIN_ORDER_RIGHT_LEFT)
-        return fail(PLGPU_ERR_INVALID, "invalid maintain_order");
+    {
+        const int rc = check_args(how, maintain_order, validate);
+        if (rc) return rc;
+    }
     std::memset(out_left_idx, 0, sizeof *out_left_idx);
     std::memset(out_right_idx, 0, sizeof *out_right_idx);
     MkKeys ka, kb;
@@ -1261,7 +1541,7 @@ PLGPU_API int plgpu_join_inner_multi(const plgpu_column* left_keys, const plgpu_
                 a.validity = neq ? nullptr : (const uint8_t*)vl;
                 b.validity = neq ? nullptr : (const uint8_t*)vr;
                 a.null_count = b.null_count = neq ? 0 : -1;
-                rc = join_inner_impl(&a, &b, neq, maintain_order, validate, out_left_idx, out_right_idx, s);
+                rc = join_impl(&a, &b, how, neq, maintain_order, validate, out_left_idx, out_right_idx, s);
             }
             dev_free(cl, s);
             dev_free(cr, s);
@@ -1291,6 +1571,11 @@ PLGPU_API int plgpu_join_inner_multi(const plgpu_column* left_keys, const plgpu_
     cl.null_count = cr.null_count = neq ? 0 : -1;
     bool done = false;
     int validation_fails = 0;
+    // semi / anti on hashed tuples: a left join whose pairs can be verified,
+    // then the semi / anti rows selected from it
+    const bool rows_only = how == PLGPU_JOIN_SEMI || how == PLGPU_JOIN_ANTI;
+    const int32_t how_h = rows_only ? PLGPU_JOIN_LEFT : how;
+    const int32_t order_h = rows_only ? PLGPU_JOIN_ORDER_LEFT : maintain_order;
     for (int attempt = 0; attempt < 4 && !rc && !done; ++attempt) {
         const uint64_t seed = 0x243F6A8885A308D3ull * (uint64_t)(2 * attempt + 1);
         // PLGPU_MK_COLLIDE (tests only): a 3-bit first hash forces collisions
@@ -1306,7 +1591,8 @@ PLGPU_API int plgpu_join_inner_multi(const plgpu_column* left_keys, const plgpu_
             rc = hip_fail(e, "join tuple hash");
             break;
         }
-        rc = join_inner_impl(&cl, &cr, neq, maintain_order, validate, out_left_idx, out_right_idx, s);
+        rc = join_impl(&cl, &cr, how_h, neq, order_h, rows_only ? PLGPU_JOIN_VALIDATE_M_M : validate, out_left_idx,
+                       out_right_idx, s);
         if (rc == PLGPU_ERR_SCHEMA && ++validation_fails < 2) {
             // a duplicate hash may be a collision of distinct tuples: a second
             // seed tells a real duplicate (fails again) from a collision
@@ -1339,6 +1625,17 @@ PLGPU_API int plgpu_join_inner_multi(const plgpu_column* left_keys, const plgpu_
     dev_free(vr, s);
     dev_free(bad, s);
     if (!rc && !done) rc = fail(PLGPU_ERR_CAPACITY, "multi-key join: unresolved 64-bit hash collisions");
+    if (!rc && rows_only) {
+        plgpu_column rows;
+        rc = jn_select_rows(*out_left_idx, *out_right_idx, how == PLGPU_JOIN_SEMI, &rows, s);
+        plgpu_column_release(out_left_idx);
+        plgpu_column_release(out_right_idx);
+        if (!rc) {
+            *out_left_idx = rows;
+            rc = make_owned_column(out_right_idx, PLGPU_U32, 0, false, s);
+            if (rc) plgpu_column_release(out_left_idx);
+        }
+    }
     (void)hipStreamSynchronize(s);
     return rc;
 }
@@ -1349,15 +1646,15 @@ PLGPU_API int plgpu_gather(const plgpu_column* cols, int32_t ncols, const plgpu_
     if (idx == nullptr || (ncols > 0 && (cols == nullptr || out_cols == nullptr)))
         return fail(PLGPU_ERR_INVALID, "NULL argument");
     if (idx->dtype != PLGPU_U32) return fail(PLGPU_ERR_SCHEMA, "gather indices must be UInt32");
-    if (idx->validity != nullptr) return fail(PLGPU_ERR_INVALID, "gather indices must not contain nulls");
     for (int i = 0; i < ncols; ++i) std::memset(&out_cols[i], 0, sizeof(plgpu_column));
     const uint32_t* ix = (const uint32_t*)idx->values + idx->offset;
     const int64_t n = idx->length;
     int rc = PLGPU_OK;
-    // null-free 8-byte columns of one length: row-major packed gather, in
-    // groups of up to kAosMax; everything else column by column
+    // null-free 8-byte columns of one length (and no null indices): row-major
+    // packed gather, in groups of up to kAosMax; everything else column by
+    // column
     std::vector<int> packed;
-    if (n >= (1 << 20) && !getenv("PLGPU_NO_AOS_GATHER")) {
+    if (n >= (1 << 20) && idx->validity == nullptr && !getenv("PLGPU_NO_AOS_GATHER")) {
         for (int i = 0; i < ncols; ++i)
             if (cols[i].validity == nullptr && dtype_bytes(cols[i].dtype) == 8 && cols[i].dtype != PLGPU_BOOL &&
                 cols[i].length == cols[0].length)
@@ -1390,7 +1687,7 @@ PLGPU_API int plgpu_gather(const plgpu_column* cols, int32_t ncols, const plgpu_
         dev_free(aos, s);
     }
     for (int i = 0; i < ncols && rc == PLGPU_OK; ++i)
-        if (!done[i]) rc = gather_into(cols[i], ix, n, &out_cols[i], s);
+        if (!done[i]) rc = gather_into(cols[i], ix, n, &out_cols[i], s, idx->validity, idx->offset);
     if (rc == PLGPU_OK) {
         hipError_t e = hipStreamSynchronize(s);
         if (e != hipSuccess) rc = hip_fail(e, "gather");
@@ -1398,4 +1695,56 @@ PLGPU_API int plgpu_gather(const plgpu_column* cols, int32_t ncols, const plgpu_
     if (rc)
         for (int i = 0; i < ncols; ++i) plgpu_column_release(&out_cols[i]);
     return rc;
+}
+
+// out[i] = a[i] when valid, else b[i] (null when both are null).  Bool
+// columns are written one ballot word per 64 rows.
+__global__ __launch_bounds__(256) void coalesce_kernel(DevCol a, DevCol b, int64_t n, void* __restrict__ out,
+                                                       uint64_t* __restrict__ out_valid) {
+    for (int64_t r0 = (int64_t)blockIdx.x * blockDim.x; r0 < n; r0 += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = r0 + threadIdx.x;
+        const bool in = r < n;
+        const bool va = in && dev_valid(a, r);
+        const bool vb = in && !va && dev_valid(b, r);
+        const uint64_t v = va ? dev_load(a, r) : (vb ? dev_load(b, r) : 0ull);
+        switch (a.dtype) {
+        case PLGPU_I64:
+        case PLGPU_F64:
+            if (in) ((uint64_t*)out)[r] = v;
+            break;
+        case PLGPU_I32:
+        case PLGPU_U32:
+            if (in) ((uint32_t*)out)[r] = (uint32_t)v;
+            break;
+        default: {
+            const uint64_t w = __ballot(in && (v & 1));
+            if ((threadIdx.x & 63) == 0 && in) ((uint64_t*)out)[r >> 6] = w;
+        }
+        }
+        const uint64_t vw = __ballot(va || vb);
+        if ((threadIdx.x & 63) == 0 && in) out_valid[r >> 6] = vw;
+    }
+}
+
+PLGPU_API int plgpu_coalesce(const plgpu_column* a, const plgpu_column* b, plgpu_column* out, void* stream) {
+    hipStream_t s = as_stream(stream);
+    if (a == nullptr || b == nullptr || out == nullptr) return fail(PLGPU_ERR_INVALID, "NULL argument");
+    std::memset(out, 0, sizeof *out);
+    if (a->dtype != b->dtype) return fail(PLGPU_ERR_SCHEMA, "coalesce of columns with different dtypes");
+    if (a->length != b->length) return fail(PLGPU_ERR_SHAPE, "coalesce of columns with different lengths");
+    if (a->dtype != PLGPU_BOOL && dtype_bytes(a->dtype) == 0) return fail(PLGPU_ERR_SCHEMA, "unsupported dtype");
+    const int64_t n = a->length;
+    int rc = make_owned_column(out, a->dtype, n, true, s);
+    if (rc) return rc;
+    if (n > 0) {
+        const int g = (int)std::min<int64_t>((n + 255) / 256, (int64_t)num_cus_jn() * 16);
+        coalesce_kernel<<<g, 256, 0, s>>>(as_dev(a), as_dev(b), n, (void*)out->values, (uint64_t*)out->validity);
+        hipError_t e = hipGetLastError();
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) {
+            plgpu_column_release(out);
+            return hip_fail(e, "coalesce");
+        }
+    }
+    return PLGPU_OK;
 }

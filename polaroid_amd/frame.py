@@ -440,10 +440,11 @@ class DataFrame:
 
     def join(self, other: "DataFrame", on: str | None = None, how: str = "inner", *,
              left_on: str | None = None, right_on: str | None = None, suffix: str = "_right",
-             validate: str = "m:m", nulls_equal: bool = False, maintain_order: str | None = None) -> "DataFrame":
+             validate: str = "m:m", nulls_equal: bool = False, coalesce: bool | None = None,
+             maintain_order: str | None = None) -> "DataFrame":
         """Eager join (py-polars DataFrame.join): runs the lazy plan."""
         return self.lazy().join(other.lazy(), on, how, left_on=left_on, right_on=right_on, suffix=suffix,
-                                validate=validate, nulls_equal=nulls_equal,
+                                validate=validate, nulls_equal=nulls_equal, coalesce=coalesce,
                                 maintain_order=maintain_order).collect()
 
     def group_by(self, *by: Any, maintain_order: bool = False) -> "GroupBy":
@@ -521,9 +522,13 @@ class LazyFrame:
 
     def join(self, other: "LazyFrame", on: str | None = None, how: str = "inner", *,
              left_on: str | None = None, right_on: str | None = None, suffix: str = "_right",
-             validate: str = "m:m", nulls_equal: bool = False, maintain_order: str | None = None) -> "LazyFrame":
-        """Equi-join on one integer key column (py-polars LazyFrame.join;
-        polars-ops/src/frame/join/args.rs:25 JoinArgs)."""
+             validate: str = "m:m", nulls_equal: bool = False, coalesce: bool | None = None,
+             maintain_order: str | None = None) -> "LazyFrame":
+        """Equi-join on 1..8 key columns (py-polars LazyFrame.join;
+        polars-ops/src/frame/join/args.rs:25 JoinArgs): how = inner / left /
+        right / full / semi / anti; `coalesce=None` is the join-specific
+        default (JoinCoalesce::JoinSpecific: every type but full coalesces
+        its key columns)."""
         if on is not None:
             if left_on is not None or right_on is not None:
                 raise ValueError("cannot use 'on' together with 'left_on' / 'right_on'")
@@ -536,14 +541,14 @@ class LazyFrame:
         if nl != nr:
             raise N.InvalidOperationError("the number of columns given as join key (left: %d, right: %d) "
                                           "should be equal" % (nl, nr))
-        if how != "inner":
-            raise N.InvalidOperationError(f"join how={how!r} is not supported on the GPU executor (inner only)")
+        if how not in N.JOIN_HOW:
+            raise N.InvalidOperationError(f"join how={how!r} is not supported on the GPU executor")
         if validate not in N.JOIN_VALIDATE:
             raise ValueError(f"invalid `validate` argument {validate!r}")
         if maintain_order not in N.JOIN_ORDER:
             raise ValueError(f"invalid `maintain_order` argument {maintain_order!r}")
         return LazyFrame(("join", self._node, other._node, left_on, right_on, suffix, validate, bool(nulls_equal),
-                          maintain_order))
+                          maintain_order, how, coalesce))
 
     def select(self, *exprs: Any) -> "LazyFrame":
         return LazyFrame(("select", self._node, _parse_exprs(exprs)))
@@ -820,7 +825,15 @@ def _group_by(df: DataFrame, key: str | tuple, aggs: list[Expr], maintain_order:
 
 
 def _join(left: DataFrame, right: DataFrame, left_on: str | tuple, right_on: str | tuple, suffix: str,
-          validate: str, nulls_equal: bool, maintain_order: str | None) -> DataFrame:
+          validate: str, nulls_equal: bool, maintain_order: str | None, how: str = "inner",
+          coalesce: bool | None = None) -> DataFrame:
+    """Join two frames on the GPU and materialise the result as the reference
+    does: semi / anti keep the left rows (_finish_anti_semi_join); otherwise
+    left columns then right columns, a right name that clashes gets `suffix`
+    (general.rs:17 _finish_join).  Coalescing drops the right key columns
+    (the left ones for a right join, dispatch_left_right.rs:19); a coalesced
+    full join keeps coalesce(left key, right key) in the left key's place
+    (general.rs:52 _coalesce_full_join)."""
     lkeys, rkeys = _gb_keys(left_on), _gb_keys(right_on)
     for df, ks in ((left, lkeys), (right, rkeys)):
         for k in ks:
@@ -832,14 +845,14 @@ def _join(left: DataFrame, right: DataFrame, left_on: str | tuple, right_on: str
             raise N.InvalidOperationError(
                 f"join keys must have the same dtype on the GPU executor (got {lk.dtype} and {rk.dtype})")
     li, ri = N.Column(), N.Column()
-    order, val = N.JOIN_ORDER[maintain_order], N.JOIN_VALIDATE[validate]
+    order, val, hw = N.JOIN_ORDER[maintain_order], N.JOIN_VALIDATE[validate], N.JOIN_HOW[how]
     if builtins.len(lks) == 1 and lks[0].dtype in (Int64, Int32, UInt32):
-        N.check(N.lib().plgpu_join_inner(C.byref(lks[0]._col), C.byref(rks[0]._col), int(nulls_equal), order, val,
-                                         C.byref(li), C.byref(ri), None))
+        N.check(N.lib().plgpu_join(C.byref(lks[0]._col), C.byref(rks[0]._col), hw, int(nulls_equal), order, val,
+                                   C.byref(li), C.byref(ri), None))
     else:
-        # several keys (or a Float64 / Boolean key): hashed tuples, pairs verified
-        N.check(N.lib().plgpu_join_inner_multi(_col_array(lks), _col_array(rks), builtins.len(lks),
-                                               int(nulls_equal), order, val, C.byref(li), C.byref(ri), None))
+        # several keys (or a Float64 / Boolean key): packed or hashed tuples
+        N.check(N.lib().plgpu_join_multi(_col_array(lks), _col_array(rks), builtins.len(lks), hw,
+                                         int(nulls_equal), order, val, C.byref(li), C.byref(ri), None))
     lidx, ridx = Series._from_native("__left_idx", li), Series._from_native("__right_idx", ri)
 
     def take(df: DataFrame, names: list[str], idx: Series) -> list[Series]:
@@ -850,9 +863,24 @@ def _join(left: DataFrame, right: DataFrame, left_on: str | tuple, right_on: str
                                      C.byref(idx._col), out, None))
         return [Series._from_native(n, out[i]) for i, n in enumerate(names)]
 
-    lnames = left.columns
-    rnames = [n for n in right.columns if n not in rkeys]
+    if how in ("semi", "anti"):
+        return DataFrame(take(left, left.columns, lidx))
+    if coalesce is None:
+        coalesce = how != "full"
+    if coalesce and how == "right":
+        lnames = [n for n in left.columns if n not in lkeys]
+        rnames = right.columns
+    else:
+        lnames = left.columns
+        rnames = [n for n in right.columns if not (coalesce and n in rkeys)]
     out = take(left, lnames, lidx)
+    if coalesce and how == "full":
+        rk_cols = take(right, rkeys, ridx)
+        for lk, rk in zip(lkeys, rk_cols):
+            i = lnames.index(lk)
+            c = N.Column()
+            N.check(N.lib().plgpu_coalesce(C.byref(out[i]._col), C.byref(rk._col), C.byref(c), None))
+            out[i] = Series._from_native(lk, c)
     for s in take(right, rnames, ridx):
         if s.name in lnames:
             s.name = s.name + suffix

@@ -16,8 +16,8 @@ subtree with a Python UDF via `NodeTraverser.set_udf`
 crates/polars-python/src/lazyframe/visitor/nodes.rs, expression classes of
 .../visitor/expr_nodes.rs) for the hot path — DataFrameScan, Filter,
 Select/HStack of arithmetic + comparisons, GroupBy on one integer key with
-sum/mean/min/max/count/len, inner Join on one integer key, Sort by one
-column — into a polaroid_amd plan and installs a UDF that
+sum/mean/min/max/count/len, inner / left / right / full / semi / anti Join
+on 1..8 key columns, Sort by 1..8 columns — into a polaroid_amd plan and installs a UDF that
 runs it through libpolaroid_gpu.so.  A query outside that path is left to
 polars' own engine unless `raise_on_fail` is set (the reference GPU engine's
 behaviour).  Once accepted, nothing falls back: a missing HIP library or a
@@ -142,8 +142,8 @@ class _Translator:
             return ("polars_scan", node.df, None if proj is None else list(proj))
         if k == "Join":
             # options: (how, nulls_equal, slice, suffix, coalesce, maintain_order), nodes.rs:536
-            how, nulls_equal, slc, suffix, _coalesce, order = node.options
-            if str(how) != "inner":
+            how, nulls_equal, slc, suffix, coalesce, order = node.options
+            if not isinstance(how, str) or how not in ("inner", "left", "right", "full", "semi", "anti"):
                 raise Unsupported(f"{how} join")
             if slc is not None:
                 raise Unsupported("join slice")
@@ -159,8 +159,10 @@ class _Translator:
             left = self.child(node.input_left)
             right = self.child(node.input_right)
             order = str(order).lower()
+            # coalesce arrives resolved for the join type (JoinCoalesce::coalesce)
             return ("join", left, right, names[0], names[1], str(suffix), "m:m", bool(nulls_equal),
-                    order if order in ("none", "left", "right", "left_right", "right_left") else "none")
+                    order if order in ("none", "left", "right", "left_right", "right_left") else "none",
+                    how, bool(coalesce))
         if k == "Sort":
             if node.slice is not None:
                 raise Unsupported("sort slice")

@@ -355,6 +355,113 @@ def join_multi_cases():
     })
     return {"cases": cases}
 
+# ---------------------------------------------------------------------------
+# 4c. Left / right / full / semi / anti joins (operations/test_join.py).
+#     String payloads and nested keys are label-encoded into integers (the
+#     encoding keeps equality and order, which is all the joins look at).
+#     Each case: left / right columns, `on` (one name or a list), `how`,
+#     `args`, and `expected` columns compared in order when `ordered`
+#     (first `prefix` rows only when the test slices), as a multiset of
+#     rows otherwise; `columns` = the asserted output column order.
+def join_types_cases():
+    cases = []
+    # test_semi_anti_join: payload ["f", "i", None] -> [0, 1, None]
+    la = {"key": [1, 2, 3], "payload": [0, 1, None]}
+    rb = {"key": [3, 4, 5, None]}
+    for how, exp in (("anti", {"key": [1, 2], "payload": [0, 1]}), ("semi", {"key": [3], "payload": [None]})):
+        cases.append({"name": f"test_semi_anti_join[{how}]", "source": "operations/test_join.py:27-48",
+                      "left": la, "right": rb, "on": "key", "how": how, "args": {},
+                      "expected": exp, "ordered": True, "columns": ["key", "payload"]})
+    # b: ["a", "b", "c", "a"] / ["c", "c", "d", "e"] -> a=0, b=1, c=2, d=3, e=4
+    la = {"a": [1, 2, 3, 1], "b": [0, 1, 2, 0], "payload": [10, 20, 30, 40]}
+    rb = {"a": [3, 3, 4, 5], "b": [2, 2, 3, 4]}
+    for how, exp in (("anti", {"a": [1, 2, 1], "b": [0, 1, 0], "payload": [10, 20, 40]}),
+                     ("semi", {"a": [3], "b": [2], "payload": [30]})):
+        cases.append({"name": f"test_semi_anti_join multi-key[{how}]", "source": "operations/test_join.py:50-65",
+                      "left": la, "right": rb, "on": ["a", "b"], "how": how, "args": {},
+                      "expected": exp, "ordered": True, "columns": ["a", "b", "payload"]})
+    # test_join_sorted_fast_paths_null
+    l1 = {"x": [0, 0, 1]}
+    r1 = {"x": [0, None], "y": [0, 1]}
+    for how, exp, cols in (("inner", {"x": [0, 0], "y": [0, 0]}, ["x", "y"]),
+                           ("left", {"x": [0, 0, 1], "y": [0, 0, None]}, ["x", "y"]),
+                           ("anti", {"x": [1]}, ["x"]),
+                           ("semi", {"x": [0, 0]}, ["x"]),
+                           ("full", {"x": [0, 0, 1, None], "x_right": [0, 0, None, None], "y": [0, 0, None, 1]},
+                            ["x", "x_right", "y"])):
+        cases.append({"name": f"test_join_sorted_fast_paths_null[{how}]", "source": "operations/test_join.py:674-691",
+                      "left": l1, "right": r1, "on": "x", "how": how, "args": {},
+                      "expected": exp, "ordered": how != "full", "columns": cols})
+    # test_join_preserve_order_left / _full
+    l2 = {"a": [None, 2, 1, 1, 5]}
+    r2 = {"a": [1, None, 2, 6], "b": [6, 7, 8, 9]}
+    for how, order, col, exp, prefix in (
+            ("left", "none", "a", [None, 2, 1, 1, 5], None),
+            ("left", "left", "a", [None, 2, 1, 1, 5], None),
+            ("left", "left_right", "a", [None, 2, 1, 1, 5], None),
+            ("left", "right", "a", [1, 1, 2, None, 5], 5),
+            ("left", "right_left", "a", [1, 1, 2, None, 5], None),
+            ("right", "left", "a", [2, 1, 1, None, 6], None),
+            ("right", "right", "a", [1, 1, None, 2, 6], None),
+            ("full", "left", "a", [None, 2, 1, 1, 5], 5),
+            ("full", "right", "a", [1, 1, None, 2, None], 5),
+            ("full", "left_right", "a_right", [None, 2, 1, 1, None, None, 6], None),
+            ("full", "right_left", "a", [1, 1, None, 2, None, None, 5], None)):
+        src = "operations/test_join.py:1311-1373" if how != "full" else "operations/test_join.py:1376-1421"
+        case = {"name": f"test_join_preserve_order_{'full' if how == 'full' else 'left'}[{how}, {order}]",
+                "source": src, "left": l2, "right": r2, "on": "a", "how": how,
+                "args": {"maintain_order": order}, "expected": {col: exp}, "ordered": True}
+        if prefix:
+            case["prefix"] = prefix
+        cases.append(case)
+    # test_join_null_equal: left and full parts
+    lhs = {"x": [1, None, None], "y": [1, 2, 3]}
+    with_null = {"x": [1, None], "z": [1, 2]}
+    without_null = {"x": [1, 3], "z": [1, 3]}
+    for order in ("none", "left_right", "right_left"):
+        src = "operations/test_join.py:1933-1985"
+        cases.append({"name": f"test_join_null_equal[{order}] left with_null", "source": src,
+                      "left": lhs, "right": with_null, "on": "x", "how": "left",
+                      "args": {"nulls_equal": True, "maintain_order": order},
+                      "expected": {"x": [1, None, None], "y": [1, 2, 3], "z": [1, 2, 2]},
+                      "ordered": order != "none"})
+        cases.append({"name": f"test_join_null_equal[{order}] left without_null", "source": src,
+                      "left": lhs, "right": without_null, "on": "x", "how": "left",
+                      "args": {"nulls_equal": True, "maintain_order": order},
+                      "expected": {"x": [1, None, None], "y": [1, 2, 3], "z": [1, None, None]},
+                      "ordered": order != "none"})
+        cases.append({"name": f"test_join_null_equal[{order}] full coalesce with_null", "source": src,
+                      "left": lhs, "right": with_null, "on": "x", "how": "full",
+                      "args": {"nulls_equal": True, "coalesce": True, "maintain_order": order},
+                      "expected": {"x": [1, None, None], "y": [1, 2, 3], "z": [1, 2, 2]},
+                      "ordered": order != "none"})
+        if order == "left_right":
+            exp = {"x": [1, None, None, None], "x_right": [1, None, None, 3], "y": [1, 2, 3, None],
+                   "z": [1, None, None, 3]}
+        else:
+            exp = {"x": [1, None, None, None], "x_right": [1, 3, None, None], "y": [1, None, 2, 3],
+                   "z": [1, 3, None, None]}
+        cases.append({"name": f"test_join_null_equal[{order}] full without_null", "source": src,
+                      "left": lhs, "right": without_null, "on": "x", "how": "full",
+                      "args": {"nulls_equal": True, "maintain_order": order},
+                      "expected": exp, "ordered": order != "none"})
+    # test_join_on_nested: the nested key values data[0..3] -> 1..4
+    lhs = {"a": [1, 2, 3], "b": [1, 2, 3]}
+    rhs = {"a": [4, 2], "c": [4, 2]}
+    src = "operations/test_join.py:1776-1836"
+    for how, order, exp, cols in (
+            ("left", "left", {"a": [1, 2, 3], "b": [1, 2, 3], "c": [None, 2, None]}, ["a", "b", "c"]),
+            ("right", "right", {"b": [None, 2], "a": [4, 2], "c": [4, 2]}, ["b", "a", "c"]),
+            ("inner", None, {"a": [2], "b": [2], "c": [2]}, ["a", "b", "c"]),
+            ("full", "left_right", {"a": [1, 2, 3, None], "b": [1, 2, 3, None], "a_right": [None, 2, None, 4],
+                                    "c": [None, 2, None, 4]}, ["a", "b", "a_right", "c"]),
+            ("semi", None, {"a": [2], "b": [2]}, ["a", "b"]),
+            ("anti", "left", {"a": [1, 3], "b": [1, 3]}, ["a", "b"])):
+        args = {} if order is None else {"maintain_order": order}
+        cases.append({"name": f"test_join_on_nested[{how}]", "source": src, "left": lhs, "right": rhs,
+                      "on": "a", "how": how, "args": args, "expected": exp, "ordered": True, "columns": cols})
+    return {"cases": cases}
+
 
 # ---------------------------------------------------------------------------
 # 5. Sorting (operations/test_sort.py).  `values` of one column; expected
@@ -476,6 +583,7 @@ def main():
                       ("filter_cases.json", filter_cases()),
                       ("join_cases.json", join_cases()),
                       ("join_multi_cases.json", join_multi_cases()),
+                      ("join_types_cases.json", join_types_cases()),
                       ("sort_cases.json", sort_cases()),
                       ("sort_multi_cases.json", sort_multi_cases()),
                       ("rolling_cases.json", rolling_cases())):

@@ -186,10 +186,16 @@ def test_translate_join_and_sort():
     jn = plan[1]
     assert jn[0] == "join" and jn[3] == "k" and jn[4] == "k" and jn[5] == "_right" and jn[8] == "left"
     assert jn[1][0] == "polars_scan" and jn[2][0] == "polars_scan"
-    # outer joins, rolling expressions (NotImplemented in the visitor) stay on polars
-    nt.lp[j].options = ("full", False, None, "_right", True, "none")
-    with pytest.raises(PE.Unsupported):
-        PE.translate(nt)
+    # every equi-join type translates (coalesce arrives resolved); cross joins
+    # and IE joins (a tuple `how`) stay on polars
+    for how, co in (("left", True), ("right", True), ("full", False), ("semi", True), ("anti", True)):
+        nt.lp[j].options = (how, True, None, "_r", co, "left_right")
+        jn = PE.translate(nt)[1]
+        assert jn[9] == how and jn[10] is co and jn[7] is True and jn[8] == "left_right" and jn[5] == "_r"
+    for how in ("cross", ("ie_join", "lt", None)):
+        nt.lp[j].options = (how, False, None, "_right", True, "none")
+        with pytest.raises(PE.Unsupported):
+            PE.translate(nt)
 
 
 @pytest.mark.gpu
