@@ -1247,6 +1247,27 @@ static int check_key(const plgpu_column* k) {
     return PLGPU_OK;
 }
 
+// Stable sort of the pairs by the left (or right) index, a null index last.
+static int jn_sort_pairs(plgpu_column* li, plgpu_column* ri, bool by_right, hipStream_t s) {
+    plgpu_column perm;
+    int rc = plgpu_arg_sort(by_right ? ri : li, 0, 1, &perm, s);
+    if (rc) {
+        plgpu_column_release(li);
+        plgpu_column_release(ri);
+        return rc;
+    }
+    plgpu_column in[2] = {*li, *ri};
+    plgpu_column out[2];
+    rc = plgpu_gather(in, 2, &perm, out, s);
+    plgpu_column_release(&perm);
+    plgpu_column_release(li);
+    plgpu_column_release(ri);
+    if (rc) return rc;
+    *li = out[0];
+    *ri = out[1];
+    return PLGPU_OK;
+}
+
 // Join of two checked key columns (validation failures return
 // PLGPU_ERR_SCHEMA; nothing else does).  How each join type maps onto a
 // build side, probe mode and drain (DESIGN.md §Join types):
@@ -1279,6 +1300,25 @@ static int join_impl(const plgpu_column* left_key, const plgpu_column* right_key
     const bool order_left = maintain_order == PLGPU_JOIN_ORDER_LEFT || maintain_order == PLGPU_JOIN_ORDER_LEFT_RIGHT;
     const bool order_right =
         maintain_order == PLGPU_JOIN_ORDER_RIGHT || maintain_order == PLGPU_JOIN_ORDER_RIGHT_LEFT;
+    {
+        // The ordered plans probe the side whose order is kept, so they build
+        // on the other side.  When that side is the much larger one (a 1e9-row
+        // table for a 1e7-row probe), build on the small side instead and
+        // stably sort the pairs by the kept side's index (nulls last), which
+        // is what the reference itself does (dispatch_left_right.rs:143,
+        // hash_join/mod.rs:164).  The base order of the swapped plan has the
+        // other side's rows ascending within each kept row, as required.
+        const int64_t nl = left_key->length, nr = right_key->length;
+        const bool swap_right = order_right && (how == PLGPU_JOIN_INNER || how == PLGPU_JOIN_LEFT ||
+                                                how == PLGPU_JOIN_FULL) && nl > 2 * nr;
+        const bool swap_left = order_left && (how == PLGPU_JOIN_INNER || how == PLGPU_JOIN_FULL) && nr > 2 * nl;
+        if (swap_right || swap_left) {
+            rc = join_impl(left_key, right_key, how, neq, swap_right ? PLGPU_JOIN_ORDER_LEFT : PLGPU_JOIN_ORDER_RIGHT,
+                           validate, out_left_idx, out_right_idx, s);
+            if (!rc) rc = jn_sort_pairs(out_left_idx, out_right_idx, swap_right, s);
+            return rc;
+        }
+    }
     bool build_right, ordered = maintain_order != PLGPU_JOIN_ORDER_NONE, drain = false;
     int mode;
     switch (how) {

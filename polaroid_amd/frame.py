@@ -873,7 +873,15 @@ def _join(left: DataFrame, right: DataFrame, left_on: str | tuple, right_on: str
     else:
         lnames = left.columns
         rnames = [n for n in right.columns if not (coalesce and n in rkeys)]
-    out = take(left, lnames, lidx)
+    # A left join in left order that produced one row per left row has the
+    # identity as its left index: the left columns are shared, not gathered
+    # (the reference's _create_left_df_from_slice shortcut for a sorted index
+    # of full length); likewise the right side of a right join.
+    same_left = (how == "left" and maintain_order not in ("right", "right_left") and lidx.len() == left.height)
+    same_right = (how == "right" and maintain_order not in ("left", "left_right") and ridx.len() == right.height)
+    if same_right:
+        take_right = [right._cols[n].alias(n) for n in rnames]
+    out = [left._cols[n].alias(n) for n in lnames] if same_left else take(left, lnames, lidx)
     if coalesce and how == "full":
         rk_cols = take(right, rkeys, ridx)
         for lk, rk in zip(lkeys, rk_cols):
@@ -881,7 +889,7 @@ def _join(left: DataFrame, right: DataFrame, left_on: str | tuple, right_on: str
             c = N.Column()
             N.check(N.lib().plgpu_coalesce(C.byref(out[i]._col), C.byref(rk._col), C.byref(c), None))
             out[i] = Series._from_native(lk, c)
-    for s in take(right, rnames, ridx):
+    for s in (take_right if same_right else take(right, rnames, ridx)):
         if s.name in lnames:
             s.name = s.name + suffix
         out.append(s)

@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--dist", action="store_true")
     ap.add_argument("--strategy", default="auto")
+    ap.add_argument("--how", default="inner", help="inner / left / right / full / semi / anti")
+    ap.add_argument("--order", default="none", help="maintain_order")
     args = ap.parse_args()
     import torch
 
@@ -56,21 +58,23 @@ def main():
     probe = pl.DataFrame([pl.Series.from_torch("k", pk), pl.Series.from_torch("pv", pv)])
     build = pl.DataFrame([pl.Series.from_torch("k", bk), pl.Series.from_torch("bv", bv)])
     out = None
+    kw = dict(on="k", how=args.how, maintain_order=args.order)
     for _ in range(args.warmup):
-        out = probe.join(build, on="k")
+        out = probe.join(build, **kw)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        out = probe.join(build, on="k")
+        out = probe.join(build, **kw)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / args.steps
     rows_out = out.height
     print(json.dumps({
-        "metric": "Mrows/sec hash inner-join probe (1e9 probe x 1e7 build, i64 key), materialised",
+        "metric": f"Mrows/sec hash {args.how}-join probe (1e9 probe x 1e7 build, i64 key), materialised",
         "value": round(n / dt / 1e6, 1), "unit": "Mrows/s", "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True,
         "dtype": "int64", "data": "synthetic keys/payloads generated on device",
-        "config": {"workload": "probe.join(build, on='k') inner, output k, pv, bv", "probe_rows": n,
+        "config": {"workload": f"probe.join(build, on='k', how='{args.how}', maintain_order='{args.order}'), "
+                               "output every column", "probe_rows": n,
                    "build_rows": m, "output_rows": rows_out},
     }), flush=True)
 
