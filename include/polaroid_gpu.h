@@ -130,7 +130,9 @@ enum plgpu_agg_kind {
     PLGPU_AGG_MIN = 3,   /* NaN ignored unless all NaN (min_ignore_nan)      */
     PLGPU_AGG_MAX = 4,
     PLGPU_AGG_COUNT = 5, /* non-null count, u32 (IdxSize)                    */
-    PLGPU_AGG_LEN = 6    /* group length incl. nulls, u32                    */
+    PLGPU_AGG_LEN = 6,   /* group length incl. nulls, u32                    */
+    PLGPU_AGG_FIRST = 7, /* value of the group's first row, null included    */
+    PLGPU_AGG_LAST = 8   /* ... last row (reduce/first_last.rs First / Last) */
 };
 
 typedef struct plgpu_agg {

@@ -18,7 +18,7 @@ LIB = os.path.join(HERE, "_build", "liboracle.so")
 
 BOOL, I32, I64, F64, U32 = 1, 2, 3, 4, 5
 SUM_KAHAN, SUM_NAIVE, SUM_EXACT = 0, 1, 2
-AGG = dict(sum=1, mean=2, min=3, max=4, count=5, len=6)
+AGG = dict(sum=1, mean=2, min=3, max=4, count=5, len=6, first=7, last=8)
 
 
 class _Col(C.Structure):  # layout of plgpu_column (include/polaroid_gpu.h)

@@ -574,6 +574,15 @@ OR_EXPORT int64_t or_group_by_agg(const plgpu_column* key, const plgpu_column* c
                 else ((int64_t*)out_vals[a])[gi] = bi;
                 break;
             }
+            case PLGPU_AGG_FIRST: case PLGPU_AGG_LAST: {
+                /* polars-expr/src/reduce/first_last.rs First / Last: the value
+                 * of the group's first / last row, null included */
+                val_t v = col_get(c, rows[aggs[a].kind == PLGPU_AGG_FIRST ? 0 : len - 1]);
+                valid = (uint8_t)v.valid;
+                if (isf) ((double*)out_vals[a])[gi] = v.valid ? v.f : 0.0;
+                else ((int64_t*)out_vals[a])[gi] = v.valid ? v.i : 0;
+                break;
+            }
             default:
                 free_groups(&g);
                 return -1;

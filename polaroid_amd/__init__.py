@@ -23,7 +23,7 @@ from ._native import (
     ShapeError,
     device_count,
 )
-from .expr import Expr, col, count, len, lit, max, mean, min, sum
+from .expr import Expr, col, count, first, last, len, lit, max, mean, min, sum
 from .frame import (
     Boolean,
     DataFrame,
@@ -43,7 +43,7 @@ __all__ = [
     "Boolean", "ComputeError", "DataFrame", "DataType", "DeviceError", "DuplicateError", "Expr", "Float64", "GroupBy",
     "Int32", "Int64", "InvalidOperationError", "LazyFrame", "LazyGroupBy", "OutOfMemoryError",
     "PolaroidError", "Series", "ShapeError", "UInt32", "col", "count", "device_count", "from_dict",
-    "len", "lit", "max", "mean", "min", "sum",
+    "first", "last", "len", "lit", "max", "mean", "min", "sum",
 ]
 
 

@@ -28,7 +28,7 @@ OP = dict(
     EQ=20, NE=21, LT=22, LE=23, GT=24, GE=25, EQ_MISSING=26, NE_MISSING=27,
     AND=30, OR=31, NOT=32, IS_NULL=33, IS_NOT_NULL=34, IS_NAN=35, IS_FINITE=36,
 )
-AGG = dict(sum=1, mean=2, min=3, max=4, count=5, len=6)
+AGG = dict(sum=1, mean=2, min=3, max=4, count=5, len=6, first=7, last=8)
 MAX_COLS = 8
 MAX_KEYS = 8
 

@@ -103,7 +103,8 @@ struct GbParams {
     uint8_t fop[kMaxFields]; // per-field merge op (partial-state merge)
     int32_t pred_acc;       // acc whose column is the simple predicate's, or -1
     int32_t f_len;
-    int32_t f_first;        // -1 unless maintain_order
+    int32_t f_first;        // min selected row per group: maintain_order / first(); else -1
+    int32_t f_last;         // max selected row per group: last(); else -1
     int32_t lbits;
     uint64_t min_init_mask; // fields initialised to ~0
     int32_t lcap;
@@ -278,6 +279,7 @@ __device__ __forceinline__ void apply_row(const GbParams& p, uint64_t* lds, int 
     };
     atomicAdd(F(p.f_len), 1ull);
     if (p.f_first >= 0) atomicMin(F(p.f_first), (unsigned long long)row);
+    if (p.f_last >= 0) atomicMax(F(p.f_last), (unsigned long long)row);
 #pragma unroll 1
     for (int k = 0; k < nacc; ++k) {
         const uint64_t d = dd[0];
@@ -382,6 +384,8 @@ __device__ __forceinline__ void flush_and_report(const GbParams& p, uint64_t* ld
             atomicAdd((unsigned long long*)gfield(p, p.f_len, gs), (unsigned long long)len);
             if (p.f_first >= 0)
                 atomicMin((unsigned long long*)gfield(p, p.f_first, gs), (unsigned long long)lds[p.f_first * L + s]);
+            if (p.f_last >= 0)
+                atomicMax((unsigned long long*)gfield(p, p.f_last, gs), (unsigned long long)lds[p.f_last * L + s]);
             for (int a = 0; a < p.nacc; ++a) {
                 const AccSpec& ac = p.acc[a];
                 if (ac.f_cnt >= 0) {
@@ -1328,6 +1332,17 @@ __global__ void gb_finalize_kernel(GbParams p, FinParams fp) {
                 }
                 break;
             }
+            case PLGPU_AGG_FIRST:
+            case PLGPU_AGG_LAST: {
+                // the value (null included) of the group's first / last
+                // selected row (polars-expr/src/reduce/first_last.rs)
+                const int64_t row = (int64_t)*gfield(p, os.kind == PLGPU_AGG_FIRST ? p.f_first : p.f_last, s);
+                valid = dev_valid(ac.c, row);
+                const uint64_t v = valid ? dev_load(ac.c, row) : 0ull;
+                if (os.out_dtype == PLGPU_I64 || os.out_dtype == PLGPU_F64) ((uint64_t*)os.values)[g] = v;
+                else ((uint32_t*)os.values)[g] = (uint32_t)v;
+                break;
+            }
             default: break;
             }
             if (os.validity && valid) atomicOr(&os.validity[g >> 5], 1u << (g & 31));
@@ -1484,8 +1499,14 @@ static int plan_groupby(const plgpu_column* key, const plgpu_column* cols, int32
     p.n = key->length;
     int nf = 1;  // field 0: keys
     p.f_len = nf++;
-    p.f_first = maintain_order ? nf++ : -1;
-    if (maintain_order) p.min_init_mask |= 1ull << p.f_first;
+    bool any_first = false, any_last = false;
+    for (int i = 0; i < naggs; ++i) {
+        any_first |= aggs[i].kind == PLGPU_AGG_FIRST;
+        any_last |= aggs[i].kind == PLGPU_AGG_LAST;
+    }
+    p.f_first = (maintain_order || any_first) ? nf++ : -1;
+    if (p.f_first >= 0) p.min_init_mask |= 1ull << p.f_first;
+    p.f_last = any_last ? nf++ : -1;
     int acc_of_col[PLGPU_MAX_COLS];
     for (int i = 0; i < PLGPU_MAX_COLS; ++i) acc_of_col[i] = -1;
     p.nacc = 0;
@@ -1518,7 +1539,9 @@ static int plan_groupby(const plgpu_column* key, const plgpu_column* cols, int32
         case PLGPU_AGG_MIN: ac.flags |= A_MIN | (isf ? A_FLAGS : 0) | A_CNT; break;
         case PLGPU_AGG_MAX: ac.flags |= A_MAX | (isf ? A_FLAGS : 0) | A_CNT; break;
         case PLGPU_AGG_COUNT: if (nullable) ac.flags |= A_CNT; break;
-        case PLGPU_AGG_LEN: break;
+        case PLGPU_AGG_LEN:
+        case PLGPU_AGG_FIRST:
+        case PLGPU_AGG_LAST: break;
         default: return fail(PLGPU_ERR_INVALID, "unknown aggregation kind");
         }
         pl->acc_of_agg[i] = acc_of_col[c];
@@ -1545,6 +1568,7 @@ static int plan_groupby(const plgpu_column* key, const plgpu_column* cols, int32
     std::memset(p.fop, 0, sizeof p.fop);
     p.fop[p.f_len] = FOP_ADD;
     if (p.f_first >= 0) p.fop[p.f_first] = FOP_MIN;
+    if (p.f_last >= 0) p.fop[p.f_last] = FOP_MAX;
     for (int a = 0; a < p.nacc; ++a) {
         const AccSpec& ac = p.acc[a];
         if (ac.f_sum >= 0) {
@@ -1915,7 +1939,7 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
         pl.fast_grid = (int)g;
     }
     // sum-only signature with the compile-time field layout
-    bool so = p.f_first < 0 && p.f_len == 1 && p.nacc > 0;
+    bool so = p.f_first < 0 && p.f_last < 0 && p.f_len == 1 && p.nacc > 0;
     for (int a = 0; a < p.nacc; ++a) {
         const AccSpec& ac = p.acc[a];
         so = so && ac.isf && ac.flags == (A_FSUM | A_FLAGS) && ac.f_sum == 2 + 4 * a && ac.f_flags == 5 + 4 * a &&
@@ -1939,7 +1963,7 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
     // aggregated columns null-free (they are copied as raw words)
     R.part = false;
     if (!pl.use_lds && n >= (int64_t(1) << 20) && R.est_groups > 0 && p.key.validity == nullptr &&
-        !(p.f_first >= 0 && n >= 0xFFFFFFFFll) && !getenv("PLGPU_NO_PART")) {
+        !((p.f_first >= 0 || p.f_last >= 0) && n >= 0xFFFFFFFFll) && !getenv("PLGPU_NO_PART")) {
         bool ok2 = true;
         for (int a = 0; a < p.nacc; ++a) ok2 = ok2 && p.acc[a].c.validity == nullptr;
         // LDS table of the partition workgroups: two per CU, or one when
@@ -2002,7 +2026,7 @@ static int gb_partition(GbRun& R) {
     for (int q = 0; q < P; ++q) maxpart = std::max<uint64_t>(maxpart, hr[q + 1] - hr[q]);
     const int64_t rows = (int64_t)std::max<uint64_t>(hr[P], 2) + 2;
     R.part_rows_total = (int64_t)hr[P];
-    const bool want_rows = p.f_first >= 0;
+    const bool want_rows = p.f_first >= 0 || p.f_last >= 0;
     const size_t words = (size_t)rows * (1 + p.nacc) + (want_rows ? ((size_t)rows + 1) / 2 : 0);
     if ((rc = dev_alloc((void**)&R.pbuf, words * 8, s))) return rc;
     R.pout.key = R.pbuf;
@@ -2268,7 +2292,8 @@ static int gb_finalize(GbRun& R, int32_t naggs, plgpu_column* out_key, plgpu_col
     int rc = make_owned_column(out_key, PLGPU_I64, groups, true, s);
     for (int i = 0; i < naggs && rc == PLGPU_OK; ++i) {
         const OutSpec& o = pl.outs[i];
-        const bool nullable = o.kind == PLGPU_AGG_MEAN || o.kind == PLGPU_AGG_MIN || o.kind == PLGPU_AGG_MAX;
+        const bool nullable = o.kind == PLGPU_AGG_MEAN || o.kind == PLGPU_AGG_MIN || o.kind == PLGPU_AGG_MAX ||
+                              o.kind == PLGPU_AGG_FIRST || o.kind == PLGPU_AGG_LAST;
         rc = make_owned_column(&out_aggs[i], o.out_dtype, groups, nullable, s);
     }
     uint64_t* first = nullptr;
@@ -2543,6 +2568,11 @@ PLGPU_API int plgpu_gb_partial_begin(const plgpu_column* key, const plgpu_column
         return fail(PLGPU_ERR_INVALID, "NULL argument");
     if (world < 1) return fail(PLGPU_ERR_INVALID, "world must be >= 1");
     *out = nullptr;
+    for (int i = 0; i < naggs && aggs; ++i)
+        if (aggs[i].kind == PLGPU_AGG_FIRST || aggs[i].kind == PLGPU_AGG_LAST)
+            // partial states hold rank-local row ids; merging first / last
+            // across ranks needs global row order, which is not exchanged
+            return fail(PLGPU_ERR_INVALID, "first / last aggregations are not supported on the partitioned path");
     plgpu_gb_partial* h = new plgpu_gb_partial();
     GbRun& R = h->run;
     R.world = world;

@@ -134,6 +134,8 @@ class Expr:
     def max(self): return Expr("agg", (self,), op="max")
     def count(self): return Expr("agg", (self,), op="count")
     def len(self): return Expr("agg", (self,), op="len")
+    def first(self): return Expr("agg", (self,), op="first")
+    def last(self): return Expr("agg", (self,), op="last")
 
     # ------------------------------------------------- window / ordering
     def rolling_sum(self, window_size: int, weights=None, *, min_samples: int | None = None,
@@ -200,6 +202,14 @@ def max(name: str) -> Expr:  # noqa: A001
 
 def count(name: str) -> Expr:
     return col(name).count()
+
+
+def first(name: str) -> Expr:
+    return col(name).first()
+
+
+def last(name: str) -> Expr:
+    return col(name).last()
 
 
 _BIN_OPS = {

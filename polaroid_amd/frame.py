@@ -753,7 +753,7 @@ def _gb_lower(df: DataFrame, key: str | tuple, aggs: list[Expr], pred: Expr | No
             specs.append((base.op, base.args[0].value))
         else:
             raise N.InvalidOperationError(
-                f"aggregation {e!r} is not supported on the GPU executor (need col(..).sum/mean/min/max/count/len)")
+                f"aggregation {e!r} is not supported on the GPU executor (need col(..).sum/mean/min/max/count/len/first/last)")
         out_names.append(name)
     # columns passed to the kernel: predicate columns + aggregated columns
     names: list[str] = []

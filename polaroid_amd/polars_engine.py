@@ -16,7 +16,7 @@ subtree with a Python UDF via `NodeTraverser.set_udf`
 crates/polars-python/src/lazyframe/visitor/nodes.rs, expression classes of
 .../visitor/expr_nodes.rs) for the hot path — DataFrameScan, Filter,
 Select/HStack of arithmetic + comparisons, GroupBy on one integer key with
-sum/mean/min/max/count/len, inner / left / right / full / semi / anti Join
+sum/mean/min/max/count/len/first/last, inner / left / right / full / semi / anti Join
 on 1..8 key columns, Sort by 1..8 columns — into a polaroid_amd plan and installs a UDF that
 runs it through libpolaroid_gpu.so.  A query outside that path is left to
 polars' own engine unless `raise_on_fail` is set (the reference GPU engine's
@@ -128,6 +128,8 @@ class _Translator:
             return getattr(c, name)()
         if name == "count":
             return c.len() if e.options else c.count()
+        if name in ("first", "last"):  # IRAggExpr::First / Last (expr_nodes.rs:677,687)
+            return getattr(c, name)()
         raise Unsupported(f"aggregation {name}")
 
     # ---------------------------------------------------------------- plans

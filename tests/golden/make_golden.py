@@ -144,6 +144,14 @@ def group_by_cases():
             "mean": fx([nan, nan, nan, None, inf, inf]),
         },
     })
+    cases.append({
+        "name": "test_group_by_wildcard (first)",
+        "source": "operations/test_group_by.py:760-770 (keys a == b, so one key is equivalent)",
+        "key": [1, 2],
+        "cols": {"a": {"dtype": "i64", "values": [1, 2]}},
+        "aggs": [["first", "a", "a_agg"]], "maintain_order": True,
+        "expected": {"key": [1, 2], "a_agg": [1, 2]},
+    })
     return {"cases": cases}
 
 
