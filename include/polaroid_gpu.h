@@ -49,7 +49,9 @@ enum plgpu_dtype {
     PLGPU_I32 = 2,  /* "i"                                             */
     PLGPU_I64 = 3,  /* "l"                                             */
     PLGPU_F64 = 4,  /* "g"                                             */
-    PLGPU_U32 = 5   /* "I"  polars IdxSize (count / len outputs)       */
+    PLGPU_U32 = 5,  /* "I"  polars IdxSize (count / len outputs)       */
+    PLGPU_STR = 6   /* "U"  large_string: int64 offsets in `values`,
+                       UTF-8 bytes in `data` (polars String / Binary)   */
 };
 
 /* One Arrow array in device memory (Arrow C Device Data Interface,
@@ -64,6 +66,8 @@ typedef struct plgpu_column {
     const uint8_t* validity;  /* device ptr, Arrow buffers[0]; NULL = all valid    */
     void (*release)(struct plgpu_column*); /* NULL for borrowed columns             */
     void* private_data;
+    const uint8_t* data;      /* device ptr, Arrow buffers[2] of PLGPU_STR (bytes); */
+                              /* NULL for fixed-width columns                       */
 } plgpu_column;
 
 /* ------------------------------------------------------- expression ISA */

@@ -25,7 +25,7 @@ class _Col(C.Structure):  # layout of plgpu_column (include/polaroid_gpu.h)
     _fields_ = [
         ("dtype", C.c_int32), ("device_id", C.c_int32), ("length", C.c_int64), ("offset", C.c_int64),
         ("null_count", C.c_int64), ("values", C.c_void_p), ("validity", C.c_void_p),
-        ("release", C.c_void_p), ("private_data", C.c_void_p),
+        ("release", C.c_void_p), ("private_data", C.c_void_p), ("data", C.c_void_p),
     ]
 
 

@@ -35,6 +35,7 @@ from .frame import (
     LazyFrame,
     LazyGroupBy,
     Series,
+    String,
     UInt32,
     from_dict,
 )
@@ -42,7 +43,7 @@ from .frame import (
 __all__ = [
     "Boolean", "ComputeError", "DataFrame", "DataType", "DeviceError", "DuplicateError", "Expr", "Float64", "GroupBy",
     "Int32", "Int64", "InvalidOperationError", "LazyFrame", "LazyGroupBy", "OutOfMemoryError",
-    "PolaroidError", "Series", "ShapeError", "UInt32", "col", "count", "device_count", "from_dict",
+    "PolaroidError", "Series", "ShapeError", "String", "UInt32", "col", "count", "device_count", "from_dict",
     "first", "last", "len", "lit", "max", "mean", "min", "sum",
 ]
 

@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libpolaroid_gpu.so")
 
 # dtypes (enum plgpu_dtype)
-BOOL, I32, I64, F64, U32 = 1, 2, 3, 4, 5
+BOOL, I32, I64, F64, U32, STR = 1, 2, 3, 4, 5, 6
 DTYPE_BYTES = {I32: 4, I64: 8, F64: 8, U32: 4}
 
 # status codes
@@ -48,6 +48,7 @@ Column._fields_ = [
     ("validity", C.c_void_p),
     ("release", C.c_void_p),
     ("private_data", C.c_void_p),
+    ("data", C.c_void_p),  # PLGPU_STR bytes (Arrow buffers[2])
 ]
 
 

@@ -145,7 +145,7 @@ __device__ __forceinline__ uint64_t wave_or64(uint64_t x) {
 }
 
 // Stable scatter of one column by the mask words.
-template <int EB>  // element bytes (4 or 8); 0 = bit-packed bool
+template <int EB>  // element bytes (4 or 8); 0 = bit-packed bool; 16 = the selected row ids
 __global__ __launch_bounds__(kFilterThreads) void filter_scatter_kernel(DevCol col, int64_t n, int64_t ntiles,
                                                                         const uint64_t* __restrict__ mask_words,
                                                                         const uint64_t* __restrict__ tile_off,
@@ -186,6 +186,7 @@ __global__ __launch_bounds__(kFilterThreads) void filter_scatter_kernel(DevCol c
                 const int64_t p = col.offset + r;
                 if (EB == 8) ((uint64_t*)out_values)[pos] = ((const uint64_t*)col.values)[p];
                 else if (EB == 4) ((uint32_t*)out_values)[pos] = ((const uint32_t*)col.values)[p];
+                else if (EB == 16) ((int64_t*)out_values)[pos] = r;  // row ids (string columns)
             }
             if (EB == 0 || col.validity != nullptr) {
                 // Pack bits of the selected rows at their output ranks, then
@@ -297,7 +298,24 @@ static int run_filter(const plgpu_column* cols, int32_t ncols, int src, const De
         PLGPU_HIP(hipMemcpyAsync(&total, offs + ntiles, 8, hipMemcpyDeviceToHost, s));
         PLGPU_HIP(hipStreamSynchronize(s));
     }
-    for (int i = 0; i < ncols; ++i) {
+    int64_t* sel_rows = nullptr;  // selected row ids, for string columns
+    for (int i = 0; i < ncols && !rc; ++i) {
+        if (cols[i].dtype != PLGPU_STR) continue;
+        if (sel_rows == nullptr) {
+            if ((rc = dev_alloc((void**)&sel_rows, std::max<uint64_t>(total, 1) * 8, s))) break;
+            if (total > 0) {
+                DevCol rows;
+                std::memset(&rows, 0, sizeof rows);
+                filter_scatter_kernel<16><<<grid_for(ntiles, 1, 256 * 8), kFilterThreads, 0, s>>>(
+                    rows, n, ntiles, mask_words, offs, (void*)sel_rows, nullptr);
+                PLGPU_HIP(hipGetLastError());
+            }
+        }
+        rc = str_gather(dev_col(cols[i]), nullptr, sel_rows, nullptr, 0, (int64_t)total, cols[i].validity != nullptr,
+                        &out_cols[i], s);
+    }
+    for (int i = 0; i < ncols && !rc; ++i) {
+        if (cols[i].dtype == PLGPU_STR) continue;
         const bool need_valid = cols[i].validity != nullptr;
         rc = make_owned_column(&out_cols[i], cols[i].dtype, (int64_t)total,
                                need_valid || cols[i].dtype == PLGPU_BOOL, s);
@@ -326,6 +344,7 @@ static int run_filter(const plgpu_column* cols, int32_t ncols, int src, const De
     dev_free(mask_words, s);
     dev_free(counts, s);
     dev_free(offs, s);
+    dev_free(sel_rows, s);
     if (rc) {
         for (int i = 0; i < ncols; ++i) plgpu_column_release(&out_cols[i]);
         return rc;

@@ -1463,15 +1463,7 @@ static int num_cus() {
     return g_num_cus;
 }
 
-static DevCol to_dev(const plgpu_column& c) {
-    DevCol d;
-    std::memset(&d, 0, sizeof d);
-    d.values = c.values;
-    d.validity = c.validity;
-    d.offset = c.offset;
-    d.dtype = c.dtype;
-    return d;
-}
+static DevCol to_dev(const plgpu_column& c) { return dev_col(c); }
 
 struct Plan {
     GbParams p;
@@ -2478,7 +2470,12 @@ __global__ __launch_bounds__(256) void mk_verify_kernel(GbParams p, MkKeys k, co
         const uint32_t m = vm[s];
         for (int i = 0; i < k.n; ++i) {
             const bool v = dev_valid(k.c[i], r);
-            bad |= v != (bool)((m >> i) & 1u) || (v && mk_word(k.c[i], r) != vw[(int64_t)i * total + s]);
+            bad |= v != (bool)((m >> i) & 1u);
+            if (!v) continue;
+            if (k.c[i].dtype == PLGPU_STR)  // bytes against the group's first row
+                bad |= !str_equal(k.c[i], r, k.c[i], (int64_t)*gfield(p, p.f_first, s));
+            else
+                bad |= mk_word(k.c[i], r) != vw[(int64_t)i * total + s];
         }
     }
     if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(collision, 1u);
@@ -2749,8 +2746,9 @@ PLGPU_API int plgpu_group_by_agg_multi(const plgpu_column* keys, int32_t nkeys, 
     mk.n = nkeys;
     for (int i = 0; i < nkeys; ++i) {
         const int32_t dt = keys[i].dtype;
-        if (dt != PLGPU_I64 && dt != PLGPU_I32 && dt != PLGPU_U32 && dt != PLGPU_F64 && dt != PLGPU_BOOL)
-            return fail(PLGPU_ERR_SCHEMA, "group-by keys must be Int64, Int32, UInt32, Float64 or Boolean");
+        if (dt != PLGPU_I64 && dt != PLGPU_I32 && dt != PLGPU_U32 && dt != PLGPU_F64 && dt != PLGPU_BOOL &&
+            dt != PLGPU_STR)
+            return fail(PLGPU_ERR_SCHEMA, "group-by keys must be Int64, Int32, UInt32, Float64, Boolean or String");
         if (keys[i].length != n) return fail(PLGPU_ERR_SHAPE, "key columns must have equal lengths");
         mk.c[i] = to_dev(keys[i]);
     }
@@ -2814,6 +2812,11 @@ PLGPU_API int plgpu_group_by_agg_multi(const plgpu_column* keys, int32_t nkeys, 
             const int gg = (int)std::min<int64_t>((groups + 255) / 256, 4096);
             for (int i = 0; i < nkeys && !rc; ++i) {
                 const bool nullable = keys[i].validity != nullptr;
+                if (keys[i].dtype == PLGPU_STR) {  // each group's key string from its first row
+                    rc = str_gather(mk.c[i], nullptr, (const int64_t*)first, nullptr, 0, groups, nullable,
+                                    &out_keys[i], s);
+                    continue;
+                }
                 rc = make_owned_column(&out_keys[i], keys[i].dtype, groups, nullable, s);
                 if (rc || groups == 0) continue;
                 if (keys[i].dtype == PLGPU_BOOL) (void)hipMemsetAsync((void*)out_keys[i].values, 0, ((groups + 63) / 64) * 8, s);

@@ -794,6 +794,7 @@ static hipError_t aos_dispatch(int nc, const AosCols& c, int64_t rows, const uin
 static int gather_into(const plgpu_column& src, const uint32_t* idx, int64_t n, plgpu_column* out, hipStream_t s,
                        const uint8_t* iv = nullptr, int64_t ioff = 0) {
     const bool nullable = src.validity != nullptr || iv != nullptr;
+    if (src.dtype == PLGPU_STR) return str_gather(dev_col(src), idx, nullptr, iv, ioff, n, nullable, out, s);
     int rc = make_owned_column(out, src.dtype, n, nullable, s);
     if (rc) return rc;
     if (n == 0) return PLGPU_OK;
@@ -842,15 +843,7 @@ static void jn_free(JnBuilt& b, hipStream_t s) {
     std::memset(&b.t, 0, sizeof b.t);
 }
 
-static DevCol as_dev(const plgpu_column* c) {
-    DevCol d;
-    std::memset(&d, 0, sizeof d);
-    d.dtype = c->dtype;
-    d.offset = c->offset;
-    d.values = c->values;
-    d.validity = c->validity;
-    return d;
-}
+static DevCol as_dev(const plgpu_column* c) { return dev_col(*c); }
 
 // Build the table over `key` (rows [0, n)); sorted row lists if `ordered`.
 static int jn_build(const plgpu_column* key, bool nulls_equal, bool ordered, JnBuilt* out, hipStream_t s) {
@@ -1535,8 +1528,9 @@ PLGPU_API int plgpu_join_multi(const plgpu_column* left_keys, const plgpu_column
     const int64_t nl = left_keys[0].length, nr = right_keys[0].length;
     for (int i = 0; i < nkeys; ++i) {
         const int32_t dt = left_keys[i].dtype;
-        if (dt != PLGPU_I64 && dt != PLGPU_I32 && dt != PLGPU_U32 && dt != PLGPU_F64 && dt != PLGPU_BOOL)
-            return fail(PLGPU_ERR_SCHEMA, "join keys must be Int64, Int32, UInt32, Float64 or Boolean");
+        if (dt != PLGPU_I64 && dt != PLGPU_I32 && dt != PLGPU_U32 && dt != PLGPU_F64 && dt != PLGPU_BOOL &&
+            dt != PLGPU_STR)
+            return fail(PLGPU_ERR_SCHEMA, "join keys must be Int64, Int32, UInt32, Float64, Boolean or String");
         if (right_keys[i].dtype != dt) return fail(PLGPU_ERR_SCHEMA, "datatypes of join keys don't match");
         if (left_keys[i].length != nl || right_keys[i].length != nr)
             return fail(PLGPU_ERR_SHAPE, "join key columns of one side must have equal lengths");

@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstring>
+
 #include <string>
 
 #include "../../include/polaroid_gpu.h"
@@ -36,6 +38,7 @@ void dev_free(void* p, hipStream_t s);
 struct OwnedBuffers {
     void* values = nullptr;
     void* validity = nullptr;
+    void* data = nullptr;
     hipStream_t stream = nullptr;
 };
 // Fill `out` as an owning column over freshly allocated buffers.
@@ -54,12 +57,34 @@ inline int dtype_bytes(int32_t dt) {
 
 // --------------------------------------------------------- device columns
 struct DevCol {
-    const void* values;
+    const void* values;       // PLGPU_STR: int64 offsets
     const uint8_t* validity;
     int64_t offset;
     int32_t dtype;
     int32_t _pad;
+    const uint8_t* data;      // PLGPU_STR: string bytes
 };
+
+inline DevCol dev_col(const plgpu_column& c) {
+    DevCol d;
+    std::memset(&d, 0, sizeof d);
+    d.values = c.values;
+    d.validity = c.validity;
+    d.offset = c.offset;
+    d.dtype = c.dtype;
+    d.data = c.data;
+    return d;
+}
+
+// Owning PLGPU_STR column: n + 1 offsets, `bytes` of string data.
+int make_owned_string_column(plgpu_column* out, int64_t length, int64_t bytes, bool with_validity, hipStream_t s);
+// An owned I64 column of length + 1 offsets -> a PLGPU_STR column of
+// `length` strings with a `bytes` data buffer.
+int owned_attach_data(plgpu_column* out, int64_t bytes, hipStream_t s);
+// out = src[idx] of a PLGPU_STR column (strings.hip); idx32 / idx64 row ids,
+// iv / ioff optional index validity (a null index gathers a null).
+int str_gather(const DevCol& src, const uint32_t* idx32, const int64_t* idx64, const uint8_t* iv, int64_t ioff,
+               int64_t n, bool nullable, plgpu_column* out, hipStream_t s);
 
 // Lowered (typed) program: the host resolves every operand type, inserts
 // casts, and emits one micro-op per step so the device interpreter does no

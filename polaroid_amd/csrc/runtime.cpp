@@ -4,6 +4,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -118,10 +119,12 @@ static void release_owned(plgpu_column* c) {
     OwnedBuffers* ob = static_cast<OwnedBuffers*>(c->private_data);
     dev_free(ob->values, ob->stream);
     dev_free(ob->validity, ob->stream);
+    dev_free(ob->data, ob->stream);
     delete ob;
     c->private_data = nullptr;
     c->values = nullptr;
     c->validity = nullptr;
+    c->data = nullptr;
     c->release = nullptr;
 }
 
@@ -150,6 +153,24 @@ int make_owned_column(plgpu_column* out, int32_t dtype, int64_t length, bool wit
     out->release = release_owned;
     out->private_data = ob;
     return PLGPU_OK;
+}
+
+int owned_attach_data(plgpu_column* out, int64_t bytes, hipStream_t s) {
+    OwnedBuffers* ob = static_cast<OwnedBuffers*>(out->private_data);
+    if (ob == nullptr) return fail(PLGPU_ERR_INVALID, "not an owned column");
+    const int rc = dev_alloc(&ob->data, (size_t)std::max<int64_t>(bytes, 1), s);
+    if (rc != PLGPU_OK) return rc;
+    out->dtype = PLGPU_STR;
+    out->length -= 1;  // the offsets buffer holds length + 1 entries
+    out->data = (const uint8_t*)ob->data;
+    return PLGPU_OK;
+}
+
+int make_owned_string_column(plgpu_column* out, int64_t length, int64_t bytes, bool with_validity, hipStream_t s) {
+    int rc = make_owned_column(out, PLGPU_I64, length + 1, with_validity, s);
+    if (rc == PLGPU_OK) rc = owned_attach_data(out, bytes, s);
+    if (rc != PLGPU_OK) plgpu_column_release(out);
+    return rc;
 }
 
 // ------------------------------------------------------ program lowering

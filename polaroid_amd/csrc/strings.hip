@@ -1,0 +1,194 @@
+// String columns (Arrow large_string: int64 offsets + UTF-8 bytes): the
+// variable-length gather that materialises them after a join, a sort, a
+// filter or as group-by output keys.
+//
+// Reference: polars-core/src/chunked_array/ops/gather.rs (take on
+// BinaryView / Utf8View arrays) and polars-compute/src/filter (filtering the
+// same).  The reference stores strings as views; the Arrow interchange the
+// GPU executor reads and writes is large_string, so the GPU works on offsets
+// and bytes.
+//
+// MI355X design: three passes over the output rows -- lengths (+ validity
+// ballots), an exclusive scan into the output offsets, then the byte copy.
+// The copy gives every string one thread for short strings and a whole wave
+// for long ones (8-byte lane words when source and destination agree on
+// alignment), so symbol-like keys (4..16 bytes) and long payloads both
+// stream.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+
+#include "plgpu_internal.hpp"
+#include "scan.hpp"
+
+namespace plgpu {
+
+constexpr int kStrThreads = 256;
+constexpr int64_t kStrLongBytes = 256;  // strings this long are copied by a whole wave
+
+__device__ __forceinline__ bool str_idx(const uint32_t* idx32, const int64_t* idx64, const uint8_t* iv, int64_t ioff,
+                                        int64_t i, int64_t* r) {
+    if (iv != nullptr && !((iv[(ioff + i) >> 3] >> ((ioff + i) & 7)) & 1)) return false;
+    *r = idx32 ? (int64_t)idx32[i] : idx64[i];
+    return true;
+}
+
+// lens[i] = byte length of output row i (0 for a null); validity ballots.
+__global__ __launch_bounds__(kStrThreads) void str_len_kernel(DevCol src, const uint32_t* __restrict__ idx32,
+                                                              const int64_t* __restrict__ idx64,
+                                                              const uint8_t* __restrict__ iv, int64_t ioff,
+                                                              int64_t n, uint64_t* __restrict__ lens,
+                                                              uint64_t* __restrict__ out_valid) {
+    const int64_t* off = (const int64_t*)src.values;
+    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x; i0 < n; i0 += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = i0 + threadIdx.x;
+        bool valid = false;
+        uint64_t len = 0;
+        int64_t r;
+        if (i < n && str_idx(idx32, idx64, iv, ioff, i, &r) && dev_valid(src, r)) {
+            valid = true;
+            len = (uint64_t)(off[src.offset + r + 1] - off[src.offset + r]);
+        }
+        if (i < n) lens[i] = len;
+        if (out_valid) {
+            const uint64_t w = __ballot(valid);
+            if ((threadIdx.x & 63) == 0 && i < n) out_valid[i >> 6] = w;
+        }
+    }
+}
+
+__device__ __forceinline__ void copy_bytes_lane(const uint8_t* __restrict__ s, uint8_t* __restrict__ d, int64_t len,
+                                                int lane, int lanes) {
+    if ((((uintptr_t)s ^ (uintptr_t)d) & 7) == 0) {
+        // same alignment: head bytes, 8-byte words, tail bytes
+        int64_t head = (int64_t)((8 - ((uintptr_t)s & 7)) & 7);
+        if (head > len) head = len;
+        for (int64_t j = lane; j < head; j += lanes) d[j] = s[j];
+        const int64_t words = (len - head) >> 3;
+        const uint64_t* sw = (const uint64_t*)(s + head);
+        uint64_t* dw = (uint64_t*)(d + head);
+        for (int64_t j = lane; j < words; j += lanes) dw[j] = sw[j];
+        for (int64_t j = head + (words << 3) + lane; j < len; j += lanes) d[j] = s[j];
+    } else {
+        for (int64_t j = lane; j < len; j += lanes) d[j] = s[j];
+    }
+}
+
+// Short strings: one thread each.  Long ones are queued for the wave copy.
+__global__ __launch_bounds__(kStrThreads) void str_copy_kernel(DevCol src, const uint32_t* __restrict__ idx32,
+                                                               const int64_t* __restrict__ idx64,
+                                                               const uint8_t* __restrict__ iv, int64_t ioff, int64_t n,
+                                                               const uint64_t* __restrict__ out_off,
+                                                               uint8_t* __restrict__ out_data,
+                                                               int64_t* __restrict__ long_rows,
+                                                               unsigned long long* __restrict__ nlong) {
+    const int64_t* off = (const int64_t*)src.values;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t len = (int64_t)(out_off[i + 1] - out_off[i]);
+        if (len == 0) continue;
+        if (len >= kStrLongBytes) {
+            long_rows[atomicAdd(nlong, 1ull)] = i;
+            continue;
+        }
+        int64_t r;
+        (void)str_idx(idx32, idx64, iv, ioff, i, &r);
+        copy_bytes_lane(src.data + off[src.offset + r], out_data + out_off[i], len, 0, 1);
+    }
+}
+
+__global__ __launch_bounds__(kStrThreads) void str_copy_long_kernel(DevCol src, const uint32_t* __restrict__ idx32,
+                                                                    const int64_t* __restrict__ idx64,
+                                                                    const uint64_t* __restrict__ out_off,
+                                                                    uint8_t* __restrict__ out_data,
+                                                                    const int64_t* __restrict__ long_rows,
+                                                                    int64_t nlong) {
+    const int64_t* off = (const int64_t*)src.values;
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t k = wave; k < nlong; k += waves) {
+        const int64_t i = long_rows[k];
+        const int64_t r = idx32 ? (int64_t)idx32[i] : idx64[i];
+        copy_bytes_lane(src.data + off[src.offset + r], out_data + out_off[i], (int64_t)(out_off[i + 1] - out_off[i]),
+                        lane, 64);
+    }
+}
+
+static int num_cus_str() {
+    static int n = 0;
+    if (n == 0) {
+        int dev = 0;
+        hipDeviceProp_t prop;
+        n = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+                ? prop.multiProcessorCount
+                : 256;
+    }
+    return n;
+}
+
+// out = src[idx] for a PLGPU_STR column; idx is UInt32 (idx32) or Int64
+// (idx64) row ids; `iv` / `ioff`: optional index validity (a null index
+// gathers a null).  The output is library-owned.
+int str_gather(const DevCol& src, const uint32_t* idx32, const int64_t* idx64, const uint8_t* iv, int64_t ioff,
+               int64_t n, bool nullable, plgpu_column* out, hipStream_t s) {
+    int rc = make_owned_column(out, PLGPU_I64, n + 1, nullable, s);  // offsets (+ validity)
+    if (rc) return rc;
+    uint64_t* lens = nullptr;
+    uint64_t* part = nullptr;
+    int64_t* long_rows = nullptr;
+    unsigned long long* nlong = nullptr;
+    uint64_t total = 0;
+    const int g = (int)std::max<int64_t>(1, std::min<int64_t>((n + kStrThreads - 1) / kStrThreads,
+                                                              (int64_t)num_cus_str() * 16));
+    rc = dev_alloc((void**)&lens, std::max<int64_t>(n, 1) * 8, s);
+    if (!rc) rc = dev_alloc((void**)&part, ((n + kScanChunk - 1) / kScanChunk + 2) * 8, s);
+    uint64_t* out_off = (uint64_t*)out->values;
+    if (!rc) {
+        if (n > 0)
+            str_len_kernel<<<g, kStrThreads, 0, s>>>(src, idx32, idx64, iv, ioff, n, lens,
+                                                     (uint64_t*)out->validity);
+        hipError_t e = hipGetLastError();
+        if (e == hipSuccess) e = scan_exclusive<uint64_t>(lens, n, out_off, part, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(&total, out_off + n, 8, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) rc = hip_fail(e, "string gather lengths");
+    }
+    if (!rc) rc = owned_attach_data(out, (int64_t)total, s);
+    if (!rc && total > 0) {
+        rc = dev_alloc((void**)&long_rows, n * 8, s);
+        if (!rc) rc = dev_alloc((void**)&nlong, 8, s);
+        unsigned long long hl = 0;
+        hipError_t e = hipSuccess;
+        if (!rc) {
+            e = hipMemsetAsync(nlong, 0, 8, s);
+            if (e == hipSuccess) {
+                str_copy_kernel<<<g, kStrThreads, 0, s>>>(src, idx32, idx64, iv, ioff, n, out_off,
+                                                          (uint8_t*)out->data, long_rows, nlong);
+                e = hipGetLastError();
+            }
+            if (e == hipSuccess) e = hipMemcpyAsync(&hl, nlong, 8, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e == hipSuccess && hl > 0) {
+                const int gl = (int)std::min<int64_t>(((int64_t)hl * 64 + kStrThreads - 1) / kStrThreads,
+                                                      (int64_t)num_cus_str() * 16);
+                str_copy_long_kernel<<<gl, kStrThreads, 0, s>>>(src, idx32, idx64, out_off, (uint8_t*)out->data,
+                                                                long_rows, (int64_t)hl);
+                e = hipGetLastError();
+            }
+            if (e != hipSuccess) rc = hip_fail(e, "string gather copy");
+        }
+    }
+    if (!rc) {
+        hipError_t e = hipStreamSynchronize(s);
+        if (e != hipSuccess) rc = hip_fail(e, "string gather");
+    }
+    dev_free(lens, s);
+    dev_free(part, s);
+    dev_free(long_rows, s);
+    dev_free(nlong, s);
+    if (rc) plgpu_column_release(out);
+    return rc;
+}
+
+}  // namespace plgpu

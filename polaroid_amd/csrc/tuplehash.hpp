@@ -31,8 +31,41 @@ __device__ __forceinline__ uint64_t mk_fmix(uint64_t x) {
     return x;
 }
 
-// Canonical key word: f64 keys compare by TotalOrd (-0 == 0, NaN == NaN).
+// 64-bit hash of a string's bytes (8-byte little-endian words, then the
+// tail; the length is mixed in, so "" and "\0" differ).
+__device__ __forceinline__ uint64_t str_hash(const DevCol& c, int64_t r, uint64_t seed = 0) {
+    const int64_t* off = (const int64_t*)c.values;
+    const int64_t b = off[c.offset + r], len = off[c.offset + r + 1] - b;
+    const uint8_t* p = c.data + b;
+    uint64_t h = (0x9E3779B97F4A7C15ull + seed) ^ (uint64_t)len;
+    int64_t i = 0;
+    for (; i + 8 <= len; i += 8) {
+        uint64_t w = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) w |= (uint64_t)p[i + j] << (8 * j);
+        h = mk_fmix(h ^ w) + 0xD6E8FEB86659FD93ull;
+    }
+    uint64_t w = 0;
+    for (int j = 0; i + j < len; ++j) w |= (uint64_t)p[i + j] << (8 * j);
+    return mk_fmix(h ^ w ^ 0xA0761D6478BD642Full);
+}
+
+// Byte equality of row ra of string column a and row rb of b.
+__device__ __forceinline__ bool str_equal(const DevCol& a, int64_t ra, const DevCol& b, int64_t rb) {
+    const int64_t* oa = (const int64_t*)a.values;
+    const int64_t* ob = (const int64_t*)b.values;
+    const int64_t sa = oa[a.offset + ra], la = oa[a.offset + ra + 1] - sa;
+    const int64_t sb = ob[b.offset + rb], lb = ob[b.offset + rb + 1] - sb;
+    if (la != lb) return false;
+    for (int64_t i = 0; i < la; ++i)
+        if (a.data[sa + i] != b.data[sb + i]) return false;
+    return true;
+}
+
+// Canonical key word: f64 keys compare by TotalOrd (-0 == 0, NaN == NaN);
+// a string key's word is its hash (equality is checked on the bytes).
 __device__ __forceinline__ uint64_t mk_word(const DevCol& c, int64_t r) {
+    if (c.dtype == PLGPU_STR) return str_hash(c, r);
     uint64_t x = dev_load(c, r);
     if (c.dtype == PLGPU_F64) {
         if ((x & 0x7FFFFFFFFFFFFFFFull) == 0) x = 0;
@@ -45,7 +78,10 @@ __device__ __forceinline__ uint64_t mk_row_hash(const MkKeys& k, int64_t r, uint
     uint64_t h = seed;
     for (int i = 0; i < k.n; ++i) {
         const DevCol& c = k.c[i];
-        const uint64_t w = dev_valid(c, r) ? mk_fmix(mk_word(c, r) ^ seed) : 0x6A09E667F3BCC909ull + (uint64_t)i;
+        // strings hash with the seed, so a re-seed also separates two strings
+        // whose unseeded hashes collide
+        const uint64_t w = dev_valid(c, r) ? mk_fmix((c.dtype == PLGPU_STR ? str_hash(c, r, seed) : mk_word(c, r)) ^ seed)
+                                           : 0x6A09E667F3BCC909ull + (uint64_t)i;
         h = mk_fmix(h * 0x9E3779B97F4A7C15ull + w + (uint64_t)i);
     }
     return h;
@@ -62,7 +98,8 @@ __device__ __forceinline__ bool mk_equal(const MkKeys& a, int64_t ra, const MkKe
     bool eq = true;
     for (int i = 0; i < a.n; ++i) {
         const bool va = dev_valid(a.c[i], ra), vb = dev_valid(b.c[i], rb);
-        eq &= va == vb && (!va || mk_word(a.c[i], ra) == mk_word(b.c[i], rb));
+        if (a.c[i].dtype == PLGPU_STR) eq &= va == vb && (!va || str_equal(a.c[i], ra, b.c[i], rb));
+        else eq &= va == vb && (!va || mk_word(a.c[i], ra) == mk_word(b.c[i], rb));
     }
     return eq;
 }
@@ -177,7 +214,7 @@ inline int mk_plan_pack(const MkKeys& ka, int64_t na, const MkKeys* kb, int64_t 
     std::memset(pk, 0, sizeof *pk);
     pk->n = ka.n;
     for (int i = 0; i < ka.n; ++i)
-        if (ka.c[i].dtype == PLGPU_F64) return PLGPU_OK;
+        if (ka.c[i].dtype == PLGPU_F64 || ka.c[i].dtype == PLGPU_STR) return PLGPU_OK;
     if (getenv("PLGPU_NO_PACK")) return PLGPU_OK;
     unsigned long long* st = nullptr;
     const size_t bytes = 2 * 3 * kMaxKeys * 8;

@@ -49,14 +49,22 @@ class _Boolean(DataType):
     code, name, np_dtype = N.BOOL, "Boolean", np.bool_
 
 
-Int64, Int32, UInt32, Float64, Boolean = _Int64(), _Int32(), _UInt32(), _Float64(), _Boolean()
-_BY_CODE = {d.code: d for d in (Int64, Int32, UInt32, Float64, Boolean)}
+class _String(DataType):
+    """UTF-8 strings as Arrow large_string (int64 offsets + bytes)."""
+    code, name, np_dtype = N.STR, "String", np.object_
+
+
+Int64, Int32, UInt32, Float64, Boolean, String = (_Int64(), _Int32(), _UInt32(), _Float64(), _Boolean(),
+                                                  _String())
+_BY_CODE = {d.code: d for d in (Int64, Int32, UInt32, Float64, Boolean, String)}
 
 
 def _dtype_from_numpy(a: np.ndarray) -> DataType:
     k = a.dtype
     if k == np.bool_:
         return Boolean
+    if k.kind in ("U", "S", "O"):
+        return String
     if k == np.int64:
         return Int64
     if k == np.int32:
@@ -123,13 +131,15 @@ class Series:
             validity = np.array([v is not None for v in vals], dtype=bool)
             if dtype is None:
                 nonnull = [v for v in vals if v is not None]
-                if any(isinstance(v, float) for v in nonnull):
+                if nonnull and builtins.all(isinstance(v, str) for v in nonnull):
+                    dtype = String
+                elif any(isinstance(v, float) for v in nonnull):
                     dtype = Float64
                 elif nonnull and builtins.all(isinstance(v, bool) for v in nonnull):
                     dtype = Boolean
                 else:
                     dtype = Int64
-            fill = False if dtype is Boolean else 0
+            fill = False if dtype is Boolean else ("" if dtype is String else 0)
             arr = np.array([fill if v is None else v for v in vals], dtype=dtype.np_dtype)
             if validity.all():
                 validity = None
@@ -139,7 +149,42 @@ class Series:
         self._upload(np.ascontiguousarray(arr), dt, validity)
 
     # construction helpers -------------------------------------------------
+    def _upload_strings(self, arr, validity: np.ndarray | None) -> None:
+        """Strings -> large_string buffers (int64 offsets, UTF-8 bytes) in HBM."""
+        n = builtins.len(arr)
+        enc = [(x if isinstance(x, (bytes, bytearray)) else str(x).encode()) if (validity is None or validity[i])
+               else b"" for i, x in enumerate(arr)]
+        offsets = np.zeros(n + 1, np.int64)
+        if n:
+            np.cumsum([builtins.len(b) for b in enc], out=offsets[1:])
+        self._upload_string_buffers(offsets, np.frombuffer(b"".join(enc), np.uint8), validity)
+
+    def _upload_string_buffers(self, offsets: np.ndarray, data: np.ndarray, validity: np.ndarray | None) -> None:
+        n = int(offsets.shape[0]) - 1
+        col_ = N.Column()
+        col_.dtype, col_.length, col_.offset = N.STR, n, 0
+        col_.null_count = 0 if validity is None else int((~validity).sum())
+        self._keep = []
+        for field, payload in (("values", np.ascontiguousarray(offsets, np.int64)),
+                               ("data", np.ascontiguousarray(data, np.uint8))):
+            buf = N.DeviceBuffer(payload.nbytes)
+            if payload.nbytes:
+                N.check(N.lib().plgpu_memcpy_h2d(C.c_void_p(buf.ptr), payload.ctypes.data_as(C.c_void_p),
+                                                 payload.nbytes, None))
+            setattr(col_, field, buf.ptr)
+            self._keep.append(buf)
+        if validity is not None:
+            bits = _pack_bits(validity)
+            mbuf = N.DeviceBuffer(bits.nbytes)
+            N.check(N.lib().plgpu_memcpy_h2d(C.c_void_p(mbuf.ptr), bits.ctypes.data_as(C.c_void_p),
+                                             bits.nbytes, None))
+            col_.validity = mbuf.ptr
+            self._keep.append(mbuf)
+        self._col = col_
+
     def _upload(self, arr: np.ndarray, dt: DataType, validity: np.ndarray | None) -> None:
+        if dt is String:
+            return self._upload_strings(arr, validity)
         n = int(arr.shape[0])
         col_ = N.Column()
         col_.dtype = dt.code
@@ -173,6 +218,9 @@ class Series:
         s.name = name
         arr = np.ascontiguousarray(values)
         dt = dtype or _dtype_from_numpy(arr)
+        if dt is String:
+            s._upload_strings(list(arr), None if valid is None else np.asarray(valid, dtype=bool))
+            return s
         if arr.dtype != dt.np_dtype:
             arr = arr.astype(dt.np_dtype)
         s._upload(arr, dt, None if valid is None else np.asarray(valid, dtype=bool))
@@ -262,10 +310,22 @@ class Series:
         nb = (off + n + 7) // 8
         return _unpack_bits(self._download(self._col.validity, nb), off, n)
 
+    def _string_buffers(self) -> tuple[np.ndarray, np.ndarray]:
+        """(offsets of this slice rebased to 0, its bytes) on the host."""
+        n, off = self.len(), int(self._col.offset)
+        offs = self._download(self._col.values + off * 8, (n + 1) * 8).view(np.int64).copy()
+        base = int(offs[0]) if n + 1 else 0
+        data = self._download(self._col.data + base if self._col.data else 0, int(offs[-1]) - base)
+        return offs - base, data
+
     def to_numpy(self) -> np.ndarray:
         """Values as numpy (null slots hold whatever the buffer holds)."""
         n, off = self.len(), int(self._col.offset)
         dt = self.dtype
+        if dt is String:
+            offs, data = self._string_buffers()
+            raw = data.tobytes()
+            return np.array([raw[offs[i]:offs[i + 1]].decode() for i in range(n)], dtype=object)
         if dt is Boolean:
             nb = (off + n + 7) // 8
             return _unpack_bits(self._download(self._col.values, nb), off, n)
@@ -283,6 +343,19 @@ class Series:
             arr = arr.combine_chunks() if arr.num_chunks != 1 else arr.chunk(0)
         m = {pa.int64(): Int64, pa.int32(): Int32, pa.uint32(): UInt32, pa.float64(): Float64,
              pa.bool_(): Boolean}
+        if arr.type in (pa.string(), pa.large_string(), pa.utf8(), pa.large_utf8()):
+            # large_string buffers as they are (string: offsets widened to int64)
+            if arr.type in (pa.string(), pa.utf8()):
+                arr = arr.cast(pa.large_string())
+            vbuf, obuf, dbuf = arr.buffers()
+            offs = np.frombuffer(obuf, np.int64)[arr.offset: arr.offset + builtins.len(arr) + 1]
+            data = np.frombuffer(dbuf, np.uint8) if dbuf is not None else np.zeros(0, np.uint8)
+            data = data[int(offs[0]) if builtins.len(offs) else 0: int(offs[-1]) if builtins.len(offs) else 0]
+            valid = arr.is_valid().to_numpy(zero_copy_only=False) if arr.null_count else None
+            s = cls.__new__(cls)
+            s.name = name
+            s._upload_string_buffers(offs - (offs[0] if builtins.len(offs) else 0), data, valid)
+            return s
         dt = m.get(arr.type)
         if dt is None:
             raise N.InvalidOperationError(f"column {name!r}: arrow type {arr.type} is not supported on the GPU")
@@ -296,6 +369,13 @@ class Series:
     def to_arrow(self):
         import pyarrow as pa
 
+        if self.dtype is String:
+            offs, data = self._string_buffers()
+            valid = self.validity_numpy()
+            vb = None if valid.all() else pa.py_buffer(np.packbits(valid, bitorder="little").tobytes())
+            return pa.Array.from_buffers(pa.large_string(), self.len(),
+                                         [vb, pa.py_buffer(offs.tobytes()), pa.py_buffer(data.tobytes())],
+                                         null_count=int((~valid).sum()))
         t = {"Int64": pa.int64(), "Int32": pa.int32(), "UInt32": pa.uint32(), "Float64": pa.float64(),
              "Boolean": pa.bool_()}[self.dtype.name]
         vals = self.to_numpy()
@@ -739,9 +819,13 @@ def _gb_lower(df: DataFrame, key: str | tuple, aggs: list[Expr], pred: Expr | No
     key = keys[0]
     # len() needs some aggregatable column for its accumulator slot (it only
     # reads the group's row count): the first non-Boolean key, else any column
-    len_col = next((k for k in keys if df._cols[k].dtype is not Boolean), None)
+    len_col = next((k for k in keys if df._cols[k].dtype not in (Boolean, String)), None)
     if len_col is None:
-        len_col = next((c for c in df.columns if df._cols[c].dtype is not Boolean), key)
+        len_col = next((c for c in df.columns if df._cols[c].dtype not in (Boolean, String)), None)
+    if len_col is None:
+        # no numeric column at all: a zero column of the frame's height
+        len_col = "__len"
+        df = DataFrame(list(df._cols.values()) + [Series.from_numpy("__len", np.zeros(df.height, np.int64))])
     specs: list[tuple[str, str]] = []  # (kind, column)
     out_names: list[str] = []
     for e in aggs:

@@ -1,0 +1,175 @@
+"""String columns (Arrow large_string in HBM): upload / download and Arrow
+interchange, filter and gather of string payloads, and string keys in
+group-by and every join type.  Checked against the oracle with the strings
+replaced by dense ids (equality is all the reference's hash paths look at:
+polars-core/src/chunked_array/ops/row_encode.rs encodes the bytes), and the
+output strings against the original strings of the rows the oracle names.
+Bar: exact strings, exact index sequences / aggregates."""
+
+import numpy as np
+import pytest
+
+import polaroid_amd as pl
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _words(rng, n, card, null_frac=0.05, long_frac=0.0):
+    pool = ["", "a", "AAPL", "MSFT", "BRK.B", "é", "日本", "x" * 9, "y" * 17] + [f"sym{i:05d}" for i in range(card)]
+    pool = pool[: max(card, 1)]
+    idx = rng.integers(0, len(pool), n)
+    vals = np.array([pool[i] for i in idx], dtype=object)
+    if long_frac:
+        for i in np.nonzero(rng.random(n) < long_frac)[0]:
+            vals[i] = ("long-" + pool[idx[i]]) * 40  # > 256 bytes: the wave copy path
+    valid = rng.random(n) >= null_frac
+    return vals, valid
+
+
+def _ids(*arrays_valid):
+    """Dense ids of the strings over all arrays (shared dictionary)."""
+    allv = np.concatenate([v for v, _ in arrays_valid]) if arrays_valid else np.zeros(0, object)
+    uniq = {s: i for i, s in enumerate(sorted(set(allv.tolist())))}
+    return [np.array([uniq[s] for s in v], dtype=np.int64) for v, _ in arrays_valid]
+
+
+def test_string_roundtrip_and_arrow(gpu):
+    import pyarrow as pa
+
+    vals = ["AAPL", None, "", "日本語", "x" * 300, "a\x00b"]
+    s = pl.Series("s", vals)
+    assert s.dtype == pl.String and s.len() == 6
+    assert s.to_list() == vals
+    assert s.slice(1, 4).to_list() == vals[1:5]
+    arr = pa.array(vals, type=pa.string())
+    for a in (arr, arr.cast(pa.large_string()), arr.slice(2, 3)):
+        t = pl.Series.from_arrow("t", a)
+        assert t.to_list() == a.to_pylist()
+        back = t.to_arrow()
+        assert back.type == pa.large_string() and back.to_pylist() == a.to_pylist()
+    df = pl.DataFrame.from_arrow(pa.table({"k": arr, "v": pa.array(np.arange(6, dtype=np.int64))}))
+    assert df["k"].to_list() == vals
+
+
+@pytest.mark.parametrize("n", [0, 1, 5000, 300_001])
+def test_filter_and_gather_strings(gpu, n):
+    rng = np.random.default_rng(n)
+    w, wv = _words(rng, n, 50, long_frac=0.01)
+    x = rng.standard_normal(n)
+    df = pl.DataFrame({"w": pl.Series.from_numpy("w", w, wv), "x": pl.Series.from_numpy("x", x)})
+    out = df.filter(pl.col("x") > 0.3)
+    sel = x > 0.3
+    assert out["w"].to_list() == [s if ok else None for s, ok in zip(w[sel], wv[sel])]
+    # sort materialises every column by a gather
+    srt = df.sort("x")
+    order = np.argsort(x, kind="stable")
+    assert srt["w"].to_list() == [s if ok else None for s, ok in zip(w[order], wv[order])]
+
+
+@pytest.mark.parametrize("n,card", [(1, 1), (1000, 7), (200_003, 60), (300_001, 5000)])
+@pytest.mark.parametrize("maintain_order", [False, True])
+def test_group_by_string_key(gpu, n, card, maintain_order):
+    rng = np.random.default_rng(n + card)
+    w, wv = _words(rng, n, card)
+    v = rng.standard_normal(n)
+    df = pl.DataFrame({"w": pl.Series.from_numpy("w", w, wv), "v": pl.Series.from_numpy("v", v)})
+    out = df.group_by("w", maintain_order=maintain_order).agg(pl.col("v").sum(), pl.col("v").first().alias("f"),
+                                                              pl.len())
+    (ids,) = _ids((w, wv))
+    okeys, outs = O.group_by_agg_multi([(ids, wv)], [O.HostCol(v)], None, [("sum", 0), ("first", 0), ("len", 0)], n)
+    kid, kval = okeys[0]
+    names = {}
+    for i, ok in zip(kid.tolist(), kval.tolist()):
+        names[len(names)] = None if not ok else w[np.nonzero(ids == i)[0][0]]
+    exp_keys = [names[g] for g in range(len(names))]
+    got_keys = out["w"].to_list()
+    assert out["w"].dtype == pl.String
+    if maintain_order:
+        assert got_keys == exp_keys
+        order = list(range(len(exp_keys)))
+    else:
+        assert sorted(got_keys, key=lambda s: (s is None, s or "")) == sorted(exp_keys, key=lambda s: (s is None, s or ""))
+        pos = {k: i for i, k in enumerate(got_keys)}
+        order = [pos[k] for k in exp_keys]
+    for nm, (vals, valid) in zip(["v", "f", "len"], outs):
+        g = out[nm].to_numpy()[order]
+        assert np.array_equal(out[nm].validity_numpy()[order], valid), nm
+        if vals.dtype == np.float64:
+            assert np.array_equal(g[valid].view(np.uint64), vals[valid].view(np.uint64)), nm
+        else:
+            assert np.array_equal(g[valid].astype(np.int64), vals[valid].astype(np.int64)), nm
+
+
+@pytest.mark.parametrize("how", ["inner", "left", "right", "full", "semi", "anti"])
+@pytest.mark.parametrize("nl,nr,card", [(0, 10, 5), (2000, 300, 40), (100_003, 20_000, 3000)])
+@pytest.mark.parametrize("nulls_equal", [False, True])
+def test_join_string_key(gpu, how, nl, nr, card, nulls_equal):
+    rng = np.random.default_rng(nl + nr + card + len(how))
+    lw, lv = _words(rng, nl, card)
+    rw, rv = _words(rng, nr, card, long_frac=0.02)
+    lid, rid = _ids((lw, lv), (rw, rv))
+    left = pl.DataFrame({"k": pl.Series.from_numpy("k", lw, lv), "li": pl.Series.from_numpy("li", np.arange(nl))})
+    right = pl.DataFrame({"k": pl.Series.from_numpy("k", rw, rv), "ri": pl.Series.from_numpy("ri", np.arange(nr)),
+                          "p": pl.Series.from_numpy("p", rw, rv)})
+    for order in ("none", "left_right", "right_left"):
+        ol, orr = O.join(O.HostCol(lid, lv), O.HostCol(rid, rv), how, nulls_equal, order)
+        out = left.join(right, on="k", how=how, nulls_equal=nulls_equal, maintain_order=order)
+
+        def idx(name):
+            s = out[name]
+            return np.where(s.validity_numpy(), s.to_numpy().astype(np.int64), -1)
+
+        gl = idx("li")
+        if how in ("semi", "anti"):
+            assert np.array_equal(gl, ol)
+            assert out["k"].to_list() == [lw[i] if lv[i] else None for i in ol]
+            continue
+        gr = idx("ri")
+        if order == "none" and how in ("inner", "full"):  # unspecified order: multisets
+            a, b = np.lexsort((gr, gl)), np.lexsort((orr, ol))
+            gl, gr, ol, orr, perm = gl[a], gr[a], ol[b], orr[b], a
+        else:
+            perm = np.arange(gl.size)
+        assert np.array_equal(gl, ol) and np.array_equal(gr, orr)
+        # the right payload strings follow the right index (null where none)
+        p = np.array(out["p"].to_list(), dtype=object)[perm]
+        assert p.tolist() == [rw[j] if j >= 0 and rv[j] else None for j in orr]
+
+
+def test_multi_key_with_string(gpu, monkeypatch):
+    rng = np.random.default_rng(5)
+    n, m = 50_000, 8000
+    lw, lv = _words(rng, n, 30)
+    rw, rv = _words(rng, m, 30)
+    la, ra = rng.integers(0, 5, n), rng.integers(0, 5, m)
+    lid, rid = _ids((lw, lv), (rw, rv))
+    left = pl.DataFrame({"w": pl.Series.from_numpy("w", lw, lv), "a": pl.Series.from_numpy("a", la),
+                         "li": pl.Series.from_numpy("li", np.arange(n))})
+    right = pl.DataFrame({"w": pl.Series.from_numpy("w", rw, rv), "a": pl.Series.from_numpy("a", ra),
+                          "ri": pl.Series.from_numpy("ri", np.arange(m))})
+    out = left.join(right, on=["w", "a"], how="left", maintain_order="left_right")
+    ol, orr = O.join_multi([(lid, lv), (la, None)], [(rid, rv), (ra, None)], "left", False, "left_right")
+    ri = out["ri"]
+    assert np.array_equal(out["li"].to_numpy(), ol)
+    assert np.array_equal(np.where(ri.validity_numpy(), ri.to_numpy(), -1), orr)
+    g = left.group_by("w", "a", maintain_order=True).agg(pl.len())
+    okeys, outs = O.group_by_agg_multi([(lid, lv), (la, None)], [O.HostCol(la)], None, [("len", 0)], n)
+    assert np.array_equal(g["a"].to_numpy(), okeys[1][0])
+    assert np.array_equal(g["len"].to_numpy(), outs[0][0])
+    # collisions forced: byte-exact verification must catch them
+    monkeypatch.setenv("PLGPU_MK_COLLIDE", "1")
+    g2 = left.group_by("w", "a", maintain_order=True).agg(pl.len())
+    assert g2["w"].to_list() == g["w"].to_list() and np.array_equal(g2["len"].to_numpy(), g["len"].to_numpy())
+    out2 = left.join(right, on=["w", "a"], how="left", maintain_order="left_right")
+    assert np.array_equal(out2["li"].to_numpy(), ol)
+
+
+def test_string_errors(gpu):
+    df = pl.DataFrame({"w": pl.Series("w", ["a", "b"]), "v": pl.Series("v", [1.0, 2.0])})
+    with pytest.raises(pl.PolaroidError):
+        df.group_by("v").agg(pl.col("w").sum())
+    with pytest.raises(pl.PolaroidError):
+        df.filter(pl.col("w") > 1)
+    with pytest.raises(pl.PolaroidError):
+        df.sort("w")
