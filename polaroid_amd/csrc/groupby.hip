@@ -2753,6 +2753,46 @@ PLGPU_API int plgpu_group_by_agg_multi(const plgpu_column* keys, int32_t nkeys, 
         mk.c[i] = to_dev(keys[i]);
     }
     hipStream_t s = as_stream(stream);
+    {
+        // String keys whose strings are all <= 7 bytes: exact Int64 codes,
+        // grouped as integer keys; the output codes turn back into strings
+        bool any_str = false, short_all = true;
+        plgpu_column ck[kMaxKeys];
+        std::memset(ck, 0, sizeof ck);
+        int rc = PLGPU_OK;
+        for (int i = 0; i < nkeys; ++i) {
+            ck[i] = keys[i];
+            if (keys[i].dtype != PLGPU_STR || !short_all || rc) continue;
+            any_str = true;
+            bool sh = false;
+            rc = str_short_codes(keys[i], &ck[i], &sh, s);
+            short_all = short_all && sh;
+        }
+        if (any_str && !rc && short_all) {
+            // one key: the single-key group-by takes the Int64 codes (and
+            // their validity) directly, no tuple packing pass
+            if (nkeys == 1)
+                rc = plgpu_group_by_agg(&ck[0], cols, ncols, program, n_instr, aggs, naggs, maintain_order,
+                                        &out_keys[0], out_aggs, info, stream);
+            else
+                rc = plgpu_group_by_agg_multi(ck, nkeys, cols, ncols, program, n_instr, aggs, naggs, maintain_order,
+                                              out_keys, out_aggs, info, stream);
+            for (int i = 0; i < nkeys && !rc; ++i) {
+                if (keys[i].dtype != PLGPU_STR) continue;
+                plgpu_column strs;
+                rc = str_from_codes(out_keys[i], &strs, s);
+                plgpu_column_release(&out_keys[i]);
+                if (!rc) out_keys[i] = strs;
+            }
+            if (rc) {
+                for (int i = 0; i < nkeys; ++i) plgpu_column_release(&out_keys[i]);
+                for (int i = 0; i < naggs && out_aggs; ++i) plgpu_column_release(&out_aggs[i]);
+            }
+        }
+        for (int i = 0; i < nkeys; ++i)
+            if (keys[i].dtype == PLGPU_STR && ck[i].dtype == PLGPU_I64) str_codes_free(&ck[i], s);
+        if (rc || (any_str && short_all)) return rc;
+    }
     const int hg = (int)std::min<int64_t>((n + 255) / 256, (int64_t)num_cus() * 16);
     {
         // integer keys whose ranges fit 63 bits together: one exact packed

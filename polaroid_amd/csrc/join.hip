@@ -1538,6 +1538,33 @@ PLGPU_API int plgpu_join_multi(const plgpu_column* left_keys, const plgpu_column
         kb.c[i] = as_dev(&right_keys[i]);
     }
     if (nl >= 0xFFFFFFFFll || nr >= 0xFFFFFFFFll) return fail(PLGPU_ERR_CAPACITY, "join side exceeds the u32 index space");
+    {
+        // String keys whose strings are all <= 7 bytes on both sides: exact
+        // Int64 codes, joined as integer keys (no byte verification)
+        bool any_str = false, short_all = true;
+        plgpu_column cl[kMaxKeys], cr[kMaxKeys];
+        std::memset(cl, 0, sizeof cl);
+        std::memset(cr, 0, sizeof cr);
+        int rc = PLGPU_OK;
+        for (int i = 0; i < nkeys; ++i) {
+            cl[i] = left_keys[i];
+            cr[i] = right_keys[i];
+            if (left_keys[i].dtype != PLGPU_STR || !short_all || rc) continue;
+            any_str = true;
+            bool a = false, b = false;
+            rc = str_short_codes(left_keys[i], &cl[i], &a, s);
+            if (!rc) rc = str_short_codes(right_keys[i], &cr[i], &b, s);
+            short_all = short_all && a && b;
+        }
+        if (any_str && !rc && short_all)
+            rc = plgpu_join_multi(cl, cr, nkeys, how, nulls_equal, maintain_order, validate, out_left_idx,
+                                  out_right_idx, stream);
+        for (int i = 0; i < nkeys; ++i) {
+            if (left_keys[i].dtype == PLGPU_STR && cl[i].dtype == PLGPU_I64) str_codes_free(&cl[i], s);
+            if (right_keys[i].dtype == PLGPU_STR && cr[i].dtype == PLGPU_I64) str_codes_free(&cr[i], s);
+        }
+        if (rc || (any_str && short_all)) return rc;
+    }
     const bool neq = nulls_equal != 0;
     const int cus = num_cus_jn();
     {

@@ -85,6 +85,13 @@ int owned_attach_data(plgpu_column* out, int64_t bytes, hipStream_t s);
 // iv / ioff optional index validity (a null index gathers a null).
 int str_gather(const DevCol& src, const uint32_t* idx32, const int64_t* idx64, const uint8_t* iv, int64_t ioff,
                int64_t n, bool nullable, plgpu_column* out, hipStream_t s);
+// Short-string key codes (strings.hip): a borrowed-style I64 column over
+// codes[(length << 56) | bytes] sharing the strings' validity / offset, or
+// *all_short = false when some string is longer than 7 bytes.  Free with
+// str_codes_free.  str_from_codes turns a code column back into strings.
+int str_short_codes(const plgpu_column& src, plgpu_column* out, bool* all_short, hipStream_t s);
+void str_codes_free(plgpu_column* c, hipStream_t s);
+int str_from_codes(const plgpu_column& codes, plgpu_column* out, hipStream_t s);
 
 // Lowered (typed) program: the host resolves every operand type, inserts
 // casts, and emits one micro-op per step so the device interpreter does no

@@ -191,4 +191,152 @@ int str_gather(const DevCol& src, const uint32_t* idx32, const int64_t* idx64, c
     return rc;
 }
 
+// ------------------------------------------------ short-string key codes
+// A string of at most 7 bytes is encoded exactly and injectively as one
+// integer: (length << 56) | bytes (little-endian).  A key column whose
+// strings are all that short is then grouped / joined as an Int64 column --
+// exact, with no hashing, no byte verification and no collision path
+// (symbols, tickers, country codes).  *any_long reports a longer string.
+// `words`: the data buffer is 8-byte aligned and `data_end` (= the last
+// offset) bounds the aligned 8-byte word loads, so a string's bytes come in
+// one or two word loads and a funnel shift instead of byte loads.
+__global__ __launch_bounds__(kStrThreads) void str_code_kernel(DevCol src, int64_t n, uint64_t* __restrict__ codes,
+                                                               unsigned long long* __restrict__ any_long,
+                                                               bool words, int64_t data_end) {
+    const int64_t* off = (const int64_t*)src.values;
+    const uint64_t* dw = (const uint64_t*)src.data;
+    bool lng = false;
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t code = 0;
+        if (dev_valid(src, r)) {
+            const int64_t b = off[src.offset + r], len = off[src.offset + r + 1] - b;
+            if (len > 7) {
+                lng = true;
+            } else if (len > 0) {
+                const int64_t w = b >> 3;
+                const int sh = (int)(b & 7) * 8;
+                uint64_t x;
+                if (words && (w + 1) * 8 <= data_end && (sh + 8 * len <= 64 || (w + 2) * 8 <= data_end)) {
+                    const uint64_t lo = dw[w];
+                    x = lo >> sh;
+                    if (sh + 8 * len > 64) x |= dw[w + 1] << (64 - sh);
+                } else {
+                    x = 0;
+                    for (int j = 0; j < len; ++j) x |= (uint64_t)src.data[b + j] << (8 * j);
+                }
+                code = ((uint64_t)len << 56) | (x & ((1ull << (8 * len)) - 1));
+            }
+        }
+        codes[r] = code;
+    }
+    if (__any(lng) && (threadIdx.x & 63) == 0) atomicOr(any_long, 1ull);
+}
+
+// Codes -> strings: lengths, scan, bytes.
+__global__ __launch_bounds__(kStrThreads) void str_code_len_kernel(DevCol codes, int64_t n, uint64_t* __restrict__ lens,
+                                                                   uint64_t* __restrict__ out_valid) {
+    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x; i0 < n; i0 += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = i0 + threadIdx.x;
+        const bool v = i < n && dev_valid(codes, i);
+        if (i < n) lens[i] = v ? (dev_load(codes, i) >> 56) : 0;
+        if (out_valid) {
+            const uint64_t w = __ballot(v);
+            if ((threadIdx.x & 63) == 0 && i < n) out_valid[i >> 6] = w;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kStrThreads) void str_code_bytes_kernel(DevCol codes, int64_t n,
+                                                                     const uint64_t* __restrict__ out_off,
+                                                                     uint8_t* __restrict__ out_data) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t len = (int64_t)(out_off[i + 1] - out_off[i]);
+        if (len == 0) continue;
+        const uint64_t c = dev_load(codes, i);
+        for (int j = 0; j < len; ++j) out_data[out_off[i] + j] = (uint8_t)(c >> (8 * j));
+    }
+}
+
+int str_short_codes(const plgpu_column& src, plgpu_column* out, bool* all_short, hipStream_t s) {
+    const int64_t n = src.length;
+    std::memset(out, 0, sizeof *out);
+    uint64_t* codes = nullptr;
+    unsigned long long* flag = nullptr;
+    int rc = dev_alloc((void**)&codes, std::max<int64_t>(n, 1) * 8, s);
+    if (!rc) rc = dev_alloc((void**)&flag, 8, s);
+    unsigned long long hf = 0;
+    if (!rc) {
+        int64_t data_end = 0;
+        hipError_t e = hipMemsetAsync(flag, 0, 8, s);
+        if (e == hipSuccess && n > 0)
+            e = hipMemcpyAsync(&data_end, (const int64_t*)src.values + src.offset + n, 8, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e == hipSuccess && n > 0) {
+            const int g = (int)std::min<int64_t>((n + kStrThreads - 1) / kStrThreads, (int64_t)num_cus_str() * 16);
+            const bool words = ((uintptr_t)src.data & 7) == 0;
+            str_code_kernel<<<g, kStrThreads, 0, s>>>(dev_col(src), n, codes, flag, words, data_end);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) e = hipMemcpyAsync(&hf, flag, 8, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) rc = hip_fail(e, "short-string codes");
+    }
+    dev_free(flag, s);
+    if (rc) {
+        dev_free(codes, s);
+        return rc;
+    }
+    *all_short = hf == 0;
+    // same validity bitmap and offset as the strings: values[offset + r] is
+    // the code of row r
+    out->dtype = PLGPU_I64;
+    out->length = n;
+    out->offset = src.offset;
+    out->null_count = src.null_count;
+    out->validity = src.validity;
+    out->values = codes - src.offset;
+    out->private_data = codes;  // the allocation (free with str_codes_free)
+    return PLGPU_OK;
+}
+
+void str_codes_free(plgpu_column* c, hipStream_t s) {
+    if (c && c->private_data) dev_free(c->private_data, s);
+    if (c) std::memset(c, 0, sizeof *c);
+}
+
+int str_from_codes(const plgpu_column& codes, plgpu_column* out, hipStream_t s) {
+    const int64_t n = codes.length;
+    const bool nullable = codes.validity != nullptr;
+    int rc = make_owned_column(out, PLGPU_I64, n + 1, nullable, s);
+    if (rc) return rc;
+    uint64_t* lens = nullptr;
+    uint64_t* part = nullptr;
+    uint64_t total = 0;
+    const int g = (int)std::max<int64_t>(1, std::min<int64_t>((n + kStrThreads - 1) / kStrThreads,
+                                                              (int64_t)num_cus_str() * 16));
+    const DevCol dc = dev_col(codes);
+    rc = dev_alloc((void**)&lens, std::max<int64_t>(n, 1) * 8, s);
+    if (!rc) rc = dev_alloc((void**)&part, ((n + kScanChunk - 1) / kScanChunk + 2) * 8, s);
+    uint64_t* out_off = (uint64_t*)out->values;
+    if (!rc) {
+        if (n > 0) str_code_len_kernel<<<g, kStrThreads, 0, s>>>(dc, n, lens, (uint64_t*)out->validity);
+        hipError_t e = hipGetLastError();
+        if (e == hipSuccess) e = scan_exclusive<uint64_t>(lens, n, out_off, part, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(&total, out_off + n, 8, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) rc = hip_fail(e, "codes to strings");
+    }
+    if (!rc) rc = owned_attach_data(out, (int64_t)total, s);
+    if (!rc && total > 0) {
+        str_code_bytes_kernel<<<g, kStrThreads, 0, s>>>(dc, n, out_off, (uint8_t*)out->data);
+        hipError_t e = hipGetLastError();
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) rc = hip_fail(e, "codes to strings");
+    }
+    dev_free(lens, s);
+    dev_free(part, s);
+    if (rc) plgpu_column_release(out);
+    return rc;
+}
+
 }  // namespace plgpu

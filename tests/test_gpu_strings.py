@@ -15,9 +15,14 @@ from oracle import oracle as O
 pytestmark = pytest.mark.gpu
 
 
-def _words(rng, n, card, null_frac=0.05, long_frac=0.0):
-    pool = ["", "a", "AAPL", "MSFT", "BRK.B", "é", "日本", "x" * 9, "y" * 17] + [f"sym{i:05d}" for i in range(card)]
-    pool = pool[: max(card, 1)]
+def _words(rng, n, card, null_frac=0.05, long_frac=0.0, short=False):
+    """`short`: every string <= 7 bytes (the exact integer-code path);
+    otherwise some keys are longer (the hashed path with byte checks)."""
+    if short:
+        pool = ["", "a", "AAPL", "MSFT", "BRK.B", "é", "日本", "\x00"] + [f"s{i:05d}" for i in range(card)]
+    else:
+        pool = ["", "a", "AAPL", "MSFT", "BRK.B", "é", "日本", "x" * 9, "y" * 17] + [f"sym{i:05d}" for i in range(card)]
+    pool = pool[: max(card, 1)] if not short else pool[: max(card, 8)]
     idx = rng.integers(0, len(pool), n)
     vals = np.array([pool[i] for i in idx], dtype=object)
     if long_frac:
@@ -69,9 +74,10 @@ def test_filter_and_gather_strings(gpu, n):
 
 @pytest.mark.parametrize("n,card", [(1, 1), (1000, 7), (200_003, 60), (300_001, 5000)])
 @pytest.mark.parametrize("maintain_order", [False, True])
-def test_group_by_string_key(gpu, n, card, maintain_order):
+@pytest.mark.parametrize("short", [False, True])
+def test_group_by_string_key(gpu, n, card, maintain_order, short):
     rng = np.random.default_rng(n + card)
-    w, wv = _words(rng, n, card)
+    w, wv = _words(rng, n, card, short=short)
     v = rng.standard_normal(n)
     df = pl.DataFrame({"w": pl.Series.from_numpy("w", w, wv), "v": pl.Series.from_numpy("v", v)})
     out = df.group_by("w", maintain_order=maintain_order).agg(pl.col("v").sum(), pl.col("v").first().alias("f"),
@@ -104,10 +110,11 @@ def test_group_by_string_key(gpu, n, card, maintain_order):
 @pytest.mark.parametrize("how", ["inner", "left", "right", "full", "semi", "anti"])
 @pytest.mark.parametrize("nl,nr,card", [(0, 10, 5), (2000, 300, 40), (100_003, 20_000, 3000)])
 @pytest.mark.parametrize("nulls_equal", [False, True])
-def test_join_string_key(gpu, how, nl, nr, card, nulls_equal):
+@pytest.mark.parametrize("short", [False, True])
+def test_join_string_key(gpu, how, nl, nr, card, nulls_equal, short):
     rng = np.random.default_rng(nl + nr + card + len(how))
-    lw, lv = _words(rng, nl, card)
-    rw, rv = _words(rng, nr, card, long_frac=0.02)
+    lw, lv = _words(rng, nl, card, short=short)
+    rw, rv = _words(rng, nr, card, long_frac=0.0 if short else 0.02, short=short)
     lid, rid = _ids((lw, lv), (rw, rv))
     left = pl.DataFrame({"k": pl.Series.from_numpy("k", lw, lv), "li": pl.Series.from_numpy("li", np.arange(nl))})
     right = pl.DataFrame({"k": pl.Series.from_numpy("k", rw, rv), "ri": pl.Series.from_numpy("ri", np.arange(nr)),
@@ -142,6 +149,17 @@ def test_multi_key_with_string(gpu, monkeypatch):
     n, m = 50_000, 8000
     lw, lv = _words(rng, n, 30)
     rw, rv = _words(rng, m, 30)
+    sw, sv = _words(rng, n, 30, short=True)  # a short-string key next to an integer key
+    sa = rng.integers(0, 5, n)
+    (sid,) = _ids((sw, sv))
+    sdf = pl.DataFrame({"w": pl.Series.from_numpy("w", sw, sv), "a": pl.Series.from_numpy("a", sa)})
+    sg = sdf.group_by("w", "a", maintain_order=True).agg(pl.len())
+    okeys, outs = O.group_by_agg_multi([(sid, sv), (sa, None)], [O.HostCol(sa)], None, [("len", 0)], n)
+    first = {}
+    for r, (i, ok) in enumerate(zip(sid.tolist(), sv.tolist())):
+        first.setdefault((i if ok else None), sw[r] if ok else None)
+    assert sg["w"].to_list() == [first[i if ok else None] for i, ok in zip(okeys[0][0].tolist(), okeys[0][1].tolist())]
+    assert np.array_equal(sg["len"].to_numpy(), outs[0][0])
     la, ra = rng.integers(0, 5, n), rng.integers(0, 5, m)
     lid, rid = _ids((lw, lv), (rw, rv))
     left = pl.DataFrame({"w": pl.Series.from_numpy("w", lw, lv), "a": pl.Series.from_numpy("a", la),
