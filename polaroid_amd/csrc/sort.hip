@@ -276,6 +276,52 @@ __global__ void srt_perm_codes_kernel(DevCol c, int64_t n, bool descending, cons
     }
 }
 
+// String sort keys (polars orders strings by their UTF-8 bytes): the key of
+// a string is the tuple (8-byte chunk 0, chunk 1, ..., length) with chunks
+// big-endian and zero-padded -- a proper prefix sorts first through the
+// length.  LSD over the tuple: the length pass, then the chunks from last
+// to first, each a stable radix sort of one u64 code per row.
+// part < 0: the length; part = k: chunk k.  Null rows get code 0 (placed by
+// the null pass afterwards, their order kept).
+__global__ void srt_str_codes_kernel(DevCol c, int64_t n, bool descending, int part,
+                                     const uint32_t* __restrict__ perm, uint64_t* __restrict__ keys) {
+    const int64_t* off = (const int64_t*)c.values;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = perm[i];
+        uint64_t k = 0;
+        if (dev_valid(c, r)) {
+            const int64_t b = off[c.offset + r], len = off[c.offset + r + 1] - b;
+            if (part < 0) {
+                k = (uint64_t)len;
+            } else {
+                const int64_t lo = (int64_t)part * 8;
+                for (int j = 0; j < 8; ++j) {
+                    const uint64_t byte = lo + j < len ? c.data[b + lo + j] : 0u;
+                    k |= byte << (56 - 8 * j);
+                }
+            }
+            if (descending) k = ~k;
+        }
+        keys[i] = k;
+    }
+}
+
+__global__ void srt_str_maxlen_kernel(DevCol c, int64_t n, unsigned long long* __restrict__ mx) {
+    const int64_t* off = (const int64_t*)c.values;
+    uint64_t m = 0;
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x)
+        if (dev_valid(c, r)) {
+            const uint64_t len = (uint64_t)(off[c.offset + r + 1] - off[c.offset + r]);
+            m = len > m ? len : m;
+        }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const uint64_t y = __shfl_xor(m, o, 64);
+        m = y > m ? y : m;
+    }
+    if ((threadIdx.x & 63) == 0 && m) atomicMax(mx, (unsigned long long)m);
+}
+
 // Null placement of column c as a one-byte code: 0 sorts first.
 __global__ void srt_null_codes_kernel(DevCol c, int64_t n, bool nulls_last, const uint32_t* __restrict__ perm,
                                       uint64_t* __restrict__ keys) {
@@ -493,8 +539,9 @@ PLGPU_API int plgpu_arg_sort_multi(const plgpu_column* keys_in, int32_t nkeys, c
     const int64_t n = keys_in[0].length;
     for (int j = 0; j < nkeys; ++j) {
         const int32_t dt = keys_in[j].dtype;
-        if (dt != PLGPU_I64 && dt != PLGPU_I32 && dt != PLGPU_U32 && dt != PLGPU_F64 && dt != PLGPU_BOOL)
-            return fail(PLGPU_ERR_SCHEMA, "sort keys must be Int64 / Int32 / UInt32 / Float64 / Boolean");
+        if (dt != PLGPU_I64 && dt != PLGPU_I32 && dt != PLGPU_U32 && dt != PLGPU_F64 && dt != PLGPU_BOOL &&
+            dt != PLGPU_STR)
+            return fail(PLGPU_ERR_SCHEMA, "sort keys must be Int64 / Int32 / UInt32 / Float64 / Boolean / String");
         if (keys_in[j].length != n) return fail(PLGPU_ERR_SHAPE, "sort columns must have equal lengths");
     }
     if (n >= 0xFFFFFFFFll) return fail(PLGPU_ERR_CAPACITY, "sort input exceeds the u32 index space");
@@ -515,20 +562,37 @@ PLGPU_API int plgpu_arg_sort_multi(const plgpu_column* keys_in, int32_t nkeys, c
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) rc = hip_fail(e, "sort iota");
     }
+    unsigned long long* maxlen = nullptr;
     for (int j = nkeys - 1; j >= 0 && !rc; --j) {
-        DevCol c;
-        std::memset(&c, 0, sizeof c);
-        c.dtype = keys_in[j].dtype;
-        c.offset = keys_in[j].offset;
-        c.values = keys_in[j].values;
-        c.validity = keys_in[j].validity;
-        srt_perm_codes_kernel<<<g, 256, 0, s>>>(c, n, descending[j] != 0, idx[cur], keys[cur]);
-        hipError_t e = hipGetLastError();
+        const DevCol c = dev_col(keys_in[j]);
+        hipError_t e = hipSuccess;
+        if (c.dtype == PLGPU_STR) {
+            unsigned long long ml = 0;
+            if (maxlen == nullptr && (rc = dev_alloc((void**)&maxlen, 8, s))) break;
+            e = hipMemsetAsync(maxlen, 0, 8, s);
+            if (e == hipSuccess) {
+                srt_str_maxlen_kernel<<<g, 256, 0, s>>>(c, n, maxlen);
+                e = hipGetLastError();
+            }
+            if (e == hipSuccess) e = hipMemcpyAsync(&ml, maxlen, 8, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            const int chunks = (int)((ml + 7) / 8);
+            for (int part = -1; part < chunks && e == hipSuccess && !rc; ++part) {
+                // LSD order: the length first, then the chunks from the last
+                const int pk = part < 0 ? -1 : chunks - 1 - part;
+                srt_str_codes_kernel<<<g, 256, 0, s>>>(c, n, descending[j] != 0, pk, idx[cur], keys[cur]);
+                e = hipGetLastError();
+                if (e == hipSuccess) rc = radix_passes(keys, idx, n, cur, sc, s);
+            }
+        } else {
+            srt_perm_codes_kernel<<<g, 256, 0, s>>>(c, n, descending[j] != 0, idx[cur], keys[cur]);
+            e = hipGetLastError();
+            if (e == hipSuccess) rc = radix_passes(keys, idx, n, cur, sc, s);
+        }
         if (e != hipSuccess) {
             rc = hip_fail(e, "sort codes");
             break;
         }
-        rc = radix_passes(keys, idx, n, cur, sc, s);
         if (!rc && c.validity && keys_in[j].null_count != 0) {
             srt_null_codes_kernel<<<g, 256, 0, s>>>(c, n, nulls_last[j] != 0, idx[cur], keys[cur]);
             e = hipGetLastError();
@@ -542,6 +606,7 @@ PLGPU_API int plgpu_arg_sort_multi(const plgpu_column* keys_in, int32_t nkeys, c
         if (e != hipSuccess) rc = hip_fail(e, "sort output");
     }
     sc.release(s);
+    dev_free(maxlen, s);
     for (int i = 0; i < 2; ++i) {
         dev_free(keys[i], s);
         dev_free(idx[i], s);

@@ -396,7 +396,12 @@ class Series:
     # sort / rolling (Series.arg_sort, Series.sort, Series.rolling_*) ---------
     def arg_sort(self, *, descending: bool = False, nulls_last: bool = False) -> "Series":
         out = N.Column()
-        N.check(N.lib().plgpu_arg_sort(C.byref(self._col), int(descending), int(nulls_last), C.byref(out), None))
+        if self.dtype in (Boolean, String):  # the multi-column sort handles these key types
+            N.check(N.lib().plgpu_arg_sort_multi((N.Column * 1)(self._col), 1, (C.c_int32 * 1)(int(descending)),
+                                                 (C.c_int32 * 1)(int(nulls_last)), C.byref(out), None))
+        else:
+            N.check(N.lib().plgpu_arg_sort(C.byref(self._col), int(descending), int(nulls_last), C.byref(out),
+                                           None))
         return Series._from_native(self.name, out)
 
     def gather(self, idx: "Series") -> "Series":
@@ -985,7 +990,7 @@ def _sort(df: DataFrame, by: str | tuple, descending: bool | tuple, nulls_last: 
     for nm in names:
         if nm not in df._cols:
             raise N.ComputeError(f'unable to find column "{nm}"; valid columns: {df.columns}')
-    if builtins.len(names) == 1 and df._cols[names[0]].dtype is not Boolean:
+    if builtins.len(names) == 1 and df._cols[names[0]].dtype not in (Boolean, String):
         idx = df._cols[names[0]].arg_sort(descending=bool(descending), nulls_last=bool(nulls_last))
     else:
         k = builtins.len(names)

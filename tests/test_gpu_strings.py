@@ -189,5 +189,30 @@ def test_string_errors(gpu):
         df.group_by("v").agg(pl.col("w").sum())
     with pytest.raises(pl.PolaroidError):
         df.filter(pl.col("w") > 1)
-    with pytest.raises(pl.PolaroidError):
-        df.sort("w")
+
+
+@pytest.mark.parametrize("n", [0, 1, 3000, 200_003])
+@pytest.mark.parametrize("descending", [False, True])
+@pytest.mark.parametrize("nulls_last", [False, True])
+def test_sort_by_string(gpu, n, descending, nulls_last):
+    """Byte-wise (UTF-8) order as the reference's string sort; a proper
+    prefix first; ties and nulls keep row order (stable)."""
+    rng = np.random.default_rng(n + 2 * descending + nulls_last)
+    w, wv = _words(rng, n, 300, long_frac=0.01)
+    extra = np.array(["ab", "ab\x00", "abc", "a", "", "b" * 20, "b" * 19 + "a", "日", "z"], dtype=object)
+    w[: min(n, extra.size)] = extra[: min(n, extra.size)]
+    df = pl.DataFrame({"w": pl.Series.from_numpy("w", w, wv), "i": pl.Series.from_numpy("i", np.arange(n))})
+    out = df.sort("w", descending=descending, nulls_last=nulls_last)
+    valid_rows = [i for i in range(n) if wv[i]]
+    null_rows = [i for i in range(n) if not wv[i]]
+    ordered = sorted(valid_rows, key=lambda i: w[i].encode(), reverse=descending)
+    exp = ordered + null_rows if nulls_last else null_rows + ordered
+    assert out["i"].to_list() == exp
+    # two keys: string then integer
+    a = rng.integers(0, 3, n)
+    df2 = pl.DataFrame({"w": pl.Series.from_numpy("w", w, wv), "a": pl.Series.from_numpy("a", a),
+                        "i": pl.Series.from_numpy("i", np.arange(n))})
+    out2 = df2.sort("w", "a")
+    # nulls of `w` compare equal to each other, so `a` orders them too
+    key = lambda i: (0, b"", int(a[i])) if not wv[i] else (1, w[i].encode(), int(a[i]))  # noqa: E731
+    assert out2["i"].to_list() == sorted(range(n), key=key)
