@@ -344,6 +344,16 @@ int plgpu_join_multi(const plgpu_column* left_keys, const plgpu_column* right_ke
                      int32_t nulls_equal, int32_t maintain_order, int32_t validate, plgpu_column* out_left_idx,
                      plgpu_column* out_right_idx, void* stream);
 
+/* Boolean column of a comparison of String column `a` with String column
+ * `b`, or (b == NULL) with the literal `lit` (lit_len bytes, host memory):
+ * op = PLGPU_OP_EQ .. PLGPU_OP_NE_MISSING; or IS_NULL / IS_NOT_NULL of `a`.
+ * Bytes compare lexicographically (a proper prefix first); a null operand
+ * gives null except for the *_MISSING ops.  Replaces
+ * polars-compute/src/comparisons/view.rs TotalEqKernel / TotalOrdKernel for
+ * BinaryViewArray (and their _broadcast scalar forms). */
+int plgpu_str_compare(const plgpu_column* a, const plgpu_column* b, const uint8_t* lit, int64_t lit_len, int32_t op,
+                      plgpu_column* out, void* stream);
+
 /* out[i] = a[i] if valid, else b[i] (same dtype and length); the coalesced
  * key columns of a full join with coalesce=True
  * (polars-ops/src/frame/join/general.rs:52 _coalesce_full_join). */

@@ -339,4 +339,108 @@ int str_from_codes(const plgpu_column& codes, plgpu_column* out, hipStream_t s) 
     return rc;
 }
 
+// ------------------------------------------------- string comparisons
+// polars-compute/src/comparisons/view.rs (TotalEqKernel / TotalOrdKernel for
+// BinaryViewArray, and their _broadcast forms against a scalar): strings
+// compare by their bytes, lexicographically, a proper prefix first; a null
+// operand gives a null result, except eq_missing / ne_missing (null equals
+// only null, never null out).  `b` is a second string column, or (b.values
+// == nullptr) the literal `lit` of `lit_len` bytes.  IS_NULL / IS_NOT_NULL
+// read `a` only.
+__device__ __forceinline__ int str_cmp3(const uint8_t* x, int64_t lx, const uint8_t* y, int64_t ly) {
+    const int64_t m = lx < ly ? lx : ly;
+    for (int64_t i = 0; i < m; ++i)
+        if (x[i] != y[i]) return x[i] < y[i] ? -1 : 1;
+    return lx < ly ? -1 : (lx > ly ? 1 : 0);
+}
+
+__global__ __launch_bounds__(kStrThreads) void str_cmp_kernel(DevCol a, DevCol b, const uint8_t* __restrict__ lit,
+                                                              int64_t lit_len, int32_t op, int64_t n,
+                                                              uint64_t* __restrict__ out_vals,
+                                                              uint64_t* __restrict__ out_valid) {
+    const int64_t* oa = (const int64_t*)a.values;
+    const int64_t* ob = (const int64_t*)b.values;
+    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x; i0 < n; i0 += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i0 + threadIdx.x;
+        bool res = false, valid = false;
+        if (r < n) {
+            const bool va = dev_valid(a, r);
+            if (op == PLGPU_OP_IS_NULL || op == PLGPU_OP_IS_NOT_NULL) {
+                res = (op == PLGPU_OP_IS_NULL) ? !va : va;
+                valid = true;
+            } else {
+                const bool vb = ob == nullptr || dev_valid(b, r);
+                int c = 0;
+                if (va && vb) {
+                    const int64_t sa = oa[a.offset + r], la = oa[a.offset + r + 1] - sa;
+                    const uint8_t* y = lit;
+                    int64_t ly = lit_len;
+                    if (ob) {
+                        const int64_t sb = ob[b.offset + r];
+                        ly = ob[b.offset + r + 1] - sb;
+                        y = b.data + sb;
+                    }
+                    c = str_cmp3(a.data + sa, la, y, ly);
+                }
+                switch (op) {
+                case PLGPU_OP_EQ: res = c == 0; break;
+                case PLGPU_OP_NE: res = c != 0; break;
+                case PLGPU_OP_LT: res = c < 0; break;
+                case PLGPU_OP_LE: res = c <= 0; break;
+                case PLGPU_OP_GT: res = c > 0; break;
+                case PLGPU_OP_GE: res = c >= 0; break;
+                case PLGPU_OP_EQ_MISSING: res = (va && vb) ? c == 0 : va == vb; break;
+                default: res = (va && vb) ? c != 0 : va != vb; break;  // NE_MISSING
+                }
+                valid = (op == PLGPU_OP_EQ_MISSING || op == PLGPU_OP_NE_MISSING) ? true : (va && vb);
+                if (!valid) res = false;
+            }
+        }
+        const uint64_t wv = __ballot(res), wm = __ballot(valid);
+        if ((threadIdx.x & 63) == 0 && r < n) {
+            out_vals[r >> 6] = wv;
+            out_valid[r >> 6] = wm;
+        }
+    }
+}
+
 }  // namespace plgpu
+
+using namespace plgpu;
+
+PLGPU_API int plgpu_str_compare(const plgpu_column* a, const plgpu_column* b, const uint8_t* lit, int64_t lit_len,
+                                int32_t op, plgpu_column* out, void* stream) {
+    hipStream_t s = as_stream(stream);
+    if (a == nullptr || out == nullptr) return fail(PLGPU_ERR_INVALID, "NULL argument");
+    std::memset(out, 0, sizeof *out);
+    if (a->dtype != PLGPU_STR || (b && b->dtype != PLGPU_STR))
+        return fail(PLGPU_ERR_SCHEMA, "string comparison of a non-String column");
+    const bool unary = op == PLGPU_OP_IS_NULL || op == PLGPU_OP_IS_NOT_NULL;
+    if (!unary && (op < PLGPU_OP_EQ || op > PLGPU_OP_NE_MISSING))
+        return fail(PLGPU_ERR_INVALID, "unsupported string comparison");
+    if (!unary && b == nullptr && lit_len > 0 && lit == nullptr) return fail(PLGPU_ERR_INVALID, "NULL literal");
+    if (b && b->length != a->length) return fail(PLGPU_ERR_SHAPE, "compared columns differ in length");
+    const int64_t n = a->length;
+    int rc = make_owned_column(out, PLGPU_BOOL, n, true, s);
+    if (rc || n == 0) return rc;
+    uint8_t* dlit = nullptr;
+    if (!unary && b == nullptr) {
+        rc = dev_alloc((void**)&dlit, std::max<int64_t>(lit_len, 1), s);
+        if (!rc && lit_len > 0 && hipMemcpyAsync(dlit, lit, lit_len, hipMemcpyHostToDevice, s) != hipSuccess)
+            rc = fail(PLGPU_ERR_HIP, "string literal upload");
+    }
+    if (!rc) {
+        DevCol db;
+        std::memset(&db, 0, sizeof db);
+        if (b) db = dev_col(*b);
+        const int g = (int)std::min<int64_t>((n + kStrThreads - 1) / kStrThreads, (int64_t)num_cus_str() * 16);
+        str_cmp_kernel<<<g, kStrThreads, 0, s>>>(dev_col(*a), db, dlit, lit_len, op, n, (uint64_t*)out->values,
+                                                 (uint64_t*)out->validity);
+        hipError_t e = hipGetLastError();
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) rc = hip_fail(e, "string comparison");
+    }
+    dev_free(dlit, s);
+    if (rc) plgpu_column_release(out);
+    return rc;
+}

@@ -711,6 +711,67 @@ def _explain(node: tuple, depth: int = 0) -> str:
     return f"{pad}{kind.upper()} {node[2]!r}\n" + _explain(node[1], depth + 1)
 
 
+_CMP_OPS = {"==": "EQ", "!=": "NE", "<": "LT", "<=": "LE", ">": "GT", ">=": "GE",
+            "eq_missing": "EQ_MISSING", "ne_missing": "NE_MISSING"}
+_CMP_MIRROR = {"<": ">", "<=": ">=", ">": "<", ">=": "<="}
+
+
+def _lower_strings(expr: Expr, df: DataFrame) -> tuple[Expr, DataFrame]:
+    """Replace every comparison that involves a String column (with a string
+    literal or another String column) and every is_null / is_not_null of a
+    String column by a Boolean column computed on the GPU
+    (plgpu_str_compare; polars-compute/src/comparisons/view.rs), so the rest
+    of the expression lowers to the numeric program as usual.  Returns the
+    rewritten expression and the frame extended by those columns."""
+    extra: list[Series] = []
+
+    def is_str(e: Expr) -> bool:
+        return (e.kind == "col" and e.value in df._cols and df._cols[e.value].dtype is String) or \
+            (e.kind == "lit" and isinstance(e.value, str))
+
+    def new_col(c_: N.Column) -> Expr:
+        name = f"__strcmp{builtins.len(extra)}"
+        extra.append(Series._from_native(name, c_))
+        return col(name)
+
+    def walk(e: Expr) -> Expr:
+        if e.kind == "bin" and e.op in _CMP_OPS and (is_str(e.args[0]) or is_str(e.args[1])):
+            a, b = e.args
+            op = e.op
+            if a.kind == "lit":  # literal on the left: mirror the comparison
+                a, b = b, a
+                op = _CMP_MIRROR.get(op, op)
+            if not (is_str(a) and is_str(b)) or a.kind != "col":
+                raise N.InvalidOperationError(f"comparison {e!r} of a String with a non-string operand")
+            out = N.Column()
+            ac = df._cols[a.value]._col
+            if b.kind == "col":
+                N.check(N.lib().plgpu_str_compare(C.byref(ac), C.byref(df._cols[b.value]._col), None, 0,
+                                                  N.OP[_CMP_OPS[op]], C.byref(out), None))
+            else:
+                lit_b = b.value.encode()
+                N.check(N.lib().plgpu_str_compare(C.byref(ac), None, lit_b, builtins.len(lit_b),
+                                                  N.OP[_CMP_OPS[op]], C.byref(out), None))
+            return new_col(out)
+        if e.kind == "un" and e.op in ("is_null", "is_not_null") and is_str(e.args[0]) and e.args[0].kind == "col":
+            out = N.Column()
+            N.check(N.lib().plgpu_str_compare(C.byref(df._cols[e.args[0].value]._col), None, None, 0,
+                                              N.OP["IS_NULL" if e.op == "is_null" else "IS_NOT_NULL"],
+                                              C.byref(out), None))
+            return new_col(out)
+        if not e.args:
+            return e
+        args = tuple(walk(a) for a in e.args)
+        if all(x is y for x, y in zip(args, e.args)):
+            return e
+        return Expr(e.kind, args, op=e.op, value=e.value, name=e._name)
+
+    new = walk(expr)
+    if not extra:
+        return expr, df
+    return new, DataFrame(list(df._cols.values()) + extra)
+
+
 def _program(expr: Expr, df: DataFrame) -> tuple[list[Series], Any, int]:
     names = expr.meta_root_names()
     if builtins.len(names) > N.MAX_COLS:
@@ -745,6 +806,7 @@ def _eval(expr: Expr, df: DataFrame) -> Series:
         else:
             res = inner.sort(descending=base.value[0], nulls_last=base.value[1])
         return res.alias(expr.output_name())
+    expr, df = _lower_strings(expr, df)
     used, prog, n = _program(expr, df)
     if not used:
         raise N.InvalidOperationError("literal-only expressions are not supported on the GPU executor")
@@ -755,6 +817,7 @@ def _eval(expr: Expr, df: DataFrame) -> Series:
 
 def _filter(df: DataFrame, pred: Expr) -> DataFrame:
     names = df.columns
+    pred, df = _lower_strings(pred, df)
     if not pred.meta_root_names():
         # Constant predicate (plan-time simplification, as polars'
         # simplify_expression does): keep every row or none.
@@ -894,6 +957,8 @@ def _gb_frame(g: _GbCall, out_key, out_aggs) -> DataFrame:
 
 def _group_by(df: DataFrame, key: str | tuple, aggs: list[Expr], maintain_order: bool,
               pred: Expr | None, info: dict | None) -> DataFrame:
+    if pred is not None:
+        pred, df = _lower_strings(pred, df)
     g = _gb_lower(df, key, aggs, pred)
     out_aggs = (N.Column * max(1, g.naggs))()
     gi = N.GroupByInfo()

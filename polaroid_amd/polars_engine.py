@@ -81,7 +81,7 @@ class _Translator:
             return col(str(e.name))
         if k == "Literal":
             v = e.value
-            if v is None or isinstance(v, (bool, int, float)):
+            if v is None or isinstance(v, (bool, int, float, str)):  # str: String comparisons
                 return lit(v)
             raise Unsupported(f"literal {v!r}")
         if k == "BinaryExpr":

@@ -216,3 +216,56 @@ def test_sort_by_string(gpu, n, descending, nulls_last):
     # nulls of `w` compare equal to each other, so `a` orders them too
     key = lambda i: (0, b"", int(a[i])) if not wv[i] else (1, w[i].encode(), int(a[i]))  # noqa: E731
     assert out2["i"].to_list() == sorted(range(n), key=key)
+
+
+def _cmp(x, y, op):
+    if x is None or y is None:
+        return None
+    a, b = x.encode(), y.encode()
+    return {"==": a == b, "!=": a != b, "<": a < b, "<=": a <= b, ">": a > b, ">=": a >= b}[op]
+
+
+@pytest.mark.parametrize("n", [0, 1, 4000, 100_003])
+def test_string_predicates(gpu, n):
+    """String comparisons (view.rs TotalEqKernel / TotalOrdKernel semantics:
+    byte order, null in -> null out, *_missing never null) in filter,
+    select and the group-by's fused predicate."""
+    rng = np.random.default_rng(n)
+    w, wv = _words(rng, n, 40, long_frac=0.01)
+    u, uv = _words(rng, n, 40, short=True)
+    x = rng.standard_normal(n)
+    wl = [s if ok else None for s, ok in zip(w, wv)]
+    ul = [s if ok else None for s, ok in zip(u, uv)]
+    df = pl.DataFrame({"w": pl.Series.from_numpy("w", w, wv), "u": pl.Series.from_numpy("u", u, uv),
+                       "x": pl.Series.from_numpy("x", x), "i": pl.Series.from_numpy("i", np.arange(n))})
+    for op in ("==", "!=", "<", "<=", ">", ">="):
+        for litv in ("AAPL", "", "sym00017", "z"):
+            e = {"==": pl.col("w") == litv, "!=": pl.col("w") != litv, "<": pl.col("w") < litv,
+                 "<=": pl.col("w") <= litv, ">": pl.col("w") > litv, ">=": pl.col("w") >= litv}[op]
+            got = df.select(e.alias("m"))["m"].to_list()
+            assert got == [_cmp(s, litv, op) for s in wl], (op, litv)
+        # column vs column, and the literal on the left (mirrored)
+        e2 = {"==": pl.col("w") == pl.col("u"), "!=": pl.col("w") != pl.col("u"), "<": pl.col("w") < pl.col("u"),
+              "<=": pl.col("w") <= pl.col("u"), ">": pl.col("w") > pl.col("u"),
+              ">=": pl.col("w") >= pl.col("u")}[op]
+        assert df.select(e2.alias("m"))["m"].to_list() == [_cmp(a, b, op) for a, b in zip(wl, ul)], op
+    left = df.select((pl.lit("MSFT") < pl.col("w")).alias("m"))["m"].to_list()
+    assert left == [_cmp(s, "MSFT", ">") for s in wl]
+    em = df.select(pl.col("w").eq_missing(pl.col("u")).alias("m"))["m"].to_list()
+    assert em == [(a == b) if (a is not None and b is not None) else (a is None and b is None) for a, b in zip(wl, ul)]
+    assert df.select(pl.col("w").is_null().alias("m"))["m"].to_list() == [s is None for s in wl]
+    # filter: string predicate combined with a numeric one (Kleene and)
+    out = df.filter((pl.col("w") == "AAPL") & (pl.col("x") > 0.0))
+    keep = [i for i in range(n) if wl[i] == "AAPL" and x[i] > 0.0]
+    assert out["i"].to_list() == keep and out["w"].to_list() == [wl[i] for i in keep]
+    assert out.columns == ["w", "u", "x", "i"]
+    # group-by with the string predicate fused into the aggregation
+    g = df.lazy().filter(pl.col("u") != "AAPL").group_by("w", maintain_order=True).agg(pl.col("x").sum()).collect()
+    sel = [i for i in range(n) if ul[i] is not None and ul[i] != "AAPL"]
+    keys = []
+    for i in sel:
+        if wl[i] not in keys:
+            keys.append(wl[i])
+    assert g["w"].to_list() == keys
+    for k, v in zip(keys, g["x"].to_list()):
+        assert v == O.fsum(np.array([x[i] for i in sel if wl[i] == k]))
