@@ -441,31 +441,46 @@ class GpuJoinOps:
         return DataFrame(series)
 
     @staticmethod
-    def local_join(left, right, left_on, right_on, suffix: str, nulls_equal: bool):
+    def local_join(left, right, left_on, right_on, suffix: str, nulls_equal: bool, how: str = "inner"):
         from .frame import _join
 
-        return _join(left, right, left_on, right_on, suffix, "m:m", nulls_equal, "none")
+        return _join(left, right, left_on, right_on, suffix, "m:m", nulls_equal, "none", how)
+
+
+# Which side a join type may broadcast: the side whose unmatched rows the
+# result does not keep (a broadcast side is seen by every rank, so rows it
+# keeps would come out once per rank).  A full join keeps both: shuffle only.
+_BROADCASTABLE = {"inner": ("left", "right"), "left": ("right",), "semi": ("right",), "anti": ("right",),
+                  "right": ("left",), "full": ()}
 
 
 def run_join(ops, left, right, left_keys: Sequence[str], right_keys: Sequence[str], suffix: str,
-             nulls_equal: bool, strategy: str, group, device, info: dict | None = None):
+             nulls_equal: bool, strategy: str, group, device, info: dict | None = None, how: str = "inner"):
     """The multi-GPU join protocol over any `ops` implementation (the GPU one
-    above, or a host model in tests/test_distributed.py)."""
+    above, or a host model in tests/test_distributed_join.py)."""
     import torch
     import torch.distributed as dist
 
+    if how not in _BROADCASTABLE:
+        raise ValueError(f"invalid join type {how!r}")
     world = dist.get_world_size(group)
     sizes = torch.tensor([ops.rows(left), ops.rows(right)], dtype=torch.int64, device=device)
     dist.all_reduce(sizes, group=group)
     nl, nr = (int(v) for v in sizes.tolist())
+    allowed = _BROADCASTABLE[how]
+    # the side to broadcast: the smaller allowed one
+    bside = min(allowed, key=lambda sd: nl if sd == "left" else nr) if allowed else None
     if strategy == "auto":
-        strategy = "broadcast" if min(nl, nr) <= JOIN_BROADCAST_ROWS else "shuffle"
+        small = bside is not None and (nl if bside == "left" else nr) <= JOIN_BROADCAST_ROWS
+        strategy = "broadcast" if small else "shuffle"
     if strategy not in ("broadcast", "shuffle"):
         raise ValueError(f"invalid join strategy {strategy!r}")
+    if strategy == "broadcast" and bside is None:
+        raise ValueError("a full join cannot broadcast either side; use strategy='shuffle'")
     lk = left_keys[0] if len(left_keys) == 1 else tuple(left_keys)
     rk = right_keys[0] if len(right_keys) == 1 else tuple(right_keys)
     if strategy == "broadcast":
-        if nr <= nl:
+        if bside == "right":
             cols, n = allgather_columns(ops.to_wire(right), ops.rows(right), group)
             right = ops.from_wire(cols, n)
         else:
@@ -475,26 +490,32 @@ def run_join(ops, left, right, left_keys: Sequence[str], right_keys: Sequence[st
     else:
         moved = 0
         sides = []
-        for df, keys in ((left, left_keys), (right, right_keys)):
-            perm, counts = ops.partition(df, keys, world, nulls_equal)
+        # a side whose unmatched rows are kept must keep its null-key rows
+        # too: they are routed (to rank 0) instead of dropped
+        keep_nulls = {"left": how in ("left", "anti", "full"), "right": how in ("right", "full")}
+        for sd, df, keys in (("left", left, left_keys), ("right", right, right_keys)):
+            perm, counts = ops.partition(df, keys, world, nulls_equal or keep_nulls[sd])
             cols, n = exchange_columns(ops.to_wire(df, perm), counts, group)
             sides.append(ops.from_wire(cols, n))
             moved += n
         left, right = sides
-    out = ops.local_join(left, right, lk, rk, suffix, nulls_equal)
+    out = ops.local_join(left, right, lk, rk, suffix, nulls_equal, how)
     if info is not None:
         info.update({"strategy": strategy, "left_rows": nl, "right_rows": nr, "rows_received": moved})
     return out
 
 
-def join(left, right, on: str | Sequence[str] | None = None, *, left_on=None, right_on=None,
+def join(left, right, on: str | Sequence[str] | None = None, how: str = "inner", *, left_on=None, right_on=None,
          suffix: str = "_right", nulls_equal: bool = False, strategy: str = "auto", group=None,
          info: dict | None = None):
-    """`left.join(right, on=..., how="inner")` over the shards held by all
-    ranks of `group` (one GPU per rank, RCCL).  Returns this rank's share of
-    the result; the union over ranks is the join of the concatenated shards.
-    strategy: "auto" (broadcast the smaller side up to JOIN_BROADCAST_ROWS
-    rows, else shuffle), "broadcast" or "shuffle"."""
+    """`left.join(right, on=..., how=...)` over the shards held by all ranks
+    of `group` (one GPU per rank, RCCL); how = inner / left / right / full /
+    semi / anti.  Returns this rank's share of the result; the union over
+    ranks is the join of the concatenated shards.  strategy: "auto"
+    (broadcast the smaller side the join type allows -- the right side of a
+    left / semi / anti join, the left of a right join, none for a full join
+    -- up to JOIN_BROADCAST_ROWS rows, else shuffle), "broadcast" or
+    "shuffle"."""
     import torch
     import torch.distributed as dist
 
@@ -511,6 +532,6 @@ def join(left, right, on: str | Sequence[str] | None = None, *, left_on=None, ri
     rks = [right_on] if isinstance(right_on, str) else list(right_on)
     if len(lks) != len(rks):
         raise N.InvalidOperationError("the number of join key columns must be equal on both sides")
-    out = run_join(GpuJoinOps, left, right, lks, rks, suffix, nulls_equal, strategy, group, device, info)
+    out = run_join(GpuJoinOps, left, right, lks, rks, suffix, nulls_equal, strategy, group, device, info, how)
     torch.cuda.synchronize()
     return out

@@ -107,18 +107,23 @@ class HostOps:
         return HostFrame(res)
 
     @staticmethod
-    def local_join(left, right, lk, rk, suffix, nulls_equal):
+    def local_join(left, right, lk, rk, suffix, nulls_equal, how="inner"):
         lk = [lk] if isinstance(lk, str) else list(lk)
         rk = [rk] if isinstance(rk, str) else list(rk)
-        return _host_join(left, right, lk, rk, suffix, nulls_equal)
+        return _host_join(left, right, lk, rk, suffix, nulls_equal, how)
 
 
-def _host_join(left, right, lk, rk, suffix, nulls_equal):
+def _host_join(left, right, lk, rk, suffix, nulls_equal, how="inner"):
+    """Rows of a join as the single-GPU executor lays them out (frame._join):
+    semi / anti the left rows; otherwise the left columns (without the keys
+    for a right join) and the right columns (without the keys unless full),
+    None for a missing partner."""
     lrows, rrows = left.rows(), right.rows()
     ln, rn = list(left.cols), list(right.cols)
     li = [ln.index(k) for k in lk]
     ri = [rn.index(k) for k in rk]
-    keep_r = [i for i, n in enumerate(rn) if n not in rk]
+    keep_l = [i for i, n in enumerate(ln) if not (how == "right" and n in lk)]
+    keep_r = [i for i, n in enumerate(rn) if how == "full" or how == "right" or n not in rk]
     index = {}
     for j, r in enumerate(rrows):
         key = tuple(r[i] for i in ri)
@@ -126,12 +131,27 @@ def _host_join(left, right, lk, rk, suffix, nulls_equal):
             continue
         index.setdefault(key, []).append(j)
     out = []
+    matched = set()
     for lrow in lrows:
         key = tuple(lrow[i] for i in li)
-        if None in key and not nulls_equal:
+        js = [] if (None in key and not nulls_equal) else index.get(key, [])
+        if how == "semi":
+            if js:
+                out.append(lrow)
             continue
-        for j in index.get(key, []):
-            out.append(lrow + tuple(rrows[j][i] for i in keep_r))
+        if how == "anti":
+            if not js:
+                out.append(lrow)
+            continue
+        for j in js:
+            matched.add(j)
+            out.append(tuple(lrow[i] for i in keep_l) + tuple(rrows[j][i] for i in keep_r))
+        if not js and how in ("left", "full"):
+            out.append(tuple(lrow[i] for i in keep_l) + (None,) * len(keep_r))
+    if how in ("right", "full"):
+        for j, r in enumerate(rrows):
+            if j not in matched:
+                out.append((None,) * len(keep_l) + tuple(r[i] for i in keep_r))
     return out
 
 
@@ -152,7 +172,7 @@ def _shard(rank, world, side, n):
                       name + "_flag": (N.BOOL, b, None)})
 
 
-def _worker(rank, world, port, strategy, keys, nulls_equal, sizes, q):
+def _worker(rank, world, port, strategy, keys, nulls_equal, sizes, q, how="inner"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -161,18 +181,18 @@ def _worker(rank, world, port, strategy, keys, nulls_equal, sizes, q):
         right = _shard(rank, world, "right", sizes[rank][1])
         info = {}
         out = D.run_join(HostOps, left, right, keys, keys, "_right", nulls_equal, strategy, None,
-                         torch.device("cpu"), info)
+                         torch.device("cpu"), info, how)
         # keys that landed here (shuffle: each key on one rank only)
         q.put((rank, out, info))
     finally:
         dist.destroy_process_group()
 
 
-def _run(world, strategy, keys, nulls_equal, sizes):
+def _run(world, strategy, keys, nulls_equal, sizes, how="inner"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, strategy, keys, nulls_equal, sizes, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, strategy, keys, nulls_equal, sizes, q, how))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -225,6 +245,41 @@ def test_join_protocol_gloo(world, strategy, keys, nulls_equal, sizes):
             for row in res[r][0]:
                 kt = tuple(row[i] for i in range(len(keys)))
                 assert seen.setdefault(kt, r) == r
+
+
+@pytest.mark.parametrize("world,strategy,how,nulls_equal", [
+    (2, "shuffle", "left", True), (3, "shuffle", "full", False), (2, "shuffle", "anti", False),
+    (2, "broadcast", "right", False), (3, "broadcast", "anti", False), (2, "auto", "semi", False),
+])
+def test_join_types_protocol_gloo(world, strategy, how, nulls_equal):
+    """Every join type over the multi-rank protocol: the union of the ranks'
+    results equals the join of the concatenated shards (null-key rows of a
+    kept side are routed, not dropped; only the allowed side broadcasts)."""
+    sizes = [(200, 150), (180, 120), (90, 60)][:world]
+    res = _run(world, strategy, ["k"], nulls_equal, sizes, how)
+    left = _concat([_shard(r, world, "left", sizes[r][0]) for r in range(world)])
+    right = _concat([_shard(r, world, "right", sizes[r][1]) for r in range(world)])
+    expect = _host_join(left, right, ["k"], ["k"], "_right", nulls_equal, how)
+    got = [row for r in range(world) for row in res[r][0]]
+    assert Counter(got) == Counter(expect) and len(expect) > 0
+    used = res[0][1]["strategy"]
+    if how == "full":
+        assert used == "shuffle"
+
+
+def test_full_join_cannot_broadcast():
+    """In-process world of one: a full join refuses to broadcast."""
+    dist.init_process_group("gloo", rank=0, world_size=1, init_method=f"tcp://127.0.0.1:{_free_port()}")
+    try:
+        f = _shard(0, 1, "left", 10)
+        g = _shard(0, 1, "right", 10)
+        with pytest.raises(ValueError, match="full join"):
+            D.run_join(HostOps, f, g, ["k"], ["k"], "_right", False, "broadcast", None, torch.device("cpu"), None,
+                       "full")
+        assert D.run_join(HostOps, f, g, ["k"], ["k"], "_right", False, "auto", None, torch.device("cpu"), None,
+                          "full") == _host_join(f, g, ["k"], ["k"], "_right", False, "full")
+    finally:
+        dist.destroy_process_group()
 
 
 def _a2a_worker(rank, world, port, q):

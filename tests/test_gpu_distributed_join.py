@@ -166,15 +166,16 @@ def _pairs_frame(keys, names, rowname, base):
     return pl.DataFrame(s)
 
 
-def _simulate_shuffle(lshards, rshards, names, world, nulls_equal):
+def _simulate_shuffle(lshards, rshards, names, world, nulls_equal, how="inner"):
     import torch
 
     ops = D.GpuJoinOps
     sides = []
-    for shards in (lshards, rshards):
+    keep_nulls = (how in ("left", "anti", "full"), how in ("right", "full"))  # as run_join routes them
+    for si, shards in enumerate((lshards, rshards)):
         wires = []
         for df in shards:
-            perm, counts = ops.partition(df, names, world, nulls_equal)
+            perm, counts = ops.partition(df, names, world, nulls_equal or keep_nulls[si])
             wires.append((ops.to_wire(df, perm), counts))
         frames = []
         for dest in range(world):
@@ -195,7 +196,7 @@ def _simulate_shuffle(lshards, rshards, names, world, nulls_equal):
             frames.append(ops.from_wire(cols, n))
         sides.append(frames)
     lk = names[0] if len(names) == 1 else tuple(names)
-    return [ops.local_join(l, r, lk, lk, "_right", nulls_equal) for l, r in zip(*sides)]
+    return [ops.local_join(l, r, lk, lk, "_right", nulls_equal, how) for l, r in zip(*sides)]
 
 
 def _check_union(outs, lkeys, rkeys, nulls_equal):
@@ -229,6 +230,39 @@ def test_shuffle_join_simulated(gpu, world, kinds, nulls_equal):
         assert o.columns == names + ["li", "ri"]
 
 
+@pytest.mark.parametrize("world", [2, 3, 8])
+@pytest.mark.parametrize("how", ["left", "right", "full", "semi", "anti"])
+@pytest.mark.parametrize("nulls_equal", [False, True])
+def test_shuffle_join_types_simulated(gpu, world, how, nulls_equal):
+    """Every join type through the shuffle (partition, wire round trip,
+    per-destination join) simulated on one GPU: the union of the ranks'
+    (left, right) index pairs equals the single-process join's."""
+    rng = np.random.default_rng(world * 7 + len(how) + nulls_equal)
+    nl = [3000, 0, 4001][:world] + [1500] * max(0, world - 3)
+    nr = [1200, 900, 0][:world] + [600] * max(0, world - 3)
+    lk_sh = [_keys(rng, n, ["i64n"]) for n in nl]
+    rk_sh = [_keys(rng, n, ["i64n"]) for n in nr]
+    lsh = [_pairs_frame(k, ["k"], "li", sum(nl[:i])) for i, k in enumerate(lk_sh)]
+    rsh = [_pairs_frame(k, ["k"], "ri", sum(nr[:i])) for i, k in enumerate(rk_sh)]
+    outs = _simulate_shuffle(lsh, rsh, ["k"], world, nulls_equal, how)
+    cat = lambda sh: (np.concatenate([s[0][0] for s in sh]), np.concatenate([s[0][1] for s in sh]))  # noqa: E731
+    lv, lm = cat(lk_sh)
+    rv, rm = cat(rk_sh)
+    ol, orr = O.join(O.HostCol(lv, lm), O.HostCol(rv, rm), how, nulls_equal)
+
+    def idx(o, name):
+        s = o[name]
+        return np.where(s.validity_numpy(), s.to_numpy().astype(np.int64), -1)
+
+    gl = np.concatenate([idx(o, "li") for o in outs])
+    if how in ("semi", "anti"):
+        assert np.array_equal(np.sort(gl), np.sort(ol))
+        return
+    gr = np.concatenate([idx(o, "ri") for o in outs])
+    a, b = np.lexsort((gr, gl)), np.lexsort((orr, ol))
+    assert np.array_equal(gl[a], ol[b]) and np.array_equal(gr[a], orr[b])
+
+
 def test_join_world1_rccl(gpu):
     """distributed.join over torch.distributed (nccl = RCCL), one rank, both
     strategies, against the single-GPU join."""
@@ -258,6 +292,16 @@ def test_join_world1_rccl(gpu):
             assert out.columns == ref.columns
             assert np.array_equal(out["flag"].to_numpy()[a], ref["flag"].to_numpy()[b])
             assert np.array_equal(out["flag"].validity_numpy()[a], ref["flag"].validity_numpy()[b])
+        for how in ("left", "right", "full", "semi", "anti"):
+            for strategy in ("shuffle", "auto"):
+                info = {}
+                out = D.join(left, right, on="k", how=how, strategy=strategy, info=info)
+                ref = left.join(right, on="k", how=how)
+                assert out.columns == ref.columns and out.height == ref.height, (how, strategy)
+                key = [c for c in ("li", "ri") if c in ref.columns]
+                got = sorted(zip(*[out[c].to_list() for c in key]), key=str)
+                exp = sorted(zip(*[ref[c].to_list() for c in key]), key=str)
+                assert got == exp, (how, strategy)
         # large enough that reading a receive buffer before RCCL finished
         # writing it would show (the buffers are host-waited on)
         import torch
