@@ -446,7 +446,12 @@ int plgpu_arg_sort_multi(const plgpu_column* keys, int32_t nkeys, const int32_t*
  * rounded window sums (divided by the non-null count); integer sums wrap.
  * Replaces polars-compute/src/rolling/no_nulls/{sum,mean}.rs rolling_sum /
  * rolling_mean and nulls/{sum,mean}.rs (rolling/sum.rs:7 SumWindow). */
-enum plgpu_rolling_kind { PLGPU_ROLLING_SUM = 1, PLGPU_ROLLING_MEAN = 2 };
+enum plgpu_rolling_kind {
+    PLGPU_ROLLING_SUM = 1,
+    PLGPU_ROLLING_MEAN = 2,
+    PLGPU_ROLLING_MIN = 3,  /* rolling/no_nulls/min_max.rs MinWindow (NaN propagates) */
+    PLGPU_ROLLING_MAX = 4   /* ... MaxWindow; output dtype = input dtype            */
+};
 
 int plgpu_rolling(const plgpu_column* values, int32_t kind, int64_t window_size,
                   int64_t min_periods, int32_t center, plgpu_column* out, void* stream);

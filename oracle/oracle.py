@@ -420,13 +420,13 @@ def rolling(col: HostCol, kind: str, window_size: int, min_periods: int | None =
     reference's Kahan sliding window; mode 1 is the exact window sum."""
     n = col.c.length
     mp = window_size if min_periods is None else min_periods
-    k = {"sum": 1, "mean": 2}[kind]
+    k = {"sum": 1, "mean": 2, "min": 3, "max": 4}[kind]
     of = np.zeros(max(n, 1), np.float64)
     oi = np.zeros(max(n, 1), np.int64)
     ov = np.zeros(max(n, 1), np.uint8)
     lib().or_rolling(C.byref(col.c), k, window_size, mp, int(center), mode, of.ctypes.data, oi.ctypes.data,
                      ov.ctypes.data)
-    isint = k == 1 and col.code != F64
+    isint = k in (1, 3, 4) and col.code != F64
     vals = (oi if isint else of)[:n].copy()
     return vals, ov[:n].astype(bool)
 

@@ -1010,9 +1010,50 @@ static void rl_offsets(int64_t i, int64_t ws, int64_t n, int center, int64_t* s,
     }
 }
 
-/* kind 1 sum / 2 mean; out_f64 or out_i64 (integer sums); out_valid bytes. */
+/* Rolling min / max (kind 3 / 4): polars-compute/src/rolling/{no_nulls,
+ * nulls}/min_max.rs MinMaxWindow with MinPropagateNan / MaxPropagateNan
+ * (polars-utils/src/min_max.rs:144,168): a NaN in the window makes the
+ * result NaN; nulls are skipped; the result is null when the window holds
+ * fewer than min_periods values (the window length when there are no nulls)
+ * or no value at all.  Restated as a direct scan of each window. */
+static void or_rolling_minmax(const plgpu_column* c, int32_t kind, int64_t ws, int64_t min_periods, int32_t center,
+                              double* out_f64, int64_t* out_i64, uint8_t* out_valid) {
+    const int64_t n = c->length;
+    const int isf = c->dtype == PLGPU_F64;
+    for (int64_t i = 0; i < n; ++i) {
+        int64_t s, e;
+        rl_offsets(i, ws, n, center, &s, &e);
+        int64_t nn = 0;
+        int nan = 0;
+        double bf = 0.0;
+        int64_t bi = 0;
+        for (int64_t r = s; r < e; ++r) {
+            if (!col_valid(c, r)) continue;
+            if (isf) {
+                const double x = rl_val(c, r);
+                if (isnan(x)) nan = 1;
+                else if (nn == 0 || (kind == 3 ? x < bf : x > bf)) bf = x;
+            } else {
+                const int64_t x = col_int(c, r);
+                if (nn == 0 || (kind == 3 ? x < bi : x > bi)) bi = x;
+            }
+            ++nn;
+        }
+        const int valid = nn >= min_periods && nn > 0;
+        out_valid[i] = (uint8_t)valid;
+        if (isf) out_f64[i] = valid ? (nan ? NAN : bf) : 0.0;
+        else out_i64[i] = valid ? bi : 0;
+    }
+}
+
+/* kind 1 sum / 2 mean / 3 min / 4 max; out_f64 or out_i64 (integer sums,
+ * integer min / max); out_valid bytes. */
 OR_EXPORT void or_rolling(const plgpu_column* c, int32_t kind, int64_t ws, int64_t min_periods, int32_t center,
                           int32_t mode, double* out_f64, int64_t* out_i64, uint8_t* out_valid) {
+    if (kind == 3 || kind == 4) {
+        or_rolling_minmax(c, kind, ws, min_periods, center, out_f64, out_i64, out_valid);
+        return;
+    }
     const int64_t n = c->length;
     const int isint = kind == 1 && c->dtype != PLGPU_F64;
     int has_nulls = 0;

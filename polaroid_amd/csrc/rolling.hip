@@ -488,18 +488,251 @@ __global__ void rl_direct_kernel(RlParams p) {
 
 using namespace plgpu;
 
+// ------------------------------------------------------- rolling min / max
+// polars-compute/src/rolling/{no_nulls,nulls}/min_max.rs (MinMaxWindow with
+// MinPropagateNan / MaxPropagateNan): a NaN in the window gives NaN, nulls
+// are skipped, fewer than min_periods values (or none) give null.
+// Values become order-preserving u64 codes in which NaN is the extreme that
+// wins (0 for min, ~0 for max) and a null is the identity, so a window's
+// answer is one unsigned min / max.  Windows of up to kMmDirect rows scan
+// their rows directly (neighbouring outputs share cached lines); longer
+// ones use van Herk / Gil-Werman: per aligned block of w rows, prefix and
+// suffix extrema, so every window -- full length w, or clipped at either end
+// of the column -- is min(suffix[s], prefix[e - 1]) in O(1).
+constexpr int64_t kMmDirect = 64;
+
+struct MmParams {
+    DevCol c;
+    int64_t n;
+    int64_t w;
+    int64_t min_periods;
+    int32_t center;
+    int32_t is_max;
+    int32_t isf;
+    int32_t out_dtype;
+    void* out;
+    uint64_t* out_valid;
+    uint64_t* pre;           // van Herk prefix codes (or null)
+    uint64_t* suf;           // van Herk suffix codes
+    const uint64_t* vcount;  // exclusive prefix counts of valid rows (nulls only), n + 1
+};
+
+__device__ __forceinline__ uint64_t mm_code(const MmParams& p, int64_t r) {
+    if (!dev_valid(p.c, r)) return p.is_max ? 0ull : ~0ull;
+    const uint64_t b = dev_load(p.c, r);
+    if (p.isf) {
+        if ((b & 0x7fffffffffffffffull) > 0x7ff0000000000000ull) return p.is_max ? ~0ull : 0ull;  // NaN wins
+        return ord_f64(b);
+    }
+    return b ^ 0x8000000000000000ull;  // ord_i64 of the sign-extended value
+}
+
+__device__ __forceinline__ uint64_t mm_best(const MmParams& p, uint64_t a, uint64_t b) {
+    return p.is_max ? (a > b ? a : b) : (a < b ? a : b);
+}
+
+__device__ __forceinline__ void mm_bounds(const MmParams& p, int64_t i, int64_t& s, int64_t& e) {
+    if (p.center) {
+        const int64_t right = (p.w + 1) / 2;
+        const int64_t left = p.w - right;
+        s = i > left ? i - left : 0;
+        e = i + right < p.n ? i + right : p.n;
+    } else {
+        s = i + 1 > p.w ? i + 1 - p.w : 0;
+        e = i + 1;
+    }
+}
+
+// One wave per aligned block of w rows: prefix and suffix extrema, 64 rows
+// at a time with a wave scan and a carried running extreme (coalesced).
+__global__ __launch_bounds__(256) void mm_blocks_kernel(MmParams p) {
+    const int64_t nb = (p.n + p.w - 1) / p.w;
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    const uint64_t ident = p.is_max ? 0ull : ~0ull;
+    for (int64_t b = wave; b < nb; b += waves) {
+        const int64_t lo = b * p.w, hi = lo + p.w < p.n ? lo + p.w : p.n;
+        uint64_t carry = ident;
+        for (int64_t c0 = lo; c0 < hi; c0 += 64) {
+            const int64_t r = c0 + lane;
+            uint64_t x = r < hi ? mm_code(p, r) : ident;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint64_t y = __shfl_up(x, off, 64);
+                if (lane >= off) x = mm_best(p, x, y);
+            }
+            x = mm_best(p, x, carry);
+            if (r < hi) p.pre[r] = x;
+            carry = __shfl(x, 63, 64);
+        }
+        carry = ident;
+        for (int64_t c1 = hi; c1 > lo; c1 -= 64) {
+            const int64_t r = c1 - 64 + lane;  // lanes below lo are outside the block
+            uint64_t x = r >= lo ? mm_code(p, r) : ident;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint64_t y = __shfl_down(x, off, 64);
+                if (lane + off < 64) x = mm_best(p, x, y);
+            }
+            x = mm_best(p, x, carry);
+            if (r >= lo) p.suf[r] = x;
+            carry = __shfl(x, 0, 64);
+        }
+    }
+}
+
+// Windows of up to kMmDirect rows: a workgroup stages the codes of its 1024
+// outputs' input span in LDS once (coalesced), then every output scans its
+// window there.
+constexpr int kMmTile = 1024;
+__global__ __launch_bounds__(256) void mm_direct_kernel(MmParams p) {
+    __shared__ uint64_t codes[kMmTile + kMmDirect];
+    const uint64_t ident = p.is_max ? 0ull : ~0ull;
+    const int64_t left = p.center ? p.w - (p.w + 1) / 2 : p.w - 1;  // rows before the output row
+    for (int64_t base = (int64_t)blockIdx.x * kMmTile; base < p.n; base += (int64_t)gridDim.x * kMmTile) {
+        const int64_t lo = base - left;  // may be negative
+        const int span = kMmTile + (int)p.w - 1;
+        for (int k = threadIdx.x; k < span; k += blockDim.x) {
+            const int64_t r = lo + k;
+            codes[k] = (r >= 0 && r < p.n) ? mm_code(p, r) : ident;
+        }
+        __syncthreads();
+        for (int k = threadIdx.x; k < kMmTile; k += blockDim.x) {
+            const int64_t i = base + k;
+            bool valid = false;
+            uint64_t v = 0;
+            if (i < p.n) {
+                int64_t s, e;
+                mm_bounds(p, i, s, e);
+                uint64_t best = ident;
+                for (int64_t r = s; r < e; ++r) best = mm_best(p, best, codes[r - lo]);
+                const int64_t cnt = p.vcount ? (int64_t)(p.vcount[e] - p.vcount[s]) : e - s;
+                valid = cnt >= p.min_periods && cnt > 0;
+                if (valid) {
+                    if (p.isf) v = best == (p.is_max ? ~0ull : 0ull) ? 0x7ff8000000000000ull : unord_f64(best);
+                    else v = best ^ 0x8000000000000000ull;
+                }
+                if (p.out_dtype == PLGPU_I32) ((int32_t*)p.out)[i] = (int32_t)v;
+                else ((uint64_t*)p.out)[i] = v;
+            }
+            const uint64_t wv = __ballot(valid);
+            if ((threadIdx.x & 63) == 0 && i < p.n) p.out_valid[i >> 6] = wv;
+        }
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(256) void mm_out_kernel(MmParams p) {
+    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x; i0 < p.n; i0 += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = i0 + threadIdx.x;
+        bool valid = false;
+        if (i < p.n) {
+            int64_t s, e;
+            mm_bounds(p, i, s, e);
+            uint64_t best;
+            if (p.pre) {
+                // [s, e) lies in one block, or spans two adjacent ones
+                best = (s / p.w == (e - 1) / p.w && s % p.w != 0) ? p.suf[s]
+                       : (s % p.w == 0 ? p.pre[e - 1] : mm_best(p, p.suf[s], p.pre[e - 1]));
+            } else {
+                best = p.is_max ? 0ull : ~0ull;
+                for (int64_t r = s; r < e; ++r) best = mm_best(p, best, mm_code(p, r));
+            }
+            const int64_t cnt = p.vcount ? (int64_t)(p.vcount[e] - p.vcount[s]) : e - s;
+            valid = cnt >= p.min_periods && cnt > 0;
+            uint64_t v = 0;
+            if (valid) {
+                if (p.isf) v = best == (p.is_max ? ~0ull : 0ull) ? 0x7ff8000000000000ull : unord_f64(best);
+                else v = best ^ 0x8000000000000000ull;
+            }
+            if (p.out_dtype == PLGPU_I32) ((int32_t*)p.out)[i] = (int32_t)v;
+            else ((uint64_t*)p.out)[i] = v;
+        }
+        const uint64_t wv = __ballot(valid);
+        if ((threadIdx.x & 63) == 0 && i < p.n) p.out_valid[i >> 6] = wv;
+    }
+}
+
+__global__ __launch_bounds__(256) void mm_valid_flags_kernel(DevCol c, int64_t n, uint8_t* __restrict__ f) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x)
+        f[r] = dev_valid(c, r) ? 1 : 0;
+}
+
+static int rolling_minmax(const plgpu_column* values, bool is_max, int64_t w, int64_t min_periods, bool center,
+                          plgpu_column* out, hipStream_t s) {
+    MmParams p;
+    std::memset(&p, 0, sizeof p);
+    p.c = dev_col(*values);
+    p.n = values->length;
+    p.w = w;
+    p.min_periods = min_periods;
+    p.center = center ? 1 : 0;
+    p.is_max = is_max ? 1 : 0;
+    p.isf = values->dtype == PLGPU_F64;
+    p.out_dtype = values->dtype;
+    int rc = make_owned_column(out, values->dtype, p.n, true, s);
+    if (rc || p.n == 0) return rc;
+    p.out = (void*)out->values;
+    p.out_valid = (uint64_t*)out->validity;
+    uint8_t* flags = nullptr;
+    uint64_t* vcount = nullptr;
+    uint64_t* part = nullptr;
+    hipError_t e = hipSuccess;
+    const unsigned g = (unsigned)std::min<int64_t>((p.n + 255) / 256, 256 * 32);
+    if (values->validity != nullptr) {
+        rc = dev_alloc((void**)&flags, p.n, s);
+        if (!rc) rc = dev_alloc((void**)&vcount, (p.n + 1) * 8, s);
+        if (!rc) rc = dev_alloc((void**)&part, ((p.n + kScanChunk - 1) / kScanChunk + 2) * 8, s);
+        if (!rc) {
+            mm_valid_flags_kernel<<<g, 256, 0, s>>>(p.c, p.n, flags);
+            e = hipGetLastError();
+            if (e == hipSuccess) e = scan_exclusive<uint8_t>(flags, p.n, vcount, part, s);
+            p.vcount = vcount;
+        }
+    }
+    if (!rc && e == hipSuccess && w > kMmDirect) {
+        rc = dev_alloc((void**)&p.pre, p.n * 8, s);
+        if (!rc) rc = dev_alloc((void**)&p.suf, p.n * 8, s);
+        if (!rc) {
+            const int64_t nb = (p.n + w - 1) / w;  // one wave (of 4 per workgroup) per block
+            mm_blocks_kernel<<<(unsigned)std::min<int64_t>((nb + 3) / 4, 256 * 64), 256, 0, s>>>(p);
+            e = hipGetLastError();
+        }
+        if (!rc && e == hipSuccess) {
+            mm_out_kernel<<<g, 256, 0, s>>>(p);
+            e = hipGetLastError();
+        }
+    } else if (!rc && e == hipSuccess) {
+        mm_direct_kernel<<<(unsigned)std::min<int64_t>((p.n + kMmTile - 1) / kMmTile, 256 * 64), 256, 0, s>>>(p);
+        e = hipGetLastError();
+    }
+    if (!rc && e == hipSuccess) e = hipStreamSynchronize(s);
+    if (!rc && e != hipSuccess) rc = hip_fail(e, "rolling min / max");
+    dev_free(flags, s);
+    dev_free(vcount, s);
+    dev_free(part, s);
+    dev_free(p.pre, s);
+    dev_free(p.suf, s);
+    if (rc) plgpu_column_release(out);
+    else out->null_count = -1;
+    return rc;
+}
+
 PLGPU_API int plgpu_rolling(const plgpu_column* values, int32_t kind, int64_t window_size, int64_t min_periods,
                             int32_t center, plgpu_column* out, void* stream) {
     hipStream_t s = as_stream(stream);
     if (values == nullptr || out == nullptr) return fail(PLGPU_ERR_INVALID, "NULL argument");
     std::memset(out, 0, sizeof *out);
-    if (kind != PLGPU_ROLLING_SUM && kind != PLGPU_ROLLING_MEAN) return fail(PLGPU_ERR_INVALID, "unknown rolling kind");
+    if (kind < PLGPU_ROLLING_SUM || kind > PLGPU_ROLLING_MAX) return fail(PLGPU_ERR_INVALID, "unknown rolling kind");
     if (values->dtype != PLGPU_F64 && values->dtype != PLGPU_I64 && values->dtype != PLGPU_I32)
         return fail(PLGPU_ERR_SCHEMA, "rolling input must be Float64 / Int64 / Int32");
     if (window_size < 1) return fail(PLGPU_ERR_INVALID, "window_size must be >= 1");
     if (min_periods < 0) return fail(PLGPU_ERR_INVALID, "min_periods must be >= 0");
     if (min_periods > window_size)
         return fail(PLGPU_ERR_INVALID, "`min_periods` should be <= `window_size`");
+    if (kind == PLGPU_ROLLING_MIN || kind == PLGPU_ROLLING_MAX)
+        return rolling_minmax(values, kind == PLGPU_ROLLING_MAX, window_size, min_periods, center != 0, out, s);
     RlParams p;
     std::memset(&p, 0, sizeof p);
     p.c.dtype = values->dtype;

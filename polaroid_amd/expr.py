@@ -148,6 +148,16 @@ class Expr:
         """Fixed-window mean (Expr.rolling_mean)."""
         return _rolling(self, "mean", window_size, weights, min_samples, center)
 
+    def rolling_min(self, window_size: int, weights=None, *, min_samples: int | None = None,
+                    center: bool = False) -> "Expr":
+        """Fixed-window minimum (Expr.rolling_min; a NaN in the window propagates)."""
+        return _rolling(self, "min", window_size, weights, min_samples, center)
+
+    def rolling_max(self, window_size: int, weights=None, *, min_samples: int | None = None,
+                    center: bool = False) -> "Expr":
+        """Fixed-window maximum (Expr.rolling_max; a NaN in the window propagates)."""
+        return _rolling(self, "max", window_size, weights, min_samples, center)
+
     def sort(self, *, descending: bool = False, nulls_last: bool = False) -> "Expr":
         return Expr("sort", (self,), op="sort", value=(bool(descending), bool(nulls_last)))
 

@@ -431,6 +431,18 @@ class Series:
             raise N.InvalidOperationError("weighted rolling windows are not supported on the GPU executor")
         return self._rolling(N.ROLLING["mean"], window_size, min_samples, center)
 
+    def rolling_min(self, window_size: int, weights=None, *, min_samples: int | None = None,
+                    center: bool = False) -> "Series":
+        if weights is not None:
+            raise N.InvalidOperationError("weighted rolling windows are not supported on the GPU executor")
+        return self._rolling(N.ROLLING["min"], window_size, min_samples, center)
+
+    def rolling_max(self, window_size: int, weights=None, *, min_samples: int | None = None,
+                    center: bool = False) -> "Series":
+        if weights is not None:
+            raise N.InvalidOperationError("weighted rolling windows are not supported on the GPU executor")
+        return self._rolling(N.ROLLING["max"], window_size, min_samples, center)
+
     # eager conveniences mirroring Series.filter ------------------------------
     def filter(self, mask: "Series") -> "Series":
         out = (N.Column * 1)()

@@ -581,6 +581,28 @@ def rolling_cases():
     cases.append({"name": "test_rolling_sum_stability_11146 (last value)",
                   "source": "operations/rolling/test_rolling.py:1476-1510",
                   "values": stab, "kind": "mean", "window": 8, "min": 1, "center": False, "expected_last": 0.0})
+    # rolling_min / rolling_max (MinMaxWindow, NaN propagates)
+    src = "operations/rolling/test_rolling.py:322-362 (sorted data; the shuffled half needs polars' RNG)"
+    cols = {"col1": [0, 1, 2, 3, 4, 5, 6], "col2": [6, 5, 4, 3, 2, 1, 0],
+            "col1_nulls": [None, None, 2, 3, 4, 5, 6], "col2_nulls": [None, None, 4, 3, 2, 1, 0]}
+    emin = {"col1": [None, None, 0, 1, 2, 3, 4], "col2": [None, None, 4, 3, 2, 1, 0],
+            "col1_nulls": [None, None, None, None, 2, 3, 4], "col2_nulls": [None, None, None, None, 2, 1, 0]}
+    emax = {"col1": [None, None, 2, 3, 4, 5, 6], "col2": [None, None, 6, 5, 4, 3, 2],
+            "col1_nulls": [None, None, None, None, 4, 5, 6], "col2_nulls": [None, None, None, None, 4, 3, 2]}
+    for kind, exp in (("min", emin), ("max", emax)):
+        for name, vals in cols.items():
+            cases.append({"name": f"test_rolling_extrema {name} rolling_{kind}(3)", "source": src,
+                          "values": vals, "kind": kind, "window": 3, "min": None, "center": False,
+                          "expected": exp[name]})
+    for kind, exp in (("min", [None, 1, 2, 2, 1]), ("max", [None, 2, 3, 3, 2])):
+        cases.append({"name": f"test_rolling_ints rolling_{kind}(2)", "source": "operations/rolling/test_rolling.py:873-880",
+                      "values": [1, 2, 3, 2, 1], "kind": kind, "window": 2, "min": None, "center": False,
+                      "expected": exp})
+    for kind in ("min", "max"):
+        cases.append({"name": f"test_rolling_nan rolling_{kind}(3): 2 nulls, 5 NaN-or-null",
+                      "source": "operations/rolling/test_rolling.py:924-933",
+                      "values": [1.0, 2.0, 3.0, nan, 5.0, 6.0, 7.0], "kind": kind, "window": 3, "min": None,
+                      "center": False, "expected_null_count": 2, "expected_nan_or_null": 5})
     return {"cases": cases}
 
 

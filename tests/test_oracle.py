@@ -248,6 +248,10 @@ def test_oracle_rolling_golden():
         for mode in (O.ROLLING_REFERENCE, O.ROLLING_EXACT):
             out, ok = O.rolling(col, case["kind"], case["window"], case["min"], case["center"], mode)
             got = [v.item() if k else None for v, k in zip(out, ok)]
+            if "expected_null_count" in case:
+                assert sum(g is None for g in got) == case["expected_null_count"], case["name"]
+                assert sum(g is None or g != g for g in got) == case["expected_nan_or_null"], case["name"]
+                continue
             if "expected_last" in case:
                 assert got[-1] == case["expected_last"], (case["name"], mode)
                 continue
