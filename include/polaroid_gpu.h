@@ -354,6 +354,14 @@ int plgpu_join_multi(const plgpu_column* left_keys, const plgpu_column* right_ke
 int plgpu_str_compare(const plgpu_column* a, const plgpu_column* b, const uint8_t* lit, int64_t lit_len, int32_t op,
                       plgpu_column* out, void* stream);
 
+/* Short-string codes: each string of at most 7 bytes as the Int64
+ * (length << 56) | bytes (little-endian), exact and injective, so String
+ * keys can cross the integer-keyed paths (the multi-GPU group-by's partial
+ * states and exchange); *all_short = 0 if some string is longer (its code
+ * is then 0).  Validity is carried.  plgpu_str_decode_short is the inverse. */
+int plgpu_str_encode_short(const plgpu_column* strs, plgpu_column* out_codes, int32_t* all_short, void* stream);
+int plgpu_str_decode_short(const plgpu_column* codes, plgpu_column* out, void* stream);
+
 /* out[i] = a[i] if valid, else b[i] (same dtype and length); the coalesced
  * key columns of a full join with coalesce=True
  * (polars-ops/src/frame/join/general.rs:52 _coalesce_full_join). */

@@ -200,15 +200,25 @@ int str_gather(const DevCol& src, const uint32_t* idx32, const int64_t* idx64, c
 // `words`: the data buffer is 8-byte aligned and `data_end` (= the last
 // offset) bounds the aligned 8-byte word loads, so a string's bytes come in
 // one or two word loads and a funnel shift instead of byte loads.
+// `out_valid` (optional): the strings' validity re-based to offset 0, one
+// ballot word per 64 rows.
 __global__ __launch_bounds__(kStrThreads) void str_code_kernel(DevCol src, int64_t n, uint64_t* __restrict__ codes,
                                                                unsigned long long* __restrict__ any_long,
-                                                               bool words, int64_t data_end) {
+                                                               bool words, int64_t data_end,
+                                                               uint64_t* __restrict__ out_valid) {
     const int64_t* off = (const int64_t*)src.values;
     const uint64_t* dw = (const uint64_t*)src.data;
     bool lng = false;
-    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+    for (int64_t r0 = (int64_t)blockIdx.x * blockDim.x; r0 < n; r0 += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = r0 + threadIdx.x;
+        const bool vr = r < n && dev_valid(src, r);
+        if (out_valid) {
+            const uint64_t wv = __ballot(vr);
+            if ((threadIdx.x & 63) == 0 && r < n) out_valid[r >> 6] = wv;
+        }
+        if (r >= n) continue;
         uint64_t code = 0;
-        if (dev_valid(src, r)) {
+        if (vr) {
             const int64_t b = off[src.offset + r], len = off[src.offset + r + 1] - b;
             if (len > 7) {
                 lng = true;
@@ -274,7 +284,7 @@ int str_short_codes(const plgpu_column& src, plgpu_column* out, bool* all_short,
         if (e == hipSuccess && n > 0) {
             const int g = (int)std::min<int64_t>((n + kStrThreads - 1) / kStrThreads, (int64_t)num_cus_str() * 16);
             const bool words = ((uintptr_t)src.data & 7) == 0;
-            str_code_kernel<<<g, kStrThreads, 0, s>>>(dev_col(src), n, codes, flag, words, data_end);
+            str_code_kernel<<<g, kStrThreads, 0, s>>>(dev_col(src), n, codes, flag, words, data_end, nullptr);
             e = hipGetLastError();
         }
         if (e == hipSuccess) e = hipMemcpyAsync(&hf, flag, 8, hipMemcpyDeviceToHost, s);
@@ -443,4 +453,49 @@ PLGPU_API int plgpu_str_compare(const plgpu_column* a, const plgpu_column* b, co
     dev_free(dlit, s);
     if (rc) plgpu_column_release(out);
     return rc;
+}
+
+PLGPU_API int plgpu_str_encode_short(const plgpu_column* strs, plgpu_column* out_codes, int32_t* all_short,
+                                     void* stream) {
+    hipStream_t s = as_stream(stream);
+    if (strs == nullptr || out_codes == nullptr || all_short == nullptr) return fail(PLGPU_ERR_INVALID, "NULL argument");
+    std::memset(out_codes, 0, sizeof *out_codes);
+    if (strs->dtype != PLGPU_STR) return fail(PLGPU_ERR_SCHEMA, "short-string codes of a non-String column");
+    const int64_t n = strs->length;
+    int rc = make_owned_column(out_codes, PLGPU_I64, n, strs->validity != nullptr, s);
+    if (rc) return rc;
+    unsigned long long* flag = nullptr;
+    unsigned long long hf = 0;
+    rc = dev_alloc((void**)&flag, 8, s);
+    if (!rc) {
+        int64_t data_end = 0;
+        hipError_t e = hipMemsetAsync(flag, 0, 8, s);
+        if (e == hipSuccess && n > 0)
+            e = hipMemcpyAsync(&data_end, (const int64_t*)strs->values + strs->offset + n, 8, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e == hipSuccess && n > 0) {
+            const int g = (int)std::min<int64_t>((n + kStrThreads - 1) / kStrThreads, (int64_t)num_cus_str() * 16);
+            str_code_kernel<<<g, kStrThreads, 0, s>>>(dev_col(*strs), n, (uint64_t*)out_codes->values, flag,
+                                                      ((uintptr_t)strs->data & 7) == 0, data_end,
+                                                      (uint64_t*)out_codes->validity);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) e = hipMemcpyAsync(&hf, flag, 8, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) rc = hip_fail(e, "short-string codes");
+    }
+    dev_free(flag, s);
+    if (rc) {
+        plgpu_column_release(out_codes);
+        return rc;
+    }
+    *all_short = hf == 0 ? 1 : 0;
+    return PLGPU_OK;
+}
+
+PLGPU_API int plgpu_str_decode_short(const plgpu_column* codes, plgpu_column* out, void* stream) {
+    if (codes == nullptr || out == nullptr) return fail(PLGPU_ERR_INVALID, "NULL argument");
+    std::memset(out, 0, sizeof *out);
+    if (codes->dtype != PLGPU_I64) return fail(PLGPU_ERR_SCHEMA, "short-string codes must be Int64");
+    return str_from_codes(*codes, out, as_stream(stream));
 }

@@ -231,12 +231,28 @@ def group_by_agg(df, key: str, aggs: Sequence[Expr], predicate: Expr | None = No
     device = _device_for(group)
     if device.type != "cuda":
         raise N.InvalidOperationError("the GPU group-by needs the nccl (RCCL) backend")
+    from .frame import DataFrame, Series, String
+
     aggs = [a if isinstance(a, Expr) else col(a) for a in aggs]
+    string_key = isinstance(key, str) and key in df.columns and df[key].dtype is String
+    if string_key:
+        # String symbols of <= 7 bytes cross the integer-keyed protocol as
+        # exact Int64 codes (the same code on every rank); decoded at the end
+        codes = N.Column()
+        short = C.c_int32(0)
+        N.check(N.lib().plgpu_str_encode_short(C.byref(df[key]._col), C.byref(codes), C.byref(short), None))
+        if _allreduce_max([0 if short.value else 1], group, device)[0]:
+            raise N.InvalidOperationError("the multi-GPU group-by takes String keys of at most 7 bytes")
+        df = DataFrame([Series._from_native(key, codes) if nm == key else df[nm] for nm in df.columns])
     g = _gb_lower(df, key, list(aggs), predicate)
     if g.keycol.dtype not in (N.I64, N.I32) or len(g.keys) != 1:
-        raise N.InvalidOperationError("the multi-GPU group-by takes one Int64 / Int32 key column")
+        raise N.InvalidOperationError("the multi-GPU group-by takes one Int64 / Int32 (or short String) key column")
     part = GpuPartial(g, world)
     out, mi = run_partitioned(part, world, group, device)
+    if string_key:
+        strs = N.Column()
+        N.check(N.lib().plgpu_str_decode_short(C.byref(out[key]._col), C.byref(strs), None))
+        out = DataFrame([Series._from_native(key, strs) if nm == key else out[nm] for nm in out.columns])
     torch.cuda.synchronize()
     if info is not None:
         d = part.info.as_dict()

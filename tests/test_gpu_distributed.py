@@ -196,3 +196,37 @@ def test_group_by_agg_world1_rccl(gpu):
         assert info["groups"] == ref.height
     finally:
         dist.destroy_process_group()
+
+
+def test_group_by_agg_world1_rccl_string_key(gpu):
+    """The multi-GPU group-by with a String symbol key (<= 7 bytes: exact
+    Int64 codes through the partial-state exchange), one RCCL rank, against
+    the single-GPU group-by; a longer key is refused."""
+    import torch.distributed as dist
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        rng = np.random.default_rng(4)
+        n = 200_000
+        pool = np.array(["AAPL", "MSFT", "", "BRK.B", "日本", "x"] + [f"S{i:04d}" for i in range(200)], dtype=object)
+        sym = pool[rng.integers(0, pool.size, n)]
+        sv = rng.random(n) > 0.02
+        v = rng.standard_normal(n)
+        df = pl.DataFrame({"sym": pl.Series.from_numpy("sym", sym, sv), "v": pl.Series.from_numpy("v", v)})
+        out = D.group_by_agg(df, "sym", [pl.col("v").sum().alias("s"), pl.len()], pl.col("v") > -1.0)
+        ref = df.lazy().filter(pl.col("v") > -1.0).group_by("sym").agg(pl.col("v").sum().alias("s"),
+                                                                        pl.len()).collect()
+        assert out["sym"].dtype == pl.String
+        got = sorted(zip(out["sym"].to_list(), out["s"].to_list(), out["len"].to_list()), key=str)
+        exp = sorted(zip(ref["sym"].to_list(), ref["s"].to_list(), ref["len"].to_list()), key=str)
+        assert got == exp
+        long_df = pl.DataFrame({"sym": pl.Series("sym", ["AAPL", "TOOLONGKEY"]), "v": pl.Series("v", [1.0, 2.0])})
+        with pytest.raises(pl.InvalidOperationError, match="7 bytes"):
+            D.group_by_agg(long_df, "sym", [pl.col("v").sum()])
+    finally:
+        dist.destroy_process_group()
