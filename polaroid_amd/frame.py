@@ -341,6 +341,15 @@ class Series:
 
         if isinstance(arr, pa.ChunkedArray):
             arr = arr.combine_chunks() if arr.num_chunks != 1 else arr.chunk(0)
+        if pa.types.is_dictionary(arr.type):
+            # polars Categorical / Enum: the dictionary and the indices go to
+            # the device as they are, and the strings are gathered there
+            # (a null index gathers a null)
+            dictionary = cls.from_arrow(name, arr.dictionary)
+            if dictionary.dtype is not String:
+                raise N.InvalidOperationError(f"column {name!r}: dictionary of {arr.dictionary.type} is not supported")
+            idx = cls.from_arrow("__idx", arr.indices.cast(pa.uint32()))
+            return dictionary.gather(idx).alias(name)
         m = {pa.int64(): Int64, pa.int32(): Int32, pa.uint32(): UInt32, pa.float64(): Float64,
              pa.bool_(): Boolean}
         if arr.type in (pa.string(), pa.large_string(), pa.utf8(), pa.large_utf8()):

@@ -262,6 +262,22 @@ def run_plan(plan: tuple, n_rows: int | None = None, to_frame=None):
     return (to_frame or _to_polars)(table)
 
 
+def _restore_dtypes(df, schema: dict):
+    """Categorical / Enum columns run on the GPU as their strings (the
+    dictionary gathered on the device); the result gets the dtype the plan's
+    schema names back."""
+    cols = getattr(df, "columns", None)
+    if not schema or cols is None or not hasattr(df, "with_columns"):
+        return df
+    casts = []
+    for name, dt in schema.items():
+        if name in cols and str(dt).startswith(("Categorical", "Enum")) and str(df.schema[name]) != str(dt):
+            import polars
+
+            casts.append(polars.col(name).cast(dt))
+    return df.with_columns(casts) if casts else df
+
+
 def _config_flag(config: Any, name: str, default: bool = False) -> bool:
     """Read a flag from a polars GPUEngine (attribute) or a plain dict."""
     if config is None:
@@ -279,6 +295,7 @@ def execute_with_polaroid(nt, duration_since_start: int | None = None, *, config
     `raise_on_fail`)."""
     try:
         plan = translate(nt)
+        schema = dict(nt.get_schema()) if hasattr(nt, "get_schema") else {}
     except Unsupported as exc:
         if _config_flag(config, "raise_on_fail"):
             raise N.InvalidOperationError(f"query is not supported by the MI355X engine: {exc}") from exc
@@ -286,7 +303,7 @@ def execute_with_polaroid(nt, duration_since_start: int | None = None, *, config
     N.lib()  # a GPU plan was accepted: the HIP library must be present
 
     def _udf(with_columns, predicate, n_rows, should_time=False):
-        df = run_plan(plan, n_rows, to_frame)
+        df = _restore_dtypes(run_plan(plan, n_rows, to_frame), schema)
         if with_columns is not None:
             df = df.select(with_columns)
         if should_time:

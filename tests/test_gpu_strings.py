@@ -269,3 +269,24 @@ def test_string_predicates(gpu, n):
     assert g["w"].to_list() == keys
     for k, v in zip(keys, g["x"].to_list()):
         assert v == O.fsum(np.array([x[i] for i in sel if wl[i] == k]))
+
+
+def test_dictionary_columns_from_arrow(gpu):
+    """polars Categorical / Enum columns arrive as Arrow dictionary arrays:
+    the dictionary and indices are uploaded and the strings gathered on the
+    GPU (a null index gives a null); they then group / join / filter as
+    String columns."""
+    import pyarrow as pa
+
+    vals = ["AAPL", "MSFT", None, "AAPL", "BRK.B", "MSFT", "AAPL", None]
+    darr = pa.array(vals).dictionary_encode()
+    for a in (darr, darr.slice(1, 6), pa.chunked_array([darr.slice(0, 3), darr.slice(3)])):
+        s = pl.Series.from_arrow("sym", a)
+        assert s.dtype == pl.String and s.to_list() == a.to_pylist()
+    t = pa.table({"sym": darr, "v": pa.array(np.arange(8, dtype=np.float64))})
+    df = pl.DataFrame.from_arrow(t)
+    g = df.group_by("sym", maintain_order=True).agg(pl.col("v").sum())
+    assert g["sym"].to_list() == ["AAPL", "MSFT", None, "BRK.B"]
+    assert g["v"].to_list() == [0.0 + 3 + 6, 1.0 + 5, 2.0 + 7, 4.0]
+    f = df.filter(pl.col("sym") == "MSFT")
+    assert f["v"].to_list() == [1.0, 5.0]
