@@ -106,7 +106,13 @@ enum plgpu_opcode {
     PLGPU_OP_IS_NULL = 33,
     PLGPU_OP_IS_NOT_NULL = 34,
     PLGPU_OP_IS_NAN = 35,
-    PLGPU_OP_IS_FINITE = 36
+    PLGPU_OP_IS_FINITE = 36,
+    /* String literal pattern tests (plgpu_str_compare only):
+     * polars-ops/src/chunked_array/binary/namespace.rs:85 starts_with, :78
+     * ends_with, strings/namespace.rs:332 contains_literal */
+    PLGPU_OP_STR_STARTS_WITH = 40,
+    PLGPU_OP_STR_ENDS_WITH = 41,
+    PLGPU_OP_STR_CONTAINS = 42
 };
 
 typedef struct plgpu_instr {
@@ -346,7 +352,8 @@ int plgpu_join_multi(const plgpu_column* left_keys, const plgpu_column* right_ke
 
 /* Boolean column of a comparison of String column `a` with String column
  * `b`, or (b == NULL) with the literal `lit` (lit_len bytes, host memory):
- * op = PLGPU_OP_EQ .. PLGPU_OP_NE_MISSING; or IS_NULL / IS_NOT_NULL of `a`.
+ * op = PLGPU_OP_EQ .. PLGPU_OP_NE_MISSING; or IS_NULL / IS_NOT_NULL of `a`;
+ * or PLGPU_OP_STR_{STARTS_WITH,ENDS_WITH,CONTAINS} against the literal.
  * Bytes compare lexicographically (a proper prefix first); a null operand
  * gives null except for the *_MISSING ops.  Replaces
  * polars-compute/src/comparisons/view.rs TotalEqKernel / TotalOrdKernel for

@@ -27,6 +27,7 @@ OP = dict(
     ADD=10, SUB=11, MUL=12, TRUEDIV=13, NEG=14, ABS=15, CAST_F64=16,
     EQ=20, NE=21, LT=22, LE=23, GT=24, GE=25, EQ_MISSING=26, NE_MISSING=27,
     AND=30, OR=31, NOT=32, IS_NULL=33, IS_NOT_NULL=34, IS_NAN=35, IS_FINITE=36,
+    STR_STARTS_WITH=40, STR_ENDS_WITH=41, STR_CONTAINS=42,
 )
 AGG = dict(sum=1, mean=2, min=3, max=4, count=5, len=6, first=7, last=8)
 MAX_COLS = 8

@@ -378,6 +378,26 @@ __global__ __launch_bounds__(kStrThreads) void str_cmp_kernel(DevCol a, DevCol b
             if (op == PLGPU_OP_IS_NULL || op == PLGPU_OP_IS_NOT_NULL) {
                 res = (op == PLGPU_OP_IS_NULL) ? !va : va;
                 valid = true;
+            } else if (op >= PLGPU_OP_STR_STARTS_WITH) {
+                // literal pattern tests; a null string gives null
+                valid = va;
+                if (va) {
+                    const int64_t sa = oa[a.offset + r], la = oa[a.offset + r + 1] - sa;
+                    const uint8_t* x = a.data + sa;
+                    if (op == PLGPU_OP_STR_STARTS_WITH || op == PLGPU_OP_STR_ENDS_WITH) {
+                        const int64_t base = op == PLGPU_OP_STR_STARTS_WITH ? 0 : la - lit_len;
+                        res = lit_len <= la;
+                        for (int64_t j = 0; res && j < lit_len; ++j) res = x[base + j] == lit[j];
+                    } else {  // contains (literal): naive scan, first-byte filter
+                        res = lit_len == 0;
+                        for (int64_t p0 = 0; !res && p0 + lit_len <= la; ++p0) {
+                            if (x[p0] != lit[0]) continue;
+                            bool m = true;
+                            for (int64_t j = 1; m && j < lit_len; ++j) m = x[p0 + j] == lit[j];
+                            res = m;
+                        }
+                    }
+                }
             } else {
                 const bool vb = ob == nullptr || dev_valid(b, r);
                 int c = 0;
@@ -426,8 +446,10 @@ PLGPU_API int plgpu_str_compare(const plgpu_column* a, const plgpu_column* b, co
     if (a->dtype != PLGPU_STR || (b && b->dtype != PLGPU_STR))
         return fail(PLGPU_ERR_SCHEMA, "string comparison of a non-String column");
     const bool unary = op == PLGPU_OP_IS_NULL || op == PLGPU_OP_IS_NOT_NULL;
-    if (!unary && (op < PLGPU_OP_EQ || op > PLGPU_OP_NE_MISSING))
+    const bool pattern = op >= PLGPU_OP_STR_STARTS_WITH && op <= PLGPU_OP_STR_CONTAINS;
+    if (!unary && !pattern && (op < PLGPU_OP_EQ || op > PLGPU_OP_NE_MISSING))
         return fail(PLGPU_ERR_INVALID, "unsupported string comparison");
+    if (pattern && b != nullptr) return fail(PLGPU_ERR_INVALID, "string pattern tests take a literal");
     if (!unary && b == nullptr && lit_len > 0 && lit == nullptr) return fail(PLGPU_ERR_INVALID, "NULL literal");
     if (b && b->length != a->length) return fail(PLGPU_ERR_SHAPE, "compared columns differ in length");
     const int64_t n = a->length;

@@ -118,6 +118,11 @@ class Expr:
     def is_nan(self): return Expr("un", (self,), op="is_nan")
     def is_finite(self): return Expr("un", (self,), op="is_finite")
 
+    @property
+    def str(self) -> "_StrNamespace":
+        """String functions (Expr.str): literal pattern tests."""
+        return _StrNamespace(self)
+
     def cast(self, dtype) -> "Expr":
         from .frame import Float64
         if dtype is Float64 or dtype == "f64":
@@ -220,6 +225,30 @@ def first(name: str) -> Expr:
 
 def last(name: str) -> Expr:
     return col(name).last()
+
+
+class _StrNamespace:
+    """Expr.str: starts_with / ends_with / contains(literal=True), evaluated
+    on the GPU as Boolean columns (frame._lower_strings)."""
+
+    def __init__(self, e: Expr):
+        self._e = e
+
+    def _fn(self, op: str, pattern) -> Expr:
+        if not isinstance(pattern, str):
+            raise N.InvalidOperationError(f"str.{op} takes a string literal on the GPU executor")
+        return Expr("strfn", (self._e,), op=op, value=pattern)
+
+    def starts_with(self, prefix: str) -> Expr:
+        return self._fn("starts_with", prefix)
+
+    def ends_with(self, suffix: str) -> Expr:
+        return self._fn("ends_with", suffix)
+
+    def contains(self, pattern: str, *, literal: bool = False, strict: bool = True) -> Expr:
+        if not literal and any(ch in pattern for ch in ".^$*+?()[]{}|\\"):
+            raise N.InvalidOperationError("regex patterns are not supported on the GPU executor (use literal=True)")
+        return self._fn("contains", pattern)
 
 
 _BIN_OPS = {

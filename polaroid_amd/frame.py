@@ -774,6 +774,14 @@ def _lower_strings(expr: Expr, df: DataFrame) -> tuple[Expr, DataFrame]:
                 N.check(N.lib().plgpu_str_compare(C.byref(ac), None, lit_b, builtins.len(lit_b),
                                                   N.OP[_CMP_OPS[op]], C.byref(out), None))
             return new_col(out)
+        if e.kind == "strfn":
+            if e.args[0].kind != "col" or not is_str(e.args[0]):
+                raise N.InvalidOperationError(f"{e!r}: str functions take a String column")
+            out = N.Column()
+            pat = e.value.encode()
+            N.check(N.lib().plgpu_str_compare(C.byref(df._cols[e.args[0].value]._col), None, pat, builtins.len(pat),
+                                              N.OP["STR_" + e.op.upper()], C.byref(out), None))
+            return new_col(out)
         if e.kind == "un" and e.op in ("is_null", "is_not_null") and is_str(e.args[0]) and e.args[0].kind == "col":
             out = N.Column()
             N.check(N.lib().plgpu_str_compare(C.byref(df._cols[e.args[0].value]._col), None, None, 0,

@@ -290,3 +290,24 @@ def test_dictionary_columns_from_arrow(gpu):
     assert g["v"].to_list() == [0.0 + 3 + 6, 1.0 + 5, 2.0 + 7, 4.0]
     f = df.filter(pl.col("sym") == "MSFT")
     assert f["v"].to_list() == [1.0, 5.0]
+
+
+def test_string_pattern_predicates(gpu):
+    """str.starts_with / ends_with / contains(literal): byte-wise tests, a
+    null string gives null (binary/namespace.rs starts_with / ends_with,
+    strings/namespace.rs contains_literal)."""
+    rng = np.random.default_rng(12)
+    n = 50_000
+    w, wv = _words(rng, n, 60, long_frac=0.01)
+    wl = [s if ok else None for s, ok in zip(w, wv)]
+    df = pl.DataFrame({"w": pl.Series.from_numpy("w", w, wv), "i": pl.Series.from_numpy("i", np.arange(n))})
+    for pat in ("", "s", "sym0001", "AAPL", "日", "long-", "9", "x" * 9, "zz"):
+        for fn, ref in (("starts_with", str.startswith), ("ends_with", str.endswith),
+                        ("contains", lambda s, p: p in s)):
+            e = getattr(pl.col("w").str, fn)(pat) if fn != "contains" else pl.col("w").str.contains(pat, literal=True)
+            got = df.select(e.alias("m"))["m"].to_list()
+            assert got == [None if s is None else ref(s, pat) for s in wl], (fn, pat)
+    out = df.filter(pl.col("w").str.starts_with("sym000") & (pl.col("i") > 1000))
+    assert out["i"].to_list() == [i for i in range(n) if wl[i] is not None and wl[i].startswith("sym000") and i > 1000]
+    with pytest.raises(pl.InvalidOperationError, match="regex"):
+        df.filter(pl.col("w").str.contains("a.*b"))
