@@ -361,6 +361,16 @@ int plgpu_join_multi(const plgpu_column* left_keys, const plgpu_column* right_ke
 int plgpu_str_compare(const plgpu_column* a, const plgpu_column* b, const uint8_t* lit, int64_t lit_len, int32_t op,
                       plgpu_column* out, void* stream);
 
+/* Group variance / standard deviation from per-group sums of squared
+ * deviations (Float64) and non-null counts (UInt32 / Int64): null when
+ * count <= ddof, else sum_sq / (count - ddof) (negative clamped to 0), the
+ * square root when take_sqrt.  Replaces polars-compute/src/moment.rs:126
+ * VarState::finalize as used by polars-expr/src/reduce/var_std.rs.  The
+ * executor computes the sums with two exact group-by passes around the
+ * per-row group mean (polaroid_amd/frame.py:_group_by_var). */
+int plgpu_var_finalize(const plgpu_column* sum_sq, const plgpu_column* count, int32_t ddof, int32_t take_sqrt,
+                       plgpu_column* out, void* stream);
+
 /* Short-string codes: each string of at most 7 bytes as the Int64
  * (length << 56) | bytes (little-endian), exact and injective, so String
  * keys can cross the integer-keyed paths (the multi-GPU group-by's partial

@@ -2887,3 +2887,54 @@ PLGPU_API int plgpu_group_by_agg_multi(const plgpu_column* keys, int32_t nkeys, 
         for (int i = 0; i < nkeys; ++i) plgpu_column_release(&out_keys[i]);
     return rc;
 }
+
+// ------------------------------------------------------- var / std finalize
+// polars-compute/src/moment.rs:126 VarState::finalize (used by
+// polars-expr/src/reduce/var_std.rs): null when the non-null count is <=
+// ddof, else sum of squared deviations / (count - ddof), a negative value
+// clamped to 0 (NaN propagates); std takes the square root.
+__global__ __launch_bounds__(256) void var_finalize_kernel(DevCol ss, DevCol cnt, int64_t n, int32_t ddof,
+                                                           int32_t take_sqrt, double* __restrict__ out,
+                                                           uint64_t* __restrict__ out_valid) {
+    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x; i0 < n; i0 += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = i0 + threadIdx.x;
+        bool valid = false;
+        if (i < n) {
+            const uint64_t c = dev_valid(cnt, i) ? dev_load(cnt, i) : 0;
+            double v = 0.0;
+            if (c > (uint64_t)ddof && dev_valid(ss, i)) {
+                v = as_f64(dev_load(ss, i)) / (double)(c - (uint64_t)ddof);
+                if (v < 0.0) v = 0.0;
+                if (take_sqrt) v = __builtin_sqrt(v);
+                valid = true;
+            }
+            out[i] = v;
+        }
+        const uint64_t w = __ballot(valid);
+        if ((threadIdx.x & 63) == 0 && i < n) out_valid[i >> 6] = w;
+    }
+}
+
+PLGPU_API int plgpu_var_finalize(const plgpu_column* sum_sq, const plgpu_column* count, int32_t ddof,
+                                 int32_t take_sqrt, plgpu_column* out, void* stream) {
+    hipStream_t s = as_stream(stream);
+    if (sum_sq == nullptr || count == nullptr || out == nullptr) return fail(PLGPU_ERR_INVALID, "NULL argument");
+    std::memset(out, 0, sizeof *out);
+    if (sum_sq->dtype != PLGPU_F64 || (count->dtype != PLGPU_U32 && count->dtype != PLGPU_I64))
+        return fail(PLGPU_ERR_SCHEMA, "var finalize takes Float64 sums and UInt32 / Int64 counts");
+    if (sum_sq->length != count->length) return fail(PLGPU_ERR_SHAPE, "columns differ in length");
+    if (ddof < 0 || ddof > 255) return fail(PLGPU_ERR_INVALID, "ddof must be 0..255");
+    const int64_t n = sum_sq->length;
+    int rc = make_owned_column(out, PLGPU_F64, n, true, s);
+    if (rc || n == 0) return rc;
+    const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
+    var_finalize_kernel<<<g, 256, 0, s>>>(to_dev(*sum_sq), to_dev(*count), n, ddof, take_sqrt,
+                                          (double*)out->values, (uint64_t*)out->validity);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) {
+        plgpu_column_release(out);
+        return hip_fail(e, "var finalize");
+    }
+    return PLGPU_OK;
+}

@@ -139,6 +139,8 @@ class Expr:
     def max(self): return Expr("agg", (self,), op="max")
     def count(self): return Expr("agg", (self,), op="count")
     def len(self): return Expr("agg", (self,), op="len")
+    def std(self, ddof: int = 1): return Expr("agg", (self,), op="std", value=int(ddof))
+    def var(self, ddof: int = 1): return Expr("agg", (self,), op="var", value=int(ddof))
     def first(self): return Expr("agg", (self,), op="first")
     def last(self): return Expr("agg", (self,), op="last")
 

@@ -984,8 +984,69 @@ def _gb_frame(g: _GbCall, out_key, out_aggs) -> DataFrame:
     return DataFrame(series)
 
 
+def _agg_base(e: Expr) -> Expr:
+    return e.args[0] if e.kind == "alias" else e
+
+
+def _group_by_var(df: DataFrame, key: str | tuple, aggs: list[Expr], maintain_order: bool,
+                  pred: Expr | None, info: dict | None) -> DataFrame:
+    """group_by().agg() with var / std (polars-expr/src/reduce/var_std.rs),
+    composed of GPU passes:
+      1. the exact group-by with sum(x) and count(x) of every var / std
+         column next to the other aggregations (first-occurrence order);
+      2. every row's group mean, by a left join of the rows with the groups'
+         means (null keys match: they form a group);
+      3. d = (x - mean)^2 per row (one rounding), exactly summed per group
+         by a second group-by with the same predicate (same group order);
+      4. plgpu_var_finalize: null when count <= ddof, else sum / (count - ddof),
+         square root for std.
+    The reference's Welford state (moment.rs VarState) rounds differently;
+    the results agree to ~1e-13 relative (tests/test_gpu_first_last.py)."""
+    keys = list(_gb_keys(key))
+    var_cols: list[str] = []
+    plain: list[tuple[int, Expr]] = []
+    for i, e in enumerate(aggs):
+        b = _agg_base(e)
+        if b.kind == "agg" and b.op in ("std", "var"):
+            if b.args[0].kind != "col":
+                raise N.InvalidOperationError("var / std of a computed expression is not supported")
+            if b.args[0].value not in var_cols:
+                var_cols.append(b.args[0].value)
+        else:
+            plain.append((i, e))
+    helpers = []
+    for c in var_cols:
+        helpers += [col(c).sum().alias(f"__vs_{c}"), col(c).count().alias(f"__vn_{c}")]
+    first = _group_by(df, key, [e for _, e in plain] + helpers, True, pred, info)
+    means = [first[k] for k in keys]
+    for c in var_cols:
+        m = _eval((col(f"__vs_{c}") / col(f"__vn_{c}").cast("f64")).alias(f"__vm_{c}"), first)
+        means.append(m)
+    rows = _join(df, DataFrame(means), key, key, "_right", "m:m", True, "left", "left")
+    sq = [_eval(((col(c).cast("f64") - col(f"__vm_{c}")) * (col(c).cast("f64") - col(f"__vm_{c}")))
+                .alias(f"__vd_{c}"), rows) for c in var_cols]
+    rows = DataFrame(list(rows._cols.values()) + sq)
+    second = _group_by(rows, key, [col(f"__vd_{c}").sum().alias(f"__vd_{c}") for c in var_cols], True, pred, None)
+    out: list[Series] = [first[k] for k in keys]
+    res: dict[int, Series] = {}
+    for i, e in plain:
+        res[i] = first[e.output_name()]
+    for i, e in enumerate(aggs):
+        b = _agg_base(e)
+        if i in res:
+            continue
+        c = b.args[0].value
+        o = N.Column()
+        N.check(N.lib().plgpu_var_finalize(C.byref(second[f"__vd_{c}"]._col), C.byref(first[f"__vn_{c}"]._col),
+                                           int(b.value), int(b.op == "std"), C.byref(o), None))
+        res[i] = Series._from_native(e.output_name(), o)
+    return DataFrame(out + [res[i] for i in range(builtins.len(aggs))])
+
+
 def _group_by(df: DataFrame, key: str | tuple, aggs: list[Expr], maintain_order: bool,
               pred: Expr | None, info: dict | None) -> DataFrame:
+    if any(_agg_base(e).kind == "agg" and _agg_base(e).op in ("std", "var") for e in aggs):
+        return _group_by_var(df, key, aggs, maintain_order, pred, info)
     if pred is not None:
         pred, df = _lower_strings(pred, df)
     g = _gb_lower(df, key, aggs, pred)

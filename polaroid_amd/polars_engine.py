@@ -16,7 +16,7 @@ subtree with a Python UDF via `NodeTraverser.set_udf`
 crates/polars-python/src/lazyframe/visitor/nodes.rs, expression classes of
 .../visitor/expr_nodes.rs) for the hot path — DataFrameScan, Filter,
 Select/HStack of arithmetic + comparisons, GroupBy on one integer key with
-sum/mean/min/max/count/len/first/last, inner / left / right / full / semi / anti Join
+sum/mean/min/max/count/len/first/last/std/var, inner / left / right / full / semi / anti Join
 on 1..8 key columns, Sort by 1..8 columns — into a polaroid_amd plan and installs a UDF that
 runs it through libpolaroid_gpu.so.  A query outside that path is left to
 polars' own engine unless `raise_on_fail` is set (the reference GPU engine's
@@ -130,6 +130,8 @@ class _Translator:
             return c.len() if e.options else c.count()
         if name in ("first", "last"):  # IRAggExpr::First / Last (expr_nodes.rs:677,687)
             return getattr(c, name)()
+        if name in ("std", "var"):  # IRAggExpr::Std / Var, options = ddof (expr_nodes.rs:737,742)
+            return getattr(c, name)(int(e.options))
         raise Unsupported(f"aggregation {name}")
 
     # ---------------------------------------------------------------- plans

@@ -1,0 +1,86 @@
+"""GPU parity of the std() / var() group-by aggregations (polars-expr/src/
+reduce/var_std.rs; finalize at polars-compute/src/moment.rs:126: null when
+the group's non-null count <= ddof, else M2 / (count - ddof), std = sqrt).
+The checker is a two-pass restatement with math.fsum per group.  Tolerance:
+1e-12 relative (+1e-300 absolute) — the reference's Welford merge and the
+executor's two exact passes round differently; validity is exact."""
+
+import math
+
+import numpy as np
+import pytest
+
+import polaroid_amd as pl
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle(key, x, valid, ddof, sel):
+    """Per group (first-occurrence order of selected rows): var, std, valid."""
+    order, groups = [], {}
+    for r in np.flatnonzero(sel):
+        k = int(key[r])
+        if k not in groups:
+            groups[k] = []
+            order.append(k)
+        if valid[r]:
+            groups[k].append(float(x[r]))
+    var, ok = [], []
+    for k in order:
+        v = groups[k]
+        if len(v) <= ddof:
+            var.append(0.0)
+            ok.append(False)
+            continue
+        m = math.fsum(v) / len(v)
+        var.append(max(math.fsum((a - m) * (a - m) for a in v) / (len(v) - ddof), 0.0))
+        ok.append(True)
+    var = np.array(var)
+    return np.array(order, dtype=np.int64), var, np.sqrt(var), np.array(ok, dtype=bool)
+
+
+def _close(got, want, ok):
+    assert np.allclose(got[ok], want[ok], rtol=1e-12, atol=1e-300)
+
+
+@pytest.mark.parametrize("n,card", [(1, 1), (50, 7), (100_003, 100), (60_001, 20_000)])
+@pytest.mark.parametrize("ddof", [0, 1, 2])
+@pytest.mark.parametrize("pred", [False, True])
+def test_var_std_vs_oracle(gpu, n, card, ddof, pred):
+    rng = np.random.default_rng(n + card + 10 * ddof + pred)
+    key = rng.integers(0, card, n).astype(np.int64)
+    x = rng.standard_normal(n) * 1e3 + 5e6  # large mean: catastrophic for one-pass formulas
+    xv = rng.random(n) > 0.15
+    i = rng.integers(-1000, 1000, n).astype(np.int64)
+    df = pl.DataFrame({"k": pl.Series.from_numpy("k", key), "x": pl.Series.from_numpy("x", x, xv),
+                       "i": pl.Series.from_numpy("i", i)})
+    lf = df.lazy()
+    sel = np.ones(n, dtype=bool)
+    if pred:
+        lf = lf.filter(pl.col("i") > -300)
+        sel = i > -300
+    out = (lf.group_by("k", maintain_order=True)
+           .agg(pl.col("x").var(ddof).alias("xv"), pl.col("x").sum().alias("xs"),
+                pl.col("x").std(ddof).alias("xsd"), pl.col("i").std(ddof).alias("isd"))
+           .collect())
+    keys, var, std, ok = _oracle(key, x, xv, ddof, sel)
+    assert out.columns == ["k", "xv", "xs", "xsd", "isd"]
+    assert np.array_equal(out["k"].to_numpy(), keys)
+    assert np.array_equal(out["xv"].validity_numpy(), ok)
+    assert np.array_equal(out["xsd"].validity_numpy(), ok)
+    _close(out["xv"].to_numpy(), var, ok)
+    _close(out["xsd"].to_numpy(), std, ok)
+    _, _, istd, iok = _oracle(key, i.astype(np.float64), np.ones(n, bool), ddof, sel)
+    assert np.array_equal(out["isd"].validity_numpy(), iok)
+    _close(out["isd"].to_numpy(), istd, iok)
+
+
+def test_var_null_keys_and_constant_groups(gpu):
+    k = np.array([1, 0, 1, 0, 2, 2, 2], dtype=np.int64)
+    km = np.array([1, 0, 1, 0, 1, 1, 1], dtype=bool)
+    x = np.array([3.0, 1.0, 3.0, 4.0, 7.0, 7.0, 7.0])
+    df = pl.DataFrame({"k": pl.Series.from_numpy("k", k, km), "x": pl.Series.from_numpy("x", x)})
+    out = df.lazy().group_by("k", maintain_order=True).agg(pl.col("x").var()).collect()
+    assert out["k"].validity_numpy().tolist() == [True, False, True]
+    v = out["x"].to_numpy()
+    assert v[0] == 0.0 and v[2] == 0.0 and v[1] == 4.5
