@@ -371,6 +371,15 @@ int plgpu_str_compare(const plgpu_column* a, const plgpu_column* b, const uint8_
 int plgpu_var_finalize(const plgpu_column* sum_sq, const plgpu_column* count, int32_t ddof, int32_t take_sqrt,
                        plgpu_column* out, void* stream);
 
+/* Per-row squared deviation from the row's group mean, the second pass of
+ * var / std for one integer / Boolean key: out[i] = (x[i] - mean[g])^2 with
+ * g the row of group_key equal to row_key[i] (group keys unique; a null
+ * row key matches the null group).  Null where x is null, the key is not a
+ * group or the mean is null.  Same values as the composed join path
+ * (x.cast(f64) - mean)^2, without materialising the joined frame. */
+int plgpu_group_sq_dev(const plgpu_column* row_key, const plgpu_column* x, const plgpu_column* group_key,
+                       const plgpu_column* group_mean, plgpu_column* out, void* stream);
+
 /* Short-string codes: each string of at most 7 bytes as the Int64
  * (length << 56) | bytes (little-endian), exact and injective, so String
  * keys can cross the integer-keyed paths (the multi-GPU group-by's partial

@@ -134,6 +134,7 @@ SIGNATURES = {
     "plgpu_str_compare": (C.c_int, [_COLP, _COLP, C.c_char_p, C.c_int64, C.c_int32, _COLP, _P]),
     "plgpu_str_encode_short": (C.c_int, [_COLP, _COLP, C.POINTER(C.c_int32), _P]),
     "plgpu_str_decode_short": (C.c_int, [_COLP, _COLP, _P]),
+    "plgpu_group_sq_dev": (C.c_int, [_COLP, _COLP, _COLP, _COLP, _COLP, _P]),
     "plgpu_var_finalize": (C.c_int, [_COLP, _COLP, C.c_int32, C.c_int32, _COLP, _P]),
     "plgpu_gather": (C.c_int, [_COLP, C.c_int32, _COLP, _COLP, _P]),
     "plgpu_hash_partition": (C.c_int, [_COLP, C.c_int32, C.c_int32, C.c_int32, _COLP, C.POINTER(C.c_int64), _P]),

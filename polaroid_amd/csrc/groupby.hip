@@ -2938,3 +2938,120 @@ PLGPU_API int plgpu_var_finalize(const plgpu_column* sum_sq, const plgpu_column*
     }
     return PLGPU_OK;
 }
+
+// ------------------------------------------------- per-row squared deviation
+// Second pass of var / std for one fixed-width key column: every row's
+// d = (x - mean[group(row)])^2, the group found in a small open-addressing
+// table of the (unique) group keys; the null key is its own group.  Null
+// when x is null, the row's key is not a group (rows the predicate dropped)
+// or the mean is null.  Same arithmetic as x.cast(f64) - mean, squared.
+constexpr uint32_t kSqEmpty = 0xFFFFFFFFu;
+
+__global__ __launch_bounds__(256) void sq_build_kernel(DevCol gk, int64_t ng, int bits, uint64_t* __restrict__ tkey,
+                                                       uint32_t* __restrict__ tidx, uint32_t* __restrict__ null_g) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= ng) return;
+    if (!dev_valid(gk, g)) {
+        *null_g = (uint32_t)g;
+        return;
+    }
+    const uint64_t k = dev_load(gk, g);
+    const uint32_t mask = (1u << bits) - 1;
+    for (uint32_t h = hash_slot(k, bits);; h = (h + 1) & mask) {
+        if (atomicCAS(&tidx[h], kSqEmpty, (uint32_t)g) == kSqEmpty) {
+            tkey[h] = k;
+            return;
+        }
+    }
+}
+
+__device__ __forceinline__ double sq_as_f64(const DevCol& c, int64_t r) {
+    const uint64_t b = dev_load(c, r);
+    switch (c.dtype) {
+    case PLGPU_F64: return as_f64(b);
+    case PLGPU_U32:
+    case PLGPU_BOOL: return (double)b;
+    default: return (double)(int64_t)b;
+    }
+}
+
+__global__ __launch_bounds__(256) void sq_dev_kernel(DevCol rk, DevCol x, int64_t n, int bits,
+                                                     const uint64_t* __restrict__ tkey,
+                                                     const uint32_t* __restrict__ tidx,
+                                                     const uint32_t* __restrict__ null_g, DevCol mean,
+                                                     double* __restrict__ out, uint64_t* __restrict__ out_valid) {
+    const uint32_t ng_null = *null_g;
+    const uint32_t mask = (1u << bits) - 1;
+    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x; i0 < n; i0 += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = i0 + threadIdx.x;
+        bool valid = false;
+        if (i < n && dev_valid(x, i)) {
+            uint32_t g = kSqEmpty;
+            if (!dev_valid(rk, i)) {
+                g = ng_null;
+            } else {
+                const uint64_t k = dev_load(rk, i);
+                for (uint32_t h = hash_slot(k, bits);; h = (h + 1) & mask) {
+                    const uint32_t t = tidx[h];
+                    if (t == kSqEmpty) break;
+                    if (tkey[h] == k) {
+                        g = t;
+                        break;
+                    }
+                }
+            }
+            if (g != kSqEmpty && dev_valid(mean, g)) {
+                const double d = sq_as_f64(x, i) - as_f64(dev_load(mean, g));
+                out[i] = d * d;
+                valid = true;
+            }
+        }
+        if (i < n && !valid) out[i] = 0.0;
+        const uint64_t w = __ballot(valid);
+        if ((threadIdx.x & 63) == 0 && i < n) out_valid[i >> 6] = w;
+    }
+}
+
+PLGPU_API int plgpu_group_sq_dev(const plgpu_column* row_key, const plgpu_column* x, const plgpu_column* group_key,
+                                 const plgpu_column* group_mean, plgpu_column* out, void* stream) {
+    hipStream_t s = as_stream(stream);
+    if (!row_key || !x || !group_key || !group_mean || !out) return fail(PLGPU_ERR_INVALID, "NULL argument");
+    std::memset(out, 0, sizeof *out);
+    const int32_t kt = row_key->dtype;
+    if (kt != group_key->dtype || (kt != PLGPU_I64 && kt != PLGPU_I32 && kt != PLGPU_U32 && kt != PLGPU_BOOL))
+        return fail(PLGPU_ERR_SCHEMA, "squared deviations take one integer / Boolean key of one dtype");
+    if (x->dtype == PLGPU_STR || group_mean->dtype != PLGPU_F64)
+        return fail(PLGPU_ERR_SCHEMA, "squared deviations take a numeric x and Float64 means");
+    if (row_key->length != x->length || group_key->length != group_mean->length)
+        return fail(PLGPU_ERR_SHAPE, "columns differ in length");
+    const int64_t n = x->length, ng = group_key->length;
+    if (ng >= (int64_t)1 << 30) return fail(PLGPU_ERR_SHAPE, "too many groups");
+    int rc = make_owned_column(out, PLGPU_F64, n, true, s);
+    if (rc || n == 0) return rc;
+    int bits = 6;
+    while (((int64_t)1 << bits) < 2 * ng) ++bits;
+    const size_t slots = (size_t)1 << bits;
+    uint64_t* tkey = nullptr;
+    uint32_t* tidx = nullptr;
+    hipError_t e = hipMallocAsync((void**)&tkey, slots * 8, s);
+    if (e == hipSuccess) e = hipMallocAsync((void**)&tidx, slots * 4 + 4, s);
+    if (e == hipSuccess) e = hipMemsetAsync(tidx, 0xFF, slots * 4 + 4, s);
+    uint32_t* null_g = tidx + slots;
+    if (e == hipSuccess && ng > 0)
+        sq_build_kernel<<<(unsigned)((ng + 255) / 256), 256, 0, s>>>(dev_col(*group_key), ng, bits, tkey, tidx, null_g);
+    if (e == hipSuccess) e = hipGetLastError();
+    if (e == hipSuccess) {
+        const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, (int64_t)1 << 30);  // a row per thread
+        sq_dev_kernel<<<g, 256, 0, s>>>(dev_col(*row_key), dev_col(*x), n, bits, tkey, tidx, null_g,
+                                        dev_col(*group_mean), (double*)out->values, (uint64_t*)out->validity);
+        e = hipGetLastError();
+    }
+    if (tkey) (void)hipFreeAsync(tkey, s);
+    if (tidx) (void)hipFreeAsync(tidx, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) {
+        plgpu_column_release(out);
+        return hip_fail(e, "squared deviations");
+    }
+    return PLGPU_OK;
+}

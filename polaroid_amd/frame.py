@@ -994,8 +994,10 @@ def _group_by_var(df: DataFrame, key: str | tuple, aggs: list[Expr], maintain_or
     composed of GPU passes:
       1. the exact group-by with sum(x) and count(x) of every var / std
          column next to the other aggregations (first-occurrence order);
-      2. every row's group mean, by a left join of the rows with the groups'
-         means (null keys match: they form a group);
+      2. every row's group mean: for one integer key plgpu_group_sq_dev
+         looks it up in a table of the group keys and writes d directly;
+         otherwise a left join of the rows with the groups' means (null keys
+         match: they form a group);
       3. d = (x - mean)^2 per row (one rounding), exactly summed per group
          by a second group-by with the same predicate (same group order);
       4. plgpu_var_finalize: null when count <= ddof, else sum / (count - ddof),
@@ -1022,10 +1024,20 @@ def _group_by_var(df: DataFrame, key: str | tuple, aggs: list[Expr], maintain_or
     for c in var_cols:
         m = _eval((col(f"__vs_{c}") / col(f"__vn_{c}").cast("f64")).alias(f"__vm_{c}"), first)
         means.append(m)
-    rows = _join(df, DataFrame(means), key, key, "_right", "m:m", True, "left", "left")
-    sq = [_eval(((col(c).cast("f64") - col(f"__vm_{c}")) * (col(c).cast("f64") - col(f"__vm_{c}")))
-                .alias(f"__vd_{c}"), rows) for c in var_cols]
-    rows = DataFrame(list(rows._cols.values()) + sq)
+    if builtins.len(keys) == 1 and df[keys[0]]._col.dtype in (N.I64, N.I32, N.U32, N.BOOL):
+        # one integer key: squared deviations straight from a group-key table
+        sq = []
+        for c, m in zip(var_cols, means[1:]):
+            o = N.Column()
+            N.check(N.lib().plgpu_group_sq_dev(C.byref(df[keys[0]]._col), C.byref(df[c]._col),
+                                               C.byref(means[0]._col), C.byref(m._col), C.byref(o), None))
+            sq.append(Series._from_native(f"__vd_{c}", o))
+        rows = DataFrame(list(df._cols.values()) + sq)
+    else:
+        rows = _join(df, DataFrame(means), key, key, "_right", "m:m", True, "left", "left")
+        sq = [_eval(((col(c).cast("f64") - col(f"__vm_{c}")) * (col(c).cast("f64") - col(f"__vm_{c}")))
+                    .alias(f"__vd_{c}"), rows) for c in var_cols]
+        rows = DataFrame(list(rows._cols.values()) + sq)
     second = _group_by(rows, key, [col(f"__vd_{c}").sum().alias(f"__vd_{c}") for c in var_cols], True, pred, None)
     out: list[Series] = [first[k] for k in keys]
     res: dict[int, Series] = {}

@@ -84,3 +84,34 @@ def test_var_null_keys_and_constant_groups(gpu):
     assert out["k"].validity_numpy().tolist() == [True, False, True]
     v = out["x"].to_numpy()
     assert v[0] == 0.0 and v[2] == 0.0 and v[1] == 4.5
+
+
+@pytest.mark.parametrize("kind", ["multi", "string", "u32_nullkey"])
+def test_var_std_key_kinds(gpu, kind):
+    """The join-composed path (multi-key, String keys) and the direct
+    group-key-table path with a nullable UInt32 key."""
+    rng = np.random.default_rng(len(kind))
+    n = 40_000
+    a = rng.integers(0, 30, n).astype(np.int64)
+    b = rng.integers(0, 4, n).astype(np.int64)
+    x = rng.standard_normal(n) * 10 + 1e4
+    if kind == "multi":
+        df = pl.DataFrame({"a": pl.Series.from_numpy("a", a), "b": pl.Series.from_numpy("b", b),
+                           "x": pl.Series.from_numpy("x", x)})
+        key, gk = ["a", "b"], a * 4 + b
+    elif kind == "string":
+        names = np.array([f"name-{v:03d}-longer-than-seven" for v in a], dtype=object)
+        df = pl.DataFrame({"s": pl.Series("s", names.tolist()), "x": pl.Series.from_numpy("x", x)})
+        key, gk = "s", a
+    else:
+        km = rng.random(n) > 0.05
+        df = pl.DataFrame({"u": pl.Series.from_numpy("u", a.astype(np.uint32), km),
+                           "x": pl.Series.from_numpy("x", x)})
+        key, gk = "u", np.where(km, a, -1)
+    out = df.lazy().group_by(key, maintain_order=True).agg(pl.col("x").std(), pl.col("x").var(0).alias("v0")).collect()
+    keys, var, std, ok = _oracle(gk, x, np.ones(n, bool), 1, np.ones(n, bool))
+    _, var0, _, ok0 = _oracle(gk, x, np.ones(n, bool), 0, np.ones(n, bool))
+    assert out.height == len(keys)
+    assert np.array_equal(out["x"].validity_numpy(), ok)
+    _close(out["x"].to_numpy(), std, ok)
+    _close(out["v0"].to_numpy(), var0, ok0)
