@@ -2947,19 +2947,28 @@ PLGPU_API int plgpu_var_finalize(const plgpu_column* sum_sq, const plgpu_column*
 // or the mean is null.  Same arithmetic as x.cast(f64) - mean, squared.
 constexpr uint32_t kSqEmpty = 0xFFFFFFFFu;
 
-__global__ __launch_bounds__(256) void sq_build_kernel(DevCol gk, int64_t ng, int bits, uint64_t* __restrict__ tkey,
+// Table slot: key, mean bits, group index | kSqNoMean when the mean is null.
+constexpr uint32_t kSqNoMean = 0x80000000u;
+constexpr int kSqLdsBits = 11;  // tables up to 2048 slots (40 KB) are staged in LDS per block
+
+__global__ __launch_bounds__(256) void sq_build_kernel(DevCol gk, DevCol mean, int64_t ng, int bits,
+                                                       uint64_t* __restrict__ tkey, uint64_t* __restrict__ tval,
                                                        uint32_t* __restrict__ tidx, uint32_t* __restrict__ null_g) {
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= ng) return;
+    const uint32_t tag = (uint32_t)g | (dev_valid(mean, g) ? 0u : kSqNoMean);
     if (!dev_valid(gk, g)) {
-        *null_g = (uint32_t)g;
+        null_g[0] = tag;
+        null_g[1] = (uint32_t)dev_load(mean, g);
+        null_g[2] = (uint32_t)(dev_load(mean, g) >> 32);
         return;
     }
     const uint64_t k = dev_load(gk, g);
     const uint32_t mask = (1u << bits) - 1;
     for (uint32_t h = hash_slot(k, bits);; h = (h + 1) & mask) {
-        if (atomicCAS(&tidx[h], kSqEmpty, (uint32_t)g) == kSqEmpty) {
+        if (atomicCAS(&tidx[h], kSqEmpty, tag) == kSqEmpty) {
             tkey[h] = k;
+            tval[h] = dev_load(mean, g);
             return;
         }
     }
@@ -2975,40 +2984,76 @@ __device__ __forceinline__ double sq_as_f64(const DevCol& c, int64_t r) {
     }
 }
 
+// Four rows per thread per step (loads issued before the probes); the key
+// table in LDS when it fits (kSqLdsBits), else read through the caches.
+template <bool LDS>
 __global__ __launch_bounds__(256) void sq_dev_kernel(DevCol rk, DevCol x, int64_t n, int bits,
-                                                     const uint64_t* __restrict__ tkey,
-                                                     const uint32_t* __restrict__ tidx,
-                                                     const uint32_t* __restrict__ null_g, DevCol mean,
+                                                     const uint64_t* __restrict__ gkey,
+                                                     const uint64_t* __restrict__ gval,
+                                                     const uint32_t* __restrict__ gidx,
+                                                     const uint32_t* __restrict__ null_g,
                                                      double* __restrict__ out, uint64_t* __restrict__ out_valid) {
-    const uint32_t ng_null = *null_g;
-    const uint32_t mask = (1u << bits) - 1;
-    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x; i0 < n; i0 += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t i = i0 + threadIdx.x;
-        bool valid = false;
-        if (i < n && dev_valid(x, i)) {
-            uint32_t g = kSqEmpty;
-            if (!dev_valid(rk, i)) {
-                g = ng_null;
-            } else {
-                const uint64_t k = dev_load(rk, i);
-                for (uint32_t h = hash_slot(k, bits);; h = (h + 1) & mask) {
-                    const uint32_t t = tidx[h];
-                    if (t == kSqEmpty) break;
-                    if (tkey[h] == k) {
-                        g = t;
-                        break;
+    extern __shared__ uint64_t sq_lds[];
+    const uint32_t slots = 1u << bits, mask = slots - 1;
+    const uint64_t* tkey = gkey;
+    const uint64_t* tval = gval;
+    const uint32_t* tidx = gidx;
+    if (LDS) {
+        uint64_t* k = sq_lds;
+        uint64_t* v = sq_lds + slots;
+        uint32_t* t = (uint32_t*)(sq_lds + 2 * slots);
+        for (uint32_t h = threadIdx.x; h < slots; h += blockDim.x) {
+            k[h] = gkey[h];
+            v[h] = gval[h];
+            t[h] = gidx[h];
+        }
+        __syncthreads();
+        tkey = k;
+        tval = v;
+        tidx = t;
+    }
+    const uint32_t null_tag = null_g[0];
+    const uint64_t null_mean = (uint64_t)null_g[1] | ((uint64_t)null_g[2] << 32);
+    constexpr int R = 4;
+    for (int64_t base = (int64_t)blockIdx.x * 256 * R; base < n; base += (int64_t)gridDim.x * 256 * R) {
+        uint64_t kk[R];
+        double xv[R];
+        bool kv[R], xok[R];
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            const int64_t i = base + j * 256 + threadIdx.x;
+            xok[j] = i < n && dev_valid(x, i);
+            kv[j] = i < n && dev_valid(rk, i);
+            kk[j] = i < n ? dev_load(rk, i) : 0;
+            xv[j] = i < n ? sq_as_f64(x, i) : 0.0;
+        }
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            const int64_t i = base + j * 256 + threadIdx.x;
+            uint32_t tag = kSqEmpty;
+            uint64_t m = 0;
+            if (xok[j]) {
+                if (!kv[j]) {
+                    tag = null_tag;
+                    m = null_mean;
+                } else {
+                    for (uint32_t h = hash_slot(kk[j], bits);; h = (h + 1) & mask) {
+                        const uint32_t t = tidx[h];
+                        if (t == kSqEmpty) break;
+                        if (tkey[h] == kk[j]) {
+                            tag = t;
+                            m = tval[h];
+                            break;
+                        }
                     }
                 }
             }
-            if (g != kSqEmpty && dev_valid(mean, g)) {
-                const double d = sq_as_f64(x, i) - as_f64(dev_load(mean, g));
-                out[i] = d * d;
-                valid = true;
-            }
+            const bool valid = xok[j] && tag != kSqEmpty && !(tag & kSqNoMean);
+            const double d = xv[j] - as_f64(m);
+            if (i < n) out[i] = valid ? d * d : 0.0;
+            const uint64_t w = __ballot(valid);
+            if ((threadIdx.x & 63) == 0 && i < n) out_valid[i >> 6] = w;
         }
-        if (i < n && !valid) out[i] = 0.0;
-        const uint64_t w = __ballot(valid);
-        if ((threadIdx.x & 63) == 0 && i < n) out_valid[i >> 6] = w;
     }
 }
 
@@ -3033,17 +3078,26 @@ PLGPU_API int plgpu_group_sq_dev(const plgpu_column* row_key, const plgpu_column
     const size_t slots = (size_t)1 << bits;
     uint64_t* tkey = nullptr;
     uint32_t* tidx = nullptr;
-    hipError_t e = hipMallocAsync((void**)&tkey, slots * 8, s);
-    if (e == hipSuccess) e = hipMallocAsync((void**)&tidx, slots * 4 + 4, s);
-    if (e == hipSuccess) e = hipMemsetAsync(tidx, 0xFF, slots * 4 + 4, s);
+    hipError_t e = hipMallocAsync((void**)&tkey, slots * 16, s);
+    if (e == hipSuccess) e = hipMallocAsync((void**)&tidx, slots * 4 + 12, s);
+    if (e == hipSuccess) e = hipMemsetAsync(tidx, 0xFF, slots * 4 + 12, s);
+    uint64_t* tval = tkey + slots;
     uint32_t* null_g = tidx + slots;
     if (e == hipSuccess && ng > 0)
-        sq_build_kernel<<<(unsigned)((ng + 255) / 256), 256, 0, s>>>(dev_col(*group_key), ng, bits, tkey, tidx, null_g);
+        sq_build_kernel<<<(unsigned)((ng + 255) / 256), 256, 0, s>>>(dev_col(*group_key), dev_col(*group_mean), ng,
+                                                                     bits, tkey, tval, tidx, null_g);
     if (e == hipSuccess) e = hipGetLastError();
     if (e == hipSuccess) {
-        const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, (int64_t)1 << 30);  // a row per thread
-        sq_dev_kernel<<<g, 256, 0, s>>>(dev_col(*row_key), dev_col(*x), n, bits, tkey, tidx, null_g,
-                                        dev_col(*group_mean), (double*)out->values, (uint64_t*)out->validity);
+        const int64_t steps = (n + 1023) / 1024;
+        if (bits <= kSqLdsBits) {
+            const unsigned g = (unsigned)std::min<int64_t>(steps, (int64_t)num_cus() * 8);
+            sq_dev_kernel<true><<<g, 256, slots * 20, s>>>(dev_col(*row_key), dev_col(*x), n, bits, tkey, tval, tidx,
+                                                            null_g, (double*)out->values, (uint64_t*)out->validity);
+        } else {
+            const unsigned g = (unsigned)std::min<int64_t>(steps, (int64_t)1 << 30);
+            sq_dev_kernel<false><<<g, 256, 0, s>>>(dev_col(*row_key), dev_col(*x), n, bits, tkey, tval, tidx, null_g,
+                                                   (double*)out->values, (uint64_t*)out->validity);
+        }
         e = hipGetLastError();
     }
     if (tkey) (void)hipFreeAsync(tkey, s);
