@@ -10,6 +10,12 @@ N > 1 each rank holds its own R-row shard (weak scaling), aggregates it
 locally into exact partial states, and the partial states are hash-
 partitioned by key and exchanged with one RCCL all-to-all, then merged
 (DESIGN.md §Multi-GPU).  Rank 0 prints one JSON line.
+
+`python bench.py --gpus N` with N > 1 outside a torch.distributed launch
+starts `torch.distributed.run --nproc-per-node N` on this same command as a
+child process (before anything touches the GPU) and exits with its code.
+At N = 8 the default shard is 1.25e9 rows per GPU: BASELINE configs[4]'s
+1e10-row group-by on one 8-GPU node.
 """
 
 from __future__ import annotations
@@ -36,11 +42,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--rows", type=float, default=1e9, help="rows per GPU")
+    ap.add_argument("--rows", type=float, default=None,
+                    help="rows per GPU (default 1e9; 1.25e9 at 8 GPUs = configs[4]'s 1e10 rows)")
     ap.add_argument("--groups", type=int, default=100, help="distinct symbols (h2oai id4: K=100)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline time budget")
-    ap.add_argument("--cpu-rows", type=float, default=3e7, help="cpu_baseline sample rows")
+    ap.add_argument("--cpu-rows", type=float, default=1e7, help="cpu_baseline sample rows (configs[0]: 1e7)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="print this rank's launch parameters and exit before touching the GPU (tests)")
     return ap.parse_args()
 
 
@@ -70,12 +79,29 @@ def make_data(torch, n: int, groups: int, seed: int):
     return sym, cols
 
 
+def host_cores() -> tuple[int, str]:
+    """Every host core this process may run on: the CPU affinity set,
+    capped by the cgroup's CPU quota when one is set (a container's share)."""
+    aff = len(os.sched_getaffinity(0))
+    note = f"sched_getaffinity: {aff}"
+    n = aff
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            q = max(1, int(int(quota) // int(period)))
+            note += f", cgroup cpu.max quota: {q}"
+            n = min(n, q)
+    except (OSError, ValueError):
+        pass
+    return n, note
+
+
 def cpu_baseline(rows: int, groups: int, seconds: float) -> dict:
     """The oracle's OpenMP restatement of the reference's streaming hash
     aggregation, timed on the host cores (rank 0, N=1 only)."""
     from oracle import oracle as O
 
-    threads = min(16, len(os.sched_getaffinity(0)))
+    threads, cores_note = host_cores()
     rng = np.random.default_rng(1)
     base = rng.uniform(10, 490, groups)
     k = rng.integers(0, groups, rows)
@@ -96,8 +122,8 @@ def cpu_baseline(rows: int, groups: int, seconds: float) -> dict:
         times.append(time.perf_counter() - t0)
     t = float(np.median(times))
     return {"value": rows / t / 1e6, "unit": "Mrows/s", "cores": threads, "kind": "port",
-            "sample": f"{rows:.0e} rows x {len(times)} runs of the same query (median), OpenMP "
-                      f"{threads} threads, oracle/polars_oracle.c:or_baseline_filter_groupby_sum"}
+            "sample": f"{rows:.0e} rows (configs[0] size) x {len(times)} runs of the same query (median), OpenMP "
+                      f"{threads} threads ({cores_note}), oracle/polars_oracle.c:or_baseline_filter_groupby_sum"}
 
 
 def load_traffic(n_rows: int):
@@ -115,14 +141,38 @@ def load_traffic(n_rows: int):
     return None
 
 
+def launch_ranks(n: int) -> int:
+    """Run this command under torch.distributed.run with n ranks (one per
+    GPU) as a child process; called before any GPU call in this process."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "RANK" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if "RANK" in os.environ and world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.rows is None:
+        args.rows = 1.25e9 if world == 8 else 1e9
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        print(json.dumps({"rank": rank, "local_rank": local, "world": world, "rows_per_gpu": args.rows,
+                          "master_addr": os.environ.get("MASTER_ADDR")}), flush=True)
+        return
     # launched by torch.distributed.run (even with one rank): the
     # hash-partitioned path over RCCL; plain `python bench.py`: one GPU
     distributed = "RANK" in os.environ and "MASTER_ADDR" in os.environ
@@ -150,13 +200,14 @@ def main():
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
-    kernel_ms = []
+    kernel_ms, phases = [], []
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         info = {}
         out = step(info)
         kernel_ms.append(info.get("main_kernel_ms", float("nan")))
+        phases.append([info.get(k, float("nan")) for k in ("partial_ms", "exchange_ms", "merge_ms")])
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
@@ -165,6 +216,14 @@ def main():
         t = torch.tensor([dt], device="cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    per_rank = None
+    if distributed:
+        # per-rank fused-kernel and phase times (ms per step), gathered to rank 0
+        mine = torch.tensor([float(np.mean(kernel_ms))] + list(np.mean(np.array(phases), axis=0)),
+                            device="cuda", dtype=torch.float64)
+        allr = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        per_rank = [[round(float(x), 4) for x in t.tolist()] for t in allr]
     ms_per_step = dt / args.steps * 1e3
     total_rows = n * world
     value = total_rows * args.steps / dt / 1e6
@@ -186,12 +245,20 @@ def main():
         "data": "synthetic OHLCV-shaped columns generated on device (torch RNG), inputs resident in HBM",
         "config": {
             "workload": "filter(close > 250).group_by(symbol).agg(open/high/low/close.sum()) "
-                        f"{n:.0e} rows per GPU, {args.groups} groups (metric size; configs[1] = 1e8 rows)",
+                        f"{n:.3g} rows per GPU, {args.groups} groups"
+                        + (f" = {total_rows:.3g} rows over {world} GPUs (configs[4])" if world == 8 else
+                           " (metric size; configs[1] = 1e8 rows)"),
             "rows_per_gpu": n, "groups": args.groups, "global_batch": total_rows,
             "columns": "symbol:i64 open,high,low,close:f64",
             "selectivity": None if out is None else round(float(info.get("rows_selected", 0)) / n, 4),
             "parallelism": f"hash-partitioned x{world} (RCCL all-to-all of partial states)" if distributed
             else "single GPU",
+        },
+        "ranks": None if per_rank is None else {
+            "rccl_world_size": dist.get_world_size(),
+            "backend": dist.get_backend(),
+            "fields": ["kernel_ms", "partial_ms", "exchange_ms", "merge_ms"],
+            "per_rank": per_rank,
         },
         "roofline": {
             "bound": "hbm",

@@ -183,6 +183,29 @@ int plgpu_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream);
 /* Release a library-produced column (no-op for borrowed ones). */
 void plgpu_column_release(plgpu_column* col);
 
+/* ---- ingestion: Arrow RecordBatches in host memory -> device columns -------
+ * The reference hands a DataFrame to an engine as one Arrow RecordBatch per
+ * chunk: crates/polars-python/src/dataframe/export.rs:80 PyDataFrame.to_arrow
+ * (what a GPU-engine scan calls on DataFrameScan.df, visitor/nodes.rs:190).
+ * plgpu_column_alloc makes an owning column for the concatenated chunks
+ * (PLGPU_STR: `str_bytes` bytes of string data).  plgpu_ingest_chunk copies
+ * rows [src_offset, src_offset + length) of one chunk's Arrow buffers, as they
+ * lie in host memory, into rows [dst_row, dst_row + length) of `dst`:
+ *   values    Arrow buffers[1] (fixed width; bit-packed for PLGPU_BOOL;
+ *             int64 offsets for PLGPU_STR, rebased so the chunk's first byte
+ *             lands at `dst_byte` of dst->data)
+ *   validity  Arrow buffers[0] or NULL (all valid; required NULL when dst has
+ *             no validity)
+ *   str_data  Arrow buffers[2] of a PLGPU_STR chunk
+ * Copies go through pinned staging buffers, asynchronously on `stream`; bits
+ * at any offset are placed by a device kernel.  The host buffers may be
+ * reused on return; the device data is complete after plgpu_synchronize. */
+int plgpu_column_alloc(int32_t dtype, int64_t length, int32_t with_validity, int64_t str_bytes,
+                       plgpu_column* out, void* stream);
+int plgpu_ingest_chunk(plgpu_column* dst, int64_t dst_row, int64_t dst_byte, const void* values,
+                       const uint8_t* validity, const uint8_t* str_data, int64_t src_offset, int64_t length,
+                       void* stream);
+
 /* ------------------------------------------------------------ hot path */
 
 /* Evaluate a physical expression over `ncols` input columns of equal length

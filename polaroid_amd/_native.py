@@ -100,6 +100,8 @@ SIGNATURES = {
     "plgpu_memcpy_d2h": (C.c_int, [_P, _P, C.c_size_t, _P]),
     "plgpu_memcpy_d2d": (C.c_int, [_P, _P, C.c_size_t, _P]),
     "plgpu_column_release": (None, [_COLP]),
+    "plgpu_column_alloc": (C.c_int, [C.c_int32, C.c_int64, C.c_int32, C.c_int64, _COLP, _P]),
+    "plgpu_ingest_chunk": (C.c_int, [_COLP, C.c_int64, C.c_int64, _P, _P, _P, C.c_int64, C.c_int64, _P]),
     "plgpu_eval": (C.c_int, [_COLP, C.c_int32, C.POINTER(Instr), C.c_int32, _COLP, _P]),
     "plgpu_filter": (C.c_int, [_COLP, C.c_int32, _COLP, _COLP, C.POINTER(C.c_int64), _P]),
     "plgpu_filter_expr": (C.c_int, [_COLP, C.c_int32, C.POINTER(Instr), C.c_int32, _COLP,

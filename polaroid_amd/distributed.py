@@ -26,6 +26,7 @@ stays the local HBM pass: weak scaling.
 from __future__ import annotations
 
 import ctypes as C
+import time
 from typing import Any, Sequence
 
 from . import _native as N
@@ -160,8 +161,13 @@ class GpuPartial:
             self.handle = C.c_void_p()
 
     def __del__(self):
-        if N is not None and N._lib is not None:  # not during interpreter shutdown
-            self.free()
+        # at interpreter shutdown module globals may already be gone, and a
+        # failed __init__ leaves no handle: nothing to free then
+        try:
+            if getattr(self, "handle", None) is not None and N._lib is not None:
+                self.free()
+        except (AttributeError, TypeError):
+            pass
 
     def begin(self, bottoms):
         self.free()
@@ -203,13 +209,33 @@ class GpuPartial:
         return _gb_frame(g, out_key, out_aggs), mi
 
 
-def run_partitioned(part, world: int, group, device):
+def _sync(device) -> None:
+    if device.type == "cuda":
+        import torch
+
+        torch.cuda.synchronize(device)
+
+
+def run_partitioned(part, world: int, group, device, timings: dict | None = None):
     """The protocol of group_by_agg over any partial implementation (the
-    GPU one above, or a host model in tests/test_distributed.py)."""
+    GPU one above, or a host model in tests/test_distributed.py).  With
+    `timings`, the wall time of each phase (device-synchronised) is stored
+    as partial_ms (local pre-aggregation + window agreement), exchange_ms
+    (export + all-to-all of the records) and merge_ms."""
+    t0 = time.perf_counter()
     bottoms = agree_windows(part, world, group, device)
+    if timings is not None:
+        _sync(device)
+    t1 = time.perf_counter()
     send, counts = part.export()
     recv, n = exchange_records(send, counts, part.record_words, group)
-    return part.merge(recv, n, bottoms)
+    t2 = time.perf_counter()
+    res = part.merge(recv, n, bottoms)
+    if timings is not None:
+        _sync(device)
+        t3 = time.perf_counter()
+        timings.update(partial_ms=(t1 - t0) * 1e3, exchange_ms=(t2 - t1) * 1e3, merge_ms=(t3 - t2) * 1e3)
+    return res
 
 
 def group_by_agg(df, key: str, aggs: Sequence[Expr], predicate: Expr | None = None, *, group=None,
@@ -222,7 +248,7 @@ def group_by_agg(df, key: str, aggs: Sequence[Expr], predicate: Expr | None = No
     import torch
     import torch.distributed as dist
 
-    from .frame import _gb_lower
+    from .frame import _gb_lower, _lower_strings
     from .expr import col
 
     if not dist.is_initialized():
@@ -234,6 +260,11 @@ def group_by_agg(df, key: str, aggs: Sequence[Expr], predicate: Expr | None = No
     from .frame import DataFrame, Series, String
 
     aggs = [a if isinstance(a, Expr) else col(a) for a in aggs]
+    if predicate is not None:
+        # String comparisons / pattern tests become Boolean columns first,
+        # against the String columns as they are (before the key turns into
+        # its Int64 codes), as the single-GPU group-by does
+        predicate, df = _lower_strings(predicate, df)
     string_key = isinstance(key, str) and key in df.columns and df[key].dtype is String
     if string_key:
         # String symbols of <= 7 bytes cross the integer-keyed protocol as
@@ -248,7 +279,8 @@ def group_by_agg(df, key: str, aggs: Sequence[Expr], predicate: Expr | None = No
     if g.keycol.dtype not in (N.I64, N.I32) or len(g.keys) != 1:
         raise N.InvalidOperationError("the multi-GPU group-by takes one Int64 / Int32 (or short String) key column")
     part = GpuPartial(g, world)
-    out, mi = run_partitioned(part, world, group, device)
+    timings: dict = {}
+    out, mi = run_partitioned(part, world, group, device, timings if info is not None else None)
     if string_key:
         strs = N.Column()
         N.check(N.lib().plgpu_str_decode_short(C.byref(out[key]._col), C.byref(strs), None))
@@ -258,6 +290,7 @@ def group_by_agg(df, key: str, aggs: Sequence[Expr], predicate: Expr | None = No
         d = part.info.as_dict()
         d["merge_groups"] = mi.groups
         d["groups"] = mi.groups
+        d.update(timings)
         info.update(d)
     return out
 

@@ -336,44 +336,12 @@ class Series:
     # Arrow interchange (polars DataFrames cross the plugin boundary as Arrow)
     @classmethod
     def from_arrow(cls, name: str, arr) -> "Series":
-        """Upload a pyarrow Array / ChunkedArray (int64/int32/uint32/float64/bool)."""
+        """Upload a pyarrow Array / ChunkedArray chunk by chunk (the buffers
+        as they are: no host concatenation, no bitmap unpacking)."""
         import pyarrow as pa
 
-        if isinstance(arr, pa.ChunkedArray):
-            arr = arr.combine_chunks() if arr.num_chunks != 1 else arr.chunk(0)
-        if pa.types.is_dictionary(arr.type):
-            # polars Categorical / Enum: the dictionary and the indices go to
-            # the device as they are, and the strings are gathered there
-            # (a null index gathers a null)
-            dictionary = cls.from_arrow(name, arr.dictionary)
-            if dictionary.dtype is not String:
-                raise N.InvalidOperationError(f"column {name!r}: dictionary of {arr.dictionary.type} is not supported")
-            idx = cls.from_arrow("__idx", arr.indices.cast(pa.uint32()))
-            return dictionary.gather(idx).alias(name)
-        m = {pa.int64(): Int64, pa.int32(): Int32, pa.uint32(): UInt32, pa.float64(): Float64,
-             pa.bool_(): Boolean}
-        if arr.type in (pa.string(), pa.large_string(), pa.utf8(), pa.large_utf8()):
-            # large_string buffers as they are (string: offsets widened to int64)
-            if arr.type in (pa.string(), pa.utf8()):
-                arr = arr.cast(pa.large_string())
-            vbuf, obuf, dbuf = arr.buffers()
-            offs = np.frombuffer(obuf, np.int64)[arr.offset: arr.offset + builtins.len(arr) + 1]
-            data = np.frombuffer(dbuf, np.uint8) if dbuf is not None else np.zeros(0, np.uint8)
-            data = data[int(offs[0]) if builtins.len(offs) else 0: int(offs[-1]) if builtins.len(offs) else 0]
-            valid = arr.is_valid().to_numpy(zero_copy_only=False) if arr.null_count else None
-            s = cls.__new__(cls)
-            s.name = name
-            s._upload_string_buffers(offs - (offs[0] if builtins.len(offs) else 0), data, valid)
-            return s
-        dt = m.get(arr.type)
-        if dt is None:
-            raise N.InvalidOperationError(f"column {name!r}: arrow type {arr.type} is not supported on the GPU")
-        valid = None
-        if arr.null_count:
-            valid = arr.is_valid().to_numpy(zero_copy_only=False)
-            arr = arr.fill_null(False if dt is Boolean else 0)
-        vals = arr.to_numpy(zero_copy_only=False)
-        return cls.from_numpy(name, vals, valid, dt)
+        chunks = list(arr.chunks) if isinstance(arr, pa.ChunkedArray) else [arr]
+        return _ingest_chunks(name, chunks, arr.type)
 
     def to_arrow(self):
         import pyarrow as pa
@@ -462,6 +430,72 @@ class Series:
         return Series._from_native(self.name, out[0])
 
 
+# ------------------------------------------------------------- ingestion
+def _arrow_physical(t) -> DataType | None:
+    """Arrow type -> physical device dtype of the path (None: unsupported)."""
+    import pyarrow as pa
+
+    if t in (pa.string(), pa.large_string()):
+        return String
+    return {pa.int64(): Int64, pa.int32(): Int32, pa.uint32(): UInt32, pa.float64(): Float64,
+            pa.bool_(): Boolean}.get(t)
+
+
+def _ingest_chunks(name: str, chunks: list, atype) -> Series:
+    """Arrow chunks (host) -> one device column through plgpu_column_alloc /
+    plgpu_ingest_chunk: every chunk's value, validity and string buffers are
+    copied as they lie (Arrow offsets honoured), through the library's
+    pinned staging buffers, with one synchronisation at the end."""
+    import pyarrow as pa
+
+    if pa.types.is_dictionary(atype):
+        # polars Categorical / Enum: the dictionary and the indices go to the
+        # device as they are, and the strings are gathered there (a null
+        # index gathers a null).  Chunks may carry different dictionaries.
+        if builtins.len(chunks) > 1:
+            chunks = list(pa.chunked_array(chunks, type=atype).unify_dictionaries().chunks)
+        dict_arr = chunks[0].dictionary if chunks else pa.array([], atype.value_type)
+        dictionary = _ingest_chunks(name, [dict_arr], dict_arr.type)
+        if dictionary.dtype is not String:
+            raise N.InvalidOperationError(f"column {name!r}: dictionary of {dict_arr.type} is not supported")
+        idx = _ingest_chunks("__idx", [c.indices.cast(pa.uint32()) for c in chunks], pa.uint32())
+        return dictionary.gather(idx).alias(name)
+    if atype in (pa.string(), pa.utf8()):
+        chunks = [c.cast(pa.large_string()) for c in chunks]
+        atype = pa.large_string()
+    dt = _arrow_physical(atype)
+    if dt is None:
+        raise N.InvalidOperationError(f"column {name!r}: arrow type {atype} is not supported on the GPU")
+    n = builtins.sum(builtins.len(c) for c in chunks)
+    nulls = builtins.sum(c.null_count for c in chunks)
+    spans = []
+    str_bytes = 0
+    for c in chunks:
+        bufs = c.buffers()
+        if dt is String:
+            offs = np.frombuffer(bufs[1], np.int64, builtins.len(c) + 1, c.offset * 8) if builtins.len(c) else None
+            b0, b1 = (int(offs[0]), int(offs[-1])) if offs is not None else (0, 0)
+            spans.append((c, bufs, str_bytes))
+            str_bytes += b1 - b0
+        else:
+            spans.append((c, bufs, 0))
+    col_ = N.Column()
+    N.check(N.lib().plgpu_column_alloc(dt.code, n, int(nulls > 0), str_bytes, C.byref(col_), None))
+    out = Series._from_native(name, col_)
+    row = 0
+    for c, bufs, byte in spans:
+        m = builtins.len(c)
+        if m:
+            vb = bufs[0].address if (c.null_count and bufs[0] is not None) else None
+            data = bufs[2].address if dt is String and bufs[2] is not None else None
+            N.check(N.lib().plgpu_ingest_chunk(C.byref(out._col), row, byte, bufs[1].address, vb, data,
+                                               c.offset, m, None))
+        row += m
+    N.check(N.lib().plgpu_synchronize(None))
+    out._col.null_count = nulls
+    return out
+
+
 # --------------------------------------------------------------- DataFrame
 class DataFrame:
     def __init__(self, data: Any = None, schema: Any = None):
@@ -525,6 +559,24 @@ class DataFrame:
     @classmethod
     def from_arrow(cls, table) -> "DataFrame":
         return cls([Series.from_arrow(nm, table.column(nm)) for nm in table.column_names])
+
+    @classmethod
+    def from_batches(cls, batches: Sequence[Any], columns: Sequence[str] | None = None) -> "DataFrame":
+        """Device frame from a list of Arrow RecordBatches, the form in which
+        the reference exports a DataFrame (PyDataFrame.to_arrow,
+        crates/polars-python/src/dataframe/export.rs:80): each column is
+        ingested chunk by chunk, without concatenating on the host."""
+        batches = list(batches)
+        if not batches:
+            raise N.InvalidOperationError("from_batches needs at least one RecordBatch (schema unknown)")
+        names = list(columns) if columns is not None else list(batches[0].schema.names)
+        out = []
+        for nm in names:
+            i = batches[0].schema.get_field_index(nm)
+            if i < 0:
+                raise N.ComputeError(f"column {nm!r} not found in the scanned batches")
+            out.append(_ingest_chunks(nm, [b.column(i) for b in batches], batches[0].schema.field(i).type))
+        return cls(out)
 
     def to_arrow(self):
         import pyarrow as pa
@@ -1018,12 +1070,12 @@ def _group_by_var(df: DataFrame, key: str | tuple, aggs: list[Expr], maintain_or
             plain.append((i, e))
     helpers = []
     for c in var_cols:
-        helpers += [col(c).sum().alias(f"__vs_{c}"), col(c).count().alias(f"__vn_{c}")]
+        # mean(): f64 from the exact sum of the values widened to f64, so an
+        # integer group whose sum overflows the input width does not wrap
+        # (the reference casts to f64 before its Welford update, var_std.rs)
+        helpers += [col(c).mean().alias(f"__vm_{c}"), col(c).count().alias(f"__vn_{c}")]
     first = _group_by(df, key, [e for _, e in plain] + helpers, True, pred, info)
-    means = [first[k] for k in keys]
-    for c in var_cols:
-        m = _eval((col(f"__vs_{c}") / col(f"__vn_{c}").cast("f64")).alias(f"__vm_{c}"), first)
-        means.append(m)
+    means = [first[k] for k in keys] + [first[f"__vm_{c}"] for c in var_cols]
     if builtins.len(keys) == 1 and df[keys[0]]._col.dtype in (N.I64, N.I32, N.U32, N.BOOL):
         # one integer key: squared deviations straight from a group-key table
         sq = []

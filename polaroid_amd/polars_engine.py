@@ -57,17 +57,38 @@ _BINOPS: dict[str, Callable[[Expr, Expr], Expr]] = {
     "LogicalAnd": lambda a, b: a & b, "LogicalOr": lambda a, b: a | b,
 }
 
+_ORDERED_CMP = frozenset({"Lt", "LtEq", "Gt", "GtEq"})
+
 _BOOLFUNCS: dict[str, Callable[[Expr], Expr]] = {
     "IsNull": lambda a: a.is_null(), "IsNotNull": lambda a: a.is_not_null(), "IsNan": lambda a: a.is_nan(),
     "IsFinite": lambda a: a.is_finite(), "Not": lambda a: ~a,
 }
 
 
+def _dtype_kind(dt) -> str:
+    """Name of a polars DataType as the visitor hands it over
+    (`Int64`, `Datetime(time_unit='ns', time_zone=None)`, `Enum(categories=...)`)."""
+    s = str(dt) if dt is not None else "?"
+    return s.split("(", 1)[0].split("[", 1)[0].strip()
+
+
+# dtypes whose columns the GPU path takes (anything else stays on polars)
+SUPPORTED_DTYPES = frozenset({"Int64", "Int32", "UInt32", "Float64", "Boolean", "String", "Categorical", "Enum"})
+
+
 class _Translator:
     def __init__(self, nt):
         self.nt = nt
+        # Enum columns order by category index, not lexically (logical/
+        # categorical.rs:58 uses_lexical_ordering; sort/categorical.rs:74):
+        # the GPU handles them as strings, so ordered uses stay on polars
+        self.enums: set[str] = set()
 
     # ---------------------------------------------------------- expressions
+    def _is_enum(self, node: int) -> bool:
+        e = self.view(node)
+        return _name(e) == "Column" and str(e.name) in self.enums
+
     def view(self, node: int):
         try:
             return self.nt.view_expression(node)
@@ -88,6 +109,8 @@ class _Translator:
             op = _enum_name(e.op)
             if op not in _BINOPS:
                 raise Unsupported(f"operator {op}")
+            if op in _ORDERED_CMP and (self._is_enum(e.left) or self._is_enum(e.right)):
+                raise Unsupported("ordered comparison on an Enum column (category order)")
             return _BINOPS[op](self.expr(e.left), self.expr(e.right))
         if k == "Cast":
             dt = str(e.dtype)
@@ -120,6 +143,8 @@ class _Translator:
         if _name(arg) != "Column":
             raise Unsupported("aggregation over a computed expression")
         c = col(str(arg.name))
+        if name in ("min", "max") and str(arg.name) in self.enums:
+            raise Unsupported(f"{name} of an Enum column (category order)")
         if name in ("sum", "mean"):
             return getattr(c, name)()
         if name in ("min", "max"):
@@ -143,7 +168,15 @@ class _Translator:
             if getattr(node, "selection", None) is not None:
                 raise Unsupported("scan predicate")
             proj = node.projection
-            return ("polars_scan", node.df, None if proj is None else list(proj))
+            schema = dict(self.nt.get_schema())  # the scan's output schema (visit.rs get_schema)
+            names = list(schema) if proj is None else list(proj)
+            for nm in names:
+                kind = _dtype_kind(schema.get(nm))
+                if kind not in SUPPORTED_DTYPES:
+                    raise Unsupported(f"column {nm!r} of dtype {schema.get(nm)}")
+                if kind == "Enum":
+                    self.enums.add(nm)
+            return ("polars_scan", node.df, None if proj is None else list(proj), schema)
         if k == "Join":
             # options: (how, nulls_equal, slice, suffix, coalesce, maintain_order), nodes.rs:536
             how, nulls_equal, slc, suffix, coalesce, order = node.options
@@ -181,6 +214,8 @@ class _Translator:
             desc = [bool(descending[i if len(descending) == k else 0]) for i in range(k)]
             nl = [bool(nulls_last[i if len(nulls_last) == k else 0]) for i in range(k)]
             child = self.child(node.input)
+            if any(str(b.name) in self.enums for b in bys):
+                raise Unsupported("sort by an Enum column (category order)")
             if k == 1:
                 return ("sort", child, str(bys[0].name), desc[0], nl[0])
             return ("sort", child, tuple(str(b.name) for b in bys), tuple(desc), tuple(nl))
@@ -234,16 +269,53 @@ def translate(nt) -> tuple:
     return _Translator(nt).plan()
 
 
+# PyDataFrame.to_arrow(compat_level): 0 / False = CompatLevel::oldest, whose
+# export uses large_string / large_binary instead of the view types
+# (crates/polars-python/src/conversion/mod.rs:1559 PyCompatLevel).
+_COMPAT_OLDEST = False
+
+
+def scan_batches(df) -> list:
+    """RecordBatches of a DataFrameScan's frame.  In the reference
+    `DataFrameScan.df` is a PyDataFrame (visitor/nodes.rs:190) whose
+    `to_arrow(compat_level)` returns one RecordBatch per chunk
+    (dataframe/export.rs:80-99); a wrapped polars DataFrame is unwrapped to
+    its PyDataFrame first (wrap_df's inverse, py-polars/src/polars/_utils/
+    wrap.py:12)."""
+    pydf = getattr(df, "_df", df)
+    return list(pydf.to_arrow(_COMPAT_OLDEST))
+
+
 def _bind_scans(node: tuple) -> tuple:
-    """Upload the polars DataFrames of the scans (Arrow -> HBM)."""
+    """Upload the scanned frames (RecordBatch chunks -> HBM)."""
     if node[0] == "polars_scan":
-        table = node[1].to_arrow()
-        if node[2] is not None:
-            table = table.select(node[2])
-        return ("scan", DataFrame.from_arrow(table))
+        _, df, proj, schema = node
+        batches = scan_batches(df)
+        names = proj if proj is not None else list(schema)
+        if not batches:
+            return ("scan", _empty_frame(names, schema))
+        return ("scan", DataFrame.from_batches(batches, names))
     if node[0] == "join":
         return (node[0], _bind_scans(node[1]), _bind_scans(node[2])) + tuple(node[3:])
     return (node[0], _bind_scans(node[1])) + tuple(node[2:])
+
+
+def _empty_frame(names: list, schema: dict) -> DataFrame:
+    """A zero-row frame with the scan's dtypes (to_arrow gives no batch)."""
+    import pyarrow as pa
+
+    from .frame import Series
+
+    arrow_of = {"Int64": pa.int64(), "Int32": pa.int32(), "UInt32": pa.uint32(), "Float64": pa.float64(),
+                "Boolean": pa.bool_(), "String": pa.large_string()}
+    cols = []
+    for nm in names:
+        kind = _dtype_kind(schema.get(nm))
+        t = arrow_of.get(kind, pa.large_string() if kind in ("Categorical", "Enum") else None)
+        if t is None:
+            raise Unsupported(f"column {nm!r} of dtype {schema.get(nm)}")
+        cols.append(Series.from_arrow(nm, pa.array([], t)))
+    return DataFrame(cols)
 
 
 def _to_polars(table):

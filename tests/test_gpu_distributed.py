@@ -225,6 +225,13 @@ def test_group_by_agg_world1_rccl_string_key(gpu):
         got = sorted(zip(out["sym"].to_list(), out["s"].to_list(), out["len"].to_list()), key=str)
         exp = sorted(zip(ref["sym"].to_list(), ref["s"].to_list(), ref["len"].to_list()), key=str)
         assert got == exp
+        # a predicate on the String key itself (lowered before the key becomes codes)
+        pred = (pl.col("sym") == "AAPL") | pl.col("sym").str.starts_with("S00")
+        out = D.group_by_agg(df, "sym", [pl.col("v").sum().alias("s"), pl.len()], pred)
+        ref = df.lazy().filter(pred).group_by("sym").agg(pl.col("v").sum().alias("s"), pl.len()).collect()
+        got = sorted(zip(out["sym"].to_list(), out["s"].to_list(), out["len"].to_list()), key=str)
+        exp = sorted(zip(ref["sym"].to_list(), ref["s"].to_list(), ref["len"].to_list()), key=str)
+        assert got == exp and len(got) == 1 + 100
         long_df = pl.DataFrame({"sym": pl.Series("sym", ["AAPL", "TOOLONGKEY"]), "v": pl.Series("v", [1.0, 2.0])})
         with pytest.raises(pl.InvalidOperationError, match="7 bytes"):
             D.group_by_agg(long_df, "sym", [pl.col("v").sum()])

@@ -115,3 +115,21 @@ def test_var_std_key_kinds(gpu, kind):
     assert np.array_equal(out["x"].validity_numpy(), ok)
     _close(out["x"].to_numpy(), std, ok)
     _close(out["v0"].to_numpy(), var0, ok0)
+
+
+@pytest.mark.parametrize("dt", [np.int32, np.uint32, np.int64])
+def test_var_std_integer_sums_past_input_width(gpu, dt):
+    """Groups whose integer sum overflows the column's width: the group mean
+    comes from the exact f64 sum, so three rows of 2e9 (Int32 / UInt32) have
+    variance 0, not ~2e18 from a wrapped sum (var_std.rs casts to f64)."""
+    big = {np.int32: 2_000_000_000, np.uint32: 4_000_000_000, np.int64: 4_000_000_000_000_000_000}[dt]
+    key = np.array([0, 0, 0, 1, 1, 2], np.int64)
+    x = np.array([big, big, big, big, big - 2, 7], dt)
+    df = pl.DataFrame({"k": pl.Series.from_numpy("k", key), "x": pl.Series.from_numpy("x", x)})
+    out = df.group_by("k", maintain_order=True).agg(pl.col("x").var().alias("v"), pl.col("x").std(0).alias("s"))
+    xs = x.astype(np.float64)
+    want_v = [0.0, float(np.var(xs[3:5], ddof=1)), None]
+    got_v = out["v"].to_list()
+    assert got_v[0] == 0.0 and got_v[2] is None
+    assert abs(got_v[1] - want_v[1]) <= 1e-12 * abs(want_v[1])
+    assert out["s"].to_list()[0] == 0.0 and out["s"].to_list()[2] == 0.0

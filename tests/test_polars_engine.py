@@ -4,7 +4,10 @@ crates/polars-python/src/lazyframe/visitor/{nodes,expr_nodes}.rs with the
 same class and attribute names, and the traverser methods of
 crates/polars-python/src/lazyframe/visit.rs (view_current_node, get_node,
 set_node, view_expression, get_schema, set_udf).  polars itself is not
-installed here, so polars DataFrames are modelled by their Arrow export.
+installed here, so `DataFrameScan.df` is modelled as the reference's
+PyDataFrame: `to_arrow(compat_level)` with no default, returning one Arrow
+RecordBatch per chunk (crates/polars-python/src/dataframe/export.rs:80-99),
+and `get_schema` hands out dtype objects whose str() is polars' dtype repr.
 """
 
 import math
@@ -35,12 +38,44 @@ class PyExprIR:
         self.node, self.output_name = node, output_name
 
 
-class FakePolarsDF:
-    def __init__(self, table):
-        self.table = table
+class FakePyDataFrame:
+    """Model of the reference's PyDataFrame (DataFrameScan.df, visitor/nodes.rs:190)."""
 
-    def to_arrow(self):
-        return self.table
+    def __init__(self, table, chunk_rows=None):
+        self.table = table
+        self.chunk_rows = chunk_rows
+        self.calls = []
+
+    def to_arrow(self, compat_level):  # export.rs:80: no default for compat_level
+        if not isinstance(compat_level, (bool, int)):
+            raise TypeError("'compat_level' argument accepts int or bool")  # conversion/mod.rs:1574
+        self.calls.append(compat_level)
+        t = self.table
+        if compat_level is False or compat_level == 0:  # CompatLevel::oldest: large_string, no views
+            t = t.cast(pa.schema([pa.field(f.name, pa.large_string() if f.type == pa.string() else f.type)
+                                  for f in t.schema]))
+        return t.to_batches(max_chunksize=self.chunk_rows)
+
+
+FakePolarsDF = FakePyDataFrame
+
+
+class _DType:
+    """A polars DataType as the visitor returns it (only its repr matters here)."""
+
+    def __init__(self, s):
+        self.s = s
+
+    def __str__(self):
+        return self.s
+
+    __repr__ = __str__
+
+
+_ARROW_TO_POLARS = {pa.int64(): "Int64", pa.int32(): "Int32", pa.uint32(): "UInt32", pa.float64(): "Float64",
+                    pa.bool_(): "Boolean", pa.string(): "String", pa.large_string(): "String",
+                    pa.timestamp("ns"): "Datetime(time_unit='ns', time_zone=None)", pa.float32(): "Float32",
+                    pa.list_(pa.int64()): "List(Int64)"}
 
 
 class FakeNT:
@@ -49,6 +84,16 @@ class FakeNT:
         self.root = None
         self.udf = None
         self.table = table
+        self.dtypes = {}
+        if table is not None:
+            self.add_dtypes(table)
+
+    def add_dtypes(self, table):
+        for f in table.schema:
+            if pa.types.is_dictionary(f.type):
+                self.dtypes[f.name] = "Categorical"
+            else:
+                self.dtypes[f.name] = _ARROW_TO_POLARS.get(f.type, str(f.type))
 
     # builders
     def e(self, kind, **kw):
@@ -84,7 +129,7 @@ class FakeNT:
         return self.ex[n]
 
     def get_schema(self):
-        return {k: None for k in self.schemas[self.root]}
+        return {k: _DType(self.dtypes.get(k, "Float64")) for k in self.schemas[self.root]}
 
     def set_udf(self, fn, is_pure=False):
         self.udf = fn
@@ -272,3 +317,114 @@ def test_translate_multi_column_sort():
     nt.lp[nt.root].sort_options = (False, [True], [False])
     plan = PE.translate(nt)
     assert plan[3] == (False, False) and plan[4] == (True, True)
+
+
+# ------------------------------------------------------------ scan binding
+def test_scan_calls_to_arrow_with_compat_level_and_takes_batches():
+    table = _table(1000)[0]
+    df = FakePyDataFrame(table, chunk_rows=300)
+    batches = PE.scan_batches(df)
+    assert df.calls == [False] and len(batches) == 4
+    assert all(isinstance(b, pa.RecordBatch) for b in batches)
+
+    class Wrapped:  # a polars DataFrame: its PyDataFrame is `_df`
+        _df = df
+
+    assert len(PE.scan_batches(Wrapped())) == 4
+
+
+def test_unsupported_scan_dtype_falls_back_without_error():
+    table = _table()[0]
+    nt = _filter_groupby_ir(table)
+    nt.dtypes["w"] = "List(Int64)"
+    PE.execute_with_polaroid(nt, None)  # polars keeps the query: no UDF, no error
+    assert nt.udf is None
+    with pytest.raises(pl.InvalidOperationError):
+        PE.execute_with_polaroid(nt, None, config={"raise_on_fail": True})
+    # a projection that leaves the column out is fine
+    nt2 = _filter_groupby_ir(table)
+    nt2.dtypes["x"] = "Decimal(precision=10, scale=2)"
+    nt2.schemas[0] = ["k", "v", "w", "x"]
+    nt2.lp[0].projection = ["k", "v", "w"]
+    PE.execute_with_polaroid(nt2, None)
+    assert callable(nt2.udf)
+
+
+def _enum_nt():
+    cats = pa.array(["zeta", "alpha", "mid"])
+    e = pa.DictionaryArray.from_arrays(pa.array([0, 1, 2, 0, 1], pa.uint32()), cats)
+    table = pa.table({"e": e, "v": pa.array([1.0, 2.0, 3.0, 4.0, 5.0])})
+    nt = FakeNT(table)
+    nt.dtypes["e"] = "Enum(categories=['zeta', 'alpha', 'mid'])"
+    scan = nt.p("DataFrameScan", ["e", "v"], df=FakePyDataFrame(table), projection=None, selection=None)
+    return nt, scan
+
+
+def test_enum_ordered_uses_stay_on_polars():
+    # Enum orders by category index (logical/categorical.rs:58, sort/categorical.rs:74),
+    # the GPU handles it as strings: sort / ordered comparisons / min / max go to polars
+    nt, scan = _enum_nt()
+    nt.p("Sort", ["e", "v"], input=scan, by_column=[PyExprIR(nt.col("e"), "e")],
+         sort_options=(False, [False], [False]), slice=None)
+    with pytest.raises(PE.Unsupported, match="Enum"):
+        PE.translate(nt)
+    nt, scan = _enum_nt()
+    nt.p("Filter", ["e", "v"], input=scan, predicate=PyExprIR(nt.bin(nt.col("e"), "Lt", nt.lit("mid")), "e"))
+    with pytest.raises(PE.Unsupported, match="Enum"):
+        PE.translate(nt)
+    nt, scan = _enum_nt()
+    a = nt.e("Agg", name="max", arguments=[nt.col("e")], options=False)
+    opts = _node("GroupbyOptions", slice=None, dynamic=None, rolling=None)
+    nt.p("GroupBy", ["v", "e"], input=scan, keys=[PyExprIR(nt.col("v"), "v")], aggs=[PyExprIR(a, "e")],
+         apply=None, maintain_order=True, options=opts)
+    with pytest.raises(PE.Unsupported, match="Enum"):
+        PE.translate(nt)
+    # equality on an Enum is order-free and stays on the GPU path
+    nt, scan = _enum_nt()
+    nt.p("Filter", ["e", "v"], input=scan, predicate=PyExprIR(nt.bin(nt.col("e"), "Eq", nt.lit("mid")), "e"))
+    assert PE.translate(nt)[0] == "filter"
+
+
+@pytest.mark.gpu
+def test_udf_multi_chunk_scan_on_gpu(gpu):
+    """Chunks of 777 rows: validity and Boolean bits land at bit offsets that
+    are not byte aligned; strings are rebased per chunk; a dictionary column
+    is unified across chunks."""
+    rng = np.random.default_rng(11)
+    n = 10_000
+    k = rng.integers(0, 9, n).astype(np.int64)
+    v = rng.standard_normal(n)
+    vmask = rng.random(n) < 0.2
+    b = rng.random(n) < 0.5
+    bmask = rng.random(n) < 0.1
+    sym = np.array(["AAPL", "MSFT", "", "GOOGLEPLEX_LONG_NAME", "Ä€"])[rng.integers(0, 5, n)]
+    smask = rng.random(n) < 0.15
+    table = pa.table({"k": pa.array(k), "v": pa.array(v, mask=vmask), "b": pa.array(b, mask=bmask),
+                      "s": pa.array(sym.tolist(), mask=smask), "w": pa.array(k.astype(np.int32) * 3)})
+    nt = FakeNT(table)
+    nt.p("DataFrameScan", ["k", "v", "b", "s", "w"], df=FakePyDataFrame(table, chunk_rows=777), projection=None,
+         selection=None)
+    PE.execute_with_polaroid(nt, None, to_frame=lambda t: t)
+    out = nt.udf(None, None, None, False)
+    for name in ("k", "v", "b", "s", "w"):
+        assert out.column(name).to_pylist() == table.column(name).to_pylist(), name
+
+
+@pytest.mark.gpu
+def test_from_arrow_sliced_chunks(gpu):
+    rng = np.random.default_rng(5)
+    base = pa.array(rng.standard_normal(5000), mask=rng.random(5000) < 0.3)
+    bools = pa.array(rng.random(5000) < 0.5, mask=rng.random(5000) < 0.3)
+    strs = pa.array([None if i % 7 == 0 else "x" * (i % 13) for i in range(5000)], pa.large_string())
+    for arr in (base, bools, strs):
+        chunks = [arr.slice(3, 100), arr.slice(1001, 1), arr.slice(0, 0), arr.slice(2000, 2999), arr.slice(13, 64)]
+        ca = pa.chunked_array(chunks, type=arr.type)
+        s = pl.Series.from_arrow("x", ca)
+        assert s.to_list() == ca.to_pylist()
+        assert s.null_count() == ca.null_count
+    # all-valid chunk next to a chunk with nulls: the column gets a validity
+    ca = pa.chunked_array([pa.array([1, 2, 3], pa.int64()), pa.array([None, 5], pa.int64())])
+    assert pl.Series.from_arrow("y", ca).to_list() == [1, 2, 3, None, 5]
+    # an empty frame of batches keeps its columns
+    df = pl.DataFrame.from_batches([pa.record_batch({"a": pa.array([], pa.int64())})])
+    assert df.height == 0 and df.columns == ["a"]
