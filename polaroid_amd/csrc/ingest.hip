@@ -7,12 +7,21 @@
 // destination column, bitmaps (validity, Boolean values) at any bit offset
 // are placed by a device kernel, String offsets are rebased on the device.
 //
-// Copies are staged through two pinned host buffers: the CPU fills one
-// (several threads) while the DMA engine drains the other, so the pageable
-// Arrow buffers reach HBM at the pinned-copy rate without pinning them.
+// Copy modes (PLGPU_INGEST_MODE), measured with tools/bench_ingest.py on one
+// MI355X box (1e8-row OHLCV table, profiles/r02_ingest.jsonl):
+//   pageable (default)  the HIP runtime's own staged copy of the pageable
+//                       Arrow buffer: 49.0 GB/s at 1M-row chunks, 55.7 GB/s
+//                       at 8M-row chunks (the host link's rate: 56.6 GB/s
+//                       for whole columns);
+//   register            pin the source pages in place, DMA, unpin:
+//                       51.2 / 56.6 GB/s;
+//   staged              our double-buffered hipHostMalloc pair filled by
+//                       host threads: 31.6 / 50.7 GB/s (the host memcpy into
+//                       the pinned buffer is the bottleneck).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <thread>
@@ -72,10 +81,41 @@ void host_copy(void* dst, const void* src, size_t n, int threads) {
 
 }  // namespace
 
-// Host -> device copy through the pinned staging pair, asynchronous on `s`
-// (the source may be reused as soon as this returns).
+// Copy mode of h2d_staged (PLGPU_INGEST_MODE, read once): 1 = the runtime's
+// own pageable copy (default), 0 = our pinned staging pair, 2 = register
+// (pin) the source range in place and DMA from it.
+static int ingest_mode() {
+    static int mode = -1;
+    if (mode < 0) {
+        const char* e = getenv("PLGPU_INGEST_MODE");
+        mode = 1;
+        if (e && !strcmp(e, "staged")) mode = 0;
+        if (e && !strcmp(e, "register")) mode = 2;
+    }
+    return mode;
+}
+
+// Host -> device copy, asynchronous on `s` (the source may be reused as
+// soon as this returns).
 int h2d_staged(void* dst, const void* src, size_t n, hipStream_t s) {
     if (n == 0) return PLGPU_OK;
+    const int mode = ingest_mode();
+    if (mode == 1) {
+        PLGPU_HIP(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, s));
+        return PLGPU_OK;
+    }
+    if (mode == 2 && n >= (size_t(1) << 20)) {
+        // pin the pages in place, DMA, unpin once the copy has completed
+        const uintptr_t a0 = (uintptr_t)src & ~uintptr_t(4095);
+        const size_t len = (((uintptr_t)src + n + 4095) & ~uintptr_t(4095)) - a0;
+        PLGPU_HIP(hipHostRegister((void*)a0, len, hipHostRegisterDefault));
+        void* dsrc = nullptr;
+        PLGPU_HIP(hipHostGetDevicePointer(&dsrc, (void*)a0, 0));
+        PLGPU_HIP(hipMemcpyAsync(dst, (const char*)dsrc + ((uintptr_t)src - a0), n, hipMemcpyDeviceToDevice, s));
+        PLGPU_HIP(hipStreamSynchronize(s));
+        PLGPU_HIP(hipHostUnregister((void*)a0));
+        return PLGPU_OK;
+    }
     Staging& S = staging();
     std::lock_guard<std::mutex> lk(S.mu);
     int rc = staging_init(S);
