@@ -40,42 +40,46 @@ constexpr int kJnTileRows = 4096;          // probe tile (16 rows per thread)
 constexpr int kJnProbeLimit = 1 << 16;      // linear-probe bound before "table full"
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
 
-// Table: keys[cap] (8 B, EMPTY = INT64_MIN) and ref[cap + 2] (4 B):
+// Table: cap + 2 cells of 16 B {key (EMPTY = INT64_MIN), ref}, 8 cells per
+// 128-B bucket (one L2 line).  A key's home bucket is hash_slot(key, bbits)
+// and it takes the first free cell from the start of that bucket on
+// (linear probing over cells, so a full bucket overflows into the next).
+// The ref word:
 //   ref < 2^31          the single build row of a unique key;
 //   ref == kRefList     duplicate key: rows[off[s] .. off[s + 1]);
 //   ref == kRefNone     no build row (special slots only).
-// Slots cap / cap + 1 are the null key / INT64_MIN key.  For 1e7 build rows
-// keys + ref are 201 MB, inside the 256 MiB Infinity Cache.
+// Cells cap / cap + 1 are the null key / INT64_MIN key.  For 1e7 build
+// rows the cells take 268 MB.
+//
+// The probe is bound by random line requests, not bytes: on MI355X about
+// 55 G random requests/s whether a request reads 8, 64 or 128 B, from a
+// table of 128 MB - 2 GB (tools/randread_bench.hip, profiles/
+// r02_randread.txt).  Eight lanes read a probe's home bucket together (one
+// 16-B load each, one line request), so a probe costs ~1.1 requests; the
+// round-1 layout (8-B keys, then a separate ref array) cost ~1.8.
 constexpr uint32_t kRefList = 0x80000000u;
 constexpr uint32_t kRefNone = 0xFFFFFFFFu;
+constexpr int kBktCells = 8;  // cells per 128-B bucket
 
 struct JnTable {
-    uint64_t* keys;
-    uint32_t* ref;
+    uint4* cells;      // cap + 2 cells {key lo, key hi, ref, -}: cap / 8 buckets of 8, then the 2 special slots
     uint32_t* off;     // cap + 3 CSR offsets (duplicate keys only)
     uint32_t* rows;    // CSR row lists
-    int bits;
+    int bits;          // cap = 2^bits cells
+    int bbits;         // 2^bbits buckets
     int64_t cap;
 };
 
-// Slot of `key`, or -1.  Keys are read with plain loads: the table is
-// immutable during the probe.
-__device__ __forceinline__ int64_t jn_find(const JnTable& t, uint64_t key) {
-    const uint64_t mask = (uint64_t)t.cap - 1;
-    uint64_t s = hash_slot(key, t.bits);
-    for (int i = 0; i < kJnProbeLimit; ++i, s = (s + 1) & mask) {
-        const uint64_t k = t.keys[s];
-        if (k == key) return (int64_t)s;
-        if (k == kEmptyKey) return -1;
-    }
-    return -1;
-}
+// Cell s of the table: its key (8 B) and ref word (4 B); one 16-B load
+// returns both.
+__device__ __forceinline__ uint64_t& jn_key(const JnTable& t, int64_t s) { return ((uint64_t*)t.cells)[2 * s]; }
+__device__ __forceinline__ uint32_t& jn_ref(const JnTable& t, int64_t s) { return ((uint32_t*)t.cells)[4 * s + 2]; }
 
 // ---------------------------------------------------------------- build
 __global__ void jn_init_kernel(JnTable t, uint32_t* cnt) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < t.cap + 2;
          i += (int64_t)gridDim.x * blockDim.x) {
-        if (i < t.cap) t.keys[i] = kEmptyKey;
+        if (i < t.cap) jn_key(t, i) = kEmptyKey;
         cnt[i] = 0;
     }
 }
@@ -95,11 +99,11 @@ __global__ void jn_build_kernel(DevCol bk, int64_t nb, JnTable t, bool nulls_equ
                 slot = t.cap + 1;
             } else {
                 slot = -2;
-                uint64_t s = hash_slot(key, t.bits);
+                uint64_t s = (uint64_t)hash_slot(key, t.bbits) * kBktCells;
                 for (int p = 0; p < kJnProbeLimit; ++p, s = (s + 1) & mask) {
-                    uint64_t k = __hip_atomic_load(&t.keys[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    uint64_t k = __hip_atomic_load(&jn_key(t, s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     if (k == kEmptyKey) {
-                        k = atomicCAS((unsigned long long*)&t.keys[s], (unsigned long long)kEmptyKey,
+                        k = atomicCAS((unsigned long long*)&jn_key(t, s), (unsigned long long)kEmptyKey,
                                       (unsigned long long)key);
                         if (k == kEmptyKey) k = key;
                     }
@@ -133,7 +137,7 @@ __global__ void jn_offsets_kernel(JnTable t, const uint32_t* __restrict__ cnt, c
         t.off[s] = (uint32_t)off64[s];
         if (s < t.cap + 2) {
             const uint32_t c = cnt[s];
-            t.ref[s] = c == 0 ? kRefNone : kRefList;
+            jn_ref(t, s) = c == 0 ? kRefNone : kRefList;
             mx = c > mx ? c : mx;
         }
     }
@@ -158,7 +162,7 @@ __global__ void jn_scatter_kernel(int64_t nb, JnTable t, const uint32_t* __restr
 __global__ void jn_unique_ref_kernel(JnTable t) {
     for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < t.cap + 2;
          s += (int64_t)gridDim.x * blockDim.x) {
-        if (t.off[s + 1] - t.off[s] == 1) t.ref[s] = t.rows[t.off[s]];
+        if (t.off[s + 1] - t.off[s] == 1) jn_ref(t, s) = t.rows[t.off[s]];
     }
 }
 
@@ -224,14 +228,29 @@ constexpr uint32_t kNullIdx = 0xFFFFFFFFu;  // null index in an output pair
 // kRefList | slot for a duplicate key, or kRefNone) and per-tile output
 // counts.  The probe keys are streamed with non-temporal loads so they do
 // not evict the table from the Infinity Cache.
+// Per round k a wave looks up its 64 rows in 8 sub-rounds: in sub-round j
+// lane group g = lane / 8 reads the bucket of row (8j + g) of the wave, each
+// lane one 16-B cell.  Rows' keys and buckets reach the groups through LDS,
+// and the (ref, slot) of a matching cell goes back to the row's lane the
+// same way; ballots tell the row's lane whether its bucket held the key or
+// an empty cell (a full bucket without the key continues, lane by lane, in
+// the next buckets - rare at load <= 0.6).
 template <bool NULLABLE, int MODE, bool MARK>
 __global__ __launch_bounds__(kJnThreads) void jn_probe_match_kernel(DevCol pk, int64_t np, JnTable t,
-                                                                    bool nulls_equal, uint32_t* __restrict__ m,
-                                                                    uint64_t* __restrict__ tile_counts,
-                                                                    int64_t ntiles, uint8_t* __restrict__ flags) {
+                                                                  bool nulls_equal, uint32_t* __restrict__ m,
+                                                                  uint64_t* __restrict__ tile_counts, int64_t ntiles,
+                                                                  uint8_t* __restrict__ flags) {
     __shared__ uint64_t wsum[kJnThreads / 64];
+    __shared__ uint4 rowbuf[kJnThreads];  // {key lo, key hi, bucket, regular}
+    __shared__ uint2 hitbuf[kJnThreads];  // {ref, slot} of the matching cell
     const uint64_t* kp = (const uint64_t*)pk.values + pk.offset;
     const bool wide = pk.dtype == PLGPU_I64;
+    const int lane = threadIdx.x & 63;
+    const int wbase = threadIdx.x & ~63;
+    const int g = lane >> 3, e = lane & 7;
+    const int bbits = t.bbits;
+    const uint4* __restrict__ bkt = t.cells;
+    const uint64_t nbm = (uint64_t(1) << bbits) - 1;
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         constexpr int R = kJnTileRows / kJnThreads;
         uint64_t key[R];
@@ -246,68 +265,90 @@ __global__ __launch_bounds__(kJnThreads) void jn_probe_match_kernel(DevCol pk, i
                 if (NULLABLE) valid[k] = dev_valid(pk, r) ? true : false;
             }
         }
-        // batched first probes: every row's home slot is loaded before any
-        // comparison, so the table reads of the 16 rows overlap
-        int64_t slot[R];
-        uint64_t home[R];
-        const uint64_t mask = (uint64_t)t.cap - 1;
-#pragma unroll
-        for (int k = 0; k < R; ++k) {
-            slot[k] = (int64_t)hash_slot(key[k], t.bits);
-            home[k] = t.keys[slot[k]];
-        }
-#pragma unroll
+        uint64_t c = 0;
         for (int k = 0; k < R; ++k) {
             const int64_t r = tile * kJnTileRows + (int64_t)k * kJnThreads + threadIdx.x;
-            if (r >= np || (NULLABLE && !valid[k])) {
-                slot[k] = (r < np && NULLABLE && !valid[k] && nulls_equal) ? t.cap : -1;
-            } else if (key[k] == kEmptyKey) {
-                slot[k] = t.cap + 1;
-            } else if (home[k] == key[k]) {
-                // hit at the home slot
-            } else if (home[k] == kEmptyKey) {
-                slot[k] = -1;
-            } else {
-                // continue the linear probe from the next slot
-                uint64_t sl = ((uint64_t)slot[k] + 1) & mask;
-                slot[k] = -1;
-                for (int i = 1; i < kJnProbeLimit; ++i, sl = (sl + 1) & mask) {
-                    const uint64_t kk = t.keys[sl];
-                    if (kk == key[k]) {
-                        slot[k] = (int64_t)sl;
-                        break;
-                    }
-                    if (kk == kEmptyKey) break;
+            const bool regular = r < np && (!NULLABLE || valid[k]) && key[k] != kEmptyKey;
+            const uint32_t b = (uint32_t)hash_slot(key[k], bbits);
+            rowbuf[threadIdx.x] = make_uint4((uint32_t)key[k], (uint32_t)(key[k] >> 32), b, regular ? 1u : 0u);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            uint4 rq[kBktCells];
+            uint4 cell[kBktCells];
+#pragma unroll
+            for (int j = 0; j < kBktCells; ++j) {
+                rq[j] = rowbuf[wbase + 8 * j + g];
+                cell[j] = rq[j].w ? bkt[(uint64_t)rq[j].z * kBktCells + e] : make_uint4(0u, 0u, 0u, 0u);
+            }
+            uint64_t beq = 0, bem = 0;
+#pragma unroll
+            for (int j = 0; j < kBktCells; ++j) {
+                const bool live = rq[j].w != 0;
+                const bool eq = live && cell[j].x == rq[j].x && cell[j].y == rq[j].y;
+                const bool em = live && cell[j].x == 0u && cell[j].y == 0x80000000u;
+                const uint64_t eqm = __ballot(eq), emm = __ballot(em);
+                if (eq) hitbuf[wbase + 8 * j + g] = make_uint2(cell[j].z, rq[j].z * kBktCells + e);
+                // this lane's row was served in sub-round lane / 8 by group lane % 8
+                if ((lane >> 3) == j) {
+                    beq = (eqm >> (8 * (lane & 7))) & 0xFFull;
+                    bem = (emm >> (8 * (lane & 7))) & 0xFFull;
                 }
             }
-        }
-        uint32_t ref[R];
-#pragma unroll
-        for (int k = 0; k < R; ++k) {
-            if (MODE == JM_DRAIN) ref[k] = (slot[k] >= 0 && flags[slot[k]]) ? 0u : kRefNone;
-            else ref[k] = slot[k] >= 0 ? t.ref[slot[k]] : kRefNone;
-        }
-        uint64_t c = 0;
-#pragma unroll
-        for (int k = 0; k < R; ++k) {
-            const int64_t r = tile * kJnTileRows + (int64_t)k * kJnThreads + threadIdx.x;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            int64_t slot = -1;
+            uint32_t ref = kRefNone;
+            if (r >= np || (NULLABLE && !valid[k])) {
+                if (r < np && NULLABLE && !valid[k] && nulls_equal) slot = t.cap;
+            } else if (key[k] == kEmptyKey) {
+                slot = t.cap + 1;
+            } else if (beq) {
+                const uint2 h = hitbuf[threadIdx.x];
+                ref = h.x;
+                slot = h.y;
+            } else if (!bem) {
+                // the home bucket is full without the key: later buckets
+                uint64_t bb = (b + 1) & nbm;
+                for (uint64_t i = 0; i < nbm; ++i, bb = (bb + 1) & nbm) {
+                    bool stop = false;
+                    for (int ee = 0; ee < kBktCells; ++ee) {
+                        const uint4 x = bkt[bb * kBktCells + ee];
+                        const uint64_t kk = (uint64_t)x.x | ((uint64_t)x.y << 32);
+                        if (kk == key[k]) {
+                            ref = x.z;
+                            slot = (int64_t)(bb * kBktCells + ee);
+                            stop = true;
+                            break;
+                        }
+                        if (kk == kEmptyKey) {
+                            stop = true;
+                            break;
+                        }
+                    }
+                    if (stop) break;
+                }
+            }
+            if (slot >= t.cap) ref = jn_ref(t, slot);  // null / INT64_MIN key slots
+            if (MODE == JM_DRAIN) ref = (slot >= 0 && flags[slot]) ? 0u : kRefNone;
             if (r >= np) continue;
-            const bool hit = ref[k] != kRefNone;
+            const bool hit = ref != kRefNone;
             uint32_t w = kRefNone;
             if (MODE == JM_SEMI || MODE == JM_ANTI || MODE == JM_DRAIN) {
                 w = hit ? 0u : kRefNone;
                 c += (MODE == JM_SEMI) == hit ? 1 : 0;
             } else {
-                if (ref[k] == kRefList) {
-                    w = kRefList | (uint32_t)slot[k];
-                    c += t.off[slot[k] + 1] - t.off[slot[k]];
+                if (ref == kRefList) {
+                    w = kRefList | (uint32_t)slot;
+                    c += t.off[slot + 1] - t.off[slot];
                 } else if (hit) {
-                    w = ref[k];
+                    w = ref;
                     c += 1;
                 } else if (MODE == JM_OUTER) {
                     c += 1;
                 }
-                if (MARK && hit) flags[slot[k]] = 1;
+                if (MARK && hit) flags[slot] = 1;
             }
             __builtin_nontemporal_store(w, m + r);
         }
@@ -433,7 +474,7 @@ __global__ __launch_bounds__(256) void pj_bcount_kernel(JnTable t, uint32_t* __r
     for (int i = threadIdx.x; i < (1 << kPjMaxBits); i += blockDim.x) h[i] = 0;
     __syncthreads();
     for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < t.cap; s += (int64_t)gridDim.x * blockDim.x) {
-        const uint64_t k = t.keys[s];
+        const uint64_t k = jn_key(t, s);
         if (k != kEmptyKey) atomicAdd(&h[pj_part(pj_hash(k), kPjMaxBits)], 1u);
     }
     __syncthreads();
@@ -449,11 +490,11 @@ __global__ void pj_init_kernel(PjTab pt, int64_t slots) {
 __global__ __launch_bounds__(256) void pj_binsert_kernel(JnTable t, PjTab pt) {
     const uint64_t mask = (1ull << pt.cbits) - 1;
     for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < t.cap; s += (int64_t)gridDim.x * blockDim.x) {
-        const uint64_t k = t.keys[s];
+        const uint64_t k = jn_key(t, s);
         if (k == kEmptyKey) continue;
         const uint64_t h = pj_hash(k);
         const uint64_t base = (uint64_t)pj_part(h, pt.pb) << pt.cbits;
-        const uint32_t ref = t.ref[s];
+        const uint32_t ref = jn_ref(t, s);
         const uint32_t w = ref == kRefList ? (kRefList | (uint32_t)s) : ref;
         uint64_t sl = h & mask;
         for (uint64_t i = 0; i <= mask; ++i, sl = (sl + 1) & mask) {
@@ -610,7 +651,7 @@ __global__ __launch_bounds__(kJnThreads) void pj_match_kernel(const uint64_t* __
             if (r >= special_lo) {
                 // null (nulls_equal) or INT64_MIN key: the global special slots
                 const int64_t gs = dev_valid(pk, prow[r]) ? t.cap + 1 : t.cap;
-                const uint32_t ref = t.ref[gs];
+                const uint32_t ref = jn_ref(t, gs);
                 w[k] = ref == kRefList ? (kRefList | (uint32_t)gs) : ref;
             } else {
                 uint64_t sl = slot[k];
@@ -836,8 +877,7 @@ struct JnBuilt {
 };
 
 static void jn_free(JnBuilt& b, hipStream_t s) {
-    dev_free(b.t.keys, s);
-    dev_free(b.t.ref, s);
+    dev_free(b.t.cells, s);
     dev_free(b.t.off, s);
     dev_free(b.t.rows, s);
     std::memset(&b.t, 0, sizeof b.t);
@@ -860,9 +900,10 @@ static int jn_build(const plgpu_column* key, bool nulls_equal, bool ordered, JnB
     JnBuilt b;
     for (int attempt = 0; !rc; ++attempt) {
         b.t.bits = bits;
+        b.t.bbits = bits - 3;
         b.t.cap = int64_t(1) << bits;
         const int64_t ne = b.t.cap + 2;
-        if ((rc = dev_alloc((void**)&b.t.keys, b.t.cap * 8, s))) break;
+        if ((rc = dev_alloc((void**)&b.t.cells, ne * 16, s))) break;
         if ((rc = dev_alloc((void**)&cnt, ne * 4, s))) break;
         PLGPU_HIP(hipMemsetAsync(status, 0, 16, s));
         const int gi = (int)std::min<int64_t>((ne + 255) / 256, 256 * 32);
@@ -880,14 +921,13 @@ static int jn_build(const plgpu_column* key, bool nulls_equal, bool ordered, JnB
             rc = fail(PLGPU_ERR_CAPACITY, "join build table did not converge");
             break;
         }
-        dev_free(b.t.keys, s);
+        dev_free(b.t.cells, s);
         dev_free(cnt, s);
-        b.t.keys = nullptr;
+        b.t.cells = nullptr;
         cnt = nullptr;
         bits += 2;
     }
     const int64_t ne = b.t.cap + 2;
-    if (!rc) rc = dev_alloc((void**)&b.t.ref, ne * 4, s);
     if (!rc) rc = dev_alloc((void**)&b.t.off, (ne + 1) * 4, s);
     if (!rc) rc = dev_alloc((void**)&off64, (ne + 1) * 8, s);
     if (!rc) rc = dev_alloc((void**)&part, ((ne + kScanChunk - 1) / kScanChunk + 1) * 8, s);
