@@ -50,8 +50,16 @@ enum plgpu_dtype {
     PLGPU_I64 = 3,  /* "l"                                             */
     PLGPU_F64 = 4,  /* "g"                                             */
     PLGPU_U32 = 5,  /* "I"  polars IdxSize (count / len outputs)       */
-    PLGPU_STR = 6   /* "U"  large_string: int64 offsets in `values`,
+    PLGPU_STR = 6,  /* "U"  large_string: int64 offsets in `values`,
                        UTF-8 bytes in `data` (polars String / Binary)   */
+    PLGPU_I8 = 7,   /* "c"                                             */
+    PLGPU_I16 = 8,  /* "s"                                             */
+    PLGPU_U8 = 9,   /* "C"                                             */
+    PLGPU_U16 = 10, /* "S"                                             */
+    PLGPU_U64 = 11, /* "L"                                             */
+    PLGPU_F32 = 12  /* "f"                                             */
+    /* polars' temporal types travel as their physical integers: Datetime /
+     * Duration as PLGPU_I64, Date as PLGPU_I32 (the host keeps the unit). */
 };
 
 /* One Arrow array in device memory (Arrow C Device Data Interface,
@@ -80,15 +88,35 @@ enum plgpu_opcode {
     PLGPU_OP_LIT_I64 = 3,   /* push i64 literal imm.i64                         */
     PLGPU_OP_LIT_BOOL = 4,  /* push bool literal imm.i64 != 0                   */
     PLGPU_OP_LIT_NULL = 5,  /* push typed null (arg = plgpu_dtype)              */
-    /* arithmetic: polars-compute/src/arithmetic/{signed,float}.rs;
-     * int (+,-,*) wrap; int op float -> float; `/` is true division (f64). */
+    /* arithmetic: polars-compute/src/arithmetic/{signed,unsigned,float}.rs.
+     * Operands are coerced to their supertype first
+     * (polars-core/src/utils/supertype.rs, dynamic literals included: an
+     * integer literal takes the smallest type that holds it, a float
+     * literal takes the float column's type or Float64), and integer
+     * results wrap at the supertype's width.  LIT_I64 / LIT_F64 are the
+     * dynamic (untyped) literals; CAST gives a literal a concrete type. */
     PLGPU_OP_ADD = 10,
     PLGPU_OP_SUB = 11,
     PLGPU_OP_MUL = 12,
-    PLGPU_OP_TRUEDIV = 13,
+    PLGPU_OP_TRUEDIV = 13,  /* ints -> Float64; float / literal = x * (1 / lit)
+                               (true_div_scalar, arithmetic/float.rs:113)    */
     PLGPU_OP_NEG = 14,
     PLGPU_OP_ABS = 15,
     PLGPU_OP_CAST_F64 = 16,
+    PLGPU_OP_FLOORDIV = 17, /* ints: floor division, x // 0 = null
+                               (floor_divmod.rs:39); floats: floor(a / b)    */
+    PLGPU_OP_MOD = 18,      /* ints: remainder with the divisor's sign, x % 0
+                               = null; floats: a - b * floor(a / b)          */
+    PLGPU_OP_DIVIDE = 19,   /* Operator::Divide (legacy_div, arithmetic/mod.rs:40):
+                               floor division for ints, true division for floats */
+    PLGPU_OP_CAST = 50,     /* cast to dtype `arg`; imm.i64: 0 = non-strict
+                               (a value that does not fit -> null), 1 =
+                               overflowing (integers wrap)                   */
+    PLGPU_OP_XOR = 51,      /* Boolean xor (null if either is null); bitwise on ints */
+    PLGPU_OP_FILL_NULL = 52,/* [x, fill] -> x where valid, else fill         */
+    PLGPU_OP_IF_ELSE = 53,  /* [cond, then, otherwise] -> when(cond).then().otherwise();
+                               a null condition selects `otherwise`
+                               (polars-compute/src/if_then_else)             */
     /* comparisons: TotalOrd semantics, polars-utils/src/total_ord.rs:317-368
      * (NaN == NaN, NaN greatest); null in -> null out. */
     PLGPU_OP_EQ = 20,
@@ -99,7 +127,8 @@ enum plgpu_opcode {
     PLGPU_OP_GE = 25,
     PLGPU_OP_EQ_MISSING = 26, /* null == null, never null out */
     PLGPU_OP_NE_MISSING = 27,
-    /* boolean: Kleene logic, polars-compute/src/bitwise + ops::and/or */
+    /* boolean: Kleene logic, polars-compute/src/bitwise + ops::and/or;
+     * AND / OR / XOR of integers are bitwise */
     PLGPU_OP_AND = 30,
     PLGPU_OP_OR = 31,
     PLGPU_OP_NOT = 32,
@@ -205,6 +234,14 @@ int plgpu_column_alloc(int32_t dtype, int64_t length, int32_t with_validity, int
 int plgpu_ingest_chunk(plgpu_column* dst, int64_t dst_row, int64_t dst_byte, const void* values,
                        const uint8_t* validity, const uint8_t* str_data, int64_t src_offset, int64_t length,
                        void* stream);
+
+/* Result dtype of a program over columns of the given dtypes (only the
+ * columns' dtype fields are read; nothing runs on the device): the static
+ * typing of polars' type coercion (polars-plan/src/plans/conversion/
+ * type_coercion, polars-core/src/utils/supertype.rs) as the executor applies
+ * it. */
+int plgpu_expr_dtype(const plgpu_column* cols, int32_t ncols, const plgpu_instr* program, int32_t n_instr,
+                     int32_t* out_dtype);
 
 /* ------------------------------------------------------------ hot path */
 

@@ -17,6 +17,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "_build", "liboracle.so")
 
 BOOL, I32, I64, F64, U32 = 1, 2, 3, 4, 5
+I8, I16, U8, U16, U64, F32 = 7, 8, 9, 10, 11, 12
+_NP_OF = {I8: np.int8, I16: np.int16, I32: np.int32, I64: np.int64, U8: np.uint8, U16: np.uint16,
+          U32: np.uint32, U64: np.uint64, F32: np.float32, F64: np.float64}
 SUM_KAHAN, SUM_NAIVE, SUM_EXACT = 0, 1, 2
 AGG = dict(sum=1, mean=2, min=3, max=4, count=5, len=6, first=7, last=8)
 
@@ -77,14 +80,13 @@ def lib():
 
 
 def _np_dtype(code: int):
-    return {I32: np.int32, I64: np.int64, F64: np.float64, U32: np.uint32}[code]
+    return _NP_OF[code]
 
 
 def _code_of(a: np.ndarray) -> int:
     if a.dtype == np.bool_:
         return BOOL
-    return {np.dtype(np.int32): I32, np.dtype(np.int64): I64, np.dtype(np.float64): F64,
-            np.dtype(np.uint32): U32}[a.dtype]
+    return {np.dtype(t): c for c, t in _NP_OF.items()}[a.dtype]
 
 
 class HostCol:
@@ -144,16 +146,15 @@ def eval_program(cols: list[HostCol], program, nrows: int):
     validity = np.unpackbits(valid, bitorder="little")[:nrows].astype(bool)
     if dt == BOOL:
         v = np.unpackbits(vals, bitorder="little")[:nrows].astype(bool)
-    elif dt == I64:
-        v = vals[: nrows * 8].view(np.int64).copy()
     else:
-        v = vals[: nrows * 8].view(np.float64).copy()
+        t = np.dtype(_NP_OF[dt])
+        v = vals[: nrows * t.itemsize].view(t).copy()
     return dt, v, validity
 
 
 def filter_column(cols: list[HostCol], program, nrows: int, which: int):
     c = cols[which]
-    eb = 4 if c.code in (I32, U32) else 8
+    eb = np.dtype(_NP_OF[c.code]).itemsize
     out = np.zeros(max(nrows, 1) * eb, dtype=np.uint8)
     outv = np.zeros((nrows + 7) // 8 + 8, dtype=np.uint8)
     p, n = _prog(program)
@@ -175,10 +176,10 @@ def group_by_agg(key: HostCol, cols: list[HostCol], program, aggs: list[tuple[st
         code = cols[ci].code
         if kind in ("count", "len"):
             dt = np.uint32
-        elif kind == "mean" or code == F64:
-            dt = np.float64
+        elif kind == "mean" or code in (F64, F32):
+            dt = np.float64  # Float32 results are exact / rounded in f64; the caller rounds to f32
         else:
-            dt = np.int64
+            dt = np.int64    # integer results as int64 bits; the caller narrows to the output dtype
         outs.append(np.zeros(maxg, dt))
         outv.append(np.zeros(maxg, np.uint8))
     agg_arr = (_Agg * max(1, len(aggs)))()

@@ -34,26 +34,58 @@ static inline int col_valid(const plgpu_column* c, int64_t r) {
     return c->validity == NULL ? 1 : bit_get(c->validity, c->offset + r);
 }
 
-/* A typed scalar as seen by the expression interpreter. */
+/* A typed scalar as seen by the expression interpreter.
+ *   dt     the polars dtype (plgpu_dtype code), or one of the dynamic
+ *          literal kinds below (polars' UnknownKind::Int / Float / a bare
+ *          null), which take their type from the other operand;
+ *   i      signed ints and Boolean (value), unsigned ints (bits);
+ *   f      Float64, or a Float32 value widened (exactly) to double;
+ *   scalar a literal or an expression of literals: a length-1 column that
+ *          the reference broadcasts with the *_scalar kernels. */
+#define DYN_INT 100
+#define DYN_FLOAT 101
+#define DYN_NULL 102
 typedef struct {
-    int dt; /* PLGPU_BOOL / PLGPU_I64 / PLGPU_F64 */
+    int dt;
     int valid;
+    int scalar;
     int64_t i;
     double f;
 } val_t;
 
+static int is_signed(int dt) { return dt == PLGPU_I8 || dt == PLGPU_I16 || dt == PLGPU_I32 || dt == PLGPU_I64; }
+static int is_unsigned(int dt) { return dt == PLGPU_U8 || dt == PLGPU_U16 || dt == PLGPU_U32 || dt == PLGPU_U64; }
+static int is_intd(int dt) { return is_signed(dt) || is_unsigned(dt); }
+static int is_floatd(int dt) { return dt == PLGPU_F32 || dt == PLGPU_F64; }
+static int bits_of(int dt) {
+    switch (dt) {
+    case PLGPU_I8: case PLGPU_U8: return 8;
+    case PLGPU_I16: case PLGPU_U16: return 16;
+    case PLGPU_I32: case PLGPU_U32: case PLGPU_F32: return 32;
+    default: return 64;
+    }
+}
+
 static val_t col_get(const plgpu_column* c, int64_t r) {
     val_t v;
     v.valid = col_valid(c, r);
+    v.scalar = 0;
     v.i = 0;
     v.f = 0.0;
+    v.dt = c->dtype;
     int64_t p = c->offset + r;
     switch (c->dtype) {
-    case PLGPU_BOOL: v.dt = PLGPU_BOOL; v.i = bit_get((const uint8_t*)c->values, p); break;
-    case PLGPU_I32: v.dt = PLGPU_I64; v.i = ((const int32_t*)c->values)[p]; break;
-    case PLGPU_U32: v.dt = PLGPU_I64; v.i = ((const uint32_t*)c->values)[p]; break;
-    case PLGPU_I64: v.dt = PLGPU_I64; v.i = ((const int64_t*)c->values)[p]; break;
-    default: v.dt = PLGPU_F64; v.f = ((const double*)c->values)[p]; break;
+    case PLGPU_BOOL: v.i = bit_get((const uint8_t*)c->values, p); break;
+    case PLGPU_I8: v.i = ((const int8_t*)c->values)[p]; break;
+    case PLGPU_I16: v.i = ((const int16_t*)c->values)[p]; break;
+    case PLGPU_I32: v.i = ((const int32_t*)c->values)[p]; break;
+    case PLGPU_I64: v.i = ((const int64_t*)c->values)[p]; break;
+    case PLGPU_U8: v.i = ((const uint8_t*)c->values)[p]; break;
+    case PLGPU_U16: v.i = ((const uint16_t*)c->values)[p]; break;
+    case PLGPU_U32: v.i = ((const uint32_t*)c->values)[p]; break;
+    case PLGPU_U64: v.i = (int64_t)((const uint64_t*)c->values)[p]; break;
+    case PLGPU_F32: v.f = ((const float*)c->values)[p]; break;
+    default: v.f = ((const double*)c->values)[p]; break;
     }
     return v;
 }
@@ -85,6 +117,239 @@ static int i_cmp(int op, int64_t a, int64_t b) {
     }
     return 0;
 }
+static int u_cmp(int op, uint64_t a, uint64_t b) {
+    switch (op) {
+    case PLGPU_OP_EQ: return a == b;
+    case PLGPU_OP_NE: return a != b;
+    case PLGPU_OP_LT: return a < b;
+    case PLGPU_OP_LE: return a <= b;
+    case PLGPU_OP_GT: return a > b;
+    case PLGPU_OP_GE: return a >= b;
+    }
+    return 0;
+}
+
+/* polars-core/src/utils/supertype.rs:146 get_supertype, the primitive
+ * numeric / Boolean rows (0 = no supertype). */
+static int supertype(int l, int r) {
+    if (l == r) return l;
+    if (l == PLGPU_BOOL) return (is_intd(r) || is_floatd(r)) ? r : 0;  /* (Int8, Boolean) => Int8, ... */
+    if (r == PLGPU_BOOL) return (is_intd(l) || is_floatd(l)) ? l : 0;
+    if (is_floatd(l) && is_floatd(r)) return PLGPU_F64;                /* (Float32, Float64) => Float64 */
+    if (is_floatd(l) || is_floatd(r)) {
+        int fl = is_floatd(l) ? l : r, in = is_floatd(l) ? r : l;
+        if (fl == PLGPU_F64) return PLGPU_F64;
+        return bits_of(in) <= 16 ? PLGPU_F32 : PLGPU_F64;                 /* (Int16, Float32) => Float32,
+                                                                           (Int32, Float32) => Float64 */
+    }
+    if (is_signed(l) == is_signed(r)) return bits_of(l) >= bits_of(r) ? l : r;
+    int s = is_signed(l) ? l : r, u = is_signed(l) ? r : l;
+    if (u == PLGPU_U64) return PLGPU_F64;                                /* (Int64, UInt64) => Float64 */
+    if (bits_of(u) < bits_of(s)) return s;                                /* (Int16, UInt8) => Int16 */
+    return bits_of(u) == 8 ? PLGPU_I16 : bits_of(u) == 16 ? PLGPU_I32 : PLGPU_I64; /* (Int8, UInt8) => Int16 */
+}
+
+/* supertype.rs:463: a dynamic int v next to dtype dt: the smallest dtype
+ * holding v (materialize_dyn_int_pos for an unsigned dt and v >= 0), then
+ * the supertype; UInt64 with a signed literal stays integral (Int64). */
+static int smallest_fit(int64_t v, int unsigned_ok) {
+    if (unsigned_ok && v >= 0) {
+        if (v <= 0xFF) return PLGPU_U8;
+        if (v <= 0xFFFF) return PLGPU_U16;
+        if (v <= 0xFFFFFFFFll) return PLGPU_U32;
+        return PLGPU_U64;
+    }
+    if (v >= INT8_MIN && v <= INT8_MAX) return PLGPU_I8;
+    if (v >= INT16_MIN && v <= INT16_MAX) return PLGPU_I16;
+    if (v >= INT32_MIN && v <= INT32_MAX) return PLGPU_I32;
+    return PLGPU_I64;
+}
+static int dyn_join(const val_t* lit, int dt) {
+    if (lit->dt == DYN_NULL) return dt;
+    if (is_floatd(dt)) return dt;                      /* materialize to the float dtype */
+    if (lit->dt == DYN_FLOAT) return PLGPU_F64;        /* UnknownKind::Float with an integer */
+    if (dt == PLGPU_BOOL) return supertype(PLGPU_BOOL, smallest_fit(lit->i, 0));
+    int sm = smallest_fit(lit->i, is_unsigned(dt));
+    if (dt == PLGPU_U64 && is_signed(sm)) return PLGPU_I64;
+    return supertype(dt, sm);
+}
+/* A literal on its own materializes as Int32 / Int64 / Float64. */
+static int dyn_alone(const val_t* v) {
+    if (v->dt == DYN_INT) return (v->i >= INT32_MIN && v->i <= INT32_MAX) ? PLGPU_I32 : PLGPU_I64;
+    if (v->dt == DYN_FLOAT) return PLGPU_F64;
+    if (v->dt == DYN_NULL) return PLGPU_BOOL;
+    return v->dt;
+}
+static int is_dyn(const val_t* v) { return v->dt == DYN_INT || v->dt == DYN_FLOAT || v->dt == DYN_NULL; }
+static int join_types(const val_t* a, const val_t* b) {
+    if (is_dyn(a) && is_dyn(b)) {
+        if (a->dt == DYN_NULL) return dyn_alone(b);
+        if (b->dt == DYN_NULL) return dyn_alone(a);
+        if (a->dt == DYN_FLOAT || b->dt == DYN_FLOAT) return PLGPU_F64;
+        return supertype(dyn_alone(a), dyn_alone(b));
+    }
+    if (is_dyn(a)) return dyn_join(a, b->dt);
+    if (is_dyn(b)) return dyn_join(b, a->dt);
+    return supertype(a->dt, b->dt);
+}
+
+/* Two's complement wrap of an integer to dtype dt (Rust `as` / wrapping_*). */
+static int64_t wrap_int(int dt, uint64_t x) {
+    switch (dt) {
+    case PLGPU_I8: return (int8_t)x;
+    case PLGPU_I16: return (int16_t)x;
+    case PLGPU_I32: return (int32_t)x;
+    case PLGPU_U8: return (uint8_t)x;
+    case PLGPU_U16: return (uint16_t)x;
+    case PLGPU_U32: return (uint32_t)x;
+    default: return (int64_t)x;
+    }
+}
+
+/* Non-strict cast (polars-core/src/chunked_array/cast.rs: a value that does
+ * not fit the target is null; `overflowing` wraps integers).  Float -> int
+ * truncates (num_traits::NumCast), int -> float rounds to nearest. */
+static val_t cast_to(val_t v, int to, int overflowing) {
+    val_t z = v;
+    z.dt = to;
+    if (!v.valid) { z.i = 0; z.f = 0; return z; }
+    if (v.dt == DYN_INT) v.dt = PLGPU_I64;
+    if (v.dt == DYN_FLOAT) v.dt = PLGPU_F64;
+    if (to == PLGPU_BOOL) { z.i = is_floatd(v.dt) ? v.f != 0.0 : v.i != 0; return z; }
+    if (v.dt == PLGPU_BOOL) { if (is_floatd(to)) z.f = (double)v.i; else z.i = v.i; return z; }
+    if (is_intd(v.dt) && is_intd(to)) {
+        /* exact value of the source: signed / unsigned 64-bit */
+        int neg = is_signed(v.dt) && v.i < 0;
+        uint64_t mag = (uint64_t)v.i;
+        int fits;
+        if (is_unsigned(to)) {
+            fits = !neg && (to == PLGPU_U64 || mag <= (((uint64_t)1 << bits_of(to)) - 1));
+        } else {
+            int64_t lo = to == PLGPU_I64 ? INT64_MIN : -((int64_t)1 << (bits_of(to) - 1));
+            int64_t hi = to == PLGPU_I64 ? INT64_MAX : ((int64_t)1 << (bits_of(to) - 1)) - 1;
+            if (v.dt == PLGPU_U64) fits = mag <= (uint64_t)hi;
+            else fits = v.i >= lo && v.i <= hi;
+        }
+        if (fits) z.i = v.i;
+        else if (overflowing) z.i = wrap_int(to, (uint64_t)v.i);
+        else { z.valid = 0; z.i = 0; }
+        return z;
+    }
+    if (is_intd(v.dt) && is_floatd(to)) {
+        if (to == PLGPU_F32) z.f = v.dt == PLGPU_U64 ? (double)(float)(uint64_t)v.i : (double)(float)v.i;
+        else z.f = v.dt == PLGPU_U64 ? (double)(uint64_t)v.i : (double)v.i;
+        return z;
+    }
+    if (is_floatd(v.dt) && is_floatd(to)) { z.f = to == PLGPU_F32 ? (double)(float)v.f : v.f; return z; }
+    /* float -> int */
+    double t = trunc(v.f);
+    int ok;
+    if (isnan(t)) ok = 0;
+    else if (to == PLGPU_U64) ok = t >= 0.0 && t < 18446744073709551616.0;
+    else if (to == PLGPU_I64) ok = t >= -9223372036854775808.0 && t < 9223372036854775808.0;
+    else if (is_unsigned(to)) ok = t >= 0.0 && t <= (double)((((uint64_t)1) << bits_of(to)) - 1);
+    else ok = t >= -(double)((int64_t)1 << (bits_of(to) - 1)) && t <= (double)(((int64_t)1 << (bits_of(to) - 1)) - 1);
+    if (!ok) { z.valid = 0; z.i = 0; return z; }
+    z.i = to == PLGPU_U64 ? (int64_t)(uint64_t)t : (int64_t)t;
+    return z;
+}
+
+/* Give an operand the type t (literal materialization or a cast). */
+static val_t coerce(val_t v, int t) {
+    if (v.dt == DYN_NULL) { v.dt = t; v.i = 0; v.f = 0; return v; }
+    if (v.dt == DYN_INT) {
+        v.dt = t;
+        if (is_floatd(t)) v.f = t == PLGPU_F32 ? (double)(float)v.i : (double)v.i;
+        return v;
+    }
+    if (v.dt == DYN_FLOAT) {
+        v.dt = t;
+        if (t == PLGPU_F32) v.f = (double)(float)v.f;
+        return v;
+    }
+    if (v.dt == t) return v;
+    int s = v.scalar;
+    v = cast_to(v, t, 0);
+    v.scalar = s;
+    return v;
+}
+
+/* polars-utils/src/floor_divmod.rs:39 (signed) and :28 (unsigned). */
+static void int_floor_divmod(int dt, int64_t a, int64_t b, int64_t* q, int64_t* m) {
+    if (dt == PLGPU_U64) {
+        *q = (int64_t)((uint64_t)a / (uint64_t)b);
+        *m = (int64_t)((uint64_t)a % (uint64_t)b);
+        return;
+    }
+    if (a == INT64_MIN && b == -1) { *q = INT64_MIN; *m = 0; return; }  /* wrapping_div */
+    int64_t d = a / b, r = a % b;
+    if (r != 0 && ((a < 0) != (b < 0))) { d -= 1; r += b; }
+    *q = d;
+    *m = r;
+}
+
+/* One arithmetic op on two operands of type t.  Integer ops wrap at t's
+ * width (polars-compute/src/arithmetic/{signed,unsigned}.rs wrapping_*); a
+ * zero divisor gives null (:35, :60); Float32 runs in single precision;
+ * a broadcast (scalar) divisor uses the reciprocal forms of
+ * arithmetic/float.rs:78-98 and :113 (true_div_scalar: x * (1 / rhs)). */
+static val_t arith(int op, val_t a, val_t b, int t) {
+    val_t z;
+    memset(&z, 0, sizeof z);
+    z.dt = t;
+    z.scalar = a.scalar && b.scalar;
+    z.valid = a.valid && b.valid;
+    const int bscalar = b.scalar && !a.scalar;
+    if (is_intd(t)) {
+        uint64_t x = (uint64_t)a.i, y = (uint64_t)b.i;
+        switch (op) {
+        case PLGPU_OP_ADD: z.i = wrap_int(t, x + y); break;
+        case PLGPU_OP_SUB: z.i = wrap_int(t, x - y); break;
+        case PLGPU_OP_MUL: z.i = wrap_int(t, x * y); break;
+        default: {  /* FLOORDIV / DIVIDE (legacy_div = floor div for ints) / MOD */
+            if (b.i == 0) { z.valid = 0; break; }
+            int64_t q, m;
+            int_floor_divmod(t, a.i, b.i, &q, &m);
+            z.i = wrap_int(t, (uint64_t)(op == PLGPU_OP_MOD ? m : q));
+        }
+        }
+        if (!z.valid) z.i = 0;
+        return z;
+    }
+    if (t == PLGPU_F32) {
+        float x = (float)a.f, y = (float)b.f, r;
+        switch (op) {
+        case PLGPU_OP_ADD: r = x + y; break;
+        case PLGPU_OP_SUB: r = x - y; break;
+        case PLGPU_OP_MUL: r = x * y; break;
+        case PLGPU_OP_FLOORDIV: r = bscalar ? floorf(x * (1.0f / y)) : floorf(x / y); break;
+        case PLGPU_OP_MOD: {
+            float q = bscalar ? floorf(x * (1.0f / y)) : floorf(x / y);
+            float yq = y * q;
+            r = x - yq;
+            break;
+        }
+        default: r = bscalar ? x * (1.0f / y) : x / y; break;  /* TRUEDIV / DIVIDE */
+        }
+        z.f = r;
+        return z;
+    }
+    double x = a.f, y = b.f;
+    switch (op) {
+    case PLGPU_OP_ADD: z.f = x + y; break;
+    case PLGPU_OP_SUB: z.f = x - y; break;
+    case PLGPU_OP_MUL: z.f = x * y; break;
+    case PLGPU_OP_FLOORDIV: z.f = bscalar ? floor(x * (1.0 / y)) : floor(x / y); break;
+    case PLGPU_OP_MOD: {
+        double q = bscalar ? floor(x * (1.0 / y)) : floor(x / y);
+        double yq = y * q;
+        z.f = x - yq;
+        break;
+    }
+    default: z.f = bscalar ? x * (1.0 / y) : x / y; break;
+    }
+    return z;
+}
 
 /* One postfix program, one row.  Returns 0 on success, -1 on type error. */
 static int eval_row(const plgpu_column* cols, const plgpu_instr* prog, int n, int64_t r, val_t* out) {
@@ -92,62 +357,83 @@ static int eval_row(const plgpu_column* cols, const plgpu_instr* prog, int n, in
     int sp = 0;
     for (int k = 0; k < n; ++k) {
         const plgpu_instr* in = &prog[k];
-        val_t a, b, z;
+        val_t a, b, c, z;
         memset(&z, 0, sizeof z);
+        if (sp >= PLGPU_MAX_STACK && (in->op <= PLGPU_OP_LIT_NULL)) return -1;
         switch (in->op) {
         case PLGPU_OP_COL: st[sp++] = col_get(&cols[in->arg], r); break;
-        case PLGPU_OP_LIT_F64: z.dt = PLGPU_F64; z.valid = 1; z.f = in->imm.f64; st[sp++] = z; break;
-        case PLGPU_OP_LIT_I64: z.dt = PLGPU_I64; z.valid = 1; z.i = in->imm.i64; st[sp++] = z; break;
-        case PLGPU_OP_LIT_BOOL: z.dt = PLGPU_BOOL; z.valid = 1; z.i = in->imm.i64 != 0; st[sp++] = z; break;
+        case PLGPU_OP_LIT_F64: z.dt = DYN_FLOAT; z.valid = 1; z.scalar = 1; z.f = in->imm.f64; st[sp++] = z; break;
+        case PLGPU_OP_LIT_I64: z.dt = DYN_INT; z.valid = 1; z.scalar = 1; z.i = in->imm.i64; st[sp++] = z; break;
+        case PLGPU_OP_LIT_BOOL: z.dt = PLGPU_BOOL; z.valid = 1; z.scalar = 1; z.i = in->imm.i64 != 0; st[sp++] = z; break;
         case PLGPU_OP_LIT_NULL:
-            z.dt = in->arg == PLGPU_F64 ? PLGPU_F64 : (in->arg == PLGPU_BOOL ? PLGPU_BOOL : PLGPU_I64);
+            z.dt = in->arg ? in->arg : DYN_NULL;
             z.valid = 0;
+            z.scalar = 1;
             st[sp++] = z;
             break;
-        case PLGPU_OP_ADD: case PLGPU_OP_SUB: case PLGPU_OP_MUL: case PLGPU_OP_TRUEDIV: {
+        case PLGPU_OP_ADD: case PLGPU_OP_SUB: case PLGPU_OP_MUL: case PLGPU_OP_TRUEDIV:
+        case PLGPU_OP_FLOORDIV: case PLGPU_OP_MOD: case PLGPU_OP_DIVIDE: {
+            if (sp < 2) return -1;
             b = st[--sp]; a = st[--sp];
             if (a.dt == PLGPU_BOOL || b.dt == PLGPU_BOOL) return -1;
-            z.valid = a.valid && b.valid;
-            /* supertype: i64 (op) i64 -> i64 except true division -> f64
-             * (polars-plan/src/plans/aexpr/schema.rs get_arithmetic_field);
-             * integer ops wrap (polars-compute/src/arithmetic/signed.rs). */
-            if (a.dt == PLGPU_I64 && b.dt == PLGPU_I64 && in->op != PLGPU_OP_TRUEDIV) {
-                uint64_t x = (uint64_t)a.i, y = (uint64_t)b.i;
-                z.dt = PLGPU_I64;
-                z.i = (int64_t)(in->op == PLGPU_OP_ADD ? x + y : in->op == PLGPU_OP_SUB ? x - y : x * y);
-            } else {
-                double x = a.dt == PLGPU_F64 ? a.f : (double)a.i;
-                double y = b.dt == PLGPU_F64 ? b.f : (double)b.i;
-                z.dt = PLGPU_F64;
-                z.f = in->op == PLGPU_OP_ADD ? x + y : in->op == PLGPU_OP_SUB ? x - y
-                    : in->op == PLGPU_OP_MUL ? x * y : x / y;
-            }
-            st[sp++] = z;
+            int t = join_types(&a, &b);
+            if (!t) return -1;
+            if (t == PLGPU_BOOL) t = PLGPU_I32;
+            /* TrueDivide: integers are cast to Float64 first
+             * (polars-expr/src/expressions/binary.rs:73 apply_operator) */
+            if (in->op == PLGPU_OP_TRUEDIV && !is_floatd(t)) t = PLGPU_F64;
+            a = coerce(a, t);
+            b = coerce(b, t);
+            st[sp++] = arith(in->op, a, b, t);
             break;
         }
         case PLGPU_OP_NEG: case PLGPU_OP_ABS:
+            if (sp < 1) return -1;
             a = st[--sp];
             if (a.dt == PLGPU_BOOL) return -1;
-            if (a.dt == PLGPU_I64) {
-                uint64_t x = (uint64_t)a.i;
-                a.i = in->op == PLGPU_OP_NEG ? (int64_t)(0 - x) : (a.i < 0 ? (int64_t)(0 - x) : a.i);
-            } else {
+            if (a.dt == DYN_INT) {
+                a.i = in->op == PLGPU_OP_NEG ? (int64_t)(0 - (uint64_t)a.i)
+                                             : (a.i < 0 ? (int64_t)(0 - (uint64_t)a.i) : a.i);
+            } else if (a.dt == DYN_FLOAT || is_floatd(a.dt)) {
                 a.f = in->op == PLGPU_OP_NEG ? -a.f : fabs(a.f);
+            } else {
+                if (a.dt == DYN_NULL) a.dt = PLGPU_I32;
+                if (in->op == PLGPU_OP_NEG && is_unsigned(a.dt)) return -1;  /* `neg` not supported for u8.. */
+                uint64_t x = (uint64_t)a.i;
+                int64_t v = in->op == PLGPU_OP_NEG ? (int64_t)(0 - x) : (a.i < 0 ? (int64_t)(0 - x) : a.i);
+                a.i = wrap_int(a.dt, (uint64_t)v);  /* wrapping_neg / wrapping_abs at the width */
+                if (!a.valid) a.i = 0;
             }
             st[sp++] = a;
             break;
         case PLGPU_OP_CAST_F64:
+        case PLGPU_OP_CAST: {
+            if (sp < 1) return -1;
             a = st[--sp];
-            if (a.dt != PLGPU_F64) { a.f = (double)a.i; a.dt = PLGPU_F64; }
+            int to = in->op == PLGPU_OP_CAST_F64 ? PLGPU_F64 : in->arg;
+            if (is_dyn(&a)) a = coerce(a, a.dt == DYN_NULL ? to : dyn_alone(&a));
+            int s = a.scalar;
+            a = cast_to(a, to, in->op == PLGPU_OP_CAST && (in->imm.i64 & 1));
+            a.scalar = s;
             st[sp++] = a;
             break;
+        }
         case PLGPU_OP_EQ: case PLGPU_OP_NE: case PLGPU_OP_LT: case PLGPU_OP_LE:
         case PLGPU_OP_GT: case PLGPU_OP_GE: case PLGPU_OP_EQ_MISSING: case PLGPU_OP_NE_MISSING: {
+            if (sp < 2) return -1;
             b = st[--sp]; a = st[--sp];
             int missing = in->op == PLGPU_OP_EQ_MISSING || in->op == PLGPU_OP_NE_MISSING;
             int op = in->op == PLGPU_OP_EQ_MISSING ? PLGPU_OP_EQ
                    : in->op == PLGPU_OP_NE_MISSING ? PLGPU_OP_NE : in->op;
+            if ((a.dt == PLGPU_BOOL) != (b.dt == PLGPU_BOOL) && !is_dyn(&a) && !is_dyn(&b)) return -1;
+            int t = join_types(&a, &b);
+            if (!t) return -1;
+            if (a.dt == PLGPU_BOOL || b.dt == PLGPU_BOOL) t = PLGPU_BOOL;
+            if (t == PLGPU_BOOL && op != PLGPU_OP_EQ && op != PLGPU_OP_NE) return -1;
+            a = coerce(a, t);
+            b = coerce(b, t);
             z.dt = PLGPU_BOOL;
+            z.scalar = a.scalar && b.scalar;
             if (!(a.valid && b.valid)) {
                 if (missing) {
                     /* null == null; null != value (polars eq_missing) */
@@ -159,52 +445,99 @@ static int eval_row(const plgpu_column* cols, const plgpu_instr* prog, int n, in
                 }
             } else {
                 z.valid = 1;
-                if (a.dt == PLGPU_F64 || b.dt == PLGPU_F64) {
-                    double x = a.dt == PLGPU_F64 ? a.f : (double)a.i;
-                    double y = b.dt == PLGPU_F64 ? b.f : (double)b.i;
-                    z.i = f_cmp(op, x, y);
-                } else {
-                    z.i = i_cmp(op, a.i, b.i);
-                }
+                if (is_floatd(t)) z.i = f_cmp(op, a.f, b.f);
+                else if (t == PLGPU_U64) z.i = u_cmp(op, (uint64_t)a.i, (uint64_t)b.i);
+                else z.i = i_cmp(op, a.i, b.i);
             }
             st[sp++] = z;
             break;
         }
-        case PLGPU_OP_AND: case PLGPU_OP_OR: {
-            /* Kleene logic (polars-arrow/src/compute/boolean_kleene.rs). */
+        case PLGPU_OP_AND: case PLGPU_OP_OR: case PLGPU_OP_XOR: {
+            if (sp < 2) return -1;
             b = st[--sp]; a = st[--sp];
-            if (a.dt != PLGPU_BOOL || b.dt != PLGPU_BOOL) return -1;
-            z.dt = PLGPU_BOOL;
-            if (in->op == PLGPU_OP_AND) {
-                if ((a.valid && !a.i) || (b.valid && !b.i)) { z.valid = 1; z.i = 0; }
-                else if (a.valid && b.valid) { z.valid = 1; z.i = 1; }
-                else z.valid = 0;
+            int ba = a.dt == PLGPU_BOOL || a.dt == DYN_NULL, bb = b.dt == PLGPU_BOOL || b.dt == DYN_NULL;
+            z.scalar = a.scalar && b.scalar;
+            if (ba && bb) {
+                z.dt = PLGPU_BOOL;
+                if (in->op == PLGPU_OP_XOR) {
+                    /* BooleanArray ^ (bitxor): null if either is null */
+                    z.valid = a.valid && b.valid;
+                    z.i = z.valid ? (a.i ^ b.i) : 0;
+                } else if (in->op == PLGPU_OP_AND) {
+                    /* Kleene logic (polars-arrow/src/compute/boolean_kleene.rs). */
+                    if ((a.valid && !a.i) || (b.valid && !b.i)) { z.valid = 1; z.i = 0; }
+                    else if (a.valid && b.valid) { z.valid = 1; z.i = 1; }
+                    else z.valid = 0;
+                } else {
+                    if ((a.valid && a.i) || (b.valid && b.i)) { z.valid = 1; z.i = 1; }
+                    else if (a.valid && b.valid) { z.valid = 1; z.i = 0; }
+                    else z.valid = 0;
+                }
             } else {
-                if ((a.valid && a.i) || (b.valid && b.i)) { z.valid = 1; z.i = 1; }
-                else if (a.valid && b.valid) { z.valid = 1; z.i = 0; }
-                else z.valid = 0;
+                /* integers: bitand / bitor / bitxor of the supertype */
+                int t = join_types(&a, &b);
+                if (!t || !is_intd(t)) return -1;
+                a = coerce(a, t);
+                b = coerce(b, t);
+                z.dt = t;
+                z.valid = a.valid && b.valid;
+                uint64_t x = (uint64_t)a.i, y = (uint64_t)b.i;
+                z.i = z.valid ? wrap_int(t, in->op == PLGPU_OP_AND ? x & y : in->op == PLGPU_OP_OR ? x | y : x ^ y) : 0;
             }
+            st[sp++] = z;
+            break;
+        }
+        case PLGPU_OP_FILL_NULL: {
+            /* FunctionExpr::FillNull: coalesce(x, fill) in the supertype */
+            if (sp < 2) return -1;
+            b = st[--sp]; a = st[--sp];
+            int t = join_types(&a, &b);
+            if (!t) return -1;
+            a = coerce(a, t);
+            b = coerce(b, t);
+            z = a.valid ? a : b;
+            z.scalar = a.scalar && b.scalar;
+            st[sp++] = z;
+            break;
+        }
+        case PLGPU_OP_IF_ELSE: {
+            /* when(c).then(a).otherwise(b): a null condition selects b
+             * (polars-core zip_with / if_then_else: mask nulls are false) */
+            if (sp < 3) return -1;
+            b = st[--sp]; a = st[--sp]; c = st[--sp];
+            if (c.dt != PLGPU_BOOL && c.dt != DYN_NULL) return -1;
+            int t = join_types(&a, &b);
+            if (!t) return -1;
+            a = coerce(a, t);
+            b = coerce(b, t);
+            z = (c.valid && c.i) ? a : b;
+            z.scalar = c.scalar && a.scalar && b.scalar;
             st[sp++] = z;
             break;
         }
         case PLGPU_OP_NOT:
+            if (sp < 1) return -1;
             a = st[--sp];
-            if (a.dt != PLGPU_BOOL) return -1;
-            a.i = !a.i;
+            if (a.dt == DYN_NULL) a.dt = PLGPU_BOOL;
+            if (a.dt == PLGPU_BOOL) a.i = a.valid ? !a.i : 0;
+            else if (is_intd(a.dt)) a.i = a.valid ? wrap_int(a.dt, ~(uint64_t)a.i) : 0;  /* bitwise not */
+            else return -1;
             st[sp++] = a;
             break;
         case PLGPU_OP_IS_NULL: case PLGPU_OP_IS_NOT_NULL:
+            if (sp < 1) return -1;
             a = st[--sp];
-            z.dt = PLGPU_BOOL; z.valid = 1;
+            z.dt = PLGPU_BOOL; z.valid = 1; z.scalar = a.scalar;
             z.i = in->op == PLGPU_OP_IS_NULL ? !a.valid : a.valid;
             st[sp++] = z;
             break;
         case PLGPU_OP_IS_NAN: case PLGPU_OP_IS_FINITE:
+            if (sp < 1) return -1;
             a = st[--sp];
-            if (a.dt == PLGPU_BOOL) return -1;
-            z.dt = PLGPU_BOOL; z.valid = a.valid;
-            if (a.dt == PLGPU_F64) z.i = in->op == PLGPU_OP_IS_NAN ? isnan(a.f) : isfinite(a.f);
-            else z.i = in->op == PLGPU_OP_IS_NAN ? 0 : 1;
+            if (a.dt == DYN_FLOAT) a.dt = PLGPU_F64;
+            if (!is_floatd(a.dt)) return -1;
+            z.dt = PLGPU_BOOL; z.valid = a.valid; z.scalar = a.scalar;
+            z.i = a.valid ? (in->op == PLGPU_OP_IS_NAN ? isnan(a.f) : isfinite(a.f)) : 0;
             st[sp++] = z;
             break;
         default:
@@ -212,13 +545,14 @@ static int eval_row(const plgpu_column* cols, const plgpu_instr* prog, int n, in
         }
     }
     if (sp != 1) return -1;
+    if (is_dyn(&st[0])) st[0] = coerce(st[0], dyn_alone(&st[0]));
     *out = st[0];
     return 0;
 }
 
 /* Evaluate a program for all rows.  out_values: BOOL -> bit-packed bytes,
- * I64 -> int64, F64 -> double; out_validity bit-packed (always written).
- * Returns the output dtype or -1. */
+ * otherwise the result dtype's own width (Float32 as float);
+ * out_validity bit-packed (always written).  Returns the output dtype or -1. */
 OR_EXPORT int or_eval(const plgpu_column* cols, int32_t ncols, const plgpu_instr* prog, int32_t n,
                       int64_t nrows, void* out_values, uint8_t* out_validity) {
     (void)ncols;
@@ -228,9 +562,15 @@ OR_EXPORT int or_eval(const plgpu_column* cols, int32_t ncols, const plgpu_instr
         if (eval_row(cols, prog, n, r, &v) != 0) return -1;
         dt = v.dt;
         bit_set(out_validity, r, v.valid);
-        if (v.dt == PLGPU_BOOL) bit_set((uint8_t*)out_values, r, v.valid ? (int)v.i : 0);
-        else if (v.dt == PLGPU_I64) ((int64_t*)out_values)[r] = v.valid ? v.i : 0;
-        else ((double*)out_values)[r] = v.valid ? v.f : 0.0;
+        switch (v.dt) {
+        case PLGPU_BOOL: bit_set((uint8_t*)out_values, r, v.valid ? (int)v.i : 0); break;
+        case PLGPU_I8: case PLGPU_U8: ((uint8_t*)out_values)[r] = (uint8_t)(v.valid ? v.i : 0); break;
+        case PLGPU_I16: case PLGPU_U16: ((uint16_t*)out_values)[r] = (uint16_t)(v.valid ? v.i : 0); break;
+        case PLGPU_I32: case PLGPU_U32: ((uint32_t*)out_values)[r] = (uint32_t)(v.valid ? v.i : 0); break;
+        case PLGPU_I64: case PLGPU_U64: ((int64_t*)out_values)[r] = v.valid ? v.i : 0; break;
+        case PLGPU_F32: ((float*)out_values)[r] = v.valid ? (float)v.f : 0.0f; break;
+        default: ((double*)out_values)[r] = v.valid ? v.f : 0.0; break;
+        }
     }
     return dt;
 }
@@ -245,13 +585,13 @@ static int eval_mask(const plgpu_column* cols, const plgpu_instr* prog, int n, i
 
 /* Filter one fixed-width column by a program-derived mask; stable order
  * (polars-compute/src/filter/primitive.rs filter_values_and_validity).
- * elem_bytes: 4 or 8; BOOL columns are not supported by this helper.
+ * any fixed-width column; BOOL columns are not supported by this helper.
  * Returns the number of selected rows. */
 OR_EXPORT int64_t or_filter(const plgpu_column* cols, int32_t ncols, const plgpu_instr* prog, int32_t n,
                             int64_t nrows, int32_t which, void* out_values, uint8_t* out_validity) {
     (void)ncols;
     const plgpu_column* c = &cols[which];
-    int eb = (c->dtype == PLGPU_I32 || c->dtype == PLGPU_U32) ? 4 : 8;
+    int eb = bits_of(c->dtype) / 8;
     int64_t o = 0;
     for (int64_t r = 0; r < nrows; ++r) {
         if (!eval_mask(cols, prog, n, r)) continue;
@@ -498,7 +838,8 @@ OR_EXPORT int64_t or_group_by_agg(const plgpu_column* key, const plgpu_column* c
         int64_t len = g.start[gi + 1] - g.start[gi];
         for (int a = 0; a < naggs; ++a) {
             const plgpu_column* c = &cols[aggs[a].col];
-            int isf = c->dtype == PLGPU_F64;
+            int isf = c->dtype == PLGPU_F64 || c->dtype == PLGPU_F32;  /* Float32 widened exactly */
+            int isu64 = c->dtype == PLGPU_U64;
             uint8_t valid = 1;
             switch (aggs[a].kind) {
             case PLGPU_AGG_LEN: ((uint32_t*)out_vals[a])[gi] = (uint32_t)len; break;
@@ -536,7 +877,7 @@ OR_EXPORT int64_t or_group_by_agg(const plgpu_column* key, const plgpu_column* c
                         val_t v = col_get(c, rows[i]);
                         if (!v.valid) continue;
                         ++nv;
-                        double x = (double)v.i;
+                        double x = isu64 ? (double)(uint64_t)v.i : (double)v.i;
                         if (sum_mode == 2) fsum_add(&fs, x);
                         else { double y = x - ke; double t = ks + y; ke = (t - ks) - y; ks = t; }
                     }
@@ -565,7 +906,9 @@ OR_EXPORT int64_t or_group_by_agg(const plgpu_column* key, const plgpu_column* c
                         else if (is_min ? (v.f < bf || (v.f == bf && signbit(v.f))) : (v.f > bf || (v.f == bf && !signbit(v.f)))) bf = v.f;
                         any_num = 1;
                     } else {
-                        if (!any_num || (is_min ? v.i < bi : v.i > bi)) bi = v.i;
+                        int less = isu64 ? (uint64_t)v.i < (uint64_t)bi : v.i < bi;
+                        int more = isu64 ? (uint64_t)v.i > (uint64_t)bi : v.i > bi;
+                        if (!any_num || (is_min ? less : more)) bi = v.i;
                         any_num = 1;
                     }
                 }
@@ -724,14 +1067,7 @@ static int jn_cmp(const void* a, const void* b) {
     return x->row < y->row ? -1 : (x->row > y->row ? 1 : 0);
 }
 
-static int64_t col_int(const plgpu_column* c, int64_t r) {
-    const int64_t p = c->offset + r;
-    switch (c->dtype) {
-    case PLGPU_I32: return ((const int32_t*)c->values)[p];
-    case PLGPU_U32: return ((const uint32_t*)c->values)[p];
-    default: return ((const int64_t*)c->values)[p];
-    }
-}
+static int64_t col_int(const plgpu_column* c, int64_t r) { return col_get(c, r).i; }  /* UInt64 as its bits */
 
 /* Returns the number of pairs (or -1 if more than cap). */
 OR_EXPORT int64_t or_join_inner(const plgpu_column* lk, const plgpu_column* rk, int32_t nulls_equal, int64_t cap,
@@ -872,14 +1208,14 @@ static srt_ctx g_srt;
 
 static int srt_cmp_val(int64_t a, int64_t b) {
     const plgpu_column* c = g_srt.c;
-    if (c->dtype == PLGPU_F64) {
-        const double x = ((const double*)c->values)[c->offset + a];
-        const double y = ((const double*)c->values)[c->offset + b];
+    if (c->dtype == PLGPU_F64 || c->dtype == PLGPU_F32) {
+        const double x = col_get(c, a).f, y = col_get(c, b).f;
         const int xn = isnan(x), yn = isnan(y);
         if (xn || yn) return xn == yn ? 0 : (xn ? 1 : -1);
         return x < y ? -1 : (x > y ? 1 : 0); /* -0.0 == 0.0 */
     }
     const int64_t x = col_int(c, a), y = col_int(c, b);
+    if (c->dtype == PLGPU_U64) return (uint64_t)x < (uint64_t)y ? -1 : ((uint64_t)x > (uint64_t)y ? 1 : 0);
     return x < y ? -1 : (x > y ? 1 : 0);
 }
 

@@ -23,28 +23,38 @@ from ._native import (
     ShapeError,
     device_count,
 )
-from .expr import Expr, col, count, first, last, len, lit, max, mean, min, sum
+from .expr import Expr, col, count, first, last, len, lit, max, mean, min, sum, when
 from .frame import (
     Boolean,
     DataFrame,
     DataType,
+    Date,
+    Datetime,
+    Duration,
+    Float32,
     Float64,
     GroupBy,
+    Int8,
+    Int16,
     Int32,
     Int64,
     LazyFrame,
     LazyGroupBy,
     Series,
     String,
+    UInt8,
+    UInt16,
     UInt32,
+    UInt64,
     from_dict,
 )
 
 __all__ = [
-    "Boolean", "ComputeError", "DataFrame", "DataType", "DeviceError", "DuplicateError", "Expr", "Float64", "GroupBy",
-    "Int32", "Int64", "InvalidOperationError", "LazyFrame", "LazyGroupBy", "OutOfMemoryError",
-    "PolaroidError", "Series", "ShapeError", "String", "UInt32", "col", "count", "device_count", "from_dict",
-    "first", "last", "len", "lit", "max", "mean", "min", "sum",
+    "Boolean", "ComputeError", "DataFrame", "DataType", "Date", "Datetime", "DeviceError", "DuplicateError",
+    "Duration", "Expr", "Float32", "Float64", "GroupBy", "Int8", "Int16", "Int32", "Int64",
+    "InvalidOperationError", "LazyFrame", "LazyGroupBy", "OutOfMemoryError", "PolaroidError", "Series",
+    "ShapeError", "String", "UInt8", "UInt16", "UInt32", "UInt64", "col", "count", "device_count", "from_dict",
+    "first", "last", "len", "lit", "max", "mean", "min", "sum", "when",
 ]
 
 

@@ -14,7 +14,8 @@ LIB_PATH = os.path.join(_HERE, "libpolaroid_gpu.so")
 
 # dtypes (enum plgpu_dtype)
 BOOL, I32, I64, F64, U32, STR = 1, 2, 3, 4, 5, 6
-DTYPE_BYTES = {I32: 4, I64: 8, F64: 8, U32: 4}
+I8, I16, U8, U16, U64, F32 = 7, 8, 9, 10, 11, 12
+DTYPE_BYTES = {I32: 4, I64: 8, F64: 8, U32: 4, I8: 1, I16: 2, U8: 1, U16: 2, U64: 8, F32: 4}
 
 # status codes
 OK = 0
@@ -24,7 +25,8 @@ ERR_INVALID, ERR_SCHEMA, ERR_SHAPE, ERR_OOM, ERR_HIP, ERR_NO_DEVICE, ERR_CAPACIT
 # opcodes (enum plgpu_opcode)
 OP = dict(
     COL=1, LIT_F64=2, LIT_I64=3, LIT_BOOL=4, LIT_NULL=5,
-    ADD=10, SUB=11, MUL=12, TRUEDIV=13, NEG=14, ABS=15, CAST_F64=16,
+    ADD=10, SUB=11, MUL=12, TRUEDIV=13, NEG=14, ABS=15, CAST_F64=16, FLOORDIV=17, MOD=18, DIVIDE=19,
+    CAST=50, XOR=51, FILL_NULL=52, IF_ELSE=53,
     EQ=20, NE=21, LT=22, LE=23, GT=24, GE=25, EQ_MISSING=26, NE_MISSING=27,
     AND=30, OR=31, NOT=32, IS_NULL=33, IS_NOT_NULL=34, IS_NAN=35, IS_FINITE=36,
     STR_STARTS_WITH=40, STR_ENDS_WITH=41, STR_CONTAINS=42,
@@ -100,6 +102,7 @@ SIGNATURES = {
     "plgpu_memcpy_d2h": (C.c_int, [_P, _P, C.c_size_t, _P]),
     "plgpu_memcpy_d2d": (C.c_int, [_P, _P, C.c_size_t, _P]),
     "plgpu_column_release": (None, [_COLP]),
+    "plgpu_expr_dtype": (C.c_int, [_COLP, C.c_int32, C.POINTER(Instr), C.c_int32, C.POINTER(C.c_int32)]),
     "plgpu_column_alloc": (C.c_int, [C.c_int32, C.c_int64, C.c_int32, C.c_int64, _COLP, _P]),
     "plgpu_ingest_chunk": (C.c_int, [_COLP, C.c_int64, C.c_int64, _P, _P, _P, C.c_int64, C.c_int64, _P]),
     "plgpu_eval": (C.c_int, [_COLP, C.c_int32, C.POINTER(Instr), C.c_int32, _COLP, _P]),

@@ -35,7 +35,7 @@ static int grid_for(int64_t items, int threads, int max_blocks = 256 * 16) {
 // ---------------------------------------------------------------- eval
 template <int SIMPLE>
 __global__ __launch_bounds__(kEvalThreads) void eval_kernel(ColArgs cols, DevProgram prog, int64_t n,
-                                                            uint64_t* __restrict__ out_values,
+                                                            void* __restrict__ out_values,
                                                             uint64_t* __restrict__ out_validity) {
     const int lane = threadIdx.x & 63;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -59,11 +59,11 @@ __global__ __launch_bounds__(kEvalThreads) void eval_kernel(ColArgs cols, DevPro
         if (prog.out_dtype == PLGPU_BOOL) {
             const uint64_t bbits = __ballot(ok && (v & 1));
             if (lane == 0 && base + (threadIdx.x & ~63) < n) {
-                out_values[word] = bbits;
+                ((uint64_t*)out_values)[word] = bbits;
                 out_validity[word] = vbits;
             }
         } else {
-            if (r < n) out_values[r] = ok ? v : 0ull;
+            if (r < n) dev_store(out_values, prog.out_dtype, r, ok ? v : 0ull);
             if (lane == 0 && base + (threadIdx.x & ~63) < n) out_validity[word] = vbits;
         }
     }
@@ -145,7 +145,7 @@ __device__ __forceinline__ uint64_t wave_or64(uint64_t x) {
 }
 
 // Stable scatter of one column by the mask words.
-template <int EB>  // element bytes (4 or 8); 0 = bit-packed bool; 16 = the selected row ids
+template <int EB>  // element bytes (1, 2, 4 or 8); 0 = bit-packed bool; 16 = the selected row ids
 __global__ __launch_bounds__(kFilterThreads) void filter_scatter_kernel(DevCol col, int64_t n, int64_t ntiles,
                                                                         const uint64_t* __restrict__ mask_words,
                                                                         const uint64_t* __restrict__ tile_off,
@@ -186,6 +186,8 @@ __global__ __launch_bounds__(kFilterThreads) void filter_scatter_kernel(DevCol c
                 const int64_t p = col.offset + r;
                 if (EB == 8) ((uint64_t*)out_values)[pos] = ((const uint64_t*)col.values)[p];
                 else if (EB == 4) ((uint32_t*)out_values)[pos] = ((const uint32_t*)col.values)[p];
+                else if (EB == 2) ((uint16_t*)out_values)[pos] = ((const uint16_t*)col.values)[p];
+                else if (EB == 1) ((uint8_t*)out_values)[pos] = ((const uint8_t*)col.values)[p];
                 else if (EB == 16) ((int64_t*)out_values)[pos] = r;  // row ids (string columns)
             }
             if (EB == 0 || col.validity != nullptr) {
@@ -335,8 +337,14 @@ static int run_filter(const plgpu_column* cols, int32_t ncols, int src, const De
         else if (dtype_bytes(cols[i].dtype) == 8)
             filter_scatter_kernel<8><<<g, kFilterThreads, 0, s>>>(dc, n, ntiles, mask_words, offs,
                                                                   (void*)out_cols[i].values, ovalid);
-        else
+        else if (dtype_bytes(cols[i].dtype) == 4)
             filter_scatter_kernel<4><<<g, kFilterThreads, 0, s>>>(dc, n, ntiles, mask_words, offs,
+                                                                  (void*)out_cols[i].values, ovalid);
+        else if (dtype_bytes(cols[i].dtype) == 2)
+            filter_scatter_kernel<2><<<g, kFilterThreads, 0, s>>>(dc, n, ntiles, mask_words, offs,
+                                                                  (void*)out_cols[i].values, ovalid);
+        else
+            filter_scatter_kernel<1><<<g, kFilterThreads, 0, s>>>(dc, n, ntiles, mask_words, offs,
                                                                   (void*)out_cols[i].values, ovalid);
         PLGPU_HIP(hipGetLastError());
         if (!need_valid && cols[i].dtype == PLGPU_BOOL) out_cols[i].null_count = 0;
@@ -371,9 +379,9 @@ PLGPU_API int plgpu_eval(const plgpu_column* cols, int32_t ncols, const plgpu_in
     ColArgs ca = pack_cols(cols, ncols);
     const int g = grid_for(n, kEvalThreads);
     if (dp.simple)
-        eval_kernel<1><<<g, kEvalThreads, 0, s>>>(ca, dp, n, (uint64_t*)out->values, (uint64_t*)out->validity);
+        eval_kernel<1><<<g, kEvalThreads, 0, s>>>(ca, dp, n, (void*)out->values, (uint64_t*)out->validity);
     else
-        eval_kernel<0><<<g, kEvalThreads, 0, s>>>(ca, dp, n, (uint64_t*)out->values, (uint64_t*)out->validity);
+        eval_kernel<0><<<g, kEvalThreads, 0, s>>>(ca, dp, n, (void*)out->values, (uint64_t*)out->validity);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         plgpu_column_release(out);

@@ -84,6 +84,8 @@ struct AccSpec {
     int32_t f_min;
     int32_t f_max;
     int32_t f_flags;
+    int32_t uns;      // UInt64 column: min / max order and f64 conversion are unsigned
+    int32_t _pad;
 };
 
 struct GbParams {
@@ -232,8 +234,9 @@ __device__ __forceinline__ uint64_t widen32(uint32_t v, int32_t dtype) {
 // 32-bit types) load when both are in range and the pair is aligned.
 __device__ __forceinline__ void load_pair(const DevCol& c, int64_t r0, int64_t n, uint64_t& a, uint64_t& b) {
     const int64_t p = c.offset + r0;
-    const bool wide = c.dtype == PLGPU_F64 || c.dtype == PLGPU_I64;
-    if (r0 + 1 < n && (p & 1) == 0) {
+    const bool wide = c.dtype == PLGPU_F64 || c.dtype == PLGPU_I64 || c.dtype == PLGPU_U64;
+    const bool w32 = c.dtype == PLGPU_I32 || c.dtype == PLGPU_U32;
+    if (r0 + 1 < n && (p & 1) == 0 && (wide || w32)) {
         if (wide) {
             const ulonglong2 v = *reinterpret_cast<const ulonglong2*>((const uint64_t*)c.values + p);
             a = v.x;
@@ -243,7 +246,7 @@ __device__ __forceinline__ void load_pair(const DevCol& c, int64_t r0, int64_t n
             a = widen32(v.x, c.dtype);
             b = widen32(v.y, c.dtype);
         }
-    } else {
+    } else {  // unaligned pair, tail, or a 1 / 2-byte / Float32 column: register-form loads
         a = r0 < n ? dev_load(c, r0) : 0ull;
         b = r0 + 1 < n ? dev_load(c, r0 + 1) : 0ull;
     }
@@ -261,7 +264,7 @@ struct ThreadDiag {
 // per-row code walks the accs in a rolled loop with one copy of the logic
 // and only two scalar registers per acc live.
 //   [0,8) flags  [8,16) f_sum  [16,24) f_isum  [24,32) f_cnt
-//   [32,40) f_min  [40,48) f_max  [48,56) f_flags  [56] isf
+//   [32,40) f_min  [40,48) f_max  [48,56) f_flags  [56] isf  [57] unsigned (UInt64)
 // Absent fields are 0xFF.
 __device__ __forceinline__ int dfield(uint64_t d, int sh) { return (int)((d >> sh) & 0xFF); }
 constexpr int kNoField = 0xFF;
@@ -302,7 +305,7 @@ __device__ __forceinline__ void apply_row(const GbParams& p, uint64_t* lds, int 
                     fsum_ok = (flags & A_FSUM) != 0;
                 }
             } else if (flags & A_FSUMCAST) {
-                sb = f64_bits((double)(int64_t)x);
+                sb = f64_bits(((d >> 57) & 1) ? (double)x : (double)(int64_t)x);
                 fsum_ok = true;
             }
             if (fsum_ok) {
@@ -324,7 +327,7 @@ __device__ __forceinline__ void apply_row(const GbParams& p, uint64_t* lds, int 
                 }
             }
             if ((flags & (A_MIN | A_MAX)) && !is_nan) {
-                const uint64_t o = isf ? ord_f64(x) : ord_i64(x);
+                const uint64_t o = isf ? ord_f64(x) : (((d >> 57) & 1) ? x : ord_i64(x));
                 if (flags & A_MIN) atomicMin(F(dfield(d, 32)), (unsigned long long)o);
                 if (flags & A_MAX) atomicMax(F(dfield(d, 40)), (unsigned long long)o);
             }
@@ -1256,6 +1259,8 @@ struct OutSpec {
     int32_t acc;
     int32_t out_dtype;
     int32_t in_isf;
+    int32_t in_uns;
+    int32_t _pad;
     void* values;
     uint32_t* validity;
 };
@@ -1295,9 +1300,8 @@ __global__ void gb_finalize_kernel(GbParams p, FinParams fp) {
             case PLGPU_AGG_SUM:
             case PLGPU_AGG_MEAN: {
                 if (os.kind == PLGPU_AGG_SUM && !os.in_isf) {
-                    const uint64_t v = *gfield(p, ac.f_isum, s);
-                    if (os.out_dtype == PLGPU_I64) ((uint64_t*)os.values)[g] = v;
-                    else ((uint32_t*)os.values)[g] = (uint32_t)v;
+                    // wrapping integer sum, stored at the output width
+                    dev_store(os.values, os.out_dtype, g, *gfield(p, ac.f_isum, s));
                     break;
                 }
                 double sum;
@@ -1311,7 +1315,7 @@ __global__ void gb_finalize_kernel(GbParams p, FinParams fp) {
                     if (cnt == 0) { valid = false; sum = 0.0; }
                     else sum = sum / (double)cnt;
                 }
-                ((double*)os.values)[g] = sum;
+                dev_store(os.values, os.out_dtype, g, f64_bits(sum));  // Float32: rounded once more
                 break;
             }
             case PLGPU_AGG_MIN:
@@ -1323,12 +1327,13 @@ __global__ void gb_finalize_kernel(GbParams p, FinParams fp) {
                     if (cnt == 0) { valid = false; v = 0.0; }
                     else if (none) v = __builtin_nan("");  // every valid value was NaN
                     else v = as_f64(unord_f64(o));
-                    ((double*)os.values)[g] = v;
+                    dev_store(os.values, os.out_dtype, g, f64_bits(v));
                 } else {
-                    const int64_t v = (cnt == 0 || none) ? 0 : (int64_t)(o ^ 0x8000000000000000ull);
+                    // (the all-ones / all-zeros "none" encodings are real
+                    // values here: an integer group with cnt > 0 has one)
+                    const uint64_t v = cnt == 0 ? 0ull : (os.in_uns ? o : (o ^ 0x8000000000000000ull));
                     if (cnt == 0) valid = false;
-                    if (os.out_dtype == PLGPU_I64) ((int64_t*)os.values)[g] = v;
-                    else ((int32_t*)os.values)[g] = (int32_t)v;
+                    dev_store(os.values, os.out_dtype, g, v);
                 }
                 break;
             }
@@ -1339,8 +1344,7 @@ __global__ void gb_finalize_kernel(GbParams p, FinParams fp) {
                 const int64_t row = (int64_t)*gfield(p, os.kind == PLGPU_AGG_FIRST ? p.f_first : p.f_last, s);
                 valid = dev_valid(ac.c, row);
                 const uint64_t v = valid ? dev_load(ac.c, row) : 0ull;
-                if (os.out_dtype == PLGPU_I64 || os.out_dtype == PLGPU_F64) ((uint64_t*)os.values)[g] = v;
-                else ((uint32_t*)os.values)[g] = (uint32_t)v;
+                dev_store(os.values, os.out_dtype, g, v);
                 break;
             }
             default: break;
@@ -1357,9 +1361,9 @@ __global__ void gather_kernel(const T* __restrict__ src, const int64_t* __restri
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         dst[i] = src[perm[i]];
 }
-__global__ void narrow_i64_kernel(const int64_t* __restrict__ a, int32_t* __restrict__ b, int64_t n) {
+__global__ void narrow_i64_kernel(const int64_t* __restrict__ a, void* __restrict__ b, int32_t dt, int64_t n) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        b[i] = (int32_t)a[i];
+        dev_store(b, dt, i, (uint64_t)a[i]);
 }
 __global__ void gather_bits_kernel(const uint32_t* __restrict__ src, const int64_t* __restrict__ perm,
                                    uint32_t* __restrict__ dst, int64_t n) {
@@ -1506,7 +1510,7 @@ static int plan_groupby(const plgpu_column* key, const plgpu_column* cols, int32
         const int c = aggs[i].col;
         if (c < 0 || c >= ncols) return fail(PLGPU_ERR_INVALID, "aggregation column index out of range");
         const int32_t dt = cols[c].dtype;
-        if (dt != PLGPU_F64 && dt != PLGPU_I64 && dt != PLGPU_I32 && dt != PLGPU_U32)
+        if (!dtype_is_int(dt) && !dtype_is_float(dt))
             return fail(PLGPU_ERR_INVALID, "aggregation not supported for this dtype");
         if (acc_of_col[c] < 0) {
             if (p.nacc == kMaxAcc) return fail(PLGPU_ERR_INVALID, "too many aggregated columns (max 6)");
@@ -1515,10 +1519,11 @@ static int plan_groupby(const plgpu_column* key, const plgpu_column* cols, int32
             std::memset(&ac, 0xff, sizeof ac);
             ac.c = to_dev(cols[c]);
             ac.flags = 0;
-            ac.isf = dt == PLGPU_F64;
+            ac.isf = dtype_is_float(dt);  // Float32 in register form (f64 bits): exact sums, TotalOrd min / max
+            ac.uns = dt == PLGPU_U64;
         }
         AccSpec& ac = p.acc[acc_of_col[c]];
-        const bool isf = dt == PLGPU_F64;
+        const bool isf = dtype_is_float(dt);
         // partial / merge mode keeps the record layout schema-only (the same on
         // every rank whatever its validity bitmaps): counts always present
         const bool nullable = cols[c].validity != nullptr || force_counts;
@@ -1579,7 +1584,7 @@ static int plan_groupby(const plgpu_column* key, const plgpu_column* cols, int32
         auto fb = [](int f) -> uint64_t { return f < 0 ? (uint64_t)kNoField : (uint64_t)f; };
         p.desc[a] = (uint64_t)(ac.flags & 0xFF) | (fb(ac.f_sum) << 8) | (fb(ac.f_isum) << 16) | (fb(ac.f_cnt) << 24) |
                     (fb(ac.f_min) << 32) | (fb(ac.f_max) << 40) | (fb(ac.f_flags) << 48) |
-                    ((uint64_t)(ac.isf ? 1 : 0) << 56);
+                    ((uint64_t)(ac.isf ? 1 : 0) << 56) | ((uint64_t)(ac.uns ? 1 : 0) << 57);
     }
     // simple predicate: reuse an aggregated column's registers when possible
     p.pred_acc = -1;
@@ -1594,11 +1599,15 @@ static int plan_groupby(const plgpu_column* key, const plgpu_column* cols, int32
         o.kind = aggs[i].kind;
         o.acc = pl->acc_of_agg[i];
         const int32_t dt = cols[aggs[i].col].dtype;
-        o.in_isf = dt == PLGPU_F64;
+        o.in_isf = dtype_is_float(dt);
+        o.in_uns = dt == PLGPU_U64;
         switch (o.kind) {
         case PLGPU_AGG_LEN:
         case PLGPU_AGG_COUNT: o.out_dtype = PLGPU_U32; break;
-        case PLGPU_AGG_MEAN: o.out_dtype = PLGPU_F64; break;
+        case PLGPU_AGG_MEAN: o.out_dtype = dt == PLGPU_F32 ? PLGPU_F32 : PLGPU_F64; break;  // reduce/mean.rs:29
+        case PLGPU_AGG_SUM:  // reduce/sum.rs:40 out_dtype: small ints sum as Int64
+            o.out_dtype = (dt == PLGPU_I8 || dt == PLGPU_I16 || dt == PLGPU_U8 || dt == PLGPU_U16) ? PLGPU_I64 : dt;
+            break;
         default: o.out_dtype = dt; break;
         }
         pl->outs.push_back(o);
@@ -1811,8 +1820,7 @@ static int gb_prepare(GbRun& R, const plgpu_column* key, const plgpu_column* col
     if (key == nullptr) return fail(PLGPU_ERR_INVALID, "key is NULL");
     if (ncols < 0 || ncols > PLGPU_MAX_COLS) return fail(PLGPU_ERR_INVALID, "too many columns (max 8)");
     if (naggs < 0 || naggs > PLGPU_MAX_COLS * 2) return fail(PLGPU_ERR_INVALID, "too many aggregations (max 16)");
-    if (key->dtype != PLGPU_I64 && key->dtype != PLGPU_I32)
-        return fail(PLGPU_ERR_SCHEMA, "group-by key must be Int64 or Int32");
+    if (!dtype_is_int(key->dtype)) return fail(PLGPU_ERR_SCHEMA, "group-by key must be an integer column");
     for (int i = 0; i < ncols; ++i)
         if (cols[i].length != key->length) return fail(PLGPU_ERR_SHAPE, "columns must match the key length");
     R.key_dtype = key->dtype;
@@ -2374,13 +2382,14 @@ static int gb_finalize(GbRun& R, int32_t naggs, plgpu_column* out_key, plgpu_col
             }
         }
     }
-    if (rc == PLGPU_OK && R.key_dtype == PLGPU_I32) {
-        // narrow the key back to Int32 (the reference keeps the key dtype)
+    if (rc == PLGPU_OK && R.key_dtype != PLGPU_I64 && dtype_bytes(R.key_dtype) > 0) {
+        // the key back in its own dtype (the reference keeps the key dtype)
         plgpu_column nk;
-        rc = make_owned_column(&nk, PLGPU_I32, groups, true, s);
+        rc = make_owned_column(&nk, R.key_dtype, groups, true, s);
         if (rc == PLGPU_OK && groups > 0) {
             const int gg = (int)std::min<int64_t>((groups + 255) / 256, 4096);
-            narrow_i64_kernel<<<gg, 256, 0, s>>>((const int64_t*)out_key->values, (int32_t*)nk.values, groups);
+            narrow_i64_kernel<<<gg, 256, 0, s>>>((const int64_t*)out_key->values, (void*)nk.values, R.key_dtype,
+                                                 groups);
             (void)hipMemcpyAsync((void*)nk.validity, out_key->validity, ((groups + 63) / 64) * 8,
                                  hipMemcpyDeviceToDevice, s);
         }
@@ -2488,14 +2497,10 @@ __global__ void mk_gather_key_kernel(DevCol c, const uint64_t* __restrict__ rows
         const int64_t r = (int64_t)rows[g];
         const bool v = dev_valid(c, r);
         const uint64_t x = dev_load(c, r);
-        switch (c.dtype) {
-        case PLGPU_F64:
-        case PLGPU_I64: ((uint64_t*)out)[g] = x; break;
-        case PLGPU_I32:
-        case PLGPU_U32: ((uint32_t*)out)[g] = (uint32_t)x; break;
-        default:
+        if (c.dtype == PLGPU_BOOL) {
             if (x & 1) atomicOr(&((uint32_t*)out)[g >> 5], 1u << (g & 31));
-            break;
+        } else {
+            dev_store(out, c.dtype, g, x);
         }
         if (out_valid && v) atomicOr(&out_valid[g >> 5], 1u << (g & 31));
     }
@@ -2644,7 +2649,7 @@ PLGPU_API int plgpu_gb_merge(const void* records, int64_t n_records, const plgpu
     for (auto& c : c2) c.length = 0;
     plgpu_column k;
     std::memset(&k, 0, sizeof k);
-    k.dtype = key_dtype == PLGPU_I32 ? PLGPU_I32 : PLGPU_I64;
+    k.dtype = dtype_is_int(key_dtype) ? key_dtype : PLGPU_I64;
     GbRun R;
     int rc = gb_prepare(R, &k, c2.data(), ncols, nullptr, 0, aggs, naggs, false, true, stream);
     if (rc) return rc;
@@ -2746,9 +2751,8 @@ PLGPU_API int plgpu_group_by_agg_multi(const plgpu_column* keys, int32_t nkeys, 
     mk.n = nkeys;
     for (int i = 0; i < nkeys; ++i) {
         const int32_t dt = keys[i].dtype;
-        if (dt != PLGPU_I64 && dt != PLGPU_I32 && dt != PLGPU_U32 && dt != PLGPU_F64 && dt != PLGPU_BOOL &&
-            dt != PLGPU_STR)
-            return fail(PLGPU_ERR_SCHEMA, "group-by keys must be Int64, Int32, UInt32, Float64, Boolean or String");
+        if (!dtype_is_int(dt) && !dtype_is_float(dt) && dt != PLGPU_BOOL && dt != PLGPU_STR)
+            return fail(PLGPU_ERR_SCHEMA, "group-by keys must be integer, float, Boolean or String columns");
         if (keys[i].length != n) return fail(PLGPU_ERR_SHAPE, "key columns must have equal lengths");
         mk.c[i] = to_dev(keys[i]);
     }
@@ -2977,10 +2981,10 @@ __global__ __launch_bounds__(256) void sq_build_kernel(DevCol gk, DevCol mean, i
 __device__ __forceinline__ double sq_as_f64(const DevCol& c, int64_t r) {
     const uint64_t b = dev_load(c, r);
     switch (c.dtype) {
-    case PLGPU_F64: return as_f64(b);
-    case PLGPU_U32:
-    case PLGPU_BOOL: return (double)b;
-    default: return (double)(int64_t)b;
+    case PLGPU_F64:
+    case PLGPU_F32: return as_f64(b);  // register form
+    case PLGPU_U64: return (double)b;
+    default: return (double)(int64_t)b;  // signed ints sign-extended, unsigned / Boolean zero-extended
     }
 }
 
@@ -3063,7 +3067,7 @@ PLGPU_API int plgpu_group_sq_dev(const plgpu_column* row_key, const plgpu_column
     if (!row_key || !x || !group_key || !group_mean || !out) return fail(PLGPU_ERR_INVALID, "NULL argument");
     std::memset(out, 0, sizeof *out);
     const int32_t kt = row_key->dtype;
-    if (kt != group_key->dtype || (kt != PLGPU_I64 && kt != PLGPU_I32 && kt != PLGPU_U32 && kt != PLGPU_BOOL))
+    if (kt != group_key->dtype || (!dtype_is_int(kt) && kt != PLGPU_BOOL))
         return fail(PLGPU_ERR_SCHEMA, "squared deviations take one integer / Boolean key of one dtype");
     if (x->dtype == PLGPU_STR || group_mean->dtype != PLGPU_F64)
         return fail(PLGPU_ERR_SCHEMA, "squared deviations take a numeric x and Float64 means");

@@ -244,7 +244,7 @@ __global__ __launch_bounds__(kJnThreads) void jn_probe_match_kernel(DevCol pk, i
     __shared__ uint4 rowbuf[kJnThreads];  // {key lo, key hi, bucket, regular}
     __shared__ uint2 hitbuf[kJnThreads];  // {ref, slot} of the matching cell
     const uint64_t* kp = (const uint64_t*)pk.values + pk.offset;
-    const bool wide = pk.dtype == PLGPU_I64;
+    const bool wide = pk.dtype == PLGPU_I64 || pk.dtype == PLGPU_U64;
     const int lane = threadIdx.x & 63;
     const int wbase = threadIdx.x & ~63;
     const int g = lane >> 3, e = lane & 7;
@@ -709,7 +709,7 @@ __device__ __forceinline__ bool idx_null(const uint8_t* iv, int64_t ioff, int64_
     return iv != nullptr && !((iv[(ioff + o) >> 3] >> ((ioff + o) & 7)) & 1);
 }
 
-template <int EB>  // element bytes 4 / 8
+template <int EB>  // element bytes 1 / 2 / 4 / 8
 __global__ __launch_bounds__(256) void gather_col_kernel(DevCol c, const uint32_t* __restrict__ idx, int64_t n,
                                                          void* __restrict__ out, uint64_t* __restrict__ out_valid,
                                                          const uint8_t* __restrict__ iv, int64_t ioff) {
@@ -730,14 +730,20 @@ __global__ __launch_bounds__(256) void gather_col_kernel(DevCol c, const uint32_
         for (int k = 0; k < K; ++k) {
             const int64_t p = c.offset + r[k];
             v[k] = 0;
-            if (in[k]) v[k] = EB == 8 ? ((const uint64_t*)c.values)[p] : ((const uint32_t*)c.values)[p];
+            if (in[k])
+                v[k] = EB == 8   ? ((const uint64_t*)c.values)[p]
+                       : EB == 4 ? ((const uint32_t*)c.values)[p]
+                       : EB == 2 ? ((const uint16_t*)c.values)[p]
+                                 : ((const uint8_t*)c.values)[p];
         }
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const int64_t o = base + (int64_t)k * blockDim.x + threadIdx.x;
             if (o < n) {
                 if (EB == 8) __builtin_nontemporal_store(v[k], (uint64_t*)out + o);
-                else __builtin_nontemporal_store((uint32_t)v[k], (uint32_t*)out + o);
+                else if (EB == 4) __builtin_nontemporal_store((uint32_t)v[k], (uint32_t*)out + o);
+                else if (EB == 2) ((uint16_t*)out)[o] = (uint16_t)v[k];
+                else ((uint8_t*)out)[o] = (uint8_t)v[k];
             }
             if (out_valid) {
                 // one validity word per wave and k (o of lane 0 is a multiple of 64)
@@ -851,8 +857,12 @@ static int gather_into(const plgpu_column& src, const uint32_t* idx, int64_t n, 
         gather_bool_kernel<<<g, 256, 0, s>>>(c, idx, n, (uint64_t*)out->values, ov, iv, ioff);
     else if (dtype_bytes(src.dtype) == 8)
         gather_col_kernel<8><<<g, 256, 0, s>>>(c, idx, n, (void*)out->values, ov, iv, ioff);
-    else
+    else if (dtype_bytes(src.dtype) == 4)
         gather_col_kernel<4><<<g, 256, 0, s>>>(c, idx, n, (void*)out->values, ov, iv, ioff);
+    else if (dtype_bytes(src.dtype) == 2)
+        gather_col_kernel<2><<<g, 256, 0, s>>>(c, idx, n, (void*)out->values, ov, iv, ioff);
+    else
+        gather_col_kernel<1><<<g, 256, 0, s>>>(c, idx, n, (void*)out->values, ov, iv, ioff);
     PLGPU_HIP(hipGetLastError());
     out->null_count = nullable ? -1 : 0;
     return PLGPU_OK;
@@ -1274,8 +1284,7 @@ static int jn_probe_partitioned(const plgpu_column* key, const JnBuilt& b, bool 
 
 static int check_key(const plgpu_column* k) {
     if (k == nullptr) return fail(PLGPU_ERR_INVALID, "join key is NULL");
-    if (k->dtype != PLGPU_I64 && k->dtype != PLGPU_I32 && k->dtype != PLGPU_U32)
-        return fail(PLGPU_ERR_SCHEMA, "join key must be an integer column (Int64 / Int32 / UInt32)");
+    if (!dtype_is_int(k->dtype)) return fail(PLGPU_ERR_SCHEMA, "join key must be an integer column");
     if (k->length >= 0xFFFFFFFFll) return fail(PLGPU_ERR_CAPACITY, "join side exceeds the u32 index space");
     return PLGPU_OK;
 }
@@ -1568,9 +1577,8 @@ PLGPU_API int plgpu_join_multi(const plgpu_column* left_keys, const plgpu_column
     const int64_t nl = left_keys[0].length, nr = right_keys[0].length;
     for (int i = 0; i < nkeys; ++i) {
         const int32_t dt = left_keys[i].dtype;
-        if (dt != PLGPU_I64 && dt != PLGPU_I32 && dt != PLGPU_U32 && dt != PLGPU_F64 && dt != PLGPU_BOOL &&
-            dt != PLGPU_STR)
-            return fail(PLGPU_ERR_SCHEMA, "join keys must be Int64, Int32, UInt32, Float64, Boolean or String");
+        if (!dtype_is_int(dt) && !dtype_is_float(dt) && dt != PLGPU_BOOL && dt != PLGPU_STR)
+            return fail(PLGPU_ERR_SCHEMA, "join keys must be integer, float, Boolean or String columns");
         if (right_keys[i].dtype != dt) return fail(PLGPU_ERR_SCHEMA, "datatypes of join keys don't match");
         if (left_keys[i].length != nl || right_keys[i].length != nr)
             return fail(PLGPU_ERR_SHAPE, "join key columns of one side must have equal lengths");
@@ -1808,19 +1816,11 @@ __global__ __launch_bounds__(256) void coalesce_kernel(DevCol a, DevCol b, int64
         const bool va = in && dev_valid(a, r);
         const bool vb = in && !va && dev_valid(b, r);
         const uint64_t v = va ? dev_load(a, r) : (vb ? dev_load(b, r) : 0ull);
-        switch (a.dtype) {
-        case PLGPU_I64:
-        case PLGPU_F64:
-            if (in) ((uint64_t*)out)[r] = v;
-            break;
-        case PLGPU_I32:
-        case PLGPU_U32:
-            if (in) ((uint32_t*)out)[r] = (uint32_t)v;
-            break;
-        default: {
+        if (a.dtype == PLGPU_BOOL) {
             const uint64_t w = __ballot(in && (v & 1));
             if ((threadIdx.x & 63) == 0 && in) ((uint64_t*)out)[r >> 6] = w;
-        }
+        } else if (in) {
+            dev_store(out, a.dtype, r, v);
         }
         const uint64_t vw = __ballot(va || vb);
         if ((threadIdx.x & 63) == 0 && in) out_valid[r >> 6] = vw;

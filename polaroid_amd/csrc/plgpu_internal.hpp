@@ -45,15 +45,28 @@ struct OwnedBuffers {
 int make_owned_column(plgpu_column* out, int32_t dtype, int64_t length, bool with_validity,
                       hipStream_t s);
 
-inline int dtype_bytes(int32_t dt) {
+__host__ __device__ inline int dtype_bytes(int32_t dt) {
     switch (dt) {
+    case PLGPU_I8:
+    case PLGPU_U8: return 1;
+    case PLGPU_I16:
+    case PLGPU_U16: return 2;
     case PLGPU_I32:
-    case PLGPU_U32: return 4;
+    case PLGPU_U32:
+    case PLGPU_F32: return 4;
     case PLGPU_I64:
+    case PLGPU_U64:
     case PLGPU_F64: return 8;
-    default: return 0;  // BOOL is bit-packed
+    default: return 0;  // BOOL is bit-packed, STR has offsets + bytes
     }
 }
+
+// Numeric classes of the physical dtypes.
+__host__ __device__ inline bool dtype_is_int(int32_t dt) {
+    return dt == PLGPU_I8 || dt == PLGPU_I16 || dt == PLGPU_I32 || dt == PLGPU_I64 || dt == PLGPU_U8 ||
+           dt == PLGPU_U16 || dt == PLGPU_U32 || dt == PLGPU_U64;
+}
+__host__ __device__ inline bool dtype_is_float(int32_t dt) { return dt == PLGPU_F32 || dt == PLGPU_F64; }
 
 // --------------------------------------------------------- device columns
 struct DevCol {
@@ -96,6 +109,8 @@ int str_from_codes(const plgpu_column& codes, plgpu_column* out, hipStream_t s);
 // Lowered (typed) program: the host resolves every operand type, inserts
 // casts, and emits one micro-op per step so the device interpreter does no
 // type dispatch of its own.
+// Operand widths: an `arg` of F32 on a float op computes in single
+// precision; D_WRAP / D_CAST take physical dtype codes.
 enum DevOp : int32_t {
     D_COL_F64 = 1, D_COL_I64, D_COL_I32, D_COL_U32, D_COL_BOOL,
     D_LIT, D_NULL,
@@ -106,7 +121,19 @@ enum DevOp : int32_t {
     D_EQ_I, D_NE_I, D_LT_I, D_LE_I, D_GT_I, D_GE_I,
     D_EQM_F, D_NEM_F, D_EQM_I, D_NEM_I, D_EQM_B, D_NEM_B,
     D_EQ_B, D_NE_B,
-    D_AND, D_OR, D_NOT, D_ISNULL, D_ISNOTNULL, D_ISNAN_F, D_ISFINITE_F, D_FALSE_VALID
+    D_AND, D_OR, D_NOT, D_ISNULL, D_ISNOTNULL, D_ISNAN_F, D_ISFINITE_F, D_FALSE_VALID,
+    // round 2: widths, division, casts, bitwise, selection
+    D_COL,            // any dtype (dev_load register form)
+    D_WRAP,           // s0 = s0 wrapped to integer dtype arg
+    D_CAST,           // s0 = cast(s0) from dtype imm>>8 & 0xff to arg; imm & 1 = overflowing
+    D_EQ_U, D_NE_U, D_LT_U, D_LE_U, D_GT_U, D_GE_U,   // UInt64 compares
+    D_FLOORDIV_I, D_MOD_I,      // arg: 1 = UInt64 (unsigned); x / 0 -> null
+    D_FLOORDIV_F, D_MOD_F,      // floor(a / b), a - b * floor(a / b)
+    D_DIV_FS, D_FLOORDIV_FS, D_MOD_FS,  // scalar divisor: a * (1 / b) forms (float.rs:78-98, :113)
+    D_BAND, D_BOR, D_BXOR,      // bitwise on integers
+    D_XOR,                      // Boolean xor, null if either is null
+    D_FILL_NULL,                // [x, fill]
+    D_IF_ELSE                   // [cond, then, otherwise]
 };
 
 struct DevInstr {
@@ -144,15 +171,37 @@ __device__ __forceinline__ bool dev_valid(const DevCol& c, int64_t r) {
     return (c.validity[p >> 3] >> (p & 7)) & 1;
 }
 
-// Raw 64-bit payload of column c at row r (ints sign/zero-extended, bool as 0/1).
+// Register form of column c at row r: signed ints sign-extended, unsigned
+// ints zero-extended (UInt64 as its bits), Float64 as its bits, Float32 as
+// the bits of the (exactly equal) double, Boolean as 0 / 1.
 __device__ __forceinline__ uint64_t dev_load(const DevCol& c, int64_t r) {
     int64_t p = c.offset + r;
     switch (c.dtype) {
     case PLGPU_F64:
-    case PLGPU_I64: return ((const uint64_t*)c.values)[p];
+    case PLGPU_I64:
+    case PLGPU_U64: return ((const uint64_t*)c.values)[p];
     case PLGPU_I32: return (uint64_t)(int64_t)((const int32_t*)c.values)[p];
     case PLGPU_U32: return (uint64_t)((const uint32_t*)c.values)[p];
+    case PLGPU_F32: return (uint64_t)__double_as_longlong((double)((const float*)c.values)[p]);
+    case PLGPU_I16: return (uint64_t)(int64_t)((const int16_t*)c.values)[p];
+    case PLGPU_U16: return (uint64_t)((const uint16_t*)c.values)[p];
+    case PLGPU_I8: return (uint64_t)(int64_t)((const int8_t*)c.values)[p];
+    case PLGPU_U8: return (uint64_t)((const uint8_t*)c.values)[p];
     default: return (((const uint8_t*)c.values)[p >> 3] >> (p & 7)) & 1;
+    }
+}
+
+// Store the register form v as one element of dtype dt at out[i].
+__device__ __forceinline__ void dev_store(void* out, int32_t dt, int64_t i, uint64_t v) {
+    switch (dt) {
+    case PLGPU_I8:
+    case PLGPU_U8: ((uint8_t*)out)[i] = (uint8_t)v; break;
+    case PLGPU_I16:
+    case PLGPU_U16: ((uint16_t*)out)[i] = (uint16_t)v; break;
+    case PLGPU_I32:
+    case PLGPU_U32: ((uint32_t*)out)[i] = (uint32_t)v; break;
+    case PLGPU_F32: ((float*)out)[i] = (float)__longlong_as_double((long long)v); break;
+    default: ((uint64_t*)out)[i] = v; break;
     }
 }
 
@@ -183,6 +232,78 @@ __device__ __forceinline__ bool cmp_i(int op, int64_t a, int64_t b) {
     }
 }
 
+// Integer register value wrapped to integer dtype dt (two's complement).
+__device__ __forceinline__ uint64_t wrap_to(uint64_t v, int dt) {
+    switch (dt) {
+    case PLGPU_I8: return (uint64_t)(int64_t)(int8_t)v;
+    case PLGPU_I16: return (uint64_t)(int64_t)(int16_t)v;
+    case PLGPU_I32: return (uint64_t)(int64_t)(int32_t)v;
+    case PLGPU_U8: return v & 0xFFull;
+    case PLGPU_U16: return v & 0xFFFFull;
+    case PLGPU_U32: return v & 0xFFFFFFFFull;
+    default: return v;
+    }
+}
+
+// Does the integer register value v (of dtype from) hold a value of dtype to?
+__device__ __forceinline__ bool int_fits(uint64_t v, int from, int to) {
+    const bool neg = from != PLGPU_U64 && (int64_t)v < 0;
+    const bool big = from == PLGPU_U64 && (int64_t)v < 0;  // >= 2^63
+    const int64_t x = (int64_t)v;
+    switch (to) {
+    case PLGPU_I8: return !big && x >= -128 && x <= 127;
+    case PLGPU_I16: return !big && x >= -32768 && x <= 32767;
+    case PLGPU_I32: return !big && x >= INT32_MIN && x <= INT32_MAX;
+    case PLGPU_I64: return !big;
+    case PLGPU_U8: return !neg && !big && x <= 255;
+    case PLGPU_U16: return !neg && !big && x <= 65535;
+    case PLGPU_U32: return !neg && !big && x <= 4294967295ll;
+    case PLGPU_U64: return !neg;
+    default: return true;
+    }
+}
+
+// cast(v: from) -> to (polars non-strict cast: a value that does not fit
+// gives null; `overflowing`: integers wrap).  Floats are in register form.
+__device__ __forceinline__ uint64_t cast_value(uint64_t v, int from, int to, bool overflowing, bool& ok) {
+    const bool fi = from == PLGPU_F32 || from == PLGPU_F64, ti = to == PLGPU_F32 || to == PLGPU_F64;
+    if (to == PLGPU_BOOL) return fi ? (as_f64(v) != 0.0 ? 1ull : 0ull) : (v != 0 ? 1ull : 0ull);
+    if (from == PLGPU_BOOL) return ti ? f64_bits(v ? 1.0 : 0.0) : v;
+    if (!fi && !ti) {
+        if (int_fits(v, from, to)) return v;
+        if (overflowing) return wrap_to(v, to);
+        ok = false;
+        return 0;
+    }
+    if (!fi && ti) {
+        if (to == PLGPU_F32) {
+            const float f = from == PLGPU_U64 ? (float)v : (float)(int64_t)v;
+            return f64_bits((double)f);
+        }
+        return f64_bits(from == PLGPU_U64 ? (double)v : (double)(int64_t)v);
+    }
+    const double d = as_f64(v);
+    if (ti) return to == PLGPU_F32 ? f64_bits((double)(float)d) : v;
+    // float -> int: truncate; NaN / out of range -> null
+    const double t = trunc(d);
+    bool in;
+    switch (to) {
+    case PLGPU_I8: in = t >= -128.0 && t <= 127.0; break;
+    case PLGPU_I16: in = t >= -32768.0 && t <= 32767.0; break;
+    case PLGPU_I32: in = t >= -2147483648.0 && t <= 2147483647.0; break;
+    case PLGPU_I64: in = t >= -9223372036854775808.0 && t < 9223372036854775808.0; break;
+    case PLGPU_U8: in = t >= 0.0 && t <= 255.0; break;
+    case PLGPU_U16: in = t >= 0.0 && t <= 65535.0; break;
+    case PLGPU_U32: in = t >= 0.0 && t <= 4294967295.0; break;
+    default: in = t >= 0.0 && t < 18446744073709551616.0; break;
+    }
+    if (!in) {  // also NaN
+        ok = false;
+        return 0;
+    }
+    return to == PLGPU_U64 ? (uint64_t)t : (uint64_t)(int64_t)t;
+}
+
 // Evaluate a lowered program for one row.  The stack lives in eight named
 // registers shifted by static moves (no runtime-indexed arrays -> no
 // scratch); the validity of stack entry j is bit j of `vm`.
@@ -211,6 +332,7 @@ __device__ __forceinline__ RowVal eval_row(const DevInstr* __restrict__ code, in
         const int arg = code[k].arg;
         const uint64_t imm = code[k].imm;
         switch (op) {
+        case D_COL:
         case D_COL_F64:
         case D_COL_I64:
         case D_COL_I32:
@@ -236,20 +358,121 @@ __device__ __forceinline__ RowVal eval_row(const DevInstr* __restrict__ code, in
         case D_ISNAN_F: s0 = __builtin_isnan(as_f64(s0)) ? 1ull : 0ull; break;
         case D_ISFINITE_F: s0 = __builtin_isfinite(as_f64(s0)) ? 1ull : 0ull; break;
         case D_FALSE_VALID: s0 = 0ull; vm |= 1u; break;
+        case D_WRAP: s0 = wrap_to(s0, arg); break;
+        case D_CAST: {
+            // imm bits 8..15: source dtype; bit 0: overflowing; bit 16: cast
+            // the second entry (s1) instead of the top
+            bool ok = true;
+            if (imm & 0x10000ull) {
+                s1 = cast_value(s1, (int)((imm >> 8) & 0xFF), arg, (imm & 1) != 0, ok);
+                if (!ok) vm &= ~2u;
+            } else {
+                s0 = cast_value(s0, (int)((imm >> 8) & 0xFF), arg, (imm & 1) != 0, ok);
+                if (!ok) vm &= ~1u;
+            }
+            break;
+        }
+        case D_IF_ELSE: {
+            // [cond = s2, then = s1, otherwise = s0]; a null condition is false
+            const bool take = ((vm >> 2) & 1u) && (s2 & 1);
+            const uint64_t v = take ? s1 : s0;
+            const bool ok = take ? ((vm >> 1) & 1u) : (vm & 1u);
+            POP1();
+            POP1();
+            s0 = v;
+            vm = (vm & ~1u) | (ok ? 1u : 0u);
+            break;
+        }
         default: {
             // binary: a = s1, b = s0
             const uint64_t a = s1, b = s0;
             const bool va = (vm >> 1) & 1u, vb = vm & 1u;
             uint64_t res = 0;
             bool ok = va & vb;
+            const bool f32 = arg == PLGPU_F32;
+            const double fa = as_f64(a), fb = as_f64(b);
+            const float ga = (float)fa, gb = (float)fb;  // exact for Float32 operands
             switch (op) {
             case D_ADD_I: res = a + b; break;
             case D_SUB_I: res = a - b; break;
             case D_MUL_I: res = a * b; break;
-            case D_ADD_F: res = f64_bits(as_f64(a) + as_f64(b)); break;
-            case D_SUB_F: res = f64_bits(as_f64(a) - as_f64(b)); break;
-            case D_MUL_F: res = f64_bits(as_f64(a) * as_f64(b)); break;
-            case D_DIV_F: res = f64_bits(as_f64(a) / as_f64(b)); break;
+            case D_ADD_F: res = f64_bits(f32 ? (double)(ga + gb) : fa + fb); break;
+            case D_SUB_F: res = f64_bits(f32 ? (double)(ga - gb) : fa - fb); break;
+            case D_MUL_F: res = f64_bits(f32 ? (double)(ga * gb) : fa * fb); break;
+            case D_DIV_F: res = f64_bits(f32 ? (double)(ga / gb) : fa / fb); break;
+            case D_DIV_FS: res = f64_bits(f32 ? (double)(ga * (1.0f / gb)) : fa * (1.0 / fb)); break;
+            case D_FLOORDIV_F: res = f64_bits(f32 ? (double)floorf(ga / gb) : floor(fa / fb)); break;
+            case D_FLOORDIV_FS:
+                res = f64_bits(f32 ? (double)floorf(ga * (1.0f / gb)) : floor(fa * (1.0 / fb)));
+                break;
+            case D_MOD_F: {
+                if (f32) {
+                    const float q = floorf(ga / gb);
+                    const float bq = gb * q;
+                    res = f64_bits((double)(ga - bq));
+                } else {
+                    const double q = floor(fa / fb);
+                    const double bq = fb * q;
+                    res = f64_bits(fa - bq);
+                }
+                break;
+            }
+            case D_MOD_FS: {
+                if (f32) {
+                    const float q = floorf(ga * (1.0f / gb));
+                    const float bq = gb * q;
+                    res = f64_bits((double)(ga - bq));
+                } else {
+                    const double q = floor(fa * (1.0 / fb));
+                    const double bq = fb * q;
+                    res = f64_bits(fa - bq);
+                }
+                break;
+            }
+            case D_FLOORDIV_I:
+            case D_MOD_I: {
+                // polars-utils/src/floor_divmod.rs: floor division, remainder
+                // with the divisor's sign; x / 0 -> null (arithmetic/signed.rs:35)
+                if (b == 0) {
+                    ok = false;
+                    break;
+                }
+                uint64_t q, rm;
+                if (arg == 1) {
+                    q = a / b;
+                    rm = a % b;
+                } else {
+                    const int64_t x = (int64_t)a, y = (int64_t)b;
+                    if (x == INT64_MIN && y == -1) {
+                        q = (uint64_t)INT64_MIN;
+                        rm = 0;
+                    } else {
+                        int64_t qq = x / y, rr = x % y;
+                        if (rr != 0 && ((x < 0) != (y < 0))) {
+                            qq -= 1;
+                            rr += y;
+                        }
+                        q = (uint64_t)qq;
+                        rm = (uint64_t)rr;
+                    }
+                }
+                res = op == D_FLOORDIV_I ? q : rm;
+                break;
+            }
+            case D_EQ_U: case D_NE_U: case D_LT_U: case D_LE_U: case D_GT_U: case D_GE_U: {
+                const int c = op - D_EQ_U;
+                res = (c == 0 ? a == b : c == 1 ? a != b : c == 2 ? a < b : c == 3 ? a <= b : c == 4 ? a > b : a >= b)
+                          ? 1ull : 0ull;
+                break;
+            }
+            case D_BAND: res = a & b; break;
+            case D_BOR: res = a | b; break;
+            case D_BXOR: res = a ^ b; break;
+            case D_XOR: res = (a ^ b) & 1ull; break;
+            case D_FILL_NULL:
+                res = va ? a : b;
+                ok = va | vb;
+                break;
             case D_EQ_F: case D_NE_F: case D_LT_F: case D_LE_F: case D_GT_F: case D_GE_F:
                 res = cmp_f(op - D_EQ_F, as_f64(a), as_f64(b)) ? 1ull : 0ull;
                 break;

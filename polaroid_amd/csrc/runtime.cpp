@@ -5,6 +5,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <algorithm>
+#include <cmath>
+#include <cstdint>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -174,19 +176,146 @@ int make_owned_string_column(plgpu_column* out, int64_t length, int64_t bytes, b
 }
 
 // ------------------------------------------------------ program lowering
+// Every operand gets polars' static type: binary operands are coerced to
+// their supertype (polars-core/src/utils/supertype.rs) before the op, and
+// integer results wrap at the supertype's width.  LIT_I64 / LIT_F64 are
+// dynamic literals (UnknownKind::Int / Float): they take the type the other
+// operand's supertype rule gives them, and their immediate is rewritten in
+// that type (a float literal against a Float32 column is rounded to f32).
 namespace {
-enum Ty { TB = 1, TI = 2, TF = 3 };
+constexpr int TY_LIT_INT = 100, TY_LIT_FLOAT = 101, TY_NULL = 102;
 
-int col_ty(int32_t dt) {
-    switch (dt) {
-    case PLGPU_BOOL: return TB;
-    case PLGPU_I32:
-    case PLGPU_I64:
-    case PLGPU_U32: return TI;
-    case PLGPU_F64: return TF;
-    default: return 0;
+bool is_int(int t) { return dtype_is_int(t); }
+bool is_uint(int t) { return t == PLGPU_U8 || t == PLGPU_U16 || t == PLGPU_U32 || t == PLGPU_U64; }
+bool is_float(int t) { return t == PLGPU_F32 || t == PLGPU_F64; }
+int int_bits(int t) { return dtype_bytes(t) * 8; }
+int sint_of_bits(int b) { return b <= 8 ? PLGPU_I8 : b <= 16 ? PLGPU_I16 : b <= 32 ? PLGPU_I32 : PLGPU_I64; }
+int uint_of_bits(int b) { return b <= 8 ? PLGPU_U8 : b <= 16 ? PLGPU_U16 : b <= 32 ? PLGPU_U32 : PLGPU_U64; }
+
+// supertype of two concrete numeric / Boolean types (supertype.rs:146); 0 = none
+int supertype(int a, int b) {
+    if (a == b) return a;
+    if (a == PLGPU_BOOL) return (is_int(b) || is_float(b)) ? b : 0;
+    if (b == PLGPU_BOOL) return (is_int(a) || is_float(a)) ? a : 0;
+    if (is_float(a) || is_float(b)) {
+        if (is_float(a) && is_float(b)) return PLGPU_F64;
+        const int f = is_float(a) ? a : b, i = is_float(a) ? b : a;
+        if (f == PLGPU_F64) return PLGPU_F64;
+        return int_bits(i) <= 16 ? PLGPU_F32 : PLGPU_F64;  // Int8/16, UInt8/16 + Float32 -> Float32
     }
+    const bool ua = is_uint(a), ub = is_uint(b);
+    if (ua == ub) return int_bits(a) >= int_bits(b) ? a : b;
+    const int s = ua ? b : a, u = ua ? a : b;
+    if (u == PLGPU_U64) return PLGPU_F64;  // "follow numpy"
+    if (int_bits(u) < int_bits(s)) return s;
+    return sint_of_bits(2 * int_bits(u));
 }
+
+// smallest type holding the dynamic int v (materialize_smallest_dyn_int /
+// materialize_dyn_int_pos)
+int smallest_int(int64_t v, bool prefer_unsigned) {
+    if (prefer_unsigned && v >= 0)
+        return v <= 255 ? PLGPU_U8 : v <= 65535 ? PLGPU_U16 : v <= 4294967295ll ? PLGPU_U32 : PLGPU_U64;
+    if (v >= -128 && v <= 127) return PLGPU_I8;
+    if (v >= -32768 && v <= 32767) return PLGPU_I16;
+    if (v >= INT32_MIN && v <= INT32_MAX) return PLGPU_I32;
+    return PLGPU_I64;
+}
+
+uint64_t bits_of(double d) {
+    uint64_t u;
+    std::memcpy(&u, &d, 8);
+    return u;
+}
+double dbl_of(uint64_t u) {
+    double d;
+    std::memcpy(&d, &u, 8);
+    return d;
+}
+
+struct Ent {
+    int ty;          // dtype code, or TY_LIT_INT / TY_LIT_FLOAT / TY_NULL
+    int lit_pos;     // index of the D_LIT / D_NULL that pushed a pending literal, else -1
+    bool scalar;     // a literal or an expression of literals (broadcast scalar)
+    int64_t ival;
+    double fval;
+};
+
+struct Lowering {
+    std::vector<Ent> st;
+    std::vector<DevInstr> code;
+
+    void emit(int32_t op, int32_t arg = 0, uint64_t imm = 0) {
+        DevInstr d;
+        d.op = op;
+        d.arg = arg;
+        d.imm = imm;
+        code.push_back(d);
+    }
+    static bool pending(const Ent& e) { return e.ty == TY_LIT_INT || e.ty == TY_LIT_FLOAT || e.ty == TY_NULL; }
+
+    // A dynamic literal takes the type `t`: rewrite its immediate in place.
+    void settle(Ent& e, int t) {
+        if (!pending(e)) return;
+        DevInstr& d = code[e.lit_pos];
+        if (e.ty == TY_LIT_INT) {
+            if (is_float(t)) d.imm = bits_of(t == PLGPU_F32 ? (double)(float)e.ival : (double)e.ival);
+            else if (t == PLGPU_BOOL) d.imm = e.ival != 0;
+            else d.imm = (uint64_t)e.ival;
+        } else if (e.ty == TY_LIT_FLOAT) {
+            d.imm = bits_of(t == PLGPU_F32 ? (double)(float)e.fval : e.fval);
+        }
+        e.ty = t;
+        e.lit_pos = -1;
+    }
+
+    // Type a dynamic literal takes next to an operand of type t.
+    static int lit_join(const Ent& lit, int t) {
+        if (t == TY_NULL) return lit.ty == TY_LIT_INT ? smallest_int(lit.ival, false) : PLGPU_F64;
+        if (lit.ty == TY_NULL) return t;
+        if (lit.ty == TY_LIT_FLOAT) return is_float(t) ? t : PLGPU_F64;
+        if (is_float(t)) return t;
+        if (t == PLGPU_BOOL) return smallest_int(lit.ival, false) == PLGPU_I8 ? PLGPU_I32 : PLGPU_I64;
+        const int sm = smallest_int(lit.ival, is_uint(t));
+        if (t == PLGPU_U64 && !is_uint(sm)) return PLGPU_I64;
+        return supertype(t, sm);
+    }
+
+    // Materialize a literal on its own (Int32 / Int64 / Float64).
+    static int lit_alone(const Ent& e) {
+        if (e.ty == TY_LIT_INT) return (e.ival >= INT32_MIN && e.ival <= INT32_MAX) ? PLGPU_I32 : PLGPU_I64;
+        if (e.ty == TY_LIT_FLOAT) return PLGPU_F64;
+        return e.ty == TY_NULL ? PLGPU_BOOL : e.ty;
+    }
+
+    // Common type of two operands (0 = incompatible).
+    static int join(const Ent& a, const Ent& b) {
+        const bool pa = pending(a), pb = pending(b);
+        if (pa && pb) {
+            if (a.ty == TY_NULL && b.ty == TY_NULL) return PLGPU_BOOL;
+            if (a.ty == TY_NULL) return lit_alone(b);
+            if (b.ty == TY_NULL) return lit_alone(a);
+            if (a.ty == TY_LIT_FLOAT || b.ty == TY_LIT_FLOAT) return PLGPU_F64;
+            return supertype(lit_alone(a), lit_alone(b));
+        }
+        if (pa) return lit_join(a, b.ty);
+        if (pb) return lit_join(b, a.ty);
+        return supertype(a.ty, b.ty);
+    }
+
+    // Bring stack entry `depth` (0 = top) to type t (settle or cast).
+    void coerce(int depth, int t) {
+        Ent& e = st[st.size() - 1 - depth];
+        if (pending(e)) {
+            settle(e, t);
+            return;
+        }
+        if (e.ty == t) return;
+        emit(D_CAST, t, ((uint64_t)e.ty << 8) | (depth ? 0x10000ull : 0ull));
+        e.ty = t;
+    }
+};
+
 int cmp_index(int32_t op) {
     switch (op) {
     case PLGPU_OP_EQ: return 0;
@@ -198,11 +327,8 @@ int cmp_index(int32_t op) {
     default: return -1;
     }
 }
-uint64_t bits_of(double d) {
-    uint64_t u;
-    std::memcpy(&u, &d, 8);
-    return u;
-}
+
+bool numeric_or_bool(int t) { return t == PLGPU_BOOL || is_int(t) || is_float(t); }
 }  // namespace
 
 int lower_program(const plgpu_column* cols, int32_t ncols, const plgpu_instr* prog, int32_t n,
@@ -210,14 +336,16 @@ int lower_program(const plgpu_column* cols, int32_t ncols, const plgpu_instr* pr
     std::memset(out, 0, sizeof *out);
     if (n <= 0) return fail(PLGPU_ERR_INVALID, "empty expression program");
     if (n > PLGPU_MAX_PROGRAM) return fail(PLGPU_ERR_INVALID, "expression program too long");
-    std::vector<int> st;  // type stack
-    std::vector<DevInstr> code;
-    auto emit = [&](int32_t op, int32_t arg = 0, uint64_t imm = 0) {
-        DevInstr d;
-        d.op = op;
-        d.arg = arg;
-        d.imm = imm;
-        code.push_back(d);
+    Lowering L;
+    auto& st = L.st;
+    auto push = [&](int ty, int lit_pos, bool scalar, int64_t iv = 0, double fv = 0) {
+        Ent e;
+        e.ty = ty;
+        e.lit_pos = lit_pos;
+        e.scalar = scalar;
+        e.ival = iv;
+        e.fval = fv;
+        st.push_back(e);
     };
     for (int k = 0; k < n; ++k) {
         const plgpu_instr& in = prog[k];
@@ -225,141 +353,266 @@ int lower_program(const plgpu_column* cols, int32_t ncols, const plgpu_instr* pr
         switch (in.op) {
         case PLGPU_OP_COL: {
             if (in.arg < 0 || in.arg >= ncols) return fail(PLGPU_ERR_INVALID, "column index out of range");
-            int t = col_ty(cols[in.arg].dtype);
-            if (!t) return fail(PLGPU_ERR_SCHEMA, "unsupported column dtype in expression");
-            int32_t dop = cols[in.arg].dtype == PLGPU_F64   ? D_COL_F64
-                          : cols[in.arg].dtype == PLGPU_I64 ? D_COL_I64
-                          : cols[in.arg].dtype == PLGPU_I32 ? D_COL_I32
-                          : cols[in.arg].dtype == PLGPU_U32 ? D_COL_U32
-                                                            : D_COL_BOOL;
-            emit(dop, in.arg);
-            st.push_back(t);
+            const int t = cols[in.arg].dtype;
+            if (!numeric_or_bool(t)) return fail(PLGPU_ERR_SCHEMA, "unsupported column dtype in expression");
+            L.emit(D_COL, in.arg);
+            push(t, -1, false);
             break;
         }
-        case PLGPU_OP_LIT_F64: emit(D_LIT, 0, bits_of(in.imm.f64)); st.push_back(TF); break;
-        case PLGPU_OP_LIT_I64: emit(D_LIT, 0, (uint64_t)in.imm.i64); st.push_back(TI); break;
-        case PLGPU_OP_LIT_BOOL: emit(D_LIT, 0, in.imm.i64 ? 1ull : 0ull); st.push_back(TB); break;
+        case PLGPU_OP_LIT_F64:
+            L.emit(D_LIT, 0, bits_of(in.imm.f64));
+            push(TY_LIT_FLOAT, (int)L.code.size() - 1, true, 0, in.imm.f64);
+            break;
+        case PLGPU_OP_LIT_I64:
+            L.emit(D_LIT, 0, (uint64_t)in.imm.i64);
+            push(TY_LIT_INT, (int)L.code.size() - 1, true, in.imm.i64);
+            break;
+        case PLGPU_OP_LIT_BOOL:
+            L.emit(D_LIT, 0, in.imm.i64 ? 1ull : 0ull);
+            push(PLGPU_BOOL, -1, true);
+            break;
         case PLGPU_OP_LIT_NULL: {
-            int t = col_ty(in.arg);
-            if (!t) return fail(PLGPU_ERR_SCHEMA, "typed null literal needs a dtype");
-            emit(D_NULL);
-            st.push_back(t);
+            L.emit(D_NULL);
+            if (in.arg == 0) push(TY_NULL, (int)L.code.size() - 1, true);
+            else if (numeric_or_bool(in.arg)) push(in.arg, -1, true);
+            else return fail(PLGPU_ERR_SCHEMA, "typed null literal needs a numeric / Boolean dtype");
             break;
         }
         case PLGPU_OP_ADD:
         case PLGPU_OP_SUB:
         case PLGPU_OP_MUL:
-        case PLGPU_OP_TRUEDIV: {
+        case PLGPU_OP_TRUEDIV:
+        case PLGPU_OP_FLOORDIV:
+        case PLGPU_OP_MOD:
+        case PLGPU_OP_DIVIDE: {
             if (!need(2)) return fail(PLGPU_ERR_INVALID, "stack underflow");
-            int b = st.back(); st.pop_back();
-            int a = st.back(); st.pop_back();
-            if (a == TB || b == TB)
+            Ent a = st[st.size() - 2], b = st.back();
+            if (a.ty == PLGPU_BOOL || b.ty == PLGPU_BOOL)
                 return fail(PLGPU_ERR_INVALID, "arithmetic on Boolean is not supported");
-            bool fl = (a == TF || b == TF || in.op == PLGPU_OP_TRUEDIV);
-            if (fl) {
-                if (b == TI) emit(D_I2F_0);
-                if (a == TI) emit(D_I2F_1);
-                emit(in.op == PLGPU_OP_ADD ? D_ADD_F : in.op == PLGPU_OP_SUB ? D_SUB_F
-                     : in.op == PLGPU_OP_MUL ? D_MUL_F : D_DIV_F);
-                st.push_back(TF);
+            int t = L.join(a, b);
+            if (!t) return fail(PLGPU_ERR_SCHEMA, "arithmetic operands have no common numeric type");
+            if (t == PLGPU_BOOL) t = PLGPU_I32;  // null op null
+            const bool divide = in.op == PLGPU_OP_TRUEDIV || (in.op == PLGPU_OP_DIVIDE && is_float(t));
+            if (in.op == PLGPU_OP_TRUEDIV && !is_float(t)) t = PLGPU_F64;  // ints -> Float64
+            L.coerce(1, t);
+            L.coerce(0, t);
+            const bool bscalar = b.scalar && !a.scalar;  // x op scalar (a broadcast divisor)
+            int32_t dop;
+            bool wrap = false;
+            if (is_float(t)) {
+                switch (in.op) {
+                case PLGPU_OP_ADD: dop = D_ADD_F; break;
+                case PLGPU_OP_SUB: dop = D_SUB_F; break;
+                case PLGPU_OP_MUL: dop = D_MUL_F; break;
+                case PLGPU_OP_FLOORDIV: dop = bscalar ? D_FLOORDIV_FS : D_FLOORDIV_F; break;
+                case PLGPU_OP_MOD: dop = bscalar ? D_MOD_FS : D_MOD_F; break;
+                default: dop = bscalar ? D_DIV_FS : D_DIV_F; break;  // true / legacy division
+                }
+                (void)divide;
+                L.emit(dop, t);
             } else {
-                emit(in.op == PLGPU_OP_ADD ? D_ADD_I : in.op == PLGPU_OP_SUB ? D_SUB_I : D_MUL_I);
-                st.push_back(TI);
+                wrap = t != PLGPU_I64 && t != PLGPU_U64;
+                switch (in.op) {
+                case PLGPU_OP_ADD: L.emit(D_ADD_I, t); break;
+                case PLGPU_OP_SUB: L.emit(D_SUB_I, t); break;
+                case PLGPU_OP_MUL: L.emit(D_MUL_I, t); break;
+                case PLGPU_OP_MOD: L.emit(D_MOD_I, t == PLGPU_U64 ? 1 : 0); break;
+                default: L.emit(D_FLOORDIV_I, t == PLGPU_U64 ? 1 : 0); break;  // floor / legacy division
+                }
+                if (wrap) L.emit(D_WRAP, t);
             }
+            st.pop_back();
+            st.back().ty = t;
+            st.back().lit_pos = -1;
+            st.back().scalar = a.scalar && b.scalar;
             break;
         }
         case PLGPU_OP_NEG:
         case PLGPU_OP_ABS: {
             if (!need(1)) return fail(PLGPU_ERR_INVALID, "stack underflow");
-            int a = st.back();
-            if (a == TB) return fail(PLGPU_ERR_INVALID, "neg/abs on Boolean is not supported");
-            emit(a == TF ? (in.op == PLGPU_OP_NEG ? D_NEG_F : D_ABS_F)
-                         : (in.op == PLGPU_OP_NEG ? D_NEG_I : D_ABS_I));
+            Ent& a = st.back();
+            if (a.ty == PLGPU_BOOL) return fail(PLGPU_ERR_INVALID, "neg/abs on Boolean is not supported");
+            if (Lowering::pending(a) && a.ty != TY_NULL) {
+                // fold into the dynamic literal
+                DevInstr& d = L.code[a.lit_pos];
+                if (a.ty == TY_LIT_INT) {
+                    a.ival = in.op == PLGPU_OP_NEG ? (int64_t)(0ull - (uint64_t)a.ival)
+                                                   : (a.ival < 0 ? (int64_t)(0ull - (uint64_t)a.ival) : a.ival);
+                    d.imm = (uint64_t)a.ival;
+                } else {
+                    a.fval = in.op == PLGPU_OP_NEG ? -a.fval : std::fabs(a.fval);
+                    d.imm = bits_of(a.fval);
+                }
+                break;
+            }
+            if (a.ty == TY_NULL) L.settle(a, PLGPU_I32);
+            if (in.op == PLGPU_OP_NEG && is_uint(a.ty))  // py-polars test_neg.py:57
+                return fail(PLGPU_ERR_INVALID, "`neg` operation not supported for unsigned integer dtypes");
+            if (is_float(a.ty)) {
+                L.emit(in.op == PLGPU_OP_NEG ? D_NEG_F : D_ABS_F);
+            } else {
+                L.emit(in.op == PLGPU_OP_NEG ? D_NEG_I : D_ABS_I);
+                if (a.ty != PLGPU_I64 && a.ty != PLGPU_U64) L.emit(D_WRAP, a.ty);
+            }
             break;
         }
-        case PLGPU_OP_CAST_F64: {
+        case PLGPU_OP_CAST_F64:
+        case PLGPU_OP_CAST: {
             if (!need(1)) return fail(PLGPU_ERR_INVALID, "stack underflow");
-            if (st.back() == TB) return fail(PLGPU_ERR_INVALID, "cast Boolean -> f64 not supported");
-            if (st.back() == TI) emit(D_I2F_0);
-            st.back() = TF;
+            const int to = in.op == PLGPU_OP_CAST_F64 ? PLGPU_F64 : in.arg;
+            const bool overflowing = in.op == PLGPU_OP_CAST && (in.imm.i64 & 1);
+            if (!numeric_or_bool(to)) return fail(PLGPU_ERR_SCHEMA, "cast target must be numeric or Boolean");
+            Ent& a = st.back();
+            if (Lowering::pending(a)) {
+                // a literal cast: settle in its own materialized type, then cast
+                L.settle(a, a.ty == TY_NULL ? to : Lowering::lit_alone(a));
+            }
+            if (a.ty != to) L.emit(D_CAST, to, ((uint64_t)a.ty << 8) | (overflowing ? 1ull : 0ull));
+            a.ty = to;
             break;
         }
         case PLGPU_OP_EQ: case PLGPU_OP_NE: case PLGPU_OP_LT: case PLGPU_OP_LE: case PLGPU_OP_GT:
         case PLGPU_OP_GE: case PLGPU_OP_EQ_MISSING: case PLGPU_OP_NE_MISSING: {
             if (!need(2)) return fail(PLGPU_ERR_INVALID, "stack underflow");
-            int b = st.back(); st.pop_back();
-            int a = st.back(); st.pop_back();
-            bool missing = in.op == PLGPU_OP_EQ_MISSING || in.op == PLGPU_OP_NE_MISSING;
-            int ci = missing ? (in.op == PLGPU_OP_EQ_MISSING ? 0 : 1) : cmp_index(in.op);
-            if (a == TB || b == TB) {
-                if (a != b) return fail(PLGPU_ERR_SCHEMA, "cannot compare Boolean with numeric");
+            Ent a = st[st.size() - 2], b = st.back();
+            const bool missing = in.op == PLGPU_OP_EQ_MISSING || in.op == PLGPU_OP_NE_MISSING;
+            const int ci = missing ? (in.op == PLGPU_OP_EQ_MISSING ? 0 : 1) : cmp_index(in.op);
+            if ((a.ty == PLGPU_BOOL) != (b.ty == PLGPU_BOOL) && !Lowering::pending(a) && !Lowering::pending(b))
+                return fail(PLGPU_ERR_SCHEMA, "cannot compare Boolean with numeric");
+            int t = L.join(a, b);
+            if (!t) return fail(PLGPU_ERR_SCHEMA, "comparison operands have no common type");
+            if ((a.ty == PLGPU_BOOL || b.ty == PLGPU_BOOL)) t = PLGPU_BOOL;
+            L.coerce(1, t);
+            L.coerce(0, t);
+            if (t == PLGPU_BOOL) {
                 if (ci > 1) return fail(PLGPU_ERR_INVALID, "ordering comparison on Boolean not supported");
-                emit(missing ? (ci == 0 ? D_EQM_B : D_NEM_B) : (ci == 0 ? D_EQ_B : D_NE_B));
-            } else if (a == TF || b == TF) {
-                if (b == TI) emit(D_I2F_0);
-                if (a == TI) emit(D_I2F_1);
-                emit(missing ? (ci == 0 ? D_EQM_F : D_NEM_F) : D_EQ_F + ci);
+                L.emit(missing ? (ci == 0 ? D_EQM_B : D_NEM_B) : (ci == 0 ? D_EQ_B : D_NE_B));
+            } else if (is_float(t)) {
+                L.emit(missing ? (ci == 0 ? D_EQM_F : D_NEM_F) : D_EQ_F + ci);
+            } else if (t == PLGPU_U64) {
+                L.emit(missing ? (ci == 0 ? D_EQM_I : D_NEM_I) : D_EQ_U + ci);
             } else {
-                emit(missing ? (ci == 0 ? D_EQM_I : D_NEM_I) : D_EQ_I + ci);
+                L.emit(missing ? (ci == 0 ? D_EQM_I : D_NEM_I) : D_EQ_I + ci);
             }
-            st.push_back(TB);
+            st.pop_back();
+            st.back().ty = PLGPU_BOOL;
+            st.back().lit_pos = -1;
+            st.back().scalar = a.scalar && b.scalar;
             break;
         }
         case PLGPU_OP_AND:
-        case PLGPU_OP_OR: {
+        case PLGPU_OP_OR:
+        case PLGPU_OP_XOR: {
             if (!need(2)) return fail(PLGPU_ERR_INVALID, "stack underflow");
-            int b = st.back(); st.pop_back();
-            int a = st.back(); st.pop_back();
-            if (a != TB || b != TB) return fail(PLGPU_ERR_SCHEMA, "and/or need Boolean operands");
-            emit(in.op == PLGPU_OP_AND ? D_AND : D_OR);
-            st.push_back(TB);
+            Ent a = st[st.size() - 2], b = st.back();
+            const bool ba = a.ty == PLGPU_BOOL || a.ty == TY_NULL, bb = b.ty == PLGPU_BOOL || b.ty == TY_NULL;
+            if (ba && bb) {
+                L.coerce(1, PLGPU_BOOL);
+                L.coerce(0, PLGPU_BOOL);
+                L.emit(in.op == PLGPU_OP_AND ? D_AND : in.op == PLGPU_OP_OR ? D_OR : D_XOR);
+                st.pop_back();
+                st.back().ty = PLGPU_BOOL;
+            } else {
+                int t = L.join(a, b);
+                if (!t || !is_int(t)) return fail(PLGPU_ERR_SCHEMA, "and/or/xor need Boolean or integer operands");
+                L.coerce(1, t);
+                L.coerce(0, t);
+                L.emit(in.op == PLGPU_OP_AND ? D_BAND : in.op == PLGPU_OP_OR ? D_BOR : D_BXOR);
+                st.pop_back();
+                st.back().ty = t;
+            }
+            st.back().lit_pos = -1;
+            st.back().scalar = a.scalar && b.scalar;
+            break;
+        }
+        case PLGPU_OP_FILL_NULL: {
+            if (!need(2)) return fail(PLGPU_ERR_INVALID, "stack underflow");
+            Ent a = st[st.size() - 2], b = st.back();
+            int t = L.join(a, b);
+            if (!t) return fail(PLGPU_ERR_SCHEMA, "fill_null: value has no common type with the column");
+            L.coerce(1, t);
+            L.coerce(0, t);
+            L.emit(D_FILL_NULL);
+            st.pop_back();
+            st.back().ty = t;
+            st.back().lit_pos = -1;
+            st.back().scalar = a.scalar && b.scalar;
+            break;
+        }
+        case PLGPU_OP_IF_ELSE: {
+            if (!need(3)) return fail(PLGPU_ERR_INVALID, "stack underflow");
+            Ent c = st[st.size() - 3], a = st[st.size() - 2], b = st.back();
+            if (c.ty != PLGPU_BOOL && c.ty != TY_NULL)
+                return fail(PLGPU_ERR_SCHEMA, "when() condition must be Boolean");
+            if (Lowering::pending(c)) L.settle(st[st.size() - 3], PLGPU_BOOL);
+            int t = L.join(a, b);
+            if (!t) return fail(PLGPU_ERR_SCHEMA, "then() and otherwise() have no common type");
+            L.coerce(1, t);
+            L.coerce(0, t);
+            L.emit(D_IF_ELSE);
+            st.pop_back();
+            st.pop_back();
+            st.back().ty = t;
+            st.back().lit_pos = -1;
+            st.back().scalar = c.scalar && a.scalar && b.scalar;
             break;
         }
         case PLGPU_OP_NOT:
             if (!need(1)) return fail(PLGPU_ERR_INVALID, "stack underflow");
-            if (st.back() != TB) return fail(PLGPU_ERR_SCHEMA, "not needs a Boolean operand");
-            emit(D_NOT);
+            if (st.back().ty == TY_NULL) L.settle(st.back(), PLGPU_BOOL);
+            if (st.back().ty == PLGPU_BOOL) {
+                L.emit(D_NOT);
+            } else if (is_int(st.back().ty)) {  // bitwise not of an integer: x ^ ~0
+                L.emit(D_LIT, 0, ~0ull);
+                L.emit(D_BXOR);
+                if (st.back().ty != PLGPU_I64 && st.back().ty != PLGPU_U64) L.emit(D_WRAP, st.back().ty);
+            } else {
+                return fail(PLGPU_ERR_SCHEMA, "not needs a Boolean operand");
+            }
             break;
         case PLGPU_OP_IS_NULL:
         case PLGPU_OP_IS_NOT_NULL:
             if (!need(1)) return fail(PLGPU_ERR_INVALID, "stack underflow");
-            emit(in.op == PLGPU_OP_IS_NULL ? D_ISNULL : D_ISNOTNULL);
-            st.back() = TB;
+            if (Lowering::pending(st.back())) L.settle(st.back(), Lowering::lit_alone(st.back()));
+            L.emit(in.op == PLGPU_OP_IS_NULL ? D_ISNULL : D_ISNOTNULL);
+            st.back().ty = PLGPU_BOOL;
             break;
         case PLGPU_OP_IS_NAN:
         case PLGPU_OP_IS_FINITE:
             if (!need(1)) return fail(PLGPU_ERR_INVALID, "stack underflow");
-            if (st.back() != TF)
+            if (st.back().ty == TY_LIT_FLOAT) L.settle(st.back(), PLGPU_F64);
+            if (!is_float(st.back().ty))
                 return fail(PLGPU_ERR_INVALID, "is_nan/is_finite operation not supported for non-float dtype");
-            emit(in.op == PLGPU_OP_IS_NAN ? D_ISNAN_F : D_ISFINITE_F);
-            st.back() = TB;
+            L.emit(in.op == PLGPU_OP_IS_NAN ? D_ISNAN_F : D_ISFINITE_F);
+            st.back().ty = PLGPU_BOOL;
             break;
         default: return fail(PLGPU_ERR_INVALID, "unknown opcode " + std::to_string(in.op));
         }
         if (st.size() > PLGPU_MAX_STACK) return fail(PLGPU_ERR_INVALID, "expression stack too deep");
-        if ((int)code.size() > PLGPU_MAX_PROGRAM) return fail(PLGPU_ERR_INVALID, "lowered program too long");
+        if ((int)L.code.size() > PLGPU_MAX_PROGRAM) return fail(PLGPU_ERR_INVALID, "lowered program too long");
     }
     if (st.size() != 1) return fail(PLGPU_ERR_INVALID, "program must leave exactly one value");
+    if (Lowering::pending(st[0])) L.settle(st[0], Lowering::lit_alone(st[0]));
+    const auto& code = L.code;
     out->n = (int32_t)code.size();
     for (size_t i = 0; i < code.size(); ++i) out->code[i] = code[i];
-    out->out_dtype = st[0] == TB ? PLGPU_BOOL : st[0] == TI ? PLGPU_I64 : PLGPU_F64;
-    // Fast path detection: exactly [COL c, LIT x, CMP] with matching types.
-    if (n == 3 && prog[0].op == PLGPU_OP_COL && cmp_index(prog[2].op) >= 0 &&
-        (prog[1].op == PLGPU_OP_LIT_F64 || prog[1].op == PLGPU_OP_LIT_I64)) {
-        int ct = col_ty(cols[prog[0].arg].dtype);
-        if (ct == TF) {
+    out->out_dtype = st[0].ty;
+    // Fast path: the lowered program is exactly [COL c, LIT x, CMP] (no
+    // casts): the predicate compares the register form with x directly.
+    if (code.size() == 3 && code[0].op == D_COL && code[1].op == D_LIT) {
+        const int op = code[2].op;
+        if (op >= D_EQ_F && op <= D_GE_F) {
             out->simple = 1;
             out->simple_isf = 1;
-            double v = prog[1].op == PLGPU_OP_LIT_F64 ? prog[1].imm.f64 : (double)prog[1].imm.i64;
-            out->simple_imm = bits_of(v);
-        } else if (ct == TI && prog[1].op == PLGPU_OP_LIT_I64) {
+            out->simple_op = op - D_EQ_F;
+        } else if (op >= D_EQ_I && op <= D_GE_I) {
             out->simple = 1;
             out->simple_isf = 0;
-            out->simple_imm = (uint64_t)prog[1].imm.i64;
+            out->simple_op = op - D_EQ_I;
         }
         if (out->simple) {
-            out->simple_col = prog[0].arg;
-            out->simple_op = cmp_index(prog[2].op);
+            out->simple_col = code[0].arg;
+            out->simple_imm = code[1].imm;
         }
     }
     return PLGPU_OK;
@@ -418,6 +671,16 @@ PLGPU_API int plgpu_memcpy_d2h(void* dst, const void* src, size_t bytes, void* s
 
 PLGPU_API int plgpu_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream) {
     PLGPU_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, as_stream(stream)));
+    return PLGPU_OK;
+}
+
+PLGPU_API int plgpu_expr_dtype(const plgpu_column* cols, int32_t ncols, const plgpu_instr* program, int32_t n_instr,
+                               int32_t* out_dtype) {
+    if (out_dtype == nullptr || (ncols > 0 && cols == nullptr)) return fail(PLGPU_ERR_INVALID, "NULL argument");
+    DevProgram dp;
+    const int rc = lower_program(cols, ncols, program, n_instr, &dp);
+    if (rc) return rc;
+    *out_dtype = dp.out_dtype;
     return PLGPU_OK;
 }
 

@@ -134,7 +134,8 @@ __global__ __launch_bounds__(256) void sh_gather_kernel(DevCol c, const uint32_t
         const int64_t r = idx ? (int64_t)idx[o] : o;
         if (EB == 8) ((uint64_t*)dst)[o] = ((const uint64_t*)c.values)[c.offset + r];
         else if (EB == 4) ((uint32_t*)dst)[o] = ((const uint32_t*)c.values)[c.offset + r];
-        else ((uint8_t*)dst)[o] = (uint8_t)dev_load(c, r);
+        else if (EB == 2) ((uint16_t*)dst)[o] = ((const uint16_t*)c.values)[c.offset + r];
+        else ((uint8_t*)dst)[o] = (uint8_t)dev_load(c, r);  // 1-byte ints, Booleans as 0 / 1
         if (dvalid) dvalid[o] = dev_valid(c, r) ? 1 : 0;
     }
 }
@@ -197,8 +198,8 @@ PLGPU_API int plgpu_hash_partition(const plgpu_column* keys, int32_t nkeys, int3
     const int64_t n = keys[0].length;
     for (int i = 0; i < nkeys; ++i) {
         const int32_t dt = keys[i].dtype;
-        if (dt != PLGPU_I64 && dt != PLGPU_I32 && dt != PLGPU_U32 && dt != PLGPU_F64 && dt != PLGPU_BOOL)
-            return fail(PLGPU_ERR_SCHEMA, "partition keys must be Int64, Int32, UInt32, Float64 or Boolean");
+        if (!dtype_is_int(dt) && !dtype_is_float(dt) && dt != PLGPU_BOOL)
+            return fail(PLGPU_ERR_SCHEMA, "partition keys must be integer, float or Boolean columns");
         if (keys[i].length != n) return fail(PLGPU_ERR_SHAPE, "partition key columns must have equal lengths");
         k.c[i] = sh_dev(keys[i]);
     }
@@ -272,12 +273,12 @@ PLGPU_API int plgpu_gather_rows(const plgpu_column* cols, int32_t ncols, const p
     for (int i = 0; i < ncols; ++i) {
         const DevCol c = sh_dev(cols[i]);
         uint8_t* dv = dst_valid ? dst_valid[i] : nullptr;
-        switch (cols[i].dtype) {
-        case PLGPU_I64:
-        case PLGPU_F64: sh_gather_kernel<8><<<g, 256, 0, s>>>(c, ix, n, dst_values[i], dv); break;
-        case PLGPU_I32:
-        case PLGPU_U32: sh_gather_kernel<4><<<g, 256, 0, s>>>(c, ix, n, dst_values[i], dv); break;
-        case PLGPU_BOOL: sh_gather_kernel<1><<<g, 256, 0, s>>>(c, ix, n, dst_values[i], dv); break;
+        const int eb = cols[i].dtype == PLGPU_BOOL ? 1 : dtype_bytes(cols[i].dtype);
+        switch (eb) {
+        case 8: sh_gather_kernel<8><<<g, 256, 0, s>>>(c, ix, n, dst_values[i], dv); break;
+        case 4: sh_gather_kernel<4><<<g, 256, 0, s>>>(c, ix, n, dst_values[i], dv); break;
+        case 2: sh_gather_kernel<2><<<g, 256, 0, s>>>(c, ix, n, dst_values[i], dv); break;
+        case 1: sh_gather_kernel<1><<<g, 256, 0, s>>>(c, ix, n, dst_values[i], dv); break;
         default: return fail(PLGPU_ERR_SCHEMA, "unsupported column dtype");
         }
     }

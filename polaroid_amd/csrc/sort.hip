@@ -35,16 +35,16 @@ constexpr int kSrtTile = kSrtThreads * kSrtPer;  // 4096 codes per tile
 __device__ __forceinline__ uint64_t sort_code(const DevCol& c, int64_t r, bool descending) {
     uint64_t b = dev_load(c, r);
     uint64_t k;
-    if (c.dtype == PLGPU_F64) {
+    if (c.dtype == PLGPU_F64 || c.dtype == PLGPU_F32) {  // Float32 in register form (f64 bits)
         if ((b & 0x7fffffffffffffffull) == 0) b = 0;                      // -0.0 == 0.0
         else if ((b & 0x7fffffffffffffffull) > 0x7ff0000000000000ull) b = 0x7ff8000000000000ull;  // one NaN
         k = ord_f64(b);
-    } else if (c.dtype == PLGPU_U32) {
+    } else if (c.dtype == PLGPU_U8 || c.dtype == PLGPU_U16 || c.dtype == PLGPU_U32 || c.dtype == PLGPU_U64) {
         k = b;
-    } else if (c.dtype == PLGPU_I32) {
+    } else if (c.dtype == PLGPU_I8 || c.dtype == PLGPU_I16 || c.dtype == PLGPU_I32) {
         k = (uint64_t)((uint32_t)b ^ 0x80000000u);  // upper bytes constant: their passes are skipped
     } else {
-        k = b ^ 0x8000000000000000ull;  // I64 / I32 (sign-extended)
+        k = b ^ 0x8000000000000000ull;  // I64
     }
     return descending ? ~k : k;
 }
@@ -446,8 +446,8 @@ PLGPU_API int plgpu_arg_sort(const plgpu_column* key, int32_t descending, int32_
     hipStream_t s = as_stream(stream);
     if (key == nullptr || out_idx == nullptr) return fail(PLGPU_ERR_INVALID, "NULL argument");
     std::memset(out_idx, 0, sizeof *out_idx);
-    if (key->dtype != PLGPU_I64 && key->dtype != PLGPU_I32 && key->dtype != PLGPU_U32 && key->dtype != PLGPU_F64)
-        return fail(PLGPU_ERR_SCHEMA, "sort key must be Int64 / Int32 / UInt32 / Float64");
+    if (!dtype_is_int(key->dtype) && !dtype_is_float(key->dtype))
+        return fail(PLGPU_ERR_SCHEMA, "sort key must be an integer or float column");
     const int64_t n = key->length;
     if (n >= 0xFFFFFFFFll) return fail(PLGPU_ERR_CAPACITY, "sort input exceeds the u32 index space");
     DevCol c;
@@ -539,9 +539,8 @@ PLGPU_API int plgpu_arg_sort_multi(const plgpu_column* keys_in, int32_t nkeys, c
     const int64_t n = keys_in[0].length;
     for (int j = 0; j < nkeys; ++j) {
         const int32_t dt = keys_in[j].dtype;
-        if (dt != PLGPU_I64 && dt != PLGPU_I32 && dt != PLGPU_U32 && dt != PLGPU_F64 && dt != PLGPU_BOOL &&
-            dt != PLGPU_STR)
-            return fail(PLGPU_ERR_SCHEMA, "sort keys must be Int64 / Int32 / UInt32 / Float64 / Boolean / String");
+        if (!dtype_is_int(dt) && !dtype_is_float(dt) && dt != PLGPU_BOOL && dt != PLGPU_STR)
+            return fail(PLGPU_ERR_SCHEMA, "sort keys must be integer, float, Boolean or String columns");
         if (keys_in[j].length != n) return fail(PLGPU_ERR_SHAPE, "sort columns must have equal lengths");
     }
     if (n >= 0xFFFFFFFFll) return fail(PLGPU_ERR_CAPACITY, "sort input exceeds the u32 index space");

@@ -67,7 +67,7 @@ __device__ __forceinline__ bool str_equal(const DevCol& a, int64_t ra, const Dev
 __device__ __forceinline__ uint64_t mk_word(const DevCol& c, int64_t r) {
     if (c.dtype == PLGPU_STR) return str_hash(c, r);
     uint64_t x = dev_load(c, r);
-    if (c.dtype == PLGPU_F64) {
+    if (c.dtype == PLGPU_F64 || c.dtype == PLGPU_F32) {
         if ((x & 0x7FFFFFFFFFFFFFFFull) == 0) x = 0;
         else if ((x & 0x7FFFFFFFFFFFFFFFull) > 0x7FF0000000000000ull) x = 0x7FF8000000000000ull;
     }
@@ -195,13 +195,10 @@ __global__ __launch_bounds__(256) void mk_unpack_kernel(const int64_t* __restric
         const uint64_t f = ((uint64_t)codes[g] >> pk.shift[i]) & mask;
         const bool valid = cv && !(pk.nullable[i] && f == 0);
         const int64_t v = valid ? pk.minv[i] + (int64_t)(f - (pk.nullable[i] ? 1u : 0u)) : 0;
-        switch (dtype) {
-        case PLGPU_I64: ((int64_t*)out)[g] = v; break;
-        case PLGPU_I32: ((int32_t*)out)[g] = (int32_t)v; break;
-        case PLGPU_U32: ((uint32_t*)out)[g] = (uint32_t)v; break;
-        default:
+        if (dtype == PLGPU_BOOL) {
             if (v & 1) atomicOr(&((uint32_t*)out)[g >> 5], 1u << (g & 31));
-            break;
+        } else {
+            dev_store(out, dtype, g, (uint64_t)v);
         }
         if (out_valid && valid) atomicOr(&out_valid[g >> 5], 1u << (g & 31));
     }
@@ -214,7 +211,8 @@ inline int mk_plan_pack(const MkKeys& ka, int64_t na, const MkKeys* kb, int64_t 
     std::memset(pk, 0, sizeof *pk);
     pk->n = ka.n;
     for (int i = 0; i < ka.n; ++i)
-        if (ka.c[i].dtype == PLGPU_F64 || ka.c[i].dtype == PLGPU_STR) return PLGPU_OK;
+        if (dtype_is_float(ka.c[i].dtype) || ka.c[i].dtype == PLGPU_U64 || ka.c[i].dtype == PLGPU_STR)
+            return PLGPU_OK;  // hashed path (UInt64 ranges do not fit the signed range pass)
     if (getenv("PLGPU_NO_PACK")) return PLGPU_OK;
     unsigned long long* st = nullptr;
     const size_t bytes = 2 * 3 * kMaxKeys * 8;

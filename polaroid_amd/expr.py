@@ -39,6 +39,8 @@ class Expr:
             return "len"
         if self.kind == "lit":
             return "literal"
+        if self.kind == "ternary":  # when/then/otherwise is named after its first then()
+            return self.args[1].output_name()
         return self.args[0].output_name()
 
     def meta_root_names(self) -> list[str]:
@@ -64,6 +66,12 @@ class Expr:
             return "len()"
         if self.kind == "rolling":
             return f"{self.args[0]!r}.rolling_{self.op}{self.value}"
+        if self.kind == "ternary":
+            return f"when({self.args[0]!r}).then({self.args[1]!r}).otherwise({self.args[2]!r})"
+        if self.kind == "cast":
+            return f"{self.args[0]!r}.cast({self.value!r}, {self.op})"
+        if self.kind == "fill_null":
+            return f"{self.args[0]!r}.fill_null({self.args[1]!r})"
         return f"{self.args[0]!r}.{self.op}()"
 
     def __bool__(self):
@@ -82,6 +90,12 @@ class Expr:
     def __rmul__(self, o): return self._bin("*", o, True)
     def __truediv__(self, o): return self._bin("/", o)
     def __rtruediv__(self, o): return self._bin("/", o, True)
+    def __floordiv__(self, o): return self._bin("//", o)
+    def __rfloordiv__(self, o): return self._bin("//", o, True)
+    def __mod__(self, o): return self._bin("%", o)
+    def __rmod__(self, o): return self._bin("%", o, True)
+    def __xor__(self, o): return self._bin("^", o)
+    def __rxor__(self, o): return self._bin("^", o, True)
     def __gt__(self, o): return self._bin(">", o)
     def __ge__(self, o): return self._bin(">=", o)
     def __lt__(self, o): return self._bin("<", o)
@@ -109,6 +123,9 @@ class Expr:
     def sub(self, o): return self._bin("-", o)
     def mul(self, o): return self._bin("*", o)
     def truediv(self, o): return self._bin("/", o)
+    def floordiv(self, o): return self._bin("//", o)
+    def mod(self, o): return self._bin("%", o)
+    def xor(self, o): return self._bin("^", o)
     def and_(self, o): return self._bin("&", o)
     def or_(self, o): return self._bin("|", o)
     def not_(self): return Expr("un", (self,), op="not")
@@ -123,11 +140,51 @@ class Expr:
         """String functions (Expr.str): literal pattern tests."""
         return _StrNamespace(self)
 
-    def cast(self, dtype) -> "Expr":
-        from .frame import Float64
-        if dtype is Float64 or dtype == "f64":
-            return Expr("un", (self,), op="cast_f64")
-        raise N.InvalidOperationError(f"cast to {dtype} is not supported on the GPU executor")
+    def cast(self, dtype, *, strict: bool = True, wrap_numerical: bool = False) -> "Expr":
+        """Expr.cast.  Non-strict: a value that does not fit becomes null;
+        wrap_numerical: integers wrap.  A strict cast is taken when it cannot
+        fail (widening casts); otherwise it raises (see frame._check_strict)."""
+        from .frame import Float64, DataType
+        if dtype == "f64":
+            dtype = Float64
+        if not isinstance(dtype, DataType):
+            raise N.InvalidOperationError(f"cast to {dtype!r} is not supported on the GPU executor")
+        mode = "wrap" if wrap_numerical else ("strict" if strict else "non-strict")
+        return Expr("cast", (self,), op=mode, value=dtype)
+
+    def fill_null(self, value: Any = None) -> "Expr":
+        """Expr.fill_null(value) (FunctionExpr::FillNull)."""
+        if value is None:
+            raise N.InvalidOperationError("fill_null needs a value (strategies are not supported on the GPU executor)")
+        return Expr("fill_null", (self, _to_expr(value)), op="fill_null")
+
+    def is_in(self, other: Sequence[Any], *, nulls_equal: bool = False) -> "Expr":
+        """Expr.is_in over a literal collection: x == v0 | x == v1 | ...
+        (BooleanFunction::IsIn); a null x gives null unless nulls_equal."""
+        vals = list(other)
+        if builtins.len(vals) > 15:
+            raise N.InvalidOperationError("is_in takes at most 15 literal values on the GPU executor")
+        has_null = any(v is None for v in vals)
+        vals = [v for v in vals if v is not None]
+        if nulls_equal:
+            out = self.is_null() if has_null else None
+            for v in vals:
+                t = self.eq_missing(v)
+                out = t if out is None else (out | t)
+            return out if out is not None else self.is_null() & lit(False)
+        out = None
+        for v in vals:
+            t = self == v
+            out = t if out is None else (out | t)
+        return out if out is not None else self.ne(self)  # empty: null for null x, else false
+
+    def is_between(self, lower_bound: Any, upper_bound: Any, closed: str = "both") -> "Expr":
+        """Expr.is_between (BooleanFunction::IsBetween): both / left / right / none."""
+        if closed not in ("both", "left", "right", "none"):
+            raise N.InvalidOperationError(f"invalid closed={closed!r}")
+        lo = self >= lower_bound if closed in ("both", "left") else self > lower_bound
+        hi = self <= upper_bound if closed in ("both", "right") else self < upper_bound
+        return lo & hi
 
     def alias(self, name: str) -> "Expr":
         return Expr("alias", (self,), value=name)
@@ -185,6 +242,38 @@ def _rolling(e: Expr, kind: str, window_size: int, weights, min_samples, center)
 
 def _to_expr(v: Any) -> Expr:
     return v if isinstance(v, Expr) else lit(v)
+
+
+class _Then:
+    def __init__(self, branches: list):
+        self._branches = branches
+
+    def when(self, cond: Any) -> "_When":
+        return _When(self._branches, _to_expr(cond))
+
+    def otherwise(self, value: Any) -> Expr:
+        out = _to_expr(value)
+        for cond, val in reversed(self._branches):
+            out = Expr("ternary", (cond, val, out), op="if_else")
+        return out
+
+    # a chain used without otherwise() ends in null, as in polars
+    def _finish(self) -> Expr:
+        return self.otherwise(None)
+
+
+class _When:
+    def __init__(self, branches: list, cond: Expr):
+        self._branches, self._cond = branches, cond
+
+    def then(self, value: Any) -> _Then:
+        return _Then(self._branches + [(self._cond, _to_expr(value))])
+
+
+def when(condition: Any) -> _When:
+    """pl.when(cond).then(a)[.when(c2).then(b)].otherwise(c) -> a ternary
+    expression (if_then_else; a null condition takes the otherwise branch)."""
+    return _When([], _to_expr(condition))
 
 
 def col(name: str) -> Expr:
@@ -254,7 +343,8 @@ class _StrNamespace:
 
 
 _BIN_OPS = {
-    "+": "ADD", "-": "SUB", "*": "MUL", "/": "TRUEDIV",
+    "+": "ADD", "-": "SUB", "*": "MUL", "/": "TRUEDIV", "//": "FLOORDIV", "%": "MOD", "div": "DIVIDE",
+    "^": "XOR", "fill_null": "FILL_NULL",
     ">": "GT", ">=": "GE", "<": "LT", "<=": "LE", "==": "EQ", "!=": "NE",
     "eq_missing": "EQ_MISSING", "ne_missing": "NE_MISSING", "&": "AND", "|": "OR",
 }
@@ -273,31 +363,10 @@ def lower(expr: Expr, col_index: dict[str, int], schema: dict[str, int]) -> list
     """
     out: list[tuple[int, int, Any]] = []
 
-    def dtype_of(e: Expr) -> int | None:
-        if e.kind == "col":
-            return schema.get(e.value)
-        if e.kind == "lit":
-            v = e.value
-            if isinstance(v, bool):
-                return N.BOOL
-            if isinstance(v, int):
-                return N.I64
-            if isinstance(v, float):
-                return N.F64
-            return None
-        if e.kind == "alias":
-            return dtype_of(e.args[0])
-        if e.kind == "bin":
-            if e.op in ("+", "-", "*"):
-                a, b = dtype_of(e.args[0]), dtype_of(e.args[1])
-                return N.F64 if N.F64 in (a, b) else (a or b)
-            return N.F64 if e.op == "/" else N.BOOL
-        return None
-
-    def emit(e: Expr, hint: int | None = None) -> None:
+    def emit(e: Expr) -> None:
         k = e.kind
         if k == "alias":
-            emit(e.args[0], hint)
+            emit(e.args[0])
         elif k == "col":
             if e.value not in col_index:
                 raise N.ComputeError(f'unable to find column "{e.value}"')
@@ -305,8 +374,7 @@ def lower(expr: Expr, col_index: dict[str, int], schema: dict[str, int]) -> list
         elif k == "lit":
             v = e.value
             if v is None:
-                dt = hint if hint in (N.F64, N.I64, N.BOOL) else N.I64
-                out.append((N.OP["LIT_NULL"], dt, 0))
+                out.append((N.OP["LIT_NULL"], 0, 0))  # untyped: takes the other operand's type
             elif isinstance(v, bool):
                 out.append((N.OP["LIT_BOOL"], 0, int(v)))
             elif isinstance(v, int):
@@ -317,11 +385,17 @@ def lower(expr: Expr, col_index: dict[str, int], schema: dict[str, int]) -> list
                 out.append((N.OP["LIT_F64"], 0, float(v)))
             else:
                 raise N.InvalidOperationError(f"literal of type {type(v).__name__} is not supported")
-        elif k == "bin":
-            a, b = e.args
-            emit(a, dtype_of(b))
-            emit(b, dtype_of(a))
+        elif k in ("bin", "fill_null"):
+            emit(e.args[0])
+            emit(e.args[1])
             out.append((N.OP[_BIN_OPS[e.op]], 0, 0))
+        elif k == "ternary":
+            for a in e.args:
+                emit(a)
+            out.append((N.OP["IF_ELSE"], 0, 0))
+        elif k == "cast":
+            emit(e.args[0])
+            out.append((N.OP["CAST"], e.value.code, 1 if e.op == "wrap" else 0))
         elif k == "un":
             emit(e.args[0])
             out.append((N.OP[_UN_OPS[e.op]], 0, 0))

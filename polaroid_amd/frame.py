@@ -21,42 +21,89 @@ from .expr import Expr, col, lower, to_instr_array
 
 # ------------------------------------------------------------------ dtypes
 class DataType:
+    """A column dtype.  `code` is the physical device dtype (enum
+    plgpu_dtype); the temporal types (Date, Datetime, Duration) are logical
+    types over a physical integer, as in polars."""
+
     code = 0
     name = "?"
     np_dtype: Any = None
+    logical = False
 
     def __repr__(self):
         return self.name
 
-
-class _Int64(DataType):
-    code, name, np_dtype = N.I64, "Int64", np.int64
-
-
-class _Int32(DataType):
-    code, name, np_dtype = N.I32, "Int32", np.int32
+    def physical(self) -> "DataType":
+        return _BY_CODE[self.code]
 
 
-class _UInt32(DataType):
-    code, name, np_dtype = N.U32, "UInt32", np.uint32
+def _phys(code, name, np_dtype):
+    t = type(name, (DataType,), {})
+    t.code, t.name, t.np_dtype = code, name, np_dtype
+    return t()
 
 
-class _Float64(DataType):
-    code, name, np_dtype = N.F64, "Float64", np.float64
+Int8, Int16, Int32, Int64 = (_phys(N.I8, "Int8", np.int8), _phys(N.I16, "Int16", np.int16),
+                             _phys(N.I32, "Int32", np.int32), _phys(N.I64, "Int64", np.int64))
+UInt8, UInt16, UInt32, UInt64 = (_phys(N.U8, "UInt8", np.uint8), _phys(N.U16, "UInt16", np.uint16),
+                                 _phys(N.U32, "UInt32", np.uint32), _phys(N.U64, "UInt64", np.uint64))
+Float32, Float64 = _phys(N.F32, "Float32", np.float32), _phys(N.F64, "Float64", np.float64)
+Boolean = _phys(N.BOOL, "Boolean", np.bool_)
+String = _phys(N.STR, "String", np.object_)  # UTF-8 as Arrow large_string (int64 offsets + bytes)
+_BY_CODE = {d.code: d for d in (Int8, Int16, Int32, Int64, UInt8, UInt16, UInt32, UInt64, Float32, Float64,
+                                Boolean, String)}
+INTEGER_DTYPES = (Int8, Int16, Int32, Int64, UInt8, UInt16, UInt32, UInt64)
+FLOAT_DTYPES = (Float32, Float64)
+_TIME_UNITS = ("ns", "us", "ms")
 
 
-class _Boolean(DataType):
-    code, name, np_dtype = N.BOOL, "Boolean", np.bool_
+class _Temporal(DataType):
+    logical = True
+
+    def __eq__(self, other):
+        return type(other) is type(self) and repr(other) == repr(self)
+
+    def __hash__(self):
+        return hash(repr(self))
 
 
-class _String(DataType):
-    """UTF-8 strings as Arrow large_string (int64 offsets + bytes)."""
-    code, name, np_dtype = N.STR, "String", np.object_
+class Datetime(_Temporal):
+    """Datetime(time_unit, time_zone): Int64 ticks since the Unix epoch (UTC)."""
+
+    code, np_dtype = N.I64, np.int64
+
+    def __init__(self, time_unit: str = "us", time_zone: str | None = None):
+        if time_unit not in _TIME_UNITS:
+            raise N.InvalidOperationError(f"invalid time_unit {time_unit!r}")
+        self.time_unit, self.time_zone = time_unit, time_zone
+
+    @property
+    def name(self):
+        return f"Datetime(time_unit={self.time_unit!r}, time_zone={self.time_zone!r})"
 
 
-Int64, Int32, UInt32, Float64, Boolean, String = (_Int64(), _Int32(), _UInt32(), _Float64(), _Boolean(),
-                                                  _String())
-_BY_CODE = {d.code: d for d in (Int64, Int32, UInt32, Float64, Boolean, String)}
+class Duration(_Temporal):
+    """Duration(time_unit): Int64 ticks."""
+
+    code, np_dtype = N.I64, np.int64
+
+    def __init__(self, time_unit: str = "us"):
+        if time_unit not in _TIME_UNITS:
+            raise N.InvalidOperationError(f"invalid time_unit {time_unit!r}")
+        self.time_unit = time_unit
+
+    @property
+    def name(self):
+        return f"Duration(time_unit={self.time_unit!r})"
+
+
+class _Date(_Temporal):
+    """Date: Int32 days since the Unix epoch."""
+
+    code, name, np_dtype = N.I32, "Date", np.int32
+
+
+Date = _Date()
 
 
 def _dtype_from_numpy(a: np.ndarray) -> DataType:
@@ -65,14 +112,19 @@ def _dtype_from_numpy(a: np.ndarray) -> DataType:
         return Boolean
     if k.kind in ("U", "S", "O"):
         return String
-    if k == np.int64:
-        return Int64
-    if k == np.int32:
-        return Int32
-    if k == np.uint32:
-        return UInt32
-    if k == np.float64:
-        return Float64
+    if k.kind == "M":
+        unit = np.datetime_data(k)[0]
+        if unit not in _TIME_UNITS:
+            raise N.InvalidOperationError(f"datetime64[{unit}] is not supported (ns / us / ms)")
+        return Datetime(unit)
+    if k.kind == "m":
+        unit = np.datetime_data(k)[0]
+        if unit not in _TIME_UNITS:
+            raise N.InvalidOperationError(f"timedelta64[{unit}] is not supported (ns / us / ms)")
+        return Duration(unit)
+    for d in INTEGER_DTYPES + FLOAT_DTYPES:
+        if k == d.np_dtype:
+            return d
     if np.issubdtype(k, np.integer):
         return Int64
     if np.issubdtype(k, np.floating):
@@ -113,15 +165,17 @@ class _Owned:
 class Series:
     """A named Arrow array in device memory."""
 
-    __slots__ = ("name", "_col", "_keep")
+    __slots__ = ("name", "_col", "_keep", "_logical")
 
     def __init__(self, name: str = "", values: Any = None, dtype: DataType | None = None):
         self.name = name
         self._keep: list = []
+        self._logical = dtype if dtype is not None and dtype.logical else None
         if values is None:
             values = []
         if isinstance(values, Series):
             self._col, self._keep = values._col, values._keep
+            self._logical = values._logical_dtype()
             return
         validity = None
         if isinstance(values, np.ndarray):
@@ -143,9 +197,12 @@ class Series:
             arr = np.array([fill if v is None else v for v in vals], dtype=dtype.np_dtype)
             if validity.all():
                 validity = None
+        if isinstance(arr, np.ndarray) and arr.dtype.kind in ("M", "m") and dtype is None:
+            dtype = _dtype_from_numpy(arr)
+            self._logical = dtype
         if dtype is not None and arr.dtype != dtype.np_dtype:
             arr = arr.astype(dtype.np_dtype)
-        dt = dtype or _dtype_from_numpy(arr)
+        dt = (dtype or _dtype_from_numpy(arr)).physical()
         self._upload(np.ascontiguousarray(arr), dt, validity)
 
     # construction helpers -------------------------------------------------
@@ -218,12 +275,15 @@ class Series:
         s.name = name
         arr = np.ascontiguousarray(values)
         dt = dtype or _dtype_from_numpy(arr)
+        s._logical = dt if dt.logical else None
         if dt is String:
             s._upload_strings(list(arr), None if valid is None else np.asarray(valid, dtype=bool))
             return s
+        if arr.dtype.kind in ("M", "m"):
+            arr = arr.view(np.int64)
         if arr.dtype != dt.np_dtype:
             arr = arr.astype(dt.np_dtype)
-        s._upload(arr, dt, None if valid is None else np.asarray(valid, dtype=bool))
+        s._upload(arr, dt.physical(), None if valid is None else np.asarray(valid, dtype=bool))
         return s
 
     def slice(self, offset: int, length: int | None = None) -> "Series":
@@ -233,6 +293,7 @@ class Series:
         length = n - offset if length is None else max(0, min(int(length), n - offset))
         s = Series.__new__(Series)
         s.name = self.name
+        s._logical = self._logical_dtype()
         c = N.Column.from_buffer_copy(self._col)
         c.offset = self._col.offset + offset
         c.length = length
@@ -244,12 +305,20 @@ class Series:
         return s
 
     @classmethod
-    def _from_native(cls, name: str, col_: N.Column) -> "Series":
+    def _from_native(cls, name: str, col_: N.Column, logical: DataType | None = None) -> "Series":
         s = cls.__new__(cls)
         s.name = name
         s._col = col_
         s._keep = [_Owned(col_)] if col_.release else []
+        s._logical = logical
         return s
+
+    def _logical_dtype(self) -> DataType | None:
+        return getattr(self, "_logical", None)
+
+    def _with_logical(self, logical: DataType | None) -> "Series":
+        self._logical = logical
+        return self
 
     @classmethod
     def from_device(cls, name: str, dtype: DataType, values_ptr: int, length: int,
@@ -258,6 +327,7 @@ class Series:
         """Borrow existing device buffers (e.g. torch tensors) without copying."""
         s = cls.__new__(cls)
         s.name = name
+        s._logical = dtype if dtype.logical else None
         c = N.Column()
         c.dtype = dtype.code
         c.length = int(length)
@@ -273,9 +343,10 @@ class Series:
     def from_torch(cls, name: str, tensor, validity=None) -> "Series":
         import torch
 
-        m = {torch.int64: Int64, torch.int32: Int32, torch.float64: Float64}
+        m = {torch.int64: Int64, torch.int32: Int32, torch.float64: Float64, torch.float32: Float32,
+             torch.int16: Int16, torch.int8: Int8, torch.uint8: UInt8}
         if tensor.dtype not in m or not tensor.is_cuda or not tensor.is_contiguous():
-            raise N.InvalidOperationError("from_torch needs a contiguous int64/int32/float64 GPU tensor")
+            raise N.InvalidOperationError("from_torch needs a contiguous int / float GPU tensor")
         vptr = validity.data_ptr() if validity is not None else None
         return cls.from_device(name, m[tensor.dtype], tensor.data_ptr(), tensor.numel(), vptr,
                                keepalive=(tensor, validity))
@@ -283,7 +354,7 @@ class Series:
     # properties -----------------------------------------------------------
     @property
     def dtype(self) -> DataType:
-        return _BY_CODE[self._col.dtype]
+        return self._logical_dtype() or _BY_CODE[self._col.dtype]
 
     def len(self) -> int:
         return int(self._col.length)
@@ -293,7 +364,7 @@ class Series:
 
     def alias(self, name: str) -> "Series":
         s = Series.__new__(Series)
-        s.name, s._col, s._keep = name, self._col, self._keep
+        s.name, s._col, s._keep, s._logical = name, self._col, self._keep, self._logical_dtype()
         return s
 
     # host materialisation (tests / display only) --------------------------
@@ -353,13 +424,16 @@ class Series:
             return pa.Array.from_buffers(pa.large_string(), self.len(),
                                          [vb, pa.py_buffer(offs.tobytes()), pa.py_buffer(data.tobytes())],
                                          null_count=int((~valid).sum()))
-        t = {"Int64": pa.int64(), "Int32": pa.int32(), "UInt32": pa.uint32(), "Float64": pa.float64(),
-             "Boolean": pa.bool_()}[self.dtype.name]
+        phys = _BY_CODE[self._col.dtype]
         vals = self.to_numpy()
         valid = self.validity_numpy()
-        return pa.array(vals, type=t, mask=None if valid.all() else ~valid)
+        arr = pa.array(vals, type=_ARROW_OF[phys.name], mask=None if valid.all() else ~valid)
+        lg = self._logical_dtype()
+        return arr.view(_arrow_logical(lg)) if lg is not None else arr
 
     def to_list(self) -> list:
+        if self._logical_dtype() is not None:
+            return self.to_arrow().to_pylist()
         vals = self.to_numpy().tolist()
         valid = self.validity_numpy()
         return [v if ok else None for v, ok in zip(vals, valid)]
@@ -384,17 +458,45 @@ class Series:
     def gather(self, idx: "Series") -> "Series":
         out = (N.Column * 1)()
         N.check(N.lib().plgpu_gather((N.Column * 1)(self._col), 1, C.byref(idx._col), out, None))
-        return Series._from_native(self.name, out[0])
+        return Series._from_native(self.name, out[0], self._logical_dtype())
 
     def sort(self, *, descending: bool = False, nulls_last: bool = False) -> "Series":
         return self.gather(self.arg_sort(descending=descending, nulls_last=nulls_last))
 
+    def _cast_to(self, dtype: DataType) -> "Series":
+        """Non-strict cast on the device (plgpu_eval of one CAST)."""
+        return _eval(Expr("cast", (col(self.name),), op="non-strict", value=dtype),
+                     DataFrame([self])).alias(self.name)._with_logical(None)
+
     def _rolling(self, kind: int, window_size: int, min_samples: int | None, center: bool) -> "Series":
+        """Fixed windows over Int32 / Int64 / Float64 on the device; the other
+        dtypes the way polars-time's rolling dispatch takes them
+        (rolling_window/dispatch.rs:228): rolling_sum of Int8 / Int16 / UInt8 /
+        UInt16 sums as Int64, means of integers are Float64; Float32 runs as
+        Float64 and is rounded back; min / max keep the dtype."""
+        lg = self._logical_dtype()
+        is_sum_mean = kind in (N.ROLLING["sum"], N.ROLLING["mean"])
+        if lg is not None and is_sum_mean and not (kind == N.ROLLING["sum"] and isinstance(lg, Duration)):
+            raise N.InvalidOperationError(f"rolling sum / mean of a {lg} column is not supported")
+        phys = _BY_CODE[self._col.dtype]
+        src, back = self, None
+        if phys is UInt32 and kind == N.ROLLING["sum"]:
+            raise N.InvalidOperationError("rolling_sum over UInt32 (wrapping at 32 bits) is not supported")
+        if phys in (Int8, Int16, UInt8, UInt16, UInt32):
+            src = self._cast_to(Int64)
+            back = None if is_sum_mean else phys
+        elif phys is Float32:
+            src, back = self._cast_to(Float64), Float32
+        elif phys is UInt64:
+            raise N.InvalidOperationError("rolling windows over UInt64 are not supported on the GPU executor")
         out = N.Column()
         ms = window_size if min_samples is None else min_samples
-        N.check(N.lib().plgpu_rolling(C.byref(self._col), kind, int(window_size), int(ms), int(center),
+        N.check(N.lib().plgpu_rolling(C.byref(src._col), kind, int(window_size), int(ms), int(center),
                                       C.byref(out), None))
-        return Series._from_native(self.name, out)
+        res = Series._from_native(self.name, out)
+        if back is not None:
+            res = res._cast_to(back)
+        return res._with_logical(lg if not is_sum_mean or isinstance(lg, Duration) else None)
 
     def rolling_sum(self, window_size: int, weights=None, *, min_samples: int | None = None,
                     center: bool = False) -> "Series":
@@ -427,18 +529,53 @@ class Series:
         cols = (N.Column * 1)(self._col)
         m = mask._col
         N.check(N.lib().plgpu_filter(cols, 1, C.byref(m), out, C.byref(n), None))
-        return Series._from_native(self.name, out[0])
+        return Series._from_native(self.name, out[0], self._logical_dtype())
 
 
 # ------------------------------------------------------------- ingestion
 def _arrow_physical(t) -> DataType | None:
-    """Arrow type -> physical device dtype of the path (None: unsupported)."""
+    """Arrow type -> device dtype of the path, logical for the temporal types
+    (None: unsupported)."""
     import pyarrow as pa
 
     if t in (pa.string(), pa.large_string()):
         return String
-    return {pa.int64(): Int64, pa.int32(): Int32, pa.uint32(): UInt32, pa.float64(): Float64,
-            pa.bool_(): Boolean}.get(t)
+    if pa.types.is_timestamp(t):
+        return Datetime(t.unit, t.tz) if t.unit in _TIME_UNITS else None
+    if pa.types.is_duration(t):
+        return Duration(t.unit) if t.unit in _TIME_UNITS else None
+    if t == pa.date32():
+        return Date
+    for d in INTEGER_DTYPES + FLOAT_DTYPES + (Boolean,):
+        if t == _ARROW_OF[d.name]:
+            return d
+    return None
+
+
+def _arrow_logical(dt: DataType):
+    import pyarrow as pa
+
+    if isinstance(dt, Datetime):
+        return pa.timestamp(dt.time_unit, dt.time_zone)
+    if isinstance(dt, Duration):
+        return pa.duration(dt.time_unit)
+    if dt is Date:
+        return pa.date32()
+    return _ARROW_OF[dt.name]
+
+
+class _ArrowOf(dict):
+    def __missing__(self, name):
+        import pyarrow as pa
+
+        self.update({"Int8": pa.int8(), "Int16": pa.int16(), "Int32": pa.int32(), "Int64": pa.int64(),
+                     "UInt8": pa.uint8(), "UInt16": pa.uint16(), "UInt32": pa.uint32(), "UInt64": pa.uint64(),
+                     "Float32": pa.float32(), "Float64": pa.float64(), "Boolean": pa.bool_(),
+                     "String": pa.large_string()})
+        return dict.__getitem__(self, name)
+
+
+_ARROW_OF = _ArrowOf()
 
 
 def _ingest_chunks(name: str, chunks: list, atype) -> Series:
@@ -466,6 +603,8 @@ def _ingest_chunks(name: str, chunks: list, atype) -> Series:
     dt = _arrow_physical(atype)
     if dt is None:
         raise N.InvalidOperationError(f"column {name!r}: arrow type {atype} is not supported on the GPU")
+    logical = dt if dt.logical else None
+    dt = dt.physical()
     n = builtins.sum(builtins.len(c) for c in chunks)
     nulls = builtins.sum(c.null_count for c in chunks)
     spans = []
@@ -481,7 +620,7 @@ def _ingest_chunks(name: str, chunks: list, atype) -> Series:
             spans.append((c, bufs, 0))
     col_ = N.Column()
     N.check(N.lib().plgpu_column_alloc(dt.code, n, int(nulls > 0), str_bytes, C.byref(col_), None))
-    out = Series._from_native(name, col_)
+    out = Series._from_native(name, col_, logical)
     row = 0
     for c, bufs, byte in spans:
         m = builtins.len(c)
@@ -853,6 +992,182 @@ def _lower_strings(expr: Expr, df: DataFrame) -> tuple[Expr, DataFrame]:
     return new, DataFrame(list(df._cols.values()) + extra)
 
 
+# ------------------------------------------------ typing before lowering
+_EPOCH_DT = None
+
+
+def _temporal_literal(v: Any, dt: DataType) -> int:
+    """A Python datetime / date / timedelta literal as the physical integer of
+    the temporal dtype `dt` it is compared with or added to."""
+    import datetime as _dt
+
+    per = {"ns": 1_000_000_000, "us": 1_000_000, "ms": 1_000}
+    if isinstance(v, np.datetime64) or isinstance(v, np.timedelta64):
+        unit = getattr(dt, "time_unit", "us")
+        return int(v.astype(f"{'M8' if isinstance(v, np.datetime64) else 'm8'}[{unit}]").view(np.int64))
+    if isinstance(v, _dt.datetime):
+        if not isinstance(dt, Datetime):
+            raise N.InvalidOperationError(f"cannot compare a datetime literal with {dt}")
+        if (v.tzinfo is None) != (dt.time_zone is None):
+            raise N.InvalidOperationError("datetime literal and column differ in time-zone awareness")
+        epoch = _dt.datetime(1970, 1, 1, tzinfo=_dt.timezone.utc if v.tzinfo else None)
+        d = v - epoch
+        return (d.days * 86400 + d.seconds) * per[dt.time_unit] + d.microseconds * per[dt.time_unit] // 1_000_000
+    if isinstance(v, _dt.date):
+        if dt is not Date:
+            raise N.InvalidOperationError(f"cannot compare a date literal with {dt}")
+        return (v - _dt.date(1970, 1, 1)).days
+    if isinstance(v, _dt.timedelta):
+        if not isinstance(dt, Duration):
+            raise N.InvalidOperationError(f"cannot combine a timedelta literal with {dt}")
+        return (v.days * 86400 + v.seconds) * per[dt.time_unit] + v.microseconds * per[dt.time_unit] // 1_000_000
+    raise N.InvalidOperationError(f"literal {v!r} is not a temporal value")
+
+
+def _is_temporal_lit(e: Expr) -> bool:
+    import datetime as _dt
+
+    return e.kind == "lit" and isinstance(e.value, (_dt.date, _dt.timedelta, np.datetime64, np.timedelta64))
+
+
+_CMP = ("==", "!=", "<", "<=", ">", ">=", "eq_missing", "ne_missing")
+
+
+def _can_fail(src: DataType, dst: DataType) -> bool:
+    """Whether a strict cast src -> dst can meet a value that does not fit
+    (only those fail in polars: int -> float and float -> float round)."""
+    s, d = src.physical(), dst.physical()
+    if s is d or d is Boolean or d in FLOAT_DTYPES or s is Boolean:
+        return False
+    if s in FLOAT_DTYPES:
+        return True
+    bits = {Int8: 8, Int16: 16, Int32: 32, Int64: 64, UInt8: 8, UInt16: 16, UInt32: 32, UInt64: 64}
+    su, du = s.name.startswith("U"), d.name.startswith("U")
+    if su == du:
+        return bits[d] < bits[s]
+    if su and not du:  # unsigned -> signed: needs one more bit
+        return bits[d] <= bits[s]
+    return True  # signed -> unsigned: negatives
+
+
+def _prepare(expr: Expr, df: DataFrame) -> tuple[Expr, DataType | None, list]:
+    """Resolve what the device program cannot see: temporal logical types
+    (literals become physical integers in the column's unit, results get
+    their logical dtype: Datetime - Datetime = Duration, Datetime +-
+    Duration = Datetime, Duration +- Duration = Duration; polars-core/src/
+    series/arithmetic), and strict casts that can fail (collected, checked
+    by _check_strict).  Returns (expr, logical dtype of the result, strict
+    casts)."""
+    strict: list = []
+
+    def dtype_of(e: Expr) -> DataType | None:
+        return df._cols[e.value].dtype if e.kind == "col" and e.value in df._cols else None
+
+    def go(e: Expr) -> tuple[Expr, DataType | None]:
+        k = e.kind
+        if k == "col":
+            d = dtype_of(e)
+            return e, d if d is not None and d.logical else None
+        if k == "lit":
+            if _is_temporal_lit(e):
+                return e, "lit"
+            return e, None
+        if k == "alias":
+            a, la = go(e.args[0])
+            return Expr("alias", (a,), value=e.value), la
+        if k == "bin":
+            (a, la), (b, lb) = go(e.args[0]), go(e.args[1])
+            if la is None and lb is None:
+                return Expr("bin", (a, b), op=e.op), None
+            # settle temporal literals against the other side's logical dtype
+            if la == "lit":
+                if lb in (None, "lit"):
+                    raise N.InvalidOperationError(f"temporal literal in {e!r} has no temporal operand")
+                a, la = Expr("lit", value=_temporal_literal(a.value, lb)), lb
+            if lb == "lit":
+                lit_dt = la
+                if e.op in ("+", "-") and isinstance(la, Datetime):
+                    lit_dt = Duration(la.time_unit)
+                b, lb = Expr("lit", value=_temporal_literal(b.value, lit_dt)), lit_dt
+            out = Expr("bin", (a, b), op=e.op)
+            if e.op in _CMP:
+                if la is not None and lb is not None and la != lb:
+                    raise N.InvalidOperationError(f"cannot compare {la} with {lb}")
+                return out, None
+            dur = lambda t: isinstance(t, Duration)  # noqa: E731
+            dtm = lambda t: isinstance(t, Datetime)  # noqa: E731
+            if e.op == "-" and dtm(la) and dtm(lb) and la == lb:
+                return out, Duration(la.time_unit)
+            if e.op in ("+", "-") and dtm(la) and dur(lb) and la.time_unit == lb.time_unit:
+                return out, la
+            if e.op == "+" and dur(la) and dtm(lb) and la.time_unit == lb.time_unit:
+                return out, lb
+            if e.op in ("+", "-") and dur(la) and dur(lb) and la == lb:
+                return out, la
+            raise N.InvalidOperationError(f"operation {e.op!r} on {la} and {lb} is not supported on the GPU executor")
+        if k == "un":
+            a, la = go(e.args[0])
+            if la is not None and e.op not in ("is_null", "is_not_null") and not (
+                    isinstance(la, Duration) and e.op in ("neg", "abs")):
+                raise N.InvalidOperationError(f"{e.op} of {la} is not supported on the GPU executor")
+            return Expr("un", (a,), op=e.op), (la if e.op in ("neg", "abs") else None)
+        if k == "cast":
+            a, la = go(e.args[0])
+            src = la if la is not None else _static_dtype(a, df)
+            dst = e.value
+            if src is not None and e.op == "strict" and _can_fail(src, dst):
+                strict.append((a, dst))
+            return Expr("cast", (a,), op=e.op, value=dst.physical()), (dst if dst.logical else None)
+        if k in ("fill_null", "ternary"):
+            parts = [go(x) for x in e.args]
+            vals = parts[1:] if k == "ternary" else parts
+            lgs = [lg for _, lg in vals]
+            base = next((lg for lg in lgs if lg not in (None, "lit")), None)
+            args = []
+            for (x, lg) in parts:
+                if lg == "lit":
+                    if base is None:
+                        raise N.InvalidOperationError(f"temporal literal in {e!r} has no temporal operand")
+                    x = Expr("lit", value=_temporal_literal(x.value, base))
+                args.append(x)
+            if base is not None and any(lg not in (base, "lit") and not (x.kind == "lit" and x.value is None)
+                                        for (x, lg) in vals):
+                raise N.InvalidOperationError(f"{e!r} mixes {base} with another dtype")
+            return Expr(k, tuple(args), op=e.op, value=e.value), base
+        return e, None
+
+    out, lg = go(expr)
+    if lg == "lit":
+        raise N.InvalidOperationError("a temporal literal alone is not supported on the GPU executor")
+    return out, lg, strict
+
+
+def _static_dtype(e: Expr, df: DataFrame) -> DataType | None:
+    """Dtype of a plain column expression (strict-cast checks)."""
+    if e.kind == "col" and e.value in df._cols:
+        return df._cols[e.value].dtype
+    if e.kind == "alias":
+        return _static_dtype(e.args[0], df)
+    return None
+
+
+def _check_strict(strict: list, df: DataFrame) -> None:
+    """A strict cast that met a value that does not fit raises, as polars'
+    strict cast does (InvalidOperationError 'conversion ... failed')."""
+    for inner, dst in strict:
+        probe = inner.is_not_null() & Expr("cast", (inner,), op="non-strict", value=dst.physical()).is_null()
+        used, prog, n = _program(probe, df)
+        out = (N.Column * builtins.len(used))()
+        cnt = C.c_int64(0)
+        N.check(N.lib().plgpu_filter_expr(_col_array(used), builtins.len(used), prog, n, out, C.byref(cnt), None))
+        for i in range(builtins.len(used)):
+            N.lib().plgpu_column_release(C.byref(out[i]))
+        if cnt.value:
+            raise N.InvalidOperationError(
+                f"conversion from `{_static_dtype(inner, df) or '?'}` to `{dst}` failed for {cnt.value} value(s); "
+                "set `strict=False` to allow null")
+
+
 def _program(expr: Expr, df: DataFrame) -> tuple[list[Series], Any, int]:
     names = expr.meta_root_names()
     if builtins.len(names) > N.MAX_COLS:
@@ -888,17 +1203,22 @@ def _eval(expr: Expr, df: DataFrame) -> Series:
             res = inner.sort(descending=base.value[0], nulls_last=base.value[1])
         return res.alias(expr.output_name())
     expr, df = _lower_strings(expr, df)
+    name = expr.output_name()
+    expr, logical, strict = _prepare(expr, df)
+    _check_strict(strict, df)
     used, prog, n = _program(expr, df)
     if not used:
         raise N.InvalidOperationError("literal-only expressions are not supported on the GPU executor")
     out = N.Column()
     N.check(N.lib().plgpu_eval(_col_array(used), builtins.len(used), prog, n, C.byref(out), None))
-    return Series._from_native(expr.output_name(), out)
+    return Series._from_native(name, out, logical)
 
 
 def _filter(df: DataFrame, pred: Expr) -> DataFrame:
     names = df.columns
     pred, df = _lower_strings(pred, df)
+    pred, _, strict = _prepare(pred, df)
+    _check_strict(strict, df)
     if not pred.meta_root_names():
         # Constant predicate (plan-time simplification, as polars'
         # simplify_expression does): keep every row or none.
@@ -920,7 +1240,7 @@ def _filter(df: DataFrame, pred: Expr) -> DataFrame:
         N.check(N.lib().plgpu_filter_expr(_col_array(series), builtins.len(series), prog, n, out,
                                           C.byref(cnt), None))
         for i, s in enumerate(series):
-            result.setdefault(s.name, Series._from_native(s.name, out[i]))
+            result.setdefault(s.name, Series._from_native(s.name, out[i], s._logical_dtype()))
     return DataFrame([result[nm] for nm in names])
 
 
@@ -953,7 +1273,7 @@ class _GbCall:
     the single-GPU path and polaroid_amd.distributed)."""
 
     __slots__ = ("key", "keys", "keycol", "keycols", "names", "cols", "ncols", "prog", "n_instr", "aggs", "naggs",
-                 "out_names", "_keep")
+                 "out_names", "key_logical", "out_logical", "_keep")
 
 
 def _gb_keys(key: str | tuple) -> list[str]:
@@ -984,6 +1304,10 @@ def _gb_lower(df: DataFrame, key: str | tuple, aggs: list[Expr], pred: Expr | No
             specs.append(("len", len_col))
         elif base.kind == "agg" and base.args[0].kind == "col":
             specs.append((base.op, base.args[0].value))
+            lg = df._cols[base.args[0].value]._logical_dtype() if base.args[0].value in df._cols else None
+            if lg is not None and base.op not in ("min", "max", "first", "last", "count", "len") and not (
+                    base.op == "sum" and isinstance(lg, Duration)):
+                raise N.InvalidOperationError(f"`{base.op}` of a {lg} column is not supported on the GPU executor")
         else:
             raise N.InvalidOperationError(
                 f"aggregation {e!r} is not supported on the GPU executor (need col(..).sum/mean/min/max/count/len/first/last)")
@@ -1021,6 +1345,11 @@ def _gb_lower(df: DataFrame, key: str | tuple, aggs: list[Expr], pred: Expr | No
     g.aggs = agg_arr
     g.naggs = builtins.len(specs)
     g.out_names = out_names
+    # logical dtypes of the outputs: keys keep theirs; min / max / first /
+    # last / Duration sums keep the column's, counts and lengths have none
+    g.key_logical = [df._cols[k]._logical_dtype() for k in keys]
+    g.out_logical = [df._cols[c_]._logical_dtype() if k_ in ("min", "max", "first", "last", "sum") else None
+                     for k_, c_ in specs]
     g._keep = [df._cols[nm] for nm in names] + [df._cols[k] for k in keys]
     return g
 
@@ -1028,11 +1357,11 @@ def _gb_lower(df: DataFrame, key: str | tuple, aggs: list[Expr], pred: Expr | No
 def _gb_frame(g: _GbCall, out_key, out_aggs) -> DataFrame:
     """`out_key`: one Column, or an array of len(g.keys) Columns."""
     if isinstance(out_key, N.Column):
-        series = [Series._from_native(g.key, out_key)]
+        series = [Series._from_native(g.key, out_key, g.key_logical[0])]
     else:
-        series = [Series._from_native(k, out_key[i]) for i, k in enumerate(g.keys)]
+        series = [Series._from_native(k, out_key[i], g.key_logical[i]) for i, k in enumerate(g.keys)]
     for i, nm in enumerate(g.out_names):
-        series.append(Series._from_native(nm, out_aggs[i]))
+        series.append(Series._from_native(nm, out_aggs[i], g.out_logical[i]))
     return DataFrame(series)
 
 
@@ -1113,10 +1442,12 @@ def _group_by(df: DataFrame, key: str | tuple, aggs: list[Expr], maintain_order:
         return _group_by_var(df, key, aggs, maintain_order, pred, info)
     if pred is not None:
         pred, df = _lower_strings(pred, df)
+        pred, _, strict = _prepare(pred, df)
+        _check_strict(strict, df)
     g = _gb_lower(df, key, aggs, pred)
     out_aggs = (N.Column * max(1, g.naggs))()
     gi = N.GroupByInfo()
-    if builtins.len(g.keys) == 1 and g.keycol.dtype in (N.I64, N.I32):
+    if builtins.len(g.keys) == 1 and g.keycol.dtype in (N.I64, N.I32, N.I16, N.I8, N.U8, N.U16, N.U32, N.U64):
         out_key = N.Column()
         N.check(N.lib().plgpu_group_by_agg(C.byref(g.keycol), g.cols, g.ncols, g.prog, g.n_instr, g.aggs,
                                            g.naggs, int(bool(maintain_order)), C.byref(out_key),
@@ -1149,12 +1480,12 @@ def _join(left: DataFrame, right: DataFrame, left_on: str | tuple, right_on: str
                 raise N.ComputeError(f'unable to find column "{k}"; valid columns: {df.columns}')
     lks, rks = [left._cols[k] for k in lkeys], [right._cols[k] for k in rkeys]
     for lk, rk in zip(lks, rks):
-        if lk.dtype is not rk.dtype:
+        if lk.dtype != rk.dtype:
             raise N.InvalidOperationError(
                 f"join keys must have the same dtype on the GPU executor (got {lk.dtype} and {rk.dtype})")
     li, ri = N.Column(), N.Column()
     order, val, hw = N.JOIN_ORDER[maintain_order], N.JOIN_VALIDATE[validate], N.JOIN_HOW[how]
-    if builtins.len(lks) == 1 and lks[0].dtype in (Int64, Int32, UInt32):
+    if builtins.len(lks) == 1 and lks[0].dtype.physical() in INTEGER_DTYPES:
         N.check(N.lib().plgpu_join(C.byref(lks[0]._col), C.byref(rks[0]._col), hw, int(nulls_equal), order, val,
                                    C.byref(li), C.byref(ri), None))
     else:
@@ -1169,7 +1500,7 @@ def _join(left: DataFrame, right: DataFrame, left_on: str | tuple, right_on: str
         out = (N.Column * builtins.len(names))()
         N.check(N.lib().plgpu_gather(_col_array([df._cols[n] for n in names]), builtins.len(names),
                                      C.byref(idx._col), out, None))
-        return [Series._from_native(n, out[i]) for i, n in enumerate(names)]
+        return [Series._from_native(n, out[i], df._cols[n]._logical_dtype()) for i, n in enumerate(names)]
 
     if how in ("semi", "anti"):
         return DataFrame(take(left, left.columns, lidx))
@@ -1196,7 +1527,7 @@ def _join(left: DataFrame, right: DataFrame, left_on: str | tuple, right_on: str
             i = lnames.index(lk)
             c = N.Column()
             N.check(N.lib().plgpu_coalesce(C.byref(out[i]._col), C.byref(rk._col), C.byref(c), None))
-            out[i] = Series._from_native(lk, c)
+            out[i] = Series._from_native(lk, c, out[i]._logical_dtype())
     for s in (take_right if same_right else take(right, rnames, ridx)):
         if s.name in lnames:
             s.name = s.name + suffix
@@ -1209,7 +1540,7 @@ def _sort(df: DataFrame, by: str | tuple, descending: bool | tuple, nulls_last: 
     for nm in names:
         if nm not in df._cols:
             raise N.ComputeError(f'unable to find column "{nm}"; valid columns: {df.columns}')
-    if builtins.len(names) == 1 and df._cols[names[0]].dtype not in (Boolean, String):
+    if builtins.len(names) == 1 and df._cols[names[0]].dtype.physical() not in (Boolean, String):
         idx = df._cols[names[0]].arg_sort(descending=bool(descending), nulls_last=bool(nulls_last))
     else:
         k = builtins.len(names)
@@ -1224,7 +1555,7 @@ def _sort(df: DataFrame, by: str | tuple, descending: bool | tuple, nulls_last: 
     out = (N.Column * builtins.len(names))()
     N.check(N.lib().plgpu_gather(_col_array([df._cols[n] for n in names]), builtins.len(names),
                                  C.byref(idx._col), out, None))
-    return DataFrame([Series._from_native(n, out[i]) for i, n in enumerate(names)])
+    return DataFrame([Series._from_native(n, out[i], df._cols[n]._logical_dtype()) for i, n in enumerate(names)])
 
 
 def _execute(node: tuple, info: dict | None = None) -> DataFrame:

@@ -55,6 +55,8 @@ _BINOPS: dict[str, Callable[[Expr, Expr], Expr]] = {
     "Plus": lambda a, b: a + b, "Minus": lambda a, b: a - b, "Multiply": lambda a, b: a * b,
     "TrueDivide": lambda a, b: a / b, "And": lambda a, b: a & b, "Or": lambda a, b: a | b,
     "LogicalAnd": lambda a, b: a & b, "LogicalOr": lambda a, b: a | b,
+    "FloorDivide": lambda a, b: a // b, "Modulus": lambda a, b: a % b, "Xor": lambda a, b: a ^ b,
+    "Divide": lambda a, b: a._bin("div", b),  # Operator::Divide (legacy_div)
 }
 
 _ORDERED_CMP = frozenset({"Lt", "LtEq", "Gt", "GtEq"})
@@ -73,7 +75,29 @@ def _dtype_kind(dt) -> str:
 
 
 # dtypes whose columns the GPU path takes (anything else stays on polars)
-SUPPORTED_DTYPES = frozenset({"Int64", "Int32", "UInt32", "Float64", "Boolean", "String", "Categorical", "Enum"})
+SUPPORTED_DTYPES = frozenset({"Int8", "Int16", "Int32", "Int64", "UInt8", "UInt16", "UInt32", "UInt64", "Float32",
+                              "Float64", "Boolean", "String", "Categorical", "Enum", "Datetime", "Date",
+                              "Duration"})
+
+
+def _dtype_obj(dt):
+    """A visitor dtype (its repr) -> polaroid_amd DataType, or None."""
+    from . import frame as F
+
+    kind = _dtype_kind(dt)
+    if hasattr(F, kind) and isinstance(getattr(F, kind), F.DataType) and not kind.startswith("_"):
+        return getattr(F, kind)
+    s = str(dt)
+    unit = next((u for u in ("ns", "us", "ms") if f"'{u}'" in s), None)
+    if kind == "Datetime" and unit:
+        tz = None
+        if "time_zone=" in s:
+            tzs = s.split("time_zone=", 1)[1].rstrip(")").strip()
+            tz = None if tzs in ("None", "") else tzs.strip("'\"")
+        return F.Datetime(unit, tz)
+    if kind == "Duration" and unit:
+        return F.Duration(unit)
+    return None
 
 
 class _Translator:
@@ -102,8 +126,18 @@ class _Translator:
             return col(str(e.name))
         if k == "Literal":
             v = e.value
-            if v is None or isinstance(v, (bool, int, float, str)):  # str: String comparisons
-                return lit(v)
+            import datetime as _dt
+
+            if v is None or isinstance(v, (bool, int, float, str, _dt.date, _dt.timedelta)):
+                # str: String comparisons; temporal values: converted against
+                # the column they meet (frame._prepare).  A typed literal
+                # (lit(1, dtype=Int8)) keeps its dtype through a cast.
+                out = lit(v)
+                dt = _dtype_obj(getattr(e, "dtype", None))
+                if dt is not None and isinstance(v, (int, float)) and not isinstance(v, bool) \
+                        and not _dtype_kind(getattr(e, "dtype", None)).startswith("Unknown") and not dt.logical:
+                    out = out.cast(dt, strict=False)
+                return out
             raise Unsupported(f"literal {v!r}")
         if k == "BinaryExpr":
             op = _enum_name(e.op)
@@ -113,10 +147,16 @@ class _Translator:
                 raise Unsupported("ordered comparison on an Enum column (category order)")
             return _BINOPS[op](self.expr(e.left), self.expr(e.right))
         if k == "Cast":
-            dt = str(e.dtype)
-            if dt.startswith("Float64"):
-                return self.expr(e.expr).cast("f64")
-            raise Unsupported(f"cast to {dt}")
+            # options: 0 strict, 1 non-strict, 2 overflowing (expr_nodes.rs:305)
+            dt = _dtype_obj(e.dtype)
+            if dt is None or dt is getattr(__import__("polaroid_amd.frame", fromlist=["String"]), "String"):
+                raise Unsupported(f"cast to {e.dtype}")
+            opt = int(getattr(e, "options", 0) or 0)
+            return self.expr(e.expr).cast(dt, strict=opt == 0, wrap_numerical=opt == 2)
+        if k == "Ternary":  # when(predicate).then(truthy).otherwise(falsy) (expr_nodes.rs:367)
+            from .expr import when
+
+            return when(self.expr(e.predicate)).then(self.expr(e.truthy)).otherwise(self.expr(e.falsy))
         if k == "Function":
             fd = e.function_data
             fname = _enum_name(fd[0]) if isinstance(fd, tuple) and fd else _enum_name(fd)
@@ -126,6 +166,22 @@ class _Translator:
                 return -self.expr(e.input[0])
             if fname in _BOOLFUNCS and len(e.input) == 1:
                 return _BOOLFUNCS[fname](self.expr(e.input[0]))
+            if fname == "fill_null" and len(e.input) == 2:  # FunctionExpr::FillNull (expr_nodes.rs:1191)
+                return self.expr(e.input[0]).fill_null(self.expr(e.input[1]))
+            if fname == "IsBetween" and len(e.input) == 3:  # (IsBetween, closed) (expr_nodes.rs:1112)
+                closed = str(fd[1]) if isinstance(fd, tuple) and len(fd) > 1 else "both"
+                return self.expr(e.input[0]).is_between(self.expr(e.input[1]), self.expr(e.input[2]), closed)
+            if fname == "IsIn" and len(e.input) == 2:  # (IsIn, nulls_equal) (expr_nodes.rs:1116)
+                other = self.view(e.input[1])
+                vals = getattr(other, "value", None)
+                if _name(other) != "Literal" or vals is None:
+                    raise Unsupported("is_in over a non-literal collection")
+                vals = vals.to_list() if hasattr(vals, "to_list") else list(vals)
+                nulls_equal = bool(fd[1]) if isinstance(fd, tuple) and len(fd) > 1 else False
+                try:
+                    return self.expr(e.input[0]).is_in(vals, nulls_equal=nulls_equal)
+                except N.InvalidOperationError as exc:
+                    raise Unsupported(str(exc)) from exc
             raise Unsupported(f"function {fname}")
         raise Unsupported(f"expression {k}")
 
@@ -304,15 +360,17 @@ def _empty_frame(names: list, schema: dict) -> DataFrame:
     """A zero-row frame with the scan's dtypes (to_arrow gives no batch)."""
     import pyarrow as pa
 
-    from .frame import Series
+    from .frame import Series, _arrow_logical
 
-    arrow_of = {"Int64": pa.int64(), "Int32": pa.int32(), "UInt32": pa.uint32(), "Float64": pa.float64(),
-                "Boolean": pa.bool_(), "String": pa.large_string()}
     cols = []
     for nm in names:
         kind = _dtype_kind(schema.get(nm))
-        t = arrow_of.get(kind, pa.large_string() if kind in ("Categorical", "Enum") else None)
-        if t is None:
+        dt = _dtype_obj(schema.get(nm))
+        if kind in ("Categorical", "Enum"):
+            t = pa.large_string()
+        elif dt is not None:
+            t = _arrow_logical(dt)
+        else:
             raise Unsupported(f"column {nm!r} of dtype {schema.get(nm)}")
         cols.append(Series.from_arrow(nm, pa.array([], t)))
     return DataFrame(cols)

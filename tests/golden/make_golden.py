@@ -606,6 +606,102 @@ def rolling_cases():
     return {"cases": cases}
 
 
+# ---------------------------------------------------------------------------
+# 9. Arithmetic / casts / bitwise / when-then over typed columns (round 2:
+#    dtype breadth).  Each case: typed input columns, an expression in the
+#    polaroid_amd DSL (evaluated with `pl` and `col` in scope), what the
+#    reference test asserts (`expected` values, `expected_dtype`, or
+#    `raises`), and `approx` where the test compares with assert_*_equal's
+#    default float tolerance.
+INT_DTYPES = ["Int8", "Int16", "Int32", "Int64", "UInt8", "UInt16", "UInt32", "UInt64"]
+
+
+def arith_cases():
+    cases = []
+
+    def add(name, source, cols, expr, **kw):
+        cases.append(dict(name=name, source=source, cols=cols, expr=expr, **kw))
+
+    add("test_floor_divide", "series/test_series.py:1128-1133", {"a": ["Int64", [1, 2, 3]]},
+        "col('a') // 2", expected=[0, 1, 1], expected_dtype="Int64")
+    add("test_true_divide", "series/test_series.py:1136-1141", {"a": ["Int64", [1, 2]]},
+        "col('a') / 2", expected=fx([0.5, 1.0]), expected_dtype="Float64")
+    add("test_true_divide rtruediv", "series/test_series.py:1143-1147", {"a": ["Int64", [1, 2]]},
+        "2 / col('a')", expected=fx([2.0, 1.0]), expected_dtype="Float64", expected_name="literal")
+    add("test_floor_divide (float by 0.5)", "dataframe/test_df.py:3091-3095", {"x": ["Float64", [10.4]]},
+        "col('x') // 0.5", expected=fx([10.4 // 0.5]), expected_dtype="Float64")
+    add("test_float_floor_divide", "lazyframe/test_lazyframe.py:877-882", {"x": ["Float64", [10.4]]},
+        "col('x') // 0.5", expected=fx([10.4 // 0.5]), expected_dtype="Float64")
+    add("test_integer_divide_scalar_zero_lhs_19142 //", "operations/arithmetic/test_arithmetic.py:847-849",
+        {"b": ["Int64", [1, 0]]}, "lit(0) // col('b')", expected=[0, None], expected_dtype="Int64",
+        expected_name="literal")
+    add("test_integer_divide_scalar_zero_lhs_19142 %", "operations/arithmetic/test_arithmetic.py:850",
+        {"b": ["Int64", [1, 0]]}, "lit(0) % col('b')", expected=[0, None], expected_dtype="Int64",
+        expected_name="literal")
+    add("test_neg_overflow_wrapping", "operations/arithmetic/test_neg.py:49-52", {"a": ["Int8", [-128]]},
+        "-col('a')", expected=[-128], expected_dtype="Int8")
+    add("test_neg_unsigned_int", "operations/arithmetic/test_neg.py:55-60", {"a": ["UInt8", [1, 2, 3]]},
+        "-col('a')", raises="InvalidOperationError")
+    add("test_literal_subtract_schema_13284", "operations/arithmetic/test_arithmetic.py:659-666",
+        {"a": ["UInt8", [23, 30]]}, "col('a') - lit(1)", expected=[22, 29], expected_dtype="UInt8")
+    for dt in INT_DTYPES:
+        for op, val, odt in (("//", 5, dt), ("+", 12, dt), ("-", 8, dt), ("*", 20, dt), ("/", 5.0, "Float64")):
+            add(f"test_int_operator_stability[{dt}] {op}", "operations/arithmetic/test_arithmetic.py:668-675",
+                {"a": [dt, [10]]}, f"col('a') {op} 2", expected=fx([val]), expected_dtype=odt)
+    add("test_literal_no_upcast fma", "operations/arithmetic/test_arithmetic.py:224-238",
+        {"a": ["Float32", [1.0, 2.0, 3.0]]}, "col('a') * -5 + 2", expected=fx([-3.0, -8.0, -13.0]),
+        expected_dtype="Float32")
+    add("test_literal_no_upcast fsm", "operations/arithmetic/test_arithmetic.py:224-238",
+        {"a": ["Float32", [1.0, 2.0, 3.0]]}, "2 - col('a') * 5", expected=fx([-3.0, -8.0, -13.0]),
+        expected_dtype="Float32", expected_name="literal")
+    add("test_literal_no_upcast fms", "operations/arithmetic/test_arithmetic.py:224-238",
+        {"a": ["Float32", [1.0, 2.0, 3.0]]}, "col('a') * 5 - 2", expected=fx([3.0, 8.0, 13.0]),
+        expected_dtype="Float32")
+    add("test_bitwise_6311 step 1", "operations/arithmetic/test_arithmetic.py:254-267",
+        {"col1": ["Int64", [0, 1, 2, 3]], "flag": ["Int64", [0, 0, 0, 0]]},
+        "pl.when((col('col1') < 1) | (col('col1') >= 3)).then(col('flag') | 2).otherwise(col('flag'))",
+        expected=[2, 0, 0, 2], expected_dtype="Int64", expected_name="flag")
+    add("test_bitwise_6311 step 2", "operations/arithmetic/test_arithmetic.py:254-267",
+        {"col1": ["Int64", [0, 1, 2, 3]], "flag": ["Int64", [2, 0, 0, 2]]},
+        "pl.when(col('col1') > -1).then(col('flag') | 4).otherwise(col('flag'))",
+        expected=[6, 4, 4, 6], expected_dtype="Int64", expected_name="flag")
+    add("test_modulo a % 2", "sql/test_numeric.py:38-70",
+        {"a": ["Float64", [1.5, None, 3.0, 13 / 3, 5.0]]}, "col('a') % 2",
+        expected=fx([1.5, None, 1.0, 1 / 3, 1.0]), expected_dtype="Float64", approx=True)
+    add("test_modulo b % 3", "sql/test_numeric.py:38-70", {"b": ["Int64", [6, 7, 8, 9, 10]]}, "col('b') % 3",
+        expected=[0, 1, 2, 0, 1], expected_dtype="Int64")
+    add("test_modulo MOD(c, 4)", "sql/test_numeric.py:38-70", {"c": ["Int64", [11, 12, 13, 14, 15]]},
+        "col('c') % 4", expected=[3, 0, 1, 2, 3], expected_dtype="Int64")
+    add("test_modulo MOD(d, 5.5)", "sql/test_numeric.py:38-70",
+        {"d": ["Float64", [16.5, 17.0, 18.5, None, 20.0]]}, "col('d') % 5.5",
+        expected=fx([0.0, 0.5, 2.0, None, 3.5]), expected_dtype="Float64", approx=True)
+    add("test_float_truediv_output_type f32/f32", "operations/arithmetic/test_arithmetic.py:925-931",
+        {"f32": ["Float32", [1.0]], "f64": ["Float64", [2.0]]}, "col('f32') / col('f32')",
+        expected=fx([1.0]), expected_dtype="Float32")
+    add("test_float_truediv_output_type f32/f64", "operations/arithmetic/test_arithmetic.py:932-934",
+        {"f32": ["Float32", [1.0]], "f64": ["Float64", [2.0]]}, "col('f32') / col('f64')",
+        expected=fx([0.5]), expected_dtype="Float64")
+    add("test_lit_cast_arithmetic_23677", "operations/test_cast.py:1032-1036", {"a": ["Float32", [1.0]]},
+        "col('a') / lit(1).cast(pl.Int32)", expected=fx([1.0]), expected_dtype="Float64")
+    strict_int = [(-1, "Int8", "UInt8", None), (-1, "Int16", "UInt16", None), (-1, "Int32", "UInt32", None),
+                  (-1, "Int64", "UInt64", None), (2 ** 7, "UInt8", "Int8", None), (2 ** 15, "UInt16", "Int16", None),
+                  (2 ** 31, "UInt32", "Int32", None), (2 ** 63, "UInt64", "Int64", None),
+                  (2 ** 7 - 1, "UInt8", "Int8", 2 ** 7 - 1), (2 ** 15 - 1, "UInt16", "Int16", 2 ** 15 - 1),
+                  (2 ** 31 - 1, "UInt32", "Int32", 2 ** 31 - 1), (2 ** 63 - 1, "UInt64", "Int64", 2 ** 63 - 1)]
+    for v, a, b, exp in strict_int:
+        add(f"test_cast_int[{v}-{a}-{b}]", "operations/test_cast.py:247-269", {"a": [a, [v]]},
+            f"col('a').cast(pl.{b}, strict=False)", expected=[exp], expected_dtype=b)
+        if exp is None:
+            add(f"test_strict_cast_int[{v}-{a}-{b}]", "operations/test_cast.py:206-244", {"a": [a, [v]]},
+                f"col('a').cast(pl.{b})", raises="InvalidOperationError")
+        else:
+            add(f"test_strict_cast_int[{v}-{a}-{b}]", "operations/test_cast.py:206-244", {"a": [a, [v]]},
+                f"col('a').cast(pl.{b})", expected=[exp], expected_dtype=b)
+    add("test_overflowing_cast_literals_21023", "operations/test_cast.py:747-763", {"a": ["Int64", [128]]},
+        "col('a').cast(pl.Int8, wrap_numerical=True)", expected=[-128], expected_dtype="Int8")
+    return {"cases": cases}
+
+
 def main():
     for name, obj in (("compare_total_order.json", compare_table()),
                       ("group_by_cases.json", group_by_cases()),
@@ -616,7 +712,8 @@ def main():
                       ("join_types_cases.json", join_types_cases()),
                       ("sort_cases.json", sort_cases()),
                       ("sort_multi_cases.json", sort_multi_cases()),
-                      ("rolling_cases.json", rolling_cases())):
+                      ("rolling_cases.json", rolling_cases()),
+                      ("arith_cases.json", arith_cases())):
         with open(os.path.join(HERE, name), "w") as f:
             json.dump(obj, f, indent=1, sort_keys=False)
             f.write("\n")

@@ -21,9 +21,10 @@ def test_lower_arith_and_logic():
                                      "GE", "COL", "IS_NULL", "NOT", "AND")]
 
 
-def test_null_literal_takes_other_side_dtype():
+def test_null_literal_is_untyped():
+    # the native lowering gives an untyped null the other operand's type
     prog = lower(pl.col("x") == None, {"x": 0}, {"x": N.F64})  # noqa: E711
-    assert prog[1] == (N.OP["LIT_NULL"], N.F64, 0)
+    assert prog[1] == (N.OP["LIT_NULL"], 0, 0)
 
 
 def test_reverse_operands():
