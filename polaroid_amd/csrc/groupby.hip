@@ -2352,12 +2352,27 @@ static int gb_finalize(GbRun& R, int32_t naggs, plgpu_column* out_key, plgpu_col
                     plgpu_column nc;
                     int r2 = make_owned_column(&nc, c->dtype, groups, c->validity != nullptr, s);
                     if (r2) return r2;
-                    if (dtype_bytes(c->dtype) == 8)
+                    switch (dtype_bytes(c->dtype)) {
+                    case 8:
                         gather_kernel<uint64_t><<<gg, 256, 0, s>>>((const uint64_t*)c->values, dperm,
                                                                    (uint64_t*)nc.values, groups);
-                    else
+                        break;
+                    case 4:
                         gather_kernel<uint32_t><<<gg, 256, 0, s>>>((const uint32_t*)c->values, dperm,
                                                                    (uint32_t*)nc.values, groups);
+                        break;
+                    case 2:
+                        gather_kernel<uint16_t><<<gg, 256, 0, s>>>((const uint16_t*)c->values, dperm,
+                                                                   (uint16_t*)nc.values, groups);
+                        break;
+                    case 1:
+                        gather_kernel<uint8_t><<<gg, 256, 0, s>>>((const uint8_t*)c->values, dperm,
+                                                                  (uint8_t*)nc.values, groups);
+                        break;
+                    default:
+                        plgpu_column_release(&nc);
+                        return fail(PLGPU_ERR_SCHEMA, "group order: unsupported output dtype");
+                    }
                     if (c->validity) {
                         (void)hipMemsetAsync((void*)nc.validity, 0, ((groups + 63) / 64) * 8, s);
                         gather_bits_kernel<<<gg, 256, 0, s>>>((const uint32_t*)c->validity, dperm,

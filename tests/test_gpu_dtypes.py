@@ -12,6 +12,7 @@ to f64 and then to f32 (within 1 ULP of the reference's f32 pairwise sum).
 
 import datetime as dt
 import math
+import zlib
 
 import numpy as np
 import pyarrow as pa
@@ -69,6 +70,14 @@ def check_eval(df, hosts, names, expr, n):
     got = out.to_numpy()
     if odt == N.BOOL:
         assert np.array_equal(got[wvalid], want[wvalid]), expr
+    elif odt in (N.F64, N.F32):
+        # a NaN's sign and payload are the ALU's (x86 yields the negative
+        # default NaN, gfx950 the positive one); polars' TotalOrd treats every
+        # NaN as one value, so NaNs compare by position and the rest by bits
+        g, w = got[wvalid], want[wvalid]
+        assert np.array_equal(np.isnan(g), np.isnan(w)), expr
+        keep = ~np.isnan(w)
+        assert np.array_equal(g[keep].view(np.uint8), w[keep].view(np.uint8)), expr
     else:
         assert np.array_equal(got[wvalid].view(np.uint8), want[wvalid].view(np.uint8)), expr
 
@@ -115,7 +124,7 @@ OPS = ["+", "-", "*", "/", "//", "%", "<", "<=", "==", "!=", ">", ">=", "eq_miss
 
 @pytest.mark.parametrize("a_dt,b_dt", PAIRS)
 def test_binary_ops_vs_oracle(gpu, a_dt, b_dt):
-    rng = np.random.default_rng(hash((a_dt, b_dt)) & 0xFFFF)
+    rng = np.random.default_rng(zlib.crc32(f"{a_dt},{b_dt}".encode()))
     n = 20_000
     a, b = rand(a_dt, n, rng), rand(b_dt, n, rng)
     if not b_dt.startswith("Float"):
@@ -129,6 +138,11 @@ def test_binary_ops_vs_oracle(gpu, a_dt, b_dt):
         check_eval(df, hosts, ["a", "b"], e, n)
     if a_dt in INTS and b_dt in INTS:
         for e in (col("a") & col("b"), col("a") | col("b"), col("a") ^ col("b")):
+            if {a_dt, b_dt} == {"Int64", "UInt64"}:
+                # their supertype is Float64, and polars has no bitwise ops on floats
+                with pytest.raises(pl.PolaroidError):
+                    df.select(e.alias("out"))
+                continue
             check_eval(df, hosts, ["a", "b"], e, n)
 
 
@@ -236,7 +250,7 @@ SUM_OUT = {"Int8": np.int64, "Int16": np.int64, "UInt8": np.int64, "UInt16": np.
 @pytest.mark.parametrize("kdt", INTS)
 @pytest.mark.parametrize("vdt", ["Int8", "UInt16", "Int32", "UInt64", "Float32"])
 def test_group_by_typed_vs_reference_rules(gpu, kdt, vdt):
-    rng = np.random.default_rng(hash((kdt, vdt)) & 0xFFFF)
+    rng = np.random.default_rng(zlib.crc32(f"{kdt},{vdt}".encode()))
     n = 30_000
     key = rand(kdt, n, rng, small=True)
     kv = rng.random(n) > 0.03
@@ -323,7 +337,8 @@ def test_temporal_columns_through_the_path(gpu):
     rng = np.random.default_rng(3)
     secs = rng.integers(0, 86400 * 30, n)
     ts = np.array([np.datetime64(base + dt.timedelta(seconds=int(s)), "ns") for s in secs])
-    days = (secs // 86400).astype(np.int32)
+    day0 = (base.date() - dt.date(1970, 1, 1)).days  # date32 = days since the epoch
+    days = (day0 + secs // 86400).astype(np.int32)
     dur = rng.integers(-10**9, 10**9, n).astype("timedelta64[ns]")
     sym = rng.integers(0, 7, n).astype(np.int64)
     px = rng.random(n) * 100
@@ -338,7 +353,7 @@ def test_temporal_columns_through_the_path(gpu):
     assert f.height == int(want.sum())
     assert f["ts"].to_arrow().type == pa.timestamp("ns")
     f2 = df.filter(col("day") < dt.date(2024, 1, 5))
-    assert f2.height == int((days < 4).sum())
+    assert f2.height == int((days < day0 + 4).sum())
     g = df.group_by("sym", maintain_order=True).agg(col("ts").min().alias("first_ts"), col("ts").max().alias("t1"),
                                                     col("dur").sum().alias("d"))
     assert repr(g["first_ts"].dtype).startswith("Datetime") and repr(g["d"].dtype).startswith("Duration")
@@ -359,6 +374,15 @@ def test_temporal_columns_through_the_path(gpu):
         df.group_by("sym").agg(col("ts").sum())
 
 
+def _same(g, r) -> bool:
+    """Equal as polars values: both null, both NaN, or equal."""
+    if g is None or r is None:
+        return g is None and r is None
+    if isinstance(g, float) and isinstance(r, float) and math.isnan(g):
+        return math.isnan(r)
+    return g == r
+
+
 @pytest.mark.parametrize("dt_", ["Int8", "UInt16", "Float32", "UInt32"])
 def test_rolling_typed(gpu, dt_):
     rng = np.random.default_rng(9)
@@ -368,7 +392,7 @@ def test_rolling_typed(gpu, dt_):
     wide = pl.Series.from_numpy("x", x.astype(np.float64) if dt_ == "Float32" else x.astype(np.int64))
     mn = s.rolling_min(7)
     assert repr(mn.dtype) == dt_
-    assert mn.to_list() == [None if v is None else v for v in wide.rolling_min(7).to_list()]
+    assert all(_same(g, r) for g, r in zip(mn.to_list(), wide.rolling_min(7).to_list()))
     mean = s.rolling_mean(5)
     assert repr(mean.dtype) == ("Float32" if dt_ == "Float32" else "Float64")
     if dt_ != "UInt32":
@@ -377,7 +401,7 @@ def test_rolling_typed(gpu, dt_):
         ref = wide.rolling_sum(5).to_list()
         got = sm.to_list()
         if dt_ == "Float32":
-            assert all(g is None and r is None or g == float(np.float32(r)) for g, r in zip(got, ref))
+            assert all(_same(g, None if r is None else float(np.float32(r))) for g, r in zip(got, ref))
         else:
             assert got == ref
     else:
