@@ -1430,6 +1430,9 @@ OR_EXPORT void or_rolling(const plgpu_column* c, int32_t kind, int64_t ws, int64
                 else buf[m++] = x;
             }
             v = or_fsum(buf, m);
+            /* SumWindow starts from S::zeroed() = +0.0 (rolling/sum.rs:31), so
+             * a window whose values cancel (or are all -0.0) sums to +0.0 */
+            if (v == 0.0) v = 0.0;
             free(buf);
             if (nan || (pinf && ninf)) v = NAN;
             else if (pinf) v = INFINITY;

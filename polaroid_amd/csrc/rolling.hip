@@ -110,7 +110,7 @@ __device__ double rl_exact_sum(const RlParams& p, int64_t s, int64_t e) {
             if (y == yr) hi = x;
         }
     }
-    return hi;
+    return hi == 0.0 ? 0.0 : hi;  // +0.0, as SumWindow's S::zeroed() start (sum.rs:31)
 }
 
 // Packed counts: non-null | +inf << 16 | -inf << 32 | NaN << 48 (each < 2^16).
@@ -295,116 +295,283 @@ __global__ __launch_bounds__(kRlThreads) void rl_tile_kernel(RlParams p) {
     }
 }
 
-// Small windows (w <= kSlideMaxW): a workgroup stages 4096 outputs' inputs
-// in LDS (coalesced), then each thread slides an exact fixed-point window
-// over 16 consecutive outputs: per output, the limbs of the value entering
-// are added and those of the value leaving subtracted (integer arithmetic,
-// so no drift), and the sum is rounded once.  Outputs go back through LDS
-// so the global stores are coalesced.
-constexpr int kSlideMaxW = 64;
-constexpr int kSlideRun = 8;
-constexpr int kSlideOut = kRlThreads * kSlideRun;  // 2048
+// Small windows (w <= kRwMaxW): wave-scan kernel.  A wave owns kRwOut
+// consecutive outputs.  It loads the rows their windows cover once
+// (coalesced, held in registers), finds their exponent range, and turns
+// every finite value into an exact fixed-point integer relative to the
+// smallest exponent: one int64 when the range is narrow enough that any
+// window's sum fits 63 bits (prices, volumes: a few binades), else a
+// 128-bit integer.  A wave64 prefix scan (DPP row shifts + row broadcasts)
+// gives wrapping prefix sums P; every window is P[e-1] - P[s-1], exact
+// modulo 2^64 / 2^128 and therefore exact, and it is rounded to f64 once.
+// Non-null / +inf / -inf / NaN counts run the same scan only when the
+// wave's rows hold a null or a non-finite value.  Prefixes of the last four
+// 64-row chunks sit in a per-wave LDS ring, so clipped and centred windows
+// read their two prefixes the same way.
+constexpr int kRwMaxW = 64;
+constexpr int kRwChunks = 16;              // output chunks of 64 per wave
+constexpr int kRwWaves = 4;                // waves per workgroup
+constexpr int kRwOut = 64 * kRwChunks;     // outputs per wave
+constexpr int kRwRing = 256;               // 4 chunks of prefixes
 
-struct RlAcc {
-    int64_t l0, l1, l2, isum;
-    int32_t nn, pinf, ninf, nan;
-};
-
-// Limbs of a finite value known to lie in the tile's window (zero allowed):
-// t = +-m * 2^sh split as l0 + l1 * 2^40 + l2 * 2^80 (low limbs >= 0, top
-// limb signed), branch-free.
-__device__ __forceinline__ void rl_limbs(uint64_t b, int bottom, int64_t& l0, int64_t& l1, int64_t& l2) {
-    constexpr uint64_t M40 = (1ull << 40) - 1;
-    const uint32_t ex = (uint32_t)(b >> 52) & 0x7FF;
-    const uint64_t m = (b & 0x000FFFFFFFFFFFFFull) | ((uint64_t)(ex != 0) << 52);
-    const int sh0 = (int)(ex ? ex : 1) - 1075 - bottom;
-    const uint32_t sh = sh0 < 0 ? 0u : (uint32_t)sh0;  // only zero can fall below (m == 0)
-    const int64_t sm = (int64_t)b < 0 ? -(int64_t)m : (int64_t)m;
-    l0 = sh < 40 ? (int64_t)(((uint64_t)sm << sh) & M40) : 0;
-    l1 = (int64_t)((sh <= 40 ? (uint64_t)(sm >> (40 - sh)) : ((uint64_t)sm << (sh - 40))) & M40);
-    l2 = sm >> (sh > 16 ? 80 - sh : 63);
+// DPP move of a 64-bit value (lanes without a source read 0).
+template <int CTRL, int RM = 0xf>
+__device__ __forceinline__ uint64_t dpp64(uint64_t v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, CTRL, RM, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), CTRL, RM, 0xf, false);
+    return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
 }
 
-// Correctly rounded double of (l0 + l1*2^40 + l2*2^80) * 2^bottom for limb
-// sums of at most a few thousand values (|total| < 2^126): the magnitude is
-// normalised, its top 64 bits carry a sticky bit for the rest (round to
-// odd), and one u64 -> f64 conversion rounds.  Results that would be
-// subnormal take fx_to_double.
-__device__ __forceinline__ double rl_to_double(int64_t l0, int64_t l1, int64_t l2, int bottom) {
-    const __int128 t = (__int128)l0 + ((__int128)l1 << 40) + ((__int128)l2 << 80);
-    if (t == 0) return 0.0;
-    const bool neg = t < 0;
-    unsigned __int128 u = neg ? (unsigned __int128)(-t) : (unsigned __int128)t;
-    const uint64_t hi = (uint64_t)(u >> 64);
-    const int lz = hi ? __clzll(hi) : 64 + __clzll((uint64_t)u);
-    u <<= lz;
-    const uint64_t top = (uint64_t)(u >> 64) | (((uint64_t)u) != 0 ? 1ull : 0ull);
-    const int e = 64 - lz + bottom;  // value ~= top * 2^e, leading bit at 2^(63 + e)
-    if (63 + e < -1021) {
-        uint64_t w0, w1, w2;
-        limbs_to_192(l0, l1, l2, w0, w1, w2);
-        return fx_to_double(w0, w1, w2, bottom);
+// Inclusive wave64 prefix sum, wrapping: row_shr 1/2/4/8 within rows of 16
+// lanes, then row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3).
+__device__ __forceinline__ uint64_t wave_scan64(uint64_t x) {
+    x += dpp64<0x111>(x);
+    x += dpp64<0x112>(x);
+    x += dpp64<0x114>(x);
+    x += dpp64<0x118>(x);
+    x += dpp64<0x142, 0xa>(x);
+    x += dpp64<0x143, 0xc>(x);
+    return x;
+}
+
+__device__ __forceinline__ void add128(uint64_t& lo, uint64_t& hi, uint64_t blo, uint64_t bhi) {
+    const uint64_t l = lo + blo;
+    hi = hi + bhi + (l < lo ? 1ull : 0ull);
+    lo = l;
+}
+
+__device__ __forceinline__ void wave_scan128(uint64_t& lo, uint64_t& hi) {
+#define PLGPU_SCAN_STEP(C, R)                                 \
+    {                                                         \
+        const uint64_t a = dpp64<C, R>(lo), b = dpp64<C, R>(hi); \
+        add128(lo, hi, a, b);                                 \
     }
+    PLGPU_SCAN_STEP(0x111, 0xf)
+    PLGPU_SCAN_STEP(0x112, 0xf)
+    PLGPU_SCAN_STEP(0x114, 0xf)
+    PLGPU_SCAN_STEP(0x118, 0xf)
+    PLGPU_SCAN_STEP(0x142, 0xa)
+    PLGPU_SCAN_STEP(0x143, 0xc)
+#undef PLGPU_SCAN_STEP
+}
+
+__device__ __forceinline__ uint64_t lane63(uint64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 63);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// 128-bit two's complement fixed-point value * 2^bottom -> f64, rounded once:
+// the magnitude's top 64 bits with a sticky bit for the rest, one u64 -> f64
+// conversion, an exact scaling.  Subnormal results take fx_to_double.
+__device__ __forceinline__ double i128_to_double(uint64_t lo, uint64_t hi, int bottom) {
+    const bool neg = (int64_t)hi < 0;
+    uint64_t ml = lo, mh = hi;
+    if (neg) {
+        ml = ~lo + 1;
+        mh = ~hi + (ml == 0 ? 1ull : 0ull);
+    }
+    if ((ml | mh) == 0) return 0.0;
+    const int lz = mh ? __clzll(mh) : 64 + __clzll(ml);
+    uint64_t top;
+    if (lz >= 64) top = ml << (lz - 64);
+    else if (lz == 0) top = mh | (ml != 0 ? 1ull : 0ull);
+    else top = (mh << lz) | (ml >> (64 - lz)) | ((ml << lz) != 0 ? 1ull : 0ull);
+    const int e = 64 - lz + bottom;
+    if (63 + e < -1021) return fx_to_double(lo, hi, neg ? ~0ull : 0ull, bottom);
     const double r = __builtin_ldexp((double)top, e);
     return neg ? -r : r;
 }
 
-template <bool NULLABLE>
-__device__ __forceinline__ void rl_acc(const RlParams& p, const uint64_t* vals, const uint8_t* vld, int j, int bottom,
-                                       int sign, RlAcc& a) {
-    if (NULLABLE && !vld[j]) return;
-    a.nn += sign;
-    const uint64_t b = vals[j];
-    if (p.out_int) {
-        a.isum = (int64_t)((uint64_t)a.isum + (uint64_t)(sign > 0 ? b : 0ull - b));
-        return;
-    }
-    const uint64_t ab = b & 0x7fffffffffffffffull;
-    if (ab >= 0x7ff0000000000000ull) {
-        if (ab > 0x7ff0000000000000ull) a.nan += sign;
-        else if (b >> 63) a.ninf += sign;
-        else a.pinf += sign;
-        return;
-    }
-    int64_t x0, x1, x2;
-    rl_limbs(b, bottom, x0, x1, x2);
-    if (sign > 0) {
-        a.l0 += x0;
-        a.l1 += x1;
-        a.l2 += x2;
-    } else {
-        a.l0 -= x0;
-        a.l1 -= x1;
-        a.l2 -= x2;
+// One row of a rolling input, as loaded (DT: F64 bits, I64, or I32
+// sign-extended); `tof` converts an integer to the bits of its f64 value.
+template <int DT>
+__device__ __forceinline__ uint64_t rw_load(const RlParams& p, int64_t r, bool tof) {
+    const int64_t q = p.c.offset + r;
+    if (DT == PLGPU_F64) return ((const uint64_t*)p.c.values)[q];
+    const int64_t v = DT == PLGPU_I64 ? ((const int64_t*)p.c.values)[q] : (int64_t)((const int32_t*)p.c.values)[q];
+    return tof ? f64_bits((double)v) : (uint64_t)v;
+}
+
+// Scan + emit phase of rl_wave_kernel for one number format.  MODE 0:
+// integer sums (wrapping, like SumWindow<int>); 1: int64 fixed point;
+// 2: 128-bit fixed point.  COUNTS: the wave's rows hold a null or a
+// non-finite value, so non-null / inf / NaN counts are scanned too (else a
+// window's non-null count is its length).  Straight-line per chunk: every
+// branch below is uniform and resolved at compile time or once per wave.
+template <int MODE, bool COUNTS, bool MEAN>
+__device__ __forceinline__ void rw_scan(const RlParams& p, const uint64_t (&x)[kRwChunks + 1],
+                                        const uint64_t (&vm)[kRwChunks + 1], int64_t o_first, int64_t o_end,
+                                        int64_t s_first, int tmin, uint64_t* rlo, uint64_t* rhi, uint64_t* rcn) {
+    const int lane = threadIdx.x & 63;
+    const int bottom = tmin - 1075;
+    // interior waves: every window is unclipped, [i - left, i + right)
+    const int64_t right = p.center ? (p.w + 1) / 2 : 1;
+    const int64_t left = p.w - right;
+    const bool interior = o_first - left >= 0 && o_end + right - 1 <= p.n;
+    uint64_t carry_lo = 0, carry_hi = 0, carry_cn = 0;
+#pragma unroll
+    for (int k = 0; k <= kRwChunks; ++k) {
+        const uint64_t b = x[k];
+        uint64_t flo, fhi = 0, code = 0;
+        if (MODE == 0) {
+            flo = b;
+            if (COUNTS) code = (vm[k] >> lane) & 1;
+        } else {
+            const uint64_t ab = b & 0x7fffffffffffffffull;
+            const bool fin = ab < 0x7ff0000000000000ull;
+            if (COUNTS) {
+                const bool v = (vm[k] >> lane) & 1;
+                code = !v ? 0 : (fin ? kC1 : ab > 0x7ff0000000000000ull ? kC1 + kCNan
+                                            : kC1 + ((b >> 63) ? kCNinf : kCPinf));
+            }
+            const uint32_t ex = (uint32_t)(b >> 52) & 0x7FF;
+            const uint64_t m = fin ? ((b & 0x000FFFFFFFFFFFFFull) | ((uint64_t)(ex != 0) << 52)) : 0ull;
+            const int sh0 = (int)(ex ? ex : 1) - tmin;
+            const uint32_t sh = sh0 < 0 ? 0u : (uint32_t)sh0;  // only zero lies below tmin
+            const bool neg = (b >> 63) != 0;
+            if (MODE == 1) {
+                const uint64_t t = m << sh;
+                flo = neg ? 0ull - t : t;
+            } else {
+                flo = sh < 64 ? m << sh : 0ull;
+                fhi = sh == 0 ? 0ull : sh < 64 ? m >> (64 - sh) : m << (sh - 64);
+                if (neg) {
+                    flo = ~flo + 1;
+                    fhi = ~fhi + (flo == 0 ? 1ull : 0ull);
+                }
+            }
+        }
+        const int slot = ((k & 3) << 6) | lane;
+        if (MODE == 2) {
+            wave_scan128(flo, fhi);
+            add128(flo, fhi, carry_lo, carry_hi);
+            carry_lo = lane63(flo);
+            carry_hi = lane63(fhi);
+            rhi[slot] = fhi;
+        } else {
+            flo = wave_scan64(flo) + carry_lo;
+            carry_lo = lane63(flo);
+        }
+        rlo[slot] = flo;
+        if (COUNTS) {
+            code = wave_scan64(code) + carry_cn;
+            carry_cn = lane63(code);
+            rcn[slot] = code;
+        }
+        wave_sync();
+        if (k == 0) continue;
+        // outputs of chunk q = k - 1: their prefixes lie in row chunks q-1..q+1
+        const int q = k - 1;
+        if (o_first + 64 * q >= o_end) break;
+        const int64_t i = o_first + 64 * q + lane;
+        int64_t s, e;
+        if (interior) {
+            s = i - left;
+            e = i + right;
+        } else {
+            rl_bounds(p, i, s, e);
+        }
+        const int je = (int)(e - 1 - s_first), js = (int)(s - 1 - s_first);
+        const int ie = je & (kRwRing - 1), is = js & (kRwRing - 1);
+        uint64_t slo = rlo[ie];
+        const uint64_t plo = js >= 0 ? rlo[is] : 0ull;
+        double sum = 0.0;
+        int64_t isum = 0;
+        if (MODE == 2) {
+            uint64_t shi = rhi[ie];
+            const uint64_t phi = js >= 0 ? rhi[is] : 0ull;
+            add128(slo, shi, ~plo, ~phi);
+            add128(slo, shi, 1, 0);
+            sum = i128_to_double(slo, shi, bottom);
+        } else if (MODE == 1) {
+            sum = __builtin_ldexp((double)(int64_t)(slo - plo), bottom);
+        } else {
+            isum = (int64_t)(slo - plo);
+        }
+        RlCounts c;
+        if (COUNTS) c = rl_unpack(rcn[ie] - (js >= 0 ? rcn[is] : 0ull));
+        else c = RlCounts{e - s, 0, 0, 0};
+        bool valid = i < o_end && c.nn >= p.min_periods && (!MEAN || c.nn > 0);
+        if (i < o_end) {
+            if (MODE == 0) {
+                if (p.out_int == PLGPU_I64) ((int64_t*)p.out)[i] = valid ? isum : 0;
+                else ((int32_t*)p.out)[i] = valid ? (int32_t)isum : 0;
+            } else {
+                double r = sum;
+                if (COUNTS) {
+                    if (c.nan || (c.pinf && c.ninf)) r = __builtin_nan("");
+                    else if (c.pinf) r = __builtin_inf();
+                    else if (c.ninf) r = -__builtin_inf();
+                }
+                if (MEAN) r = r / (double)c.nn;
+                ((double*)p.out)[i] = valid ? r : 0.0;
+            }
+        }
+        const uint64_t bits = __ballot(valid);
+        if (lane == 0) p.out_valid[(o_first >> 6) + q] = bits;
+        wave_sync();
     }
 }
 
-template <bool NULLABLE>
-__global__ __launch_bounds__(kRlThreads) void rl_slide_kernel(RlParams p) {
-    __shared__ uint64_t vals[kSlideOut + kSlideMaxW];
-    __shared__ uint8_t vld[NULLABLE ? kSlideOut + kSlideMaxW : 1];
-    __shared__ uint64_t outv[kSlideOut];
-    __shared__ uint64_t outm[kSlideOut / 64];
-    __shared__ uint32_t red[2];
-    const int tid = threadIdx.x;
-    const int64_t o0 = (int64_t)blockIdx.x * kSlideOut;
-    const int64_t o1 = o0 + kSlideOut < p.n ? o0 + kSlideOut : p.n;
-    int64_t lo, hi, tmp;
-    rl_bounds(p, o0, lo, tmp);
-    rl_bounds(p, o1 - 1, tmp, hi);
-    const int m = (int)(hi - lo);
-    if (tid < 2) red[tid] = 0;
-    if (tid < kSlideOut / 64) outm[tid] = 0;
-    __syncthreads();
+// A wave's outputs summed exactly one by one (values spanning more binades
+// than 128 bits hold).  Out of line, with its own copy of the parameters, so
+// the kernel's parameters never have their address taken.
+__device__ __noinline__ void rw_exact_outputs(RlParams p, int64_t o_first, int64_t o_end) {
+    const int lane = threadIdx.x & 63;
+    for (int q = 0; q < kRwChunks; ++q) {
+        const int64_t i = o_first + 64 * q + lane;
+        if (o_first + 64 * q >= o_end) break;
+        bool valid = false;
+        if (i < o_end) {
+            int64_t s, e;
+            rl_bounds(p, i, s, e);
+            RlCounts k = {0, 0, 0, 0};
+            for (int64_t r = s; r < e; ++r) rl_count(p, r, k);
+            rl_write(p, i, rl_exact_sum(p, s, e), 0, k, e - s, valid);
+        }
+        const uint64_t bits = __ballot(valid);
+        if (lane == 0) p.out_valid[(o_first >> 6) + q] = bits;
+    }
+}
+
+template <int DT, bool NULLABLE>
+__global__ __launch_bounds__(256) void rl_wave_kernel(RlParams p) {
+    __shared__ uint64_t ring_lo[kRwWaves][kRwRing];
+    __shared__ uint64_t ring_hi[kRwWaves][kRwRing];
+    __shared__ uint64_t ring_cn[kRwWaves][kRwRing];
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
+    const int64_t o_first = ((int64_t)blockIdx.x * kRwWaves + wv) * kRwOut;
+    if (o_first >= p.n) return;  // (no workgroup barriers below)
+    const int64_t o_end = o_first + kRwOut < p.n ? o_first + kRwOut : p.n;
+    int64_t s_first, tmp;
+    rl_bounds(p, o_first, s_first, tmp);
+    const bool isint = p.out_int != 0;
+
+    // 1. load the rows [s_first, s_first + 64 * (kRwChunks + 1)) into registers
+    uint64_t x[kRwChunks + 1];
+    uint64_t vm[kRwChunks + 1];
     uint32_t mx = 0, inv_mn = 0;
-    for (int j = tid; j < m; j += kRlThreads) {
-        const int64_t r = lo + j;
-        const bool v = !NULLABLE || dev_valid(p.c, r);
-        const uint64_t b = p.out_int ? dev_load(p.c, r) : rl_bits(p, r);
-        vals[j] = b;
-        if (NULLABLE) vld[j] = v;
-        if (!p.out_int && v) {
+    bool odd = false;  // a null (in range) or a non-finite value
+#pragma unroll
+    for (int k = 0; k <= kRwChunks; ++k) {
+        const int64_t r = s_first + 64 * k + lane;
+        const bool in = r < p.n;
+        const bool v = in && (!NULLABLE || dev_valid(p.c, r));
+        const uint64_t b = in ? rw_load<DT>(p, r, !isint) : 0ull;
+        vm[k] = __ballot(v);
+        x[k] = v ? b : 0ull;
+        if (NULLABLE) odd |= in && !v;
+        if (v) {
             const uint32_t ex = (uint32_t)(b >> 52) & 0x7FF;
+            odd |= ex == 0x7FF;
             if (ex != 0x7FF && (b << 1) != 0) {
                 const uint32_t e1 = ex ? ex : 1;
                 mx = e1 > mx ? e1 : mx;
@@ -412,54 +579,43 @@ __global__ __launch_bounds__(kRlThreads) void rl_slide_kernel(RlParams p) {
             }
         }
     }
-    atomicMax(&red[0], mx);
-    atomicMax(&red[1], inv_mn);
-    __syncthreads();
-    const int tmax = (int)red[0], tmin = 0x7FF - (int)red[1];
-    const bool exact_path = !p.out_int && tmax > 0 && tmax - tmin > kSumWindowBits - 53;
-    const int bottom = (tmax > 0 ? tmax : 1) - 1075 - (kSumWindowBits - 53);
-    const int64_t i0 = o0 + (int64_t)tid * kSlideRun;
-    RlAcc a = {0, 0, 0, 0, 0, 0, 0, 0};
-    int64_t ps = 0, pe = 0;
-    for (int k = 0; k < kSlideRun; ++k) {
-        const int64_t i = i0 + k;
-        if (i >= o1) break;
-        int64_t s, e;
-        rl_bounds(p, i, s, e);
-        double sum = 0.0;
-        RlCounts cnt;
-        if (exact_path) {
-            cnt = {0, 0, 0, 0};
-            for (int64_t r = s; r < e; ++r) rl_count(p, r, cnt);
-            sum = rl_exact_sum(p, s, e);
-        } else {
-            if (k == 0) {
-                for (int64_t r = s; r < e; ++r) rl_acc<NULLABLE>(p, vals, vld, (int)(r - lo), bottom, 1, a);
-            } else {
-                for (int64_t r = ps; r < s; ++r) rl_acc<NULLABLE>(p, vals, vld, (int)(r - lo), bottom, -1, a);
-                for (int64_t r = pe; r < e; ++r) rl_acc<NULLABLE>(p, vals, vld, (int)(r - lo), bottom, 1, a);
-            }
-            cnt = {a.nn, a.pinf, a.ninf, a.nan};
-            if (!p.out_int) sum = rl_to_double(a.l0, a.l1, a.l2, bottom);
-        }
-        ps = s;
-        pe = e;
-        bool valid;
-        RlParams q = p;  // write into the LDS staging buffer (index i - o0)
-        q.out = outv;
-        q.out_int = p.out_int ? PLGPU_I64 : 0;
-        rl_write(q, i - o0, sum, a.isum, cnt, e - s, valid);
-        if (valid) atomicOr((unsigned long long*)&outm[(i - o0) >> 6], 1ull << ((i - o0) & 63));
+    const bool counts = __ballot(odd) != 0;
+    uint64_t* rlo = ring_lo[wv];
+    uint64_t* rhi = ring_hi[wv];
+    uint64_t* rcn = ring_cn[wv];
+    if (isint) {
+        // (the exponent fields of integers mean nothing; only nulls count)
+        if (__ballot(NULLABLE && odd) != 0) rw_scan<0, true, false>(p, x, vm, o_first, o_end, s_first, 0, rlo, rhi, rcn);
+        else rw_scan<0, false, false>(p, x, vm, o_first, o_end, s_first, 0, rlo, rhi, rcn);
+        return;
     }
-    __syncthreads();
-    // coalesced write-out of values and validity words
-    for (int j = tid; j < (int)(o1 - o0); j += kRlThreads) {
-        const int64_t i = o0 + j;
-        if (!p.out_int) ((double*)p.out)[i] = __longlong_as_double((long long)outv[j]);
-        else if (p.out_int == PLGPU_I64) ((int64_t*)p.out)[i] = (int64_t)outv[j];
-        else ((int32_t*)p.out)[i] = (int32_t)(int64_t)outv[j];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint32_t a = __shfl_xor(mx, off, 64), c = __shfl_xor(inv_mn, off, 64);
+        mx = a > mx ? a : mx;
+        inv_mn = c > inv_mn ? c : inv_mn;
     }
-    for (int j = tid; j < (int)((o1 - o0 + 63) / 64); j += kRlThreads) p.out_valid[(o0 >> 6) + j] = outm[j];
+    const int tmax = (int)mx, tmin = mx ? 0x7FF - (int)inv_mn : 1024;
+    int lw = 0;
+    while ((int64_t(1) << lw) <= p.w) ++lw;  // p.w < 2^lw
+    const int span = tmax - tmin;
+    // int64 when any window's sum fits 63 bits and results cannot be subnormal
+    const bool narrow = mx == 0 || (tmin >= 128 && lw + 53 + span <= 63);
+    if (!narrow && lw + 53 + span > 127) {
+        rw_exact_outputs(p, o_first, o_end);  // beyond 128 bits
+        return;
+    }
+#define PLGPU_RW(M, C)                                                                                   \
+    (p.mean ? rw_scan<M, C, true>(p, x, vm, o_first, o_end, s_first, tmin, rlo, rhi, rcn)               \
+            : rw_scan<M, C, false>(p, x, vm, o_first, o_end, s_first, tmin, rlo, rhi, rcn))
+    if (narrow) {
+        if (counts) PLGPU_RW(1, true);
+        else PLGPU_RW(1, false);
+    } else {
+        if (counts) PLGPU_RW(2, true);
+        else PLGPU_RW(2, false);
+    }
+#undef PLGPU_RW
 }
 
 // Windows too wide for the LDS stage: per-output direct summation.
@@ -752,10 +908,19 @@ PLGPU_API int plgpu_rolling(const plgpu_column* values, int32_t kind, int64_t wi
     p.out = (void*)out->values;
     p.out_valid = (uint64_t*)out->validity;
     const int64_t tiles = (p.n + kRlOut - 1) / kRlOut;
-    if (window_size <= kSlideMaxW) {
-        const int64_t g = (p.n + kSlideOut - 1) / kSlideOut;
-        if (p.c.validity) rl_slide_kernel<true><<<(unsigned)g, kRlThreads, 0, s>>>(p);
-        else rl_slide_kernel<false><<<(unsigned)g, kRlThreads, 0, s>>>(p);
+    if (window_size <= kRwMaxW) {
+        const unsigned g = (unsigned)((p.n + (int64_t)kRwOut * kRwWaves - 1) / ((int64_t)kRwOut * kRwWaves));
+        const bool nl = p.c.validity != nullptr;
+        if (values->dtype == PLGPU_F64) {
+            if (nl) rl_wave_kernel<PLGPU_F64, true><<<g, 64 * kRwWaves, 0, s>>>(p);
+            else rl_wave_kernel<PLGPU_F64, false><<<g, 64 * kRwWaves, 0, s>>>(p);
+        } else if (values->dtype == PLGPU_I64) {
+            if (nl) rl_wave_kernel<PLGPU_I64, true><<<g, 64 * kRwWaves, 0, s>>>(p);
+            else rl_wave_kernel<PLGPU_I64, false><<<g, 64 * kRwWaves, 0, s>>>(p);
+        } else {
+            if (nl) rl_wave_kernel<PLGPU_I32, true><<<g, 64 * kRwWaves, 0, s>>>(p);
+            else rl_wave_kernel<PLGPU_I32, false><<<g, 64 * kRwWaves, 0, s>>>(p);
+        }
     } else if (window_size - 1 + kRlOut <= 2048)
         rl_tile_kernel<2048><<<(unsigned)tiles, kRlThreads, 0, s>>>(p);
     else if (window_size - 1 + kRlOut <= 4096)

@@ -228,6 +228,43 @@ def test_rolling_nulls_and_specials(gpu, kind):
         _rolling_check(v, valid, kind, w, ms, center)
 
 
+def _span_data(kind, n, rng):
+    if kind == "narrow":      # one int64 fixed-point word per value
+        return rng.uniform(100, 150, n)
+    if kind == "mixed":       # ~40 binades, mixed signs: 128-bit words
+        return rng.standard_normal(n) * np.exp2(rng.integers(-20, 20, n))
+    if kind == "tiny":        # subnormal values and results
+        v = rng.standard_normal(n) * 5e-324 * 2 ** 40
+        v[::7] = rng.integers(-3, 4, v[::7].shape[0]) * 5e-324
+        return v
+    if kind == "cancel":      # exact cancellations around large values
+        v = rng.uniform(-1, 1, n)
+        v[::5] = 2.0 ** 60
+        v[2::5] = -(2.0 ** 60)
+        return v
+    v = rng.uniform(-1, 1, n)  # "huge": beyond 128 bits, per-output exact
+    v[::31] = 1e200
+    v[1::31] = -1e200
+    v[3::31] = -0.0          # all -0.0 windows sum to +0.0 (SumWindow starts at +0.0)
+    return v
+
+
+@pytest.mark.parametrize("span", ["narrow", "mixed", "tiny", "cancel", "huge"])
+@pytest.mark.parametrize("w", [1, 2, 5, 63, 64])
+def test_rolling_wave_kernel_modes(gpu, span, w):
+    """The w <= 64 wave-scan kernel in each number format it picks per wave
+    (int64 / 128-bit fixed point, per-output exact), across wave and
+    workgroup boundaries (1024 / 4096 outputs), centred and clipped."""
+    rng = np.random.default_rng(w * 7 + len(span))
+    n = 4096 * 3 + 1024 + 17
+    v = _span_data(span, n, rng)
+    valid = rng.random(n) > 0.1
+    for ms, center in ((w, False), (1, True), (max(1, w // 3), False)):
+        for kind in ("sum", "mean"):
+            _rolling_check(v, None, kind, w, ms, center, ref_bound=False)
+            _rolling_check(v, valid, kind, w, ms, center, ref_bound=False)
+
+
 def test_rolling_wide_exponent_span_is_exact(gpu):
     """A tile whose values span far more than one fixed-point window takes
     the exact per-output path (1e300 next to 1e-300 and cancellations)."""
