@@ -351,6 +351,25 @@ class Series:
         return cls.from_device(name, m[tensor.dtype], tensor.data_ptr(), tensor.numel(), vptr,
                                keepalive=(tensor, validity))
 
+    def to_torch(self):
+        """The values as a new torch tensor on the device (a device-to-device
+        copy; nulls keep whatever their slots hold).  Fixed-width dtypes only."""
+        import torch
+
+        m = {"Int64": torch.int64, "Int32": torch.int32, "Float64": torch.float64, "Float32": torch.float32,
+             "Int16": torch.int16, "Int8": torch.int8, "UInt8": torch.uint8, "UInt32": torch.int32,
+             "UInt64": torch.int64, "UInt16": torch.int16}
+        phys = _BY_CODE[self._col.dtype]
+        if phys.name not in m:
+            raise N.InvalidOperationError(f"to_torch: {phys} has no torch tensor form")
+        t = torch.empty(self.len(), dtype=m[phys.name], device="cuda")
+        nb = t.element_size() * self.len()
+        if nb:
+            src = int(self._col.values) + int(self._col.offset) * t.element_size()
+            N.check(N.lib().plgpu_memcpy_d2d(C.c_void_p(t.data_ptr()), C.c_void_p(src), nb, None))
+            N.check(N.lib().plgpu_synchronize(None))
+        return t
+
     # properties -----------------------------------------------------------
     @property
     def dtype(self) -> DataType:
