@@ -39,9 +39,11 @@ hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 // through size-keyed free lists instead of being returned with hipFree
 // (which synchronises the device).  Every entry point enqueues its work on
 // one stream and frees only after the kernels that use a block were
-// enqueued, so stream order makes reuse safe.  (hipMallocAsync's default
-// pool was measured to lose writes into a recycled block on this ROCm
-// build, see DESIGN.md "Allocator"; it is not used.)
+// enqueued, so stream order makes reuse safe.  PLGPU_ALLOC=async switches
+// to hipMallocAsync / hipFreeAsync: the GPU parity suites pass under it
+// (profiles/r02_alloc_async_ab.log), so an earlier "lost writes" report
+// against that pool was not the pool's fault -- it predates the exchange's
+// receive-buffer fence (distributed._settle), the likelier cause.
 namespace {
 struct Pool {
     std::mutex mu;
@@ -67,9 +69,27 @@ void release_cached(Pool& P) {
 }
 }  // namespace
 
+// PLGPU_ALLOC=async: stream-ordered hipMallocAsync / hipFreeAsync from the
+// device's default pool instead of the cache (A/B runs of the allocator).
+static bool alloc_async() {
+    static const int on = [] {
+        const char* e = getenv("PLGPU_ALLOC");
+        return (e && !strcmp(e, "async")) ? 1 : 0;
+    }();
+    return on != 0;
+}
+
 int dev_alloc(void** p, size_t bytes, hipStream_t s) {
-    (void)s;
     *p = nullptr;
+    if (alloc_async()) {
+        const hipError_t e = hipMallocAsync(p, bytes == 0 ? 256 : bytes, s);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            *p = nullptr;
+            return fail(PLGPU_ERR_OOM, "hipMallocAsync failed");
+        }
+        return PLGPU_OK;
+    }
     const size_t want = round_bytes(bytes == 0 ? 256 : bytes);
     int dev = 0;
     (void)hipGetDevice(&dev);
@@ -101,8 +121,11 @@ int dev_alloc(void** p, size_t bytes, hipStream_t s) {
 }
 
 void dev_free(void* p, hipStream_t s) {
-    (void)s;
     if (p == nullptr) return;
+    if (alloc_async()) {
+        (void)hipFreeAsync(p, s);
+        return;
+    }
     int dev = 0;
     (void)hipGetDevice(&dev);
     Pool& P = pool_for(dev);

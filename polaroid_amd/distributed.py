@@ -25,6 +25,8 @@ stays the local HBM pass: weak scaling.
 
 from __future__ import annotations
 
+import os
+
 import ctypes as C
 import time
 from typing import Any, Sequence
@@ -66,11 +68,15 @@ def _settle(device) -> None:
 
 
 # Largest per-peer message of one all-to-all.  On this image's RCCL
-# (2.26.6) an all_to_all_single moving 4 GB to one peer corrupted data
-# (tools/check_shuffle_scale.py: key checksum mismatch at 5e8 int64 rows,
-# fine at 4e7), so bigger exchanges go in rounds of point-to-point
-# transfers of at most this many bytes per peer.
-A2A_MAX_BYTES = 1 << 30
+# (2.26.6) all_to_all_single loses the second half of any message above
+# 1 GiB: tools/repro_a2a_large.py (torch + RCCL only, world 1) gets 1 GiB
+# right and 1.99 / 2 / 3 / 4 / 6 GiB wrong from element n/2 on
+# (profiles/r02_a2a_repro.log), with the receive fence (_settle) in place
+# (tools/check_shuffle_scale.py without rounds: profiles/
+# r02_shuffle_no_rounds.log).  Bigger exchanges therefore go in rounds of
+# point-to-point transfers of at most this many bytes per peer
+# (PLGPU_A2A_MAX_BYTES overrides it for such checks).
+A2A_MAX_BYTES = int(os.environ.get("PLGPU_A2A_MAX_BYTES", 1 << 30))
 
 
 def alltoallv(out, inp, out_splits: Sequence[int], in_splits: Sequence[int], group=None) -> None:
