@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "plgpu_internal.hpp"
+#include "scan.hpp"
 
 namespace plgpu {
 
@@ -71,32 +72,60 @@ __global__ __launch_bounds__(kEvalThreads) void eval_kernel(ColArgs cols, DevPro
 
 // ------------------------------------------------------------- filter
 // Mask source: either a BOOL column (values & validity, null = false) or a
-// lowered program.  Writes one u64 per 64 rows and one count per tile.
-template <int SRC>  // 0 = bool column, 1 = simple predicate, 2 = program
+// lowered program.  Writes one u64 per 64 rows and one count per tile.  A
+// thread owns rows it * 256 + tid (it < 16) of its tile: the simple-predicate
+// form loads all 16 before the first ballot, so each wave keeps 16 loads in
+// flight.
+template <int SRC>  // 0 = bool column, 1 = simple predicate, 2 = program, 3 = simple on a null-free 8-byte column
 __global__ __launch_bounds__(kFilterThreads) void filter_mask_kernel(ColArgs cols, DevProgram prog, DevCol mask,
                                                                      int64_t n, int64_t ntiles,
                                                                      uint64_t* __restrict__ mask_words,
                                                                      uint32_t* __restrict__ tile_counts) {
+    constexpr int IT = kTileRows / kFilterThreads;
     __shared__ uint32_t wave_cnt[kFilterThreads / 64];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         uint32_t cnt = 0;
-        for (int it = 0; it < kTileRows / kFilterThreads; ++it) {
-            const int64_t r = t * kTileRows + it * kFilterThreads + threadIdx.x;
-            bool sel = false;
-            if (r < n) {
-                if (SRC == 0) {
-                    sel = dev_valid(mask, r) && (dev_load(mask, r) & 1);
-                } else if (SRC == 1) {
-                    const DevCol& c = cols.c[prog.simple_col];
-                    sel = dev_valid(c, r) && simple_pred(prog.simple_isf, prog.simple_op, dev_load(c, r), prog.simple_imm);
-                } else {
-                    RowVal rv = eval_row(prog.code, prog.n, cols.c, r);
-                    sel = rv.valid && (rv.v & 1);
+        bool sel[IT];
+        if (SRC == 3) {
+            // simple predicate over a null-free 8-byte column: 16 branch-free
+            // loads (row index clamped at the end), then the compares
+            const DevCol c = cols.c[prog.simple_col];
+            const uint64_t* __restrict__ v = (const uint64_t*)c.values + c.offset;
+            uint64_t x[IT];
+#pragma unroll
+            for (int it = 0; it < IT; ++it) {
+                const int64_t r = t * kTileRows + it * kFilterThreads + threadIdx.x;
+                x[it] = __builtin_nontemporal_load(v + (r < n ? r : n - 1));
+            }
+#pragma unroll
+            for (int it = 0; it < IT; ++it) {
+                const int64_t r = t * kTileRows + it * kFilterThreads + threadIdx.x;
+                sel[it] = r < n && simple_pred(prog.simple_isf, prog.simple_op, x[it], prog.simple_imm);
+            }
+        } else {
+#pragma unroll
+            for (int it = 0; it < IT; ++it) {
+                const int64_t r = t * kTileRows + it * kFilterThreads + threadIdx.x;
+                sel[it] = false;
+                if (r < n) {
+                    if (SRC == 0) {
+                        sel[it] = dev_valid(mask, r) && (dev_load(mask, r) & 1);
+                    } else if (SRC == 1) {
+                        const DevCol& c = cols.c[prog.simple_col];
+                        sel[it] = dev_valid(c, r) &&
+                                  simple_pred(prog.simple_isf, prog.simple_op, dev_load(c, r), prog.simple_imm);
+                    } else {
+                        RowVal rv = eval_row(prog.code, prog.n, cols.c, r);
+                        sel[it] = rv.valid && (rv.v & 1);
+                    }
                 }
             }
-            const uint64_t w = __ballot(sel);
+        }
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const uint64_t w = __ballot(sel[it]);
             if (lane == 0) mask_words[t * kTileWords + it * (kFilterThreads / 64) + wave] = w;
             cnt += (uint32_t)__popcll(w);
         }
@@ -109,33 +138,6 @@ __global__ __launch_bounds__(kFilterThreads) void filter_mask_kernel(ColArgs col
         }
         __syncthreads();
     }
-}
-
-// Exclusive scan of tile counts (single workgroup; ntiles <= a few 1e5).
-__global__ __launch_bounds__(1024) void scan_tiles_kernel(const uint32_t* __restrict__ counts, int64_t ntiles,
-                                                         uint64_t* __restrict__ offsets,
-                                                         uint64_t* __restrict__ total) {
-    __shared__ uint64_t part[1024];
-    const int tid = threadIdx.x;
-    const int64_t per = (ntiles + 1023) / 1024;
-    const int64_t lo = tid * per;
-    const int64_t hi = lo + per < ntiles ? lo + per : ntiles;
-    uint64_t s = 0;
-    for (int64_t i = lo; i < hi; ++i) s += counts[i];
-    part[tid] = s;
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {
-        uint64_t x = tid >= off ? part[tid - off] : 0;
-        __syncthreads();
-        part[tid] += x;
-        __syncthreads();
-    }
-    uint64_t run = part[tid] - s;  // exclusive
-    for (int64_t i = lo; i < hi; ++i) {
-        offsets[i] = run;
-        run += counts[i];
-    }
-    if (tid == 1023) *total = part[1023];
 }
 
 __device__ __forceinline__ uint64_t wave_or64(uint64_t x) {
@@ -223,6 +225,67 @@ __global__ __launch_bounds__(kFilterThreads) void filter_scatter_kernel(DevCol c
     }
 }
 
+// Stable scatter of up to 8 null-free 8-byte columns in one launch: the
+// tile's mask words and their prefix are read once, then every column's
+// selected rows are copied (each thread's 16 loads of a column issued
+// together).
+struct Scatter8Args {
+    const uint64_t* src[PLGPU_MAX_COLS];
+    uint64_t* dst[PLGPU_MAX_COLS];
+    int32_t ncols;
+};
+
+__global__ __launch_bounds__(kFilterThreads) void filter_scatter8_kernel(Scatter8Args a, int64_t n, int64_t ntiles,
+                                                                         const uint64_t* __restrict__ mask_words,
+                                                                         const uint64_t* __restrict__ tile_off) {
+    constexpr int IT = kTileRows / kFilterThreads;
+    __shared__ uint64_t words[kTileWords];
+    __shared__ uint32_t prefix[kTileWords];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const uint64_t lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        if (threadIdx.x < kTileWords) {
+            const uint64_t w = mask_words[t * kTileWords + threadIdx.x];
+            words[threadIdx.x] = w;
+            uint32_t x = (uint32_t)__popcll(w), c = x;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t y = __shfl_up(x, off, 64);
+                if (lane >= off) x += y;
+            }
+            prefix[threadIdx.x] = x - c;
+        }
+        __syncthreads();
+        const uint64_t base_off = tile_off[t];
+        uint64_t pos[IT];
+        bool sel[IT];
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int wi = it * (kFilterThreads / 64) + wave;
+            const uint64_t w = words[wi];
+            sel[it] = (w >> lane) & 1;
+            pos[it] = base_off + prefix[wi] + (uint32_t)__popcll(w & lt_mask);
+        }
+        for (int j = 0; j < a.ncols; ++j) {
+            // branch-free loads (row clamped at the end of the column): the
+            // lines are fetched whole anyway; only the stores are predicated
+            const uint64_t* __restrict__ src = a.src[j];
+            uint64_t* __restrict__ dst = a.dst[j];
+            uint64_t v[IT];
+#pragma unroll
+            for (int it = 0; it < IT; ++it) {
+                const int64_t r = t * kTileRows + it * kFilterThreads + threadIdx.x;
+                v[it] = __builtin_nontemporal_load(src + (r < n ? r : n - 1));
+            }
+#pragma unroll
+            for (int it = 0; it < IT; ++it)
+                if (sel[it]) dst[pos[it]] = v[it];
+        }
+        __syncthreads();
+    }
+}
+
 static ColArgs pack_cols(const plgpu_column* cols, int32_t ncols) {
     ColArgs a;
     std::memset(&a, 0, sizeof a);
@@ -279,24 +342,28 @@ static int run_filter(const plgpu_column* cols, int32_t ncols, int src, const De
     uint64_t* mask_words = nullptr;
     uint32_t* counts = nullptr;
     uint64_t* offs = nullptr;  // ntiles offsets + 1 total
+    uint64_t* scan_part = nullptr;
     uint64_t total = 0;
     if (ntiles > 0) {
         if ((rc = dev_alloc((void**)&mask_words, ntiles * kTileWords * 8, s))) return rc;
         if ((rc = dev_alloc((void**)&counts, ntiles * 4, s))) { dev_free(mask_words, s); return rc; }
-        if ((rc = dev_alloc((void**)&offs, (ntiles + 1) * 8, s))) {
+        if ((rc = dev_alloc((void**)&offs, (ntiles + 1) * 8, s)) ||
+            (rc = dev_alloc((void**)&scan_part, ((ntiles + kScanChunk - 1) / kScanChunk + 1) * 8, s))) {
             dev_free(mask_words, s);
             dev_free(counts, s);
+            dev_free(offs, s);
             return rc;
         }
         const int g = grid_for(ntiles, 1, 256 * 8);
         if (src == 0)
             filter_mask_kernel<0><<<g, kFilterThreads, 0, s>>>(ca, dp, md, n, ntiles, mask_words, counts);
+        else if (dp.simple && cols[dp.simple_col].validity == nullptr && dtype_bytes(cols[dp.simple_col].dtype) == 8)
+            filter_mask_kernel<3><<<g, kFilterThreads, 0, s>>>(ca, dp, md, n, ntiles, mask_words, counts);
         else if (dp.simple)
             filter_mask_kernel<1><<<g, kFilterThreads, 0, s>>>(ca, dp, md, n, ntiles, mask_words, counts);
         else
             filter_mask_kernel<2><<<g, kFilterThreads, 0, s>>>(ca, dp, md, n, ntiles, mask_words, counts);
-        scan_tiles_kernel<<<1, 1024, 0, s>>>(counts, ntiles, offs, offs + ntiles);
-        PLGPU_HIP(hipGetLastError());
+        PLGPU_HIP(scan_exclusive<uint32_t>(counts, ntiles, offs, scan_part, s));
         PLGPU_HIP(hipMemcpyAsync(&total, offs + ntiles, 8, hipMemcpyDeviceToHost, s));
         PLGPU_HIP(hipStreamSynchronize(s));
     }
@@ -316,8 +383,28 @@ static int run_filter(const plgpu_column* cols, int32_t ncols, int src, const De
         rc = str_gather(dev_col(cols[i]), nullptr, sel_rows, nullptr, 0, (int64_t)total, cols[i].validity != nullptr,
                         &out_cols[i], s);
     }
+    // null-free 8-byte columns: one multi-column scatter launch
+    auto wide8 = [&](int i) {
+        return cols[i].dtype != PLGPU_STR && cols[i].dtype != PLGPU_BOOL && cols[i].validity == nullptr &&
+               dtype_bytes(cols[i].dtype) == 8;
+    };
+    Scatter8Args sa;
+    std::memset(&sa, 0, sizeof sa);
     for (int i = 0; i < ncols && !rc; ++i) {
-        if (cols[i].dtype == PLGPU_STR) continue;
+        if (!wide8(i)) continue;
+        rc = make_owned_column(&out_cols[i], cols[i].dtype, (int64_t)total, false, s);
+        if (rc) break;
+        sa.src[sa.ncols] = (const uint64_t*)cols[i].values + cols[i].offset;
+        sa.dst[sa.ncols] = (uint64_t*)out_cols[i].values;
+        ++sa.ncols;
+    }
+    if (!rc && sa.ncols > 0 && total > 0) {
+        filter_scatter8_kernel<<<grid_for(ntiles, 1, 256 * 8), kFilterThreads, 0, s>>>(sa, n, ntiles, mask_words,
+                                                                                         offs);
+        PLGPU_HIP(hipGetLastError());
+    }
+    for (int i = 0; i < ncols && !rc; ++i) {
+        if (cols[i].dtype == PLGPU_STR || wide8(i)) continue;
         const bool need_valid = cols[i].validity != nullptr;
         rc = make_owned_column(&out_cols[i], cols[i].dtype, (int64_t)total,
                                need_valid || cols[i].dtype == PLGPU_BOOL, s);
@@ -352,6 +439,7 @@ static int run_filter(const plgpu_column* cols, int32_t ncols, int src, const De
     dev_free(mask_words, s);
     dev_free(counts, s);
     dev_free(offs, s);
+    dev_free(scan_part, s);
     dev_free(sel_rows, s);
     if (rc) {
         for (int i = 0; i < ncols; ++i) plgpu_column_release(&out_cols[i]);
