@@ -713,8 +713,9 @@ template <int EB>  // element bytes 1 / 2 / 4 / 8
 __global__ __launch_bounds__(256) void gather_col_kernel(DevCol c, const uint32_t* __restrict__ idx, int64_t n,
                                                          void* __restrict__ out, uint64_t* __restrict__ out_valid,
                                                          const uint8_t* __restrict__ iv, int64_t ioff) {
-    // 4 outputs per thread (strided by the block), loads issued together
-    constexpr int K = 4;
+    // 8 outputs per thread (strided by the block), loads issued together and
+    // branch-free (a null index reads row 0), so none waits on another
+    constexpr int K = 8;
     const int64_t step = (int64_t)gridDim.x * blockDim.x * K;
     for (int64_t base = (int64_t)blockIdx.x * blockDim.x * K; base < n; base += step) {
         uint32_t r[K];
@@ -722,19 +723,19 @@ __global__ __launch_bounds__(256) void gather_col_kernel(DevCol c, const uint32_
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const int64_t o = base + (int64_t)k * blockDim.x + threadIdx.x;
-            r[k] = o < n ? __builtin_nontemporal_load(idx + o) : 0u;
+            r[k] = __builtin_nontemporal_load(idx + (o < n ? o : n - 1));
             in[k] = o < n && !idx_null(iv, ioff, o);
+            if (!in[k]) r[k] = 0;
         }
         uint64_t v[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const int64_t p = c.offset + r[k];
-            v[k] = 0;
-            if (in[k])
-                v[k] = EB == 8   ? ((const uint64_t*)c.values)[p]
-                       : EB == 4 ? ((const uint32_t*)c.values)[p]
-                       : EB == 2 ? ((const uint16_t*)c.values)[p]
-                                 : ((const uint8_t*)c.values)[p];
+            v[k] = EB == 8   ? ((const uint64_t*)c.values)[p]
+                   : EB == 4 ? ((const uint32_t*)c.values)[p]
+                   : EB == 2 ? ((const uint16_t*)c.values)[p]
+                             : ((const uint8_t*)c.values)[p];
+            if (!in[k]) v[k] = 0;
         }
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -805,14 +806,31 @@ __global__ __launch_bounds__(256) void aos_gather_kernel(const uint64_t* __restr
                                                          const uint32_t* __restrict__ idx, int64_t n, AosCols c) {
     constexpr int NP = (NC + 1) & ~1;
     constexpr int L = NP / 2;  // lanes per row
+    // K lane-rows per thread per step: the K index loads, then the K row
+    // loads, are issued back to back (the row loads depend on the indices)
+    constexpr int K = 4;
     const int64_t nl = n * L;
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nl; t += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t o = t / L;
-        const int q = (int)(t - o * L);
-        const int64_t r = idx[o];
-        const ulonglong2 x = reinterpret_cast<const ulonglong2*>(aos + r * NP)[q];
-        __builtin_nontemporal_store(x.x, c.dst[2 * q] + o);
-        if (2 * q + 1 < NC) __builtin_nontemporal_store(x.y, c.dst[2 * q + 1] + o);
+    const int64_t G = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t0 < nl; t0 += G * K) {
+        int64_t o[K];
+        int q[K];
+        uint32_t r[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int64_t t = t0 + k * G;
+            o[k] = (t < nl ? t : nl - 1) / L;
+            q[k] = (int)((t < nl ? t : nl - 1) - o[k] * L);
+            r[k] = __builtin_nontemporal_load(idx + o[k]);
+        }
+        ulonglong2 x[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) x[k] = reinterpret_cast<const ulonglong2*>(aos + (int64_t)r[k] * NP)[q[k]];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            if (t0 + k * G >= nl) break;
+            __builtin_nontemporal_store(x[k].x, c.dst[2 * q[k]] + o[k]);
+            if (2 * q[k] + 1 < NC) __builtin_nontemporal_store(x[k].y, c.dst[2 * q[k] + 1] + o[k]);
+        }
     }
 }
 
@@ -845,6 +863,15 @@ static int gather_into(const plgpu_column& src, const uint32_t* idx, int64_t n, 
     int rc = make_owned_column(out, src.dtype, n, nullable, s);
     if (rc) return rc;
     if (n == 0) return PLGPU_OK;
+    if (src.length == 0) {
+        // every index is null (an empty side of an outer join): all-null
+        // output, and the kernels' branch-free row-0 reads must not run
+        PLGPU_HIP(hipMemsetAsync((void*)out->values, 0,
+                                 src.dtype == PLGPU_BOOL ? ((n + 63) / 64) * 8 : n * dtype_bytes(src.dtype), s));
+        if (out->validity) PLGPU_HIP(hipMemsetAsync((void*)out->validity, 0, ((n + 63) / 64) * 8, s));
+        out->null_count = n;
+        return PLGPU_OK;
+    }
     DevCol c;
     std::memset(&c, 0, sizeof c);
     c.dtype = src.dtype;
