@@ -463,6 +463,21 @@ int plgpu_join_inner(const plgpu_column* left_key, const plgpu_column* right_key
                      int32_t nulls_equal, int32_t maintain_order, int32_t validate,
                      plgpu_column* out_left_idx, plgpu_column* out_right_idx, void* stream);
 
+/* Inner join on one integer key returning the left row indices and the right
+ * side's one payload column gathered at the pairs (pair order as
+ * plgpu_join_inner).  The fused form of hash_join_tuples_inner followed by
+ * the take of the right frame's single non-key column
+ * (polars-ops/src/frame/join/hash_join/single_keys_inner.rs:45 +
+ * general.rs:17 _finish_join): with unique right keys and a null-free 8-byte
+ * payload the payload rides in the hash table's cells, so the probe returns
+ * it and no random gather of the right side follows; other inputs take the
+ * pairs + gather route with the same result. */
+int plgpu_join_inner_payload(const plgpu_column* left_key, const plgpu_column* right_key,
+                             const plgpu_column* right_payload, int32_t nulls_equal,
+                             int32_t maintain_order, int32_t validate,
+                             plgpu_column* out_left_idx, plgpu_column* out_right_payload,
+                             void* stream);
+
 /* Inner join on 1..8 key columns per side (pairwise equal dtypes: I64 / I32 /
  * U32 / F64 / BOOL).  Replaces the multi-key branch of the reference's join
  * (polars-ops/src/frame/join/mod.rs:625 prepare_keys_multiple: both sides'

@@ -235,14 +235,17 @@ constexpr uint32_t kNullIdx = 0xFFFFFFFFu;  // null index in an output pair
 // same way; ballots tell the row's lane whether its bucket held the key or
 // an empty cell (a full bucket without the key continues, lane by lane, in
 // the next buckets - rare at load <= 0.6).
-template <bool NULLABLE, int MODE, bool MARK>
+// INLINE (row-format table, unique build keys): a cell holds {key, payload}
+// instead of {key, ref}; a hit writes the payload to mp[r] and m[r] = 0.
+template <bool NULLABLE, int MODE, bool MARK, bool INLINE = false>
 __global__ __launch_bounds__(kJnThreads) void jn_probe_match_kernel(DevCol pk, int64_t np, JnTable t,
                                                                   bool nulls_equal, uint32_t* __restrict__ m,
                                                                   uint64_t* __restrict__ tile_counts, int64_t ntiles,
-                                                                  uint8_t* __restrict__ flags) {
+                                                                  uint8_t* __restrict__ flags,
+                                                                  uint64_t* __restrict__ mp = nullptr) {
     __shared__ uint64_t wsum[kJnThreads / 64];
     __shared__ uint4 rowbuf[kJnThreads];  // {key lo, key hi, bucket, regular}
-    __shared__ uint2 hitbuf[kJnThreads];  // {ref, slot} of the matching cell
+    __shared__ uint4 hitbuf[kJnThreads];  // {ref (payload lo), slot, payload hi, -} of the matching cell
     const uint64_t* kp = (const uint64_t*)pk.values + pk.offset;
     const bool wide = pk.dtype == PLGPU_I64 || pk.dtype == PLGPU_U64;
     const int lane = threadIdx.x & 63;
@@ -288,7 +291,7 @@ __global__ __launch_bounds__(kJnThreads) void jn_probe_match_kernel(DevCol pk, i
                 const bool eq = live && cell[j].x == rq[j].x && cell[j].y == rq[j].y;
                 const bool em = live && cell[j].x == 0u && cell[j].y == 0x80000000u;
                 const uint64_t eqm = __ballot(eq), emm = __ballot(em);
-                if (eq) hitbuf[wbase + 8 * j + g] = make_uint2(cell[j].z, rq[j].z * kBktCells + e);
+                if (eq) hitbuf[wbase + 8 * j + g] = make_uint4(cell[j].z, rq[j].z * kBktCells + e, cell[j].w, 0u);
                 // this lane's row was served in sub-round lane / 8 by group lane % 8
                 if ((lane >> 3) == j) {
                     beq = (eqm >> (8 * (lane & 7))) & 0xFFull;
@@ -300,14 +303,16 @@ __global__ __launch_bounds__(kJnThreads) void jn_probe_match_kernel(DevCol pk, i
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             int64_t slot = -1;
             uint32_t ref = kRefNone;
+            uint64_t pay = 0;
             if (r >= np || (NULLABLE && !valid[k])) {
                 if (r < np && NULLABLE && !valid[k] && nulls_equal) slot = t.cap;
             } else if (key[k] == kEmptyKey) {
                 slot = t.cap + 1;
             } else if (beq) {
-                const uint2 h = hitbuf[threadIdx.x];
+                const uint4 h = hitbuf[threadIdx.x];
                 ref = h.x;
                 slot = h.y;
+                pay = (uint64_t)h.x | ((uint64_t)h.z << 32);
             } else if (!bem) {
                 // the home bucket is full without the key: later buckets
                 uint64_t bb = (b + 1) & nbm;
@@ -318,6 +323,7 @@ __global__ __launch_bounds__(kJnThreads) void jn_probe_match_kernel(DevCol pk, i
                         const uint64_t kk = (uint64_t)x.x | ((uint64_t)x.y << 32);
                         if (kk == key[k]) {
                             ref = x.z;
+                            pay = (uint64_t)x.z | ((uint64_t)x.w << 32);
                             slot = (int64_t)(bb * kBktCells + ee);
                             stop = true;
                             break;
@@ -330,7 +336,16 @@ __global__ __launch_bounds__(kJnThreads) void jn_probe_match_kernel(DevCol pk, i
                     if (stop) break;
                 }
             }
-            if (slot >= t.cap) ref = jn_ref(t, slot);  // null / INT64_MIN key slots
+            if (slot >= t.cap) {  // null / INT64_MIN key slots
+                if (INLINE) {
+                    ref = t.off[slot + 1] > t.off[slot] ? 0u : kRefNone;
+                    const uint4 x = t.cells[slot];
+                    pay = (uint64_t)x.z | ((uint64_t)x.w << 32);
+                } else {
+                    ref = jn_ref(t, slot);
+                }
+            }
+            if (INLINE && slot >= 0 && slot < t.cap) ref = 0u;  // a key match: the payload is in the cell
             if (MODE == JM_DRAIN) ref = (slot >= 0 && flags[slot]) ? 0u : kRefNone;
             if (r >= np) continue;
             const bool hit = ref != kRefNone;
@@ -339,7 +354,13 @@ __global__ __launch_bounds__(kJnThreads) void jn_probe_match_kernel(DevCol pk, i
                 w = hit ? 0u : kRefNone;
                 c += (MODE == JM_SEMI) == hit ? 1 : 0;
             } else {
-                if (ref == kRefList) {
+                if (INLINE) {
+                    if (hit) {
+                        w = 0u;
+                        __builtin_nontemporal_store(pay, mp + r);
+                        c += 1;
+                    }
+                } else if (ref == kRefList) {
                     w = kRefList | (uint32_t)slot;
                     c += t.off[slot + 1] - t.off[slot];
                 } else if (hit) {
@@ -355,6 +376,52 @@ __global__ __launch_bounds__(kJnThreads) void jn_probe_match_kernel(DevCol pk, i
         uint64_t total;
         (void)block_excl_scan(c, wsum, total);
         if (threadIdx.x == 0) tile_counts[tile] = total;
+    }
+}
+
+// Row-format table: every occupied cell's ref word (a unique build row)
+// is replaced by that row's 8-byte payload (cells {key, payload}).
+__global__ void jn_inline_kernel(JnTable t, DevCol pay) {
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < t.cap + 2;
+         s += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t ref = jn_ref(t, s);
+        if (ref >= kRefList) continue;  // empty (kRefNone); lists never reach here
+        const uint64_t v = dev_load(pay, ref);
+        uint32_t* c = (uint32_t*)&t.cells[s];
+        c[2] = (uint32_t)v;
+        c[3] = (uint32_t)(v >> 32);
+    }
+}
+
+// Emit of the row-format probe: probe row and payload of every hit, in
+// probe-row order.
+__global__ __launch_bounds__(kJnThreads) void jn_inline_emit_kernel(int64_t np, const uint32_t* __restrict__ m,
+                                                                    const uint64_t* __restrict__ mp,
+                                                                    const uint64_t* __restrict__ tile_off,
+                                                                    int64_t ntiles, uint32_t* __restrict__ out_p,
+                                                                    uint64_t* __restrict__ out_v) {
+    __shared__ uint64_t wsum[kJnThreads / 64];
+    constexpr int R = kJnTileRows / kJnThreads;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        uint32_t w[R];
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const int64_t r = tile * kJnTileRows + (int64_t)k * kJnThreads + threadIdx.x;
+            w[k] = r < np ? __builtin_nontemporal_load(m + r) : kRefNone;
+        }
+        uint64_t run = tile_off[tile];
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const int64_t r = tile * kJnTileRows + (int64_t)k * kJnThreads + threadIdx.x;
+            const uint32_t c = w[k] != kRefNone ? 1u : 0u;
+            uint64_t total;
+            const uint64_t pos = run + block_excl_scan(c, wsum, total);
+            if (c) {
+                out_p[pos] = (uint32_t)r;
+                __builtin_nontemporal_store(__builtin_nontemporal_load(mp + r), out_v + pos);
+            }
+            run += total;
+        }
     }
 }
 
@@ -787,15 +854,31 @@ struct AosCols {
 
 template <int NC>
 __global__ __launch_bounds__(256) void aos_pack_kernel(AosCols c, int64_t rows, uint64_t* __restrict__ aos) {
+    // 256 rows per step: column loads coalesced, rows transposed through LDS
+    // (row stride NP + 2 words against bank conflicts), then the block's
+    // 256 * NP words stored as consecutive 16-byte chunks
     constexpr int NP = (NC + 1) & ~1;  // row stride in u64 (16-byte aligned rows)
-    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += (int64_t)gridDim.x * blockDim.x) {
+    constexpr int STR = NP + 2;
+    __shared__ __attribute__((aligned(16))) uint64_t tile[256 * STR];
+    for (int64_t r0 = (int64_t)blockIdx.x * 256; r0 < rows; r0 += (int64_t)gridDim.x * 256) {
+        const int64_t r = r0 + threadIdx.x;
+        const int64_t rr = r < rows ? r : rows - 1;
         uint64_t v[NP];
 #pragma unroll
-        for (int k = 0; k < NC; ++k) v[k] = __builtin_nontemporal_load(c.src[k] + r);
+        for (int k = 0; k < NC; ++k) v[k] = __builtin_nontemporal_load(c.src[k] + rr);
         if (NP != NC) v[NP - 1] = 0;
-        ulonglong2* q = reinterpret_cast<ulonglong2*>(aos + r * NP);
 #pragma unroll
-        for (int k = 0; k < NP / 2; ++k) q[k] = make_ulonglong2(v[2 * k], v[2 * k + 1]);
+        for (int k = 0; k < NP / 2; ++k)
+            *reinterpret_cast<ulonglong2*>(&tile[threadIdx.x * STR + 2 * k]) = make_ulonglong2(v[2 * k], v[2 * k + 1]);
+        __syncthreads();
+        const int nrows = rows - r0 < 256 ? (int)(rows - r0) : 256;
+        const int nchunks = nrows * (NP / 2);
+        ulonglong2* dst = reinterpret_cast<ulonglong2*>(aos + r0 * NP);
+        for (int j = threadIdx.x; j < nchunks; j += 256) {
+            const int row = j / (NP / 2), q = j - row * (NP / 2);
+            dst[j] = *reinterpret_cast<const ulonglong2*>(&tile[row * STR + 2 * q]);
+        }
+        __syncthreads();
     }
 }
 
@@ -1575,6 +1658,99 @@ PLGPU_API int plgpu_join_inner(const plgpu_column* left_key, const plgpu_column*
                                plgpu_column* out_right_idx, void* stream) {
     return plgpu_join(left_key, right_key, PLGPU_JOIN_INNER, nulls_equal, maintain_order, validate, out_left_idx,
                       out_right_idx, stream);
+}
+
+// Inner join returning the left row indices and the right side's one
+// payload column gathered at the pairs (pairs and order as plgpu_join_inner).
+// When the right side is the build side and its keys are unique, the payload
+// rides in the hash table's cells (a row-format table): the probe's bucket
+// read returns it, so no random gather of the build side follows.  Any other
+// case computes the pairs and gathers.
+PLGPU_API int plgpu_join_inner_payload(const plgpu_column* left_key, const plgpu_column* right_key,
+                                       const plgpu_column* right_payload, int32_t nulls_equal,
+                                       int32_t maintain_order, int32_t validate, plgpu_column* out_left_idx,
+                                       plgpu_column* out_right_payload, void* stream) {
+    hipStream_t s = as_stream(stream);
+    if (right_payload == nullptr || out_left_idx == nullptr || out_right_payload == nullptr)
+        return fail(PLGPU_ERR_INVALID, "NULL argument");
+    std::memset(out_left_idx, 0, sizeof *out_left_idx);
+    std::memset(out_right_payload, 0, sizeof *out_right_payload);
+    int rc = check_key(left_key);
+    if (!rc) rc = check_key(right_key);
+    if (!rc) rc = check_args(PLGPU_JOIN_INNER, maintain_order, validate);
+    if (rc) return rc;
+    if (right_payload->length != right_key->length)
+        return fail(PLGPU_ERR_SHAPE, "payload and key lengths differ");
+    const bool neq = nulls_equal != 0;
+    const bool order_ok = maintain_order == PLGPU_JOIN_ORDER_NONE || maintain_order == PLGPU_JOIN_ORDER_LEFT;
+    const bool inline_ok = order_ok && (validate == PLGPU_JOIN_VALIDATE_M_M || validate == PLGPU_JOIN_VALIDATE_M_1) &&
+                           right_payload->validity == nullptr && dtype_bytes(right_payload->dtype) == 8 &&
+                           right_payload->dtype != PLGPU_STR && left_key->length >= (int64_t(1) << 16) &&
+                           (right_key->length <= left_key->length || maintain_order == PLGPU_JOIN_ORDER_LEFT);
+    JnBuilt b;
+    bool use_inline = false;
+    if (inline_ok) {
+        rc = jn_build(right_key, neq, false, &b, s);
+        if (rc) return rc;
+        use_inline = b.max_count <= 1;
+        if (!use_inline) jn_free(b, s);
+    }
+    if (!use_inline) {
+        // pairs, then the gather (duplicate build keys, nullable payloads, ...)
+        plgpu_column ri;
+        rc = join_impl(left_key, right_key, PLGPU_JOIN_INNER, neq, maintain_order, validate, out_left_idx, &ri, s);
+        if (rc) return rc;
+        rc = gather_into(*right_payload, (const uint32_t*)ri.values, ri.length, out_right_payload, s);
+        if (!rc) {
+            const hipError_t e = hipStreamSynchronize(s);
+            if (e != hipSuccess) rc = hip_fail(e, "join payload gather");
+        }
+        plgpu_column_release(&ri);
+        if (rc) plgpu_column_release(out_left_idx);
+        return rc;
+    }
+    JnPass pp;
+    uint64_t* mp = nullptr;
+    {
+        const int ge = (int)std::min<int64_t>((b.t.cap + 2 + 255) / 256, 256 * 32);
+        jn_inline_kernel<<<ge, 256, 0, s>>>(b.t, dev_col(*right_payload));
+        PLGPU_HIP(hipGetLastError());
+    }
+    rc = jn_pass_alloc(left_key->length, &pp, s);
+    if (!rc) rc = dev_alloc((void**)&mp, std::max<int64_t>(left_key->length, 1) * 8, s);
+    if (!rc) {
+        const DevCol pk = as_dev(left_key);
+        const int g = jn_pass_grid(pp);
+        if (pk.validity)
+            jn_probe_match_kernel<true, JM_INNER, false, true><<<g, kJnThreads, 0, s>>>(
+                pk, pp.np, b.t, neq, pp.m, pp.tcount, pp.ntiles, nullptr, mp);
+        else
+            jn_probe_match_kernel<false, JM_INNER, false, true><<<g, kJnThreads, 0, s>>>(
+                pk, pp.np, b.t, neq, pp.m, pp.tcount, pp.ntiles, nullptr, mp);
+        rc = jn_pass_scan(&pp, s, "join probe match (row-format table)");
+    }
+    if (!rc && pp.total >= 0xFFFFFFFFull) rc = fail(PLGPU_ERR_CAPACITY, "join output exceeds the u32 index space");
+    if (!rc) rc = make_owned_column(out_left_idx, PLGPU_U32, (int64_t)pp.total, false, s);
+    if (!rc) rc = make_owned_column(out_right_payload, right_payload->dtype, (int64_t)pp.total, false, s);
+    if (!rc && pp.total > 0) {
+        jn_inline_emit_kernel<<<jn_pass_grid(pp), kJnThreads, 0, s>>>(pp.np, pp.m, mp, pp.toff, pp.ntiles,
+                                                                     (uint32_t*)out_left_idx->values,
+                                                                     (uint64_t*)out_right_payload->values);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) rc = hip_fail(e, "join emit (row-format table)");
+    }
+    if (!rc) {
+        const hipError_t e = hipStreamSynchronize(s);
+        if (e != hipSuccess) rc = hip_fail(e, "join (row-format table)");
+    }
+    dev_free(mp, s);
+    jn_pass_free(pp, s);
+    jn_free(b, s);
+    if (rc) {
+        plgpu_column_release(out_left_idx);
+        plgpu_column_release(out_right_payload);
+    }
+    return rc;
 }
 
 PLGPU_API int plgpu_join_inner_multi(const plgpu_column* left_keys, const plgpu_column* right_keys, int32_t nkeys,

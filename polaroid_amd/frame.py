@@ -1504,6 +1504,27 @@ def _join(left: DataFrame, right: DataFrame, left_on: str | tuple, right_on: str
                 f"join keys must have the same dtype on the GPU executor (got {lk.dtype} and {rk.dtype})")
     li, ri = N.Column(), N.Column()
     order, val, hw = N.JOIN_ORDER[maintain_order], N.JOIN_VALIDATE[validate], N.JOIN_HOW[how]
+    rpay = [n for n in right.columns if n not in rkeys]
+    if (how == "inner" and coalesce is not False and builtins.len(lks) == 1 and builtins.len(rpay) == 1
+            and lks[0].dtype.physical() in INTEGER_DTYPES and right.height <= left.height
+            and maintain_order in (None, "none", "left")):
+        # one right column besides the key: the fused join + take
+        # (plgpu_join_inner_payload: a row-format table when the keys are unique)
+        pc = right._cols[rpay[0]]
+        rv = N.Column()
+        N.check(N.lib().plgpu_join_inner_payload(C.byref(lks[0]._col), C.byref(rks[0]._col), C.byref(pc._col),
+                                                 int(nulls_equal), order, val, C.byref(li), C.byref(rv), None))
+        lidx = Series._from_native("__left_idx", li)
+        out = []
+        if left.columns:
+            cols = (N.Column * builtins.len(left.columns))()
+            N.check(N.lib().plgpu_gather(_col_array([left._cols[n] for n in left.columns]),
+                                         builtins.len(left.columns), C.byref(lidx._col), cols, None))
+            out = [Series._from_native(n, cols[i], left._cols[n]._logical_dtype())
+                   for i, n in enumerate(left.columns)]
+        name = rpay[0] + suffix if rpay[0] in left.columns else rpay[0]
+        out.append(Series._from_native(name, rv, pc._logical_dtype()))
+        return DataFrame(out)
     if builtins.len(lks) == 1 and lks[0].dtype.physical() in INTEGER_DTYPES:
         N.check(N.lib().plgpu_join(C.byref(lks[0]._col), C.byref(rks[0]._col), hw, int(nulls_equal), order, val,
                                    C.byref(li), C.byref(ri), None))
