@@ -463,20 +463,22 @@ int plgpu_join_inner(const plgpu_column* left_key, const plgpu_column* right_key
                      int32_t nulls_equal, int32_t maintain_order, int32_t validate,
                      plgpu_column* out_left_idx, plgpu_column* out_right_idx, void* stream);
 
-/* Inner join on one integer key returning the left row indices and the right
- * side's one payload column gathered at the pairs (pair order as
- * plgpu_join_inner).  The fused form of hash_join_tuples_inner followed by
- * the take of the right frame's single non-key column
- * (polars-ops/src/frame/join/hash_join/single_keys_inner.rs:45 +
- * general.rs:17 _finish_join): with unique right keys and a null-free 8-byte
- * payload the payload rides in the hash table's cells, so the probe returns
- * it and no random gather of the right side follows; other inputs take the
- * pairs + gather route with the same result. */
-int plgpu_join_inner_payload(const plgpu_column* left_key, const plgpu_column* right_key,
-                             const plgpu_column* right_payload, int32_t nulls_equal,
-                             int32_t maintain_order, int32_t validate,
-                             plgpu_column* out_left_idx, plgpu_column* out_right_payload,
-                             void* stream);
+/* Inner join on one integer key plus the take of both frames' columns: the
+ * left frame's `left_cols` and the right frame's `right_cols` (0..8 each,
+ * every one as long as its side's key) at the matching pairs, in the pair
+ * order of plgpu_join_inner; *out_len rows.  The fused form of
+ * polars-ops/src/frame/join/hash_join/single_keys_inner.rs:45
+ * hash_join_tuples_inner followed by _finish_join's takes
+ * (polars-ops/src/frame/join/general.rs:17).  With one right column, unique
+ * right keys and a null-free 8-byte right column the hash table is
+ * row-format (each cell {key, payload}) and the emit pass writes the
+ * payload and the null-free 8-byte left columns straight to their output
+ * rows; other inputs take the pairs + gather route with the same result. */
+int plgpu_join_inner_take(const plgpu_column* left_key, const plgpu_column* right_key,
+                          const plgpu_column* left_cols, int32_t nleft,
+                          const plgpu_column* right_cols, int32_t nright, int32_t nulls_equal,
+                          int32_t maintain_order, int32_t validate, plgpu_column* out_left,
+                          plgpu_column* out_right, int64_t* out_len, void* stream);
 
 /* Inner join on 1..8 key columns per side (pairwise equal dtypes: I64 / I32 /
  * U32 / F64 / BOOL).  Replaces the multi-key branch of the reference's join

@@ -236,7 +236,8 @@ constexpr uint32_t kNullIdx = 0xFFFFFFFFu;  // null index in an output pair
 // an empty cell (a full bucket without the key continues, lane by lane, in
 // the next buckets - rare at load <= 0.6).
 // INLINE (row-format table, unique build keys): a cell holds {key, payload}
-// instead of {key, ref}; a hit writes the payload to mp[r] and m[r] = 0.
+// instead of {key, ref}; every row writes mp[r] (its payload, 0 on a miss)
+// and each wave one 64-bit hit mask into m's buffer.
 template <bool NULLABLE, int MODE, bool MARK, bool INLINE = false>
 __global__ __launch_bounds__(kJnThreads) void jn_probe_match_kernel(DevCol pk, int64_t np, JnTable t,
                                                                   bool nulls_equal, uint32_t* __restrict__ m,
@@ -355,11 +356,13 @@ __global__ __launch_bounds__(kJnThreads) void jn_probe_match_kernel(DevCol pk, i
                 c += (MODE == JM_SEMI) == hit ? 1 : 0;
             } else {
                 if (INLINE) {
-                    if (hit) {
-                        w = 0u;
-                        __builtin_nontemporal_store(pay, mp + r);
-                        c += 1;
-                    }
+                    // dense payload words (0 for a miss) and one hit bit per
+                    // row, ballot words in m's buffer; no match word
+                    __builtin_nontemporal_store(hit ? pay : 0ull, mp + r);
+                    const uint64_t hw = __ballot(hit);
+                    if ((threadIdx.x & 63) == 0) reinterpret_cast<uint64_t*>(m)[r >> 6] = hw;
+                    c += hit ? 1 : 0;
+                    continue;
                 } else if (ref == kRefList) {
                     w = kRefList | (uint32_t)slot;
                     c += t.off[slot + 1] - t.off[slot];
@@ -393,32 +396,45 @@ __global__ void jn_inline_kernel(JnTable t, DevCol pay) {
     }
 }
 
-// Emit of the row-format probe: probe row and payload of every hit, in
-// probe-row order.
-__global__ __launch_bounds__(kJnThreads) void jn_inline_emit_kernel(int64_t np, const uint32_t* __restrict__ m,
-                                                                    const uint64_t* __restrict__ mp,
-                                                                    const uint64_t* __restrict__ tile_off,
-                                                                    int64_t ntiles, uint32_t* __restrict__ out_p,
-                                                                    uint64_t* __restrict__ out_v) {
+// Emit of the row-format probe, fused with the take of the left columns:
+// every hit row's payload and its null-free 8-byte left columns go straight
+// to their output position (probe-row order); the row id too when other
+// left columns are gathered afterwards.
+struct TakeCols {
+    const uint64_t* src[PLGPU_MAX_COLS];
+    uint64_t* dst[PLGPU_MAX_COLS];
+    int32_t n;
+};
+
+template <int NC>
+__global__ __launch_bounds__(kJnThreads) void jn_take_emit_kernel(int64_t np, const uint64_t* __restrict__ mwords,
+                                                                  const uint64_t* __restrict__ mp,
+                                                                  const uint64_t* __restrict__ tile_off,
+                                                                  int64_t ntiles, TakeCols lc,
+                                                                  uint64_t* __restrict__ out_v,
+                                                                  uint32_t* __restrict__ out_idx) {
     __shared__ uint64_t wsum[kJnThreads / 64];
     constexpr int R = kJnTileRows / kJnThreads;
+    const int lane = threadIdx.x & 63;
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        uint32_t w[R];
-#pragma unroll
-        for (int k = 0; k < R; ++k) {
-            const int64_t r = tile * kJnTileRows + (int64_t)k * kJnThreads + threadIdx.x;
-            w[k] = r < np ? __builtin_nontemporal_load(m + r) : kRefNone;
-        }
         uint64_t run = tile_off[tile];
-#pragma unroll
+#pragma unroll 2
         for (int k = 0; k < R; ++k) {
             const int64_t r = tile * kJnTileRows + (int64_t)k * kJnThreads + threadIdx.x;
-            const uint32_t c = w[k] != kRefNone ? 1u : 0u;
+            const int64_t rr = r < np ? r : np - 1;
+            const uint64_t w = mwords[rr >> 6];
+            const uint64_t pv = __builtin_nontemporal_load(mp + rr);
+            uint64_t v[NC > 0 ? NC : 1];
+#pragma unroll
+            for (int j = 0; j < NC; ++j) v[j] = __builtin_nontemporal_load(lc.src[j] + rr);
+            const uint32_t hit = (r < np && ((w >> lane) & 1)) ? 1u : 0u;
             uint64_t total;
-            const uint64_t pos = run + block_excl_scan(c, wsum, total);
-            if (c) {
-                out_p[pos] = (uint32_t)r;
-                __builtin_nontemporal_store(__builtin_nontemporal_load(mp + r), out_v + pos);
+            const uint64_t pos = run + block_excl_scan(hit, wsum, total);
+            if (hit) {
+                out_v[pos] = pv;
+#pragma unroll
+                for (int j = 0; j < NC; ++j) lc.dst[j][pos] = v[j];
+                if (out_idx) out_idx[pos] = (uint32_t)r;
             }
             run += total;
         }
@@ -1660,32 +1676,52 @@ PLGPU_API int plgpu_join_inner(const plgpu_column* left_key, const plgpu_column*
                       out_right_idx, stream);
 }
 
-// Inner join returning the left row indices and the right side's one
-// payload column gathered at the pairs (pairs and order as plgpu_join_inner).
-// When the right side is the build side and its keys are unique, the payload
-// rides in the hash table's cells (a row-format table): the probe's bucket
-// read returns it, so no random gather of the build side follows.  Any other
-// case computes the pairs and gathers.
-PLGPU_API int plgpu_join_inner_payload(const plgpu_column* left_key, const plgpu_column* right_key,
-                                       const plgpu_column* right_payload, int32_t nulls_equal,
-                                       int32_t maintain_order, int32_t validate, plgpu_column* out_left_idx,
-                                       plgpu_column* out_right_payload, void* stream) {
+template <int NC>
+static void jn_take_emit(const JnPass& pp, const TakeCols& lc, uint64_t* mp, uint64_t* out_v, uint32_t* out_idx,
+                         hipStream_t s) {
+    jn_take_emit_kernel<NC><<<jn_pass_grid(pp), kJnThreads, 0, s>>>(pp.np, (const uint64_t*)pp.m, mp, pp.toff,
+                                                                    pp.ntiles, lc, out_v, out_idx);
+}
+
+// Inner join + take: the left frame's columns and the right frame's columns
+// at the matching pairs (pairs and their order as plgpu_join_inner), i.e.
+// the reference's hash_join_tuples_inner followed by _finish_join's takes.
+// With one right column, unique right keys and a null-free 8-byte right
+// column the table is row-format: each cell holds {key, payload}, the
+// probe's bucket read returns the payload, and the emit pass writes it and
+// the null-free 8-byte left columns straight to their output rows -- no
+// index pairs, no random gather of the build side.  Everything else takes
+// pairs + gathers.
+PLGPU_API int plgpu_join_inner_take(const plgpu_column* left_key, const plgpu_column* right_key,
+                                    const plgpu_column* left_cols, int32_t nleft, const plgpu_column* right_cols,
+                                    int32_t nright, int32_t nulls_equal, int32_t maintain_order, int32_t validate,
+                                    plgpu_column* out_left, plgpu_column* out_right, int64_t* out_len,
+                                    void* stream) {
     hipStream_t s = as_stream(stream);
-    if (right_payload == nullptr || out_left_idx == nullptr || out_right_payload == nullptr)
+    if (out_len == nullptr || (nleft > 0 && (left_cols == nullptr || out_left == nullptr)) ||
+        (nright > 0 && (right_cols == nullptr || out_right == nullptr)))
         return fail(PLGPU_ERR_INVALID, "NULL argument");
-    std::memset(out_left_idx, 0, sizeof *out_left_idx);
-    std::memset(out_right_payload, 0, sizeof *out_right_payload);
+    if (nleft < 0 || nleft > PLGPU_MAX_COLS || nright < 0 || nright > PLGPU_MAX_COLS)
+        return fail(PLGPU_ERR_INVALID, "0..8 columns per side");
+    for (int i = 0; i < nleft; ++i) std::memset(&out_left[i], 0, sizeof out_left[i]);
+    for (int i = 0; i < nright; ++i) std::memset(&out_right[i], 0, sizeof out_right[i]);
+    *out_len = 0;
     int rc = check_key(left_key);
     if (!rc) rc = check_key(right_key);
     if (!rc) rc = check_args(PLGPU_JOIN_INNER, maintain_order, validate);
+    for (int i = 0; i < nleft && !rc; ++i)
+        if (left_cols[i].length != left_key->length) rc = fail(PLGPU_ERR_SHAPE, "left column length differs");
+    for (int i = 0; i < nright && !rc; ++i)
+        if (right_cols[i].length != right_key->length) rc = fail(PLGPU_ERR_SHAPE, "right column length differs");
     if (rc) return rc;
-    if (right_payload->length != right_key->length)
-        return fail(PLGPU_ERR_SHAPE, "payload and key lengths differ");
     const bool neq = nulls_equal != 0;
+    auto fused8 = [](const plgpu_column& c) {
+        return c.validity == nullptr && c.dtype != PLGPU_STR && c.dtype != PLGPU_BOOL && dtype_bytes(c.dtype) == 8;
+    };
     const bool order_ok = maintain_order == PLGPU_JOIN_ORDER_NONE || maintain_order == PLGPU_JOIN_ORDER_LEFT;
-    const bool inline_ok = order_ok && (validate == PLGPU_JOIN_VALIDATE_M_M || validate == PLGPU_JOIN_VALIDATE_M_1) &&
-                           right_payload->validity == nullptr && dtype_bytes(right_payload->dtype) == 8 &&
-                           right_payload->dtype != PLGPU_STR && left_key->length >= (int64_t(1) << 16) &&
+    const bool inline_ok = order_ok && nright == 1 && fused8(right_cols[0]) &&
+                           (validate == PLGPU_JOIN_VALIDATE_M_M || validate == PLGPU_JOIN_VALIDATE_M_1) &&
+                           left_key->length >= (int64_t(1) << 16) &&
                            (right_key->length <= left_key->length || maintain_order == PLGPU_JOIN_ORDER_LEFT);
     JnBuilt b;
     bool use_inline = false;
@@ -1695,25 +1731,34 @@ PLGPU_API int plgpu_join_inner_payload(const plgpu_column* left_key, const plgpu
         use_inline = b.max_count <= 1;
         if (!use_inline) jn_free(b, s);
     }
+    auto release_all = [&]() {
+        for (int i = 0; i < nleft; ++i) plgpu_column_release(&out_left[i]);
+        for (int i = 0; i < nright; ++i) plgpu_column_release(&out_right[i]);
+    };
     if (!use_inline) {
-        // pairs, then the gather (duplicate build keys, nullable payloads, ...)
-        plgpu_column ri;
-        rc = join_impl(left_key, right_key, PLGPU_JOIN_INNER, neq, maintain_order, validate, out_left_idx, &ri, s);
+        plgpu_column li, ri;
+        rc = join_impl(left_key, right_key, PLGPU_JOIN_INNER, neq, maintain_order, validate, &li, &ri, s);
         if (rc) return rc;
-        rc = gather_into(*right_payload, (const uint32_t*)ri.values, ri.length, out_right_payload, s);
+        for (int i = 0; i < nleft && !rc; ++i)
+            rc = gather_into(left_cols[i], (const uint32_t*)li.values, li.length, &out_left[i], s);
+        for (int i = 0; i < nright && !rc; ++i)
+            rc = gather_into(right_cols[i], (const uint32_t*)ri.values, ri.length, &out_right[i], s);
         if (!rc) {
             const hipError_t e = hipStreamSynchronize(s);
-            if (e != hipSuccess) rc = hip_fail(e, "join payload gather");
+            if (e != hipSuccess) rc = hip_fail(e, "join take");
         }
+        *out_len = li.length;
+        plgpu_column_release(&li);
         plgpu_column_release(&ri);
-        if (rc) plgpu_column_release(out_left_idx);
+        if (rc) release_all();
         return rc;
     }
     JnPass pp;
     uint64_t* mp = nullptr;
+    uint32_t* idx = nullptr;
     {
         const int ge = (int)std::min<int64_t>((b.t.cap + 2 + 255) / 256, 256 * 32);
-        jn_inline_kernel<<<ge, 256, 0, s>>>(b.t, dev_col(*right_payload));
+        jn_inline_kernel<<<ge, 256, 0, s>>>(b.t, dev_col(right_cols[0]));
         PLGPU_HIP(hipGetLastError());
     }
     rc = jn_pass_alloc(left_key->length, &pp, s);
@@ -1729,27 +1774,54 @@ PLGPU_API int plgpu_join_inner_payload(const plgpu_column* left_key, const plgpu
                 pk, pp.np, b.t, neq, pp.m, pp.tcount, pp.ntiles, nullptr, mp);
         rc = jn_pass_scan(&pp, s, "join probe match (row-format table)");
     }
+    const int64_t total = (int64_t)pp.total;
     if (!rc && pp.total >= 0xFFFFFFFFull) rc = fail(PLGPU_ERR_CAPACITY, "join output exceeds the u32 index space");
-    if (!rc) rc = make_owned_column(out_left_idx, PLGPU_U32, (int64_t)pp.total, false, s);
-    if (!rc) rc = make_owned_column(out_right_payload, right_payload->dtype, (int64_t)pp.total, false, s);
-    if (!rc && pp.total > 0) {
-        jn_inline_emit_kernel<<<jn_pass_grid(pp), kJnThreads, 0, s>>>(pp.np, pp.m, mp, pp.toff, pp.ntiles,
-                                                                     (uint32_t*)out_left_idx->values,
-                                                                     (uint64_t*)out_right_payload->values);
-        const hipError_t e = hipGetLastError();
-        if (e != hipSuccess) rc = hip_fail(e, "join emit (row-format table)");
+    // left columns: fused (null-free 8-byte) or gathered by the row ids
+    TakeCols lc;
+    std::memset(&lc, 0, sizeof lc);
+    bool need_idx = false;
+    for (int i = 0; i < nleft && !rc; ++i) {
+        if (!fused8(left_cols[i])) {
+            need_idx = true;
+            continue;
+        }
+        rc = make_owned_column(&out_left[i], left_cols[i].dtype, total, false, s);
+        if (!rc) {
+            lc.src[lc.n] = (const uint64_t*)left_cols[i].values + left_cols[i].offset;
+            lc.dst[lc.n] = (uint64_t*)out_left[i].values;
+            ++lc.n;
+        }
     }
+    if (!rc) rc = make_owned_column(&out_right[0], right_cols[0].dtype, total, false, s);
+    if (!rc && need_idx) rc = dev_alloc((void**)&idx, std::max<int64_t>(total, 1) * 4, s);
+    if (!rc && total > 0) {
+        uint64_t* ov = (uint64_t*)out_right[0].values;
+        switch (lc.n) {
+        case 0: jn_take_emit<0>(pp, lc, mp, ov, idx, s); break;
+        case 1: jn_take_emit<1>(pp, lc, mp, ov, idx, s); break;
+        case 2: jn_take_emit<2>(pp, lc, mp, ov, idx, s); break;
+        case 3: jn_take_emit<3>(pp, lc, mp, ov, idx, s); break;
+        case 4: jn_take_emit<4>(pp, lc, mp, ov, idx, s); break;
+        case 5: jn_take_emit<5>(pp, lc, mp, ov, idx, s); break;
+        case 6: jn_take_emit<6>(pp, lc, mp, ov, idx, s); break;
+        case 7: jn_take_emit<7>(pp, lc, mp, ov, idx, s); break;
+        default: jn_take_emit<8>(pp, lc, mp, ov, idx, s); break;
+        }
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) rc = hip_fail(e, "join take emit");
+    }
+    for (int i = 0; i < nleft && !rc && need_idx; ++i)
+        if (!fused8(left_cols[i])) rc = gather_into(left_cols[i], idx, total, &out_left[i], s);
     if (!rc) {
         const hipError_t e = hipStreamSynchronize(s);
         if (e != hipSuccess) rc = hip_fail(e, "join (row-format table)");
     }
+    dev_free(idx, s);
     dev_free(mp, s);
     jn_pass_free(pp, s);
     jn_free(b, s);
-    if (rc) {
-        plgpu_column_release(out_left_idx);
-        plgpu_column_release(out_right_payload);
-    }
+    if (rc) release_all();
+    else *out_len = total;
     return rc;
 }
 

@@ -139,49 +139,6 @@ __global__ __launch_bounds__(256) void srt_bits_kernel(const uint64_t* __restric
     }
 }
 
-// One read of the codes for every pass of a onesweep sort: their OR / AND
-// (constant bytes are skipped) and the column-wide histogram of each of the
-// 8 bytes (wave-private LDS histograms, flushed with one global atomic per
-// bin and wave).
-__global__ __launch_bounds__(256) void srt_stats_kernel(const uint64_t* __restrict__ keys, int64_t n,
-                                                        unsigned long long* __restrict__ bits,
-                                                        uint32_t* __restrict__ hist) {
-    __shared__ uint32_t h[4][8][256];
-    const int wv = threadIdx.x >> 6;
-    for (int i = threadIdx.x; i < 4 * 8 * 256; i += blockDim.x) (&h[0][0][0])[i] = 0;
-    __syncthreads();
-    uint64_t o = 0, a = ~0ull;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const uint64_t k = __builtin_nontemporal_load(keys + i);
-        o |= k;
-        a &= k;
-#pragma unroll
-        for (int b = 0; b < 8; ++b) atomicAdd(&h[wv][b][(k >> (8 * b)) & 0xFF], 1u);
-    }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        o |= __shfl_xor(o, off, 64);
-        a &= __shfl_xor(a, off, 64);
-    }
-    if ((threadIdx.x & 63) == 0) {
-        atomicOr(&bits[0], (unsigned long long)o);
-        atomicAnd(&bits[1], (unsigned long long)a);
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < 8 * 256; i += blockDim.x) {
-        const uint32_t c = h[0][0][i] + h[1][0][i] + h[2][0][i] + h[3][0][i];
-        if (c) atomicAdd(&hist[i], c);
-    }
-}
-
-// Exclusive scan of each byte's 256 counts -> global digit bases.
-__global__ __launch_bounds__(256) void srt_bases_kernel(const uint32_t* __restrict__ hist,
-                                                        uint64_t* __restrict__ bases) {
-    __shared__ uint64_t wsum[4];
-    uint64_t total;
-    bases[blockIdx.x * 256 + threadIdx.x] = block_excl_scan(hist[blockIdx.x * 256 + threadIdx.x], wsum, total);
-}
-
 // Representations of the (code, row id) stream between passes:
 //   SEP    - codes u64 + row ids u32 in two buffers (12 B per row);
 //   PACKED - one u64 word (remaining code bits << 32 | row id) once the
@@ -216,34 +173,14 @@ __global__ __launch_bounds__(kSrtThreads) void srt_upsweep_kernel(const uint64_t
 // counts into local positions; the tile is staged in LDS in digit order and
 // written out in runs.  IN_P: input is PACKED.  OUT: SrtOut; a SEP -> PACK
 // transition keeps (code >> cons) & kmask as the remaining code.
-// Onesweep form (ONE): no upsweep.  A workgroup takes the next tile from a
-// ticket counter, so every earlier tile belongs to a running or finished
-// workgroup; thread d publishes the tile's count of digit d, looks back
-// over the earlier tiles' published counts until one carries an inclusive
-// prefix (decoupled look-back), and publishes its own prefix.  Status words
-// are {epoch:16, flag:2, value:46} (flag 1 = count, 2 = inclusive prefix),
-// written and read with agent-scope atomics (coherent across the XCDs'
-// L2s); a word of another epoch (an earlier pass) reads as not ready.  The
-// wait is bounded: on timeout the tile reports `err` (the host fails the
-// sort) instead of hanging.
-struct SrtOne {
-    uint64_t* status;          // ntiles * 256 words
-    unsigned int* ticket;
-    const uint64_t* dbase;     // this pass's 256 global digit bases
-    unsigned int* err;
-    uint32_t epoch;
-};
-constexpr uint64_t kSrtValMask = (1ull << 46) - 1;
-constexpr uint32_t kSrtSpinLimit = 1u << 22;
-
-template <bool IN_P, int OUT, bool ONE = false>
+template <bool IN_P, int OUT>
 __global__ __launch_bounds__(kSrtThreads) void srt_downsweep_kernel(const uint64_t* __restrict__ keys_in,
                                                                     const uint32_t* __restrict__ idx_in, int64_t n,
                                                                     int shift, int64_t ntiles,
                                                                     const uint64_t* __restrict__ off,
                                                                     uint64_t* __restrict__ keys_out,
                                                                     uint32_t* __restrict__ idx_out, int cons,
-                                                                    uint64_t kmask, SrtOne one = SrtOne{}) {
+                                                                    uint64_t kmask) {
     constexpr int NW = kSrtThreads / 64;
     constexpr int ROWS = kSrtTile / kSrtThreads;  // rows of 64 per wave (16)
     __shared__ uint64_t skey[OUT == SRT_IDX ? 1 : kSrtTile];
@@ -253,15 +190,8 @@ __global__ __launch_bounds__(kSrtThreads) void srt_downsweep_kernel(const uint64
     __shared__ uint64_t gbase[256];  // global position of local slot 0 of each digit run
     __shared__ uint32_t cnt[NW][256];
     __shared__ uint64_t wsum[NW];
-    __shared__ int64_t tile_sh;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    int64_t tile = blockIdx.x;
-    if (ONE) {
-        if (tid == 0) tile_sh = (int64_t)atomicAdd(one.ticket, 1u);
-        __syncthreads();
-        tile = tile_sh;
-    }
-    const int64_t base = tile * kSrtTile;
+    const int64_t base = (int64_t)blockIdx.x * kSrtTile;
     const int m = n - base < kSrtTile ? (int)(n - base) : kSrtTile;
     for (int w = 0; w < NW; ++w) cnt[w][tid] = 0;
     uint64_t k[ROWS];
@@ -304,37 +234,7 @@ __global__ __launch_bounds__(kSrtThreads) void srt_downsweep_kernel(const uint64
         uint64_t total;
         const uint32_t ds = (uint32_t)block_excl_scan(t, wsum, total);
         dstart[tid] = ds;
-        if (ONE) {
-            const uint64_t tag = (uint64_t)one.epoch << 48;
-            uint64_t* st = one.status + tile * 256 + tid;
-            __hip_atomic_store(st, tag | ((tile == 0 ? 2ull : 1ull) << 46) | t, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-            uint64_t excl = 0;
-            if (tile > 0) {
-                int64_t q = tile - 1;
-                uint32_t spins = 0;
-                while (true) {
-                    const uint64_t v =
-                        __hip_atomic_load(one.status + q * 256 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const uint32_t fl = (uint32_t)(v >> 48) == one.epoch ? (uint32_t)((v >> 46) & 3u) : 0u;
-                    if (fl == 0) {
-                        if (++spins > kSrtSpinLimit) {
-                            atomicOr(one.err, 1u);
-                            break;
-                        }
-                        __builtin_amdgcn_s_sleep(1);
-                        continue;
-                    }
-                    excl += v & kSrtValMask;
-                    if (fl == 2 || q == 0) break;
-                    --q;
-                }
-                __hip_atomic_store(st, tag | (2ull << 46) | (excl + t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            gbase[tid] = one.dbase[tid] + excl - ds;
-        } else {
-            gbase[tid] = off[(int64_t)tid * ntiles + blockIdx.x] - ds;
-        }
+        gbase[tid] = off[(int64_t)tid * ntiles + blockIdx.x] - ds;
     }
     __syncthreads();
 #pragma unroll
@@ -444,34 +344,14 @@ __global__ void srt_place_nulls_kernel(const uint32_t* __restrict__ nulls, int64
 using namespace plgpu;
 
 // Scratch of the radix passes over n codes.
-// Onesweep (default) or, with PLGPU_SORT_UPSWEEP set, the upsweep / scan /
-// downsweep passes (kept for A/B runs).
-static bool srt_onesweep() {
-    static const bool on = getenv("PLGPU_SORT_UPSWEEP") == nullptr;
-    return on;
-}
-
 struct SrtScratch {
     uint32_t* cnt = nullptr;
     uint64_t* off = nullptr;
     uint64_t* part = nullptr;
     unsigned long long* hist = nullptr;
-    // onesweep: per-tile status words, ticket + error words, byte histograms
-    // and global digit bases
-    uint64_t* status = nullptr;
-    unsigned int* ctl = nullptr;
-    uint32_t* bhist = nullptr;
-    uint64_t* bases = nullptr;
     int alloc(int64_t n, hipStream_t s) {
         const int64_t ntiles = (n + kSrtTile - 1) / kSrtTile;
         int rc = dev_alloc((void**)&hist, 16, s);
-        if (srt_onesweep()) {
-            if (!rc && n > 0) rc = dev_alloc((void**)&status, ntiles * 256 * 8, s);
-            if (!rc) rc = dev_alloc((void**)&ctl, 16, s);
-            if (!rc) rc = dev_alloc((void**)&bhist, 8 * 256 * 4, s);
-            if (!rc) rc = dev_alloc((void**)&bases, 8 * 256 * 8, s);
-            return rc;
-        }
         if (!rc && n > 0) rc = dev_alloc((void**)&cnt, ntiles * 256 * 4, s);
         if (!rc && n > 0) rc = dev_alloc((void**)&off, (ntiles * 256 + 1) * 8, s);
         if (!rc && n > 0) rc = dev_alloc((void**)&part, ((ntiles * 256 + kScanChunk - 1) / kScanChunk + 1) * 8, s);
@@ -482,18 +362,10 @@ struct SrtScratch {
         dev_free(off, s);
         dev_free(part, s);
         dev_free(hist, s);
-        dev_free(status, s);
-        dev_free(ctl, s);
-        dev_free(bhist, s);
-        dev_free(bases, s);
         cnt = nullptr;
         off = nullptr;
         part = nullptr;
         hist = nullptr;
-        status = nullptr;
-        ctl = nullptr;
-        bhist = nullptr;
-        bases = nullptr;
     }
 };
 
@@ -503,38 +375,20 @@ struct SrtScratch {
 // to the PACKED representation as soon as the remaining code bits fit 32.
 template <bool IN_P, int OUT>
 static void srt_down(const uint64_t* ki, const uint32_t* ii, int64_t nv, int shift, int64_t ntiles,
-                     const uint64_t* off, uint64_t* ko, uint32_t* io, int cons, uint64_t kmask, hipStream_t s,
-                     const SrtOne* one = nullptr) {
-    if (one)
-        srt_downsweep_kernel<IN_P, OUT, true><<<(unsigned)ntiles, kSrtThreads, 0, s>>>(ki, ii, nv, shift, ntiles, off,
-                                                                                    ko, io, cons, kmask, *one);
-    else
-        srt_downsweep_kernel<IN_P, OUT><<<(unsigned)ntiles, kSrtThreads, 0, s>>>(ki, ii, nv, shift, ntiles, off, ko,
-                                                                              io, cons, kmask);
+                     const uint64_t* off, uint64_t* ko, uint32_t* io, int cons, uint64_t kmask, hipStream_t s) {
+    srt_downsweep_kernel<IN_P, OUT><<<(unsigned)ntiles, kSrtThreads, 0, s>>>(ki, ii, nv, shift, ntiles, off, ko, io,
+                                                                          cons, kmask);
 }
 
 static int radix_passes(uint64_t* keys[2], uint32_t* idx[2], int64_t nv, int& cur, SrtScratch& sc, hipStream_t s,
                         bool ids_implicit = false) {
     if (nv <= 0) return PLGPU_OK;
     const int cus = 256;
-    const bool one = srt_onesweep();
     unsigned long long h[2] = {0ull, ~0ull};
     hipError_t e = hipMemcpyAsync(sc.hist, h, 16, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess && one) e = hipMemsetAsync(sc.bhist, 0, 8 * 256 * 4, s);
     if (e == hipSuccess) {
-        if (one)
-            srt_stats_kernel<<<(unsigned)std::min<int64_t>((nv + 255) / 256, cus * 4), 256, 0, s>>>(keys[cur], nv,
-                                                                                                 sc.hist, sc.bhist);
-        else
-            srt_bits_kernel<<<(unsigned)std::min<int64_t>((nv + 255) / 256, cus * 8), 256, 0, s>>>(keys[cur], nv,
-                                                                                                sc.hist);
+        srt_bits_kernel<<<(unsigned)std::min<int64_t>((nv + 255) / 256, cus * 8), 256, 0, s>>>(keys[cur], nv, sc.hist);
         e = hipGetLastError();
-    }
-    if (e == hipSuccess && one) {
-        srt_bases_kernel<<<8, 256, 0, s>>>(sc.bhist, sc.bases);
-        e = hipGetLastError();
-        if (e == hipSuccess) e = hipMemsetAsync(sc.status, 0, ((nv + kSrtTile - 1) / kSrtTile) * 256 * 8, s);
-        if (e == hipSuccess) e = hipMemsetAsync(sc.ctl, 0, 16, s);
     }
     if (e == hipSuccess) e = hipMemcpyAsync(h, sc.hist, 16, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
@@ -559,18 +413,9 @@ static int radix_passes(uint64_t* keys[2], uint32_t* idx[2], int64_t nv, int& cu
         const int S = 8 * bytes[j];
         const int shift = packed ? 32 + S - cons : S;
         const uint32_t* ii = (ids_implicit && j == 0) ? nullptr : idx[cur];
-        SrtOne o1;
-        if (one) {
-            // the ticket restarts each pass; the epoch tells this pass's
-            // status words from the last one's
-            o1 = SrtOne{sc.status, sc.ctl, sc.bases + 256 * bytes[j], sc.ctl + 1, (uint32_t)(j + 1)};
-            e = hipMemsetAsync(sc.ctl, 0, 4, s);
-        } else {
-            srt_upsweep_kernel<<<(unsigned)ntiles, kSrtThreads, 0, s>>>(keys[cur], nv, shift, ntiles, sc.cnt);
-            e = scan_exclusive<uint32_t>(sc.cnt, ntiles * 256, sc.off, sc.part, s);
-        }
+        srt_upsweep_kernel<<<(unsigned)ntiles, kSrtThreads, 0, s>>>(keys[cur], nv, shift, ntiles, sc.cnt);
+        e = scan_exclusive<uint32_t>(sc.cnt, ntiles * 256, sc.off, sc.part, s);
         if (e != hipSuccess) return hip_fail(e, "sort scan");
-        const SrtOne* op = one ? &o1 : nullptr;
         const bool last = j == nb - 1;
         const int ncons = S + 8;
         const bool to_pack = !packed && !last && !nopack && hi_bits - ncons <= 32;
@@ -578,27 +423,20 @@ static int radix_passes(uint64_t* keys[2], uint32_t* idx[2], int64_t nv, int& cu
         uint64_t* ko = keys[cur ^ 1];
         uint32_t* io = idx[cur ^ 1];
         if (packed) {
-            if (last) srt_down<true, SRT_IDX>(keys[cur], ii, nv, shift, ntiles, sc.off, ko, io, 0, 0, s, op);
-            else srt_down<true, SRT_PACK>(keys[cur], ii, nv, shift, ntiles, sc.off, ko, io, 0, 0, s, op);
+            if (last) srt_down<true, SRT_IDX>(keys[cur], ii, nv, shift, ntiles, sc.off, ko, io, 0, 0, s);
+            else srt_down<true, SRT_PACK>(keys[cur], ii, nv, shift, ntiles, sc.off, ko, io, 0, 0, s);
         } else if (last) {
-            srt_down<false, SRT_IDX>(keys[cur], ii, nv, shift, ntiles, sc.off, ko, io, 0, 0, s, op);
+            srt_down<false, SRT_IDX>(keys[cur], ii, nv, shift, ntiles, sc.off, ko, io, 0, 0, s);
         } else if (to_pack) {
-            srt_down<false, SRT_PACK>(keys[cur], ii, nv, shift, ntiles, sc.off, ko, io, ncons, kmask, s, op);
+            srt_down<false, SRT_PACK>(keys[cur], ii, nv, shift, ntiles, sc.off, ko, io, ncons, kmask, s);
             packed = true;
             cons = ncons;
         } else {
-            srt_down<false, SRT_SEP>(keys[cur], ii, nv, shift, ntiles, sc.off, ko, io, 0, 0, s, op);
+            srt_down<false, SRT_SEP>(keys[cur], ii, nv, shift, ntiles, sc.off, ko, io, 0, 0, s);
         }
         e = hipGetLastError();
         if (e != hipSuccess) return hip_fail(e, "sort pass");
         cur ^= 1;
-    }
-    if (one) {
-        unsigned int err = 0;
-        e = hipMemcpyAsync(&err, sc.ctl + 1, 4, hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
-        if (e != hipSuccess) return hip_fail(e, "sort status");
-        if (err) return fail(PLGPU_ERR_HIP, "sort: a tile's look-back timed out");
     }
     return PLGPU_OK;
 }

@@ -1505,25 +1505,23 @@ def _join(left: DataFrame, right: DataFrame, left_on: str | tuple, right_on: str
     li, ri = N.Column(), N.Column()
     order, val, hw = N.JOIN_ORDER[maintain_order], N.JOIN_VALIDATE[validate], N.JOIN_HOW[how]
     rpay = [n for n in right.columns if n not in rkeys]
-    if (how == "inner" and coalesce is not False and builtins.len(lks) == 1 and builtins.len(rpay) == 1
-            and lks[0].dtype.physical() in INTEGER_DTYPES and right.height <= left.height
-            and maintain_order in (None, "none", "left")):
-        # one right column besides the key: the fused join + take
-        # (plgpu_join_inner_payload: a row-format table when the keys are unique)
-        pc = right._cols[rpay[0]]
-        rv = N.Column()
-        N.check(N.lib().plgpu_join_inner_payload(C.byref(lks[0]._col), C.byref(rks[0]._col), C.byref(pc._col),
-                                                 int(nulls_equal), order, val, C.byref(li), C.byref(rv), None))
-        lidx = Series._from_native("__left_idx", li)
-        out = []
-        if left.columns:
-            cols = (N.Column * builtins.len(left.columns))()
-            N.check(N.lib().plgpu_gather(_col_array([left._cols[n] for n in left.columns]),
-                                         builtins.len(left.columns), C.byref(lidx._col), cols, None))
-            out = [Series._from_native(n, cols[i], left._cols[n]._logical_dtype())
-                   for i, n in enumerate(left.columns)]
-        name = rpay[0] + suffix if rpay[0] in left.columns else rpay[0]
-        out.append(Series._from_native(name, rv, pc._logical_dtype()))
+    if (how == "inner" and coalesce is not False and builtins.len(lks) == 1
+            and lks[0].dtype.physical() in INTEGER_DTYPES
+            and builtins.len(left.columns) <= N.MAX_COLS and builtins.len(rpay) <= N.MAX_COLS):
+        # join + the takes in one call (plgpu_join_inner_take): a row-format
+        # table when one unique-keyed right column rides along
+        lc = [left._cols[n] for n in left.columns]
+        rc_ = [right._cols[n] for n in rpay]
+        ol = (N.Column * max(1, builtins.len(lc)))()
+        orr = (N.Column * max(1, builtins.len(rc_)))()
+        nout = C.c_int64(0)
+        N.check(N.lib().plgpu_join_inner_take(C.byref(lks[0]._col), C.byref(rks[0]._col), _col_array(lc),
+                                              builtins.len(lc), _col_array(rc_), builtins.len(rc_),
+                                              int(nulls_equal), order, val, ol, orr, C.byref(nout), None))
+        out = [Series._from_native(n, ol[i], left._cols[n]._logical_dtype()) for i, n in enumerate(left.columns)]
+        for i, n in enumerate(rpay):
+            out.append(Series._from_native(n + suffix if n in left.columns else n, orr[i],
+                                           right._cols[n]._logical_dtype()))
         return DataFrame(out)
     if builtins.len(lks) == 1 and lks[0].dtype.physical() in INTEGER_DTYPES:
         N.check(N.lib().plgpu_join(C.byref(lks[0]._col), C.byref(rks[0]._col), hw, int(nulls_equal), order, val,
