@@ -84,6 +84,11 @@ __global__ void jn_init_kernel(JnTable t, uint32_t* cnt) {
     }
 }
 
+__global__ void jn_empty_kernel(JnTable t) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < t.cap; i += (int64_t)gridDim.x * blockDim.x)
+        jn_key(t, i) = kEmptyKey;
+}
+
 // Insert the build keys; bslot[i] = slot of row i (kNoSlot: a null key that
 // never matches).  status[0] counts rows that found no free slot.
 __global__ void jn_build_kernel(DevCol bk, int64_t nb, JnTable t, bool nulls_equal, uint32_t* __restrict__ cnt,
@@ -339,8 +344,9 @@ __global__ __launch_bounds__(kJnThreads) void jn_probe_match_kernel(DevCol pk, i
             }
             if (slot >= t.cap) {  // null / INT64_MIN key slots
                 if (INLINE) {
-                    ref = t.off[slot + 1] > t.off[slot] ? 0u : kRefNone;
+                    // row-format special cells: key word 1 = occupied
                     const uint4 x = t.cells[slot];
+                    ref = (x.x == 1u && x.y == 0u) ? 0u : kRefNone;
                     pay = (uint64_t)x.z | ((uint64_t)x.w << 32);
                 } else {
                     ref = jn_ref(t, slot);
@@ -382,17 +388,61 @@ __global__ __launch_bounds__(kJnThreads) void jn_probe_match_kernel(DevCol pk, i
     }
 }
 
-// Row-format table: every occupied cell's ref word (a unique build row)
-// is replaced by that row's 8-byte payload (cells {key, payload}).
-__global__ void jn_inline_kernel(JnTable t, DevCol pay) {
-    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < t.cap + 2;
-         s += (int64_t)gridDim.x * blockDim.x) {
-        const uint32_t ref = jn_ref(t, s);
-        if (ref >= kRefList) continue;  // empty (kRefNone); lists never reach here
-        const uint64_t v = dev_load(pay, ref);
-        uint32_t* c = (uint32_t*)&t.cells[s];
-        c[2] = (uint32_t)v;
-        c[3] = (uint32_t)(v >> 32);
+// Row-format build in one pass (no CSR): insert each build key with its
+// payload; a key met twice sets status[1] (the caller falls back to the
+// general build), a row that finds no free cell status[0].  The two special
+// cells (null key, INT64_MIN key) count their rows in status[2] / [3] and
+// carry key word 1 once occupied.
+__global__ void jn_build_rowformat_kernel(DevCol bk, int64_t nb, JnTable t, bool nulls_equal, DevCol pay,
+                                          unsigned long long* status) {
+    const uint64_t mask = (uint64_t)t.cap - 1;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nb; i += (int64_t)gridDim.x * blockDim.x) {
+        int64_t slot = -1;
+        if (!dev_valid(bk, i)) {
+            if (!nulls_equal) continue;
+            slot = t.cap;
+        } else {
+            const uint64_t key = dev_load(bk, i);
+            if (key == kEmptyKey) {
+                slot = t.cap + 1;
+            } else {
+                uint64_t s = (uint64_t)hash_slot(key, t.bbits) * kBktCells;
+                bool placed = false;
+                for (int p = 0; p < kJnProbeLimit; ++p, s = (s + 1) & mask) {
+                    uint64_t k = __hip_atomic_load(&jn_key(t, s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (k == kEmptyKey) {
+                        k = atomicCAS((unsigned long long*)&jn_key(t, s), (unsigned long long)kEmptyKey,
+                                      (unsigned long long)key);
+                        if (k == kEmptyKey) {
+                            const uint64_t v = dev_load(pay, i);
+                            uint32_t* c = (uint32_t*)&t.cells[s];
+                            c[2] = (uint32_t)v;
+                            c[3] = (uint32_t)(v >> 32);
+                            placed = true;
+                            break;
+                        }
+                    }
+                    if (k == key) {
+                        atomicOr(&status[1], 1ull);  // duplicate key
+                        placed = true;
+                        break;
+                    }
+                }
+                if (!placed) atomicAdd(&status[0], 1ull);
+                continue;
+            }
+        }
+        // special cell: the first row claims it, a second is a duplicate
+        if (atomicAdd(&status[2 + (slot - t.cap)], 1ull) == 0) {
+            const uint64_t v = dev_load(pay, i);
+            uint32_t* c = (uint32_t*)&t.cells[slot];
+            c[0] = 1u;
+            c[1] = 0u;
+            c[2] = (uint32_t)v;
+            c[3] = (uint32_t)(v >> 32);
+        } else {
+            atomicOr(&status[1], 1ull);
+        }
     }
 }
 
@@ -413,31 +463,56 @@ __global__ __launch_bounds__(kJnThreads) void jn_take_emit_kernel(int64_t np, co
                                                                   int64_t ntiles, TakeCols lc,
                                                                   uint64_t* __restrict__ out_v,
                                                                   uint32_t* __restrict__ out_idx) {
-    __shared__ uint64_t wsum[kJnThreads / 64];
+    // A tile's 64 hit words (row chunk k, wave w -> word 4k + w, row order)
+    // are scanned once; a row's output position is then the tile offset +
+    // its word's prefix + the hits below it in the word.
     constexpr int R = kJnTileRows / kJnThreads;
-    const int lane = threadIdx.x & 63;
+    constexpr int NW = kJnThreads / 64;
+    constexpr int U = NC <= 2 ? 8 : 4;  // row chunks whose loads are issued together
+    __shared__ uint64_t words[kJnTileRows / 64];
+    __shared__ uint32_t prefix[kJnTileRows / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        uint64_t run = tile_off[tile];
-#pragma unroll 2
-        for (int k = 0; k < R; ++k) {
-            const int64_t r = tile * kJnTileRows + (int64_t)k * kJnThreads + threadIdx.x;
-            const int64_t rr = r < np ? r : np - 1;
-            const uint64_t w = mwords[rr >> 6];
-            const uint64_t pv = __builtin_nontemporal_load(mp + rr);
-            uint64_t v[NC > 0 ? NC : 1];
+        if (threadIdx.x < kJnTileRows / 64) {
+            const int64_t wi = tile * (kJnTileRows / 64) + threadIdx.x;
+            const uint64_t w = wi * 64 < np ? mwords[wi] : 0ull;
+            uint32_t x = (uint32_t)__popcll(w), c = x;
 #pragma unroll
-            for (int j = 0; j < NC; ++j) v[j] = __builtin_nontemporal_load(lc.src[j] + rr);
-            const uint32_t hit = (r < np && ((w >> lane) & 1)) ? 1u : 0u;
-            uint64_t total;
-            const uint64_t pos = run + block_excl_scan(hit, wsum, total);
-            if (hit) {
-                out_v[pos] = pv;
-#pragma unroll
-                for (int j = 0; j < NC; ++j) lc.dst[j][pos] = v[j];
-                if (out_idx) out_idx[pos] = (uint32_t)r;
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t y = __shfl_up(x, off, 64);
+                if (lane >= off) x += y;
             }
-            run += total;
+            words[threadIdx.x] = w;
+            prefix[threadIdx.x] = x - c;
         }
+        __syncthreads();
+        const uint64_t run = tile_off[tile];
+        for (int k0 = 0; k0 < R; k0 += U) {
+            uint64_t pv[U], v[U][NC > 0 ? NC : 1];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t r = tile * kJnTileRows + (int64_t)(k0 + u) * kJnThreads + threadIdx.x;
+                const int64_t rr = r < np ? r : np - 1;
+                pv[u] = __builtin_nontemporal_load(mp + rr);
+#pragma unroll
+                for (int j = 0; j < NC; ++j) v[u][j] = __builtin_nontemporal_load(lc.src[j] + rr);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int wi = (k0 + u) * NW + wave;
+                const uint64_t w = words[wi];
+                if ((w >> lane) & 1) {
+                    const uint64_t pos = run + prefix[wi] + (uint32_t)__popcll(w & lt);
+                    out_v[pos] = pv[u];
+#pragma unroll
+                    for (int j = 0; j < NC; ++j) lc.dst[j][pos] = v[u][j];
+                    if (out_idx)
+                        out_idx[pos] = (uint32_t)(tile * kJnTileRows + (int64_t)(k0 + u) * kJnThreads + threadIdx.x);
+                }
+            }
+        }
+        __syncthreads();
     }
 }
 
@@ -1127,6 +1202,63 @@ static int jn_build(const plgpu_column* key, bool nulls_equal, bool ordered, JnB
     return PLGPU_OK;
 }
 
+// Row-format table over a unique-keyed build side (jn_build_rowformat_kernel);
+// *unique = false (and nothing built) when a key repeats.
+static int jn_build_rowformat(const plgpu_column* key, const plgpu_column* pay, bool nulls_equal, JnBuilt* out,
+                              bool* unique, hipStream_t s) {
+    const int64_t nb = key->length;
+    int bits = std::max(10, log2_ceil64((nb * 5 + 2) / 3));  // load <= 0.6
+    unsigned long long* status = nullptr;
+    int rc = dev_alloc((void**)&status, 32, s);
+    *unique = true;
+    JnBuilt b;
+    for (int attempt = 0; !rc; ++attempt) {
+        b.t.bits = bits;
+        b.t.bbits = bits - 3;
+        b.t.cap = int64_t(1) << bits;
+        const int64_t ne = b.t.cap + 2;
+        if ((rc = dev_alloc((void**)&b.t.cells, ne * 16, s))) break;
+        hipError_t e = hipMemsetAsync(status, 0, 32, s);
+        // keys EMPTY everywhere; special cells all zero (unoccupied)
+        if (e == hipSuccess) e = hipMemsetAsync(b.t.cells, 0x00, ne * 16, s);
+        if (e == hipSuccess) {
+            const int gi = (int)std::min<int64_t>((ne + 255) / 256, 256 * 32);
+            jn_empty_kernel<<<gi, 256, 0, s>>>(b.t);
+            const int gb = (int)std::min<int64_t>((nb + 255) / 256, 256 * 32);
+            if (nb > 0) jn_build_rowformat_kernel<<<gb, 256, 0, s>>>(dev_col(*key), nb, b.t, nulls_equal, dev_col(*pay),
+                                                                     status);
+            e = hipGetLastError();
+        }
+        unsigned long long st[4] = {0, 0, 0, 0};
+        if (e == hipSuccess) e = hipMemcpyAsync(st, status, 32, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) {
+            rc = hip_fail(e, "join row-format build");
+            break;
+        }
+        if (st[1]) {
+            *unique = false;
+            break;
+        }
+        if (st[0] == 0) break;
+        if (attempt >= 3) {
+            rc = fail(PLGPU_ERR_CAPACITY, "join build table did not converge");
+            break;
+        }
+        dev_free(b.t.cells, s);
+        b.t.cells = nullptr;
+        bits += 2;
+    }
+    dev_free(status, s);
+    if (rc || !*unique) {
+        jn_free(b, s);
+        return rc;
+    }
+    b.rows = nb;
+    *out = b;
+    return PLGPU_OK;
+}
+
 // One probe pass: per-row match words, per-tile output counts and their
 // exclusive scan; `total` output rows.
 struct JnPass {
@@ -1726,10 +1858,8 @@ PLGPU_API int plgpu_join_inner_take(const plgpu_column* left_key, const plgpu_co
     JnBuilt b;
     bool use_inline = false;
     if (inline_ok) {
-        rc = jn_build(right_key, neq, false, &b, s);
+        rc = jn_build_rowformat(right_key, &right_cols[0], neq, &b, &use_inline, s);
         if (rc) return rc;
-        use_inline = b.max_count <= 1;
-        if (!use_inline) jn_free(b, s);
     }
     auto release_all = [&]() {
         for (int i = 0; i < nleft; ++i) plgpu_column_release(&out_left[i]);
@@ -1756,11 +1886,6 @@ PLGPU_API int plgpu_join_inner_take(const plgpu_column* left_key, const plgpu_co
     JnPass pp;
     uint64_t* mp = nullptr;
     uint32_t* idx = nullptr;
-    {
-        const int ge = (int)std::min<int64_t>((b.t.cap + 2 + 255) / 256, 256 * 32);
-        jn_inline_kernel<<<ge, 256, 0, s>>>(b.t, dev_col(right_cols[0]));
-        PLGPU_HIP(hipGetLastError());
-    }
     rc = jn_pass_alloc(left_key->length, &pp, s);
     if (!rc) rc = dev_alloc((void**)&mp, std::max<int64_t>(left_key->length, 1) * 8, s);
     if (!rc) {
