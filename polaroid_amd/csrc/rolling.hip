@@ -309,7 +309,7 @@ __global__ __launch_bounds__(kRlThreads) void rl_tile_kernel(RlParams p) {
 // 64-row chunks sit in a per-wave LDS ring, so clipped and centred windows
 // read their two prefixes the same way.
 constexpr int kRwMaxW = 64;
-constexpr int kRwChunks = 16;              // output chunks of 64 per wave
+constexpr int kRwChunks = 8;               // output chunks of 64 per wave
 constexpr int kRwWaves = 4;                // waves per workgroup
 constexpr int kRwOut = 64 * kRwChunks;     // outputs per wave
 constexpr int kRwRing = 256;               // 4 chunks of prefixes
