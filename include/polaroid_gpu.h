@@ -480,6 +480,16 @@ int plgpu_join_inner_take(const plgpu_column* left_key, const plgpu_column* righ
                           int32_t maintain_order, int32_t validate, plgpu_column* out_left,
                           plgpu_column* out_right, int64_t* out_len, void* stream);
 
+/* plgpu_join_inner_take on 1..8 key columns per side (as plgpu_join_inner_multi):
+ * integer / Boolean keys whose ranges pack into one exact Int64 take the
+ * single-key route on the packed keys (row-format table included); other
+ * keys compute the verified pairs and gather. */
+int plgpu_join_inner_take_multi(const plgpu_column* left_keys, const plgpu_column* right_keys,
+                                int32_t nkeys, const plgpu_column* left_cols, int32_t nleft,
+                                const plgpu_column* right_cols, int32_t nright, int32_t nulls_equal,
+                                int32_t maintain_order, int32_t validate, plgpu_column* out_left,
+                                plgpu_column* out_right, int64_t* out_len, void* stream);
+
 /* Inner join on 1..8 key columns per side (pairwise equal dtypes: I64 / I32 /
  * U32 / F64 / BOOL).  Replaces the multi-key branch of the reference's join
  * (polars-ops/src/frame/join/mod.rs:625 prepare_keys_multiple: both sides'

@@ -134,6 +134,8 @@ SIGNATURES = {
     "plgpu_join_inner": (C.c_int, [_COLP, _COLP, C.c_int32, C.c_int32, C.c_int32, _COLP, _COLP, _P]),
     "plgpu_join_inner_take": (C.c_int, [_COLP, _COLP, _COLP, C.c_int32, _COLP, C.c_int32, C.c_int32, C.c_int32,
                                         C.c_int32, _COLP, _COLP, C.POINTER(C.c_int64), _P]),
+    "plgpu_join_inner_take_multi": (C.c_int, [_COLP, _COLP, C.c_int32, _COLP, C.c_int32, _COLP, C.c_int32, C.c_int32,
+                                              C.c_int32, C.c_int32, _COLP, _COLP, C.POINTER(C.c_int64), _P]),
     "plgpu_join": (C.c_int, [_COLP, _COLP, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _COLP, _COLP, _P]),
     "plgpu_join_multi": (C.c_int, [_COLP, _COLP, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _COLP,
                                    _COLP, _P]),

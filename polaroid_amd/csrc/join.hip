@@ -2249,3 +2249,106 @@ PLGPU_API int plgpu_coalesce(const plgpu_column* a, const plgpu_column* b, plgpu
     }
     return PLGPU_OK;
 }
+
+// plgpu_join_inner_take over 1..8 key columns: integer / Boolean keys whose
+// ranges pack into one exact Int64 (mk_plan_pack) run the single-key take on
+// the packed keys (a tuple holding a null is a null key unless nulls_equal),
+// so the row-format table applies to multi-key joins too; other keys compute
+// the pairs (plgpu_join_multi: hashed, verified) and gather.
+PLGPU_API int plgpu_join_inner_take_multi(const plgpu_column* left_keys, const plgpu_column* right_keys,
+                                          int32_t nkeys, const plgpu_column* left_cols, int32_t nleft,
+                                          const plgpu_column* right_cols, int32_t nright, int32_t nulls_equal,
+                                          int32_t maintain_order, int32_t validate, plgpu_column* out_left,
+                                          plgpu_column* out_right, int64_t* out_len, void* stream) {
+    hipStream_t s = as_stream(stream);
+    if (left_keys == nullptr || right_keys == nullptr || out_len == nullptr ||
+        (nleft > 0 && (left_cols == nullptr || out_left == nullptr)) ||
+        (nright > 0 && (right_cols == nullptr || out_right == nullptr)))
+        return fail(PLGPU_ERR_INVALID, "NULL argument");
+    if (nkeys < 1 || nkeys > kMaxKeys) return fail(PLGPU_ERR_INVALID, "number of join keys must be 1..8");
+    if (nleft < 0 || nleft > PLGPU_MAX_COLS || nright < 0 || nright > PLGPU_MAX_COLS)
+        return fail(PLGPU_ERR_INVALID, "0..8 columns per side");
+    const int64_t nl = left_keys[0].length, nr = right_keys[0].length;
+    bool packable = true;
+    MkKeys ka, kb;
+    std::memset(&ka, 0, sizeof ka);
+    std::memset(&kb, 0, sizeof kb);
+    ka.n = kb.n = nkeys;
+    for (int i = 0; i < nkeys; ++i) {
+        const int32_t dt = left_keys[i].dtype;
+        if (right_keys[i].dtype != dt) return fail(PLGPU_ERR_SCHEMA, "datatypes of join keys don't match");
+        if (left_keys[i].length != nl || right_keys[i].length != nr)
+            return fail(PLGPU_ERR_SHAPE, "join key columns of one side must have equal lengths");
+        if (!dtype_is_int(dt) && dt != PLGPU_BOOL) packable = false;
+        ka.c[i] = as_dev(&left_keys[i]);
+        kb.c[i] = as_dev(&right_keys[i]);
+    }
+    const bool neq = nulls_equal != 0;
+    const int cus = num_cus_jn();
+    MkPack pk;
+    pk.ok = false;
+    if (packable && nl < 0xFFFFFFFFll && nr < 0xFFFFFFFFll) {
+        const int rc = mk_plan_pack(ka, nl, &kb, nr, cus * 16, &pk, s);
+        if (rc) return rc;
+    }
+    if (pk.ok) {
+        uint64_t *cl = nullptr, *cr = nullptr;
+        int rc = dev_alloc((void**)&cl, (std::max<int64_t>(nl, 1) + (nl + 63) / 64 + 1) * 8, s);
+        if (!rc) rc = dev_alloc((void**)&cr, (std::max<int64_t>(nr, 1) + (nr + 63) / 64 + 1) * 8, s);
+        uint64_t* vl = cl ? cl + std::max<int64_t>(nl, 1) : nullptr;
+        uint64_t* vr = cr ? cr + std::max<int64_t>(nr, 1) : nullptr;
+        if (!rc && nl > 0)
+            mk_pack_kernel<<<(unsigned)std::min<int64_t>((nl + 255) / 256, cus * 16), 256, 0, s>>>(
+                ka, pk, nl, cl, neq ? nullptr : vl);
+        if (!rc && nr > 0)
+            mk_pack_kernel<<<(unsigned)std::min<int64_t>((nr + 255) / 256, cus * 16), 256, 0, s>>>(
+                kb, pk, nr, cr, neq ? nullptr : vr);
+        if (!rc) {
+            const hipError_t e = hipGetLastError();
+            if (e != hipSuccess) rc = hip_fail(e, "mk_pack_kernel");
+        }
+        if (!rc) {
+            plgpu_column a, b;
+            std::memset(&a, 0, sizeof a);
+            std::memset(&b, 0, sizeof b);
+            a.dtype = b.dtype = PLGPU_I64;
+            a.length = nl;
+            b.length = nr;
+            a.values = cl;
+            b.values = cr;
+            a.validity = neq ? nullptr : (const uint8_t*)vl;
+            b.validity = neq ? nullptr : (const uint8_t*)vr;
+            a.null_count = b.null_count = neq ? 0 : -1;
+            rc = plgpu_join_inner_take(&a, &b, left_cols, nleft, right_cols, nright, nulls_equal, maintain_order,
+                                       validate, out_left, out_right, out_len, stream);
+        }
+        (void)hipStreamSynchronize(s);
+        dev_free(cl, s);
+        dev_free(cr, s);
+        return rc;
+    }
+    // pairs (hashed and verified), then the takes
+    for (int i = 0; i < nleft; ++i) std::memset(&out_left[i], 0, sizeof out_left[i]);
+    for (int i = 0; i < nright; ++i) std::memset(&out_right[i], 0, sizeof out_right[i]);
+    *out_len = 0;
+    plgpu_column li, ri;
+    int rc = plgpu_join_multi(left_keys, right_keys, nkeys, PLGPU_JOIN_INNER, nulls_equal, maintain_order, validate,
+                              &li, &ri, stream);
+    if (rc) return rc;
+    for (int i = 0; i < nleft && !rc; ++i)
+        rc = gather_into(left_cols[i], (const uint32_t*)li.values, li.length, &out_left[i], s);
+    for (int i = 0; i < nright && !rc; ++i)
+        rc = gather_into(right_cols[i], (const uint32_t*)ri.values, ri.length, &out_right[i], s);
+    if (!rc) {
+        const hipError_t e = hipStreamSynchronize(s);
+        if (e != hipSuccess) rc = hip_fail(e, "join take");
+    }
+    *out_len = li.length;
+    plgpu_column_release(&li);
+    plgpu_column_release(&ri);
+    if (rc) {
+        for (int i = 0; i < nleft; ++i) plgpu_column_release(&out_left[i]);
+        for (int i = 0; i < nright; ++i) plgpu_column_release(&out_right[i]);
+    }
+    return rc;
+}

@@ -1505,8 +1505,9 @@ def _join(left: DataFrame, right: DataFrame, left_on: str | tuple, right_on: str
     li, ri = N.Column(), N.Column()
     order, val, hw = N.JOIN_ORDER[maintain_order], N.JOIN_VALIDATE[validate], N.JOIN_HOW[how]
     rpay = [n for n in right.columns if n not in rkeys]
-    if (how == "inner" and coalesce is not False and builtins.len(lks) == 1
-            and lks[0].dtype.physical() in INTEGER_DTYPES
+    take_single = builtins.len(lks) == 1 and lks[0].dtype.physical() in INTEGER_DTYPES
+    take_multi = builtins.len(lks) > 1 and builtins.all(k.dtype.physical() in INTEGER_DTYPES + (Boolean,) for k in lks)
+    if (how == "inner" and coalesce is not False and (take_single or take_multi)
             and builtins.len(left.columns) <= N.MAX_COLS and builtins.len(rpay) <= N.MAX_COLS):
         # join + the takes in one call (plgpu_join_inner_take): a row-format
         # table when one unique-keyed right column rides along
@@ -1515,9 +1516,15 @@ def _join(left: DataFrame, right: DataFrame, left_on: str | tuple, right_on: str
         ol = (N.Column * max(1, builtins.len(lc)))()
         orr = (N.Column * max(1, builtins.len(rc_)))()
         nout = C.c_int64(0)
-        N.check(N.lib().plgpu_join_inner_take(C.byref(lks[0]._col), C.byref(rks[0]._col), _col_array(lc),
-                                              builtins.len(lc), _col_array(rc_), builtins.len(rc_),
-                                              int(nulls_equal), order, val, ol, orr, C.byref(nout), None))
+        if take_single:
+            N.check(N.lib().plgpu_join_inner_take(C.byref(lks[0]._col), C.byref(rks[0]._col), _col_array(lc),
+                                                  builtins.len(lc), _col_array(rc_), builtins.len(rc_),
+                                                  int(nulls_equal), order, val, ol, orr, C.byref(nout), None))
+        else:
+            N.check(N.lib().plgpu_join_inner_take_multi(_col_array(lks), _col_array(rks), builtins.len(lks),
+                                                        _col_array(lc), builtins.len(lc), _col_array(rc_),
+                                                        builtins.len(rc_), int(nulls_equal), order, val, ol, orr,
+                                                        C.byref(nout), None))
         out = [Series._from_native(n, ol[i], left._cols[n]._logical_dtype()) for i, n in enumerate(left.columns)]
         for i, n in enumerate(rpay):
             out.append(Series._from_native(n + suffix if n in left.columns else n, orr[i],
