@@ -615,8 +615,15 @@ __device__ __forceinline__ void part_chunk(int64_t n, int64_t& lo, int64_t& hi) 
     hi = std::min<int64_t>(n, lo + per * kPartTile);
 }
 
-// Pass 1: selected rows per (partition, chunk).
-template <int PRED>
+// A null-free 8-byte column's value at row min(r, hi - 1): a branch-free
+// load, so a thread's loads of a tile all go out together.
+__device__ __forceinline__ uint64_t ld8c(const DevCol& c, int64_t r, int64_t hi) {
+    return __builtin_nontemporal_load((const uint64_t*)c.values + c.offset + (r < hi ? r : hi - 1));
+}
+
+// Pass 1: selected rows per (partition, chunk).  F8: the key and (PRED 1)
+// the predicate column are null-free 8-byte columns.
+template <int PRED, bool F8 = false>
 __global__ __launch_bounds__(kPartThreads) void gb_part_count_kernel(GbParams p, DevProgram prog, int pbits,
                                                                      uint32_t* __restrict__ cnt) {
     __shared__ uint32_t h[1 << kPartMaxBits];
@@ -625,8 +632,27 @@ __global__ __launch_bounds__(kPartThreads) void gb_part_count_kernel(GbParams p,
     __syncthreads();
     int64_t lo, hi;
     part_chunk(p.n, lo, hi);
-    for (int64_t r = lo + threadIdx.x; r < hi; r += blockDim.x)
-        if (part_sel<PRED>(p, prog, r)) atomicAdd(&h[part_of(dev_load(p.key, r), pbits)], 1u);
+    if (F8) {
+        for (int64_t base = lo; base < hi; base += kPartTile) {
+            uint64_t key[kPartPer], pv[kPartPer];
+#pragma unroll
+            for (int k = 0; k < kPartPer; ++k) {
+                const int64_t r = base + k * kPartThreads + threadIdx.x;
+                key[k] = ld8c(p.key, r, hi);
+                if (PRED == 1) pv[k] = ld8c(p.pred_col, r, hi);
+            }
+#pragma unroll
+            for (int k = 0; k < kPartPer; ++k) {
+                const int64_t r = base + k * kPartThreads + threadIdx.x;
+                const bool sel =
+                    r < hi && (PRED == 0 || simple_pred(prog.simple_isf, prog.simple_op, pv[k], prog.simple_imm));
+                if (sel) atomicAdd(&h[part_of(key[k], pbits)], 1u);
+            }
+        }
+    } else {
+        for (int64_t r = lo + threadIdx.x; r < hi; r += blockDim.x)
+            if (part_sel<PRED>(p, prog, r)) atomicAdd(&h[part_of(dev_load(p.key, r), pbits)], 1u);
+    }
     __syncthreads();
     for (int i = threadIdx.x; i < P; i += blockDim.x) cnt[(int64_t)i * gridDim.x + blockIdx.x] = h[i];
 }
@@ -651,7 +677,7 @@ struct PartOut {
 // column.  (Writing straight from global memory in slot order made every
 // 128-B line of a column be requested once per row it holds: 27 ms per 1e9
 // rows, request-bound.)
-template <int PRED>
+template <int PRED, bool F8 = false>
 __global__ __launch_bounds__(kPartThreads) void gb_part_scatter_kernel(GbParams p, DevProgram prog, int pbits,
                                                                        const uint64_t* __restrict__ off, PartOut o) {
     __shared__ uint32_t h[1 << kPartMaxBits];
@@ -675,26 +701,61 @@ __global__ __launch_bounds__(kPartThreads) void gb_part_scatter_kernel(GbParams 
         // the first kPartRegAcc aggregated columns are loaded with the key,
         // so a tile waits for memory once
         uint64_t av[kPartRegAcc][kPartPer];
+        if (F8) {
+            // null-free 8-byte key / aggregated / predicate columns:
+            // branch-free loads, all of the tile's in flight together
+            uint64_t pv[kPartPer];
 #pragma unroll
-        for (int a = 0; a < kPartRegAcc; ++a) {
+            for (int a = 0; a < kPartRegAcc; ++a) {
+                if (a >= p.nacc) break;
+#pragma unroll
+                for (int k = 0; k < kPartPer; ++k) av[a][k] = ld8c(p.acc[a].c, base + k * kPartThreads + threadIdx.x, hi);
+            }
 #pragma unroll
             for (int k = 0; k < kPartPer; ++k) {
                 const int64_t r = base + k * kPartThreads + threadIdx.x;
-                av[a][k] = (a < p.nacc && r < hi) ? dev_load(p.acc[a].c, r) : 0;
+                key[k] = ld8c(p.key, r, hi);
+                if (PRED == 1 && (p.pred_acc < 0 || p.pred_acc >= kPartRegAcc)) pv[k] = ld8c(p.pred_col, r, hi);
             }
-        }
 #pragma unroll
-        for (int k = 0; k < kPartPer; ++k) {
-            const int64_t r = base + k * kPartThreads + threadIdx.x;
-            key[k] = r < hi ? dev_load(p.key, r) : 0;
-        }
+            for (int k = 0; k < kPartPer; ++k) {
+                const int64_t r = base + k * kPartThreads + threadIdx.x;
+                pr[k] = ~0u;
+                bool sel = r < hi;
+                if (PRED == 1) {
+                    uint64_t x = pv[k];
 #pragma unroll
-        for (int k = 0; k < kPartPer; ++k) {
-            const int64_t r = base + k * kPartThreads + threadIdx.x;
-            pr[k] = ~0u;
-            if (r < hi && part_sel<PRED>(p, prog, r)) {
-                const uint32_t q = part_of(key[k], pbits);
-                pr[k] = (q << 16) | atomicAdd(&h[q], 1u);
+                    for (int a = 0; a < kPartRegAcc; ++a)
+                        if (a == p.pred_acc) x = av[a][k];
+                    sel = sel && simple_pred(prog.simple_isf, prog.simple_op, x, prog.simple_imm);
+                }
+                if (sel) {
+                    const uint32_t q = part_of(key[k], pbits);
+                    pr[k] = (q << 16) | atomicAdd(&h[q], 1u);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int a = 0; a < kPartRegAcc; ++a) {
+#pragma unroll
+                for (int k = 0; k < kPartPer; ++k) {
+                    const int64_t r = base + k * kPartThreads + threadIdx.x;
+                    av[a][k] = (a < p.nacc && r < hi) ? dev_load(p.acc[a].c, r) : 0;
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < kPartPer; ++k) {
+                const int64_t r = base + k * kPartThreads + threadIdx.x;
+                key[k] = r < hi ? dev_load(p.key, r) : 0;
+            }
+#pragma unroll
+            for (int k = 0; k < kPartPer; ++k) {
+                const int64_t r = base + k * kPartThreads + threadIdx.x;
+                pr[k] = ~0u;
+                if (r < hi && part_sel<PRED>(p, prog, r)) {
+                    const uint32_t q = part_of(key[k], pbits);
+                    pr[k] = (q << 16) | atomicAdd(&h[q], 1u);
+                }
             }
         }
         __syncthreads();
@@ -2003,8 +2064,14 @@ static int gb_partition(GbRun& R) {
     uint64_t* off = R.prange;
     uint64_t* range = R.prange + ncnt + 1;
     std::vector<uint64_t> hr(P + 1);
+    // the fast forms: null-free 8-byte key, aggregated and predicate columns
+    auto c8 = [](const DevCol& c) { return c.validity == nullptr && dtype_bytes(c.dtype) == 8 && c.dtype != PLGPU_STR; };
+    bool f8 = c8(p.key) && R.pred <= 1 && (R.pred == 0 || c8(p.pred_col));
+    for (int a = 0; a < p.nacc && a < kPartRegAcc; ++a) f8 = f8 && c8(p.acc[a].c);
     if (!rc) {
-        switch (R.pred) {
+        if (f8 && R.pred == 0) gb_part_count_kernel<0, true><<<G, kPartThreads, 0, s>>>(p, R.dp, R.pbits, cnt);
+        else if (f8 && R.pred == 1) gb_part_count_kernel<1, true><<<G, kPartThreads, 0, s>>>(p, R.dp, R.pbits, cnt);
+        else switch (R.pred) {
         case 0: gb_part_count_kernel<0><<<G, kPartThreads, 0, s>>>(p, R.dp, R.pbits, cnt); break;
         case 1: gb_part_count_kernel<1><<<G, kPartThreads, 0, s>>>(p, R.dp, R.pbits, cnt); break;
         default: gb_part_count_kernel<2><<<G, kPartThreads, 0, s>>>(p, R.dp, R.pbits, cnt); break;
@@ -2032,7 +2099,9 @@ static int gb_partition(GbRun& R) {
     R.pout.key = R.pbuf;
     for (int a = 0; a < p.nacc; ++a) R.pout.acc[a] = R.pbuf + (size_t)rows * (1 + a);
     R.pout.rows = want_rows ? (uint32_t*)(R.pbuf + (size_t)rows * (1 + p.nacc)) : nullptr;
-    switch (R.pred) {
+    if (f8 && R.pred == 0) gb_part_scatter_kernel<0, true><<<G, kPartThreads, 0, s>>>(p, R.dp, R.pbits, off, R.pout);
+    else if (f8 && R.pred == 1) gb_part_scatter_kernel<1, true><<<G, kPartThreads, 0, s>>>(p, R.dp, R.pbits, off, R.pout);
+    else switch (R.pred) {
     case 0: gb_part_scatter_kernel<0><<<G, kPartThreads, 0, s>>>(p, R.dp, R.pbits, off, R.pout); break;
     case 1: gb_part_scatter_kernel<1><<<G, kPartThreads, 0, s>>>(p, R.dp, R.pbits, off, R.pout); break;
     default: gb_part_scatter_kernel<2><<<G, kPartThreads, 0, s>>>(p, R.dp, R.pbits, off, R.pout); break;
