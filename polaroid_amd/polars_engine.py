@@ -32,7 +32,7 @@ from . import _native as N
 from .expr import Expr, col, lit
 from .frame import DataFrame, LazyFrame
 
-__all__ = ["execute_with_polaroid", "Unsupported", "translate"]
+__all__ = ["ColumnCache", "column_cache", "execute_with_polaroid", "Unsupported", "translate"]
 
 
 class Unsupported(Exception):
@@ -342,18 +342,104 @@ def scan_batches(df) -> list:
     return list(pydf.to_arrow(_COMPAT_OLDEST))
 
 
-def _bind_scans(node: tuple) -> tuple:
-    """Upload the scanned frames (RecordBatch chunks -> HBM)."""
+class ColumnCache:
+    """Device-resident scan columns, so repeated queries over the same frame
+    do not re-upload it over the host link.
+
+    A column's key is its Arrow type and the (address, size) of every buffer
+    of every chunk, plus each chunk's offset and length: polars exports a
+    primitive column zero-copy, so an unchanged frame gives the same key.
+    The entry holds a reference to the chunks, so their host memory cannot
+    be freed and reused by other data while the entry lives (no false hit);
+    polars' buffers are immutable (a write to a shared buffer copies it).
+    Entries are evicted least recently used beyond `capacity` bytes."""
+
+    def __init__(self, capacity: int = 32 << 30):
+        from collections import OrderedDict
+
+        self.capacity = capacity
+        self._d: "OrderedDict[tuple, tuple]" = OrderedDict()
+        self.bytes = 0
+        self.hits = 0
+        self.misses = 0
+
+    @staticmethod
+    def key(chunks: list, atype) -> tuple:
+        parts: list = [str(atype)]
+        for c in chunks:
+            bufs = list(c.buffers())
+            if hasattr(c, "dictionary"):  # Categorical / Enum: the dictionary's buffers too
+                bufs += list(c.dictionary.buffers())
+            parts.append((c.offset, len(c), tuple(None if b is None else (b.address, b.size) for b in bufs)))
+        return tuple(parts)
+
+    def get(self, key: tuple):
+        e = self._d.get(key)
+        if e is None:
+            self.misses += 1
+            return None
+        self._d.move_to_end(key)
+        self.hits += 1
+        return e[0]
+
+    def put(self, key: tuple, series, chunks: list, nbytes: int) -> None:
+        if nbytes > self.capacity:
+            return
+        self._d[key] = (series, chunks, nbytes)
+        self.bytes += nbytes
+        while self.bytes > self.capacity and self._d:
+            _, (_, _, nb) = self._d.popitem(last=False)
+            self.bytes -= nb
+
+    def clear(self) -> None:
+        self._d.clear()
+        self.bytes = 0
+        self.hits = 0
+        self.misses = 0
+
+
+_COLUMN_CACHE = ColumnCache()
+
+
+def column_cache() -> ColumnCache:
+    return _COLUMN_CACHE
+
+
+def _scan_frame(batches: list, names: list, cache: "ColumnCache | None") -> DataFrame:
+    """The projected columns of the scanned batches on the device, each
+    taken from the resident cache or ingested chunk by chunk."""
+    from .frame import _ingest_chunks
+
+    cols = []
+    for nm in names:
+        i = batches[0].schema.get_field_index(nm)
+        if i < 0:
+            raise N.ComputeError(f"column {nm!r} not found in the scanned batches")
+        atype = batches[0].schema.field(i).type
+        chunks = [b.column(i) for b in batches]
+        key = ColumnCache.key(chunks, atype) if cache is not None else None
+        s = cache.get(key) if cache is not None else None
+        if s is None:
+            s = _ingest_chunks(nm, chunks, atype)
+            if cache is not None:
+                cache.put(key, s, chunks, sum(c.nbytes for c in chunks))
+        cols.append(s.alias(nm))
+    return DataFrame(cols)
+
+
+def _bind_scans(node: tuple, cache: "ColumnCache | None" = None) -> tuple:
+    """Upload the scanned frames (RecordBatch chunks -> HBM), or find their
+    columns resident in `cache`."""
     if node[0] == "polars_scan":
         _, df, proj, schema = node
         batches = scan_batches(df)
         names = proj if proj is not None else list(schema)
         if not batches:
             return ("scan", _empty_frame(names, schema))
-        return ("scan", DataFrame.from_batches(batches, names))
+        return ("scan", _scan_frame(batches, names, cache))
     if node[0] == "join":
-        return (node[0], _bind_scans(node[1]), _bind_scans(node[2])) + tuple(node[3:])
-    return (node[0], _bind_scans(node[1])) + tuple(node[2:])
+        return (node[0], _bind_scans(node[1], cache), _bind_scans(node[2], cache)) + tuple(node[3:])
+    return (node[0], _bind_scans(node[1], cache)) + tuple(node[2:])
 
 
 def _empty_frame(names: list, schema: dict) -> DataFrame:
@@ -382,11 +468,11 @@ def _to_polars(table):
     return polars.from_arrow(table)
 
 
-def run_plan(plan: tuple, n_rows: int | None = None, to_frame=None):
+def run_plan(plan: tuple, n_rows: int | None = None, to_frame=None, cache: "ColumnCache | None" = None):
     """Execute a translated plan on the GPU; returns a polars DataFrame (or
     whatever `to_frame` makes of the result's Arrow table)."""
     N.lib()  # fail loudly when the HIP library is missing
-    lf = LazyFrame(_bind_scans(plan))
+    lf = LazyFrame(_bind_scans(plan, cache))
     out = lf.collect()
     table = out.to_arrow()
     if n_rows is not None:
@@ -433,9 +519,22 @@ def execute_with_polaroid(nt, duration_since_start: int | None = None, *, config
             raise N.InvalidOperationError(f"query is not supported by the MI355X engine: {exc}") from exc
         return
     N.lib()  # a GPU plan was accepted: the HIP library must be present
+    # scanned columns stay resident between queries unless the engine config
+    # sets device_cache_bytes = 0 (any other value resizes the cache)
+    cache_bytes = None
+    if isinstance(config, dict):
+        cache_bytes = config.get("device_cache_bytes")
+    elif config is not None:
+        cache_bytes = getattr(config, "device_cache_bytes", None)
+    cache = _COLUMN_CACHE
+    if cache_bytes is not None:
+        cache.capacity = int(cache_bytes)
+        if cache.capacity <= 0:
+            cache.clear()
+            cache = None
 
     def _udf(with_columns, predicate, n_rows, should_time=False):
-        df = _restore_dtypes(run_plan(plan, n_rows, to_frame), schema)
+        df = _restore_dtypes(run_plan(plan, n_rows, to_frame, cache), schema)
         if with_columns is not None:
             df = df.select(with_columns)
         if should_time:

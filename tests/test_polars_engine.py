@@ -428,3 +428,59 @@ def test_from_arrow_sliced_chunks(gpu):
     # an empty frame of batches keeps its columns
     df = pl.DataFrame.from_batches([pa.record_batch({"a": pa.array([], pa.int64())})])
     assert df.height == 0 and df.columns == ["a"]
+
+
+def test_column_cache_keys_and_eviction():
+    """The resident-column cache (CPU side): the same Arrow chunks give the
+    same key, other buffers another; LRU eviction by bytes."""
+    a = pa.array(np.arange(1000, dtype=np.int64))
+    b = pa.array(np.arange(1000, dtype=np.int64))
+    ka, kb = PE.ColumnCache.key([a], a.type), PE.ColumnCache.key([b], b.type)
+    assert ka == PE.ColumnCache.key([a], a.type) and ka != kb
+    assert PE.ColumnCache.key([a.slice(10, 20)], a.type) != ka  # offset / length are part of the key
+    c = PE.ColumnCache(capacity=20_000)
+    c.put(ka, "A", [a], 8_000)
+    c.put(kb, "B", [b], 8_000)
+    assert c.get(ka) == "A"  # A is now most recent
+    k3 = PE.ColumnCache.key([pa.array([1.0])], pa.float64())
+    c.put(k3, "C", [], 8_000)  # over capacity: B (least recent) goes
+    assert c.get(kb) is None and c.get(ka) == "A" and c.get(k3) == "C"
+    assert c.bytes == 16_000 and c.hits == 3 and c.misses == 1
+    c.put(("big",), "X", [], 50_000)  # larger than the whole cache: not kept
+    assert c.get(("big",)) is None
+
+
+@pytest.mark.gpu
+def test_udf_reuses_resident_columns(gpu):
+    """A second query over the same frame takes its columns from the device
+    cache (no re-upload) and gives the same result; another frame misses."""
+    PE.column_cache().clear()
+    rng = np.random.default_rng(2)
+    n = 50_000
+    table = pa.table({"k": pa.array(rng.integers(0, 50, n)), "v": pa.array(rng.standard_normal(n))})
+    pydf = FakePyDataFrame(table)
+    outs = []
+    for _ in range(2):
+        nt = FakeNT(table)
+        scan = nt.p("DataFrameScan", ["k", "v"], df=pydf, projection=None, selection=None)
+        nt.p("Filter", ["k", "v"], input=scan, predicate=PyExprIR(nt.bin(nt.col("v"), "Gt", nt.lit(0.0)), "v"))
+        PE.execute_with_polaroid(nt, None, to_frame=lambda t: t)
+        outs.append(nt.udf(None, None, None, False))
+    assert outs[0].equals(outs[1])
+    c = PE.column_cache()
+    assert c.hits >= 2 and c.misses == 2  # k and v uploaded once
+    want = table.filter(pa.compute.greater(table.column("v"), 0.0))
+    assert outs[0].column("v").to_pylist() == want.column("v").to_pylist()
+    # a different frame: new buffers, new keys
+    t2 = pa.table({"k": pa.array(rng.integers(0, 50, n)), "v": pa.array(rng.standard_normal(n))})
+    nt = FakeNT(t2)
+    nt.p("DataFrameScan", ["k", "v"], df=FakePyDataFrame(t2), projection=None, selection=None)
+    PE.execute_with_polaroid(nt, None, to_frame=lambda t: t)
+    out = nt.udf(None, None, None, False)
+    assert out.column("v").to_pylist() == t2.column("v").to_pylist() and c.misses == 4
+    # device_cache_bytes = 0 turns the cache off
+    nt = FakeNT(t2)
+    nt.p("DataFrameScan", ["k", "v"], df=FakePyDataFrame(t2), projection=None, selection=None)
+    PE.execute_with_polaroid(nt, None, config={"device_cache_bytes": 0}, to_frame=lambda t: t)
+    assert nt.udf(None, None, None, False).column("k").to_pylist() == t2.column("k").to_pylist()
+    PE.column_cache().capacity = 32 << 30
