@@ -51,6 +51,7 @@ constexpr int kHeadroomBinades = 8;   // above the sampled max exponent
 constexpr int64_t kMaxRowsPerWg = int64_t(1) << 22;  // keeps 40-bit limbs exact in int64
 constexpr int kPlanSamples = 65536;
 constexpr int kPlanSetSlots = 4096;   // LDS hash set of the distinct-key sample (32 KiB)
+constexpr int kPlanSetWord = 32;      // the plan's global key set, in words after the status block
 
 // Acc flags
 enum : int32_t { A_FSUM = 1, A_FSUMCAST = 2, A_ISUM = 4, A_CNT = 8, A_MIN = 16, A_MAX = 32, A_FLAGS = 64 };
@@ -835,26 +836,35 @@ __device__ __forceinline__ int64_t fast_row(int64_t t, int T, int rows, int j) {
     return t * (int64_t)T * rows + (int64_t)(j >> 1) * 2 * T + 2 * threadIdx.x + (j & 1);
 }
 
-template <int NACC, int PRED, int ROWS>
+typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
+
+// 16-byte load; NT: non-temporal (streamed once, not kept in the caches).
+template <bool NT>
+__device__ __forceinline__ u64x2_t ld16(const uint64_t* p) {
+    if (NT) return __builtin_nontemporal_load(reinterpret_cast<const u64x2_t*>(p));
+    return *reinterpret_cast<const u64x2_t*>(p);
+}
+
+template <int NACC, int PRED, int ROWS, bool NT = false>
 __device__ __forceinline__ void fast_load(const GbParams& p, int64_t t, FastTile<NACC, ROWS>& x) {
     const int T = blockDim.x;
     const uint64_t* kp = (const uint64_t*)p.key.values + p.key.offset;
 #pragma unroll
     for (int q = 0; q < ROWS / 2; ++q) {
         const int64_t r = fast_row(t, T, ROWS, 2 * q);
-        const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(kp + r);
+        const u64x2_t a = ld16<NT>(kp + r);
         x.key[2 * q] = a.x;
         x.key[2 * q + 1] = a.y;
 #pragma unroll
         for (int c = 0; c < NACC; ++c) {
             const uint64_t* vp = (const uint64_t*)p.acc[c].c.values + p.acc[c].c.offset;
-            const ulonglong2 b = *reinterpret_cast<const ulonglong2*>(vp + r);
+            const u64x2_t b = ld16<NT>(vp + r);
             x.v[c][2 * q] = b.x;
             x.v[c][2 * q + 1] = b.y;
         }
         if (PRED == 1 && p.pred_acc < 0) {
             const uint64_t* pp = (const uint64_t*)p.pred_col.values + p.pred_col.offset;
-            const ulonglong2 b = *reinterpret_cast<const ulonglong2*>(pp + r);
+            const u64x2_t b = ld16<NT>(pp + r);
             x.pv[2 * q] = b.x;
             x.pv[2 * q + 1] = b.y;
         }
@@ -872,7 +882,8 @@ __device__ __forceinline__ void fast_load(const GbParams& p, int64_t t, FastTile
 // The two limbs land in fields (3+4a, 4+4a): the 3-limb representation with
 // a zero low limb, so the flush and finalize are unchanged.
 // ABL (timing ablations, never dispatched in production): 1 no atomics,
-// 2 len atomic only, 3 limb conversion without limb atomics.
+// 2 len atomic only, 3 limb conversion without limb atomics, 5 no
+// prefetch, 11 default-policy (not non-temporal) loads.
 // WPE: minimum waves per SIMD the register allocation must allow (1 = no
 // constraint); 6 caps VGPRs at 80, i.e. three 512-thread workgroups per CU.
 template <int NACC, int PRED, bool SUMONLY, int ROWS, int LIMBS = 3, int ABL = 0, int WPE = 1>
@@ -903,11 +914,14 @@ __global__ __launch_bounds__(kGbThreads) __attribute__((amdgpu_waves_per_eu(WPE)
     __syncthreads();
 
     const int T = blockDim.x;
+    // the tile stream is read once: non-temporal loads (6.60 vs 6.84 ms at
+    // 1e9 rows, tools/ablate.py; ablation 11 = default-policy loads)
+    constexpr bool NTL = ABL != 11;
     const int64_t ntiles = p.n_full / ((int64_t)T * ROWS);
     constexpr uint32_t VM = (1u << NACC) - 1u;
     int64_t t = blockIdx.x;
     FastTile<NACC, ROWS> cur;
-    if (ABL != 5 && t < ntiles) fast_load<NACC, PRED, ROWS>(p, t, cur);
+    if (ABL != 5 && t < ntiles) fast_load<NACC, PRED, ROWS, NTL>(p, t, cur);
     for (; t < ntiles; t += gridDim.x) {
         if (ABL == 5) fast_load<NACC, PRED, ROWS>(p, t, cur);  // ablation: no prefetch
         // ---- predicate + batched LDS probes of the tile's rows
@@ -934,7 +948,7 @@ __global__ __launch_bounds__(kGbThreads) __attribute__((amdgpu_waves_per_eu(WPE)
         // ---- next tile's loads go out before this tile's atomics
         FastTile<NACC, ROWS> nxt;
         const int64_t tn = t + gridDim.x;
-        if (ABL != 5 && tn < ntiles) fast_load<NACC, PRED, ROWS>(p, tn, nxt);
+        if (ABL != 5 && tn < ntiles) fast_load<NACC, PRED, ROWS, NTL>(p, tn, nxt);
         // ---- apply rows one at a time (rolled; arrays shift statically)
 #pragma unroll 1
         for (int j = 0; j < ROWS; ++j) {
@@ -1203,32 +1217,41 @@ __device__ __forceinline__ int64_t plan_row(int64_t i, int64_t n, int64_t sample
     return (i >> 4) * cstep + (i & 15);
 }
 
-// Planning launch: blocks [0, nacc) sample the summed columns' max exponent
-// (-> fixed-point bottom); block nacc counts distinct keys in a strided
-// sample with an LDS hash set (-> table sizes).
-__global__ __launch_bounds__(kPlanThreads) void gb_plan_kernel(GbParams p, int32_t* bottoms, int64_t samples) {
-    __shared__ uint32_t red[kPlanThreads];
-    __shared__ uint32_t red2[kPlanThreads];
+// Planning launch, kPlanBlocks workgroups per task, each sampling its
+// 1/kPlanBlocks share of the samples in one batch (one memory round trip per
+// thread).  Tasks [0, nacc): the summed columns' largest and smallest
+// exponents (atomic max into ST_MAXEX / ST_MINEX; the host derives the
+// fixed-point bottoms).  Task nacc: distinct keys of the sample -- each
+// workgroup dedups its share in an LDS set and inserts its new keys into a
+// global set (`gset`, kPlanSetSlots words, zeroed, holding key ^ kEmptyKey
+// so 0 means empty), counting successful inserts in ST_DISTINCT.
+// (One workgroup per task took 147 us per plan at 1e9 rows: 16 dependent
+// rounds of strided loads.)
+constexpr int kPlanBlocks = 16;
+
+__global__ __launch_bounds__(kPlanThreads) void gb_plan_kernel(GbParams p, uint64_t* __restrict__ gset,
+                                                               int64_t samples) {
     __shared__ uint64_t set[kPlanSetSlots];
-    __shared__ uint32_t distinct;
-    const int a = blockIdx.x;
+    __shared__ uint32_t red[2][kPlanThreads / 64];
+    const int a = blockIdx.x / kPlanBlocks;
+    const int64_t per = (samples + kPlanBlocks - 1) / kPlanBlocks;
+    const int64_t s0 = (int64_t)(blockIdx.x % kPlanBlocks) * per;
+    const int64_t s1 = s0 + per < samples ? s0 + per : samples;
     const int64_t n = p.n;
-    const int64_t step = n > samples ? n / samples : 1;
     if (a == p.nacc) {
         for (int i = threadIdx.x; i < kPlanSetSlots; i += blockDim.x) set[i] = kEmptyKey;
-        if (threadIdx.x == 0) distinct = 0;
         __syncthreads();
         const int bits = __builtin_ctz(kPlanSetSlots);
         // kPlanBatch strided samples per thread are loaded before any is
         // inserted: one memory round trip per batch, not per sample
-        for (int64_t i0 = threadIdx.x; i0 < samples && i0 * step < n; i0 += (int64_t)blockDim.x * kPlanBatch) {
+        for (int64_t i0 = s0 + threadIdx.x; i0 < s1; i0 += (int64_t)blockDim.x * kPlanBatch) {
           uint64_t kb[kPlanBatch];
           bool okb[kPlanBatch];
 #pragma unroll
           for (int u = 0; u < kPlanBatch; ++u) {
             const int64_t i = i0 + (int64_t)u * blockDim.x;
             const int64_t r = plan_row(i, n, samples);
-            okb[u] = i < samples && r < n && dev_valid(p.key, r);
+            okb[u] = i < s1 && r < n && dev_valid(p.key, r);
             kb[u] = okb[u] ? dev_load(p.key, r) : 0;
           }
 #pragma unroll 1
@@ -1236,7 +1259,8 @@ __global__ __launch_bounds__(kPlanThreads) void gb_plan_kernel(GbParams p, int32
             if (!okb[u]) continue;
             const uint64_t k = kb[u];
             if (k == kEmptyKey) continue;
-            uint32_t h = hash_slot(k, bits);
+            const uint32_t h = hash_slot(k, bits);
+            bool fresh = false;
             for (int q = 0; q < 64; ++q) {
                 const uint32_t s = (h + q) & (kPlanSetSlots - 1);
                 uint64_t o = lds_load(&set[s]);
@@ -1244,18 +1268,25 @@ __global__ __launch_bounds__(kPlanThreads) void gb_plan_kernel(GbParams p, int32
                 if (o == kEmptyKey) {
                     o = atomicCAS((unsigned long long*)&set[s], (unsigned long long)kEmptyKey, (unsigned long long)k);
                     if (o == kEmptyKey) {
-                        atomicAdd(&distinct, 1u);
+                        fresh = true;
                         break;
                     }
                     if (o == k) break;
                 }
             }
+            if (!fresh) continue;
+            // new to this workgroup: into the global set
+            const unsigned long long w = (unsigned long long)(k ^ kEmptyKey);
+            for (int q = 0; q < 64; ++q) {
+                const uint32_t s = (h + q) & (kPlanSetSlots - 1);
+                const unsigned long long o = atomicCAS((unsigned long long*)&gset[s], 0ull, w);
+                if (o == 0ull) {
+                    atomicAdd((unsigned long long*)&p.status[ST_DISTINCT], 1ull);
+                    break;
+                }
+                if (o == w) break;
+            }
           }
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            p.status[ST_DISTINCT] = distinct;
-            p.status[ST_SAMPLED] = (uint64_t)((n + step - 1) / step < samples ? (n + step - 1) / step : samples);
         }
         return;
     }
@@ -1263,14 +1294,14 @@ __global__ __launch_bounds__(kPlanThreads) void gb_plan_kernel(GbParams p, int32
     uint32_t mx = 0, mn = 0x7FF;
     if (ac.flags & (A_FSUM | A_FSUMCAST)) {
         const DevCol& c = ac.c;
-        for (int64_t i0 = threadIdx.x; i0 < samples && i0 * step < n; i0 += (int64_t)blockDim.x * kPlanBatch) {
+        for (int64_t i0 = s0 + threadIdx.x; i0 < s1; i0 += (int64_t)blockDim.x * kPlanBatch) {
             uint64_t xb[kPlanBatch];
             bool okb[kPlanBatch];
 #pragma unroll
             for (int u = 0; u < kPlanBatch; ++u) {
                 const int64_t i = i0 + (int64_t)u * blockDim.x;
                 const int64_t r = plan_row(i, n, samples);
-                okb[u] = i < samples && r < n && dev_valid(c, r);
+                okb[u] = i < s1 && r < n && dev_valid(c, r);
                 xb[u] = okb[u] ? dev_load(c, r) : 0;
             }
 #pragma unroll
@@ -1285,23 +1316,35 @@ __global__ __launch_bounds__(kPlanThreads) void gb_plan_kernel(GbParams p, int32
             }
         }
     }
-    red[threadIdx.x] = mx;
-    red2[threadIdx.x] = mn;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const uint32_t o = __shfl_xor(mx, off, 64);
+        mx = mx > o ? mx : o;
+        const uint32_t q = __shfl_xor(mn, off, 64);
+        mn = mn < q ? mn : q;
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = mx;
+        red[1][threadIdx.x >> 6] = mn;
+    }
     __syncthreads();
-    for (int off = kPlanThreads / 2; off >= 1; off >>= 1) {
-        if (threadIdx.x < off) {
-            red[threadIdx.x] = max(red[threadIdx.x], red[threadIdx.x + off]);
-            red2[threadIdx.x] = min(red2[threadIdx.x], red2[threadIdx.x + off]);
-        }
-        __syncthreads();
-    }
     if (threadIdx.x == 0) {
-        p.status[ST_MINEX + a] = 0x7FF - red2[0];
-        int e = red[0] == 0 ? 2046 : (int)red[0] + kHeadroomBinades;
-        if (e > 2046) e = 2046;
-        // a value fits iff ex <= bottom + 1075 + (window - 53)
-        bottoms[a] = e - 1075 - (kSumWindowBits - 53);
+        for (int w = 1; w < kPlanThreads / 64; ++w) {
+            mx = red[0][w] > mx ? red[0][w] : mx;
+            mn = red[1][w] < mn ? red[1][w] : mn;
+        }
+        if (mx) atomicMax((unsigned long long*)&p.status[ST_MAXEX + a], (unsigned long long)mx);
+        if (mn != 0x7FF) atomicMax((unsigned long long*)&p.status[ST_MINEX + a], (unsigned long long)(0x7FF - mn));
     }
+}
+
+// Fixed-point bottom of a summed column from its largest sampled exponent
+// (0: none sampled): kHeadroomBinades above it, so a value fits iff
+// ex <= bottom + 1075 + (window - 53).
+static int32_t plan_bottom(uint64_t maxex) {
+    int e = maxex == 0 ? 2046 : (int)maxex + kHeadroomBinades;
+    if (e > 2046) e = 2046;
+    return e - 1075 - (kSumWindowBits - 53);
 }
 
 __global__ void gb_init_table_kernel(uint64_t* gtab, int64_t words_per_field, int nfields, uint64_t min_init_mask) {
@@ -1784,6 +1827,7 @@ static hipError_t launch_ablation(const Plan& pl, const DevProgram& dp, hipStrea
     case 7: return launch_fast_rows<4, 1, true, 2, 2, 0>(pl, dp, s);
     case 8: return launch_fast_rows<4, 1, true, 2, 2, 5>(pl, dp, s);
     case 9: return launch_fast_rows<4, 1, true, 4, 2, 5>(pl, dp, s);
+    case 11: return launch_fast_rows<4, 1, true, 2, 2, 11>(pl, dp, s);
     default: return launch_fast_rows<4, 1, true, 2, 3, 0>(pl, dp, s);
     }
 }
@@ -1896,11 +1940,15 @@ static int gb_prepare(GbRun& R, const plgpu_column* key, const plgpu_column* col
     if ((rc = plan_groupby(key, cols, ncols, aggs, naggs, maintain_order || R.want_first, R.dp, &R.pl,
                            force_counts)))
         return rc;
-    if ((rc = dev_alloc((void**)&R.status, ST_WORDS * 8 + kMaxAcc * 4, R.s))) return rc;
+    // status words, the bottoms, then (at word kPlanSetWord) the plan's
+    // global distinct-key set; one allocation, one memset
+    static_assert(ST_WORDS * 8 + kMaxAcc * 4 <= kPlanSetWord * 8, "status layout");
+    const size_t bytes = (size_t)(kPlanSetWord + kPlanSetSlots) * 8;
+    if ((rc = dev_alloc((void**)&R.status, bytes, R.s))) return rc;
     R.bottoms = (int32_t*)(R.status + ST_WORDS);
     R.pl.p.status = R.status;
     R.pl.p.bottoms = R.bottoms;
-    PLGPU_HIP(hipMemsetAsync(R.status, 0, ST_WORDS * 8 + kMaxAcc * 4, R.s));
+    PLGPU_HIP(hipMemsetAsync(R.status, 0, bytes, R.s));
     return PLGPU_OK;
 }
 
@@ -1945,11 +1993,12 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
     Plan& pl = R.pl;
     GbParams& p = pl.p;
     const int64_t n = p.n;
-    gb_plan_kernel<<<p.nacc + 1, kPlanThreads, 0, R.s>>>(p, R.bottoms, kPlanSamples);
+    gb_plan_kernel<<<(p.nacc + 1) * kPlanBlocks, kPlanThreads, 0, R.s>>>(p, R.status + kPlanSetWord, kPlanSamples);
     PLGPU_HIP(hipGetLastError());
     PLGPU_HIP(hipMemcpyAsync(R.st, R.status, sizeof R.st, hipMemcpyDeviceToHost, R.s));
-    PLGPU_HIP(hipMemcpyAsync(R.hb, R.bottoms, sizeof R.hb, hipMemcpyDeviceToHost, R.s));
     PLGPU_HIP(hipStreamSynchronize(R.s));
+    R.st[ST_SAMPLED] = (uint64_t)std::min<int64_t>(n, kPlanSamples);
+    for (int a = 0; a < kMaxAcc; ++a) R.hb[a] = a < p.nacc ? plan_bottom(R.st[ST_MAXEX + a]) : 0;
     if (fixed)
         for (int a = 0; a < kMaxAcc; ++a) R.hb[a] = fixed[a];
     int64_t hll = -1;
@@ -2245,13 +2294,37 @@ static int gb_main(GbRun& R, bool auto_refit, bool* refit, int32_t* hint) {
         if (n > 0 && R.part) {
             PLGPU_HIP(launch_partitioned(R));
         } else if (n > 0) {
+            // the tail (< one tile of the fast kernel, or every row when the
+            // fast path does not apply) goes through the generic kernel; next
+            // to a fast launch it runs on a side stream, concurrently (its
+            // few workgroups took 28 us after the fast kernel otherwise)
+            const bool tail = p.row_begin < n;
+            hipStream_t ts = R.s;
+            hipEvent_t fork = nullptr, join = nullptr;
+            if (tail && p.n_full > 0 && (ts = side_stream()) != nullptr) {
+                PLGPU_HIP(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
+                PLGPU_HIP(hipEventCreateWithFlags(&join, hipEventDisableTiming));
+                PLGPU_HIP(hipEventRecord(fork, R.s));
+                PLGPU_HIP(hipStreamWaitEvent(ts, fork, 0));
+            } else {
+                ts = R.s;
+            }
             if (p.n_full > 0) PLGPU_HIP(launch_fast_dispatch(pl, R.dp, R.pred, R.s));
-            if (p.row_begin < n) {
-                Plan tail = pl;
+            if (tail) {
+                Plan tp = pl;
                 const int64_t rows = n - p.row_begin;
                 const int64_t g = (rows + 4 * kGbThreads - 1) / (4 * kGbThreads);
-                tail.grid = (int)std::min<int64_t>(pl.grid, g < 1 ? 1 : g);
-                PLGPU_HIP(launch_main_dispatch(tail, R.dp, R.pred, R.s));
+                tp.grid = (int)std::min<int64_t>(pl.grid, g < 1 ? 1 : g);
+                PLGPU_HIP(launch_main_dispatch(tp, R.dp, R.pred, ts));
+            }
+            if (join) {
+                // (destroying a recorded event is deferred by the runtime
+                // until it completes)
+                const hipError_t e1 = hipEventRecord(join, ts);
+                const hipError_t e2 = e1 == hipSuccess ? hipStreamWaitEvent(R.s, join, 0) : e1;
+                (void)hipEventDestroy(fork);
+                (void)hipEventDestroy(join);
+                PLGPU_HIP(e2);
             }
         }
         PLGPU_HIP(hipEventRecord(ev1, R.s));

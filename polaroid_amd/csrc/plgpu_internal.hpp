@@ -31,6 +31,10 @@ int hip_fail(hipError_t e, const char* what);
     } while (0)
 
 hipStream_t as_stream(void* s);
+// A library-owned non-blocking stream of the current device, for small work
+// that overlaps a long launch (joined back with events); nullptr if it could
+// not be created.
+hipStream_t side_stream();
 int dev_alloc(void** p, size_t bytes, hipStream_t s);
 void dev_free(void* p, hipStream_t s);
 

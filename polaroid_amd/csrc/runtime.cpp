@@ -35,6 +35,22 @@ int hip_fail(hipError_t e, const char* what) {
 
 hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+hipStream_t side_stream() {
+    // non-blocking: no implicit ordering against the legacy null stream the
+    // callers usually enqueue on; ordering comes only from their events
+    static std::mutex mu;
+    static hipStream_t streams[64] = {};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (dev < 0 || dev >= 64) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    if (streams[dev] == nullptr && hipStreamCreateWithFlags(&streams[dev], hipStreamNonBlocking) != hipSuccess) {
+        (void)hipGetLastError();
+        streams[dev] = nullptr;
+    }
+    return streams[dev];
+}
+
 // Caching device allocator.  Blocks come from hipMalloc and are recycled
 // through size-keyed free lists instead of being returned with hipFree
 // (which synchronises the device).  Every entry point enqueues its work on
