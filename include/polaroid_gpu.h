@@ -308,11 +308,11 @@ int plgpu_group_by_agg_multi(const plgpu_column* keys, int32_t nkeys, const plgp
  * pre-aggregates are exact partial states (records) moved by one RCCL
  * all-to-all.  A record is `record_words` u64 words:
  * [kind (0 key, 1 null key, 2 INT64_MIN key), key, state fields...].
- * All ranks must aggregate with the SAME f64 fixed-point windows
- * (`bottoms`, PLGPU_GB_MAX_ACC int32): each rank starts from its sampled
- * windows, ranks agree on the element-wise MAX of the hints, and a rank
- * re-runs its partial stage while its used windows differ from the agreed
- * ones (polaroid_amd/distributed.py). */
+ * Each rank aggregates with its own f64 fixed-point windows (`bottoms`,
+ * PLGPU_GB_MAX_ACC int32, refitted locally as needed); the windows travel
+ * with the record counts, and plgpu_gb_merge_sources shifts every source's
+ * exact sum states onto the lowest window before folding them
+ * (polaroid_amd/distributed.py).  No collective precedes the exchange. */
 typedef struct plgpu_gb_partial plgpu_gb_partial;
 
 #define PLGPU_GB_MAX_ACC 6
@@ -326,12 +326,14 @@ int plgpu_gb_plan_bottoms(const plgpu_column* key, const plgpu_column* cols, int
                           const plgpu_agg* aggs, int32_t naggs, int32_t* out_bottoms,
                           void* stream);
 
-/* Filter + pre-aggregate this shard.  `bottoms` (6 int32) are the agreed
- * windows, or NULL to use this shard's sampled ones; the windows actually
- * used come back in out_bottoms_used[6].  Returns a handle holding the
- * partial table, the number of groups (*out_records), and whether a window
- * must move for an exact sum (*out_refit, new windows in out_bottoms_hint[6];
- * without a refit the hint equals the used windows). */
+/* Filter + pre-aggregate this shard.  `bottoms` NULL: this shard's own
+ * windows (sampled, refitted here when a value does not fit); otherwise the
+ * fixed windows to use, and whether one must move for an exact sum is
+ * reported (*out_refit, new windows in out_bottoms_hint[6]; without a refit
+ * the hint equals the used windows).  The windows used come back in
+ * out_bottoms_used[6].  Returns a handle holding the partial table and the
+ * number of groups (*out_records).  A column whose values need the wide
+ * (multi-window) sum is refused with PLGPU_ERR_CAPACITY. */
 int plgpu_gb_partial_begin(const plgpu_column* key, const plgpu_column* cols, int32_t ncols,
                            const plgpu_instr* program, int32_t n_instr, const plgpu_agg* aggs,
                            int32_t naggs, const int32_t* bottoms, int32_t world,
@@ -354,6 +356,21 @@ int plgpu_gb_merge(const void* records, int64_t n_records, const plgpu_column* c
                    int32_t ncols, const plgpu_agg* aggs, int32_t naggs, const int32_t* bottoms,
                    int32_t key_dtype, plgpu_column* out_key, plgpu_column* out_aggs,
                    plgpu_groupby_info* info, void* stream);
+
+/* Fold the records received from `n_sources` ranks: source j's
+ * src_records[j] records lie consecutively, in source order (the layout of
+ * an all-to-all's receive buffer), aggregated with that source's windows
+ * src_bottoms[j * PLGPU_GB_MAX_ACC + a].  Per column, the sums are shifted
+ * onto the lowest window of any source that sent records (exact); a state
+ * that would leave the 192-bit range fails with PLGPU_ERR_CAPACITY.  Then
+ * finalized like plgpu_gb_merge.  Replaces the window agreement before the
+ * partial stage (polars-stream/src/nodes/group_by.rs:378 combine_subset
+ * folds pre-aggregates of any origin). */
+int plgpu_gb_merge_sources(const void* records, int32_t n_sources, const int64_t* src_records,
+                           const int32_t* src_bottoms, const plgpu_column* cols, int32_t ncols,
+                           const plgpu_agg* aggs, int32_t naggs, int32_t key_dtype,
+                           plgpu_column* out_key, plgpu_column* out_aggs, plgpu_groupby_info* info,
+                           void* stream);
 
 /* ---- hash join ------------------------------------------------------------
  * maintain_order (polars-ops/src/frame/join/args.rs:100 MaintainOrderJoin)

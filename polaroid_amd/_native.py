@@ -129,6 +129,9 @@ SIGNATURES = {
     "plgpu_gb_merge": (C.c_int, [_P, C.c_int64, _COLP, C.c_int32, C.POINTER(Agg), C.c_int32,
                                  C.POINTER(C.c_int32), C.c_int32, _COLP, _COLP,
                                  C.POINTER(GroupByInfo), _P]),
+    "plgpu_gb_merge_sources": (C.c_int, [_P, C.c_int32, C.POINTER(C.c_int64), C.POINTER(C.c_int32), _COLP,
+                                         C.c_int32, C.POINTER(Agg), C.c_int32, C.c_int32, _COLP, _COLP,
+                                         C.POINTER(GroupByInfo), _P]),
     "plgpu_join_inner_multi": (C.c_int, [_COLP, _COLP, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _COLP, _COLP,
                                          _P]),
     "plgpu_join_inner": (C.c_int, [_COLP, _COLP, C.c_int32, C.c_int32, C.c_int32, _COLP, _COLP, _P]),

@@ -71,6 +71,7 @@ enum : int {
     ST_SAMPLED = 7,      // plan: keys sampled
     ST_MAXEX = 8,        // + acc
     ST_FXFLAGS = 16,     // + acc: bit0 overflow, bit1 inexact
+    ST_SHIFT_OVF = 14,   // merge: a shifted f64 sum state left the 192-bit range
     ST_MINEX = 17,       // + acc: 0x7FF - smallest exponent of a nonzero finite value (plan / maxexp)
     ST_WORDS = 24
 };
@@ -1516,13 +1517,52 @@ __global__ void gb_export_kernel(GbParams p, int world, uint64_t* cursor, uint64
     }
 }
 
-// Fold records (from any rank) into the global table.
-__global__ void gb_merge_kernel(GbParams p, const uint64_t* __restrict__ rec, int64_t nrec) {
+// (w2:w1:w0) <<= d as a two's-complement 192-bit integer, 0 <= d; false
+// (value unchanged) when the result would not fit.
+__device__ __forceinline__ bool shl192(uint64_t& w0, uint64_t& w1, uint64_t& w2, int d) {
+    if (d == 0) return true;
+    const uint64_t sign = (uint64_t)((int64_t)w2 >> 63);
+    if (d >= 191) return (w0 | w1 | w2) == 0;
+    // the top d + 1 bits must all equal the sign
+    const uint64_t x[3] = {w0, w1, w2};
+    for (int b = 191 - d; b < 192; b += 64) {
+        const int lo = b, hi = b + 64 < 192 ? b + 64 : 192;  // bits [lo, hi) of this chunk
+        const int wi = lo >> 6, sh = lo & 63;
+        uint64_t chunk = x[wi] >> sh;
+        if (sh && wi + 1 < 3) chunk |= x[wi + 1] << (64 - sh);
+        const int nb = hi - lo;
+        const uint64_t m = nb == 64 ? ~0ull : ((1ull << nb) - 1);
+        if ((chunk & m) != (sign & m)) return false;
+    }
+    const int q = d >> 6, r = d & 63;
+    uint64_t o[3];
+    for (int i = 0; i < 3; ++i) {
+        const int j = i - q;
+        uint64_t v = j >= 0 ? (r ? x[j] << r : x[j]) : 0ull;
+        if (r && j - 1 >= 0) v |= x[j - 1] >> (64 - r);
+        o[i] = v;
+    }
+    w0 = o[0];
+    w1 = o[1];
+    w2 = o[2];
+    return true;
+}
+
+// Fold records (from any rank) into the global table.  With nsrc > 0 the
+// records come from nsrc sources in order (source j: records
+// [src_start[j], src_start[j + 1])), each aggregated with its own
+// fixed-point windows; an f64 sum state of acc a is shifted left by
+// src_shift[j * kMaxAcc + a] bits onto the table's window (exact).
+__global__ void gb_merge_kernel(GbParams p, const uint64_t* __restrict__ rec, int64_t nrec, int nsrc,
+                                const int64_t* __restrict__ src_start, const int32_t* __restrict__ src_shift) {
     const int rw = p.nfields + 1;
     uint32_t special = 0;
+    bool ovf = false;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nrec; i += (int64_t)gridDim.x * blockDim.x) {
         const uint64_t* r = rec + i * rw;
         const uint64_t kind = r[0];
+        int src = 0;
+        while (src + 1 < nsrc && i >= src_start[src + 1]) ++src;
         int64_t gs;
         if (kind == 1) {
             gs = p.gcap;
@@ -1545,9 +1585,20 @@ __global__ void gb_merge_kernel(GbParams p, const uint64_t* __restrict__ rec, in
             case FOP_MIN: if (v != ~0ull) atomicMin(q, (unsigned long long)v); break;
             case FOP_MAX: if (v) atomicMax(q, (unsigned long long)v); break;
             case FOP_OR: if (v) atomicOr(q, (unsigned long long)v); break;
-            case FOP_ADD192:
-                g_add192(gfield(p, f, gs), gfield(p, f + 1, gs), gfield(p, f + 2, gs), v, r[2 + f], r[3 + f]);
+            case FOP_ADD192: {
+                uint64_t w0 = v, w1 = r[2 + f], w2 = r[3 + f];
+                if (nsrc > 0) {
+                    int d = 0;
+                    for (int a = 0; a < p.nacc; ++a)
+                        if (p.acc[a].f_sum == f) d = src_shift[src * kMaxAcc + a];
+                    if (!shl192(w0, w1, w2, d)) {
+                        ovf = true;
+                        break;
+                    }
+                }
+                g_add192(gfield(p, f, gs), gfield(p, f + 1, gs), gfield(p, f + 2, gs), w0, w1, w2);
                 break;
+            }
             default: break;
             }
         }
@@ -1555,6 +1606,7 @@ __global__ void gb_merge_kernel(GbParams p, const uint64_t* __restrict__ rec, in
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) special |= __shfl_xor(special, off, 64);
     if ((threadIdx.x & 63) == 0 && special) atomicOr((unsigned long long*)&p.status[ST_SPECIAL], (unsigned long long)special);
+    if (__any(ovf) && (threadIdx.x & 63) == 0) atomicOr((unsigned long long*)&p.status[ST_SHIFT_OVF], 1ull);
 }
 
 // ------------------------------------------------------------- host
@@ -2738,7 +2790,14 @@ PLGPU_API int plgpu_gb_partial_begin(const plgpu_column* key, const plgpu_column
     bool refit = false;
     int rc = gb_prepare(R, key, cols, ncols, program, n_instr, aggs, naggs, false, true, stream);
     if (!rc) rc = gb_plan(R, bottoms);
-    if (!rc) rc = gb_main(R, false, &refit, out_bottoms_hint);
+    // own windows (bottoms NULL): refits happen here, since each source's
+    // windows travel with its records (plgpu_gb_merge_sources); fixed
+    // windows: a needed refit is reported
+    if (!rc) rc = gb_main(R, bottoms == nullptr, &refit, out_bottoms_hint);
+    if (!rc && R.wide)
+        rc = fail(PLGPU_ERR_CAPACITY,
+                  "f64 sum: the values of one column span more binades than the partitioned "
+                  "group-by's fixed-point window; use the single-GPU group-by for this column");
     if (rc) {
         delete h;
         return rc;
@@ -2791,13 +2850,46 @@ PLGPU_API int plgpu_gb_partial_export(plgpu_gb_partial* h, void* dst_records, in
 
 PLGPU_API void plgpu_gb_partial_free(plgpu_gb_partial* h) { delete h; }
 
-PLGPU_API int plgpu_gb_merge(const void* records, int64_t n_records, const plgpu_column* cols, int32_t ncols,
-                             const plgpu_agg* aggs, int32_t naggs, const int32_t* bottoms, int32_t key_dtype,
-                             plgpu_column* out_key, plgpu_column* out_aggs, plgpu_groupby_info* info, void* stream) {
-    if (out_key == nullptr || bottoms == nullptr || (cols == nullptr && ncols > 0))
-        return fail(PLGPU_ERR_INVALID, "NULL argument");
+// Merge of records from `nsrc` sources (nsrc 0: one source already on the
+// table's windows `bottoms`).  With sources, the table takes, per acc, the
+// lowest window of any source holding records, and each source's sum
+// states are shifted onto it.
+static int gb_merge_impl(const void* records, int64_t n_records, int32_t nsrc, const int64_t* src_records,
+                         const int32_t* src_bottoms, const plgpu_column* cols, int32_t ncols, const plgpu_agg* aggs,
+                         int32_t naggs, const int32_t* bottoms, int32_t key_dtype, plgpu_column* out_key,
+                         plgpu_column* out_aggs, plgpu_groupby_info* info, void* stream) {
+    if (out_key == nullptr || (cols == nullptr && ncols > 0)) return fail(PLGPU_ERR_INVALID, "NULL argument");
     if (ncols < 0 || ncols > PLGPU_MAX_COLS) return fail(PLGPU_ERR_INVALID, "too many columns (max 8)");
     if (n_records < 0 || (n_records > 0 && records == nullptr)) return fail(PLGPU_ERR_INVALID, "bad records");
+    int32_t tb[kMaxAcc];
+    std::vector<int64_t> start;
+    std::vector<int32_t> shift;
+    if (nsrc > 0) {
+        start.assign(nsrc + 1, 0);
+        for (int j = 0; j < nsrc; ++j) {
+            if (src_records[j] < 0) return fail(PLGPU_ERR_INVALID, "bad source record count");
+            start[j + 1] = start[j] + src_records[j];
+        }
+        if (start[nsrc] != n_records) return fail(PLGPU_ERR_INVALID, "source record counts do not add up");
+        for (int a = 0; a < kMaxAcc; ++a) {
+            bool any = false;
+            tb[a] = 0;
+            for (int j = 0; j < nsrc; ++j) {
+                if (src_records[j] == 0) continue;
+                const int32_t b = src_bottoms[j * kMaxAcc + a];
+                tb[a] = any ? std::min(tb[a], b) : b;
+                any = true;
+            }
+            if (!any) tb[a] = src_bottoms[a];
+        }
+        shift.assign((size_t)nsrc * kMaxAcc, 0);
+        for (int j = 0; j < nsrc; ++j)
+            for (int a = 0; a < kMaxAcc; ++a)
+                if (src_records[j] > 0) shift[j * kMaxAcc + a] = src_bottoms[j * kMaxAcc + a] - tb[a];
+    } else {
+        if (bottoms == nullptr) return fail(PLGPU_ERR_INVALID, "NULL argument");
+        for (int a = 0; a < kMaxAcc; ++a) tb[a] = bottoms[a];
+    }
     std::memset(out_key, 0, sizeof *out_key);
     for (int i = 0; i < naggs && out_aggs; ++i) std::memset(&out_aggs[i], 0, sizeof(plgpu_column));
     // the schema alone fixes the record layout: a length-0 key of the right
@@ -2811,27 +2903,76 @@ PLGPU_API int plgpu_gb_merge(const void* records, int64_t n_records, const plgpu
     int rc = gb_prepare(R, &k, c2.data(), ncols, nullptr, 0, aggs, naggs, false, true, stream);
     if (rc) return rc;
     for (int a = 0; a < kMaxAcc; ++a) {
-        R.hb[a] = bottoms[a];
-        R.pl.p.bottom[a] = bottoms[a];
+        R.hb[a] = tb[a];
+        R.pl.p.bottom[a] = tb[a];
     }
     R.gbits = log2_ceil(std::max<int64_t>(1024, n_records * 2));
     GbParams& p = R.pl.p;
-    for (R.attempts = 0;; ++R.attempts) {
-        if ((rc = gb_alloc_table(R))) return rc;
-        PLGPU_HIP(hipMemcpyAsync(R.bottoms, R.hb, sizeof R.hb, hipMemcpyHostToDevice, R.s));
-        if (n_records > 0) {
-            const int g = (int)std::min<int64_t>((n_records + 255) / 256, 256 * 16);
-            gb_merge_kernel<<<g, 256, 0, R.s>>>(p, (const uint64_t*)records, n_records);
-            PLGPU_HIP(hipGetLastError());
+    // source table on the device: nsrc + 1 starts, then nsrc x kMaxAcc shifts
+    int64_t* dsrc = nullptr;
+    if (nsrc > 0) {
+        const size_t bytes = (size_t)(nsrc + 1) * 8 + shift.size() * 4;
+        if ((rc = dev_alloc((void**)&dsrc, bytes, R.s))) return rc;
+        std::vector<uint8_t> h(bytes);
+        std::memcpy(h.data(), start.data(), (size_t)(nsrc + 1) * 8);
+        std::memcpy(h.data() + (size_t)(nsrc + 1) * 8, shift.data(), shift.size() * 4);
+        hipError_t e = hipMemcpyAsync(dsrc, h.data(), bytes, hipMemcpyHostToDevice, R.s);
+        if (e == hipSuccess) e = hipStreamSynchronize(R.s);  // `h` is a host temporary
+        if (e != hipSuccess) {
+            dev_free(dsrc, R.s);
+            return hip_fail(e, "merge sources");
         }
-        PLGPU_HIP(hipMemcpyAsync(R.st, R.status, sizeof R.st, hipMemcpyDeviceToHost, R.s));
-        PLGPU_HIP(hipStreamSynchronize(R.s));
+    }
+    for (R.attempts = 0;; ++R.attempts) {
+        if ((rc = gb_alloc_table(R))) break;
+        hipError_t e = hipMemcpyAsync(R.bottoms, R.hb, sizeof R.hb, hipMemcpyHostToDevice, R.s);
+        if (e == hipSuccess && n_records > 0) {
+            const int g = (int)std::min<int64_t>((n_records + 255) / 256, 256 * 16);
+            gb_merge_kernel<<<g, 256, 0, R.s>>>(p, (const uint64_t*)records, n_records, nsrc, dsrc,
+                                                dsrc ? (const int32_t*)(dsrc + nsrc + 1) : nullptr);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) e = hipMemcpyAsync(R.st, R.status, sizeof R.st, hipMemcpyDeviceToHost, R.s);
+        if (e == hipSuccess) e = hipStreamSynchronize(R.s);
+        if (e != hipSuccess) {
+            rc = hip_fail(e, "gb_merge_kernel");
+            break;
+        }
+        if (R.st[ST_SHIFT_OVF]) {
+            rc = fail(PLGPU_ERR_CAPACITY,
+                      "multi-GPU group-by: the ranks' f64 sums span more binades than one 192-bit state holds");
+            break;
+        }
         if (R.st[ST_TABLE_FULL] == 0) break;
-        if (R.attempts >= 3) return fail(PLGPU_ERR_CAPACITY, "merge did not converge");
+        if (R.attempts >= 3) {
+            rc = fail(PLGPU_ERR_CAPACITY, "merge did not converge");
+            break;
+        }
         R.gbits += 3;
     }
+    dev_free(dsrc, R.s);
+    if (rc) return rc;
     if (info) gb_fill_info(R, info);
     return gb_finalize(R, naggs, out_key, out_aggs);
+}
+
+PLGPU_API int plgpu_gb_merge(const void* records, int64_t n_records, const plgpu_column* cols, int32_t ncols,
+                             const plgpu_agg* aggs, int32_t naggs, const int32_t* bottoms, int32_t key_dtype,
+                             plgpu_column* out_key, plgpu_column* out_aggs, plgpu_groupby_info* info, void* stream) {
+    return gb_merge_impl(records, n_records, 0, nullptr, nullptr, cols, ncols, aggs, naggs, bottoms, key_dtype,
+                         out_key, out_aggs, info, stream);
+}
+
+PLGPU_API int plgpu_gb_merge_sources(const void* records, int32_t n_sources, const int64_t* src_records,
+                                     const int32_t* src_bottoms, const plgpu_column* cols, int32_t ncols,
+                                     const plgpu_agg* aggs, int32_t naggs, int32_t key_dtype, plgpu_column* out_key,
+                                     plgpu_column* out_aggs, plgpu_groupby_info* info, void* stream) {
+    if (n_sources < 1 || src_records == nullptr || src_bottoms == nullptr)
+        return fail(PLGPU_ERR_INVALID, "merge: need >= 1 source with its record count and windows");
+    int64_t n = 0;
+    for (int j = 0; j < n_sources; ++j) n += src_records[j];
+    return gb_merge_impl(records, n, n_sources, src_records, src_bottoms, cols, ncols, aggs, naggs, nullptr,
+                         key_dtype, out_key, out_aggs, info, stream);
 }
 
 // ------------------------------------------------------ multi-key group-by

@@ -7,16 +7,17 @@ partition's share with `combine_subset` (group_by.rs:378) in
 `combine_locals` (group_by.rs:216).  Here the "locals" are GPUs:
 
 1. every rank filters + pre-aggregates its own shard in HBM
-   (`plgpu_gb_partial_begin`, the same fused kernel as the single-GPU path);
-   f64 sums are exact 192-bit fixed-point states, so ranks first agree on
-   the fixed-point windows (element-wise MAX all-reduce, a re-run only on a
-   rank whose windows moved);
+   (`plgpu_gb_partial_begin`, the same fused kernel as the single-GPU path)
+   with its own f64 fixed-point windows (exact 192-bit states; a window
+   that does not fit the shard is refitted locally);
 2. the partial groups are written as records grouped by destination rank
-   (`plgpu_gb_partial_export`), record counts go through one all-to-all and
-   the records through a second one (`torch.distributed.all_to_all_single`,
-   RCCL over xGMI on MI355X);
-3. each rank folds what it received into its partition and finalizes it
-   (`plgpu_gb_merge`), returning a DataFrame of the groups it owns.
+   (`plgpu_gb_partial_export`); one all-to-all carries each destination's
+   record count together with the sender's windows and status, a second
+   one the records (`torch.distributed.all_to_all_single`, RCCL over xGMI
+   on MI355X);
+3. each rank shifts every source's sum states onto the lowest window
+   (exact), folds them into its partition and finalizes it
+   (`plgpu_gb_merge_sources`), returning a DataFrame of the groups it owns.
 
 The only data-path collective is the record exchange, whose volume is
 groups x record size (independent of the row count), so the per-rank work
@@ -33,9 +34,6 @@ from typing import Any, Sequence
 
 from . import _native as N
 from .expr import Expr
-
-MAX_WINDOW_ROUNDS = 4
-
 
 def _device_for(group) -> Any:
     import torch
@@ -114,37 +112,27 @@ def alltoallv(out, inp, out_splits: Sequence[int], in_splits: Sequence[int], gro
                 req.wait()
 
 
-def exchange_records(send, counts: Sequence[int], record_words: int, group=None):
+def exchange_records(send, counts: Sequence[int], record_words: int, group=None, header: Sequence[int] = ()):
     """All-to-all of records grouped by destination rank.  `send` is a flat
-    int64 tensor of sum(counts) * record_words words; returns (recv, n)."""
+    int64 tensor of sum(counts) * record_words words.  `header` (ints) goes
+    to every destination with its count.  Returns (recv, n, rows): rows[q] =
+    [records from rank q] + rank q's header, in source-rank order (the
+    order of the records in `recv`)."""
     import torch
     import torch.distributed as dist
 
     device = send.device
-    sc = torch.tensor(list(counts), dtype=torch.int64, device=device)
+    world = len(counts)
+    h = len(header)
+    sc = torch.tensor([[int(c)] + [int(x) for x in header] for c in counts], dtype=torch.int64, device=device)
     rc = torch.empty_like(sc)
     dist.all_to_all_single(rc, sc, group=group)
-    rcounts = [int(v) for v in rc.tolist()]
+    rows = [[int(v) for v in r] for r in rc.view(world, 1 + h).tolist()]
+    rcounts = [r[0] for r in rows]
     recv = torch.empty(sum(rcounts) * record_words, dtype=torch.int64, device=device)
     alltoallv(recv, send, [c * record_words for c in rcounts], [c * record_words for c in counts], group)
     _settle(device)
-    return recv, sum(rcounts)
-
-
-def agree_windows(part, world: int, group, device) -> list[int]:
-    """Run the partial stage until every rank used the same windows.
-
-    `part.begin(bottoms)` returns (used, refit, hint); bottoms None = the
-    shard's sampled windows.  Returns the agreed windows."""
-    used, refit, hint = part.begin(None)
-    for _ in range(MAX_WINDOW_ROUNDS):
-        agreed = _allreduce_max(list(hint), group, device)
-        need = int(list(used) != agreed)
-        if _allreduce_max([need], group, device)[0] == 0:
-            return agreed
-        if need:
-            used, refit, hint = part.begin(agreed)
-    raise N.ComputeError("multi-GPU group-by: fixed-point windows did not converge")
+    return recv, sum(rcounts), rows
 
 
 class GpuPartial:
@@ -175,20 +163,18 @@ class GpuPartial:
         except (AttributeError, TypeError):
             pass
 
-    def begin(self, bottoms):
+    def begin(self) -> list[int]:
+        """Pre-aggregate the shard with its own windows; returns them."""
         self.free()
         g = self.g
-        arg = None
-        if bottoms is not None:
-            arg = (C.c_int32 * N.GB_MAX_ACC)(*bottoms)
         nrec = C.c_int64(0)
         refit = C.c_int32(0)
         hint = (C.c_int32 * N.GB_MAX_ACC)()
         N.check(N.lib().plgpu_gb_partial_begin(C.byref(g.keycol), g.cols, g.ncols, g.prog, g.n_instr, g.aggs,
-                                               g.naggs, arg, self.world, C.byref(self.handle), C.byref(nrec),
+                                               g.naggs, None, self.world, C.byref(self.handle), C.byref(nrec),
                                                self.bottoms, C.byref(refit), hint, C.byref(self.info), None))
         self.nrec = int(nrec.value)
-        return list(self.bottoms), bool(refit.value), list(hint)
+        return list(self.bottoms)
 
     def export(self):
         """-> (flat int64 CUDA tensor of records grouped by rank, counts)."""
@@ -202,16 +188,20 @@ class GpuPartial:
         self.free()
         return send, [int(c) for c in counts]
 
-    def merge(self, recv, n: int, bottoms):
+    def merge(self, recv, src_counts: Sequence[int], src_bottoms: Sequence[Sequence[int]]):
+        """Fold the records of every source rank (windows per source)."""
         from .frame import _gb_frame
 
         g = self.g
-        b = (C.c_int32 * N.GB_MAX_ACC)(*bottoms)
+        ns = len(src_counts)
+        cnt = (C.c_int64 * ns)(*src_counts)
+        bot = (C.c_int32 * (ns * N.GB_MAX_ACC))(*[int(b) for row in src_bottoms for b in row])
         out_key = N.Column()
         out_aggs = (N.Column * max(1, g.naggs))()
         mi = N.GroupByInfo()
-        N.check(N.lib().plgpu_gb_merge(recv.data_ptr() if n else None, n, g.cols, g.ncols, g.aggs, g.naggs, b,
-                                       g.keycol.dtype, C.byref(out_key), out_aggs, C.byref(mi), None))
+        N.check(N.lib().plgpu_gb_merge_sources(recv.data_ptr() if sum(src_counts) else None, ns, cnt, bot, g.cols,
+                                               g.ncols, g.aggs, g.naggs, g.keycol.dtype, C.byref(out_key),
+                                               out_aggs, C.byref(mi), None))
         return _gb_frame(g, out_key, out_aggs), mi
 
 
@@ -224,19 +214,39 @@ def _sync(device) -> None:
 
 def run_partitioned(part, world: int, group, device, timings: dict | None = None):
     """The protocol of group_by_agg over any partial implementation (the
-    GPU one above, or a host model in tests/test_distributed.py).  With
-    `timings`, the wall time of each phase (device-synchronised) is stored
-    as partial_ms (local pre-aggregation + window agreement), exchange_ms
-    (export + all-to-all of the records) and merge_ms."""
+    GPU one above, or a host model in tests/test_distributed.py).
+
+    The partial stage runs with no collective.  A rank whose partial stage
+    fails still takes part in the count exchange (status 1, no records), so
+    every rank learns of the failure and raises instead of waiting in a
+    collective.  With `timings`, the wall time of each phase (device-
+    synchronised) is stored as partial_ms (local pre-aggregation), exchange_ms
+    (export + the two all-to-alls) and merge_ms."""
     t0 = time.perf_counter()
-    bottoms = agree_windows(part, world, group, device)
+    err = None
+    try:
+        bottoms = part.begin()
+    except N.PolaroidError as e:  # refused locally (e.g. a wide-range f64 sum)
+        err = e
+        bottoms = [0] * N.GB_MAX_ACC
     if timings is not None:
         _sync(device)
     t1 = time.perf_counter()
-    send, counts = part.export()
-    recv, n = exchange_records(send, counts, part.record_words, group)
+    if err is None:
+        send, counts = part.export()
+    else:
+        import torch
+
+        send, counts = torch.empty(0, dtype=torch.int64, device=device), [0] * world
+    recv, n, rows = exchange_records(send, counts, part.record_words, group,
+                                     header=[1 if err is not None else 0] + list(bottoms))
+    failed = [q for q, r in enumerate(rows) if r[1]]
+    if err is not None:
+        raise err
+    if failed:
+        raise N.ComputeError(f"multi-GPU group-by: the partial stage failed on rank(s) {failed}")
     t2 = time.perf_counter()
-    res = part.merge(recv, n, bottoms)
+    res = part.merge(recv, [r[0] for r in rows], [r[2:] for r in rows])
     if timings is not None:
         _sync(device)
         t3 = time.perf_counter()

@@ -2,11 +2,12 @@
 world_size 2 over gloo, with a host model of the partial stage in place of
 the GPU kernels (those are covered by tests/test_gpu_distributed.py).
 
-Checks: every rank ends on the same fixed-point windows (including a round
-where one rank must refit and the others re-run), records are routed by
-destination rank with one all-to-all of counts and one of records, each
-group lands on exactly one rank, and the union of the partitions equals the
-single-process aggregation.
+Checks: the partial stage runs without a collective, each rank's windows
+travel with its record counts (one all-to-all of counts + header, one of
+records), every destination receives every source's windows in source
+order, each group lands on exactly one rank, the union of the partitions
+equals the single-process aggregation, and a partial stage that fails on one
+rank makes every rank raise instead of hanging in a collective.
 """
 
 import os
@@ -37,27 +38,27 @@ def _shard(rank, n=5000, groups=97):
     return keys, vals
 
 
+def _bottoms(rank):
+    return [10 * rank + 1, -3, 0, 0, 0, rank]
+
+
 class HostPartial:
     """Models GpuPartial: begin / export / merge over numpy."""
 
     record_words = RW
 
-    def __init__(self, rank, world, keys, vals, refit_rank):
+    def __init__(self, rank, world, keys, vals, fail_rank):
         self.rank, self.world = rank, world
         self.keys, self.vals = keys, vals
-        self.refit_rank = refit_rank
-        self.begins = []
+        self.fail_rank = fail_rank
         self.groups = None
 
-    def begin(self, bottoms):
-        used = list(bottoms) if bottoms is not None else [10 * self.rank + 1, -3, 0, 0, 0, 0]
-        self.begins.append(used)
+    def begin(self):
+        if self.rank == self.fail_rank:
+            raise D.N.ComputeError("refused on this rank")
         ks, inv = np.unique(self.keys, return_inverse=True)
         self.groups = (ks, np.array([self.vals[inv == i].sum() for i in range(len(ks))], dtype=np.int64))
-        if self.rank == self.refit_rank and len(self.begins) == 1:
-            hint = [u + 50 for u in used]   # "overflow": the window must move up
-            return used, True, hint
-        return used, False, used
+        return _bottoms(self.rank)
 
     def export(self):
         ks, sums = self.groups
@@ -67,58 +68,69 @@ class HostPartial:
         counts = [int((dest == r).sum()) for r in range(self.world)]
         return torch.from_numpy(rec.copy()), counts
 
-    def merge(self, recv, n, bottoms):
+    def merge(self, recv, src_counts, src_bottoms):
+        n = sum(src_counts)
         r = recv.numpy().reshape(n, RW)
         out = {}
         for _, k, s in r:
             out[int(k)] = out.get(int(k), 0) + int(s)
-        return (out, list(bottoms)), None
+        return (out, list(src_counts), [list(b) for b in src_bottoms]), None
 
 
-def _worker(rank, port, refit_rank, q):
+def _worker(rank, port, fail_rank, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=WORLD)
     try:
         keys, vals = _shard(rank)
-        part = HostPartial(rank, WORLD, keys, vals, refit_rank)
-        (out, bottoms), _ = D.run_partitioned(part, WORLD, None, torch.device("cpu"))
+        part = HostPartial(rank, WORLD, keys, vals, fail_rank)
+        try:
+            (out, src_counts, src_bottoms), _ = D.run_partitioned(part, WORLD, None, torch.device("cpu"))
+            err = None
+        except D.N.PolaroidError as e:
+            out, src_counts, src_bottoms, err = None, None, None, type(e).__name__ + ": " + str(e)
         # exchange_records on its own: ragged counts including empty segments
         rw = 2
         counts = [0, 3] if rank == 0 else [5, 0]
         send = torch.arange(sum(counts) * rw, dtype=torch.int64) + 1000 * rank
-        recv, nrec = D.exchange_records(send, counts, rw)
-        q.put((rank, out, bottoms, part.begins, recv.tolist(), nrec))
+        recv, nrec, rows = D.exchange_records(send, counts, rw, header=[7, rank])
+        q.put((rank, out, src_counts, src_bottoms, err, recv.tolist(), nrec, rows))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("refit_rank", [-1, 0, 1])
-def test_partitioned_group_by_protocol_gloo(refit_rank):
+@pytest.mark.parametrize("fail_rank", [-1, 0, 1])
+def test_partitioned_group_by_protocol_gloo(fail_rank):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, port, refit_rank, q)) for r in range(WORLD)]
+    procs = [ctx.Process(target=_worker, args=(r, port, fail_rank, q)) for r in range(WORLD)]
     for p in procs:
         p.start()
     res = {}
     for _ in range(WORLD):
-        rank, out, bottoms, begins, recv, nrec = q.get(timeout=120)
-        res[rank] = (out, bottoms, begins, recv, nrec)
+        rank, out, src_counts, src_bottoms, err, recv, nrec, rows = q.get(timeout=120)
+        res[rank] = (out, src_counts, src_bottoms, err, recv, nrec, rows)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    # same windows everywhere, and they are the MAX over the ranks' hints
-    b0, b1 = res[0][1], res[1][1]
-    assert b0 == b1
-    sampled = [[10 * r + 1, -3, 0, 0, 0, 0] for r in range(WORLD)]
-    expect = [max(s[i] for s in sampled) for i in range(6)]
-    if refit_rank >= 0:
-        expect = [max(e, s + 50) for e, s in zip(expect, sampled[refit_rank])]
-    assert b0 == expect
-    # the partial that was merged ran with the agreed windows
+    # ragged exchange: rank 0 receives rank1's 5 records, rank 1 receives rank0's 3;
+    # every destination gets [count] + each source's header, in source order
+    assert res[0][5] == 5 and res[0][4] == list(range(1000, 1010))
+    assert res[1][5] == 3 and res[1][4] == list(range(0, 6))
+    assert res[0][6] == [[0, 7, 0], [5, 7, 1]]
+    assert res[1][6] == [[3, 7, 0], [0, 7, 1]]
+    if fail_rank >= 0:
+        # the failing rank re-raises its own error, the others name it
+        assert "refused on this rank" in res[fail_rank][3]
+        other = 1 - fail_rank
+        assert res[other][3].startswith("ComputeError") and f"[{fail_rank}]" in res[other][3]
+        return
+    # every destination received each source's own windows, in rank order
     for r in range(WORLD):
-        assert res[r][2][-1] == expect
+        assert res[r][3] is None
+        assert res[r][2] == [_bottoms(q) for q in range(WORLD)]
+        assert len(res[r][0]) <= sum(res[r][1]) <= WORLD * len(res[r][0])
     # partitions are disjoint and their union is the full aggregation
     k0, k1 = set(res[0][0]), set(res[1][0])
     assert not (k0 & k1)
@@ -132,6 +144,3 @@ def test_partitioned_group_by_protocol_gloo(refit_rank):
     assert merged == full
     for r in range(WORLD):
         assert all(k % WORLD == r for k in res[r][0])
-    # ragged exchange: rank 0 receives rank1's 5 records, rank 1 receives rank0's 3
-    assert res[0][4] == 5 and res[0][3] == list(range(1000, 1010))
-    assert res[1][4] == 3 and res[1][3] == list(range(0, 6))

@@ -2,10 +2,11 @@
 through the C-ABI, against the oracle's exact leg on the concatenated data.
 
 A W-way partitioned run is simulated in one process on one GPU: W shards are
-pre-aggregated by plgpu_gb_partial_begin (after the same window agreement
-distributed.agree_windows performs), exported with plgpu_gb_partial_export,
-the records for each destination are concatenated the way all_to_all_single
-lays them out, and each destination merges with plgpu_gb_merge.  The union
+pre-aggregated by plgpu_gb_partial_begin, each with its own fixed-point
+windows, exported with plgpu_gb_partial_export, the records for each
+destination are concatenated the way all_to_all_single lays them out, and
+each destination merges them with plgpu_gb_merge_sources given every
+source's record count and windows.  The union
 of the W partitions must equal the single-pass result bit for bit (exact
 f64 sums are associative, so sharding cannot change them).  The real
 torch.distributed path is exercised at world_size 1 over RCCL.
@@ -51,31 +52,20 @@ def _simulate(shards, world, aggs, pred):
 
     exprs = [getattr(pl.col(c), k)().alias(f"{k}_{c}") for k, c in aggs]
     parts = [D.GpuPartial(_gb_lower(df, "k", exprs, pred), world) for df in shards]
-    state = [p.begin(None) for p in parts]          # (used, refit, hint)
-    for _ in range(D.MAX_WINDOW_ROUNDS):
-        agreed = [max(s[2][i] for s in state) for i in range(6)]
-        need = [s[0] != agreed for s in state]
-        if not any(need):
-            break
-        for i, p in enumerate(parts):
-            if need[i]:
-                state[i] = p.begin(agreed)
-    else:
-        raise AssertionError("windows did not converge")
+    windows = [p.begin() for p in parts]
     rw = parts[0].record_words
     exported = [p.export() for p in parts]
     frames = []
     for dest in range(world):
-        segs = []
-        n = 0
+        segs, cnts = [], []
         for send, counts in exported:
             off = sum(counts[:dest]) * rw
             segs.append(send[off: off + counts[dest] * rw])
-            n += counts[dest]
+            cnts.append(counts[dest])
         recv = torch.cat(segs) if segs else torch.empty(0, dtype=torch.int64, device="cuda")
-        out, _ = parts[dest].merge(recv.contiguous(), n, agreed)
+        out, _ = parts[dest].merge(recv.contiguous(), cnts, windows)
         frames.append(out)
-    return frames, agreed
+    return frames, windows
 
 
 def _check(frames, cols, key, kvalid, aggs, pred_prog, names):
@@ -149,8 +139,17 @@ def test_partitioned_with_predicate(gpu):
 
 def test_partitioned_window_agreement(gpu):
     """Shards of very different magnitude sample different windows; the
-    agreed (MAX) window must reproduce the exact sum of all shards."""
-    frames, agreed = _run_case(2, 2, 40000, 50, scales=[1e-3, 1e12], nulls=False, specials=False)
+    merge shifts every source's exact states onto the lowest window, which
+    must reproduce the exact sum of all shards."""
+    frames, windows = _run_case(2, 2, 40000, 50, scales=[1e-3, 1e12], nulls=False, specials=False)
+    assert windows[0][0] < windows[1][0] - 40
+
+
+def test_partitioned_windows_too_far_apart(gpu):
+    """Sums whose windows differ by more than one 192-bit state spans are
+    refused (PLGPU_ERR_CAPACITY -> ComputeError), never wrong."""
+    with pytest.raises(pl.ComputeError, match="192-bit"):
+        _run_case(2, 2, 20000, 10, scales=[1e-40, 1e40], nulls=False, specials=False)
 
 
 def test_partitioned_fast_path_shards(gpu):
