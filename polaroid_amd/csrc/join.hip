@@ -1824,6 +1824,489 @@ static void jn_take_emit(const JnPass& pp, const TakeCols& lc, uint64_t* mp, uin
 // the null-free 8-byte left columns straight to their output rows -- no
 // index pairs, no random gather of the build side.  Everything else takes
 // pairs + gathers.
+// ------------------------------------ XCD-partitioned row-format join (xp)
+// An inner join whose output order is free (maintain_order "none"), with
+// unique build keys and null-free 8-byte payload / left columns.  The probe
+// is bound by random line requests when the table lives in HBM / the
+// Infinity Cache (about 55 G/s, ~20 ms per 1e9 probes).  A table slice held
+// in ONE XCD's 4 MiB L2 serves single-lane reads at 265-279 G/s
+// (tools/randread_bench.hip "xcd" rows, profiles/r02_randread.txt).  So:
+//   build   - the build keys are hash-partitioned into P = 8 S sub-tables of
+//             2^cbits 16-B cells {key, payload} (about 1 MiB each); XCD x
+//             owns sub-tables [x S, (x + 1) S);
+//   count   - probe rows per (sub-table, workgroup chunk), then a scan;
+//   scatter - each probe row's key and left columns are written, column by
+//             column through LDS, into sub-table order (one run per
+//             sub-table per 4096-row tile);
+//   probe   - workgroup b runs on XCD b % 8 (round-robin dispatch) and
+//             sweeps that XCD's rows in order, so the workgroups of an XCD
+//             probe the same one or two sub-tables at a time, from L2; the
+//             hits of a tile get their output range from one atomic add on
+//             a cursor, so the output order is the probe tile completion
+//             order (unspecified, as the reference's "none" order is).
+// The XCD placement is a speed assumption only; results never depend on it.
+constexpr int kXpThreads = 256;
+constexpr int kXpPer = 16;
+constexpr int kXpTile = kXpThreads * kXpPer;   // count / scatter tile: 4096 rows
+constexpr int kXpProbeRows = 8;                // probe rows per thread
+constexpr int kXpProbeTile = kXpThreads * kXpProbeRows;
+constexpr int kXpMaxParts = 1024;
+constexpr uint64_t kXpSalt = 0x6A09E667F3BCC909ull;
+
+struct XpTable {
+    uint4* cells;  // P * 2^cbits cells {key lo, key hi, payload lo, payload hi}; EMPTY key = INT64_MIN
+    int P;
+    int cbits;
+};
+
+__device__ __forceinline__ uint64_t xp_hash(uint64_t k) { return mk_fmix(k ^ kXpSalt); }
+__device__ __forceinline__ uint32_t xp_part(uint64_t h, int P) { return (uint32_t)(((h >> 32) * (uint64_t)P) >> 32); }
+
+__global__ void xp_init_kernel(XpTable t, int64_t ncells) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ncells; i += (int64_t)gridDim.x * blockDim.x)
+        t.cells[i] = make_uint4(0u, 0x80000000u, 0u, 0u);
+}
+
+// status[0]: a row found no free cell; [1]: duplicate key; [2]: an
+// INT64_MIN build key (the EMPTY marker) -- each sends the join back to the
+// general paths.  Null build keys join nothing (nulls_equal false).
+__global__ void xp_build_kernel(DevCol bk, int64_t nb, XpTable t, DevCol pay, unsigned long long* status) {
+    const uint64_t cmask = (1ull << t.cbits) - 1;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nb; i += (int64_t)gridDim.x * blockDim.x) {
+        if (!dev_valid(bk, i)) continue;
+        const uint64_t key = dev_load(bk, i);
+        if (key == kEmptyKey) {
+            atomicOr(&status[2], 1ull);
+            continue;
+        }
+        const uint64_t h = xp_hash(key);
+        const uint64_t base = (uint64_t)xp_part(h, t.P) << t.cbits;
+        uint64_t s = h & cmask;
+        bool placed = false;
+        for (uint64_t p = 0; p <= cmask; ++p, s = (s + 1) & cmask) {
+            uint64_t* kw = (uint64_t*)&t.cells[base + s];
+            uint64_t k = __hip_atomic_load(kw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (k == kEmptyKey) {
+                k = atomicCAS((unsigned long long*)kw, (unsigned long long)kEmptyKey, (unsigned long long)key);
+                if (k == kEmptyKey) {
+                    const uint64_t v = dev_load(pay, i);
+                    uint32_t* c = (uint32_t*)&t.cells[base + s];
+                    c[2] = (uint32_t)v;
+                    c[3] = (uint32_t)(v >> 32);
+                    placed = true;
+                    break;
+                }
+            }
+            if (k == key) {
+                atomicOr(&status[1], 1ull);
+                placed = true;
+                break;
+            }
+        }
+        if (!placed) atomicOr(&status[0], 1ull);
+    }
+}
+
+// Probe rows of workgroup b's contiguous chunk of tiles.
+__device__ __forceinline__ void xp_chunk(int64_t n, int64_t& lo, int64_t& hi) {
+    const int64_t tiles = (n + kXpTile - 1) / kXpTile;
+    const int64_t per = (tiles + gridDim.x - 1) / gridDim.x;
+    lo = std::min<int64_t>(n, (int64_t)blockIdx.x * per * kXpTile);
+    hi = std::min<int64_t>(n, lo + per * kXpTile);
+}
+
+// Sub-table of probe row r, or ~0u for a row that joins nothing (null key,
+// or the INT64_MIN key, which no build row holds on this path).
+__device__ __forceinline__ uint32_t xp_row_part(const uint64_t* kp, const uint8_t* kvalid, int64_t koff, int64_t r,
+                                                int64_t hi, int P, uint64_t& key) {
+    key = __builtin_nontemporal_load(kp + (r < hi ? r : hi - 1));
+    const bool ok = r < hi && (kvalid == nullptr || ((kvalid[(koff + r) >> 3] >> ((koff + r) & 7)) & 1)) &&
+                    key != kEmptyKey;
+    return ok ? xp_part(xp_hash(key), P) : ~0u;
+}
+
+// cnt[q * G + b]: probe rows of workgroup b's chunk in sub-table q.
+__global__ __launch_bounds__(kXpThreads) void xp_count_kernel(const uint64_t* __restrict__ kp,
+                                                              const uint8_t* __restrict__ kvalid, int64_t koff,
+                                                              int64_t np, int P, uint32_t* __restrict__ cnt) {
+    __shared__ uint32_t h[kXpMaxParts];
+    for (int i = threadIdx.x; i < P; i += blockDim.x) h[i] = 0;
+    __syncthreads();
+    int64_t lo, hi;
+    xp_chunk(np, lo, hi);
+    for (int64_t base = lo; base < hi; base += kXpTile) {
+        uint32_t q[kXpPer];
+        uint64_t key;
+#pragma unroll
+        for (int k = 0; k < kXpPer; ++k) q[k] = xp_row_part(kp, kvalid, koff, base + k * kXpThreads + threadIdx.x, hi, P, key);
+#pragma unroll
+        for (int k = 0; k < kXpPer; ++k)
+            if (q[k] != ~0u) atomicAdd(&h[q[k]], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < P; i += blockDim.x) cnt[(int64_t)i * gridDim.x + blockIdx.x] = h[i];
+}
+
+// Columns moved into sub-table order: src[0] is the key (kp), the others
+// null-free 8-byte columns; dst[j] the partitioned arrays.
+struct XpCols {
+    const uint64_t* src[PLGPU_MAX_COLS + 1];
+    uint64_t* dst[PLGPU_MAX_COLS + 1];
+    int32_t n;
+};
+
+__global__ __launch_bounds__(kXpThreads) void xp_scatter_kernel(const uint8_t* __restrict__ kvalid, int64_t koff,
+                                                                int64_t np, int P, const uint64_t* __restrict__ off,
+                                                                XpCols c) {
+    __shared__ uint32_t h[kXpMaxParts];
+    __shared__ uint32_t lstart[kXpMaxParts];
+    __shared__ uint64_t gcur[kXpMaxParts];
+    __shared__ uint64_t sval[kXpTile];
+    __shared__ uint16_t spart[kXpTile];
+    __shared__ uint64_t wsum[kXpThreads / 64];
+    __shared__ uint32_t tile_n;
+    constexpr int QPT = kXpMaxParts / kXpThreads;
+    for (int i = threadIdx.x; i < P; i += blockDim.x) gcur[i] = off[(int64_t)i * gridDim.x + blockIdx.x];
+    int64_t lo, hi;
+    xp_chunk(np, lo, hi);
+    for (int64_t base = lo; base < hi; base += kXpTile) {
+        for (int i = threadIdx.x; i < P; i += blockDim.x) h[i] = 0;
+        __syncthreads();
+        uint32_t pr[kXpPer];
+        uint64_t key[kXpPer], v1[kXpPer];
+        // the first non-key column's loads go out with the keys'
+#pragma unroll
+        for (int k = 0; k < kXpPer; ++k) {
+            const int64_t r = base + k * kXpThreads + threadIdx.x;
+            key[k] = __builtin_nontemporal_load(c.src[0] + (r < hi ? r : hi - 1));
+            if (c.n > 1) v1[k] = __builtin_nontemporal_load(c.src[1] + (r < hi ? r : hi - 1));
+        }
+#pragma unroll
+        for (int k = 0; k < kXpPer; ++k) {
+            const int64_t r = base + k * kXpThreads + threadIdx.x;
+            const bool ok = r < hi && (kvalid == nullptr || ((kvalid[(koff + r) >> 3] >> ((koff + r) & 7)) & 1)) &&
+                            key[k] != kEmptyKey;
+            const uint32_t q = ok ? xp_part(xp_hash(key[k]), P) : ~0u;
+            pr[k] = q == ~0u ? ~0u : ((q << 16) | atomicAdd(&h[q], 1u));
+        }
+        __syncthreads();
+        uint32_t cq[QPT], sum = 0;
+#pragma unroll
+        for (int j = 0; j < QPT; ++j) {
+            const int q = threadIdx.x * QPT + j;
+            cq[j] = q < P ? h[q] : 0u;
+            sum += cq[j];
+        }
+        uint64_t total;
+        uint32_t run = (uint32_t)block_excl_scan(sum, wsum, total);
+#pragma unroll
+        for (int j = 0; j < QPT; ++j) {
+            const int q = threadIdx.x * QPT + j;
+            if (q < P) lstart[q] = run;
+            run += cq[j];
+        }
+        if (threadIdx.x == 0) tile_n = (uint32_t)total;
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kXpPer; ++k) {
+            if (pr[k] == ~0u) continue;
+            const uint32_t q = pr[k] >> 16;
+            pr[k] = lstart[q] + (pr[k] & 0xFFFFu);
+            spart[pr[k]] = (uint16_t)q;
+        }
+        const uint32_t m = tile_n;
+        for (int col = 0; col < c.n; ++col) {
+            uint64_t v[kXpPer];
+            if (col == 1) {
+#pragma unroll
+                for (int k = 0; k < kXpPer; ++k) v[k] = v1[k];
+            } else if (col > 1) {
+#pragma unroll
+                for (int k = 0; k < kXpPer; ++k) {
+                    const int64_t r = base + k * kXpThreads + threadIdx.x;
+                    v[k] = __builtin_nontemporal_load(c.src[col] + (r < hi ? r : hi - 1));
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < kXpPer; ++k)
+                if (pr[k] != ~0u) sval[pr[k]] = col == 0 ? key[k] : v[k];
+            __syncthreads();
+            uint64_t* dst = c.dst[col];
+            for (uint32_t t = threadIdx.x; t < m; t += blockDim.x) {
+                const uint32_t q = spart[t];
+                dst[gcur[q] + (t - lstart[q])] = sval[t];
+            }
+            __syncthreads();
+        }
+        for (int i = threadIdx.x; i < P; i += blockDim.x) gcur[i] += h[i];
+    }
+}
+
+// Probe of the partitioned rows.  xr[x] .. xr[x + 1]: the rows of XCD x's
+// sub-tables.  A hit writes the payload and the row's left columns (lsrc[j],
+// partitioned arrays) at out position cursor-range base + its rank in the
+// tile (row chunk major, wave ballots), so each wave's writes are contiguous.
+template <int NC>
+__global__ __launch_bounds__(kXpThreads) void xp_probe_kernel(const uint64_t* __restrict__ pkey, TakeCols lc,
+                                                              const int64_t* __restrict__ xr, XpTable t,
+                                                              uint64_t* __restrict__ out_pay,
+                                                              unsigned long long* __restrict__ cursor) {
+    constexpr int R = kXpProbeRows;
+    constexpr int NW = kXpThreads / 64;
+    __shared__ uint32_t cnt[R * NW];
+    __shared__ uint64_t tile_base;
+    __shared__ int64_t next_tile;
+    const int x = blockIdx.x & 7;
+    const int64_t lo = xr[x], hi = xr[x + 1];
+    const int64_t ntiles = (hi - lo + kXpProbeTile - 1) / kXpProbeTile;
+    const uint64_t cmask = (1ull << t.cbits) - 1;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    // the workgroups of XCD x take its tiles in order from one queue
+    // (cursor[8 + 16 x]), so together they sweep one or two sub-tables at a
+    // time whatever order they were dispatched in
+    unsigned long long* queue = cursor + 8 + 16 * x;
+    for (;;) {
+        __syncthreads();
+        if (threadIdx.x == 0) next_tile = (int64_t)atomicAdd(queue, 1ull);
+        __syncthreads();
+        const int64_t tile = next_tile;
+        if (tile >= ntiles) break;
+        const int64_t base = lo + tile * kXpProbeTile;
+        uint64_t key[R], cell[R], pay[R];
+        bool live[R];
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const int64_t r = base + k * kXpThreads + threadIdx.x;
+            live[k] = r < hi;
+            key[k] = __builtin_nontemporal_load(pkey + (r < hi ? r : hi - 1));
+        }
+        // rounds of single-cell probes, every pending row's load in flight
+        uint64_t sub[R];
+        uint32_t hit = 0, pend = 0;
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const uint64_t h = xp_hash(key[k]);
+            sub[k] = ((uint64_t)xp_part(h, t.P) << t.cbits);
+            cell[k] = h & cmask;
+            pend |= (live[k] ? 1u : 0u) << k;
+        }
+        // (bounded: every cell of a sub-table visited once at most, even if
+        // a sub-table were full)
+        for (uint64_t round = 0; pend && round <= cmask; ++round) {
+            uint4 cv[R];
+#pragma unroll
+            for (int k = 0; k < R; ++k)
+                cv[k] = ((pend >> k) & 1u) ? t.cells[sub[k] + cell[k]] : make_uint4(0u, 0x80000000u, 0u, 0u);
+#pragma unroll
+            for (int k = 0; k < R; ++k) {
+                if (!((pend >> k) & 1u)) continue;
+                const uint64_t kk = (uint64_t)cv[k].x | ((uint64_t)cv[k].y << 32);
+                if (kk == key[k]) {
+                    hit |= 1u << k;
+                    pay[k] = (uint64_t)cv[k].z | ((uint64_t)cv[k].w << 32);
+                    pend &= ~(1u << k);
+                } else if (kk == kEmptyKey) {
+                    pend &= ~(1u << k);
+                } else {
+                    cell[k] = (cell[k] + 1) & cmask;
+                }
+            }
+        }
+        // output ranks: chunk k, wave w -> cnt[k * NW + w]
+        uint64_t bal[R];
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            bal[k] = __ballot((hit >> k) & 1u);
+            if (lane == 0) cnt[k * NW + wave] = (uint32_t)__popcll(bal[k]);
+        }
+        __syncthreads();
+        if (threadIdx.x < 64) {
+            const uint32_t v = threadIdx.x < R * NW ? cnt[threadIdx.x] : 0u;
+            uint32_t xs = v;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t y = __shfl_up(xs, off, 64);
+                if (lane >= off) xs += y;
+            }
+            if (threadIdx.x < R * NW) cnt[threadIdx.x] = xs - v;
+            if (threadIdx.x == 63)
+                tile_base = xs ? atomicAdd(cursor, (unsigned long long)xs) : 0ull;
+        }
+        __syncthreads();
+        const uint64_t ob = tile_base;
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            if (!((hit >> k) & 1u)) continue;
+            const int64_t r = base + k * kXpThreads + threadIdx.x;
+            const uint64_t pos = ob + cnt[k * NW + wave] + (uint32_t)__popcll(bal[k] & lt);
+            out_pay[pos] = pay[k];
+#pragma unroll
+            for (int j = 0; j < NC; ++j) lc.dst[j][pos] = __builtin_nontemporal_load(lc.src[j] + r);
+        }
+        __syncthreads();
+    }
+}
+
+template <int NC>
+static void xp_probe_launch(int grid, const uint64_t* pkey, const TakeCols& lc, const int64_t* xr, const XpTable& t,
+                            uint64_t* out_pay, unsigned long long* cursor, hipStream_t s) {
+    xp_probe_kernel<NC><<<grid, kXpThreads, 0, s>>>(pkey, lc, xr, t, out_pay, cursor);
+}
+
+__global__ void xp_xcd_ranges_kernel(const uint64_t* __restrict__ off, int S, int G, int64_t* __restrict__ xr) {
+    const int x = threadIdx.x;
+    if (x <= 8) xr[x] = (int64_t)off[(int64_t)x * S * G];
+}
+
+static int64_t env_i64(const char* name, int64_t dflt) {
+    const char* e = getenv(name);
+    return e ? atoll(e) : dflt;
+}
+
+// The xp join.  Returns 1 (nothing allocated, outputs untouched) when the
+// build side does not qualify (duplicate or INT64_MIN keys, a full
+// sub-table): the caller takes the general paths.
+static int xp_join(const plgpu_column* lk, const plgpu_column* rk, const plgpu_column* lcols, int32_t nleft,
+                   const plgpu_column& pay, plgpu_column* out_left, plgpu_column* out_right, int64_t* out_len,
+                   hipStream_t s) {
+    const int64_t np = lk->length, nb = rk->length;
+    const int cbits = (int)env_i64("PLGPU_XP_CBITS", 16);
+    const double load = 0.4;
+    const int64_t per_sub = std::max<int64_t>(1, (int64_t)((double)(int64_t(1) << cbits) * load));
+    const int S = (int)std::max<int64_t>(1, (nb + 8 * per_sub - 1) / (8 * per_sub));
+    const int P = 8 * S;
+    if (P > kXpMaxParts) return 1;
+    XpTable t;
+    t.P = P;
+    t.cbits = cbits;
+    t.cells = nullptr;
+    const int64_t ncells = (int64_t)P << cbits;
+    unsigned long long* st = nullptr;
+    int rc = dev_alloc((void**)&t.cells, (size_t)ncells * 16, s);
+    if (!rc) rc = dev_alloc((void**)&st, 8 * (8 + 16 * 8), s);
+    if (rc) {
+        dev_free(t.cells, s);
+        return rc;
+    }
+    unsigned long long hst[4] = {0, 0, 0, 0};
+    hipError_t e = hipMemsetAsync(st, 0, 8 * 8, s);
+    if (e == hipSuccess) {
+        xp_init_kernel<<<(int)std::min<int64_t>((ncells + 255) / 256, 8192), 256, 0, s>>>(t, ncells);
+        xp_build_kernel<<<(int)std::min<int64_t>((nb + 255) / 256, 8192), 256, 0, s>>>(dev_col(*rk), nb, t,
+                                                                                       dev_col(pay), st);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(hst, st, sizeof hst, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) rc = hip_fail(e, "xp build");
+    if (rc || hst[0] || hst[1] || hst[2]) {
+        dev_free(st, s);
+        dev_free(t.cells, s);
+        return rc ? rc : 1;
+    }
+    // probe side: count, scan, XCD ranges
+    const int G = num_cus_jn() * 4;
+    const int64_t ncnt = (int64_t)P * G;
+    uint32_t* cnt = nullptr;
+    uint64_t* off = nullptr;
+    uint64_t* part = nullptr;
+    int64_t* xr = nullptr;
+    rc = dev_alloc((void**)&cnt, ncnt * 4, s);
+    if (!rc) rc = dev_alloc((void**)&off, (ncnt + 1) * 8, s);
+    if (!rc) rc = dev_alloc((void**)&part, ((ncnt + kScanChunk - 1) / kScanChunk + 1) * 8, s);
+    if (!rc) rc = dev_alloc((void**)&xr, 16 * 8, s);
+    const uint64_t* kp = (const uint64_t*)lk->values + lk->offset;
+    int64_t rows = 0;
+    if (!rc) {
+        xp_count_kernel<<<G, kXpThreads, 0, s>>>(kp, lk->validity, lk->offset, np, P, cnt);
+        e = hipGetLastError();
+        if (e == hipSuccess) e = scan_exclusive<uint32_t>(cnt, ncnt, off, part, s);
+        if (e == hipSuccess) {
+            xp_xcd_ranges_kernel<<<1, 64, 0, s>>>(off, S, G, xr);
+            e = hipGetLastError();
+        }
+        uint64_t total = 0;
+        if (e == hipSuccess) e = hipMemcpyAsync(&total, off + ncnt, 8, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) rc = hip_fail(e, "xp count");
+        rows = (int64_t)total;
+    }
+    // partitioned key + the left columns that are not the key itself
+    XpCols xc;
+    std::memset(&xc, 0, sizeof xc);
+    int src_of[PLGPU_MAX_COLS];
+    xc.src[0] = kp;
+    xc.n = 1;
+    for (int i = 0; i < nleft; ++i) {
+        const plgpu_column& c = lcols[i];
+        const bool is_key = c.values == lk->values && c.offset == lk->offset && c.validity == nullptr;
+        if (is_key) {
+            src_of[i] = 0;
+            continue;
+        }
+        src_of[i] = xc.n;
+        xc.src[xc.n++] = (const uint64_t*)c.values + c.offset;
+    }
+    uint64_t* pbuf = nullptr;
+    if (!rc) rc = dev_alloc((void**)&pbuf, (size_t)std::max<int64_t>(rows, 1) * 8 * xc.n, s);
+    for (int j = 0; j < xc.n && !rc; ++j) xc.dst[j] = pbuf + (size_t)j * std::max<int64_t>(rows, 1);
+    if (!rc && rows > 0) {
+        xp_scatter_kernel<<<G, kXpThreads, 0, s>>>(lk->validity, lk->offset, np, P, off, xc);
+        e = hipGetLastError();
+        if (e != hipSuccess) rc = hip_fail(e, "xp scatter");
+    }
+    dev_free(cnt, s);
+    dev_free(part, s);
+    dev_free(off, s);
+    // outputs at capacity `rows` (every probe row matches at most once);
+    // their length is set to the hit count
+    for (int i = 0; i < nleft && !rc; ++i) rc = make_owned_column(&out_left[i], lcols[i].dtype, rows, false, s);
+    if (!rc) rc = make_owned_column(&out_right[0], pay.dtype, rows, false, s);
+    unsigned long long hits = 0;
+    if (!rc && rows > 0) {
+        (void)hipMemsetAsync(st, 0, 8 * (8 + 16 * 8), s);
+        TakeCols lc;
+        std::memset(&lc, 0, sizeof lc);
+        lc.n = nleft;
+        for (int i = 0; i < nleft; ++i) {
+            lc.src[i] = xc.dst[src_of[i]];
+            lc.dst[i] = (uint64_t*)out_left[i].values;
+        }
+        const int grid = num_cus_jn() * (int)env_i64("PLGPU_XP_WG_PER_CU", 8);
+        uint64_t* ov = (uint64_t*)out_right[0].values;
+        switch (nleft) {
+        case 0: xp_probe_launch<0>(grid, xc.dst[0], lc, xr, t, ov, st, s); break;
+        case 1: xp_probe_launch<1>(grid, xc.dst[0], lc, xr, t, ov, st, s); break;
+        case 2: xp_probe_launch<2>(grid, xc.dst[0], lc, xr, t, ov, st, s); break;
+        case 3: xp_probe_launch<3>(grid, xc.dst[0], lc, xr, t, ov, st, s); break;
+        case 4: xp_probe_launch<4>(grid, xc.dst[0], lc, xr, t, ov, st, s); break;
+        case 5: xp_probe_launch<5>(grid, xc.dst[0], lc, xr, t, ov, st, s); break;
+        case 6: xp_probe_launch<6>(grid, xc.dst[0], lc, xr, t, ov, st, s); break;
+        case 7: xp_probe_launch<7>(grid, xc.dst[0], lc, xr, t, ov, st, s); break;
+        default: xp_probe_launch<8>(grid, xc.dst[0], lc, xr, t, ov, st, s); break;
+        }
+        e = hipGetLastError();
+        if (e == hipSuccess) e = hipMemcpyAsync(&hits, st, 8, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) rc = hip_fail(e, "xp probe");
+    }
+    if (!rc && hits >= 0xFFFFFFFFull) rc = fail(PLGPU_ERR_CAPACITY, "join output exceeds the u32 index space");
+    dev_free(pbuf, s);
+    dev_free(xr, s);
+    dev_free(st, s);
+    dev_free(t.cells, s);
+    if (rc) {
+        for (int i = 0; i < nleft; ++i) plgpu_column_release(&out_left[i]);
+        plgpu_column_release(&out_right[0]);
+        return rc;
+    }
+    for (int i = 0; i < nleft; ++i) out_left[i].length = (int64_t)hits;
+    out_right[0].length = (int64_t)hits;
+    *out_len = (int64_t)hits;
+    return PLGPU_OK;
+}
+
 PLGPU_API int plgpu_join_inner_take(const plgpu_column* left_key, const plgpu_column* right_key,
                                     const plgpu_column* left_cols, int32_t nleft, const plgpu_column* right_cols,
                                     int32_t nright, int32_t nulls_equal, int32_t maintain_order, int32_t validate,
@@ -1855,6 +2338,21 @@ PLGPU_API int plgpu_join_inner_take(const plgpu_column* left_key, const plgpu_co
                            (validate == PLGPU_JOIN_VALIDATE_M_M || validate == PLGPU_JOIN_VALIDATE_M_1) &&
                            left_key->length >= (int64_t(1) << 16) &&
                            (right_key->length <= left_key->length || maintain_order == PLGPU_JOIN_ORDER_LEFT);
+    // XCD-partitioned probe (opt-in, PLGPU_XP=1: measured slower, DESIGN.md
+    // "XCD-partitioned probe"): order-free output, 8-byte keys, every left
+    // column null-free 8-byte, nulls not joined, large enough to pay for the
+    // partitioning (PLGPU_XP_MIN_PROBE / _MIN_BUILD rows)
+    bool xp_ok = inline_ok && maintain_order == PLGPU_JOIN_ORDER_NONE && !neq &&
+                 dtype_bytes(left_key->dtype) == 8 && left_key->dtype != PLGPU_F64 &&
+                 left_key->dtype == right_key->dtype && getenv("PLGPU_XP") != nullptr &&
+                 left_key->length >= env_i64("PLGPU_XP_MIN_PROBE", int64_t(1) << 24) &&
+                 right_key->length >= env_i64("PLGPU_XP_MIN_BUILD", int64_t(1) << 18);
+    for (int i = 0; i < nleft && xp_ok; ++i) xp_ok = fused8(left_cols[i]);
+    if (xp_ok) {
+        rc = xp_join(left_key, right_key, left_cols, nleft, right_cols[0], out_left, out_right, out_len, s);
+        if (rc <= 0) return rc;  // done, or an error; 1: fall through
+        rc = PLGPU_OK;
+    }
     JnBuilt b;
     bool use_inline = false;
     if (inline_ok) {
