@@ -1,5 +1,7 @@
 # A/B of non-temporal loads / stores in the rolling wave kernel and the
-# filter scatter (env switches), interleaved, one JSON line per run.
+# filter scatter.  PLGPU_RL_NT / PLGPU_FILTER_NT were temporary switches of
+# the build measured in profiles/r02_nt_ab_rolling_filter.log (no gain, so
+# they were removed again); kept as the record of that run.
 set -o pipefail
 for rep in 1 2; do
   for nt in 0 1 2 3; do
