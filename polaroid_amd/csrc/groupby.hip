@@ -1276,7 +1276,12 @@ __global__ __launch_bounds__(kPlanThreads) void gb_plan_kernel(GbParams p, uint6
                 }
             }
             if (!fresh) continue;
-            // new to this workgroup: into the global set
+            // new to this workgroup: into the global set, unless the count
+            // already reached the saturation mark (then only the HLL pass
+            // can size the table, and more inserts would only probe a full set)
+            if (__hip_atomic_load(&p.status[ST_DISTINCT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
+                (uint64_t)kPlanSetSlots / 2)
+                continue;
             const unsigned long long w = (unsigned long long)(k ^ kEmptyKey);
             for (int q = 0; q < 64; ++q) {
                 const uint32_t s = (h + q) & (kPlanSetSlots - 1);
