@@ -846,13 +846,17 @@ __device__ __forceinline__ u64x2_t ld16(const uint64_t* p) {
     return *reinterpret_cast<const u64x2_t*>(p);
 }
 
+// rbase: first row of tile 0 (even); rmax >= 0: row pairs beyond it are
+// clamped to it (the partitioned buffers end a pair after the last row).
 template <int NACC, int PRED, int ROWS, bool NT = false>
-__device__ __forceinline__ void fast_load(const GbParams& p, int64_t t, FastTile<NACC, ROWS>& x) {
+__device__ __forceinline__ void fast_load(const GbParams& p, int64_t t, FastTile<NACC, ROWS>& x, int64_t rbase = 0,
+                                          int64_t rmax = -1) {
     const int T = blockDim.x;
     const uint64_t* kp = (const uint64_t*)p.key.values + p.key.offset;
 #pragma unroll
     for (int q = 0; q < ROWS / 2; ++q) {
-        const int64_t r = fast_row(t, T, ROWS, 2 * q);
+        int64_t r = rbase + fast_row(t, T, ROWS, 2 * q);
+        if (rmax >= 0) r = r < rmax ? r : rmax;
         const u64x2_t a = ld16<NT>(kp + r);
         x.key[2 * q] = a.x;
         x.key[2 * q + 1] = a.y;
@@ -887,7 +891,12 @@ __device__ __forceinline__ void fast_load(const GbParams& p, int64_t t, FastTile
 // prefetch, 11 default-policy (not non-temporal) loads.
 // WPE: minimum waves per SIMD the register allocation must allow (1 = no
 // constraint); 6 caps VGPRs at 80, i.e. three 512-thread workgroups per CU.
-template <int NACC, int PRED, bool SUMONLY, int ROWS, int LIMBS = 3, int ABL = 0, int WPE = 1>
+// PART: the workgroups aggregate the partition buffers of the many-groups
+// path (gb_partition): workgroup b takes its share of partition
+// b / part_blocks (rows [part_range[q], part_range[q + 1]), already
+// selected, so PRED is 0) with an LDS table of lcap slots for that
+// partition's groups.
+template <int NACC, int PRED, bool SUMONLY, int ROWS, int LIMBS = 3, int ABL = 0, int WPE = 1, bool PART = false>
 __global__ __launch_bounds__(kGbThreads) __attribute__((amdgpu_waves_per_eu(WPE))) void gb_fast_kernel(
     GbParams p, DevProgram prog) {
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
@@ -918,13 +927,24 @@ __global__ __launch_bounds__(kGbThreads) __attribute__((amdgpu_waves_per_eu(WPE)
     // the tile stream is read once: non-temporal loads (6.60 vs 6.84 ms at
     // 1e9 rows, tools/ablate.py; ablation 11 = default-policy loads)
     constexpr bool NTL = ABL != 11;
-    const int64_t ntiles = p.n_full / ((int64_t)T * ROWS);
+    int64_t ntiles = p.n_full / ((int64_t)T * ROWS);
+    int64_t t = blockIdx.x, tstep = gridDim.x;
+    int64_t rbase = 0, rlo = 0, rhi = 0, rmax = -1;
+    if (PART) {
+        const int q = blockIdx.x / p.part_blocks;
+        rlo = (int64_t)p.part_range[q];
+        rhi = (int64_t)p.part_range[q + 1];
+        rbase = rlo & ~int64_t(1);
+        rmax = p.n & ~int64_t(1);
+        ntiles = (rhi - rbase + (int64_t)T * ROWS - 1) / ((int64_t)T * ROWS);
+        t = blockIdx.x % p.part_blocks;
+        tstep = p.part_blocks;
+    }
     constexpr uint32_t VM = (1u << NACC) - 1u;
-    int64_t t = blockIdx.x;
     FastTile<NACC, ROWS> cur;
-    if (ABL != 5 && t < ntiles) fast_load<NACC, PRED, ROWS, NTL>(p, t, cur);
-    for (; t < ntiles; t += gridDim.x) {
-        if (ABL == 5) fast_load<NACC, PRED, ROWS>(p, t, cur);  // ablation: no prefetch
+    if (ABL != 5 && t < ntiles) fast_load<NACC, PRED, ROWS, NTL>(p, t, cur, rbase, rmax);
+    for (; t < ntiles; t += tstep) {
+        if (ABL == 5) fast_load<NACC, PRED, ROWS>(p, t, cur, rbase, rmax);  // ablation: no prefetch
         // ---- predicate + batched LDS probes of the tile's rows
         int slot[ROWS];
         uint64_t probe[ROWS];
@@ -939,6 +959,10 @@ __global__ __launch_bounds__(kGbThreads) __attribute__((amdgpu_waves_per_eu(WPE)
                     if (a == p.pred_acc) x = cur.v[a][j];
                 sel = simple_pred(prog.simple_isf, prog.simple_op, x, prog.simple_imm);
             }
+            if (PART) {
+                const int64_t r = rbase + fast_row(t, T, ROWS, j);
+                sel = r >= rlo && r < rhi;
+            }
             slot[j] = sel ? (cur.key[j] == kEmptyKey ? p.lcap + 1 : kGlobalKey) : kNotSelected;
             h[j] = hash_slot(cur.key[j], p.lbits);
             probe[j] = lds_load(&lds[h[j]]);
@@ -948,12 +972,12 @@ __global__ __launch_bounds__(kGbThreads) __attribute__((amdgpu_waves_per_eu(WPE)
             if (slot[j] == kGlobalKey && probe[j] == cur.key[j]) slot[j] = (int)h[j];
         // ---- next tile's loads go out before this tile's atomics
         FastTile<NACC, ROWS> nxt;
-        const int64_t tn = t + gridDim.x;
-        if (ABL != 5 && tn < ntiles) fast_load<NACC, PRED, ROWS, NTL>(p, tn, nxt);
+        const int64_t tn = t + tstep;
+        if (ABL != 5 && tn < ntiles) fast_load<NACC, PRED, ROWS, NTL>(p, tn, nxt, rbase, rmax);
         // ---- apply rows one at a time (rolled; arrays shift statically)
 #pragma unroll 1
         for (int j = 0; j < ROWS; ++j) {
-            const int64_t r = fast_row(t, T, ROWS, j);
+            const int64_t r = rbase + fast_row(t, T, ROWS, j);
             int s = slot[0];
             if (s != kNotSelected) {
                 ++d.nsel;
@@ -2015,16 +2039,37 @@ static int gb_prepare(GbRun& R, const plgpu_column* key, const plgpu_column* col
 // row is a new group.
 constexpr int kHllBits = 12;
 
+__device__ __forceinline__ void hll_add(uint32_t* r, uint64_t k) {
+    const uint64_t h = mk_fmix(k ^ 0x5851F42D4C957F2Dull);
+    const uint32_t j = (uint32_t)(h >> (64 - kHllBits));
+    const uint32_t rho = (uint32_t)__clzll((h << kHllBits) | (1ull << (kHllBits - 1))) + 1;
+    if (rho > r[j]) atomicMax(&r[j], rho);
+}
+
 __global__ __launch_bounds__(256) void gb_hll_kernel(DevCol key, int64_t n, uint32_t* __restrict__ regs) {
     __shared__ uint32_t r[1 << kHllBits];
     for (int i = threadIdx.x; i < (1 << kHllBits); i += blockDim.x) r[i] = 0;
     __syncthreads();
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        if (!dev_valid(key, i)) continue;
-        const uint64_t h = mk_fmix(dev_load(key, i) ^ 0x5851F42D4C957F2Dull);
-        const uint32_t j = (uint32_t)(h >> (64 - kHllBits));
-        const uint32_t rho = (uint32_t)__clzll((h << kHllBits) | (1ull << (kHllBits - 1))) + 1;
-        if (rho > r[j]) atomicMax(&r[j], rho);
+    const int64_t T = (int64_t)gridDim.x * blockDim.x;
+    int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (key.validity == nullptr && dtype_bytes(key.dtype) == 8) {
+        // null-free 8-byte keys: 8 branch-free streamed loads in flight
+        const uint64_t* kp = (const uint64_t*)key.values + key.offset;
+        constexpr int U = 8;
+        for (; i0 < n; i0 += T * U) {
+            uint64_t k[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t i = i0 + u * T;
+                k[u] = __builtin_nontemporal_load(kp + (i < n ? i : n - 1));
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (i0 + u * T < n) hll_add(r, k[u]);
+        }
+    } else {
+        for (int64_t i = i0; i < n; i += T)
+            if (dev_valid(key, i)) hll_add(r, dev_load(key, i));
     }
     __syncthreads();
     for (int i = threadIdx.x; i < (1 << kHllBits); i += blockDim.x)
@@ -2136,9 +2181,15 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
         // LDS table of the partition workgroups: two per CU, or one when
         // 2^kPartMaxBits partitions of the smaller table are not enough
         const int64_t want = R.est_groups + (R.est_groups >> 3);
+        // sum-only on the 2-limb window: the fast kernel's slim table
+        // (2 + 3 nacc fields); the full layout must still fit one workgroup
+        // per CU for a 3-limb rerun through the generic kernel
+        const int fields = (pl.sum_only && pl.limbs == 2) ? 2 + 3 * p.nacc : p.nfields;
         for (size_t budget : {(size_t)80 * 1024, (size_t)160 * 1024}) {
             int lb = 13;
-            while (lb > 6 && (size_t)p.nfields * ((1u << lb) + 2) * 8 > budget) --lb;
+            while (lb > 6 && ((size_t)fields * ((1u << lb) + 2) * 8 > budget ||
+                              (size_t)p.nfields * ((1u << lb) + 2) * 8 > (size_t)160 * 1024))
+                --lb;
             const int64_t per = (int64_t(1) << lb) / 2;  // groups per partition at load 1/2
             int pb = 0;
             while (pb < kPartMaxBits && want > (per << pb)) ++pb;
@@ -2197,7 +2248,8 @@ static int gb_partition(GbRun& R) {
     if (rc) return rc;
     uint64_t maxpart = 0;
     for (int q = 0; q < P; ++q) maxpart = std::max<uint64_t>(maxpart, hr[q + 1] - hr[q]);
-    const int64_t rows = (int64_t)std::max<uint64_t>(hr[P], 2) + 2;
+    // even, so every column's buffer starts 16-byte aligned (pair loads)
+    const int64_t rows = ((int64_t)std::max<uint64_t>(hr[P], 2) + 3) & ~int64_t(1);
     R.part_rows_total = (int64_t)hr[P];
     const bool want_rows = p.f_first >= 0 || p.f_last >= 0;
     const size_t words = (size_t)rows * (1 + p.nacc) + (want_rows ? ((size_t)rows + 1) / 2 : 0);
@@ -2219,6 +2271,21 @@ static int gb_partition(GbRun& R) {
     while ((int64_t)maxpart > (int64_t)nb * (kMaxRowsPerWg / 2)) nb *= 2;
     R.part_blocks = nb;
     return PLGPU_OK;
+}
+
+template <int NACC>
+static hipError_t launch_part_fast(const Plan& pp, int grid, hipStream_t s) {
+    const void* kern = (const void*)gb_fast_kernel<NACC, 0, true, 2, 2, 0, 1, true>;
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr_set = true;
+    }
+    const size_t lds = (size_t)(2 + 3 * NACC) * (pp.p.lcap + 2) * 8;
+    DevProgram none;
+    std::memset(&none, 0, sizeof none);
+    gb_fast_kernel<NACC, 0, true, 2, 2, 0, 1, true><<<grid, kGbThreads, lds, s>>>(pp.p, none);
+    return hipGetLastError();
 }
 
 // The main pass over the partition buffers.
@@ -2244,6 +2311,19 @@ static hipError_t launch_partitioned(const GbRun& R) {
     q.part_blocks = R.part_blocks;
     q.lbits = R.part_lbits;
     q.lcap = 1 << R.part_lbits;
+    if (pp.sum_only && pp.limbs == 2 && p.nacc >= 1 && p.nacc <= 6) {
+        // sum-only accs on the 2-limb window: the fast kernel's slim LDS
+        // layout over the partition buffers
+        const int grid = (1 << R.pbits) * R.part_blocks;
+        switch (p.nacc) {
+        case 1: return launch_part_fast<1>(pp, grid, R.s);
+        case 2: return launch_part_fast<2>(pp, grid, R.s);
+        case 3: return launch_part_fast<3>(pp, grid, R.s);
+        case 4: return launch_part_fast<4>(pp, grid, R.s);
+        case 5: return launch_part_fast<5>(pp, grid, R.s);
+        default: return launch_part_fast<6>(pp, grid, R.s);
+        }
+    }
     const size_t lds = (size_t)p.nfields * (q.lcap + 2) * 8;
     static bool attr_set = false;
     if (!attr_set) {
@@ -2408,7 +2488,7 @@ static int gb_main(GbRun& R, bool auto_refit, bool* refit, int32_t* hint) {
         for (int a = 0; a < p.nacc; ++a)
             if ((p.acc[a].flags & (A_FSUM | A_FSUMCAST)) && ((R.st[ST_FXFLAGS] >> (2 * a)) & 3u)) flagged |= 1u << a;
         flagged &= ~R.wide;
-        if (flagged && pl.limbs == 2 && p.n_full > 0 && pl.sum_only) {
+        if (flagged && pl.limbs == 2 && (p.n_full > 0 || R.part) && pl.sum_only) {
             // a value fell below the 2-limb window (or out of the top): redo
             // the pass with the full 3-limb window before any refit
             pl.limbs = 3;
@@ -2472,7 +2552,7 @@ static void gb_fill_info(const GbRun& R, plgpu_groupby_info* info) {
     info->table_capacity = p.gcap;
     info->main_kernel_ms = R.ms;
     info->path = R.part ? 3 : (p.n_full > 0 ? (R.pl.sum_only ? 2 : 1) : 0);
-    info->sum_limbs = p.n_full > 0 && R.pl.sum_only ? R.pl.limbs : 3;
+    info->sum_limbs = (p.n_full > 0 || R.part) && R.pl.sum_only ? R.pl.limbs : 3;
     for (int a = 0; a < p.nacc; ++a)
         if (((R.st[ST_FXFLAGS] >> (2 * a)) & 2u) && !((R.wide >> a) & 1u)) info->sum_inexact |= 1 << a;
 }

@@ -348,6 +348,35 @@ def test_group_by_partitioned_vs_oracle(gpu, card, pname, maintain_order):
     assert info["path"] == 3, info
 
 
+@pytest.mark.parametrize("card", [5000, 60000, 300000])
+@pytest.mark.parametrize("data", ["prices", "specials", "tiny"])
+def test_group_by_partitioned_sum_only(gpu, card, data):
+    """Many groups with f64 sums / means only: the partition buffers are
+    aggregated by the fast kernel's slim 2-limb table (gb_fast_kernel PART);
+    a value below the 2-limb window ("tiny") reruns with 3 limbs."""
+    rng = np.random.default_rng(card + len(data))
+    n = 1_500_001
+    # magnitudes within a few binades (the 2-limb window's condition)
+    a = rng.uniform(10, 500, n)
+    d = rng.uniform(1, 5, n) * rng.choice([-1.0, 1.0], n)
+    if data == "specials":
+        a[rng.random(n) < 0.001] = np.nan
+        a[rng.random(n) < 0.0005] = np.inf
+        d[rng.random(n) < 0.001] = -0.0
+    if data == "tiny":
+        # three rows the plan's 65,536-row sample almost surely misses
+        d[rng.choice(n, 3, replace=False)] = 1e-30
+    cols = {"a": (a, None), "d": (d, None)}
+    key = rng.integers(0, card, n).astype(np.int64) * 7919 - 3
+    key[rng.random(n) < 0.001] = np.iinfo(np.int64).min
+    aggs = [("sum", "a"), ("sum", "d"), ("mean", "a")]
+    info = {}
+    mk, names, prog = PREDICATES["simple_f64"]
+    _check_group_by(cols, key, None, aggs, mk(), prog, names, False, info)
+    assert info["path"] == 3, info
+    assert info["sum_limbs"] == (3 if data == "tiny" else 2), info
+
+
 def test_group_by_special_keys_and_i32_key(gpu):
     rng = np.random.default_rng(5)
     n = 20000

@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--only", default="groupby,groupby_hc,join,sort")
+    ap.add_argument("--values", default="unit", help="unit: v0, v1 uniform on [0, 1); prices: uniform on [10, 500)")
     args = ap.parse_args()
     import torch
 
@@ -58,12 +59,14 @@ def main():
         return torch.randint(lo, hi, (m,), device=dev, generator=g, dtype=torch.int64)
 
     def floats(m):
-        return torch.rand(m, device=dev, generator=g, dtype=torch.float64)
+        x = torch.rand(m, device=dev, generator=g, dtype=torch.float64)
+        return x * 490 + 10 if args.values == "prices" else x
 
+    thr = 255.0 if args.values == "prices" else 0.5
     if "groupby" in only:
         df = pl.DataFrame([pl.Series.from_torch("sym", ints(0, 100, n)), pl.Series.from_torch("day", ints(0, 250, n)),
                            pl.Series.from_torch("v0", floats(n)), pl.Series.from_torch("v1", floats(n))])
-        q = (df.lazy().filter(pl.col("v0") > 0.5).group_by("sym", "day")
+        q = (df.lazy().filter(pl.col("v0") > thr).group_by("sym", "day")
              .agg(pl.col("v0").sum(), pl.col("v1").sum()))
         info = {}
         t, out = _timed(lambda: q.collect(info=info), args.steps, args.warmup)
@@ -77,7 +80,7 @@ def main():
         card = 100_000
         df = pl.DataFrame([pl.Series.from_torch("id", ints(0, card, n)), pl.Series.from_torch("v0", floats(n)),
                            pl.Series.from_torch("v1", floats(n))])
-        q = df.lazy().filter(pl.col("v0") > 0.5).group_by("id").agg(pl.col("v0").sum(), pl.col("v1").sum())
+        q = df.lazy().filter(pl.col("v0") > thr).group_by("id").agg(pl.col("v0").sum(), pl.col("v1").sum())
         info = {}
         t, out = _timed(lambda: q.collect(info=info), args.steps, args.warmup)
         print(json.dumps({"workload": f"filter + group_by(id: {card} groups).agg(2 x f64 sum)", "rows": n,
