@@ -1,4 +1,7 @@
+# PMC passes (L2 hit / miss, FETCH_SIZE, SQ) over tools/bench_join.py with the
+# opt-in XCD-partitioned join probe.
 set -o pipefail
+export PLGPU_XP=1  # the opt-in XCD-partitioned probe
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 OUT=$R/gpurun_out/pmc_xp
