@@ -586,7 +586,7 @@ __global__ __launch_bounds__(kGbThreads) void gb_kernel(GbParams p, DevProgram p
 // multiplicative hash).  Order inside a partition is irrelevant: every
 // aggregate is order-independent (exact sums, min / max, counts, min row).
 constexpr int kPartMaxBits = 10;
-constexpr int kPartThreads = 256;
+constexpr int kPartThreads = 512;
 
 __device__ __forceinline__ uint32_t part_of(uint64_t key, int pbits) {
     return pbits == 0 ? 0u : (uint32_t)(mk_fmix(key ^ 0x2545F4914F6CDD1Dull) >> (64 - pbits));
@@ -607,7 +607,7 @@ __device__ __forceinline__ bool part_sel(const GbParams& p, const DevProgram& pr
 // cnt[q * G + b] gives every (partition, chunk) run its place and pass 2
 // needs no global atomics.
 constexpr int kPartPer = 8;
-constexpr int64_t kPartTile = (int64_t)kPartThreads * kPartPer;  // 2048 rows
+constexpr int64_t kPartTile = (int64_t)kPartThreads * kPartPer;  // 4096 rows
 constexpr int kPartRegAcc = 3;
 
 __device__ __forceinline__ void part_chunk(int64_t n, int64_t& lo, int64_t& hi) {
