@@ -19,7 +19,7 @@ import polaroid_amd as pl  # noqa: E402
 
 n = int(float(sys.argv[1])) if len(sys.argv) > 1 else int(1e9)
 modes = sys.argv[2:] or ["base"]
-KNOBS = ("PLGPU_ABLATE", "PLGPU_NO_FAST", "PLGPU_NO_SUMONLY", "PLGPU_OCC_GRID", "PLGPU_NO_LIMB2")
+KNOBS = ("PLGPU_ABLATE", "PLGPU_NO_FAST", "PLGPU_NO_SUMONLY", "PLGPU_OCC_GRID", "PLGPU_NO_LIMB2", "PLGPU_FAST_THREADS")
 sym, cols = bench.make_data(torch, n, 100, 1234)
 df = pl.DataFrame([pl.Series.from_torch("symbol", sym)] + [pl.Series.from_torch(k, v) for k, v in cols.items()])
 q = df.lazy().filter(pl.col("close") > bench.THRESHOLD).group_by("symbol").agg(
