@@ -28,9 +28,10 @@
 
 namespace plgpu {
 
-constexpr int kSrtThreads = 256;
+constexpr int kSrtThreads = 256;                  // upsweep / stats workgroups
 constexpr int kSrtPer = 16;
 constexpr int kSrtTile = kSrtThreads * kSrtPer;  // 4096 codes per tile
+constexpr int kSrtDThreads = 512;                 // downsweep: 8 waves x 8 rows of 64 per tile
 
 __device__ __forceinline__ uint64_t sort_code(const DevCol& c, int64_t r, bool descending) {
     uint64_t b = dev_load(c, r);
@@ -139,6 +140,87 @@ __global__ __launch_bounds__(256) void srt_bits_kernel(const uint64_t* __restric
     }
 }
 
+// Bijective XCD-aware remap of a 1-D grid (cdna_hip_programming.md T1):
+// blocks that share an XCD (same blockIdx % 8) take consecutive tiles, so
+// the digit-major count words and the digit runs that neighbouring tiles
+// write into the same lines are combined in one L2 instead of being written
+// back as partial lines from several.
+__device__ __forceinline__ int64_t xcd_tile(int64_t bid, int64_t nwg) {
+    const int64_t q = nwg / 8, r = nwg % 8, x = bid % 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+}
+
+// Null-free column, first read: each 4096-row tile writes its codes, its
+// OR / AND of them (reduced over the tiles by srt_tbits_kernel: constant
+// bytes) and its byte-0 digit counts, digit-major like the upsweep's -- the
+// first pass's upsweep whenever byte 0 varies.  Replaces codes + bits +
+// first upsweep (three reads of the column) by one.
+__global__ __launch_bounds__(kSrtThreads) void srt_codes_stats_kernel(DevCol c, int64_t n, bool descending,
+                                                                      int64_t ntiles, uint64_t* __restrict__ keys,
+                                                                      uint32_t* __restrict__ cnt,
+                                                                      uint64_t* __restrict__ tbits) {
+    __shared__ uint32_t h[256];
+    __shared__ uint64_t wo[kSrtThreads / 64], wa[kSrtThreads / 64];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const int64_t tile = xcd_tile(blockIdx.x, ntiles);
+    const int64_t base = tile * kSrtTile;
+    uint64_t o = 0, a = ~0ull;
+    uint64_t k[kSrtPer];
+#pragma unroll
+    for (int j = 0; j < kSrtPer; ++j) {
+        const int64_t i = base + j * kSrtThreads + threadIdx.x;
+        k[j] = i < n ? sort_code(c, i, descending) : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < kSrtPer; ++j) {
+        const int64_t i = base + j * kSrtThreads + threadIdx.x;
+        if (i < n) {
+            keys[i] = k[j];
+            o |= k[j];
+            a &= k[j];
+            atomicAdd(&h[k[j] & 0xFF], 1u);
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        o |= __shfl_xor(o, off, 64);
+        a &= __shfl_xor(a, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        wo[threadIdx.x >> 6] = o;
+        wa[threadIdx.x >> 6] = a;
+    }
+    __syncthreads();
+    cnt[(int64_t)threadIdx.x * ntiles + tile] = h[threadIdx.x];
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kSrtThreads / 64; ++w) {
+            o |= wo[w];
+            a &= wa[w];
+        }
+        tbits[2 * tile] = o;
+        tbits[2 * tile + 1] = a;
+    }
+}
+
+__global__ __launch_bounds__(256) void srt_tbits_kernel(const uint64_t* __restrict__ tbits, int64_t nt,
+                                                        unsigned long long* __restrict__ bits) {
+    uint64_t o = 0, a = ~0ull;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nt; i += (int64_t)gridDim.x * blockDim.x) {
+        o |= tbits[2 * i];
+        a &= tbits[2 * i + 1];
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        o |= __shfl_xor(o, off, 64);
+        a &= __shfl_xor(a, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicOr(&bits[0], (unsigned long long)o);
+        atomicAnd(&bits[1], (unsigned long long)a);
+    }
+}
+
 // Representations of the (code, row id) stream between passes:
 //   SEP    - codes u64 + row ids u32 in two buffers (12 B per row);
 //   PACKED - one u64 word (remaining code bits << 32 | row id) once the
@@ -156,14 +238,15 @@ __global__ __launch_bounds__(kSrtThreads) void srt_upsweep_kernel(const uint64_t
     __shared__ uint32_t h[256];
     h[threadIdx.x] = 0;
     __syncthreads();
-    const int64_t base = (int64_t)blockIdx.x * kSrtTile;
+    const int64_t tile = xcd_tile(blockIdx.x, ntiles);
+    const int64_t base = tile * kSrtTile;
 #pragma unroll
     for (int k = 0; k < kSrtPer; ++k) {
         const int64_t i = base + k * kSrtThreads + threadIdx.x;
         if (i < n) atomicAdd(&h[(__builtin_nontemporal_load(keys + i) >> shift) & 0xFF], 1u);
     }
     __syncthreads();
-    cnt[(int64_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
+    cnt[(int64_t)threadIdx.x * ntiles + tile] = h[threadIdx.x];
 }
 
 // Downsweep: stable scatter of one tile by the digit at `shift` (of the
@@ -173,16 +256,16 @@ __global__ __launch_bounds__(kSrtThreads) void srt_upsweep_kernel(const uint64_t
 // counts into local positions; the tile is staged in LDS in digit order and
 // written out in runs.  IN_P: input is PACKED.  OUT: SrtOut; a SEP -> PACK
 // transition keeps (code >> cons) & kmask as the remaining code.
-template <bool IN_P, int OUT>
-__global__ __launch_bounds__(kSrtThreads) void srt_downsweep_kernel(const uint64_t* __restrict__ keys_in,
+template <bool IN_P, int OUT, int TH, int WPE>
+__global__ __launch_bounds__(TH) __attribute__((amdgpu_waves_per_eu(OUT == SRT_SEP ? 1 : WPE))) void srt_downsweep_kernel(const uint64_t* __restrict__ keys_in,
                                                                     const uint32_t* __restrict__ idx_in, int64_t n,
                                                                     int shift, int64_t ntiles,
                                                                     const uint64_t* __restrict__ off,
                                                                     uint64_t* __restrict__ keys_out,
                                                                     uint32_t* __restrict__ idx_out, int cons,
-                                                                    uint64_t kmask) {
-    constexpr int NW = kSrtThreads / 64;
-    constexpr int ROWS = kSrtTile / kSrtThreads;  // rows of 64 per wave (16)
+                                                                    uint64_t kmask, int xcd) {
+    constexpr int NW = TH / 64;
+    constexpr int ROWS = kSrtTile / TH;  // rows of 64 per wave
     __shared__ uint64_t skey[OUT == SRT_IDX ? 1 : kSrtTile];
     __shared__ uint32_t sidx[OUT == SRT_PACK ? 1 : kSrtTile];
     __shared__ uint8_t sdig[kSrtTile];
@@ -191,9 +274,17 @@ __global__ __launch_bounds__(kSrtThreads) void srt_downsweep_kernel(const uint64
     __shared__ uint32_t cnt[NW][256];
     __shared__ uint64_t wsum[NW];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int64_t base = (int64_t)blockIdx.x * kSrtTile;
+    // xcd: consecutive tiles on one XCD (bijective remap of the round-robin
+    // dispatch), so the digit runs that neighbouring tiles write into the
+    // same output lines meet in one L2 instead of leaving it as two partial
+    // line write-backs
+    const int64_t tile = xcd ? xcd_tile(blockIdx.x, ntiles) : (int64_t)blockIdx.x;
+    const int64_t base = tile * kSrtTile;
     const int m = n - base < kSrtTile ? (int)(n - base) : kSrtTile;
-    for (int w = 0; w < NW; ++w) cnt[w][tid] = 0;
+    // this tile's digit offsets (256 scattered words): issued first so their
+    // latency hides behind the key loads and the ranking
+    const uint64_t my_off = tid < 256 ? off[(int64_t)tid * ntiles + tile] : 0;
+    for (int i = tid; i < NW * 256; i += TH) cnt[i >> 8][i & 255] = 0;
     uint64_t k[ROWS];
     uint32_t rk[ROWS];
     const int c0 = wid * (kSrtTile / NW);  // this wave's chunk
@@ -224,17 +315,22 @@ __global__ __launch_bounds__(kSrtThreads) void srt_downsweep_kernel(const uint64
     }
     __syncthreads();
     {
-        // thread = digit: wave prefixes and the tile's digit starts
-        uint32_t c[NW], t = 0;
-        for (int w = 0; w < NW; ++w) {
-            c[w] = cnt[w][tid];
-            cnt[w][tid] = t;
-            t += c[w];
+        // thread = digit (threads >= 256 add nothing): wave prefixes and the
+        // tile's digit starts
+        uint32_t t = 0;
+        if (tid < 256) {
+            for (int w = 0; w < NW; ++w) {
+                const uint32_t c = cnt[w][tid];
+                cnt[w][tid] = t;
+                t += c;
+            }
         }
         uint64_t total;
         const uint32_t ds = (uint32_t)block_excl_scan(t, wsum, total);
-        dstart[tid] = ds;
-        gbase[tid] = off[(int64_t)tid * ntiles + blockIdx.x] - ds;
+        if (tid < 256) {
+            dstart[tid] = ds;
+            gbase[tid] = my_off - ds;
+        }
     }
     __syncthreads();
 #pragma unroll
@@ -259,7 +355,7 @@ __global__ __launch_bounds__(kSrtThreads) void srt_downsweep_kernel(const uint64
     }
     __syncthreads();
     // coalesced write-out: consecutive threads, consecutive slots of a digit run
-    for (int p = tid; p < m; p += kSrtThreads) {
+    for (int p = tid; p < m; p += TH) {
         const uint64_t o = gbase[sdig[p]] + (uint64_t)p;
         if (OUT != SRT_IDX) keys_out[o] = skey[p];
         if (OUT != SRT_PACK) idx_out[o] = sidx[p];
@@ -349,9 +445,11 @@ struct SrtScratch {
     uint64_t* off = nullptr;
     uint64_t* part = nullptr;
     unsigned long long* hist = nullptr;
-    int alloc(int64_t n, hipStream_t s) {
+    uint64_t* tbits = nullptr;  // per-tile OR / AND (srt_codes_stats_kernel)
+    int alloc(int64_t n, hipStream_t s, bool stats = false) {
         const int64_t ntiles = (n + kSrtTile - 1) / kSrtTile;
         int rc = dev_alloc((void**)&hist, 16, s);
+        if (!rc && n > 0 && stats) rc = dev_alloc((void**)&tbits, ntiles * 16, s);
         if (!rc && n > 0) rc = dev_alloc((void**)&cnt, ntiles * 256 * 4, s);
         if (!rc && n > 0) rc = dev_alloc((void**)&off, (ntiles * 256 + 1) * 8, s);
         if (!rc && n > 0) rc = dev_alloc((void**)&part, ((ntiles * 256 + kScanChunk - 1) / kScanChunk + 1) * 8, s);
@@ -362,6 +460,8 @@ struct SrtScratch {
         dev_free(off, s);
         dev_free(part, s);
         dev_free(hist, s);
+        dev_free(tbits, s);
+        tbits = nullptr;
         cnt = nullptr;
         off = nullptr;
         part = nullptr;
@@ -373,21 +473,58 @@ struct SrtScratch {
 // finds them), carrying idx[cur] (nullptr in idx[cur]: row ids are the
 // positions); the result (row ids) ends in idx[cur].  Codes and ids switch
 // to the PACKED representation as soon as the remaining code bits fit 32.
+// Downsweep shape, PLGPU_SORT_DT (read per call, for A/B in one process):
+// "256" (default) = 4 waves x 16 rows per tile, "512" = 8 waves x 8 rows,
+// "512w6" = the same held to 80 VGPRs (6 waves per SIMD).  Measured at 1e9
+// keys (tools/ab_sort.py): 256 33.5 ms, 512w6 35.5 ms per arg_sort.
+static int srt_dmode() {
+    const char* e = getenv("PLGPU_SORT_DT");
+    if (e == nullptr) return 0;
+    if (strcmp(e, "512") == 0) return 1;
+    if (strcmp(e, "512w6") == 0) return 2;
+    return 0;
+}
+
 template <bool IN_P, int OUT>
 static void srt_down(const uint64_t* ki, const uint32_t* ii, int64_t nv, int shift, int64_t ntiles,
                      const uint64_t* off, uint64_t* ko, uint32_t* io, int cons, uint64_t kmask, hipStream_t s) {
-    srt_downsweep_kernel<IN_P, OUT><<<(unsigned)ntiles, kSrtThreads, 0, s>>>(ki, ii, nv, shift, ntiles, off, ko, io,
-                                                                          cons, kmask);
+    const char* xe = getenv("PLGPU_SORT_XCD");  // "0": round-robin tiles (A/B)
+    const int xcd = (xe && strcmp(xe, "0") == 0) ? 0 : 1;
+    switch (srt_dmode()) {
+    case 0:
+        srt_downsweep_kernel<IN_P, OUT, 256, 1>
+            <<<(unsigned)ntiles, 256, 0, s>>>(ki, ii, nv, shift, ntiles, off, ko, io, cons, kmask, xcd);
+        break;
+    case 2:
+        srt_downsweep_kernel<IN_P, OUT, kSrtDThreads, 6>
+            <<<(unsigned)ntiles, kSrtDThreads, 0, s>>>(ki, ii, nv, shift, ntiles, off, ko, io, cons, kmask, xcd);
+        break;
+    default:
+        srt_downsweep_kernel<IN_P, OUT, kSrtDThreads, 1>
+            <<<(unsigned)ntiles, kSrtDThreads, 0, s>>>(ki, ii, nv, shift, ntiles, off, ko, io, cons, kmask, xcd);
+    }
 }
 
+// pre: srt_codes_stats_kernel produced keys[cur], the per-tile OR / AND in
+// sc.tbits and the byte-0 digit counts in sc.cnt.  final_out (optional): the
+// last pass writes the sorted row ids there (*wrote_final = true) instead of
+// into idx[cur].
 static int radix_passes(uint64_t* keys[2], uint32_t* idx[2], int64_t nv, int& cur, SrtScratch& sc, hipStream_t s,
-                        bool ids_implicit = false) {
+                        bool ids_implicit = false, bool pre = false, uint32_t* final_out = nullptr,
+                        bool* wrote_final = nullptr) {
+    if (wrote_final) *wrote_final = false;
     if (nv <= 0) return PLGPU_OK;
     const int cus = 256;
     unsigned long long h[2] = {0ull, ~0ull};
     hipError_t e = hipMemcpyAsync(sc.hist, h, 16, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) {
-        srt_bits_kernel<<<(unsigned)std::min<int64_t>((nv + 255) / 256, cus * 8), 256, 0, s>>>(keys[cur], nv, sc.hist);
+        const int64_t nt = (nv + kSrtTile - 1) / kSrtTile;
+        if (pre)
+            srt_tbits_kernel<<<(unsigned)std::min<int64_t>((nt + 255) / 256, cus * 4), 256, 0, s>>>(sc.tbits, nt,
+                                                                                                    sc.hist);
+        else
+            srt_bits_kernel<<<(unsigned)std::min<int64_t>((nv + 255) / 256, cus * 8), 256, 0, s>>>(keys[cur], nv,
+                                                                                                   sc.hist);
         e = hipGetLastError();
     }
     if (e == hipSuccess) e = hipMemcpyAsync(h, sc.hist, 16, hipMemcpyDeviceToHost, s);
@@ -413,7 +550,8 @@ static int radix_passes(uint64_t* keys[2], uint32_t* idx[2], int64_t nv, int& cu
         const int S = 8 * bytes[j];
         const int shift = packed ? 32 + S - cons : S;
         const uint32_t* ii = (ids_implicit && j == 0) ? nullptr : idx[cur];
-        srt_upsweep_kernel<<<(unsigned)ntiles, kSrtThreads, 0, s>>>(keys[cur], nv, shift, ntiles, sc.cnt);
+        if (!(pre && j == 0 && S == 0))  // byte-0 counts already in sc.cnt
+            srt_upsweep_kernel<<<(unsigned)ntiles, kSrtThreads, 0, s>>>(keys[cur], nv, shift, ntiles, sc.cnt);
         e = scan_exclusive<uint32_t>(sc.cnt, ntiles * 256, sc.off, sc.part, s);
         if (e != hipSuccess) return hip_fail(e, "sort scan");
         const bool last = j == nb - 1;
@@ -422,6 +560,10 @@ static int radix_passes(uint64_t* keys[2], uint32_t* idx[2], int64_t nv, int& cu
         const uint64_t kmask = hi_bits - ncons >= 64 ? ~0ull : ((1ull << (hi_bits - ncons)) - 1);
         uint64_t* ko = keys[cur ^ 1];
         uint32_t* io = idx[cur ^ 1];
+        if (last && final_out) {
+            io = final_out;
+            *wrote_final = true;
+        }
         if (packed) {
             if (last) srt_down<true, SRT_IDX>(keys[cur], ii, nv, shift, ntiles, sc.off, ko, io, 0, 0, s);
             else srt_down<true, SRT_PACK>(keys[cur], ii, nv, shift, ntiles, sc.off, ko, io, 0, 0, s);
@@ -468,7 +610,6 @@ PLGPU_API int plgpu_arg_sort(const plgpu_column* key, int32_t descending, int32_
         if (!rc) rc = dev_alloc((void**)&idx[i], n * 4, s);
     }
     int64_t nv = n;  // valid rows
-    const int cus = 256;
     if (!rc && c.validity) {
         uint64_t* voff = nullptr;
         uint32_t* vcnt = nullptr;
@@ -493,26 +634,30 @@ PLGPU_API int plgpu_arg_sort(const plgpu_column* key, int32_t descending, int32_
         dev_free(voff, s);
         dev_free(part, s);
         part = nullptr;
-    } else if (!rc) {
-        // row ids stay implicit (= positions) until the first pass writes them
-        srt_codes_kernel<<<(unsigned)std::min<int64_t>((n + 255) / 256, cus * 16), 256, 0, s>>>(
-            c, n, descending != 0, keys[0], nullptr);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) rc = hip_fail(e, "sort codes");
     }
     int cur = 0;
     SrtScratch sc;
-    if (!rc) rc = sc.alloc(nv, s);
-    if (!rc) rc = radix_passes(keys, idx, nv, cur, sc, s, c.validity == nullptr);
+    const bool stats = c.validity == nullptr;
+    if (!rc) rc = sc.alloc(nv, s, stats);
+    if (!rc && stats) {
+        // row ids stay implicit (= positions) until the first pass writes them
+        const int64_t ntiles = (n + kSrtTile - 1) / kSrtTile;
+        srt_codes_stats_kernel<<<(unsigned)ntiles, kSrtThreads, 0, s>>>(c, n, descending != 0, ntiles, keys[0],
+                                                                         sc.cnt, sc.tbits);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) rc = hip_fail(e, "sort codes");
+    }
+    uint32_t* out = (uint32_t*)out_idx->values;
+    const int64_t nn = n - nv;
+    // nulls first (default) or last, each group in row order
+    uint32_t* vdst = nulls_last ? out : out + nn;
+    uint32_t* ndst = nulls_last ? out + nv : out;
+    bool wrote = false;
+    if (!rc) rc = radix_passes(keys, idx, nv, cur, sc, s, stats, stats, vdst, &wrote);
     sc.release(s);
     if (!rc) {
-        uint32_t* out = (uint32_t*)out_idx->values;
-        const int64_t nn = n - nv;
-        // nulls first (default) or last, each group in row order
-        uint32_t* vdst = nulls_last ? out : out + nn;
-        uint32_t* ndst = nulls_last ? out + nv : out;
         hipError_t e = hipSuccess;
-        if (nv > 0) e = hipMemcpyAsync(vdst, idx[cur], nv * 4, hipMemcpyDeviceToDevice, s);
+        if (nv > 0 && !wrote) e = hipMemcpyAsync(vdst, idx[cur], nv * 4, hipMemcpyDeviceToDevice, s);
         if (e == hipSuccess && nn > 0) e = hipMemcpyAsync(ndst, nulls, nn * 4, hipMemcpyDeviceToDevice, s);
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (e != hipSuccess) rc = hip_fail(e, "sort output");
