@@ -31,7 +31,6 @@ namespace plgpu {
 constexpr int kSrtThreads = 256;                  // upsweep / stats workgroups
 constexpr int kSrtPer = 16;
 constexpr int kSrtTile = kSrtThreads * kSrtPer;  // 4096 codes per tile
-constexpr int kSrtDThreads = 512;                 // downsweep: 8 waves x 8 rows of 64 per tile
 
 __device__ __forceinline__ uint64_t sort_code(const DevCol& c, int64_t r, bool descending) {
     uint64_t b = dev_load(c, r);
@@ -256,16 +255,17 @@ __global__ __launch_bounds__(kSrtThreads) void srt_upsweep_kernel(const uint64_t
 // counts into local positions; the tile is staged in LDS in digit order and
 // written out in runs.  IN_P: input is PACKED.  OUT: SrtOut; a SEP -> PACK
 // transition keeps (code >> cons) & kmask as the remaining code.
-template <bool IN_P, int OUT, int TH, int WPE>
-__global__ __launch_bounds__(TH) __attribute__((amdgpu_waves_per_eu(OUT == SRT_SEP ? 1 : WPE))) void srt_downsweep_kernel(const uint64_t* __restrict__ keys_in,
+template <bool IN_P, int OUT>
+__global__ __launch_bounds__(kSrtThreads) void srt_downsweep_kernel(const uint64_t* __restrict__ keys_in,
                                                                     const uint32_t* __restrict__ idx_in, int64_t n,
                                                                     int shift, int64_t ntiles,
                                                                     const uint64_t* __restrict__ off,
                                                                     uint64_t* __restrict__ keys_out,
                                                                     uint32_t* __restrict__ idx_out, int cons,
                                                                     uint64_t kmask, int xcd) {
+    constexpr int TH = kSrtThreads;
     constexpr int NW = TH / 64;
-    constexpr int ROWS = kSrtTile / TH;  // rows of 64 per wave
+    constexpr int ROWS = kSrtTile / TH;  // rows of 64 per wave (16)
     __shared__ uint64_t skey[OUT == SRT_IDX ? 1 : kSrtTile];
     __shared__ uint32_t sidx[OUT == SRT_PACK ? 1 : kSrtTile];
     __shared__ uint8_t sdig[kSrtTile];
@@ -473,36 +473,13 @@ struct SrtScratch {
 // finds them), carrying idx[cur] (nullptr in idx[cur]: row ids are the
 // positions); the result (row ids) ends in idx[cur].  Codes and ids switch
 // to the PACKED representation as soon as the remaining code bits fit 32.
-// Downsweep shape, PLGPU_SORT_DT (read per call, for A/B in one process):
-// "256" (default) = 4 waves x 16 rows per tile, "512" = 8 waves x 8 rows,
-// "512w6" = the same held to 80 VGPRs (6 waves per SIMD).  Measured at 1e9
-// keys (tools/ab_sort.py): 256 33.5 ms, 512w6 35.5 ms per arg_sort.
-static int srt_dmode() {
-    const char* e = getenv("PLGPU_SORT_DT");
-    if (e == nullptr) return 0;
-    if (strcmp(e, "512") == 0) return 1;
-    if (strcmp(e, "512w6") == 0) return 2;
-    return 0;
-}
-
 template <bool IN_P, int OUT>
 static void srt_down(const uint64_t* ki, const uint32_t* ii, int64_t nv, int shift, int64_t ntiles,
                      const uint64_t* off, uint64_t* ko, uint32_t* io, int cons, uint64_t kmask, hipStream_t s) {
     const char* xe = getenv("PLGPU_SORT_XCD");  // "0": round-robin tiles (A/B)
     const int xcd = (xe && strcmp(xe, "0") == 0) ? 0 : 1;
-    switch (srt_dmode()) {
-    case 0:
-        srt_downsweep_kernel<IN_P, OUT, 256, 1>
-            <<<(unsigned)ntiles, 256, 0, s>>>(ki, ii, nv, shift, ntiles, off, ko, io, cons, kmask, xcd);
-        break;
-    case 2:
-        srt_downsweep_kernel<IN_P, OUT, kSrtDThreads, 6>
-            <<<(unsigned)ntiles, kSrtDThreads, 0, s>>>(ki, ii, nv, shift, ntiles, off, ko, io, cons, kmask, xcd);
-        break;
-    default:
-        srt_downsweep_kernel<IN_P, OUT, kSrtDThreads, 1>
-            <<<(unsigned)ntiles, kSrtDThreads, 0, s>>>(ki, ii, nv, shift, ntiles, off, ko, io, cons, kmask, xcd);
-    }
+    srt_downsweep_kernel<IN_P, OUT>
+        <<<(unsigned)ntiles, kSrtThreads, 0, s>>>(ki, ii, nv, shift, ntiles, off, ko, io, cons, kmask, xcd);
 }
 
 // pre: srt_codes_stats_kernel produced keys[cur], the per-tile OR / AND in

@@ -2,8 +2,10 @@
 
     python tools/ab_sort.py [ROWS] [MODE ...]
 
-A MODE is `K=V;K=V` over DT (PLGPU_SORT_DT: "256", "512", "512w6"; see
-sort.hip srt_dmode) and XCD (PLGPU_SORT_XCD: "0" = round-robin tiles).  Modes run interleaved in one process, 5 rounds with the first
+A MODE is `K=V;K=V` over the sort's PLGPU_SORT_* switches (today XCD:
+PLGPU_SORT_XCD=0 = round-robin tiles in the downsweep; "XCD=1" is the
+default).  Earlier switches measured with it and removed:
+DT (512-thread downsweep shapes) and RANK (batched leader atomics).  Modes run interleaved in one process, 5 rounds with the first
 discarded; every mode's permutation must equal the first mode's (stable sort:
 the permutation is unique).  Key: shuffled timestamps < 2^40 as in
 tools/bench_sort_rolling.py, so 5 radix passes run.  Prints per-mode median
@@ -19,11 +21,11 @@ import torch  # noqa: E402
 import polaroid_amd as pl  # noqa: E402
 
 n = int(float(sys.argv[1])) if len(sys.argv) > 1 else int(1e9)
-modes = sys.argv[2:] or ["DT=256;XCD=0", "DT=256", "DT=512w6;XCD=0", "DT=512w6"]
+modes = sys.argv[2:] or ["XCD=0", "XCD=1"]
 
 
 def set_mode(m):
-    for k in ("PLGPU_SORT_DT", "PLGPU_SORT_XCD"):
+    for k in ("PLGPU_SORT_XCD",):
         os.environ.pop(k, None)
     for kv in filter(None, m.split(";")):
         k, v = kv.split("=")
