@@ -690,4 +690,15 @@ __device__ __forceinline__ double fx_to_double(uint64_t w0, uint64_t w1, uint64_
 }
 
 
+// Bijective XCD-aware remap of a 1-D grid (cdna_hip_programming.md T1):
+// blocks that share an XCD (same blockIdx % 8) take consecutive tiles, so
+// output lines that neighbouring tiles share (the sort's digit runs and
+// digit-major count words, the partition runs of the many-groups scatter)
+// are completed in one L2 instead of being written back as partial lines
+// from several.
+__device__ __forceinline__ int64_t xcd_tile(int64_t bid, int64_t nwg) {
+    const int64_t q = nwg / 8, r = nwg % 8, x = bid % 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+}
+
 }  // namespace plgpu

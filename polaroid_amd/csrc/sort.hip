@@ -139,16 +139,6 @@ __global__ __launch_bounds__(256) void srt_bits_kernel(const uint64_t* __restric
     }
 }
 
-// Bijective XCD-aware remap of a 1-D grid (cdna_hip_programming.md T1):
-// blocks that share an XCD (same blockIdx % 8) take consecutive tiles, so
-// the digit-major count words and the digit runs that neighbouring tiles
-// write into the same lines are combined in one L2 instead of being written
-// back as partial lines from several.
-__device__ __forceinline__ int64_t xcd_tile(int64_t bid, int64_t nwg) {
-    const int64_t q = nwg / 8, r = nwg % 8, x = bid % 8;
-    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
-}
-
 // Null-free column, first read: each 4096-row tile writes its codes, its
 // OR / AND of them (reduced over the tiles by srt_tbits_kernel: constant
 // bytes) and its byte-0 digit counts, digit-major like the upsweep's -- the
