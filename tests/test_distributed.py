@@ -1,6 +1,7 @@
 """The multi-GPU group-by protocol (polaroid_amd/distributed.py) on CPU:
-world_size 2 over gloo, with a host model of the partial stage in place of
-the GPU kernels (those are covered by tests/test_gpu_distributed.py).
+world_size 2, and 8 (configs[4]'s rank count), over gloo, with a host model
+of the partial stage in place of the GPU kernels (those are covered by
+tests/test_gpu_distributed.py).
 
 Checks: the partial stage runs without a collective, each rank's windows
 travel with its record counts (one all-to-all of counts + header, one of
@@ -21,7 +22,6 @@ import torch.multiprocessing as mp
 
 from polaroid_amd import distributed as D
 
-WORLD = 2
 RW = 3  # record: [kind, key, sum]
 
 
@@ -77,21 +77,24 @@ class HostPartial:
         return (out, list(src_counts), [list(b) for b in src_bottoms]), None
 
 
-def _worker(rank, port, fail_rank, q):
+def _worker(rank, world, port, fail_rank, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         keys, vals = _shard(rank)
-        part = HostPartial(rank, WORLD, keys, vals, fail_rank)
+        part = HostPartial(rank, world, keys, vals, fail_rank)
         try:
-            (out, src_counts, src_bottoms), _ = D.run_partitioned(part, WORLD, None, torch.device("cpu"))
+            (out, src_counts, src_bottoms), _ = D.run_partitioned(part, world, None, torch.device("cpu"))
             err = None
         except D.N.PolaroidError as e:
             out, src_counts, src_bottoms, err = None, None, None, type(e).__name__ + ": " + str(e)
-        # exchange_records on its own: ragged counts including empty segments
+        # exchange_records on its own: ragged counts including empty
+        # segments (rank r sends r + 3 records to rank r + 1 and none to the
+        # others; at world 2: [0, 3] and [4, 0])
         rw = 2
-        counts = [0, 3] if rank == 0 else [5, 0]
+        counts = [0] * world
+        counts[(rank + 1) % world] = rank + 3
         send = torch.arange(sum(counts) * rw, dtype=torch.int64) + 1000 * rank
         recv, nrec, rows = D.exchange_records(send, counts, rw, header=[7, rank])
         q.put((rank, out, src_counts, src_bottoms, err, recv.tolist(), nrec, rows))
@@ -99,48 +102,54 @@ def _worker(rank, port, fail_rank, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("fail_rank", [-1, 0, 1])
-def test_partitioned_group_by_protocol_gloo(fail_rank):
+@pytest.mark.parametrize("world,fail_rank", [(2, -1), (2, 0), (2, 1), (8, -1), (8, 5)])
+def test_partitioned_group_by_protocol_gloo(world, fail_rank):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, port, fail_rank, q)) for r in range(WORLD)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, fail_rank, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
-    for _ in range(WORLD):
-        rank, out, src_counts, src_bottoms, err, recv, nrec, rows = q.get(timeout=120)
+    for _ in range(world):
+        rank, out, src_counts, src_bottoms, err, recv, nrec, rows = q.get(timeout=180)
         res[rank] = (out, src_counts, src_bottoms, err, recv, nrec, rows)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    # ragged exchange: rank 0 receives rank1's 5 records, rank 1 receives rank0's 3;
-    # every destination gets [count] + each source's header, in source order
-    assert res[0][5] == 5 and res[0][4] == list(range(1000, 1010))
-    assert res[1][5] == 3 and res[1][4] == list(range(0, 6))
-    assert res[0][6] == [[0, 7, 0], [5, 7, 1]]
-    assert res[1][6] == [[3, 7, 0], [0, 7, 1]]
+    # ragged exchange: rank r receives the r + 2 records of rank r - 1 (mod
+    # world); every destination gets [count] + each source's header, in
+    # source order
+    for r in range(world):
+        src = (r - 1) % world
+        nsrc = src + 3
+        assert res[r][5] == nsrc
+        assert res[r][4] == [1000 * src + i for i in range(nsrc * 2)]
+        assert res[r][6] == [[nsrc if q == src else 0, 7, q] for q in range(world)]
     if fail_rank >= 0:
         # the failing rank re-raises its own error, the others name it
         assert "refused on this rank" in res[fail_rank][3]
-        other = 1 - fail_rank
-        assert res[other][3].startswith("ComputeError") and f"[{fail_rank}]" in res[other][3]
+        for other in range(world):
+            if other != fail_rank:
+                assert res[other][3].startswith("ComputeError") and f"[{fail_rank}]" in res[other][3]
         return
     # every destination received each source's own windows, in rank order
-    for r in range(WORLD):
+    for r in range(world):
         assert res[r][3] is None
-        assert res[r][2] == [_bottoms(q) for q in range(WORLD)]
-        assert len(res[r][0]) <= sum(res[r][1]) <= WORLD * len(res[r][0])
+        assert res[r][2] == [_bottoms(q) for q in range(world)]
+        assert len(res[r][0]) <= sum(res[r][1]) <= world * len(res[r][0])
     # partitions are disjoint and their union is the full aggregation
-    k0, k1 = set(res[0][0]), set(res[1][0])
-    assert not (k0 & k1)
+    seen = set()
+    merged = {}
+    for r in range(world):
+        ks = set(res[r][0])
+        assert not (ks & seen)
+        seen |= ks
+        merged.update(res[r][0])
+        assert all(k % world == r for k in res[r][0])
     full = {}
-    for r in range(WORLD):
+    for r in range(world):
         keys, vals = _shard(r)
         for k, v in zip(keys.tolist(), vals.tolist()):
             full[k] = full.get(k, 0) + v
-    merged = dict(res[0][0])
-    merged.update(res[1][0])
     assert merged == full
-    for r in range(WORLD):
-        assert all(k % WORLD == r for k in res[r][0])
