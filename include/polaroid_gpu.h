@@ -349,6 +349,16 @@ int plgpu_gb_partial_export(plgpu_gb_partial* h, void* dst_records, int64_t* out
 
 void plgpu_gb_partial_free(plgpu_gb_partial* h);
 
+/* Rows of a key column routed to the rank that owns their key's partial
+ * states (the partition function plgpu_gb_partial_export routes records by;
+ * the null key and the INT64_MIN key go to rank 0): *out_perm receives a
+ * UInt32 row-index column grouped by rank in rank order, out_counts[world]
+ * the rows per rank.  Used to move per-rank first() / last() results to the
+ * owner of their groups (the partitioned sink's `combine_subset` for
+ * reduce/first_last.rs, polars-stream/src/nodes/group_by.rs:378). */
+int plgpu_gb_route(const plgpu_column* key, int32_t world, plgpu_column* out_perm,
+                   int64_t* out_counts, void* stream);
+
 /* Fold `n_records` received records (device memory) into this rank's
  * partition and finalize it like plgpu_group_by_agg (`cols` supplies the
  * dtypes only; `key_dtype` is the original key dtype). */

@@ -126,6 +126,7 @@ SIGNATURES = {
                                          C.POINTER(GroupByInfo), _P]),
     "plgpu_gb_partial_export": (C.c_int, [_P, _P, C.POINTER(C.c_int64), _P]),
     "plgpu_gb_partial_free": (None, [_P]),
+    "plgpu_gb_route": (C.c_int, [_COLP, C.c_int32, _COLP, C.POINTER(C.c_int64), _P]),
     "plgpu_gb_merge": (C.c_int, [_P, C.c_int64, _COLP, C.c_int32, C.POINTER(Agg), C.c_int32,
                                  C.POINTER(C.c_int32), C.c_int32, _COLP, _COLP,
                                  C.POINTER(GroupByInfo), _P]),

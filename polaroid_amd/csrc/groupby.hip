@@ -2943,6 +2943,73 @@ PLGPU_API int plgpu_gb_partial_export(plgpu_gb_partial* h, void* dst_records, in
 
 PLGPU_API void plgpu_gb_partial_free(plgpu_gb_partial* h) { delete h; }
 
+// Route rows by the partial states' owner rank (dest_rank of the row's key,
+// as gb_export_kernel routes records): pass 0 counts per rank, pass 1 writes
+// each row's index at its rank's cursor.  Order inside a rank is unspecified.
+__device__ __forceinline__ int route_rank(const DevCol& key, int64_t r, int world) {
+    if (!dev_valid(key, r)) return dest_rank(1, 0, world);
+    const uint64_t k = dev_load(key, r);
+    return dest_rank(k == kEmptyKey ? 2 : 0, k, world);
+}
+
+__global__ void gb_route_kernel(DevCol key, int64_t n, int world, int pass, unsigned long long* ctr,
+                                uint32_t* __restrict__ perm) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+        const int d = route_rank(key, r, world);
+        const unsigned long long at = atomicAdd(&ctr[d], 1ull);
+        if (pass) perm[at] = (uint32_t)r;
+    }
+}
+
+PLGPU_API int plgpu_gb_route(const plgpu_column* key, int32_t world, plgpu_column* out_perm, int64_t* out_counts,
+                             void* stream) {
+    if (key == nullptr || out_perm == nullptr || out_counts == nullptr) return fail(PLGPU_ERR_INVALID, "NULL argument");
+    if (world < 1 || world > 1024) return fail(PLGPU_ERR_INVALID, "world must be 1..1024");
+    if (!dtype_is_int(key->dtype) || dtype_bytes(key->dtype) > 8 || key->dtype == PLGPU_U64)
+        return fail(PLGPU_ERR_SCHEMA, "route key must be a signed or 32-bit integer column");
+    const int64_t n = key->length;
+    if (n < 0 || n >= 0xFFFFFFFFll) return fail(PLGPU_ERR_CAPACITY, "route input exceeds the u32 index space");
+    std::memset(out_perm, 0, sizeof *out_perm);
+    hipStream_t s = as_stream(stream);
+    int rc = make_owned_column(out_perm, PLGPU_U32, n, false, s);
+    if (rc) return rc;
+    unsigned long long* ctr = nullptr;  // [world] counts, then [world] cursors
+    if ((rc = dev_alloc((void**)&ctr, (size_t)world * 16, s))) {
+        plgpu_column_release(out_perm);
+        return rc;
+    }
+    const DevCol k = to_dev(*key);
+    const int g = (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4096));
+    std::vector<unsigned long long> hc(world), cur(world);
+    hipError_t e = hipMemsetAsync(ctr, 0, (size_t)world * 8, s);
+    if (e == hipSuccess && n > 0) {
+        gb_route_kernel<<<g, 256, 0, s>>>(k, n, world, 0, ctr, nullptr);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(hc.data(), ctr, (size_t)world * 8, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    unsigned long long run = 0;
+    for (int w = 0; w < world; ++w) {
+        cur[w] = run;
+        run += hc[w];
+        out_counts[w] = (int64_t)hc[w];
+    }
+    if (e == hipSuccess && n > 0) {
+        e = hipMemcpyAsync(ctr + world, cur.data(), (size_t)world * 8, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess) {
+            gb_route_kernel<<<g, 256, 0, s>>>(k, n, world, 1, ctr + world, (uint32_t*)out_perm->values);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) e = hipStreamSynchronize(s);  // `cur` is a host temporary
+    }
+    dev_free(ctr, s);
+    if (e != hipSuccess) {
+        plgpu_column_release(out_perm);
+        return hip_fail(e, "gb_route_kernel");
+    }
+    return PLGPU_OK;
+}
+
 // Merge of records from `nsrc` sources (nsrc 0: one source already on the
 // table's windows `bottoms`).  With sources, the table takes, per acc, the
 // lowest window of any source holding records, and each source's sum

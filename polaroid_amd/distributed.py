@@ -254,6 +254,62 @@ def run_partitioned(part, world: int, group, device, timings: dict | None = None
     return res
 
 
+def run_first_last(ops, local, world: int, group=None):
+    """first() / last() across ranks (reduce/first_last.rs: the value of the
+    group's first / last selected row, nulls included).  The shards are the
+    row order: rank r holds the rows after rank r-1's.  Each rank's
+    single-GPU group-by gives `local` (key + its first / last values); its
+    rows go to the rank owning their key's partial states (`ops.route`, the
+    same partition function as the records), arrive in source-rank order
+    (all-to-all), and the owner takes first() / last() over them
+    (`ops.combine`): the lowest rank holding a group has its first row, the
+    highest its last.  Returns this rank's (key + first / last) frame."""
+    perm, counts = ops.route(local, world)
+    recv, n = exchange_columns(ops.to_wire(local, perm), counts, group)
+    return ops.combine(ops.from_wire(recv, n))
+
+
+class GpuFirstLastOps:
+    """The device half of run_first_last, through the C-ABI."""
+
+    def __init__(self, key: str, exprs: Sequence[Expr]):
+        self.key = key
+        self.exprs = list(exprs)
+
+    def route(self, local, world: int):
+        from .frame import Series
+
+        perm = N.Column()
+        counts = (C.c_int64 * world)()
+        N.check(N.lib().plgpu_gb_route(C.byref(local[self.key]._col), world, C.byref(perm), counts, None))
+        return Series._from_native("__perm", perm), [int(c) for c in counts]
+
+    @staticmethod
+    def to_wire(local, perm):
+        return GpuJoinOps.to_wire(local, perm)
+
+    @staticmethod
+    def from_wire(cols, n: int):
+        return GpuJoinOps.from_wire(cols, n)
+
+    def combine(self, rows):
+        from .frame import _agg_base, _group_by
+        from .expr import col
+
+        out = []
+        for e in self.exprs:
+            nm = e.output_name()
+            c = col(nm)
+            out.append((c.first() if _agg_base(e).op == "first" else c.last()).alias(nm))
+        return _group_by(rows, self.key, out, False, None, None)
+
+
+def _first_last_split(aggs: Sequence[Expr]) -> list[int]:
+    from .frame import _agg_base
+
+    return [i for i, e in enumerate(aggs) if _agg_base(e).kind == "agg" and _agg_base(e).op in ("first", "last")]
+
+
 def group_by_agg(df, key: str, aggs: Sequence[Expr], predicate: Expr | None = None, *, group=None,
                  info: dict | None = None):
     """`df.lazy().filter(predicate).group_by(key).agg(*aggs)` over the shards
@@ -264,7 +320,7 @@ def group_by_agg(df, key: str, aggs: Sequence[Expr], predicate: Expr | None = No
     import torch
     import torch.distributed as dist
 
-    from .frame import _gb_lower, _lower_strings
+    from .frame import _agg_base, _gb_lower, _group_by, _join, _lower_strings
     from .expr import col
 
     if not dist.is_initialized():
@@ -291,21 +347,49 @@ def group_by_agg(df, key: str, aggs: Sequence[Expr], predicate: Expr | None = No
         if _allreduce_max([0 if short.value else 1], group, device)[0]:
             raise N.InvalidOperationError("the multi-GPU group-by takes String keys of at most 7 bytes")
         df = DataFrame([Series._from_native(key, codes) if nm == key else df[nm] for nm in df.columns])
-    g = _gb_lower(df, key, list(aggs), predicate)
-    if g.keycol.dtype not in (N.I64, N.I32) or len(g.keys) != 1:
+    if not isinstance(key, str) or key not in df.columns or df[key]._col.dtype not in (N.I64, N.I32):
         raise N.InvalidOperationError("the multi-GPU group-by takes one Int64 / Int32 (or short String) key column")
-    part = GpuPartial(g, world)
+    # first() / last() travel as values (run_first_last); every other
+    # aggregation as exact partial states
+    fl = _first_last_split(aggs)
+    rest = [e for i, e in enumerate(aggs) if i not in fl]
+    for i in fl:
+        c = _agg_base(aggs[i]).args[0]
+        if c.kind != "col" or c.value not in df.columns or df[c.value]._col.dtype not in _TORCH_WIRE:
+            raise N.InvalidOperationError("multi-GPU first() / last() take Int64 / Int32 / UInt32 / Float64 / "
+                                          "Boolean columns")
     timings: dict = {}
-    out, mi = run_partitioned(part, world, group, device, timings if info is not None else None)
+    out = part = mi = None
+    if rest or not fl:
+        g = _gb_lower(df, key, rest, predicate)
+        part = GpuPartial(g, world)
+        out, mi = run_partitioned(part, world, group, device, timings if info is not None else None)
+    if fl:
+        t0 = time.perf_counter()
+        ops = GpuFirstLastOps(key, [aggs[i] for i in fl])
+        local = _group_by(df, key, ops.exprs, False, predicate, None)
+        logical = {e.output_name(): local[e.output_name()]._logical_dtype() for e in ops.exprs}
+        owned = run_first_last(ops, local, world, group)
+        for nm, lg in logical.items():
+            owned[nm]._with_logical(lg)
+        if out is None:
+            joined = owned
+        else:
+            # both hold exactly this rank's groups (the same rows selected, the
+            # same partition function); the null key matches itself
+            joined = _join(out, owned, key, key, "_right", "m:m", True, "left", "inner")
+        out = DataFrame([joined[key]] + [joined[e.output_name()] for e in aggs])
+        if info is not None:
+            torch.cuda.synchronize()
+            timings["first_last_ms"] = (time.perf_counter() - t0) * 1e3
     if string_key:
         strs = N.Column()
         N.check(N.lib().plgpu_str_decode_short(C.byref(out[key]._col), C.byref(strs), None))
         out = DataFrame([Series._from_native(key, strs) if nm == key else out[nm] for nm in out.columns])
     torch.cuda.synchronize()
     if info is not None:
-        d = part.info.as_dict()
-        d["merge_groups"] = mi.groups
-        d["groups"] = mi.groups
+        d = part.info.as_dict() if part is not None else {}
+        d["merge_groups"] = d["groups"] = mi.groups if mi is not None else out.height
         d.update(timings)
         info.update(d)
     return out

@@ -153,3 +153,95 @@ def test_partitioned_group_by_protocol_gloo(world, fail_rank):
         for k, v in zip(keys.tolist(), vals.tolist()):
             full[k] = full.get(k, 0) + v
     assert merged == full
+
+
+# ------------------------------------------------- first() / last() across ranks
+def _fl_shard(rank, n=400):
+    """Rows of rank `rank` (rank order = row order): key, nullable key, and a
+    nullable value that records its global position."""
+    rng = np.random.default_rng(700 + rank)
+    keys = rng.integers(0, 37, n).astype(np.int64) - 5
+    kvalid = rng.random(n) > 0.05
+    vals = np.arange(n, dtype=np.int64) + rank * 1_000_000
+    vvalid = rng.random(n) > 0.2
+    return keys, kvalid, vals, vvalid
+
+
+def _first_last(keys, kvalid, vals, vvalid):
+    """{(key valid, key): ((first value or None), (last value or None))}."""
+    out = {}
+    for k, kv, v, vv in zip(keys.tolist(), kvalid.tolist(), vals.tolist(), vvalid.tolist()):
+        g = (bool(kv), k if kv else 0)
+        x = v if vv else None
+        out[g] = (out[g][0], x) if g in out else (x, x)
+    return out
+
+
+class HostFirstLastOps:
+    """Models GpuFirstLastOps over numpy: route by key % world (the null key
+    to rank 0), wire columns as CPU tensors, combine = first / last row per
+    key in arrival order."""
+
+    def route(self, local, world):
+        ks = sorted(local)
+        dest = [0 if not kv else k % world for kv, k in ks]
+        perm = [ks[i] for i in np.argsort(dest, kind="stable")]
+        return perm, [dest.count(r) for r in range(world)]
+
+    def to_wire(self, local, perm):
+        kv = torch.tensor([int(kv) for kv, _ in perm], dtype=torch.uint8)
+        k = torch.tensor([k for _, k in perm], dtype=torch.int64)
+        cols = [D.WireColumn("k", D.N.I64, k, kv)]
+        for j, nm in enumerate(("first", "last")):
+            v = [local[g][j] for g in perm]
+            cols.append(D.WireColumn(nm, D.N.I64, torch.tensor([0 if x is None else x for x in v], dtype=torch.int64),
+                                     torch.tensor([int(x is not None) for x in v], dtype=torch.uint8)))
+        return cols
+
+    def from_wire(self, cols, n):
+        return [c.values.tolist() for c in cols], [c.valid.tolist() for c in cols], n
+
+    def combine(self, rows):
+        (k, f, l), (kv, fv, lv), n = rows
+        out = {}
+        for i in range(n):
+            g = (bool(kv[i]), k[i] if kv[i] else 0)
+            fx, lx = (f[i] if fv[i] else None), (l[i] if lv[i] else None)
+            out[g] = (out[g][0], lx) if g in out else (fx, lx)
+        return out
+
+
+def _fl_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        local = _first_last(*_fl_shard(rank))
+        q.put((rank, D.run_first_last(HostFirstLastOps(), local, world)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_first_last_protocol_gloo(world):
+    """run_first_last: the owners' first / last over the per-rank results,
+    received in source-rank order, equal first / last over the concatenated
+    shards (nulls included); each group on exactly one rank."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fl_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    merged = {}
+    for r in range(world):
+        assert not (set(res[r]) & set(merged))
+        assert all((not kv and r == 0) or (kv and k % world == r) for kv, k in res[r])
+        merged.update(res[r])
+    shards = [_fl_shard(r) for r in range(world)]
+    full = _first_last(*[np.concatenate([s[i] for s in shards]) for i in range(4)])
+    assert merged == full

@@ -236,3 +236,126 @@ def test_group_by_agg_world1_rccl_string_key(gpu):
             D.group_by_agg(long_df, "sym", [pl.col("v").sum()])
     finally:
         dist.destroy_process_group()
+
+
+def _fl_simulate(shards, world, key, exprs, pred):
+    """run_first_last over `shards` in one process: each shard's local
+    first / last frame is routed by plgpu_gb_route, every destination
+    receives the sources' rows in source-rank order (as all_to_all lays them
+    out) and combines them."""
+    import torch
+
+    from polaroid_amd.frame import _group_by
+
+    ops = D.GpuFirstLastOps(key, exprs)
+    sent = []
+    for df in shards:
+        local = _group_by(df, key, exprs, False, pred, None)
+        perm, counts = ops.route(local, world)
+        sent.append((ops.to_wire(local, perm), counts))
+    frames = []
+    for dest in range(world):
+        cols = []
+        n = sum(c[dest] for _, c in sent)
+        for j in range(len(sent[0][0])):
+            # a column is sent with a validity mask if any source holds nulls in it (_wire_spec)
+            nullable = any(w[j].valid is not None for w, _ in sent)
+            vals, valid = [], []
+            for wire, counts in sent:
+                off = sum(counts[:dest])
+                vals.append(wire[j].values[off: off + counts[dest]])
+                if nullable:
+                    valid.append(wire[j].valid[off: off + counts[dest]] if wire[j].valid is not None else
+                                 torch.ones(counts[dest], dtype=torch.uint8, device="cuda"))
+            proto = sent[0][0][j]
+            cols.append(D.WireColumn(proto.name, proto.dtype, torch.cat(vals).contiguous(),
+                                     torch.cat(valid).contiguous() if nullable else None))
+        frames.append(ops.combine(ops.from_wire(cols, n)))
+    return frames
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_first_last_across_ranks(gpu, world):
+    """first() / last() over W shards (rank order = row order): the union of
+    the W owners' results equals the single-GPU group-by of the concatenated
+    rows, values and nulls included, and each group lands on the rank that
+    owns its partial states (plgpu_gb_route = the records' partition)."""
+    rng = np.random.default_rng(40 + world)
+    n = 20_000
+    N_ = n * world
+    key = rng.integers(0, 500, N_).astype(np.int64) * 7 - 1000
+    key[rng.random(N_) < 0.01] = np.iinfo(np.int64).min
+    kvalid = rng.random(N_) > 0.01
+    a = rng.standard_normal(N_)
+    va = rng.random(N_) > 0.1
+    b = rng.integers(-50, 50, N_).astype(np.int32)
+    full = pl.DataFrame({"k": pl.Series.from_numpy("k", key, kvalid), "a": pl.Series.from_numpy("a", a, va),
+                         "b": pl.Series.from_numpy("b", b)})
+    shards = [pl.DataFrame({"k": pl.Series.from_numpy("k", key[s * n:(s + 1) * n], kvalid[s * n:(s + 1) * n]),
+                            "a": pl.Series.from_numpy("a", a[s * n:(s + 1) * n], va[s * n:(s + 1) * n]),
+                            "b": pl.Series.from_numpy("b", b[s * n:(s + 1) * n])}) for s in range(world)]
+    exprs = [pl.col("a").first().alias("fa"), pl.col("a").last().alias("la"), pl.col("b").first().alias("fb"),
+             pl.col("b").last().alias("lb")]
+    pred = pl.col("b") > -30
+    frames = _fl_simulate(shards, world, "k", exprs, pred)
+    ref = full.lazy().filter(pred).group_by("k").agg(*exprs).collect()
+
+    def rows(f):
+        ks = f["k"].to_numpy().astype(np.int64)
+        kv = f["k"].validity_numpy()
+        out = {}
+        for i in range(f.height):
+            vals = []
+            for c in ("fa", "la", "fb", "lb"):
+                v = f[c].validity_numpy()[i]
+                vals.append(f[c].to_numpy()[i].item() if v else None)
+            out[(bool(kv[i]), int(ks[i]) if kv[i] else 0)] = tuple(vals)
+        return out
+
+    got = {}
+    for dest, f in enumerate(frames):
+        r = rows(f)
+        # ownership: a group's rows were routed to `dest` by the records' partition function
+        perm, counts = D.GpuFirstLastOps("k", exprs).route(f, world)
+        assert counts[dest] == f.height
+        assert not (set(r) & set(got))
+        got.update(r)
+    assert got == rows(ref)
+
+
+def test_group_by_agg_world1_rccl_first_last(gpu):
+    """group_by_agg with first() / last() next to exact sums, over RCCL at
+    world 1 (states + values exchanged, joined on the owner), against the
+    single-GPU group-by; first / last alone skip the partial states."""
+    import torch.distributed as dist
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        rng = np.random.default_rng(5)
+        n = 100_000
+        cols = _frame(rng, n)
+        key = rng.integers(0, 300, n).astype(np.int32)
+        kv = rng.random(n) > 0.02
+        df = pl.DataFrame({"k": pl.Series.from_numpy("k", key, kv), "a": pl.Series.from_numpy("a", *cols["a"]),
+                           "d": pl.Series.from_numpy("d", *cols["d"])})
+        for exprs in ([pl.col("a").sum().alias("s"), pl.col("d").first().alias("f"), pl.len(),
+                       pl.col("a").last().alias("l")],
+                      [pl.col("d").last().alias("l"), pl.col("a").first().alias("f")]):
+            info = {}
+            out = D.group_by_agg(df, "k", exprs, pl.col("d") > 0.0, info=info)
+            ref = df.lazy().filter(pl.col("d") > 0.0).group_by("k").agg(*exprs).collect()
+            assert out.columns == ref.columns and out["k"].dtype == pl.Int32
+            assert info["groups"] == ref.height and "first_last_ms" in info
+
+            def table(f):
+                return sorted(zip(*[[(v if not (isinstance(v, float) and v != v) else "nan") for v in f[c].to_list()]
+                                    for c in f.columns]), key=repr)
+
+            assert table(out) == table(ref)
+    finally:
+        dist.destroy_process_group()
