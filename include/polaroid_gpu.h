@@ -359,6 +359,21 @@ void plgpu_gb_partial_free(plgpu_gb_partial* h);
 int plgpu_gb_route(const plgpu_column* key, int32_t world, plgpu_column* out_perm,
                    int64_t* out_counts, void* stream);
 
+/* Packed tuple keys agreed across ranks (the multi-key group-by's exact
+ * Int64 packing, row_encode.rs:11 semantics: tuple equality, a null distinct
+ * from every value).  plgpu_key_ranges writes per key column [min, max,
+ * any null] (signed; no valid value: min = INT64_MAX > max = INT64_MIN) into
+ * out_ranges[3 * nkeys]; the caller reduces them over the ranks (min / max /
+ * max).  plgpu_key_pack packs every row's tuple with the plan those ranges
+ * give into *out_codes (Int64, no nulls; *out_ok = 0 and no column when the
+ * fields need more than 63 bits); plgpu_key_unpack turns codes back into
+ * key columns of `dtypes`.  Keys: integer (not UInt64) or Boolean. */
+int plgpu_key_ranges(const plgpu_column* keys, int32_t nkeys, int64_t* out_ranges, void* stream);
+int plgpu_key_pack(const plgpu_column* keys, int32_t nkeys, const int64_t* ranges,
+                   plgpu_column* out_codes, int32_t* out_ok, void* stream);
+int plgpu_key_unpack(const plgpu_column* codes, const int32_t* dtypes, int32_t nkeys,
+                     const int64_t* ranges, plgpu_column* out_keys, void* stream);
+
 /* Fold `n_records` received records (device memory) into this rank's
  * partition and finalize it like plgpu_group_by_agg (`cols` supplies the
  * dtypes only; `key_dtype` is the original key dtype). */

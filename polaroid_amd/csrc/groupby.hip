@@ -3010,6 +3010,143 @@ PLGPU_API int plgpu_gb_route(const plgpu_column* key, int32_t world, plgpu_colum
     return PLGPU_OK;
 }
 
+// ---------------------------------------- packed tuple keys across ranks
+// The multi-key group-by packs integer / Boolean key tuples into one exact
+// Int64 code (mk_plan_pack).  Across GPUs every rank must pack with the same
+// plan, so the ranges are exported, reduced over the ranks by the caller
+// (min / max / or), and the agreed ranges drive the packing and decoding.
+static bool mk_packable(const plgpu_column* keys, int32_t nkeys) {
+    for (int i = 0; i < nkeys; ++i) {
+        const int32_t dt = keys[i].dtype;
+        if ((!dtype_is_int(dt) && dt != PLGPU_BOOL) || dt == PLGPU_U64) return false;
+    }
+    return true;
+}
+
+static void mk_ranges_to_ord(const int64_t* ranges, int32_t nkeys, uint64_t* h) {
+    for (int i = 0; i < nkeys; ++i) {
+        h[3 * i] = (uint64_t)ranges[3 * i] ^ 0x8000000000000000ull;
+        h[3 * i + 1] = (uint64_t)ranges[3 * i + 1] ^ 0x8000000000000000ull;
+        h[3 * i + 2] = ranges[3 * i + 2] != 0;
+    }
+}
+
+PLGPU_API int plgpu_key_ranges(const plgpu_column* keys, int32_t nkeys, int64_t* out_ranges, void* stream) {
+    if (keys == nullptr || out_ranges == nullptr) return fail(PLGPU_ERR_INVALID, "NULL argument");
+    if (nkeys < 1 || nkeys > kMaxKeys) return fail(PLGPU_ERR_INVALID, "number of key columns must be 1..8");
+    if (!mk_packable(keys, nkeys)) return fail(PLGPU_ERR_SCHEMA, "packed keys must be integer or Boolean columns");
+    MkKeys mk;
+    std::memset(&mk, 0, sizeof mk);
+    mk.n = nkeys;
+    const int64_t n = keys[0].length;
+    for (int i = 0; i < nkeys; ++i) {
+        if (keys[i].length != n) return fail(PLGPU_ERR_SHAPE, "key columns must have equal lengths");
+        mk.c[i] = to_dev(keys[i]);
+    }
+    hipStream_t s = as_stream(stream);
+    unsigned long long* st = nullptr;
+    int rc = dev_alloc((void**)&st, 3 * kMaxKeys * 8, s);
+    if (rc) return rc;
+    unsigned long long h[3 * kMaxKeys];
+    for (int i = 0; i < kMaxKeys; ++i) h[3 * i] = ~0ull, h[3 * i + 1] = 0, h[3 * i + 2] = 0;
+    hipError_t e = hipMemcpyAsync(st, h, sizeof h, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && n > 0) {
+        const int g = (int)std::min<int64_t>((n + 255) / 256, (int64_t)num_cus() * 16);
+        mk_range_kernel<<<g, 256, 0, s>>>(mk, n, st);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(h, st, sizeof h, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    dev_free(st, s);
+    if (e != hipSuccess) return hip_fail(e, "key range pass");
+    // signed min / max (no valid value: min = INT64_MAX > max = INT64_MIN)
+    for (int i = 0; i < nkeys; ++i) {
+        out_ranges[3 * i] = (int64_t)(h[3 * i] ^ 0x8000000000000000ull);
+        out_ranges[3 * i + 1] = (int64_t)(h[3 * i + 1] ^ 0x8000000000000000ull);
+        out_ranges[3 * i + 2] = h[3 * i + 2] ? 1 : 0;
+    }
+    return PLGPU_OK;
+}
+
+PLGPU_API int plgpu_key_pack(const plgpu_column* keys, int32_t nkeys, const int64_t* ranges, plgpu_column* out_codes,
+                             int32_t* out_ok, void* stream) {
+    if (keys == nullptr || ranges == nullptr || out_codes == nullptr || out_ok == nullptr)
+        return fail(PLGPU_ERR_INVALID, "NULL argument");
+    if (nkeys < 1 || nkeys > kMaxKeys) return fail(PLGPU_ERR_INVALID, "number of key columns must be 1..8");
+    if (!mk_packable(keys, nkeys)) return fail(PLGPU_ERR_SCHEMA, "packed keys must be integer or Boolean columns");
+    std::memset(out_codes, 0, sizeof *out_codes);
+    *out_ok = 0;
+    MkKeys mk;
+    std::memset(&mk, 0, sizeof mk);
+    mk.n = nkeys;
+    const int64_t n = keys[0].length;
+    for (int i = 0; i < nkeys; ++i) {
+        if (keys[i].length != n) return fail(PLGPU_ERR_SHAPE, "key columns must have equal lengths");
+        mk.c[i] = to_dev(keys[i]);
+    }
+    uint64_t h[3 * kMaxKeys];
+    mk_ranges_to_ord(ranges, nkeys, h);
+    MkPack pk;
+    std::memset(&pk, 0, sizeof pk);
+    pk.n = nkeys;
+    mk_plan_from_ranges(h, nkeys, &pk);
+    if (!pk.ok) return PLGPU_OK;
+    hipStream_t s = as_stream(stream);
+    int rc = make_owned_column(out_codes, PLGPU_I64, n, false, s);
+    if (rc) return rc;
+    if (n > 0) {
+        const int g = (int)std::min<int64_t>((n + 255) / 256, (int64_t)num_cus() * 16);
+        mk_pack_kernel<<<g, 256, 0, s>>>(mk, pk, n, (uint64_t*)out_codes->values, nullptr);
+        hipError_t e = hipGetLastError();
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) {
+            plgpu_column_release(out_codes);
+            return hip_fail(e, "mk_pack_kernel");
+        }
+    }
+    *out_ok = 1;
+    return PLGPU_OK;
+}
+
+PLGPU_API int plgpu_key_unpack(const plgpu_column* codes, const int32_t* dtypes, int32_t nkeys, const int64_t* ranges,
+                               plgpu_column* out_keys, void* stream) {
+    if (codes == nullptr || dtypes == nullptr || ranges == nullptr || out_keys == nullptr)
+        return fail(PLGPU_ERR_INVALID, "NULL argument");
+    if (nkeys < 1 || nkeys > kMaxKeys) return fail(PLGPU_ERR_INVALID, "number of key columns must be 1..8");
+    if (codes->dtype != PLGPU_I64) return fail(PLGPU_ERR_SCHEMA, "packed codes must be an Int64 column");
+    for (int i = 0; i < nkeys; ++i) std::memset(&out_keys[i], 0, sizeof(plgpu_column));
+    uint64_t h[3 * kMaxKeys];
+    mk_ranges_to_ord(ranges, nkeys, h);
+    MkPack pk;
+    std::memset(&pk, 0, sizeof pk);
+    pk.n = nkeys;
+    mk_plan_from_ranges(h, nkeys, &pk);
+    if (!pk.ok) return fail(PLGPU_ERR_INVALID, "these key ranges do not pack into 63 bits");
+    hipStream_t s = as_stream(stream);
+    const int64_t groups = codes->length;
+    const int gg = (int)std::max<int64_t>(1, std::min<int64_t>((groups + 255) / 256, 4096));
+    const int64_t* cv = (const int64_t*)codes->values + codes->offset;
+    int rc = PLGPU_OK;
+    for (int i = 0; i < nkeys && !rc; ++i) {
+        const bool nullable = pk.nullable[i] != 0;
+        rc = make_owned_column(&out_keys[i], dtypes[i], groups, nullable, s);
+        if (rc || groups == 0) continue;
+        if (dtypes[i] == PLGPU_BOOL) (void)hipMemsetAsync((void*)out_keys[i].values, 0, ((groups + 63) / 64) * 8, s);
+        if (nullable) (void)hipMemsetAsync((void*)out_keys[i].validity, 0, ((groups + 63) / 64) * 8, s);
+        mk_unpack_kernel<<<gg, 256, 0, s>>>(cv, nullptr, groups, pk, i, dtypes[i], (void*)out_keys[i].values,
+                                            (uint32_t*)out_keys[i].validity);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) rc = hip_fail(e, "mk_unpack_kernel");
+    }
+    if (!rc) {
+        hipError_t e = hipStreamSynchronize(s);
+        if (e != hipSuccess) rc = hip_fail(e, "key unpack");
+    }
+    if (rc)
+        for (int i = 0; i < nkeys; ++i) plgpu_column_release(&out_keys[i]);
+    return rc;
+}
+
 // Merge of records from `nsrc` sources (nsrc 0: one source already on the
 // table's windows `bottoms`).  With sources, the table takes, per acc, the
 // lowest window of any source holding records, and each source's sum

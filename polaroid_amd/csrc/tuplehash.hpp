@@ -204,6 +204,32 @@ __global__ __launch_bounds__(256) void mk_unpack_kernel(const int64_t* __restric
     }
 }
 
+// Packing plan from per-key [ord(min), ord(max), any null] ranges (min >
+// max: no valid value); pk->ok = 0 when the fields need more than 63 bits.
+inline void mk_plan_from_ranges(const uint64_t* h, int n, MkPack* pk) {
+    int shift = 0;
+    pk->ok = 0;
+    for (int i = 0; i < n; ++i) {
+        uint64_t mn = h[3 * i], mx = h[3 * i + 1];
+        const bool nul = h[3 * i + 2] != 0;
+        if (mn > mx) {  // no valid value anywhere: one code (null or 0)
+            mn = mx = 0x8000000000000000ull;
+        }
+        const uint64_t span = mx - mn;  // of ord values == of the signed values
+        const uint64_t codes = span + (nul ? 2u : 1u);
+        if (span >= (1ull << 62)) return;
+        int b = 0;
+        while (b < 63 && (1ull << b) < codes) ++b;
+        pk->minv[i] = (int64_t)(mn ^ 0x8000000000000000ull);
+        pk->shift[i] = shift;
+        pk->bits[i] = b;
+        pk->nullable[i] = nul ? 1 : 0;
+        shift += b;
+        if (shift > 63) return;
+    }
+    pk->ok = 1;
+}
+
 // Range pass over `ka` (and `kb`, the other join side, when non-null) and the
 // packing plan; pk->ok = 0 when a key is Float64 or the fields need > 63 bits.
 inline int mk_plan_pack(const MkKeys& ka, int64_t na, const MkKeys* kb, int64_t nb, int grid, MkPack* pk,
@@ -237,7 +263,7 @@ inline int mk_plan_pack(const MkKeys& ka, int64_t na, const MkKeys* kb, int64_t 
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     dev_free(st, s);
     if (e != hipSuccess) return hip_fail(e, "key range pass");
-    int shift = 0;
+    uint64_t r[3 * kMaxKeys];
     for (int i = 0; i < ka.n; ++i) {
         uint64_t mn = h[3 * i], mx = h[3 * i + 1];
         bool nul = h[3 * i + 2] != 0;
@@ -247,22 +273,11 @@ inline int mk_plan_pack(const MkKeys& ka, int64_t na, const MkKeys* kb, int64_t 
             mx = mx2 > mx ? mx2 : mx;
             nul = nul || h[3 * (kMaxKeys + i) + 2] != 0;
         }
-        if (mn > mx) {  // no valid value anywhere: one code (null or 0)
-            mn = mx = 0x8000000000000000ull;
-        }
-        const uint64_t span = mx - mn;  // of ord values == of the signed values
-        const uint64_t codes = span + (nul ? 2u : 1u);
-        if (span >= (1ull << 62)) return PLGPU_OK;
-        int b = 0;
-        while (b < 63 && (1ull << b) < codes) ++b;
-        pk->minv[i] = (int64_t)(mn ^ 0x8000000000000000ull);
-        pk->shift[i] = shift;
-        pk->bits[i] = b;
-        pk->nullable[i] = nul ? 1 : 0;
-        shift += b;
-        if (shift > 63) return PLGPU_OK;
+        r[3 * i] = mn;
+        r[3 * i + 1] = mx;
+        r[3 * i + 2] = nul ? 1 : 0;
     }
-    pk->ok = 1;
+    mk_plan_from_ranges(r, ka.n, pk);
     return PLGPU_OK;
 }
 

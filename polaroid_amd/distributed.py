@@ -310,6 +310,62 @@ def _first_last_split(aggs: Sequence[Expr]) -> list[int]:
     return [i for i, e in enumerate(aggs) if _agg_base(e).kind == "agg" and _agg_base(e).op in ("first", "last")]
 
 
+_PACKABLE = (N.I64, N.I32, N.U32, N.I16, N.U16, N.I8, N.U8, N.BOOL)
+
+
+def _pack_keys(df, keys: list, group, device):
+    """Several integer / Boolean key columns -> one exact Int64 code column
+    that every rank computes with the same plan (plgpu_key_ranges on each
+    shard, reduced over the ranks, then plgpu_key_pack), so the single-key
+    partitioned protocol groups tuples exactly (row_encode.rs:11 semantics:
+    a null is its own value).  Returns (plan, frame with the code column,
+    its name)."""
+    import torch
+    import torch.distributed as dist
+
+    from .frame import DataFrame, Series, _col_array
+
+    for k in keys:
+        if k not in df.columns:
+            raise N.ComputeError(f'unable to find column "{k}"')
+        if df[k]._col.dtype not in _PACKABLE:
+            raise N.InvalidOperationError("the multi-GPU multi-key group-by takes integer / Boolean key columns")
+    nk = len(keys)
+    kcols = _col_array([df[k] for k in keys])
+    r = (C.c_int64 * (3 * nk))()
+    N.check(N.lib().plgpu_key_ranges(kcols, nk, r, None))
+    t = torch.tensor(list(r), dtype=torch.int64, device=device).view(nk, 3)
+    lo, hi = t[:, 0].contiguous(), t[:, 1:].contiguous()
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=group)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=group)
+    agreed = torch.cat([lo.view(nk, 1), hi], dim=1).view(-1).tolist()
+    ranges = (C.c_int64 * (3 * nk))(*agreed)
+    codes = N.Column()
+    ok = C.c_int32(0)
+    N.check(N.lib().plgpu_key_pack(kcols, nk, ranges, C.byref(codes), C.byref(ok), None))
+    if not ok.value:  # the same agreed ranges on every rank: every rank refuses
+        raise N.InvalidOperationError("the multi-GPU multi-key group-by: the key ranges need more than 63 bits")
+    name = "__key"
+    while name in df.columns:
+        name += "_"
+    plan = (keys, [df[k]._col.dtype for k in keys], [df[k]._logical_dtype() for k in keys], ranges)
+    return plan, DataFrame(list(df._cols.values()) + [Series._from_native(name, codes)]), name
+
+
+def _unpack_keys(out, code_name: str, plan, agg_names: list):
+    """The code column of a result back into its key columns (first), then
+    the aggregations."""
+    from .frame import DataFrame, Series
+
+    keys, dtypes, logical, ranges = plan
+    nk = len(keys)
+    res = (N.Column * nk)()
+    N.check(N.lib().plgpu_key_unpack(C.byref(out[code_name]._col), (C.c_int32 * nk)(*dtypes), nk, ranges, res,
+                                     None))
+    return DataFrame([Series._from_native(k, res[i], logical[i]) for i, k in enumerate(keys)] +
+                     [out[nm] for nm in agg_names])
+
+
 def group_by_agg(df, key: str, aggs: Sequence[Expr], predicate: Expr | None = None, *, group=None,
                  info: dict | None = None):
     """`df.lazy().filter(predicate).group_by(key).agg(*aggs)` over the shards
@@ -347,8 +403,14 @@ def group_by_agg(df, key: str, aggs: Sequence[Expr], predicate: Expr | None = No
         if _allreduce_max([0 if short.value else 1], group, device)[0]:
             raise N.InvalidOperationError("the multi-GPU group-by takes String keys of at most 7 bytes")
         df = DataFrame([Series._from_native(key, codes) if nm == key else df[nm] for nm in df.columns])
+    packed = None
+    if not isinstance(key, str) and len(key) > 1:
+        packed, df, key = _pack_keys(df, list(key), group, device)
+    elif not isinstance(key, str):
+        key = key[0]
     if not isinstance(key, str) or key not in df.columns or df[key]._col.dtype not in (N.I64, N.I32):
-        raise N.InvalidOperationError("the multi-GPU group-by takes one Int64 / Int32 (or short String) key column")
+        raise N.InvalidOperationError("the multi-GPU group-by takes one Int64 / Int32 (or short String) key column, "
+                                      "or several integer / Boolean key columns")
     # first() / last() travel as values (run_first_last); every other
     # aggregation as exact partial states
     fl = _first_last_split(aggs)
@@ -382,6 +444,8 @@ def group_by_agg(df, key: str, aggs: Sequence[Expr], predicate: Expr | None = No
         if info is not None:
             torch.cuda.synchronize()
             timings["first_last_ms"] = (time.perf_counter() - t0) * 1e3
+    if packed is not None:
+        out = _unpack_keys(out, key, packed, [e.output_name() for e in aggs])
     if string_key:
         strs = N.Column()
         N.check(N.lib().plgpu_str_decode_short(C.byref(out[key]._col), C.byref(strs), None))

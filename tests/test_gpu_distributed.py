@@ -359,3 +359,99 @@ def test_group_by_agg_world1_rccl_first_last(gpu):
             assert table(out) == table(ref)
     finally:
         dist.destroy_process_group()
+
+
+def _ranges(cols):
+    import ctypes as C
+
+    from polaroid_amd import _native as N
+    from polaroid_amd.frame import _col_array
+
+    r = (C.c_int64 * (3 * len(cols)))()
+    N.check(N.lib().plgpu_key_ranges(_col_array(cols), len(cols), r, None))
+    return list(r)
+
+
+def test_key_pack_agreed_across_shards(gpu):
+    """plgpu_key_ranges per shard, reduced (min / max / or) as the ranks do,
+    then plgpu_key_pack on each shard: equal tuples get equal codes on every
+    shard, distinct tuples distinct codes (nulls are values), and
+    plgpu_key_unpack restores the tuples; an empty shard reduces neutrally."""
+    import ctypes as C
+
+    from polaroid_amd import _native as N
+    from polaroid_amd.frame import _col_array
+
+    rng = np.random.default_rng(9)
+    shards = []
+    for s, n in enumerate([30_000, 0, 17_000]):
+        k1 = rng.integers(-5, 40 + 100 * s, n).astype(np.int64)
+        k2 = rng.integers(0, 3, n).astype(np.int32)
+        kb = rng.random(n) < 0.5
+        shards.append([pl.Series.from_numpy("k1", k1, rng.random(n) > 0.1), pl.Series.from_numpy("k2", k2),
+                       pl.Series.from_numpy("kb", kb, rng.random(n) > 0.2)])
+    rs = [_ranges(c) for c in shards]
+    assert rs[1][0] > rs[1][1]  # empty shard: min > max
+    agreed = []
+    for i in range(3):
+        agreed += [min(r[3 * i] for r in rs), max(r[3 * i + 1] for r in rs), max(r[3 * i + 2] for r in rs)]
+    ranges = (C.c_int64 * 9)(*agreed)
+    seen = {}
+    for cols in shards:
+        codes = N.Column()
+        ok = C.c_int32(0)
+        N.check(N.lib().plgpu_key_pack(_col_array(cols), 3, ranges, C.byref(codes), C.byref(ok), None))
+        assert ok.value == 1
+        cs = pl.Series._from_native("c", codes)
+        got = cs.to_numpy().astype(np.int64)
+        tuples = list(zip(*[[(None if not v else x) for x, v in zip(c.to_numpy().tolist(), c.validity_numpy())]
+                            for c in cols]))
+        for t, c in zip(tuples, got.tolist()):
+            assert seen.setdefault(t, c) == c
+        out = (N.Column * 3)()
+        N.check(N.lib().plgpu_key_unpack(C.byref(cs._col), (C.c_int32 * 3)(*[c._col.dtype for c in cols]), 3,
+                                         ranges, out, None))
+        back = [pl.Series._from_native(c.name, out[i]) for i, c in enumerate(cols)]
+        assert list(zip(*[b.to_list() for b in back])) == [tuple(x if x is None else (bool(x) if i == 2 else int(x))
+                                                                 for i, x in enumerate(t)) for t in tuples]
+    assert len(set(seen.values())) == len(seen)
+
+
+def test_group_by_agg_world1_rccl_multi_key(gpu):
+    """The multi-GPU group-by on (Int64, Int32, Boolean) keys with nulls:
+    packed codes agreed over the ranks, then the single-key protocol; against
+    the single-GPU multi-key group-by.  Float keys are refused."""
+    import torch.distributed as dist
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        rng = np.random.default_rng(6)
+        n = 120_000
+        cols = _frame(rng, n)
+        df = pl.DataFrame({"k1": pl.Series.from_numpy("k1", rng.integers(-50, 50, n).astype(np.int64) * 1000,
+                                                      rng.random(n) > 0.05),
+                           "k2": pl.Series.from_numpy("k2", rng.integers(0, 7, n).astype(np.int32)),
+                           "kb": pl.Series.from_numpy("kb", rng.random(n) < 0.3, rng.random(n) > 0.1),
+                           "a": pl.Series.from_numpy("a", *cols["a"]), "d": pl.Series.from_numpy("d", *cols["d"])})
+        exprs = [pl.col("a").sum().alias("s"), pl.col("d").max().alias("m"), pl.len(), pl.col("d").first().alias("f")]
+        out = D.group_by_agg(df, ("k1", "k2", "kb"), exprs, pl.col("d") > -2.0)
+        ref = df.lazy().filter(pl.col("d") > -2.0).group_by("k1", "k2", "kb").agg(*exprs).collect()
+        assert out.columns == ref.columns
+        assert [out[c].dtype for c in out.columns] == [ref[c].dtype for c in ref.columns]
+
+        def table(f):
+            return sorted(zip(*[[(v if not (isinstance(v, float) and v != v) else "nan") for v in f[c].to_list()]
+                                for c in f.columns]), key=repr)
+
+        assert table(out) == table(ref)
+        fdf = pl.DataFrame({"k": pl.Series.from_numpy("k", np.array([1.0, 2.0])),
+                            "j": pl.Series.from_numpy("j", np.array([1, 2], dtype=np.int64))})
+        with pytest.raises(pl.InvalidOperationError, match="integer / Boolean"):
+            D.group_by_agg(fdf, ("k", "j"), [pl.len()])
+    finally:
+        dist.destroy_process_group()
