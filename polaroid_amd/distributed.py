@@ -366,6 +366,80 @@ def _unpack_keys(out, code_name: str, plan, agg_names: list):
                      [out[nm] for nm in agg_names])
 
 
+def _group_by_var(df, key, aggs: Sequence[Expr], predicate, group, info: dict | None):
+    """var() / std(ddof) across ranks (polars-expr/src/reduce/var_std.rs),
+    composed like the single-GPU frame._group_by_var from exact passes:
+      1. the multi-GPU group-by with each var / std column's mean and count
+         next to the other aggregations (this rank's partition of groups);
+      2. the owners' (key, mean) rows all-gathered, so every rank holds every
+         group's mean (groups x 8 B per column, independent of rows);
+      3. every local row's squared deviation from its group's mean
+         (plgpu_group_sq_dev for one integer key, else a left join), exactly
+         summed per group by a second multi-GPU group-by (same partitions);
+      4. the second result aligned to the first on the key, then
+         plgpu_var_finalize (null when count <= ddof; sqrt for std)."""
+    from .expr import col
+    from .frame import DataFrame, Series, _agg_base, _eval, _join
+
+    keys = [key] if isinstance(key, str) else list(key)
+    key = keys[0] if len(keys) == 1 else tuple(keys)
+    for k in keys:
+        if k not in df.columns:
+            raise N.ComputeError(f'unable to find column "{k}"')
+        if df[k]._col.dtype not in _TORCH_WIRE:
+            raise N.InvalidOperationError("multi-GPU var / std take integer / Float64 / Boolean key columns")
+    var_cols: list[str] = []
+    plain: list[Expr] = []
+    for e in aggs:
+        b = _agg_base(e)
+        if b.kind == "agg" and b.op in ("std", "var"):
+            if b.args[0].kind != "col":
+                raise N.InvalidOperationError("var / std of a computed expression is not supported")
+            if b.args[0].value not in var_cols:
+                var_cols.append(b.args[0].value)
+        else:
+            plain.append(e)
+    helpers = []
+    for c in var_cols:
+        helpers += [col(c).mean().alias(f"__vm_{c}"), col(c).count().alias(f"__vn_{c}")]
+    first = group_by_agg(df, key, plain + helpers, predicate, group=group, info=info)
+    means = DataFrame([first[k] for k in keys] + [first[f"__vm_{c}"] for c in var_cols])
+    wire, total = allgather_columns(GpuJoinOps.to_wire(means), means.height, group)
+    allm = GpuJoinOps.from_wire(wire, total)
+    for k in keys:  # logical key dtypes (Datetime, ...) survive the wire as their physical
+        allm[k]._with_logical(df[k]._logical_dtype())
+    if len(keys) == 1 and df[keys[0]]._col.dtype in (N.I64, N.I32, N.U32, N.BOOL):
+        sq = []
+        for c in var_cols:
+            o = N.Column()
+            N.check(N.lib().plgpu_group_sq_dev(C.byref(df[keys[0]]._col), C.byref(df[c]._col),
+                                               C.byref(allm[keys[0]]._col), C.byref(allm[f"__vm_{c}"]._col),
+                                               C.byref(o), None))
+            sq.append(Series._from_native(f"__vd_{c}", o))
+        rows = DataFrame(list(df._cols.values()) + sq)
+    else:
+        rows = _join(df, allm, key, key, "_right", "m:m", True, "left", "left")
+        sq = [_eval(((col(c).cast("f64") - col(f"__vm_{c}")) * (col(c).cast("f64") - col(f"__vm_{c}")))
+                    .alias(f"__vd_{c}"), rows) for c in var_cols]
+        rows = DataFrame(list(rows._cols.values()) + sq)
+    second = group_by_agg(rows, key, [col(f"__vd_{c}").sum().alias(f"__vd_{c}") for c in var_cols], predicate,
+                          group=group)
+    # the same groups on this rank, in another order: align on the key
+    second = _join(DataFrame([first[k] for k in keys]), second, key, key, "_right", "m:m", True, "left", "inner")
+    res: dict[str, Series] = {}
+    for e in aggs:
+        b = _agg_base(e)
+        if not (b.kind == "agg" and b.op in ("std", "var")):
+            res[e.output_name()] = first[e.output_name()]
+            continue
+        c = b.args[0].value
+        o = N.Column()
+        N.check(N.lib().plgpu_var_finalize(C.byref(second[f"__vd_{c}"]._col), C.byref(first[f"__vn_{c}"]._col),
+                                           int(b.value), int(b.op == "std"), C.byref(o), None))
+        res[e.output_name()] = Series._from_native(e.output_name(), o)
+    return DataFrame([first[k] for k in keys] + [res[e.output_name()] for e in aggs])
+
+
 def group_by_agg(df, key: str, aggs: Sequence[Expr], predicate: Expr | None = None, *, group=None,
                  info: dict | None = None):
     """`df.lazy().filter(predicate).group_by(key).agg(*aggs)` over the shards
@@ -388,6 +462,8 @@ def group_by_agg(df, key: str, aggs: Sequence[Expr], predicate: Expr | None = No
     from .frame import DataFrame, Series, String
 
     aggs = [a if isinstance(a, Expr) else col(a) for a in aggs]
+    if any(_agg_base(e).kind == "agg" and _agg_base(e).op in ("std", "var") for e in aggs):
+        return _group_by_var(df, key, aggs, predicate, group, info)
     if predicate is not None:
         # String comparisons / pattern tests become Boolean columns first,
         # against the String columns as they are (before the key turns into

@@ -455,3 +455,44 @@ def test_group_by_agg_world1_rccl_multi_key(gpu):
             D.group_by_agg(fdf, ("k", "j"), [pl.len()])
     finally:
         dist.destroy_process_group()
+
+
+def test_group_by_agg_world1_rccl_var_std(gpu):
+    """var / std(ddof) across ranks (means all-gathered, squared deviations
+    summed exactly by a second partitioned pass, aligned on the key), one
+    RCCL rank, against the single-GPU var / std (itself pinned against the
+    reference's Welford results in test_gpu_var_std.py); single and two
+    keys, with nulls, a predicate and groups of one row (ddof=1 -> null)."""
+    import torch.distributed as dist
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        rng = np.random.default_rng(8)
+        n = 80_000
+        cols = _frame(rng, n)
+        k = rng.integers(0, 400, n).astype(np.int64)
+        k[:5] = [10_000, 10_001, 10_002, 10_003, 10_004]  # one-row groups
+        df = pl.DataFrame({"k": pl.Series.from_numpy("k", k, rng.random(n) > 0.03),
+                           "j": pl.Series.from_numpy("j", rng.integers(0, 3, n).astype(np.int32)),
+                           "b": pl.Series.from_numpy("b", rng.integers(-1000, 1000, n).astype(np.int64)),
+                           "d": pl.Series.from_numpy("d", *cols["d"])})
+        exprs = [pl.col("d").var().alias("vd"), pl.col("b").std().alias("sb"), pl.col("d").sum().alias("s"),
+                 pl.col("b").var(ddof=0).alias("vb0")]
+        for key in ("k", ("k", "j")):
+            by = (key,) if isinstance(key, str) else key
+            out = D.group_by_agg(df, key, exprs, pl.col("d") > -4.0)
+            ref = df.lazy().filter(pl.col("d") > -4.0).group_by(*by).agg(*exprs).collect()
+            assert out.columns == ref.columns
+
+            def table(f):
+                return sorted(zip(*[[(v if not (isinstance(v, float) and v != v) else "nan") for v in f[c].to_list()]
+                                    for c in f.columns]), key=repr)
+
+            assert table(out) == table(ref)
+    finally:
+        dist.destroy_process_group()
