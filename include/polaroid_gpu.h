@@ -374,6 +374,13 @@ int plgpu_key_pack(const plgpu_column* keys, int32_t nkeys, const int64_t* range
 int plgpu_key_unpack(const plgpu_column* codes, const int32_t* dtypes, int32_t nkeys,
                      const int64_t* ranges, plgpu_column* out_keys, void* stream);
 
+/* Float64 / Float32 keys across ranks: each key as the Int64 of its
+ * canonical bits (-0.0 as 0.0, every NaN as one NaN; polars-utils/src/
+ * total_ord.rs TotalEq groups exactly these together), validity carried, so
+ * a float key crosses the integer-keyed partitioned group-by (the output
+ * key is each group's first value, carried by a first() aggregation). */
+int plgpu_float_key_encode(const plgpu_column* keys, plgpu_column* out_codes, void* stream);
+
 /* Fold `n_records` received records (device memory) into this rank's
  * partition and finalize it like plgpu_group_by_agg (`cols` supplies the
  * dtypes only; `key_dtype` is the original key dtype). */

@@ -128,6 +128,7 @@ SIGNATURES = {
     "plgpu_gb_partial_free": (None, [_P]),
     "plgpu_gb_route": (C.c_int, [_COLP, C.c_int32, _COLP, C.POINTER(C.c_int64), _P]),
     "plgpu_key_ranges": (C.c_int, [_COLP, C.c_int32, C.POINTER(C.c_int64), _P]),
+    "plgpu_float_key_encode": (C.c_int, [_COLP, _COLP, _P]),
     "plgpu_key_pack": (C.c_int, [_COLP, C.c_int32, C.POINTER(C.c_int64), _COLP, C.POINTER(C.c_int32), _P]),
     "plgpu_key_unpack": (C.c_int, [_COLP, C.POINTER(C.c_int32), C.c_int32, C.POINTER(C.c_int64), _COLP, _P]),
     "plgpu_gb_merge": (C.c_int, [_P, C.c_int64, _COLP, C.c_int32, C.POINTER(Agg), C.c_int32,

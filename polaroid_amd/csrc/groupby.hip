@@ -3147,6 +3147,45 @@ PLGPU_API int plgpu_key_unpack(const plgpu_column* codes, const int32_t* dtypes,
     return rc;
 }
 
+// Float keys across ranks: a Float64 / Float32 key as the Int64 of its
+// canonical bits (mk_word: -0.0 -> 0.0, every NaN -> one NaN), equal exactly
+// when the reference's TotalEq groups them together.  The canonical bits
+// are never INT64_MIN (that is -0.0's pattern).
+__global__ __launch_bounds__(256) void float_code_kernel(DevCol c, int64_t n, int64_t* __restrict__ out,
+                                                         uint64_t* __restrict__ valid_words) {
+    for (int64_t r0 = (int64_t)blockIdx.x * blockDim.x; r0 < n; r0 += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = r0 + threadIdx.x;
+        const bool in = r < n;
+        const bool v = in && dev_valid(c, r);
+        if (in) out[r] = v ? (int64_t)mk_word(c, r) : 0;
+        const uint64_t b = __ballot(v);
+        if ((threadIdx.x & 63) == 0 && r < n) valid_words[r >> 6] = b;
+    }
+}
+
+PLGPU_API int plgpu_float_key_encode(const plgpu_column* keys, plgpu_column* out_codes, void* stream) {
+    if (keys == nullptr || out_codes == nullptr) return fail(PLGPU_ERR_INVALID, "NULL argument");
+    std::memset(out_codes, 0, sizeof *out_codes);
+    if (keys->dtype != PLGPU_F64 && keys->dtype != PLGPU_F32)
+        return fail(PLGPU_ERR_SCHEMA, "float key codes of a non-float column");
+    hipStream_t s = as_stream(stream);
+    const int64_t n = keys->length;
+    int rc = make_owned_column(out_codes, PLGPU_I64, n, true, s);
+    if (rc) return rc;
+    if (n > 0) {
+        const int g = (int)std::min<int64_t>((n + 255) / 256, (int64_t)num_cus() * 16);
+        float_code_kernel<<<g, 256, 0, s>>>(to_dev(*keys), n, (int64_t*)out_codes->values,
+                                            (uint64_t*)out_codes->validity);
+        hipError_t e = hipGetLastError();
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) {
+            plgpu_column_release(out_codes);
+            return hip_fail(e, "float key codes");
+        }
+    }
+    return PLGPU_OK;
+}
+
 // Merge of records from `nsrc` sources (nsrc 0: one source already on the
 // table's windows `bottoms`).  With sources, the table takes, per acc, the
 // lowest window of any source holding records, and each source's sum

@@ -480,13 +480,31 @@ def group_by_agg(df, key: str, aggs: Sequence[Expr], predicate: Expr | None = No
             raise N.InvalidOperationError("the multi-GPU group-by takes String keys of at most 7 bytes")
         df = DataFrame([Series._from_native(key, codes) if nm == key else df[nm] for nm in df.columns])
     packed = None
-    if not isinstance(key, str) and len(key) > 1:
-        packed, df, key = _pack_keys(df, list(key), group, device)
-    elif not isinstance(key, str):
+    float_key = None
+    if isinstance(key, str) and key in df.columns and df[key]._col.dtype in (N.F64, N.F32):
+        # a float key crosses as the Int64 of its canonical bits (TotalEq
+        # classes: -0.0 with 0.0, every NaN together); decoded at the end
+        # The output key is each group's first selected value (the reference
+        # takes the group's first row: -0.0 or 0.0, the NaN's own bits), so
+        # the original column rides along as a first() aggregation.
+        float_key = "__kf_first"
+        while float_key in df.columns:
+            float_key += "_"
+        codes = N.Column()
+        N.check(N.lib().plgpu_float_key_encode(C.byref(df[key]._col), C.byref(codes), None))
+        df = DataFrame([Series._from_native(key, codes) if nm == key else df[nm] for nm in df.columns] +
+                       [df[key].alias(float_key)])
+        aggs = aggs + [col(float_key).first().alias(float_key)]
+    if not isinstance(key, str) and len(key) == 1:
         key = key[0]
+    if not isinstance(key, str) or (key in df.columns and df[key]._col.dtype in _PACKABLE
+                                    and df[key]._col.dtype not in (N.I64, N.I32)):
+        # several integer / Boolean keys, or one narrow / unsigned / Boolean
+        # key: one exact Int64 code with a plan agreed over the ranks
+        packed, df, key = _pack_keys(df, [key] if isinstance(key, str) else list(key), group, device)
     if not isinstance(key, str) or key not in df.columns or df[key]._col.dtype not in (N.I64, N.I32):
-        raise N.InvalidOperationError("the multi-GPU group-by takes one Int64 / Int32 (or short String) key column, "
-                                      "or several integer / Boolean key columns")
+        raise N.InvalidOperationError("the multi-GPU group-by takes one integer / float (or short String) key "
+                                      "column, or several integer / Boolean key columns")
     # first() / last() travel as values (run_first_last); every other
     # aggregation as exact partial states
     fl = _first_last_split(aggs)
@@ -494,8 +512,7 @@ def group_by_agg(df, key: str, aggs: Sequence[Expr], predicate: Expr | None = No
     for i in fl:
         c = _agg_base(aggs[i]).args[0]
         if c.kind != "col" or c.value not in df.columns or df[c.value]._col.dtype not in _TORCH_WIRE:
-            raise N.InvalidOperationError("multi-GPU first() / last() take Int64 / Int32 / UInt32 / Float64 / "
-                                          "Boolean columns")
+            raise N.InvalidOperationError("multi-GPU first() / last() take numeric or Boolean columns")
     timings: dict = {}
     out = part = mi = None
     if rest or not fl:
@@ -522,6 +539,9 @@ def group_by_agg(df, key: str, aggs: Sequence[Expr], predicate: Expr | None = No
             timings["first_last_ms"] = (time.perf_counter() - t0) * 1e3
     if packed is not None:
         out = _unpack_keys(out, key, packed, [e.output_name() for e in aggs])
+    if float_key is not None:
+        out = DataFrame([out[float_key].alias(key) if nm == key else out[nm] for nm in out.columns
+                         if nm != float_key])
     if string_key:
         strs = N.Column()
         N.check(N.lib().plgpu_str_decode_short(C.byref(out[key]._col), C.byref(strs), None))
@@ -560,7 +580,8 @@ def group_by_agg(df, key: str, aggs: Sequence[Expr], predicate: Expr | None = No
 
 JOIN_BROADCAST_ROWS = 1 << 26  # the smaller side is broadcast up to 64M rows (all ranks)
 
-_TORCH_WIRE = {N.I64: "int64", N.F64: "int64", N.I32: "int32", N.U32: "int32", N.BOOL: "uint8"}
+_TORCH_WIRE = {N.I64: "int64", N.F64: "int64", N.I32: "int32", N.U32: "int32", N.BOOL: "uint8", N.U64: "int64",
+               N.F32: "int32", N.I16: "int16", N.U16: "int16", N.I8: "int8", N.U8: "uint8"}
 
 
 class WireColumn:

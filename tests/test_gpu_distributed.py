@@ -496,3 +496,41 @@ def test_group_by_agg_world1_rccl_var_std(gpu):
             assert table(out) == table(ref)
     finally:
         dist.destroy_process_group()
+
+
+def test_group_by_agg_world1_rccl_float_and_narrow_keys(gpu):
+    """One Float64 key (canonical-bit codes: -0.0 with 0.0, NaNs together,
+    a null group), one Float32, UInt16 and Boolean key (packed codes), over
+    RCCL at world 1, against the single-GPU group-by."""
+    import torch.distributed as dist
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        rng = np.random.default_rng(12)
+        n = 60_000
+        cols = _frame(rng, n)
+        kf = np.array([0.0, -0.0, np.nan, -np.nan, 1.5, -2.25, np.inf, -np.inf, 1e300])[rng.integers(0, 9, n)]
+        kv = rng.random(n) > 0.05
+        df = pl.DataFrame({"kf": pl.Series.from_numpy("kf", kf, kv),
+                           "kf32": pl.Series.from_numpy("kf32", kf.astype(np.float32), kv),
+                           "ku": pl.Series.from_numpy("ku", rng.integers(0, 60000, n).astype(np.uint16)),
+                           "kb": pl.Series.from_numpy("kb", rng.random(n) < 0.4, rng.random(n) > 0.1),
+                           "a": pl.Series.from_numpy("a", *cols["a"]), "d": pl.Series.from_numpy("d", *cols["d"])})
+        exprs = [pl.col("a").sum().alias("s"), pl.col("d").min().alias("m"), pl.len(), pl.col("d").last().alias("l")]
+
+        def table(f):
+            return sorted(zip(*[[(v if not (isinstance(v, float) and v != v) else "nan") for v in f[c].to_list()]
+                                for c in f.columns]), key=repr)
+
+        for key in ("kf", "kf32", "ku", "kb"):
+            out = D.group_by_agg(df, key, exprs, pl.col("d") > -3.0)
+            ref = df.lazy().filter(pl.col("d") > -3.0).group_by(key).agg(*exprs).collect()
+            assert out.columns == ref.columns and out[key].dtype == ref[key].dtype, key
+            assert table(out) == table(ref), key
+    finally:
+        dist.destroy_process_group()
