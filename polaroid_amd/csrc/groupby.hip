@@ -3159,7 +3159,7 @@ __global__ __launch_bounds__(256) void float_code_kernel(DevCol c, int64_t n, in
         const bool v = in && dev_valid(c, r);
         if (in) out[r] = v ? (int64_t)mk_word(c, r) : 0;
         const uint64_t b = __ballot(v);
-        if ((threadIdx.x & 63) == 0 && r < n) valid_words[r >> 6] = b;
+        if (valid_words && (threadIdx.x & 63) == 0 && r < n) valid_words[r >> 6] = b;
     }
 }
 
@@ -3170,7 +3170,9 @@ PLGPU_API int plgpu_float_key_encode(const plgpu_column* keys, plgpu_column* out
         return fail(PLGPU_ERR_SCHEMA, "float key codes of a non-float column");
     hipStream_t s = as_stream(stream);
     const int64_t n = keys->length;
-    int rc = make_owned_column(out_codes, PLGPU_I64, n, true, s);
+    // validity only when the keys have nulls: a null-free key keeps the
+    // group-by's fast kernels
+    int rc = make_owned_column(out_codes, PLGPU_I64, n, keys->validity != nullptr, s);
     if (rc) return rc;
     if (n > 0) {
         const int g = (int)std::min<int64_t>((n + 255) / 256, (int64_t)num_cus() * 16);
