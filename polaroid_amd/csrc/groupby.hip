@@ -2188,7 +2188,12 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
         // (2 + 3 nacc fields); the full layout must still fit one workgroup
         // per CU for a 3-limb rerun through the generic kernel
         const int fields = (pl.sum_only && pl.limbs == 2) ? 2 + 3 * p.nacc : p.nfields;
-        for (size_t budget : {(size_t)80 * 1024, (size_t)160 * 1024}) {
+        // Fewer, larger partition tables first (160 KB, one workgroup per
+        // CU): measured 2-7 % faster than 80 KB tables at 14k-100k groups
+        // (profiles/r02_ab_part.log).  PLGPU_PART_LDS_KB (A/B only): the
+        // first LDS budget tried.
+        const size_t first_kb = getenv("PLGPU_PART_LDS_KB") ? (size_t)atoi(getenv("PLGPU_PART_LDS_KB")) : 160;
+        for (size_t budget : {first_kb * 1024, (size_t)80 * 1024, (size_t)160 * 1024}) {
             int lb = 13;
             while (lb > 6 && ((size_t)fields * ((1u << lb) + 2) * 8 > budget ||
                               (size_t)p.nfields * ((1u << lb) + 2) * 8 > (size_t)160 * 1024))
@@ -2270,7 +2275,9 @@ static int gb_partition(GbRun& R) {
     PLGPU_HIP(hipGetLastError());
     R.part_range = range;
     // workgroups per partition: fill the chip, bound rows per workgroup
-    int nb = (int)std::max<int64_t>(1, (2 * (int64_t)num_cus() + P - 1) / P);
+    // PLGPU_PART_WGS_PER_CU (A/B only): workgroups per CU over all partitions
+    const int64_t wpc = getenv("PLGPU_PART_WGS_PER_CU") ? std::max(1, atoi(getenv("PLGPU_PART_WGS_PER_CU"))) : 4;
+    int nb = (int)std::max<int64_t>(1, (wpc * (int64_t)num_cus() + P - 1) / P);
     while ((int64_t)maxpart > (int64_t)nb * (kMaxRowsPerWg / 2)) nb *= 2;
     R.part_blocks = nb;
     return PLGPU_OK;
