@@ -944,6 +944,34 @@ __global__ __launch_bounds__(kGbThreads) __attribute__((amdgpu_waves_per_eu(WPE)
         tstep = p.part_blocks;
     }
     constexpr uint32_t VM = (1u << NACC) - 1u;
+    // RACC (partition buffers, sum-only, 2 limbs): each lane keeps KR
+    // register accumulators {slot, len, limbs} and adds a row whose group
+    // it already holds there instead of in LDS.  Time-ordered keys put only
+    // a few groups into a wave at a time, whose same-address LDS atomics
+    // serialise (bank-conflict ratio 0.92 measured); ABL 13 turns it off.
+    constexpr bool RACC = PART && SUMONLY && LIMBS == 2 && ABL == 0;
+    constexpr int KR = RACC ? 4 : 1;
+    int rs[KR];
+    uint64_t rn[KR], rlo_[KR][NA], rhi_[KR][NA];
+#pragma unroll
+    for (int k = 0; k < KR; ++k) {
+        rs[k] = -1;
+        rn[k] = 0;
+#pragma unroll
+        for (int a = 0; a < NA; ++a) rlo_[k][a] = rhi_[k][a] = 0;
+    }
+    int rvict = 0;
+    auto racc_flush = [&](int k) {
+        if (rs[k] < 0) return;
+        unsigned long long* q = (unsigned long long*)&lds[rs[k]];
+        atomicAdd(q + L, (unsigned long long)rn[k]);
+#pragma unroll
+        for (int a = 0; a < NACC; ++a) {
+            atomicAdd(q + so_mid(a) * L, (unsigned long long)rlo_[k][a]);
+            atomicAdd(q + so_top(a) * L, (unsigned long long)rhi_[k][a]);
+        }
+        rs[k] = -1;
+    };
     FastTile<NACC, ROWS> cur;
     if (ABL != 5 && t < ntiles) fast_load<NACC, PRED, ROWS, NTL>(p, t, cur, rbase, rmax);
     for (; t < ntiles; t += tstep) {
@@ -993,7 +1021,57 @@ __global__ __launch_bounds__(kGbThreads) __attribute__((amdgpu_waves_per_eu(WPE)
                     bot[a] = bot0[a];
                 }
                 if (s == kGlobalKey) s = lds_find(lds, p.lbits, p.lcap, cur.key[0]);
-                if (SUMONLY && s >= 0) {
+                bool held = false;
+                if (RACC && s >= 0) {
+                    uint64_t lo[NA], hi[NA];
+                    bool ok = true;
+#pragma unroll
+                    for (int a = 0; a < NACC; ++a) {
+                        uint64_t l0, l1, l2;
+                        ok = fx_limbs_fast<LIMBS>(rv[a], bot[a], l0, l1, l2) && ok;
+                        lo[a] = l0;
+                        hi[a] = l1;
+                    }
+                    if (ok) {
+                        // fully in-window row: into the lane's accumulator
+                        // for slot s (evicting one round-robin if none holds it)
+                        int k = -1;
+#pragma unroll
+                        for (int i = 0; i < KR; ++i)
+                            if (rs[i] == s) k = i;
+                        if (k < 0) {
+#pragma unroll
+                            for (int i = 0; i < KR; ++i)
+                                if (k < 0 && rs[i] < 0) k = i;
+                        }
+                        if (k < 0) {
+                            k = rvict;
+                            rvict = (rvict + 1) % KR;
+#pragma unroll
+                            for (int i = 0; i < KR; ++i)
+                                if (i == k) racc_flush(i);
+                        }
+#pragma unroll
+                        for (int i = 0; i < KR; ++i) {
+                            if (i != k) continue;
+                            if (rs[i] < 0) {
+                                rs[i] = s;
+                                rn[i] = 0;
+#pragma unroll
+                                for (int a = 0; a < NA; ++a) rlo_[i][a] = rhi_[i][a] = 0;
+                            }
+                            rn[i] += 1;
+#pragma unroll
+                            for (int a = 0; a < NACC; ++a) {
+                                rlo_[i][a] += lo[a];
+                                rhi_[i][a] += hi[a];
+                            }
+                        }
+                        held = true;
+                    }
+                }
+                if (held) {
+                } else if (SUMONLY && s >= 0) {
                     unsigned long long* q = (unsigned long long*)&lds[s];
                     if (ABL == 1) {
 #pragma unroll
@@ -1060,6 +1138,10 @@ __global__ __launch_bounds__(kGbThreads) __attribute__((amdgpu_waves_per_eu(WPE)
             }
         }
         if (ABL != 5) cur = nxt;
+    }
+    if (RACC) {
+#pragma unroll
+        for (int k = 0; k < KR; ++k) racc_flush(k);
     }
     if (SLIM) {
         __syncthreads();
@@ -2283,9 +2365,9 @@ static int gb_partition(GbRun& R) {
     return PLGPU_OK;
 }
 
-template <int NACC, int LIMBS>
-static hipError_t launch_part_fast(const Plan& pp, int grid, hipStream_t s) {
-    const void* kern = (const void*)gb_fast_kernel<NACC, 0, true, 2, LIMBS, 0, 1, true>;
+template <int NACC, int LIMBS, int ABL>
+static hipError_t launch_part_fast_abl(const Plan& pp, int grid, hipStream_t s) {
+    const void* kern = (const void*)gb_fast_kernel<NACC, 0, true, 2, LIMBS, ABL, 1, true>;
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -2294,8 +2376,16 @@ static hipError_t launch_part_fast(const Plan& pp, int grid, hipStream_t s) {
     const size_t lds = (size_t)(LIMBS == 2 ? 2 + 3 * NACC : pp.p.nfields) * (pp.p.lcap + 2) * 8;
     DevProgram none;
     std::memset(&none, 0, sizeof none);
-    gb_fast_kernel<NACC, 0, true, 2, LIMBS, 0, 1, true><<<grid, kGbThreads, lds, s>>>(pp.p, none);
+    gb_fast_kernel<NACC, 0, true, 2, LIMBS, ABL, 1, true><<<grid, kGbThreads, lds, s>>>(pp.p, none);
     return hipGetLastError();
+}
+
+// PLGPU_PART_RACC=0 (A/B only): no register accumulators (ablation 13)
+template <int NACC, int LIMBS>
+static hipError_t launch_part_fast(const Plan& pp, int grid, hipStream_t s) {
+    static const bool off = getenv("PLGPU_PART_RACC") && atoi(getenv("PLGPU_PART_RACC")) == 0;
+    if (LIMBS == 2 && off) return launch_part_fast_abl<NACC, LIMBS, 13>(pp, grid, s);
+    return launch_part_fast_abl<NACC, LIMBS, 0>(pp, grid, s);
 }
 
 template <int NACC>

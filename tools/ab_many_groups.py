@@ -23,7 +23,7 @@ import polaroid_amd as pl  # noqa: E402
 
 n = int(float(sys.argv[1])) if len(sys.argv) > 1 else int(1e9)
 modes = sys.argv[2:] or ["base", "PART_XCD=1"]
-KNOBS = ("PLGPU_PART_XCD", "PLGPU_PART_G", "PLGPU_PART_LDS_KB", "PLGPU_PART_WGS_PER_CU")
+KNOBS = ("PLGPU_PART_XCD", "PLGPU_PART_G", "PLGPU_PART_LDS_KB", "PLGPU_PART_WGS_PER_CU", "PLGPU_PART_RACC")
 
 
 def set_mode(m):
