@@ -73,6 +73,7 @@ enum : int {
     ST_FXFLAGS = 16,     // + acc: bit0 overflow, bit1 inexact
     ST_SHIFT_OVF = 14,   // merge: a shifted f64 sum state left the 192-bit range
     ST_MINEX = 17,       // + acc: 0x7FF - smallest exponent of a nonzero finite value (plan / maxexp)
+    ST_RUNS = 23,        // plan: sampled adjacent row pairs with equal keys (sorted / clustered keys)
     ST_WORDS = 24
 };
 
@@ -949,8 +950,11 @@ __global__ __launch_bounds__(kGbThreads) __attribute__((amdgpu_waves_per_eu(WPE)
     // it already holds there instead of in LDS.  Time-ordered keys put only
     // a few groups into a wave at a time, whose same-address LDS atomics
     // serialise (bank-conflict ratio 0.92 measured); ABL 13 turns it off.
-    constexpr bool RACC = PART && SUMONLY && LIMBS == 2 && ABL == 0;
-    constexpr int KR = RACC ? 4 : 1;
+    // ABL 14: the same with one accumulator in the single-table kernel,
+    // chosen by the plan for sorted / clustered keys (a frame sorted by
+    // symbol gives every lane long runs of one group).
+    constexpr bool RACC = SUMONLY && LIMBS == 2 && ((PART && ABL == 0) || (!PART && ABL == 14));
+    constexpr int KR = RACC ? (PART ? 4 : 1) : 1;
     int rs[KR];
     uint64_t rn[KR], rlo_[KR][NA], rhi_[KR][NA];
 #pragma unroll
@@ -1352,6 +1356,7 @@ __global__ __launch_bounds__(kPlanThreads) void gb_plan_kernel(GbParams p, uint6
         for (int i = threadIdx.x; i < kPlanSetSlots; i += blockDim.x) set[i] = kEmptyKey;
         __syncthreads();
         const int bits = __builtin_ctz(kPlanSetSlots);
+        unsigned long long runs = 0;  // samples whose next row holds the same key
         // kPlanBatch strided samples per thread are loaded before any is
         // inserted: one memory round trip per batch, not per sample
         for (int64_t i0 = s0 + threadIdx.x; i0 < s1; i0 += (int64_t)blockDim.x * kPlanBatch) {
@@ -1363,6 +1368,8 @@ __global__ __launch_bounds__(kPlanThreads) void gb_plan_kernel(GbParams p, uint6
             const int64_t r = plan_row(i, n, samples);
             okb[u] = i < s1 && r < n && dev_valid(p.key, r);
             kb[u] = okb[u] ? dev_load(p.key, r) : 0;
+            const bool nx = okb[u] && r + 1 < n && dev_valid(p.key, r + 1);
+            runs += (nx && dev_load(p.key, r + 1) == kb[u]) ? 1u : 0u;
           }
 #pragma unroll 1
           for (int u = 0; u < kPlanBatch; ++u) {
@@ -1403,6 +1410,7 @@ __global__ __launch_bounds__(kPlanThreads) void gb_plan_kernel(GbParams p, uint6
             }
           }
         }
+        if (runs) atomicAdd((unsigned long long*)&p.status[ST_RUNS], runs);
         return;
     }
     const AccSpec& ac = p.acc[a];
@@ -1752,6 +1760,7 @@ struct Plan {
     int fast_rows;     // rows per thread per tile in the fast kernel (2 / 4)
     int fast_threads;  // workgroup size of the fast kernel
     int fast_grid;
+    bool runs;         // sampled keys mostly equal their next row's (sorted / clustered input)
     mutable int launched_grid;  // grid of the last fast launch (info)
 };
 
@@ -1977,6 +1986,7 @@ static hipError_t launch_fast_rows(const Plan& pl, const DevProgram& dp, hipStre
 
 template <int NACC, int PRED, bool SUMONLY>
 static hipError_t launch_fast(const Plan& pl, const DevProgram& dp, hipStream_t s) {
+    if (SUMONLY && pl.limbs == 2 && pl.runs) return launch_fast_rows<NACC, PRED, SUMONLY, 2, 2, 14>(pl, dp, s);
     if (SUMONLY && pl.limbs == 2) return launch_fast_rows<NACC, PRED, SUMONLY, 2, 2>(pl, dp, s);
     return launch_fast_rows<NACC, PRED, SUMONLY, 2>(pl, dp, s);
 }
@@ -2185,6 +2195,9 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
     PLGPU_HIP(hipMemcpyAsync(R.st, R.status, sizeof R.st, hipMemcpyDeviceToHost, R.s));
     PLGPU_HIP(hipStreamSynchronize(R.s));
     R.st[ST_SAMPLED] = (uint64_t)std::min<int64_t>(n, kPlanSamples);
+    // sorted / clustered keys: the fused kernel's lanes keep a register
+    // accumulator (PLGPU_RUNS=0/1 forces the choice, A/B only)
+    pl.runs = getenv("PLGPU_RUNS") ? atoi(getenv("PLGPU_RUNS")) != 0 : R.st[ST_RUNS] * 2 > R.st[ST_SAMPLED];
     for (int a = 0; a < kMaxAcc; ++a) R.hb[a] = a < p.nacc ? plan_bottom(R.st[ST_MAXEX + a]) : 0;
     if (fixed)
         for (int a = 0; a < kMaxAcc; ++a) R.hb[a] = fixed[a];

@@ -553,3 +553,35 @@ def test_sum_wide_with_program_predicate(gpu):
     key = rng.integers(0, 30, n).astype(np.int64)
     mk, names, prog = PREDICATES["program"]
     _check_group_by(cols, key, None, [("sum", "a"), ("mean", "a"), ("len", "a")], mk(), prog, names, False)
+
+
+@pytest.mark.parametrize("layout", ["sorted", "runs_forced_random", "sorted_specials", "sorted_part"])
+def test_group_by_register_accumulators(gpu, layout, monkeypatch):
+    """Sorted / clustered keys: the plan sees adjacent equal keys and the
+    fused kernel's lanes sum rows of a group they already hold in a register
+    accumulator (flushed into the LDS table on a group change and at the
+    end); PLGPU_RUNS=1 forces that variant on random keys, specials mix its
+    rows with the per-row path, and "sorted_part" runs the partitioned
+    kernel's 4-slot form on sorted many-groups keys.  Exact vs the oracle."""
+    rng = np.random.default_rng(len(layout) + 77)
+    n = 3_000_017
+    card = 30_000 if layout == "sorted_part" else 100
+    a = rng.uniform(10, 500, n)
+    d = rng.uniform(1, 5, n) * rng.choice([-1.0, 1.0], n)
+    if layout == "sorted_specials":
+        a[rng.random(n) < 0.001] = np.nan
+        a[rng.random(n) < 0.0005] = np.inf
+        d[rng.random(n) < 0.001] = -0.0
+    key = rng.integers(0, card, n).astype(np.int64) * 7919 - 3
+    if layout == "runs_forced_random":
+        monkeypatch.setenv("PLGPU_RUNS", "1")
+    else:
+        key = np.sort(key)
+    cols = {"a": (a, None), "d": (d, None)}
+    aggs = [("sum", "a"), ("sum", "d"), ("mean", "a")]
+    info = {}
+    mk, names, prog = PREDICATES["simple_f64"]
+    _check_group_by(cols, key, None, aggs, mk(), prog, names, False, info)
+    assert info["sum_limbs"] == 2, info
+    if layout == "sorted_part":
+        assert info["path"] == 3, info
