@@ -12,8 +12,11 @@ import bench  # noqa: E402
 import polaroid_amd as pl  # noqa: E402
 
 n = int(float(sys.argv[1])) if len(sys.argv) > 1 else int(1e9)
+mixed = len(sys.argv) > 2 and sys.argv[2] == "mixed"  # min / max / count next to sums
 sym, cols = bench.make_data(torch, n, 100, seed=1234)
 aggs = [pl.col(k).sum() for k in ("open", "high", "low", "close")]
+if mixed:
+    aggs = [pl.col("open").sum(), pl.col("high").max(), pl.col("low").min(), pl.col("close").count()]
 for order in ("random", "sorted"):
     if order == "sorted":
         perm = torch.sort(sym, stable=True).indices
@@ -30,4 +33,4 @@ for order in ("random", "sorted"):
         out = q.collect(info=info)
         torch.cuda.synchronize()
         res.append(((time.perf_counter() - t0) * 1e3, info["main_kernel_ms"]))
-    print(order, "total / kernel ms:", [(round(a, 2), round(b, 2)) for a, b in res[1:]], "groups", out.height, flush=True)
+    print(order, "mixed" if mixed else "sums", "total / kernel ms:", [(round(a, 2), round(b, 2)) for a, b in res[1:]], "groups", out.height, flush=True)
