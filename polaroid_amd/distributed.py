@@ -379,15 +379,33 @@ def _group_by_var(df, key, aggs: Sequence[Expr], predicate, group, info: dict | 
       4. the second result aligned to the first on the key, then
          plgpu_var_finalize (null when count <= ddof; sqrt for std)."""
     from .expr import col
-    from .frame import DataFrame, Series, _agg_base, _eval, _join
+    from .frame import DataFrame, Series, String, _agg_base, _eval, _join, _lower_strings
 
     keys = [key] if isinstance(key, str) else list(key)
     key = keys[0] if len(keys) == 1 else tuple(keys)
+    str_keys = []
     for k in keys:
         if k not in df.columns:
             raise N.ComputeError(f'unable to find column "{k}"')
-        if df[k]._col.dtype not in _TORCH_WIRE:
-            raise N.InvalidOperationError("multi-GPU var / std take integer / Float64 / Boolean key columns")
+        if df[k].dtype is String and len(keys) == 1:
+            str_keys.append(k)
+        elif df[k]._col.dtype not in _TORCH_WIRE:
+            raise N.InvalidOperationError("multi-GPU var / std take numeric / Boolean keys or one short String key")
+    if str_keys:
+        # a short String key runs as its exact Int64 codes (the means cross
+        # the all-gather as integers) and is decoded at the end
+        if predicate is not None:
+            predicate, df = _lower_strings(predicate, df)
+        codes = N.Column()
+        short = C.c_int32(0)
+        N.check(N.lib().plgpu_str_encode_short(C.byref(df[key]._col), C.byref(codes), C.byref(short), None))
+        if _allreduce_max([0 if short.value else 1], group, _device_for(group))[0]:
+            raise N.InvalidOperationError("the multi-GPU group-by takes String keys of at most 7 bytes")
+        df = DataFrame([Series._from_native(key, codes) if nm == key else df[nm] for nm in df.columns])
+        out = _group_by_var(df, key, aggs, predicate, group, info)
+        strs = N.Column()
+        N.check(N.lib().plgpu_str_decode_short(C.byref(out[key]._col), C.byref(strs), None))
+        return DataFrame([Series._from_native(key, strs) if nm == key else out[nm] for nm in out.columns])
     var_cols: list[str] = []
     plain: list[Expr] = []
     for e in aggs:

@@ -483,7 +483,9 @@ def test_group_by_agg_world1_rccl_var_std(gpu):
                            "d": pl.Series.from_numpy("d", *cols["d"])})
         exprs = [pl.col("d").var().alias("vd"), pl.col("b").std().alias("sb"), pl.col("d").sum().alias("s"),
                  pl.col("b").var(ddof=0).alias("vb0")]
-        for key in ("k", ("k", "j")):
+        sym = np.array(["AAPL", "MSFT", "", "BRK.B", "x"], dtype=object)[rng.integers(0, 5, n)]
+        df = pl.DataFrame([df[c] for c in df.columns] + [pl.Series.from_numpy("sym", sym, rng.random(n) > 0.02)])
+        for key in ("k", ("k", "j"), "sym"):
             by = (key,) if isinstance(key, str) else key
             out = D.group_by_agg(df, key, exprs, pl.col("d") > -4.0)
             ref = df.lazy().filter(pl.col("d") > -4.0).group_by(*by).agg(*exprs).collect()
