@@ -209,6 +209,24 @@ int plgpu_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream);
 int plgpu_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream);
 int plgpu_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream);
 
+/* Test hooks and diagnostics, each read once from the environment variable
+ * PLGPU_<NAME> (upper case) when the library loads and settable here:
+ *   "debug"       per-attempt group-by diagnostics on stderr
+ *   "no_pack"     multi-key operators hash their key tuples even when the
+ *                 tuples would pack into one Int64 (exercises the hashed path)
+ *   "mk_collide"  a 3-bit first tuple hash (forces the collision / re-seed path)
+ *   "runs"        -1: the plan decides; 0 / 1 force the sorted-key variant of
+ *                 the fused group-by kernel
+ * An unknown name is PLGPU_ERR_INVALID. */
+int plgpu_set_option(const char* name, int64_t value);
+int plgpu_get_option(const char* name, int64_t* out);
+
+/* Checked build only (make CHECKS=1, libpolaroid_gpu_checked.so): the bits of
+ * the group-by kernels' index invariants violated since the last call (the
+ * violating accesses were skipped), then cleared.  Always 0 in the product
+ * build. */
+int plgpu_debug_checks(uint32_t* out);
+
 /* Release a library-produced column (no-op for borrowed ones). */
 void plgpu_column_release(plgpu_column* col);
 
@@ -226,9 +244,10 @@ void plgpu_column_release(plgpu_column* col);
  *   validity  Arrow buffers[0] or NULL (all valid; required NULL when dst has
  *             no validity)
  *   str_data  Arrow buffers[2] of a PLGPU_STR chunk
- * Copies go through pinned staging buffers, asynchronously on `stream`; bits
- * at any offset are placed by a device kernel.  The host buffers may be
- * reused on return; the device data is complete after plgpu_synchronize. */
+ * Copies are the runtime's staged copies of the pageable buffers,
+ * asynchronously on `stream`; bits at any offset are placed by a device
+ * kernel.  The host buffers may be reused on return; the device data is
+ * complete after plgpu_synchronize. */
 int plgpu_column_alloc(int32_t dtype, int64_t length, int32_t with_validity, int64_t str_bytes,
                        plgpu_column* out, void* stream);
 int plgpu_ingest_chunk(plgpu_column* dst, int64_t dst_row, int64_t dst_byte, const void* values,

@@ -10,7 +10,9 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpolaroid_gpu.so")
+# PLGPU_LIB: another build of the library (the checked build of
+# `make CHECKS=1`, libpolaroid_gpu_checked.so), for debugging runs only
+LIB_PATH = os.environ.get("PLGPU_LIB") or os.path.join(_HERE, "libpolaroid_gpu.so")
 
 # dtypes (enum plgpu_dtype)
 BOOL, I32, I64, F64, U32, STR = 1, 2, 3, 4, 5, 6
@@ -93,6 +95,9 @@ _COLP = C.POINTER(Column)
 SIGNATURES = {
     "plgpu_abi_version": (C.c_int, []),
     "plgpu_last_error": (C.c_char_p, []),
+    "plgpu_set_option": (C.c_int, [C.c_char_p, C.c_int64]),
+    "plgpu_get_option": (C.c_int, [C.c_char_p, C.POINTER(C.c_int64)]),
+    "plgpu_debug_checks": (C.c_int, [C.POINTER(C.c_uint32)]),
     "plgpu_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "plgpu_set_device": (C.c_int, [C.c_int]),
     "plgpu_synchronize": (C.c_int, [_P]),
@@ -246,6 +251,30 @@ def check(rc: int) -> None:
     if rc != OK:
         msg = lib().plgpu_last_error().decode(errors="replace")
         raise _ERRMAP.get(rc, PolaroidError)(msg)
+
+
+def set_option(name: str, value: int) -> int:
+    """Set a library option (test hooks / diagnostics, include/polaroid_gpu.h
+    plgpu_set_option); returns the previous value."""
+    prev = C.c_int64(0)
+    check(lib().plgpu_get_option(name.encode(), C.byref(prev)))
+    check(lib().plgpu_set_option(name.encode(), int(value)))
+    return int(prev.value)
+
+
+class option:
+    """Context manager: `with option("no_pack", 1): ...` restores the value."""
+
+    def __init__(self, name: str, value: int):
+        self.name, self.value, self.prev = name, int(value), None
+
+    def __enter__(self):
+        self.prev = set_option(self.name, self.value)
+        return self
+
+    def __exit__(self, *exc):
+        set_option(self.name, self.prev)
+        return False
 
 
 def device_count() -> int:

@@ -98,7 +98,7 @@ struct GbParams {
     int64_t n;
     int64_t row_begin;            // generic kernel: first row it owns
     int64_t n_full;               // fast kernel: rows [0, n_full), a multiple of its tile
-    int32_t ablate;               // timing experiments only (PLGPU_ABLATE); 0 in production
+    int32_t _pad1;
     int32_t _pad2;
     int32_t nacc;
     int32_t nfields;
@@ -126,6 +126,33 @@ struct GbParams {
     int32_t part_blocks;
     int32_t _pad3;
 };
+
+// ------------------------------------------------------ invariant checks
+// Checked build (make CHECKS=1: -DPLGPU_CHECKS, libpolaroid_gpu_checked.so):
+// a violated index invariant sets its bit in g_gb_checks and the access is
+// skipped, never performed; plgpu_debug_checks returns and clears the bits.
+// The product build compiles every check away (gb_ok is constant true).
+enum : uint32_t {
+    CK_LDS_SLOT = 1,      // LDS table slot outside [0, lcap + 2)
+    CK_GLOBAL_SLOT = 2,   // global table slot outside [0, gcap + 2)
+    CK_FAST_SLOT = 4,     // fused kernel LDS slot outside [0, lcap + 2)
+    CK_FIRST_ROW = 8,     // first / last row id outside [0, n)
+    CK_MERGE_SLOT = 16,   // merge slot outside the table
+    CK_REP_ROW = 32,      // multi-key representative row outside [0, n)
+    CK_VERIFY_SLOT = 64,  // multi-key verify slot outside the table
+    CK_PART_POS = 128,    // partition scatter position outside the buffers
+    CK_KEY_ROW = 256,     // multi-key output key row outside [0, n)
+    CK_PERM = 512         // group-order permutation entry outside [0, groups)
+};
+#ifdef PLGPU_CHECKS
+__device__ unsigned int g_gb_checks;
+__device__ __forceinline__ bool gb_ok(bool c, uint32_t bit) {
+    if (!c) atomicOr(&g_gb_checks, bit);
+    return c;
+}
+#else
+__device__ __forceinline__ constexpr bool gb_ok(bool, uint32_t) { return true; }
+#endif
 
 // ------------------------------------------------------------ helpers
 __device__ __forceinline__ uint64_t lds_load(uint64_t* p) {
@@ -283,6 +310,7 @@ __device__ __forceinline__ void apply_row(const GbParams& p, uint64_t* lds, int 
         if (LDS) return (unsigned long long*)&lds[f * L + s];
         return (unsigned long long*)gfield(p, f, s);
     };
+    if (!gb_ok(s >= 0 && s < (LDS ? (int64_t)L : p.gcap + 2), LDS ? CK_LDS_SLOT : CK_GLOBAL_SLOT)) return;
     atomicAdd(F(p.f_len), 1ull);
     if (p.f_first >= 0) atomicMin(F(p.f_first), (unsigned long long)row);
     if (p.f_last >= 0) atomicMax(F(p.f_last), (unsigned long long)row);
@@ -670,6 +698,7 @@ struct PartOut {
     uint64_t* key;
     uint64_t* acc[kMaxAcc];
     uint32_t* rows;  // null unless the first-row field is in use
+    int64_t cap;     // rows each buffer holds
 };
 
 // Pass 2: per tile of 2048 rows, the selected rows are ranked by partition in
@@ -812,6 +841,7 @@ __global__ __launch_bounds__(kPartThreads) void gb_part_scatter_kernel(GbParams 
             for (uint32_t t = threadIdx.x; t < m; t += blockDim.x) {
                 const uint32_t q = spart[t];
                 const uint64_t pos = gcur[q] + (t - lstart[q]);
+                if (!gb_ok(pos < (uint64_t)o.cap, CK_PART_POS)) continue;
                 if (dst) dst[pos] = sval[t];
                 else o.rows[pos] = (uint32_t)sval[t];
             }
@@ -848,6 +878,25 @@ template <bool NT>
 __device__ __forceinline__ u64x2_t ld16(const uint64_t* p) {
     if (NT) return __builtin_nontemporal_load(reinterpret_cast<const u64x2_t*>(p));
     return *reinterpret_cast<const u64x2_t*>(p);
+}
+
+// The rows after the last full tile (fewer than one tile): one more, masked
+// tile of guarded single-row loads (rows >= n read as 0 and are not
+// selected), so the fused kernel covers every row in one launch.
+template <int NACC, int PRED, int ROWS>
+__device__ __forceinline__ void fast_load_tail(const GbParams& p, int64_t t, FastTile<NACC, ROWS>& x) {
+    const int T = blockDim.x;
+    const uint64_t* kp = (const uint64_t*)p.key.values + p.key.offset;
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
+        const int64_t r = fast_row(t, T, ROWS, j);
+        const bool in = r < p.n;
+        x.key[j] = in ? kp[r] : 0ull;
+#pragma unroll
+        for (int c = 0; c < NACC; ++c)
+            x.v[c][j] = in ? ((const uint64_t*)p.acc[c].c.values + p.acc[c].c.offset)[r] : 0ull;
+        if (PRED == 1 && p.pred_acc < 0) x.pv[j] = in ? ((const uint64_t*)p.pred_col.values + p.pred_col.offset)[r] : 0ull;
+    }
 }
 
 // rbase: first row of tile 0 (even); rmax >= 0: row pairs beyond it are
@@ -890,19 +939,19 @@ __device__ __forceinline__ void fast_load(const GbParams& p, int64_t t, FastTile
 // and the host reruns with 3 limbs, so results never depend on the choice.
 // The two limbs land in fields (3+4a, 4+4a): the 3-limb representation with
 // a zero low limb, so the flush and finalize are unchanged.
-// ABL (timing ablations, never dispatched in production): 1 no atomics,
-// 2 len atomic only, 3 limb conversion without limb atomics, 5 no
-// prefetch, 11 default-policy (not non-temporal) loads.
-// WPE: minimum waves per SIMD the register allocation must allow (1 = no
-// constraint); 6 caps VGPRs at 80, i.e. three 512-thread workgroups per CU.
+// RUNS (sum-only, 2 limbs): per-lane register accumulators for sorted /
+// clustered keys (below).
 // PART: the workgroups aggregate the partition buffers of the many-groups
 // path (gb_partition): workgroup b takes its share of partition
 // b / part_blocks (rows [part_range[q], part_range[q + 1]), already
 // selected, so PRED is 0) with an LDS table of lcap slots for that
 // partition's groups.
-template <int NACC, int PRED, bool SUMONLY, int ROWS, int LIMBS = 3, int ABL = 0, int WPE = 1, bool PART = false>
-__global__ __launch_bounds__(kGbThreads) __attribute__((amdgpu_waves_per_eu(WPE))) void gb_fast_kernel(
-    GbParams p, DevProgram prog) {
+// Without PART the launch covers every row: the full tiles, then the rows
+// after the last full tile as one masked tile (fast_load_tail).
+// (Measured and removed variants -- no prefetch, default-policy loads,
+// 80-VGPR caps, 4 rows per thread -- are logged in DESIGN.md.)
+template <int NACC, int PRED, bool SUMONLY, int ROWS, int LIMBS = 3, bool RUNS = false, bool PART = false>
+__global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProgram prog) {
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
     constexpr int NA = NACC > 0 ? NACC : 1;
     // SLIM (sum-only, 2 limbs): LDS fields key 0, len 1, acc a: limbs
@@ -929,9 +978,9 @@ __global__ __launch_bounds__(kGbThreads) __attribute__((amdgpu_waves_per_eu(WPE)
 
     const int T = blockDim.x;
     // the tile stream is read once: non-temporal loads (6.60 vs 6.84 ms at
-    // 1e9 rows, tools/ablate.py; ablation 11 = default-policy loads)
-    constexpr bool NTL = ABL != 11;
+    // 1e9 rows with default-policy loads, tools/ablate.py)
     int64_t ntiles = p.n_full / ((int64_t)T * ROWS);
+    int64_t nall = ntiles + (p.n > p.n_full ? 1 : 0);  // + the masked tail tile
     int64_t t = blockIdx.x, tstep = gridDim.x;
     int64_t rbase = 0, rlo = 0, rhi = 0, rmax = -1;
     if (PART) {
@@ -941,19 +990,24 @@ __global__ __launch_bounds__(kGbThreads) __attribute__((amdgpu_waves_per_eu(WPE)
         rbase = rlo & ~int64_t(1);
         rmax = p.n & ~int64_t(1);
         ntiles = (rhi - rbase + (int64_t)T * ROWS - 1) / ((int64_t)T * ROWS);
+        nall = ntiles;
         t = blockIdx.x % p.part_blocks;
         tstep = p.part_blocks;
     }
+    auto load_tile = [&](int64_t tt, FastTile<NACC, ROWS>& x) {
+        if (PART || tt < ntiles) fast_load<NACC, PRED, ROWS, true>(p, tt, x, rbase, rmax);
+        else fast_load_tail<NACC, PRED, ROWS>(p, tt, x);
+    };
     constexpr uint32_t VM = (1u << NACC) - 1u;
     // RACC (partition buffers, sum-only, 2 limbs): each lane keeps KR
     // register accumulators {slot, len, limbs} and adds a row whose group
     // it already holds there instead of in LDS.  Time-ordered keys put only
     // a few groups into a wave at a time, whose same-address LDS atomics
-    // serialise (bank-conflict ratio 0.92 measured); ABL 13 turns it off.
-    // ABL 14: the same with one accumulator in the single-table kernel,
-    // chosen by the plan for sorted / clustered keys (a frame sorted by
-    // symbol gives every lane long runs of one group).
-    constexpr bool RACC = SUMONLY && LIMBS == 2 && ((PART && ABL == 0) || (!PART && ABL == 14));
+    // serialise (bank-conflict ratio 0.92 measured).  RUNS: the same with
+    // one accumulator in the single-table kernel, chosen by the plan for
+    // sorted / clustered keys (a frame sorted by symbol gives every lane
+    // long runs of one group).
+    constexpr bool RACC = SUMONLY && LIMBS == 2 && (PART || RUNS);
     constexpr int KR = RACC ? (PART ? 4 : 1) : 1;
     int rs[KR];
     uint64_t rn[KR], rlo_[KR][NA], rhi_[KR][NA];
@@ -977,9 +1031,8 @@ __global__ __launch_bounds__(kGbThreads) __attribute__((amdgpu_waves_per_eu(WPE)
         rs[k] = -1;
     };
     FastTile<NACC, ROWS> cur;
-    if (ABL != 5 && t < ntiles) fast_load<NACC, PRED, ROWS, NTL>(p, t, cur, rbase, rmax);
-    for (; t < ntiles; t += tstep) {
-        if (ABL == 5) fast_load<NACC, PRED, ROWS>(p, t, cur, rbase, rmax);  // ablation: no prefetch
+    if (t < nall) load_tile(t, cur);
+    for (; t < nall; t += tstep) {
         // ---- predicate + batched LDS probes of the tile's rows
         int slot[ROWS];
         uint64_t probe[ROWS];
@@ -997,6 +1050,8 @@ __global__ __launch_bounds__(kGbThreads) __attribute__((amdgpu_waves_per_eu(WPE)
             if (PART) {
                 const int64_t r = rbase + fast_row(t, T, ROWS, j);
                 sel = r >= rlo && r < rhi;
+            } else if (t >= ntiles) {
+                sel = sel && fast_row(t, T, ROWS, j) < p.n;
             }
             slot[j] = sel ? (cur.key[j] == kEmptyKey ? p.lcap + 1 : kGlobalKey) : kNotSelected;
             h[j] = hash_slot(cur.key[j], p.lbits);
@@ -1008,7 +1063,7 @@ __global__ __launch_bounds__(kGbThreads) __attribute__((amdgpu_waves_per_eu(WPE)
         // ---- next tile's loads go out before this tile's atomics
         FastTile<NACC, ROWS> nxt;
         const int64_t tn = t + tstep;
-        if (ABL != 5 && tn < ntiles) fast_load<NACC, PRED, ROWS, NTL>(p, tn, nxt, rbase, rmax);
+        if (tn < nall) load_tile(tn, nxt);
         // ---- apply rows one at a time (rolled; arrays shift statically)
 #pragma unroll 1
         for (int j = 0; j < ROWS; ++j) {
@@ -1025,6 +1080,7 @@ __global__ __launch_bounds__(kGbThreads) __attribute__((amdgpu_waves_per_eu(WPE)
                     bot[a] = bot0[a];
                 }
                 if (s == kGlobalKey) s = lds_find(lds, p.lbits, p.lcap, cur.key[0]);
+                if (s >= 0 && !gb_ok(s < L, CK_FAST_SLOT)) s = -1;
                 bool held = false;
                 if (RACC && s >= 0) {
                     uint64_t lo[NA], hi[NA];
@@ -1077,27 +1133,17 @@ __global__ __launch_bounds__(kGbThreads) __attribute__((amdgpu_waves_per_eu(WPE)
                 if (held) {
                 } else if (SUMONLY && s >= 0) {
                     unsigned long long* q = (unsigned long long*)&lds[s];
-                    if (ABL == 1) {
-#pragma unroll
-                        for (int a = 0; a < NACC; ++a) d.special ^= (uint32_t)rv[a] & 0x80000000u;
-                    } else {
-                        atomicAdd(q + L, 1ull);
-                    }
+                    atomicAdd(q + L, 1ull);
                     uint32_t slow = 0;
 #pragma unroll
                     for (int a = 0; a < NACC; ++a) {
-                        if (ABL == 1 || ABL == 2) break;
                         uint64_t l0, l1, l2;
                         const bool ok = fx_limbs_fast<LIMBS>(rv[a], bot[a], l0, l1, l2);
                         slow |= (ok ? 0u : 1u) << a;
-                        if (ABL == 3) {
-                            d.special ^= (uint32_t)(l0 ^ l1 ^ l2) & 0x80000000u;
-                        } else {
-                            // zero limbs (slow lanes, zero values) add nothing
-                            if (LIMBS == 3) atomicAdd(q + (2 + 4 * a) * L, (unsigned long long)l0);
-                            atomicAdd(q + so_mid(a) * L, (unsigned long long)(LIMBS == 3 ? l1 : l0));
-                            atomicAdd(q + so_top(a) * L, (unsigned long long)(LIMBS == 3 ? l2 : l1));
-                        }
+                        // zero limbs (slow lanes, zero values) add nothing
+                        if (LIMBS == 3) atomicAdd(q + (2 + 4 * a) * L, (unsigned long long)l0);
+                        atomicAdd(q + so_mid(a) * L, (unsigned long long)(LIMBS == 3 ? l1 : l0));
+                        atomicAdd(q + so_top(a) * L, (unsigned long long)(LIMBS == 3 ? l2 : l1));
                     }
                     if (slow) {
                         // inf / NaN flags, rounding below the window, overflow
@@ -1141,7 +1187,7 @@ __global__ __launch_bounds__(kGbThreads) __attribute__((amdgpu_waves_per_eu(WPE)
                 for (int a = 0; a < NACC; ++a) cur.v[a][i] = cur.v[a][i + 1];
             }
         }
-        if (ABL != 5) cur = nxt;
+        cur = nxt;
     }
     if (RACC) {
 #pragma unroll
@@ -1569,6 +1615,10 @@ __global__ void gb_finalize_kernel(GbParams p, FinParams fp) {
                 // the value (null included) of the group's first / last
                 // selected row (polars-expr/src/reduce/first_last.rs)
                 const int64_t row = (int64_t)*gfield(p, os.kind == PLGPU_AGG_FIRST ? p.f_first : p.f_last, s);
+                if (!gb_ok(row >= 0 && row < p.n, CK_FIRST_ROW)) {
+                    valid = false;
+                    break;
+                }
                 valid = dev_valid(ac.c, row);
                 const uint64_t v = valid ? dev_load(ac.c, row) : 0ull;
                 dev_store(os.values, os.out_dtype, g, v);
@@ -1586,7 +1636,7 @@ template <typename T>
 __global__ void gather_kernel(const T* __restrict__ src, const int64_t* __restrict__ perm, T* __restrict__ dst,
                               int64_t n) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        dst[i] = src[perm[i]];
+        if (gb_ok(perm[i] >= 0 && perm[i] < n, CK_PERM)) dst[i] = src[perm[i]];
 }
 __global__ void narrow_i64_kernel(const int64_t* __restrict__ a, void* __restrict__ b, int32_t dt, int64_t n) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -1699,6 +1749,7 @@ __global__ void gb_merge_kernel(GbParams p, const uint64_t* __restrict__ rec, in
             atomicAdd((unsigned long long*)&p.status[ST_TABLE_FULL], 1ull);
             continue;
         }
+        if (!gb_ok(gs < p.gcap + 2, CK_MERGE_SLOT)) continue;
         for (int f = 1; f < p.nfields; ++f) {
             const uint64_t v = r[1 + f];
             unsigned long long* q = (unsigned long long*)gfield(p, f, gs);
@@ -1756,9 +1807,6 @@ struct Plan {
     bool use_lds;
     bool sum_only;
     int limbs;         // SUMONLY: 40-bit LDS limbs per f64 sum (3, or 2 for narrow exponent spans)
-    int ablate;        // timing ablation variant (PLGPU_ABLATE; never set in production)
-    int fast_rows;     // rows per thread per tile in the fast kernel (2 / 4)
-    int fast_threads;  // workgroup size of the fast kernel
     int fast_grid;
     bool runs;         // sampled keys mostly equal their next row's (sorted / clustered input)
     mutable int launched_grid;  // grid of the last fast launch (info)
@@ -1959,9 +2007,10 @@ static int resident_per_cu(const void* kern, int threads, size_t lds) {
     return nb;
 }
 
-template <int NACC, int PRED, bool SUMONLY, int ROWS, int LIMBS = 3, int ABL = 0, int WPE = 1>
+template <int NACC, int PRED, bool SUMONLY, int LIMBS = 3, bool RUNS = false>
 static hipError_t launch_fast_rows(const Plan& pl, const DevProgram& dp, hipStream_t s) {
-    const void* kern = (const void*)gb_fast_kernel<NACC, PRED, SUMONLY, ROWS, LIMBS, ABL, WPE>;
+    constexpr int ROWS = 2;
+    const void* kern = (const void*)gb_fast_kernel<NACC, PRED, SUMONLY, ROWS, LIMBS, RUNS>;
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -1969,51 +2018,28 @@ static hipError_t launch_fast_rows(const Plan& pl, const DevProgram& dp, hipStre
     }
     const size_t lds = (SUMONLY && LIMBS == 2) ? (size_t)(2 + 3 * NACC) * (pl.p.lcap + 2) * 8 : pl.lds_bytes;
     // kGridRounds rounds of the workgroups resident per CU: later rounds'
-    // table init / flush overlap earlier rounds' streaming (PLGPU_OCC_GRID=k
-    // overrides the round count for tuning)
-    const char* e = getenv("PLGPU_OCC_GRID");
-    const int rounds = e ? std::max(1, atoi(e)) : kGridRounds;
+    // table init / flush overlap earlier rounds' streaming
     const int64_t need = (pl.p.n_full + kMaxRowsPerWg - 1) / kMaxRowsPerWg;
-    int64_t g = (int64_t)num_cus() * resident_per_cu(kern, pl.fast_threads, lds) * rounds;
+    int64_t g = (int64_t)num_cus() * resident_per_cu(kern, kGbThreads, lds) * kGridRounds;
     if (g < need) g = need;
-    const int64_t useful = pl.p.n_full / ((int64_t)pl.fast_threads * ROWS);
+    const int64_t useful = pl.p.n_full / ((int64_t)kGbThreads * ROWS);
     if (g > useful) g = std::max<int64_t>(1, useful);
     const int grid = (int)g;
     pl.launched_grid = grid;
-    gb_fast_kernel<NACC, PRED, SUMONLY, ROWS, LIMBS, ABL, WPE><<<grid, pl.fast_threads, lds, s>>>(pl.p, dp);
+    gb_fast_kernel<NACC, PRED, SUMONLY, ROWS, LIMBS, RUNS><<<grid, kGbThreads, lds, s>>>(pl.p, dp);
     return hipGetLastError();
 }
 
 template <int NACC, int PRED, bool SUMONLY>
 static hipError_t launch_fast(const Plan& pl, const DevProgram& dp, hipStream_t s) {
-    if (SUMONLY && pl.limbs == 2 && pl.runs) return launch_fast_rows<NACC, PRED, SUMONLY, 2, 2, 14>(pl, dp, s);
-    if (SUMONLY && pl.limbs == 2) return launch_fast_rows<NACC, PRED, SUMONLY, 2, 2>(pl, dp, s);
-    return launch_fast_rows<NACC, PRED, SUMONLY, 2>(pl, dp, s);
-}
-
-// Ablations of the headline configuration only (tools/ablate.py).
-static hipError_t launch_ablation(const Plan& pl, const DevProgram& dp, hipStream_t s) {
-    switch (pl.ablate) {
-    case 1: return launch_fast_rows<4, 1, true, 2, 3, 1>(pl, dp, s);
-    case 2: return launch_fast_rows<4, 1, true, 2, 3, 2>(pl, dp, s);
-    case 3: return launch_fast_rows<4, 1, true, 2, 3, 3>(pl, dp, s);
-    case 4: return launch_fast_rows<4, 1, true, 2, 2, 3>(pl, dp, s);
-    case 5: return launch_fast_rows<4, 1, true, 2, 3, 0, 6>(pl, dp, s);
-    case 6: return launch_fast_rows<4, 1, true, 2, 2, 0, 6>(pl, dp, s);
-    case 7: return launch_fast_rows<4, 1, true, 2, 2, 0>(pl, dp, s);
-    case 8: return launch_fast_rows<4, 1, true, 2, 2, 5>(pl, dp, s);
-    case 9: return launch_fast_rows<4, 1, true, 4, 2, 5>(pl, dp, s);
-    case 11: return launch_fast_rows<4, 1, true, 2, 2, 11>(pl, dp, s);
-    default: return launch_fast_rows<4, 1, true, 2, 3, 0>(pl, dp, s);
-    }
+    if (SUMONLY && pl.limbs == 2 && pl.runs) return launch_fast_rows<NACC, PRED, SUMONLY, 2, true>(pl, dp, s);
+    if (SUMONLY && pl.limbs == 2) return launch_fast_rows<NACC, PRED, SUMONLY, 2>(pl, dp, s);
+    return launch_fast_rows<NACC, PRED, SUMONLY>(pl, dp, s);
 }
 
 template <int NACC>
 static hipError_t launch_fast_nacc(const Plan& pl, const DevProgram& dp, int pred, hipStream_t s) {
-    if (pl.sum_only) {
-        if (NACC == 4 && pred == 1 && pl.ablate > 0) return launch_ablation(pl, dp, s);
-        return pred == 0 ? launch_fast<NACC, 0, true>(pl, dp, s) : launch_fast<NACC, 1, true>(pl, dp, s);
-    }
+    if (pl.sum_only) return pred == 0 ? launch_fast<NACC, 0, true>(pl, dp, s) : launch_fast<NACC, 1, true>(pl, dp, s);
     return pred == 0 ? launch_fast<NACC, 0, false>(pl, dp, s) : launch_fast<NACC, 1, false>(pl, dp, s);
 }
 
@@ -2196,14 +2222,13 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
     PLGPU_HIP(hipStreamSynchronize(R.s));
     R.st[ST_SAMPLED] = (uint64_t)std::min<int64_t>(n, kPlanSamples);
     // sorted / clustered keys: the fused kernel's lanes keep a register
-    // accumulator (PLGPU_RUNS=0/1 forces the choice, A/B only)
-    pl.runs = getenv("PLGPU_RUNS") ? atoi(getenv("PLGPU_RUNS")) != 0 : R.st[ST_RUNS] * 2 > R.st[ST_SAMPLED];
+    // accumulator (option "runs" = 0 / 1 forces the choice in tests)
+    pl.runs = options().runs >= 0 ? options().runs != 0 : R.st[ST_RUNS] * 2 > R.st[ST_SAMPLED];
     for (int a = 0; a < kMaxAcc; ++a) R.hb[a] = a < p.nacc ? plan_bottom(R.st[ST_MAXEX + a]) : 0;
     if (fixed)
         for (int a = 0; a < kMaxAcc; ++a) R.hb[a] = fixed[a];
     int64_t hll = -1;
-    if (R.st[ST_DISTINCT] >= (uint64_t)kPlanSetSlots / 2 && n > 4 * (int64_t)kPlanSamples &&
-        !getenv("PLGPU_NO_HLL")) {
+    if (R.st[ST_DISTINCT] >= (uint64_t)kPlanSetSlots / 2 && n > 4 * (int64_t)kPlanSamples) {
         uint32_t* regs = nullptr;
         std::vector<uint32_t> h(1 << kHllBits);
         int rc = dev_alloc((void**)&regs, h.size() * 4, R.s);
@@ -2230,12 +2255,7 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
     bool fast = pl.use_lds && R.pred != 2 && ok(p.key);
     for (int a = 0; a < p.nacc; ++a) fast = fast && ok(p.acc[a].c);
     if (R.pred == 1 && p.pred_acc < 0) fast = fast && ok(p.pred_col);
-    if (getenv("PLGPU_NO_FAST")) fast = false;
-    pl.ablate = getenv("PLGPU_ABLATE") ? atoi(getenv("PLGPU_ABLATE")) : 0;
-    pl.fast_rows = 2;
-    pl.fast_threads = getenv("PLGPU_FAST_THREADS") ? atoi(getenv("PLGPU_FAST_THREADS")) : 512;
-    if (pl.fast_threads != 256 && pl.fast_threads != 512) pl.fast_threads = 512;
-    const int64_t tile = (int64_t)pl.fast_rows * pl.fast_threads;
+    const int64_t tile = (int64_t)2 * kGbThreads;
     p.n_full = fast ? (n / tile) * tile : 0;
     {
         // as many workgroups as the LDS budget allows per CU (up to 8)
@@ -2255,11 +2275,11 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
         so = so && ac.isf && ac.flags == (A_FSUM | A_FLAGS) && ac.f_sum == 2 + 4 * a && ac.f_flags == 5 + 4 * a &&
              ac.f_cnt < 0;
     }
-    pl.sum_only = so && !getenv("PLGPU_NO_SUMONLY");
+    pl.sum_only = so;
     // two LDS limbs when every sampled nonzero value of every summed column
     // sits at least kLimb2Margin binades above the 2-limb window's bottom
     pl.limbs = 3;
-    if (pl.sum_only && !getenv("PLGPU_NO_LIMB2")) {
+    if (pl.sum_only) {
         bool two = true;
         for (int a = 0; a < p.nacc; ++a) {
             const int mn = 0x7FF - (int)R.st[ST_MINEX + a];
@@ -2267,13 +2287,15 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
         }
         if (two) pl.limbs = 2;
     }
-    p.row_begin = p.n_full;
+    // the fused kernel covers every row (its last tile is masked); below one
+    // tile, or off the fast path, the generic kernel takes them all
+    p.row_begin = p.n_full > 0 ? n : 0;
     // partitioned path: too many groups for one LDS table, but few enough
     // that 2^kPartMaxBits partitions of LDS tables hold them; key and
     // aggregated columns null-free (they are copied as raw words)
     R.part = false;
     if (!pl.use_lds && n >= (int64_t(1) << 20) && R.est_groups > 0 && p.key.validity == nullptr &&
-        !((p.f_first >= 0 || p.f_last >= 0) && n >= 0xFFFFFFFFll) && !getenv("PLGPU_NO_PART")) {
+        !((p.f_first >= 0 || p.f_last >= 0) && n >= 0xFFFFFFFFll)) {
         bool ok2 = true;
         for (int a = 0; a < p.nacc; ++a) ok2 = ok2 && p.acc[a].c.validity == nullptr;
         // LDS table of the partition workgroups: two per CU, or one when
@@ -2285,10 +2307,8 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
         const int fields = (pl.sum_only && pl.limbs == 2) ? 2 + 3 * p.nacc : p.nfields;
         // Fewer, larger partition tables first (160 KB, one workgroup per
         // CU): measured 2-7 % faster than 80 KB tables at 14k-100k groups
-        // (profiles/r02_ab_part.log).  PLGPU_PART_LDS_KB (A/B only): the
-        // first LDS budget tried.
-        const size_t first_kb = getenv("PLGPU_PART_LDS_KB") ? (size_t)atoi(getenv("PLGPU_PART_LDS_KB")) : 160;
-        for (size_t budget : {first_kb * 1024, (size_t)80 * 1024, (size_t)160 * 1024}) {
+        // (profiles/r02_ab_part.log)
+        for (size_t budget : {(size_t)160 * 1024, (size_t)80 * 1024}) {
             int lb = 13;
             while (lb > 6 && ((size_t)fields * ((1u << lb) + 2) * 8 > budget ||
                               (size_t)p.nfields * ((1u << lb) + 2) * 8 > (size_t)160 * 1024))
@@ -2314,7 +2334,7 @@ static int gb_partition(GbRun& R) {
     GbParams& p = R.pl.p;
     hipStream_t s = R.s;
     const int P = 1 << R.pbits;
-    const int G = getenv("PLGPU_PART_G") ? std::max(1, atoi(getenv("PLGPU_PART_G"))) : num_cus() * 8;
+    const int G = num_cus() * 8;
     const int64_t ncnt = (int64_t)P * G;
     uint32_t* cnt = nullptr;
     uint64_t* part = nullptr;
@@ -2360,6 +2380,7 @@ static int gb_partition(GbRun& R) {
     R.pout.key = R.pbuf;
     for (int a = 0; a < p.nacc; ++a) R.pout.acc[a] = R.pbuf + (size_t)rows * (1 + a);
     R.pout.rows = want_rows ? (uint32_t*)(R.pbuf + (size_t)rows * (1 + p.nacc)) : nullptr;
+    R.pout.cap = rows;
     if (f8 && R.pred == 0) gb_part_scatter_kernel<0, true><<<G, kPartThreads, 0, s>>>(p, R.dp, R.pbits, off, R.pout);
     else if (f8 && R.pred == 1) gb_part_scatter_kernel<1, true><<<G, kPartThreads, 0, s>>>(p, R.dp, R.pbits, off, R.pout);
     else switch (R.pred) {
@@ -2369,18 +2390,18 @@ static int gb_partition(GbRun& R) {
     }
     PLGPU_HIP(hipGetLastError());
     R.part_range = range;
-    // workgroups per partition: fill the chip, bound rows per workgroup
-    // PLGPU_PART_WGS_PER_CU (A/B only): workgroups per CU over all partitions
-    const int64_t wpc = getenv("PLGPU_PART_WGS_PER_CU") ? std::max(1, atoi(getenv("PLGPU_PART_WGS_PER_CU"))) : 4;
+    // workgroups per partition: fill the chip (4 per CU over all partitions,
+    // profiles/r02_ab_part.log), bound rows per workgroup
+    const int64_t wpc = 4;
     int nb = (int)std::max<int64_t>(1, (wpc * (int64_t)num_cus() + P - 1) / P);
     while ((int64_t)maxpart > (int64_t)nb * (kMaxRowsPerWg / 2)) nb *= 2;
     R.part_blocks = nb;
     return PLGPU_OK;
 }
 
-template <int NACC, int LIMBS, int ABL>
-static hipError_t launch_part_fast_abl(const Plan& pp, int grid, hipStream_t s) {
-    const void* kern = (const void*)gb_fast_kernel<NACC, 0, true, 2, LIMBS, ABL, 1, true>;
+template <int NACC, int LIMBS>
+static hipError_t launch_part_fast(const Plan& pp, int grid, hipStream_t s) {
+    const void* kern = (const void*)gb_fast_kernel<NACC, 0, true, 2, LIMBS, false, true>;
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -2389,16 +2410,8 @@ static hipError_t launch_part_fast_abl(const Plan& pp, int grid, hipStream_t s) 
     const size_t lds = (size_t)(LIMBS == 2 ? 2 + 3 * NACC : pp.p.nfields) * (pp.p.lcap + 2) * 8;
     DevProgram none;
     std::memset(&none, 0, sizeof none);
-    gb_fast_kernel<NACC, 0, true, 2, LIMBS, ABL, 1, true><<<grid, kGbThreads, lds, s>>>(pp.p, none);
+    gb_fast_kernel<NACC, 0, true, 2, LIMBS, false, true><<<grid, kGbThreads, lds, s>>>(pp.p, none);
     return hipGetLastError();
-}
-
-// PLGPU_PART_RACC=0 (A/B only): no register accumulators (ablation 13)
-template <int NACC, int LIMBS>
-static hipError_t launch_part_fast(const Plan& pp, int grid, hipStream_t s) {
-    static const bool off = getenv("PLGPU_PART_RACC") && atoi(getenv("PLGPU_PART_RACC")) == 0;
-    if (LIMBS == 2 && off) return launch_part_fast_abl<NACC, LIMBS, 13>(pp, grid, s);
-    return launch_part_fast_abl<NACC, LIMBS, 0>(pp, grid, s);
 }
 
 template <int NACC>
@@ -2534,7 +2547,7 @@ static int gb_main(GbRun& R, bool auto_refit, bool* refit, int32_t* hint) {
     Plan& pl = R.pl;
     GbParams& p = pl.p;
     const int64_t n = p.n;
-    const bool debug = getenv("PLGPU_DEBUG") != nullptr;
+    const bool debug = options().debug != 0;
     if (refit) *refit = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     PLGPU_HIP(hipEventCreate(&ev0));
@@ -2549,37 +2562,12 @@ static int gb_main(GbRun& R, bool auto_refit, bool* refit, int32_t* hint) {
         if (n > 0 && R.part) {
             PLGPU_HIP(launch_partitioned(R));
         } else if (n > 0) {
-            // the tail (< one tile of the fast kernel, or every row when the
-            // fast path does not apply) goes through the generic kernel; next
-            // to a fast launch it runs on a side stream, concurrently (its
-            // few workgroups took 28 us after the fast kernel otherwise)
-            const bool tail = p.row_begin < n;
-            hipStream_t ts = R.s;
-            hipEvent_t fork = nullptr, join = nullptr;
-            if (tail && p.n_full > 0 && (ts = side_stream()) != nullptr) {
-                PLGPU_HIP(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
-                PLGPU_HIP(hipEventCreateWithFlags(&join, hipEventDisableTiming));
-                PLGPU_HIP(hipEventRecord(fork, R.s));
-                PLGPU_HIP(hipStreamWaitEvent(ts, fork, 0));
+            // the fused kernel covers every row (its last tile masked); off
+            // the fast path, or below one tile, the generic kernel does
+            if (p.n_full > 0) {
+                PLGPU_HIP(launch_fast_dispatch(pl, R.dp, R.pred, R.s));
             } else {
-                ts = R.s;
-            }
-            if (p.n_full > 0) PLGPU_HIP(launch_fast_dispatch(pl, R.dp, R.pred, R.s));
-            if (tail) {
-                Plan tp = pl;
-                const int64_t rows = n - p.row_begin;
-                const int64_t g = (rows + 4 * kGbThreads - 1) / (4 * kGbThreads);
-                tp.grid = (int)std::min<int64_t>(pl.grid, g < 1 ? 1 : g);
-                PLGPU_HIP(launch_main_dispatch(tp, R.dp, R.pred, ts));
-            }
-            if (join) {
-                // (destroying a recorded event is deferred by the runtime
-                // until it completes)
-                const hipError_t e1 = hipEventRecord(join, ts);
-                const hipError_t e2 = e1 == hipSuccess ? hipStreamWaitEvent(R.s, join, 0) : e1;
-                (void)hipEventDestroy(fork);
-                (void)hipEventDestroy(join);
-                PLGPU_HIP(e2);
+                PLGPU_HIP(launch_main_dispatch(pl, R.dp, R.pred, R.s));
             }
         }
         PLGPU_HIP(hipEventRecord(ev1, R.s));
@@ -2866,6 +2854,7 @@ __global__ __launch_bounds__(256) void mk_rep_kernel(GbParams p, MkKeys k, uint6
     for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < total; s += (int64_t)gridDim.x * blockDim.x) {
         if (*gfield(p, p.f_len, s) == 0) continue;
         const int64_t rep = (int64_t)*gfield(p, p.f_first, s);
+        if (!gb_ok(rep >= 0 && rep < p.n, CK_REP_ROW)) continue;
         uint32_t m = 0;
         for (int i = 0; i < k.n; ++i) {
             const bool v = dev_valid(k.c[i], rep);
@@ -2887,7 +2876,7 @@ __global__ __launch_bounds__(256) void mk_verify_kernel(GbParams p, MkKeys k, co
     bool bad = false;
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
         const int64_t s = g_lookup(p, hashes[r]);
-        if (s < 0 || *gfield(p, p.f_len, s) == 0) continue;
+        if (s < 0 || !gb_ok(s < total, CK_VERIFY_SLOT) || *gfield(p, p.f_len, s) == 0) continue;
         const uint32_t m = vm[s];
         for (int i = 0; i < k.n; ++i) {
             const bool v = dev_valid(k.c[i], r);
@@ -2903,10 +2892,11 @@ __global__ __launch_bounds__(256) void mk_verify_kernel(GbParams p, MkKeys k, co
 }
 
 // out[g] = key column c at row rows[g] (validity bit-packed, zeroed first).
-__global__ void mk_gather_key_kernel(DevCol c, const uint64_t* __restrict__ rows, int64_t g_n, void* out,
+__global__ void mk_gather_key_kernel(DevCol c, const uint64_t* __restrict__ rows, int64_t g_n, int64_t n, void* out,
                                      uint32_t* out_valid) {
     for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < g_n; g += (int64_t)gridDim.x * blockDim.x) {
         const int64_t r = (int64_t)rows[g];
+        if (!gb_ok(r >= 0 && r < n, CK_KEY_ROW)) continue;
         const bool v = dev_valid(c, r);
         const uint64_t x = dev_load(c, r);
         if (c.dtype == PLGPU_BOOL) {
@@ -2936,6 +2926,20 @@ PLGPU_API int plgpu_group_by_agg(const plgpu_column* key, const plgpu_column* co
     if (rc) return rc;
     if (info) gb_fill_info(R, info);
     return gb_finalize(R, naggs, out_key, out_aggs);
+}
+
+PLGPU_API int plgpu_debug_checks(uint32_t* out) {
+    if (out == nullptr) return fail(PLGPU_ERR_INVALID, "NULL argument");
+    *out = 0;
+#ifdef PLGPU_CHECKS
+    PLGPU_HIP(hipDeviceSynchronize());
+    PLGPU_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_gb_checks), sizeof *out));
+    const uint32_t zero = 0;
+    PLGPU_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_gb_checks), &zero, sizeof zero));
+    return PLGPU_OK;
+#else
+    return PLGPU_OK;
+#endif
 }
 
 // ------------------------------------------------------- multi-GPU partials
@@ -3567,7 +3571,7 @@ PLGPU_API int plgpu_group_by_agg_multi(const plgpu_column* keys, int32_t nkeys, 
         const uint64_t seed = 0x243F6A8885A308D3ull * (uint64_t)(2 * attempt + 1);
         // PLGPU_MK_COLLIDE (tests only): a 3-bit first hash forces the
         // collision -> re-seed path
-        const uint64_t mask = attempt == 0 && getenv("PLGPU_MK_COLLIDE") ? 7ull : ~0ull;
+        const uint64_t mask = attempt == 0 && options().mk_collide ? 7ull : ~0ull;
         if (n > 0) mk_hash_kernel<<<std::max(hg, 1), 256, 0, s>>>(mk, n, seed, mask, hashes);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) { rc = hip_fail(e, "mk_hash_kernel"); break; }
@@ -3611,7 +3615,7 @@ PLGPU_API int plgpu_group_by_agg_multi(const plgpu_column* keys, int32_t nkeys, 
                 if (rc || groups == 0) continue;
                 if (keys[i].dtype == PLGPU_BOOL) (void)hipMemsetAsync((void*)out_keys[i].values, 0, ((groups + 63) / 64) * 8, s);
                 if (nullable) (void)hipMemsetAsync((void*)out_keys[i].validity, 0, ((groups + 63) / 64) * 8, s);
-                mk_gather_key_kernel<<<gg, 256, 0, s>>>(mk.c[i], first, groups, (void*)out_keys[i].values,
+                mk_gather_key_kernel<<<gg, 256, 0, s>>>(mk.c[i], first, groups, n, (void*)out_keys[i].values,
                                                         (uint32_t*)out_keys[i].validity);
                 e = hipGetLastError();
                 if (e != hipSuccess) rc = hip_fail(e, "mk_gather_key_kernel");

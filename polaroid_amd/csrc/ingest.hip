@@ -7,17 +7,14 @@
 // destination column, bitmaps (validity, Boolean values) at any bit offset
 // are placed by a device kernel, String offsets are rebased on the device.
 //
-// Copy modes (PLGPU_INGEST_MODE), measured with tools/bench_ingest.py on one
-// MI355X box (1e8-row OHLCV table, profiles/r02_ingest.jsonl):
-//   pageable (default)  the HIP runtime's own staged copy of the pageable
-//                       Arrow buffer: 49.0 GB/s at 1M-row chunks, 55.7 GB/s
-//                       at 8M-row chunks (the host link's rate: 56.6 GB/s
-//                       for whole columns);
-//   register            pin the source pages in place, DMA, unpin:
-//                       51.2 / 56.6 GB/s;
-//   staged              our double-buffered hipHostMalloc pair filled by
-//                       host threads: 31.6 / 50.7 GB/s (the host memcpy into
-//                       the pinned buffer is the bottleneck).
+// Copies are the HIP runtime's own staged copy of the pageable Arrow
+// buffer.  Measured with tools/bench_ingest.py on one MI355X box (1e8-row
+// OHLCV table, profiles/r02_ingest.jsonl): 49.0 GB/s at 1M-row chunks,
+// 55.7 GB/s at 8M-row chunks, the host link's rate (56.6 GB/s for whole
+// columns).  Two alternatives were measured and removed: pinning the source
+// pages in place (51.2 / 56.6 GB/s, no gain) and a double-buffered pinned
+// staging pair filled by host threads (31.6 / 50.7 GB/s: the host memcpy
+// into the pinned buffer is the bottleneck).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -30,106 +27,12 @@
 #include "plgpu_internal.hpp"
 
 namespace plgpu {
-namespace {
 
-constexpr size_t kStageBytes = size_t(32) << 20;  // one pinned staging buffer
-constexpr int kStages = 2;
-constexpr size_t kParallelCopyMin = size_t(4) << 20;
-
-struct Staging {
-    std::mutex mu;
-    void* buf[kStages] = {nullptr, nullptr};
-    hipEvent_t done[kStages] = {nullptr, nullptr};
-    bool used[kStages] = {false, false};
-    int next = 0;
-    int threads = 0;
-};
-
-Staging& staging() {
-    static Staging S;
-    return S;
-}
-
-int staging_init(Staging& S) {
-    if (S.buf[0]) return PLGPU_OK;
-    for (int k = 0; k < kStages; ++k) {
-        PLGPU_HIP(hipHostMalloc(&S.buf[k], kStageBytes, hipHostMallocDefault));
-        PLGPU_HIP(hipEventCreateWithFlags(&S.done[k], hipEventDisableTiming));
-    }
-    const unsigned hc = std::max(1u, std::thread::hardware_concurrency());
-    S.threads = (int)std::min(8u, hc);
-    return PLGPU_OK;
-}
-
-// memcpy with up to S.threads threads (the CPU side of one staged piece).
-void host_copy(void* dst, const void* src, size_t n, int threads) {
-    if (n < kParallelCopyMin || threads <= 1) {
-        std::memcpy(dst, src, n);
-        return;
-    }
-    const size_t part = ((n + threads - 1) / threads + 4095) & ~size_t(4095);
-    std::vector<std::thread> ts;
-    for (int t = 1; t < threads; ++t) {
-        const size_t lo = part * t;
-        if (lo >= n) break;
-        const size_t m = std::min(part, n - lo);
-        ts.emplace_back([=] { std::memcpy((char*)dst + lo, (const char*)src + lo, m); });
-    }
-    std::memcpy(dst, src, std::min(part, n));
-    for (auto& t : ts) t.join();
-}
-
-}  // namespace
-
-// Copy mode of h2d_staged (PLGPU_INGEST_MODE, read once): 1 = the runtime's
-// own pageable copy (default), 0 = our pinned staging pair, 2 = register
-// (pin) the source range in place and DMA from it.
-static int ingest_mode() {
-    static int mode = -1;
-    if (mode < 0) {
-        const char* e = getenv("PLGPU_INGEST_MODE");
-        mode = 1;
-        if (e && !strcmp(e, "staged")) mode = 0;
-        if (e && !strcmp(e, "register")) mode = 2;
-    }
-    return mode;
-}
-
-// Host -> device copy, asynchronous on `s` (the source may be reused as
-// soon as this returns).
+// Host -> device copy, asynchronous on `s`; the runtime stages a pageable
+// source before returning, so the source may be reused afterwards.
 int h2d_staged(void* dst, const void* src, size_t n, hipStream_t s) {
     if (n == 0) return PLGPU_OK;
-    const int mode = ingest_mode();
-    if (mode == 1) {
-        PLGPU_HIP(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, s));
-        return PLGPU_OK;
-    }
-    if (mode == 2 && n >= (size_t(1) << 20)) {
-        // pin the pages in place, DMA, unpin once the copy has completed
-        const uintptr_t a0 = (uintptr_t)src & ~uintptr_t(4095);
-        const size_t len = (((uintptr_t)src + n + 4095) & ~uintptr_t(4095)) - a0;
-        PLGPU_HIP(hipHostRegister((void*)a0, len, hipHostRegisterDefault));
-        void* dsrc = nullptr;
-        PLGPU_HIP(hipHostGetDevicePointer(&dsrc, (void*)a0, 0));
-        PLGPU_HIP(hipMemcpyAsync(dst, (const char*)dsrc + ((uintptr_t)src - a0), n, hipMemcpyDeviceToDevice, s));
-        PLGPU_HIP(hipStreamSynchronize(s));
-        PLGPU_HIP(hipHostUnregister((void*)a0));
-        return PLGPU_OK;
-    }
-    Staging& S = staging();
-    std::lock_guard<std::mutex> lk(S.mu);
-    int rc = staging_init(S);
-    if (rc) return rc;
-    for (size_t off = 0; off < n; off += kStageBytes) {
-        const size_t m = std::min(kStageBytes, n - off);
-        const int k = S.next;
-        S.next = (S.next + 1) % kStages;
-        if (S.used[k]) PLGPU_HIP(hipEventSynchronize(S.done[k]));  // the DMA that last read this buffer
-        host_copy(S.buf[k], (const char*)src + off, m, S.threads);
-        PLGPU_HIP(hipMemcpyAsync((char*)dst + off, S.buf[k], m, hipMemcpyHostToDevice, s));
-        PLGPU_HIP(hipEventRecord(S.done[k], s));
-        S.used[k] = true;
-    }
+    PLGPU_HIP(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, s));
     return PLGPU_OK;
 }
 

@@ -581,272 +581,6 @@ __global__ __launch_bounds__(kJnThreads) void jn_probe_emit_kernel(int64_t np, J
 }
 
 
-// ------------------------------------------ partitioned probe (large builds)
-// For builds whose table cannot stay in L2 (>= 2^18 distinct keys) the
-// random table reads of the plain probe are served by the Infinity Cache at
-// ~1.5 line requests per probe row, which bounds it at ~30 ms per 1e9 rows.
-// The partitioned probe (maintain_order="none") turns them into streaming:
-//   build - the distinct keys of the global table are split into P = 2^pb
-//           partition tables of 2^cbits slots ({key, ref word}, load <= 0.6,
-//           ~0.5-1.5 MB each, sized to sit in one XCD's 4 MiB L2);
-//   count / scatter - the probe rows are radix-partitioned by the same hash
-//           into (key, row) pairs: per-chunk LDS histograms, a device scan,
-//           and 4096-row tiles ranked in LDS so every partition's rows of a
-//           tile leave as one coalesced run; null (nulls_equal) and
-//           INT64_MIN keys go to one extra "special" bucket;
-//   match - partitions are numbered so that the P/8 partitions of an XCD
-//           group are contiguous, and blocks b, b+8, ... (one XCD under the
-//           observed round-robin placement; speed only, never correctness)
-//           sweep one group, so each XCD's L2 holds the one or two tables
-//           its blocks are probing;
-//   emit  - the plain emit kernel through the row map.
-// Output pairs come in partition order, which maintain_order="none"
-// leaves unspecified (the reference's order there is its thread chunking).
-constexpr int kPjThreads = 256;
-constexpr int kPjPer = 16;
-constexpr int kPjTile = kPjThreads * kPjPer;  // 4096 rows
-constexpr int kPjMaxBits = 10;
-constexpr int kPjMaxBuckets = (1 << kPjMaxBits) + 1;  // + the special bucket
-constexpr int kPjQpt = (kPjMaxBuckets + kPjThreads - 1) / kPjThreads;
-constexpr uint64_t kPjSalt = 0x9FB21C651E98DF25ull;
-
-__device__ __forceinline__ uint64_t pj_hash(uint64_t key) { return mk_fmix(key ^ kPjSalt); }
-
-// Top pb bits of the hash, rotated so the P/8 partitions of XCD group
-// (raw & 7) are contiguous: q = (raw & 7) * P/8 + raw / 8.
-__device__ __forceinline__ uint32_t pj_part(uint64_t h, int pb) {
-    const uint32_t raw = (uint32_t)(h >> (64 - pb));
-    return ((raw & 7u) << (pb - 3)) | (raw >> 3);
-}
-
-struct PjTab {
-    uint64_t* keys;  // P * 2^cbits, EMPTY = INT64_MIN
-    uint32_t* refs;  // ref word: build row, or kRefList | global slot
-    int pb;
-    int cbits;
-};
-
-// Distinct regular keys per partition at pb = kPjMaxBits.
-__global__ __launch_bounds__(256) void pj_bcount_kernel(JnTable t, uint32_t* __restrict__ pcount) {
-    __shared__ uint32_t h[1 << kPjMaxBits];
-    for (int i = threadIdx.x; i < (1 << kPjMaxBits); i += blockDim.x) h[i] = 0;
-    __syncthreads();
-    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < t.cap; s += (int64_t)gridDim.x * blockDim.x) {
-        const uint64_t k = jn_key(t, s);
-        if (k != kEmptyKey) atomicAdd(&h[pj_part(pj_hash(k), kPjMaxBits)], 1u);
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < (1 << kPjMaxBits); i += blockDim.x)
-        if (h[i]) atomicAdd(&pcount[i], h[i]);
-}
-
-__global__ void pj_init_kernel(PjTab pt, int64_t slots) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < slots; i += (int64_t)gridDim.x * blockDim.x)
-        pt.keys[i] = kEmptyKey;
-}
-
-__global__ __launch_bounds__(256) void pj_binsert_kernel(JnTable t, PjTab pt) {
-    const uint64_t mask = (1ull << pt.cbits) - 1;
-    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < t.cap; s += (int64_t)gridDim.x * blockDim.x) {
-        const uint64_t k = jn_key(t, s);
-        if (k == kEmptyKey) continue;
-        const uint64_t h = pj_hash(k);
-        const uint64_t base = (uint64_t)pj_part(h, pt.pb) << pt.cbits;
-        const uint32_t ref = jn_ref(t, s);
-        const uint32_t w = ref == kRefList ? (kRefList | (uint32_t)s) : ref;
-        uint64_t sl = h & mask;
-        for (uint64_t i = 0; i <= mask; ++i, sl = (sl + 1) & mask) {
-            const unsigned long long prev =
-                atomicCAS((unsigned long long*)&pt.keys[base + sl], (unsigned long long)kEmptyKey, (unsigned long long)k);
-            if (prev == (unsigned long long)kEmptyKey) {
-                pt.refs[base + sl] = w;
-                break;
-            }
-        }
-    }
-}
-
-// Bucket of probe row r (P = special, ~0u = dropped null); key word out.
-__device__ __forceinline__ uint32_t pj_bucket(const DevCol& pk, int64_t r, int pb, bool neq, uint64_t& key) {
-    key = 0;
-    if (!dev_valid(pk, r)) return neq ? (1u << pb) : ~0u;
-    key = dev_load(pk, r);
-    if (key == kEmptyKey) return 1u << pb;
-    return pj_part(pj_hash(key), pb);
-}
-
-__device__ __forceinline__ void pj_chunk(int64_t n, int64_t& lo, int64_t& hi) {
-    const int64_t tiles = (n + kPjTile - 1) / kPjTile;
-    const int64_t per = (tiles + gridDim.x - 1) / gridDim.x;
-    lo = std::min<int64_t>(n, (int64_t)blockIdx.x * per * kPjTile);
-    hi = std::min<int64_t>(n, lo + per * kPjTile);
-}
-
-// cnt[q * G + b]: rows of block b's chunk in bucket q.
-__global__ __launch_bounds__(kPjThreads) void pj_count_kernel(DevCol pk, int64_t np, int pb, bool neq,
-                                                              uint32_t* __restrict__ cnt) {
-    __shared__ uint32_t h[kPjMaxBuckets];
-    const int B = (1 << pb) + 1;
-    for (int i = threadIdx.x; i < B; i += blockDim.x) h[i] = 0;
-    __syncthreads();
-    int64_t lo, hi;
-    pj_chunk(np, lo, hi);
-    for (int64_t r = lo + threadIdx.x; r < hi; r += blockDim.x) {
-        uint64_t key;
-        const uint32_t q = pj_bucket(pk, r, pb, neq, key);
-        if (q != ~0u) atomicAdd(&h[q], 1u);
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < B; i += blockDim.x) cnt[(int64_t)i * gridDim.x + blockIdx.x] = h[i];
-}
-
-__global__ __launch_bounds__(kPjThreads) void pj_scatter_kernel(DevCol pk, int64_t np, int pb, bool neq,
-                                                                const uint64_t* __restrict__ off,
-                                                                uint64_t* __restrict__ okey,
-                                                                uint32_t* __restrict__ orow) {
-    __shared__ uint32_t h[kPjMaxBuckets];
-    __shared__ uint32_t lstart[kPjMaxBuckets];
-    __shared__ uint64_t gcur[kPjMaxBuckets];
-    __shared__ uint64_t skey[kPjTile];
-    __shared__ uint16_t srow[kPjTile];
-    __shared__ uint16_t sbk[kPjTile];
-    __shared__ uint64_t wsum[kPjThreads / 64];
-    __shared__ uint32_t tile_n;
-    const int B = (1 << pb) + 1;
-    for (int i = threadIdx.x; i < B; i += blockDim.x) gcur[i] = off[(int64_t)i * gridDim.x + blockIdx.x];
-    int64_t lo, hi;
-    pj_chunk(np, lo, hi);
-    for (int64_t base = lo; base < hi; base += kPjTile) {
-        for (int i = threadIdx.x; i < B; i += blockDim.x) h[i] = 0;
-        __syncthreads();
-        uint32_t pr[kPjPer];
-        uint64_t key[kPjPer];
-#pragma unroll
-        for (int k = 0; k < kPjPer; ++k) {
-            const int64_t r = base + k * kPjThreads + threadIdx.x;
-            pr[k] = ~0u;
-            key[k] = 0;
-            if (r < hi) {
-                const uint32_t q = pj_bucket(pk, r, pb, neq, key[k]);
-                if (q != ~0u) pr[k] = (q << 12) | atomicAdd(&h[q], 1u);
-            }
-        }
-        __syncthreads();
-        uint32_t c[kPjQpt], sum = 0;
-#pragma unroll
-        for (int j = 0; j < kPjQpt; ++j) {
-            const int q = threadIdx.x * kPjQpt + j;
-            c[j] = q < B ? h[q] : 0u;
-            sum += c[j];
-        }
-        uint64_t total;
-        uint32_t run = (uint32_t)block_excl_scan(sum, wsum, total);
-#pragma unroll
-        for (int j = 0; j < kPjQpt; ++j) {
-            const int q = threadIdx.x * kPjQpt + j;
-            if (q < B) lstart[q] = run;
-            run += c[j];
-        }
-        if (threadIdx.x == 0) tile_n = (uint32_t)total;
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < kPjPer; ++k) {
-            if (pr[k] == ~0u) continue;
-            const uint32_t q = pr[k] >> 12;
-            const uint32_t slot = lstart[q] + (pr[k] & 0xFFFu);
-            skey[slot] = key[k];
-            srow[slot] = (uint16_t)(k * kPjThreads + threadIdx.x);
-            sbk[slot] = (uint16_t)q;
-        }
-        __syncthreads();
-        const uint32_t m = tile_n;
-        for (uint32_t t = threadIdx.x; t < m; t += blockDim.x) {
-            const uint32_t q = sbk[t];
-            const uint64_t pos = gcur[q] + (t - lstart[q]);
-            okey[pos] = skey[t];
-            orow[pos] = (uint32_t)(base + srow[t]);
-        }
-        __syncthreads();
-        for (int i = threadIdx.x; i < B; i += blockDim.x) gcur[i] += h[i];
-    }
-}
-
-// Match pass over the partitioned rows: m[r] = ref word, per-tile output
-// counts.  Tiles [grp[x], grp[x + 1]) belong to XCD group x.
-__global__ __launch_bounds__(kJnThreads) void pj_match_kernel(const uint64_t* __restrict__ pkey,
-                                                              const uint32_t* __restrict__ prow, int64_t n,
-                                                              int64_t special_lo, PjTab pt, JnTable t, DevCol pk,
-                                                              bool neq, const int64_t* __restrict__ grp,
-                                                              uint32_t* __restrict__ m,
-                                                              uint64_t* __restrict__ tile_counts) {
-    __shared__ uint64_t wsum[kJnThreads / 64];
-    constexpr int R = kJnTileRows / kJnThreads;
-    const int x = blockIdx.x & 7;
-    const int64_t W = gridDim.x >> 3;
-    const int64_t t_hi = grp[x + 1];
-    const uint64_t mask = (1ull << pt.cbits) - 1;
-    for (int64_t tile = grp[x] + (blockIdx.x >> 3); tile < t_hi; tile += W) {
-        uint64_t key[R];
-#pragma unroll
-        for (int k = 0; k < R; ++k) {
-            const int64_t r = tile * kJnTileRows + (int64_t)k * kJnThreads + threadIdx.x;
-            key[k] = r < n ? __builtin_nontemporal_load(pkey + r) : 0;
-        }
-        uint64_t slot[R], home[R];
-#pragma unroll
-        for (int k = 0; k < R; ++k) {
-            const uint64_t h = pj_hash(key[k]);
-            slot[k] = ((uint64_t)pj_part(h, pt.pb) << pt.cbits) | (h & mask);
-            home[k] = pt.keys[slot[k]];
-        }
-        uint32_t w[R];
-        uint64_t c = 0;
-#pragma unroll
-        for (int k = 0; k < R; ++k) {
-            const int64_t r = tile * kJnTileRows + (int64_t)k * kJnThreads + threadIdx.x;
-            w[k] = kRefNone;
-            if (r >= n) continue;
-            if (r >= special_lo) {
-                // null (nulls_equal) or INT64_MIN key: the global special slots
-                const int64_t gs = dev_valid(pk, prow[r]) ? t.cap + 1 : t.cap;
-                const uint32_t ref = jn_ref(t, gs);
-                w[k] = ref == kRefList ? (kRefList | (uint32_t)gs) : ref;
-            } else {
-                uint64_t sl = slot[k];
-                uint64_t kk = home[k];
-                const uint64_t tb = sl & ~mask;
-                for (uint64_t i = 0; i <= mask; ++i) {
-                    if (kk == key[k]) {
-                        w[k] = pt.refs[sl];
-                        break;
-                    }
-                    if (kk == kEmptyKey) break;
-                    sl = tb | ((sl + 1) & mask);
-                    kk = pt.keys[sl];
-                }
-            }
-            if (w[k] != kRefNone) {
-                if (w[k] & kRefList) {
-                    const uint32_t gs = w[k] & ~kRefList;
-                    c += t.off[gs + 1] - t.off[gs];
-                } else {
-                    c += 1;
-                }
-            }
-            __builtin_nontemporal_store(w[k], m + r);
-        }
-        uint64_t total;
-        (void)block_excl_scan(c, wsum, total);
-        if (threadIdx.x == 0) tile_counts[tile] = total;
-    }
-}
-
-
-__global__ void pj_bounds_kernel(const uint64_t* __restrict__ off, int B, int G, int64_t* __restrict__ range) {
-    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q <= B; q += gridDim.x * blockDim.x)
-        range[q] = (int64_t)off[(int64_t)q * G];
-}
-
 static int num_cus_jn() {
     static int n = 0;
     if (n == 0) {
@@ -1403,143 +1137,6 @@ __global__ __launch_bounds__(kJnThreads) void jn_select_kernel(const uint32_t* _
 }
 
 
-// Partitioned probe (see pj_* kernels).  *used = false (nothing done) when
-// the build has too few distinct keys for it to pay.
-static int jn_probe_partitioned(const plgpu_column* key, const JnBuilt& b, bool nulls_equal, plgpu_column* out_p,
-                                plgpu_column* out_b, bool* used, hipStream_t s) {
-    *used = false;
-    const int64_t np = key->length;
-    const DevCol pk = as_dev(key);
-    const int cus = num_cus_jn();
-    // opt-in (PLGPU_JOIN_PARTITIONED=1): measured slower end to end on the
-    // 1e9 x 1e7 workload, because the pairs leave in partition order and the
-    // materialising gathers of the probe columns become random (DESIGN.md
-    // §Join, "partitioned probe")
-    const char* force = getenv("PLGPU_JOIN_PARTITIONED");
-    const bool forced = force && force[0] == '1';
-    if (!forced) return PLGPU_OK;
-    // distinct keys per fine partition
-    constexpr int PF = 1 << kPjMaxBits;
-    uint32_t* pcount = nullptr;
-    int rc = dev_alloc((void**)&pcount, PF * 4, s);
-    if (rc) return rc;
-    std::vector<uint32_t> fine(PF);
-    hipError_t e = hipMemsetAsync(pcount, 0, PF * 4, s);
-    if (e == hipSuccess) {
-        pj_bcount_kernel<<<(unsigned)std::min<int64_t>((b.t.cap + 255) / 256, cus * 8), 256, 0, s>>>(b.t, pcount);
-        e = hipGetLastError();
-    }
-    if (e == hipSuccess) e = hipMemcpyAsync(fine.data(), pcount, PF * 4, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
-    dev_free(pcount, s);
-    if (e != hipSuccess) return hip_fail(e, "partitioned join: build count");
-    int64_t distinct = 0;
-    for (uint32_t c : fine) distinct += c;
-    int pb = 3;
-    while (pb < kPjMaxBits && distinct > (int64_t(40000) << pb)) ++pb;
-    std::vector<int64_t> coarse((size_t)1 << pb, 0);
-    for (int q = 0; q < PF; ++q) {
-        const int raw = ((q & ((PF >> 3) - 1)) << 3) | (q >> (kPjMaxBits - 3));  // un-rotate pj_part
-        coarse[raw >> (kPjMaxBits - pb)] += fine[q];
-    }
-    int64_t mx = 1;
-    for (int64_t c : coarse) mx = std::max(mx, c);
-    int cb = 6;
-    while ((double)(int64_t(1) << cb) * 0.6 < (double)mx) ++cb;
-    const int P = 1 << pb, B = P + 1;
-    PjTab pt;
-    pt.pb = pb;
-    pt.cbits = cb;
-    pt.keys = nullptr;
-    pt.refs = nullptr;
-    const int64_t slots = (int64_t)P << cb;
-    const int64_t G = std::max<int64_t>(1, std::min<int64_t>((np + kPjTile - 1) / kPjTile, (int64_t)cus * 4));
-    const int64_t ncnt = (int64_t)B * G;
-    uint32_t* cnt = nullptr;
-    uint64_t *off = nullptr, *part = nullptr, *pkey = nullptr, *tcount = nullptr, *toff = nullptr, *tpart = nullptr;
-    uint32_t *prow = nullptr, *m = nullptr;
-    int64_t* range = nullptr;
-    rc = dev_alloc((void**)&pt.keys, slots * 8, s);
-    if (!rc) rc = dev_alloc((void**)&pt.refs, slots * 4, s);
-    if (!rc) rc = dev_alloc((void**)&cnt, ncnt * 4, s);
-    if (!rc) rc = dev_alloc((void**)&off, (ncnt + 1) * 8, s);
-    if (!rc) rc = dev_alloc((void**)&part, ((ncnt + kScanChunk - 1) / kScanChunk + 1) * 8, s);
-    if (!rc) rc = dev_alloc((void**)&range, (B + 1 + 9) * 8, s);
-    std::vector<int64_t> hr(B + 1);
-    if (!rc) {
-        pj_init_kernel<<<(unsigned)std::min<int64_t>((slots + 255) / 256, cus * 16), 256, 0, s>>>(pt, slots);
-        pj_binsert_kernel<<<(unsigned)std::min<int64_t>((b.t.cap + 255) / 256, cus * 16), 256, 0, s>>>(b.t, pt);
-        pj_count_kernel<<<(unsigned)G, kPjThreads, 0, s>>>(pk, np, pb, nulls_equal, cnt);
-        e = hipGetLastError();
-        if (e == hipSuccess) e = scan_exclusive<uint32_t>(cnt, ncnt, off, part, s);
-        if (e == hipSuccess) {
-            pj_bounds_kernel<<<(B + 256) / 256, 256, 0, s>>>(off, B, (int)G, range);
-            e = hipGetLastError();
-        }
-        if (e == hipSuccess) e = hipMemcpyAsync(hr.data(), range, (B + 1) * 8, hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
-        if (e != hipSuccess) rc = hip_fail(e, "partitioned join: probe count");
-    }
-    const int64_t n = hr[B];  // rows kept (null keys dropped unless nulls_equal)
-    const int64_t ntiles = std::max<int64_t>(1, (n + kJnTileRows - 1) / kJnTileRows);
-    if (!rc) rc = dev_alloc((void**)&pkey, std::max<int64_t>(n, 1) * 8, s);
-    if (!rc) rc = dev_alloc((void**)&prow, std::max<int64_t>(n, 1) * 4, s);
-    if (!rc) rc = dev_alloc((void**)&m, std::max<int64_t>(n, 1) * 4, s);
-    if (!rc) rc = dev_alloc((void**)&tcount, ntiles * 8, s);
-    if (!rc) rc = dev_alloc((void**)&toff, (ntiles + 1) * 8, s);
-    if (!rc) rc = dev_alloc((void**)&tpart, ((ntiles + kScanChunk - 1) / kScanChunk + 1) * 8, s);
-    uint64_t total = 0;
-    if (!rc) {
-        // XCD group x: partitions [x P/8, (x+1) P/8) -> tiles [grp[x], grp[x+1])
-        int64_t grp[9];
-        grp[0] = 0;
-        for (int x = 1; x < 8; ++x) grp[x] = std::max(grp[x - 1], hr[(int64_t)x * (P >> 3)] / kJnTileRows);
-        grp[8] = ntiles;
-        int64_t* dgrp = range + B + 1;
-        e = hipMemcpyAsync(dgrp, grp, sizeof grp, hipMemcpyHostToDevice, s);
-        if (e == hipSuccess) {
-            pj_scatter_kernel<<<(unsigned)G, kPjThreads, 0, s>>>(pk, np, pb, nulls_equal, off, pkey, prow);
-            pj_match_kernel<<<(unsigned)(cus * 8), kJnThreads, 0, s>>>(pkey, prow, n, hr[P], pt, b.t, pk, nulls_equal,
-                                                                     dgrp, m, tcount);
-            e = hipGetLastError();
-        }
-        if (e == hipSuccess) e = scan_exclusive<uint64_t>(tcount, ntiles, toff, tpart, s);
-        if (e == hipSuccess) e = hipMemcpyAsync(&total, toff + ntiles, 8, hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
-        if (e != hipSuccess) rc = hip_fail(e, "partitioned join: probe");
-    }
-    if (!rc && total >= 0xFFFFFFFFull) rc = fail(PLGPU_ERR_CAPACITY, "join output exceeds the u32 index space");
-    if (!rc) rc = make_owned_column(out_p, PLGPU_U32, (int64_t)total, false, s);
-    if (!rc) rc = make_owned_column(out_b, PLGPU_U32, (int64_t)total, false, s);
-    if (!rc && total > 0) {
-        const int g = (int)std::min<int64_t>(ntiles, (int64_t)cus * 8);
-        jn_probe_emit_kernel<JM_INNER><<<g, kJnThreads, 0, s>>>(n, b.t, m, toff, ntiles, (uint32_t*)out_p->values,
-                                                                (uint32_t*)out_b->values, prow);
-        e = hipGetLastError();
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
-        if (e != hipSuccess) rc = hip_fail(e, "partitioned join: emit");
-    }
-    dev_free(pt.keys, s);
-    dev_free(pt.refs, s);
-    dev_free(cnt, s);
-    dev_free(off, s);
-    dev_free(part, s);
-    dev_free(range, s);
-    dev_free(pkey, s);
-    dev_free(prow, s);
-    dev_free(m, s);
-    dev_free(tcount, s);
-    dev_free(toff, s);
-    dev_free(tpart, s);
-    if (rc) {
-        plgpu_column_release(out_p);
-        plgpu_column_release(out_b);
-        return rc;
-    }
-    *used = true;
-    return PLGPU_OK;
-}
-
 static int check_key(const plgpu_column* k) {
     if (k == nullptr) return fail(PLGPU_ERR_INVALID, "join key is NULL");
     if (!dtype_is_int(k->dtype)) return fail(PLGPU_ERR_SCHEMA, "join key must be an integer column");
@@ -1683,13 +1280,6 @@ static int join_impl(const plgpu_column* left_key, const plgpu_column* right_key
     const plgpu_column* bkey = build_right ? right_key : left_key;
     plgpu_column* op = build_right ? out_left_idx : out_right_idx;
     plgpu_column* ob = build_right ? out_right_idx : out_left_idx;
-    bool used = false;
-    if (mode == JM_INNER && !ordered && !drain) rc = jn_probe_partitioned(pkey, b, neq, op, ob, &used, s);
-    if (rc || used) {
-        jn_free(b, s);
-        (void)hipStreamSynchronize(s);
-        return rc;
-    }
     uint8_t* flags = nullptr;
     JnPass pp, dp;
     if (drain) {
@@ -1824,489 +1414,6 @@ static void jn_take_emit(const JnPass& pp, const TakeCols& lc, uint64_t* mp, uin
 // the null-free 8-byte left columns straight to their output rows -- no
 // index pairs, no random gather of the build side.  Everything else takes
 // pairs + gathers.
-// ------------------------------------ XCD-partitioned row-format join (xp)
-// An inner join whose output order is free (maintain_order "none"), with
-// unique build keys and null-free 8-byte payload / left columns.  The probe
-// is bound by random line requests when the table lives in HBM / the
-// Infinity Cache (about 55 G/s, ~20 ms per 1e9 probes).  A table slice held
-// in ONE XCD's 4 MiB L2 serves single-lane reads at 265-279 G/s
-// (tools/randread_bench.hip "xcd" rows, profiles/r02_randread.txt).  So:
-//   build   - the build keys are hash-partitioned into P = 8 S sub-tables of
-//             2^cbits 16-B cells {key, payload} (about 1 MiB each); XCD x
-//             owns sub-tables [x S, (x + 1) S);
-//   count   - probe rows per (sub-table, workgroup chunk), then a scan;
-//   scatter - each probe row's key and left columns are written, column by
-//             column through LDS, into sub-table order (one run per
-//             sub-table per 4096-row tile);
-//   probe   - workgroup b runs on XCD b % 8 (round-robin dispatch) and
-//             sweeps that XCD's rows in order, so the workgroups of an XCD
-//             probe the same one or two sub-tables at a time, from L2; the
-//             hits of a tile get their output range from one atomic add on
-//             a cursor, so the output order is the probe tile completion
-//             order (unspecified, as the reference's "none" order is).
-// The XCD placement is a speed assumption only; results never depend on it.
-constexpr int kXpThreads = 256;
-constexpr int kXpPer = 16;
-constexpr int kXpTile = kXpThreads * kXpPer;   // count / scatter tile: 4096 rows
-constexpr int kXpProbeRows = 8;                // probe rows per thread
-constexpr int kXpProbeTile = kXpThreads * kXpProbeRows;
-constexpr int kXpMaxParts = 1024;
-constexpr uint64_t kXpSalt = 0x6A09E667F3BCC909ull;
-
-struct XpTable {
-    uint4* cells;  // P * 2^cbits cells {key lo, key hi, payload lo, payload hi}; EMPTY key = INT64_MIN
-    int P;
-    int cbits;
-};
-
-__device__ __forceinline__ uint64_t xp_hash(uint64_t k) { return mk_fmix(k ^ kXpSalt); }
-__device__ __forceinline__ uint32_t xp_part(uint64_t h, int P) { return (uint32_t)(((h >> 32) * (uint64_t)P) >> 32); }
-
-__global__ void xp_init_kernel(XpTable t, int64_t ncells) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ncells; i += (int64_t)gridDim.x * blockDim.x)
-        t.cells[i] = make_uint4(0u, 0x80000000u, 0u, 0u);
-}
-
-// status[0]: a row found no free cell; [1]: duplicate key; [2]: an
-// INT64_MIN build key (the EMPTY marker) -- each sends the join back to the
-// general paths.  Null build keys join nothing (nulls_equal false).
-__global__ void xp_build_kernel(DevCol bk, int64_t nb, XpTable t, DevCol pay, unsigned long long* status) {
-    const uint64_t cmask = (1ull << t.cbits) - 1;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nb; i += (int64_t)gridDim.x * blockDim.x) {
-        if (!dev_valid(bk, i)) continue;
-        const uint64_t key = dev_load(bk, i);
-        if (key == kEmptyKey) {
-            atomicOr(&status[2], 1ull);
-            continue;
-        }
-        const uint64_t h = xp_hash(key);
-        const uint64_t base = (uint64_t)xp_part(h, t.P) << t.cbits;
-        uint64_t s = h & cmask;
-        bool placed = false;
-        for (uint64_t p = 0; p <= cmask; ++p, s = (s + 1) & cmask) {
-            uint64_t* kw = (uint64_t*)&t.cells[base + s];
-            uint64_t k = __hip_atomic_load(kw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (k == kEmptyKey) {
-                k = atomicCAS((unsigned long long*)kw, (unsigned long long)kEmptyKey, (unsigned long long)key);
-                if (k == kEmptyKey) {
-                    const uint64_t v = dev_load(pay, i);
-                    uint32_t* c = (uint32_t*)&t.cells[base + s];
-                    c[2] = (uint32_t)v;
-                    c[3] = (uint32_t)(v >> 32);
-                    placed = true;
-                    break;
-                }
-            }
-            if (k == key) {
-                atomicOr(&status[1], 1ull);
-                placed = true;
-                break;
-            }
-        }
-        if (!placed) atomicOr(&status[0], 1ull);
-    }
-}
-
-// Probe rows of workgroup b's contiguous chunk of tiles.
-__device__ __forceinline__ void xp_chunk(int64_t n, int64_t& lo, int64_t& hi) {
-    const int64_t tiles = (n + kXpTile - 1) / kXpTile;
-    const int64_t per = (tiles + gridDim.x - 1) / gridDim.x;
-    lo = std::min<int64_t>(n, (int64_t)blockIdx.x * per * kXpTile);
-    hi = std::min<int64_t>(n, lo + per * kXpTile);
-}
-
-// Sub-table of probe row r, or ~0u for a row that joins nothing (null key,
-// or the INT64_MIN key, which no build row holds on this path).
-__device__ __forceinline__ uint32_t xp_row_part(const uint64_t* kp, const uint8_t* kvalid, int64_t koff, int64_t r,
-                                                int64_t hi, int P, uint64_t& key) {
-    key = __builtin_nontemporal_load(kp + (r < hi ? r : hi - 1));
-    const bool ok = r < hi && (kvalid == nullptr || ((kvalid[(koff + r) >> 3] >> ((koff + r) & 7)) & 1)) &&
-                    key != kEmptyKey;
-    return ok ? xp_part(xp_hash(key), P) : ~0u;
-}
-
-// cnt[q * G + b]: probe rows of workgroup b's chunk in sub-table q.
-__global__ __launch_bounds__(kXpThreads) void xp_count_kernel(const uint64_t* __restrict__ kp,
-                                                              const uint8_t* __restrict__ kvalid, int64_t koff,
-                                                              int64_t np, int P, uint32_t* __restrict__ cnt) {
-    __shared__ uint32_t h[kXpMaxParts];
-    for (int i = threadIdx.x; i < P; i += blockDim.x) h[i] = 0;
-    __syncthreads();
-    int64_t lo, hi;
-    xp_chunk(np, lo, hi);
-    for (int64_t base = lo; base < hi; base += kXpTile) {
-        uint32_t q[kXpPer];
-        uint64_t key;
-#pragma unroll
-        for (int k = 0; k < kXpPer; ++k) q[k] = xp_row_part(kp, kvalid, koff, base + k * kXpThreads + threadIdx.x, hi, P, key);
-#pragma unroll
-        for (int k = 0; k < kXpPer; ++k)
-            if (q[k] != ~0u) atomicAdd(&h[q[k]], 1u);
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < P; i += blockDim.x) cnt[(int64_t)i * gridDim.x + blockIdx.x] = h[i];
-}
-
-// Columns moved into sub-table order: src[0] is the key (kp), the others
-// null-free 8-byte columns; dst[j] the partitioned arrays.
-struct XpCols {
-    const uint64_t* src[PLGPU_MAX_COLS + 1];
-    uint64_t* dst[PLGPU_MAX_COLS + 1];
-    int32_t n;
-};
-
-__global__ __launch_bounds__(kXpThreads) void xp_scatter_kernel(const uint8_t* __restrict__ kvalid, int64_t koff,
-                                                                int64_t np, int P, const uint64_t* __restrict__ off,
-                                                                XpCols c) {
-    __shared__ uint32_t h[kXpMaxParts];
-    __shared__ uint32_t lstart[kXpMaxParts];
-    __shared__ uint64_t gcur[kXpMaxParts];
-    __shared__ uint64_t sval[kXpTile];
-    __shared__ uint16_t spart[kXpTile];
-    __shared__ uint64_t wsum[kXpThreads / 64];
-    __shared__ uint32_t tile_n;
-    constexpr int QPT = kXpMaxParts / kXpThreads;
-    for (int i = threadIdx.x; i < P; i += blockDim.x) gcur[i] = off[(int64_t)i * gridDim.x + blockIdx.x];
-    int64_t lo, hi;
-    xp_chunk(np, lo, hi);
-    for (int64_t base = lo; base < hi; base += kXpTile) {
-        for (int i = threadIdx.x; i < P; i += blockDim.x) h[i] = 0;
-        __syncthreads();
-        uint32_t pr[kXpPer];
-        uint64_t key[kXpPer], v1[kXpPer];
-        // the first non-key column's loads go out with the keys'
-#pragma unroll
-        for (int k = 0; k < kXpPer; ++k) {
-            const int64_t r = base + k * kXpThreads + threadIdx.x;
-            key[k] = __builtin_nontemporal_load(c.src[0] + (r < hi ? r : hi - 1));
-            if (c.n > 1) v1[k] = __builtin_nontemporal_load(c.src[1] + (r < hi ? r : hi - 1));
-        }
-#pragma unroll
-        for (int k = 0; k < kXpPer; ++k) {
-            const int64_t r = base + k * kXpThreads + threadIdx.x;
-            const bool ok = r < hi && (kvalid == nullptr || ((kvalid[(koff + r) >> 3] >> ((koff + r) & 7)) & 1)) &&
-                            key[k] != kEmptyKey;
-            const uint32_t q = ok ? xp_part(xp_hash(key[k]), P) : ~0u;
-            pr[k] = q == ~0u ? ~0u : ((q << 16) | atomicAdd(&h[q], 1u));
-        }
-        __syncthreads();
-        uint32_t cq[QPT], sum = 0;
-#pragma unroll
-        for (int j = 0; j < QPT; ++j) {
-            const int q = threadIdx.x * QPT + j;
-            cq[j] = q < P ? h[q] : 0u;
-            sum += cq[j];
-        }
-        uint64_t total;
-        uint32_t run = (uint32_t)block_excl_scan(sum, wsum, total);
-#pragma unroll
-        for (int j = 0; j < QPT; ++j) {
-            const int q = threadIdx.x * QPT + j;
-            if (q < P) lstart[q] = run;
-            run += cq[j];
-        }
-        if (threadIdx.x == 0) tile_n = (uint32_t)total;
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < kXpPer; ++k) {
-            if (pr[k] == ~0u) continue;
-            const uint32_t q = pr[k] >> 16;
-            pr[k] = lstart[q] + (pr[k] & 0xFFFFu);
-            spart[pr[k]] = (uint16_t)q;
-        }
-        const uint32_t m = tile_n;
-        for (int col = 0; col < c.n; ++col) {
-            uint64_t v[kXpPer];
-            if (col == 1) {
-#pragma unroll
-                for (int k = 0; k < kXpPer; ++k) v[k] = v1[k];
-            } else if (col > 1) {
-#pragma unroll
-                for (int k = 0; k < kXpPer; ++k) {
-                    const int64_t r = base + k * kXpThreads + threadIdx.x;
-                    v[k] = __builtin_nontemporal_load(c.src[col] + (r < hi ? r : hi - 1));
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < kXpPer; ++k)
-                if (pr[k] != ~0u) sval[pr[k]] = col == 0 ? key[k] : v[k];
-            __syncthreads();
-            uint64_t* dst = c.dst[col];
-            for (uint32_t t = threadIdx.x; t < m; t += blockDim.x) {
-                const uint32_t q = spart[t];
-                dst[gcur[q] + (t - lstart[q])] = sval[t];
-            }
-            __syncthreads();
-        }
-        for (int i = threadIdx.x; i < P; i += blockDim.x) gcur[i] += h[i];
-    }
-}
-
-// Probe of the partitioned rows.  xr[x] .. xr[x + 1]: the rows of XCD x's
-// sub-tables.  A hit writes the payload and the row's left columns (lsrc[j],
-// partitioned arrays) at out position cursor-range base + its rank in the
-// tile (row chunk major, wave ballots), so each wave's writes are contiguous.
-template <int NC>
-__global__ __launch_bounds__(kXpThreads) void xp_probe_kernel(const uint64_t* __restrict__ pkey, TakeCols lc,
-                                                              const int64_t* __restrict__ xr, XpTable t,
-                                                              uint64_t* __restrict__ out_pay,
-                                                              unsigned long long* __restrict__ cursor) {
-    constexpr int R = kXpProbeRows;
-    constexpr int NW = kXpThreads / 64;
-    __shared__ uint32_t cnt[R * NW];
-    __shared__ uint64_t tile_base;
-    __shared__ int64_t next_tile;
-    const int x = blockIdx.x & 7;
-    const int64_t lo = xr[x], hi = xr[x + 1];
-    const int64_t ntiles = (hi - lo + kXpProbeTile - 1) / kXpProbeTile;
-    const uint64_t cmask = (1ull << t.cbits) - 1;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    // the workgroups of XCD x take its tiles in order from one queue
-    // (cursor[8 + 16 x]), so together they sweep one or two sub-tables at a
-    // time whatever order they were dispatched in
-    unsigned long long* queue = cursor + 8 + 16 * x;
-    for (;;) {
-        __syncthreads();
-        if (threadIdx.x == 0) next_tile = (int64_t)atomicAdd(queue, 1ull);
-        __syncthreads();
-        const int64_t tile = next_tile;
-        if (tile >= ntiles) break;
-        const int64_t base = lo + tile * kXpProbeTile;
-        uint64_t key[R], cell[R], pay[R];
-        bool live[R];
-#pragma unroll
-        for (int k = 0; k < R; ++k) {
-            const int64_t r = base + k * kXpThreads + threadIdx.x;
-            live[k] = r < hi;
-            key[k] = __builtin_nontemporal_load(pkey + (r < hi ? r : hi - 1));
-        }
-        // rounds of single-cell probes, every pending row's load in flight
-        uint64_t sub[R];
-        uint32_t hit = 0, pend = 0;
-#pragma unroll
-        for (int k = 0; k < R; ++k) {
-            const uint64_t h = xp_hash(key[k]);
-            sub[k] = ((uint64_t)xp_part(h, t.P) << t.cbits);
-            cell[k] = h & cmask;
-            pend |= (live[k] ? 1u : 0u) << k;
-        }
-        // (bounded: every cell of a sub-table visited once at most, even if
-        // a sub-table were full)
-        for (uint64_t round = 0; pend && round <= cmask; ++round) {
-            uint4 cv[R];
-#pragma unroll
-            for (int k = 0; k < R; ++k)
-                cv[k] = ((pend >> k) & 1u) ? t.cells[sub[k] + cell[k]] : make_uint4(0u, 0x80000000u, 0u, 0u);
-#pragma unroll
-            for (int k = 0; k < R; ++k) {
-                if (!((pend >> k) & 1u)) continue;
-                const uint64_t kk = (uint64_t)cv[k].x | ((uint64_t)cv[k].y << 32);
-                if (kk == key[k]) {
-                    hit |= 1u << k;
-                    pay[k] = (uint64_t)cv[k].z | ((uint64_t)cv[k].w << 32);
-                    pend &= ~(1u << k);
-                } else if (kk == kEmptyKey) {
-                    pend &= ~(1u << k);
-                } else {
-                    cell[k] = (cell[k] + 1) & cmask;
-                }
-            }
-        }
-        // output ranks: chunk k, wave w -> cnt[k * NW + w]
-        uint64_t bal[R];
-#pragma unroll
-        for (int k = 0; k < R; ++k) {
-            bal[k] = __ballot((hit >> k) & 1u);
-            if (lane == 0) cnt[k * NW + wave] = (uint32_t)__popcll(bal[k]);
-        }
-        __syncthreads();
-        if (threadIdx.x < 64) {
-            const uint32_t v = threadIdx.x < R * NW ? cnt[threadIdx.x] : 0u;
-            uint32_t xs = v;
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const uint32_t y = __shfl_up(xs, off, 64);
-                if (lane >= off) xs += y;
-            }
-            if (threadIdx.x < R * NW) cnt[threadIdx.x] = xs - v;
-            if (threadIdx.x == 63)
-                tile_base = xs ? atomicAdd(cursor, (unsigned long long)xs) : 0ull;
-        }
-        __syncthreads();
-        const uint64_t ob = tile_base;
-#pragma unroll
-        for (int k = 0; k < R; ++k) {
-            if (!((hit >> k) & 1u)) continue;
-            const int64_t r = base + k * kXpThreads + threadIdx.x;
-            const uint64_t pos = ob + cnt[k * NW + wave] + (uint32_t)__popcll(bal[k] & lt);
-            out_pay[pos] = pay[k];
-#pragma unroll
-            for (int j = 0; j < NC; ++j) lc.dst[j][pos] = __builtin_nontemporal_load(lc.src[j] + r);
-        }
-        __syncthreads();
-    }
-}
-
-template <int NC>
-static void xp_probe_launch(int grid, const uint64_t* pkey, const TakeCols& lc, const int64_t* xr, const XpTable& t,
-                            uint64_t* out_pay, unsigned long long* cursor, hipStream_t s) {
-    xp_probe_kernel<NC><<<grid, kXpThreads, 0, s>>>(pkey, lc, xr, t, out_pay, cursor);
-}
-
-__global__ void xp_xcd_ranges_kernel(const uint64_t* __restrict__ off, int S, int G, int64_t* __restrict__ xr) {
-    const int x = threadIdx.x;
-    if (x <= 8) xr[x] = (int64_t)off[(int64_t)x * S * G];
-}
-
-static int64_t env_i64(const char* name, int64_t dflt) {
-    const char* e = getenv(name);
-    return e ? atoll(e) : dflt;
-}
-
-// The xp join.  Returns 1 (nothing allocated, outputs untouched) when the
-// build side does not qualify (duplicate or INT64_MIN keys, a full
-// sub-table): the caller takes the general paths.
-static int xp_join(const plgpu_column* lk, const plgpu_column* rk, const plgpu_column* lcols, int32_t nleft,
-                   const plgpu_column& pay, plgpu_column* out_left, plgpu_column* out_right, int64_t* out_len,
-                   hipStream_t s) {
-    const int64_t np = lk->length, nb = rk->length;
-    const int cbits = (int)env_i64("PLGPU_XP_CBITS", 16);
-    const double load = 0.4;
-    const int64_t per_sub = std::max<int64_t>(1, (int64_t)((double)(int64_t(1) << cbits) * load));
-    const int S = (int)std::max<int64_t>(1, (nb + 8 * per_sub - 1) / (8 * per_sub));
-    const int P = 8 * S;
-    if (P > kXpMaxParts) return 1;
-    XpTable t;
-    t.P = P;
-    t.cbits = cbits;
-    t.cells = nullptr;
-    const int64_t ncells = (int64_t)P << cbits;
-    unsigned long long* st = nullptr;
-    int rc = dev_alloc((void**)&t.cells, (size_t)ncells * 16, s);
-    if (!rc) rc = dev_alloc((void**)&st, 8 * (8 + 16 * 8), s);
-    if (rc) {
-        dev_free(t.cells, s);
-        return rc;
-    }
-    unsigned long long hst[4] = {0, 0, 0, 0};
-    hipError_t e = hipMemsetAsync(st, 0, 8 * 8, s);
-    if (e == hipSuccess) {
-        xp_init_kernel<<<(int)std::min<int64_t>((ncells + 255) / 256, 8192), 256, 0, s>>>(t, ncells);
-        xp_build_kernel<<<(int)std::min<int64_t>((nb + 255) / 256, 8192), 256, 0, s>>>(dev_col(*rk), nb, t,
-                                                                                       dev_col(pay), st);
-        e = hipGetLastError();
-    }
-    if (e == hipSuccess) e = hipMemcpyAsync(hst, st, sizeof hst, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
-    if (e != hipSuccess) rc = hip_fail(e, "xp build");
-    if (rc || hst[0] || hst[1] || hst[2]) {
-        dev_free(st, s);
-        dev_free(t.cells, s);
-        return rc ? rc : 1;
-    }
-    // probe side: count, scan, XCD ranges
-    const int G = num_cus_jn() * 4;
-    const int64_t ncnt = (int64_t)P * G;
-    uint32_t* cnt = nullptr;
-    uint64_t* off = nullptr;
-    uint64_t* part = nullptr;
-    int64_t* xr = nullptr;
-    rc = dev_alloc((void**)&cnt, ncnt * 4, s);
-    if (!rc) rc = dev_alloc((void**)&off, (ncnt + 1) * 8, s);
-    if (!rc) rc = dev_alloc((void**)&part, ((ncnt + kScanChunk - 1) / kScanChunk + 1) * 8, s);
-    if (!rc) rc = dev_alloc((void**)&xr, 16 * 8, s);
-    const uint64_t* kp = (const uint64_t*)lk->values + lk->offset;
-    int64_t rows = 0;
-    if (!rc) {
-        xp_count_kernel<<<G, kXpThreads, 0, s>>>(kp, lk->validity, lk->offset, np, P, cnt);
-        e = hipGetLastError();
-        if (e == hipSuccess) e = scan_exclusive<uint32_t>(cnt, ncnt, off, part, s);
-        if (e == hipSuccess) {
-            xp_xcd_ranges_kernel<<<1, 64, 0, s>>>(off, S, G, xr);
-            e = hipGetLastError();
-        }
-        uint64_t total = 0;
-        if (e == hipSuccess) e = hipMemcpyAsync(&total, off + ncnt, 8, hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
-        if (e != hipSuccess) rc = hip_fail(e, "xp count");
-        rows = (int64_t)total;
-    }
-    // partitioned key + the left columns that are not the key itself
-    XpCols xc;
-    std::memset(&xc, 0, sizeof xc);
-    int src_of[PLGPU_MAX_COLS];
-    xc.src[0] = kp;
-    xc.n = 1;
-    for (int i = 0; i < nleft; ++i) {
-        const plgpu_column& c = lcols[i];
-        const bool is_key = c.values == lk->values && c.offset == lk->offset && c.validity == nullptr;
-        if (is_key) {
-            src_of[i] = 0;
-            continue;
-        }
-        src_of[i] = xc.n;
-        xc.src[xc.n++] = (const uint64_t*)c.values + c.offset;
-    }
-    uint64_t* pbuf = nullptr;
-    if (!rc) rc = dev_alloc((void**)&pbuf, (size_t)std::max<int64_t>(rows, 1) * 8 * xc.n, s);
-    for (int j = 0; j < xc.n && !rc; ++j) xc.dst[j] = pbuf + (size_t)j * std::max<int64_t>(rows, 1);
-    if (!rc && rows > 0) {
-        xp_scatter_kernel<<<G, kXpThreads, 0, s>>>(lk->validity, lk->offset, np, P, off, xc);
-        e = hipGetLastError();
-        if (e != hipSuccess) rc = hip_fail(e, "xp scatter");
-    }
-    dev_free(cnt, s);
-    dev_free(part, s);
-    dev_free(off, s);
-    // outputs at capacity `rows` (every probe row matches at most once);
-    // their length is set to the hit count
-    for (int i = 0; i < nleft && !rc; ++i) rc = make_owned_column(&out_left[i], lcols[i].dtype, rows, false, s);
-    if (!rc) rc = make_owned_column(&out_right[0], pay.dtype, rows, false, s);
-    unsigned long long hits = 0;
-    if (!rc && rows > 0) {
-        (void)hipMemsetAsync(st, 0, 8 * (8 + 16 * 8), s);
-        TakeCols lc;
-        std::memset(&lc, 0, sizeof lc);
-        lc.n = nleft;
-        for (int i = 0; i < nleft; ++i) {
-            lc.src[i] = xc.dst[src_of[i]];
-            lc.dst[i] = (uint64_t*)out_left[i].values;
-        }
-        const int grid = num_cus_jn() * (int)env_i64("PLGPU_XP_WG_PER_CU", 8);
-        uint64_t* ov = (uint64_t*)out_right[0].values;
-        switch (nleft) {
-        case 0: xp_probe_launch<0>(grid, xc.dst[0], lc, xr, t, ov, st, s); break;
-        case 1: xp_probe_launch<1>(grid, xc.dst[0], lc, xr, t, ov, st, s); break;
-        case 2: xp_probe_launch<2>(grid, xc.dst[0], lc, xr, t, ov, st, s); break;
-        case 3: xp_probe_launch<3>(grid, xc.dst[0], lc, xr, t, ov, st, s); break;
-        case 4: xp_probe_launch<4>(grid, xc.dst[0], lc, xr, t, ov, st, s); break;
-        case 5: xp_probe_launch<5>(grid, xc.dst[0], lc, xr, t, ov, st, s); break;
-        case 6: xp_probe_launch<6>(grid, xc.dst[0], lc, xr, t, ov, st, s); break;
-        case 7: xp_probe_launch<7>(grid, xc.dst[0], lc, xr, t, ov, st, s); break;
-        default: xp_probe_launch<8>(grid, xc.dst[0], lc, xr, t, ov, st, s); break;
-        }
-        e = hipGetLastError();
-        if (e == hipSuccess) e = hipMemcpyAsync(&hits, st, 8, hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
-        if (e != hipSuccess) rc = hip_fail(e, "xp probe");
-    }
-    if (!rc && hits >= 0xFFFFFFFFull) rc = fail(PLGPU_ERR_CAPACITY, "join output exceeds the u32 index space");
-    dev_free(pbuf, s);
-    dev_free(xr, s);
-    dev_free(st, s);
-    dev_free(t.cells, s);
-    if (rc) {
-        for (int i = 0; i < nleft; ++i) plgpu_column_release(&out_left[i]);
-        plgpu_column_release(&out_right[0]);
-        return rc;
-    }
-    for (int i = 0; i < nleft; ++i) out_left[i].length = (int64_t)hits;
-    out_right[0].length = (int64_t)hits;
-    *out_len = (int64_t)hits;
-    return PLGPU_OK;
-}
-
 PLGPU_API int plgpu_join_inner_take(const plgpu_column* left_key, const plgpu_column* right_key,
                                     const plgpu_column* left_cols, int32_t nleft, const plgpu_column* right_cols,
                                     int32_t nright, int32_t nulls_equal, int32_t maintain_order, int32_t validate,
@@ -2338,21 +1445,6 @@ PLGPU_API int plgpu_join_inner_take(const plgpu_column* left_key, const plgpu_co
                            (validate == PLGPU_JOIN_VALIDATE_M_M || validate == PLGPU_JOIN_VALIDATE_M_1) &&
                            left_key->length >= (int64_t(1) << 16) &&
                            (right_key->length <= left_key->length || maintain_order == PLGPU_JOIN_ORDER_LEFT);
-    // XCD-partitioned probe (opt-in, PLGPU_XP=1: measured slower, DESIGN.md
-    // "XCD-partitioned probe"): order-free output, 8-byte keys, every left
-    // column null-free 8-byte, nulls not joined, large enough to pay for the
-    // partitioning (PLGPU_XP_MIN_PROBE / _MIN_BUILD rows)
-    bool xp_ok = inline_ok && maintain_order == PLGPU_JOIN_ORDER_NONE && !neq &&
-                 dtype_bytes(left_key->dtype) == 8 && left_key->dtype != PLGPU_F64 &&
-                 left_key->dtype == right_key->dtype && getenv("PLGPU_XP") != nullptr &&
-                 left_key->length >= env_i64("PLGPU_XP_MIN_PROBE", int64_t(1) << 24) &&
-                 right_key->length >= env_i64("PLGPU_XP_MIN_BUILD", int64_t(1) << 18);
-    for (int i = 0; i < nleft && xp_ok; ++i) xp_ok = fused8(left_cols[i]);
-    if (xp_ok) {
-        rc = xp_join(left_key, right_key, left_cols, nleft, right_cols[0], out_left, out_right, out_len, s);
-        if (rc <= 0) return rc;  // done, or an error; 1: fall through
-        rc = PLGPU_OK;
-    }
     JnBuilt b;
     bool use_inline = false;
     if (inline_ok) {
@@ -2586,7 +1678,7 @@ PLGPU_API int plgpu_join_multi(const plgpu_column* left_keys, const plgpu_column
     for (int attempt = 0; attempt < 4 && !rc && !done; ++attempt) {
         const uint64_t seed = 0x243F6A8885A308D3ull * (uint64_t)(2 * attempt + 1);
         // PLGPU_MK_COLLIDE (tests only): a 3-bit first hash forces collisions
-        const uint64_t mask = attempt == 0 && getenv("PLGPU_MK_COLLIDE") ? 7ull : ~0ull;
+        const uint64_t mask = attempt == 0 && options().mk_collide ? 7ull : ~0ull;
         if (nl > 0)
             jn_tuple_hash_kernel<<<(unsigned)std::min<int64_t>((nl + 255) / 256, cus * 16), 256, 0, s>>>(ka, nl, seed,
                                                                                                        mask, neq, hl, vl);
@@ -2661,7 +1753,7 @@ PLGPU_API int plgpu_gather(const plgpu_column* cols, int32_t ncols, const plgpu_
     // packed gather, in groups of up to kAosMax; everything else column by
     // column
     std::vector<int> packed;
-    if (n >= (1 << 20) && idx->validity == nullptr && !getenv("PLGPU_NO_AOS_GATHER")) {
+    if (n >= (1 << 20) && idx->validity == nullptr) {
         for (int i = 0; i < ncols; ++i)
             if (cols[i].validity == nullptr && dtype_bytes(cols[i].dtype) == 8 && cols[i].dtype != PLGPU_BOOL &&
                 cols[i].length == cols[0].length)

@@ -31,10 +31,16 @@ int hip_fail(hipError_t e, const char* what);
     } while (0)
 
 hipStream_t as_stream(void* s);
-// A library-owned non-blocking stream of the current device, for small work
-// that overlaps a long launch (joined back with events); nullptr if it could
-// not be created.
-hipStream_t side_stream();
+
+// Test hooks / diagnostics (runtime.cpp): read once from PLGPU_<NAME> at
+// load, settable with plgpu_set_option.
+struct Options {
+    int debug = 0;       // per-attempt group-by diagnostics on stderr
+    int no_pack = 0;     // multi-key operators hash tuples even when they would pack (tests)
+    int mk_collide = 0;  // 3-bit first tuple hash: forces the collision / re-seed path (tests)
+    int runs = -1;       // -1: the plan picks the sorted-key variant; 0 / 1 force it (tests)
+};
+Options& options();
 int dev_alloc(void** p, size_t bytes, hipStream_t s);
 void dev_free(void* p, hipStream_t s);
 

@@ -35,31 +35,37 @@ int hip_fail(hipError_t e, const char* what) {
 
 hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
-hipStream_t side_stream() {
-    // non-blocking: no implicit ordering against the legacy null stream the
-    // callers usually enqueue on; ordering comes only from their events
-    static std::mutex mu;
-    static hipStream_t streams[64] = {};
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (dev < 0 || dev >= 64) return nullptr;
-    std::lock_guard<std::mutex> lk(mu);
-    if (streams[dev] == nullptr && hipStreamCreateWithFlags(&streams[dev], hipStreamNonBlocking) != hipSuccess) {
-        (void)hipGetLastError();
-        streams[dev] = nullptr;
-    }
-    return streams[dev];
+// ------------------------------------------------------------ options
+// Test hooks and diagnostics: each read once from the environment
+// (PLGPU_<NAME>, an integer) when the library loads, and settable through
+// plgpu_set_option.  No measurement variant lives here: losing A/B variants
+// leave the product once their numbers are logged.
+static Options read_env_options() {
+    Options o;
+    auto get = [](const char* name, int def) {
+        const char* e = getenv(name);
+        return e ? atoi(e) : def;
+    };
+    o.debug = get("PLGPU_DEBUG", 0);
+    o.no_pack = get("PLGPU_NO_PACK", 0);
+    o.mk_collide = get("PLGPU_MK_COLLIDE", 0);
+    o.runs = get("PLGPU_RUNS", -1);
+    return o;
+}
+
+Options& options() {
+    static Options o = read_env_options();
+    return o;
 }
 
 // Caching device allocator.  Blocks come from hipMalloc and are recycled
 // through size-keyed free lists instead of being returned with hipFree
-// (which synchronises the device).  Every entry point enqueues its work on
-// one stream and frees only after the kernels that use a block were
-// enqueued, so stream order makes reuse safe.  PLGPU_ALLOC=async switches
-// to hipMallocAsync / hipFreeAsync: the GPU parity suites pass under it
-// (profiles/r02_alloc_async_ab.log), so an earlier "lost writes" report
-// against that pool was not the pool's fault -- it predates the exchange's
-// receive-buffer fence (distributed._settle), the likelier cause.
+// (which synchronises the device).  Every entry point enqueues all of its
+// work on the caller's one stream (the library has no stream of its own)
+// and frees only after the kernels that use a block were enqueued there, so
+// stream order makes reuse safe.  (hipMallocAsync / hipFreeAsync from the
+// device's default pool passed the same parity suites, profiles/
+// r02_alloc_async_ab.log; the cache stays because it never synchronises.)
 namespace {
 struct Pool {
     std::mutex mu;
@@ -85,27 +91,9 @@ void release_cached(Pool& P) {
 }
 }  // namespace
 
-// PLGPU_ALLOC=async: stream-ordered hipMallocAsync / hipFreeAsync from the
-// device's default pool instead of the cache (A/B runs of the allocator).
-static bool alloc_async() {
-    static const int on = [] {
-        const char* e = getenv("PLGPU_ALLOC");
-        return (e && !strcmp(e, "async")) ? 1 : 0;
-    }();
-    return on != 0;
-}
-
 int dev_alloc(void** p, size_t bytes, hipStream_t s) {
+    (void)s;
     *p = nullptr;
-    if (alloc_async()) {
-        const hipError_t e = hipMallocAsync(p, bytes == 0 ? 256 : bytes, s);
-        if (e != hipSuccess) {
-            (void)hipGetLastError();
-            *p = nullptr;
-            return fail(PLGPU_ERR_OOM, "hipMallocAsync failed");
-        }
-        return PLGPU_OK;
-    }
     const size_t want = round_bytes(bytes == 0 ? 256 : bytes);
     int dev = 0;
     (void)hipGetDevice(&dev);
@@ -137,11 +125,8 @@ int dev_alloc(void** p, size_t bytes, hipStream_t s) {
 }
 
 void dev_free(void* p, hipStream_t s) {
+    (void)s;
     if (p == nullptr) return;
-    if (alloc_async()) {
-        (void)hipFreeAsync(p, s);
-        return;
-    }
     int dev = 0;
     (void)hipGetDevice(&dev);
     Pool& P = pool_for(dev);
@@ -720,6 +705,30 @@ PLGPU_API int plgpu_expr_dtype(const plgpu_column* cols, int32_t ncols, const pl
     const int rc = lower_program(cols, ncols, program, n_instr, &dp);
     if (rc) return rc;
     *out_dtype = dp.out_dtype;
+    return PLGPU_OK;
+}
+
+PLGPU_API int plgpu_set_option(const char* name, int64_t value) {
+    if (name == nullptr) return fail(PLGPU_ERR_INVALID, "option name is NULL");
+    Options& o = options();
+    int* f = nullptr;
+    if (!strcmp(name, "debug")) f = &o.debug;
+    else if (!strcmp(name, "no_pack")) f = &o.no_pack;
+    else if (!strcmp(name, "mk_collide")) f = &o.mk_collide;
+    else if (!strcmp(name, "runs")) f = &o.runs;
+    if (f == nullptr) return fail(PLGPU_ERR_INVALID, std::string("unknown option ") + name);
+    *f = (int)value;
+    return PLGPU_OK;
+}
+
+PLGPU_API int plgpu_get_option(const char* name, int64_t* out) {
+    if (name == nullptr || out == nullptr) return fail(PLGPU_ERR_INVALID, "NULL argument");
+    const Options& o = options();
+    if (!strcmp(name, "debug")) *out = o.debug;
+    else if (!strcmp(name, "no_pack")) *out = o.no_pack;
+    else if (!strcmp(name, "mk_collide")) *out = o.mk_collide;
+    else if (!strcmp(name, "runs")) *out = o.runs;
+    else return fail(PLGPU_ERR_INVALID, std::string("unknown option ") + name);
     return PLGPU_OK;
 }
 

@@ -252,7 +252,7 @@ __global__ __launch_bounds__(kSrtThreads) void srt_downsweep_kernel(const uint64
                                                                     const uint64_t* __restrict__ off,
                                                                     uint64_t* __restrict__ keys_out,
                                                                     uint32_t* __restrict__ idx_out, int cons,
-                                                                    uint64_t kmask, int xcd) {
+                                                                    uint64_t kmask) {
     constexpr int TH = kSrtThreads;
     constexpr int NW = TH / 64;
     constexpr int ROWS = kSrtTile / TH;  // rows of 64 per wave (16)
@@ -264,11 +264,11 @@ __global__ __launch_bounds__(kSrtThreads) void srt_downsweep_kernel(const uint64
     __shared__ uint32_t cnt[NW][256];
     __shared__ uint64_t wsum[NW];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    // xcd: consecutive tiles on one XCD (bijective remap of the round-robin
+    // consecutive tiles on one XCD (bijective remap of the round-robin
     // dispatch), so the digit runs that neighbouring tiles write into the
     // same output lines meet in one L2 instead of leaving it as two partial
     // line write-backs
-    const int64_t tile = xcd ? xcd_tile(blockIdx.x, ntiles) : (int64_t)blockIdx.x;
+    const int64_t tile = xcd_tile(blockIdx.x, ntiles);
     const int64_t base = tile * kSrtTile;
     const int m = n - base < kSrtTile ? (int)(n - base) : kSrtTile;
     // this tile's digit offsets (256 scattered words): issued first so their
@@ -466,10 +466,9 @@ struct SrtScratch {
 template <bool IN_P, int OUT>
 static void srt_down(const uint64_t* ki, const uint32_t* ii, int64_t nv, int shift, int64_t ntiles,
                      const uint64_t* off, uint64_t* ko, uint32_t* io, int cons, uint64_t kmask, hipStream_t s) {
-    const char* xe = getenv("PLGPU_SORT_XCD");  // "0": round-robin tiles (A/B)
-    const int xcd = (xe && strcmp(xe, "0") == 0) ? 0 : 1;
+    // XCD-aware tiles (round-robin tiles measured slower, profiles/r02_sort_xcd_ab.log)
     srt_downsweep_kernel<IN_P, OUT>
-        <<<(unsigned)ntiles, kSrtThreads, 0, s>>>(ki, ii, nv, shift, ntiles, off, ko, io, cons, kmask, xcd);
+        <<<(unsigned)ntiles, kSrtThreads, 0, s>>>(ki, ii, nv, shift, ntiles, off, ko, io, cons, kmask);
 }
 
 // pre: srt_codes_stats_kernel produced keys[cur], the per-tile OR / AND in
@@ -510,7 +509,6 @@ static int radix_passes(uint64_t* keys[2], uint32_t* idx[2], int64_t nv, int& cu
         return PLGPU_OK;
     }
     const int hi_bits = 8 * (bytes[nb - 1] + 1);
-    const bool nopack = getenv("PLGPU_SORT_NO_PACK") != nullptr;
     bool packed = false;
     int cons = 0;  // code bits dropped by the packing
     for (int j = 0; j < nb; ++j) {
@@ -523,7 +521,7 @@ static int radix_passes(uint64_t* keys[2], uint32_t* idx[2], int64_t nv, int& cu
         if (e != hipSuccess) return hip_fail(e, "sort scan");
         const bool last = j == nb - 1;
         const int ncons = S + 8;
-        const bool to_pack = !packed && !last && !nopack && hi_bits - ncons <= 32;
+        const bool to_pack = !packed && !last && hi_bits - ncons <= 32;
         const uint64_t kmask = hi_bits - ncons >= 64 ? ~0ull : ((1ull << (hi_bits - ncons)) - 1);
         uint64_t* ko = keys[cur ^ 1];
         uint32_t* io = idx[cur ^ 1];

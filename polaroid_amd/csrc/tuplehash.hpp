@@ -239,7 +239,7 @@ inline int mk_plan_pack(const MkKeys& ka, int64_t na, const MkKeys* kb, int64_t 
     for (int i = 0; i < ka.n; ++i)
         if (dtype_is_float(ka.c[i].dtype) || ka.c[i].dtype == PLGPU_U64 || ka.c[i].dtype == PLGPU_STR)
             return PLGPU_OK;  // hashed path (UInt64 ranges do not fit the signed range pass)
-    if (getenv("PLGPU_NO_PACK")) return PLGPU_OK;
+    if (options().no_pack) return PLGPU_OK;  // tests: force the hashed path
     unsigned long long* st = nullptr;
     const size_t bytes = 2 * 3 * kMaxKeys * 8;
     int rc = dev_alloc((void**)&st, bytes, s);

@@ -88,9 +88,9 @@ def test_ohlcv_bar(gpu):
 
 
 @pytest.mark.parametrize("pack", [True, False])
-def test_first_last_multi_key(gpu, pack, monkeypatch):
+def test_first_last_multi_key(gpu, pack, plgpu_option):
     if not pack:
-        monkeypatch.setenv("PLGPU_NO_PACK", "1")
+        plgpu_option("no_pack", 1)
     rng = np.random.default_rng(3)
     n = 100_000
     a = rng.integers(0, 50, n).astype(np.int64)

@@ -92,11 +92,11 @@ AGGS = [("sum", "a"), ("mean", "d"), ("min", "b"), ("max", "a"), ("count", "d"),
 @pytest.mark.parametrize("card", [1, 5, 300, 20000])
 @pytest.mark.parametrize("maintain_order", [False, True])
 @pytest.mark.parametrize("pack", [True, False])
-def test_two_int_keys_vs_oracle(gpu, card, maintain_order, pack, monkeypatch):
+def test_two_int_keys_vs_oracle(gpu, card, maintain_order, pack, plgpu_option):
     """Integer keys go through the exact packed Int64 key; PLGPU_NO_PACK
     forces the hash + verify path on the same data."""
     if not pack:
-        monkeypatch.setenv("PLGPU_NO_PACK", "1")
+        plgpu_option("no_pack", 1)
     rng = np.random.default_rng(card + 7)
     n = 150_000
     cols = _rand_frame(rng, n)
@@ -137,10 +137,10 @@ def test_key_count_and_single_non_int_key(gpu, nkeys):
 
 
 @pytest.mark.parametrize("pack", [True, False])
-def test_many_groups_and_special_hashes(gpu, pack, monkeypatch):
+def test_many_groups_and_special_hashes(gpu, pack, plgpu_option):
     """~1e6 distinct tuples over 2e6 rows (global-table path)."""
     if not pack:
-        monkeypatch.setenv("PLGPU_NO_PACK", "1")
+        plgpu_option("no_pack", 1)
     rng = np.random.default_rng(99)
     n = 2_000_000
     cols = {"a": (rng.standard_normal(n), None), "b": (rng.integers(-9, 9, n).astype(np.int64), None)}
@@ -152,11 +152,11 @@ def test_many_groups_and_special_hashes(gpu, pack, monkeypatch):
     assert info["groups"] > 600_000
 
 
-def test_collision_triggers_reseed(gpu, monkeypatch):
+def test_collision_triggers_reseed(gpu, plgpu_option):
     """A forced 3-bit first hash merges distinct tuples; the verify pass
     must catch it and the re-seeded run must be exact."""
-    monkeypatch.setenv("PLGPU_MK_COLLIDE", "1")
-    monkeypatch.setenv("PLGPU_NO_PACK", "1")  # integer keys would be packed exactly
+    plgpu_option("mk_collide", 1)
+    plgpu_option("no_pack", 1)  # integer keys would be packed exactly
     rng = np.random.default_rng(4)
     n = 30_000
     cols = _rand_frame(rng, n)

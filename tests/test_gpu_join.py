@@ -189,12 +189,10 @@ def test_join_large_properties(gpu):
                                              (2_000_003, 700_000, 1_500_000, False),
                                              (1_000_000, 450_000, 200_000, True)])
 @pytest.mark.parametrize("nulls_equal", [False, True])
-def test_join_partitioned_vs_oracle(gpu, nl, nr, card, dups, nulls_equal, monkeypatch):
-    """The partitioned probe (per-XCD L2 partition tables; maintain_order
-    "none"), forced on at every size: pairs as a multiset, bit-exact, with
-    null / INT64_MIN / INT64_MAX keys, duplicate build keys (CSR row lists)
-    and P from 8 to 32 partitions."""
-    monkeypatch.setenv("PLGPU_JOIN_PARTITIONED", "1")
+def test_join_unordered_vs_oracle(gpu, nl, nr, card, dups, nulls_equal):
+    """maintain_order "none" at sizes up to 2e6 x 7e5: pairs as a multiset,
+    bit-exact, with null / INT64_MIN / INT64_MAX keys and duplicate build
+    keys (CSR row lists)."""
     rng = np.random.default_rng(nl + nr + card)
     nf = 0.05 if nl < 500_000 else 1e-4  # nulls_equal joins every null pair: keep that product small
     # INT64_MIN / INT64_MAX keys at 1 % join as 1e4 x 1e4 blocks at the
@@ -218,15 +216,9 @@ def test_join_partitioned_vs_oracle(gpu, nl, nr, card, dups, nulls_equal, monkey
     assert np.array_equal(gl, ol[b]) and np.array_equal(gr, orr[b])
     assert np.array_equal(kv, lv[gl])
     assert np.array_equal(gk[kv], lk[gl][kv])
-    # the same join without the partitioned probe gives the same multiset
-    monkeypatch.setenv("PLGPU_JOIN_PARTITIONED", "0")
-    ref = left.join(right, on="k", nulls_equal=nulls_equal)
-    c = np.lexsort((ref["ri"].to_numpy(), ref["li"].to_numpy()))
-    assert np.array_equal(ref["li"].to_numpy()[c], gl) and np.array_equal(ref["ri"].to_numpy()[c], gr)
 
 
-def test_join_partitioned_int32_and_validation(gpu, monkeypatch):
-    monkeypatch.setenv("PLGPU_JOIN_PARTITIONED", "1")
+def test_join_int32_and_validation(gpu):
     rng = np.random.default_rng(4)
     pool = rng.integers(-2**31, 2**31 - 1, 20_000).astype(np.int32)
     lk = pool[rng.integers(0, pool.size, 100_000)]  # left keys repeat: 1:1 must fail
@@ -289,50 +281,3 @@ def test_join_row_format_table(gpu, unique, nulls_equal, order, pdtype):
         assert norm(zip(got_l.tolist(), out["p"].to_list())) == norm(
             zip(want_l.tolist(), [None if pvalid is not None and not pvalid[r] else pay[r].item()
                                   for r in want_r]))
-
-
-@pytest.mark.parametrize("case", ["plain", "many_parts", "nullable_probe", "dup_build", "min_build_key",
-                                  "f64_cols", "too_many_parts"])
-def test_join_xcd_partitioned(gpu, monkeypatch, case):
-    """The XCD-partitioned probe (opt-in xp_join: order-free inner join, unique
-    build keys, null-free 8-byte columns): the output rows equal the
-    oracle's pairs as a multiset, with every left column and the payload
-    taken at its pair.  Thresholds are lowered so the path runs at test
-    size; small sub-tables force hundreds of partitions; duplicate and
-    INT64_MIN build keys fall back to the other paths with the same result."""
-    monkeypatch.setenv("PLGPU_XP", "1")
-    monkeypatch.setenv("PLGPU_XP_MIN_PROBE", "1000")
-    monkeypatch.setenv("PLGPU_XP_MIN_BUILD", "100")
-    if case in ("many_parts", "nullable_probe", "f64_cols"):
-        monkeypatch.setenv("PLGPU_XP_CBITS", "8")   # 102 keys per sub-table
-    if case == "too_many_parts":
-        monkeypatch.setenv("PLGPU_XP_CBITS", "4")   # > 1024 sub-tables: falls back
-    rng = np.random.default_rng(len(case) * 31 + 7)
-    nl, nr = 700_003, 50_000
-    rk = (rng.permutation(400_000)[:nr].astype(np.int64) - 200_000) * 1_000_003
-    if case == "dup_build":
-        rk[10:20] = rk[0]
-    if case == "min_build_key":
-        rk[3] = np.iinfo(np.int64).min
-    lk = (rng.integers(0, 400_000, nl).astype(np.int64) - 200_000) * 1_000_003
-    lk[::97] = np.iinfo(np.int64).min   # never joins on this path (no such build key)
-    lv = None
-    if case == "nullable_probe":
-        lv = rng.random(nl) > 0.05
-    pay = np.arange(nr, dtype=np.int64) * 11 + 5
-    li = np.arange(nl, dtype=np.int64) * 3 - 1
-    if case == "f64_cols":
-        pay = pay.astype(np.float64) * 0.5
-        li = li.astype(np.float64) * -0.25
-    ol, orr = O.join_inner(O.HostCol(lk, lv), O.HostCol(rk, None), False)
-    left = pl.DataFrame({"k": pl.Series.from_numpy("k", lk, lv), "li": pl.Series.from_numpy("li", li)})
-    right = pl.DataFrame({"k": pl.Series.from_numpy("k", rk), "p": pl.Series.from_numpy("p", pay)})
-    out = left.join(right, on="k", maintain_order="none")
-    assert out.columns == ["k", "li", "p"]
-    assert out.height == len(ol)
-    got = np.stack([out["k"].to_numpy().view(np.int64), out["li"].to_numpy().view(np.int64),
-                    out["p"].to_numpy().view(np.int64)], axis=1)
-    want = np.stack([lk[ol], li[ol].view(np.int64), pay[orr].view(np.int64)], axis=1)
-    got = got[np.lexsort(got.T[::-1])]
-    want = want[np.lexsort(want.T[::-1])]
-    assert np.array_equal(got, want)

@@ -61,11 +61,11 @@ def _df(keys, names, idxname):
 @pytest.mark.parametrize("nulls_equal", [False, True])
 @pytest.mark.parametrize("order", ["none", "left", "right", "left_right", "right_left"])
 @pytest.mark.parametrize("pack", [True, False])
-def test_join_multi_pairs_vs_oracle(gpu, nl, nr, card, nkeys, nulls_equal, order, pack, monkeypatch):
+def test_join_multi_pairs_vs_oracle(gpu, nl, nr, card, nkeys, nulls_equal, order, pack, plgpu_option):
     """Key sets without Float64 pack into one exact Int64 key; PLGPU_NO_PACK
     forces the hash + pair-verify path."""
     if not pack:
-        monkeypatch.setenv("PLGPU_NO_PACK", "1")
+        plgpu_option("no_pack", 1)
     rng = np.random.default_rng(nl + 3 * nr + card + nkeys)
     lk, rk = _keys(rng, nl, card)[:nkeys], _keys(rng, nr, card)[:nkeys]
     names = ["a", "b", "f", "t"][:nkeys]
@@ -99,11 +99,11 @@ def test_join_multi_validate_and_errors(gpu):
         left.join(f, on=["a", "b"])
 
 
-def test_join_multi_left_right_on_and_collisions(gpu, monkeypatch):
+def test_join_multi_left_right_on_and_collisions(gpu, plgpu_option):
     """Different key names per side; a forced 3-bit first hash must be
     caught by the pair verification and re-run."""
-    monkeypatch.setenv("PLGPU_MK_COLLIDE", "1")
-    monkeypatch.setenv("PLGPU_NO_PACK", "1")
+    plgpu_option("mk_collide", 1)
+    plgpu_option("no_pack", 1)
     rng = np.random.default_rng(2)
     lk, rk = _keys(rng, 5000, 30), _keys(rng, 700, 30)
     ol, orr = O.join_inner_multi(lk[:3], rk[:3], False)

@@ -556,11 +556,11 @@ def test_sum_wide_with_program_predicate(gpu):
 
 
 @pytest.mark.parametrize("layout", ["sorted", "runs_forced_random", "sorted_specials", "sorted_part"])
-def test_group_by_register_accumulators(gpu, layout, monkeypatch):
+def test_group_by_register_accumulators(gpu, layout, plgpu_option):
     """Sorted / clustered keys: the plan sees adjacent equal keys and the
     fused kernel's lanes sum rows of a group they already hold in a register
     accumulator (flushed into the LDS table on a group change and at the
-    end); PLGPU_RUNS=1 forces that variant on random keys, specials mix its
+    end); option runs=1 forces that variant on random keys, specials mix its
     rows with the per-row path, and "sorted_part" runs the partitioned
     kernel's 4-slot form on sorted many-groups keys.  Exact vs the oracle."""
     rng = np.random.default_rng(len(layout) + 77)
@@ -574,7 +574,7 @@ def test_group_by_register_accumulators(gpu, layout, monkeypatch):
         d[rng.random(n) < 0.001] = -0.0
     key = rng.integers(0, card, n).astype(np.int64) * 7919 - 3
     if layout == "runs_forced_random":
-        monkeypatch.setenv("PLGPU_RUNS", "1")
+        plgpu_option("runs", 1)
     else:
         key = np.sort(key)
     cols = {"a": (a, None), "d": (d, None)}

@@ -144,7 +144,7 @@ def test_join_string_key(gpu, how, nl, nr, card, nulls_equal, short):
         assert p.tolist() == [rw[j] if j >= 0 and rv[j] else None for j in orr]
 
 
-def test_multi_key_with_string(gpu, monkeypatch):
+def test_multi_key_with_string(gpu, plgpu_option):
     rng = np.random.default_rng(5)
     n, m = 50_000, 8000
     lw, lv = _words(rng, n, 30)
@@ -176,7 +176,7 @@ def test_multi_key_with_string(gpu, monkeypatch):
     assert np.array_equal(g["a"].to_numpy(), okeys[1][0])
     assert np.array_equal(g["len"].to_numpy(), outs[0][0])
     # collisions forced: byte-exact verification must catch them
-    monkeypatch.setenv("PLGPU_MK_COLLIDE", "1")
+    plgpu_option("mk_collide", 1)
     g2 = left.group_by("w", "a", maintain_order=True).agg(pl.len())
     assert g2["w"].to_list() == g["w"].to_list() and np.array_equal(g2["len"].to_numpy(), g["len"].to_numpy())
     out2 = left.join(right, on=["w", "a"], how="left", maintain_order="left_right")

@@ -199,14 +199,14 @@ def _mkeys(rng, n, card):
 @pytest.mark.parametrize("nulls_equal", [False, True])
 @pytest.mark.parametrize("how", HOWS)
 @pytest.mark.parametrize("pack", [True, False])
-def test_join_types_multi_vs_oracle(gpu, nl, nr, card, nkeys, nulls_equal, how, pack, monkeypatch):
+def test_join_types_multi_vs_oracle(gpu, nl, nr, card, nkeys, nulls_equal, how, pack, plgpu_option):
     """Integer tuples pack into one Int64 key; Float64 keys (nkeys=3) or
     PLGPU_NO_PACK take the hashed path with pair verification (semi / anti
     through a verified left join)."""
     import polaroid_amd as pl
 
     if not pack:
-        monkeypatch.setenv("PLGPU_NO_PACK", "1")
+        plgpu_option("no_pack", 1)
     rng = np.random.default_rng(nl + 3 * nr + card + nkeys + len(how))
     lk, rk = _mkeys(rng, nl, card)[:nkeys], _mkeys(rng, nr, card)[:nkeys]
     names = ["a", "b", "f"][:nkeys]
@@ -226,13 +226,13 @@ def test_join_types_multi_vs_oracle(gpu, nl, nr, card, nkeys, nulls_equal, how, 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("how", HOWS)
-def test_join_types_hash_collisions(gpu, how, monkeypatch):
+def test_join_types_hash_collisions(gpu, how, plgpu_option):
     """A forced 3-bit first tuple hash: every type must detect the false
     matches through pair verification and re-run."""
     import polaroid_amd as pl
 
-    monkeypatch.setenv("PLGPU_MK_COLLIDE", "1")
-    monkeypatch.setenv("PLGPU_NO_PACK", "1")
+    plgpu_option("mk_collide", 1)
+    plgpu_option("no_pack", 1)
     rng = np.random.default_rng(9)
     lk, rk = _mkeys(rng, 4000, 30), _mkeys(rng, 600, 30)
     names = ["a", "b", "f"]

@@ -5,8 +5,9 @@
 An OHLCV-shaped table (symbol i64, open/high/low/close f64 with 1 % nulls
 in `close`) is cut into RecordBatches of --chunk rows, the form in which
 PyDataFrame.to_arrow hands a frame over (crates/polars-python/src/
-dataframe/export.rs:80).  Times, in one child process per PLGPU_INGEST_MODE (pageable / staged /
-register, see polaroid_amd/csrc/ingest.hip):
+dataframe/export.rs:80).  Times (the pinned-staging and page-registering
+copy modes measured in profiles/r02_ingest.jsonl were removed from the
+library as no faster, see polaroid_amd/csrc/ingest.hip):
   staged_ms  DataFrame.from_batches: plgpu_column_alloc + plgpu_ingest_chunk
           per chunk and column (bitmaps placed on the device), one
           synchronisation at the end;
@@ -33,18 +34,7 @@ def main():
     ap.add_argument("--rows", type=float, default=1e8)
     ap.add_argument("--chunk", type=int, default=1 << 20)
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--modes", default="staged,pageable,register",
-                    help="PLGPU_INGEST_MODE values to time (each in a child process)")
-    ap.add_argument("--child", action="store_true")
     args = ap.parse_args()
-    if not args.child:
-        import subprocess
-
-        for mode in args.modes.split(","):
-            env = dict(os.environ, PLGPU_INGEST_MODE=mode)
-            subprocess.run([sys.executable, __file__, "--child", "--rows", str(args.rows), "--chunk",
-                            str(args.chunk), "--reps", str(args.reps)], env=env, check=True)
-        return
     import pyarrow as pa
 
     import polaroid_amd as pl
@@ -81,7 +71,7 @@ def main():
         del bufs
     ts, tp = min(staged), min(pageable)
     print(json.dumps({
-        "bench": "arrow ingestion host->HBM", "mode": os.environ.get("PLGPU_INGEST_MODE", "staged"), "rows": n, "chunk_rows": args.chunk, "batches": len(batches),
+        "bench": "arrow ingestion host->HBM", "mode": "pageable", "rows": n, "chunk_rows": args.chunk, "batches": len(batches),
         "bytes": nbytes, "staged_ms": round(ts * 1e3, 2), "staged_GBps": round(nbytes / ts / 1e9, 2),
         "pageable_whole_column_ms": round(tp * 1e3, 2), "pageable_GBps": round(n * 40 / tp / 1e9, 2),
     }), flush=True)
