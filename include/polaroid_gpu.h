@@ -179,6 +179,17 @@ typedef struct plgpu_agg {
     int32_t col;  /* input column index */
 } plgpu_agg;
 
+/* An aggregation input computed from the columns: the elementwise
+ * expression under an aggregation (`(close * volume).sum()`), which the
+ * reference's partitionable group-by pre-aggregates directly
+ * (polars-plan/src/plans/aexpr/properties/general.rs:335 can_pre_agg).
+ * `program` is an expression program over the call's columns. */
+typedef struct plgpu_agg_input {
+    const plgpu_instr* program;
+    int32_t n_instr;
+    int32_t _pad;
+} plgpu_agg_input;
+
 /* Diagnostics of one group-by call (for tests / bench / rocprof cross-check). */
 typedef struct plgpu_groupby_info {
     int64_t rows_in;
@@ -315,6 +326,24 @@ int plgpu_group_by_agg_multi(const plgpu_column* keys, int32_t nkeys, const plgp
                              const plgpu_agg* aggs, int32_t naggs, int32_t maintain_order,
                              plgpu_column* out_keys, plgpu_column* out_aggs,
                              plgpu_groupby_info* info, void* stream);
+
+/* The general form of both: 0..8 key columns, and aggregations over the
+ * columns or over computed inputs.  An agg.col >= ncols names
+ * inputs[agg.col - ncols], an elementwise expression over the columns (see
+ * plgpu_agg_input): `x op y` of two Float64 columns or a column and a
+ * literal (+ - * /) is computed in registers by the fused kernel; any other
+ * expression is evaluated once into a column first.
+ * nkeys == 0 is a global reduction, `lf.filter(p).select(aggs)`
+ * (polars-expr/src/reduce/sum.rs:112 reduce_ca and its siblings): every
+ * selected row in one group, and one output row even when no row is
+ * selected (sum / len / count 0, the other aggregations null, as the
+ * reference's empty reductions); `out_keys` is not written.  `ncols` must be
+ * >= 1 then, to give the length. */
+int plgpu_group_by_agg_ex(const plgpu_column* keys, int32_t nkeys, const plgpu_column* cols, int32_t ncols,
+                          const plgpu_agg_input* inputs, int32_t ninputs, const plgpu_instr* program,
+                          int32_t n_instr, const plgpu_agg* aggs, int32_t naggs, int32_t maintain_order,
+                          plgpu_column* out_keys, plgpu_column* out_aggs, plgpu_groupby_info* info,
+                          void* stream);
 
 
 /* ---- hash-partitioned group-by (one process per GPU) ----------------------

@@ -197,6 +197,48 @@ def group_by_agg(key: HostCol, cols: list[HostCol], program, aggs: list[tuple[st
                                                        for o, v in zip(outs, outv)]
 
 
+def _input_col(cols: list[HostCol], program, nrows: int, kinds: set) -> HostCol:
+    """One computed aggregation input: the program evaluated by or_eval (the
+    elementwise restatement).  A Boolean input sums as IdxSize counts
+    (polars-expr/src/reduce/sum.rs:147-180 BoolSumReducer) and averages as
+    0 / 1 Float64 (reduce/mean.rs)."""
+    dt, v, valid = eval_program(cols, program, nrows)
+    if dt == BOOL:
+        v = v.astype(np.float64 if "mean" in kinds else np.uint32)
+    return HostCol(np.ascontiguousarray(v), valid)
+
+
+def group_by_agg_inputs(key: HostCol | None, cols: list[HostCol], program, inputs: list, aggs: list[tuple[str, int]],
+                        nrows: int, sum_mode: int = SUM_EXACT):
+    """Aggregations over computed inputs, the partitionable group-by's
+    pre-aggregated expressions (polars-plan/src/plans/aexpr/properties/
+    general.rs:303-356 can_pre_agg: Agg over BinaryExpr / Ternary / Cast /
+    elementwise Function): each input program is evaluated over every row by
+    or_eval and aggregated as a column (agg column index len(cols) + j names
+    inputs[j]).  key None: a global reduction (select(aggs); reduce/sum.rs:112
+    reduce_ca and siblings), one group -- and one output row even when no row
+    is selected: sum / len / count 0, mean / min / max / first / last null
+    (the reducers' init values, reduce/sum.rs:94, len.rs, count.rs; mean and
+    min / max finish an empty state as null).  Returns (keys, key_valid,
+    [(values, valid)]) like group_by_agg."""
+    nc = len(cols)
+    extra = []
+    for j, prog in enumerate(inputs):
+        kinds = {k for k, c in aggs if c == nc + j}
+        extra.append(_input_col(cols, prog, nrows, kinds))
+    allc = list(cols) + extra
+    k = key if key is not None else HostCol(np.zeros(nrows, np.int64))
+    keys, kvalid, outs = group_by_agg(k, allc, program, aggs, nrows, sum_mode)
+    if key is None and keys.shape[0] == 0:
+        keys, kvalid = np.zeros(1, np.int64), np.ones(1, bool)
+        empty = []
+        for (kind, ci), (o, _) in zip(aggs, outs):
+            ok = kind in ("sum", "len", "count")
+            empty.append((np.zeros(1, o.dtype), np.array([ok])))
+        outs = empty
+    return keys, kvalid, outs
+
+
 def _row_words(values: np.ndarray, valid: np.ndarray | None) -> np.ndarray:
     """One key column as 2 uint64 words per row (validity, canonical value):
     the unordered row encoding of polars-core/src/chunked_array/ops/

@@ -69,6 +69,11 @@ class Agg(C.Structure):
     _fields_ = [("kind", C.c_int32), ("col", C.c_int32)]
 
 
+class AggInput(C.Structure):
+    """plgpu_agg_input: an aggregation input given as a program over the columns."""
+    _fields_ = [("program", C.POINTER(Instr)), ("n_instr", C.c_int32), ("_pad", C.c_int32)]
+
+
 class GroupByInfo(C.Structure):
     _fields_ = [
         ("rows_in", C.c_int64),
@@ -120,6 +125,9 @@ SIGNATURES = {
     "plgpu_group_by_agg_multi": (C.c_int, [_COLP, C.c_int32, _COLP, C.c_int32, C.POINTER(Instr), C.c_int32,
                                            C.POINTER(Agg), C.c_int32, C.c_int32, _COLP, _COLP,
                                            C.POINTER(GroupByInfo), _P]),
+    "plgpu_group_by_agg_ex": (C.c_int, [_COLP, C.c_int32, _COLP, C.c_int32, C.POINTER(AggInput), C.c_int32,
+                                        C.POINTER(Instr), C.c_int32, C.POINTER(Agg), C.c_int32, C.c_int32, _COLP,
+                                        _COLP, C.POINTER(GroupByInfo), _P]),
     "plgpu_gb_record_words": (C.c_int, [_COLP, C.c_int32, C.POINTER(Agg), C.c_int32,
                                         C.POINTER(C.c_int32)]),
     "plgpu_gb_plan_bottoms": (C.c_int, [_COLP, _COLP, C.c_int32, C.POINTER(Agg), C.c_int32,

@@ -77,8 +77,16 @@ enum : int {
     ST_WORDS = 24
 };
 
+// An aggregation input derived from the columns in registers (an
+// elementwise expression under the aggregation, polars-plan/src/plans/
+// aexpr/properties/general.rs:335 can_pre_agg): value = x op y with x the
+// acc's column, y a second Float64 column (c2) or a literal (dimm); every
+// other expression is materialised by the host before the pass.
+enum : int32_t { DOP_NONE = 0, DOP_ADD = 1, DOP_SUB = 2, DOP_MUL = 3, DOP_DIV = 4, DOP_DIVS = 5,
+                 DOP_OPMASK = 7, DOP_SWAP = 8, DOP_LIT = 16 };
+
 struct AccSpec {
-    DevCol c;         // the aggregated column
+    DevCol c;         // the aggregated column (derived: the first operand column)
     int32_t flags;
     int32_t isf;      // column is f64 (compared / summed as f64)
     int32_t f_sum;    // FSUM/FSUMCAST: 3 limb fields
@@ -88,7 +96,9 @@ struct AccSpec {
     int32_t f_max;
     int32_t f_flags;
     int32_t uns;      // UInt64 column: min / max order and f64 conversion are unsigned
-    int32_t _pad;
+    int32_t dop;      // DOP_*: derived input (0: the column itself)
+    DevCol c2;        // derived: the second operand column (unless DOP_LIT)
+    uint64_t dimm;    // derived: the literal operand's f64 bits (DOP_LIT)
 };
 
 struct GbParams {
@@ -155,6 +165,40 @@ __device__ __forceinline__ constexpr bool gb_ok(bool, uint32_t) { return true; }
 #endif
 
 // ------------------------------------------------------------ helpers
+// Derived input: x op y in f64 (DOP_SWAP: y op x; DOP_DIVS: a * (1 / b), the
+// scalar-divisor form, polars-compute/src/arithmetic/float.rs:78).  The
+// library is built with -ffp-contract=off: one IEEE rounding per operation,
+// as the reference's elementwise kernel.
+__device__ __forceinline__ uint64_t derive(int32_t dop, uint64_t x, uint64_t y) {
+    const double xa = as_f64(x), ya = as_f64(y);
+    const double a = (dop & DOP_SWAP) ? ya : xa, b = (dop & DOP_SWAP) ? xa : ya;
+    double r;
+    switch (dop & DOP_OPMASK) {
+    case DOP_ADD: r = a + b; break;
+    case DOP_SUB: r = a - b; break;
+    case DOP_MUL: r = a * b; break;
+    case DOP_DIV: r = a / b; break;
+    default: r = a * (1.0 / b); break;
+    }
+    return f64_bits(r);
+}
+
+// Aggregation input of row r (register form) and its validity.
+__device__ __forceinline__ uint64_t acc_value(const AccSpec& ac, int64_t r, bool& valid) {
+    valid = dev_valid(ac.c, r);
+    const uint64_t x = dev_load(ac.c, r);
+    if (ac.dop == DOP_NONE) return x;
+    if (ac.dop & DOP_LIT) return derive(ac.dop, x, ac.dimm);
+    valid = valid && dev_valid(ac.c2, r);
+    return derive(ac.dop, x, dev_load(ac.c2, r));
+}
+
+// Group key of row r: `values` NULL is the keyless form (a global
+// reduction, select(agg...)): every row in the one group 0.
+__device__ __forceinline__ uint64_t key_at(const DevCol& k, int64_t r) {
+    return k.values ? dev_load(k, r) : 0ull;
+}
+
 __device__ __forceinline__ uint64_t lds_load(uint64_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
@@ -526,8 +570,12 @@ __global__ __launch_bounds__(kGbThreads) void gb_kernel(GbParams p, DevProgram p
         const int64_t r2 = r0 + 2 * T;
         uint64_t key[4], pv[4];
         uint64_t v[kMaxAcc][4];
-        load_pair(p.key, r0, n, key[0], key[1]);
-        load_pair(p.key, r2, n, key[2], key[3]);
+        if (p.key.values) {
+            load_pair(p.key, r0, n, key[0], key[1]);
+            load_pair(p.key, r2, n, key[2], key[3]);
+        } else {
+            key[0] = key[1] = key[2] = key[3] = 0;  // keyless: one group
+        }
 #pragma unroll
         for (int a = 0; a < kMaxAcc; ++a) {
             if (a < nacc) {
@@ -858,10 +906,11 @@ __global__ __launch_bounds__(kPartThreads) void gb_part_scatter_kernel(GbParams 
 // tail and every other case go through gb_kernel.  Loads of the next tile
 // are issued before the current tile's LDS atomics, so HBM reads overlap
 // the aggregation.
-template <int NACC, int ROWS>
+template <int NACC, int ROWS, bool DERIV = false>
 struct FastTile {
     uint64_t key[ROWS];
     uint64_t v[NACC > 0 ? NACC : 1][ROWS];
+    uint64_t w[DERIV && NACC > 0 ? NACC : 1][ROWS];  // DERIV: second operand columns
     uint64_t pv[ROWS];
 };
 
@@ -883,42 +932,55 @@ __device__ __forceinline__ u64x2_t ld16(const uint64_t* p) {
 // The rows after the last full tile (fewer than one tile): one more, masked
 // tile of guarded single-row loads (rows >= n read as 0 and are not
 // selected), so the fused kernel covers every row in one launch.
-template <int NACC, int PRED, int ROWS>
-__device__ __forceinline__ void fast_load_tail(const GbParams& p, int64_t t, FastTile<NACC, ROWS>& x) {
+template <int NACC, int PRED, int ROWS, bool DERIV>
+__device__ __forceinline__ void fast_load_tail(const GbParams& p, int64_t t, FastTile<NACC, ROWS, DERIV>& x) {
     const int T = blockDim.x;
     const uint64_t* kp = (const uint64_t*)p.key.values + p.key.offset;
 #pragma unroll
     for (int j = 0; j < ROWS; ++j) {
         const int64_t r = fast_row(t, T, ROWS, j);
         const bool in = r < p.n;
-        x.key[j] = in ? kp[r] : 0ull;
+        x.key[j] = in && p.key.values ? kp[r] : 0ull;
 #pragma unroll
-        for (int c = 0; c < NACC; ++c)
+        for (int c = 0; c < NACC; ++c) {
             x.v[c][j] = in ? ((const uint64_t*)p.acc[c].c.values + p.acc[c].c.offset)[r] : 0ull;
+            if (DERIV && p.acc[c].dop != DOP_NONE && !(p.acc[c].dop & DOP_LIT))
+                x.w[c][j] = in ? ((const uint64_t*)p.acc[c].c2.values + p.acc[c].c2.offset)[r] : 0ull;
+        }
         if (PRED == 1 && p.pred_acc < 0) x.pv[j] = in ? ((const uint64_t*)p.pred_col.values + p.pred_col.offset)[r] : 0ull;
     }
 }
 
 // rbase: first row of tile 0 (even); rmax >= 0: row pairs beyond it are
 // clamped to it (the partitioned buffers end a pair after the last row).
-template <int NACC, int PRED, int ROWS, bool NT = false>
-__device__ __forceinline__ void fast_load(const GbParams& p, int64_t t, FastTile<NACC, ROWS>& x, int64_t rbase = 0,
-                                          int64_t rmax = -1) {
+template <int NACC, int PRED, int ROWS, bool NT, bool DERIV>
+__device__ __forceinline__ void fast_load(const GbParams& p, int64_t t, FastTile<NACC, ROWS, DERIV>& x,
+                                          int64_t rbase = 0, int64_t rmax = -1) {
     const int T = blockDim.x;
     const uint64_t* kp = (const uint64_t*)p.key.values + p.key.offset;
 #pragma unroll
     for (int q = 0; q < ROWS / 2; ++q) {
         int64_t r = rbase + fast_row(t, T, ROWS, 2 * q);
         if (rmax >= 0) r = r < rmax ? r : rmax;
-        const u64x2_t a = ld16<NT>(kp + r);
-        x.key[2 * q] = a.x;
-        x.key[2 * q + 1] = a.y;
+        if (p.key.values) {
+            const u64x2_t a = ld16<NT>(kp + r);
+            x.key[2 * q] = a.x;
+            x.key[2 * q + 1] = a.y;
+        } else {
+            x.key[2 * q] = x.key[2 * q + 1] = 0;  // keyless: one group
+        }
 #pragma unroll
         for (int c = 0; c < NACC; ++c) {
             const uint64_t* vp = (const uint64_t*)p.acc[c].c.values + p.acc[c].c.offset;
             const u64x2_t b = ld16<NT>(vp + r);
             x.v[c][2 * q] = b.x;
             x.v[c][2 * q + 1] = b.y;
+            if (DERIV && p.acc[c].dop != DOP_NONE && !(p.acc[c].dop & DOP_LIT)) {
+                const uint64_t* wp = (const uint64_t*)p.acc[c].c2.values + p.acc[c].c2.offset;
+                const u64x2_t w = ld16<NT>(wp + r);
+                x.w[c][2 * q] = w.x;
+                x.w[c][2 * q + 1] = w.y;
+            }
         }
         if (PRED == 1 && p.pred_acc < 0) {
             const uint64_t* pp = (const uint64_t*)p.pred_col.values + p.pred_col.offset;
@@ -950,7 +1012,10 @@ __device__ __forceinline__ void fast_load(const GbParams& p, int64_t t, FastTile
 // after the last full tile as one masked tile (fast_load_tail).
 // (Measured and removed variants -- no prefetch, default-policy loads,
 // 80-VGPR caps, 4 rows per thread -- are logged in DESIGN.md.)
-template <int NACC, int PRED, bool SUMONLY, int ROWS, int LIMBS = 3, bool RUNS = false, bool PART = false>
+// DERIV: some accs are derived inputs (x op y, AccSpec.dop), computed in
+// registers from the loaded operand columns as each row is applied.
+template <int NACC, int PRED, bool SUMONLY, int ROWS, int LIMBS = 3, bool RUNS = false, bool PART = false,
+          bool DERIV = false>
 __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProgram prog) {
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
     constexpr int NA = NACC > 0 ? NACC : 1;
@@ -974,6 +1039,13 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
     uint64_t dd0[NA];
     int bot0[NA];
     load_descs(p, dd0, bot0);
+    int32_t dop0[NA];
+    uint64_t dim0[NA];
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+        dop0[a] = DERIV && a < NACC ? p.acc[a].dop : DOP_NONE;
+        dim0[a] = DERIV && a < NACC ? p.acc[a].dimm : 0ull;
+    }
     __syncthreads();
 
     const int T = blockDim.x;
@@ -994,9 +1066,9 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
         t = blockIdx.x % p.part_blocks;
         tstep = p.part_blocks;
     }
-    auto load_tile = [&](int64_t tt, FastTile<NACC, ROWS>& x) {
-        if (PART || tt < ntiles) fast_load<NACC, PRED, ROWS, true>(p, tt, x, rbase, rmax);
-        else fast_load_tail<NACC, PRED, ROWS>(p, tt, x);
+    auto load_tile = [&](int64_t tt, FastTile<NACC, ROWS, DERIV>& x) {
+        if (PART || tt < ntiles) fast_load<NACC, PRED, ROWS, true, DERIV>(p, tt, x, rbase, rmax);
+        else fast_load_tail<NACC, PRED, ROWS, DERIV>(p, tt, x);
     };
     constexpr uint32_t VM = (1u << NACC) - 1u;
     // RACC (partition buffers, sum-only, 2 limbs): each lane keeps KR
@@ -1030,7 +1102,7 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
         }
         rs[k] = -1;
     };
-    FastTile<NACC, ROWS> cur;
+    FastTile<NACC, ROWS, DERIV> cur;
     if (t < nall) load_tile(t, cur);
     for (; t < nall; t += tstep) {
         // ---- predicate + batched LDS probes of the tile's rows
@@ -1061,7 +1133,7 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
         for (int j = 0; j < ROWS; ++j)
             if (slot[j] == kGlobalKey && probe[j] == cur.key[j]) slot[j] = (int)h[j];
         // ---- next tile's loads go out before this tile's atomics
-        FastTile<NACC, ROWS> nxt;
+        FastTile<NACC, ROWS, DERIV> nxt;
         const int64_t tn = t + tstep;
         if (tn < nall) load_tile(tn, nxt);
         // ---- apply rows one at a time (rolled; arrays shift statically)
@@ -1076,6 +1148,8 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
 #pragma unroll
                 for (int a = 0; a < NA; ++a) {
                     rv[a] = cur.v[a][0];
+                    if (DERIV && dop0[a] != DOP_NONE)
+                        rv[a] = derive(dop0[a], cur.v[a][0], (dop0[a] & DOP_LIT) ? dim0[a] : cur.w[a][0]);
                     dd[a] = dd0[a];
                     bot[a] = bot0[a];
                 }
@@ -1184,7 +1258,10 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
                 slot[i] = slot[i + 1];
                 cur.key[i] = cur.key[i + 1];
 #pragma unroll
-                for (int a = 0; a < NACC; ++a) cur.v[a][i] = cur.v[a][i + 1];
+                for (int a = 0; a < NACC; ++a) {
+                    cur.v[a][i] = cur.v[a][i + 1];
+                    if (DERIV) cur.w[a][i] = cur.w[a][i + 1];
+                }
             }
         }
         cur = nxt;
@@ -1235,8 +1312,9 @@ __global__ __launch_bounds__(256) void gb_maxexp_kernel(GbParams p, int a) {
     const AccSpec& ac = p.acc[a];
     uint32_t mx = 0, inv_mn = 0;  // inv_mn = 0x7FF - (smallest exponent of a nonzero finite value)
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < p.n; r += (int64_t)gridDim.x * blockDim.x) {
-        if (!dev_valid(ac.c, r)) continue;
-        uint64_t x = dev_load(ac.c, r);
+        bool valid;
+        uint64_t x = acc_value(ac, r, valid);
+        if (!valid) continue;
         if (ac.flags & A_FSUMCAST) x = f64_bits((double)(int64_t)x);
         const uint32_t ex = (uint32_t)(x >> 52) & 0x7FF;
         if (ex != 0x7FF && ex > mx) mx = ex;
@@ -1270,7 +1348,9 @@ __global__ __launch_bounds__(256) void gb_wide_kernel(GbParams p, DevProgram pro
     const AccSpec& ac = p.acc[a];
     constexpr uint64_t M24 = (1ull << kWideDigit) - 1;
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < p.n; r += (int64_t)gridDim.x * blockDim.x) {
-        if (!dev_valid(ac.c, r)) continue;
+        bool valid;
+        uint64_t x = acc_value(ac, r, valid);
+        if (!valid) continue;
         if (PRED == 1) {
             if (!dev_valid(p.pred_col, r)) continue;
             if (!simple_pred(prog.simple_isf, prog.simple_op, dev_load(p.pred_col, r), prog.simple_imm)) continue;
@@ -1278,7 +1358,6 @@ __global__ __launch_bounds__(256) void gb_wide_kernel(GbParams p, DevProgram pro
             const RowVal rv = eval_row(prog.code, prog.n, p.cols, r);
             if (!(rv.valid && (rv.v & 1))) continue;
         }
-        uint64_t x = dev_load(ac.c, r);
         if (ac.flags & A_FSUMCAST) x = f64_bits((double)(int64_t)x);
         uint32_t ex = (uint32_t)(x >> 52) & 0x7FF;
         uint64_t m = x & 0x000FFFFFFFFFFFFFull;
@@ -1289,7 +1368,7 @@ __global__ __launch_bounds__(256) void gb_wide_kernel(GbParams p, DevProgram pro
         if (!dev_valid(p.key, r)) {
             gs = p.gcap;
         } else {
-            const uint64_t k = dev_load(p.key, r);
+            const uint64_t k = key_at(p.key, r);
             gs = k == kEmptyKey ? p.gcap + 1 : g_find(p, k);
         }
         if (gs < 0) continue;
@@ -1413,9 +1492,9 @@ __global__ __launch_bounds__(kPlanThreads) void gb_plan_kernel(GbParams p, uint6
             const int64_t i = i0 + (int64_t)u * blockDim.x;
             const int64_t r = plan_row(i, n, samples);
             okb[u] = i < s1 && r < n && dev_valid(p.key, r);
-            kb[u] = okb[u] ? dev_load(p.key, r) : 0;
+            kb[u] = okb[u] ? key_at(p.key, r) : 0;
             const bool nx = okb[u] && r + 1 < n && dev_valid(p.key, r + 1);
-            runs += (nx && dev_load(p.key, r + 1) == kb[u]) ? 1u : 0u;
+            runs += (nx && key_at(p.key, r + 1) == kb[u]) ? 1u : 0u;
           }
 #pragma unroll 1
           for (int u = 0; u < kPlanBatch; ++u) {
@@ -1462,7 +1541,6 @@ __global__ __launch_bounds__(kPlanThreads) void gb_plan_kernel(GbParams p, uint6
     const AccSpec& ac = p.acc[a];
     uint32_t mx = 0, mn = 0x7FF;
     if (ac.flags & (A_FSUM | A_FSUMCAST)) {
-        const DevCol& c = ac.c;
         for (int64_t i0 = s0 + threadIdx.x; i0 < s1; i0 += (int64_t)blockDim.x * kPlanBatch) {
             uint64_t xb[kPlanBatch];
             bool okb[kPlanBatch];
@@ -1470,8 +1548,9 @@ __global__ __launch_bounds__(kPlanThreads) void gb_plan_kernel(GbParams p, uint6
             for (int u = 0; u < kPlanBatch; ++u) {
                 const int64_t i = i0 + (int64_t)u * blockDim.x;
                 const int64_t r = plan_row(i, n, samples);
-                okb[u] = i < s1 && r < n && dev_valid(c, r);
-                xb[u] = okb[u] ? dev_load(c, r) : 0;
+                bool v = false;
+                xb[u] = (i < s1 && r < n) ? acc_value(ac, r, v) : 0;
+                okb[u] = i < s1 && r < n && v;
             }
 #pragma unroll
             for (int u = 0; u < kPlanBatch; ++u) {
@@ -1619,8 +1698,8 @@ __global__ void gb_finalize_kernel(GbParams p, FinParams fp) {
                     valid = false;
                     break;
                 }
-                valid = dev_valid(ac.c, row);
-                const uint64_t v = valid ? dev_load(ac.c, row) : 0ull;
+                const uint64_t v0 = acc_value(ac, row, valid);
+                const uint64_t v = valid ? v0 : 0ull;
                 dev_store(os.values, os.out_dtype, g, v);
                 break;
             }
@@ -1812,9 +1891,31 @@ struct Plan {
     mutable int launched_grid;  // grid of the last fast launch (info)
 };
 
-static int plan_groupby(const plgpu_column* key, const plgpu_column* cols, int32_t ncols, const plgpu_agg* aggs,
-                        int32_t naggs, bool maintain_order, const DevProgram& dp, Plan* pl,
-                        bool force_counts = false) {
+// One aggregation input (plan_groupby): a column, or a derived value x op y
+// computed in registers (DOP_*, both operands Float64).
+struct InSpec {
+    plgpu_column col;   // the column (derived: the first operand)
+    plgpu_column col2;  // derived: the second operand column (unless DOP_LIT)
+    int32_t dtype;      // dtype of the input (derived: Float64)
+    int32_t dop;        // DOP_NONE: the column itself
+    uint64_t imm;       // DOP_LIT: the literal's f64 bits
+};
+
+static std::vector<InSpec> column_inputs(const plgpu_column* cols, int32_t ncols) {
+    std::vector<InSpec> v((size_t)std::max(ncols, 0));
+    for (int i = 0; i < ncols; ++i) {
+        std::memset(&v[i], 0, sizeof v[i]);
+        v[i].col = cols[i];
+        v[i].dtype = cols[i].dtype;
+    }
+    return v;
+}
+
+// Aggregations `aggs` (agg.col indexes `ins`) -> accumulators, table fields
+// and output specs.  `cols` are the columns the predicate program reads.
+static int plan_groupby(const plgpu_column* key, const plgpu_column* cols, int32_t ncols, const InSpec* ins,
+                        int32_t nins, const plgpu_agg* aggs, int32_t naggs, bool maintain_order, const DevProgram& dp,
+                        Plan* pl, bool force_counts = false) {
     GbParams& p = pl->p;
     std::memset(&p, 0, sizeof p);
     p.key = to_dev(*key);
@@ -1830,13 +1931,13 @@ static int plan_groupby(const plgpu_column* key, const plgpu_column* cols, int32
     p.f_first = (maintain_order || any_first) ? nf++ : -1;
     if (p.f_first >= 0) p.min_init_mask |= 1ull << p.f_first;
     p.f_last = any_last ? nf++ : -1;
-    int acc_of_col[PLGPU_MAX_COLS];
-    for (int i = 0; i < PLGPU_MAX_COLS; ++i) acc_of_col[i] = -1;
+    std::vector<int> acc_of_col((size_t)std::max(nins, 1), -1);
     p.nacc = 0;
     for (int i = 0; i < naggs; ++i) {
         const int c = aggs[i].col;
-        if (c < 0 || c >= ncols) return fail(PLGPU_ERR_INVALID, "aggregation column index out of range");
-        const int32_t dt = cols[c].dtype;
+        if (c < 0 || c >= nins) return fail(PLGPU_ERR_INVALID, "aggregation column index out of range");
+        const InSpec& in = ins[c];
+        const int32_t dt = in.dtype;
         if (!dtype_is_int(dt) && !dtype_is_float(dt))
             return fail(PLGPU_ERR_INVALID, "aggregation not supported for this dtype");
         if (acc_of_col[c] < 0) {
@@ -1844,16 +1945,20 @@ static int plan_groupby(const plgpu_column* key, const plgpu_column* cols, int32
             acc_of_col[c] = p.nacc;
             AccSpec& ac = p.acc[p.nacc++];
             std::memset(&ac, 0xff, sizeof ac);
-            ac.c = to_dev(cols[c]);
+            ac.c = to_dev(in.col);
             ac.flags = 0;
             ac.isf = dtype_is_float(dt);  // Float32 in register form (f64 bits): exact sums, TotalOrd min / max
             ac.uns = dt == PLGPU_U64;
+            ac.dop = in.dop;
+            std::memset(&ac.c2, 0, sizeof ac.c2);
+            if (in.dop != DOP_NONE && !(in.dop & DOP_LIT)) ac.c2 = to_dev(in.col2);
+            ac.dimm = in.imm;
         }
         AccSpec& ac = p.acc[acc_of_col[c]];
         const bool isf = dtype_is_float(dt);
         // partial / merge mode keeps the record layout schema-only (the same on
         // every rank whatever its validity bitmaps): counts always present
-        const bool nullable = cols[c].validity != nullptr || force_counts;
+        const bool nullable = in.col.validity != nullptr || (ac.c2.validity != nullptr) || force_counts;
         switch (aggs[i].kind) {
         case PLGPU_AGG_SUM: ac.flags |= isf ? (A_FSUM | A_FLAGS) : A_ISUM; break;
         case PLGPU_AGG_MEAN:
@@ -1872,7 +1977,8 @@ static int plan_groupby(const plgpu_column* key, const plgpu_column* cols, int32
     }
     for (int a = 0; a < p.nacc; ++a) {
         AccSpec& ac = p.acc[a];
-        if ((ac.flags & A_CNT) && ac.c.validity == nullptr && !force_counts) ac.flags &= ~A_CNT;
+        if ((ac.flags & A_CNT) && ac.c.validity == nullptr && ac.c2.validity == nullptr && !force_counts)
+            ac.flags &= ~A_CNT;
         if (ac.flags & (A_FSUM | A_FSUMCAST)) {
             ac.f_sum = nf;
             nf += 3;
@@ -1914,10 +2020,14 @@ static int plan_groupby(const plgpu_column* key, const plgpu_column* cols, int32
                     ((uint64_t)(ac.isf ? 1 : 0) << 56) | ((uint64_t)(ac.uns ? 1 : 0) << 57);
     }
     // simple predicate: reuse an aggregated column's registers when possible
+    // (an acc reading that column as it is)
     p.pred_acc = -1;
     if (dp.simple) {
         p.pred_col = to_dev(cols[dp.simple_col]);
-        if (acc_of_col[dp.simple_col] >= 0) p.pred_acc = acc_of_col[dp.simple_col];
+        for (int a = 0; a < p.nacc && p.pred_acc < 0; ++a)
+            if (p.acc[a].c.values == p.pred_col.values && p.acc[a].c.offset == p.pred_col.offset &&
+                p.acc[a].c.dtype == p.pred_col.dtype && p.acc[a].c.validity == p.pred_col.validity)
+                p.pred_acc = a;
     }
     pl->outs.clear();
     for (int i = 0; i < naggs; ++i) {
@@ -1925,7 +2035,7 @@ static int plan_groupby(const plgpu_column* key, const plgpu_column* cols, int32
         std::memset(&o, 0, sizeof o);
         o.kind = aggs[i].kind;
         o.acc = pl->acc_of_agg[i];
-        const int32_t dt = cols[aggs[i].col].dtype;
+        const int32_t dt = ins[aggs[i].col].dtype;
         o.in_isf = dtype_is_float(dt);
         o.in_uns = dt == PLGPU_U64;
         switch (o.kind) {
@@ -2007,10 +2117,10 @@ static int resident_per_cu(const void* kern, int threads, size_t lds) {
     return nb;
 }
 
-template <int NACC, int PRED, bool SUMONLY, int LIMBS = 3, bool RUNS = false>
+template <int NACC, int PRED, bool SUMONLY, int LIMBS = 3, bool RUNS = false, bool DERIV = false>
 static hipError_t launch_fast_rows(const Plan& pl, const DevProgram& dp, hipStream_t s) {
     constexpr int ROWS = 2;
-    const void* kern = (const void*)gb_fast_kernel<NACC, PRED, SUMONLY, ROWS, LIMBS, RUNS>;
+    const void* kern = (const void*)gb_fast_kernel<NACC, PRED, SUMONLY, ROWS, LIMBS, RUNS, false, DERIV>;
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -2026,32 +2136,45 @@ static hipError_t launch_fast_rows(const Plan& pl, const DevProgram& dp, hipStre
     if (g > useful) g = std::max<int64_t>(1, useful);
     const int grid = (int)g;
     pl.launched_grid = grid;
-    gb_fast_kernel<NACC, PRED, SUMONLY, ROWS, LIMBS, RUNS><<<grid, kGbThreads, lds, s>>>(pl.p, dp);
+    gb_fast_kernel<NACC, PRED, SUMONLY, ROWS, LIMBS, RUNS, false, DERIV><<<grid, kGbThreads, lds, s>>>(pl.p, dp);
     return hipGetLastError();
 }
 
-template <int NACC, int PRED, bool SUMONLY>
+template <int NACC, int PRED, bool SUMONLY, bool DERIV>
 static hipError_t launch_fast(const Plan& pl, const DevProgram& dp, hipStream_t s) {
-    if (SUMONLY && pl.limbs == 2 && pl.runs) return launch_fast_rows<NACC, PRED, SUMONLY, 2, true>(pl, dp, s);
-    if (SUMONLY && pl.limbs == 2) return launch_fast_rows<NACC, PRED, SUMONLY, 2>(pl, dp, s);
-    return launch_fast_rows<NACC, PRED, SUMONLY>(pl, dp, s);
+    if (SUMONLY && pl.limbs == 2 && pl.runs) return launch_fast_rows<NACC, PRED, SUMONLY, 2, true, DERIV>(pl, dp, s);
+    if (SUMONLY && pl.limbs == 2) return launch_fast_rows<NACC, PRED, SUMONLY, 2, false, DERIV>(pl, dp, s);
+    return launch_fast_rows<NACC, PRED, SUMONLY, 3, false, DERIV>(pl, dp, s);
 }
 
-template <int NACC>
+template <int NACC, bool DERIV>
 static hipError_t launch_fast_nacc(const Plan& pl, const DevProgram& dp, int pred, hipStream_t s) {
-    if (pl.sum_only) return pred == 0 ? launch_fast<NACC, 0, true>(pl, dp, s) : launch_fast<NACC, 1, true>(pl, dp, s);
-    return pred == 0 ? launch_fast<NACC, 0, false>(pl, dp, s) : launch_fast<NACC, 1, false>(pl, dp, s);
+    if (pl.sum_only)
+        return pred == 0 ? launch_fast<NACC, 0, true, DERIV>(pl, dp, s) : launch_fast<NACC, 1, true, DERIV>(pl, dp, s);
+    return pred == 0 ? launch_fast<NACC, 0, false, DERIV>(pl, dp, s) : launch_fast<NACC, 1, false, DERIV>(pl, dp, s);
 }
 
 static hipError_t launch_fast_dispatch(const Plan& pl, const DevProgram& dp, int pred, hipStream_t s) {
+    bool dv = false;
+    for (int a = 0; a < pl.p.nacc; ++a) dv = dv || pl.p.acc[a].dop != DOP_NONE;
+    if (dv) {
+        switch (pl.p.nacc) {
+        case 1: return launch_fast_nacc<1, true>(pl, dp, pred, s);
+        case 2: return launch_fast_nacc<2, true>(pl, dp, pred, s);
+        case 3: return launch_fast_nacc<3, true>(pl, dp, pred, s);
+        case 4: return launch_fast_nacc<4, true>(pl, dp, pred, s);
+        case 5: return launch_fast_nacc<5, true>(pl, dp, pred, s);
+        default: return launch_fast_nacc<6, true>(pl, dp, pred, s);
+        }
+    }
     switch (pl.p.nacc) {
-    case 0: return launch_fast_nacc<0>(pl, dp, pred, s);
-    case 1: return launch_fast_nacc<1>(pl, dp, pred, s);
-    case 2: return launch_fast_nacc<2>(pl, dp, pred, s);
-    case 3: return launch_fast_nacc<3>(pl, dp, pred, s);
-    case 4: return launch_fast_nacc<4>(pl, dp, pred, s);
-    case 5: return launch_fast_nacc<5>(pl, dp, pred, s);
-    default: return launch_fast_nacc<6>(pl, dp, pred, s);
+    case 0: return launch_fast_nacc<0, false>(pl, dp, pred, s);
+    case 1: return launch_fast_nacc<1, false>(pl, dp, pred, s);
+    case 2: return launch_fast_nacc<2, false>(pl, dp, pred, s);
+    case 3: return launch_fast_nacc<3, false>(pl, dp, pred, s);
+    case 4: return launch_fast_nacc<4, false>(pl, dp, pred, s);
+    case 5: return launch_fast_nacc<5, false>(pl, dp, pred, s);
+    default: return launch_fast_nacc<6, false>(pl, dp, pred, s);
     }
 }
 
@@ -2069,6 +2192,72 @@ static hipError_t launch_main_dispatch(const Plan& pl, const DevProgram& dp, int
 // One group-by execution: plan, sampled windows, table, main launches,
 // finalize.  Shared by plgpu_group_by_agg (single GPU) and the partial /
 // merge entry points of the hash-partitioned multi-GPU group-by.
+
+// Aggregation inputs given as programs over the columns (plgpu_agg_input):
+// agg.col >= ncols names input agg.col - ncols.  Each is classified once:
+//   a single column                        -> that column;
+//   x op y, x / y Float64 columns or one a literal, op + - * / (one IEEE
+//   rounding, the lowering's own typing)    -> fused: computed in registers
+//                                              by the fused kernel (DOP_*);
+//   anything else                          -> materialised by plgpu_eval
+//                                              before the pass.
+// A fused input is materialised as well when the pass does not run the
+// fused kernel (generic kernel, partitioned many-groups path).
+struct DerivIn {
+    const plgpu_instr* prog;
+    int32_t n;
+    int32_t kind;    // 1 column, 2 fused, 0 materialise
+    int32_t ca, cb;  // column operands (cb -1: literal)
+    int32_t dop;
+    uint64_t imm;
+    int32_t out_dtype;
+};
+
+struct Deriv {
+    std::vector<DerivIn> in;
+};
+
+static int classify_inputs(const plgpu_column* cols, int32_t ncols, const plgpu_agg_input* inputs, int32_t ninputs,
+                           Deriv* d) {
+    d->in.assign((size_t)std::max(ninputs, 0), DerivIn{});
+    for (int j = 0; j < ninputs; ++j) {
+        DerivIn& di = d->in[j];
+        di.prog = inputs[j].program;
+        di.n = inputs[j].n_instr;
+        DevProgram lp;
+        int rc = lower_program(cols, ncols, di.prog, di.n, &lp);
+        if (rc) return rc;
+        di.out_dtype = lp.out_dtype;
+        di.kind = 0;
+        di.cb = -1;
+        if (lp.n == 1 && lp.code[0].op == D_COL) {
+            di.kind = 1;
+            di.ca = lp.code[0].arg;
+            continue;
+        }
+        if (lp.n != 3 || lp.code[2].arg != PLGPU_F64) continue;
+        int32_t op;
+        switch (lp.code[2].op) {
+        case D_ADD_F: op = DOP_ADD; break;
+        case D_SUB_F: op = DOP_SUB; break;
+        case D_MUL_F: op = DOP_MUL; break;
+        case D_DIV_F: op = DOP_DIV; break;
+        case D_DIV_FS: op = DOP_DIVS; break;
+        default: continue;
+        }
+        const DevInstr &i0 = lp.code[0], &i1 = lp.code[1];
+        auto f64col = [&](const DevInstr& i) { return i.op == D_COL && cols[i.arg].dtype == PLGPU_F64; };
+        if (f64col(i0) && f64col(i1)) {
+            di.kind = 2, di.ca = i0.arg, di.cb = i1.arg, di.dop = op;
+        } else if (f64col(i0) && i1.op == D_LIT) {
+            di.kind = 2, di.ca = i0.arg, di.dop = op | DOP_LIT, di.imm = i1.imm;
+        } else if (i0.op == D_LIT && f64col(i1)) {
+            di.kind = 2, di.ca = i1.arg, di.dop = op | DOP_LIT | DOP_SWAP, di.imm = i0.imm;
+        }
+    }
+    return PLGPU_OK;
+}
+
 struct GbRun {
     Plan pl;
     DevProgram dp;
@@ -2102,6 +2291,14 @@ struct GbRun {
     const uint64_t* part_range = nullptr;    // P + 1 partition boundaries (inside prange)
     int64_t part_rows_total = 0;
     PartOut pout;
+    // aggregation inputs: the predicate's columns, the derived inputs and
+    // the columns materialised for them (owned)
+    const plgpu_column* cols = nullptr;
+    int32_t ncols = 0;
+    const Deriv* deriv = nullptr;
+    std::vector<InSpec> ins;
+    std::vector<plgpu_column> mat;
+    std::vector<int> acc_input;  // input index of each acc
 
     GbRun() {
         std::memset(st, 0, sizeof st);
@@ -2117,12 +2314,49 @@ struct GbRun {
         dev_free(status, s);
         dev_free(pbuf, s);
         dev_free(prange, s);
+        for (auto& c : mat) plgpu_column_release(&c);
     }
 };
 
+// Materialise aggregation input j (plgpu_eval of its program) into R.mat.
+static int gb_materialize(GbRun& R, int j, plgpu_column* out) {
+    const DerivIn& di = R.deriv->in[j];
+    plgpu_column c;
+    std::memset(&c, 0, sizeof c);
+    int rc = plgpu_eval(R.cols, R.ncols, di.prog, di.n, &c, R.s);
+    if (rc) return rc;
+    R.mat.push_back(c);
+    *out = c;
+    return PLGPU_OK;
+}
+
+// The fused derived accs as plain columns: when the pass will not run the
+// fused kernel.  (Their sampled exponents stay valid: same values.)
+static int gb_unfuse(GbRun& R) {
+    GbParams& p = R.pl.p;
+    for (int a = 0; a < p.nacc; ++a) {
+        if (p.acc[a].dop == DOP_NONE) continue;
+        plgpu_column c;
+        int rc = gb_materialize(R, R.acc_input[a] - R.ncols, &c);
+        if (rc) return rc;
+        p.acc[a].c = to_dev(c);
+        p.acc[a].dop = DOP_NONE;
+        std::memset(&p.acc[a].c2, 0, sizeof p.acc[a].c2);
+        // the predicate no longer shares this acc's registers
+        if (p.pred_acc == a) p.pred_acc = -1;
+    }
+    return PLGPU_OK;
+}
+
+static bool gb_has_fused(const GbRun& R) {
+    for (int a = 0; a < R.pl.p.nacc; ++a)
+        if (R.pl.p.acc[a].dop != DOP_NONE) return true;
+    return false;
+}
+
 static int gb_prepare(GbRun& R, const plgpu_column* key, const plgpu_column* cols, int32_t ncols,
                       const plgpu_instr* program, int32_t n_instr, const plgpu_agg* aggs, int32_t naggs,
-                      bool maintain_order, bool force_counts, void* stream) {
+                      bool maintain_order, bool force_counts, void* stream, const Deriv* deriv = nullptr) {
     R.s = as_stream(stream);
     if (key == nullptr) return fail(PLGPU_ERR_INVALID, "key is NULL");
     if (ncols < 0 || ncols > PLGPU_MAX_COLS) return fail(PLGPU_ERR_INVALID, "too many columns (max 8)");
@@ -2132,6 +2366,9 @@ static int gb_prepare(GbRun& R, const plgpu_column* key, const plgpu_column* col
         if (cols[i].length != key->length) return fail(PLGPU_ERR_SHAPE, "columns must match the key length");
     R.key_dtype = key->dtype;
     R.maintain = maintain_order;
+    R.cols = cols;
+    R.ncols = ncols;
+    R.deriv = deriv;
     std::memset(&R.dp, 0, sizeof R.dp);
     int rc;
     if (program != nullptr && n_instr > 0) {
@@ -2139,9 +2376,36 @@ static int gb_prepare(GbRun& R, const plgpu_column* key, const plgpu_column* col
         if (R.dp.out_dtype != PLGPU_BOOL) return fail(PLGPU_ERR_SCHEMA, "filter predicate must be of type `Boolean`");
         R.pred = R.dp.simple ? 1 : 2;
     }
-    if ((rc = plan_groupby(key, cols, ncols, aggs, naggs, maintain_order || R.want_first, R.dp, &R.pl,
-                           force_counts)))
+    // aggregation inputs: the columns, then the derived inputs (a column,
+    // a fused x op y, or materialised now)
+    R.ins = column_inputs(cols, ncols);
+    if (deriv) {
+        for (size_t j = 0; j < deriv->in.size(); ++j) {
+            const DerivIn& di = deriv->in[j];
+            InSpec in;
+            std::memset(&in, 0, sizeof in);
+            if (di.kind == 1) {
+                in = R.ins[di.ca];
+            } else if (di.kind == 2) {
+                in.col = cols[di.ca];
+                if (di.cb >= 0) in.col2 = cols[di.cb];
+                in.dtype = PLGPU_F64;
+                in.dop = di.dop;
+                in.imm = di.imm;
+            } else {
+                if ((rc = gb_materialize(R, (int)j, &in.col))) return rc;
+                in.dtype = in.col.dtype;
+            }
+            R.ins.push_back(in);
+        }
+    }
+    if ((rc = plan_groupby(key, cols, ncols, R.ins.data(), (int32_t)R.ins.size(), aggs, naggs,
+                           maintain_order || R.want_first, R.dp, &R.pl, force_counts)))
         return rc;
+    // the input index of each acc (first aggregation that created it)
+    R.acc_input.assign(kMaxAcc, -1);
+    for (int i = 0; i < naggs; ++i)
+        if (R.acc_input[R.pl.acc_of_agg[i]] < 0) R.acc_input[R.pl.acc_of_agg[i]] = aggs[i].col;
     // status words, the bottoms, then (at word kPlanSetWord) the plan's
     // global distinct-key set; one allocation, one memset
     static_assert(ST_WORDS * 8 + kMaxAcc * 4 <= kPlanSetWord * 8, "status layout");
@@ -2253,7 +2517,10 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
                ((uintptr_t)c.values & 15) == 0;
     };
     bool fast = pl.use_lds && R.pred != 2 && ok(p.key);
-    for (int a = 0; a < p.nacc; ++a) fast = fast && ok(p.acc[a].c);
+    for (int a = 0; a < p.nacc; ++a) {
+        fast = fast && ok(p.acc[a].c);
+        if (p.acc[a].dop != DOP_NONE && !(p.acc[a].dop & DOP_LIT)) fast = fast && ok(p.acc[a].c2);
+    }
     if (R.pred == 1 && p.pred_acc < 0) fast = fast && ok(p.pred_col);
     const int64_t tile = (int64_t)2 * kGbThreads;
     p.n_full = fast ? (n / tile) * tile : 0;
@@ -2325,6 +2592,9 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
         }
     }
     if (R.part) p.n_full = 0, p.row_begin = 0;
+    // fused derived inputs run in the fused kernel only; any other pass
+    // reads them materialised
+    if (gb_has_fused(R) && (p.n_full == 0 || R.part)) return gb_unfuse(R);
     return PLGPU_OK;
 }
 
@@ -2912,20 +3182,29 @@ __global__ void mk_gather_key_kernel(DevCol c, const uint64_t* __restrict__ rows
 
 using namespace plgpu;
 
-PLGPU_API int plgpu_group_by_agg(const plgpu_column* key, const plgpu_column* cols, int32_t ncols,
-                                 const plgpu_instr* program, int32_t n_instr, const plgpu_agg* aggs, int32_t naggs,
-                                 int32_t maintain_order, plgpu_column* out_key, plgpu_column* out_aggs,
-                                 plgpu_groupby_info* info, void* stream) {
+static int gb_single_impl(const plgpu_column* key, const plgpu_column* cols, int32_t ncols, const Deriv* deriv,
+                          const plgpu_instr* program, int32_t n_instr, const plgpu_agg* aggs, int32_t naggs,
+                          int32_t maintain_order, plgpu_column* out_key, plgpu_column* out_aggs,
+                          plgpu_groupby_info* info, void* stream) {
     if (out_key == nullptr) return fail(PLGPU_ERR_INVALID, "out_key is NULL");
     std::memset(out_key, 0, sizeof *out_key);
     for (int i = 0; i < naggs && out_aggs; ++i) std::memset(&out_aggs[i], 0, sizeof(plgpu_column));
     GbRun R;
-    int rc = gb_prepare(R, key, cols, ncols, program, n_instr, aggs, naggs, maintain_order != 0, false, stream);
+    int rc = gb_prepare(R, key, cols, ncols, program, n_instr, aggs, naggs, maintain_order != 0, false, stream,
+                        deriv);
     if (!rc) rc = gb_plan(R, nullptr);
     if (!rc) rc = gb_main(R, true, nullptr, nullptr);
     if (rc) return rc;
     if (info) gb_fill_info(R, info);
     return gb_finalize(R, naggs, out_key, out_aggs);
+}
+
+PLGPU_API int plgpu_group_by_agg(const plgpu_column* key, const plgpu_column* cols, int32_t ncols,
+                                 const plgpu_instr* program, int32_t n_instr, const plgpu_agg* aggs, int32_t naggs,
+                                 int32_t maintain_order, plgpu_column* out_key, plgpu_column* out_aggs,
+                                 plgpu_groupby_info* info, void* stream) {
+    return gb_single_impl(key, cols, ncols, nullptr, program, n_instr, aggs, naggs, maintain_order, out_key,
+                          out_aggs, info, stream);
 }
 
 PLGPU_API int plgpu_debug_checks(uint32_t* out) {
@@ -2959,7 +3238,8 @@ PLGPU_API int plgpu_gb_record_words(const plgpu_column* cols, int32_t ncols, con
     Plan pl;
     DevProgram dp;
     std::memset(&dp, 0, sizeof dp);
-    const int rc = plan_groupby(&k, c2.data(), ncols, aggs, naggs, false, dp, &pl, true);
+    const std::vector<InSpec> ins = column_inputs(c2.data(), ncols);
+    const int rc = plan_groupby(&k, c2.data(), ncols, ins.data(), ncols, aggs, naggs, false, dp, &pl, true);
     if (rc) return rc;
     *out_words = pl.p.nfields + 1;
     return PLGPU_OK;
@@ -3431,9 +3711,9 @@ PLGPU_API int plgpu_gb_merge_sources(const void* records, int32_t n_sources, con
 // Packed path: group by the exact Int64 code, then decode the output codes
 // into the key columns.
 static int gb_multi_packed(const MkKeys& mk, const MkPack& pk, int64_t n, const plgpu_column* keys, int32_t nkeys,
-                           const plgpu_column* cols, int32_t ncols, const plgpu_instr* program, int32_t n_instr,
-                           const plgpu_agg* aggs, int32_t naggs, int32_t maintain_order, plgpu_column* out_keys,
-                           plgpu_column* out_aggs, plgpu_groupby_info* info, void* stream) {
+                           const plgpu_column* cols, int32_t ncols, const Deriv* deriv, const plgpu_instr* program,
+                           int32_t n_instr, const plgpu_agg* aggs, int32_t naggs, int32_t maintain_order,
+                           plgpu_column* out_keys, plgpu_column* out_aggs, plgpu_groupby_info* info, void* stream) {
     hipStream_t s = as_stream(stream);
     uint64_t* codes = nullptr;
     int rc = dev_alloc((void**)&codes, (size_t)std::max<int64_t>(n, 1) * 8, s);
@@ -3453,7 +3733,9 @@ static int gb_multi_packed(const MkKeys& mk, const MkPack& pk, int64_t n, const 
     std::memset(&hout, 0, sizeof hout);
     {
         GbRun R;
-        if (!rc) rc = gb_prepare(R, &ck, cols, ncols, program, n_instr, aggs, naggs, maintain_order != 0, false, stream);
+        if (!rc)
+            rc = gb_prepare(R, &ck, cols, ncols, program, n_instr, aggs, naggs, maintain_order != 0, false, stream,
+                            deriv);
         if (!rc) rc = gb_plan(R, nullptr);
         if (!rc) rc = gb_main(R, true, nullptr, nullptr);
         if (!rc && info) gb_fill_info(R, info);
@@ -3486,11 +3768,10 @@ static int gb_multi_packed(const MkKeys& mk, const MkPack& pk, int64_t n, const 
     return rc;
 }
 
-PLGPU_API int plgpu_group_by_agg_multi(const plgpu_column* keys, int32_t nkeys, const plgpu_column* cols,
-                                       int32_t ncols, const plgpu_instr* program, int32_t n_instr,
-                                       const plgpu_agg* aggs, int32_t naggs, int32_t maintain_order,
-                                       plgpu_column* out_keys, plgpu_column* out_aggs, plgpu_groupby_info* info,
-                                       void* stream) {
+static int gb_multi_impl(const plgpu_column* keys, int32_t nkeys, const plgpu_column* cols, int32_t ncols,
+                         const Deriv* deriv, const plgpu_instr* program, int32_t n_instr, const plgpu_agg* aggs,
+                         int32_t naggs, int32_t maintain_order, plgpu_column* out_keys, plgpu_column* out_aggs,
+                         plgpu_groupby_info* info, void* stream) {
     if (keys == nullptr || out_keys == nullptr) return fail(PLGPU_ERR_INVALID, "keys / out_keys is NULL");
     if (nkeys < 1 || nkeys > kMaxKeys) return fail(PLGPU_ERR_INVALID, "number of key columns must be 1..8");
     for (int i = 0; i < nkeys; ++i) std::memset(&out_keys[i], 0, sizeof(plgpu_column));
@@ -3526,11 +3807,11 @@ PLGPU_API int plgpu_group_by_agg_multi(const plgpu_column* keys, int32_t nkeys, 
             // one key: the single-key group-by takes the Int64 codes (and
             // their validity) directly, no tuple packing pass
             if (nkeys == 1)
-                rc = plgpu_group_by_agg(&ck[0], cols, ncols, program, n_instr, aggs, naggs, maintain_order,
-                                        &out_keys[0], out_aggs, info, stream);
+                rc = gb_single_impl(&ck[0], cols, ncols, deriv, program, n_instr, aggs, naggs, maintain_order,
+                                    &out_keys[0], out_aggs, info, stream);
             else
-                rc = plgpu_group_by_agg_multi(ck, nkeys, cols, ncols, program, n_instr, aggs, naggs, maintain_order,
-                                              out_keys, out_aggs, info, stream);
+                rc = gb_multi_impl(ck, nkeys, cols, ncols, deriv, program, n_instr, aggs, naggs, maintain_order,
+                                   out_keys, out_aggs, info, stream);
             for (int i = 0; i < nkeys && !rc; ++i) {
                 if (keys[i].dtype != PLGPU_STR) continue;
                 plgpu_column strs;
@@ -3554,7 +3835,7 @@ PLGPU_API int plgpu_group_by_agg_multi(const plgpu_column* keys, int32_t nkeys, 
         MkPack pk;
         int rc = mk_plan_pack(mk, n, nullptr, 0, std::max(hg, 1), &pk, s);
         if (rc) return rc;
-        if (pk.ok) return gb_multi_packed(mk, pk, n, keys, nkeys, cols, ncols, program, n_instr, aggs, naggs,
+        if (pk.ok) return gb_multi_packed(mk, pk, n, keys, nkeys, cols, ncols, deriv, program, n_instr, aggs, naggs,
                                           maintain_order, out_keys, out_aggs, info, stream);
     }
     uint64_t* hashes = nullptr;
@@ -3577,7 +3858,7 @@ PLGPU_API int plgpu_group_by_agg_multi(const plgpu_column* keys, int32_t nkeys, 
         if (e != hipSuccess) { rc = hip_fail(e, "mk_hash_kernel"); break; }
         GbRun R;
         R.want_first = true;
-        rc = gb_prepare(R, &hk, cols, ncols, program, n_instr, aggs, naggs, maintain_order != 0, false, stream);
+        rc = gb_prepare(R, &hk, cols, ncols, program, n_instr, aggs, naggs, maintain_order != 0, false, stream, deriv);
         if (!rc) rc = gb_plan(R, nullptr);
         if (!rc) rc = gb_main(R, true, nullptr, nullptr);
         if (rc) break;
@@ -3640,6 +3921,84 @@ PLGPU_API int plgpu_group_by_agg_multi(const plgpu_column* keys, int32_t nkeys, 
     if (rc)
         for (int i = 0; i < nkeys; ++i) plgpu_column_release(&out_keys[i]);
     return rc;
+}
+
+PLGPU_API int plgpu_group_by_agg_multi(const plgpu_column* keys, int32_t nkeys, const plgpu_column* cols,
+                                       int32_t ncols, const plgpu_instr* program, int32_t n_instr,
+                                       const plgpu_agg* aggs, int32_t naggs, int32_t maintain_order,
+                                       plgpu_column* out_keys, plgpu_column* out_aggs, plgpu_groupby_info* info,
+                                       void* stream) {
+    return gb_multi_impl(keys, nkeys, cols, ncols, nullptr, program, n_instr, aggs, naggs, maintain_order, out_keys,
+                         out_aggs, info, stream);
+}
+
+// Global reduction: every selected row in one group (the keyless key
+// column, key_at), then the one output row -- or, with no row selected, the
+// reference's empty reductions (sum / len / count 0, the rest null).
+static int gb_keyless(const plgpu_column* cols, int32_t ncols, const Deriv* deriv, const plgpu_instr* program,
+                      int32_t n_instr, const plgpu_agg* aggs, int32_t naggs, plgpu_column* out_aggs,
+                      plgpu_groupby_info* info, void* stream) {
+    if (ncols < 1) return fail(PLGPU_ERR_INVALID, "a global reduction needs at least one column (the length)");
+    plgpu_column k;
+    std::memset(&k, 0, sizeof k);
+    k.dtype = PLGPU_I64;
+    k.length = cols[0].length;
+    k.device_id = cols[0].device_id;
+    plgpu_column out_key;
+    int rc = gb_single_impl(&k, cols, ncols, deriv, program, n_instr, aggs, naggs, 0, &out_key, out_aggs, info,
+                            stream);
+    if (rc) return rc;
+    const int64_t groups = out_key.length;
+    plgpu_column_release(&out_key);
+    if (groups == 1) return PLGPU_OK;
+    if (groups != 0) return fail(PLGPU_ERR_CAPACITY, "internal: a global reduction produced several groups");
+    hipStream_t s = as_stream(stream);
+    for (int i = 0; i < naggs && rc == PLGPU_OK; ++i) {
+        const int32_t dt = out_aggs[i].dtype;
+        const bool has_valid = out_aggs[i].validity != nullptr;
+        plgpu_column_release(&out_aggs[i]);
+        rc = make_owned_column(&out_aggs[i], dt, 1, has_valid, s);
+        if (rc) break;
+        const int32_t kind = aggs[i].kind;
+        const bool valid = kind == PLGPU_AGG_SUM || kind == PLGPU_AGG_LEN || kind == PLGPU_AGG_COUNT;
+        const size_t vb = dt == PLGPU_BOOL ? 8 : (size_t)std::max(dtype_bytes(dt), 1);
+        hipError_t e = hipMemsetAsync((void*)out_aggs[i].values, 0, vb, s);
+        if (e == hipSuccess && has_valid) e = hipMemsetAsync((void*)out_aggs[i].validity, valid ? 0x01 : 0x00, 1, s);
+        if (e == hipSuccess && has_valid) e = hipMemsetAsync((uint8_t*)out_aggs[i].validity + 1, 0, 7, s);
+        if (e != hipSuccess) rc = hip_fail(e, "empty reduction");
+        out_aggs[i].null_count = (has_valid && !valid) ? 1 : 0;
+    }
+    if (rc == PLGPU_OK) {
+        hipError_t e = hipStreamSynchronize(s);
+        if (e != hipSuccess) rc = hip_fail(e, "empty reduction");
+    }
+    if (rc)
+        for (int i = 0; i < naggs; ++i) plgpu_column_release(&out_aggs[i]);
+    return rc;
+}
+
+PLGPU_API int plgpu_group_by_agg_ex(const plgpu_column* keys, int32_t nkeys, const plgpu_column* cols, int32_t ncols,
+                                    const plgpu_agg_input* inputs, int32_t ninputs, const plgpu_instr* program,
+                                    int32_t n_instr, const plgpu_agg* aggs, int32_t naggs, int32_t maintain_order,
+                                    plgpu_column* out_keys, plgpu_column* out_aggs, plgpu_groupby_info* info,
+                                    void* stream) {
+    if (nkeys < 0 || nkeys > kMaxKeys) return fail(PLGPU_ERR_INVALID, "number of key columns must be 0..8");
+    if (nkeys > 0 && (keys == nullptr || out_keys == nullptr)) return fail(PLGPU_ERR_INVALID, "keys / out_keys is NULL");
+    if (ninputs < 0 || (ninputs > 0 && inputs == nullptr)) return fail(PLGPU_ERR_INVALID, "bad aggregation inputs");
+    if (ncols < 0 || ncols > PLGPU_MAX_COLS) return fail(PLGPU_ERR_INVALID, "too many columns (max 8)");
+    if (naggs > 0 && out_aggs == nullptr) return fail(PLGPU_ERR_INVALID, "out_aggs is NULL");
+    for (int i = 0; i < naggs; ++i) std::memset(&out_aggs[i], 0, sizeof(plgpu_column));
+    for (int i = 0; i < nkeys; ++i) std::memset(&out_keys[i], 0, sizeof(plgpu_column));
+    Deriv d;
+    int rc = classify_inputs(cols, ncols, inputs, ninputs, &d);
+    if (rc) return rc;
+    const Deriv* dv = ninputs > 0 ? &d : nullptr;
+    if (nkeys == 0) return gb_keyless(cols, ncols, dv, program, n_instr, aggs, naggs, out_aggs, info, stream);
+    if (nkeys == 1 && dtype_is_int(keys[0].dtype))
+        return gb_single_impl(&keys[0], cols, ncols, dv, program, n_instr, aggs, naggs, maintain_order, &out_keys[0],
+                              out_aggs, info, stream);
+    return gb_multi_impl(keys, nkeys, cols, ncols, dv, program, n_instr, aggs, naggs, maintain_order, out_keys,
+                         out_aggs, info, stream);
 }
 
 // ------------------------------------------------------- var / std finalize

@@ -480,6 +480,22 @@ def group_by_agg(df, key: str, aggs: Sequence[Expr], predicate: Expr | None = No
     from .frame import DataFrame, Series, String
 
     aggs = [a if isinstance(a, Expr) else col(a) for a in aggs]
+    # aggregations over expressions: each expression evaluated once into a
+    # column of this rank's shard, whose partial states then cross the
+    # protocol as a column's do (elementwise, so sharding does not change it)
+    from .frame import _eval
+
+    extra = []
+    for i, e in enumerate(aggs):
+        b = _agg_base(e)
+        if b.kind == "agg" and b.args[0].kind != "col":
+            nm = f"__in{i}"
+            while nm in df.columns:
+                nm += "_"
+            extra.append(_eval(b.args[0].alias(nm), df))
+            aggs[i] = Expr("agg", (col(nm),), op=b.op, value=b.value).alias(e.output_name())
+    if extra:
+        df = DataFrame(list(df._cols.values()) + extra)
     if any(_agg_base(e).kind == "agg" and _agg_base(e).op in ("std", "var") for e in aggs):
         return _group_by_var(df, key, aggs, predicate, group, info)
     if predicate is not None:

@@ -261,6 +261,12 @@ class _Then:
     def _finish(self) -> Expr:
         return self.otherwise(None)
 
+    def __getattr__(self, name: str):
+        # pl.when(c).then(x).sum() / .alias(...): the chain as an expression
+        if name.startswith("_"):
+            raise AttributeError(name)
+        return getattr(self._finish(), name)
+
 
 class _When:
     def __init__(self, branches: list, cond: Expr):

@@ -16,7 +16,7 @@ from typing import Any, Iterable, Sequence
 import numpy as np
 
 from . import _native as N
-from .expr import Expr, col, lower, to_instr_array
+from .expr import Expr, col, lit, lower, to_instr_array
 
 
 # ------------------------------------------------------------------ dtypes
@@ -1292,19 +1292,29 @@ class _GbCall:
     the single-GPU path and polaroid_amd.distributed)."""
 
     __slots__ = ("key", "keys", "keycol", "keycols", "names", "cols", "ncols", "prog", "n_instr", "aggs", "naggs",
-                 "out_names", "key_logical", "out_logical", "_keep")
+                 "inputs", "ninputs", "out_names", "key_logical", "out_logical", "_keep")
 
 
-def _gb_keys(key: str | tuple) -> list[str]:
+def _gb_keys(key: str | tuple | None) -> list[str]:
+    if key is None:
+        return []
     return [key] if isinstance(key, str) else list(key)
 
 
-def _gb_lower(df: DataFrame, key: str | tuple, aggs: list[Expr], pred: Expr | None) -> _GbCall:
+_BOOL_AGG_CAST = {"sum": "UInt32", "mean": "Float64"}  # reduce/sum.rs: Boolean sums count (IdxSize)
+
+
+def _gb_lower(df: DataFrame, key: str | tuple | None, aggs: list[Expr], pred: Expr | None) -> _GbCall:
+    """The group-by's C-ABI arguments.  An aggregation over a plain column
+    reads the column; over any other elementwise expression (`(close *
+    volume).sum()`, polars' can_pre_agg inputs, plans/aexpr/properties/
+    general.rs:335) it reads a computed input (plgpu_agg_input), which the
+    fused kernel evaluates in registers when it is `x op y` of Float64 columns
+    / literals.  `key` None: a global reduction (select(aggs))."""
     keys = _gb_keys(key)
     for k in keys:
         if k not in df._cols:
             raise N.ComputeError(f'unable to find column "{k}"')
-    key = keys[0]
     # len() needs some aggregatable column for its accumulator slot (it only
     # reads the group's row count): the first non-Boolean key, else any column
     len_col = next((k for k in keys if df._cols[k].dtype not in (Boolean, String)), None)
@@ -1314,67 +1324,113 @@ def _gb_lower(df: DataFrame, key: str | tuple, aggs: list[Expr], pred: Expr | No
         # no numeric column at all: a zero column of the frame's height
         len_col = "__len"
         df = DataFrame(list(df._cols.values()) + [Series.from_numpy("__len", np.zeros(df.height, np.int64))])
-    specs: list[tuple[str, str]] = []  # (kind, column)
+    specs: list[tuple[str, Any]] = []  # (kind, column name | ("input", j))
+    exprs: list[Expr] = []             # computed inputs
     out_names: list[str] = []
+    out_logical: list = []
     for e in aggs:
         name = e.output_name()
         base = e.args[0] if e.kind == "alias" else e
         if base.kind == "len":
             specs.append(("len", len_col))
-        elif base.kind == "agg" and base.args[0].kind == "col":
-            specs.append((base.op, base.args[0].value))
-            lg = df._cols[base.args[0].value]._logical_dtype() if base.args[0].value in df._cols else None
+            out_logical.append(None)
+        elif base.kind == "agg" and base.args[0].kind == "col" and base.args[0].value in df._cols:
+            c_ = base.args[0].value
+            specs.append((base.op, c_))
+            lg = df._cols[c_]._logical_dtype()
             if lg is not None and base.op not in ("min", "max", "first", "last", "count", "len") and not (
                     base.op == "sum" and isinstance(lg, Duration)):
                 raise N.InvalidOperationError(f"`{base.op}` of a {lg} column is not supported on the GPU executor")
+            out_logical.append(lg if base.op in ("min", "max", "first", "last", "sum") else None)
+        elif base.kind == "agg" and base.op in ("sum", "mean", "min", "max", "count", "len", "first", "last"):
+            x, df = _lower_strings(base.args[0], df)
+            x, lg, strict = _prepare(x, df)
+            _check_strict(strict, df)
+            if not x.meta_root_names():
+                raise N.InvalidOperationError(f"aggregation {e!r} of a literal is not supported on the GPU executor")
+            if lg is not None and base.op not in ("min", "max", "first", "last", "count", "len") and not (
+                    base.op == "sum" and isinstance(lg, Duration)):
+                raise N.InvalidOperationError(f"`{base.op}` of a {lg} expression is not supported on the GPU executor")
+            exprs.append(x)
+            specs.append((base.op, ("input", builtins.len(exprs) - 1)))
+            out_logical.append(lg if base.op in ("min", "max", "first", "last", "sum") else None)
         else:
             raise N.InvalidOperationError(
-                f"aggregation {e!r} is not supported on the GPU executor (need col(..).sum/mean/min/max/count/len/first/last)")
+                f"aggregation {e!r} is not supported on the GPU executor "
+                "(need <expr>.sum/mean/min/max/count/len/first/last)")
         out_names.append(name)
-    # columns passed to the kernel: predicate columns + aggregated columns
+    # columns passed to the kernel: predicate columns, aggregated columns,
+    # then the columns the computed inputs read
     names: list[str] = []
     g = _GbCall()
     g.prog, g.n_instr = None, 0
     if pred is not None:
         names = pred.meta_root_names()
     for _, c_ in specs:
-        if c_ not in names:
+        if isinstance(c_, str) and c_ not in names:
             names.append(c_)
+    for x in exprs:
+        for c_ in x.meta_root_names():
+            if c_ not in names:
+                names.append(c_)
     if builtins.len(names) > N.MAX_COLS:
         raise N.InvalidOperationError("group-by references more than 8 columns")
     for nm in names:
         if nm not in df._cols:
             raise N.ComputeError(f'unable to find column "{nm}"')
     idx = {nm: i for i, nm in enumerate(names)}
+    schema = {nm: df._cols[nm].dtype.code for nm in names}
     if pred is not None:
-        schema = {nm: df._cols[nm].dtype.code for nm in names}
         p = lower(pred, idx, schema)
         g.prog, g.n_instr = to_instr_array(p), builtins.len(p)
+    ncols = builtins.len(names)
+    cols = _col_array([df._cols[nm] for nm in names])
+    inputs = (N.AggInput * max(1, builtins.len(exprs)))()
+    keep_progs = []
+    for j, x in enumerate(exprs):
+        prog = to_instr_array(lower(x, idx, schema))
+        dt = C.c_int32(0)
+        N.check(N.lib().plgpu_expr_dtype(cols, ncols, prog, builtins.len(prog), C.byref(dt)))
+        if dt.value == N.BOOL:
+            kinds = {k for k, c_ in specs if c_ == ("input", j)}
+            if kinds - set(_BOOL_AGG_CAST) - {"count", "len"}:
+                raise N.InvalidOperationError("min / max / first / last of a Boolean expression are not supported "
+                                              "on the GPU executor")
+            if builtins.len({_BOOL_AGG_CAST[k] for k in kinds if k in _BOOL_AGG_CAST}) > 1:
+                raise N.InvalidOperationError("sum and mean of one Boolean expression in one group-by")
+            to = next((_BOOL_AGG_CAST[k] for k in kinds if k in _BOOL_AGG_CAST), None)
+            if to is not None:
+                prog = to_instr_array(lower(x.cast(UInt32 if to == "UInt32" else Float64), idx, schema))
+        keep_progs.append(prog)
+        inputs[j].program = C.cast(prog, C.POINTER(N.Instr))
+        inputs[j].n_instr = builtins.len(prog)
     agg_arr = (N.Agg * max(1, builtins.len(specs)))()
     for i, (k, c_) in enumerate(specs):
         agg_arr[i].kind = _AGG_CODE[k]
-        agg_arr[i].col = idx[c_]
-    g.key = key
+        agg_arr[i].col = idx[c_] if isinstance(c_, str) else ncols + c_[1]
+    g.key = keys[0] if keys else None
     g.keys = keys
-    g.keycol = df._cols[key]._col
+    g.keycol = df._cols[keys[0]]._col if keys else None
     g.keycols = _col_array([df._cols[k] for k in keys])
     g.names = names
-    g.cols = _col_array([df._cols[nm] for nm in names])
-    g.ncols = builtins.len(names)
+    g.cols = cols
+    g.ncols = ncols
+    g.inputs = inputs
+    g.ninputs = builtins.len(exprs)
     g.aggs = agg_arr
     g.naggs = builtins.len(specs)
     g.out_names = out_names
     # logical dtypes of the outputs: keys keep theirs; min / max / first /
-    # last / Duration sums keep the column's, counts and lengths have none
+    # last / Duration sums keep the input's, counts and lengths have none
     g.key_logical = [df._cols[k]._logical_dtype() for k in keys]
-    g.out_logical = [df._cols[c_]._logical_dtype() if k_ in ("min", "max", "first", "last", "sum") else None
-                     for k_, c_ in specs]
-    g._keep = [df._cols[nm] for nm in names] + [df._cols[k] for k in keys]
+    g.out_logical = out_logical
+    g._keep = [df._cols[nm] for nm in names] + [df._cols[k] for k in keys] + keep_progs
     return g
 
 
 def _gb_frame(g: _GbCall, out_key, out_aggs) -> DataFrame:
-    """`out_key`: one Column, or an array of len(g.keys) Columns."""
+    """`out_key`: one Column, or an array of len(g.keys) Columns (none for a
+    global reduction)."""
     if isinstance(out_key, N.Column):
         series = [Series._from_native(g.key, out_key, g.key_logical[0])]
     else:
@@ -1407,11 +1463,17 @@ def _group_by_var(df: DataFrame, key: str | tuple, aggs: list[Expr], maintain_or
     keys = list(_gb_keys(key))
     var_cols: list[str] = []
     plain: list[tuple[int, Expr]] = []
+    aggs = list(aggs)
     for i, e in enumerate(aggs):
         b = _agg_base(e)
         if b.kind == "agg" and b.op in ("std", "var"):
             if b.args[0].kind != "col":
-                raise N.InvalidOperationError("var / std of a computed expression is not supported")
+                # var / std of an expression: the expression evaluated once
+                # into a column (plgpu_eval), then as for a column
+                nm = f"__vx{i}"
+                df = DataFrame(list(df._cols.values()) + [_eval(b.args[0].alias(nm), df)])
+                b = Expr("agg", (col(nm),), op=b.op, value=b.value)
+                aggs[i] = b.alias(e.output_name())
             if b.args[0].value not in var_cols:
                 var_cols.append(b.args[0].value)
         else:
@@ -1424,7 +1486,16 @@ def _group_by_var(df: DataFrame, key: str | tuple, aggs: list[Expr], maintain_or
         helpers += [col(c).mean().alias(f"__vm_{c}"), col(c).count().alias(f"__vn_{c}")]
     first = _group_by(df, key, [e for _, e in plain] + helpers, True, pred, info)
     means = [first[k] for k in keys] + [first[f"__vm_{c}"] for c in var_cols]
-    if builtins.len(keys) == 1 and df[keys[0]]._col.dtype in (N.I64, N.I32, N.U32, N.BOOL):
+    if not keys:
+        # a global var / std: the one mean as a literal (host scalar)
+        sq = []
+        for c, m in zip(var_cols, means):
+            mv = m.to_list()[0]
+            mv = float("nan") if mv is None else float(mv)
+            sq.append(_eval(((col(c).cast("f64") - lit(mv)) * (col(c).cast("f64") - lit(mv))).alias(f"__vd_{c}"),
+                            df))
+        rows = DataFrame(list(df._cols.values()) + sq)
+    elif builtins.len(keys) == 1 and df[keys[0]]._col.dtype in (N.I64, N.I32, N.U32, N.BOOL):
         # one integer key: squared deviations straight from a group-key table
         sq = []
         for c, m in zip(var_cols, means[1:]):
@@ -1466,17 +1537,12 @@ def _group_by(df: DataFrame, key: str | tuple, aggs: list[Expr], maintain_order:
     g = _gb_lower(df, key, aggs, pred)
     out_aggs = (N.Column * max(1, g.naggs))()
     gi = N.GroupByInfo()
-    if builtins.len(g.keys) == 1 and g.keycol.dtype in (N.I64, N.I32, N.I16, N.I8, N.U8, N.U16, N.U32, N.U64):
-        out_key = N.Column()
-        N.check(N.lib().plgpu_group_by_agg(C.byref(g.keycol), g.cols, g.ncols, g.prog, g.n_instr, g.aggs,
-                                           g.naggs, int(bool(maintain_order)), C.byref(out_key),
-                                           out_aggs, C.byref(gi), None))
-    else:
-        # several keys (or a UInt32 / Float64 / Boolean key): hashed tuples
-        out_key = (N.Column * builtins.len(g.keys))()
-        N.check(N.lib().plgpu_group_by_agg_multi(g.keycols, builtins.len(g.keys), g.cols, g.ncols, g.prog,
-                                                 g.n_instr, g.aggs, g.naggs, int(bool(maintain_order)),
-                                                 out_key, out_aggs, C.byref(gi), None))
+    # one integer key: the single-key kernels; several keys (or a Float /
+    # Boolean / String key): packed or hashed tuples; none: a global reduction
+    out_key = (N.Column * max(1, builtins.len(g.keys)))()
+    N.check(N.lib().plgpu_group_by_agg_ex(g.keycols, builtins.len(g.keys), g.cols, g.ncols, g.inputs, g.ninputs,
+                                          g.prog, g.n_instr, g.aggs, g.naggs, int(bool(maintain_order)), out_key,
+                                          out_aggs, C.byref(gi), None))
     if info is not None:
         info.update(gi.as_dict())
     return _gb_frame(g, out_key, out_aggs)
@@ -1622,8 +1688,19 @@ def _execute(node: tuple, info: dict | None = None) -> DataFrame:
             child = child[1]
         df = _execute(child, info)
         return _group_by(df, node[2], node[3], node[4], pred, info)
+    if kind == "select" and node[2] and builtins.all(_agg_base(e).kind in ("agg", "len") for e in node[2]):
+        # select(aggregations): a global reduction (polars-expr/src/reduce/
+        # sum.rs:112 reduce_ca and siblings), the fused group-by kernel with
+        # one group; a filter below it runs inside the same pass
+        child, pred = node[1], None
+        if child[0] == "filter":
+            pred, child = child[2], child[1]
+        return _group_by(_execute(child, info), None, node[2], False, pred, info)
     if kind in ("select", "with_columns"):
         df = _execute(node[1], info)
+        if builtins.any(_agg_base(e).kind in ("agg", "len") for e in node[2]):
+            raise N.InvalidOperationError("mixing aggregations and elementwise expressions in one select is not "
+                                          "supported on the GPU executor")
         new = [_eval(e, df) for e in node[2]]
         if kind == "select":
             return DataFrame(new)

@@ -185,10 +185,18 @@ class _Translator:
             raise Unsupported(f"function {fname}")
         raise Unsupported(f"expression {k}")
 
-    def agg(self, node: int, key: str) -> Expr:
+    def agg(self, node: int, key: str | None) -> Expr:
+        """IRAggExpr (expr_nodes.rs) -> an aggregation over a column or over an
+        elementwise expression (the inputs the reference's partitionable
+        group-by pre-aggregates, plans/aexpr/properties/general.rs:303-356
+        can_pre_agg).  `key` None: a select of aggregations."""
         e = self.view(node)
         k = _name(e)
         if k == "Len":
+            if key is None:
+                from .expr import len as len_
+
+                return len_()
             return col(key).len()
         if k != "Agg":
             raise Unsupported(f"aggregation expression {k}")
@@ -196,11 +204,12 @@ class _Translator:
         if len(e.arguments) != 1:
             raise Unsupported("multi-argument aggregation")
         arg = self.nt.view_expression(e.arguments[0])
-        if _name(arg) != "Column":
-            raise Unsupported("aggregation over a computed expression")
-        c = col(str(arg.name))
-        if name in ("min", "max") and str(arg.name) in self.enums:
-            raise Unsupported(f"{name} of an Enum column (category order)")
+        if _name(arg) == "Column":
+            c = col(str(arg.name))
+            if name in ("min", "max") and str(arg.name) in self.enums:
+                raise Unsupported(f"{name} of an Enum column (category order)")
+        else:
+            c = self.expr(e.arguments[0])  # raises Unsupported outside the elementwise path
         if name in ("sum", "mean"):
             return getattr(c, name)()
         if name in ("min", "max"):
@@ -282,6 +291,9 @@ class _Translator:
             if k == "SimpleProjection":
                 names = list(self.nt.get_schema().keys())
                 return ("select", child, [col(n) for n in names])
+            if k == "Select" and node.expr and all(_name(self.view(ei.node)) in ("Agg", "Len") for ei in node.expr):
+                # select(aggregations): a global reduction on the GPU
+                return ("select", child, [self.agg(ei.node, None).alias(ei.output_name) for ei in node.expr])
             if k in ("Select", "HStack"):
                 exprs = node.expr if k == "Select" else node.exprs
                 out = []

@@ -702,6 +702,98 @@ def arith_cases():
     return {"cases": cases}
 
 
+# ---------------------------------------------------------------------------
+# 12. Aggregations over computed inputs and global reductions (select(aggs)).
+#     Each aggregation is an expression string of the polars API (evaluated
+#     with col / lit / when in scope); `key` None is a select, else group ids
+#     (string keys label-encoded).  `tol`: relative tolerance for an output the
+#     reference itself compares approximately or computes with a different
+#     rounding (Welford var / std, np.isclose).
+def reduce_cases():
+    cases = []
+    cases.append({
+        "name": "test_boolean_aggs (select)",
+        "source": "operations/aggregation/test_aggregations.py:30-42",
+        "cols": {"bool": {"dtype": "bool", "values": [True, False, None, True]}},
+        "key": None,
+        "aggs": [["col('bool').mean()", "mean"], ["col('bool').std()", "std"], ["col('bool').var()", "var"]],
+        "expected": {"mean": fx([0.6666666666666666]), "std": fx([0.5773502691896258]),
+                     "var": fx([0.33333333333333337])},
+        "tol": {"std": 1e-12, "var": 1e-12},
+    })
+    cases.append({
+        "name": "test_boolean_aggs (group_by literal key)",
+        "source": "operations/aggregation/test_aggregations.py:44-49 (group_by(pl.lit(1)): one group)",
+        "cols": {"bool": {"dtype": "bool", "values": [True, False, None, True]}},
+        "key": [1, 1, 1, 1],
+        "aggs": [["col('bool').mean()", "mean"]],
+        "expected": {"key": [1], "mean": fx([0.6666666666666666])},
+    })
+    cases.append({
+        "name": "test_sum_empty_and_null_set (select)",
+        "source": "operations/aggregation/test_aggregations.py:441-445",
+        "cols": {"a": {"dtype": "f32", "values": [None, None, None]}, "b": {"dtype": "i64", "values": [1, 1, 1]}},
+        "key": None,
+        "aggs": [["col('a').sum()", "a"]],
+        "expected": {"a": fx([0.0])},
+    })
+    cases.append({
+        "name": "test_sum_empty_and_null_set (group_by)",
+        "source": "operations/aggregation/test_aggregations.py:441-446",
+        "cols": {"a": {"dtype": "f32", "values": [None, None, None]}, "b": {"dtype": "i64", "values": [1, 1, 1]}},
+        "key": [1, 1, 1],
+        "aggs": [["col('a').sum()", "a"]],
+        "expected": {"key": [1], "a": fx([0.0])},
+    })
+    cases.append({
+        "name": "test_empty_agg_22005",
+        "source": "operations/aggregation/test_aggregations.py:940-946",
+        "cols": {"a": {"dtype": "i64", "values": []}},
+        "key": None,
+        "aggs": [["col('a').sum()", "a"]],
+        "expected": {"a": [0]},
+    })
+    cases.append({
+        "name": "test_group_by_when_then_no_aggregation_predicate",
+        "source": "operations/test_group_by.py:1039-1053",
+        "cols": {"val": {"dtype": "i64", "values": [-3, -2, 1, 4, -3, 5]}},
+        "key": [0, 0, 1, 1, 0, 0], "key_labels": ["aa", "bb"],
+        "aggs": [["when(col('val') >= 0).then(col('val')).sum()", "pos"],
+                 ["when(col('val') < 0).then(col('val')).sum()", "neg"]],
+        "sort_by_key": True,
+        "expected": {"key": [0, 1], "pos": [5, 5], "neg": [-8, 0]},
+    })
+    ids = [130352432, 130352277, 130352611, 130352833, 130352305, 130352258, 130352764, 130352475, 130352368,
+           130352346]
+    cases.append({
+        "name": "test_min_max_2850",
+        "source": "operations/aggregation/test_aggregations.py:705-733",
+        "cols": {"id": {"dtype": "i64", "values": ids}},
+        "key": None,
+        "aggs": [["col('id').min()", "min"], ["col('id').max()", "max"]],
+        "expected": {"min": [130352258], "max": [130352833]},
+    })
+    cases.append({
+        "name": "test_cse_expr_selection_context (d1)",
+        "source": "test_cse.py:211-226 (derived = (a * b).sum(), aliased d1)",
+        "cols": {"a": {"dtype": "i64", "values": [1, 2, 3, 4]}, "b": {"dtype": "i64", "values": [1, 2, 3, 4]},
+                 "c": {"dtype": "i64", "values": [1, 2, 3, 4]}},
+        "key": None,
+        "aggs": [["(col('a') * col('b')).sum()", "d1"]],
+        "expected": {"d1": [30]},
+    })
+    cases.append({
+        "name": "test_mean_overflow",
+        "source": "operations/aggregation/test_aggregations.py:298-302 (Series.mean, np.isclose)",
+        "cols": {"a": {"dtype": "i64", "values": [9_223_372_036_854_775_800, 100]}},
+        "key": None,
+        "aggs": [["col('a').mean()", "a"]],
+        "expected": {"a": fx([4.611686018427388e18])},
+        "tol": {"a": 1e-9},
+    })
+    return {"cases": cases}
+
+
 def main():
     for name, obj in (("compare_total_order.json", compare_table()),
                       ("group_by_cases.json", group_by_cases()),
@@ -713,7 +805,8 @@ def main():
                       ("sort_cases.json", sort_cases()),
                       ("sort_multi_cases.json", sort_multi_cases()),
                       ("rolling_cases.json", rolling_cases()),
-                      ("arith_cases.json", arith_cases())):
+                      ("arith_cases.json", arith_cases()),
+                      ("reduce_cases.json", reduce_cases())):
         with open(os.path.join(HERE, name), "w") as f:
             json.dump(obj, f, indent=1, sort_keys=False)
             f.write("\n")

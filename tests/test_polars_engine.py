@@ -484,3 +484,67 @@ def test_udf_reuses_resident_columns(gpu):
     PE.execute_with_polaroid(nt, None, config={"device_cache_bytes": 0}, to_frame=lambda t: t)
     assert nt.udf(None, None, None, False).column("k").to_pylist() == t2.column("k").to_pylist()
     PE.column_cache().capacity = 32 << 30
+
+
+def _vwap_ir(table, select=False):
+    """group_by("k").agg((v * w).sum(), (v - 1.0).mean(), when(w > 0).then(v).otherwise(0.0).sum())
+    -- the aggregation inputs the reference pre-aggregates (general.rs:303-356
+    can_pre_agg) -- or, with `select`, filter(w > 0).select(the same aggs, len())."""
+    nt = FakeNT(table)
+    scan = nt.p("DataFrameScan", ["k", "v", "w"], df=FakePolarsDF(table), projection=None, selection=None)
+    vw = nt.bin(nt.col("v"), "Multiply", nt.col("w"))
+    vm1 = nt.bin(nt.col("v"), "Minus", nt.lit(1.0))
+    tern = nt.e("Ternary", predicate=nt.bin(nt.col("w"), "Gt", nt.lit(0)), truthy=nt.col("v"), falsy=nt.lit(0.0))
+    a1 = nt.e("Agg", name="sum", arguments=[vw], options=None)
+    a2 = nt.e("Agg", name="mean", arguments=[vm1], options=None)
+    a3 = nt.e("Agg", name="sum", arguments=[tern], options=None)
+    if select:
+        filt = nt.p("Filter", ["k", "v", "w"], input=scan,
+                    predicate=PyExprIR(nt.bin(nt.col("w"), "Gt", nt.lit(0)), "w"))
+        nt.p("Select", ["vw", "vm1", "pos", "len"], input=filt,
+             expr=[PyExprIR(a1, "vw"), PyExprIR(a2, "vm1"), PyExprIR(a3, "pos"), PyExprIR(nt.e("Len"), "len")])
+        return nt
+    opts = _node("GroupbyOptions", slice=None, dynamic=None, rolling=None)
+    nt.p("GroupBy", ["k", "vw", "vm1", "pos"], input=scan, keys=[PyExprIR(nt.col("k"), "k")],
+         aggs=[PyExprIR(a1, "vw"), PyExprIR(a2, "vm1"), PyExprIR(a3, "pos")], apply=None, maintain_order=True,
+         options=opts)
+    return nt
+
+
+def test_translate_aggregations_over_expressions_and_select():
+    table = _table()[0]
+    plan = PE.translate(_vwap_ir(table))
+    assert plan[0] == "group_by" and [a.output_name() for a in plan[3]] == ["vw", "vm1", "pos"]
+    assert plan[3][0].args[0].args[0].kind == "bin"  # (v * w).sum(): an input expression
+    plan = PE.translate(_vwap_ir(table, select=True))
+    assert plan[0] == "select" and plan[1][0] == "filter"
+    assert [a.output_name() for a in plan[2]] == ["vw", "vm1", "pos", "len"]
+    # a select mixing aggregations and elementwise expressions stays on polars
+    nt = _vwap_ir(table, select=True)
+    nt.lp[nt.root].expr.append(PyExprIR(nt.col("v"), "v"))
+    with pytest.raises(PE.Unsupported):
+        PE.translate(nt)
+
+
+@pytest.mark.gpu
+def test_udf_aggregations_over_expressions_on_gpu(gpu):
+    table, k, v, w, vvalid = _table(100_000, 21)
+    nt = _vwap_ir(table)
+    PE.execute_with_polaroid(nt, None, to_frame=lambda t: t)
+    out = nt.udf(None, None, None, False)
+    keys = out.column("k").to_pylist()
+    assert keys == list(dict.fromkeys(k.tolist()))
+    for i, kk in enumerate(keys):
+        m = (k == kk) & vvalid
+        assert out.column("vw")[i].as_py() == math.fsum(v[m] * w[m])
+        assert out.column("vm1")[i].as_py() == math.fsum(v[m] - 1.0) / int(m.sum())
+        pos = np.where(w[k == kk] > 0, v[k == kk], 0.0)
+        assert out.column("pos")[i].as_py() == math.fsum(pos[vvalid[k == kk]])
+    nt = _vwap_ir(table, select=True)
+    PE.execute_with_polaroid(nt, None, to_frame=lambda t: t)
+    out = nt.udf(None, None, None, False)
+    assert out.num_rows == 1
+    sel = w > 0
+    m = sel & vvalid
+    assert out.column("vw")[0].as_py() == math.fsum(v[m] * w[m])
+    assert out.column("len")[0].as_py() == int(sel.sum())
