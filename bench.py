@@ -48,6 +48,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline time budget")
     ap.add_argument("--cpu-rows", type=float, default=1e7, help="cpu_baseline sample rows (configs[0]: 1e7)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--plugin-rows", type=float, default=1e8,
+                    help="rows of the plugin leg (host Arrow frame through execute_with_polaroid; configs[1] = 1e8)")
+    ap.add_argument("--no-plugin", action="store_true")
     ap.add_argument("--dry-run", action="store_true",
                     help="print this rank's launch parameters and exit before touching the GPU (tests)")
     return ap.parse_args()
@@ -124,6 +127,48 @@ def cpu_baseline(rows: int, groups: int, seconds: float) -> dict:
     return {"value": rows / t / 1e6, "unit": "Mrows/s", "cores": threads, "kind": "port",
             "sample": f"{rows:.0e} rows (configs[0] size) x {len(times)} runs of the same query (median), OpenMP "
                       f"{threads} threads ({cores_note}), oracle/polars_oracle.c:or_baseline_filter_groupby_sum"}
+
+
+def plugin_leg(rows: int, groups: int) -> dict:
+    """The headline query through the polars plugin (execute_with_polaroid,
+    driven by a model of polars' NodeTraverser, tools/ir_model.py) on a host
+    Arrow frame: cold = the first query (scan: Arrow chunks -> HBM over the
+    host link, then the query), warm = the same query again (the scanned
+    columns resident in the plugin's ColumnCache).  rank 0, N = 1 only."""
+    import pyarrow as pa
+
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import ir_model
+
+    from polaroid_amd import polars_engine as PE
+
+    rng = np.random.default_rng(7)
+    base = rng.uniform(10, 490, groups)
+    k = rng.integers(0, groups, rows)
+    p = base[k]
+    o = p * np.exp(0.02 * rng.standard_normal(rows))
+    c = p * np.exp(0.02 * rng.standard_normal(rows))
+    sp = rng.random(rows) * 0.01
+    table = pa.table({"symbol": pa.array((k * 7919 + 1_000_000).astype(np.int64)), "open": pa.array(o),
+                      "high": pa.array(np.maximum(o, c) * (1 + sp)), "low": pa.array(np.minimum(o, c) * (1 - sp)),
+                      "close": pa.array(c)})
+    del k, p, o, c, sp
+    cols = ["open", "high", "low", "close"]
+    PE.column_cache().clear()
+    times = []
+    for _ in range(3):
+        nt = ir_model.filter_group_by_sum(table, "symbol", "close", THRESHOLD, cols, chunk_rows=1 << 23)
+        PE.execute_with_polaroid(nt, None, config={"device_cache_bytes": 64 << 30}, to_frame=lambda t: t)
+        t0 = time.perf_counter()
+        out = nt.udf(None, None, None, False)
+        times.append((time.perf_counter() - t0) * 1e3)
+        assert 0 < out.num_rows <= groups
+    PE.column_cache().clear()
+    cold, warm = times[0], min(times[1:])
+    return {"rows": rows, "bytes": int(table.nbytes), "cold_ms": round(cold, 2), "warm_ms": round(warm, 3),
+            "cold_Mrows_s": round(rows / cold / 1e3, 1), "warm_Mrows_s": round(rows / warm / 1e3, 1),
+            "note": "execute_with_polaroid on a host Arrow frame of 8M-row RecordBatches; cold = scan over the "
+                    "host link + query, warm = scanned columns resident (ColumnCache); result to Arrow"}
 
 
 def load_traffic(n_rows: int):
@@ -276,6 +321,12 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(int(args.cpu_rows), args.groups, args.cpu_seconds)
+    if rank == 0 and world == 1 and not args.no_plugin:
+        del df, query, out, sym, cols
+        torch.cuda.empty_cache()
+        result["plugin"] = plugin_leg(int(args.plugin_rows), args.groups)
+        result["plugin_cold_ms"] = result["plugin"]["cold_ms"]
+        result["plugin_warm_ms"] = result["plugin"]["warm_ms"]
     if rank == 0:
         print(json.dumps(result), flush=True)
     if distributed:

@@ -204,6 +204,8 @@ typedef struct plgpu_groupby_info {
     double main_kernel_ms;       /* device time of the aggregation kernel(s)   */
     int32_t path;                /* 0 generic, 1 fast, 2 fast sum-only, 3 partitioned */
     int32_t sum_limbs;           /* 40-bit LDS limbs per f64 sum (2 or 3)      */
+    int32_t local_range;         /* 1: range-local fused kernel (clustered keys) */
+    int32_t _pad;
 } plgpu_groupby_info;
 
 /* ---------------------------------------------------------------- basics */
@@ -228,6 +230,8 @@ int plgpu_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream);
  *   "mk_collide"  a 3-bit first tuple hash (forces the collision / re-seed path)
  *   "runs"        -1: the plan decides; 0 / 1 force the sorted-key variant of
  *                 the fused group-by kernel
+ *   "local"       -1: the plan decides; 0 keeps the group-by off the
+ *                 range-local fused kernel (clustered keys)
  * An unknown name is PLGPU_ERR_INVALID. */
 int plgpu_set_option(const char* name, int64_t value);
 int plgpu_get_option(const char* name, int64_t* out);

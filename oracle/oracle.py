@@ -202,7 +202,13 @@ def _input_col(cols: list[HostCol], program, nrows: int, kinds: set) -> HostCol:
     elementwise restatement).  A Boolean input sums as IdxSize counts
     (polars-expr/src/reduce/sum.rs:147-180 BoolSumReducer) and averages as
     0 / 1 Float64 (reduce/mean.rs)."""
-    dt, v, valid = eval_program(cols, program, nrows)
+    if nrows == 0:
+        # no row: the program's dtype from one all-zero row of the same columns
+        probe = [HostCol(np.zeros(1, np.bool_ if c.code == BOOL else _NP_OF[c.code])) for c in cols]
+        dt, _, _ = eval_program(probe, program, 1)
+        v, valid = np.zeros(0, np.bool_ if dt == BOOL else _NP_OF[dt]), np.zeros(0, bool)
+    else:
+        dt, v, valid = eval_program(cols, program, nrows)
     if dt == BOOL:
         v = v.astype(np.float64 if "mean" in kinds else np.uint32)
     return HostCol(np.ascontiguousarray(v), valid)

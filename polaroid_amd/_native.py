@@ -88,6 +88,8 @@ class GroupByInfo(C.Structure):
         ("main_kernel_ms", C.c_double),
         ("path", C.c_int32),
         ("sum_limbs", C.c_int32),
+        ("local_range", C.c_int32),
+        ("_pad", C.c_int32),
     ]
 
     def as_dict(self) -> dict:

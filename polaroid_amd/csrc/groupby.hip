@@ -74,7 +74,8 @@ enum : int {
     ST_SHIFT_OVF = 14,   // merge: a shifted f64 sum state left the 192-bit range
     ST_MINEX = 17,       // + acc: 0x7FF - smallest exponent of a nonzero finite value (plan / maxexp)
     ST_RUNS = 23,        // plan: sampled adjacent row pairs with equal keys (sorted / clustered keys)
-    ST_WORDS = 24
+    ST_LOCAL = 24,       // plan: most distinct keys among the samples of one 1/kPlanKeyBlocks row range
+    ST_WORDS = 25
 };
 
 // An aggregation input derived from the columns in registers (an
@@ -134,7 +135,10 @@ struct GbParams {
     const uint64_t* part_range;
     const uint32_t* part_rows;
     int32_t part_blocks;
-    int32_t _pad3;
+    // fast kernel, range-local mode (clustered keys): workgroup b takes the
+    // contiguous tiles [b * tiles_per_wg, (b + 1) * tiles_per_wg); 0 = the
+    // grid-strided tile order
+    int32_t tiles_per_wg;
 };
 
 // ------------------------------------------------------ invariant checks
@@ -1055,6 +1059,13 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
     int64_t nall = ntiles + (p.n > p.n_full ? 1 : 0);  // + the masked tail tile
     int64_t t = blockIdx.x, tstep = gridDim.x;
     int64_t rbase = 0, rlo = 0, rhi = 0, rmax = -1;
+    if (!PART && p.tiles_per_wg > 0) {
+        // range-local mode: one contiguous run of tiles per workgroup, so
+        // its LDS table holds only the keys of that row range
+        t = (int64_t)blockIdx.x * p.tiles_per_wg;
+        nall = std::min<int64_t>(nall, t + p.tiles_per_wg);
+        tstep = 1;
+    }
     if (PART) {
         const int q = blockIdx.x / p.part_blocks;
         rlo = (int64_t)p.part_range[q];
@@ -1467,21 +1478,31 @@ __device__ __forceinline__ int64_t plan_row(int64_t i, int64_t n, int64_t sample
 // (One workgroup per task took 147 us per plan at 1e9 rows: 16 dependent
 // rounds of strided loads.)
 constexpr int kPlanBlocks = 16;
+// The key task runs kPlanKeyBlocks workgroups, each over the samples of one
+// contiguous 1/kPlanKeyBlocks of the rows, and reports the most distinct
+// keys any one of them saw (ST_LOCAL): keys that are clustered in row order
+// (time-ordered (symbol, day), frames sorted by a key) show few per range
+// even when the column holds many.
+constexpr int kPlanKeyBlocks = 128;
 
 __global__ __launch_bounds__(kPlanThreads) void gb_plan_kernel(GbParams p, uint64_t* __restrict__ gset,
                                                                int64_t samples) {
     __shared__ uint64_t set[kPlanSetSlots];
     __shared__ uint32_t red[2][kPlanThreads / 64];
-    const int a = blockIdx.x / kPlanBlocks;
-    const int64_t per = (samples + kPlanBlocks - 1) / kPlanBlocks;
-    const int64_t s0 = (int64_t)(blockIdx.x % kPlanBlocks) * per;
+    const bool key_task = (int)blockIdx.x >= p.nacc * kPlanBlocks;
+    const int a = key_task ? p.nacc : (int)blockIdx.x / kPlanBlocks;
+    const int nb = key_task ? kPlanKeyBlocks : kPlanBlocks;
+    const int bi = key_task ? (int)blockIdx.x - p.nacc * kPlanBlocks : (int)blockIdx.x % kPlanBlocks;
+    const int64_t per = (samples + nb - 1) / nb;
+    const int64_t s0 = (int64_t)bi * per;
     const int64_t s1 = s0 + per < samples ? s0 + per : samples;
     const int64_t n = p.n;
-    if (a == p.nacc) {
+    if (key_task) {
         for (int i = threadIdx.x; i < kPlanSetSlots; i += blockDim.x) set[i] = kEmptyKey;
         __syncthreads();
         const int bits = __builtin_ctz(kPlanSetSlots);
         unsigned long long runs = 0;  // samples whose next row holds the same key
+        uint32_t nlocal = 0;          // distinct keys new to this workgroup's set
         // kPlanBatch strided samples per thread are loaded before any is
         // inserted: one memory round trip per batch, not per sample
         for (int64_t i0 = s0 + threadIdx.x; i0 < s1; i0 += (int64_t)blockDim.x * kPlanBatch) {
@@ -1517,6 +1538,7 @@ __global__ __launch_bounds__(kPlanThreads) void gb_plan_kernel(GbParams p, uint6
                 }
             }
             if (!fresh) continue;
+            ++nlocal;
             // new to this workgroup: into the global set, unless the count
             // already reached the saturation mark (then only the HLL pass
             // can size the table, and more inserts would only probe a full set)
@@ -1536,6 +1558,15 @@ __global__ __launch_bounds__(kPlanThreads) void gb_plan_kernel(GbParams p, uint6
           }
         }
         if (runs) atomicAdd((unsigned long long*)&p.status[ST_RUNS], runs);
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) nlocal += __shfl_xor(nlocal, off, 64);
+        if ((threadIdx.x & 63) == 0) red[0][threadIdx.x >> 6] = nlocal;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t t = 0;
+            for (int w = 0; w < kPlanThreads / 64; ++w) t += red[0][w];
+            atomicMax((unsigned long long*)&p.status[ST_LOCAL], (unsigned long long)t);
+        }
         return;
     }
     const AccSpec& ac = p.acc[a];
@@ -1888,6 +1919,7 @@ struct Plan {
     int limbs;         // SUMONLY: 40-bit LDS limbs per f64 sum (3, or 2 for narrow exponent spans)
     int fast_grid;
     bool runs;         // sampled keys mostly equal their next row's (sorted / clustered input)
+    bool local;        // range-local mode: contiguous tiles per workgroup, LDS sized by range-local keys
     mutable int launched_grid;  // grid of the last fast launch (info)
 };
 
@@ -2136,7 +2168,14 @@ static hipError_t launch_fast_rows(const Plan& pl, const DevProgram& dp, hipStre
     if (g > useful) g = std::max<int64_t>(1, useful);
     const int grid = (int)g;
     pl.launched_grid = grid;
-    gb_fast_kernel<NACC, PRED, SUMONLY, ROWS, LIMBS, RUNS, false, DERIV><<<grid, kGbThreads, lds, s>>>(pl.p, dp);
+    GbParams q = pl.p;
+    q.tiles_per_wg = 0;
+    if (pl.local) {
+        const int64_t tile = (int64_t)kGbThreads * ROWS;
+        const int64_t nall = pl.p.n_full / tile + (pl.p.n > pl.p.n_full ? 1 : 0);
+        q.tiles_per_wg = (int32_t)((nall + grid - 1) / grid);
+    }
+    gb_fast_kernel<NACC, PRED, SUMONLY, ROWS, LIMBS, RUNS, false, DERIV><<<grid, kGbThreads, lds, s>>>(q, dp);
     return hipGetLastError();
 }
 
@@ -2480,7 +2519,8 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
     Plan& pl = R.pl;
     GbParams& p = pl.p;
     const int64_t n = p.n;
-    gb_plan_kernel<<<(p.nacc + 1) * kPlanBlocks, kPlanThreads, 0, R.s>>>(p, R.status + kPlanSetWord, kPlanSamples);
+    gb_plan_kernel<<<p.nacc * kPlanBlocks + kPlanKeyBlocks, kPlanThreads, 0, R.s>>>(p, R.status + kPlanSetWord,
+                                                                                   kPlanSamples);
     PLGPU_HIP(hipGetLastError());
     PLGPU_HIP(hipMemcpyAsync(R.st, R.status, sizeof R.st, hipMemcpyDeviceToHost, R.s));
     PLGPU_HIP(hipStreamSynchronize(R.s));
@@ -2509,6 +2549,30 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
         hll = (int64_t)hll_estimate(h.data());
     }
     size_tables(&pl, R.st[ST_DISTINCT], R.st[ST_SAMPLED], &R.gbits, hll, &R.est_groups);
+    // range-local mode: too many keys for one LDS table over the column, but
+    // few within each contiguous row range (the plan's per-range sample
+    // count ST_LOCAL: a range's samples repeat their keys); the fused kernel
+    // then gives each workgroup one contiguous run of tiles and an LDS table
+    // sized for about twice the keys one range showed.  Keys beyond it take
+    // the global table, so the choice only changes speed.
+    pl.local = false;
+    const int lbits0 = p.lbits, lcap0 = p.lcap;
+    const size_t lds0 = pl.lds_bytes;
+    {
+        const uint64_t local = R.st[ST_LOCAL];
+        const uint64_t per_range = (uint64_t)std::min<int64_t>(n, kPlanSamples) / kPlanKeyBlocks;
+        if (!pl.use_lds && n >= (int64_t(1) << 22) && local > 0 && local * 4 <= per_range * 3 &&
+            options().local != 0) {
+            const int lb = log2_ceil(std::max<int64_t>(64, 2 * (int64_t)local));
+            const size_t bytes = (size_t)p.nfields * ((1u << lb) + 2) * 8;
+            if (bytes <= (size_t)160 * 1024) {
+                pl.local = pl.use_lds = true;
+                p.lbits = lb;
+                p.lcap = 1 << lb;
+                pl.lds_bytes = bytes;
+            }
+        }
+    }
     // fast path eligibility: no nulls, 8-byte columns
     // at even offsets of 16-byte aligned buffers, simple or no predicate,
     // LDS table in use
@@ -2522,6 +2586,13 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
         if (p.acc[a].dop != DOP_NONE && !(p.acc[a].dop & DOP_LIT)) fast = fast && ok(p.acc[a].c2);
     }
     if (R.pred == 1 && p.pred_acc < 0) fast = fast && ok(p.pred_col);
+    if (pl.local && !fast) {
+        // the generic kernel walks the rows grid-strided: no range-local table
+        pl.local = pl.use_lds = false;
+        p.lbits = lbits0;
+        p.lcap = lcap0;
+        pl.lds_bytes = lds0;
+    }
     const int64_t tile = (int64_t)2 * kGbThreads;
     p.n_full = fast ? (n / tile) * tile : 0;
     {
@@ -2929,6 +3000,7 @@ static void gb_fill_info(const GbRun& R, plgpu_groupby_info* info) {
     info->main_kernel_ms = R.ms;
     info->path = R.part ? 3 : (p.n_full > 0 ? (R.pl.sum_only ? 2 : 1) : 0);
     info->sum_limbs = (p.n_full > 0 || R.part) && R.pl.sum_only ? R.pl.limbs : 3;
+    info->local_range = R.pl.local ? 1 : 0;
     for (int a = 0; a < p.nacc; ++a)
         if (((R.st[ST_FXFLAGS] >> (2 * a)) & 2u) && !((R.wide >> a) & 1u)) info->sum_inexact |= 1 << a;
 }

@@ -39,6 +39,7 @@ struct Options {
     int no_pack = 0;     // multi-key operators hash tuples even when they would pack (tests)
     int mk_collide = 0;  // 3-bit first tuple hash: forces the collision / re-seed path (tests)
     int runs = -1;       // -1: the plan picks the sorted-key variant; 0 / 1 force it (tests)
+    int local = -1;      // -1: the plan picks the range-local kernel; 0 keeps it off (tests)
 };
 Options& options();
 int dev_alloc(void** p, size_t bytes, hipStream_t s);

@@ -1334,7 +1334,8 @@ def _gb_lower(df: DataFrame, key: str | tuple | None, aggs: list[Expr], pred: Ex
         if base.kind == "len":
             specs.append(("len", len_col))
             out_logical.append(None)
-        elif base.kind == "agg" and base.args[0].kind == "col" and base.args[0].value in df._cols:
+        elif (base.kind == "agg" and base.args[0].kind == "col" and base.args[0].value in df._cols
+              and df._cols[base.args[0].value].dtype is not Boolean):
             c_ = base.args[0].value
             specs.append((base.op, c_))
             lg = df._cols[c_]._logical_dtype()
@@ -1392,15 +1393,15 @@ def _gb_lower(df: DataFrame, key: str | tuple | None, aggs: list[Expr], pred: Ex
         dt = C.c_int32(0)
         N.check(N.lib().plgpu_expr_dtype(cols, ncols, prog, builtins.len(prog), C.byref(dt)))
         if dt.value == N.BOOL:
+            # Boolean inputs: sums count (IdxSize), means average 0 / 1
             kinds = {k for k, c_ in specs if c_ == ("input", j)}
             if kinds - set(_BOOL_AGG_CAST) - {"count", "len"}:
                 raise N.InvalidOperationError("min / max / first / last of a Boolean expression are not supported "
                                               "on the GPU executor")
             if builtins.len({_BOOL_AGG_CAST[k] for k in kinds if k in _BOOL_AGG_CAST}) > 1:
                 raise N.InvalidOperationError("sum and mean of one Boolean expression in one group-by")
-            to = next((_BOOL_AGG_CAST[k] for k in kinds if k in _BOOL_AGG_CAST), None)
-            if to is not None:
-                prog = to_instr_array(lower(x.cast(UInt32 if to == "UInt32" else Float64), idx, schema))
+            to = next((_BOOL_AGG_CAST[k] for k in kinds if k in _BOOL_AGG_CAST), "UInt32")
+            prog = to_instr_array(lower(x.cast(UInt32 if to == "UInt32" else Float64), idx, schema))
         keep_progs.append(prog)
         inputs[j].program = C.cast(prog, C.POINTER(N.Instr))
         inputs[j].n_instr = builtins.len(prog)

@@ -399,9 +399,18 @@ class ColumnCache:
             return
         self._d[key] = (series, chunks, nbytes)
         self.bytes += nbytes
+        self._evict()
+
+    def _evict(self) -> None:
         while self.bytes > self.capacity and self._d:
             _, (_, _, nb) = self._d.popitem(last=False)
             self.bytes -= nb
+
+    def resize(self, capacity: int) -> None:
+        """New capacity in bytes; entries beyond it are released now (their
+        device memory returns to the pool), least recently used first."""
+        self.capacity = max(0, int(capacity))
+        self._evict()
 
     def clear(self) -> None:
         self._d.clear()
@@ -540,13 +549,22 @@ def execute_with_polaroid(nt, duration_since_start: int | None = None, *, config
         cache_bytes = getattr(config, "device_cache_bytes", None)
     cache = _COLUMN_CACHE
     if cache_bytes is not None:
-        cache.capacity = int(cache_bytes)
+        cache.resize(int(cache_bytes))
         if cache.capacity <= 0:
             cache.clear()
             cache = None
 
     def _udf(with_columns, predicate, n_rows, should_time=False):
-        df = _restore_dtypes(run_plan(plan, n_rows, to_frame, cache), schema)
+        try:
+            res = run_plan(plan, n_rows, to_frame, cache)
+        except N.OutOfMemoryError:
+            if cache is None or not len(cache._d):
+                raise
+            # resident columns of earlier queries hold the memory this one
+            # needs: release them and run once more (scans re-upload)
+            cache.clear()
+            res = run_plan(plan, n_rows, to_frame, cache)
+        df = _restore_dtypes(res, schema)
         if with_columns is not None:
             df = df.select(with_columns)
         if should_time:

@@ -577,6 +577,8 @@ def test_group_by_register_accumulators(gpu, layout, plgpu_option):
         plgpu_option("runs", 1)
     else:
         key = np.sort(key)
+    if layout == "sorted_part":
+        plgpu_option("local", 0)  # keep sorted many-groups keys on the partitioned path
     cols = {"a": (a, None), "d": (d, None)}
     aggs = [("sum", "a"), ("sum", "d"), ("mean", "a")]
     info = {}
@@ -585,3 +587,38 @@ def test_group_by_register_accumulators(gpu, layout, plgpu_option):
     assert info["sum_limbs"] == 2, info
     if layout == "sorted_part":
         assert info["path"] == 3, info
+
+
+@pytest.mark.parametrize("layout", ["day_ordered", "symbol_sorted", "clustered_blocks", "random_control"])
+@pytest.mark.parametrize("aggs_kind", ["sums", "mixed"])
+def test_group_by_range_local_kernel(gpu, layout, aggs_kind):
+    """Keys clustered in row order (time-ordered (symbol, day) codes, a frame
+    sorted by symbol, blocks of a few keys): the plan sees few keys per row
+    range although the column holds many, and the fused kernel gives each
+    workgroup one contiguous run of tiles with an LDS table sized for that
+    range (keys it misses take the global table).  Random keys keep the
+    partitioned path.  Exact vs the oracle."""
+    rng = np.random.default_rng(len(layout) * 7 + len(aggs_kind))
+    n = 4_500_001
+    if layout == "day_ordered":
+        day = (np.arange(n) * 200) // n
+        key = (rng.integers(0, 150, n) + 1000 * day).astype(np.int64)  # 30k groups, 150 per day
+    elif layout == "symbol_sorted":
+        key = np.sort(rng.integers(0, 40_000, n)).astype(np.int64) * 13
+    elif layout == "clustered_blocks":
+        blk = np.arange(n) // 65536
+        key = (rng.integers(0, 64, n) * 100_003 + blk * 7).astype(np.int64)
+    else:
+        key = rng.integers(0, 40_000, n).astype(np.int64)
+    a = rng.uniform(10, 500, n)
+    d = rng.standard_normal(n)
+    cols = {"a": (a, None), "d": (d, None)}
+    aggs = [("sum", "a"), ("sum", "d")] if aggs_kind == "sums" else \
+        [("sum", "a"), ("min", "d"), ("max", "a"), ("count", "d"), ("len", "a")]
+    info = {}
+    mk, names, prog = PREDICATES["simple_f64"]
+    _check_group_by(cols, key, None, aggs, mk(), prog, names, False, info)
+    if layout == "random_control":
+        assert info["local_range"] == 0, info
+    else:
+        assert info["local_range"] == 1 and info["path"] in (1, 2), info
