@@ -1800,14 +1800,16 @@ __global__ void gb_export_kernel(GbParams p, int world, uint64_t* cursor, uint64
 }
 
 // (w2:w1:w0) <<= d as a two's-complement 192-bit integer, 0 <= d; false
-// (value unchanged) when the result would not fit.
-__device__ __forceinline__ bool shl192(uint64_t& w0, uint64_t& w1, uint64_t& w2, int d) {
-    if (d == 0) return true;
+// (value unchanged) when the result would not fit with `guard` bits to
+// spare (so that 2^guard such values still add without wrapping).
+__device__ __forceinline__ bool shl192(uint64_t& w0, uint64_t& w1, uint64_t& w2, int d, int guard = 0) {
+    if (d == 0 && guard == 0) return true;
     const uint64_t sign = (uint64_t)((int64_t)w2 >> 63);
-    if (d >= 191) return (w0 | w1 | w2) == 0;
-    // the top d + 1 bits must all equal the sign
+    const int top = d + guard;
+    if (top >= 191) return (w0 | w1 | w2) == 0;
+    // the top d + guard + 1 bits must all equal the sign
     const uint64_t x[3] = {w0, w1, w2};
-    for (int b = 191 - d; b < 192; b += 64) {
+    for (int b = 191 - top; b < 192; b += 64) {
         const int lo = b, hi = b + 64 < 192 ? b + 64 : 192;  // bits [lo, hi) of this chunk
         const int wi = lo >> 6, sh = lo & 63;
         uint64_t chunk = x[wi] >> sh;
@@ -1816,6 +1818,7 @@ __device__ __forceinline__ bool shl192(uint64_t& w0, uint64_t& w1, uint64_t& w2,
         const uint64_t m = nb == 64 ? ~0ull : ((1ull << nb) - 1);
         if ((chunk & m) != (sign & m)) return false;
     }
+    if (d == 0) return true;
     const int q = d >> 6, r = d & 63;
     uint64_t o[3];
     for (int i = 0; i < 3; ++i) {
@@ -1840,6 +1843,9 @@ __global__ void gb_merge_kernel(GbParams p, const uint64_t* __restrict__ rec, in
     const int rw = p.nfields + 1;
     uint32_t special = 0;
     bool ovf = false;
+    // up to nsrc states fold into one cell: each must leave ceil(log2 nsrc)
+    // sign bits to spare, so their sum cannot wrap the 192-bit cell
+    const int guard = nsrc > 1 ? 32 - __clz((unsigned)(nsrc - 1)) : 0;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nrec; i += (int64_t)gridDim.x * blockDim.x) {
         const uint64_t* r = rec + i * rw;
         const uint64_t kind = r[0];
@@ -1874,7 +1880,7 @@ __global__ void gb_merge_kernel(GbParams p, const uint64_t* __restrict__ rec, in
                     int d = 0;
                     for (int a = 0; a < p.nacc; ++a)
                         if (p.acc[a].f_sum == f) d = src_shift[src * kMaxAcc + a];
-                    if (!shl192(w0, w1, w2, d)) {
+                    if (!shl192(w0, w1, w2, d, guard)) {
                         ovf = true;
                         break;
                     }

@@ -224,19 +224,23 @@ def run_partitioned(part, world: int, group, device, timings: dict | None = None
     (export + the two all-to-alls) and merge_ms."""
     t0 = time.perf_counter()
     err = None
+    bottoms = [0] * N.GB_MAX_ACC
+    send = counts = None
     try:
         bottoms = part.begin()
-    except N.PolaroidError as e:  # refused locally (e.g. a wide-range f64 sum)
+        if timings is not None:
+            _sync(device)
+        t1 = time.perf_counter()
+        send, counts = part.export()
+    except Exception as e:  # noqa: BLE001 -- refused locally (a wide-range f64 sum) or any failure
+        # before the exchange: the count exchange still runs, with status 1
+        # and no records, so every rank learns of it instead of waiting
         err = e
         bottoms = [0] * N.GB_MAX_ACC
-    if timings is not None:
-        _sync(device)
-    t1 = time.perf_counter()
-    if err is None:
-        send, counts = part.export()
-    else:
+    if err is not None or send is None:
         import torch
 
+        t1 = time.perf_counter()
         send, counts = torch.empty(0, dtype=torch.int64, device=device), [0] * world
     recv, n, rows = exchange_records(send, counts, part.record_words, group,
                                      header=[1 if err is not None else 0] + list(bottoms))
@@ -263,9 +267,26 @@ def run_first_last(ops, local, world: int, group=None):
     same partition function as the records), arrive in source-rank order
     (all-to-all), and the owner takes first() / last() over them
     (`ops.combine`): the lowest rank holding a group has its first row, the
-    highest its last.  Returns this rank's (key + first / last) frame."""
-    perm, counts = ops.route(local, world)
-    recv, n = exchange_columns(ops.to_wire(local, perm), counts, group)
+    highest its last.  Returns this rank's (key + first / last) frame.
+
+    `local` may be a callable producing that frame: a failure there or in
+    the routing (on any rank) is agreed by one status all-reduce before the
+    exchange, so every rank raises instead of waiting in a collective."""
+    err = None
+    wire = counts = None
+    try:
+        if callable(local):
+            local = local()
+        perm, counts = ops.route(local, world)
+        wire = ops.to_wire(local, perm)
+    except Exception as e:  # noqa: BLE001
+        err = e
+    failed = _allreduce_max([1 if err is not None else 0], group, _device_for(group))[0]
+    if err is not None:
+        raise err
+    if failed:
+        raise N.ComputeError("multi-GPU first() / last(): the local stage failed on another rank")
+    recv, n = exchange_columns(wire, counts, group)
     return ops.combine(ops.from_wire(recv, n))
 
 
@@ -556,9 +577,14 @@ def group_by_agg(df, key: str, aggs: Sequence[Expr], predicate: Expr | None = No
     if fl:
         t0 = time.perf_counter()
         ops = GpuFirstLastOps(key, [aggs[i] for i in fl])
-        local = _group_by(df, key, ops.exprs, False, predicate, None)
-        logical = {e.output_name(): local[e.output_name()]._logical_dtype() for e in ops.exprs}
-        owned = run_first_last(ops, local, world, group)
+        logical = {}
+
+        def local_stage():
+            loc = _group_by(df, key, ops.exprs, False, predicate, None)
+            logical.update({e.output_name(): loc[e.output_name()]._logical_dtype() for e in ops.exprs})
+            return loc
+
+        owned = run_first_last(ops, local_stage, world, group)
         for nm, lg in logical.items():
             owned[nm]._with_logical(lg)
         if out is None:

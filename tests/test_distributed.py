@@ -245,3 +245,40 @@ def test_first_last_protocol_gloo(world):
     shards = [_fl_shard(r) for r in range(world)]
     full = _first_last(*[np.concatenate([s[i] for s in shards]) for i in range(4)])
     assert merged == full
+
+
+def _fl_fail_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        def local():
+            if rank == world - 1:
+                raise RuntimeError("local first/last stage failed")
+            return _first_last(*_fl_shard(rank))
+
+        try:
+            D.run_first_last(HostFirstLastOps(), local, world)
+            q.put((rank, "no error"))
+        except Exception as e:  # noqa: BLE001
+            q.put((rank, type(e).__name__))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_first_last_failure_reaches_every_rank_gloo():
+    """A rank whose local first / last stage fails: every rank raises (the
+    status all-reduce before the exchange), none waits in a collective."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fl_fail_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[world - 1] == "RuntimeError"
+    assert all(res[r] == "ComputeError" for r in range(world - 1))

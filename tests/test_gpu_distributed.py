@@ -12,6 +12,7 @@ f64 sums are associative, so sharding cannot change them).  The real
 torch.distributed path is exercised at world_size 1 over RCCL.
 """
 
+import math
 import os
 import socket
 
@@ -536,3 +537,34 @@ def test_group_by_agg_world1_rccl_float_and_narrow_keys(gpu):
             assert table(out) == table(ref), key
     finally:
         dist.destroy_process_group()
+
+
+def test_merge_sources_sum_guard_bits(gpu):
+    """Several sources' 192-bit sum states fold into one cell: each shifted
+    state must leave ceil(log2 sources) sign bits to spare, so states that
+    each fit cannot wrap the cell when added (refused, never wrong).
+    Records are built by hand: [kind, key, len, w0, w1, w2, flags]."""
+    import torch
+
+    a = pl.Series.from_numpy("a", np.zeros(1))
+    df = pl.DataFrame({"k": pl.Series.from_numpy("k", np.zeros(1, np.int64)), "a": a})
+    g = _gb_lower(df, "k", [pl.col("a").sum().alias("s")], None)
+    part = D.GpuPartial(g, 3)
+    assert part.record_words == 7
+    base = -100
+
+    def run(big_w1):
+        rec = [[0, 5, 1, 1, 0, 0, 0],          # source 0: state 1 at bottom `base`
+               [0, 5, 1, 0, big_w1, 0, 0],     # sources 1, 2: state big_w1 * 2^64 at bottom base + 78
+               [0, 5, 1, 0, big_w1, 0, 0]]
+        t = torch.tensor(rec, dtype=torch.int64, device="cuda").flatten()
+        bottoms = [[base] + [0] * 5, [base + 78] + [0] * 5, [base + 78] + [0] * 5]
+        return part.merge(t, [1, 1, 1], bottoms)[0]
+
+    # 2^112 shifted by 78 is 2^190: alone it fits 192 bits, two of them wrap
+    with pytest.raises(pl.ComputeError, match="192-bit"):
+        run(1 << 48)
+    # 2^100 shifted: 2^178 each, the exact sum is representable
+    out = run(1 << 36)
+    want = math.ldexp(1.0, base) + 2 * math.ldexp(1.0, 100 + base + 78)
+    assert out["s"].to_list() == [want]
