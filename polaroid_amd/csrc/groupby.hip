@@ -2538,7 +2538,16 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
     if (fixed)
         for (int a = 0; a < kMaxAcc; ++a) R.hb[a] = fixed[a];
     int64_t hll = -1;
-    if (R.st[ST_DISTINCT] >= (uint64_t)kPlanSetSlots / 2 && n > 4 * (int64_t)kPlanSamples) {
+    // clustered keys (the range-local test below): every row range's keys
+    // showed in its samples, so the column holds at most ~kPlanKeyBlocks x
+    // that many; twice that sizes the global table without the HLL pass
+    // (a miss only costs a table-size rerun)
+    const uint64_t local = R.st[ST_LOCAL];
+    const uint64_t per_range = (uint64_t)std::min<int64_t>(n, kPlanSamples) / kPlanKeyBlocks;
+    const bool clustered = n >= (int64_t(1) << 22) && local > 0 && local * 4 <= per_range * 3 && options().local != 0;
+    if (clustered && R.st[ST_DISTINCT] >= (uint64_t)kPlanSetSlots / 2)
+        hll = std::min<int64_t>(n, (int64_t)local * kPlanKeyBlocks * 2);
+    if (hll < 0 && R.st[ST_DISTINCT] >= (uint64_t)kPlanSetSlots / 2 && n > 4 * (int64_t)kPlanSamples) {
         uint32_t* regs = nullptr;
         std::vector<uint32_t> h(1 << kHllBits);
         int rc = dev_alloc((void**)&regs, h.size() * 4, R.s);
@@ -2565,10 +2574,7 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
     const int lbits0 = p.lbits, lcap0 = p.lcap;
     const size_t lds0 = pl.lds_bytes;
     {
-        const uint64_t local = R.st[ST_LOCAL];
-        const uint64_t per_range = (uint64_t)std::min<int64_t>(n, kPlanSamples) / kPlanKeyBlocks;
-        if (!pl.use_lds && n >= (int64_t(1) << 22) && local > 0 && local * 4 <= per_range * 3 &&
-            options().local != 0) {
+        if (!pl.use_lds && clustered) {
             const int lb = log2_ceil(std::max<int64_t>(64, 2 * (int64_t)local));
             const size_t bytes = (size_t)p.nfields * ((1u << lb) + 2) * 8;
             if (bytes <= (size_t)160 * 1024) {
@@ -3788,19 +3794,37 @@ PLGPU_API int plgpu_gb_merge_sources(const void* records, int32_t n_sources, con
 // ------------------------------------------------------ multi-key group-by
 // Packed path: group by the exact Int64 code, then decode the output codes
 // into the key columns.
-static int gb_multi_packed(const MkKeys& mk, const MkPack& pk, int64_t n, const plgpu_column* keys, int32_t nkeys,
+// `checked`: pk comes from sampled ranges (mk_plan_pack_sampled); a row
+// outside them sets *repack (nothing else done) and the caller repacks
+// with the exact ranges.
+static int gb_multi_packed(const MkKeys& mk, MkPack pk, int64_t n, const plgpu_column* keys, int32_t nkeys,
                            const plgpu_column* cols, int32_t ncols, const Deriv* deriv, const plgpu_instr* program,
                            int32_t n_instr, const plgpu_agg* aggs, int32_t naggs, int32_t maintain_order,
-                           plgpu_column* out_keys, plgpu_column* out_aggs, plgpu_groupby_info* info, void* stream) {
+                           plgpu_column* out_keys, plgpu_column* out_aggs, plgpu_groupby_info* info, void* stream,
+                           bool checked = false, bool* repack = nullptr) {
     hipStream_t s = as_stream(stream);
+    if (repack) *repack = false;
     uint64_t* codes = nullptr;
-    int rc = dev_alloc((void**)&codes, (size_t)std::max<int64_t>(n, 1) * 8, s);
+    int rc = dev_alloc((void**)&codes, (size_t)std::max<int64_t>(n, 1) * 8 + (checked ? 8 : 0), s);
     if (rc) return rc;
     if (n > 0) {
+        unsigned int* outside = checked ? (unsigned int*)(codes + std::max<int64_t>(n, 1)) : nullptr;
+        hipError_t e = hipSuccess;
+        if (outside) e = hipMemsetAsync(outside, 0, 4, s);
         const int g = (int)std::min<int64_t>((n + 255) / 256, (int64_t)num_cus() * 16);
-        mk_pack_kernel<<<g, 256, 0, s>>>(mk, pk, n, codes, nullptr);
-        hipError_t e = hipGetLastError();
+        if (e == hipSuccess) {
+            mk_pack_kernel<<<g, 256, 0, s>>>(mk, pk, n, codes, nullptr, outside);
+            e = hipGetLastError();
+        }
+        unsigned int bad = 0;
+        if (e == hipSuccess && outside) e = hipMemcpyAsync(&bad, outside, 4, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess && outside) e = hipStreamSynchronize(s);
         if (e != hipSuccess) rc = hip_fail(e, "mk_pack_kernel");
+        if (!rc && bad) {
+            dev_free(codes, s);
+            *repack = true;
+            return PLGPU_OK;
+        }
     }
     plgpu_column ck;
     std::memset(&ck, 0, sizeof ck);
@@ -3910,8 +3934,21 @@ static int gb_multi_impl(const plgpu_column* keys, int32_t nkeys, const plgpu_co
     {
         // integer keys whose ranges fit 63 bits together: one exact packed
         // Int64 key, grouped by the single-key paths (no hash, no verify)
+        // The plan comes from a sample of the key columns first (no full
+        // range pass); a row outside the sampled (widened) ranges sends it
+        // to the exact range pass and a repack.
         MkPack pk;
-        int rc = mk_plan_pack(mk, n, nullptr, 0, std::max(hg, 1), &pk, s);
+        int rc = PLGPU_OK;
+        if (n >= (int64_t(1) << 20)) {
+            if ((rc = mk_plan_pack_sampled(mk, n, &pk, s))) return rc;
+            if (pk.ok) {
+                bool repack = false;
+                rc = gb_multi_packed(mk, pk, n, keys, nkeys, cols, ncols, deriv, program, n_instr, aggs, naggs,
+                                     maintain_order, out_keys, out_aggs, info, stream, true, &repack);
+                if (rc || !repack) return rc;
+            }
+        }
+        rc = mk_plan_pack(mk, n, nullptr, 0, std::max(hg, 1), &pk, s);
         if (rc) return rc;
         if (pk.ok) return gb_multi_packed(mk, pk, n, keys, nkeys, cols, ncols, deriv, program, n_instr, aggs, naggs,
                                           maintain_order, out_keys, out_aggs, info, stream);

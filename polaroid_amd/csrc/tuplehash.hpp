@@ -154,11 +154,51 @@ __global__ __launch_bounds__(256) void mk_range_kernel(MkKeys k, int64_t n, unsi
     }
 }
 
+// Sampled key ranges (the group-by's optimistic packing): `samples` rows in
+// clusters of 16 consecutive rows spread evenly over the column, per key
+// [ord(min), ord(max), any null] into stats as mk_range_kernel does.
+__global__ __launch_bounds__(256) void mk_sample_range_kernel(MkKeys k, int64_t n, int64_t samples,
+                                                              unsigned long long* __restrict__ stats) {
+    const int64_t m = n < samples ? n : samples;
+    const int64_t cstep = n <= samples ? 16 : n / (samples >> 4);
+    for (int i = 0; i < k.n; ++i) {
+        const DevCol& c = k.c[i];
+        uint64_t mn = ~0ull, mx = 0, nul = 0;
+        for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += (int64_t)gridDim.x * blockDim.x) {
+            const int64_t r = n <= samples ? j : (j >> 4) * cstep + (j & 15);
+            if (r >= n) continue;
+            if (!dev_valid(c, r)) {
+                nul = 1;
+                continue;
+            }
+            const uint64_t o = dev_load(c, r) ^ 0x8000000000000000ull;
+            mn = o < mn ? o : mn;
+            mx = o > mx ? o : mx;
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const uint64_t a = __shfl_xor(mn, off, 64), b = __shfl_xor(mx, off, 64);
+            mn = a < mn ? a : mn;
+            mx = b > mx ? b : mx;
+            nul |= __shfl_xor(nul, off, 64);
+        }
+        if ((threadIdx.x & 63) == 0) {
+            if (mn != ~0ull) atomicMin(&stats[3 * i], (unsigned long long)mn);
+            if (mx != 0) atomicMax(&stats[3 * i + 1], (unsigned long long)mx);
+            if (nul) atomicOr(&stats[3 * i + 2], 1ull);
+        }
+    }
+}
+
 // Packed Int64 code per row; `valid_words` (optional): one bit per row, 0
 // when the tuple holds a null and nulls are not values (join without
-// nulls_equal).
+// nulls_equal).  `outside` (optional, a plan from sampled ranges): set when
+// some row's field does not fit its bits (the code would be wrong; the
+// caller repacks with exact ranges).
 __global__ __launch_bounds__(256) void mk_pack_kernel(MkKeys k, MkPack pk, int64_t n, uint64_t* __restrict__ out,
-                                                      uint64_t* __restrict__ valid_words) {
+                                                      uint64_t* __restrict__ valid_words,
+                                                      unsigned int* __restrict__ outside = nullptr) {
+    bool bad = false;
     for (int64_t r0 = (int64_t)blockIdx.x * blockDim.x; r0 < n; r0 += (int64_t)gridDim.x * blockDim.x) {
         const int64_t r = r0 + threadIdx.x;
         const bool in = r < n;
@@ -172,7 +212,9 @@ __global__ __launch_bounds__(256) void mk_pack_kernel(MkKeys k, MkPack pk, int64
                 else {
                     f = 0;
                     anynull = true;
+                    bad |= !pk.nullable[i];
                 }
+                if (outside) bad |= pk.bits[i] < 64 && (f >> pk.bits[i]) != 0;
                 code |= f << pk.shift[i];
             }
             out[r] = code;
@@ -182,6 +224,7 @@ __global__ __launch_bounds__(256) void mk_pack_kernel(MkKeys k, MkPack pk, int64
             if ((threadIdx.x & 63) == 0 && r - (threadIdx.x & 63) < n) valid_words[(r - (threadIdx.x & 63)) >> 6] = b;
         }
     }
+    if (outside && __any(bad) && (threadIdx.x & 63) == 0) atomicOr(outside, 1u);
 }
 
 // Packed codes -> key column i (dtype of the input key; validity zeroed
@@ -228,6 +271,61 @@ inline void mk_plan_from_ranges(const uint64_t* h, int n, MkPack* pk) {
         if (shift > 63) return;
     }
     pk->ok = 1;
+}
+
+// Packing plan from sampled ranges, widened by each key's sampled span (and
+// a null code reserved for every key), so that values the sample missed
+// near its ends still fit; mk_pack_kernel's `outside` flag catches the rest
+// and the caller repacks with the exact ranges.  pk->ok = 0 when a key is not
+// packable or the widened fields need > 63 bits.
+inline int mk_plan_pack_sampled(const MkKeys& ka, int64_t na, MkPack* pk, hipStream_t s) {
+    std::memset(pk, 0, sizeof *pk);
+    pk->n = ka.n;
+    for (int i = 0; i < ka.n; ++i)
+        if (dtype_is_float(ka.c[i].dtype) || ka.c[i].dtype == PLGPU_U64 || ka.c[i].dtype == PLGPU_STR)
+            return PLGPU_OK;
+    if (options().no_pack) return PLGPU_OK;
+    unsigned long long* st = nullptr;
+    const size_t bytes = 3 * kMaxKeys * 8;
+    int rc = dev_alloc((void**)&st, bytes, s);
+    if (rc) return rc;
+    unsigned long long h[3 * kMaxKeys];
+    for (int j = 0; j < kMaxKeys; ++j) h[3 * j] = ~0ull, h[3 * j + 1] = 0, h[3 * j + 2] = 0;
+    hipError_t e = hipMemcpyAsync(st, h, bytes, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && na > 0) {
+        mk_sample_range_kernel<<<16, 256, 0, s>>>(ka, na, 65536, st);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(h, st, bytes, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    dev_free(st, s);
+    if (e != hipSuccess) return hip_fail(e, "sampled key range pass");
+    uint64_t r[3 * kMaxKeys];
+    for (int i = 0; i < ka.n; ++i) {
+        uint64_t mn = h[3 * i], mx = h[3 * i + 1];
+        if (mn > mx) mn = mx = 0x8000000000000000ull;
+        const uint64_t span = (mx - mn) + 1024;
+        mn = mn > span ? mn - span : 0;
+        mx = mx < ~0ull - span ? mx + span : ~0ull;
+        // the dtype's own range bounds the widened one
+        const int b = dtype_bytes(ka.c[i].dtype) * 8;
+        if (ka.c[i].dtype == PLGPU_BOOL) {
+            mn = 0x8000000000000000ull;
+            mx = mn + 1;
+        } else if (b > 0 && b < 64) {
+            const bool uns = ka.c[i].dtype == PLGPU_U8 || ka.c[i].dtype == PLGPU_U16 || ka.c[i].dtype == PLGPU_U32;
+            const int64_t lo = uns ? 0 : -(int64_t(1) << (b - 1));
+            const int64_t hi = uns ? (int64_t(1) << b) - 1 : (int64_t(1) << (b - 1)) - 1;
+            const uint64_t olo = (uint64_t)lo ^ 0x8000000000000000ull, ohi = (uint64_t)hi ^ 0x8000000000000000ull;
+            mn = mn < olo ? olo : mn;
+            mx = mx > ohi ? ohi : mx;
+        }
+        r[3 * i] = mn;
+        r[3 * i + 1] = mx;
+        r[3 * i + 2] = 1;
+    }
+    mk_plan_from_ranges(r, ka.n, pk);
+    return PLGPU_OK;
 }
 
 // Range pass over `ka` (and `kb`, the other join side, when non-null) and the

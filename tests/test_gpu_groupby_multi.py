@@ -226,3 +226,26 @@ def test_packed_key_ranges_extremes(gpu):
             "bk": (b, rng.random(n) > 0.3)}, cols, [("sum", "a"), ("len", "b")], True)
     wide = rng.choice(np.array([np.iinfo(np.int64).min, np.iinfo(np.int64).max, 0]), n)
     _check({"w1": (wide, None), "w2": (wide[::-1].copy(), None)}, cols, [("sum", "d"), ("len", "a")], False)
+
+
+@pytest.mark.parametrize("case", ["in_sample_range", "outlier_row", "null_in_unsampled_row", "narrow_dtypes"])
+def test_sampled_packing_plan(gpu, case):
+    """Above 2^20 rows the packing plan comes from a sample of the key
+    columns (widened by the sampled span, a null code reserved per key); a
+    row outside it (an outlier the sample missed) sends the group-by to the
+    exact range pass and a repack, with the same result."""
+    rng = np.random.default_rng(len(case))
+    n = 1_500_003
+    k1 = rng.integers(0, 1000, n).astype(np.int64) * 3 - 500
+    k2 = rng.integers(0, 50, n).astype(np.int32)
+    v1 = None
+    if case == "outlier_row":
+        k1[n // 2 + 7] = 1 << 40  # far outside any widened sampled range
+    if case == "null_in_unsampled_row":
+        v1 = np.ones(n, bool)
+        v1[n // 2 + 7] = False
+    if case == "narrow_dtypes":
+        k1 = (k1 % 120).astype(np.int8)
+        k2 = k2.astype(np.uint16)
+    cols = _rand_frame(rng, n)
+    _check({"k1": (k1, v1), "k2": (k2, None)}, cols, [("sum", "a"), ("len", "b"), ("max", "d")], False)
