@@ -3574,7 +3574,7 @@ PLGPU_API int plgpu_key_pack(const plgpu_column* keys, int32_t nkeys, const int6
     if (rc) return rc;
     if (n > 0) {
         const int g = (int)std::min<int64_t>((n + 255) / 256, (int64_t)num_cus() * 16);
-        mk_pack_kernel<<<g, 256, 0, s>>>(mk, pk, n, (uint64_t*)out_codes->values, nullptr);
+        mk_pack_launch(mk, pk, n, (uint64_t*)out_codes->values, nullptr, nullptr, g, s);
         hipError_t e = hipGetLastError();
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (e != hipSuccess) {
@@ -3813,7 +3813,7 @@ static int gb_multi_packed(const MkKeys& mk, MkPack pk, int64_t n, const plgpu_c
         if (outside) e = hipMemsetAsync(outside, 0, 4, s);
         const int g = (int)std::min<int64_t>((n + 255) / 256, (int64_t)num_cus() * 16);
         if (e == hipSuccess) {
-            mk_pack_kernel<<<g, 256, 0, s>>>(mk, pk, n, codes, nullptr, outside);
+            mk_pack_launch(mk, pk, n, codes, nullptr, outside, g, s);
             e = hipGetLastError();
         }
         unsigned int bad = 0;

@@ -1618,12 +1618,12 @@ PLGPU_API int plgpu_join_multi(const plgpu_column* left_keys, const plgpu_column
             if (!rc) rc = dev_alloc((void**)&cr, (std::max<int64_t>(nr, 1) + (nr + 63) / 64 + 1) * 8, s);
             uint64_t* vl = cl ? cl + std::max<int64_t>(nl, 1) : nullptr;
             uint64_t* vr = cr ? cr + std::max<int64_t>(nr, 1) : nullptr;
-            if (!rc && nl > 0)
-                mk_pack_kernel<<<(unsigned)std::min<int64_t>((nl + 255) / 256, cus * 16), 256, 0, s>>>(
-                    ka, pk, nl, cl, neq ? nullptr : vl);
-            if (!rc && nr > 0)
-                mk_pack_kernel<<<(unsigned)std::min<int64_t>((nr + 255) / 256, cus * 16), 256, 0, s>>>(
-                    kb, pk, nr, cr, neq ? nullptr : vr);
+            if (!rc)
+                mk_pack_launch(ka, pk, nl, cl, neq ? nullptr : vl, nullptr,
+                               (int)std::min<int64_t>((nl + 255) / 256, cus * 16), s);
+            if (!rc)
+                mk_pack_launch(kb, pk, nr, cr, neq ? nullptr : vr, nullptr,
+                               (int)std::min<int64_t>((nr + 255) / 256, cus * 16), s);
             if (!rc) {
                 hipError_t e = hipGetLastError();
                 if (e != hipSuccess) rc = hip_fail(e, "mk_pack_kernel");
@@ -1887,12 +1887,12 @@ PLGPU_API int plgpu_join_inner_take_multi(const plgpu_column* left_keys, const p
         if (!rc) rc = dev_alloc((void**)&cr, (std::max<int64_t>(nr, 1) + (nr + 63) / 64 + 1) * 8, s);
         uint64_t* vl = cl ? cl + std::max<int64_t>(nl, 1) : nullptr;
         uint64_t* vr = cr ? cr + std::max<int64_t>(nr, 1) : nullptr;
-        if (!rc && nl > 0)
-            mk_pack_kernel<<<(unsigned)std::min<int64_t>((nl + 255) / 256, cus * 16), 256, 0, s>>>(
-                ka, pk, nl, cl, neq ? nullptr : vl);
-        if (!rc && nr > 0)
-            mk_pack_kernel<<<(unsigned)std::min<int64_t>((nr + 255) / 256, cus * 16), 256, 0, s>>>(
-                kb, pk, nr, cr, neq ? nullptr : vr);
+        if (!rc)
+            mk_pack_launch(ka, pk, nl, cl, neq ? nullptr : vl, nullptr,
+                           (int)std::min<int64_t>((nl + 255) / 256, cus * 16), s);
+        if (!rc)
+            mk_pack_launch(kb, pk, nr, cr, neq ? nullptr : vr, nullptr,
+                           (int)std::min<int64_t>((nr + 255) / 256, cus * 16), s);
         if (!rc) {
             const hipError_t e = hipGetLastError();
             if (e != hipSuccess) rc = hip_fail(e, "mk_pack_kernel");

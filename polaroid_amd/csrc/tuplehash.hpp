@@ -227,6 +227,89 @@ __global__ __launch_bounds__(256) void mk_pack_kernel(MkKeys k, MkPack pk, int64
     if (outside && __any(bad) && (threadIdx.x & 63) == 0) atomicOr(outside, 1u);
 }
 
+// Two consecutive rows (r, r + 1) of a null-free 4- or 8-byte integer key
+// column: one 16-byte (8-byte) load when both are in range and the pair is
+// aligned, register-form loads otherwise.
+__device__ __forceinline__ void mk_load_pair(const DevCol& c, int64_t r, int64_t n, uint64_t& a, uint64_t& b) {
+    const int64_t p = c.offset + r;
+    if (r + 1 < n && (p & 1) == 0) {
+        if (c.dtype == PLGPU_I64) {
+            const ulonglong2 v = *reinterpret_cast<const ulonglong2*>((const uint64_t*)c.values + p);
+            a = v.x;
+            b = v.y;
+            return;
+        }
+        const uint2 v = *reinterpret_cast<const uint2*>((const uint32_t*)c.values + p);
+        a = c.dtype == PLGPU_U32 ? (uint64_t)v.x : (uint64_t)(int64_t)(int32_t)v.x;
+        b = c.dtype == PLGPU_U32 ? (uint64_t)v.y : (uint64_t)(int64_t)(int32_t)v.y;
+        return;
+    }
+    a = r < n ? dev_load(c, r) : 0ull;
+    b = r + 1 < n ? dev_load(c, r + 1) : 0ull;
+}
+
+// mk_pack_kernel for null-free I64 / I32 / U32 keys and no validity output:
+// each thread packs U pairs of consecutive rows per step, every key column
+// read with pair loads and the codes stored as 16-byte pairs.
+template <int U>
+__global__ __launch_bounds__(256) void mk_pack_vec_kernel(MkKeys k, MkPack pk, int64_t n, uint64_t* __restrict__ out,
+                                                          unsigned int* __restrict__ outside) {
+    const int64_t T = (int64_t)gridDim.x * blockDim.x;
+    bool bad = false;
+    for (int64_t base = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 2; base < n; base += T * 2 * U) {
+        uint64_t code[U][2];
+#pragma unroll
+        for (int u = 0; u < U; ++u) code[u][0] = code[u][1] = 0;
+#pragma unroll
+        for (int i = 0; i < kMaxKeys; ++i) {
+            if (i >= k.n) break;
+            uint64_t v[U][2];
+#pragma unroll
+            for (int u = 0; u < U; ++u) mk_load_pair(k.c[i], base + (int64_t)u * T * 2, n, v[u][0], v[u][1]);
+            const uint64_t noff = pk.nullable[i] ? 1u : 0u;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    const uint64_t f = (uint64_t)((int64_t)v[u][e] - pk.minv[i]) + noff;
+                    if (outside) bad |= base + (int64_t)u * T * 2 + e < n && pk.bits[i] < 64 && (f >> pk.bits[i]) != 0;
+                    code[u][e] |= f << pk.shift[i];
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t r = base + (int64_t)u * T * 2;
+            if (r + 1 < n) {
+                *reinterpret_cast<ulonglong2*>(out + r) = make_ulonglong2(code[u][0], code[u][1]);
+            } else if (r < n) {
+                out[r] = code[u][0];
+            }
+        }
+    }
+    if (outside && __any(bad) && (threadIdx.x & 63) == 0) atomicOr(outside, 1u);
+}
+
+// Launch the packing pass: the vector form when it applies.
+inline void mk_pack_launch(const MkKeys& k, const MkPack& pk, int64_t n, uint64_t* out, uint64_t* valid_words,
+                           unsigned int* outside, int grid, hipStream_t s) {
+    if (n <= 0) return;
+    bool vec = ((uintptr_t)out & 15) == 0;
+    for (int i = 0; i < k.n; ++i)
+        vec = vec && k.c[i].validity == nullptr &&
+              (k.c[i].dtype == PLGPU_I64 || k.c[i].dtype == PLGPU_I32 || k.c[i].dtype == PLGPU_U32) &&
+              ((uintptr_t)k.c[i].values & 15) == 0;
+    if (vec) {
+        // null-free keys: every tuple is valid
+        if (valid_words) (void)hipMemsetAsync(valid_words, 0xFF, (size_t)((n + 63) / 64) * 8, s);
+        const int64_t pairs = (n + 1) / 2;
+        const int g = (int)std::max<int64_t>(1, std::min<int64_t>((pairs + 255) / 256, (int64_t)grid));
+        mk_pack_vec_kernel<2><<<g, 256, 0, s>>>(k, pk, n, out, outside);
+    } else {
+        mk_pack_kernel<<<grid, 256, 0, s>>>(k, pk, n, out, valid_words, outside);
+    }
+}
+
 // Packed codes -> key column i (dtype of the input key; validity zeroed
 // beforehand; Boolean values bit-packed, zeroed beforehand).
 __global__ __launch_bounds__(256) void mk_unpack_kernel(const int64_t* __restrict__ codes, const uint32_t* code_valid,
