@@ -4306,9 +4306,13 @@ PLGPU_API int plgpu_group_sq_dev(const plgpu_column* row_key, const plgpu_column
     const size_t slots = (size_t)1 << bits;
     uint64_t* tkey = nullptr;
     uint32_t* tidx = nullptr;
-    hipError_t e = hipMallocAsync((void**)&tkey, slots * 16, s);
-    if (e == hipSuccess) e = hipMallocAsync((void**)&tidx, slots * 4 + 12, s);
-    if (e == hipSuccess) e = hipMemsetAsync(tidx, 0xFF, slots * 4 + 12, s);
+    // the library's stream-ordered cache, like every other scratch buffer
+    if ((rc = dev_alloc((void**)&tkey, slots * 16, s)) || (rc = dev_alloc((void**)&tidx, slots * 4 + 12, s))) {
+        dev_free(tkey, s);
+        plgpu_column_release(out);
+        return rc;
+    }
+    hipError_t e = hipMemsetAsync(tidx, 0xFF, slots * 4 + 12, s);
     uint64_t* tval = tkey + slots;
     uint32_t* null_g = tidx + slots;
     if (e == hipSuccess && ng > 0)
@@ -4328,8 +4332,8 @@ PLGPU_API int plgpu_group_sq_dev(const plgpu_column* row_key, const plgpu_column
         }
         e = hipGetLastError();
     }
-    if (tkey) (void)hipFreeAsync(tkey, s);
-    if (tidx) (void)hipFreeAsync(tidx, s);
+    dev_free(tkey, s);
+    dev_free(tidx, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) {
         plgpu_column_release(out);
