@@ -51,6 +51,7 @@ def parse():
     ap.add_argument("--plugin-rows", type=float, default=1e8,
                     help="rows of the plugin leg (host Arrow frame through execute_with_polaroid; configs[1] = 1e8)")
     ap.add_argument("--no-plugin", action="store_true")
+    ap.add_argument("--no-vwap", action="store_true")
     ap.add_argument("--dry-run", action="store_true",
                     help="print this rank's launch parameters and exit before touching the GPU (tests)")
     return ap.parse_args()
@@ -169,6 +170,45 @@ def plugin_leg(rows: int, groups: int) -> dict:
             "cold_Mrows_s": round(rows / cold / 1e3, 1), "warm_Mrows_s": round(rows / warm / 1e3, 1),
             "note": "execute_with_polaroid on a host Arrow frame of 8M-row RecordBatches; cold = scan over the "
                     "host link + query, warm = scanned columns resident (ColumnCache); result to Arrow"}
+
+
+def vwap_leg(torch, pl, df, sym, close, steps: int, warmup: int) -> dict:
+    """VWAP over the same resident frame: filter(close > 250).group_by(symbol)
+    .agg((close * volume).sum(), volume.sum()); the product is computed in the
+    fused kernel's registers (DESIGN.md "Aggregations over expressions"), so the
+    algorithmic bytes are key + close + volume = 24 B/row.  rank 0, N = 1."""
+    n = sym.numel()
+    g = torch.Generator(device=sym.device)
+    g.manual_seed(99)
+    vol = torch.empty(n, dtype=torch.float64, device=sym.device)
+    chunk = 1 << 26
+    for s in range(0, n, chunk):
+        e = min(n, s + chunk)
+        vol[s:e] = torch.floor(torch.rand(e - s, device=sym.device, generator=g, dtype=torch.float64) * 1000.0) + 1.0
+    vdf = pl.DataFrame([pl.Series.from_torch("symbol", sym), pl.Series.from_torch("close", close),
+                        pl.Series.from_torch("volume", vol)])
+    q = vdf.lazy().filter(pl.col("close") > THRESHOLD).group_by("symbol").agg(
+        (pl.col("close") * pl.col("volume")).sum().alias("pv"), pl.col("volume").sum().alias("v"))
+    for _ in range(warmup):
+        q.collect()
+    torch.cuda.synchronize()
+    kms = []
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        info = {}
+        out = q.collect(info=info)
+        kms.append(info.get("main_kernel_ms", float("nan")))
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    k = float(np.mean(kms))
+    achieved = 24 * n / (k * 1e-3) / 1e9
+    assert 0 < out.height <= n
+    del vdf, vol
+    return {"query": "filter(close > 250).group_by(symbol).agg((close * volume).sum(), volume.sum())",
+            "rows": n, "ms_per_step": round(dt * 1e3, 3), "Mrows_s": round(n / dt / 1e6, 1),
+            "kernel": "gb_fast_kernel<NACC=2,PRED=1,SUMONLY,DERIV> (close * volume in registers)",
+            "kernel_ms": round(k, 4), "bytes_per_row": 24, "achieved_GBs": round(achieved, 1),
+            "frac": round(achieved / HBM_PEAK_GBS, 4)}
 
 
 def load_traffic(n_rows: int):
@@ -321,6 +361,8 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(int(args.cpu_rows), args.groups, args.cpu_seconds)
+    if rank == 0 and world == 1 and not args.no_vwap:
+        result["vwap"] = vwap_leg(torch, pl, df, sym, cols["close"], args.steps, args.warmup)
     if rank == 0 and world == 1 and not args.no_plugin:
         del df, query, out, sym, cols
         torch.cuda.empty_cache()

@@ -89,7 +89,7 @@ class GroupByInfo(C.Structure):
         ("path", C.c_int32),
         ("sum_limbs", C.c_int32),
         ("local_range", C.c_int32),
-        ("_pad", C.c_int32),
+        ("register_runs", C.c_int32),
     ]
 
     def as_dict(self) -> dict:

@@ -100,6 +100,8 @@ struct AccSpec {
     int32_t dop;      // DOP_*: derived input (0: the column itself)
     DevCol c2;        // derived: the second operand column (unless DOP_LIT)
     uint64_t dimm;    // derived: the literal operand's f64 bits (DOP_LIT)
+    int32_t v_from;   // fused kernel (DERIV): c is acc v_from's column too (-1: own load)
+    int32_t w_from;   // fused kernel (DERIV): c2 is acc w_from's column (-1: own load)
 };
 
 struct GbParams {
@@ -947,8 +949,9 @@ __device__ __forceinline__ void fast_load_tail(const GbParams& p, int64_t t, Fas
         x.key[j] = in && p.key.values ? kp[r] : 0ull;
 #pragma unroll
         for (int c = 0; c < NACC; ++c) {
-            x.v[c][j] = in ? ((const uint64_t*)p.acc[c].c.values + p.acc[c].c.offset)[r] : 0ull;
-            if (DERIV && p.acc[c].dop != DOP_NONE && !(p.acc[c].dop & DOP_LIT))
+            if (!DERIV || p.acc[c].v_from < 0)
+                x.v[c][j] = in ? ((const uint64_t*)p.acc[c].c.values + p.acc[c].c.offset)[r] : 0ull;
+            if (DERIV && p.acc[c].dop != DOP_NONE && !(p.acc[c].dop & DOP_LIT) && p.acc[c].w_from < 0)
                 x.w[c][j] = in ? ((const uint64_t*)p.acc[c].c2.values + p.acc[c].c2.offset)[r] : 0ull;
         }
         if (PRED == 1 && p.pred_acc < 0) x.pv[j] = in ? ((const uint64_t*)p.pred_col.values + p.pred_col.offset)[r] : 0ull;
@@ -975,11 +978,13 @@ __device__ __forceinline__ void fast_load(const GbParams& p, int64_t t, FastTile
         }
 #pragma unroll
         for (int c = 0; c < NACC; ++c) {
-            const uint64_t* vp = (const uint64_t*)p.acc[c].c.values + p.acc[c].c.offset;
-            const u64x2_t b = ld16<NT>(vp + r);
-            x.v[c][2 * q] = b.x;
-            x.v[c][2 * q + 1] = b.y;
-            if (DERIV && p.acc[c].dop != DOP_NONE && !(p.acc[c].dop & DOP_LIT)) {
+            if (!DERIV || p.acc[c].v_from < 0) {
+                const uint64_t* vp = (const uint64_t*)p.acc[c].c.values + p.acc[c].c.offset;
+                const u64x2_t b = ld16<NT>(vp + r);
+                x.v[c][2 * q] = b.x;
+                x.v[c][2 * q + 1] = b.y;
+            }
+            if (DERIV && p.acc[c].dop != DOP_NONE && !(p.acc[c].dop & DOP_LIT) && p.acc[c].w_from < 0) {
                 const uint64_t* wp = (const uint64_t*)p.acc[c].c2.values + p.acc[c].c2.offset;
                 const u64x2_t w = ld16<NT>(wp + r);
                 x.w[c][2 * q] = w.x;
@@ -993,6 +998,25 @@ __device__ __forceinline__ void fast_load(const GbParams& p, int64_t t, FastTile
             x.pv[2 * q + 1] = b.y;
         }
     }
+}
+
+// DERIV: fill the operand registers whose column another acc loaded
+// (v_from / w_from, uniform), once the tile's loads are being consumed --
+// not at prefetch time, where the copy would wait for the loads.
+template <int NACC, int ROWS, bool DERIV>
+__device__ __forceinline__ void fast_share(const int32_t (&vf)[NACC > 0 ? NACC : 1],
+                                           const int32_t (&wf)[NACC > 0 ? NACC : 1],
+                                           FastTile<NACC, ROWS, DERIV>& x) {
+    if (!DERIV) return;
+#pragma unroll
+    for (int c = 0; c < NACC; ++c)
+#pragma unroll
+        for (int b = 0; b < NACC; ++b)
+#pragma unroll
+            for (int j = 0; j < ROWS; ++j) {
+                if (b == vf[c]) x.v[c][j] = x.v[b][j];
+                if (b == wf[c]) x.w[c][j] = x.v[b][j];
+            }
 }
 
 // SUMONLY: every acc is an f64 sum / mean (flags A_FSUM|A_FLAGS, no count /
@@ -1043,12 +1067,14 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
     uint64_t dd0[NA];
     int bot0[NA];
     load_descs(p, dd0, bot0);
-    int32_t dop0[NA];
+    int32_t dop0[NA], vf0[NA], wf0[NA];
     uint64_t dim0[NA];
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
         dop0[a] = DERIV && a < NACC ? p.acc[a].dop : DOP_NONE;
         dim0[a] = DERIV && a < NACC ? p.acc[a].dimm : 0ull;
+        vf0[a] = DERIV && a < NACC ? p.acc[a].v_from : -1;
+        wf0[a] = DERIV && a < NACC ? p.acc[a].w_from : -1;
     }
     __syncthreads();
 
@@ -1113,9 +1139,95 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
         }
         rs[k] = -1;
     };
+    // GRUNS (RUNS without SUMONLY: min / max / count / first / last next to
+    // the sums): one register run per lane holding every acc's state for the
+    // group of slot gs -- len, first / last row, the 3-limb sum, min / max
+    // as ordered bits, the integer sum -- folded into LDS when the lane
+    // meets another group.  A row that is not fully in-window (inf / NaN,
+    // bits outside the sum window) takes apply_row as before.
+    constexpr bool GRUNS = RUNS && !SUMONLY;
+    constexpr int NG = GRUNS ? NA : 1;
+    int gs = -1;
+    uint64_t gn = 0, gfirst = 0, glast = 0;
+    uint64_t gl0[NG], gl1[NG], gl2[NG], gmin[NG], gmax[NG], gis[NG];
+    auto grun_flush = [&]() {
+        if (!GRUNS || gs < 0) return;
+        unsigned long long* q = (unsigned long long*)&lds[gs];
+        atomicAdd(q + p.f_len * L, (unsigned long long)gn);
+        if (p.f_first >= 0) atomicMin(q + p.f_first * L, (unsigned long long)gfirst);
+        if (p.f_last >= 0) atomicMax(q + p.f_last * L, (unsigned long long)glast);
+#pragma unroll
+        for (int a = 0; a < NG && a < NACC; ++a) {
+            const uint64_t dsc = dd0[a];
+            const uint32_t flags = (uint32_t)dsc & 0xFF;
+            const int f_cnt = dfield(dsc, 24);
+            if (f_cnt != kNoField) atomicAdd(q + f_cnt * L, (unsigned long long)gn);
+            const bool isf = (dsc >> 56) & 1;
+            if ((isf && (flags & A_FSUM)) || (!isf && (flags & A_FSUMCAST))) {
+                const int f = dfield(dsc, 8);
+                if (gl0[a]) atomicAdd(q + f * L, (unsigned long long)gl0[a]);
+                if (gl1[a]) atomicAdd(q + (f + 1) * L, (unsigned long long)gl1[a]);
+                if (gl2[a]) atomicAdd(q + (f + 2) * L, (unsigned long long)gl2[a]);
+            }
+            if (flags & A_MIN) atomicMin(q + dfield(dsc, 32) * L, (unsigned long long)gmin[a]);
+            if (flags & A_MAX) atomicMax(q + dfield(dsc, 40) * L, (unsigned long long)gmax[a]);
+            if (flags & A_ISUM) atomicAdd(q + dfield(dsc, 16) * L, (unsigned long long)gis[a]);
+        }
+        gs = -1;
+    };
+    auto grun_take = [&](int sl, int64_t r, const uint64_t (&x)[NA]) -> bool {
+        if (!GRUNS) return false;
+        uint64_t l0[NG], l1[NG], l2[NG], o[NG];
+        bool ok = true;
+#pragma unroll
+        for (int a = 0; a < NG && a < NACC; ++a) {
+            const uint64_t dsc = dd0[a];
+            const uint32_t flags = (uint32_t)dsc & 0xFF;
+            const bool isf = (dsc >> 56) & 1;
+            const bool uns = (dsc >> 57) & 1;
+            uint64_t sb = x[a];
+            bool fs = false;
+            if (isf) {
+                ok = ok && (x[a] & 0x7fffffffffffffffull) < 0x7ff0000000000000ull;
+                fs = (flags & A_FSUM) != 0;
+            } else if (flags & A_FSUMCAST) {
+                sb = f64_bits(uns ? (double)x[a] : (double)(int64_t)x[a]);
+                fs = true;
+            }
+            l0[a] = l1[a] = l2[a] = 0;
+            if (fs) ok = fx_limbs_fast<3>(sb, bot0[a], l0[a], l1[a], l2[a]) && ok;
+            o[a] = isf ? ord_f64(x[a]) : (uns ? x[a] : ord_i64(x[a]));
+        }
+        if (!ok) return false;
+        if (gs != sl) {
+            grun_flush();
+            gs = sl;
+            gn = 0;
+            gfirst = glast = (uint64_t)r;
+#pragma unroll
+            for (int a = 0; a < NG; ++a) {
+                gl0[a] = gl1[a] = gl2[a] = gis[a] = gmax[a] = 0;
+                gmin[a] = ~0ull;
+            }
+        }
+        ++gn;
+        gfirst = std::min<uint64_t>(gfirst, (uint64_t)r);
+        glast = std::max<uint64_t>(glast, (uint64_t)r);
+#pragma unroll
+        for (int a = 0; a < NG && a < NACC; ++a) {
+            gl0[a] += l0[a];
+            gl1[a] += l1[a];
+            gl2[a] += l2[a];
+            gmin[a] = std::min(gmin[a], o[a]);
+            gmax[a] = std::max(gmax[a], o[a]);
+            gis[a] += x[a];
+        }
+        return true;
+    };
     FastTile<NACC, ROWS, DERIV> cur;
     if (t < nall) load_tile(t, cur);
     for (; t < nall; t += tstep) {
+        fast_share<NACC, ROWS, DERIV>(vf0, wf0, cur);
         // ---- predicate + batched LDS probes of the tile's rows
         int slot[ROWS];
         uint64_t probe[ROWS];
@@ -1258,7 +1370,7 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
                         }
                     }
                 } else if (s >= 0) {
-                    apply_row<true, NA>(p, lds, L, s, r, rv, VM, dd, bot, NACC, d);
+                    if (!grun_take(s, r, rv)) apply_row<true, NA>(p, lds, L, s, r, rv, VM, dd, bot, NACC, d);
                 } else {
                     ++d.nglobal;
                     global_row<NA>(p, cur.key[0], true, r, rv, VM, dd, bot, NACC, d);
@@ -1313,6 +1425,7 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
         }
         flush_and_report<false>(p, lds, L, d);
     } else {
+        grun_flush();
         flush_and_report<true>(p, lds, L, d);
     }
 }
@@ -1927,6 +2040,7 @@ struct Plan {
     bool runs;         // sampled keys mostly equal their next row's (sorted / clustered input)
     bool local;        // range-local mode: contiguous tiles per workgroup, LDS sized by range-local keys
     mutable int launched_grid;  // grid of the last fast launch (info)
+    mutable bool launched_runs = false;  // that launch used the register-run variant (info)
 };
 
 // One aggregation input (plan_groupby): a column, or a derived value x op y
@@ -2012,6 +2126,20 @@ static int plan_groupby(const plgpu_column* key, const plgpu_column* cols, int32
         default: return fail(PLGPU_ERR_INVALID, "unknown aggregation kind");
         }
         pl->acc_of_agg[i] = acc_of_col[c];
+    }
+    // operand columns shared between accs ((close * volume).sum() next to
+    // volume.sum()) are loaded once by the fused kernel
+    auto same_col = [](const DevCol& x, const DevCol& y) {
+        return x.values == y.values && x.offset == y.offset && x.dtype == y.dtype;
+    };
+    for (int a = 0; a < p.nacc; ++a) {
+        AccSpec& ac = p.acc[a];
+        ac.v_from = ac.w_from = -1;
+        for (int b = 0; b < a && ac.v_from < 0; ++b)
+            if (same_col(p.acc[b].c, ac.c)) ac.v_from = b;
+        if (ac.dop != DOP_NONE && !(ac.dop & DOP_LIT))
+            for (int b = 0; b < p.nacc && ac.w_from < 0; ++b)
+                if (same_col(p.acc[b].c, ac.c2) && p.acc[b].v_from < 0 && b != a) ac.w_from = b;
     }
     for (int a = 0; a < p.nacc; ++a) {
         AccSpec& ac = p.acc[a];
@@ -2174,6 +2302,7 @@ static hipError_t launch_fast_rows(const Plan& pl, const DevProgram& dp, hipStre
     if (g > useful) g = std::max<int64_t>(1, useful);
     const int grid = (int)g;
     pl.launched_grid = grid;
+    pl.launched_runs = RUNS;
     GbParams q = pl.p;
     q.tiles_per_wg = 0;
     if (pl.local) {
@@ -2189,6 +2318,7 @@ template <int NACC, int PRED, bool SUMONLY, bool DERIV>
 static hipError_t launch_fast(const Plan& pl, const DevProgram& dp, hipStream_t s) {
     if (SUMONLY && pl.limbs == 2 && pl.runs) return launch_fast_rows<NACC, PRED, SUMONLY, 2, true, DERIV>(pl, dp, s);
     if (SUMONLY && pl.limbs == 2) return launch_fast_rows<NACC, PRED, SUMONLY, 2, false, DERIV>(pl, dp, s);
+    if (!SUMONLY && NACC > 0 && !DERIV && pl.runs) return launch_fast_rows<NACC, PRED, false, 3, true, false>(pl, dp, s);
     return launch_fast_rows<NACC, PRED, SUMONLY, 3, false, DERIV>(pl, dp, s);
 }
 
@@ -3013,6 +3143,7 @@ static void gb_fill_info(const GbRun& R, plgpu_groupby_info* info) {
     info->path = R.part ? 3 : (p.n_full > 0 ? (R.pl.sum_only ? 2 : 1) : 0);
     info->sum_limbs = (p.n_full > 0 || R.part) && R.pl.sum_only ? R.pl.limbs : 3;
     info->local_range = R.pl.local ? 1 : 0;
+    info->register_runs = p.n_full > 0 && !R.part && R.pl.launched_runs ? 1 : 0;
     for (int a = 0; a < p.nacc; ++a)
         if (((R.st[ST_FXFLAGS] >> (2 * a)) & 2u) && !((R.wide >> a) & 1u)) info->sum_inexact |= 1 << a;
 }

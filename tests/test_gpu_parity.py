@@ -589,6 +589,41 @@ def test_group_by_register_accumulators(gpu, layout, plgpu_option):
         assert info["path"] == 3, info
 
 
+@pytest.mark.parametrize("layout", ["sorted", "runs_forced_random", "sorted_specials", "sorted_maintain_order",
+                                    "random_control"])
+def test_group_by_register_runs_mixed_aggs(gpu, layout, plgpu_option):
+    """Sorted keys with min / max / count / len / integer sums / first / last
+    next to the f64 sums: the fused kernel's lanes keep one register run per
+    group (every acc's state) and fold it into the LDS table on a group
+    change; rows with inf / NaN take the per-row path.  Exact vs the oracle."""
+    rng = np.random.default_rng(len(layout) + 901)
+    n = 2_000_003
+    a = rng.uniform(10, 500, n)
+    d = rng.standard_normal(n)
+    b = rng.integers(-10**12, 10**12, n).astype(np.int64)
+    c = rng.integers(-2**40, 2**40, n).astype(np.int64)  # the fused kernel takes 8-byte columns
+    if layout == "sorted_specials":
+        a[rng.random(n) < 0.001] = np.nan
+        a[rng.random(n) < 0.0005] = -np.inf
+        d[rng.random(n) < 0.001] = -0.0
+        d[rng.random(n) < 0.0002] = 1e-310  # subnormal: outside the fast conversion
+    key = rng.integers(0, 120, n).astype(np.int64) * 104729 - 7
+    if layout == "runs_forced_random":
+        plgpu_option("runs", 1)
+    elif layout != "random_control":
+        key = np.sort(key, kind="stable")
+    cols = {"a": (a, None), "b": (b, None), "c": (c, None), "d": (d, None)}
+    aggs = [("sum", "a"), ("min", "d"), ("max", "a"), ("count", "d"), ("len", "a"), ("sum", "b"),
+            ("min", "c"), ("max", "b"), ("mean", "d"), ("sum", "c")]
+    if layout == "sorted_maintain_order":
+        aggs += [("first", "d"), ("last", "a")]
+    info = {}
+    mk, names, prog = PREDICATES["simple_f64"]
+    _check_group_by(cols, key, None, aggs, mk(), prog, names, layout == "sorted_maintain_order", info)
+    assert info["path"] == 1, info
+    assert info["register_runs"] == (0 if layout == "random_control" else 1), info
+
+
 @pytest.mark.parametrize("layout", ["day_ordered", "symbol_sorted", "clustered_blocks", "random_control"])
 @pytest.mark.parametrize("aggs_kind", ["sums", "mixed"])
 def test_group_by_range_local_kernel(gpu, layout, aggs_kind):
