@@ -158,16 +158,20 @@ enum : uint32_t {
     CK_VERIFY_SLOT = 64,  // multi-key verify slot outside the table
     CK_PART_POS = 128,    // partition scatter position outside the buffers
     CK_KEY_ROW = 256,     // multi-key output key row outside [0, n)
-    CK_PERM = 512         // group-order permutation entry outside [0, groups)
+    CK_PERM = 512,        // group-order permutation entry outside [0, groups)
+    CK_FIELD = 1024       // apply_row: table field outside [0, nfields)
 };
 #ifdef PLGPU_CHECKS
 __device__ unsigned int g_gb_checks;
+__device__ unsigned long long g_gb_sink;  // target of a skipped field access
 __device__ __forceinline__ bool gb_ok(bool c, uint32_t bit) {
     if (!c) atomicOr(&g_gb_checks, bit);
     return c;
 }
+__device__ __forceinline__ unsigned long long* gb_sink() { return &g_gb_sink; }
 #else
 __device__ __forceinline__ constexpr bool gb_ok(bool, uint32_t) { return true; }
+__device__ __forceinline__ unsigned long long* gb_sink() { return nullptr; }
 #endif
 
 // ------------------------------------------------------------ helpers
@@ -357,6 +361,7 @@ __device__ __forceinline__ void apply_row(const GbParams& p, uint64_t* lds, int 
                                           uint64_t (&v)[NA], uint32_t vm, uint64_t (&dd)[NA], int (&bot)[NA],
                                           int nacc, ThreadDiag& diag) {
     auto F = [&](int f) -> unsigned long long* {
+        if (!gb_ok(f >= 0 && f < p.nfields, CK_FIELD)) return gb_sink();
         if (LDS) return (unsigned long long*)&lds[f * L + s];
         return (unsigned long long*)gfield(p, f, s);
     };
@@ -381,6 +386,10 @@ __device__ __forceinline__ void apply_row(const GbParams& p, uint64_t* lds, int 
                 if (ab >= 0x7ff0000000000000ull) {
                     const uint32_t fl = ab > 0x7ff0000000000000ull ? FL_NAN : ((x >> 63) ? FL_NINF : FL_PINF);
                     is_nan = fl == FL_NAN;
+                    // every f64 acc has a flags field (plan_groupby), also
+                    // one aggregated only by len / count / first / last: its
+                    // absence was round 2's out-of-table write (DESIGN.md
+                    // "GPU fault audit")
                     atomicOr(F(dfield(d, 48)), (unsigned long long)fl);
                 } else {
                     fsum_ok = (flags & A_FSUM) != 0;
@@ -1140,16 +1149,20 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
         rs[k] = -1;
     };
     // GRUNS (RUNS without SUMONLY: min / max / count / first / last next to
-    // the sums): one register run per lane holding every acc's state for the
-    // group of slot gs -- len, first / last row, the 3-limb sum, min / max
-    // as ordered bits, the integer sum -- folded into LDS when the lane
-    // meets another group.  A row that is not fully in-window (inf / NaN,
-    // bits outside the sum window) takes apply_row as before.
+    // the sums, sorted / clustered keys): one register run per lane holding
+    // the state of the group of LDS slot gs -- len, first / last row, per
+    // acc two registers r0 / r1 (an f64 sum's top two limbs of the window,
+    // LIMBS == 2; an integer sum in r0) and min / max as ordered bits --
+    // folded into the LDS table when the lane meets another group.  A value
+    // below the 2-limb window, inf / NaN flags and (rare) an integer column
+    // summed both as integers and as f64 go straight to the LDS fields.
+    // The plan picks this variant only when its sampled exponents fit the
+    // 2-limb window and no acc casts integers to f64 sums.
     constexpr bool GRUNS = RUNS && !SUMONLY;
     constexpr int NG = GRUNS ? NA : 1;
     int gs = -1;
     uint64_t gn = 0, gfirst = 0, glast = 0;
-    uint64_t gl0[NG], gl1[NG], gl2[NG], gmin[NG], gmax[NG], gis[NG];
+    uint64_t gr0[NG], gr1[NG], gmin[NG], gmax[NG];
     auto grun_flush = [&]() {
         if (!GRUNS || gs < 0) return;
         unsigned long long* q = (unsigned long long*)&lds[gs];
@@ -1163,42 +1176,21 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
             const int f_cnt = dfield(dsc, 24);
             if (f_cnt != kNoField) atomicAdd(q + f_cnt * L, (unsigned long long)gn);
             const bool isf = (dsc >> 56) & 1;
-            if ((isf && (flags & A_FSUM)) || (!isf && (flags & A_FSUMCAST))) {
+            if (isf && (flags & A_FSUM)) {
+                // the top two limbs: 3-limb fields (f + 1, f + 2), low limb 0
                 const int f = dfield(dsc, 8);
-                if (gl0[a]) atomicAdd(q + f * L, (unsigned long long)gl0[a]);
-                if (gl1[a]) atomicAdd(q + (f + 1) * L, (unsigned long long)gl1[a]);
-                if (gl2[a]) atomicAdd(q + (f + 2) * L, (unsigned long long)gl2[a]);
+                if (gr0[a]) atomicAdd(q + (f + 1) * L, (unsigned long long)gr0[a]);
+                if (gr1[a]) atomicAdd(q + (f + 2) * L, (unsigned long long)gr1[a]);
+            } else if (!isf && (flags & A_ISUM) && gr0[a]) {
+                atomicAdd(q + dfield(dsc, 16) * L, (unsigned long long)gr0[a]);
             }
             if (flags & A_MIN) atomicMin(q + dfield(dsc, 32) * L, (unsigned long long)gmin[a]);
             if (flags & A_MAX) atomicMax(q + dfield(dsc, 40) * L, (unsigned long long)gmax[a]);
-            if (flags & A_ISUM) atomicAdd(q + dfield(dsc, 16) * L, (unsigned long long)gis[a]);
         }
         gs = -1;
     };
     auto grun_take = [&](int sl, int64_t r, const uint64_t (&x)[NA]) -> bool {
         if (!GRUNS) return false;
-        uint64_t l0[NG], l1[NG], l2[NG], o[NG];
-        bool ok = true;
-#pragma unroll
-        for (int a = 0; a < NG && a < NACC; ++a) {
-            const uint64_t dsc = dd0[a];
-            const uint32_t flags = (uint32_t)dsc & 0xFF;
-            const bool isf = (dsc >> 56) & 1;
-            const bool uns = (dsc >> 57) & 1;
-            uint64_t sb = x[a];
-            bool fs = false;
-            if (isf) {
-                ok = ok && (x[a] & 0x7fffffffffffffffull) < 0x7ff0000000000000ull;
-                fs = (flags & A_FSUM) != 0;
-            } else if (flags & A_FSUMCAST) {
-                sb = f64_bits(uns ? (double)x[a] : (double)(int64_t)x[a]);
-                fs = true;
-            }
-            l0[a] = l1[a] = l2[a] = 0;
-            if (fs) ok = fx_limbs_fast<3>(sb, bot0[a], l0[a], l1[a], l2[a]) && ok;
-            o[a] = isf ? ord_f64(x[a]) : (uns ? x[a] : ord_i64(x[a]));
-        }
-        if (!ok) return false;
         if (gs != sl) {
             grun_flush();
             gs = sl;
@@ -1206,21 +1198,51 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
             gfirst = glast = (uint64_t)r;
 #pragma unroll
             for (int a = 0; a < NG; ++a) {
-                gl0[a] = gl1[a] = gl2[a] = gis[a] = gmax[a] = 0;
+                gr0[a] = gr1[a] = gmax[a] = 0;
                 gmin[a] = ~0ull;
             }
         }
         ++gn;
         gfirst = std::min<uint64_t>(gfirst, (uint64_t)r);
         glast = std::max<uint64_t>(glast, (uint64_t)r);
+        unsigned long long* q = (unsigned long long*)&lds[sl];
 #pragma unroll
         for (int a = 0; a < NG && a < NACC; ++a) {
-            gl0[a] += l0[a];
-            gl1[a] += l1[a];
-            gl2[a] += l2[a];
-            gmin[a] = std::min(gmin[a], o[a]);
-            gmax[a] = std::max(gmax[a], o[a]);
-            gis[a] += x[a];
+            const uint64_t dsc = dd0[a];
+            const uint32_t flags = (uint32_t)dsc & 0xFF;
+            const bool isf = (dsc >> 56) & 1;
+            const bool uns = (dsc >> 57) & 1;
+            const uint64_t ab = x[a] & 0x7fffffffffffffffull;
+            if (isf && ab >= 0x7ff0000000000000ull) {
+                // inf / NaN: the flags word (every f64 acc has one)
+                atomicOr(q + dfield(dsc, 48) * L, (unsigned long long)(ab > 0x7ff0000000000000ull ? FL_NAN
+                                                                     : ((x[a] >> 63) ? FL_NINF : FL_PINF)));
+            } else if (isf && (flags & A_FSUM)) {
+                uint64_t l0, l1, l2;
+                if (fx_limbs_fast<2>(x[a], bot0[a], l0, l1, l2)) {
+                    gr0[a] += l0;
+                    gr1[a] += l1;
+                } else {
+                    // below the 2-limb window (or out of the top): exact
+                    // conversion straight into the three LDS limb fields
+                    uint32_t ex = 0, fl = 0;
+                    const bool ok = fx_limbs(x[a], bot0[a], l0, l1, l2, fl, ex);
+                    d.fxbits |= fl << (2 * a);
+                    if (ok) {
+                        const int f = dfield(dsc, 8);
+                        atomicAdd(q + f * L, (unsigned long long)l0);
+                        atomicAdd(q + (f + 1) * L, (unsigned long long)l1);
+                        atomicAdd(q + (f + 2) * L, (unsigned long long)l2);
+                    }
+                }
+            } else if (!isf && (flags & A_ISUM)) {
+                gr0[a] += x[a];
+            }
+            if (!(isf && ab > 0x7ff0000000000000ull)) {  // NaN takes no part in min / max
+                const uint64_t o = isf ? ord_f64(x[a]) : (uns ? x[a] : ord_i64(x[a]));
+                gmin[a] = std::min(gmin[a], o);
+                gmax[a] = std::max(gmax[a], o);
+            }
         }
         return true;
     };
@@ -2143,6 +2165,8 @@ static int plan_groupby(const plgpu_column* key, const plgpu_column* cols, int32
     }
     for (int a = 0; a < p.nacc; ++a) {
         AccSpec& ac = p.acc[a];
+        // an inf / NaN row of an f64 acc always ORs the flags word
+        if (ac.isf) ac.flags |= A_FLAGS;
         if ((ac.flags & A_CNT) && ac.c.validity == nullptr && ac.c2.validity == nullptr && !force_counts)
             ac.flags &= ~A_CNT;
         if (ac.flags & (A_FSUM | A_FSUMCAST)) {
@@ -2318,7 +2342,8 @@ template <int NACC, int PRED, bool SUMONLY, bool DERIV>
 static hipError_t launch_fast(const Plan& pl, const DevProgram& dp, hipStream_t s) {
     if (SUMONLY && pl.limbs == 2 && pl.runs) return launch_fast_rows<NACC, PRED, SUMONLY, 2, true, DERIV>(pl, dp, s);
     if (SUMONLY && pl.limbs == 2) return launch_fast_rows<NACC, PRED, SUMONLY, 2, false, DERIV>(pl, dp, s);
-    if (!SUMONLY && NACC > 0 && !DERIV && pl.runs) return launch_fast_rows<NACC, PRED, false, 3, true, false>(pl, dp, s);
+    if (!SUMONLY && NACC > 0 && !DERIV && pl.runs && pl.limbs == 2)
+        return launch_fast_rows<NACC, PRED, false, 2, true, false>(pl, dp, s);
     return launch_fast_rows<NACC, PRED, SUMONLY, 3, false, DERIV>(pl, dp, s);
 }
 
@@ -2758,10 +2783,15 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
     pl.sum_only = so;
     // two LDS limbs when every sampled nonzero value of every summed column
     // sits at least kLimb2Margin binades above the 2-limb window's bottom
+    // (the register-run kernel for mixed aggregations holds two limbs the
+    // same way, for f64 sums; integer columns summed as f64 keep it off)
     pl.limbs = 3;
-    if (pl.sum_only) {
+    {
         bool two = true;
         for (int a = 0; a < p.nacc; ++a) {
+            const AccSpec& ac = p.acc[a];
+            if (ac.flags & A_FSUMCAST) two = false;
+            if (!(ac.flags & A_FSUM)) continue;
             const int mn = 0x7FF - (int)R.st[ST_MINEX + a];
             if (mn != 0x7FF && mn < R.hb[a] + 40 + 1075 + kLimb2Margin) two = false;
         }

@@ -589,6 +589,28 @@ def test_group_by_register_accumulators(gpu, layout, plgpu_option):
         assert info["path"] == 3, info
 
 
+@pytest.mark.parametrize("card", [7, 3000, 200_000])
+@pytest.mark.parametrize("nullable", [False, True])
+def test_len_count_first_last_of_float_with_specials(gpu, card, nullable):
+    """len / count / first / last of a Float64 column holding NaN / inf: such
+    an acc has no flags field (no sum / min / max), and an inf / NaN row must
+    not write one (round 2's out-of-table write, DESIGN.md "GPU fault
+    audit"; the checked build's CK_FIELD bit guards it).  Fused (LDS), generic
+    and global-table paths.  Exact vs the oracle."""
+    rng = np.random.default_rng(card + nullable)
+    n = 400_000
+    a = rng.standard_normal(n)
+    a[rng.random(n) < 0.05] = np.nan
+    a[rng.random(n) < 0.05] = np.inf
+    a[rng.random(n) < 0.05] = -np.inf
+    d = rng.standard_normal(n)
+    cols = {"a": (a, (rng.random(n) > 0.1) if nullable else None), "d": (d, None)}
+    key = rng.integers(0, card, n).astype(np.int64)
+    for aggs, mo in (([("len", "a"), ("sum", "d")], False), ([("count", "a"), ("len", "a")], False),
+                     ([("first", "a"), ("last", "a"), ("sum", "d")], True)):
+        _check_group_by(cols, key, None, aggs, None, None, [], mo)
+
+
 @pytest.mark.parametrize("layout", ["sorted", "runs_forced_random", "sorted_specials", "sorted_maintain_order",
                                     "random_control"])
 def test_group_by_register_runs_mixed_aggs(gpu, layout, plgpu_option):
@@ -599,14 +621,16 @@ def test_group_by_register_runs_mixed_aggs(gpu, layout, plgpu_option):
     rng = np.random.default_rng(len(layout) + 901)
     n = 2_000_003
     a = rng.uniform(10, 500, n)
-    d = rng.standard_normal(n)
+    d = rng.uniform(1, 5, n) * rng.choice([-1.0, 1.0], n)  # narrow exponent span: the 2-limb window
     b = rng.integers(-10**12, 10**12, n).astype(np.int64)
     c = rng.integers(-2**40, 2**40, n).astype(np.int64)  # the fused kernel takes 8-byte columns
     if layout == "sorted_specials":
         a[rng.random(n) < 0.001] = np.nan
         a[rng.random(n) < 0.0005] = -np.inf
         d[rng.random(n) < 0.001] = -0.0
-        d[rng.random(n) < 0.0002] = 1e-310  # subnormal: outside the fast conversion
+        # a few values the plan's sample misses, below the 2-limb window:
+        # straight into the LDS limb fields
+        d[[17, 1_000_003, n - 5]] = [1e-310, 3e-30, -7e-20]
     key = rng.integers(0, 120, n).astype(np.int64) * 104729 - 7
     if layout == "runs_forced_random":
         plgpu_option("runs", 1)
