@@ -617,7 +617,9 @@ int plgpu_gather(const plgpu_column* cols, int32_t ncols, const plgpu_column* id
  * partition, in row order within each; out_counts[p] = rows of partition p.
  * A key tuple holding a null is dropped when nulls_equal == 0 (it cannot
  * join) and routed to partition 0 otherwise.  The partition of a row depends
- * only on its key values, so every rank routes equal keys alike.  Replaces
+ * only on its key values, so every rank routes equal keys alike (floats by
+ * TotalEq class, -0.0 with 0.0 and every NaN together; String keys by a hash
+ * of their bytes).  Replaces
  * polars-utils/src/hashing.rs:101 HashPartitioner::hash_to_partition as
  * used by polars-stream/src/nodes/joins/equi_join.rs:445 / :740
  * (partition_and_sink / partition_and_probe). */

@@ -178,6 +178,7 @@ static DevCol sh_dev(const plgpu_column& c) {
     d.offset = c.offset;
     d.values = c.values;
     d.validity = c.validity;
+    d.data = c.data;  // PLGPU_STR: the bytes (hashed, mk_row_hash)
     return d;
 }
 
@@ -198,8 +199,8 @@ PLGPU_API int plgpu_hash_partition(const plgpu_column* keys, int32_t nkeys, int3
     const int64_t n = keys[0].length;
     for (int i = 0; i < nkeys; ++i) {
         const int32_t dt = keys[i].dtype;
-        if (!dtype_is_int(dt) && !dtype_is_float(dt) && dt != PLGPU_BOOL)
-            return fail(PLGPU_ERR_SCHEMA, "partition keys must be integer, float or Boolean columns");
+        if (!dtype_is_int(dt) && !dtype_is_float(dt) && dt != PLGPU_BOOL && dt != PLGPU_STR)
+            return fail(PLGPU_ERR_SCHEMA, "partition keys must be integer, float, Boolean or String columns");
         if (keys[i].length != n) return fail(PLGPU_ERR_SHAPE, "partition key columns must have equal lengths");
         k.c[i] = sh_dev(keys[i]);
     }

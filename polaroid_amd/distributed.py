@@ -35,6 +35,12 @@ from typing import Any, Sequence
 from . import _native as N
 from .expr import Expr
 
+class _RowShuffle(Exception):
+    """This input takes the row-shuffle protocol (group_by_agg): raised at
+    the same protocol point on every rank (a schema property, or a status
+    agreed by a collective), never by one rank alone."""
+
+
 def _device_for(group) -> Any:
     import torch
     import torch.distributed as dist
@@ -170,9 +176,14 @@ class GpuPartial:
         nrec = C.c_int64(0)
         refit = C.c_int32(0)
         hint = (C.c_int32 * N.GB_MAX_ACC)()
-        N.check(N.lib().plgpu_gb_partial_begin(C.byref(g.keycol), g.cols, g.ncols, g.prog, g.n_instr, g.aggs,
-                                               g.naggs, None, self.world, C.byref(self.handle), C.byref(nrec),
-                                               self.bottoms, C.byref(refit), hint, C.byref(self.info), None))
+        rc = N.lib().plgpu_gb_partial_begin(C.byref(g.keycol), g.cols, g.ncols, g.prog, g.n_instr, g.aggs,
+                                            g.naggs, None, self.world, C.byref(self.handle), C.byref(nrec),
+                                            self.bottoms, C.byref(refit), hint, C.byref(self.info), None)
+        if rc == N.ERR_CAPACITY and b"binades" in (N.lib().plgpu_last_error() or b""):
+            # an f64 sum wider than one fixed-point window: its exact state
+            # does not fit a record; the rows take the shuffle protocol
+            raise _RowShuffle("wide f64 sum")
+        N.check(rc)
         self.nrec = int(nrec.value)
         return list(self.bottoms)
 
@@ -232,8 +243,8 @@ def run_partitioned(part, world: int, group, device, timings: dict | None = None
             _sync(device)
         t1 = time.perf_counter()
         send, counts = part.export()
-    except Exception as e:  # noqa: BLE001 -- refused locally (a wide-range f64 sum) or any failure
-        # before the exchange: the count exchange still runs, with status 1
+    except Exception as e:  # noqa: BLE001 -- a wide-range f64 sum (status 2) or any failure
+        # before the exchange: the count exchange still runs, with the status
         # and no records, so every rank learns of it instead of waiting
         err = e
         bottoms = [0] * N.GB_MAX_ACC
@@ -242,13 +253,17 @@ def run_partitioned(part, world: int, group, device, timings: dict | None = None
 
         t1 = time.perf_counter()
         send, counts = torch.empty(0, dtype=torch.int64, device=device), [0] * world
-    recv, n, rows = exchange_records(send, counts, part.record_words, group,
-                                     header=[1 if err is not None else 0] + list(bottoms))
-    failed = [q for q, r in enumerate(rows) if r[1]]
-    if err is not None:
+    status = 0 if err is None else (2 if isinstance(err, _RowShuffle) else 1)
+    recv, n, rows = exchange_records(send, counts, part.record_words, group, header=[status] + list(bottoms))
+    failed = [q for q, r in enumerate(rows) if r[1] == 1]
+    if err is not None and status == 1:
         raise err
     if failed:
         raise N.ComputeError(f"multi-GPU group-by: the partial stage failed on rank(s) {failed}")
+    if any(r[1] == 2 for r in rows):
+        # some rank's shard holds a sum no record state fits: every rank
+        # switches to the row shuffle together
+        raise _RowShuffle("wide f64 sum on some rank")
     t2 = time.perf_counter()
     res = part.merge(recv, [r[0] for r in rows], [r[2:] for r in rows])
     if timings is not None:
@@ -350,7 +365,7 @@ def _pack_keys(df, keys: list, group, device):
         if k not in df.columns:
             raise N.ComputeError(f'unable to find column "{k}"')
         if df[k]._col.dtype not in _PACKABLE:
-            raise N.InvalidOperationError("the multi-GPU multi-key group-by takes integer / Boolean key columns")
+            raise _RowShuffle("a Float / String column in a key tuple")
     nk = len(keys)
     kcols = _col_array([df[k] for k in keys])
     r = (C.c_int64 * (3 * nk))()
@@ -364,8 +379,8 @@ def _pack_keys(df, keys: list, group, device):
     codes = N.Column()
     ok = C.c_int32(0)
     N.check(N.lib().plgpu_key_pack(kcols, nk, ranges, C.byref(codes), C.byref(ok), None))
-    if not ok.value:  # the same agreed ranges on every rank: every rank refuses
-        raise N.InvalidOperationError("the multi-GPU multi-key group-by: the key ranges need more than 63 bits")
+    if not ok.value:  # the same agreed ranges on every rank: every rank switches
+        raise _RowShuffle("key ranges need more than 63 bits")
     name = "__key"
     while name in df.columns:
         name += "_"
@@ -411,7 +426,7 @@ def _group_by_var(df, key, aggs: Sequence[Expr], predicate, group, info: dict | 
         if df[k].dtype is String and len(keys) == 1:
             str_keys.append(k)
         elif df[k]._col.dtype not in _TORCH_WIRE:
-            raise N.InvalidOperationError("multi-GPU var / std take numeric / Boolean keys or one short String key")
+            raise _RowShuffle("var / std with String keys in a tuple")
     if str_keys:
         # a short String key runs as its exact Int64 codes (the means cross
         # the all-gather as integers) and is decoded at the end
@@ -421,7 +436,7 @@ def _group_by_var(df, key, aggs: Sequence[Expr], predicate, group, info: dict | 
         short = C.c_int32(0)
         N.check(N.lib().plgpu_str_encode_short(C.byref(df[key]._col), C.byref(codes), C.byref(short), None))
         if _allreduce_max([0 if short.value else 1], group, _device_for(group))[0]:
-            raise N.InvalidOperationError("the multi-GPU group-by takes String keys of at most 7 bytes")
+            raise _RowShuffle("String keys longer than 7 bytes")
         df = DataFrame([Series._from_native(key, codes) if nm == key else df[nm] for nm in df.columns])
         out = _group_by_var(df, key, aggs, predicate, group, info)
         strs = N.Column()
@@ -433,7 +448,7 @@ def _group_by_var(df, key, aggs: Sequence[Expr], predicate, group, info: dict | 
         b = _agg_base(e)
         if b.kind == "agg" and b.op in ("std", "var"):
             if b.args[0].kind != "col":
-                raise N.InvalidOperationError("var / std of a computed expression is not supported")
+                raise _RowShuffle("var / std of a computed expression")
             if b.args[0].value not in var_cols:
                 var_cols.append(b.args[0].value)
         else:
@@ -485,19 +500,119 @@ def group_by_agg(df, key: str, aggs: Sequence[Expr], predicate: Expr | None = No
     held by all ranks of `group`.  Returns this rank's partition of the
     result (the groups whose key hashes to this rank; the null-key and
     INT64_MIN groups live on rank 0).  Group order is unspecified, as in the
-    reference without maintain_order."""
+    reference without maintain_order.
+
+    Two protocols, chosen identically on every rank:
+      partial states (the default): each rank pre-aggregates its shard and
+        only group records cross the links (volume ~ groups);
+      row shuffle: keys or values no fixed-size record carries -- String
+        keys longer than 7 bytes, key tuples with Float / String columns or
+        more than 63 bits, an f64 sum wider than one fixed-point window on
+        any rank, var / std with such keys or of an expression -- send the selected
+        rows to the rank owning their key (volume ~ selected rows) and
+        aggregate them there with the single-GPU group-by."""
+    import torch.distributed as dist
+
+    if not dist.is_initialized():
+        raise N.InvalidOperationError("torch.distributed is not initialised")
+    device = _device_for(group)
+    if device.type != "cuda":
+        raise N.InvalidOperationError("the GPU group-by needs the nccl (RCCL) backend")
+    try:
+        return _group_by_agg_states(df, key, aggs, predicate, group, info)
+    except _RowShuffle as why:
+        return run_shuffled(GpuShuffleOps, df, key, aggs, predicate, group, device, info, str(why))
+
+
+class GpuShuffleOps:
+    """The device half of the row-shuffle group-by, through the C-ABI."""
+
+    @staticmethod
+    def select(df, predicate, names: Sequence[str]):
+        from .frame import DataFrame
+
+        src = df.filter(predicate) if predicate is not None else df
+        return DataFrame([src[c] for c in names])
+
+    partition = staticmethod(lambda df, keys, world, nulls_equal: GpuJoinOps.partition(df, keys, world, nulls_equal))
+    to_wire = staticmethod(lambda df, perm=None: GpuJoinOps.to_wire(df, perm))
+    from_wire = staticmethod(lambda cols, n: GpuJoinOps.from_wire(cols, n))
+
+    @staticmethod
+    def logical(df, names: Sequence[str]):
+        return [df[c]._logical_dtype() for c in names]
+
+    @staticmethod
+    def restore(rows, names: Sequence[str], logical):
+        for c, lg in zip(names, logical):
+            rows[c]._with_logical(lg)
+        return rows
+
+    @staticmethod
+    def local_group_by(rows, key, aggs):
+        from .frame import _group_by
+
+        return _group_by(rows, key, list(aggs), False, None, None)
+
+    @staticmethod
+    def rows(df) -> int:
+        return df.height
+
+
+def run_shuffled(ops, df, key, aggs: Sequence[Expr], predicate, group, device, info: dict | None = None,
+                 why: str = ""):
+    """Row-shuffle group-by over any `ops` (the GPU one above, or a host
+    model in tests/test_distributed.py): the predicate and a projection onto
+    the key and input columns run locally, the selected rows go to the rank
+    owning their key (plgpu_hash_partition: the same key -- TotalEq for
+    floats, the bytes for Strings -- routes alike on every rank; null keys to
+    rank 0) in one all-to-all per buffer, and each rank aggregates what it
+    received with the single-GPU group-by.  The partitions are stable and
+    the exchange concatenates sources in rank order, so every group's rows
+    arrive in the global row order (first() / last() hold).  A failure
+    before the exchange is agreed by one status all-reduce."""
+    import torch.distributed as dist
+
+    from .expr import col
+
+    world = dist.get_world_size(group)
+    keys = [key] if isinstance(key, str) else list(key)
+    aggs = [a if isinstance(a, Expr) else col(a) for a in aggs]
+    err = wire = counts = None
+    names: list[str] = []
+    try:
+        names = list(dict.fromkeys(keys + [c for e in aggs for c in e.meta_root_names()]))
+        sub = ops.select(df, predicate, names)
+        logical = ops.logical(sub, names)
+        perm, counts = ops.partition(sub, keys, world, True)
+        wire = ops.to_wire(sub, perm)
+    except Exception as e:  # noqa: BLE001
+        err = e
+    failed = _allreduce_max([1 if err is not None else 0], group, device)[0]
+    if err is not None:
+        raise err
+    if failed:
+        raise N.ComputeError("multi-GPU group-by (row shuffle): the local stage failed on another rank")
+    cols, n = exchange_columns(wire, counts, group)
+    rows = ops.restore(ops.from_wire(cols, n), names, logical)
+    out = ops.local_group_by(rows, keys[0] if len(keys) == 1 else tuple(keys), aggs)
+    if info is not None:
+        info.update({"protocol": "row_shuffle", "reason": why, "rows_sent": int(sum(counts)), "rows_received": n,
+                     "groups": ops.rows(out)})
+    return out
+
+
+def _group_by_agg_states(df, key, aggs: Sequence[Expr], predicate, group, info: dict | None):
+    """The partial-states protocol of group_by_agg; raises _RowShuffle (on
+    every rank alike) for an input it cannot carry."""
     import torch
     import torch.distributed as dist
 
     from .frame import _agg_base, _gb_lower, _group_by, _join, _lower_strings
     from .expr import col
 
-    if not dist.is_initialized():
-        raise N.InvalidOperationError("torch.distributed is not initialised")
     world = dist.get_world_size(group)
     device = _device_for(group)
-    if device.type != "cuda":
-        raise N.InvalidOperationError("the GPU group-by needs the nccl (RCCL) backend")
     from .frame import DataFrame, Series, String
 
     aggs = [a if isinstance(a, Expr) else col(a) for a in aggs]
@@ -532,7 +647,7 @@ def group_by_agg(df, key: str, aggs: Sequence[Expr], predicate: Expr | None = No
         short = C.c_int32(0)
         N.check(N.lib().plgpu_str_encode_short(C.byref(df[key]._col), C.byref(codes), C.byref(short), None))
         if _allreduce_max([0 if short.value else 1], group, device)[0]:
-            raise N.InvalidOperationError("the multi-GPU group-by takes String keys of at most 7 bytes")
+            raise _RowShuffle("String keys longer than 7 bytes")
         df = DataFrame([Series._from_native(key, codes) if nm == key else df[nm] for nm in df.columns])
     packed = None
     float_key = None
@@ -558,8 +673,7 @@ def group_by_agg(df, key: str, aggs: Sequence[Expr], predicate: Expr | None = No
         # key: one exact Int64 code with a plan agreed over the ranks
         packed, df, key = _pack_keys(df, [key] if isinstance(key, str) else list(key), group, device)
     if not isinstance(key, str) or key not in df.columns or df[key]._col.dtype not in (N.I64, N.I32):
-        raise N.InvalidOperationError("the multi-GPU group-by takes one integer / float (or short String) key "
-                                      "column, or several integer / Boolean key columns")
+        raise _RowShuffle("a key the record protocol does not carry")
     # first() / last() travel as values (run_first_last); every other
     # aggregation as exact partial states
     fl = _first_last_split(aggs)
@@ -567,7 +681,7 @@ def group_by_agg(df, key: str, aggs: Sequence[Expr], predicate: Expr | None = No
     for i in fl:
         c = _agg_base(aggs[i]).args[0]
         if c.kind != "col" or c.value not in df.columns or df[c.value]._col.dtype not in _TORCH_WIRE:
-            raise N.InvalidOperationError("multi-GPU first() / last() take numeric or Boolean columns")
+            raise _RowShuffle("first() / last() of a String column")
     timings: dict = {}
     out = part = mi = None
     if rest or not fl:
@@ -646,12 +760,27 @@ _TORCH_WIRE = {N.I64: "int64", N.F64: "int64", N.I32: "int32", N.U32: "int32", N
 
 class WireColumn:
     """One column on the wire: values (8 / 4 bytes per row, Booleans one
-    byte) and an optional validity byte mask, as flat torch tensors."""
+    byte) and an optional validity byte mask, as flat torch tensors.  A
+    String column sends each row's byte length as its values and the bytes
+    themselves, rows in order, in `data` (uint8)."""
 
-    __slots__ = ("name", "dtype", "values", "valid")
+    __slots__ = ("name", "dtype", "values", "valid", "data")
 
-    def __init__(self, name: str, dtype: int, values, valid):
-        self.name, self.dtype, self.values, self.valid = name, dtype, values, valid
+    def __init__(self, name: str, dtype: int, values, valid, data=None):
+        self.name, self.dtype, self.values, self.valid, self.data = name, dtype, values, valid, data
+
+
+def _segment_sums(lens, counts: Sequence[int]) -> list[int]:
+    """Sums of `lens` over consecutive segments of counts[i] rows (the
+    bytes of each destination's rows of a String column)."""
+    import torch
+
+    if not counts:
+        return []
+    ends = torch.tensor([sum(counts[:i + 1]) for i in range(len(counts))], dtype=torch.int64, device=lens.device)
+    cs = torch.cat([torch.zeros(1, dtype=torch.int64, device=lens.device), torch.cumsum(lens, 0)])
+    at = cs[ends].tolist()
+    return [int(a - b) for a, b in zip(at, [0] + at[:-1])]
 
 
 def _wire_spec(cols: Sequence[WireColumn], group) -> list[tuple[str, int, bool]]:
@@ -703,7 +832,17 @@ def exchange_columns(cols: Sequence[WireColumn], counts: Sequence[int], group=No
             r = torch.empty(n, dtype=t.dtype, device=t.device)
             alltoallv(r, t, rcounts, list(counts), group)
             bufs.append(r)
-        out.append(WireColumn(name, dt, bufs[0], bufs[1]))
+        data = None
+        if dt == N.STR:
+            # the bytes of each destination's rows: their byte counts first
+            sb = _segment_sums(c.values, counts)
+            sbt = torch.tensor(sb, dtype=torch.int64, device=device)
+            rbt = torch.empty_like(sbt)
+            dist.all_to_all_single(rbt, sbt, group=group)
+            rb = [int(v) for v in rbt.tolist()]
+            data = torch.empty(sum(rb), dtype=torch.uint8, device=device)
+            alltoallv(data, c.data, rb, sb, group)
+        out.append(WireColumn(name, dt, bufs[0], bufs[1], data))
     _settle(device)
     return out, n
 
@@ -737,7 +876,20 @@ def allgather_columns(cols: Sequence[WireColumn], rows: int, group=None):
             dist.all_gather(parts, padded, group=group)
             bufs.append(torch.cat([p[:k] for p, k in zip(parts, counts)]) if total else
                         torch.empty(0, dtype=t.dtype, device=t.device))
-        out.append(WireColumn(name, dt, bufs[0], bufs[1]))
+        data = None
+        if dt == N.STR:
+            nb = torch.tensor([int(c.data.numel())], dtype=torch.int64, device=device)
+            alln = [torch.empty_like(nb) for _ in range(world)]
+            dist.all_gather(alln, nb, group=group)
+            bcounts = [int(t.item()) for t in alln]
+            bcap = max(bcounts) if bcounts else 0
+            padded = torch.zeros(bcap, dtype=torch.uint8, device=device)
+            padded[:bcounts[dist.get_rank(group)]] = c.data
+            parts = [torch.empty(bcap, dtype=torch.uint8, device=device) for _ in range(world)]
+            dist.all_gather(parts, padded, group=group)
+            data = torch.cat([p[:k] for p, k in zip(parts, bcounts)]) if bcap else \
+                torch.empty(0, dtype=torch.uint8, device=device)
+        out.append(WireColumn(name, dt, bufs[0], bufs[1], data))
     _settle(device)
     return out, total
 
@@ -771,27 +923,84 @@ class GpuJoinOps:
         n = df.height if perm is None else perm.len()
         dev = torch.device("cuda", torch.cuda.current_device())
         names = df.columns
-        out = []
-        for nm in names:
+        fixed = [nm for nm in names if df[nm]._col.dtype != N.STR]
+        wire = {}
+        for nm in fixed:
             s = df[nm]
-            dt = s.dtype.code
+            dt = s._col.dtype
             vals = torch.empty(n, dtype=getattr(torch, _TORCH_WIRE[dt]), device=dev)
             valid = torch.empty(n, dtype=torch.uint8, device=dev) if s._col.validity else None
-            out.append(WireColumn(nm, dt, vals, valid))
-        if names and n:
-            dv = (C.c_void_p * len(names))(*[c.values.data_ptr() for c in out])
-            vv = (C.c_void_p * len(names))(*[c.valid.data_ptr() if c.valid is not None else None for c in out])
-            N.check(N.lib().plgpu_gather_rows(_col_array([df[nm] for nm in names]), len(names),
+            wire[nm] = WireColumn(nm, dt, vals, valid)
+        if fixed and n:
+            out = [wire[nm] for nm in fixed]
+            dv = (C.c_void_p * len(fixed))(*[c.values.data_ptr() for c in out])
+            vv = (C.c_void_p * len(fixed))(*[c.valid.data_ptr() if c.valid is not None else None for c in out])
+            N.check(N.lib().plgpu_gather_rows(_col_array([df[nm] for nm in fixed]), len(fixed),
                                               C.byref(perm._col) if perm is not None else None, dv, vv, None))
-        return out
+        for nm in names:
+            if nm not in wire:
+                wire[nm] = GpuJoinOps._string_to_wire(df[nm], perm, n, dev)
+        return [wire[nm] for nm in names]
+
+    @staticmethod
+    def _string_to_wire(s, perm, n: int, dev) -> WireColumn:
+        """A String column (rows in `perm` order) -> per-row byte lengths,
+        a validity byte mask and the bytes (plgpu_gather packs the rows)."""
+        import torch
+
+        from .frame import Series, UInt32, _col_array
+
+        if perm is None:
+            idx_t = torch.arange(n, dtype=torch.int32, device=dev)
+            perm = Series.from_device("__perm", UInt32, idx_t.data_ptr(), n, keepalive=idx_t)
+        g = N.Column()
+        N.check(N.lib().plgpu_gather(_col_array([s]), 1, C.byref(perm._col), C.byref(g), None))
+        gs = Series._from_native(s.name, g)
+        offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        N.check(N.lib().plgpu_memcpy_d2d(C.c_void_p(offs.data_ptr()), C.c_void_p(int(g.values) + 8 * int(g.offset)),
+                                         8 * (n + 1), None))
+        N.check(N.lib().plgpu_synchronize(None))
+        b0, b1 = (int(v) for v in offs[[0, n]].tolist())
+        data = torch.empty(b1 - b0, dtype=torch.uint8, device=dev)
+        if b1 > b0:
+            N.check(N.lib().plgpu_memcpy_d2d(C.c_void_p(data.data_ptr()), C.c_void_p(int(g.data) + b0), b1 - b0, None))
+        valid = None
+        if g.validity:
+            nbytes = (int(g.offset) + n + 7) // 8
+            bits = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+            N.check(N.lib().plgpu_memcpy_d2d(C.c_void_p(bits.data_ptr()), C.c_void_p(int(g.validity)), nbytes, None))
+            shifts = torch.arange(8, dtype=torch.uint8, device=dev)
+            valid = ((bits.view(-1, 1) >> shifts) & 1).view(-1)[int(g.offset): int(g.offset) + n].contiguous()
+        N.check(N.lib().plgpu_synchronize(None))
+        del gs
+        return WireColumn(s.name, N.STR, (offs[1:] - offs[:-1]).contiguous(), valid, data)
 
     @staticmethod
     def from_wire(cols: Sequence[WireColumn], n: int):
         from .frame import DataFrame, Series, _BY_CODE
 
+        import torch
+
         series = []
         for c in cols:
             dt = _BY_CODE[c.dtype]
+            if c.dtype == N.STR:
+                offs = torch.zeros(n + 1, dtype=torch.int64, device=c.values.device)
+                if n:
+                    torch.cumsum(c.values, 0, out=offs[1:])
+                data = c.data if c.data.numel() else torch.zeros(1, dtype=torch.uint8, device=c.values.device)
+                keep = [offs, data, c.valid]
+                mptr, nulls = None, 0
+                if c.valid is not None:
+                    vb = N.DeviceBuffer(((n + 63) // 64) * 8)
+                    z = C.c_int64(0)
+                    N.check(N.lib().plgpu_pack_bits(C.c_void_p(c.valid.data_ptr()), n, C.c_void_p(vb.ptr),
+                                                    C.byref(z), None))
+                    mptr, nulls = vb.ptr, int(z.value)
+                    keep.append(vb)
+                series.append(Series.from_device(c.name, dt, offs.data_ptr(), n, mptr, keepalive=keep,
+                                                 null_count=nulls, data_ptr=data.data_ptr()))
+                continue
             keep: list = [c.values, c.valid]
             vptr = c.values.data_ptr()
             if c.dtype == N.BOOL:

@@ -323,8 +323,9 @@ class Series:
     @classmethod
     def from_device(cls, name: str, dtype: DataType, values_ptr: int, length: int,
                     validity_ptr: int | None = None, offset: int = 0, keepalive: Any = None,
-                    null_count: int = -1) -> "Series":
-        """Borrow existing device buffers (e.g. torch tensors) without copying."""
+                    null_count: int = -1, data_ptr: int | None = None) -> "Series":
+        """Borrow existing device buffers (e.g. torch tensors) without copying.
+        String: `values_ptr` holds the int64 offsets, `data_ptr` the bytes."""
         s = cls.__new__(cls)
         s.name = name
         s._logical = dtype if dtype.logical else None
@@ -335,6 +336,8 @@ class Series:
         c.null_count = 0 if validity_ptr is None else int(null_count)
         c.values = int(values_ptr)
         c.validity = int(validity_ptr) if validity_ptr else None
+        if data_ptr:
+            c.data = int(data_ptr)
         s._col = c
         s._keep = [keepalive] if keepalive is not None else []
         return s

@@ -282,3 +282,179 @@ def test_first_last_failure_reaches_every_rank_gloo():
         assert p.exitcode == 0
     assert res[world - 1] == "RuntimeError"
     assert all(res[r] == "ComputeError" for r in range(world - 1))
+
+
+# ------------------------------------------------ row-shuffle protocol
+_STR = D.N.STR
+
+
+class HostShuffleOps:
+    """Models GpuShuffleOps over numpy: frames are {name: (dtype, values,
+    valid)}; String columns are object arrays on the wire as byte lengths +
+    UTF-8 bytes (the device wire format); the local group-by keeps first /
+    last / sum / len per key in arrival order."""
+
+    @staticmethod
+    def select(df, predicate, names):
+        assert predicate is None
+        return {c: df[c] for c in names}
+
+    @staticmethod
+    def logical(df, names):
+        return [None] * len(names)
+
+    @staticmethod
+    def restore(rows, names, logical):
+        return rows
+
+    @staticmethod
+    def partition(df, keys, world, nulls_equal):
+        n = len(next(iter(df.values()))[1])
+        dest = np.zeros(n, dtype=np.int64)
+        for k in keys:
+            dt, v, m = df[k]
+            h = np.array([sum(x.encode()) if dt == _STR else int(x) for x in v], dtype=np.int64)
+            if m is not None:
+                h[~m] = 0
+            dest = dest * 1000003 + h
+        dest = np.abs(dest) % world
+        perm = np.argsort(dest, kind="stable")
+        return perm, [int((dest == r).sum()) for r in range(world)]
+
+    @staticmethod
+    def to_wire(df, perm=None):
+        out = []
+        for name, (dt, v, m) in df.items():
+            vv = v[perm]
+            mm = None if m is None else torch.from_numpy(m[perm].astype(np.uint8))
+            if dt == _STR:
+                enc = [x.encode() for x in vv]
+                lens = torch.tensor([len(b) for b in enc], dtype=torch.int64)
+                data = torch.frombuffer(bytearray(b"".join(enc)) or bytearray(1), dtype=torch.uint8)[:int(lens.sum())]
+                out.append(D.WireColumn(name, dt, lens, mm, data.clone()))
+            else:
+                out.append(D.WireColumn(name, dt, torch.from_numpy(np.ascontiguousarray(vv)), mm))
+        return out
+
+    @staticmethod
+    def from_wire(cols, n):
+        res = {}
+        for c in cols:
+            m = None if c.valid is None else c.valid.numpy().astype(bool)
+            if c.dtype == _STR:
+                lens = c.values.numpy()
+                raw = bytes(c.data.numpy().tobytes())
+                offs = np.concatenate([[0], np.cumsum(lens)])
+                v = np.array([raw[offs[i]:offs[i + 1]].decode() for i in range(n)], dtype=object)
+            else:
+                v = c.values.numpy()
+            assert v.shape[0] == n
+            res[c.name] = (c.dtype, v, m)
+        return res
+
+    @staticmethod
+    def local_group_by(rows, key, aggs):
+        assert isinstance(key, str)
+        _, kv, km = rows[key]
+        out = {}
+        for i in range(len(kv)):
+            k = None if (km is not None and not km[i]) else kv[i]
+            _, sv, _ = rows["s"]
+            _, xv, _ = rows["x"]
+            g = out.setdefault(k, [0, 0, None, None])
+            g[0] += int(xv[i])
+            g[1] += 1
+            if g[2] is None:
+                g[2] = sv[i]
+            g[3] = sv[i]
+        return out
+
+    @staticmethod
+    def rows(df):
+        return len(df)
+
+
+def _sh_shard(rank, n=300):
+    rng = np.random.default_rng(rank + 11)
+    pool = np.array([f"long-symbol-{i}" for i in range(40)] + ["", "é"], dtype=object)
+    k = pool[rng.integers(0, pool.size, n)]
+    km = rng.random(n) > 0.1
+    s = np.array([f"r{rank}-row{i}" for i in range(n)], dtype=object)
+    x = rng.integers(-100, 100, n).astype(np.int64)
+    return {"k": (_STR, k, km), "s": (_STR, s, None), "x": (D.N.I64, x, None)}
+
+
+def _sh_worker(rank, world, port, q, fail):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from polaroid_amd.expr import col
+
+        class Ops(HostShuffleOps):
+            @staticmethod
+            def select(df, predicate, names):
+                if fail and rank == 1:
+                    raise RuntimeError("local stage failed")
+                return HostShuffleOps.select(df, predicate, names)
+
+        aggs = [col("x").sum(), col("s").first(), col("s").last()]
+        try:
+            out = D.run_shuffled(Ops, _sh_shard(rank), "k", aggs, None, None, torch.device("cpu"))
+            q.put((rank, out))
+        except Exception as e:  # noqa: BLE001
+            q.put((rank, type(e).__name__))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_row_shuffle_protocol_gloo(world):
+    """run_shuffled: String keys and payloads cross the wire as lengths +
+    bytes, every key lands on exactly one rank, the sources arrive in rank
+    order (first / last over the concatenated shards), and the union equals
+    the single-process aggregation."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sh_worker, args=(r, world, port, q, False)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    merged = {}
+    for r in range(world):
+        assert not (set(res[r]) & set(merged))
+        merged.update(res[r])
+    full = {}
+    for r in range(world):
+        sh = _sh_shard(r)
+        _, kv, km = sh["k"]
+        for i in range(len(kv)):
+            k = kv[i] if km[i] else None
+            g = full.setdefault(k, [0, 0, None, None])
+            g[0] += int(sh["x"][1][i])
+            g[1] += 1
+            if g[2] is None:
+                g[2] = sh["s"][1][i]
+            g[3] = sh["s"][1][i]
+    assert merged == full
+    assert None in res[0]  # the null key routes to rank 0
+
+
+def test_row_shuffle_failure_reaches_every_rank_gloo():
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sh_worker, args=(r, world, port, q, True)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[1] == "RuntimeError"
+    assert res[0] == "ComputeError" and res[2] == "ComputeError"

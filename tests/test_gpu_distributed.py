@@ -201,7 +201,7 @@ def test_group_by_agg_world1_rccl(gpu):
 def test_group_by_agg_world1_rccl_string_key(gpu):
     """The multi-GPU group-by with a String symbol key (<= 7 bytes: exact
     Int64 codes through the partial-state exchange), one RCCL rank, against
-    the single-GPU group-by; a longer key is refused."""
+    the single-GPU group-by; a longer key takes the row shuffle."""
     import torch.distributed as dist
 
     with socket.socket() as s:
@@ -232,9 +232,13 @@ def test_group_by_agg_world1_rccl_string_key(gpu):
         got = sorted(zip(out["sym"].to_list(), out["s"].to_list(), out["len"].to_list()), key=str)
         exp = sorted(zip(ref["sym"].to_list(), ref["s"].to_list(), ref["len"].to_list()), key=str)
         assert got == exp and len(got) == 1 + 100
-        long_df = pl.DataFrame({"sym": pl.Series("sym", ["AAPL", "TOOLONGKEY"]), "v": pl.Series("v", [1.0, 2.0])})
-        with pytest.raises(pl.InvalidOperationError, match="7 bytes"):
-            D.group_by_agg(long_df, "sym", [pl.col("v").sum()])
+        # a longer key takes the row-shuffle protocol
+        long_df = pl.DataFrame({"sym": pl.Series("sym", ["AAPL", "TOOLONGKEY", "AAPL"]),
+                                "v": pl.Series("v", [1.0, 2.0, 4.0])})
+        info = {}
+        out = D.group_by_agg(long_df, "sym", [pl.col("v").sum()], info=info)
+        assert sorted(zip(out["sym"].to_list(), out["v"].to_list())) == [("AAPL", 5.0), ("TOOLONGKEY", 2.0)]
+        assert info["protocol"] == "row_shuffle"
     finally:
         dist.destroy_process_group()
 
@@ -421,7 +425,8 @@ def test_key_pack_agreed_across_shards(gpu):
 def test_group_by_agg_world1_rccl_multi_key(gpu):
     """The multi-GPU group-by on (Int64, Int32, Boolean) keys with nulls:
     packed codes agreed over the ranks, then the single-key protocol; against
-    the single-GPU multi-key group-by.  Float keys are refused."""
+    the single-GPU multi-key group-by.  A Float key in the tuple takes the
+    row shuffle."""
     import torch.distributed as dist
 
     with socket.socket() as s:
@@ -452,8 +457,9 @@ def test_group_by_agg_world1_rccl_multi_key(gpu):
         assert table(out) == table(ref)
         fdf = pl.DataFrame({"k": pl.Series.from_numpy("k", np.array([1.0, 2.0])),
                             "j": pl.Series.from_numpy("j", np.array([1, 2], dtype=np.int64))})
-        with pytest.raises(pl.InvalidOperationError, match="integer / Boolean"):
-            D.group_by_agg(fdf, ("k", "j"), [pl.len()])
+        info = {}
+        out = D.group_by_agg(fdf, ("k", "j"), [pl.len()], info=info)  # a Float in the tuple: row shuffle
+        assert info["protocol"] == "row_shuffle" and sorted(out["len"].to_list()) == [1, 1]
     finally:
         dist.destroy_process_group()
 
@@ -568,3 +574,190 @@ def test_merge_sources_sum_guard_bits(gpu):
     out = run(1 << 36)
     want = math.ldexp(1.0, base) + 2 * math.ldexp(1.0, 100 + base + 78)
     assert out["s"].to_list() == [want]
+
+
+# ------------------------------------------------- row-shuffle protocol
+def _canon(v):
+    if isinstance(v, float):
+        return ("f", "nan" if math.isnan(v) else v.hex())
+    return v
+
+
+def _rows_of(df, names):
+    cols = [df[c].to_list() for c in names]
+    return sorted((tuple(_canon(v) for v in r) for r in zip(*cols)), key=repr)
+
+
+def _shuffle_simulate(shards, world, key, aggs, pred):
+    """run_shuffled over `shards` in one process: each shard's selected rows
+    are partitioned and put on the wire, every destination receives the
+    sources' segments in source-rank order (as exchange_columns lays them
+    out, String bytes included) and aggregates them."""
+    import torch
+
+    ops = D.GpuShuffleOps
+    keys = [key] if isinstance(key, str) else list(key)
+    names = list(dict.fromkeys(keys + [c for e in aggs for c in e.meta_root_names()]))
+    sent, logical = [], None
+    for df in shards:
+        sub = ops.select(df, pred, names)
+        logical = ops.logical(sub, names)
+        perm, counts = ops.partition(sub, keys, world, True)
+        sent.append((ops.to_wire(sub, perm), counts))
+    frames = []
+    for dest in range(world):
+        n = sum(c[dest] for _, c in sent)
+        cols = []
+        for j in range(len(names)):
+            nullable = any(w[j].valid is not None for w, _ in sent)
+            vals, valid, data = [], [], []
+            for wire, counts in sent:
+                off = sum(counts[:dest])
+                vals.append(wire[j].values[off: off + counts[dest]])
+                if nullable:
+                    valid.append(wire[j].valid[off: off + counts[dest]] if wire[j].valid is not None else
+                                 torch.ones(counts[dest], dtype=torch.uint8, device="cuda"))
+                if wire[j].data is not None:
+                    sb = D._segment_sums(wire[j].values, counts)
+                    b0 = sum(sb[:dest])
+                    data.append(wire[j].data[b0: b0 + sb[dest]])
+            proto = sent[0][0][j]
+            cols.append(D.WireColumn(proto.name, proto.dtype, torch.cat(vals).contiguous(),
+                                     torch.cat(valid).contiguous() if nullable else None,
+                                     torch.cat(data).contiguous() if data else None))
+        rows = ops.restore(ops.from_wire(cols, n), names, logical)
+        frames.append(ops.local_group_by(rows, keys[0] if len(keys) == 1 else tuple(keys), aggs))
+    return frames
+
+
+def _shuffle_case_frame(rng, n, case):
+    """(columns dict of Series inputs, key, aggs, predicate) for one of the
+    inputs the partial-state records cannot carry."""
+    pool = np.array(["AAPL.NASDAQ", "MSFT", "", "BRK.B-CLASS", "日本語の銘柄", "x" * 40] +
+                    [f"SYMBOL-{i:05d}" for i in range(300)], dtype=object)
+    v = rng.standard_normal(n) * 100
+    v[rng.random(n) < 0.01] = np.nan
+    w = rng.uniform(1, 5, n)
+    i = rng.integers(-50, 50, n).astype(np.int64)
+    cols = {"v": (v, rng.random(n) > 0.05), "w": (w, None), "i": (i, None)}
+    if case == "long_string_key":
+        cols["s"] = (pool[rng.integers(0, pool.size, n)], rng.random(n) > 0.02)
+        key = "s"
+        aggs = [pl.col("v").sum().alias("sum_v"), pl.col("v").mean().alias("mean_v"), pl.col("w").min().alias("mn"),
+                pl.col("w").max().alias("mx"), pl.col("v").count().alias("cnt"), pl.len(),
+                pl.col("w").first().alias("fw"), pl.col("i").last().alias("li")]
+    elif case == "float_string_tuple":
+        f = rng.choice(np.array([-0.0, 0.0, 1.5, np.nan, -2.25]), n)
+        cols["f"] = (f, rng.random(n) > 0.03)
+        cols["s"] = (pool[rng.integers(0, 20, n)], None)
+        key = ("f", "s", "i")
+        aggs = [pl.col("w").sum().alias("sw"), pl.len(), pl.col("v").max().alias("mv")]
+    elif case == "wide_sum":
+        x = rng.standard_normal(n)
+        x[rng.random(n) < 0.3] *= 1e300
+        x[rng.random(n) < 0.3] *= 1e-300
+        cols["x"] = (x, None)
+        key = "i"
+        aggs = [pl.col("x").sum().alias("sx"), pl.col("x").mean().alias("mx"), pl.col("w").sum().alias("sw")]
+    elif case == "wide_int_tuple":
+        # two full-range Int64 keys: the tuple needs more than 63 bits
+        cols["k1"] = (rng.integers(-2**62, 2**62, n).astype(np.int64) // 997 * 997, None)
+        cols["k2"] = (rng.choice(np.array([-2**63, 2**63 - 1, 0, 5], dtype=np.int64), n), rng.random(n) > 0.05)
+        key = ("k1", "k2")
+        aggs = [pl.col("w").sum().alias("sw"), pl.col("i").first().alias("fi"), pl.col("v").last().alias("lv")]
+    else:  # var / std with a String key in a tuple
+        cols["s"] = (pool[rng.integers(0, 10, n)], None)
+        key = ("s", "i")
+        aggs = [pl.col("w").var().alias("var_w"), pl.col("v").std().alias("std_v"), pl.len()]
+    return cols, key, aggs, pl.col("w") > 1.5
+
+
+SHUFFLE_CASES = ["long_string_key", "float_string_tuple", "wide_sum", "wide_int_tuple", "var_std_tuple"]
+
+
+@pytest.mark.parametrize("case", SHUFFLE_CASES)
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_row_shuffle_group_by_vs_single_gpu(gpu, world, case):
+    """The row-shuffle protocol (inputs no fixed-size partial record
+    carries), simulated over W shards in one process: the union of the W
+    partitions equals the single-GPU group-by of the concatenated shards row
+    for row (exact sums; first / last in global row order; every group on
+    exactly one rank)."""
+    rng = np.random.default_rng(world * 31 + len(case))
+    n = 60_000
+    cols, key, aggs, pred = _shuffle_case_frame(rng, n, case)
+    full = pl.DataFrame({k: pl.Series.from_numpy(k, a, m) for k, (a, m) in cols.items()})
+    cuts = np.linspace(0, n, world + 1).astype(int)
+    shards = [pl.DataFrame({k: pl.Series.from_numpy(k, a[cuts[r]:cuts[r + 1]],
+                                                    None if m is None else m[cuts[r]:cuts[r + 1]])
+                            for k, (a, m) in cols.items()}) for r in range(world)]
+    frames = _shuffle_simulate(shards, world, key, aggs, pred)
+    ref = full.lazy().filter(pred).group_by(key).agg(*aggs).collect()
+    names = ref.columns
+    got = [r for f in frames for r in _rows_of(f, names)]
+    assert sorted(got, key=repr) == _rows_of(ref, names)
+    keys = [key] if isinstance(key, str) else list(key)
+    seen = [tuple(_canon(v) for v in r) for f in frames for r in zip(*[f[k].to_list() for k in keys])]
+    assert len(seen) == len(set(seen))  # each group on exactly one rank
+
+
+def test_group_by_agg_world1_rccl_row_shuffle(gpu):
+    """The row-shuffle protocol through torch.distributed (nccl = RCCL), one
+    rank: every input the partial records cannot carry is accepted, reported
+    as info["protocol"] == "row_shuffle", and equals the single-GPU group-by;
+    the common keys keep the partial-state protocol."""
+    import torch.distributed as dist
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        for case in SHUFFLE_CASES:
+            rng = np.random.default_rng(len(case))
+            cols, key, aggs, pred = _shuffle_case_frame(rng, 50_000, case)
+            df = pl.DataFrame({k: pl.Series.from_numpy(k, a, m) for k, (a, m) in cols.items()})
+            info = {}
+            out = D.group_by_agg(df, key, aggs, pred, info=info)
+            ref = df.lazy().filter(pred).group_by(key).agg(*aggs).collect()
+            assert _rows_of(out, ref.columns) == _rows_of(ref, ref.columns), case
+            assert info.get("protocol") == "row_shuffle", (case, info)
+        info = {}
+        df = pl.DataFrame({"k": pl.Series("k", [1, 2, 1]), "v": pl.Series("v", [1.0, 2.0, 3.0])})
+        D.group_by_agg(df, "k", [pl.col("v").sum()], info=info)
+        assert "protocol" not in info
+    finally:
+        dist.destroy_process_group()
+
+
+def test_join_world1_rccl_string_key_and_payload(gpu):
+    """The multi-GPU join's wire carries String columns (per-row lengths +
+    bytes): a String-keyed shuffle join with String payloads, one RCCL rank,
+    against the single-GPU join."""
+    import torch.distributed as dist
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        rng = np.random.default_rng(8)
+        pool = np.array([f"instrument-{i:04d}" for i in range(500)] + ["", "é"], dtype=object)
+        left = pl.DataFrame({"k": pl.Series.from_numpy("k", pool[rng.integers(0, pool.size, 20_000)],
+                                                       rng.random(20_000) > 0.05),
+                             "x": pl.Series.from_numpy("x", rng.standard_normal(20_000))})
+        right = pl.DataFrame({"k": pl.Series.from_numpy("k", pool[:400]),
+                              "name": pl.Series.from_numpy("name", np.array([f"n{i}" * (i % 5) for i in range(400)],
+                                                                            dtype=object))})
+        for strategy in ("shuffle", "broadcast"):
+            info = {}
+            out = D.join(left, right, on="k", strategy=strategy, info=info)
+            ref = left.join(right, on="k")
+            assert info["strategy"] == strategy
+            assert _rows_of(out, ref.columns) == _rows_of(ref, ref.columns)
+    finally:
+        dist.destroy_process_group()
