@@ -171,7 +171,10 @@ enum plgpu_agg_kind {
     PLGPU_AGG_COUNT = 5, /* non-null count, u32 (IdxSize)                    */
     PLGPU_AGG_LEN = 6,   /* group length incl. nulls, u32                    */
     PLGPU_AGG_FIRST = 7, /* value of the group's first row, null included    */
-    PLGPU_AGG_LAST = 8   /* ... last row (reduce/first_last.rs First / Last) */
+    PLGPU_AGG_LAST = 8,  /* ... last row (reduce/first_last.rs First / Last) */
+    PLGPU_AGG_VAR = 9,   /* variance of a Float64 column, f64 out; ddof in bits */
+                         /* 8..15 of the kind (plgpu_group_by_agg_ex only)      */
+    PLGPU_AGG_STD = 10   /* its square root                                    */
 };
 
 typedef struct plgpu_agg {

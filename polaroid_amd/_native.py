@@ -33,7 +33,7 @@ OP = dict(
     AND=30, OR=31, NOT=32, IS_NULL=33, IS_NOT_NULL=34, IS_NAN=35, IS_FINITE=36,
     STR_STARTS_WITH=40, STR_ENDS_WITH=41, STR_CONTAINS=42,
 )
-AGG = dict(sum=1, mean=2, min=3, max=4, count=5, len=6, first=7, last=8)
+AGG = dict(sum=1, mean=2, min=3, max=4, count=5, len=6, first=7, last=8, var=9, std=10)  # var / std: ddof << 8
 MAX_COLS = 8
 MAX_KEYS = 8
 

@@ -75,7 +75,8 @@ enum : int {
     ST_MINEX = 17,       // + acc: 0x7FF - smallest exponent of a nonzero finite value (plan / maxexp)
     ST_RUNS = 23,        // plan: sampled adjacent row pairs with equal keys (sorted / clustered keys)
     ST_LOCAL = 24,       // plan: most distinct keys among the samples of one 1/kPlanKeyBlocks row range
-    ST_WORDS = 25
+    ST_VAR_OUT = 25,     // finalize: a fused variance whose exact state left its range (caller reruns)
+    ST_WORDS = 26
 };
 
 // An aggregation input derived from the columns in registers (an
@@ -83,8 +84,10 @@ enum : int {
 // aexpr/properties/general.rs:335 can_pre_agg): value = x op y with x the
 // acc's column, y a second Float64 column (c2) or a literal (dimm); every
 // other expression is materialised by the host before the pass.
-enum : int32_t { DOP_NONE = 0, DOP_ADD = 1, DOP_SUB = 2, DOP_MUL = 3, DOP_DIV = 4, DOP_DIVS = 5,
-                 DOP_OPMASK = 7, DOP_SWAP = 8, DOP_LIT = 16 };
+// DOP_SQHI / DOP_SQLO (unary, with DOP_LIT): x * x rounded, and its exact
+// error fma(x, x, -(x * x)) -- the fused variance's second-moment inputs.
+enum : int32_t { DOP_NONE = 0, DOP_ADD = 1, DOP_SUB = 2, DOP_MUL = 3, DOP_DIV = 4, DOP_DIVS = 5, DOP_SQHI = 6,
+                 DOP_SQLO = 7, DOP_OPMASK = 7, DOP_SWAP = 8, DOP_LIT = 16 };
 
 struct AccSpec {
     DevCol c;         // the aggregated column (derived: the first operand column)
@@ -188,7 +191,13 @@ __device__ __forceinline__ uint64_t derive(int32_t dop, uint64_t x, uint64_t y) 
     case DOP_SUB: r = a - b; break;
     case DOP_MUL: r = a * b; break;
     case DOP_DIV: r = a / b; break;
-    default: r = a * (1.0 / b); break;
+    case DOP_DIVS: r = a * (1.0 / b); break;
+    case DOP_SQHI: r = xa * xa; break;
+    default: {
+        const double h = xa * xa;
+        r = __builtin_fma(xa, xa, -h);  // exact: x * x == h + r for 2^-484 <= |x| < 2^511
+        break;
+    }
     }
     return f64_bits(r);
 }
@@ -1778,10 +1787,130 @@ struct OutSpec {
     int32_t out_dtype;
     int32_t in_isf;
     int32_t in_uns;
-    int32_t _pad;
+    int32_t ddof;     // VAR / STD
+    int32_t acc_hi;   // VAR / STD: the accs of x * x rounded and of its exact error
+    int32_t acc_lo;
     void* values;
     uint32_t* validity;
 };
+
+// ---- fused variance: exact second moment from exact sums
+// With S1 = sum x = W1 * 2^b1, and x * x = h + l exactly (DOP_SQHI / SQLO,
+// |x| in [2^-484, 2^511)) summed exactly as W2 * 2^b2 and W3 * 2^b3:
+//   n * sum((x - mean)^2) = n * (W2 * 2^b2 + W3 * 2^b3) - W1^2 * 2^(2 b1),
+// an integer times 2^e, e = min(b2, b3, 2 b1), formed exactly in a 1024-bit
+// two's complement accumulator and rounded once to f64.
+constexpr int kVarWords = 16;
+
+// |W| of a 192-bit two's complement word triple; returns the sign.
+__device__ __forceinline__ bool abs192(uint64_t& w0, uint64_t& w1, uint64_t& w2) {
+    const bool neg = (int64_t)w2 < 0;
+    if (neg) {
+        w0 = ~w0; w1 = ~w1; w2 = ~w2;
+        w0 += 1;
+        const uint64_t c0 = w0 == 0;
+        w1 += c0;
+        w2 += (c0 && w1 == 0) ? 1 : 0;
+    }
+    return neg;
+}
+
+// acc += (negate ? -1 : 1) * (m[0..k) << sh) over the full width; false when
+// the shifted value would not fit (the caller falls back).
+__device__ bool big_add_shifted(uint64_t (&acc)[kVarWords], const uint64_t* m, int k, int sh, bool negate) {
+    int top = k - 1;
+    while (top >= 0 && m[top] == 0) --top;
+    if (top < 0) return true;
+    const int bitlen = top * 64 + 64 - __clzll(m[top]);
+    if (sh < 0 || bitlen + sh > kVarWords * 64 - 2) return false;
+    const int ws = sh >> 6, bs = sh & 63;
+    uint64_t carry = negate ? 1 : 0;
+    for (int i = 0; i < kVarWords; ++i) {
+        const int j = i - ws;
+        uint64_t t = 0;
+        if (j >= 0 && j <= k) {
+            const uint64_t lo = j < k ? m[j] : 0ull;
+            const uint64_t hi = (j >= 1 && j - 1 < k) ? m[j - 1] : 0ull;
+            t = bs ? (lo << bs) | (hi >> (64 - bs)) : lo;
+        }
+        if (negate) t = ~t;
+        const uint64_t s1 = acc[i] + t;
+        const uint64_t c1 = s1 < t ? 1ull : 0ull;
+        const uint64_t s2 = s1 + carry;
+        const uint64_t c2 = s2 < s1 ? 1ull : 0ull;
+        acc[i] = s2;
+        carry = c1 | c2;
+    }
+    return true;
+}
+
+// acc * 2^e2 as f64, rounded once (half-even); acc >= 0 (a negative value
+// cannot occur for an exact sum of squares, and is clamped to 0).
+__device__ double big_to_double(const uint64_t (&acc)[kVarWords], int e2) {
+    if ((int64_t)acc[kVarWords - 1] < 0) return 0.0;
+    int t = kVarWords - 1;
+    while (t >= 0 && acc[t] == 0) --t;
+    if (t < 0) return 0.0;
+    const int p = t * 64 + 63 - __clzll(acc[t]);  // leading bit
+    const int q = p - 63;                           // bit offset of the 64-bit window
+    uint64_t x;
+    bool sticky = false;
+    if (q <= 0) {
+        x = acc[0] << (-q);
+    } else {
+        const int w = q >> 6, b = q & 63;
+        x = b ? (acc[w] >> b) | (acc[w + 1] << (64 - b)) : acc[w];
+        sticky = b ? (acc[w] & ((1ull << b) - 1)) != 0 : false;
+        for (int i = 0; i < w && !sticky; ++i) sticky = acc[i] != 0;
+    }
+    uint64_t keep = x >> 11;
+    const uint64_t rem = x & 0x7FF;
+    if (rem > 0x400 || (rem == 0x400 && (sticky || (keep & 1)))) ++keep;
+    int ex = p - 52 + e2;
+    if (keep == (1ull << 53)) {
+        keep >>= 1;
+        ++ex;
+    }
+    return ldexp((double)keep, ex);
+}
+
+// The variance of one group from its exact states; false: out of range.
+__device__ bool var_exact(uint64_t a0, uint64_t a1, uint64_t a2, int b1, uint64_t h0, uint64_t h1, uint64_t h2,
+                          int b2, uint64_t l0, uint64_t l1, uint64_t l2, int b3, uint64_t n, double& num) {
+    (void)abs192(a0, a1, a2);  // W1^2 only
+    const bool hneg = abs192(h0, h1, h2), lneg = abs192(l0, l1, l2);
+    const uint64_t W1[3] = {a0, a1, a2};
+    uint64_t sq[6] = {0, 0, 0, 0, 0, 0};
+    for (int i = 0; i < 3; ++i) {
+        unsigned __int128 c = 0;
+        for (int j = 0; j < 3; ++j) {
+            c += (unsigned __int128)W1[i] * W1[j] + sq[i + j];
+            sq[i + j] = (uint64_t)c;
+            c >>= 64;
+        }
+        sq[i + 3] = (uint64_t)c;
+    }
+    auto times_n = [&](uint64_t w0, uint64_t w1, uint64_t w2, uint64_t (&o)[4]) {
+        unsigned __int128 c = (unsigned __int128)w0 * n;
+        o[0] = (uint64_t)c;
+        c = (c >> 64) + (unsigned __int128)w1 * n;
+        o[1] = (uint64_t)c;
+        c = (c >> 64) + (unsigned __int128)w2 * n;
+        o[2] = (uint64_t)c;
+        o[3] = (uint64_t)(c >> 64);
+    };
+    uint64_t nh[4], nl[4];
+    times_n(h0, h1, h2, nh);
+    times_n(l0, l1, l2, nl);
+    const int e = min(min(b2, b3), 2 * b1);
+    uint64_t acc[kVarWords];
+    for (int i = 0; i < kVarWords; ++i) acc[i] = 0;
+    if (!big_add_shifted(acc, nh, 4, b2 - e, hneg)) return false;
+    if (!big_add_shifted(acc, nl, 4, b3 - e, lneg)) return false;
+    if (!big_add_shifted(acc, sq, 6, 2 * b1 - e, true)) return false;
+    num = big_to_double(acc, e);
+    return true;
+}
 
 struct FinParams {
     OutSpec out[PLGPU_MAX_COLS * 2];
@@ -1834,6 +1963,38 @@ __global__ void gb_finalize_kernel(GbParams p, FinParams fp) {
                     else sum = sum / (double)cnt;
                 }
                 dev_store(os.values, os.out_dtype, g, f64_bits(sum));  // Float32: rounded once more
+                break;
+            }
+            case PLGPU_AGG_VAR:
+            case PLGPU_AGG_STD: {
+                // moment.rs:126 VarState::finalize: null when count <= ddof;
+                // an inf / NaN value makes it NaN
+                double v = 0.0;
+                if (cnt <= (uint64_t)os.ddof) {
+                    valid = false;
+                } else if (flags) {
+                    v = __builtin_nan("");
+                } else {
+                    const AccSpec& ah = p.acc[os.acc_hi];
+                    const AccSpec& al = p.acc[os.acc_lo];
+                    const uint64_t hf = *gfield(p, ah.f_flags, s) | *gfield(p, al.f_flags, s);
+                    double num = 0.0;
+                    const bool ok = hf == 0 &&
+                                    var_exact(*gfield(p, ac.f_sum, s), *gfield(p, ac.f_sum + 1, s),
+                                              *gfield(p, ac.f_sum + 2, s), p.bottoms[os.acc],
+                                              *gfield(p, ah.f_sum, s), *gfield(p, ah.f_sum + 1, s),
+                                              *gfield(p, ah.f_sum + 2, s), p.bottoms[os.acc_hi],
+                                              *gfield(p, al.f_sum, s), *gfield(p, al.f_sum + 1, s),
+                                              *gfield(p, al.f_sum + 2, s), p.bottoms[os.acc_lo], cnt, num);
+                    if (!ok) {
+                        // x * x overflowed, or the exact state left the accumulator
+                        atomicOr((unsigned long long*)&p.status[ST_VAR_OUT], 1ull);
+                    } else {
+                        v = (num / (double)cnt) / (double)(cnt - (uint64_t)os.ddof);
+                        if (os.kind == PLGPU_AGG_STD) v = __builtin_sqrt(v);
+                    }
+                }
+                ((double*)os.values)[g] = v;
                 break;
             }
             case PLGPU_AGG_MIN:
@@ -2053,6 +2214,7 @@ struct Plan {
     GbParams p;
     std::vector<OutSpec> outs;
     int acc_of_agg[64];
+    int acc_in[kMaxAcc];  // the input index each acc aggregates
     size_t lds_bytes;
     int grid;
     bool use_lds;
@@ -2099,24 +2261,25 @@ static int plan_groupby(const plgpu_column* key, const plgpu_column* cols, int32
     p.f_len = nf++;
     bool any_first = false, any_last = false;
     for (int i = 0; i < naggs; ++i) {
-        any_first |= aggs[i].kind == PLGPU_AGG_FIRST;
-        any_last |= aggs[i].kind == PLGPU_AGG_LAST;
+        any_first |= (aggs[i].kind & 0xFF) == PLGPU_AGG_FIRST;
+        any_last |= (aggs[i].kind & 0xFF) == PLGPU_AGG_LAST;
     }
     p.f_first = (maintain_order || any_first) ? nf++ : -1;
     if (p.f_first >= 0) p.min_init_mask |= 1ull << p.f_first;
     p.f_last = any_last ? nf++ : -1;
     std::vector<int> acc_of_col((size_t)std::max(nins, 1), -1);
     p.nacc = 0;
-    for (int i = 0; i < naggs; ++i) {
-        const int c = aggs[i].col;
-        if (c < 0 || c >= nins) return fail(PLGPU_ERR_INVALID, "aggregation column index out of range");
+    // the acc of input c (created on first use); -1 with the error set
+    auto acc_for = [&](int c) -> int {
+        if (c < 0 || c >= nins) return fail(PLGPU_ERR_INVALID, "aggregation column index out of range"), -1;
         const InSpec& in = ins[c];
         const int32_t dt = in.dtype;
         if (!dtype_is_int(dt) && !dtype_is_float(dt))
-            return fail(PLGPU_ERR_INVALID, "aggregation not supported for this dtype");
+            return fail(PLGPU_ERR_INVALID, "aggregation not supported for this dtype"), -1;
         if (acc_of_col[c] < 0) {
-            if (p.nacc == kMaxAcc) return fail(PLGPU_ERR_INVALID, "too many aggregated columns (max 6)");
+            if (p.nacc == kMaxAcc) return fail(PLGPU_ERR_INVALID, "too many aggregated columns (max 6)"), -1;
             acc_of_col[c] = p.nacc;
+            pl->acc_in[p.nacc] = c;
             AccSpec& ac = p.acc[p.nacc++];
             std::memset(&ac, 0xff, sizeof ac);
             ac.c = to_dev(in.col);
@@ -2128,12 +2291,37 @@ static int plan_groupby(const plgpu_column* key, const plgpu_column* cols, int32
             if (in.dop != DOP_NONE && !(in.dop & DOP_LIT)) ac.c2 = to_dev(in.col2);
             ac.dimm = in.imm;
         }
-        AccSpec& ac = p.acc[acc_of_col[c]];
+        return acc_of_col[c];
+    };
+    std::vector<int> var_hi((size_t)std::max(naggs, 1), -1), var_lo((size_t)std::max(naggs, 1), -1);
+    for (int i = 0; i < naggs; ++i) {
+        const int c = aggs[i].col;
+        const int a = acc_for(c);
+        if (a < 0) return PLGPU_ERR_INVALID;
+        const InSpec& in = ins[c];
+        const int32_t dt = in.dtype;
+        AccSpec& ac = p.acc[a];
         const bool isf = dtype_is_float(dt);
         // partial / merge mode keeps the record layout schema-only (the same on
         // every rank whatever its validity bitmaps): counts always present
         const bool nullable = in.col.validity != nullptr || (ac.c2.validity != nullptr) || force_counts;
-        switch (aggs[i].kind) {
+        switch (aggs[i].kind & 0xFF) {
+        case PLGPU_AGG_VAR:
+        case PLGPU_AGG_STD: {
+            // exact sum and count of x; exact sums of x * x's two parts
+            // (derived inputs hi, hi + 1, plgpu_group_by_agg_ex)
+            const int hi = (aggs[i].kind >> 16) & 0xFFF;
+            if (!isf || hi == 0) return fail(PLGPU_ERR_INVALID, "var / std in one pass take a Float64 column");
+            ac.flags |= A_FSUM | A_FLAGS;
+            if (nullable) ac.flags |= A_CNT;
+            const int ah = acc_for(hi), al = ah < 0 ? -1 : acc_for(hi + 1);
+            if (ah < 0 || al < 0) return PLGPU_ERR_INVALID;
+            p.acc[ah].flags |= A_FSUM | A_FLAGS;
+            p.acc[al].flags |= A_FSUM | A_FLAGS;
+            var_hi[i] = ah;
+            var_lo[i] = al;
+            break;
+        }
         case PLGPU_AGG_SUM: ac.flags |= isf ? (A_FSUM | A_FLAGS) : A_ISUM; break;
         case PLGPU_AGG_MEAN:
             ac.flags |= isf ? (A_FSUM | A_FLAGS) : A_FSUMCAST;
@@ -2147,7 +2335,7 @@ static int plan_groupby(const plgpu_column* key, const plgpu_column* cols, int32
         case PLGPU_AGG_LAST: break;
         default: return fail(PLGPU_ERR_INVALID, "unknown aggregation kind");
         }
-        pl->acc_of_agg[i] = acc_of_col[c];
+        pl->acc_of_agg[i] = a;
     }
     // operand columns shared between accs ((close * volume).sum() next to
     // volume.sum()) are loaded once by the fused kernel
@@ -2223,12 +2411,17 @@ static int plan_groupby(const plgpu_column* key, const plgpu_column* cols, int32
     for (int i = 0; i < naggs; ++i) {
         OutSpec o;
         std::memset(&o, 0, sizeof o);
-        o.kind = aggs[i].kind;
+        o.kind = aggs[i].kind & 0xFF;
         o.acc = pl->acc_of_agg[i];
+        o.ddof = (aggs[i].kind >> 8) & 0xFF;
+        o.acc_hi = var_hi[i];
+        o.acc_lo = var_lo[i];
         const int32_t dt = ins[aggs[i].col].dtype;
         o.in_isf = dtype_is_float(dt);
         o.in_uns = dt == PLGPU_U64;
         switch (o.kind) {
+        case PLGPU_AGG_VAR:
+        case PLGPU_AGG_STD: o.out_dtype = PLGPU_F64; break;
         case PLGPU_AGG_LEN:
         case PLGPU_AGG_COUNT: o.out_dtype = PLGPU_U32; break;
         case PLGPU_AGG_MEAN: o.out_dtype = dt == PLGPU_F32 ? PLGPU_F32 : PLGPU_F64; break;  // reduce/mean.rs:29
@@ -2403,10 +2596,16 @@ static hipError_t launch_main_dispatch(const Plan& pl, const DevProgram& dp, int
 //                                              before the pass.
 // A fused input is materialised as well when the pass does not run the
 // fused kernel (generic kernel, partitioned many-groups path).
+__global__ void sq_split_kernel(DevCol x, int64_t n, int32_t dop, uint64_t* __restrict__ out) {
+    const uint64_t* v = (const uint64_t*)x.values;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[x.offset + i] = derive(dop, v[x.offset + i], 0ull);
+}
+
 struct DerivIn {
     const plgpu_instr* prog;
     int32_t n;
-    int32_t kind;    // 1 column, 2 fused, 0 materialise
+    int32_t kind;    // 1 column, 2 fused, 0 materialise, 3 a var column's x * x split (DOP_SQHI / DOP_SQLO)
     int32_t ca, cb;  // column operands (cb -1: literal)
     int32_t dop;
     uint64_t imm;
@@ -2520,11 +2719,31 @@ struct GbRun {
 
 // Materialise aggregation input j (plgpu_eval of its program) into R.mat.
 static int gb_materialize(GbRun& R, int j, plgpu_column* out) {
+    if (R.deriv == nullptr || j < 0 || j >= (int)R.deriv->in.size())
+        return fail(PLGPU_ERR_INVALID, "internal: derived input index out of range");
     const DerivIn& di = R.deriv->in[j];
     plgpu_column c;
     std::memset(&c, 0, sizeof c);
-    int rc = plgpu_eval(R.cols, R.ncols, di.prog, di.n, &c, R.s);
-    if (rc) return rc;
+    int rc;
+    if (di.kind == 3) {
+        // x * x or its exact error, rows at the column's own offset so its
+        // validity bitmap is shared as it is
+        const plgpu_column& x = R.cols[di.ca];
+        if ((rc = make_owned_column(&c, PLGPU_F64, x.offset + x.length, false, R.s))) return rc;
+        c.offset = x.offset;
+        c.length = x.length;
+        c.validity = x.validity;
+        c.null_count = x.null_count;
+        const int g = (int)std::min<int64_t>((x.length + 255) / 256, 256 * 32);
+        if (x.length > 0) sq_split_kernel<<<g, 256, 0, R.s>>>(to_dev(x), x.length, di.dop, (uint64_t*)c.values);
+        if (hipGetLastError() != hipSuccess) {
+            plgpu_column_release(&c);
+            return fail(PLGPU_ERR_HIP, "var square split");
+        }
+    } else {
+        rc = plgpu_eval(R.cols, R.ncols, di.prog, di.n, &c, R.s);
+        if (rc) return rc;
+    }
     R.mat.push_back(c);
     *out = c;
     return PLGPU_OK;
@@ -2586,7 +2805,7 @@ static int gb_prepare(GbRun& R, const plgpu_column* key, const plgpu_column* col
             std::memset(&in, 0, sizeof in);
             if (di.kind == 1) {
                 in = R.ins[di.ca];
-            } else if (di.kind == 2) {
+            } else if (di.kind == 2 || di.kind == 3) {
                 in.col = cols[di.ca];
                 if (di.cb >= 0) in.col2 = cols[di.cb];
                 in.dtype = PLGPU_F64;
@@ -2602,10 +2821,10 @@ static int gb_prepare(GbRun& R, const plgpu_column* key, const plgpu_column* col
     if ((rc = plan_groupby(key, cols, ncols, R.ins.data(), (int32_t)R.ins.size(), aggs, naggs,
                            maintain_order || R.want_first, R.dp, &R.pl, force_counts)))
         return rc;
-    // the input index of each acc (first aggregation that created it)
+    // the input index of each acc (also the var / std accs of x * x's parts,
+    // which no aggregation names directly)
     R.acc_input.assign(kMaxAcc, -1);
-    for (int i = 0; i < naggs; ++i)
-        if (R.acc_input[R.pl.acc_of_agg[i]] < 0) R.acc_input[R.pl.acc_of_agg[i]] = aggs[i].col;
+    for (int a = 0; a < R.pl.p.nacc; ++a) R.acc_input[a] = R.pl.acc_in[a];
     // status words, the bottoms, then (at word kPlanSetWord) the plan's
     // global distinct-key set; one allocation, one memset
     static_assert(ST_WORDS * 8 + kMaxAcc * 4 <= kPlanSetWord * 8, "status layout");
@@ -3193,8 +3412,17 @@ static int gb_finalize(GbRun& R, int32_t naggs, plgpu_column* out_key, plgpu_col
     for (int i = 0; i < naggs && rc == PLGPU_OK; ++i) {
         const OutSpec& o = pl.outs[i];
         const bool nullable = o.kind == PLGPU_AGG_MEAN || o.kind == PLGPU_AGG_MIN || o.kind == PLGPU_AGG_MAX ||
-                              o.kind == PLGPU_AGG_FIRST || o.kind == PLGPU_AGG_LAST;
-        rc = make_owned_column(&out_aggs[i], o.out_dtype, groups, nullable, s);
+                              o.kind == PLGPU_AGG_FIRST || o.kind == PLGPU_AGG_LAST || o.kind == PLGPU_AGG_VAR ||
+                              o.kind == PLGPU_AGG_STD;
+        if (o.kind == PLGPU_AGG_VAR || o.kind == PLGPU_AGG_STD) {
+            // exactness of the fused second moment: no wide (multi-window)
+            // sum among its three, and |x| >= 2^-484 for every nonzero x
+            // (the window bottom), so x * x splits exactly into h + l
+            const bool wide = ((R.wide >> o.acc) | (R.wide >> o.acc_hi) | (R.wide >> o.acc_lo)) & 1u;
+            if (wide || R.hb[o.acc] < -484)
+                rc = fail(PLGPU_ERR_CAPACITY, "var: the fused second moment is out of its exact range");
+        }
+        if (rc == PLGPU_OK) rc = make_owned_column(&out_aggs[i], o.out_dtype, groups, nullable, s);
     }
     uint64_t* first = nullptr;
     if (rc == PLGPU_OK && (R.maintain || keep_first) && groups > 0) rc = dev_alloc((void**)&first, groups * 8, s);
@@ -3216,12 +3444,15 @@ static int gb_finalize(GbRun& R, int32_t naggs, plgpu_column* out_key, plgpu_col
         gb_finalize_kernel<<<fg, 256, 0, s>>>(p, fp);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) rc = hip_fail(e, "gb_finalize_kernel");
-        uint64_t produced = 0;
+        uint64_t produced = 0, var_out = 0;
         if (rc == PLGPU_OK) {
             e = hipMemcpyAsync(&produced, R.status + ST_GROUPS_OUT, 8, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipMemcpyAsync(&var_out, R.status + ST_VAR_OUT, 8, hipMemcpyDeviceToHost, s);
             if (e == hipSuccess) e = hipStreamSynchronize(s);
             if (e != hipSuccess) rc = hip_fail(e, "finalize count");
         }
+        if (rc == PLGPU_OK && var_out)
+            rc = fail(PLGPU_ERR_CAPACITY, "var: the fused second moment is out of its exact range");
         if (rc == PLGPU_OK && (int64_t)produced != groups) {
             char buf[256];
             snprintf(buf, sizeof buf,
@@ -4235,7 +4466,7 @@ static int gb_keyless(const plgpu_column* cols, int32_t ncols, const Deriv* deri
         plgpu_column_release(&out_aggs[i]);
         rc = make_owned_column(&out_aggs[i], dt, 1, has_valid, s);
         if (rc) break;
-        const int32_t kind = aggs[i].kind;
+        const int32_t kind = aggs[i].kind & 0xFF;
         const bool valid = kind == PLGPU_AGG_SUM || kind == PLGPU_AGG_LEN || kind == PLGPU_AGG_COUNT;
         const size_t vb = dt == PLGPU_BOOL ? 8 : (size_t)std::max(dtype_bytes(dt), 1);
         hipError_t e = hipMemsetAsync((void*)out_aggs[i].values, 0, vb, s);
@@ -4268,12 +4499,43 @@ PLGPU_API int plgpu_group_by_agg_ex(const plgpu_column* keys, int32_t nkeys, con
     Deriv d;
     int rc = classify_inputs(cols, ncols, inputs, ninputs, &d);
     if (rc) return rc;
-    const Deriv* dv = ninputs > 0 ? &d : nullptr;
-    if (nkeys == 0) return gb_keyless(cols, ncols, dv, program, n_instr, aggs, naggs, out_aggs, info, stream);
+    // var / std (fused second moment, DESIGN.md "var / std in one pass"):
+    // every var column x adds two derived inputs, x * x rounded and its exact
+    // error, whose exact sums next to x's give n * sum(x^2) - (sum x)^2
+    // exactly; the rewritten kind carries the first of them in bits 16..27
+    std::vector<plgpu_agg> ag(aggs, aggs + std::max(naggs, 0));
+    int hi_of[PLGPU_MAX_COLS];
+    for (int c = 0; c < PLGPU_MAX_COLS; ++c) hi_of[c] = -1;
+    bool any_var = false;
+    for (int i = 0; i < naggs; ++i) {
+        const int base = aggs[i].kind & 0xFF;
+        if (base != PLGPU_AGG_VAR && base != PLGPU_AGG_STD) continue;
+        const int c = aggs[i].col;
+        if (c < 0 || c >= ncols || cols[c].dtype != PLGPU_F64)
+            return fail(PLGPU_ERR_INVALID, "var / std in one pass take a Float64 column");
+        if (hi_of[c] < 0) {
+            hi_of[c] = ncols + (int)d.in.size();
+            for (int q = 0; q < 2; ++q) {
+                DerivIn di;
+                std::memset(&di, 0, sizeof di);
+                di.kind = 3;
+                di.ca = c;
+                di.cb = -1;
+                di.dop = (q == 0 ? DOP_SQHI : DOP_SQLO) | DOP_LIT;
+                di.out_dtype = PLGPU_F64;
+                d.in.push_back(di);
+            }
+        }
+        ag[i].kind = (aggs[i].kind & 0xFFFF) | (hi_of[c] << 16);
+        any_var = true;
+    }
+    const Deriv* dv = (ninputs > 0 || any_var) ? &d : nullptr;
+    const plgpu_agg* ap = naggs > 0 ? ag.data() : aggs;
+    if (nkeys == 0) return gb_keyless(cols, ncols, dv, program, n_instr, ap, naggs, out_aggs, info, stream);
     if (nkeys == 1 && dtype_is_int(keys[0].dtype))
-        return gb_single_impl(&keys[0], cols, ncols, dv, program, n_instr, aggs, naggs, maintain_order, &out_keys[0],
+        return gb_single_impl(&keys[0], cols, ncols, dv, program, n_instr, ap, naggs, maintain_order, &out_keys[0],
                               out_aggs, info, stream);
-    return gb_multi_impl(keys, nkeys, cols, ncols, dv, program, n_instr, aggs, naggs, maintain_order, out_keys,
+    return gb_multi_impl(keys, nkeys, cols, ncols, dv, program, n_instr, ap, naggs, maintain_order, out_keys,
                          out_aggs, info, stream);
 }
 

@@ -1337,6 +1337,12 @@ def _gb_lower(df: DataFrame, key: str | tuple | None, aggs: list[Expr], pred: Ex
         if base.kind == "len":
             specs.append(("len", len_col))
             out_logical.append(None)
+        elif (base.kind == "agg" and base.op in ("var", "std") and base.args[0].kind == "col"
+              and base.args[0].value in df._cols and df._cols[base.args[0].value].dtype is Float64):
+            # one fused pass (plgpu_group_by_agg_ex: exact sums of x and of
+            # x * x's two parts, ddof in bits 8..15 of the kind)
+            specs.append(((base.op, int(base.value)), base.args[0].value))
+            out_logical.append(None)
         elif (base.kind == "agg" and base.args[0].kind == "col" and base.args[0].value in df._cols
               and df._cols[base.args[0].value].dtype is not Boolean):
             c_ = base.args[0].value
@@ -1410,7 +1416,7 @@ def _gb_lower(df: DataFrame, key: str | tuple | None, aggs: list[Expr], pred: Ex
         inputs[j].n_instr = builtins.len(prog)
     agg_arr = (N.Agg * max(1, builtins.len(specs)))()
     for i, (k, c_) in enumerate(specs):
-        agg_arr[i].kind = _AGG_CODE[k]
+        agg_arr[i].kind = _AGG_CODE[k[0]] | (k[1] << 8) if isinstance(k, tuple) else _AGG_CODE[k]
         agg_arr[i].col = idx[c_] if isinstance(c_, str) else ncols + c_[1]
     g.key = keys[0] if keys else None
     g.keys = keys
@@ -1448,6 +1454,38 @@ def _agg_base(e: Expr) -> Expr:
     return e.args[0] if e.kind == "alias" else e
 
 
+def _group_by_fused_var(df: DataFrame, key: str | tuple, aggs: list[Expr], maintain_order: bool,
+                        pred: Expr | None, info: dict | None) -> DataFrame:
+    """var / std of Float64 columns in fused passes.  A var column takes
+    three of the kernel's six accumulators (x, and x * x's two parts), so
+    more than two var columns, or two next to other aggregated columns, run
+    as several passes over the same selected rows with first-occurrence
+    group order (identical groups and order in every pass), put side by
+    side."""
+    vcols = list(dict.fromkeys(_agg_base(e).args[0].value for e in aggs
+                               if _agg_base(e).kind == "agg" and _agg_base(e).op in ("std", "var")))
+    plain = [e for e in aggs if not (_agg_base(e).kind == "agg" and _agg_base(e).op in ("std", "var"))]
+    pcols = {c for e in plain for c in e.meta_root_names()}
+    if 3 * builtins.len(vcols) + builtins.len(pcols) <= N.GB_MAX_ACC:
+        return _group_by_plain(df, key, aggs, maintain_order, pred, info)
+    names = [e.output_name() for e in aggs]
+    parts = []
+    batches = [vcols[i:i + 2] for i in range(0, builtins.len(vcols), 2)]
+    for bi, vb in enumerate(batches):
+        sel = [e for e in aggs if _agg_base(e).kind == "agg" and _agg_base(e).op in ("std", "var")
+               and _agg_base(e).args[0].value in vb]
+        parts.append(_group_by_plain(df, key, sel, True, pred, info if bi == 0 else None))
+    if plain:
+        parts.append(_group_by_plain(df, key, plain, True, pred, None))
+    keys = _gb_keys(key)
+    cols = {}
+    for part in parts:
+        for nm in part.columns:
+            if nm not in keys:
+                cols[nm] = part[nm]
+    return DataFrame([parts[0][k] for k in keys] + [cols[nm] for nm in names])
+
+
 def _group_by_var(df: DataFrame, key: str | tuple, aggs: list[Expr], maintain_order: bool,
                   pred: Expr | None, info: dict | None) -> DataFrame:
     """group_by().agg() with var / std (polars-expr/src/reduce/var_std.rs),
@@ -1482,6 +1520,31 @@ def _group_by_var(df: DataFrame, key: str | tuple, aggs: list[Expr], maintain_or
                 var_cols.append(b.args[0].value)
         else:
             plain.append((i, e))
+    # one pass: exact sums of x and of x * x (split into its rounded product
+    # and that product's exact error), combined exactly per group (DESIGN.md
+    # "var / std in one pass"); an integer column as its f64 values (the
+    # reference casts before its Welford update); inputs whose exact state
+    # would leave its range, and Float32 columns, take the passes below
+    fdf, faggs, casts = df, list(aggs), {}
+    for i, e in enumerate(faggs):
+        b = _agg_base(e)
+        if b.kind == "agg" and b.op in ("std", "var") and fdf._cols[b.args[0].value].dtype in INTEGER_DTYPES:
+            c = b.args[0].value
+            if c not in casts:
+                casts[c] = f"__vf_{c}"
+                fdf = DataFrame(list(fdf._cols.values()) + [_eval(col(c).cast("f64").alias(casts[c]), fdf)])
+            faggs[i] = Expr("agg", (col(casts[c]),), op=b.op, value=b.value).alias(e.output_name())
+    vbases = [_agg_base(e) for e in faggs if _agg_base(e).kind == "agg" and _agg_base(e).op in ("std", "var")]
+    if builtins.all(fdf._cols[b.args[0].value].dtype is Float64 and 0 <= int(b.value) <= 255 for b in vbases):
+        try:
+            out = _group_by_fused_var(fdf, key, faggs, maintain_order, pred, info)
+            if info is not None:
+                info["var_path"] = "fused"
+            return out
+        except (N.ComputeError, N.InvalidOperationError):
+            pass  # out of the exact range, or too many columns: the passes below
+    if info is not None:
+        info["var_path"] = "two_pass"
     helpers = []
     for c in var_cols:
         # mean(): f64 from the exact sum of the values widened to f64, so an
@@ -1534,6 +1597,11 @@ def _group_by(df: DataFrame, key: str | tuple, aggs: list[Expr], maintain_order:
               pred: Expr | None, info: dict | None) -> DataFrame:
     if any(_agg_base(e).kind == "agg" and _agg_base(e).op in ("std", "var") for e in aggs):
         return _group_by_var(df, key, aggs, maintain_order, pred, info)
+    return _group_by_plain(df, key, aggs, maintain_order, pred, info)
+
+
+def _group_by_plain(df: DataFrame, key: str | tuple, aggs: list[Expr], maintain_order: bool,
+                    pred: Expr | None, info: dict | None) -> DataFrame:
     if pred is not None:
         pred, df = _lower_strings(pred, df)
         pred, _, strict = _prepare(pred, df)

@@ -39,6 +39,17 @@ def _oracle(key, x, valid, ddof, sel):
     return np.array(order, dtype=np.int64), var, np.sqrt(var), np.array(ok, dtype=bool)
 
 
+def _exact_var(vals, ddof):
+    """The exact variance of the f64 values (rational arithmetic), rounded once."""
+    from fractions import Fraction
+
+    fv = [Fraction(float(v)) for v in vals]
+    n = len(fv)
+    s1 = sum(fv)
+    s2 = sum(v * v for v in fv)
+    return float((n * s2 - s1 * s1) / (n * (n - ddof)))
+
+
 def _close(got, want, ok):
     assert np.allclose(got[ok], want[ok], rtol=1e-12, atol=1e-300)
 
@@ -133,3 +144,122 @@ def test_var_std_integer_sums_past_input_width(gpu, dt):
     assert got_v[0] == 0.0 and got_v[2] is None
     assert abs(got_v[1] - want_v[1]) <= 1e-12 * abs(want_v[1])
     assert out["s"].to_list()[0] == 0.0 and out["s"].to_list()[2] == 0.0
+
+
+def _var_frame(rng, n, card, nulls=True):
+    key = rng.integers(0, card, n).astype(np.int64)
+    x = rng.standard_normal(n) * 1e3 + 5e6  # large mean: catastrophic for a rounded one-pass formula
+    y = rng.uniform(-5, 5, n)
+    xv = (rng.random(n) > 0.15) if nulls else np.ones(n, bool)
+    return key, x, y, xv
+
+
+@pytest.mark.parametrize("n,card", [(1, 1), (50, 7), (100_003, 100), (60_001, 20_000), (1_000_003, 300)])
+@pytest.mark.parametrize("ddof", [0, 1, 2])
+@pytest.mark.parametrize("pred", [False, True])
+def test_var_std_fused_vs_exact(gpu, n, card, ddof, pred):
+    """var / std in one pass (exact sums of x and of x * x's two parts,
+    combined exactly per group): within 1e-12 of the exact two-pass checker,
+    validity exact, the fused path taken (info["var_path"])."""
+    rng = np.random.default_rng(n + card + 7 * ddof + pred)
+    key, x, y, xv = _var_frame(rng, n, card)
+    df = pl.DataFrame({"k": pl.Series.from_numpy("k", key), "x": pl.Series.from_numpy("x", x, xv),
+                       "y": pl.Series.from_numpy("y", y)})
+    lf = df.lazy()
+    sel = np.ones(n, dtype=bool)
+    if pred:
+        lf = lf.filter(pl.col("y") > -1.0)
+        sel = y > -1.0
+    info = {}
+    out = (lf.group_by("k", maintain_order=True)
+           .agg(pl.col("x").var(ddof).alias("xv"), pl.col("x").std(ddof).alias("xsd"),
+                pl.col("y").var(ddof).alias("yv"), pl.col("x").mean().alias("xm"))
+           .collect(info=info))
+    assert info["var_path"] == "fused", info
+    keys, var, std, ok = _oracle(key, x, xv, ddof, sel)
+    assert np.array_equal(out["k"].to_numpy(), keys)
+    assert np.array_equal(out["xv"].validity_numpy(), ok)
+    _close(out["xv"].to_numpy(), var, ok)
+    _close(out["xsd"].to_numpy(), std, ok)
+    _, yvar, _, yok = _oracle(key, y, np.ones(n, bool), ddof, sel)
+    assert np.array_equal(out["yv"].validity_numpy(), yok)
+    _close(out["yv"].to_numpy(), yvar, yok)
+
+
+def test_var_fused_exact_cases(gpu):
+    """Constant groups give exactly 0; a mean of 1e9 with spread 1e-3 keeps
+    full precision (the exact state has no cancellation error); NaN / inf
+    make the group's var NaN; integer columns run as their f64 values;
+    global and multi-key forms."""
+    rng = np.random.default_rng(5)
+    n = 200_000
+    key = rng.integers(0, 50, n).astype(np.int64)
+    const = np.where(key % 2 == 0, 7.25, -3.5)
+    tight = 1e9 + rng.standard_normal(n) * 1e-3
+    sp = rng.standard_normal(n)
+    sp[key == 3] = np.nan
+    sp[(key == 4) & (rng.random(n) < 0.1)] = np.inf
+    iv = rng.integers(-2**40, 2**40, n).astype(np.int64)
+    df = pl.DataFrame({"k": pl.Series.from_numpy("k", key), "c": pl.Series.from_numpy("c", const),
+                       "t": pl.Series.from_numpy("t", tight), "s": pl.Series.from_numpy("s", sp),
+                       "i": pl.Series.from_numpy("i", iv)})
+    info = {}
+    out = (df.lazy().group_by("k", maintain_order=True)
+           .agg(pl.col("c").var().alias("cv"), pl.col("t").var().alias("tv"), pl.col("s").std().alias("ss"),
+                pl.col("i").var(0).alias("iv")).collect(info=info))
+    assert info["var_path"] == "fused"
+    assert out["cv"].to_list() == [0.0] * out.height
+    ones = np.ones(n, bool)
+    # the two-pass checker's rounded mean (error ~ulp(1e9) / 2) shifts every
+    # deviation and costs it ~1e-9 here: check against the exact variance
+    tv_got = out["tv"].to_numpy()
+    for j, kk_ in enumerate(out["k"].to_numpy()[:10]):
+        exact = _exact_var(tight[key == kk_], 1)
+        assert math.isclose(tv_got[j], exact, rel_tol=4e-16), (tv_got[j], exact)
+    _, ss, sstd, sok = _oracle(key, sp, ones, 1, ones)
+    got = out["ss"].to_numpy()
+    kk = out["k"].to_numpy()
+    assert np.isnan(got[kk == 3]).all() and np.isnan(got[kk == 4]).all()
+    fin = (kk != 3) & (kk != 4)
+    _close(got[fin], sstd[fin], sok[fin])
+    _, ivar, _, iok = _oracle(key, iv.astype(np.float64), ones, 0, ones)
+    _close(out["iv"].to_numpy(), ivar, iok)
+    # global var / std and two keys
+    g = df.lazy().select(pl.col("t").var().alias("v"), pl.col("t").std(0).alias("s")).collect(info=(gi := {}))
+    assert gi["var_path"] == "fused"
+    assert math.isclose(g["v"].to_list()[0], _exact_var(tight, 1), rel_tol=4e-16)
+    assert math.isclose(g["s"].to_list()[0], math.sqrt(_exact_var(tight, 0)), rel_tol=4e-16)
+    k2 = (key % 3).astype(np.int64)
+    df2 = pl.DataFrame({"a": pl.Series.from_numpy("a", key), "b": pl.Series.from_numpy("b", k2),
+                        "t": pl.Series.from_numpy("t", tight)})
+    o2 = df2.lazy().group_by("a", "b", maintain_order=True).agg(pl.col("t").var().alias("v")).collect(info=(i2 := {}))
+    assert i2["var_path"] == "fused"
+    for a_, b_, v_ in list(zip(o2["a"].to_list(), o2["b"].to_list(), o2["v"].to_list()))[:12]:
+        assert math.isclose(v_, _exact_var(tight[(key == a_) & (k2 == b_)], 1), rel_tol=4e-16)
+
+
+@pytest.mark.parametrize("case", ["tiny", "huge", "wide"])
+def test_var_fused_out_of_range_falls_back(gpu, case):
+    """Inputs whose exact fused state would leave its range take the two
+    passes (info["var_path"] == "two_pass") and are still right: |x| below
+    2^-484 (x * x's error would be subnormal), x * x overflowing, and values
+    spanning more binades than one sum window."""
+    rng = np.random.default_rng(len(case))
+    n = 30_000
+    key = rng.integers(0, 20, n).astype(np.int64)
+    x = rng.standard_normal(n)
+    if case == "tiny":
+        x *= 1e-150
+    elif case == "huge":
+        x *= 1e160
+    else:
+        x[rng.random(n) < 0.3] *= 1e250
+        x[rng.random(n) < 0.3] *= 1e-250
+    df = pl.DataFrame({"k": pl.Series.from_numpy("k", key), "x": pl.Series.from_numpy("x", x)})
+    info = {}
+    out = df.lazy().group_by("k", maintain_order=True).agg(pl.col("x").var().alias("v")).collect(info=info)
+    assert info["var_path"] == "two_pass", info
+    keys, var, _, ok = _oracle(key, x, np.ones(n, bool), 1, np.ones(n, bool))
+    assert np.array_equal(out["k"].to_numpy(), keys)
+    got = out["v"].to_numpy()
+    assert np.allclose(got[ok], var[ok], rtol=1e-12, atol=0) or case == "huge" and np.isinf(var[ok]).any()

@@ -33,16 +33,20 @@ def main():
     base = df.lazy().filter(pl.col("close") > 250.0).group_by("symbol")
     for name, q in (("sum", base.agg(pl.col("close").sum())), ("std", base.agg(pl.col("close").std())),
                     ("var", base.agg(pl.col("close").var(0)))):
-        out = q.collect()
+        info = {}
+        out = q.collect(info=info)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
+        kms = []
         for _ in range(args.steps):
-            out = q.collect()
+            it = {}
+            out = q.collect(info=it)
+            kms.append(it.get("main_kernel_ms", float("nan")))
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / args.steps
         print(json.dumps({"query": f"filter(close > 250).group_by(symbol).agg(close.{name}())", "rows": n,
-                          "groups": out.height, "ms": round(dt * 1e3, 3),
-                          "Mrows_per_s": round(n / dt / 1e6, 1)}), flush=True)
+                          "groups": out.height, "ms": round(dt * 1e3, 3), "kernel_ms": round(sum(kms) / len(kms), 3),
+                          "path": info.get("var_path"), "Mrows_per_s": round(n / dt / 1e6, 1)}), flush=True)
         del out
 
 
