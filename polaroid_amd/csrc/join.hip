@@ -707,38 +707,63 @@ __global__ __launch_bounds__(256) void aos_pack_kernel(AosCols c, int64_t rows, 
     }
 }
 
-// NP/2 lanes cooperate on one row: each loads 16 bytes (two columns) of
-// it, so one load instruction of a wave fetches whole contiguous rows.
+// Gather of packed rows: a block gathers 256 destination rows per step (NP/2
+// lanes per row, each loading 16 bytes = two columns of it, so one load
+// instruction of a wave fetches whole contiguous rows; non-temporal, the
+// random lines are not reused) into an LDS image held column-major, then
+// stores each column's 256 values as 2 KiB of consecutive 16-byte chunks --
+// the inverse of aos_pack_kernel.  Against 8-byte stores straight from the
+// loading lanes (NC scattered 128-byte segments per store instruction):
+// 58.7 -> 54.6 ms for pack + gather of 1e9 rows x 8 columns by a random
+// index, 50.7 -> 43.3 ms by the identity (profiles/r03_gather_ab.log).
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+
 template <int NC>
 __global__ __launch_bounds__(256) void aos_gather_kernel(const uint64_t* __restrict__ aos,
-                                                         const uint32_t* __restrict__ idx, int64_t n, AosCols c) {
+                                                           const uint32_t* __restrict__ idx, int64_t n, AosCols c) {
     constexpr int NP = (NC + 1) & ~1;
-    constexpr int L = NP / 2;  // lanes per row
-    // K lane-rows per thread per step: the K index loads, then the K row
-    // loads, are issued back to back (the row loads depend on the indices)
-    constexpr int K = 4;
-    const int64_t nl = n * L;
-    const int64_t G = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t0 < nl; t0 += G * K) {
-        int64_t o[K];
-        int q[K];
-        uint32_t r[K];
+    constexpr int L = NP / 2;          // lanes per row
+    constexpr int PER = L;             // 16-B row pieces per thread per 256-row step
+    constexpr int R = 256;             // rows per block step
+    constexpr int CS = R + 2;          // LDS column stride in u64
+    __shared__ __attribute__((aligned(16))) uint64_t img[NP * CS];
+    for (int64_t r0 = (int64_t)blockIdx.x * R; r0 < n; r0 += (int64_t)gridDim.x * R) {
+        const int nrows = n - r0 < R ? (int)(n - r0) : R;
+        uint32_t r[PER];
+        int row[PER], q[PER];
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const int64_t t = t0 + k * G;
-            o[k] = (t < nl ? t : nl - 1) / L;
-            q[k] = (int)((t < nl ? t : nl - 1) - o[k] * L);
-            r[k] = __builtin_nontemporal_load(idx + o[k]);
+        for (int k = 0; k < PER; ++k) {
+            const int t = k * 256 + threadIdx.x;
+            row[k] = t / L;
+            q[k] = t - row[k] * L;
+            r[k] = __builtin_nontemporal_load(idx + r0 + (row[k] < nrows ? row[k] : nrows - 1));
         }
-        ulonglong2 x[K];
+        u64x2 x[PER];
 #pragma unroll
-        for (int k = 0; k < K; ++k) x[k] = reinterpret_cast<const ulonglong2*>(aos + (int64_t)r[k] * NP)[q[k]];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            if (t0 + k * G >= nl) break;
-            __builtin_nontemporal_store(x[k].x, c.dst[2 * q[k]] + o[k]);
-            if (2 * q[k] + 1 < NC) __builtin_nontemporal_store(x[k].y, c.dst[2 * q[k] + 1] + o[k]);
+        for (int k = 0; k < PER; ++k) {
+            const u64x2* src = reinterpret_cast<const u64x2*>(aos + (int64_t)r[k] * NP) + q[k];
+            x[k] = __builtin_nontemporal_load(src);
         }
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            img[(2 * q[k]) * CS + row[k]] = x[k].x;
+            img[(2 * q[k] + 1) * CS + row[k]] = x[k].y;
+        }
+        __syncthreads();
+        if (nrows == R) {
+            // NC columns x R / 2 chunks of two rows
+            for (int j = threadIdx.x; j < NC * (R / 2); j += 256) {
+                const int col = j / (R / 2), p = (j - col * (R / 2)) * 2;
+                const u64x2 v = *reinterpret_cast<const u64x2*>(&img[col * CS + p]);
+                __builtin_nontemporal_store(v, reinterpret_cast<u64x2*>(c.dst[col] + r0 + p));
+            }
+        } else {
+            for (int j = threadIdx.x; j < NC * R; j += 256) {
+                const int col = j / R, p = j - col * R;
+                if (p < nrows) c.dst[col][r0 + p] = img[col * CS + p];
+            }
+        }
+        __syncthreads();
     }
 }
 
