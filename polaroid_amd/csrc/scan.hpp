@@ -68,10 +68,9 @@ __global__ __launch_bounds__(1024) void scan_parts_kernel(uint64_t* __restrict__
     if (threadIdx.x == 0) *total_out = total;
 }
 
-template <typename T>
-__global__ __launch_bounds__(kScanThreads) void scan_apply_kernel(const T* __restrict__ in, int64_t n,
-                                                                  const uint64_t* __restrict__ part,
-                                                                  uint64_t* __restrict__ out) {
+template <typename T, typename O = uint64_t>
+__global__ __launch_bounds__(kScanThreads) void scan_apply_kernel(const T* in, int64_t n,
+                                                                  const uint64_t* __restrict__ part, O* out) {
     __shared__ uint64_t wsum[kScanThreads / 64];
     // thread owns kScanPer consecutive values so the chunk scans in order
     const int64_t base = (int64_t)blockIdx.x * kScanChunk + (int64_t)threadIdx.x * kScanPer;
@@ -88,7 +87,7 @@ __global__ __launch_bounds__(kScanThreads) void scan_apply_kernel(const T* __res
 #pragma unroll
     for (int k = 0; k < kScanPer; ++k) {
         const int64_t i = base + k;
-        if (i < n) out[i] = run;
+        if (i < n) out[i] = (O)run;
         run += v[k];
     }
 }
@@ -103,6 +102,16 @@ static hipError_t scan_exclusive(const T* in, int64_t n, uint64_t* out, uint64_t
     return hipGetLastError();
 }
 
+// In-place exclusive scan of n u32 values whose total stays below 2^32 (the
+// sort's digit counts: n < 2^32 rows): cnt[i] = sum(cnt[0..i)); the total
+// lands in part[nb].  part: scratch of ceil(n / chunk) + 1.
+static hipError_t scan_exclusive32_inplace(uint32_t* cnt, int64_t n, uint64_t* part, hipStream_t s) {
+    const int64_t nb = std::max<int64_t>(1, (n + kScanChunk - 1) / kScanChunk);
+    scan_reduce_kernel<uint32_t><<<(unsigned)nb, kScanThreads, 0, s>>>(cnt, n, part);
+    scan_parts_kernel<<<1, 1024, 0, s>>>(part, nb, part + nb);
+    scan_apply_kernel<uint32_t, uint32_t><<<(unsigned)nb, kScanThreads, 0, s>>>(cnt, n, part, cnt);
+    return hipGetLastError();
+}
 
 }  // namespace
 }  // namespace plgpu

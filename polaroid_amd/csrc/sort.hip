@@ -221,6 +221,9 @@ __global__ __launch_bounds__(256) void srt_tbits_kernel(const uint64_t* __restri
 enum SrtOut { SRT_SEP = 0, SRT_PACK = 1, SRT_IDX = 2 };
 
 // Upsweep: digit counts of every tile, digit-major (cnt[d * ntiles + t]).
+// (A resident grid looping over the tiles, the next tile's keys loaded
+// before this one's counts, measured no faster: 1.63 against 1.56 ms; the
+// same loop made the downsweep slower, 3.9 -> 5.5-6.0 ms: not kept.)
 __global__ __launch_bounds__(kSrtThreads) void srt_upsweep_kernel(const uint64_t* __restrict__ keys, int64_t n,
                                                                   int shift, int64_t ntiles,
                                                                   uint32_t* __restrict__ cnt) {
@@ -244,12 +247,16 @@ __global__ __launch_bounds__(kSrtThreads) void srt_upsweep_kernel(const uint64_t
 // in LDS -- no barriers), then one block-wide combine turns (wave, digit)
 // counts into local positions; the tile is staged in LDS in digit order and
 // written out in runs.  IN_P: input is PACKED.  OUT: SrtOut; a SEP -> PACK
-// transition keeps (code >> cons) & kmask as the remaining code.
+// transition keeps (code >> cons) & kmask as the remaining code.  off: the
+// scanned digit-major counts (u32, n < 2^32; scanned in place).  (A side
+// array of the next pass's digit bytes, written here so the next upsweep
+// reads 1 B instead of 8 per code, cut the upsweep 1.78 -> 0.38 ms but cost
+// every downsweep 1.2 ms of scattered byte stores: not kept.)
 template <bool IN_P, int OUT>
 __global__ __launch_bounds__(kSrtThreads) void srt_downsweep_kernel(const uint64_t* __restrict__ keys_in,
                                                                     const uint32_t* __restrict__ idx_in, int64_t n,
                                                                     int shift, int64_t ntiles,
-                                                                    const uint64_t* __restrict__ off,
+                                                                    const uint32_t* __restrict__ off,
                                                                     uint64_t* __restrict__ keys_out,
                                                                     uint32_t* __restrict__ idx_out, int cons,
                                                                     uint64_t kmask) {
@@ -258,7 +265,11 @@ __global__ __launch_bounds__(kSrtThreads) void srt_downsweep_kernel(const uint64
     constexpr int ROWS = kSrtTile / TH;  // rows of 64 per wave (16)
     __shared__ uint64_t skey[OUT == SRT_IDX ? 1 : kSrtTile];
     __shared__ uint32_t sidx[OUT == SRT_PACK ? 1 : kSrtTile];
-    __shared__ uint8_t sdig[kSrtTile];
+    // packed in and out: a staged code's digit is re-read from the code, so
+    // the digit array is not staged (4 KiB less LDS: 4 workgroups per CU
+    // instead of 3)
+    constexpr bool DIG_FROM_KEY = IN_P && OUT == SRT_PACK;
+    __shared__ uint8_t sdig[DIG_FROM_KEY ? 1 : kSrtTile];
     __shared__ uint32_t dstart[256];
     __shared__ uint64_t gbase[256];  // global position of local slot 0 of each digit run
     __shared__ uint32_t cnt[NW][256];
@@ -273,7 +284,7 @@ __global__ __launch_bounds__(kSrtThreads) void srt_downsweep_kernel(const uint64
     const int m = n - base < kSrtTile ? (int)(n - base) : kSrtTile;
     // this tile's digit offsets (256 scattered words): issued first so their
     // latency hides behind the key loads and the ranking
-    const uint64_t my_off = tid < 256 ? off[(int64_t)tid * ntiles + tile] : 0;
+    const uint64_t my_off = tid < 256 ? (uint64_t)off[(int64_t)tid * ntiles + tile] : 0;
     for (int i = tid; i < NW * 256; i += TH) cnt[i >> 8][i & 255] = 0;
     uint64_t k[ROWS];
     uint32_t rk[ROWS];
@@ -329,7 +340,7 @@ __global__ __launch_bounds__(kSrtThreads) void srt_downsweep_kernel(const uint64
         if (i < m) {
             const uint32_t d = (uint32_t)(k[r] >> shift) & 0xFF;
             const uint32_t pos = dstart[d] + cnt[wid][d] + rk[r];
-            sdig[pos] = (uint8_t)d;
+            if (!DIG_FROM_KEY) sdig[pos] = (uint8_t)d;
             if (IN_P) {
                 if (OUT == SRT_IDX) sidx[pos] = (uint32_t)k[r];
                 else skey[pos] = k[r];
@@ -346,7 +357,8 @@ __global__ __launch_bounds__(kSrtThreads) void srt_downsweep_kernel(const uint64
     __syncthreads();
     // coalesced write-out: consecutive threads, consecutive slots of a digit run
     for (int p = tid; p < m; p += TH) {
-        const uint64_t o = gbase[sdig[p]] + (uint64_t)p;
+        const uint32_t d = DIG_FROM_KEY ? (uint32_t)(skey[p] >> shift) & 0xFF : sdig[p];
+        const uint64_t o = gbase[d] + (uint64_t)p;
         if (OUT != SRT_IDX) keys_out[o] = skey[p];
         if (OUT != SRT_PACK) idx_out[o] = sidx[p];
     }
@@ -431,8 +443,7 @@ using namespace plgpu;
 
 // Scratch of the radix passes over n codes.
 struct SrtScratch {
-    uint32_t* cnt = nullptr;
-    uint64_t* off = nullptr;
+    uint32_t* cnt = nullptr;  // per-tile digit counts, scanned in place into offsets
     uint64_t* part = nullptr;
     unsigned long long* hist = nullptr;
     uint64_t* tbits = nullptr;  // per-tile OR / AND (srt_codes_stats_kernel)
@@ -441,19 +452,16 @@ struct SrtScratch {
         int rc = dev_alloc((void**)&hist, 16, s);
         if (!rc && n > 0 && stats) rc = dev_alloc((void**)&tbits, ntiles * 16, s);
         if (!rc && n > 0) rc = dev_alloc((void**)&cnt, ntiles * 256 * 4, s);
-        if (!rc && n > 0) rc = dev_alloc((void**)&off, (ntiles * 256 + 1) * 8, s);
         if (!rc && n > 0) rc = dev_alloc((void**)&part, ((ntiles * 256 + kScanChunk - 1) / kScanChunk + 1) * 8, s);
         return rc;
     }
     void release(hipStream_t s) {
         dev_free(cnt, s);
-        dev_free(off, s);
         dev_free(part, s);
         dev_free(hist, s);
         dev_free(tbits, s);
         tbits = nullptr;
         cnt = nullptr;
-        off = nullptr;
         part = nullptr;
         hist = nullptr;
     }
@@ -465,7 +473,7 @@ struct SrtScratch {
 // to the PACKED representation as soon as the remaining code bits fit 32.
 template <bool IN_P, int OUT>
 static void srt_down(const uint64_t* ki, const uint32_t* ii, int64_t nv, int shift, int64_t ntiles,
-                     const uint64_t* off, uint64_t* ko, uint32_t* io, int cons, uint64_t kmask, hipStream_t s) {
+                     const uint32_t* off, uint64_t* ko, uint32_t* io, int cons, uint64_t kmask, hipStream_t s) {
     // XCD-aware tiles (round-robin tiles measured slower, profiles/r02_sort_xcd_ab.log)
     srt_downsweep_kernel<IN_P, OUT>
         <<<(unsigned)ntiles, kSrtThreads, 0, s>>>(ki, ii, nv, shift, ntiles, off, ko, io, cons, kmask);
@@ -517,7 +525,7 @@ static int radix_passes(uint64_t* keys[2], uint32_t* idx[2], int64_t nv, int& cu
         const uint32_t* ii = (ids_implicit && j == 0) ? nullptr : idx[cur];
         if (!(pre && j == 0 && S == 0))  // byte-0 counts already in sc.cnt
             srt_upsweep_kernel<<<(unsigned)ntiles, kSrtThreads, 0, s>>>(keys[cur], nv, shift, ntiles, sc.cnt);
-        e = scan_exclusive<uint32_t>(sc.cnt, ntiles * 256, sc.off, sc.part, s);
+        e = scan_exclusive32_inplace(sc.cnt, ntiles * 256, sc.part, s);
         if (e != hipSuccess) return hip_fail(e, "sort scan");
         const bool last = j == nb - 1;
         const int ncons = S + 8;
@@ -529,17 +537,18 @@ static int radix_passes(uint64_t* keys[2], uint32_t* idx[2], int64_t nv, int& cu
             io = final_out;
             *wrote_final = true;
         }
+        const uint32_t* off = sc.cnt;
         if (packed) {
-            if (last) srt_down<true, SRT_IDX>(keys[cur], ii, nv, shift, ntiles, sc.off, ko, io, 0, 0, s);
-            else srt_down<true, SRT_PACK>(keys[cur], ii, nv, shift, ntiles, sc.off, ko, io, 0, 0, s);
+            if (last) srt_down<true, SRT_IDX>(keys[cur], ii, nv, shift, ntiles, off, ko, io, 0, 0, s);
+            else srt_down<true, SRT_PACK>(keys[cur], ii, nv, shift, ntiles, off, ko, io, 0, 0, s);
         } else if (last) {
-            srt_down<false, SRT_IDX>(keys[cur], ii, nv, shift, ntiles, sc.off, ko, io, 0, 0, s);
+            srt_down<false, SRT_IDX>(keys[cur], ii, nv, shift, ntiles, off, ko, io, 0, 0, s);
         } else if (to_pack) {
-            srt_down<false, SRT_PACK>(keys[cur], ii, nv, shift, ntiles, sc.off, ko, io, ncons, kmask, s);
+            srt_down<false, SRT_PACK>(keys[cur], ii, nv, shift, ntiles, off, ko, io, ncons, kmask, s);
             packed = true;
             cons = ncons;
         } else {
-            srt_down<false, SRT_SEP>(keys[cur], ii, nv, shift, ntiles, sc.off, ko, io, 0, 0, s);
+            srt_down<false, SRT_SEP>(keys[cur], ii, nv, shift, ntiles, off, ko, io, 0, 0, s);
         }
         e = hipGetLastError();
         if (e != hipSuccess) return hip_fail(e, "sort pass");
