@@ -205,7 +205,8 @@ typedef struct plgpu_groupby_info {
     int32_t sum_inexact;         /* bit i: f64 sum acc i rounded below window  */
     int64_t table_capacity;      /* global hash-table slots                    */
     double main_kernel_ms;       /* device time of the aggregation kernel(s)   */
-    int32_t path;                /* 0 generic, 1 fast, 2 fast sum-only, 3 partitioned */
+    int32_t path;                /* 0 generic, 1 fast, 2 fast sum-only, 3 partitioned,
+                                    4 fast variance triple (one var / std column)   */
     int32_t sum_limbs;           /* 40-bit LDS limbs per f64 sum (2 or 3)      */
     int32_t local_range;         /* 1: range-local fused kernel (clustered keys) */
     int32_t register_runs;       /* 1: fused kernel with per-lane register runs (sorted keys) */

@@ -1061,10 +1061,15 @@ __device__ __forceinline__ void fast_share(const int32_t (&vf)[NACC > 0 ? NACC :
 // DERIV: some accs are derived inputs (x op y, AccSpec.dop), computed in
 // registers from the loaded operand columns as each row is applied.
 template <int NACC, int PRED, bool SUMONLY, int ROWS, int LIMBS = 3, bool RUNS = false, bool PART = false,
-          bool DERIV = false>
+          bool DERIV = false, bool VAR = false>
 __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProgram prog) {
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
     constexpr int NA = NACC > 0 ? NACC : 1;
+    // VAR (sum-only, NACC 3): the fused variance's three sums of one column
+    // x -- x, h = x * x and l = fma(x, x, -h) -- with h and l computed from
+    // x's registers: one column loaded, no operand registers per acc
+    static_assert(!VAR || (NACC == 3 && SUMONLY && !DERIV), "VAR: three sums of one column");
+    constexpr int NL = VAR ? 1 : NACC;  // accs whose column the tile loads
     // SLIM (sum-only, 2 limbs): LDS fields key 0, len 1, acc a: limbs
     // 2+3a, 3+3a, flags 4+3a (the unused low limb of the 3-limb layout is
     // not stored, so more workgroups fit per CU)
@@ -1121,9 +1126,9 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
         t = blockIdx.x % p.part_blocks;
         tstep = p.part_blocks;
     }
-    auto load_tile = [&](int64_t tt, FastTile<NACC, ROWS, DERIV>& x) {
-        if (PART || tt < ntiles) fast_load<NACC, PRED, ROWS, true, DERIV>(p, tt, x, rbase, rmax);
-        else fast_load_tail<NACC, PRED, ROWS, DERIV>(p, tt, x);
+    auto load_tile = [&](int64_t tt, FastTile<NL, ROWS, DERIV>& x) {
+        if (PART || tt < ntiles) fast_load<NL, PRED, ROWS, true, DERIV>(p, tt, x, rbase, rmax);
+        else fast_load_tail<NL, PRED, ROWS, DERIV>(p, tt, x);
     };
     constexpr uint32_t VM = (1u << NACC) - 1u;
     // RACC (partition buffers, sum-only, 2 limbs): each lane keeps KR
@@ -1255,10 +1260,10 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
         }
         return true;
     };
-    FastTile<NACC, ROWS, DERIV> cur;
+    FastTile<NL, ROWS, DERIV> cur;
     if (t < nall) load_tile(t, cur);
     for (; t < nall; t += tstep) {
-        fast_share<NACC, ROWS, DERIV>(vf0, wf0, cur);
+        if constexpr (!VAR) fast_share<NACC, ROWS, DERIV>(vf0, wf0, cur);
         // ---- predicate + batched LDS probes of the tile's rows
         int slot[ROWS];
         uint64_t probe[ROWS];
@@ -1268,9 +1273,13 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
             bool sel = true;
             if (PRED == 1) {
                 uint64_t x = cur.pv[j];
+                if (VAR) {
+                    if (p.pred_acc >= 0) x = cur.v[0][j];  // every acc reads x's column
+                } else {
 #pragma unroll
-                for (int a = 0; a < NACC; ++a)
-                    if (a == p.pred_acc) x = cur.v[a][j];
+                    for (int a = 0; a < NACC; ++a)
+                        if (a == p.pred_acc) x = cur.v[a][j];
+                }
                 sel = simple_pred(prog.simple_isf, prog.simple_op, x, prog.simple_imm);
             }
             if (PART) {
@@ -1287,7 +1296,7 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
         for (int j = 0; j < ROWS; ++j)
             if (slot[j] == kGlobalKey && probe[j] == cur.key[j]) slot[j] = (int)h[j];
         // ---- next tile's loads go out before this tile's atomics
-        FastTile<NACC, ROWS, DERIV> nxt;
+        FastTile<NL, ROWS, DERIV> nxt;
         const int64_t tn = t + tstep;
         if (tn < nall) load_tile(tn, nxt);
         // ---- apply rows one at a time (rolled; arrays shift statically)
@@ -1301,9 +1310,13 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
                 int bot[NA];
 #pragma unroll
                 for (int a = 0; a < NA; ++a) {
-                    rv[a] = cur.v[a][0];
-                    if (DERIV && dop0[a] != DOP_NONE)
-                        rv[a] = derive(dop0[a], cur.v[a][0], (dop0[a] & DOP_LIT) ? dim0[a] : cur.w[a][0]);
+                    if (VAR) {
+                        rv[a] = a == 0 ? cur.v[0][0] : derive(a == 1 ? DOP_SQHI : DOP_SQLO, cur.v[0][0], 0ull);
+                    } else {
+                        rv[a] = cur.v[a][0];
+                        if (DERIV && dop0[a] != DOP_NONE)
+                            rv[a] = derive(dop0[a], cur.v[a][0], (dop0[a] & DOP_LIT) ? dim0[a] : cur.w[a][0]);
+                    }
                     dd[a] = dd0[a];
                     bot[a] = bot0[a];
                 }
@@ -1412,7 +1425,7 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
                 slot[i] = slot[i + 1];
                 cur.key[i] = cur.key[i + 1];
 #pragma unroll
-                for (int a = 0; a < NACC; ++a) {
+                for (int a = 0; a < NL; ++a) {
                     cur.v[a][i] = cur.v[a][i + 1];
                     if (DERIV) cur.w[a][i] = cur.w[a][i + 1];
                 }
@@ -1630,7 +1643,8 @@ constexpr int kPlanBlocks = 16;
 constexpr int kPlanKeyBlocks = 128;
 
 __global__ __launch_bounds__(kPlanThreads) void gb_plan_kernel(GbParams p, uint64_t* __restrict__ gset,
-                                                               int64_t samples) {
+                                                               int64_t samples, int32_t psimple, int32_t pisf,
+                                                               int32_t pop, uint64_t pimm) {
     __shared__ uint64_t set[kPlanSetSlots];
     __shared__ uint32_t red[2][kPlanThreads / 64];
     const bool key_task = (int)blockIdx.x >= p.nacc * kPlanBlocks;
@@ -1715,6 +1729,7 @@ __global__ __launch_bounds__(kPlanThreads) void gb_plan_kernel(GbParams p, uint6
     }
     const AccSpec& ac = p.acc[a];
     uint32_t mx = 0, mn = 0x7FF;
+    const bool sqlo = ac.dop != DOP_NONE && (ac.dop & DOP_OPMASK) == DOP_SQLO;
     if (ac.flags & (A_FSUM | A_FSUMCAST)) {
         for (int64_t i0 = s0 + threadIdx.x; i0 < s1; i0 += (int64_t)blockDim.x * kPlanBatch) {
             uint64_t xb[kPlanBatch];
@@ -1725,6 +1740,10 @@ __global__ __launch_bounds__(kPlanThreads) void gb_plan_kernel(GbParams p, uint6
                 const int64_t r = plan_row(i, n, samples);
                 bool v = false;
                 xb[u] = (i < s1 && r < n) ? acc_value(ac, r, v) : 0;
+                // a simple predicate (col <cmp> literal): only the rows the
+                // sums will take shape their windows
+                if (psimple && i < s1 && r < n)
+                    v = v && dev_valid(p.pred_col, r) && simple_pred(pisf, pop, dev_load(p.pred_col, r), pimm);
                 okb[u] = i < s1 && r < n && v;
             }
 #pragma unroll
@@ -1735,7 +1754,17 @@ __global__ __launch_bounds__(kPlanThreads) void gb_plan_kernel(GbParams p, uint6
                 const uint32_t ex = (uint32_t)(x >> 52) & 0x7FF;
                 if (ex != 0x7FF && ex > mx) mx = ex;
                 // smallest exponent of a nonzero finite value (subnormals: 0)
-                if ((x & 0x7fffffffffffffffull) != 0 && ex != 0x7FF && ex < mn) mn = ex;
+                uint32_t el = ex;
+                if (sqlo && ex != 0) {
+                    // the error term l = fma(x, x, -x * x) of a fused
+                    // variance: its set bits end at the lowest bit of x * x,
+                    // wherever its leading bit falls (its magnitude spreads
+                    // over ~20 binades below ulp(x * x) / 2), so the 2-limb
+                    // test takes the exponent its lowest set bit implies
+                    const uint64_t m = (x & 0x000FFFFFFFFFFFFFull) | (1ull << 52);
+                    el = ex + (uint32_t)__builtin_ctzll(m);
+                }
+                if ((x & 0x7fffffffffffffffull) != 0 && ex != 0x7FF && el < mn) mn = el;
             }
         }
     }
@@ -2225,6 +2254,7 @@ struct Plan {
     bool local;        // range-local mode: contiguous tiles per workgroup, LDS sized by range-local keys
     mutable int launched_grid;  // grid of the last fast launch (info)
     mutable bool launched_runs = false;  // that launch used the register-run variant (info)
+    mutable bool launched_var = false;   // that launch was the variance-triple variant (info)
 };
 
 // One aggregation input (plan_groupby): a column, or a derived value x op y
@@ -2500,10 +2530,10 @@ static int resident_per_cu(const void* kern, int threads, size_t lds) {
     return nb;
 }
 
-template <int NACC, int PRED, bool SUMONLY, int LIMBS = 3, bool RUNS = false, bool DERIV = false>
+template <int NACC, int PRED, bool SUMONLY, int LIMBS = 3, bool RUNS = false, bool DERIV = false, bool VAR = false>
 static hipError_t launch_fast_rows(const Plan& pl, const DevProgram& dp, hipStream_t s) {
     constexpr int ROWS = 2;
-    const void* kern = (const void*)gb_fast_kernel<NACC, PRED, SUMONLY, ROWS, LIMBS, RUNS, false, DERIV>;
+    const void* kern = (const void*)gb_fast_kernel<NACC, PRED, SUMONLY, ROWS, LIMBS, RUNS, false, DERIV, VAR>;
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -2520,6 +2550,7 @@ static hipError_t launch_fast_rows(const Plan& pl, const DevProgram& dp, hipStre
     const int grid = (int)g;
     pl.launched_grid = grid;
     pl.launched_runs = RUNS;
+    pl.launched_var = VAR;
     GbParams q = pl.p;
     q.tiles_per_wg = 0;
     if (pl.local) {
@@ -2527,7 +2558,7 @@ static hipError_t launch_fast_rows(const Plan& pl, const DevProgram& dp, hipStre
         const int64_t nall = pl.p.n_full / tile + (pl.p.n > pl.p.n_full ? 1 : 0);
         q.tiles_per_wg = (int32_t)((nall + grid - 1) / grid);
     }
-    gb_fast_kernel<NACC, PRED, SUMONLY, ROWS, LIMBS, RUNS, false, DERIV><<<grid, kGbThreads, lds, s>>>(q, dp);
+    gb_fast_kernel<NACC, PRED, SUMONLY, ROWS, LIMBS, RUNS, false, DERIV, VAR><<<grid, kGbThreads, lds, s>>>(q, dp);
     return hipGetLastError();
 }
 
@@ -2547,9 +2578,32 @@ static hipError_t launch_fast_nacc(const Plan& pl, const DevProgram& dp, int pre
     return pred == 0 ? launch_fast<NACC, 0, false, DERIV>(pl, dp, s) : launch_fast<NACC, 1, false, DERIV>(pl, dp, s);
 }
 
+// The fused variance's triple (x, x * x, its error: three sums of one
+// column, the derived two sharing x's load) on the sum-only layout.
+static bool var_triple(const Plan& pl) {
+    const GbParams& p = pl.p;
+    if (!pl.sum_only || p.nacc != 3) return false;
+    const AccSpec& a0 = p.acc[0];
+    for (int a = 1; a < 3; ++a) {
+        const AccSpec& ac = p.acc[a];
+        if (ac.dop != ((a == 1 ? DOP_SQHI : DOP_SQLO) | DOP_LIT) || ac.c.values != a0.c.values ||
+            ac.c.offset != a0.c.offset || ac.c.validity != a0.c.validity || ac.c.dtype != a0.c.dtype)
+            return false;
+    }
+    return a0.dop == DOP_NONE && a0.c.dtype == PLGPU_F64;
+}
+
+template <int PRED>
+static hipError_t launch_fast_var(const Plan& pl, const DevProgram& dp, hipStream_t s) {
+    if (pl.limbs == 2) return launch_fast_rows<3, PRED, true, 2, false, false, true>(pl, dp, s);
+    return launch_fast_rows<3, PRED, true, 3, false, false, true>(pl, dp, s);
+}
+
 static hipError_t launch_fast_dispatch(const Plan& pl, const DevProgram& dp, int pred, hipStream_t s) {
     bool dv = false;
     for (int a = 0; a < pl.p.nacc; ++a) dv = dv || pl.p.acc[a].dop != DOP_NONE;
+    if (dv && var_triple(pl) && !pl.runs)
+        return pred == 0 ? launch_fast_var<0>(pl, dp, s) : launch_fast_var<1>(pl, dp, s);
     if (dv) {
         switch (pl.p.nacc) {
         case 1: return launch_fast_nacc<1, true>(pl, dp, pred, s);
@@ -2899,11 +2953,27 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
     Plan& pl = R.pl;
     GbParams& p = pl.p;
     const int64_t n = p.n;
-    gb_plan_kernel<<<p.nacc * kPlanBlocks + kPlanKeyBlocks, kPlanThreads, 0, R.s>>>(p, R.status + kPlanSetWord,
-                                                                                   kPlanSamples);
+    // a simple predicate filters the sampled values, so the windows (and
+    // the 2-limb choice) follow the rows the sums take; when some summed
+    // column has no selected nonzero value in the sample, its acc tasks run
+    // again unfiltered (the key task is not repeated)
+    const bool ps = R.pred == 1;
+    gb_plan_kernel<<<p.nacc * kPlanBlocks + kPlanKeyBlocks, kPlanThreads, 0, R.s>>>(
+        p, R.status + kPlanSetWord, kPlanSamples, ps ? 1 : 0, ps ? R.dp.simple_isf : 0, ps ? R.dp.simple_op : 0,
+        ps ? R.dp.simple_imm : 0ull);
     PLGPU_HIP(hipGetLastError());
     PLGPU_HIP(hipMemcpyAsync(R.st, R.status, sizeof R.st, hipMemcpyDeviceToHost, R.s));
     PLGPU_HIP(hipStreamSynchronize(R.s));
+    bool unsampled = false;
+    for (int a = 0; a < p.nacc; ++a)
+        if ((p.acc[a].flags & (A_FSUM | A_FSUMCAST)) && R.st[ST_MAXEX + a] == 0) unsampled = true;
+    if (ps && unsampled) {
+        gb_plan_kernel<<<p.nacc * kPlanBlocks, kPlanThreads, 0, R.s>>>(p, R.status + kPlanSetWord, kPlanSamples, 0,
+                                                                       0, 0, 0ull);
+        PLGPU_HIP(hipGetLastError());
+        PLGPU_HIP(hipMemcpyAsync(R.st, R.status, sizeof R.st, hipMemcpyDeviceToHost, R.s));
+        PLGPU_HIP(hipStreamSynchronize(R.s));
+    }
     R.st[ST_SAMPLED] = (uint64_t)std::min<int64_t>(n, kPlanSamples);
     // sorted / clustered keys: the fused kernel's lanes keep a register
     // accumulator (option "runs" = 0 / 1 forces the choice in tests)
@@ -3309,13 +3379,14 @@ static int gb_main(GbRun& R, bool auto_refit, bool* refit, int32_t* hint) {
             fprintf(stderr,
                     "[plgpu] gb attempt %d: n=%lld grid=%d/%d lds=%d lcap=%d gcap=%lld nfields=%d lds_bytes=%zu "
                     "fast=%lld sumonly=%d distinct=%llu/%llu newkeys=%llu special=%llu global_rows=%llu full=%llu "
-                    "selected=%llu fx=%llx\n",
+                    "selected=%llu fx=%llx limbs=%d runs=%d nacc=%d\n",
                     R.attempts, (long long)n, pl.grid, pl.fast_grid, (int)pl.use_lds, p.lcap, (long long)p.gcap,
                     p.nfields, pl.lds_bytes, (long long)p.n_full, (int)pl.sum_only,
                     (unsigned long long)R.st[ST_DISTINCT], (unsigned long long)R.st[ST_SAMPLED],
                     (unsigned long long)R.st[ST_NEWKEYS], (unsigned long long)R.st[ST_SPECIAL],
                     (unsigned long long)R.st[ST_GLOBAL_ROWS], (unsigned long long)R.st[ST_TABLE_FULL],
-                    (unsigned long long)R.st[ST_SELECTED], (unsigned long long)R.st[ST_FXFLAGS]);
+                    (unsigned long long)R.st[ST_SELECTED], (unsigned long long)R.st[ST_FXFLAGS], pl.limbs, (int)pl.runs,
+                    p.nacc);
         }
         bool again = false;
         if (R.st[ST_TABLE_FULL] > 0) {
@@ -3389,7 +3460,7 @@ static void gb_fill_info(const GbRun& R, plgpu_groupby_info* info) {
     info->grid = p.n_full > 0 ? R.pl.launched_grid : R.pl.grid;
     info->table_capacity = p.gcap;
     info->main_kernel_ms = R.ms;
-    info->path = R.part ? 3 : (p.n_full > 0 ? (R.pl.sum_only ? 2 : 1) : 0);
+    info->path = R.part ? 3 : (p.n_full > 0 ? (R.pl.launched_var ? 4 : (R.pl.sum_only ? 2 : 1)) : 0);
     info->sum_limbs = (p.n_full > 0 || R.part) && R.pl.sum_only ? R.pl.limbs : 3;
     info->local_range = R.pl.local ? 1 : 0;
     info->register_runs = p.n_full > 0 && !R.part && R.pl.launched_runs ? 1 : 0;

@@ -263,3 +263,80 @@ def test_var_fused_out_of_range_falls_back(gpu, case):
     assert np.array_equal(out["k"].to_numpy(), keys)
     got = out["v"].to_numpy()
     assert np.allclose(got[ok], var[ok], rtol=1e-12, atol=0) or case == "huge" and np.isinf(var[ok]).any()
+
+
+@pytest.mark.parametrize("n", [1, 1023, 1024, 1025, 100_003, 1_000_003])
+@pytest.mark.parametrize("pred", ["none", "on_x", "other"])
+@pytest.mark.parametrize("kind", ["var0", "std1"])
+def test_var_single_column_triple_kernel(gpu, n, pred, kind):
+    """One var / std column as the only aggregation (no maintain_order): the
+    fused kernel's variance-triple variant (info["path"] == 4: x loaded once,
+    x * x and its exact error computed in registers), on the 2-limb window
+    here, across the masked tail tile, with no predicate, a predicate on x
+    itself (the predicate reuses x's registers) and on another column;
+    within 1e-12 of the two-pass checker, validity exact."""
+    rng = np.random.default_rng(n + len(pred) + len(kind))
+    key = rng.integers(0, 100, n).astype(np.int64)
+    x = 250 + rng.random(n) * 250
+    y = rng.uniform(-5, 5, n)
+    df = pl.DataFrame({"k": pl.Series.from_numpy("k", key), "x": pl.Series.from_numpy("x", x),
+                       "y": pl.Series.from_numpy("y", y)})
+    lf, sel = df.lazy(), np.ones(n, dtype=bool)
+    if pred == "on_x":
+        lf, sel = lf.filter(pl.col("x") > 300.0), x > 300.0
+    elif pred == "other":
+        lf, sel = lf.filter(pl.col("y") > -1.0), y > -1.0
+    ddof = int(kind[-1])
+    e = pl.col("x").var(ddof) if kind.startswith("var") else pl.col("x").std(ddof)
+    info = {}
+    out = lf.group_by("k").agg(e.alias("v")).collect(info=info)
+    assert info["var_path"] == "fused"
+    if n >= 1024:
+        assert info["path"] == 4, info
+    keys, var, std, ok = _oracle(key, x, np.ones(n, bool), ddof, sel)
+    order = np.argsort(keys)
+    got_k = out["k"].to_numpy()
+    go = np.argsort(got_k)
+    assert np.array_equal(got_k[go], keys[order])
+    want = (var if kind.startswith("var") else std)[order]
+    okk = ok[order]
+    assert np.array_equal(out["v"].validity_numpy()[go], okk)
+    _close(out["v"].to_numpy()[go], want, okk)
+
+
+@pytest.mark.parametrize("spread", ["narrow", "wide"])
+def test_var_triple_kernel_windows(gpu, spread):
+    """The variance-triple kernel on both windows: values spanning few
+    binades run on 2 limbs; values from 1e-3 to 1e3 (x * x over ~40 binades)
+    on 3 limbs; both exact within 1e-12, the same kernel variant."""
+    rng = np.random.default_rng(11 if spread == "narrow" else 12)
+    n = 300_001
+    key = rng.integers(0, 37, n).astype(np.int64)
+    if spread == "narrow":
+        x = 1e6 + rng.standard_normal(n) * 3.0
+    else:
+        x = np.exp(rng.uniform(np.log(1e-3), np.log(1e3), n)) * np.where(rng.random(n) < 0.5, -1, 1)
+    df = pl.DataFrame({"k": pl.Series.from_numpy("k", key), "x": pl.Series.from_numpy("x", x)})
+    info = {}
+    out = df.lazy().group_by("k").agg(pl.col("x").var().alias("v")).collect(info=info)
+    assert info["var_path"] == "fused" and info["path"] == 4, info
+    assert info["sum_limbs"] == (2 if spread == "narrow" else 3), info
+    got = dict(zip(out["k"].to_list(), out["v"].to_list()))
+    for k in range(37):
+        assert math.isclose(got[k], _exact_var(x[key == k], 1), rel_tol=1e-12), k
+
+
+def test_var_triple_sorted_keys_take_the_register_run_path(gpu):
+    """Symbol-sorted rows: the plan picks the register-run kernel (the
+    variance triple is not used there) and the result is the same."""
+    rng = np.random.default_rng(3)
+    n = 200_000
+    key = np.sort(rng.integers(0, 50, n)).astype(np.int64)
+    x = 100 + rng.random(n)
+    df = pl.DataFrame({"k": pl.Series.from_numpy("k", key), "x": pl.Series.from_numpy("x", x)})
+    info = {}
+    out = df.lazy().group_by("k").agg(pl.col("x").std().alias("s")).collect(info=info)
+    assert info["var_path"] == "fused" and info["path"] != 4
+    got = dict(zip(out["k"].to_list(), out["s"].to_list()))
+    for k in np.unique(key)[:20]:
+        assert math.isclose(got[int(k)], math.sqrt(_exact_var(x[key == k], 1)), rel_tol=1e-12)
