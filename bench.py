@@ -52,6 +52,7 @@ def parse():
                     help="rows of the plugin leg (host Arrow frame through execute_with_polaroid; configs[1] = 1e8)")
     ap.add_argument("--no-plugin", action="store_true")
     ap.add_argument("--no-vwap", action="store_true")
+    ap.add_argument("--no-std", action="store_true")
     ap.add_argument("--dry-run", action="store_true",
                     help="print this rank's launch parameters and exit before touching the GPU (tests)")
     return ap.parse_args()
@@ -172,6 +173,29 @@ def plugin_leg(rows: int, groups: int) -> dict:
                     "host link + query, warm = scanned columns resident (ColumnCache); result to Arrow"}
 
 
+def timed_leg(torch, q, n: int, steps: int, warmup: int, bytes_per_row: int) -> dict:
+    """Wall time per collect() of a resident-frame query and the mean HIP-event
+    time of its aggregation kernel, with the kernel's HBM fraction at the
+    query's algorithmic bytes per row."""
+    for _ in range(warmup):
+        q.collect()
+    torch.cuda.synchronize()
+    kms = []
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        info = {}
+        out = q.collect(info=info)
+        kms.append(info.get("main_kernel_ms", float("nan")))
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    k = float(np.mean(kms))
+    achieved = bytes_per_row * n / (k * 1e-3) / 1e9
+    assert 0 < out.height <= n
+    return {"rows": n, "ms_per_step": round(dt * 1e3, 3), "Mrows_s": round(n / dt / 1e6, 1),
+            "kernel_ms": round(k, 4), "bytes_per_row": bytes_per_row, "achieved_GBs": round(achieved, 1),
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "path": info.get("path")}
+
+
 def vwap_leg(torch, pl, df, sym, close, steps: int, warmup: int) -> dict:
     """VWAP over the same resident frame: filter(close > 250).group_by(symbol)
     .agg((close * volume).sum(), volume.sum()); the product is computed in the
@@ -189,26 +213,20 @@ def vwap_leg(torch, pl, df, sym, close, steps: int, warmup: int) -> dict:
                         pl.Series.from_torch("volume", vol)])
     q = vdf.lazy().filter(pl.col("close") > THRESHOLD).group_by("symbol").agg(
         (pl.col("close") * pl.col("volume")).sum().alias("pv"), pl.col("volume").sum().alias("v"))
-    for _ in range(warmup):
-        q.collect()
-    torch.cuda.synchronize()
-    kms = []
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        info = {}
-        out = q.collect(info=info)
-        kms.append(info.get("main_kernel_ms", float("nan")))
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / steps
-    k = float(np.mean(kms))
-    achieved = 24 * n / (k * 1e-3) / 1e9
-    assert 0 < out.height <= n
+    r = timed_leg(torch, q, n, steps, warmup, 24)
     del vdf, vol
     return {"query": "filter(close > 250).group_by(symbol).agg((close * volume).sum(), volume.sum())",
-            "rows": n, "ms_per_step": round(dt * 1e3, 3), "Mrows_s": round(n / dt / 1e6, 1),
-            "kernel": "gb_fast_kernel<NACC=2,PRED=1,SUMONLY,DERIV> (close * volume in registers)",
-            "kernel_ms": round(k, 4), "bytes_per_row": 24, "achieved_GBs": round(achieved, 1),
-            "frac": round(achieved / HBM_PEAK_GBS, 4)}
+            "kernel": "gb_fast_kernel<NACC=2,PRED=1,SUMONLY,DERIV> (close * volume in registers)", **r}
+
+
+def std_leg(torch, pl, df, steps: int, warmup: int) -> dict:
+    """close.std() per symbol over the same resident frame (one fused pass:
+    exact sums of x, x * x and its error, DESIGN.md "var / std in one pass");
+    algorithmic bytes key + close = 16 B/row.  rank 0, N = 1."""
+    q = df.lazy().filter(pl.col("close") > THRESHOLD).group_by("symbol").agg(pl.col("close").std().alias("sd"))
+    r = timed_leg(torch, q, df.height, steps, warmup, 16)
+    return {"query": "filter(close > 250).group_by(symbol).agg(close.std())",
+            "kernel": "gb_fast_kernel<NACC=3,PRED=1,SUMONLY,VAR> (variance triple)", **r}
 
 
 def load_traffic(n_rows: int):
@@ -363,6 +381,8 @@ def main():
         result["cpu_baseline"] = cpu_baseline(int(args.cpu_rows), args.groups, args.cpu_seconds)
     if rank == 0 and world == 1 and not args.no_vwap:
         result["vwap"] = vwap_leg(torch, pl, df, sym, cols["close"], args.steps, args.warmup)
+    if rank == 0 and world == 1 and not args.no_std:
+        result["std"] = std_leg(torch, pl, df, args.steps, args.warmup)
     if rank == 0 and world == 1 and not args.no_plugin:
         del df, query, out, sym, cols
         torch.cuda.empty_cache()

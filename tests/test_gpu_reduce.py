@@ -187,6 +187,41 @@ def test_fused_derived_sum_only_vwap(gpu):
         _compare(out, "k", okeys, oouts, ["pv", "v"])
 
 
+@pytest.mark.parametrize("n", [1025, 100_003, 1_000_001])
+@pytest.mark.parametrize("form", ["one_acc", "vwap", "three_accs", "literal"])
+@pytest.mark.parametrize("pred", ["none", "on_a", "on_b", "other"])
+def test_derived_forms_over_two_columns(gpu, n, form, pred):
+    """Sum / mean aggregations whose inputs are drawn from two Float64 columns
+    a, b -- a op b, b op a, a op literal, a or b itself -- on the sum-only
+    fused kernel (path 2) with the predicate on a, on b (the predicate reuses
+    an operand's registers) or on a third column, across the masked tail
+    tile; bit-exact against the oracle."""
+    rng = np.random.default_rng(n + len(form) * 3 + len(pred))
+    k = rng.integers(0, 64, n).astype(np.int64)
+    a = rng.uniform(100, 200, n)
+    b = rng.uniform(1e3, 1e5, n)
+    c = rng.uniform(-1, 1, n)
+    df = pl.DataFrame({"k": pl.Series.from_numpy("k", k), "a": pl.Series.from_numpy("a", a),
+                       "b": pl.Series.from_numpy("b", b), "c": pl.Series.from_numpy("c", c)})
+    forms = {
+        "one_acc": [("sum", col("a") - col("b"))],
+        "vwap": [("sum", col("a") * col("b")), ("sum", col("b"))],
+        "three_accs": [("sum", col("b") / col("a")), ("mean", col("a")), ("sum", col("b") + col("a"))],
+        "literal": [("sum", col("a") * 2.5), ("mean", col("b") - col("a"))],
+    }[form]
+    p = {"none": None, "on_a": col("a") > 150.0, "on_b": col("b") < 5e4, "other": col("c") > 0.0}[pred]
+    lf = df.lazy()
+    if p is not None:
+        lf = lf.filter(p)
+    names = [f"o{i}" for i in range(len(forms))]
+    info = {}
+    out = lf.group_by("k").agg(*[getattr(e, op)().alias(nm) for (op, e), nm in zip(forms, names)]).collect(info=info)
+    assert info["path"] == 2, info
+    cols = {"k": (k, None), "a": (a, None), "b": (b, None), "c": (c, None)}
+    okeys, _, oouts = _oracle(cols, ["k", "a", "b", "c"], "k", forms, p, n)
+    _compare(out, "k", okeys, oouts, names)
+
+
 def test_derived_inputs_off_the_fused_path(gpu):
     """Nullable operands (generic kernel), many groups (partitioned path),
     several keys and a String key: the fused inputs are materialised there,
