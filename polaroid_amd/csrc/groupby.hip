@@ -1068,7 +1068,7 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
     // VAR (sum-only, NACC 3): the fused variance's three sums of one column
     // x -- x, h = x * x and l = fma(x, x, -h) -- with h and l computed from
     // x's registers: one column loaded, no operand registers per acc
-    static_assert(!VAR || (NACC == 3 && SUMONLY && !DERIV), "VAR: three sums of one column");
+    static_assert(!VAR || (NACC == 3 && !DERIV), "VAR: three sums of one column");
     constexpr int NL = VAR ? 1 : NACC;  // accs whose column the tile loads
     // SLIM (sum-only, 2 limbs): LDS fields key 0, len 1, acc a: limbs
     // 2+3a, 3+3a, flags 4+3a (the unused low limb of the 3-limb layout is
@@ -2579,10 +2579,11 @@ static hipError_t launch_fast_nacc(const Plan& pl, const DevProgram& dp, int pre
 }
 
 // The fused variance's triple (x, x * x, its error: three sums of one
-// column, the derived two sharing x's load) on the sum-only layout.
+// column, the derived two sharing x's load), on the sum-only layout or the
+// general one (maintain_order's first-row field, x's count).
 static bool var_triple(const Plan& pl) {
     const GbParams& p = pl.p;
-    if (!pl.sum_only || p.nacc != 3) return false;
+    if (p.nacc != 3) return false;
     const AccSpec& a0 = p.acc[0];
     for (int a = 1; a < 3; ++a) {
         const AccSpec& ac = p.acc[a];
@@ -2595,6 +2596,7 @@ static bool var_triple(const Plan& pl) {
 
 template <int PRED>
 static hipError_t launch_fast_var(const Plan& pl, const DevProgram& dp, hipStream_t s) {
+    if (!pl.sum_only) return launch_fast_rows<3, PRED, false, 3, false, false, true>(pl, dp, s);
     if (pl.limbs == 2) return launch_fast_rows<3, PRED, true, 2, false, false, true>(pl, dp, s);
     return launch_fast_rows<3, PRED, true, 3, false, false, true>(pl, dp, s);
 }

@@ -304,6 +304,28 @@ def test_var_single_column_triple_kernel(gpu, n, pred, kind):
     _close(out["v"].to_numpy()[go], want, okk)
 
 
+@pytest.mark.parametrize("n", [1025, 100_003, 1_000_003])
+@pytest.mark.parametrize("pred", [False, True])
+def test_var_triple_kernel_maintain_order(gpu, n, pred):
+    """maintain_order=True (the first-row field: not the sum-only layout):
+    one std column still runs the variance-triple variant (path 4), groups in
+    first-occurrence order, within 1e-12 of the two-pass checker."""
+    rng = np.random.default_rng(n + pred)
+    key = rng.integers(0, 100, n).astype(np.int64)
+    x = 250 + rng.random(n) * 250
+    df = pl.DataFrame({"k": pl.Series.from_numpy("k", key), "x": pl.Series.from_numpy("x", x)})
+    lf, sel = df.lazy(), np.ones(n, dtype=bool)
+    if pred:
+        lf, sel = lf.filter(pl.col("x") < 450.0), x < 450.0
+    info = {}
+    out = lf.group_by("k", maintain_order=True).agg(pl.col("x").std().alias("s")).collect(info=info)
+    assert info["var_path"] == "fused" and info["path"] == 4, info
+    keys, _, std, ok = _oracle(key, x, np.ones(n, bool), 1, sel)
+    assert np.array_equal(out["k"].to_numpy(), keys)
+    assert np.array_equal(out["s"].validity_numpy(), ok)
+    _close(out["s"].to_numpy(), std, ok)
+
+
 @pytest.mark.parametrize("spread", ["narrow", "wide"])
 def test_var_triple_kernel_windows(gpu, spread):
     """The variance-triple kernel on both windows: values spanning few

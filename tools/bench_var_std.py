@@ -19,6 +19,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=float, default=1e9)
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--maintain-order", action="store_true")
     args = ap.parse_args()
     import torch
 
@@ -30,7 +31,7 @@ def main():
     sym = torch.randint(0, 100, (n,), device="cuda", generator=g, dtype=torch.int64)
     close = torch.rand(n, device="cuda", generator=g, dtype=torch.float64) * 500
     df = pl.DataFrame([pl.Series.from_torch("symbol", sym), pl.Series.from_torch("close", close)])
-    base = df.lazy().filter(pl.col("close") > 250.0).group_by("symbol")
+    base = df.lazy().filter(pl.col("close") > 250.0).group_by("symbol", maintain_order=args.maintain_order)
     for name, q in (("sum", base.agg(pl.col("close").sum())), ("std", base.agg(pl.col("close").std())),
                     ("var", base.agg(pl.col("close").var(0)))):
         info = {}
@@ -46,7 +47,8 @@ def main():
         dt = (time.perf_counter() - t0) / args.steps
         print(json.dumps({"query": f"filter(close > 250).group_by(symbol).agg(close.{name}())", "rows": n,
                           "groups": out.height, "ms": round(dt * 1e3, 3), "kernel_ms": round(sum(kms) / len(kms), 3),
-                          "path": info.get("var_path"), "Mrows_per_s": round(n / dt / 1e6, 1)}), flush=True)
+                          "path": info.get("var_path"), "kernel_path": info.get("path"),
+                          "maintain_order": args.maintain_order, "Mrows_per_s": round(n / dt / 1e6, 1)}), flush=True)
         del out
 
 
