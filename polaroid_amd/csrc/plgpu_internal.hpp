@@ -40,7 +40,6 @@ struct Options {
     int mk_collide = 0;  // 3-bit first tuple hash: forces the collision / re-seed path (tests)
     int runs = -1;       // -1: the plan picks the sorted-key variant; 0 / 1 force it (tests)
     int local = -1;      // -1: the plan picks the range-local kernel; 0 keeps it off (tests)
-    int ab = 0;          // TEMPORARY A/B selector while a variant is measured (removed after)
 };
 Options& options();
 int dev_alloc(void** p, size_t bytes, hipStream_t s);

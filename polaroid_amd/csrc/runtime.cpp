@@ -51,7 +51,6 @@ static Options read_env_options() {
     o.mk_collide = get("PLGPU_MK_COLLIDE", 0);
     o.runs = get("PLGPU_RUNS", -1);
     o.local = get("PLGPU_LOCAL", -1);
-    o.ab = get("PLGPU_AB", 0);
     return o;
 }
 
@@ -719,7 +718,6 @@ PLGPU_API int plgpu_set_option(const char* name, int64_t value) {
     else if (!strcmp(name, "mk_collide")) f = &o.mk_collide;
     else if (!strcmp(name, "runs")) f = &o.runs;
     else if (!strcmp(name, "local")) f = &o.local;
-    else if (!strcmp(name, "ab")) f = &o.ab;
     if (f == nullptr) return fail(PLGPU_ERR_INVALID, std::string("unknown option ") + name);
     *f = (int)value;
     return PLGPU_OK;
@@ -733,7 +731,6 @@ PLGPU_API int plgpu_get_option(const char* name, int64_t* out) {
     else if (!strcmp(name, "mk_collide")) *out = o.mk_collide;
     else if (!strcmp(name, "runs")) *out = o.runs;
     else if (!strcmp(name, "local")) *out = o.local;
-    else if (!strcmp(name, "ab")) *out = o.ab;
     else return fail(PLGPU_ERR_INVALID, std::string("unknown option ") + name);
     return PLGPU_OK;
 }
