@@ -279,7 +279,14 @@ def main():
     # launched by torch.distributed.run (even with one rank): the
     # hash-partitioned path over RCCL; plain `python bench.py`: one GPU
     distributed = "RANK" in os.environ and "MASTER_ADDR" in os.environ
+    json_out = sys.stdout
     if distributed:
+        # RCCL prints its version banner on the process's stdout when the
+        # first communicator forms: send fd 1 to stderr for the run and keep
+        # the original stdout for the one JSON line
+        sys.stdout.flush()
+        json_out = os.fdopen(os.dup(1), "w")
+        os.dup2(2, 1)
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     import polaroid_amd as pl
@@ -390,7 +397,7 @@ def main():
         result["plugin_cold_ms"] = result["plugin"]["cold_ms"]
         result["plugin_warm_ms"] = result["plugin"]["warm_ms"]
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        print(json.dumps(result), file=json_out, flush=True)
     if distributed:
         dist.destroy_process_group()
 
