@@ -59,6 +59,26 @@ def _allreduce_max(vals: Sequence[int], group, device) -> list[int]:
     return [int(v) for v in t.tolist()]
 
 
+def agreed_stage(fn, group, device, what: str):
+    """Run a rank-local stage whose success can depend on this rank's shard
+    (a strict cast that overflows on one shard only, an allocation a larger
+    shard cannot get) and agree its outcome with one status all-reduce
+    before any other collective: the failing rank re-raises its error, every
+    other rank raises ComputeError, so no rank waits in a collective the
+    failed one never reaches."""
+    err = res = None
+    try:
+        res = fn()
+    except Exception as e:  # noqa: BLE001 -- agreed below, then re-raised
+        err = e
+    failed = _allreduce_max([1 if err is not None else 0], group, device)[0]
+    if err is not None:
+        raise err
+    if failed:
+        raise N.ComputeError(f"multi-GPU group-by: {what} failed on another rank")
+    return res
+
+
 def _settle(device) -> None:
     """Host-wait for the received buffers.  RCCL writes them on its own
     (non-blocking) stream and a synchronous collective only orders torch's
@@ -621,16 +641,20 @@ def _group_by_agg_states(df, key, aggs: Sequence[Expr], predicate, group, info: 
     # protocol as a column's do (elementwise, so sharding does not change it)
     from .frame import _eval
 
-    extra = []
+    todo = []
     for i, e in enumerate(aggs):
         b = _agg_base(e)
         if b.kind == "agg" and b.args[0].kind != "col":
             nm = f"__in{i}"
             while nm in df.columns:
                 nm += "_"
-            extra.append(_eval(b.args[0].alias(nm), df))
+            todo.append(b.args[0].alias(nm))
             aggs[i] = Expr("agg", (col(nm),), op=b.op, value=b.value).alias(e.output_name())
-    if extra:
+    if todo:
+        # whether an expression evaluates depends on the shard's data (a
+        # strict cast, memory): agreed before the first collective
+        extra = agreed_stage(lambda: [_eval(x, df) for x in todo], group, device,
+                             "evaluating an aggregation input")
         df = DataFrame(list(df._cols.values()) + extra)
     if any(_agg_base(e).kind == "agg" and _agg_base(e).op in ("std", "var") for e in aggs):
         return _group_by_var(df, key, aggs, predicate, group, info)
@@ -645,8 +669,17 @@ def _group_by_agg_states(df, key, aggs: Sequence[Expr], predicate, group, info: 
         # exact Int64 codes (the same code on every rank); decoded at the end
         codes = N.Column()
         short = C.c_int32(0)
-        N.check(N.lib().plgpu_str_encode_short(C.byref(df[key]._col), C.byref(codes), C.byref(short), None))
-        if _allreduce_max([0 if short.value else 1], group, device)[0]:
+        err = None
+        try:
+            N.check(N.lib().plgpu_str_encode_short(C.byref(df[key]._col), C.byref(codes), C.byref(short), None))
+        except N.PolaroidError as e:
+            err = e
+        failed, longer = _allreduce_max([1 if err is not None else 0, 0 if short.value else 1], group, device)
+        if err is not None:
+            raise err
+        if failed:
+            raise N.ComputeError("multi-GPU group-by: encoding the String key failed on another rank")
+        if longer:
             raise _RowShuffle("String keys longer than 7 bytes")
         df = DataFrame([Series._from_native(key, codes) if nm == key else df[nm] for nm in df.columns])
     packed = None

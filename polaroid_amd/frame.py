@@ -1466,7 +1466,10 @@ def _group_by_fused_var(df: DataFrame, key: str | tuple, aggs: list[Expr], maint
                                if _agg_base(e).kind == "agg" and _agg_base(e).op in ("std", "var")))
     plain = [e for e in aggs if not (_agg_base(e).kind == "agg" and _agg_base(e).op in ("std", "var"))]
     pcols = {c for e in plain for c in e.meta_root_names()}
-    if 3 * builtins.len(vcols) + builtins.len(pcols) <= N.GB_MAX_ACC:
+    # len() takes an accumulator of its own, on the key column (_gb_lower's
+    # len_col), which no other plain aggregation names
+    nlen = 1 if builtins.any(_agg_base(e).kind == "len" for e in plain) else 0
+    if 3 * builtins.len(vcols) + builtins.len(pcols) + nlen <= N.GB_MAX_ACC:
         return _group_by_plain(df, key, aggs, maintain_order, pred, info)
     names = [e.output_name() for e in aggs]
     parts = []

@@ -185,11 +185,64 @@ class _Translator:
             raise Unsupported(f"function {fname}")
         raise Unsupported(f"expression {k}")
 
-    def agg(self, node: int, key: str | None) -> Expr:
+    def input_schema(self, input_node: int) -> dict:
+        """Output schema of plan node `input_node` (visit.rs get_schema at that
+        node); the traverser is restored."""
+        here = self.nt.get_node()
+        self.nt.set_node(input_node)
+        try:
+            return dict(self.nt.get_schema())
+        finally:
+            self.nt.set_node(here)
+
+    _CMP_OPS = frozenset({"Eq", "NotEq", "Lt", "LtEq", "Gt", "GtEq", "EqValidity", "NotEqValidity"})
+    _LOGIC_OPS = frozenset({"And", "Or", "LogicalAnd", "LogicalOr", "Xor"})
+
+    def expr_kind(self, node: int, schema: dict) -> str:
+        """The dtype kind an expression yields (`Boolean`, `String`, `Datetime`,
+        `Duration`, ...; `?` when the translator cannot tell), enough to keep
+        the aggregations the device path lacks on polars."""
+        e = self.view(node)
+        k = _name(e)
+        if k == "Column":
+            kind = _dtype_kind(schema.get(str(e.name)))
+            return "String" if kind in ("Categorical", "Enum") else kind
+        if k == "Literal":
+            v = e.value
+            return "Boolean" if isinstance(v, bool) else "String" if isinstance(v, str) else "?"
+        if k == "Cast":
+            return _dtype_kind(e.dtype)
+        if k == "BinaryExpr":
+            op = _enum_name(e.op)
+            if op in self._CMP_OPS:
+                return "Boolean"
+            a, b = self.expr_kind(e.left, schema), self.expr_kind(e.right, schema)
+            if op in self._LOGIC_OPS:
+                return "Boolean" if "Boolean" in (a, b) else a
+            if "Datetime" in (a, b) or "Date" in (a, b):
+                # Datetime - Datetime = Duration, Datetime +- Duration = Datetime
+                return "Duration" if op == "Minus" and a == b else ("Datetime" if "Datetime" in (a, b) else "Date")
+            return "Duration" if "Duration" in (a, b) else "?"
+        if k == "Ternary":
+            return self.expr_kind(e.truthy, schema)
+        if k == "Function":
+            fd = e.function_data
+            fname = _enum_name(fd[0]) if isinstance(fd, tuple) and fd else _enum_name(fd)
+            if fname in _BOOLFUNCS or fname in ("IsBetween", "IsIn"):
+                return "Boolean"
+            if e.input:
+                return self.expr_kind(e.input[0], schema)
+        return "?"
+
+    def agg(self, node: int, key: str | None, schema: dict | None = None) -> Expr:
         """IRAggExpr (expr_nodes.rs) -> an aggregation over a column or over an
         elementwise expression (the inputs the reference's partitionable
         group-by pre-aggregates, plans/aexpr/properties/general.rs:303-356
-        can_pre_agg).  `key` None: a select of aggregations."""
+        can_pre_agg).  `key` None: a select of aggregations.  `schema` (the
+        input node's) gates the input dtypes the device aggregations lack --
+        String inputs, min / max / first / last of Boolean, sum / mean of
+        Date / Datetime and mean of Duration -- so those queries stay on
+        polars instead of failing at collect time."""
         e = self.view(node)
         k = _name(e)
         if k == "Len":
@@ -203,6 +256,16 @@ class _Translator:
         name = str(e.name)
         if len(e.arguments) != 1:
             raise Unsupported("multi-argument aggregation")
+        if schema is not None:
+            kind = self.expr_kind(e.arguments[0], schema)
+            if kind == "String":
+                raise Unsupported(f"{name} of a String / Categorical input")
+            if kind == "Boolean" and name in ("min", "max", "first", "last"):
+                raise Unsupported(f"{name} of a Boolean input")
+            if kind in ("Date", "Datetime", "Time") and name in ("sum", "mean", "std", "var"):
+                raise Unsupported(f"{name} of a {kind} input")
+            if kind == "Duration" and name in ("mean", "std", "var"):
+                raise Unsupported(f"{name} of a Duration input")
         arg = self.nt.view_expression(e.arguments[0])
         if _name(arg) == "Column":
             c = col(str(arg.name))
@@ -293,7 +356,8 @@ class _Translator:
                 return ("select", child, [col(n) for n in names])
             if k == "Select" and node.expr and all(_name(self.view(ei.node)) in ("Agg", "Len") for ei in node.expr):
                 # select(aggregations): a global reduction on the GPU
-                return ("select", child, [self.agg(ei.node, None).alias(ei.output_name) for ei in node.expr])
+                ins = self.input_schema(node.input)
+                return ("select", child, [self.agg(ei.node, None, ins).alias(ei.output_name) for ei in node.expr])
             if k in ("Select", "HStack"):
                 exprs = node.expr if k == "Select" else node.exprs
                 out = []
@@ -317,8 +381,9 @@ class _Translator:
                 names.append(str(kx.name))
             key = names[0] if len(names) == 1 else tuple(names)
             aggs = []
+            ins = self.input_schema(node.input)
             for ai in node.aggs:
-                a = self.agg(ai.node, names[0])
+                a = self.agg(ai.node, names[0], ins)
                 aggs.append(a.alias(ai.output_name))
             return ("group_by", child, key, aggs, bool(node.maintain_order))
         raise Unsupported(f"plan node {k}")

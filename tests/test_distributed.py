@@ -444,6 +444,57 @@ def test_row_shuffle_protocol_gloo(world):
     assert None in res[0]  # the null key routes to rank 0
 
 
+def _agreed_worker(rank, world, port, q):
+    """An aggregation input evaluated per shard (the stage _group_by_agg_states
+    runs before its first collective): a strict cast that overflows only in
+    rank 1's shard.  Afterwards every rank enters the next collective, which
+    must not hang."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        shard = np.arange(10, dtype=np.int64) + (300 if rank == 1 else 0)
+
+        def strict_cast_u8():
+            if shard.max() > 255:
+                raise D.N.InvalidOperationError("conversion from `i64` to `u8` failed in column 'x'")
+            return shard.astype(np.uint8)
+
+        try:
+            D.agreed_stage(strict_cast_u8, None, torch.device("cpu"), "evaluating an aggregation input")
+            res = "ok"
+        except Exception as e:  # noqa: BLE001
+            res = type(e).__name__
+        # the next collective of the protocol: reached by every rank
+        t = torch.tensor([rank], dtype=torch.int64)
+        dist.all_reduce(t)
+        q.put((rank, res, int(t.item())))
+        # and a stage that succeeds everywhere returns its value
+        assert D.agreed_stage(lambda: rank * 2, None, torch.device("cpu"), "x") == rank * 2
+    finally:
+        dist.destroy_process_group()
+
+
+def test_aggregation_input_failure_on_one_rank_reaches_every_rank_gloo():
+    """an expression input that fails on one rank's shard only
+    makes every rank raise (the failing rank its own error), instead of the
+    others waiting in the next collective."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_agreed_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {r: (s, t) for r, s, t in (q.get(timeout=180) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[1][0] == "InvalidOperationError"
+    assert res[0][0] == "ComputeError" and res[2][0] == "ComputeError"
+    assert all(t == 0 + 1 + 2 for _, t in res.values())
+
+
 def test_row_shuffle_failure_reaches_every_rank_gloo():
     world = 3
     ctx = mp.get_context("spawn")

@@ -238,6 +238,29 @@ def test_var_fused_exact_cases(gpu):
         assert math.isclose(v_, _exact_var(tight[(key == a_) & (k2 == b_)], 1), rel_tol=4e-16)
 
 
+def test_var_fused_batches_count_len(gpu):
+    """len() takes an accumulator of its own: two var columns (six
+    accumulators) next to len() run as fused batches, not the two-pass path
+    (ADVICE r3), and stay within 1e-12 of the checker."""
+    rng = np.random.default_rng(5)
+    n = 100_003
+    key, x, y, xv = _var_frame(rng, n, 50)
+    df = pl.DataFrame({"k": pl.Series.from_numpy("k", key), "x": pl.Series.from_numpy("x", x, xv),
+                       "y": pl.Series.from_numpy("y", y)})
+    info = {}
+    out = (df.lazy().group_by("k", maintain_order=True)
+           .agg(pl.col("x").var().alias("xv"), pl.col("y").var().alias("yv"), pl.len())
+           .collect(info=info))
+    assert info["var_path"] == "fused", info
+    ones = np.ones(n, bool)
+    keys, var, _, ok = _oracle(key, x, xv, 1, ones)
+    assert np.array_equal(out["k"].to_numpy(), keys)
+    _close(out["xv"].to_numpy(), var, ok)
+    _, yvar, _, yok = _oracle(key, y, ones, 1, ones)
+    _close(out["yv"].to_numpy(), yvar, yok)
+    assert out["len"].to_list() == [int((key == k).sum()) for k in keys]
+
+
 @pytest.mark.parametrize("case", ["tiny", "huge", "wide"])
 def test_var_fused_out_of_range_falls_back(gpu, case):
     """Inputs whose exact fused state would leave its range take the two

@@ -526,6 +526,61 @@ def test_translate_aggregations_over_expressions_and_select():
         PE.translate(nt)
 
 
+def _typed_agg_ir(agg_name, arg, dtypes, select=True):
+    """select(<agg>(arg)) or group_by("k").agg(<agg>(arg)) over a scan whose
+    columns have the given polars dtypes; `arg` builds the argument node."""
+    table = _table()[0]
+    nt = FakeNT(table)
+    nt.dtypes.update(dtypes)
+    cols = ["k", "v", "w"] + [c for c in dtypes if c not in ("k", "v", "w")]
+    scan = nt.p("DataFrameScan", cols, df=FakePolarsDF(table), projection=None, selection=None)
+    a = nt.e("Agg", name=agg_name, arguments=[arg(nt)], options=None)
+    if select:
+        nt.p("Select", ["out"], input=scan, expr=[PyExprIR(a, "out")])
+    else:
+        opts = _node("GroupbyOptions", slice=None, dynamic=None, rolling=None)
+        nt.p("GroupBy", ["k", "out"], input=scan, keys=[PyExprIR(nt.col("k"), "k")], aggs=[PyExprIR(a, "out")],
+             apply=None, maintain_order=False, options=opts)
+    return nt
+
+
+@pytest.mark.parametrize("select", [True, False])
+def test_aggregations_the_device_lacks_stay_on_polars(select):
+    """Input dtypes the device aggregations do not take are refused at
+    translate time, so polars runs those queries (no UDF, no collect-time
+    error): min / max / first / last of Boolean (column or comparison),
+    anything over String / Categorical, sum / mean of Datetime / Date, mean
+    of Duration.  The supported neighbours still translate."""
+    refused = [
+        ("max", lambda nt: nt.col("b"), {"b": "Boolean"}),
+        ("first", lambda nt: nt.col("b"), {"b": "Boolean"}),
+        ("min", lambda nt: nt.bin(nt.col("v"), "Gt", nt.lit(0.5)), {}),
+        ("min", lambda nt: nt.col("s"), {"s": "String"}),
+        ("count", lambda nt: nt.col("s"), {"s": "Categorical"}),
+        ("mean", lambda nt: nt.col("t"), {"t": "Datetime(time_unit='us', time_zone=None)"}),
+        ("sum", lambda nt: nt.col("d"), {"d": "Date"}),
+        ("mean", lambda nt: nt.col("u"), {"u": "Duration(time_unit='ns')"}),
+    ]
+    for name, arg, dt in refused:
+        nt = _typed_agg_ir(name, arg, dt, select)
+        with pytest.raises(PE.Unsupported):
+            PE.translate(nt)
+        PE.execute_with_polaroid(nt, None)
+        assert nt.udf is None, (name, dt)
+    accepted = [
+        ("sum", lambda nt: nt.col("b"), {"b": "Boolean"}),
+        ("mean", lambda nt: nt.bin(nt.col("v"), "Gt", nt.lit(0.5)), {}),
+        ("max", lambda nt: nt.col("t"), {"t": "Datetime(time_unit='us', time_zone=None)"}),
+        ("sum", lambda nt: nt.col("u"), {"u": "Duration(time_unit='ns')"}),
+        ("sum", lambda nt: nt.col("v"), {}),
+    ]
+    for name, arg, dt in accepted:
+        nt = _typed_agg_ir(name, arg, dt, select)
+        PE.translate(nt)
+        PE.execute_with_polaroid(nt, None)
+        assert callable(nt.udf), (name, dt)
+
+
 @pytest.mark.gpu
 def test_udf_aggregations_over_expressions_on_gpu(gpu):
     table, k, v, w, vvalid = _table(100_000, 21)
