@@ -37,6 +37,12 @@ THRESHOLD = 250.0
 BYTES_PER_ROW = 8 + 4 * 8      # key + open/high/low/close read once (close is also the predicate)
 
 
+def progress(msg: str) -> None:
+    """One line per finished phase on stderr (the JSON line stays alone on
+    stdout), so a long run shows it is alive."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -53,6 +59,9 @@ def parse():
     ap.add_argument("--no-plugin", action="store_true")
     ap.add_argument("--no-vwap", action="store_true")
     ap.add_argument("--no-std", action="store_true")
+    ap.add_argument("--no-sort", action="store_true", help="skip the configs[2] sort + rolling leg")
+    ap.add_argument("--no-join", action="store_true", help="skip the configs[3] join leg")
+    ap.add_argument("--leg-steps", type=int, default=5, help="timed steps of the sort and join legs (<= --steps)")
     ap.add_argument("--dry-run", action="store_true",
                     help="print this rank's launch parameters and exit before touching the GPU (tests)")
     return ap.parse_args()
@@ -229,6 +238,206 @@ def std_leg(torch, pl, df, steps: int, warmup: int) -> dict:
             "kernel": "gb_fast_kernel<NACC=3,PRED=1,SUMONLY,VAR> (variance triple)", **r}
 
 
+def _kernel_table(kt: dict, steps: int) -> dict:
+    """plgpu_ktime_read sums -> {kernel: {ms_mean (per launch), ms_per_step, launches}}."""
+    return {k: {"ms_mean": round(ms / max(c, 1), 4), "ms_per_step": round(ms / steps, 4), "launches": c}
+            for k, (ms, c) in sorted(kt.items(), key=lambda kv: -kv[1][0])}
+
+
+def _time_steps(torch, step, steps: int, warmup: int):
+    """Warm up, then time `steps` calls of step() between device
+    synchronisations with the library's kernel timer on (HIP events around
+    each named launch, on the stream it runs on).  Returns (ms per step,
+    per-kernel table, last result)."""
+    from polaroid_amd import _native as N
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    prev = N.set_option("ktime", 1)
+    N.ktime_read(reset=True)
+    try:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            res = step()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / steps
+        kt = N.ktime_read(reset=True)
+    finally:
+        N.set_option("ktime", prev)
+    return dt * 1e3, _kernel_table(kt, steps), res
+
+
+def _leg_roofline(kernels: dict, name: str, algo_bytes: float, what: str) -> dict:
+    k = kernels.get(name, {}).get("ms_mean")
+    if not k:
+        return {"kernel": name, "kernel_ms": None}
+    gbs = algo_bytes / (k * 1e-3) / 1e9
+    return {"kernel": name, "kernel_ms": k, "algorithmic_GB": round(algo_bytes / 1e9, 3), "bytes": what,
+            "achieved_GBs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
+
+
+SORT_ROWS = 1_000_000_000      # configs[2]: 1e9 rows, 8 columns mixed i64 / f64
+SORT_WINDOW = 20
+JOIN_PROBE, JOIN_BUILD = 1_000_000_000, 10_000_000   # configs[3]
+# random 128-byte line requests per second from a 256 MiB table on one
+# MI355X (tools/randread_bench.hip, profiles/r02_randread.txt: 54.5 G/s at
+# grid 8192): the floor of a probe pass that needs one table line per row
+RANDREQ_PER_S = 54.5e9
+
+
+def sort_leg(torch, pl, steps: int, warmup: int, rows: int = SORT_ROWS, window: int = SORT_WINDOW) -> dict:
+    """configs[2]: `df.sort("ts")` of a 1e9-row frame of 8 columns (ts, sym,
+    qty, flags: i64; price, bid, ask, vol: f64; ts a shuffled timestamp
+    below 2^40), then `rolling_mean(20)` of the sorted price.  One step = the
+    radix arg_sort + the gather of all 8 columns + the rolling window.
+    Reference: polars-core/src/chunked_array/ops/sort/arg_sort.rs:82 and
+    polars-compute/src/rolling/no_nulls/mean.rs.  rank 0, N = 1."""
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev)
+    g.manual_seed(11)
+    chunk = 1 << 27
+    cols = {}
+    for k in ("ts", "sym", "qty", "flags"):
+        t = torch.empty(rows, dtype=torch.int64, device=dev)
+        hi = (1 << 40) if k == "ts" else (1 << 20)
+        for s in range(0, rows, chunk):
+            e = min(rows, s + chunk)
+            t[s:e] = torch.randint(0, hi, (e - s,), device=dev, generator=g)
+        cols[k] = t
+    for k in ("price", "bid", "ask", "vol"):
+        t = torch.empty(rows, dtype=torch.float64, device=dev)
+        for s in range(0, rows, chunk):
+            e = min(rows, s + chunk)
+            t[s:e] = 100 + torch.rand(e - s, device=dev, generator=g, dtype=torch.float64) * 50
+        cols[k] = t
+    df = pl.DataFrame([pl.Series.from_torch(k, v) for k, v in cols.items()])
+
+    def step():
+        srt = df.sort("ts")
+        roll = srt["price"].rolling_mean(window)
+        return srt.height + roll.len()
+
+    ms, kernels, res = _time_steps(torch, step, steps, warmup)
+    assert res == 2 * rows
+    del df, cols
+    torch.cuda.empty_cache()
+    # the sort's floor: read the 8 input columns once and write the 8 sorted
+    # columns once (128 B/row); rolling_mean reads and writes 8 B/row
+    algo = rows * (8 * 8 * 2 + 16)
+    gather = _leg_roofline(kernels, "aos_gather_kernel", rows * (64 + 4 + 64),
+                           "64 B packed row read + 4 B row id read + 64 B column stores per row")
+    pack = _leg_roofline(kernels, "aos_pack_kernel", rows * 128, "64 B read + 64 B packed row written per row")
+    roll = _leg_roofline(kernels, "rl_wave_kernel", rows * 16, "8 B read + 8 B written per row")
+    return {"query": f"df.sort('ts') (8 columns: 4 x i64, 4 x f64) + sorted price.rolling_mean({window})",
+            "rows": rows, "ms_per_step": round(ms, 3), "Mrows_s": round(rows / ms / 1e3, 1),
+            "algorithmic_GB": round(algo / 1e9, 1),
+            "step_frac": round(algo / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "roofline": gather, "pack": pack, "rolling": roll, "kernels": kernels,
+            "note": "step_frac: the read-once / write-once floor (128 B/row sort + 16 B/row rolling) over the step "
+                    "time; roofline: the dominant kernel (aos_gather_kernel) at its own algorithmic bytes"}
+
+
+def join_leg(torch, pl, steps: int, warmup: int, n: int = JOIN_PROBE, m: int = JOIN_BUILD) -> dict:
+    """configs[3]: `probe.join(build, on="k")` inner, 1e9 probe rows x 1e7
+    unique build keys (i64), half the probe rows match; every output column
+    materialised (k, probe payload, build payload).  Reference: polars-ops/
+    src/frame/join/hash_join/single_keys_inner.rs:40 + general.rs:17
+    _finish_join.  rank 0, N = 1."""
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev)
+    g.manual_seed(7)
+    pk = torch.empty(n, dtype=torch.int64, device=dev)
+    pv = torch.empty(n, dtype=torch.float64, device=dev)
+    chunk = 1 << 27
+    for s in range(0, n, chunk):
+        e = min(n, s + chunk)
+        pk[s:e] = torch.randint(0, 2 * m, (e - s,), device=dev, generator=g)
+        pv[s:e] = torch.rand(e - s, device=dev, generator=g, dtype=torch.float64)
+    bk = torch.randperm(2 * m, device=dev, generator=g)[:m].to(torch.int64)
+    bv = torch.rand(m, device=dev, generator=g, dtype=torch.float64)
+    probe = pl.DataFrame([pl.Series.from_torch("k", pk), pl.Series.from_torch("pv", pv)])
+    build = pl.DataFrame([pl.Series.from_torch("k", bk), pl.Series.from_torch("bv", bv)])
+    out_rows = []
+
+    def step():
+        out = probe.join(build, on="k")
+        out_rows.append(out.height)
+        return out.height
+
+    ms, kernels, res = _time_steps(torch, step, steps, warmup)
+    assert 0.45 * n < res < 0.55 * n
+    del probe, build, pk, pv, bk, bv
+    torch.cuda.empty_cache()
+    match = _leg_roofline(kernels, "jn_probe_match_kernel", n * (8 + 8) + n // 8,
+                          "8 B probe key read + 8 B payload word written per row + 1 hit bit")
+    if match.get("kernel_ms"):
+        floor_ms = n / RANDREQ_PER_S * 1e3
+        match["random_request_floor_ms"] = round(floor_ms, 3)
+        match["frac_of_request_floor"] = round(floor_ms / match["kernel_ms"], 4)
+        match["request_floor_note"] = ("one random 128 B table line per probe row at 54.5 G requests/s "
+                                       "(profiles/r02_randread.txt, 256 MiB table)")
+    emit = _leg_roofline(kernels, "jn_take_emit_kernel", n * (8 + 8 + 1 / 8) + res * 24,
+                         "payload words + probe payload read, 3 x 8 B written per output row")
+    algo = n * 16 + m * 16 + res * 24
+    return {"query": "probe.join(build, on='k') inner, output k, pv, bv", "probe_rows": n, "build_rows": m,
+            "output_rows": res, "ms_per_step": round(ms, 3), "Mrows_s": round(n / ms / 1e3, 1),
+            "algorithmic_GB": round(algo / 1e9, 2),
+            "step_frac": round(algo / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "roofline": match, "emit": emit, "kernels": kernels,
+            "note": "step_frac: probe (k, pv) + build (k, bv) read once, 3 output columns written once, over the "
+                    "step time; roofline: the match pass (bound by random table line requests, not bytes)"}
+
+
+def cpu_sort_baseline(rows: int, seconds: float) -> dict:
+    """configs[2]'s query on the host cores: the oracle's restatement of the
+    reference's parallel stable arg_sort + per-column take + Kahan
+    rolling_mean (oracle/polars_oracle.c:or_baseline_sort_rolling)."""
+    from oracle import oracle as O
+
+    threads, cores_note = host_cores()
+    rng = np.random.default_rng(11)
+    key = rng.integers(0, 1 << 40, rows).astype(np.int64)
+    cols = [key] + [rng.integers(0, 1 << 20, rows).astype(np.int64) for _ in range(3)] + \
+           [100 + rng.random(rows) * 50 for _ in range(4)]
+    times = []
+    t_end = time.perf_counter() + seconds
+    while time.perf_counter() < t_end or not times:
+        t0 = time.perf_counter()
+        O.baseline_sort_rolling(key, cols, 4, SORT_WINDOW, threads)
+        times.append(time.perf_counter() - t0)
+    t = float(np.median(times))
+    return {"value": rows / t / 1e6, "unit": "Mrows/s", "cores": threads, "kind": "port",
+            "sample": f"{rows:.0e} rows x 8 columns x {len(times)} runs (median), OpenMP {threads} threads "
+                      f"({cores_note}), oracle/polars_oracle.c:or_baseline_sort_rolling"}
+
+
+def cpu_join_baseline(probe_rows: int, seconds: float) -> dict:
+    """configs[3]'s join on the host cores: the full 1e7-key build side and a
+    probe sample, through the oracle's restatement of the reference's
+    partitioned build + chunked probe + take (or_baseline_join_inner)."""
+    from oracle import oracle as O
+
+    threads, cores_note = host_cores()
+    rng = np.random.default_rng(7)
+    bk = rng.permutation(2 * JOIN_BUILD)[:JOIN_BUILD].astype(np.int64)
+    bv = rng.random(JOIN_BUILD)
+    pk = rng.integers(0, 2 * JOIN_BUILD, probe_rows).astype(np.int64)
+    pv = rng.random(probe_rows)
+    times = []
+    t_end = time.perf_counter() + seconds
+    while time.perf_counter() < t_end or not times:
+        t0 = time.perf_counter()
+        O.baseline_join_inner(pk, pv, bk, bv, threads)
+        times.append(time.perf_counter() - t0)
+    t = float(np.median(times))
+    return {"value": probe_rows / t / 1e6, "unit": "Mrows/s (probe rows)", "cores": threads, "kind": "port",
+            "sample": f"{probe_rows:.0e} probe rows x {JOIN_BUILD:.0e} build keys (configs[3]'s build side) x "
+                      f"{len(times)} runs (median), build included, OpenMP {threads} threads ({cores_note}), "
+                      "oracle/polars_oracle.c:or_baseline_join_inner"}
+
+
 def load_traffic(n_rows: int):
     """HBM bytes per launch from the committed rocprofv3 PMC summary, if any
     (profiles/traffic.json written by tools/pmc_traffic.py)."""
@@ -336,6 +545,7 @@ def main():
         per_rank = [[round(float(x), 4) for x in t.tolist()] for t in allr]
     ms_per_step = dt / args.steps * 1e3
     total_rows = n * world
+    progress(f"headline: {ms_per_step:.3f} ms per step")
     value = total_rows * args.steps / dt / 1e6
     kms = float(np.mean(kernel_ms))
     achieved = BYTES_PER_ROW * n / (kms * 1e-3) / 1e9
@@ -386,14 +596,34 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(int(args.cpu_rows), args.groups, args.cpu_seconds)
+        progress("cpu_baseline done")
     if rank == 0 and world == 1 and not args.no_vwap:
         result["vwap"] = vwap_leg(torch, pl, df, sym, cols["close"], args.steps, args.warmup)
+        progress("vwap leg done")
     if rank == 0 and world == 1 and not args.no_std:
         result["std"] = std_leg(torch, pl, df, args.steps, args.warmup)
-    if rank == 0 and world == 1 and not args.no_plugin:
+        progress("std leg done")
+    if rank == 0 and world == 1 and not (args.no_sort and args.no_join and args.no_plugin):
+        # the remaining legs need the HBM the headline frame holds
         del df, query, out, sym, cols
         torch.cuda.empty_cache()
+        pl._native.release_cached()
+    leg_steps = max(1, min(args.steps, args.leg_steps))
+    if rank == 0 and world == 1 and not args.no_sort:
+        result["sort"] = sort_leg(torch, pl, leg_steps, 1)
+        progress(f"sort leg: {result['sort']['ms_per_step']} ms per step")
+        if not args.no_cpu:
+            result["sort"]["cpu_baseline"] = cpu_sort_baseline(int(args.cpu_rows), args.cpu_seconds / 2)
+        pl._native.release_cached()
+    if rank == 0 and world == 1 and not args.no_join:
+        result["join"] = join_leg(torch, pl, leg_steps, 1)
+        progress(f"join leg: {result['join']['ms_per_step']} ms per step")
+        if not args.no_cpu:
+            result["join"]["cpu_baseline"] = cpu_join_baseline(int(args.cpu_rows), args.cpu_seconds / 2)
+        pl._native.release_cached()
+    if rank == 0 and world == 1 and not args.no_plugin:
         result["plugin"] = plugin_leg(int(args.plugin_rows), args.groups)
+        progress("plugin leg done")
         result["plugin_cold_ms"] = result["plugin"]["cold_ms"]
         result["plugin_warm_ms"] = result["plugin"]["warm_ms"]
     if rank == 0:

@@ -239,6 +239,17 @@ int plgpu_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream);
  * An unknown name is PLGPU_ERR_INVALID. */
 int plgpu_set_option(const char* name, int64_t value);
 int plgpu_get_option(const char* name, int64_t* out);
+/* Kernel timer (option "ktime" = 1): HIP-event times of the library's named
+ * kernels since the last reset, one "name\tms_total\tlaunches\n" line per
+ * kernel into buf (NUL-terminated); waits for pending launches.  reset != 0
+ * clears the sums.  Measurement support (no reference counterpart; the
+ * reference's equivalent is its profiling via `should_time`,
+ * crates/polars-mem-engine/src/executors/scan/python_scan.rs:91). */
+int plgpu_ktime_read(char* buf, int64_t cap, int32_t reset);
+/* Return the allocator's cached free blocks on the current device to the HIP
+ * runtime (waits for the device first), e.g. before another allocator in the
+ * process needs the memory.  Live columns are untouched. */
+int plgpu_release_cached(void);
 
 /* Checked build only (make CHECKS=1, libpolaroid_gpu_checked.so): the bits of
  * the group-by kernels' index invariants violated since the last call (the

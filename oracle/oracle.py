@@ -75,6 +75,12 @@ def lib():
         L.or_baseline_filter_groupby_sum.argtypes = [
             C.c_void_p, C.c_void_p, C.c_double, C.c_void_p, C.c_int32, C.c_int64, C.c_int32,
             C.POINTER(C.c_double)]
+        L.or_baseline_sort_rolling.restype = C.c_double
+        L.or_baseline_sort_rolling.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int64, C.c_int64,
+                                               C.c_int32, C.c_void_p, C.c_void_p]
+        L.or_baseline_join_inner.restype = C.c_int64
+        L.or_baseline_join_inner.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_int64,
+                                             C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]
         _lib = L
     return _lib
 
@@ -492,3 +498,37 @@ def baseline_filter_groupby_sum(key: np.ndarray, pred: np.ndarray, k: float, sum
     g = lib().or_baseline_filter_groupby_sum(key.ctypes.data, pred.ctypes.data, k, ptrs, len(sums),
                                              key.shape[0], threads, C.byref(chk))
     return int(g), chk.value
+
+
+def baseline_sort_rolling(key: np.ndarray, cols: list[np.ndarray], roll: int, window: int,
+                          threads: int) -> tuple[list[np.ndarray], np.ndarray, float]:
+    """CPU baseline of configs[2] (or_baseline_sort_rolling): sort the frame
+    by `key` (stable), gather every column, rolling_mean(window) of
+    cols[roll].  Returns (sorted columns, rolling output, checksum)."""
+    n = key.shape[0]
+    key = np.ascontiguousarray(key, dtype=np.int64)
+    cols = [np.ascontiguousarray(c).view(np.uint64) for c in cols]
+    outs = [np.empty(n, dtype=np.uint64) for _ in cols]
+    roll_out = np.empty(n, dtype=np.float64)
+    ip = (C.c_void_p * len(cols))(*[c.ctypes.data for c in cols])
+    op = (C.c_void_p * len(outs))(*[o.ctypes.data for o in outs])
+    chk = lib().or_baseline_sort_rolling(key.ctypes.data, ip, len(cols), roll, n, window, threads, op,
+                                         roll_out.ctypes.data)
+    return outs, roll_out, chk
+
+
+def baseline_join_inner(pk: np.ndarray, pv: np.ndarray, bk: np.ndarray, bv: np.ndarray,
+                        threads: int) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """CPU baseline of configs[3] (or_baseline_join_inner): inner join on one
+    Int64 key, probe rows in order within each thread's chunk, materialised
+    (probe key, probe payload, build payload)."""
+    np_, nb = pk.shape[0], bk.shape[0]
+    cap = np_ * 2 + 16
+    ok = np.empty(cap, dtype=np.int64)
+    opv = np.empty(cap, dtype=np.float64)
+    obv = np.empty(cap, dtype=np.float64)
+    n = lib().or_baseline_join_inner(pk.ctypes.data, pv.ctypes.data, np_, bk.ctypes.data, bv.ctypes.data, nb,
+                                     threads, ok.ctypes.data, opv.ctypes.data, obv.ctypes.data, cap)
+    if n < 0:
+        raise RuntimeError("baseline join: more output rows than the buffer holds")
+    return ok[:n], opv[:n], obv[:n]

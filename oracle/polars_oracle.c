@@ -1451,3 +1451,205 @@ OR_EXPORT void or_rolling(const plgpu_column* c, int32_t kind, int64_t ws, int64
         else out_f64[i] = valid ? v : 0.0;
     }
 }
+
+/* ------------------------------------------- CPU baselines: sort, join
+ * The bench's cpu_baseline legs for configs[2] and configs[3] (TEST
+ * INFRASTRUCTURE: timed beside the GPU, never the product).  Both use every
+ * thread they are given, as the reference's rayon POOL does. */
+
+/* configs[2]: `df.sort("ts")` over ncols 8-byte columns, then
+ * rolling_mean(ws) of column `roll`.
+ *  - arg_sort: polars-core/src/chunked_array/ops/sort/arg_sort.rs:82
+ *    arg_sort_no_nulls collects (row, value) pairs and sorts them with
+ *    sort_by_branch -> par_sort_by (a parallel stable merge sort).  Restated:
+ *    T contiguous runs sorted in parallel (qsort with the row id as the tie
+ *    break, i.e. stable), then pairwise merge rounds, each round's merges in
+ *    parallel;
+ *  - the frame gather: DataFrame::take_unchecked, one take per column, the
+ *    columns in parallel (POOL.install over the columns);
+ *  - rolling_mean: rolling/no_nulls/mod.rs:43 rolling_apply_agg_window with
+ *    mean.rs MeanWindow over sum.rs:7 SumWindow (Kahan add / sub), one
+ *    thread (a rolling kernel runs per chunk, sequentially).
+ * Returns a checksum of the rolling output so nothing is elided. */
+typedef struct { int64_t v; int64_t r; } bl_pair;
+
+static int bl_pair_cmp(const void* a, const void* b) {
+    const bl_pair* x = (const bl_pair*)a;
+    const bl_pair* y = (const bl_pair*)b;
+    if (x->v != y->v) return x->v < y->v ? -1 : 1;
+    return x->r < y->r ? -1 : (x->r > y->r ? 1 : 0);
+}
+
+static void bl_merge(const bl_pair* a, int64_t na, const bl_pair* b, int64_t nb, bl_pair* out) {
+    int64_t i = 0, j = 0, k = 0;
+    while (i < na && j < nb) out[k++] = bl_pair_cmp(&b[j], &a[i]) < 0 ? b[j++] : a[i++];
+    while (i < na) out[k++] = a[i++];
+    while (j < nb) out[k++] = b[j++];
+}
+
+OR_EXPORT double or_baseline_sort_rolling(const int64_t* key, const uint64_t* const* cols, int32_t ncols,
+                                          int32_t roll, int64_t n, int64_t ws, int32_t threads,
+                                          uint64_t* const* out_cols, double* out_roll) {
+    int T = threads > 0 ? threads : 1;
+    bl_pair* p = (bl_pair*)malloc(sizeof(bl_pair) * (size_t)(n > 0 ? n : 1));
+    bl_pair* q = (bl_pair*)malloc(sizeof(bl_pair) * (size_t)(n > 0 ? n : 1));
+    int R = 1;
+    while (R < T) R <<= 1; /* runs: a power of two >= T */
+#pragma omp parallel for num_threads(T) schedule(static)
+    for (int t = 0; t < R; ++t) {
+        const int64_t lo = n * t / R, hi = n * (t + 1) / R;
+        for (int64_t r = lo; r < hi; ++r) { p[r].v = key[r]; p[r].r = r; }
+        qsort(p + lo, (size_t)(hi - lo), sizeof(bl_pair), bl_pair_cmp);
+    }
+    for (int width = 1; width < R; width <<= 1) {
+#pragma omp parallel for num_threads(T) schedule(dynamic, 1)
+        for (int t = 0; t < R; t += 2 * width) {
+            const int64_t lo = n * t / R, mid = n * (t + width) / R, hi = n * (t + 2 * width) / R;
+            bl_merge(p + lo, mid - lo, p + mid, hi - mid, q + lo);
+        }
+        bl_pair* tmp = p; p = q; q = tmp;
+    }
+#pragma omp parallel for num_threads(T) schedule(static) collapse(2)
+    for (int c = 0; c < ncols; ++c)
+        for (int t = 0; t < T; ++t) {
+            const int64_t lo = n * t / T, hi = n * (t + 1) / T;
+            const uint64_t* src = cols[c];
+            uint64_t* dst = out_cols[c];
+            for (int64_t i = lo; i < hi; ++i) dst[i] = src[p[i].r];
+        }
+    /* rolling_mean(ws), min_periods = ws: the first ws - 1 outputs are null */
+    const double* x = (const double*)out_cols[roll];
+    double sum = 0.0, err_add = 0.0, err_sub = 0.0, chk = 0.0;
+    for (int64_t i = 0; i < n; ++i) {
+        if (i >= ws) {  /* SumWindow::update: Kahan subtract of the leaving value first */
+            const double y = (0.0 - x[i - ws]) - err_sub;
+            const double ns = sum + y;
+            err_sub = (ns - sum) - y;
+            sum = ns;
+        }
+        {   /* then Kahan add of the entering value */
+            const double y = x[i] - err_add;
+            const double ns = sum + y;
+            err_add = (ns - sum) - y;
+            sum = ns;
+        }
+        out_roll[i] = i + 1 >= ws ? sum / (double)ws : 0.0;
+        chk += out_roll[i];
+    }
+    free(p);
+    free(q);
+    return chk;
+}
+
+/* configs[3]: `probe.join(build, on="k")` inner, materialised (probe key,
+ * probe payload, build payload).
+ *  - build: polars-ops/src/frame/join/hash_join/single_keys.rs build_tables:
+ *    the build keys hash-partitioned over the threads; each thread scans
+ *    every build key and inserts those of its partition into its own table
+ *    (key -> the rows in row order);
+ *  - probe: single_keys_inner.rs:40 hash_join_tuples_inner, the probe side
+ *    split into one contiguous chunk per thread, each probing in row order
+ *    (probe_inner, :11) into a thread-local pair list; the lists are
+ *    concatenated in chunk order;
+ *  - materialise: general.rs:17 _finish_join, one take per column.
+ * Tables are open addressing (the reference's hashbrown maps) over a 64-bit
+ * mix of the key.  Returns the number of output rows. */
+OR_EXPORT int64_t or_baseline_join_inner(const int64_t* pk, const double* pv, int64_t np, const int64_t* bk,
+                                         const double* bv, int64_t nb, int32_t threads, int64_t* out_k,
+                                         double* out_pv, double* out_bv, int64_t cap) {
+    int T = threads > 0 ? threads : 1;
+    int P = 1;
+    while (P < T) P <<= 1;
+    imap_t* tabs = (imap_t*)calloc((size_t)P, sizeof(imap_t));
+    int64_t** heads = (int64_t**)calloc((size_t)P, sizeof(int64_t*));
+    int64_t* next = (int64_t*)malloc(sizeof(int64_t) * (size_t)(nb > 0 ? nb : 1));
+#pragma omp parallel for num_threads(T) schedule(dynamic, 1)
+    for (int part = 0; part < P; ++part) {
+        imap_t* m = &tabs[part];
+        imap_init(m, nb / P + 16);
+        int64_t ng = 0, hcap = nb / P + 16;
+        int64_t* head = (int64_t*)malloc(sizeof(int64_t) * (size_t)hcap);
+        int64_t* tail = (int64_t*)malloc(sizeof(int64_t) * (size_t)hcap);
+        for (int64_t r = 0; r < nb; ++r) {
+            const uint64_t h = mix64((uint64_t)bk[r]);
+            if ((int)(h >> 58) % P != part) continue;
+            if (m->cap < 2 * (ng + 1)) {
+                imap_t m2;
+                imap_init(&m2, 2 * m->cap);
+                for (int64_t s = 0; s < m->cap; ++s)
+                    if (m->used[s]) { int d; imap_get_or_insert(&m2, m->keys[s], m->gid[s], &d); }
+                imap_free(m);
+                *m = m2;
+            }
+            int ins;
+            const int64_t g = imap_get_or_insert(m, bk[r], ng, &ins);
+            next[r] = -1;
+            if (ins) {
+                if (ng == hcap) {
+                    hcap *= 2;
+                    head = (int64_t*)realloc(head, sizeof(int64_t) * (size_t)hcap);
+                    tail = (int64_t*)realloc(tail, sizeof(int64_t) * (size_t)hcap);
+                }
+                head[ng] = tail[ng] = r;
+                ++ng;
+            } else {
+                next[tail[g]] = r;
+                tail[g] = r;
+            }
+        }
+        free(tail);
+        heads[part] = head;
+    }
+    int64_t* cnt = (int64_t*)calloc((size_t)T + 1, sizeof(int64_t));
+    int64_t** lp = (int64_t**)calloc((size_t)T, sizeof(int64_t*));
+    int64_t** lb = (int64_t**)calloc((size_t)T, sizeof(int64_t*));
+#pragma omp parallel for num_threads(T) schedule(static)
+    for (int t = 0; t < T; ++t) {
+        const int64_t lo = np * t / T, hi = np * (t + 1) / T;
+        int64_t c = 0, cp = (hi - lo) / 2 + 16;
+        int64_t* a = (int64_t*)malloc(sizeof(int64_t) * (size_t)cp);
+        int64_t* b = (int64_t*)malloc(sizeof(int64_t) * (size_t)cp);
+        for (int64_t r = lo; r < hi; ++r) {
+            const uint64_t h0 = mix64((uint64_t)pk[r]);
+            const int part = (int)(h0 >> 58) % P;
+            const imap_t* m = &tabs[part];
+            uint64_t h = h0 & (uint64_t)(m->cap - 1);
+            int64_t g = -1;
+            while (m->used[h]) {
+                if (m->keys[h] == pk[r]) { g = m->gid[h]; break; }
+                h = (h + 1) & (uint64_t)(m->cap - 1);
+            }
+            if (g < 0) continue;
+            for (int64_t br = heads[part][g]; br >= 0; br = next[br]) {
+                if (c == cp) {
+                    cp *= 2;
+                    a = (int64_t*)realloc(a, sizeof(int64_t) * (size_t)cp);
+                    b = (int64_t*)realloc(b, sizeof(int64_t) * (size_t)cp);
+                }
+                a[c] = r;
+                b[c] = br;
+                ++c;
+            }
+        }
+        lp[t] = a;
+        lb[t] = b;
+        cnt[t + 1] = c;
+    }
+    for (int t = 0; t < T; ++t) cnt[t + 1] += cnt[t];
+    const int64_t total = cnt[T];
+    if (total <= cap) {
+#pragma omp parallel for num_threads(T) schedule(static)
+        for (int t = 0; t < T; ++t) {
+            const int64_t o = cnt[t], c = cnt[t + 1] - cnt[t];
+            for (int64_t i = 0; i < c; ++i) {
+                out_k[o + i] = pk[lp[t][i]];
+                out_pv[o + i] = pv[lp[t][i]];
+                out_bv[o + i] = bv[lb[t][i]];
+            }
+        }
+    }
+    for (int t = 0; t < T; ++t) { free(lp[t]); free(lb[t]); }
+    for (int part = 0; part < P; ++part) { imap_free(&tabs[part]); free(heads[part]); }
+    free(lp); free(lb); free(cnt); free(tabs); free(heads); free(next);
+    return total <= cap ? total : -1;
+}

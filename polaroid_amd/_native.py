@@ -104,6 +104,8 @@ SIGNATURES = {
     "plgpu_last_error": (C.c_char_p, []),
     "plgpu_set_option": (C.c_int, [C.c_char_p, C.c_int64]),
     "plgpu_get_option": (C.c_int, [C.c_char_p, C.POINTER(C.c_int64)]),
+    "plgpu_ktime_read": (C.c_int, [C.c_char_p, C.c_int64, C.c_int32]),
+    "plgpu_release_cached": (C.c_int, []),
     "plgpu_debug_checks": (C.c_int, [C.POINTER(C.c_uint32)]),
     "plgpu_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "plgpu_set_device": (C.c_int, [C.c_int]),
@@ -270,6 +272,24 @@ def set_option(name: str, value: int) -> int:
     check(lib().plgpu_get_option(name.encode(), C.byref(prev)))
     check(lib().plgpu_set_option(name.encode(), int(value)))
     return int(prev.value)
+
+
+def release_cached() -> None:
+    """Hand the library allocator's cached free blocks back to HIP."""
+    check(lib().plgpu_release_cached())
+
+
+def ktime_read(reset: bool = True) -> dict:
+    """Per-kernel HIP-event times recorded while option "ktime" was 1
+    (plgpu_ktime_read): {kernel name: (total ms, launches)}."""
+    cap = 1 << 16
+    buf = C.create_string_buffer(cap)
+    check(lib().plgpu_ktime_read(buf, cap, int(bool(reset))))
+    out = {}
+    for line in buf.value.decode().splitlines():
+        name, ms, cnt = line.split("\t")
+        out[name] = (float(ms), int(cnt))
+    return out
 
 
 class option:

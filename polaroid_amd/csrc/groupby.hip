@@ -2558,6 +2558,7 @@ static hipError_t launch_fast_rows(const Plan& pl, const DevProgram& dp, hipStre
         const int64_t nall = pl.p.n_full / tile + (pl.p.n > pl.p.n_full ? 1 : 0);
         q.tiles_per_wg = (int32_t)((nall + grid - 1) / grid);
     }
+    KtScope kt("gb_fast_kernel", s);
     gb_fast_kernel<NACC, PRED, SUMONLY, ROWS, LIMBS, RUNS, false, DERIV, VAR><<<grid, kGbThreads, lds, s>>>(q, dp);
     return hipGetLastError();
 }

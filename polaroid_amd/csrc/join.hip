@@ -771,8 +771,14 @@ template <int NC>
 static hipError_t aos_run(const AosCols& c, int64_t rows, const uint32_t* idx, int64_t n, uint64_t* aos,
                           hipStream_t s) {
     const int g = std::max(1, num_cus_jn() * 16);
-    aos_pack_kernel<NC><<<g, 256, 0, s>>>(c, rows, aos);
-    aos_gather_kernel<NC><<<g, 256, 0, s>>>(aos, idx, n, c);
+    {
+        KtScope kt("aos_pack_kernel", s);
+        aos_pack_kernel<NC><<<g, 256, 0, s>>>(c, rows, aos);
+    }
+    {
+        KtScope kt("aos_gather_kernel", s);
+        aos_gather_kernel<NC><<<g, 256, 0, s>>>(aos, idx, n, c);
+    }
     return hipGetLastError();
 }
 
@@ -984,8 +990,11 @@ static int jn_build_rowformat(const plgpu_column* key, const plgpu_column* pay, 
             const int gi = (int)std::min<int64_t>((ne + 255) / 256, 256 * 32);
             jn_empty_kernel<<<gi, 256, 0, s>>>(b.t);
             const int gb = (int)std::min<int64_t>((nb + 255) / 256, 256 * 32);
-            if (nb > 0) jn_build_rowformat_kernel<<<gb, 256, 0, s>>>(dev_col(*key), nb, b.t, nulls_equal, dev_col(*pay),
-                                                                     status);
+            if (nb > 0) {
+                KtScope kt("jn_build_rowformat_kernel", s);
+                jn_build_rowformat_kernel<<<gb, 256, 0, s>>>(dev_col(*key), nb, b.t, nulls_equal, dev_col(*pay),
+                                                             status);
+            }
             e = hipGetLastError();
         }
         unsigned long long st[4] = {0, 0, 0, 0};
@@ -1063,6 +1072,7 @@ template <int MODE, bool MARK>
 static void jn_launch_match(const DevCol& pk, const JnPass& p, const JnBuilt& b, bool neq, uint8_t* flags,
                             hipStream_t s) {
     const int g = jn_pass_grid(p);
+    KtScope kt("jn_probe_match_kernel", s);
     if (pk.validity)
         jn_probe_match_kernel<true, MODE, MARK><<<g, kJnThreads, 0, s>>>(pk, p.np, b.t, neq, p.m, p.tcount, p.ntiles,
                                                                          flags);
@@ -1099,6 +1109,7 @@ static int jn_emit(const JnPass& p, const JnBuilt& b, int mode, uint32_t* out_p,
                    const uint32_t* rowmap, hipStream_t s) {
     if (p.total == 0) return PLGPU_OK;
     const int g = jn_pass_grid(p);
+    KtScope kt("jn_probe_emit_kernel", s);
     switch (mode) {
     case JM_INNER:
         jn_probe_emit_kernel<JM_INNER><<<g, kJnThreads, 0, s>>>(p.np, b.t, p.m, p.toff, p.ntiles, out_p, out_b, rowmap);
@@ -1426,6 +1437,7 @@ PLGPU_API int plgpu_join_inner(const plgpu_column* left_key, const plgpu_column*
 template <int NC>
 static void jn_take_emit(const JnPass& pp, const TakeCols& lc, uint64_t* mp, uint64_t* out_v, uint32_t* out_idx,
                          hipStream_t s) {
+    KtScope kt("jn_take_emit_kernel", s);
     jn_take_emit_kernel<NC><<<jn_pass_grid(pp), kJnThreads, 0, s>>>(pp.np, (const uint64_t*)pp.m, mp, pp.toff,
                                                                     pp.ntiles, lc, out_v, out_idx);
 }
@@ -1506,6 +1518,7 @@ PLGPU_API int plgpu_join_inner_take(const plgpu_column* left_key, const plgpu_co
     if (!rc) {
         const DevCol pk = as_dev(left_key);
         const int g = jn_pass_grid(pp);
+        KtScope kt("jn_probe_match_kernel", s);
         if (pk.validity)
             jn_probe_match_kernel<true, JM_INNER, false, true><<<g, kJnThreads, 0, s>>>(
                 pk, pp.np, b.t, neq, pp.m, pp.tcount, pp.ntiles, nullptr, mp);

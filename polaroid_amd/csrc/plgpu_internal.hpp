@@ -40,8 +40,30 @@ struct Options {
     int mk_collide = 0;  // 3-bit first tuple hash: forces the collision / re-seed path (tests)
     int runs = -1;       // -1: the plan picks the sorted-key variant; 0 / 1 force it (tests)
     int local = -1;      // -1: the plan picks the range-local kernel; 0 keeps it off (tests)
+    int ktime = 0;       // 1: time the named kernels with HIP events (plgpu_ktime_read)
 };
 Options& options();
+
+// Kernel timer (option "ktime", runtime.cpp): HIP events recorded on the
+// launching stream immediately before and after one named kernel launch,
+// summed per name and read back by plgpu_ktime_read.  The bench reports
+// these live per-kernel times next to its step times, and they are the same
+// quantity a rocprofv3 kernel trace reports.  Off (the default), a scope
+// costs one load and a branch.
+int kt_begin(const char* name, hipStream_t s);
+void kt_end(int slot, hipStream_t s);
+struct KtScope {
+    int slot = -1;
+    hipStream_t s;
+    KtScope(const char* name, hipStream_t st) : s(st) {
+        if (options().ktime) slot = kt_begin(name, st);
+    }
+    ~KtScope() {
+        if (slot >= 0) kt_end(slot, s);
+    }
+    KtScope(const KtScope&) = delete;
+    KtScope& operator=(const KtScope&) = delete;
+};
 int dev_alloc(void** p, size_t bytes, hipStream_t s);
 void dev_free(void* p, hipStream_t s);
 

@@ -911,6 +911,7 @@ PLGPU_API int plgpu_rolling(const plgpu_column* values, int32_t kind, int64_t wi
     if (window_size <= kRwMaxW) {
         const unsigned g = (unsigned)((p.n + (int64_t)kRwOut * kRwWaves - 1) / ((int64_t)kRwOut * kRwWaves));
         const bool nl = p.c.validity != nullptr;
+        KtScope kt("rl_wave_kernel", s);
         if (values->dtype == PLGPU_F64) {
             if (nl) rl_wave_kernel<PLGPU_F64, true><<<g, 64 * kRwWaves, 0, s>>>(p);
             else rl_wave_kernel<PLGPU_F64, false><<<g, 64 * kRwWaves, 0, s>>>(p);

@@ -51,12 +51,61 @@ static Options read_env_options() {
     o.mk_collide = get("PLGPU_MK_COLLIDE", 0);
     o.runs = get("PLGPU_RUNS", -1);
     o.local = get("PLGPU_LOCAL", -1);
+    o.ktime = get("PLGPU_KTIME", 0);
     return o;
 }
 
 Options& options() {
     static Options o = read_env_options();
     return o;
+}
+
+// ------------------------------------------------------------ kernel timer
+// Pending (name, start, stop) event pairs; plgpu_ktime_read waits for them
+// and folds them into per-name sums.  Events are pooled across reads.
+namespace {
+struct KtPending {
+    const char* name;
+    hipEvent_t a, b;
+};
+struct KtSum {
+    std::string name;
+    double ms = 0.0;
+    int64_t count = 0;
+};
+std::mutex g_kt_mu;
+std::vector<KtPending> g_kt_pending;
+std::vector<hipEvent_t> g_kt_pool;
+std::vector<KtSum> g_kt_sums;
+
+hipEvent_t kt_event() {
+    if (!g_kt_pool.empty()) {
+        hipEvent_t e = g_kt_pool.back();
+        g_kt_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+}  // namespace
+
+int kt_begin(const char* name, hipStream_t s) {
+    std::lock_guard<std::mutex> g(g_kt_mu);
+    hipEvent_t a = kt_event(), b = kt_event();
+    if (a == nullptr || b == nullptr || hipEventRecord(a, s) != hipSuccess) {
+        if (a) g_kt_pool.push_back(a);
+        if (b) g_kt_pool.push_back(b);
+        return -1;
+    }
+    g_kt_pending.push_back({name, a, b});
+    return (int)g_kt_pending.size() - 1;
+}
+
+void kt_end(int slot, hipStream_t s) {
+    std::lock_guard<std::mutex> g(g_kt_mu);
+    if (slot < 0 || slot >= (int)g_kt_pending.size()) return;
+    (void)hipEventRecord(g_kt_pending[slot].b, s);
 }
 
 // Caching device allocator.  Blocks come from hipMalloc and are recycled
@@ -718,6 +767,7 @@ PLGPU_API int plgpu_set_option(const char* name, int64_t value) {
     else if (!strcmp(name, "mk_collide")) f = &o.mk_collide;
     else if (!strcmp(name, "runs")) f = &o.runs;
     else if (!strcmp(name, "local")) f = &o.local;
+    else if (!strcmp(name, "ktime")) f = &o.ktime;
     if (f == nullptr) return fail(PLGPU_ERR_INVALID, std::string("unknown option ") + name);
     *f = (int)value;
     return PLGPU_OK;
@@ -731,7 +781,46 @@ PLGPU_API int plgpu_get_option(const char* name, int64_t* out) {
     else if (!strcmp(name, "mk_collide")) *out = o.mk_collide;
     else if (!strcmp(name, "runs")) *out = o.runs;
     else if (!strcmp(name, "local")) *out = o.local;
+    else if (!strcmp(name, "ktime")) *out = o.ktime;
     else return fail(PLGPU_ERR_INVALID, std::string("unknown option ") + name);
+    return PLGPU_OK;
+}
+
+PLGPU_API int plgpu_release_cached(void) {
+    int dev = 0;
+    PLGPU_HIP(hipGetDevice(&dev));
+    PLGPU_HIP(hipDeviceSynchronize());
+    Pool& P = pool_for(dev);
+    std::lock_guard<std::mutex> lk(P.mu);
+    release_cached(P);
+    return PLGPU_OK;
+}
+
+PLGPU_API int plgpu_ktime_read(char* buf, int64_t cap, int32_t reset) {
+    if (buf == nullptr || cap <= 0) return fail(PLGPU_ERR_INVALID, "NULL argument");
+    std::lock_guard<std::mutex> g(g_kt_mu);
+    for (KtPending& p : g_kt_pending) {
+        float ms = 0.f;
+        const hipError_t e = hipEventSynchronize(p.b);
+        if (e == hipSuccess && hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+            auto it = std::find_if(g_kt_sums.begin(), g_kt_sums.end(), [&](const KtSum& k) { return k.name == p.name; });
+            if (it == g_kt_sums.end()) it = g_kt_sums.insert(g_kt_sums.end(), KtSum{p.name, 0.0, 0});
+            it->ms += ms;
+            it->count += 1;
+        }
+        g_kt_pool.push_back(p.a);
+        g_kt_pool.push_back(p.b);
+    }
+    g_kt_pending.clear();
+    std::string out;
+    char line[256];
+    for (const KtSum& k : g_kt_sums) {
+        snprintf(line, sizeof line, "%s\t%.6f\t%lld\n", k.name.c_str(), k.ms, (long long)k.count);
+        out += line;
+    }
+    if (reset) g_kt_sums.clear();
+    if ((int64_t)out.size() + 1 > cap) return fail(PLGPU_ERR_CAPACITY, "ktime buffer too small");
+    std::memcpy(buf, out.c_str(), out.size() + 1);
     return PLGPU_OK;
 }
 

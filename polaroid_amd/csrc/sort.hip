@@ -475,6 +475,7 @@ template <bool IN_P, int OUT>
 static void srt_down(const uint64_t* ki, const uint32_t* ii, int64_t nv, int shift, int64_t ntiles,
                      const uint32_t* off, uint64_t* ko, uint32_t* io, int cons, uint64_t kmask, hipStream_t s) {
     // XCD-aware tiles (round-robin tiles measured slower, profiles/r02_sort_xcd_ab.log)
+    KtScope kt("srt_downsweep_kernel", s);
     srt_downsweep_kernel<IN_P, OUT>
         <<<(unsigned)ntiles, kSrtThreads, 0, s>>>(ki, ii, nv, shift, ntiles, off, ko, io, cons, kmask);
 }
@@ -523,8 +524,10 @@ static int radix_passes(uint64_t* keys[2], uint32_t* idx[2], int64_t nv, int& cu
         const int S = 8 * bytes[j];
         const int shift = packed ? 32 + S - cons : S;
         const uint32_t* ii = (ids_implicit && j == 0) ? nullptr : idx[cur];
-        if (!(pre && j == 0 && S == 0))  // byte-0 counts already in sc.cnt
+        if (!(pre && j == 0 && S == 0)) {  // byte-0 counts already in sc.cnt
+            KtScope kt("srt_upsweep_kernel", s);
             srt_upsweep_kernel<<<(unsigned)ntiles, kSrtThreads, 0, s>>>(keys[cur], nv, shift, ntiles, sc.cnt);
+        }
         e = scan_exclusive32_inplace(sc.cnt, ntiles * 256, sc.part, s);
         if (e != hipSuccess) return hip_fail(e, "sort scan");
         const bool last = j == nb - 1;
@@ -616,6 +619,7 @@ PLGPU_API int plgpu_arg_sort(const plgpu_column* key, int32_t descending, int32_
     if (!rc && stats) {
         // row ids stay implicit (= positions) until the first pass writes them
         const int64_t ntiles = (n + kSrtTile - 1) / kSrtTile;
+        KtScope kt("srt_codes_stats_kernel", s);
         srt_codes_stats_kernel<<<(unsigned)ntiles, kSrtThreads, 0, s>>>(c, n, descending != 0, ntiles, keys[0],
                                                                          sc.cnt, sc.tbits);
         hipError_t e = hipGetLastError();

@@ -435,3 +435,39 @@ def test_sort_multi_matches_python_sorted():
             kb = (kb[0] if not nlb else 1 - kb[0], kb[1])
             return (ka, kb, i)
         assert perm.tolist() == sorted(range(n), key=key)
+
+
+@pytest.mark.parametrize("threads", [1, 3, 8])
+def test_baseline_sort_rolling_matches_oracle(threads):
+    """bench.py's configs[2] cpu_baseline computes the reference's result:
+    the stable sort permutation applied to every column, and rolling_mean
+    equal to the oracle's restatement of the Kahan sliding window."""
+    rng = np.random.default_rng(threads)
+    n = 50_003
+    key = rng.integers(0, 5_000, n).astype(np.int64)  # many ties: stability matters
+    cols = [rng.integers(0, 1 << 20, n).astype(np.int64) for _ in range(4)] + \
+           [100 + rng.random(n) * 50 for _ in range(4)]
+    outs, roll, _ = O.baseline_sort_rolling(key, cols, 4, 20, threads)
+    perm = np.argsort(key, kind="stable")
+    for c, o in zip(cols, outs):
+        assert np.array_equal(o.view(c.dtype), c[perm])
+    want, valid = O.rolling(O.HostCol(cols[4][perm]), "mean", 20)
+    assert np.array_equal(roll[valid].view(np.uint64), want[valid].view(np.uint64))
+
+
+@pytest.mark.parametrize("threads", [1, 4, 8])
+def test_baseline_join_inner_matches_oracle(threads):
+    """bench.py's configs[3] cpu_baseline: the inner join's pairs equal the
+    oracle's (as a multiset; within a thread's probe chunk in row order),
+    duplicate build keys included."""
+    rng = np.random.default_rng(10 + threads)
+    nb, npr = 3_000, 40_000
+    bk = rng.permutation(6_000)[:nb].astype(np.int64)
+    bk[:50] = bk[50:100]  # duplicate build keys
+    bv = rng.random(nb)
+    pk = rng.integers(0, 6_000, npr).astype(np.int64)
+    pv = rng.random(npr)
+    ok, opv, obv = O.baseline_join_inner(pk, pv, bk, bv, threads)
+    li, ri = O.join_inner(O.HostCol(pk), O.HostCol(bk))
+    want = sorted(zip(pk[li].tolist(), pv[li].tolist(), bv[ri].tolist()))
+    assert sorted(zip(ok.tolist(), opv.tolist(), obv.tolist())) == want
