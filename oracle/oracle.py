@@ -81,6 +81,12 @@ def lib():
         L.or_baseline_join_inner.restype = C.c_int64
         L.or_baseline_join_inner.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_int64,
                                              C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]
+        L.or_float_sum.restype = C.c_double
+        L.or_float_sum.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
+        L.or_var_welford.restype = C.c_double
+        L.or_var_welford.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32]
+        L.or_var_chunked.restype = C.c_double
+        L.or_var_chunked.argtypes = [C.c_void_p, C.c_int64, C.c_int32]
         _lib = L
     return _lib
 
@@ -532,3 +538,28 @@ def baseline_join_inner(pk: np.ndarray, pv: np.ndarray, bk: np.ndarray, bv: np.n
     if n < 0:
         raise RuntimeError("baseline join: more output rows than the buffer holds")
     return ok[:n], opv[:n], obv[:n]
+
+
+def float_sum(x: np.ndarray, valid: np.ndarray | None = None) -> float:
+    """The reference's keyless f64 sum of one chunk (polars-compute/src/
+    float_sum.rs sum_arr_as_f64: 16-lane stripes, 128-value pairwise
+    blocks); null values add +0.0."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    v = None if valid is None else np.ascontiguousarray(valid, dtype=np.uint8)
+    return lib().or_float_sum(x.ctypes.data, None if v is None else v.ctypes.data, x.shape[0])
+
+
+def var_welford(x: np.ndarray, part: np.ndarray | None = None, ddof: int = 1) -> float:
+    """The streaming group-by's variance of one group's values in row order
+    (VarState.insert_one per row; one state per `part` id, combined in
+    order); NaN for None."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    p = np.zeros(x.shape[0], np.int64) if part is None else np.ascontiguousarray(part, dtype=np.int64)
+    return lib().or_var_welford(x.ctypes.data, p.ctypes.data, x.shape[0], ddof)
+
+
+def var_chunked(x: np.ndarray, ddof: int = 1) -> float:
+    """The in-memory keyless variance (moment.rs var: VarState::new per
+    128-value chunk, combined in order); NaN for None."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    return lib().or_var_chunked(x.ctypes.data, x.shape[0], ddof)

@@ -1653,3 +1653,115 @@ OR_EXPORT int64_t or_baseline_join_inner(const int64_t* pk, const double* pv, in
     free(lp); free(lb); free(cnt); free(tabs); free(heads); free(next);
     return total <= cap ? total : -1;
 }
+
+/* ------------------------------------------ keyless float sum (pairwise)
+ * polars-compute/src/float_sum.rs sum_arr_as_f64, the fold of the in-memory
+ * engine's keyless `select(x.sum())` / `x.mean()` (ChunkAgg::sum /
+ * _sum_as_f64, polars-core/src/chunked_array/ops/aggregate/mod.rs:68,94,
+ * one call per chunk):
+ *  - the first n % 128 values ("rest") are summed by Iterator::sum; the rest
+ *    of the array ("main", a multiple of 128) pairwise: a block of
+ *    PAIRWISE_RECURSION_LIMIT = 128 values is summed in STRIPE = 16 lanes
+ *    (lane j takes values j, j + 16, ...), the lanes folded 16 -> 8 -> 4 and
+ *    then (v0 + v2) + (v1 + v3) (vector_horizontal_sum); a longer run splits
+ *    at floor(blocks / 2) * 128 and adds the halves (pairwise_sum);
+ *  - masked (null) values contribute +0.0 (a select, not a skip);
+ *  - result: mainsum + restsum.
+ * Iterator::sum of f64 starts from -0.0 on the reference's toolchain
+ * (rust-toolchain.toml: nightly-2025-10-24), so an empty "rest" adds -0.0. */
+static double fs_block(const double* x, const uint8_t* valid) {
+    double v[16];
+    for (int j = 0; j < 16; ++j) v[j] = 0.0;
+    for (int c = 0; c < 128; c += 16)
+        for (int j = 0; j < 16; ++j) v[j] = v[j] + ((valid == NULL || valid[c + j]) ? x[c + j] : 0.0);
+    for (int w = 16; w > 4; w /= 2)
+        for (int j = 0; j < w / 2; ++j) v[j] = v[j] + v[w / 2 + j];
+    return (v[0] + v[2]) + (v[1] + v[3]);
+}
+
+static double fs_pairwise(const double* x, const uint8_t* valid, int64_t n) {
+    if (n == 128) return fs_block(x, valid);
+    const int64_t left = (n / 128 / 2) * 128;
+    return fs_pairwise(x, valid, left) + fs_pairwise(x + left, valid ? valid + left : NULL, n - left);
+}
+
+OR_EXPORT double or_float_sum(const double* x, const uint8_t* valid, int64_t n) {
+    const int64_t rem = n % 128;
+    const double mainsum = n > rem ? fs_pairwise(x + rem, valid ? valid + rem : NULL, n - rem) : 0.0;
+    double restsum = -0.0;
+    for (int64_t i = 0; i < rem; ++i) restsum = restsum + ((valid == NULL || valid[i]) ? x[i] : 0.0);
+    return mainsum + restsum;
+}
+
+/* ------------------------------------------------ variance (VarState)
+ * polars-compute/src/moment.rs VarState (Schubert & Gertz 2018):
+ *  - or_var_welford: the streaming group-by's VarReducer
+ *    (polars-expr/src/reduce/var_std.rs:89 reduce_one -> insert_one per row,
+ *    :84 combine): one state per partition id part[i] (a thread's or a
+ *    morsel's rows), each fed row by row with insert_one, the states combined
+ *    in order; finalize(ddof) (negative -> 0).
+ *  - or_var_chunked: the in-memory keyless `x.var()` (moment.rs:641 var):
+ *    VarState::new over consecutive chunks of CHUNK_SIZE = 128 values (mean
+ *    and squared deviations summed with alg_sum_f64, which lets the compiler
+ *    reassociate; restated in row order), combined in order.
+ * Return NaN for "None" (weight <= ddof). */
+typedef struct { double w, mean, dp; } vs_t;
+
+static void vs_zero_nan(vs_t* s) {
+    if (s->w == 0.0) { s->mean = 0.0; s->dp = 0.0; }
+}
+static void vs_insert(vs_t* s, double x) {
+    const double nw = s->w + 1.0;
+    const double dm = x - s->mean;
+    const double nm = s->mean + dm / nw;
+    s->dp += (x - nm) * dm;
+    s->w = nw;
+    s->mean = nm;
+    vs_zero_nan(s);
+}
+static void vs_combine(vs_t* s, const vs_t* o) {
+    if (o->w == 0.0) return;
+    const double nw = s->w + o->w;
+    const double frac = o->w / nw;
+    const double dm = o->mean - s->mean;
+    const double nm = s->mean + dm * frac;
+    s->dp += o->dp + o->w * (o->mean - nm) * dm;
+    s->w = nw;
+    s->mean = nm;
+    vs_zero_nan(s);
+}
+static double vs_finalize(const vs_t* s, int32_t ddof) {
+    if (s->w <= (double)ddof) return NAN;
+    const double v = s->dp / (s->w - (double)ddof);
+    return v < 0.0 ? 0.0 : v;
+}
+
+OR_EXPORT double or_var_welford(const double* x, const int64_t* part, int64_t n, int32_t ddof) {
+    vs_t tot = {0.0, 0.0, 0.0}, cur = {0.0, 0.0, 0.0};
+    for (int64_t i = 0; i < n; ++i) {
+        if (i > 0 && part[i] != part[i - 1]) {
+            vs_combine(&tot, &cur);
+            cur.w = cur.mean = cur.dp = 0.0;
+        }
+        vs_insert(&cur, x[i]);
+    }
+    vs_combine(&tot, &cur);
+    return vs_finalize(&tot, ddof);
+}
+
+OR_EXPORT double or_var_chunked(const double* x, int64_t n, int32_t ddof) {
+    vs_t tot = {0.0, 0.0, 0.0};
+    for (int64_t c = 0; c < n; c += 128) {
+        const int64_t m = n - c < 128 ? n - c : 128;
+        double s = 0.0;
+        for (int64_t i = 0; i < m; ++i) s += x[c + i];
+        vs_t ch;
+        ch.w = (double)m;
+        ch.mean = s / ch.w;
+        double dp = 0.0;
+        for (int64_t i = 0; i < m; ++i) dp += (x[c + i] - ch.mean) * (x[c + i] - ch.mean);
+        ch.dp = dp;
+        vs_combine(&tot, &ch);
+    }
+    return vs_finalize(&tot, ddof);
+}

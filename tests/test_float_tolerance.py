@@ -58,3 +58,27 @@ def test_rolling_sum_vs_sumwindow():
             assert r["window_ulp"] <= 1.0, r
         elif "40 binades" not in r["data"]:
             assert r["window_rel_abs"] <= 1e-11, r
+
+
+def test_keyless_sum_vs_pairwise_float_sum():
+    """select(x.sum()) / x.mean(): the in-memory engine's pairwise
+    float_sum (16 lanes, 128-value blocks) is within a few ULP of the exact
+    sum the GPU returns (measured 0 / 2 / 3 ULP at 6e6 rows, up to 8 on
+    1e6 mixed-sign rows, where |sum| << sum|x|)."""
+    for r in T.keyless_rows(1_000_000):
+        assert r["sum_pairwise_ulp"] <= 16.0, r
+        assert r["mean_pairwise_ulp"] <= 16.0, r
+        assert r["sum_pairwise_rel_abs"] <= 1e-17, r
+
+
+def test_variance_vs_welford():
+    """var / std: the GPU returns the exact variance of the stored values
+    (within ~2 ULP, tests/test_gpu_var_std.py); the reference's Welford
+    states are themselves tens to ~1e5 ULP away, most where the mean is
+    large against the spread (the price-like set: ~1e4+ ULP)."""
+    rows = T.var_rows(60_000)
+    for r in rows:
+        assert r["var_keyless_chunked_ulp"] <= 1e3, r
+        assert r["var_welford_ulp"] <= 1e6, r
+    prices = next(r for r in rows if r["data"].startswith("mean 1e6"))
+    assert prices["var_welford_ulp"] > 100

@@ -471,3 +471,59 @@ def test_baseline_join_inner_matches_oracle(threads):
     li, ri = O.join_inner(O.HostCol(pk), O.HostCol(bk))
     want = sorted(zip(pk[li].tolist(), pv[li].tolist(), bv[ri].tolist()))
     assert sorted(zip(ok.tolist(), opv.tolist(), obv.tolist())) == want
+
+
+def _float_sum_spec(x, valid=None):
+    """An independent Python reading of float_sum.rs sum_arr_as_f64, to pin
+    the C restatement's lane / block order (no reference fixture covers it)."""
+    x = [float(v) if valid is None or valid[i] else 0.0 for i, v in enumerate(x)]
+    rem = len(x) % 128
+
+    def block(b):
+        lanes = [0.0] * 16
+        for c in range(0, 128, 16):
+            for j in range(16):
+                lanes[j] = lanes[j] + b[c + j]
+        w = 16
+        while w > 4:
+            for j in range(w // 2):
+                lanes[j] = lanes[j] + lanes[w // 2 + j]
+            w //= 2
+        return (lanes[0] + lanes[2]) + (lanes[1] + lanes[3])
+
+    def pairwise(a):
+        if len(a) == 128:
+            return block(a)
+        left = (len(a) // 128 // 2) * 128
+        return pairwise(a[:left]) + pairwise(a[left:])
+
+    main = pairwise(x[rem:]) if len(x) > rem else 0.0
+    rest = -0.0
+    for v in x[:rem]:
+        rest = rest + v
+    return main + rest
+
+
+@pytest.mark.parametrize("n", [0, 1, 127, 128, 129, 255, 256, 384, 1000, 5 * 128 + 17, 20_000])
+def test_float_sum_restatement(n):
+    rng = np.random.default_rng(n)
+    x = rng.standard_normal(n) * np.exp2(rng.integers(-30, 30, n))
+    valid = rng.random(n) > 0.2
+    for v in (None, valid):
+        got = O.float_sum(x, v)
+        want = _float_sum_spec(x, v)
+        assert np.float64(got).view(np.uint64) == np.float64(want).view(np.uint64)
+    # exact inputs: integers below 2^40 sum exactly in any order
+    xi = rng.integers(-2**40, 2**40, n).astype(np.float64)
+    assert O.float_sum(xi) == float(xi.astype(np.int64).sum())
+
+
+def test_variance_restatements():
+    """Welford (insert_one / combine) and the chunked VarState give the
+    textbook variance on exact data and agree with numpy to rounding."""
+    x = np.arange(1, 1001, dtype=np.float64)
+    assert O.var_welford(x) == pytest.approx(float(np.var(x, ddof=1)), rel=1e-15)
+    assert O.var_chunked(x, 0) == pytest.approx(float(np.var(x)), rel=1e-15)
+    part = np.arange(1000) // 100
+    assert O.var_welford(x, part) == pytest.approx(float(np.var(x, ddof=1)), rel=1e-15)
+    assert math.isnan(O.var_welford(x[:1], None, 1)) and O.var_welford(x[:1], None, 0) == 0.0

@@ -15,6 +15,14 @@ oracle's restatements of the reference's folds:
            100,000 rows, then the morsel partials folded in order
   window   polars-compute/src/rolling/sum.rs:7 SumWindow (Kahan add /
            subtract while sliding)
+  pairwise polars-compute/src/float_sum.rs sum_arr_as_f64 (16-lane stripes,
+           128-value pairwise blocks): the in-memory engine's keyless
+           select(x.sum()) / x.mean() (ChunkAgg::sum, aggregate/mod.rs:68,94)
+  welford  polars-compute/src/moment.rs VarState.insert_one per row
+           (reduce/var_std.rs:89), one state per thread / morsel, combined:
+           the streaming group-by's var / std
+  chunked  moment.rs:641 var (VarState::new per 128 values, combined): the
+           in-memory keyless x.var() / x.std()
 
     python tools/tolerance_table.py [--rows-per-group 1500000] [--json out]
 """
@@ -84,6 +92,71 @@ def group_rows(rows_per_group: int, ngroups: int = 4, seed: int = 7):
     return res
 
 
+def keyless_rows(n: int = 6_000_000, seed: int = 5):
+    """select(x.sum()) / select(x.mean()) over one chunk: the reference's
+    pairwise float_sum against the exact sum the GPU returns (and the mean
+    as that sum / count, each rounded once)."""
+    rng = np.random.default_rng(seed)
+    res = []
+    for name, x in datasets(n, rng).items():
+        ex = math.fsum(x)
+        ref = O.float_sum(x)
+        row = {"data": name, "rows": n,
+               "sum_pairwise_ulp": float(ulps(np.array([ref]), np.array([ex]))[0]),
+               "sum_pairwise_rel_abs": abs(ref - ex) / float(np.abs(x).sum()),
+               "mean_pairwise_ulp": float(ulps(np.array([ref / n]), np.array([ex / n]))[0])}
+        res.append(row)
+    return res
+
+
+def exact_var(x: np.ndarray, ddof: int = 1) -> float:
+    """The exact variance of the stored values, rounded once: x as integers
+    over their common lowest exponent, n * sum(x^2) - sum(x)^2 in Python
+    integers, divided as a Fraction."""
+    from fractions import Fraction
+
+    m, e = np.frexp(x)
+    mi = (m * 2.0 ** 53).astype(np.int64)  # exact: |m| in [0.5, 1)
+    e = e.astype(np.int64) - 53
+    lo = int(e.min())
+    s1 = s2 = 0
+    for a, b in zip(mi.tolist(), (e - lo).tolist()):
+        v = a << b
+        s1 += v
+        s2 += v * v
+    n = x.shape[0]
+    num = n * s2 - s1 * s1
+    return float(Fraction(num, n * (n - ddof)) * Fraction(2) ** (2 * lo))
+
+
+def var_rows(n: int = 300_000, ngroups: int = 4, seed: int = 9):
+    """var(ddof=1) per group (streaming Welford, one thread and per morsel)
+    and keyless (chunked VarState) against the exact variance, which the
+    GPU's fused pass returns within ~2 ULP (tests/test_gpu_var_std.py)."""
+    rng = np.random.default_rng(seed)
+    key = rng.integers(0, ngroups, n * ngroups)
+    res = []
+    sets = dict(datasets(n * ngroups, rng))
+    sets["mean 1e6, spread 3 (prices)"] = 1e6 + rng.standard_normal(n * ngroups) * 3.0
+    for name, x in sets.items():
+        worst = {"welford": 0.0, "welford_morsel": 0.0}
+        for g in range(ngroups):
+            sel = np.nonzero(key == g)[0]
+            xs = x[sel]
+            ex = exact_var(xs)
+            w1 = O.var_welford(xs)
+            wm = O.var_welford(xs, sel // MORSEL)
+            worst["welford"] = max(worst["welford"], float(ulps(np.array([w1]), np.array([ex]))[0]))
+            worst["welford_morsel"] = max(worst["welford_morsel"], float(ulps(np.array([wm]), np.array([ex]))[0]))
+        exk = exact_var(x)
+        ck = O.var_chunked(x)
+        res.append({"data": name, "rows_per_group": int(np.bincount(key).min()),
+                    "var_welford_ulp": worst["welford"], "var_welford_morsel_ulp": worst["welford_morsel"],
+                    "keyless_rows": int(x.shape[0]),
+                    "var_keyless_chunked_ulp": float(ulps(np.array([ck]), np.array([exk]))[0])})
+    return res
+
+
 def rolling_rows(n: int = 1_000_000, seed: int = 11):
     rng = np.random.default_rng(seed)
     res = []
@@ -108,6 +181,8 @@ def main():
     args = ap.parse_args()
     g = group_rows(args.rows_per_group)
     r = rolling_rows(args.rolling_rows)
+    k = keyless_rows()
+    v = var_rows()
     print("| data | rows/group | sum vs kahan ulp | vs naive ulp | vs morsel ulp | naive rel. to sum|x| | "
           "mean vs kahan ulp | mean vs naive ulp |")
     print("|---|---|---|---|---|---|---|---|")
@@ -120,8 +195,20 @@ def main():
     print("|---|---|---|---|")
     for x in r:
         print(f"| {x['data']} | {x['window']} | {x['window_ulp']:.3g} | {x['window_rel_abs']:.2e} |")
+    print()
+    print("| data | rows | select sum vs pairwise float_sum ulp | rel. to sum|x| | select mean ulp |")
+    print("|---|---|---|---|---|")
+    for x in k:
+        print(f"| {x['data']} | {x['rows']:,} | {x['sum_pairwise_ulp']:.3g} | {x['sum_pairwise_rel_abs']:.2e} | "
+              f"{x['mean_pairwise_ulp']:.3g} |")
+    print()
+    print("| data | rows/group | group var vs Welford ulp (one thread) | per morsel | keyless var vs chunked ulp |")
+    print("|---|---|---|---|---|")
+    for x in v:
+        print(f"| {x['data']} | {x['rows_per_group']:,} | {x['var_welford_ulp']:.3g} | "
+              f"{x['var_welford_morsel_ulp']:.3g} | {x['var_keyless_chunked_ulp']:.3g} |")
     if args.json:
-        json.dump({"group_by": g, "rolling": r}, open(args.json, "w"), indent=1)
+        json.dump({"group_by": g, "rolling": r, "keyless": k, "var": v}, open(args.json, "w"), indent=1)
 
 
 if __name__ == "__main__":
