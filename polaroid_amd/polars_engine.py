@@ -256,6 +256,8 @@ class _Translator:
         name = str(e.name)
         if len(e.arguments) != 1:
             raise Unsupported("multi-argument aggregation")
+        if name in ("min", "max") and self._is_enum(e.arguments[0]):
+            raise Unsupported(f"{name} of an Enum column (category order)")
         if schema is not None:
             kind = self.expr_kind(e.arguments[0], schema)
             if kind == "String":
