@@ -210,6 +210,8 @@ typedef struct plgpu_groupby_info {
     int32_t sum_limbs;           /* 40-bit LDS limbs per f64 sum (2 or 3)      */
     int32_t local_range;         /* 1: range-local fused kernel (clustered keys) */
     int32_t register_runs;       /* 1: fused kernel with per-lane register runs (sorted keys) */
+    int32_t key_pack;            /* key columns packed in the fused kernel's registers (0: a key / code column) */
+    int32_t _reserved;
 } plgpu_groupby_info;
 
 /* ---------------------------------------------------------------- basics */
@@ -228,6 +230,9 @@ int plgpu_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream);
 
 /* Test hooks and diagnostics, each read once from the environment variable
  * PLGPU_<NAME> (upper case) when the library loads and settable here:
+ *   "ktime"       1: time the named kernels with HIP events (plgpu_ktime_read)
+ *   "fuse_keys"   0: multi-key / Categorical group-bys write their packed
+ *                 code column instead of forming the codes in the fused kernel
  *   "debug"       per-attempt group-by diagnostics on stderr
  *   "no_pack"     multi-key operators hash their key tuples even when the
  *                 tuples would pack into one Int64 (exercises the hashed path)

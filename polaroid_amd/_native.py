@@ -90,6 +90,8 @@ class GroupByInfo(C.Structure):
         ("sum_limbs", C.c_int32),
         ("local_range", C.c_int32),
         ("register_runs", C.c_int32),
+        ("key_pack", C.c_int32),
+        ("_reserved", C.c_int32),
     ]
 
     def as_dict(self) -> dict:

@@ -76,7 +76,8 @@ enum : int {
     ST_RUNS = 23,        // plan: sampled adjacent row pairs with equal keys (sorted / clustered keys)
     ST_LOCAL = 24,       // plan: most distinct keys among the samples of one 1/kPlanKeyBlocks row range
     ST_VAR_OUT = 25,     // finalize: a fused variance whose exact state left its range (caller reruns)
-    ST_WORDS = 26
+    ST_KPACK = 26,       // fused key packing: a selected row's key field left its planned bits (caller repacks)
+    ST_WORDS = 27
 };
 
 // An aggregation input derived from the columns in registers (an
@@ -105,6 +106,24 @@ struct AccSpec {
     uint64_t dimm;    // derived: the literal operand's f64 bits (DOP_LIT)
     int32_t v_from;   // fused kernel (DERIV): c is acc v_from's column too (-1: own load)
     int32_t w_from;   // fused kernel (DERIV): c2 is acc w_from's column (-1: own load)
+};
+
+// Fused key packing (round 4): the group key of row r is the exact Int64
+// code of the tuple of up to kKpMax null-free Int64 / Int32 / UInt32 key
+// columns in mk_plan_pack's layout (field i = v - minv[i] + nul[i] at bit
+// shift[i], polars-core/src/chunked_array/ops/row_encode.rs:189 encodes
+// the same tuple as bytes), formed in registers from the key columns as the
+// tile arrives -- no code column is written or read.  n = 0: the key is
+// GbParams::key itself.  A selected row whose field leaves its bits sets
+// ST_KPACK and the caller repacks with the exact ranges.
+constexpr int kKpMax = 4;
+struct KeyPack {
+    int32_t n;
+    int32_t _pad;
+    DevCol c[kKpMax];
+    uint64_t base[kKpMax];  // minv[i] - nul[i] (wrapping): field i = v - base[i]
+    int32_t shift[kKpMax];
+    int32_t bits[kKpMax];
 };
 
 struct GbParams {
@@ -144,6 +163,7 @@ struct GbParams {
     // contiguous tiles [b * tiles_per_wg, (b + 1) * tiles_per_wg); 0 = the
     // grid-strided tile order
     int32_t tiles_per_wg;
+    KeyPack kp;             // fused key packing (kp.n > 0): the key is the packed tuple code
 };
 
 // ------------------------------------------------------ invariant checks
@@ -216,6 +236,31 @@ __device__ __forceinline__ uint64_t acc_value(const AccSpec& ac, int64_t r, bool
 // reduction, select(agg...)): every row in the one group 0.
 __device__ __forceinline__ uint64_t key_at(const DevCol& k, int64_t r) {
     return k.values ? dev_load(k, r) : 0ull;
+}
+
+// Field i of a packed key from the column's loaded word (`raw`: the 8-byte
+// value, or a 4-byte value in the low half), OR-ing into `bad` when it does
+// not fit its planned bits.
+__device__ __forceinline__ uint64_t kp_field(const KeyPack& k, int i, uint64_t raw, bool& bad) {
+    const int32_t dt = k.c[i].dtype;
+    const uint64_t v = dt == PLGPU_I32 ? (uint64_t)(int64_t)(int32_t)(uint32_t)raw
+                                       : (dt == PLGPU_U32 ? (uint64_t)(uint32_t)raw : raw);
+    const uint64_t f = v - k.base[i];
+    bad |= k.bits[i] < 64 && (f >> k.bits[i]) != 0;
+    return f << k.shift[i];
+}
+
+// The group key of row r as every pass but the fused kernel's tile loads
+// reads it: the key column, or the packed code of the key columns.
+__device__ __forceinline__ uint64_t gb_key(const GbParams& p, int64_t r) {
+    if (p.kp.n == 0) return key_at(p.key, r);
+    uint64_t code = 0;
+    bool bad = false;
+    for (int i = 0; i < p.kp.n; ++i) code |= kp_field(p.kp, i, dev_load(p.kp.c[i], r), bad);
+    return code;
+}
+__device__ __forceinline__ bool gb_key_valid(const GbParams& p, int64_t r) {
+    return p.kp.n > 0 || dev_valid(p.key, r);
 }
 
 __device__ __forceinline__ uint64_t lds_load(uint64_t* p) {
@@ -351,6 +396,7 @@ struct ThreadDiag {
     uint32_t nsel;
     uint32_t nglobal;
     uint32_t special;
+    uint32_t kbad;     // fused key packing: a selected row's field left its bits
 };
 
 // Packed per-acc descriptor word (uniform): field indices and flags, so the
@@ -522,6 +568,7 @@ __device__ __forceinline__ void flush_and_report(const GbParams& p, uint64_t* ld
     }
     uint64_t nsel = d.nsel, nglob = d.nglobal;
     uint32_t special = d.special, fx = d.fxbits;
+    const bool kbad = __any(d.kbad != 0);
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
         nsel += __shfl_xor(nsel, off, 64);
@@ -530,6 +577,7 @@ __device__ __forceinline__ void flush_and_report(const GbParams& p, uint64_t* ld
         fx |= __shfl_xor(fx, off, 64);
     }
     if ((threadIdx.x & 63) == 0) {
+        if (kbad) atomicOr((unsigned long long*)&p.status[ST_KPACK], 1ull);
         if (nsel) atomicAdd((unsigned long long*)&p.status[ST_SELECTED], (unsigned long long)nsel);
         if (nglob) atomicAdd((unsigned long long*)&p.status[ST_GLOBAL_ROWS], (unsigned long long)nglob);
         if (special) atomicOr((unsigned long long*)&p.status[ST_SPECIAL], (unsigned long long)special);
@@ -567,7 +615,7 @@ __global__ __launch_bounds__(kGbThreads) void gb_kernel(GbParams p, DevProgram p
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
     const int L = p.lcap + 2;
     if (USE_LDS) init_lds(p, lds, L);
-    ThreadDiag d = {0u, 0u, 0u, 0u};
+    ThreadDiag d = {0u, 0u, 0u, 0u, 0u};
     const int nacc = p.nacc;
     uint64_t dd0[kMaxAcc];
     int bot0[kMaxAcc];
@@ -930,9 +978,13 @@ __global__ __launch_bounds__(kPartThreads) void gb_part_scatter_kernel(GbParams 
 // tail and every other case go through gb_kernel.  Loads of the next tile
 // are issued before the current tile's LDS atomics, so HBM reads overlap
 // the aggregation.
-template <int NACC, int ROWS, bool DERIV = false>
+// PACK: the key is formed from up to kKpFast packed key columns (KeyPack),
+// whose raw words the tile holds until its rows are consumed.
+constexpr int kKpFast = 2;
+template <int NACC, int ROWS, bool DERIV = false, bool PACK = false>
 struct FastTile {
     uint64_t key[ROWS];
+    uint64_t kr[PACK ? kKpFast : 1][ROWS];
     uint64_t v[NACC > 0 ? NACC : 1][ROWS];
     uint64_t w[DERIV && NACC > 0 ? NACC : 1][ROWS];  // DERIV: second operand columns
     uint64_t pv[ROWS];
@@ -956,15 +1008,20 @@ __device__ __forceinline__ u64x2_t ld16(const uint64_t* p) {
 // The rows after the last full tile (fewer than one tile): one more, masked
 // tile of guarded single-row loads (rows >= n read as 0 and are not
 // selected), so the fused kernel covers every row in one launch.
-template <int NACC, int PRED, int ROWS, bool DERIV>
-__device__ __forceinline__ void fast_load_tail(const GbParams& p, int64_t t, FastTile<NACC, ROWS, DERIV>& x) {
+template <int NACC, int PRED, int ROWS, bool DERIV, bool PACK>
+__device__ __forceinline__ void fast_load_tail(const GbParams& p, int64_t t, FastTile<NACC, ROWS, DERIV, PACK>& x) {
     const int T = blockDim.x;
     const uint64_t* kp = (const uint64_t*)p.key.values + p.key.offset;
 #pragma unroll
     for (int j = 0; j < ROWS; ++j) {
         const int64_t r = fast_row(t, T, ROWS, j);
         const bool in = r < p.n;
-        x.key[j] = in && p.key.values ? kp[r] : 0ull;
+        if (PACK) {
+#pragma unroll
+            for (int i = 0; i < kKpFast; ++i) x.kr[i][j] = in && i < p.kp.n ? dev_load(p.kp.c[i], r) : 0ull;
+        } else {
+            x.key[j] = in && p.key.values ? kp[r] : 0ull;
+        }
 #pragma unroll
         for (int c = 0; c < NACC; ++c) {
             if (!DERIV || p.acc[c].v_from < 0)
@@ -978,8 +1035,10 @@ __device__ __forceinline__ void fast_load_tail(const GbParams& p, int64_t t, Fas
 
 // rbase: first row of tile 0 (even); rmax >= 0: row pairs beyond it are
 // clamped to it (the partitioned buffers end a pair after the last row).
-template <int NACC, int PRED, int ROWS, bool NT, bool DERIV>
-__device__ __forceinline__ void fast_load(const GbParams& p, int64_t t, FastTile<NACC, ROWS, DERIV>& x,
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+
+template <int NACC, int PRED, int ROWS, bool NT, bool DERIV, bool PACK>
+__device__ __forceinline__ void fast_load(const GbParams& p, int64_t t, FastTile<NACC, ROWS, DERIV, PACK>& x,
                                           int64_t rbase = 0, int64_t rmax = -1) {
     const int T = blockDim.x;
     const uint64_t* kp = (const uint64_t*)p.key.values + p.key.offset;
@@ -987,7 +1046,28 @@ __device__ __forceinline__ void fast_load(const GbParams& p, int64_t t, FastTile
     for (int q = 0; q < ROWS / 2; ++q) {
         int64_t r = rbase + fast_row(t, T, ROWS, 2 * q);
         if (rmax >= 0) r = r < rmax ? r : rmax;
-        if (p.key.values) {
+        if (PACK) {
+            // each packed key column: one 16-byte (Int64) or 8-byte (Int32 /
+            // UInt32) load per row pair, kept raw until the rows are consumed
+#pragma unroll
+            for (int i = 0; i < kKpFast; ++i) {
+                if (i >= p.kp.n) {
+                    x.kr[i][2 * q] = x.kr[i][2 * q + 1] = 0;
+                    continue;
+                }
+                const DevCol& kc = p.kp.c[i];
+                if (kc.dtype == PLGPU_I64) {
+                    const u64x2_t a = ld16<NT>((const uint64_t*)kc.values + kc.offset + r);
+                    x.kr[i][2 * q] = a.x;
+                    x.kr[i][2 * q + 1] = a.y;
+                } else {
+                    const u32x2_t* ap = reinterpret_cast<const u32x2_t*>((const uint32_t*)kc.values + kc.offset + r);
+                    const u32x2_t a = NT ? __builtin_nontemporal_load(ap) : *ap;
+                    x.kr[i][2 * q] = a.x;
+                    x.kr[i][2 * q + 1] = a.y;
+                }
+            }
+        } else if (p.key.values) {
             const u64x2_t a = ld16<NT>(kp + r);
             x.key[2 * q] = a.x;
             x.key[2 * q + 1] = a.y;
@@ -1021,10 +1101,10 @@ __device__ __forceinline__ void fast_load(const GbParams& p, int64_t t, FastTile
 // DERIV: fill the operand registers whose column another acc loaded
 // (v_from / w_from, uniform), once the tile's loads are being consumed --
 // not at prefetch time, where the copy would wait for the loads.
-template <int NACC, int ROWS, bool DERIV>
+template <int NACC, int ROWS, bool DERIV, bool PACK>
 __device__ __forceinline__ void fast_share(const int32_t (&vf)[NACC > 0 ? NACC : 1],
                                            const int32_t (&wf)[NACC > 0 ? NACC : 1],
-                                           FastTile<NACC, ROWS, DERIV>& x) {
+                                           FastTile<NACC, ROWS, DERIV, PACK>& x) {
     if (!DERIV) return;
 #pragma unroll
     for (int c = 0; c < NACC; ++c)
@@ -1060,9 +1140,12 @@ __device__ __forceinline__ void fast_share(const int32_t (&vf)[NACC > 0 ? NACC :
 // 80-VGPR caps, 4 rows per thread -- are logged in DESIGN.md.)
 // DERIV: some accs are derived inputs (x op y, AccSpec.dop), computed in
 // registers from the loaded operand columns as each row is applied.
+// PACK: the key is the fused packed code of p.kp's (at most kKpFast) key
+// columns (KeyPack), formed as each tile's rows are consumed.
 template <int NACC, int PRED, bool SUMONLY, int ROWS, int LIMBS = 3, bool RUNS = false, bool PART = false,
-          bool DERIV = false, bool VAR = false>
+          bool DERIV = false, bool VAR = false, bool PACK = false>
 __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProgram prog) {
+    static_assert(!PACK || !PART, "PACK: the single-table kernel");
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
     constexpr int NA = NACC > 0 ? NACC : 1;
     // VAR (sum-only, NACC 3): the fused variance's three sums of one column
@@ -1086,7 +1169,7 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
     } else {
         init_lds(p, lds, L);
     }
-    ThreadDiag d = {0u, 0u, 0u, 0u};
+    ThreadDiag d = {0u, 0u, 0u, 0u, 0u};
     uint64_t dd0[NA];
     int bot0[NA];
     load_descs(p, dd0, bot0);
@@ -1126,10 +1209,21 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
         t = blockIdx.x % p.part_blocks;
         tstep = p.part_blocks;
     }
-    auto load_tile = [&](int64_t tt, FastTile<NL, ROWS, DERIV>& x) {
-        if (PART || tt < ntiles) fast_load<NL, PRED, ROWS, true, DERIV>(p, tt, x, rbase, rmax);
-        else fast_load_tail<NL, PRED, ROWS, DERIV>(p, tt, x);
+    auto load_tile = [&](int64_t tt, FastTile<NL, ROWS, DERIV, PACK>& x) {
+        if (PART || tt < ntiles) fast_load<NL, PRED, ROWS, true, DERIV, PACK>(p, tt, x, rbase, rmax);
+        else fast_load_tail<NL, PRED, ROWS, DERIV, PACK>(p, tt, x);
     };
+    // PACK: the plan's field bases / shifts / widths, hoisted (uniform)
+    uint64_t kpb[kKpFast];
+    int32_t kpsh[kKpFast], kpbits[kKpFast], kpdt[kKpFast];
+#pragma unroll
+    for (int i = 0; i < kKpFast; ++i) {
+        const bool on = PACK && i < p.kp.n;
+        kpb[i] = on ? p.kp.base[i] : 0ull;
+        kpsh[i] = on ? p.kp.shift[i] : 0;
+        kpbits[i] = on ? p.kp.bits[i] : 64;
+        kpdt[i] = on ? p.kp.c[i].dtype : PLGPU_I64;
+    }
     constexpr uint32_t VM = (1u << NACC) - 1u;
     // RACC (partition buffers, sum-only, 2 limbs): each lane keeps KR
     // register accumulators {slot, len, limbs} and adds a row whose group
@@ -1260,10 +1354,29 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
         }
         return true;
     };
-    FastTile<NL, ROWS, DERIV> cur;
+    FastTile<NL, ROWS, DERIV, PACK> cur;
     if (t < nall) load_tile(t, cur);
     for (; t < nall; t += tstep) {
-        if constexpr (!VAR) fast_share<NACC, ROWS, DERIV>(vf0, wf0, cur);
+        if constexpr (!VAR) fast_share<NACC, ROWS, DERIV, PACK>(vf0, wf0, cur);
+        bool kout[ROWS];
+#pragma unroll
+        for (int j = 0; j < ROWS; ++j) {
+            kout[j] = false;
+            if (PACK) {
+                // the packed code of row j (mk_plan_pack's layout)
+                uint64_t code = 0;
+#pragma unroll
+                for (int i = 0; i < kKpFast; ++i) {
+                    const uint64_t raw = cur.kr[i][j];
+                    const uint64_t v = kpdt[i] == PLGPU_I32 ? (uint64_t)(int64_t)(int32_t)(uint32_t)raw
+                                                            : (kpdt[i] == PLGPU_U32 ? (uint64_t)(uint32_t)raw : raw);
+                    const uint64_t f = v - kpb[i];
+                    kout[j] |= kpbits[i] < 64 && (f >> kpbits[i]) != 0;
+                    code |= f << kpsh[i];
+                }
+                cur.key[j] = code;
+            }
+        }
         // ---- predicate + batched LDS probes of the tile's rows
         int slot[ROWS];
         uint64_t probe[ROWS];
@@ -1288,6 +1401,7 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
             } else if (t >= ntiles) {
                 sel = sel && fast_row(t, T, ROWS, j) < p.n;
             }
+            if (PACK && sel && kout[j]) d.kbad = 1u;
             slot[j] = sel ? (cur.key[j] == kEmptyKey ? p.lcap + 1 : kGlobalKey) : kNotSelected;
             h[j] = hash_slot(cur.key[j], p.lbits);
             probe[j] = lds_load(&lds[h[j]]);
@@ -1296,7 +1410,7 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
         for (int j = 0; j < ROWS; ++j)
             if (slot[j] == kGlobalKey && probe[j] == cur.key[j]) slot[j] = (int)h[j];
         // ---- next tile's loads go out before this tile's atomics
-        FastTile<NL, ROWS, DERIV> nxt;
+        FastTile<NL, ROWS, DERIV, PACK> nxt;
         const int64_t tn = t + tstep;
         if (tn < nall) load_tile(tn, nxt);
         // ---- apply rows one at a time (rolled; arrays shift statically)
@@ -1533,10 +1647,10 @@ __global__ __launch_bounds__(256) void gb_wide_kernel(GbParams p, DevProgram pro
         if (ex == 0) ex = 1;
         else m |= 1ull << 52;
         int64_t gs;
-        if (!dev_valid(p.key, r)) {
+        if (!gb_key_valid(p, r)) {
             gs = p.gcap;
         } else {
-            const uint64_t k = key_at(p.key, r);
+            const uint64_t k = gb_key(p, r);
             gs = k == kEmptyKey ? p.gcap + 1 : g_find(p, k);
         }
         if (gs < 0) continue;
@@ -1670,10 +1784,10 @@ __global__ __launch_bounds__(kPlanThreads) void gb_plan_kernel(GbParams p, uint6
           for (int u = 0; u < kPlanBatch; ++u) {
             const int64_t i = i0 + (int64_t)u * blockDim.x;
             const int64_t r = plan_row(i, n, samples);
-            okb[u] = i < s1 && r < n && dev_valid(p.key, r);
-            kb[u] = okb[u] ? key_at(p.key, r) : 0;
-            const bool nx = okb[u] && r + 1 < n && dev_valid(p.key, r + 1);
-            runs += (nx && key_at(p.key, r + 1) == kb[u]) ? 1u : 0u;
+            okb[u] = i < s1 && r < n && gb_key_valid(p, r);
+            kb[u] = okb[u] ? gb_key(p, r) : 0;
+            const bool nx = okb[u] && r + 1 < n && gb_key_valid(p, r + 1);
+            runs += (nx && gb_key(p, r + 1) == kb[u]) ? 1u : 0u;
           }
 #pragma unroll 1
           for (int u = 0; u < kPlanBatch; ++u) {
@@ -2530,10 +2644,11 @@ static int resident_per_cu(const void* kern, int threads, size_t lds) {
     return nb;
 }
 
-template <int NACC, int PRED, bool SUMONLY, int LIMBS = 3, bool RUNS = false, bool DERIV = false, bool VAR = false>
+template <int NACC, int PRED, bool SUMONLY, int LIMBS = 3, bool RUNS = false, bool DERIV = false, bool VAR = false,
+          bool PACK = false>
 static hipError_t launch_fast_rows(const Plan& pl, const DevProgram& dp, hipStream_t s) {
     constexpr int ROWS = 2;
-    const void* kern = (const void*)gb_fast_kernel<NACC, PRED, SUMONLY, ROWS, LIMBS, RUNS, false, DERIV, VAR>;
+    const void* kern = (const void*)gb_fast_kernel<NACC, PRED, SUMONLY, ROWS, LIMBS, RUNS, false, DERIV, VAR, PACK>;
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -2559,24 +2674,28 @@ static hipError_t launch_fast_rows(const Plan& pl, const DevProgram& dp, hipStre
         q.tiles_per_wg = (int32_t)((nall + grid - 1) / grid);
     }
     KtScope kt("gb_fast_kernel", s);
-    gb_fast_kernel<NACC, PRED, SUMONLY, ROWS, LIMBS, RUNS, false, DERIV, VAR><<<grid, kGbThreads, lds, s>>>(q, dp);
+    gb_fast_kernel<NACC, PRED, SUMONLY, ROWS, LIMBS, RUNS, false, DERIV, VAR, PACK>
+        <<<grid, kGbThreads, lds, s>>>(q, dp);
     return hipGetLastError();
 }
 
-template <int NACC, int PRED, bool SUMONLY, bool DERIV>
+template <int NACC, int PRED, bool SUMONLY, bool DERIV, bool PACK = false>
 static hipError_t launch_fast(const Plan& pl, const DevProgram& dp, hipStream_t s) {
-    if (SUMONLY && pl.limbs == 2 && pl.runs) return launch_fast_rows<NACC, PRED, SUMONLY, 2, true, DERIV>(pl, dp, s);
-    if (SUMONLY && pl.limbs == 2) return launch_fast_rows<NACC, PRED, SUMONLY, 2, false, DERIV>(pl, dp, s);
+    if (SUMONLY && pl.limbs == 2 && pl.runs)
+        return launch_fast_rows<NACC, PRED, SUMONLY, 2, true, DERIV, false, PACK>(pl, dp, s);
+    if (SUMONLY && pl.limbs == 2) return launch_fast_rows<NACC, PRED, SUMONLY, 2, false, DERIV, false, PACK>(pl, dp, s);
     if (!SUMONLY && NACC > 0 && !DERIV && pl.runs && pl.limbs == 2)
-        return launch_fast_rows<NACC, PRED, false, 2, true, false>(pl, dp, s);
-    return launch_fast_rows<NACC, PRED, SUMONLY, 3, false, DERIV>(pl, dp, s);
+        return launch_fast_rows<NACC, PRED, false, 2, true, false, false, PACK>(pl, dp, s);
+    return launch_fast_rows<NACC, PRED, SUMONLY, 3, false, DERIV, false, PACK>(pl, dp, s);
 }
 
-template <int NACC, bool DERIV>
+template <int NACC, bool DERIV, bool PACK = false>
 static hipError_t launch_fast_nacc(const Plan& pl, const DevProgram& dp, int pred, hipStream_t s) {
     if (pl.sum_only)
-        return pred == 0 ? launch_fast<NACC, 0, true, DERIV>(pl, dp, s) : launch_fast<NACC, 1, true, DERIV>(pl, dp, s);
-    return pred == 0 ? launch_fast<NACC, 0, false, DERIV>(pl, dp, s) : launch_fast<NACC, 1, false, DERIV>(pl, dp, s);
+        return pred == 0 ? launch_fast<NACC, 0, true, DERIV, PACK>(pl, dp, s)
+                         : launch_fast<NACC, 1, true, DERIV, PACK>(pl, dp, s);
+    return pred == 0 ? launch_fast<NACC, 0, false, DERIV, PACK>(pl, dp, s)
+                     : launch_fast<NACC, 1, false, DERIV, PACK>(pl, dp, s);
 }
 
 // The fused variance's triple (x, x * x, its error: three sums of one
@@ -2605,6 +2724,20 @@ static hipError_t launch_fast_var(const Plan& pl, const DevProgram& dp, hipStrea
 static hipError_t launch_fast_dispatch(const Plan& pl, const DevProgram& dp, int pred, hipStream_t s) {
     bool dv = false;
     for (int a = 0; a < pl.p.nacc; ++a) dv = dv || pl.p.acc[a].dop != DOP_NONE;
+    if (pl.p.kp.n > 0) {
+        // fused key packing: plain (non-derived) inputs only (gb_plan
+        // guarantees it, falling back to a code column otherwise)
+        if (dv || pl.p.kp.n > kKpFast) return hipErrorInvalidValue;
+        switch (pl.p.nacc) {
+        case 0: return launch_fast_nacc<0, false, true>(pl, dp, pred, s);
+        case 1: return launch_fast_nacc<1, false, true>(pl, dp, pred, s);
+        case 2: return launch_fast_nacc<2, false, true>(pl, dp, pred, s);
+        case 3: return launch_fast_nacc<3, false, true>(pl, dp, pred, s);
+        case 4: return launch_fast_nacc<4, false, true>(pl, dp, pred, s);
+        case 5: return launch_fast_nacc<5, false, true>(pl, dp, pred, s);
+        default: return launch_fast_nacc<6, false, true>(pl, dp, pred, s);
+        }
+    }
     if (dv && var_triple(pl) && !pl.runs)
         return pred == 0 ? launch_fast_var<0>(pl, dp, s) : launch_fast_var<1>(pl, dp, s);
     if (dv) {
@@ -2629,6 +2762,7 @@ static hipError_t launch_fast_dispatch(const Plan& pl, const DevProgram& dp, int
 }
 
 static hipError_t launch_main_dispatch(const Plan& pl, const DevProgram& dp, int pred, hipStream_t s) {
+    if (pl.p.kp.n > 0) return hipErrorInvalidValue;  // the generic kernel reads a key column
     if (pl.use_lds) {
         if (pred == 0) return launch_main<0, true>(pl, dp, s);
         if (pred == 1) return launch_main<1, true>(pl, dp, s);
@@ -2737,6 +2871,11 @@ struct GbRun {
     int64_t* wide_digits[kMaxAcc] = {nullptr};
     double* wide_sum[kMaxAcc] = {nullptr};
     int64_t est_groups = -1;                 // plan's group estimate (sampled / HLL)
+    // fused key packing (p.kp.n > 0): the plan found the fused kernel does
+    // not apply (kp_fallback), or a selected row left the packing plan
+    // (kp_bad); the caller then writes a code column / repacks
+    bool kp_fallback = false;
+    bool kp_bad = false;
     // partitioned path (gb_partition): buffers, ranges, launch shape
     bool part = false;
     int pbits = 0;
@@ -2995,6 +3134,11 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
     if (clustered && R.st[ST_DISTINCT] >= (uint64_t)kPlanSetSlots / 2)
         hll = std::min<int64_t>(n, (int64_t)local * kPlanKeyBlocks * 2);
     if (hll < 0 && R.st[ST_DISTINCT] >= (uint64_t)kPlanSetSlots / 2 && n > 4 * (int64_t)kPlanSamples) {
+        if (p.kp.n > 0) {
+            // many groups: not the fused single-table kernel's case
+            R.kp_fallback = true;
+            return PLGPU_OK;
+        }
         uint32_t* regs = nullptr;
         std::vector<uint32_t> h(1 << kHllBits);
         int rc = dev_alloc((void**)&regs, h.size() * 4, R.s);
@@ -3039,7 +3183,17 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
         return (c.dtype == PLGPU_I64 || c.dtype == PLGPU_F64) && c.validity == nullptr && (c.offset & 1) == 0 &&
                ((uintptr_t)c.values & 15) == 0;
     };
-    bool fast = pl.use_lds && R.pred != 2 && ok(p.key);
+    auto ok_kp = [](const KeyPack& k) {
+        bool good = k.n > 0 && k.n <= kKpFast;
+        for (int i = 0; i < k.n && good; ++i) {
+            const DevCol& c = k.c[i];
+            const bool w8 = c.dtype == PLGPU_I64, w4 = c.dtype == PLGPU_I32 || c.dtype == PLGPU_U32;
+            good = (w8 || w4) && c.validity == nullptr && (c.offset & 1) == 0 &&
+                   ((uintptr_t)c.values & (w8 ? 15 : 7)) == 0;
+        }
+        return good;
+    };
+    bool fast = pl.use_lds && R.pred != 2 && (p.kp.n > 0 ? ok_kp(p.kp) : ok(p.key));
     for (int a = 0; a < p.nacc; ++a) {
         fast = fast && ok(p.acc[a].c);
         if (p.acc[a].dop != DOP_NONE && !(p.acc[a].dop & DOP_LIT)) fast = fast && ok(p.acc[a].c2);
@@ -3127,6 +3281,11 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
         }
     }
     if (R.part) p.n_full = 0, p.row_begin = 0;
+    if (p.kp.n > 0 && (p.n_full == 0 || R.part || gb_has_fused(R))) {
+        // the packed key lives only in the fused kernel's registers
+        R.kp_fallback = true;
+        return PLGPU_OK;
+    }
     // fused derived inputs run in the fused kernel only; any other pass
     // reads them materialised
     if (gb_has_fused(R) && (p.n_full == 0 || R.part)) return gb_unfuse(R);
@@ -3391,6 +3550,12 @@ static int gb_main(GbRun& R, bool auto_refit, bool* refit, int32_t* hint) {
                     (unsigned long long)R.st[ST_SELECTED], (unsigned long long)R.st[ST_FXFLAGS], pl.limbs, (int)pl.runs,
                     p.nacc);
         }
+        if (R.st[ST_KPACK]) {
+            // a selected row's key left the sampled packing plan: the caller
+            // repacks with the exact ranges (this pass's result is dropped)
+            R.kp_bad = true;
+            break;
+        }
         bool again = false;
         if (R.st[ST_TABLE_FULL] > 0) {
             R.gbits = std::max(R.gbits + 3, log2_ceil((int64_t)R.st[ST_NEWKEYS] * 4));
@@ -3443,7 +3608,7 @@ static int gb_main(GbRun& R, bool auto_refit, bool* refit, int32_t* hint) {
     if (rc == PLGPU_OK) (void)hipEventElapsedTime(&R.ms, ev0, ev1);
     (void)hipEventDestroy(ev0);
     (void)hipEventDestroy(ev1);
-    if (rc == PLGPU_OK && R.wide) rc = gb_wide(R);
+    if (rc == PLGPU_OK && R.wide && !R.kp_bad) rc = gb_wide(R);
     return rc;
 }
 
@@ -3467,6 +3632,7 @@ static void gb_fill_info(const GbRun& R, plgpu_groupby_info* info) {
     info->sum_limbs = (p.n_full > 0 || R.part) && R.pl.sum_only ? R.pl.limbs : 3;
     info->local_range = R.pl.local ? 1 : 0;
     info->register_runs = p.n_full > 0 && !R.part && R.pl.launched_runs ? 1 : 0;
+    info->key_pack = p.kp.n;
     for (int a = 0; a < p.nacc; ++a)
         if (((R.st[ST_FXFLAGS] >> (2 * a)) & 2u) && !((R.wide >> a) & 1u)) info->sum_inexact |= 1 << a;
 }
@@ -4263,6 +4429,59 @@ PLGPU_API int plgpu_gb_merge_sources(const void* records, int32_t n_sources, con
 // `checked`: pk comes from sampled ranges (mk_plan_pack_sampled); a row
 // outside them sets *repack (nothing else done) and the caller repacks
 // with the exact ranges.
+// The packing plan as the fused kernel's KeyPack, or n = 0 when the key
+// columns do not qualify (more than kKpFast, nullable, not Int64 / Int32 /
+// UInt32, misaligned, or a small input).
+static KeyPack kp_from_plan(const MkKeys& mk, const MkPack& pk, int64_t n) {
+    KeyPack k;
+    std::memset(&k, 0, sizeof k);
+    if (!options().fuse_keys || mk.n < 1 || mk.n > kKpFast || n < (int64_t(1) << 20)) return k;
+    for (int i = 0; i < mk.n; ++i) {
+        const DevCol& c = mk.c[i];
+        const bool w8 = c.dtype == PLGPU_I64, w4 = c.dtype == PLGPU_I32 || c.dtype == PLGPU_U32;
+        if (!(w8 || w4) || c.validity != nullptr || (c.offset & 1) != 0 ||
+            ((uintptr_t)c.values & (w8 ? 15 : 7)) != 0)
+            return k;
+    }
+    for (int i = 0; i < mk.n; ++i) {
+        k.c[i] = mk.c[i];
+        k.base[i] = (uint64_t)pk.minv[i] - (pk.nullable[i] ? 1u : 0u);
+        k.shift[i] = pk.shift[i];
+        k.bits[i] = pk.bits[i];
+    }
+    k.n = mk.n;
+    return k;
+}
+
+// Decode the group-by's output codes (hout) into the key columns.
+static int gb_multi_decode(const MkPack& pk, const plgpu_column* keys, int32_t nkeys, plgpu_column& hout,
+                           plgpu_column* out_keys, plgpu_column* out_aggs, int32_t naggs, hipStream_t s) {
+    int rc = PLGPU_OK;
+    const int64_t groups = hout.length;
+    const int gg = (int)std::max<int64_t>(1, std::min<int64_t>((groups + 255) / 256, 4096));
+    for (int i = 0; i < nkeys && !rc; ++i) {
+        const bool nullable = pk.nullable[i] != 0;
+        rc = make_owned_column(&out_keys[i], keys[i].dtype, groups, nullable, s);
+        if (rc || groups == 0) continue;
+        if (keys[i].dtype == PLGPU_BOOL) (void)hipMemsetAsync((void*)out_keys[i].values, 0, ((groups + 63) / 64) * 8, s);
+        if (nullable) (void)hipMemsetAsync((void*)out_keys[i].validity, 0, ((groups + 63) / 64) * 8, s);
+        mk_unpack_kernel<<<gg, 256, 0, s>>>((const int64_t*)hout.values, nullptr, groups, pk, i, keys[i].dtype,
+                                            (void*)out_keys[i].values, (uint32_t*)out_keys[i].validity);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) rc = hip_fail(e, "mk_unpack_kernel");
+    }
+    if (!rc) {
+        hipError_t e = hipStreamSynchronize(s);
+        if (e != hipSuccess) rc = hip_fail(e, "multi-key decode");
+    }
+    plgpu_column_release(&hout);
+    if (rc) {
+        for (int i = 0; i < nkeys; ++i) plgpu_column_release(&out_keys[i]);
+        for (int i = 0; i < naggs; ++i) plgpu_column_release(&out_aggs[i]);
+    }
+    return rc;
+}
+
 static int gb_multi_packed(const MkKeys& mk, MkPack pk, int64_t n, const plgpu_column* keys, int32_t nkeys,
                            const plgpu_column* cols, int32_t ncols, const Deriv* deriv, const plgpu_instr* program,
                            int32_t n_instr, const plgpu_agg* aggs, int32_t naggs, int32_t maintain_order,
@@ -4270,6 +4489,40 @@ static int gb_multi_packed(const MkKeys& mk, MkPack pk, int64_t n, const plgpu_c
                            bool checked = false, bool* repack = nullptr) {
     hipStream_t s = as_stream(stream);
     if (repack) *repack = false;
+    const KeyPack kp = kp_from_plan(mk, pk, n);
+    if (kp.n > 0) {
+        // fused key packing: the fused kernel forms each row's code from the
+        // key columns it loads (no code column written or read).  Off the
+        // fused kernel (many groups, derived inputs, ...) the plan says so
+        // and the code column below is used instead.
+        plgpu_column ck;
+        std::memset(&ck, 0, sizeof ck);
+        ck.dtype = PLGPU_I64;
+        ck.length = n;
+        ck.values = keys[0].values;  // never read as a key column while p.kp.n > 0
+        plgpu_column hout;
+        std::memset(&hout, 0, sizeof hout);
+        GbRun R;
+        int rc = gb_prepare(R, &ck, cols, ncols, program, n_instr, aggs, naggs, maintain_order != 0, false, stream,
+                            deriv);
+        if (!rc) {
+            R.pl.p.kp = kp;
+            rc = gb_plan(R, nullptr);
+        }
+        if (!rc && !R.kp_fallback) {
+            rc = gb_main(R, true, nullptr, nullptr);
+            if (!rc && R.kp_bad) {
+                if (!checked) return fail(PLGPU_ERR_HIP, "fused key packing: a row outside the exact packing plan");
+                *repack = true;
+                return PLGPU_OK;
+            }
+            if (!rc && info) gb_fill_info(R, info);
+            if (!rc) rc = gb_finalize(R, naggs, &hout, out_aggs);
+            if (rc) return rc;
+            return gb_multi_decode(pk, keys, nkeys, hout, out_keys, out_aggs, naggs, s);
+        }
+        if (rc) return rc;
+    }
     uint64_t* codes = nullptr;
     int rc = dev_alloc((void**)&codes, (size_t)std::max<int64_t>(n, 1) * 8 + (checked ? 8 : 0), s);
     if (rc) return rc;
@@ -4311,29 +4564,7 @@ static int gb_multi_packed(const MkKeys& mk, MkPack pk, int64_t n, const plgpu_c
     }
     dev_free(codes, s);
     if (rc) return rc;
-    const int64_t groups = hout.length;
-    const int gg = (int)std::max<int64_t>(1, std::min<int64_t>((groups + 255) / 256, 4096));
-    for (int i = 0; i < nkeys && !rc; ++i) {
-        const bool nullable = pk.nullable[i] != 0;
-        rc = make_owned_column(&out_keys[i], keys[i].dtype, groups, nullable, s);
-        if (rc || groups == 0) continue;
-        if (keys[i].dtype == PLGPU_BOOL) (void)hipMemsetAsync((void*)out_keys[i].values, 0, ((groups + 63) / 64) * 8, s);
-        if (nullable) (void)hipMemsetAsync((void*)out_keys[i].validity, 0, ((groups + 63) / 64) * 8, s);
-        mk_unpack_kernel<<<gg, 256, 0, s>>>((const int64_t*)hout.values, nullptr, groups, pk, i, keys[i].dtype,
-                                            (void*)out_keys[i].values, (uint32_t*)out_keys[i].validity);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) rc = hip_fail(e, "mk_unpack_kernel");
-    }
-    if (!rc) {
-        hipError_t e = hipStreamSynchronize(s);
-        if (e != hipSuccess) rc = hip_fail(e, "multi-key decode");
-    }
-    plgpu_column_release(&hout);
-    if (rc) {
-        for (int i = 0; i < nkeys; ++i) plgpu_column_release(&out_keys[i]);
-        for (int i = 0; i < naggs; ++i) plgpu_column_release(&out_aggs[i]);
-    }
-    return rc;
+    return gb_multi_decode(pk, keys, nkeys, hout, out_keys, out_aggs, naggs, s);
 }
 
 static int gb_multi_impl(const plgpu_column* keys, int32_t nkeys, const plgpu_column* cols, int32_t ncols,
@@ -4606,7 +4837,12 @@ PLGPU_API int plgpu_group_by_agg_ex(const plgpu_column* keys, int32_t nkeys, con
     const Deriv* dv = (ninputs > 0 || any_var) ? &d : nullptr;
     const plgpu_agg* ap = naggs > 0 ? ag.data() : aggs;
     if (nkeys == 0) return gb_keyless(cols, ncols, dv, program, n_instr, ap, naggs, out_aggs, info, stream);
-    if (nkeys == 1 && dtype_is_int(keys[0].dtype))
+    // one null-free 4-byte key (Int32 / UInt32: dates, Categorical codes)
+    // of a large input: the packed path, whose fused kernel reads the 4-byte
+    // key itself (fused key packing) instead of the generic kernel
+    const bool narrow = nkeys == 1 && (keys[0].dtype == PLGPU_I32 || keys[0].dtype == PLGPU_U32) &&
+                        keys[0].validity == nullptr && keys[0].length >= (int64_t(1) << 20) && options().fuse_keys;
+    if (nkeys == 1 && dtype_is_int(keys[0].dtype) && !narrow)
         return gb_single_impl(&keys[0], cols, ncols, dv, program, n_instr, ap, naggs, maintain_order, &out_keys[0],
                               out_aggs, info, stream);
     return gb_multi_impl(keys, nkeys, cols, ncols, dv, program, n_instr, ap, naggs, maintain_order, out_keys,

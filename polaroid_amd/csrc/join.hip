@@ -1518,13 +1518,15 @@ PLGPU_API int plgpu_join_inner_take(const plgpu_column* left_key, const plgpu_co
     if (!rc) {
         const DevCol pk = as_dev(left_key);
         const int g = jn_pass_grid(pp);
-        KtScope kt("jn_probe_match_kernel", s);
-        if (pk.validity)
-            jn_probe_match_kernel<true, JM_INNER, false, true><<<g, kJnThreads, 0, s>>>(
-                pk, pp.np, b.t, neq, pp.m, pp.tcount, pp.ntiles, nullptr, mp);
-        else
-            jn_probe_match_kernel<false, JM_INNER, false, true><<<g, kJnThreads, 0, s>>>(
-                pk, pp.np, b.t, neq, pp.m, pp.tcount, pp.ntiles, nullptr, mp);
+        {
+            KtScope kt("jn_probe_match_kernel", s);
+            if (pk.validity)
+                jn_probe_match_kernel<true, JM_INNER, false, true><<<g, kJnThreads, 0, s>>>(
+                    pk, pp.np, b.t, neq, pp.m, pp.tcount, pp.ntiles, nullptr, mp);
+            else
+                jn_probe_match_kernel<false, JM_INNER, false, true><<<g, kJnThreads, 0, s>>>(
+                    pk, pp.np, b.t, neq, pp.m, pp.tcount, pp.ntiles, nullptr, mp);
+        }
         rc = jn_pass_scan(&pp, s, "join probe match (row-format table)");
     }
     const int64_t total = (int64_t)pp.total;

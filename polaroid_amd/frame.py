@@ -163,9 +163,51 @@ class _Owned:
 
 # ------------------------------------------------------------------ Series
 class Series:
-    """A named Arrow array in device memory."""
+    """A named Arrow array in device memory.
 
-    __slots__ = ("name", "_col", "_keep", "_logical")
+    A Categorical / Enum column arrives as an Arrow dictionary array and is
+    kept as its codes (`_cat`: the unique dictionary strings and the UInt32
+    indices into them, both on the device).  Its value is the strings: the
+    first use that needs them gathers them on the device (`_col`), while
+    the group-by keys on the codes directly (polars-core/src/frame/group_by/
+    into_groups.rs:132-139 groups a Categorical by its physical codes)."""
+
+    __slots__ = ("name", "_c", "_keep", "_logical", "_cat")
+
+    @property
+    def _col(self) -> N.Column:
+        c = self._c
+        if c is None:
+            c = self._materialize_cat()
+        return c
+
+    @_col.setter
+    def _col(self, col_: N.Column) -> None:
+        self._c = col_
+        self._cat = None
+
+    def _materialize_cat(self) -> N.Column:
+        """The strings of a Categorical column, gathered once from its
+        dictionary by its codes (a null code gathers a null)."""
+        dictionary, codes = self._cat
+        strs = dictionary.gather(codes)
+        self._c = strs._col
+        self._keep = list(self._keep) + [strs]
+        return self._c
+
+    @classmethod
+    def _categorical(cls, name: str, dictionary: "Series", codes: "Series") -> "Series":
+        s = cls.__new__(cls)
+        s.name = name
+        s._c = None
+        s._keep = [dictionary, codes]
+        s._logical = None
+        s._cat = (dictionary, codes)
+        return s
+
+    def _cat_codes(self) -> "tuple[Series, Series] | None":
+        """(dictionary, UInt32 codes) of a Categorical column, else None."""
+        return getattr(self, "_cat", None)
 
     def __init__(self, name: str = "", values: Any = None, dtype: DataType | None = None):
         self.name = name
@@ -174,7 +216,7 @@ class Series:
         if values is None:
             values = []
         if isinstance(values, Series):
-            self._col, self._keep = values._col, values._keep
+            self._c, self._keep, self._cat = values._c, values._keep, values._cat_codes()
             self._logical = values._logical_dtype()
             return
         validity = None
@@ -376,17 +418,19 @@ class Series:
     # properties -----------------------------------------------------------
     @property
     def dtype(self) -> DataType:
-        return self._logical_dtype() or _BY_CODE[self._col.dtype]
+        if self._c is None:  # Categorical: its values are strings
+            return String
+        return self._logical_dtype() or _BY_CODE[self._c.dtype]
 
     def len(self) -> int:
-        return int(self._col.length)
+        return int((self._c if self._c is not None else self._cat[1]._col).length)
 
     def __len__(self) -> int:
         return self.len()
 
     def alias(self, name: str) -> "Series":
         s = Series.__new__(Series)
-        s.name, s._col, s._keep, s._logical = name, self._col, self._keep, self._logical_dtype()
+        s.name, s._c, s._keep, s._logical, s._cat = name, self._c, self._keep, self._logical_dtype(), self._cat_codes()
         return s
 
     # host materialisation (tests / display only) --------------------------
@@ -439,6 +483,11 @@ class Series:
     def to_arrow(self):
         import pyarrow as pa
 
+        if self._c is None and self._cat_codes() is not None:
+            # Categorical, strings never gathered: its codes and dictionary
+            # as an Arrow dictionary array (what polars exports it as)
+            dictionary, codes = self._cat
+            return pa.DictionaryArray.from_arrays(codes.to_arrow(), dictionary.to_arrow())
         if self.dtype is String:
             offs, data = self._string_buffers()
             valid = self.validity_numpy()
@@ -618,6 +667,13 @@ def _ingest_chunks(name: str, chunks: list, atype) -> Series:
         if dictionary.dtype is not String:
             raise N.InvalidOperationError(f"column {name!r}: dictionary of {dict_arr.type} is not supported")
         idx = _ingest_chunks("__idx", [c.indices.cast(pa.uint32()) for c in chunks], pa.uint32())
+        import pyarrow.compute as pc
+
+        if dict_arr.null_count == 0 and pc.count_distinct(dict_arr).as_py() == builtins.len(dict_arr):
+            # unique categories (polars' dictionaries are): equal strings <=>
+            # equal codes, so the codes stand for the values; the strings are
+            # gathered only where they are needed
+            return Series._categorical(name, dictionary, idx)
         return dictionary.gather(idx).alias(name)
     if atype in (pa.string(), pa.utf8()):
         chunks = [c.cast(pa.large_string()) for c in chunks]
@@ -1603,12 +1659,35 @@ def _group_by(df: DataFrame, key: str | tuple, aggs: list[Expr], maintain_order:
     return _group_by_plain(df, key, aggs, maintain_order, pred, info)
 
 
+def _cat_keys(df: DataFrame, key: str | tuple, aggs: list[Expr], pred: Expr | None):
+    """Categorical key columns -> their UInt32 codes (polars-core/src/frame/
+    group_by/into_groups.rs:132-139 groups a Categorical by its physical
+    codes): the frame with those key columns replaced, and their
+    dictionaries, which decode the output keys.  A key column an aggregation
+    or the predicate also reads keeps its strings."""
+    keys = _gb_keys(key)
+    used = {c for e in aggs for c in e.meta_root_names()}
+    if pred is not None:
+        used |= set(pred.meta_root_names())
+    dicts: dict = {}
+    cols = []
+    for nm, s in df._cols.items():
+        cc = s._cat_codes() if nm in keys and nm not in used else None
+        if cc is not None:
+            dicts[nm] = cc[0]
+            cols.append(cc[1].alias(nm))
+        else:
+            cols.append(s)
+    return (DataFrame(cols) if dicts else df), dicts
+
+
 def _group_by_plain(df: DataFrame, key: str | tuple, aggs: list[Expr], maintain_order: bool,
                     pred: Expr | None, info: dict | None) -> DataFrame:
     if pred is not None:
         pred, df = _lower_strings(pred, df)
         pred, _, strict = _prepare(pred, df)
         _check_strict(strict, df)
+    df, cat_dicts = _cat_keys(df, key, aggs, pred)
     g = _gb_lower(df, key, aggs, pred)
     out_aggs = (N.Column * max(1, g.naggs))()
     gi = N.GroupByInfo()
@@ -1620,7 +1699,13 @@ def _group_by_plain(df: DataFrame, key: str | tuple, aggs: list[Expr], maintain_
                                           out_aggs, C.byref(gi), None))
     if info is not None:
         info.update(gi.as_dict())
-    return _gb_frame(g, out_key, out_aggs)
+        info["categorical_codes"] = builtins.len(cat_dicts)
+    out = _gb_frame(g, out_key, out_aggs)
+    if cat_dicts:
+        # output keys: the group codes over the column's dictionary
+        out = DataFrame([Series._categorical(nm, cat_dicts[nm], s) if nm in cat_dicts else s
+                         for nm, s in out._cols.items()])
+    return out
 
 
 def _join(left: DataFrame, right: DataFrame, left_on: str | tuple, right_on: str | tuple, suffix: str,

@@ -794,8 +794,44 @@ def reduce_cases():
     return {"cases": cases}
 
 
+def categorical_cases():
+    """Group-by on Categorical keys: the groups, their first-occurrence order
+    (maintain_order) and sizes the reference's tests assert."""
+    cases = []
+    # operations/test_group_by.py:903-957 test_perfect_hash_table_null_values:
+    # a Categorical with nulls grouped with maintain_order; `groups` is the
+    # expected key column and the expected agg lists' lengths are the sizes
+    values = ["3", "41", "17", "5", "26", "27", "43", "45", "41", "13", "45", "48", "17", "22", "31", "25", "28",
+              "13", "7", "26", "17", "4", "43", "47", "30", "28", "8", "27", "6", "7", "26", "11", "37", "29", "49",
+              "20", "29", "28", "23", "9", None, "38", "19", "7", "38", "3", "30", "37", "41", "5", "16", "26", "31",
+              "6", "25", "11", "17", "31", "31", "20", "26", None, "39", "10", "38", "4", "39", "15", "13", "35",
+              "38", "11", "39", "11", "48", "36", "18", "11", "34", "16", "28", "9", "37", "8", "17", "48", "44",
+              "28", "25", "30", "37", "30", "18", "12", None, "27", "10", "3", "16", "27", "6"]
+    groups = ["3", "41", "17", "5", "26", "27", "43", "45", "13", "48", "22", "31", "25", "28", "7", "4", "47", "30",
+              "8", "6", "11", "37", "29", "49", "20", "23", "9", None, "38", "19", "16", "39", "10", "15", "35", "36",
+              "18", "34", "44", "12"]
+    sizes = [3, 3, 5, 2, 5, 4, 2, 2, 3, 3, 1, 4, 3, 5, 3, 2, 1, 4, 2, 3, 5, 4, 2, 1, 2, 1, 2, 3, 4, 1, 3, 3, 2, 1,
+             1, 1, 2, 1, 1, 1]
+    cases.append({"name": "perfect_hash_table_null_values",
+                  "source": "operations/test_group_by.py:903-957",
+                  "key": values, "maintain_order": True, "groups": groups, "len": sizes})
+    # datatypes/test_categorical.py:104-118 test_unset_sorted_on_append: two
+    # Categorical frames concatenated without rechunking (two chunks, the
+    # dictionaries unified), group_by("key").len() == [4, 4]
+    cases.append({"name": "unset_sorted_on_append",
+                  "source": "datatypes/test_categorical.py:104-118",
+                  "chunks": [["a", "a", "b", "b"], ["a", "a", "b", "b"]], "vals": [1, 3, 2, 4, 5, 7, 6, 8],
+                  "maintain_order": False, "groups": ["a", "b"], "len": [4, 4]})
+    # operations/test_group_by.py:608-626 test_group_by_custom_agg_empty_list:
+    # an empty Categorical key grouped: no rows (and a Categorical key column)
+    cases.append({"name": "empty_categorical_key",
+                  "source": "operations/test_group_by.py:608-626",
+                  "key": [], "maintain_order": False, "groups": [], "len": []})
+    return {"cases": cases}
+
+
 def main():
-    for name, obj in (("compare_total_order.json", compare_table()),
+    for name, obj in (("categorical_cases.json", categorical_cases()),("compare_total_order.json", compare_table()),
                       ("group_by_cases.json", group_by_cases()),
                       ("group_by_multi_cases.json", group_by_multi_cases()),
                       ("filter_cases.json", filter_cases()),

@@ -1,0 +1,207 @@
+"""Fused key packing and Categorical keys (round 4).
+
+* Several integer keys (and one Int32 / UInt32 key) of a large input are
+  packed into the exact Int64 tuple code (mk_plan_pack's layout) inside the
+  fused group-by kernel's registers: no code column is written or read
+  (info["key_pack"] = the number of key columns packed in the kernel).
+  Checked bit-exact against the oracle's row-encoding restatement
+  (oracle.group_by_agg_multi, polars-core/src/chunked_array/ops/
+  row_encode.rs), against the code-column path (option fuse_keys = 0) on the
+  same data, through the sampled plan's repack (an outlier row) and through
+  the fallbacks (many groups, derived inputs).
+* A Categorical column (an Arrow dictionary array: polars' export) groups
+  by its UInt32 codes (polars-core/src/frame/group_by/into_groups.rs:132-139
+  groups a Categorical by its physical codes); the strings are gathered only
+  for the output keys (info["categorical_codes"]).  Pinned by the fixtures of
+  tests/golden/categorical_cases.json (test_group_by.py:903-957 with nulls
+  and maintain_order, test_categorical.py:104-118 two chunks, an empty key).
+"""
+
+import math
+
+import numpy as np
+import pyarrow as pa
+import pytest
+
+import polaroid_amd as pl
+from conftest import load_golden
+from test_gpu_groupby_multi import _check
+from test_gpu_parity import _rand_frame
+
+pytestmark = pytest.mark.gpu
+
+N = 1_500_003  # above the sampled-plan / fused-packing threshold (2^20 rows)
+
+
+@pytest.mark.parametrize("layout", ["day_ordered", "random"])
+@pytest.mark.parametrize("aggs", ["sums", "mixed"])
+@pytest.mark.parametrize("pred", [None, "simple_f64"])
+def test_fused_two_keys_vs_oracle(gpu, layout, aggs, pred):
+    """(symbol: Int64, day: Int32) packed in the fused kernel, exact vs the
+    oracle: time-ordered days (range-local table) and random tuples."""
+    rng = np.random.default_rng(len(layout) + 3 * len(aggs) + (pred is None))
+    sym = (rng.integers(0, 100, N) * 7919 + 1_000_000).astype(np.int64)
+    day = ((np.arange(N) * 250) // N).astype(np.int32) if layout == "day_ordered" else \
+        rng.integers(0, 40, N).astype(np.int32)
+    cols = _rand_frame(rng, N)
+    ag = [("sum", "a"), ("sum", "d")] if aggs == "sums" else \
+        [("sum", "a"), ("min", "d"), ("max", "b"), ("count", "d"), ("len", "a"), ("mean", "d")]
+    info = {}
+    _check({"sym": (sym, None), "day": (day, None)}, cols, ag, False, pred, info=info)
+    assert info["key_pack"] == 2, info
+
+
+@pytest.mark.parametrize("dtype", [np.int32, np.uint32])
+@pytest.mark.parametrize("maintain_order", [False, True])
+def test_fused_single_narrow_key(gpu, dtype, maintain_order):
+    """One null-free Int32 / UInt32 key (dates, Categorical codes): the fused
+    kernel reads the 4-byte key and packs it (was: the generic kernel)."""
+    rng = np.random.default_rng(int(maintain_order) + (dtype == np.uint32) * 2)
+    lo = 0 if dtype == np.uint32 else -(1 << 30)
+    k = (rng.integers(0, 300, N) * 1_000_003 % (1 << 30) + lo).astype(dtype)
+    cols = _rand_frame(rng, N)
+    info = {}
+    _check({"k": (k, None)}, cols, [("sum", "a"), ("len", "b"), ("max", "d")], maintain_order, info=info)
+    assert info["key_pack"] == 1, info
+
+
+def test_fused_matches_code_column_path(gpu, plgpu_option):
+    """fuse_keys = 0 (the packed code column) gives the same frame."""
+    rng = np.random.default_rng(5)
+    sym = rng.integers(0, 100, N).astype(np.int64)
+    day = rng.integers(0, 250, N).astype(np.int32)
+    a = rng.uniform(10, 500, N)
+    df = pl.DataFrame({"sym": pl.Series.from_numpy("sym", sym), "day": pl.Series.from_numpy("day", day),
+                       "a": pl.Series.from_numpy("a", a)})
+    q = df.lazy().filter(pl.col("a") > 250.0).group_by("sym", "day", maintain_order=True).agg(
+        pl.col("a").sum(), pl.len())
+    i1, i0 = {}, {}
+    fused = q.collect(info=i1)
+    plgpu_option("fuse_keys", 0)
+    plain = q.collect(info=i0)
+    assert i1["key_pack"] == 2 and i0["key_pack"] == 0
+    for c in ("sym", "day", "len"):
+        assert fused[c].to_list() == plain[c].to_list()
+    assert np.array_equal(fused["a"].to_numpy().view(np.uint64), plain["a"].to_numpy().view(np.uint64))
+
+
+def test_fused_outlier_repacks(gpu):
+    """A row outside the sampled packing plan (far from every sampled key)
+    is caught in the fused kernel (ST_KPACK): the group-by repacks with the
+    exact ranges and runs fused again, exact."""
+    rng = np.random.default_rng(9)
+    k1 = (rng.integers(0, 1000, N) * 3 - 500).astype(np.int64)
+    k1[N // 2 + 7] = 1 << 40
+    k2 = rng.integers(0, 50, N).astype(np.int32)
+    cols = _rand_frame(rng, N)
+    info = {}
+    _check({"k1": (k1, None), "k2": (k2, None)}, cols, [("sum", "a"), ("len", "b")], False, info=info)
+    assert info["key_pack"] == 2, info
+
+
+def test_fused_fallbacks(gpu):
+    """Off the fused kernel the code column is used, with the same result:
+    many groups (the partitioned / global path) and derived inputs."""
+    rng = np.random.default_rng(11)
+    n = 2_000_000
+    k1 = rng.integers(0, 1000, n).astype(np.int64)
+    k2 = rng.integers(0, 1000, n).astype(np.int32)
+    cols = {"a": (rng.standard_normal(n), None), "b": (rng.integers(-9, 9, n).astype(np.int64), None)}
+    info = {}
+    _check({"k1": (k1, None), "k2": (k2, None)}, cols, [("sum", "a"), ("len", "a")], False, info=info)
+    assert info["key_pack"] == 0 and info["groups"] > 600_000
+    # (a * b).sum(): a derived input fused in registers is not a PACK variant
+    df = pl.DataFrame({"k1": pl.Series.from_numpy("k1", k1 % 10), "k2": pl.Series.from_numpy("k2", k2 % 10),
+                       "a": pl.Series.from_numpy("a", cols["a"][0]),
+                       "b": pl.Series.from_numpy("b", cols["a"][0] * 2.0)})
+    info = {}
+    out = df.lazy().group_by("k1", "k2").agg((pl.col("a") * pl.col("b")).sum().alias("ab")).collect(info=info)
+    assert info["key_pack"] == 0
+    got = dict(zip(zip(out["k1"].to_list(), out["k2"].to_list()), out["ab"].to_list()))
+    a, b = cols["a"][0], cols["a"][0] * 2.0
+    for key in list(got)[:10]:
+        m = ((k1 % 10) == key[0]) & ((k2 % 10) == key[1])
+        assert got[key] == math.fsum(a[m] * b[m])
+
+
+def _cat_frame(strings, vals=None, chunks=None):
+    """A frame with a Categorical column "c" built as polars exports it: an
+    Arrow dictionary array (one chunk, or several with their own dictionaries)."""
+    if chunks is None:
+        chunks = [strings]
+    arrs = [pa.array(ch, pa.string()).dictionary_encode() for ch in chunks]
+    s = pl.Series.from_arrow("c", pa.chunked_array(arrs) if len(arrs) > 1 else arrs[0])
+    cols = [s]
+    if vals is not None:
+        cols.append(pl.Series.from_numpy("v", np.asarray(vals)))
+    return pl.DataFrame(cols)
+
+
+def test_categorical_golden(gpu):
+    for case in load_golden("categorical_cases.json")["cases"]:
+        if "chunks" in case:
+            df = _cat_frame(None, case["vals"], case["chunks"])
+        else:
+            df = _cat_frame(case["key"], np.arange(len(case["key"]), dtype=np.int64))
+        info = {}
+        out = df.lazy().group_by("c", maintain_order=case["maintain_order"]).agg(pl.len()).collect(info=info)
+        got = list(zip(out["c"].to_list(), out["len"].to_list()))
+        want = list(zip(case["groups"], case["len"]))
+        if not case["maintain_order"]:
+            got, want = sorted(got, key=str), sorted(want, key=str)
+        assert got == want, case["name"]
+        if len(case["groups"]):
+            assert info.get("categorical_codes") == 1, (case["name"], info)
+
+
+@pytest.mark.parametrize("nulls", [False, True])
+@pytest.mark.parametrize("maintain_order", [False, True])
+def test_categorical_headline_vs_strings(gpu, nulls, maintain_order):
+    """The headline query on a Categorical symbol: grouped by the codes
+    (fused 4-byte key when null-free) and identical to the same query on the
+    String column."""
+    rng = np.random.default_rng(int(nulls) * 2 + maintain_order)
+    syms = np.array([f"SYM{i:03d}" for i in range(100)], dtype=object)
+    k = rng.integers(0, 100, N)
+    strs = syms[k].tolist()
+    if nulls:
+        for i in rng.integers(0, N, 1000):
+            strs[i] = None
+    close = rng.uniform(10, 490, N)
+    df = _cat_frame(strs, close)
+    info = {}
+    q = df.lazy().filter(pl.col("v") > 250.0).group_by("c", maintain_order=maintain_order).agg(
+        pl.col("v").sum().alias("s"), pl.len())
+    out = q.collect(info=info)
+    assert info["categorical_codes"] == 1
+    assert info["key_pack"] == (0 if nulls else 1), info
+    sdf = pl.DataFrame([pl.Series("c", strs, pl.String), pl.Series.from_numpy("v", close)])
+    ref = sdf.lazy().filter(pl.col("v") > 250.0).group_by("c", maintain_order=maintain_order).agg(
+        pl.col("v").sum().alias("s"), pl.len()).collect()
+    a = sorted(zip(out["c"].to_list(), out["s"].to_list(), out["len"].to_list()), key=str)
+    b = sorted(zip(ref["c"].to_list(), ref["s"].to_list(), ref["len"].to_list()), key=str)
+    assert a == b
+    if maintain_order:
+        assert out["c"].to_list() == ref["c"].to_list()
+    # the output keys stay codes over the dictionary until exported
+    arr = out["c"].to_arrow()
+    assert pa.types.is_dictionary(arr.type) and arr.to_pylist() == out["c"].to_list()
+
+
+def test_categorical_key_also_used_elsewhere(gpu):
+    """A Categorical key that the predicate or an aggregation also reads
+    keeps its strings for those (and still groups correctly)."""
+    rng = np.random.default_rng(2)
+    n = 200_000
+    strs = np.array(["AAPL", "MSFT", "GOOG", "AMZN"], dtype=object)[rng.integers(0, 4, n)].tolist()
+    v = rng.uniform(0, 1, n)
+    df = _cat_frame(strs, v)
+    out = df.lazy().filter(pl.col("c") != "MSFT").group_by("c").agg(pl.col("v").sum().alias("s")).collect()
+    got = dict(zip(out["c"].to_list(), out["s"].to_list()))
+    sa = np.array(strs, dtype=object)
+    assert set(got) == {"AAPL", "GOOG", "AMZN"}
+    for key, val in got.items():
+        assert val == math.fsum(v[sa == key])
+    # the column's strings are gathered for other uses (a filter of the frame)
+    f = df.filter(pl.col("c") == "GOOG")
+    assert f["c"].to_list() == [s for s in strs if s == "GOOG"]

@@ -1,0 +1,171 @@
+"""Cross-check a bench line against the rocprofv3 runs of the same lease
+(tools/bench_profile.sh output):
+
+    python tools/bench_evidence.py gpurun_out/<tag> [--out profiles/<name>]
+
+For every leg's roofline kernel (headline gb_fast_kernel, vwap / std legs,
+sort: aos_gather_kernel, join: jn_probe_match_kernel) it reports
+  - kernel_ms of the plain bench line (HIP events, bench.json),
+  - kernel_ms of the profiled run's own line (trace.json),
+  - the rocprofv3 kernel-trace mean of the same launches (trace/),
+  - frac recomputed from the trace mean at the line's algorithmic bytes,
+    and its distance from the line's frac,
+  - HBM bytes per launch from the FETCH_SIZE / WRITE_SIZE passes (pmc1 /
+    pmc2; KiB; FETCH_SIZE doubled for the wide streaming kernels per
+    MI355X_MICROARCH.md "HBM", raw for random-access kernels, whose
+    correction is uncalibrated),
+and checks that no kernel mean exceeds its step.  With --out it writes
+<out>.json and <out>.md, and profiles/traffic.json for the headline.
+"""
+import argparse
+import csv
+import json
+import os
+import re
+import statistics
+import sys
+from collections import defaultdict
+
+HBM_PEAK = 8000.0
+
+# leg -> (kernel-name regex over the trace, algorithmic bytes / launch key, streaming?)
+LEGS = {
+    "headline": (r"gb_fast_kernel<4, 1, true, 2, 2, false, false, false, false", "headline", True),
+    "vwap": (r"gb_fast_kernel<2, 1, true, 2, 2, false, false, true, false", "vwap", True),
+    "std": (r"gb_fast_kernel<3, 1, true, 2, 2, false, false, false, true", "std", True),
+    "sort": (r"aos_gather_kernel<8>", "sort", False),
+    "sort_pack": (r"aos_pack_kernel<8>", "sort_pack", True),
+    "rolling": (r"rl_wave_kernel<4, false>", "rolling", True),
+    "join": (r"jn_probe_match_kernel<false, 0, false, true>", "join", False),
+    "join_emit": (r"jn_take_emit_kernel<2>", "join_emit", True),
+}
+
+
+def last_json(path):
+    for line in reversed(open(path).read().strip().splitlines()):
+        line = line.strip()
+        if line.startswith("{"):
+            return json.loads(line)
+    raise SystemExit(f"no JSON line in {path}")
+
+
+def line_view(d):
+    """leg -> (kernel_ms, algorithmic bytes per launch, step ms, line frac)."""
+    out = {}
+    r = d["roofline"]
+    rows = d["config"]["rows_per_gpu"]
+    out["headline"] = (r["kernel_ms"], r["bytes_per_row"] * rows, d["ms_per_step"], r["frac"])
+    for leg in ("vwap", "std"):
+        if leg in d:
+            L = d[leg]
+            out[leg] = (L["kernel_ms"], L["bytes_per_row"] * L["rows"], L["ms_per_step"], L["frac"])
+    if "sort" in d:
+        L = d["sort"]
+        for key, sub in (("sort", L["roofline"]), ("sort_pack", L["pack"]), ("rolling", L["rolling"])):
+            if sub.get("kernel_ms"):
+                out[key] = (sub["kernel_ms"], sub["algorithmic_GB"] * 1e9, L["ms_per_step"], sub["frac"])
+    if "join" in d:
+        L = d["join"]
+        for key, sub in (("join", L["roofline"]), ("join_emit", L["emit"])):
+            if sub.get("kernel_ms"):
+                out[key] = (sub["kernel_ms"], sub["algorithmic_GB"] * 1e9, L["ms_per_step"], sub["frac"])
+    return out
+
+
+def trace_durations(path):
+    dur = defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        dur[r["Kernel_Name"]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+    return dur
+
+
+def pick(table, pattern):
+    rx = re.compile(pattern)
+    vals = []
+    names = []
+    for name, v in table.items():
+        if rx.search(name):
+            vals += v
+            names.append(name)
+    return vals, names
+
+
+def counters(path):
+    c = defaultdict(lambda: defaultdict(list))
+    for r in csv.DictReader(open(path)):
+        c[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return c
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+    d = args.dir
+    plain = last_json(os.path.join(d, "bench.json"))
+    prof = last_json(os.path.join(d, "trace.json"))
+    lp, lq = line_view(plain), line_view(prof)
+    tr = trace_durations(os.path.join(d, "trace", "run_kernel_trace.csv"))
+    fetch = counters(os.path.join(d, "pmc1", "run_counter_collection.csv"))
+    write = counters(os.path.join(d, "pmc2", "run_counter_collection.csv"))
+    rows = []
+    for leg, (pat, _, streaming) in LEGS.items():
+        if leg not in lp:
+            continue
+        k_plain, algo, step_plain, frac_plain = lp[leg]
+        k_prof = lq.get(leg, (None,) * 4)[0]
+        step_prof = lq.get(leg, (None,) * 4)[2]
+        durs, names = pick(tr, pat)
+        # the profiled run's timed launches are the last ones of the leg
+        # (warmup launches come first); the mean over all of them is reported too
+        tmean = statistics.mean(durs) if durs else None
+        fvals, _ = pick({k: v["FETCH_SIZE"] for k, v in fetch.items() if "FETCH_SIZE" in v}, pat)
+        wvals, _ = pick({k: v["WRITE_SIZE"] for k, v in write.items() if "WRITE_SIZE" in v}, pat)
+        rd = statistics.mean(fvals) * 1024 * (2 if streaming else 1) if fvals else None
+        wr = statistics.mean(wvals) * 1024 if wvals else None
+        row = {
+            "leg": leg, "kernel": names[0] if names else pat, "launches_traced": len(durs),
+            "algorithmic_bytes": algo,
+            "line_kernel_ms": k_plain, "line_frac": frac_plain, "line_step_ms": step_plain,
+            "profiled_line_kernel_ms": k_prof, "profiled_step_ms": step_prof,
+            "trace_mean_ms": round(tmean, 4) if tmean else None,
+            "trace_frac": round(algo / (tmean * 1e-3) / 1e9 / HBM_PEAK, 4) if tmean else None,
+            "hbm_read_bytes": rd, "hbm_write_bytes": wr,
+            "read_correction": "FETCH_SIZE x 2 (wide streaming reads, gfx950)" if streaming
+            else "FETCH_SIZE raw (random access: uncalibrated)",
+        }
+        if tmean:
+            row["trace_vs_line_pct"] = round(100 * (tmean - k_plain) / k_plain, 2)
+            row["trace_vs_profiled_line_pct"] = round(100 * (tmean - k_prof) / k_prof, 2) if k_prof else None
+            row["frac_diff_pct"] = round(100 * (row["trace_frac"] - frac_plain) / frac_plain, 2)
+            row["kernel_mean_within_step"] = tmean <= (step_prof or step_plain) and k_plain <= step_plain
+        if rd is not None and wr is not None:
+            row["hbm_bytes_per_launch"] = rd + wr
+            row["traffic_over_algorithmic"] = round((rd + wr) / algo, 4)
+        rows.append(row)
+    hdr = ("| leg | kernel | line kernel ms (HIP events) | trace mean ms | trace vs line | line frac | trace frac "
+           "| HBM bytes / launch (PMC) | / algorithmic | mean <= step |")
+    md = [f"Bench evidence from `{d}` (plain run, then the same command under rocprofv3 in the same lease).", "",
+          hdr, "|---|---|---|---|---|---|---|---|---|---|"]
+    for r in rows:
+        md.append(f"| {r['leg']} | `{r['kernel'][:70]}` | {r['line_kernel_ms']} | {r['trace_mean_ms']} | "
+                  f"{r.get('trace_vs_line_pct')} % | {r['line_frac']} | {r['trace_frac']} | "
+                  f"{(r.get('hbm_bytes_per_launch') or 0) / 1e9:.3f} GB | {r.get('traffic_over_algorithmic')} | "
+                  f"{r.get('kernel_mean_within_step')} |")
+    print("\n".join(md))
+    if args.out:
+        json.dump({"dir": d, "plain_line": {"value": plain["value"], "ms_per_step": plain["ms_per_step"]},
+                   "legs": rows}, open(args.out + ".json", "w"), indent=1)
+        open(args.out + ".md", "w").write("\n".join(md) + "\n")
+        h = next((r for r in rows if r["leg"] == "headline"), None)
+        if h and h.get("hbm_bytes_per_launch"):
+            root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+            json.dump({"rows": plain["config"]["rows_per_gpu"], "kernel": h["kernel"],
+                       "hbm_bytes_per_launch": h["hbm_bytes_per_launch"], "correction": h["read_correction"],
+                       "duration_ms": h["trace_mean_ms"], "source": args.out + ".json"},
+                      open(os.path.join(root, "profiles", "traffic.json"), "w"), indent=1)
+
+
+if __name__ == "__main__":
+    sys.exit(main())
