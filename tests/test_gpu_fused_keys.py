@@ -33,6 +33,12 @@ pytestmark = pytest.mark.gpu
 N = 1_500_003  # above the sampled-plan / fused-packing threshold (2^20 rows)
 
 
+def _dense(rng, n):
+    """_rand_frame's columns without validity (the fused kernel's inputs are
+    null-free; NaN / inf / -0.0 stay)."""
+    return {k: (v, None) for k, (v, _) in _rand_frame(rng, n).items()}
+
+
 @pytest.mark.parametrize("layout", ["day_ordered", "random"])
 @pytest.mark.parametrize("aggs", ["sums", "mixed"])
 @pytest.mark.parametrize("pred", [None, "simple_f64"])
@@ -40,10 +46,13 @@ def test_fused_two_keys_vs_oracle(gpu, layout, aggs, pred):
     """(symbol: Int64, day: Int32) packed in the fused kernel, exact vs the
     oracle: time-ordered days (range-local table) and random tuples."""
     rng = np.random.default_rng(len(layout) + 3 * len(aggs) + (pred is None))
-    sym = (rng.integers(0, 100, N) * 7919 + 1_000_000).astype(np.int64)
-    day = ((np.arange(N) * 250) // N).astype(np.int32) if layout == "day_ordered" else \
-        rng.integers(0, 40, N).astype(np.int32)
-    cols = _rand_frame(rng, N)
+    # day-ordered: 25,000 groups, ~100 per row range (the range-local table,
+    # which needs >= 2^22 rows); random: 800 groups (one LDS table)
+    n = 4_500_001 if layout == "day_ordered" else N
+    sym = (rng.integers(0, 100, n) * 7919 + 1_000_000).astype(np.int64)
+    day = ((np.arange(n) * 250) // n).astype(np.int32) if layout == "day_ordered" else \
+        rng.integers(0, 8, n).astype(np.int32)
+    cols = _dense(rng, n)
     ag = [("sum", "a"), ("sum", "d")] if aggs == "sums" else \
         [("sum", "a"), ("min", "d"), ("max", "b"), ("count", "d"), ("len", "a"), ("mean", "d")]
     info = {}
@@ -59,7 +68,7 @@ def test_fused_single_narrow_key(gpu, dtype, maintain_order):
     rng = np.random.default_rng(int(maintain_order) + (dtype == np.uint32) * 2)
     lo = 0 if dtype == np.uint32 else -(1 << 30)
     k = (rng.integers(0, 300, N) * 1_000_003 % (1 << 30) + lo).astype(dtype)
-    cols = _rand_frame(rng, N)
+    cols = _dense(rng, N)
     info = {}
     _check({"k": (k, None)}, cols, [("sum", "a"), ("len", "b"), ("max", "d")], maintain_order, info=info)
     assert info["key_pack"] == 1, info
@@ -93,7 +102,7 @@ def test_fused_outlier_repacks(gpu):
     k1 = (rng.integers(0, 1000, N) * 3 - 500).astype(np.int64)
     k1[N // 2 + 7] = 1 << 40
     k2 = rng.integers(0, 50, N).astype(np.int32)
-    cols = _rand_frame(rng, N)
+    cols = _dense(rng, N)
     info = {}
     _check({"k1": (k1, None), "k2": (k2, None)}, cols, [("sum", "a"), ("len", "b")], False, info=info)
     assert info["key_pack"] == 2, info
