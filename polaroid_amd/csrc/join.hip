@@ -446,6 +446,215 @@ __global__ void jn_build_rowformat_kernel(DevCol bk, int64_t nb, JnTable t, bool
     }
 }
 
+// ------------------------------------------------- wide row-format table
+// The row-format table for W = 2..3 build payload columns (round 4): 32-B
+// cells {key, p0, p1, p2}, four to a 128-B bucket, so one probe still reads
+// one line and gets every payload of its build row with the key (a
+// row-container hash table; the reference's _finish_join then takes each
+// right column at the pairs, polars-ops/src/frame/join/general.rs:17).
+// Special cells cap (null key) and cap + 1 (INT64_MIN key): key word 1 once
+// occupied.
+constexpr int kBktWide = 4;  // 32-B cells per 128-B bucket
+struct WideCell {
+    uint64_t key;
+    uint64_t p[3];
+};
+
+__global__ void jn_empty_wide_kernel(WideCell* cells, int64_t cap) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += (int64_t)gridDim.x * blockDim.x)
+        cells[i].key = kEmptyKey;
+}
+
+struct WidePay {
+    DevCol c[3];
+};
+
+template <int W>
+__global__ void jn_build_wide_kernel(DevCol bk, int64_t nb, WideCell* cells, int64_t cap, int bbits, bool nulls_equal,
+                                     WidePay pay, unsigned long long* status) {
+    const uint64_t mask = (uint64_t)cap - 1;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nb; i += (int64_t)gridDim.x * blockDim.x) {
+        int64_t slot = -1;
+        if (!dev_valid(bk, i)) {
+            if (!nulls_equal) continue;
+            slot = cap;
+        } else {
+            const uint64_t key = dev_load(bk, i);
+            if (key == kEmptyKey) {
+                slot = cap + 1;
+            } else {
+                uint64_t sl = (uint64_t)hash_slot(key, bbits) * kBktWide;
+                bool placed = false;
+                for (int q = 0; q < kJnProbeLimit; ++q, sl = (sl + 1) & mask) {
+                    uint64_t k = __hip_atomic_load(&cells[sl].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (k == kEmptyKey) {
+                        k = atomicCAS((unsigned long long*)&cells[sl].key, (unsigned long long)kEmptyKey,
+                                      (unsigned long long)key);
+                        if (k == kEmptyKey) {
+#pragma unroll
+                            for (int w = 0; w < W; ++w) cells[sl].p[w] = dev_load(pay.c[w], i);
+                            placed = true;
+                            break;
+                        }
+                    }
+                    if (k == key) {
+                        atomicOr(&status[1], 1ull);  // duplicate key
+                        placed = true;
+                        break;
+                    }
+                }
+                if (!placed) atomicAdd(&status[0], 1ull);
+                continue;
+            }
+        }
+        if (atomicAdd(&status[2 + (slot - cap)], 1ull) == 0) {
+            cells[slot].key = 1ull;
+#pragma unroll
+            for (int w = 0; w < W; ++w) cells[slot].p[w] = dev_load(pay.c[w], i);
+        } else {
+            atomicOr(&status[1], 1ull);
+        }
+    }
+}
+
+// Match pass over the wide table (inner join, no marks): per round k a wave
+// looks up its 64 rows in 4 sub-rounds, lane group g = lane / 4 reading the
+// bucket of row 16 j + g of the wave, each lane one 32-B cell (two 16-B
+// loads).  The payloads of a matching cell go back to the row's lane through
+// LDS.  Every row writes its W payload words (0 on a miss) to W dense arrays
+// and each wave one 64-bit hit mask into `mwords`.
+template <bool NULLABLE, int W>
+__global__ __launch_bounds__(kJnThreads) void jn_probe_match_wide_kernel(DevCol pk, int64_t np, WideCell* cells,
+                                                                       int64_t cap, int bbits, bool nulls_equal,
+                                                                       uint64_t* __restrict__ mwords,
+                                                                       uint64_t* __restrict__ tile_counts,
+                                                                       int64_t ntiles, uint64_t* __restrict__ mp0,
+                                                                       uint64_t* __restrict__ mp1,
+                                                                       uint64_t* __restrict__ mp2) {
+    __shared__ uint64_t wsum[kJnThreads / 64];
+    __shared__ uint64_t rkey[kJnThreads];
+    __shared__ uint32_t rbkt[kJnThreads];  // home bucket, or ~0: not a regular key
+    __shared__ uint64_t hpay[W][kJnThreads];
+    const uint64_t* kp = (const uint64_t*)pk.values + pk.offset;
+    const bool wide = pk.dtype == PLGPU_I64 || pk.dtype == PLGPU_U64;
+    const int lane = threadIdx.x & 63;
+    const int wbase = threadIdx.x & ~63;
+    const int g = lane >> 2, e = lane & 3;
+    const uint64_t nbm = (uint64_t(1) << bbits) - 1;
+    uint64_t* mp[3] = {mp0, mp1, mp2};
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        constexpr int R = kJnTileRows / kJnThreads;
+        uint64_t key[R];
+        bool valid[R];
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const int64_t r = tile * kJnTileRows + (int64_t)k * kJnThreads + threadIdx.x;
+            valid[k] = r < np;
+            key[k] = 0;
+            if (valid[k]) {
+                key[k] = wide ? __builtin_nontemporal_load(kp + r) : dev_load(pk, r);
+                if (NULLABLE) valid[k] = dev_valid(pk, r) ? true : false;
+            }
+        }
+        uint64_t c = 0;
+        for (int k = 0; k < R; ++k) {
+            const int64_t r = tile * kJnTileRows + (int64_t)k * kJnThreads + threadIdx.x;
+            const bool regular = r < np && (!NULLABLE || valid[k]) && key[k] != kEmptyKey;
+            const uint32_t b = (uint32_t)hash_slot(key[k], bbits);
+            rkey[threadIdx.x] = key[k];
+            rbkt[threadIdx.x] = regular ? b : ~0u;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            uint32_t qb[4];
+            uint64_t qk[4];
+            uint4 ca[4], cb[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                qb[j] = rbkt[wbase + 16 * j + g];
+                qk[j] = rkey[wbase + 16 * j + g];
+                const uint4* cp = reinterpret_cast<const uint4*>(cells + (uint64_t)qb[j] * kBktWide + e);
+                ca[j] = qb[j] != ~0u ? cp[0] : make_uint4(0u, 0x80000000u, 0u, 0u);
+                cb[j] = qb[j] != ~0u && W > 1 ? cp[1] : make_uint4(0u, 0u, 0u, 0u);
+            }
+            uint64_t beq = 0, bem = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint64_t ck = (uint64_t)ca[j].x | ((uint64_t)ca[j].y << 32);
+                const bool live = qb[j] != ~0u;
+                const bool eq = live && ck == qk[j];
+                const bool em = live && ck == kEmptyKey;
+                const uint64_t eqm = __ballot(eq), emm = __ballot(em);
+                if (eq) {
+                    const int row = wbase + 16 * j + g;
+                    hpay[0][row] = (uint64_t)ca[j].z | ((uint64_t)ca[j].w << 32);
+                    if (W > 1) hpay[1 % W][row] = (uint64_t)cb[j].x | ((uint64_t)cb[j].y << 32);
+                    if (W > 2) hpay[2 % W][row] = (uint64_t)cb[j].z | ((uint64_t)cb[j].w << 32);
+                }
+                // this lane's row was served in sub-round lane / 16 by group lane % 16
+                if ((lane >> 4) == j) {
+                    beq = (eqm >> (4 * (lane & 15))) & 0xFull;
+                    bem = (emm >> (4 * (lane & 15))) & 0xFull;
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            bool hit = false;
+            uint64_t pay[W];
+#pragma unroll
+            for (int w = 0; w < W; ++w) pay[w] = 0;
+            if (r >= np || (NULLABLE && !valid[k])) {
+                if (r < np && NULLABLE && !valid[k] && nulls_equal && cells[cap].key == 1ull) {
+                    hit = true;
+#pragma unroll
+                    for (int w = 0; w < W; ++w) pay[w] = cells[cap].p[w];
+                }
+            } else if (key[k] == kEmptyKey) {
+                if (cells[cap + 1].key == 1ull) {
+                    hit = true;
+#pragma unroll
+                    for (int w = 0; w < W; ++w) pay[w] = cells[cap + 1].p[w];
+                }
+            } else if (beq) {
+                hit = true;
+#pragma unroll
+                for (int w = 0; w < W; ++w) pay[w] = hpay[w][threadIdx.x];
+            } else if (!bem) {
+                // the home bucket is full without the key: later buckets
+                uint64_t bb = (b + 1) & nbm;
+                for (uint64_t i = 0; i < nbm && !hit; ++i, bb = (bb + 1) & nbm) {
+                    bool stop = false;
+                    for (int ee = 0; ee < kBktWide; ++ee) {
+                        const WideCell& x = cells[bb * kBktWide + ee];
+                        if (x.key == key[k]) {
+                            hit = true;
+#pragma unroll
+                            for (int w = 0; w < W; ++w) pay[w] = x.p[w];
+                            stop = true;
+                            break;
+                        }
+                        if (x.key == kEmptyKey) {
+                            stop = true;
+                            break;
+                        }
+                    }
+                    if (stop) break;
+                }
+            }
+            if (r >= np) continue;
+#pragma unroll
+            for (int w = 0; w < W; ++w) __builtin_nontemporal_store(hit ? pay[w] : 0ull, mp[w] + r);
+            const uint64_t hw = __ballot(hit);
+            if ((threadIdx.x & 63) == 0) mwords[r >> 6] = hw;
+            c += hit ? 1 : 0;
+        }
+        uint64_t total;
+        (void)block_excl_scan(c, wsum, total);
+        if (threadIdx.x == 0) tile_counts[tile] = total;
+    }
+}
+
 // Emit of the row-format probe, fused with the take of the left columns:
 // every hit row's payload and its null-free 8-byte left columns go straight
 // to their output position (probe-row order); the row id too when other
@@ -456,12 +665,16 @@ struct TakeCols {
     int32_t n;
 };
 
-template <int NC>
+struct TakePay {
+    const uint64_t* src[3];  // dense payload words of the match pass
+    uint64_t* dst[3];        // the right output columns
+};
+
+template <int NC, int W = 1>
 __global__ __launch_bounds__(kJnThreads) void jn_take_emit_kernel(int64_t np, const uint64_t* __restrict__ mwords,
-                                                                  const uint64_t* __restrict__ mp,
+                                                                  TakePay tp,
                                                                   const uint64_t* __restrict__ tile_off,
                                                                   int64_t ntiles, TakeCols lc,
-                                                                  uint64_t* __restrict__ out_v,
                                                                   uint32_t* __restrict__ out_idx) {
     // A tile's 64 hit words (row chunk k, wave w -> word 4k + w, row order)
     // are scanned once; a row's output position is then the tile offset +
@@ -489,12 +702,13 @@ __global__ __launch_bounds__(kJnThreads) void jn_take_emit_kernel(int64_t np, co
         __syncthreads();
         const uint64_t run = tile_off[tile];
         for (int k0 = 0; k0 < R; k0 += U) {
-            uint64_t pv[U], v[U][NC > 0 ? NC : 1];
+            uint64_t pv[U][W], v[U][NC > 0 ? NC : 1];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int64_t r = tile * kJnTileRows + (int64_t)(k0 + u) * kJnThreads + threadIdx.x;
                 const int64_t rr = r < np ? r : np - 1;
-                pv[u] = __builtin_nontemporal_load(mp + rr);
+#pragma unroll
+                for (int q = 0; q < W; ++q) pv[u][q] = __builtin_nontemporal_load(tp.src[q] + rr);
 #pragma unroll
                 for (int j = 0; j < NC; ++j) v[u][j] = __builtin_nontemporal_load(lc.src[j] + rr);
             }
@@ -504,7 +718,8 @@ __global__ __launch_bounds__(kJnThreads) void jn_take_emit_kernel(int64_t np, co
                 const uint64_t w = words[wi];
                 if ((w >> lane) & 1) {
                     const uint64_t pos = run + prefix[wi] + (uint32_t)__popcll(w & lt);
-                    out_v[pos] = pv[u];
+#pragma unroll
+                    for (int q = 0; q < W; ++q) tp.dst[q][pos] = pv[u][q];
 #pragma unroll
                     for (int j = 0; j < NC; ++j) lc.dst[j][pos] = v[u][j];
                     if (out_idx)
@@ -963,6 +1178,78 @@ static int jn_build(const plgpu_column* key, bool nulls_equal, bool ordered, JnB
         return rc;
     }
     b.rows = nb;
+    *out = b;
+    return PLGPU_OK;
+}
+
+// Wide row-format table over a unique-keyed build side with W = 2..3
+// payload columns (jn_build_wide_kernel); *unique = false (and nothing
+// built) when a key repeats.  cells: (cap + 2) 32-B cells.
+struct WideBuilt {
+    WideCell* cells = nullptr;
+    int64_t cap = 0;
+    int bbits = 0;
+};
+
+static int jn_build_wide(const plgpu_column* key, const plgpu_column* pays, int W, bool nulls_equal, WideBuilt* out,
+                         bool* unique, hipStream_t s) {
+    const int64_t nb = key->length;
+    int bits = std::max(10, log2_ceil64((nb * 5 + 2) / 3));  // load <= 0.6
+    unsigned long long* status = nullptr;
+    int rc = dev_alloc((void**)&status, 32, s);
+    *unique = true;
+    WidePay wp;
+    std::memset(&wp, 0, sizeof wp);
+    for (int w = 0; w < W; ++w) wp.c[w] = dev_col(pays[w]);
+    WideBuilt b;
+    for (int attempt = 0; !rc; ++attempt) {
+        b.cap = int64_t(1) << bits;
+        b.bbits = bits - 2;  // 4 cells per bucket
+        const int64_t ne = b.cap + 2;
+        if ((rc = dev_alloc((void**)&b.cells, ne * sizeof(WideCell), s))) break;
+        hipError_t e = hipMemsetAsync(status, 0, 32, s);
+        if (e == hipSuccess) e = hipMemsetAsync(b.cells, 0x00, ne * sizeof(WideCell), s);
+        if (e == hipSuccess) {
+            const int gi = (int)std::min<int64_t>((ne + 255) / 256, 256 * 32);
+            jn_empty_wide_kernel<<<gi, 256, 0, s>>>(b.cells, b.cap);
+            const int gb = (int)std::min<int64_t>((nb + 255) / 256, 256 * 32);
+            if (nb > 0) {
+                KtScope kt("jn_build_wide_kernel", s);
+                if (W == 2)
+                    jn_build_wide_kernel<2><<<gb, 256, 0, s>>>(dev_col(*key), nb, b.cells, b.cap, b.bbits, nulls_equal,
+                                                               wp, status);
+                else
+                    jn_build_wide_kernel<3><<<gb, 256, 0, s>>>(dev_col(*key), nb, b.cells, b.cap, b.bbits, nulls_equal,
+                                                               wp, status);
+            }
+            e = hipGetLastError();
+        }
+        unsigned long long st[4] = {0, 0, 0, 0};
+        if (e == hipSuccess) e = hipMemcpyAsync(st, status, 32, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) {
+            rc = hip_fail(e, "join wide row-format build");
+            break;
+        }
+        if (st[1]) {
+            *unique = false;
+            break;
+        }
+        if (st[0] == 0) break;
+        if (attempt >= 3) {
+            rc = fail(PLGPU_ERR_CAPACITY, "join build table did not converge");
+            break;
+        }
+        dev_free(b.cells, s);
+        b.cells = nullptr;
+        bits += 2;
+    }
+    dev_free(status, s);
+    if (rc || !*unique) {
+        dev_free(b.cells, s);
+        b.cells = nullptr;
+        return rc;
+    }
     *out = b;
     return PLGPU_OK;
 }
@@ -1435,11 +1722,18 @@ PLGPU_API int plgpu_join_inner(const plgpu_column* left_key, const plgpu_column*
 }
 
 template <int NC>
-static void jn_take_emit(const JnPass& pp, const TakeCols& lc, uint64_t* mp, uint64_t* out_v, uint32_t* out_idx,
+static void jn_take_emit(const JnPass& pp, const TakeCols& lc, const TakePay& tp, int W, uint32_t* out_idx,
                          hipStream_t s) {
     KtScope kt("jn_take_emit_kernel", s);
-    jn_take_emit_kernel<NC><<<jn_pass_grid(pp), kJnThreads, 0, s>>>(pp.np, (const uint64_t*)pp.m, mp, pp.toff,
-                                                                    pp.ntiles, lc, out_v, out_idx);
+    if (W == 1)
+        jn_take_emit_kernel<NC, 1><<<jn_pass_grid(pp), kJnThreads, 0, s>>>(pp.np, (const uint64_t*)pp.m, tp, pp.toff,
+                                                                           pp.ntiles, lc, out_idx);
+    else if (W == 2)
+        jn_take_emit_kernel<NC, 2><<<jn_pass_grid(pp), kJnThreads, 0, s>>>(pp.np, (const uint64_t*)pp.m, tp, pp.toff,
+                                                                           pp.ntiles, lc, out_idx);
+    else
+        jn_take_emit_kernel<NC, 3><<<jn_pass_grid(pp), kJnThreads, 0, s>>>(pp.np, (const uint64_t*)pp.m, tp, pp.toff,
+                                                                           pp.ntiles, lc, out_idx);
 }
 
 // Inner join + take: the left frame's columns and the right frame's columns
@@ -1478,14 +1772,23 @@ PLGPU_API int plgpu_join_inner_take(const plgpu_column* left_key, const plgpu_co
         return c.validity == nullptr && c.dtype != PLGPU_STR && c.dtype != PLGPU_BOOL && dtype_bytes(c.dtype) == 8;
     };
     const bool order_ok = maintain_order == PLGPU_JOIN_ORDER_NONE || maintain_order == PLGPU_JOIN_ORDER_LEFT;
-    const bool inline_ok = order_ok && nright == 1 && fused8(right_cols[0]) &&
+    bool pay8 = nright >= 1 && nright <= 3;
+    for (int i = 0; i < nright && pay8; ++i) pay8 = fused8(right_cols[i]);
+    const bool inline_ok = order_ok && pay8 &&
                            (validate == PLGPU_JOIN_VALIDATE_M_M || validate == PLGPU_JOIN_VALIDATE_M_1) &&
                            left_key->length >= (int64_t(1) << 16) &&
                            (right_key->length <= left_key->length || maintain_order == PLGPU_JOIN_ORDER_LEFT);
+    // W = nright payload words per table cell: 16-B cells for one, 32-B
+    // cells (wide table) for two or three
+    const int W = nright;
     JnBuilt b;
+    WideBuilt wb;
     bool use_inline = false;
-    if (inline_ok) {
+    if (inline_ok && W == 1) {
         rc = jn_build_rowformat(right_key, &right_cols[0], neq, &b, &use_inline, s);
+        if (rc) return rc;
+    } else if (inline_ok) {
+        rc = jn_build_wide(right_key, right_cols, W, neq, &wb, &use_inline, s);
         if (rc) return rc;
     }
     auto release_all = [&]() {
@@ -1511,21 +1814,37 @@ PLGPU_API int plgpu_join_inner_take(const plgpu_column* left_key, const plgpu_co
         return rc;
     }
     JnPass pp;
-    uint64_t* mp = nullptr;
+    uint64_t* mp = nullptr;  // W dense payload arrays of np words
     uint32_t* idx = nullptr;
+    const int64_t npw = std::max<int64_t>(left_key->length, 1);
     rc = jn_pass_alloc(left_key->length, &pp, s);
-    if (!rc) rc = dev_alloc((void**)&mp, std::max<int64_t>(left_key->length, 1) * 8, s);
+    if (!rc) rc = dev_alloc((void**)&mp, npw * 8 * W, s);
     if (!rc) {
         const DevCol pk = as_dev(left_key);
         const int g = jn_pass_grid(pp);
         {
             KtScope kt("jn_probe_match_kernel", s);
-            if (pk.validity)
+            uint64_t* mw = reinterpret_cast<uint64_t*>(pp.m);
+            uint64_t* m1 = W > 1 ? mp + npw : nullptr;
+            uint64_t* m2 = W > 2 ? mp + 2 * npw : nullptr;
+            if (W == 1 && pk.validity)
                 jn_probe_match_kernel<true, JM_INNER, false, true><<<g, kJnThreads, 0, s>>>(
                     pk, pp.np, b.t, neq, pp.m, pp.tcount, pp.ntiles, nullptr, mp);
-            else
+            else if (W == 1)
                 jn_probe_match_kernel<false, JM_INNER, false, true><<<g, kJnThreads, 0, s>>>(
                     pk, pp.np, b.t, neq, pp.m, pp.tcount, pp.ntiles, nullptr, mp);
+            else if (W == 2 && pk.validity)
+                jn_probe_match_wide_kernel<true, 2><<<g, kJnThreads, 0, s>>>(
+                    pk, pp.np, wb.cells, wb.cap, wb.bbits, neq, mw, pp.tcount, pp.ntiles, mp, m1, m2);
+            else if (W == 2)
+                jn_probe_match_wide_kernel<false, 2><<<g, kJnThreads, 0, s>>>(
+                    pk, pp.np, wb.cells, wb.cap, wb.bbits, neq, mw, pp.tcount, pp.ntiles, mp, m1, m2);
+            else if (pk.validity)
+                jn_probe_match_wide_kernel<true, 3><<<g, kJnThreads, 0, s>>>(
+                    pk, pp.np, wb.cells, wb.cap, wb.bbits, neq, mw, pp.tcount, pp.ntiles, mp, m1, m2);
+            else
+                jn_probe_match_wide_kernel<false, 3><<<g, kJnThreads, 0, s>>>(
+                    pk, pp.np, wb.cells, wb.cap, wb.bbits, neq, mw, pp.tcount, pp.ntiles, mp, m1, m2);
         }
         rc = jn_pass_scan(&pp, s, "join probe match (row-format table)");
     }
@@ -1547,20 +1866,27 @@ PLGPU_API int plgpu_join_inner_take(const plgpu_column* left_key, const plgpu_co
             ++lc.n;
         }
     }
-    if (!rc) rc = make_owned_column(&out_right[0], right_cols[0].dtype, total, false, s);
+    TakePay tp;
+    std::memset(&tp, 0, sizeof tp);
+    for (int q = 0; q < W && !rc; ++q) {
+        rc = make_owned_column(&out_right[q], right_cols[q].dtype, total, false, s);
+        if (!rc) {
+            tp.src[q] = mp + q * npw;
+            tp.dst[q] = (uint64_t*)out_right[q].values;
+        }
+    }
     if (!rc && need_idx) rc = dev_alloc((void**)&idx, std::max<int64_t>(total, 1) * 4, s);
     if (!rc && total > 0) {
-        uint64_t* ov = (uint64_t*)out_right[0].values;
         switch (lc.n) {
-        case 0: jn_take_emit<0>(pp, lc, mp, ov, idx, s); break;
-        case 1: jn_take_emit<1>(pp, lc, mp, ov, idx, s); break;
-        case 2: jn_take_emit<2>(pp, lc, mp, ov, idx, s); break;
-        case 3: jn_take_emit<3>(pp, lc, mp, ov, idx, s); break;
-        case 4: jn_take_emit<4>(pp, lc, mp, ov, idx, s); break;
-        case 5: jn_take_emit<5>(pp, lc, mp, ov, idx, s); break;
-        case 6: jn_take_emit<6>(pp, lc, mp, ov, idx, s); break;
-        case 7: jn_take_emit<7>(pp, lc, mp, ov, idx, s); break;
-        default: jn_take_emit<8>(pp, lc, mp, ov, idx, s); break;
+        case 0: jn_take_emit<0>(pp, lc, tp, W, idx, s); break;
+        case 1: jn_take_emit<1>(pp, lc, tp, W, idx, s); break;
+        case 2: jn_take_emit<2>(pp, lc, tp, W, idx, s); break;
+        case 3: jn_take_emit<3>(pp, lc, tp, W, idx, s); break;
+        case 4: jn_take_emit<4>(pp, lc, tp, W, idx, s); break;
+        case 5: jn_take_emit<5>(pp, lc, tp, W, idx, s); break;
+        case 6: jn_take_emit<6>(pp, lc, tp, W, idx, s); break;
+        case 7: jn_take_emit<7>(pp, lc, tp, W, idx, s); break;
+        default: jn_take_emit<8>(pp, lc, tp, W, idx, s); break;
         }
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) rc = hip_fail(e, "join take emit");
@@ -1575,6 +1901,7 @@ PLGPU_API int plgpu_join_inner_take(const plgpu_column* left_key, const plgpu_co
     dev_free(mp, s);
     jn_pass_free(pp, s);
     jn_free(b, s);
+    dev_free(wb.cells, s);
     if (rc) release_all();
     else *out_len = total;
     return rc;

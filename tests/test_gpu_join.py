@@ -238,12 +238,14 @@ def test_join_int32_and_validation(gpu):
 @pytest.mark.parametrize("nulls_equal", [False, True])
 @pytest.mark.parametrize("order", ["none", "left"])
 @pytest.mark.parametrize("pdtype", ["i64", "f64", "f64-nullable"])
-def test_join_row_format_table(gpu, unique, nulls_equal, order, pdtype):
-    """Inner join with one right payload column (plgpu_join_inner_payload):
-    unique right keys put the payload into the table's cells; duplicates or
-    a nullable payload take the pairs + gather route.  Either way the result
-    equals the oracle's pairs with the payload taken at the right index."""
-    rng = np.random.default_rng(int(unique) * 4 + int(nulls_equal) * 2 + len(order) + len(pdtype))
+@pytest.mark.parametrize("npay", [1, 2, 3])
+def test_join_row_format_table(gpu, unique, nulls_equal, order, pdtype, npay):
+    """Inner join with 1..3 right payload columns (plgpu_join_inner_take):
+    unique right keys put the payloads into the table's cells (16-B cells
+    for one, 32-B cells of the wide table for two or three); duplicates or a
+    nullable payload take the pairs + gather route.  Either way the result
+    equals the oracle's pairs with every payload taken at the right index."""
+    rng = np.random.default_rng(int(unique) * 4 + int(nulls_equal) * 2 + len(order) + len(pdtype) + 16 * npay)
     nl, nr = 300_001, 60_000
     if unique:
         rk = (rng.permutation(200_000)[:nr].astype(np.int64) - 100_000) * 1_000_003
@@ -253,31 +255,38 @@ def test_join_row_format_table(gpu, unique, nulls_equal, order, pdtype):
     else:
         rk, rv = _rand_keys(rng, nr, 100_000, 0.01, True)
     lk, lv = _rand_keys(rng, nl, 200_000, 0.02, True)
-    pay = np.arange(nr, dtype=np.int64) * 7 + 1
+    base = np.arange(nr, dtype=np.int64) * 7 + 1
+    pays = [base, base * -3 + 11, base ^ 0x5555][:npay]
     pvalid = None
     if pdtype.startswith("f64"):
-        pay = pay.astype(np.float64) * 0.25
+        pays = [p.astype(np.float64) * 0.25 for p in pays]
     if pdtype.endswith("nullable"):
         pvalid = rng.random(nr) > 0.1
+    names = ["p", "q", "r"][:npay]
     ol, orr = O.join_inner(O.HostCol(lk, lv), O.HostCol(rk, rv), nulls_equal)
     left = pl.DataFrame({"k": pl.Series.from_numpy("k", lk, lv), "li": pl.Series.from_numpy("li", np.arange(nl))})
-    right = pl.DataFrame({"k": pl.Series.from_numpy("k", rk, rv), "p": pl.Series.from_numpy("p", pay, pvalid)})
+    right = pl.DataFrame([pl.Series.from_numpy("k", rk, rv)] +
+                         [pl.Series.from_numpy(nm, pays[j], pvalid if j == 0 else None) for j, nm in enumerate(names)])
     out = left.join(right, on="k", nulls_equal=nulls_equal, maintain_order=order)
-    assert out.columns == ["k", "li", "p"]
+    assert out.columns == ["k", "li"] + names
     got_l = out["li"].to_numpy().astype(np.int64)
     perm = np.argsort(ol, kind="stable")  # the oracle's pairs in left-row order
     want_l, want_r = ol[perm], orr[perm]
     if order == "left" or unique:
         assert np.array_equal(got_l, want_l)
-        gp, gv = out["p"].to_numpy(), out["p"].validity_numpy()
-        wv = np.ones(len(want_r), bool) if pvalid is None else pvalid[want_r]
-        assert np.array_equal(gv, wv)
-        assert np.array_equal(gp[gv], pay[want_r][wv])
+        for j, nm in enumerate(names):
+            gp, gv = out[nm].to_numpy(), out[nm].validity_numpy()
+            wv = np.ones(len(want_r), bool) if (pvalid is None or j > 0) else pvalid[want_r]
+            assert np.array_equal(gv, wv), nm
+            assert np.array_equal(gp[gv], pays[j][want_r][wv]), nm
     else:
         # order "none" with duplicate keys: the same pairs as a multiset
         def norm(pairs):
             return sorted(pairs, key=lambda t: (t[0], t[1] is None, t[1] if t[1] is not None else 0))
 
         assert norm(zip(got_l.tolist(), out["p"].to_list())) == norm(
-            zip(want_l.tolist(), [None if pvalid is not None and not pvalid[r] else pay[r].item()
+            zip(want_l.tolist(), [None if pvalid is not None and not pvalid[r] else pays[0][r].item()
                                   for r in want_r]))
+        if npay > 1:
+            assert sorted(zip(got_l.tolist(), out[names[-1]].to_list())) == sorted(
+                zip(want_l.tolist(), pays[-1][want_r].tolist()))

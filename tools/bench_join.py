@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--strategy", default="auto")
     ap.add_argument("--how", default="inner", help="inner / left / right / full / semi / anti")
     ap.add_argument("--order", default="none", help="maintain_order")
+    ap.add_argument("--payloads", type=int, default=1, help="build payload columns (8-byte, null-free)")
     args = ap.parse_args()
     import torch
 
@@ -54,19 +55,26 @@ def main():
         pk[s:e] = torch.randint(0, 2 * m, (e - s,), device="cuda", generator=g)
         pv[s:e] = torch.rand(e - s, device="cuda", generator=g, dtype=torch.float64)
     bk = torch.randperm(2 * m, device="cuda", generator=g)[:m].to(torch.int64)
-    bv = torch.rand(m, device="cuda", generator=g, dtype=torch.float64)
+    bvs = [torch.rand(m, device="cuda", generator=g, dtype=torch.float64) for _ in range(args.payloads)]
     probe = pl.DataFrame([pl.Series.from_torch("k", pk), pl.Series.from_torch("pv", pv)])
-    build = pl.DataFrame([pl.Series.from_torch("k", bk), pl.Series.from_torch("bv", bv)])
+    build = pl.DataFrame([pl.Series.from_torch("k", bk)] +
+                         [pl.Series.from_torch(f"bv{i}" if i else "bv", t) for i, t in enumerate(bvs)])
     out = None
     kw = dict(on="k", how=args.how, maintain_order=args.order)
+    from polaroid_amd import _native as N
+
     for _ in range(args.warmup):
         out = probe.join(build, **kw)
     torch.cuda.synchronize()
+    prev = N.set_option("ktime", 1)
+    N.ktime_read(reset=True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         out = probe.join(build, **kw)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / args.steps
+    kt = N.ktime_read(reset=True)
+    N.set_option("ktime", prev)
     rows_out = out.height
     print(json.dumps({
         "metric": f"Mrows/sec hash {args.how}-join probe (1e9 probe x 1e7 build, i64 key), materialised",
@@ -75,7 +83,8 @@ def main():
         "dtype": "int64", "data": "synthetic keys/payloads generated on device",
         "config": {"workload": f"probe.join(build, on='k', how='{args.how}', maintain_order='{args.order}'), "
                                "output every column", "probe_rows": n,
-                   "build_rows": m, "output_rows": rows_out},
+                   "build_rows": m, "output_rows": rows_out, "build_payloads": args.payloads},
+        "kernels": {k: round(ms / args.steps, 4) for k, (ms, c) in kt.items()},
     }), flush=True)
 
 
