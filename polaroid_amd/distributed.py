@@ -50,6 +50,52 @@ def _device_for(group) -> Any:
     return torch.device("cpu")
 
 
+def _staged(group, *tensors) -> bool:
+    """A gloo group over device tensors (ranks sharing one GPU in a test,
+    or a host-only transport): the collective goes through host copies."""
+    import torch.distributed as dist
+
+    return dist.get_backend(group) == "gloo" and any(t is not None and t.is_cuda for t in tensors)
+
+
+def _a2a(out, inp, out_splits=None, in_splits=None, group=None) -> None:
+    """all_to_all_single on the group's transport (host-staged for gloo)."""
+    import torch.distributed as dist
+
+    kw = {} if out_splits is None else {"output_split_sizes": list(out_splits), "input_split_sizes": list(in_splits)}
+    if _staged(group, out, inp):
+        o = out.new_empty(out.shape, device="cpu")
+        dist.all_to_all_single(o, inp.cpu(), group=group, **kw)
+        out.copy_(o)
+        return
+    dist.all_to_all_single(out, inp, group=group, **kw)
+
+
+def _all_gather(parts, t, group=None) -> None:
+    """all_gather on the group's transport (host-staged for gloo)."""
+    import torch.distributed as dist
+
+    if _staged(group, t):
+        hp = [p.new_empty(p.shape, device="cpu") for p in parts]
+        dist.all_gather(hp, t.cpu(), group=group)
+        for p, h in zip(parts, hp):
+            p.copy_(h)
+        return
+    dist.all_gather(parts, t, group=group)
+
+
+def _all_reduce(t, op, group=None) -> None:
+    """all_reduce on the group's transport (host-staged for gloo)."""
+    import torch.distributed as dist
+
+    if _staged(group, t):
+        h = t.cpu()
+        dist.all_reduce(h, op=op, group=group)
+        t.copy_(h)
+        return
+    dist.all_reduce(t, op=op, group=group)
+
+
 def _allreduce_max(vals: Sequence[int], group, device) -> list[int]:
     import torch
     import torch.distributed as dist
@@ -109,9 +155,8 @@ def alltoallv(out, inp, out_splits: Sequence[int], in_splits: Sequence[int], gro
     import torch.distributed as dist
 
     esz = inp.element_size()
-    if max(list(out_splits) + list(in_splits) + [0]) * esz <= A2A_MAX_BYTES:
-        dist.all_to_all_single(out, inp, output_split_sizes=list(out_splits), input_split_sizes=list(in_splits),
-                               group=group)
+    if max(list(out_splits) + list(in_splits) + [0]) * esz <= A2A_MAX_BYTES or _staged(group, out, inp):
+        _a2a(out, inp, out_splits, in_splits, group)
         return
     world = dist.get_world_size(group)
     me = dist.get_rank(group)
@@ -152,7 +197,7 @@ def exchange_records(send, counts: Sequence[int], record_words: int, group=None,
     h = len(header)
     sc = torch.tensor([[int(c)] + [int(x) for x in header] for c in counts], dtype=torch.int64, device=device)
     rc = torch.empty_like(sc)
-    dist.all_to_all_single(rc, sc, group=group)
+    _a2a(rc, sc, group=group)
     rows = [[int(v) for v in r] for r in rc.view(world, 1 + h).tolist()]
     rcounts = [r[0] for r in rows]
     recv = torch.empty(sum(rcounts) * record_words, dtype=torch.int64, device=device)
@@ -392,8 +437,8 @@ def _pack_keys(df, keys: list, group, device):
     N.check(N.lib().plgpu_key_ranges(kcols, nk, r, None))
     t = torch.tensor(list(r), dtype=torch.int64, device=device).view(nk, 3)
     lo, hi = t[:, 0].contiguous(), t[:, 1:].contiguous()
-    dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=group)
-    dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=group)
+    _all_reduce(lo, dist.ReduceOp.MIN, group)
+    _all_reduce(hi, dist.ReduceOp.MAX, group)
     agreed = torch.cat([lo.view(nk, 1), hi], dim=1).view(-1).tolist()
     ranges = (C.c_int64 * (3 * nk))(*agreed)
     codes = N.Column()
@@ -851,7 +896,7 @@ def exchange_columns(cols: Sequence[WireColumn], counts: Sequence[int], group=No
     device = cols[0].values.device if cols else torch.device("cpu")
     sc = torch.tensor(list(counts), dtype=torch.int64, device=device)
     rc = torch.empty_like(sc)
-    dist.all_to_all_single(rc, sc, group=group)
+    _a2a(rc, sc, group=group)
     rcounts = [int(v) for v in rc.tolist()]
     n = sum(rcounts)
     out = []
@@ -871,7 +916,7 @@ def exchange_columns(cols: Sequence[WireColumn], counts: Sequence[int], group=No
             sb = _segment_sums(c.values, counts)
             sbt = torch.tensor(sb, dtype=torch.int64, device=device)
             rbt = torch.empty_like(sbt)
-            dist.all_to_all_single(rbt, sbt, group=group)
+            _a2a(rbt, sbt, group=group)
             rb = [int(v) for v in rbt.tolist()]
             data = torch.empty(sum(rb), dtype=torch.uint8, device=device)
             alltoallv(data, c.data, rb, sb, group)
@@ -891,7 +936,7 @@ def allgather_columns(cols: Sequence[WireColumn], rows: int, group=None):
     device = cols[0].values.device if cols else torch.device("cpu")
     cnt = torch.tensor([rows], dtype=torch.int64, device=device)
     allc = [torch.empty_like(cnt) for _ in range(world)]
-    dist.all_gather(allc, cnt, group=group)
+    _all_gather(allc, cnt, group)
     counts = [int(t.item()) for t in allc]
     cap = max(counts) if counts else 0
     total = sum(counts)
@@ -906,20 +951,20 @@ def allgather_columns(cols: Sequence[WireColumn], rows: int, group=None):
             padded = torch.zeros(cap, dtype=t.dtype, device=t.device)
             padded[:rows] = t[:rows]
             parts = [torch.empty(cap, dtype=t.dtype, device=t.device) for _ in range(world)]
-            dist.all_gather(parts, padded, group=group)
+            _all_gather(parts, padded, group)
             bufs.append(torch.cat([p[:k] for p, k in zip(parts, counts)]) if total else
                         torch.empty(0, dtype=t.dtype, device=t.device))
         data = None
         if dt == N.STR:
             nb = torch.tensor([int(c.data.numel())], dtype=torch.int64, device=device)
             alln = [torch.empty_like(nb) for _ in range(world)]
-            dist.all_gather(alln, nb, group=group)
+            _all_gather(alln, nb, group)
             bcounts = [int(t.item()) for t in alln]
             bcap = max(bcounts) if bcounts else 0
             padded = torch.zeros(bcap, dtype=torch.uint8, device=device)
             padded[:bcounts[dist.get_rank(group)]] = c.data
             parts = [torch.empty(bcap, dtype=torch.uint8, device=device) for _ in range(world)]
-            dist.all_gather(parts, padded, group=group)
+            _all_gather(parts, padded, group)
             data = torch.cat([p[:k] for p, k in zip(parts, bcounts)]) if bcap else \
                 torch.empty(0, dtype=torch.uint8, device=device)
         out.append(WireColumn(name, dt, bufs[0], bufs[1], data))
@@ -1077,7 +1122,7 @@ def run_join(ops, left, right, left_keys: Sequence[str], right_keys: Sequence[st
         raise ValueError(f"invalid join type {how!r}")
     world = dist.get_world_size(group)
     sizes = torch.tensor([ops.rows(left), ops.rows(right)], dtype=torch.int64, device=device)
-    dist.all_reduce(sizes, group=group)
+    _all_reduce(sizes, dist.ReduceOp.SUM, group)
     nl, nr = (int(v) for v in sizes.tolist())
     allowed = _BROADCASTABLE[how]
     # the side to broadcast: the smaller allowed one
