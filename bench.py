@@ -61,6 +61,7 @@ def parse():
     ap.add_argument("--no-std", action="store_true")
     ap.add_argument("--no-sort", action="store_true", help="skip the configs[2] sort + rolling leg")
     ap.add_argument("--no-join", action="store_true", help="skip the configs[3] join leg")
+    ap.add_argument("--no-keys", action="store_true", help="skip the Categorical / String / (symbol, day) legs")
     ap.add_argument("--leg-steps", type=int, default=5, help="timed steps of the sort and join legs (<= --steps)")
     ap.add_argument("--dry-run", action="store_true",
                     help="print this rank's launch parameters and exit before touching the GPU (tests)")
@@ -236,6 +237,76 @@ def std_leg(torch, pl, df, steps: int, warmup: int) -> dict:
     r = timed_leg(torch, q, df.height, steps, warmup, 16)
     return {"query": "filter(close > 250).group_by(symbol).agg(close.std())",
             "kernel": "gb_fast_kernel<NACC=3,PRED=1,SUMONLY,VAR> (variance triple)", **r}
+
+
+def key_frame(torch, pl, sym, cols: dict, case: str):
+    """The headline frame with another symbol encoding (the same rows):
+    "categorical" (UInt32 codes over a 100-string dictionary, as polars
+    exports a Categorical), "string" (5-byte tickers as Arrow large_string)
+    or "sym_day" (the Int64 symbol and an Int32 day rising with the row
+    number: time-ordered daily bars).  Returns (frame, group-by keys, buffers
+    to keep alive)."""
+    import pyarrow as pa
+
+    from polaroid_amd import _native as N
+
+    n = sym.numel()
+    vals = [pl.Series.from_torch(nm, t) for nm, t in cols.items()]
+    k = (sym - 1_000_000) // 7919  # 0..99
+    if case == "categorical":
+        codes = k.to(torch.int32)
+        cs = pl.Series.from_device("symbol", pl.UInt32, codes.data_ptr(), n, keepalive=codes)
+        dictionary = pl.Series.from_arrow("symbol", pa.array([f"SYM{i:02d}" for i in range(100)], pa.large_string()))
+        return pl.DataFrame([pl.Series._categorical("symbol", dictionary, cs)] + vals), ("symbol",), [codes]
+    if case == "string":
+        pool = torch.tensor([list(f"SYM{i:02d}".encode()) for i in range(100)], dtype=torch.uint8, device=sym.device)
+        data = torch.empty(n * 5, dtype=torch.uint8, device=sym.device)
+        ch = 1 << 27
+        for s in range(0, n, ch):
+            e = min(n, s + ch)
+            data[s * 5:e * 5] = pool[k[s:e]].reshape(-1)
+        offsets = torch.arange(0, (n + 1) * 5, 5, dtype=torch.int64, device=sym.device)
+        st = pl.Series.from_device("symbol", pl.Int64, offsets.data_ptr(), n, keepalive=(offsets, data))
+        st._col.dtype = N.STR
+        st._col.data = data.data_ptr()
+        return pl.DataFrame([st] + vals), ("symbol",), [offsets, data]
+    day = (torch.arange(n, device=sym.device, dtype=torch.int64) // (n // 250 + 1)).to(torch.int32)
+    return (pl.DataFrame([pl.Series.from_torch("symbol", sym), pl.Series.from_torch("day", day)] + vals),
+            ("symbol", "day"), [day])
+
+
+def keys_leg(torch, pl, sym, cols: dict, steps: int, warmup: int, headline_ms: float) -> dict:
+    """The headline query over the other key encodings of the same rows
+    (key_frame): Categorical symbol (grouped by its UInt32 codes, the
+    reference's into_groups.rs:132-139), String symbol, and (symbol, day)
+    (both keys packed into the group code inside the fused kernel).  Each
+    case: ms per collect(), the fused kernel's HIP-event time, and the ratio
+    to the Int64 headline's step.  rank 0, N = 1."""
+    from polaroid_amd import _native as N
+
+    out = {}
+    sums = [pl.col(c).sum() for c in ("open", "high", "low", "close")]
+    for case, bpr in (("categorical", 36), ("sym_day", 44), ("string", 45)):
+        df, keys, keep = key_frame(torch, pl, sym, cols, case)
+        q = df.lazy().filter(pl.col("close") > THRESHOLD).group_by(*keys).agg(*sums)
+
+        def step():
+            info = {}
+            q.collect(info=info)
+            return info
+
+        ms, kernels, info = _time_steps(torch, step, steps, warmup)
+        kms = kernels.get("gb_fast_kernel", {}).get("ms_mean")
+        out[case] = {"ms_per_step": round(ms, 3), "vs_int64_headline": round(ms / headline_ms, 3),
+                     "kernel_ms": kms, "bytes_per_row": bpr,
+                     "frac": round(bpr * sym.numel() / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if kms else None,
+                     "key_pack": info.get("key_pack"), "categorical_codes": info.get("categorical_codes", 0),
+                     "kernels": kernels}
+        del df, q, keep
+        torch.cuda.empty_cache()
+    out["note"] = ("bytes_per_row: the fused kernel's algorithmic bytes (categorical: 4 B codes + 32 B; sym_day: "
+                   "8 + 4 + 32; string: 8 B offsets + 5 B of bytes + 32)")
+    return out
 
 
 def _kernel_table(kt: dict, steps: int) -> dict:
@@ -603,6 +674,9 @@ def main():
     if rank == 0 and world == 1 and not args.no_std:
         result["std"] = std_leg(torch, pl, df, args.steps, args.warmup)
         progress("std leg done")
+    if rank == 0 and world == 1 and not args.no_keys:
+        result["keys"] = keys_leg(torch, pl, sym, cols, args.leg_steps * 2, 2, ms_per_step)
+        progress("keys leg done")
     if rank == 0 and world == 1 and not (args.no_sort and args.no_join and args.no_plugin):
         # the remaining legs need the HBM the headline frame holds
         del df, query, out, sym, cols

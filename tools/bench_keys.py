@@ -28,7 +28,6 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--only", default="int64,categorical,string,sym_day")
     args = ap.parse_args()
-    import pyarrow as pa
     import torch
 
     import bench
@@ -37,39 +36,14 @@ def main():
 
     n = int(args.rows)
     sym, cols = bench.make_data(torch, n, 100, seed=1234)
-    k = (sym - 1_000_000) // 7919  # 0..99
     vals = [pl.Series.from_torch(nm, t) for nm, t in cols.items()]
     sums = [pl.col(c).sum() for c in ("open", "high", "low", "close")]
     pred = pl.col("close") > bench.THRESHOLD
 
     def frame(case):
-        keep = []
         if case == "int64":
-            return pl.DataFrame([pl.Series.from_torch("symbol", sym)] + vals), ("symbol",), keep
-        if case == "categorical":
-            codes = k.to(torch.int32)
-            keep.append(codes)
-            cs = pl.Series.from_device("symbol", pl.UInt32, codes.data_ptr(), n, keepalive=codes)
-            dictionary = pl.Series.from_arrow("symbol", pa.array([f"SYM{i:02d}" for i in range(100)],
-                                                                 pa.large_string()))
-            return pl.DataFrame([pl.Series._categorical("symbol", dictionary, cs)] + vals), ("symbol",), keep
-        if case == "string":
-            pool = torch.tensor([list(f"SYM{i:02d}".encode()) for i in range(100)], dtype=torch.uint8,
-                                device="cuda")
-            data = torch.empty(n * 5, dtype=torch.uint8, device="cuda")
-            ch = 1 << 27
-            for s in range(0, n, ch):
-                e = min(n, s + ch)
-                data[s * 5:e * 5] = pool[k[s:e]].reshape(-1)
-            offsets = torch.arange(0, (n + 1) * 5, 5, dtype=torch.int64, device="cuda")
-            st = pl.Series.from_device("symbol", pl.Int64, offsets.data_ptr(), n, keepalive=(offsets, data))
-            st._col.dtype = N.STR
-            st._col.data = data.data_ptr()
-            return pl.DataFrame([st] + vals), ("symbol",), keep
-        day = (torch.arange(n, device="cuda", dtype=torch.int64) // (n // 250 + 1)).to(torch.int32)
-        keep.append(day)
-        ds = pl.Series.from_torch("day", day)
-        return pl.DataFrame([pl.Series.from_torch("symbol", sym), ds] + vals), ("symbol", "day"), keep
+            return pl.DataFrame([pl.Series.from_torch("symbol", sym)] + vals), ("symbol",), []
+        return bench.key_frame(torch, pl, sym, cols, case)
 
     for case in args.only.split(","):
         df, keys, keep = frame(case)
