@@ -116,6 +116,11 @@ struct AccSpec {
 // tile arrives -- no code column is written or read.  n = 0: the key is
 // GbParams::key itself.  A selected row whose field leaves its bits sets
 // ST_KPACK and the caller repacks with the exact ranges.
+// A String key (n = 1, c[0].dtype PLGPU_STR, null-free) is formed the same
+// way as its exact short-string code (len << 56) | bytes (strings.hip
+// str_code_kernel) from the offsets and one or two aligned data words; a
+// selected string longer than 7 bytes sets ST_KPACK (the caller takes the
+// hashed long-string path).
 constexpr int kKpMax = 4;
 struct KeyPack {
     int32_t n;
@@ -124,6 +129,7 @@ struct KeyPack {
     uint64_t base[kKpMax];  // minv[i] - nul[i] (wrapping): field i = v - base[i]
     int32_t shift[kKpMax];
     int32_t bits[kKpMax];
+    int64_t data_end;       // String key: bytes in the data buffer (bounds the word loads)
 };
 
 struct GbParams {
@@ -250,10 +256,39 @@ __device__ __forceinline__ uint64_t kp_field(const KeyPack& k, int i, uint64_t r
     return f << k.shift[i];
 }
 
+// Short-string code of the string [b, b + len) of a String column's data
+// (len <= 7; `bad` when longer): aligned word loads within data_end, bytes
+// otherwise.
+__device__ __forceinline__ uint64_t kp_str_code(const uint8_t* data, int64_t data_end, uint64_t b, uint64_t len,
+                                                bool& bad) {
+    if (len > 7) {
+        bad = true;
+        return 0;
+    }
+    if (len == 0) return 0;
+    const uint64_t* dw = (const uint64_t*)data;
+    const uint64_t w = b >> 3;
+    const int sh = (int)(b & 7) * 8;
+    uint64_t x;
+    if ((int64_t)((w + 1) * 8) <= data_end && (sh + 8 * (int)len <= 64 || (int64_t)((w + 2) * 8) <= data_end)) {
+        x = dw[w] >> sh;
+        if (sh + 8 * (int)len > 64) x |= dw[w + 1] << (64 - sh);
+    } else {
+        x = 0;
+        for (uint64_t j = 0; j < len; ++j) x |= (uint64_t)data[b + j] << (8 * j);
+    }
+    return (len << 56) | (x & ((1ull << (8 * len)) - 1));
+}
+
 // The group key of row r as every pass but the fused kernel's tile loads
 // reads it: the key column, or the packed code of the key columns.
 __device__ __forceinline__ uint64_t gb_key(const GbParams& p, int64_t r) {
     if (p.kp.n == 0) return key_at(p.key, r);
+    if (p.kp.c[0].dtype == PLGPU_STR) {
+        const int64_t* o = (const int64_t*)p.kp.c[0].values + p.kp.c[0].offset + r;
+        bool bad = false;
+        return kp_str_code(p.kp.c[0].data, p.kp.data_end, (uint64_t)o[0], (uint64_t)(o[1] - o[0]), bad);
+    }
     uint64_t code = 0;
     bool bad = false;
     for (int i = 0; i < p.kp.n; ++i) code |= kp_field(p.kp, i, dev_load(p.kp.c[i], r), bad);
@@ -1016,7 +1051,12 @@ __device__ __forceinline__ void fast_load_tail(const GbParams& p, int64_t t, Fas
     for (int j = 0; j < ROWS; ++j) {
         const int64_t r = fast_row(t, T, ROWS, j);
         const bool in = r < p.n;
-        if (PACK) {
+        if (PACK && p.kp.c[0].dtype == PLGPU_STR) {
+            // String key: kr[0][j] = offset of row r, kr[1][j] = of row r + 1
+            const int64_t* o = (const int64_t*)p.kp.c[0].values + p.kp.c[0].offset;
+            x.kr[0][j] = in ? (uint64_t)o[r] : 0ull;
+            x.kr[1][j] = in ? (uint64_t)o[r + 1] : 0ull;
+        } else if (PACK) {
 #pragma unroll
             for (int i = 0; i < kKpFast; ++i) x.kr[i][j] = in && i < p.kp.n ? dev_load(p.kp.c[i], r) : 0ull;
         } else {
@@ -1046,7 +1086,17 @@ __device__ __forceinline__ void fast_load(const GbParams& p, int64_t t, FastTile
     for (int q = 0; q < ROWS / 2; ++q) {
         int64_t r = rbase + fast_row(t, T, ROWS, 2 * q);
         if (rmax >= 0) r = r < rmax ? r : rmax;
-        if (PACK) {
+        if (PACK && p.kp.c[0].dtype == PLGPU_STR) {
+            // String key: the pair's offsets (16 B) and the next row's (8 B):
+            // kr[0][j] = start, kr[1][j] = end of row 2q + j
+            const int64_t* o = (const int64_t*)p.kp.c[0].values + p.kp.c[0].offset + r;
+            const u64x2_t a = ld16<NT>((const uint64_t*)o);
+            const uint64_t e = NT ? __builtin_nontemporal_load((const uint64_t*)o + 2) : ((const uint64_t*)o)[2];
+            x.kr[0][2 * q] = a.x;
+            x.kr[0][2 * q + 1] = a.y;
+            x.kr[1][2 * q] = a.y;
+            x.kr[1][2 * q + 1] = e;
+        } else if (PACK) {
             // each packed key column: one 16-byte (Int64) or 8-byte (Int32 /
             // UInt32) load per row pair, kept raw until the rows are consumed
 #pragma unroll
@@ -1359,10 +1409,22 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
     for (; t < nall; t += tstep) {
         if constexpr (!VAR) fast_share<NACC, ROWS, DERIV, PACK>(vf0, wf0, cur);
         bool kout[ROWS];
+        const bool kstr = PACK && kpdt[0] == PLGPU_STR;
+        if (kstr) {
+            // String key: each row's short-string code from its offsets and
+            // one or two data words (dependent loads, issued for the tile's
+            // rows together)
+#pragma unroll
+            for (int j = 0; j < ROWS; ++j) {
+                kout[j] = false;
+                cur.key[j] = kp_str_code(p.kp.c[0].data, p.kp.data_end, cur.kr[0][j], cur.kr[1][j] - cur.kr[0][j],
+                                         kout[j]);
+            }
+        }
 #pragma unroll
         for (int j = 0; j < ROWS; ++j) {
-            kout[j] = false;
-            if (PACK) {
+            if (!kstr) kout[j] = false;
+            if (PACK && !kstr) {
                 // the packed code of row j (mk_plan_pack's layout)
                 uint64_t code = 0;
 #pragma unroll
@@ -3184,6 +3246,9 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
                ((uintptr_t)c.values & 15) == 0;
     };
     auto ok_kp = [](const KeyPack& k) {
+        if (k.n == 1 && k.c[0].dtype == PLGPU_STR)
+            return k.c[0].validity == nullptr && (k.c[0].offset & 1) == 0 && ((uintptr_t)k.c[0].values & 15) == 0 &&
+                   ((uintptr_t)k.c[0].data & 7) == 0;
         bool good = k.n > 0 && k.n <= kKpFast;
         for (int i = 0; i < k.n && good; ++i) {
             const DevCol& c = k.c[i];
@@ -4567,6 +4632,53 @@ static int gb_multi_packed(const MkKeys& mk, MkPack pk, int64_t n, const plgpu_c
     return gb_multi_decode(pk, keys, nkeys, hout, out_keys, out_aggs, naggs, s);
 }
 
+// A single null-free String key grouped on short-string codes formed in the
+// fused kernel (KeyPack with a String column).  *done = false (nothing
+// produced) when the fused kernel does not apply or a selected string is
+// longer than 7 bytes.
+static int gb_str_fused(const plgpu_column& key, const plgpu_column* cols, int32_t ncols, const Deriv* deriv,
+                        const plgpu_instr* program, int32_t n_instr, const plgpu_agg* aggs, int32_t naggs,
+                        int32_t maintain_order, plgpu_column* out_keys, plgpu_column* out_aggs,
+                        plgpu_groupby_info* info, hipStream_t s, bool* done) {
+    *done = false;
+    const int64_t n = key.length;
+    int64_t data_end = 0;
+    PLGPU_HIP(hipMemcpyAsync(&data_end, (const int64_t*)key.values + key.offset + n, 8, hipMemcpyDeviceToHost, s));
+    PLGPU_HIP(hipStreamSynchronize(s));
+    KeyPack kp;
+    std::memset(&kp, 0, sizeof kp);
+    kp.n = 1;
+    kp.c[0] = dev_col(key);
+    kp.bits[0] = 64;
+    kp.data_end = data_end;
+    plgpu_column ck;
+    std::memset(&ck, 0, sizeof ck);
+    ck.dtype = PLGPU_I64;
+    ck.length = n;
+    ck.values = key.values;  // never read as a key column while p.kp.n > 0
+    GbRun R;
+    int rc = gb_prepare(R, &ck, cols, ncols, program, n_instr, aggs, naggs, maintain_order != 0, false, s, deriv);
+    if (!rc) {
+        R.pl.p.kp = kp;
+        rc = gb_plan(R, nullptr);
+    }
+    if (rc || R.kp_fallback) return rc;
+    rc = gb_main(R, true, nullptr, nullptr);
+    if (rc || R.kp_bad) return rc;  // a long string: the hashed path
+    plgpu_column hout;
+    std::memset(&hout, 0, sizeof hout);
+    if (info) gb_fill_info(R, info);
+    if ((rc = gb_finalize(R, naggs, &hout, out_aggs))) return rc;
+    rc = str_from_codes(hout, &out_keys[0], s);
+    plgpu_column_release(&hout);
+    if (rc) {
+        for (int i = 0; i < naggs; ++i) plgpu_column_release(&out_aggs[i]);
+        return rc;
+    }
+    *done = true;
+    return PLGPU_OK;
+}
+
 static int gb_multi_impl(const plgpu_column* keys, int32_t nkeys, const plgpu_column* cols, int32_t ncols,
                          const Deriv* deriv, const plgpu_instr* program, int32_t n_instr, const plgpu_agg* aggs,
                          int32_t naggs, int32_t maintain_order, plgpu_column* out_keys, plgpu_column* out_aggs,
@@ -4587,6 +4699,16 @@ static int gb_multi_impl(const plgpu_column* keys, int32_t nkeys, const plgpu_co
         mk.c[i] = to_dev(keys[i]);
     }
     hipStream_t s = as_stream(stream);
+    if (nkeys == 1 && keys[0].dtype == PLGPU_STR && keys[0].validity == nullptr && n >= (int64_t(1) << 20) &&
+        options().fuse_keys) {
+        // one null-free String key: its short-string codes formed inside the
+        // fused kernel (no code column); a string longer than 7 bytes, or a
+        // plan off the fused kernel, falls through to the passes below
+        bool done = false;
+        const int rc = gb_str_fused(keys[0], cols, ncols, deriv, program, n_instr, aggs, naggs, maintain_order,
+                                    out_keys, out_aggs, info, s, &done);
+        if (rc || done) return rc;
+    }
     {
         // String keys whose strings are all <= 7 bytes: exact Int64 codes,
         // grouped as integer keys; the output codes turn back into strings

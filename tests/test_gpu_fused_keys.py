@@ -214,3 +214,43 @@ def test_categorical_key_also_used_elsewhere(gpu):
     # the column's strings are gathered for other uses (a filter of the frame)
     f = df.filter(pl.col("c") == "GOOG")
     assert f["c"].to_list() == [s for s in strs if s == "GOOG"]
+
+
+def _string_frame(keys_list, vals):
+    return pl.DataFrame([pl.Series("s", keys_list, pl.String), pl.Series.from_numpy("v", vals)])
+
+
+@pytest.mark.parametrize("case", ["short", "long_selected", "long_unselected", "empty_strings"])
+def test_fused_string_key(gpu, case):
+    """One null-free String key of a large input: its exact short-string
+    codes are formed inside the fused kernel from the offsets and data words
+    (no code column); a selected string longer than 7 bytes sends the
+    query to the hashed long-string path (key_pack 0), one in an unselected
+    row does not.  Same groups and exact sums as Python on the strings."""
+    rng = np.random.default_rng(len(case))
+    n = 1_200_001
+    pool = np.array([f"S{i}" for i in range(150)] + ["", "abcdefg"], dtype=object)
+    if case == "empty_strings":
+        pool[:20] = ""
+    idx = rng.integers(0, len(pool), n)
+    strs = pool[idx].astype(object)
+    v = rng.uniform(0, 100, n)
+    if case == "long_selected":
+        strs[n // 3] = "a-much-longer-symbol"
+        v[n // 3] = 99.0
+    if case == "long_unselected":
+        strs[n // 3] = "a-much-longer-symbol"
+        v[n // 3] = 1.0
+    df = _string_frame(strs.tolist(), v)
+    info = {}
+    out = df.lazy().filter(pl.col("v") > 50.0).group_by("s").agg(pl.col("v").sum().alias("sv"), pl.len()).collect(
+        info=info)
+    assert info["key_pack"] == (0 if case == "long_selected" else 1), info
+    sel = v > 50.0
+    want = {}
+    for sv, x in zip(strs[sel].tolist(), v[sel].tolist()):
+        want.setdefault(sv, []).append(x)
+    got = dict(zip(out["s"].to_list(), zip(out["sv"].to_list(), out["len"].to_list())))
+    assert set(got) == set(want)
+    for key, xs in want.items():
+        assert got[key] == (math.fsum(xs), len(xs)), key
