@@ -1263,16 +1263,23 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
         if (PART || tt < ntiles) fast_load<NL, PRED, ROWS, true, DERIV, PACK>(p, tt, x, rbase, rmax);
         else fast_load_tail<NL, PRED, ROWS, DERIV, PACK>(p, tt, x);
     };
-    // PACK: the plan's field bases / shifts / widths, hoisted (uniform)
-    uint64_t kpb[kKpFast];
-    int32_t kpsh[kKpFast], kpbits[kKpFast], kpdt[kKpFast];
+    // PACK: the plan's fields as uniform constants, hoisted.  Field i of a
+    // raw word w is ((w & kpm) ^ kpx) - kpc: kpm keeps a 4-byte value's low
+    // half, kpx = 2^31 sign-extends an Int32 ((v ^ 2^31) - 2^31), kpc =
+    // kpx + base; a field fits iff (field & kphm) == 0.
+    uint64_t kpm[kKpFast], kpx[kKpFast], kpc[kKpFast], kphm[kKpFast];
+    int32_t kpsh[kKpFast], kpdt[kKpFast];
 #pragma unroll
     for (int i = 0; i < kKpFast; ++i) {
         const bool on = PACK && i < p.kp.n;
-        kpb[i] = on ? p.kp.base[i] : 0ull;
+        const int32_t dt = on ? p.kp.c[i].dtype : PLGPU_I64;
+        const int32_t bits = on ? p.kp.bits[i] : 64;
+        kpm[i] = (dt == PLGPU_I32 || dt == PLGPU_U32) ? 0xFFFFFFFFull : ~0ull;
+        kpx[i] = dt == PLGPU_I32 ? 0x80000000ull : 0ull;
+        kpc[i] = kpx[i] + (on ? p.kp.base[i] : 0ull);
+        kphm[i] = bits >= 64 ? 0ull : ~((1ull << bits) - 1);
         kpsh[i] = on ? p.kp.shift[i] : 0;
-        kpbits[i] = on ? p.kp.bits[i] : 64;
-        kpdt[i] = on ? p.kp.c[i].dtype : PLGPU_I64;
+        kpdt[i] = dt;
     }
     constexpr uint32_t VM = (1u << NACC) - 1u;
     // RACC (partition buffers, sum-only, 2 limbs): each lane keeps KR
@@ -1427,15 +1434,14 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
             if (PACK && !kstr) {
                 // the packed code of row j (mk_plan_pack's layout)
                 uint64_t code = 0;
+                bool out = false;
 #pragma unroll
                 for (int i = 0; i < kKpFast; ++i) {
-                    const uint64_t raw = cur.kr[i][j];
-                    const uint64_t v = kpdt[i] == PLGPU_I32 ? (uint64_t)(int64_t)(int32_t)(uint32_t)raw
-                                                            : (kpdt[i] == PLGPU_U32 ? (uint64_t)(uint32_t)raw : raw);
-                    const uint64_t f = v - kpb[i];
-                    kout[j] |= kpbits[i] < 64 && (f >> kpbits[i]) != 0;
+                    const uint64_t f = ((cur.kr[i][j] & kpm[i]) ^ kpx[i]) - kpc[i];
+                    out |= (f & kphm[i]) != 0;
                     code |= f << kpsh[i];
                 }
+                kout[j] = out;
                 cur.key[j] = code;
             }
         }
@@ -3162,9 +3168,12 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
     // column has no selected nonzero value in the sample, its acc tasks run
     // again unfiltered (the key task is not repeated)
     const bool ps = R.pred == 1;
-    gb_plan_kernel<<<p.nacc * kPlanBlocks + kPlanKeyBlocks, kPlanThreads, 0, R.s>>>(
-        p, R.status + kPlanSetWord, kPlanSamples, ps ? 1 : 0, ps ? R.dp.simple_isf : 0, ps ? R.dp.simple_op : 0,
-        ps ? R.dp.simple_imm : 0ull);
+    {
+        KtScope kt("gb_plan_kernel", R.s);
+        gb_plan_kernel<<<p.nacc * kPlanBlocks + kPlanKeyBlocks, kPlanThreads, 0, R.s>>>(
+            p, R.status + kPlanSetWord, kPlanSamples, ps ? 1 : 0, ps ? R.dp.simple_isf : 0, ps ? R.dp.simple_op : 0,
+            ps ? R.dp.simple_imm : 0ull);
+    }
     PLGPU_HIP(hipGetLastError());
     PLGPU_HIP(hipMemcpyAsync(R.st, R.status, sizeof R.st, hipMemcpyDeviceToHost, R.s));
     PLGPU_HIP(hipStreamSynchronize(R.s));
@@ -3746,7 +3755,10 @@ static int gb_finalize(GbRun& R, int32_t naggs, plgpu_column* out_key, plgpu_col
         fp.cap = groups;
         for (int a = 0; a < kMaxAcc; ++a) fp.wide[a] = R.wide_sum[a];
         const int fg = (int)std::min<int64_t>((p.gcap + 2 + 255) / 256, 256 * 16);
-        gb_finalize_kernel<<<fg, 256, 0, s>>>(p, fp);
+        {
+            KtScope kt("gb_finalize_kernel", s);
+            gb_finalize_kernel<<<fg, 256, 0, s>>>(p, fp);
+        }
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) rc = hip_fail(e, "gb_finalize_kernel");
         uint64_t produced = 0, var_out = 0;
@@ -4530,8 +4542,11 @@ static int gb_multi_decode(const MkPack& pk, const plgpu_column* keys, int32_t n
         if (rc || groups == 0) continue;
         if (keys[i].dtype == PLGPU_BOOL) (void)hipMemsetAsync((void*)out_keys[i].values, 0, ((groups + 63) / 64) * 8, s);
         if (nullable) (void)hipMemsetAsync((void*)out_keys[i].validity, 0, ((groups + 63) / 64) * 8, s);
-        mk_unpack_kernel<<<gg, 256, 0, s>>>((const int64_t*)hout.values, nullptr, groups, pk, i, keys[i].dtype,
-                                            (void*)out_keys[i].values, (uint32_t*)out_keys[i].validity);
+        {
+            KtScope kt("mk_unpack_kernel", s);
+            mk_unpack_kernel<<<gg, 256, 0, s>>>((const int64_t*)hout.values, nullptr, groups, pk, i, keys[i].dtype,
+                                                (void*)out_keys[i].values, (uint32_t*)out_keys[i].validity);
+        }
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) rc = hip_fail(e, "mk_unpack_kernel");
     }

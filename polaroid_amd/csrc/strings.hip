@@ -284,7 +284,10 @@ int str_short_codes(const plgpu_column& src, plgpu_column* out, bool* all_short,
         if (e == hipSuccess && n > 0) {
             const int g = (int)std::min<int64_t>((n + kStrThreads - 1) / kStrThreads, (int64_t)num_cus_str() * 16);
             const bool words = ((uintptr_t)src.data & 7) == 0;
-            str_code_kernel<<<g, kStrThreads, 0, s>>>(dev_col(src), n, codes, flag, words, data_end, nullptr);
+            {
+                KtScope kt("str_code_kernel", s);
+                str_code_kernel<<<g, kStrThreads, 0, s>>>(dev_col(src), n, codes, flag, words, data_end, nullptr);
+            }
             e = hipGetLastError();
         }
         if (e == hipSuccess) e = hipMemcpyAsync(&hf, flag, 8, hipMemcpyDeviceToHost, s);

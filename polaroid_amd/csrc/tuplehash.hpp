@@ -304,7 +304,10 @@ inline void mk_pack_launch(const MkKeys& k, const MkPack& pk, int64_t n, uint64_
         if (valid_words) (void)hipMemsetAsync(valid_words, 0xFF, (size_t)((n + 63) / 64) * 8, s);
         const int64_t pairs = (n + 1) / 2;
         const int g = (int)std::max<int64_t>(1, std::min<int64_t>((pairs + 255) / 256, (int64_t)grid));
-        mk_pack_vec_kernel<2><<<g, 256, 0, s>>>(k, pk, n, out, outside);
+        {
+            KtScope kt("mk_pack_vec_kernel", s);
+            mk_pack_vec_kernel<2><<<g, 256, 0, s>>>(k, pk, n, out, outside);
+        }
     } else {
         mk_pack_kernel<<<grid, 256, 0, s>>>(k, pk, n, out, valid_words, outside);
     }
@@ -376,7 +379,10 @@ inline int mk_plan_pack_sampled(const MkKeys& ka, int64_t na, MkPack* pk, hipStr
     for (int j = 0; j < kMaxKeys; ++j) h[3 * j] = ~0ull, h[3 * j + 1] = 0, h[3 * j + 2] = 0;
     hipError_t e = hipMemcpyAsync(st, h, bytes, hipMemcpyHostToDevice, s);
     if (e == hipSuccess && na > 0) {
-        mk_sample_range_kernel<<<16, 256, 0, s>>>(ka, na, 65536, st);
+        {
+            KtScope kt("mk_sample_range_kernel", s);
+            mk_sample_range_kernel<<<16, 256, 0, s>>>(ka, na, 65536, st);
+        }
         e = hipGetLastError();
     }
     if (e == hipSuccess) e = hipMemcpyAsync(h, st, bytes, hipMemcpyDeviceToHost, s);
