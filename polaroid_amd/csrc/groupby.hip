@@ -2713,9 +2713,8 @@ static int resident_per_cu(const void* kern, int threads, size_t lds) {
 }
 
 template <int NACC, int PRED, bool SUMONLY, int LIMBS = 3, bool RUNS = false, bool DERIV = false, bool VAR = false,
-          bool PACK = false>
+          bool PACK = false, int ROWS = 2>
 static hipError_t launch_fast_rows(const Plan& pl, const DevProgram& dp, hipStream_t s) {
-    constexpr int ROWS = 2;
     const void* kern = (const void*)gb_fast_kernel<NACC, PRED, SUMONLY, ROWS, LIMBS, RUNS, false, DERIV, VAR, PACK>;
     static bool attr_set = false;
     if (!attr_set) {
@@ -2723,22 +2722,25 @@ static hipError_t launch_fast_rows(const Plan& pl, const DevProgram& dp, hipStre
         attr_set = true;
     }
     const size_t lds = (SUMONLY && LIMBS == 2) ? (size_t)(2 + 3 * NACC) * (pl.p.lcap + 2) * 8 : pl.lds_bytes;
+    GbParams q = pl.p;
+    q.tiles_per_wg = 0;
+    // the plan's n_full is a multiple of the 2-row tile; a wider tile takes
+    // its own multiple (the masked last tile covers the rest)
+    if (ROWS != 2) q.n_full = (pl.p.n / ((int64_t)kGbThreads * ROWS)) * kGbThreads * ROWS;
     // kGridRounds rounds of the workgroups resident per CU: later rounds'
     // table init / flush overlap earlier rounds' streaming
-    const int64_t need = (pl.p.n_full + kMaxRowsPerWg - 1) / kMaxRowsPerWg;
+    const int64_t need = (q.n_full + kMaxRowsPerWg - 1) / kMaxRowsPerWg;
     int64_t g = (int64_t)num_cus() * resident_per_cu(kern, kGbThreads, lds) * kGridRounds;
     if (g < need) g = need;
-    const int64_t useful = pl.p.n_full / ((int64_t)kGbThreads * ROWS);
+    const int64_t useful = q.n_full / ((int64_t)kGbThreads * ROWS);
     if (g > useful) g = std::max<int64_t>(1, useful);
     const int grid = (int)g;
     pl.launched_grid = grid;
     pl.launched_runs = RUNS;
     pl.launched_var = VAR;
-    GbParams q = pl.p;
-    q.tiles_per_wg = 0;
     if (pl.local) {
         const int64_t tile = (int64_t)kGbThreads * ROWS;
-        const int64_t nall = pl.p.n_full / tile + (pl.p.n > pl.p.n_full ? 1 : 0);
+        const int64_t nall = q.n_full / tile + (pl.p.n > q.n_full ? 1 : 0);
         q.tiles_per_wg = (int32_t)((nall + grid - 1) / grid);
     }
     KtScope kt("gb_fast_kernel", s);
@@ -2749,6 +2751,12 @@ static hipError_t launch_fast_rows(const Plan& pl, const DevProgram& dp, hipStre
 
 template <int NACC, int PRED, bool SUMONLY, bool DERIV, bool PACK = false>
 static hipError_t launch_fast(const Plan& pl, const DevProgram& dp, hipStream_t s) {
+    // A/B (option rows4 bit 1: derived inputs, bit 2: plain columns): 4 rows
+    // per thread for few-column sum-only passes
+    if constexpr (SUMONLY && NACC == 2 && PRED == 1 && !PACK) {
+        if (pl.limbs == 2 && !pl.runs && pl.p.n >= (1 << 20) && (options().rows4 & (DERIV ? 2 : 4)))
+            return launch_fast_rows<NACC, PRED, SUMONLY, 2, false, DERIV, false, false, 4>(pl, dp, s);
+    }
     if (SUMONLY && pl.limbs == 2 && pl.runs)
         return launch_fast_rows<NACC, PRED, SUMONLY, 2, true, DERIV, false, PACK>(pl, dp, s);
     if (SUMONLY && pl.limbs == 2) return launch_fast_rows<NACC, PRED, SUMONLY, 2, false, DERIV, false, PACK>(pl, dp, s);
@@ -2785,6 +2793,9 @@ static bool var_triple(const Plan& pl) {
 template <int PRED>
 static hipError_t launch_fast_var(const Plan& pl, const DevProgram& dp, hipStream_t s) {
     if (!pl.sum_only) return launch_fast_rows<3, PRED, false, 3, false, false, true>(pl, dp, s);
+    // A/B (option rows4 bit 0): 4 rows per thread (twice the bytes in flight)
+    if (pl.limbs == 2 && pl.p.n >= (1 << 20) && (options().rows4 & 1))
+        return launch_fast_rows<3, PRED, true, 2, false, false, true, false, 4>(pl, dp, s);
     if (pl.limbs == 2) return launch_fast_rows<3, PRED, true, 2, false, false, true>(pl, dp, s);
     return launch_fast_rows<3, PRED, true, 3, false, false, true>(pl, dp, s);
 }
