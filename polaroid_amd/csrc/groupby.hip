@@ -1281,6 +1281,10 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
         kpsh[i] = on ? p.kp.shift[i] : 0;
         kpdt[i] = dt;
     }
+    // identity plan: one non-String key, base 0, 64 bits (gb_multi_impl's
+    // narrow single key)
+    const bool kpid = PACK && p.kp.n == 1 && kpdt[0] != PLGPU_STR && p.kp.bits[0] >= 64 && p.kp.base[0] == 0 &&
+                      p.kp.shift[0] == 0;
     constexpr uint32_t VM = (1u << NACC) - 1u;
     // RACC (partition buffers, sum-only, 2 limbs): each lane keeps KR
     // register accumulators {slot, len, limbs} and adds a row whose group
@@ -1428,10 +1432,19 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
                                          kout[j]);
             }
         }
+        if (PACK && kpid) {
+            // one 4-byte (or 8-byte) key as itself: its sign- or zero-extended
+            // value is the code (no range to check)
+#pragma unroll
+            for (int j = 0; j < ROWS; ++j) {
+                kout[j] = false;
+                cur.key[j] = ((cur.kr[0][j] & kpm[0]) ^ kpx[0]) - kpx[0];
+            }
+        }
 #pragma unroll
         for (int j = 0; j < ROWS; ++j) {
-            if (!kstr) kout[j] = false;
-            if (PACK && !kstr) {
+            if (!kstr && !kpid) kout[j] = false;
+            if (PACK && !kstr && !kpid) {
                 // the packed code of row j (mk_plan_pack's layout)
                 uint64_t code = 0;
                 bool out = false;
@@ -3218,6 +3231,9 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
     if (hll < 0 && R.st[ST_DISTINCT] >= (uint64_t)kPlanSetSlots / 2 && n > 4 * (int64_t)kPlanSamples) {
         if (p.kp.n > 0) {
             // many groups: not the fused single-table kernel's case
+            if (options().debug)
+                fprintf(stderr, "[plgpu] key pack fallback: %llu distinct of %llu sampled\n",
+                        (unsigned long long)R.st[ST_DISTINCT], (unsigned long long)R.st[ST_SAMPLED]);
             R.kp_fallback = true;
             return PLGPU_OK;
         }
@@ -3368,6 +3384,9 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
     if (R.part) p.n_full = 0, p.row_begin = 0;
     if (p.kp.n > 0 && (p.n_full == 0 || R.part || gb_has_fused(R))) {
         // the packed key lives only in the fused kernel's registers
+        if (options().debug)
+            fprintf(stderr, "[plgpu] key pack fallback: n_full=%lld part=%d fused=%d use_lds=%d pred=%d\n",
+                    (long long)p.n_full, (int)R.part, (int)gb_has_fused(R), (int)pl.use_lds, R.pred);
         R.kp_fallback = true;
         return PLGPU_OK;
     }
@@ -4581,6 +4600,9 @@ static int gb_multi_packed(const MkKeys& mk, MkPack pk, int64_t n, const plgpu_c
     hipStream_t s = as_stream(stream);
     if (repack) *repack = false;
     const KeyPack kp = kp_from_plan(mk, pk, n);
+    if (options().debug)
+        fprintf(stderr, "[plgpu] gb_multi_packed: n=%lld keys=%d fused key pack=%d checked=%d\n", (long long)n, mk.n,
+                kp.n, (int)checked);
     if (kp.n > 0) {
         // fused key packing: the fused kernel forms each row's code from the
         // key columns it loads (no code column written or read).  Off the
@@ -4774,6 +4796,20 @@ static int gb_multi_impl(const plgpu_column* keys, int32_t nkeys, const plgpu_co
         for (int i = 0; i < nkeys; ++i)
             if (keys[i].dtype == PLGPU_STR && ck[i].dtype == PLGPU_I64) str_codes_free(&ck[i], s);
         if (rc || (any_str && short_all)) return rc;
+    }
+    if (nkeys == 1 && (keys[0].dtype == PLGPU_I32 || keys[0].dtype == PLGPU_U32) && keys[0].validity == nullptr &&
+        n >= (int64_t(1) << 20) && options().fuse_keys) {
+        // one null-free 4-byte key (dates, Categorical codes): its extended
+        // value is the code (identity plan: no sample, no range check); the
+        // fused kernel reads the 4-byte column itself
+        MkPack pk;
+        std::memset(&pk, 0, sizeof pk);
+        pk.n = 1;
+        pk.ok = 1;
+        pk.bits[0] = 64;
+        bool repack = false;
+        return gb_multi_packed(mk, pk, n, keys, nkeys, cols, ncols, deriv, program, n_instr, aggs, naggs,
+                               maintain_order, out_keys, out_aggs, info, stream, true, &repack);
     }
     const int hg = (int)std::min<int64_t>((n + 255) / 256, (int64_t)num_cus() * 16);
     {

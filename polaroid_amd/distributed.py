@@ -47,6 +47,10 @@ def _device_for(group) -> Any:
 
     if dist.get_backend(group) == "nccl":
         return torch.device("cuda", torch.cuda.current_device())
+    # gloo on a process that owns a GPU (ranks sharing one device in a test):
+    # device buffers, collectives staged through host memory (_staged)
+    if torch.cuda.is_available() and torch.cuda.is_initialized():
+        return torch.device("cuda", torch.cuda.current_device())
     return torch.device("cpu")
 
 
@@ -582,7 +586,7 @@ def group_by_agg(df, key: str, aggs: Sequence[Expr], predicate: Expr | None = No
         raise N.InvalidOperationError("torch.distributed is not initialised")
     device = _device_for(group)
     if device.type != "cuda":
-        raise N.InvalidOperationError("the GPU group-by needs the nccl (RCCL) backend")
+        raise N.InvalidOperationError("the GPU group-by needs a process that owns a GPU (nccl / RCCL backend)")
     try:
         return _group_by_agg_states(df, key, aggs, predicate, group, info)
     except _RowShuffle as why:
@@ -1180,7 +1184,7 @@ def join(left, right, on: str | Sequence[str] | None = None, how: str = "inner",
         raise N.InvalidOperationError("torch.distributed is not initialised")
     device = _device_for(group)
     if device.type != "cuda":
-        raise N.InvalidOperationError("the GPU join needs the nccl (RCCL) backend")
+        raise N.InvalidOperationError("the GPU join needs a process that owns a GPU (nccl / RCCL backend)")
     if on is not None:
         left_on = right_on = on
     if left_on is None or right_on is None:

@@ -483,8 +483,8 @@ class Series:
     def to_arrow(self):
         import pyarrow as pa
 
-        if self._c is None and self._cat_codes() is not None:
-            # Categorical, strings never gathered: its codes and dictionary
+        if self._cat_codes() is not None:
+            # Categorical (gathered strings or not): its codes and dictionary
             # as an Arrow dictionary array (what polars exports it as)
             dictionary, codes = self._cat
             return pa.DictionaryArray.from_arrays(codes.to_arrow(), dictionary.to_arrow())
@@ -1375,8 +1375,15 @@ def _gb_lower(df: DataFrame, key: str | tuple | None, aggs: list[Expr], pred: Ex
         if k not in df._cols:
             raise N.ComputeError(f'unable to find column "{k}"')
     # len() needs some aggregatable column for its accumulator slot (it only
-    # reads the group's row count): the first non-Boolean key, else any column
-    len_col = next((k for k in keys if df._cols[k].dtype not in (Boolean, String)), None)
+    # reads the group's row count): a column another aggregation already reads
+    # (one accumulator, no extra column pass), else an 8-byte key column (the
+    # fused kernel's loads), else the first non-Boolean key, else any column
+    plain = [b.args[0].value for b in (e.args[0] if e.kind == "alias" else e for e in aggs)
+             if b.kind == "agg" and b.args and b.args[0].kind == "col" and b.args[0].value in df._cols
+             and df._cols[b.args[0].value].dtype not in (Boolean, String)]
+    len_col = plain[0] if plain else next((k for k in keys if df._cols[k].dtype in (Int64, UInt64, Float64)), None)
+    if len_col is None:
+        len_col = next((k for k in keys if df._cols[k].dtype not in (Boolean, String)), None)
     if len_col is None:
         len_col = next((c for c in df.columns if df._cols[c].dtype not in (Boolean, String)), None)
     if len_col is None:

@@ -47,11 +47,13 @@ def test_fused_two_keys_vs_oracle(gpu, layout, aggs, pred):
     oracle: time-ordered days (range-local table) and random tuples."""
     rng = np.random.default_rng(len(layout) + 3 * len(aggs) + (pred is None))
     # day-ordered: 25,000 groups, ~100 per row range (the range-local table,
-    # which needs >= 2^22 rows); random: 800 groups (one LDS table)
+    # which needs >= 2^22 rows); random: 120 groups (one LDS table: the
+    # mixed aggregations' table layout holds 256 slots at load 1/2)
     n = 4_500_001 if layout == "day_ordered" else N
-    sym = (rng.integers(0, 100, n) * 7919 + 1_000_000).astype(np.int64)
+    nsym = 100 if layout == "day_ordered" else 30
+    sym = (rng.integers(0, nsym, n) * 7919 + 1_000_000).astype(np.int64)
     day = ((np.arange(n) * 250) // n).astype(np.int32) if layout == "day_ordered" else \
-        rng.integers(0, 8, n).astype(np.int32)
+        rng.integers(0, 4, n).astype(np.int32)
     cols = _dense(rng, n)
     ag = [("sum", "a"), ("sum", "d")] if aggs == "sums" else \
         [("sum", "a"), ("min", "d"), ("max", "b"), ("count", "d"), ("len", "a"), ("mean", "d")]
@@ -78,7 +80,7 @@ def test_fused_matches_code_column_path(gpu, plgpu_option):
     """fuse_keys = 0 (the packed code column) gives the same frame."""
     rng = np.random.default_rng(5)
     sym = rng.integers(0, 100, N).astype(np.int64)
-    day = rng.integers(0, 250, N).astype(np.int32)
+    day = rng.integers(0, 5, N).astype(np.int32)  # 500 groups: one LDS table
     a = rng.uniform(10, 500, N)
     df = pl.DataFrame({"sym": pl.Series.from_numpy("sym", sym), "day": pl.Series.from_numpy("day", day),
                        "a": pl.Series.from_numpy("a", a)})
@@ -99,9 +101,9 @@ def test_fused_outlier_repacks(gpu):
     is caught in the fused kernel (ST_KPACK): the group-by repacks with the
     exact ranges and runs fused again, exact."""
     rng = np.random.default_rng(9)
-    k1 = (rng.integers(0, 1000, N) * 3 - 500).astype(np.int64)
+    k1 = (rng.integers(0, 40, N) * 3 - 500).astype(np.int64)
     k1[N // 2 + 7] = 1 << 40
-    k2 = rng.integers(0, 50, N).astype(np.int32)
+    k2 = rng.integers(0, 10, N).astype(np.int32)  # ~400 groups: one LDS table
     cols = _dense(rng, N)
     info = {}
     _check({"k1": (k1, None), "k2": (k2, None)}, cols, [("sum", "a"), ("len", "b")], False, info=info)
