@@ -1016,7 +1016,7 @@ __global__ __launch_bounds__(kPartThreads) void gb_part_scatter_kernel(GbParams 
 // PACK: the key is formed from up to kKpFast packed key columns (KeyPack),
 // whose raw words the tile holds until its rows are consumed.
 constexpr int kKpFast = 2;
-template <int NACC, int ROWS, bool DERIV = false, bool PACK = false>
+template <int NACC, int ROWS, bool DERIV = false, int PACK = 0>
 struct FastTile {
     uint64_t key[ROWS];
     uint64_t kr[PACK ? kKpFast : 1][ROWS];
@@ -1043,7 +1043,7 @@ __device__ __forceinline__ u64x2_t ld16(const uint64_t* p) {
 // The rows after the last full tile (fewer than one tile): one more, masked
 // tile of guarded single-row loads (rows >= n read as 0 and are not
 // selected), so the fused kernel covers every row in one launch.
-template <int NACC, int PRED, int ROWS, bool DERIV, bool PACK>
+template <int NACC, int PRED, int ROWS, bool DERIV, int PACK>
 __device__ __forceinline__ void fast_load_tail(const GbParams& p, int64_t t, FastTile<NACC, ROWS, DERIV, PACK>& x) {
     const int T = blockDim.x;
     const uint64_t* kp = (const uint64_t*)p.key.values + p.key.offset;
@@ -1051,12 +1051,12 @@ __device__ __forceinline__ void fast_load_tail(const GbParams& p, int64_t t, Fas
     for (int j = 0; j < ROWS; ++j) {
         const int64_t r = fast_row(t, T, ROWS, j);
         const bool in = r < p.n;
-        if (PACK && p.kp.c[0].dtype == PLGPU_STR) {
+        if (PACK == 2) {
             // String key: kr[0][j] = offset of row r, kr[1][j] = of row r + 1
             const int64_t* o = (const int64_t*)p.kp.c[0].values + p.kp.c[0].offset;
             x.kr[0][j] = in ? (uint64_t)o[r] : 0ull;
             x.kr[1][j] = in ? (uint64_t)o[r + 1] : 0ull;
-        } else if (PACK) {
+        } else if (PACK == 1) {
 #pragma unroll
             for (int i = 0; i < kKpFast; ++i) x.kr[i][j] = in && i < p.kp.n ? dev_load(p.kp.c[i], r) : 0ull;
         } else {
@@ -1077,7 +1077,7 @@ __device__ __forceinline__ void fast_load_tail(const GbParams& p, int64_t t, Fas
 // clamped to it (the partitioned buffers end a pair after the last row).
 typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 
-template <int NACC, int PRED, int ROWS, bool NT, bool DERIV, bool PACK>
+template <int NACC, int PRED, int ROWS, bool NT, bool DERIV, int PACK>
 __device__ __forceinline__ void fast_load(const GbParams& p, int64_t t, FastTile<NACC, ROWS, DERIV, PACK>& x,
                                           int64_t rbase = 0, int64_t rmax = -1) {
     const int T = blockDim.x;
@@ -1086,7 +1086,7 @@ __device__ __forceinline__ void fast_load(const GbParams& p, int64_t t, FastTile
     for (int q = 0; q < ROWS / 2; ++q) {
         int64_t r = rbase + fast_row(t, T, ROWS, 2 * q);
         if (rmax >= 0) r = r < rmax ? r : rmax;
-        if (PACK && p.kp.c[0].dtype == PLGPU_STR) {
+        if (PACK == 2) {
             // String key: the pair's offsets (16 B) and the next row's (8 B):
             // kr[0][j] = start, kr[1][j] = end of row 2q + j
             const int64_t* o = (const int64_t*)p.kp.c[0].values + p.kp.c[0].offset + r;
@@ -1096,7 +1096,7 @@ __device__ __forceinline__ void fast_load(const GbParams& p, int64_t t, FastTile
             x.kr[0][2 * q + 1] = a.y;
             x.kr[1][2 * q] = a.y;
             x.kr[1][2 * q + 1] = e;
-        } else if (PACK) {
+        } else if (PACK == 1) {
             // each packed key column: one 16-byte (Int64) or 8-byte (Int32 /
             // UInt32) load per row pair, kept raw until the rows are consumed
 #pragma unroll
@@ -1151,7 +1151,7 @@ __device__ __forceinline__ void fast_load(const GbParams& p, int64_t t, FastTile
 // DERIV: fill the operand registers whose column another acc loaded
 // (v_from / w_from, uniform), once the tile's loads are being consumed --
 // not at prefetch time, where the copy would wait for the loads.
-template <int NACC, int ROWS, bool DERIV, bool PACK>
+template <int NACC, int ROWS, bool DERIV, int PACK>
 __device__ __forceinline__ void fast_share(const int32_t (&vf)[NACC > 0 ? NACC : 1],
                                            const int32_t (&wf)[NACC > 0 ? NACC : 1],
                                            FastTile<NACC, ROWS, DERIV, PACK>& x) {
@@ -1193,7 +1193,7 @@ __device__ __forceinline__ void fast_share(const int32_t (&vf)[NACC > 0 ? NACC :
 // PACK: the key is the fused packed code of p.kp's (at most kKpFast) key
 // columns (KeyPack), formed as each tile's rows are consumed.
 template <int NACC, int PRED, bool SUMONLY, int ROWS, int LIMBS = 3, bool RUNS = false, bool PART = false,
-          bool DERIV = false, bool VAR = false, bool PACK = false>
+          bool DERIV = false, bool VAR = false, int PACK = 0>
 __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProgram prog) {
     static_assert(!PACK || !PART, "PACK: the single-table kernel");
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
@@ -1283,7 +1283,7 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
     }
     // identity plan: one non-String key, base 0, 64 bits (gb_multi_impl's
     // narrow single key)
-    const bool kpid = PACK && p.kp.n == 1 && kpdt[0] != PLGPU_STR && p.kp.bits[0] >= 64 && p.kp.base[0] == 0 &&
+    const bool kpid = PACK == 1 && p.kp.n == 1 && p.kp.bits[0] >= 64 && p.kp.base[0] == 0 &&
                       p.kp.shift[0] == 0;
     constexpr uint32_t VM = (1u << NACC) - 1u;
     // RACC (partition buffers, sum-only, 2 limbs): each lane keeps KR
@@ -1420,7 +1420,7 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
     for (; t < nall; t += tstep) {
         if constexpr (!VAR) fast_share<NACC, ROWS, DERIV, PACK>(vf0, wf0, cur);
         bool kout[ROWS];
-        const bool kstr = PACK && kpdt[0] == PLGPU_STR;
+        constexpr bool kstr = PACK == 2;
         if (kstr) {
             // String key: each row's short-string code from its offsets and
             // one or two data words (dependent loads, issued for the tile's
@@ -1432,7 +1432,7 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
                                          kout[j]);
             }
         }
-        if (PACK && kpid) {
+        if (PACK == 1 && kpid) {
             // one 4-byte (or 8-byte) key as itself: its sign- or zero-extended
             // value is the code (no range to check)
 #pragma unroll
@@ -1444,7 +1444,7 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
 #pragma unroll
         for (int j = 0; j < ROWS; ++j) {
             if (!kstr && !kpid) kout[j] = false;
-            if (PACK && !kstr && !kpid) {
+            if (PACK == 1 && !kpid) {
                 // the packed code of row j (mk_plan_pack's layout)
                 uint64_t code = 0;
                 bool out = false;
@@ -2726,7 +2726,7 @@ static int resident_per_cu(const void* kern, int threads, size_t lds) {
 }
 
 template <int NACC, int PRED, bool SUMONLY, int LIMBS = 3, bool RUNS = false, bool DERIV = false, bool VAR = false,
-          bool PACK = false, int ROWS = 2>
+          int PACK = 0, int ROWS = 2>
 static hipError_t launch_fast_rows(const Plan& pl, const DevProgram& dp, hipStream_t s) {
     const void* kern = (const void*)gb_fast_kernel<NACC, PRED, SUMONLY, ROWS, LIMBS, RUNS, false, DERIV, VAR, PACK>;
     static bool attr_set = false;
@@ -2762,7 +2762,7 @@ static hipError_t launch_fast_rows(const Plan& pl, const DevProgram& dp, hipStre
     return hipGetLastError();
 }
 
-template <int NACC, int PRED, bool SUMONLY, bool DERIV, bool PACK = false>
+template <int NACC, int PRED, bool SUMONLY, bool DERIV, int PACK = 0>
 static hipError_t launch_fast(const Plan& pl, const DevProgram& dp, hipStream_t s) {
     // A/B (option rows4 bit 1: derived inputs, bit 2: plain columns): 4 rows
     // per thread for few-column sum-only passes
@@ -2778,13 +2778,19 @@ static hipError_t launch_fast(const Plan& pl, const DevProgram& dp, hipStream_t 
     return launch_fast_rows<NACC, PRED, SUMONLY, 3, false, DERIV, false, PACK>(pl, dp, s);
 }
 
-template <int NACC, bool DERIV, bool PACK = false>
+template <int NACC, bool DERIV, int PACK = 0>
 static hipError_t launch_fast_nacc(const Plan& pl, const DevProgram& dp, int pred, hipStream_t s) {
+    if constexpr (PACK == 2) {
+        // String key codes: sum-only layouts (gb_plan falls back otherwise)
+        if (!pl.sum_only) return hipErrorInvalidValue;
+        return pred == 0 ? launch_fast<NACC, 0, true, DERIV, 2>(pl, dp, s) : launch_fast<NACC, 1, true, DERIV, 2>(pl, dp, s);
+    } else {
     if (pl.sum_only)
         return pred == 0 ? launch_fast<NACC, 0, true, DERIV, PACK>(pl, dp, s)
                          : launch_fast<NACC, 1, true, DERIV, PACK>(pl, dp, s);
     return pred == 0 ? launch_fast<NACC, 0, false, DERIV, PACK>(pl, dp, s)
                      : launch_fast<NACC, 1, false, DERIV, PACK>(pl, dp, s);
+    }
 }
 
 // The fused variance's triple (x, x * x, its error: three sums of one
@@ -2820,14 +2826,25 @@ static hipError_t launch_fast_dispatch(const Plan& pl, const DevProgram& dp, int
         // fused key packing: plain (non-derived) inputs only (gb_plan
         // guarantees it, falling back to a code column otherwise)
         if (dv || pl.p.kp.n > kKpFast) return hipErrorInvalidValue;
+        if (pl.p.kp.c[0].dtype == PLGPU_STR) {
+            switch (pl.p.nacc) {
+            case 0: return hipErrorInvalidValue;
+            case 1: return launch_fast_nacc<1, false, 2>(pl, dp, pred, s);
+            case 2: return launch_fast_nacc<2, false, 2>(pl, dp, pred, s);
+            case 3: return launch_fast_nacc<3, false, 2>(pl, dp, pred, s);
+            case 4: return launch_fast_nacc<4, false, 2>(pl, dp, pred, s);
+            case 5: return launch_fast_nacc<5, false, 2>(pl, dp, pred, s);
+            default: return launch_fast_nacc<6, false, 2>(pl, dp, pred, s);
+            }
+        }
         switch (pl.p.nacc) {
-        case 0: return launch_fast_nacc<0, false, true>(pl, dp, pred, s);
-        case 1: return launch_fast_nacc<1, false, true>(pl, dp, pred, s);
-        case 2: return launch_fast_nacc<2, false, true>(pl, dp, pred, s);
-        case 3: return launch_fast_nacc<3, false, true>(pl, dp, pred, s);
-        case 4: return launch_fast_nacc<4, false, true>(pl, dp, pred, s);
-        case 5: return launch_fast_nacc<5, false, true>(pl, dp, pred, s);
-        default: return launch_fast_nacc<6, false, true>(pl, dp, pred, s);
+        case 0: return launch_fast_nacc<0, false, 1>(pl, dp, pred, s);
+        case 1: return launch_fast_nacc<1, false, 1>(pl, dp, pred, s);
+        case 2: return launch_fast_nacc<2, false, 1>(pl, dp, pred, s);
+        case 3: return launch_fast_nacc<3, false, 1>(pl, dp, pred, s);
+        case 4: return launch_fast_nacc<4, false, 1>(pl, dp, pred, s);
+        case 5: return launch_fast_nacc<5, false, 1>(pl, dp, pred, s);
+        default: return launch_fast_nacc<6, false, 1>(pl, dp, pred, s);
         }
     }
     if (dv && var_triple(pl) && !pl.runs)
@@ -3382,7 +3399,8 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
         }
     }
     if (R.part) p.n_full = 0, p.row_begin = 0;
-    if (p.kp.n > 0 && (p.n_full == 0 || R.part || gb_has_fused(R))) {
+    if (p.kp.n > 0 && (p.n_full == 0 || R.part || gb_has_fused(R) ||
+                       (p.kp.c[0].dtype == PLGPU_STR && (!pl.sum_only || p.nacc == 0)))) {
         // the packed key lives only in the fused kernel's registers
         if (options().debug)
             fprintf(stderr, "[plgpu] key pack fallback: n_full=%lld part=%d fused=%d use_lds=%d pred=%d\n",
