@@ -127,6 +127,16 @@ struct KeyPack {
     int32_t _pad;
     DevCol c[kKpMax];
     uint64_t base[kKpMax];  // minv[i] - nul[i] (wrapping): field i = v - base[i]
+    // field i fits iff v - base[i] (wrapping) <= span[i] = min(2^bits - 1,
+    // 2^64 - 1 - ord(base)), ord(x) = x ^ 2^63: one unsigned compare that is
+    // false for every v < base too (kp_span)
+    uint64_t span[kKpMax];
+    // 4-byte columns whose base lies in the column type's range: the same
+    // test on 32-bit ordered values (ord32(v) - b32 <= span32, ord32 = v ^ x32)
+    uint32_t b32[kKpMax];
+    uint32_t span32[kKpMax];
+    uint32_t x32[kKpMax];
+    int32_t mode[kKpMax];   // 0: 8-byte column, 1: 4-byte on 32-bit values, 2: 4-byte widened to 64 bits
     int32_t shift[kKpMax];
     int32_t bits[kKpMax];
     int64_t data_end;       // String key: bytes in the data buffer (bounds the word loads)
@@ -252,7 +262,7 @@ __device__ __forceinline__ uint64_t kp_field(const KeyPack& k, int i, uint64_t r
     const uint64_t v = dt == PLGPU_I32 ? (uint64_t)(int64_t)(int32_t)(uint32_t)raw
                                        : (dt == PLGPU_U32 ? (uint64_t)(uint32_t)raw : raw);
     const uint64_t f = v - k.base[i];
-    bad |= k.bits[i] < 64 && (f >> k.bits[i]) != 0;
+    bad |= f > k.span[i];
     return f << k.shift[i];
 }
 
@@ -1264,22 +1274,20 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
         else fast_load_tail<NL, PRED, ROWS, DERIV, PACK>(p, tt, x);
     };
     // PACK: the plan's fields as uniform constants, hoisted.  Field i of a
-    // raw word w is ((w & kpm) ^ kpx) - kpc: kpm keeps a 4-byte value's low
-    // half, kpx = 2^31 sign-extends an Int32 ((v ^ 2^31) - 2^31), kpc =
-    // kpx + base; a field fits iff (field & kphm) == 0.
-    uint64_t kpm[kKpFast], kpx[kKpFast], kpc[kKpFast], kphm[kKpFast];
-    int32_t kpsh[kKpFast], kpdt[kKpFast];
+    // raw word w: an 8-byte column's w - base (mode 0); a 4-byte column's
+    // (w ^ x32) - b32 on 32 bits (mode 1), or widened, ((w & kpm) ^ kpx) -
+    // kpc with kpx = 2^31 sign-extending an Int32 and kpc = kpx + base (mode
+    // 2).  It fits iff it is <= its span (KeyPack::span / span32).
+    uint64_t kpm[kKpFast], kpx[kKpFast], kpc[kKpFast];
+    int32_t kpsh[kKpFast];
 #pragma unroll
     for (int i = 0; i < kKpFast; ++i) {
         const bool on = PACK && i < p.kp.n;
         const int32_t dt = on ? p.kp.c[i].dtype : PLGPU_I64;
-        const int32_t bits = on ? p.kp.bits[i] : 64;
         kpm[i] = (dt == PLGPU_I32 || dt == PLGPU_U32) ? 0xFFFFFFFFull : ~0ull;
         kpx[i] = dt == PLGPU_I32 ? 0x80000000ull : 0ull;
         kpc[i] = kpx[i] + (on ? p.kp.base[i] : 0ull);
-        kphm[i] = bits >= 64 ? 0ull : ~((1ull << bits) - 1);
         kpsh[i] = on ? p.kp.shift[i] : 0;
-        kpdt[i] = dt;
     }
     // identity plan: one non-String key, base 0, 64 bits (gb_multi_impl's
     // narrow single key)
@@ -1443,19 +1451,39 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
         }
 #pragma unroll
         for (int j = 0; j < ROWS; ++j) {
-            if (!kstr && !kpid) kout[j] = false;
-            if (PACK == 1 && !kpid) {
-                // the packed code of row j (mk_plan_pack's layout)
-                uint64_t code = 0;
-                bool out = false;
+            if (!kstr) kout[j] = false;
+        }
+        if (PACK == 1 && !kpid) {
+            // the packed codes (mk_plan_pack's layout), field by field; each
+            // field's form is uniform, so one branch per field and tile
 #pragma unroll
-                for (int i = 0; i < kKpFast; ++i) {
-                    const uint64_t f = ((cur.kr[i][j] & kpm[i]) ^ kpx[i]) - kpc[i];
-                    out |= (f & kphm[i]) != 0;
-                    code |= f << kpsh[i];
+            for (int j = 0; j < ROWS; ++j) cur.key[j] = 0;
+#pragma unroll
+            for (int i = 0; i < kKpFast; ++i) {
+                if (i >= p.kp.n) continue;
+                const int md = p.kp.mode[i];
+                if (md == 0) {
+#pragma unroll
+                    for (int j = 0; j < ROWS; ++j) {
+                        const uint64_t f = cur.kr[i][j] - kpc[i];
+                        kout[j] |= f > p.kp.span[i];
+                        cur.key[j] |= f << kpsh[i];
+                    }
+                } else if (md == 1) {
+#pragma unroll
+                    for (int j = 0; j < ROWS; ++j) {
+                        const uint32_t f = ((uint32_t)cur.kr[i][j] ^ p.kp.x32[i]) - p.kp.b32[i];
+                        kout[j] |= f > p.kp.span32[i];
+                        cur.key[j] |= (uint64_t)f << kpsh[i];
+                    }
+                } else {
+#pragma unroll
+                    for (int j = 0; j < ROWS; ++j) {
+                        const uint64_t f = ((cur.kr[i][j] & kpm[i]) ^ kpx[i]) - kpc[i];
+                        kout[j] |= f > p.kp.span[i];
+                        cur.key[j] |= f << kpsh[i];
+                    }
                 }
-                kout[j] = out;
-                cur.key[j] = code;
             }
         }
         // ---- predicate + batched LDS probes of the tile's rows
@@ -2764,12 +2792,6 @@ static hipError_t launch_fast_rows(const Plan& pl, const DevProgram& dp, hipStre
 
 template <int NACC, int PRED, bool SUMONLY, bool DERIV, int PACK = 0>
 static hipError_t launch_fast(const Plan& pl, const DevProgram& dp, hipStream_t s) {
-    // A/B (option rows4 bit 1: derived inputs, bit 2: plain columns): 4 rows
-    // per thread for few-column sum-only passes
-    if constexpr (SUMONLY && NACC == 2 && PRED == 1 && !PACK) {
-        if (pl.limbs == 2 && !pl.runs && pl.p.n >= (1 << 20) && (options().rows4 & (DERIV ? 2 : 4)))
-            return launch_fast_rows<NACC, PRED, SUMONLY, 2, false, DERIV, false, false, 4>(pl, dp, s);
-    }
     if (SUMONLY && pl.limbs == 2 && pl.runs)
         return launch_fast_rows<NACC, PRED, SUMONLY, 2, true, DERIV, false, PACK>(pl, dp, s);
     if (SUMONLY && pl.limbs == 2) return launch_fast_rows<NACC, PRED, SUMONLY, 2, false, DERIV, false, PACK>(pl, dp, s);
@@ -2812,9 +2834,6 @@ static bool var_triple(const Plan& pl) {
 template <int PRED>
 static hipError_t launch_fast_var(const Plan& pl, const DevProgram& dp, hipStream_t s) {
     if (!pl.sum_only) return launch_fast_rows<3, PRED, false, 3, false, false, true>(pl, dp, s);
-    // A/B (option rows4 bit 0): 4 rows per thread (twice the bytes in flight)
-    if (pl.limbs == 2 && pl.p.n >= (1 << 20) && (options().rows4 & 1))
-        return launch_fast_rows<3, PRED, true, 2, false, false, true, false, 4>(pl, dp, s);
     if (pl.limbs == 2) return launch_fast_rows<3, PRED, true, 2, false, false, true>(pl, dp, s);
     return launch_fast_rows<3, PRED, true, 3, false, false, true>(pl, dp, s);
 }
@@ -4554,6 +4573,28 @@ PLGPU_API int plgpu_gb_merge_sources(const void* records, int32_t n_sources, con
 // `checked`: pk comes from sampled ranges (mk_plan_pack_sampled); a row
 // outside them sets *repack (nothing else done) and the caller repacks
 // with the exact ranges.
+// Field i's fit test (KeyPack::span): v - base <= min(2^bits - 1, 2^64 - 1 -
+// ord(base)) holds exactly for base <= v < base + 2^bits (signed): a v below
+// base wraps to more than 2^64 - 1 - ord(base).  Same on 32 bits for a 4-byte
+// column whose base is a value of its type.
+static void kp_span(KeyPack& k, int i) {
+    const int bits = k.bits[i];
+    const uint64_t mask = bits >= 64 ? ~0ull : (1ull << bits) - 1;
+    const uint64_t ordb = k.base[i] ^ 0x8000000000000000ull;
+    k.span[i] = std::min<uint64_t>(mask, ~0ull - ordb);
+    const int32_t dt = k.c[i].dtype;
+    const int64_t b = (int64_t)k.base[i];
+    k.mode[i] = 0;
+    if (dt == PLGPU_I32 || dt == PLGPU_U32) {
+        const bool in_range = dt == PLGPU_I32 ? (b >= INT32_MIN && b <= INT32_MAX) : (b >= 0 && b <= (int64_t)UINT32_MAX);
+        k.mode[i] = in_range ? 1 : 2;
+        k.x32[i] = dt == PLGPU_I32 ? 0x80000000u : 0u;
+        k.b32[i] = (uint32_t)b ^ k.x32[i];
+        const uint32_t m32 = bits >= 32 ? 0xFFFFFFFFu : (1u << bits) - 1;
+        k.span32[i] = std::min<uint32_t>(m32, 0xFFFFFFFFu - k.b32[i]);
+    }
+}
+
 // The packing plan as the fused kernel's KeyPack, or n = 0 when the key
 // columns do not qualify (more than kKpFast, nullable, not Int64 / Int32 /
 // UInt32, misaligned, or a small input).
@@ -4573,6 +4614,7 @@ static KeyPack kp_from_plan(const MkKeys& mk, const MkPack& pk, int64_t n) {
         k.base[i] = (uint64_t)pk.minv[i] - (pk.nullable[i] ? 1u : 0u);
         k.shift[i] = pk.shift[i];
         k.bits[i] = pk.bits[i];
+        kp_span(k, i);
     }
     k.n = mk.n;
     return k;
@@ -4716,6 +4758,7 @@ static int gb_str_fused(const plgpu_column& key, const plgpu_column* cols, int32
     kp.n = 1;
     kp.c[0] = dev_col(key);
     kp.bits[0] = 64;
+    kp.span[0] = ~0ull;
     kp.data_end = data_end;
     plgpu_column ck;
     std::memset(&ck, 0, sizeof ck);

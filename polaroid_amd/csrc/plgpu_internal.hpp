@@ -42,7 +42,6 @@ struct Options {
     int local = -1;      // -1: the plan picks the range-local kernel; 0 keeps it off (tests)
     int ktime = 0;       // 1: time the named kernels with HIP events (plgpu_ktime_read)
     int fuse_keys = 1;   // 0: packed multi-key codes go through a code column (tests / A-B)
-    int rows4 = 0;       // A/B: 4 rows per thread in few-column fused passes (bit 0 var, 1 derived, 2 plain)
 };
 Options& options();
 

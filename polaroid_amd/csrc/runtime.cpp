@@ -53,7 +53,6 @@ static Options read_env_options() {
     o.local = get("PLGPU_LOCAL", -1);
     o.ktime = get("PLGPU_KTIME", 0);
     o.fuse_keys = get("PLGPU_FUSE_KEYS", 1);
-    o.rows4 = get("PLGPU_ROWS4", 0);
     return o;
 }
 
@@ -771,7 +770,6 @@ PLGPU_API int plgpu_set_option(const char* name, int64_t value) {
     else if (!strcmp(name, "local")) f = &o.local;
     else if (!strcmp(name, "ktime")) f = &o.ktime;
     else if (!strcmp(name, "fuse_keys")) f = &o.fuse_keys;
-    else if (!strcmp(name, "rows4")) f = &o.rows4;
     if (f == nullptr) return fail(PLGPU_ERR_INVALID, std::string("unknown option ") + name);
     *f = (int)value;
     return PLGPU_OK;
@@ -787,7 +785,6 @@ PLGPU_API int plgpu_get_option(const char* name, int64_t* out) {
     else if (!strcmp(name, "local")) *out = o.local;
     else if (!strcmp(name, "ktime")) *out = o.ktime;
     else if (!strcmp(name, "fuse_keys")) *out = o.fuse_keys;
-    else if (!strcmp(name, "rows4")) *out = o.rows4;
     else return fail(PLGPU_ERR_INVALID, std::string("unknown option ") + name);
     return PLGPU_OK;
 }

@@ -195,6 +195,15 @@ __global__ __launch_bounds__(256) void mk_sample_range_kernel(MkKeys k, int64_t 
 // nulls_equal).  `outside` (optional, a plan from sampled ranges): set when
 // some row's field does not fit its bits (the code would be wrong; the
 // caller repacks with exact ranges).
+// Largest field value of key i that is a packed value: v - base <= span
+// holds exactly for base <= v < base + 2^bits (a v below base wraps past
+// 2^64 - 1 - ord(base), ord(x) = x ^ 2^63), base = minv - nullable.
+__device__ __forceinline__ uint64_t mk_span(const MkPack& pk, int i) {
+    const uint64_t mask = pk.bits[i] >= 64 ? ~0ull : (1ull << pk.bits[i]) - 1;
+    const uint64_t ordb = ((uint64_t)pk.minv[i] - (pk.nullable[i] ? 1u : 0u)) ^ 0x8000000000000000ull;
+    return mask < ~0ull - ordb ? mask : ~0ull - ordb;
+}
+
 __global__ __launch_bounds__(256) void mk_pack_kernel(MkKeys k, MkPack pk, int64_t n, uint64_t* __restrict__ out,
                                                       uint64_t* __restrict__ valid_words,
                                                       unsigned int* __restrict__ outside = nullptr) {
@@ -214,7 +223,7 @@ __global__ __launch_bounds__(256) void mk_pack_kernel(MkKeys k, MkPack pk, int64
                     anynull = true;
                     bad |= !pk.nullable[i];
                 }
-                if (outside) bad |= pk.bits[i] < 64 && (f >> pk.bits[i]) != 0;
+                if (outside) bad |= f > mk_span(pk, i);
                 code |= f << pk.shift[i];
             }
             out[r] = code;
@@ -267,12 +276,13 @@ __global__ __launch_bounds__(256) void mk_pack_vec_kernel(MkKeys k, MkPack pk, i
 #pragma unroll
             for (int u = 0; u < U; ++u) mk_load_pair(k.c[i], base + (int64_t)u * T * 2, n, v[u][0], v[u][1]);
             const uint64_t noff = pk.nullable[i] ? 1u : 0u;
+            const uint64_t span = mk_span(pk, i);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
 #pragma unroll
                 for (int e = 0; e < 2; ++e) {
                     const uint64_t f = (uint64_t)((int64_t)v[u][e] - pk.minv[i]) + noff;
-                    if (outside) bad |= base + (int64_t)u * T * 2 + e < n && pk.bits[i] < 64 && (f >> pk.bits[i]) != 0;
+                    if (outside) bad |= base + (int64_t)u * T * 2 + e < n && f > span;
                     code[u][e] |= f << pk.shift[i];
                 }
             }

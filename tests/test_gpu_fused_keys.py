@@ -70,6 +70,12 @@ def test_fused_single_narrow_key(gpu, dtype, maintain_order):
     rng = np.random.default_rng(int(maintain_order) + (dtype == np.uint32) * 2)
     lo = 0 if dtype == np.uint32 else -(1 << 30)
     k = (rng.integers(0, 300, N) * 1_000_003 % (1 << 30) + lo).astype(dtype)
+    # the type's extremes and -1 (all-ones in 32 bits) as keys too
+    info_ = np.iinfo(dtype)
+    k[rng.integers(0, N, 50)] = info_.min
+    k[rng.integers(0, N, 50)] = info_.max
+    if dtype == np.int32:
+        k[rng.integers(0, N, 50)] = -1
     cols = _dense(rng, N)
     info = {}
     _check({"k": (k, None)}, cols, [("sum", "a"), ("len", "b"), ("max", "d")], maintain_order, info=info)
@@ -96,14 +102,26 @@ def test_fused_matches_code_column_path(gpu, plgpu_option):
     assert np.array_equal(fused["a"].to_numpy().view(np.uint64), plain["a"].to_numpy().view(np.uint64))
 
 
-def test_fused_outlier_repacks(gpu):
+@pytest.mark.parametrize("outlier", ["i64_high", "i32_low", "i32_high", "i32_negative_base"])
+def test_fused_outlier_repacks(gpu, outlier):
     """A row outside the sampled packing plan (far from every sampled key)
     is caught in the fused kernel (ST_KPACK): the group-by repacks with the
-    exact ranges and runs fused again, exact."""
+    exact ranges and runs fused again, exact.  The Int32 cases take the
+    32-bit field test (KeyPack mode 1), below and above the sampled range."""
     rng = np.random.default_rng(9)
     k1 = (rng.integers(0, 40, N) * 3 - 500).astype(np.int64)
-    k1[N // 2 + 7] = 1 << 40
     k2 = rng.integers(0, 10, N).astype(np.int32)  # ~400 groups: one LDS table
+    if outlier == "i32_negative_base":
+        k2 = (k2 - 1_000_000).astype(np.int32)
+    r = N // 2 + 7
+    if outlier == "i64_high":
+        k1[r] = 1 << 40
+    elif outlier == "i32_low":
+        k2[r] = np.iinfo(np.int32).min + 3
+    elif outlier == "i32_high":
+        k2[r] = np.iinfo(np.int32).max
+    else:
+        k2[r] = 2_000_000_000
     cols = _dense(rng, N)
     info = {}
     _check({"k1": (k1, None), "k2": (k2, None)}, cols, [("sum", "a"), ("len", "b")], False, info=info)
@@ -256,3 +274,4 @@ def test_fused_string_key(gpu, case):
     assert set(got) == set(want)
     for key, xs in want.items():
         assert got[key] == (math.fsum(xs), len(xs)), key
+
