@@ -226,6 +226,10 @@ int plgpu_alloc(void** out_ptr, size_t bytes, void* stream);
 int plgpu_free(void* ptr, void* stream);
 int plgpu_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream);
 int plgpu_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream);
+/* n device -> host copies (dst[i] <- src[i], bytes[i]) with one
+ * synchronisation: small ranges go through a library-owned pinned buffer.
+ * Returns when every dst holds its bytes (a query's result columns). */
+int plgpu_memcpy_d2h_many(int32_t n, void* const* dst, const void* const* src, const size_t* bytes, void* stream);
 int plgpu_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream);
 
 /* Test hooks and diagnostics, each read once from the environment variable

@@ -116,6 +116,8 @@ SIGNATURES = {
     "plgpu_free": (C.c_int, [_P, _P]),
     "plgpu_memcpy_h2d": (C.c_int, [_P, _P, C.c_size_t, _P]),
     "plgpu_memcpy_d2h": (C.c_int, [_P, _P, C.c_size_t, _P]),
+    "plgpu_memcpy_d2h_many": (C.c_int, [C.c_int32, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
+                                        C.POINTER(C.c_size_t), _P]),
     "plgpu_memcpy_d2d": (C.c_int, [_P, _P, C.c_size_t, _P]),
     "plgpu_column_release": (None, [_COLP]),
     "plgpu_expr_dtype": (C.c_int, [_COLP, C.c_int32, C.POINTER(Instr), C.c_int32, C.POINTER(C.c_int32)]),
@@ -265,6 +267,21 @@ def check(rc: int) -> None:
     if rc != OK:
         msg = lib().plgpu_last_error().decode(errors="replace")
         raise _ERRMAP.get(rc, PolaroidError)(msg)
+
+
+def download_many(ranges: list) -> list:
+    """[(device address, nbytes)] -> one host uint8 array per range, in one
+    round trip (plgpu_memcpy_d2h_many)."""
+    import numpy as np
+
+    outs = [np.empty(nb, dtype=np.uint8) for _, nb in ranges]
+    n = len(ranges)
+    if n:
+        dst = (C.c_void_p * n)(*[o.ctypes.data if o.nbytes else None for o in outs])
+        src = (C.c_void_p * n)(*[p if nb else None for p, nb in ranges])
+        sz = (C.c_size_t * n)(*[nb for _, nb in ranges])
+        check(lib().plgpu_memcpy_d2h_many(n, dst, src, sz, None))
+    return outs
 
 
 def set_option(name: str, value: int) -> int:

@@ -46,6 +46,7 @@ constexpr int kMaxFields = 48;
 constexpr int kLdsProbe = 16;
 constexpr int kGlobalProbe = 4096;
 constexpr int kLimb2Margin = 4;
+constexpr int kMinTilesPerWg = 160;  // fast kernel: fewer rounds below this many tiles per workgroup
 constexpr int kGridRounds = 8;        // fast kernel grid = rounds x resident workgroups       // binades below the smallest sampled exponent kept by 2 limbs
 constexpr int kHeadroomBinades = 8;   // above the sampled max exponent
 constexpr int64_t kMaxRowsPerWg = int64_t(1) << 22;  // keeps 40-bit limbs exact in int64
@@ -2768,12 +2769,20 @@ static hipError_t launch_fast_rows(const Plan& pl, const DevProgram& dp, hipStre
     // the plan's n_full is a multiple of the 2-row tile; a wider tile takes
     // its own multiple (the masked last tile covers the rest)
     if (ROWS != 2) q.n_full = (pl.p.n / ((int64_t)kGbThreads * ROWS)) * kGbThreads * ROWS;
-    // kGridRounds rounds of the workgroups resident per CU: later rounds'
-    // table init / flush overlap earlier rounds' streaming
+    // up to kGridRounds rounds of the workgroups resident per CU (later
+    // rounds' table init / flush overlap earlier rounds' streaming), but at
+    // least kMinTilesPerWg tiles per workgroup: every workgroup flushes its
+    // table to the global one, a fixed cost a short input cannot amortise
+    // (1e8 rows: 0.66 ms in one round against 0.84 ms in 8,
+    // profiles/r04_grid_rounds_ab.txt)
     const int64_t need = (q.n_full + kMaxRowsPerWg - 1) / kMaxRowsPerWg;
-    int64_t g = (int64_t)num_cus() * resident_per_cu(kern, kGbThreads, lds) * kGridRounds;
-    if (g < need) g = need;
     const int64_t useful = q.n_full / ((int64_t)kGbThreads * ROWS);
+    const int64_t resident = (int64_t)num_cus() * resident_per_cu(kern, kGbThreads, lds);
+    const int64_t rounds = options().grid_rounds > 0
+                               ? options().grid_rounds
+                               : std::min<int64_t>(kGridRounds, std::max<int64_t>(1, useful / (resident * kMinTilesPerWg)));
+    int64_t g = resident * rounds;
+    if (g < need) g = need;
     if (g > useful) g = std::max<int64_t>(1, useful);
     const int grid = (int)g;
     pl.launched_grid = grid;

@@ -53,6 +53,7 @@ static Options read_env_options() {
     o.local = get("PLGPU_LOCAL", -1);
     o.ktime = get("PLGPU_KTIME", 0);
     o.fuse_keys = get("PLGPU_FUSE_KEYS", 1);
+    o.grid_rounds = get("PLGPU_GRID_ROUNDS", 0);
     return o;
 }
 
@@ -744,6 +745,61 @@ PLGPU_API int plgpu_memcpy_d2h(void* dst, const void* src, size_t bytes, void* s
     return PLGPU_OK;
 }
 
+// Small device -> host downloads batched through one pinned staging buffer
+// (library-owned, grown on demand up to kD2hStageMax): every range's copy is
+// queued on the stream, then one synchronisation and host copies out.  A
+// range larger than the cap is copied on its own.  A query's result columns
+// (a few KB each) come back in one round trip instead of one per buffer.
+namespace {
+constexpr size_t kD2hStageMax = size_t(64) << 20;
+std::mutex g_stage_mu;
+void* g_stage = nullptr;
+size_t g_stage_bytes = 0;
+}  // namespace
+
+PLGPU_API int plgpu_memcpy_d2h_many(int32_t n, void* const* dst, const void* const* src, const size_t* bytes,
+                                    void* stream) {
+    if (n < 0 || (n > 0 && (dst == nullptr || src == nullptr || bytes == nullptr)))
+        return fail(PLGPU_ERR_INVALID, "memcpy_d2h_many: bad arguments");
+    hipStream_t s = as_stream(stream);
+    size_t total = 0;
+    for (int32_t i = 0; i < n; ++i)
+        if (bytes[i] <= kD2hStageMax) total += (bytes[i] + 255) & ~size_t(255);
+    std::lock_guard<std::mutex> lk(g_stage_mu);
+    if (total > kD2hStageMax) total = 0;  // too much for the stage: direct copies
+    if (total > g_stage_bytes) {
+        if (g_stage) (void)hipHostFree(g_stage);
+        g_stage = nullptr;
+        g_stage_bytes = 0;
+        const size_t want = std::max<size_t>(total, size_t(1) << 20);
+        if (hipHostMalloc(&g_stage, want, hipHostMallocDefault) != hipSuccess) {
+            (void)hipGetLastError();
+            g_stage = nullptr;
+            total = 0;
+        } else {
+            g_stage_bytes = want;
+        }
+    }
+    size_t off = 0;
+    for (int32_t i = 0; i < n; ++i) {
+        if (bytes[i] == 0) continue;
+        if (total > 0 && bytes[i] <= kD2hStageMax) {
+            PLGPU_HIP(hipMemcpyAsync((char*)g_stage + off, src[i], bytes[i], hipMemcpyDeviceToHost, s));
+            off += (bytes[i] + 255) & ~size_t(255);
+        } else {
+            PLGPU_HIP(hipMemcpyAsync(dst[i], src[i], bytes[i], hipMemcpyDeviceToHost, s));
+        }
+    }
+    PLGPU_HIP(hipStreamSynchronize(s));
+    off = 0;
+    for (int32_t i = 0; i < n; ++i) {
+        if (bytes[i] == 0 || !(total > 0 && bytes[i] <= kD2hStageMax)) continue;
+        std::memcpy(dst[i], (const char*)g_stage + off, bytes[i]);
+        off += (bytes[i] + 255) & ~size_t(255);
+    }
+    return PLGPU_OK;
+}
+
 PLGPU_API int plgpu_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream) {
     PLGPU_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, as_stream(stream)));
     return PLGPU_OK;
@@ -770,6 +826,7 @@ PLGPU_API int plgpu_set_option(const char* name, int64_t value) {
     else if (!strcmp(name, "local")) f = &o.local;
     else if (!strcmp(name, "ktime")) f = &o.ktime;
     else if (!strcmp(name, "fuse_keys")) f = &o.fuse_keys;
+    else if (!strcmp(name, "grid_rounds")) f = &o.grid_rounds;
     if (f == nullptr) return fail(PLGPU_ERR_INVALID, std::string("unknown option ") + name);
     *f = (int)value;
     return PLGPU_OK;
@@ -785,6 +842,7 @@ PLGPU_API int plgpu_get_option(const char* name, int64_t* out) {
     else if (!strcmp(name, "local")) *out = o.local;
     else if (!strcmp(name, "ktime")) *out = o.ktime;
     else if (!strcmp(name, "fuse_keys")) *out = o.fuse_keys;
+    else if (!strcmp(name, "grid_rounds")) *out = o.grid_rounds;
     else return fail(PLGPU_ERR_INVALID, std::string("unknown option ") + name);
     return PLGPU_OK;
 }

@@ -649,11 +649,12 @@ class _ArrowOf(dict):
 _ARROW_OF = _ArrowOf()
 
 
-def _ingest_chunks(name: str, chunks: list, atype) -> Series:
+def _ingest_chunks(name: str, chunks: list, atype, sync: bool = True) -> Series:
     """Arrow chunks (host) -> one device column through plgpu_column_alloc /
     plgpu_ingest_chunk: every chunk's value, validity and string buffers are
-    copied as they lie (Arrow offsets honoured), through the library's
-    pinned staging buffers, with one synchronisation at the end."""
+    copied as they lie (Arrow offsets honoured), with one synchronisation at
+    the end (none with sync=False: the caller synchronises once after all
+    its columns, as the plugin's scan does)."""
     import pyarrow as pa
 
     if pa.types.is_dictionary(atype):
@@ -678,6 +679,7 @@ def _ingest_chunks(name: str, chunks: list, atype) -> Series:
     if atype in (pa.string(), pa.utf8()):
         chunks = [c.cast(pa.large_string()) for c in chunks]
         atype = pa.large_string()
+        sync = True  # the cast buffers die with this call: wait for their copies
     dt = _arrow_physical(atype)
     if dt is None:
         raise N.InvalidOperationError(f"column {name!r}: arrow type {atype} is not supported on the GPU")
@@ -708,7 +710,8 @@ def _ingest_chunks(name: str, chunks: list, atype) -> Series:
             N.check(N.lib().plgpu_ingest_chunk(C.byref(out._col), row, byte, bufs[1].address, vb, data,
                                                c.offset, m, None))
         row += m
-    N.check(N.lib().plgpu_synchronize(None))
+    if sync:
+        N.check(N.lib().plgpu_synchronize(None))
     out._col.null_count = nulls
     return out
 
@@ -796,9 +799,34 @@ class DataFrame:
         return cls(out)
 
     def to_arrow(self):
+        """The frame as an Arrow table.  The buffers of its fixed-width
+        columns come back in one device -> host round trip
+        (plgpu_memcpy_d2h_many); String / Categorical columns take their
+        own path."""
         import pyarrow as pa
 
-        return pa.table({nm: s.to_arrow() for nm, s in self._cols.items()})
+        plain = [nm for nm, s in self._cols.items()
+                 if s._cat_codes() is None and s.dtype not in (String, Boolean) and s.len() > 0]
+        ranges = []
+        for nm in plain:
+            s = self._cols[nm]
+            n, off = s.len(), int(s._col.offset)
+            eb = np.dtype(s.dtype.np_dtype).itemsize
+            ranges.append((s._col.values + off * eb, n * eb))
+            ranges.append((s._col.validity, (off + n + 7) // 8) if s._col.validity else (0, 0))
+        host = N.download_many(ranges)
+        got = {}
+        for i, nm in enumerate(plain):
+            s = self._cols[nm]
+            n, off = s.len(), int(s._col.offset)
+            vals = host[2 * i].view(s.dtype.np_dtype)
+            valid = _unpack_bits(host[2 * i + 1], off, n) if s._col.validity else None
+            phys = _BY_CODE[s._col.dtype]
+            arr = pa.array(vals, type=_ARROW_OF[phys.name],
+                           mask=None if valid is None or valid.all() else ~valid)
+            lg = s._logical_dtype()
+            got[nm] = arr.view(_arrow_logical(lg)) if lg is not None else arr
+        return pa.table({nm: got[nm] if nm in got else s.to_arrow() for nm, s in self._cols.items()})
 
     def lazy(self) -> "LazyFrame":
         return LazyFrame(("scan", self))

@@ -508,10 +508,11 @@ def _scan_frame(batches: list, names: list, cache: "ColumnCache | None") -> Data
         key = ColumnCache.key(chunks, atype) if cache is not None else None
         s = cache.get(key) if cache is not None else None
         if s is None:
-            s = _ingest_chunks(nm, chunks, atype)
+            s = _ingest_chunks(nm, chunks, atype, sync=False)
             if cache is not None:
                 cache.put(key, s, chunks, sum(c.nbytes for c in chunks))
         cols.append(s.alias(nm))
+    N.check(N.lib().plgpu_synchronize(None))  # every column's copies issued: one wait
     return DataFrame(cols)
 
 

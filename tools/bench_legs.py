@@ -1,0 +1,42 @@
+"""One of bench.py's resident-frame legs alone (for profilers): the
+headline, vwap or std query over configs[1]'s 1e9-row frame.
+
+    python tools/bench_legs.py --leg vwap [--rows 1e9 --steps 5 --warmup 2]
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--leg", choices=["headline", "vwap", "std"], required=True)
+    ap.add_argument("--rows", type=float, default=1e9)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    args = ap.parse_args()
+    import torch
+
+    import bench
+    import polaroid_amd as pl
+
+    n = int(args.rows)
+    sym, cols = bench.make_data(torch, n, 100, seed=1234)
+    df = pl.DataFrame([pl.Series.from_torch("symbol", sym)] + [pl.Series.from_torch(c, t) for c, t in cols.items()])
+    if args.leg == "vwap":
+        r = bench.vwap_leg(torch, pl, df, sym, cols["close"], args.steps, args.warmup)
+    elif args.leg == "std":
+        r = bench.std_leg(torch, pl, df, args.steps, args.warmup)
+    else:
+        q = df.lazy().filter(pl.col("close") > bench.THRESHOLD).group_by("symbol").agg(
+            *[pl.col(c).sum() for c in ("open", "high", "low", "close")])
+        r = bench.timed_leg(torch, q, n, args.steps, args.warmup, 40)
+    print(json.dumps({"leg": args.leg, **r}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
