@@ -3663,9 +3663,12 @@ static int gb_main(GbRun& R, bool auto_refit, bool* refit, int32_t* hint) {
     const int64_t n = p.n;
     const bool debug = options().debug != 0;
     if (refit) *refit = false;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    PLGPU_HIP(hipEventCreate(&ev0));
-    PLGPU_HIP(hipEventCreate(&ev1));
+    hipEvent_t ev0 = ev_acquire(), ev1 = ev_acquire();
+    if (ev0 == nullptr || ev1 == nullptr) {
+        ev_release(ev0);
+        ev_release(ev1);
+        return fail(PLGPU_ERR_HIP, "hipEventCreate failed");
+    }
     int rc = PLGPU_OK;
     if (R.part && n > 0 && R.pbuf == nullptr) rc = gb_partition(R);
     for (R.attempts = 0; rc == PLGPU_OK; ++R.attempts) {
@@ -3756,8 +3759,8 @@ static int gb_main(GbRun& R, bool auto_refit, bool* refit, int32_t* hint) {
         }
     }
     if (rc == PLGPU_OK) (void)hipEventElapsedTime(&R.ms, ev0, ev1);
-    (void)hipEventDestroy(ev0);
-    (void)hipEventDestroy(ev1);
+    ev_release(ev0);
+    ev_release(ev1);
     if (rc == PLGPU_OK && R.wide && !R.kp_bad) rc = gb_wide(R);
     return rc;
 }

@@ -241,8 +241,9 @@ constexpr uint32_t kNullIdx = 0xFFFFFFFFu;  // null index in an output pair
 // an empty cell (a full bucket without the key continues, lane by lane, in
 // the next buckets - rare at load <= 0.6).
 // INLINE (row-format table, unique build keys): a cell holds {key, payload}
-// instead of {key, ref}; every row writes mp[r] (its payload, 0 on a miss)
-// and each wave one 64-bit hit mask into m's buffer.
+// instead of {key, ref}; each wave writes one 64-bit hit mask into m's
+// buffer and its hits' payloads, packed in hit order, at the start of its
+// 64-word segment of mp (misses write nothing).
 template <bool NULLABLE, int MODE, bool MARK, bool INLINE = false>
 __global__ __launch_bounds__(kJnThreads) void jn_probe_match_kernel(DevCol pk, int64_t np, JnTable t,
                                                                   bool nulls_equal, uint32_t* __restrict__ m,
@@ -362,10 +363,14 @@ __global__ __launch_bounds__(kJnThreads) void jn_probe_match_kernel(DevCol pk, i
                 c += (MODE == JM_SEMI) == hit ? 1 : 0;
             } else {
                 if (INLINE) {
-                    // dense payload words (0 for a miss) and one hit bit per
-                    // row, ballot words in m's buffer; no match word
-                    __builtin_nontemporal_store(hit ? pay : 0ull, mp + r);
+                    // one hit bit per row (ballot words in m's buffer; no
+                    // match word) and the hits' payload words packed at the
+                    // start of their wave's 64-word segment of mp (misses
+                    // write nothing; the emit reads them back the same way)
                     const uint64_t hw = __ballot(hit);
+                    const int ln = threadIdx.x & 63;
+                    const uint64_t lt = ln == 0 ? 0ull : (~0ull >> (64 - ln));
+                    if (hit) __builtin_nontemporal_store(pay, mp + (r & ~int64_t(63)) + __popcll(hw & lt));
                     if ((threadIdx.x & 63) == 0) reinterpret_cast<uint64_t*>(m)[r >> 6] = hw;
                     c += hit ? 1 : 0;
                     continue;
@@ -522,7 +527,8 @@ __global__ void jn_build_wide_kernel(DevCol bk, int64_t nb, WideCell* cells, int
 // bucket of row 16 j + g of the wave, each lane one 32-B cell (two 16-B
 // loads).  The payloads of a matching cell go back to the row's lane through
 // LDS.  Every row writes its W payload words (0 on a miss) to W dense arrays
-// and each wave one 64-bit hit mask into `mwords`.
+// and each wave one 64-bit hit mask into `mwords`; a hit row's W payload
+// words go to the wave's 64-word segment of W arrays, packed in hit order.
 template <bool NULLABLE, int W>
 __global__ __launch_bounds__(kJnThreads) void jn_probe_match_wide_kernel(DevCol pk, int64_t np, WideCell* cells,
                                                                        int64_t cap, int bbits, bool nulls_equal,
@@ -643,9 +649,15 @@ __global__ __launch_bounds__(kJnThreads) void jn_probe_match_wide_kernel(DevCol 
                 }
             }
             if (r >= np) continue;
-#pragma unroll
-            for (int w = 0; w < W; ++w) __builtin_nontemporal_store(hit ? pay[w] : 0ull, mp[w] + r);
             const uint64_t hw = __ballot(hit);
+            // the hits' payloads packed at the start of the wave's 64-word
+            // segment of each array (as the single-payload match pass)
+            const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+            if (hit) {
+#pragma unroll
+                for (int w = 0; w < W; ++w)
+                    __builtin_nontemporal_store(pay[w], mp[w] + (r & ~int64_t(63)) + __popcll(hw & lt));
+            }
             if ((threadIdx.x & 63) == 0) mwords[r >> 6] = hw;
             c += hit ? 1 : 0;
         }
@@ -707,8 +719,13 @@ __global__ __launch_bounds__(kJnThreads) void jn_take_emit_kernel(int64_t np, co
             for (int u = 0; u < U; ++u) {
                 const int64_t r = tile * kJnTileRows + (int64_t)(k0 + u) * kJnThreads + threadIdx.x;
                 const int64_t rr = r < np ? r : np - 1;
+                // a hit's payloads sit packed at the start of its wave's
+                // 64-word segment (the match pass's layout): only hits load
+                const uint64_t w = words[(k0 + u) * NW + wave];
+                const bool h = (w >> lane) & 1;
+                const int64_t pq = (r & ~int64_t(63)) + __popcll(w & lt);
 #pragma unroll
-                for (int q = 0; q < W; ++q) pv[u][q] = __builtin_nontemporal_load(tp.src[q] + rr);
+                for (int q = 0; q < W; ++q) pv[u][q] = h ? __builtin_nontemporal_load(tp.src[q] + pq) : 0ull;
 #pragma unroll
                 for (int j = 0; j < NC; ++j) v[u][j] = __builtin_nontemporal_load(lc.src[j] + rr);
             }

@@ -52,6 +52,10 @@ Options& options();
 // these live per-kernel times next to its step times, and they are the same
 // quantity a rocprofv3 kernel trace reports.  Off (the default), a scope
 // costs one load and a branch.
+// Recycled HIP events (hipEventCreate / Destroy per query cost more than
+// the query's host work at 1e8 rows); ev_acquire returns nullptr on failure.
+hipEvent_t ev_acquire();
+void ev_release(hipEvent_t e);
 int kt_begin(const char* name, hipStream_t s);
 void kt_end(int slot, hipStream_t s);
 struct KtScope {

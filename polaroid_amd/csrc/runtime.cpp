@@ -92,6 +92,17 @@ hipEvent_t kt_event() {
 }
 }  // namespace
 
+hipEvent_t ev_acquire() {
+    std::lock_guard<std::mutex> g(g_kt_mu);
+    return kt_event();
+}
+
+void ev_release(hipEvent_t e) {
+    if (e == nullptr) return;
+    std::lock_guard<std::mutex> g(g_kt_mu);
+    g_kt_pool.push_back(e);
+}
+
 int kt_begin(const char* name, hipStream_t s) {
     std::lock_guard<std::mutex> g(g_kt_mu);
     hipEvent_t a = kt_event(), b = kt_event();

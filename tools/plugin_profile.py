@@ -25,6 +25,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=float, default=1e8)
     ap.add_argument("--calls", type=int, default=20)
+    ap.add_argument("--prewarm", action="store_true", help="a small query first, then the pool released (bench.py's state)")
     args = ap.parse_args()
     import pyarrow as pa
     import torch
@@ -76,6 +77,16 @@ def main():
                                                           for k, v in t.items()}, "groups": tab.num_rows}),
               flush=True)
 
+    if args.prewarm:
+        # as inside bench.py: the library's code object loaded and the host
+        # link's copy path initialised by earlier work in the process, its
+        # memory pool released before the leg
+        small = pa.table({c: table.column(c).slice(0, 1 << 20) for c in table.column_names})
+        snt = ir_model.filter_group_by_sum(small, "symbol", "close", bench.THRESHOLD, cols, chunk_rows=1 << 20)
+        PE.execute_with_polaroid(snt, None, to_frame=lambda t: t)
+        snt.udf(None, None, None, False)
+        cache.clear()
+        N.release_cached()
     phases("cold")
     for i in range(3):
         phases(f"warm{i}")
