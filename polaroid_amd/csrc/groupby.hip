@@ -46,6 +46,12 @@ constexpr int kMaxFields = 48;
 constexpr int kLdsProbe = 16;
 constexpr int kGlobalProbe = 4096;
 constexpr int kLimb2Margin = 4;
+// SLIM table (sum-only, 2 limbs) of NACC sums: the keys (L words), then per
+// slot its len and each acc's two limbs and flags word, slot-major, padded
+// to an odd word count (two LDS banks per word: an odd stride spreads the
+// slots over 32 bank pairs).  LDS words per slot:
+constexpr int slim_vwords(int nacc) { return (1 + 3 * nacc) | 1; }
+constexpr int slim_words(int nacc) { return 1 + slim_vwords(nacc); }
 constexpr int kMinTilesPerWg = 160;  // fast kernel: fewer rounds below this many tiles per workgroup
 constexpr int kGridRounds = 8;        // fast kernel grid = rounds x resident workgroups       // binades below the smallest sampled exponent kept by 2 limbs
 constexpr int kHeadroomBinades = 8;   // above the sampled max exponent
@@ -1214,19 +1220,26 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
     // x's registers: one column loaded, no operand registers per acc
     static_assert(!VAR || (NACC == 3 && !DERIV), "VAR: three sums of one column");
     constexpr int NL = VAR ? 1 : NACC;  // accs whose column the tile loads
-    // SLIM (sum-only, 2 limbs): LDS fields key 0, len 1, acc a: limbs
-    // 2+3a, 3+3a, flags 4+3a (the unused low limb of the 3-limb layout is
-    // not stored, so more workgroups fit per CU)
+    // SLIM (sum-only, 2 limbs): fields key 0, len 1, acc a: limbs 2+3a,
+    // 3+3a, flags 4+3a (the unused low limb of the 3-limb layout is not
+    // stored, so more workgroups fit per CU).  The keys are one array (the
+    // probes scan it); a slot's other fields are adjacent (slot-major,
+    // slim_vwords per slot), so a row's atomics share one address register
+    // and take immediate offsets.  Other layouts: field-major, field f of
+    // slot s at f * L + s.
     constexpr bool SLIM = SUMONLY && LIMBS == 2;
+    constexpr int FV = slim_vwords(NACC);
     auto so_mid = [](int a) { return SLIM ? 2 + 3 * a : 3 + 4 * a; };
     auto so_top = [](int a) { return SLIM ? 3 + 3 * a : 4 + 4 * a; };
     auto so_flags = [](int a) { return SLIM ? 4 + 3 * a : 5 + 4 * a; };
     const int L = p.lcap + 2;
+    // field f (>= 1) of slot s
+    auto fld = [&](int s_, int f) -> unsigned long long* {
+        return (unsigned long long*)(SLIM ? &lds[L + s_ * FV + (f - 1)] : &lds[f * L + s_]);
+    };
     if (SLIM) {
-        for (int f = 0; f < 2 + 3 * NACC; ++f) {
-            const uint64_t v = f == 0 ? kEmptyKey : 0ull;
-            for (int i = threadIdx.x; i < L; i += blockDim.x) lds[f * L + i] = v;
-        }
+        for (int i = threadIdx.x; i < L; i += blockDim.x) lds[i] = kEmptyKey;
+        for (int i = threadIdx.x; i < L * FV; i += blockDim.x) lds[L + i] = 0ull;
     } else {
         init_lds(p, lds, L);
     }
@@ -1317,12 +1330,11 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
     int rvict = 0;
     auto racc_flush = [&](int k) {
         if (rs[k] < 0) return;
-        unsigned long long* q = (unsigned long long*)&lds[rs[k]];
-        atomicAdd(q + L, (unsigned long long)rn[k]);
+        atomicAdd(fld(rs[k], 1), (unsigned long long)rn[k]);
 #pragma unroll
         for (int a = 0; a < NACC; ++a) {
-            atomicAdd(q + so_mid(a) * L, (unsigned long long)rlo_[k][a]);
-            atomicAdd(q + so_top(a) * L, (unsigned long long)rhi_[k][a]);
+            atomicAdd(fld(rs[k], so_mid(a)), (unsigned long long)rlo_[k][a]);
+            atomicAdd(fld(rs[k], so_top(a)), (unsigned long long)rhi_[k][a]);
         }
         rs[k] = -1;
     };
@@ -1597,8 +1609,7 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
                 }
                 if (held) {
                 } else if (SUMONLY && s >= 0) {
-                    unsigned long long* q = (unsigned long long*)&lds[s];
-                    atomicAdd(q + L, 1ull);
+                    atomicAdd(fld(s, 1), 1ull);
                     uint32_t slow = 0;
 #pragma unroll
                     for (int a = 0; a < NACC; ++a) {
@@ -1606,9 +1617,9 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
                         const bool ok = fx_limbs_fast<LIMBS>(rv[a], bot[a], l0, l1, l2);
                         slow |= (ok ? 0u : 1u) << a;
                         // zero limbs (slow lanes, zero values) add nothing
-                        if (LIMBS == 3) atomicAdd(q + (2 + 4 * a) * L, (unsigned long long)l0);
-                        atomicAdd(q + so_mid(a) * L, (unsigned long long)(LIMBS == 3 ? l1 : l0));
-                        atomicAdd(q + so_top(a) * L, (unsigned long long)(LIMBS == 3 ? l2 : l1));
+                        if (LIMBS == 3) atomicAdd(fld(s, 2 + 4 * a), (unsigned long long)l0);
+                        atomicAdd(fld(s, so_mid(a)), (unsigned long long)(LIMBS == 3 ? l1 : l0));
+                        atomicAdd(fld(s, so_top(a)), (unsigned long long)(LIMBS == 3 ? l2 : l1));
                     }
                     if (slow) {
                         // inf / NaN flags, rounding below the window, overflow
@@ -1618,7 +1629,7 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
                             const uint64_t x = rv[a];
                             const uint64_t ab = x & 0x7fffffffffffffffull;
                             if (ab >= 0x7ff0000000000000ull) {
-                                atomicOr(q + so_flags(a) * L,
+                                atomicOr(fld(s, so_flags(a)),
                                          (unsigned long long)(ab > 0x7ff0000000000000ull ? FL_NAN
                                                               : ((x >> 63) ? FL_NINF : FL_PINF)));
                             } else {
@@ -1630,9 +1641,9 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
                                                                                     ex);
                                 d.fxbits |= fl << (2 * a);
                                 if (ok) {
-                                    if (LIMBS == 3) atomicAdd(q + (2 + 4 * a) * L, (unsigned long long)l0);
-                                    atomicAdd(q + so_mid(a) * L, (unsigned long long)(LIMBS == 3 ? l1 : l0));
-                                    atomicAdd(q + so_top(a) * L, (unsigned long long)(LIMBS == 3 ? l2 : l1));
+                                    if (LIMBS == 3) atomicAdd(fld(s, 2 + 4 * a), (unsigned long long)l0);
+                                    atomicAdd(fld(s, so_mid(a)), (unsigned long long)(LIMBS == 3 ? l1 : l0));
+                                    atomicAdd(fld(s, so_top(a)), (unsigned long long)(LIMBS == 3 ? l2 : l1));
                                 }
                             }
                         }
@@ -1664,7 +1675,7 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
     if (SLIM) {
         __syncthreads();
         for (int sl = threadIdx.x; sl < L; sl += blockDim.x) {
-            const uint64_t len = lds[L + sl];
+            const uint64_t len = *fld(sl, 1);
             if (len == 0) continue;
             int64_t gs;
             if (sl == p.lcap) {
@@ -1685,9 +1696,9 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
             for (int a = 0; a < NACC; ++a) {
                 const int f = p.acc[a].f_sum;
                 uint64_t w0, w1, w2;
-                limbs_to_192(0, (int64_t)lds[so_mid(a) * L + sl], (int64_t)lds[so_top(a) * L + sl], w0, w1, w2);
+                limbs_to_192(0, (int64_t)*fld(sl, so_mid(a)), (int64_t)*fld(sl, so_top(a)), w0, w1, w2);
                 g_add192(gfield(p, f, gs), gfield(p, f + 1, gs), gfield(p, f + 2, gs), w0, w1, w2);
-                const uint64_t fl = lds[so_flags(a) * L + sl];
+                const uint64_t fl = *fld(sl, so_flags(a));
                 if (fl) atomicOr((unsigned long long*)gfield(p, p.acc[a].f_flags, gs), (unsigned long long)fl);
             }
         }
@@ -2763,7 +2774,7 @@ static hipError_t launch_fast_rows(const Plan& pl, const DevProgram& dp, hipStre
         (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_set = true;
     }
-    const size_t lds = (SUMONLY && LIMBS == 2) ? (size_t)(2 + 3 * NACC) * (pl.p.lcap + 2) * 8 : pl.lds_bytes;
+    const size_t lds = (SUMONLY && LIMBS == 2) ? (size_t)slim_words(NACC) * (pl.p.lcap + 2) * 8 : pl.lds_bytes;
     GbParams q = pl.p;
     q.tiles_per_wg = 0;
     // the plan's n_full is a multiple of the 2-row tile; a wider tile takes
@@ -3406,7 +3417,7 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
         // sum-only on the 2-limb window: the fast kernel's slim table
         // (2 + 3 nacc fields); the full layout must still fit one workgroup
         // per CU for a 3-limb rerun through the generic kernel
-        const int fields = (pl.sum_only && pl.limbs == 2) ? 2 + 3 * p.nacc : p.nfields;
+        const int fields = (pl.sum_only && pl.limbs == 2) ? slim_words(p.nacc) : p.nfields;
         // Fewer, larger partition tables first (160 KB, one workgroup per
         // CU): measured 2-7 % faster than 80 KB tables at 14k-100k groups
         // (profiles/r02_ab_part.log)
@@ -3521,7 +3532,7 @@ static hipError_t launch_part_fast(const Plan& pp, int grid, hipStream_t s) {
         (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_set = true;
     }
-    const size_t lds = (size_t)(LIMBS == 2 ? 2 + 3 * NACC : pp.p.nfields) * (pp.p.lcap + 2) * 8;
+    const size_t lds = (size_t)(LIMBS == 2 ? slim_words(NACC) : pp.p.nfields) * (pp.p.lcap + 2) * 8;
     DevProgram none;
     std::memset(&none, 0, sizeof none);
     gb_fast_kernel<NACC, 0, true, 2, LIMBS, false, true><<<grid, kGbThreads, lds, s>>>(pp.p, none);
