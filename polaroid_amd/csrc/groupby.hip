@@ -366,6 +366,27 @@ __device__ __forceinline__ int64_t g_find(const GbParams& p, uint64_t key) {
 // fx_limbs (inf / NaN, bits below the window, overflow).
 template <int LIMBS>
 __device__ __forceinline__ bool fx_limbs_fast(uint64_t x, int bottom, uint64_t& l0, uint64_t& l1, uint64_t& l2) {
+    if (LIMBS == 2) {
+        // The 2-limb form with the least VALU work (the fused kernels are
+        // issue-bound): the mantissa keeps its implicit bit only for ex != 0,
+        // so a zero gives zero limbs whatever the shift, and nothing is
+        // zeroed for values outside the window -- their limbs are garbage
+        // and the callers use limbs only on a true return.  Shift amounts
+        // are taken mod 64 (the hardware's own masking).
+        constexpr uint64_t M40 = (1ull << 40) - 1;
+        constexpr int W = kSumWindowBits - 40;
+        const uint32_t hi = (uint32_t)(x >> 32), lo = (uint32_t)x;
+        const uint32_t ex = (hi >> 20) & 0x7FF;
+        const uint32_t sh = ex - (uint32_t)(1075 + bottom + 40);
+        const bool inrange = sh <= (uint32_t)(W - 53) && ex != 0;
+        const bool zero = ((hi << 1) | lo) == 0;
+        const uint64_t m = (x & 0x000FFFFFFFFFFFFFull) | ((uint64_t)(ex != 0 ? 1u : 0u) << 52);
+        const int64_t sm = (int32_t)hi < 0 ? -(int64_t)m : (int64_t)m;
+        l0 = ((uint64_t)sm << (sh & 63)) & M40;
+        l1 = (uint64_t)(sm >> ((40 - sh) & 63));  // sh <= 27 when used
+        l2 = 0;
+        return inrange || zero;
+    }
     // The signed value t = +-m * 2^sh (sh >= 0, t < 2^W) is split as
     // t = l0 + l1 * 2^40 (+ l2 * 2^80) with l0 (and l1 in the 3-limb case)
     // taken as the low 40 bits (>= 0) and the top limb as the arithmetic
@@ -1611,15 +1632,27 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
                 } else if (SUMONLY && s >= 0) {
                     atomicAdd(fld(s, 1), 1ull);
                     uint32_t slow = 0;
+                    uint64_t fl0[NA], fl1[NA], fl2[NA];
 #pragma unroll
                     for (int a = 0; a < NACC; ++a) {
-                        uint64_t l0, l1, l2;
-                        const bool ok = fx_limbs_fast<LIMBS>(rv[a], bot[a], l0, l1, l2);
+                        const bool ok = fx_limbs_fast<LIMBS>(rv[a], bot[a], fl0[a], fl1[a], fl2[a]);
                         slow |= (ok ? 0u : 1u) << a;
-                        // zero limbs (slow lanes, zero values) add nothing
-                        if (LIMBS == 3) atomicAdd(fld(s, 2 + 4 * a), (unsigned long long)l0);
-                        atomicAdd(fld(s, so_mid(a)), (unsigned long long)(LIMBS == 3 ? l1 : l0));
-                        atomicAdd(fld(s, so_top(a)), (unsigned long long)(LIMBS == 3 ? l2 : l1));
+                    }
+                    // the limbs of a slow value are not added here (2 limbs:
+                    // they are unspecified; 3 limbs: zero); the common row
+                    // has none and takes the unmasked block
+                    auto add_limbs = [&](int a) {
+                        if (LIMBS == 3) atomicAdd(fld(s, 2 + 4 * a), (unsigned long long)fl0[a]);
+                        atomicAdd(fld(s, so_mid(a)), (unsigned long long)(LIMBS == 3 ? fl1[a] : fl0[a]));
+                        atomicAdd(fld(s, so_top(a)), (unsigned long long)(LIMBS == 3 ? fl2[a] : fl1[a]));
+                    };
+                    if (LIMBS == 3 || slow == 0) {
+#pragma unroll
+                        for (int a = 0; a < NACC; ++a) add_limbs(a);
+                    } else {
+#pragma unroll
+                        for (int a = 0; a < NACC; ++a)
+                            if (!((slow >> a) & 1u)) add_limbs(a);
                     }
                     if (slow) {
                         // inf / NaN flags, rounding below the window, overflow
