@@ -30,7 +30,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <numeric>
+#include <string>
 #include <tuple>
 #include <vector>
 
@@ -3270,6 +3272,68 @@ static double hll_estimate(const uint32_t* regs) {
     return e;
 }
 
+// Plan statistics of recent group-bys (the plan kernels' status words and
+// the HLL estimate), keyed by the plan's inputs: the key / packed-key
+// columns, the accumulators (columns, derived operands, field layout), the
+// row count and the simple predicate.  A repeated query over resident
+// columns (the plugin's warm path) skips the sampling launches and their
+// round trip.  The statistics only steer table sizes and kernel choice:
+// every pass still checks its own results (table full, window flags,
+// packed-key fit) and reruns, so a stale entry -- a freed column's address
+// reused by other data -- costs speed, never exactness.  Option
+// plan_cache = 0 disables it.
+namespace {
+struct PlanStats {
+    uint64_t st[ST_WORDS];
+    int64_t hll;
+};
+std::mutex g_plan_mu;
+std::vector<std::pair<std::string, PlanStats>> g_plan_cache;  // most recent last
+constexpr size_t kPlanCacheEntries = 32;
+
+std::string plan_key(const GbRun& R) {
+    const GbParams& p = R.pl.p;
+    std::string k;
+    auto put = [&k](const void* x, size_t nb) { k.append((const char*)x, nb); };
+    put(&p.n, sizeof p.n);
+    put(&p.key, sizeof p.key);
+    put(&p.kp, sizeof p.kp);
+    put(&p.nacc, sizeof p.nacc);
+    for (int a = 0; a < p.nacc; ++a) put(&p.acc[a], sizeof p.acc[a]);
+    put(&R.pred, sizeof R.pred);
+    if (R.pred == 1) {
+        put(&R.dp.simple_isf, sizeof R.dp.simple_isf);
+        put(&R.dp.simple_op, sizeof R.dp.simple_op);
+        put(&R.dp.simple_imm, sizeof R.dp.simple_imm);
+        put(&p.pred_col, sizeof p.pred_col);
+        put(&p.pred_acc, sizeof p.pred_acc);
+    }
+    return k;
+}
+
+bool plan_cache_get(const std::string& key, PlanStats* out) {
+    std::lock_guard<std::mutex> g(g_plan_mu);
+    for (size_t i = g_plan_cache.size(); i-- > 0;) {
+        if (g_plan_cache[i].first != key) continue;
+        *out = g_plan_cache[i].second;
+        std::rotate(g_plan_cache.begin() + (ptrdiff_t)i, g_plan_cache.begin() + (ptrdiff_t)i + 1, g_plan_cache.end());
+        return true;
+    }
+    return false;
+}
+
+void plan_cache_put(const std::string& key, const PlanStats& v) {
+    std::lock_guard<std::mutex> g(g_plan_mu);
+    for (auto& e : g_plan_cache)
+        if (e.first == key) {
+            e.second = v;
+            return;
+        }
+    if (g_plan_cache.size() >= kPlanCacheEntries) g_plan_cache.erase(g_plan_cache.begin());
+    g_plan_cache.emplace_back(key, v);
+}
+}  // namespace
+
 // Planning launch -> distinct-key estimate, fixed-point bottoms, table
 // sizes, kernel choice.  `fixed` (nullable) overrides the sampled bottoms.
 static int gb_plan(GbRun& R, const int32_t* fixed) {
@@ -3281,24 +3345,38 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
     // column has no selected nonzero value in the sample, its acc tasks run
     // again unfiltered (the key task is not repeated)
     const bool ps = R.pred == 1;
-    {
-        KtScope kt("gb_plan_kernel", R.s);
-        gb_plan_kernel<<<p.nacc * kPlanBlocks + kPlanKeyBlocks, kPlanThreads, 0, R.s>>>(
-            p, R.status + kPlanSetWord, kPlanSamples, ps ? 1 : 0, ps ? R.dp.simple_isf : 0, ps ? R.dp.simple_op : 0,
-            ps ? R.dp.simple_imm : 0ull);
-    }
-    PLGPU_HIP(hipGetLastError());
-    PLGPU_HIP(hipMemcpyAsync(R.st, R.status, sizeof R.st, hipMemcpyDeviceToHost, R.s));
-    PLGPU_HIP(hipStreamSynchronize(R.s));
-    bool unsampled = false;
-    for (int a = 0; a < p.nacc; ++a)
-        if ((p.acc[a].flags & (A_FSUM | A_FSUMCAST)) && R.st[ST_MAXEX + a] == 0) unsampled = true;
-    if (ps && unsampled) {
-        gb_plan_kernel<<<p.nacc * kPlanBlocks, kPlanThreads, 0, R.s>>>(p, R.status + kPlanSetWord, kPlanSamples, 0,
-                                                                       0, 0, 0ull);
+    // (large inputs only: below 2^24 rows the sampling is a small share)
+    const bool use_cache = fixed == nullptr && options().plan_cache != 0 && n >= (int64_t(1) << 24);
+    const std::string ckey = use_cache ? plan_key(R) : std::string();
+    PlanStats cached;
+    const bool hit = use_cache && plan_cache_get(ckey, &cached);
+    if (hit) {
+        std::memcpy(R.st, cached.st, sizeof R.st);
+    } else {
+        {
+            KtScope kt("gb_plan_kernel", R.s);
+            gb_plan_kernel<<<p.nacc * kPlanBlocks + kPlanKeyBlocks, kPlanThreads, 0, R.s>>>(
+                p, R.status + kPlanSetWord, kPlanSamples, ps ? 1 : 0, ps ? R.dp.simple_isf : 0,
+                ps ? R.dp.simple_op : 0, ps ? R.dp.simple_imm : 0ull);
+        }
         PLGPU_HIP(hipGetLastError());
         PLGPU_HIP(hipMemcpyAsync(R.st, R.status, sizeof R.st, hipMemcpyDeviceToHost, R.s));
         PLGPU_HIP(hipStreamSynchronize(R.s));
+        bool unsampled = false;
+        for (int a = 0; a < p.nacc; ++a)
+            if ((p.acc[a].flags & (A_FSUM | A_FSUMCAST)) && R.st[ST_MAXEX + a] == 0) unsampled = true;
+        if (ps && unsampled) {
+            gb_plan_kernel<<<p.nacc * kPlanBlocks, kPlanThreads, 0, R.s>>>(p, R.status + kPlanSetWord, kPlanSamples,
+                                                                           0, 0, 0, 0ull);
+            PLGPU_HIP(hipGetLastError());
+            PLGPU_HIP(hipMemcpyAsync(R.st, R.status, sizeof R.st, hipMemcpyDeviceToHost, R.s));
+            PLGPU_HIP(hipStreamSynchronize(R.s));
+        }
+        if (use_cache) {
+            std::memcpy(cached.st, R.st, sizeof R.st);
+            cached.hll = -1;
+            plan_cache_put(ckey, cached);
+        }
     }
     R.st[ST_SAMPLED] = (uint64_t)std::min<int64_t>(n, kPlanSamples);
     // sorted / clustered keys: the fused kernel's lanes keep a register
@@ -3326,20 +3404,28 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
             R.kp_fallback = true;
             return PLGPU_OK;
         }
-        uint32_t* regs = nullptr;
-        std::vector<uint32_t> h(1 << kHllBits);
-        int rc = dev_alloc((void**)&regs, h.size() * 4, R.s);
-        if (rc) return rc;
-        hipError_t e = hipMemsetAsync(regs, 0, h.size() * 4, R.s);
-        if (e == hipSuccess) {
-            gb_hll_kernel<<<num_cus() * 4, 256, 0, R.s>>>(p.key, n, regs);
-            e = hipGetLastError();
+        if (hit && cached.hll >= 0) {
+            hll = cached.hll;
+        } else {
+            uint32_t* regs = nullptr;
+            std::vector<uint32_t> h(1 << kHllBits);
+            int rc = dev_alloc((void**)&regs, h.size() * 4, R.s);
+            if (rc) return rc;
+            hipError_t e = hipMemsetAsync(regs, 0, h.size() * 4, R.s);
+            if (e == hipSuccess) {
+                gb_hll_kernel<<<num_cus() * 4, 256, 0, R.s>>>(p.key, n, regs);
+                e = hipGetLastError();
+            }
+            if (e == hipSuccess) e = hipMemcpyAsync(h.data(), regs, h.size() * 4, hipMemcpyDeviceToHost, R.s);
+            if (e == hipSuccess) e = hipStreamSynchronize(R.s);
+            dev_free(regs, R.s);
+            if (e != hipSuccess) return hip_fail(e, "gb_hll_kernel");
+            hll = (int64_t)hll_estimate(h.data());
+            if (use_cache) {
+                cached.hll = hll;
+                plan_cache_put(ckey, cached);
+            }
         }
-        if (e == hipSuccess) e = hipMemcpyAsync(h.data(), regs, h.size() * 4, hipMemcpyDeviceToHost, R.s);
-        if (e == hipSuccess) e = hipStreamSynchronize(R.s);
-        dev_free(regs, R.s);
-        if (e != hipSuccess) return hip_fail(e, "gb_hll_kernel");
-        hll = (int64_t)hll_estimate(h.data());
     }
     size_tables(&pl, R.st[ST_DISTINCT], R.st[ST_SAMPLED], &R.gbits, hll, &R.est_groups);
     // range-local mode: too many keys for one LDS table over the column, but

@@ -42,6 +42,7 @@ struct Options {
     int local = -1;      // -1: the plan picks the range-local kernel; 0 keeps it off (tests)
     int ktime = 0;       // 1: time the named kernels with HIP events (plgpu_ktime_read)
     int fuse_keys = 1;   // 0: packed multi-key codes go through a code column (tests / A-B)
+    int plan_cache = 1;  // 0: every group-by samples its inputs (no reuse of recent plan statistics)
     int grid_rounds = 0; // fused group-by grid in rounds of resident workgroups (0: kGridRounds; A-B)
 };
 Options& options();

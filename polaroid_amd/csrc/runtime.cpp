@@ -54,6 +54,7 @@ static Options read_env_options() {
     o.ktime = get("PLGPU_KTIME", 0);
     o.fuse_keys = get("PLGPU_FUSE_KEYS", 1);
     o.grid_rounds = get("PLGPU_GRID_ROUNDS", 0);
+    o.plan_cache = get("PLGPU_PLAN_CACHE", 1);
     return o;
 }
 
@@ -838,6 +839,7 @@ PLGPU_API int plgpu_set_option(const char* name, int64_t value) {
     else if (!strcmp(name, "ktime")) f = &o.ktime;
     else if (!strcmp(name, "fuse_keys")) f = &o.fuse_keys;
     else if (!strcmp(name, "grid_rounds")) f = &o.grid_rounds;
+    else if (!strcmp(name, "plan_cache")) f = &o.plan_cache;
     if (f == nullptr) return fail(PLGPU_ERR_INVALID, std::string("unknown option ") + name);
     *f = (int)value;
     return PLGPU_OK;
@@ -854,6 +856,7 @@ PLGPU_API int plgpu_get_option(const char* name, int64_t* out) {
     else if (!strcmp(name, "ktime")) *out = o.ktime;
     else if (!strcmp(name, "fuse_keys")) *out = o.fuse_keys;
     else if (!strcmp(name, "grid_rounds")) *out = o.grid_rounds;
+    else if (!strcmp(name, "plan_cache")) *out = o.plan_cache;
     else return fail(PLGPU_ERR_INVALID, std::string("unknown option ") + name);
     return PLGPU_OK;
 }
