@@ -237,6 +237,10 @@ int plgpu_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream);
  *   "ktime"       1: time the named kernels with HIP events (plgpu_ktime_read)
  *   "fuse_keys"   0: multi-key / Categorical group-bys write their packed
  *                 code column instead of forming the codes in the fused kernel
+ *   "plan_cache"  0: every group-by samples its inputs (no reuse of the plan
+ *                 statistics of a recent group-by over the same columns)
+ *   "grid_rounds" > 0: the fused group-by grid in that many rounds of resident
+ *                 workgroups (A/B; 0: scaled with the input)
  *   "debug"       per-attempt group-by diagnostics on stderr
  *   "no_pack"     multi-key operators hash their key tuples even when the
  *                 tuples would pack into one Int64 (exercises the hashed path)
