@@ -3334,6 +3334,11 @@ void plan_cache_put(const std::string& key, const PlanStats& v) {
 }
 }  // namespace
 
+void gb_plan_cache_clear() {
+    std::lock_guard<std::mutex> g(g_plan_mu);
+    g_plan_cache.clear();
+}
+
 // Planning launch -> distinct-key estimate, fixed-point bottoms, table
 // sizes, kernel choice.  `fixed` (nullable) overrides the sampled bottoms.
 static int gb_plan(GbRun& R, const int32_t* fixed) {

@@ -55,6 +55,8 @@ Options& options();
 // costs one load and a branch.
 // Recycled HIP events (hipEventCreate / Destroy per query cost more than
 // the query's host work at 1e8 rows); ev_acquire returns nullptr on failure.
+// Forget the group-by plan statistics kept for repeated queries (groupby.hip).
+void gb_plan_cache_clear();
 hipEvent_t ev_acquire();
 void ev_release(hipEvent_t e);
 int kt_begin(const char* name, hipStream_t s);

@@ -866,8 +866,11 @@ PLGPU_API int plgpu_release_cached(void) {
     PLGPU_HIP(hipGetDevice(&dev));
     PLGPU_HIP(hipDeviceSynchronize());
     Pool& P = pool_for(dev);
-    std::lock_guard<std::mutex> lk(P.mu);
-    release_cached(P);
+    {
+        std::lock_guard<std::mutex> lk(P.mu);
+        release_cached(P);
+    }
+    gb_plan_cache_clear();  // the released addresses will hold other data
     return PLGPU_OK;
 }
 
