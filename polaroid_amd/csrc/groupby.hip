@@ -2224,11 +2224,23 @@ struct FinParams {
 
 __global__ void gb_finalize_kernel(GbParams p, FinParams fp) {
     const int64_t total = p.gcap + 2;
-    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < total;
-         s += (int64_t)gridDim.x * blockDim.x) {
-        const uint64_t len = *gfield(p, p.f_len, s);
+    const int lane = threadIdx.x & 63;
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    // output positions: one counter add per wave (ballot of its live slots),
+    // not one per group -- a single-address atomic per group serialises
+    // (14k groups: ~0.07 ms; 1e6 groups: milliseconds)
+    for (int64_t s0 = (int64_t)blockIdx.x * blockDim.x; s0 < total; s0 += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t s = s0 + threadIdx.x;
+        const uint64_t len = s < total ? *gfield(p, p.f_len, s) : 0ull;
+        const uint64_t live = __ballot(len != 0);
+        if (live == 0) continue;
+        const int first = __ffsll((unsigned long long)live) - 1;
+        unsigned long long base = 0;
+        if (lane == first) base = atomicAdd((unsigned long long*)&p.status[ST_GROUPS_OUT],
+                                            (unsigned long long)__popcll(live));
+        base = __shfl(base, first, 64);
         if (len == 0) continue;
-        const int64_t g = (int64_t)atomicAdd((unsigned long long*)&p.status[ST_GROUPS_OUT], 1ull);
+        const int64_t g = (int64_t)base + __popcll(live & lt);
         if (g >= fp.cap) continue;
         const bool null_key = s == p.gcap;
         fp.out_keys[g] = null_key ? 0 : (int64_t)(s == p.gcap + 1 ? kEmptyKey : *gfield(p, 0, s));

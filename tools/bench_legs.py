@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--rows", type=float, default=1e9)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--groups", type=int, default=100, help="distinct symbols (the headline's 100 by default)")
     args = ap.parse_args()
     import torch
 
@@ -25,7 +26,7 @@ def main():
     import polaroid_amd as pl
 
     n = int(args.rows)
-    sym, cols = bench.make_data(torch, n, 100, seed=1234)
+    sym, cols = bench.make_data(torch, n, args.groups, seed=1234)
     df = pl.DataFrame([pl.Series.from_torch("symbol", sym)] + [pl.Series.from_torch(c, t) for c, t in cols.items()])
     if args.leg == "vwap":
         r = bench.vwap_leg(torch, pl, df, sym, cols["close"], args.steps, args.warmup)
@@ -35,7 +36,7 @@ def main():
         q = df.lazy().filter(pl.col("close") > bench.THRESHOLD).group_by("symbol").agg(
             *[pl.col(c).sum() for c in ("open", "high", "low", "close")])
         r = bench.timed_leg(torch, q, n, args.steps, args.warmup, 40)
-    print(json.dumps({"leg": args.leg, **r}), flush=True)
+    print(json.dumps({"leg": args.leg, "groups": args.groups, **r}), flush=True)
 
 
 if __name__ == "__main__":
