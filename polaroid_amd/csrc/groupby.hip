@@ -3346,9 +3346,45 @@ void plan_cache_put(const std::string& key, const PlanStats& v) {
 }
 }  // namespace
 
+// The same for the multi-key packing plan (the sampled key ranges of
+// mk_plan_pack_sampled, or the exact ranges once a row left them): the
+// fused kernel flags any row outside the plan and the caller repacks, so a
+// stale plan costs a repack, never exactness.
+namespace {
+std::vector<std::pair<std::string, MkPack>> g_pack_cache;  // most recent last
+
+std::string pack_key(const MkKeys& mk, int64_t n) {
+    std::string k((const char*)&mk, sizeof mk);
+    k.append((const char*)&n, sizeof n);
+    return k;
+}
+
+bool pack_cache_get(const std::string& key, MkPack* out) {
+    std::lock_guard<std::mutex> g(g_plan_mu);
+    for (auto& e : g_pack_cache)
+        if (e.first == key) {
+            *out = e.second;
+            return true;
+        }
+    return false;
+}
+
+void pack_cache_put(const std::string& key, const MkPack& v) {
+    std::lock_guard<std::mutex> g(g_plan_mu);
+    for (auto& e : g_pack_cache)
+        if (e.first == key) {
+            e.second = v;
+            return;
+        }
+    if (g_pack_cache.size() >= kPlanCacheEntries) g_pack_cache.erase(g_pack_cache.begin());
+    g_pack_cache.emplace_back(key, v);
+}
+}  // namespace
+
 void gb_plan_cache_clear() {
     std::lock_guard<std::mutex> g(g_plan_mu);
     g_plan_cache.clear();
+    g_pack_cache.clear();
 }
 
 // Planning launch -> distinct-key estimate, fixed-point bottoms, table
@@ -5040,8 +5076,15 @@ static int gb_multi_impl(const plgpu_column* keys, int32_t nkeys, const plgpu_co
         // to the exact range pass and a repack.
         MkPack pk;
         int rc = PLGPU_OK;
+        // a repeated query over the same resident key columns reuses the
+        // last packing plan (large inputs; option plan_cache)
+        const bool reuse = options().plan_cache != 0 && n >= (int64_t(1) << 24);
+        const std::string pkey = reuse ? pack_key(mk, n) : std::string();
         if (n >= (int64_t(1) << 20)) {
-            if ((rc = mk_plan_pack_sampled(mk, n, &pk, s))) return rc;
+            if (!(reuse && pack_cache_get(pkey, &pk))) {
+                if ((rc = mk_plan_pack_sampled(mk, n, &pk, s))) return rc;
+                if (reuse && pk.ok) pack_cache_put(pkey, pk);
+            }
             if (pk.ok) {
                 bool repack = false;
                 rc = gb_multi_packed(mk, pk, n, keys, nkeys, cols, ncols, deriv, program, n_instr, aggs, naggs,
@@ -5051,6 +5094,7 @@ static int gb_multi_impl(const plgpu_column* keys, int32_t nkeys, const plgpu_co
         }
         rc = mk_plan_pack(mk, n, nullptr, 0, std::max(hg, 1), &pk, s);
         if (rc) return rc;
+        if (reuse && pk.ok) pack_cache_put(pkey, pk);  // the exact ranges: no repack next time
         if (pk.ok) return gb_multi_packed(mk, pk, n, keys, nkeys, cols, ncols, deriv, program, n_instr, aggs, naggs,
                                           maintain_order, out_keys, out_aggs, info, stream);
     }
