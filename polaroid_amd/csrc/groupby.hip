@@ -289,7 +289,12 @@ __device__ __forceinline__ uint64_t kp_str_code(const uint8_t* data, int64_t dat
     const uint64_t w = b >> 3;
     const int sh = (int)(b & 7) * 8;
     uint64_t x;
-    if ((int64_t)((w + 1) * 8) <= data_end && (sh + 8 * (int)len <= 64 || (int64_t)((w + 2) * 8) <= data_end)) {
+    if ((int64_t)b + 16 <= data_end) {
+        // both words inside the buffer (every row but the last few): a
+        // funnel shift of the pair, no per-row branch on the word boundary
+        const uint64_t lo = dw[w], hi = dw[w + 1];
+        x = (lo >> sh) | ((hi << 1) << (63 - sh));
+    } else if ((int64_t)((w + 1) * 8) <= data_end && (sh + 8 * (int)len <= 64 || (int64_t)((w + 2) * 8) <= data_end)) {
         x = dw[w] >> sh;
         if (sh + 8 * (int)len > 64) x |= dw[w + 1] << (64 - sh);
     } else {
