@@ -249,3 +249,20 @@ def test_sampled_packing_plan(gpu, case):
         k2 = k2.astype(np.uint16)
     cols = _rand_frame(rng, n)
     _check({"k1": (k1, v1), "k2": (k2, None)}, cols, [("sum", "a"), ("len", "b"), ("max", "d")], False)
+
+
+def test_hashed_tuples_between_one_table_and_a_million(gpu, plgpu_option):
+    """~3e5 hashed tuples over 2e6 rows (option no_pack): more groups than
+    one LDS table, fewer than the generic path's million; exact vs the
+    oracle (this flow stays on the global table, DESIGN "Multi-key
+    operators")."""
+    plgpu_option("no_pack", 1)
+    rng = np.random.default_rng(123)
+    n = 2_000_000
+    cols = {"a": (rng.standard_normal(n), None), "b": (rng.integers(-9, 9, n).astype(np.int64), None)}
+    k1 = rng.integers(0, 548, n).astype(np.int64)
+    k2 = rng.integers(0, 548, n).astype(np.int64)
+    info = {}
+    _check({"k1": (k1, None), "k2": (k2, None)}, cols, [("sum", "a"), ("max", "b"), ("len", "a")], False,
+           info=info)
+    assert 200_000 < info["groups"] < 400_000
