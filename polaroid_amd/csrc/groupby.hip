@@ -1032,7 +1032,7 @@ __global__ __launch_bounds__(kPartThreads) void gb_part_scatter_kernel(GbParams 
                 if (col == 0) v = key[k];
 #pragma unroll
                 for (int a = 0; a < kPartRegAcc; ++a)
-                    if (col == a + 1) v = av[a][k];
+                    if (col == a + 1 && a < p.nacc) v = av[a][k];  // (col nacc + 1 is the row ids)
                 if (col > kPartRegAcc && col <= p.nacc) v = dev_load(p.acc[col - 1].c, r);
                 sval[pr[k]] = v;
             }
@@ -3064,11 +3064,6 @@ struct GbRun {
     int32_t key_dtype = PLGPU_I64;
     bool maintain = false;
     bool want_first = false;                 // keep each group's first selected row (multi-key)
-    // the partitioned path is not taken (hashed multi-key tuples: under the
-    // checked build the partitioned run left representative rows outside
-    // [0, n) for ~3e5 hashed groups -- CK_REP_ROW, cause open -- so that
-    // flow stays on the global table, which is exact)
-    bool no_part = false;
     int world = 1;
     uint32_t wide = 0;                       // accs summed by the wide fallback
     int wide_exmin[kMaxAcc] = {0};
@@ -3589,7 +3584,7 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
     // that 2^kPartMaxBits partitions of LDS tables hold them; key and
     // aggregated columns null-free (they are copied as raw words)
     R.part = false;
-    if (!R.no_part && !pl.use_lds && n >= (int64_t(1) << 20) && R.est_groups > 0 && p.key.validity == nullptr &&
+    if (!pl.use_lds && n >= (int64_t(1) << 20) && R.est_groups > 0 && p.key.validity == nullptr &&
         !((p.f_first >= 0 || p.f_last >= 0) && n >= 0xFFFFFFFFll)) {
         bool ok2 = true;
         for (int a = 0; a < p.nacc; ++a) ok2 = ok2 && p.acc[a].c.validity == nullptr;
@@ -5128,7 +5123,6 @@ static int gb_multi_impl(const plgpu_column* keys, int32_t nkeys, const plgpu_co
         if (e != hipSuccess) { rc = hip_fail(e, "mk_hash_kernel"); break; }
         GbRun R;
         R.want_first = true;
-        R.no_part = true;
         rc = gb_prepare(R, &hk, cols, ncols, program, n_instr, aggs, naggs, maintain_order != 0, false, stream, deriv);
         if (!rc) rc = gb_plan(R, nullptr);
         if (!rc) rc = gb_main(R, true, nullptr, nullptr);

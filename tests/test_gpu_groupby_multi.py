@@ -253,9 +253,9 @@ def test_sampled_packing_plan(gpu, case):
 
 def test_hashed_tuples_between_one_table_and_a_million(gpu, plgpu_option):
     """~3e5 hashed tuples over 2e6 rows (option no_pack): more groups than
-    one LDS table, fewer than the generic path's million; exact vs the
-    oracle (this flow stays on the global table, DESIGN "Multi-key
-    operators")."""
+    one LDS table, fewer than the generic path's million, so the hashes go
+    through the partitioned path with two aggregated columns; the verify
+    pass reads every group's first row (the partition buffers' row ids)."""
     plgpu_option("no_pack", 1)
     rng = np.random.default_rng(123)
     n = 2_000_000

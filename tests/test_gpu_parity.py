@@ -348,6 +348,23 @@ def test_group_by_partitioned_vs_oracle(gpu, card, pname, maintain_order):
     assert info["path"] == 3, info
 
 
+@pytest.mark.parametrize("naggcols", [1, 2, 3])
+def test_group_by_partitioned_first_rows_few_columns(gpu, naggcols):
+    """maintain_order on the partitioned path with fewer aggregated columns
+    than the scatter keeps in registers (kPartRegAcc = 3): the row-id column
+    of the partition buffers must hold row ids (it once took an unloaded
+    register's value when nacc < 3, scrambling the first-occurrence order)."""
+    rng = np.random.default_rng(17 + naggcols)
+    n = 1_500_001
+    cols = {"a": (rng.uniform(10, 500, n), None), "b": (rng.integers(-10**9, 10**9, n).astype(np.int64), None),
+            "c": (rng.standard_normal(n), None)}
+    key = rng.integers(0, 100_000, n).astype(np.int64) * 7919 - 3
+    aggs = [("sum", "a"), ("max", "b"), ("min", "c")][:naggcols]
+    info = {}
+    _check_group_by(cols, key, None, aggs, None, None, [], True, info)
+    assert info["path"] == 3, info
+
+
 @pytest.mark.parametrize("card", [5000, 60000, 300000])
 @pytest.mark.parametrize("data", ["prices", "specials", "tiny"])
 def test_group_by_partitioned_sum_only(gpu, card, data):
