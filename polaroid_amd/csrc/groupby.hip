@@ -814,7 +814,7 @@ __global__ __launch_bounds__(kGbThreads) void gb_kernel(GbParams p, DevProgram p
 // independent of the table hashes (hash_slot / g_find use the top bits of a
 // multiplicative hash).  Order inside a partition is irrelevant: every
 // aggregate is order-independent (exact sums, min / max, counts, min row).
-constexpr int kPartMaxBits = 10;
+constexpr int kPartMaxBits = 11;
 constexpr int kPartThreads = 512;
 
 __device__ __forceinline__ uint32_t part_of(uint64_t key, int pbits) {
