@@ -62,6 +62,10 @@ def parse():
     ap.add_argument("--no-sort", action="store_true", help="skip the configs[2] sort + rolling leg")
     ap.add_argument("--no-join", action="store_true", help="skip the configs[3] join leg")
     ap.add_argument("--no-keys", action="store_true", help="skip the Categorical / String / (symbol, day) legs")
+    ap.add_argument("--no-filter", action="store_true", help="skip the filter-only leg (row a1)")
+    ap.add_argument("--no-many-groups", action="store_true", help="skip the many-groups leg")
+    ap.add_argument("--many-groups", type=str, default=",".join(str(g) for g in MANY_GROUPS),
+                    help="comma-separated group counts of the many-groups leg")
     ap.add_argument("--leg-steps", type=int, default=5, help="timed steps of the sort and join legs (<= --steps)")
     ap.add_argument("--dry-run", action="store_true",
                     help="print this rank's launch parameters and exit before touching the GPU (tests)")
@@ -308,6 +312,132 @@ def keys_leg(torch, pl, sym, cols: dict, steps: int, warmup: int, headline_ms: f
         torch.cuda.empty_cache()
     out["note"] = ("bytes_per_row: the fused kernel's algorithmic bytes (categorical: 4 B codes + 32 B; sym_day: "
                    "8 + 4 + 32; string: 8 B offsets + 5 B of bytes + 32)")
+    return out
+
+
+def filter_leg(torch, pl, df, steps: int, warmup: int, cpu_rows: int, cpu_seconds: float, no_cpu: bool) -> dict:
+    """Row a1: `filter(close > 250).collect()` over the headline frame's 5
+    columns (no aggregation): the mask + tile-count pass, the tile scan and
+    the one multi-column scatter (polars-compute/src/filter/mod.rs:18 filter,
+    each column by the one mask).  Algorithmic bytes: the 5 columns read
+    once (40 B/row) and the selected rows written once (40 B each).  rank 0,
+    N = 1."""
+    n = df.height
+
+    def step():
+        return df.filter(pl.col("close") > THRESHOLD).height
+
+    ms, kernels, sel = _time_steps(torch, step, steps, warmup)
+    algo = n * 40 + sel * 40
+    scatter = _leg_roofline(kernels, "filter_scatter8_kernel", n * 40 + n / 8 + sel * 40,
+                            "5 x 8 B read per row + the mask bit, 5 x 8 B written per selected row")
+    mask = _leg_roofline(kernels, "filter_mask_kernel", n * 8 + n / 8,
+                         "8 B predicate read per row + 1 mask bit written")
+    r = {"query": "filter(close > 250).collect() over symbol, open, high, low, close", "rows": n,
+         "rows_selected": sel, "ms_per_step": round(ms, 3), "Mrows_s": round(n / ms / 1e3, 1),
+         "algorithmic_GB": round(algo / 1e9, 2), "step_frac": round(algo / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+         "roofline": scatter, "mask": mask, "kernels": kernels,
+         "note": "step_frac: 5 columns read once + selected rows written once over the step time; roofline: the "
+                 "dominant kernel (the multi-column scatter) at its own algorithmic bytes"}
+    if not no_cpu:
+        from oracle import oracle as O
+
+        threads, cores_note = host_cores()
+        rng = np.random.default_rng(3)
+        c = rng.uniform(10, 490, cpu_rows)
+        hc = [rng.integers(0, 1 << 40, cpu_rows).astype(np.int64)] + [c * rng.uniform(0.99, 1.01, cpu_rows)
+                                                                       for _ in range(3)] + [c]
+        O.baseline_filter(c[:1000], THRESHOLD, [x[:1000] for x in hc], threads)
+        times = []
+        t_end = time.perf_counter() + cpu_seconds
+        while time.perf_counter() < t_end or not times:
+            t0 = time.perf_counter()
+            O.baseline_filter(c, THRESHOLD, hc, threads)
+            times.append(time.perf_counter() - t0)
+        t = float(np.median(times))
+        r["cpu_baseline"] = {"value": round(cpu_rows / t / 1e6, 1), "unit": "Mrows/s", "cores": threads,
+                             "kind": "port",
+                             "sample": f"{cpu_rows:.0e} rows x 5 columns x {len(times)} runs (median), OpenMP "
+                                       f"{threads} threads ({cores_note}), oracle/polars_oracle.c:or_baseline_filter"}
+    return r
+
+
+MANY_GROUPS = (20_000, 600_000, 1_000_000, 10_000_000)
+
+
+def many_groups_leg(torch, pl, cols: dict, steps: int, warmup: int, groups_list, cpu_rows: int,
+                    cpu_seconds: float, no_cpu: bool) -> dict:
+    """The headline query with G random symbols (G = 2e4 ... 1e7) over the
+    same 1e9 price rows: the partitioned path (DESIGN.md "Group-by for many
+    groups") -- count pass, one or two radix scatter passes, then the
+    partitions' LDS aggregation.  Per G: ms per step, the path taken, and
+    each kernel's HBM fraction at its own algorithmic bytes (count: key +
+    predicate read, 8 B key per selected row at level 2; scatter: 40 B read
+    per row + 40 B written per selected row at level 1, 40 + 40 B per
+    selected row at level 2; aggregation: 40 B per selected row).  rank 0,
+    N = 1."""
+    n = cols["close"].numel()
+    dev = cols["close"].device
+    sums = [pl.col(c).sum() for c in ("open", "high", "low", "close")]
+    out = {}
+    for G in groups_list:
+        g = torch.Generator(device=dev)
+        g.manual_seed(G)
+        key = torch.empty(n, dtype=torch.int64, device=dev)
+        chunk = 1 << 26
+        for s0 in range(0, n, chunk):
+            e = min(n, s0 + chunk)
+            key[s0:e] = torch.randint(0, G, (e - s0,), device=dev, generator=g, dtype=torch.int64) * 7919 + 1_000_000
+        df = pl.DataFrame([pl.Series.from_torch("symbol", key)] + [pl.Series.from_torch(k, v) for k, v in cols.items()])
+        q = df.lazy().filter(pl.col("close") > THRESHOLD).group_by("symbol").agg(*sums)
+
+        def step():
+            info = {}
+            res = q.collect(info=info)
+            info["out_groups"] = res.height
+            return info
+
+        ms, kernels, info = _time_steps(torch, step, steps, warmup)
+        sel = int(info.get("rows_selected", 0))
+        levels = int(info.get("part_layout", 0)) >> 8
+        r = {"groups": int(info.get("out_groups", 0)), "ms_per_step": round(ms, 3), "Mrows_s": round(n / ms / 1e3, 1),
+             "path": info.get("path"), "partition_bits": int(info.get("part_layout", 0)) & 0xFF,
+             "scatter_passes": levels, "rows_selected": sel,
+             "step_frac_read_once": round(40 * n / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+        if info.get("path") == 3:
+            r["count"] = _leg_roofline(kernels, "gbp_count_kernel", n * 16 + (sel * 8 if levels == 2 else 0),
+                                       "key + predicate read per row (+ 8 B key per selected row at level 2)")
+            r["scatter"] = _leg_roofline(kernels, "gbp_scatter_kernel",
+                                         n * 40 + sel * 40 + (sel * 80 if levels == 2 else 0),
+                                         "40 B read per row + 40 B written per selected row (+ 40 + 40 B per "
+                                         "selected row at level 2)")
+            r["aggregate"] = _leg_roofline(kernels, "gb_part_agg_kernel", sel * 40, "40 B read per selected row")
+        r["kernels"] = kernels
+        out[str(G)] = r
+        progress(f"many_groups {G}: {r['ms_per_step']} ms per step")
+        del df, q, key
+        torch.cuda.empty_cache()
+    if not no_cpu:
+        from oracle import oracle as O
+
+        threads, cores_note = host_cores()
+        G = 1_000_000
+        rng = np.random.default_rng(5)
+        key = (rng.integers(0, G, cpu_rows) * 7919 + 1_000_000).astype(np.int64)
+        c = rng.uniform(10, 490, cpu_rows)
+        hs = [c * rng.uniform(0.99, 1.01, cpu_rows) for _ in range(3)] + [c]
+        times = []
+        t_end = time.perf_counter() + cpu_seconds
+        while time.perf_counter() < t_end or not times:
+            t0 = time.perf_counter()
+            O.baseline_filter_groupby_sum(key, c, THRESHOLD, hs, threads)
+            times.append(time.perf_counter() - t0)
+        t = float(np.median(times))
+        out["cpu_baseline"] = {"value": round(cpu_rows / t / 1e6, 1), "unit": "Mrows/s", "cores": threads,
+                               "kind": "port",
+                               "sample": f"{cpu_rows:.0e} rows, {G:.0e} random groups x {len(times)} runs (median), "
+                                         f"OpenMP {threads} threads ({cores_note}), "
+                                         "oracle/polars_oracle.c:or_baseline_filter_groupby_sum"}
     return out
 
 
@@ -679,6 +809,18 @@ def main():
     if rank == 0 and world == 1 and not args.no_keys:
         result["keys"] = keys_leg(torch, pl, sym, cols, args.leg_steps * 2, 2, ms_per_step)
         progress("keys leg done")
+    if rank == 0 and world == 1 and not args.no_filter:
+        result["filter"] = filter_leg(torch, pl, df, args.leg_steps, 2, int(args.cpu_rows), args.cpu_seconds / 2,
+                                      args.no_cpu)
+        progress(f"filter leg: {result['filter']['ms_per_step']} ms per step")
+    if rank == 0 and world == 1 and not args.no_many_groups:
+        del query, out
+        query = out = None
+        torch.cuda.empty_cache()
+        result["many_groups"] = many_groups_leg(torch, pl, cols, max(2, args.leg_steps // 2), 1,
+                                                [int(x) for x in args.many_groups.split(",") if x],
+                                                int(args.cpu_rows), args.cpu_seconds / 2, args.no_cpu)
+        progress("many_groups leg done")
     if rank == 0 and world == 1 and not (args.no_sort and args.no_join and args.no_plugin):
         # the remaining legs need the HBM the headline frame holds
         del df, query, out, sym, cols

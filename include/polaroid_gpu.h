@@ -211,7 +211,7 @@ typedef struct plgpu_groupby_info {
     int32_t local_range;         /* 1: range-local fused kernel (clustered keys) */
     int32_t register_runs;       /* 1: fused kernel with per-lane register runs (sorted keys) */
     int32_t key_pack;            /* key columns packed in the fused kernel's registers (0: a key / code column) */
-    int32_t _reserved;
+    int32_t part_layout;         /* partitioned path: partition bits | scatter passes << 8 (0: not partitioned) */
 } plgpu_groupby_info;
 
 /* ---------------------------------------------------------------- basics */
@@ -249,6 +249,13 @@ int plgpu_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream);
  *                 the fused group-by kernel
  *   "local"       -1: the plan decides; 0 keeps the group-by off the
  *                 range-local fused kernel (clustered keys)
+ *   "gb_path"     -1: the plan decides; forces the single-key group-by's
+ *                 path where its inputs allow it: 0 generic kernel on the
+ *                 global table, 1 generic kernel with LDS tables, 2 fused
+ *                 kernel, 3 partitioned (results never depend on it)
+ *   "part_bits"   partitioned group-by: at least this many partition bits
+ *   "part_levels" partitioned group-by: 1 / 2 scatter passes (-1: by the
+ *                 partition bits, two above 8)
  * An unknown name is PLGPU_ERR_INVALID. */
 int plgpu_set_option(const char* name, int64_t value);
 int plgpu_get_option(const char* name, int64_t* out);

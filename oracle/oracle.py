@@ -81,6 +81,9 @@ def lib():
         L.or_baseline_join_inner.restype = C.c_int64
         L.or_baseline_join_inner.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_int64,
                                              C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]
+        L.or_baseline_filter.restype = C.c_int64
+        L.or_baseline_filter.argtypes = [C.c_void_p, C.c_double, C.c_void_p, C.c_int32, C.c_int64, C.c_int32,
+                                         C.c_void_p]
         L.or_float_sum.restype = C.c_double
         L.or_float_sum.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
         L.or_var_welford.restype = C.c_double
@@ -504,6 +507,19 @@ def baseline_filter_groupby_sum(key: np.ndarray, pred: np.ndarray, k: float, sum
     g = lib().or_baseline_filter_groupby_sum(key.ctypes.data, pred.ctypes.data, k, ptrs, len(sums),
                                              key.shape[0], threads, C.byref(chk))
     return int(g), chk.value
+
+
+def baseline_filter(pred: np.ndarray, k: float, cols: list[np.ndarray], threads: int) -> list[np.ndarray]:
+    """CPU baseline of filter(pred > k).collect() (or_baseline_filter): every
+    8-byte column compacted by the mask, row order kept."""
+    n = pred.shape[0]
+    cols = [np.ascontiguousarray(c).view(np.uint64) for c in cols]
+    outs = [np.empty(n, dtype=np.uint64) for _ in cols]
+    ip = (C.c_void_p * len(cols))(*[c.ctypes.data for c in cols])
+    op = (C.c_void_p * len(outs))(*[o.ctypes.data for o in outs])
+    m = lib().or_baseline_filter(np.ascontiguousarray(pred, dtype=np.float64).ctypes.data, k, ip, len(cols), n,
+                                 threads, op)
+    return [o[:m] for o in outs]
 
 
 def baseline_sort_rolling(key: np.ndarray, cols: list[np.ndarray], roll: int, window: int,

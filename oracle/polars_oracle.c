@@ -1765,3 +1765,46 @@ OR_EXPORT double or_var_chunked(const double* x, int64_t n, int32_t ddof) {
     }
     return vs_finalize(&tot, ddof);
 }
+
+/* ------------------------------------------------- CPU baseline: filter */
+/* filter(pred > k).collect() of ncols 8-byte columns on the host cores, as
+ * the reference's FilterExec runs it (polars-mem-engine/src/executors/
+ * filter.rs:70 -> DataFrame::filter, each column by the one mask,
+ * polars-compute/src/filter/mod.rs:18 filter with the primitive kernel of
+ * filter/primitive.rs): the mask is evaluated per thread chunk with
+ * tot_gt (a NaN compares greater), a prefix over the chunks' counts places
+ * each chunk's rows, and every column is compacted in row order.  `out`:
+ * ncols buffers of nrows words.  Returns the selected rows. */
+OR_EXPORT int64_t or_baseline_filter(const double* pred, double k, const uint64_t* const* cols, int32_t ncols,
+                                     int64_t nrows, int32_t threads, uint64_t* const* out) {
+    int T = threads > 0 ? threads : 1;
+    int64_t* cnt = (int64_t*)calloc((size_t)T + 1, sizeof(int64_t));
+#pragma omp parallel num_threads(T)
+    {
+#ifdef _OPENMP
+        int t = omp_get_thread_num();
+#else
+        int t = 0;
+#endif
+        const int64_t lo = nrows * t / T, hi = nrows * (t + 1) / T;
+        int64_t c = 0;
+        for (int64_t r = lo; r < hi; ++r) {
+            const double x = pred[r];
+            c += (isnan(x) || x > k) ? 1 : 0;
+        }
+        cnt[t + 1] = c;
+#pragma omp barrier
+#pragma omp single
+        for (int i = 0; i < T; ++i) cnt[i + 1] += cnt[i];
+        int64_t o = cnt[t];
+        for (int64_t r = lo; r < hi; ++r) {
+            const double x = pred[r];
+            if (!(isnan(x) || x > k)) continue;
+            for (int ci = 0; ci < ncols; ++ci) out[ci][o] = cols[ci][r];
+            ++o;
+        }
+    }
+    const int64_t total = cnt[T];
+    free(cnt);
+    return total;
+}

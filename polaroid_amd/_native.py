@@ -91,7 +91,7 @@ class GroupByInfo(C.Structure):
         ("local_range", C.c_int32),
         ("register_runs", C.c_int32),
         ("key_pack", C.c_int32),
-        ("_reserved", C.c_int32),
+        ("part_layout", C.c_int32),
     ]
 
     def as_dict(self) -> dict:

@@ -355,15 +355,22 @@ static int run_filter(const plgpu_column* cols, int32_t ncols, int src, const De
             return rc;
         }
         const int g = grid_for(ntiles, 1, 256 * 8);
-        if (src == 0)
-            filter_mask_kernel<0><<<g, kFilterThreads, 0, s>>>(ca, dp, md, n, ntiles, mask_words, counts);
-        else if (dp.simple && cols[dp.simple_col].validity == nullptr && dtype_bytes(cols[dp.simple_col].dtype) == 8)
-            filter_mask_kernel<3><<<g, kFilterThreads, 0, s>>>(ca, dp, md, n, ntiles, mask_words, counts);
-        else if (dp.simple)
-            filter_mask_kernel<1><<<g, kFilterThreads, 0, s>>>(ca, dp, md, n, ntiles, mask_words, counts);
-        else
-            filter_mask_kernel<2><<<g, kFilterThreads, 0, s>>>(ca, dp, md, n, ntiles, mask_words, counts);
-        PLGPU_HIP(scan_exclusive<uint32_t>(counts, ntiles, offs, scan_part, s));
+        {
+            KtScope kt("filter_mask_kernel", s);
+            if (src == 0)
+                filter_mask_kernel<0><<<g, kFilterThreads, 0, s>>>(ca, dp, md, n, ntiles, mask_words, counts);
+            else if (dp.simple && cols[dp.simple_col].validity == nullptr &&
+                     dtype_bytes(cols[dp.simple_col].dtype) == 8)
+                filter_mask_kernel<3><<<g, kFilterThreads, 0, s>>>(ca, dp, md, n, ntiles, mask_words, counts);
+            else if (dp.simple)
+                filter_mask_kernel<1><<<g, kFilterThreads, 0, s>>>(ca, dp, md, n, ntiles, mask_words, counts);
+            else
+                filter_mask_kernel<2><<<g, kFilterThreads, 0, s>>>(ca, dp, md, n, ntiles, mask_words, counts);
+        }
+        {
+            KtScope kt("filter_tile_scan", s);
+            PLGPU_HIP(scan_exclusive<uint32_t>(counts, ntiles, offs, scan_part, s));
+        }
         PLGPU_HIP(hipMemcpyAsync(&total, offs + ntiles, 8, hipMemcpyDeviceToHost, s));
         PLGPU_HIP(hipStreamSynchronize(s));
     }
@@ -399,6 +406,7 @@ static int run_filter(const plgpu_column* cols, int32_t ncols, int src, const De
         ++sa.ncols;
     }
     if (!rc && sa.ncols > 0 && total > 0) {
+        KtScope kt("filter_scatter8_kernel", s);
         filter_scatter8_kernel<<<grid_for(ntiles, 1, 256 * 8), kFilterThreads, 0, s>>>(sa, n, ntiles, mask_words,
                                                                                          offs);
         PLGPU_HIP(hipGetLastError());

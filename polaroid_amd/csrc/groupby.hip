@@ -806,248 +806,332 @@ __global__ __launch_bounds__(kGbThreads) void gb_kernel(GbParams p, DevProgram p
 }
 
 // ------------------------------------------------------ partitioned path
-// Keys with more groups than one LDS table holds: the selected rows are
-// first scattered into 2^pbits hash partitions (key, aggregated values and,
-// for the first-row field, the input row id, all widened to 8 bytes), so
-// every partition's groups fit the LDS table of the workgroups that then
-// aggregate it (gb_kernel<0, true, true>).  The partition hash is
-// independent of the table hashes (hash_slot / g_find use the top bits of a
-// multiplicative hash).  Order inside a partition is irrelevant: every
-// aggregate is order-independent (exact sums, min / max, counts, min row).
-constexpr int kPartMaxBits = 11;
-constexpr int kPartThreads = 512;
+// Keys with more groups than one LDS table holds (DESIGN.md "Group-by for
+// many groups"): the selected rows are radix-partitioned by a hash of the
+// key into 2^B partitions of raw 8-byte words (the key, each aggregated
+// column in register form and, for the first / last row fields, the input
+// row id), so that every partition's groups fit the LDS table of the
+// workgroup(s) that then aggregate it.  Up to kPartOneLevel bits take one
+// scatter pass; more take two: B1 = B / 2 bits over the input rows, then
+// B2 = B - B1 bits within each level-1 partition, so each pass keeps runs of
+// >= ~16 rows per partition and column (the reference partitions by
+// polars-utils/src/hashing.rs:72 HashPartitioner before its per-partition
+// hash tables, polars-stream/src/nodes/group_by.rs:85).  The partition hash
+// is independent of the table hashes (hash_slot / g_find take the top bits
+// of a multiplicative hash).  Order inside a partition is irrelevant: every
+// aggregate is order-independent (exact sums, min / max, counts, min / max
+// row).
+//
+// Each pass is a radix-sort pass over (tile, digit) (sort.hip's downsweep
+// structure): a count kernel writes every 4096-row tile's digit counts
+// digit-major, one device scan turns them into output positions, and the
+// scatter kernel ranks its tile's selected rows per wave with ballots (no
+// atomics, no barriers), stages each column in LDS in digit order and
+// writes one run per digit.  Level 2 tiles never straddle a level-1
+// partition: the count matrix is laid out (level-1 partition, digit, tile),
+// so the same one scan places every level-2 run after the runs of the
+// partitions before it.
+constexpr int kPartMaxBits = 16;   // partitions in all
+constexpr int kPartOneLevel = 8;   // up to this many bits: one scatter pass
+constexpr int kPsDigitBits = 8;    // digit bits per scatter pass
+constexpr int kPsThreads = 256;
+constexpr int kPsPer = 16;
+constexpr int kPsTile = kPsThreads * kPsPer;  // 4096 rows; a wave ranks 1024 consecutive rows
 
-__device__ __forceinline__ uint32_t part_of(uint64_t key, int pbits) {
-    return pbits == 0 ? 0u : (uint32_t)(mk_fmix(key ^ 0x2545F4914F6CDD1Dull) >> (64 - pbits));
-}
-
-template <int PRED>
-__device__ __forceinline__ bool part_sel(const GbParams& p, const DevProgram& prog, int64_t r) {
-    if (PRED == 0) return true;
-    if (PRED == 1)
-        return dev_valid(p.pred_col, r) &&
-               simple_pred(prog.simple_isf, prog.simple_op, dev_load(p.pred_col, r), prog.simple_imm);
-    const RowVal rv = eval_row(prog.code, prog.n, p.cols, r);
-    return rv.valid && (rv.v & 1);
-}
-
-// Each partition workgroup of pass 1 / 2 owns one contiguous chunk of rows
-// (a multiple of the tile), so the scan of the partition-major count matrix
-// cnt[q * G + b] gives every (partition, chunk) run its place and pass 2
-// needs no global atomics.
-constexpr int kPartPer = 8;
-constexpr int64_t kPartTile = (int64_t)kPartThreads * kPartPer;  // 4096 rows
-constexpr int kPartRegAcc = 3;
-
-__device__ __forceinline__ void part_chunk(int64_t n, int64_t& lo, int64_t& hi) {
-    const int64_t tiles = (n + kPartTile - 1) / kPartTile;
-    const int64_t per = (tiles + gridDim.x - 1) / gridDim.x;
-    lo = std::min<int64_t>(n, (int64_t)blockIdx.x * per * kPartTile);
-    hi = std::min<int64_t>(n, lo + per * kPartTile);
-}
-
-// A null-free 8-byte column's value at row min(r, hi - 1): a branch-free
-// load, so a thread's loads of a tile all go out together.
-__device__ __forceinline__ uint64_t ld8c(const DevCol& c, int64_t r, int64_t hi) {
-    return __builtin_nontemporal_load((const uint64_t*)c.values + c.offset + (r < hi ? r : hi - 1));
-}
-
-// Pass 1: selected rows per (partition, chunk).  F8: the key and (PRED 1)
-// the predicate column are null-free 8-byte columns.
-template <int PRED, bool F8 = false>
-__global__ __launch_bounds__(kPartThreads) void gb_part_count_kernel(GbParams p, DevProgram prog, int pbits,
-                                                                     uint32_t* __restrict__ cnt) {
-    __shared__ uint32_t h[1 << kPartMaxBits];
-    const int P = 1 << pbits;
-    for (int i = threadIdx.x; i < P; i += blockDim.x) h[i] = 0;
-    __syncthreads();
-    int64_t lo, hi;
-    part_chunk(p.n, lo, hi);
-    if (F8) {
-        for (int64_t base = lo; base < hi; base += kPartTile) {
-            uint64_t key[kPartPer], pv[kPartPer];
-#pragma unroll
-            for (int k = 0; k < kPartPer; ++k) {
-                const int64_t r = base + k * kPartThreads + threadIdx.x;
-                key[k] = ld8c(p.key, r, hi);
-                if (PRED == 1) pv[k] = ld8c(p.pred_col, r, hi);
-            }
-#pragma unroll
-            for (int k = 0; k < kPartPer; ++k) {
-                const int64_t r = base + k * kPartThreads + threadIdx.x;
-                const bool sel =
-                    r < hi && (PRED == 0 || simple_pred(prog.simple_isf, prog.simple_op, pv[k], prog.simple_imm));
-                if (sel) atomicAdd(&h[part_of(key[k], pbits)], 1u);
-            }
-        }
-    } else {
-        for (int64_t r = lo + threadIdx.x; r < hi; r += blockDim.x)
-            if (part_sel<PRED>(p, prog, r)) atomicAdd(&h[part_of(dev_load(p.key, r), pbits)], 1u);
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < P; i += blockDim.x) cnt[(int64_t)i * gridDim.x + blockIdx.x] = h[i];
-}
-
-// Partition boundaries: range[q] = off[q * G] (q = 0..P).
-__global__ void gb_part_bounds_kernel(const uint64_t* __restrict__ off, int P, int G, uint64_t* __restrict__ range) {
-    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q <= P; q += gridDim.x * blockDim.x)
-        range[q] = off[(int64_t)q * G];
-}
+__device__ __forceinline__ uint64_t part_hash(uint64_t key) { return mk_fmix(key ^ 0x2545F4914F6CDD1Dull); }
 
 struct PartOut {
     uint64_t* key;
     uint64_t* acc[kMaxAcc];
-    uint32_t* rows;  // null unless the first-row field is in use
+    uint32_t* rows;  // null unless the first / last row fields are in use
     int64_t cap;     // rows each buffer holds
 };
 
-// Pass 2: per tile of 2048 rows, the selected rows are ranked by partition in
-// LDS (histogram -> block scan -> partition-ordered slots).  Then, column by
-// column (key, each aggregated column, the row ids), the tile's values are
-// read coalesced, placed in LDS at their slots and written out slot by slot,
-// so each partition's rows of the tile leave as one coalesced run per
-// column.  (Writing straight from global memory in slot order made every
-// 128-B line of a column be requested once per row it holds: 27 ms per 1e9
-// rows, request-bound.)
-template <int PRED, bool F8 = false>
-__global__ __launch_bounds__(kPartThreads) void gb_part_scatter_kernel(GbParams p, DevProgram prog, int pbits,
-                                                                       const uint64_t* __restrict__ off, PartOut o) {
-    __shared__ uint32_t h[1 << kPartMaxBits];
-    __shared__ uint32_t lstart[1 << kPartMaxBits];
-    __shared__ uint64_t gcur[1 << kPartMaxBits];
-    __shared__ uint64_t sval[kPartTile];
-    __shared__ uint16_t spart[kPartTile];
-    __shared__ uint64_t wsum[kPartThreads / 64];
-    __shared__ uint32_t tile_sel;
-    const int P = 1 << pbits;
-    constexpr int QPT = (1 << kPartMaxBits) / kPartThreads;  // partitions per thread in the scan
-    for (int i = threadIdx.x; i < P; i += blockDim.x) gcur[i] = off[(int64_t)i * gridDim.x + blockIdx.x];
-    int64_t lo, hi;
-    part_chunk(p.n, lo, hi);
+// Tile geometry of one scatter pass.  Level 1 (range == null): tile t is
+// input rows [t * kPsTile, ...).  Level 2: the tiles of each level-1
+// partition q are tstart[q] .. tstart[q + 1] - 1 (tpart maps a tile back
+// to q), over the partition's rows [range[q], range[q + 1]) of the level-1
+// buffers.  The digit of a key: (part_hash(key) >> sh) & (2^dbits - 1).
+struct PsGeom {
+    int64_t n;
+    int64_t ntiles;
+    const uint64_t* range;
+    const uint32_t* tstart;
+    const uint32_t* tpart;
+    int32_t sh;
+    int32_t dbits;
+};
+
+struct PsTile {
+    int64_t lo, hi;  // rows of the tile
+    int64_t mbase;   // count matrix entry of (tile, digit d): mbase + d * ntq + tl
+    int64_t ntq, tl;
+};
+
+__device__ __forceinline__ PsTile ps_tile(const PsGeom& g, int64_t t) {
+    PsTile x;
+    if (g.range == nullptr) {
+        x.lo = t * kPsTile;
+        x.hi = std::min<int64_t>(g.n, x.lo + kPsTile);
+        x.mbase = 0;
+        x.ntq = g.ntiles;
+        x.tl = t;
+    } else {
+        const uint32_t q = g.tpart[t];
+        const uint32_t t0 = g.tstart[q];
+        x.ntq = (int64_t)(g.tstart[q + 1] - t0);
+        x.tl = t - t0;
+        x.mbase = (int64_t)t0 << g.dbits;
+        x.lo = (int64_t)g.range[q] + x.tl * kPsTile;
+        x.hi = std::min<int64_t>((int64_t)g.range[q + 1], x.lo + kPsTile);
+    }
+    return x;
+}
+
+// Row k of this thread within its tile (c0 + k * 64 + lane, clamped to the
+// tile's last row): f(k, i) for k = 0 .. kPsPer - 1.  A full tile takes the
+// unclamped form, whose offsets are one register plus immediates (with a
+// uniform base pointer: saddr loads, no 64-bit address per row).
+template <typename F>
+__device__ __forceinline__ void ps_rows(const PsTile& tl, int c0, F&& f) {
+    const uint32_t i0 = (uint32_t)(c0 + (int)(threadIdx.x & 63));
+    if (tl.hi - tl.lo == kPsTile) {
+#pragma unroll
+        for (int k = 0; k < kPsPer; ++k) f(k, i0 + (uint32_t)(k * 64));
+    } else {
+        const uint32_t last = (uint32_t)(tl.hi - tl.lo - 1);
+#pragma unroll
+        for (int k = 0; k < kPsPer; ++k) f(k, min(i0 + (uint32_t)(k * 64), last));
+    }
+}
+
+// One column's values at this thread's rows of the tile: the level-1
+// buffers (L2), a null-free 8-byte column (F8) or any column in register
+// form (dev_load).
+template <bool L2, bool F8>
+__device__ __forceinline__ void ps_col(const DevCol& c, const uint64_t* buf, const PsTile& tl, int c0,
+                                       uint64_t (&v)[kPsPer]) {
+    if (L2 || F8) {
+        const uint64_t* b = (L2 ? buf : (const uint64_t*)c.values + c.offset) + tl.lo;
+        ps_rows(tl, c0, [&](int k, uint32_t i) { v[k] = __builtin_nontemporal_load(b + i); });
+    } else {
+        ps_rows(tl, c0, [&](int k, uint32_t i) { v[k] = dev_load(c, tl.lo + (int64_t)i); });
+    }
+}
+
+// The tile's keys (and a simple predicate's column) for this thread's rows,
+// and which rows are selected.  L2: the level-1 buffers (every row
+// selected).  F8: the key and predicate columns are null-free 8-byte
+// columns.
+template <int PRED, bool L2, bool F8>
+__device__ __forceinline__ void ps_keys(const GbParams& p, const DevProgram& prog, const PartOut& in, const PsTile& tl,
+                                        int c0, uint64_t (&key)[kPsPer], uint64_t (&pv)[kPsPer],
+                                        bool (&sel)[kPsPer]) {
+    const int lane = threadIdx.x & 63;
+    ps_col<L2, F8>(p.key, in.key, tl, c0, key);
+    if (!L2 && PRED == 1) ps_col<false, F8>(p.pred_col, nullptr, tl, c0, pv);
+#pragma unroll
+    for (int k = 0; k < kPsPer; ++k) {
+        const int64_t r = tl.lo + c0 + k * 64 + lane;
+        bool s = r < tl.hi;
+        if (!L2 && PRED == 1)
+            s = s && (F8 || dev_valid(p.pred_col, r)) &&
+                simple_pred(prog.simple_isf, prog.simple_op, pv[k], prog.simple_imm);
+        if (!L2 && PRED == 2 && s) {
+            const RowVal rv = eval_row(prog.code, prog.n, p.cols, r);
+            s = rv.valid && (rv.v & 1);
+        }
+        sel[k] = s;
+    }
+}
+
+// Count pass: the selected rows of each tile per digit, written digit-major
+// per level-1 partition (cnt[mbase + d * ntq + tl]).
+template <int PRED, bool L2, bool F8>
+__global__ __launch_bounds__(kPsThreads) void gbp_count_kernel(GbParams p, DevProgram prog, PsGeom g, PartOut in,
+                                                               uint32_t* __restrict__ cnt) {
+    __shared__ uint32_t h[1 << kPsDigitBits];
+    const int P = 1 << g.dbits;
+    const int64_t t = xcd_tile(blockIdx.x, g.ntiles);
+    const PsTile tl = ps_tile(g, t);
+    if (threadIdx.x < P) h[threadIdx.x] = 0;
+    uint64_t key[kPsPer], pv[kPsPer];
+    bool sel[kPsPer];
+    const int c0 = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) * (kPsTile / (kPsThreads / 64));
+    ps_keys<PRED, L2, F8>(p, prog, in, tl, c0, key, pv, sel);
+    __syncthreads();
+    const uint32_t mask = (uint32_t)P - 1;
+#pragma unroll
+    for (int k = 0; k < kPsPer; ++k)
+        if (sel[k]) atomicAdd(&h[(uint32_t)(part_hash(key[k]) >> g.sh) & mask], 1u);
+    __syncthreads();
+    if (threadIdx.x < P) cnt[tl.mbase + (int64_t)threadIdx.x * tl.ntq + tl.tl] = h[threadIdx.x];
+}
+
+// Scatter pass: wave w ranks its 1024 rows of the tile row by row (peer
+// masks from dbits ballots, per-wave digit counters in LDS, no barriers),
+// one block-wide combine turns (wave, digit) counts into tile positions,
+// then column by column the values are staged in LDS in digit order and
+// written out as one run per digit (the next column's loads are issued
+// before this column's write-out).  off: the scanned count matrix.
+template <int PRED, bool L2, bool F8>
+__global__ __launch_bounds__(kPsThreads) void gbp_scatter_kernel(GbParams p, DevProgram prog, PsGeom g, PartOut in,
+                                                                 const uint32_t* __restrict__ off, PartOut o) {
+    constexpr int NW = kPsThreads / 64;
+    constexpr int ND = 1 << kPsDigitBits;
+    __shared__ uint64_t sval[kPsTile];
+    __shared__ uint8_t sdig[kPsTile];
+    __shared__ uint32_t cw[NW][ND];
+    __shared__ uint32_t dstart[ND];
+    __shared__ uint64_t gbase[ND];
+    __shared__ uint64_t wsum[NW];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int P = 1 << g.dbits;
+    const int64_t t = xcd_tile(blockIdx.x, g.ntiles);
+    const PsTile tl = ps_tile(g, t);
+    // this tile's digit offsets (P scattered words): issued first, so their
+    // latency hides behind the key loads and the ranking
+    const uint64_t my_off = tid < P ? (uint64_t)off[tl.mbase + (int64_t)tid * tl.ntq + tl.tl] : 0ull;
+    for (int i = tid; i < NW * ND; i += kPsThreads) cw[i / ND][i % ND] = 0;
+    const int c0 = __builtin_amdgcn_readfirstlane(wid) * (kPsTile / NW);
+    uint64_t key[kPsPer], pv[kPsPer];
+    bool sel[kPsPer];
+    ps_keys<PRED, L2, F8>(p, prog, in, tl, c0, key, pv, sel);
+    __syncthreads();
+    const uint64_t lt = (1ull << lane) - 1;
+    const uint32_t mask = (uint32_t)P - 1;
+    uint32_t rk[kPsPer];  // rank | digit << 16 (then the LDS slot); ~0: not selected
+#pragma unroll
+    for (int k = 0; k < kPsPer; ++k) {
+        const uint32_t d = (uint32_t)(part_hash(key[k]) >> g.sh) & mask;
+        uint64_t peers = __ballot(sel[k]);
+#pragma unroll
+        for (int b = 0; b < kPsDigitBits; ++b) {
+            if (b >= g.dbits) break;
+            const uint64_t bb = __ballot((d >> b) & 1);
+            peers &= ((d >> b) & 1) ? bb : ~bb;
+        }
+        const uint32_t rank = (uint32_t)__popcll(peers & lt);
+        const uint32_t old = cw[wid][d];
+        rk[k] = sel[k] ? ((old + rank) | (d << 16)) : ~0u;
+        // the group's leader bumps the counter (program order within the
+        // wave keeps every peer's read before this write)
+        if (sel[k] && rank == 0) cw[wid][d] = old + (uint32_t)__popcll(peers);
+    }
+    __syncthreads();
+    uint64_t m;  // selected rows of the tile
+    {
+        uint32_t ts = 0;
+        if (tid < P) {
+            for (int w = 0; w < NW; ++w) {
+                const uint32_t c = cw[w][tid];
+                cw[w][tid] = ts;
+                ts += c;
+            }
+        }
+        const uint32_t ds = (uint32_t)block_excl_scan(ts, wsum, m);
+        if (tid < P) {
+            dstart[tid] = ds;
+            gbase[tid] = my_off - ds;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kPsPer; ++k) {
+        if (rk[k] == ~0u) continue;
+        const uint32_t d = rk[k] >> 16;
+        const uint32_t pos = dstart[d] + cw[wid][d] + (rk[k] & 0xFFFFu);
+        sdig[pos] = (uint8_t)d;
+        rk[k] = pos;
+    }
     const int ncols = 1 + p.nacc + (o.rows ? 1 : 0);
-    // (a prefetch of the next tile's F8 loads before this tile's LDS work
-    // measured no faster: 13.6 / 15.9 against 13.4 / 15.0 ms at 1e9 rows,
-    // 64 / 256 partitions)
-    for (int64_t base = lo; base < hi; base += kPartTile) {
-        for (int i = threadIdx.x; i < P; i += blockDim.x) h[i] = 0;
+    // column order: the key, then the predicate's column when it is an
+    // aggregated one (its registers die first), then the rest
+    const int pa = (!L2 && PRED == 1) ? p.pred_acc : -1;
+    auto col_at = [&](int i) -> int {
+        if (pa < 0 || i == 0) return i;
+        if (i == 1) return pa + 1;
+        return i - 1 <= pa ? i - 1 : i;
+    };
+    uint64_t cv[kPsPer];
+#pragma unroll
+    for (int k = 0; k < kPsPer; ++k) cv[k] = key[k];
+#pragma unroll 1
+    for (int ci = 0; ci < ncols; ++ci) {
+        // col 0: key; 1..nacc: aggregated columns; nacc + 1: row ids
+        const int col = col_at(ci);
+#pragma unroll
+        for (int k = 0; k < kPsPer; ++k)
+            if (rk[k] != ~0u) sval[rk[k]] = cv[k];
         __syncthreads();
-        uint32_t pr[kPartPer];
-        uint64_t key[kPartPer];
-        // the first kPartRegAcc aggregated columns are loaded with the key,
-        // so a tile waits for memory once
-        uint64_t av[kPartRegAcc][kPartPer];
-        if (F8) {
-            // null-free 8-byte key / aggregated / predicate columns:
-            // branch-free loads, all of the tile's in flight together
-            uint64_t pv[kPartPer];
+        if (ci + 1 < ncols) {
+            const int nc = col_at(ci + 1);
+            const int a = nc - 1;
+            const bool rows = nc > p.nacc;
+            const bool use_pv = !L2 && PRED == 1 && !rows && a == p.pred_acc;
+            if (use_pv) {
 #pragma unroll
-            for (int a = 0; a < kPartRegAcc; ++a) {
-                if (a >= p.nacc) break;
-#pragma unroll
-                for (int k = 0; k < kPartPer; ++k) av[a][k] = ld8c(p.acc[a].c, base + k * kPartThreads + threadIdx.x, hi);
+                for (int k = 0; k < kPsPer; ++k) cv[k] = pv[k];
+            } else if (rows && L2) {
+                const uint32_t* b = in.rows + tl.lo;
+                ps_rows(tl, c0, [&](int k, uint32_t i) { cv[k] = (uint64_t)__builtin_nontemporal_load(b + i); });
+            } else if (rows) {
+                ps_rows(tl, c0, [&](int k, uint32_t i) { cv[k] = (uint64_t)(tl.lo + (int64_t)i); });
+            } else {
+                ps_col<L2, F8>(p.acc[a].c, L2 ? in.acc[a] : nullptr, tl, c0, cv);
             }
-#pragma unroll
-            for (int k = 0; k < kPartPer; ++k) {
-                const int64_t r = base + k * kPartThreads + threadIdx.x;
-                key[k] = ld8c(p.key, r, hi);
-                if (PRED == 1 && (p.pred_acc < 0 || p.pred_acc >= kPartRegAcc)) pv[k] = ld8c(p.pred_col, r, hi);
-            }
-#pragma unroll
-            for (int k = 0; k < kPartPer; ++k) {
-                const int64_t r = base + k * kPartThreads + threadIdx.x;
-                pr[k] = ~0u;
-                bool sel = r < hi;
-                if (PRED == 1) {
-                    uint64_t x = pv[k];
-#pragma unroll
-                    for (int a = 0; a < kPartRegAcc; ++a)
-                        if (a == p.pred_acc) x = av[a][k];
-                    sel = sel && simple_pred(prog.simple_isf, prog.simple_op, x, prog.simple_imm);
-                }
-                if (sel) {
-                    const uint32_t q = part_of(key[k], pbits);
-                    pr[k] = (q << 16) | atomicAdd(&h[q], 1u);
-                }
+        }
+        if (col <= p.nacc) {
+            uint64_t* dst = col == 0 ? o.key : o.acc[col - 1];
+            for (int q = tid; q < (int)m; q += kPsThreads) {
+                const uint64_t pos = gbase[sdig[q]] + (uint64_t)q;
+                if (gb_ok(pos < (uint64_t)o.cap, CK_PART_POS)) dst[pos] = sval[q];
             }
         } else {
-#pragma unroll
-            for (int a = 0; a < kPartRegAcc; ++a) {
-#pragma unroll
-                for (int k = 0; k < kPartPer; ++k) {
-                    const int64_t r = base + k * kPartThreads + threadIdx.x;
-                    av[a][k] = (a < p.nacc && r < hi) ? dev_load(p.acc[a].c, r) : 0;
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < kPartPer; ++k) {
-                const int64_t r = base + k * kPartThreads + threadIdx.x;
-                key[k] = r < hi ? dev_load(p.key, r) : 0;
-            }
-#pragma unroll
-            for (int k = 0; k < kPartPer; ++k) {
-                const int64_t r = base + k * kPartThreads + threadIdx.x;
-                pr[k] = ~0u;
-                if (r < hi && part_sel<PRED>(p, prog, r)) {
-                    const uint32_t q = part_of(key[k], pbits);
-                    pr[k] = (q << 16) | atomicAdd(&h[q], 1u);
-                }
+            for (int q = tid; q < (int)m; q += kPsThreads) {
+                const uint64_t pos = gbase[sdig[q]] + (uint64_t)q;
+                if (gb_ok(pos < (uint64_t)o.cap, CK_PART_POS)) o.rows[pos] = (uint32_t)sval[q];
             }
         }
         __syncthreads();
-        // exclusive scan of the tile histogram over the partitions
-        uint32_t c[QPT], sum = 0;
-#pragma unroll
-        for (int j = 0; j < QPT; ++j) {
-            const int q = threadIdx.x * QPT + j;
-            c[j] = q < P ? h[q] : 0u;
-            sum += c[j];
+    }
+}
+
+// Level-1 partition of each level-2 tile (tstart: first tile of each of
+// the P1 level-1 partitions, tstart[P1] = tiles).
+__global__ void gbp_tpart_kernel(const uint32_t* __restrict__ tstart, int P1, int64_t ntiles,
+                                 uint32_t* __restrict__ tpart) {
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < ntiles; t += (int64_t)gridDim.x * blockDim.x) {
+        int lo = 0, hi = P1;  // the last q with tstart[q] <= t
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (tstart[mid] <= (uint32_t)t) lo = mid;
+            else hi = mid;
         }
-        uint64_t total;
-        uint32_t run = (uint32_t)block_excl_scan(sum, wsum, total);
-#pragma unroll
-        for (int j = 0; j < QPT; ++j) {
-            const int q = threadIdx.x * QPT + j;
-            if (q < P) lstart[q] = run;
-            run += c[j];
+        tpart[t] = (uint32_t)lo;
+    }
+}
+
+// Partition bounds from a scanned count matrix (in place, u32; total =
+// selected rows).  Level 1: range[d] = off[d * ntiles].  Level 2: range[q *
+// P2 + d] = off[tstart[q] * P2 + d * ntq], or the level-1 partition's start
+// when it has no tile.
+__global__ void gbp_bounds_kernel(const uint32_t* __restrict__ off, const uint64_t* __restrict__ total, int P,
+                                  int64_t ntiles, uint64_t* __restrict__ range) {
+    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q <= P; q += gridDim.x * blockDim.x)
+        range[q] = q < P ? (uint64_t)off[(int64_t)q * ntiles] : *total;
+}
+__global__ void gbp_bounds2_kernel(const uint32_t* __restrict__ off, const uint64_t* __restrict__ range1,
+                                   const uint32_t* __restrict__ tstart, int P1, int b2, uint64_t* __restrict__ range) {
+    const int P = P1 << b2;
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j <= P; j += gridDim.x * blockDim.x) {
+        if (j == P) {
+            range[j] = range1[P1];
+            continue;
         }
-        if (threadIdx.x == 0) tile_sel = (uint32_t)total;
-        __syncthreads();
-        // slot of each selected row (in registers), partition of each slot
-#pragma unroll
-        for (int k = 0; k < kPartPer; ++k) {
-            if (pr[k] == ~0u) continue;
-            const uint32_t q = pr[k] >> 16;
-            const uint32_t slot = lstart[q] + (pr[k] & 0xFFFFu);
-            pr[k] = slot;
-            spart[slot] = (uint16_t)q;
-        }
-        const uint32_t m = tile_sel;
-        for (int col = 0; col < ncols; ++col) {
-            // col 0: key; 1..nacc: aggregated columns; last: row ids
-#pragma unroll
-            for (int k = 0; k < kPartPer; ++k) {
-                if (pr[k] == ~0u) continue;
-                const int64_t r = base + k * kPartThreads + threadIdx.x;
-                uint64_t v = (uint64_t)r;
-                if (col == 0) v = key[k];
-#pragma unroll
-                for (int a = 0; a < kPartRegAcc; ++a)
-                    if (col == a + 1 && a < p.nacc) v = av[a][k];  // (col nacc + 1 is the row ids)
-                if (col > kPartRegAcc && col <= p.nacc) v = dev_load(p.acc[col - 1].c, r);
-                sval[pr[k]] = v;
-            }
-            __syncthreads();
-            uint64_t* dst = col == 0 ? o.key : (col <= p.nacc ? o.acc[col - 1] : nullptr);
-            for (uint32_t t = threadIdx.x; t < m; t += blockDim.x) {
-                const uint32_t q = spart[t];
-                const uint64_t pos = gcur[q] + (t - lstart[q]);
-                if (!gb_ok(pos < (uint64_t)o.cap, CK_PART_POS)) continue;
-                if (dst) dst[pos] = sval[t];
-                else o.rows[pos] = (uint32_t)sval[t];
-            }
-            __syncthreads();
-        }
-        for (int i = threadIdx.x; i < P; i += blockDim.x) gcur[i] += h[i];
+        const int q = j >> b2, d = j & ((1 << b2) - 1);
+        const int64_t ntq = (int64_t)(tstart[q + 1] - tstart[q]);
+        range[j] = ntq > 0 ? (uint64_t)off[((int64_t)tstart[q] << b2) + (int64_t)d * ntq] : range1[q];
     }
 }
 
@@ -3081,6 +3165,7 @@ struct GbRun {
     int pbits = 0;
     int part_lbits = 0;
     int part_blocks = 1;
+    int part_levels = 0;                     // scatter passes taken (info)
     uint64_t* pbuf = nullptr;
     uint64_t* prange = nullptr;              // scan of the count matrix + partition bounds
     const uint64_t* part_range = nullptr;    // P + 1 partition boundaries (inside prange)
@@ -3471,6 +3556,7 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
             if (rc) return rc;
             hipError_t e = hipMemsetAsync(regs, 0, h.size() * 4, R.s);
             if (e == hipSuccess) {
+                KtScope kt("gb_hll_kernel", R.s);
                 gb_hll_kernel<<<num_cus() * 4, 256, 0, R.s>>>(p.key, n, regs);
                 e = hipGetLastError();
             }
@@ -3486,6 +3572,22 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
         }
     }
     size_tables(&pl, R.st[ST_DISTINCT], R.st[ST_SAMPLED], &R.gbits, hll, &R.est_groups);
+    // forced paths (option gb_path, tests): LDS tables on or off; the
+    // fused-kernel and partitioned choices follow below
+    const int gpath = options().gb_path;
+    if (gpath == 0) {
+        pl.use_lds = false;
+        pl.lds_bytes = 0;
+    } else if ((gpath == 1 || gpath == 2) && !pl.use_lds) {
+        // the largest table one workgroup per CU holds; keys beyond it take
+        // the global table
+        int lb = 12;
+        while (lb > 6 && (size_t)p.nfields * ((1u << lb) + 2) * 8 > 160 * 1024) --lb;
+        pl.use_lds = true;
+        p.lbits = lb;
+        p.lcap = 1 << lb;
+        pl.lds_bytes = (size_t)p.nfields * (p.lcap + 2) * 8;
+    }
     // range-local mode: too many keys for one LDS table over the column, but
     // few within each contiguous row range (the plan's per-range sample
     // count ST_LOCAL: a range's samples repeat their keys); the fused kernel
@@ -3496,7 +3598,7 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
     const int lbits0 = p.lbits, lcap0 = p.lcap;
     const size_t lds0 = pl.lds_bytes;
     {
-        if (!pl.use_lds && clustered) {
+        if (!pl.use_lds && clustered && gpath < 0) {
             const int lb = log2_ceil(std::max<int64_t>(64, 2 * (int64_t)local));
             const size_t bytes = (size_t)p.nfields * ((1u << lb) + 2) * 8;
             if (bytes <= (size_t)160 * 1024) {
@@ -3533,6 +3635,7 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
         if (p.acc[a].dop != DOP_NONE && !(p.acc[a].dop & DOP_LIT)) fast = fast && ok(p.acc[a].c2);
     }
     if (R.pred == 1 && p.pred_acc < 0) fast = fast && ok(p.pred_col);
+    if (gpath == 0 || gpath == 1 || gpath == 3) fast = false;
     if (pl.local && !fast) {
         // the generic kernel walks the rows grid-strided: no range-local table
         pl.local = pl.use_lds = false;
@@ -3582,12 +3685,12 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
     p.row_begin = p.n_full > 0 ? n : 0;
     // partitioned path: too many groups for one LDS table, but few enough
     // that 2^kPartMaxBits partitions of LDS tables hold them; key and
-    // aggregated columns null-free (they are copied as raw words)
+    // aggregated columns null-free (they are copied as raw words); the
+    // u32 count matrix and row ids bound n below 2^32
     R.part = false;
-    if (!pl.use_lds && n >= (int64_t(1) << 20) && R.est_groups > 0 && p.key.validity == nullptr &&
-        !((p.f_first >= 0 || p.f_last >= 0) && n >= 0xFFFFFFFFll)) {
-        bool ok2 = true;
-        for (int a = 0; a < p.nacc; ++a) ok2 = ok2 && p.acc[a].c.validity == nullptr;
+    bool part_ok = n > 0 && n < 0xFFFFFFFFll && R.est_groups > 0 && p.key.validity == nullptr;
+    for (int a = 0; a < p.nacc; ++a) part_ok = part_ok && p.acc[a].c.validity == nullptr;
+    if (part_ok && ((gpath < 0 && !pl.use_lds && n >= (int64_t(1) << 20)) || gpath == 3)) {
         // LDS table of the partition workgroups: two per CU, or one when
         // 2^kPartMaxBits partitions of the smaller table are not enough
         const int64_t want = R.est_groups + (R.est_groups >> 3);
@@ -3598,15 +3701,16 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
         // Fewer, larger partition tables first (160 KB, one workgroup per
         // CU): measured 2-7 % faster than 80 KB tables at 14k-100k groups
         // (profiles/r02_ab_part.log)
+        const int min_pb = std::min(kPartMaxBits, std::max(0, options().part_bits));
         for (size_t budget : {(size_t)160 * 1024, (size_t)80 * 1024}) {
             int lb = 13;
             while (lb > 6 && ((size_t)fields * ((1u << lb) + 2) * 8 > budget ||
                               (size_t)p.nfields * ((1u << lb) + 2) * 8 > (size_t)160 * 1024))
                 --lb;
             const int64_t per = (int64_t(1) << lb) / 2;  // groups per partition at load 1/2
-            int pb = 0;
+            int pb = min_pb;
             while (pb < kPartMaxBits && want > (per << pb)) ++pb;
-            if (ok2 && want <= (per << pb)) {
+            if (want <= (per << pb)) {
                 R.part = true;
                 R.pbits = pb;
                 R.part_lbits = lb;
@@ -3631,67 +3735,173 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
 }
 
 // Scatter the selected rows into the hash partitions (once per run; the
-// attempts of gb_main reuse them).
+// attempts of gb_main reuse them): one pass of 2^pbits digits, or two
+// (level 1 over the input rows, level 2 within each level-1 partition).
+template <int PRED, bool L2, bool F8>
+static hipError_t gbp_pass(const GbRun& R, const PsGeom& g, const PartOut& in, uint32_t* cnt, uint64_t* part,
+                           bool scatter, const PartOut& out) {
+    hipStream_t s = R.s;
+    const unsigned grid = (unsigned)g.ntiles;
+    if (!scatter) {
+        {
+            KtScope kt("gbp_count_kernel", s);
+            gbp_count_kernel<PRED, L2, F8><<<grid, kPsThreads, 0, s>>>(R.pl.p, R.dp, g, in, cnt);
+        }
+        hipError_t e = hipGetLastError();
+        if (e == hipSuccess) e = scan_exclusive32_inplace(cnt, g.ntiles << g.dbits, part, s);
+        return e;
+    }
+    {
+        KtScope kt("gbp_scatter_kernel", s);
+        gbp_scatter_kernel<PRED, L2, F8><<<grid, kPsThreads, 0, s>>>(R.pl.p, R.dp, g, in, cnt, out);
+    }
+    return hipGetLastError();
+}
+
+static hipError_t gbp_pass1(const GbRun& R, bool f8, const PsGeom& g, uint32_t* cnt, uint64_t* part, bool scatter,
+                            const PartOut& out) {
+    PartOut none;
+    std::memset(&none, 0, sizeof none);
+    if (f8 && R.pred == 0) return gbp_pass<0, false, true>(R, g, none, cnt, part, scatter, out);
+    if (f8 && R.pred == 1) return gbp_pass<1, false, true>(R, g, none, cnt, part, scatter, out);
+    switch (R.pred) {
+    case 0: return gbp_pass<0, false, false>(R, g, none, cnt, part, scatter, out);
+    case 1: return gbp_pass<1, false, false>(R, g, none, cnt, part, scatter, out);
+    default: return gbp_pass<2, false, false>(R, g, none, cnt, part, scatter, out);
+    }
+}
+
+// Partition buffers for `rows` selected rows: key, nacc columns, row ids.
+static int gbp_alloc(GbRun& R, int64_t sel, uint64_t** buf, PartOut* o) {
+    const GbParams& p = R.pl.p;
+    // even, so every column's buffer starts 16-byte aligned (pair loads)
+    const int64_t rows = ((int64_t)std::max<int64_t>(sel, 2) + 3) & ~int64_t(1);
+    const bool want_rows = p.f_first >= 0 || p.f_last >= 0;
+    const size_t words = (size_t)rows * (1 + p.nacc) + (want_rows ? ((size_t)rows + 1) / 2 : 0);
+    int rc = dev_alloc((void**)buf, words * 8, R.s);
+    if (rc) return rc;
+    std::memset(o, 0, sizeof *o);
+    o->key = *buf;
+    for (int a = 0; a < p.nacc; ++a) o->acc[a] = *buf + (size_t)rows * (1 + a);
+    o->rows = want_rows ? (uint32_t*)(*buf + (size_t)rows * (1 + p.nacc)) : nullptr;
+    o->cap = rows;
+    return PLGPU_OK;
+}
+
 static int gb_partition(GbRun& R) {
     GbParams& p = R.pl.p;
     hipStream_t s = R.s;
-    const int P = 1 << R.pbits;
-    const int G = num_cus() * 8;
-    const int64_t ncnt = (int64_t)P * G;
-    uint32_t* cnt = nullptr;
-    uint64_t* part = nullptr;
-    int rc = dev_alloc((void**)&cnt, ncnt * 4, s);
-    if (!rc) rc = dev_alloc((void**)&R.prange, (ncnt + 1 + P + 1) * 8, s);
-    if (!rc) rc = dev_alloc((void**)&part, ((ncnt + kScanChunk - 1) / kScanChunk + 1) * 8, s);
-    uint64_t* off = R.prange;
-    uint64_t* range = R.prange + ncnt + 1;
-    std::vector<uint64_t> hr(P + 1);
+    const int B = R.pbits;
+    const int lv = options().part_levels;
+    const bool two = B >= 2 && (B > kPartOneLevel || lv == 2) && !(lv == 1 && B <= kPartOneLevel);
+    const int b1 = two ? B / 2 : B, b2 = B - b1;
+    const int P1 = 1 << b1, P = 1 << B;
     // the fast forms: null-free 8-byte key, aggregated and predicate columns
     auto c8 = [](const DevCol& c) { return c.validity == nullptr && dtype_bytes(c.dtype) == 8 && c.dtype != PLGPU_STR; };
     bool f8 = c8(p.key) && R.pred <= 1 && (R.pred == 0 || c8(p.pred_col));
-    for (int a = 0; a < p.nacc && a < kPartRegAcc; ++a) f8 = f8 && c8(p.acc[a].c);
+    for (int a = 0; a < p.nacc; ++a) f8 = f8 && c8(p.acc[a].c);
+    PsGeom g1;
+    std::memset(&g1, 0, sizeof g1);
+    g1.n = p.n;
+    g1.ntiles = (p.n + kPsTile - 1) / kPsTile;
+    g1.sh = b1 ? 64 - b1 : 0;
+    g1.dbits = b1;
+    const int64_t ncnt1 = g1.ntiles << b1;
+    uint32_t* cnt = nullptr;
+    uint64_t* part = nullptr;
+    // final bounds (P + 1), then the level-1 bounds (P1 + 1) of a two-pass run
+    int rc = dev_alloc((void**)&R.prange, (size_t)(P + 1 + (two ? P1 + 1 : 0)) * 8, s);
+    uint64_t* range = R.prange;
+    uint64_t* range1 = two ? R.prange + P + 1 : range;
+    if (!rc) rc = dev_alloc((void**)&cnt, (size_t)ncnt1 * 4, s);
+    if (!rc) rc = dev_alloc((void**)&part, (size_t)((ncnt1 + kScanChunk - 1) / kScanChunk + 2) * 8, s);
+    std::vector<uint64_t> hr1((size_t)P1 + 1);
     if (!rc) {
-        if (f8 && R.pred == 0) gb_part_count_kernel<0, true><<<G, kPartThreads, 0, s>>>(p, R.dp, R.pbits, cnt);
-        else if (f8 && R.pred == 1) gb_part_count_kernel<1, true><<<G, kPartThreads, 0, s>>>(p, R.dp, R.pbits, cnt);
-        else switch (R.pred) {
-        case 0: gb_part_count_kernel<0><<<G, kPartThreads, 0, s>>>(p, R.dp, R.pbits, cnt); break;
-        case 1: gb_part_count_kernel<1><<<G, kPartThreads, 0, s>>>(p, R.dp, R.pbits, cnt); break;
-        default: gb_part_count_kernel<2><<<G, kPartThreads, 0, s>>>(p, R.dp, R.pbits, cnt); break;
-        }
-        hipError_t e = hipGetLastError();
-        if (e == hipSuccess) e = scan_exclusive<uint32_t>(cnt, ncnt, off, part, s);
+        hipError_t e = gbp_pass1(R, f8, g1, cnt, part, false, R.pout);
+        const int64_t nb = std::max<int64_t>(1, (ncnt1 + kScanChunk - 1) / kScanChunk);
         if (e == hipSuccess) {
-            gb_part_bounds_kernel<<<(P + 256) / 256, 256, 0, s>>>(off, P, G, range);
+            gbp_bounds_kernel<<<(P1 + 256) / 256, 256, 0, s>>>(cnt, part + nb, P1, g1.ntiles, range1);
             e = hipGetLastError();
         }
-        if (e == hipSuccess) e = hipMemcpyAsync(hr.data(), range, (P + 1) * 8, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(hr1.data(), range1, (size_t)(P1 + 1) * 8, hipMemcpyDeviceToHost, s);
         if (e == hipSuccess) e = hipStreamSynchronize(s);
-        if (e != hipSuccess) rc = hip_fail(e, "gb_part_count_kernel");
+        if (e != hipSuccess) rc = hip_fail(e, "gbp_count_kernel");
+    }
+    uint64_t* buf1 = nullptr;
+    PartOut out1;
+    if (!rc) rc = gbp_alloc(R, (int64_t)hr1[P1], &buf1, &out1);
+    if (!rc) {
+        const hipError_t e = gbp_pass1(R, f8, g1, cnt, part, true, out1);
+        if (e != hipSuccess) rc = hip_fail(e, "gbp_scatter_kernel");
     }
     dev_free(cnt, s);
     dev_free(part, s);
-    if (rc) return rc;
+    cnt = nullptr;
+    part = nullptr;
+    if (rc) {
+        dev_free(buf1, s);
+        return rc;
+    }
+    std::vector<uint64_t> hr;
+    if (!two) {
+        R.pbuf = buf1;
+        R.pout = out1;
+        hr = hr1;
+    } else {
+        // level 2: the tiles of each level-1 partition
+        std::vector<uint32_t> ts((size_t)P1 + 1);
+        uint64_t t = 0;
+        for (int q = 0; q < P1; ++q) {
+            ts[q] = (uint32_t)t;
+            t += (hr1[q + 1] - hr1[q] + kPsTile - 1) / kPsTile;
+        }
+        ts[P1] = (uint32_t)t;
+        PsGeom g2;
+        std::memset(&g2, 0, sizeof g2);
+        g2.ntiles = (int64_t)t;
+        g2.range = range1;
+        g2.sh = 64 - B;
+        g2.dbits = b2;
+        const int64_t ncnt2 = g2.ntiles << b2;
+        uint32_t* meta = nullptr;
+        rc = dev_alloc((void**)&meta, (size_t)(P1 + 1 + std::max<int64_t>(g2.ntiles, 1)) * 4, s);
+        if (!rc) rc = dev_alloc((void**)&cnt, (size_t)std::max<int64_t>(ncnt2, 1) * 4, s);
+        if (!rc) rc = dev_alloc((void**)&part, (size_t)((ncnt2 + kScanChunk - 1) / kScanChunk + 2) * 8, s);
+        hr.resize((size_t)P + 1);
+        if (!rc) {
+            g2.tstart = meta;
+            g2.tpart = meta + P1 + 1;
+            hipError_t e = hipMemcpyAsync(meta, ts.data(), ts.size() * 4, hipMemcpyHostToDevice, s);
+            if (e == hipSuccess && g2.ntiles > 0) {
+                gbp_tpart_kernel<<<(unsigned)std::min<int64_t>((g2.ntiles + 255) / 256, 4096), 256, 0, s>>>(
+                    meta, P1, g2.ntiles, meta + P1 + 1);
+                e = hipGetLastError();
+            }
+            if (e == hipSuccess && g2.ntiles > 0) e = gbp_pass<0, true, true>(R, g2, out1, cnt, part, false, out1);
+            if (e == hipSuccess) {
+                gbp_bounds2_kernel<<<(P + 256) / 256, 256, 0, s>>>(cnt, range1, meta, P1, b2, range);
+                e = hipGetLastError();
+            }
+            if (e == hipSuccess) e = hipMemcpyAsync(hr.data(), range, (size_t)(P + 1) * 8, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e != hipSuccess) rc = hip_fail(e, "gbp_count_kernel (level 2)");
+        }
+        if (!rc) rc = gbp_alloc(R, (int64_t)hr[P], &R.pbuf, &R.pout);
+        if (!rc && g2.ntiles > 0) {
+            const hipError_t e = gbp_pass<0, true, true>(R, g2, out1, cnt, part, true, R.pout);
+            if (e != hipSuccess) rc = hip_fail(e, "gbp_scatter_kernel (level 2)");
+        }
+        dev_free(cnt, s);
+        dev_free(part, s);
+        dev_free(meta, s);
+        dev_free(buf1, s);
+        if (rc) return rc;
+    }
     uint64_t maxpart = 0;
     for (int q = 0; q < P; ++q) maxpart = std::max<uint64_t>(maxpart, hr[q + 1] - hr[q]);
-    // even, so every column's buffer starts 16-byte aligned (pair loads)
-    const int64_t rows = ((int64_t)std::max<uint64_t>(hr[P], 2) + 3) & ~int64_t(1);
     R.part_rows_total = (int64_t)hr[P];
-    const bool want_rows = p.f_first >= 0 || p.f_last >= 0;
-    const size_t words = (size_t)rows * (1 + p.nacc) + (want_rows ? ((size_t)rows + 1) / 2 : 0);
-    if ((rc = dev_alloc((void**)&R.pbuf, words * 8, s))) return rc;
-    R.pout.key = R.pbuf;
-    for (int a = 0; a < p.nacc; ++a) R.pout.acc[a] = R.pbuf + (size_t)rows * (1 + a);
-    R.pout.rows = want_rows ? (uint32_t*)(R.pbuf + (size_t)rows * (1 + p.nacc)) : nullptr;
-    R.pout.cap = rows;
-    if (f8 && R.pred == 0) gb_part_scatter_kernel<0, true><<<G, kPartThreads, 0, s>>>(p, R.dp, R.pbits, off, R.pout);
-    else if (f8 && R.pred == 1) gb_part_scatter_kernel<1, true><<<G, kPartThreads, 0, s>>>(p, R.dp, R.pbits, off, R.pout);
-    else switch (R.pred) {
-    case 0: gb_part_scatter_kernel<0><<<G, kPartThreads, 0, s>>>(p, R.dp, R.pbits, off, R.pout); break;
-    case 1: gb_part_scatter_kernel<1><<<G, kPartThreads, 0, s>>>(p, R.dp, R.pbits, off, R.pout); break;
-    default: gb_part_scatter_kernel<2><<<G, kPartThreads, 0, s>>>(p, R.dp, R.pbits, off, R.pout); break;
-    }
-    PLGPU_HIP(hipGetLastError());
     R.part_range = range;
+    R.part_levels = two ? 2 : 1;
     // workgroups per partition: fill the chip (4 per CU over all partitions,
     // profiles/r02_ab_part.log), bound rows per workgroup
     const int64_t wpc = 4;
@@ -3865,6 +4075,7 @@ static int gb_main(GbRun& R, bool auto_refit, bool* refit, int32_t* hint) {
         for (int a = 0; a < kMaxAcc; ++a) p.bottom[a] = R.hb[a];
         PLGPU_HIP(hipEventRecord(ev0, R.s));
         if (n > 0 && R.part) {
+            KtScope kt("gb_part_agg_kernel", R.s);
             PLGPU_HIP(launch_partitioned(R));
         } else if (n > 0) {
             // the fused kernel covers every row (its last tile masked); off
@@ -3974,6 +4185,7 @@ static void gb_fill_info(const GbRun& R, plgpu_groupby_info* info) {
     info->local_range = R.pl.local ? 1 : 0;
     info->register_runs = p.n_full > 0 && !R.part && R.pl.launched_runs ? 1 : 0;
     info->key_pack = p.kp.n;
+    info->part_layout = R.part ? (R.pbits | (R.part_levels << 8)) : 0;
     for (int a = 0; a < p.nacc; ++a)
         if (((R.st[ST_FXFLAGS] >> (2 * a)) & 2u) && !((R.wide >> a) & 1u)) info->sum_inexact |= 1 << a;
 }
@@ -4779,6 +4991,14 @@ PLGPU_API int plgpu_gb_merge_sources(const void* records, int32_t n_sources, con
 // column whose base is a value of its type.
 static void kp_span(KeyPack& k, int i) {
     const int bits = k.bits[i];
+    if (bits >= 64) {
+        // identity field (one key whose extended value is the code): every
+        // value fits, whatever its sign
+        k.span[i] = ~0ull;
+        k.mode[i] = (k.c[i].dtype == PLGPU_I32 || k.c[i].dtype == PLGPU_U32) ? 2 : 0;  // widened
+        k.span32[i] = 0xFFFFFFFFu;
+        return;
+    }
     const uint64_t mask = bits >= 64 ? ~0ull : (1ull << bits) - 1;
     const uint64_t ordb = k.base[i] ^ 0x8000000000000000ull;
     k.span[i] = std::min<uint64_t>(mask, ~0ull - ordb);
@@ -5068,9 +5288,12 @@ static int gb_multi_impl(const plgpu_column* keys, int32_t nkeys, const plgpu_co
         pk.n = 1;
         pk.ok = 1;
         pk.bits[0] = 64;
+        // (nothing lies outside a 64-bit identity field, so no repack; if
+        // one were ever reported, the exact packing below takes over)
         bool repack = false;
-        return gb_multi_packed(mk, pk, n, keys, nkeys, cols, ncols, deriv, program, n_instr, aggs, naggs,
-                               maintain_order, out_keys, out_aggs, info, stream, true, &repack);
+        const int rc = gb_multi_packed(mk, pk, n, keys, nkeys, cols, ncols, deriv, program, n_instr, aggs, naggs,
+                                       maintain_order, out_keys, out_aggs, info, stream, true, &repack);
+        if (rc || !repack) return rc;
     }
     const int hg = (int)std::min<int64_t>((n + 255) / 256, (int64_t)num_cus() * 16);
     {

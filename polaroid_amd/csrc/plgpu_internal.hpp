@@ -44,6 +44,12 @@ struct Options {
     int fuse_keys = 1;   // 0: packed multi-key codes go through a code column (tests / A-B)
     int plan_cache = 1;  // 0: every group-by samples its inputs (no reuse of recent plan statistics)
     int grid_rounds = 0; // fused group-by grid in rounds of resident workgroups (0: kGridRounds; A-B)
+    // group-by path hooks (tests: the forced-path parity sweep, DESIGN.md
+    // "Group-by paths"): -1 lets the plan choose
+    int gb_path = -1;     // 0 generic kernel on the global table, 1 generic with LDS tables,
+                          // 2 fused kernel, 3 partitioned (where the inputs allow it)
+    int part_bits = -1;   // partitioned path: at least this many partition bits
+    int part_levels = -1; // partitioned path: 1 / 2 scatter passes (-1: by the partition bits)
 };
 Options& options();
 
@@ -59,16 +65,20 @@ Options& options();
 void gb_plan_cache_clear();
 hipEvent_t ev_acquire();
 void ev_release(hipEvent_t e);
-int kt_begin(const char* name, hipStream_t s);
-void kt_end(int slot, hipStream_t s);
+// A scope owns its event pair until it ends; only then does the pair join
+// the pending list that plgpu_ktime_read drains, so a read from another
+// thread never sees (or recycles) a scope that is still open.
+bool kt_begin(hipStream_t s, hipEvent_t* a, hipEvent_t* b);
+void kt_end(const char* name, hipEvent_t a, hipEvent_t b, hipStream_t s);
 struct KtScope {
-    int slot = -1;
+    const char* name;
+    hipEvent_t a = nullptr, b = nullptr;
     hipStream_t s;
-    KtScope(const char* name, hipStream_t st) : s(st) {
-        if (options().ktime) slot = kt_begin(name, st);
+    KtScope(const char* nm, hipStream_t st) : name(nm), s(st) {
+        if (options().ktime && !kt_begin(st, &a, &b)) a = b = nullptr;
     }
     ~KtScope() {
-        if (slot >= 0) kt_end(slot, s);
+        if (a) kt_end(name, a, b, s);
     }
     KtScope(const KtScope&) = delete;
     KtScope& operator=(const KtScope&) = delete;

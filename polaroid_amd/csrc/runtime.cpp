@@ -40,21 +40,40 @@ hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 // (PLGPU_<NAME>, an integer) when the library loads, and settable through
 // plgpu_set_option.  No measurement variant lives here: losing A/B variants
 // leave the product once their numbers are logged.
+// name, environment variable and field of every option
+namespace {
+struct OptField {
+    const char* name;
+    const char* env;
+    int Options::*f;
+};
+const OptField kOptFields[] = {
+    {"debug", "PLGPU_DEBUG", &Options::debug},
+    {"no_pack", "PLGPU_NO_PACK", &Options::no_pack},
+    {"mk_collide", "PLGPU_MK_COLLIDE", &Options::mk_collide},
+    {"runs", "PLGPU_RUNS", &Options::runs},
+    {"local", "PLGPU_LOCAL", &Options::local},
+    {"ktime", "PLGPU_KTIME", &Options::ktime},
+    {"fuse_keys", "PLGPU_FUSE_KEYS", &Options::fuse_keys},
+    {"grid_rounds", "PLGPU_GRID_ROUNDS", &Options::grid_rounds},
+    {"plan_cache", "PLGPU_PLAN_CACHE", &Options::plan_cache},
+    {"gb_path", "PLGPU_GB_PATH", &Options::gb_path},
+    {"part_bits", "PLGPU_PART_BITS", &Options::part_bits},
+    {"part_levels", "PLGPU_PART_LEVELS", &Options::part_levels},
+};
+const OptField* opt_field(const char* name) {
+    for (const OptField& f : kOptFields)
+        if (!strcmp(name, f.name)) return &f;
+    return nullptr;
+}
+}  // namespace
+
 static Options read_env_options() {
     Options o;
-    auto get = [](const char* name, int def) {
-        const char* e = getenv(name);
-        return e ? atoi(e) : def;
-    };
-    o.debug = get("PLGPU_DEBUG", 0);
-    o.no_pack = get("PLGPU_NO_PACK", 0);
-    o.mk_collide = get("PLGPU_MK_COLLIDE", 0);
-    o.runs = get("PLGPU_RUNS", -1);
-    o.local = get("PLGPU_LOCAL", -1);
-    o.ktime = get("PLGPU_KTIME", 0);
-    o.fuse_keys = get("PLGPU_FUSE_KEYS", 1);
-    o.grid_rounds = get("PLGPU_GRID_ROUNDS", 0);
-    o.plan_cache = get("PLGPU_PLAN_CACHE", 1);
+    for (const OptField& f : kOptFields) {
+        const char* e = getenv(f.env);
+        if (e) o.*(f.f) = atoi(e);
+    }
     return o;
 }
 
@@ -104,22 +123,23 @@ void ev_release(hipEvent_t e) {
     g_kt_pool.push_back(e);
 }
 
-int kt_begin(const char* name, hipStream_t s) {
+bool kt_begin(hipStream_t s, hipEvent_t* a, hipEvent_t* b) {
     std::lock_guard<std::mutex> g(g_kt_mu);
-    hipEvent_t a = kt_event(), b = kt_event();
-    if (a == nullptr || b == nullptr || hipEventRecord(a, s) != hipSuccess) {
-        if (a) g_kt_pool.push_back(a);
-        if (b) g_kt_pool.push_back(b);
-        return -1;
+    *a = kt_event();
+    *b = kt_event();
+    if (*a == nullptr || *b == nullptr || hipEventRecord(*a, s) != hipSuccess) {
+        if (*a) g_kt_pool.push_back(*a);
+        if (*b) g_kt_pool.push_back(*b);
+        *a = *b = nullptr;
+        return false;
     }
-    g_kt_pending.push_back({name, a, b});
-    return (int)g_kt_pending.size() - 1;
+    return true;
 }
 
-void kt_end(int slot, hipStream_t s) {
+void kt_end(const char* name, hipEvent_t a, hipEvent_t b, hipStream_t s) {
     std::lock_guard<std::mutex> g(g_kt_mu);
-    if (slot < 0 || slot >= (int)g_kt_pending.size()) return;
-    (void)hipEventRecord(g_kt_pending[slot].b, s);
+    (void)hipEventRecord(b, s);
+    g_kt_pending.push_back({name, a, b});
 }
 
 // Caching device allocator.  Blocks come from hipMalloc and are recycled
@@ -829,35 +849,17 @@ PLGPU_API int plgpu_expr_dtype(const plgpu_column* cols, int32_t ncols, const pl
 
 PLGPU_API int plgpu_set_option(const char* name, int64_t value) {
     if (name == nullptr) return fail(PLGPU_ERR_INVALID, "option name is NULL");
-    Options& o = options();
-    int* f = nullptr;
-    if (!strcmp(name, "debug")) f = &o.debug;
-    else if (!strcmp(name, "no_pack")) f = &o.no_pack;
-    else if (!strcmp(name, "mk_collide")) f = &o.mk_collide;
-    else if (!strcmp(name, "runs")) f = &o.runs;
-    else if (!strcmp(name, "local")) f = &o.local;
-    else if (!strcmp(name, "ktime")) f = &o.ktime;
-    else if (!strcmp(name, "fuse_keys")) f = &o.fuse_keys;
-    else if (!strcmp(name, "grid_rounds")) f = &o.grid_rounds;
-    else if (!strcmp(name, "plan_cache")) f = &o.plan_cache;
+    const OptField* f = opt_field(name);
     if (f == nullptr) return fail(PLGPU_ERR_INVALID, std::string("unknown option ") + name);
-    *f = (int)value;
+    options().*(f->f) = (int)value;
     return PLGPU_OK;
 }
 
 PLGPU_API int plgpu_get_option(const char* name, int64_t* out) {
     if (name == nullptr || out == nullptr) return fail(PLGPU_ERR_INVALID, "NULL argument");
-    const Options& o = options();
-    if (!strcmp(name, "debug")) *out = o.debug;
-    else if (!strcmp(name, "no_pack")) *out = o.no_pack;
-    else if (!strcmp(name, "mk_collide")) *out = o.mk_collide;
-    else if (!strcmp(name, "runs")) *out = o.runs;
-    else if (!strcmp(name, "local")) *out = o.local;
-    else if (!strcmp(name, "ktime")) *out = o.ktime;
-    else if (!strcmp(name, "fuse_keys")) *out = o.fuse_keys;
-    else if (!strcmp(name, "grid_rounds")) *out = o.grid_rounds;
-    else if (!strcmp(name, "plan_cache")) *out = o.plan_cache;
-    else return fail(PLGPU_ERR_INVALID, std::string("unknown option ") + name);
+    const OptField* f = opt_field(name);
+    if (f == nullptr) return fail(PLGPU_ERR_INVALID, std::string("unknown option ") + name);
+    *out = options().*(f->f);
     return PLGPU_OK;
 }
 

@@ -199,6 +199,9 @@ __global__ __launch_bounds__(256) void mk_sample_range_kernel(MkKeys k, int64_t 
 // holds exactly for base <= v < base + 2^bits (a v below base wraps past
 // 2^64 - 1 - ord(base), ord(x) = x ^ 2^63), base = minv - nullable.
 __device__ __forceinline__ uint64_t mk_span(const MkPack& pk, int i) {
+    // a 64-bit field (the identity plan of one key: the sign- or
+    // zero-extended value is the code) holds every value
+    if (pk.bits[i] >= 64) return ~0ull;
     const uint64_t mask = pk.bits[i] >= 64 ? ~0ull : (1ull << pk.bits[i]) - 1;
     const uint64_t ordb = ((uint64_t)pk.minv[i] - (pk.nullable[i] ? 1u : 0u)) ^ 0x8000000000000000ull;
     return mask < ~0ull - ordb ? mask : ~0ull - ordb;

@@ -1,0 +1,177 @@
+"""Many groups (round 5): the partitioned group-by over 2^B hash partitions,
+one scatter pass (B <= 8) or two (level 1 over the input, level 2 within
+each level-1 partition), exact against the oracle: keys, first-occurrence
+order under maintain_order, and every aggregate bit for bit.
+
+* 1e6 and 1e7 random groups, 1-4 aggregated columns, with and without the
+  predicate and maintain_order (the sizes the plan sends to two passes);
+* the partition bits and pass count forced (options gb_path = 3, part_bits,
+  part_levels) over the same frame, every form bitwise equal to the oracle;
+* program predicates and 4-byte key / value columns (the scatter's generic
+  loads), Int64 extremes as keys.
+
+Reference: polars-stream/src/nodes/group_by.rs:75 flush_evictions, :85
+add_pre_agg (hash-partitioned pre-aggregation), polars-utils/src/
+hashing.rs:72 HashPartitioner.
+"""
+
+import numpy as np
+import pytest
+
+import polaroid_amd as pl
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+I64_MIN = np.iinfo(np.int64).min
+I64_MAX = np.iinfo(np.int64).max
+
+
+def _bits(a):
+    return np.asarray(a, dtype=np.float64).view(np.uint64)
+
+
+def _ohlc(rng, n):
+    close = rng.uniform(10.0, 500.0, n)
+    return {
+        "open": close * rng.uniform(0.99, 1.01, n),
+        "high": close * rng.uniform(1.0, 1.02, n),
+        "low": close * rng.uniform(0.98, 1.0, n),
+        "close": close,
+    }
+
+
+# (1, col, 0) load column, (2, 0, x) f64 literal, (24, 0, 0) greater-than
+def _gt_prog(ci, x):
+    return [(1, ci, 0), (2, 0, x), (24, 0, 0)]
+
+
+def _expected(cols, key, aggs, prog_names, prog):
+    names = list(dict.fromkeys([c for _, c in aggs] + list(prog_names)))
+    hc = [O.HostCol(cols[c], None) for c in names]
+    p = prog(names) if prog else None
+    return O.group_by_agg(O.HostCol(key, None), hc, p, [(kind, names.index(c)) for kind, c in aggs], key.shape[0],
+                          O.SUM_EXACT)
+
+
+def _gpu(cols, key, aggs, pred, maintain):
+    data = {"k": pl.Series.from_numpy("k", key)}
+    for c, v in cols.items():
+        data[c] = pl.Series.from_numpy(c, v)
+    lf = pl.DataFrame(data).lazy()
+    if pred is not None:
+        lf = lf.filter(pred)
+    info = {}
+    out = lf.group_by("k", maintain_order=maintain).agg(
+        *[getattr(pl.col(c), kind)().alias(f"{kind}_{c}") for kind, c in aggs]).collect(info=info)
+    return out, info
+
+
+def _compare(out, exp, aggs, maintain):
+    okeys, okvalid, oouts = exp
+    gk = out["k"].to_numpy().astype(np.int64)
+    assert gk.shape[0] == okeys.shape[0]
+    assert out["k"].validity_numpy().all() and okvalid.all()
+    if maintain:
+        go = oo = slice(None)
+    else:
+        go, oo = np.argsort(gk, kind="stable"), np.argsort(okeys, kind="stable")
+    assert np.array_equal(gk[go], okeys[oo])
+    for (kind, c), (ov, ovalid) in zip(aggs, oouts):
+        s = out[f"{kind}_{c}"]
+        gv, gvalid = s.to_numpy()[go], s.validity_numpy()[go]
+        ov, ovalid = ov[oo], ovalid[oo]
+        assert np.array_equal(gvalid, ovalid), (kind, c)
+        if ov.dtype == np.float64:
+            assert np.array_equal(_bits(gv)[ovalid], _bits(ov)[ovalid]), (kind, c)
+        else:
+            assert np.array_equal(gv[ovalid].astype(np.int64), ov[ovalid].astype(np.int64)), (kind, c)
+
+
+MANY = [
+    # groups, aggregated columns, fused predicate, maintain_order
+    (1_000_000, [("sum", "close")], False, True),
+    (1_000_000, [("sum", "open"), ("sum", "high"), ("sum", "low"), ("sum", "close")], True, False),
+    (1_000_000, [("sum", "close"), ("min", "low"), ("max", "high"), ("len", "close")], True, True),
+    (10_000_000, [("sum", "open"), ("mean", "close")], True, True),
+    (10_000_000, [("sum", "open"), ("sum", "high"), ("sum", "low"), ("sum", "close")], True, False),
+]
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("case", range(len(MANY)))
+def test_many_groups_exact(gpu, case):
+    groups, aggs, pred, maintain = MANY[case]
+    rng = np.random.default_rng(100 + case)
+    n = 3 * groups
+    # random keys: ~0.95 of the key space occurs at 3 rows per key
+    key = rng.integers(0, groups, n).astype(np.int64) * 7919 - 3 * groups
+    cols = _ohlc(rng, n)
+    exp = _expected(cols, key, aggs, ["close"] if pred else [],
+                    (lambda names: _gt_prog(names.index("close"), 250.0)) if pred else None)
+    out, info = _gpu(cols, key, aggs, (pl.col("close") > 250.0) if pred else None, maintain)
+    assert info["path"] == 3, info
+    assert info["part_layout"] >> 8 == 2, info   # two scatter passes
+    _compare(out, exp, aggs, maintain)
+
+
+FORCED = [(0, 1), (1, 1), (6, 1), (8, 1), (4, 2), (9, 2), (12, 2), (16, 2)]
+
+
+@pytest.mark.parametrize("card", [300, 20_000, 200_000])
+@pytest.mark.parametrize("maintain", [False, True])
+def test_partition_bits_and_passes_forced(gpu, card, maintain, plgpu_option):
+    """The same frame through every forced partition layout (bits, passes),
+    with sum-only and mixed aggregations, each bitwise equal to the oracle."""
+    rng = np.random.default_rng(card + maintain)
+    n = 1_500_001
+    key = rng.integers(0, card, n).astype(np.int64) * 1_000_003 - 7
+    key[rng.random(n) < 0.001] = I64_MIN
+    key[rng.random(n) < 0.001] = I64_MAX
+    cols = _ohlc(rng, n)
+    cols["vol"] = rng.integers(-10**12, 10**12, n).astype(np.int64)
+    cols["close"][rng.random(n) < 0.0005] = np.nan
+    cols["open"][rng.random(n) < 0.0005] = -np.inf
+    agg_sets = [
+        [("sum", "open"), ("sum", "high"), ("mean", "close")],
+        [("sum", "close"), ("min", "low"), ("max", "vol"), ("sum", "vol"), ("count", "high"), ("len", "open")],
+    ]
+    for aggs in agg_sets:
+        exp = _expected(cols, key, aggs, ["close"], lambda names: _gt_prog(names.index("close"), 250.0))
+        for bits, levels in FORCED:
+            plgpu_option("gb_path", 3)
+            plgpu_option("part_bits", bits)
+            plgpu_option("part_levels", levels)
+            out, info = _gpu(cols, key, aggs, pl.col("close") > 250.0, maintain)
+            assert info["path"] == 3, (bits, levels, info)
+            got_bits, got_levels = info["part_layout"] & 0xFF, info["part_layout"] >> 8
+            assert got_bits >= bits and got_levels == (2 if (levels == 2 or got_bits > 8) and got_bits >= 2 else 1), \
+                (bits, levels, info)
+            _compare(out, exp, aggs, maintain)
+
+
+@pytest.mark.parametrize("levels", [1, 2])
+def test_partitioned_program_predicate_and_narrow_columns(gpu, levels, plgpu_option):
+    """A program predicate (evaluated per row in the count and scatter
+    passes) and 4-byte key / value columns (the scatter's generic loads)."""
+    rng = np.random.default_rng(7 + levels)
+    n = 1_200_003
+    key = rng.integers(-40_000, 40_000, n).astype(np.int32)
+    cols = {"a": rng.standard_normal(n) * 100, "b": rng.integers(-50, 50, n).astype(np.int32),
+            "d": rng.uniform(-5, 5, n)}
+    aggs = [("sum", "a"), ("max", "b"), ("sum", "b"), ("min", "d"), ("len", "a")]
+    # ((a * 2 + b) > d): the oracle's program over names [a, b, d]
+    prog = [(1, 0, 0), (3, 0, 2), (12, 0, 0), (1, 1, 0), (10, 0, 0), (1, 2, 0), (24, 0, 0)]
+    names = ["a", "b", "d"]
+    hc = [O.HostCol(cols[c], None) for c in names]
+    exp = O.group_by_agg(O.HostCol(key, None), hc, prog, [(kind, names.index(c)) for kind, c in aggs], n,
+                         O.SUM_EXACT)
+    plgpu_option("gb_path", 3)
+    plgpu_option("part_bits", 10 if levels == 2 else 7)
+    plgpu_option("part_levels", levels)
+    for maintain in (False, True):
+        out, info = _gpu(cols, key, aggs, (pl.col("a") * 2 + pl.col("b")) > pl.col("d"), maintain)
+        assert info["path"] == 3 and info["part_layout"] >> 8 == levels, info
+        assert out["k"].dtype == pl.Int32
+        okeys, okvalid, oouts = exp
+        _compare(out, (okeys.astype(np.int64), okvalid, oouts), aggs, maintain)

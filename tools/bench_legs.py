@@ -1,5 +1,5 @@
 """One of bench.py's resident-frame legs alone (for profilers): the
-headline, vwap or std query over configs[1]'s 1e9-row frame.
+headline, vwap, std, filter or many_groups (--groups G random symbols) query over configs[1]'s 1e9-row frame.
 
     python tools/bench_legs.py --leg vwap [--rows 1e9 --steps 5 --warmup 2]
 """
@@ -14,7 +14,7 @@ sys.path.insert(0, ROOT)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--leg", choices=["headline", "vwap", "std"], required=True)
+    ap.add_argument("--leg", choices=["headline", "vwap", "std", "filter", "many_groups"], required=True)
     ap.add_argument("--rows", type=float, default=1e9)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
@@ -30,6 +30,11 @@ def main():
     df = pl.DataFrame([pl.Series.from_torch("symbol", sym)] + [pl.Series.from_torch(c, t) for c, t in cols.items()])
     if args.leg == "vwap":
         r = bench.vwap_leg(torch, pl, df, sym, cols["close"], args.steps, args.warmup)
+    elif args.leg == "filter":
+        r = bench.filter_leg(torch, pl, df, args.steps, args.warmup, 0, 0.0, True)
+    elif args.leg == "many_groups":
+        del df
+        r = bench.many_groups_leg(torch, pl, cols, args.steps, args.warmup, [args.groups], 0, 0.0, True)
     elif args.leg == "std":
         r = bench.std_leg(torch, pl, df, args.steps, args.warmup)
     else:
