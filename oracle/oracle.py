@@ -84,6 +84,9 @@ def lib():
         L.or_baseline_filter.restype = C.c_int64
         L.or_baseline_filter.argtypes = [C.c_void_p, C.c_double, C.c_void_p, C.c_int32, C.c_int64, C.c_int32,
                                          C.c_void_p]
+        L.or_rolling_var.restype = None
+        L.or_rolling_var.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                     C.c_void_p, C.c_void_p]
         L.or_float_sum.restype = C.c_double
         L.or_float_sum.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
         L.or_var_welford.restype = C.c_double
@@ -493,6 +496,20 @@ def rolling(col: HostCol, kind: str, window_size: int, min_periods: int | None =
     isint = k in (1, 3, 4) and col.code != F64
     vals = (oi if isint else of)[:n].copy()
     return vals, ov[:n].astype(bool)
+
+
+def rolling_var(col: HostCol, window_size: int, min_periods: int | None = None, center: bool = False,
+                ddof: int = 1, std: bool = False, mode: int = ROLLING_REFERENCE):
+    """rolling_var / rolling_std -> (values, valid).  mode 0 restates the
+    reference's MomentWindow<VarianceMoment> (a sliding Welford VarState);
+    mode 1 is the exact form the GPU computes (or_rolling_var)."""
+    n = col.c.length
+    mp = window_size if min_periods is None else min_periods
+    of = np.zeros(max(n, 1), np.float64)
+    ov = np.zeros(max(n, 1), np.uint8)
+    lib().or_rolling_var(C.byref(col.c), window_size, mp, int(center), ddof, int(std), mode, of.ctypes.data,
+                         ov.ctypes.data)
+    return of[:n].copy(), ov[:n].astype(bool)
 
 
 def fsum(x: np.ndarray) -> float:

@@ -1808,3 +1808,196 @@ OR_EXPORT int64_t or_baseline_filter(const double* pred, double k, const uint64_
     free(cnt);
     return total;
 }
+
+/* ------------------------------------------------- rolling var / std */
+/* Mode 0 restates the reference: polars-compute/src/rolling/moment.rs:138
+ * MomentWindow<VarianceMoment> (:16) -- a VarState (polars-compute/src/
+ * moment.rs:87 insert_one, :99 remove_one, :126 finalize) slid over the
+ * window (reset when the new window starts past the old one's end, :228);
+ * a non-finite value enters as 0.0 and is counted apart, and any makes the
+ * result NaN (:196); nulls are skipped (nulls/moment.rs, moment.rs:255);
+ * the result is null when fewer than min_periods non-null values are in
+ * the window (no_nulls/mod.rs:61, nulls/mod.rs:73) or weight <= ddof
+ * (moment.rs:127); rolling_std is its square root (polars-time/src/
+ * chunkedarray/rolling_window/dispatch.rs:526).
+ *
+ * Mode 1 is the exact form the GPU computes: with c the window's non-null
+ * count, var = (RN(c * sum x^2 - (sum x)^2) / c) / (c - ddof), the
+ * numerator formed exactly (big integer over the window's smallest
+ * exponent) and rounded once -- the group-by's fused variance
+ * (groupby.hip var_exact) applied to each window. */
+static void vs_remove(vs_t* s, double x) {
+    const double nw = s->w - 1.0;
+    const double dm = x - s->mean;
+    const double nm = s->mean - dm / nw;
+    s->dp -= (x - nm) * dm;
+    s->w = nw;
+    s->mean = nm;
+    vs_zero_nan(s);
+}
+
+#define RV_LIMBS 80 /* 5120 bits: c * sum t^2 for any f64 span, c < 2^16 */
+typedef struct { uint64_t w[RV_LIMBS]; } rv_big;
+
+static void rvb_add_shifted(rv_big* a, unsigned __int128 v, int sh, int negate) {
+    /* a += (negate ? -1 : 1) * (v << sh), two's complement over RV_LIMBS */
+    const int ws = sh / 64, bs = sh % 64;
+    const uint64_t lo = (uint64_t)v, hi = (uint64_t)(v >> 64);
+    uint64_t parts[3];
+    parts[0] = bs ? lo << bs : lo;
+    parts[1] = bs ? (hi << bs) | (lo >> (64 - bs)) : hi;
+    parts[2] = bs ? hi >> (64 - bs) : 0;
+    uint64_t carry = 0;
+    for (int i = ws; i < RV_LIMBS; ++i) {
+        const int k = i - ws;
+        const uint64_t d = k < 3 ? parts[k] : 0;
+        if (k >= 3 && carry == 0) break;
+        if (!negate) {
+            const unsigned __int128 t = (unsigned __int128)a->w[i] + d + carry;
+            a->w[i] = (uint64_t)t;
+            carry = (uint64_t)(t >> 64);
+        } else {
+            const unsigned __int128 t = (unsigned __int128)a->w[i] - d - carry;
+            a->w[i] = (uint64_t)t;
+            carry = (uint64_t)(t >> 64) ? 1 : 0; /* borrow */
+        }
+    }
+}
+
+/* x (>= 0) * 2^e rounded to nearest-even f64 (subnormals included). */
+static double rvb_to_double(const rv_big* a, int e) {
+    int top = RV_LIMBS - 1;
+    while (top >= 0 && a->w[top] == 0) --top;
+    if (top < 0) return 0.0;
+    const int p = top * 64 + 63 - __builtin_clzll(a->w[top]); /* leading bit */
+    /* keep bits down to position q: 53 significant bits, fewer when the
+     * result is subnormal (bit q weighs 2^(q + e) >= 2^-1074) */
+    int q = p - 52;
+    if (q + e < -1074) q = -1074 - e;
+    if (q <= 0) return ldexp((double)a->w[0], e); /* exact: < 2^53 */
+    uint64_t keep = 0;
+    for (int b = p; b >= q; --b) keep = (keep << 1) | ((a->w[b / 64] >> (b % 64)) & 1);
+    const int rb = q - 1;
+    const int round = (int)((a->w[rb / 64] >> (rb % 64)) & 1);
+    int sticky = 0;
+    for (int b = 0; b < rb && !sticky; ++b) sticky = (int)((a->w[b / 64] >> (b % 64)) & 1);
+    if (round && (sticky || (keep & 1))) ++keep;
+    return ldexp((double)keep, q + e);
+}
+
+/* Exact variance of the finite values xs[0..m) (c = m + nonfinite is the
+ * count), the GPU's rounding: (RN(c sum t^2 - (sum t)^2) / c) / (c - ddof). */
+static double rv_exact(const double* xs, int64_t m, int64_t c, int32_t ddof) {
+    int emin = 1 << 20;
+    for (int64_t i = 0; i < m; ++i) {
+        if (xs[i] == 0.0) continue;
+        int ex;
+        (void)frexp(xs[i], &ex);
+        const int e0 = ex - 53; /* xs[i] = t * 2^e0 with |t| < 2^53 */
+        if (e0 < emin) emin = e0;
+    }
+    if (emin < -1074) emin = -1074;
+    if (emin == 1 << 20) return 0.0; /* every value zero */
+    rv_big sq, s1;
+    memset(&sq, 0, sizeof sq);
+    memset(&s1, 0, sizeof s1);
+    for (int64_t i = 0; i < m; ++i) {
+        if (xs[i] == 0.0) continue;
+        int ex;
+        const double fr = frexp(fabs(xs[i]), &ex);
+        const uint64_t t = (uint64_t)ldexp(fr, 53); /* |x| = t * 2^(ex - 53) */
+        int sh = ex - 53 - emin;
+        uint64_t tt = t;
+        if (sh < 0) { tt = t >> (-sh); sh = 0; } /* subnormal: exact (low bits zero) */
+        /* t^2 << 2 sh into sq; t << sh into s1 (signed) */
+        rvb_add_shifted(&sq, (unsigned __int128)tt * tt, 2 * sh, 0);
+        rvb_add_shifted(&s1, tt, sh, xs[i] < 0);
+    }
+    /* num = c * sq - s1^2 */
+    rv_big num;
+    memset(&num, 0, sizeof num);
+    for (int i = 0; i < RV_LIMBS; ++i) {
+        if (sq.w[i] == 0) continue;
+        rvb_add_shifted(&num, (unsigned __int128)sq.w[i] * (uint64_t)c, 64 * i, 0);
+    }
+    const int neg1 = (int64_t)s1.w[RV_LIMBS - 1] < 0;
+    if (neg1) { /* |s1| */
+        unsigned __int128 carry = 1;
+        for (int i = 0; i < RV_LIMBS; ++i) {
+            const unsigned __int128 s = (unsigned __int128)(~s1.w[i]) + carry;
+            s1.w[i] = (uint64_t)s;
+            carry = s >> 64;
+        }
+    }
+    for (int i = 0; i < RV_LIMBS; ++i) {
+        if (s1.w[i] == 0) continue;
+        for (int j = 0; j < RV_LIMBS && i + j < RV_LIMBS; ++j) {
+            if (s1.w[j] == 0) continue;
+            rvb_add_shifted(&num, (unsigned __int128)s1.w[i] * s1.w[j], 64 * (i + j), 1);
+        }
+    }
+    if ((int64_t)num.w[RV_LIMBS - 1] < 0) return 0.0; /* cannot happen: c sum t^2 >= (sum t)^2 */
+    const double nr = rvb_to_double(&num, 2 * emin);
+    return (nr / (double)c) / (double)(c - ddof);
+}
+
+OR_EXPORT void or_rolling_var(const plgpu_column* c, int64_t ws, int64_t min_periods, int32_t center, int32_t ddof,
+                              int32_t std, int32_t mode, double* out, uint8_t* out_valid) {
+    const int64_t n = c->length;
+    int has_nulls = 0;
+    for (int64_t r = 0; r < n && !has_nulls; ++r) has_nulls = !col_valid(c, r);
+    vs_t st;
+    memset(&st, 0, sizeof st);
+    int64_t nonfinite = 0, nulls = 0, last_start = 0, last_end = 0;
+    double* buf = (double*)malloc(sizeof(double) * (size_t)(ws > 0 ? ws : 1));
+    for (int64_t i = 0; i < n; ++i) {
+        int64_t s, e;
+        rl_offsets(i, ws, n, center, &s, &e);
+        double v = 0.0;
+        int valid = 0;
+        if (mode == 0) {
+            if (!has_nulls && e - s < min_periods) {
+                out[i] = 0.0;
+                out_valid[i] = 0;
+                continue;
+            }
+            if (s >= last_end) {
+                memset(&st, 0, sizeof st);
+                nonfinite = nulls = 0;
+                last_start = last_end = s;
+            }
+            for (int64_t r = last_start; r < s; ++r) {
+                if (!col_valid(c, r)) { --nulls; continue; }
+                const double x = rl_val(c, r);
+                if (isfinite(x)) vs_remove(&st, x);
+                else { vs_remove(&st, 0.0); --nonfinite; }
+            }
+            for (int64_t r = last_end; r < e; ++r) {
+                if (!col_valid(c, r)) { ++nulls; continue; }
+                const double x = rl_val(c, r);
+                if (isfinite(x)) vs_insert(&st, x);
+                else { vs_insert(&st, 0.0); ++nonfinite; }
+            }
+            last_start = s;
+            last_end = e;
+            const int some = st.w > (double)ddof;
+            valid = some && (e - s) - nulls >= min_periods;
+            if (valid) v = nonfinite > 0 ? NAN : vs_finalize(&st, ddof);
+        } else {
+            int64_t m = 0, cnt = 0, nf = 0;
+            for (int64_t r = s; r < e; ++r) {
+                if (!col_valid(c, r)) continue;
+                ++cnt;
+                const double x = rl_val(c, r);
+                if (isfinite(x)) buf[m++] = x;
+                else ++nf;
+            }
+            valid = cnt >= min_periods && cnt > ddof;
+            if (valid) v = nf > 0 ? NAN : rv_exact(buf, m, cnt, ddof);
+        }
+        if (valid && std) v = sqrt(v);
+        out[i] = valid ? v : 0.0;
+        out_valid[i] = (uint8_t)valid;
+    }
+    free(buf);
+}

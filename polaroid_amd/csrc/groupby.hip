@@ -188,6 +188,9 @@ struct GbParams {
     // contiguous tiles [b * tiles_per_wg, (b + 1) * tiles_per_wg); 0 = the
     // grid-strided tile order
     int32_t tiles_per_wg;
+    // partitioned run with one workgroup per partition: each partition's
+    // groups live in a region of 2^rbits global slots (g_slot); 0 = off
+    int32_t rbits;
     KeyPack kp;             // fused key packing (kp.n > 0): the key is the packed tuple code
 };
 
@@ -342,28 +345,59 @@ __device__ __forceinline__ int lds_find(uint64_t* lkeys, int lbits, int lcap, ui
     return -1;
 }
 
-// Global probe: slot index or -1.  A plain load may return a stale EMPTY
+// Partition hash of the many-groups path (its top bits pick the partition;
+// independent of the table hashes, which multiply by the golden ratio).
+__device__ __forceinline__ uint64_t part_hash(uint64_t key) { return mk_fmix(key ^ 0x2545F4914F6CDD1Dull); }
+
+// Probe i of `key` in the global table.  A partitioned run whose partitions
+// each have one workgroup (p.rbits > 0) keeps every partition's groups in a
+// region of its own, 2^rbits slots at region index = the partition (the
+// partition hash's top gbits - rbits bits), probed with the LDS table's hash:
+// the partition's workgroup then writes its LDS table into the region slot
+// for slot (DESIGN.md "Group-by for many groups").
+__device__ __forceinline__ uint64_t g_slot(const GbParams& p, uint64_t key, uint64_t i) {
+    if (p.rbits > 0) {
+        const int qb = p.gbits - p.rbits;
+        const uint64_t q = qb > 0 ? part_hash(key) >> (64 - qb) : 0ull;
+        const uint64_t rm = (1ull << p.rbits) - 1;
+        return (q << p.rbits) | (((uint64_t)hash_slot(key, p.rbits) + i) & rm);
+    }
+    const uint64_t h = p.gbits == 0 ? 0 : ((key * 0x9E3779B97F4A7C15ull) >> (64 - p.gbits));
+    return (h + i) & ((uint64_t)p.gcap - 1);
+}
+__device__ __forceinline__ int g_probe_limit(const GbParams& p) {
+    const int64_t span = p.rbits > 0 ? (int64_t(1) << p.rbits) : p.gcap;
+    return span < kGlobalProbe ? (int)span : kGlobalProbe;
+}
+
+// Global probe: slot index or -1; `inserted` when this call claimed the
+// slot (the caller counts new keys, one atomic per wave: a per-key add to
+// one status word serialises).  A plain load may return a stale EMPTY
 // (another CU inserted since); the CAS then returns the true key, so the
 // protocol never needs an acquire: keys only ever go EMPTY -> key.
-__device__ __forceinline__ int64_t g_find(const GbParams& p, uint64_t key) {
+__device__ __forceinline__ int64_t g_find_ins(const GbParams& p, uint64_t key, bool& inserted) {
     uint64_t* gkeys = p.gtab;
-    const uint64_t mask = (uint64_t)p.gcap - 1;
-    const uint64_t h = p.gbits == 0 ? 0 : ((key * 0x9E3779B97F4A7C15ull) >> (64 - p.gbits));
-    const int lim = p.gcap < kGlobalProbe ? (int)p.gcap : kGlobalProbe;
+    const int lim = g_probe_limit(p);
     for (int i = 0; i < lim; ++i) {
-        const uint64_t s = (h + (uint64_t)i) & mask;
+        const uint64_t s = g_slot(p, key, (uint64_t)i);
         uint64_t k = __hip_atomic_load(&gkeys[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (k == key) return (int64_t)s;
         if (k == kEmptyKey) {
             k = atomicCAS((unsigned long long*)&gkeys[s], (unsigned long long)kEmptyKey, (unsigned long long)key);
             if (k == kEmptyKey) {
-                atomicAdd((unsigned long long*)&p.status[ST_NEWKEYS], 1ull);
+                inserted = true;
                 return (int64_t)s;
             }
             if (k == key) return (int64_t)s;
         }
     }
     return -1;
+}
+__device__ __forceinline__ int64_t g_find(const GbParams& p, uint64_t key) {
+    bool ins = false;
+    const int64_t s = g_find_ins(p, key, ins);
+    if (ins) atomicAdd((unsigned long long*)&p.status[ST_NEWKEYS], 1ull);
+    return s;
 }
 
 // Branch-free conversion for the common case: a finite value whose bits all
@@ -477,6 +511,7 @@ struct ThreadDiag {
     uint32_t nglobal;
     uint32_t special;
     uint32_t kbad;     // fused key packing: a selected row's field left its bits
+    uint32_t newkeys;  // global-table slots this thread claimed
 };
 
 // Packed per-acc descriptor word (uniform): field indices and flags, so the
@@ -577,13 +612,30 @@ __device__ __forceinline__ void global_row(const GbParams& p, uint64_t key, bool
     int64_t gs;
     if (!kvalid) gs = p.gcap;
     else if (key == kEmptyKey) gs = p.gcap + 1;
-    else gs = g_find(p, key);
+    else {
+        bool ins = false;
+        gs = g_find_ins(p, key, ins);
+        diag.newkeys += ins ? 1u : 0u;
+    }
     if (gs < 0) {
         atomicAdd((unsigned long long*)&p.status[ST_TABLE_FULL], 1ull);
         return;
     }
     if (gs >= p.gcap) diag.special |= gs == p.gcap ? 1u : 2u;
     apply_row<false, NA>(p, nullptr, 0, gs, row, v, vm, dd, bot, nacc, diag);
+}
+
+// Partition region of a one-workgroup-per-partition run (p.rbits > 0):
+// claim LDS slot s's own global slot for `key` -- region q (this
+// workgroup's partition), slot s -- or -1 when an overflow row's key took it
+// first (the caller then probes with g_find).  A claimed slot belongs to this
+// thread alone: its fields are written with plain stores.
+__device__ __forceinline__ int64_t g_direct_claim(const GbParams& p, int s, uint64_t key) {
+    const int64_t t = ((int64_t)(blockIdx.x / p.part_blocks) << p.rbits) + s;
+    return atomicCAS((unsigned long long*)&p.gtab[t], (unsigned long long)kEmptyKey, (unsigned long long)key) ==
+                   kEmptyKey
+               ? t
+               : -1;
 }
 
 // End of a main launch: fold the workgroup's LDS table into the global
@@ -603,7 +655,36 @@ __device__ __forceinline__ void flush_and_report(const GbParams& p, uint64_t* ld
                 gs = p.gcap + 1;
                 d.special |= 2u;
             } else {
-                gs = g_find(p, lds[s]);
+                const int64_t t = p.rbits > 0 ? g_direct_claim(p, s, lds[s]) : -1;
+                if (t >= 0) {
+                    // the partition's own region slot: plain stores of the
+                    // LDS state (the global fields start at the same initial
+                    // values as the LDS ones)
+                    ++d.newkeys;
+                    *gfield(p, p.f_len, t) = len;
+                    if (p.f_first >= 0) *gfield(p, p.f_first, t) = lds[p.f_first * L + s];
+                    if (p.f_last >= 0) *gfield(p, p.f_last, t) = lds[p.f_last * L + s];
+                    for (int a = 0; a < p.nacc; ++a) {
+                        const AccSpec& ac = p.acc[a];
+                        if (ac.f_cnt >= 0) *gfield(p, ac.f_cnt, t) = lds[ac.f_cnt * L + s];
+                        if (ac.flags & (A_FSUM | A_FSUMCAST)) {
+                            uint64_t w0, w1, w2;
+                            limbs_to_192((int64_t)lds[ac.f_sum * L + s], (int64_t)lds[(ac.f_sum + 1) * L + s],
+                                         (int64_t)lds[(ac.f_sum + 2) * L + s], w0, w1, w2);
+                            *gfield(p, ac.f_sum, t) = w0;
+                            *gfield(p, ac.f_sum + 1, t) = w1;
+                            *gfield(p, ac.f_sum + 2, t) = w2;
+                        }
+                        if (ac.flags & A_ISUM) *gfield(p, ac.f_isum, t) = lds[ac.f_isum * L + s];
+                        if (ac.flags & A_MIN) *gfield(p, ac.f_min, t) = lds[ac.f_min * L + s];
+                        if (ac.flags & A_MAX) *gfield(p, ac.f_max, t) = lds[ac.f_max * L + s];
+                        if (ac.f_flags >= 0) *gfield(p, ac.f_flags, t) = lds[ac.f_flags * L + s];
+                    }
+                    continue;
+                }
+                bool ins = false;
+                gs = g_find_ins(p, lds[s], ins);
+                d.newkeys += ins ? 1u : 0u;
                 if (gs < 0) {
                     atomicAdd((unsigned long long*)&p.status[ST_TABLE_FULL], 1ull);
                     continue;
@@ -646,13 +727,14 @@ __device__ __forceinline__ void flush_and_report(const GbParams& p, uint64_t* ld
             }
         }
     }
-    uint64_t nsel = d.nsel, nglob = d.nglobal;
+    uint64_t nsel = d.nsel, nglob = d.nglobal, nk = d.newkeys;
     uint32_t special = d.special, fx = d.fxbits;
     const bool kbad = __any(d.kbad != 0);
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
         nsel += __shfl_xor(nsel, off, 64);
         nglob += __shfl_xor(nglob, off, 64);
+        nk += __shfl_xor(nk, off, 64);
         special |= __shfl_xor(special, off, 64);
         fx |= __shfl_xor(fx, off, 64);
     }
@@ -660,6 +742,7 @@ __device__ __forceinline__ void flush_and_report(const GbParams& p, uint64_t* ld
         if (kbad) atomicOr((unsigned long long*)&p.status[ST_KPACK], 1ull);
         if (nsel) atomicAdd((unsigned long long*)&p.status[ST_SELECTED], (unsigned long long)nsel);
         if (nglob) atomicAdd((unsigned long long*)&p.status[ST_GLOBAL_ROWS], (unsigned long long)nglob);
+        if (nk) atomicAdd((unsigned long long*)&p.status[ST_NEWKEYS], (unsigned long long)nk);
         if (special) atomicOr((unsigned long long*)&p.status[ST_SPECIAL], (unsigned long long)special);
         if (fx) atomicOr((unsigned long long*)&p.status[ST_FXFLAGS], (unsigned long long)fx);
     }
@@ -837,8 +920,6 @@ constexpr int kPsDigitBits = 8;    // digit bits per scatter pass
 constexpr int kPsThreads = 256;
 constexpr int kPsPer = 16;
 constexpr int kPsTile = kPsThreads * kPsPer;  // 4096 rows; a wave ranks 1024 consecutive rows
-
-__device__ __forceinline__ uint64_t part_hash(uint64_t key) { return mk_fmix(key ^ 0x2545F4914F6CDD1Dull); }
 
 struct PartOut {
     uint64_t* key;
@@ -1809,7 +1890,26 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
                 gs = p.gcap + 1;
                 d.special |= 2u;
             } else {
-                gs = g_find(p, lds[sl]);
+                const int64_t t = PART && p.rbits > 0 ? g_direct_claim(p, sl, lds[sl]) : -1;
+                if (t >= 0) {
+                    // the partition's own region slot: plain stores
+                    ++d.newkeys;
+                    *gfield(p, p.f_len, t) = len;
+#pragma unroll
+                    for (int a = 0; a < NACC; ++a) {
+                        const int f = p.acc[a].f_sum;
+                        uint64_t w0, w1, w2;
+                        limbs_to_192(0, (int64_t)*fld(sl, so_mid(a)), (int64_t)*fld(sl, so_top(a)), w0, w1, w2);
+                        *gfield(p, f, t) = w0;
+                        *gfield(p, f + 1, t) = w1;
+                        *gfield(p, f + 2, t) = w2;
+                        *gfield(p, p.acc[a].f_flags, t) = *fld(sl, so_flags(a));
+                    }
+                    continue;
+                }
+                bool ins = false;
+                gs = g_find_ins(p, lds[sl], ins);
+                d.newkeys += ins ? 1u : 0u;
                 if (gs < 0) {
                     atomicAdd((unsigned long long*)&p.status[ST_TABLE_FULL], 1ull);
                     continue;
@@ -3166,6 +3266,7 @@ struct GbRun {
     int part_lbits = 0;
     int part_blocks = 1;
     int part_levels = 0;                     // scatter passes taken (info)
+    int rbits = 0;                           // global-table region bits (GbParams::rbits)
     uint64_t* pbuf = nullptr;
     uint64_t* prange = nullptr;              // scan of the count matrix + partition bounds
     const uint64_t* part_range = nullptr;    // P + 1 partition boundaries (inside prange)
@@ -3908,6 +4009,13 @@ static int gb_partition(GbRun& R) {
     int nb = (int)std::max<int64_t>(1, (wpc * (int64_t)num_cus() + P - 1) / P);
     while ((int64_t)maxpart > (int64_t)nb * (kMaxRowsPerWg / 2)) nb *= 2;
     R.part_blocks = nb;
+    // one workgroup per partition: its groups get a region of the global
+    // table that it fills slot for slot from its LDS table (plain stores,
+    // no probing, no atomics), 2^(pbits + lbits) slots in all
+    if (nb == 1 && options().part_direct != 0) {
+        R.rbits = R.part_lbits;
+        R.gbits = R.pbits + R.part_lbits;
+    }
     return PLGPU_OK;
 }
 
@@ -3986,6 +4094,7 @@ static int gb_alloc_table(GbRun& R) {
     R.gtab = nullptr;
     p.gbits = R.gbits;
     p.gcap = int64_t(1) << R.gbits;
+    p.rbits = R.rbits;
     const size_t wpf = (size_t)(p.gcap + 2);
     int rc = dev_alloc((void**)&R.gtab, wpf * p.nfields * 8, R.s);
     if (rc) return rc;
@@ -4110,6 +4219,8 @@ static int gb_main(GbRun& R, bool auto_refit, bool* refit, int32_t* hint) {
         }
         bool again = false;
         if (R.st[ST_TABLE_FULL] > 0) {
+            // (a full partition region: the rerun takes the plain hashed table)
+            R.rbits = 0;
             R.gbits = std::max(R.gbits + 3, log2_ceil((int64_t)R.st[ST_NEWKEYS] * 4));
             again = true;
         }
@@ -4374,11 +4485,9 @@ __global__ void mk_hash_kernel(MkKeys k, int64_t n, uint64_t seed, uint64_t mask
 // Read-only probe of the global table: slot of `key`, or -1.
 __device__ __forceinline__ int64_t g_lookup(const GbParams& p, uint64_t key) {
     if (key == kEmptyKey) return p.gcap + 1;
-    const uint64_t mask = (uint64_t)p.gcap - 1;
-    const uint64_t h = p.gbits == 0 ? 0 : ((key * 0x9E3779B97F4A7C15ull) >> (64 - p.gbits));
-    const int lim = p.gcap < kGlobalProbe ? (int)p.gcap : kGlobalProbe;
+    const int lim = g_probe_limit(p);
     for (int i = 0; i < lim; ++i) {
-        const uint64_t s = (h + (uint64_t)i) & mask;
+        const uint64_t s = g_slot(p, key, (uint64_t)i);
         const uint64_t k = p.gtab[s];
         if (k == key) return (int64_t)s;
         if (k == kEmptyKey) return -1;

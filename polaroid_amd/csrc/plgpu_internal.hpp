@@ -50,6 +50,7 @@ struct Options {
                           // 2 fused kernel, 3 partitioned (where the inputs allow it)
     int part_bits = -1;   // partitioned path: at least this many partition bits
     int part_levels = -1; // partitioned path: 1 / 2 scatter passes (-1: by the partition bits)
+    int part_direct = 1;  // partitioned path: one-workgroup partitions flush into their own table region
 };
 Options& options();
 

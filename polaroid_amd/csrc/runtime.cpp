@@ -60,6 +60,7 @@ const OptField kOptFields[] = {
     {"gb_path", "PLGPU_GB_PATH", &Options::gb_path},
     {"part_bits", "PLGPU_PART_BITS", &Options::part_bits},
     {"part_levels", "PLGPU_PART_LEVELS", &Options::part_levels},
+    {"part_direct", "PLGPU_PART_DIRECT", &Options::part_direct},
 };
 const OptField* opt_field(const char* name) {
     for (const OptField& f : kOptFields)
