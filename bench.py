@@ -406,12 +406,13 @@ def many_groups_leg(torch, pl, cols: dict, steps: int, warmup: int, groups_list,
              "step_frac_read_once": round(40 * n / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
         if info.get("path") == 3:
             r["count"] = _leg_roofline(kernels, "gbp_count_kernel", n * 16 + (sel * 8 if levels == 2 else 0),
-                                       "key + predicate read per row (+ 8 B key per selected row at level 2)")
+                                       "key + predicate read per row (+ 8 B key per selected row at level 2)", True)
             r["scatter"] = _leg_roofline(kernels, "gbp_scatter_kernel",
                                          n * 40 + sel * 40 + (sel * 80 if levels == 2 else 0),
                                          "40 B read per row + 40 B written per selected row (+ 40 + 40 B per "
-                                         "selected row at level 2)")
-            r["aggregate"] = _leg_roofline(kernels, "gb_part_agg_kernel", sel * 40, "40 B read per selected row")
+                                         "selected row at level 2)", True)
+            r["aggregate"] = _leg_roofline(kernels, "gb_part_agg_kernel", sel * 40, "40 B read per selected row",
+                                           True)
         r["kernels"] = kernels
         out[str(G)] = r
         progress(f"many_groups {G}: {r['ms_per_step']} ms per step")
@@ -472,8 +473,10 @@ def _time_steps(torch, step, steps: int, warmup: int):
     return dt * 1e3, _kernel_table(kt, steps), res
 
 
-def _leg_roofline(kernels: dict, name: str, algo_bytes: float, what: str) -> dict:
-    k = kernels.get(name, {}).get("ms_mean")
+def _leg_roofline(kernels: dict, name: str, algo_bytes: float, what: str, per_step: bool = False) -> dict:
+    """The kernel's HBM fraction at `algo_bytes` per launch (per_step: per
+    step, over all its launches in the step, e.g. both scatter passes)."""
+    k = kernels.get(name, {}).get("ms_per_step" if per_step else "ms_mean")
     if not k:
         return {"kernel": name, "kernel_ms": None}
     gbs = algo_bytes / (k * 1e-3) / 1e9
@@ -524,7 +527,11 @@ def sort_leg(torch, pl, steps: int, warmup: int, rows: int = SORT_ROWS, window: 
 
     ms, kernels, res = _time_steps(torch, step, steps, warmup)
     assert res == 2 * rows
-    del df, cols
+    # rolling_std(20) of the price column on its own (volatility: the exact
+    # windowed second moment, rl_wave_var_kernel)
+    price = df["price"]
+    ms_std, kern_std, _ = _time_steps(torch, lambda: price.rolling_std(window).len(), steps, warmup)
+    del df, cols, price
     torch.cuda.empty_cache()
     # the sort's floor: read the 8 input columns once and write the 8 sorted
     # columns once (128 B/row); rolling_mean reads and writes 8 B/row
@@ -533,11 +540,14 @@ def sort_leg(torch, pl, steps: int, warmup: int, rows: int = SORT_ROWS, window: 
                            "64 B packed row read + 4 B row id read + 64 B column stores per row")
     pack = _leg_roofline(kernels, "aos_pack_kernel", rows * 128, "64 B read + 64 B packed row written per row")
     roll = _leg_roofline(kernels, "rl_wave_kernel", rows * 16, "8 B read + 8 B written per row")
+    roll_std = _leg_roofline(kern_std, "rl_wave_var_kernel", rows * 16, "8 B read + 8 B written per row")
+    roll_std["ms_per_step"] = round(ms_std, 3)
+    roll_std["query"] = f"price.rolling_std({window})"
     return {"query": f"df.sort('ts') (8 columns: 4 x i64, 4 x f64) + sorted price.rolling_mean({window})",
             "rows": rows, "ms_per_step": round(ms, 3), "Mrows_s": round(rows / ms / 1e3, 1),
             "algorithmic_GB": round(algo / 1e9, 1),
             "step_frac": round(algo / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-            "roofline": gather, "pack": pack, "rolling": roll, "kernels": kernels,
+            "roofline": gather, "pack": pack, "rolling": roll, "rolling_std": roll_std, "kernels": kernels,
             "note": "step_frac: the read-once / write-once floor (128 B/row sort + 16 B/row rolling) over the step "
                     "time; roofline: the dominant kernel (aos_gather_kernel) at its own algorithmic bytes"}
 

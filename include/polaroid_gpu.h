@@ -704,12 +704,21 @@ int plgpu_arg_sort_multi(const plgpu_column* keys, int32_t nkeys, const int32_t*
  * rolling_mean.  Float64 (and integer mean) results are the correctly
  * rounded window sums (divided by the non-null count); integer sums wrap.
  * Replaces polars-compute/src/rolling/no_nulls/{sum,mean}.rs rolling_sum /
- * rolling_mean and nulls/{sum,mean}.rs (rolling/sum.rs:7 SumWindow). */
+ * rolling_mean and nulls/{sum,mean}.rs (rolling/sum.rs:7 SumWindow).
+ * VAR / STD (ddof in bits 8..15 of kind): Series.rolling_var / rolling_std,
+ * replacing polars-compute/src/rolling/{no_nulls,nulls}/moment.rs
+ * rolling_var (rolling/moment.rs:138 MomentWindow<VarianceMoment>) and
+ * polars-time/src/chunkedarray/rolling_window/dispatch.rs:526 (std = its
+ * square root): Float64 output, (RN(c sum x^2 - (sum x)^2) / c) / (c - ddof)
+ * with the numerator exact; a non-finite value gives NaN; null below
+ * min_periods non-null values or at c <= ddof. */
 enum plgpu_rolling_kind {
     PLGPU_ROLLING_SUM = 1,
     PLGPU_ROLLING_MEAN = 2,
     PLGPU_ROLLING_MIN = 3,  /* rolling/no_nulls/min_max.rs MinWindow (NaN propagates) */
-    PLGPU_ROLLING_MAX = 4   /* ... MaxWindow; output dtype = input dtype            */
+    PLGPU_ROLLING_MAX = 4,  /* ... MaxWindow; output dtype = input dtype            */
+    PLGPU_ROLLING_VAR = 5,
+    PLGPU_ROLLING_STD = 6
 };
 
 int plgpu_rolling(const plgpu_column* values, int32_t kind, int64_t window_size,

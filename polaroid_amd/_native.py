@@ -187,7 +187,7 @@ GB_MAX_ACC = 6
 JOIN_ORDER = {None: 0, "none": 0, "left": 1, "right": 2, "left_right": 3, "right_left": 4}
 JOIN_VALIDATE = {"m:m": 0, "1:m": 1, "m:1": 2, "1:1": 3}
 JOIN_HOW = {"inner": 0, "left": 1, "right": 2, "full": 3, "semi": 4, "anti": 5}
-ROLLING = {"sum": 1, "mean": 2, "min": 3, "max": 4}
+ROLLING = {"sum": 1, "mean": 2, "min": 3, "max": 4, "var": 5, "std": 6}
 
 _lib = None
 

@@ -1509,7 +1509,9 @@ __global__ __launch_bounds__(kGbThreads) void gb_fast_kernel(GbParams p, DevProg
     // one accumulator in the single-table kernel, chosen by the plan for
     // sorted / clustered keys (a frame sorted by symbol gives every lane
     // long runs of one group).
-    constexpr bool RACC = SUMONLY && LIMBS == 2 && (PART || RUNS);
+    // (partition buffers: only for clustered / sorted keys, RUNS; random keys
+    // would evict on nearly every row)
+    constexpr bool RACC = SUMONLY && LIMBS == 2 && RUNS;
     constexpr int KR = RACC ? (PART ? 4 : 1) : 1;
     int rs[KR];
     uint64_t rn[KR], rlo_[KR][NA], rhi_[KR][NA];
@@ -2409,6 +2411,10 @@ struct FinParams {
     uint64_t* out_first;  // optional
     int64_t cap;          // allocated output rows (guards against a miscount)
     const double* wide[kMaxAcc];  // per acc: rounded wide sums per slot, or null
+    // validity as one byte per output row (row 0: the key, row 1 + o:
+    // output o; stride cap), packed into the bitmaps afterwards
+    // (gb_pack_valid_kernel): no per-group atomics on shared words
+    uint8_t* vbytes;
 };
 
 __global__ void gb_finalize_kernel(GbParams p, FinParams fp) {
@@ -2433,7 +2439,7 @@ __global__ void gb_finalize_kernel(GbParams p, FinParams fp) {
         if (g >= fp.cap) continue;
         const bool null_key = s == p.gcap;
         fp.out_keys[g] = null_key ? 0 : (int64_t)(s == p.gcap + 1 ? kEmptyKey : *gfield(p, 0, s));
-        if (!null_key) atomicOr(&fp.out_key_valid[g >> 5], 1u << (g & 31));
+        fp.vbytes[g] = null_key ? 0 : 1;
         if (fp.out_first) fp.out_first[g] = *gfield(p, p.f_first, s);
         for (int o = 0; o < fp.nout; ++o) {
             const OutSpec& os = fp.out[o];
@@ -2532,9 +2538,35 @@ __global__ void gb_finalize_kernel(GbParams p, FinParams fp) {
             }
             default: break;
             }
-            if (os.validity && valid) atomicOr(&os.validity[g >> 5], 1u << (g & 31));
+            if (os.validity) fp.vbytes[(int64_t)(1 + o) * fp.cap + g] = valid ? 1 : 0;
         }
     }
+}
+
+// Validity bytes (FinParams::vbytes) -> Arrow bitmaps: one 32-bit word per
+// thread per column.
+struct PackValid {
+    uint32_t* dst[PLGPU_MAX_COLS * 2 + 1];  // null: no bitmap for that row of bytes
+    int32_t n;
+};
+__global__ void gb_pack_valid_kernel(const uint8_t* __restrict__ vb, int64_t cap, PackValid pv) {
+    const int64_t words = ((cap + 63) / 64) * 2;  // the bitmap's whole 64-bit words (bits past cap: 0)
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words * pv.n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)(i / words);
+        const int64_t w = i - (int64_t)c * words;
+        if (pv.dst[c] == nullptr) continue;
+        const uint8_t* b = vb + (int64_t)c * cap + w * 32;
+        const int m = (int)std::max<int64_t>(0, std::min<int64_t>(32, cap - w * 32));
+        uint32_t bits = 0;
+        for (int j = 0; j < m; ++j) bits |= (uint32_t)(b[j] != 0) << j;
+        pv.dst[c][w] = bits;
+    }
+}
+
+__global__ void widen_u32_kernel(const uint32_t* __restrict__ a, int64_t* __restrict__ b, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        b[i] = (int64_t)a[i];
 }
 
 // Gather rows of fixed-width buffers by a permutation (maintain_order).
@@ -2548,11 +2580,19 @@ __global__ void narrow_i64_kernel(const int64_t* __restrict__ a, void* __restric
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         dev_store(b, dt, i, (uint64_t)a[i]);
 }
+// One destination bitmap word per thread (bits past n: 0), no atomics.
 __global__ void gather_bits_kernel(const uint32_t* __restrict__ src, const int64_t* __restrict__ perm,
                                    uint32_t* __restrict__ dst, int64_t n) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t j = perm[i];
-        if ((src[j >> 5] >> (j & 31)) & 1u) atomicOr(&dst[i >> 5], 1u << (i & 31));
+    const int64_t words = (n + 31) / 32;
+    for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < words;
+         w += (int64_t)gridDim.x * blockDim.x) {
+        uint32_t bits = 0;
+        const int m = (int)std::min<int64_t>(32, n - w * 32);
+        for (int k = 0; k < m; ++k) {
+            const int64_t j = perm[w * 32 + k];
+            bits |= ((src[j >> 5] >> (j & 31)) & 1u) << k;
+        }
+        dst[w] = bits;
     }
 }
 
@@ -2723,6 +2763,7 @@ struct Plan {
     int fast_grid;
     bool runs;         // sampled keys mostly equal their next row's (sorted / clustered input)
     bool local;        // range-local mode: contiguous tiles per workgroup, LDS sized by range-local keys
+    bool part_racc = false;  // partitioned path: register accumulators (clustered / sorted keys)
     mutable int launched_grid;  // grid of the last fast launch (info)
     mutable bool launched_runs = false;  // that launch used the register-run variant (info)
     mutable bool launched_var = false;   // that launch was the variance-triple variant (info)
@@ -3803,7 +3844,8 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
         // CU): measured 2-7 % faster than 80 KB tables at 14k-100k groups
         // (profiles/r02_ab_part.log)
         const int min_pb = std::min(kPartMaxBits, std::max(0, options().part_bits));
-        for (size_t budget : {(size_t)160 * 1024, (size_t)80 * 1024}) {
+        const size_t b0 = options().part_lds_kb > 0 ? (size_t)options().part_lds_kb * 1024 : (size_t)160 * 1024;
+        for (size_t budget : {b0, (size_t)80 * 1024}) {
             int lb = 13;
             while (lb > 6 && ((size_t)fields * ((1u << lb) + 2) * 8 > budget ||
                               (size_t)p.nfields * ((1u << lb) + 2) * 8 > (size_t)160 * 1024))
@@ -3820,6 +3862,9 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
         }
     }
     if (R.part) p.n_full = 0, p.row_begin = 0;
+    // the partition kernel's register accumulators pay when the rows of a
+    // partition repeat their groups nearby (sorted or clustered keys)
+    pl.part_racc = R.part && (pl.runs || clustered);
     if (p.kp.n > 0 && (p.n_full == 0 || R.part || gb_has_fused(R) ||
                        (p.kp.c[0].dtype == PLGPU_STR && (!pl.sum_only || p.nacc == 0)))) {
         // the packed key lives only in the fused kernel's registers
@@ -4019,9 +4064,9 @@ static int gb_partition(GbRun& R) {
     return PLGPU_OK;
 }
 
-template <int NACC, int LIMBS>
+template <int NACC, int LIMBS, bool RACC>
 static hipError_t launch_part_fast(const Plan& pp, int grid, hipStream_t s) {
-    const void* kern = (const void*)gb_fast_kernel<NACC, 0, true, 2, LIMBS, false, true>;
+    const void* kern = (const void*)gb_fast_kernel<NACC, 0, true, 2, LIMBS, RACC, true>;
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -4030,13 +4075,15 @@ static hipError_t launch_part_fast(const Plan& pp, int grid, hipStream_t s) {
     const size_t lds = (size_t)(LIMBS == 2 ? slim_words(NACC) : pp.p.nfields) * (pp.p.lcap + 2) * 8;
     DevProgram none;
     std::memset(&none, 0, sizeof none);
-    gb_fast_kernel<NACC, 0, true, 2, LIMBS, false, true><<<grid, kGbThreads, lds, s>>>(pp.p, none);
+    gb_fast_kernel<NACC, 0, true, 2, LIMBS, RACC, true><<<grid, kGbThreads, lds, s>>>(pp.p, none);
     return hipGetLastError();
 }
 
+// register accumulators (RACC) on the 2-limb window, for clustered keys
 template <int NACC>
 static hipError_t launch_part_fast_limbs(const Plan& pp, int grid, hipStream_t s) {
-    return pp.limbs == 2 ? launch_part_fast<NACC, 2>(pp, grid, s) : launch_part_fast<NACC, 3>(pp, grid, s);
+    if (pp.limbs != 2) return launch_part_fast<NACC, 3, false>(pp, grid, s);
+    return pp.part_racc ? launch_part_fast<NACC, 2, true>(pp, grid, s) : launch_part_fast<NACC, 2, false>(pp, grid, s);
 }
 
 // The main pass over the partition buffers.
@@ -4336,19 +4383,35 @@ static int gb_finalize(GbRun& R, int32_t naggs, plgpu_column* out_key, plgpu_col
             fp.out[i] = pl.outs[i];
             fp.out[i].values = (void*)out_aggs[i].values;
             fp.out[i].validity = (uint32_t*)out_aggs[i].validity;
-            if (fp.out[i].validity) (void)hipMemsetAsync(fp.out[i].validity, 0, ((groups + 63) / 64) * 8, s);
         }
         fp.out_keys = (int64_t*)out_key->values;
         fp.out_key_valid = (uint32_t*)out_key->validity;
-        (void)hipMemsetAsync((void*)out_key->validity, 0, ((groups + 63) / 64) * 8, s);
         fp.out_first = first;
         fp.cap = groups;
         for (int a = 0; a < kMaxAcc; ++a) fp.wide[a] = R.wide_sum[a];
+        uint8_t* vbytes = nullptr;
+        rc = dev_alloc((void**)&vbytes, (size_t)(1 + naggs) * groups, s);
+        if (rc) {
+            dev_free(first, s);
+            plgpu_column_release(out_key);
+            for (int i = 0; i < naggs; ++i) plgpu_column_release(&out_aggs[i]);
+            return rc;
+        }
+        fp.vbytes = vbytes;
         const int fg = (int)std::min<int64_t>((p.gcap + 2 + 255) / 256, 256 * 16);
         {
             KtScope kt("gb_finalize_kernel", s);
             gb_finalize_kernel<<<fg, 256, 0, s>>>(p, fp);
+            PackValid pv;
+            std::memset(&pv, 0, sizeof pv);
+            pv.n = 1 + naggs;
+            pv.dst[0] = (uint32_t*)out_key->validity;
+            for (int i = 0; i < naggs; ++i) pv.dst[1 + i] = (uint32_t*)out_aggs[i].validity;
+            const int64_t work = ((groups + 63) / 64) * 2 * pv.n;
+            gb_pack_valid_kernel<<<(unsigned)std::min<int64_t>((work + 255) / 256, 4096), 256, 0, s>>>(vbytes, groups,
+                                                                                                       pv);
         }
+        dev_free(vbytes, s);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) rc = hip_fail(e, "gb_finalize_kernel");
         uint64_t produced = 0, var_out = 0;
@@ -4372,68 +4435,72 @@ static int gb_finalize(GbRun& R, int32_t naggs, plgpu_column* out_key, plgpu_col
         }
     }
     if (rc == PLGPU_OK && R.maintain && groups > 1) {
-        // order groups by first occurrence (host argsort of `groups` row ids)
-        std::vector<uint64_t> hf(groups);
-        std::vector<int64_t> perm(groups);
-        hipError_t e = hipMemcpyAsync(hf.data(), first, groups * 8, hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
-        if (e != hipSuccess) rc = hip_fail(e, "copy first rows");
+        // order groups by first occurrence: a stable radix arg_sort of the
+        // groups' first rows on the device (sort.hip), then every output
+        // column gathered by it
+        plgpu_column fc, pidx;
+        std::memset(&fc, 0, sizeof fc);
+        std::memset(&pidx, 0, sizeof pidx);
+        fc.dtype = PLGPU_I64;
+        fc.length = groups;
+        fc.values = first;
+        rc = plgpu_arg_sort(&fc, 0, 0, &pidx, s);
+        int64_t* dperm = nullptr;
+        if (rc == PLGPU_OK) rc = dev_alloc((void**)&dperm, groups * 8, s);
         if (rc == PLGPU_OK) {
-            std::iota(perm.begin(), perm.end(), 0);
-            std::sort(perm.begin(), perm.end(), [&](int64_t a, int64_t b) { return hf[a] < hf[b]; });
-            int64_t* dperm = nullptr;
-            rc = dev_alloc((void**)&dperm, groups * 8, s);
-            if (rc == PLGPU_OK) {
-                (void)hipMemcpyAsync(dperm, perm.data(), groups * 8, hipMemcpyHostToDevice, s);
-                const int gg = (int)std::min<int64_t>((groups + 255) / 256, 4096);
-                auto permute = [&](plgpu_column* c) -> int {
-                    plgpu_column nc;
-                    int r2 = make_owned_column(&nc, c->dtype, groups, c->validity != nullptr, s);
-                    if (r2) return r2;
-                    switch (dtype_bytes(c->dtype)) {
-                    case 8:
-                        gather_kernel<uint64_t><<<gg, 256, 0, s>>>((const uint64_t*)c->values, dperm,
-                                                                   (uint64_t*)nc.values, groups);
-                        break;
-                    case 4:
-                        gather_kernel<uint32_t><<<gg, 256, 0, s>>>((const uint32_t*)c->values, dperm,
-                                                                   (uint32_t*)nc.values, groups);
-                        break;
-                    case 2:
-                        gather_kernel<uint16_t><<<gg, 256, 0, s>>>((const uint16_t*)c->values, dperm,
-                                                                   (uint16_t*)nc.values, groups);
-                        break;
-                    case 1:
-                        gather_kernel<uint8_t><<<gg, 256, 0, s>>>((const uint8_t*)c->values, dperm,
-                                                                  (uint8_t*)nc.values, groups);
-                        break;
-                    default:
-                        plgpu_column_release(&nc);
-                        return fail(PLGPU_ERR_SCHEMA, "group order: unsupported output dtype");
-                    }
-                    if (c->validity) {
-                        (void)hipMemsetAsync((void*)nc.validity, 0, ((groups + 63) / 64) * 8, s);
-                        gather_bits_kernel<<<gg, 256, 0, s>>>((const uint32_t*)c->validity, dperm,
-                                                              (uint32_t*)nc.validity, groups);
-                    }
-                    plgpu_column_release(c);
-                    *c = nc;
-                    return PLGPU_OK;
-                };
-                rc = permute(out_key);
-                for (int i = 0; i < naggs && rc == PLGPU_OK; ++i) rc = permute(&out_aggs[i]);
-                dev_free(dperm, s);
-                if (rc == PLGPU_OK && keep_first) {
-                    // first rows in output order = the sorted first rows
-                    std::sort(hf.begin(), hf.end());
-                    (void)hipMemcpyAsync(first, hf.data(), groups * 8, hipMemcpyHostToDevice, s);
+            const int gg = (int)std::min<int64_t>((groups + 255) / 256, 4096);
+            widen_u32_kernel<<<gg, 256, 0, s>>>((const uint32_t*)pidx.values, dperm, groups);
+            auto permute = [&](plgpu_column* c) -> int {
+                plgpu_column nc;
+                int r2 = make_owned_column(&nc, c->dtype, groups, c->validity != nullptr, s);
+                if (r2) return r2;
+                switch (dtype_bytes(c->dtype)) {
+                case 8:
+                    gather_kernel<uint64_t><<<gg, 256, 0, s>>>((const uint64_t*)c->values, dperm,
+                                                               (uint64_t*)nc.values, groups);
+                    break;
+                case 4:
+                    gather_kernel<uint32_t><<<gg, 256, 0, s>>>((const uint32_t*)c->values, dperm,
+                                                               (uint32_t*)nc.values, groups);
+                    break;
+                case 2:
+                    gather_kernel<uint16_t><<<gg, 256, 0, s>>>((const uint16_t*)c->values, dperm,
+                                                               (uint16_t*)nc.values, groups);
+                    break;
+                case 1:
+                    gather_kernel<uint8_t><<<gg, 256, 0, s>>>((const uint8_t*)c->values, dperm,
+                                                              (uint8_t*)nc.values, groups);
+                    break;
+                default:
+                    plgpu_column_release(&nc);
+                    return fail(PLGPU_ERR_SCHEMA, "group order: unsupported output dtype");
                 }
+                if (c->validity) {
+                    (void)hipMemsetAsync((void*)nc.validity, 0, ((groups + 63) / 64) * 8, s);
+                    gather_bits_kernel<<<gg, 256, 0, s>>>((const uint32_t*)c->validity, dperm,
+                                                          (uint32_t*)nc.validity, groups);
+                }
+                plgpu_column_release(c);
+                *c = nc;
+                return PLGPU_OK;
+            };
+            rc = permute(out_key);
+            for (int i = 0; i < naggs && rc == PLGPU_OK; ++i) rc = permute(&out_aggs[i]);
+            if (rc == PLGPU_OK && keep_first) {
+                // first rows in output order
+                uint64_t* sf = nullptr;
+                rc = dev_alloc((void**)&sf, groups * 8, s);
                 if (rc == PLGPU_OK) {
-                    e = hipStreamSynchronize(s);  // keep `perm` alive until the copy ran
-                    if (e != hipSuccess) rc = hip_fail(e, "permute");
+                    gather_kernel<uint64_t><<<gg, 256, 0, s>>>(first, dperm, sf, groups);
+                    dev_free(first, s);
+                    first = sf;
                 }
             }
+            hipError_t e = hipGetLastError();
+            if (rc == PLGPU_OK && e != hipSuccess) rc = hip_fail(e, "permute");
         }
+        dev_free(dperm, s);
+        plgpu_column_release(&pidx);
     }
     if (rc == PLGPU_OK && R.key_dtype != PLGPU_I64 && dtype_bytes(R.key_dtype) > 0) {
         // the key back in its own dtype (the reference keeps the key dtype)

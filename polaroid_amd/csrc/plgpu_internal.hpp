@@ -51,6 +51,7 @@ struct Options {
     int part_bits = -1;   // partitioned path: at least this many partition bits
     int part_levels = -1; // partitioned path: 1 / 2 scatter passes (-1: by the partition bits)
     int part_direct = 1;  // partitioned path: one-workgroup partitions flush into their own table region
+    int part_lds_kb = 0;  // partitioned path: LDS table budget per workgroup (0: 160 KiB)
 };
 Options& options();
 

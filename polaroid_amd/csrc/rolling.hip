@@ -46,7 +46,15 @@ struct RlParams {
     int32_t out_int;  // integer sum output (I64 / I32)
     void* out;
     uint64_t* out_valid;  // always written (one word per 64 outputs)
+    int32_t var;          // 0: sum / mean; 1: rolling_var; 2: rolling_std
+    int32_t ddof;
+    int32_t var_f32;      // std of a Float32 column: sqrt of the variance rounded to f32
+    int32_t _pad;
 };
+
+__device__ __forceinline__ double rv_std(const RlParams& p, double v) {
+    return __builtin_sqrt(p.var_f32 ? (double)(float)v : v);
+}
 
 __device__ __forceinline__ void rl_bounds(const RlParams& p, int64_t i, int64_t& s, int64_t& e) {
     if (p.center) {
@@ -541,11 +549,271 @@ __device__ __noinline__ void rw_exact_outputs(RlParams p, int64_t o_first, int64
     }
 }
 
-template <int DT, bool NULLABLE>
+// ----------------------------------------------------- rolling var / std
+// polars-compute/src/rolling/moment.rs:138 MomentWindow<VarianceMoment>
+// slides a Welford VarState (polars-compute/src/moment.rs:87,99,126) over
+// the window; a non-finite value enters as 0.0 and makes the result NaN,
+// nulls are skipped, and the result is null below min_periods non-null
+// values or at a count <= ddof.  Here every window's variance is formed
+// from exact sums: with c the non-null count and the values x = t * 2^b
+// (t integers over the wave's smallest exponent),
+//   var = (RN(c * sum t^2 - (sum t)^2) * 2^(2b) / c) / (c - ddof),
+// the numerator exact and rounded once -- the group-by's fused variance
+// (groupby.hip var_exact) per window -- and std its square root.
+// Fast form (the wave's values within a few binades, none tiny): wave
+// prefix scans of t (int64) and t^2 (128-bit), as the window sums.  Other
+// waves: each output summed exactly in big integers (rw_var_exact_outputs).
+constexpr int kRvL = 68;  // 4352-bit integers: c * sum t^2 for any finite f64 window of <= 2^16 values
+
+// a += (neg ? -1 : 1) * (v << sh), two's complement over kRvL words.
+__device__ __forceinline__ void rv_add(uint64_t* a, unsigned __int128 v, int sh, bool neg) {
+    const int ws = sh >> 6, bs = sh & 63;
+    const uint64_t lo = (uint64_t)v, hi = (uint64_t)(v >> 64);
+    const uint64_t d0 = bs ? lo << bs : lo;
+    const uint64_t d1 = bs ? (hi << bs) | (lo >> (64 - bs)) : hi;
+    const uint64_t d2 = bs ? hi >> (64 - bs) : 0ull;
+    uint64_t c = 0;
+    for (int i = ws; i < kRvL; ++i) {
+        const int k = i - ws;
+        const uint64_t d = k == 0 ? d0 : (k == 1 ? d1 : (k == 2 ? d2 : 0ull));
+        if (k >= 3 && c == 0) break;
+        if (!neg) {
+            const unsigned __int128 t = (unsigned __int128)a[i] + d + c;
+            a[i] = (uint64_t)t;
+            c = (uint64_t)(t >> 64);
+        } else {
+            const unsigned __int128 t = (unsigned __int128)a[i] - d - c;
+            a[i] = (uint64_t)t;
+            c = (uint64_t)(t >> 64) ? 1ull : 0ull;
+        }
+    }
+}
+
+// a (>= 0) * 2^e rounded to nearest-even f64, subnormal results included.
+__device__ double rv_round(const uint64_t* a, int e) {
+    int top = kRvL - 1;
+    while (top >= 0 && a[top] == 0) --top;
+    if (top < 0) return 0.0;
+    const int pl = top * 64 + 63 - __clzll(a[top]);
+    int q = pl - 52;
+    if (q + e < -1074) q = -1074 - e;
+    if (q <= 0) return __builtin_ldexp((double)a[0], e);  // < 2^53: exact
+    auto bit = [&](int b) -> uint64_t { return (a[b >> 6] >> (b & 63)) & 1ull; };
+    uint64_t keep = 0;
+    for (int b = pl; b >= q; --b) keep = (keep << 1) | bit(b);
+    const bool rnd = bit(q - 1) != 0;
+    bool sticky = false;
+    for (int b = 0; b < q - 1 && !sticky; ++b) sticky = bit(b) != 0;
+    if (rnd && (sticky || (keep & 1))) ++keep;
+    return __builtin_ldexp((double)keep, q + e);
+}
+
+// Exact variance of the non-null values of [s, e) (any finite values).
+__device__ double rv_window_exact(const RlParams& p, int64_t s, int64_t e, int64_t c) {
+    int emin = 1 << 20;
+    for (int64_t r = s; r < e; ++r) {
+        if (!dev_valid(p.c, r)) continue;
+        const uint64_t b = rl_bits(p, r);
+        const uint32_t ex = (uint32_t)(b >> 52) & 0x7FF;
+        if (ex == 0x7FF || (b << 1) == 0) continue;
+        const int e0 = (int)(ex ? ex : 1) - 1075;  // x = t * 2^e0, t < 2^53
+        emin = e0 < emin ? e0 : emin;
+    }
+    if (emin == 1 << 20) return 0.0;
+    uint64_t sq[kRvL], s1[kRvL], num[kRvL];
+    for (int i = 0; i < kRvL; ++i) sq[i] = s1[i] = num[i] = 0;
+    for (int64_t r = s; r < e; ++r) {
+        if (!dev_valid(p.c, r)) continue;
+        const uint64_t b = rl_bits(p, r);
+        const uint32_t ex = (uint32_t)(b >> 52) & 0x7FF;
+        if (ex == 0x7FF || (b << 1) == 0) continue;
+        const uint64_t t = (b & 0x000FFFFFFFFFFFFFull) | ((uint64_t)(ex != 0) << 52);
+        const int sh = (int)(ex ? ex : 1) - 1075 - emin;
+        rv_add(sq, (unsigned __int128)t * t, 2 * sh, false);
+        rv_add(s1, t, sh, (b >> 63) != 0);
+    }
+    for (int i = 0; i < kRvL; ++i)
+        if (sq[i]) rv_add(num, (unsigned __int128)sq[i] * (uint64_t)c, 64 * i, false);
+    if ((int64_t)s1[kRvL - 1] < 0) {  // |sum t|
+        uint64_t cy = 1;
+        for (int i = 0; i < kRvL; ++i) {
+            const unsigned __int128 t = (unsigned __int128)(~s1[i]) + cy;
+            s1[i] = (uint64_t)t;
+            cy = (uint64_t)(t >> 64);
+        }
+    }
+    for (int i = 0; i < kRvL; ++i) {
+        if (!s1[i]) continue;
+        for (int j = 0; i + j < kRvL; ++j)
+            if (s1[j]) rv_add(num, (unsigned __int128)s1[i] * s1[j], 64 * (i + j), true);
+    }
+    if ((int64_t)num[kRvL - 1] < 0) return 0.0;  // (c sum t^2 >= (sum t)^2: unreachable)
+    const double nr = rv_round(num, 2 * emin);
+    return (nr / (double)c) / (double)(c - p.ddof);
+}
+
+// A wave's outputs one by one, exactly (out of line: its big integers live
+// in private memory; only waves whose values the fast form cannot hold).
+__device__ __noinline__ void rw_var_exact_outputs(RlParams p, int64_t o_first, int64_t o_end) {
+    const int lane = threadIdx.x & 63;
+    for (int q = 0; q < kRwChunks; ++q) {
+        const int64_t i = o_first + 64 * q + lane;
+        if (o_first + 64 * q >= o_end) break;
+        bool valid = false;
+        if (i < o_end) {
+            int64_t s, e;
+            rl_bounds(p, i, s, e);
+            RlCounts k = {0, 0, 0, 0};
+            for (int64_t r = s; r < e; ++r) rl_count(p, r, k);
+            valid = k.nn >= p.min_periods && k.nn > p.ddof;
+            double v = 0.0;
+            if (valid) {
+                v = (k.nan || k.pinf || k.ninf) ? __builtin_nan("") : rv_window_exact(p, s, e, k.nn);
+                if (p.var == 2) v = rv_std(p, v);
+            }
+            ((double*)p.out)[i] = valid ? v : 0.0;
+        }
+        const uint64_t bits = __ballot(valid);
+        if (lane == 0) p.out_valid[(o_first >> 6) + q] = bits;
+    }
+}
+
+// |v| of a 192-bit value's... (w2:w1:w0, >= 0) * 2^e as f64, rounded once
+// (no subnormal results: the fast form's values are not tiny).
+__device__ __forceinline__ double u192_to_double(uint64_t w0, uint64_t w1, uint64_t w2, int e) {
+    if ((w0 | w1 | w2) == 0) return 0.0;
+    uint64_t top, rest;
+    int sh;
+    if (w2) {
+        const int lz = __clzll(w2);
+        top = lz ? (w2 << lz) | (w1 >> (64 - lz)) : w2;
+        rest = (lz ? w1 << lz : w1) | w0;
+        sh = 128 - lz;
+    } else if (w1) {
+        const int lz = __clzll(w1);
+        top = lz ? (w1 << lz) | (w0 >> (64 - lz)) : w1;
+        rest = lz ? w0 << lz : w0;
+        sh = 64 - lz;
+    } else {
+        const int lz = __clzll(w0);
+        top = w0 << lz;
+        rest = 0;
+        sh = -lz;
+    }
+    top |= rest != 0 ? 1ull : 0ull;  // sticky: one u64 -> f64 rounding is then exact-once
+    return __builtin_ldexp((double)top, sh + e);
+}
+
+// Scan + emit of the fast form: prefix sums of t (int64), t^2 (128-bit)
+// and, with COUNTS, the non-null / inf / NaN counts; per output the exact
+// window sums S1, S2 give num = c * S2 - S1^2 (192-bit, exact).
+template <bool COUNTS>
+__device__ __forceinline__ void rw_var_scan(const RlParams& p, const uint64_t (&x)[kRwChunks + 1],
+                                            const uint64_t (&vm)[kRwChunks + 1], int64_t o_first, int64_t o_end,
+                                            int64_t s_first, int tmin, uint64_t* r1, uint64_t* r2l, uint64_t* r2h,
+                                            uint64_t* rcn) {
+    const int lane = threadIdx.x & 63;
+    const int bottom = tmin - 1075;
+    const int64_t right = p.center ? (p.w + 1) / 2 : 1;
+    const int64_t left = p.w - right;
+    const bool interior = o_first - left >= 0 && o_end + right - 1 <= p.n;
+    uint64_t c1 = 0, c2l = 0, c2h = 0, ccn = 0;
+#pragma unroll
+    for (int k = 0; k <= kRwChunks; ++k) {
+        const uint64_t b = x[k];
+        const uint64_t ab = b & 0x7fffffffffffffffull;
+        const bool fin = ab < 0x7ff0000000000000ull;
+        uint64_t code = 0;
+        if (COUNTS) {
+            const bool v = (vm[k] >> lane) & 1;
+            code = !v ? 0 : (fin ? kC1 : ab > 0x7ff0000000000000ull ? kC1 + kCNan
+                                        : kC1 + ((b >> 63) ? kCNinf : kCPinf));
+        }
+        const uint32_t ex = (uint32_t)(b >> 52) & 0x7FF;
+        const uint64_t m = fin ? ((b & 0x000FFFFFFFFFFFFFull) | ((uint64_t)(ex != 0) << 52)) : 0ull;
+        const int sh0 = (int)(ex ? ex : 1) - tmin;
+        const uint32_t sh = sh0 < 0 ? 0u : (uint32_t)sh0;
+        const uint64_t t = m << sh;  // |t| < 2^63
+        const unsigned __int128 u = (unsigned __int128)t * t;
+        uint64_t f1 = (b >> 63) ? 0ull - t : t;
+        uint64_t f2l = (uint64_t)u, f2h = (uint64_t)(u >> 64);
+        f1 = wave_scan64(f1) + c1;
+        c1 = lane63(f1);
+        wave_scan128(f2l, f2h);
+        add128(f2l, f2h, c2l, c2h);
+        c2l = lane63(f2l);
+        c2h = lane63(f2h);
+        const int slot = ((k & 3) << 6) | lane;
+        r1[slot] = f1;
+        r2l[slot] = f2l;
+        r2h[slot] = f2h;
+        if (COUNTS) {
+            code = wave_scan64(code) + ccn;
+            ccn = lane63(code);
+            rcn[slot] = code;
+        }
+        wave_sync();
+        if (k == 0) continue;
+        const int q = k - 1;
+        if (o_first + 64 * q >= o_end) break;
+        const int64_t i = o_first + 64 * q + lane;
+        int64_t s, e;
+        if (interior) {
+            s = i - left;
+            e = i + right;
+        } else {
+            rl_bounds(p, i, s, e);
+        }
+        const int je = (int)(e - 1 - s_first), js = (int)(s - 1 - s_first);
+        const int ie = je & (kRwRing - 1), is = js & (kRwRing - 1);
+        const int64_t S1 = (int64_t)(r1[ie] - (js >= 0 ? r1[is] : 0ull));
+        uint64_t s2l = r2l[ie], s2h = r2h[ie];
+        if (js >= 0) {
+            add128(s2l, s2h, ~r2l[is], ~r2h[is]);
+            add128(s2l, s2h, 1, 0);
+        }
+        RlCounts cn;
+        if (COUNTS) cn = rl_unpack(rcn[ie] - (js >= 0 ? rcn[is] : 0ull));
+        else cn = RlCounts{e - s, 0, 0, 0};
+        const uint64_t c = (uint64_t)cn.nn;
+        const bool valid = i < o_end && cn.nn >= p.min_periods && cn.nn > p.ddof;
+        if (i < o_end) {
+            // num = c * S2 - S1^2, exact in 192 bits
+            const unsigned __int128 lo = (unsigned __int128)s2l * c;
+            const unsigned __int128 hi = (unsigned __int128)s2h * c + (uint64_t)(lo >> 64);
+            uint64_t w0 = (uint64_t)lo, w1 = (uint64_t)hi, w2 = (uint64_t)(hi >> 64);
+            const uint64_t a1 = (uint64_t)(S1 < 0 ? -S1 : S1);
+            const unsigned __int128 q2 = (unsigned __int128)a1 * a1;
+            const uint64_t q0 = (uint64_t)q2, q1 = (uint64_t)(q2 >> 64);
+            const uint64_t b0 = w0 < q0 ? 1ull : 0ull;
+            w0 -= q0;
+            const unsigned __int128 d1 = (unsigned __int128)w1 - q1 - b0;
+            w1 = (uint64_t)d1;
+            w2 -= (uint64_t)(d1 >> 64) ? 1ull : 0ull;
+            double v = 0.0;
+            if (valid) {
+                if (COUNTS && (cn.nan || cn.pinf || cn.ninf)) {
+                    v = __builtin_nan("");
+                } else {
+                    const double nr = (int64_t)w2 < 0 ? 0.0 : u192_to_double(w0, w1, w2, 2 * bottom);
+                    v = (nr / (double)c) / (double)(c - (uint64_t)p.ddof);
+                }
+                if (p.var == 2) v = rv_std(p, v);
+            }
+            ((double*)p.out)[i] = valid ? v : 0.0;
+        }
+        const uint64_t bits = __ballot(valid);
+        if (lane == 0) p.out_valid[(o_first >> 6) + q] = bits;
+        wave_sync();
+    }
+}
+
+template <int DT, bool NULLABLE, bool VAR = false>
 __global__ __launch_bounds__(256) void rl_wave_kernel(RlParams p) {
     __shared__ uint64_t ring_lo[kRwWaves][kRwRing];
     __shared__ uint64_t ring_hi[kRwWaves][kRwRing];
     __shared__ uint64_t ring_cn[kRwWaves][kRwRing];
+    __shared__ uint64_t ring_v2[VAR ? kRwWaves : 1][VAR ? kRwRing : 1];  // var: the t^2 prefixes' high words
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
     const int64_t o_first = ((int64_t)blockIdx.x * kRwWaves + wv) * kRwOut;
@@ -553,7 +821,7 @@ __global__ __launch_bounds__(256) void rl_wave_kernel(RlParams p) {
     const int64_t o_end = o_first + kRwOut < p.n ? o_first + kRwOut : p.n;
     int64_t s_first, tmp;
     rl_bounds(p, o_first, s_first, tmp);
-    const bool isint = p.out_int != 0;
+    const bool isint = p.out_int != 0;  // (var / std: integers enter as their f64 values)
 
     // 1. load the rows [s_first, s_first + 64 * (kRwChunks + 1)) into registers
     uint64_t x[kRwChunks + 1];
@@ -599,6 +867,18 @@ __global__ __launch_bounds__(256) void rl_wave_kernel(RlParams p) {
     int lw = 0;
     while ((int64_t(1) << lw) <= p.w) ++lw;  // p.w < 2^lw
     const int span = tmax - tmin;
+    if (VAR) {
+        // fast form: t < 2^63 with window sums in 64 bits, t^2's window
+        // sums in 127 bits, and no result near the subnormal range
+        const bool vfast = mx == 0 || (tmin >= 600 && lw + 53 + span <= 63 && 2 * (53 + span) + lw <= 126);
+        if (!vfast) {
+            rw_var_exact_outputs(p, o_first, o_end);
+            return;
+        }
+        if (counts) rw_var_scan<true>(p, x, vm, o_first, o_end, s_first, tmin, rlo, rhi, ring_v2[wv], rcn);
+        else rw_var_scan<false>(p, x, vm, o_first, o_end, s_first, tmin, rlo, rhi, ring_v2[wv], rcn);
+        return;
+    }
     // int64 when any window's sum fits 63 bits and results cannot be subnormal
     const bool narrow = mx == 0 || (tmin >= 128 && lw + 53 + span <= 63);
     if (!narrow && lw + 53 + span > 127) {
@@ -616,6 +896,30 @@ __global__ __launch_bounds__(256) void rl_wave_kernel(RlParams p) {
         else PLGPU_RW(2, false);
     }
 #undef PLGPU_RW
+}
+
+// rolling var / std over windows wider than the wave kernel's: each output
+// from its exact window sums (rv_window_exact; O(window) per output).
+__global__ void rl_direct_var_kernel(RlParams p) {
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < p.n; base += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = base + threadIdx.x;
+        bool valid = false;
+        if (i < p.n) {
+            int64_t s, e;
+            rl_bounds(p, i, s, e);
+            RlCounts k = {0, 0, 0, 0};
+            for (int64_t r = s; r < e; ++r) rl_count(p, r, k);
+            valid = k.nn >= p.min_periods && k.nn > p.ddof;
+            double v = 0.0;
+            if (valid) {
+                v = (k.nan || k.pinf || k.ninf) ? __builtin_nan("") : rv_window_exact(p, s, e, k.nn);
+                if (p.var == 2) v = rv_std(p, v);
+            }
+            ((double*)p.out)[i] = valid ? v : 0.0;
+        }
+        const uint64_t wv = __ballot(valid);
+        if ((threadIdx.x & 63) == 0 && i < p.n) p.out_valid[i >> 6] = wv;
+    }
 }
 
 // Windows too wide for the LDS stage: per-output direct summation.
@@ -880,7 +1184,13 @@ PLGPU_API int plgpu_rolling(const plgpu_column* values, int32_t kind, int64_t wi
     hipStream_t s = as_stream(stream);
     if (values == nullptr || out == nullptr) return fail(PLGPU_ERR_INVALID, "NULL argument");
     std::memset(out, 0, sizeof *out);
-    if (kind < PLGPU_ROLLING_SUM || kind > PLGPU_ROLLING_MAX) return fail(PLGPU_ERR_INVALID, "unknown rolling kind");
+    // bits 8..15: ddof; bit 16 (std of a Float32 column): the variance is
+    // rounded to Float32 before the square root, as the reference's f32 sqrt
+    const int32_t base = kind & 0xFF, ddof = (kind >> 8) & 0xFF, var_f32 = (kind >> 16) & 1;
+    if (base < PLGPU_ROLLING_SUM || base > PLGPU_ROLLING_STD) return fail(PLGPU_ERR_INVALID, "unknown rolling kind");
+    const bool var = base == PLGPU_ROLLING_VAR || base == PLGPU_ROLLING_STD;
+    if (!var && ddof != 0) return fail(PLGPU_ERR_INVALID, "ddof applies to rolling var / std only");
+    kind = base;
     if (values->dtype != PLGPU_F64 && values->dtype != PLGPU_I64 && values->dtype != PLGPU_I32)
         return fail(PLGPU_ERR_SCHEMA, "rolling input must be Float64 / Int64 / Int32");
     if (window_size < 1) return fail(PLGPU_ERR_INVALID, "window_size must be >= 1");
@@ -900,8 +1210,11 @@ PLGPU_API int plgpu_rolling(const plgpu_column* values, int32_t kind, int64_t wi
     p.min_periods = min_periods;
     p.center = center != 0;
     p.mean = kind == PLGPU_ROLLING_MEAN;
+    p.var = var ? (kind == PLGPU_ROLLING_STD ? 2 : 1) : 0;
+    p.ddof = ddof;
+    p.var_f32 = var_f32;
     p.isf = values->dtype == PLGPU_F64;
-    p.out_int = (!p.mean && !p.isf) ? values->dtype : 0;
+    p.out_int = (!p.mean && !var && !p.isf) ? values->dtype : 0;
     const int32_t odt = p.out_int ? values->dtype : PLGPU_F64;
     int rc = make_owned_column(out, odt, p.n, true, s);
     if (rc || p.n == 0) return rc;
@@ -911,8 +1224,19 @@ PLGPU_API int plgpu_rolling(const plgpu_column* values, int32_t kind, int64_t wi
     if (window_size <= kRwMaxW) {
         const unsigned g = (unsigned)((p.n + (int64_t)kRwOut * kRwWaves - 1) / ((int64_t)kRwOut * kRwWaves));
         const bool nl = p.c.validity != nullptr;
-        KtScope kt("rl_wave_kernel", s);
-        if (values->dtype == PLGPU_F64) {
+        KtScope kt(var ? "rl_wave_var_kernel" : "rl_wave_kernel", s);
+        if (var) {
+            if (values->dtype == PLGPU_F64) {
+                if (nl) rl_wave_kernel<PLGPU_F64, true, true><<<g, 64 * kRwWaves, 0, s>>>(p);
+                else rl_wave_kernel<PLGPU_F64, false, true><<<g, 64 * kRwWaves, 0, s>>>(p);
+            } else if (values->dtype == PLGPU_I64) {
+                if (nl) rl_wave_kernel<PLGPU_I64, true, true><<<g, 64 * kRwWaves, 0, s>>>(p);
+                else rl_wave_kernel<PLGPU_I64, false, true><<<g, 64 * kRwWaves, 0, s>>>(p);
+            } else {
+                if (nl) rl_wave_kernel<PLGPU_I32, true, true><<<g, 64 * kRwWaves, 0, s>>>(p);
+                else rl_wave_kernel<PLGPU_I32, false, true><<<g, 64 * kRwWaves, 0, s>>>(p);
+            }
+        } else if (values->dtype == PLGPU_F64) {
             if (nl) rl_wave_kernel<PLGPU_F64, true><<<g, 64 * kRwWaves, 0, s>>>(p);
             else rl_wave_kernel<PLGPU_F64, false><<<g, 64 * kRwWaves, 0, s>>>(p);
         } else if (values->dtype == PLGPU_I64) {
@@ -922,7 +1246,9 @@ PLGPU_API int plgpu_rolling(const plgpu_column* values, int32_t kind, int64_t wi
             if (nl) rl_wave_kernel<PLGPU_I32, true><<<g, 64 * kRwWaves, 0, s>>>(p);
             else rl_wave_kernel<PLGPU_I32, false><<<g, 64 * kRwWaves, 0, s>>>(p);
         }
-    } else if (window_size - 1 + kRlOut <= 2048)
+    } else if (var)
+        rl_direct_var_kernel<<<(unsigned)std::min<int64_t>((p.n + 255) / 256, 256 * 64), 256, 0, s>>>(p);
+    else if (window_size - 1 + kRlOut <= 2048)
         rl_tile_kernel<2048><<<(unsigned)tiles, kRlThreads, 0, s>>>(p);
     else if (window_size - 1 + kRlOut <= 4096)
         rl_tile_kernel<4096><<<(unsigned)tiles, kRlThreads, 0, s>>>(p);

@@ -61,6 +61,7 @@ const OptField kOptFields[] = {
     {"part_bits", "PLGPU_PART_BITS", &Options::part_bits},
     {"part_levels", "PLGPU_PART_LEVELS", &Options::part_levels},
     {"part_direct", "PLGPU_PART_DIRECT", &Options::part_direct},
+    {"part_lds_kb", "PLGPU_PART_LDS_KB", &Options::part_lds_kb},
 };
 const OptField* opt_field(const char* name) {
     for (const OptField& f : kOptFields)

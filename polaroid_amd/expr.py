@@ -222,6 +222,16 @@ class Expr:
         """Fixed-window maximum (Expr.rolling_max; a NaN in the window propagates)."""
         return _rolling(self, "max", window_size, weights, min_samples, center)
 
+    def rolling_var(self, window_size: int, weights=None, *, min_samples: int | None = None,
+                    center: bool = False, ddof: int = 1) -> "Expr":
+        """Fixed-window variance (Expr.rolling_var; a non-finite value gives NaN)."""
+        return _rolling(self, "var", window_size, weights, min_samples, center, ddof)
+
+    def rolling_std(self, window_size: int, weights=None, *, min_samples: int | None = None,
+                    center: bool = False, ddof: int = 1) -> "Expr":
+        """Fixed-window standard deviation (Expr.rolling_std)."""
+        return _rolling(self, "std", window_size, weights, min_samples, center, ddof)
+
     def sort(self, *, descending: bool = False, nulls_last: bool = False) -> "Expr":
         return Expr("sort", (self,), op="sort", value=(bool(descending), bool(nulls_last)))
 
@@ -229,7 +239,7 @@ class Expr:
         return Expr("sort", (self,), op="arg_sort", value=(bool(descending), bool(nulls_last)))
 
 
-def _rolling(e: Expr, kind: str, window_size: int, weights, min_samples, center) -> Expr:
+def _rolling(e: Expr, kind: str, window_size: int, weights, min_samples, center, ddof: int = 0) -> Expr:
     if weights is not None:
         raise N.InvalidOperationError("weighted rolling windows are not supported on the GPU executor")
     if not isinstance(window_size, int) or window_size < 1:
@@ -237,7 +247,9 @@ def _rolling(e: Expr, kind: str, window_size: int, weights, min_samples, center)
     ms = window_size if min_samples is None else int(min_samples)
     if ms > window_size:
         raise N.InvalidOperationError("`min_samples` should be <= `window_size`")
-    return Expr("rolling", (e,), op=kind, value=(window_size, ms, bool(center)))
+    if not 0 <= int(ddof) <= 255:
+        raise N.InvalidOperationError("`ddof` must be in 0..255")
+    return Expr("rolling", (e,), op=kind, value=(window_size, ms, bool(center), int(ddof)))
 
 
 def _to_expr(v: Any) -> Expr:

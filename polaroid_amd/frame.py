@@ -539,13 +539,32 @@ class Series:
         return _eval(Expr("cast", (col(self.name),), op="non-strict", value=dtype),
                      DataFrame([self])).alias(self.name)._with_logical(None)
 
-    def _rolling(self, kind: int, window_size: int, min_samples: int | None, center: bool) -> "Series":
+    def _rolling(self, kind: int, window_size: int, min_samples: int | None, center: bool,
+                 ddof: int = 0) -> "Series":
         """Fixed windows over Int32 / Int64 / Float64 on the device; the other
         dtypes the way polars-time's rolling dispatch takes them
         (rolling_window/dispatch.rs:228): rolling_sum of Int8 / Int16 / UInt8 /
         UInt16 sums as Int64, means of integers are Float64; Float32 runs as
-        Float64 and is rounded back; min / max keep the dtype."""
+        Float64 and is rounded back; min / max keep the dtype.  var / std
+        (dispatch.rs:478,526) run on the values as floats (`to_float`:
+        integers as Float64; Float32 stays Float32, the variance rounded to
+        Float32 before std's square root, as the reference's f32 sqrt)."""
         lg = self._logical_dtype()
+        is_var = kind in (N.ROLLING["var"], N.ROLLING["std"])
+        if is_var:
+            if lg is not None:
+                raise N.InvalidOperationError(f"rolling var / std of a {lg} column is not supported")
+            phys = _BY_CODE[self._col.dtype]
+            src, f32 = self, phys is Float32
+            if phys in (Int8, Int16, UInt8, UInt16, UInt32, UInt64, Float32):
+                src = self._cast_to(Float64)
+            out = N.Column()
+            ms = window_size if min_samples is None else min_samples
+            code = kind | (int(ddof) << 8) | ((1 << 16) if f32 and kind == N.ROLLING["std"] else 0)
+            N.check(N.lib().plgpu_rolling(C.byref(src._col), code, int(window_size), int(ms), int(center),
+                                          C.byref(out), None))
+            res = Series._from_native(self.name, out)
+            return res._cast_to(Float32) if f32 else res
         is_sum_mean = kind in (N.ROLLING["sum"], N.ROLLING["mean"])
         if lg is not None and is_sum_mean and not (kind == N.ROLLING["sum"] and isinstance(lg, Duration)):
             raise N.InvalidOperationError(f"rolling sum / mean of a {lg} column is not supported")
@@ -592,6 +611,22 @@ class Series:
         if weights is not None:
             raise N.InvalidOperationError("weighted rolling windows are not supported on the GPU executor")
         return self._rolling(N.ROLLING["max"], window_size, min_samples, center)
+
+    def rolling_var(self, window_size: int, weights=None, *, min_samples: int | None = None,
+                    center: bool = False, ddof: int = 1) -> "Series":
+        if weights is not None:
+            raise N.InvalidOperationError("weighted rolling windows are not supported on the GPU executor")
+        if min_samples is not None and min_samples > window_size:
+            raise N.InvalidOperationError("`min_samples` should be <= `window_size`")
+        return self._rolling(N.ROLLING["var"], window_size, min_samples, center, ddof)
+
+    def rolling_std(self, window_size: int, weights=None, *, min_samples: int | None = None,
+                    center: bool = False, ddof: int = 1) -> "Series":
+        if weights is not None:
+            raise N.InvalidOperationError("weighted rolling windows are not supported on the GPU executor")
+        if min_samples is not None and min_samples > window_size:
+            raise N.InvalidOperationError("`min_samples` should be <= `window_size`")
+        return self._rolling(N.ROLLING["std"], window_size, min_samples, center, ddof)
 
     # eager conveniences mirroring Series.filter ------------------------------
     def filter(self, mask: "Series") -> "Series":
@@ -1301,8 +1336,8 @@ def _eval(expr: Expr, df: DataFrame) -> Series:
     if base.kind in ("rolling", "sort"):
         inner = _eval(base.args[0], df)
         if base.kind == "rolling":
-            w, ms, center = base.value
-            res = inner._rolling(N.ROLLING[base.op], w, ms, center)
+            w, ms, center, ddof = base.value
+            res = inner._rolling(N.ROLLING[base.op], w, ms, center, ddof)
         elif base.op == "arg_sort":
             res = inner.arg_sort(descending=base.value[0], nulls_last=base.value[1])
         else:

@@ -30,6 +30,38 @@ def unhex(v):
     return v
 
 
+def check_rolling_case(got, case, tag=""):
+    """One transcribed rolling assertion (tests/golden/rolling_cases.json)
+    against `got` (a list, None for null outputs)."""
+    import math
+
+    def same(g, e):
+        if e is None or g is None:
+            return g is None and e is None
+        if isinstance(e, float) and math.isnan(e):
+            return isinstance(g, float) and math.isnan(g)
+        if case.get("approx"):
+            return math.isclose(g, e, rel_tol=1e-6, abs_tol=1e-12)
+        return g == e
+
+    name = (case["name"], tag)
+    if "round" in case:
+        got = [None if g is None else round(g, case["round"]) for g in got]
+    if "expected_null_count" in case:
+        assert sum(g is None for g in got) == case["expected_null_count"], name
+        assert sum(g is None or g != g for g in got) == case["expected_nan_or_null"], name
+    elif "expected_last" in case:
+        assert got[-1] == case["expected_last"], name
+    elif "expected_sum" in case:
+        assert sum(g for g in got if g is not None) == case["expected_sum"], (name, got)
+    elif "expected_at" in case:
+        i, e = case["expected_at"]
+        assert same(got[i], unhex(e) if isinstance(e, str) else e), (name, got)
+    else:
+        exp = [unhex(v) if isinstance(v, str) else v for v in case["expected"]]
+        assert len(got) == len(exp) and all(same(g, e) for g, e in zip(got, exp)), (name, got, exp)
+
+
 @pytest.fixture
 def plgpu_option():
     """Set library options (plgpu_set_option test hooks) for one test; every

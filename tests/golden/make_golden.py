@@ -603,6 +603,45 @@ def rolling_cases():
                       "source": "operations/rolling/test_rolling.py:924-933",
                       "values": [1.0, 2.0, 3.0, nan, 5.0, 6.0, 7.0], "kind": kind, "window": 3, "min": None,
                       "center": False, "expected_null_count": 2, "expected_nan_or_null": 5})
+    # rolling_var / rolling_std (MomentWindow<VarianceMoment>; round 5).
+    # `approx`: the reference test compares with pytest.approx (rel 1e-6).
+    vsrc = "crates/polars-compute/src/rolling/no_nulls/moment.rs:104-133 (test_rolling_var)"
+    for ddof, ms, exp in ((1, 2, [None, 8.0, 2.0, 0.5]), (0, 2, [None, 4.0, 1.0, 0.25]),
+                          (1, 1, [None, 8.0, 2.0, 0.5])):
+        cases.append({"name": f"test_rolling_var(w=2, min={ms}, ddof={ddof})", "source": vsrc,
+                      "values": [1.0, 5.0, 3.0, 4.0], "kind": "var", "window": 2, "min": ms, "center": False,
+                      "ddof": ddof, "expected": exp})
+    cases.append({"name": "test_rolling_var_numerical_stability_5197",
+                  "source": "operations/rolling/test_rolling.py:626-640",
+                  "values": [1.2] * 4 + [3.3] * 7, "kind": "var", "window": 5, "min": None, "center": False,
+                  "ddof": 1, "approx": True,
+                  "expected": [None] * 4 + [0.882, 1.3229999999999997, 1.3229999999999997, 0.8819999999999983,
+                                            0.0, 0.0, 0.0]})
+    for kind, ddof, exp in (("std", 1, 0.7071067811865476), ("var", 1, 0.5), ("std", 0, 0.5), ("var", 0, 0.25)):
+        cases.append({"name": f"test_rolling_ints rolling_{kind}(2, ddof={ddof})[1]",
+                      "source": "operations/rolling/test_rolling.py:893-896",
+                      "values": [1, 2, 3, 2, 1], "kind": kind, "window": 2, "min": None, "center": False,
+                      "ddof": ddof, "approx": True, "expected_at": [1, exp]})
+    cases.append({"name": "test_rolling_std_nulls_min_samples_1_20076",
+                  "source": "operations/rolling/test_rolling.py:956-961",
+                  "values": [1, 2, None, 4], "kind": "std", "window": 3, "min": 1, "center": False, "ddof": 1,
+                  "expected": [None, 0.7071067811865476, 0.7071067811865476, 1.4142135623730951]})
+    cases.append({"name": "test_rolling_var_zero_weight", "source": "operations/test_rolling.py:632-636",
+                  "values": [1.0, None, 1.0, 2.0], "kind": "var", "window": 2, "min": None, "center": False,
+                  "ddof": 1, "expected": [None, None, None, 0.5]})
+    for kind in ("var", "std"):
+        cases.append({"name": f"test_rolling_var_stability_12905 rolling_{kind}(12, min_samples=2).sum() == 0",
+                      "source": "operations/rolling/test_rolling_fixed.py:4-7",
+                      "values": [36743.6] * 10, "kind": kind, "window": 12, "min": 2, "center": False, "ddof": 1,
+                      "expected_sum": 0.0})
+        cases.append({"name": f"test_rolling fruits_cars A rolling_{kind}(3)",
+                      "source": "lazyframe/test_lazyframe.py:747-763 (.round(1))",
+                      "values": [1, 2, 3, 4, 5], "kind": kind, "window": 3, "min": None, "center": False, "ddof": 1,
+                      "round": 1, "expected": [None, None, 1.0, 1.0, 1.0]})
+        cases.append({"name": f"test_rolling fruits_cars A rolling_{kind}(3, min_samples=1)[0] is null",
+                      "source": "lazyframe/test_lazyframe.py:768-775",
+                      "values": [1, 2, 3, 4, 5], "kind": kind, "window": 3, "min": 1, "center": False, "ddof": 1,
+                      "expected_at": [0, None]})
     return {"cases": cases}
 
 

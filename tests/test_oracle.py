@@ -12,7 +12,7 @@ import math
 import numpy as np
 import pytest
 
-from conftest import load_golden, unhex
+from conftest import check_rolling_case, load_golden, unhex
 from oracle import oracle as O
 
 OPS = dict(eq=20, ne=21, lt=22, le=23, gt=24, ge=25, eq_missing=26, ne_missing=27)
@@ -240,23 +240,61 @@ def test_oracle_sort_golden():
 
 
 def test_oracle_rolling_golden():
-    """The restated SumWindow / MeanWindow reproduces every transcribed
-    rolling assertion; the exact mode agrees on these cases."""
+    """The restated SumWindow / MeanWindow / MinMaxWindow / MomentWindow
+    reproduce every transcribed rolling assertion; the exact mode agrees on
+    these cases."""
     for case in load_golden("rolling_cases.json")["cases"]:
         vals = [unhex(v) if isinstance(v, str) else v for v in case["values"]]
         col, _, _ = _host(vals)
         for mode in (O.ROLLING_REFERENCE, O.ROLLING_EXACT):
-            out, ok = O.rolling(col, case["kind"], case["window"], case["min"], case["center"], mode)
+            if case["kind"] in ("var", "std"):
+                out, ok = O.rolling_var(col, case["window"], case["min"], case["center"], case["ddof"],
+                                        case["kind"] == "std", mode)
+            else:
+                out, ok = O.rolling(col, case["kind"], case["window"], case["min"], case["center"], mode)
             got = [v.item() if k else None for v, k in zip(out, ok)]
-            if "expected_null_count" in case:
-                assert sum(g is None for g in got) == case["expected_null_count"], case["name"]
-                assert sum(g is None or g != g for g in got) == case["expected_nan_or_null"], case["name"]
-                continue
-            if "expected_last" in case:
-                assert got[-1] == case["expected_last"], (case["name"], mode)
-                continue
-            exp = [unhex(v) if isinstance(v, str) else v for v in case["expected"]]
-            assert all(_same_val(g, e) for g, e in zip(got, exp)), (case["name"], mode, got, exp)
+            check_rolling_case(got, case, mode)
+
+
+def test_oracle_rolling_var_exact_is_the_exact_rational():
+    """The exact mode of or_rolling_var is (RN(c sum x^2 - (sum x)^2) / c) /
+    (c - ddof) with the numerator rounded once from the exact rational
+    (Fractions), over values spanning 1e-320 .. 1e300, zeros, nulls and
+    centred windows; std is its square root."""
+    from fractions import Fraction
+
+    rng = np.random.default_rng(3)
+    n = 1500
+    x = rng.uniform(10, 500, n) * rng.choice([1.0, -1.0], n)
+    x[::97] = rng.standard_normal(x[::97].shape[0]) * 1e-200
+    x[5] = 1e300
+    x[700:705] = [3e-320, 1e-310, 0.0, -2e-315, 5e-324]
+    valid = rng.random(n) > 0.1
+
+    def tof(f):
+        try:
+            return float(f)
+        except OverflowError:
+            return math.inf
+
+    for w, ms, center, ddof in ((20, 5, False, 1), (7, 1, True, 0), (64, 64, False, 2)):
+        for std in (False, True):
+            out, ok = O.rolling_var(O.HostCol(x, valid), w, ms, center, ddof, std, O.ROLLING_EXACT)
+            for i in range(n):
+                if center:
+                    right = (w + 1) // 2
+                    s, e = max(0, i - (w - right)), min(n, i + right)
+                else:
+                    s, e = max(0, i + 1 - w), i + 1
+                vals = [Fraction(float(t)) for t, v in zip(x[s:e], valid[s:e]) if v]
+                c = len(vals)
+                if c < ms or c <= ddof:
+                    assert not ok[i], (w, i)
+                    continue
+                ref = (tof(c * sum(t * t for t in vals) - sum(vals) ** 2) / c) / (c - ddof)
+                if std:
+                    ref = math.sqrt(ref)
+                assert ok[i] and (out[i] == ref or (math.isinf(ref) and math.isinf(out[i]))), (w, i, out[i], ref)
 
 
 def test_oracle_rolling_reference_vs_exact_ulp():

@@ -14,7 +14,7 @@ sys.path.insert(0, ROOT)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--leg", choices=["headline", "vwap", "std", "filter", "many_groups"], required=True)
+    ap.add_argument("--leg", choices=["headline", "vwap", "std", "filter", "many_groups", "sort", "join"], required=True)
     ap.add_argument("--rows", type=float, default=1e9)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
@@ -26,6 +26,10 @@ def main():
     import polaroid_amd as pl
 
     n = int(args.rows)
+    if args.leg in ("sort", "join"):
+        r = (bench.sort_leg if args.leg == "sort" else bench.join_leg)(torch, pl, args.steps, args.warmup)
+        print(json.dumps({"leg": args.leg, **r}), flush=True)
+        return
     sym, cols = bench.make_data(torch, n, args.groups, seed=1234)
     df = pl.DataFrame([pl.Series.from_torch("symbol", sym)] + [pl.Series.from_torch(c, t) for c, t in cols.items()])
     if args.leg == "vwap":
