@@ -2417,23 +2417,45 @@ struct FinParams {
     uint8_t* vbytes;
 };
 
-__global__ void gb_finalize_kernel(GbParams p, FinParams fp) {
+__global__ __launch_bounds__(256) void gb_finalize_kernel(GbParams p, FinParams fp) {
     const int64_t total = p.gcap + 2;
-    const int lane = threadIdx.x & 63;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    // output positions: one counter add per wave (ballot of its live slots),
-    // not one per group -- a single-address atomic per group serialises
-    // (14k groups: ~0.07 ms; 1e6 groups: milliseconds)
-    for (int64_t s0 = (int64_t)blockIdx.x * blockDim.x; s0 < total; s0 += (int64_t)gridDim.x * blockDim.x) {
+    // output positions: each workgroup owns one contiguous range of slots,
+    // counts its live groups, and takes its output range with ONE counter
+    // add (one add per wave on the single status word serialised: ~6 ms at
+    // 2^25 slots); then each 256-slot chunk's live groups are ranked by
+    // wave ballots and a block prefix
+    __shared__ uint64_t wcnt[4];
+    __shared__ unsigned long long gbase;
+    const int64_t per = (((total + gridDim.x - 1) / gridDim.x) + 255) & ~int64_t(255);
+    const int64_t lo = std::min<int64_t>(total, (int64_t)blockIdx.x * per), hi = std::min<int64_t>(total, lo + per);
+    uint64_t mine = 0;
+    for (int64_t s = lo + threadIdx.x; s < hi; s += blockDim.x) mine += *gfield(p, p.f_len, s) != 0 ? 1 : 0;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) mine += __shfl_xor(mine, off, 64);
+    if (lane == 0) wcnt[wid] = mine;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint64_t t = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+        gbase = t ? atomicAdd((unsigned long long*)&p.status[ST_GROUPS_OUT], (unsigned long long)t) : 0ull;
+    }
+    __syncthreads();
+    uint64_t run = gbase;
+    for (int64_t s0 = lo; s0 < hi; s0 += blockDim.x) {
         const int64_t s = s0 + threadIdx.x;
-        const uint64_t len = s < total ? *gfield(p, p.f_len, s) : 0ull;
+        const uint64_t len = s < hi ? *gfield(p, p.f_len, s) : 0ull;
         const uint64_t live = __ballot(len != 0);
-        if (live == 0) continue;
-        const int first = __ffsll((unsigned long long)live) - 1;
-        unsigned long long base = 0;
-        if (lane == first) base = atomicAdd((unsigned long long*)&p.status[ST_GROUPS_OUT],
-                                            (unsigned long long)__popcll(live));
-        base = __shfl(base, first, 64);
+        __syncthreads();  // the previous chunk's readers of wcnt are done
+        if (lane == 0) wcnt[wid] = (uint64_t)__popcll(live);
+        __syncthreads();
+        uint64_t before = 0, chunk = 0;
+        for (int w = 0; w < 4; ++w) {
+            before += w < wid ? wcnt[w] : 0;
+            chunk += wcnt[w];
+        }
+        const uint64_t base = run + before;
+        run += chunk;
         if (len == 0) continue;
         const int64_t g = (int64_t)base + __popcll(live & lt);
         if (g >= fp.cap) continue;

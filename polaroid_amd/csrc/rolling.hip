@@ -808,23 +808,33 @@ __device__ __forceinline__ void rw_var_scan(const RlParams& p, const uint64_t (&
     }
 }
 
-template <int DT, bool NULLABLE, bool VAR = false>
-__global__ __launch_bounds__(256) void rl_wave_kernel(RlParams p) {
-    __shared__ uint64_t ring_lo[kRwWaves][kRwRing];
-    __shared__ uint64_t ring_hi[kRwWaves][kRwRing];
-    __shared__ uint64_t ring_cn[kRwWaves][kRwRing];
-    __shared__ uint64_t ring_v2[VAR ? kRwWaves : 1][VAR ? kRwRing : 1];  // var: the t^2 prefixes' high words
+// The rows [s_first, s_first + 64 (kRwChunks + 1)) of one wave's block as
+// loaded (the row index clamped to the column, so the loads are
+// branch-free and all in flight together; rows past n are masked by
+// rw_block).  4-byte integers sign-extended.
+template <int DT>
+__device__ __forceinline__ void rw_load_block(const RlParams& p, int64_t s_first, uint64_t (&x)[kRwChunks + 1]) {
     const int lane = threadIdx.x & 63;
-    const int wv = threadIdx.x >> 6;
-    const int64_t o_first = ((int64_t)blockIdx.x * kRwWaves + wv) * kRwOut;
-    if (o_first >= p.n) return;  // (no workgroup barriers below)
-    const int64_t o_end = o_first + kRwOut < p.n ? o_first + kRwOut : p.n;
-    int64_t s_first, tmp;
-    rl_bounds(p, o_first, s_first, tmp);
-    const bool isint = p.out_int != 0;  // (var / std: integers enter as their f64 values)
+    const int64_t last = p.n - 1;
+#pragma unroll
+    for (int k = 0; k <= kRwChunks; ++k) {
+        int64_t r = s_first + 64 * k + lane;
+        r = r < last ? r : last;
+        const int64_t q = p.c.offset + r;
+        if (DT == PLGPU_F64 || DT == PLGPU_I64) x[k] = __builtin_nontemporal_load((const uint64_t*)p.c.values + q);
+        else x[k] = (uint64_t)(int64_t)__builtin_nontemporal_load((const int32_t*)p.c.values + q);
+    }
+}
 
-    // 1. load the rows [s_first, s_first + 64 * (kRwChunks + 1)) into registers
-    uint64_t x[kRwChunks + 1];
+// One wave's block of kRwOut outputs from its loaded rows: validity, the
+// exponent range and the number format, then the scan + emit.
+template <int DT, bool NULLABLE, bool VAR>
+__device__ __forceinline__ void rw_block(const RlParams& p, uint64_t (&x)[kRwChunks + 1], int64_t o_first,
+                                         int64_t s_first, uint64_t* rlo, uint64_t* rhi, uint64_t* rcn,
+                                         uint64_t* rv2) {
+    const int lane = threadIdx.x & 63;
+    const int64_t o_end = o_first + kRwOut < p.n ? o_first + kRwOut : p.n;
+    const bool isint = p.out_int != 0;  // (var / std: integers enter as their f64 values)
     uint64_t vm[kRwChunks + 1];
     uint32_t mx = 0, inv_mn = 0;
     bool odd = false;  // a null (in range) or a non-finite value
@@ -833,7 +843,7 @@ __global__ __launch_bounds__(256) void rl_wave_kernel(RlParams p) {
         const int64_t r = s_first + 64 * k + lane;
         const bool in = r < p.n;
         const bool v = in && (!NULLABLE || dev_valid(p.c, r));
-        const uint64_t b = in ? rw_load<DT>(p, r, !isint) : 0ull;
+        const uint64_t b = (DT == PLGPU_F64 || isint) ? x[k] : f64_bits((double)(int64_t)x[k]);
         vm[k] = __ballot(v);
         x[k] = v ? b : 0ull;
         if (NULLABLE) odd |= in && !v;
@@ -848,9 +858,6 @@ __global__ __launch_bounds__(256) void rl_wave_kernel(RlParams p) {
         }
     }
     const bool counts = __ballot(odd) != 0;
-    uint64_t* rlo = ring_lo[wv];
-    uint64_t* rhi = ring_hi[wv];
-    uint64_t* rcn = ring_cn[wv];
     if (isint) {
         // (the exponent fields of integers mean nothing; only nulls count)
         if (__ballot(NULLABLE && odd) != 0) rw_scan<0, true, false>(p, x, vm, o_first, o_end, s_first, 0, rlo, rhi, rcn);
@@ -875,8 +882,8 @@ __global__ __launch_bounds__(256) void rl_wave_kernel(RlParams p) {
             rw_var_exact_outputs(p, o_first, o_end);
             return;
         }
-        if (counts) rw_var_scan<true>(p, x, vm, o_first, o_end, s_first, tmin, rlo, rhi, ring_v2[wv], rcn);
-        else rw_var_scan<false>(p, x, vm, o_first, o_end, s_first, tmin, rlo, rhi, ring_v2[wv], rcn);
+        if (counts) rw_var_scan<true>(p, x, vm, o_first, o_end, s_first, tmin, rlo, rhi, rv2, rcn);
+        else rw_var_scan<false>(p, x, vm, o_first, o_end, s_first, tmin, rlo, rhi, rv2, rcn);
         return;
     }
     // int64 when any window's sum fits 63 bits and results cannot be subnormal
@@ -896,6 +903,58 @@ __global__ __launch_bounds__(256) void rl_wave_kernel(RlParams p) {
         else PLGPU_RW(2, false);
     }
 #undef PLGPU_RW
+}
+
+// One block of kRwOut outputs per wave.
+template <int DT, bool NULLABLE, bool VAR = false>
+__global__ __launch_bounds__(256) void rl_wave_kernel(RlParams p) {
+    __shared__ uint64_t ring_lo[kRwWaves][kRwRing];
+    __shared__ uint64_t ring_hi[kRwWaves][kRwRing];
+    __shared__ uint64_t ring_cn[kRwWaves][kRwRing];
+    __shared__ uint64_t ring_v2[VAR ? kRwWaves : 1][VAR ? kRwRing : 1];  // var: the t^2 prefixes' high words
+    const int wv = threadIdx.x >> 6;
+    const int64_t o_first = ((int64_t)blockIdx.x * kRwWaves + wv) * kRwOut;
+    if (o_first >= p.n) return;  // (no workgroup barriers below)
+    int64_t s_first, tmp;
+    rl_bounds(p, o_first, s_first, tmp);
+    uint64_t x[kRwChunks + 1];
+    rw_load_block<DT>(p, s_first, x);
+    rw_block<DT, NULLABLE, VAR>(p, x, o_first, s_first, ring_lo[wv], ring_hi[wv], ring_cn[wv],
+                                VAR ? ring_v2[wv] : nullptr);
+}
+
+// Resident waves, each over blocks b, b + stride, ...: the next block's
+// rows are loaded before this block is scanned, so every wave keeps its
+// loads in flight while it computes (the one-block form waits for them).
+template <int DT, bool VAR = false>
+__global__ __launch_bounds__(256) void rl_stream_kernel(RlParams p) {
+    __shared__ uint64_t ring_lo[kRwWaves][kRwRing];
+    __shared__ uint64_t ring_hi[kRwWaves][kRwRing];
+    __shared__ uint64_t ring_cn[kRwWaves][kRwRing];
+    __shared__ uint64_t ring_v2[VAR ? kRwWaves : 1][VAR ? kRwRing : 1];
+    const int wv = threadIdx.x >> 6;
+    const int64_t nblocks = (p.n + kRwOut - 1) / kRwOut;
+    const int64_t stride = (int64_t)gridDim.x * kRwWaves;
+    int64_t b = (int64_t)blockIdx.x * kRwWaves + wv;
+    if (b >= nblocks) return;  // (no workgroup barriers below)
+    int64_t s_first, tmp;
+    rl_bounds(p, b * kRwOut, s_first, tmp);
+    uint64_t x[kRwChunks + 1];
+    rw_load_block<DT>(p, s_first, x);
+    for (; b < nblocks; b += stride) {
+        const int64_t bn = b + stride;
+        int64_t sn = 0;
+        uint64_t xn[kRwChunks + 1];
+        if (bn < nblocks) {
+            rl_bounds(p, bn * kRwOut, sn, tmp);
+            rw_load_block<DT>(p, sn, xn);
+        }
+        rw_block<DT, false, VAR>(p, x, b * kRwOut, s_first, ring_lo[wv], ring_hi[wv], ring_cn[wv],
+                                 VAR ? ring_v2[wv] : nullptr);
+#pragma unroll
+        for (int k = 0; k <= kRwChunks; ++k) x[k] = xn[k];
+        s_first = sn;
+    }
 }
 
 // rolling var / std over windows wider than the wave kernel's: each output
@@ -1179,6 +1238,18 @@ static int rolling_minmax(const plgpu_column* values, bool is_max, int64_t w, in
     return rc;
 }
 
+static int num_cus_rl() {
+    static int n = 0;
+    if (n == 0) {
+        int dev = 0;
+        hipDeviceProp_t prop;
+        n = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+                ? prop.multiProcessorCount
+                : 256;
+    }
+    return n;
+}
+
 PLGPU_API int plgpu_rolling(const plgpu_column* values, int32_t kind, int64_t window_size, int64_t min_periods,
                             int32_t center, plgpu_column* out, void* stream) {
     hipStream_t s = as_stream(stream);
@@ -1225,7 +1296,21 @@ PLGPU_API int plgpu_rolling(const plgpu_column* values, int32_t kind, int64_t wi
         const unsigned g = (unsigned)((p.n + (int64_t)kRwOut * kRwWaves - 1) / ((int64_t)kRwOut * kRwWaves));
         const bool nl = p.c.validity != nullptr;
         KtScope kt(var ? "rl_wave_var_kernel" : "rl_wave_kernel", s);
-        if (var) {
+        if (!nl && options().rl_stream != 0) {
+            // null-free: resident waves streaming their blocks
+            const int per_cu = options().rl_grid > 0 ? options().rl_grid : 4;
+            const unsigned gs = (unsigned)std::max<int64_t>(1, std::min<int64_t>((int64_t)g, (int64_t)num_cus_rl() * per_cu));
+            if (values->dtype == PLGPU_F64) {
+                if (var) rl_stream_kernel<PLGPU_F64, true><<<gs, 64 * kRwWaves, 0, s>>>(p);
+                else rl_stream_kernel<PLGPU_F64, false><<<gs, 64 * kRwWaves, 0, s>>>(p);
+            } else if (values->dtype == PLGPU_I64) {
+                if (var) rl_stream_kernel<PLGPU_I64, true><<<gs, 64 * kRwWaves, 0, s>>>(p);
+                else rl_stream_kernel<PLGPU_I64, false><<<gs, 64 * kRwWaves, 0, s>>>(p);
+            } else {
+                if (var) rl_stream_kernel<PLGPU_I32, true><<<gs, 64 * kRwWaves, 0, s>>>(p);
+                else rl_stream_kernel<PLGPU_I32, false><<<gs, 64 * kRwWaves, 0, s>>>(p);
+            }
+        } else if (var) {
             if (values->dtype == PLGPU_F64) {
                 if (nl) rl_wave_kernel<PLGPU_F64, true, true><<<g, 64 * kRwWaves, 0, s>>>(p);
                 else rl_wave_kernel<PLGPU_F64, false, true><<<g, 64 * kRwWaves, 0, s>>>(p);

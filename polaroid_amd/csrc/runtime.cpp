@@ -62,6 +62,8 @@ const OptField kOptFields[] = {
     {"part_levels", "PLGPU_PART_LEVELS", &Options::part_levels},
     {"part_direct", "PLGPU_PART_DIRECT", &Options::part_direct},
     {"part_lds_kb", "PLGPU_PART_LDS_KB", &Options::part_lds_kb},
+    {"rl_stream", "PLGPU_RL_STREAM", &Options::rl_stream},
+    {"rl_grid", "PLGPU_RL_GRID", &Options::rl_grid},
 };
 const OptField* opt_field(const char* name) {
     for (const OptField& f : kOptFields)

@@ -36,19 +36,28 @@ def main():
     else:
         x = torch.randn(n, device="cuda", generator=g, dtype=torch.float64)
         x *= torch.exp2(torch.randint(-20, 20, (n,), device="cuda", generator=g).to(torch.float64))
+    from polaroid_amd import _native as N
+
     s = pl.Series.from_torch("x", x)
     fn = getattr(s, "rolling_" + args.kind)
     fn(args.window, center=args.center)
     torch.cuda.synchronize()
+    N.set_option("ktime", 1)
+    N.ktime_read(reset=True)
     ts = []
     for _ in range(args.steps):
         t0 = time.perf_counter()
         fn(args.window, center=args.center)
         torch.cuda.synchronize()
         ts.append(time.perf_counter() - t0)
+    kt = N.ktime_read(reset=True)
     t = min(ts)
+    kern = {k: round(ms / max(c, 1), 4) for k, (ms, c) in kt.items()}
+    km = max(kern.values()) if kern else None
     print(json.dumps({"rows": n, "window": args.window, "kind": args.kind, "center": args.center, "data": args.data,
-                      "ms": round(t * 1e3, 3), "GBps_algorithmic": round(16 * n / t / 1e9, 1)}), flush=True)
+                      "ms": round(t * 1e3, 3), "GBps_algorithmic": round(16 * n / t / 1e9, 1), "kernel_ms": kern,
+                      "kernel_frac": round(16 * n / (km * 1e-3) / 1e9 / 8000.0, 4) if km else None,
+                      "options": {k: v for k, v in os.environ.items() if k.startswith("PLGPU_")}}), flush=True)
 
 
 if __name__ == "__main__":
