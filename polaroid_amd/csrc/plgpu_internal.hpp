@@ -52,8 +52,9 @@ struct Options {
     int part_levels = -1; // partitioned path: 1 / 2 scatter passes (-1: by the partition bits)
     int part_direct = 1;  // partitioned path: one-workgroup partitions flush into their own table region
     int part_lds_kb = 0;  // partitioned path: LDS table budget per workgroup (0: 160 KiB)
-    int rl_stream = 1;    // rolling windows <= 64, null-free: resident streaming waves (0: one block per wave)
+    int rl_stream = 0;    // rolling windows <= 64, null-free: resident streaming waves (0: one block per wave; A/B)
     int rl_grid = 0;      // rolling stream kernel: workgroups per CU (0: 4)
+    int rl_occ = 0;       // rolling wave kernel (Float64, null-free): 6 = register cap for 6 waves per SIMD (A/B)
 };
 Options& options();
 
