@@ -420,13 +420,34 @@ int plgpu_gb_plan_bottoms(const plgpu_column* key, const plgpu_column* cols, int
  * the hint equals the used windows).  The windows used come back in
  * out_bottoms_used[6].  Returns a handle holding the partial table and the
  * number of groups (*out_records).  A column whose values need the wide
- * (multi-window) sum is refused with PLGPU_ERR_CAPACITY. */
+ * (multi-window) sum keeps exact per-group digit states instead: the ranks
+ * agree one digit range per column (plgpu_gb_partial_wide, a max all-reduce,
+ * plgpu_gb_partial_set_wide) before the export. */
 int plgpu_gb_partial_begin(const plgpu_column* key, const plgpu_column* cols, int32_t ncols,
                            const plgpu_instr* program, int32_t n_instr, const plgpu_agg* aggs,
                            int32_t naggs, const int32_t* bottoms, int32_t world,
                            plgpu_gb_partial** out, int64_t* out_records, int32_t* out_bottoms_used,
                            int32_t* out_refit, int32_t* out_bottoms_hint,
                            plgpu_groupby_info* info, void* stream);
+
+/* Wide f64 sums across ranks (round 5; polars-stream/src/nodes/group_by.rs:85
+ * add_pre_agg ships fixed-size pre-aggregates whatever the values): per acc
+ * a, out_wide[a] = 1 when this shard's values of that f64 sum span more
+ * binades than one fixed-point window, and [out_exmin[a], out_exmax[a]] the
+ * biased exponents its values take (the window's range for a non-wide f64
+ * sum; 0x7FF / 0 for other accs).  The ranks reduce (max of wide, min of
+ * exmin, max of exmax); when any wide[a] is set, every rank calls
+ * plgpu_gb_partial_set_wide with the reduced arrays: those columns' states
+ * become per-group digit words (24-bit digits in int64 words, the single-GPU
+ * wide sum's form) over the agreed range, appended to every record, and
+ * plgpu_gb_merge_sources_wide adds them and rounds each group once.  The
+ * result is bit-identical to the single-GPU group-by.  Record words then
+ * come from plgpu_gb_partial_record_words. */
+int plgpu_gb_partial_wide(const plgpu_gb_partial* h, int32_t* out_wide, int32_t* out_exmin,
+                          int32_t* out_exmax);
+int plgpu_gb_partial_set_wide(plgpu_gb_partial* h, const int32_t* wide, const int32_t* exmin,
+                              const int32_t* exmax);
+int plgpu_gb_partial_record_words(const plgpu_gb_partial* h, int32_t* out_words);
 
 /* Write the partial groups as records into device buffer `dst_records`
  * (out_records * record_words u64), grouped by destination rank in rank
@@ -490,6 +511,15 @@ int plgpu_gb_merge_sources(const void* records, int32_t n_sources, const int64_t
                            const plgpu_agg* aggs, int32_t naggs, int32_t key_dtype,
                            plgpu_column* out_key, plgpu_column* out_aggs, plgpu_groupby_info* info,
                            void* stream);
+
+/* plgpu_gb_merge_sources for records carrying wide digit states (the
+ * reduced wide / exmin / exmax of plgpu_gb_partial_set_wide). */
+int plgpu_gb_merge_sources_wide(const void* records, int32_t n_sources, const int64_t* src_records,
+                                const int32_t* src_bottoms, const int32_t* wide,
+                                const int32_t* wide_exmin, const int32_t* wide_exmax,
+                                const plgpu_column* cols, int32_t ncols, const plgpu_agg* aggs,
+                                int32_t naggs, int32_t key_dtype, plgpu_column* out_key,
+                                plgpu_column* out_aggs, plgpu_groupby_info* info, void* stream);
 
 /* ---- hash join ------------------------------------------------------------
  * maintain_order (polars-ops/src/frame/join/args.rs:100 MaintainOrderJoin)

@@ -147,6 +147,10 @@ SIGNATURES = {
                                          C.POINTER(GroupByInfo), _P]),
     "plgpu_gb_partial_export": (C.c_int, [_P, _P, C.POINTER(C.c_int64), _P]),
     "plgpu_gb_partial_free": (None, [_P]),
+    "plgpu_gb_partial_wide": (C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "plgpu_gb_partial_set_wide": (C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                                            C.POINTER(C.c_int32)]),
+    "plgpu_gb_partial_record_words": (C.c_int, [_P, C.POINTER(C.c_int32)]),
     "plgpu_gb_route": (C.c_int, [_COLP, C.c_int32, _COLP, C.POINTER(C.c_int64), _P]),
     "plgpu_key_ranges": (C.c_int, [_COLP, C.c_int32, C.POINTER(C.c_int64), _P]),
     "plgpu_float_key_encode": (C.c_int, [_COLP, _COLP, _P]),
@@ -158,6 +162,10 @@ SIGNATURES = {
     "plgpu_gb_merge_sources": (C.c_int, [_P, C.c_int32, C.POINTER(C.c_int64), C.POINTER(C.c_int32), _COLP,
                                          C.c_int32, C.POINTER(Agg), C.c_int32, C.c_int32, _COLP, _COLP,
                                          C.POINTER(GroupByInfo), _P]),
+    "plgpu_gb_merge_sources_wide": (C.c_int, [_P, C.c_int32, C.POINTER(C.c_int64), C.POINTER(C.c_int32),
+                                              C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                                              _COLP, C.c_int32, C.POINTER(Agg), C.c_int32, C.c_int32, _COLP, _COLP,
+                                              C.POINTER(GroupByInfo), _P]),
     "plgpu_join_inner_multi": (C.c_int, [_COLP, _COLP, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _COLP, _COLP,
                                          _P]),
     "plgpu_join_inner": (C.c_int, [_COLP, _COLP, C.c_int32, C.c_int32, C.c_int32, _COLP, _COLP, _P]),

@@ -412,6 +412,22 @@ __global__ __launch_bounds__(256) void gb_maxexp_kernel(GbParams p, int a) {
 // (half-even), so the sum is still the correctly rounded exact sum.
 constexpr int kWideDigit = 24;
 
+// Digit words per group of a wide sum whose values' biased exponents lie in
+// [exmin, exmax] (six words of headroom for the carries of the group's sum).
+static inline int wide_nwords(int exmin, int exmax) { return (exmax - exmin) / kWideDigit + 6; }
+
+// Wide f64 sums in the multi-GPU partial-state records: per wide acc (acc
+// order) the group's digit words over the ranks' agreed exponent range,
+// appended after the record's fields.  `digits`: the table's digit arrays
+// (slots x nwords).
+struct WideRec {
+    int32_t n;
+    int32_t acc[kMaxAcc];
+    int32_t nwords[kMaxAcc];
+    int32_t off[kMaxAcc];  // word offset of acc i's digits from the record start
+    int64_t* digits[kMaxAcc];
+};
+
 template <int PRED>
 __global__ __launch_bounds__(256) void gb_wide_kernel(GbParams p, DevProgram prog, int a, int exmin, int nwords,
                                                       int64_t* __restrict__ wide) {
@@ -1072,8 +1088,7 @@ __global__ void gb_export_count_kernel(GbParams p, int world, uint64_t* counts) 
     }
 }
 
-__global__ void gb_export_kernel(GbParams p, int world, uint64_t* cursor, uint64_t* out) {
-    const int rw = p.nfields + 1;
+__global__ void gb_export_kernel(GbParams p, int world, uint64_t* cursor, uint64_t* out, WideRec wr, int rw) {
     for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < p.gcap + 2;
          s += (int64_t)gridDim.x * blockDim.x) {
         uint64_t kind, key;
@@ -1083,6 +1098,10 @@ __global__ void gb_export_kernel(GbParams p, int world, uint64_t* cursor, uint64
         r[0] = kind;
         r[1] = key;
         for (int f = 1; f < p.nfields; ++f) r[1 + f] = *gfield(p, f, s);
+        for (int i = 0; i < wr.n; ++i) {
+            const int64_t* d = wr.digits[i] + s * wr.nwords[i];
+            for (int k = 0; k < wr.nwords[i]; ++k) r[wr.off[i] + k] = (uint64_t)d[k];
+        }
     }
 }
 
@@ -1126,8 +1145,11 @@ __device__ __forceinline__ bool shl192(uint64_t& w0, uint64_t& w1, uint64_t& w2,
 // fixed-point windows; an f64 sum state of acc a is shifted left by
 // src_shift[j * kMaxAcc + a] bits onto the table's window (exact).
 __global__ void gb_merge_kernel(GbParams p, const uint64_t* __restrict__ rec, int64_t nrec, int nsrc,
-                                const int64_t* __restrict__ src_start, const int32_t* __restrict__ src_shift) {
-    const int rw = p.nfields + 1;
+                                const int64_t* __restrict__ src_start, const int32_t* __restrict__ src_shift,
+                                WideRec wr, int rw) {
+    // the 192-bit states of wide accs are not merged (their digits are)
+    uint64_t skip = 0;
+    for (int i = 0; i < wr.n; ++i) skip |= 1ull << p.acc[wr.acc[i]].f_sum;
     uint32_t special = 0;
     bool ovf = false;
     // up to nsrc states fold into one cell: each must leave ceil(log2 nsrc)
@@ -1162,6 +1184,7 @@ __global__ void gb_merge_kernel(GbParams p, const uint64_t* __restrict__ rec, in
             case FOP_MAX: if (v) atomicMax(q, (unsigned long long)v); break;
             case FOP_OR: if (v) atomicOr(q, (unsigned long long)v); break;
             case FOP_ADD192: {
+                if ((skip >> f) & 1ull) break;
                 uint64_t w0 = v, w1 = r[2 + f], w2 = r[3 + f];
                 if (nsrc > 0) {
                     int d = 0;
@@ -1176,6 +1199,13 @@ __global__ void gb_merge_kernel(GbParams p, const uint64_t* __restrict__ rec, in
                 break;
             }
             default: break;
+            }
+        }
+        for (int w = 0; w < wr.n; ++w) {
+            int64_t* d = wr.digits[w] + gs * wr.nwords[w];
+            for (int k = 0; k < wr.nwords[w]; ++k) {
+                const uint64_t v = r[wr.off[w] + k];
+                if (v) atomicAdd((unsigned long long*)&d[k], (unsigned long long)v);
             }
         }
     }
@@ -1612,6 +1642,8 @@ struct GbRun {
     int64_t* wide_digits[kMaxAcc] = {nullptr};
     double* wide_sum[kMaxAcc] = {nullptr};
     int64_t est_groups = -1;                 // plan's group estimate (sampled / HLL)
+    bool wide_round = true;                  // gb_wide rounds (false: multi-GPU partial digits)
+    std::string plan_ckey;                   // plan-cache key when the statistics came from the cache
     // fused key packing (p.kp.n > 0): the plan found the fused kernel does
     // not apply (kp_fallback), or a selected row left the packing plan
     // (kp_bad); the caller then writes a code column / repacks
@@ -1882,6 +1914,15 @@ bool plan_cache_get(const std::string& key, PlanStats* out) {
     return false;
 }
 
+void plan_cache_erase(const std::string& key) {
+    std::lock_guard<std::mutex> g(g_plan_mu);
+    for (size_t i = 0; i < g_plan_cache.size(); ++i)
+        if (g_plan_cache[i].first == key) {
+            g_plan_cache.erase(g_plan_cache.begin() + (ptrdiff_t)i);
+            return;
+        }
+}
+
 void plan_cache_put(const std::string& key, const PlanStats& v) {
     std::lock_guard<std::mutex> g(g_plan_mu);
     for (auto& e : g_plan_cache)
@@ -1935,6 +1976,26 @@ void gb_plan_cache_clear() {
     g_pack_cache.clear();
 }
 
+// Distinct keys of the key column by HyperLogLog (gb_hll_kernel, ~1.6 %).
+static int gb_hll_count(GbRun& R, int64_t* out) {
+    uint32_t* regs = nullptr;
+    std::vector<uint32_t> h(1 << kHllBits);
+    int rc = dev_alloc((void**)&regs, h.size() * 4, R.s);
+    if (rc) return rc;
+    hipError_t e = hipMemsetAsync(regs, 0, h.size() * 4, R.s);
+    if (e == hipSuccess) {
+        KtScope kt("gb_hll_kernel", R.s);
+        gb_hll_kernel<<<num_cus() * 4, 256, 0, R.s>>>(R.pl.p.key, R.pl.p.n, regs);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(h.data(), regs, h.size() * 4, hipMemcpyDeviceToHost, R.s);
+    if (e == hipSuccess) e = hipStreamSynchronize(R.s);
+    dev_free(regs, R.s);
+    if (e != hipSuccess) return hip_fail(e, "gb_hll_kernel");
+    *out = (int64_t)hll_estimate(h.data());
+    return PLGPU_OK;
+}
+
 // Planning launch -> distinct-key estimate, fixed-point bottoms, table
 // sizes, kernel choice.  `fixed` (nullable) overrides the sampled bottoms.
 static int gb_plan(GbRun& R, const int32_t* fixed) {
@@ -1953,6 +2014,7 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
     const bool hit = use_cache && plan_cache_get(ckey, &cached);
     if (hit) {
         std::memcpy(R.st, cached.st, sizeof R.st);
+        R.plan_ckey = ckey;
     } else {
         {
             KtScope kt("gb_plan_kernel", R.s);
@@ -2008,21 +2070,8 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
         if (hit && cached.hll >= 0) {
             hll = cached.hll;
         } else {
-            uint32_t* regs = nullptr;
-            std::vector<uint32_t> h(1 << kHllBits);
-            int rc = dev_alloc((void**)&regs, h.size() * 4, R.s);
+            int rc = gb_hll_count(R, &hll);
             if (rc) return rc;
-            hipError_t e = hipMemsetAsync(regs, 0, h.size() * 4, R.s);
-            if (e == hipSuccess) {
-                KtScope kt("gb_hll_kernel", R.s);
-                gb_hll_kernel<<<num_cus() * 4, 256, 0, R.s>>>(p.key, n, regs);
-                e = hipGetLastError();
-            }
-            if (e == hipSuccess) e = hipMemcpyAsync(h.data(), regs, h.size() * 4, hipMemcpyDeviceToHost, R.s);
-            if (e == hipSuccess) e = hipStreamSynchronize(R.s);
-            dev_free(regs, R.s);
-            if (e != hipSuccess) return hip_fail(e, "gb_hll_kernel");
-            hll = (int64_t)hll_estimate(h.data());
             if (use_cache) {
                 cached.hll = hll;
                 plan_cache_put(ckey, cached);
@@ -2482,27 +2531,53 @@ static int gb_refit(GbRun& R, uint32_t flagged, int32_t* hint, bool* changed, ui
     return PLGPU_OK;
 }
 
-// Exact wide sums for the accs in R.wide (see gb_wide_kernel).
-static int gb_wide(GbRun& R) {
+// Exact wide sums for the accs in R.wide (see gb_wide_kernel): the digit
+// pass over the rows, then (round) the rounding into R.wide_sum, which
+// normalises the digits in place.  Multi-GPU partial states export the
+// digits unrounded (round = false).
+static int gb_wide(GbRun& R, bool round = true) {
     GbParams& p = R.pl.p;
     for (int a = 0; a < p.nacc; ++a) {
         if (!((R.wide >> a) & 1u)) continue;
+        dev_free(R.wide_digits[a], R.s);
+        dev_free(R.wide_sum[a], R.s);
+        R.wide_digits[a] = nullptr;
+        R.wide_sum[a] = nullptr;
         const int exmin = R.wide_exmin[a];
-        const int nwords = (R.wide_exmax[a] - exmin) / kWideDigit + 6;
+        const int nwords = wide_nwords(exmin, R.wide_exmax[a]);
         const size_t slots = (size_t)(p.gcap + 2);
         int rc = dev_alloc((void**)&R.wide_digits[a], slots * nwords * 8, R.s);
-        if (!rc) rc = dev_alloc((void**)&R.wide_sum[a], slots * 8, R.s);
+        if (!rc && round) rc = dev_alloc((void**)&R.wide_sum[a], slots * 8, R.s);
         if (rc) return rc;
         PLGPU_HIP(hipMemsetAsync(R.wide_digits[a], 0, slots * nwords * 8, R.s));
         const int g = std::max(1, num_cus() * 8);
         if (R.pred == 0) gb_wide_kernel<0><<<g, 256, 0, R.s>>>(p, R.dp, a, exmin, nwords, R.wide_digits[a]);
         else if (R.pred == 1) gb_wide_kernel<1><<<g, 256, 0, R.s>>>(p, R.dp, a, exmin, nwords, R.wide_digits[a]);
         else gb_wide_kernel<2><<<g, 256, 0, R.s>>>(p, R.dp, a, exmin, nwords, R.wide_digits[a]);
-        const int fg = (int)std::min<int64_t>((p.gcap + 2 + 255) / 256, 256 * 16);
-        gb_wide_round_kernel<<<fg, 256, 0, R.s>>>(p, exmin, nwords, R.wide_digits[a], R.wide_sum[a]);
+        if (round) {
+            const int fg = (int)std::min<int64_t>((p.gcap + 2 + 255) / 256, 256 * 16);
+            gb_wide_round_kernel<<<fg, 256, 0, R.s>>>(p, exmin, nwords, R.wide_digits[a], R.wide_sum[a]);
+        }
         PLGPU_HIP(hipGetLastError());
     }
     return PLGPU_OK;
+}
+
+// The record layout's wide part for the accs in R.wide over R.wide_exmin /
+// exmax; returns the record's words.
+static int wide_layout(const GbRun& R, WideRec& wr) {
+    std::memset(&wr, 0, sizeof wr);
+    int w = R.pl.p.nfields + 1;
+    for (int a = 0; a < R.pl.p.nacc; ++a) {
+        if (!((R.wide >> a) & 1u)) continue;
+        wr.acc[wr.n] = a;
+        wr.nwords[wr.n] = wide_nwords(R.wide_exmin[a], R.wide_exmax[a]);
+        wr.off[wr.n] = w;
+        wr.digits[wr.n] = R.wide_digits[a];
+        w += wr.nwords[wr.n];
+        ++wr.n;
+    }
+    return w;
 }
 
 // Main launches with table-size reruns; window refits too when auto_refit.
@@ -2565,6 +2640,14 @@ static int gb_main(GbRun& R, bool auto_refit, bool* refit, int32_t* hint) {
             // (a full partition region: the rerun takes the plain hashed table)
             R.rbits = 0;
             R.gbits = std::max(R.gbits + 3, log2_ceil((int64_t)R.st[ST_NEWKEYS] * 4));
+            if (R.attempts == 0 && p.key.values != nullptr && p.kp.n == 0) {
+                // the plan's estimate was far off (stale plan statistics, a
+                // skewed sample): count the key column's distinct values once
+                // so the next table holds them all
+                int64_t hll = 0;
+                if ((rc = gb_hll_count(R, &hll))) break;
+                R.gbits = std::max(R.gbits, log2_ceil(std::min<int64_t>(n, hll + hll / 4 + 1024) * 2));
+            }
             again = true;
         }
         uint32_t flagged = 0;
@@ -2614,7 +2697,14 @@ static int gb_main(GbRun& R, bool auto_refit, bool* refit, int32_t* hint) {
     if (rc == PLGPU_OK) (void)hipEventElapsedTime(&R.ms, ev0, ev1);
     ev_release(ev0);
     ev_release(ev1);
-    if (rc == PLGPU_OK && R.wide && !R.kp_bad) rc = gb_wide(R);
+    // cached statistics the run contradicted (a table-size or window rerun,
+    // or several times the estimated groups: the columns' addresses now hold
+    // other data) are dropped, so the next query samples afresh
+    if (!R.plan_ckey.empty() &&
+        (rc != PLGPU_OK || R.attempts > 0 || R.kp_bad ||
+         (int64_t)R.st[ST_NEWKEYS] > 2 * std::max<int64_t>(R.est_groups, 4096)))
+        plan_cache_erase(R.plan_ckey);
+    if (rc == PLGPU_OK && R.wide && !R.kp_bad) rc = gb_wide(R, R.wide_round);
     return rc;
 }
 
@@ -3017,17 +3107,16 @@ PLGPU_API int plgpu_gb_partial_begin(const plgpu_column* key, const plgpu_column
     plgpu_gb_partial* h = new plgpu_gb_partial();
     GbRun& R = h->run;
     R.world = world;
+    R.wide_round = false;  // a wide sum's digits travel in the records
     bool refit = false;
     int rc = gb_prepare(R, key, cols, ncols, program, n_instr, aggs, naggs, false, true, stream);
     if (!rc) rc = gb_plan(R, bottoms);
     // own windows (bottoms NULL): refits happen here, since each source's
     // windows travel with its records (plgpu_gb_merge_sources); fixed
-    // windows: a needed refit is reported
+    // windows: a needed refit is reported.  A column wider than one window
+    // keeps exact per-group digits (gb_wide); the ranks agree on one digit
+    // range (plgpu_gb_partial_wide / _set_wide) before the export.
     if (!rc) rc = gb_main(R, bottoms == nullptr, &refit, out_bottoms_hint);
-    if (!rc && R.wide)
-        rc = fail(PLGPU_ERR_CAPACITY,
-                  "f64 sum: the values of one column span more binades than the partitioned "
-                  "group-by's fixed-point window; use the single-GPU group-by for this column");
     if (rc) {
         delete h;
         return rc;
@@ -3043,12 +3132,82 @@ PLGPU_API int plgpu_gb_partial_begin(const plgpu_column* key, const plgpu_column
     return PLGPU_OK;
 }
 
+PLGPU_API int plgpu_gb_partial_wide(const plgpu_gb_partial* h, int32_t* out_wide, int32_t* out_exmin,
+                                    int32_t* out_exmax) {
+    if (h == nullptr || out_wide == nullptr || out_exmin == nullptr || out_exmax == nullptr)
+        return fail(PLGPU_ERR_INVALID, "NULL argument");
+    const GbRun& R = h->run;
+    const GbParams& p = R.pl.p;
+    for (int a = 0; a < kMaxAcc; ++a) {
+        out_wide[a] = 0;
+        out_exmin[a] = 0x7FF;  // neutral for the ranks' min / max
+        out_exmax[a] = 0;
+        if (a >= p.nacc || !(p.acc[a].flags & (A_FSUM | A_FSUMCAST))) continue;
+        if ((R.wide >> a) & 1u) {
+            out_wide[a] = 1;
+            out_exmin[a] = R.wide_exmin[a];
+            out_exmax[a] = R.wide_exmax[a];
+        } else {
+            // every value of an exact fixed-point state has its bits in
+            // [bottom, bottom + kSumWindowBits): biased exponents (mantissa
+            // LSB at ex - 1075, subnormals as ex 1) in this range
+            out_exmin[a] = std::max(1, R.hb[a] + 1075);
+            out_exmax[a] = std::min(0x7FE, std::max(out_exmin[a], R.hb[a] + 1075 + kSumWindowBits - 53));
+        }
+    }
+    return PLGPU_OK;
+}
+
+PLGPU_API int plgpu_gb_partial_set_wide(plgpu_gb_partial* h, const int32_t* wide, const int32_t* exmin,
+                                        const int32_t* exmax) {
+    if (h == nullptr || wide == nullptr || exmin == nullptr || exmax == nullptr)
+        return fail(PLGPU_ERR_INVALID, "NULL argument");
+    GbRun& R = h->run;
+    const GbParams& p = R.pl.p;
+    uint32_t mask = 0;
+    for (int a = 0; a < kMaxAcc; ++a) {
+        if (!wide[a]) continue;
+        if (a >= p.nacc || !(p.acc[a].flags & (A_FSUM | A_FSUMCAST)))
+            return fail(PLGPU_ERR_INVALID, "wide: only f64 sums take digit states");
+        if (exmin[a] < 1 || exmax[a] > 0x7FE || exmin[a] > exmax[a])
+            return fail(PLGPU_ERR_INVALID, "wide: bad exponent range");
+        if (((R.wide >> a) & 1u) && (exmin[a] > R.wide_exmin[a] || exmax[a] < R.wide_exmax[a]))
+            return fail(PLGPU_ERR_INVALID, "wide: the agreed range must cover this rank's");
+        mask |= 1u << a;
+    }
+    if (mask == 0) return R.wide ? fail(PLGPU_ERR_INVALID, "wide: this rank holds a wide sum") : PLGPU_OK;
+    if ((R.wide & ~mask) != 0) return fail(PLGPU_ERR_INVALID, "wide: this rank holds a wide sum");
+    R.wide = mask;
+    for (int a = 0; a < kMaxAcc; ++a)
+        if ((mask >> a) & 1u) {
+            R.wide_exmin[a] = exmin[a];
+            R.wide_exmax[a] = exmax[a];
+        }
+    int rc = gb_wide(R, false);
+    if (rc == PLGPU_OK) {
+        hipError_t e = hipStreamSynchronize(R.s);
+        if (e != hipSuccess) rc = hip_fail(e, "gb_wide_kernel");
+    }
+    return rc;
+}
+
+PLGPU_API int plgpu_gb_partial_record_words(const plgpu_gb_partial* h, int32_t* out_words) {
+    if (h == nullptr || out_words == nullptr) return fail(PLGPU_ERR_INVALID, "NULL argument");
+    WideRec wr;
+    *out_words = wide_layout(h->run, wr);
+    return PLGPU_OK;
+}
+
 PLGPU_API int plgpu_gb_partial_export(plgpu_gb_partial* h, void* dst_records, int64_t* out_counts, void* stream) {
     if (h == nullptr || out_counts == nullptr) return fail(PLGPU_ERR_INVALID, "NULL argument");
     GbRun& R = h->run;
     hipStream_t s = stream ? as_stream(stream) : R.s;
     const GbParams& p = R.pl.p;
     const int W = R.world;
+    WideRec wr;
+    const int rw = wide_layout(R, wr);
+    for (int i = 0; i < wr.n; ++i)
+        if (wr.digits[i] == nullptr) return fail(PLGPU_ERR_INVALID, "wide: digits missing");
     uint64_t* counts = nullptr;  // [W] counts, [W] cursors
     int rc = dev_alloc((void**)&counts, (size_t)W * 16, s);
     if (rc) return rc;
@@ -3070,7 +3229,7 @@ PLGPU_API int plgpu_gb_partial_export(plgpu_gb_partial* h, void* dst_records, in
             return fail(PLGPU_ERR_INVALID, "dst_records is NULL");
         }
         PLGPU_HIP(hipMemcpyAsync(counts + W, cur.data(), (size_t)W * 8, hipMemcpyHostToDevice, s));
-        gb_export_kernel<<<fg, 256, 0, s>>>(p, W, counts + W, (uint64_t*)dst_records);
+        gb_export_kernel<<<fg, 256, 0, s>>>(p, W, counts + W, (uint64_t*)dst_records, wr, rw);
         PLGPU_HIP(hipGetLastError());
     }
     PLGPU_HIP(hipStreamSynchronize(s));
@@ -3332,7 +3491,9 @@ PLGPU_API int plgpu_float_key_encode(const plgpu_column* keys, plgpu_column* out
 static int gb_merge_impl(const void* records, int64_t n_records, int32_t nsrc, const int64_t* src_records,
                          const int32_t* src_bottoms, const plgpu_column* cols, int32_t ncols, const plgpu_agg* aggs,
                          int32_t naggs, const int32_t* bottoms, int32_t key_dtype, plgpu_column* out_key,
-                         plgpu_column* out_aggs, plgpu_groupby_info* info, void* stream) {
+                         plgpu_column* out_aggs, plgpu_groupby_info* info, void* stream,
+                         const int32_t* wide = nullptr, const int32_t* wide_exmin = nullptr,
+                         const int32_t* wide_exmax = nullptr) {
     if (out_key == nullptr || (cols == nullptr && ncols > 0)) return fail(PLGPU_ERR_INVALID, "NULL argument");
     if (ncols < 0 || ncols > PLGPU_MAX_COLS) return fail(PLGPU_ERR_INVALID, "too many columns (max 8)");
     if (n_records < 0 || (n_records > 0 && records == nullptr)) return fail(PLGPU_ERR_INVALID, "bad records");
@@ -3383,6 +3544,18 @@ static int gb_merge_impl(const void* records, int64_t n_records, int32_t nsrc, c
     }
     R.gbits = log2_ceil(std::max<int64_t>(1024, n_records * 2));
     GbParams& p = R.pl.p;
+    if (wide) {
+        for (int a = 0; a < kMaxAcc; ++a) {
+            if (!wide[a]) continue;
+            if (a >= p.nacc || !(p.acc[a].flags & (A_FSUM | A_FSUMCAST)))
+                return fail(PLGPU_ERR_INVALID, "wide: only f64 sums take digit states");
+            if (wide_exmin[a] < 1 || wide_exmax[a] > 0x7FE || wide_exmin[a] > wide_exmax[a])
+                return fail(PLGPU_ERR_INVALID, "wide: bad exponent range");
+            R.wide |= 1u << a;
+            R.wide_exmin[a] = wide_exmin[a];
+            R.wide_exmax[a] = wide_exmax[a];
+        }
+    }
     // source table on the device: nsrc + 1 starts, then nsrc x kMaxAcc shifts
     int64_t* dsrc = nullptr;
     if (nsrc > 0) {
@@ -3400,11 +3573,24 @@ static int gb_merge_impl(const void* records, int64_t n_records, int32_t nsrc, c
     }
     for (R.attempts = 0;; ++R.attempts) {
         if ((rc = gb_alloc_table(R))) break;
+        // wide sums: zeroed digit arrays for this table
+        for (int a = 0; a < kMaxAcc && !rc; ++a) {
+            if (!((R.wide >> a) & 1u)) continue;
+            dev_free(R.wide_digits[a], R.s);
+            R.wide_digits[a] = nullptr;
+            const size_t words = (size_t)(p.gcap + 2) * wide_nwords(R.wide_exmin[a], R.wide_exmax[a]);
+            rc = dev_alloc((void**)&R.wide_digits[a], words * 8, R.s);
+            if (!rc && hipMemsetAsync(R.wide_digits[a], 0, words * 8, R.s) != hipSuccess)
+                rc = fail(PLGPU_ERR_HIP, "wide digits");
+        }
+        if (rc) break;
+        WideRec wr;
+        const int rw = wide_layout(R, wr);
         hipError_t e = hipMemcpyAsync(R.bottoms, R.hb, sizeof R.hb, hipMemcpyHostToDevice, R.s);
         if (e == hipSuccess && n_records > 0) {
             const int g = (int)std::min<int64_t>((n_records + 255) / 256, 256 * 16);
             gb_merge_kernel<<<g, 256, 0, R.s>>>(p, (const uint64_t*)records, n_records, nsrc, dsrc,
-                                                dsrc ? (const int32_t*)(dsrc + nsrc + 1) : nullptr);
+                                                dsrc ? (const int32_t*)(dsrc + nsrc + 1) : nullptr, wr, rw);
             e = hipGetLastError();
         }
         if (e == hipSuccess) e = hipMemcpyAsync(R.st, R.status, sizeof R.st, hipMemcpyDeviceToHost, R.s);
@@ -3426,6 +3612,16 @@ static int gb_merge_impl(const void* records, int64_t n_records, int32_t nsrc, c
         R.gbits += 3;
     }
     dev_free(dsrc, R.s);
+    for (int a = 0; a < kMaxAcc && !rc; ++a) {
+        // the merged digits, rounded once per group
+        if (!((R.wide >> a) & 1u)) continue;
+        rc = dev_alloc((void**)&R.wide_sum[a], (size_t)(p.gcap + 2) * 8, R.s);
+        if (rc) break;
+        const int fg = (int)std::min<int64_t>((p.gcap + 2 + 255) / 256, 256 * 16);
+        gb_wide_round_kernel<<<fg, 256, 0, R.s>>>(p, R.wide_exmin[a], wide_nwords(R.wide_exmin[a], R.wide_exmax[a]),
+                                                  R.wide_digits[a], R.wide_sum[a]);
+        if (hipGetLastError() != hipSuccess) rc = fail(PLGPU_ERR_HIP, "gb_wide_round_kernel");
+    }
     if (rc) return rc;
     if (info) gb_fill_info(R, info);
     return gb_finalize(R, naggs, out_key, out_aggs);
@@ -3448,6 +3644,22 @@ PLGPU_API int plgpu_gb_merge_sources(const void* records, int32_t n_sources, con
     for (int j = 0; j < n_sources; ++j) n += src_records[j];
     return gb_merge_impl(records, n, n_sources, src_records, src_bottoms, cols, ncols, aggs, naggs, nullptr,
                          key_dtype, out_key, out_aggs, info, stream);
+}
+
+PLGPU_API int plgpu_gb_merge_sources_wide(const void* records, int32_t n_sources, const int64_t* src_records,
+                                          const int32_t* src_bottoms, const int32_t* wide, const int32_t* wide_exmin,
+                                          const int32_t* wide_exmax, const plgpu_column* cols, int32_t ncols,
+                                          const plgpu_agg* aggs, int32_t naggs, int32_t key_dtype,
+                                          plgpu_column* out_key, plgpu_column* out_aggs, plgpu_groupby_info* info,
+                                          void* stream) {
+    if (n_sources < 1 || src_records == nullptr || src_bottoms == nullptr)
+        return fail(PLGPU_ERR_INVALID, "merge: need >= 1 source with its record count and windows");
+    if (wide == nullptr || wide_exmin == nullptr || wide_exmax == nullptr)
+        return fail(PLGPU_ERR_INVALID, "NULL argument");
+    int64_t n = 0;
+    for (int j = 0; j < n_sources; ++j) n += src_records[j];
+    return gb_merge_impl(records, n, n_sources, src_records, src_bottoms, cols, ncols, aggs, naggs, nullptr,
+                         key_dtype, out_key, out_aggs, info, stream, wide, wide_exmin, wide_exmax);
 }
 
 // ------------------------------------------------------ multi-key group-by

@@ -905,10 +905,11 @@ __device__ __forceinline__ void rw_block(const RlParams& p, uint64_t (&x)[kRwChu
 #undef PLGPU_RW
 }
 
-// One block of kRwOut outputs per wave.  MINW > 0: at least MINW waves per
-// SIMD (the compiler caps the registers accordingly; A/B, option rl_occ).
-template <int DT, bool NULLABLE, bool VAR = false, int MINW = 0>
-__global__ __launch_bounds__(256, MINW > 0 ? MINW : 1) void rl_wave_kernel(RlParams p) {
+// One block of kRwOut outputs per wave.  (A register cap for 6 waves per
+// SIMD, __launch_bounds__(256, 6), spilled 6 VGPRs and still ended at 5
+// waves: not kept.)
+template <int DT, bool NULLABLE, bool VAR = false>
+__global__ __launch_bounds__(256) void rl_wave_kernel(RlParams p) {
     __shared__ uint64_t ring_lo[kRwWaves][kRwRing];
     __shared__ uint64_t ring_hi[kRwWaves][kRwRing];
     __shared__ uint64_t ring_cn[kRwWaves][kRwRing];
@@ -1324,7 +1325,6 @@ PLGPU_API int plgpu_rolling(const plgpu_column* values, int32_t kind, int64_t wi
             }
         } else if (values->dtype == PLGPU_F64) {
             if (nl) rl_wave_kernel<PLGPU_F64, true><<<g, 64 * kRwWaves, 0, s>>>(p);
-            else if (options().rl_occ == 6) rl_wave_kernel<PLGPU_F64, false, false, 6><<<g, 64 * kRwWaves, 0, s>>>(p);
             else rl_wave_kernel<PLGPU_F64, false><<<g, 64 * kRwWaves, 0, s>>>(p);
         } else if (values->dtype == PLGPU_I64) {
             if (nl) rl_wave_kernel<PLGPU_I64, true><<<g, 64 * kRwWaves, 0, s>>>(p);

@@ -9,7 +9,10 @@ partition's share with `combine_subset` (group_by.rs:378) in
 1. every rank filters + pre-aggregates its own shard in HBM
    (`plgpu_gb_partial_begin`, the same fused kernel as the single-GPU path)
    with its own f64 fixed-point windows (exact 192-bit states; a window
-   that does not fit the shard is refitted locally);
+   that does not fit the shard is refitted locally); one small all-reduce
+   agrees the stage's status and, for an f64 sum whose values span more
+   binades than one window on some rank, one digit range per column over
+   which every rank keeps that column's exact per-group digit state;
 2. the partial groups are written as records grouped by destination rank
    (`plgpu_gb_partial_export`); one all-to-all carries each destination's
    record count together with the sender's windows and status, a second
@@ -20,8 +23,9 @@ partition's share with `combine_subset` (group_by.rs:378) in
    (`plgpu_gb_merge_sources`), returning a DataFrame of the groups it owns.
 
 The only data-path collective is the record exchange, whose volume is
-groups x record size (independent of the row count), so the per-rank work
-stays the local HBM pass: weak scaling.
+groups x record size (independent of the row count; a wide column adds its
+digit words to every record), so the per-rank work stays the local HBM
+pass: weak scaling.
 """
 
 from __future__ import annotations
@@ -220,6 +224,7 @@ class GpuPartial:
         self.nrec = 0
         self.bottoms = (C.c_int32 * N.GB_MAX_ACC)()
         self.info = N.GroupByInfo()
+        self.wide = None  # agreed (wide, exmin, exmax) when some column's states are digits
         w = C.c_int32(0)
         N.check(N.lib().plgpu_gb_record_words(g.cols, g.ncols, g.aggs, g.naggs, C.byref(w)))
         self.record_words = int(w.value)
@@ -245,16 +250,30 @@ class GpuPartial:
         nrec = C.c_int64(0)
         refit = C.c_int32(0)
         hint = (C.c_int32 * N.GB_MAX_ACC)()
-        rc = N.lib().plgpu_gb_partial_begin(C.byref(g.keycol), g.cols, g.ncols, g.prog, g.n_instr, g.aggs,
-                                            g.naggs, None, self.world, C.byref(self.handle), C.byref(nrec),
-                                            self.bottoms, C.byref(refit), hint, C.byref(self.info), None)
-        if rc == N.ERR_CAPACITY and b"binades" in (N.lib().plgpu_last_error() or b""):
-            # an f64 sum wider than one fixed-point window: its exact state
-            # does not fit a record; the rows take the shuffle protocol
-            raise _RowShuffle("wide f64 sum")
-        N.check(rc)
+        N.check(N.lib().plgpu_gb_partial_begin(C.byref(g.keycol), g.cols, g.ncols, g.prog, g.n_instr, g.aggs,
+                                               g.naggs, None, self.world, C.byref(self.handle), C.byref(nrec),
+                                               self.bottoms, C.byref(refit), hint, C.byref(self.info), None))
         self.nrec = int(nrec.value)
         return list(self.bottoms)
+
+    def wide_info(self):
+        """-> (wide[a], exmin[a], exmax[a]): which f64 sums of this shard
+        need digit states, and the biased exponents each f64 sum's values
+        take (plgpu_gb_partial_wide)."""
+        A = N.GB_MAX_ACC
+        w, lo, hi = (C.c_int32 * A)(), (C.c_int32 * A)(), (C.c_int32 * A)()
+        N.check(N.lib().plgpu_gb_partial_wide(self.handle, w, lo, hi))
+        return list(w), list(lo), list(hi)
+
+    def set_wide(self, wide, exmin, exmax) -> None:
+        """Digit states over the ranks' agreed ranges for the columns in
+        `wide`; the record grows by their digit words."""
+        A = N.GB_MAX_ACC
+        self.wide = ((C.c_int32 * A)(*wide), (C.c_int32 * A)(*exmin), (C.c_int32 * A)(*exmax))
+        N.check(N.lib().plgpu_gb_partial_set_wide(self.handle, *self.wide))
+        w = C.c_int32(0)
+        N.check(N.lib().plgpu_gb_partial_record_words(self.handle, C.byref(w)))
+        self.record_words = int(w.value)
 
     def export(self):
         """-> (flat int64 CUDA tensor of records grouped by rank, counts)."""
@@ -279,9 +298,14 @@ class GpuPartial:
         out_key = N.Column()
         out_aggs = (N.Column * max(1, g.naggs))()
         mi = N.GroupByInfo()
-        N.check(N.lib().plgpu_gb_merge_sources(recv.data_ptr() if sum(src_counts) else None, ns, cnt, bot, g.cols,
-                                               g.ncols, g.aggs, g.naggs, g.keycol.dtype, C.byref(out_key),
-                                               out_aggs, C.byref(mi), None))
+        rec = recv.data_ptr() if sum(src_counts) else None
+        if self.wide is not None:
+            N.check(N.lib().plgpu_gb_merge_sources_wide(rec, ns, cnt, bot, *self.wide, g.cols, g.ncols, g.aggs,
+                                                        g.naggs, g.keycol.dtype, C.byref(out_key), out_aggs,
+                                                        C.byref(mi), None))
+        else:
+            N.check(N.lib().plgpu_gb_merge_sources(rec, ns, cnt, bot, g.cols, g.ncols, g.aggs, g.naggs,
+                                                   g.keycol.dtype, C.byref(out_key), out_aggs, C.byref(mi), None))
         return _gb_frame(g, out_key, out_aggs), mi
 
 
@@ -292,53 +316,90 @@ def _sync(device) -> None:
         torch.cuda.synchronize(device)
 
 
+def agree_wide(vals, world: int, rank: int, failed: bool, group, device):
+    """One max all-reduce after the partial stage: per rank a failure flag,
+    and per acc (wide, -exmin, exmax) from `vals` = part.wide_info() (None
+    on a failed rank or a partial without f64 sums).  Returns (failed ranks,
+    wide, exmin, exmax) over all ranks: a column is wide when it is on any
+    rank, and its digit range is the union of every rank's exponent range."""
+    A = N.GB_MAX_ACC
+    flat = [0] * world + [0] * A + [-0x7FF] * A + [0] * A
+    if failed:
+        flat[rank] = 1
+    elif vals is not None:
+        w, lo, hi = vals
+        flat[world:world + A] = [int(x) for x in w]
+        flat[world + A:world + 2 * A] = [-int(x) for x in lo]
+        flat[world + 2 * A:] = [int(x) for x in hi]
+    red = _allreduce_max(flat, group, device)
+    return ([q for q in range(world) if red[q]], red[world:world + A],
+            [-x for x in red[world + A:world + 2 * A]], red[world + 2 * A:])
+
+
 def run_partitioned(part, world: int, group, device, timings: dict | None = None):
     """The protocol of group_by_agg over any partial implementation (the
     GPU one above, or a host model in tests/test_distributed.py).
 
-    The partial stage runs with no collective.  A rank whose partial stage
-    fails still takes part in the count exchange (status 1, no records), so
-    every rank learns of the failure and raises instead of waiting in a
-    collective.  With `timings`, the wall time of each phase (device-
-    synchronised) is stored as partial_ms (local pre-aggregation), exchange_ms
-    (export + the two all-to-alls) and merge_ms."""
+    The partial stage runs with no collective.  Its outcome is agreed by one
+    small all-reduce (agree_wide): a rank whose stage failed makes every
+    rank raise instead of waiting in a collective, and an f64 sum wider than
+    one fixed-point window on any rank turns that column's states into exact
+    digit words over the union of the ranks' exponent ranges on every rank
+    (part.set_wide), so the records still carry it (the single-GPU wide
+    sum, bit-identical).  A failure in the export still reaches every rank
+    through the count exchange (status 1, no records).  With `timings`, the
+    wall time of each phase (device-synchronised) is stored as partial_ms
+    (local pre-aggregation and the agreement), exchange_ms (export + the two
+    all-to-alls), merge_ms, and wide_accs / record_words."""
+    import torch.distributed as dist
+
     t0 = time.perf_counter()
     err = None
     bottoms = [0] * N.GB_MAX_ACC
-    send = counts = None
+    vals = None
     try:
         bottoms = part.begin()
+        vals = part.wide_info() if hasattr(part, "wide_info") else None
+    except Exception as e:  # noqa: BLE001 -- agreed below, then re-raised
+        err = e
+        bottoms = [0] * N.GB_MAX_ACC
+    failed, wide, exmin, exmax = agree_wide(vals, world, dist.get_rank(group), err is not None, group, device)
+    if err is not None:
+        raise err
+    if failed:
+        raise N.ComputeError(f"multi-GPU group-by: the partial stage failed on rank(s) {failed}")
+    send = counts = None
+    try:
+        if any(wide):
+            part.set_wide(wide, exmin, exmax)
         if timings is not None:
             _sync(device)
         t1 = time.perf_counter()
         send, counts = part.export()
-    except Exception as e:  # noqa: BLE001 -- a wide-range f64 sum (status 2) or any failure
-        # before the exchange: the count exchange still runs, with the status
-        # and no records, so every rank learns of it instead of waiting
+    except Exception as e:  # noqa: BLE001 -- any failure before the exchange:
+        # the count exchange still runs, with the status and no records, so
+        # every rank learns of it instead of waiting
         err = e
-        bottoms = [0] * N.GB_MAX_ACC
     if err is not None or send is None:
         import torch
 
         t1 = time.perf_counter()
         send, counts = torch.empty(0, dtype=torch.int64, device=device), [0] * world
-    status = 0 if err is None else (2 if isinstance(err, _RowShuffle) else 1)
+    status = 0 if err is None else 1
     recv, n, rows = exchange_records(send, counts, part.record_words, group, header=[status] + list(bottoms))
     failed = [q for q, r in enumerate(rows) if r[1] == 1]
-    if err is not None and status == 1:
+    if err is not None:
         raise err
     if failed:
-        raise N.ComputeError(f"multi-GPU group-by: the partial stage failed on rank(s) {failed}")
-    if any(r[1] == 2 for r in rows):
-        # some rank's shard holds a sum no record state fits: every rank
-        # switches to the row shuffle together
-        raise _RowShuffle("wide f64 sum on some rank")
+        raise N.ComputeError(f"multi-GPU group-by: the export failed on rank(s) {failed}")
     t2 = time.perf_counter()
     res = part.merge(recv, [r[0] for r in rows], [r[2:] for r in rows])
     if timings is not None:
         _sync(device)
         t3 = time.perf_counter()
-        timings.update(partial_ms=(t1 - t0) * 1e3, exchange_ms=(t2 - t1) * 1e3, merge_ms=(t3 - t2) * 1e3)
+        timings.update(partial_ms=(t1 - t0) * 1e3, exchange_ms=(t2 - t1) * 1e3, merge_ms=(t3 - t2) * 1e3,
+                       wide_accs=sum(1 for w in wide if w), record_words=part.record_words,
+                       exchange_bytes=int(sum(counts)) * part.record_words * 8)
     return res
 
 
@@ -576,8 +637,7 @@ def group_by_agg(df, key: str, aggs: Sequence[Expr], predicate: Expr | None = No
         only group records cross the links (volume ~ groups);
       row shuffle: keys or values no fixed-size record carries -- String
         keys longer than 7 bytes, key tuples with Float / String columns or
-        more than 63 bits, an f64 sum wider than one fixed-point window on
-        any rank, var / std with such keys or of an expression -- send the selected
+        more than 63 bits, var / std with such keys or of an expression -- send the selected
         rows to the rank owning their key (volume ~ selected rows) and
         aggregate them there with the single-GPU group-by."""
     import torch.distributed as dist

@@ -1592,9 +1592,13 @@ def _group_by_fused_var(df: DataFrame, key: str | tuple, aggs: list[Expr], maint
                                if _agg_base(e).kind == "agg" and _agg_base(e).op in ("std", "var")))
     plain = [e for e in aggs if not (_agg_base(e).kind == "agg" and _agg_base(e).op in ("std", "var"))]
     pcols = {c for e in plain for c in e.meta_root_names()}
-    # len() takes an accumulator of its own, on the key column (_gb_lower's
-    # len_col), which no other plain aggregation names
-    nlen = 1 if builtins.any(_agg_base(e).kind == "len" for e in plain) else 0
+    # len() rides on _gb_lower's len_col: the first aggregation over a plain
+    # numeric column (var / std included) when there is one, which already
+    # holds an accumulator; otherwise a key column, an accumulator of its own
+    has_col = builtins.any(
+        b.kind == "agg" and b.args and b.args[0].kind == "col" and b.args[0].value in df._cols
+        and df._cols[b.args[0].value].dtype not in (Boolean, String) for b in map(_agg_base, aggs))
+    nlen = 1 if not has_col and builtins.any(_agg_base(e).kind == "len" for e in plain) else 0
     if 3 * builtins.len(vcols) + builtins.len(pcols) + nlen <= N.GB_MAX_ACC:
         return _group_by_plain(df, key, aggs, maintain_order, pred, info)
     names = [e.output_name() for e in aggs]

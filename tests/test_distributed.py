@@ -155,6 +155,98 @@ def test_partitioned_group_by_protocol_gloo(world, fail_rank):
     assert merged == full
 
 
+# ------------------------------------------- wide f64 sums: one agreed digit range
+def _wide_report(rank):
+    """(wide, exmin, exmax) a rank reports for its 6 accs: acc 0 is wide on
+    odd ranks only (its range differs per rank), acc 1 a plain f64 sum, the
+    rest not f64 sums (0x7FF / 0)."""
+    w = [rank % 2, 0, 0, 0, 0, 0]
+    lo = [100 + 7 * rank, 1000 - rank, 0x7FF, 0x7FF, 0x7FF, 0x7FF]
+    hi = [1900 - 5 * rank, 1060 + rank, 0, 0, 0, 0]
+    return w, lo, hi
+
+
+class HostWidePartial(HostPartial):
+    """HostPartial with the wide-sum agreement: records grow by the digit
+    words once set_wide runs (here two words: the agreed range's ends)."""
+
+    def __init__(self, *a):
+        super().__init__(*a)
+        self.agreed = None
+
+    def wide_info(self):
+        return _wide_report(self.rank)
+
+    def set_wide(self, wide, exmin, exmax):
+        self.agreed = (list(wide), list(exmin), list(exmax))
+        self.record_words = RW + 2
+
+    def export(self):
+        ks, sums = self.groups
+        dest = ks % self.world
+        order = np.argsort(dest, kind="stable")
+        lo, hi = self.agreed[1][0], self.agreed[2][0]
+        rec = np.stack([np.zeros_like(ks), ks, sums, np.full_like(ks, lo), np.full_like(ks, hi)], axis=1)
+        return torch.from_numpy(rec[order].reshape(-1).copy()), [int((dest == r).sum()) for r in range(self.world)]
+
+    def merge(self, recv, src_counts, src_bottoms):
+        n = sum(src_counts)
+        r = recv.numpy().reshape(n, RW + 2)
+        out = {}
+        for _, k, v, lo, hi in r:
+            assert (lo, hi) == (self.agreed[1][0], self.agreed[2][0])
+            out[int(k)] = out.get(int(k), 0) + int(v)
+        return (out, self.agreed, self.record_words), None
+
+
+def _wide_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        keys, vals = _shard(rank)
+        part = HostWidePartial(rank, world, keys, vals, -1)
+        timings = {}
+        (out, agreed, rw), _ = D.run_partitioned(part, world, None, torch.device("cpu"), timings)
+        q.put((rank, out, agreed, rw, timings["wide_accs"], timings["record_words"]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_wide_sum_agreement_gloo(world):
+    """A column wide on some ranks only: one all-reduce gives every rank the
+    same wide flags and the union of the ranks' exponent ranges, every rank
+    switches to the digit records (record words grow alike), and the
+    partitions still add up to the full aggregation."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_wide_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        rank, out, agreed, rw, nwide, rwords = q.get(timeout=180)
+        res[rank] = (out, agreed, rw, nwide, rwords)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    reps = [_wide_report(r) for r in range(world)]
+    want = ([max(r[0][a] for r in reps) for a in range(6)], [min(r[1][a] for r in reps) for a in range(6)],
+            [max(r[2][a] for r in reps) for a in range(6)])
+    merged, full = {}, {}
+    for r in range(world):
+        out, agreed, rw, nwide, rwords = res[r]
+        assert agreed == want and rw == RW + 2 and nwide == 1 and rwords == RW + 2
+        merged.update(out)
+    for r in range(world):
+        keys, vals = _shard(r)
+        for k, v in zip(keys.tolist(), vals.tolist()):
+            full[k] = full.get(k, 0) + v
+    assert merged == full
+
+
 # ------------------------------------------------- first() / last() across ranks
 def _fl_shard(rank, n=400):
     """Rows of rank `rank` (rank order = row order): key, nullable key, and a

@@ -69,6 +69,81 @@ def _simulate(shards, world, aggs, pred):
     return frames, windows
 
 
+def _simulate_wide(shards, world, aggs, pred):
+    """_simulate with the wide-sum agreement of run_partitioned (agree_wide:
+    wide on any shard, the union of the exponent ranges)."""
+    import torch
+
+    exprs = [getattr(pl.col(c), k)().alias(f"{k}_{c}") for k, c in aggs]
+    parts = [D.GpuPartial(_gb_lower(df, "k", exprs, pred), world) for df in shards]
+    windows = [p.begin() for p in parts]
+    reps = [p.wide_info() for p in parts]
+    A = len(reps[0][0])
+    wide = [max(r[0][a] for r in reps) for a in range(A)]
+    lo = [min(r[1][a] for r in reps) for a in range(A)]
+    hi = [max(r[2][a] for r in reps) for a in range(A)]
+    if any(wide):
+        for p in parts:
+            p.set_wide(wide, lo, hi)
+    rw = parts[0].record_words
+    assert all(p.record_words == rw for p in parts)
+    exported = [p.export() for p in parts]
+    frames = []
+    for dest in range(world):
+        segs, cnts = [], []
+        for send, counts in exported:
+            off = sum(counts[:dest]) * rw
+            segs.append(send[off: off + counts[dest] * rw])
+            cnts.append(counts[dest])
+        recv = torch.cat(segs) if segs else torch.empty(0, dtype=torch.int64, device="cuda")
+        out, _ = parts[dest].merge(recv.contiguous(), cnts, windows)
+        frames.append(out)
+    return frames, wide, rw
+
+
+@pytest.mark.parametrize("layout", ["one_wide", "all_wide", "none_wide"])
+@pytest.mark.parametrize("world", [2, 3])
+def test_wide_sum_partial_states_bit_identical(gpu, world, layout):
+    """An f64 sum whose values span more binades than one window on some
+    shards (1e300 / 1e-300 / subnormal values, signs mixed, cancelling
+    groups, NaN / inf and nulls) crosses the partial-state protocol as digit
+    records over the union of the shards' exponent ranges: the union of the
+    partitions equals the oracle's exact group-by bit for bit (the
+    single-GPU wide sum's result)."""
+    rng = np.random.default_rng(world * 7 + len(layout))
+    n = 40_000
+    shards_np = []
+    for s in range(world):
+        x = rng.standard_normal(n) * 10.0 ** (s * 3)
+        wide_here = layout == "all_wide" or (layout == "one_wide" and s == world - 1)
+        if wide_here:
+            x[rng.random(n) < 0.2] *= 1e300 / 10.0 ** (s * 3)
+            x[rng.random(n) < 0.2] *= 1e-300
+            x[rng.random(n) < 0.01] = 5e-324 * rng.integers(1, 100)
+        x[rng.random(n) < 0.002] = np.nan
+        x[rng.random(n) < 0.001] = -np.inf
+        b = rng.integers(-10**12, 10**12, n).astype(np.int64)
+        xv = rng.random(n) > 0.03
+        shards_np.append((x, xv, b))
+    key = rng.integers(0, 300, world * n).astype(np.int64) * 7919 - 11
+    # a cancelling group: +1e300 and -1e300 and a tiny value
+    key[:6] = 42
+    shards_np[0][0][:6] = [1e300, -1e300, 3e-310, 1e300, -1e300, 2.5]
+    shards_np[0][1][:6] = True
+    aggs = [("sum", "x"), ("mean", "x"), ("sum", "b"), ("count", "x"), ("len", "x")]
+    shards = []
+    for s in range(world):
+        x, xv, b = shards_np[s]
+        sl = slice(s * n, (s + 1) * n)
+        shards.append(pl.DataFrame({"k": pl.Series.from_numpy("k", key[sl]), "x": pl.Series.from_numpy("x", x, xv),
+                                    "b": pl.Series.from_numpy("b", b)}))
+    frames, wide, rw = _simulate_wide(shards, world, aggs, None)
+    assert bool(wide[0]) == (layout != "none_wide")
+    cols = {"x": (np.concatenate([t[0] for t in shards_np]), np.concatenate([t[1] for t in shards_np])),
+            "b": (np.concatenate([t[2] for t in shards_np]), None)}
+    _check(frames, cols, key, None, aggs, None, ["x", "b"])
+
+
 def _check(frames, cols, key, kvalid, aggs, pred_prog, names):
     n = key.shape[0]
     hc = [O.HostCol(cols[c][0], cols[c][1]) for c in names]
@@ -716,7 +791,8 @@ def test_group_by_agg_world1_rccl_row_shuffle(gpu):
     """The row-shuffle protocol through torch.distributed (nccl = RCCL), one
     rank: every input the partial records cannot carry is accepted, reported
     as info["protocol"] == "row_shuffle", and equals the single-GPU group-by;
-    the common keys keep the partial-state protocol."""
+    the common keys keep the partial-state protocol, and so does a wide f64
+    sum (digit records, round 5)."""
     import torch.distributed as dist
 
     with socket.socket() as s:
@@ -734,7 +810,11 @@ def test_group_by_agg_world1_rccl_row_shuffle(gpu):
             out = D.group_by_agg(df, key, aggs, pred, info=info)
             ref = df.lazy().filter(pred).group_by(key).agg(*aggs).collect()
             assert _rows_of(out, ref.columns) == _rows_of(ref, ref.columns), case
-            assert info.get("protocol") == "row_shuffle", (case, info)
+            if case == "wide_sum":
+                # (round 5) a wide f64 sum stays on the partial states as digits
+                assert "protocol" not in info and info["wide_accs"] == 1, (case, info)
+            else:
+                assert info.get("protocol") == "row_shuffle", (case, info)
         info = {}
         df = pl.DataFrame({"k": pl.Series("k", [1, 2, 1]), "v": pl.Series("v", [1.0, 2.0, 3.0])})
         D.group_by_agg(df, "k", [pl.col("v").sum()], info=info)

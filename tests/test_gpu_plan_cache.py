@@ -5,7 +5,11 @@ choice, so a stale entry must never change a result: here the columns'
 device buffers are rewritten in place between two queries (same addresses,
 same plan key) with values six hundred binades away and forty times the
 groups, and the second result must equal the one computed with the cache
-off, bit for bit, and the exact sums."""
+off, bit for bit, and the exact sums.  Then the keys grow to ~1e6 groups on
+the same buffers: the stale small distinct count sends that run
+to the LDS table, whose overflow reruns it exactly, and the contradicted
+entry is dropped, so the query after it samples afresh and takes the
+partitioned path."""
 
 import math
 
@@ -59,3 +63,44 @@ def test_stale_plan_statistics_never_change_results(gpu, plgpu_option):
     for i in range(0, len(ks), max(1, len(ks) // 9)):
         m = (kh == ks[i]) & (vh > 0.5)
         assert np.float64(ss[i].view(np.float64)) == math.fsum(vh[m])
+
+
+def test_stale_small_distinct_count_grows_to_a_million_groups(gpu, plgpu_option):
+    import torch
+
+    import polaroid_amd as pl
+
+    g = torch.Generator(device="cuda")
+    g.manual_seed(11)
+    k = torch.randint(0, 2000, (N,), device="cuda", generator=g, dtype=torch.int64)
+    v = torch.rand(N, device="cuda", generator=g, dtype=torch.float64)
+    df = pl.DataFrame([pl.Series.from_torch("k", k), pl.Series.from_torch("v", v)])
+    plgpu_option("plan_cache", 1)
+    small = {}
+    _query(pl, df).collect(info=small)
+    assert small["groups"] <= 2000 and small["path"] != 3, small
+    # same buffers: ~1e6 random groups
+    k.copy_(torch.randint(0, 1_100_000, (N,), device="cuda", generator=g, dtype=torch.int64) * 7 - 5)
+    stale_info, again_info = {}, {}
+    stale = _query(pl, df).collect(info=stale_info)
+    again = _query(pl, df).collect(info=again_info)
+    plgpu_option("plan_cache", 0)
+    fresh_info = {}
+    fresh = _query(pl, df).collect(info=fresh_info)
+    assert fresh_info["groups"] > 900_000, fresh_info
+    for x, y, z in zip(_sorted(stale), _sorted(again), _sorted(fresh)):
+        assert np.array_equal(x, z) and np.array_equal(y, z)
+    assert stale_info["reruns"] > 0 or stale_info["path"] == fresh_info["path"], stale_info
+    # the contradicted entry was dropped: the next query planned afresh
+    assert again_info["path"] == fresh_info["path"] == 3, (again_info, fresh_info)
+    assert again_info["reruns"] == 0, again_info
+    # exact against math.fsum for a few groups
+    kh, vh = k.cpu().numpy(), v.cpu().numpy()
+    ks, ss, ls = _sorted(fresh)
+    m = vh > 0.5
+    order = np.argsort(kh[m], kind="stable")
+    sk, sv = kh[m][order], vh[m][order]
+    for i in range(0, len(ks), len(ks) // 7):
+        lo, hi = np.searchsorted(sk, ks[i]), np.searchsorted(sk, ks[i], side="right")
+        assert ls[i] == hi - lo
+        assert np.float64(ss[i].view(np.float64)) == math.fsum(sv[lo:hi])

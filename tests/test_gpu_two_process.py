@@ -4,7 +4,9 @@ gloo, with every device buffer of the exchange staged through host memory
 (distributed._a2a / _all_gather / _all_reduce switch on the gloo backend).
 
 Each rank runs the real GpuPartial begin / export / merge (the
-partial-state protocol, configs[4]'s path), the row shuffle (String keys
+partial-state protocol, configs[4]'s path; also with a 1e300 / 1e-300
+column wide on one rank only, carried as digit records over the agreed
+range), the row shuffle (String keys
 longer than 7 bytes), the first / last value exchange, and the join's
 shuffle strategy.  The union of the ranks' outputs must equal the
 single-GPU result on the concatenated shards bit for bit.  This is the
@@ -38,13 +40,20 @@ def _shard(rank, n=120_000):
     a[rng.random(n) < 0.01] = np.nan
     d = rng.uniform(-5, 5, n)
     long_keys = np.array([f"instrument-{i:04d}" for i in range(300)], dtype=object)[rng.integers(0, 300, n)]
-    return k, a, d, long_keys
+    # x: within one fixed-point window on rank 0, 1e300 / 1e-300 values on
+    # rank 1 (wider than any window): the wide-sum digit states
+    x = rng.standard_normal(n) * 50
+    if rank == 1:
+        x[rng.random(n) < 0.3] *= 1e300
+        x[rng.random(n) < 0.3] *= 1e-300
+    return k, a, d, long_keys, x
 
 
 def _frame(pl, rank):
-    k, a, d, s = _shard(rank)
+    k, a, d, s, x = _shard(rank)
     return pl.DataFrame({"k": pl.Series.from_numpy("k", k), "a": pl.Series.from_numpy("a", a),
-                         "d": pl.Series.from_numpy("d", d), "s": pl.Series("s", s.tolist(), pl.String)})
+                         "d": pl.Series.from_numpy("d", d), "s": pl.Series("s", s.tolist(), pl.String),
+                         "x": pl.Series.from_numpy("x", x)})
 
 
 def _rows(df, cols):
@@ -71,6 +80,12 @@ def _worker(rank, port, q):
             r = D.group_by_agg(df, "k", [pl.col("a").sum().alias("sa"), pl.col("d").mean().alias("md"),
                                          pl.len().alias("n")], pred, info=info)
             out["states"] = (_rows(r, ["k", "sa", "md", "n"]), info.get("protocol", "partial_states"))
+            info = {}
+            r = D.group_by_agg(df, "k", [pl.col("x").sum().alias("sx"), pl.col("x").mean().alias("mx"),
+                                         pl.col("a").sum().alias("sa")], pred, info=info)
+            out["wide"] = (_rows(r, ["k", "sx", "mx", "sa"]),
+                           (info.get("protocol", "partial_states"), info.get("wide_accs"), info.get("record_words"),
+                            info.get("exchange_bytes"), r.height))
             info = {}
             r = D.group_by_agg(df, "s", [pl.col("a").sum().alias("sa"), pl.col("d").first().alias("fd"),
                                          pl.col("d").last().alias("ld")], pred, info=info)
@@ -128,19 +143,23 @@ def test_two_rank_processes_real_kernels_over_gloo(gpu):
         assert p.exitcode == 0
     # the single-GPU results on the concatenated shards (rank order = row order)
     parts = [_shard(r) for r in range(WORLD)]
-    k, a, d, s = (np.concatenate([p[i] for p in parts]) for i in range(4))
+    k, a, d, s, x = (np.concatenate([p[i] for p in parts]) for i in range(5))
     full = pl.DataFrame({"k": pl.Series.from_numpy("k", k), "a": pl.Series.from_numpy("a", a),
-                         "d": pl.Series.from_numpy("d", d), "s": pl.Series("s", s.tolist(), pl.String)})
+                         "d": pl.Series.from_numpy("d", d), "s": pl.Series("s", s.tolist(), pl.String),
+                         "x": pl.Series.from_numpy("x", x)})
     pred = pl.col("d") > 0.0
     checks = {
         "states": full.lazy().filter(pred).group_by("k").agg(
             pl.col("a").sum().alias("sa"), pl.col("d").mean().alias("md"), pl.len().alias("n")).collect(),
+        "wide": full.lazy().filter(pred).group_by("k").agg(
+            pl.col("x").sum().alias("sx"), pl.col("x").mean().alias("mx"), pl.col("a").sum().alias("sa")).collect(),
         "shuffle": full.lazy().filter(pred).group_by("s").agg(
             pl.col("a").sum().alias("sa"), pl.col("d").first().alias("fd"), pl.col("d").last().alias("ld")).collect(),
         "first_last": full.lazy().group_by("k").agg(pl.col("d").first().alias("fd"),
                                                     pl.col("d").last().alias("ld")).collect(),
     }
-    cols = {"states": ["k", "sa", "md", "n"], "shuffle": ["s", "sa", "fd", "ld"], "first_last": ["k", "fd", "ld"]}
+    cols = {"states": ["k", "sa", "md", "n"], "wide": ["k", "sx", "mx", "sa"], "shuffle": ["s", "sa", "fd", "ld"],
+            "first_last": ["k", "fd", "ld"]}
     for name, ref in checks.items():
         union = {c: [] for c in cols[name]}
         seen = set()
@@ -153,6 +172,13 @@ def test_two_rank_processes_real_kernels_over_gloo(gpu):
                 union[c] += rows[c]
         _same(_canon(union, cols[name][0]), _canon(_rows(ref, cols[name]), cols[name][0]))
     assert res[0]["shuffle"][1] == "row_shuffle"
+    # the wide column kept the partial-state protocol on both ranks, as digit
+    # records of the agreed range; exchange bytes = records x record size
+    for r in range(WORLD):
+        proto, nwide, rwords, xbytes, groups = res[r]["wide"][1]
+        assert proto == "partial_states" and nwide == 1, res[r]["wide"][1]
+        assert rwords == res[0]["wide"][1][2] and rwords > 20
+        assert 0 < xbytes <= 2 * 400 * rwords * 8
     # join: every probe row of either shard against the union of the right
     # sides (the rows each rank holds), as a multiset
     def order(t):  # a total order with NaN payloads

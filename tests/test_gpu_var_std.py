@@ -238,10 +238,16 @@ def test_var_fused_exact_cases(gpu):
         assert math.isclose(v_, _exact_var(tight[(key == a_) & (k2 == b_)], 1), rel_tol=4e-16)
 
 
-def test_var_fused_batches_count_len(gpu):
-    """len() takes an accumulator of its own: two var columns (six
-    accumulators) next to len() run as fused batches, not the two-pass path
-    (ADVICE r3), and stay within 1e-12 of the checker."""
+def test_var_fused_batches_count_len(gpu, monkeypatch):
+    """len() rides on the first var column's accumulator: two var columns
+    (six accumulators) next to len() run as one fused pass, not
+    as batches nor the two-pass path, and stay within 1e-12 of
+    the checker."""
+    from polaroid_amd import frame as F
+
+    calls = []
+    inner = F._group_by_plain
+    monkeypatch.setattr(F, "_group_by_plain", lambda *a, **k: calls.append(1) or inner(*a, **k))
     rng = np.random.default_rng(5)
     n = 100_003
     key, x, y, xv = _var_frame(rng, n, 50)
@@ -252,6 +258,7 @@ def test_var_fused_batches_count_len(gpu):
            .agg(pl.col("x").var().alias("xv"), pl.col("y").var().alias("yv"), pl.len())
            .collect(info=info))
     assert info["var_path"] == "fused", info
+    assert len(calls) == 1, calls
     ones = np.ones(n, bool)
     keys, var, _, ok = _oracle(key, x, xv, 1, ones)
     assert np.array_equal(out["k"].to_numpy(), keys)
