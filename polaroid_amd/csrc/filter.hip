@@ -235,6 +235,7 @@ struct Scatter8Args {
     int32_t ncols;
 };
 
+template <bool PIPE>
 __global__ __launch_bounds__(kFilterThreads) void filter_scatter8_kernel(Scatter8Args a, int64_t n, int64_t ntiles,
                                                                          const uint64_t* __restrict__ mask_words,
                                                                          const uint64_t* __restrict__ tile_off) {
@@ -267,20 +268,39 @@ __global__ __launch_bounds__(kFilterThreads) void filter_scatter8_kernel(Scatter
             sel[it] = (w >> lane) & 1;
             pos[it] = base_off + prefix[wi] + (uint32_t)__popcll(w & lt_mask);
         }
-        for (int j = 0; j < a.ncols; ++j) {
-            // branch-free loads (row clamped at the end of the column): the
-            // lines are fetched whole anyway; only the stores are predicated
+        // branch-free loads (row clamped at the end of the column): the
+        // lines are fetched whole anyway; only the stores are predicated
+        auto load_col = [&](int j, uint64_t (&v)[IT]) {
             const uint64_t* __restrict__ src = a.src[j];
-            uint64_t* __restrict__ dst = a.dst[j];
-            uint64_t v[IT];
 #pragma unroll
             for (int it = 0; it < IT; ++it) {
                 const int64_t r = t * kTileRows + it * kFilterThreads + threadIdx.x;
                 v[it] = __builtin_nontemporal_load(src + (r < n ? r : n - 1));
             }
+        };
+        if (PIPE) {
+            // column j + 1's loads go out before column j's stores, so the
+            // wave always has a column's lines in flight
+            uint64_t v[IT], w[IT];
+            load_col(0, v);
+            for (int j = 0; j < a.ncols; ++j) {
+                if (j + 1 < a.ncols) load_col(j + 1, w);
+                uint64_t* __restrict__ dst = a.dst[j];
 #pragma unroll
-            for (int it = 0; it < IT; ++it)
-                if (sel[it]) dst[pos[it]] = v[it];
+                for (int it = 0; it < IT; ++it)
+                    if (sel[it]) dst[pos[it]] = v[it];
+#pragma unroll
+                for (int it = 0; it < IT; ++it) v[it] = w[it];
+            }
+        } else {
+            for (int j = 0; j < a.ncols; ++j) {
+                uint64_t v[IT];
+                load_col(j, v);
+                uint64_t* __restrict__ dst = a.dst[j];
+#pragma unroll
+                for (int it = 0; it < IT; ++it)
+                    if (sel[it]) dst[pos[it]] = v[it];
+            }
         }
         __syncthreads();
     }
@@ -407,8 +427,12 @@ static int run_filter(const plgpu_column* cols, int32_t ncols, int src, const De
     }
     if (!rc && sa.ncols > 0 && total > 0) {
         KtScope kt("filter_scatter8_kernel", s);
-        filter_scatter8_kernel<<<grid_for(ntiles, 1, 256 * 8), kFilterThreads, 0, s>>>(sa, n, ntiles, mask_words,
-                                                                                         offs);
+        if (options().filt_pipe != 0)
+            filter_scatter8_kernel<true><<<grid_for(ntiles, 1, 256 * 8), kFilterThreads, 0, s>>>(sa, n, ntiles,
+                                                                                               mask_words, offs);
+        else
+            filter_scatter8_kernel<false><<<grid_for(ntiles, 1, 256 * 8), kFilterThreads, 0, s>>>(sa, n, ntiles,
+                                                                                                mask_words, offs);
         PLGPU_HIP(hipGetLastError());
     }
     for (int i = 0; i < ncols && !rc; ++i) {

@@ -54,6 +54,7 @@ struct Options {
     int part_lds_kb = 0;  // partitioned path: LDS table budget per workgroup (0: 160 KiB)
     int rl_stream = 0;    // rolling windows <= 64, null-free: resident streaming waves (0: one block per wave; A/B)
     int rl_grid = 0;      // rolling stream kernel: workgroups per CU (0: 4)
+    int filt_pipe = 1;    // filter scatter: next column's loads before this column's stores (A/B)
 };
 Options& options();
 

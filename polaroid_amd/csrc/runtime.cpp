@@ -64,6 +64,7 @@ const OptField kOptFields[] = {
     {"part_lds_kb", "PLGPU_PART_LDS_KB", &Options::part_lds_kb},
     {"rl_stream", "PLGPU_RL_STREAM", &Options::rl_stream},
     {"rl_grid", "PLGPU_RL_GRID", &Options::rl_grid},
+    {"filt_pipe", "PLGPU_FILT_PIPE", &Options::filt_pipe},
 };
 const OptField* opt_field(const char* name) {
     for (const OptField& f : kOptFields)

@@ -126,9 +126,11 @@ def test_wide_sum_partial_states_bit_identical(gpu, world, layout):
         xv = rng.random(n) > 0.03
         shards_np.append((x, xv, b))
     key = rng.integers(0, 300, world * n).astype(np.int64) * 7919 - 11
-    # a cancelling group: +1e300 and -1e300 and a tiny value
+    # a cancelling group: +1e300 and -1e300 and a tiny value on a wide
+    # shard (+-1e3 otherwise)
     key[:6] = 42
-    shards_np[0][0][:6] = [1e300, -1e300, 3e-310, 1e300, -1e300, 2.5]
+    big, tiny = (1e300, 3e-310) if layout == "all_wide" else (1e3, 0.125)
+    shards_np[0][0][:6] = [big, -big, tiny, big, -big, 2.5]
     shards_np[0][1][:6] = True
     aggs = [("sum", "x"), ("mean", "x"), ("sum", "b"), ("count", "x"), ("len", "x")]
     shards = []
