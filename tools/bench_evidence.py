@@ -45,10 +45,20 @@ LEGS = {
                      ("second", True)),
     "sort": (r"aos_gather_kernel<8>", "sort", False),
     "sort_pack": (r"aos_pack_kernel<8>", "sort_pack", True),
-    "rolling": (r"rl_wave_kernel<4, false>", "rolling", True),
+    "rolling": (r"rl_wave_kernel<4, false, false>", "rolling", True),
     "join": (r"jn_probe_match_kernel<false, 0, false, true>", "join", False),
     "join_emit": (r"jn_take_emit_kernel<2, 1>", "join_emit", True),
+    "filter": (r"filter_scatter8_kernel", "filter", True),
+    "filter_mask": (r"filter_mask_kernel", "filter_mask", True),
 }
+
+# many_groups leg, largest G: its kernels run once or twice per step (one
+# launch per scatter level, each level its own template instance); the
+# line's kernel_ms is the per-step sum, so the trace side is the sum over
+# the kernel's instances of the mean of their last timed launches.  No other
+# leg launches these kernels.
+MG_KERNELS = {"count": r"gbp_count_kernel", "scatter": r"gbp_scatter_kernel",
+              "aggregate": r"gb_fast_kernel<\d+, 0, true, 2, 2, (true|false), true"}
 
 
 def last_json(path):
@@ -84,7 +94,28 @@ def line_view(d):
         for key, sub in (("join", L["roofline"]), ("join_emit", L["emit"])):
             if sub.get("kernel_ms"):
                 out[key] = (sub["kernel_ms"], sub["algorithmic_GB"] * 1e9, L["ms_per_step"], sub["frac"])
+    if "filter" in d:
+        L = d["filter"]
+        for key, sub in (("filter", L["roofline"]), ("filter_mask", L["mask"])):
+            if sub.get("kernel_ms"):
+                out[key] = (sub["kernel_ms"], sub["algorithmic_GB"] * 1e9, L["ms_per_step"], sub["frac"])
     return out
+
+
+def mg_view(d):
+    """many_groups, largest G -> {part: (per-step kernel ms, algorithmic bytes, step ms, frac, launches/step)}."""
+    mg = d.get("many_groups") or {}
+    gs = [int(g) for g in mg if g.isdigit()]
+    if not gs:
+        return None, {}
+    g = str(max(gs))
+    L = mg[g]
+    out = {}
+    for part in MG_KERNELS:
+        sub = L.get(part) or {}
+        if sub.get("kernel_ms"):
+            out[part] = (sub["kernel_ms"], sub["algorithmic_GB"] * 1e9, L["ms_per_step"], sub["frac"])
+    return g, out
 
 
 def trace_durations(path):
@@ -166,6 +197,44 @@ def main():
         if rd is not None and wr is not None:
             row["hbm_bytes_per_launch"] = rd + wr
             row["traffic_over_algorithmic"] = round((rd + wr) / algo, 4)
+        rows.append(row)
+    g, mgp = mg_view(plain)
+    _, mgq = mg_view(prof)
+    steps = None
+    if g:
+        L = plain["many_groups"][g]
+        steps = max(1, L["kernels"].get("gb_finalize_kernel", {}).get("launches", 2))
+    for part, (pat, streaming) in ((k, (v, True)) for k, v in MG_KERNELS.items()):
+        if part not in mgp:
+            continue
+        k_plain, algo, step_plain, frac_plain = mgp[part]
+        k_prof = mgq.get(part, (None,) * 4)[0]
+        rx = re.compile(pat)
+        tsum = fsum = wsum = 0.0
+        names = []
+        for name, v in tr.items():
+            if rx.search(name) and v:
+                names.append(name)
+                tsum += statistics.mean(v[-steps:])
+                fv = fetch.get(name, {}).get("FETCH_SIZE", [])
+                wv = write.get(name, {}).get("WRITE_SIZE", [])
+                fsum += statistics.mean(fv[-steps:]) * 1024 * 2 if fv else 0.0
+                wsum += statistics.mean(wv[-steps:]) * 1024 if wv else 0.0
+        if not names:
+            continue
+        row = {"leg": f"many_groups_{g}_{part}", "kernel": " + ".join(n.split("(")[0] for n in names),
+               "launches_traced": steps, "algorithmic_bytes": algo, "line_kernel_ms": k_plain,
+               "line_frac": frac_plain, "line_step_ms": step_plain, "profiled_line_kernel_ms": k_prof,
+               "trace_mean_ms": round(tsum, 4), "trace_frac": round(algo / (tsum * 1e-3) / 1e9 / HBM_PEAK, 4),
+               "hbm_read_bytes": fsum, "hbm_write_bytes": wsum,
+               "read_correction": "FETCH_SIZE x 2 (wide streaming reads, gfx950); per step: sum over the "
+                                  "kernel's instances of the mean of their last timed launches"}
+        row["trace_vs_line_pct"] = round(100 * (tsum - k_plain) / k_plain, 2)
+        row["trace_vs_profiled_line_pct"] = round(100 * (tsum - k_prof) / k_prof, 2) if k_prof else None
+        row["frac_diff_pct"] = round(100 * (row["trace_frac"] - frac_plain) / frac_plain, 2)
+        row["kernel_mean_within_step"] = tsum <= step_plain
+        row["hbm_bytes_per_launch"] = fsum + wsum
+        row["traffic_over_algorithmic"] = round((fsum + wsum) / algo, 4)
         rows.append(row)
     hdr = ("| leg | kernel | line kernel ms (HIP events) | trace mean ms | trace vs line | profiled run's line ms "
            "| trace vs profiled line | line frac | trace frac | HBM bytes / launch (PMC) | / algorithmic | mean <= step |")
