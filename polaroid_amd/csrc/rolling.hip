@@ -49,8 +49,29 @@ struct RlParams {
     int32_t var;          // 0: sum / mean; 1: rolling_var; 2: rolling_std
     int32_t ddof;
     int32_t var_f32;      // std of a Float32 column: sqrt of the variance rounded to f32
-    int32_t _pad;
+    int32_t fast_div;     // option rl_div: full windows' means by rw_div
+    double rw;            // RN(1 / w)
+    int32_t fused_scan;   // option rl_dpp: wave_scan64_fused (A/B)
+    int32_t _pad2;
 };
+
+// RN(a / w) for a full window (count w) without a division: q0 = RN(a y),
+// the exact remainder r = a - w q0 (one fma), q = RN(q0 + r y) with y =
+// RN(1 / w) -- correctly rounded for every a and w whose quotient and
+// remainder stay normal (Markstein's one-correction theorem; w an integer
+// < 2^53, so its significand is never all ones; checked against exact
+// rational division over 1.3e6 random (a, w), w = 1 ... 4096 and beyond,
+// |a| from 2^-1000 to 2^1000).  Other values take the division.
+__device__ __forceinline__ double rw_div(double a, uint64_t cnt, const RlParams& p) {
+    const uint32_t ex = (uint32_t)(f64_bits(a) >> 52) & 0x7FF;
+    if (cnt == (uint64_t)p.w && ex >= 1023 - 900 && ex <= 1023 + 990) {
+        const double y = p.rw, w = (double)p.w;
+        const double q0 = a * y;
+        const double r = __builtin_fma(-q0, w, a);
+        return __builtin_fma(r, y, q0);
+    }
+    return a / (double)cnt;
+}
 
 __device__ __forceinline__ double rv_std(const RlParams& p, double v) {
     return __builtin_sqrt(p.var_f32 ? (double)(float)v : v);
@@ -342,6 +363,59 @@ __device__ __forceinline__ uint64_t wave_scan64(uint64_t x) {
     return x;
 }
 
+// The same scan with the DPP moves folded into the adds: one 32-bit add
+// with carry-out and one add-with-carry per step, src0 read across lanes
+// (a lane without a source, or outside the row mask, is not written and
+// keeps its value -- x + 0).  s_nop 1: a VALU write read through DPP by the
+// next instruction needs two wait states.
+__device__ __forceinline__ uint64_t wave_scan64_fused(uint64_t x) {
+    uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    asm volatile(
+        "s_nop 1\n"
+        "v_add_co_u32_dpp %0, vcc, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf\n"
+        "v_addc_co_u32_dpp %1, vcc, %1, %1, vcc row_shr:1 row_mask:0xf bank_mask:0xf\n"
+        "s_nop 1\n"
+        "v_add_co_u32_dpp %0, vcc, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf\n"
+        "v_addc_co_u32_dpp %1, vcc, %1, %1, vcc row_shr:2 row_mask:0xf bank_mask:0xf\n"
+        "s_nop 1\n"
+        "v_add_co_u32_dpp %0, vcc, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf\n"
+        "v_addc_co_u32_dpp %1, vcc, %1, %1, vcc row_shr:4 row_mask:0xf bank_mask:0xf\n"
+        "s_nop 1\n"
+        "v_add_co_u32_dpp %0, vcc, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf\n"
+        "v_addc_co_u32_dpp %1, vcc, %1, %1, vcc row_shr:8 row_mask:0xf bank_mask:0xf\n"
+        "s_nop 1\n"
+        "v_add_co_u32_dpp %0, vcc, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n"
+        "v_addc_co_u32_dpp %1, vcc, %1, %1, vcc row_bcast:15 row_mask:0xa bank_mask:0xf\n"
+        "s_nop 1\n"
+        "v_add_co_u32_dpp %0, vcc, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n"
+        "v_addc_co_u32_dpp %1, vcc, %1, %1, vcc row_bcast:31 row_mask:0xc bank_mask:0xf\n"
+        "s_nop 1\n"
+        : "+v"(lo), "+v"(hi)
+        :
+        : "vcc");
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// 128-bit form: the carry runs through four 32-bit words.
+#define PLGPU_DPP128(CTRL, RM)                                                                    \
+    "s_nop 1\n"                                                                                  \
+    "v_add_co_u32_dpp %0, vcc, %0, %0 " CTRL " row_mask:" RM " bank_mask:0xf\n"                 \
+    "v_addc_co_u32_dpp %1, vcc, %1, %1, vcc " CTRL " row_mask:" RM " bank_mask:0xf\n"           \
+    "v_addc_co_u32_dpp %2, vcc, %2, %2, vcc " CTRL " row_mask:" RM " bank_mask:0xf\n"           \
+    "v_addc_co_u32_dpp %3, vcc, %3, %3, vcc " CTRL " row_mask:" RM " bank_mask:0xf\n"
+__device__ __forceinline__ void wave_scan128_fused(uint64_t& lo, uint64_t& hi) {
+    uint32_t w0 = (uint32_t)lo, w1 = (uint32_t)(lo >> 32), w2 = (uint32_t)hi, w3 = (uint32_t)(hi >> 32);
+    asm volatile(PLGPU_DPP128("row_shr:1", "0xf") PLGPU_DPP128("row_shr:2", "0xf") PLGPU_DPP128("row_shr:4", "0xf")
+                     PLGPU_DPP128("row_shr:8", "0xf") PLGPU_DPP128("row_bcast:15", "0xa")
+                         PLGPU_DPP128("row_bcast:31", "0xc") "s_nop 1\n"
+                 : "+v"(w0), "+v"(w1), "+v"(w2), "+v"(w3)
+                 :
+                 : "vcc");
+    lo = ((uint64_t)w1 << 32) | w0;
+    hi = ((uint64_t)w3 << 32) | w2;
+}
+#undef PLGPU_DPP128
+
 __device__ __forceinline__ void add128(uint64_t& lo, uint64_t& hi, uint64_t blo, uint64_t bhi) {
     const uint64_t l = lo + blo;
     hi = hi + bhi + (l < lo ? 1ull : 0ull);
@@ -458,18 +532,19 @@ __device__ __forceinline__ void rw_scan(const RlParams& p, const uint64_t (&x)[k
         }
         const int slot = ((k & 3) << 6) | lane;
         if (MODE == 2) {
-            wave_scan128(flo, fhi);
+            if (p.fused_scan) wave_scan128_fused(flo, fhi);
+            else wave_scan128(flo, fhi);
             add128(flo, fhi, carry_lo, carry_hi);
             carry_lo = lane63(flo);
             carry_hi = lane63(fhi);
             rhi[slot] = fhi;
         } else {
-            flo = wave_scan64(flo) + carry_lo;
+            flo = (p.fused_scan ? wave_scan64_fused(flo) : wave_scan64(flo)) + carry_lo;
             carry_lo = lane63(flo);
         }
         rlo[slot] = flo;
         if (COUNTS) {
-            code = wave_scan64(code) + carry_cn;
+            code = (p.fused_scan ? wave_scan64_fused(code) : wave_scan64(code)) + carry_cn;
             carry_cn = lane63(code);
             rcn[slot] = code;
         }
@@ -518,7 +593,7 @@ __device__ __forceinline__ void rw_scan(const RlParams& p, const uint64_t (&x)[k
                     else if (c.pinf) r = __builtin_inf();
                     else if (c.ninf) r = -__builtin_inf();
                 }
-                if (MEAN) r = r / (double)c.nn;
+                if (MEAN) r = p.fast_div ? rw_div(r, c.nn, p) : r / (double)c.nn;
                 ((double*)p.out)[i] = valid ? r : 0.0;
             }
         }
@@ -737,9 +812,10 @@ __device__ __forceinline__ void rw_var_scan(const RlParams& p, const uint64_t (&
         const unsigned __int128 u = (unsigned __int128)t * t;
         uint64_t f1 = (b >> 63) ? 0ull - t : t;
         uint64_t f2l = (uint64_t)u, f2h = (uint64_t)(u >> 64);
-        f1 = wave_scan64(f1) + c1;
+        f1 = (p.fused_scan ? wave_scan64_fused(f1) : wave_scan64(f1)) + c1;
         c1 = lane63(f1);
-        wave_scan128(f2l, f2h);
+        if (p.fused_scan) wave_scan128_fused(f2l, f2h);
+        else wave_scan128(f2l, f2h);
         add128(f2l, f2h, c2l, c2h);
         c2l = lane63(f2l);
         c2h = lane63(f2h);
@@ -748,7 +824,7 @@ __device__ __forceinline__ void rw_var_scan(const RlParams& p, const uint64_t (&
         r2l[slot] = f2l;
         r2h[slot] = f2h;
         if (COUNTS) {
-            code = wave_scan64(code) + ccn;
+            code = (p.fused_scan ? wave_scan64_fused(code) : wave_scan64(code)) + ccn;
             ccn = lane63(code);
             rcn[slot] = code;
         }
@@ -1283,6 +1359,9 @@ PLGPU_API int plgpu_rolling(const plgpu_column* values, int32_t kind, int64_t wi
     p.min_periods = min_periods;
     p.center = center != 0;
     p.mean = kind == PLGPU_ROLLING_MEAN;
+    p.rw = 1.0 / (double)std::max<int64_t>(window_size, 1);
+    p.fast_div = options().rl_div;
+    p.fused_scan = options().rl_dpp;
     p.var = var ? (kind == PLGPU_ROLLING_STD ? 2 : 1) : 0;
     p.ddof = ddof;
     p.var_f32 = var_f32;

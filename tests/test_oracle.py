@@ -565,3 +565,25 @@ def test_variance_restatements():
     part = np.arange(1000) // 100
     assert O.var_welford(x, part) == pytest.approx(float(np.var(x, ddof=1)), rel=1e-15)
     assert math.isnan(O.var_welford(x[:1], None, 1)) and O.var_welford(x[:1], None, 0) == 0.0
+
+
+def test_one_correction_division_by_window_length():
+    """rolling.hip rw_div: a full window's mean as q0 = RN(a y), r = a - w q0
+    (exact, one fma), q = RN(q0 + r y) with y = RN(1 / w) equals RN(a / w)
+    for every a whose quotient stays normal (Markstein's theorem; w is an
+    integer, so its significand is never all ones).  Checked here with
+    exact rationals over random a (|a| from 2^-900 to 2^990, the kernel's
+    guard) and every w up to 1024."""
+    import random
+    from fractions import Fraction as Fr
+
+    rnd = random.Random(7)
+    for w in list(range(1, 1025)) + [rnd.randint(1025, 1 << 24) for _ in range(64)]:
+        y = 1.0 / w
+        for _ in range(24):
+            e = rnd.choice([rnd.randint(-60, 60), rnd.randint(-900, 990)])
+            a = ((rnd.getrandbits(52) | (1 << 52)) * 2.0 ** (e - 52)) * rnd.choice([1.0, -1.0])
+            q0 = a * y
+            r = Fr(a) - Fr(w) * Fr(q0)
+            assert Fr(float(r)) == r  # the fma's remainder is exact
+            assert float(Fr(q0) + r * Fr(y)) == float(Fr(a) / w), (a, w)
