@@ -66,7 +66,6 @@ const OptField kOptFields[] = {
     {"rl_grid", "PLGPU_RL_GRID", &Options::rl_grid},
     {"filt_pipe", "PLGPU_FILT_PIPE", &Options::filt_pipe},
     {"rl_div", "PLGPU_RL_DIV", &Options::rl_div},
-    {"rl_dpp", "PLGPU_RL_DPP", &Options::rl_dpp},
 };
 const OptField* opt_field(const char* name) {
     for (const OptField& f : kOptFields)
