@@ -104,7 +104,8 @@ struct PsGeom {
 };
 
 struct PsTile {
-    int64_t lo, hi;  // rows of the tile
+    int64_t base;    // the tile's kPsTile-aligned block of rows (its loads)
+    int64_t lo, hi;  // rows of the tile (within the block)
     int64_t mbase;   // count matrix entry of (tile, digit d): mbase + d * ntq + tl
     int64_t ntq, tl;
 };
@@ -112,37 +113,43 @@ struct PsTile {
 __device__ __forceinline__ PsTile ps_tile(const PsGeom& g, int64_t t) {
     PsTile x;
     if (g.range == nullptr) {
-        x.lo = t * kPsTile;
+        x.base = x.lo = t * kPsTile;
         x.hi = std::min<int64_t>(g.n, x.lo + kPsTile);
         x.mbase = 0;
         x.ntq = g.ntiles;
         x.tl = t;
     } else {
+        // level 2: the aligned blocks of the level-1 buffers that level-1
+        // partition q touches, each cut to the partition's rows (aligned
+        // loads: a partition starts anywhere)
         const uint32_t q = g.tpart[t];
         const uint32_t t0 = g.tstart[q];
         x.ntq = (int64_t)(g.tstart[q + 1] - t0);
         x.tl = t - t0;
         x.mbase = (int64_t)t0 << g.dbits;
-        x.lo = (int64_t)g.range[q] + x.tl * kPsTile;
-        x.hi = std::min<int64_t>((int64_t)g.range[q + 1], x.lo + kPsTile);
+        const int64_t r0 = (int64_t)g.range[q], r1 = (int64_t)g.range[q + 1];
+        x.base = (r0 & ~(int64_t)(kPsTile - 1)) + x.tl * kPsTile;
+        x.lo = std::max<int64_t>(r0, x.base);
+        x.hi = std::min<int64_t>(r1, x.base + kPsTile);
     }
     return x;
 }
 
-// Row k of this thread within its tile (c0 + k * 64 + lane, clamped to the
-// tile's last row): f(k, i) for k = 0 .. kPsPer - 1.  A full tile takes the
-// unclamped form, whose offsets are one register plus immediates (with a
-// uniform base pointer: saddr loads, no 64-bit address per row).
+// Row k of this thread within its tile's block (c0 + k * 64 + lane,
+// clamped to the tile's rows [lo, hi)): f(k, i) for k = 0 .. kPsPer - 1, i
+// relative to the block.  A full tile takes the unclamped form, whose
+// offsets are one register plus immediates (with a uniform base pointer:
+// saddr loads, no 64-bit address per row).
 template <typename F>
 __device__ __forceinline__ void ps_rows(const PsTile& tl, int c0, F&& f) {
     const uint32_t i0 = (uint32_t)(c0 + (int)(threadIdx.x & 63));
-    if (tl.hi - tl.lo == kPsTile) {
+    if (tl.lo == tl.base && tl.hi - tl.base == kPsTile) {
 #pragma unroll
         for (int k = 0; k < kPsPer; ++k) f(k, i0 + (uint32_t)(k * 64));
     } else {
-        const uint32_t last = (uint32_t)(tl.hi - tl.lo - 1);
+        const uint32_t first = (uint32_t)(tl.lo - tl.base), last = (uint32_t)(tl.hi - tl.base - 1);
 #pragma unroll
-        for (int k = 0; k < kPsPer; ++k) f(k, min(i0 + (uint32_t)(k * 64), last));
+        for (int k = 0; k < kPsPer; ++k) f(k, min(max(i0 + (uint32_t)(k * 64), first), last));
     }
 }
 
@@ -153,10 +160,10 @@ template <bool L2, bool F8>
 __device__ __forceinline__ void ps_col(const DevCol& c, const uint64_t* buf, const PsTile& tl, int c0,
                                        uint64_t (&v)[kPsPer]) {
     if (L2 || F8) {
-        const uint64_t* b = (L2 ? buf : (const uint64_t*)c.values + c.offset) + tl.lo;
+        const uint64_t* b = (L2 ? buf : (const uint64_t*)c.values + c.offset) + tl.base;
         ps_rows(tl, c0, [&](int k, uint32_t i) { v[k] = __builtin_nontemporal_load(b + i); });
     } else {
-        ps_rows(tl, c0, [&](int k, uint32_t i) { v[k] = dev_load(c, tl.lo + (int64_t)i); });
+        ps_rows(tl, c0, [&](int k, uint32_t i) { v[k] = dev_load(c, tl.base + (int64_t)i); });
     }
 }
 
@@ -173,8 +180,8 @@ __device__ __forceinline__ void ps_keys(const GbParams& p, const DevProgram& pro
     if (!L2 && PRED == 1) ps_col<false, F8>(p.pred_col, nullptr, tl, c0, pv);
 #pragma unroll
     for (int k = 0; k < kPsPer; ++k) {
-        const int64_t r = tl.lo + c0 + k * 64 + lane;
-        bool s = r < tl.hi;
+        const int64_t r = tl.base + c0 + k * 64 + lane;
+        bool s = r >= tl.lo && r < tl.hi;
         if (!L2 && PRED == 1)
             s = s && (F8 || dev_valid(p.pred_col, r)) &&
                 simple_pred(prog.simple_isf, prog.simple_op, pv[k], prog.simple_imm);
@@ -314,10 +321,10 @@ __global__ __launch_bounds__(kPsThreads) void gbp_scatter_kernel(GbParams p, Dev
 #pragma unroll
                 for (int k = 0; k < kPsPer; ++k) cv[k] = pv[k];
             } else if (rows && L2) {
-                const uint32_t* b = in.rows + tl.lo;
+                const uint32_t* b = in.rows + tl.base;
                 ps_rows(tl, c0, [&](int k, uint32_t i) { cv[k] = (uint64_t)__builtin_nontemporal_load(b + i); });
             } else if (rows) {
-                ps_rows(tl, c0, [&](int k, uint32_t i) { cv[k] = (uint64_t)(tl.lo + (int64_t)i); });
+                ps_rows(tl, c0, [&](int k, uint32_t i) { cv[k] = (uint64_t)(tl.base + (int64_t)i); });
             } else {
                 ps_col<L2, F8>(p.acc[a].c, L2 ? in.acc[a] : nullptr, tl, c0, cv);
             }
@@ -2287,8 +2294,9 @@ static hipError_t gbp_pass1(const GbRun& R, bool f8, const PsGeom& g, uint32_t* 
 // Partition buffers for `rows` selected rows: key, nacc columns, row ids.
 static int gbp_alloc(GbRun& R, int64_t sel, uint64_t** buf, PartOut* o) {
     const GbParams& p = R.pl.p;
-    // even, so every column's buffer starts 16-byte aligned (pair loads)
-    const int64_t rows = ((int64_t)std::max<int64_t>(sel, 2) + 3) & ~int64_t(1);
+    // a multiple of 16 rows, so every column's buffer starts on a 128-B line
+    // (pair loads; the level-2 tiles' aligned block loads)
+    const int64_t rows = ((int64_t)std::max<int64_t>(sel, 2) + 17) & ~int64_t(15);
     const bool want_rows = p.f_first >= 0 || p.f_last >= 0;
     const size_t words = (size_t)rows * (1 + p.nacc) + (want_rows ? ((size_t)rows + 1) / 2 : 0);
     int rc = dev_alloc((void**)buf, words * 8, R.s);
@@ -2366,7 +2374,8 @@ static int gb_partition(GbRun& R) {
         uint64_t t = 0;
         for (int q = 0; q < P1; ++q) {
             ts[q] = (uint32_t)t;
-            t += (hr1[q + 1] - hr1[q] + kPsTile - 1) / kPsTile;
+            // the aligned blocks this partition's rows touch (ps_tile)
+            if (hr1[q + 1] > hr1[q]) t += ((hr1[q + 1] - 1) / kPsTile) - (hr1[q] / kPsTile) + 1;
         }
         ts[P1] = (uint32_t)t;
         PsGeom g2;

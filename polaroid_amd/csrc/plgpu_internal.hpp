@@ -55,6 +55,7 @@ struct Options {
     int rl_stream = 0;    // rolling windows <= 64, null-free: resident streaming waves (0: one block per wave; A/B)
     int rl_grid = 0;      // rolling stream kernel: workgroups per CU (0: 4)
     int filt_pipe = 1;    // filter scatter: next column's loads before this column's stores (A/B)
+    int part_threads = 0; // partitioned aggregation: threads per workgroup (0: 1024; A/B)
     int rl_div = 1;       // rolling mean of full windows by one correction step instead of a division (A/B)
 };
 Options& options();

@@ -66,6 +66,7 @@ const OptField kOptFields[] = {
     {"rl_grid", "PLGPU_RL_GRID", &Options::rl_grid},
     {"filt_pipe", "PLGPU_FILT_PIPE", &Options::filt_pipe},
     {"rl_div", "PLGPU_RL_DIV", &Options::rl_div},
+    {"part_threads", "PLGPU_PART_THREADS", &Options::part_threads},
 };
 const OptField* opt_field(const char* name) {
     for (const OptField& f : kOptFields)
