@@ -72,13 +72,13 @@ def test_stale_small_distinct_count_grows_to_a_million_groups(gpu, plgpu_option)
 
     g = torch.Generator(device="cuda")
     g.manual_seed(11)
-    k = torch.randint(0, 2000, (N,), device="cuda", generator=g, dtype=torch.int64)
+    k = torch.randint(0, 500, (N,), device="cuda", generator=g, dtype=torch.int64)
     v = torch.rand(N, device="cuda", generator=g, dtype=torch.float64)
     df = pl.DataFrame([pl.Series.from_torch("k", k), pl.Series.from_torch("v", v)])
     plgpu_option("plan_cache", 1)
     small = {}
     _query(pl, df).collect(info=small)
-    assert small["groups"] <= 2000 and small["path"] != 3, small
+    assert small["groups"] <= 500 and small["path"] != 3, small  # one LDS table
     # same buffers: ~1e6 random groups
     k.copy_(torch.randint(0, 1_100_000, (N,), device="cuda", generator=g, dtype=torch.int64) * 7 - 5)
     stale_info, again_info = {}, {}
