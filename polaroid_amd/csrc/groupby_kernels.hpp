@@ -400,7 +400,8 @@ __device__ __forceinline__ int64_t g_find(const GbParams& p, uint64_t key) {
 // returned in l0, l1 (l2 = 0).  Returns false (limbs 0) when the value needs
 // fx_limbs (inf / NaN, bits below the window, overflow).
 template <int LIMBS>
-__device__ __forceinline__ bool fx_limbs_fast(uint64_t x, int bottom, uint64_t& l0, uint64_t& l1, uint64_t& l2) {
+__device__ __forceinline__ bool fx_limbs_fast(uint64_t x, int bottom, uint64_t& l0, uint64_t& l1, uint64_t& l2,
+                                              bool nonneg = false) {
     if (LIMBS == 2) {
         // The 2-limb form with the least VALU work (the fused kernels are
         // issue-bound): the mantissa keeps its implicit bit only for ex != 0,
@@ -416,7 +417,9 @@ __device__ __forceinline__ bool fx_limbs_fast(uint64_t x, int bottom, uint64_t& 
         const bool inrange = sh <= (uint32_t)(W - 53) && ex != 0;
         const bool zero = ((hi << 1) | lo) == 0;
         const uint64_t m = (x & 0x000FFFFFFFFFFFFFull) | ((uint64_t)(ex != 0 ? 1u : 0u) << 52);
-        const int64_t sm = (int32_t)hi < 0 ? -(int64_t)m : (int64_t)m;
+        // nonneg: the caller knows x >= 0 (the variance triple's x * x), no
+        // sign to apply (a NaN's sign does not matter: it fails the window)
+        const int64_t sm = (!nonneg && (int32_t)hi < 0) ? -(int64_t)m : (int64_t)m;
         l0 = ((uint64_t)sm << (sh & 63)) & M40;
         l1 = (uint64_t)(sm >> ((40 - sh) & 63));  // sh <= 27 when used
         l2 = 0;
@@ -1480,7 +1483,7 @@ __global__ __launch_bounds__(PART && !RUNS ? kGbPartThreads : kGbThreads) void g
                     uint64_t fl0[NA], fl1[NA], fl2[NA];
 #pragma unroll
                     for (int a = 0; a < NACC; ++a) {
-                        const bool ok = fx_limbs_fast<LIMBS>(rv[a], bot[a], fl0[a], fl1[a], fl2[a]);
+                        const bool ok = fx_limbs_fast<LIMBS>(rv[a], bot[a], fl0[a], fl1[a], fl2[a], VAR && a == 1);
                         slow |= (ok ? 0u : 1u) << a;
                     }
                     // the limbs of a slow value are not added here (2 limbs:
