@@ -817,9 +817,17 @@ def main():
         result["std"] = std_leg(torch, pl, df, args.steps, args.warmup)
         progress("std leg done")
     if rank == 0 and world == 1 and not args.no_keys:
+        torch.cuda.empty_cache()
+        pl._native.release_cached()
         result["keys"] = keys_leg(torch, pl, sym, cols, args.leg_steps * 2, 2, ms_per_step)
         progress("keys leg done")
     if rank == 0 and world == 1 and not args.no_filter:
+        # the earlier legs' frames are gone; their cached device blocks are
+        # returned first, so the filter's outputs come from a clean pool (as
+        # in a standalone run: 11.6-12.5 ms against 14.1 ms per step behind a
+        # fragmented cache, gpurun_out/r05x_*)
+        torch.cuda.empty_cache()
+        pl._native.release_cached()
         result["filter"] = filter_leg(torch, pl, df, args.leg_steps, 2, int(args.cpu_rows), args.cpu_seconds / 2,
                                       args.no_cpu)
         progress(f"filter leg: {result['filter']['ms_per_step']} ms per step")
