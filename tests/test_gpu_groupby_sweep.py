@@ -16,8 +16,8 @@ Where the inputs rule a path out (nulls for the fused and partitioned paths,
 the next path that accepts them; `_expect_path` states which, so a path
 refusing more than DESIGN.md "Group-by paths" lists is a failure too.  The
 derived-input (DERIV), variance-triple (VAR), keyless, packed multi-key
-(PACK 1), String-key (PACK 2), sorted-key (RUNS) and wide-sum variants are
-crossed with the same paths below.
+(PACK 1), String-key (PACK 2), sorted-key (RUNS), range-local (time-ordered
+keys) and wide-sum variants are crossed with the same paths below.
 
 This is the class of test that would have caught the partition scatter's
 row-id bug of rounds 2-3 (DESIGN.md "Multi-key operators", round-4 fix).
@@ -270,6 +270,45 @@ def test_sweep_sorted_keys(gpu, path, plgpu_option):
                 for maintain in (False, True):
                     out, info = _gpu(df, "k", specs, pf() if pf else None, maintain)
                     _compare(out, "k", exp, len(specs), maintain, (path, ncol, pname, maintain, info.get("path")))
+
+
+@pytest.mark.parametrize("path", ["auto", "generic_global", "part2"])
+def test_sweep_range_local(gpu, path, plgpu_option):
+    """Time-ordered keys (the range-local fused table: each workgroup one
+    contiguous run of tiles, its LDS table sized for that range's keys) x
+    1-6 aggregated columns (sum-only and mixed) x maintain_order x predicate,
+    and the same frame forced onto the global table and the partitioned
+    path.  Exact vs the oracle, first-occurrence order included."""
+    rng = np.random.default_rng(31)
+    n = 4_500_001
+    day = (np.arange(n) * 200) // n
+    k = (rng.integers(0, 150, n) + 1000 * day).astype(np.int64)  # 30k groups, 150 per row range
+    c = rng.uniform(10, 500, n)
+    cols = {"k": (k, None), "c": (c, None), "b": (rng.uniform(0.5, 2.0, n), None),
+            "a": (rng.standard_normal(n) * 100, None), "d": (rng.uniform(-5, 5, n), None),
+            "e": (c * rng.uniform(0.99, 1.01, n), None), "f": (rng.uniform(1, 1000, n), None),
+            "q": (rng.integers(-10**12, 10**12, n).astype(np.int64), None)}
+    df = pl.DataFrame({nm: pl.Series.from_numpy(nm, v, m) for nm, (v, m) in cols.items()})
+    _set(plgpu_option, path)
+    saw_local = False
+    for pool in (SUMONLY, MIXED[:3] + [("max", "e"), ("count", "f"), ("sum", "q")]):
+        for ncol in (1, 2, 4, 6):
+            specs = [(kind, col(c_)) for kind, c_ in pool[:ncol]]
+            for pname in ("none", "simple", "program"):
+                pf = PREDS[pname]
+                exp = _oracle(cols, "k", specs, pf() if pf else None, n)
+                for maintain in (False, True):
+                    out, info = _gpu(df, "k", specs, pf() if pf else None, maintain)
+                    tag = (path, ncol, pname, maintain, info.get("path"), info.get("local_range"))
+                    _compare(out, "k", exp, len(specs), maintain, tag)
+                    if info["local_range"]:
+                        saw_local = True
+                        assert info["path"] in (1, 2), tag
+                    if path != "auto" or pname == "program":
+                        assert info["local_range"] == 0, tag  # the fused kernel only
+    # (the plan takes the range-local table while a range's keys fit one LDS
+    # table in the full layout: the narrower column counts here)
+    assert saw_local == (path == "auto")
 
 
 def _var_check(out, cols, key, xname, ddof, pred_mask, maintain, tag):
