@@ -232,7 +232,7 @@ def vwap_leg(torch, pl, df, sym, close, steps: int, warmup: int) -> dict:
     r = timed_leg(torch, q, n, steps, warmup, 24)
     del vdf, vol
     return {"query": "filter(close > 250).group_by(symbol).agg((close * volume).sum(), volume.sum())",
-            "kernel": "gb_fast_kernel<NACC=2,PRED=1,SUMONLY,DERIV> (close * volume in registers)", **r}
+            "kernel": "gb_fast_kernel<NACC=2,PRED=1,SUMONLY,VAR=2> (product pair: close * volume in registers)", **r}
 
 
 def std_leg(torch, pl, df, steps: int, warmup: int) -> dict:

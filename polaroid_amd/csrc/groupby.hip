@@ -1518,6 +1518,9 @@ static hipError_t launch_fast_dispatch(const Plan& pl, const DevProgram& dp, int
     }
     if (dv && var_triple(pl) && !pl.runs)
         return pred == 0 ? launch_fast_var<0>(pl, dp, s) : launch_fast_var<1>(pl, dp, s);
+    const int pair = dv && options().gb_pair ? product_pair(pl) : -1;
+    if (pair == 0) return pred == 0 ? launch_fast_pair<0, 2>(pl, dp, s) : launch_fast_pair<1, 2>(pl, dp, s);
+    if (pair == 1) return pred == 0 ? launch_fast_pair<0, 3>(pl, dp, s) : launch_fast_pair<1, 3>(pl, dp, s);
     if (dv) {
         switch (pl.p.nacc) {
         case 1: return launch_fast_nacc<1, true>(pl, dp, pred, s);

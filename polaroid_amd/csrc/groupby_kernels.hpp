@@ -1076,17 +1076,23 @@ __device__ __forceinline__ void fast_share(const int32_t (&vf)[NACC > 0 ? NACC :
 // the register-run variant keeps kGbThreads, its registers would spill)
 constexpr int kGbPartThreads = 1024;
 template <int NACC, int PRED, bool SUMONLY, int ROWS, int LIMBS = 3, bool RUNS = false, bool PART = false,
-          bool DERIV = false, bool VAR = false, int PACK = 0>
+          bool DERIV = false, int VAR = 0, int PACK = 0>
 __global__ __launch_bounds__(PART && !RUNS ? kGbPartThreads : kGbThreads) void gb_fast_kernel(GbParams p,
                                                                                                DevProgram prog) {
     static_assert(!PACK || !PART, "PACK: the single-table kernel");
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
     constexpr int NA = NACC > 0 ? NACC : 1;
-    // VAR (sum-only, NACC 3): the fused variance's three sums of one column
+    // VAR 1 (sum-only, NACC 3): the fused variance's three sums of one column
     // x -- x, h = x * x and l = fma(x, x, -h) -- with h and l computed from
-    // x's registers: one column loaded, no operand registers per acc
-    static_assert(!VAR || (NACC == 3 && !DERIV), "VAR: three sums of one column");
-    constexpr int NL = VAR ? 1 : NACC;  // accs whose column the tile loads
+    // x's registers: one column loaded, no operand registers per acc.
+    // VAR 2 / 3 (NACC 2): a product and one of its operands ((close *
+    // volume).sum() next to volume.sum()): the tile loads acc 0's and acc
+    // 1's columns as plain sums do, acc VAR - 2 sums v[0] * v[1] (the host
+    // puts the product's other operand in its column, pair_normalize), with
+    // none of the general derived path's operand registers or op switch
+    static_assert(VAR != 1 || (NACC == 3 && !DERIV), "VAR 1: three sums of one column");
+    static_assert(VAR < 2 || (NACC == 2 && !DERIV), "VAR 2 / 3: a product and its operand");
+    constexpr int NL = VAR == 1 ? 1 : NACC;  // accs whose column the tile loads
     // SLIM (sum-only, 2 limbs): fields key 0, len 1, acc a: limbs 2+3a,
     // 3+3a, flags 4+3a (the unused low limb of the 3-limb layout is not
     // stored, so more workgroups fit per CU).  The keys are one array (the
@@ -1377,7 +1383,7 @@ __global__ __launch_bounds__(PART && !RUNS ? kGbPartThreads : kGbThreads) void g
             bool sel = true;
             if (PRED == 1) {
                 uint64_t x = cur.pv[j];
-                if (VAR) {
+                if (VAR == 1) {
                     if (p.pred_acc >= 0) x = cur.v[0][j];  // every acc reads x's column
                 } else {
 #pragma unroll
@@ -1415,8 +1421,10 @@ __global__ __launch_bounds__(PART && !RUNS ? kGbPartThreads : kGbThreads) void g
                 int bot[NA];
 #pragma unroll
                 for (int a = 0; a < NA; ++a) {
-                    if (VAR) {
+                    if (VAR == 1) {
                         rv[a] = a == 0 ? cur.v[0][0] : derive(a == 1 ? DOP_SQHI : DOP_SQLO, cur.v[0][0], 0ull);
+                    } else if (VAR >= 2) {
+                        rv[a] = a == VAR - 2 ? f64_bits(as_f64(cur.v[0][0]) * as_f64(cur.v[1][0])) : cur.v[a][0];
                     } else {
                         rv[a] = cur.v[a][0];
                         if (DERIV && dop0[a] != DOP_NONE)
@@ -1483,7 +1491,7 @@ __global__ __launch_bounds__(PART && !RUNS ? kGbPartThreads : kGbThreads) void g
                     uint64_t fl0[NA], fl1[NA], fl2[NA];
 #pragma unroll
                     for (int a = 0; a < NACC; ++a) {
-                        const bool ok = fx_limbs_fast<LIMBS>(rv[a], bot[a], fl0[a], fl1[a], fl2[a], VAR && a == 1);
+                        const bool ok = fx_limbs_fast<LIMBS>(rv[a], bot[a], fl0[a], fl1[a], fl2[a], VAR == 1 && a == 1);
                         slow |= (ok ? 0u : 1u) << a;
                     }
                     // the limbs of a slow value are not added here (2 limbs:
@@ -1665,7 +1673,25 @@ inline int resident_per_cu(const void* kern, int threads, size_t lds) {
     return nb;
 }
 
-template <int NACC, int PRED, bool SUMONLY, int LIMBS = 3, bool RUNS = false, bool DERIV = false, bool VAR = false,
+inline bool same_dev_col(const DevCol& x, const DevCol& y) {
+    return x.values == y.values && x.offset == y.offset && x.dtype == y.dtype && x.validity == y.validity;
+}
+
+// The product pair's launch parameters (gb_fast_kernel VAR 2 / 3): acc pi's
+// column becomes the product's operand that is not the other acc's column
+// (x * y commutes exactly), and a simple predicate (pred) shares the acc
+// whose column it reads.
+inline void pair_normalize(GbParams& q, int pi, bool pred) {
+    AccSpec& pa = q.acc[pi];
+    if (!same_dev_col(pa.c2, q.acc[1 - pi].c)) std::swap(pa.c, pa.c2);
+    if (pred) {
+        q.pred_acc = -1;
+        for (int a = 0; a < 2 && q.pred_acc < 0; ++a)
+            if (same_dev_col(q.acc[a].c, q.pred_col)) q.pred_acc = a;
+    }
+}
+
+template <int NACC, int PRED, bool SUMONLY, int LIMBS = 3, bool RUNS = false, bool DERIV = false, int VAR = 0,
           int PACK = 0, int ROWS = 2>
 hipError_t launch_fast_rows(const Plan& pl, const DevProgram& dp, hipStream_t s) {
     const void* kern = (const void*)gb_fast_kernel<NACC, PRED, SUMONLY, ROWS, LIMBS, RUNS, false, DERIV, VAR, PACK>;
@@ -1677,6 +1703,7 @@ hipError_t launch_fast_rows(const Plan& pl, const DevProgram& dp, hipStream_t s)
     const size_t lds = (SUMONLY && LIMBS == 2) ? (size_t)slim_words(NACC) * (pl.p.lcap + 2) * 8 : pl.lds_bytes;
     GbParams q = pl.p;
     q.tiles_per_wg = 0;
+    if (VAR >= 2) pair_normalize(q, VAR - 2, PRED == 1);
     // the plan's n_full is a multiple of the 2-row tile; a wider tile takes
     // its own multiple (the masked last tile covers the rest)
     if (ROWS != 2) q.n_full = (pl.p.n / ((int64_t)kGbThreads * ROWS)) * kGbThreads * ROWS;
@@ -1698,7 +1725,7 @@ hipError_t launch_fast_rows(const Plan& pl, const DevProgram& dp, hipStream_t s)
     const int grid = (int)g;
     pl.launched_grid = grid;
     pl.launched_runs = RUNS;
-    pl.launched_var = VAR;
+    pl.launched_var = VAR == 1;
     if (pl.local) {
         const int64_t tile = (int64_t)kGbThreads * ROWS;
         const int64_t nall = q.n_full / tile + (pl.p.n > q.n_full ? 1 : 0);
@@ -1758,6 +1785,30 @@ hipError_t launch_fast_var(const Plan& pl, const DevProgram& dp, hipStream_t s) 
     return launch_fast_rows<3, PRED, true, 3, false, false, true>(pl, dp, s);
 }
 
+
+// A product and one of its operands, f64 sums on the sum-only layout:
+// (close * volume).sum() next to volume.sum(), in either order.  Returns the
+// product's acc index, or -1.
+inline int product_pair(const Plan& pl) {
+    const GbParams& p = pl.p;
+    if (p.nacc != 2 || !pl.sum_only) return -1;
+    for (int pi = 0; pi < 2; ++pi) {
+        const AccSpec& pa = p.acc[pi];
+        const AccSpec& oa = p.acc[1 - pi];
+        if ((pa.dop & ~DOP_SWAP) != DOP_MUL || oa.dop != DOP_NONE) continue;
+        if (pa.c.dtype != PLGPU_F64 || pa.c2.dtype != PLGPU_F64 || oa.c.dtype != PLGPU_F64) continue;
+        if (pa.c.validity || pa.c2.validity || oa.c.validity) continue;
+        if (same_dev_col(pa.c2, oa.c) || same_dev_col(pa.c, oa.c)) return pi;
+    }
+    return -1;
+}
+
+template <int PRED, int VAR>
+hipError_t launch_fast_pair(const Plan& pl, const DevProgram& dp, hipStream_t s) {
+    if (pl.limbs == 2 && pl.runs) return launch_fast_rows<2, PRED, true, 2, true, false, VAR>(pl, dp, s);
+    if (pl.limbs == 2) return launch_fast_rows<2, PRED, true, 2, false, false, VAR>(pl, dp, s);
+    return launch_fast_rows<2, PRED, true, 3, false, false, VAR>(pl, dp, s);
+}
 
 template <int NACC, int LIMBS, bool RACC>
 hipError_t launch_part_fast(const Plan& pp, int grid, hipStream_t s) {
@@ -1824,6 +1875,10 @@ extern template hipError_t launch_fast_nacc<6, false, 2>(const Plan&, const DevP
 extern template hipError_t launch_part_fast_limbs<6>(const Plan&, int, hipStream_t);
 extern template hipError_t launch_fast_var<0>(const Plan&, const DevProgram&, hipStream_t);
 extern template hipError_t launch_fast_var<1>(const Plan&, const DevProgram&, hipStream_t);
+extern template hipError_t launch_fast_pair<0, 2>(const Plan&, const DevProgram&, hipStream_t);
+extern template hipError_t launch_fast_pair<1, 2>(const Plan&, const DevProgram&, hipStream_t);
+extern template hipError_t launch_fast_pair<0, 3>(const Plan&, const DevProgram&, hipStream_t);
+extern template hipError_t launch_fast_pair<1, 3>(const Plan&, const DevProgram&, hipStream_t);
 #endif
 
 }  // namespace plgpu

@@ -67,6 +67,7 @@ const OptField kOptFields[] = {
     {"filt_pipe", "PLGPU_FILT_PIPE", &Options::filt_pipe},
     {"rl_div", "PLGPU_RL_DIV", &Options::rl_div},
     {"part_threads", "PLGPU_PART_THREADS", &Options::part_threads},
+    {"gb_pair", "PLGPU_GB_PAIR", &Options::gb_pair},
 };
 const OptField* opt_field(const char* name) {
     for (const OptField& f : kOptFields)

@@ -188,14 +188,16 @@ def test_fused_derived_sum_only_vwap(gpu):
 
 
 @pytest.mark.parametrize("n", [1025, 100_003, 1_000_001])
-@pytest.mark.parametrize("form", ["one_acc", "vwap", "three_accs", "literal"])
+@pytest.mark.parametrize("form", ["one_acc", "vwap", "vwap_rev", "vwap_swap", "three_accs", "literal"])
 @pytest.mark.parametrize("pred", ["none", "on_a", "on_b", "other"])
 def test_derived_forms_over_two_columns(gpu, n, form, pred):
     """Sum / mean aggregations whose inputs are drawn from two Float64 columns
     a, b -- a op b, b op a, a op literal, a or b itself -- on the sum-only
     fused kernel (path 2) with the predicate on a, on b (the predicate reuses
     an operand's registers) or on a third column, across the masked tail
-    tile; bit-exact against the oracle."""
+    tile; bit-exact against the oracle.  The vwap forms (a product and one of
+    its operands, in either order, the operand first or second in the
+    product) run the product-pair variant (gb_fast_kernel VAR 2 / 3)."""
     rng = np.random.default_rng(n + len(form) * 3 + len(pred))
     k = rng.integers(0, 64, n).astype(np.int64)
     a = rng.uniform(100, 200, n)
@@ -206,6 +208,8 @@ def test_derived_forms_over_two_columns(gpu, n, form, pred):
     forms = {
         "one_acc": [("sum", col("a") - col("b"))],
         "vwap": [("sum", col("a") * col("b")), ("sum", col("b"))],
+        "vwap_rev": [("sum", col("b")), ("sum", col("a") * col("b"))],
+        "vwap_swap": [("mean", col("b") * col("a")), ("sum", col("b"))],
         "three_accs": [("sum", col("b") / col("a")), ("mean", col("a")), ("sum", col("b") + col("a"))],
         "literal": [("sum", col("a") * 2.5), ("mean", col("b") - col("a"))],
     }[form]

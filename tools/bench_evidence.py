@@ -29,19 +29,20 @@ from collections import defaultdict
 HBM_PEAK = 8000.0
 
 # leg -> (kernel-name regex over the trace, algorithmic bytes / launch key, streaming?)
-# The last template argument of gb_fast_kernel is PACK (0: a key column,
+# gb_fast_kernel's last two template arguments: VAR (0 none, 1 the variance
+# triple, 2 / 3 the product pair) and PACK (0: a key column,
 # 1: integer key columns packed in the kernel, 2: String key codes).  The
 # keys leg runs its Categorical case and then its (symbol, day) case on the
 # PACK = 1 variant with equal launch counts: "first" / "second" half of that
 # kernel's launches in trace order.
 LEGS = {
-    "headline": (r"gb_fast_kernel<4, 1, true, 2, 2, false, false, false, false, 0>", "headline", True),
-    "vwap": (r"gb_fast_kernel<2, 1, true, 2, 2, false, false, true, false, 0>", "vwap", True),
-    "std": (r"gb_fast_kernel<3, 1, true, 2, 2, false, false, false, true, 0>", "std", True),
-    "keys_categorical": (r"gb_fast_kernel<4, 1, true, 2, 2, false, false, false, false, 1>", "keys_categorical",
+    "headline": (r"gb_fast_kernel<4, 1, true, 2, 2, false, false, false, 0, 0>", "headline", True),
+    "vwap": (r"gb_fast_kernel<2, 1, true, 2, 2, false, false, false, 2, 0>", "vwap", True),
+    "std": (r"gb_fast_kernel<3, 1, true, 2, 2, false, false, false, 1, 0>", "std", True),
+    "keys_categorical": (r"gb_fast_kernel<4, 1, true, 2, 2, false, false, false, 0, 1>", "keys_categorical",
                          ("first", True)),
-    "keys_string": (r"gb_fast_kernel<4, 1, true, 2, 2, false, false, false, false, 2>", "keys_string", True),
-    "keys_sym_day": (r"gb_fast_kernel<4, 1, true, 2, 2, false, false, false, false, 1>", "keys_sym_day",
+    "keys_string": (r"gb_fast_kernel<4, 1, true, 2, 2, false, false, false, 0, 2>", "keys_string", True),
+    "keys_sym_day": (r"gb_fast_kernel<4, 1, true, 2, 2, false, false, false, 0, 1>", "keys_sym_day",
                      ("second", True)),
     "sort": (r"aos_gather_kernel<8>", "sort", False),
     "sort_pack": (r"aos_pack_kernel<8>", "sort_pack", True),

@@ -14,12 +14,13 @@ import re
 import sys
 
 VARIANTS = {
-    "headline 4 sums (SUMONLY, 2 limbs)": "ILi4ELi1ELb1ELi2ELi2ELb0ELb0ELb0ELb0ELi0EE",
-    "vwap DERIV 2 accs": "ILi2ELi1ELb1ELi2ELi2ELb0ELb0ELb1ELb0ELi0EE",
-    "vwap-like 2 plain sums": "ILi2ELi1ELb1ELi2ELi2ELb0ELb0ELb0ELb0ELi0EE",
-    "std VAR triple": "ILi3ELi1ELb1ELi2ELi2ELb0ELb0ELb0ELb1ELi0EE",
-    "headline PACK (fused integer keys)": "ILi4ELi1ELb1ELi2ELi2ELb0ELb0ELb0ELb0ELi1EE",
-    "headline PACK (String key codes)": "ILi4ELi1ELb1ELi2ELi2ELb0ELb0ELb0ELb0ELi2EE",
+    "headline 4 sums (SUMONLY, 2 limbs)": "ILi4ELi1ELb1ELi2ELi2ELb0ELb0ELb0ELi0ELi0EE",
+    "vwap DERIV 2 accs": "ILi2ELi1ELb1ELi2ELi2ELb0ELb0ELb1ELi0ELi0EE",
+    "vwap product pair (VAR 2)": "ILi2ELi1ELb1ELi2ELi2ELb0ELb0ELb0ELi2ELi0EE",
+    "vwap-like 2 plain sums": "ILi2ELi1ELb1ELi2ELi2ELb0ELb0ELb0ELi0ELi0EE",
+    "std VAR triple": "ILi3ELi1ELb1ELi2ELi2ELb0ELb0ELb0ELi1ELi0EE",
+    "headline PACK (fused integer keys)": "ILi4ELi1ELb1ELi2ELi2ELb0ELb0ELb0ELi0ELi1EE",
+    "headline PACK (String key codes)": "ILi4ELi1ELb1ELi2ELi2ELb0ELb0ELb0ELi0ELi2EE",
 }
 
 
