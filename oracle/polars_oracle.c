@@ -653,6 +653,52 @@ static double fsum_result(fsum_t* s) {
 }
 static void fsum_free(fsum_t* s) { free(s->p); }
 
+/* The correctly rounded sum of finite x[0..n) when the partials above
+ * overflow on the way (1.7e308 + 1.7e308 - 1.7e308: `math.fsum` raises
+ * there): values of magnitude >= 2^-800 are summed scaled by 2^-128 (exact),
+ * the others unscaled, and the two sets of exact partials are added back
+ * together at scale; a partial that overflows there means the sum rounds
+ * to +-inf. */
+static double fsum_overflowing(const double* x, int64_t n) {
+    fsum_t big, small, all;
+    fsum_init(&big);
+    fsum_init(&small);
+    for (int64_t i = 0; i < n; ++i) {
+        if (fabs(x[i]) >= 0x1p-800) fsum_add(&big, ldexp(x[i], -128));
+        else fsum_add(&small, x[i]);
+    }
+    fsum_init(&all);
+    double r = 0.0;
+    int inf = 0;
+    for (int j = 0; j < big.n && !inf; ++j) {
+        const double y = ldexp(big.p[j], 128);
+        if (isinf(y)) { r = y; inf = 1; }
+        else fsum_add(&all, y);
+    }
+    for (int j = 0; j < small.n && !inf; ++j) fsum_add(&all, small.p[j]);
+    if (!inf) {
+        r = fsum_result(&all);
+        /* overflow again: the partials' sum is beyond the largest double */
+        if (isnan(r)) r = big.n ? copysign(INFINITY, big.p[big.n - 1]) : r;
+    }
+    fsum_free(&big);
+    fsum_free(&small);
+    fsum_free(&all);
+    return r;
+}
+
+/* fsum of finite or special x[0..n), exact through intermediate overflow */
+static double fsum_array(const double* x, int64_t n) {
+    fsum_t s;
+    fsum_init(&s);
+    for (int64_t i = 0; i < n; ++i) fsum_add(&s, x[i]);
+    double r = fsum_result(&s);
+    const int special = s.has_special;
+    fsum_free(&s);
+    if (!special && !isfinite(r)) r = fsum_overflowing(x, n);
+    return r;
+}
+
 /* ------------------------------------------------------------ group_by */
 /* Row-order hash grouping (polars-core/src/frame/group_by/hashing.rs
  * group_by_threaded_slice / into_groups.rs): groups in order of first
@@ -804,16 +850,14 @@ static double f64_sum_group(const plgpu_column* c, const int64_t* rows, int64_t 
         *nvalid = nv;
         return sum;
     } else {
-        fsum_t s;
-        fsum_init(&s);
+        double* buf = (double*)malloc(sizeof(double) * (size_t)(len > 0 ? len : 1));
         for (int64_t i = 0; i < len; ++i) {
             val_t v = col_get(c, rows[i]);
             if (!v.valid) continue;
-            ++nv;
-            fsum_add(&s, v.f);
+            buf[nv++] = v.f;
         }
-        double r = fsum_result(&s);
-        fsum_free(&s);
+        double r = fsum_array(buf, nv);
+        free(buf);
         *nvalid = nv;
         return r + 0.0; /* exact zero -> +0.0, as the fold from +0.0 gives */
     }
@@ -940,14 +984,7 @@ OR_EXPORT int64_t or_group_by_agg(const plgpu_column* key, const plgpu_column* c
 
 /* Exact, correctly rounded sum of a plain f64 array (pinned to math.fsum
  * in tests/test_oracle.py). */
-OR_EXPORT double or_fsum(const double* x, int64_t n) {
-    fsum_t s;
-    fsum_init(&s);
-    for (int64_t i = 0; i < n; ++i) fsum_add(&s, x[i]);
-    double r = fsum_result(&s);
-    fsum_free(&s);
-    return r;
-}
+OR_EXPORT double or_fsum(const double* x, int64_t n) { return fsum_array(x, n); }
 
 /* ------------------------------------------------------ CPU baseline */
 /* The bench's cpu_baseline leg: `filter(col(p) > k).group_by(key).agg(

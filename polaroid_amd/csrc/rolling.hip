@@ -50,7 +50,9 @@ struct RlParams {
     int32_t ddof;
     int32_t var_f32;      // std of a Float32 column: sqrt of the variance rounded to f32
     int32_t fast_div;     // option rl_div: full windows' means by rw_div
+    int32_t full;         // option rl_full: interior int64-form waves by rw_scan_full
     double rw;            // RN(1 / w)
+    double wd;            // w as an f64
 };
 
 // RN(a / w) for a full window (count w) without a division: q0 = RN(a y),
@@ -63,7 +65,7 @@ struct RlParams {
 __device__ __forceinline__ double rw_div(double a, uint64_t cnt, const RlParams& p) {
     const uint32_t ex = (uint32_t)(f64_bits(a) >> 52) & 0x7FF;
     if (cnt == (uint64_t)p.w && ex >= 1023 - 900 && ex <= 1023 + 990) {
-        const double y = p.rw, w = (double)p.w;
+        const double y = p.rw, w = p.wd;
         const double q0 = a * y;
         const double r = __builtin_fma(-q0, w, a);
         return __builtin_fma(r, y, q0);
@@ -570,6 +572,66 @@ __device__ __forceinline__ void rw_scan(const RlParams& p, const uint64_t (&x)[k
     }
 }
 
+// rw_scan's common case, an interior wave (every window full, [i - left,
+// i + right)) in the int64 form with no null or non-finite row: the emit's
+// indexing in 32 bits relative to the wave, the ring slot of prefix -1 (read
+// only by the wave's first output) holding zero instead of a per-lane test,
+// the stores through the wave's base address, and the mean by the
+// one-correction quotient with no per-lane range test when the wave's
+// exponents keep every window's quotient normal (DIV1, rw_block).  Round 5:
+// the general scan's emit took about 60 VALU instructions per 64 outputs.
+template <bool MEAN>
+__device__ __forceinline__ void rw_scan_full(const RlParams& p, const uint64_t (&x)[kRwChunks + 1],
+                                             int64_t o_first, int64_t o_end, int64_t s_first, int tmin, bool div1,
+                                             uint64_t* rlo) {
+    const int lane = threadIdx.x & 63;
+    const int bottom = tmin - 1075;
+    const int w = (int)p.w;
+    const int right = p.center ? (w + 1) / 2 : 1;
+    // je of the wave's first output: the row of its window's last value
+    const int e0 = (int)(o_first - s_first) + right - 1;
+    const int nout = (int)(o_end - o_first);
+    const bool ok = p.w >= p.min_periods;  // (w >= 1: a mean's count is never 0)
+    double* out = (double*)p.out + o_first;
+    uint64_t* ov = p.out_valid + (o_first >> 6);
+    const double y = p.rw, wd = p.wd;
+    if (lane == 63) rlo[kRwRing - 1] = 0ull;  // prefix -1 (chunk 3 overwrites it after its one read)
+    uint64_t carry = 0;
+#pragma unroll
+    for (int k = 0; k <= kRwChunks; ++k) {
+        // finite, normal or zero (the int64 form has tmin >= 128): m << (ex - tmin)
+        const uint64_t b = x[k];
+        const uint32_t ex = (uint32_t)(b >> 52) & 0x7FF;
+        const uint64_t m = (b & 0x000FFFFFFFFFFFFFull) | (1ull << 52);
+        const uint64_t t = ex ? m << (ex - (uint32_t)tmin) : 0ull;
+        uint64_t flo = (int64_t)b < 0 ? 0ull - t : t;
+        flo = wave_scan64_fused(flo) + carry;
+        carry = lane63(flo);
+        rlo[((k & 3) << 6) | lane] = flo;
+        wave_sync();
+        if (k == 0) continue;
+        const int q = k - 1;
+        if (64 * q >= nout) break;
+        const int j = 64 * q + lane;
+        const int je = e0 + j;
+        const uint64_t d = rlo[je & (kRwRing - 1)] - rlo[(je - w) & (kRwRing - 1)];
+        double r = __builtin_ldexp((double)(int64_t)d, bottom);
+        if (MEAN) {
+            if (div1) {
+                const double q0 = r * y;
+                r = __builtin_fma(__builtin_fma(-q0, wd, r), y, q0);
+            } else {
+                r = r / wd;
+            }
+        }
+        const bool in = j < nout;
+        if (in) out[j] = ok ? r : 0.0;
+        const uint64_t bits = __ballot(in && ok);
+        if (lane == 0) ov[q] = bits;
+        wave_sync();
+    }
+}
+
 // A wave's outputs summed exactly one by one (values spanning more binades
 // than 128 bits hold).  Out of line, with its own copy of the parameters, so
 // the kernel's parameters never have their address taken.
@@ -933,6 +995,18 @@ __device__ __forceinline__ void rw_block(const RlParams& p, uint64_t (&x)[kRwChu
     if (!narrow && lw + 53 + span > 127) {
         rw_exact_outputs(p, o_first, o_end);  // beyond 128 bits
         return;
+    }
+    if (narrow && !counts && p.full) {
+        const int64_t right = p.center ? (p.w + 1) / 2 : 1;
+        if (o_first - (p.w - right) >= 0 && o_end + right - 1 <= p.n) {
+            // the one-correction mean without its per-lane test: nonzero
+            // window sums lie in [2^(tmin - 1075), 2^(tmax - 1022 + lw)),
+            // inside rw_div's exponent range
+            const bool div1 = p.fast_div && tmin - 1075 >= -900 && tmax - 1022 + lw <= 990;
+            if (p.mean) rw_scan_full<true>(p, x, o_first, o_end, s_first, tmin, div1, rlo);
+            else rw_scan_full<false>(p, x, o_first, o_end, s_first, tmin, div1, rlo);
+            return;
+        }
     }
 #define PLGPU_RW(M, C)                                                                                   \
     (p.mean ? rw_scan<M, C, true>(p, x, vm, o_first, o_end, s_first, tmin, rlo, rhi, rcn)               \
@@ -1327,6 +1401,8 @@ PLGPU_API int plgpu_rolling(const plgpu_column* values, int32_t kind, int64_t wi
     p.mean = kind == PLGPU_ROLLING_MEAN;
     p.rw = 1.0 / (double)std::max<int64_t>(window_size, 1);
     p.fast_div = options().rl_div;
+    p.full = options().rl_full;
+    p.wd = (double)window_size;
     p.var = var ? (kind == PLGPU_ROLLING_STD ? 2 : 1) : 0;
     p.ddof = ddof;
     p.var_f32 = var_f32;

@@ -68,6 +68,7 @@ const OptField kOptFields[] = {
     {"rl_div", "PLGPU_RL_DIV", &Options::rl_div},
     {"part_threads", "PLGPU_PART_THREADS", &Options::part_threads},
     {"gb_pair", "PLGPU_GB_PAIR", &Options::gb_pair},
+    {"rl_full", "PLGPU_RL_FULL", &Options::rl_full},
 };
 const OptField* opt_field(const char* name) {
     for (const OptField& f : kOptFields)

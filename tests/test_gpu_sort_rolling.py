@@ -258,6 +258,28 @@ def test_rolling_wave_kernel_modes(gpu, span, w):
             _rolling_check(v, valid, kind, w, ms, center, ref_bound=False)
 
 
+@pytest.mark.parametrize("data", ["narrow", "zeros", "low", "high", "overflow"])
+@pytest.mark.parametrize("full", [1, 0])
+def test_rolling_full_waves_specialised_scan(gpu, plgpu_option, data, full):
+    """Interior int64-form waves take rw_scan_full (option rl_full): its
+    window indexing, the zeroed prefix -1 and the one-correction mean with
+    no per-lane range test when the wave's exponents allow it ("low" /
+    "high": just outside that range, divided; "overflow": sums that round
+    to inf).  Bit-exact against the oracle with the option on and off."""
+    plgpu_option("rl_full", full)
+    rng = np.random.default_rng(len(data) * 5 + full)
+    n = 4096 * 2 + 777
+    v = {"narrow": lambda: rng.uniform(100, 150, n),
+         "zeros": lambda: np.where(rng.random(n) < 0.5, 0.0, -0.0),
+         "low": lambda: rng.uniform(1, 2, n) * 2.0 ** -851,
+         "high": lambda: rng.uniform(1, 2, n) * 2.0 ** 990,
+         "overflow": lambda: rng.uniform(0.5, 1, n) * 1.7e308}[data]()
+    for w in (1, 2, 20, 64):
+        for center in (False, True):
+            for kind in ("sum", "mean"):
+                _rolling_check(v, None, kind, w, w, center, ref_bound=False)
+
+
 def test_rolling_wide_exponent_span_is_exact(gpu):
     """A tile whose values span far more than one fixed-point window takes
     the exact per-output path (1e300 next to 1e-300 and cancellations)."""

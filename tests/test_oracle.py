@@ -587,3 +587,31 @@ def test_one_correction_division_by_window_length():
             r = Fr(a) - Fr(w) * Fr(q0)
             assert Fr(float(r)) == r  # the fma's remainder is exact
             assert float(Fr(q0) + r * Fr(y)) == float(Fr(a) / w), (a, w)
+
+
+def test_fsum_exact_through_intermediate_overflow():
+    """The oracle's exact sum stays correctly rounded when its partials
+    overflow on the way (where math.fsum raises): the exact rational sum,
+    rounded once, or +-inf beyond the largest double."""
+    from fractions import Fraction
+
+    def exact(xs):
+        f = sum((Fraction(v) for v in xs), Fraction(0))
+        try:
+            return float(f)
+        except OverflowError:
+            return math.inf if f > 0 else -math.inf
+
+    big = 1.7e308
+    cases = [[big, big, -big], [big, big], [-big, -big], [1e308, 1e308, -1e308, -1e308, 1e-300],
+             [big, big, -big, -big, 2.0 ** -1074], [big] * 3 + [-big] * 2 + [1.0]]
+    rng = np.random.default_rng(5)
+    for _ in range(200):
+        n = int(rng.integers(2, 12))
+        xs = rng.uniform(-1, 1, n) * 1.79e308
+        xs[rng.random(n) < 0.3] *= 2.0 ** -int(rng.integers(0, 1100))
+        cases.append(list(xs))
+    for xs in cases:
+        got = O.fsum(np.array(xs, dtype=np.float64))
+        want = exact(xs)
+        assert got == want and math.copysign(1, got) == math.copysign(1, want) or (got == 0 and want == 0), (xs, got, want)
