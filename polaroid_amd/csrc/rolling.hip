@@ -573,29 +573,39 @@ __device__ __forceinline__ void rw_scan(const RlParams& p, const uint64_t (&x)[k
 }
 
 // rw_scan's common case, an interior wave (every window full, [i - left,
-// i + right)) in the int64 form with no null or non-finite row: the emit's
-// indexing in 32 bits relative to the wave, the ring slot of prefix -1 (read
-// only by the wave's first output) holding zero instead of a per-lane test,
-// the stores through the wave's base address, and the mean by the
-// one-correction quotient with no per-lane range test when the wave's
-// exponents keep every window's quotient normal (DIV1, rw_block).  Round 5:
-// the general scan's emit took about 60 VALU instructions per 64 outputs.
+// i + right)) in the int64 form with no null or non-finite row.  Its
+// prefixes are not kept in a ring: all kRwChunks + 1 chunks' prefixes fit
+// the wave's three rings as one array (rw_block's rlo, 3 * kRwRing words),
+// prefix r at word r + 1 and word 0 = 0 for prefix -1, so each output's two
+// reads are a per-lane base plus a per-chunk immediate offset, as are the
+// stores; the mean is the one-correction quotient with no per-lane range
+// test when the wave's exponents keep every window's quotient normal (DIV1,
+// rw_block).  Round 5: the general scan's emit took about 60 VALU
+// instructions per 64 outputs (64-bit bounds, clipping and count tests,
+// ring wrap, store addresses, `1 / w` read back from a spilled SGPR lane).
+static_assert(kRwChunks * 64 + 64 + 1 <= 3 * kRwRing, "rw_scan_full: the prefixes in the wave's rings");
 template <bool MEAN>
 __device__ __forceinline__ void rw_scan_full(const RlParams& p, const uint64_t (&x)[kRwChunks + 1],
                                              int64_t o_first, int64_t o_end, int64_t s_first, int tmin, bool div1,
-                                             uint64_t* rlo) {
+                                             uint64_t* pre) {
     const int lane = threadIdx.x & 63;
     const int bottom = tmin - 1075;
     const int w = (int)p.w;
     const int right = p.center ? (w + 1) / 2 : 1;
-    // je of the wave's first output: the row of its window's last value
+    // the output's window ends at row e0 + j of the wave's rows (j = its index)
     const int e0 = (int)(o_first - s_first) + right - 1;
     const int nout = (int)(o_end - o_first);
     const bool ok = p.w >= p.min_periods;  // (w >= 1: a mean's count is never 0)
-    double* out = (double*)p.out + o_first;
+    double* ol = (double*)p.out + o_first + lane;
     uint64_t* ov = p.out_valid + (o_first >> 6);
-    const double y = p.rw, wd = p.wd;
-    if (lane == 63) rlo[kRwRing - 1] = 0ull;  // prefix -1 (chunk 3 overwrites it after its one read)
+    const uint64_t* pe = pre + 1 + e0 + lane;
+    const uint64_t* ps = pe - w;
+    uint64_t* pw = pre + 1 + lane;
+    // 1 / w and w in VGPRs (as uniform values they spill to VGPR lanes and
+    // are read back every chunk)
+    double y = p.rw, wd = p.wd;
+    asm volatile("" : "+v"(y), "+v"(wd));
+    if (lane == 0) pre[0] = 0ull;  // prefix -1
     uint64_t carry = 0;
 #pragma unroll
     for (int k = 0; k <= kRwChunks; ++k) {
@@ -607,14 +617,12 @@ __device__ __forceinline__ void rw_scan_full(const RlParams& p, const uint64_t (
         uint64_t flo = (int64_t)b < 0 ? 0ull - t : t;
         flo = wave_scan64_fused(flo) + carry;
         carry = lane63(flo);
-        rlo[((k & 3) << 6) | lane] = flo;
+        pw[64 * k] = flo;
         wave_sync();
         if (k == 0) continue;
         const int q = k - 1;
         if (64 * q >= nout) break;
-        const int j = 64 * q + lane;
-        const int je = e0 + j;
-        const uint64_t d = rlo[je & (kRwRing - 1)] - rlo[(je - w) & (kRwRing - 1)];
+        const uint64_t d = pe[64 * q] - ps[64 * q];
         double r = __builtin_ldexp((double)(int64_t)d, bottom);
         if (MEAN) {
             if (div1) {
@@ -624,11 +632,10 @@ __device__ __forceinline__ void rw_scan_full(const RlParams& p, const uint64_t (
                 r = r / wd;
             }
         }
-        const bool in = j < nout;
-        if (in) out[j] = ok ? r : 0.0;
+        const bool in = 64 * q + lane < nout;
+        if (in) ol[64 * q] = ok ? r : 0.0;
         const uint64_t bits = __ballot(in && ok);
         if (lane == 0) ov[q] = bits;
-        wave_sync();
     }
 }
 
@@ -1026,9 +1033,8 @@ __device__ __forceinline__ void rw_block(const RlParams& p, uint64_t (&x)[kRwChu
 // waves: not kept.)
 template <int DT, bool NULLABLE, bool VAR = false>
 __global__ __launch_bounds__(256) void rl_wave_kernel(RlParams p) {
-    __shared__ uint64_t ring_lo[kRwWaves][kRwRing];
-    __shared__ uint64_t ring_hi[kRwWaves][kRwRing];
-    __shared__ uint64_t ring_cn[kRwWaves][kRwRing];
+    // each wave's three rings, adjacent (rw_scan_full uses them as one array)
+    __shared__ uint64_t ring[kRwWaves][3 * kRwRing];
     __shared__ uint64_t ring_v2[VAR ? kRwWaves : 1][VAR ? kRwRing : 1];  // var: the t^2 prefixes' high words
     const int wv = threadIdx.x >> 6;
     const int64_t o_first = ((int64_t)blockIdx.x * kRwWaves + wv) * kRwOut;
@@ -1037,7 +1043,7 @@ __global__ __launch_bounds__(256) void rl_wave_kernel(RlParams p) {
     rl_bounds(p, o_first, s_first, tmp);
     uint64_t x[kRwChunks + 1];
     rw_load_block<DT>(p, s_first, x);
-    rw_block<DT, NULLABLE, VAR>(p, x, o_first, s_first, ring_lo[wv], ring_hi[wv], ring_cn[wv],
+    rw_block<DT, NULLABLE, VAR>(p, x, o_first, s_first, ring[wv], ring[wv] + kRwRing, ring[wv] + 2 * kRwRing,
                                 VAR ? ring_v2[wv] : nullptr);
 }
 
@@ -1046,9 +1052,8 @@ __global__ __launch_bounds__(256) void rl_wave_kernel(RlParams p) {
 // loads in flight while it computes (the one-block form waits for them).
 template <int DT, bool VAR = false>
 __global__ __launch_bounds__(256) void rl_stream_kernel(RlParams p) {
-    __shared__ uint64_t ring_lo[kRwWaves][kRwRing];
-    __shared__ uint64_t ring_hi[kRwWaves][kRwRing];
-    __shared__ uint64_t ring_cn[kRwWaves][kRwRing];
+    // each wave's three rings, adjacent (rw_scan_full uses them as one array)
+    __shared__ uint64_t ring[kRwWaves][3 * kRwRing];
     __shared__ uint64_t ring_v2[VAR ? kRwWaves : 1][VAR ? kRwRing : 1];
     const int wv = threadIdx.x >> 6;
     const int64_t nblocks = (p.n + kRwOut - 1) / kRwOut;
@@ -1067,7 +1072,7 @@ __global__ __launch_bounds__(256) void rl_stream_kernel(RlParams p) {
             rl_bounds(p, bn * kRwOut, sn, tmp);
             rw_load_block<DT>(p, sn, xn);
         }
-        rw_block<DT, false, VAR>(p, x, b * kRwOut, s_first, ring_lo[wv], ring_hi[wv], ring_cn[wv],
+        rw_block<DT, false, VAR>(p, x, b * kRwOut, s_first, ring[wv], ring[wv] + kRwRing, ring[wv] + 2 * kRwRing,
                                  VAR ? ring_v2[wv] : nullptr);
 #pragma unroll
         for (int k = 0; k <= kRwChunks; ++k) x[k] = xn[k];
