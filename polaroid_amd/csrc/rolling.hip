@@ -53,6 +53,8 @@ struct RlParams {
     int32_t full;         // option rl_full: interior int64-form waves by rw_scan_full
     double rw;            // RN(1 / w)
     double wd;            // w as an f64
+    double rw2;           // var / std: RN(1 / (w - ddof)) (w > ddof)
+    double wd2;           // var / std: w - ddof as an f64
 };
 
 // RN(a / w) for a full window (count w) without a division: q0 = RN(a y),
@@ -919,6 +921,93 @@ __device__ __forceinline__ void rw_var_scan(const RlParams& p, const uint64_t (&
     }
 }
 
+// rw_var_scan's common case, as rw_scan_full for the sum: an interior wave
+// (every window full, count w) with no null or non-finite row.  Its three
+// prefix rings sit at fixed distances in the wave's ring array (t, t^2 low
+// and high words at words 0, kRwRing, 2 kRwRing), indexed in 32 bits
+// relative to the wave, ring slot kRwRing - 1 zeroed for prefix -1 (read
+// only by the wave's first output; chunk 3 overwrites it afterwards).  The
+// two quotients num / w / (w - ddof) take the one-correction form when the
+// wave's exponents keep them normal (DIV1, rw_block).
+template <bool DIV1>
+__device__ __forceinline__ void rw_var_scan_full(const RlParams& p, const uint64_t (&x)[kRwChunks + 1],
+                                                 int64_t o_first, int64_t o_end, int64_t s_first, int tmin,
+                                                 uint64_t* ring) {
+    const int lane = threadIdx.x & 63;
+    const int bottom = tmin - 1075;
+    const int w = (int)p.w;
+    const int right = p.center ? (w + 1) / 2 : 1;
+    const int e0 = (int)(o_first - s_first) + right - 1;
+    const int nout = (int)(o_end - o_first);
+    const bool ok = p.w >= p.min_periods && p.w > p.ddof;
+    double* ol = (double*)p.out + o_first + lane;
+    uint64_t* ov = p.out_valid + (o_first >> 6);
+    double y = p.rw, wd = p.wd, y2 = p.rw2, wd2 = p.wd2;
+    asm volatile("" : "+v"(y), "+v"(wd), "+v"(y2), "+v"(wd2));
+    const uint32_t cw = (uint32_t)w;
+    if (lane == 63) ring[kRwRing - 1] = ring[2 * kRwRing - 1] = ring[3 * kRwRing - 1] = 0ull;
+    uint64_t c1 = 0, c2l = 0, c2h = 0;
+#pragma unroll
+    for (int k = 0; k <= kRwChunks; ++k) {
+        // finite, normal or zero (the fast form has tmin >= 600)
+        const uint64_t b = x[k];
+        const uint32_t ex = (uint32_t)(b >> 52) & 0x7FF;
+        const uint64_t m = (b & 0x000FFFFFFFFFFFFFull) | (1ull << 52);
+        const uint64_t t = ex ? m << (ex - (uint32_t)tmin) : 0ull;  // |t| < 2^63
+        const unsigned __int128 u = (unsigned __int128)t * t;
+        uint64_t f1 = (int64_t)b < 0 ? 0ull - t : t;
+        uint64_t f2l = (uint64_t)u, f2h = (uint64_t)(u >> 64);
+        f1 = wave_scan64_fused(f1) + c1;
+        c1 = lane63(f1);
+        wave_scan128_fused(f2l, f2h);
+        add128(f2l, f2h, c2l, c2h);
+        c2l = lane63(f2l);
+        c2h = lane63(f2h);
+        const int slot = ((k & 3) << 6) | lane;
+        ring[slot] = f1;
+        ring[kRwRing + slot] = f2l;
+        ring[2 * kRwRing + slot] = f2h;
+        wave_sync();
+        if (k == 0) continue;
+        const int q = k - 1;
+        if (64 * q >= nout) break;
+        const int je = e0 + 64 * q + lane;
+        const int ie = je & (kRwRing - 1), is = (je - w) & (kRwRing - 1);
+        const int64_t S1 = (int64_t)(ring[ie] - ring[is]);
+        uint64_t s2l = ring[kRwRing + ie], s2h = ring[2 * kRwRing + ie];
+        add128(s2l, s2h, ~ring[kRwRing + is], ~ring[2 * kRwRing + is]);
+        add128(s2l, s2h, 1, 0);
+        // num = w * S2 - S1^2, exact in 192 bits
+        const unsigned __int128 lo = (unsigned __int128)s2l * cw;
+        const unsigned __int128 hi = (unsigned __int128)s2h * cw + (uint64_t)(lo >> 64);
+        uint64_t w0 = (uint64_t)lo, w1 = (uint64_t)hi, w2 = (uint64_t)(hi >> 64);
+        const uint64_t a1 = (uint64_t)(S1 < 0 ? -S1 : S1);
+        const unsigned __int128 q2 = (unsigned __int128)a1 * a1;
+        const uint64_t q0 = (uint64_t)q2, q1 = (uint64_t)(q2 >> 64);
+        const uint64_t b0 = w0 < q0 ? 1ull : 0ull;
+        w0 -= q0;
+        const unsigned __int128 d1 = (unsigned __int128)w1 - q1 - b0;
+        w1 = (uint64_t)d1;
+        w2 -= (uint64_t)(d1 >> 64) ? 1ull : 0ull;
+        const double nr = (int64_t)w2 < 0 ? 0.0 : u192_to_double(w0, w1, w2, 2 * bottom);
+        double v;
+        if (DIV1) {
+            const double a0 = nr * y;
+            const double v1 = __builtin_fma(__builtin_fma(-a0, wd, nr), y, a0);
+            const double a2 = v1 * y2;
+            v = __builtin_fma(__builtin_fma(-a2, wd2, v1), y2, a2);
+        } else {
+            v = (nr / wd) / wd2;
+        }
+        if (p.var == 2) v = rv_std(p, v);
+        const bool in = 64 * q + lane < nout;
+        if (in) ol[64 * q] = ok ? v : 0.0;
+        const uint64_t bits = __ballot(in && ok);
+        if (lane == 0) ov[q] = bits;
+        wave_sync();
+    }
+}
+
 // The rows [s_first, s_first + 64 (kRwChunks + 1)) of one wave's block as
 // loaded (the row index clamped to the column, so the loads are
 // branch-free and all in flight together; rows past n are masked by
@@ -991,6 +1080,17 @@ __device__ __forceinline__ void rw_block(const RlParams& p, uint64_t (&x)[kRwChu
         const bool vfast = mx == 0 || (tmin >= 600 && lw + 53 + span <= 63 && 2 * (53 + span) + lw <= 126);
         if (!vfast) {
             rw_var_exact_outputs(p, o_first, o_end);
+            return;
+        }
+        const int64_t right = p.center ? (p.w + 1) / 2 : 1;
+        if (!counts && p.full && o_first - (p.w - right) >= 0 && o_end + right - 1 <= p.n) {
+            // nonzero numerators lie in [2^(2 bottom), 2^(2 (tmax - 1022) + 2 lw)):
+            // both quotients inside rw_div's exponent range
+            const int b2 = 2 * (tmin - 1075), top = 2 * (tmax - 1022) + 2 * lw;
+            if (p.fast_div && b2 - 2 * lw >= -900 && top <= 990)
+                rw_var_scan_full<true>(p, x, o_first, o_end, s_first, tmin, rlo);
+            else
+                rw_var_scan_full<false>(p, x, o_first, o_end, s_first, tmin, rlo);
             return;
         }
         if (counts) rw_var_scan<true>(p, x, vm, o_first, o_end, s_first, tmin, rlo, rhi, rv2, rcn);
@@ -1408,6 +1508,8 @@ PLGPU_API int plgpu_rolling(const plgpu_column* values, int32_t kind, int64_t wi
     p.fast_div = options().rl_div;
     p.full = options().rl_full;
     p.wd = (double)window_size;
+    p.wd2 = (double)std::max<int64_t>(window_size - ddof, 1);
+    p.rw2 = 1.0 / p.wd2;
     p.var = var ? (kind == PLGPU_ROLLING_STD ? 2 : 1) : 0;
     p.ddof = ddof;
     p.var_f32 = var_f32;

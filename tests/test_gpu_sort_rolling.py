@@ -409,6 +409,27 @@ def test_rolling_var_wave_forms(gpu, span, w):
             _var_check(v, valid, w, ms, center, ddof, std)
 
 
+@pytest.mark.parametrize("data", ["narrow", "constant", "low", "high"])
+@pytest.mark.parametrize("full", [1, 0])
+def test_rolling_var_full_waves_specialised_scan(gpu, plgpu_option, data, full):
+    """Interior fast-form waves take rw_var_scan_full (option rl_full): its
+    32-bit ring indexing, the zeroed prefix -1 slots and the one-correction
+    quotients num / w / (w - ddof) ("low" / "high": exponents just outside
+    their range, divided; "constant": zero numerators).  Bit-exact against
+    the oracle with the option on and off; ddof up to w (all null)."""
+    plgpu_option("rl_full", full)
+    rng = np.random.default_rng(len(data) * 7 + full)
+    n = 4096 * 2 + 777
+    v = {"narrow": lambda: rng.uniform(100, 150, n),
+         "constant": lambda: np.full(n, 3.25),
+         "low": lambda: rng.uniform(1, 2, n) * 2.0 ** -420,
+         "high": lambda: rng.uniform(1, 2, n) * 2.0 ** 494}[data]()
+    for w in (2, 20, 64):
+        for center in (False, True):
+            for ddof in (0, 1, w):
+                _var_check(v, None, w, w, center, ddof, std=(ddof == 1))
+
+
 def test_rolling_var_specials_nulls_and_dtypes(gpu):
     """NaN / inf in the window give NaN (MomentWindow's non-finite count),
     nulls are skipped, Int32 / Int64 enter as Float64 and Float32 stays
