@@ -256,6 +256,20 @@ int plgpu_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream);
  *   "part_bits"   partitioned group-by: at least this many partition bits
  *   "part_levels" partitioned group-by: 1 / 2 scatter passes (-1: by the
  *                 partition bits, two above 8)
+ * A / B switches of measured kernel variants (results never depend on them):
+ *   "part_direct"  1: one-workgroup partitions flush into their own region
+ *   "part_lds_kb"  partitioned aggregation's LDS table budget (0: 160 KiB)
+ *   "part_threads" partitioned aggregation's threads per workgroup (0: by
+ *                  the rows per workgroup)
+ *   "rl_stream"    1: rolling windows <= 64 by resident streaming waves
+ *   "rl_grid"      the streaming rolling kernel's workgroups per CU
+ *   "rl_div"       1: full windows' means by the one-correction quotient
+ *   "rl_full"      1: interior null-free rolling waves by the specialised
+ *                  scans (sum / mean / var / std)
+ *   "filt_pipe"    1: the filter scatter issues the next column's loads
+ *                  before this column's stores
+ *   "gb_pair"      1: (x * y).sum() next to y.sum() by the fused kernel's
+ *                  product-pair variant
  * An unknown name is PLGPU_ERR_INVALID. */
 int plgpu_set_option(const char* name, int64_t value);
 int plgpu_get_option(const char* name, int64_t* out);
