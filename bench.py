@@ -319,7 +319,8 @@ def filter_leg(torch, pl, df, steps: int, warmup: int, cpu_rows: int, cpu_second
     """Row a1: `filter(close > 250).collect()` over the headline frame's 5
     columns (no aggregation): the mask + tile-count pass, the tile scan and
     the one multi-column scatter (polars-compute/src/filter/mod.rs:18 filter,
-    each column by the one mask).  Algorithmic bytes: the 5 columns read
+    each column by the one mask; option filt_fused: the one-pass look-back
+    kernel instead, measured slower).  Algorithmic bytes: the 5 columns read
     once (40 B/row) and the selected rows written once (40 B each).  rank 0,
     N = 1."""
     n = df.height
@@ -329,10 +330,16 @@ def filter_leg(torch, pl, df, steps: int, warmup: int, cpu_rows: int, cpu_second
 
     ms, kernels, sel = _time_steps(torch, step, steps, warmup)
     algo = n * 40 + sel * 40
-    scatter = _leg_roofline(kernels, "filter_scatter8_kernel", n * 40 + n / 8 + sel * 40,
-                            "5 x 8 B read per row + the mask bit, 5 x 8 B written per selected row")
-    mask = _leg_roofline(kernels, "filter_mask_kernel", n * 8 + n / 8,
-                         "8 B predicate read per row + 1 mask bit written")
+    if "filter_fused8_kernel" in kernels:
+        # the one-pass look-back kernel: the algorithmic bytes are the leg's
+        scatter = _leg_roofline(kernels, "filter_fused8_kernel", algo,
+                                "5 x 8 B read per row (the predicate column once), 5 x 8 B written per selected row")
+        mask = None
+    else:
+        scatter = _leg_roofline(kernels, "filter_scatter8_kernel", n * 40 + n / 8 + sel * 40,
+                                "5 x 8 B read per row + the mask bit, 5 x 8 B written per selected row")
+        mask = _leg_roofline(kernels, "filter_mask_kernel", n * 8 + n / 8,
+                             "8 B predicate read per row + 1 mask bit written")
     r = {"query": "filter(close > 250).collect() over symbol, open, high, low, close", "rows": n,
          "rows_selected": sel, "ms_per_step": round(ms, 3), "Mrows_s": round(n / ms / 1e3, 1),
          "algorithmic_GB": round(algo / 1e9, 2), "step_frac": round(algo / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),

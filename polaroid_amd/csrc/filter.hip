@@ -306,6 +306,147 @@ __global__ __launch_bounds__(kFilterThreads) void filter_scatter8_kernel(Scatter
     }
 }
 
+// One pass for the common filter (a simple predicate over a null-free
+// 8-byte column, every output column null-free and 8 bytes wide): each
+// workgroup takes the next tile by ticket (tiles start in order), forms its
+// mask words from the predicate column's registers, publishes its count,
+// looks back over its predecessors' published counts for its output offset
+// (decoupled look-back: a tile's word holds its count, flag kFtAgg, or its
+// inclusive prefix, flag kFtIncl), publishes its inclusive prefix and
+// scatters its selected rows as filter_scatter8_kernel does.  The predicate
+// column is read once (its registers serve the scatter when it is an output
+// column), and no mask words, tile scan or host round trip sit between the
+// passes.  Every tile waits only on tiles with earlier tickets, which are
+// already running, and tile 0 publishes its prefix without waiting, so every
+// wave reaches its exit.
+constexpr uint64_t kFtAgg = 1ull << 62, kFtIncl = 2ull << 62, kFtValue = (1ull << 62) - 1;
+
+__device__ __forceinline__ uint64_t ft_load(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void ft_store(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <bool PIPE>
+__global__ __launch_bounds__(kFilterThreads) void filter_fused8_kernel(Scatter8Args a, const uint64_t* __restrict__ pcol,
+                                                                       int32_t pj, DevProgram prog, int64_t n,
+                                                                       uint64_t* __restrict__ status,
+                                                                       uint32_t* __restrict__ ticket) {
+    constexpr int IT = kTileRows / kFilterThreads;
+    constexpr int NW = kFilterThreads / 64;
+    __shared__ uint64_t words[kTileWords];
+    __shared__ uint32_t prefix[kTileWords];
+    __shared__ uint32_t wave_cnt[NW];
+    __shared__ int64_t tile_sh;
+    __shared__ uint64_t base_sh;
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const uint64_t lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    if (threadIdx.x == 0) tile_sh = (int64_t)atomicAdd(ticket, 1u);
+    __syncthreads();
+    const int64_t t = tile_sh;
+    // the columns in scatter order: the predicate column first (its rows are
+    // already in registers), then the others
+    auto col_at = [&](int k) { return k == 0 ? pj : (k - 1 < pj ? k - 1 : k); };
+    auto load_col = [&](int j, uint64_t (&v)[IT]) {
+        const uint64_t* __restrict__ src = a.src[j];
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int64_t r = t * kTileRows + it * kFilterThreads + threadIdx.x;
+            v[it] = __builtin_nontemporal_load(src + (r < n ? r : n - 1));
+        }
+    };
+    // the predicate column's rows of the tile (clamped at the end; rows
+    // >= n are never selected)
+    uint64_t v[IT], w[IT];
+    bool sel[IT];
+    {
+        const uint64_t* __restrict__ src = pcol;
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int64_t r = t * kTileRows + it * kFilterThreads + threadIdx.x;
+            v[it] = __builtin_nontemporal_load(src + (r < n ? r : n - 1));
+        }
+    }
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int64_t r = t * kTileRows + it * kFilterThreads + threadIdx.x;
+        sel[it] = r < n && simple_pred(prog.simple_isf, prog.simple_op, v[it], prog.simple_imm);
+        const uint64_t bw = __ballot(sel[it]);
+        if (lane == 0) words[it * NW + wave] = bw;
+        cnt += (uint32_t)__popcll(bw);
+    }
+    if (lane == 0) wave_cnt[wave] = cnt;
+    __syncthreads();
+    // the next column's loads go out before the look-back (they do not
+    // depend on the tile's output offset)
+    if (PIPE && a.ncols > 1) load_col(col_at(1), w);
+    if (wave == 0) {
+        uint64_t total = 0;
+#pragma unroll
+        for (int q = 0; q < NW; ++q) total += wave_cnt[q];
+        // publish the count (tile 0: its inclusive prefix), then look back
+        if (lane == 0) ft_store(&status[t], (t == 0 ? kFtIncl : kFtAgg) | total);
+        uint64_t excl = 0;
+        int64_t j0 = t - 1;
+        while (j0 >= 0) {
+            const int64_t j = j0 - lane;
+            const uint64_t st = j >= 0 ? ft_load(&status[j]) : kFtIncl;
+            const uint64_t flag = st & ~kFtValue;
+            const uint64_t incl = __ballot(flag == kFtIncl);
+            const uint64_t ready = __ballot(flag != 0);
+            const int first = incl ? __builtin_ctzll(incl) : 64;  // nearest inclusive predecessor
+            const uint64_t need = first >= 63 ? ~0ull : ((2ull << first) - 1);
+            if ((ready & need) != need) {
+                __builtin_amdgcn_s_sleep(1);
+                continue;  // a predecessor in the window has not published yet
+            }
+            uint64_t x = lane <= first ? (st & kFtValue) : 0ull;
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) x += __shfl_xor(x, off, 64);
+            excl += x;
+            if (first < 64) break;
+            j0 -= 64;
+        }
+        if (lane == 0) {
+            if (t > 0) ft_store(&status[t], kFtIncl | (excl + total));
+            base_sh = excl;
+        }
+        // the tile's 64 mask words' exclusive prefix
+        const uint64_t mw = words[lane];
+        uint32_t px = (uint32_t)__popcll(mw), c = px;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(px, off, 64);
+            if (lane >= off) px += y;
+        }
+        prefix[lane] = px - c;
+    }
+    __syncthreads();
+    uint64_t* const* dsts = a.dst;
+    const uint64_t base_off = base_sh;
+    uint32_t lp[IT];  // output position within the tile's selected rows
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int wi = it * NW + wave;
+        lp[it] = prefix[wi] + (uint32_t)__popcll(words[wi] & lt_mask);
+    }
+    for (int k = 0; k < a.ncols; ++k) {
+        if (!PIPE && k > 0) load_col(col_at(k), v);
+        uint64_t* __restrict__ dst = dsts[col_at(k)] + base_off;
+#pragma unroll
+        for (int it = 0; it < IT; ++it)
+            if (sel[it]) dst[lp[it]] = v[it];
+        if (PIPE && k + 1 < a.ncols) {
+#pragma unroll
+            for (int it = 0; it < IT; ++it) v[it] = w[it];
+            if (k + 2 < a.ncols) load_col(col_at(k + 2), w);
+        }
+    }
+}
+
 static ColArgs pack_cols(const plgpu_column* cols, int32_t ncols) {
     ColArgs a;
     std::memset(&a, 0, sizeof a);
@@ -358,6 +499,60 @@ static int run_filter(const plgpu_column* cols, int32_t ncols, int src, const De
     DevProgram dp;
     if (prog) dp = *prog;
     else std::memset(&dp, 0, sizeof dp);
+
+    // the one-pass form (filter_fused8_kernel): a simple predicate over a
+    // null-free 8-byte column, every column null-free and 8 bytes wide, and
+    // output columns allocated at the input's length (their length set to
+    // the selected count afterwards) within a quarter of the free memory
+    bool all8 = ncols > 0 && src != 0 && dp.simple && options().filt_fused != 0 && n > 0;
+    for (int i = 0; i < ncols && all8; ++i)
+        all8 = cols[i].dtype != PLGPU_STR && cols[i].dtype != PLGPU_BOOL && cols[i].validity == nullptr &&
+               dtype_bytes(cols[i].dtype) == 8;
+    if (all8) {
+        size_t fr = 0, tot = 0;
+        all8 = hipMemGetInfo(&fr, &tot) == hipSuccess && (uint64_t)ncols * (uint64_t)n * 8 <= fr / 4;
+    }
+    if (all8) {
+        uint64_t* status = nullptr;  // ntiles words + the ticket
+        if ((rc = dev_alloc((void**)&status, (ntiles + 1) * 8, s))) return rc;
+        Scatter8Args sa;
+        std::memset(&sa, 0, sizeof sa);
+        for (int i = 0; i < ncols && !rc; ++i) {
+            rc = make_owned_column(&out_cols[i], cols[i].dtype, n, false, s);
+            sa.src[i] = (const uint64_t*)cols[i].values + cols[i].offset;
+            sa.dst[i] = rc ? nullptr : (uint64_t*)out_cols[i].values;
+        }
+        sa.ncols = ncols;
+        uint64_t last = 0;
+        if (!rc) {
+            hipError_t e = hipMemsetAsync(status, 0, (ntiles + 1) * 8, s);
+            const plgpu_column& pc = cols[dp.simple_col];
+            const uint64_t* pcol = (const uint64_t*)pc.values + pc.offset;
+            if (e == hipSuccess) {
+                KtScope kt("filter_fused8_kernel", s);
+                if (options().filt_pipe != 0)
+                    filter_fused8_kernel<true><<<(unsigned)ntiles, kFilterThreads, 0, s>>>(
+                        sa, pcol, dp.simple_col, dp, n, status, (uint32_t*)(status + ntiles));
+                else
+                    filter_fused8_kernel<false><<<(unsigned)ntiles, kFilterThreads, 0, s>>>(
+                        sa, pcol, dp.simple_col, dp, n, status, (uint32_t*)(status + ntiles));
+                e = hipGetLastError();
+            }
+            if (e == hipSuccess) e = hipMemcpyAsync(&last, status + ntiles - 1, 8, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e != hipSuccess) rc = hip_fail(e, "filter_fused8_kernel");
+            if (!rc && (last & ~kFtValue) != kFtIncl) rc = fail(PLGPU_ERR_CAPACITY, "internal: filter prefix not published");
+        }
+        dev_free(status, s);
+        if (rc) {
+            for (int i = 0; i < ncols; ++i) plgpu_column_release(&out_cols[i]);
+            return rc;
+        }
+        const int64_t total = (int64_t)(last & kFtValue);
+        for (int i = 0; i < ncols; ++i) out_cols[i].length = total;
+        *out_len = total;
+        return PLGPU_OK;
+    }
 
     uint64_t* mask_words = nullptr;
     uint32_t* counts = nullptr;

@@ -69,6 +69,7 @@ const OptField kOptFields[] = {
     {"part_threads", "PLGPU_PART_THREADS", &Options::part_threads},
     {"gb_pair", "PLGPU_GB_PAIR", &Options::gb_pair},
     {"rl_full", "PLGPU_RL_FULL", &Options::rl_full},
+    {"filt_fused", "PLGPU_FILT_FUSED", &Options::filt_fused},
 };
 const OptField* opt_field(const char* name) {
     for (const OptField& f : kOptFields)

@@ -181,6 +181,38 @@ def test_eval_arith_vs_oracle(gpu, n):
             assert np.array_equal(gv[evalid].astype(ev.dtype), ev[evalid]), repr(e)
 
 
+@pytest.mark.parametrize("n", [1, 4095, 4096, 4097, 64 * 4096 + 5, 3_000_001])
+@pytest.mark.parametrize("fused", [1, 0])
+def test_filter_one_pass_lookback(gpu, plgpu_option, n, fused):
+    """The one-pass filter (filter_fused8_kernel: tiles by ticket, output
+    offsets by decoupled look-back over up to ~730 predecessors) on null-free
+    8-byte columns, against numpy and against the three-pass path (option
+    filt_fused off): half / all / none selected, NaN in the predicate column
+    (NaN > k holds: NaN sorts above every number), an Int64 predicate and
+    sliced inputs."""
+    plgpu_option("filt_fused", fused)
+    rng = np.random.default_rng(n + fused)
+    x = rng.uniform(0, 500, n + 3)
+    x[rng.random(n + 3) < 0.01] = np.nan
+    b = rng.integers(-1000, 1000, n + 3).astype(np.int64)
+    c = rng.standard_normal(n + 3)
+    for off in (0, 3):
+        xs, bs, cs = x[off:off + n], b[off:off + n], c[off:off + n]
+        full = [pl.Series.from_numpy("x", x), pl.Series.from_numpy("b", b), pl.Series.from_numpy("c", c)]
+        df = pl.DataFrame([f.slice(off, n) for f in full])
+        cases = [(pl.col("x") > 250.0, (xs > 250.0) | np.isnan(xs)),
+                 (pl.col("x") > -1.0, np.ones(n, bool)),
+                 (pl.col("x") < -1.0, np.zeros(n, bool)),
+                 (pl.col("b") >= 10, bs >= 10)]
+        for e, m in cases:
+            out = df.filter(e)
+            assert out.height == int(m.sum())
+            assert np.array_equal(_bits(out["x"].to_numpy()), _bits(xs[m]))
+            assert np.array_equal(out["b"].to_numpy(), bs[m])
+            assert np.array_equal(_bits(out["c"].to_numpy()), _bits(cs[m]))
+            assert out["x"].validity_numpy().all()
+
+
 def test_filter_on_sliced_columns(gpu):
     rng = np.random.default_rng(3)
     n = 5000

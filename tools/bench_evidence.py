@@ -49,7 +49,7 @@ LEGS = {
     "rolling": (r"rl_wave_kernel<4, false, false>", "rolling", True),
     "join": (r"jn_probe_match_kernel<false, 0, false, true>", "join", False),
     "join_emit": (r"jn_take_emit_kernel<2, 1>", "join_emit", True),
-    "filter": (r"filter_scatter8_kernel", "filter", True),
+    "filter": (r"filter_(scatter8|fused8)_kernel", "filter", True),
     "filter_mask": (r"filter_mask_kernel", "filter_mask", True),
 }
 
@@ -97,8 +97,8 @@ def line_view(d):
                 out[key] = (sub["kernel_ms"], sub["algorithmic_GB"] * 1e9, L["ms_per_step"], sub["frac"])
     if "filter" in d:
         L = d["filter"]
-        for key, sub in (("filter", L["roofline"]), ("filter_mask", L["mask"])):
-            if sub.get("kernel_ms"):
+        for key, sub in (("filter", L["roofline"]), ("filter_mask", L.get("mask"))):
+            if sub and sub.get("kernel_ms"):
                 out[key] = (sub["kernel_ms"], sub["algorithmic_GB"] * 1e9, L["ms_per_step"], sub["frac"])
     return out
 
