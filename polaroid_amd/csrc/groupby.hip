@@ -40,6 +40,14 @@
 
 namespace plgpu {
 
+// A small device -> host download (status words) through the runtime's
+// pinned stage: the copy is queued and one synchronisation waits for it (a
+// copy into pageable memory is staged and blocking, then a second wait).
+static int d2h_stage(int n, void* const* dst, const void* const* src, const size_t* bytes, hipStream_t s) {
+    return plgpu_memcpy_d2h_many(n, dst, src, bytes, (void*)s);
+}
+
+
 #ifdef PLGPU_CHECKS
 static std::vector<GbChecksTake>& gb_checks_takers() {
     static std::vector<GbChecksTake> v;
@@ -1698,6 +1706,14 @@ struct GbRun {
     }
 };
 
+// The run's status words into R.st (host), one synchronisation.
+static int d2h_status(GbRun& R) {
+    void* d[1] = {R.st};
+    const void* src[1] = {R.status};
+    const size_t b[1] = {sizeof R.st};
+    return d2h_stage(1, d, src, b, R.s);
+}
+
 // Materialise aggregation input j (plgpu_eval of its program) into R.mat.
 static int gb_materialize(GbRun& R, int j, plgpu_column* out) {
     if (R.deriv == nullptr || j < 0 || j >= (int)R.deriv->in.size())
@@ -2033,8 +2049,7 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
                 ps ? R.dp.simple_op : 0, ps ? R.dp.simple_imm : 0ull);
         }
         PLGPU_HIP(hipGetLastError());
-        PLGPU_HIP(hipMemcpyAsync(R.st, R.status, sizeof R.st, hipMemcpyDeviceToHost, R.s));
-        PLGPU_HIP(hipStreamSynchronize(R.s));
+        if (int rs = d2h_status(R)) return rs;
         bool unsampled = false;
         for (int a = 0; a < p.nacc; ++a)
             if ((p.acc[a].flags & (A_FSUM | A_FSUMCAST)) && R.st[ST_MAXEX + a] == 0) unsampled = true;
@@ -2042,8 +2057,7 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
             gb_plan_kernel<<<p.nacc * kPlanBlocks, kPlanThreads, 0, R.s>>>(p, R.status + kPlanSetWord, kPlanSamples,
                                                                            0, 0, 0, 0ull);
             PLGPU_HIP(hipGetLastError());
-            PLGPU_HIP(hipMemcpyAsync(R.st, R.status, sizeof R.st, hipMemcpyDeviceToHost, R.s));
-            PLGPU_HIP(hipStreamSynchronize(R.s));
+            if (int rs = d2h_status(R)) return rs;
         }
         if (use_cache) {
             std::memcpy(cached.st, R.st, sizeof R.st);
@@ -2523,8 +2537,7 @@ static int gb_refit(GbRun& R, uint32_t flagged, int32_t* hint, bool* changed, ui
     for (int a = 0; a < p.nacc; ++a)
         if ((flagged >> a) & 1u) gb_maxexp_kernel<<<std::max(1, num_cus() * 4), 256, 0, R.s>>>(p, a);
     PLGPU_HIP(hipGetLastError());
-    PLGPU_HIP(hipMemcpyAsync(R.st, R.status, sizeof R.st, hipMemcpyDeviceToHost, R.s));
-    PLGPU_HIP(hipStreamSynchronize(R.s));
+    if (int rs = d2h_status(R)) return rs;
     for (int a = 0; a < p.nacc; ++a) {
         if (!((flagged >> a) & 1u)) continue;
         const int tmax = std::max((int)R.st[ST_MAXEX + a], 1);
@@ -2626,8 +2639,7 @@ static int gb_main(GbRun& R, bool auto_refit, bool* refit, int32_t* hint) {
             }
         }
         PLGPU_HIP(hipEventRecord(ev1, R.s));
-        PLGPU_HIP(hipMemcpyAsync(R.st, R.status, sizeof R.st, hipMemcpyDeviceToHost, R.s));
-        PLGPU_HIP(hipStreamSynchronize(R.s));
+        if (int rs = d2h_status(R)) return rs;
         if (debug) {
             fprintf(stderr,
                     "[plgpu] gb attempt %d: n=%lld grid=%d/%d lds=%d lcap=%d gcap=%lld nfields=%d lds_bytes=%zu "
@@ -2814,10 +2826,10 @@ static int gb_finalize(GbRun& R, int32_t naggs, plgpu_column* out_key, plgpu_col
         if (e != hipSuccess) rc = hip_fail(e, "gb_finalize_kernel");
         uint64_t produced = 0, var_out = 0;
         if (rc == PLGPU_OK) {
-            e = hipMemcpyAsync(&produced, R.status + ST_GROUPS_OUT, 8, hipMemcpyDeviceToHost, s);
-            if (e == hipSuccess) e = hipMemcpyAsync(&var_out, R.status + ST_VAR_OUT, 8, hipMemcpyDeviceToHost, s);
-            if (e == hipSuccess) e = hipStreamSynchronize(s);
-            if (e != hipSuccess) rc = hip_fail(e, "finalize count");
+            void* d[2] = {&produced, &var_out};
+            const void* src[2] = {R.status + ST_GROUPS_OUT, R.status + ST_VAR_OUT};
+            const size_t b[2] = {8, 8};
+            rc = d2h_stage(2, d, src, b, s);
         }
         if (rc == PLGPU_OK && var_out)
             rc = fail(PLGPU_ERR_CAPACITY, "var: the fused second moment is out of its exact range");
