@@ -814,6 +814,17 @@ def main():
         },
         "cpu_baseline": None,
     }
+    if rank == 0 and world == 1 and not args.no_filter:
+        # first after the headline, over its frame, with the cached device
+        # blocks returned: the filter's 20 GB of outputs come from a clean
+        # pool (behind the other legs' allocations the scatter measured 10.0
+        # to 12.6 ms from box to box against 10.0 ms standalone,
+        # profiles/r05s_evidence.md, r05t_evidence.md)
+        torch.cuda.empty_cache()
+        pl._native.release_cached()
+        result["filter"] = filter_leg(torch, pl, df, args.leg_steps, 2, int(args.cpu_rows), args.cpu_seconds / 2,
+                                      args.no_cpu)
+        progress(f"filter leg: {result['filter']['ms_per_step']} ms per step")
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(int(args.cpu_rows), args.groups, args.cpu_seconds)
         progress("cpu_baseline done")
@@ -828,16 +839,6 @@ def main():
         pl._native.release_cached()
         result["keys"] = keys_leg(torch, pl, sym, cols, args.leg_steps * 2, 2, ms_per_step)
         progress("keys leg done")
-    if rank == 0 and world == 1 and not args.no_filter:
-        # the earlier legs' frames are gone; their cached device blocks are
-        # returned first, so the filter's outputs come from a clean pool (as
-        # in a standalone run: 11.6-12.5 ms against 14.1 ms per step behind a
-        # fragmented cache, gpurun_out/r05x_*)
-        torch.cuda.empty_cache()
-        pl._native.release_cached()
-        result["filter"] = filter_leg(torch, pl, df, args.leg_steps, 2, int(args.cpu_rows), args.cpu_seconds / 2,
-                                      args.no_cpu)
-        progress(f"filter leg: {result['filter']['ms_per_step']} ms per step")
     if rank == 0 and world == 1 and not args.no_many_groups:
         del query, out
         query = out = None
