@@ -1090,9 +1090,13 @@ __global__ __launch_bounds__(PART && !RUNS ? kGbPartThreads : kGbThreads) void g
     // 1's columns as plain sums do, acc VAR - 2 sums v[0] * v[1] (the host
     // puts the product's other operand in its column, pair_normalize), with
     // none of the general derived path's operand registers or op switch
-    static_assert(VAR != 1 || (NACC == 3 && !DERIV), "VAR 1: three sums of one column");
-    static_assert(VAR < 2 || (NACC == 2 && !DERIV), "VAR 2 / 3: a product and its operand");
-    constexpr int NL = VAR == 1 ? 1 : NACC;  // accs whose column the tile loads
+    // VAR 4: the triple with x >= 0 (or NaN) on every selected row -- the
+    // fused predicate x > c (or >=) with c >= 0 on x's column -- so x's limbs
+    // need no sign either (launch_fast_var)
+    constexpr bool TRIPLE = VAR == 1 || VAR == 4;
+    static_assert(!TRIPLE || (NACC == 3 && !DERIV), "VAR 1 / 4: three sums of one column");
+    static_assert(VAR != 2 && VAR != 3 || (NACC == 2 && !DERIV), "VAR 2 / 3: a product and its operand");
+    constexpr int NL = TRIPLE ? 1 : NACC;  // accs whose column the tile loads
     // SLIM (sum-only, 2 limbs): fields key 0, len 1, acc a: limbs 2+3a,
     // 3+3a, flags 4+3a (the unused low limb of the 3-limb layout is not
     // stored, so more workgroups fit per CU).  The keys are one array (the
@@ -1383,7 +1387,7 @@ __global__ __launch_bounds__(PART && !RUNS ? kGbPartThreads : kGbThreads) void g
             bool sel = true;
             if (PRED == 1) {
                 uint64_t x = cur.pv[j];
-                if (VAR == 1) {
+                if (TRIPLE) {
                     if (p.pred_acc >= 0) x = cur.v[0][j];  // every acc reads x's column
                 } else {
 #pragma unroll
@@ -1421,9 +1425,9 @@ __global__ __launch_bounds__(PART && !RUNS ? kGbPartThreads : kGbThreads) void g
                 int bot[NA];
 #pragma unroll
                 for (int a = 0; a < NA; ++a) {
-                    if (VAR == 1) {
+                    if (TRIPLE) {
                         rv[a] = a == 0 ? cur.v[0][0] : derive(a == 1 ? DOP_SQHI : DOP_SQLO, cur.v[0][0], 0ull);
-                    } else if (VAR >= 2) {
+                    } else if (VAR == 2 || VAR == 3) {
                         rv[a] = a == VAR - 2 ? f64_bits(as_f64(cur.v[0][0]) * as_f64(cur.v[1][0])) : cur.v[a][0];
                     } else {
                         rv[a] = cur.v[a][0];
@@ -1491,7 +1495,8 @@ __global__ __launch_bounds__(PART && !RUNS ? kGbPartThreads : kGbThreads) void g
                     uint64_t fl0[NA], fl1[NA], fl2[NA];
 #pragma unroll
                     for (int a = 0; a < NACC; ++a) {
-                        const bool ok = fx_limbs_fast<LIMBS>(rv[a], bot[a], fl0[a], fl1[a], fl2[a], VAR == 1 && a == 1);
+                        const bool ok = fx_limbs_fast<LIMBS>(rv[a], bot[a], fl0[a], fl1[a], fl2[a],
+                                                                  TRIPLE && (a == 1 || (VAR == 4 && a == 0)));
                         slow |= (ok ? 0u : 1u) << a;
                     }
                     // the limbs of a slow value are not added here (2 limbs:
@@ -1703,7 +1708,7 @@ hipError_t launch_fast_rows(const Plan& pl, const DevProgram& dp, hipStream_t s)
     const size_t lds = (SUMONLY && LIMBS == 2) ? (size_t)slim_words(NACC) * (pl.p.lcap + 2) * 8 : pl.lds_bytes;
     GbParams q = pl.p;
     q.tiles_per_wg = 0;
-    if (VAR >= 2) pair_normalize(q, VAR - 2, PRED == 1);
+    if (VAR == 2 || VAR == 3) pair_normalize(q, VAR - 2, PRED == 1);
     // the plan's n_full is a multiple of the 2-row tile; a wider tile takes
     // its own multiple (the masked last tile covers the rest)
     if (ROWS != 2) q.n_full = (pl.p.n / ((int64_t)kGbThreads * ROWS)) * kGbThreads * ROWS;
@@ -1725,7 +1730,7 @@ hipError_t launch_fast_rows(const Plan& pl, const DevProgram& dp, hipStream_t s)
     const int grid = (int)g;
     pl.launched_grid = grid;
     pl.launched_runs = RUNS;
-    pl.launched_var = VAR == 1;
+    pl.launched_var = VAR == 1 || VAR == 4;
     if (pl.local) {
         const int64_t tile = (int64_t)kGbThreads * ROWS;
         const int64_t nall = q.n_full / tile + (pl.p.n > q.n_full ? 1 : 0);
@@ -1778,11 +1783,28 @@ inline bool var_triple(const Plan& pl) {
     return a0.dop == DOP_NONE && a0.c.dtype == PLGPU_F64;
 }
 
+// x >= 0 (or NaN) on every row the fused predicate keeps: a float compare
+// on x's own column that accepts no value below c (x > c, x >= c, x == c)
+// with c >= 0 (NaN compares greatest and fails the limb window anyway; -0.0
+// converts to zero limbs either way).
+inline bool var_x_nonneg(const Plan& pl, const DevProgram& dp) {
+    if (!dp.simple || !dp.simple_isf || pl.p.pred_acc != 0 || dp.simple_op < 0 || dp.simple_op > 5) return false;
+    const uint32_t accept = (0x643152u >> (4 * dp.simple_op)) & 0xFu;  // simple_pred's classes: 1 lt, 2 eq, 4 gt
+    if (accept & 1u) return false;
+    double c;
+    std::memcpy(&c, &dp.simple_imm, 8);
+    return c >= 0.0;
+}
+
 template <int PRED>
 hipError_t launch_fast_var(const Plan& pl, const DevProgram& dp, hipStream_t s) {
-    if (!pl.sum_only) return launch_fast_rows<3, PRED, false, 3, false, false, true>(pl, dp, s);
-    if (pl.limbs == 2) return launch_fast_rows<3, PRED, true, 2, false, false, true>(pl, dp, s);
-    return launch_fast_rows<3, PRED, true, 3, false, false, true>(pl, dp, s);
+    if (!pl.sum_only) return launch_fast_rows<3, PRED, false, 3, false, false, 1>(pl, dp, s);
+    if (pl.limbs == 2) {
+        if (PRED == 1 && options().var_pos && var_x_nonneg(pl, dp))
+            return launch_fast_rows<3, PRED, true, 2, false, false, 4>(pl, dp, s);
+        return launch_fast_rows<3, PRED, true, 2, false, false, 1>(pl, dp, s);
+    }
+    return launch_fast_rows<3, PRED, true, 3, false, false, 1>(pl, dp, s);
 }
 
 

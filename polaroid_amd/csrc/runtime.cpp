@@ -70,6 +70,7 @@ const OptField kOptFields[] = {
     {"gb_pair", "PLGPU_GB_PAIR", &Options::gb_pair},
     {"rl_full", "PLGPU_RL_FULL", &Options::rl_full},
     {"filt_fused", "PLGPU_FILT_FUSED", &Options::filt_fused},
+    {"var_pos", "PLGPU_VAR_POS", &Options::var_pos},
 };
 const OptField* opt_field(const char* name) {
     for (const OptField& f : kOptFields)

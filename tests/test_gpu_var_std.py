@@ -392,3 +392,35 @@ def test_var_triple_sorted_keys_take_the_register_run_path(gpu):
     got = dict(zip(out["k"].to_list(), out["s"].to_list()))
     for k in np.unique(key)[:20]:
         assert math.isclose(got[int(k)], math.sqrt(_exact_var(x[key == k], 1)), rel_tol=1e-12)
+
+
+@pytest.mark.parametrize("pname", ["gt0", "ge0", "gt250", "eq"])
+def test_var_triple_nonneg_predicate(gpu, plgpu_option, pname):
+    """A predicate on x that keeps no value below a non-negative literal
+    (x > c, x >= c, x == c, c >= 0) runs the triple variant whose x limbs
+    carry no sign (gb_fast_kernel VAR 4, option var_pos): bit-identical to
+    the signed variant on data with negatives, zeros, -0.0, NaN and +inf
+    (the predicate drops the negatives; NaN compares greatest and is kept)."""
+    rng = np.random.default_rng(len(pname))
+    n = 300_003
+    key = rng.integers(0, 100, n).astype(np.int64)
+    x = rng.uniform(-500, 500, n)
+    x[rng.random(n) < 0.05] = 0.0
+    x[rng.random(n) < 0.05] = -0.0
+    x[rng.random(n) < 0.05] = 3.5
+    x[rng.integers(0, n, 3)] = np.nan
+    x[rng.integers(0, n, 2)] = np.inf
+    df = pl.DataFrame({"k": pl.Series.from_numpy("k", key), "x": pl.Series.from_numpy("x", x)})
+    p = {"gt0": pl.col("x") > 0.0, "ge0": pl.col("x") >= 0.0, "gt250": pl.col("x") > 250.0,
+         "eq": pl.col("x") == 3.5}[pname]
+    res = []
+    for on in (1, 0):
+        plgpu_option("var_pos", on)
+        info = {}
+        out = (df.lazy().filter(p).group_by("k").agg(pl.col("x").std(1).alias("s"), )
+               .collect(info=info))
+        assert info["path"] == 4, info
+        o = np.argsort(out["k"].to_numpy())
+        res.append((out["k"].to_numpy()[o], out["s"].to_numpy()[o].view(np.int64), out["s"].validity_numpy()[o]))
+    for a, b in zip(res[0], res[1]):
+        assert np.array_equal(a, b), pname

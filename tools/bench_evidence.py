@@ -38,7 +38,7 @@ HBM_PEAK = 8000.0
 LEGS = {
     "headline": (r"gb_fast_kernel<4, 1, true, 2, 2, false, false, false, 0, 0>", "headline", True),
     "vwap": (r"gb_fast_kernel<2, 1, true, 2, 2, false, false, false, 2, 0>", "vwap", True),
-    "std": (r"gb_fast_kernel<3, 1, true, 2, 2, false, false, false, 1, 0>", "std", True),
+    "std": (r"gb_fast_kernel<3, 1, true, 2, 2, false, false, false, [14], 0>", "std", True),
     "keys_categorical": (r"gb_fast_kernel<4, 1, true, 2, 2, false, false, false, 0, 1>", "keys_categorical",
                          ("first", True)),
     "keys_string": (r"gb_fast_kernel<4, 1, true, 2, 2, false, false, false, 0, 2>", "keys_string", True),

@@ -19,6 +19,7 @@ VARIANTS = {
     "vwap product pair (VAR 2)": "ILi2ELi1ELb1ELi2ELi2ELb0ELb0ELb0ELi2ELi0EE",
     "vwap-like 2 plain sums": "ILi2ELi1ELb1ELi2ELi2ELb0ELb0ELb0ELi0ELi0EE",
     "std VAR triple": "ILi3ELi1ELb1ELi2ELi2ELb0ELb0ELb0ELi1ELi0EE",
+    "std VAR triple, x >= 0 (VAR 4)": "ILi3ELi1ELb1ELi2ELi2ELb0ELb0ELb0ELi4ELi0EE",
     "headline PACK (fused integer keys)": "ILi4ELi1ELb1ELi2ELi2ELb0ELb0ELb0ELi0ELi1EE",
     "headline PACK (String key codes)": "ILi4ELi1ELb1ELi2ELi2ELb0ELb0ELb0ELi0ELi2EE",
 }
