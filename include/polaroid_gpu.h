@@ -272,6 +272,8 @@ int plgpu_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream);
  *                  product-pair variant
  *   "var_pos"      1: the fused variance's x limbs unsigned when the fused
  *                  predicate keeps only x >= 0
+ *   "sum_pos"      1: the fused 4-sum kernel's limbs of the predicate's own
+ *                  column unsigned when the predicate keeps only x >= 0
  *   "filt_fused"   1: a simple-predicate filter of null-free 8-byte columns
  *                  in one pass (decoupled look-back; off: measured slower)
  * An unknown name is PLGPU_ERR_INVALID. */

@@ -1096,6 +1096,10 @@ __global__ __launch_bounds__(PART && !RUNS ? kGbPartThreads : kGbThreads) void g
     constexpr bool TRIPLE = VAR == 1 || VAR == 4;
     static_assert(!TRIPLE || (NACC == 3 && !DERIV), "VAR 1 / 4: three sums of one column");
     static_assert(VAR != 2 && VAR != 3 || (NACC == 2 && !DERIV), "VAR 2 / 3: a product and its operand");
+    // VAR 5 (sum-only, plain inputs): the last acc's column is the fused
+    // predicate's and keeps no value below a literal >= 0, so its limbs need
+    // no sign (the headline's close.sum() under close > 250)
+    static_assert(VAR != 5 || (SUMONLY && !DERIV && NACC > 0), "VAR 5: plain sums");
     constexpr int NL = TRIPLE ? 1 : NACC;  // accs whose column the tile loads
     // SLIM (sum-only, 2 limbs): fields key 0, len 1, acc a: limbs 2+3a,
     // 3+3a, flags 4+3a (the unused low limb of the 3-limb layout is not
@@ -1496,7 +1500,8 @@ __global__ __launch_bounds__(PART && !RUNS ? kGbPartThreads : kGbThreads) void g
 #pragma unroll
                     for (int a = 0; a < NACC; ++a) {
                         const bool ok = fx_limbs_fast<LIMBS>(rv[a], bot[a], fl0[a], fl1[a], fl2[a],
-                                                                  TRIPLE && (a == 1 || (VAR == 4 && a == 0)));
+                                                                  (TRIPLE && (a == 1 || (VAR == 4 && a == 0))) ||
+                                                                      (VAR == 5 && a == NACC - 1));
                         slow |= (ok ? 0u : 1u) << a;
                     }
                     // the limbs of a slow value are not added here (2 limbs:
@@ -1742,10 +1747,28 @@ hipError_t launch_fast_rows(const Plan& pl, const DevProgram& dp, hipStream_t s)
     return hipGetLastError();
 }
 
+// x >= 0 (or NaN) on every row the fused predicate keeps: a float compare
+// on acc `a`'s own column that accepts no value below c (x > c, x >= c,
+// x == c) with c >= 0 (NaN compares greatest and fails the limb window
+// anyway; -0.0 converts to zero limbs either way).
+inline bool var_x_nonneg(const Plan& pl, const DevProgram& dp, int a = 0) {
+    if (!dp.simple || !dp.simple_isf || pl.p.pred_acc != a || dp.simple_op < 0 || dp.simple_op > 5) return false;
+    if (pl.p.acc[a].dop != DOP_NONE || pl.p.acc[a].c.dtype != PLGPU_F64) return false;
+    const uint32_t accept = (0x643152u >> (4 * dp.simple_op)) & 0xFu;  // simple_pred's classes: 1 lt, 2 eq, 4 gt
+    if (accept & 1u) return false;
+    double c;
+    std::memcpy(&c, &dp.simple_imm, 8);
+    return c >= 0.0;
+}
+
 template <int NACC, int PRED, bool SUMONLY, bool DERIV, int PACK = 0>
 hipError_t launch_fast(const Plan& pl, const DevProgram& dp, hipStream_t s) {
     if (SUMONLY && pl.limbs == 2 && pl.runs)
         return launch_fast_rows<NACC, PRED, SUMONLY, 2, true, DERIV, false, PACK>(pl, dp, s);
+    if constexpr (NACC == 4 && PRED == 1 && SUMONLY && !DERIV) {
+        if (pl.limbs == 2 && options().sum_pos && var_x_nonneg(pl, dp, NACC - 1))
+            return launch_fast_rows<NACC, PRED, SUMONLY, 2, false, DERIV, 5, PACK>(pl, dp, s);
+    }
     if (SUMONLY && pl.limbs == 2) return launch_fast_rows<NACC, PRED, SUMONLY, 2, false, DERIV, false, PACK>(pl, dp, s);
     if (!SUMONLY && NACC > 0 && !DERIV && pl.runs && pl.limbs == 2)
         return launch_fast_rows<NACC, PRED, false, 2, true, false, false, PACK>(pl, dp, s);
@@ -1781,19 +1804,6 @@ inline bool var_triple(const Plan& pl) {
             return false;
     }
     return a0.dop == DOP_NONE && a0.c.dtype == PLGPU_F64;
-}
-
-// x >= 0 (or NaN) on every row the fused predicate keeps: a float compare
-// on x's own column that accepts no value below c (x > c, x >= c, x == c)
-// with c >= 0 (NaN compares greatest and fails the limb window anyway; -0.0
-// converts to zero limbs either way).
-inline bool var_x_nonneg(const Plan& pl, const DevProgram& dp) {
-    if (!dp.simple || !dp.simple_isf || pl.p.pred_acc != 0 || dp.simple_op < 0 || dp.simple_op > 5) return false;
-    const uint32_t accept = (0x643152u >> (4 * dp.simple_op)) & 0xFu;  // simple_pred's classes: 1 lt, 2 eq, 4 gt
-    if (accept & 1u) return false;
-    double c;
-    std::memcpy(&c, &dp.simple_imm, 8);
-    return c >= 0.0;
 }
 
 template <int PRED>

@@ -60,6 +60,7 @@ struct Options {
     int rl_full = 1;      // rolling sum / mean: interior int64-form waves by the specialised scan (A/B)
     int filt_fused = 0;   // filter: the one-pass look-back kernel where it applies (A/B; measured slower)
     int var_pos = 1;      // fused variance: x's limbs unsigned when the predicate keeps x >= 0 (A/B)
+    int sum_pos = 1;      // fused 4-sum kernel: the predicate column's limbs unsigned when it keeps x >= 0 (A/B)
     int gb_pair = 1;      // (x * y).sum() next to y.sum(): the product-pair fused variant (A/B)
 };
 Options& options();

@@ -71,6 +71,7 @@ const OptField kOptFields[] = {
     {"rl_full", "PLGPU_RL_FULL", &Options::rl_full},
     {"filt_fused", "PLGPU_FILT_FUSED", &Options::filt_fused},
     {"var_pos", "PLGPU_VAR_POS", &Options::var_pos},
+    {"sum_pos", "PLGPU_SUM_POS", &Options::sum_pos},
 };
 const OptField* opt_field(const char* name) {
     for (const OptField& f : kOptFields)

@@ -275,3 +275,35 @@ def test_fused_string_key(gpu, case):
     for key, xs in want.items():
         assert got[key] == (math.fsum(xs), len(xs)), key
 
+
+
+@pytest.mark.parametrize("pname", ["gt0", "ge0", "gt250"])
+@pytest.mark.parametrize("keys", ["int64", "sym_day"])
+def test_nonneg_predicate_column_sum(gpu, plgpu_option, pname, keys):
+    """Four sums whose last column is the fused predicate's and keeps no
+    value below a literal >= 0 (the headline's close.sum() under
+    close > 250) run the variant whose last limbs carry no sign
+    (gb_fast_kernel VAR 5, option sum_pos): bit-identical to the signed
+    variant on data with negatives, zeros, -0.0, NaN and +inf."""
+    rng = np.random.default_rng(len(pname) + len(keys))
+    n = 400_003
+    sym = rng.integers(0, 100, n).astype(np.int64)
+    day = (np.arange(n) // 5000).astype(np.int32)
+    cols = {c: rng.uniform(-500, 500, n) for c in ("open", "high", "low", "close")}
+    x = cols["close"]
+    x[rng.random(n) < 0.05] = 0.0
+    x[rng.random(n) < 0.05] = -0.0
+    x[rng.integers(0, n, 3)] = np.nan
+    x[rng.integers(0, n, 2)] = np.inf
+    df = pl.DataFrame({"sym": pl.Series.from_numpy("sym", sym), "day": pl.Series.from_numpy("day", day),
+                       **{c: pl.Series.from_numpy(c, v) for c, v in cols.items()}})
+    p = {"gt0": pl.col("close") > 0.0, "ge0": pl.col("close") >= 0.0, "gt250": pl.col("close") > 250.0}[pname]
+    by = ["sym"] if keys == "int64" else ["sym", "day"]
+    res = []
+    for on in (1, 0):
+        plgpu_option("sum_pos", on)
+        out = df.lazy().filter(p).group_by(*by).agg(*[pl.col(c).sum() for c in cols]).collect()
+        o = np.lexsort([out[k].to_numpy() for k in reversed(by)])
+        res.append([out[k].to_numpy()[o] for k in by] + [out[c].to_numpy()[o].view(np.int64) for c in cols])
+    for a, b in zip(res[0], res[1]):
+        assert np.array_equal(a, b), pname

@@ -36,13 +36,13 @@ HBM_PEAK = 8000.0
 # PACK = 1 variant with equal launch counts: "first" / "second" half of that
 # kernel's launches in trace order.
 LEGS = {
-    "headline": (r"gb_fast_kernel<4, 1, true, 2, 2, false, false, false, 0, 0>", "headline", True),
+    "headline": (r"gb_fast_kernel<4, 1, true, 2, 2, false, false, false, [05], 0>", "headline", True),
     "vwap": (r"gb_fast_kernel<2, 1, true, 2, 2, false, false, false, 2, 0>", "vwap", True),
     "std": (r"gb_fast_kernel<3, 1, true, 2, 2, false, false, false, [14], 0>", "std", True),
-    "keys_categorical": (r"gb_fast_kernel<4, 1, true, 2, 2, false, false, false, 0, 1>", "keys_categorical",
+    "keys_categorical": (r"gb_fast_kernel<4, 1, true, 2, 2, false, false, false, [05], 1>", "keys_categorical",
                          ("first", True)),
-    "keys_string": (r"gb_fast_kernel<4, 1, true, 2, 2, false, false, false, 0, 2>", "keys_string", True),
-    "keys_sym_day": (r"gb_fast_kernel<4, 1, true, 2, 2, false, false, false, 0, 1>", "keys_sym_day",
+    "keys_string": (r"gb_fast_kernel<4, 1, true, 2, 2, false, false, false, [05], 2>", "keys_string", True),
+    "keys_sym_day": (r"gb_fast_kernel<4, 1, true, 2, 2, false, false, false, [05], 1>", "keys_sym_day",
                      ("second", True)),
     "sort": (r"aos_gather_kernel<8>", "sort", False),
     "sort_pack": (r"aos_pack_kernel<8>", "sort_pack", True),

@@ -20,7 +20,9 @@ VARIANTS = {
     "vwap-like 2 plain sums": "ILi2ELi1ELb1ELi2ELi2ELb0ELb0ELb0ELi0ELi0EE",
     "std VAR triple": "ILi3ELi1ELb1ELi2ELi2ELb0ELb0ELb0ELi1ELi0EE",
     "std VAR triple, x >= 0 (VAR 4)": "ILi3ELi1ELb1ELi2ELi2ELb0ELb0ELb0ELi4ELi0EE",
+    "headline, close >= 0 (VAR 5)": "ILi4ELi1ELb1ELi2ELi2ELb0ELb0ELb0ELi5ELi0EE",
     "headline PACK (fused integer keys)": "ILi4ELi1ELb1ELi2ELi2ELb0ELb0ELb0ELi0ELi1EE",
+    "headline PACK 1, close >= 0 (VAR 5)": "ILi4ELi1ELb1ELi2ELi2ELb0ELb0ELb0ELi5ELi1EE",
     "headline PACK (String key codes)": "ILi4ELi1ELb1ELi2ELi2ELb0ELb0ELb0ELi0ELi2EE",
 }
 
