@@ -62,6 +62,7 @@ def parse():
     ap.add_argument("--no-sort", action="store_true", help="skip the configs[2] sort + rolling leg")
     ap.add_argument("--no-join", action="store_true", help="skip the configs[3] join leg")
     ap.add_argument("--no-keys", action="store_true", help="skip the Categorical / String / (symbol, day) legs")
+    ap.add_argument("--no-nulls", action="store_true", help="skip the validity-bitmap leg (1 %% nulls)")
     ap.add_argument("--no-filter", action="store_true", help="skip the filter-only leg (row a1)")
     ap.add_argument("--no-many-groups", action="store_true", help="skip the many-groups leg")
     ap.add_argument("--many-groups", type=str, default=",".join(str(g) for g in MANY_GROUPS),
@@ -449,6 +450,93 @@ def many_groups_leg(torch, pl, cols: dict, steps: int, warmup: int, groups_list,
     return out
 
 
+NULLS_GROUPS = (100, 1_000_000)
+NULL_FRAC = 0.01
+
+
+def null_bitmap(torch, n: int, frac: float, seed: int, dev):
+    """An Arrow validity bitmap (LSB-first bit per row, 1 = valid) with about
+    `frac` nulls at random rows, generated on the device in chunks."""
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    nbytes = (n + 7) // 8
+    out = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    w = torch.tensor([1, 2, 4, 8, 16, 32, 64, 128], dtype=torch.uint8, device=dev)
+    chunk = 1 << 24
+    for s0 in range(0, nbytes, chunk):
+        e = min(nbytes, s0 + chunk)
+        bits = (torch.rand((e - s0) * 8, device=dev, generator=g) >= frac).to(torch.uint8).view(e - s0, 8)
+        out[s0:e] = (bits * w).sum(dim=1).to(torch.uint8)
+    return out
+
+
+def nulls_leg(torch, pl, sym, cols: dict, steps: int, warmup: int, headline_ms: float) -> dict:
+    """The headline query with Arrow validity bitmaps: ~1 % nulls in each of
+    open, high, low, close ("values"), and the same plus ~1 % null symbols
+    ("key_and_values"), at 100 groups (the headline's keys: the fused
+    kernel's NULLS variant) and 1e6 random groups (the partitioned path, the
+    null bits travelling with the partitioned rows), each against the
+    null-free step of the same keys (100: the headline's step; 1e6: measured
+    here).  Reference: polars-expr/src/reduce/sum.rs:108 reduce_one over
+    Option<T>, :117 the has_nulls branch; polars-stream/src/nodes/
+    group_by.rs:85 add_pre_agg.  rank 0, N = 1."""
+    n = sym.numel()
+    dev = sym.device
+    sums = [pl.col(c).sum() for c in ("open", "high", "low", "close")]
+    bitmaps = {c: null_bitmap(torch, n, NULL_FRAC, 500 + i, dev) for i, c in enumerate(cols)}
+    kbits = null_bitmap(torch, n, NULL_FRAC, 600, dev)
+    out = {"null_fraction": NULL_FRAC}
+    for G in NULLS_GROUPS:
+        if G == 100:
+            key = sym
+        else:
+            g = torch.Generator(device=dev)
+            g.manual_seed(G)
+            key = torch.empty(n, dtype=torch.int64, device=dev)
+            for s0 in range(0, n, 1 << 26):
+                e = min(n, s0 + (1 << 26))
+                key[s0:e] = torch.randint(0, G, (e - s0,), device=dev, generator=g, dtype=torch.int64) * 7919 + 1_000_000
+        cases = {}
+        variants = (("null_free", False, False), ("values", True, False), ("key_and_values", True, True))
+        for name, vnull, knull in variants:
+            if name == "null_free" and G == 100:
+                continue
+            df = pl.DataFrame([pl.Series.from_torch("symbol", key, kbits if knull else None)] +
+                              [pl.Series.from_torch(c, t, bitmaps[c] if vnull else None) for c, t in cols.items()])
+            q = df.lazy().filter(pl.col("close") > THRESHOLD).group_by("symbol").agg(*sums)
+
+            def step():
+                info = {}
+                res = q.collect(info=info)
+                info["out_groups"] = res.height
+                return info
+
+            ms, kernels, info = _time_steps(torch, step, steps, warmup)
+            bpr = 40 + (0.5 if vnull else 0) + (0.125 if knull else 0)
+            r = {"ms_per_step": round(ms, 3), "groups": int(info.get("out_groups", 0)), "path": info.get("path"),
+                 "rows_selected": int(info.get("rows_selected", 0)), "bytes_per_row": bpr, "kernels": kernels}
+            kms = kernels.get("gb_fast_kernel", {}).get("ms_mean")
+            if info.get("path") in (1, 2) and kms:
+                r["kernel_ms"] = kms
+                r["frac"] = round(bpr * n / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+            cases[name] = r
+            progress(f"nulls leg {G} {name}: {r['ms_per_step']} ms per step (path {r['path']})")
+            del df, q
+        base = headline_ms if G == 100 else cases["null_free"]["ms_per_step"]
+        for name in ("values", "key_and_values"):
+            cases[name]["vs_null_free"] = round(cases[name]["ms_per_step"] / base, 3)
+        cases["null_free_ms"] = round(base, 3)
+        out[str(G)] = cases
+        if G != 100:
+            del key
+        torch.cuda.empty_cache()
+    del bitmaps, kbits
+    out["note"] = ("vs_null_free: step over the null-free step of the same keys (100 groups: the headline step of "
+                   "this run); bytes_per_row: 40 + 1 validity bit per nullable column; frac: the fused kernel at "
+                   "those bytes")
+    return out
+
+
 def _kernel_table(kt: dict, steps: int) -> dict:
     """plgpu_ktime_read sums -> {kernel: {ms_mean (per launch), ms_per_step, launches}}."""
     return {k: {"ms_mean": round(ms / max(c, 1), 4), "ms_per_step": round(ms / steps, 4), "launches": c}
@@ -590,6 +678,33 @@ def join_leg(torch, pl, steps: int, warmup: int, n: int = JOIN_PROBE, m: int = J
     assert 0.45 * n < res < 0.55 * n
     del probe, build, pk, pv, bk, bv
     torch.cuda.empty_cache()
+    algo = n * 16 + m * 16 + res * 24
+    out = {"query": "probe.join(build, on='k') inner, output k, pv, bv", "probe_rows": n, "build_rows": m,
+           "output_rows": res, "ms_per_step": round(ms, 3), "Mrows_s": round(n / ms / 1e3, 1),
+           "algorithmic_GB": round(algo / 1e9, 2),
+           "step_frac": round(algo / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "kernels": kernels}
+    if "rj_match_kernel" in kernels:
+        # the partitioned join (join.hip jn_radix_take): count + scatter of
+        # the probe rows into 2^8 partitions, the L2-resident match pass,
+        # then the row-format join's emit
+        match = _leg_roofline(kernels, "rj_match_kernel", n * 8 + n / 8 + res * 8,
+                              "partitioned key read (8 B per probe row), hit bits + the hits' payload words "
+                              "written; sub-table reads served by the XCD's L2")
+        match.update(_pmc_traffic("rj_match_kernel"))
+        emit = _leg_roofline(kernels, "jn_take_emit_kernel", n * (16 + 1 / 8) + res * (8 + 24),
+                             "partitioned k, pv + hit bits read per row, the hit's payload read, 3 x 8 B written "
+                             "per output row")
+        emit.update(_pmc_traffic("jn_take_emit_kernel"))
+        count = _leg_roofline(kernels, "gbp_count_kernel", n * 8, "8 B probe key read per row")
+        scatter = _leg_roofline(kernels, "gbp_scatter_kernel", n * 32, "k, pv read and written once (32 B per row)")
+        floor = n * 8 + n * 32 + (n * 8 + res * 8) + (n * 16 + res * 32) + m * 16
+        out.update({"path": "partitioned (radix) join", "roofline": match, "emit": emit, "count": count,
+                    "scatter": scatter, "design_floor_GB": round(floor / 1e9, 2),
+                    "design_floor_ms_at_peak": round(floor / (HBM_PEAK_GBS * 1e9) * 1e3, 3),
+                    "note": "step_frac: probe (k, pv) + build (k, bv) read once, 3 output columns written once, "
+                            "over the step time; design floor: count (8 B) + scatter (32 B) + match (8 B + 8 B "
+                            "per hit) + emit (16 B + 32 B per hit) + build; roofline: the match pass"})
+        return out
     match = _leg_roofline(kernels, "jn_probe_match_kernel", n * (8 + 8) + n // 8,
                           "8 B probe key read + 8 B payload word written per row + 1 hit bit")
     if match.get("kernel_ms"):
@@ -600,14 +715,10 @@ def join_leg(torch, pl, steps: int, warmup: int, n: int = JOIN_PROBE, m: int = J
                                        "(profiles/r02_randread.txt, 256 MiB table)")
     emit = _leg_roofline(kernels, "jn_take_emit_kernel", n * (8 + 8 + 1 / 8) + res * 24,
                          "payload words + probe payload read, 3 x 8 B written per output row")
-    algo = n * 16 + m * 16 + res * 24
-    return {"query": "probe.join(build, on='k') inner, output k, pv, bv", "probe_rows": n, "build_rows": m,
-            "output_rows": res, "ms_per_step": round(ms, 3), "Mrows_s": round(n / ms / 1e3, 1),
-            "algorithmic_GB": round(algo / 1e9, 2),
-            "step_frac": round(algo / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-            "roofline": match, "emit": emit, "kernels": kernels,
-            "note": "step_frac: probe (k, pv) + build (k, bv) read once, 3 output columns written once, over the "
-                    "step time; roofline: the match pass (bound by random table line requests, not bytes)"}
+    out.update({"path": "row-format table", "roofline": match, "emit": emit,
+                "note": "step_frac: probe (k, pv) + build (k, bv) read once, 3 output columns written once, over "
+                        "the step time; roofline: the match pass (bound by random table line requests, not bytes)"})
+    return out
 
 
 def cpu_sort_baseline(rows: int, seconds: float) -> dict:
@@ -671,6 +782,21 @@ def load_traffic(n_rows: int):
     except Exception:
         return None
     return None
+
+
+def _pmc_traffic(kernel: str) -> dict:
+    """A leg kernel's HBM bytes per launch from the committed rocprofv3 PMC
+    passes (profiles/traffic.json "legs", written by tools/bench_evidence.py
+    from the same command's FETCH_SIZE / WRITE_SIZE passes), if present."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        t = json.load(open(path)).get("legs", {}).get(kernel)
+    except Exception:
+        return {}
+    if not t:
+        return {}
+    return {"pmc_traffic_GB": round(float(t["hbm_bytes_per_launch"]) / 1e9, 3),
+            "pmc_source": t.get("source", "profiles/traffic.json")}
 
 
 def launch_ranks(n: int) -> int:
@@ -834,6 +960,9 @@ def main():
     if rank == 0 and world == 1 and not args.no_std:
         result["std"] = std_leg(torch, pl, df, args.steps, args.warmup)
         progress("std leg done")
+    if rank == 0 and world == 1 and not args.no_nulls:
+        result["nulls"] = nulls_leg(torch, pl, sym, cols, args.leg_steps, 2, ms_per_step)
+        progress("nulls leg done")
     if rank == 0 and world == 1 and not args.no_keys:
         torch.cuda.empty_cache()
         pl._native.release_cached()

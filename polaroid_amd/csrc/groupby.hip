@@ -93,6 +93,7 @@ struct PartOut {
     uint64_t* key;
     uint64_t* acc[kMaxAcc];
     uint32_t* rows;  // null unless the first / last row fields are in use
+    uint8_t* nulls;  // null unless an input column is nullable: GbParams::part_nulls bits per row
     int64_t cap;     // rows each buffer holds
 };
 
@@ -179,10 +180,15 @@ __device__ __forceinline__ void ps_col(const DevCol& c, const uint64_t* buf, con
 // and which rows are selected.  L2: the level-1 buffers (every row
 // selected).  F8: the key and predicate columns are null-free 8-byte
 // columns.
-template <int PRED, bool L2, bool F8>
+// NUL: some key / aggregated / predicate column has a validity bitmap (or,
+// at level 2, the level-1 buffers carry null bits): nb[k] gets the row's
+// GbParams::part_nulls bits, a null predicate value drops the row, and a
+// null-key row is spread over the partitions by its position (ps_digit):
+// it aggregates into the null group wherever it lands.
+template <int PRED, bool L2, bool F8, bool NUL = false>
 __device__ __forceinline__ void ps_keys(const GbParams& p, const DevProgram& prog, const PartOut& in, const PsTile& tl,
                                         int c0, uint64_t (&key)[kPsPer], uint64_t (&pv)[kPsPer],
-                                        bool (&sel)[kPsPer]) {
+                                        bool (&sel)[kPsPer], uint32_t (&nb)[kPsPer]) {
     const int lane = threadIdx.x & 63;
     ps_col<L2, F8>(p.key, in.key, tl, c0, key);
     if (!L2 && PRED == 1) ps_col<false, F8>(p.pred_col, nullptr, tl, c0, pv);
@@ -190,8 +196,19 @@ __device__ __forceinline__ void ps_keys(const GbParams& p, const DevProgram& pro
     for (int k = 0; k < kPsPer; ++k) {
         const int64_t r = tl.base + c0 + k * 64 + lane;
         bool s = r >= tl.lo && r < tl.hi;
+        nb[k] = 0;
+        if (NUL && s) {
+            if (L2) {
+                nb[k] = in.nulls ? in.nulls[r] : 0u;
+            } else {
+                uint32_t m = dev_valid(p.key, r) ? 0u : 0x40u;
+                for (int a = 0; a < p.nacc; ++a)
+                    if (!dev_valid(p.acc[a].c, r)) m |= 1u << a;
+                nb[k] = m;
+            }
+        }
         if (!L2 && PRED == 1)
-            s = s && (F8 || dev_valid(p.pred_col, r)) &&
+            s = s && ((F8 && !NUL) || dev_valid(p.pred_col, r)) &&
                 simple_pred(prog.simple_isf, prog.simple_op, pv[k], prog.simple_imm);
         if (!L2 && PRED == 2 && s) {
             const RowVal rv = eval_row(prog.code, prog.n, p.cols, r);
@@ -201,9 +218,16 @@ __device__ __forceinline__ void ps_keys(const GbParams& p, const DevProgram& pro
     }
 }
 
+// The partition hash of row r (its input row at level 1, its position in
+// the level-1 buffers at level 2): its key's, or for a null key (nb bit 6)
+// one of its position, so the null group's rows spread over the partitions.
+__device__ __forceinline__ uint64_t ps_hash(uint64_t key, uint32_t nb, int64_t r) {
+    return part_hash((nb & 0x40u) ? (uint64_t)r * 0x9E3779B97F4A7C15ull : key);
+}
+
 // Count pass: the selected rows of each tile per digit, written digit-major
 // per level-1 partition (cnt[mbase + d * ntq + tl]).
-template <int PRED, bool L2, bool F8>
+template <int PRED, bool L2, bool F8, bool NUL = false>
 __global__ __launch_bounds__(kPsThreads) void gbp_count_kernel(GbParams p, DevProgram prog, PsGeom g, PartOut in,
                                                                uint32_t* __restrict__ cnt) {
     __shared__ uint32_t h[1 << kPsDigitBits];
@@ -213,13 +237,17 @@ __global__ __launch_bounds__(kPsThreads) void gbp_count_kernel(GbParams p, DevPr
     if (threadIdx.x < P) h[threadIdx.x] = 0;
     uint64_t key[kPsPer], pv[kPsPer];
     bool sel[kPsPer];
+    uint32_t nb[kPsPer];
     const int c0 = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) * (kPsTile / (kPsThreads / 64));
-    ps_keys<PRED, L2, F8>(p, prog, in, tl, c0, key, pv, sel);
+    ps_keys<PRED, L2, F8, NUL>(p, prog, in, tl, c0, key, pv, sel, nb);
     __syncthreads();
     const uint32_t mask = (uint32_t)P - 1;
 #pragma unroll
-    for (int k = 0; k < kPsPer; ++k)
-        if (sel[k]) atomicAdd(&h[(uint32_t)(part_hash(key[k]) >> g.sh) & mask], 1u);
+    for (int k = 0; k < kPsPer; ++k) {
+        const int64_t r = tl.base + c0 + k * 64 + (threadIdx.x & 63);
+        const uint64_t hh = NUL ? ps_hash(key[k], nb[k], r) : part_hash(key[k]);
+        if (sel[k]) atomicAdd(&h[(uint32_t)(hh >> g.sh) & mask], 1u);
+    }
     __syncthreads();
     if (threadIdx.x < P) cnt[tl.mbase + (int64_t)threadIdx.x * tl.ntq + tl.tl] = h[threadIdx.x];
 }
@@ -230,7 +258,7 @@ __global__ __launch_bounds__(kPsThreads) void gbp_count_kernel(GbParams p, DevPr
 // then column by column the values are staged in LDS in digit order and
 // written out as one run per digit (the next column's loads are issued
 // before this column's write-out).  off: the scanned count matrix.
-template <int PRED, bool L2, bool F8>
+template <int PRED, bool L2, bool F8, bool NUL = false>
 __global__ __launch_bounds__(kPsThreads) void gbp_scatter_kernel(GbParams p, DevProgram prog, PsGeom g, PartOut in,
                                                                  const uint32_t* __restrict__ off, PartOut o) {
     constexpr int NW = kPsThreads / 64;
@@ -252,14 +280,17 @@ __global__ __launch_bounds__(kPsThreads) void gbp_scatter_kernel(GbParams p, Dev
     const int c0 = __builtin_amdgcn_readfirstlane(wid) * (kPsTile / NW);
     uint64_t key[kPsPer], pv[kPsPer];
     bool sel[kPsPer];
-    ps_keys<PRED, L2, F8>(p, prog, in, tl, c0, key, pv, sel);
+    uint32_t nb[kPsPer];
+    ps_keys<PRED, L2, F8, NUL>(p, prog, in, tl, c0, key, pv, sel, nb);
     __syncthreads();
     const uint64_t lt = (1ull << lane) - 1;
     const uint32_t mask = (uint32_t)P - 1;
     uint32_t rk[kPsPer];  // rank | digit << 16 (then the LDS slot); ~0: not selected
 #pragma unroll
     for (int k = 0; k < kPsPer; ++k) {
-        const uint32_t d = (uint32_t)(part_hash(key[k]) >> g.sh) & mask;
+        const int64_t r = tl.base + c0 + k * 64 + lane;
+        const uint64_t hh = NUL ? ps_hash(key[k], nb[k], r) : part_hash(key[k]);
+        const uint32_t d = (uint32_t)(hh >> g.sh) & mask;
         uint64_t peers = __ballot(sel[k]);
 #pragma unroll
         for (int b = 0; b < kPsDigitBits; ++b) {
@@ -300,12 +331,16 @@ __global__ __launch_bounds__(kPsThreads) void gbp_scatter_kernel(GbParams p, Dev
         sdig[pos] = (uint8_t)d;
         rk[k] = pos;
     }
-    const int ncols = 1 + p.nacc + (o.rows ? 1 : 0);
+    // columns: key 0, aggregated 1 .. nacc, then row ids (if kept), then
+    // null bits (NUL, if kept)
+    const int rows_col = o.rows ? p.nacc + 1 : -1;
+    const int nulls_col = NUL && o.nulls ? p.nacc + 1 + (o.rows ? 1 : 0) : -1;
+    const int ncols = 1 + p.nacc + (o.rows ? 1 : 0) + (nulls_col >= 0 ? 1 : 0);
     // column order: the key, then the predicate's column when it is an
     // aggregated one (its registers die first), then the rest
     const int pa = (!L2 && PRED == 1) ? p.pred_acc : -1;
     auto col_at = [&](int i) -> int {
-        if (pa < 0 || i == 0) return i;
+        if (pa < 0 || i == 0 || i > p.nacc) return i;
         if (i == 1) return pa + 1;
         return i - 1 <= pa ? i - 1 : i;
     };
@@ -323,9 +358,12 @@ __global__ __launch_bounds__(kPsThreads) void gbp_scatter_kernel(GbParams p, Dev
         if (ci + 1 < ncols) {
             const int nc = col_at(ci + 1);
             const int a = nc - 1;
-            const bool rows = nc > p.nacc;
-            const bool use_pv = !L2 && PRED == 1 && !rows && a == p.pred_acc;
-            if (use_pv) {
+            const bool rows = nc == rows_col;
+            const bool use_pv = !L2 && PRED == 1 && nc <= p.nacc && a == p.pred_acc;
+            if (nc == nulls_col) {
+#pragma unroll
+                for (int k = 0; k < kPsPer; ++k) cv[k] = nb[k];
+            } else if (use_pv) {
 #pragma unroll
                 for (int k = 0; k < kPsPer; ++k) cv[k] = pv[k];
             } else if (rows && L2) {
@@ -342,6 +380,11 @@ __global__ __launch_bounds__(kPsThreads) void gbp_scatter_kernel(GbParams p, Dev
             for (int q = tid; q < (int)m; q += kPsThreads) {
                 const uint64_t pos = gbase[sdig[q]] + (uint64_t)q;
                 if (gb_ok(pos < (uint64_t)o.cap, CK_PART_POS)) dst[pos] = sval[q];
+            }
+        } else if (col == nulls_col) {
+            for (int q = tid; q < (int)m; q += kPsThreads) {
+                const uint64_t pos = gbase[sdig[q]] + (uint64_t)q;
+                if (gb_ok(pos < (uint64_t)o.cap, CK_PART_POS)) o.nulls[pos] = (uint8_t)sval[q];
             }
         } else {
             for (int q = tid; q < (int)m; q += kPsThreads) {
@@ -1497,6 +1540,18 @@ static hipError_t launch_main(const Plan& pl, const DevProgram& dp, hipStream_t 
 }
 
 static hipError_t launch_fast_dispatch(const Plan& pl, const DevProgram& dp, int pred, hipStream_t s) {
+    if (pl.nulls) {
+        // validity bitmaps on the key, aggregated or predicate columns
+        switch (pl.p.nacc) {
+        case 0: return launch_fast_nulls<0>(pl, dp, pred, s);
+        case 1: return launch_fast_nulls<1>(pl, dp, pred, s);
+        case 2: return launch_fast_nulls<2>(pl, dp, pred, s);
+        case 3: return launch_fast_nulls<3>(pl, dp, pred, s);
+        case 4: return launch_fast_nulls<4>(pl, dp, pred, s);
+        case 5: return launch_fast_nulls<5>(pl, dp, pred, s);
+        default: return launch_fast_nulls<6>(pl, dp, pred, s);
+        }
+    }
     bool dv = false;
     for (int a = 0; a < pl.p.nacc; ++a) dv = dv || pl.p.acc[a].dop != DOP_NONE;
     if (pl.p.kp.n > 0) {
@@ -1678,6 +1733,7 @@ struct GbRun {
     uint64_t* prange = nullptr;              // scan of the count matrix + partition bounds
     const uint64_t* part_range = nullptr;    // P + 1 partition boundaries (inside prange)
     int64_t part_rows_total = 0;
+    std::vector<uint64_t> part_hrange;       // host copy of the P + 1 bounds
     PartOut pout;
     // aggregation inputs: the predicate's columns, the derived inputs and
     // the columns materialised for them (owned)
@@ -2143,8 +2199,10 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
     // fast path eligibility: no nulls, 8-byte columns
     // at even offsets of 16-byte aligned buffers, simple or no predicate,
     // LDS table in use
+    // (validity bitmaps allowed: the NULLS variant reads one validity byte
+    // per row pair and column beside the values; plain inputs only)
     auto ok = [](const DevCol& c) {
-        return (c.dtype == PLGPU_I64 || c.dtype == PLGPU_F64) && c.validity == nullptr && (c.offset & 1) == 0 &&
+        return (c.dtype == PLGPU_I64 || c.dtype == PLGPU_F64) && (c.offset & 1) == 0 &&
                ((uintptr_t)c.values & 15) == 0;
     };
     auto ok_kp = [](const KeyPack& k) {
@@ -2166,7 +2224,20 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
         if (p.acc[a].dop != DOP_NONE && !(p.acc[a].dop & DOP_LIT)) fast = fast && ok(p.acc[a].c2);
     }
     if (R.pred == 1 && p.pred_acc < 0) fast = fast && ok(p.pred_col);
-    if (gpath == 0 || gpath == 1 || gpath == 3) fast = false;
+    {
+        bool nul = p.key.validity != nullptr || (R.pred == 1 && p.pred_col.validity != nullptr);
+        bool dv = false;
+        for (int a = 0; a < p.nacc; ++a) {
+            nul = nul || p.acc[a].c.validity != nullptr || p.acc[a].c2.validity != nullptr;
+            dv = dv || p.acc[a].dop != DOP_NONE;
+        }
+        // nullable inputs: the NULLS variant takes plain inputs and a key
+        // column (derived operands or a packed key take the generic kernel /
+        // the code column)
+        if (nul && (p.kp.n > 0 || dv)) fast = false;
+        pl.nulls = nul;
+    }
+    if (gpath == 0 || gpath == 1 || gpath == 3 || gpath == 5) fast = false;
     if (pl.local && !fast) {
         // the generic kernel walks the rows grid-strided: no range-local table
         pl.local = pl.use_lds = false;
@@ -2215,15 +2286,18 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
     // tile, or off the fast path, the generic kernel takes them all
     p.row_begin = p.n_full > 0 ? n : 0;
     // partitioned path: too many groups for one LDS table, but few enough
-    // that 2^kPartMaxBits partitions of LDS tables hold them; key and
-    // aggregated columns null-free (they are copied as raw words); the
-    // u32 count matrix and row ids bound n below 2^32
+    // that 2^kPartMaxBits partitions of LDS tables hold them; the key and
+    // aggregated columns are copied as raw words (their null bits beside
+    // them); the u32 count matrix and row ids bound n below 2^32
     R.part = false;
     // (a keyless reduction has no key column to partition by)
+    // (validity bitmaps travel with the rows as the null-bits column)
     bool part_ok = n > 0 && n < 0xFFFFFFFFll && R.est_groups > 0 && p.key.values != nullptr &&
-                   p.key.validity == nullptr;
-    for (int a = 0; a < p.nacc; ++a) part_ok = part_ok && p.acc[a].c.validity == nullptr;
-    if (part_ok && ((gpath < 0 && !pl.use_lds && n >= (int64_t(1) << 20)) || gpath == 3)) {
+                   p.key.dtype != PLGPU_STR;
+    // gb_path 5 (tests): the partitioned path with the checks above skipped,
+    // so that the partition launchers' own preconditions must refuse
+    if (gpath == 5) part_ok = true;
+    if (part_ok && ((gpath < 0 && !pl.use_lds && n >= (int64_t(1) << 20)) || gpath == 3 || gpath == 5)) {
         // LDS table of the partition workgroups: two per CU, or one when
         // 2^kPartMaxBits partitions of the smaller table are not enough
         const int64_t want = R.est_groups + (R.est_groups >> 3);
@@ -2274,7 +2348,7 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
 // Scatter the selected rows into the hash partitions (once per run; the
 // attempts of gb_main reuse them): one pass of 2^pbits digits, or two
 // (level 1 over the input rows, level 2 within each level-1 partition).
-template <int PRED, bool L2, bool F8>
+template <int PRED, bool L2, bool F8, bool NUL = false>
 static hipError_t gbp_pass(const GbRun& R, const PsGeom& g, const PartOut& in, uint32_t* cnt, uint64_t* part,
                            bool scatter, const PartOut& out) {
     hipStream_t s = R.s;
@@ -2282,7 +2356,7 @@ static hipError_t gbp_pass(const GbRun& R, const PsGeom& g, const PartOut& in, u
     if (!scatter) {
         {
             KtScope kt("gbp_count_kernel", s);
-            gbp_count_kernel<PRED, L2, F8><<<grid, kPsThreads, 0, s>>>(R.pl.p, R.dp, g, in, cnt);
+            gbp_count_kernel<PRED, L2, F8, NUL><<<grid, kPsThreads, 0, s>>>(R.pl.p, R.dp, g, in, cnt);
         }
         hipError_t e = hipGetLastError();
         if (e == hipSuccess) e = scan_exclusive32_inplace(cnt, g.ntiles << g.dbits, part, s);
@@ -2290,38 +2364,47 @@ static hipError_t gbp_pass(const GbRun& R, const PsGeom& g, const PartOut& in, u
     }
     {
         KtScope kt("gbp_scatter_kernel", s);
-        gbp_scatter_kernel<PRED, L2, F8><<<grid, kPsThreads, 0, s>>>(R.pl.p, R.dp, g, in, cnt, out);
+        gbp_scatter_kernel<PRED, L2, F8, NUL><<<grid, kPsThreads, 0, s>>>(R.pl.p, R.dp, g, in, cnt, out);
     }
     return hipGetLastError();
 }
 
-static hipError_t gbp_pass1(const GbRun& R, bool f8, const PsGeom& g, uint32_t* cnt, uint64_t* part, bool scatter,
-                            const PartOut& out) {
+template <bool NUL>
+static hipError_t gbp_pass1_nul(const GbRun& R, bool f8, const PsGeom& g, uint32_t* cnt, uint64_t* part,
+                                bool scatter, const PartOut& out) {
     PartOut none;
     std::memset(&none, 0, sizeof none);
-    if (f8 && R.pred == 0) return gbp_pass<0, false, true>(R, g, none, cnt, part, scatter, out);
-    if (f8 && R.pred == 1) return gbp_pass<1, false, true>(R, g, none, cnt, part, scatter, out);
+    if (f8 && R.pred == 0) return gbp_pass<0, false, true, NUL>(R, g, none, cnt, part, scatter, out);
+    if (f8 && R.pred == 1) return gbp_pass<1, false, true, NUL>(R, g, none, cnt, part, scatter, out);
     switch (R.pred) {
-    case 0: return gbp_pass<0, false, false>(R, g, none, cnt, part, scatter, out);
-    case 1: return gbp_pass<1, false, false>(R, g, none, cnt, part, scatter, out);
-    default: return gbp_pass<2, false, false>(R, g, none, cnt, part, scatter, out);
+    case 0: return gbp_pass<0, false, false, NUL>(R, g, none, cnt, part, scatter, out);
+    case 1: return gbp_pass<1, false, false, NUL>(R, g, none, cnt, part, scatter, out);
+    default: return gbp_pass<2, false, false, NUL>(R, g, none, cnt, part, scatter, out);
     }
 }
+static hipError_t gbp_pass1(const GbRun& R, bool f8, bool nul, const PsGeom& g, uint32_t* cnt, uint64_t* part,
+                            bool scatter, const PartOut& out) {
+    return nul ? gbp_pass1_nul<true>(R, f8, g, cnt, part, scatter, out)
+               : gbp_pass1_nul<false>(R, f8, g, cnt, part, scatter, out);
+}
 
-// Partition buffers for `rows` selected rows: key, nacc columns, row ids.
-static int gbp_alloc(GbRun& R, int64_t sel, uint64_t** buf, PartOut* o) {
+// Partition buffers for `rows` selected rows: key, nacc columns, row ids,
+// null bits (nul).
+static int gbp_alloc(GbRun& R, int64_t sel, bool nul, uint64_t** buf, PartOut* o) {
     const GbParams& p = R.pl.p;
     // a multiple of 16 rows, so every column's buffer starts on a 128-B line
     // (pair loads; the level-2 tiles' aligned block loads)
     const int64_t rows = ((int64_t)std::max<int64_t>(sel, 2) + 17) & ~int64_t(15);
     const bool want_rows = p.f_first >= 0 || p.f_last >= 0;
-    const size_t words = (size_t)rows * (1 + p.nacc) + (want_rows ? ((size_t)rows + 1) / 2 : 0);
+    const size_t rwords = want_rows ? ((size_t)rows + 1) / 2 : 0;
+    const size_t words = (size_t)rows * (1 + p.nacc) + rwords + (nul ? ((size_t)rows + 7) / 8 : 0);
     int rc = dev_alloc((void**)buf, words * 8, R.s);
     if (rc) return rc;
     std::memset(o, 0, sizeof *o);
     o->key = *buf;
     for (int a = 0; a < p.nacc; ++a) o->acc[a] = *buf + (size_t)rows * (1 + a);
     o->rows = want_rows ? (uint32_t*)(*buf + (size_t)rows * (1 + p.nacc)) : nullptr;
+    o->nulls = nul ? (uint8_t*)(*buf + (size_t)rows * (1 + p.nacc) + rwords) : nullptr;
     o->cap = rows;
     return PLGPU_OK;
 }
@@ -2329,15 +2412,27 @@ static int gbp_alloc(GbRun& R, int64_t sel, uint64_t** buf, PartOut* o) {
 static int gb_partition(GbRun& R) {
     GbParams& p = R.pl.p;
     hipStream_t s = R.s;
+    // the count / scatter kernels read the key column at every row and copy
+    // the key and aggregated columns as raw words: a keyless reduction must
+    // never reach them (the plan refuses it; this holds for every caller)
+    if (p.key.values == nullptr || p.key.dtype == PLGPU_STR || p.n <= 0 || p.n >= 0xFFFFFFFFll)
+        return fail(PLGPU_ERR_INVALID, "partitioned group-by: needs a key column and 1 .. 2^32 - 1 rows");
+    for (int a = 0; a < p.nacc; ++a)
+        if (p.acc[a].c.values == nullptr)
+            return fail(PLGPU_ERR_INVALID, "partitioned group-by: an aggregated column without values");
     const int B = R.pbits;
     const int lv = options().part_levels;
     const bool two = B >= 2 && (B > kPartOneLevel || lv == 2) && !(lv == 1 && B <= kPartOneLevel);
     const int b1 = two ? B / 2 : B, b2 = B - b1;
     const int P1 = 1 << b1, P = 1 << B;
-    // the fast forms: null-free 8-byte key, aggregated and predicate columns
-    auto c8 = [](const DevCol& c) { return c.validity == nullptr && dtype_bytes(c.dtype) == 8 && c.dtype != PLGPU_STR; };
+    // the fast forms: 8-byte key, aggregated and predicate columns (plain
+    // loads); nul: some of them has a validity bitmap (its bits travel with
+    // the rows as the null-bits column)
+    auto c8 = [](const DevCol& c) { return dtype_bytes(c.dtype) == 8 && c.dtype != PLGPU_STR; };
     bool f8 = c8(p.key) && R.pred <= 1 && (R.pred == 0 || c8(p.pred_col));
     for (int a = 0; a < p.nacc; ++a) f8 = f8 && c8(p.acc[a].c);
+    bool nul = p.key.validity != nullptr || (R.pred == 1 && p.pred_col.validity != nullptr);
+    for (int a = 0; a < p.nacc; ++a) nul = nul || p.acc[a].c.validity != nullptr;
     PsGeom g1;
     std::memset(&g1, 0, sizeof g1);
     g1.n = p.n;
@@ -2355,7 +2450,7 @@ static int gb_partition(GbRun& R) {
     if (!rc) rc = dev_alloc((void**)&part, (size_t)((ncnt1 + kScanChunk - 1) / kScanChunk + 2) * 8, s);
     std::vector<uint64_t> hr1((size_t)P1 + 1);
     if (!rc) {
-        hipError_t e = gbp_pass1(R, f8, g1, cnt, part, false, R.pout);
+        hipError_t e = gbp_pass1(R, f8, nul, g1, cnt, part, false, R.pout);
         const int64_t nb = std::max<int64_t>(1, (ncnt1 + kScanChunk - 1) / kScanChunk);
         if (e == hipSuccess) {
             gbp_bounds_kernel<<<(P1 + 256) / 256, 256, 0, s>>>(cnt, part + nb, P1, g1.ntiles, range1);
@@ -2367,9 +2462,9 @@ static int gb_partition(GbRun& R) {
     }
     uint64_t* buf1 = nullptr;
     PartOut out1;
-    if (!rc) rc = gbp_alloc(R, (int64_t)hr1[P1], &buf1, &out1);
+    if (!rc) rc = gbp_alloc(R, (int64_t)hr1[P1], nul, &buf1, &out1);
     if (!rc) {
-        const hipError_t e = gbp_pass1(R, f8, g1, cnt, part, true, out1);
+        const hipError_t e = gbp_pass1(R, f8, nul, g1, cnt, part, true, out1);
         if (e != hipSuccess) rc = hip_fail(e, "gbp_scatter_kernel");
     }
     dev_free(cnt, s);
@@ -2416,7 +2511,9 @@ static int gb_partition(GbRun& R) {
                     meta, P1, g2.ntiles, meta + P1 + 1);
                 e = hipGetLastError();
             }
-            if (e == hipSuccess && g2.ntiles > 0) e = gbp_pass<0, true, true>(R, g2, out1, cnt, part, false, out1);
+            if (e == hipSuccess && g2.ntiles > 0)
+                e = nul ? gbp_pass<0, true, true, true>(R, g2, out1, cnt, part, false, out1)
+                        : gbp_pass<0, true, true>(R, g2, out1, cnt, part, false, out1);
             if (e == hipSuccess) {
                 gbp_bounds2_kernel<<<(P + 256) / 256, 256, 0, s>>>(cnt, range1, meta, P1, b2, range);
                 e = hipGetLastError();
@@ -2425,9 +2522,10 @@ static int gb_partition(GbRun& R) {
             if (e == hipSuccess) e = hipStreamSynchronize(s);
             if (e != hipSuccess) rc = hip_fail(e, "gbp_count_kernel (level 2)");
         }
-        if (!rc) rc = gbp_alloc(R, (int64_t)hr[P], &R.pbuf, &R.pout);
+        if (!rc) rc = gbp_alloc(R, (int64_t)hr[P], nul, &R.pbuf, &R.pout);
         if (!rc && g2.ntiles > 0) {
-            const hipError_t e = gbp_pass<0, true, true>(R, g2, out1, cnt, part, true, R.pout);
+            const hipError_t e = nul ? gbp_pass<0, true, true, true>(R, g2, out1, cnt, part, true, R.pout)
+                                     : gbp_pass<0, true, true>(R, g2, out1, cnt, part, true, R.pout);
             if (e != hipSuccess) rc = hip_fail(e, "gbp_scatter_kernel (level 2)");
         }
         dev_free(cnt, s);
@@ -2438,6 +2536,7 @@ static int gb_partition(GbRun& R) {
     }
     uint64_t maxpart = 0;
     for (int q = 0; q < P; ++q) maxpart = std::max<uint64_t>(maxpart, hr[q + 1] - hr[q]);
+    R.part_hrange = hr;
     R.part_rows_total = (int64_t)hr[P];
     R.part_range = range;
     R.part_levels = two ? 2 : 1;
@@ -2454,6 +2553,45 @@ static int gb_partition(GbRun& R) {
         R.rbits = R.part_lbits;
         R.gbits = R.pbits + R.part_lbits;
     }
+    return PLGPU_OK;
+}
+
+// The partition passes of the many-groups path, reused by the join's
+// partitioned probe (join.hip jn_radix_take): every row selected, the key
+// and up to kMaxAcc carried columns scattered as raw 8-byte words.
+int radix_partition8(const DevCol& key, const DevCol* cols, int ncols, int64_t n, int bits, hipStream_t s,
+                     RadixParts* out) {
+    if (ncols < 0 || ncols > kMaxAcc || bits < 0 || bits > kPartMaxBits || n <= 0 || n >= 0xFFFFFFFFll)
+        return fail(PLGPU_ERR_INVALID, "radix partition: 0..6 columns, 0..16 bits, 1 .. 2^32 - 1 rows");
+    auto c8 = [](const DevCol& c) {
+        return c.values != nullptr && c.validity == nullptr && dtype_bytes(c.dtype) == 8 && c.dtype != PLGPU_STR;
+    };
+    if (!c8(key)) return fail(PLGPU_ERR_INVALID, "radix partition: null-free 8-byte columns");
+    for (int i = 0; i < ncols; ++i)
+        if (!c8(cols[i])) return fail(PLGPU_ERR_INVALID, "radix partition: null-free 8-byte columns");
+    GbRun R;
+    R.s = s;
+    GbParams& p = R.pl.p;
+    std::memset(&p, 0, sizeof p);
+    p.key = key;
+    p.n = n;
+    p.nacc = ncols;
+    for (int i = 0; i < ncols; ++i) p.acc[i].c = cols[i];
+    p.pred_acc = -1;
+    p.f_first = p.f_last = -1;
+    R.pred = 0;
+    R.pbits = bits;
+    const int rc = gb_partition(R);
+    if (rc) return rc;
+    out->buf = R.pbuf;
+    out->key = R.pout.key;
+    for (int i = 0; i < ncols; ++i) out->col[i] = R.pout.acc[i];
+    out->range = R.prange;
+    out->bounds = R.part_range;
+    out->hrange = R.part_hrange;
+    out->levels = R.part_levels;
+    R.pbuf = nullptr;  // owned by the caller now
+    R.prange = nullptr;
     return PLGPU_OK;
 }
 
@@ -2477,6 +2615,7 @@ static hipError_t launch_partitioned(const GbRun& R) {
     q.n_full = 0;
     q.part_range = R.part_range;
     q.part_rows = R.pout.rows;
+    q.part_nulls = R.pout.nulls;
     q.part_blocks = R.part_blocks;
     q.lbits = R.part_lbits;
     q.lcap = 1 << R.part_lbits;

@@ -11,4 +11,6 @@ template hipError_t launch_fast_nacc<1, false, 1>(const Plan&, const DevProgram&
 template hipError_t launch_fast_nacc<1, true, 0>(const Plan&, const DevProgram&, int, hipStream_t);
 template hipError_t launch_fast_nacc<1, false, 2>(const Plan&, const DevProgram&, int, hipStream_t);
 template hipError_t launch_part_fast_limbs<1>(const Plan&, int, hipStream_t);
+template hipError_t launch_fast_nulls<0>(const Plan&, const DevProgram&, int, hipStream_t);
+template hipError_t launch_fast_nulls<1>(const Plan&, const DevProgram&, int, hipStream_t);
 }  // namespace plgpu

@@ -13,4 +13,5 @@ template hipError_t launch_fast_pair<0, 2>(const Plan&, const DevProgram&, hipSt
 template hipError_t launch_fast_pair<1, 2>(const Plan&, const DevProgram&, hipStream_t);
 template hipError_t launch_fast_pair<0, 3>(const Plan&, const DevProgram&, hipStream_t);
 template hipError_t launch_fast_pair<1, 3>(const Plan&, const DevProgram&, hipStream_t);
+template hipError_t launch_fast_nulls<2>(const Plan&, const DevProgram&, int, hipStream_t);
 }  // namespace plgpu

@@ -11,4 +11,5 @@ template hipError_t launch_fast_nacc<3, false, 2>(const Plan&, const DevProgram&
 template hipError_t launch_part_fast_limbs<3>(const Plan&, int, hipStream_t);
 template hipError_t launch_fast_var<0>(const Plan&, const DevProgram&, hipStream_t);
 template hipError_t launch_fast_var<1>(const Plan&, const DevProgram&, hipStream_t);
+template hipError_t launch_fast_nulls<3>(const Plan&, const DevProgram&, int, hipStream_t);
 }  // namespace plgpu

@@ -9,4 +9,5 @@ template hipError_t launch_fast_nacc<4, false, 1>(const Plan&, const DevProgram&
 template hipError_t launch_fast_nacc<4, true, 0>(const Plan&, const DevProgram&, int, hipStream_t);
 template hipError_t launch_fast_nacc<4, false, 2>(const Plan&, const DevProgram&, int, hipStream_t);
 template hipError_t launch_part_fast_limbs<4>(const Plan&, int, hipStream_t);
+template hipError_t launch_fast_nulls<4>(const Plan&, const DevProgram&, int, hipStream_t);
 }  // namespace plgpu

@@ -166,6 +166,10 @@ struct GbParams {
     // part_rows maps them back to input rows (first-row field)
     const uint64_t* part_range;
     const uint32_t* part_rows;
+    // null bits of each partitioned row (null unless an input column has a
+    // validity bitmap): bit a = acc a's value is null, bit 6 = the key is
+    // null (the row belongs to the null group)
+    const uint8_t* part_nulls;
     int32_t part_blocks;
     // fast kernel, range-local mode (clustered keys): workgroup b takes the
     // contiguous tiles [b * tiles_per_wg, (b + 1) * tiles_per_wg); 0 = the
@@ -339,9 +343,7 @@ __device__ __forceinline__ int lds_find(uint64_t* lkeys, int lbits, int lcap, ui
     return -1;
 }
 
-// Partition hash of the many-groups path (its top bits pick the partition;
-// independent of the table hashes, which multiply by the golden ratio).
-__device__ __forceinline__ uint64_t part_hash(uint64_t key) { return mk_fmix(key ^ 0x2545F4914F6CDD1Dull); }
+// (part_hash, the many-groups path's partition hash: tuplehash.hpp)
 
 // Probe i of `key` in the global table.  A partitioned run whose partitions
 // each have one workgroup (p.rbits > 0) keeps every partition's groups in a
@@ -840,10 +842,19 @@ __global__ __launch_bounds__(kGbThreads) void gb_kernel(GbParams p, DevProgram p
             vm[j] = 0;
             slot[j] = kNotSelected;
             if (sel) {
+                bool kval;
+                if (PART && p.part_nulls) {
+                    // the partition buffers' null bits (bit a: acc a, bit 6: key)
+                    const uint32_t nb = p.part_nulls[r];
+                    vm[j] = ((1u << nacc) - 1u) & ~nb;
+                    kval = !((nb >> 6) & 1u);
+                } else {
 #pragma unroll
-                for (int a = 0; a < kMaxAcc; ++a)
-                    if (a < nacc && dev_valid(p.acc[a].c, r)) vm[j] |= 1u << a;
-                if (!dev_valid(p.key, r)) slot[j] = USE_LDS ? p.lcap : kGlobalNull;
+                    for (int a = 0; a < kMaxAcc; ++a)
+                        if (a < nacc && dev_valid(p.acc[a].c, r)) vm[j] |= 1u << a;
+                    kval = dev_valid(p.key, r);
+                }
+                if (!kval) slot[j] = USE_LDS ? p.lcap : kGlobalNull;
                 else if (USE_LDS && key[j] == kEmptyKey) slot[j] = p.lcap + 1;
                 else slot[j] = kGlobalKey;
             }
@@ -895,13 +906,17 @@ __global__ __launch_bounds__(kGbThreads) void gb_kernel(GbParams p, DevProgram p
 // PACK: the key is formed from up to kKpFast packed key columns (KeyPack),
 // whose raw words the tile holds until its rows are consumed.
 constexpr int kKpFast = 2;
-template <int NACC, int ROWS, bool DERIV = false, int PACK = 0>
+template <int NACC, int ROWS, bool DERIV = false, int PACK = 0, bool NUL = false>
 struct FastTile {
     uint64_t key[ROWS];
     uint64_t kr[PACK ? kKpFast : 1][ROWS];
     uint64_t v[NACC > 0 ? NACC : 1][ROWS];
     uint64_t w[DERIV && NACC > 0 ? NACC : 1][ROWS];  // DERIV: second operand columns
     uint64_t pv[ROWS];
+    // NUL: null bits of each row pair, row 2q in bits 0-7 and row 2q + 1 in
+    // bits 8-15 of nv[q] (the part_nulls layout: bit a acc a, 6 the key, 7
+    // the predicate's own column)
+    uint32_t nv[NUL ? (ROWS + 1) / 2 : 1];
 };
 
 // Row j of tile t for this thread: pairs of consecutive rows, pair q at
@@ -922,8 +937,9 @@ __device__ __forceinline__ u64x2_t ld16(const uint64_t* p) {
 // The rows after the last full tile (fewer than one tile): one more, masked
 // tile of guarded single-row loads (rows >= n read as 0 and are not
 // selected), so the fused kernel covers every row in one launch.
-template <int NACC, int PRED, int ROWS, bool DERIV, int PACK>
-__device__ __forceinline__ void fast_load_tail(const GbParams& p, int64_t t, FastTile<NACC, ROWS, DERIV, PACK>& x) {
+template <int NACC, int PRED, int ROWS, bool DERIV, int PACK, bool NUL = false>
+__device__ __forceinline__ void fast_load_tail(const GbParams& p, int64_t t,
+                                               FastTile<NACC, ROWS, DERIV, PACK, NUL>& x) {
     const int T = blockDim.x;
     const uint64_t* kp = (const uint64_t*)p.key.values + p.key.offset;
 #pragma unroll
@@ -956,8 +972,8 @@ __device__ __forceinline__ void fast_load_tail(const GbParams& p, int64_t t, Fas
 // clamped to it (the partitioned buffers end a pair after the last row).
 typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 
-template <int NACC, int PRED, int ROWS, bool NT, bool DERIV, int PACK>
-__device__ __forceinline__ void fast_load(const GbParams& p, int64_t t, FastTile<NACC, ROWS, DERIV, PACK>& x,
+template <int NACC, int PRED, int ROWS, bool NT, bool DERIV, int PACK, bool NUL = false>
+__device__ __forceinline__ void fast_load(const GbParams& p, int64_t t, FastTile<NACC, ROWS, DERIV, PACK, NUL>& x,
                                           int64_t rbase = 0, int64_t rmax = -1) {
     const int T = blockDim.x;
     const uint64_t* kp = (const uint64_t*)p.key.values + p.key.offset;
@@ -1027,13 +1043,57 @@ __device__ __forceinline__ void fast_load(const GbParams& p, int64_t t, FastTile
     }
 }
 
+// Null bits of rows r, r + 1 of a column (r and the column offset even, so
+// both bits sit in one validity byte): bit 0 row r, bit 1 row r + 1, set =
+// null; 0 without a bitmap.
+__device__ __forceinline__ uint32_t pair_nulls(const DevCol& c, int64_t r) {
+    if (!c.validity) return 0u;
+    const uint64_t b = (uint64_t)(c.offset + r);
+    const uint32_t byte = __builtin_nontemporal_load(c.validity + (b >> 3));
+    return ~(byte >> (b & 7)) & 3u;
+}
+
+// NUL: the tile's null bits (FastTile::nv), from the columns' validity
+// bitmaps (one byte per row pair and column) or, over the partition buffers
+// (PART), from part_nulls (two bytes per pair).  Rows past n (the masked tail
+// tile) read nothing.
+template <int NACC, int PRED, int ROWS, bool PART, bool DERIV, int PACK, bool NUL>
+__device__ __forceinline__ void fast_nulls(const GbParams& p, int64_t t, FastTile<NACC, ROWS, DERIV, PACK, NUL>& x,
+                                           int64_t rbase, int64_t rmax) {
+    if constexpr (NUL) {
+        const int T = blockDim.x;
+#pragma unroll
+        for (int q = 0; q < ROWS / 2; ++q) {
+            int64_t r = rbase + fast_row(t, T, ROWS, 2 * q);
+            if (rmax >= 0) r = r < rmax ? r : rmax;
+            uint32_t m = 0;
+            if (PART) {
+                if (p.part_nulls) m = __builtin_nontemporal_load((const uint16_t*)(p.part_nulls + r));
+            } else if (r < p.n) {
+#pragma unroll
+                for (int c = 0; c < NACC; ++c) {
+                    const uint32_t b = pair_nulls(p.acc[c].c, r);
+                    m |= ((b & 1u) << c) | ((b >> 1) << (8 + c));
+                }
+                const uint32_t bk = pair_nulls(p.key, r);
+                m |= ((bk & 1u) << 6) | ((bk >> 1) << 14);
+                if (PRED == 1 && p.pred_acc < 0) {
+                    const uint32_t bp = pair_nulls(p.pred_col, r);
+                    m |= ((bp & 1u) << 7) | ((bp >> 1) << 15);
+                }
+            }
+            x.nv[q] = m;
+        }
+    }
+}
+
 // DERIV: fill the operand registers whose column another acc loaded
 // (v_from / w_from, uniform), once the tile's loads are being consumed --
 // not at prefetch time, where the copy would wait for the loads.
-template <int NACC, int ROWS, bool DERIV, int PACK>
+template <int NACC, int ROWS, bool DERIV, int PACK, bool NUL = false>
 __device__ __forceinline__ void fast_share(const int32_t (&vf)[NACC > 0 ? NACC : 1],
                                            const int32_t (&wf)[NACC > 0 ? NACC : 1],
-                                           FastTile<NACC, ROWS, DERIV, PACK>& x) {
+                                           FastTile<NACC, ROWS, DERIV, PACK, NUL>& x) {
     if (!DERIV) return;
 #pragma unroll
     for (int c = 0; c < NACC; ++c)
@@ -1075,11 +1135,18 @@ __device__ __forceinline__ void fast_share(const int32_t (&vf)[NACC > 0 ? NACC :
 // one workgroup per partition and LDS table, more waves share the table;
 // the register-run variant keeps kGbThreads, its registers would spill)
 constexpr int kGbPartThreads = 1024;
+// NULLS: key, aggregated and predicate columns may carry validity bitmaps
+// (or, with PART, the partition buffers' part_nulls bytes): a null
+// aggregated value takes no part in its acc (a sum adds nothing, counts /
+// min / max skip it), a null key row joins the null group (LDS slot lcap ->
+// global slot gcap), a null predicate value drops the row.  Bits travel
+// with each tile (FastTile::nv: one byte per row pair and column read).
 template <int NACC, int PRED, bool SUMONLY, int ROWS, int LIMBS = 3, bool RUNS = false, bool PART = false,
-          bool DERIV = false, int VAR = 0, int PACK = 0>
+          bool DERIV = false, int VAR = 0, int PACK = 0, bool NULLS = false>
 __global__ __launch_bounds__(PART && !RUNS ? kGbPartThreads : kGbThreads) void gb_fast_kernel(GbParams p,
                                                                                                DevProgram prog) {
     static_assert(!PACK || !PART, "PACK: the single-table kernel");
+    static_assert(!NULLS || (!RUNS && !DERIV && VAR == 0 && PACK == 0), "NULLS: plain inputs");
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
     constexpr int NA = NACC > 0 ? NACC : 1;
     // VAR 1 (sum-only, NACC 3): the fused variance's three sums of one column
@@ -1095,7 +1162,7 @@ __global__ __launch_bounds__(PART && !RUNS ? kGbPartThreads : kGbThreads) void g
     // need no sign either (launch_fast_var)
     constexpr bool TRIPLE = VAR == 1 || VAR == 4;
     static_assert(!TRIPLE || (NACC == 3 && !DERIV), "VAR 1 / 4: three sums of one column");
-    static_assert(VAR != 2 && VAR != 3 || (NACC == 2 && !DERIV), "VAR 2 / 3: a product and its operand");
+    static_assert((VAR != 2 && VAR != 3) || (NACC == 2 && !DERIV), "VAR 2 / 3: a product and its operand");
     // VAR 5 (sum-only, plain inputs): the last acc's column is the fused
     // predicate's and keeps no value below a literal >= 0, so its limbs need
     // no sign (the headline's close.sum() under close > 250)
@@ -1164,10 +1231,13 @@ __global__ __launch_bounds__(PART && !RUNS ? kGbPartThreads : kGbThreads) void g
         t = blockIdx.x % p.part_blocks;
         tstep = p.part_blocks;
     }
-    auto load_tile = [&](int64_t tt, FastTile<NL, ROWS, DERIV, PACK>& x) {
-        if (PART || tt < ntiles) fast_load<NL, PRED, ROWS, true, DERIV, PACK>(p, tt, x, rbase, rmax);
-        else fast_load_tail<NL, PRED, ROWS, DERIV, PACK>(p, tt, x);
+    auto load_tile = [&](int64_t tt, FastTile<NL, ROWS, DERIV, PACK, NULLS>& x) {
+        if (PART || tt < ntiles) fast_load<NL, PRED, ROWS, true, DERIV, PACK, NULLS>(p, tt, x, rbase, rmax);
+        else fast_load_tail<NL, PRED, ROWS, DERIV, PACK, NULLS>(p, tt, x);
+        fast_nulls<NL, PRED, ROWS, PART, DERIV, PACK, NULLS>(p, tt, x, rbase, rmax);
     };
+    // NULLS: the null bit of the predicate's column (its acc's, or its own)
+    const int pbit = p.pred_acc >= 0 ? p.pred_acc : 7;
     // PACK: the plan's fields as uniform constants, hoisted.  Field i of a
     // raw word w: an 8-byte column's w - base (mode 0); a 4-byte column's
     // (w ^ x32) - b32 on 32 bits (mode 1), or widened, ((w & kpm) ^ kpx) -
@@ -1319,10 +1389,10 @@ __global__ __launch_bounds__(PART && !RUNS ? kGbPartThreads : kGbThreads) void g
         }
         return true;
     };
-    FastTile<NL, ROWS, DERIV, PACK> cur;
+    FastTile<NL, ROWS, DERIV, PACK, NULLS> cur;
     if (t < nall) load_tile(t, cur);
     for (; t < nall; t += tstep) {
-        if constexpr (!VAR) fast_share<NACC, ROWS, DERIV, PACK>(vf0, wf0, cur);
+        if constexpr (!VAR) fast_share<NACC, ROWS, DERIV, PACK, NULLS>(vf0, wf0, cur);
         bool kout[ROWS];
         constexpr bool kstr = PACK == 2;
         if (kstr) {
@@ -1386,8 +1456,10 @@ __global__ __launch_bounds__(PART && !RUNS ? kGbPartThreads : kGbThreads) void g
         int slot[ROWS];
         uint64_t probe[ROWS];
         uint32_t h[ROWS];
+        uint32_t nrw[ROWS];  // NULLS: the row's null bits
 #pragma unroll
         for (int j = 0; j < ROWS; ++j) {
+            nrw[j] = NULLS ? (cur.nv[j >> 1] >> (8 * (j & 1))) & 0xFFu : 0u;
             bool sel = true;
             if (PRED == 1) {
                 uint64_t x = cur.pv[j];
@@ -1399,6 +1471,7 @@ __global__ __launch_bounds__(PART && !RUNS ? kGbPartThreads : kGbThreads) void g
                         if (a == p.pred_acc) x = cur.v[a][j];
                 }
                 sel = simple_pred(prog.simple_isf, prog.simple_op, x, prog.simple_imm);
+                if (NULLS) sel = sel && !((nrw[j] >> pbit) & 1u);
             }
             if (PART) {
                 const int64_t r = rbase + fast_row(t, T, ROWS, j);
@@ -1407,7 +1480,9 @@ __global__ __launch_bounds__(PART && !RUNS ? kGbPartThreads : kGbThreads) void g
                 sel = sel && fast_row(t, T, ROWS, j) < p.n;
             }
             if (PACK && sel && kout[j]) d.kbad = 1u;
-            slot[j] = sel ? (cur.key[j] == kEmptyKey ? p.lcap + 1 : kGlobalKey) : kNotSelected;
+            slot[j] = sel ? (NULLS && ((nrw[j] >> 6) & 1u) ? p.lcap
+                                                           : (cur.key[j] == kEmptyKey ? p.lcap + 1 : kGlobalKey))
+                          : kNotSelected;
             h[j] = hash_slot(cur.key[j], p.lbits);
             probe[j] = lds_load(&lds[h[j]]);
         }
@@ -1415,7 +1490,7 @@ __global__ __launch_bounds__(PART && !RUNS ? kGbPartThreads : kGbThreads) void g
         for (int j = 0; j < ROWS; ++j)
             if (slot[j] == kGlobalKey && probe[j] == cur.key[j]) slot[j] = (int)h[j];
         // ---- next tile's loads go out before this tile's atomics
-        FastTile<NL, ROWS, DERIV, PACK> nxt;
+        FastTile<NL, ROWS, DERIV, PACK, NULLS> nxt;
         const int64_t tn = t + tstep;
         if (tn < nall) load_tile(tn, nxt);
         // ---- apply rows one at a time (rolled; arrays shift statically)
@@ -1440,7 +1515,10 @@ __global__ __launch_bounds__(PART && !RUNS ? kGbPartThreads : kGbThreads) void g
                     }
                     dd[a] = dd0[a];
                     bot[a] = bot0[a];
+                    // a null value adds nothing to a sum-only layout's sums
+                    if (NULLS && SUMONLY && ((nrw[0] >> a) & 1u)) rv[a] = 0ull;
                 }
+                const uint32_t vm = NULLS ? VM & ~nrw[0] : VM;
                 if (s == kGlobalKey) s = lds_find(lds, p.lbits, p.lcap, cur.key[0]);
                 if (s >= 0 && !gb_ok(s < L, CK_FAST_SLOT)) s = -1;
                 bool held = false;
@@ -1548,15 +1626,16 @@ __global__ __launch_bounds__(PART && !RUNS ? kGbPartThreads : kGbThreads) void g
                         }
                     }
                 } else if (s >= 0) {
-                    if (!grun_take(s, r, rv)) apply_row<true, NA>(p, lds, L, s, r, rv, VM, dd, bot, NACC, d);
+                    if (!grun_take(s, r, rv)) apply_row<true, NA>(p, lds, L, s, r, rv, vm, dd, bot, NACC, d);
                 } else {
                     ++d.nglobal;
-                    global_row<NA>(p, cur.key[0], true, r, rv, VM, dd, bot, NACC, d);
+                    global_row<NA>(p, cur.key[0], true, r, rv, vm, dd, bot, NACC, d);
                 }
             }
 #pragma unroll
             for (int i = 0; i + 1 < ROWS; ++i) {
                 slot[i] = slot[i + 1];
+                nrw[i] = nrw[i + 1];
                 cur.key[i] = cur.key[i + 1];
 #pragma unroll
                 for (int a = 0; a < NL; ++a) {
@@ -1667,6 +1746,7 @@ struct Plan {
     bool runs;         // sampled keys mostly equal their next row's (sorted / clustered input)
     bool local;        // range-local mode: contiguous tiles per workgroup, LDS sized by range-local keys
     bool part_racc = false;  // partitioned path: register accumulators (clustered / sorted keys)
+    bool nulls = false;      // the fused kernel's NULLS variant (nullable key / values / predicate)
     mutable int launched_grid;  // grid of the last fast launch (info)
     mutable bool launched_runs = false;  // that launch used the register-run variant (info)
     mutable bool launched_var = false;   // that launch was the variance-triple variant (info)
@@ -1702,9 +1782,10 @@ inline void pair_normalize(GbParams& q, int pi, bool pred) {
 }
 
 template <int NACC, int PRED, bool SUMONLY, int LIMBS = 3, bool RUNS = false, bool DERIV = false, int VAR = 0,
-          int PACK = 0, int ROWS = 2>
+          int PACK = 0, int ROWS = 2, bool NULLS = false>
 hipError_t launch_fast_rows(const Plan& pl, const DevProgram& dp, hipStream_t s) {
-    const void* kern = (const void*)gb_fast_kernel<NACC, PRED, SUMONLY, ROWS, LIMBS, RUNS, false, DERIV, VAR, PACK>;
+    const void* kern =
+        (const void*)gb_fast_kernel<NACC, PRED, SUMONLY, ROWS, LIMBS, RUNS, false, DERIV, VAR, PACK, NULLS>;
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -1742,9 +1823,24 @@ hipError_t launch_fast_rows(const Plan& pl, const DevProgram& dp, hipStream_t s)
         q.tiles_per_wg = (int32_t)((nall + grid - 1) / grid);
     }
     KtScope kt("gb_fast_kernel", s);
-    gb_fast_kernel<NACC, PRED, SUMONLY, ROWS, LIMBS, RUNS, false, DERIV, VAR, PACK>
+    gb_fast_kernel<NACC, PRED, SUMONLY, ROWS, LIMBS, RUNS, false, DERIV, VAR, PACK, NULLS>
         <<<grid, kGbThreads, lds, s>>>(q, dp);
     return hipGetLastError();
+}
+
+// Nullable key / aggregated / predicate columns (gb_plan sends plain inputs
+// here: no derived operands, no packed key, no register runs): the sum-only
+// 2-limb layout, or the general one (3-limb sums, counts, min / max, first /
+// last rows).
+template <int NACC>
+hipError_t launch_fast_nulls(const Plan& pl, const DevProgram& dp, int pred, hipStream_t s) {
+    if constexpr (NACC > 0) {
+        if (pl.sum_only && pl.limbs == 2)
+            return pred == 0 ? launch_fast_rows<NACC, 0, true, 2, false, false, 0, 0, 2, true>(pl, dp, s)
+                             : launch_fast_rows<NACC, 1, true, 2, false, false, 0, 0, 2, true>(pl, dp, s);
+    }
+    return pred == 0 ? launch_fast_rows<NACC, 0, false, 3, false, false, 0, 0, 2, true>(pl, dp, s)
+                     : launch_fast_rows<NACC, 1, false, 3, false, false, 0, 0, 2, true>(pl, dp, s);
 }
 
 // x >= 0 (or NaN) on every row the fused predicate keeps: a float compare
@@ -1842,9 +1938,9 @@ hipError_t launch_fast_pair(const Plan& pl, const DevProgram& dp, hipStream_t s)
     return launch_fast_rows<2, PRED, true, 3, false, false, VAR>(pl, dp, s);
 }
 
-template <int NACC, int LIMBS, bool RACC>
+template <int NACC, int LIMBS, bool RACC, bool NULLS = false>
 hipError_t launch_part_fast(const Plan& pp, int grid, hipStream_t s) {
-    const void* kern = (const void*)gb_fast_kernel<NACC, 0, true, 2, LIMBS, RACC, true>;
+    const void* kern = (const void*)gb_fast_kernel<NACC, 0, true, 2, LIMBS, RACC, true, false, 0, 0, NULLS>;
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -1859,13 +1955,17 @@ hipError_t launch_part_fast(const Plan& pp, int grid, hipStream_t s) {
     const int64_t per_wg = pp.p.n / std::max(grid, 1);
     int threads = RACC || per_wg < 65536 ? kGbThreads : kGbPartThreads;
     if (!RACC && options().part_threads > 0) threads = std::min(kGbPartThreads, options().part_threads);
-    gb_fast_kernel<NACC, 0, true, 2, LIMBS, RACC, true><<<grid, threads, lds, s>>>(pp.p, none);
+    gb_fast_kernel<NACC, 0, true, 2, LIMBS, RACC, true, false, 0, 0, NULLS><<<grid, threads, lds, s>>>(pp.p, none);
     return hipGetLastError();
 }
 
 // register accumulators (RACC) on the 2-limb window, for clustered keys
 template <int NACC>
 hipError_t launch_part_fast_limbs(const Plan& pp, int grid, hipStream_t s) {
+    // nullable rows (the partition buffers' null bits): no register runs
+    if (pp.p.part_nulls)
+        return pp.limbs == 2 ? launch_part_fast<NACC, 2, false, true>(pp, grid, s)
+                             : launch_part_fast<NACC, 3, false, true>(pp, grid, s);
     if (pp.limbs != 2) return launch_part_fast<NACC, 3, false>(pp, grid, s);
     return pp.part_racc ? launch_part_fast<NACC, 2, true>(pp, grid, s) : launch_part_fast<NACC, 2, false>(pp, grid, s);
 }
@@ -1905,6 +2005,13 @@ extern template hipError_t launch_fast_nacc<6, false, 1>(const Plan&, const DevP
 extern template hipError_t launch_fast_nacc<6, true, 0>(const Plan&, const DevProgram&, int, hipStream_t);
 extern template hipError_t launch_fast_nacc<6, false, 2>(const Plan&, const DevProgram&, int, hipStream_t);
 extern template hipError_t launch_part_fast_limbs<6>(const Plan&, int, hipStream_t);
+extern template hipError_t launch_fast_nulls<0>(const Plan&, const DevProgram&, int, hipStream_t);
+extern template hipError_t launch_fast_nulls<1>(const Plan&, const DevProgram&, int, hipStream_t);
+extern template hipError_t launch_fast_nulls<2>(const Plan&, const DevProgram&, int, hipStream_t);
+extern template hipError_t launch_fast_nulls<3>(const Plan&, const DevProgram&, int, hipStream_t);
+extern template hipError_t launch_fast_nulls<4>(const Plan&, const DevProgram&, int, hipStream_t);
+extern template hipError_t launch_fast_nulls<5>(const Plan&, const DevProgram&, int, hipStream_t);
+extern template hipError_t launch_fast_nulls<6>(const Plan&, const DevProgram&, int, hipStream_t);
 extern template hipError_t launch_fast_var<0>(const Plan&, const DevProgram&, hipStream_t);
 extern template hipError_t launch_fast_var<1>(const Plan&, const DevProgram&, hipStream_t);
 extern template hipError_t launch_fast_pair<0, 2>(const Plan&, const DevProgram&, hipStream_t);

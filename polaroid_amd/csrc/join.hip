@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -1753,6 +1754,400 @@ static void jn_take_emit(const JnPass& pp, const TakeCols& lc, const TakePay& tp
                                                                            pp.ntiles, lc, out_idx);
 }
 
+// ------------------------------------------------ partitioned join (round 6)
+// The order-free inner join + take of BASELINE configs[3] (one unique-keyed
+// build payload, null-free 8-byte keys and columns) as a radix join, so that
+// every table read is served by an XCD's L2 instead of the ~55 G random
+// line requests/s of the HBM / Infinity-Cache-resident row-format table:
+//   1. the build keys go into P = 2^pbits sub-tables, one per partition
+//      (the top pbits bits of part_hash(key)), each nbk 64-B buckets of four
+//      16-B cells {key, payload} at load <= 1/2 (~1.25 MiB for 2^15 keys);
+//   2. the probe rows -- key and carried left columns as raw words -- are
+//      radix-partitioned by the same bits (radix_partition8: the group-by's
+//      count / scan / LDS-staged scatter), so a partition's rows meet only
+//      its own sub-table;
+//   3. the match pass (rj_match_kernel) walks the partitioned rows in
+//      4,096-row tiles, split into eight contiguous ranges, one per
+//      workgroup group (blockIdx % 8: the blocks one XCD receives), so an
+//      XCD probes one or two sub-tables at a time and holds them in its L2;
+//      four lanes read a probe row's home bucket together (one 64-B
+//      request); it writes the row-format join's intermediate layout (hit
+//      words, packed payloads, tile counts);
+//   4. the row-format join's scan and emit (jn_take_emit_kernel) place the
+//      rows: the key and carried columns come from the partition buffers,
+//      the payloads from the match pass.  Outputs are allocated at the exact
+//      result length; no atomics.
+// The rows come out in partition order: maintain_order = "none", the
+// reference's and this library's default.  The reference builds per-
+// partition tables the same way (polars-ops/src/frame/join/hash_join/
+// single_keys.rs:16 build_tables) and probes each partition's rows against
+// its own table (single_keys_inner.rs:40 probe_inner).
+constexpr int kMaxAccCarry = 6;                 // carried left columns besides the key (radix_partition8)
+constexpr int kRjGroups = 8;                    // workgroup groups (one XCD each)
+constexpr int kRjMaxBits = 12;                  // partitions <= 4,096
+
+struct RjTable {
+    const uint4* cells;  // P * nbk buckets of 4 cells {key lo, key hi, payload lo, payload hi}
+    uint32_t nbk;        // buckets per sub-table
+    int32_t pbits;
+};
+
+__device__ __forceinline__ uint32_t rj_part(uint64_t h, int pbits) {
+    return pbits ? (uint32_t)(h >> (64 - pbits)) : 0u;
+}
+// home bucket within the sub-table: the hash's low word scaled to nbk
+__device__ __forceinline__ uint32_t rj_bucket(uint64_t h, uint32_t nbk) {
+    return (uint32_t)(((uint64_t)(uint32_t)h * nbk) >> 32);
+}
+
+__global__ __launch_bounds__(256) void rj_count_kernel(DevCol bk, int64_t nb, int pbits, uint32_t* __restrict__ counts) {
+    __shared__ uint32_t h[1 << kRjMaxBits];
+    const int P = 1 << pbits;
+    for (int i = threadIdx.x; i < P; i += blockDim.x) h[i] = 0;
+    __syncthreads();
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nb; i += (int64_t)gridDim.x * blockDim.x)
+        atomicAdd(&h[rj_part(part_hash(dev_load(bk, i)), pbits)], 1u);
+    __syncthreads();
+    for (int i = threadIdx.x; i < P; i += blockDim.x)
+        if (h[i]) atomicAdd(&counts[i], h[i]);
+}
+
+__global__ __launch_bounds__(256) void rj_init_kernel(uint4* __restrict__ cells, int64_t ncells) {
+    const uint4 e = make_uint4((uint32_t)kEmptyKey, (uint32_t)(kEmptyKey >> 32), 0u, 0u);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ncells; i += (int64_t)gridDim.x * blockDim.x)
+        cells[i] = e;
+}
+
+// status[0]: a key found no free cell; [1]: a key met twice; [2]: an
+// INT64_MIN key (the empty marker).  The caller falls back for any.
+__global__ __launch_bounds__(256) void rj_build_kernel(DevCol bk, DevCol pay, int64_t nb, uint4* __restrict__ cells,
+                                                      uint32_t nbk, int pbits, unsigned long long* status) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nb; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t key = dev_load(bk, i);
+        if (key == kEmptyKey) {
+            atomicOr(&status[2], 1ull);
+            continue;
+        }
+        const uint64_t h = part_hash(key);
+        uint64_t* sub = (uint64_t*)(cells + (size_t)rj_part(h, pbits) * nbk * 4);
+        uint32_t b = rj_bucket(h, nbk);
+        bool placed = false;
+        for (uint32_t q = 0; q < nbk && !placed; ++q) {
+            for (int c = 0; c < 4; ++c) {
+                uint64_t* kp = sub + ((size_t)b * 4 + c) * 2;
+                uint64_t k = __hip_atomic_load(kp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (k == kEmptyKey) {
+                    k = atomicCAS((unsigned long long*)kp, (unsigned long long)kEmptyKey, (unsigned long long)key);
+                    if (k == kEmptyKey) {
+                        kp[1] = dev_load(pay, i);
+                        placed = true;
+                        break;
+                    }
+                }
+                if (k == key) {
+                    atomicOr(&status[1], 1ull);
+                    placed = true;
+                    break;
+                }
+            }
+            b = b + 1 == nbk ? 0u : b + 1;
+        }
+        if (!placed) atomicOr(&status[0], 1ull);
+    }
+}
+
+// The match pass of the partitioned probe, in the row-format join's
+// intermediate layout (jn_probe_match_kernel<.., INLINE>), so that its scan
+// and its emit (jn_take_emit_kernel) finish the join: per 64 partitioned rows
+// one hit word, the hits' payloads packed in hit order at the start of the
+// rows' 64-word segment of mp, and per 4,096-row tile its hit count.  Row r
+// of tile t is t * 4096 + k * 256 + tid (k = 0 .. 15).  The tiles are taken
+// in partitioned-row order within eight contiguous ranges, one per workgroup
+// group (blockIdx % 8: the blocks one XCD receives), so an XCD walks its
+// partitions in order and their sub-tables stay in its L2.  Each wave
+// probes cooperatively: in a step, lanes 4g .. 4g + 3 read the four cells of
+// row g's home bucket (one 64-B request per row), kRjBatch steps' reads in
+// flight together.  No atomics: the scan of the tile counts places the rows.
+template <int kRjBatch>
+__global__ __launch_bounds__(kJnThreads) void rj_match_kernel(const uint64_t* __restrict__ keys, int64_t np,
+                                                             int64_t ntiles, RjTable t, uint64_t* __restrict__ mwords,
+                                                             uint64_t* __restrict__ mp,
+                                                             uint64_t* __restrict__ tile_counts) {
+    constexpr int R = kJnTileRows / kJnThreads;      // 16 rows per thread
+    constexpr int NW = kJnThreads / 64;
+    constexpr int CB = kRjBatch / 4;                  // 64-row chunks per batch
+    __shared__ uint64_t skey[NW][R * 64];             // the wave's keys, then its hits' payloads
+    __shared__ uint64_t wsum[NW];
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int64_t per = (ntiles + kRjGroups - 1) / kRjGroups;
+    const int64_t tile = (int64_t)(blockIdx.x % kRjGroups) * per + (int64_t)(blockIdx.x / kRjGroups);
+    if (tile >= ntiles) return;  // (uniform: the whole workgroup)
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    const int g = lane >> 2, c4 = lane & 3;
+    const uint4 empty_cell = make_uint4((uint32_t)kEmptyKey, (uint32_t)(kEmptyKey >> 32), 0u, 0u);
+    const uint32_t nbk = t.nbk;
+    // the tile's keys: all loads out at once
+    uint64_t key[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+        const int64_t r = tile * kJnTileRows + (int64_t)k * kJnThreads + threadIdx.x;
+        key[k] = __builtin_nontemporal_load(keys + (r < np ? r : np - 1));
+    }
+#pragma unroll
+    for (int k = 0; k < R; ++k) skey[w][k * 64 + lane] = key[k];
+    uint32_t cnt = 0;
+#pragma unroll 1
+    for (int k0 = 0; k0 < R; k0 += CB) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // step i: rows i * 16 .. i * 16 + 15 of the batch (chunk i / 4)
+        uint64_t kq[kRjBatch];
+        uint4 cell[kRjBatch];
+        bool open[kRjBatch];
+#pragma unroll
+        for (int i = 0; i < kRjBatch; ++i) {
+            const int q = i * 16 + g;
+            const int64_t r = tile * kJnTileRows + (int64_t)(k0 + (q >> 6)) * kJnThreads + w * 64 + (q & 63);
+            kq[i] = skey[w][k0 * 64 + q];
+            open[i] = r < np && kq[i] != kEmptyKey;
+            const uint64_t h = part_hash(kq[i]);
+            const uint4* sub = t.cells + (size_t)rj_part(h, t.pbits) * nbk * 4;
+            // (every lane loads -- a key past the end or INT64_MIN reads a
+            // valid bucket and is discarded: no pointer select, no flat load)
+            const uint4 c = sub[(size_t)rj_bucket(h, nbk) * 4 + c4];
+            cell[i] = open[i] ? c : empty_cell;
+        }
+        uint64_t hm[kRjBatch];
+#pragma unroll
+        for (int i = 0; i < kRjBatch; ++i) hm[i] = 0;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // rounds of bucket reads: every step's open rows read their next
+        // bucket together (a full home bucket without the key continues;
+        // rare at load <= 1/2)
+        for (uint32_t rd = 0;; ++rd) {
+            bool again = false;
+#pragma unroll
+            for (int i = 0; i < kRjBatch; ++i) {
+                const uint64_t ck = (uint64_t)cell[i].x | ((uint64_t)cell[i].y << 32);
+                const bool hit = open[i] && ck == kq[i];
+                const uint64_t m = __ballot(hit);
+                const uint64_t done = m | __ballot(ck == kEmptyKey);
+                if (hit) skey[w][k0 * 64 + i * 16 + g] = (uint64_t)cell[i].z | ((uint64_t)cell[i].w << 32);
+                hm[i] |= m;
+                open[i] = open[i] && ((done >> (4 * g)) & 0xFull) == 0;
+                again = again || open[i];
+            }
+            if (!__any(again) || rd + 1 >= nbk) break;
+#pragma unroll
+            for (int i = 0; i < kRjBatch; ++i) {
+                if (!open[i]) continue;
+                const uint64_t h = part_hash(kq[i]);
+                const uint4* sub = t.cells + (size_t)rj_part(h, t.pbits) * nbk * 4;
+                uint32_t b = rj_bucket(h, nbk) + rd + 1;
+                while (b >= nbk) b -= nbk;
+                cell[i] = sub[(size_t)b * 4 + c4];
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // each chunk's hit word (16 bits per step) and its packed payloads
+#pragma unroll
+        for (int c = 0; c < CB; ++c) {
+            uint64_t hw = 0;
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) {
+                const uint64_t x = hm[c * 4 + s4];
+                const uint64_t gm = __ballot(lane < 16 && ((x >> (4 * lane)) & 0xFull) != 0) & 0xFFFFull;
+                hw |= gm << (16 * s4);
+            }
+            const int64_t r = tile * kJnTileRows + (int64_t)(k0 + c) * kJnThreads + threadIdx.x;
+            const int64_t seg = r - lane;
+            if (seg < np) {
+                if (lane == 0) mwords[seg >> 6] = hw;
+                if ((hw >> lane) & 1ull) mp[seg + __popcll(hw & lt)] = skey[w][(k0 + c) * 64 + lane];
+            }
+            cnt += (uint32_t)__popcll(hw);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if (lane == 0) wsum[w] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t s = 0;
+#pragma unroll
+        for (int i = 0; i < NW; ++i) s += wsum[i];
+        tile_counts[tile] = s;
+    }
+}
+
+// -> PLGPU_OK with *done = true, or *done = false (the build side has a
+// repeated or INT64_MIN key: the caller runs the row-format join instead).
+static int jn_radix_take(const plgpu_column* left_key, const plgpu_column* right_key, const plgpu_column* left_cols,
+                         int32_t nleft, const plgpu_column* right_pay, plgpu_column* out_left,
+                         plgpu_column* out_right, int64_t* out_len, bool* done, hipStream_t s) {
+    *done = false;
+    const int64_t np = left_key->length, nb = right_key->length;
+    // carried left columns (each once; the key is carried as the partition key)
+    int carry_of[PLGPU_MAX_COLS];
+    DevCol carry[kMaxAccCarry];
+    int nc = 0;
+    auto same = [](const plgpu_column& a, const plgpu_column& b) {
+        return a.values == b.values && a.offset == b.offset && a.dtype == b.dtype;
+    };
+    for (int i = 0; i < nleft; ++i) {
+        carry_of[i] = -1;
+        if (same(left_cols[i], *left_key)) continue;
+        for (int j = 0; j < i && carry_of[i] < 0; ++j)
+            if (carry_of[j] >= 0 && same(left_cols[i], left_cols[j])) carry_of[i] = carry_of[j];
+        if (carry_of[i] >= 0) continue;
+        if (nc == kMaxAccCarry) return PLGPU_OK;
+        carry_of[i] = nc;
+        carry[nc++] = as_dev(&left_cols[i]);
+    }
+    // partitions of ~2^15 build keys (sub-tables of ~1.25 MiB)
+    const int64_t per = options().join_radix_keys > 0 ? options().join_radix_keys : (int64_t(1) << 15);
+    int pbits = 0;
+    while (pbits < kRjMaxBits && (nb >> pbits) > per) ++pbits;
+    // one scatter pass (<= 2^8 partitions) while the sub-tables stay under
+    // twice the target (~2.5 MiB): a second pass costs more than the L2
+    // misses it saves (1e7 keys: 2^8 partitions of ~39k keys)
+    if (pbits > 8 && (nb >> 8) <= 2 * per && options().join_radix_keys <= 0) pbits = 8;
+    const int P = 1 << pbits;
+    const int cus = num_cus_jn();
+    const DevCol bk = as_dev(right_key), bp = as_dev(right_pay);
+    uint32_t* cnt = nullptr;
+    unsigned long long* status = nullptr;  // build flags
+    int rc = dev_alloc((void**)&cnt, (size_t)P * 4, s);
+    if (!rc) rc = dev_alloc((void**)&status, 4 * 8, s);
+    std::vector<uint32_t> hc((size_t)P);
+    if (!rc) {
+        hipError_t e = hipMemsetAsync(cnt, 0, (size_t)P * 4, s);
+        if (e == hipSuccess) e = hipMemsetAsync(status, 0, 4 * 8, s);
+        if (e == hipSuccess && nb > 0) {
+            rj_count_kernel<<<(unsigned)std::max<int64_t>(1, std::min<int64_t>((nb + 255) / 256, cus * 4)), 256, 0,
+                              s>>>(bk, nb, pbits, cnt);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) e = hipMemcpyAsync(hc.data(), cnt, (size_t)P * 4, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) rc = hip_fail(e, "rj_count_kernel");
+    }
+    dev_free(cnt, s);
+    uint32_t maxc = 0;
+    for (uint32_t c : hc) maxc = std::max(maxc, c);
+    const int load = options().join_radix_load > 0 ? std::min(90, options().join_radix_load) : 35;
+    const uint32_t nbk = std::max<uint32_t>(1u, (uint32_t)(((uint64_t)maxc * 100 + 4 * load - 1) / (4 * load)));
+    uint4* cells = nullptr;
+    const int64_t ncells = (int64_t)P * nbk * 4;
+    if (!rc) rc = dev_alloc((void**)&cells, (size_t)ncells * 16, s);
+    if (!rc) {
+        rj_init_kernel<<<(unsigned)std::min<int64_t>((ncells + 255) / 256, cus * 16), 256, 0, s>>>(cells, ncells);
+        if (nb > 0) {
+            KtScope kt("rj_build_kernel", s);
+            rj_build_kernel<<<(unsigned)std::max<int64_t>(1, std::min<int64_t>((nb + 255) / 256, cus * 16)), 256, 0,
+                              s>>>(bk, bp, nb, cells, nbk, pbits, status);
+        }
+        hipError_t e = hipGetLastError();
+        unsigned long long hs[3] = {0, 0, 0};
+        if (e == hipSuccess) e = hipMemcpyAsync(hs, status, sizeof hs, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) rc = hip_fail(e, "rj_build_kernel");
+        if (!rc && (hs[0] || hs[1] || hs[2])) {
+            // duplicate / INT64_MIN build keys: the row-format join decides
+            dev_free(cells, s);
+            dev_free(status, s);
+            return PLGPU_OK;
+        }
+    }
+    dev_free(status, s);
+    if (rc) {
+        dev_free(cells, s);
+        return rc;
+    }
+    RjTable tab;
+    tab.cells = cells;
+    tab.nbk = nbk;
+    tab.pbits = pbits;
+    // the probe rows, partitioned with their carried columns
+    RadixParts parts;
+    rc = radix_partition8(as_dev(left_key), carry, nc, np, pbits, s, &parts);
+    // match pass (hit words, packed payloads, tile counts) and its scan
+    JnPass pp;
+    uint64_t* mp = nullptr;
+    if (!rc) rc = jn_pass_alloc(np, &pp, s);
+    if (!rc) rc = dev_alloc((void**)&mp, (size_t)std::max<int64_t>(np, 1) * 8, s);
+    if (!rc) {
+        KtScope kt("rj_match_kernel", s);
+        const unsigned grid = (unsigned)(((pp.ntiles + kRjGroups - 1) / kRjGroups) * kRjGroups);
+        if (options().join_radix_batch == 4)
+            rj_match_kernel<4><<<grid, kJnThreads, 0, s>>>(parts.key, np, pp.ntiles, tab, (uint64_t*)pp.m, mp,
+                                                           pp.tcount);
+        else
+            rj_match_kernel<8><<<grid, kJnThreads, 0, s>>>(parts.key, np, pp.ntiles, tab, (uint64_t*)pp.m, mp,
+                                                           pp.tcount);
+    }
+    if (!rc) rc = jn_pass_scan(&pp, s, "rj_match_kernel");
+    const int64_t total = (int64_t)pp.total;
+    // outputs: exact length; the emit writes every left column from the
+    // partition buffers (the key listing(s) from the partitioned keys) and
+    // the payloads from mp
+    TakeCols lc;
+    std::memset(&lc, 0, sizeof lc);
+    for (int i = 0; i < nleft && !rc; ++i) {
+        rc = make_owned_column(&out_left[i], left_cols[i].dtype, total, false, s);
+        if (rc) break;
+        lc.src[lc.n] = carry_of[i] < 0 ? parts.key : parts.col[carry_of[i]];
+        lc.dst[lc.n] = (uint64_t*)out_left[i].values;
+        ++lc.n;
+    }
+    if (!rc) rc = make_owned_column(&out_right[0], right_pay->dtype, total, false, s);
+    TakePay tp;
+    std::memset(&tp, 0, sizeof tp);
+    if (!rc) {
+        tp.src[0] = mp;
+        tp.dst[0] = (uint64_t*)out_right[0].values;
+    }
+    if (!rc && total > 0) {
+        switch (lc.n) {
+        case 0: jn_take_emit<0>(pp, lc, tp, 1, nullptr, s); break;
+        case 1: jn_take_emit<1>(pp, lc, tp, 1, nullptr, s); break;
+        case 2: jn_take_emit<2>(pp, lc, tp, 1, nullptr, s); break;
+        case 3: jn_take_emit<3>(pp, lc, tp, 1, nullptr, s); break;
+        case 4: jn_take_emit<4>(pp, lc, tp, 1, nullptr, s); break;
+        case 5: jn_take_emit<5>(pp, lc, tp, 1, nullptr, s); break;
+        case 6: jn_take_emit<6>(pp, lc, tp, 1, nullptr, s); break;
+        case 7: jn_take_emit<7>(pp, lc, tp, 1, nullptr, s); break;
+        default: jn_take_emit<8>(pp, lc, tp, 1, nullptr, s); break;
+        }
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) rc = hip_fail(e, "join take emit");
+    }
+    if (!rc) {
+        const hipError_t e = hipStreamSynchronize(s);
+        if (e != hipSuccess) rc = hip_fail(e, "partitioned join");
+    }
+    if (!rc) {
+        *out_len = total;
+        *done = true;
+    } else {
+        for (int i = 0; i < nleft; ++i) plgpu_column_release(&out_left[i]);
+        plgpu_column_release(&out_right[0]);
+    }
+    dev_free(mp, s);
+    jn_pass_free(pp, s);
+    dev_free(parts.buf, s);
+    dev_free(parts.range, s);
+    dev_free(cells, s);
+    return rc;
+}
+
 // Inner join + take: the left frame's columns and the right frame's columns
 // at the matching pairs (pairs and their order as plgpu_join_inner), i.e.
 // the reference's hash_join_tuples_inner followed by _finish_join's takes.
@@ -1788,6 +2183,26 @@ PLGPU_API int plgpu_join_inner_take(const plgpu_column* left_key, const plgpu_co
     auto fused8 = [](const plgpu_column& c) {
         return c.validity == nullptr && c.dtype != PLGPU_STR && c.dtype != PLGPU_BOOL && dtype_bytes(c.dtype) == 8;
     };
+    // order-free join, one unique-keyed payload, null-free 8-byte integer
+    // keys and 8-byte columns: the partitioned join (jn_radix_take) where
+    // the build table outgrows the L2s and the probe side is long
+    // (option join_radix: 1 there, 2 wherever it applies, 0 off)
+    const int jr = options().join_radix;
+    if (jr != 0 && maintain_order == PLGPU_JOIN_ORDER_NONE && nright == 1 && fused8(right_cols[0]) &&
+        fused8(*left_key) && fused8(*right_key) && dtype_is_int(left_key->dtype) &&
+        (validate == PLGPU_JOIN_VALIDATE_M_M || validate == PLGPU_JOIN_VALIDATE_M_1) &&
+        right_key->length <= left_key->length && left_key->length < 0xFFFFFFFFll &&
+        (jr == 2 ? left_key->length > 0
+                 : left_key->length >= (int64_t(1) << 22) && right_key->length >= (int64_t(1) << 17))) {
+        bool ok = true;
+        for (int i = 0; i < nleft; ++i) ok = ok && fused8(left_cols[i]);
+        if (ok) {
+            bool done = false;
+            rc = jn_radix_take(left_key, right_key, left_cols, nleft, &right_cols[0], out_left, out_right, out_len,
+                               &done, s);
+            if (rc || done) return rc;
+        }
+    }
     const bool order_ok = maintain_order == PLGPU_JOIN_ORDER_NONE || maintain_order == PLGPU_JOIN_ORDER_LEFT;
     bool pay8 = nright >= 1 && nright <= 3;
     for (int i = 0; i < nright && pay8; ++i) pay8 = fused8(right_cols[i]);

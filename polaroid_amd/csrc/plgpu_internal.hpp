@@ -12,6 +12,7 @@
 #include <cstring>
 
 #include <string>
+#include <vector>
 
 #include "../../include/polaroid_gpu.h"
 
@@ -47,7 +48,8 @@ struct Options {
     // group-by path hooks (tests: the forced-path parity sweep, DESIGN.md
     // "Group-by paths"): -1 lets the plan choose
     int gb_path = -1;     // 0 generic kernel on the global table, 1 generic with LDS tables,
-                          // 2 fused kernel, 3 partitioned (where the inputs allow it)
+                          // 2 fused kernel, 3 partitioned (where the inputs allow it),
+                          // 5 partitioned without the plan's input checks (the launchers refuse)
     int part_bits = -1;   // partitioned path: at least this many partition bits
     int part_levels = -1; // partitioned path: 1 / 2 scatter passes (-1: by the partition bits)
     int part_direct = 1;  // partitioned path: one-workgroup partitions flush into their own table region
@@ -62,6 +64,13 @@ struct Options {
     int var_pos = 1;      // fused variance: x's limbs unsigned when the predicate keeps x >= 0 (A/B)
     int sum_pos = 1;      // fused 4-sum kernel: the predicate column's limbs unsigned when it keeps x >= 0 (A/B)
     int gb_pair = 1;      // (x * y).sum() next to y.sum(): the product-pair fused variant (A/B)
+    // order-free inner join + take by radix partitions with L2-resident
+    // sub-tables (join.hip "partitioned join"): 1 where it pays (large probe
+    // and build sides), 2 forced wherever it applies (tests), 0 off (A/B)
+    int join_radix = 1;
+    int join_radix_keys = 0;  // build keys per partition target (0: 2^15)
+    int join_radix_load = 0;  // sub-table load factor in percent (0: 35)
+    int join_radix_batch = 0; // match pass: probe steps with bucket reads in flight together, 4 or 8 (0: 8)
 };
 Options& options();
 
@@ -141,6 +150,24 @@ struct DevCol {
     int32_t _pad;
     const uint8_t* data;      // PLGPU_STR: string bytes
 };
+
+// Radix partition of null-free 8-byte columns by the top `bits` bits of
+// part_hash(key) (groupby.hip gb_partition: count, scan and LDS-staged
+// scatter passes; one pass up to 2^8 partitions, two above): partition q
+// holds rows [hrange[q], hrange[q + 1]) of `key` and of each col[i].  `buf`
+// and `range` (the P + 1 bounds on the device, at `bounds`) are owned by the
+// caller (dev_free).  Used by the join's partitioned probe.
+struct RadixParts {
+    uint64_t* buf = nullptr;
+    uint64_t* key = nullptr;
+    uint64_t* col[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    uint64_t* range = nullptr;
+    const uint64_t* bounds = nullptr;
+    std::vector<uint64_t> hrange;
+    int levels = 0;
+};
+int radix_partition8(const DevCol& key, const DevCol* cols, int ncols, int64_t n, int bits, hipStream_t s,
+                     RadixParts* out);
 
 inline DevCol dev_col(const plgpu_column& c) {
     DevCol d;

@@ -72,6 +72,10 @@ const OptField kOptFields[] = {
     {"filt_fused", "PLGPU_FILT_FUSED", &Options::filt_fused},
     {"var_pos", "PLGPU_VAR_POS", &Options::var_pos},
     {"sum_pos", "PLGPU_SUM_POS", &Options::sum_pos},
+    {"join_radix", "PLGPU_JOIN_RADIX", &Options::join_radix},
+    {"join_radix_keys", "PLGPU_JOIN_RADIX_KEYS", &Options::join_radix_keys},
+    {"join_radix_load", "PLGPU_JOIN_RADIX_LOAD", &Options::join_radix_load},
+    {"join_radix_batch", "PLGPU_JOIN_RADIX_BATCH", &Options::join_radix_batch},
 };
 const OptField* opt_field(const char* name) {
     for (const OptField& f : kOptFields)

@@ -31,6 +31,12 @@ __device__ __forceinline__ uint64_t mk_fmix(uint64_t x) {
     return x;
 }
 
+// Partition hash of the many-groups group-by and the partitioned join (its
+// top bits pick the partition; independent of the table hashes, which
+// multiply by the golden ratio).  A bijection of the key (fmix64 is
+// invertible), so distinct keys never share all 64 bits.
+__device__ __forceinline__ uint64_t part_hash(uint64_t key) { return mk_fmix(key ^ 0x2545F4914F6CDD1Dull); }
+
 // 64-bit hash of a string's bytes (8-byte little-endian words, then the
 // tail; the length is mixed in, so "" and "\0" differ).
 __device__ __forceinline__ uint64_t str_hash(const DevCol& c, int64_t r, uint64_t seed = 0) {

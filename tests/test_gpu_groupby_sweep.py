@@ -14,7 +14,8 @@ Paths are forced with the library's test hooks (plgpu_set_option):
 Where the inputs rule a path out (nulls for the fused and partitioned paths,
 4-byte columns and program predicates for the fused kernel), the plan takes
 the next path that accepts them; `_expect_path` states which, so a path
-refusing more than DESIGN.md "Group-by paths" lists is a failure too.  The
+refusing more than DESIGN.md "Group-by paths" lists is a failure too (since
+round 6 no path refuses validity bitmaps).  The
 derived-input (DERIV), variance-triple (VAR), keyless, packed multi-key
 (PACK 1), String-key (PACK 2), sorted-key (RUNS), range-local (time-ordered
 keys) and wide-sum variants are crossed with the same paths below.
@@ -164,13 +165,12 @@ def _expect_path(path, key_nulls, val_nulls, narrow, pred, sum_only, maintain):
     if gp in (0, 1):
         return 0
     if gp == 2:
-        if key_nulls or val_nulls or narrow or pred == "program":
-            return 0                      # the fused kernel needs null-free 8-byte columns
+        if narrow or pred == "program":
+            return 0                      # the fused kernel needs 8-byte columns and a simple predicate
+        # (validity bitmaps: the NULLS variant, round 6)
         return 2 if sum_only and not maintain else 1   # maintain_order: the first-row field
     if gp == 3:
-        if key_nulls or val_nulls:
-            return 0                      # partition buffers carry raw words: no validity
-        return 3
+        return 3                          # null bits travel with the partitioned rows (round 6)
     return None
 
 
@@ -433,3 +433,21 @@ def test_sweep_wide_sums(gpu, path, plgpu_option):
         for maintain in (False, True):
             out, info = _gpu(df, "k", specs, pf() if pf else None, maintain)
             _compare(out, "k", exp, len(specs), maintain, (path, pname, maintain, info.get("path")))
+
+
+def test_partition_launchers_refuse_a_keyless_reduction(gpu, frame, plgpu_option):
+    """gb_path 5 skips the plan's input checks and forces the partitioned
+    path: the partition launchers' own precondition (groupby.hip
+    gb_partition) must turn a keyless reduction -- round 5's r05c fault, a
+    null key column read by gbp_count_kernel -- into InvalidOperationError,
+    never a device access; a nullable key is taken (its null bits travel
+    with the rows) and stays exact."""
+    df, cols = frame
+    plgpu_option("gb_path", 5)
+    with pytest.raises(pl.InvalidOperationError, match="partitioned group-by"):
+        df.lazy().select(col("c").sum().alias("o0")).collect()
+    specs = [("sum", col("cn")), ("min", col("an")), ("count", col("an"))]
+    exp = _oracle(cols, "kn", specs, None, N, names_extra=("an", "cn"))
+    out, info = _gpu(df, "kn", specs, None, False)
+    assert info["path"] == 3
+    _compare(out, "kn", exp, len(specs), False, ("gb_path 5", info.get("path")))

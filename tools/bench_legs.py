@@ -14,7 +14,7 @@ sys.path.insert(0, ROOT)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--leg", choices=["headline", "vwap", "std", "filter", "many_groups", "sort", "join"], required=True)
+    ap.add_argument("--leg", choices=["headline", "vwap", "std", "filter", "many_groups", "sort", "join", "nulls"], required=True)
     ap.add_argument("--rows", type=float, default=1e9)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
@@ -39,6 +39,12 @@ def main():
     elif args.leg == "many_groups":
         del df
         r = bench.many_groups_leg(torch, pl, cols, args.steps, args.warmup, [args.groups], 0, 0.0, True)
+    elif args.leg == "nulls":
+        q = df.lazy().filter(pl.col("close") > bench.THRESHOLD).group_by("symbol").agg(
+            *[pl.col(c).sum() for c in ("open", "high", "low", "close")])
+        h = bench.timed_leg(torch, q, n, args.steps, args.warmup, 40)
+        del q, df
+        r = {"headline": h, **bench.nulls_leg(torch, pl, sym, cols, args.steps, args.warmup, h["ms_per_step"])}
     elif args.leg == "std":
         r = bench.std_leg(torch, pl, df, args.steps, args.warmup)
     else:
