@@ -659,7 +659,13 @@ int plgpu_join_inner(const plgpu_column* left_key, const plgpu_column* right_key
  * right keys and a null-free 8-byte right column the hash table is
  * row-format (each cell {key, payload}) and the emit pass writes the
  * payload and the null-free 8-byte left columns straight to their output
- * rows; other inputs take the pairs + gather route with the same result. */
+ * rows; other inputs take the pairs + gather route with the same result.
+ * With maintain_order "none" (the reference's default), null-free 8-byte
+ * integer keys and columns, a long probe side and a build side beyond the
+ * L2s, the join is radix-partitioned (round 6): per-partition L2-resident
+ * sub-tables (polars-ops/src/frame/join/hash_join/single_keys.rs:16
+ * build_tables), the probe rows scattered by partition, rows out in
+ * partition order. */
 int plgpu_join_inner_take(const plgpu_column* left_key, const plgpu_column* right_key,
                           const plgpu_column* left_cols, int32_t nleft,
                           const plgpu_column* right_cols, int32_t nright, int32_t nulls_equal,

@@ -185,30 +185,51 @@ __device__ __forceinline__ void ps_col(const DevCol& c, const uint64_t* buf, con
 // GbParams::part_nulls bits, a null predicate value drops the row, and a
 // null-key row is spread over the partitions by its position (ps_digit):
 // it aggregates into the null group wherever it lands.
-template <int PRED, bool L2, bool F8, bool NUL = false>
+// Null bit of row rb + lane of a column whose bitmap holds whole aligned
+// words for the wave's 64 rows (rb a multiple of 64, p.vwords): one uniform
+// word load per wave.  1 = null.
+__device__ __forceinline__ uint32_t ps_null_word(const DevCol& c, int64_t rb) {
+    if (!c.validity) return 0u;
+    const uint64_t w = ((const uint64_t*)c.validity)[(uint64_t)(c.offset + rb) >> 6];
+    return (uint32_t)(~w >> (threadIdx.x & 63)) & 1u;
+}
+
+template <int PRED, bool L2, bool F8, bool NUL = false, bool ACCS = true>
 __device__ __forceinline__ void ps_keys(const GbParams& p, const DevProgram& prog, const PartOut& in, const PsTile& tl,
                                         int c0, uint64_t (&key)[kPsPer], uint64_t (&pv)[kPsPer],
                                         bool (&sel)[kPsPer], uint32_t (&nb)[kPsPer]) {
     const int lane = threadIdx.x & 63;
     ps_col<L2, F8>(p.key, in.key, tl, c0, key);
     if (!L2 && PRED == 1) ps_col<false, F8>(p.pred_col, nullptr, tl, c0, pv);
+    // full level-1 tile and word-aligned bitmaps: a wave's 64 rows' bits are
+    // one word per column (ACCS: the aggregated columns' bits too -- the
+    // count pass needs only the key's and the predicate's)
+    const bool words = NUL && !L2 && p.vwords && tl.lo == tl.base && tl.hi - tl.base == kPsTile;
 #pragma unroll
     for (int k = 0; k < kPsPer; ++k) {
         const int64_t r = tl.base + c0 + k * 64 + lane;
         bool s = r >= tl.lo && r < tl.hi;
         nb[k] = 0;
-        if (NUL && s) {
-            if (L2) {
-                nb[k] = in.nulls ? in.nulls[r] : 0u;
-            } else {
-                uint32_t m = dev_valid(p.key, r) ? 0u : 0x40u;
+        bool pvalid = true;
+        if (NUL && L2) {
+            nb[k] = in.nulls && s ? in.nulls[r] : 0u;
+        } else if (NUL && words) {
+            const int64_t rb = r - lane;
+            uint32_t m = ps_null_word(p.key, rb) << 6;
+            if (ACCS)
+                for (int a = 0; a < p.nacc; ++a) m |= ps_null_word(p.acc[a].c, rb) << a;
+            nb[k] = m;
+            if (PRED == 1) pvalid = !ps_null_word(p.pred_col, rb);
+        } else if (NUL && s) {
+            uint32_t m = dev_valid(p.key, r) ? 0u : 0x40u;
+            if (ACCS)
                 for (int a = 0; a < p.nacc; ++a)
                     if (!dev_valid(p.acc[a].c, r)) m |= 1u << a;
-                nb[k] = m;
-            }
+            nb[k] = m;
+            if (PRED == 1) pvalid = dev_valid(p.pred_col, r);
         }
         if (!L2 && PRED == 1)
-            s = s && ((F8 && !NUL) || dev_valid(p.pred_col, r)) &&
+            s = s && ((F8 && !NUL) || (NUL ? pvalid : dev_valid(p.pred_col, r))) &&
                 simple_pred(prog.simple_isf, prog.simple_op, pv[k], prog.simple_imm);
         if (!L2 && PRED == 2 && s) {
             const RowVal rv = eval_row(prog.code, prog.n, p.cols, r);
@@ -239,7 +260,7 @@ __global__ __launch_bounds__(kPsThreads) void gbp_count_kernel(GbParams p, DevPr
     bool sel[kPsPer];
     uint32_t nb[kPsPer];
     const int c0 = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) * (kPsTile / (kPsThreads / 64));
-    ps_keys<PRED, L2, F8, NUL>(p, prog, in, tl, c0, key, pv, sel, nb);
+    ps_keys<PRED, L2, F8, NUL, false>(p, prog, in, tl, c0, key, pv, sel, nb);
     __syncthreads();
     const uint32_t mask = (uint32_t)P - 1;
 #pragma unroll
@@ -2236,6 +2257,14 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
         // the code column)
         if (nul && (p.kp.n > 0 || dv)) fast = false;
         pl.nulls = nul;
+        // whole-word validity reads (GbParams::vwords): every bitmap at a
+        // column offset that is a multiple of 64 in an 8-byte aligned buffer
+        auto wa = [](const DevCol& c) {
+            return c.validity == nullptr || ((c.offset & 63) == 0 && ((uintptr_t)c.validity & 7) == 0);
+        };
+        bool vw = wa(p.key) && (R.pred != 1 || wa(p.pred_col));
+        for (int a = 0; a < p.nacc; ++a) vw = vw && wa(p.acc[a].c);
+        p.vwords = vw ? 1 : 0;
     }
     if (gpath == 0 || gpath == 1 || gpath == 3 || gpath == 5) fast = false;
     if (pl.local && !fast) {

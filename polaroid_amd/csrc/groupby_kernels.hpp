@@ -178,6 +178,11 @@ struct GbParams {
     // partitioned run with one workgroup per partition: each partition's
     // groups live in a region of 2^rbits global slots (g_slot); 0 = off
     int32_t rbits;
+    // every validity bitmap of the key / aggregated / predicate columns has a
+    // column offset that is a multiple of 64 and an 8-byte aligned buffer:
+    // a wave's validity bits come as whole 64-bit words (fast_nulls,
+    // ps_keys) instead of one byte load per lane
+    int32_t vwords;
     KeyPack kp;             // fused key packing (kp.n > 0): the key is the packed tuple code
 };
 
@@ -1053,13 +1058,30 @@ __device__ __forceinline__ uint32_t pair_nulls(const DevCol& c, int64_t r) {
     return ~(byte >> (b & 7)) & 3u;
 }
 
+// Null bits of this lane's row pair from the 128-bit window of a wave's
+// 128 consecutive rows (first row rw, a multiple of 128; the column offset
+// a multiple of 64): lanes load the window's two aligned words alternately
+// (one request per wave), every lane takes both words by readlane and its
+// two bits (rows rw + 2 lane, + 1) by a shift.
+__device__ __forceinline__ uint32_t pair_nulls_words(const DevCol& c, int64_t rw) {
+    if (!c.validity) return 0u;
+    const int lane = threadIdx.x & 63;
+    const uint64_t* w = (const uint64_t*)c.validity + ((uint64_t)(c.offset + rw) >> 6);
+    const uint64_t mine = __builtin_nontemporal_load(w + (lane & 1));
+    const uint32_t lo0 = __builtin_amdgcn_readlane((uint32_t)mine, 0), hi0 = __builtin_amdgcn_readlane((uint32_t)(mine >> 32), 0);
+    const uint32_t lo1 = __builtin_amdgcn_readlane((uint32_t)mine, 1), hi1 = __builtin_amdgcn_readlane((uint32_t)(mine >> 32), 1);
+    const uint64_t word = lane < 32 ? ((uint64_t)hi0 << 32 | lo0) : ((uint64_t)hi1 << 32 | lo1);
+    return ~(uint32_t)(word >> (2 * (lane & 31))) & 3u;
+}
+
 // NUL: the tile's null bits (FastTile::nv), from the columns' validity
-// bitmaps (one byte per row pair and column) or, over the partition buffers
-// (PART), from part_nulls (two bytes per pair).  Rows past n (the masked tail
-// tile) read nothing.
+// bitmaps (one byte per row pair and column, or whole words: p.vwords) or,
+// over the partition buffers (PART), from part_nulls (two bytes per pair).
+// Rows past n (the masked tail tile) read nothing.  Issued before the
+// tile's value loads, so the bits arrive first.
 template <int NACC, int PRED, int ROWS, bool PART, bool DERIV, int PACK, bool NUL>
 __device__ __forceinline__ void fast_nulls(const GbParams& p, int64_t t, FastTile<NACC, ROWS, DERIV, PACK, NUL>& x,
-                                           int64_t rbase, int64_t rmax) {
+                                           int64_t rbase, int64_t rmax, bool full) {
     if constexpr (NUL) {
         const int T = blockDim.x;
 #pragma unroll
@@ -1069,6 +1091,21 @@ __device__ __forceinline__ void fast_nulls(const GbParams& p, int64_t t, FastTil
             uint32_t m = 0;
             if (PART) {
                 if (p.part_nulls) m = __builtin_nontemporal_load((const uint16_t*)(p.part_nulls + r));
+            } else if (full && p.vwords) {
+                // a full tile: the wave's 128 rows end at or below n_full, a
+                // multiple of 1024, so the two words lie inside the bitmap
+                const int64_t rw = r - 2 * (threadIdx.x & 63);
+#pragma unroll
+                for (int c = 0; c < NACC; ++c) {
+                    const uint32_t b = pair_nulls_words(p.acc[c].c, rw);
+                    m |= ((b & 1u) << c) | ((b >> 1) << (8 + c));
+                }
+                const uint32_t bk = pair_nulls_words(p.key, rw);
+                m |= ((bk & 1u) << 6) | ((bk >> 1) << 14);
+                if (PRED == 1 && p.pred_acc < 0) {
+                    const uint32_t bp = pair_nulls_words(p.pred_col, rw);
+                    m |= ((bp & 1u) << 7) | ((bp >> 1) << 15);
+                }
             } else if (r < p.n) {
 #pragma unroll
                 for (int c = 0; c < NACC; ++c) {
@@ -1232,9 +1269,9 @@ __global__ __launch_bounds__(PART && !RUNS ? kGbPartThreads : kGbThreads) void g
         tstep = p.part_blocks;
     }
     auto load_tile = [&](int64_t tt, FastTile<NL, ROWS, DERIV, PACK, NULLS>& x) {
+        fast_nulls<NL, PRED, ROWS, PART, DERIV, PACK, NULLS>(p, tt, x, rbase, rmax, tt < ntiles);
         if (PART || tt < ntiles) fast_load<NL, PRED, ROWS, true, DERIV, PACK, NULLS>(p, tt, x, rbase, rmax);
         else fast_load_tail<NL, PRED, ROWS, DERIV, PACK, NULLS>(p, tt, x);
-        fast_nulls<NL, PRED, ROWS, PART, DERIV, PACK, NULLS>(p, tt, x, rbase, rmax);
     };
     // NULLS: the null bit of the predicate's column (its acc's, or its own)
     const int pbit = p.pred_acc >= 0 ? p.pred_acc : 7;

@@ -1864,38 +1864,53 @@ __global__ __launch_bounds__(256) void rj_build_kernel(DevCol bk, DevCol pay, in
 // of tile t is t * 4096 + k * 256 + tid (k = 0 .. 15).  The tiles are taken
 // in partitioned-row order within eight contiguous ranges, one per workgroup
 // group (blockIdx % 8: the blocks one XCD receives), so an XCD walks its
-// partitions in order and their sub-tables stay in its L2.  Each wave
-// probes cooperatively: in a step, lanes 4g .. 4g + 3 read the four cells of
-// row g's home bucket (one 64-B request per row), kRjBatch steps' reads in
-// flight together.  No atomics: the scan of the tile counts places the rows.
+// partitions in order and their sub-tables stay in its L2.  Each row is
+// hashed once, by its own lane (key and home bucket staged in LDS); the
+// wave then probes cooperatively: in a step, lanes 4g .. 4g + 3 read the
+// four cells of row g's home bucket (one 64-B request per row), kRjBatch
+// steps' reads in flight together.  A workgroup takes half a tile; the two
+// halves add their hit counts to the tile's, and the scan of the tile counts
+// places the rows.
 template <int kRjBatch>
 __global__ __launch_bounds__(kJnThreads) void rj_match_kernel(const uint64_t* __restrict__ keys, int64_t np,
                                                              int64_t ntiles, RjTable t, uint64_t* __restrict__ mwords,
                                                              uint64_t* __restrict__ mp,
-                                                             uint64_t* __restrict__ tile_counts) {
-    constexpr int R = kJnTileRows / kJnThreads;      // 16 rows per thread
+                                                             unsigned long long* __restrict__ tile_counts) {
+    // a workgroup takes half a 4,096-row tile: chunks 8h .. 8h + 7 (row
+    // tile * 4096 + k * 256 + tid), its hit count added to the tile's
+    constexpr int R = kJnTileRows / kJnThreads / 2;  // 8 rows per thread
     constexpr int NW = kJnThreads / 64;
     constexpr int CB = kRjBatch / 4;                  // 64-row chunks per batch
     __shared__ uint64_t skey[NW][R * 64];             // the wave's keys, then its hits' payloads
+    __shared__ uint32_t sgb[NW][R * 64];              // each row's home bucket (~0: no probe)
     __shared__ uint64_t wsum[NW];
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int64_t per = (ntiles + kRjGroups - 1) / kRjGroups;
-    const int64_t tile = (int64_t)(blockIdx.x % kRjGroups) * per + (int64_t)(blockIdx.x / kRjGroups);
-    if (tile >= ntiles) return;  // (uniform: the whole workgroup)
+    const int64_t nhalf = 2 * ntiles;
+    const int64_t per = (nhalf + kRjGroups - 1) / kRjGroups;
+    const int64_t half = (int64_t)(blockIdx.x % kRjGroups) * per + (int64_t)(blockIdx.x / kRjGroups);
+    if (half >= nhalf) return;  // (uniform: the whole workgroup)
+    const int64_t tile = half >> 1, kb = (half & 1) * R;
     const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     const int g = lane >> 2, c4 = lane & 3;
     const uint4 empty_cell = make_uint4((uint32_t)kEmptyKey, (uint32_t)(kEmptyKey >> 32), 0u, 0u);
     const uint32_t nbk = t.nbk;
-    // the tile's keys: all loads out at once
+    // the half tile's keys (all loads out at once), each hashed once by its
+    // own lane: the home bucket over the whole table (partition * nbk +
+    // bucket), or ~0 for a row past the end or an INT64_MIN key
     uint64_t key[R];
 #pragma unroll
     for (int k = 0; k < R; ++k) {
-        const int64_t r = tile * kJnTileRows + (int64_t)k * kJnThreads + threadIdx.x;
+        const int64_t r = tile * kJnTileRows + (int64_t)(kb + k) * kJnThreads + threadIdx.x;
         key[k] = __builtin_nontemporal_load(keys + (r < np ? r : np - 1));
     }
 #pragma unroll
-    for (int k = 0; k < R; ++k) skey[w][k * 64 + lane] = key[k];
+    for (int k = 0; k < R; ++k) {
+        const int64_t r = tile * kJnTileRows + (int64_t)(kb + k) * kJnThreads + threadIdx.x;
+        const uint64_t h = part_hash(key[k]);
+        skey[w][k * 64 + lane] = key[k];
+        sgb[w][k * 64 + lane] = r < np && key[k] != kEmptyKey ? rj_part(h, t.pbits) * nbk + rj_bucket(h, nbk) : ~0u;
+    }
     uint32_t cnt = 0;
 #pragma unroll 1
     for (int k0 = 0; k0 < R; k0 += CB) {
@@ -1904,19 +1919,17 @@ __global__ __launch_bounds__(kJnThreads) void rj_match_kernel(const uint64_t* __
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         // step i: rows i * 16 .. i * 16 + 15 of the batch (chunk i / 4)
         uint64_t kq[kRjBatch];
+        uint32_t bq[kRjBatch];
         uint4 cell[kRjBatch];
         bool open[kRjBatch];
 #pragma unroll
         for (int i = 0; i < kRjBatch; ++i) {
-            const int q = i * 16 + g;
-            const int64_t r = tile * kJnTileRows + (int64_t)(k0 + (q >> 6)) * kJnThreads + w * 64 + (q & 63);
-            kq[i] = skey[w][k0 * 64 + q];
-            open[i] = r < np && kq[i] != kEmptyKey;
-            const uint64_t h = part_hash(kq[i]);
-            const uint4* sub = t.cells + (size_t)rj_part(h, t.pbits) * nbk * 4;
-            // (every lane loads -- a key past the end or INT64_MIN reads a
-            // valid bucket and is discarded: no pointer select, no flat load)
-            const uint4 c = sub[(size_t)rj_bucket(h, nbk) * 4 + c4];
+            const int q = k0 * 64 + i * 16 + g;
+            kq[i] = skey[w][q];
+            bq[i] = sgb[w][q];
+            open[i] = bq[i] != ~0u;
+            // (every lane loads: a closed row reads bucket 0 and discards it)
+            const uint4 c = t.cells[(size_t)(open[i] ? bq[i] : 0u) * 4 + c4];
             cell[i] = open[i] ? c : empty_cell;
         }
         uint64_t hm[kRjBatch];
@@ -1945,11 +1958,10 @@ __global__ __launch_bounds__(kJnThreads) void rj_match_kernel(const uint64_t* __
 #pragma unroll
             for (int i = 0; i < kRjBatch; ++i) {
                 if (!open[i]) continue;
-                const uint64_t h = part_hash(kq[i]);
-                const uint4* sub = t.cells + (size_t)rj_part(h, t.pbits) * nbk * 4;
-                uint32_t b = rj_bucket(h, nbk) + rd + 1;
-                while (b >= nbk) b -= nbk;
-                cell[i] = sub[(size_t)b * 4 + c4];
+                // the next bucket within the row's partition
+                const uint32_t q = bq[i] / nbk;
+                bq[i] = bq[i] + 1 == (q + 1) * nbk ? q * nbk : bq[i] + 1;
+                cell[i] = t.cells[(size_t)bq[i] * 4 + c4];
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1965,7 +1977,7 @@ __global__ __launch_bounds__(kJnThreads) void rj_match_kernel(const uint64_t* __
                 const uint64_t gm = __ballot(lane < 16 && ((x >> (4 * lane)) & 0xFull) != 0) & 0xFFFFull;
                 hw |= gm << (16 * s4);
             }
-            const int64_t r = tile * kJnTileRows + (int64_t)(k0 + c) * kJnThreads + threadIdx.x;
+            const int64_t r = tile * kJnTileRows + (int64_t)(kb + k0 + c) * kJnThreads + threadIdx.x;
             const int64_t seg = r - lane;
             if (seg < np) {
                 if (lane == 0) mwords[seg >> 6] = hw;
@@ -1983,7 +1995,7 @@ __global__ __launch_bounds__(kJnThreads) void rj_match_kernel(const uint64_t* __
         uint64_t s = 0;
 #pragma unroll
         for (int i = 0; i < NW; ++i) s += wsum[i];
-        tile_counts[tile] = s;
+        if (s) atomicAdd(&tile_counts[tile], (unsigned long long)s);
     }
 }
 
@@ -2083,15 +2095,19 @@ static int jn_radix_take(const plgpu_column* left_key, const plgpu_column* right
     uint64_t* mp = nullptr;
     if (!rc) rc = jn_pass_alloc(np, &pp, s);
     if (!rc) rc = dev_alloc((void**)&mp, (size_t)std::max<int64_t>(np, 1) * 8, s);
+    if (!rc && hipMemsetAsync(pp.tcount, 0, (size_t)pp.ntiles * 8, s) != hipSuccess)
+        rc = fail(PLGPU_ERR_HIP, "rj_match_kernel tile counts");
     if (!rc) {
         KtScope kt("rj_match_kernel", s);
-        const unsigned grid = (unsigned)(((pp.ntiles + kRjGroups - 1) / kRjGroups) * kRjGroups);
-        if (options().join_radix_batch == 4)
-            rj_match_kernel<4><<<grid, kJnThreads, 0, s>>>(parts.key, np, pp.ntiles, tab, (uint64_t*)pp.m, mp,
-                                                           pp.tcount);
+        const unsigned grid = (unsigned)(((2 * pp.ntiles + kRjGroups - 1) / kRjGroups) * kRjGroups);
+        unsigned long long* tc = (unsigned long long*)pp.tcount;
+        // 4 probe steps in flight per wave: 54 VGPRs, the LDS bound of 6
+        // workgroups per CU (7.69 ms against 7.96 for 8 steps at 86 VGPRs,
+        // 1e9 x 1e7, gpurun_out/r06i_*)
+        if (options().join_radix_batch == 8)
+            rj_match_kernel<8><<<grid, kJnThreads, 0, s>>>(parts.key, np, pp.ntiles, tab, (uint64_t*)pp.m, mp, tc);
         else
-            rj_match_kernel<8><<<grid, kJnThreads, 0, s>>>(parts.key, np, pp.ntiles, tab, (uint64_t*)pp.m, mp,
-                                                           pp.tcount);
+            rj_match_kernel<4><<<grid, kJnThreads, 0, s>>>(parts.key, np, pp.ntiles, tab, (uint64_t*)pp.m, mp, tc);
     }
     if (!rc) rc = jn_pass_scan(&pp, s, "rj_match_kernel");
     const int64_t total = (int64_t)pp.total;

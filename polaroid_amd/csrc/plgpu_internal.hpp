@@ -70,7 +70,7 @@ struct Options {
     int join_radix = 1;
     int join_radix_keys = 0;  // build keys per partition target (0: 2^15)
     int join_radix_load = 0;  // sub-table load factor in percent (0: 35)
-    int join_radix_batch = 0; // match pass: probe steps with bucket reads in flight together, 4 or 8 (0: 8)
+    int join_radix_batch = 0; // match pass: probe steps with bucket reads in flight together, 4 or 8 (0: 4)
 };
 Options& options();
 

@@ -14,16 +14,17 @@ import re
 import sys
 
 VARIANTS = {
-    "headline 4 sums (SUMONLY, 2 limbs)": "ILi4ELi1ELb1ELi2ELi2ELb0ELb0ELb0ELi0ELi0EE",
+    "headline 4 sums (SUMONLY, 2 limbs)": "ILi4ELi1ELb1ELi2ELi2ELb0ELb0ELb0ELi0ELi0ELb0EE",
     "vwap DERIV 2 accs": "ILi2ELi1ELb1ELi2ELi2ELb0ELb0ELb1ELi0ELi0EE",
     "vwap product pair (VAR 2)": "ILi2ELi1ELb1ELi2ELi2ELb0ELb0ELb0ELi2ELi0EE",
     "vwap-like 2 plain sums": "ILi2ELi1ELb1ELi2ELi2ELb0ELb0ELb0ELi0ELi0EE",
     "std VAR triple": "ILi3ELi1ELb1ELi2ELi2ELb0ELb0ELb0ELi1ELi0EE",
     "std VAR triple, x >= 0 (VAR 4)": "ILi3ELi1ELb1ELi2ELi2ELb0ELb0ELb0ELi4ELi0EE",
-    "headline, close >= 0 (VAR 5)": "ILi4ELi1ELb1ELi2ELi2ELb0ELb0ELb0ELi5ELi0EE",
+    "headline, close >= 0 (VAR 5)": "ILi4ELi1ELb1ELi2ELi2ELb0ELb0ELb0ELi5ELi0ELb0EE",
     "headline PACK (fused integer keys)": "ILi4ELi1ELb1ELi2ELi2ELb0ELb0ELb0ELi0ELi1EE",
     "headline PACK 1, close >= 0 (VAR 5)": "ILi4ELi1ELb1ELi2ELi2ELb0ELb0ELb0ELi5ELi1EE",
     "headline PACK (String key codes)": "ILi4ELi1ELb1ELi2ELi2ELb0ELb0ELb0ELi0ELi2EE",
+    "headline NULLS (validity bitmaps)": "ILi4ELi1ELb1ELi2ELi2ELb0ELb0ELb0ELi0ELi0ELb1EE",
 }
 
 
