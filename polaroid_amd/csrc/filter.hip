@@ -503,7 +503,11 @@ static int run_filter(const plgpu_column* cols, int32_t ncols, int src, const De
     // the one-pass form (filter_fused8_kernel): a simple predicate over a
     // null-free 8-byte column, every column null-free and 8 bytes wide, and
     // output columns allocated at the input's length (their length set to
-    // the selected count afterwards) within a quarter of the free memory
+    // the selected count afterwards) within a quarter of the free memory.
+    // Off by default (measured slower, DESIGN "Filter compaction"): it
+    // OVER-ALLOCATES -- each output keeps n * 8 bytes for the result's
+    // lifetime -- and the free/4 guard makes the choice depend on memory
+    // pressure; size the outputs from a count before turning it on.
     bool all8 = ncols > 0 && src != 0 && dp.simple && options().filt_fused != 0 && n > 0;
     for (int i = 0; i < ncols && all8; ++i)
         all8 = cols[i].dtype != PLGPU_STR && cols[i].dtype != PLGPU_BOOL && cols[i].validity == nullptr &&

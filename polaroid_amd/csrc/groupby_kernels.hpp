@@ -1884,6 +1884,10 @@ hipError_t launch_fast_nulls(const Plan& pl, const DevProgram& dp, int pred, hip
 // on acc `a`'s own column that accepts no value below c (x > c, x >= c,
 // x == c) with c >= 0 (NaN compares greatest and fails the limb window
 // anyway; -0.0 converts to zero limbs either way).
+// pred_acc is the FIRST acc reading the predicate's column (groupby.hip
+// gb_plan), so sum_pos (VAR 5, a = NACC - 1) only fires when that column
+// feeds the last acc alone; if it also feeds an earlier acc this returns
+// false and the signed-limb kernel runs (correct, just not the variant).
 inline bool var_x_nonneg(const Plan& pl, const DevProgram& dp, int a = 0) {
     if (!dp.simple || !dp.simple_isf || pl.p.pred_acc != a || dp.simple_op < 0 || dp.simple_op > 5) return false;
     if (pl.p.acc[a].dop != DOP_NONE || pl.p.acc[a].c.dtype != PLGPU_F64) return false;

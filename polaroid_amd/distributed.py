@@ -331,7 +331,7 @@ def agree_wide(vals, world: int, rank: int, failed: bool, group, device):
         flat[world:world + A] = [int(x) for x in w]
         flat[world + A:world + 2 * A] = [-int(x) for x in lo]
         flat[world + 2 * A:] = [int(x) for x in hi]
-    red = _allreduce_max(flat, group, device)
+    red = flat if world == 1 else _allreduce_max(flat, group, device)  # one rank: nothing to agree
     return ([q for q in range(world) if red[q]], red[world:world + A],
             [-x for x in red[world + A:world + 2 * A]], red[world + 2 * A:])
 
@@ -633,8 +633,10 @@ def group_by_agg(df, key: str, aggs: Sequence[Expr], predicate: Expr | None = No
     reference without maintain_order.
 
     Two protocols, chosen identically on every rank:
-      partial states (the default): each rank pre-aggregates its shard and
-        only group records cross the links (volume ~ groups);
+      partial states (the default): each rank pre-aggregates its shard
+        with no collective, one small all-reduce agrees the stage's status
+        and any wide f64 sum's digit range (agree_wide), and only group
+        records cross the links (two all-to-alls, volume ~ groups);
       row shuffle: keys or values no fixed-size record carries -- String
         keys longer than 7 bytes, key tuples with Float / String columns or
         more than 63 bits, var / std with such keys or of an expression -- send the selected

@@ -554,6 +554,8 @@ class Series:
         if is_var:
             if lg is not None:
                 raise N.InvalidOperationError(f"rolling var / std of a {lg} column is not supported")
+            if not 0 <= int(ddof) <= 255:  # the reference's ddof is a u8; packed into bits 8..15 below
+                raise N.InvalidOperationError("`ddof` must be in 0..255")
             phys = _BY_CODE[self._col.dtype]
             src, f32 = self, phys is Float32
             if phys in (Int8, Int16, UInt8, UInt16, UInt32, UInt64, Float32):

@@ -25,6 +25,7 @@ import pytest
 
 import polaroid_amd as pl
 from conftest import load_golden
+from oracle import oracle as O
 from test_gpu_groupby_multi import _check
 from test_gpu_parity import _rand_frame
 
@@ -277,33 +278,62 @@ def test_fused_string_key(gpu, case):
 
 
 
-@pytest.mark.parametrize("pname", ["gt0", "ge0", "gt250"])
-@pytest.mark.parametrize("keys", ["int64", "sym_day"])
-def test_nonneg_predicate_column_sum(gpu, plgpu_option, pname, keys):
+_NONNEG_PREDS = {  # name -> (expr, the oracle's program over column 0 = close)
+    "gt0": (lambda: pl.col("close") > 0.0, [(1, 0, 0), (2, 0, 0.0), (24, 0, 0)]),
+    "ge0": (lambda: pl.col("close") >= 0.0, [(1, 0, 0), (2, 0, 0.0), (25, 0, 0)]),
+    "gt250": (lambda: pl.col("close") > 250.0, [(1, 0, 0), (2, 0, 250.0), (24, 0, 0)]),
+    "eq0": (lambda: pl.col("close") == 0.0, [(1, 0, 0), (2, 0, 0.0), (20, 0, 0)]),
+    "eq": (lambda: pl.col("close") == 3.5, [(1, 0, 0), (2, 0, 3.5), (20, 0, 0)]),
+    "gtneg": (lambda: pl.col("close") > -1.0, [(1, 0, 0), (2, 0, -1.0), (24, 0, 0)]),
+}
+
+
+@pytest.mark.parametrize("pname", list(_NONNEG_PREDS))
+@pytest.mark.parametrize("keys", ["int64", "sym_day", "runs"])
+@pytest.mark.parametrize("order", ["close_last", "close_first"])
+def test_nonneg_predicate_column_sum(gpu, plgpu_option, pname, keys, order):
     """Four sums whose last column is the fused predicate's and keeps no
     value below a literal >= 0 (the headline's close.sum() under
     close > 250) run the variant whose last limbs carry no sign
-    (gb_fast_kernel VAR 5, option sum_pos): bit-identical to the signed
-    variant on data with negatives, zeros, -0.0, NaN and +inf."""
-    rng = np.random.default_rng(len(pname) + len(keys))
+    (gb_fast_kernel VAR 5, option sum_pos).  Checked bit-exact against the
+    oracle (or_group_by_agg, SUM_EXACT) with the option on and off, on data
+    with negatives, zeros, -0.0, NaN, +inf and exact hits of the literal;
+    keys: an Int64 key, (Int64, Int32) packed in the kernel, and a sorted
+    key (the RUNS layout).  close_first puts the predicate's column in the
+    first acc: var_x_nonneg's pred_acc is then 0 and the signed kernel runs
+    (gtneg: a negative literal, never the unsigned variant)."""
+    rng = np.random.default_rng(len(pname) + len(keys) + len(order))
     n = 400_003
     sym = rng.integers(0, 100, n).astype(np.int64)
+    if keys == "runs":
+        sym = np.sort(sym)
     day = (np.arange(n) // 5000).astype(np.int32)
-    cols = {c: rng.uniform(-500, 500, n) for c in ("open", "high", "low", "close")}
+    names = ["open", "high", "low", "close"] if order == "close_last" else ["close", "open", "high", "low"]
+    cols = {c: rng.uniform(-500, 500, n) for c in names}
     x = cols["close"]
     x[rng.random(n) < 0.05] = 0.0
     x[rng.random(n) < 0.05] = -0.0
+    x[rng.random(n) < 0.02] = 3.5
     x[rng.integers(0, n, 3)] = np.nan
     x[rng.integers(0, n, 2)] = np.inf
+    x[rng.integers(0, n, 2)] = -np.inf
     df = pl.DataFrame({"sym": pl.Series.from_numpy("sym", sym), "day": pl.Series.from_numpy("day", day),
                        **{c: pl.Series.from_numpy(c, v) for c, v in cols.items()}})
-    p = {"gt0": pl.col("close") > 0.0, "ge0": pl.col("close") >= 0.0, "gt250": pl.col("close") > 250.0}[pname]
-    by = ["sym"] if keys == "int64" else ["sym", "day"]
-    res = []
+    mk, prog = _NONNEG_PREDS[pname]
+    by = ["sym", "day"] if keys == "sym_day" else ["sym"]
+    hk = [(sym, None)] + ([(day, None)] if keys == "sym_day" else [])
+    hc = [O.HostCol(cols[c]) for c in ["close"] + [c for c in names if c != "close"]]
+    oidx = {c: i for i, c in enumerate(["close"] + [c for c in names if c != "close"])}
+    okeys, oouts = O.group_by_agg_multi(hk, hc, prog, [("sum", oidx[c]) for c in names], n)
+    want = {tuple(int(k[0][i]) for k in okeys): [o[0][i] for o in oouts] for i in range(len(okeys[0][0]))}
     for on in (1, 0):
         plgpu_option("sum_pos", on)
-        out = df.lazy().filter(p).group_by(*by).agg(*[pl.col(c).sum() for c in cols]).collect()
-        o = np.lexsort([out[k].to_numpy() for k in reversed(by)])
-        res.append([out[k].to_numpy()[o] for k in by] + [out[c].to_numpy()[o].view(np.int64) for c in cols])
-    for a, b in zip(res[0], res[1]):
-        assert np.array_equal(a, b), pname
+        info = {}
+        out = df.lazy().filter(mk()).group_by(*by).agg(*[pl.col(c).sum() for c in names]).collect(info=info)
+        assert out.height == len(want), (pname, on)
+        kc = [out[k].to_numpy() for k in by]
+        vc = [out[c].to_numpy() for c in names]
+        for i in range(out.height):
+            w = want[tuple(int(k[i]) for k in kc)]
+            got = np.array([v[i] for v in vc])
+            assert np.array_equal(got.view(np.int64), np.array(w).view(np.int64)), (pname, keys, order, on, i)

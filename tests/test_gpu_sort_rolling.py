@@ -458,3 +458,18 @@ def test_rolling_var_expression(gpu):
     out = df.select(pl.col("a").rolling_var(2).alias("v"), pl.col("a").rolling_std(2, ddof=0).alias("s"))
     assert out["v"].to_list() == [None, 8.0, 2.0, 0.5]
     assert out["s"].to_list() == [None, 2.0, 1.0, 0.5]
+
+
+def test_rolling_var_ddof_range(gpu):
+    """ddof is the reference's u8 (rolling/no_nulls/moment.rs RollingVarParams):
+    the Series and Expr paths both refuse values outside 0..255 instead of
+    wrapping them into the packed kind code."""
+    s = pl.Series("a", [1.0, 5.0, 3.0, 4.0])
+    for ddof in (-1, 256):
+        with pytest.raises(pl.InvalidOperationError):
+            s.rolling_var(2, ddof=ddof)
+        with pytest.raises(pl.InvalidOperationError):
+            s.rolling_std(2, ddof=ddof)
+        with pytest.raises(pl.InvalidOperationError):
+            pl.DataFrame({"a": [1.0, 2.0]}).select(pl.col("a").rolling_std(2, ddof=ddof))
+    assert s.rolling_var(2, ddof=255).to_list() == [None, None, None, None]

@@ -400,7 +400,8 @@ def test_var_triple_nonneg_predicate(gpu, plgpu_option, pname):
     (x > c, x >= c, x == c, c >= 0) runs the triple variant whose x limbs
     carry no sign (gb_fast_kernel VAR 4, option var_pos): bit-identical to
     the signed variant on data with negatives, zeros, -0.0, NaN and +inf
-    (the predicate drops the negatives; NaN compares greatest and is kept)."""
+    (the predicate drops the negatives; NaN compares greatest and is kept),
+    and against the exact variance per group."""
     rng = np.random.default_rng(len(pname))
     n = 300_003
     key = rng.integers(0, 100, n).astype(np.int64)
@@ -424,3 +425,18 @@ def test_var_triple_nonneg_predicate(gpu, plgpu_option, pname):
         res.append((out["k"].to_numpy()[o], out["s"].to_numpy()[o].view(np.int64), out["s"].validity_numpy()[o]))
     for a, b in zip(res[0], res[1]):
         assert np.array_equal(a, b), pname
+    # and against the exact value (rational arithmetic, rounded once; the
+    # fused triple's std is sqrt of the correctly rounded variance): groups
+    # with a kept NaN / inf are NaN, a single kept row is null
+    sel = {"gt0": x > 0.0, "ge0": x >= 0.0, "gt250": x > 250.0, "eq": x == 3.5}[pname] | (np.isnan(x) & (pname != "eq"))
+    ks, sbits, sok = res[0]
+    sv = sbits.view(np.float64)
+    assert np.array_equal(ks, np.unique(key[sel]))
+    for i, k in enumerate(ks.tolist()):
+        vals = x[sel & (key == k)]
+        if vals.size <= 1:
+            assert not sok[i], k
+        elif not np.all(np.isfinite(vals)):
+            assert sok[i] and math.isnan(sv[i]), k
+        else:
+            assert sok[i] and math.isclose(sv[i], math.sqrt(_exact_var(vals, 1)), rel_tol=4e-16, abs_tol=0.0), k

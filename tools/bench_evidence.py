@@ -36,18 +36,18 @@ HBM_PEAK = 8000.0
 # PACK = 1 variant with equal launch counts: "first" / "second" half of that
 # kernel's launches in trace order.
 LEGS = {
-    "headline": (r"gb_fast_kernel<4, 1, true, 2, 2, false, false, false, [05], 0>", "headline", True),
-    "vwap": (r"gb_fast_kernel<2, 1, true, 2, 2, false, false, false, 2, 0>", "vwap", True),
-    "std": (r"gb_fast_kernel<3, 1, true, 2, 2, false, false, false, [14], 0>", "std", True),
-    "keys_categorical": (r"gb_fast_kernel<4, 1, true, 2, 2, false, false, false, [05], 1>", "keys_categorical",
+    "headline": (r"gb_fast_kernel<4, 1, true, 2, 2, false, false, false, [05], 0, false>", "headline", True),
+    "vwap": (r"gb_fast_kernel<2, 1, true, 2, 2, false, false, false, 2, 0, false>", "vwap", True),
+    "std": (r"gb_fast_kernel<3, 1, true, 2, 2, false, false, false, [14], 0, false>", "std", True),
+    "keys_categorical": (r"gb_fast_kernel<4, 1, true, 2, 2, false, false, false, [05], 1, false>", "keys_categorical",
                          ("first", True)),
-    "keys_string": (r"gb_fast_kernel<4, 1, true, 2, 2, false, false, false, [05], 2>", "keys_string", True),
-    "keys_sym_day": (r"gb_fast_kernel<4, 1, true, 2, 2, false, false, false, [05], 1>", "keys_sym_day",
+    "keys_string": (r"gb_fast_kernel<4, 1, true, 2, 2, false, false, false, [05], 2, false>", "keys_string", True),
+    "keys_sym_day": (r"gb_fast_kernel<4, 1, true, 2, 2, false, false, false, [05], 1, false>", "keys_sym_day",
                      ("second", True)),
     "sort": (r"aos_gather_kernel<8>", "sort", False),
     "sort_pack": (r"aos_pack_kernel<8>", "sort_pack", True),
     "rolling": (r"rl_wave_kernel<4, false, false>", "rolling", True),
-    "join": (r"jn_probe_match_kernel<false, 0, false, true>", "join", False),
+    "join": (r"rj_match_kernel<", "join", False),
     "join_emit": (r"jn_take_emit_kernel<2, 1>", "join_emit", True),
     "filter": (r"filter_(scatter8|fused8)_kernel", "filter", True),
     "filter_mask": (r"filter_mask_kernel", "filter_mask", True),
@@ -57,9 +57,12 @@ LEGS = {
 # launch per scatter level, each level its own template instance); the
 # line's kernel_ms is the per-step sum, so the trace side is the sum over
 # the kernel's instances of the mean of their last timed launches.  No other
-# leg launches these kernels.
-MG_KERNELS = {"count": r"gbp_count_kernel", "scatter": r"gbp_scatter_kernel",
-              "aggregate": r"gb_fast_kernel<\d+, 0, true, 2, 2, (true|false), true"}
+# leg launches these instances.
+# (null-free instances only: the nulls leg runs the NUL = true ones; the
+# partitioned join runs <0, false, true, false>, the keyless-predicate form)
+MG_KERNELS = {"count": r"gbp_count_kernel<(1, false|0, true), true, false>",
+              "scatter": r"gbp_scatter_kernel<(1, false|0, true), true, false>",
+              "aggregate": r"gb_fast_kernel<\d+, 0, true, 2, 2, (true|false), true, false, 0, 0, false>"}
 
 
 def last_json(path):
