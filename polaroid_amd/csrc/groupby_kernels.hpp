@@ -920,8 +920,13 @@ struct FastTile {
     uint64_t pv[ROWS];
     // NUL: null bits of each row pair, row 2q in bits 0-7 and row 2q + 1 in
     // bits 8-15 of nv[q] (the part_nulls layout: bit a acc a, 6 the key, 7
-    // the predicate's own column)
+    // the predicate's own column).  fast_nulls leaves the loaded validity
+    // words raw in nr[q][column] (column NACC the key, NACC + 1 the
+    // predicate's own) and fast_nulls_finish turns them into nv when the
+    // tile is consumed: a shift of a loaded word at prefetch time would make
+    // the next tile's loads wait for it (one HBM latency per tile).
     uint32_t nv[NUL ? (ROWS + 1) / 2 : 1];
+    uint32_t nr[NUL ? (ROWS + 1) / 2 : 1][NUL ? (NACC > 0 ? NACC : 1) + 2 : 1];
 };
 
 // Row j of tile t for this thread: pairs of consecutive rows, pair q at
@@ -1048,37 +1053,40 @@ __device__ __forceinline__ void fast_load(const GbParams& p, int64_t t, FastTile
     }
 }
 
-// Null bits of rows r, r + 1 of a column (r and the column offset even, so
-// both bits sit in one validity byte): bit 0 row r, bit 1 row r + 1, set =
-// null; 0 without a bitmap.
-__device__ __forceinline__ uint32_t pair_nulls(const DevCol& c, int64_t r) {
-    if (!c.validity) return 0u;
-    const uint64_t b = (uint64_t)(c.offset + r);
-    const uint32_t byte = __builtin_nontemporal_load(c.validity + (b >> 3));
-    return ~(byte >> (b & 7)) & 3u;
+// Bit position of row r of a column in 32-bit words counted from the
+// bitmap's address rounded down to 4 bytes: a word read there never leaves
+// the aligned word of a bitmap byte (no page crossing, any byte alignment).
+__device__ __forceinline__ uint64_t pair_bit(const DevCol& c, int64_t r) {
+    return ((uint64_t)(uintptr_t)c.validity & 3u) * 8u + (uint64_t)(c.offset + r);
 }
 
-// Null bits of this lane's row pair from the 128-bit window of a wave's
-// 128 consecutive rows (first row rw, a multiple of 128; the column offset
-// a multiple of 64): lanes load the window's two aligned words alternately
-// (one request per wave), every lane takes both words by readlane and its
-// two bits (rows rw + 2 lane, + 1) by a shift.
-__device__ __forceinline__ uint32_t pair_nulls_words(const DevCol& c, int64_t rw) {
-    if (!c.validity) return 0u;
+// The validity word holding rows r, r + 1 of a column (r and the column
+// offset even, so both bits sit in one 32-bit word), raw: set = valid; ~0
+// without a bitmap.  Its bits are taken at pair_bit & 31 (fast_nulls_finish).
+__device__ __forceinline__ uint32_t pair_word(const DevCol& c, int64_t r) {
+    if (!c.validity) return ~0u;
+    const uint32_t* w = (const uint32_t*)((uintptr_t)c.validity & ~(uintptr_t)3);
+    return __builtin_nontemporal_load(w + (pair_bit(c, r) >> 5));
+}
+
+// The 32-bit word of a wave's 128-row window (first row rw, a multiple of
+// 128; the column offset a multiple of 64) that holds this lane's row pair
+// (rows rw + 2 lane, + 1): 16 lanes share each of the window's four words,
+// one request per wave.  The pair's bits are at (2 lane) & 31.
+__device__ __forceinline__ uint32_t pair_word_wave(const DevCol& c, int64_t rw) {
+    if (!c.validity) return ~0u;
     const int lane = threadIdx.x & 63;
-    const uint64_t* w = (const uint64_t*)c.validity + ((uint64_t)(c.offset + rw) >> 6);
-    const uint64_t mine = __builtin_nontemporal_load(w + (lane & 1));
-    const uint32_t lo0 = __builtin_amdgcn_readlane((uint32_t)mine, 0), hi0 = __builtin_amdgcn_readlane((uint32_t)(mine >> 32), 0);
-    const uint32_t lo1 = __builtin_amdgcn_readlane((uint32_t)mine, 1), hi1 = __builtin_amdgcn_readlane((uint32_t)(mine >> 32), 1);
-    const uint64_t word = lane < 32 ? ((uint64_t)hi0 << 32 | lo0) : ((uint64_t)hi1 << 32 | lo1);
-    return ~(uint32_t)(word >> (2 * (lane & 31))) & 3u;
+    const uint64_t b = (uint64_t)(c.offset + rw) + 2u * (uint32_t)lane;
+    return __builtin_nontemporal_load((const uint32_t*)c.validity + (b >> 5));
 }
 
-// NUL: the tile's null bits (FastTile::nv), from the columns' validity
-// bitmaps (one byte per row pair and column, or whole words: p.vwords) or,
-// over the partition buffers (PART), from part_nulls (two bytes per pair).
-// Rows past n (the masked tail tile) read nothing.  Issued before the
-// tile's value loads, so the bits arrive first.
+// NUL: the tile's validity words (FastTile::nr), from the columns' bitmaps
+// (whole words per wave when p.vwords, else the word of each pair) or, over
+// the partition buffers (PART), part_nulls (two bytes per pair, already in
+// nv's layout).  Rows past n (the masked tail tile) read nothing.  Issued
+// before the tile's value loads; nothing here waits for them.  (p.vwords:
+// 8-byte aligned bitmaps at offsets that are multiples of 64, so the
+// wave-window word and pair_bit agree.)
 template <int NACC, int PRED, int ROWS, bool PART, bool DERIV, int PACK, bool NUL>
 __device__ __forceinline__ void fast_nulls(const GbParams& p, int64_t t, FastTile<NACC, ROWS, DERIV, PACK, NUL>& x,
                                            int64_t rbase, int64_t rmax, bool full) {
@@ -1088,36 +1096,60 @@ __device__ __forceinline__ void fast_nulls(const GbParams& p, int64_t t, FastTil
         for (int q = 0; q < ROWS / 2; ++q) {
             int64_t r = rbase + fast_row(t, T, ROWS, 2 * q);
             if (rmax >= 0) r = r < rmax ? r : rmax;
-            uint32_t m = 0;
             if (PART) {
-                if (p.part_nulls) m = __builtin_nontemporal_load((const uint16_t*)(p.part_nulls + r));
+                x.nr[q][0] = p.part_nulls ? __builtin_nontemporal_load((const uint16_t*)(p.part_nulls + r)) : 0u;
             } else if (full && p.vwords) {
                 // a full tile: the wave's 128 rows end at or below n_full, a
-                // multiple of 1024, so the two words lie inside the bitmap
+                // multiple of 1024, so the words lie inside the bitmap
                 const int64_t rw = r - 2 * (threadIdx.x & 63);
 #pragma unroll
-                for (int c = 0; c < NACC; ++c) {
-                    const uint32_t b = pair_nulls_words(p.acc[c].c, rw);
-                    m |= ((b & 1u) << c) | ((b >> 1) << (8 + c));
-                }
-                const uint32_t bk = pair_nulls_words(p.key, rw);
-                m |= ((bk & 1u) << 6) | ((bk >> 1) << 14);
-                if (PRED == 1 && p.pred_acc < 0) {
-                    const uint32_t bp = pair_nulls_words(p.pred_col, rw);
-                    m |= ((bp & 1u) << 7) | ((bp >> 1) << 15);
-                }
+                for (int c = 0; c < NACC; ++c) x.nr[q][c] = pair_word_wave(p.acc[c].c, rw);
+                x.nr[q][NACC] = pair_word_wave(p.key, rw);
+                x.nr[q][NACC + 1] = PRED == 1 && p.pred_acc < 0 ? pair_word_wave(p.pred_col, rw) : ~0u;
             } else if (r < p.n) {
 #pragma unroll
-                for (int c = 0; c < NACC; ++c) {
-                    const uint32_t b = pair_nulls(p.acc[c].c, r);
-                    m |= ((b & 1u) << c) | ((b >> 1) << (8 + c));
-                }
-                const uint32_t bk = pair_nulls(p.key, r);
-                m |= ((bk & 1u) << 6) | ((bk >> 1) << 14);
-                if (PRED == 1 && p.pred_acc < 0) {
-                    const uint32_t bp = pair_nulls(p.pred_col, r);
-                    m |= ((bp & 1u) << 7) | ((bp >> 1) << 15);
-                }
+                for (int c = 0; c < NACC; ++c) x.nr[q][c] = pair_word(p.acc[c].c, r);
+                x.nr[q][NACC] = pair_word(p.key, r);
+                x.nr[q][NACC + 1] = PRED == 1 && p.pred_acc < 0 ? pair_word(p.pred_col, r) : ~0u;
+            } else {
+#pragma unroll
+                for (int c = 0; c < NACC + 2; ++c) x.nr[q][c] = ~0u;
+            }
+        }
+    }
+}
+
+// NUL: the raw words of fast_nulls as FastTile::nv, once the tile's loads
+// have landed.  A pair's bits sit at pair_bit & 31 of its word (with
+// p.vwords that is (2 lane) & 31).
+template <int NACC, int PRED, int ROWS, bool PART, bool DERIV, int PACK, bool NUL>
+__device__ __forceinline__ void fast_nulls_finish(const GbParams& p, int64_t t,
+                                                  FastTile<NACC, ROWS, DERIV, PACK, NUL>& x, int64_t rbase,
+                                                  int64_t rmax) {
+    if constexpr (NUL) {
+        const int T = blockDim.x;
+#pragma unroll
+        for (int q = 0; q < ROWS / 2; ++q) {
+            if (PART) {
+                x.nv[q] = x.nr[q][0];
+                continue;
+            }
+            int64_t r = rbase + fast_row(t, T, ROWS, 2 * q);
+            if (rmax >= 0) r = r < rmax ? r : rmax;
+            auto bits = [&](const DevCol& c, uint32_t w) -> uint32_t {
+                return ~(w >> ((uint32_t)pair_bit(c, r) & 31u)) & 3u;
+            };
+            uint32_t m = 0;
+#pragma unroll
+            for (int c = 0; c < NACC; ++c) {
+                const uint32_t b = bits(p.acc[c].c, x.nr[q][c]);
+                m |= ((b & 1u) << c) | ((b >> 1) << (8 + c));
+            }
+            const uint32_t bk = bits(p.key, x.nr[q][NACC]);
+            m |= ((bk & 1u) << 6) | ((bk >> 1) << 14);
+            if (PRED == 1) {
+                const uint32_t bp = bits(p.pred_col, x.nr[q][NACC + 1]);
+                m |= ((bp & 1u) << 7) | ((bp >> 1) << 15);
             }
             x.nv[q] = m;
         }
@@ -1430,6 +1462,7 @@ __global__ __launch_bounds__(PART && !RUNS ? kGbPartThreads : kGbThreads) void g
     if (t < nall) load_tile(t, cur);
     for (; t < nall; t += tstep) {
         if constexpr (!VAR) fast_share<NACC, ROWS, DERIV, PACK, NULLS>(vf0, wf0, cur);
+        fast_nulls_finish<NL, PRED, ROWS, PART, DERIV, PACK, NULLS>(p, t, cur, rbase, rmax);
         bool kout[ROWS];
         constexpr bool kstr = PACK == 2;
         if (kstr) {
