@@ -185,15 +185,6 @@ __device__ __forceinline__ void ps_col(const DevCol& c, const uint64_t* buf, con
 // GbParams::part_nulls bits, a null predicate value drops the row, and a
 // null-key row is spread over the partitions by its position (ps_digit):
 // it aggregates into the null group wherever it lands.
-// Null bit of row rb + lane of a column whose bitmap holds whole aligned
-// words for the wave's 64 rows (rb a multiple of 64, p.vwords): one uniform
-// word load per wave.  1 = null.
-__device__ __forceinline__ uint32_t ps_null_word(const DevCol& c, int64_t rb) {
-    if (!c.validity) return 0u;
-    const uint64_t w = ((const uint64_t*)c.validity)[(uint64_t)(c.offset + rb) >> 6];
-    return (uint32_t)(~w >> (threadIdx.x & 63)) & 1u;
-}
-
 template <int PRED, bool L2, bool F8, bool NUL = false, bool ACCS = true>
 __device__ __forceinline__ void ps_keys(const GbParams& p, const DevProgram& prog, const PartOut& in, const PsTile& tl,
                                         int c0, uint64_t (&key)[kPsPer], uint64_t (&pv)[kPsPer],
@@ -205,6 +196,24 @@ __device__ __forceinline__ void ps_keys(const GbParams& p, const DevProgram& pro
     // one word per column (ACCS: the aggregated columns' bits too -- the
     // count pass needs only the key's and the predicate's)
     const bool words = NUL && !L2 && p.vwords && tl.lo == tl.base && tl.hi - tl.base == kPsTile;
+    // words: every column's validity word of each of the wave's kPsPer row
+    // blocks, loaded first and together (uniform loads with no dependence
+    // between them), the bits taken afterwards; ~0 (all valid) for a column
+    // without a bitmap
+    uint64_t wk[kPsPer], wp[kPsPer], wa[kMaxAcc][kPsPer];
+    if (NUL && !L2 && words) {
+        auto word = [&](const DevCol& c, int64_t rb) -> uint64_t {
+            return c.validity ? ((const uint64_t*)c.validity)[(uint64_t)(c.offset + rb) >> 6] : ~0ull;
+        };
+#pragma unroll
+        for (int k = 0; k < kPsPer; ++k) {
+            const int64_t rb = tl.base + c0 + k * 64;
+            wk[k] = word(p.key, rb);
+            wp[k] = PRED == 1 ? word(p.pred_col, rb) : ~0ull;
+#pragma unroll
+            for (int a = 0; a < kMaxAcc; ++a) wa[a][k] = ACCS && a < p.nacc ? word(p.acc[a].c, rb) : ~0ull;
+        }
+    }
 #pragma unroll
     for (int k = 0; k < kPsPer; ++k) {
         const int64_t r = tl.base + c0 + k * 64 + lane;
@@ -214,12 +223,11 @@ __device__ __forceinline__ void ps_keys(const GbParams& p, const DevProgram& pro
         if (NUL && L2) {
             nb[k] = in.nulls && s ? in.nulls[r] : 0u;
         } else if (NUL && words) {
-            const int64_t rb = r - lane;
-            uint32_t m = ps_null_word(p.key, rb) << 6;
-            if (ACCS)
-                for (int a = 0; a < p.nacc; ++a) m |= ps_null_word(p.acc[a].c, rb) << a;
+            uint32_t m = ((uint32_t)(~wk[k] >> lane) & 1u) << 6;
+#pragma unroll
+            for (int a = 0; a < kMaxAcc; ++a) m |= ((uint32_t)(~wa[a][k] >> lane) & 1u) << a;
             nb[k] = m;
-            if (PRED == 1) pvalid = !ps_null_word(p.pred_col, rb);
+            if (PRED == 1) pvalid = ((wp[k] >> lane) & 1u) != 0;
         } else if (NUL && s) {
             uint32_t m = dev_valid(p.key, r) ? 0u : 0x40u;
             if (ACCS)
@@ -387,6 +395,10 @@ __global__ __launch_bounds__(kPsThreads) void gbp_scatter_kernel(GbParams p, Dev
             } else if (use_pv) {
 #pragma unroll
                 for (int k = 0; k < kPsPer; ++k) cv[k] = pv[k];
+                if (NUL && !L2) {
+#pragma unroll
+                    for (int k = 0; k < kPsPer; ++k) cv[k] = ((nb[k] >> a) & 1u) ? 0ull : cv[k];
+                }
             } else if (rows && L2) {
                 const uint32_t* b = in.rows + tl.base;
                 ps_rows(tl, c0, [&](int k, uint32_t i) { cv[k] = (uint64_t)__builtin_nontemporal_load(b + i); });
@@ -394,6 +406,12 @@ __global__ __launch_bounds__(kPsThreads) void gbp_scatter_kernel(GbParams p, Dev
                 ps_rows(tl, c0, [&](int k, uint32_t i) { cv[k] = (uint64_t)(tl.base + (int64_t)i); });
             } else {
                 ps_col<L2, F8>(p.acc[a].c, L2 ? in.acc[a] : nullptr, tl, c0, cv);
+                // level 1: a null value is written as 0 (+0.0), which a sum
+                // adds as nothing; the other aggregations read its null bit
+                if (NUL && !L2) {
+#pragma unroll
+                    for (int k = 0; k < kPsPer; ++k) cv[k] = ((nb[k] >> a) & 1u) ? 0ull : cv[k];
+                }
             }
         }
         if (col <= p.nacc) {
@@ -941,6 +959,117 @@ struct FinParams {
     uint8_t* vbytes;
 };
 
+// Table slot s (len selected rows) -> output row g: the key, its validity
+// byte, the first row, and every output's value and validity byte.
+__device__ void fin_slot(const GbParams& p, const FinParams& fp, const uint64_t* tab, int64_t stride, int64_t s,
+                         int special, int64_t g, uint64_t len) {
+    if (g >= fp.cap) return;
+    auto F = [&](int f) { return tab + (int64_t)f * stride + s; };
+    const bool null_key = special == 1;
+    fp.out_keys[g] = null_key ? 0 : (int64_t)(special == 2 ? kEmptyKey : *F(0));
+    fp.vbytes[g] = null_key ? 0 : 1;
+    if (fp.out_first) fp.out_first[g] = *F(p.f_first);
+    for (int o = 0; o < fp.nout; ++o) {
+        const OutSpec& os = fp.out[o];
+        const AccSpec& ac = p.acc[os.acc];
+        bool valid = true;
+        const uint64_t cnt = ac.f_cnt >= 0 ? *F(ac.f_cnt) : len;
+        const uint64_t flags = ac.f_flags >= 0 ? *F(ac.f_flags) : 0;
+        switch (os.kind) {
+        case PLGPU_AGG_LEN: ((uint32_t*)os.values)[g] = (uint32_t)len; break;
+        case PLGPU_AGG_COUNT: ((uint32_t*)os.values)[g] = (uint32_t)cnt; break;
+        case PLGPU_AGG_SUM:
+        case PLGPU_AGG_MEAN: {
+            if (os.kind == PLGPU_AGG_SUM && !os.in_isf) {
+                // wrapping integer sum, stored at the output width
+                dev_store(os.values, os.out_dtype, g, *F(ac.f_isum));
+                break;
+            }
+            double sum;
+            if (flags & FL_NAN || ((flags & FL_PINF) && (flags & FL_NINF))) sum = __builtin_nan("");
+            else if (flags & FL_PINF) sum = __builtin_inf();
+            else if (flags & FL_NINF) sum = -__builtin_inf();
+            else if (fp.wide[os.acc]) sum = fp.wide[os.acc][s];
+            else sum = fx_to_double(*F(ac.f_sum), *F(ac.f_sum + 1),
+                                    *F(ac.f_sum + 2), p.bottoms[os.acc]);
+            if (os.kind == PLGPU_AGG_MEAN) {
+                if (cnt == 0) { valid = false; sum = 0.0; }
+                else sum = sum / (double)cnt;
+            }
+            dev_store(os.values, os.out_dtype, g, f64_bits(sum));  // Float32: rounded once more
+            break;
+        }
+        case PLGPU_AGG_VAR:
+        case PLGPU_AGG_STD: {
+            // moment.rs:126 VarState::finalize: null when count <= ddof;
+            // an inf / NaN value makes it NaN
+            double v = 0.0;
+            if (cnt <= (uint64_t)os.ddof) {
+                valid = false;
+            } else if (flags) {
+                v = __builtin_nan("");
+            } else {
+                const AccSpec& ah = p.acc[os.acc_hi];
+                const AccSpec& al = p.acc[os.acc_lo];
+                const uint64_t hf = *F(ah.f_flags) | *F(al.f_flags);
+                double num = 0.0;
+                const bool ok = hf == 0 &&
+                                var_exact(*F(ac.f_sum), *F(ac.f_sum + 1),
+                                          *F(ac.f_sum + 2), p.bottoms[os.acc],
+                                          *F(ah.f_sum), *F(ah.f_sum + 1),
+                                          *F(ah.f_sum + 2), p.bottoms[os.acc_hi],
+                                          *F(al.f_sum), *F(al.f_sum + 1),
+                                          *F(al.f_sum + 2), p.bottoms[os.acc_lo], cnt, num);
+                if (!ok) {
+                    // x * x overflowed, or the exact state left the accumulator
+                    atomicOr((unsigned long long*)&p.status[ST_VAR_OUT], 1ull);
+                } else {
+                    v = (num / (double)cnt) / (double)(cnt - (uint64_t)os.ddof);
+                    if (os.kind == PLGPU_AGG_STD) v = __builtin_sqrt(v);
+                }
+            }
+            ((double*)os.values)[g] = v;
+            break;
+        }
+        case PLGPU_AGG_MIN:
+        case PLGPU_AGG_MAX: {
+            const uint64_t o = *F(os.kind == PLGPU_AGG_MIN ? ac.f_min : ac.f_max);
+            const bool none = os.kind == PLGPU_AGG_MIN ? (o == ~0ull) : (o == 0ull);
+            if (os.in_isf) {
+                double v;
+                if (cnt == 0) { valid = false; v = 0.0; }
+                else if (none) v = __builtin_nan("");  // every valid value was NaN
+                else v = as_f64(unord_f64(o));
+                dev_store(os.values, os.out_dtype, g, f64_bits(v));
+            } else {
+                // (the all-ones / all-zeros "none" encodings are real
+                // values here: an integer group with cnt > 0 has one)
+                const uint64_t v = cnt == 0 ? 0ull : (os.in_uns ? o : (o ^ 0x8000000000000000ull));
+                if (cnt == 0) valid = false;
+                dev_store(os.values, os.out_dtype, g, v);
+            }
+            break;
+        }
+        case PLGPU_AGG_FIRST:
+        case PLGPU_AGG_LAST: {
+            // the value (null included) of the group's first / last
+            // selected row (polars-expr/src/reduce/first_last.rs)
+            const int64_t row = (int64_t)*F(os.kind == PLGPU_AGG_FIRST ? p.f_first : p.f_last);
+            if (!gb_ok(row >= 0 && row < p.n, CK_FIRST_ROW)) {
+                valid = false;
+                break;
+            }
+            const uint64_t v0 = acc_value(ac, row, valid);
+            const uint64_t v = valid ? v0 : 0ull;
+            dev_store(os.values, os.out_dtype, g, v);
+            break;
+        }
+        default: break;
+        }
+        if (os.validity) fp.vbytes[(int64_t)(1 + o) * fp.cap + g] = valid ? 1 : 0;
+    }
+}
+
 __global__ __launch_bounds__(256) void gb_finalize_kernel(GbParams p, FinParams fp) {
     const int64_t total = p.gcap + 2;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -982,111 +1111,25 @@ __global__ __launch_bounds__(256) void gb_finalize_kernel(GbParams p, FinParams 
         run += chunk;
         if (len == 0) continue;
         const int64_t g = (int64_t)base + __popcll(live & lt);
-        if (g >= fp.cap) continue;
-        const bool null_key = s == p.gcap;
-        fp.out_keys[g] = null_key ? 0 : (int64_t)(s == p.gcap + 1 ? kEmptyKey : *gfield(p, 0, s));
-        fp.vbytes[g] = null_key ? 0 : 1;
-        if (fp.out_first) fp.out_first[g] = *gfield(p, p.f_first, s);
-        for (int o = 0; o < fp.nout; ++o) {
-            const OutSpec& os = fp.out[o];
-            const AccSpec& ac = p.acc[os.acc];
-            bool valid = true;
-            const uint64_t cnt = ac.f_cnt >= 0 ? *gfield(p, ac.f_cnt, s) : len;
-            const uint64_t flags = ac.f_flags >= 0 ? *gfield(p, ac.f_flags, s) : 0;
-            switch (os.kind) {
-            case PLGPU_AGG_LEN: ((uint32_t*)os.values)[g] = (uint32_t)len; break;
-            case PLGPU_AGG_COUNT: ((uint32_t*)os.values)[g] = (uint32_t)cnt; break;
-            case PLGPU_AGG_SUM:
-            case PLGPU_AGG_MEAN: {
-                if (os.kind == PLGPU_AGG_SUM && !os.in_isf) {
-                    // wrapping integer sum, stored at the output width
-                    dev_store(os.values, os.out_dtype, g, *gfield(p, ac.f_isum, s));
-                    break;
-                }
-                double sum;
-                if (flags & FL_NAN || ((flags & FL_PINF) && (flags & FL_NINF))) sum = __builtin_nan("");
-                else if (flags & FL_PINF) sum = __builtin_inf();
-                else if (flags & FL_NINF) sum = -__builtin_inf();
-                else if (fp.wide[os.acc]) sum = fp.wide[os.acc][s];
-                else sum = fx_to_double(*gfield(p, ac.f_sum, s), *gfield(p, ac.f_sum + 1, s),
-                                        *gfield(p, ac.f_sum + 2, s), p.bottoms[os.acc]);
-                if (os.kind == PLGPU_AGG_MEAN) {
-                    if (cnt == 0) { valid = false; sum = 0.0; }
-                    else sum = sum / (double)cnt;
-                }
-                dev_store(os.values, os.out_dtype, g, f64_bits(sum));  // Float32: rounded once more
-                break;
-            }
-            case PLGPU_AGG_VAR:
-            case PLGPU_AGG_STD: {
-                // moment.rs:126 VarState::finalize: null when count <= ddof;
-                // an inf / NaN value makes it NaN
-                double v = 0.0;
-                if (cnt <= (uint64_t)os.ddof) {
-                    valid = false;
-                } else if (flags) {
-                    v = __builtin_nan("");
-                } else {
-                    const AccSpec& ah = p.acc[os.acc_hi];
-                    const AccSpec& al = p.acc[os.acc_lo];
-                    const uint64_t hf = *gfield(p, ah.f_flags, s) | *gfield(p, al.f_flags, s);
-                    double num = 0.0;
-                    const bool ok = hf == 0 &&
-                                    var_exact(*gfield(p, ac.f_sum, s), *gfield(p, ac.f_sum + 1, s),
-                                              *gfield(p, ac.f_sum + 2, s), p.bottoms[os.acc],
-                                              *gfield(p, ah.f_sum, s), *gfield(p, ah.f_sum + 1, s),
-                                              *gfield(p, ah.f_sum + 2, s), p.bottoms[os.acc_hi],
-                                              *gfield(p, al.f_sum, s), *gfield(p, al.f_sum + 1, s),
-                                              *gfield(p, al.f_sum + 2, s), p.bottoms[os.acc_lo], cnt, num);
-                    if (!ok) {
-                        // x * x overflowed, or the exact state left the accumulator
-                        atomicOr((unsigned long long*)&p.status[ST_VAR_OUT], 1ull);
-                    } else {
-                        v = (num / (double)cnt) / (double)(cnt - (uint64_t)os.ddof);
-                        if (os.kind == PLGPU_AGG_STD) v = __builtin_sqrt(v);
-                    }
-                }
-                ((double*)os.values)[g] = v;
-                break;
-            }
-            case PLGPU_AGG_MIN:
-            case PLGPU_AGG_MAX: {
-                const uint64_t o = *gfield(p, os.kind == PLGPU_AGG_MIN ? ac.f_min : ac.f_max, s);
-                const bool none = os.kind == PLGPU_AGG_MIN ? (o == ~0ull) : (o == 0ull);
-                if (os.in_isf) {
-                    double v;
-                    if (cnt == 0) { valid = false; v = 0.0; }
-                    else if (none) v = __builtin_nan("");  // every valid value was NaN
-                    else v = as_f64(unord_f64(o));
-                    dev_store(os.values, os.out_dtype, g, f64_bits(v));
-                } else {
-                    // (the all-ones / all-zeros "none" encodings are real
-                    // values here: an integer group with cnt > 0 has one)
-                    const uint64_t v = cnt == 0 ? 0ull : (os.in_uns ? o : (o ^ 0x8000000000000000ull));
-                    if (cnt == 0) valid = false;
-                    dev_store(os.values, os.out_dtype, g, v);
-                }
-                break;
-            }
-            case PLGPU_AGG_FIRST:
-            case PLGPU_AGG_LAST: {
-                // the value (null included) of the group's first / last
-                // selected row (polars-expr/src/reduce/first_last.rs)
-                const int64_t row = (int64_t)*gfield(p, os.kind == PLGPU_AGG_FIRST ? p.f_first : p.f_last, s);
-                if (!gb_ok(row >= 0 && row < p.n, CK_FIRST_ROW)) {
-                    valid = false;
-                    break;
-                }
-                const uint64_t v0 = acc_value(ac, row, valid);
-                const uint64_t v = valid ? v0 : 0ull;
-                dev_store(os.values, os.out_dtype, g, v);
-                break;
-            }
-            default: break;
-            }
-            if (os.validity) fp.vbytes[(int64_t)(1 + o) * fp.cap + g] = valid ? 1 : 0;
-        }
+        fin_slot(p, fp, p.gtab, p.gcap + 2, s, s == p.gcap ? 1 : (s == p.gcap + 1 ? 2 : 0), g, len);
     }
+}
+
+// The groups of a compact-region run (GbParams::region_cnt): block q
+// finalizes region q's dense prefix of the region table into outputs
+// [off[q], off[q + 1]) (off: the exclusive scan of the region counts) and
+// adds its count to ST_GROUPS_OUT, so the overflow table's finalize
+// (gb_finalize_kernel, launched next) places its groups after them.
+__global__ __launch_bounds__(256) void gb_finalize_regions_kernel(GbParams p, FinParams fp,
+                                                                  const uint64_t* __restrict__ off, int lbits) {
+    const int q = blockIdx.x;
+    const uint64_t b = off[q], c = off[q + 1] - b;
+    const int64_t t0 = (int64_t)q << lbits;  // region q: the partition's LDS table size
+    for (uint64_t i = threadIdx.x; i < c; i += blockDim.x) {
+        const int64_t s = t0 + (int64_t)i;
+        fin_slot(p, fp, p.rtab, p.rcap, s, 0, (int64_t)(b + i), p.rtab[(int64_t)p.f_len * p.rcap + s]);
+    }
+    if (threadIdx.x == 0 && c) atomicAdd((unsigned long long*)&p.status[ST_GROUPS_OUT], (unsigned long long)c);
 }
 
 // Validity bytes (FinParams::vbytes) -> Arrow bitmaps: one 32-bit word per
@@ -1750,6 +1793,12 @@ struct GbRun {
     int part_blocks = 1;
     int part_levels = 0;                     // scatter passes taken (info)
     int rbits = 0;                           // global-table region bits (GbParams::rbits)
+    // compact regions (GbParams::region_cnt): allowed by the caller (a result
+    // read only through gb_finalize), on for this attempt (compact_now)
+    bool compact_ok = false;
+    bool compact_now = false;
+    uint32_t* region_cnt = nullptr;
+    uint64_t* rtab = nullptr;                // compact regions' table (GbParams::rtab)
     uint64_t* pbuf = nullptr;
     uint64_t* prange = nullptr;              // scan of the count matrix + partition bounds
     const uint64_t* part_range = nullptr;    // P + 1 partition boundaries (inside prange)
@@ -1778,6 +1827,8 @@ struct GbRun {
         dev_free(gtab, s);
         dev_free(status, s);
         dev_free(pbuf, s);
+        dev_free(region_cnt, s);
+        dev_free(rtab, s);
         dev_free(prange, s);
         for (auto& c : mat) plgpu_column_release(&c);
     }
@@ -2341,7 +2392,8 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
         const size_t b0 = options().part_lds_kb > 0 ? (size_t)options().part_lds_kb * 1024 : (size_t)160 * 1024;
         for (size_t budget : {b0, (size_t)80 * 1024}) {
             int lb = 13;
-            while (lb > 6 && ((size_t)fields * ((1u << lb) + 2) * 8 > budget ||
+            // (+ 256 B: the fast kernel's static LDS, compact regions' wave counts)
+            while (lb > 6 && ((size_t)fields * ((1u << lb) + 2) * 8 + 256 > budget ||
                               (size_t)p.nfields * ((1u << lb) + 2) * 8 > (size_t)160 * 1024))
                 --lb;
             const int64_t per = (int64_t(1) << lb) / 2;  // groups per partition at load 1/2
@@ -2461,7 +2513,14 @@ static int gb_partition(GbRun& R) {
     bool f8 = c8(p.key) && R.pred <= 1 && (R.pred == 0 || c8(p.pred_col));
     for (int a = 0; a < p.nacc; ++a) f8 = f8 && c8(p.acc[a].c);
     bool nul = p.key.validity != nullptr || (R.pred == 1 && p.pred_col.validity != nullptr);
+    // the count pass reads only the key's and the predicate's bits
+    const bool nul_cnt = nul;
     for (int a = 0; a < p.nacc; ++a) nul = nul || p.acc[a].c.validity != nullptr;
+    // sum-only accs (every one an f64 sum): the level-1 scatter writes a null
+    // value as +0.0, which the exact sum adds as nothing, so the partition
+    // buffers carry null bits only for a nullable key (nul_out); other
+    // aggregations keep every value's bit
+    const bool nul_out = R.pl.sum_only ? p.key.validity != nullptr : nul;
     PsGeom g1;
     std::memset(&g1, 0, sizeof g1);
     g1.n = p.n;
@@ -2479,7 +2538,7 @@ static int gb_partition(GbRun& R) {
     if (!rc) rc = dev_alloc((void**)&part, (size_t)((ncnt1 + kScanChunk - 1) / kScanChunk + 2) * 8, s);
     std::vector<uint64_t> hr1((size_t)P1 + 1);
     if (!rc) {
-        hipError_t e = gbp_pass1(R, f8, nul, g1, cnt, part, false, R.pout);
+        hipError_t e = gbp_pass1(R, f8, nul_cnt, g1, cnt, part, false, R.pout);
         const int64_t nb = std::max<int64_t>(1, (ncnt1 + kScanChunk - 1) / kScanChunk);
         if (e == hipSuccess) {
             gbp_bounds_kernel<<<(P1 + 256) / 256, 256, 0, s>>>(cnt, part + nb, P1, g1.ntiles, range1);
@@ -2491,7 +2550,7 @@ static int gb_partition(GbRun& R) {
     }
     uint64_t* buf1 = nullptr;
     PartOut out1;
-    if (!rc) rc = gbp_alloc(R, (int64_t)hr1[P1], nul, &buf1, &out1);
+    if (!rc) rc = gbp_alloc(R, (int64_t)hr1[P1], nul_out, &buf1, &out1);
     if (!rc) {
         const hipError_t e = gbp_pass1(R, f8, nul, g1, cnt, part, true, out1);
         if (e != hipSuccess) rc = hip_fail(e, "gbp_scatter_kernel");
@@ -2541,8 +2600,8 @@ static int gb_partition(GbRun& R) {
                 e = hipGetLastError();
             }
             if (e == hipSuccess && g2.ntiles > 0)
-                e = nul ? gbp_pass<0, true, true, true>(R, g2, out1, cnt, part, false, out1)
-                        : gbp_pass<0, true, true>(R, g2, out1, cnt, part, false, out1);
+                e = nul_out ? gbp_pass<0, true, true, true>(R, g2, out1, cnt, part, false, out1)
+                            : gbp_pass<0, true, true>(R, g2, out1, cnt, part, false, out1);
             if (e == hipSuccess) {
                 gbp_bounds2_kernel<<<(P + 256) / 256, 256, 0, s>>>(cnt, range1, meta, P1, b2, range);
                 e = hipGetLastError();
@@ -2551,10 +2610,10 @@ static int gb_partition(GbRun& R) {
             if (e == hipSuccess) e = hipStreamSynchronize(s);
             if (e != hipSuccess) rc = hip_fail(e, "gbp_count_kernel (level 2)");
         }
-        if (!rc) rc = gbp_alloc(R, (int64_t)hr[P], nul, &R.pbuf, &R.pout);
+        if (!rc) rc = gbp_alloc(R, (int64_t)hr[P], nul_out, &R.pbuf, &R.pout);
         if (!rc && g2.ntiles > 0) {
-            const hipError_t e = nul ? gbp_pass<0, true, true, true>(R, g2, out1, cnt, part, true, R.pout)
-                                     : gbp_pass<0, true, true>(R, g2, out1, cnt, part, true, R.pout);
+            const hipError_t e = nul_out ? gbp_pass<0, true, true, true>(R, g2, out1, cnt, part, true, R.pout)
+                                         : gbp_pass<0, true, true>(R, g2, out1, cnt, part, true, R.pout);
             if (e != hipSuccess) rc = hip_fail(e, "gbp_scatter_kernel (level 2)");
         }
         dev_free(cnt, s);
@@ -2643,6 +2702,8 @@ static hipError_t launch_partitioned(const GbRun& R) {
     q.row_begin = 0;
     q.n_full = 0;
     q.part_range = R.part_range;
+    // (compact regions: p's rtab / rcap / region_cnt and the overflow table
+    // from gb_alloc_table)
     q.part_rows = R.pout.rows;
     q.part_nulls = R.pout.nulls;
     q.part_blocks = R.part_blocks;
@@ -2677,10 +2738,27 @@ static hipError_t launch_partitioned(const GbRun& R) {
 static int gb_alloc_table(GbRun& R) {
     GbParams& p = R.pl.p;
     dev_free(R.gtab, R.s);
+    dev_free(R.rtab, R.s);
     R.gtab = nullptr;
+    R.rtab = nullptr;
+    p.rtab = nullptr;
+    p.rcap = 0;
+    p.region_cnt = nullptr;
     p.gbits = R.gbits;
-    p.gcap = int64_t(1) << R.gbits;
     p.rbits = R.rbits;
+    if (R.compact_now) {
+        // compact regions: the region table (2^(pbits + lbits) slots, written
+        // whole where read, never initialised) and a small hashed overflow
+        // table (plain probing) for the keys that find no LDS slot
+        p.rcap = int64_t(1) << (R.pbits + R.part_lbits);
+        int rc = dev_alloc((void**)&R.rtab, (size_t)p.rcap * p.nfields * 8, R.s);
+        if (rc) return rc;
+        p.rtab = R.rtab;
+        p.region_cnt = R.region_cnt;
+        p.gbits = std::max(16, R.pbits + 2);
+        p.rbits = 0;
+    }
+    p.gcap = int64_t(1) << p.gbits;
     const size_t wpf = (size_t)(p.gcap + 2);
     int rc = dev_alloc((void**)&R.gtab, wpf * p.nfields * 8, R.s);
     if (rc) return rc;
@@ -2790,6 +2868,11 @@ static int gb_main(GbRun& R, bool auto_refit, bool* refit, int32_t* hint) {
     int rc = PLGPU_OK;
     if (R.part && n > 0 && R.pbuf == nullptr) rc = gb_partition(R);
     for (R.attempts = 0; rc == PLGPU_OK; ++R.attempts) {
+        R.compact_now = R.compact_ok && R.part && n > 0 && pl.sum_only && pl.limbs == 2 && R.rbits > 0 &&
+                        R.part_blocks == 1 && R.wide == 0 && options().part_compact != 0;
+        if (R.compact_now && R.region_cnt == nullptr &&
+            (rc = dev_alloc((void**)&R.region_cnt, ((size_t)1 << R.pbits) * 4, R.s)))
+            break;
         if ((rc = gb_alloc_table(R))) break;
         PLGPU_HIP(hipMemcpyAsync(R.bottoms, R.hb, sizeof R.hb, hipMemcpyHostToDevice, R.s));
         for (int a = 0; a < kMaxAcc; ++a) p.bottom[a] = R.hb[a];
@@ -2828,7 +2911,12 @@ static int gb_main(GbRun& R, bool auto_refit, bool* refit, int32_t* hint) {
             break;
         }
         bool again = false;
-        if (R.st[ST_TABLE_FULL] > 0) {
+        if (R.st[ST_TABLE_FULL] > 0 && R.compact_now) {
+            // the compact run's overflow table filled: rerun on the probed
+            // regions of the whole table
+            R.compact_ok = false;
+            again = true;
+        } else if (R.st[ST_TABLE_FULL] > 0) {
             // (a full partition region: the rerun takes the plain hashed table)
             R.rbits = 0;
             R.gbits = std::max(R.gbits + 3, log2_ceil((int64_t)R.st[ST_NEWKEYS] * 4));
@@ -2868,6 +2956,8 @@ static int gb_main(GbRun& R, bool auto_refit, bool* refit, int32_t* hint) {
                 break;
             }
             R.wide |= wide;
+            // the wide pass finds each row's slot by probing: no compact regions
+            if (wide && R.compact_now) again = true;
             if (changed) {
                 if (auto_refit) {
                     for (int a = 0; a < kMaxAcc; ++a)
@@ -2977,8 +3067,27 @@ static int gb_finalize(GbRun& R, int32_t naggs, plgpu_column* out_key, plgpu_col
         }
         fp.vbytes = vbytes;
         const int fg = (int)std::min<int64_t>((p.gcap + 2 + 255) / 256, 256 * 16);
+        uint64_t* roff = nullptr;  // compact regions: scan of the region counts + scratch
+        const int nreg = R.compact_now ? 1 << R.pbits : 0;
+        if (nreg) {
+            const int64_t nb = std::max<int64_t>(1, (nreg + kScanChunk - 1) / kScanChunk);
+            rc = dev_alloc((void**)&roff, (size_t)(nreg + 1 + nb + 2) * 8, s);
+            if (!rc && scan_exclusive<uint32_t>(R.region_cnt, nreg, roff, roff + nreg + 1, s) != hipSuccess)
+                rc = fail(PLGPU_ERR_HIP, "region count scan");
+            if (rc) {
+                dev_free(roff, s);
+                dev_free(vbytes, s);
+                dev_free(first, s);
+                plgpu_column_release(out_key);
+                for (int i = 0; i < naggs; ++i) plgpu_column_release(&out_aggs[i]);
+                return rc;
+            }
+        }
         {
             KtScope kt("gb_finalize_kernel", s);
+            // compact regions: the regions first, then the overflow table
+            // (its groups and the two special ones) after them
+            if (nreg) gb_finalize_regions_kernel<<<nreg, 256, 0, s>>>(p, fp, roff, R.part_lbits);
             gb_finalize_kernel<<<fg, 256, 0, s>>>(p, fp);
             PackValid pv;
             std::memset(&pv, 0, sizeof pv);
@@ -2990,6 +3099,7 @@ static int gb_finalize(GbRun& R, int32_t naggs, plgpu_column* out_key, plgpu_col
                                                                                                        pv);
         }
         dev_free(vbytes, s);
+        dev_free(roff, s);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) rc = hip_fail(e, "gb_finalize_kernel");
         uint64_t produced = 0, var_out = 0;
@@ -3218,6 +3328,7 @@ static int gb_single_impl(const plgpu_column* key, const plgpu_column* cols, int
     GbRun R;
     int rc = gb_prepare(R, key, cols, ncols, program, n_instr, aggs, naggs, maintain_order != 0, false, stream,
                         deriv);
+    R.compact_ok = maintain_order == 0;  // the table is read only by gb_finalize below
     if (!rc) rc = gb_plan(R, nullptr);
     if (!rc) rc = gb_main(R, true, nullptr, nullptr);
     if (rc) return rc;

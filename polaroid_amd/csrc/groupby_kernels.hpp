@@ -184,6 +184,19 @@ struct GbParams {
     // ps_keys) instead of one byte load per lane
     int32_t vwords;
     KeyPack kp;             // fused key packing (kp.n > 0): the key is the packed tuple code
+    // compact regions (one workgroup per partition, the slim sum-only
+    // layout; null = off): the workgroup of partition q writes its LDS
+    // groups densely, in slot order, to slots [q lcap, q lcap +
+    // region_cnt[q]) of the region table rtab (field f of slot t at
+    // rtab[f * rcap + t], never initialised) and stores that count.  gtab
+    // is then a small hashed overflow table (rbits = 0, initialised): the
+    // rows of keys that found no LDS slot (a key's rows all miss, or none
+    // do: one workgroup sees every row of its partition) and the two
+    // special groups.  The finalize reads the regions' dense prefixes, then
+    // the overflow table.
+    uint32_t* region_cnt;
+    uint64_t* rtab;
+    int64_t rcap;
 };
 
 // ------------------------------------------------------ invariant checks
@@ -1215,7 +1228,7 @@ template <int NACC, int PRED, bool SUMONLY, int ROWS, int LIMBS = 3, bool RUNS =
 __global__ __launch_bounds__(PART && !RUNS ? kGbPartThreads : kGbThreads) void gb_fast_kernel(GbParams p,
                                                                                                DevProgram prog) {
     static_assert(!PACK || !PART, "PACK: the single-table kernel");
-    static_assert(!NULLS || (!RUNS && !DERIV && VAR == 0 && PACK == 0), "NULLS: plain inputs");
+    static_assert(!NULLS || (!RUNS && !DERIV && (VAR == 0 || VAR == 5) && PACK == 0), "NULLS: plain inputs");
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
     constexpr int NA = NACC > 0 ? NACC : 1;
     // VAR 1 (sum-only, NACC 3): the fused variance's three sums of one column
@@ -1722,6 +1735,73 @@ __global__ __launch_bounds__(PART && !RUNS ? kGbPartThreads : kGbThreads) void g
     }
     if (SLIM) {
         __syncthreads();
+        // LDS slot sl's state: plain stores into its own slot t, or added
+        // into a shared slot gs
+        // (tab, stride: the hashed table, or the compact region table)
+        auto store_slot = [&](int sl, uint64_t* tab, int64_t stride, int64_t t, uint64_t len) {
+            tab[(int64_t)p.f_len * stride + t] = len;
+#pragma unroll
+            for (int a = 0; a < NACC; ++a) {
+                const int f = p.acc[a].f_sum;
+                uint64_t w0, w1, w2;
+                limbs_to_192(0, (int64_t)*fld(sl, so_mid(a)), (int64_t)*fld(sl, so_top(a)), w0, w1, w2);
+                tab[(int64_t)f * stride + t] = w0;
+                tab[(int64_t)(f + 1) * stride + t] = w1;
+                tab[(int64_t)(f + 2) * stride + t] = w2;
+                tab[(int64_t)p.acc[a].f_flags * stride + t] = *fld(sl, so_flags(a));
+            }
+        };
+        auto add_slot = [&](int sl, int64_t gs, uint64_t len) {
+            atomicAdd((unsigned long long*)gfield(p, p.f_len, gs), (unsigned long long)len);
+#pragma unroll
+            for (int a = 0; a < NACC; ++a) {
+                const int f = p.acc[a].f_sum;
+                uint64_t w0, w1, w2;
+                limbs_to_192(0, (int64_t)*fld(sl, so_mid(a)), (int64_t)*fld(sl, so_top(a)), w0, w1, w2);
+                g_add192(gfield(p, f, gs), gfield(p, f + 1, gs), gfield(p, f + 2, gs), w0, w1, w2);
+                const uint64_t fl = *fld(sl, so_flags(a));
+                if (fl) atomicOr((unsigned long long*)gfield(p, p.acc[a].f_flags, gs), (unsigned long long)fl);
+            }
+        };
+        if (PART && p.region_cnt) {
+            // compact regions: the live slots ranked in slot order (wave
+            // ballots + the waves' counts), written densely from the
+            // region's first slot; the two special groups add into the
+            // table's shared special slots
+            // the waves' counts: 16 words after the slim table (launch_part_fast
+            // sizes the dynamic LDS with them; no static LDS, so the kernel's
+            // dynamic limit stays the full 160 KiB)
+            uint32_t* wcnt = (uint32_t*)&lds[(size_t)L * slim_words(NACC)];
+            const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+            const int64_t t0 = (int64_t)(blockIdx.x / p.part_blocks) << p.lbits;
+            uint32_t run = 0;
+            for (int s0 = 0; s0 < L; s0 += blockDim.x) {
+                const int sl = s0 + threadIdx.x;
+                const uint64_t len = sl < L ? *fld(sl, 1) : 0ull;
+                const bool live = len != 0 && sl < p.lcap;
+                const uint64_t bl = __ballot(live);
+                if (lane == 0) wcnt[wid] = (uint32_t)__popcll(bl);
+                __syncthreads();
+                uint32_t before = 0, tot = 0;
+                for (int w = 0; w < nw; ++w) {
+                    before += w < wid ? wcnt[w] : 0u;
+                    tot += wcnt[w];
+                }
+                __syncthreads();
+                if (live) {
+                    const uint32_t idx = run + before + (uint32_t)__popcll(bl & ((1ull << lane) - 1ull));
+                    ++d.newkeys;
+                    p.rtab[t0 + idx] = lds[sl];
+                    store_slot(sl, p.rtab, p.rcap, t0 + idx, len);
+                } else if (len != 0) {
+                    d.special |= sl == p.lcap ? 1u : 2u;
+                    add_slot(sl, sl == p.lcap ? p.gcap : p.gcap + 1, len);
+                }
+                run += tot;
+            }
+            if (threadIdx.x == 0) p.region_cnt[blockIdx.x / p.part_blocks] = run;
+            flush_and_report<false>(p, lds, L, d);
+        } else {
         for (int sl = threadIdx.x; sl < L; sl += blockDim.x) {
             const uint64_t len = *fld(sl, 1);
             if (len == 0) continue;
@@ -1737,17 +1817,7 @@ __global__ __launch_bounds__(PART && !RUNS ? kGbPartThreads : kGbThreads) void g
                 if (t >= 0) {
                     // the partition's own region slot: plain stores
                     ++d.newkeys;
-                    *gfield(p, p.f_len, t) = len;
-#pragma unroll
-                    for (int a = 0; a < NACC; ++a) {
-                        const int f = p.acc[a].f_sum;
-                        uint64_t w0, w1, w2;
-                        limbs_to_192(0, (int64_t)*fld(sl, so_mid(a)), (int64_t)*fld(sl, so_top(a)), w0, w1, w2);
-                        *gfield(p, f, t) = w0;
-                        *gfield(p, f + 1, t) = w1;
-                        *gfield(p, f + 2, t) = w2;
-                        *gfield(p, p.acc[a].f_flags, t) = *fld(sl, so_flags(a));
-                    }
+                    store_slot(sl, p.gtab, p.gcap + 2, t, len);
                     continue;
                 }
                 bool ins = false;
@@ -1758,18 +1828,10 @@ __global__ __launch_bounds__(PART && !RUNS ? kGbPartThreads : kGbThreads) void g
                     continue;
                 }
             }
-            atomicAdd((unsigned long long*)gfield(p, p.f_len, gs), (unsigned long long)len);
-#pragma unroll
-            for (int a = 0; a < NACC; ++a) {
-                const int f = p.acc[a].f_sum;
-                uint64_t w0, w1, w2;
-                limbs_to_192(0, (int64_t)*fld(sl, so_mid(a)), (int64_t)*fld(sl, so_top(a)), w0, w1, w2);
-                g_add192(gfield(p, f, gs), gfield(p, f + 1, gs), gfield(p, f + 2, gs), w0, w1, w2);
-                const uint64_t fl = *fld(sl, so_flags(a));
-                if (fl) atomicOr((unsigned long long*)gfield(p, p.acc[a].f_flags, gs), (unsigned long long)fl);
-            }
+            add_slot(sl, gs, len);
         }
         flush_and_report<false>(p, lds, L, d);
+        }
     } else {
         grun_flush();
         flush_and_report<true>(p, lds, L, d);
@@ -1898,21 +1960,6 @@ hipError_t launch_fast_rows(const Plan& pl, const DevProgram& dp, hipStream_t s)
     return hipGetLastError();
 }
 
-// Nullable key / aggregated / predicate columns (gb_plan sends plain inputs
-// here: no derived operands, no packed key, no register runs): the sum-only
-// 2-limb layout, or the general one (3-limb sums, counts, min / max, first /
-// last rows).
-template <int NACC>
-hipError_t launch_fast_nulls(const Plan& pl, const DevProgram& dp, int pred, hipStream_t s) {
-    if constexpr (NACC > 0) {
-        if (pl.sum_only && pl.limbs == 2)
-            return pred == 0 ? launch_fast_rows<NACC, 0, true, 2, false, false, 0, 0, 2, true>(pl, dp, s)
-                             : launch_fast_rows<NACC, 1, true, 2, false, false, 0, 0, 2, true>(pl, dp, s);
-    }
-    return pred == 0 ? launch_fast_rows<NACC, 0, false, 3, false, false, 0, 0, 2, true>(pl, dp, s)
-                     : launch_fast_rows<NACC, 1, false, 3, false, false, 0, 0, 2, true>(pl, dp, s);
-}
-
 // x >= 0 (or NaN) on every row the fused predicate keeps: a float compare
 // on acc `a`'s own column that accepts no value below c (x > c, x >= c,
 // x == c) with c >= 0 (NaN compares greatest and fails the limb window
@@ -1929,6 +1976,25 @@ inline bool var_x_nonneg(const Plan& pl, const DevProgram& dp, int a = 0) {
     double c;
     std::memcpy(&c, &dp.simple_imm, 8);
     return c >= 0.0;
+}
+
+// Nullable key / aggregated / predicate columns (gb_plan sends plain inputs
+// here: no derived operands, no packed key, no register runs): the sum-only
+// 2-limb layout, or the general one (3-limb sums, counts, min / max, first /
+// last rows).
+template <int NACC>
+hipError_t launch_fast_nulls(const Plan& pl, const DevProgram& dp, int pred, hipStream_t s) {
+    if constexpr (NACC > 0) {
+        // VAR 5 (sum_pos): a null value of the predicate's column drops its
+        // row, so the selected values of the last acc are still >= 0
+        if (pl.sum_only && pl.limbs == 2 && pred == 1 && options().sum_pos && var_x_nonneg(pl, dp, NACC - 1))
+            return launch_fast_rows<NACC, 1, true, 2, false, false, 5, 0, 2, true>(pl, dp, s);
+        if (pl.sum_only && pl.limbs == 2)
+            return pred == 0 ? launch_fast_rows<NACC, 0, true, 2, false, false, 0, 0, 2, true>(pl, dp, s)
+                             : launch_fast_rows<NACC, 1, true, 2, false, false, 0, 0, 2, true>(pl, dp, s);
+    }
+    return pred == 0 ? launch_fast_rows<NACC, 0, false, 3, false, false, 0, 0, 2, true>(pl, dp, s)
+                     : launch_fast_rows<NACC, 1, false, 3, false, false, 0, 0, 2, true>(pl, dp, s);
 }
 
 template <int NACC, int PRED, bool SUMONLY, bool DERIV, int PACK = 0>
@@ -2020,7 +2086,8 @@ hipError_t launch_part_fast(const Plan& pp, int grid, hipStream_t s) {
         (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_set = true;
     }
-    const size_t lds = (size_t)(LIMBS == 2 ? slim_words(NACC) : pp.p.nfields) * (pp.p.lcap + 2) * 8;
+    // (+ 64 B: compact regions' wave counts after the slim table)
+    const size_t lds = (size_t)(LIMBS == 2 ? slim_words(NACC) : pp.p.nfields) * (pp.p.lcap + 2) * 8 + 64;
     DevProgram none;
     std::memset(&none, 0, sizeof none);
     // 1024 threads where each workgroup has many rows to share its table's

@@ -54,12 +54,14 @@ struct Options {
     int part_levels = -1; // partitioned path: 1 / 2 scatter passes (-1: by the partition bits)
     int part_direct = 1;  // partitioned path: one-workgroup partitions flush into their own table region
     int part_lds_kb = 0;  // partitioned path: LDS table budget per workgroup (0: 160 KiB)
+    int part_compact = 1; // partitioned path, slim sum-only layout: compact regions + region finalize (A/B)
     int rl_stream = 0;    // rolling windows <= 64, null-free: resident streaming waves (0: one block per wave; A/B)
     int rl_grid = 0;      // rolling stream kernel: workgroups per CU (0: 4)
     int filt_pipe = 1;    // filter scatter: next column's loads before this column's stores (A/B)
     int part_threads = 0; // partitioned aggregation: threads per workgroup (0: 1024; A/B)
     int rl_div = 1;       // rolling mean of full windows by one correction step instead of a division (A/B)
     int rl_full = 1;      // rolling sum / mean: interior int64-form waves by the specialised scan (A/B)
+    int rl_var128 = 1;    // rolling var / std, interior waves: 128-bit modular numerators where they fit (A/B)
     int filt_fused = 0;   // filter: the one-pass look-back kernel where it applies (A/B; measured slower)
     int var_pos = 1;      // fused variance: x's limbs unsigned when the predicate keeps x >= 0 (A/B)
     int sum_pos = 1;      // fused 4-sum kernel: the predicate column's limbs unsigned when it keeps x >= 0 (A/B)

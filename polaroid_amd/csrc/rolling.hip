@@ -50,6 +50,7 @@ struct RlParams {
     int32_t ddof;
     int32_t var_f32;      // std of a Float32 column: sqrt of the variance rounded to f32
     int32_t fast_div;     // option rl_div: full windows' means by rw_div
+    int32_t var128;       // option rl_var128: rw_var_scan_full's numerators modulo 2^128 where they fit
     int32_t full;         // option rl_full: interior int64-form waves by rw_scan_full
     double rw;            // RN(1 / w)
     double wd;            // w as an f64
@@ -929,7 +930,24 @@ __device__ __forceinline__ void rw_var_scan(const RlParams& p, const uint64_t (&
 // only by the wave's first output; chunk 3 overwrites it afterwards).  The
 // two quotients num / w / (w - ddof) take the one-correction form when the
 // wave's exponents keep them normal (DIV1, rw_block).
-template <bool DIV1>
+// A nonnegative 128-bit integer (nh:nl) * 2^e as f64, rounded once (no
+// subnormal results), without branches: the leading word and the bits
+// below it as one sticky bit, then the one u64 -> f64 rounding.
+__device__ __forceinline__ double u128_to_double(uint64_t nl, uint64_t nh, int e) {
+    const bool hi = nh != 0;
+    const uint64_t w = hi ? nh : nl;
+    const int lz = __clzll(w | 1ull) - (w == 0 ? 1 : 0);  // (w == 0: nl == nh == 0, result 0)
+    const uint64_t below = hi ? nl : 0ull;
+    uint64_t top = lz ? (w << lz) | (below >> (64 - lz)) : w;
+    const uint64_t rest = lz ? below << lz : below;
+    top |= rest != 0 ? 1ull : 0ull;
+    return __builtin_ldexp((double)top, (hi ? 128 : 64) - 64 - lz + e);
+}
+
+// N128: the wave's numerators are below 2^128 (rw_block: 2 (54 + span) +
+// 2 lw <= 129, so w S2 - S1^2 = sum over pairs (t_i - t_j)^2 < 2^128), so
+// w S2 and S1^2 are formed modulo 2^128 and their difference is exact.
+template <bool DIV1, bool N128>
 __device__ __forceinline__ void rw_var_scan_full(const RlParams& p, const uint64_t (&x)[kRwChunks + 1],
                                                  int64_t o_first, int64_t o_end, int64_t s_first, int tmin,
                                                  uint64_t* ring) {
@@ -977,19 +995,28 @@ __device__ __forceinline__ void rw_var_scan_full(const RlParams& p, const uint64
         uint64_t s2l = ring[kRwRing + ie], s2h = ring[2 * kRwRing + ie];
         add128(s2l, s2h, ~ring[kRwRing + is], ~ring[2 * kRwRing + is]);
         add128(s2l, s2h, 1, 0);
-        // num = w * S2 - S1^2, exact in 192 bits
-        const unsigned __int128 lo = (unsigned __int128)s2l * cw;
-        const unsigned __int128 hi = (unsigned __int128)s2h * cw + (uint64_t)(lo >> 64);
-        uint64_t w0 = (uint64_t)lo, w1 = (uint64_t)hi, w2 = (uint64_t)(hi >> 64);
+        double nr;
         const uint64_t a1 = (uint64_t)(S1 < 0 ? -S1 : S1);
         const unsigned __int128 q2 = (unsigned __int128)a1 * a1;
-        const uint64_t q0 = (uint64_t)q2, q1 = (uint64_t)(q2 >> 64);
-        const uint64_t b0 = w0 < q0 ? 1ull : 0ull;
-        w0 -= q0;
-        const unsigned __int128 d1 = (unsigned __int128)w1 - q1 - b0;
-        w1 = (uint64_t)d1;
-        w2 -= (uint64_t)(d1 >> 64) ? 1ull : 0ull;
-        const double nr = (int64_t)w2 < 0 ? 0.0 : u192_to_double(w0, w1, w2, 2 * bottom);
+        if (N128) {
+            // num = w * S2 - S1^2 modulo 2^128 (exact: it is below 2^128)
+            const unsigned __int128 lo = (unsigned __int128)s2l * cw;
+            const unsigned __int128 num = (((unsigned __int128)(s2h * cw + (uint64_t)(lo >> 64))) << 64 |
+                                           (uint64_t)lo) - q2;
+            nr = u128_to_double((uint64_t)num, (uint64_t)(num >> 64), 2 * bottom);
+        } else {
+            // num = w * S2 - S1^2, exact in 192 bits
+            const unsigned __int128 lo = (unsigned __int128)s2l * cw;
+            const unsigned __int128 hi = (unsigned __int128)s2h * cw + (uint64_t)(lo >> 64);
+            uint64_t w0 = (uint64_t)lo, w1 = (uint64_t)hi, w2 = (uint64_t)(hi >> 64);
+            const uint64_t q0 = (uint64_t)q2, q1 = (uint64_t)(q2 >> 64);
+            const uint64_t b0 = w0 < q0 ? 1ull : 0ull;
+            w0 -= q0;
+            const unsigned __int128 d1 = (unsigned __int128)w1 - q1 - b0;
+            w1 = (uint64_t)d1;
+            w2 -= (uint64_t)(d1 >> 64) ? 1ull : 0ull;
+            nr = (int64_t)w2 < 0 ? 0.0 : u192_to_double(w0, w1, w2, 2 * bottom);
+        }
         double v;
         if (DIV1) {
             const double a0 = nr * y;
@@ -1087,10 +1114,11 @@ __device__ __forceinline__ void rw_block(const RlParams& p, uint64_t (&x)[kRwChu
             // nonzero numerators lie in [2^(2 bottom), 2^(2 (tmax - 1022) + 2 lw)):
             // both quotients inside rw_div's exponent range
             const int b2 = 2 * (tmin - 1075), top = 2 * (tmax - 1022) + 2 * lw;
-            if (p.fast_div && b2 - 2 * lw >= -900 && top <= 990)
-                rw_var_scan_full<true>(p, x, o_first, o_end, s_first, tmin, rlo);
-            else
-                rw_var_scan_full<false>(p, x, o_first, o_end, s_first, tmin, rlo);
+            const bool div1 = p.fast_div && b2 - 2 * lw >= -900 && top <= 990;
+            const bool n128 = p.var128 && 2 * (54 + span) + 2 * lw <= 129;
+            if (div1 && n128) rw_var_scan_full<true, true>(p, x, o_first, o_end, s_first, tmin, rlo);
+            else if (div1) rw_var_scan_full<true, false>(p, x, o_first, o_end, s_first, tmin, rlo);
+            else rw_var_scan_full<false, false>(p, x, o_first, o_end, s_first, tmin, rlo);
             return;
         }
         if (counts) rw_var_scan<true>(p, x, vm, o_first, o_end, s_first, tmin, rlo, rhi, rv2, rcn);
@@ -1506,6 +1534,7 @@ PLGPU_API int plgpu_rolling(const plgpu_column* values, int32_t kind, int64_t wi
     p.mean = kind == PLGPU_ROLLING_MEAN;
     p.rw = 1.0 / (double)std::max<int64_t>(window_size, 1);
     p.fast_div = options().rl_div;
+    p.var128 = options().rl_var128;
     p.full = options().rl_full;
     p.wd = (double)window_size;
     p.wd2 = (double)std::max<int64_t>(window_size - ddof, 1);

@@ -61,6 +61,8 @@ const OptField kOptFields[] = {
     {"part_bits", "PLGPU_PART_BITS", &Options::part_bits},
     {"part_levels", "PLGPU_PART_LEVELS", &Options::part_levels},
     {"part_direct", "PLGPU_PART_DIRECT", &Options::part_direct},
+    {"part_compact", "PLGPU_PART_COMPACT", &Options::part_compact},
+    {"rl_var128", "PLGPU_RL_VAR128", &Options::rl_var128},
     {"part_lds_kb", "PLGPU_PART_LDS_KB", &Options::part_lds_kb},
     {"rl_stream", "PLGPU_RL_STREAM", &Options::rl_stream},
     {"rl_grid", "PLGPU_RL_GRID", &Options::rl_grid},

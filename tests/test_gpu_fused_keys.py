@@ -289,7 +289,7 @@ _NONNEG_PREDS = {  # name -> (expr, the oracle's program over column 0 = close)
 
 
 @pytest.mark.parametrize("pname", list(_NONNEG_PREDS))
-@pytest.mark.parametrize("keys", ["int64", "sym_day", "runs"])
+@pytest.mark.parametrize("keys", ["int64", "sym_day", "runs", "int64_nulls"])
 @pytest.mark.parametrize("order", ["close_last", "close_first"])
 def test_nonneg_predicate_column_sum(gpu, plgpu_option, pname, keys, order):
     """Four sums whose last column is the fused predicate's and keeps no
@@ -299,7 +299,9 @@ def test_nonneg_predicate_column_sum(gpu, plgpu_option, pname, keys, order):
     oracle (or_group_by_agg, SUM_EXACT) with the option on and off, on data
     with negatives, zeros, -0.0, NaN, +inf and exact hits of the literal;
     keys: an Int64 key, (Int64, Int32) packed in the kernel, and a sorted
-    key (the RUNS layout).  close_first puts the predicate's column in the
+    key (the RUNS layout), and an Int64 key over value columns with ~2 %
+    nulls (the NULLS variant; a null close drops its row, so VAR 5 still
+    holds).  close_first puts the predicate's column in the
     first acc: var_x_nonneg's pred_acc is then 0 and the signed kernel runs
     (gtneg: a negative literal, never the unsigned variant)."""
     rng = np.random.default_rng(len(pname) + len(keys) + len(order))
@@ -317,12 +319,13 @@ def test_nonneg_predicate_column_sum(gpu, plgpu_option, pname, keys, order):
     x[rng.integers(0, n, 3)] = np.nan
     x[rng.integers(0, n, 2)] = np.inf
     x[rng.integers(0, n, 2)] = -np.inf
+    valid = {c: (rng.random(n) > 0.02 if keys == "int64_nulls" else None) for c in names}
     df = pl.DataFrame({"sym": pl.Series.from_numpy("sym", sym), "day": pl.Series.from_numpy("day", day),
-                       **{c: pl.Series.from_numpy(c, v) for c, v in cols.items()}})
+                       **{c: pl.Series.from_numpy(c, v, valid[c]) for c, v in cols.items()}})
     mk, prog = _NONNEG_PREDS[pname]
     by = ["sym", "day"] if keys == "sym_day" else ["sym"]
     hk = [(sym, None)] + ([(day, None)] if keys == "sym_day" else [])
-    hc = [O.HostCol(cols[c]) for c in ["close"] + [c for c in names if c != "close"]]
+    hc = [O.HostCol(cols[c], valid[c]) for c in ["close"] + [c for c in names if c != "close"]]
     oidx = {c: i for i, c in enumerate(["close"] + [c for c in names if c != "close"])}
     okeys, oouts = O.group_by_agg_multi(hk, hc, prog, [("sum", oidx[c]) for c in names], n)
     want = {tuple(int(k[0][i]) for k in okeys): [o[0][i] for o in oouts] for i in range(len(okeys[0][0]))}
@@ -331,6 +334,8 @@ def test_nonneg_predicate_column_sum(gpu, plgpu_option, pname, keys, order):
         info = {}
         out = df.lazy().filter(mk()).group_by(*by).agg(*[pl.col(c).sum() for c in names]).collect(info=info)
         assert out.height == len(want), (pname, on)
+        if keys != "sym_day":  # (8,001 (sym, day) groups over 4e5 rows: the plan's choice)
+            assert info["path"] == 2, info
         kc = [out[k].to_numpy() for k in by]
         vc = [out[c].to_numpy() for c in names]
         for i in range(out.height):

@@ -175,3 +175,76 @@ def test_partitioned_program_predicate_and_narrow_columns(gpu, levels, plgpu_opt
         assert out["k"].dtype == pl.Int32
         okeys, okvalid, oouts = exp
         _compare(out, (okeys.astype(np.int64), okvalid, oouts), aggs, maintain)
+
+
+@pytest.mark.parametrize("compact", [1, 0])
+@pytest.mark.parametrize("nullable", [False, True])
+def test_compact_regions(gpu, compact, nullable, plgpu_option):
+    """Compact regions (option part_compact): each partition's workgroup
+    writes its groups densely from its region's first slot and the finalize
+    reads only those prefixes plus the two special groups (the null key and
+    the key equal to the table's empty marker, Int64 extremes here).  Bitwise
+    equal to the oracle with the option on and off, with NaN / inf values,
+    null keys and null values (the NULLS partition kernel)."""
+    rng = np.random.default_rng(31 + compact + 2 * nullable)
+    n = 2_000_003
+    key = rng.integers(0, 400_000, n).astype(np.int64) * 104_729 + 11
+    key[rng.random(n) < 0.001] = I64_MIN
+    key[rng.random(n) < 0.001] = I64_MAX
+    cols = _ohlc(rng, n)
+    cols["close"][rng.random(n) < 0.0005] = np.nan
+    cols["open"][rng.random(n) < 0.0005] = np.inf
+    kvalid = (rng.random(n) > 0.01) if nullable else None
+    vvalid = {c: ((rng.random(n) > 0.02) if nullable and c != "close" else None) for c in cols}
+    aggs = [("sum", "open"), ("sum", "high"), ("sum", "low"), ("sum", "close")]
+    plgpu_option("part_compact", compact)
+    plgpu_option("gb_path", 3)
+    data = {"k": pl.Series.from_numpy("k", key, kvalid)}
+    for c, v in cols.items():
+        data[c] = pl.Series.from_numpy(c, v, vvalid[c])
+    info = {}
+    out = pl.DataFrame(data).lazy().filter(pl.col("close") > 100.0).group_by("k").agg(
+        *[pl.col(c).sum().alias(f"sum_{c}") for _, c in aggs]).collect(info=info)
+    assert info["path"] == 3, info
+    names = [c for _, c in aggs]
+    hc = [O.HostCol(cols[c], vvalid[c]) for c in names]
+    okeys, okvalid, oouts = O.group_by_agg(O.HostCol(key, kvalid), hc, _gt_prog(names.index("close"), 100.0),
+                                           [(kind, names.index(c)) for kind, c in aggs], n, O.SUM_EXACT)
+    gk, gkv = out["k"].to_numpy().astype(np.int64), out["k"].validity_numpy()
+    assert gk.shape[0] == okeys.shape[0]
+    assert gkv.sum() == okvalid.sum() and (~gkv).sum() == (~okvalid).sum() <= 1
+    tg = [("n", 0) if not v else ("k", int(k_)) for k_, v in zip(gk, gkv)]
+    to = [("n", 0) if not v else ("k", int(k_)) for k_, v in zip(okeys, okvalid)]
+    pos = {t: i for i, t in enumerate(to)}
+    oo = np.array([pos[t] for t in tg], dtype=np.int64)
+    for (kind, c), (ov, ovalid) in zip(aggs, oouts):
+        s = out[f"{kind}_{c}"]
+        assert np.array_equal(s.validity_numpy(), ovalid[oo]), c
+        assert np.array_equal(_bits(s.to_numpy()), _bits(ov[oo])), c
+
+
+def test_compact_regions_rerun_on_stale_plan(gpu):
+    """A plan whose group estimate is stale (the cached statistics of columns
+    rewritten in place, six times the groups) sizes partitions too small:
+    rows miss their partition's LDS table, the compact run is redone on the
+    probed regions, and the result stays exact."""
+    import torch
+
+    n = 3_000_001
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5)
+    k = torch.randint(0, 200_000, (n,), device="cuda", generator=g, dtype=torch.int64)
+    x = torch.rand(n, device="cuda", generator=g, dtype=torch.float64) * 100.0
+    df = pl.DataFrame([pl.Series.from_torch("k", k), pl.Series.from_torch("x", x)])
+    q = df.lazy().group_by("k").agg(pl.col("x").sum().alias("s"))
+    info = {}
+    q.collect(info=info)
+    k.copy_(torch.randint(0, 1_200_000, (n,), device="cuda", generator=g, dtype=torch.int64))
+    torch.cuda.synchronize()
+    info = {}
+    out = q.collect(info=info)
+    kh, xh = k.cpu().numpy(), x.cpu().numpy()
+    okeys, _, oouts = O.group_by_agg(O.HostCol(kh, None), [O.HostCol(xh, None)], None, [("sum", 0)], n, O.SUM_EXACT)
+    go, oo = np.argsort(out["k"].to_numpy()), np.argsort(okeys)
+    assert np.array_equal(out["k"].to_numpy()[go], okeys[oo])
+    assert np.array_equal(_bits(out["s"].to_numpy()[go]), _bits(oouts[0][0][oo]))

@@ -473,3 +473,24 @@ def test_rolling_var_ddof_range(gpu):
         with pytest.raises(pl.InvalidOperationError):
             pl.DataFrame({"a": [1.0, 2.0]}).select(pl.col("a").rolling_std(2, ddof=ddof))
     assert s.rolling_var(2, ddof=255).to_list() == [None, None, None, None]
+
+
+@pytest.mark.parametrize("var128", [1, 0])
+@pytest.mark.parametrize("span", [0, 1, 3, 4, 6])
+def test_rolling_var_numerator_modulo_2_128(gpu, plgpu_option, var128, span):
+    """rw_var_scan_full forms w S2 - S1^2 modulo 2^128 (option rl_var128)
+    when the wave's exponent span bounds it below 2^128 (2 (54 + span) +
+    2 lw <= 129; w = 64 allows span <= 3, w = 20 span <= 4, w = 2 span <=
+    8), else in 192 bits.  Mixed signs with alternating extremes put the
+    numerators at their largest; spans on both sides of each window's limit.
+    Bit-exact against the oracle's exact variance with the option on and off."""
+    plgpu_option("rl_var128", var128)
+    rng = np.random.default_rng(span * 3 + var128)
+    n = 4096 * 2 + 555
+    mag = np.ldexp(rng.uniform(1.0, 2.0, n), rng.integers(0, span + 1, n))
+    v = np.where(rng.random(n) < 0.5, -mag, mag)
+    v[::2] = np.ldexp(1.999999, span)  # alternating near-extremes
+    v[1::4] = -np.ldexp(1.999999, span)
+    for w in (2, 20, 64):
+        for ddof in (0, 1):
+            _var_check(v, None, w, w, False, ddof, std=(ddof == 1))
