@@ -411,6 +411,7 @@ def many_groups_leg(torch, pl, cols: dict, steps: int, warmup: int, groups_list,
         r = {"groups": int(info.get("out_groups", 0)), "ms_per_step": round(ms, 3), "Mrows_s": round(n / ms / 1e3, 1),
              "path": info.get("path"), "partition_bits": int(info.get("part_layout", 0)) & 0xFF,
              "scatter_passes": levels, "rows_selected": sel,
+             "lds_miss_rows": int(info.get("global_path_rows", 0)), "reruns": int(info.get("reruns", 0)),
              "step_frac_read_once": round(40 * n / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
         if info.get("path") == 3:
             r["count"] = _leg_roofline(kernels, "gbp_count_kernel", n * 16 + (sel * 8 if levels == 2 else 0),

@@ -1563,7 +1563,7 @@ static void size_tables(Plan* pl, uint64_t distinct, uint64_t sampled, int* gbit
     const int nf = p.nfields;
     // Max LDS slots at one workgroup per CU (160 KiB), power of two.
     int lmax_bits = 12;
-    while (lmax_bits > 6 && (size_t)nf * ((1u << lmax_bits) + 2) * 8 > 160 * 1024) --lmax_bits;
+    while (lmax_bits > 6 && (size_t)nf * ((1u << lmax_bits) + 2) * 8 + kWgScratch > 160 * 1024) --lmax_bits;
     const bool saturated = distinct >= (uint64_t)kPlanSetSlots / 2;
     int want_bits = log2_ceil(std::max<int64_t>(64, (int64_t)distinct * 2));
     pl->use_lds = !saturated && want_bits <= lmax_bits;
@@ -2241,7 +2241,7 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
         // the largest table one workgroup per CU holds; keys beyond it take
         // the global table
         int lb = 12;
-        while (lb > 6 && (size_t)p.nfields * ((1u << lb) + 2) * 8 > 160 * 1024) --lb;
+        while (lb > 6 && (size_t)p.nfields * ((1u << lb) + 2) * 8 + kWgScratch > 160 * 1024) --lb;
         pl.use_lds = true;
         p.lbits = lb;
         p.lcap = 1 << lb;
@@ -2260,7 +2260,7 @@ static int gb_plan(GbRun& R, const int32_t* fixed) {
         if (!pl.use_lds && clustered && gpath < 0) {
             const int lb = log2_ceil(std::max<int64_t>(64, 2 * (int64_t)local));
             const size_t bytes = (size_t)p.nfields * ((1u << lb) + 2) * 8;
-            if (bytes <= (size_t)160 * 1024) {
+            if (bytes + kWgScratch <= (size_t)160 * 1024) {
                 pl.local = pl.use_lds = true;
                 p.lbits = lb;
                 p.lcap = 1 << lb;

@@ -197,6 +197,8 @@ struct GbParams {
     uint32_t* region_cnt;
     uint64_t* rtab;
     int64_t rcap;
+    int32_t wave_report;    // option wave_report: per-wave status atomics (A/B of report_wg)
+    int32_t _pad3;
 };
 
 // ------------------------------------------------------ invariant checks
@@ -762,6 +764,55 @@ __device__ __forceinline__ void flush_and_report(const GbParams& p, uint64_t* ld
         if (nk) atomicAdd((unsigned long long*)&p.status[ST_NEWKEYS], (unsigned long long)nk);
         if (special) atomicOr((unsigned long long*)&p.status[ST_SPECIAL], (unsigned long long)special);
         if (fx) atomicOr((unsigned long long*)&p.status[ST_FXFLAGS], (unsigned long long)fx);
+    }
+}
+
+// The end of a fused launch whose dynamic LDS has kWgScratch bytes after
+// its table (`sc`): the diagnostics summed per wave, then per workgroup
+// through `sc`, and published with one atomic per status word and
+// workgroup.  Same-address atomics serialise (about 11 ns each on one
+// status word, measured on the finalize's counter), so per-wave publication
+// costs ~0.7 ms at the headline's 32,768 waves and most of the many-groups
+// aggregation at 2^15 workgroups of 8 waves.
+constexpr int kWgScratch = 256;  // 16 waves x 4 words
+__device__ __forceinline__ void report_wg(const GbParams& p, const ThreadDiag& d, uint32_t* sc) {
+    uint64_t nsel = d.nsel, nglob = d.nglobal, nk = d.newkeys;
+    uint32_t special = d.special, fx = d.fxbits;
+    const bool kbad = __any(d.kbad != 0);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        nsel += __shfl_xor(nsel, off, 64);
+        nglob += __shfl_xor(nglob, off, 64);
+        nk += __shfl_xor(nk, off, 64);
+        special |= __shfl_xor(special, off, 64);
+        fx |= __shfl_xor(fx, off, 64);
+    }
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    __syncthreads();  // (the scratch's earlier use is over)
+    if (lane == 0) {
+        // a workgroup's rows stay below kMaxRowsPerWg: 32-bit counts
+        sc[4 * wid] = (uint32_t)nsel;
+        sc[4 * wid + 1] = (uint32_t)nglob;
+        sc[4 * wid + 2] = (uint32_t)nk;
+        sc[4 * wid + 3] = special | (fx << 2) | (kbad ? 0x80000000u : 0u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t a = 0, b = 0, c = 0;
+        uint32_t o = 0;
+        for (int w = 0; w < nw; ++w) {
+            a += sc[4 * w];
+            b += sc[4 * w + 1];
+            c += sc[4 * w + 2];
+            o |= sc[4 * w + 3];
+        }
+        if (o >> 31) atomicOr((unsigned long long*)&p.status[ST_KPACK], 1ull);
+        if (a) atomicAdd((unsigned long long*)&p.status[ST_SELECTED], (unsigned long long)a);
+        if (b) atomicAdd((unsigned long long*)&p.status[ST_GLOBAL_ROWS], (unsigned long long)b);
+        if (c) atomicAdd((unsigned long long*)&p.status[ST_NEWKEYS], (unsigned long long)c);
+        if (o & 3u) atomicOr((unsigned long long*)&p.status[ST_SPECIAL], (unsigned long long)(o & 3u));
+        if ((o >> 2) & 0xFFFu)
+            atomicOr((unsigned long long*)&p.status[ST_FXFLAGS], (unsigned long long)((o >> 2) & 0xFFFu));
     }
 }
 
@@ -1735,6 +1786,10 @@ __global__ __launch_bounds__(PART && !RUNS ? kGbPartThreads : kGbThreads) void g
     }
     if (SLIM) {
         __syncthreads();
+        // kWgScratch bytes after the slim table (every slim launch sizes the
+        // dynamic LDS with them; no static LDS, so the kernel's dynamic limit
+        // stays the full 160 KiB)
+        uint32_t* wsc = (uint32_t*)&lds[(size_t)L * slim_words(NACC)];
         // LDS slot sl's state: plain stores into its own slot t, or added
         // into a shared slot gs
         // (tab, stride: the hashed table, or the compact region table)
@@ -1768,10 +1823,7 @@ __global__ __launch_bounds__(PART && !RUNS ? kGbPartThreads : kGbThreads) void g
             // ballots + the waves' counts), written densely from the
             // region's first slot; the two special groups add into the
             // table's shared special slots
-            // the waves' counts: 16 words after the slim table (launch_part_fast
-            // sizes the dynamic LDS with them; no static LDS, so the kernel's
-            // dynamic limit stays the full 160 KiB)
-            uint32_t* wcnt = (uint32_t*)&lds[(size_t)L * slim_words(NACC)];
+            uint32_t* wcnt = wsc;  // the waves' counts
             const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
             const int64_t t0 = (int64_t)(blockIdx.x / p.part_blocks) << p.lbits;
             uint32_t run = 0;
@@ -1800,7 +1852,8 @@ __global__ __launch_bounds__(PART && !RUNS ? kGbPartThreads : kGbThreads) void g
                 run += tot;
             }
             if (threadIdx.x == 0) p.region_cnt[blockIdx.x / p.part_blocks] = run;
-            flush_and_report<false>(p, lds, L, d);
+            if (p.wave_report) flush_and_report<false>(p, lds, L, d);
+            else report_wg(p, d, wsc);
         } else {
         for (int sl = threadIdx.x; sl < L; sl += blockDim.x) {
             const uint64_t len = *fld(sl, 1);
@@ -1830,7 +1883,8 @@ __global__ __launch_bounds__(PART && !RUNS ? kGbPartThreads : kGbThreads) void g
             }
             add_slot(sl, gs, len);
         }
-        flush_and_report<false>(p, lds, L, d);
+        if (p.wave_report) flush_and_report<false>(p, lds, L, d);
+            else report_wg(p, d, wsc);
         }
     } else {
         grun_flush();
@@ -1923,9 +1977,11 @@ hipError_t launch_fast_rows(const Plan& pl, const DevProgram& dp, hipStream_t s)
         (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_set = true;
     }
-    const size_t lds = (SUMONLY && LIMBS == 2) ? (size_t)slim_words(NACC) * (pl.p.lcap + 2) * 8 : pl.lds_bytes;
+    const size_t lds =
+        (SUMONLY && LIMBS == 2) ? (size_t)slim_words(NACC) * (pl.p.lcap + 2) * 8 + kWgScratch : pl.lds_bytes;
     GbParams q = pl.p;
     q.tiles_per_wg = 0;
+    q.wave_report = options().wave_report;
     if (VAR == 2 || VAR == 3) pair_normalize(q, VAR - 2, PRED == 1);
     // the plan's n_full is a multiple of the 2-row tile; a wider tile takes
     // its own multiple (the masked last tile covers the rest)
@@ -2086,8 +2142,8 @@ hipError_t launch_part_fast(const Plan& pp, int grid, hipStream_t s) {
         (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_set = true;
     }
-    // (+ 64 B: compact regions' wave counts after the slim table)
-    const size_t lds = (size_t)(LIMBS == 2 ? slim_words(NACC) : pp.p.nfields) * (pp.p.lcap + 2) * 8 + 64;
+    // (+ the slim flush's workgroup scratch after the table)
+    const size_t lds = (size_t)(LIMBS == 2 ? slim_words(NACC) : pp.p.nfields) * (pp.p.lcap + 2) * 8 + kWgScratch;
     DevProgram none;
     std::memset(&none, 0, sizeof none);
     // 1024 threads where each workgroup has many rows to share its table's
@@ -2096,7 +2152,9 @@ hipError_t launch_part_fast(const Plan& pp, int grid, hipStream_t s) {
     const int64_t per_wg = pp.p.n / std::max(grid, 1);
     int threads = RACC || per_wg < 65536 ? kGbThreads : kGbPartThreads;
     if (!RACC && options().part_threads > 0) threads = std::min(kGbPartThreads, options().part_threads);
-    gb_fast_kernel<NACC, 0, true, 2, LIMBS, RACC, true, false, 0, 0, NULLS><<<grid, threads, lds, s>>>(pp.p, none);
+    GbParams q = pp.p;
+    q.wave_report = options().wave_report;
+    gb_fast_kernel<NACC, 0, true, 2, LIMBS, RACC, true, false, 0, 0, NULLS><<<grid, threads, lds, s>>>(q, none);
     return hipGetLastError();
 }
 

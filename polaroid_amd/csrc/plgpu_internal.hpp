@@ -62,6 +62,8 @@ struct Options {
     int rl_div = 1;       // rolling mean of full windows by one correction step instead of a division (A/B)
     int rl_full = 1;      // rolling sum / mean: interior int64-form waves by the specialised scan (A/B)
     int rl_var128 = 1;    // rolling var / std, interior waves: 128-bit modular numerators where they fit (A/B)
+    int alloc_skew = 0;   // device pool: blocks >= 256 MiB at rotating 64 KiB offsets (A/B)
+    int wave_report = 0;  // fused kernels: publish diagnostics per wave instead of per workgroup (A/B)
     int filt_fused = 0;   // filter: the one-pass look-back kernel where it applies (A/B; measured slower)
     int var_pos = 1;      // fused variance: x's limbs unsigned when the predicate keeps x >= 0 (A/B)
     int sum_pos = 1;      // fused 4-sum kernel: the predicate column's limbs unsigned when it keeps x >= 0 (A/B)

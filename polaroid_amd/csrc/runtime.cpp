@@ -63,6 +63,7 @@ const OptField kOptFields[] = {
     {"part_direct", "PLGPU_PART_DIRECT", &Options::part_direct},
     {"part_compact", "PLGPU_PART_COMPACT", &Options::part_compact},
     {"rl_var128", "PLGPU_RL_VAR128", &Options::rl_var128},
+    {"alloc_skew", "PLGPU_ALLOC_SKEW", &Options::alloc_skew},
     {"part_lds_kb", "PLGPU_PART_LDS_KB", &Options::part_lds_kb},
     {"rl_stream", "PLGPU_RL_STREAM", &Options::rl_stream},
     {"rl_grid", "PLGPU_RL_GRID", &Options::rl_grid},
@@ -173,6 +174,10 @@ struct Pool {
     std::mutex mu;
     std::multimap<size_t, void*> free_blocks;        // size -> ptr
     std::unordered_map<void*, size_t> sizes;         // every block we own
+    // option alloc_skew: large blocks handed out at base + a rotating
+    // multiple of 64 KiB (returned pointer -> base)
+    std::unordered_map<void*, void*> skewed;
+    uint32_t skew_ctr = 0;
     size_t cached = 0;
 };
 Pool& pool_for(int dev) {
@@ -196,16 +201,28 @@ void release_cached(Pool& P) {
 int dev_alloc(void** p, size_t bytes, hipStream_t s) {
     (void)s;
     *p = nullptr;
-    const size_t want = round_bytes(bytes == 0 ? 256 : bytes);
+    // option alloc_skew (A/B): blocks of 256 MiB and more start at one of 16
+    // offsets 64 KiB apart inside a block 1 MiB larger, so the concurrent
+    // streams of a multi-column kernel land at different offsets modulo the
+    // HBM channel interleave whatever their bases
+    const bool skew = options().alloc_skew != 0 && bytes >= (size_t(256) << 20);
+    const size_t want = round_bytes(bytes == 0 ? 256 : bytes + (skew ? size_t(1) << 20 : 0));
     int dev = 0;
     (void)hipGetDevice(&dev);
     Pool& P = pool_for(dev);
     std::lock_guard<std::mutex> lk(P.mu);
     auto it = P.free_blocks.lower_bound(want);
+    auto skew_out = [&]() {
+        if (!skew) return;
+        char* q = (char*)*p + (size_t)(P.skew_ctr++ % 16) * (size_t(64) << 10);
+        P.skewed[q] = *p;
+        *p = q;
+    };
     if (it != P.free_blocks.end() && it->first <= want + want / 4) {
         *p = it->second;
         P.cached -= it->first;
         P.free_blocks.erase(it);
+        skew_out();
         return PLGPU_OK;
     }
     hipError_t e = hipMalloc(p, want);
@@ -223,6 +240,7 @@ int dev_alloc(void** p, size_t bytes, hipStream_t s) {
         }
     }
     P.sizes[*p] = want;
+    skew_out();
     return PLGPU_OK;
 }
 
@@ -233,6 +251,11 @@ void dev_free(void* p, hipStream_t s) {
     (void)hipGetDevice(&dev);
     Pool& P = pool_for(dev);
     std::lock_guard<std::mutex> lk(P.mu);
+    auto sk = P.skewed.find(p);
+    if (sk != P.skewed.end()) {
+        p = sk->second;
+        P.skewed.erase(sk);
+    }
     auto it = P.sizes.find(p);
     if (it == P.sizes.end()) {
         (void)hipFree(p);  // not ours: release directly
