@@ -941,17 +941,6 @@ def main():
         },
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not args.no_filter:
-        # first after the headline, over its frame, with the cached device
-        # blocks returned: the filter's 20 GB of outputs come from a clean
-        # pool (behind the other legs' allocations the scatter measured 10.0
-        # to 12.6 ms from box to box against 10.0 ms standalone,
-        # profiles/r05s_evidence.md, r05t_evidence.md)
-        torch.cuda.empty_cache()
-        pl._native.release_cached()
-        result["filter"] = filter_leg(torch, pl, df, args.leg_steps, 2, int(args.cpu_rows), args.cpu_seconds / 2,
-                                      args.no_cpu)
-        progress(f"filter leg: {result['filter']['ms_per_step']} ms per step")
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(int(args.cpu_rows), args.groups, args.cpu_seconds)
         progress("cpu_baseline done")
@@ -977,6 +966,14 @@ def main():
                                                 [int(x) for x in args.many_groups.split(",") if x],
                                                 int(args.cpu_rows), args.cpu_seconds / 2, args.no_cpu)
         progress("many_groups leg done")
+    if rank == 0 and world == 1 and not args.no_filter:
+        # over the headline frame, behind the other legs' allocations (the
+        # pool is not returned first: the scatter's 10.0-11.5 ms spread
+        # follows where its outputs land in HBM, from a returned pool or not,
+        # profiles/r06_ab/r06r_filter_k0.json, tools/filter_pool_ab.py)
+        result["filter"] = filter_leg(torch, pl, df, args.leg_steps, 2, int(args.cpu_rows), args.cpu_seconds / 2,
+                                      args.no_cpu)
+        progress(f"filter leg: {result['filter']['ms_per_step']} ms per step")
     if rank == 0 and world == 1 and not (args.no_sort and args.no_join and args.no_plugin):
         # the remaining legs need the HBM the headline frame holds
         del df, query, out, sym, cols

@@ -21,6 +21,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=float, default=1e4)
     ap.add_argument("--calls", type=int, default=300)
+    ap.add_argument("--keys", default="symbol", help="symbol | sym_day (Int64 symbol + Int32 day, packed in the kernel)")
     args = ap.parse_args()
     import torch
 
@@ -32,8 +33,13 @@ def main():
     sym = torch.randint(0, 100, (n,), device="cuda", generator=g)
     cols = {k: torch.rand(n, device="cuda", generator=g, dtype=torch.float64) * 500
             for k in ("open", "high", "low", "close")}
-    df = pl.DataFrame([pl.Series.from_torch("symbol", sym)] + [pl.Series.from_torch(k, v) for k, v in cols.items()])
-    q = df.lazy().filter(pl.col("close") > 250.0).group_by("symbol").agg(
+    series = [pl.Series.from_torch("symbol", sym)] + [pl.Series.from_torch(k, v) for k, v in cols.items()]
+    by = ["symbol"]
+    if args.keys == "sym_day":
+        series.append(pl.Series.from_torch("day", (torch.arange(n, device="cuda") * 250 // n).to(torch.int32)))
+        by = ["symbol", "day"]
+    df = pl.DataFrame(series)
+    q = df.lazy().filter(pl.col("close") > 250.0).group_by(*by).agg(
         *[pl.col(k).sum() for k in ("open", "high", "low", "close")])
     for _ in range(20):
         q.collect()
@@ -50,7 +56,7 @@ def main():
     pr.disable()
     s = io.StringIO()
     pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(18)
-    print(json.dumps({"rows": n, "ms_per_collect": round(per * 1e3, 4)}), flush=True)
+    print(json.dumps({"rows": n, "keys": args.keys, "ms_per_collect": round(per * 1e3, 4)}), flush=True)
     print(s.getvalue())
 
 
