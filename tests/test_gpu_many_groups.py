@@ -248,3 +248,21 @@ def test_compact_regions_rerun_on_stale_plan(gpu):
     go, oo = np.argsort(out["k"].to_numpy()), np.argsort(okeys)
     assert np.array_equal(out["k"].to_numpy()[go], okeys[oo])
     assert np.array_equal(_bits(out["s"].to_numpy()[go]), _bits(oouts[0][0][oo]))
+
+
+@pytest.mark.parametrize("compact", [1, 0])
+def test_compact_regions_sorted_keys(gpu, compact, plgpu_option):
+    """Sorted (clustered) keys take the partition kernel's register
+    accumulators (part_racc) before the compact flush: bitwise equal to the
+    oracle with compact regions on and off."""
+    rng = np.random.default_rng(77 + compact)
+    n = 2_000_003
+    key = np.sort(rng.integers(0, 300_000, n)).astype(np.int64) * 13 - 5
+    cols = _ohlc(rng, n)
+    aggs = [("sum", "open"), ("sum", "close")]
+    plgpu_option("part_compact", compact)
+    plgpu_option("gb_path", 3)
+    out, info = _gpu(cols, key, aggs, pl.col("close") > 100.0, False)
+    assert info["path"] == 3, info
+    exp = _expected(cols, key, aggs, ["close"], lambda names: _gt_prog(names.index("close"), 100.0))
+    _compare(out, exp, aggs, False)
