@@ -276,6 +276,18 @@ int plgpu_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream);
  *                  column unsigned when the predicate keeps only x >= 0
  *   "filt_fused"   1: a simple-predicate filter of null-free 8-byte columns
  *                  in one pass (decoupled look-back; off: measured slower)
+ *   "part_compact" 1: sum-only one-workgroup partitions write their groups
+ *                  densely into a region table, misses go to a small hashed
+ *                  overflow table, the finalize reads only the dense runs
+ *   "part_null_sentinel" 1: sum-only partitioned runs write a null Int64 key
+ *                  as a value outside the non-null keys' range (no null-bits
+ *                  column in the partition buffers)
+ *   "rl_var128"    1: rolling var / std interior waves form their numerators
+ *                  modulo 2^128 where the wave's exponent span bounds them
+ *   "wave_report"  1: the slim fused kernels publish their diagnostics per
+ *                  wave instead of once per workgroup
+ *   "alloc_skew"   1: device blocks of 256 MiB and more start at rotating
+ *                  64 KiB offsets (placement probe; off)
  * An unknown name is PLGPU_ERR_INVALID. */
 int plgpu_set_option(const char* name, int64_t value);
 int plgpu_get_option(const char* name, int64_t* out);

@@ -102,6 +102,7 @@ struct PartOut {
 // partition q are tstart[q] .. tstart[q + 1] - 1 (tpart maps a tile back
 // to q), over the partition's rows [range[q], range[q + 1]) of the level-1
 // buffers.  The digit of a key: (part_hash(key) >> sh) & (2^dbits - 1).
+constexpr int kKeyRangeSlots = 256;  // PsGeom::keyrange pairs
 struct PsGeom {
     int64_t n;
     int64_t ntiles;
@@ -110,6 +111,15 @@ struct PsGeom {
     const uint32_t* tpart;
     int32_t sh;
     int32_t dbits;
+    // null-key sentinel (sum-only runs with a nullable Int64 key): the level-1
+    // count pass reduces the non-null keys' range into keyrange[0 .. 1]
+    // (signed min, max pairs, kKeyRangeSlots of them by tile); the level-1
+    // scatter then writes a null key as
+    // `sentinel`, a value no row holds, so no null-bits column is needed
+    int64_t* keyrange;
+    int64_t sentinel;
+    int32_t has_sentinel;
+    int32_t _pad;
 };
 
 struct PsTile {
@@ -269,12 +279,40 @@ __global__ __launch_bounds__(kPsThreads) void gbp_count_kernel(GbParams p, DevPr
     uint32_t nb[kPsPer];
     const int c0 = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) * (kPsTile / (kPsThreads / 64));
     ps_keys<PRED, L2, F8, NUL, false>(p, prog, in, tl, c0, key, pv, sel, nb);
+    if (NUL && !L2 && g.keyrange) {
+        // the non-null keys' signed range (every row in the tile, selected
+        // or not: a superset is enough for a sentinel outside it)
+        int64_t lo = INT64_MAX, hi = INT64_MIN;
+#pragma unroll
+        for (int k = 0; k < kPsPer; ++k) {
+            const int64_t r = tl.base + c0 + k * 64 + (threadIdx.x & 63);
+            if (r >= tl.lo && r < tl.hi && !((nb[k] >> 6) & 1u)) {
+                lo = min(lo, (int64_t)key[k]);
+                hi = max(hi, (int64_t)key[k]);
+            }
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            lo = min(lo, (int64_t)__shfl_xor(lo, off, 64));
+            hi = max(hi, (int64_t)__shfl_xor(hi, off, 64));
+        }
+        // one of kKeyRangeSlots pairs by tile (same-address atomics serialise;
+        // the host folds the slots)
+        if ((threadIdx.x & 63) == 0 && lo <= hi) {
+            int64_t* kr = g.keyrange + 2 * (t % kKeyRangeSlots);
+            atomicMin((long long*)&kr[0], (long long)lo);
+            atomicMax((long long*)&kr[1], (long long)hi);
+        }
+    }
     __syncthreads();
     const uint32_t mask = (uint32_t)P - 1;
 #pragma unroll
     for (int k = 0; k < kPsPer; ++k) {
         const int64_t r = tl.base + c0 + k * 64 + (threadIdx.x & 63);
-        const uint64_t hh = NUL ? ps_hash(key[k], nb[k], r) : part_hash(key[k]);
+        // (level 2 of a sentinel run: the null group's rows spread by position
+        // again, as the null bit spreads them at level 1)
+        const uint64_t hh = NUL ? ps_hash(key[k], nb[k], r)
+                                : ps_hash(key[k], (L2 && g.has_sentinel && key[k] == (uint64_t)g.sentinel) ? 0x40u : 0u, r);
         if (sel[k]) atomicAdd(&h[(uint32_t)(hh >> g.sh) & mask], 1u);
     }
     __syncthreads();
@@ -318,7 +356,10 @@ __global__ __launch_bounds__(kPsThreads) void gbp_scatter_kernel(GbParams p, Dev
 #pragma unroll
     for (int k = 0; k < kPsPer; ++k) {
         const int64_t r = tl.base + c0 + k * 64 + lane;
-        const uint64_t hh = NUL ? ps_hash(key[k], nb[k], r) : part_hash(key[k]);
+        // (level 2 of a sentinel run: the null group's rows spread by position
+        // again, as the null bit spreads them at level 1)
+        const uint64_t hh = NUL ? ps_hash(key[k], nb[k], r)
+                                : ps_hash(key[k], (L2 && g.has_sentinel && key[k] == (uint64_t)g.sentinel) ? 0x40u : 0u, r);
         const uint32_t d = (uint32_t)(hh >> g.sh) & mask;
         uint64_t peers = __ballot(sel[k]);
 #pragma unroll
@@ -376,6 +417,10 @@ __global__ __launch_bounds__(kPsThreads) void gbp_scatter_kernel(GbParams p, Dev
     uint64_t cv[kPsPer];
 #pragma unroll
     for (int k = 0; k < kPsPer; ++k) cv[k] = key[k];
+    if (NUL && !L2 && g.has_sentinel) {
+#pragma unroll
+        for (int k = 0; k < kPsPer; ++k) cv[k] = ((nb[k] >> 6) & 1u) ? (uint64_t)g.sentinel : cv[k];
+    }
 #pragma unroll 1
     for (int ci = 0; ci < ncols; ++ci) {
         // col 0: key; 1..nacc: aggregated columns; nacc + 1: row ids
@@ -1799,6 +1844,8 @@ struct GbRun {
     bool compact_now = false;
     uint32_t* region_cnt = nullptr;
     uint64_t* rtab = nullptr;                // compact regions' table (GbParams::rtab)
+    bool has_null_key = false;               // partitioned: null keys written as null_key (GbParams)
+    int64_t null_key = 0;
     uint64_t* pbuf = nullptr;
     uint64_t* prange = nullptr;              // scan of the count matrix + partition bounds
     const uint64_t* part_range = nullptr;    // P + 1 partition boundaries (inside prange)
@@ -2520,7 +2567,12 @@ static int gb_partition(GbRun& R) {
     // value as +0.0, which the exact sum adds as nothing, so the partition
     // buffers carry null bits only for a nullable key (nul_out); other
     // aggregations keep every value's bit
-    const bool nul_out = R.pl.sum_only ? p.key.validity != nullptr : nul;
+    bool nul_out = R.pl.sum_only ? p.key.validity != nullptr : nul;
+    // sum-only with a nullable Int64 key: the level-1 count pass finds the
+    // non-null keys' range and a null key is written as a value outside it
+    // (GbParams::null_key), so the partition buffers carry no null bits
+    const bool want_sent = R.pl.sum_only && p.key.validity != nullptr && p.key.dtype == PLGPU_I64 && f8 &&
+                           options().part_null_sentinel != 0;
     PsGeom g1;
     std::memset(&g1, 0, sizeof g1);
     g1.n = p.n;
@@ -2535,8 +2587,18 @@ static int gb_partition(GbRun& R) {
     uint64_t* range = R.prange;
     uint64_t* range1 = two ? R.prange + P + 1 : range;
     if (!rc) rc = dev_alloc((void**)&cnt, (size_t)ncnt1 * 4, s);
-    if (!rc) rc = dev_alloc((void**)&part, (size_t)((ncnt1 + kScanChunk - 1) / kScanChunk + 2) * 8, s);
+    // (+ the key range slots of a sentinel run)
+    if (!rc)
+        rc = dev_alloc((void**)&part, (size_t)((ncnt1 + kScanChunk - 1) / kScanChunk + 2 + 2 * kKeyRangeSlots) * 8,
+                       s);
     std::vector<uint64_t> hr1((size_t)P1 + 1);
+    std::vector<int64_t> krange(2 * kKeyRangeSlots);
+    for (int i = 0; i < kKeyRangeSlots; ++i) krange[2 * i] = INT64_MAX, krange[2 * i + 1] = INT64_MIN;
+    if (!rc && want_sent) {
+        g1.keyrange = (int64_t*)(part + (ncnt1 + kScanChunk - 1) / kScanChunk + 2);
+        if (hipMemcpyAsync(g1.keyrange, krange.data(), krange.size() * 8, hipMemcpyHostToDevice, s) != hipSuccess)
+            rc = fail(PLGPU_ERR_HIP, "key range init");
+    }
     if (!rc) {
         hipError_t e = gbp_pass1(R, f8, nul_cnt, g1, cnt, part, false, R.pout);
         const int64_t nb = std::max<int64_t>(1, (ncnt1 + kScanChunk - 1) / kScanChunk);
@@ -2545,8 +2607,26 @@ static int gb_partition(GbRun& R) {
             e = hipGetLastError();
         }
         if (e == hipSuccess) e = hipMemcpyAsync(hr1.data(), range1, (size_t)(P1 + 1) * 8, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess && g1.keyrange)
+            e = hipMemcpyAsync(krange.data(), g1.keyrange, krange.size() * 8, hipMemcpyDeviceToHost, s);
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (e != hipSuccess) rc = hip_fail(e, "gbp_count_kernel");
+    }
+    R.has_null_key = false;
+    if (!rc && g1.keyrange) {
+        // a value outside [min, max] of the non-null keys, never kEmptyKey
+        // (INT64_MIN: the key that has a special slot of its own)
+        int64_t lo = INT64_MAX, hi = INT64_MIN;
+        for (int i = 0; i < kKeyRangeSlots; ++i) lo = std::min(lo, krange[2 * i]), hi = std::max(hi, krange[2 * i + 1]);
+        if (lo > hi) R.null_key = 0, R.has_null_key = true;
+        else if (hi < INT64_MAX) R.null_key = hi + 1, R.has_null_key = true;
+        else if (lo > INT64_MIN + 1) R.null_key = lo - 1, R.has_null_key = true;
+        g1.keyrange = nullptr;
+        if (R.has_null_key) {
+            g1.has_sentinel = 1;
+            g1.sentinel = R.null_key;
+            nul_out = false;
+        }
     }
     uint64_t* buf1 = nullptr;
     PartOut out1;
@@ -2584,6 +2664,8 @@ static int gb_partition(GbRun& R) {
         g2.range = range1;
         g2.sh = 64 - B;
         g2.dbits = b2;
+        g2.has_sentinel = g1.has_sentinel;
+        g2.sentinel = g1.sentinel;
         const int64_t ncnt2 = g2.ntiles << b2;
         uint32_t* meta = nullptr;
         rc = dev_alloc((void**)&meta, (size_t)(P1 + 1 + std::max<int64_t>(g2.ntiles, 1)) * 4, s);
@@ -2706,6 +2788,8 @@ static hipError_t launch_partitioned(const GbRun& R) {
     // from gb_alloc_table)
     q.part_rows = R.pout.rows;
     q.part_nulls = R.pout.nulls;
+    q.has_null_key = R.has_null_key ? 1 : 0;
+    q.null_key = R.null_key;
     q.part_blocks = R.part_blocks;
     q.lbits = R.part_lbits;
     q.lcap = 1 << R.part_lbits;

@@ -198,7 +198,10 @@ struct GbParams {
     uint64_t* rtab;
     int64_t rcap;
     int32_t wave_report;    // option wave_report: per-wave status atomics (A/B of report_wg)
-    int32_t _pad3;
+    // partition buffers of a sum-only run whose null keys were written as
+    // null_key (a value no non-null key holds): those rows are the null group
+    int32_t has_null_key;
+    int64_t null_key;
 };
 
 // ------------------------------------------------------ invariant checks
@@ -1614,9 +1617,9 @@ __global__ __launch_bounds__(PART && !RUNS ? kGbPartThreads : kGbThreads) void g
                 sel = sel && fast_row(t, T, ROWS, j) < p.n;
             }
             if (PACK && sel && kout[j]) d.kbad = 1u;
-            slot[j] = sel ? (NULLS && ((nrw[j] >> 6) & 1u) ? p.lcap
-                                                           : (cur.key[j] == kEmptyKey ? p.lcap + 1 : kGlobalKey))
-                          : kNotSelected;
+            const bool knull = (NULLS && ((nrw[j] >> 6) & 1u)) ||
+                               (PART && p.has_null_key && cur.key[j] == (uint64_t)p.null_key);
+            slot[j] = sel ? (knull ? p.lcap : (cur.key[j] == kEmptyKey ? p.lcap + 1 : kGlobalKey)) : kNotSelected;
             h[j] = hash_slot(cur.key[j], p.lbits);
             probe[j] = lds_load(&lds[h[j]]);
         }

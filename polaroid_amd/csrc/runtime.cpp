@@ -64,6 +64,8 @@ const OptField kOptFields[] = {
     {"part_compact", "PLGPU_PART_COMPACT", &Options::part_compact},
     {"rl_var128", "PLGPU_RL_VAR128", &Options::rl_var128},
     {"alloc_skew", "PLGPU_ALLOC_SKEW", &Options::alloc_skew},
+    {"wave_report", "PLGPU_WAVE_REPORT", &Options::wave_report},
+    {"part_null_sentinel", "PLGPU_PART_NULL_SENTINEL", &Options::part_null_sentinel},
     {"part_lds_kb", "PLGPU_PART_LDS_KB", &Options::part_lds_kb},
     {"rl_stream", "PLGPU_RL_STREAM", &Options::rl_stream},
     {"rl_grid", "PLGPU_RL_GRID", &Options::rl_grid},

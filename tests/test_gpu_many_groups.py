@@ -266,3 +266,48 @@ def test_compact_regions_sorted_keys(gpu, compact, plgpu_option):
     assert info["path"] == 3, info
     exp = _expected(cols, key, aggs, ["close"], lambda names: _gt_prog(names.index("close"), 100.0))
     _compare(out, exp, aggs, False)
+
+
+@pytest.mark.parametrize("extremes", ["none", "max", "max_and_min"])
+@pytest.mark.parametrize("sentinel", [1, 0])
+def test_null_key_sentinel(gpu, plgpu_option, extremes, sentinel):
+    """A sum-only partitioned run over a nullable Int64 key writes each null
+    key as a value outside the non-null keys' range (above the maximum, else
+    below the minimum, never INT64_MIN, which has a special slot of its own)
+    instead of carrying a null-bits column (option part_null_sentinel).  Keys
+    holding INT64_MAX (sentinel below the range) or INT64_MAX and INT64_MIN + 1
+    (no sentinel: the null-bits column) with the option on and off, bitwise
+    equal to the oracle, INT64_MIN keys and the null group included."""
+    rng = np.random.default_rng(3 + sentinel + len(extremes))
+    n = 1_500_007
+    key = rng.integers(-200_000, 200_000, n).astype(np.int64)
+    if extremes in ("max", "max_and_min"):
+        key[rng.random(n) < 0.001] = I64_MAX
+    if extremes == "max_and_min":
+        key[rng.random(n) < 0.001] = I64_MIN + 1
+    key[rng.random(n) < 0.001] = I64_MIN
+    kvalid = rng.random(n) > 0.02
+    cols = _ohlc(rng, n)
+    vvalid = rng.random(n) > 0.01
+    aggs = [("sum", "open"), ("sum", "close")]
+    plgpu_option("part_null_sentinel", sentinel)
+    plgpu_option("gb_path", 3)
+    data = {"k": pl.Series.from_numpy("k", key, kvalid), "open": pl.Series.from_numpy("open", cols["open"], vvalid),
+            "close": pl.Series.from_numpy("close", cols["close"])}
+    info = {}
+    out = pl.DataFrame(data).lazy().filter(pl.col("close") > 100.0).group_by("k").agg(
+        *[pl.col(c).sum().alias(f"sum_{c}") for _, c in aggs]).collect(info=info)
+    assert info["path"] == 3, info
+    names = ["open", "close"]
+    okeys, okvalid, oouts = O.group_by_agg(O.HostCol(key, kvalid), [O.HostCol(cols["open"], vvalid),
+                                                                     O.HostCol(cols["close"])],
+                                           _gt_prog(1, 100.0), [("sum", 0), ("sum", 1)], n, O.SUM_EXACT)
+    gk, gkv = out["k"].to_numpy().astype(np.int64), out["k"].validity_numpy()
+    tg = [("n", 0) if not v else ("k", int(k_)) for k_, v in zip(gk, gkv)]
+    to = [("n", 0) if not v else ("k", int(k_)) for k_, v in zip(okeys, okvalid)]
+    assert len(tg) == len(to) and set(tg) == set(to)
+    pos = {t: i for i, t in enumerate(to)}
+    oo = np.array([pos[t] for t in tg], dtype=np.int64)
+    for (kind, c), (ov, ovalid) in zip(aggs, oouts):
+        s = out[f"{kind}_{c}"]
+        assert np.array_equal(_bits(s.to_numpy()), _bits(ov[oo])), c
