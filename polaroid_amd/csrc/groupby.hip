@@ -4130,10 +4130,9 @@ static int gb_multi_decode(const MkPack& pk, const plgpu_column* keys, int32_t n
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) rc = hip_fail(e, "mk_unpack_kernel");
     }
-    if (!rc) {
-        hipError_t e = hipStreamSynchronize(s);
-        if (e != hipSuccess) rc = hip_fail(e, "multi-key decode");
-    }
+    // (no synchronisation: the key columns are ready in the caller's stream
+    // order, and hout's block is reused only by work enqueued after these
+    // kernels)
     plgpu_column_release(&hout);
     if (rc) {
         for (int i = 0; i < nkeys; ++i) plgpu_column_release(&out_keys[i]);
