@@ -63,6 +63,7 @@ struct Options {
     int rl_full = 1;      // rolling sum / mean: interior int64-form waves by the specialised scan (A/B)
     int rl_var128 = 1;    // rolling var / std, interior waves: 128-bit modular numerators where they fit (A/B)
     int alloc_skew = 0;   // device pool: blocks >= 256 MiB at rotating 64 KiB offsets (A/B)
+    int alloc_contig = 0; // device pool: blocks >= 256 MiB physically contiguous where the driver can (A/B)
     int wave_report = 0;  // fused kernels: publish diagnostics per wave instead of per workgroup (A/B)
     int part_null_sentinel = 1; // partitioned sum-only runs: null Int64 keys as an unused key value (A/B)
     int filt_fused = 0;   // filter: the one-pass look-back kernel where it applies (A/B; measured slower)

@@ -64,6 +64,7 @@ const OptField kOptFields[] = {
     {"part_compact", "PLGPU_PART_COMPACT", &Options::part_compact},
     {"rl_var128", "PLGPU_RL_VAR128", &Options::rl_var128},
     {"alloc_skew", "PLGPU_ALLOC_SKEW", &Options::alloc_skew},
+    {"alloc_contig", "PLGPU_ALLOC_CONTIG", &Options::alloc_contig},
     {"wave_report", "PLGPU_WAVE_REPORT", &Options::wave_report},
     {"part_null_sentinel", "PLGPU_PART_NULL_SENTINEL", &Options::part_null_sentinel},
     {"part_lds_kb", "PLGPU_PART_LDS_KB", &Options::part_lds_kb},
@@ -227,7 +228,14 @@ int dev_alloc(void** p, size_t bytes, hipStream_t s) {
         skew_out();
         return PLGPU_OK;
     }
-    hipError_t e = hipMalloc(p, want);
+    hipError_t e = hipErrorOutOfMemory;
+    if (options().alloc_contig != 0 && want >= (size_t(256) << 20)) {
+        // (option alloc_contig, A/B: physically contiguous large blocks, for
+        // the TLB reach of streams over them; plain hipMalloc when refused)
+        e = hipExtMallocWithFlags(p, want, hipDeviceMallocContiguous);
+        if (e != hipSuccess) (void)hipGetLastError();
+    }
+    if (e != hipSuccess) e = hipMalloc(p, want);
     if (e != hipSuccess) {
         (void)hipGetLastError();
         (void)hipDeviceSynchronize();
