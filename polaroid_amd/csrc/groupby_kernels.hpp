@@ -220,6 +220,7 @@ enum : uint32_t {
     CK_PART_POS = 128,    // partition scatter position outside the buffers
     CK_KEY_ROW = 256,     // multi-key output key row outside [0, n)
     CK_PERM = 512,        // group-order permutation entry outside [0, groups)
+    CK_REGION = 1024,     // compact region slot outside its partition's region / the region table
     CK_FIELD = 1024       // apply_row: table field outside [0, nfields)
 };
 #ifdef PLGPU_CHECKS
@@ -1846,8 +1847,10 @@ __global__ __launch_bounds__(PART && !RUNS ? kGbPartThreads : kGbThreads) void g
                 if (live) {
                     const uint32_t idx = run + before + (uint32_t)__popcll(bl & ((1ull << lane) - 1ull));
                     ++d.newkeys;
-                    p.rtab[t0 + idx] = lds[sl];
-                    store_slot(sl, p.rtab, p.rcap, t0 + idx, len);
+                    if (gb_ok(idx < (uint32_t)p.lcap && t0 + (int64_t)idx < p.rcap, CK_REGION)) {
+                        p.rtab[t0 + idx] = lds[sl];
+                        store_slot(sl, p.rtab, p.rcap, t0 + idx, len);
+                    }
                 } else if (len != 0) {
                     d.special |= sl == p.lcap ? 1u : 2u;
                     add_slot(sl, sl == p.lcap ? p.gcap : p.gcap + 1, len);

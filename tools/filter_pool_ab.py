@@ -7,6 +7,7 @@ filter(close > 250) timed
      blocks left cached in the library's pool),
   C  after B with the pool returned again,
   D<m> the pool returned and a block of m MiB + 4 KiB held (placement probe),
+  S  the same columns copied into one block at staggered starts,
 
 each 5 steps after 2 warm-ups, one JSON line per state with the scatter and
 mask kernel times (HIP events) and the pool's cached bytes before the state.
@@ -36,8 +37,26 @@ def main():
     sym, cols = bench.make_data(torch, n, 100, seed=1234)
     df = pl.DataFrame([pl.Series.from_torch("symbol", sym)] + [pl.Series.from_torch(c, t) for c, t in cols.items()])
 
-    def run(tag):
-        r = bench.filter_leg(torch, pl, df, 5, 2, 0, 0.0, True)
+    # S: the same columns copied to staggered starts (column i at i * 2 MiB +
+    # i * 4 KiB past a 2 MiB boundary of one shared block), so the five
+    # streams do not share their start offsets modulo any large power of two
+    stag = None
+
+    def staggered():
+        names = ["symbol"] + list(cols)
+        src = [sym] + list(cols.values())
+        step = n + (1 << 18) + 512
+        blk = torch.empty(step * len(src), dtype=torch.int64, device="cuda")
+        out = []
+        for i, (nm, t) in enumerate(zip(names, src)):
+            o = i * step + i * 512
+            v = blk[o:o + n].view(t.dtype)
+            v.copy_(t)
+            out.append(pl.Series.from_torch(nm, v))
+        return pl.DataFrame(out), blk
+
+    def run(tag, frame=None):
+        r = bench.filter_leg(torch, pl, frame if frame is not None else df, 5, 2, 0, 0.0, True)
         k = r["kernels"]
         print(json.dumps({"state": tag, "ms_per_step": r["ms_per_step"],
                           "scatter_ms": k.get("filter_scatter8_kernel", {}).get("ms_mean"),
@@ -47,6 +66,12 @@ def main():
 
     hold = []
     for st in args.states.split(","):
+        if st == "S":
+            if stag is None:
+                stag = staggered()
+            r_frame = stag[0]
+            run("S", r_frame)
+            continue
         if st in ("A", "C"):
             torch.cuda.empty_cache()
             pl._native.release_cached()
