@@ -65,6 +65,8 @@ const OptField kOptFields[] = {
     {"rl_var128", "PLGPU_RL_VAR128", &Options::rl_var128},
     {"alloc_skew", "PLGPU_ALLOC_SKEW", &Options::alloc_skew},
     {"alloc_contig", "PLGPU_ALLOC_CONTIG", &Options::alloc_contig},
+    {"srt_w4", "PLGPU_SRT_W4", &Options::srt_w4},
+    {"srt_up_tiles", "PLGPU_SRT_UP_TILES", &Options::srt_up_tiles},
     {"wave_report", "PLGPU_WAVE_REPORT", &Options::wave_report},
     {"part_null_sentinel", "PLGPU_PART_NULL_SENTINEL", &Options::part_null_sentinel},
     {"part_lds_kb", "PLGPU_PART_LDS_KB", &Options::part_lds_kb},

@@ -224,21 +224,45 @@ enum SrtOut { SRT_SEP = 0, SRT_PACK = 1, SRT_IDX = 2 };
 // (A resident grid looping over the tiles, the next tile's keys loaded
 // before this one's counts, measured no faster: 1.63 against 1.56 ms; the
 // same loop made the downsweep slower, 3.9 -> 5.5-6.0 ms: not kept.)
+// tpw tiles per workgroup (option srt_up_tiles; 1: one tile per workgroup,
+// XCD-remapped): each tile's histogram is written on its own, the next
+// tile's codes already in flight while this one's are counted.
 __global__ __launch_bounds__(kSrtThreads) void srt_upsweep_kernel(const uint64_t* __restrict__ keys, int64_t n,
                                                                   int shift, int64_t ntiles,
-                                                                  uint32_t* __restrict__ cnt) {
+                                                                  uint32_t* __restrict__ cnt, int tpw) {
     __shared__ uint32_t h[256];
-    h[threadIdx.x] = 0;
-    __syncthreads();
-    const int64_t tile = xcd_tile(blockIdx.x, ntiles);
-    const int64_t base = tile * kSrtTile;
+    const int64_t nwg = (ntiles + tpw - 1) / tpw;
+    const int64_t t0 = xcd_tile(blockIdx.x, nwg) * tpw;
+    const int64_t t1 = t0 + tpw < ntiles ? t0 + tpw : ntiles;
+    uint64_t v[kSrtPer];
+    auto load = [&](int64_t tile) {
+        const int64_t base = tile * kSrtTile;
 #pragma unroll
-    for (int k = 0; k < kSrtPer; ++k) {
-        const int64_t i = base + k * kSrtThreads + threadIdx.x;
-        if (i < n) atomicAdd(&h[(__builtin_nontemporal_load(keys + i) >> shift) & 0xFF], 1u);
+        for (int k = 0; k < kSrtPer; ++k) {
+            const int64_t i = base + k * kSrtThreads + threadIdx.x;
+            v[k] = i < n ? __builtin_nontemporal_load(keys + i) : ~0ull;
+        }
+    };
+    if (t0 < t1) load(t0);
+    for (int64_t tile = t0; tile < t1; ++tile) {
+        h[threadIdx.x] = 0;
+        __syncthreads();
+        const int64_t base = tile * kSrtTile;
+        uint32_t d[kSrtPer];
+        bool in[kSrtPer];
+#pragma unroll
+        for (int k = 0; k < kSrtPer; ++k) {
+            d[k] = (uint32_t)(v[k] >> shift) & 0xFF;
+            in[k] = base + k * kSrtThreads + threadIdx.x < n;
+        }
+        if (tile + 1 < t1) load(tile + 1);
+#pragma unroll
+        for (int k = 0; k < kSrtPer; ++k)
+            if (in[k]) atomicAdd(&h[d[k]], 1u);
+        __syncthreads();
+        cnt[(int64_t)threadIdx.x * ntiles + tile] = h[threadIdx.x];
+        __syncthreads();
     }
-    __syncthreads();
-    cnt[(int64_t)threadIdx.x * ntiles + tile] = h[threadIdx.x];
 }
 
 // Downsweep: stable scatter of one tile by the digit at `shift` (of the
@@ -252,8 +276,12 @@ __global__ __launch_bounds__(kSrtThreads) void srt_upsweep_kernel(const uint64_t
 // array of the next pass's digit bytes, written here so the next upsweep
 // reads 1 B instead of 8 per code, cut the upsweep 1.78 -> 0.38 ms but cost
 // every downsweep 1.2 ms of scattered byte stores: not kept.)
-template <bool IN_P, int OUT>
-__global__ __launch_bounds__(kSrtThreads) void srt_downsweep_kernel(const uint64_t* __restrict__ keys_in,
+// WPE: the occupancy the register allocation targets (waves per SIMD; 1 =
+// the compiler's choice, 142 VGPRs for the packed passes: 3 workgroups per
+// CU; 4 = 128 VGPRs with a few spilled words: 4 workgroups per CU, which the
+// LDS allows), option srt_w4 (A/B)
+template <bool IN_P, int OUT, int WPE = 1>
+__global__ __launch_bounds__(kSrtThreads) __attribute__((amdgpu_waves_per_eu(WPE))) void srt_downsweep_kernel(const uint64_t* __restrict__ keys_in,
                                                                     const uint32_t* __restrict__ idx_in, int64_t n,
                                                                     int shift, int64_t ntiles,
                                                                     const uint32_t* __restrict__ off,
@@ -476,6 +504,13 @@ static void srt_down(const uint64_t* ki, const uint32_t* ii, int64_t nv, int shi
                      const uint32_t* off, uint64_t* ko, uint32_t* io, int cons, uint64_t kmask, hipStream_t s) {
     // XCD-aware tiles (round-robin tiles measured slower, profiles/r02_sort_xcd_ab.log)
     KtScope kt("srt_downsweep_kernel", s);
+    if constexpr (IN_P && OUT != SRT_SEP) {
+        if (options().srt_w4) {
+            srt_downsweep_kernel<IN_P, OUT, 4>
+                <<<(unsigned)ntiles, kSrtThreads, 0, s>>>(ki, ii, nv, shift, ntiles, off, ko, io, cons, kmask);
+            return;
+        }
+    }
     srt_downsweep_kernel<IN_P, OUT>
         <<<(unsigned)ntiles, kSrtThreads, 0, s>>>(ki, ii, nv, shift, ntiles, off, ko, io, cons, kmask);
 }
@@ -526,7 +561,11 @@ static int radix_passes(uint64_t* keys[2], uint32_t* idx[2], int64_t nv, int& cu
         const uint32_t* ii = (ids_implicit && j == 0) ? nullptr : idx[cur];
         if (!(pre && j == 0 && S == 0)) {  // byte-0 counts already in sc.cnt
             KtScope kt("srt_upsweep_kernel", s);
-            srt_upsweep_kernel<<<(unsigned)ntiles, kSrtThreads, 0, s>>>(keys[cur], nv, shift, ntiles, sc.cnt);
+        {
+            const int tpw = std::max<int>(1, (int)options().srt_up_tiles);
+            srt_upsweep_kernel<<<(unsigned)((ntiles + tpw - 1) / tpw), kSrtThreads, 0, s>>>(keys[cur], nv, shift,
+                                                                                           ntiles, sc.cnt, tpw);
+        }
         }
         e = scan_exclusive32_inplace(sc.cnt, ntiles * 256, sc.part, s);
         if (e != hipSuccess) return hip_fail(e, "sort scan");
