@@ -288,6 +288,11 @@ int plgpu_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream);
  *                  wave instead of once per workgroup
  *   "alloc_skew"   1: device blocks of 256 MiB and more start at rotating
  *                  64 KiB offsets (placement probe; off)
+ *   "alloc_contig" 1: device blocks of 256 MiB and more physically
+ *                  contiguous where the driver grants it (placement probe; off)
+ *   "srt_w4"       1: the sort's packed downsweeps compiled for 4 waves per
+ *                  SIMD (off: measured slower)
+ *   "srt_up_tiles" tiles per sort upsweep workgroup (1; more measured slower)
  * An unknown name is PLGPU_ERR_INVALID. */
 int plgpu_set_option(const char* name, int64_t value);
 int plgpu_get_option(const char* name, int64_t* out);
