@@ -293,6 +293,7 @@ int plgpu_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream);
  *   "srt_w4"       1: the sort's packed downsweeps compiled for 4 waves per
  *                  SIMD (off: measured slower)
  *   "srt_up_tiles" tiles per sort upsweep workgroup (1; more measured slower)
+ *   "part_rows4"   1: 512-thread partition workgroups take 4 rows per thread
  * An unknown name is PLGPU_ERR_INVALID. */
 int plgpu_set_option(const char* name, int64_t value);
 int plgpu_get_option(const char* name, int64_t* out);

@@ -1280,7 +1280,7 @@ constexpr int kGbPartThreads = 1024;
 // with each tile (FastTile::nv: one byte per row pair and column read).
 template <int NACC, int PRED, bool SUMONLY, int ROWS, int LIMBS = 3, bool RUNS = false, bool PART = false,
           bool DERIV = false, int VAR = 0, int PACK = 0, bool NULLS = false>
-__global__ __launch_bounds__(PART && !RUNS ? kGbPartThreads : kGbThreads) void gb_fast_kernel(GbParams p,
+__global__ __launch_bounds__(PART && !RUNS && ROWS == 2 ? kGbPartThreads : kGbThreads) void gb_fast_kernel(GbParams p,
                                                                                                DevProgram prog) {
     static_assert(!PACK || !PART, "PACK: the single-table kernel");
     static_assert(!NULLS || (!RUNS && !DERIV && (VAR == 0 || VAR == 5) && PACK == 0), "NULLS: plain inputs");
@@ -2160,6 +2160,22 @@ hipError_t launch_part_fast(const Plan& pp, int grid, hipStream_t s) {
     if (!RACC && options().part_threads > 0) threads = std::min(kGbPartThreads, options().part_threads);
     GbParams q = pp.p;
     q.wave_report = options().wave_report;
+    if constexpr (LIMBS == 2 && !RACC) {
+        // option part_rows4 (A/B): 512-thread workgroups holding 4 rows per
+        // thread (two row pairs in flight per tile instead of one), compiled
+        // for 512 threads: a partition workgroup owns its CU's LDS, so the
+        // extra registers cost no occupancy
+        if (threads == kGbThreads && options().part_rows4) {
+            const void* k4 = (const void*)gb_fast_kernel<NACC, 0, true, 4, 2, false, true, false, 0, 0, NULLS>;
+            static bool attr4 = false;
+            if (!attr4) {
+                (void)hipFuncSetAttribute(k4, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                attr4 = true;
+            }
+            gb_fast_kernel<NACC, 0, true, 4, 2, false, true, false, 0, 0, NULLS><<<grid, threads, lds, s>>>(q, none);
+            return hipGetLastError();
+        }
+    }
     gb_fast_kernel<NACC, 0, true, 2, LIMBS, RACC, true, false, 0, 0, NULLS><<<grid, threads, lds, s>>>(q, none);
     return hipGetLastError();
 }

@@ -66,6 +66,7 @@ struct Options {
     int alloc_contig = 0; // device pool: blocks >= 256 MiB physically contiguous where the driver can (A/B)
     int srt_w4 = 0;       // sort: packed downsweeps compiled for 4 waves per SIMD (A/B)
     int srt_up_tiles = 1; // sort: tiles per upsweep workgroup, the next tile's codes prefetched (A/B)
+    int part_rows4 = 0;   // partitioned aggregation, 512-thread workgroups: 4 rows per thread (A/B)
     int wave_report = 0;  // fused kernels: publish diagnostics per wave instead of per workgroup (A/B)
     int part_null_sentinel = 1; // partitioned sum-only runs: null Int64 keys as an unused key value (A/B)
     int filt_fused = 0;   // filter: the one-pass look-back kernel where it applies (A/B; measured slower)

@@ -67,6 +67,7 @@ const OptField kOptFields[] = {
     {"alloc_contig", "PLGPU_ALLOC_CONTIG", &Options::alloc_contig},
     {"srt_w4", "PLGPU_SRT_W4", &Options::srt_w4},
     {"srt_up_tiles", "PLGPU_SRT_UP_TILES", &Options::srt_up_tiles},
+    {"part_rows4", "PLGPU_PART_ROWS4", &Options::part_rows4},
     {"wave_report", "PLGPU_WAVE_REPORT", &Options::wave_report},
     {"part_null_sentinel", "PLGPU_PART_NULL_SENTINEL", &Options::part_null_sentinel},
     {"part_lds_kb", "PLGPU_PART_LDS_KB", &Options::part_lds_kb},

@@ -187,3 +187,22 @@ def test_integration_rust_bindings_match_header():
     assert not bad, f"parameter counts differ (header, Rust): {bad}"
     for c_name, r_name in (("plgpu_groupby_info", "PlgpuGroupByInfo"), ("plgpu_column", "PlgpuColumn")):
         assert hs[c_name] == rs[r_name], (c_name, hs[c_name], rs[r_name])
+
+
+def test_documented_options_exist(N):
+    """Every option name the header documents under plgpu_set_option is one
+    the library knows (set, read back, restored) -- no GPU needed; an
+    undocumented name is PLGPU_ERR_INVALID."""
+    import re
+
+    hdr = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include",
+                            "polaroid_gpu.h")).read()
+    i = hdr.index("int plgpu_set_option(")
+    block = hdr[hdr.rindex("/*", 0, i):i]
+    names = sorted(set(re.findall(r'^\s*\*\s+"([a-z0-9_]+)"', block, re.M)))
+    assert len(names) >= 20, names
+    for name in names:
+        prev = N.set_option(name, 0)
+        assert N.set_option(name, prev) == 0, name
+    v = C.c_int64(0)
+    assert N.lib().plgpu_get_option(b"no_such_option", C.byref(v)) == N.ERR_INVALID
