@@ -284,6 +284,9 @@ int plgpu_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream);
  *                  column in the partition buffers)
  *   "rl_var128"    1: rolling var / std interior waves form their numerators
  *                  modulo 2^128 where the wave's exponent span bounds them
+ *   "rl_var_hot"   1: rolling var / std run their common blocks (interior,
+ *                  finite, 128-bit numerators) in a kernel of their own and
+ *                  the other blocks from a device-side list afterwards
  *   "wave_report"  1: the slim fused kernels publish their diagnostics per
  *                  wave instead of once per workgroup
  *   "alloc_skew"   1: device blocks of 256 MiB and more start at rotating

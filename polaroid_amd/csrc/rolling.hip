@@ -56,6 +56,7 @@ struct RlParams {
     double wd;            // w as an f64
     double rw2;           // var / std: RN(1 / (w - ddof)) (w > ddof)
     double wd2;           // var / std: w - ddof as an f64
+    uint32_t* rest;       // rl_var_hot_kernel: blocks for rl_var_rest_kernel (word 0: count)
 };
 
 // RN(a / w) for a full window (count w) without a division: q0 = RN(a y),
@@ -944,10 +945,29 @@ __device__ __forceinline__ double u128_to_double(uint64_t nl, uint64_t nh, int e
     return __builtin_ldexp((double)top, (hi ? 128 : 64) - 64 - lz + e);
 }
 
+// sqrt(x), correctly rounded, for x == 0 or 2^-767 <= x < 2^1024: the
+// compiler's f64 square root sequence (v_rsq_f64, then two Newton steps on
+// the root and its half-reciprocal) without its small-input scaling and its
+// class test, which such inputs never take.
+__device__ __forceinline__ double sqrt_rn_scaled_free(double x) {
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y, h = y * 0.5;
+    const double r = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, r, g);
+    h = __builtin_fma(h, r, h);
+    double d = __builtin_fma(-g, g, x);
+    g = __builtin_fma(d, h, g);
+    d = __builtin_fma(-g, g, x);
+    g = __builtin_fma(d, h, g);
+    return x == 0.0 ? x : g;
+}
+
 // N128: the wave's numerators are below 2^128 (rw_block: 2 (54 + span) +
 // 2 lw <= 129, so w S2 - S1^2 = sum over pairs (t_i - t_j)^2 < 2^128), so
 // w S2 and S1^2 are formed modulo 2^128 and their difference is exact.
-template <bool DIV1, bool N128>
+// EMIT: 0 p.var / p.var_f32 decide (rv_std); 1 the variance; 2 its square
+// root by sqrt_rn_scaled_free (the caller bounds nonzero variances >= 2^-767)
+template <bool DIV1, bool N128, int EMIT = 0>
 __device__ __forceinline__ void rw_var_scan_full(const RlParams& p, const uint64_t (&x)[kRwChunks + 1],
                                                  int64_t o_first, int64_t o_end, int64_t s_first, int tmin,
                                                  uint64_t* ring) {
@@ -1026,7 +1046,8 @@ __device__ __forceinline__ void rw_var_scan_full(const RlParams& p, const uint64
         } else {
             v = (nr / wd) / wd2;
         }
-        if (p.var == 2) v = rv_std(p, v);
+        if (EMIT == 0 && p.var == 2) v = rv_std(p, v);
+        if (EMIT == 2) v = sqrt_rn_scaled_free(v);
         const bool in = 64 * q + lane < nout;
         if (in) ol[64 * q] = ok ? v : 0.0;
         const uint64_t bits = __ballot(in && ok);
@@ -1205,6 +1226,107 @@ __global__ __launch_bounds__(256) void rl_stream_kernel(RlParams p) {
 #pragma unroll
         for (int k = 0; k <= kRwChunks; ++k) x[k] = xn[k];
         s_first = sn;
+    }
+}
+
+// rolling var / std, its common block alone (option rl_var_hot): a
+// null-free interior block whose values are finite and fit the fast form
+// with both one-correction quotients and the numerators modulo 2^128
+// (rw_block's conditions for rw_var_scan_full<true, true>).  Without the
+// general paths inlined the kernel holds fewer registers (more waves per
+// SIMD, no scalar spills in the loop).  Any other block goes to
+// p.rest (count in word 0, then block indices) for rl_var_rest_kernel.
+template <int DT, bool STD>
+__device__ __forceinline__ bool rw_var_hot_block(const RlParams& p, uint64_t (&x)[kRwChunks + 1], int64_t o_first,
+                                                 int64_t s_first, uint64_t* ring, int lw, int64_t right) {
+    const int64_t o_end = o_first + kRwOut < p.n ? o_first + kRwOut : p.n;
+    if (!(o_first - (p.w - right) >= 0 && o_end + right - 1 <= p.n)) return false;
+    uint32_t mx = 0, inv_mn = 0;
+    bool odd = false;
+#pragma unroll
+    for (int k = 0; k <= kRwChunks; ++k) {
+        const int64_t r = s_first + 64 * k + (threadIdx.x & 63);
+        const uint64_t b = r >= p.n ? 0ull : DT == PLGPU_F64 ? x[k] : f64_bits((double)(int64_t)x[k]);
+        x[k] = b;
+        const uint32_t ex = (uint32_t)(b >> 52) & 0x7FF;
+        odd |= ex == 0x7FF;
+        if ((b << 1) != 0) {
+            const uint32_t e1 = ex ? ex : 1;
+            mx = e1 > mx ? e1 : mx;
+            inv_mn = 0x7FF - e1 > inv_mn ? 0x7FF - e1 : inv_mn;
+        }
+    }
+    if (__ballot(odd) != 0) return false;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint32_t a = __shfl_xor(mx, off, 64), c = __shfl_xor(inv_mn, off, 64);
+        mx = a > mx ? a : mx;
+        inv_mn = c > inv_mn ? c : inv_mn;
+    }
+    const int tmax = (int)mx, tmin = mx ? 0x7FF - (int)inv_mn : 1024;
+    const int span = tmax - tmin;
+    const bool vfast = mx == 0 || (tmin >= 600 && lw + 53 + span <= 63 && 2 * (53 + span) + lw <= 126);
+    const int b2 = 2 * (tmin - 1075), top = 2 * (tmax - 1022) + 2 * lw;
+    // (nonzero variances >= 2^(b2 - 2 lw) >= 2^-760: sqrt_rn_scaled_free's range)
+    const bool div1 = b2 - 2 * lw >= -760 && top <= 990;
+    const bool n128 = 2 * (54 + span) + 2 * lw <= 129;
+    if (!(vfast && div1 && n128)) return false;
+    rw_var_scan_full<true, true, STD ? 2 : 1>(p, x, o_first, o_end, s_first, tmin, ring);
+    return true;
+}
+
+template <int DT, bool STREAM, bool STD>
+__global__ __launch_bounds__(256) void rl_var_hot_kernel(RlParams p) {
+    __shared__ uint64_t ring[kRwWaves][3 * kRwRing];
+    const int wv = threadIdx.x >> 6;
+    const int64_t nblocks = (p.n + kRwOut - 1) / kRwOut;
+    const int64_t stride = STREAM ? (int64_t)gridDim.x * kRwWaves : nblocks;
+    int64_t b = (int64_t)blockIdx.x * kRwWaves + wv;
+    if (b >= nblocks) return;  // (no workgroup barriers below)
+    int lw = 0;
+    while ((int64_t(1) << lw) <= p.w) ++lw;  // p.w < 2^lw
+    const int64_t right = p.center ? (p.w + 1) / 2 : 1;
+    int64_t s_first, tmp;
+    rl_bounds(p, b * kRwOut, s_first, tmp);
+    uint64_t x[kRwChunks + 1];
+    rw_load_block<DT>(p, s_first, x);
+    for (; b < nblocks; b += stride) {
+        // (STREAM: resident waves, the next block's rows in flight while
+        // this one is scanned)
+        const int64_t bn = b + stride;
+        int64_t sn = 0;
+        uint64_t xn[kRwChunks + 1];
+        if constexpr (STREAM) {
+            if (bn < nblocks) {
+                rl_bounds(p, bn * kRwOut, sn, tmp);
+                rw_load_block<DT>(p, sn, xn);
+            }
+        }
+        if (!rw_var_hot_block<DT, STD>(p, x, b * kRwOut, s_first, ring[wv], lw, right) && (threadIdx.x & 63) == 0)
+            p.rest[1 + atomicAdd(&p.rest[0], 1u)] = (uint32_t)b;
+        if constexpr (STREAM) {
+#pragma unroll
+            for (int k = 0; k <= kRwChunks; ++k) x[k] = xn[k];
+            s_first = sn;
+        }
+    }
+}
+
+// The blocks rl_var_hot_kernel left, one per wave, by rw_block.
+template <int DT>
+__global__ __launch_bounds__(256) void rl_var_rest_kernel(RlParams p) {
+    __shared__ uint64_t ring[kRwWaves][3 * kRwRing];
+    __shared__ uint64_t ring_v2[kRwWaves][kRwRing];
+    const int wv = threadIdx.x >> 6;
+    const uint32_t cnt = __builtin_nontemporal_load(&p.rest[0]);
+    for (uint32_t j = blockIdx.x * kRwWaves + wv; j < cnt; j += gridDim.x * kRwWaves) {
+        const int64_t b = p.rest[1 + j];
+        int64_t s_first, tmp;
+        rl_bounds(p, b * kRwOut, s_first, tmp);
+        uint64_t x[kRwChunks + 1];
+        rw_load_block<DT>(p, s_first, x);
+        rw_block<DT, false, true>(p, x, b * kRwOut, s_first, ring[wv], ring[wv] + kRwRing, ring[wv] + 2 * kRwRing,
+                                  ring_v2[wv]);
     }
 }
 
@@ -1554,7 +1676,35 @@ PLGPU_API int plgpu_rolling(const plgpu_column* values, int32_t kind, int64_t wi
         const unsigned g = (unsigned)((p.n + (int64_t)kRwOut * kRwWaves - 1) / ((int64_t)kRwOut * kRwWaves));
         const bool nl = p.c.validity != nullptr;
         KtScope kt(var ? "rl_wave_var_kernel" : "rl_wave_kernel", s);
-        if (!nl && options().rl_stream != 0) {
+        const bool hot = var && !nl && !p.var_f32 && options().rl_var_hot && p.full && p.fast_div && p.var128;
+        if (hot) {
+            // the common blocks by rl_var_hot_kernel, the rest listed for
+            // rl_var_rest_kernel (stream-ordered; the count read on the device)
+            const int64_t nblocks = (p.n + kRwOut - 1) / kRwOut;
+            int arc = dev_alloc((void**)&p.rest, (size_t)(nblocks + 1) * 4, s);
+            if (!arc && hipMemsetAsync(p.rest, 0, 4, s) != hipSuccess) arc = PLGPU_ERR_HIP;
+            if (arc) {
+                if (p.rest) dev_free(p.rest, s);
+                plgpu_column_release(out);
+                return arc == PLGPU_ERR_HIP ? hip_fail(hipGetLastError(), "rolling") : arc;
+            }
+            const bool st = options().rl_stream != 0;
+            const int per_cu = options().rl_grid > 0 ? options().rl_grid : 4;
+            const unsigned gs = (unsigned)std::max<int64_t>(1, std::min<int64_t>((int64_t)g, (int64_t)num_cus_rl() * per_cu));
+            const unsigned gr = (unsigned)std::max<int64_t>(1, std::min<int64_t>((int64_t)g, (int64_t)num_cus_rl()));
+#define PLGPU_RLHOT(DT)                                                      \
+    do {                                                                     \
+        if (st && p.var == 2) rl_var_hot_kernel<DT, true, true><<<gs, 64 * kRwWaves, 0, s>>>(p);    \
+        else if (st) rl_var_hot_kernel<DT, true, false><<<gs, 64 * kRwWaves, 0, s>>>(p);       \
+        else if (p.var == 2) rl_var_hot_kernel<DT, false, true><<<g, 64 * kRwWaves, 0, s>>>(p); \
+        else rl_var_hot_kernel<DT, false, false><<<g, 64 * kRwWaves, 0, s>>>(p);               \
+        rl_var_rest_kernel<DT><<<gr, 64 * kRwWaves, 0, s>>>(p);              \
+    } while (0)
+            if (values->dtype == PLGPU_F64) PLGPU_RLHOT(PLGPU_F64);
+            else if (values->dtype == PLGPU_I64) PLGPU_RLHOT(PLGPU_I64);
+            else PLGPU_RLHOT(PLGPU_I32);
+#undef PLGPU_RLHOT
+        } else if (!nl && options().rl_stream != 0) {
             // null-free: resident waves streaming their blocks
             const int per_cu = options().rl_grid > 0 ? options().rl_grid : 4;
             const unsigned gs = (unsigned)std::max<int64_t>(1, std::min<int64_t>((int64_t)g, (int64_t)num_cus_rl() * per_cu));
@@ -1599,6 +1749,7 @@ PLGPU_API int plgpu_rolling(const plgpu_column* values, int32_t kind, int64_t wi
         rl_direct_kernel<<<(unsigned)std::min<int64_t>((p.n + 255) / 256, 256 * 64), 256, 0, s>>>(p);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (p.rest) dev_free(p.rest, s);
     if (e != hipSuccess) {
         plgpu_column_release(out);
         return hip_fail(e, "rolling");

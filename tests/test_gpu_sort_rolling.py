@@ -494,3 +494,25 @@ def test_rolling_var_numerator_modulo_2_128(gpu, plgpu_option, var128, span):
     for w in (2, 20, 64):
         for ddof in (0, 1):
             _var_check(v, None, w, w, False, ddof, std=(ddof == 1))
+
+
+@pytest.mark.parametrize("hot", [1, 0])
+def test_rolling_var_common_block_kernel(gpu, plgpu_option, hot):
+    """Option rl_var_hot: interior finite blocks whose numerators fit 128 bits
+    run in rl_var_hot_kernel (std by the scaling-free square root), every
+    other block is listed for rl_var_rest_kernel.  Prices with one NaN block,
+    one 40-binade block and one block of values near 2^-380 (variances under
+    the square root's unscaled range) between common blocks; bit-exact
+    against the oracle with the option on and off."""
+    plgpu_option("rl_var_hot", hot)
+    rng = np.random.default_rng(70 + hot)
+    n = 512 * 24 + 333
+    v = rng.uniform(100, 150, n)
+    v[512 * 5 + 100] = np.nan
+    v[512 * 9:512 * 10] = rng.standard_normal(512) * np.exp2(rng.integers(-20, 20, 512))
+    v[512 * 14:512 * 15] = rng.uniform(1, 2, 512) * 2.0 ** -380
+    for w in (5, 20, 64):
+        for ddof in (0, 1):
+            for std in (False, True):
+                _var_check(v, None, w, w, False, ddof, std)
+                _var_check(v, None, w, 1, True, ddof, std)
