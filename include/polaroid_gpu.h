@@ -287,6 +287,8 @@ int plgpu_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream);
  *   "rl_var_hot"   1: rolling var / std run their common blocks (interior,
  *                  finite, 128-bit numerators) in a kernel of their own and
  *                  the other blocks from a device-side list afterwards
+ *   "rl_mean_hot"  1: the same split for rolling sum / mean (interior,
+ *                  finite blocks in the 64-bit form)
  *   "wave_report"  1: the slim fused kernels publish their diagnostics per
  *                  wave instead of once per workgroup
  *   "alloc_skew"   1: device blocks of 256 MiB and more start at rotating

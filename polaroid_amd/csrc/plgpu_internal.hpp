@@ -61,6 +61,7 @@ struct Options {
     int part_threads = 0; // partitioned aggregation: threads per workgroup (0: 1024; A/B)
     int rl_div = 1;       // rolling mean of full windows by one correction step instead of a division (A/B)
     int rl_full = 1;      // rolling sum / mean: interior int64-form waves by the specialised scan (A/B)
+    int rl_mean_hot = 1;  // rolling sum / mean: common blocks by a kernel of their own, the rest listed (A/B)
     int rl_var_hot = 1;   // rolling var / std: common blocks by a kernel of their own, the rest listed (A/B)
     int rl_var128 = 1;    // rolling var / std, interior waves: 128-bit modular numerators where they fit (A/B)
     int alloc_skew = 0;   // device pool: blocks >= 256 MiB at rotating 64 KiB offsets (A/B)

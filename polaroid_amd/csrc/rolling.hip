@@ -1275,6 +1275,62 @@ __device__ __forceinline__ bool rw_var_hot_block(const RlParams& p, uint64_t (&x
     return true;
 }
 
+// rolling sum / mean, the same split (option rl_mean_hot): an interior,
+// finite block in the int64 form (rw_block's conditions for rw_scan_full).
+template <int DT>
+__device__ __forceinline__ bool rw_mean_hot_block(const RlParams& p, uint64_t (&x)[kRwChunks + 1], int64_t o_first,
+                                                  int64_t s_first, uint64_t* ring, int lw, int64_t right) {
+    const int64_t o_end = o_first + kRwOut < p.n ? o_first + kRwOut : p.n;
+    if (!(o_first - (p.w - right) >= 0 && o_end + right - 1 <= p.n)) return false;
+    uint32_t mx = 0, inv_mn = 0;
+    bool odd = false;
+#pragma unroll
+    for (int k = 0; k <= kRwChunks; ++k) {
+        const int64_t r = s_first + 64 * k + (threadIdx.x & 63);
+        const uint64_t b = r >= p.n ? 0ull : DT == PLGPU_F64 ? x[k] : f64_bits((double)(int64_t)x[k]);
+        x[k] = b;
+        const uint32_t ex = (uint32_t)(b >> 52) & 0x7FF;
+        odd |= ex == 0x7FF;
+        if ((b << 1) != 0) {
+            const uint32_t e1 = ex ? ex : 1;
+            mx = e1 > mx ? e1 : mx;
+            inv_mn = 0x7FF - e1 > inv_mn ? 0x7FF - e1 : inv_mn;
+        }
+    }
+    if (__ballot(odd) != 0) return false;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint32_t a = __shfl_xor(mx, off, 64), c = __shfl_xor(inv_mn, off, 64);
+        mx = a > mx ? a : mx;
+        inv_mn = c > inv_mn ? c : inv_mn;
+    }
+    const int tmax = (int)mx, tmin = mx ? 0x7FF - (int)inv_mn : 1024;
+    const int span = tmax - tmin;
+    if (!(mx == 0 || (tmin >= 128 && lw + 53 + span <= 63))) return false;
+    const bool div1 = p.fast_div && tmin - 1075 >= -900 && tmax - 1022 + lw <= 990;
+    if (p.mean) rw_scan_full<true>(p, x, o_first, o_end, s_first, tmin, div1, ring);
+    else rw_scan_full<false>(p, x, o_first, o_end, s_first, tmin, div1, ring);
+    return true;
+}
+
+template <int DT>
+__global__ __launch_bounds__(256) void rl_mean_hot_kernel(RlParams p) {
+    __shared__ uint64_t ring[kRwWaves][kRwChunks * 64 + 64 + 1];  // rw_scan_full's prefixes
+    const int wv = threadIdx.x >> 6;
+    const int64_t nblocks = (p.n + kRwOut - 1) / kRwOut;
+    const int64_t b = (int64_t)blockIdx.x * kRwWaves + wv;
+    if (b >= nblocks) return;  // (no workgroup barriers below)
+    int lw = 0;
+    while ((int64_t(1) << lw) <= p.w) ++lw;  // p.w < 2^lw
+    const int64_t right = p.center ? (p.w + 1) / 2 : 1;
+    int64_t s_first, tmp;
+    rl_bounds(p, b * kRwOut, s_first, tmp);
+    uint64_t x[kRwChunks + 1];
+    rw_load_block<DT>(p, s_first, x);
+    if (!rw_mean_hot_block<DT>(p, x, b * kRwOut, s_first, ring[wv], lw, right) && (threadIdx.x & 63) == 0)
+        p.rest[1 + atomicAdd(&p.rest[0], 1u)] = (uint32_t)b;
+}
+
 template <int DT, bool STREAM, bool STD>
 __global__ __launch_bounds__(256) void rl_var_hot_kernel(RlParams p) {
     __shared__ uint64_t ring[kRwWaves][3 * kRwRing];
@@ -1312,11 +1368,11 @@ __global__ __launch_bounds__(256) void rl_var_hot_kernel(RlParams p) {
     }
 }
 
-// The blocks rl_var_hot_kernel left, one per wave, by rw_block.
-template <int DT>
+// The blocks rl_var_hot_kernel / rl_mean_hot_kernel left, one per wave, by rw_block.
+template <int DT, bool VAR = true>
 __global__ __launch_bounds__(256) void rl_var_rest_kernel(RlParams p) {
     __shared__ uint64_t ring[kRwWaves][3 * kRwRing];
-    __shared__ uint64_t ring_v2[kRwWaves][kRwRing];
+    __shared__ uint64_t ring_v2[VAR ? kRwWaves : 1][VAR ? kRwRing : 1];
     const int wv = threadIdx.x >> 6;
     const uint32_t cnt = __builtin_nontemporal_load(&p.rest[0]);
     for (uint32_t j = blockIdx.x * kRwWaves + wv; j < cnt; j += gridDim.x * kRwWaves) {
@@ -1325,8 +1381,8 @@ __global__ __launch_bounds__(256) void rl_var_rest_kernel(RlParams p) {
         rl_bounds(p, b * kRwOut, s_first, tmp);
         uint64_t x[kRwChunks + 1];
         rw_load_block<DT>(p, s_first, x);
-        rw_block<DT, false, true>(p, x, b * kRwOut, s_first, ring[wv], ring[wv] + kRwRing, ring[wv] + 2 * kRwRing,
-                                  ring_v2[wv]);
+        rw_block<DT, false, VAR>(p, x, b * kRwOut, s_first, ring[wv], ring[wv] + kRwRing, ring[wv] + 2 * kRwRing,
+                                 VAR ? ring_v2[wv] : nullptr);
     }
 }
 
@@ -1677,7 +1733,8 @@ PLGPU_API int plgpu_rolling(const plgpu_column* values, int32_t kind, int64_t wi
         const bool nl = p.c.validity != nullptr;
         KtScope kt(var ? "rl_wave_var_kernel" : "rl_wave_kernel", s);
         const bool hot = var && !nl && !p.var_f32 && options().rl_var_hot && p.full && p.fast_div && p.var128;
-        if (hot) {
+        const bool mhot = !var && !nl && !p.out_int && options().rl_mean_hot && p.full;
+        if (hot || mhot) {
             // the common blocks by rl_var_hot_kernel, the rest listed for
             // rl_var_rest_kernel (stream-ordered; the count read on the device)
             const int64_t nblocks = (p.n + kRwOut - 1) / kRwOut;
@@ -1694,6 +1751,11 @@ PLGPU_API int plgpu_rolling(const plgpu_column* values, int32_t kind, int64_t wi
             const unsigned gr = (unsigned)std::max<int64_t>(1, std::min<int64_t>((int64_t)g, (int64_t)num_cus_rl()));
 #define PLGPU_RLHOT(DT)                                                      \
     do {                                                                     \
+        if (mhot) {                                                          \
+            rl_mean_hot_kernel<DT><<<g, 64 * kRwWaves, 0, s>>>(p);           \
+            rl_var_rest_kernel<DT, false><<<gr, 64 * kRwWaves, 0, s>>>(p);   \
+            break;                                                           \
+        }                                                                    \
         if (st && p.var == 2) rl_var_hot_kernel<DT, true, true><<<gs, 64 * kRwWaves, 0, s>>>(p);    \
         else if (st) rl_var_hot_kernel<DT, true, false><<<gs, 64 * kRwWaves, 0, s>>>(p);       \
         else if (p.var == 2) rl_var_hot_kernel<DT, false, true><<<g, 64 * kRwWaves, 0, s>>>(p); \

@@ -64,6 +64,7 @@ const OptField kOptFields[] = {
     {"part_compact", "PLGPU_PART_COMPACT", &Options::part_compact},
     {"rl_var128", "PLGPU_RL_VAR128", &Options::rl_var128},
     {"rl_var_hot", "PLGPU_RL_VAR_HOT", &Options::rl_var_hot},
+    {"rl_mean_hot", "PLGPU_RL_MEAN_HOT", &Options::rl_mean_hot},
     {"alloc_skew", "PLGPU_ALLOC_SKEW", &Options::alloc_skew},
     {"alloc_contig", "PLGPU_ALLOC_CONTIG", &Options::alloc_contig},
     {"srt_w4", "PLGPU_SRT_W4", &Options::srt_w4},

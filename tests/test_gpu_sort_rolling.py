@@ -516,3 +516,33 @@ def test_rolling_var_common_block_kernel(gpu, plgpu_option, hot):
             for std in (False, True):
                 _var_check(v, None, w, w, False, ddof, std)
                 _var_check(v, None, w, 1, True, ddof, std)
+
+
+@pytest.mark.parametrize("hot", [1, 0])
+@pytest.mark.parametrize("kind", ["sum", "mean"])
+def test_rolling_common_block_kernel(gpu, plgpu_option, kind, hot):
+    """Option rl_mean_hot: interior finite blocks in the 64-bit form run in
+    rl_mean_hot_kernel, every other block is listed for the general kernel.
+    Prices with one NaN block, one 40-binade block (beyond 64 bits), one of
+    values near 2^-930 (below the 64-bit form) and one near 2^970 (sums near
+    the top of the one-correction quotient's range) between common blocks; Int64 and Int32 means enter as Float64.  Bit-exact against
+    the oracle's exact mode with the option on and off."""
+    plgpu_option("rl_mean_hot", hot)
+    rng = np.random.default_rng(90 + hot)
+    n = 512 * 24 + 333
+    v = rng.uniform(100, 150, n)
+    v[512 * 5 + 100] = np.nan
+    v[512 * 9:512 * 10] = rng.standard_normal(512) * np.exp2(rng.integers(-20, 20, 512))
+    v[512 * 14:512 * 15] = rng.uniform(1, 2, 512) * 2.0 ** -930
+    v[512 * 18:512 * 19] = rng.uniform(1, 2, 512) * 2.0 ** 970
+    for w in (1, 5, 20, 64):
+        _rolling_check(v, None, kind, w, w, False, ref_bound=False)
+        _rolling_check(v, None, kind, w, 1, True, ref_bound=False)
+    if kind == "mean":
+        for dt in (np.int64, np.int32):
+            iv = rng.integers(-10**6, 10**6, n).astype(dt)
+            s = pl.Series.from_numpy("x", iv, None)
+            out = s.rolling_mean(20, min_samples=20)
+            ev, eok = O.rolling(O.HostCol(iv.astype(np.float64), None), "mean", 20, 20, False, O.ROLLING_EXACT)
+            assert np.array_equal(out.validity_numpy(), eok)
+            assert np.array_equal(out.to_numpy()[eok].view(np.int64), ev[eok].view(np.int64))
